@@ -1,0 +1,737 @@
+// engine.hip — device state, hot-path kernels and the C ABI (include/gsim.h).
+//
+// The reference keeps one peerScore (score.go:64-86) and one GossipSubRouter
+// (gossipsub.go:420-477) per node, each a set of Go maps.  Here the whole
+// simulated network is one structure-of-arrays over a CSR peer graph: row i is
+// observer i's peerStats map, column j its neighbour, and every per-topic
+// topicStats field is a [T][E] topic-major array so that a wavefront walking
+// consecutive edges of one topic reads consecutive addresses.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gsim.h"
+#include "gsim_internal.h"
+#include "philox.h"
+
+using namespace gsim;
+
+// ---------------------------------------------------------------------------
+// Kernel 1: peerScore.refreshScores (score.go:504-565) fused with
+// peerScore.score (score.go:265-342).  One thread per observer->neighbour edge,
+// grid-stride; the topic loop reads the [T][E] arrays at t*E + e, so each
+// wave-instruction touches 64 consecutive records of one topic (coalesced).
+// Topic parameters are wave-uniform (scalar loads).  Operation order is the
+// reference's, compiled with -ffp-contract=off: results are bit-identical to
+// the CPU oracle.
+template <bool REFRESH, bool SCORE>
+__global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
+        const uint8_t st = a.estate[e];
+        if (!(st & GSIM_ES_TRACKED)) {
+            if (SCORE) a.score[e] = 0.0;
+            continue;
+        }
+        const bool conn = (st & GSIM_ES_CONNECTED) != 0;
+        if (REFRESH && !conn && a.now > a.expire[e]) {
+            // retention elapsed: delete(ps.peerStats, p) (score.go:512-516)
+            a.estate[e] = 0;
+            a.bp[e] = 0.0;
+            a.expire[e] = 0;
+            for (int32_t t = 0; t < a.T; ++t) {
+                const int64_t i = (int64_t)t * a.E + e;
+                a.first[i] = 0.0; a.meshd[i] = 0.0; a.fail[i] = 0.0; a.invalid[i] = 0.0;
+                a.graft[i] = 0; a.mtime[i] = 0; a.tflags[i] = 0;
+            }
+            *a.purged = 1;
+            if (SCORE) a.score[e] = 0.0;
+            continue;
+        }
+        const bool decay = REFRESH && conn;   // retained scores are not decayed
+        double score = 0.0;
+        for (int32_t t = 0; t < a.T; ++t) {
+            const gsim_topic_score_params* tp = &a.tp[t];
+            if (!tp->scored) continue;
+            const int64_t i = (int64_t)t * a.E + e;
+            double first = a.first[i], meshd = a.meshd[i], fail = a.fail[i], inval = a.invalid[i];
+            uint8_t fl = a.tflags[i];
+            int64_t mt = 0;
+            if (decay) {
+                double x;
+                x = first * tp->first_message_deliveries_decay;  if (x < a.dtz) x = 0.0;
+                if (x != first) { first = x; a.first[i] = x; }
+                x = meshd * tp->mesh_message_deliveries_decay;   if (x < a.dtz) x = 0.0;
+                if (x != meshd) { meshd = x; a.meshd[i] = x; }
+                x = fail * tp->mesh_failure_penalty_decay;       if (x < a.dtz) x = 0.0;
+                if (x != fail) { fail = x; a.fail[i] = x; }
+                x = inval * tp->invalid_message_deliveries_decay; if (x < a.dtz) x = 0.0;
+                if (x != inval) { inval = x; a.invalid[i] = x; }
+                if (fl & GSIM_TF_IN_MESH) {
+                    mt = a.now - a.graft[i];
+                    a.mtime[i] = mt;
+                    if (mt > tp->mesh_message_deliveries_activation_ns && !(fl & GSIM_TF_ACTIVE)) {
+                        fl |= GSIM_TF_ACTIVE;
+                        a.tflags[i] = fl;
+                    }
+                }
+            } else if (SCORE && (fl & GSIM_TF_IN_MESH)) {
+                mt = a.mtime[i];
+            }
+            if (SCORE) {
+                double ts = 0.0;
+                if (fl & GSIM_TF_IN_MESH) {                               // P1
+                    double p1 = 0.0;
+                    if (tp->time_in_mesh_quantum_ns != 0) p1 = (double)(mt / tp->time_in_mesh_quantum_ns);
+                    if (p1 > tp->time_in_mesh_cap) p1 = tp->time_in_mesh_cap;
+                    ts += p1 * tp->time_in_mesh_weight;
+                }
+                ts += first * tp->first_message_deliveries_weight;         // P2
+                if (fl & GSIM_TF_ACTIVE) {                                 // P3
+                    if (meshd < tp->mesh_message_deliveries_threshold) {
+                        const double deficit = tp->mesh_message_deliveries_threshold - meshd;
+                        const double p3 = deficit * deficit;
+                        ts += p3 * tp->mesh_message_deliveries_weight;
+                    }
+                }
+                ts += fail * tp->mesh_failure_penalty_weight;              // P3b
+                const double p4 = inval * inval;                           // P4
+                ts += p4 * tp->invalid_message_deliveries_weight;
+                score += ts * tp->topic_weight;
+            }
+        }
+        double bp = a.bp[e];
+        if (decay) {
+            double x = bp * a.bp_decay;
+            if (x < a.dtz) x = 0.0;
+            if (x != bp) { bp = x; a.bp[e] = x; }
+        }
+        if (SCORE) {
+            if (a.topic_cap > 0 && score > a.topic_cap) score = a.topic_cap;
+            const double p5 = a.p5[a.col[e]];                              // P5
+            score += p5 * a.w5;
+            score += a.p6[e] * a.w6;                                       // P6
+            if (bp > a.bp_thr) {                                           // P7
+                const double excess = bp - a.bp_thr;
+                const double p7 = excess * excess;
+                score += p7 * a.w7;
+            }
+            a.score[e] = score;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 2: ipColocationFactor (score.go:344-388) as a segmented count over
+// each observer's row keyed by IP id.  Only re-run when the tracked set or the
+// IP assignment changes (AddPeer/RemovePeer/purge), not every heartbeat.
+// Thread per edge; the row scan hits L1/L2 (rows are k ~ 32).
+__global__ __launch_bounds__(256) void k_ip_colocation(ColocArgs a)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
+        double res = 0.0;
+        if (a.estate[e] & GSIM_ES_TRACKED) {
+            const uint32_t i = a.owner[e];
+            const uint32_t b = a.row_ptr[i], en = a.row_ptr[i + 1];
+            const uint32_t j = a.col[e];
+            for (uint32_t q = a.ip_ptr[j]; q < a.ip_ptr[j + 1]; ++q) {
+                const uint32_t ip = a.ip_ids[q];
+                if (a.ip_white && a.ip_white[ip]) continue;
+                int32_t cnt = 0;
+                for (uint32_t e2 = b; e2 < en; ++e2) {
+                    if (!(a.estate[e2] & GSIM_ES_TRACKED)) continue;
+                    const uint32_t j2 = a.col[e2];
+                    for (uint32_t q2 = a.ip_ptr[j2]; q2 < a.ip_ptr[j2 + 1]; ++q2)
+                        if (a.ip_ids[q2] == ip) { ++cnt; break; }
+                }
+                if (cnt > a.thr) {
+                    const double surplus = (double)(cnt - a.thr);
+                    res += surplus * surplus;
+                }
+            }
+        }
+        a.p6[e] = res;
+    }
+}
+
+// SetTopicScoreParams recap (score.go:224-238).
+__global__ __launch_bounds__(256) void k_recap(int64_t E, const uint8_t* estate, double* first, double* meshd,
+                                               double first_cap, double mesh_cap, int do_first, int do_mesh)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride) {
+        if (!(estate[e] & GSIM_ES_TRACKED)) continue;
+        if (do_first && first[e] > first_cap) first[e] = first_cap;
+        if (do_mesh && meshd[e] > mesh_cap) meshd[e] = mesh_cap;
+    }
+}
+
+// Seeded synthetic steady-state-like counters for benchmarking at full size
+// (SURVEY.md §8(d)): a Philox draw per edge-topic record decides mesh
+// membership (probability D/k), activation, graft time and the four counters.
+__global__ __launch_bounds__(256) void k_fill_synthetic(ScoreArgs a, uint64_t seed, double p_mesh)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const double inv = 1.0 / 4294967296.0;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
+        for (int32_t t = 0; t < a.T; ++t) {
+            const int64_t i = (int64_t)t * a.E + e;
+            const u32x4 r = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), 0x5eed, 1, k0, k1);
+            const u32x4 q = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), 0x5eed, 2, k0, k1);
+            const bool in_mesh = r.x * inv < p_mesh;
+            uint8_t fl = in_mesh ? GSIM_TF_IN_MESH : 0;
+            if (in_mesh && (r.y & 15) != 0) fl |= GSIM_TF_ACTIVE;
+            a.tflags[i] = fl;
+            a.graft[i] = in_mesh ? a.now - (int64_t)(r.z % 3600u) * 1000000000LL : 0;
+            a.mtime[i] = in_mesh ? a.now - a.graft[i] : 0;
+            a.first[i] = (double)(q.x % 2000u) * 0.25;
+            a.meshd[i] = in_mesh ? (double)(q.y % 1600u) * 0.25 : 0.0;
+            a.fail[i] = (q.z & 7) == 0 ? (double)(q.z % 4000u) * 0.125 : 0.0;
+            a.invalid[i] = (q.w & 31) == 0 ? (double)(q.w % 64u) * 0.125 : 0.0;
+        }
+        const u32x4 b = philox4x32_10((uint32_t)e, (uint32_t)(e >> 32), 0x5eed, 3, k0, k1);
+        a.bp[e] = (b.x & 3) == 0 ? (double)(b.y % 200u) * 0.125 : 0.0;
+        a.estate[e] = GSIM_ES_TRACKED | GSIM_ES_CONNECTED;
+        a.expire[e] = 0;
+    }
+}
+
+__global__ void k_fill_u8(uint8_t* p, int64_t n, uint8_t v)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+
+// ---------------------------------------------------------------------------
+// host side
+
+namespace {
+
+int grid_for(int64_t n, int block = 256, int cap = 16384)
+{
+    int64_t g = (n + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+template <typename T>
+int dalloc(gsim_handle* h, T** p, int64_t n)
+{
+    *p = nullptr;
+    if (n <= 0) n = 1;
+    hipError_t e = hipMalloc((void**)p, sizeof(T) * (size_t)n);
+    if (e != hipSuccess) {
+        h->err = std::string("hipMalloc failed: ") + hipGetErrorString(e);
+        return GSIM_ENOMEM;
+    }
+    h->bytes_allocated += sizeof(T) * (size_t)n;
+    return GSIM_OK;
+}
+
+template <typename T>
+void dfree(T*& p)
+{
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+}  // namespace
+
+int hip_check(gsim_handle* h, hipError_t e, const char* what)
+{
+    if (e == hipSuccess) return GSIM_OK;
+    h->err = std::string(what) + ": " + hipGetErrorString(e);
+    return GSIM_EDEVICE;
+}
+
+void free_graph(gsim_handle* h)
+{
+    dfree(h->d_row_ptr); dfree(h->d_col); dfree(h->d_rev); dfree(h->d_owner);
+    dfree(h->d_sub); dfree(h->d_outbound);
+    dfree(h->d_ip_ptr); dfree(h->d_ip_ids); dfree(h->d_ip_white); dfree(h->d_p5);
+    dfree(h->d_first); dfree(h->d_meshd); dfree(h->d_fail); dfree(h->d_invalid);
+    dfree(h->d_graft); dfree(h->d_mtime); dfree(h->d_tflags);
+    dfree(h->d_bp); dfree(h->d_estate); dfree(h->d_expire); dfree(h->d_p6); dfree(h->d_score);
+    dfree(h->d_backoff);
+    h->bytes_allocated = 0;
+    h->n = h->e = 0;
+}
+
+static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
+{
+    ScoreArgs a{};
+    a.E = h->e;
+    a.T = h->t;
+    a.tp = h->d_tp;
+    a.dtz = h->pp.decay_to_zero;
+    a.bp_decay = h->pp.behaviour_penalty_decay;
+    a.topic_cap = h->pp.topic_score_cap;
+    a.w5 = h->pp.app_specific_weight;
+    a.w6 = h->pp.ip_colocation_factor_weight;
+    a.bp_thr = h->pp.behaviour_penalty_threshold;
+    a.w7 = h->pp.behaviour_penalty_weight;
+    a.col = h->d_col;
+    a.p5 = h->d_p5;
+    a.first = h->d_first; a.meshd = h->d_meshd; a.fail = h->d_fail; a.invalid = h->d_invalid;
+    a.graft = h->d_graft; a.mtime = h->d_mtime; a.tflags = h->d_tflags;
+    a.bp = h->d_bp; a.estate = h->d_estate; a.expire = h->d_expire; a.p6 = h->d_p6; a.score = h->d_score;
+    a.now = now;
+    a.purged = h->d_flags;
+    return a;
+}
+
+int launch_ip_colocation(gsim_handle* h)
+{
+    ColocArgs c{};
+    c.E = h->e; c.row_ptr = h->d_row_ptr; c.col = h->d_col; c.owner = h->d_owner;
+    c.ip_ptr = h->d_ip_ptr; c.ip_ids = h->d_ip_ids; c.ip_white = h->has_white ? h->d_ip_white : nullptr;
+    c.estate = h->d_estate; c.p6 = h->d_p6; c.thr = h->pp.ip_colocation_factor_threshold;
+    hipLaunchKernelGGL(k_ip_colocation, dim3(grid_for(h->e)), dim3(256), 0, h->stream, c);
+    h->p6_dirty = false;
+    return hip_check(h, hipGetLastError(), "k_ip_colocation");
+}
+
+int launch_refresh_scores(gsim_handle* h, int64_t now)
+{
+    ScoreArgs a = make_score_args(h, now);
+    const dim3 g(grid_for(h->e)), b(256);
+    if (h->p6_dirty) {
+        int rc = launch_ip_colocation(h);
+        if (rc) return rc;
+    }
+    if (h->maybe_retained) {
+        // a purge inside refresh changes the tracked set, so P6 must be
+        // re-derived between decay and scoring (score.go:514 removeIPs).
+        hipLaunchKernelGGL((k_refresh_score<true, false>), g, b, 0, h->stream, a);
+        int rc = launch_ip_colocation(h);
+        if (rc) return rc;
+        hipLaunchKernelGGL((k_refresh_score<false, true>), g, b, 0, h->stream, a);
+    } else {
+        hipLaunchKernelGGL((k_refresh_score<true, true>), g, b, 0, h->stream, a);
+    }
+    return hip_check(h, hipGetLastError(), "k_refresh_score");
+}
+
+int launch_compute_scores(gsim_handle* h)
+{
+    if (h->p6_dirty) {
+        int rc = launch_ip_colocation(h);
+        if (rc) return rc;
+    }
+    ScoreArgs a = make_score_args(h, 0);
+    hipLaunchKernelGGL((k_refresh_score<false, true>), dim3(grid_for(h->e)), dim3(256), 0, h->stream, a);
+    return hip_check(h, hipGetLastError(), "k_refresh_score<score>");
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+
+#define GSIM_ENTER(h)                                                     \
+    do {                                                                  \
+        if (!(h)) return GSIM_EINVAL;                                     \
+        hipError_t _e = hipSetDevice((h)->device);                        \
+        if (_e != hipSuccess) return hip_check((h), _e, "hipSetDevice");  \
+    } while (0)
+
+#define GSIM_NEED_GRAPH(h)                                                \
+    do {                                                                  \
+        if ((h)->e == 0 && (h)->n == 0) {                                 \
+            (h)->err = "no graph loaded (call gsim_load_graph first)";    \
+            return GSIM_ESTATE;                                           \
+        }                                                                 \
+    } while (0)
+
+extern "C" {
+
+static int create_impl(const gsim_peer_score_params* params, const gsim_topic_score_params* topics,
+                       int32_t n_topics, const gsim_thresholds* thresholds, const gsim_gossipsub_params* gossip,
+                       int32_t device, gsim_handle** out, char* err, size_t errlen, bool validate)
+{
+    if (!out) return GSIM_EINVAL;
+    *out = nullptr;
+    auto fail = [&](int rc, const std::string& m) {
+        if (err && errlen) std::snprintf(err, errlen, "%s", m.c_str());
+        return rc;
+    };
+    if (!params || !thresholds || !gossip || (n_topics > 0 && !topics))
+        return fail(GSIM_EINVAL, "null parameter block");
+    if (n_topics < 0 || n_topics > GSIM_MAX_TOPICS) return fail(GSIM_ERANGE, "n_topics must be in [0, 64]");
+    char buf[512] = {0};
+    if (validate && gsim_validate_peer_params(params, topics, n_topics, buf, sizeof buf))
+        return fail(GSIM_EINVAL, buf);
+    if (validate && gsim_validate_thresholds(thresholds, buf, sizeof buf)) return fail(GSIM_EINVAL, buf);
+    if (gossip->history_gossip > gossip->history_length) {
+        std::snprintf(buf, sizeof buf,
+                      "invalid parameters for message cache; gossip slots (%d) cannot be larger than history slots (%d)",
+                      gossip->history_gossip, gossip->history_length);
+        return fail(GSIM_EINVAL, buf);
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(GSIM_EDEVICE, "no HIP device available (the engine has no CPU fallback)");
+    if (device < 0 || device >= ndev) return fail(GSIM_EINVAL, "device ordinal out of range");
+    if (hipSetDevice(device) != hipSuccess) return fail(GSIM_EDEVICE, "hipSetDevice failed");
+
+    gsim_handle* h = new gsim_handle();
+    h->device = device;
+    h->validate = validate;
+    h->pp = *params;
+    h->th = *thresholds;
+    h->gp = *gossip;
+    h->tp.assign(topics, topics + n_topics);
+    h->t = n_topics;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return fail(GSIM_EDEVICE, "hipStreamCreate failed");
+    }
+    for (auto& ev : h->ev) (void)hipEventCreate(&ev);
+    if (dalloc(h, &h->d_tp, std::max(1, n_topics)) || dalloc(h, &h->d_flags, 16)) {
+        std::string m = h->err;
+        gsim_destroy(h);
+        return fail(GSIM_ENOMEM, m);
+    }
+    if (n_topics > 0)
+        (void)hipMemcpy(h->d_tp, topics, sizeof(gsim_topic_score_params) * (size_t)n_topics, hipMemcpyHostToDevice);
+    (void)hipMemset(h->d_flags, 0, 16 * sizeof(int32_t));
+    *out = h;
+    return GSIM_OK;
+}
+
+int gsim_create(const gsim_peer_score_params* params, const gsim_topic_score_params* topics, int32_t n_topics,
+                const gsim_thresholds* thresholds, const gsim_gossipsub_params* gossip, int32_t device,
+                gsim_handle** out, char* err, size_t errlen)
+{
+    return create_impl(params, topics, n_topics, thresholds, gossip, device, out, err, errlen, true);
+}
+
+int gsim_create_unvalidated(const gsim_peer_score_params* params, const gsim_topic_score_params* topics,
+                            int32_t n_topics, const gsim_thresholds* thresholds,
+                            const gsim_gossipsub_params* gossip, int32_t device, gsim_handle** out, char* err,
+                            size_t errlen)
+{
+    return create_impl(params, topics, n_topics, thresholds, gossip, device, out, err, errlen, false);
+}
+
+int gsim_destroy(gsim_handle* h)
+{
+    if (!h) return GSIM_OK;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    free_graph(h);
+    free_extra(h);
+    dfree(h->d_tp);
+    dfree(h->d_flags);
+    for (auto& ev : h->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return GSIM_OK;
+}
+
+const char* gsim_last_error(const gsim_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const uint32_t* col,
+                    const uint8_t* outbound, const uint64_t* subs, const uint32_t* ip_ptr, const uint32_t* ip_ids,
+                    uint32_t n_ips)
+{
+    GSIM_ENTER(h);
+    if (n <= 0 || !row_ptr || !col) { h->err = "empty graph"; return GSIM_EINVAL; }
+    if (n >= (int64_t)UINT32_MAX) { h->err = "too many peers"; return GSIM_ERANGE; }
+    const int64_t E = row_ptr[n];
+    if (row_ptr[0] != 0) { h->err = "row_ptr[0] must be 0"; return GSIM_EINVAL; }
+    // validate the CSR and derive reverse edges / owners on the host
+    std::vector<uint32_t> rev((size_t)E), owner((size_t)E);
+    for (int64_t i = 0; i < n; ++i) {
+        if (row_ptr[i + 1] < row_ptr[i]) { h->err = "row_ptr not monotone"; return GSIM_EINVAL; }
+        for (uint32_t e = row_ptr[i]; e < row_ptr[i + 1]; ++e) {
+            owner[e] = (uint32_t)i;
+            if (col[e] >= (uint64_t)n) { h->err = "col index out of range"; return GSIM_EINVAL; }
+            if (col[e] == (uint32_t)i) { h->err = "self loop"; return GSIM_EINVAL; }
+            if (e > row_ptr[i] && col[e] <= col[e - 1]) { h->err = "rows must be sorted, no duplicates"; return GSIM_EINVAL; }
+        }
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        for (uint32_t e = row_ptr[i]; e < row_ptr[i + 1]; ++e) {
+            const uint32_t j = col[e];
+            const uint32_t* b = col + row_ptr[j];
+            const uint32_t* en = col + row_ptr[j + 1];
+            const uint32_t* p = std::lower_bound(b, en, (uint32_t)i);
+            if (p == en || *p != (uint32_t)i) { h->err = "graph is not symmetric"; return GSIM_EINVAL; }
+            rev[e] = (uint32_t)(p - col);
+        }
+    }
+    if (ip_ptr) {
+        if (ip_ptr[0] != 0) { h->err = "ip_ptr[0] must be 0"; return GSIM_EINVAL; }
+        for (int64_t i = 0; i < n; ++i)
+            if (ip_ptr[i + 1] < ip_ptr[i]) { h->err = "ip_ptr not monotone"; return GSIM_EINVAL; }
+        for (uint32_t q = 0; q < ip_ptr[n]; ++q)
+            if (ip_ids[q] >= n_ips) { h->err = "ip id out of range"; return GSIM_EINVAL; }
+    }
+    if (subs && h->t < 64) {
+        const uint64_t mask = h->t == 0 ? 0 : ((1ull << h->t) - 1);
+        for (int64_t i = 0; i < n; ++i)
+            if (subs[i] & ~mask) { h->err = "subscription bit beyond n_topics"; return GSIM_EINVAL; }
+    }
+
+    (void)hipStreamSynchronize(h->stream);
+    free_graph(h);
+    free_extra(h);
+    h->n = n;
+    h->e = E;
+    h->n_ips = n_ips;
+    const int64_t ET = E * (int64_t)std::max(1, h->t);
+    const int64_t nip = ip_ptr ? ip_ptr[n] : 0;
+    int rc = GSIM_OK;
+    rc = rc ? rc : dalloc(h, &h->d_row_ptr, n + 1);
+    rc = rc ? rc : dalloc(h, &h->d_col, E);
+    rc = rc ? rc : dalloc(h, &h->d_rev, E);
+    rc = rc ? rc : dalloc(h, &h->d_owner, E);
+    rc = rc ? rc : dalloc(h, &h->d_sub, n);
+    rc = rc ? rc : dalloc(h, &h->d_outbound, E);
+    rc = rc ? rc : dalloc(h, &h->d_ip_ptr, n + 1);
+    rc = rc ? rc : dalloc(h, &h->d_ip_ids, nip);
+    rc = rc ? rc : dalloc(h, &h->d_ip_white, (int64_t)n_ips);
+    rc = rc ? rc : dalloc(h, &h->d_p5, n);
+    rc = rc ? rc : dalloc(h, &h->d_first, ET);
+    rc = rc ? rc : dalloc(h, &h->d_meshd, ET);
+    rc = rc ? rc : dalloc(h, &h->d_fail, ET);
+    rc = rc ? rc : dalloc(h, &h->d_invalid, ET);
+    rc = rc ? rc : dalloc(h, &h->d_graft, ET);
+    rc = rc ? rc : dalloc(h, &h->d_mtime, ET);
+    rc = rc ? rc : dalloc(h, &h->d_tflags, ET);
+    rc = rc ? rc : dalloc(h, &h->d_backoff, ET);
+    rc = rc ? rc : dalloc(h, &h->d_bp, E);
+    rc = rc ? rc : dalloc(h, &h->d_estate, E);
+    rc = rc ? rc : dalloc(h, &h->d_expire, E);
+    rc = rc ? rc : dalloc(h, &h->d_p6, E);
+    rc = rc ? rc : dalloc(h, &h->d_score, E);
+    if (rc) { std::string m = h->err; free_graph(h); h->err = m; return rc; }
+
+    hipStream_t s = h->stream;
+    hipError_t he = hipSuccess;
+    auto up = [&](void* d, const void* src, size_t bytes) {
+        if (he == hipSuccess && bytes) he = hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, s);
+    };
+    auto zero = [&](void* d, size_t bytes) {
+        if (he == hipSuccess && bytes) he = hipMemsetAsync(d, 0, bytes, s);
+    };
+    up(h->d_row_ptr, row_ptr, sizeof(uint32_t) * (size_t)(n + 1));
+    up(h->d_col, col, sizeof(uint32_t) * (size_t)E);
+    up(h->d_rev, rev.data(), sizeof(uint32_t) * (size_t)E);
+    up(h->d_owner, owner.data(), sizeof(uint32_t) * (size_t)E);
+    if (subs) up(h->d_sub, subs, sizeof(uint64_t) * (size_t)n); else zero(h->d_sub, sizeof(uint64_t) * (size_t)n);
+    if (outbound) up(h->d_outbound, outbound, (size_t)E); else zero(h->d_outbound, (size_t)E);
+    if (ip_ptr) {
+        up(h->d_ip_ptr, ip_ptr, sizeof(uint32_t) * (size_t)(n + 1));
+        up(h->d_ip_ids, ip_ids, sizeof(uint32_t) * (size_t)nip);
+    } else {
+        zero(h->d_ip_ptr, sizeof(uint32_t) * (size_t)(n + 1));
+    }
+    zero(h->d_ip_white, (size_t)std::max<uint32_t>(n_ips, 1));
+    zero(h->d_p5, sizeof(double) * (size_t)n);
+    zero(h->d_first, sizeof(double) * (size_t)ET);
+    zero(h->d_meshd, sizeof(double) * (size_t)ET);
+    zero(h->d_fail, sizeof(double) * (size_t)ET);
+    zero(h->d_invalid, sizeof(double) * (size_t)ET);
+    zero(h->d_graft, sizeof(int64_t) * (size_t)ET);
+    zero(h->d_mtime, sizeof(int64_t) * (size_t)ET);
+    zero(h->d_tflags, (size_t)ET);
+    zero(h->d_backoff, sizeof(int64_t) * (size_t)ET);
+    zero(h->d_bp, sizeof(double) * (size_t)E);
+    zero(h->d_expire, sizeof(int64_t) * (size_t)E);
+    zero(h->d_p6, sizeof(double) * (size_t)E);
+    zero(h->d_score, sizeof(double) * (size_t)E);
+    if (he != hipSuccess) return hip_check(h, he, "graph upload");
+    // AddPeer for every connection (score.go:595-609): tracked + connected
+    hipLaunchKernelGGL(k_fill_u8, dim3(grid_for(E)), dim3(256), 0, s, h->d_estate, E,
+                       (uint8_t)(GSIM_ES_TRACKED | GSIM_ES_CONNECTED));
+    h->has_white = false;
+    h->p6_dirty = true;
+    h->maybe_retained = false;
+    int rc2 = alloc_extra(h);
+    if (rc2) return rc2;
+    he = hipStreamSynchronize(s);
+    return hip_check(h, he, "gsim_load_graph");
+}
+
+int gsim_set_app_score(gsim_handle* h, const double* p5)
+{
+    GSIM_ENTER(h);
+    GSIM_NEED_GRAPH(h);
+    if (!p5) return GSIM_EINVAL;
+    hipError_t e = hipMemcpyAsync(h->d_p5, p5, sizeof(double) * (size_t)h->n, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    return hip_check(h, e, "gsim_set_app_score");
+}
+
+int gsim_set_ip_whitelist(gsim_handle* h, const uint8_t* white)
+{
+    GSIM_ENTER(h);
+    GSIM_NEED_GRAPH(h);
+    hipError_t e = hipSuccess;
+    if (white && h->n_ips) {
+        e = hipMemcpyAsync(h->d_ip_white, white, (size_t)h->n_ips, hipMemcpyHostToDevice, h->stream);
+        h->has_white = true;
+    } else {
+        h->has_white = false;
+    }
+    h->p6_dirty = true;
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    return hip_check(h, e, "gsim_set_ip_whitelist");
+}
+
+int gsim_set_topic_params(gsim_handle* h, int32_t t, const gsim_topic_score_params* p)
+{
+    GSIM_ENTER(h);
+    if (!p || t < 0 || t >= h->t) { h->err = "topic index out of range"; return GSIM_EINVAL; }
+    char buf[256] = {0};
+    if (h->validate && p->scored && gsim_validate_topic_params(p, buf, sizeof buf)) { h->err = buf; return GSIM_EINVAL; }
+    const gsim_topic_score_params old = h->tp[t];
+    h->tp[t] = *p;
+    hipError_t e = hipMemcpyAsync(h->d_tp + t, p, sizeof(*p), hipMemcpyHostToDevice, h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "gsim_set_topic_params");
+    if (old.scored && h->e > 0) {
+        const int df = p->first_message_deliveries_cap < old.first_message_deliveries_cap;
+        const int dm = p->mesh_message_deliveries_cap < old.mesh_message_deliveries_cap;
+        if (df || dm) {
+            const int64_t off = (int64_t)t * h->e;
+            hipLaunchKernelGGL(k_recap, dim3(grid_for(h->e)), dim3(256), 0, h->stream, h->e, h->d_estate,
+                               h->d_first + off, h->d_meshd + off, p->first_message_deliveries_cap,
+                               p->mesh_message_deliveries_cap, df, dm);
+            e = hipGetLastError();
+        }
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    return hip_check(h, e, "gsim_set_topic_params");
+}
+
+int gsim_refresh_scores(gsim_handle* h, int64_t now)
+{
+    GSIM_ENTER(h);
+    GSIM_NEED_GRAPH(h);
+    return launch_refresh_scores(h, now);
+}
+
+int gsim_compute_scores(gsim_handle* h)
+{
+    GSIM_ENTER(h);
+    GSIM_NEED_GRAPH(h);
+    return launch_compute_scores(h);
+}
+
+int gsim_compute_ip_colocation(gsim_handle* h)
+{
+    GSIM_ENTER(h);
+    GSIM_NEED_GRAPH(h);
+    return launch_ip_colocation(h);
+}
+
+int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now, double p_mesh)
+{
+    GSIM_ENTER(h);
+    GSIM_NEED_GRAPH(h);
+    ScoreArgs a = make_score_args(h, now);
+    hipLaunchKernelGGL(k_fill_synthetic, dim3(grid_for(h->e)), dim3(256), 0, h->stream, a, seed, p_mesh);
+    h->p6_dirty = true;
+    h->maybe_retained = false;
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    return hip_check(h, e, "gsim_fill_synthetic");
+}
+
+int gsim_read_scores(gsim_handle* h, double* out)
+{
+    GSIM_ENTER(h);
+    GSIM_NEED_GRAPH(h);
+    if (!out) return GSIM_EINVAL;
+    hipError_t e = hipMemcpyAsync(out, h->d_score, sizeof(double) * (size_t)h->e, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    return hip_check(h, e, "gsim_read_scores");
+}
+
+int gsim_field_bytes(gsim_handle* h, int32_t f, size_t* out)
+{
+    if (!h || !out) return GSIM_EINVAL;
+    FieldRef r;
+    if (!field_ref(h, f, &r)) { h->err = "unknown field"; return GSIM_EINVAL; }
+    *out = r.bytes;
+    return GSIM_OK;
+}
+
+int gsim_read_field(gsim_handle* h, int32_t f, void* dst, size_t bytes)
+{
+    GSIM_ENTER(h);
+    GSIM_NEED_GRAPH(h);
+    FieldRef r;
+    if (!field_ref(h, f, &r)) { h->err = "unknown field"; return GSIM_EINVAL; }
+    if (bytes != r.bytes || !dst) { h->err = "field size mismatch"; return GSIM_EINVAL; }
+    hipError_t e = hipMemcpyAsync(dst, r.ptr, bytes, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    return hip_check(h, e, "gsim_read_field");
+}
+
+int gsim_write_field(gsim_handle* h, int32_t f, const void* src, size_t bytes)
+{
+    GSIM_ENTER(h);
+    GSIM_NEED_GRAPH(h);
+    FieldRef r;
+    if (!field_ref(h, f, &r)) { h->err = "unknown field"; return GSIM_EINVAL; }
+    if (bytes != r.bytes || !src) { h->err = "field size mismatch"; return GSIM_EINVAL; }
+    hipError_t e = hipMemcpyAsync(r.ptr, src, bytes, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (f == GSIM_F_ESTATE) { h->p6_dirty = true; h->maybe_retained = true; }
+    return hip_check(h, e, "gsim_write_field");
+}
+
+int gsim_event_record(gsim_handle* h, int32_t slot)
+{
+    GSIM_ENTER(h);
+    if (slot < 0 || slot >= kEvents) return GSIM_EINVAL;
+    return hip_check(h, hipEventRecord(h->ev[slot], h->stream), "hipEventRecord");
+}
+
+int gsim_event_elapsed(gsim_handle* h, int32_t from, int32_t to, float* ms)
+{
+    GSIM_ENTER(h);
+    if (from < 0 || from >= kEvents || to < 0 || to >= kEvents || !ms) return GSIM_EINVAL;
+    hipError_t e = hipEventSynchronize(h->ev[to]);
+    if (e == hipSuccess) e = hipEventElapsedTime(ms, h->ev[from], h->ev[to]);
+    return hip_check(h, e, "hipEventElapsedTime");
+}
+
+int gsim_synchronize(gsim_handle* h)
+{
+    GSIM_ENTER(h);
+    return hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+}
+
+}  // extern "C"
+
+bool field_ref(gsim_handle* h, int32_t f, FieldRef* r)
+{
+    const size_t E = (size_t)h->e, ET = E * (size_t)std::max(1, h->t);
+    switch (f) {
+    case GSIM_F_FIRST:      *r = {h->d_first, ET * 8}; return true;
+    case GSIM_F_MESHD:      *r = {h->d_meshd, ET * 8}; return true;
+    case GSIM_F_FAIL:       *r = {h->d_fail, ET * 8}; return true;
+    case GSIM_F_INVALID:    *r = {h->d_invalid, ET * 8}; return true;
+    case GSIM_F_GRAFT_TIME: *r = {h->d_graft, ET * 8}; return true;
+    case GSIM_F_MESH_TIME:  *r = {h->d_mtime, ET * 8}; return true;
+    case GSIM_F_TFLAGS:     *r = {h->d_tflags, ET}; return true;
+    case GSIM_F_BP:         *r = {h->d_bp, E * 8}; return true;
+    case GSIM_F_ESTATE:     *r = {h->d_estate, E}; return true;
+    case GSIM_F_EXPIRE:     *r = {h->d_expire, E * 8}; return true;
+    case GSIM_F_P6:         *r = {h->d_p6, E * 8}; return true;
+    case GSIM_F_SCORE:      *r = {h->d_score, E * 8}; return true;
+    case GSIM_F_BACKOFF:    *r = {h->d_backoff, ET * 8}; return true;
+    default: return extra_field_ref(h, f, r);
+    }
+}

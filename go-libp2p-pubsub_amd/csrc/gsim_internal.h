@@ -1,0 +1,109 @@
+// gsim_internal.h — engine handle and kernel argument blocks (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "gsim.h"
+
+namespace gsim {
+
+constexpr int GSIM_MAX_TOPICS = 64;   // subscriptions are a u64 bitmask
+constexpr int kEvents = 16;
+
+struct ScoreArgs {
+    int64_t E;
+    int32_t T;
+    const gsim_topic_score_params* tp;
+    double dtz, bp_decay, topic_cap, w5, w6, bp_thr, w7;
+    const uint32_t* col;
+    const double* p5;
+    double *first, *meshd, *fail, *invalid;
+    int64_t *graft, *mtime;
+    uint8_t* tflags;
+    double* bp;
+    uint8_t* estate;
+    int64_t* expire;
+    const double* p6;
+    double* score;
+    int64_t now;
+    int32_t* purged;
+};
+
+struct ColocArgs {
+    int64_t E;
+    const uint32_t *row_ptr, *col, *owner, *ip_ptr, *ip_ids;
+    const uint8_t* ip_white;
+    const uint8_t* estate;
+    double* p6;
+    int32_t thr;
+};
+
+struct FieldRef {
+    void* ptr;
+    size_t bytes;
+};
+
+}  // namespace gsim
+
+struct gsim_handle {
+    int device = 0;
+    bool validate = true;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[gsim::kEvents] = {};
+    std::string err;
+
+    gsim_peer_score_params pp{};
+    std::vector<gsim_topic_score_params> tp;
+    gsim_thresholds th{};
+    gsim_gossipsub_params gp{};
+    int32_t t = 0;
+
+    int64_t n = 0, e = 0;
+    uint32_t n_ips = 0;
+    size_t bytes_allocated = 0;
+    bool has_white = false;
+    bool p6_dirty = true;
+    bool maybe_retained = false;
+
+    // device: parameters and scratch flags
+    gsim_topic_score_params* d_tp = nullptr;
+    int32_t* d_flags = nullptr;
+
+    // device: graph
+    uint32_t *d_row_ptr = nullptr, *d_col = nullptr, *d_rev = nullptr, *d_owner = nullptr;
+    uint64_t* d_sub = nullptr;
+    uint8_t* d_outbound = nullptr;
+    uint32_t *d_ip_ptr = nullptr, *d_ip_ids = nullptr;
+    uint8_t* d_ip_white = nullptr;
+    double* d_p5 = nullptr;
+
+    // device: topicStats [T][E]
+    double *d_first = nullptr, *d_meshd = nullptr, *d_fail = nullptr, *d_invalid = nullptr;
+    int64_t *d_graft = nullptr, *d_mtime = nullptr;
+    uint8_t* d_tflags = nullptr;
+    int64_t* d_backoff = nullptr;
+
+    // device: peerStats [E]
+    double* d_bp = nullptr;
+    uint8_t* d_estate = nullptr;
+    int64_t* d_expire = nullptr;
+    double* d_p6 = nullptr;
+    double* d_score = nullptr;
+
+    // heartbeat / delivery state lives in heartbeat.hip
+    struct Extra* x = nullptr;
+};
+
+int hip_check(gsim_handle* h, hipError_t e, const char* what);
+bool field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r);
+int launch_ip_colocation(gsim_handle* h);
+int launch_refresh_scores(gsim_handle* h, int64_t now);
+int launch_compute_scores(gsim_handle* h);
+
+// implemented in heartbeat.hip
+int alloc_extra(gsim_handle* h);
+void free_extra(gsim_handle* h);
+bool extra_field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r);

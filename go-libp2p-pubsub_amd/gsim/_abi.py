@@ -1,0 +1,147 @@
+"""ctypes mirror of include/gsim.h (the engine's C ABI).
+
+The structures below are field-for-field copies of the C structs, which are
+themselves field-for-field copies of the Go structs in score_params.go and
+gossipsub.go.  Loading fails loudly: there is no CPU fallback for the engine.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, c_char_p, c_double, c_float, c_int32, c_int64, c_size_t,
+                    c_uint8, c_uint32, c_uint64, c_void_p)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libgsim.so")
+
+GSIM_OK = 0
+GSIM_EINVAL = -22
+GSIM_ENOMEM = -12
+GSIM_EDEVICE = -5
+GSIM_ERANGE = -34
+GSIM_ESTATE = -71
+
+(F_FIRST, F_MESHD, F_FAIL, F_INVALID, F_GRAFT_TIME, F_MESH_TIME, F_TFLAGS, F_BP, F_ESTATE,
+ F_EXPIRE, F_P6, F_SCORE, F_BACKOFF) = range(13)
+
+TF_IN_MESH = 0x01
+TF_ACTIVE = 0x02
+ES_TRACKED = 0x01
+ES_CONNECTED = 0x02
+
+
+class CTopicScoreParams(Structure):
+    _fields_ = [
+        ("skip_atomic_validation", c_int32), ("scored", c_int32), ("topic_weight", c_double),
+        ("time_in_mesh_weight", c_double), ("time_in_mesh_quantum_ns", c_int64), ("time_in_mesh_cap", c_double),
+        ("first_message_deliveries_weight", c_double), ("first_message_deliveries_decay", c_double),
+        ("first_message_deliveries_cap", c_double),
+        ("mesh_message_deliveries_weight", c_double), ("mesh_message_deliveries_decay", c_double),
+        ("mesh_message_deliveries_cap", c_double), ("mesh_message_deliveries_threshold", c_double),
+        ("mesh_message_deliveries_window_ns", c_int64), ("mesh_message_deliveries_activation_ns", c_int64),
+        ("mesh_failure_penalty_weight", c_double), ("mesh_failure_penalty_decay", c_double),
+        ("invalid_message_deliveries_weight", c_double), ("invalid_message_deliveries_decay", c_double),
+    ]
+
+
+class CPeerScoreParams(Structure):
+    _fields_ = [
+        ("skip_atomic_validation", c_int32), ("has_app_specific_score", c_int32),
+        ("topic_score_cap", c_double), ("app_specific_weight", c_double),
+        ("ip_colocation_factor_weight", c_double), ("ip_colocation_factor_threshold", c_int32), ("_pad0", c_int32),
+        ("behaviour_penalty_weight", c_double), ("behaviour_penalty_threshold", c_double),
+        ("behaviour_penalty_decay", c_double),
+        ("decay_interval_ns", c_int64), ("decay_to_zero", c_double), ("retain_score_ns", c_int64),
+        ("seen_msg_ttl_ns", c_int64),
+    ]
+
+
+class CThresholds(Structure):
+    _fields_ = [
+        ("skip_atomic_validation", c_int32), ("_pad0", c_int32),
+        ("gossip_threshold", c_double), ("publish_threshold", c_double), ("graylist_threshold", c_double),
+        ("accept_px_threshold", c_double), ("opportunistic_graft_threshold", c_double),
+    ]
+
+
+class CGossipSubParams(Structure):
+    _fields_ = [
+        ("d", c_int32), ("dlo", c_int32), ("dhi", c_int32), ("dscore", c_int32), ("dout", c_int32),
+        ("history_length", c_int32), ("history_gossip", c_int32), ("dlazy", c_int32),
+        ("gossip_factor", c_double), ("gossip_retransmission", c_int32), ("prune_peers", c_int32),
+        ("heartbeat_initial_delay_ns", c_int64), ("heartbeat_interval_ns", c_int64),
+        ("slow_heartbeat_warning", c_double), ("fanout_ttl_ns", c_int64), ("prune_backoff_ns", c_int64),
+        ("unsubscribe_backoff_ns", c_int64), ("connectors", c_int32), ("max_pending_connections", c_int32),
+        ("connection_timeout_ns", c_int64), ("direct_connect_ticks", c_uint64),
+        ("direct_connect_initial_delay_ns", c_int64), ("opportunistic_graft_ticks", c_uint64),
+        ("opportunistic_graft_peers", c_int32), ("max_ihave_length", c_int32),
+        ("graft_flood_threshold_ns", c_int64), ("max_ihave_messages", c_int32), ("_pad0", c_int32),
+        ("iwant_followup_time_ns", c_int64),
+    ]
+
+
+# (name, restype, argtypes) for every symbol include/gsim.h declares.
+SIGNATURES = [
+    ("gsim_default_gossipsub_params", None, [POINTER(CGossipSubParams)]),
+    ("gsim_validate_topic_params", c_int32, [POINTER(CTopicScoreParams), c_char_p, c_size_t]),
+    ("gsim_validate_peer_params", c_int32,
+     [POINTER(CPeerScoreParams), POINTER(CTopicScoreParams), c_int32, c_char_p, c_size_t]),
+    ("gsim_validate_thresholds", c_int32, [POINTER(CThresholds), c_char_p, c_size_t]),
+    ("gsim_score_parameter_decay", c_double, [c_int64]),
+    ("gsim_score_parameter_decay_with_base", c_double, [c_int64, c_int64, c_double]),
+    ("gsim_create", c_int32,
+     [POINTER(CPeerScoreParams), POINTER(CTopicScoreParams), c_int32, POINTER(CThresholds),
+      POINTER(CGossipSubParams), c_int32, POINTER(c_void_p), c_char_p, c_size_t]),
+    ("gsim_create_unvalidated", c_int32,
+     [POINTER(CPeerScoreParams), POINTER(CTopicScoreParams), c_int32, POINTER(CThresholds),
+      POINTER(CGossipSubParams), c_int32, POINTER(c_void_p), c_char_p, c_size_t]),
+    ("gsim_destroy", c_int32, [c_void_p]),
+    ("gsim_last_error", c_char_p, [c_void_p]),
+    ("gsim_load_graph", c_int32,
+     [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32]),
+    ("gsim_set_app_score", c_int32, [c_void_p, c_void_p]),
+    ("gsim_set_ip_whitelist", c_int32, [c_void_p, c_void_p]),
+    ("gsim_set_topic_params", c_int32, [c_void_p, c_int32, POINTER(CTopicScoreParams)]),
+    ("gsim_refresh_scores", c_int32, [c_void_p, c_int64]),
+    ("gsim_compute_scores", c_int32, [c_void_p]),
+    ("gsim_compute_ip_colocation", c_int32, [c_void_p]),
+    ("gsim_read_scores", c_int32, [c_void_p, c_void_p]),
+    ("gsim_field_bytes", c_int32, [c_void_p, c_int32, POINTER(c_size_t)]),
+    ("gsim_read_field", c_int32, [c_void_p, c_int32, c_void_p, c_size_t]),
+    ("gsim_write_field", c_int32, [c_void_p, c_int32, c_void_p, c_size_t]),
+    ("gsim_event_record", c_int32, [c_void_p, c_int32]),
+    ("gsim_event_elapsed", c_int32, [c_void_p, c_int32, c_int32, POINTER(c_float)]),
+    ("gsim_synchronize", c_int32, [c_void_p]),
+    ("gsim_gen_random_regular", c_int32, [c_int64, c_int32, c_uint64, c_void_p, c_void_p, c_void_p]),
+    ("gsim_fill_synthetic", c_int32, [c_void_p, c_uint64, c_int64, c_double]),
+]
+
+_lib = None
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load libgsim.so (built in-tree by `make -C go-libp2p-pubsub_amd`).
+
+    torch is imported first when available so that the HIP runtime torch
+    bundles and the one libgsim links resolve to a single copy (both carry the
+    SONAME libamdhip64.so.7).
+    """
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError(f"libgsim.so not built at {p}; run `make -C go-libp2p-pubsub_amd` "
+                          "(the engine has no CPU fallback)")
+    try:  # share one HIP runtime with torch if the caller uses torch
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is present in this image
+        pass
+    lib = ctypes.CDLL(p)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib

@@ -1,0 +1,210 @@
+"""Host-side engine handle over the C ABI (include/gsim.h).
+
+`Engine` plays the role the reference's GossipSubRouter+peerScore pair plays
+for one node (gossipsub.go:420-477, score.go:64-86), but for a whole simulated
+network held on one MI355X.  Everything computational runs in libgsim.so's HIP
+kernels; this module only marshals arrays.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _abi
+from .params import GossipSubParams, PeerScoreParams, PeerScoreThresholds
+
+_FIELD_DTYPES = {
+    _abi.F_FIRST: np.float64, _abi.F_MESHD: np.float64, _abi.F_FAIL: np.float64, _abi.F_INVALID: np.float64,
+    _abi.F_GRAFT_TIME: np.int64, _abi.F_MESH_TIME: np.int64, _abi.F_TFLAGS: np.uint8, _abi.F_BP: np.float64,
+    _abi.F_ESTATE: np.uint8, _abi.F_EXPIRE: np.int64, _abi.F_P6: np.float64, _abi.F_SCORE: np.float64,
+    _abi.F_BACKOFF: np.int64,
+}
+TOPIC_FIELDS = {_abi.F_FIRST, _abi.F_MESHD, _abi.F_FAIL, _abi.F_INVALID, _abi.F_GRAFT_TIME,
+                _abi.F_MESH_TIME, _abi.F_TFLAGS, _abi.F_BACKOFF}
+
+
+class GsimError(RuntimeError):
+    def __init__(self, rc: int, msg: str):
+        super().__init__(f"gsim error {rc}: {msg}")
+        self.rc = rc
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+@dataclass
+class Network:
+    """A simulated peer graph: CSR rows = observers, columns = neighbours."""
+    n: int
+    row_ptr: np.ndarray           # uint32 [n+1]
+    col: np.ndarray               # uint32 [E]
+    outbound: np.ndarray          # uint8  [E]
+    sub: np.ndarray               # uint64 [n] topic bitmask
+    ip_ptr: Optional[np.ndarray] = None   # uint32 [n+1]
+    ip_ids: Optional[np.ndarray] = None   # uint32
+    n_ips: int = 0
+
+    @property
+    def e(self) -> int:
+        return int(self.row_ptr[-1])
+
+    def rev(self) -> np.ndarray:
+        """Reverse-edge index (j->i for every i->j)."""
+        owner = np.repeat(np.arange(self.n, dtype=np.int64), np.diff(self.row_ptr.astype(np.int64)))
+        key_fwd = owner * self.n + self.col.astype(np.int64)
+        key_rev = self.col.astype(np.int64) * self.n + owner
+        order = np.argsort(key_fwd, kind="stable")
+        pos = np.searchsorted(key_fwd[order], key_rev)
+        return order[pos].astype(np.uint32)
+
+    def owner(self) -> np.ndarray:
+        return np.repeat(np.arange(self.n, dtype=np.uint32), np.diff(self.row_ptr.astype(np.int64)))
+
+
+def random_regular(n: int, k: int, seed: int = 1, n_topics: int = 1, unique_ips: bool = True) -> Network:
+    """Seeded random k-regular network; all peers join all topics."""
+    lib = _abi.load()
+    row_ptr = np.empty(n + 1, dtype=np.uint32)
+    col = np.empty(n * k, dtype=np.uint32)
+    ob = np.empty(n * k, dtype=np.uint8)
+    rc = lib.gsim_gen_random_regular(n, k, seed, _ptr(row_ptr), _ptr(col), _ptr(ob))
+    if rc != 0:
+        raise GsimError(rc, "gsim_gen_random_regular failed")
+    mask = (1 << n_topics) - 1 if n_topics < 64 else (1 << 64) - 1
+    sub = np.full(n, mask, dtype=np.uint64)
+    ip_ptr = ip_ids = None
+    n_ips = 0
+    if unique_ips:
+        ip_ptr = np.arange(n + 1, dtype=np.uint32)
+        ip_ids = np.arange(n, dtype=np.uint32)
+        n_ips = n
+    return Network(n, row_ptr, col, ob, sub, ip_ptr, ip_ids, n_ips)
+
+
+class Engine:
+    """One simulated GossipSub network on one GPU."""
+
+    def __init__(self, params: PeerScoreParams, thresholds: PeerScoreThresholds,
+                 gossip: Optional[GossipSubParams] = None, topics: Optional[Sequence[str]] = None,
+                 device: int = 0, validate: bool = True):
+        """validate=False mirrors newPeerScore (score.go:183) as the reference's
+        unit tests use it; the default mirrors WithPeerScore (gossipsub.go:278)."""
+        self.lib = _abi.load()
+        self.params = params
+        self.thresholds = thresholds
+        self.gossip = gossip or GossipSubParams()
+        self.topics: List[str] = sorted(set(topics or []) | set(params.Topics))
+        self.topic_index = {t: i for i, t in enumerate(self.topics)}
+        pc = params.to_c()
+        self._tarr = params.topic_array(self.topics)
+        tc = thresholds.to_c()
+        gc = self.gossip.to_c()
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(512)
+        create = self.lib.gsim_create if validate else self.lib.gsim_create_unvalidated
+        rc = create(ctypes.byref(pc), self._tarr, len(self.topics), ctypes.byref(tc),
+                                  ctypes.byref(gc), device, ctypes.byref(h), buf, len(buf))
+        if rc != 0:
+            if rc == _abi.GSIM_EINVAL:
+                raise ValueError(buf.value.decode())
+            raise GsimError(rc, buf.value.decode())
+        self.h = h
+        self.net: Optional[Network] = None
+
+    # -- lifecycle -----------------------------------------------------------
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gsim_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int):
+        if rc != 0:
+            msg = self.lib.gsim_last_error(self.h)
+            msg = msg.decode() if msg else ""
+            if rc == _abi.GSIM_EINVAL:
+                raise ValueError(msg)
+            raise GsimError(rc, msg)
+
+    # -- setup -----------------------------------------------------------------
+    def load_graph(self, net: Network):
+        self._check(self.lib.gsim_load_graph(
+            self.h, net.n, _ptr(net.row_ptr), _ptr(net.col), _ptr(net.outbound), _ptr(net.sub),
+            _ptr(net.ip_ptr), _ptr(net.ip_ids), net.n_ips))
+        self.net = net
+        if self.params.AppSpecificScore is not None:
+            self.set_app_score(np.array([self.params.AppSpecificScore(p) for p in range(net.n)],
+                                        dtype=np.float64) if net.n <= 100000 else np.zeros(net.n))
+
+    def set_app_score(self, p5: np.ndarray):
+        p5 = np.ascontiguousarray(p5, dtype=np.float64)
+        self._check(self.lib.gsim_set_app_score(self.h, _ptr(p5)))
+
+    def set_ip_whitelist(self, white: Optional[np.ndarray]):
+        w = None if white is None else np.ascontiguousarray(white, dtype=np.uint8)
+        self._check(self.lib.gsim_set_ip_whitelist(self.h, _ptr(w)))
+
+    def set_topic_score_params(self, topic: str, p):
+        """Topic.SetScoreParams -> peerScore.SetTopicScoreParams (topic.go:44-82, score.go:201-241)."""
+        c = p.to_c(True)
+        self._check(self.lib.gsim_set_topic_params(self.h, self.topic_index[topic], ctypes.byref(c)))
+        self.params.Topics[topic] = p
+
+    # -- hot path ----------------------------------------------------------------
+    def refresh_scores(self, now: int):
+        self._check(self.lib.gsim_refresh_scores(self.h, int(now)))
+
+    def compute_scores(self):
+        self._check(self.lib.gsim_compute_scores(self.h))
+
+    def compute_ip_colocation(self):
+        self._check(self.lib.gsim_compute_ip_colocation(self.h))
+
+    def fill_synthetic(self, seed: int, now: int, p_mesh: float):
+        self._check(self.lib.gsim_fill_synthetic(self.h, int(seed), int(now), float(p_mesh)))
+
+    def scores(self) -> np.ndarray:
+        out = np.empty(self.net.e, dtype=np.float64)
+        self._check(self.lib.gsim_read_scores(self.h, _ptr(out)))
+        return out
+
+    # -- raw state ----------------------------------------------------------------
+    def field_shape(self, f: int):
+        e = self.net.e
+        return (max(1, len(self.topics)), e) if f in TOPIC_FIELDS else (e,)
+
+    def read(self, f: int) -> np.ndarray:
+        out = np.empty(self.field_shape(f), dtype=_FIELD_DTYPES[f])
+        self._check(self.lib.gsim_read_field(self.h, f, _ptr(out), out.nbytes))
+        return out
+
+    def write(self, f: int, arr: np.ndarray):
+        a = np.ascontiguousarray(arr, dtype=_FIELD_DTYPES[f]).reshape(self.field_shape(f))
+        self._check(self.lib.gsim_write_field(self.h, f, _ptr(a), a.nbytes))
+
+    # -- timing on the engine stream ----------------------------------------------
+    def event_record(self, slot: int):
+        self._check(self.lib.gsim_event_record(self.h, slot))
+
+    def event_elapsed_ms(self, a: int, b: int) -> float:
+        ms = ctypes.c_float()
+        self._check(self.lib.gsim_event_elapsed(self.h, a, b, ctypes.byref(ms)))
+        return float(ms.value)
+
+    def synchronize(self):
+        self._check(self.lib.gsim_synchronize(self.h))

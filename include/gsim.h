@@ -1,0 +1,263 @@
+/*
+ * gsim.h — C ABI of the MI355X-native GossipSub scoring + heartbeat engine.
+ *
+ * This is the drop-in boundary for the reference's hot path.
+ * Every entry point names the reference interface it replaces (file:line into
+ * mouzzarr/go-libp2p-pubsub).  Conventions:
+ *   - plain C types only; durations are int64 nanoseconds (Go time.Duration);
+ *   - every function returns int: 0 = OK, negative errno-style on error;
+ *     a human-readable message is available from gsim_last_error(h)
+ *     (the reference returns Go `error`s with the same meaning);
+ *   - no allocation crosses the boundary; callers own every buffer they pass,
+ *     inputs are copied in, readbacks copy out (blocking);
+ *   - a handle is single-threaded (the reference serializes all router and
+ *     peerScore work on one event loop, pubsub.go:561-675);
+ *   - topics cross as dense indices 0..T-1 (the Go shim maps topic strings to
+ *     indices in sorted order); peers cross as dense indices 0..N-1.
+ */
+#ifndef GSIM_H
+#define GSIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define GSIM_OK        0
+#define GSIM_EINVAL  (-22) /* invalid argument / parameter validation failed */
+#define GSIM_ENOMEM  (-12) /* device or host allocation failed               */
+#define GSIM_EDEVICE  (-5) /* HIP runtime error, or no gfx950 device           */
+#define GSIM_ERANGE  (-34) /* size outside what the engine supports           */
+#define GSIM_ESTATE  (-71) /* call out of order (e.g. step before load_graph)  */
+
+/* ---- parameter blocks (field-for-field mirrors of the Go structs) ------- */
+
+/* TopicScoreParams, score_params.go:117-170. */
+typedef struct gsim_topic_score_params {
+    int32_t skip_atomic_validation;
+    int32_t scored;                 /* 1 if present in PeerScoreParams.Topics */
+    double  topic_weight;
+    /* P1 */
+    double  time_in_mesh_weight;
+    int64_t time_in_mesh_quantum_ns;
+    double  time_in_mesh_cap;
+    /* P2 */
+    double  first_message_deliveries_weight;
+    double  first_message_deliveries_decay;
+    double  first_message_deliveries_cap;
+    /* P3 */
+    double  mesh_message_deliveries_weight;
+    double  mesh_message_deliveries_decay;
+    double  mesh_message_deliveries_cap;
+    double  mesh_message_deliveries_threshold;
+    int64_t mesh_message_deliveries_window_ns;
+    int64_t mesh_message_deliveries_activation_ns;
+    /* P3b */
+    double  mesh_failure_penalty_weight;
+    double  mesh_failure_penalty_decay;
+    /* P4 */
+    double  invalid_message_deliveries_weight;
+    double  invalid_message_deliveries_decay;
+} gsim_topic_score_params;
+
+/* PeerScoreParams, score_params.go:66-115.  AppSpecificScore (a Go callback)
+ * is replaced by a per-peer array set with gsim_set_app_score();
+ * IPColocationFactorWhitelist (CIDR list) by a per-IP flag array set with
+ * gsim_set_ip_whitelist(). */
+typedef struct gsim_peer_score_params {
+    int32_t skip_atomic_validation;
+    int32_t has_app_specific_score;   /* AppSpecificScore != nil */
+    double  topic_score_cap;
+    double  app_specific_weight;
+    double  ip_colocation_factor_weight;
+    int32_t ip_colocation_factor_threshold;
+    int32_t _pad0;
+    double  behaviour_penalty_weight;
+    double  behaviour_penalty_threshold;
+    double  behaviour_penalty_decay;
+    int64_t decay_interval_ns;
+    double  decay_to_zero;
+    int64_t retain_score_ns;
+    int64_t seen_msg_ttl_ns;
+} gsim_peer_score_params;
+
+/* PeerScoreThresholds, score_params.go:12-35. */
+typedef struct gsim_thresholds {
+    int32_t skip_atomic_validation;
+    int32_t _pad0;
+    double  gossip_threshold;
+    double  publish_threshold;
+    double  graylist_threshold;
+    double  accept_px_threshold;
+    double  opportunistic_graft_threshold;
+} gsim_thresholds;
+
+/* GossipSubParams, gossipsub.go:63-205 (defaults gossipsub.go:244-275). */
+typedef struct gsim_gossipsub_params {
+    int32_t d, dlo, dhi, dscore, dout;
+    int32_t history_length, history_gossip;
+    int32_t dlazy;
+    double  gossip_factor;
+    int32_t gossip_retransmission;
+    int32_t prune_peers;
+    int64_t heartbeat_initial_delay_ns;
+    int64_t heartbeat_interval_ns;
+    double  slow_heartbeat_warning;
+    int64_t fanout_ttl_ns;
+    int64_t prune_backoff_ns;
+    int64_t unsubscribe_backoff_ns;
+    int32_t connectors;
+    int32_t max_pending_connections;
+    int64_t connection_timeout_ns;
+    uint64_t direct_connect_ticks;
+    int64_t direct_connect_initial_delay_ns;
+    uint64_t opportunistic_graft_ticks;
+    int32_t opportunistic_graft_peers;
+    int32_t max_ihave_length;
+    int64_t graft_flood_threshold_ns;
+    int32_t max_ihave_messages;
+    int32_t _pad0;
+    int64_t iwant_followup_time_ns;
+} gsim_gossipsub_params;
+
+/* ---- host-side parameter API (no device needed) ------------------------ */
+
+/* DefaultGossipSubParams(), gossipsub.go:244-275. */
+void gsim_default_gossipsub_params(gsim_gossipsub_params* out);
+
+/* TopicScoreParams.validate(), score_params.go:236-398.  err may be NULL. */
+int gsim_validate_topic_params(const gsim_topic_score_params* p, char* err, size_t errlen);
+/* PeerScoreParams.validate(), score_params.go:173-234 (validates every scored
+ * topic first, as the reference does). */
+int gsim_validate_peer_params(const gsim_peer_score_params* p,
+                              const gsim_topic_score_params* topics, int32_t n_topics,
+                              char* err, size_t errlen);
+/* PeerScoreThresholds.validate(), score_params.go:37-64. */
+int gsim_validate_thresholds(const gsim_thresholds* p, char* err, size_t errlen);
+/* NewMessageCache(gossip, history) panics if gossip > history, mcache.go:21-26;
+ * here it is a GSIM_EINVAL from gsim_create. */
+
+/* ScoreParameterDecay / ScoreParameterDecayWithBase, score_params.go:405-417. */
+double gsim_score_parameter_decay(int64_t decay_ns);
+double gsim_score_parameter_decay_with_base(int64_t decay_ns, int64_t base_ns, double decay_to_zero);
+
+/* ---- engine lifecycle -------------------------------------------------- */
+
+typedef struct gsim_handle gsim_handle;
+
+/* Replaces WithPeerScore(params, thresholds) (gossipsub.go:278-319) +
+ * WithGossipSubParams (gossipsub.go:398-411) + newPeerScore (score.go:183-195).
+ * Validates like the reference (GSIM_EINVAL + message; the message is also
+ * written to err when err != NULL since no handle exists on failure).
+ * device: HIP device ordinal. */
+int gsim_create(const gsim_peer_score_params* params,
+                const gsim_topic_score_params* topics, int32_t n_topics,
+                const gsim_thresholds* thresholds,
+                const gsim_gossipsub_params* gossip,
+                int32_t device, gsim_handle** out, char* err, size_t errlen);
+/* newPeerScore (score.go:183-195) without WithPeerScore's validation: the
+ * reference's unit tests build peerScore this way with parameters validate()
+ * would reject (e.g. decay 1.0).  Also disables validation in
+ * gsim_set_topic_params for this handle. */
+int gsim_create_unvalidated(const gsim_peer_score_params* params,
+                            const gsim_topic_score_params* topics, int32_t n_topics,
+                            const gsim_thresholds* thresholds,
+                            const gsim_gossipsub_params* gossip,
+                            int32_t device, gsim_handle** out, char* err, size_t errlen);
+int gsim_destroy(gsim_handle* h);
+const char* gsim_last_error(const gsim_handle* h);
+
+/* Load the simulated network: a CSR of N observers.  Row i lists the peers i
+ * is connected to (must be symmetric: j in row i <=> i in row j; rows sorted
+ * ascending, no self loops, no duplicates).  outbound[e] = 1 if observer
+ * row(e) initiated the connection to col[e] (gossipsub.go:525-552).
+ * subscriptions[i] = bitmask of topics peer i subscribes to (T <= 64).
+ * ip_ptr/ip_ids = per-peer CSR of IP ids as seen by its neighbours
+ * (score.go:984-1024 getIPs; IPv6 /64 prefixes are just more ids).
+ * Every edge starts tracked+connected (AddPeer, score.go:595-609) with zero
+ * counters, nothing in any mesh.  Copies everything. */
+int gsim_load_graph(gsim_handle* h, int64_t n_peers,
+                    const uint32_t* row_ptr, const uint32_t* col_idx,
+                    const uint8_t* outbound, const uint64_t* subscriptions,
+                    const uint32_t* ip_ptr, const uint32_t* ip_ids, uint32_t n_ips);
+
+/* AppSpecificScore(p) for every peer (score_params.go:78) — host refreshes. */
+int gsim_set_app_score(gsim_handle* h, const double* p5);
+/* IPColocationFactorWhitelist (score_params.go:91): whitelisted[ip_id] = 1 if
+ * any whitelisted CIDR contains that IP (host precomputes net.IPNet.Contains). */
+int gsim_set_ip_whitelist(gsim_handle* h, const uint8_t* whitelisted);
+/* SetTopicScoreParams (score.go:201-241, topic.go:44-82): validates, installs,
+ * and recaps first/mesh counters when caps are lowered. */
+int gsim_set_topic_params(gsim_handle* h, int32_t topic, const gsim_topic_score_params* p);
+
+/* ---- hot path ---------------------------------------------------------- */
+
+/* peerScore.refreshScores (score.go:504-565) for every observer at virtual
+ * time now_ns, fused with peerScore.score (score.go:265-342) of every edge into
+ * the score snapshot; P6 (score.go:344-388) is re-derived first when the
+ * tracked set changed. */
+int gsim_refresh_scores(gsim_handle* h, int64_t now_ns);
+/* peerScore.score only (no decay) for every edge -> score snapshot. */
+int gsim_compute_scores(gsim_handle* h);
+/* ipColocationFactor (score.go:344-388) for every edge (segmented count over
+ * each observer's neighbour IPs). */
+int gsim_compute_ip_colocation(gsim_handle* h);
+
+/* Copy the score snapshot (E doubles, edge order) to host. */
+int gsim_read_scores(gsim_handle* h, double* out);
+
+/* ---- raw state access (tests, checkpoint/resume, golden fixtures) ------- */
+typedef enum gsim_field {
+    GSIM_F_FIRST = 0,     /* f64 [T][E] firstMessageDeliveries          score.go:49 */
+    GSIM_F_MESHD,         /* f64 [T][E] meshMessageDeliveries           score.go:52 */
+    GSIM_F_FAIL,          /* f64 [T][E] meshFailurePenalty              score.go:58 */
+    GSIM_F_INVALID,       /* f64 [T][E] invalidMessageDeliveries        score.go:61 */
+    GSIM_F_GRAFT_TIME,    /* i64 [T][E] graftTime (ns)                  score.go:42 */
+    GSIM_F_MESH_TIME,     /* i64 [T][E] meshTime (ns)                   score.go:46 */
+    GSIM_F_TFLAGS,        /* u8  [T][E] bit0 inMesh, bit1 meshMessageDeliveriesActive */
+    GSIM_F_BP,            /* f64 [E]    behaviourPenalty                score.go:34 */
+    GSIM_F_ESTATE,        /* u8  [E]    bit0 tracked (peerStats exists), bit1 connected */
+    GSIM_F_EXPIRE,        /* i64 [E]    retention expiry (ns)           score.go:22 */
+    GSIM_F_P6,            /* f64 [E]    ipColocationFactor value        */
+    GSIM_F_SCORE,         /* f64 [E]    score snapshot                  */
+    GSIM_F_BACKOFF,       /* i64 [T][E] prune backoff expiry, 0 = none gossipsub.go:432 */
+    GSIM_F__COUNT
+} gsim_field;
+
+#define GSIM_TF_IN_MESH   0x01u
+#define GSIM_TF_ACTIVE    0x02u
+#define GSIM_ES_TRACKED   0x01u
+#define GSIM_ES_CONNECTED 0x02u
+
+/* Size in bytes of a field for the loaded graph. */
+int gsim_field_bytes(gsim_handle* h, int32_t field, size_t* out);
+int gsim_read_field(gsim_handle* h, int32_t field, void* dst, size_t bytes);
+int gsim_write_field(gsim_handle* h, int32_t field, const void* src, size_t bytes);
+
+/* ---- device timing on the engine's own stream (bench/profiling) -------- */
+/* Record HIP event `slot` (0..15) on the engine stream. */
+int gsim_event_record(gsim_handle* h, int32_t slot);
+/* Milliseconds between two recorded events (synchronizes on `to`). */
+int gsim_event_elapsed(gsim_handle* h, int32_t from, int32_t to, float* ms);
+int gsim_synchronize(gsim_handle* h);
+
+/* ---- synthetic inputs -------------------------------- */
+/* Random k-regular simple graph on n vertices (configuration model, bad
+ * pairs repaired by random double-edge swaps), seeded.  row_ptr (n+1) and
+ * col_idx (n*k) are caller-allocated; rows come out sorted.  outbound
+ * (n*k, may be NULL) gets a Bernoulli(0.5) initiator per undirected edge. */
+int gsim_gen_random_regular(int64_t n, int32_t k, uint64_t seed,
+                            uint32_t* row_ptr, uint32_t* col_idx, uint8_t* outbound);
+/* Fill every edge-topic record with seeded steady-state-like counters on the
+ * device (mesh membership with probability p_mesh, graft times within the
+ * last hour of now_ns); every edge tracked+connected.  For benchmarking at
+ * sizes where a host upload would dominate. */
+int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now_ns, double p_mesh);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSIM_H */

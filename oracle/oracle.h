@@ -1,0 +1,139 @@
+/*
+ * oracle.h — CPU restatement of the reference hot path.  TEST INFRASTRUCTURE.
+ *
+ * This library is the parity checker for the HIP engine and the timed
+ * `cpu_baseline` in bench.py.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it; the product path never does.
+ *
+ * It restates, function by function, mouzzarr/go-libp2p-pubsub:
+ *   score.go (peerScore), score_params.go, gossipsub.go (heartbeat, handlers,
+ *   emitGossip), mcache.go, timecache/, gossip_tracer.go
+ * over the same structure-of-arrays/CSR layout the engine uses, executing the
+ * deterministic BSP semantics of DESIGN.md §3 (virtual clock, ascending topic
+ * order, Philox4x32-10 selection).  Parity is pinned by the reference's own
+ * known-answer tests (score_test.go, score_params_test.go, mcache_test.go,
+ * gossip_tracer_test.go, timecache tests) ported in tests/test_oracle_kats.py.
+ */
+#ifndef GSIM_ORACLE_H
+#define GSIM_ORACLE_H
+
+#include <stdint.h>
+#include "../include/gsim.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Every array is caller-owned (numpy in the tests). [T][E] = topic-major. */
+typedef struct orc_net {
+    int64_t n, e;
+    int32_t t;
+    int32_t _pad;
+    const uint32_t* row_ptr;   /* [N+1] */
+    const uint32_t* col;       /* [E]   */
+    const uint32_t* rev;       /* [E]   reverse edge index */
+    const uint64_t* sub;       /* [N]   topic bitmask */
+    const uint8_t*  outbound;  /* [E]   */
+    const uint32_t* ip_ptr;    /* [N+1] */
+    const uint32_t* ip_ids;    /* [ip_ptr[N]] */
+    const uint8_t*  ip_white;  /* [n_ips] or NULL */
+    const double*   p5;        /* [N] AppSpecificScore per peer, or NULL (=0) */
+    double*  first;            /* [T][E] */
+    double*  meshd;            /* [T][E] */
+    double*  fail;             /* [T][E] */
+    double*  invalid;          /* [T][E] */
+    int64_t* graft_time;       /* [T][E] */
+    int64_t* mesh_time;        /* [T][E] */
+    uint8_t* tflags;           /* [T][E] */
+    double*  bp;               /* [E] */
+    uint8_t* estate;           /* [E] */
+    int64_t* expire;           /* [E] */
+    double*  p6;               /* [E] */
+    double*  score;            /* [E] */
+    int64_t* backoff;          /* [T][E] */
+    const gsim_peer_score_params*  pp;
+    const gsim_topic_score_params* tp;   /* [T] */
+    const gsim_thresholds*         th;
+    const gsim_gossipsub_params*   gp;
+} orc_net;
+
+/* ---- score.go ---------------------------------------------------------- */
+void   orc_refresh_scores(orc_net* s, int64_t now);              /* score.go:504-565 */
+double orc_score_edge(const orc_net* s, int64_t e);              /* score.go:265-342 */
+void   orc_compute_scores(orc_net* s);                           /* score() for every edge */
+void   orc_ip_colocation(orc_net* s);                            /* score.go:344-388 */
+void   orc_add_penalty(orc_net* s, int64_t e, int32_t count);    /* score.go:391-405 */
+void   orc_graft(orc_net* s, int64_t e, int32_t topic, int64_t now); /* score.go:649-667 */
+void   orc_prune(orc_net* s, int64_t e, int32_t topic);          /* score.go:669-691 */
+void   orc_add_peer(orc_net* s, int64_t e);                      /* score.go:595-609 */
+void   orc_remove_peer(orc_net* s, int64_t e, int64_t now);      /* score.go:611-644 */
+void   orc_set_topic_params(orc_net* s, int32_t topic, gsim_topic_score_params* tp_slot,
+                            const gsim_topic_score_params* np); /* score.go:201-241 */
+void   orc_mark_first(orc_net* s, int64_t e, int32_t topic);     /* score.go:919-946 */
+void   orc_mark_duplicate(orc_net* s, int64_t e, int32_t topic, int32_t has_validated,
+                          int64_t validated, int64_t now);      /* score.go:951-981 */
+void   orc_mark_invalid(orc_net* s, int64_t e, int32_t topic);   /* score.go:901-914 */
+
+/* Message delivery records of ONE observer (score.go:90-120, 693-877). */
+typedef struct orc_drecs orc_drecs;
+orc_drecs* orc_drecs_new(int64_t seen_ttl);
+void orc_drecs_free(orc_drecs* d);
+void orc_validate_message(orc_net* s, orc_drecs* d, uint64_t mid, int64_t now);   /* 693-700 */
+void orc_deliver_message(orc_net* s, orc_drecs* d, int64_t from_e, uint64_t mid,
+                         int32_t topic, int64_t now);                            /* 702-726 */
+/* reason codes = order of tracer.go:28-38 (see ORC_REJECT_*) */
+void orc_reject_message(orc_net* s, orc_drecs* d, int64_t from_e, uint64_t mid,
+                        int32_t topic, int32_t reason, int64_t now);             /* 728-793 */
+void orc_duplicate_message(orc_net* s, orc_drecs* d, int64_t from_e, uint64_t mid,
+                           int32_t topic, int64_t now);                          /* 795-827 */
+void orc_drecs_gc(orc_drecs* d, int64_t now);                                    /* 863-877 */
+void orc_drecs_expire_head(orc_drecs* d, int64_t expire);  /* test hack: score_test.go:595 */
+
+enum {
+    ORC_REJECT_BLACKLISTED_PEER = 0, ORC_REJECT_BLACKLISTED_SOURCE, ORC_REJECT_MISSING_SIGNATURE,
+    ORC_REJECT_UNEXPECTED_SIGNATURE, ORC_REJECT_UNEXPECTED_AUTH_INFO, ORC_REJECT_INVALID_SIGNATURE,
+    ORC_REJECT_VALIDATION_QUEUE_FULL, ORC_REJECT_VALIDATION_THROTTLED, ORC_REJECT_VALIDATION_FAILED,
+    ORC_REJECT_VALIDATION_IGNORED, ORC_REJECT_SELF_ORIGIN
+};
+
+/* ---- mcache.go (one router's MessageCache) ------------------------------ */
+typedef struct orc_mcache orc_mcache;
+orc_mcache* orc_mcache_new(int32_t gossip, int32_t history);            /* mcache.go:21-36 */
+void orc_mcache_free(orc_mcache* m);
+void orc_mcache_put(orc_mcache* m, uint64_t mid, int32_t topic);        /* mcache.go:55-59 */
+int  orc_mcache_get(orc_mcache* m, uint64_t mid);                       /* mcache.go:61-64 */
+int  orc_mcache_get_for_peer(orc_mcache* m, uint64_t mid, uint32_t peer, int32_t* count); /* 66-80 */
+int  orc_mcache_gossip_ids(orc_mcache* m, int32_t topic, uint64_t* out, int32_t cap);     /* 82-92 */
+void orc_mcache_shift(orc_mcache* m);                                   /* mcache.go:94-104 */
+int  orc_mcache_len(orc_mcache* m);
+
+/* ---- gossip_tracer.go (one router's promise tracker) -------------------- */
+typedef struct orc_gtracer orc_gtracer;
+orc_gtracer* orc_gtracer_new(int64_t followup);
+void orc_gtracer_free(orc_gtracer* g);
+/* AddPromise picks msg_ids[pick] (the reference uses rand.Intn; the caller
+ * supplies the index, gossip_tracer.go:48-75). */
+void orc_gtracer_add_promise(orc_gtracer* g, uint32_t peer, const uint64_t* mids, int32_t n,
+                             int32_t pick, int64_t now);
+/* GetBrokenPromises, gossip_tracer.go:79-115: fills peers/counts (sorted by
+ * peer), returns the number of peers with broken promises. */
+int  orc_gtracer_broken(orc_gtracer* g, int64_t now, uint32_t* peers, int32_t* counts, int32_t cap);
+void orc_gtracer_fulfill(orc_gtracer* g, uint64_t mid);                 /* 119-141 */
+void orc_gtracer_throttle(orc_gtracer* g, uint32_t peer);               /* 182-200 */
+int  orc_gtracer_peer_promises(orc_gtracer* g);                         /* len(peerPromises) */
+
+/* ---- timecache/ --------------------------------------------------------- */
+typedef struct orc_tcache orc_tcache;
+orc_tcache* orc_tcache_new(int32_t strategy /*0 first-seen, 1 last-seen*/, int64_t ttl);
+void orc_tcache_free(orc_tcache* c);
+int  orc_tcache_add(orc_tcache* c, uint64_t id, int64_t now);  /* first_seen_cache.go:47-56 / last_seen_cache.go:38-45 */
+int  orc_tcache_has(orc_tcache* c, uint64_t id, int64_t now);  /* first_seen_cache.go:37-45 / last_seen_cache.go:47-58 */
+void orc_tcache_sweep(orc_tcache* c, int64_t now);             /* timecache/util.go:26-35 */
+
+/* ---- Philox4x32-10 (the canonical selection stream) ----- */
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,83 @@
+"""Shared parameter fixtures and seeded random engine states (test infrastructure)."""
+from __future__ import annotations
+
+import numpy as np
+
+from gsim import _abi
+from gsim.params import Minute, PeerScoreParams, PeerScoreThresholds, Second, TopicScoreParams
+
+
+def beacon_topic(**over) -> TopicScoreParams:
+    """The only production-like TopicScoreParams set in the reference
+    (gossipsub_spam_test.go:638-656), used as the "beacon-style" fixture."""
+    kw = dict(TopicWeight=0.25, TimeInMeshWeight=0.0027, TimeInMeshQuantum=Second, TimeInMeshCap=3600,
+              FirstMessageDeliveriesWeight=0.664, FirstMessageDeliveriesDecay=0.9916,
+              FirstMessageDeliveriesCap=1500, MeshMessageDeliveriesWeight=-0.25, MeshMessageDeliveriesDecay=0.97,
+              MeshMessageDeliveriesCap=400, MeshMessageDeliveriesThreshold=100,
+              MeshMessageDeliveriesActivation=30 * Second, MeshMessageDeliveriesWindow=5 * Minute,
+              MeshFailurePenaltyWeight=-0.25, MeshFailurePenaltyDecay=0.997,
+              InvalidMessageDeliveriesWeight=-99, InvalidMessageDeliveriesDecay=0.9994)
+    kw.update(over)
+    return TopicScoreParams(**kw)
+
+
+def beacon_params(n_topics: int, topic_cap: float = 0.0, **over) -> PeerScoreParams:
+    """gossipsub_spam_test.go:627-637 peer params (+P6/P7 enabled for coverage)."""
+    kw = dict(AppSpecificScore=lambda p: 0.0, AppSpecificWeight=1.0, IPColocationFactorWeight=-35.11,
+              IPColocationFactorThreshold=2, BehaviourPenaltyWeight=-15.92, BehaviourPenaltyThreshold=6,
+              BehaviourPenaltyDecay=0.986, DecayInterval=Second, DecayToZero=0.01, RetainScore=10 * Second,
+              TopicScoreCap=topic_cap)
+    kw.update(over)
+    p = PeerScoreParams(**kw)
+    # vary the topics a little so per-topic parameters are exercised
+    for t in range(n_topics):
+        p.Topics[f"topic{t:02d}"] = beacon_topic(TopicWeight=0.25 + 0.05 * t,
+                                                 MeshMessageDeliveriesThreshold=100 - 3 * t)
+    return p
+
+
+def beacon_thresholds() -> PeerScoreThresholds:
+    """gossipsub_spam_test.go:657-662."""
+    return PeerScoreThresholds(GossipThreshold=-100, PublishThreshold=-200, GraylistThreshold=-300,
+                               AcceptPXThreshold=0)
+
+
+def sybil_ips(n: int, frac: float, per_ip: int, rng) -> tuple:
+    """Honest peers get a unique IP; a `frac` share of peers share one IP per `per_ip`."""
+    ip_of = np.arange(n, dtype=np.uint32)
+    syb = rng.permutation(n)[: int(n * frac)]
+    ip_of[syb] = n + (np.arange(len(syb)) // per_ip)
+    ips, inv = np.unique(ip_of, return_inverse=True)
+    ip_ptr = np.arange(n + 1, dtype=np.uint32)
+    return ip_ptr, inv.astype(np.uint32), len(ips)
+
+
+def randomize_state(st, rng, now: int, retained_frac: float = 0.05):
+    """Fill a NetState with adversarially varied counters, flags and times."""
+    T, E = st.first.shape
+
+    def counters(scale):
+        x = rng.exponential(scale, size=(T, E))
+        x[rng.random((T, E)) < 0.3] = 0.0
+        x[rng.random((T, E)) < 0.05] = 0.0101    # just above DecayToZero: snaps to 0 after decay
+        return x
+
+    st.first[...] = counters(20.0)
+    st.meshd[...] = counters(60.0)
+    st.fail[...] = counters(50.0)
+    st.invalid[...] = counters(2.0)
+    st.tflags[...] = (rng.random((T, E)) < 0.3).astype(np.uint8) * _abi.TF_IN_MESH
+    st.tflags[...] |= (rng.random((T, E)) < 0.5).astype(np.uint8) * _abi.TF_ACTIVE
+    st.graft_time[...] = now - rng.integers(0, 4000 * Second, size=(T, E))
+    st.mesh_time[...] = rng.integers(0, 4000 * Second, size=(T, E))
+    st.bp[...] = np.where(rng.random(E) < 0.5, rng.exponential(8.0, E), 0.0)
+    r = rng.random(E)
+    st.estate[...] = _abi.ES_TRACKED | _abi.ES_CONNECTED
+    st.estate[r < retained_frac] = _abi.ES_TRACKED
+    st.estate[(r >= retained_frac) & (r < retained_frac * 1.2)] = 0
+    st.expire[...] = now + rng.integers(-5 * Second, 5 * Second, size=E)
+    st.expire[st.estate != _abi.ES_TRACKED] = 0
+    untracked = st.estate == 0
+    for f in ("first", "meshd", "fail", "invalid", "graft_time", "mesh_time", "tflags"):
+        getattr(st, f)[:, untracked] = 0
+    st.bp[untracked] = 0

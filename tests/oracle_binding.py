@@ -1,0 +1,169 @@
+"""ctypes binding of oracle/liboracle.so (test infrastructure only).
+
+`NetState` holds every state array of a simulated network in numpy, in the
+exact layout the engine uses, and exposes an `orc_net` view for the oracle.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, Structure, c_double, c_int32, c_int64, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+
+import sys  # noqa: E402
+
+sys.path.insert(0, os.path.join(REPO, "go-libp2p-pubsub_amd"))
+from gsim import _abi  # noqa: E402
+
+
+class OrcNet(Structure):
+    _fields_ = [
+        ("n", c_int64), ("e", c_int64), ("t", c_int32), ("_pad", c_int32),
+        ("row_ptr", c_void_p), ("col", c_void_p), ("rev", c_void_p), ("sub", c_void_p), ("outbound", c_void_p),
+        ("ip_ptr", c_void_p), ("ip_ids", c_void_p), ("ip_white", c_void_p), ("p5", c_void_p),
+        ("first", c_void_p), ("meshd", c_void_p), ("fail", c_void_p), ("invalid", c_void_p),
+        ("graft_time", c_void_p), ("mesh_time", c_void_p), ("tflags", c_void_p),
+        ("bp", c_void_p), ("estate", c_void_p), ("expire", c_void_p), ("p6", c_void_p), ("score", c_void_p),
+        ("backoff", c_void_p),
+        ("pp", c_void_p), ("tp", c_void_p), ("th", c_void_p), ("gp", c_void_p),
+    ]
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_LIB):
+            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+        lib = ctypes.CDLL(ORACLE_LIB)
+        P = POINTER(OrcNet)
+        sig = {
+            "orc_refresh_scores": (None, [P, c_int64]),
+            "orc_score_edge": (c_double, [P, c_int64]),
+            "orc_compute_scores": (None, [P]),
+            "orc_ip_colocation": (None, [P]),
+            "orc_add_penalty": (None, [P, c_int64, c_int32]),
+            "orc_graft": (None, [P, c_int64, c_int32, c_int64]),
+            "orc_prune": (None, [P, c_int64, c_int32]),
+            "orc_add_peer": (None, [P, c_int64]),
+            "orc_remove_peer": (None, [P, c_int64, c_int64]),
+            "orc_set_topic_params": (None, [P, c_int32, c_void_p, c_void_p]),
+            "orc_mark_first": (None, [P, c_int64, c_int32]),
+            "orc_mark_duplicate": (None, [P, c_int64, c_int32, c_int32, c_int64, c_int64]),
+            "orc_mark_invalid": (None, [P, c_int64, c_int32]),
+            "orc_drecs_new": (c_void_p, [c_int64]),
+            "orc_drecs_free": (None, [c_void_p]),
+            "orc_validate_message": (None, [P, c_void_p, c_uint64, c_int64]),
+            "orc_deliver_message": (None, [P, c_void_p, c_int64, c_uint64, c_int32, c_int64]),
+            "orc_reject_message": (None, [P, c_void_p, c_int64, c_uint64, c_int32, c_int32, c_int64]),
+            "orc_duplicate_message": (None, [P, c_void_p, c_int64, c_uint64, c_int32, c_int64]),
+            "orc_drecs_gc": (None, [c_void_p, c_int64]),
+            "orc_drecs_expire_head": (None, [c_void_p, c_int64]),
+            "orc_mcache_new": (c_void_p, [c_int32, c_int32]),
+            "orc_mcache_free": (None, [c_void_p]),
+            "orc_mcache_put": (None, [c_void_p, c_uint64, c_int32]),
+            "orc_mcache_get": (c_int32, [c_void_p, c_uint64]),
+            "orc_mcache_get_for_peer": (c_int32, [c_void_p, c_uint64, c_uint32, POINTER(c_int32)]),
+            "orc_mcache_gossip_ids": (c_int32, [c_void_p, c_int32, c_void_p, c_int32]),
+            "orc_mcache_shift": (None, [c_void_p]),
+            "orc_mcache_len": (c_int32, [c_void_p]),
+            "orc_gtracer_new": (c_void_p, [c_int64]),
+            "orc_gtracer_free": (None, [c_void_p]),
+            "orc_gtracer_add_promise": (None, [c_void_p, c_uint32, c_void_p, c_int32, c_int32, c_int64]),
+            "orc_gtracer_broken": (c_int32, [c_void_p, c_int64, c_void_p, c_void_p, c_int32]),
+            "orc_gtracer_fulfill": (None, [c_void_p, c_uint64]),
+            "orc_gtracer_throttle": (None, [c_void_p, c_uint32]),
+            "orc_gtracer_peer_promises": (c_int32, [c_void_p]),
+            "orc_tcache_new": (c_void_p, [c_int32, c_int64]),
+            "orc_tcache_free": (None, [c_void_p]),
+            "orc_tcache_add": (c_int32, [c_void_p, c_uint64, c_int64]),
+            "orc_tcache_has": (c_int32, [c_void_p, c_uint64, c_int64]),
+            "orc_tcache_sweep": (None, [c_void_p, c_int64]),
+            "orc_philox4x32_10": (None, [c_void_p, c_void_p, c_void_p]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(c_void_p)
+
+
+class NetState:
+    """All engine state of one network, host-side, in engine layout."""
+
+    TOPIC_FIELDS = ("first", "meshd", "fail", "invalid", "graft_time", "mesh_time", "tflags", "backoff")
+    EDGE_FIELDS = ("bp", "estate", "expire", "p6", "score")
+    DTYPES = {"first": np.float64, "meshd": np.float64, "fail": np.float64, "invalid": np.float64,
+              "graft_time": np.int64, "mesh_time": np.int64, "tflags": np.uint8, "backoff": np.int64,
+              "bp": np.float64, "estate": np.uint8, "expire": np.int64, "p6": np.float64, "score": np.float64}
+    FIELD_IDS = {"first": _abi.F_FIRST, "meshd": _abi.F_MESHD, "fail": _abi.F_FAIL, "invalid": _abi.F_INVALID,
+                 "graft_time": _abi.F_GRAFT_TIME, "mesh_time": _abi.F_MESH_TIME, "tflags": _abi.F_TFLAGS,
+                 "backoff": _abi.F_BACKOFF, "bp": _abi.F_BP, "estate": _abi.F_ESTATE, "expire": _abi.F_EXPIRE,
+                 "p6": _abi.F_P6, "score": _abi.F_SCORE}
+
+    def __init__(self, net, params, thresholds=None, gossip=None, topics=None, p5=None, ip_white=None):
+        from gsim.params import GossipSubParams, PeerScoreThresholds
+        self.net = net
+        self.params = params
+        self.topics = sorted(set(topics or []) | set(params.Topics))
+        self.T = max(1, len(self.topics))
+        E = net.e
+        for f in self.TOPIC_FIELDS:
+            setattr(self, f, np.zeros((self.T, E), dtype=self.DTYPES[f]))
+        for f in self.EDGE_FIELDS:
+            setattr(self, f, np.zeros(E, dtype=self.DTYPES[f]))
+        self.estate[:] = _abi.ES_TRACKED | _abi.ES_CONNECTED
+        self.rev = net.rev()
+        self.p5 = np.zeros(net.n) if p5 is None else np.ascontiguousarray(p5, dtype=np.float64)
+        self.ip_white = None if ip_white is None else np.ascontiguousarray(ip_white, dtype=np.uint8)
+        self.pp = params.to_c()
+        self.tp = params.topic_array(self.topics)
+        self.th = (thresholds or PeerScoreThresholds()).to_c()
+        self.gp = (gossip or GossipSubParams()).to_c()
+        self._view = None
+
+    def view(self):
+        n = self.net
+        v = OrcNet()
+        v.n, v.e, v.t = n.n, n.e, len(self.topics)
+        v.row_ptr, v.col, v.rev, v.sub, v.outbound = _p(n.row_ptr), _p(n.col), _p(self.rev), _p(n.sub), _p(n.outbound)
+        v.ip_ptr, v.ip_ids = _p(n.ip_ptr), _p(n.ip_ids)
+        if n.ip_ptr is None:  # no IPs known (ps.host == nil in the reference tests)
+            self._zero_ip_ptr = np.zeros(n.n + 1, dtype=np.uint32)
+            self._zero_ip_ids = np.zeros(1, dtype=np.uint32)
+            v.ip_ptr, v.ip_ids = _p(self._zero_ip_ptr), _p(self._zero_ip_ids)
+        v.ip_white = _p(self.ip_white)
+        v.p5 = _p(self.p5)
+        for f in self.TOPIC_FIELDS + self.EDGE_FIELDS:
+            setattr(v, f, _p(getattr(self, f)))
+        v.pp = ctypes.cast(ctypes.byref(self.pp), c_void_p)
+        v.tp = ctypes.cast(self.tp, c_void_p)
+        v.th = ctypes.cast(ctypes.byref(self.th), c_void_p)
+        v.gp = ctypes.cast(ctypes.byref(self.gp), c_void_p)
+        self._view = v
+        return ctypes.byref(v)
+
+    def copy_fields_from(self, other):
+        for f in self.TOPIC_FIELDS + self.EDGE_FIELDS:
+            getattr(self, f)[...] = getattr(other, f)
+
+    def push_to_engine(self, eng):
+        for f in self.TOPIC_FIELDS + self.EDGE_FIELDS:
+            eng.write(self.FIELD_IDS[f], getattr(self, f))
+
+    def pull_from_engine(self, eng):
+        for f in self.TOPIC_FIELDS + self.EDGE_FIELDS:
+            getattr(self, f)[...] = eng.read(self.FIELD_IDS[f])

@@ -1,0 +1,102 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every
+symbol include/gsim.h declares, validates like the reference, and refuses to
+run without a device (there is no CPU fallback)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO, gpu_available
+from gsim import _abi
+from gsim.engine import Engine, random_regular
+from gsim.params import PeerScoreParams, PeerScoreThresholds, Second, TopicScoreParams
+
+HEADER = os.path.join(REPO, "include", "gsim.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gsim_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_surface():
+    fns = declared_functions()
+    for must in ["gsim_create", "gsim_destroy", "gsim_load_graph", "gsim_refresh_scores", "gsim_read_scores",
+                 "gsim_set_topic_params", "gsim_set_app_score", "gsim_set_ip_whitelist", "gsim_last_error"]:
+        assert must in fns
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _abi.load()
+    missing = [f for f in declared_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+
+
+def test_python_signatures_cover_header():
+    declared = set(declared_functions())
+    bound = {name for name, _, _ in _abi.SIGNATURES}
+    assert declared == bound
+
+
+def test_struct_layout_matches_c(tmp_path):
+    """Compile a probe against gsim.h and compare sizeof/offsetof with ctypes."""
+    import subprocess
+    structs = {"gsim_topic_score_params": _abi.CTopicScoreParams, "gsim_peer_score_params": _abi.CPeerScoreParams,
+               "gsim_thresholds": _abi.CThresholds, "gsim_gossipsub_params": _abi.CGossipSubParams}
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "gsim.h"', "int main(void){"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'printf("{cname}.{fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("return 0;}")
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.check_call(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)])
+    got = dict(l.rsplit(" ", 1) for l in subprocess.check_output([str(exe)]).decode().splitlines())
+    for cname, py in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert int(got[f"{cname}.{fname}"]) == getattr(py, fname).offset, (cname, fname)
+
+
+def test_random_regular_generator_is_simple_and_regular():
+    net = random_regular(2000, 32, seed=1)
+    deg = np.diff(net.row_ptr.astype(np.int64))
+    assert (deg == 32).all()
+    owner = net.owner()
+    assert not (owner == net.col).any()                    # no self loops
+    for i in range(0, 2000, 97):                           # rows sorted, no duplicates
+        row = net.col[net.row_ptr[i]:net.row_ptr[i + 1]]
+        assert (np.diff(row.astype(np.int64)) > 0).all()
+    rev = net.rev()
+    assert (net.col[rev] == owner).all()                   # symmetric
+    assert (net.outbound + net.outbound[rev] == 1).all()   # exactly one initiator per connection
+    again = random_regular(2000, 32, seed=1)
+    assert (again.col == net.col).all() and (again.outbound == net.outbound).all()
+
+
+def _params():
+    tp = TopicScoreParams(TopicWeight=1, TimeInMeshQuantum=Second, InvalidMessageDeliveriesWeight=-1,
+                          InvalidMessageDeliveriesDecay=0.5)
+    return PeerScoreParams(AppSpecificScore=lambda p: 0.0, DecayInterval=Second, DecayToZero=0.01,
+                           Topics={"t": tp})
+
+
+def test_create_validates_before_touching_device():
+    p = _params()
+    p.DecayToZero = 2.0
+    with pytest.raises(ValueError, match="DecayToZero"):
+        Engine(p, PeerScoreThresholds())
+    with pytest.raises(ValueError, match="gossip threshold"):
+        Engine(_params(), PeerScoreThresholds(GossipThreshold=1))
+
+
+@pytest.mark.skipif(gpu_available(), reason="checks the no-device path")
+def test_create_without_device_fails_loudly():
+    from gsim.engine import GsimError
+    with pytest.raises(GsimError, match="no HIP device"):
+        Engine(_params(), PeerScoreThresholds())
