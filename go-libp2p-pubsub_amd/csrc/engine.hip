@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -20,8 +21,29 @@
 
 using namespace gsim;
 
+// Exact Go int64 division (truncation toward zero) of meshTime by a positive
+// TimeInMeshQuantum (score.go:287): an fp64 quotient estimate corrected by the
+// exact integer remainder.  Cheaper in VALU and registers than the generic
+// 64-bit division expansion; the result is identical for every input.
+__device__ __forceinline__ int64_t div_trunc_pos(int64_t n, int64_t d)
+{
+    const bool neg = n < 0;
+    const uint64_t un = neg ? (uint64_t)0 - (uint64_t)n : (uint64_t)n;
+    const uint64_t ud = (uint64_t)d;
+    uint64_t q = (uint64_t)((double)un / (double)ud);
+    // the estimate is within a few units of the true quotient; fix it exactly
+    while (q * ud > un) --q;
+    while (un - q * ud >= ud) ++q;
+    return neg ? -(int64_t)q : (int64_t)q;
+}
+
+__device__ __forceinline__ int64_t go_div(int64_t n, int64_t d)
+{
+    return d > 0 ? div_trunc_pos(n, d) : n / d;
+}
+
 // ---------------------------------------------------------------------------
-// Kernel 1: peerScore.refreshScores (score.go:504-565) fused with
+// Kernel 1:peerScore.refreshScores (score.go:504-565) fused with
 // peerScore.score (score.go:265-342).  One thread per observer->neighbour edge,
 // grid-stride; the topic loop reads the [T][E] arrays at t*E + e, so each
 // wave-instruction touches 64 consecutive records of one topic (coalesced).
@@ -87,7 +109,7 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
                 double ts = 0.0;
                 if (fl & GSIM_TF_IN_MESH) {                               // P1
                     double p1 = 0.0;
-                    if (tp->time_in_mesh_quantum_ns != 0) p1 = (double)(mt / tp->time_in_mesh_quantum_ns);
+                    if (tp->time_in_mesh_quantum_ns != 0) p1 = (double)go_div(mt, tp->time_in_mesh_quantum_ns);
                     if (p1 > tp->time_in_mesh_cap) p1 = tp->time_in_mesh_cap;
                     ts += p1 * tp->time_in_mesh_weight;
                 }
@@ -123,6 +145,150 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
             }
             a.score[e] = score;
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 1b (production path): the same computation as k_refresh_score,
+// restructured for memory-level parallelism.  A 256-thread block owns a tile
+// of 64 consecutive edges; wave w takes topics w, w+4, w+8, w+12 of the tile
+// and issues all of their loads before the first use, so each wave makes one
+// HBM round trip per tile instead of one per topic (the per-thread topic loop
+// above serializes on vmcnt, which on CDNA counts stores too).  Each topic's
+// weighted contribution ts*TopicWeight goes to LDS; wave 0 then adds them in
+// ascending topic order and finishes P5-P7, so the sum is bit-identical to
+// the reference order (score.go:274-341).
+constexpr int kTileEdges = 64;
+constexpr int kTopicsPerWavePass = 4;
+
+template <bool REFRESH, bool SCORE>
+__global__ __launch_bounds__(256) void k_refresh_score_tile(ScoreArgs a)
+{
+    extern __shared__ double s_contrib[];   // [T][64]
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t ntiles = (a.E + kTileEdges - 1) / kTileEdges;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t e = tile * kTileEdges + lane;
+        const bool valid = e < a.E;
+        const uint8_t st = valid ? a.estate[e] : 0;
+        const bool tracked = st & GSIM_ES_TRACKED;
+        const bool conn = st & GSIM_ES_CONNECTED;
+        const bool purge = REFRESH && tracked && !conn && a.now > a.expire[e];
+        const bool decay = REFRESH && tracked && conn;
+        const bool live = valid && tracked && !purge;
+
+        for (int t0 = wid; t0 < a.T; t0 += 4 * kTopicsPerWavePass) {
+            double f[kTopicsPerWavePass], md[kTopicsPerWavePass], fa[kTopicsPerWavePass], iv[kTopicsPerWavePass];
+            int64_t g[kTopicsPerWavePass];
+            uint8_t fl[kTopicsPerWavePass];
+#pragma unroll
+            for (int j = 0; j < kTopicsPerWavePass; ++j) {
+                const int t = t0 + 4 * j;
+                f[j] = md[j] = fa[j] = iv[j] = 0.0;
+                g[j] = 0;
+                fl[j] = 0;
+                if (t < a.T && live && a.tp[t].scored) {
+                    const int64_t i = (int64_t)t * a.E + e;
+                    f[j] = a.first[i];
+                    md[j] = a.meshd[i];
+                    fa[j] = a.fail[i];
+                    iv[j] = a.invalid[i];
+                    fl[j] = a.tflags[i];
+                    g[j] = decay ? a.graft[i] : (SCORE ? a.mtime[i] : 0);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kTopicsPerWavePass; ++j) {
+                const int t = t0 + 4 * j;
+                if (t >= a.T || !valid) continue;
+                const int64_t i = (int64_t)t * a.E + e;
+                if (purge) {
+                    a.first[i] = 0.0; a.meshd[i] = 0.0; a.fail[i] = 0.0; a.invalid[i] = 0.0;
+                    a.graft[i] = 0; a.mtime[i] = 0; a.tflags[i] = 0;
+                    continue;
+                }
+                const gsim_topic_score_params* tp = &a.tp[t];
+                if (!live || !tp->scored) continue;
+                double first = f[j], meshd = md[j], fail = fa[j], inval = iv[j];
+                uint8_t fj = fl[j];
+                int64_t mt = g[j];
+                if (decay) {
+                    double x;
+                    x = first * tp->first_message_deliveries_decay;  if (x < a.dtz) x = 0.0;
+                    if (x != first) { first = x; a.first[i] = x; }
+                    x = meshd * tp->mesh_message_deliveries_decay;   if (x < a.dtz) x = 0.0;
+                    if (x != meshd) { meshd = x; a.meshd[i] = x; }
+                    x = fail * tp->mesh_failure_penalty_decay;       if (x < a.dtz) x = 0.0;
+                    if (x != fail) { fail = x; a.fail[i] = x; }
+                    x = inval * tp->invalid_message_deliveries_decay; if (x < a.dtz) x = 0.0;
+                    if (x != inval) { inval = x; a.invalid[i] = x; }
+                    if (fj & GSIM_TF_IN_MESH) {
+                        mt = a.now - g[j];
+                        a.mtime[i] = mt;
+                        if (mt > tp->mesh_message_deliveries_activation_ns && !(fj & GSIM_TF_ACTIVE)) {
+                            fj |= GSIM_TF_ACTIVE;
+                            a.tflags[i] = fj;
+                        }
+                    }
+                }
+                if (SCORE) {
+                    double ts = 0.0;
+                    if (fj & GSIM_TF_IN_MESH) {                               // P1
+                        double p1 = 0.0;
+                        if (tp->time_in_mesh_quantum_ns != 0) p1 = (double)go_div(mt, tp->time_in_mesh_quantum_ns);
+                        if (p1 > tp->time_in_mesh_cap) p1 = tp->time_in_mesh_cap;
+                        ts += p1 * tp->time_in_mesh_weight;
+                    }
+                    ts += first * tp->first_message_deliveries_weight;         // P2
+                    if (fj & GSIM_TF_ACTIVE) {                                 // P3
+                        if (meshd < tp->mesh_message_deliveries_threshold) {
+                            const double deficit = tp->mesh_message_deliveries_threshold - meshd;
+                            const double p3 = deficit * deficit;
+                            ts += p3 * tp->mesh_message_deliveries_weight;
+                        }
+                    }
+                    ts += fail * tp->mesh_failure_penalty_weight;              // P3b
+                    const double p4 = inval * inval;                           // P4
+                    ts += p4 * tp->invalid_message_deliveries_weight;
+                    s_contrib[t * kTileEdges + lane] = ts * tp->topic_weight;
+                }
+            }
+        }
+        __syncthreads();
+        if (wid == 0 && valid) {
+            if (!tracked) {
+                if (SCORE) a.score[e] = 0.0;
+            } else if (purge) {                              // score.go:512-516
+                a.estate[e] = 0;
+                a.bp[e] = 0.0;
+                a.expire[e] = 0;
+                *a.purged = 1;
+                if (SCORE) a.score[e] = 0.0;
+            } else {
+                double bp = a.bp[e];
+                if (decay) {
+                    double x = bp * a.bp_decay;
+                    if (x < a.dtz) x = 0.0;
+                    if (x != bp) { bp = x; a.bp[e] = x; }
+                }
+                if (SCORE) {
+                    double score = 0.0;
+                    for (int32_t t = 0; t < a.T; ++t)
+                        if (a.tp[t].scored) score += s_contrib[t * kTileEdges + lane];
+                    if (a.topic_cap > 0 && score > a.topic_cap) score = a.topic_cap;
+                    const double p5 = a.p5[a.col[e]];                      // P5
+                    score += p5 * a.w5;
+                    score += a.p6[e] * a.w6;                               // P6
+                    if (bp > a.bp_thr) {                                   // P7
+                        const double excess = bp - a.bp_thr;
+                        const double p7 = excess * excess;
+                        score += p7 * a.w7;
+                    }
+                    a.score[e] = score;
+                }
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -186,7 +352,7 @@ __global__ __launch_bounds__(256) void k_fill_synthetic(ScoreArgs a, uint64_t se
             const u32x4 r = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), 0x5eed, 1, k0, k1);
             const u32x4 q = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), 0x5eed, 2, k0, k1);
             const bool in_mesh = r.x * inv < p_mesh;
-            uint8_t fl = in_mesh ? GSIM_TF_IN_MESH : 0;
+            uint8_t fl = in_mesh ? (GSIM_TF_IN_MESH | GSIM_TF_MESH) : 0;
             if (in_mesh && (r.y & 15) != 0) fl |= GSIM_TF_ACTIVE;
             a.tflags[i] = fl;
             a.graft[i] = in_mesh ? a.now - (int64_t)(r.z % 3600u) * 1000000000LL : 0;
@@ -200,6 +366,37 @@ __global__ __launch_bounds__(256) void k_fill_synthetic(ScoreArgs a, uint64_t se
         a.bp[e] = (b.x & 3) == 0 ? (double)(b.y % 200u) * 0.125 : 0.0;
         a.estate[e] = GSIM_ES_TRACKED | GSIM_ES_CONNECTED;
         a.expire[e] = 0;
+    }
+}
+
+// Aggregate state census (counts per category, see gsim_census in gsim.h).
+__global__ __launch_bounds__(256) void k_census(ScoreArgs a, unsigned long long* out)
+{
+    unsigned long long c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
+        const uint8_t st = a.estate[e];
+        if (!(st & GSIM_ES_TRACKED)) continue;
+        c[7] += 1;
+        if (!(st & GSIM_ES_CONNECTED)) continue;
+        for (int32_t t = 0; t < a.T; ++t) {
+            if (!a.tp[t].scored) continue;
+            const int64_t i = (int64_t)t * a.E + e;
+            const uint8_t fl = a.tflags[i];
+            c[0] += 1;
+            c[1] += (fl & GSIM_TF_IN_MESH) != 0;
+            c[2] += a.first[i] != 0.0;
+            c[3] += a.meshd[i] != 0.0;
+            c[4] += a.fail[i] != 0.0;
+            c[5] += a.invalid[i] != 0.0;
+            c[6] += (fl & GSIM_TF_MESH) != 0;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        unsigned long long v = c[k];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&out[k], v);
     }
 }
 
@@ -299,10 +496,33 @@ int launch_ip_colocation(gsim_handle* h)
     return hip_check(h, hipGetLastError(), "k_ip_colocation");
 }
 
+// GSIM_SCORE_KERNEL=thread selects the thread-per-edge variant (A/B only).
+static bool use_thread_kernel()
+{
+    static int v = -1;
+    if (v < 0) {
+        const char* s = std::getenv("GSIM_SCORE_KERNEL");
+        v = (s && std::strcmp(s, "thread") == 0) ? 1 : 0;
+    }
+    return v == 1;
+}
+
+template <bool REFRESH, bool SCORE>
+static void launch_score_kernel(gsim_handle* h, const ScoreArgs& a)
+{
+    if (use_thread_kernel()) {
+        hipLaunchKernelGGL((k_refresh_score<REFRESH, SCORE>), dim3(grid_for(h->e)), dim3(256), 0, h->stream, a);
+        return;
+    }
+    const int64_t tiles = (h->e + kTileEdges - 1) / kTileEdges;
+    const int grid = (int)std::min<int64_t>(std::max<int64_t>(tiles, 1), 256 * 16);
+    const size_t lds = sizeof(double) * kTileEdges * (size_t)std::max(1, h->t);
+    hipLaunchKernelGGL((k_refresh_score_tile<REFRESH, SCORE>), dim3(grid), dim3(256), lds, h->stream, a);
+}
+
 int launch_refresh_scores(gsim_handle* h, int64_t now)
 {
     ScoreArgs a = make_score_args(h, now);
-    const dim3 g(grid_for(h->e)), b(256);
     if (h->p6_dirty) {
         int rc = launch_ip_colocation(h);
         if (rc) return rc;
@@ -310,12 +530,12 @@ int launch_refresh_scores(gsim_handle* h, int64_t now)
     if (h->maybe_retained) {
         // a purge inside refresh changes the tracked set, so P6 must be
         // re-derived between decay and scoring (score.go:514 removeIPs).
-        hipLaunchKernelGGL((k_refresh_score<true, false>), g, b, 0, h->stream, a);
+        launch_score_kernel<true, false>(h, a);
         int rc = launch_ip_colocation(h);
         if (rc) return rc;
-        hipLaunchKernelGGL((k_refresh_score<false, true>), g, b, 0, h->stream, a);
+        launch_score_kernel<false, true>(h, a);
     } else {
-        hipLaunchKernelGGL((k_refresh_score<true, true>), g, b, 0, h->stream, a);
+        launch_score_kernel<true, true>(h, a);
     }
     return hip_check(h, hipGetLastError(), "k_refresh_score");
 }
@@ -327,7 +547,7 @@ int launch_compute_scores(gsim_handle* h)
         if (rc) return rc;
     }
     ScoreArgs a = make_score_args(h, 0);
-    hipLaunchKernelGGL((k_refresh_score<false, true>), dim3(grid_for(h->e)), dim3(256), 0, h->stream, a);
+    launch_score_kernel<false, true>(h, a);
     return hip_check(h, hipGetLastError(), "k_refresh_score<score>");
 }
 
@@ -645,6 +865,26 @@ int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now, double p_mes
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     return hip_check(h, e, "gsim_fill_synthetic");
+}
+
+int gsim_census(gsim_handle* h, int64_t* out8)
+{
+    GSIM_ENTER(h);
+    GSIM_NEED_GRAPH(h);
+    if (!out8) return GSIM_EINVAL;
+    unsigned long long* d = nullptr;
+    hipError_t e = hipMalloc((void**)&d, 8 * sizeof(unsigned long long));
+    if (e != hipSuccess) return hip_check(h, e, "hipMalloc census");
+    e = hipMemsetAsync(d, 0, 8 * sizeof(unsigned long long), h->stream);
+    ScoreArgs a = make_score_args(h, 0);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_census, dim3(grid_for(h->e, 256, 4096)), dim3(256), 0, h->stream, a, d);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(out8, d, 8 * sizeof(int64_t), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    (void)hipFree(d);
+    return hip_check(h, e, "gsim_census");
 }
 
 int gsim_read_scores(gsim_handle* h, double* out)

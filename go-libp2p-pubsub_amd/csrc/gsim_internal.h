@@ -11,7 +11,7 @@
 namespace gsim {
 
 constexpr int GSIM_MAX_TOPICS = 64;   // subscriptions are a u64 bitmask
-constexpr int kEvents = 16;
+constexpr int kEvents = 512;
 
 struct ScoreArgs {
     int64_t E;

@@ -1,24 +1,472 @@
-// heartbeat.hip — heartbeat mesh maintenance and message delivery state.
+// heartbeat.hip — GossipSub heartbeat mesh maintenance and control handling.
+//
+// gossipsub.go:1345-1606 runs once per node per heartbeat over Go maps.  Here
+// one 64-lane wavefront owns one observer: lane l holds the observer's l-th
+// connection (its score snapshot, outbound flag, neighbour subscriptions),
+// so every per-topic set operation of the reference (mesh size, filtered
+// candidate lists, getPeers' shuffle+truncate, the Dhi score sort, the
+// opportunistic median) becomes a wave ballot, popcount or keyed
+// min-reduction with no memory traffic beyond the row's own records.
+// Topics are processed in ascending order.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
 
 #include "gsim.h"
 #include "gsim_internal.h"
+#include "philox.h"
+
+using namespace gsim;
 
 struct Extra {
-    int unused = 0;
+    uint8_t* d_ctl = nullptr;   // [2][T][E] control inbox by round parity
+    uint32_t max_degree = 0;
+    uint64_t seed = 0x9E3779B97F4A7C15ull;
 };
+
+struct HbArgs {
+    int64_t N, E;
+    int32_t T;
+    const uint32_t *row_ptr, *col, *rev;
+    const uint64_t* sub;
+    const uint8_t* outbound;
+    const uint8_t* estate;
+    const double* score;
+    const gsim_topic_score_params* tp;
+    uint8_t* tflags;
+    int64_t* backoff;
+    double *meshd, *fail, *bp;
+    int64_t *graft, *mtime;
+    uint8_t* ctl_in;    // inbox this phase reads (round parity)
+    uint8_t* ctl_out;   // inbox this phase writes
+    uint64_t tick;
+    int64_t now;
+    uint64_t seed;
+    int32_t D, Dlo, Dhi, Dscore, Dout, opp_peers;
+    uint64_t opp_ticks;
+    int64_t prune_backoff, graft_flood;
+    double opp_threshold;
+};
+
+namespace {
+
+constexpr int64_t kSecond = 1000000000LL;
+constexpr int64_t kBackoffSlack = 2 * kSecond;   // 2*GossipSubHeartbeatInterval (gossipsub.go:1638)
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(v, off, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t hb_key(const HbArgs& a, uint32_t obs, int32_t t, uint32_t purpose, uint32_t col,
+                                           uint32_t pos)
+{
+    return select_key(a.seed, (uint32_t)a.tick, obs, (uint32_t)t, purpose, col, pos);
+}
+
+// getPeers (gossipsub.go:1908-1928) restated: among candidate lanes keep the
+// `count` with the smallest Philox key (all of them if count <= 0 or fewer).
+__device__ bool select_smallest(const HbArgs& a, bool cand, int count, uint32_t obs, int32_t t, uint32_t purpose,
+                                uint32_t col, uint32_t pos)
+{
+    const uint64_t m = ballot(cand);
+    const int n = __popcll(m);
+    if (n == 0) return false;
+    if (count <= 0 || n <= count) return cand;
+    uint64_t key = cand ? hb_key(a, obs, t, purpose, col, pos) : ~0ull;
+    bool sel = false;
+    for (int c = 0; c < count; ++c) {
+        const uint64_t mn = wave_min_u64(key);
+        if (key == mn) { sel = true; key = ~0ull; }
+    }
+    return sel;
+}
+
+// peerScore.Graft / Prune on one edge-topic record (score.go:649-691)
+__device__ __forceinline__ void stats_graft(const HbArgs& a, bool tracked, bool scored, int64_t i, uint8_t& fl)
+{
+    if (!tracked || !scored) return;
+    fl = (uint8_t)((fl | GSIM_TF_IN_MESH) & ~GSIM_TF_ACTIVE);
+    a.graft[i] = a.now;
+    a.mtime[i] = 0;
+}
+
+__device__ __forceinline__ void stats_prune(const HbArgs& a, bool tracked, bool scored, double thr, int64_t i,
+                                            uint8_t& fl)
+{
+    if (!tracked || !scored) return;
+    if (fl & GSIM_TF_ACTIVE) {
+        const double md = a.meshd[i];
+        if (md < thr) {
+            const double deficit = thr - md;
+            a.fail[i] = a.fail[i] + deficit * deficit;
+        }
+    }
+    fl &= (uint8_t)~GSIM_TF_IN_MESH;
+}
+
+}  // namespace
+
+// One wavefront = one observer's heartbeat (gossipsub.go:1345-1557).
+__global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
+{
+    __shared__ uint8_t s_plst[4][64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int64_t obs = (int64_t)blockIdx.x * 4 + wid; obs < a.N; obs += (int64_t)gridDim.x * 4) {
+        const uint32_t b = a.row_ptr[obs];
+        const int deg = (int)(a.row_ptr[obs + 1] - b);
+        const bool valid = lane < deg;
+        const uint32_t e = b + (uint32_t)lane;
+        const uint32_t col = valid ? a.col[e] : 0u;
+        const uint8_t est = valid ? a.estate[e] : 0;
+        const bool tracked = est & GSIM_ES_TRACKED;
+        const bool conn = est & GSIM_ES_CONNECTED;
+        const bool outb = valid && a.outbound[e];
+        const double S = valid ? a.score[e] : 0.0;
+        const uint64_t subj = valid ? a.sub[col] : 0ull;
+        const uint64_t subi = a.sub[obs];
+        const uint64_t outmask = ballot(outb);
+
+        // clearBackoff every 15 ticks (gossipsub.go:1627-1646)
+        if (a.tick % 15 == 0 && valid) {
+            for (int32_t t = 0; t < a.T; ++t) {
+                const int64_t i = (int64_t)t * a.E + e;
+                const int64_t bo = a.backoff[i];
+                if (bo != 0 && bo + kBackoffSlack < a.now) a.backoff[i] = 0;
+            }
+        }
+
+        for (int32_t t = 0; t < a.T; ++t) {
+            if (!((subi >> t) & 1ull)) continue;           // not joined
+            const gsim_topic_score_params* tp = &a.tp[t];
+            const bool scored = tp->scored != 0;
+            const double thr = tp->mesh_message_deliveries_threshold;
+            const int64_t i = (int64_t)t * a.E + e;
+            uint8_t fl = valid ? a.tflags[i] : 0;
+            const uint8_t fl0 = fl;
+            int64_t bo = valid ? a.backoff[i] : 0;
+            const int64_t bo0 = bo;
+            const bool tpeer = valid && conn && ((subj >> t) & 1ull);
+            bool m = valid && (fl & GSIM_TF_MESH);
+            uint8_t ctl = 0;
+            const uint32_t pos = (uint32_t)lane;
+
+            auto prune = [&]() {
+                stats_prune(a, tracked, scored, thr, i, fl);
+                fl &= (uint8_t)~GSIM_TF_MESH;
+                m = false;
+                const int64_t ex = a.now + a.prune_backoff;
+                if (bo < ex) bo = ex;
+                ctl |= GSIM_CTL_PRUNE;
+            };
+            auto graft = [&]() {
+                stats_graft(a, tracked, scored, i, fl);
+                fl |= GSIM_TF_MESH;
+                m = true;
+                ctl |= GSIM_CTL_GRAFT;
+            };
+
+            // drop all peers with negative score (1403-1410)
+            if (m && S < 0) prune();
+
+            // too few peers: graft up to D (1412-1427)
+            int l = __popcll(ballot(m));
+            if (l < a.Dlo) {
+                const bool cand = tpeer && !m && bo == 0 && S >= 0;
+                if (select_smallest(a, cand, a.D - l, (uint32_t)obs, t, P_GRAFT_DLO, col, pos)) graft();
+            }
+
+            // too many peers: keep Dscore best + random, Dout outbound (1429-1490)
+            l = __popcll(ballot(m));
+            if (l > a.Dhi) {
+                const uint64_t mm = ballot(m);
+                const uint64_t k1 = m ? hb_key(a, (uint32_t)obs, t, P_PRUNE_SHUF1, col, pos) : ~0ull;
+                int rank1 = 0;
+                for (int q = 0; q < 64; ++q) {
+                    const double sq = __shfl(S, q, 64);
+                    const uint64_t kq = __shfl(k1, q, 64);
+                    if (((mm >> q) & 1ull) && (sq > S || (sq == S && kq < k1))) ++rank1;
+                }
+                const int ds = a.Dscore < l ? a.Dscore : l;
+                const bool tail = m && rank1 >= ds;
+                const uint64_t k2 = tail ? hb_key(a, (uint32_t)obs, t, P_PRUNE_SHUF2, col, pos) : ~0ull;
+                int p = rank1;
+                if (tail) {
+                    p = ds;
+                    for (int q = 0; q < 64; ++q) {
+                        const uint64_t kq = __shfl(k2, q, 64);
+                        if (kq < k2) ++p;   // non-tail lanes hold ~0 and never count
+                    }
+                }
+                if (m) s_plst[wid][p] = (uint8_t)lane;
+                // the LDS slice is private to this wave: a wave-scope fence
+                // orders the lanes' writes before lane 0 reads them (other waves
+                // of the block may be on a different branch, so no block barrier)
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                uint64_t prune_mask = 0;
+                if (lane == 0) {
+                    uint8_t* pl = s_plst[wid];
+                    int outbound = 0;
+                    for (int q = 0; q < a.D && q < l; ++q) outbound += (int)((outmask >> pl[q]) & 1ull);
+                    auto rotate = [&](int idx) {
+                        const uint8_t v = pl[idx];
+                        for (int j = idx; j > 0; --j) pl[j] = pl[j - 1];
+                        pl[0] = v;
+                    };
+                    if (outbound < a.Dout) {
+                        if (outbound > 0) {
+                            int ihave = outbound;
+                            for (int q = 1; q < a.D && ihave > 0; ++q)
+                                if ((outmask >> pl[q]) & 1ull) { rotate(q); --ihave; }
+                        }
+                        int ineed = a.Dout - outbound;
+                        for (int q = a.D; q < l && ineed > 0; ++q)
+                            if ((outmask >> pl[q]) & 1ull) { rotate(q); --ineed; }
+                    }
+                    for (int q = a.D; q < l; ++q) prune_mask |= 1ull << pl[q];
+                }
+                prune_mask = __shfl(prune_mask, 0, 64);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                if ((prune_mask >> lane) & 1ull) prune();
+            }
+
+            // enough outbound peers? (1492-1518)
+            l = __popcll(ballot(m));
+            if (l >= a.Dlo) {
+                const int ob = __popcll(ballot(m && outb));
+                if (ob < a.Dout) {
+                    const bool cand = tpeer && !m && bo == 0 && outb && S >= 0;
+                    if (select_smallest(a, cand, a.Dout - ob, (uint32_t)obs, t, P_GRAFT_DOUT, col, pos)) graft();
+                }
+            }
+
+            // opportunistic grafting (1520-1552)
+            l = __popcll(ballot(m));
+            if (a.opp_ticks && a.tick % a.opp_ticks == 0 && l > 1) {
+                const uint64_t mm = ballot(m);
+                int rank = 0;
+                for (int q = 0; q < 64; ++q) {
+                    const double sq = __shfl(S, q, 64);
+                    if (((mm >> q) & 1ull) && (sq < S || (sq == S && q < lane))) ++rank;
+                }
+                const uint64_t at = ballot(m && rank == l / 2);
+                const double median = __shfl(S, (int)__ffsll((long long)at) - 1, 64);
+                if (median < a.opp_threshold) {
+                    const bool cand = tpeer && !m && bo == 0 && S > median;
+                    if (select_smallest(a, cand, a.opp_peers, (uint32_t)obs, t, P_GRAFT_OPP, col, pos)) graft();
+                }
+            }
+
+            if (valid) {
+                if (fl != fl0) a.tflags[i] = fl;
+                if (bo != bo0) a.backoff[i] = bo;
+                if (ctl) {
+                    const int64_t r = (int64_t)t * a.E + a.rev[e];
+                    a.ctl_out[r] = (uint8_t)(a.ctl_out[r] | ctl);
+                }
+            }
+        }
+    }
+}
+
+// HandleRPC control processing for every receiver: handleGraft
+// (gossipsub.go:741-837) and handlePrune (839-871), senders in row order.
+// The control records of one (receiver, topic) are usually few, so they are
+// walked with a wave-uniform loop over the set bits of a ballot; the mesh size
+// is carried in a scalar.
+__global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int64_t rcv = (int64_t)blockIdx.x * 4 + wid; rcv < a.N; rcv += (int64_t)gridDim.x * 4) {
+        const uint32_t b = a.row_ptr[rcv];
+        const int deg = (int)(a.row_ptr[rcv + 1] - b);
+        const bool valid = lane < deg;
+        const uint32_t e = b + (uint32_t)lane;
+        const uint64_t subr = a.sub[rcv];
+        for (int32_t t = 0; t < a.T; ++t) {
+            const int64_t i = (int64_t)t * a.E + e;
+            const uint8_t c = valid ? a.ctl_in[i] : 0;
+            uint64_t pending = ballot(c != 0);
+            if (!pending) continue;
+            if (c) a.ctl_in[i] = 0;
+            if (!((subr >> t) & 1ull)) continue;            // unknown topic: ignored
+            const gsim_topic_score_params* tp = &a.tp[t];
+            const bool scored = tp->scored != 0;
+            const double thr = tp->mesh_message_deliveries_threshold;
+            uint8_t fl = valid ? a.tflags[i] : 0;
+            int mesh = __popcll(ballot(valid && (fl & GSIM_TF_MESH)));
+            while (pending) {
+                const int q = __ffsll((long long)pending) - 1;
+                pending &= pending - 1;
+                int delta = 0;
+                if (lane == q) {
+                    const uint8_t est = a.estate[e];
+                    const bool tracked = est & GSIM_ES_TRACKED;
+                    int64_t bo = a.backoff[i];
+                    const int64_t bo0 = bo;
+                    uint8_t reply = 0;
+                    if ((c & GSIM_CTL_GRAFT) && !(fl & GSIM_TF_MESH)) {
+                        if (bo != 0 && a.now < bo) {
+                            // GRAFT while backing off: P7 penalty (+1 more under the flood cutoff)
+                            if (tracked) {
+                                double x = a.bp[e] + 1.0;
+                                if (a.now < bo + (a.graft_flood - a.prune_backoff)) x = x + 1.0;
+                                a.bp[e] = x;
+                            }
+                            const int64_t ex = a.now + a.prune_backoff;
+                            if (bo < ex) bo = ex;
+                            reply = GSIM_CTL_PRUNE;
+                        } else if (a.score[e] < 0) {
+                            reply = GSIM_CTL_PRUNE;
+                            const int64_t ex = a.now + a.prune_backoff;
+                            if (bo < ex) bo = ex;
+                        } else if (mesh >= a.Dhi && !a.outbound[e]) {
+                            reply = GSIM_CTL_PRUNE;
+                            const int64_t ex = a.now + a.prune_backoff;
+                            if (bo < ex) bo = ex;
+                        } else {
+                            stats_graft(a, tracked, scored, i, fl);
+                            fl |= GSIM_TF_MESH;
+                            delta += 1;
+                        }
+                    }
+                    if (c & GSIM_CTL_PRUNE) {
+                        if (fl & GSIM_TF_MESH) delta -= 1;
+                        stats_prune(a, tracked, scored, thr, i, fl);
+                        fl &= (uint8_t)~GSIM_TF_MESH;
+                        const int64_t secs = a.prune_backoff / kSecond;
+                        const int64_t ex = a.now + (secs > 0 ? secs * kSecond : a.prune_backoff);
+                        if (bo < ex) bo = ex;
+                    }
+                    a.tflags[i] = fl;
+                    if (bo != bo0) a.backoff[i] = bo;
+                    if (reply) {
+                        const int64_t r = (int64_t)t * a.E + a.rev[e];
+                        a.ctl_out[r] = (uint8_t)(a.ctl_out[r] | reply);
+                    }
+                }
+                mesh += __shfl(delta, q, 64);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
 
 int alloc_extra(gsim_handle* h)
 {
     free_extra(h);
     h->x = new Extra();
+    if (h->e == 0) return GSIM_OK;
+    const size_t bytes = 2 * (size_t)h->e * (size_t)std::max(1, h->t);
+    hipError_t e = hipMalloc((void**)&h->x->d_ctl, bytes);
+    if (e != hipSuccess) return hip_check(h, e, "hipMalloc ctl");
+    h->bytes_allocated += bytes;
+    e = hipMemsetAsync(h->x->d_ctl, 0, bytes, h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "memset ctl");
+    std::vector<uint32_t> rp((size_t)h->n + 1);
+    e = hipMemcpy(rp.data(), h->d_row_ptr, sizeof(uint32_t) * rp.size(), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_check(h, e, "row_ptr readback");
+    uint32_t md = 0;
+    for (int64_t i = 0; i < h->n; ++i) md = std::max(md, rp[(size_t)i + 1] - rp[(size_t)i]);
+    h->x->max_degree = md;
     return GSIM_OK;
 }
 
 void free_extra(gsim_handle* h)
 {
+    if (!h->x) return;
+    if (h->x->d_ctl) (void)hipFree(h->x->d_ctl);
     delete h->x;
     h->x = nullptr;
 }
 
-bool extra_field_ref(gsim_handle*, int32_t, gsim::FieldRef*) { return false; }
+bool extra_field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r)
+{
+    if (f == GSIM_F_CTL && h->x && h->x->d_ctl) {
+        *r = {h->x->d_ctl, 2 * (size_t)h->e * (size_t)std::max(1, h->t)};
+        return true;
+    }
+    return false;
+}
+
+static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parity_in)
+{
+    HbArgs a{};
+    a.N = h->n; a.E = h->e; a.T = h->t;
+    a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.rev = h->d_rev; a.sub = h->d_sub;
+    a.outbound = h->d_outbound; a.estate = h->d_estate; a.score = h->d_score; a.tp = h->d_tp;
+    a.tflags = h->d_tflags; a.backoff = h->d_backoff; a.meshd = h->d_meshd; a.fail = h->d_fail; a.bp = h->d_bp;
+    a.graft = h->d_graft; a.mtime = h->d_mtime;
+    const size_t TE = (size_t)h->e * (size_t)std::max(1, h->t);
+    a.ctl_in = h->x->d_ctl + (size_t)(parity_in & 1) * TE;
+    a.ctl_out = h->x->d_ctl + (size_t)((parity_in + 1) & 1) * TE;
+    a.tick = tick; a.now = now; a.seed = h->x->seed;
+    a.D = h->gp.d; a.Dlo = h->gp.dlo; a.Dhi = h->gp.dhi; a.Dscore = h->gp.dscore; a.Dout = h->gp.dout;
+    a.opp_peers = h->gp.opportunistic_graft_peers; a.opp_ticks = h->gp.opportunistic_graft_ticks;
+    a.prune_backoff = h->gp.prune_backoff_ns; a.graft_flood = h->gp.graft_flood_threshold_ns;
+    a.opp_threshold = h->th.opportunistic_graft_threshold;
+    return a;
+}
+
+static int grid_rows(int64_t n)
+{
+    int64_t g = (n + 3) / 4;
+    return (int)std::min<int64_t>(std::max<int64_t>(g, 1), 65536);
+}
+
+static int check_degree(gsim_handle* h)
+{
+    if (h->x->max_degree > 64) {
+        h->err = "heartbeat kernels support rows of at most 64 connections in this build";
+        return GSIM_ERANGE;
+    }
+    return GSIM_OK;
+}
+
+extern "C" {
+
+int gsim_set_seed(gsim_handle* h, uint64_t seed)
+{
+    if (!h || !h->x) return GSIM_EINVAL;
+    h->x->seed = seed;
+    return GSIM_OK;
+}
+
+int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
+{
+    if (!h) return GSIM_EINVAL;
+    if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
+    if (h->e == 0 || !h->x) { h->err = "no graph loaded"; return GSIM_ESTATE; }
+    int rc = check_degree(h);
+    if (rc) return rc;
+    // heartbeat output goes to the parity-0 inbox, read by control round 0
+    HbArgs a = make_hb_args(h, tick, now, 1);
+    hipLaunchKernelGGL(k_heartbeat, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a);
+    return hip_check(h, hipGetLastError(), "k_heartbeat");
+}
+
+int gsim_handle_control(gsim_handle* h, int32_t round, int64_t now)
+{
+    if (!h) return GSIM_EINVAL;
+    if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
+    if (h->e == 0 || !h->x) { h->err = "no graph loaded"; return GSIM_ESTATE; }
+    int rc = check_degree(h);
+    if (rc) return rc;
+    HbArgs a = make_hb_args(h, 0, now, round & 1);
+    hipLaunchKernelGGL(k_handle_control, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a);
+    return hip_check(h, hipGetLastError(), "k_handle_control");
+}
+
+}  // extern "C"

@@ -22,10 +22,15 @@ GSIM_ERANGE = -34
 GSIM_ESTATE = -71
 
 (F_FIRST, F_MESHD, F_FAIL, F_INVALID, F_GRAFT_TIME, F_MESH_TIME, F_TFLAGS, F_BP, F_ESTATE,
- F_EXPIRE, F_P6, F_SCORE, F_BACKOFF) = range(13)
+ F_EXPIRE, F_P6, F_SCORE, F_BACKOFF, F_CTL) = range(14)
 
 TF_IN_MESH = 0x01
 TF_ACTIVE = 0x02
+TF_MESH = 0x04
+CTL_GRAFT = 0x01
+CTL_PRUNE = 0x02
+CTL_NOPX = 0x04
+CTL_IHAVE = 0x08
 ES_TRACKED = 0x01
 ES_CONNECTED = 0x02
 
@@ -114,6 +119,10 @@ SIGNATURES = [
     ("gsim_synchronize", c_int32, [c_void_p]),
     ("gsim_gen_random_regular", c_int32, [c_int64, c_int32, c_uint64, c_void_p, c_void_p, c_void_p]),
     ("gsim_fill_synthetic", c_int32, [c_void_p, c_uint64, c_int64, c_double]),
+    ("gsim_set_seed", c_int32, [c_void_p, c_uint64]),
+    ("gsim_census", c_int32, [c_void_p, c_void_p]),
+    ("gsim_heartbeat", c_int32, [c_void_p, c_uint64, c_int64]),
+    ("gsim_handle_control", c_int32, [c_void_p, c_int32, c_int64]),
 ]
 
 _lib = None

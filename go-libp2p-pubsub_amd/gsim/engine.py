@@ -20,10 +20,11 @@ _FIELD_DTYPES = {
     _abi.F_FIRST: np.float64, _abi.F_MESHD: np.float64, _abi.F_FAIL: np.float64, _abi.F_INVALID: np.float64,
     _abi.F_GRAFT_TIME: np.int64, _abi.F_MESH_TIME: np.int64, _abi.F_TFLAGS: np.uint8, _abi.F_BP: np.float64,
     _abi.F_ESTATE: np.uint8, _abi.F_EXPIRE: np.int64, _abi.F_P6: np.float64, _abi.F_SCORE: np.float64,
-    _abi.F_BACKOFF: np.int64,
+    _abi.F_BACKOFF: np.int64, _abi.F_CTL: np.uint8,
 }
 TOPIC_FIELDS = {_abi.F_FIRST, _abi.F_MESHD, _abi.F_FAIL, _abi.F_INVALID, _abi.F_GRAFT_TIME,
                 _abi.F_MESH_TIME, _abi.F_TFLAGS, _abi.F_BACKOFF}
+PARITY_TOPIC_FIELDS = {_abi.F_CTL}
 
 
 class GsimError(RuntimeError):
@@ -186,7 +187,28 @@ class Engine:
     # -- raw state ----------------------------------------------------------------
     def field_shape(self, f: int):
         e = self.net.e
+        if f in PARITY_TOPIC_FIELDS:
+            return (2, max(1, len(self.topics)), e)
         return (max(1, len(self.topics)), e) if f in TOPIC_FIELDS else (e,)
+
+    # -- heartbeat / control ------------------------------------------------------
+    def census(self) -> dict:
+        out = np.zeros(8, dtype=np.int64)
+        self._check(self.lib.gsim_census(self.h, _ptr(out)))
+        keys = ["records", "in_mesh", "nz_first", "nz_meshd", "nz_fail", "nz_invalid", "mesh_links",
+                "tracked_edges"]
+        return {k: int(v) for k, v in zip(keys, out)}
+
+    def set_seed(self, seed: int):
+        self._check(self.lib.gsim_set_seed(self.h, int(seed)))
+
+    def heartbeat(self, tick: int, now: int):
+        """GossipSubRouter.heartbeat for every observer (gossipsub.go:1345-1606)."""
+        self._check(self.lib.gsim_heartbeat(self.h, int(tick), int(now)))
+
+    def handle_control(self, rnd: int, now: int):
+        """handleGraft/handlePrune for the inbox of control round `rnd`."""
+        self._check(self.lib.gsim_handle_control(self.h, int(rnd), int(now)))
 
     def read(self, f: int) -> np.ndarray:
         out = np.empty(self.field_shape(f), dtype=_FIELD_DTYPES[f])

@@ -206,6 +206,33 @@ int gsim_compute_scores(gsim_handle* h);
  * each observer's neighbour IPs). */
 int gsim_compute_ip_colocation(gsim_handle* h);
 
+/* Seed of the Philox stream that replaces the reference's global math/rand
+ * (gossipsub.go:1954-1973, gossip_tracer.go:53). */
+int gsim_set_seed(gsim_handle* h, uint64_t seed);
+
+/* GossipSubRouter.heartbeat (gossipsub.go:1345-1606) for every observer at
+ * heartbeat tick `tick` (heartbeatTicks after its increment, so the first
+ * heartbeat is tick 1) and virtual time now_ns: clearBackoff every 15 ticks,
+ * per joined topic in ascending order: negative-score prune, Dlo graft, Dhi
+ * score/random prune with the Dout rotation, Dout top-up, opportunistic graft
+ * every OpportunisticGraftTicks; Graft/Prune traced into the score counters.
+ * Uses the current score snapshot as the heartbeat's score cache
+ * (gossipsub.go:1375-1383): call gsim_refresh_scores first.  GRAFT/PRUNE
+ * records land in the receivers' control inbox for round 0. */
+int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now_ns);
+/* Control-message round: every receiver handles the GRAFT/PRUNE records in
+ * its inbox for `round` (handleGraft gossipsub.go:741-837, handlePrune
+ * 839-871), senders in ascending peer order; PRUNE replies land in the inbox
+ * of round+1. */
+int gsim_handle_control(gsim_handle* h, int32_t round, int64_t now_ns);
+
+/* Aggregate census of the state (the network-wide analogue of the
+ * reference's score inspection, score.go:448-500): out8 = {connected scored
+ * edge-topic records, of those inMesh, non-zero firstMessageDeliveries,
+ * non-zero meshMessageDeliveries, non-zero meshFailurePenalty, non-zero
+ * invalidMessageDeliveries, router mesh links, tracked edges}. */
+int gsim_census(gsim_handle* h, int64_t* out8);
+
 /* Copy the score snapshot (E doubles, edge order) to host. */
 int gsim_read_scores(gsim_handle* h, double* out);
 
@@ -224,11 +251,18 @@ typedef enum gsim_field {
     GSIM_F_P6,            /* f64 [E]    ipColocationFactor value        */
     GSIM_F_SCORE,         /* f64 [E]    score snapshot                  */
     GSIM_F_BACKOFF,       /* i64 [T][E] prune backoff expiry, 0 = none gossipsub.go:432 */
+    GSIM_F_CTL,           /* u8 [2][T][E] control inbox by round parity (receiver's edge) */
     GSIM_F__COUNT
 } gsim_field;
 
-#define GSIM_TF_IN_MESH   0x01u
-#define GSIM_TF_ACTIVE    0x02u
+#define GSIM_TF_IN_MESH   0x01u  /* topicStats.inMesh (score.go:39)               */
+#define GSIM_TF_ACTIVE    0x02u  /* topicStats.meshMessageDeliveriesActive         */
+#define GSIM_TF_MESH      0x04u  /* router membership: gs.mesh[topic][p] (gossipsub.go:424) */
+/* control inbox bits (GSIM_F_CTL), one byte per [parity][topic][receiver edge] */
+#define GSIM_CTL_GRAFT    0x01u  /* ControlGraft  (pb/rpc.proto) */
+#define GSIM_CTL_PRUNE    0x02u  /* ControlPrune with Backoff = PruneBackoff/1s */
+#define GSIM_CTL_NOPX     0x04u  /* prune sent without peer exchange (noPX) */
+#define GSIM_CTL_IHAVE    0x08u  /* ControlIHave for this topic */
 #define GSIM_ES_TRACKED   0x01u
 #define GSIM_ES_CONNECTED 0x02u
 
@@ -238,7 +272,7 @@ int gsim_read_field(gsim_handle* h, int32_t field, void* dst, size_t bytes);
 int gsim_write_field(gsim_handle* h, int32_t field, const void* src, size_t bytes);
 
 /* ---- device timing on the engine's own stream (bench/profiling) -------- */
-/* Record HIP event `slot` (0..15) on the engine stream. */
+/* Record HIP event `slot` (0..511) on the engine stream. */
 int gsim_event_record(gsim_handle* h, int32_t slot);
 /* Milliseconds between two recorded events (synchronizes on `to`). */
 int gsim_event_elapsed(gsim_handle* h, int32_t from, int32_t to, float* ms);

@@ -55,7 +55,19 @@ typedef struct orc_net {
     const gsim_topic_score_params* tp;   /* [T] */
     const gsim_thresholds*         th;
     const gsim_gossipsub_params*   gp;
+    uint8_t* ctl;              /* [2][T][E] control inbox by round parity */
 } orc_net;
+
+/* ---- gossipsub.go heartbeat / control handling (oracle_net.c) ----------- */
+/* One heartbeat (gossipsub.go:1345-1606) for every observer at tick `tick`
+ * (heartbeatTicks after the increment) and virtual time now; mesh
+ * maintenance uses the score snapshot s->score (the heartbeat's lazy score
+ * cache, gossipsub.go:1375-1383).  GRAFT/PRUNE go to ctl[tick parity 0]. */
+void orc_heartbeat(orc_net* s, uint64_t tick, int64_t now, uint64_t seed);
+/* HandleRPC control processing (handleGraft gossipsub.go:741-837, handlePrune
+ * 839-871) of every receiver for the inbox of `round` (parity round&1);
+ * PRUNE replies go to parity (round+1)&1.  Returns #records handled. */
+int64_t orc_handle_control(orc_net* s, int32_t round, int64_t now);
 
 /* ---- score.go ---------------------------------------------------------- */
 void   orc_refresh_scores(orc_net* s, int64_t now);              /* score.go:504-565 */

@@ -1,0 +1,326 @@
+/*
+ * oracle_net.c — network-level restatement of the GossipSub heartbeat and
+ * control handlers.  TEST INFRASTRUCTURE (see oracle.h).
+ *
+ * Every observer runs gossipsub.go's heartbeat (1345-1606) on its own row of
+ * the CSR graph.  The reference's random choices (shufflePeers, getPeers;
+ * gossipsub.go:1908-1973) are restated as "order by a Philox key" so the
+ * choice is reproducible; sort.Slice ties are broken by that
+ * key.  Observers are independent within a phase, so the OpenMP split over
+ * observers gives identical results.
+ */
+#include "oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#define TF_IN_MESH GSIM_TF_IN_MESH
+#define TF_MESH    GSIM_TF_MESH
+#define ES_TRACKED GSIM_ES_TRACKED
+#define ES_CONN    GSIM_ES_CONNECTED
+
+enum { P_GRAFT_DLO = 1, P_PRUNE_SHUF1 = 2, P_PRUNE_SHUF2 = 3, P_GRAFT_DOUT = 4, P_GRAFT_OPP = 5 };
+
+static const int64_t kSecond = 1000000000LL;
+/* clearBackoff adds 2*GossipSubHeartbeatInterval — the package default
+ * (gossipsub.go:44), not params.HeartbeatInterval (gossipsub.go:1638). */
+static const int64_t kBackoffSlack = 2 * 1000000000LL;
+
+typedef struct cand { uint64_t key; uint32_t e; double score; } cand;
+
+static uint64_t okey(uint64_t seed, uint64_t tick, uint32_t obs, int32_t topic, uint32_t purpose, uint32_t item,
+                     uint32_t pos)
+{
+    uint32_t ctr[4] = {(uint32_t)tick, obs, ((uint32_t)topic << 8) | purpose, item};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t out[4];
+    orc_philox4x32_10(ctr, key, out);
+    return ((uint64_t)out[0] << 32) | pos;
+}
+
+static int cmp_key(const void* a, const void* b)
+{
+    uint64_t x = ((const cand*)a)->key, y = ((const cand*)b)->key;
+    return x < y ? -1 : x > y;
+}
+
+typedef struct hb {
+    orc_net* s;
+    uint32_t i, b, en;
+    int32_t t;
+    uint64_t tick, seed;
+    int64_t now;
+    uint8_t* out;            /* inbox buffer the replies/heartbeat messages go to */
+} hb;
+
+static inline int64_t ti(const hb* h, uint32_t e) { return (int64_t)h->t * h->s->e + e; }
+static inline int in_mesh(const hb* h, uint32_t e) { return (h->s->tflags[ti(h, e)] & TF_MESH) != 0; }
+static inline int has_backoff(const hb* h, uint32_t e) { return h->s->backoff[ti(h, e)] != 0; }
+static inline int topic_peer(const hb* h, uint32_t e)
+{
+    /* gs.p.topics[topic]: connected peers that announced the subscription */
+    return (h->s->estate[e] & ES_CONN) && ((h->s->sub[h->s->col[e]] >> h->t) & 1u);
+}
+
+static int mesh_count(const hb* h)
+{
+    int c = 0;
+    for (uint32_t e = h->b; e < h->en; ++e) c += in_mesh(h, e);
+    return c;
+}
+
+/* doAddBackoff, gossipsub.go:881-891: keep the later expiry. */
+static void do_add_backoff(hb* h, uint32_t e, int64_t interval)
+{
+    int64_t expire = h->now + interval;
+    int64_t* bo = &h->s->backoff[ti(h, e)];
+    if (*bo < expire) *bo = expire;
+}
+
+static void send_ctl(hb* h, uint32_t e, uint8_t bits)
+{
+    h->out[(int64_t)h->t * h->s->e + h->s->rev[e]] |= bits;
+}
+
+/* heartbeat prunePeer closure, gossipsub.go:1387-1393 */
+static void prune_peer(hb* h, uint32_t e)
+{
+    orc_prune(h->s, e, h->t);
+    h->s->tflags[ti(h, e)] &= (uint8_t)~TF_MESH;
+    do_add_backoff(h, e, h->s->gp->prune_backoff_ns);
+    send_ctl(h, e, GSIM_CTL_PRUNE);
+}
+
+/* heartbeat graftPeer closure, gossipsub.go:1395-1401 */
+static void graft_peer(hb* h, uint32_t e)
+{
+    orc_graft(h->s, e, h->t, h->now);
+    h->s->tflags[ti(h, e)] |= TF_MESH;
+    send_ctl(h, e, GSIM_CTL_GRAFT);
+}
+
+typedef int (*filter_fn)(const hb* h, uint32_t e, double arg);
+
+/* getPeers, gossipsub.go:1908-1928: filter the topic peers, shuffle (= order
+ * by Philox key), truncate to count when count > 0. */
+static int get_peers(const hb* h, int count, filter_fn f, double arg, uint32_t purpose, cand* out)
+{
+    int n = 0;
+    for (uint32_t e = h->b; e < h->en; ++e) {
+        if (!topic_peer(h, e) || !f(h, e, arg)) continue;
+        out[n].key = okey(h->seed, h->tick, h->i, h->t, purpose, h->s->col[e], e - h->b);
+        out[n].e = e;
+        out[n].score = h->s->score[e];
+        ++n;
+    }
+    qsort(out, (size_t)n, sizeof(cand), cmp_key);
+    if (count > 0 && n > count) n = count;
+    return n;
+}
+
+static int f_graft(const hb* h, uint32_t e, double arg)      /* gossipsub.go:1416-1422 */
+{
+    (void)arg;
+    return !in_mesh(h, e) && !has_backoff(h, e) && h->s->score[e] >= 0;
+}
+
+static int f_dout(const hb* h, uint32_t e, double arg)       /* gossipsub.go:1506-1512 */
+{
+    (void)arg;
+    return !in_mesh(h, e) && !has_backoff(h, e) && h->s->outbound[e] && h->s->score[e] >= 0;
+}
+
+static int f_opp(const hb* h, uint32_t e, double median)     /* gossipsub.go:1540-1545 */
+{
+    return !in_mesh(h, e) && !has_backoff(h, e) && h->s->score[e] > median;
+}
+
+/* stable insertion sort by score descending (sort.Slice with the score
+ * closure; ties keep the prior shuffle order, gossipsub.go:1434-1437) */
+static void sort_score_desc(cand* v, int n)
+{
+    for (int a = 1; a < n; ++a) {
+        cand x = v[a];
+        int b = a - 1;
+        while (b >= 0 && v[b].score < x.score) { v[b + 1] = v[b]; --b; }
+        v[b + 1] = x;
+    }
+}
+
+static int cmp_score_asc(const void* a, const void* b)
+{
+    double x = *(const double*)a, y = *(const double*)b;
+    return x < y ? -1 : x > y;
+}
+
+/* Mesh maintenance for one (observer, topic), gossipsub.go:1386-1552. */
+static void maintain(hb* h)
+{
+    orc_net* s = h->s;
+    const gsim_gossipsub_params* gp = s->gp;
+    cand buf[4096];
+    const uint32_t deg = h->en - h->b;
+    cand* c = deg <= 4096 ? buf : (cand*)malloc(sizeof(cand) * deg);
+
+    /* drop all peers with negative score, without PX (1403-1410) */
+    for (uint32_t e = h->b; e < h->en; ++e)
+        if (in_mesh(h, e) && s->score[e] < 0) prune_peer(h, e);
+
+    /* do we have enough peers? (1412-1427) */
+    int l = mesh_count(h);
+    if (l < gp->dlo) {
+        int n = get_peers(h, gp->d - l, f_graft, 0, P_GRAFT_DLO, c);
+        for (int q = 0; q < n; ++q) graft_peer(h, c[q].e);
+    }
+
+    /* do we have too many peers? (1429-1490) */
+    l = mesh_count(h);
+    if (l > gp->dhi) {
+        int n = 0;
+        for (uint32_t e = h->b; e < h->en; ++e) {
+            if (!in_mesh(h, e)) continue;
+            c[n].key = okey(h->seed, h->tick, h->i, h->t, P_PRUNE_SHUF1, s->col[e], e - h->b);
+            c[n].e = e;
+            c[n].score = s->score[e];
+            ++n;
+        }
+        qsort(c, (size_t)n, sizeof(cand), cmp_key);           /* shufflePeers(plst) */
+        sort_score_desc(c, n);                                 /* sort by score desc */
+        int ds = gp->dscore < n ? gp->dscore : n;
+        for (int q = ds; q < n; ++q)                           /* shufflePeers(plst[Dscore:]) */
+            c[q].key = okey(h->seed, h->tick, h->i, h->t, P_PRUNE_SHUF2, s->col[c[q].e], c[q].e - h->b);
+        qsort(c + ds, (size_t)(n - ds), sizeof(cand), cmp_key);
+        int outbound = 0;
+        for (int q = 0; q < gp->d && q < n; ++q) outbound += s->outbound[c[q].e] != 0;
+        if (outbound < gp->dout) {
+            #define ROTATE(idx) do { cand p_ = c[idx]; for (int j_ = (idx); j_ > 0; --j_) c[j_] = c[j_ - 1]; c[0] = p_; } while (0)
+            if (outbound > 0) {
+                int ihave = outbound;
+                for (int q = 1; q < gp->d && ihave > 0; ++q)
+                    if (s->outbound[c[q].e]) { ROTATE(q); --ihave; }
+            }
+            int ineed = gp->dout - outbound;
+            for (int q = gp->d; q < n && ineed > 0; ++q)
+                if (s->outbound[c[q].e]) { ROTATE(q); --ineed; }
+            #undef ROTATE
+        }
+        for (int q = gp->d; q < n; ++q) prune_peer(h, c[q].e);
+    }
+
+    /* do we have enough outbound peers? (1492-1518) */
+    l = mesh_count(h);
+    if (l >= gp->dlo) {
+        int outbound = 0;
+        for (uint32_t e = h->b; e < h->en; ++e) outbound += in_mesh(h, e) && s->outbound[e];
+        if (outbound < gp->dout) {
+            int n = get_peers(h, gp->dout - outbound, f_dout, 0, P_GRAFT_DOUT, c);
+            for (int q = 0; q < n; ++q) graft_peer(h, c[q].e);
+        }
+    }
+
+    /* opportunistic grafting (1520-1552) */
+    l = mesh_count(h);
+    if (gp->opportunistic_graft_ticks && h->tick % gp->opportunistic_graft_ticks == 0 && l > 1) {
+        double* sc = (double*)malloc(sizeof(double) * (size_t)l);
+        int n = 0;
+        for (uint32_t e = h->b; e < h->en; ++e) if (in_mesh(h, e)) sc[n++] = s->score[e];
+        qsort(sc, (size_t)n, sizeof(double), cmp_score_asc);
+        double median = sc[n / 2];
+        free(sc);
+        if (median < s->th->opportunistic_graft_threshold) {
+            int m = get_peers(h, gp->opportunistic_graft_peers, f_opp, median, P_GRAFT_OPP, c);
+            for (int q = 0; q < m; ++q) graft_peer(h, c[q].e);
+        }
+    }
+    if (c != buf) free(c);
+}
+
+void orc_heartbeat(orc_net* s, uint64_t tick, int64_t now, uint64_t seed)
+{
+    uint8_t* out = s->ctl;   /* heartbeat output = parity-0 inbox, handled in round 0 */
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t i = 0; i < s->n; ++i) {
+        hb h = {s, (uint32_t)i, s->row_ptr[i], s->row_ptr[i + 1], 0, tick, seed, now, out};
+        /* clearBackoff every 15 ticks (gossipsub.go:1627-1646) */
+        if (tick % 15 == 0)
+            for (int32_t t = 0; t < s->t; ++t)
+                for (uint32_t e = h.b; e < h.en; ++e) {
+                    int64_t* bo = &s->backoff[(int64_t)t * s->e + e];
+                    if (*bo != 0 && *bo + kBackoffSlack < now) *bo = 0;
+                }
+        /* maintain the mesh for topics we have joined (1385-1557) */
+        for (int32_t t = 0; t < s->t; ++t) {
+            if (!((s->sub[i] >> t) & 1u)) continue;
+            h.t = t;
+            maintain(&h);
+        }
+    }
+}
+
+/* handleGraft for one (receiver, sender edge, topic), gossipsub.go:748-825. */
+static void handle_graft(hb* h, uint32_t e)
+{
+    orc_net* s = h->s;
+    const gsim_gossipsub_params* gp = s->gp;
+    if (!((s->sub[h->i] >> h->t) & 1u)) return;                /* unknown topic: ignore */
+    if (in_mesh(h, e)) return;                                 /* already in mesh */
+    int64_t expire = s->backoff[ti(h, e)];
+    if (expire != 0 && h->now < expire) {                      /* backing off that peer */
+        orc_add_penalty(s, e, 1);
+        int64_t flood_cutoff = expire + (gp->graft_flood_threshold_ns - gp->prune_backoff_ns);
+        if (h->now < flood_cutoff) orc_add_penalty(s, e, 1);
+        do_add_backoff(h, e, gp->prune_backoff_ns);
+        send_ctl(h, e, GSIM_CTL_PRUNE);
+        return;
+    }
+    if (s->score[e] < 0) {                                     /* negative score */
+        send_ctl(h, e, GSIM_CTL_PRUNE);
+        do_add_backoff(h, e, gp->prune_backoff_ns);
+        return;
+    }
+    if (mesh_count(h) >= gp->dhi && !s->outbound[e]) {         /* mesh full, inbound */
+        send_ctl(h, e, GSIM_CTL_PRUNE);
+        do_add_backoff(h, e, gp->prune_backoff_ns);
+        return;
+    }
+    orc_graft(s, e, h->t, h->now);                             /* tracer.Graft + mesh add */
+    s->tflags[ti(h, e)] |= TF_MESH;
+}
+
+/* handlePrune for one (receiver, sender edge, topic), gossipsub.go:842-870. */
+static void handle_prune(hb* h, uint32_t e)
+{
+    orc_net* s = h->s;
+    if (!((s->sub[h->i] >> h->t) & 1u)) return;
+    orc_prune(s, e, h->t);
+    s->tflags[ti(h, e)] &= (uint8_t)~TF_MESH;
+    /* makePrune sends Backoff = PruneBackoff / time.Second (whole seconds);
+     * handlePrune obeys it when > 0, else uses its own PruneBackoff. */
+    int64_t secs = s->gp->prune_backoff_ns / kSecond;
+    if (secs > 0) do_add_backoff(h, e, secs * kSecond);
+    else do_add_backoff(h, e, s->gp->prune_backoff_ns);
+}
+
+int64_t orc_handle_control(orc_net* s, int32_t round, int64_t now)
+{
+    const int64_t TE = (int64_t)s->t * s->e;
+    uint8_t* in = s->ctl + (int64_t)(round & 1) * TE;
+    uint8_t* out = s->ctl + (int64_t)((round + 1) & 1) * TE;
+    int64_t handled = 0;
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : handled)
+    for (int64_t j = 0; j < s->n; ++j) {
+        hb h = {s, (uint32_t)j, s->row_ptr[j], s->row_ptr[j + 1], 0, 0, 0, now, out};
+        for (int32_t t = 0; t < s->t; ++t) {
+            h.t = t;
+            for (uint32_t e = h.b; e < h.en; ++e) {     /* senders in row order */
+                uint8_t c = in[(int64_t)t * s->e + e];
+                if (!c) continue;
+                in[(int64_t)t * s->e + e] = 0;
+                ++handled;
+                if (c & GSIM_CTL_GRAFT) handle_graft(&h, e);
+                if (c & GSIM_CTL_PRUNE) handle_prune(&h, e);
+            }
+        }
+    }
+    return handled;
+}

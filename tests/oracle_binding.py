@@ -32,6 +32,7 @@ class OrcNet(Structure):
         ("bp", c_void_p), ("estate", c_void_p), ("expire", c_void_p), ("p6", c_void_p), ("score", c_void_p),
         ("backoff", c_void_p),
         ("pp", c_void_p), ("tp", c_void_p), ("th", c_void_p), ("gp", c_void_p),
+        ("ctl", c_void_p),
     ]
 
 
@@ -88,6 +89,8 @@ def load():
             "orc_tcache_has": (c_int32, [c_void_p, c_uint64, c_int64]),
             "orc_tcache_sweep": (None, [c_void_p, c_int64]),
             "orc_philox4x32_10": (None, [c_void_p, c_void_p, c_void_p]),
+            "orc_heartbeat": (None, [P, c_uint64, c_int64, c_uint64]),
+            "orc_handle_control": (c_int64, [P, c_int32, c_int64]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -126,6 +129,7 @@ class NetState:
         for f in self.EDGE_FIELDS:
             setattr(self, f, np.zeros(E, dtype=self.DTYPES[f]))
         self.estate[:] = _abi.ES_TRACKED | _abi.ES_CONNECTED
+        self.ctl = np.zeros((2, self.T, E), dtype=np.uint8)
         self.rev = net.rev()
         self.p5 = np.zeros(net.n) if p5 is None else np.ascontiguousarray(p5, dtype=np.float64)
         self.ip_white = None if ip_white is None else np.ascontiguousarray(ip_white, dtype=np.uint8)
@@ -153,6 +157,7 @@ class NetState:
         v.tp = ctypes.cast(self.tp, c_void_p)
         v.th = ctypes.cast(ctypes.byref(self.th), c_void_p)
         v.gp = ctypes.cast(ctypes.byref(self.gp), c_void_p)
+        v.ctl = _p(self.ctl)
         self._view = v
         return ctypes.byref(v)
 
@@ -163,7 +168,9 @@ class NetState:
     def push_to_engine(self, eng):
         for f in self.TOPIC_FIELDS + self.EDGE_FIELDS:
             eng.write(self.FIELD_IDS[f], getattr(self, f))
+        eng.write(_abi.F_CTL, self.ctl)
 
     def pull_from_engine(self, eng):
         for f in self.TOPIC_FIELDS + self.EDGE_FIELDS:
             getattr(self, f)[...] = eng.read(self.FIELD_IDS[f])
+        self.ctl[...] = eng.read(_abi.F_CTL)
