@@ -293,6 +293,144 @@ __global__ __launch_bounds__(256) void k_refresh_score_tile(ScoreArgs a)
 }
 
 // ---------------------------------------------------------------------------
+// Kernel 1c: wave-independent variant.  Each wavefront owns 64 consecutive
+// edges and walks the topics in ascending order in chunks of CHUNK, issuing
+// all loads of a chunk before using any, and accumulates the score in
+// registers in the reference's order (no LDS, no block barriers).  The
+// per-edge inputs of the P5-P7 tail (bp, P6, col -> P5 gather) are issued at
+// the start of the tile so they overlap the first chunk.
+template <bool REFRESH, bool SCORE, int CHUNK>
+__global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    const int64_t ntiles = (a.E + 63) / 64;
+    for (int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); tile < ntiles; tile += nwaves) {
+        const int64_t e = tile * 64 + lane;
+        const bool valid = e < a.E;
+        const uint8_t st = valid ? a.estate[e] : 0;
+        const bool tracked = st & GSIM_ES_TRACKED;
+        const bool conn = st & GSIM_ES_CONNECTED;
+        const bool purge = REFRESH && tracked && !conn && a.now > a.expire[e];
+        const bool decay = REFRESH && tracked && conn;
+        const bool live = valid && tracked && !purge;
+        double bp = 0.0, p6 = 0.0, p5 = 0.0;
+        if (live) {
+            bp = a.bp[e];
+            if (SCORE) {
+                p6 = a.p6[e];
+                p5 = a.p5[a.col[e]];
+            }
+        }
+        double score = 0.0;
+        for (int t0 = 0; t0 < a.T; t0 += CHUNK) {
+            double f[CHUNK], md[CHUNK], fa[CHUNK], iv[CHUNK];
+            int64_t g[CHUNK];
+            uint8_t fl[CHUNK];
+#pragma unroll
+            for (int j = 0; j < CHUNK; ++j) {
+                const int t = t0 + j;
+                f[j] = md[j] = fa[j] = iv[j] = 0.0;
+                g[j] = 0;
+                fl[j] = 0;
+                if (t < a.T && live && a.tp[t].scored) {
+                    const int64_t i = (int64_t)t * a.E + e;
+                    f[j] = a.first[i];
+                    md[j] = a.meshd[i];
+                    fa[j] = a.fail[i];
+                    iv[j] = a.invalid[i];
+                    fl[j] = a.tflags[i];
+                    g[j] = decay ? a.graft[i] : (SCORE ? a.mtime[i] : 0);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < CHUNK; ++j) {
+                const int t = t0 + j;
+                if (t >= a.T || !valid) continue;
+                const int64_t i = (int64_t)t * a.E + e;
+                if (purge) {
+                    a.first[i] = 0.0; a.meshd[i] = 0.0; a.fail[i] = 0.0; a.invalid[i] = 0.0;
+                    a.graft[i] = 0; a.mtime[i] = 0; a.tflags[i] = 0;
+                    continue;
+                }
+                const gsim_topic_score_params* tp = &a.tp[t];
+                if (!live || !tp->scored) continue;
+                double first = f[j], meshd = md[j], fail = fa[j], inval = iv[j];
+                uint8_t fj = fl[j];
+                int64_t mt = g[j];
+                if (decay) {
+                    double x;
+                    x = first * tp->first_message_deliveries_decay;  if (x < a.dtz) x = 0.0;
+                    if (x != first) { first = x; a.first[i] = x; }
+                    x = meshd * tp->mesh_message_deliveries_decay;   if (x < a.dtz) x = 0.0;
+                    if (x != meshd) { meshd = x; a.meshd[i] = x; }
+                    x = fail * tp->mesh_failure_penalty_decay;       if (x < a.dtz) x = 0.0;
+                    if (x != fail) { fail = x; a.fail[i] = x; }
+                    x = inval * tp->invalid_message_deliveries_decay; if (x < a.dtz) x = 0.0;
+                    if (x != inval) { inval = x; a.invalid[i] = x; }
+                    if (fj & GSIM_TF_IN_MESH) {
+                        mt = a.now - g[j];
+                        a.mtime[i] = mt;
+                        if (mt > tp->mesh_message_deliveries_activation_ns && !(fj & GSIM_TF_ACTIVE)) {
+                            fj |= GSIM_TF_ACTIVE;
+                            a.tflags[i] = fj;
+                        }
+                    }
+                }
+                if (SCORE) {
+                    double ts = 0.0;
+                    if (fj & GSIM_TF_IN_MESH) {                               // P1
+                        double p1 = 0.0;
+                        if (tp->time_in_mesh_quantum_ns != 0) p1 = (double)go_div(mt, tp->time_in_mesh_quantum_ns);
+                        if (p1 > tp->time_in_mesh_cap) p1 = tp->time_in_mesh_cap;
+                        ts += p1 * tp->time_in_mesh_weight;
+                    }
+                    ts += first * tp->first_message_deliveries_weight;         // P2
+                    if (fj & GSIM_TF_ACTIVE) {                                 // P3
+                        if (meshd < tp->mesh_message_deliveries_threshold) {
+                            const double deficit = tp->mesh_message_deliveries_threshold - meshd;
+                            const double p3 = deficit * deficit;
+                            ts += p3 * tp->mesh_message_deliveries_weight;
+                        }
+                    }
+                    ts += fail * tp->mesh_failure_penalty_weight;              // P3b
+                    const double p4 = inval * inval;                           // P4
+                    ts += p4 * tp->invalid_message_deliveries_weight;
+                    score += ts * tp->topic_weight;
+                }
+            }
+        }
+        if (!valid) continue;
+        if (!tracked) {
+            if (SCORE) a.score[e] = 0.0;
+        } else if (purge) {                                  // score.go:512-516
+            a.estate[e] = 0;
+            a.bp[e] = 0.0;
+            a.expire[e] = 0;
+            *a.purged = 1;
+            if (SCORE) a.score[e] = 0.0;
+        } else {
+            if (decay) {
+                double x = bp * a.bp_decay;
+                if (x < a.dtz) x = 0.0;
+                if (x != bp) { bp = x; a.bp[e] = x; }
+            }
+            if (SCORE) {
+                if (a.topic_cap > 0 && score > a.topic_cap) score = a.topic_cap;
+                score += p5 * a.w5;                                        // P5
+                score += p6 * a.w6;                                        // P6
+                if (bp > a.bp_thr) {                                       // P7
+                    const double excess = bp - a.bp_thr;
+                    const double p7 = excess * excess;
+                    score += p7 * a.w7;
+                }
+                a.score[e] = score;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Kernel 2: ipColocationFactor (score.go:344-388) as a segmented count over
 // each observer's row keyed by IP id.  Only re-run when the tracked set or the
 // IP assignment changes (AddPeer/RemovePeer/purge), not every heartbeat.
@@ -496,28 +634,42 @@ int launch_ip_colocation(gsim_handle* h)
     return hip_check(h, hipGetLastError(), "k_ip_colocation");
 }
 
-// GSIM_SCORE_KERNEL=thread selects the thread-per-edge variant (A/B only).
-static bool use_thread_kernel()
+// Kernel variant for the refresh+score pass (A/B): GSIM_SCORE_KERNEL =
+// thread | tile | wave4 | wave8 (default wave4) or gsim_set_kernel_variant().
+static int score_variant_from_env()
 {
-    static int v = -1;
-    if (v < 0) {
-        const char* s = std::getenv("GSIM_SCORE_KERNEL");
-        v = (s && std::strcmp(s, "thread") == 0) ? 1 : 0;
-    }
-    return v == 1;
+    const char* s = std::getenv("GSIM_SCORE_KERNEL");
+    if (!s) return 2;
+    if (!std::strcmp(s, "thread")) return 0;
+    if (!std::strcmp(s, "tile")) return 1;
+    if (!std::strcmp(s, "wave8")) return 3;
+    return 2;
 }
 
 template <bool REFRESH, bool SCORE>
 static void launch_score_kernel(gsim_handle* h, const ScoreArgs& a)
 {
-    if (use_thread_kernel()) {
+    if (h->score_variant < 0) h->score_variant = score_variant_from_env();
+    const int64_t tiles = (h->e + kTileEdges - 1) / kTileEdges;
+    switch (h->score_variant) {
+    case 0:
         hipLaunchKernelGGL((k_refresh_score<REFRESH, SCORE>), dim3(grid_for(h->e)), dim3(256), 0, h->stream, a);
         return;
+    case 1: {
+        const int grid = (int)std::min<int64_t>(std::max<int64_t>(tiles, 1), 256 * 16);
+        const size_t lds = sizeof(double) * kTileEdges * (size_t)std::max(1, h->t);
+        hipLaunchKernelGGL((k_refresh_score_tile<REFRESH, SCORE>), dim3(grid), dim3(256), lds, h->stream, a);
+        return;
     }
-    const int64_t tiles = (h->e + kTileEdges - 1) / kTileEdges;
-    const int grid = (int)std::min<int64_t>(std::max<int64_t>(tiles, 1), 256 * 16);
-    const size_t lds = sizeof(double) * kTileEdges * (size_t)std::max(1, h->t);
-    hipLaunchKernelGGL((k_refresh_score_tile<REFRESH, SCORE>), dim3(grid), dim3(256), lds, h->stream, a);
+    default: {
+        const int grid = (int)std::min<int64_t>(std::max<int64_t>((tiles + 3) / 4, 1), 256 * 32);
+        if (h->score_variant == 3)
+            hipLaunchKernelGGL((k_refresh_score_wave<REFRESH, SCORE, 8>), dim3(grid), dim3(256), 0, h->stream, a);
+        else
+            hipLaunchKernelGGL((k_refresh_score_wave<REFRESH, SCORE, 4>), dim3(grid), dim3(256), 0, h->stream, a);
+        return;
+    }
+    }
 }
 
 int launch_refresh_scores(gsim_handle* h, int64_t now)
@@ -865,6 +1017,14 @@ int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now, double p_mes
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     return hip_check(h, e, "gsim_fill_synthetic");
+}
+
+int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant)
+{
+    if (!h) return GSIM_EINVAL;
+    if (which != 0 || variant < 0 || variant > 3) { h->err = "unknown kernel variant"; return GSIM_EINVAL; }
+    h->score_variant = variant;
+    return GSIM_OK;
 }
 
 int gsim_census(gsim_handle* h, int64_t* out8)

@@ -67,6 +67,7 @@ struct gsim_handle {
     bool has_white = false;
     bool p6_dirty = true;
     bool maybe_retained = false;
+    int score_variant = -1;   // refresh+score kernel variant (-1: from env)
 
     // device: parameters and scratch flags
     gsim_topic_score_params* d_tp = nullptr;

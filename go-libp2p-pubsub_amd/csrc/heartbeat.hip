@@ -53,6 +53,7 @@ namespace {
 
 constexpr int64_t kSecond = 1000000000LL;
 constexpr int64_t kBackoffSlack = 2 * kSecond;   // 2*GossipSubHeartbeatInterval (gossipsub.go:1638)
+constexpr int kFlagChunk = 8;                    // topics whose flags are loaded together
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
@@ -144,16 +145,35 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             }
         }
 
-        for (int32_t t = 0; t < a.T; ++t) {
+        for (int32_t t0 = 0; t0 < a.T; t0 += kFlagChunk) {
+          // the flags of a chunk of topics are loaded together (one memory
+          // round trip per chunk instead of one per topic)
+          uint8_t flc[kFlagChunk];
+#pragma unroll
+          for (int j = 0; j < kFlagChunk; ++j) {
+              const int32_t t = t0 + j;
+              flc[j] = (t < a.T && valid && ((subi >> t) & 1ull)) ? a.tflags[(int64_t)t * a.E + e] : 0;
+          }
+          for (int j = 0; j < kFlagChunk; ++j) {
+            const int32_t t = t0 + j;
+            if (t >= a.T) break;
             if (!((subi >> t) & 1ull)) continue;           // not joined
             const gsim_topic_score_params* tp = &a.tp[t];
             const bool scored = tp->scored != 0;
             const double thr = tp->mesh_message_deliveries_threshold;
             const int64_t i = (int64_t)t * a.E + e;
-            uint8_t fl = valid ? a.tflags[i] : 0;
+            uint8_t fl = flc[j];
             const uint8_t fl0 = fl;
-            int64_t bo = valid ? a.backoff[i] : 0;
-            const int64_t bo0 = bo;
+            // backoff is only consulted when a graft selection or a prune
+            // happens, so it is loaded lazily (steady-state ticks read none)
+            int64_t bo = 0;
+            bool have_bo = false, bo_dirty = false;
+            auto need_bo = [&]() {
+                if (!have_bo) {
+                    bo = valid ? a.backoff[i] : 0;
+                    have_bo = true;
+                }
+            };
             const bool tpeer = valid && conn && ((subj >> t) & 1ull);
             bool m = valid && (fl & GSIM_TF_MESH);
             uint8_t ctl = 0;
@@ -163,8 +183,9 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
                 stats_prune(a, tracked, scored, thr, i, fl);
                 fl &= (uint8_t)~GSIM_TF_MESH;
                 m = false;
+                need_bo();
                 const int64_t ex = a.now + a.prune_backoff;
-                if (bo < ex) bo = ex;
+                if (bo < ex) { bo = ex; bo_dirty = true; }
                 ctl |= GSIM_CTL_PRUNE;
             };
             auto graft = [&]() {
@@ -180,6 +201,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             // too few peers: graft up to D (1412-1427)
             int l = __popcll(ballot(m));
             if (l < a.Dlo) {
+                need_bo();
                 const bool cand = tpeer && !m && bo == 0 && S >= 0;
                 if (select_smallest(a, cand, a.D - l, (uint32_t)obs, t, P_GRAFT_DLO, col, pos)) graft();
             }
@@ -219,7 +241,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
                     for (int q = 0; q < a.D && q < l; ++q) outbound += (int)((outmask >> pl[q]) & 1ull);
                     auto rotate = [&](int idx) {
                         const uint8_t v = pl[idx];
-                        for (int j = idx; j > 0; --j) pl[j] = pl[j - 1];
+                        for (int w = idx; w > 0; --w) pl[w] = pl[w - 1];
                         pl[0] = v;
                     };
                     if (outbound < a.Dout) {
@@ -245,6 +267,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             if (l >= a.Dlo) {
                 const int ob = __popcll(ballot(m && outb));
                 if (ob < a.Dout) {
+                    need_bo();
                     const bool cand = tpeer && !m && bo == 0 && outb && S >= 0;
                     if (select_smallest(a, cand, a.Dout - ob, (uint32_t)obs, t, P_GRAFT_DOUT, col, pos)) graft();
                 }
@@ -262,6 +285,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
                 const uint64_t at = ballot(m && rank == l / 2);
                 const double median = __shfl(S, (int)__ffsll((long long)at) - 1, 64);
                 if (median < a.opp_threshold) {
+                    need_bo();
                     const bool cand = tpeer && !m && bo == 0 && S > median;
                     if (select_smallest(a, cand, a.opp_peers, (uint32_t)obs, t, P_GRAFT_OPP, col, pos)) graft();
                 }
@@ -269,12 +293,13 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
 
             if (valid) {
                 if (fl != fl0) a.tflags[i] = fl;
-                if (bo != bo0) a.backoff[i] = bo;
+                if (bo_dirty) a.backoff[i] = bo;
                 if (ctl) {
                     const int64_t r = (int64_t)t * a.E + a.rev[e];
                     a.ctl_out[r] = (uint8_t)(a.ctl_out[r] | ctl);
                 }
             }
+          }
         }
     }
 }
@@ -293,9 +318,18 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
         const bool valid = lane < deg;
         const uint32_t e = b + (uint32_t)lane;
         const uint64_t subr = a.sub[rcv];
-        for (int32_t t = 0; t < a.T; ++t) {
+        for (int32_t t0 = 0; t0 < a.T; t0 += kFlagChunk) {
+          uint8_t cc[kFlagChunk];
+#pragma unroll
+          for (int j = 0; j < kFlagChunk; ++j) {
+              const int32_t t = t0 + j;
+              cc[j] = (t < a.T && valid) ? a.ctl_in[(int64_t)t * a.E + e] : 0;
+          }
+          for (int j = 0; j < kFlagChunk; ++j) {
+            const int32_t t = t0 + j;
+            if (t >= a.T) break;
             const int64_t i = (int64_t)t * a.E + e;
-            const uint8_t c = valid ? a.ctl_in[i] : 0;
+            const uint8_t c = cc[j];
             uint64_t pending = ballot(c != 0);
             if (!pending) continue;
             if (c) a.ctl_in[i] = 0;
@@ -357,6 +391,7 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                 }
                 mesh += __shfl(delta, q, 64);
             }
+          }
         }
     }
 }

@@ -117,6 +117,7 @@ SIGNATURES = [
     ("gsim_event_record", c_int32, [c_void_p, c_int32]),
     ("gsim_event_elapsed", c_int32, [c_void_p, c_int32, c_int32, POINTER(c_float)]),
     ("gsim_synchronize", c_int32, [c_void_p]),
+    ("gsim_set_kernel_variant", c_int32, [c_void_p, c_int32, c_int32]),
     ("gsim_gen_random_regular", c_int32, [c_int64, c_int32, c_uint64, c_void_p, c_void_p, c_void_p]),
     ("gsim_fill_synthetic", c_int32, [c_void_p, c_uint64, c_int64, c_double]),
     ("gsim_set_seed", c_int32, [c_void_p, c_uint64]),

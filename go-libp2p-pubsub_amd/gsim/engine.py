@@ -230,3 +230,6 @@ class Engine:
 
     def synchronize(self):
         self._check(self.lib.gsim_synchronize(self.h))
+
+    def set_kernel_variant(self, which: int, variant: int):
+        self._check(self.lib.gsim_set_kernel_variant(self.h, which, variant))
