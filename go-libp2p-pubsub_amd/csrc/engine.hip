@@ -148,149 +148,7 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
     }
 }
 
-// ---------------------------------------------------------------------------
-// Kernel 1b (production path): the same computation as k_refresh_score,
-// restructured for memory-level parallelism.  A 256-thread block owns a tile
-// of 64 consecutive edges; wave w takes topics w, w+4, w+8, w+12 of the tile
-// and issues all of their loads before the first use, so each wave makes one
-// HBM round trip per tile instead of one per topic (the per-thread topic loop
-// above serializes on vmcnt, which on CDNA counts stores too).  Each topic's
-// weighted contribution ts*TopicWeight goes to LDS; wave 0 then adds them in
-// ascending topic order and finishes P5-P7, so the sum is bit-identical to
-// the reference order (score.go:274-341).
 constexpr int kTileEdges = 64;
-constexpr int kTopicsPerWavePass = 4;
-
-template <bool REFRESH, bool SCORE>
-__global__ __launch_bounds__(256) void k_refresh_score_tile(ScoreArgs a)
-{
-    extern __shared__ double s_contrib[];   // [T][64]
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int64_t ntiles = (a.E + kTileEdges - 1) / kTileEdges;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t e = tile * kTileEdges + lane;
-        const bool valid = e < a.E;
-        const uint8_t st = valid ? a.estate[e] : 0;
-        const bool tracked = st & GSIM_ES_TRACKED;
-        const bool conn = st & GSIM_ES_CONNECTED;
-        const bool purge = REFRESH && tracked && !conn && a.now > a.expire[e];
-        const bool decay = REFRESH && tracked && conn;
-        const bool live = valid && tracked && !purge;
-
-        for (int t0 = wid; t0 < a.T; t0 += 4 * kTopicsPerWavePass) {
-            double f[kTopicsPerWavePass], md[kTopicsPerWavePass], fa[kTopicsPerWavePass], iv[kTopicsPerWavePass];
-            int64_t g[kTopicsPerWavePass];
-            uint8_t fl[kTopicsPerWavePass];
-#pragma unroll
-            for (int j = 0; j < kTopicsPerWavePass; ++j) {
-                const int t = t0 + 4 * j;
-                f[j] = md[j] = fa[j] = iv[j] = 0.0;
-                g[j] = 0;
-                fl[j] = 0;
-                if (t < a.T && live && a.tp[t].scored) {
-                    const int64_t i = (int64_t)t * a.E + e;
-                    f[j] = a.first[i];
-                    md[j] = a.meshd[i];
-                    fa[j] = a.fail[i];
-                    iv[j] = a.invalid[i];
-                    fl[j] = a.tflags[i];
-                    g[j] = decay ? a.graft[i] : (SCORE ? a.mtime[i] : 0);
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < kTopicsPerWavePass; ++j) {
-                const int t = t0 + 4 * j;
-                if (t >= a.T || !valid) continue;
-                const int64_t i = (int64_t)t * a.E + e;
-                if (purge) {
-                    a.first[i] = 0.0; a.meshd[i] = 0.0; a.fail[i] = 0.0; a.invalid[i] = 0.0;
-                    a.graft[i] = 0; a.mtime[i] = 0; a.tflags[i] = 0;
-                    continue;
-                }
-                const gsim_topic_score_params* tp = &a.tp[t];
-                if (!live || !tp->scored) continue;
-                double first = f[j], meshd = md[j], fail = fa[j], inval = iv[j];
-                uint8_t fj = fl[j];
-                int64_t mt = g[j];
-                if (decay) {
-                    double x;
-                    x = first * tp->first_message_deliveries_decay;  if (x < a.dtz) x = 0.0;
-                    if (x != first) { first = x; a.first[i] = x; }
-                    x = meshd * tp->mesh_message_deliveries_decay;   if (x < a.dtz) x = 0.0;
-                    if (x != meshd) { meshd = x; a.meshd[i] = x; }
-                    x = fail * tp->mesh_failure_penalty_decay;       if (x < a.dtz) x = 0.0;
-                    if (x != fail) { fail = x; a.fail[i] = x; }
-                    x = inval * tp->invalid_message_deliveries_decay; if (x < a.dtz) x = 0.0;
-                    if (x != inval) { inval = x; a.invalid[i] = x; }
-                    if (fj & GSIM_TF_IN_MESH) {
-                        mt = a.now - g[j];
-                        a.mtime[i] = mt;
-                        if (mt > tp->mesh_message_deliveries_activation_ns && !(fj & GSIM_TF_ACTIVE)) {
-                            fj |= GSIM_TF_ACTIVE;
-                            a.tflags[i] = fj;
-                        }
-                    }
-                }
-                if (SCORE) {
-                    double ts = 0.0;
-                    if (fj & GSIM_TF_IN_MESH) {                               // P1
-                        double p1 = 0.0;
-                        if (tp->time_in_mesh_quantum_ns != 0) p1 = (double)go_div(mt, tp->time_in_mesh_quantum_ns);
-                        if (p1 > tp->time_in_mesh_cap) p1 = tp->time_in_mesh_cap;
-                        ts += p1 * tp->time_in_mesh_weight;
-                    }
-                    ts += first * tp->first_message_deliveries_weight;         // P2
-                    if (fj & GSIM_TF_ACTIVE) {                                 // P3
-                        if (meshd < tp->mesh_message_deliveries_threshold) {
-                            const double deficit = tp->mesh_message_deliveries_threshold - meshd;
-                            const double p3 = deficit * deficit;
-                            ts += p3 * tp->mesh_message_deliveries_weight;
-                        }
-                    }
-                    ts += fail * tp->mesh_failure_penalty_weight;              // P3b
-                    const double p4 = inval * inval;                           // P4
-                    ts += p4 * tp->invalid_message_deliveries_weight;
-                    s_contrib[t * kTileEdges + lane] = ts * tp->topic_weight;
-                }
-            }
-        }
-        __syncthreads();
-        if (wid == 0 && valid) {
-            if (!tracked) {
-                if (SCORE) a.score[e] = 0.0;
-            } else if (purge) {                              // score.go:512-516
-                a.estate[e] = 0;
-                a.bp[e] = 0.0;
-                a.expire[e] = 0;
-                *a.purged = 1;
-                if (SCORE) a.score[e] = 0.0;
-            } else {
-                double bp = a.bp[e];
-                if (decay) {
-                    double x = bp * a.bp_decay;
-                    if (x < a.dtz) x = 0.0;
-                    if (x != bp) { bp = x; a.bp[e] = x; }
-                }
-                if (SCORE) {
-                    double score = 0.0;
-                    for (int32_t t = 0; t < a.T; ++t)
-                        if (a.tp[t].scored) score += s_contrib[t * kTileEdges + lane];
-                    if (a.topic_cap > 0 && score > a.topic_cap) score = a.topic_cap;
-                    const double p5 = a.p5[a.col[e]];                      // P5
-                    score += p5 * a.w5;
-                    score += a.p6[e] * a.w6;                               // P6
-                    if (bp > a.bp_thr) {                                   // P7
-                        const double excess = bp - a.bp_thr;
-                        const double p7 = excess * excess;
-                        score += p7 * a.w7;
-                    }
-                    a.score[e] = score;
-                }
-            }
-        }
-        __syncthreads();
-    }
-}
 
 // ---------------------------------------------------------------------------
 // Kernel 1c: wave-independent variant.  Each wavefront owns 64 consecutive
@@ -319,9 +177,10 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
             bp = a.bp[e];
             if (SCORE) {
                 p6 = a.p6[e];
-                p5 = a.p5[a.col[e]];
+                p5 = (a.diag & DIAG_NO_P5) ? 0.0 : a.p5[a.col[e]];
             }
         }
+        const bool st_ok = !(a.diag & DIAG_NO_STORES);
         double score = 0.0;
         for (int t0 = 0; t0 < a.T; t0 += CHUNK) {
             double f[CHUNK], md[CHUNK], fa[CHUNK], iv[CHUNK];
@@ -340,7 +199,7 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
                     fa[j] = a.fail[i];
                     iv[j] = a.invalid[i];
                     fl[j] = a.tflags[i];
-                    g[j] = decay ? a.graft[i] : (SCORE ? a.mtime[i] : 0);
+                    if (!(a.diag & DIAG_NO_GRAFT)) g[j] = decay ? a.graft[i] : (SCORE ? a.mtime[i] : 0);
                 }
             }
 #pragma unroll
@@ -361,19 +220,19 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
                 if (decay) {
                     double x;
                     x = first * tp->first_message_deliveries_decay;  if (x < a.dtz) x = 0.0;
-                    if (x != first) { first = x; a.first[i] = x; }
+                    if (x != first) { first = x; if (st_ok) a.first[i] = x; }
                     x = meshd * tp->mesh_message_deliveries_decay;   if (x < a.dtz) x = 0.0;
-                    if (x != meshd) { meshd = x; a.meshd[i] = x; }
+                    if (x != meshd) { meshd = x; if (st_ok) a.meshd[i] = x; }
                     x = fail * tp->mesh_failure_penalty_decay;       if (x < a.dtz) x = 0.0;
-                    if (x != fail) { fail = x; a.fail[i] = x; }
+                    if (x != fail) { fail = x; if (st_ok) a.fail[i] = x; }
                     x = inval * tp->invalid_message_deliveries_decay; if (x < a.dtz) x = 0.0;
-                    if (x != inval) { inval = x; a.invalid[i] = x; }
+                    if (x != inval) { inval = x; if (st_ok) a.invalid[i] = x; }
                     if (fj & GSIM_TF_IN_MESH) {
                         mt = a.now - g[j];
-                        a.mtime[i] = mt;
+                        if (st_ok && !(a.diag & DIAG_NO_MTIME)) a.mtime[i] = mt;
                         if (mt > tp->mesh_message_deliveries_activation_ns && !(fj & GSIM_TF_ACTIVE)) {
                             fj |= GSIM_TF_ACTIVE;
-                            a.tflags[i] = fj;
+                            if (st_ok) a.tflags[i] = fj;
                         }
                     }
                 }
@@ -381,7 +240,8 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
                     double ts = 0.0;
                     if (fj & GSIM_TF_IN_MESH) {                               // P1
                         double p1 = 0.0;
-                        if (tp->time_in_mesh_quantum_ns != 0) p1 = (double)go_div(mt, tp->time_in_mesh_quantum_ns);
+                        if (tp->time_in_mesh_quantum_ns != 0 && !(a.diag & DIAG_NO_DIV))
+                            p1 = (double)go_div(mt, tp->time_in_mesh_quantum_ns);
                         if (p1 > tp->time_in_mesh_cap) p1 = tp->time_in_mesh_cap;
                         ts += p1 * tp->time_in_mesh_weight;
                     }
@@ -620,6 +480,7 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     a.bp = h->d_bp; a.estate = h->d_estate; a.expire = h->d_expire; a.p6 = h->d_p6; a.score = h->d_score;
     a.now = now;
     a.purged = h->d_flags;
+    a.diag = h->diag;
     return a;
 }
 
@@ -641,7 +502,6 @@ static int score_variant_from_env()
     const char* s = std::getenv("GSIM_SCORE_KERNEL");
     if (!s) return 2;
     if (!std::strcmp(s, "thread")) return 0;
-    if (!std::strcmp(s, "tile")) return 1;
     if (!std::strcmp(s, "wave8")) return 3;
     return 2;
 }
@@ -655,12 +515,6 @@ static void launch_score_kernel(gsim_handle* h, const ScoreArgs& a)
     case 0:
         hipLaunchKernelGGL((k_refresh_score<REFRESH, SCORE>), dim3(grid_for(h->e)), dim3(256), 0, h->stream, a);
         return;
-    case 1: {
-        const int grid = (int)std::min<int64_t>(std::max<int64_t>(tiles, 1), 256 * 16);
-        const size_t lds = sizeof(double) * kTileEdges * (size_t)std::max(1, h->t);
-        hipLaunchKernelGGL((k_refresh_score_tile<REFRESH, SCORE>), dim3(grid), dim3(256), lds, h->stream, a);
-        return;
-    }
     default: {
         const int grid = (int)std::min<int64_t>(std::max<int64_t>((tiles + 3) / 4, 1), 256 * 32);
         if (h->score_variant == 3)
@@ -1022,7 +876,14 @@ int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now, double p_mes
 int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant)
 {
     if (!h) return GSIM_EINVAL;
-    if (which != 0 || variant < 0 || variant > 3) { h->err = "unknown kernel variant"; return GSIM_EINVAL; }
+    if (which == 1) {           // diagnostic ablation mask (timing experiments only)
+        h->diag = (uint32_t)variant;
+        return GSIM_OK;
+    }
+    if (which != 0 || variant < 0 || variant > 3 || variant == 1) {
+        h->err = "unknown kernel variant";
+        return GSIM_EINVAL;
+    }
     h->score_variant = variant;
     return GSIM_OK;
 }

@@ -30,6 +30,17 @@ struct ScoreArgs {
     double* score;
     int64_t now;
     int32_t* purged;
+    uint32_t diag;   // diagnostic ablations (DIAG_*), 0 in production
+};
+
+// Diagnostic ablations of the refresh+score wave kernel, for A/B timing only
+// (results are wrong when any is set; never used by tests or the bench value).
+enum : uint32_t {
+    DIAG_NO_P5 = 1,      // skip the P5 gather
+    DIAG_NO_MTIME = 2,   // skip the meshTime store
+    DIAG_NO_STORES = 4,  // skip every record store
+    DIAG_NO_GRAFT = 8,   // skip the graftTime load
+    DIAG_NO_DIV = 16,    // skip the P1 division
 };
 
 struct ColocArgs {
@@ -68,6 +79,7 @@ struct gsim_handle {
     bool p6_dirty = true;
     bool maybe_retained = false;
     int score_variant = -1;   // refresh+score kernel variant (-1: from env)
+    uint32_t diag = 0;        // DIAG_* ablations (A/B diagnostics only)
 
     // device: parameters and scratch flags
     gsim_topic_score_params* d_tp = nullptr;

@@ -279,8 +279,9 @@ int gsim_event_elapsed(gsim_handle* h, int32_t from, int32_t to, float* ms);
 int gsim_synchronize(gsim_handle* h);
 /* Select an implementation variant of a hot-path kernel for A/B timing in
  * one process (results are identical across variants).  which = 0: the
- * refreshScores+score pass; variant 0 thread-per-edge, 1 LDS tile,
- * 2 wave (4-topic chunks, default), 3 wave (8-topic chunks). */
+ * refreshScores+score pass; variant 0 thread-per-edge, 2 wave (4-topic
+ * chunks, default), 3 wave (8-topic chunks).  which = 1: diagnostic ablation
+ * mask for timing experiments (results are wrong while it is non-zero). */
 int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant);
 
 /* ---- synthetic inputs -------------------------------- */

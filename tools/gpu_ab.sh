@@ -10,7 +10,7 @@ echo "== pytest -m gpu"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
 tail -2 "$OUT/pytest_gpu.log"
 echo "== A/B"
-timeout -k 10 400 python -u tools/ab_kernels.py > "$OUT/ab.log" 2>&1
+timeout -k 10 400 python -u tools/ab_kernels.py --diag > "$OUT/ab.log" 2>&1
 tail -1 "$OUT/ab.log"
 echo "== bench"
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > "$OUT/bench.log" 2>&1
