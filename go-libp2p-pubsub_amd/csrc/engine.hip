@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
         const bool decay = REFRESH && conn;   // retained scores are not decayed
         double score = 0.0;
         for (int32_t t = 0; t < a.T; ++t) {
-            const gsim_topic_score_params* tp = &a.tp[t];
+            const ctp_t tp = const_tp(a.tp) + t;
             if (!tp->scored) continue;
             const int64_t i = (int64_t)t * a.E + e;
             double first = a.first[i], meshd = a.meshd[i], fail = a.fail[i], inval = a.invalid[i];
@@ -166,20 +166,27 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
     for (int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); tile < ntiles; tile += nwaves) {
         const int64_t e = tile * 64 + lane;
         const bool valid = e < a.E;
-        const uint8_t st = valid ? a.estate[e] : 0;
-        const bool tracked = st & GSIM_ES_TRACKED;
-        const bool conn = st & GSIM_ES_CONNECTED;
-        const bool purge = REFRESH && tracked && !conn && a.now > a.expire[e];
-        const bool decay = REFRESH && tracked && conn;
-        const bool live = valid && tracked && !purge;
+        // per-edge inputs are loaded unconditionally (not behind estate) so
+        // they share one memory round trip with the first topic chunk
+        uint8_t st = 0;
+        int64_t expire = 0;
         double bp = 0.0, p6 = 0.0, p5 = 0.0;
-        if (live) {
+        uint32_t c = 0;
+        if (valid) {
+            st = a.estate[e];
+            expire = a.expire[e];
             bp = a.bp[e];
             if (SCORE) {
                 p6 = a.p6[e];
-                p5 = (a.diag & DIAG_NO_P5) ? 0.0 : a.p5[a.col[e]];
+                c = a.col[e];
             }
         }
+        if (SCORE && valid && !(a.diag & DIAG_NO_P5)) p5 = a.p5[c];
+        const bool tracked = st & GSIM_ES_TRACKED;
+        const bool conn = st & GSIM_ES_CONNECTED;
+        const bool purge = REFRESH && tracked && !conn && a.now > expire;
+        const bool decay = REFRESH && tracked && conn;
+        const bool live = valid && tracked && !purge;
         const bool st_ok = !(a.diag & DIAG_NO_STORES);
         double score = 0.0;
         for (int t0 = 0; t0 < a.T; t0 += CHUNK) {
@@ -192,7 +199,7 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
                 f[j] = md[j] = fa[j] = iv[j] = 0.0;
                 g[j] = 0;
                 fl[j] = 0;
-                if (t < a.T && live && a.tp[t].scored) {
+                if (t < a.T && live && const_tp(a.tp)[t].scored) {
                     const int64_t i = (int64_t)t * a.E + e;
                     f[j] = a.first[i];
                     md[j] = a.meshd[i];
@@ -212,7 +219,7 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
                     a.graft[i] = 0; a.mtime[i] = 0; a.tflags[i] = 0;
                     continue;
                 }
-                const gsim_topic_score_params* tp = &a.tp[t];
+                const ctp_t tp = const_tp(a.tp) + t;
                 if (!live || !tp->scored) continue;
                 double first = f[j], meshd = md[j], fail = fa[j], inval = iv[j];
                 uint8_t fj = fl[j];
@@ -378,7 +385,7 @@ __global__ __launch_bounds__(256) void k_census(ScoreArgs a, unsigned long long*
         c[7] += 1;
         if (!(st & GSIM_ES_CONNECTED)) continue;
         for (int32_t t = 0; t < a.T; ++t) {
-            if (!a.tp[t].scored) continue;
+            if (!const_tp(a.tp)[t].scored) continue;
             const int64_t i = (int64_t)t * a.E + e;
             const uint8_t fl = a.tflags[i];
             c[0] += 1;

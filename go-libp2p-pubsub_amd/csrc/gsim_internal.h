@@ -52,6 +52,17 @@ struct ColocArgs {
     int32_t thr;
 };
 
+// Topic parameters are read-only for a kernel's lifetime.  Reading them
+// through the constant address space (4) lets the compiler use scalar
+// s_load (scalar cache, lgkmcnt) instead of vector loads that it must order
+// against the kernel's stores with s_waitcnt vmcnt(0) — which serializes every
+// memory round trip of the hot loops.
+typedef const __attribute__((address_space(4))) gsim_topic_score_params* ctp_t;
+__device__ __forceinline__ ctp_t const_tp(const gsim_topic_score_params* p)
+{
+    return (ctp_t)(p);
+}
+
 struct FieldRef {
     void* ptr;
     size_t bytes;

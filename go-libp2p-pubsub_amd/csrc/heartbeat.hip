@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             const int32_t t = t0 + j;
             if (t >= a.T) break;
             if (!((subi >> t) & 1ull)) continue;           // not joined
-            const gsim_topic_score_params* tp = &a.tp[t];
+            const ctp_t tp = const_tp(a.tp) + t;
             const bool scored = tp->scored != 0;
             const double thr = tp->mesh_message_deliveries_threshold;
             const int64_t i = (int64_t)t * a.E + e;
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
             if (!pending) continue;
             if (c) a.ctl_in[i] = 0;
             if (!((subr >> t) & 1ull)) continue;            // unknown topic: ignored
-            const gsim_topic_score_params* tp = &a.tp[t];
+            const ctp_t tp = const_tp(a.tp) + t;
             const bool scored = tp->scored != 0;
             const double thr = tp->mesh_message_deliveries_threshold;
             uint8_t fl = valid ? a.tflags[i] : 0;
