@@ -101,6 +101,8 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
                         fl |= GSIM_TF_ACTIVE;
                         a.tflags[i] = fl;
                     }
+                } else {
+                    a.mtime[i] = 0;   // unobservable outside the mesh
                 }
             } else if (SCORE && (fl & GSIM_TF_IN_MESH)) {
                 mt = a.mtime[i];
@@ -157,12 +159,32 @@ constexpr int kTileEdges = 64;
 // registers in the reference's order (no LDS, no block barriers).  The
 // per-edge inputs of the P5-P7 tail (bp, P6, col -> P5 gather) are issued at
 // the start of the tile so they overlap the first chunk.
+// Store policy for the [T][E] planes.  A wave-instruction store with only a few
+// active lanes writes scattered 8-B pieces and the memory side pays for whole
+// sectors (measured: sparse meshTime/counter stores cost more than rewriting
+// the full lines).  So a field is rewritten densely (every lane that holds the
+// exact stored value writes it back) when more than kDenseLanes lanes of the
+// wave changed it, and sparsely otherwise.  Either way the resulting memory
+// contents are identical.
+constexpr int kDenseLanes = 8;
+
+template <typename T>
+__device__ __forceinline__ void policy_store(T* p, int64_t i, T v, bool changed, bool can_rewrite)
+{
+    const uint64_t m = __ballot(changed);
+    if (!m) return;
+    const bool dense = __popcll(m) > kDenseLanes;
+    if (changed || (dense && can_rewrite)) p[i] = v;
+}
+
 template <bool REFRESH, bool SCORE, int CHUNK>
 __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
 {
     const int lane = threadIdx.x & 63;
     const int64_t nwaves = (int64_t)gridDim.x * 4;
     const int64_t ntiles = (a.E + 63) / 64;
+    const ctp_t tpa = const_tp(a.tp);
+    const bool st_ok = !(a.diag & DIAG_NO_STORES);
     for (int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); tile < ntiles; tile += nwaves) {
         const int64_t e = tile * 64 + lane;
         const bool valid = e < a.E;
@@ -187,7 +209,6 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
         const bool purge = REFRESH && tracked && !conn && a.now > expire;
         const bool decay = REFRESH && tracked && conn;
         const bool live = valid && tracked && !purge;
-        const bool st_ok = !(a.diag & DIAG_NO_STORES);
         double score = 0.0;
         for (int t0 = 0; t0 < a.T; t0 += CHUNK) {
             double f[CHUNK], md[CHUNK], fa[CHUNK], iv[CHUNK];
@@ -199,7 +220,7 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
                 f[j] = md[j] = fa[j] = iv[j] = 0.0;
                 g[j] = 0;
                 fl[j] = 0;
-                if (t < a.T && live && const_tp(a.tp)[t].scored) {
+                if (t < a.T && valid && tpa[t].scored) {
                     const int64_t i = (int64_t)t * a.E + e;
                     f[j] = a.first[i];
                     md[j] = a.meshd[i];
@@ -212,38 +233,43 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
 #pragma unroll
             for (int j = 0; j < CHUNK; ++j) {
                 const int t = t0 + j;
-                if (t >= a.T || !valid) continue;
-                const int64_t i = (int64_t)t * a.E + e;
-                if (purge) {
-                    a.first[i] = 0.0; a.meshd[i] = 0.0; a.fail[i] = 0.0; a.invalid[i] = 0.0;
-                    a.graft[i] = 0; a.mtime[i] = 0; a.tflags[i] = 0;
-                    continue;
-                }
-                const ctp_t tp = const_tp(a.tp) + t;
-                if (!live || !tp->scored) continue;
+                if (t >= a.T) break;                         // wave-uniform
+                const ctp_t tp = tpa + t;
+                if (!tp->scored) continue;                   // wave-uniform
+                const int64_t i = (int64_t)t * a.E + (valid ? e : 0);
                 double first = f[j], meshd = md[j], fail = fa[j], inval = iv[j];
                 uint8_t fj = fl[j];
                 int64_t mt = g[j];
-                if (decay) {
+                bool cf = false, cm = false, cfa = false, ci = false, cfl = false, wmt = false;
+                int64_t mt_store = 0;
+                if (purge) {                                 // score.go:512-516
+                    first = meshd = fail = inval = 0.0;
+                    fj = 0;
+                    cf = cm = cfa = ci = cfl = wmt = true;
+                } else if (decay) {
                     double x;
                     x = first * tp->first_message_deliveries_decay;  if (x < a.dtz) x = 0.0;
-                    if (x != first) { first = x; if (st_ok) a.first[i] = x; }
+                    if (x != first) { first = x; cf = true; }
                     x = meshd * tp->mesh_message_deliveries_decay;   if (x < a.dtz) x = 0.0;
-                    if (x != meshd) { meshd = x; if (st_ok) a.meshd[i] = x; }
+                    if (x != meshd) { meshd = x; cm = true; }
                     x = fail * tp->mesh_failure_penalty_decay;       if (x < a.dtz) x = 0.0;
-                    if (x != fail) { fail = x; if (st_ok) a.fail[i] = x; }
+                    if (x != fail) { fail = x; cfa = true; }
                     x = inval * tp->invalid_message_deliveries_decay; if (x < a.dtz) x = 0.0;
-                    if (x != inval) { inval = x; if (st_ok) a.invalid[i] = x; }
+                    if (x != inval) { inval = x; ci = true; }
+                    // meshTime is refreshed for in-mesh records (score.go:551-556);
+                    // for records outside the mesh it is unobservable (read only
+                    // under inMesh, score.go:286,486) and is stored as 0.
+                    wmt = true;
                     if (fj & GSIM_TF_IN_MESH) {
                         mt = a.now - g[j];
-                        if (st_ok && !(a.diag & DIAG_NO_MTIME)) a.mtime[i] = mt;
+                        mt_store = mt;
                         if (mt > tp->mesh_message_deliveries_activation_ns && !(fj & GSIM_TF_ACTIVE)) {
                             fj |= GSIM_TF_ACTIVE;
-                            if (st_ok) a.tflags[i] = fj;
+                            cfl = true;
                         }
                     }
                 }
-                if (SCORE) {
+                if (SCORE && live) {
                     double ts = 0.0;
                     if (fj & GSIM_TF_IN_MESH) {                               // P1
                         double p1 = 0.0;
@@ -264,6 +290,15 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
                     const double p4 = inval * inval;                           // P4
                     ts += p4 * tp->invalid_message_deliveries_weight;
                     score += ts * tp->topic_weight;
+                }
+                if (REFRESH && st_ok) {
+                    policy_store(a.first, i, first, valid && cf, valid);
+                    policy_store(a.meshd, i, meshd, valid && cm, valid);
+                    policy_store(a.fail, i, fail, valid && cfa, valid);
+                    policy_store(a.invalid, i, inval, valid && ci, valid);
+                    policy_store(a.tflags, i, fj, valid && cfl, valid);
+                    if (!(a.diag & DIAG_NO_MTIME)) policy_store(a.mtime, i, mt_store, valid && wmt, false);
+                    if (purge) a.graft[i] = 0;
                 }
             }
         }

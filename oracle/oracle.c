@@ -68,6 +68,11 @@ void orc_refresh_scores(orc_net* s, int64_t now)
                 int64_t mt = now - s->graft_time[i];  /* now.Sub(tstats.graftTime) */
                 s->mesh_time[i] = mt;
                 if (mt > tp->mesh_message_deliveries_activation_ns) s->tflags[i] |= TF_ACTIVE;
+            } else {
+                /* meshTime of a record outside the mesh is never read (score.go:286,
+                 * 486) and Graft resets it; the restatement normalizes it to 0 so the
+                 * engine may rewrite the plane densely. */
+                s->mesh_time[i] = 0;
             }
         }
         double b = s->bp[e] * pp->behaviour_penalty_decay;
