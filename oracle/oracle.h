@@ -58,6 +58,38 @@ typedef struct orc_net {
     uint8_t* ctl;              /* [2][T][E] control inbox by round parity */
 } orc_net;
 
+/* ---- message propagation (oracle_deliver.c) ------------------------------ */
+/* Message ring and seen-set of the whole network (caller-owned arrays).
+ * seen[slot][peer] = first-seen round (timecache + mcache put time), or
+ * 0xFFFFFFFF when unseen.  Round g happens at
+ *   T(g) = t0 + (g / R) * HB + (g % R + 1) * HB / (R + 1)   (integer ns). */
+typedef struct orc_msgs {
+    int32_t ring, rounds;
+    int64_t t0, hb;
+    uint32_t* topic;           /* [ring] */
+    uint32_t* origin;          /* [ring] */
+    uint8_t*  invalid;         /* [ring] validator verdict: 1 = reject */
+    uint32_t* seen;            /* [ring][N] */
+    int32_t*  lastput;         /* [T][N] tick of the newest mcache.Put per (peer, topic) */
+    int64_t   stats[4];        /* arrivals, first deliveries, duplicates, graylisted */
+    void*     priv;            /* frontier storage (oracle-owned) */
+} orc_msgs;
+
+int64_t orc_round_time(const orc_msgs* m, int64_t g);
+/* Topic.Publish at the origin (pubsub.go:1196-1202 via pushMsg): slot =
+ * id % ring is reset, the origin marks it seen at round g and joins the
+ * forwarding frontier of round g. */
+void orc_publish(orc_net* s, orc_msgs* m, uint64_t id, uint32_t topic, uint32_t origin, uint8_t invalid,
+                 int64_t g);
+/* One propagation round g: receivers process the arrivals forwarded in round
+ * g-1 (AcceptFrom graylist gossipsub.go:598-609; pushMsg pubsub.go:1118-1162:
+ * seen-set check, DeliverMessage/DuplicateMessage/RejectMessage score.go
+ * 702-827), then handle the control inbox of round (g % R), then every
+ * first-receiver forwards to its mesh peers except the sender and the origin
+ * (Publish, gossipsub.go:975-1045). */
+void orc_round(orc_net* s, orc_msgs* m, int64_t g);
+void orc_msgs_free_priv(orc_msgs* m);
+
 /* ---- gossipsub.go heartbeat / control handling (oracle_net.c) ----------- */
 /* One heartbeat (gossipsub.go:1345-1606) for every observer at tick `tick`
  * (heartbeatTicks after the increment) and virtual time now; mesh

@@ -1,0 +1,152 @@
+/*
+ * oracle_deliver.c — network-level restatement of message propagation.
+ * TEST INFRASTRUCTURE (see oracle.h).
+ *
+ * Per round every receiver handles what its mesh peers forwarded in the
+ * previous round, in (receiver, message, receiving-edge) order — the lowest
+ * receiving edge of a round is the first delivery — exactly
+ * as pushMsg would for those RPCs (pubsub.go:1118-1162), then the control
+ * inbox is handled, then every peer that saw a message for the first time
+ * forwards it to its mesh (Publish, gossipsub.go:975-1045).
+ */
+#include "oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#define UNSEEN 0xFFFFFFFFu
+
+typedef struct fr_ent { uint32_t peer, slot, from; } fr_ent;
+typedef struct arr_ent { uint32_t recv, slot, er; } arr_ent;
+
+typedef struct priv {
+    fr_ent* fr; int64_t nfr, capfr;     /* peers that first-saw a message this round */
+    arr_ent* ar; int64_t nar, capar;    /* forwarded this round, handled next round */
+} priv;
+
+static priv* P(orc_msgs* m)
+{
+    if (!m->priv) m->priv = calloc(1, sizeof(priv));
+    return (priv*)m->priv;
+}
+
+void orc_msgs_free_priv(orc_msgs* m)
+{
+    if (!m->priv) return;
+    priv* p = (priv*)m->priv;
+    free(p->fr);
+    free(p->ar);
+    free(p);
+    m->priv = NULL;
+}
+
+static void fr_push(priv* p, uint32_t peer, uint32_t slot, uint32_t from)
+{
+    if (p->nfr == p->capfr) {
+        p->capfr = p->capfr ? 2 * p->capfr : 1024;
+        p->fr = (fr_ent*)realloc(p->fr, sizeof(fr_ent) * (size_t)p->capfr);
+    }
+    p->fr[p->nfr].peer = peer; p->fr[p->nfr].slot = slot; p->fr[p->nfr].from = from;
+    p->nfr++;
+}
+
+static void ar_push(priv* p, uint32_t recv, uint32_t slot, uint32_t er)
+{
+    if (p->nar == p->capar) {
+        p->capar = p->capar ? 2 * p->capar : 4096;
+        p->ar = (arr_ent*)realloc(p->ar, sizeof(arr_ent) * (size_t)p->capar);
+    }
+    p->ar[p->nar].recv = recv; p->ar[p->nar].slot = slot; p->ar[p->nar].er = er;
+    p->nar++;
+}
+
+static int cmp_arr(const void* a, const void* b)
+{
+    const arr_ent* x = (const arr_ent*)a;
+    const arr_ent* y = (const arr_ent*)b;
+    if (x->recv != y->recv) return x->recv < y->recv ? -1 : 1;
+    if (x->slot != y->slot) return x->slot < y->slot ? -1 : 1;
+    return x->er < y->er ? -1 : x->er > y->er;
+}
+
+int64_t orc_round_time(const orc_msgs* m, int64_t g)
+{
+    const int64_t r = g % m->rounds, k = g / m->rounds;
+    return m->t0 + k * m->hb + (r + 1) * m->hb / (m->rounds + 1);
+}
+
+void orc_publish(orc_net* s, orc_msgs* m, uint64_t id, uint32_t topic, uint32_t origin, uint8_t invalid,
+                 int64_t g)
+{
+    const uint32_t slot = (uint32_t)(id % (uint64_t)m->ring);
+    m->topic[slot] = topic;
+    m->origin[slot] = origin;
+    m->invalid[slot] = invalid;
+    uint32_t* row = m->seen + (int64_t)slot * s->n;
+    for (int64_t i = 0; i < s->n; ++i) row[i] = UNSEEN;
+    /* the origin validated and saw its own message (markSeen) and puts it in
+     * its mcache (gossipsub.go:976); its own DeliverMessage is not scored
+     * (trace.go skips ReceivedFrom == self) */
+    row[origin] = (uint32_t)g;
+    m->lastput[(int64_t)topic * s->n + origin] = (int32_t)(g / m->rounds);
+    fr_push(P(m), origin, slot, origin);
+}
+
+void orc_round(orc_net* s, orc_msgs* m, int64_t g)
+{
+    priv* p = P(m);
+    const int64_t now = orc_round_time(m, g);
+    const double gray = s->th->graylist_threshold;
+
+    /* 1. receivers handle last round's forwards, in canonical order */
+    arr_ent* ar = p->ar;
+    const int64_t nar = p->nar;
+    p->ar = NULL; p->nar = 0; p->capar = 0;
+    qsort(ar, (size_t)nar, sizeof(arr_ent), cmp_arr);
+    for (int64_t q = 0; q < nar; ++q) {
+        const uint32_t i = ar[q].recv, slot = ar[q].slot, er = ar[q].er;
+        const int32_t t = (int32_t)m->topic[slot];
+        if (s->score[er] < gray) {             /* AcceptFrom -> AcceptNone */
+            m->stats[3]++;
+            continue;
+        }
+        m->stats[0]++;
+        uint32_t* cell = &m->seen[(int64_t)slot * s->n + i];
+        if (*cell == UNSEEN) {
+            *cell = (uint32_t)g;               /* markSeen */
+            m->stats[1]++;
+            if (m->invalid[slot]) {
+                /* ValidateMessage + RejectMessage(ValidationFailed), score.go:728-793 */
+                orc_mark_invalid(s, er, t);
+            } else {
+                /* DeliverMessage, score.go:702-726; mcache.Put; forward next */
+                orc_mark_first(s, er, t);
+                m->lastput[(int64_t)t * s->n + i] = (int32_t)(g / m->rounds);
+                fr_push(p, i, slot, s->col[er]);
+            }
+        } else {
+            m->stats[2]++;                     /* DuplicateMessage, score.go:795-827 */
+            if (m->invalid[slot]) orc_mark_invalid(s, er, t);
+            else orc_mark_duplicate(s, er, t, 1, orc_round_time(m, (int64_t)*cell), now);
+        }
+    }
+    free(ar);
+
+    /* 2. control records of this round */
+    orc_handle_control(s, (int32_t)(g % m->rounds), now);
+
+    /* 3. first receivers (and this round's publishers) forward to their mesh */
+    for (int64_t q = 0; q < p->nfr; ++q) {
+        const uint32_t j = p->fr[q].peer, slot = p->fr[q].slot, from = p->fr[q].from;
+        const int32_t t = (int32_t)m->topic[slot];
+        const uint32_t origin = m->origin[slot];
+        for (uint32_t e = s->row_ptr[j]; e < s->row_ptr[j + 1]; ++e) {
+            const uint32_t i = s->col[e];
+            if (!(s->tflags[(int64_t)t * s->e + e] & GSIM_TF_MESH)) continue;
+            if (!(s->estate[e] & GSIM_ES_CONNECTED)) continue;
+            if (i == from || i == origin) continue;
+            ar_push(p, i, slot, s->rev[e]);
+        }
+    }
+    p->nfr = 0;
+}

@@ -36,6 +36,14 @@ class OrcNet(Structure):
     ]
 
 
+class OrcMsgs(Structure):
+    _fields_ = [
+        ("ring", c_int32), ("rounds", c_int32), ("t0", c_int64), ("hb", c_int64),
+        ("topic", c_void_p), ("origin", c_void_p), ("invalid", c_void_p), ("seen", c_void_p),
+        ("lastput", c_void_p), ("stats", c_int64 * 4), ("priv", c_void_p),
+    ]
+
+
 _lib = None
 
 
@@ -91,6 +99,10 @@ def load():
             "orc_philox4x32_10": (None, [c_void_p, c_void_p, c_void_p]),
             "orc_heartbeat": (None, [P, c_uint64, c_int64, c_uint64]),
             "orc_handle_control": (c_int64, [P, c_int32, c_int64]),
+            "orc_round_time": (c_int64, [POINTER(OrcMsgs), c_int64]),
+            "orc_publish": (None, [P, POINTER(OrcMsgs), c_uint64, c_uint32, c_uint32, ctypes.c_uint8, c_int64]),
+            "orc_round": (None, [P, POINTER(OrcMsgs), c_int64]),
+            "orc_msgs_free_priv": (None, [POINTER(OrcMsgs)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -174,3 +186,41 @@ class NetState:
         for f in self.TOPIC_FIELDS + self.EDGE_FIELDS:
             getattr(self, f)[...] = eng.read(self.FIELD_IDS[f])
         self.ctl[...] = eng.read(_abi.F_CTL)
+
+
+UNSEEN = 0xFFFFFFFF
+
+
+class Msgs:
+    """Oracle message ring + seen-set of a network (oracle_deliver.c)."""
+
+    def __init__(self, n, T, ring, rounds, t0, hb):
+        self.seen = np.full((ring, n), UNSEEN, dtype=np.uint32)
+        self.topic = np.zeros(ring, dtype=np.uint32)
+        self.origin = np.zeros(ring, dtype=np.uint32)
+        self.invalid = np.zeros(ring, dtype=np.uint8)
+        self.lastput = np.full((T, n), -1, dtype=np.int32)
+        m = OrcMsgs()
+        m.ring, m.rounds, m.t0, m.hb = ring, rounds, t0, hb
+        m.topic, m.origin, m.invalid = _p(self.topic), _p(self.origin), _p(self.invalid)
+        m.seen, m.lastput = _p(self.seen), _p(self.lastput)
+        self.m = m
+
+    @property
+    def stats(self):
+        return list(self.m.stats)
+
+    def round_time(self, g):
+        return load().orc_round_time(ctypes.byref(self.m), g)
+
+    def publish(self, st, mid, topic, origin, invalid, g):
+        load().orc_publish(st.view(), ctypes.byref(self.m), mid, topic, origin, invalid, g)
+
+    def round(self, st, g):
+        load().orc_round(st.view(), ctypes.byref(self.m), g)
+
+    def __del__(self):
+        try:
+            load().orc_msgs_free_priv(ctypes.byref(self.m))
+        except Exception:
+            pass
