@@ -538,14 +538,15 @@ int launch_ip_colocation(gsim_handle* h)
 }
 
 // Kernel variant for the refresh+score pass (A/B): GSIM_SCORE_KERNEL =
-// thread | tile | wave4 | wave8 (default wave4) or gsim_set_kernel_variant().
+// thread | wave4 | wave8 (default thread: measured fastest on MI355X, run 7
+// in DESIGN.md §5) or gsim_set_kernel_variant().
 static int score_variant_from_env()
 {
     const char* s = std::getenv("GSIM_SCORE_KERNEL");
-    if (!s) return 2;
-    if (!std::strcmp(s, "thread")) return 0;
+    if (!s) return 0;
+    if (!std::strcmp(s, "wave4")) return 2;
     if (!std::strcmp(s, "wave8")) return 3;
-    return 2;
+    return 0;
 }
 
 template <bool REFRESH, bool SCORE>
@@ -695,6 +696,7 @@ int gsim_destroy(gsim_handle* h)
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     free_graph(h);
     free_extra(h);
+    free_deliver(h);
     dfree(h->d_tp);
     dfree(h->d_flags);
     for (auto& ev : h->ev)
@@ -752,6 +754,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     (void)hipStreamSynchronize(h->stream);
     free_graph(h);
     free_extra(h);
+    free_deliver(h);
     h->n = n;
     h->e = E;
     h->n_ips = n_ips;
@@ -1035,6 +1038,6 @@ bool field_ref(gsim_handle* h, int32_t f, FieldRef* r)
     case GSIM_F_P6:         *r = {h->d_p6, E * 8}; return true;
     case GSIM_F_SCORE:      *r = {h->d_score, E * 8}; return true;
     case GSIM_F_BACKOFF:    *r = {h->d_backoff, ET * 8}; return true;
-    default: return extra_field_ref(h, f, r);
+    default: return extra_field_ref(h, f, r) || deliver_field_ref(h, f, r);
     }
 }

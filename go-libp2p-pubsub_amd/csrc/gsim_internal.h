@@ -68,6 +68,8 @@ struct FieldRef {
     size_t bytes;
 };
 
+struct Deliver;   // message ring, seen-set and round lists (deliver.hip)
+
 }  // namespace gsim
 
 struct gsim_handle {
@@ -117,8 +119,9 @@ struct gsim_handle {
     double* d_p6 = nullptr;
     double* d_score = nullptr;
 
-    // heartbeat / delivery state lives in heartbeat.hip
+    // heartbeat state lives in heartbeat.hip, message propagation in deliver.hip
     struct Extra* x = nullptr;
+    gsim::Deliver* dl = nullptr;
 };
 
 int hip_check(gsim_handle* h, hipError_t e, const char* what);
@@ -131,3 +134,7 @@ int launch_compute_scores(gsim_handle* h);
 int alloc_extra(gsim_handle* h);
 void free_extra(gsim_handle* h);
 bool extra_field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r);
+
+// implemented in deliver.hip
+void free_deliver(gsim_handle* h);
+bool deliver_field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r);

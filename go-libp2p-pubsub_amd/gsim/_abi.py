@@ -22,7 +22,7 @@ GSIM_ERANGE = -34
 GSIM_ESTATE = -71
 
 (F_FIRST, F_MESHD, F_FAIL, F_INVALID, F_GRAFT_TIME, F_MESH_TIME, F_TFLAGS, F_BP, F_ESTATE,
- F_EXPIRE, F_P6, F_SCORE, F_BACKOFF, F_CTL) = range(14)
+ F_EXPIRE, F_P6, F_SCORE, F_BACKOFF, F_CTL, F_SEEN, F_LASTPUT) = range(16)
 
 TF_IN_MESH = 0x01
 TF_ACTIVE = 0x02
@@ -86,6 +86,21 @@ class CGossipSubParams(Structure):
 
 
 # (name, restype, argtypes) for every symbol include/gsim.h declares.
+class CMsgConfig(Structure):
+    _fields_ = [("ring", c_int32), ("rounds", c_int32), ("t0_ns", c_int64), ("heartbeat_ns", c_int64),
+                ("max_frontier", c_int64), ("max_arrivals", c_int64)]
+
+
+class CMsg(Structure):
+    _fields_ = [("id", c_uint64), ("topic", c_uint32), ("origin", c_uint32), ("invalid", ctypes.c_uint8),
+                ("_pad", ctypes.c_uint8 * 7)]
+
+
+# numpy view of gsim_msg (24 bytes)
+MSG_DTYPE = [("id", "<u8"), ("topic", "<u4"), ("origin", "<u4"), ("invalid", "u1"), ("_pad", "u1", (7,))]
+
+UNSEEN = 0xFFFFFFFF
+
 SIGNATURES = [
     ("gsim_default_gossipsub_params", None, [POINTER(CGossipSubParams)]),
     ("gsim_validate_topic_params", c_int32, [POINTER(CTopicScoreParams), c_char_p, c_size_t]),
@@ -124,6 +139,10 @@ SIGNATURES = [
     ("gsim_census", c_int32, [c_void_p, c_void_p]),
     ("gsim_heartbeat", c_int32, [c_void_p, c_uint64, c_int64]),
     ("gsim_handle_control", c_int32, [c_void_p, c_int32, c_int64]),
+    ("gsim_msgs_init", c_int32, [c_void_p, POINTER(CMsgConfig)]),
+    ("gsim_publish", c_int32, [c_void_p, c_void_p, c_int32, c_int64]),
+    ("gsim_round", c_int32, [c_void_p, c_int64]),
+    ("gsim_msg_stats", c_int32, [c_void_p, c_void_p]),
 ]
 
 _lib = None

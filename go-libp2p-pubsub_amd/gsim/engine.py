@@ -20,7 +20,7 @@ _FIELD_DTYPES = {
     _abi.F_FIRST: np.float64, _abi.F_MESHD: np.float64, _abi.F_FAIL: np.float64, _abi.F_INVALID: np.float64,
     _abi.F_GRAFT_TIME: np.int64, _abi.F_MESH_TIME: np.int64, _abi.F_TFLAGS: np.uint8, _abi.F_BP: np.float64,
     _abi.F_ESTATE: np.uint8, _abi.F_EXPIRE: np.int64, _abi.F_P6: np.float64, _abi.F_SCORE: np.float64,
-    _abi.F_BACKOFF: np.int64, _abi.F_CTL: np.uint8,
+    _abi.F_BACKOFF: np.int64, _abi.F_CTL: np.uint8, _abi.F_SEEN: np.uint32, _abi.F_LASTPUT: np.int32,
 }
 TOPIC_FIELDS = {_abi.F_FIRST, _abi.F_MESHD, _abi.F_FAIL, _abi.F_INVALID, _abi.F_GRAFT_TIME,
                 _abi.F_MESH_TIME, _abi.F_TFLAGS, _abi.F_BACKOFF}
@@ -189,6 +189,10 @@ class Engine:
         e = self.net.e
         if f in PARITY_TOPIC_FIELDS:
             return (2, max(1, len(self.topics)), e)
+        if f == _abi.F_SEEN:
+            return (self._msg_cfg.ring, self.net.n)
+        if f == _abi.F_LASTPUT:
+            return (max(1, len(self.topics)), self.net.n)
         return (max(1, len(self.topics)), e) if f in TOPIC_FIELDS else (e,)
 
     # -- heartbeat / control ------------------------------------------------------
@@ -209,6 +213,38 @@ class Engine:
     def handle_control(self, rnd: int, now: int):
         """handleGraft/handlePrune for the inbox of control round `rnd`."""
         self._check(self.lib.gsim_handle_control(self.h, int(rnd), int(now)))
+
+    # -- message propagation ------------------------------------------------------
+    def msgs_init(self, ring: int, rounds: int, t0: int, heartbeat: Optional[int] = None,
+                  max_frontier: Optional[int] = None, max_arrivals: Optional[int] = None):
+        """Allocate the message ring / seen-set (gsim_msgs_init)."""
+        c = _abi.CMsgConfig()
+        c.ring, c.rounds, c.t0_ns = int(ring), int(rounds), int(t0)
+        c.heartbeat_ns = int(heartbeat if heartbeat is not None else self.gossip.HeartbeatInterval)
+        c.max_frontier = int(max_frontier if max_frontier is not None else max(4 * self.net.n, 1024))
+        c.max_arrivals = int(max_arrivals if max_arrivals is not None else max(2 * self.net.e, 4096))
+        self._check(self.lib.gsim_msgs_init(self.h, ctypes.byref(c)))
+        self._msg_cfg = c
+
+    def round_time(self, g: int) -> int:
+        c = self._msg_cfg
+        return c.t0_ns + (g // c.rounds) * c.heartbeat_ns + (g % c.rounds + 1) * c.heartbeat_ns // (c.rounds + 1)
+
+    def publish(self, msgs, rnd: int):
+        """Topic.Publish of each (id, topic, origin, invalid) at its origin in round `rnd`."""
+        arr = np.zeros(len(msgs), dtype=_abi.MSG_DTYPE)
+        for k, (mid, topic, origin, invalid) in enumerate(msgs):
+            arr[k]["id"], arr[k]["topic"], arr[k]["origin"], arr[k]["invalid"] = mid, topic, origin, invalid
+        self._check(self.lib.gsim_publish(self.h, _ptr(arr), len(arr), int(rnd)))
+
+    def round(self, rnd: int):
+        """One propagation round for the whole network (gsim_round)."""
+        self._check(self.lib.gsim_round(self.h, int(rnd)))
+
+    def msg_stats(self) -> list:
+        out = np.zeros(4, dtype=np.int64)
+        self._check(self.lib.gsim_msg_stats(self.h, _ptr(out)))
+        return [int(x) for x in out]
 
     def read(self, f: int) -> np.ndarray:
         out = np.empty(self.field_shape(f), dtype=_FIELD_DTYPES[f])

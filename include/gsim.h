@@ -226,6 +226,55 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now_ns);
  * of round+1. */
 int gsim_handle_control(gsim_handle* h, int32_t round, int64_t now_ns);
 
+/* ---- message propagation ------------------------------ */
+/* Rounds are numbered globally: round g belongs to heartbeat tick g / rounds
+ * and happens at virtual time
+ *   T(g) = t0 + (g / rounds) * heartbeat + (g % rounds + 1) * heartbeat / (rounds + 1).
+ * The seen-set is a ring of `ring` message slots x N peers (u32 first-seen
+ * round, 0xFFFFFFFF = unseen): the timecache (timecache/first_seen_cache.go)
+ * restricted to messages that can still arrive.  A slot may be reused once
+ * its message can no longer be forwarded or gossiped; SeenMsgTTL must
+ * outlast that (it does for every reference configuration). */
+typedef struct gsim_msg_config {
+    int32_t ring;            /* message slots (live-message window) */
+    int32_t rounds;          /* propagation rounds per heartbeat, >= 2 */
+    int64_t t0_ns;           /* virtual time of tick 0 */
+    int64_t heartbeat_ns;    /* heartbeat interval (GossipSubParams.HeartbeatInterval) */
+    int64_t max_frontier;    /* capacity: first receptions per round */
+    int64_t max_arrivals;    /* capacity: forwarded message copies per round */
+} gsim_msg_config;
+
+/* One published message (Topic.Publish, topic.go:217-283, at its origin). */
+typedef struct gsim_msg {
+    uint64_t id;             /* message id; slot = id % ring */
+    uint32_t topic;          /* dense topic index */
+    uint32_t origin;         /* publishing peer (must be subscribed) */
+    uint8_t  invalid;        /* validator verdict: 1 = ValidationFailed at every receiver */
+    uint8_t  _pad[7];
+} gsim_msg;
+
+/* Allocate the message ring, seen-set and round buffers (after load_graph). */
+int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg);
+/* Publish `count` messages in round g: each slot is reset, the origin marks
+ * the message seen (markSeen, pubsub.go:987-995) and puts it in its mcache
+ * (gossipsub.go:976); the origin forwards it in round g. */
+int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t round);
+/* Propagation round g for the whole network:
+ *  1. every receiver handles the copies forwarded to it in round g-1, in
+ *     (message, receiving connection) order: AcceptFrom graylist
+ *     (gossipsub.go:598-609), seen-set check (pubsub.go:1118-1162), then
+ *     DeliverMessage / DuplicateMessage / RejectMessage (score.go:693-827);
+ *     of several same-round copies the lowest connection is the first;
+ *  2. control inbox of round g % rounds (rounds 0 and 1 of a heartbeat);
+ *  3. every peer that saw a message for the first time in round g forwards
+ *     it to its mesh except the sender and the origin (gossipsub.go:975-1045). */
+int gsim_round(gsim_handle* h, int64_t round);
+/* Cumulative totals since gsim_msgs_init: out4 = {msg-edge deliveries
+ * (accepted arrivals, duplicates included), first deliveries, duplicates,
+ * graylisted arrivals}.  Synchronizes.  GSIM_ERANGE when a round overflowed
+ * max_frontier or max_arrivals (results are then incomplete). */
+int gsim_msg_stats(gsim_handle* h, int64_t* out4);
+
 /* Aggregate census of the state (the network-wide analogue of the
  * reference's score inspection, score.go:448-500): out8 = {connected scored
  * edge-topic records, of those inMesh, non-zero firstMessageDeliveries,
@@ -252,6 +301,8 @@ typedef enum gsim_field {
     GSIM_F_SCORE,         /* f64 [E]    score snapshot                  */
     GSIM_F_BACKOFF,       /* i64 [T][E] prune backoff expiry, 0 = none gossipsub.go:432 */
     GSIM_F_CTL,           /* u8 [2][T][E] control inbox by round parity (receiver's edge) */
+    GSIM_F_SEEN,          /* u32 [ring][N] first-seen round, 0xFFFFFFFF unseen (after msgs_init) */
+    GSIM_F_LASTPUT,       /* i32 [T][N] tick of the newest mcache.Put, -1 none (after msgs_init) */
     GSIM_F__COUNT
 } gsim_field;
 

@@ -45,7 +45,8 @@ def test_struct_layout_matches_c(tmp_path):
     """Compile a probe against gsim.h and compare sizeof/offsetof with ctypes."""
     import subprocess
     structs = {"gsim_topic_score_params": _abi.CTopicScoreParams, "gsim_peer_score_params": _abi.CPeerScoreParams,
-               "gsim_thresholds": _abi.CThresholds, "gsim_gossipsub_params": _abi.CGossipSubParams}
+               "gsim_thresholds": _abi.CThresholds, "gsim_gossipsub_params": _abi.CGossipSubParams,
+               "gsim_msg_config": _abi.CMsgConfig, "gsim_msg": _abi.CMsg}
     lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "gsim.h"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')

@@ -197,3 +197,75 @@ def test_lastput_tracks_newest_mcache_put_per_topic():
     run_rounds(st, msgs, g0, g0 + R - 2)
     assert (msgs.lastput[1] == 3).all()
     assert (msgs.lastput[0] == -1).all()
+
+
+# ---- GPU parity -------------------------------------------------------------------
+
+def _schedule(rng, ticks, T, R, rate, inv_frac, n):
+    """Poisson publications per (round, topic): {round: [(id, topic, origin, invalid)]}."""
+    sched, mid = {}, 0
+    for k in ticks:
+        for r in range(R):
+            g = k * R + r
+            batch = []
+            for t in range(T):
+                for _ in range(rng.poisson(rate / R)):
+                    batch.append((mid, t, int(rng.integers(0, n)), int(rng.random() < inv_frac)))
+                    mid += 1
+            if batch:
+                sched[g] = batch
+    return sched
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k,T,ticks,rate,inv_frac,retained,ring", [
+    (1500, 16, 2, [1, 2, 3, 4], 6, 0.1, 0.0, 64),
+    (3000, 32, 3, [14, 15, 16], 12, 0.05, 0.03, 64),     # ring slots reused; clearBackoff tick
+])
+def test_rounds_bit_exact(require_gpu, n, k, T, ticks, rate, inv_frac, retained, ring):
+    from fixtures import beacon_params, beacon_topic, randomize_state
+    from gsim.engine import Engine, random_regular
+    from test_heartbeat import _random_mesh_state, assert_same
+    rng = np.random.default_rng(n + k)
+    params = beacon_params(T)
+    # a short duplicate window on one topic: only near-simultaneous copies count
+    params.Topics["topic01"] = beacon_topic(MeshMessageDeliveriesWindow=150 * 10**6)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2)
+    th = PeerScoreThresholds(GossipThreshold=-100, PublishThreshold=-200, GraylistThreshold=-300)
+    net = random_regular(n, k, seed=n, n_topics=T)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    randomize_state(st, rng, tick_time(0), retained_frac=retained)
+    _random_mesh_state(st, rng, 0.3)
+    msgs = ob.Msgs(n, T, ring, R, T0, HB)
+    eng = Engine(params, th, gossip=gp)
+    eng.load_graph(net)
+    eng.set_seed(SEED)
+    st.push_to_engine(eng)
+    eng.msgs_init(ring, R, T0, HB)
+    sched = _schedule(rng, ticks, T, R, rate, inv_frac, n)
+    lib = ob.load()
+    for kk in ticks:
+        now = tick_time(kk)
+        eng.refresh_scores(now)
+        eng.heartbeat(kk, now)
+        v = st.view()
+        lib.orc_refresh_scores(v, now)
+        lib.orc_ip_colocation(v)
+        lib.orc_compute_scores(v)
+        lib.orc_heartbeat(v, kk, now, SEED)
+        for g in range(kk * R, kk * R + R):
+            for (mid, t, o, inv) in sched.get(g, []):
+                msgs.publish(st, mid, t, o, inv, g)
+            if g in sched:
+                eng.publish(sched[g], g)
+            msgs.round(st, g)
+            eng.round(g)
+        gpu = ob.NetState(net, params, thresholds=th, gossip=gp)
+        gpu.pull_from_engine(eng)
+        assert_same(st, gpu)
+        seen = eng.read(_abi.F_SEEN)
+        assert np.array_equal(seen, msgs.seen), f"seen-set differs at tick {kk}: {(seen != msgs.seen).sum()} cells"
+        assert np.array_equal(eng.read(_abi.F_LASTPUT), msgs.lastput)
+        assert eng.msg_stats() == msgs.stats
+    assert msgs.stats[1] > 0 and msgs.stats[2] > 0
+    eng.close()
