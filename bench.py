@@ -1,13 +1,20 @@
 #!/usr/bin/env python3
-"""bench.py — peer-heartbeat updates/sec on the 1M-peer, 16-topic network (C3).
+"""bench.py — peer-heartbeat updates/sec + msg-edge deliveries/sec on the
+1M-peer, 16-topic network (C3), one MI355X per rank.
 
 A "step" is one heartbeat tick of the whole simulated network with every byte
 of state resident in HBM:
-  refreshScores+score (decay, P1-P7 snapshot)  -> k_refresh_score_tile
-  heartbeat mesh maintenance (all peers/topics) -> k_heartbeat
-  control rounds 0 and 1 (GRAFT/PRUNE handling) -> k_handle_control x2
+  refreshScores+score (decay, P1-P7 snapshot)        k_refresh_score
+  heartbeat mesh maintenance (all peers, all topics)  k_heartbeat
+  10 propagation rounds, each: publications (Poisson 4 msg/s/topic, seed 2),
+  seen-set claim/resolve + delivery counters, control inbox (rounds 0-1),
+  mesh forwarding                                     k_publish, k_claim,
+                                                      k_resolve, k_handle_control,
+                                                      k_forward
 W untimed warmup ticks, then exactly K timed ticks bracketed by barrier +
-device sync; max over ranks; rank 0 prints one JSON line.
+device sync; max over ranks; rank 0 prints one JSON line.  Per-kernel-class
+device time comes from HIP events recorded on the engine stream around every
+launch inside the timed region (gsim_profile).
 
 Multi-GPU: each rank simulates its own 1M-peer network on its own GPU (weak
 scaling, "replicas only" until the sharded halo-exchange path lands;
@@ -30,6 +37,9 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 SECOND = 1_000_000_000
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 ROUNDS = 10                    # propagation rounds per heartbeat
+MSG_RATE = 4.0                 # messages / s / topic
+MSG_RING = 512                 # live-message window (>= 8 heartbeats of publications)
+DUP_BYTES, FIRST_BYTES = 40, 72   # algorithmic bytes per delivery
 
 CONFIGS = {
     # id: (peers, degree, topics, D, Dlo, Dhi)
@@ -52,6 +62,28 @@ def tick_time(k: int) -> int:
     return 3600 * SECOND + k * SECOND
 
 
+def message_schedule(n: int, T: int, ticks: range, seed: int = 2) -> dict:
+    """{round: gsim_msg array}: Poisson(MSG_RATE) messages per topic per
+    heartbeat, each in a uniform round of its tick, origin uniform."""
+    from gsim import _abi
+    rng = np.random.default_rng(seed)
+    out, mid = {}, 0
+    for k in ticks:
+        per_round = [[] for _ in range(ROUNDS)]
+        for t in range(T):
+            for _ in range(rng.poisson(MSG_RATE)):
+                per_round[int(rng.integers(0, ROUNDS))].append((mid, t, int(rng.integers(0, n))))
+                mid += 1
+        for r, lst in enumerate(per_round):
+            if lst:
+                a = np.zeros(len(lst), dtype=_abi.MSG_DTYPE)
+                a["id"] = [x[0] for x in lst]
+                a["topic"] = [x[1] for x in lst]
+                a["origin"] = [x[2] for x in lst]
+                out[k * ROUNDS + r] = a
+    return out
+
+
 def build_engine(cfg, seed, device):
     import gsim
     from fixtures import beacon_params, beacon_thresholds
@@ -63,37 +95,41 @@ def build_engine(cfg, seed, device):
     eng.load_graph(net)
     eng.set_seed(0x5EED0000 + seed)
     eng.fill_synthetic(seed=seed * 7919 + 1, now=tick_time(0), p_mesh=D / k)
+    eng.msgs_init(MSG_RING, ROUNDS, tick_time(0), SECOND,
+                  max_frontier=max(16 * n, 1 << 16), max_arrivals=max(8 * net.e, 1 << 20))
     return eng, net
 
 
-def run_tick(eng, k):
+def run_tick(eng, k, sched):
     now = tick_time(k)
-    dt = SECOND // (ROUNDS + 1)
     eng.refresh_scores(now)
     eng.heartbeat(k, now)
-    eng.handle_control(0, now + dt)
-    eng.handle_control(1, now + 2 * dt)
+    for g in range(k * ROUNDS, (k + 1) * ROUNDS):
+        m = sched.get(g)
+        if m is not None:
+            eng.publish_array(m, g)
+        eng.round(g)
 
 
 def cpu_baseline(cfg, budget_s: float = 15.0):
-    """Time the C oracle (OpenMP over observers) on a bounded sample of the
-    same workload: same degree, topics and parameters, 50k peers."""
+    """Time the C oracle (OpenMP over observers in the heartbeat phases) on a
+    bounded sample of the same workload: same degree, topics, parameters and
+    message rate, 50k peers."""
     import oracle_binding as ob
-    from fixtures import beacon_params, beacon_thresholds, randomize_state
+    from fixtures import beacon_params, beacon_thresholds, synthetic_state
     import gsim
     n, k, T, D, Dlo, Dhi = 50_000, cfg[1], cfg[2], cfg[3], cfg[4], cfg[5]
     net = gsim.random_regular(n, k, seed=2, n_topics=T)
     params = beacon_params(T)
     st = ob.NetState(net, params, thresholds=beacon_thresholds(), gossip=gsim.GossipSubParams(D=D, Dlo=Dlo, Dhi=Dhi))
-    rng = np.random.default_rng(3)
-    randomize_state(st, rng, tick_time(0), retained_frac=0.0)
-    st.tflags[...] = np.where(rng.random(st.tflags.shape) < D / k, 0x05, 0).astype(np.uint8)
+    synthetic_state(st, np.random.default_rng(3), tick_time(0), D / k)   # gsim_fill_synthetic's distributions
+    msgs = ob.Msgs(n, T, MSG_RING, ROUNDS, tick_time(0), SECOND)
+    sched = message_schedule(n, T, range(1, 201))
     lib = ob.load()
     v = st.view()
     lib.orc_ip_colocation(v)
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     steps = 0
-    dt = SECOND // (ROUNDS + 1)
     t0 = time.perf_counter()
     while True:
         kk = steps + 1
@@ -101,15 +137,19 @@ def cpu_baseline(cfg, budget_s: float = 15.0):
         lib.orc_refresh_scores(v, now)
         lib.orc_compute_scores(v)
         lib.orc_heartbeat(v, kk, now, 0x5EED0001)
-        lib.orc_handle_control(v, 0, now + dt)
-        lib.orc_handle_control(v, 1, now + 2 * dt)
+        for g in range(kk * ROUNDS, (kk + 1) * ROUNDS):
+            for m in sched.get(g, []):
+                msgs.publish(st, int(m["id"]), int(m["topic"]), int(m["origin"]), 0, g)
+            msgs.round(st, g)
         steps += 1
         if time.perf_counter() - t0 > budget_s or steps >= 200:
             break
     el = time.perf_counter() - t0
     return {"value": n * steps / el, "unit": "peer-heartbeat updates/sec", "cores": threads, "kind": "port",
-            "sample": f"C oracle heartbeat tick (refreshScores+score, mesh maintenance, 2 control rounds) on a "
-                      f"{n}-peer k={k} T={T} network, {steps} ticks, OpenMP {threads} threads, {el:.1f}s"}
+            "msg_edge_deliveries_per_sec": msgs.stats[0] / el,
+            "sample": f"C oracle heartbeat tick (refreshScores+score, mesh maintenance, {ROUNDS} propagation "
+                      f"rounds at {MSG_RATE:g} msg/s/topic) on a {n}-peer k={k} T={T} network, {steps} ticks, "
+                      f"OpenMP {threads} threads in the heartbeat phases, {el:.1f}s"}
 
 
 def load_traffic(workload: str):
@@ -130,8 +170,6 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
-    if args.steps * 3 + 1 > 512:
-        raise SystemExit("--steps must be <= 170 (event pool)")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -147,13 +185,15 @@ def main():
     n, k, T = cfg[0], cfg[1], cfg[2]
     eng, net = build_engine(cfg, seed=1 + rank, device=local)
     E = net.e
+    sched = message_schedule(n, T, range(1, args.warmup + args.steps + 1), seed=2 + rank)
 
     kk = 0
     for _ in range(args.warmup):
         kk += 1
-        run_tick(eng, kk)
+        run_tick(eng, kk, sched)
     eng.synchronize()
     census0 = eng.census()
+    stats0 = eng.msg_stats()
 
     def barrier():
         if dist is not None:
@@ -163,64 +203,82 @@ def main():
             torch.cuda.synchronize()
 
     barrier()
+    eng.profile(True)
     eng.synchronize()
     t0 = time.perf_counter()
-    dt = SECOND // (ROUNDS + 1)
     for s in range(args.steps):
         kk += 1
-        now = tick_time(kk)
-        eng.event_record(3 * s)
-        eng.refresh_scores(now)
-        eng.event_record(3 * s + 1)
-        eng.heartbeat(kk, now)
-        eng.event_record(3 * s + 2)
-        eng.handle_control(0, now + dt)
-        eng.handle_control(1, now + 2 * dt)
-    eng.event_record(3 * args.steps)
+        run_tick(eng, kk, sched)
     eng.synchronize()
     barrier()
     wall = time.perf_counter() - t0
-    ph = np.zeros(3)
-    for s in range(args.steps):
-        ph += [eng.event_elapsed_ms(3 * s + j, 3 * s + j + 1) for j in range(3)]
-    ph /= args.steps
+    prof = eng.profile_read()
+    eng.profile(False)
     census1 = eng.census()
+    stats1 = eng.msg_stats()
     if dist is not None:
         import torch
         t = torch.tensor([wall], device=f"cuda:{local}", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
+        d = torch.tensor([stats1[0] - stats0[0]], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(d)
+        deliveries = float(d.item())
+    else:
+        deliveries = float(stats1[0] - stats0[0])
 
     if rank == 0:
-        workload = f"{args.config}: {n} peers, random-regular k={k}, {T} topics, beacon-style params"
-        value = n * world * args.steps / wall
-        alg = (refresh_bytes(census0, E) + refresh_bytes(census1, E)) // 2
-        refresh_ms = float(ph[0])
-        achieved = alg / (refresh_ms * 1e-3) / 1e9
+        K = args.steps
+        workload = (f"{args.config}: {n} peers, random-regular k={k}, {T} topics, beacon-style params, "
+                    f"{MSG_RATE:g} msg/s/topic, {ROUNDS} rounds/heartbeat")
+        value = n * world * K / wall
+        kms = {c: ms / K for c, (ms, _) in prof.items()}        # per tick
+        launches = {c: cnt for c, (_, cnt) in prof.items()}
+        # refresh+score: census-based compulsory bytes per launch
+        alg_refresh = (refresh_bytes(census0, E) + refresh_bytes(census1, E)) // 2
+        ref_ms = prof["refresh_score"][0] / max(1, launches["refresh_score"])
+        ref_gbs = alg_refresh / (ref_ms * 1e-3) / 1e9
+        # delivery: SURVEY.md §8(d) bytes per first / duplicate delivery, over claim+resolve+forward
+        firsts = stats1[1] - stats0[1]
+        dups = stats1[2] - stats0[2]
+        alg_deliv = (FIRST_BYTES * firsts + DUP_BYTES * dups) / K
+        deliv_ms = kms["claim"] + kms["resolve"] + kms["forward"]
+        deliv_gbs = alg_deliv / (deliv_ms * 1e-3) / 1e9 if deliv_ms > 0 else 0.0
+        roof_refresh = {"bound": "hbm", "achieved": ref_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": ref_gbs / HBM_PEAK_GBS, "traffic": load_traffic(args.config),
+                        "kernel": "k_refresh_score<true,true>", "kernel_ms": ref_ms,
+                        "algorithmic_bytes_per_launch": alg_refresh}
+        roof_deliv = {"bound": "hbm", "achieved": deliv_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": deliv_gbs / HBM_PEAK_GBS, "traffic": None,
+                      "kernel": "k_claim+k_resolve+k_forward (per tick)", "kernel_ms": deliv_ms,
+                      "algorithmic_bytes_per_tick": alg_deliv}
+        dominant = roof_refresh if ref_ms * launches["refresh_score"] / K >= deliv_ms else roof_deliv
         out = {
             "metric": "peer-heartbeat updates/sec + msg-edge deliveries/sec, 1M-peer gossipsub sim",
             "value": value,
             "unit": "peer-heartbeat updates/sec",
             "n_gpus": world,
-            "steps": args.steps,
+            "steps": K,
             "warmup": args.warmup,
-            "ms_per_step": wall / args.steps * 1e3,
+            "ms_per_step": wall / K * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (seeded random-regular graph, Philox-seeded steady-state counters and meshes)",
+            "data": "synthetic (seeded random-regular graph, Philox-seeded steady-state counters and meshes, "
+                    "Poisson message publications)",
             "config": {"workload": workload, "peers_per_gpu": n, "degree": k, "topics": T,
-                       "edge_topic_records": E * T,
-                       "step": "heartbeat tick: refreshScores+score, mesh maintenance, 2 control rounds",
+                       "edge_topic_records": E * T, "rounds_per_heartbeat": ROUNDS,
+                       "step": "heartbeat tick: refreshScores+score, mesh maintenance, "
+                               f"{ROUNDS} propagation rounds (publish, deliver, control, forward)",
                        "parallelism": f"replica-per-gpu x{world}"},
-            "phases_ms": {"refresh_score": refresh_ms, "heartbeat": float(ph[1]), "control_rounds": float(ph[2])},
+            "msg_edge_deliveries_per_sec": deliveries / wall,
+            "deliveries_per_tick": {"accepted": (stats1[0] - stats0[0]) / K, "first": firsts / K,
+                                    "duplicate": dups / K, "graylisted": (stats1[3] - stats0[3]) / K},
+            "kernel_ms_per_tick": kms,
             "census": census1,
-            "msg_edge_deliveries_per_sec": None,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.config),
-                         "kernel": "k_refresh_score_tile<true,true>", "kernel_ms": refresh_ms,
-                         "algorithmic_bytes_per_launch": alg},
+            "roofline": dominant,
+            "roofline_kernels": {"refresh_score": roof_refresh, "delivery": roof_deliv},
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(cfg)

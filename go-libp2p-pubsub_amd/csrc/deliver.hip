@@ -239,8 +239,10 @@ __global__ void k_forward(RoundArgs a)
     for (uint32_t q = wid; q < n; q += waves) {
         const uint32_t j = a.f_peer[q], slot = a.f_slot[q], from = a.f_from[q];
         if (lane == 0) a.seen[(int64_t)slot * a.N + j] = (uint32_t)a.g;
-        if (a.minv[slot]) continue;
         const uint32_t t = a.mtopic[slot], origin = a.morigin[slot];
+        // receivers reject an invalid message and do not forward it; its
+        // origin publishes it regardless
+        if (a.minv[slot] && j != origin) continue;
         const uint32_t b = a.row_ptr[j], e_end = a.row_ptr[j + 1];
         const uint8_t* fl = a.tflags + (int64_t)t * a.E;
         for (uint32_t e0 = b; e0 < e_end; e0 += 64) {
@@ -412,6 +414,7 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
     }
     e = hipMemcpyAsync(d->d_pub, msgs, sizeof(gsim_msg) * (size_t)count, hipMemcpyHostToDevice, h->stream);
     if (e != hipSuccess) return hip_check(h, e, "publish upload");
+    ProfScope ps(h, GSIM_K_PUBLISH);
     const int64_t per_block = 256 * 16;
     const int gx = (int)std::min<int64_t>((h->n + per_block - 1) / per_block, 1024);
     hipLaunchKernelGGL(k_reset_slots, dim3(std::max(gx, 1), count), dim3(256), 0, h->stream, d->d_seen, h->n,
@@ -435,8 +438,14 @@ int gsim_round(gsim_handle* h, int64_t round)
         return GSIM_ESTATE;
     }
     RoundArgs a = make_round_args(h, round);
-    hipLaunchKernelGGL(k_claim, dim3(kListGrid), dim3(256), 0, h->stream, a);
-    hipLaunchKernelGGL(k_resolve, dim3(kListGrid), dim3(256), 0, h->stream, a);
+    {
+        ProfScope ps(h, GSIM_K_CLAIM);
+        hipLaunchKernelGGL(k_claim, dim3(kListGrid), dim3(256), 0, h->stream, a);
+    }
+    {
+        ProfScope ps(h, GSIM_K_RESOLVE);
+        hipLaunchKernelGGL(k_resolve, dim3(kListGrid), dim3(256), 0, h->stream, a);
+    }
     int rc = hip_check(h, hipGetLastError(), "k_claim/k_resolve");
     if (rc) return rc;
     const int32_t r = (int32_t)(round % d->cfg.rounds);
@@ -446,7 +455,10 @@ int gsim_round(gsim_handle* h, int64_t round)
         rc = gsim_handle_control(h, r, a.now);
         if (rc) return rc;
     }
-    hipLaunchKernelGGL(k_forward, dim3(kListGrid), dim3(256), 0, h->stream, a);
+    {
+        ProfScope ps(h, GSIM_K_FORWARD);
+        hipLaunchKernelGGL(k_forward, dim3(kListGrid), dim3(256), 0, h->stream, a);
+    }
     d->next_round = round + 1;
     return hip_check(h, hipGetLastError(), "k_forward");
 }

@@ -400,10 +400,10 @@ __global__ __launch_bounds__(256) void k_fill_synthetic(ScoreArgs a, uint64_t se
             a.first[i] = (double)(q.x % 2000u) * 0.25;
             a.meshd[i] = in_mesh ? (double)(q.y % 1600u) * 0.25 : 0.0;
             a.fail[i] = (q.z & 7) == 0 ? (double)(q.z % 4000u) * 0.125 : 0.0;
-            a.invalid[i] = (q.w & 31) == 0 ? (double)(q.w % 64u) * 0.125 : 0.0;
+            a.invalid[i] = (q.w & 511) == 0 ? (double)(q.w % 64u) * 0.125 : 0.0;
         }
         const u32x4 b = philox4x32_10((uint32_t)e, (uint32_t)(e >> 32), 0x5eed, 3, k0, k1);
-        a.bp[e] = (b.x & 3) == 0 ? (double)(b.y % 200u) * 0.125 : 0.0;
+        a.bp[e] = (b.x & 15) == 0 ? (double)(b.y % 100u) * 0.125 : 0.0;
         a.estate[e] = GSIM_ES_TRACKED | GSIM_ES_CONNECTED;
         a.expire[e] = 0;
     }
@@ -528,6 +528,7 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
 
 int launch_ip_colocation(gsim_handle* h)
 {
+    ProfScope ps(h, GSIM_K_IP_COLOCATION);
     ColocArgs c{};
     c.E = h->e; c.row_ptr = h->d_row_ptr; c.col = h->d_col; c.owner = h->d_owner;
     c.ip_ptr = h->d_ip_ptr; c.ip_ids = h->d_ip_ids; c.ip_white = h->has_white ? h->d_ip_white : nullptr;
@@ -552,6 +553,7 @@ static int score_variant_from_env()
 template <bool REFRESH, bool SCORE>
 static void launch_score_kernel(gsim_handle* h, const ScoreArgs& a)
 {
+    ProfScope ps(h, REFRESH ? GSIM_K_REFRESH_SCORE : GSIM_K_SCORE);
     if (h->score_variant < 0) h->score_variant = score_variant_from_env();
     const int64_t tiles = (h->e + kTileEdges - 1) / kTileEdges;
     switch (h->score_variant) {
@@ -701,6 +703,7 @@ int gsim_destroy(gsim_handle* h)
     dfree(h->d_flags);
     for (auto& ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
+    for (auto& ev : h->prof_pool) (void)hipEventDestroy(ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return GSIM_OK;
@@ -1019,7 +1022,67 @@ int gsim_synchronize(gsim_handle* h)
     return hip_check(h, hipStreamSynchronize(h->stream), "hipStreamSynchronize");
 }
 
+int gsim_profile(gsim_handle* h, int32_t enable)
+{
+    GSIM_ENTER(h);
+    hipError_t e = hipStreamSynchronize(h->stream);
+    h->prof_on = enable != 0;
+    h->prof_used = 0;
+    h->prof_lost = false;
+    h->prof_marks.clear();
+    return hip_check(h, e, "gsim_profile");
+}
+
+int gsim_profile_read(gsim_handle* h, double* ms, int64_t* launches, int32_t n)
+{
+    GSIM_ENTER(h);
+    if (n < 0 || (n > 0 && (!ms || !launches))) return GSIM_EINVAL;
+    for (int32_t c = 0; c < n; ++c) { ms[c] = 0.0; launches[c] = 0; }
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "gsim_profile_read");
+    for (const auto& m : h->prof_marks) {
+        float t = 0.f;
+        e = hipEventElapsedTime(&t, h->prof_pool[m.a], h->prof_pool[m.b]);
+        if (e != hipSuccess) return hip_check(h, e, "hipEventElapsedTime");
+        if (m.cls < n) { ms[m.cls] += t; launches[m.cls] += 1; }
+    }
+    const bool lost = h->prof_lost;
+    h->prof_marks.clear();
+    h->prof_used = 0;
+    h->prof_lost = false;
+    if (lost) { h->err = "profile event pool exhausted; totals are partial"; return GSIM_ERANGE; }
+    return GSIM_OK;
+}
+
 }  // extern "C"
+
+static int32_t prof_mark(gsim_handle* h)
+{
+    constexpr size_t kProfMax = 1 << 16;
+    if (!h->prof_on) return -1;
+    if (h->prof_used == h->prof_pool.size()) {
+        hipEvent_t ev = nullptr;
+        if (h->prof_pool.size() >= kProfMax || hipEventCreate(&ev) != hipSuccess) {
+            h->prof_lost = true;
+            return -1;
+        }
+        h->prof_pool.push_back(ev);
+    }
+    if (hipEventRecord(h->prof_pool[h->prof_used], h->stream) != hipSuccess) {
+        h->prof_lost = true;
+        return -1;
+    }
+    return (int32_t)h->prof_used++;
+}
+
+ProfScope::ProfScope(gsim_handle* hh, int32_t c) : h(hh), cls(c), a(prof_mark(hh)) {}
+
+ProfScope::~ProfScope()
+{
+    if (a < 0) return;
+    const int32_t b = prof_mark(h);
+    if (b >= 0) h->prof_marks.push_back({cls, (uint32_t)a, (uint32_t)b});
+}
 
 bool field_ref(gsim_handle* h, int32_t f, FieldRef* r)
 {

@@ -119,6 +119,14 @@ struct gsim_handle {
     double* d_p6 = nullptr;
     double* d_score = nullptr;
 
+    // per-kernel-class device timing (gsim_profile); events are pooled
+    struct ProfMark { int32_t cls; uint32_t a, b; };
+    bool prof_on = false;
+    bool prof_lost = false;
+    std::vector<hipEvent_t> prof_pool;
+    size_t prof_used = 0;
+    std::vector<ProfMark> prof_marks;
+
     // heartbeat state lives in heartbeat.hip, message propagation in deliver.hip
     struct Extra* x = nullptr;
     gsim::Deliver* dl = nullptr;
@@ -129,6 +137,16 @@ bool field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r);
 int launch_ip_colocation(gsim_handle* h);
 int launch_refresh_scores(gsim_handle* h, int64_t now);
 int launch_compute_scores(gsim_handle* h);
+
+// Brackets the launches of one kernel class with pooled HIP events on the
+// engine stream while profiling is enabled (gsim_profile).
+struct ProfScope {
+    gsim_handle* h;
+    int32_t cls;
+    int32_t a;
+    ProfScope(gsim_handle* hh, int32_t c);
+    ~ProfScope();
+};
 
 // implemented in heartbeat.hip
 int alloc_extra(gsim_handle* h);

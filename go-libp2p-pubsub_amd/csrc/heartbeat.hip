@@ -119,7 +119,6 @@ __device__ __forceinline__ void stats_prune(const HbArgs& a, bool tracked, bool 
 // One wavefront = one observer's heartbeat (gossipsub.go:1345-1557).
 __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
 {
-    __shared__ uint8_t s_plst[4][64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (int64_t obs = (int64_t)blockIdx.x * 4 + wid; obs < a.N; obs += (int64_t)gridDim.x * 4) {
         const uint32_t b = a.row_ptr[obs];
@@ -134,7 +133,6 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
         const double S = valid ? a.score[e] : 0.0;
         const uint64_t subj = valid ? a.sub[col] : 0ull;
         const uint64_t subi = a.sub[obs];
-        const uint64_t outmask = ballot(outb);
 
         // clearBackoff every 15 ticks (gossipsub.go:1627-1646)
         if (a.tick % 15 == 0 && valid) {
@@ -220,46 +218,38 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
                 const int ds = a.Dscore < l ? a.Dscore : l;
                 const bool tail = m && rank1 >= ds;
                 const uint64_t k2 = tail ? hb_key(a, (uint32_t)obs, t, P_PRUNE_SHUF2, col, pos) : ~0ull;
-                int p = rank1;
-                if (tail) {
-                    p = ds;
+                // every lane takes part in the shuffles (a shuffle inside a
+                // divergent branch would read inactive lanes)
+                int below = 0;
+                for (int q = 0; q < 64; ++q) {
+                    const uint64_t kq = __shfl(k2, q, 64);
+                    if (kq < k2) ++below;   // non-tail lanes hold ~0 and never count
+                }
+                const int p = tail ? ds + below : rank1;
+                // Keep plst[:D] after Go's Dout rotation (1457-1485), computed
+                // data-parallel from each lane's position p in plst:
+                //  pass 1 moves every outbound peer at positions 1..D-1 to the
+                //  front, leaving the other first-D peers ("rest") behind them
+                //  in order; pass 2 rotates the first j outbound peers beyond D
+                //  to the front, pushing the last j "rest" peers out of plst[:D].
+                const bool inD = m && p < a.D;
+                const int obD = __popcll(ballot(inD && outb));
+                bool keep = inD;
+                if (obD < a.Dout) {
+                    const bool rest = inD && !(outb && p >= 1);
+                    const bool cb = m && p >= a.D && outb;
+                    const uint64_t restmask = ballot(rest), cbmask = ballot(cb);
+                    int rb = 0, rr = 0;
                     for (int q = 0; q < 64; ++q) {
-                        const uint64_t kq = __shfl(k2, q, 64);
-                        if (kq < k2) ++p;   // non-tail lanes hold ~0 and never count
+                        const int pq = __shfl(p, q, 64);
+                        if (((cbmask >> q) & 1ull) && pq < p) ++rb;
+                        if (((restmask >> q) & 1ull) && pq > p) ++rr;
                     }
+                    const int nb = __popcll(cbmask);
+                    const int j = a.Dout - obD < nb ? a.Dout - obD : nb;
+                    keep = (inD && !(rest && rr < j)) || (cb && rb < j);
                 }
-                if (m) s_plst[wid][p] = (uint8_t)lane;
-                // the LDS slice is private to this wave: a wave-scope fence
-                // orders the lanes' writes before lane 0 reads them (other waves
-                // of the block may be on a different branch, so no block barrier)
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                uint64_t prune_mask = 0;
-                if (lane == 0) {
-                    uint8_t* pl = s_plst[wid];
-                    int outbound = 0;
-                    for (int q = 0; q < a.D && q < l; ++q) outbound += (int)((outmask >> pl[q]) & 1ull);
-                    auto rotate = [&](int idx) {
-                        const uint8_t v = pl[idx];
-                        for (int w = idx; w > 0; --w) pl[w] = pl[w - 1];
-                        pl[0] = v;
-                    };
-                    if (outbound < a.Dout) {
-                        if (outbound > 0) {
-                            int ihave = outbound;
-                            for (int q = 1; q < a.D && ihave > 0; ++q)
-                                if ((outmask >> pl[q]) & 1ull) { rotate(q); --ihave; }
-                        }
-                        int ineed = a.Dout - outbound;
-                        for (int q = a.D; q < l && ineed > 0; ++q)
-                            if ((outmask >> pl[q]) & 1ull) { rotate(q); --ineed; }
-                    }
-                    for (int q = a.D; q < l; ++q) prune_mask |= 1ull << pl[q];
-                }
-                prune_mask = __shfl(prune_mask, 0, 64);
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                if ((prune_mask >> lane) & 1ull) prune();
+                if (m && !keep) prune();
             }
 
             // enough outbound peers? (1492-1518)
@@ -488,6 +478,7 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     if (rc) return rc;
     // heartbeat output goes to the parity-0 inbox, read by control round 0
     HbArgs a = make_hb_args(h, tick, now, 1);
+    ProfScope ps(h, GSIM_K_HEARTBEAT);
     hipLaunchKernelGGL(k_heartbeat, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_heartbeat");
 }
@@ -500,6 +491,7 @@ int gsim_handle_control(gsim_handle* h, int32_t round, int64_t now)
     int rc = check_degree(h);
     if (rc) return rc;
     HbArgs a = make_hb_args(h, 0, now, round & 1);
+    ProfScope ps(h, GSIM_K_CONTROL);
     hipLaunchKernelGGL(k_handle_control, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_handle_control");
 }

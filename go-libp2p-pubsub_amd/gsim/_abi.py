@@ -101,6 +101,9 @@ MSG_DTYPE = [("id", "<u8"), ("topic", "<u4"), ("origin", "<u4"), ("invalid", "u1
 
 UNSEEN = 0xFFFFFFFF
 
+KERNEL_CLASSES = ["refresh_score", "score", "ip_colocation", "heartbeat", "control", "publish", "claim",
+                  "resolve", "forward"]
+
 SIGNATURES = [
     ("gsim_default_gossipsub_params", None, [POINTER(CGossipSubParams)]),
     ("gsim_validate_topic_params", c_int32, [POINTER(CTopicScoreParams), c_char_p, c_size_t]),
@@ -143,6 +146,8 @@ SIGNATURES = [
     ("gsim_publish", c_int32, [c_void_p, c_void_p, c_int32, c_int64]),
     ("gsim_round", c_int32, [c_void_p, c_int64]),
     ("gsim_msg_stats", c_int32, [c_void_p, c_void_p]),
+    ("gsim_profile", c_int32, [c_void_p, c_int32]),
+    ("gsim_profile_read", c_int32, [c_void_p, c_void_p, c_void_p, c_int32]),
 ]
 
 _lib = None

@@ -221,8 +221,10 @@ class Engine:
         c = _abi.CMsgConfig()
         c.ring, c.rounds, c.t0_ns = int(ring), int(rounds), int(t0)
         c.heartbeat_ns = int(heartbeat if heartbeat is not None else self.gossip.HeartbeatInterval)
-        c.max_frontier = int(max_frontier if max_frontier is not None else max(4 * self.net.n, 1024))
-        c.max_arrivals = int(max_arrivals if max_arrivals is not None else max(2 * self.net.e, 4096))
+        # defaults are the exact upper bounds: each (peer, slot) is first seen
+        # once per round at most, and forwards over at most its row
+        c.max_frontier = int(max_frontier if max_frontier is not None else min(ring * self.net.n, 2**31 - 1))
+        c.max_arrivals = int(max_arrivals if max_arrivals is not None else min(ring * self.net.e, 2**31 - 1))
         self._check(self.lib.gsim_msgs_init(self.h, ctypes.byref(c)))
         self._msg_cfg = c
 
@@ -236,6 +238,11 @@ class Engine:
         for k, (mid, topic, origin, invalid) in enumerate(msgs):
             arr[k]["id"], arr[k]["topic"], arr[k]["origin"], arr[k]["invalid"] = mid, topic, origin, invalid
         self._check(self.lib.gsim_publish(self.h, _ptr(arr), len(arr), int(rnd)))
+
+    def publish_array(self, arr: np.ndarray, rnd: int):
+        """Like publish() for a prebuilt numpy array of dtype _abi.MSG_DTYPE."""
+        a = np.ascontiguousarray(arr)
+        self._check(self.lib.gsim_publish(self.h, _ptr(a), len(a), int(rnd)))
 
     def round(self, rnd: int):
         """One propagation round for the whole network (gsim_round)."""
@@ -266,6 +273,18 @@ class Engine:
 
     def synchronize(self):
         self._check(self.lib.gsim_synchronize(self.h))
+
+    def profile(self, enable: bool = True):
+        """Record per-kernel-class device time with HIP events (gsim_profile)."""
+        self._check(self.lib.gsim_profile(self.h, int(bool(enable))))
+
+    def profile_read(self) -> dict:
+        """{class: (ms, launches)} since the last read (synchronizes)."""
+        n = len(_abi.KERNEL_CLASSES)
+        ms = np.zeros(n, dtype=np.float64)
+        cnt = np.zeros(n, dtype=np.int64)
+        self._check(self.lib.gsim_profile_read(self.h, _ptr(ms), _ptr(cnt), n))
+        return {c: (float(ms[i]), int(cnt[i])) for i, c in enumerate(_abi.KERNEL_CLASSES)}
 
     def set_kernel_variant(self, which: int, variant: int):
         self._check(self.lib.gsim_set_kernel_variant(self.h, which, variant))

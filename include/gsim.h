@@ -328,6 +328,25 @@ int gsim_event_record(gsim_handle* h, int32_t slot);
 /* Milliseconds between two recorded events (synchronizes on `to`). */
 int gsim_event_elapsed(gsim_handle* h, int32_t from, int32_t to, float* ms);
 int gsim_synchronize(gsim_handle* h);
+/* Per-kernel-class device time, measured with HIP events recorded on the
+ * engine stream around each class's launches while profiling is enabled. */
+typedef enum gsim_kernel_class {
+    GSIM_K_REFRESH_SCORE = 0,  /* refreshScores (+ fused score) pass */
+    GSIM_K_SCORE,              /* score-only pass */
+    GSIM_K_IP_COLOCATION,      /* P6 segmented count */
+    GSIM_K_HEARTBEAT,          /* mesh maintenance */
+    GSIM_K_CONTROL,            /* GRAFT/PRUNE handling */
+    GSIM_K_PUBLISH,            /* slot reset + origin self-delivery */
+    GSIM_K_CLAIM,              /* seen-set claims */
+    GSIM_K_RESOLVE,            /* first/duplicate/invalid classification + counters */
+    GSIM_K_FORWARD,            /* seen commit + mesh forwarding */
+    GSIM_K__COUNT
+} gsim_kernel_class;
+/* Enable (1) or disable (0) recording; clears recorded totals. */
+int gsim_profile(gsim_handle* h, int32_t enable);
+/* Synchronize, then write per-class milliseconds and launch counts recorded
+ * since the last read (n entries, indexed by gsim_kernel_class) and reset. */
+int gsim_profile_read(gsim_handle* h, double* ms, int64_t* launches, int32_t n);
 /* Select an implementation variant of a hot-path kernel for A/B timing in
  * one process (results are identical across variants).  which = 0: the
  * refreshScores+score pass; variant 0 thread-per-edge, 2 wave (4-topic

@@ -81,3 +81,25 @@ def randomize_state(st, rng, now: int, retained_frac: float = 0.05):
     for f in ("first", "meshd", "fail", "invalid", "graft_time", "mesh_time", "tflags"):
         getattr(st, f)[:, untracked] = 0
     st.bp[untracked] = 0
+
+
+def synthetic_state(st, rng, now: int, p_mesh: float):
+    """Host twin of gsim_fill_synthetic's distributions (engine.hip
+    k_fill_synthetic): a mostly healthy steady-state network — mesh links with
+    probability p_mesh, graft times within the last hour, first deliveries
+    U{0..1999}/4, mesh deliveries U{0..1599}/4 on mesh links, occasional
+    failure penalties, rare invalid deliveries and behaviour penalties."""
+    T, E = st.first.shape
+    in_mesh = rng.random((T, E)) < p_mesh
+    st.tflags[...] = np.where(in_mesh, _abi.TF_IN_MESH | _abi.TF_MESH, 0).astype(np.uint8)
+    st.tflags[in_mesh & (rng.integers(0, 16, (T, E)) != 0)] |= _abi.TF_ACTIVE
+    st.graft_time[...] = np.where(in_mesh, now - rng.integers(0, 3600, (T, E)) * Second, 0)
+    st.mesh_time[...] = np.where(in_mesh, now - st.graft_time, 0)
+    st.first[...] = rng.integers(0, 2000, (T, E)) * 0.25
+    st.meshd[...] = np.where(in_mesh, rng.integers(0, 1600, (T, E)) * 0.25, 0.0)
+    st.fail[...] = np.where(rng.integers(0, 8, (T, E)) == 0, rng.integers(0, 4000, (T, E)) * 0.125, 0.0)
+    st.invalid[...] = np.where(rng.integers(0, 512, (T, E)) == 0, rng.integers(0, 64, (T, E)) * 0.125, 0.0)
+    st.bp[...] = np.where(rng.integers(0, 16, E) == 0, rng.integers(0, 100, E) * 0.125, 0.0)
+    st.estate[...] = _abi.ES_TRACKED | _abi.ES_CONNECTED
+    st.expire[...] = 0
+    st.backoff[...] = 0

@@ -223,9 +223,9 @@ def _schedule(rng, ticks, T, R, rate, inv_frac, n):
     (3000, 32, 3, [14, 15, 16], 12, 0.05, 0.03, 64),     # ring slots reused; clearBackoff tick
 ])
 def test_rounds_bit_exact(require_gpu, n, k, T, ticks, rate, inv_frac, retained, ring):
-    from fixtures import beacon_params, beacon_topic, randomize_state
+    from fixtures import beacon_params, beacon_topic, synthetic_state
     from gsim.engine import Engine, random_regular
-    from test_heartbeat import _random_mesh_state, assert_same
+    from test_heartbeat import assert_same
     rng = np.random.default_rng(n + k)
     params = beacon_params(T)
     # a short duplicate window on one topic: only near-simultaneous copies count
@@ -234,8 +234,12 @@ def test_rounds_bit_exact(require_gpu, n, k, T, ticks, rate, inv_frac, retained,
     th = PeerScoreThresholds(GossipThreshold=-100, PublishThreshold=-200, GraylistThreshold=-300)
     net = random_regular(n, k, seed=n, n_topics=T)
     st = ob.NetState(net, params, thresholds=th, gossip=gp)
-    randomize_state(st, rng, tick_time(0), retained_frac=retained)
-    _random_mesh_state(st, rng, 0.3)
+    synthetic_state(st, rng, tick_time(0), 8 / k)
+    # some retained (disconnected) peers and heavy behaviour penalties: graylisted senders
+    r = rng.random(net.e)
+    st.estate[r < retained] = _abi.ES_TRACKED
+    st.expire[r < retained] = tick_time(0) + rng.integers(1, 5, int((r < retained).sum())) * Second
+    st.bp[rng.random(net.e) < 0.02] = 40.0
     msgs = ob.Msgs(n, T, ring, R, T0, HB)
     eng = Engine(params, th, gossip=gp)
     eng.load_graph(net)
@@ -260,12 +264,12 @@ def test_rounds_bit_exact(require_gpu, n, k, T, ticks, rate, inv_frac, retained,
                 eng.publish(sched[g], g)
             msgs.round(st, g)
             eng.round(g)
-        gpu = ob.NetState(net, params, thresholds=th, gossip=gp)
-        gpu.pull_from_engine(eng)
-        assert_same(st, gpu)
+        assert eng.msg_stats() == msgs.stats, f"tick {kk}"
         seen = eng.read(_abi.F_SEEN)
         assert np.array_equal(seen, msgs.seen), f"seen-set differs at tick {kk}: {(seen != msgs.seen).sum()} cells"
         assert np.array_equal(eng.read(_abi.F_LASTPUT), msgs.lastput)
-        assert eng.msg_stats() == msgs.stats
-    assert msgs.stats[1] > 0 and msgs.stats[2] > 0
+        gpu = ob.NetState(net, params, thresholds=th, gossip=gp)
+        gpu.pull_from_engine(eng)
+        assert_same(st, gpu)
+    assert msgs.stats[1] > n and msgs.stats[2] > n and msgs.stats[3] > 0
     eng.close()

@@ -219,6 +219,8 @@ def assert_same(cpu, gpu):
     (500, 16, 1, 0.0, [1, 2, 3]),            # empty start: Dlo grafting, GRAFT acceptance
     (1200, 32, 3, 0.55, [14, 15, 16]),       # oversubscribed: Dhi prune + Dout rotation, clearBackoff
     (800, 24, 2, 0.3, [59, 60, 61]),         # opportunistic grafting tick
+    (600, 16, 2, 0.85, [1, 2, 3]),           # Dhi prune on short rows (16 connections)
+    (300, 64, 1, 0.3, [4, 5]),               # full-wave rows (64 connections)
 ])
 def test_heartbeat_and_control_bit_exact(require_gpu, n, k, T, p_mesh, ticks):
     rng = np.random.default_rng(n + T)
@@ -247,3 +249,57 @@ def test_heartbeat_and_control_bit_exact(require_gpu, n, k, T, p_mesh, ticks):
         gpu.pull_from_engine(eng)
         assert_same(st, gpu)
     eng.close()
+
+
+def _go_dout_keep(plst, outbound, D, Dout):
+    """gossipsub.go:1457-1488 verbatim: returns plst[:D] after the rotation."""
+    plst = list(plst)
+    ob = sum(1 for p in plst[:D] if outbound[p])
+    if ob < Dout:
+        def rotate(i):
+            p = plst[i]
+            for j in range(i, 0, -1):
+                plst[j] = plst[j - 1]
+            plst[0] = p
+        if ob > 0:
+            ihave = ob
+            i = 1
+            while i < D and ihave > 0:
+                if outbound[plst[i]]:
+                    rotate(i)
+                    ihave -= 1
+                i += 1
+        ineed = Dout - ob
+        i = D
+        while i < len(plst) and ineed > 0:
+            if outbound[plst[i]]:
+                rotate(i)
+                ineed -= 1
+            i += 1
+    return set(plst[:D])
+
+
+def _closed_form_keep(plst, outbound, D, Dout):
+    """The data-parallel form k_heartbeat evaluates per lane (heartbeat.hip)."""
+    pos = {p: i for i, p in enumerate(plst)}
+    inD = {p for p in plst if pos[p] < D}
+    obD = sum(1 for p in inD if outbound[p])
+    if obD >= Dout:
+        return inD
+    rest = {p for p in inD if not (outbound[p] and pos[p] >= 1)}
+    cb = sorted((p for p in plst if pos[p] >= D and outbound[p]), key=lambda p: pos[p])
+    j = min(Dout - obD, len(cb))
+    rest_sorted = sorted(rest, key=lambda p: pos[p])
+    pushed = set(rest_sorted[len(rest_sorted) - j:]) if j else set()
+    return (inD - pushed) | set(cb[:j])
+
+
+def test_dout_rotation_closed_form_matches_go():
+    rng = np.random.default_rng(7)
+    for _ in range(20000):
+        D = int(rng.integers(2, 12))
+        Dout = int(rng.integers(0, D // 2 + 1))
+        l = int(rng.integers(D + 1, 40))
+        plst = list(rng.permutation(64)[:l])
+        outbound = {p: bool(rng.random() < rng.random()) for p in plst}
+        assert _go_dout_keep(plst, outbound, D, Dout) == _closed_form_keep(plst, outbound, D, Dout)
