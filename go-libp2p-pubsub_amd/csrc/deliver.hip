@@ -144,74 +144,111 @@ __global__ void k_claim(RoundArgs a)
     }
 }
 
-// Step 1b: classify every accepted copy and apply the score tracer.
-__global__ void k_resolve(RoundArgs a)
+// Exclusive prefix of v over the 256 threads of a block (4 waves); *total gets
+// the block sum.  Must be reached by every thread of the block.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wt, uint32_t* total)
 {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_wt[wid] = incl;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t x = s_wt[w];
+        if (w < wid) wbase += x;
+        tot += x;
+    }
+    *total = tot;
+    return wbase + incl - v;
+}
+
+constexpr int kResolveItems = 4;   // arrivals per thread per block chunk
+
+// Step 1b: classify every accepted copy and apply the score tracer.  First
+// deliveries are appended to the frontier with one global atomic per block
+// chunk (256 x kResolveItems copies).
+__global__ __launch_bounds__(256) void k_resolve(RoundArgs a)
+{
+    __shared__ uint32_t s_wt[4];
+    __shared__ uint32_t s_base;
     const uint32_t n = min(a.cnt[2 + ((a.g + 1) & 1)], (uint32_t)a.max_arrivals);
     const int lane = threadIdx.x & 63;
-    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-    const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     ctp_t tp = const_tp(a.tp);
     const int32_t tick = (int32_t)(a.g / a.R);
     unsigned long long s_acc = 0, s_first = 0, s_gray = 0;
-    for (uint32_t base = wid * 64; base < n; base += waves * 64) {
-        const uint32_t i = base + lane;
-        bool first = false;
-        uint32_t recv = 0, slot = 0, from = 0;
-        if (i < n) {
+    constexpr uint32_t chunk = 256 * kResolveItems;
+    for (uint32_t c0 = blockIdx.x * chunk; c0 < n; c0 += gridDim.x * chunk) {
+        uint32_t fr[kResolveItems], fs[kResolveItems], ff[kResolveItems];
+        uint32_t fmask = 0;
+#pragma unroll
+        for (int r = 0; r < kResolveItems; ++r) {
+            fr[r] = fs[r] = ff[r] = 0;
+            const uint32_t i = c0 + (uint32_t)r * 256 + threadIdx.x;
+            if (i >= n) continue;
             const uint32_t er = a.a_er[i];
-            slot = a.a_slot[i];
-            recv = a.a_recv[i];
+            const uint32_t slot = a.a_slot[i];
+            const uint32_t recv = a.a_recv[i];
             if (a.score[er] < a.gray) {
                 s_gray++;
-            } else {
-                s_acc++;
-                const uint32_t c = a.seen[(int64_t)slot * a.N + recv];
-                const int32_t t = (int32_t)a.mtopic[slot];
-                const bool inv = a.minv[slot] != 0;
-                first = c == (kClaim | er);
-                const bool scored = (a.estate[er] & GSIM_ES_TRACKED) && tp[t].scored;
-                const int64_t te = (int64_t)t * a.E + er;
-                if (first) {
-                    s_first++;
-                    from = a.col[er];
-                    if (scored) {
-                        if (inv) {
-                            inc_capped(&a.invalid[te], __builtin_inf());
-                        } else {
-                            inc_capped(&a.first[te], tp[t].first_message_deliveries_cap);
-                            if (a.tflags[te] & GSIM_TF_IN_MESH)
-                                inc_capped(&a.meshd[te], tp[t].mesh_message_deliveries_cap);
-                        }
-                    }
-                    if (!inv) a.lastput[(int64_t)t * a.N + recv] = tick;
-                } else if (scored) {
+                continue;
+            }
+            s_acc++;
+            const uint32_t c = a.seen[(int64_t)slot * a.N + recv];
+            const int32_t t = (int32_t)a.mtopic[slot];
+            const bool inv = a.minv[slot] != 0;
+            const bool first = c == (kClaim | er);
+            const bool scored = (a.estate[er] & GSIM_ES_TRACKED) && tp[t].scored;
+            const int64_t te = (int64_t)t * a.E + er;
+            if (first) {
+                s_first++;
+                fmask |= 1u << r;
+                fr[r] = recv;
+                fs[r] = slot;
+                ff[r] = a.col[er];
+                if (scored) {
                     if (inv) {
                         inc_capped(&a.invalid[te], __builtin_inf());
-                    } else if (a.tflags[te] & GSIM_TF_IN_MESH) {
-                        const int64_t validated = (c & kClaim) ? a.now : round_time(a, (int64_t)c);
-                        if (a.now - validated <= tp[t].mesh_message_deliveries_window_ns)
+                    } else {
+                        inc_capped(&a.first[te], tp[t].first_message_deliveries_cap);
+                        if (a.tflags[te] & GSIM_TF_IN_MESH)
                             inc_capped(&a.meshd[te], tp[t].mesh_message_deliveries_cap);
                     }
                 }
-            }
-        }
-        const uint64_t m = __ballot(first);
-        if (m) {
-            uint32_t b = 0;
-            if (lane == 0) b = atomicAdd(&a.cnt[a.g & 1], (uint32_t)__popcll(m));
-            b = __shfl(b, 0, 64);
-            if (first) {
-                const uint32_t idx = b + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-                if ((int64_t)idx < a.max_frontier) {
-                    a.f_peer[idx] = recv;
-                    a.f_slot[idx] = slot;
-                    a.f_from[idx] = from;
-                } else {
-                    atomicOr(&a.cnt[4], 1u);
+                if (!inv) a.lastput[(int64_t)t * a.N + recv] = tick;
+            } else if (scored) {
+                if (inv) {
+                    inc_capped(&a.invalid[te], __builtin_inf());
+                } else if (a.tflags[te] & GSIM_TF_IN_MESH) {
+                    const int64_t validated = (c & kClaim) ? a.now : round_time(a, (int64_t)c);
+                    if (a.now - validated <= tp[t].mesh_message_deliveries_window_ns)
+                        inc_capped(&a.meshd[te], tp[t].mesh_message_deliveries_cap);
                 }
             }
         }
+        uint32_t total;
+        const uint32_t excl = block_excl_scan((uint32_t)__popc(fmask), s_wt, &total);
+        if (threadIdx.x == 0) s_base = total ? atomicAdd(&a.cnt[a.g & 1], total) : 0u;
+        __syncthreads();
+        uint32_t pos = s_base + excl;
+#pragma unroll
+        for (int r = 0; r < kResolveItems; ++r) {
+            if (!((fmask >> r) & 1u)) continue;
+            if ((int64_t)pos < a.max_frontier) {
+                a.f_peer[pos] = fr[r];
+                a.f_slot[pos] = fs[r];
+                a.f_from[pos] = ff[r];
+            } else {
+                atomicOr(&a.cnt[4], 1u);
+            }
+            ++pos;
+        }
+        __syncthreads();   // s_wt / s_base reuse
     }
     s_acc = wave_sum_u64(s_acc);
     s_first = wave_sum_u64(s_first);
@@ -224,51 +261,76 @@ __global__ void k_resolve(RoundArgs a)
     }
 }
 
-// Step 3: commit first-seen rounds and forward to the mesh.
-__global__ void k_forward(RoundArgs a)
+// Mesh targets of frontier entry q as a lane mask over the sender's row
+// (rows of at most 64 connections); lane 0 commits the first-seen round.
+// Must be called by a whole wave.
+__device__ __forceinline__ uint64_t forward_mask(const RoundArgs& a, uint32_t q, bool commit)
 {
+    const int lane = threadIdx.x & 63;
+    const uint32_t j = a.f_peer[q], slot = a.f_slot[q], from = a.f_from[q];
+    if (commit && lane == 0) a.seen[(int64_t)slot * a.N + j] = (uint32_t)a.g;
+    const uint32_t t = a.mtopic[slot], origin = a.morigin[slot];
+    // receivers reject an invalid message and do not forward it; its
+    // origin publishes it regardless
+    if (a.minv[slot] && j != origin) return 0;
+    const uint32_t b = a.row_ptr[j], deg = a.row_ptr[j + 1] - b;
+    const uint32_t e = b + (uint32_t)lane;
+    bool ok = false;
+    if ((uint32_t)lane < deg) {
+        const uint32_t i = a.col[e];
+        ok = (a.tflags[(int64_t)t * a.E + e] & GSIM_TF_MESH) && (a.estate[e] & GSIM_ES_CONNECTED) && i != from &&
+             i != origin;
+    }
+    return __ballot(ok);
+}
+
+// Step 3: commit first-seen rounds and forward to the mesh.  A block takes 256
+// frontier entries (64 per wave): pass 1 builds each entry's target mask,
+// one global atomic reserves the block's output range, pass 2 writes it.
+__global__ __launch_bounds__(256) void k_forward(RoundArgs a)
+{
+    __shared__ uint32_t s_wt[4];
+    __shared__ uint32_t s_base;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // the lists of round g+1's parity were consumed by round g-1 / g
         a.cnt[(a.g + 1) & 1] = 0;
         a.cnt[2 + ((a.g + 1) & 1)] = 0;
     }
     const uint32_t n = min(a.cnt[a.g & 1], (uint32_t)a.max_frontier);
-    const int lane = threadIdx.x & 63;
-    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-    const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    for (uint32_t q = wid; q < n; q += waves) {
-        const uint32_t j = a.f_peer[q], slot = a.f_slot[q], from = a.f_from[q];
-        if (lane == 0) a.seen[(int64_t)slot * a.N + j] = (uint32_t)a.g;
-        const uint32_t t = a.mtopic[slot], origin = a.morigin[slot];
-        // receivers reject an invalid message and do not forward it; its
-        // origin publishes it regardless
-        if (a.minv[slot] && j != origin) continue;
-        const uint32_t b = a.row_ptr[j], e_end = a.row_ptr[j + 1];
-        const uint8_t* fl = a.tflags + (int64_t)t * a.E;
-        for (uint32_t e0 = b; e0 < e_end; e0 += 64) {
-            const uint32_t e = e0 + lane;
-            bool ok = false;
-            uint32_t i = 0;
-            if (e < e_end) {
-                i = a.col[e];
-                ok = (fl[e] & GSIM_TF_MESH) && (a.estate[e] & GSIM_ES_CONNECTED) && i != from && i != origin;
-            }
-            const uint64_t m = __ballot(ok);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (uint32_t c0 = blockIdx.x * 256; c0 < n; c0 += gridDim.x * 256) {
+        const uint32_t w0 = c0 + (uint32_t)wid * 64;
+        uint64_t my_mask = 0;
+        for (int q = 0; q < 64; ++q) {
+            if (w0 + q >= n) break;
+            const uint64_t m = forward_mask(a, w0 + q, true);
+            if (lane == q) my_mask = m;
+        }
+        uint32_t total;
+        const uint32_t excl = block_excl_scan((uint32_t)__popcll(my_mask), s_wt, &total);
+        if (threadIdx.x == 0) s_base = total ? atomicAdd(&a.cnt[2 + (a.g & 1)], total) : 0u;
+        __syncthreads();
+        const uint32_t base = s_base;
+        for (int q = 0; q < 64; ++q) {
+            const uint32_t idx = w0 + q;
+            if (idx >= n) break;
+            const uint64_t m = __shfl(my_mask, q, 64);
             if (!m) continue;
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(&a.cnt[2 + (a.g & 1)], (uint32_t)__popcll(m));
-            base = __shfl(base, 0, 64);
-            if (ok) {
-                const uint32_t idx = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-                if ((int64_t)idx < a.max_arrivals) {
-                    a.o_er[idx] = a.rev[e];
-                    a.o_slot[idx] = slot;
-                    a.o_recv[idx] = i;
+            const uint32_t off = base + __shfl(excl, q, 64);
+            if ((m >> lane) & 1ull) {
+                const uint32_t j = a.f_peer[idx];
+                const uint32_t e = a.row_ptr[j] + (uint32_t)lane;
+                const uint32_t pos = off + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+                if ((int64_t)pos < a.max_arrivals) {
+                    a.o_er[pos] = a.rev[e];
+                    a.o_slot[pos] = a.f_slot[idx];
+                    a.o_recv[pos] = a.col[e];
                 } else {
                     atomicOr(&a.cnt[4], 1u);
                 }
             }
         }
+        __syncthreads();   // s_wt / s_base reuse
     }
 }
 
@@ -436,6 +498,10 @@ int gsim_round(gsim_handle* h, int64_t round)
     if (d->next_round >= 0 && round != d->next_round) {
         h->err = "rounds must be consecutive";
         return GSIM_ESTATE;
+    }
+    if (h->max_degree > 64) {
+        h->err = "propagation kernels support rows of at most 64 connections in this build";
+        return GSIM_ERANGE;
     }
     RoundArgs a = make_round_args(h, round);
     {

@@ -87,6 +87,7 @@ struct gsim_handle {
 
     int64_t n = 0, e = 0;
     uint32_t n_ips = 0;
+    uint32_t max_degree = 0;   // longest CSR row (set when the graph is loaded)
     size_t bytes_allocated = 0;
     bool has_white = false;
     bool p6_dirty = true;

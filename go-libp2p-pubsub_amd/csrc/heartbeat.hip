@@ -406,6 +406,7 @@ int alloc_extra(gsim_handle* h)
     uint32_t md = 0;
     for (int64_t i = 0; i < h->n; ++i) md = std::max(md, rp[(size_t)i + 1] - rp[(size_t)i]);
     h->x->max_degree = md;
+    h->max_degree = md;
     return GSIM_OK;
 }
 
