@@ -7,10 +7,10 @@ of state resident in HBM:
   refreshScores+score (decay, P1-P7 snapshot)        k_refresh_score
   heartbeat mesh maintenance (all peers, all topics)  k_heartbeat
   10 propagation rounds, each: publications (Poisson 4 msg/s/topic, seed 2),
-  seen-set claim/resolve + delivery counters, control inbox (rounds 0-1),
-  mesh forwarding                                     k_publish, k_claim,
-                                                      k_resolve, k_handle_control,
-                                                      k_forward
+  mesh forwarding + AcceptFrom + seen-set claims + duplicate/invalid
+  counters, seen commit + first-delivery credit, control inbox (rounds 0-1)
+                                                      k_publish, k_send,
+                                                      k_commit, k_handle_control
 W untimed warmup ticks, then exactly K timed ticks bracketed by barrier +
 device sync; max over ranks; rank 0 prints one JSON line.  Per-kernel-class
 device time comes from HIP events recorded on the engine stream around every
@@ -95,8 +95,7 @@ def build_engine(cfg, seed, device):
     eng.load_graph(net)
     eng.set_seed(0x5EED0000 + seed)
     eng.fill_synthetic(seed=seed * 7919 + 1, now=tick_time(0), p_mesh=D / k)
-    eng.msgs_init(MSG_RING, ROUNDS, tick_time(0), SECOND,
-                  max_frontier=max(16 * n, 1 << 16), max_arrivals=max(8 * net.e, 1 << 20))
+    eng.msgs_init(MSG_RING, ROUNDS, tick_time(0), SECOND)
     return eng, net
 
 
@@ -238,11 +237,11 @@ def main():
         alg_refresh = (refresh_bytes(census0, E) + refresh_bytes(census1, E)) // 2
         ref_ms = prof["refresh_score"][0] / max(1, launches["refresh_score"])
         ref_gbs = alg_refresh / (ref_ms * 1e-3) / 1e9
-        # delivery: SURVEY.md §8(d) bytes per first / duplicate delivery, over claim+resolve+forward
+        # delivery: SURVEY.md §8(d) bytes per first / duplicate delivery, over send+commit(+accept)
         firsts = stats1[1] - stats0[1]
         dups = stats1[2] - stats0[2]
         alg_deliv = (FIRST_BYTES * firsts + DUP_BYTES * dups) / K
-        deliv_ms = kms["claim"] + kms["resolve"] + kms["forward"]
+        deliv_ms = kms["send"] + kms["commit"] + kms["accept"]
         deliv_gbs = alg_deliv / (deliv_ms * 1e-3) / 1e9 if deliv_ms > 0 else 0.0
         roof_refresh = {"bound": "hbm", "achieved": ref_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": ref_gbs / HBM_PEAK_GBS, "traffic": load_traffic(args.config),
@@ -250,7 +249,7 @@ def main():
                         "algorithmic_bytes_per_launch": alg_refresh}
         roof_deliv = {"bound": "hbm", "achieved": deliv_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": deliv_gbs / HBM_PEAK_GBS, "traffic": None,
-                      "kernel": "k_claim+k_resolve+k_forward (per tick)", "kernel_ms": deliv_ms,
+                      "kernel": "k_send+k_commit+k_accept (per tick)", "kernel_ms": deliv_ms,
                       "algorithmic_bytes_per_tick": alg_deliv}
         dominant = roof_refresh if ref_ms * launches["refresh_score"] / K >= deliv_ms else roof_deliv
         out = {

@@ -8,23 +8,31 @@
 //                                  InvalidMessageDelivery score.go:901-981
 //   Publish forwarding to mesh     gossipsub.go:975-1045
 //
-// Bulk-synchronous restatement.  Round g:
-//   k_claim    every accepted copy forwarded in round g-1 does an atomicMin
-//              of (0x80000000 | receiving edge) into seen[slot][receiver];
-//              committed cells hold a round number < 0x80000000 and are left
-//              alone, so the lowest receiving edge claims an unseen cell.
-//   k_resolve  each copy re-reads its cell: its own claim -> first delivery
-//              (markFirst or markInvalid, joins the frontier); anything else
-//              -> duplicate (markDuplicate with validated = the first-seen
-//              round's time, or now for a same-round claim).  Counter updates
-//              are CAS loops of x -> min(x + 1, cap): every copy applies the
-//              same function, so the result is independent of their order.
-//   control    rounds 0 and 1 of each heartbeat (GRAFT/PRUNE inbox).
-//   k_forward  one wave per frontier entry commits seen = g and appends a
-//              copy for every mesh connection except the sender and the origin.
-// Lists are compacted with wave ballots (one atomicAdd per wave); list
-// lengths stay on the device, kernels use fixed grids with grid-stride loops,
-// so a round never synchronizes with the host.
+// Bulk-synchronous restatement.  The seen-set is the only
+// message state: seen[slot][peer] = first-seen round, so the forwarding
+// frontier of round g-1 is {j : seen[m][j] == g-1} and no per-copy list is
+// ever materialized.  Round g:
+//   k_send    one wave per 64 consecutive senders, for every slot active in
+//             round g-1 (a coalesced load of seen[m][j0..j0+63] per slot):
+//             each frontier sender walks its row with a lane group, and for
+//             every mesh target evaluates AcceptFrom, loads the receiver's
+//             seen cell and applies the score tracer to the RECEIVER's record
+//             of the sender, which in record order sits at the
+//             sender's own edge index: the counter traffic is coalesced along
+//             the sender's row.  A copy to a cell already committed is a
+//             duplicate (validated = its first-seen round); a copy to an
+//             uncommitted cell claims it with an atomicMin of
+//             (0x80000000 | edge): the lowest edge, i.e. the lowest sender,
+//             wins.  Every same-round copy, first or duplicate, has
+//             validated = now and therefore the same counter update; only
+//             firstMessageDeliveries needs the winner.
+//   k_commit  one wave per 64 consecutive receivers, for the same slots: a
+//             claimed cell commits seen = g and from = the winner, and the
+//             winner's record gets markFirstMessageDelivery's P2 credit.
+//   control   rounds 0 and 1 of each heartbeat (GRAFT/PRUNE inbox).
+// Counter updates are plain read-modify-writes: in k_send a record (receiver
+// i, sender j) is only touched by the lanes that walk j's row, always the
+// same lanes of the same wave; in k_commit only by receiver i's lane.
 #include <algorithm>
 #include <vector>
 
@@ -34,17 +42,16 @@ namespace gsim {
 
 constexpr uint32_t kUnseen = 0xFFFFFFFFu;
 constexpr uint32_t kClaim = 0x80000000u;
-constexpr int kListGrid = 2048;   // blocks of the grid-stride list kernels
+constexpr int kMaxRing = 8192;     // active-slot list lives in LDS (u16)
 
 struct Deliver {
     gsim_msg_config cfg{};
     uint32_t *d_mtopic = nullptr, *d_morigin = nullptr;
     uint8_t* d_minv = nullptr;
-    uint32_t* d_seen = nullptr;        // [ring][N]
+    uint32_t* d_seen = nullptr;        // [ring][N] first-seen round
+    uint32_t* d_from = nullptr;        // [ring][N] sender of the first copy
     int32_t* d_lastput = nullptr;      // [T][N]
-    uint32_t* d_f[2][3] = {};          // frontier by round parity: peer, slot, from
-    uint32_t* d_a[2][3] = {};          // arrivals by round parity: er, slot, receiver
-    uint32_t* d_cnt = nullptr;         // [0..1] frontier lengths, [2..3] arrival lengths, [4] overflow
+    uint32_t* d_nfirst = nullptr;      // [2][ring] first receptions per slot, by round parity
     unsigned long long* d_stats = nullptr;   // [4]
     gsim_msg* d_pub = nullptr;
     int32_t pub_cap = 0;
@@ -55,22 +62,20 @@ struct RoundArgs {
     int64_t N, E;
     int32_t T, ring, R;
     int64_t t0, hb, g, now;
-    const uint32_t *row_ptr, *col, *rev;
-    const uint8_t* estate;
-    const double* score;
+    const uint32_t *row_ptr, *col, *owner;
+    const uint8_t* rstate;     // router connected bit, edge order
+    const uint8_t* mflags;     // router mesh bits, edge order
+    const uint8_t* acc;        // AcceptFrom verdicts, record order
+    const uint8_t* estate;     // record order
+    const uint8_t* tflags;     // score bits, record order
     const gsim_topic_score_params* tp;
-    double gray;
-    uint8_t* tflags;
     double *first, *meshd, *invalid;
-    const uint32_t *mtopic, *morigin;
-    const uint8_t* minv;
-    uint32_t* seen;
+    uint32_t *mtopic, *morigin;
+    uint8_t* minv;
+    uint32_t *seen, *from;
     int32_t* lastput;
-    const uint32_t *a_er, *a_slot, *a_recv;    // arrivals consumed this round
-    uint32_t *f_peer, *f_slot, *f_from;        // frontier of this round
-    uint32_t *o_er, *o_slot, *o_recv;          // arrivals produced this round
-    uint32_t* cnt;
-    int64_t max_frontier, max_arrivals;
+    const uint32_t* nfirst_prev;   // slots with a frontier in round g-1
+    uint32_t* nfirst_cur;          // first receptions of round g
     unsigned long long* stats;
 };
 
@@ -79,27 +84,38 @@ __device__ __forceinline__ int64_t round_time(const RoundArgs& a, int64_t g)
     return a.t0 + (g / a.R) * a.hb + (g % a.R + 1) * a.hb / (a.R + 1);
 }
 
-// x -> min(x + 1, cap) on an fp64 counter (markFirst / markDuplicate, score.go
-// 919-981); cap = +inf gives invalidMessageDeliveries += 1 (score.go:901-914).
+// x -> min(x + 1, cap) (markFirst / markDuplicate, score.go:919-981)
 __device__ __forceinline__ void inc_capped(double* p, double cap)
 {
-    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
-    unsigned long long old = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (;;) {
-        double x = __longlong_as_double((long long)old) + 1.0;
-        if (x > cap) x = cap;
-        const unsigned long long nw = (unsigned long long)__double_as_longlong(x);
-        if (nw == old) return;
-        const unsigned long long prev = atomicCAS(q, old, nw);
-        if (prev == old) return;
-        old = prev;
-    }
+    double x = *p + 1.0;
+    if (x > cap) x = cap;
+    *p = x;
 }
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
+}
+
+// Ordered list of the slots that had first receptions (or a publication) in
+// round g-1, built by wave 0 into LDS; every thread of the block must call it.
+__device__ __forceinline__ int active_slots(const RoundArgs& a, uint16_t* s_act, int* s_n)
+{
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        int n = 0;
+        for (int m0 = 0; m0 < a.ring; m0 += 64) {
+            const int m = m0 + lane;
+            const bool act = m < a.ring && a.nfirst_prev[m] != 0;
+            const uint64_t b = __ballot(act);
+            if (act) s_act[n + __popcll(b & ((1ull << lane) - 1))] = (uint16_t)m;
+            n += __popcll(b);
+        }
+        if (lane == 0) *s_n = n;
+    }
+    __syncthreads();
+    return *s_n;
 }
 
 __global__ void k_reset_slots(uint32_t* seen, int64_t N, int32_t ring, const gsim_msg* pub, int32_t count)
@@ -117,220 +133,140 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, int32_t count)
     if (m >= count) return;
     const gsim_msg p = pub[m];
     const uint32_t slot = (uint32_t)(p.id % (uint64_t)a.ring);
-    uint32_t* mt = const_cast<uint32_t*>(a.mtopic);
-    uint32_t* mo = const_cast<uint32_t*>(a.morigin);
-    uint8_t* mi = const_cast<uint8_t*>(a.minv);
-    mt[slot] = p.topic;
-    mo[slot] = p.origin;
-    mi[slot] = p.invalid;
+    a.mtopic[slot] = p.topic;
+    a.morigin[slot] = p.origin;
+    a.minv[slot] = p.invalid;
     a.seen[(int64_t)slot * a.N + p.origin] = (uint32_t)a.g;
+    a.from[(int64_t)slot * a.N + p.origin] = p.origin;
     a.lastput[(int64_t)p.topic * a.N + p.origin] = (int32_t)(a.g / a.R);
-    const uint32_t idx = atomicAdd(&a.cnt[a.g & 1], 1u);
-    if ((int64_t)idx >= a.max_frontier) { atomicOr(&a.cnt[4], 1u); return; }
-    a.f_peer[idx] = p.origin;
-    a.f_slot[idx] = slot;
-    a.f_from[idx] = p.origin;
+    a.nfirst_cur[slot] = 1;   // the origin forwards in round g+1
 }
 
-// Step 1a: claim unseen cells (lowest receiving edge wins).
-__global__ void k_claim(RoundArgs a)
+// Round g, step 1: every frontier sender of round g-1 forwards to its mesh.
+// W = lanes per row (power of two >= the longest row); group q of a wave
+// always walks the senders j0 + q*W .. j0 + q*W + W-1.
+template <int W>
+__global__ __launch_bounds__(256) void k_send(RoundArgs a)
 {
-    const uint32_t n = min(a.cnt[2 + ((a.g + 1) & 1)], (uint32_t)a.max_arrivals);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t er = a.a_er[i];
-        if (a.score[er] < a.gray) continue;
-        uint32_t* cell = a.seen + (int64_t)a.a_slot[i] * a.N + a.a_recv[i];
-        __hip_atomic_fetch_min(cell, kClaim | er, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// Exclusive prefix of v over the 256 threads of a block (4 waves); *total gets
-// the block sum.  Must be reached by every thread of the block.
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wt, uint32_t* total)
-{
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t incl = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
-    }
-    if (lane == 63) s_wt[wid] = incl;
-    __syncthreads();
-    uint32_t wbase = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        const uint32_t x = s_wt[w];
-        if (w < wid) wbase += x;
-        tot += x;
-    }
-    *total = tot;
-    return wbase + incl - v;
-}
-
-constexpr int kResolveItems = 4;   // arrivals per thread per block chunk
-
-// Step 1b: classify every accepted copy and apply the score tracer.  First
-// deliveries are appended to the frontier with one global atomic per block
-// chunk (256 x kResolveItems copies).
-__global__ __launch_bounds__(256) void k_resolve(RoundArgs a)
-{
-    __shared__ uint32_t s_wt[4];
-    __shared__ uint32_t s_base;
-    const uint32_t n = min(a.cnt[2 + ((a.g + 1) & 1)], (uint32_t)a.max_arrivals);
+    __shared__ uint16_t s_act[kMaxRing];
+    __shared__ int s_n;
+    const int nact = a.g > 0 ? active_slots(a, s_act, &s_n) : 0;   // round 0 has no predecessor
     const int lane = threadIdx.x & 63;
-    ctp_t tp = const_tp(a.tp);
-    const int32_t tick = (int32_t)(a.g / a.R);
-    unsigned long long s_acc = 0, s_first = 0, s_gray = 0;
-    constexpr uint32_t chunk = 256 * kResolveItems;
-    for (uint32_t c0 = blockIdx.x * chunk; c0 < n; c0 += gridDim.x * chunk) {
-        uint32_t fr[kResolveItems], fs[kResolveItems], ff[kResolveItems];
-        uint32_t fmask = 0;
-#pragma unroll
-        for (int r = 0; r < kResolveItems; ++r) {
-            fr[r] = fs[r] = ff[r] = 0;
-            const uint32_t i = c0 + (uint32_t)r * 256 + threadIdx.x;
-            if (i >= n) continue;
-            const uint32_t er = a.a_er[i];
-            const uint32_t slot = a.a_slot[i];
-            const uint32_t recv = a.a_recv[i];
-            if (a.score[er] < a.gray) {
-                s_gray++;
+    const int64_t j0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+    if (j0 >= a.N) return;
+    const int64_t jl = j0 + lane;
+    const bool vj = jl < a.N;
+    const int grp = lane / W, gl = lane % W;
+    const uint64_t gmask = (W == 64) ? ~0ull : (((1ull << W) - 1) << (grp * W));
+    const ctp_t tpa = const_tp(a.tp);
+    const uint32_t gprev = (uint32_t)(a.g - 1);
+    unsigned long long n_acc = 0, n_gray = 0;
+    for (int k = 0; k < nact; ++k) {
+        const uint32_t m = s_act[k];
+        const int64_t row_m = (int64_t)m * a.N;
+        const uint32_t origin = a.morigin[m];
+        const bool inv = a.minv[m] != 0;
+        const uint32_t sv = vj ? a.seen[row_m + jl] : kUnseen;
+        // receivers reject an invalid message and do not forward it; its
+        // origin publishes it regardless
+        const bool fr = sv == gprev && (!inv || (uint32_t)jl == origin);
+        const uint64_t mask = __ballot(fr);
+        if (!mask) continue;
+        const uint32_t from_l = fr ? a.from[row_m + jl] : 0u;
+        const int32_t t = (int32_t)a.mtopic[m];
+        const ctp_t tp = tpa + t;
+        const bool scored_t = tp->scored != 0;
+        const int64_t window = tp->mesh_message_deliveries_window_ns;
+        const double mcap = tp->mesh_message_deliveries_cap;
+        const int64_t plane = (int64_t)t * a.E;
+        uint64_t gm = mask & gmask;
+        while (__ballot(gm != 0)) {
+            int b = -1;
+            if (gm) { b = __ffsll((long long)gm) - 1; gm &= gm - 1; }
+            const uint32_t fromj = __shfl(from_l, b < 0 ? lane : b, 64);
+            if (b < 0) continue;
+            const uint32_t j = (uint32_t)(j0 + b);
+            const uint32_t beg = a.row_ptr[j];
+            const uint32_t deg = a.row_ptr[j + 1] - beg;
+            if ((uint32_t)gl >= deg) continue;
+            const uint32_t e = beg + (uint32_t)gl;
+            const uint32_t i = a.col[e];
+            if (!(a.mflags[plane + e] & GSIM_TF_MESH) || !(a.rstate[e] & GSIM_ES_CONNECTED) || i == fromj ||
+                i == origin)
+                continue;
+            if (!a.acc[e]) { n_gray++; continue; }     // AcceptFrom: graylisted sender
+            n_acc++;
+            uint32_t* cell = a.seen + row_m + i;
+            const uint32_t c = *cell;
+            const bool old = c < kClaim;                 // committed in an earlier round
+            if (!old) __hip_atomic_fetch_min(cell, kClaim | e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!scored_t || !(a.estate[e] & GSIM_ES_TRACKED)) continue;
+            const int64_t ir = plane + e;
+            if (inv) {                                   // markInvalidMessageDelivery
+                a.invalid[ir] = a.invalid[ir] + 1.0;
                 continue;
             }
-            s_acc++;
-            const uint32_t c = a.seen[(int64_t)slot * a.N + recv];
-            const int32_t t = (int32_t)a.mtopic[slot];
-            const bool inv = a.minv[slot] != 0;
-            const bool first = c == (kClaim | er);
-            const bool scored = (a.estate[er] & GSIM_ES_TRACKED) && tp[t].scored;
-            const int64_t te = (int64_t)t * a.E + er;
-            if (first) {
-                s_first++;
-                fmask |= 1u << r;
-                fr[r] = recv;
-                fs[r] = slot;
-                ff[r] = a.col[er];
-                if (scored) {
-                    if (inv) {
-                        inc_capped(&a.invalid[te], __builtin_inf());
-                    } else {
-                        inc_capped(&a.first[te], tp[t].first_message_deliveries_cap);
-                        if (a.tflags[te] & GSIM_TF_IN_MESH)
-                            inc_capped(&a.meshd[te], tp[t].mesh_message_deliveries_cap);
-                    }
-                }
-                if (!inv) a.lastput[(int64_t)t * a.N + recv] = tick;
-            } else if (scored) {
-                if (inv) {
-                    inc_capped(&a.invalid[te], __builtin_inf());
-                } else if (a.tflags[te] & GSIM_TF_IN_MESH) {
-                    const int64_t validated = (c & kClaim) ? a.now : round_time(a, (int64_t)c);
-                    if (a.now - validated <= tp[t].mesh_message_deliveries_window_ns)
-                        inc_capped(&a.meshd[te], tp[t].mesh_message_deliveries_cap);
-                }
-            }
+            if (!(a.tflags[ir] & GSIM_TF_IN_MESH)) continue;
+            // markDuplicateMessageDelivery's window test; a same-round copy
+            // (first or duplicate) has validated = now
+            const bool in_window = old ? (a.now - round_time(a, (int64_t)c) <= window) : (window >= 0);
+            if (in_window) inc_capped(&a.meshd[ir], mcap);
         }
-        uint32_t total;
-        const uint32_t excl = block_excl_scan((uint32_t)__popc(fmask), s_wt, &total);
-        if (threadIdx.x == 0) s_base = total ? atomicAdd(&a.cnt[a.g & 1], total) : 0u;
-        __syncthreads();
-        uint32_t pos = s_base + excl;
-#pragma unroll
-        for (int r = 0; r < kResolveItems; ++r) {
-            if (!((fmask >> r) & 1u)) continue;
-            if ((int64_t)pos < a.max_frontier) {
-                a.f_peer[pos] = fr[r];
-                a.f_slot[pos] = fs[r];
-                a.f_from[pos] = ff[r];
-            } else {
-                atomicOr(&a.cnt[4], 1u);
-            }
-            ++pos;
-        }
-        __syncthreads();   // s_wt / s_base reuse
     }
-    s_acc = wave_sum_u64(s_acc);
-    s_first = wave_sum_u64(s_first);
-    s_gray = wave_sum_u64(s_gray);
-    if (lane == 0 && (s_acc | s_gray)) {
-        atomicAdd(&a.stats[0], s_acc);
-        atomicAdd(&a.stats[1], s_first);
-        atomicAdd(&a.stats[2], s_acc - s_first);
-        atomicAdd(&a.stats[3], s_gray);
+    n_acc = wave_sum_u64(n_acc);
+    n_gray = wave_sum_u64(n_gray);
+    if (lane == 0 && (n_acc | n_gray)) {
+        atomicAdd(&a.stats[0], n_acc);
+        atomicAdd(&a.stats[2], n_acc);          // k_commit moves the firsts out
+        atomicAdd(&a.stats[3], n_gray);
     }
 }
 
-// Mesh targets of frontier entry q as a lane mask over the sender's row
-// (rows of at most 64 connections); lane 0 commits the first-seen round.
-// Must be called by a whole wave.
-__device__ __forceinline__ uint64_t forward_mask(const RoundArgs& a, uint32_t q, bool commit)
+// Round g, step 2: commit every claimed cell (markSeen) and credit the
+// winner's first delivery (markFirstMessageDelivery, score.go:919-946).
+__global__ __launch_bounds__(256) void k_commit(RoundArgs a)
 {
+    __shared__ uint16_t s_act[kMaxRing];
+    __shared__ int s_n;
+    const int nact = a.g > 0 ? active_slots(a, s_act, &s_n) : 0;
     const int lane = threadIdx.x & 63;
-    const uint32_t j = a.f_peer[q], slot = a.f_slot[q], from = a.f_from[q];
-    if (commit && lane == 0) a.seen[(int64_t)slot * a.N + j] = (uint32_t)a.g;
-    const uint32_t t = a.mtopic[slot], origin = a.morigin[slot];
-    // receivers reject an invalid message and do not forward it; its
-    // origin publishes it regardless
-    if (a.minv[slot] && j != origin) return 0;
-    const uint32_t b = a.row_ptr[j], deg = a.row_ptr[j + 1] - b;
-    const uint32_t e = b + (uint32_t)lane;
-    bool ok = false;
-    if ((uint32_t)lane < deg) {
-        const uint32_t i = a.col[e];
-        ok = (a.tflags[(int64_t)t * a.E + e] & GSIM_TF_MESH) && (a.estate[e] & GSIM_ES_CONNECTED) && i != from &&
-             i != origin;
+    const int64_t i0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+    if (i0 >= a.N) return;
+    const int64_t i = i0 + lane;
+    const bool vi = i < a.N;
+    const ctp_t tpa = const_tp(a.tp);
+    const int32_t tick = (int32_t)(a.g / a.R);
+    unsigned long long n_first = 0;
+    for (int k = 0; k < nact; ++k) {
+        const uint32_t m = s_act[k];
+        const int64_t cell = (int64_t)m * a.N + i;
+        const uint32_t c = vi ? a.seen[cell] : kUnseen;
+        const bool claimed = c != kUnseen && (c & kClaim);
+        const uint64_t cm = __ballot(claimed);
+        if (!cm) continue;
+        if (lane == 0) atomicAdd(&a.nfirst_cur[m], (uint32_t)__popcll(cm));
+        if (!claimed) continue;
+        n_first++;
+        const uint32_t ew = c & ~kClaim;           // winning edge = the receiver's record of the sender
+        const int32_t t = (int32_t)a.mtopic[m];
+        const bool inv = a.minv[m] != 0;
+        a.seen[cell] = (uint32_t)a.g;
+        a.from[cell] = a.owner[ew];
+        if (inv) continue;                          // RejectMessage: counted by k_send
+        a.lastput[(int64_t)t * a.N + i] = tick;     // mcache.Put
+        const ctp_t tp = tpa + t;
+        if (!tp->scored || !(a.estate[ew] & GSIM_ES_TRACKED)) continue;
+        const int64_t ir = (int64_t)t * a.E + ew;
+        inc_capped(&a.first[ir], tp->first_message_deliveries_cap);
+        // with a negative window k_send credits no same-round copy; the first
+        // delivery is credited regardless of the window
+        if (tp->mesh_message_deliveries_window_ns < 0 && (a.tflags[ir] & GSIM_TF_IN_MESH))
+            inc_capped(&a.meshd[ir], tp->mesh_message_deliveries_cap);
     }
-    return __ballot(ok);
-}
-
-// Step 3: commit first-seen rounds and forward to the mesh.  A block takes 256
-// frontier entries (64 per wave): pass 1 builds each entry's target mask,
-// one global atomic reserves the block's output range, pass 2 writes it.
-__global__ __launch_bounds__(256) void k_forward(RoundArgs a)
-{
-    __shared__ uint32_t s_wt[4];
-    __shared__ uint32_t s_base;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        // the lists of round g+1's parity were consumed by round g-1 / g
-        a.cnt[(a.g + 1) & 1] = 0;
-        a.cnt[2 + ((a.g + 1) & 1)] = 0;
-    }
-    const uint32_t n = min(a.cnt[a.g & 1], (uint32_t)a.max_frontier);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (uint32_t c0 = blockIdx.x * 256; c0 < n; c0 += gridDim.x * 256) {
-        const uint32_t w0 = c0 + (uint32_t)wid * 64;
-        uint64_t my_mask = 0;
-        for (int q = 0; q < 64; ++q) {
-            if (w0 + q >= n) break;
-            const uint64_t m = forward_mask(a, w0 + q, true);
-            if (lane == q) my_mask = m;
-        }
-        uint32_t total;
-        const uint32_t excl = block_excl_scan((uint32_t)__popcll(my_mask), s_wt, &total);
-        if (threadIdx.x == 0) s_base = total ? atomicAdd(&a.cnt[2 + (a.g & 1)], total) : 0u;
-        __syncthreads();
-        const uint32_t base = s_base;
-        for (int q = 0; q < 64; ++q) {
-            const uint32_t idx = w0 + q;
-            if (idx >= n) break;
-            const uint64_t m = __shfl(my_mask, q, 64);
-            if (!m) continue;
-            const uint32_t off = base + __shfl(excl, q, 64);
-            if ((m >> lane) & 1ull) {
-                const uint32_t j = a.f_peer[idx];
-                const uint32_t e = a.row_ptr[j] + (uint32_t)lane;
-                const uint32_t pos = off + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-                if ((int64_t)pos < a.max_arrivals) {
-                    a.o_er[pos] = a.rev[e];
-                    a.o_slot[pos] = a.f_slot[idx];
-                    a.o_recv[pos] = a.col[e];
-                } else {
-                    atomicOr(&a.cnt[4], 1u);
-                }
-            }
-        }
-        __syncthreads();   // s_wt / s_base reuse
+    n_first = wave_sum_u64(n_first);
+    if (lane == 0 && n_first) {
+        atomicAdd(&a.stats[1], n_first);
+        atomicAdd(&a.stats[2], 0ull - n_first);   // duplicates = accepted - first
     }
 }
 
@@ -345,10 +281,8 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_seen); f(d->d_lastput);
-    for (int p = 0; p < 2; ++p)
-        for (int k = 0; k < 3; ++k) { f(d->d_f[p][k]); f(d->d_a[p][k]); }
-    f(d->d_cnt); f(d->d_stats); f(d->d_pub);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_seen); f(d->d_from); f(d->d_lastput);
+    f(d->d_nfirst); f(d->d_stats); f(d->d_pub);
     delete d;
 }
 
@@ -375,17 +309,15 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.N = h->n; a.E = h->e; a.T = h->t; a.ring = d->cfg.ring; a.R = d->cfg.rounds;
     a.t0 = d->cfg.t0_ns; a.hb = d->cfg.heartbeat_ns; a.g = g;
     a.now = a.t0 + (g / a.R) * a.hb + (g % a.R + 1) * a.hb / (a.R + 1);
-    a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.rev = h->d_rev;
-    a.estate = h->d_estate; a.score = h->d_score; a.tp = h->d_tp; a.gray = h->th.graylist_threshold;
-    a.tflags = h->d_tflags; a.first = h->d_first; a.meshd = h->d_meshd; a.invalid = h->d_invalid;
+    a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.owner = h->d_owner;
+    a.rstate = h->d_rstate; a.mflags = h->d_mflags; a.acc = h->d_acc;
+    a.estate = h->d_estate; a.tflags = h->d_tflags; a.tp = h->d_tp;
+    a.first = h->d_first; a.meshd = h->d_meshd; a.invalid = h->d_invalid;
     a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv;
-    a.seen = d->d_seen; a.lastput = d->d_lastput;
-    const int pin = (int)((g + 1) & 1), pout = (int)(g & 1);
-    a.a_er = d->d_a[pin][0]; a.a_slot = d->d_a[pin][1]; a.a_recv = d->d_a[pin][2];
-    a.o_er = d->d_a[pout][0]; a.o_slot = d->d_a[pout][1]; a.o_recv = d->d_a[pout][2];
-    a.f_peer = d->d_f[pout][0]; a.f_slot = d->d_f[pout][1]; a.f_from = d->d_f[pout][2];
-    a.cnt = d->d_cnt;
-    a.max_frontier = d->cfg.max_frontier; a.max_arrivals = d->cfg.max_arrivals;
+    a.seen = d->d_seen; a.from = d->d_from; a.lastput = d->d_lastput;
+    const size_t ring = (size_t)d->cfg.ring;
+    a.nfirst_prev = d->d_nfirst + (size_t)((g + 1) & 1) * ring;
+    a.nfirst_cur = d->d_nfirst + (size_t)(g & 1) * ring;
     a.stats = d->d_stats;
     return a;
 }
@@ -397,11 +329,11 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     if (!h || !cfg) return GSIM_EINVAL;
     if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
     if (h->e == 0) { h->err = "no graph loaded"; return GSIM_ESTATE; }
-    if (cfg->ring <= 0 || cfg->rounds < 2 || cfg->heartbeat_ns <= 0 || cfg->max_frontier <= 0 ||
-        cfg->max_arrivals <= 0 || cfg->max_frontier > 0x7FFFFFFF || cfg->max_arrivals > 0x7FFFFFFF) {
-        h->err = "invalid message configuration";
+    if (cfg->ring <= 0 || cfg->ring > kMaxRing || cfg->rounds < 2 || cfg->heartbeat_ns <= 0) {
+        h->err = "invalid message configuration (ring must be in [1, 8192], rounds >= 2, heartbeat > 0)";
         return GSIM_EINVAL;
     }
+    if (h->e >= (int64_t)kClaim) { h->err = "too many edges for the seen-set claim encoding"; return GSIM_ERANGE; }
     (void)hipStreamSynchronize(h->stream);
     free_deliver(h);
     Deliver* d = new Deliver();
@@ -416,13 +348,9 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_morigin, ring * 4);
     A((void**)&d->d_minv, ring);
     A((void**)&d->d_seen, ring * N * 4);
+    A((void**)&d->d_from, ring * N * 4);
     A((void**)&d->d_lastput, T * N * 4);
-    for (int p = 0; p < 2; ++p)
-        for (int k = 0; k < 3; ++k) {
-            A((void**)&d->d_f[p][k], (size_t)cfg->max_frontier * 4);
-            A((void**)&d->d_a[p][k], (size_t)cfg->max_arrivals * 4);
-        }
-    A((void**)&d->d_cnt, 8 * 4);
+    A((void**)&d->d_nfirst, 2 * ring * 4);
     A((void**)&d->d_stats, 4 * 8);
     if (e != hipSuccess) {
         dl_free(d);
@@ -431,11 +359,12 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     }
     h->dl = d;
     e = hipMemsetAsync(d->d_seen, 0xFF, ring * N * 4, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_from, 0, ring * N * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_lastput, 0xFF, T * N * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_mtopic, 0, ring * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_morigin, 0, ring * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_minv, 0, ring, h->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(d->d_cnt, 0, 8 * 4, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_nfirst, 0, 2 * ring * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_stats, 0, 4 * 8, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     return hip_check(h, e, "gsim_msgs_init");
@@ -494,7 +423,7 @@ int gsim_round(gsim_handle* h, int64_t round)
     if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
     Deliver* d = h->dl;
     if (!d) { h->err = "gsim_msgs_init not called"; return GSIM_ESTATE; }
-    if (round < 0 || round >= 0x7FFFFFFF) return GSIM_ERANGE;
+    if (round < 0 || round >= 0x7FFFFFFF) { h->err = "round out of range [0, 2^31-1)"; return GSIM_ERANGE; }
     if (d->next_round >= 0 && round != d->next_round) {
         h->err = "rounds must be consecutive";
         return GSIM_ESTATE;
@@ -503,16 +432,33 @@ int gsim_round(gsim_handle* h, int64_t round)
         h->err = "propagation kernels support rows of at most 64 connections in this build";
         return GSIM_ERANGE;
     }
+    int rc = 0;
+    {
+        ProfScope ps(h, GSIM_K_ACCEPT);
+        rc = refresh_accept(h);
+        if (rc) return rc;
+    }
     RoundArgs a = make_round_args(h, round);
+    const int64_t waves = (h->n + 63) / 64;
+    const int grid = (int)std::max<int64_t>((waves + 3) / 4, 1);
     {
-        ProfScope ps(h, GSIM_K_CLAIM);
-        hipLaunchKernelGGL(k_claim, dim3(kListGrid), dim3(256), 0, h->stream, a);
+        ProfScope ps(h, GSIM_K_SEND);
+        if (h->max_degree <= 16)
+            hipLaunchKernelGGL(k_send<16>, dim3(grid), dim3(256), 0, h->stream, a);
+        else if (h->max_degree <= 32)
+            hipLaunchKernelGGL(k_send<32>, dim3(grid), dim3(256), 0, h->stream, a);
+        else
+            hipLaunchKernelGGL(k_send<64>, dim3(grid), dim3(256), 0, h->stream, a);
     }
     {
-        ProfScope ps(h, GSIM_K_RESOLVE);
-        hipLaunchKernelGGL(k_resolve, dim3(kListGrid), dim3(256), 0, h->stream, a);
+        ProfScope ps(h, GSIM_K_COMMIT);
+        hipLaunchKernelGGL(k_commit, dim3(grid), dim3(256), 0, h->stream, a);
+        // the counters of round g+1 were last read as "previous" by round g
+        hipError_t e = hipMemsetAsync(d->d_nfirst + (size_t)((round + 1) & 1) * (size_t)d->cfg.ring, 0,
+                                      (size_t)d->cfg.ring * 4, h->stream);
+        if (e != hipSuccess) return hip_check(h, e, "nfirst reset");
     }
-    int rc = hip_check(h, hipGetLastError(), "k_claim/k_resolve");
+    rc = hip_check(h, hipGetLastError(), "k_send/k_commit");
     if (rc) return rc;
     const int32_t r = (int32_t)(round % d->cfg.rounds);
     if (r < 2) {
@@ -521,12 +467,8 @@ int gsim_round(gsim_handle* h, int64_t round)
         rc = gsim_handle_control(h, r, a.now);
         if (rc) return rc;
     }
-    {
-        ProfScope ps(h, GSIM_K_FORWARD);
-        hipLaunchKernelGGL(k_forward, dim3(kListGrid), dim3(256), 0, h->stream, a);
-    }
     d->next_round = round + 1;
-    return hip_check(h, hipGetLastError(), "k_forward");
+    return GSIM_OK;
 }
 
 int gsim_msg_stats(gsim_handle* h, int64_t* out4)
@@ -536,16 +478,10 @@ int gsim_msg_stats(gsim_handle* h, int64_t* out4)
     Deliver* d = h->dl;
     if (!d) { h->err = "gsim_msgs_init not called"; return GSIM_ESTATE; }
     unsigned long long s[4];
-    uint32_t ovf = 0;
     hipError_t e = hipMemcpyAsync(s, d->d_stats, sizeof(s), hipMemcpyDeviceToHost, h->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(&ovf, d->d_cnt + 4, 4, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return hip_check(h, e, "gsim_msg_stats");
     for (int k = 0; k < 4; ++k) out4[k] = (int64_t)s[k];
-    if (ovf) {
-        h->err = "a round overflowed max_frontier or max_arrivals";
-        return GSIM_ERANGE;
-    }
     return GSIM_OK;
 }
 

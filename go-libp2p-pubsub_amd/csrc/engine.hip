@@ -44,9 +44,11 @@ __device__ __forceinline__ int64_t go_div(int64_t n, int64_t d)
 
 // ---------------------------------------------------------------------------
 // Kernel 1:peerScore.refreshScores (score.go:504-565) fused with
-// peerScore.score (score.go:265-342).  One thread per observer->neighbour edge,
-// grid-stride; the topic loop reads the [T][E] arrays at t*E + e, so each
-// wave-instruction touches 64 consecutive records of one topic (coalesced).
+// peerScore.score (score.go:265-342).  One thread per record (record order,
+// the record of observer col[r] about neighbour owner[r]),
+// grid-stride; the topic loop reads the [T][E] arrays at t*E + r, so each
+// wave-instruction touches 64 consecutive records of one topic (coalesced),
+// and the P5 gather p5[owner[r]] hits one or two rows per wave.
 // Topic parameters are wave-uniform (scalar loads).  Operation order is the
 // reference's, compiled with -ffp-contract=off: results are bit-identical to
 // the CPU oracle.
@@ -137,7 +139,7 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
         }
         if (SCORE) {
             if (a.topic_cap > 0 && score > a.topic_cap) score = a.topic_cap;
-            const double p5 = a.p5[a.col[e]];                              // P5
+            const double p5 = a.p5[a.owner[e]];                           // P5 (neighbour = row owner)
             score += p5 * a.w5;
             score += a.p6[e] * a.w6;                                       // P6
             if (bp > a.bp_thr) {                                           // P7
@@ -200,7 +202,7 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
             bp = a.bp[e];
             if (SCORE) {
                 p6 = a.p6[e];
-                c = a.col[e];
+                c = a.owner[e];   // the neighbour this record is about
             }
         }
         if (SCORE && valid && !(a.diag & DIAG_NO_P5)) p5 = a.p5[c];
@@ -336,13 +338,15 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
 // Kernel 2: ipColocationFactor (score.go:344-388) as a segmented count over
 // each observer's row keyed by IP id.  Only re-run when the tracked set or the
 // IP assignment changes (AddPeer/RemovePeer/purge), not every heartbeat.
-// Thread per edge; the row scan hits L1/L2 (rows are k ~ 32).
+// Thread per observer edge e (observer owner[e], neighbour col[e]); the
+// result is the P6 value of record rev[e].  The row scan hits L1/L2.
 __global__ __launch_bounds__(256) void k_ip_colocation(ColocArgs a)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
+        const uint32_t r = a.rev[e];
         double res = 0.0;
-        if (a.estate[e] & GSIM_ES_TRACKED) {
+        if (a.estate[r] & GSIM_ES_TRACKED) {
             const uint32_t i = a.owner[e];
             const uint32_t b = a.row_ptr[i], en = a.row_ptr[i + 1];
             const uint32_t j = a.col[e];
@@ -351,7 +355,7 @@ __global__ __launch_bounds__(256) void k_ip_colocation(ColocArgs a)
                 if (a.ip_white && a.ip_white[ip]) continue;
                 int32_t cnt = 0;
                 for (uint32_t e2 = b; e2 < en; ++e2) {
-                    if (!(a.estate[e2] & GSIM_ES_TRACKED)) continue;
+                    if (!(a.estate[a.rev[e2]] & GSIM_ES_TRACKED)) continue;
                     const uint32_t j2 = a.col[e2];
                     for (uint32_t q2 = a.ip_ptr[j2]; q2 < a.ip_ptr[j2 + 1]; ++q2)
                         if (a.ip_ids[q2] == ip) { ++cnt; break; }
@@ -362,7 +366,7 @@ __global__ __launch_bounds__(256) void k_ip_colocation(ColocArgs a)
                 }
             }
         }
-        a.p6[e] = res;
+        a.p6[r] = res;
     }
 }
 
@@ -383,29 +387,35 @@ __global__ __launch_bounds__(256) void k_recap(int64_t E, const uint8_t* estate,
 // membership (probability D/k), activation, graft time and the four counters.
 __global__ __launch_bounds__(256) void k_fill_synthetic(ScoreArgs a, uint64_t seed, double p_mesh)
 {
+    // thread per observer edge e; its record lives at r = rev[e]
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     const double inv = 1.0 / 4294967296.0;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
+        const int64_t r = a.rev[e];
         for (int32_t t = 0; t < a.T; ++t) {
             const int64_t i = (int64_t)t * a.E + e;
-            const u32x4 r = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), 0x5eed, 1, k0, k1);
+            const int64_t ir = (int64_t)t * a.E + r;
+            const u32x4 x = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), 0x5eed, 1, k0, k1);
             const u32x4 q = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), 0x5eed, 2, k0, k1);
-            const bool in_mesh = r.x * inv < p_mesh;
-            uint8_t fl = in_mesh ? (GSIM_TF_IN_MESH | GSIM_TF_MESH) : 0;
-            if (in_mesh && (r.y & 15) != 0) fl |= GSIM_TF_ACTIVE;
-            a.tflags[i] = fl;
-            a.graft[i] = in_mesh ? a.now - (int64_t)(r.z % 3600u) * 1000000000LL : 0;
-            a.mtime[i] = in_mesh ? a.now - a.graft[i] : 0;
-            a.first[i] = (double)(q.x % 2000u) * 0.25;
-            a.meshd[i] = in_mesh ? (double)(q.y % 1600u) * 0.25 : 0.0;
-            a.fail[i] = (q.z & 7) == 0 ? (double)(q.z % 4000u) * 0.125 : 0.0;
-            a.invalid[i] = (q.w & 511) == 0 ? (double)(q.w % 64u) * 0.125 : 0.0;
+            const bool in_mesh = x.x * inv < p_mesh;
+            uint8_t fl = in_mesh ? GSIM_TF_IN_MESH : 0;
+            if (in_mesh && (x.y & 15) != 0) fl |= GSIM_TF_ACTIVE;
+            a.tflags[ir] = fl;
+            a.mflags[i] = in_mesh ? GSIM_TF_MESH : 0;
+            const int64_t g = in_mesh ? a.now - (int64_t)(x.z % 3600u) * 1000000000LL : 0;
+            a.graft[ir] = g;
+            a.mtime[ir] = in_mesh ? a.now - g : 0;
+            a.first[ir] = (double)(q.x % 2000u) * 0.25;
+            a.meshd[ir] = in_mesh ? (double)(q.y % 1600u) * 0.25 : 0.0;
+            a.fail[ir] = (q.z & 7) == 0 ? (double)(q.z % 4000u) * 0.125 : 0.0;
+            a.invalid[ir] = (q.w & 511) == 0 ? (double)(q.w % 64u) * 0.125 : 0.0;
         }
         const u32x4 b = philox4x32_10((uint32_t)e, (uint32_t)(e >> 32), 0x5eed, 3, k0, k1);
-        a.bp[e] = (b.x & 15) == 0 ? (double)(b.y % 100u) * 0.125 : 0.0;
-        a.estate[e] = GSIM_ES_TRACKED | GSIM_ES_CONNECTED;
-        a.expire[e] = 0;
+        a.bp[r] = (b.x & 15) == 0 ? (double)(b.y % 100u) * 0.125 : 0.0;
+        a.estate[r] = GSIM_ES_TRACKED | GSIM_ES_CONNECTED;
+        a.expire[r] = 0;
+        a.rstate[e] = GSIM_ES_CONNECTED;
     }
 }
 
@@ -429,8 +439,12 @@ __global__ __launch_bounds__(256) void k_census(ScoreArgs a, unsigned long long*
             c[3] += a.meshd[i] != 0.0;
             c[4] += a.fail[i] != 0.0;
             c[5] += a.invalid[i] != 0.0;
-            c[6] += (fl & GSIM_TF_MESH) != 0;
         }
+    }
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
+        if (!(a.rstate[e] & GSIM_ES_CONNECTED)) continue;   // router mesh links (edge order)
+        for (int32_t t = 0; t < a.T; ++t)
+            c[6] += (a.mflags[(int64_t)t * a.E + e] & GSIM_TF_MESH) != 0;
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -438,6 +452,59 @@ __global__ __launch_bounds__(256) void k_census(ScoreArgs a, unsigned long long*
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
         if ((threadIdx.x & 63) == 0 && v) atomicAdd(&out[k], v);
     }
+}
+
+// Layout permutations between the ABI's edge-order view and record order
+// (DESIGN.md §2).  rev is an involution, so one gather serves both ways.
+template <typename T>
+__global__ __launch_bounds__(256) void k_gather_rev(const T* __restrict__ in, T* __restrict__ out,
+                                                    const uint32_t* __restrict__ rev, int64_t E, int64_t total)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += stride) {
+        const int64_t p = x / E, e = x - p * E;
+        out[x] = in[p * E + rev[e]];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_tflags_compose(const uint8_t* rec, const uint8_t* mf, uint8_t* out,
+                                                        const uint32_t* rev, int64_t E, int64_t total)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += stride) {
+        const int64_t p = x / E, e = x - p * E;
+        out[x] = (uint8_t)((rec[p * E + rev[e]] & (GSIM_TF_IN_MESH | GSIM_TF_ACTIVE)) | (mf[x] & GSIM_TF_MESH));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_tflags_split(const uint8_t* in, uint8_t* rec, uint8_t* mf,
+                                                      const uint32_t* rev, int64_t E, int64_t total)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += stride) {
+        const int64_t p = x / E, e = x - p * E;
+        rec[x] = (uint8_t)(in[p * E + rev[e]] & (GSIM_TF_IN_MESH | GSIM_TF_ACTIVE));
+        mf[x] = (uint8_t)(in[x] & GSIM_TF_MESH);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_estate_split(const uint8_t* in, uint8_t* rec, uint8_t* rs,
+                                                      const uint32_t* rev, int64_t E)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride) {
+        rec[e] = in[rev[e]];
+        rs[e] = (uint8_t)(in[e] & GSIM_ES_CONNECTED);
+    }
+}
+
+// AcceptFrom (gossipsub.go:598-609) verdict of every record's observer for
+// its neighbour, from the score snapshot: score >= graylistThreshold.
+__global__ __launch_bounds__(256) void k_accept(const double* score, uint8_t* acc, int64_t E, double gray)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < E; r += stride)
+        acc[r] = score[r] >= gray ? 1 : 0;
 }
 
 __global__ void k_fill_u8(uint8_t* p, int64_t n, uint8_t v)
@@ -495,9 +562,9 @@ void free_graph(gsim_handle* h)
     dfree(h->d_sub); dfree(h->d_outbound);
     dfree(h->d_ip_ptr); dfree(h->d_ip_ids); dfree(h->d_ip_white); dfree(h->d_p5);
     dfree(h->d_first); dfree(h->d_meshd); dfree(h->d_fail); dfree(h->d_invalid);
-    dfree(h->d_graft); dfree(h->d_mtime); dfree(h->d_tflags);
+    dfree(h->d_graft); dfree(h->d_mtime); dfree(h->d_tflags); dfree(h->d_mflags);
     dfree(h->d_bp); dfree(h->d_estate); dfree(h->d_expire); dfree(h->d_p6); dfree(h->d_score);
-    dfree(h->d_backoff);
+    dfree(h->d_backoff); dfree(h->d_rstate); dfree(h->d_acc);
     h->bytes_allocated = 0;
     h->n = h->e = 0;
 }
@@ -515,10 +582,11 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     a.w6 = h->pp.ip_colocation_factor_weight;
     a.bp_thr = h->pp.behaviour_penalty_threshold;
     a.w7 = h->pp.behaviour_penalty_weight;
-    a.col = h->d_col;
+    a.owner = h->d_owner;
     a.p5 = h->d_p5;
     a.first = h->d_first; a.meshd = h->d_meshd; a.fail = h->d_fail; a.invalid = h->d_invalid;
     a.graft = h->d_graft; a.mtime = h->d_mtime; a.tflags = h->d_tflags;
+    a.mflags = h->d_mflags; a.rstate = h->d_rstate; a.rev = h->d_rev;
     a.bp = h->d_bp; a.estate = h->d_estate; a.expire = h->d_expire; a.p6 = h->d_p6; a.score = h->d_score;
     a.now = now;
     a.purged = h->d_flags;
@@ -530,7 +598,7 @@ int launch_ip_colocation(gsim_handle* h)
 {
     ProfScope ps(h, GSIM_K_IP_COLOCATION);
     ColocArgs c{};
-    c.E = h->e; c.row_ptr = h->d_row_ptr; c.col = h->d_col; c.owner = h->d_owner;
+    c.E = h->e; c.row_ptr = h->d_row_ptr; c.col = h->d_col; c.rev = h->d_rev; c.owner = h->d_owner;
     c.ip_ptr = h->d_ip_ptr; c.ip_ids = h->d_ip_ids; c.ip_white = h->has_white ? h->d_ip_white : nullptr;
     c.estate = h->d_estate; c.p6 = h->d_p6; c.thr = h->pp.ip_colocation_factor_threshold;
     hipLaunchKernelGGL(k_ip_colocation, dim3(grid_for(h->e)), dim3(256), 0, h->stream, c);
@@ -588,6 +656,7 @@ int launch_refresh_scores(gsim_handle* h, int64_t now)
     } else {
         launch_score_kernel<true, true>(h, a);
     }
+    h->score_version++;
     return hip_check(h, hipGetLastError(), "k_refresh_score");
 }
 
@@ -599,11 +668,88 @@ int launch_compute_scores(gsim_handle* h)
     }
     ScoreArgs a = make_score_args(h, 0);
     launch_score_kernel<false, true>(h, a);
+    h->score_version++;
     return hip_check(h, hipGetLastError(), "k_refresh_score<score>");
+}
+
+int refresh_accept(gsim_handle* h)
+{
+    if (h->acc_version == h->score_version) return GSIM_OK;
+    hipLaunchKernelGGL(k_accept, dim3(grid_for(h->e)), dim3(256), 0, h->stream, (const double*)h->d_score,
+                       h->d_acc, h->e, h->th.graylist_threshold);
+    h->acc_version = h->score_version;
+    return hip_check(h, hipGetLastError(), "k_accept");
 }
 
 // ---------------------------------------------------------------------------
 // C ABI
+
+// Copy a field to the host in the ABI's edge-order view.
+static int read_field_impl(gsim_handle* h, const FieldRef& r, void* dst)
+{
+    hipError_t e = hipSuccess;
+    if (r.kind == FK_RAW) {
+        e = hipMemcpyAsync(dst, r.ptr, r.bytes, hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        return hip_check(h, e, "gsim_read_field");
+    }
+    void* tmp = nullptr;
+    e = hipMalloc(&tmp, std::max<size_t>(r.bytes, 8));
+    if (e != hipSuccess) return hip_check(h, e, "gsim_read_field scratch");
+    const int64_t E = h->e;
+    const int64_t total = r.kind == FK_RECORD ? (int64_t)(r.bytes / (size_t)r.elem) : (int64_t)r.bytes;
+    const int g = grid_for(total);
+    if (r.kind == FK_RECORD && r.elem == 8)
+        hipLaunchKernelGGL(k_gather_rev<uint64_t>, dim3(g), dim3(256), 0, h->stream, (const uint64_t*)r.ptr,
+                           (uint64_t*)tmp, (const uint32_t*)h->d_rev, E, total);
+    else if (r.kind == FK_RECORD || r.kind == FK_ESTATE)
+        hipLaunchKernelGGL(k_gather_rev<uint8_t>, dim3(g), dim3(256), 0, h->stream, (const uint8_t*)r.ptr,
+                           (uint8_t*)tmp, (const uint32_t*)h->d_rev, E, total);
+    else
+        hipLaunchKernelGGL(k_tflags_compose, dim3(g), dim3(256), 0, h->stream, (const uint8_t*)h->d_tflags,
+                           (const uint8_t*)h->d_mflags, (uint8_t*)tmp, (const uint32_t*)h->d_rev, E, total);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(dst, tmp, r.bytes, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    (void)hipFree(tmp);
+    return hip_check(h, e, "gsim_read_field");
+}
+
+// Install a field given in the ABI's edge-order view.
+static int write_field_impl(gsim_handle* h, const FieldRef& r, const void* src)
+{
+    hipError_t e = hipSuccess;
+    if (r.kind == FK_RAW) {
+        e = hipMemcpyAsync(r.ptr, src, r.bytes, hipMemcpyHostToDevice, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        return hip_check(h, e, "gsim_write_field");
+    }
+    void* tmp = nullptr;
+    e = hipMalloc(&tmp, std::max<size_t>(r.bytes, 8));
+    if (e != hipSuccess) return hip_check(h, e, "gsim_write_field scratch");
+    e = hipMemcpyAsync(tmp, src, r.bytes, hipMemcpyHostToDevice, h->stream);
+    const int64_t E = h->e;
+    const int64_t total = r.kind == FK_RECORD ? (int64_t)(r.bytes / (size_t)r.elem) : (int64_t)r.bytes;
+    const int g = grid_for(total);
+    if (e == hipSuccess) {
+        if (r.kind == FK_RECORD && r.elem == 8)
+            hipLaunchKernelGGL(k_gather_rev<uint64_t>, dim3(g), dim3(256), 0, h->stream, (const uint64_t*)tmp,
+                               (uint64_t*)r.ptr, (const uint32_t*)h->d_rev, E, total);
+        else if (r.kind == FK_RECORD)
+            hipLaunchKernelGGL(k_gather_rev<uint8_t>, dim3(g), dim3(256), 0, h->stream, (const uint8_t*)tmp,
+                               (uint8_t*)r.ptr, (const uint32_t*)h->d_rev, E, total);
+        else if (r.kind == FK_ESTATE)
+            hipLaunchKernelGGL(k_estate_split, dim3(g), dim3(256), 0, h->stream, (const uint8_t*)tmp,
+                               h->d_estate, h->d_rstate, (const uint32_t*)h->d_rev, E);
+        else
+            hipLaunchKernelGGL(k_tflags_split, dim3(g), dim3(256), 0, h->stream, (const uint8_t*)tmp, h->d_tflags,
+                               h->d_mflags, (const uint32_t*)h->d_rev, E, total);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    (void)hipFree(tmp);
+    return hip_check(h, e, "gsim_write_field");
+}
 
 #define GSIM_ENTER(h)                                                     \
     do {                                                                  \
@@ -781,7 +927,10 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     rc = rc ? rc : dalloc(h, &h->d_graft, ET);
     rc = rc ? rc : dalloc(h, &h->d_mtime, ET);
     rc = rc ? rc : dalloc(h, &h->d_tflags, ET);
+    rc = rc ? rc : dalloc(h, &h->d_mflags, ET);
     rc = rc ? rc : dalloc(h, &h->d_backoff, ET);
+    rc = rc ? rc : dalloc(h, &h->d_rstate, E);
+    rc = rc ? rc : dalloc(h, &h->d_acc, E);
     rc = rc ? rc : dalloc(h, &h->d_bp, E);
     rc = rc ? rc : dalloc(h, &h->d_estate, E);
     rc = rc ? rc : dalloc(h, &h->d_expire, E);
@@ -818,6 +967,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     zero(h->d_graft, sizeof(int64_t) * (size_t)ET);
     zero(h->d_mtime, sizeof(int64_t) * (size_t)ET);
     zero(h->d_tflags, (size_t)ET);
+    zero(h->d_mflags, (size_t)ET);
     zero(h->d_backoff, sizeof(int64_t) * (size_t)ET);
     zero(h->d_bp, sizeof(double) * (size_t)E);
     zero(h->d_expire, sizeof(int64_t) * (size_t)E);
@@ -827,6 +977,8 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     // AddPeer for every connection (score.go:595-609): tracked + connected
     hipLaunchKernelGGL(k_fill_u8, dim3(grid_for(E)), dim3(256), 0, s, h->d_estate, E,
                        (uint8_t)(GSIM_ES_TRACKED | GSIM_ES_CONNECTED));
+    hipLaunchKernelGGL(k_fill_u8, dim3(grid_for(E)), dim3(256), 0, s, h->d_rstate, E, (uint8_t)GSIM_ES_CONNECTED);
+    h->score_version++;
     h->has_white = false;
     h->p6_dirty = true;
     h->maybe_retained = false;
@@ -915,6 +1067,7 @@ int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now, double p_mes
     ScoreArgs a = make_score_args(h, now);
     hipLaunchKernelGGL(k_fill_synthetic, dim3(grid_for(h->e)), dim3(256), 0, h->stream, a, seed, p_mesh);
     h->p6_dirty = true;
+    h->score_version++;
     h->maybe_retained = false;
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
@@ -961,9 +1114,9 @@ int gsim_read_scores(gsim_handle* h, double* out)
     GSIM_ENTER(h);
     GSIM_NEED_GRAPH(h);
     if (!out) return GSIM_EINVAL;
-    hipError_t e = hipMemcpyAsync(out, h->d_score, sizeof(double) * (size_t)h->e, hipMemcpyDeviceToHost, h->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-    return hip_check(h, e, "gsim_read_scores");
+    FieldRef r;
+    field_ref(h, GSIM_F_SCORE, &r);
+    return read_field_impl(h, r, out);
 }
 
 int gsim_field_bytes(gsim_handle* h, int32_t f, size_t* out)
@@ -982,9 +1135,7 @@ int gsim_read_field(gsim_handle* h, int32_t f, void* dst, size_t bytes)
     FieldRef r;
     if (!field_ref(h, f, &r)) { h->err = "unknown field"; return GSIM_EINVAL; }
     if (bytes != r.bytes || !dst) { h->err = "field size mismatch"; return GSIM_EINVAL; }
-    hipError_t e = hipMemcpyAsync(dst, r.ptr, bytes, hipMemcpyDeviceToHost, h->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-    return hip_check(h, e, "gsim_read_field");
+    return read_field_impl(h, r, dst);
 }
 
 int gsim_write_field(gsim_handle* h, int32_t f, const void* src, size_t bytes)
@@ -994,10 +1145,10 @@ int gsim_write_field(gsim_handle* h, int32_t f, const void* src, size_t bytes)
     FieldRef r;
     if (!field_ref(h, f, &r)) { h->err = "unknown field"; return GSIM_EINVAL; }
     if (bytes != r.bytes || !src) { h->err = "field size mismatch"; return GSIM_EINVAL; }
-    hipError_t e = hipMemcpyAsync(r.ptr, src, bytes, hipMemcpyHostToDevice, h->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    int rc = write_field_impl(h, r, src);
     if (f == GSIM_F_ESTATE) { h->p6_dirty = true; h->maybe_retained = true; }
-    return hip_check(h, e, "gsim_write_field");
+    if (f == GSIM_F_SCORE) h->score_version++;
+    return rc;
 }
 
 int gsim_event_record(gsim_handle* h, int32_t slot)
@@ -1088,18 +1239,18 @@ bool field_ref(gsim_handle* h, int32_t f, FieldRef* r)
 {
     const size_t E = (size_t)h->e, ET = E * (size_t)std::max(1, h->t);
     switch (f) {
-    case GSIM_F_FIRST:      *r = {h->d_first, ET * 8}; return true;
-    case GSIM_F_MESHD:      *r = {h->d_meshd, ET * 8}; return true;
-    case GSIM_F_FAIL:       *r = {h->d_fail, ET * 8}; return true;
-    case GSIM_F_INVALID:    *r = {h->d_invalid, ET * 8}; return true;
-    case GSIM_F_GRAFT_TIME: *r = {h->d_graft, ET * 8}; return true;
-    case GSIM_F_MESH_TIME:  *r = {h->d_mtime, ET * 8}; return true;
-    case GSIM_F_TFLAGS:     *r = {h->d_tflags, ET}; return true;
-    case GSIM_F_BP:         *r = {h->d_bp, E * 8}; return true;
-    case GSIM_F_ESTATE:     *r = {h->d_estate, E}; return true;
-    case GSIM_F_EXPIRE:     *r = {h->d_expire, E * 8}; return true;
-    case GSIM_F_P6:         *r = {h->d_p6, E * 8}; return true;
-    case GSIM_F_SCORE:      *r = {h->d_score, E * 8}; return true;
+    case GSIM_F_FIRST:      *r = {h->d_first, ET * 8, FK_RECORD, 8}; return true;
+    case GSIM_F_MESHD:      *r = {h->d_meshd, ET * 8, FK_RECORD, 8}; return true;
+    case GSIM_F_FAIL:       *r = {h->d_fail, ET * 8, FK_RECORD, 8}; return true;
+    case GSIM_F_INVALID:    *r = {h->d_invalid, ET * 8, FK_RECORD, 8}; return true;
+    case GSIM_F_GRAFT_TIME: *r = {h->d_graft, ET * 8, FK_RECORD, 8}; return true;
+    case GSIM_F_MESH_TIME:  *r = {h->d_mtime, ET * 8, FK_RECORD, 8}; return true;
+    case GSIM_F_TFLAGS:     *r = {h->d_tflags, ET, FK_TFLAGS, 1}; return true;
+    case GSIM_F_BP:         *r = {h->d_bp, E * 8, FK_RECORD, 8}; return true;
+    case GSIM_F_ESTATE:     *r = {h->d_estate, E, FK_ESTATE, 1}; return true;
+    case GSIM_F_EXPIRE:     *r = {h->d_expire, E * 8, FK_RECORD, 8}; return true;
+    case GSIM_F_P6:         *r = {h->d_p6, E * 8, FK_RECORD, 8}; return true;
+    case GSIM_F_SCORE:      *r = {h->d_score, E * 8, FK_RECORD, 8}; return true;
     case GSIM_F_BACKOFF:    *r = {h->d_backoff, ET * 8}; return true;
     default: return extra_field_ref(h, f, r) || deliver_field_ref(h, f, r);
     }

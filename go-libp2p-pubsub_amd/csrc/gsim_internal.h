@@ -18,11 +18,14 @@ struct ScoreArgs {
     int32_t T;
     const gsim_topic_score_params* tp;
     double dtz, bp_decay, topic_cap, w5, w6, bp_thr, w7;
-    const uint32_t* col;
+    const uint32_t* owner;     // owner[r]: the neighbour a record is about (§2)
     const double* p5;
     double *first, *meshd, *fail, *invalid;
     int64_t *graft, *mtime;
-    uint8_t* tflags;
+    uint8_t* tflags;           // score bits only (inMesh, active)
+    uint8_t* mflags;           // router mesh bits, edge order (fill/census)
+    uint8_t* rstate;           // router connected bit, edge order (fill)
+    const uint32_t* rev;
     double* bp;
     uint8_t* estate;
     int64_t* expire;
@@ -45,7 +48,7 @@ enum : uint32_t {
 
 struct ColocArgs {
     int64_t E;
-    const uint32_t *row_ptr, *col, *owner, *ip_ptr, *ip_ids;
+    const uint32_t *row_ptr, *col, *rev, *owner, *ip_ptr, *ip_ids;
     const uint8_t* ip_white;
     const uint8_t* estate;
     double* p6;
@@ -63,9 +66,19 @@ __device__ __forceinline__ ctp_t const_tp(const gsim_topic_score_params* p)
     return (ctp_t)(p);
 }
 
+// How a field's ABI (edge-order) view maps onto device memory.
+enum FieldKind : int {
+    FK_RAW = 0,      // same layout
+    FK_RECORD,       // record order: view[p][e] = dev[p][rev[e]]
+    FK_TFLAGS,       // view = score bits (record order) | router mesh bit (edge order)
+    FK_ESTATE,       // record order + router connected mirror (edge order)
+};
+
 struct FieldRef {
     void* ptr;
     size_t bytes;
+    int kind = FK_RAW;
+    int elem = 1;      // element size in bytes (FK_RECORD)
 };
 
 struct Deliver;   // message ring, seen-set and round lists (deliver.hip)
@@ -107,18 +120,28 @@ struct gsim_handle {
     uint8_t* d_ip_white = nullptr;
     double* d_p5 = nullptr;
 
-    // device: topicStats [T][E]
+    // Score state is stored in RECORD order: the record of
+    // observer i about neighbour j sits at index r = rev[e_ij], i.e. at the
+    // position of i in j's row, so a message j forwards updates its receivers'
+    // records with coalesced accesses along j's row.  rev is an involution,
+    // so the ABI's edge-order view is a gather through rev both ways.
+    // device: topicStats [T][E], record order
     double *d_first = nullptr, *d_meshd = nullptr, *d_fail = nullptr, *d_invalid = nullptr;
     int64_t *d_graft = nullptr, *d_mtime = nullptr;
-    uint8_t* d_tflags = nullptr;
+    uint8_t* d_tflags = nullptr;      // GSIM_TF_IN_MESH | GSIM_TF_ACTIVE
+    // device: router state [T][E] / [E], edge (observer) order
+    uint8_t* d_mflags = nullptr;      // GSIM_TF_MESH: gs.mesh[topic] membership
     int64_t* d_backoff = nullptr;
+    uint8_t* d_rstate = nullptr;      // GSIM_ES_CONNECTED as the router sees it
 
-    // device: peerStats [E]
+    // device: peerStats [E], record order
     double* d_bp = nullptr;
     uint8_t* d_estate = nullptr;
     int64_t* d_expire = nullptr;
     double* d_p6 = nullptr;
     double* d_score = nullptr;
+    uint8_t* d_acc = nullptr;         // score >= graylistThreshold (AcceptFrom), derived
+    uint64_t score_version = 1, acc_version = 0;
 
     // per-kernel-class device timing (gsim_profile); events are pooled
     struct ProfMark { int32_t cls; uint32_t a, b; };
@@ -138,6 +161,7 @@ bool field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r);
 int launch_ip_colocation(gsim_handle* h);
 int launch_refresh_scores(gsim_handle* h, int64_t now);
 int launch_compute_scores(gsim_handle* h);
+int refresh_accept(gsim_handle* h);   // recompute d_acc if the snapshot changed
 
 // Brackets the launches of one kernel class with pooled HIP events on the
 // engine stream while profiling is enabled (gsim_profile).

@@ -34,7 +34,9 @@ struct HbArgs {
     const uint8_t* estate;
     const double* score;
     const gsim_topic_score_params* tp;
-    uint8_t* tflags;
+    uint8_t* mflags;    // router mesh bit, edge order [T][E]
+    const uint8_t* rstate;   // router connected bit, edge order [E]
+    uint8_t* tflags;    // score bits (inMesh, active), record order [T][E]
     int64_t* backoff;
     double *meshd, *fail, *bp;
     int64_t *graft, *mtime;
@@ -91,24 +93,43 @@ __device__ bool select_smallest(const HbArgs& a, bool cand, int count, uint32_t 
     return sel;
 }
 
+// The score bits of one (observer, neighbour, topic) record, loaded on first
+// use: Graft/Prune are rare, and the record lives at rev[e] (record order,
+// DESIGN.md §2), away from the observer's row.
+struct ScoreFlags {
+    int64_t ir;          // record index t*E + rev[e]
+    uint8_t v = 0, v0 = 0;
+    bool have = false;
+    __device__ uint8_t& get(const HbArgs& a)
+    {
+        if (!have) { v = v0 = a.tflags[ir]; have = true; }
+        return v;
+    }
+    __device__ void store(const HbArgs& a) const
+    {
+        if (have && v != v0) a.tflags[ir] = v;
+    }
+};
+
 // peerScore.Graft / Prune on one edge-topic record (score.go:649-691)
-__device__ __forceinline__ void stats_graft(const HbArgs& a, bool tracked, bool scored, int64_t i, uint8_t& fl)
+__device__ __forceinline__ void stats_graft(const HbArgs& a, bool tracked, bool scored, ScoreFlags& sf)
 {
     if (!tracked || !scored) return;
+    uint8_t& fl = sf.get(a);
     fl = (uint8_t)((fl | GSIM_TF_IN_MESH) & ~GSIM_TF_ACTIVE);
-    a.graft[i] = a.now;
-    a.mtime[i] = 0;
+    a.graft[sf.ir] = a.now;
+    a.mtime[sf.ir] = 0;
 }
 
-__device__ __forceinline__ void stats_prune(const HbArgs& a, bool tracked, bool scored, double thr, int64_t i,
-                                            uint8_t& fl)
+__device__ __forceinline__ void stats_prune(const HbArgs& a, bool tracked, bool scored, double thr, ScoreFlags& sf)
 {
     if (!tracked || !scored) return;
+    uint8_t& fl = sf.get(a);
     if (fl & GSIM_TF_ACTIVE) {
-        const double md = a.meshd[i];
+        const double md = a.meshd[sf.ir];
         if (md < thr) {
             const double deficit = thr - md;
-            a.fail[i] = a.fail[i] + deficit * deficit;
+            a.fail[sf.ir] = a.fail[sf.ir] + deficit * deficit;
         }
     }
     fl &= (uint8_t)~GSIM_TF_IN_MESH;
@@ -126,11 +147,12 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
         const bool valid = lane < deg;
         const uint32_t e = b + (uint32_t)lane;
         const uint32_t col = valid ? a.col[e] : 0u;
-        const uint8_t est = valid ? a.estate[e] : 0;
+        const uint32_t rv = valid ? a.rev[e] : 0u;           // this observer's record of col
+        const uint8_t est = valid ? a.estate[rv] : 0;
         const bool tracked = est & GSIM_ES_TRACKED;
-        const bool conn = est & GSIM_ES_CONNECTED;
+        const bool conn = valid && (a.rstate[e] & GSIM_ES_CONNECTED);
         const bool outb = valid && a.outbound[e];
-        const double S = valid ? a.score[e] : 0.0;
+        const double S = valid ? a.score[rv] : 0.0;
         const uint64_t subj = valid ? a.sub[col] : 0ull;
         const uint64_t subi = a.sub[obs];
 
@@ -150,7 +172,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
 #pragma unroll
           for (int j = 0; j < kFlagChunk; ++j) {
               const int32_t t = t0 + j;
-              flc[j] = (t < a.T && valid && ((subi >> t) & 1ull)) ? a.tflags[(int64_t)t * a.E + e] : 0;
+              flc[j] = (t < a.T && valid && ((subi >> t) & 1ull)) ? a.mflags[(int64_t)t * a.E + e] : 0;
           }
           for (int j = 0; j < kFlagChunk; ++j) {
             const int32_t t = t0 + j;
@@ -160,6 +182,8 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             const bool scored = tp->scored != 0;
             const double thr = tp->mesh_message_deliveries_threshold;
             const int64_t i = (int64_t)t * a.E + e;
+            ScoreFlags sf;
+            sf.ir = (int64_t)t * a.E + rv;
             uint8_t fl = flc[j];
             const uint8_t fl0 = fl;
             // backoff is only consulted when a graft selection or a prune
@@ -178,7 +202,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             const uint32_t pos = (uint32_t)lane;
 
             auto prune = [&]() {
-                stats_prune(a, tracked, scored, thr, i, fl);
+                stats_prune(a, tracked, scored, thr, sf);
                 fl &= (uint8_t)~GSIM_TF_MESH;
                 m = false;
                 need_bo();
@@ -187,7 +211,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
                 ctl |= GSIM_CTL_PRUNE;
             };
             auto graft = [&]() {
-                stats_graft(a, tracked, scored, i, fl);
+                stats_graft(a, tracked, scored, sf);
                 fl |= GSIM_TF_MESH;
                 m = true;
                 ctl |= GSIM_CTL_GRAFT;
@@ -282,7 +306,8 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             }
 
             if (valid) {
-                if (fl != fl0) a.tflags[i] = fl;
+                if (fl != fl0) a.mflags[i] = fl;
+                sf.store(a);
                 if (bo_dirty) a.backoff[i] = bo;
                 if (ctl) {
                     const int64_t r = (int64_t)t * a.E + a.rev[e];
@@ -327,15 +352,18 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
             const ctp_t tp = const_tp(a.tp) + t;
             const bool scored = tp->scored != 0;
             const double thr = tp->mesh_message_deliveries_threshold;
-            uint8_t fl = valid ? a.tflags[i] : 0;
+            uint8_t fl = valid ? a.mflags[i] : 0;
             int mesh = __popcll(ballot(valid && (fl & GSIM_TF_MESH)));
             while (pending) {
                 const int q = __ffsll((long long)pending) - 1;
                 pending &= pending - 1;
                 int delta = 0;
                 if (lane == q) {
-                    const uint8_t est = a.estate[e];
+                    const uint32_t rv = a.rev[e];                // receiver's record of the sender
+                    const uint8_t est = a.estate[rv];
                     const bool tracked = est & GSIM_ES_TRACKED;
+                    ScoreFlags sf;
+                    sf.ir = (int64_t)t * a.E + rv;
                     int64_t bo = a.backoff[i];
                     const int64_t bo0 = bo;
                     uint8_t reply = 0;
@@ -343,14 +371,14 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                         if (bo != 0 && a.now < bo) {
                             // GRAFT while backing off: P7 penalty (+1 more under the flood cutoff)
                             if (tracked) {
-                                double x = a.bp[e] + 1.0;
+                                double x = a.bp[rv] + 1.0;
                                 if (a.now < bo + (a.graft_flood - a.prune_backoff)) x = x + 1.0;
-                                a.bp[e] = x;
+                                a.bp[rv] = x;
                             }
                             const int64_t ex = a.now + a.prune_backoff;
                             if (bo < ex) bo = ex;
                             reply = GSIM_CTL_PRUNE;
-                        } else if (a.score[e] < 0) {
+                        } else if (a.score[rv] < 0) {
                             reply = GSIM_CTL_PRUNE;
                             const int64_t ex = a.now + a.prune_backoff;
                             if (bo < ex) bo = ex;
@@ -359,20 +387,21 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                             const int64_t ex = a.now + a.prune_backoff;
                             if (bo < ex) bo = ex;
                         } else {
-                            stats_graft(a, tracked, scored, i, fl);
+                            stats_graft(a, tracked, scored, sf);
                             fl |= GSIM_TF_MESH;
                             delta += 1;
                         }
                     }
                     if (c & GSIM_CTL_PRUNE) {
                         if (fl & GSIM_TF_MESH) delta -= 1;
-                        stats_prune(a, tracked, scored, thr, i, fl);
+                        stats_prune(a, tracked, scored, thr, sf);
                         fl &= (uint8_t)~GSIM_TF_MESH;
                         const int64_t secs = a.prune_backoff / kSecond;
                         const int64_t ex = a.now + (secs > 0 ? secs * kSecond : a.prune_backoff);
                         if (bo < ex) bo = ex;
                     }
-                    a.tflags[i] = fl;
+                    a.mflags[i] = fl;
+                    sf.store(a);
                     if (bo != bo0) a.backoff[i] = bo;
                     if (reply) {
                         const int64_t r = (int64_t)t * a.E + a.rev[e];
@@ -433,7 +462,7 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.N = h->n; a.E = h->e; a.T = h->t;
     a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.rev = h->d_rev; a.sub = h->d_sub;
     a.outbound = h->d_outbound; a.estate = h->d_estate; a.score = h->d_score; a.tp = h->d_tp;
-    a.tflags = h->d_tflags; a.backoff = h->d_backoff; a.meshd = h->d_meshd; a.fail = h->d_fail; a.bp = h->d_bp;
+    a.tflags = h->d_tflags; a.mflags = h->d_mflags; a.rstate = h->d_rstate; a.backoff = h->d_backoff; a.meshd = h->d_meshd; a.fail = h->d_fail; a.bp = h->d_bp;
     a.graft = h->d_graft; a.mtime = h->d_mtime;
     const size_t TE = (size_t)h->e * (size_t)std::max(1, h->t);
     a.ctl_in = h->x->d_ctl + (size_t)(parity_in & 1) * TE;

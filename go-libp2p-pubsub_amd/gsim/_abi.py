@@ -101,8 +101,8 @@ MSG_DTYPE = [("id", "<u8"), ("topic", "<u4"), ("origin", "<u4"), ("invalid", "u1
 
 UNSEEN = 0xFFFFFFFF
 
-KERNEL_CLASSES = ["refresh_score", "score", "ip_colocation", "heartbeat", "control", "publish", "claim",
-                  "resolve", "forward"]
+KERNEL_CLASSES = ["refresh_score", "score", "ip_colocation", "heartbeat", "control", "publish", "send",
+                  "commit", "accept"]
 
 SIGNATURES = [
     ("gsim_default_gossipsub_params", None, [POINTER(CGossipSubParams)]),

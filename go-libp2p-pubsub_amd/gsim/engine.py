@@ -221,10 +221,9 @@ class Engine:
         c = _abi.CMsgConfig()
         c.ring, c.rounds, c.t0_ns = int(ring), int(rounds), int(t0)
         c.heartbeat_ns = int(heartbeat if heartbeat is not None else self.gossip.HeartbeatInterval)
-        # defaults are the exact upper bounds: each (peer, slot) is first seen
-        # once per round at most, and forwards over at most its row
-        c.max_frontier = int(max_frontier if max_frontier is not None else min(ring * self.net.n, 2**31 - 1))
-        c.max_arrivals = int(max_arrivals if max_arrivals is not None else min(ring * self.net.e, 2**31 - 1))
+        # reserved fields of the ABI (the engine keeps no per-copy lists)
+        c.max_frontier = int(max_frontier or 0)
+        c.max_arrivals = int(max_arrivals or 0)
         self._check(self.lib.gsim_msgs_init(self.h, ctypes.byref(c)))
         self._msg_cfg = c
 

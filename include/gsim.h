@@ -232,16 +232,16 @@ int gsim_handle_control(gsim_handle* h, int32_t round, int64_t now_ns);
  *   T(g) = t0 + (g / rounds) * heartbeat + (g % rounds + 1) * heartbeat / (rounds + 1).
  * The seen-set is a ring of `ring` message slots x N peers (u32 first-seen
  * round, 0xFFFFFFFF = unseen): the timecache (timecache/first_seen_cache.go)
- * restricted to messages that can still arrive.  A slot may be reused once
- * its message can no longer be forwarded or gossiped; SeenMsgTTL must
- * outlast that (it does for every reference configuration). */
+ * restricted to messages that can still arrive.  Publishing into a slot ends
+ * the propagation of its previous message; SeenMsgTTL and the ring must
+ * outlast a message's propagation (they do for every reference configuration). */
 typedef struct gsim_msg_config {
-    int32_t ring;            /* message slots (live-message window) */
+    int32_t ring;            /* message slots (live-message window), 1..8192 */
     int32_t rounds;          /* propagation rounds per heartbeat, >= 2 */
     int64_t t0_ns;           /* virtual time of tick 0 */
     int64_t heartbeat_ns;    /* heartbeat interval (GossipSubParams.HeartbeatInterval) */
-    int64_t max_frontier;    /* capacity: first receptions per round */
-    int64_t max_arrivals;    /* capacity: forwarded message copies per round */
+    int64_t max_frontier;    /* reserved (ignored): the engine keeps no per-copy lists */
+    int64_t max_arrivals;    /* reserved (ignored) */
 } gsim_msg_config;
 
 /* One published message (Topic.Publish, topic.go:217-283, at its origin). */
@@ -253,26 +253,26 @@ typedef struct gsim_msg {
     uint8_t  _pad[7];
 } gsim_msg;
 
-/* Allocate the message ring, seen-set and round buffers (after load_graph). */
+/* Allocate the message ring and seen-set (after load_graph). */
 int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg);
 /* Publish `count` messages in round g: each slot is reset, the origin marks
  * the message seen (markSeen, pubsub.go:987-995) and puts it in its mcache
- * (gossipsub.go:976); the origin forwards it in round g. */
+ * (gossipsub.go:976); the origin forwards it in round g+1. */
 int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t round);
 /* Propagation round g for the whole network:
- *  1. every receiver handles the copies forwarded to it in round g-1, in
- *     (message, receiving connection) order: AcceptFrom graylist
+ *  1. every peer that saw a message for the first time in round g-1 (or
+ *     published it then) forwards it to its current mesh except the sender
+ *     and the origin (gossipsub.go:975-1045; receivers do not forward an
+ *     invalid message);
+ *  2. every receiver handles those copies: AcceptFrom graylist
  *     (gossipsub.go:598-609), seen-set check (pubsub.go:1118-1162), then
  *     DeliverMessage / DuplicateMessage / RejectMessage (score.go:693-827);
  *     of several same-round copies the lowest connection is the first;
- *  2. control inbox of round g % rounds (rounds 0 and 1 of a heartbeat);
- *  3. every peer that saw a message for the first time in round g forwards
- *     it to its mesh except the sender and the origin (gossipsub.go:975-1045). */
+ *  3. control inbox of round g % rounds (rounds 0 and 1 of a heartbeat). */
 int gsim_round(gsim_handle* h, int64_t round);
 /* Cumulative totals since gsim_msgs_init: out4 = {msg-edge deliveries
  * (accepted arrivals, duplicates included), first deliveries, duplicates,
- * graylisted arrivals}.  Synchronizes.  GSIM_ERANGE when a round overflowed
- * max_frontier or max_arrivals (results are then incomplete). */
+ * graylisted arrivals}.  Synchronizes. */
 int gsim_msg_stats(gsim_handle* h, int64_t* out4);
 
 /* Aggregate census of the state (the network-wide analogue of the
@@ -337,9 +337,9 @@ typedef enum gsim_kernel_class {
     GSIM_K_HEARTBEAT,          /* mesh maintenance */
     GSIM_K_CONTROL,            /* GRAFT/PRUNE handling */
     GSIM_K_PUBLISH,            /* slot reset + origin self-delivery */
-    GSIM_K_CLAIM,              /* seen-set claims */
-    GSIM_K_RESOLVE,            /* first/duplicate/invalid classification + counters */
-    GSIM_K_FORWARD,            /* seen commit + mesh forwarding */
+    GSIM_K_SEND,               /* mesh forwarding: AcceptFrom, seen-set claims, duplicate/invalid counters */
+    GSIM_K_COMMIT,             /* seen commit + first-delivery credit */
+    GSIM_K_ACCEPT,             /* AcceptFrom verdicts from a new score snapshot */
     GSIM_K__COUNT
 } gsim_kernel_class;
 /* Enable (1) or disable (0) recording; clears recorded totals. */

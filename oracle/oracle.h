@@ -77,16 +77,17 @@ typedef struct orc_msgs {
 
 int64_t orc_round_time(const orc_msgs* m, int64_t g);
 /* Topic.Publish at the origin (pubsub.go:1196-1202 via pushMsg): slot =
- * id % ring is reset, the origin marks it seen at round g and joins the
- * forwarding frontier of round g. */
+ * id % ring is reset, the origin marks it seen at round g and forwards it in
+ * round g+1. */
 void orc_publish(orc_net* s, orc_msgs* m, uint64_t id, uint32_t topic, uint32_t origin, uint8_t invalid,
                  int64_t g);
-/* One propagation round g: receivers process the arrivals forwarded in round
- * g-1 (AcceptFrom graylist gossipsub.go:598-609; pushMsg pubsub.go:1118-1162:
- * seen-set check, DeliverMessage/DuplicateMessage/RejectMessage score.go
- * 702-827), then handle the control inbox of round (g % R), then every
- * first-receiver forwards to its mesh peers except the sender and the origin
- * (Publish, gossipsub.go:975-1045). */
+/* One propagation round g: every peer that first saw (or published) a
+ * message in round g-1 forwards it to its current mesh peers except the
+ * sender and the origin (Publish, gossipsub.go:975-1045); receivers process
+ * those copies (AcceptFrom graylist gossipsub.go:598-609; pushMsg
+ * pubsub.go:1118-1162: seen-set check, DeliverMessage/DuplicateMessage/
+ * RejectMessage score.go 702-827); then the control inbox of round (g % R)
+ * is handled.  A message whose slot was reused is no longer forwarded. */
 void orc_round(orc_net* s, orc_msgs* m, int64_t g);
 void orc_msgs_free_priv(orc_msgs* m);
 

@@ -2,12 +2,16 @@
  * oracle_deliver.c — network-level restatement of message propagation.
  * TEST INFRASTRUCTURE (see oracle.h).
  *
- * Per round every receiver handles what its mesh peers forwarded in the
- * previous round, in (receiver, message, receiving-edge) order — the lowest
- * receiving edge of a round is the first delivery — exactly
- * as pushMsg would for those RPCs (pubsub.go:1118-1162), then the control
- * inbox is handled, then every peer that saw a message for the first time
- * forwards it to its mesh (Publish, gossipsub.go:975-1045).
+ * Round g:
+ *  1. every peer that saw a message for the first time in round g-1 (or
+ *     published it in round g-1) forwards it to its current mesh except the
+ *     sender and the origin (Publish, gossipsub.go:975-1045); a message whose
+ *     ring slot was reused since is no longer forwarded;
+ *  2. every receiver handles those copies in (receiver, message,
+ *     receiving-edge) order — the lowest receiving edge of a round is the
+ *     first delivery — exactly as pushMsg would for those RPCs
+ *     (pubsub.go:1118-1162);
+ *  3. the control inbox of the round is handled.
  */
 #include "oracle.h"
 
@@ -21,7 +25,8 @@ typedef struct arr_ent { uint32_t recv, slot, er; } arr_ent;
 
 typedef struct priv {
     fr_ent* fr; int64_t nfr, capfr;     /* peers that first-saw a message this round */
-    arr_ent* ar; int64_t nar, capar;    /* forwarded this round, handled next round */
+    fr_ent* fp; int64_t nfp, capfp;     /* ... in the previous round: they forward now */
+    arr_ent* ar; int64_t nar, capar;    /* copies forwarded this round */
 } priv;
 
 static priv* P(orc_msgs* m)
@@ -35,6 +40,7 @@ void orc_msgs_free_priv(orc_msgs* m)
     if (!m->priv) return;
     priv* p = (priv*)m->priv;
     free(p->fr);
+    free(p->fp);
     free(p->ar);
     free(p);
     m->priv = NULL;
@@ -98,7 +104,23 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
     const int64_t now = orc_round_time(m, g);
     const double gray = s->th->graylist_threshold;
 
-    /* 1. receivers handle last round's forwards, in canonical order */
+    /* 1. last round's first receivers (and publishers) forward to their mesh */
+    for (int64_t q = 0; q < p->nfp; ++q) {
+        const uint32_t j = p->fp[q].peer, slot = p->fp[q].slot, from = p->fp[q].from;
+        if (m->seen[(int64_t)slot * s->n + j] != (uint32_t)(g - 1)) continue;   /* slot reused */
+        const int32_t t = (int32_t)m->topic[slot];
+        const uint32_t origin = m->origin[slot];
+        for (uint32_t e = s->row_ptr[j]; e < s->row_ptr[j + 1]; ++e) {
+            const uint32_t i = s->col[e];
+            if (!(s->tflags[(int64_t)t * s->e + e] & GSIM_TF_MESH)) continue;
+            if (!(s->estate[e] & GSIM_ES_CONNECTED)) continue;
+            if (i == from || i == origin) continue;
+            ar_push(p, i, slot, s->rev[e]);
+        }
+    }
+    p->nfp = 0;
+
+    /* 2. receivers handle the copies, in canonical order */
     arr_ent* ar = p->ar;
     const int64_t nar = p->nar;
     p->ar = NULL; p->nar = 0; p->capar = 0;
@@ -119,7 +141,7 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
                 /* ValidateMessage + RejectMessage(ValidationFailed), score.go:728-793 */
                 orc_mark_invalid(s, er, t);
             } else {
-                /* DeliverMessage, score.go:702-726; mcache.Put; forward next */
+                /* DeliverMessage, score.go:702-726; mcache.Put; forward next round */
                 orc_mark_first(s, er, t);
                 m->lastput[(int64_t)t * s->n + i] = (int32_t)(g / m->rounds);
                 fr_push(p, i, slot, s->col[er]);
@@ -132,21 +154,11 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
     }
     free(ar);
 
-    /* 2. control records of this round */
+    /* 3. control records of this round */
     orc_handle_control(s, (int32_t)(g % m->rounds), now);
 
-    /* 3. first receivers (and this round's publishers) forward to their mesh */
-    for (int64_t q = 0; q < p->nfr; ++q) {
-        const uint32_t j = p->fr[q].peer, slot = p->fr[q].slot, from = p->fr[q].from;
-        const int32_t t = (int32_t)m->topic[slot];
-        const uint32_t origin = m->origin[slot];
-        for (uint32_t e = s->row_ptr[j]; e < s->row_ptr[j + 1]; ++e) {
-            const uint32_t i = s->col[e];
-            if (!(s->tflags[(int64_t)t * s->e + e] & GSIM_TF_MESH)) continue;
-            if (!(s->estate[e] & GSIM_ES_CONNECTED)) continue;
-            if (i == from || i == origin) continue;
-            ar_push(p, i, slot, s->rev[e]);
-        }
-    }
-    p->nfr = 0;
+    /* this round's first receivers forward in the next one */
+    fr_ent* tmp = p->fp; const int64_t cap = p->capfp;
+    p->fp = p->fr; p->nfp = p->nfr; p->capfp = p->capfr;
+    p->fr = tmp; p->nfr = 0; p->capfr = cap;
 }

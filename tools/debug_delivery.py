@@ -16,7 +16,11 @@ from gsim.params import GossipSubParams, PeerScoreThresholds, Second  # noqa: E4
 from test_delivery import HB, R, T0, _schedule  # noqa: E402
 from test_heartbeat import SEED, tick_time  # noqa: E402
 
-n, k, T, ticks, rate, inv_frac, retained, ring = 1500, 16, 2, [1, 2, 3, 4], 6, 0.1, 0.0, 64
+CASES = {
+    "a": (1500, 16, 2, [1, 2, 3, 4], 6, 0.1, 0.0, 64),
+    "b": (3000, 32, 3, [14, 15, 16], 12, 0.05, 0.03, 64),
+}
+n, k, T, ticks, rate, inv_frac, retained, ring = CASES[sys.argv[1] if len(sys.argv) > 1 else "a"]
 rng = np.random.default_rng(n + k)
 params = beacon_params(T)
 params.Topics["topic01"] = beacon_topic(MeshMessageDeliveriesWindow=150 * 10**6)
@@ -93,7 +97,7 @@ for kk in ticks:
             msgs.publish(st, mid, t, o, inv, g)
         if g in sched:
             eng.publish(sched[g], g)
-            print("publish", g, sched[g])
+            pass
         msgs.round(st, g)
         eng.round(g)
         if cmp(f"round {g}"):
