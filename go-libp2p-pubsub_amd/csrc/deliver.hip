@@ -9,30 +9,37 @@
 //   Publish forwarding to mesh     gossipsub.go:975-1045
 //
 // Bulk-synchronous restatement.  The seen-set is the only
-// message state: seen[slot][peer] = first-seen round, so the forwarding
-// frontier of round g-1 is {j : seen[m][j] == g-1} and no per-copy list is
-// ever materialized.  Round g:
-//   k_send    one wave per 64 consecutive senders, for every slot active in
-//             round g-1 (a coalesced load of seen[m][j0..j0+63] per slot):
-//             each frontier sender walks its row with a lane group, and for
-//             every mesh target evaluates AcceptFrom, loads the receiver's
-//             seen cell and applies the score tracer to the RECEIVER's record
-//             of the sender, which in record order sits at the
-//             sender's own edge index: the counter traffic is coalesced along
-//             the sender's row.  A copy to a cell already committed is a
-//             duplicate (validated = its first-seen round); a copy to an
-//             uncommitted cell claims it with an atomicMin of
-//             (0x80000000 | edge): the lowest edge, i.e. the lowest sender,
-//             wins.  Every same-round copy, first or duplicate, has
-//             validated = now and therefore the same counter update; only
-//             firstMessageDeliveries needs the winner.
-//   k_commit  one wave per 64 consecutive receivers, for the same slots: a
-//             claimed cell commits seen = g and from = the winner, and the
-//             winner's record gets markFirstMessageDelivery's P2 credit.
-//   control   rounds 0 and 1 of each heartbeat (GRAFT/PRUNE inbox).
-// Counter updates are plain read-modify-writes: in k_send a record (receiver
-// i, sender j) is only touched by the lanes that walk j's row, always the
-// same lanes of the same wave; in k_commit only by receiver i's lane.
+// message state: one 64-bit cell per (slot, peer),
+//   committed   hi = first-seen round,                lo = sender of the first copy
+//   claimed     hi = 0x80000000 | parity << 30 | edge, lo = sender | credit flags
+//   unseen      all ones
+// so the forwarding frontier of round g-1 is every cell whose first-seen
+// round is g-1 (committed, or claimed in round g-1) and no per-copy list is
+// ever materialized.  One kernel per round:
+//   k_send  one wave per 64 consecutive peers, for every slot that had new
+//           claims in round g-1 (a coalesced load of the wave's cells):
+//           (1) commit: a cell claimed in round g-1 becomes committed and its
+//               winner's record gets markFirstMessageDelivery's P2 credit;
+//           (2) forward: each frontier sender walks its row with a lane group
+//               and, for every mesh target, evaluates AcceptFrom, loads the
+//               receiver's cell and applies the score tracer to the
+//               RECEIVER's record of the sender — in record order (DESIGN.md
+//               §2) that record sits at the sender's own edge index, so the
+//               counter traffic is coalesced along the sender's row.  A copy
+//               to a cell first seen in an earlier round is a duplicate
+//               (validated = that round); a copy to an unseen cell or one
+//               claimed this round claims it with a 64-bit atomicMin: the
+//               lowest edge — the lowest sender — wins.  Every same-round
+//               copy, first or duplicate, has validated = now and so the same
+//               counter update; only the P2 credit needs the winner, and it
+//               is applied when the claim is committed.
+//   k_commit commits the claims of the last round before anything else reads
+//           the state (end of a tick, field reads), and k_reset_slots those of
+//           a slot being reused.
+// Counter updates are plain read-modify-writes: meshMessageDeliveries and
+// invalidMessageDeliveries of a record (receiver i, sender j) are only
+// touched by the lanes walking j's row, always the same lanes of the same
+// wave; firstMessageDeliveries only by the lane owning receiver i.
 #include <algorithm>
 #include <vector>
 
@@ -40,29 +47,36 @@
 
 namespace gsim {
 
-constexpr uint32_t kUnseen = 0xFFFFFFFFu;
+constexpr uint64_t kUnseen64 = ~0ull;
 constexpr uint32_t kClaim = 0x80000000u;
-constexpr int kMaxRing = 8192;     // active-slot list lives in LDS (u16)
+constexpr uint32_t kEdgeMask = 0x3FFFFFFFu;       // claim edge bits (E < 2^30 - 1)
+constexpr uint32_t kCreditFirst = 0x80000000u;     // lo-word flag: winner's record gets P2
+constexpr uint32_t kCreditMesh = 0x40000000u;      // lo-word flag: ... and P3 (negative window)
+constexpr uint32_t kPeerMask = 0x3FFFFFFFu;
+constexpr int kMaxRing = 8192;     // active-slot list lives in LDS (u16, sized by the ring)
+constexpr int kSlotBatch = 8;      // active slots whose cells are loaded together
 
 struct Deliver {
     gsim_msg_config cfg{};
     uint32_t *d_mtopic = nullptr, *d_morigin = nullptr;
     uint8_t* d_minv = nullptr;
-    uint32_t* d_seen = nullptr;        // [ring][N] first-seen round
-    uint32_t* d_from = nullptr;        // [ring][N] sender of the first copy
+    uint64_t* d_cell = nullptr;        // [ring][N] seen-set cells (layout above)
     int32_t* d_lastput = nullptr;      // [T][N]
-    uint32_t* d_nfirst = nullptr;      // [2][ring] first receptions per slot, by round parity
+    uint32_t* d_nnew = nullptr;        // [2][ring/32] bitmask: slots with new claims (or a publication), by round parity
     unsigned long long* d_stats = nullptr;   // [4]
+    uint32_t* d_seen32 = nullptr;      // scratch for the F_SEEN view
     gsim_msg* d_pub = nullptr;
     int32_t pub_cap = 0;
     int64_t next_round = -1;           // -1: any
+    int64_t pending = -1;              // round whose claims are not committed yet
+    bool lazy = true;                  // every window >= 0: commits may trail a round
 };
 
 struct RoundArgs {
     int64_t N, E;
     int32_t T, ring, R;
     int64_t t0, hb, g, now;
-    const uint32_t *row_ptr, *col, *owner;
+    const uint32_t *row_ptr, *col;
     const uint8_t* rstate;     // router connected bit, edge order
     const uint8_t* mflags;     // router mesh bits, edge order
     const uint8_t* acc;        // AcceptFrom verdicts, record order
@@ -72,10 +86,10 @@ struct RoundArgs {
     double *first, *meshd, *invalid;
     uint32_t *mtopic, *morigin;
     uint8_t* minv;
-    uint32_t *seen, *from;
+    uint64_t* cell;
     int32_t* lastput;
-    const uint32_t* nfirst_prev;   // slots with a frontier in round g-1
-    uint32_t* nfirst_cur;          // first receptions of round g
+    const uint32_t* nnew_prev;     // bitmask: slots with new claims (or a publication) in round g-1
+    uint32_t* nnew_cur;            // bitmask: slots with new claims in round g
     unsigned long long* stats;
 };
 
@@ -84,30 +98,39 @@ __device__ __forceinline__ int64_t round_time(const RoundArgs& a, int64_t g)
     return a.t0 + (g / a.R) * a.hb + (g % a.R + 1) * a.hb / (a.R + 1);
 }
 
-// x -> min(x + 1, cap) (markFirst / markDuplicate, score.go:919-981)
-__device__ __forceinline__ void inc_capped(double* p, double cap)
-{
-    double x = *p + 1.0;
-    if (x > cap) x = cap;
-    *p = x;
-}
-
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
 
-// Ordered list of the slots that had first receptions (or a publication) in
-// round g-1, built by wave 0 into LDS; every thread of the block must call it.
-__device__ __forceinline__ int active_slots(const RoundArgs& a, uint16_t* s_act, int* s_n)
+// x -> min(x + 1, cap) on a counter other lanes may update concurrently
+// (only the negative-window P3 credit of a first delivery needs it).
+__device__ __forceinline__ void atomic_inc_capped(double* p, double cap)
+{
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    unsigned long long old = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+        double x = __longlong_as_double((long long)old) + 1.0;
+        if (x > cap) x = cap;
+        const unsigned long long nw = (unsigned long long)__double_as_longlong(x);
+        if (nw == old) return;
+        const unsigned long long prev = atomicCAS(q, old, nw);
+        if (prev == old) return;
+        old = prev;
+    }
+}
+
+// Ordered list of the active slots (bit set in nnew), built by wave 0 into
+// LDS; every thread of the block must call it.
+__device__ __forceinline__ int active_slots(const uint32_t* nnew, int ring, uint16_t* s_act, int* s_n)
 {
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         int n = 0;
-        for (int m0 = 0; m0 < a.ring; m0 += 64) {
+        for (int m0 = 0; m0 < ring; m0 += 64) {
             const int m = m0 + lane;
-            const bool act = m < a.ring && a.nfirst_prev[m] != 0;
+            const bool act = m < ring && ((nnew[m >> 5] >> (m & 31)) & 1u);
             const uint64_t b = __ballot(act);
             if (act) s_act[n + __popcll(b & ((1ull << lane) - 1))] = (uint16_t)m;
             n += __popcll(b);
@@ -118,156 +141,274 @@ __device__ __forceinline__ int active_slots(const RoundArgs& a, uint16_t* s_act,
     return *s_n;
 }
 
-__global__ void k_reset_slots(uint32_t* seen, int64_t N, int32_t ring, const gsim_msg* pub, int32_t count)
+// Commit one claimed cell of round gc (markSeen + the winner's P2/P3 credit,
+// markFirstMessageDelivery score.go:919-946; mcache.Put for lastput).
+template <bool ATOMIC = false>
+__device__ __forceinline__ void commit_claim(const RoundArgs& a, uint64_t* cellp, uint64_t c, int64_t gc,
+                                             uint32_t m, int64_t peer)
 {
-    const int m = blockIdx.y;
-    if (m >= count) return;
-    uint32_t* row = seen + (int64_t)(pub[m].id % (uint64_t)ring) * N;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x)
-        row[i] = kUnseen;
+    const uint32_t hi = (uint32_t)(c >> 32), lo = (uint32_t)c;
+    *cellp = ((uint64_t)(uint32_t)gc << 32) | (lo & kPeerMask);
+    if (a.minv[m]) return;                                // RejectMessage: counted when sent
+    const int32_t t = (int32_t)a.mtopic[m];
+    int32_t* lp = a.lastput + (int64_t)t * a.N + peer;
+    const int32_t tick = (int32_t)(gc / a.R);
+    if (ATOMIC) atomicMax(lp, tick); else if (*lp < tick) *lp = tick;
+    if (!(lo & kCreditFirst)) return;
+    const ctp_t tp = const_tp(a.tp) + t;
+    const int64_t ir = (int64_t)t * a.E + (hi & kEdgeMask);
+    const double cap = tp->first_message_deliveries_cap;
+    if (ATOMIC) {
+        atomic_inc_capped(&a.first[ir], cap);
+    } else {
+        const double x = a.first[ir] + 1.0;
+        a.first[ir] = x > cap ? cap : x;
+    }
+    // with a negative window no same-round copy was credited; the first
+    // delivery is credited regardless of the window
+    if (lo & kCreditMesh) atomic_inc_capped(&a.meshd[ir], tp->mesh_message_deliveries_cap);
+}
+
+__device__ __forceinline__ bool is_claim_of(uint64_t c, uint32_t parity)
+{
+    const uint32_t hi = (uint32_t)(c >> 32);
+    return c != kUnseen64 && (hi & kClaim) && ((hi >> 30) & 1u) == parity;
+}
+
+// Reset the rows of the slots being published into; a claim still pending
+// there (its message was propagating) is committed first.
+__global__ void k_reset_slots(RoundArgs a, const gsim_msg* pub, int32_t count)
+{
+    const int k = blockIdx.y;
+    if (k >= count) return;
+    const uint32_t m = (uint32_t)(pub[k].id % (uint64_t)a.ring);
+    uint64_t* row = a.cell + (int64_t)m * a.N;
+    const uint32_t q = (uint32_t)((a.g - 1) & 1);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.N; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = row[i];
+        // several reused rows may credit one record: atomic updates here
+        if (a.g > 0 && is_claim_of(c, q)) commit_claim<true>(a, row + i, c, a.g - 1, m, i);
+        row[i] = kUnseen64;
+    }
 }
 
 __global__ void k_publish(RoundArgs a, const gsim_msg* pub, int32_t count)
 {
-    const int m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= count) return;
-    const gsim_msg p = pub[m];
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= count) return;
+    const gsim_msg p = pub[k];
     const uint32_t slot = (uint32_t)(p.id % (uint64_t)a.ring);
     a.mtopic[slot] = p.topic;
     a.morigin[slot] = p.origin;
     a.minv[slot] = p.invalid;
-    a.seen[(int64_t)slot * a.N + p.origin] = (uint32_t)a.g;
-    a.from[(int64_t)slot * a.N + p.origin] = p.origin;
-    a.lastput[(int64_t)p.topic * a.N + p.origin] = (int32_t)(a.g / a.R);
-    a.nfirst_cur[slot] = 1;   // the origin forwards in round g+1
+    a.cell[(int64_t)slot * a.N + p.origin] = ((uint64_t)(uint32_t)a.g << 32) | p.origin;
+    int32_t* lp = a.lastput + (int64_t)p.topic * a.N + p.origin;
+    const int32_t tick = (int32_t)(a.g / a.R);
+    if (*lp < tick) *lp = tick;
+    atomicOr(&a.nnew_cur[slot >> 5], 1u << (slot & 31));   // the origin forwards in round g+1
 }
 
-// Round g, step 1: every frontier sender of round g-1 forwards to its mesh.
-// W = lanes per row (power of two >= the longest row); group q of a wave
-// always walks the senders j0 + q*W .. j0 + q*W + W-1.
+// Round g.  W = lanes per row (power of two >= the longest row); group q of
+// a wave always walks the senders j0 + q*W .. j0 + q*W + W-1, two at a time
+// (their loads interleaved: two dependent memory trips per pair of rows).
 template <int W>
 __global__ __launch_bounds__(256) void k_send(RoundArgs a)
 {
-    __shared__ uint16_t s_act[kMaxRing];
+    extern __shared__ uint16_t s_act[];   // [ring] active slots, then [ring/32] new-claim bits
     __shared__ int s_n;
-    const int nact = a.g > 0 ? active_slots(a, s_act, &s_n) : 0;   // round 0 has no predecessor
+    __shared__ unsigned long long s_stats[4];
+    uint32_t* s_new = reinterpret_cast<uint32_t*>(s_act + ((a.ring + 1) & ~1));
+    for (int w = threadIdx.x; w < (a.ring + 31) / 32; w += blockDim.x) s_new[w] = 0;
+    if (threadIdx.x < 4) s_stats[threadIdx.x] = 0;
+    const int nact0 = a.g > 0 ? active_slots(a.nnew_prev, a.ring, s_act, &s_n) : 0;   // round 0 has no predecessor
     const int lane = threadIdx.x & 63;
     const int64_t j0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
-    if (j0 >= a.N) return;
+    const int nact = j0 < a.N ? nact0 : 0;               // no early return: the block meets below
     const int64_t jl = j0 + lane;
     const bool vj = jl < a.N;
     const int grp = lane / W, gl = lane % W;
     const uint64_t gmask = (W == 64) ? ~0ull : (((1ull << W) - 1) << (grp * W));
     const ctp_t tpa = const_tp(a.tp);
     const uint32_t gprev = (uint32_t)(a.g - 1);
-    unsigned long long n_acc = 0, n_gray = 0;
-    for (int k = 0; k < nact; ++k) {
-        const uint32_t m = s_act[k];
-        const int64_t row_m = (int64_t)m * a.N;
-        const uint32_t origin = a.morigin[m];
-        const bool inv = a.minv[m] != 0;
-        const uint32_t sv = vj ? a.seen[row_m + jl] : kUnseen;
-        // receivers reject an invalid message and do not forward it; its
-        // origin publishes it regardless
-        const bool fr = sv == gprev && (!inv || (uint32_t)jl == origin);
-        const uint64_t mask = __ballot(fr);
-        if (!mask) continue;
-        const uint32_t from_l = fr ? a.from[row_m + jl] : 0u;
-        const int32_t t = (int32_t)a.mtopic[m];
-        const ctp_t tp = tpa + t;
-        const bool scored_t = tp->scored != 0;
-        const int64_t window = tp->mesh_message_deliveries_window_ns;
-        const double mcap = tp->mesh_message_deliveries_cap;
-        const int64_t plane = (int64_t)t * a.E;
-        uint64_t gm = mask & gmask;
-        while (__ballot(gm != 0)) {
-            int b = -1;
-            if (gm) { b = __ffsll((long long)gm) - 1; gm &= gm - 1; }
-            const uint32_t fromj = __shfl(from_l, b < 0 ? lane : b, 64);
-            if (b < 0) continue;
-            const uint32_t j = (uint32_t)(j0 + b);
-            const uint32_t beg = a.row_ptr[j];
-            const uint32_t deg = a.row_ptr[j + 1] - beg;
-            if ((uint32_t)gl >= deg) continue;
-            const uint32_t e = beg + (uint32_t)gl;
-            const uint32_t i = a.col[e];
-            if (!(a.mflags[plane + e] & GSIM_TF_MESH) || !(a.rstate[e] & GSIM_ES_CONNECTED) || i == fromj ||
-                i == origin)
-                continue;
-            if (!a.acc[e]) { n_gray++; continue; }     // AcceptFrom: graylisted sender
-            n_acc++;
-            uint32_t* cell = a.seen + row_m + i;
-            const uint32_t c = *cell;
-            const bool old = c < kClaim;                 // committed in an earlier round
-            if (!old) __hip_atomic_fetch_min(cell, kClaim | e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (!scored_t || !(a.estate[e] & GSIM_ES_TRACKED)) continue;
-            const int64_t ir = plane + e;
-            if (inv) {                                   // markInvalidMessageDelivery
-                a.invalid[ir] = a.invalid[ir] + 1.0;
-                continue;
+    const uint32_t par = (uint32_t)(a.g & 1), qpar = par ^ 1u;
+    const uint32_t claim_hi = kClaim | (par << 30);
+    // row bounds of the wave's senders, shuffled to the group that walks a row
+    const uint32_t rp0 = vj ? a.row_ptr[jl] : 0u;
+    const uint32_t rp1 = vj ? a.row_ptr[jl + 1] : 0u;
+    unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
+    for (int k0 = 0; k0 < nact; k0 += kSlotBatch) {
+        uint64_t cv[kSlotBatch];
+#pragma unroll
+        for (int b = 0; b < kSlotBatch; ++b) {
+            const int k = k0 + b;
+            cv[b] = (k < nact && vj) ? a.cell[(int64_t)s_act[k] * a.N + jl] : kUnseen64;
+        }
+#pragma unroll
+        for (int b = 0; b < kSlotBatch; ++b) {
+            const int k = k0 + b;
+            if (k >= nact) break;                        // wave-uniform
+            const uint32_t m = s_act[k];
+            const int64_t row_m = (int64_t)m * a.N;
+            const uint64_t c0 = cv[b];
+            const bool pend = is_claim_of(c0, qpar);     // first received in round g-1, not committed
+            // (1) commit this lane's claim of round g-1
+            if (pend) commit_claim(a, a.cell + row_m + jl, c0, a.g - 1, m, jl);
+            const uint32_t origin = a.morigin[m];
+            const bool inv = a.minv[m] != 0;
+            // receivers reject an invalid message and do not forward it; its
+            // origin publishes it regardless
+            const bool fr = (pend || (uint32_t)(c0 >> 32) == gprev) && (!inv || (uint32_t)jl == origin);
+            const uint64_t mask = __ballot(fr);
+            if (!mask) continue;
+            // (2) forward
+            const uint32_t from_l = (uint32_t)c0 & kPeerMask;
+            const int32_t t = (int32_t)a.mtopic[m];
+            const ctp_t tp = tpa + t;
+            const bool scored_t = tp->scored != 0;
+            const int64_t window = tp->mesh_message_deliveries_window_ns;
+            const double mcap = tp->mesh_message_deliveries_cap;
+            const int64_t plane = (int64_t)t * a.E;
+            const unsigned long long first_before = n_first;
+            uint64_t gm = mask & gmask;
+            while (__ballot(gm != 0)) {
+                int b1 = -1, b2 = -1;
+                if (gm) { b1 = __ffsll((long long)gm) - 1; gm &= gm - 1; }
+                if (gm) { b2 = __ffsll((long long)gm) - 1; gm &= gm - 1; }
+                const int s1 = b1 < 0 ? lane : b1, s2 = b2 < 0 ? lane : b2;
+                const uint32_t f1 = __shfl(from_l, s1, 64), f2 = __shfl(from_l, s2, 64);
+                const uint32_t beg1 = __shfl(rp0, s1, 64), end1 = __shfl(rp1, s1, 64);
+                const uint32_t beg2 = __shfl(rp0, s2, 64), end2 = __shfl(rp1, s2, 64);
+                const bool v1 = b1 >= 0 && (uint32_t)gl < end1 - beg1;
+                const bool v2 = b2 >= 0 && (uint32_t)gl < end2 - beg2;
+                const uint32_t e1 = beg1 + (uint32_t)gl, e2 = beg2 + (uint32_t)gl;
+                const uint32_t j1 = (uint32_t)(j0 + (b1 < 0 ? 0 : b1)), j2 = (uint32_t)(j0 + (b2 < 0 ? 0 : b2));
+                // trip 1: the edge's router and record state
+                uint32_t i1 = 0, i2 = 0;
+                uint8_t mf1 = 0, mf2 = 0, rs1 = 0, rs2 = 0, ac1 = 0, ac2 = 0, es1 = 0, es2 = 0, tf1 = 0, tf2 = 0;
+                if (v1) {
+                    i1 = a.col[e1]; mf1 = a.mflags[plane + e1]; rs1 = a.rstate[e1]; ac1 = a.acc[e1];
+                    es1 = a.estate[e1]; tf1 = a.tflags[plane + e1];
+                }
+                if (v2) {
+                    i2 = a.col[e2]; mf2 = a.mflags[plane + e2]; rs2 = a.rstate[e2]; ac2 = a.acc[e2];
+                    es2 = a.estate[e2]; tf2 = a.tflags[plane + e2];
+                }
+                const bool tg1 = v1 && (mf1 & GSIM_TF_MESH) && (rs1 & GSIM_ES_CONNECTED) && i1 != f1 && i1 != origin;
+                const bool tg2 = v2 && (mf2 & GSIM_TF_MESH) && (rs2 & GSIM_ES_CONNECTED) && i2 != f2 && i2 != origin;
+                n_gray += (tg1 && !ac1) + (tg2 && !ac2);     // AcceptFrom: graylisted sender
+                const bool ok1 = tg1 && ac1, ok2 = tg2 && ac2;
+                n_acc += ok1 + ok2;
+                // trip 2: the receiver's cell and the counter to update
+                const bool sc1 = ok1 && scored_t && (es1 & GSIM_ES_TRACKED);
+                const bool sc2 = ok2 && scored_t && (es2 & GSIM_ES_TRACKED);
+                uint64_t c1 = 0, c2 = 0;
+                double x1 = 0.0, x2 = 0.0;
+                if (ok1) c1 = a.cell[row_m + i1];
+                if (ok2) c2 = a.cell[row_m + i2];
+                if (sc1) x1 = inv ? a.invalid[plane + e1] : ((tf1 & GSIM_TF_IN_MESH) ? a.meshd[plane + e1] : 0.0);
+                if (sc2) x2 = inv ? a.invalid[plane + e2] : ((tf2 & GSIM_TF_IN_MESH) ? a.meshd[plane + e2] : 0.0);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const bool ok = u ? ok2 : ok1;
+                    if (!ok) continue;
+                    const uint64_t c = u ? c2 : c1;
+                    const uint32_t e = u ? e2 : e1, i = u ? i2 : i1, j = u ? j2 : j1;
+                    const bool sc = u ? sc2 : sc1;
+                    const uint8_t tf = u ? tf2 : tf1;
+                    const double x = u ? x2 : x1;
+                    const uint32_t hi = (uint32_t)(c >> 32);
+                    // first-seen round of an earlier round, or -1 for unseen /
+                    // claimed in this round
+                    int64_t seen_round = -1;
+                    if (c != kUnseen64) {
+                        if (!(hi & kClaim)) seen_round = hi;
+                        else if (((hi >> 30) & 1u) != par) seen_round = a.g - 1;
+                    }
+                    if (seen_round < 0 && (c == kUnseen64 || (hi & kEdgeMask) > e)) {
+                        // claim unless a lower edge already holds the cell
+                        uint32_t lo = j;
+                        if (sc && !inv) {
+                            lo |= kCreditFirst;
+                            if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo |= kCreditMesh;
+                        }
+                        const uint64_t v = ((uint64_t)(claim_hi | e) << 32) | lo;
+                        const uint64_t prev = __hip_atomic_fetch_min(a.cell + row_m + i, v, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT);
+                        if (prev == kUnseen64) n_first++;
+                    }
+                    if (!sc) continue;
+                    const int64_t ir = plane + e;
+                    if (inv) {
+                        a.invalid[ir] = x + 1.0;                 // markInvalidMessageDelivery
+                    } else if (tf & GSIM_TF_IN_MESH) {
+                        // markDuplicateMessageDelivery's window test; a same-round
+                        // copy (first or duplicate) has validated = now
+                        const bool in_window = seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window)
+                                                               : (window >= 0);
+                        if (in_window) a.meshd[ir] = (x + 1.0 > mcap) ? mcap : x + 1.0;
+                    }
+                }
             }
-            if (!(a.tflags[ir] & GSIM_TF_IN_MESH)) continue;
-            // markDuplicateMessageDelivery's window test; a same-round copy
-            // (first or duplicate) has validated = now
-            const bool in_window = old ? (a.now - round_time(a, (int64_t)c) <= window) : (window >= 0);
-            if (in_window) inc_capped(&a.meshd[ir], mcap);
+            // the slot stays active next round if any copy claimed a new cell
+            if (__ballot(n_first != first_before) && lane == 0) atomicOr(&s_new[m >> 5], 1u << (m & 31));
         }
     }
     n_acc = wave_sum_u64(n_acc);
     n_gray = wave_sum_u64(n_gray);
+    n_first = wave_sum_u64(n_first);
     if (lane == 0 && (n_acc | n_gray)) {
-        atomicAdd(&a.stats[0], n_acc);
-        atomicAdd(&a.stats[2], n_acc);          // k_commit moves the firsts out
-        atomicAdd(&a.stats[3], n_gray);
+        atomicAdd(&s_stats[0], n_acc);
+        atomicAdd(&s_stats[1], n_first);
+        atomicAdd(&s_stats[3], n_gray);
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < (a.ring + 31) / 32; w += blockDim.x)
+        if (s_new[w]) atomicOr(&a.nnew_cur[w], s_new[w]);
+    if (threadIdx.x == 0 && (s_stats[0] | s_stats[3])) {
+        atomicAdd(&a.stats[0], s_stats[0]);
+        atomicAdd(&a.stats[1], s_stats[1]);
+        atomicAdd(&a.stats[2], s_stats[0] - s_stats[1]);
+        atomicAdd(&a.stats[3], s_stats[3]);
     }
 }
 
-// Round g, step 2: commit every claimed cell (markSeen) and credit the
-// winner's first delivery (markFirstMessageDelivery, score.go:919-946).
+// Commit every claim of round g (markSeen + P2 credit) before the state is
+// read or changed by anything but the next round.
 __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
 {
-    __shared__ uint16_t s_act[kMaxRing];
+    extern __shared__ uint16_t s_act[];
     __shared__ int s_n;
-    const int nact = a.g > 0 ? active_slots(a, s_act, &s_n) : 0;
+    const int nact = active_slots(a.nnew_cur, a.ring, s_act, &s_n);
     const int lane = threadIdx.x & 63;
     const int64_t i0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
-    if (i0 >= a.N) return;
+    if (i0 >= a.N || nact == 0) return;
     const int64_t i = i0 + lane;
     const bool vi = i < a.N;
-    const ctp_t tpa = const_tp(a.tp);
-    const int32_t tick = (int32_t)(a.g / a.R);
-    unsigned long long n_first = 0;
-    for (int k = 0; k < nact; ++k) {
-        const uint32_t m = s_act[k];
-        const int64_t cell = (int64_t)m * a.N + i;
-        const uint32_t c = vi ? a.seen[cell] : kUnseen;
-        const bool claimed = c != kUnseen && (c & kClaim);
-        const uint64_t cm = __ballot(claimed);
-        if (!cm) continue;
-        if (lane == 0) atomicAdd(&a.nfirst_cur[m], (uint32_t)__popcll(cm));
-        if (!claimed) continue;
-        n_first++;
-        const uint32_t ew = c & ~kClaim;           // winning edge = the receiver's record of the sender
-        const int32_t t = (int32_t)a.mtopic[m];
-        const bool inv = a.minv[m] != 0;
-        a.seen[cell] = (uint32_t)a.g;
-        a.from[cell] = a.owner[ew];
-        if (inv) continue;                          // RejectMessage: counted by k_send
-        a.lastput[(int64_t)t * a.N + i] = tick;     // mcache.Put
-        const ctp_t tp = tpa + t;
-        if (!tp->scored || !(a.estate[ew] & GSIM_ES_TRACKED)) continue;
-        const int64_t ir = (int64_t)t * a.E + ew;
-        inc_capped(&a.first[ir], tp->first_message_deliveries_cap);
-        // with a negative window k_send credits no same-round copy; the first
-        // delivery is credited regardless of the window
-        if (tp->mesh_message_deliveries_window_ns < 0 && (a.tflags[ir] & GSIM_TF_IN_MESH))
-            inc_capped(&a.meshd[ir], tp->mesh_message_deliveries_cap);
+    const uint32_t par = (uint32_t)(a.g & 1);
+    for (int k0 = 0; k0 < nact; k0 += kSlotBatch) {
+        uint64_t cv[kSlotBatch];
+#pragma unroll
+        for (int b = 0; b < kSlotBatch; ++b) {
+            const int k = k0 + b;
+            cv[b] = (k < nact && vi) ? a.cell[(int64_t)s_act[k] * a.N + i] : kUnseen64;
+        }
+#pragma unroll
+        for (int b = 0; b < kSlotBatch; ++b) {
+            const int k = k0 + b;
+            if (k >= nact) break;
+            if (is_claim_of(cv[b], par)) {
+                const uint32_t m = s_act[k];
+                commit_claim(a, a.cell + (int64_t)m * a.N + i, cv[b], a.g, m, i);
+            }
+        }
     }
-    n_first = wave_sum_u64(n_first);
-    if (lane == 0 && n_first) {
-        atomicAdd(&a.stats[1], n_first);
-        atomicAdd(&a.stats[2], 0ull - n_first);   // duplicates = accepted - first
-    }
+}
+
+__global__ void k_seen_view(const uint64_t* cell, uint32_t* out, int64_t n)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += stride)
+        out[x] = (uint32_t)(cell[x] >> 32);
 }
 
 }  // namespace gsim
@@ -281,8 +422,8 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_seen); f(d->d_from); f(d->d_lastput);
-    f(d->d_nfirst); f(d->d_stats); f(d->d_pub);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_lastput);
+    f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     delete d;
 }
 
@@ -297,10 +438,12 @@ bool deliver_field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r)
 {
     Deliver* d = h->dl;
     if (!d) return false;
-    if (f == GSIM_F_SEEN) { *r = {d->d_seen, (size_t)d->cfg.ring * (size_t)h->n * 4}; return true; }
+    if (f == GSIM_F_SEEN) { *r = {d->d_cell, (size_t)d->cfg.ring * (size_t)h->n * 4, FK_SEEN, 4}; return true; }
     if (f == GSIM_F_LASTPUT) { *r = {d->d_lastput, (size_t)std::max(1, h->t) * (size_t)h->n * 4}; return true; }
     return false;
 }
+
+static int nnew_words(const Deliver* d) { return (d->cfg.ring + 31) / 32; }
 
 static RoundArgs make_round_args(gsim_handle* h, int64_t g)
 {
@@ -309,17 +452,52 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.N = h->n; a.E = h->e; a.T = h->t; a.ring = d->cfg.ring; a.R = d->cfg.rounds;
     a.t0 = d->cfg.t0_ns; a.hb = d->cfg.heartbeat_ns; a.g = g;
     a.now = a.t0 + (g / a.R) * a.hb + (g % a.R + 1) * a.hb / (a.R + 1);
-    a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.owner = h->d_owner;
+    a.row_ptr = h->d_row_ptr; a.col = h->d_col;
     a.rstate = h->d_rstate; a.mflags = h->d_mflags; a.acc = h->d_acc;
     a.estate = h->d_estate; a.tflags = h->d_tflags; a.tp = h->d_tp;
     a.first = h->d_first; a.meshd = h->d_meshd; a.invalid = h->d_invalid;
     a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv;
-    a.seen = d->d_seen; a.from = d->d_from; a.lastput = d->d_lastput;
-    const size_t ring = (size_t)d->cfg.ring;
-    a.nfirst_prev = d->d_nfirst + (size_t)((g + 1) & 1) * ring;
-    a.nfirst_cur = d->d_nfirst + (size_t)(g & 1) * ring;
+    a.cell = d->d_cell; a.lastput = d->d_lastput;
+    const size_t w = (size_t)nnew_words(d);
+    a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
+    a.nnew_cur = d->d_nnew + (size_t)(g & 1) * w;
     a.stats = d->d_stats;
     return a;
+}
+
+static int grid_peers(int64_t n)
+{
+    const int64_t waves = (n + 63) / 64;
+    return (int)std::max<int64_t>((waves + 3) / 4, 1);
+}
+
+int deliver_flush(gsim_handle* h)
+{
+    Deliver* d = h->dl;
+    if (!d || d->pending < 0) return GSIM_OK;
+    ProfScope ps(h, GSIM_K_COMMIT);
+    RoundArgs a = make_round_args(h, d->pending);
+    hipLaunchKernelGGL(k_commit, dim3(grid_peers(h->n)), dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t),
+                       h->stream, a);
+    d->pending = -1;
+    return hip_check(h, hipGetLastError(), "k_commit");
+}
+
+int deliver_read_seen(gsim_handle* h, void* dst)
+{
+    Deliver* d = h->dl;
+    int rc = deliver_flush(h);
+    if (rc) return rc;
+    const size_t n = (size_t)d->cfg.ring * (size_t)h->n;
+    hipError_t e = hipSuccess;
+    if (!d->d_seen32) e = hipMalloc((void**)&d->d_seen32, std::max<size_t>(n * 4, 4));
+    if (e != hipSuccess) return hip_check(h, e, "seen view scratch");
+    hipLaunchKernelGGL(k_seen_view, dim3(std::min<int64_t>(((int64_t)n + 255) / 256, 16384)), dim3(256), 0, h->stream,
+                       (const uint64_t*)d->d_cell, d->d_seen32, (int64_t)n);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(dst, d->d_seen32, n * 4, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    return hip_check(h, e, "gsim_read_field(SEEN)");
 }
 
 extern "C" {
@@ -333,12 +511,16 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
         h->err = "invalid message configuration (ring must be in [1, 8192], rounds >= 2, heartbeat > 0)";
         return GSIM_EINVAL;
     }
-    if (h->e >= (int64_t)kClaim) { h->err = "too many edges for the seen-set claim encoding"; return GSIM_ERANGE; }
+    if (h->e >= (int64_t)kEdgeMask || h->n >= (int64_t)kPeerMask) {
+        h->err = "too many edges or peers for the seen-set claim encoding (< 2^30 - 1)";
+        return GSIM_ERANGE;
+    }
     (void)hipStreamSynchronize(h->stream);
     free_deliver(h);
     Deliver* d = new Deliver();
     d->cfg = *cfg;
     const size_t ring = (size_t)cfg->ring, N = (size_t)h->n, T = (size_t)std::max(1, h->t);
+    const size_t words = (size_t)nnew_words(d);
     hipError_t e = hipSuccess;
     auto A = [&](void** p, size_t bytes) {
         if (e == hipSuccess) e = hipMalloc(p, std::max<size_t>(bytes, 4));
@@ -347,10 +529,9 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_mtopic, ring * 4);
     A((void**)&d->d_morigin, ring * 4);
     A((void**)&d->d_minv, ring);
-    A((void**)&d->d_seen, ring * N * 4);
-    A((void**)&d->d_from, ring * N * 4);
+    A((void**)&d->d_cell, ring * N * 8);
     A((void**)&d->d_lastput, T * N * 4);
-    A((void**)&d->d_nfirst, 2 * ring * 4);
+    A((void**)&d->d_nnew, 2 * words * 4);
     A((void**)&d->d_stats, 4 * 8);
     if (e != hipSuccess) {
         dl_free(d);
@@ -358,13 +539,12 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
         return e == hipErrorOutOfMemory ? GSIM_ENOMEM : GSIM_EDEVICE;
     }
     h->dl = d;
-    e = hipMemsetAsync(d->d_seen, 0xFF, ring * N * 4, h->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(d->d_from, 0, ring * N * 4, h->stream);
+    e = hipMemsetAsync(d->d_cell, 0xFF, ring * N * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_lastput, 0xFF, T * N * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_mtopic, 0, ring * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_morigin, 0, ring * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_minv, 0, ring, h->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(d->d_nfirst, 0, 2 * ring * 4, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_nnew, 0, 2 * words * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_stats, 0, 4 * 8, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     return hip_check(h, e, "gsim_msgs_init");
@@ -406,11 +586,11 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
     e = hipMemcpyAsync(d->d_pub, msgs, sizeof(gsim_msg) * (size_t)count, hipMemcpyHostToDevice, h->stream);
     if (e != hipSuccess) return hip_check(h, e, "publish upload");
     ProfScope ps(h, GSIM_K_PUBLISH);
+    RoundArgs a = make_round_args(h, round);
     const int64_t per_block = 256 * 16;
     const int gx = (int)std::min<int64_t>((h->n + per_block - 1) / per_block, 1024);
-    hipLaunchKernelGGL(k_reset_slots, dim3(std::max(gx, 1), count), dim3(256), 0, h->stream, d->d_seen, h->n,
-                       d->cfg.ring, (const gsim_msg*)d->d_pub, count);
-    RoundArgs a = make_round_args(h, round);
+    hipLaunchKernelGGL(k_reset_slots, dim3(std::max(gx, 1), count), dim3(256), 0, h->stream, a,
+                       (const gsim_msg*)d->d_pub, count);
     hipLaunchKernelGGL(k_publish, dim3((count + 255) / 256), dim3(256), 0, h->stream, a,
                        (const gsim_msg*)d->d_pub, count);
     d->next_round = round;
@@ -438,28 +618,35 @@ int gsim_round(gsim_handle* h, int64_t round)
         rc = refresh_accept(h);
         if (rc) return rc;
     }
+    // commits may trail their round only while every window is >= 0: with a
+    // negative window the first delivery's P3 credit must land before control
+    bool lazy = true;
+    for (const auto& tp : h->tp)
+        if (tp.scored && tp.mesh_message_deliveries_window_ns < 0) lazy = false;
     RoundArgs a = make_round_args(h, round);
-    const int64_t waves = (h->n + 63) / 64;
-    const int grid = (int)std::max<int64_t>((waves + 3) / 4, 1);
+    const size_t lds = (((size_t)d->cfg.ring + 1) & ~(size_t)1) * sizeof(uint16_t) + (size_t)nnew_words(d) * 4;
     {
         ProfScope ps(h, GSIM_K_SEND);
+        const int grid = grid_peers(h->n);
         if (h->max_degree <= 16)
-            hipLaunchKernelGGL(k_send<16>, dim3(grid), dim3(256), 0, h->stream, a);
+            hipLaunchKernelGGL(k_send<16>, dim3(grid), dim3(256), lds, h->stream, a);
         else if (h->max_degree <= 32)
-            hipLaunchKernelGGL(k_send<32>, dim3(grid), dim3(256), 0, h->stream, a);
+            hipLaunchKernelGGL(k_send<32>, dim3(grid), dim3(256), lds, h->stream, a);
         else
-            hipLaunchKernelGGL(k_send<64>, dim3(grid), dim3(256), 0, h->stream, a);
+            hipLaunchKernelGGL(k_send<64>, dim3(grid), dim3(256), lds, h->stream, a);
+        // the claims of round g-1 were committed by k_send; round g+1's bits
+        // were last read (as "previous") by round g
+        d->pending = round;
+        hipError_t e = hipMemsetAsync(d->d_nnew + (size_t)((round + 1) & 1) * (size_t)nnew_words(d), 0,
+                                      (size_t)nnew_words(d) * 4, h->stream);
+        if (e != hipSuccess) return hip_check(h, e, "nnew reset");
     }
-    {
-        ProfScope ps(h, GSIM_K_COMMIT);
-        hipLaunchKernelGGL(k_commit, dim3(grid), dim3(256), 0, h->stream, a);
-        // the counters of round g+1 were last read as "previous" by round g
-        hipError_t e = hipMemsetAsync(d->d_nfirst + (size_t)((round + 1) & 1) * (size_t)d->cfg.ring, 0,
-                                      (size_t)d->cfg.ring * 4, h->stream);
-        if (e != hipSuccess) return hip_check(h, e, "nfirst reset");
-    }
-    rc = hip_check(h, hipGetLastError(), "k_send/k_commit");
+    rc = hip_check(h, hipGetLastError(), "k_send");
     if (rc) return rc;
+    if (!lazy) {
+        rc = deliver_flush(h);
+        if (rc) return rc;
+    }
     const int32_t r = (int32_t)(round % d->cfg.rounds);
     if (r < 2) {
         // rounds >= 2 of a heartbeat have an empty control inbox: handling

@@ -641,6 +641,8 @@ static void launch_score_kernel(gsim_handle* h, const ScoreArgs& a)
 
 int launch_refresh_scores(gsim_handle* h, int64_t now)
 {
+    int rc0 = deliver_flush(h);   // the last round's first deliveries precede the decay
+    if (rc0) return rc0;
     ScoreArgs a = make_score_args(h, now);
     if (h->p6_dirty) {
         int rc = launch_ip_colocation(h);
@@ -662,6 +664,8 @@ int launch_refresh_scores(gsim_handle* h, int64_t now)
 
 int launch_compute_scores(gsim_handle* h)
 {
+    int rc0 = deliver_flush(h);
+    if (rc0) return rc0;
     if (h->p6_dirty) {
         int rc = launch_ip_colocation(h);
         if (rc) return rc;
@@ -1020,6 +1024,8 @@ int gsim_set_topic_params(gsim_handle* h, int32_t t, const gsim_topic_score_para
     if (!p || t < 0 || t >= h->t) { h->err = "topic index out of range"; return GSIM_EINVAL; }
     char buf[256] = {0};
     if (h->validate && p->scored && gsim_validate_topic_params(p, buf, sizeof buf)) { h->err = buf; return GSIM_EINVAL; }
+    int rcf = deliver_flush(h);
+    if (rcf) return rcf;
     const gsim_topic_score_params old = h->tp[t];
     h->tp[t] = *p;
     hipError_t e = hipMemcpyAsync(h->d_tp + t, p, sizeof(*p), hipMemcpyHostToDevice, h->stream);
@@ -1064,6 +1070,8 @@ int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now, double p_mes
 {
     GSIM_ENTER(h);
     GSIM_NEED_GRAPH(h);
+    int rcf = deliver_flush(h);
+    if (rcf) return rcf;
     ScoreArgs a = make_score_args(h, now);
     hipLaunchKernelGGL(k_fill_synthetic, dim3(grid_for(h->e)), dim3(256), 0, h->stream, a, seed, p_mesh);
     h->p6_dirty = true;
@@ -1094,6 +1102,8 @@ int gsim_census(gsim_handle* h, int64_t* out8)
     GSIM_ENTER(h);
     GSIM_NEED_GRAPH(h);
     if (!out8) return GSIM_EINVAL;
+    int rcf = deliver_flush(h);
+    if (rcf) return rcf;
     unsigned long long* d = nullptr;
     hipError_t e = hipMalloc((void**)&d, 8 * sizeof(unsigned long long));
     if (e != hipSuccess) return hip_check(h, e, "hipMalloc census");
@@ -1135,6 +1145,9 @@ int gsim_read_field(gsim_handle* h, int32_t f, void* dst, size_t bytes)
     FieldRef r;
     if (!field_ref(h, f, &r)) { h->err = "unknown field"; return GSIM_EINVAL; }
     if (bytes != r.bytes || !dst) { h->err = "field size mismatch"; return GSIM_EINVAL; }
+    if (r.kind == FK_SEEN) return deliver_read_seen(h, dst);
+    int rc = deliver_flush(h);
+    if (rc) return rc;
     return read_field_impl(h, r, dst);
 }
 
@@ -1145,7 +1158,10 @@ int gsim_write_field(gsim_handle* h, int32_t f, const void* src, size_t bytes)
     FieldRef r;
     if (!field_ref(h, f, &r)) { h->err = "unknown field"; return GSIM_EINVAL; }
     if (bytes != r.bytes || !src) { h->err = "field size mismatch"; return GSIM_EINVAL; }
-    int rc = write_field_impl(h, r, src);
+    if (r.kind == FK_SEEN) { h->err = "the seen-set is read-only"; return GSIM_EINVAL; }
+    int rc = deliver_flush(h);
+    if (rc) return rc;
+    rc = write_field_impl(h, r, src);
     if (f == GSIM_F_ESTATE) { h->p6_dirty = true; h->maybe_retained = true; }
     if (f == GSIM_F_SCORE) h->score_version++;
     return rc;

@@ -72,6 +72,7 @@ enum FieldKind : int {
     FK_RECORD,       // record order: view[p][e] = dev[p][rev[e]]
     FK_TFLAGS,       // view = score bits (record order) | router mesh bit (edge order)
     FK_ESTATE,       // record order + router connected mirror (edge order)
+    FK_SEEN,         // first-seen rounds: the high words of the 64-bit seen-set cells (read-only)
 };
 
 struct FieldRef {
@@ -181,3 +182,5 @@ bool extra_field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r);
 // implemented in deliver.hip
 void free_deliver(gsim_handle* h);
 bool deliver_field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r);
+int deliver_flush(gsim_handle* h);                  // commit the last round's claims (if any)
+int deliver_read_seen(gsim_handle* h, void* dst);

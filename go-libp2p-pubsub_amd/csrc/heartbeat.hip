@@ -506,6 +506,8 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     if (h->e == 0 || !h->x) { h->err = "no graph loaded"; return GSIM_ESTATE; }
     int rc = check_degree(h);
     if (rc) return rc;
+    rc = deliver_flush(h);
+    if (rc) return rc;
     // heartbeat output goes to the parity-0 inbox, read by control round 0
     HbArgs a = make_hb_args(h, tick, now, 1);
     ProfScope ps(h, GSIM_K_HEARTBEAT);
