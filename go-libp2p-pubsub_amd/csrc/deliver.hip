@@ -77,17 +77,17 @@ struct RoundArgs {
     int32_t T, ring, R;
     int64_t t0, hb, g, now;
     const uint32_t *row_ptr, *col;
-    const uint8_t* rstate;     // router connected bit, edge order
+    const uint8_t* dstate;     // GSIM_DS_* per edge index (router connected; record accept/tracked)
     const uint8_t* mflags;     // router mesh bits, edge order
-    const uint8_t* acc;        // AcceptFrom verdicts, record order
-    const uint8_t* estate;     // record order
     const uint8_t* tflags;     // score bits, record order
     const gsim_topic_score_params* tp;
     double *first, *meshd, *invalid;
+    uint8_t* mcnt;             // pending meshd increments, record order
     uint32_t *mtopic, *morigin;
     uint8_t* minv;
     uint64_t* cell;
     int32_t* lastput;
+    uint32_t diag;                 // DIAG_D_* ablations (timing experiments only)
     const uint32_t* nnew_prev;     // bitmask: slots with new claims (or a publication) in round g-1
     uint32_t* nnew_cur;            // bitmask: slots with new claims in round g
     unsigned long long* stats;
@@ -154,7 +154,7 @@ __device__ __forceinline__ void commit_claim(const RoundArgs& a, uint64_t* cellp
     int32_t* lp = a.lastput + (int64_t)t * a.N + peer;
     const int32_t tick = (int32_t)(gc / a.R);
     if (ATOMIC) atomicMax(lp, tick); else if (*lp < tick) *lp = tick;
-    if (!(lo & kCreditFirst)) return;
+    if (!(lo & kCreditFirst) || (a.diag & DIAG_D_NO_COMMIT)) return;
     const ctp_t tp = const_tp(a.tp) + t;
     const int64_t ir = (int64_t)t * a.E + (hi & kEdgeMask);
     const double cap = tp->first_message_deliveries_cap;
@@ -243,6 +243,49 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
             const int k = k0 + b;
             cv[b] = (k < nact && vj) ? a.cell[(int64_t)s_act[k] * a.N + jl] : kUnseen64;
         }
+        // (1) commit this lane's claims of round g-1: the winners' records are
+        // loaded for the whole batch first (one memory trip), then updated in
+        // slot order (a record winning several slots continues from the value
+        // stored for the earlier one)
+        {
+            double fv[kSlotBatch];
+            int64_t irb[kSlotBatch];
+#pragma unroll
+            for (int b = 0; b < kSlotBatch; ++b) {
+                irb[b] = -1;
+                fv[b] = 0.0;
+                const int k = k0 + b;
+                if (k < nact && is_claim_of(cv[b], qpar) && ((uint32_t)cv[b] & kCreditFirst) &&
+                    !a.minv[s_act[k]]) {
+                    irb[b] = (int64_t)a.mtopic[s_act[k]] * a.E + ((uint32_t)(cv[b] >> 32) & kEdgeMask);
+                    fv[b] = a.first[irb[b]];
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < kSlotBatch; ++b) {
+                const int k = k0 + b;
+                if (k >= nact || !is_claim_of(cv[b], qpar)) continue;
+                const uint32_t m = s_act[k];
+                const uint64_t c0 = cv[b];
+                a.cell[(int64_t)m * a.N + jl] = ((uint64_t)gprev << 32) | ((uint32_t)c0 & kPeerMask);
+                if (a.minv[m]) continue;                 // RejectMessage: counted when sent
+                const int32_t t = (int32_t)a.mtopic[m];
+                int32_t* lp = a.lastput + (int64_t)t * a.N + jl;
+                const int32_t tick = (int32_t)((a.g - 1) / a.R);
+                if (*lp < tick) *lp = tick;              // mcache.Put
+                if (irb[b] < 0 || (a.diag & DIAG_D_NO_COMMIT)) continue;
+                double x = fv[b];
+#pragma unroll
+                for (int bb = 0; bb < b; ++bb)
+                    if (irb[bb] == irb[b]) x = fv[bb];
+                const double cap = (tpa + t)->first_message_deliveries_cap;
+                x = (x + 1.0 > cap) ? cap : x + 1.0;
+                fv[b] = x;
+                a.first[irb[b]] = x;                     // markFirstMessageDelivery P2
+                if ((uint32_t)c0 & kCreditMesh)
+                    atomic_inc_capped(&a.meshd[irb[b]], (tpa + t)->mesh_message_deliveries_cap);
+            }
+        }
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
@@ -250,9 +293,7 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
             const uint32_t m = s_act[k];
             const int64_t row_m = (int64_t)m * a.N;
             const uint64_t c0 = cv[b];
-            const bool pend = is_claim_of(c0, qpar);     // first received in round g-1, not committed
-            // (1) commit this lane's claim of round g-1
-            if (pend) commit_claim(a, a.cell + row_m + jl, c0, a.g - 1, m, jl);
+            const bool pend = is_claim_of(c0, qpar);     // first received in round g-1 (committed above)
             const uint32_t origin = a.morigin[m];
             const bool inv = a.minv[m] != 0;
             // receivers reject an invalid message and do not forward it; its
@@ -283,30 +324,33 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
                 const uint32_t e1 = beg1 + (uint32_t)gl, e2 = beg2 + (uint32_t)gl;
                 const uint32_t j1 = (uint32_t)(j0 + (b1 < 0 ? 0 : b1)), j2 = (uint32_t)(j0 + (b2 < 0 ? 0 : b2));
                 // trip 1: the edge's router and record state
+                const bool rowst = !(a.diag & DIAG_D_NO_ROWSTATE);
                 uint32_t i1 = 0, i2 = 0;
-                uint8_t mf1 = 0, mf2 = 0, rs1 = 0, rs2 = 0, ac1 = 0, ac2 = 0, es1 = 0, es2 = 0, tf1 = 0, tf2 = 0;
+                uint8_t mf1 = 0, mf2 = 0, ds1 = 0, ds2 = 0, tf1 = 0, tf2 = 0;
                 if (v1) {
-                    i1 = a.col[e1]; mf1 = a.mflags[plane + e1]; rs1 = a.rstate[e1]; ac1 = a.acc[e1];
-                    es1 = a.estate[e1]; tf1 = a.tflags[plane + e1];
+                    i1 = a.col[e1]; mf1 = a.mflags[plane + e1];
+                    ds1 = rowst ? a.dstate[e1] : (uint8_t)0xFF; tf1 = rowst ? a.tflags[plane + e1] : GSIM_TF_IN_MESH;
                 }
                 if (v2) {
-                    i2 = a.col[e2]; mf2 = a.mflags[plane + e2]; rs2 = a.rstate[e2]; ac2 = a.acc[e2];
-                    es2 = a.estate[e2]; tf2 = a.tflags[plane + e2];
+                    i2 = a.col[e2]; mf2 = a.mflags[plane + e2];
+                    ds2 = rowst ? a.dstate[e2] : (uint8_t)0xFF; tf2 = rowst ? a.tflags[plane + e2] : GSIM_TF_IN_MESH;
                 }
-                const bool tg1 = v1 && (mf1 & GSIM_TF_MESH) && (rs1 & GSIM_ES_CONNECTED) && i1 != f1 && i1 != origin;
-                const bool tg2 = v2 && (mf2 & GSIM_TF_MESH) && (rs2 & GSIM_ES_CONNECTED) && i2 != f2 && i2 != origin;
-                n_gray += (tg1 && !ac1) + (tg2 && !ac2);     // AcceptFrom: graylisted sender
-                const bool ok1 = tg1 && ac1, ok2 = tg2 && ac2;
+                const bool tg1 = v1 && (mf1 & GSIM_TF_MESH) && (ds1 & GSIM_DS_CONNECTED) && i1 != f1 && i1 != origin;
+                const bool tg2 = v2 && (mf2 & GSIM_TF_MESH) && (ds2 & GSIM_DS_CONNECTED) && i2 != f2 && i2 != origin;
+                const bool ok1 = tg1 && (ds1 & GSIM_DS_ACCEPT), ok2 = tg2 && (ds2 & GSIM_DS_ACCEPT);
+                n_gray += (tg1 && !ok1) + (tg2 && !ok2);     // AcceptFrom: graylisted sender
                 n_acc += ok1 + ok2;
                 // trip 2: the receiver's cell and the counter to update
-                const bool sc1 = ok1 && scored_t && (es1 & GSIM_ES_TRACKED);
-                const bool sc2 = ok2 && scored_t && (es2 & GSIM_ES_TRACKED);
+                const bool cnt = !(a.diag & DIAG_D_NO_COUNTERS);
+                const bool sc1 = ok1 && scored_t && (ds1 & GSIM_DS_TRACKED) && cnt;
+                const bool sc2 = ok2 && scored_t && (ds2 & GSIM_DS_TRACKED) && cnt;
                 uint64_t c1 = 0, c2 = 0;
+                uint32_t n1 = 0, n2 = 0;
                 double x1 = 0.0, x2 = 0.0;
                 if (ok1) c1 = a.cell[row_m + i1];
                 if (ok2) c2 = a.cell[row_m + i2];
-                if (sc1) x1 = inv ? a.invalid[plane + e1] : ((tf1 & GSIM_TF_IN_MESH) ? a.meshd[plane + e1] : 0.0);
-                if (sc2) x2 = inv ? a.invalid[plane + e2] : ((tf2 & GSIM_TF_IN_MESH) ? a.meshd[plane + e2] : 0.0);
+                if (sc1) { if (inv) x1 = a.invalid[plane + e1]; else if (tf1 & GSIM_TF_IN_MESH) n1 = a.mcnt[plane + e1]; }
+                if (sc2) { if (inv) x2 = a.invalid[plane + e2]; else if (tf2 & GSIM_TF_IN_MESH) n2 = a.mcnt[plane + e2]; }
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
                     const bool ok = u ? ok2 : ok1;
@@ -315,7 +359,6 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
                     const uint32_t e = u ? e2 : e1, i = u ? i2 : i1, j = u ? j2 : j1;
                     const bool sc = u ? sc2 : sc1;
                     const uint8_t tf = u ? tf2 : tf1;
-                    const double x = u ? x2 : x1;
                     const uint32_t hi = (uint32_t)(c >> 32);
                     // first-seen round of an earlier round, or -1 for unseen /
                     // claimed in this round
@@ -332,20 +375,33 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
                             if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo |= kCreditMesh;
                         }
                         const uint64_t v = ((uint64_t)(claim_hi | e) << 32) | lo;
-                        const uint64_t prev = __hip_atomic_fetch_min(a.cell + row_m + i, v, __ATOMIC_RELAXED,
-                                                                     __HIP_MEMORY_SCOPE_AGENT);
+                        uint64_t prev;
+                        if (a.diag & DIAG_D_PLAIN_CLAIM) {
+                            prev = c;
+                            a.cell[row_m + i] = v;
+                        } else {
+                            prev = __hip_atomic_fetch_min(a.cell + row_m + i, v, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                        }
                         if (prev == kUnseen64) n_first++;
                     }
                     if (!sc) continue;
                     const int64_t ir = plane + e;
                     if (inv) {
-                        a.invalid[ir] = x + 1.0;                 // markInvalidMessageDelivery
+                        a.invalid[ir] = (u ? x2 : x1) + 1.0;    // markInvalidMessageDelivery
                     } else if (tf & GSIM_TF_IN_MESH) {
                         // markDuplicateMessageDelivery's window test; a same-round
                         // copy (first or duplicate) has validated = now
                         const bool in_window = seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window)
                                                                : (window >= 0);
-                        if (in_window) a.meshd[ir] = (x + 1.0 > mcap) ? mcap : x + 1.0;
+                        if (in_window) {
+                            uint32_t n = u ? n2 : n1;
+                            if (n == 255u) {   // spill a full count into the counter (this lane owns the record)
+                                a.meshd[ir] = apply_incs(a.meshd[ir], n, mcap);
+                                n = 0;
+                            }
+                            a.mcnt[ir] = (uint8_t)(n + 1);
+                        }
                     }
                 }
             }
@@ -453,15 +509,16 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.t0 = d->cfg.t0_ns; a.hb = d->cfg.heartbeat_ns; a.g = g;
     a.now = a.t0 + (g / a.R) * a.hb + (g % a.R + 1) * a.hb / (a.R + 1);
     a.row_ptr = h->d_row_ptr; a.col = h->d_col;
-    a.rstate = h->d_rstate; a.mflags = h->d_mflags; a.acc = h->d_acc;
-    a.estate = h->d_estate; a.tflags = h->d_tflags; a.tp = h->d_tp;
-    a.first = h->d_first; a.meshd = h->d_meshd; a.invalid = h->d_invalid;
+    a.dstate = h->d_dstate; a.mflags = h->d_mflags;
+    a.tflags = h->d_tflags; a.tp = h->d_tp;
+    a.first = h->d_first; a.meshd = h->d_meshd; a.invalid = h->d_invalid; a.mcnt = h->d_mcnt;
     a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv;
     a.cell = d->d_cell; a.lastput = d->d_lastput;
     const size_t w = (size_t)nnew_words(d);
     a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
     a.nnew_cur = d->d_nnew + (size_t)(g & 1) * w;
     a.stats = d->d_stats;
+    a.diag = h->diag;
     return a;
 }
 
@@ -624,6 +681,7 @@ int gsim_round(gsim_handle* h, int64_t round)
     for (const auto& tp : h->tp)
         if (tp.scored && tp.mesh_message_deliveries_window_ns < 0) lazy = false;
     RoundArgs a = make_round_args(h, round);
+    h->mcnt_dirty = true;
     const size_t lds = (((size_t)d->cfg.ring + 1) & ~(size_t)1) * sizeof(uint16_t) + (size_t)nnew_words(d) * 4;
     {
         ProfScope ps(h, GSIM_K_SEND);

@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
             a.expire[e] = 0;
             for (int32_t t = 0; t < a.T; ++t) {
                 const int64_t i = (int64_t)t * a.E + e;
-                a.first[i] = 0.0; a.meshd[i] = 0.0; a.fail[i] = 0.0; a.invalid[i] = 0.0;
+                a.first[i] = 0.0; a.meshd[i] = 0.0; a.fail[i] = 0.0; a.invalid[i] = 0.0; a.mcnt[i] = 0;
                 a.graft[i] = 0; a.mtime[i] = 0; a.tflags[i] = 0;
             }
             *a.purged = 1;
@@ -86,6 +86,12 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
             double first = a.first[i], meshd = a.meshd[i], fail = a.fail[i], inval = a.invalid[i];
             uint8_t fl = a.tflags[i];
             int64_t mt = 0;
+            const uint8_t pc = a.mcnt[i];
+            if (pc) {   // deliveries since the last pass precede this decay
+                meshd = apply_incs(meshd, pc, tp->mesh_message_deliveries_cap);
+                a.meshd[i] = meshd;
+                a.mcnt[i] = 0;
+            }
             if (decay) {
                 double x;
                 x = first * tp->first_message_deliveries_decay;  if (x < a.dtz) x = 0.0;
@@ -215,13 +221,14 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
         for (int t0 = 0; t0 < a.T; t0 += CHUNK) {
             double f[CHUNK], md[CHUNK], fa[CHUNK], iv[CHUNK];
             int64_t g[CHUNK];
-            uint8_t fl[CHUNK];
+            uint8_t fl[CHUNK], mc[CHUNK];
 #pragma unroll
             for (int j = 0; j < CHUNK; ++j) {
                 const int t = t0 + j;
                 f[j] = md[j] = fa[j] = iv[j] = 0.0;
                 g[j] = 0;
                 fl[j] = 0;
+                mc[j] = 0;
                 if (t < a.T && valid && tpa[t].scored) {
                     const int64_t i = (int64_t)t * a.E + e;
                     f[j] = a.first[i];
@@ -229,6 +236,7 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
                     fa[j] = a.fail[i];
                     iv[j] = a.invalid[i];
                     fl[j] = a.tflags[i];
+                    mc[j] = a.mcnt[i];
                     if (!(a.diag & DIAG_NO_GRAFT)) g[j] = decay ? a.graft[i] : (SCORE ? a.mtime[i] : 0);
                 }
             }
@@ -243,7 +251,12 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
                 uint8_t fj = fl[j];
                 int64_t mt = g[j];
                 bool cf = false, cm = false, cfa = false, ci = false, cfl = false, wmt = false;
+                const bool cmc = mc[j] != 0 || purge;
                 int64_t mt_store = 0;
+                if (mc[j] && !purge) {   // deliveries since the last pass precede this decay
+                    meshd = apply_incs(meshd, mc[j], tp->mesh_message_deliveries_cap);
+                    cm = true;
+                }
                 if (purge) {                                 // score.go:512-516
                     first = meshd = fail = inval = 0.0;
                     fj = 0;
@@ -296,11 +309,15 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
                 if (REFRESH && st_ok) {
                     policy_store(a.first, i, first, valid && cf, valid);
                     policy_store(a.meshd, i, meshd, valid && cm, valid);
+                    if (cmc && valid) a.mcnt[i] = 0;
                     policy_store(a.fail, i, fail, valid && cfa, valid);
                     policy_store(a.invalid, i, inval, valid && ci, valid);
                     policy_store(a.tflags, i, fj, valid && cfl, valid);
                     if (!(a.diag & DIAG_NO_MTIME)) policy_store(a.mtime, i, mt_store, valid && wmt, false);
                     if (purge) a.graft[i] = 0;
+                } else if (!REFRESH && valid && mc[j]) {   // score-only pass: still settle the counts
+                    a.meshd[i] = meshd;
+                    a.mcnt[i] = 0;
                 }
             }
         }
@@ -382,6 +399,21 @@ __global__ __launch_bounds__(256) void k_recap(int64_t E, const uint8_t* estate,
     }
 }
 
+// Apply every pending meshd increment (before the counter is read through the
+// ABI or its cap changes).
+__global__ __launch_bounds__(256) void k_apply_mcnt(ScoreArgs a)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t total = a.E * (int64_t)a.T;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += stride) {
+        const uint8_t n = a.mcnt[x];
+        if (!n) continue;
+        const int32_t t = (int32_t)(x / a.E);
+        a.meshd[x] = apply_incs(a.meshd[x], n, const_tp(a.tp)[t].mesh_message_deliveries_cap);
+        a.mcnt[x] = 0;
+    }
+}
+
 // Seeded synthetic steady-state-like counters for benchmarking at full size
 // (SURVEY.md §8(d)): a Philox draw per edge-topic record decides mesh
 // membership (probability D/k), activation, graft time and the four counters.
@@ -436,7 +468,7 @@ __global__ __launch_bounds__(256) void k_census(ScoreArgs a, unsigned long long*
             c[0] += 1;
             c[1] += (fl & GSIM_TF_IN_MESH) != 0;
             c[2] += a.first[i] != 0.0;
-            c[3] += a.meshd[i] != 0.0;
+            c[3] += apply_incs(a.meshd[i], a.mcnt[i], const_tp(a.tp)[t].mesh_message_deliveries_cap) != 0.0;
             c[4] += a.fail[i] != 0.0;
             c[5] += a.invalid[i] != 0.0;
         }
@@ -498,13 +530,17 @@ __global__ __launch_bounds__(256) void k_estate_split(const uint8_t* in, uint8_t
     }
 }
 
-// AcceptFrom (gossipsub.go:598-609) verdict of every record's observer for
-// its neighbour, from the score snapshot: score >= graylistThreshold.
-__global__ __launch_bounds__(256) void k_accept(const double* score, uint8_t* acc, int64_t E, double gray)
+// Delivery state of every edge index e (GSIM_DS_*): the router's connected
+// bit of edge e, and of record e the AcceptFrom verdict (gossipsub.go:598-609:
+// score snapshot >= graylistThreshold) and whether it is tracked.
+__global__ __launch_bounds__(256) void k_delivery_state(const double* score, const uint8_t* estate,
+                                                        const uint8_t* rstate, uint8_t* ds, int64_t E, double gray)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < E; r += stride)
-        acc[r] = score[r] >= gray ? 1 : 0;
+        ds[r] = (uint8_t)(((rstate[r] & GSIM_ES_CONNECTED) ? GSIM_DS_CONNECTED : 0) |
+                          (score[r] >= gray ? GSIM_DS_ACCEPT : 0) |
+                          ((estate[r] & GSIM_ES_TRACKED) ? GSIM_DS_TRACKED : 0));
 }
 
 __global__ void k_fill_u8(uint8_t* p, int64_t n, uint8_t v)
@@ -564,7 +600,7 @@ void free_graph(gsim_handle* h)
     dfree(h->d_first); dfree(h->d_meshd); dfree(h->d_fail); dfree(h->d_invalid);
     dfree(h->d_graft); dfree(h->d_mtime); dfree(h->d_tflags); dfree(h->d_mflags);
     dfree(h->d_bp); dfree(h->d_estate); dfree(h->d_expire); dfree(h->d_p6); dfree(h->d_score);
-    dfree(h->d_backoff); dfree(h->d_rstate); dfree(h->d_acc);
+    dfree(h->d_backoff); dfree(h->d_rstate); dfree(h->d_dstate); dfree(h->d_mcnt);
     h->bytes_allocated = 0;
     h->n = h->e = 0;
 }
@@ -585,6 +621,7 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     a.owner = h->d_owner;
     a.p5 = h->d_p5;
     a.first = h->d_first; a.meshd = h->d_meshd; a.fail = h->d_fail; a.invalid = h->d_invalid;
+    a.mcnt = h->d_mcnt;
     a.graft = h->d_graft; a.mtime = h->d_mtime; a.tflags = h->d_tflags;
     a.mflags = h->d_mflags; a.rstate = h->d_rstate; a.rev = h->d_rev;
     a.bp = h->d_bp; a.estate = h->d_estate; a.expire = h->d_expire; a.p6 = h->d_p6; a.score = h->d_score;
@@ -658,6 +695,7 @@ int launch_refresh_scores(gsim_handle* h, int64_t now)
     } else {
         launch_score_kernel<true, true>(h, a);
     }
+    h->mcnt_dirty = false;   // the score pass settled every pending count
     h->score_version++;
     return hip_check(h, hipGetLastError(), "k_refresh_score");
 }
@@ -672,6 +710,7 @@ int launch_compute_scores(gsim_handle* h)
     }
     ScoreArgs a = make_score_args(h, 0);
     launch_score_kernel<false, true>(h, a);
+    h->mcnt_dirty = false;
     h->score_version++;
     return hip_check(h, hipGetLastError(), "k_refresh_score<score>");
 }
@@ -679,10 +718,20 @@ int launch_compute_scores(gsim_handle* h)
 int refresh_accept(gsim_handle* h)
 {
     if (h->acc_version == h->score_version) return GSIM_OK;
-    hipLaunchKernelGGL(k_accept, dim3(grid_for(h->e)), dim3(256), 0, h->stream, (const double*)h->d_score,
-                       h->d_acc, h->e, h->th.graylist_threshold);
+    hipLaunchKernelGGL(k_delivery_state, dim3(grid_for(h->e)), dim3(256), 0, h->stream, (const double*)h->d_score,
+                       (const uint8_t*)h->d_estate, (const uint8_t*)h->d_rstate, h->d_dstate, h->e,
+                       h->th.graylist_threshold);
     h->acc_version = h->score_version;
-    return hip_check(h, hipGetLastError(), "k_accept");
+    return hip_check(h, hipGetLastError(), "k_delivery_state");
+}
+
+int materialize_mcnt(gsim_handle* h)
+{
+    if (!h->mcnt_dirty) return GSIM_OK;
+    ScoreArgs a = make_score_args(h, 0);
+    hipLaunchKernelGGL(k_apply_mcnt, dim3(grid_for(h->e * (int64_t)std::max(1, h->t))), dim3(256), 0, h->stream, a);
+    h->mcnt_dirty = false;
+    return hip_check(h, hipGetLastError(), "k_apply_mcnt");
 }
 
 // ---------------------------------------------------------------------------
@@ -934,7 +983,8 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     rc = rc ? rc : dalloc(h, &h->d_mflags, ET);
     rc = rc ? rc : dalloc(h, &h->d_backoff, ET);
     rc = rc ? rc : dalloc(h, &h->d_rstate, E);
-    rc = rc ? rc : dalloc(h, &h->d_acc, E);
+    rc = rc ? rc : dalloc(h, &h->d_dstate, E);
+    rc = rc ? rc : dalloc(h, &h->d_mcnt, ET);
     rc = rc ? rc : dalloc(h, &h->d_bp, E);
     rc = rc ? rc : dalloc(h, &h->d_estate, E);
     rc = rc ? rc : dalloc(h, &h->d_expire, E);
@@ -972,6 +1022,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     zero(h->d_mtime, sizeof(int64_t) * (size_t)ET);
     zero(h->d_tflags, (size_t)ET);
     zero(h->d_mflags, (size_t)ET);
+    zero(h->d_mcnt, (size_t)ET);
     zero(h->d_backoff, sizeof(int64_t) * (size_t)ET);
     zero(h->d_bp, sizeof(double) * (size_t)E);
     zero(h->d_expire, sizeof(int64_t) * (size_t)E);
@@ -986,6 +1037,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     h->has_white = false;
     h->p6_dirty = true;
     h->maybe_retained = false;
+    h->mcnt_dirty = false;
     int rc2 = alloc_extra(h);
     if (rc2) return rc2;
     he = hipStreamSynchronize(s);
@@ -1025,6 +1077,7 @@ int gsim_set_topic_params(gsim_handle* h, int32_t t, const gsim_topic_score_para
     char buf[256] = {0};
     if (h->validate && p->scored && gsim_validate_topic_params(p, buf, sizeof buf)) { h->err = buf; return GSIM_EINVAL; }
     int rcf = deliver_flush(h);
+    if (!rcf) rcf = materialize_mcnt(h);   // pending increments saw the old cap
     if (rcf) return rcf;
     const gsim_topic_score_params old = h->tp[t];
     h->tp[t] = *p;
@@ -1071,6 +1124,7 @@ int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now, double p_mes
     GSIM_ENTER(h);
     GSIM_NEED_GRAPH(h);
     int rcf = deliver_flush(h);
+    if (!rcf) rcf = materialize_mcnt(h);
     if (rcf) return rcf;
     ScoreArgs a = make_score_args(h, now);
     hipLaunchKernelGGL(k_fill_synthetic, dim3(grid_for(h->e)), dim3(256), 0, h->stream, a, seed, p_mesh);
@@ -1147,6 +1201,7 @@ int gsim_read_field(gsim_handle* h, int32_t f, void* dst, size_t bytes)
     if (bytes != r.bytes || !dst) { h->err = "field size mismatch"; return GSIM_EINVAL; }
     if (r.kind == FK_SEEN) return deliver_read_seen(h, dst);
     int rc = deliver_flush(h);
+    if (!rc) rc = materialize_mcnt(h);
     if (rc) return rc;
     return read_field_impl(h, r, dst);
 }
@@ -1160,9 +1215,10 @@ int gsim_write_field(gsim_handle* h, int32_t f, const void* src, size_t bytes)
     if (bytes != r.bytes || !src) { h->err = "field size mismatch"; return GSIM_EINVAL; }
     if (r.kind == FK_SEEN) { h->err = "the seen-set is read-only"; return GSIM_EINVAL; }
     int rc = deliver_flush(h);
+    if (!rc) rc = materialize_mcnt(h);
     if (rc) return rc;
     rc = write_field_impl(h, r, src);
-    if (f == GSIM_F_ESTATE) { h->p6_dirty = true; h->maybe_retained = true; }
+    if (f == GSIM_F_ESTATE) { h->p6_dirty = true; h->maybe_retained = true; h->score_version++; }
     if (f == GSIM_F_SCORE) h->score_version++;
     return rc;
 }

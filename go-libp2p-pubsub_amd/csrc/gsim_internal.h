@@ -21,6 +21,7 @@ struct ScoreArgs {
     const uint32_t* owner;     // owner[r]: the neighbour a record is about (§2)
     const double* p5;
     double *first, *meshd, *fail, *invalid;
+    uint8_t* mcnt;             // pending meshMessageDeliveries increments (see apply_incs)
     int64_t *graft, *mtime;
     uint8_t* tflags;           // score bits only (inMesh, active)
     uint8_t* mflags;           // router mesh bits, edge order (fill/census)
@@ -44,6 +45,11 @@ enum : uint32_t {
     DIAG_NO_STORES = 4,  // skip every record store
     DIAG_NO_GRAFT = 8,   // skip the graftTime load
     DIAG_NO_DIV = 16,    // skip the P1 division
+    // delivery (k_send) ablations
+    DIAG_D_NO_COUNTERS = 32,    // skip the meshMessageDeliveries / invalid read-modify-writes
+    DIAG_D_PLAIN_CLAIM = 64,    // plain store instead of the claim atomicMin (racy)
+    DIAG_D_NO_ROWSTATE = 128,   // skip the acc/estate/tflags/rstate loads (all pass)
+    DIAG_D_NO_COMMIT = 256,     // skip the P2 credit of commits
 };
 
 struct ColocArgs {
@@ -54,6 +60,20 @@ struct ColocArgs {
     double* p6;
     int32_t thr;
 };
+
+// meshMessageDeliveries increments from message delivery are kept as a
+// per-record u8 count between score passes (the delivery kernel then touches
+// one byte per copy instead of read-modify-writing an f64): applying them is
+// the exact sequence of markDuplicate/markFirst updates x -> min(x + 1, cap)
+// (score.go:935-941, 975-980), performed before anything reads the counter.
+__device__ __forceinline__ double apply_incs(double x, uint32_t n, double cap)
+{
+    for (uint32_t k = 0; k < n; ++k) {
+        x = x + 1.0;
+        if (x > cap) { x = cap; break; }   // further increments keep the cap
+    }
+    return x;
+}
 
 // Topic parameters are read-only for a kernel's lifetime.  Reading them
 // through the constant address space (4) lets the compiler use scalar
@@ -128,6 +148,8 @@ struct gsim_handle {
     // so the ABI's edge-order view is a gather through rev both ways.
     // device: topicStats [T][E], record order
     double *d_first = nullptr, *d_meshd = nullptr, *d_fail = nullptr, *d_invalid = nullptr;
+    uint8_t* d_mcnt = nullptr;        // pending meshd increments (apply_incs)
+    bool mcnt_dirty = false;
     int64_t *d_graft = nullptr, *d_mtime = nullptr;
     uint8_t* d_tflags = nullptr;      // GSIM_TF_IN_MESH | GSIM_TF_ACTIVE
     // device: router state [T][E] / [E], edge (observer) order
@@ -141,7 +163,7 @@ struct gsim_handle {
     int64_t* d_expire = nullptr;
     double* d_p6 = nullptr;
     double* d_score = nullptr;
-    uint8_t* d_acc = nullptr;         // score >= graylistThreshold (AcceptFrom), derived
+    uint8_t* d_dstate = nullptr;      // delivery state per edge, derived (GSIM_DS_*)
     uint64_t score_version = 1, acc_version = 0;
 
     // per-kernel-class device timing (gsim_profile); events are pooled
@@ -162,7 +184,16 @@ bool field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r);
 int launch_ip_colocation(gsim_handle* h);
 int launch_refresh_scores(gsim_handle* h, int64_t now);
 int launch_compute_scores(gsim_handle* h);
-int refresh_accept(gsim_handle* h);   // recompute d_acc if the snapshot changed
+int refresh_accept(gsim_handle* h);   // recompute d_dstate if the snapshot changed
+int materialize_mcnt(gsim_handle* h); // apply pending meshd increments everywhere
+
+// Delivery state byte per edge index e: what one forwarded
+// copy over e needs besides the topic planes.
+enum : uint8_t {
+    GSIM_DS_CONNECTED = 0x01,   // router: the sender (row owner) is connected to col[e]
+    GSIM_DS_ACCEPT = 0x02,      // record e: the receiver accepts RPCs from the sender (AcceptFrom)
+    GSIM_DS_TRACKED = 0x04,     // record e: the receiver keeps peerStats for the sender
+};
 
 // Brackets the launches of one kernel class with pooled HIP events on the
 // engine stream while profiling is enabled (gsim_profile).

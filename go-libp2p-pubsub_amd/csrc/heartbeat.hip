@@ -39,6 +39,7 @@ struct HbArgs {
     uint8_t* tflags;    // score bits (inMesh, active), record order [T][E]
     int64_t* backoff;
     double *meshd, *fail, *bp;
+    const uint8_t* mcnt;
     int64_t *graft, *mtime;
     uint8_t* ctl_in;    // inbox this phase reads (round parity)
     uint8_t* ctl_out;   // inbox this phase writes
@@ -121,12 +122,14 @@ __device__ __forceinline__ void stats_graft(const HbArgs& a, bool tracked, bool 
     a.mtime[sf.ir] = 0;
 }
 
-__device__ __forceinline__ void stats_prune(const HbArgs& a, bool tracked, bool scored, double thr, ScoreFlags& sf)
+__device__ __forceinline__ void stats_prune(const HbArgs& a, bool tracked, bool scored, double thr, double mcap,
+                                            ScoreFlags& sf)
 {
     if (!tracked || !scored) return;
     uint8_t& fl = sf.get(a);
     if (fl & GSIM_TF_ACTIVE) {
-        const double md = a.meshd[sf.ir];
+        // pending delivery increments are part of the counter's value
+        const double md = apply_incs(a.meshd[sf.ir], a.mcnt[sf.ir], mcap);
         if (md < thr) {
             const double deficit = thr - md;
             a.fail[sf.ir] = a.fail[sf.ir] + deficit * deficit;
@@ -181,6 +184,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             const ctp_t tp = const_tp(a.tp) + t;
             const bool scored = tp->scored != 0;
             const double thr = tp->mesh_message_deliveries_threshold;
+            const double mcap = tp->mesh_message_deliveries_cap;
             const int64_t i = (int64_t)t * a.E + e;
             ScoreFlags sf;
             sf.ir = (int64_t)t * a.E + rv;
@@ -202,7 +206,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             const uint32_t pos = (uint32_t)lane;
 
             auto prune = [&]() {
-                stats_prune(a, tracked, scored, thr, sf);
+                stats_prune(a, tracked, scored, thr, mcap, sf);
                 fl &= (uint8_t)~GSIM_TF_MESH;
                 m = false;
                 need_bo();
@@ -352,6 +356,7 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
             const ctp_t tp = const_tp(a.tp) + t;
             const bool scored = tp->scored != 0;
             const double thr = tp->mesh_message_deliveries_threshold;
+            const double mcap = tp->mesh_message_deliveries_cap;
             uint8_t fl = valid ? a.mflags[i] : 0;
             int mesh = __popcll(ballot(valid && (fl & GSIM_TF_MESH)));
             while (pending) {
@@ -394,7 +399,7 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                     }
                     if (c & GSIM_CTL_PRUNE) {
                         if (fl & GSIM_TF_MESH) delta -= 1;
-                        stats_prune(a, tracked, scored, thr, sf);
+                        stats_prune(a, tracked, scored, thr, mcap, sf);
                         fl &= (uint8_t)~GSIM_TF_MESH;
                         const int64_t secs = a.prune_backoff / kSecond;
                         const int64_t ex = a.now + (secs > 0 ? secs * kSecond : a.prune_backoff);
@@ -463,7 +468,7 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.rev = h->d_rev; a.sub = h->d_sub;
     a.outbound = h->d_outbound; a.estate = h->d_estate; a.score = h->d_score; a.tp = h->d_tp;
     a.tflags = h->d_tflags; a.mflags = h->d_mflags; a.rstate = h->d_rstate; a.backoff = h->d_backoff; a.meshd = h->d_meshd; a.fail = h->d_fail; a.bp = h->d_bp;
-    a.graft = h->d_graft; a.mtime = h->d_mtime;
+    a.graft = h->d_graft; a.mtime = h->d_mtime; a.mcnt = h->d_mcnt;
     const size_t TE = (size_t)h->e * (size_t)std::max(1, h->t);
     a.ctl_in = h->x->d_ctl + (size_t)(parity_in & 1) * TE;
     a.ctl_out = h->x->d_ctl + (size_t)((parity_in + 1) & 1) * TE;
