@@ -38,7 +38,8 @@ SECOND = 1_000_000_000
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 ROUNDS = 10                    # propagation rounds per heartbeat
 MSG_RATE = 4.0                 # messages / s / topic
-MSG_RING = 512                 # live-message window (>= 8 heartbeats of publications)
+MSG_RING = 1024                # live-message window: >= 16 heartbeats of publications, so no slot
+                               # is republished while its message can still be gossiped or promised
 DUP_BYTES, FIRST_BYTES = 40, 72   # algorithmic bytes per delivery
 
 CONFIGS = {
@@ -134,8 +135,9 @@ def cpu_baseline(cfg, budget_s: float = 15.0):
         kk = steps + 1
         now = tick_time(kk)
         lib.orc_refresh_scores(v, now)
+        msgs.penalties(st, now)
         lib.orc_compute_scores(v)
-        lib.orc_heartbeat(v, kk, now, 0x5EED0001)
+        msgs.heartbeat(st, kk, now, 0x5EED0001)
         for g in range(kk * ROUNDS, (kk + 1) * ROUNDS):
             for m in sched.get(g, []):
                 msgs.publish(st, int(m["id"]), int(m["topic"]), int(m["origin"]), 0, g)

@@ -44,6 +44,7 @@
 #include <vector>
 
 #include "gsim_internal.h"
+#include "philox.h"
 
 namespace gsim {
 
@@ -70,6 +71,20 @@ struct Deliver {
     int64_t next_round = -1;           // -1: any
     int64_t pending = -1;              // round whose claims are not committed yet
     bool lazy = true;                  // every window >= 0: commits may trail a round
+    // gossip
+    int32_t* d_slot_last = nullptr;    // [ring] last round with a new claim or the publication
+    uint8_t* d_ihave = nullptr;        // [T][E] receiver edge: IHAVE(topic) from col[e] this heartbeat
+    uint8_t* d_gstate = nullptr;       // [E] edge order: owner's snapshot score of col >= gossipThreshold
+    uint64_t* d_resp = nullptr;        // IWANT responses (record edge | slot << 32), delivered in round 2
+    uint32_t* d_nresp = nullptr;       // [1] responses queued; [1] overflow; [2] ring-reuse error
+    int64_t resp_cap = 0;
+    uint32_t* d_prom = nullptr;        // [P][E] promise ring, edge order of the promiser: slot or none
+    uint64_t* d_pcand = nullptr;       // [E] per-IWANT promise candidate (min Philox key | slot)
+    uint8_t* d_behaviour = nullptr;    // [N] GSIM_BEHAVE_*
+    int32_t prom_ticks = 1;            // P
+    std::vector<int64_t> prom_made;    // [P] tick that filled each ring index, -1 = empty
+    int64_t ihave_tick = -1;           // heartbeat whose IHAVE marks are pending
+    int64_t resp_round = -1;           // round in which the queued responses arrive
 };
 
 struct RoundArgs {
@@ -91,11 +106,22 @@ struct RoundArgs {
     const uint32_t* nnew_prev;     // bitmask: slots with new claims (or a publication) in round g-1
     uint32_t* nnew_cur;            // bitmask: slots with new claims in round g
     unsigned long long* stats;
+    int32_t* slot_last;
+    uint32_t* err;                 // [0] responses queued, [1] overflow, [2] ring slot reused too early
+    int32_t reuse_guard;           // rounds a slot must stay unpublished after its last activity
 };
 
 __device__ __forceinline__ int64_t round_time(const RoundArgs& a, int64_t g)
 {
     return a.t0 + (g / a.R) * a.hb + (g % a.R + 1) * a.hb / (a.R + 1);
+}
+
+// lanes of group `grp` when a wave is split into groups of W lanes
+template <int W>
+__device__ __forceinline__ uint64_t group_mask(int grp)
+{
+    if constexpr (W == 64) return ~0ull;
+    else return ((1ull << W) - 1) << (grp * W);
 }
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
@@ -184,6 +210,9 @@ __global__ void k_reset_slots(RoundArgs a, const gsim_msg* pub, int32_t count)
     const uint32_t m = (uint32_t)(pub[k].id % (uint64_t)a.ring);
     uint64_t* row = a.cell + (int64_t)m * a.N;
     const uint32_t q = (uint32_t)((a.g - 1) & 1);
+    // the previous message may still sit in a gossip window or a promise
+    if (blockIdx.x == 0 && threadIdx.x == 0 && a.slot_last[m] >= 0 && a.g - a.slot_last[m] < a.reuse_guard)
+        atomicOr(&a.err[2], 1u);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.N; i += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t c = row[i];
         // several reused rows may credit one record: atomic updates here
@@ -206,6 +235,7 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, int32_t count)
     const int32_t tick = (int32_t)(a.g / a.R);
     if (*lp < tick) *lp = tick;
     atomicOr(&a.nnew_cur[slot >> 5], 1u << (slot & 31));   // the origin forwards in round g+1
+    a.slot_last[slot] = (int32_t)a.g;
 }
 
 // Round g.  W = lanes per row (power of two >= the longest row); group q of
@@ -227,7 +257,7 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
     const int64_t jl = j0 + lane;
     const bool vj = jl < a.N;
     const int grp = lane / W, gl = lane % W;
-    const uint64_t gmask = (W == 64) ? ~0ull : (((1ull << W) - 1) << (grp * W));
+    const uint64_t gmask = group_mask<W>(grp);
     const ctp_t tpa = const_tp(a.tp);
     const uint32_t gprev = (uint32_t)(a.g - 1);
     const uint32_t par = (uint32_t)(a.g & 1), qpar = par ^ 1u;
@@ -418,8 +448,16 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
         atomicAdd(&s_stats[3], n_gray);
     }
     __syncthreads();
-    for (int w = threadIdx.x; w < (a.ring + 31) / 32; w += blockDim.x)
-        if (s_new[w]) atomicOr(&a.nnew_cur[w], s_new[w]);
+    for (int w = threadIdx.x; w < (a.ring + 31) / 32; w += blockDim.x) {
+        uint32_t bits = s_new[w];
+        if (!bits) continue;
+        atomicOr(&a.nnew_cur[w], bits);
+        while (bits) {                                   // mcache activity of the slot
+            const int q = __ffs(bits) - 1;
+            bits &= bits - 1;
+            atomicMax(&a.slot_last[w * 32 + q], (int32_t)a.g);
+        }
+    }
     if (threadIdx.x == 0 && (s_stats[0] | s_stats[3])) {
         atomicAdd(&a.stats[0], s_stats[0]);
         atomicAdd(&a.stats[1], s_stats[1]);
@@ -460,6 +498,305 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Gossip.  Heartbeat k's emitGossip marked ihave[t][e] in
+// the receivers' rows (heartbeat.hip).  Control round 0 of tick k runs
+// handleIHave for every receiver, and — because nothing a handleIWant gate
+// reads can change between rounds 0 and 1 (score snapshot, mcache window,
+// behaviour) — the advertisers' handleIWant with it: the messages they send
+// are queued for round 2.  Invariants this relies on (checked by the oracle,
+// which implements the reference's counters in full): a receiver gets at most
+// one IHAVE RPC per advertiser per heartbeat (peerhave <= 1, iasked = 0); the
+// ring is not larger than MaxIHaveLength (no IHAVE/IWANT truncation); and a
+// receiver asks an advertiser for a message at most once while it is in the
+// advertiser's mcache, because the answer always arrives (peertx <= 1).
+
+struct IhArgs {
+    int64_t N, E;
+    int32_t T, ring, R;
+    int64_t g, tick;
+    int32_t lo_round;              // first round of the gossip window
+    const uint32_t *row_ptr, *col, *rev;
+    const uint64_t* sub;
+    const uint32_t *mtopic, *morigin;
+    const uint8_t* minv;
+    const uint64_t* cell;
+    const int32_t* slot_last;
+    const uint8_t *ihave, *gstate, *behaviour;
+    uint64_t* pcand;
+    uint32_t* prom;
+    int32_t P, prom_idx;
+    uint64_t* resp;
+    uint32_t* nresp;               // [0] count, [1] overflow
+    int64_t resp_cap;
+    bool respond;                  // GossipRetransmission >= 1
+    uint64_t seed;
+};
+
+// first-seen round of a cell at control time of round g (any claim still
+// pending is from round g-1 or g), or -1
+__device__ __forceinline__ int64_t cell_round(uint64_t c, int64_t g)
+{
+    if (c == kUnseen64) return -1;
+    const uint32_t hi = (uint32_t)(c >> 32);
+    if (!(hi & kClaim)) return hi;
+    return (((hi >> 30) & 1u) == (uint32_t)(g & 1)) ? g : g - 1;
+}
+
+constexpr int kRespStage = 256;    // per-wave LDS staging of queued responses
+
+template <int W>
+__global__ __launch_bounds__(256) void k_ihave(IhArgs a)
+{
+    extern __shared__ uint16_t s_act[];   // [ring] candidate slots, then per-wave response staging
+    __shared__ int s_n;
+    const int wid = threadIdx.x >> 6;
+    uint64_t* stage = reinterpret_cast<uint64_t*>(s_act + ((a.ring + 3) & ~3)) + wid * kRespStage;
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        int n = 0;
+        for (int m0 = 0; m0 < a.ring; m0 += 64) {
+            const int m = m0 + lane;
+            const bool act = m < a.ring && a.slot_last[m] >= a.lo_round;   // someone put it in the window
+            const uint64_t b = __ballot(act);
+            if (act) s_act[n + __popcll(b & ((1ull << lane) - 1))] = (uint16_t)m;
+            n += __popcll(b);
+        }
+        if (lane == 0) s_n = n;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t p0 = ((int64_t)blockIdx.x * 4 + wid) * 64;
+    const int nact = p0 < a.N ? s_n : 0;
+    const int64_t pl = p0 + lane;
+    const bool vp = pl < a.N;
+    const int grp = lane / W, gl = lane % W;
+    const uint64_t gmask = group_mask<W>(grp);
+    const uint64_t subp = vp ? a.sub[pl] : 0ull;
+    const uint32_t rp0 = vp ? a.row_ptr[pl] : 0u;
+    const uint32_t rp1 = vp ? a.row_ptr[pl + 1] : 0u;
+    bool asked = false;                       // this lane's receiver sent an IWANT
+    int nstage = 0;
+    auto flush_stage = [&]() {
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        uint32_t base = 0;
+        if (lane == 0 && nstage) base = atomicAdd(&a.nresp[0], (uint32_t)nstage);
+        base = __shfl(base, 0, 64);
+        for (int q = lane; q < nstage; q += 64) {
+            if ((int64_t)base + q < a.resp_cap) a.resp[base + q] = stage[q];
+            else atomicOr(&a.nresp[1], 1u);
+        }
+        nstage = 0;
+    };
+    for (int k0 = 0; k0 < nact; k0 += kSlotBatch) {
+        uint64_t cv[kSlotBatch];
+#pragma unroll
+        for (int b = 0; b < kSlotBatch; ++b) {
+            const int k = k0 + b;
+            cv[b] = (k < nact && vp) ? a.cell[(int64_t)s_act[k] * a.N + pl] : 0ull;
+        }
+#pragma unroll
+        for (int b = 0; b < kSlotBatch; ++b) {
+            const int k = k0 + b;
+            if (k >= nact) break;                            // wave-uniform
+            const uint32_t m = s_act[k];
+            const int32_t t = (int32_t)a.mtopic[m];
+            // handleIHave: a joined topic and a message not seen yet (seenMessage)
+            const bool wanted = vp && cv[b] == kUnseen64 && ((subp >> t) & 1ull);
+            const uint64_t mask = __ballot(wanted);
+            if (!mask) continue;
+            const uint32_t origin = a.morigin[m];
+            const bool inv = a.minv[m] != 0;
+            const int64_t row_m = (int64_t)m * a.N;
+            const int64_t plane = (int64_t)t * a.E;
+            uint64_t gm = mask & gmask;
+            while (__ballot(gm != 0)) {
+                int bs = -1;
+                if (gm) { bs = __ffsll((long long)gm) - 1; gm &= gm - 1; }
+                const int sl = bs < 0 ? lane : bs;
+                const uint32_t beg = __shfl(rp0, sl, 64), end = __shfl(rp1, sl, 64);
+                const bool v = bs >= 0 && (uint32_t)gl < end - beg;
+                const uint32_t e = beg + (uint32_t)gl;
+                const uint32_t prcv = (uint32_t)(p0 + (bs < 0 ? 0 : bs));
+                bool req = false, resp = false;
+                uint32_t i = 0, r = 0;
+                if (v && a.ihave[plane + e] && a.gstate[e]) {          // IHAVE(t) from i, score >= gossipThreshold
+                    i = a.col[e];
+                    const int64_t fr = cell_round(a.cell[row_m + i], a.g);
+                    // the IHAVE lists i's mcache gossip window: puts of ticks k-HG .. k-1
+                    req = fr >= a.lo_round && fr < (int64_t)a.tick * a.R && (!inv || i == origin);
+                }
+                if (req) {
+                    const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, prcv, 0, P_PROMISE, m, i);
+                    if (key < a.pcand[e]) a.pcand[e] = key;          // AddPromise's random pick
+                    r = a.rev[e];
+                    // handleIWant at i: score gate on p, honoured IWANT, retransmission budget
+                    resp = a.respond && a.gstate[r] && !(a.behaviour[i] & GSIM_BEHAVE_IGNORE_IWANT);
+                }
+                const uint64_t rb = __ballot(req) & gmask;
+                if (rb && lane == bs) asked = true;
+                const uint64_t sb = __ballot(resp);
+                if (sb) {
+                    if (nstage + __popcll(sb) > kRespStage) flush_stage();
+                    if (resp) stage[nstage + __popcll(sb & ((1ull << lane) - 1))] = (uint64_t)r | ((uint64_t)m << 32);
+                    nstage += __popcll(sb);
+                }
+            }
+        }
+    }
+    flush_stage();
+    // AddPromise (gossip_tracer.go:48-75): one tracked id per IWANT, unless
+    // the same (id, peer) promise is still pending
+    uint64_t am = __ballot(asked) & gmask;
+    while (__ballot(am != 0)) {
+        int bs = -1;
+        if (am) { bs = __ffsll((long long)am) - 1; am &= am - 1; }
+        const int sl = bs < 0 ? lane : bs;
+        const uint32_t beg = __shfl(rp0, sl, 64), end = __shfl(rp1, sl, 64);
+        if (bs < 0 || (uint32_t)gl >= end - beg) continue;
+        const uint32_t e = beg + (uint32_t)gl;
+        const uint64_t key = a.pcand[e];
+        if (key == ~0ull) continue;
+        a.pcand[e] = ~0ull;
+        const uint32_t slot = (uint32_t)key;
+        bool exists = false;
+        for (int q = 0; q < a.P; ++q) exists |= a.prom[(int64_t)q * a.E + e] == slot;
+        if (!exists) a.prom[(int64_t)a.prom_idx * a.E + e] = slot;
+    }
+}
+
+// Round 2: the messages queued by handleIWant arrive.  Same tracer rules as
+// k_send's copies; a record can receive several responses in one launch, so
+// counters are updated atomically.
+__device__ __forceinline__ void atomic_mcnt_inc(uint8_t* mcnt, int64_t ir, double* meshd, double cap)
+{
+    uint32_t* w = reinterpret_cast<uint32_t*>(mcnt + (ir & ~(int64_t)3));
+    const int sh = (int)(ir & 3) * 8;
+    uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+        const uint32_t byte = (old >> sh) & 0xFFu;
+        const uint32_t nb = byte == 255u ? 1u : byte + 1u;
+        const uint32_t nw = (old & ~(0xFFu << sh)) | (nb << sh);
+        const uint32_t prev = atomicCAS(w, old, nw);
+        if (prev == old) {
+            if (byte == 255u) {                      // spill the full count
+                unsigned long long* q = reinterpret_cast<unsigned long long*>(meshd);
+                unsigned long long o = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (;;) {
+                    const double x = apply_incs(__longlong_as_double((long long)o), 255u, cap);
+                    const unsigned long long nx = (unsigned long long)__double_as_longlong(x);
+                    const unsigned long long pv = atomicCAS(q, o, nx);
+                    if (pv == o) break;
+                    o = pv;
+                }
+            }
+            return;
+        }
+        old = prev;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint64_t* resp, const uint32_t* nresp,
+                                                       const uint32_t* owner)
+{
+    extern __shared__ uint32_t s_new2[];
+    __shared__ unsigned long long s_stats[4];
+    for (int w = threadIdx.x; w < (a.ring + 31) / 32; w += blockDim.x) s_new2[w] = 0;
+    if (threadIdx.x < 4) s_stats[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t n = *nresp;
+    const uint32_t par = (uint32_t)(a.g & 1);
+    const uint32_t claim_hi = kClaim | (par << 30);
+    const ctp_t tpa = const_tp(a.tp);
+    unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) {
+        const uint64_t ent = resp[x];
+        const uint32_t r = (uint32_t)ent, m = (uint32_t)(ent >> 32);
+        const uint8_t ds = a.dstate[r];
+        if (!(ds & GSIM_DS_ACCEPT)) { n_gray++; continue; }        // AcceptFrom
+        n_acc++;
+        const uint32_t p = a.col[r], i = owner[r];
+        const int32_t t = (int32_t)a.mtopic[m];
+        const ctp_t tp = tpa + t;
+        const bool inv = a.minv[m] != 0;
+        const int64_t ir = (int64_t)t * a.E + r;
+        const bool sc = tp->scored && (ds & GSIM_DS_TRACKED);
+        const uint8_t tf = a.tflags[ir];
+        const int64_t window = tp->mesh_message_deliveries_window_ns;
+        uint64_t* cellp = a.cell + (int64_t)m * a.N + p;
+        const uint64_t c = *cellp;
+        const uint32_t hi = (uint32_t)(c >> 32);
+        int64_t seen_round = -1;
+        if (c != kUnseen64) {
+            if (!(hi & kClaim)) seen_round = hi;
+            else if (((hi >> 30) & 1u) != par) seen_round = a.g - 1;
+        }
+        if (seen_round < 0 && (c == kUnseen64 || (hi & kEdgeMask) > r)) {
+            uint32_t lo = i;
+            if (sc && !inv) {
+                lo |= kCreditFirst;
+                if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo |= kCreditMesh;
+            }
+            const uint64_t v = ((uint64_t)(claim_hi | r) << 32) | lo;
+            const uint64_t prev = __hip_atomic_fetch_min(cellp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (prev == kUnseen64) {
+                n_first++;
+                atomicOr(&s_new2[m >> 5], 1u << (m & 31));
+            }
+        }
+        if (!sc) continue;
+        if (inv) {
+            atomicAdd(&a.invalid[ir], 1.0);                           // markInvalidMessageDelivery
+        } else if (tf & GSIM_TF_IN_MESH) {
+            const bool in_window = seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window) : (window >= 0);
+            if (in_window) atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], tp->mesh_message_deliveries_cap);
+        }
+    }
+    n_acc = wave_sum_u64(n_acc);
+    n_gray = wave_sum_u64(n_gray);
+    n_first = wave_sum_u64(n_first);
+    if ((threadIdx.x & 63) == 0 && (n_acc | n_gray)) {
+        atomicAdd(&s_stats[0], n_acc);
+        atomicAdd(&s_stats[1], n_first);
+        atomicAdd(&s_stats[3], n_gray);
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < (a.ring + 31) / 32; w += blockDim.x) {
+        uint32_t bits = s_new2[w];
+        if (!bits) continue;
+        atomicOr(&a.nnew_cur[w], bits);
+        while (bits) {
+            const int q = __ffs(bits) - 1;
+            bits &= bits - 1;
+            atomicMax(&a.slot_last[w * 32 + q], (int32_t)a.g);
+        }
+    }
+    if (threadIdx.x == 0 && (s_stats[0] | s_stats[3])) {
+        atomicAdd(&a.stats[0], s_stats[0]);
+        atomicAdd(&a.stats[1], s_stats[1]);
+        atomicAdd(&a.stats[2], s_stats[0] - s_stats[1]);
+        atomicAdd(&a.stats[3], s_stats[3]);
+    }
+}
+
+// applyIwantPenalties: the promises of ring index q expired before this
+// heartbeat; a promise is broken unless its receiver has seen the message
+// (fulfillPromise at first reception).  Record order: the penalty lands on
+// the promiser's record of the advertiser, rev[e].
+__global__ __launch_bounds__(256) void k_promise_check(uint32_t* prom_q, const uint64_t* cell, const uint32_t* owner,
+                                                       const uint32_t* rev, uint8_t* pen, int64_t E, int64_t N)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride) {
+        const uint32_t slot = prom_q[e];
+        if (slot == 0xFFFFFFFFu) continue;
+        prom_q[e] = 0xFFFFFFFFu;
+        if (cell[(int64_t)slot * N + owner[e]] == kUnseen64) pen[rev[e]] = (uint8_t)(pen[rev[e]] + 1);
+    }
+}
+
 __global__ void k_seen_view(const uint64_t* cell, uint32_t* out, int64_t n)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -480,6 +817,8 @@ static void dl_free(Deliver* d)
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
+    f(d->d_slot_last); f(d->d_ihave); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_prom); f(d->d_pcand);
+    f(d->d_behaviour);
     delete d;
 }
 
@@ -501,6 +840,13 @@ bool deliver_field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r)
 
 static int nnew_words(const Deliver* d) { return (d->cfg.ring + 31) / 32; }
 
+static int grid_peers(int64_t n)
+{
+    const int64_t waves = (n + 63) / 64;
+    return (int)std::max<int64_t>((waves + 3) / 4, 1);
+}
+
+
 static RoundArgs make_round_args(gsim_handle* h, int64_t g)
 {
     Deliver* d = h->dl;
@@ -519,14 +865,102 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.nnew_cur = d->d_nnew + (size_t)(g & 1) * w;
     a.stats = d->d_stats;
     a.diag = h->diag;
+    a.slot_last = d->d_slot_last;
+    a.err = d->d_nresp;
+    a.reuse_guard = (std::max(h->gp.history_gossip, h->gp.history_length) + d->prom_ticks + 2) * d->cfg.rounds;
     return a;
 }
 
-static int grid_peers(int64_t n)
+bool deliver_gossip_view(gsim_handle* h, GossipView* v)
 {
-    const int64_t waves = (n + 63) / 64;
-    return (int)std::max<int64_t>((waves + 3) / 4, 1);
+    Deliver* d = h->dl;
+    if (!d) return false;
+    v->lastput = d->d_lastput;
+    v->ihave = d->d_ihave;
+    v->gstate = d->d_gstate;
+    return true;
 }
+
+static int64_t round_time_host(const Deliver* d, int64_t g)
+{
+    const int64_t R = d->cfg.rounds, hb = d->cfg.heartbeat_ns;
+    return d->cfg.t0_ns + (g / R) * hb + (g % R + 1) * hb / (R + 1);
+}
+
+// applyIwantPenalties before the heartbeat at `now`: every promise ring index
+// whose promises expired (expire.Before(now)) is checked and emptied; the
+// penalties reach bp in the refresh pass that follows (before scoring).
+int deliver_promise_check(gsim_handle* h, int64_t now)
+{
+    Deliver* d = h->dl;
+    if (!d) return GSIM_OK;
+    for (int q = 0; q < d->prom_ticks; ++q) {
+        const int64_t made = d->prom_made[(size_t)q];
+        if (made < 0) continue;
+        const int64_t expire = round_time_host(d, made * d->cfg.rounds) + h->gp.iwant_followup_time_ns;
+        if (!(expire < now)) continue;
+        hipLaunchKernelGGL(k_promise_check, dim3(std::min<int64_t>((h->e + 255) / 256, 16384)), dim3(256), 0,
+                           h->stream, d->d_prom + (size_t)q * (size_t)h->e, (const uint64_t*)d->d_cell,
+                           (const uint32_t*)h->d_owner, (const uint32_t*)h->d_rev, h->d_pen, h->e, h->n);
+        d->prom_made[(size_t)q] = -1;
+        int rc = hip_check(h, hipGetLastError(), "k_promise_check");
+        if (rc) return rc;
+    }
+    return GSIM_OK;
+}
+
+// The heartbeat's emitGossip writes fresh IHAVE marks.
+int deliver_heartbeat_begin(gsim_handle* h, uint64_t tick)
+{
+    Deliver* d = h->dl;
+    if (!d) return GSIM_OK;
+    hipError_t e = hipMemsetAsync(d->d_ihave, 0, (size_t)h->e * (size_t)std::max(1, h->t), h->stream);
+    d->ihave_tick = (int64_t)tick;
+    return hip_check(h, e, "ihave reset");
+}
+
+// Control round 0: handleIHave (+ the advertisers' handleIWant) for the
+// heartbeat's IHAVE marks.
+static int launch_ihave(gsim_handle* h, int64_t g)
+{
+    Deliver* d = h->dl;
+    const int64_t tick = g / d->cfg.rounds;
+    if (d->ihave_tick != tick) return GSIM_OK;
+    d->ihave_tick = -1;
+    if (h->gp.max_ihave_messages < 1 || h->gp.max_ihave_length < 1) return GSIM_OK;
+    IhArgs a{};
+    a.N = h->n; a.E = h->e; a.T = h->t; a.ring = d->cfg.ring; a.R = d->cfg.rounds;
+    a.g = g; a.tick = tick;
+    a.lo_round = (int32_t)std::max<int64_t>((tick - h->gp.history_gossip) * d->cfg.rounds, 0);
+    a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.rev = h->d_rev; a.sub = h->d_sub;
+    a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv;
+    a.cell = d->d_cell; a.slot_last = d->d_slot_last;
+    a.ihave = d->d_ihave; a.gstate = d->d_gstate; a.behaviour = d->d_behaviour;
+    a.pcand = d->d_pcand; a.prom = d->d_prom; a.P = d->prom_ticks;
+    a.prom_idx = (int32_t)(tick % d->prom_ticks);
+    if (d->prom_made[(size_t)a.prom_idx] >= 0) {
+        h->err = "IWANT promise ring index still pending (refresh_scores must run every heartbeat)";
+        return GSIM_ESTATE;
+    }
+    d->prom_made[(size_t)a.prom_idx] = tick;
+    a.resp = d->d_resp; a.nresp = d->d_nresp; a.resp_cap = d->resp_cap;
+    a.respond = h->gp.gossip_retransmission >= 1;
+    a.seed = h->x ? gsim_get_seed(h) : 0;
+    const size_t lds = (((size_t)d->cfg.ring + 3) & ~(size_t)3) * sizeof(uint16_t) + 4 * kRespStage * sizeof(uint64_t);
+    const int grid = grid_peers(h->n);
+    ProfScope ps(h, GSIM_K_GOSSIP);
+    hipError_t e = hipMemsetAsync(d->d_nresp, 0, 2 * sizeof(uint32_t), h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "nresp reset");
+    if (h->max_degree <= 16)
+        hipLaunchKernelGGL(k_ihave<16>, dim3(grid), dim3(256), lds, h->stream, a);
+    else if (h->max_degree <= 32)
+        hipLaunchKernelGGL(k_ihave<32>, dim3(grid), dim3(256), lds, h->stream, a);
+    else
+        hipLaunchKernelGGL(k_ihave<64>, dim3(grid), dim3(256), lds, h->stream, a);
+    d->resp_round = g + 2;
+    return hip_check(h, hipGetLastError(), "k_ihave");
+}
+
 
 int deliver_flush(gsim_handle* h)
 {
@@ -572,6 +1006,12 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
         h->err = "too many edges or peers for the seen-set claim encoding (< 2^30 - 1)";
         return GSIM_ERANGE;
     }
+    if (cfg->ring > h->gp.max_ihave_length) {
+        // a gossip window could then exceed MaxIHaveLength ids: the per-peer
+        // IHAVE / IWANT truncation (gossipsub.go:679-690, 1766-1771) is not modeled
+        h->err = "ring larger than MaxIHaveLength (IHAVE/IWANT truncation is not modeled on the device)";
+        return GSIM_ERANGE;
+    }
     (void)hipStreamSynchronize(h->stream);
     free_deliver(h);
     Deliver* d = new Deliver();
@@ -590,6 +1030,23 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_lastput, T * N * 4);
     A((void**)&d->d_nnew, 2 * words * 4);
     A((void**)&d->d_stats, 4 * 8);
+    // promises live from round 0 of tick k until the first heartbeat after
+    // round_time(kR) + IWantFollowupTime; one spare ring index
+    {
+        const int64_t hb = cfg->heartbeat_ns;
+        const int64_t span = hb / (cfg->rounds + 1) + h->gp.iwant_followup_time_ns;
+        d->prom_ticks = (int32_t)std::min<int64_t>(span / hb + 2, 64);
+        d->prom_made.assign((size_t)d->prom_ticks, -1);
+    }
+    d->resp_cap = cfg->max_arrivals > 0 ? cfg->max_arrivals : std::max<int64_t>(8 * h->n, 1 << 20);
+    A((void**)&d->d_slot_last, ring * 4);
+    A((void**)&d->d_ihave, T * (size_t)h->e);
+    A((void**)&d->d_gstate, (size_t)h->e);
+    A((void**)&d->d_resp, (size_t)d->resp_cap * 8);
+    A((void**)&d->d_nresp, 4 * 4);
+    A((void**)&d->d_prom, (size_t)d->prom_ticks * (size_t)h->e * 4);
+    A((void**)&d->d_pcand, (size_t)h->e * 8);
+    A((void**)&d->d_behaviour, N);
     if (e != hipSuccess) {
         dl_free(d);
         h->err = std::string("message ring allocation: ") + hipGetErrorString(e);
@@ -603,6 +1060,13 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     if (e == hipSuccess) e = hipMemsetAsync(d->d_minv, 0, ring, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_nnew, 0, 2 * words * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_stats, 0, 4 * 8, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_slot_last, 0xFF, ring * 4, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_ihave, 0, T * (size_t)h->e, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_gstate, 0, (size_t)h->e, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_nresp, 0, 4 * 4, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_prom, 0xFF, (size_t)d->prom_ticks * (size_t)h->e * 4, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_pcand, 0xFF, (size_t)h->e * 8, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_behaviour, 0, N, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     return hip_check(h, e, "gsim_msgs_init");
 }
@@ -701,6 +1165,16 @@ int gsim_round(gsim_handle* h, int64_t round)
     }
     rc = hip_check(h, hipGetLastError(), "k_send");
     if (rc) return rc;
+    if (d->resp_round == round) {
+        // the messages handleIWant sent in control round 1 arrive with this round's copies
+        ProfScope ps(h, GSIM_K_GOSSIP);
+        const size_t lds2 = (size_t)nnew_words(d) * 4;
+        hipLaunchKernelGGL(k_gossip_deliver, dim3(2048), dim3(256), lds2, h->stream, a, (const uint64_t*)d->d_resp,
+                           (const uint32_t*)d->d_nresp, (const uint32_t*)h->d_owner);
+        d->resp_round = -1;
+        rc = hip_check(h, hipGetLastError(), "k_gossip_deliver");
+        if (rc) return rc;
+    }
     if (!lazy) {
         rc = deliver_flush(h);
         if (rc) return rc;
@@ -710,6 +1184,10 @@ int gsim_round(gsim_handle* h, int64_t round)
         // rounds >= 2 of a heartbeat have an empty control inbox: handling
         // PRUNE replies (round 1) emits nothing
         rc = gsim_handle_control(h, r, a.now);
+        if (rc) return rc;
+    }
+    if (r == 0) {
+        rc = launch_ihave(h, round);
         if (rc) return rc;
     }
     d->next_round = round + 1;
@@ -723,11 +1201,29 @@ int gsim_msg_stats(gsim_handle* h, int64_t* out4)
     Deliver* d = h->dl;
     if (!d) { h->err = "gsim_msgs_init not called"; return GSIM_ESTATE; }
     unsigned long long s[4];
+    uint32_t err[4] = {0, 0, 0, 0};
     hipError_t e = hipMemcpyAsync(s, d->d_stats, sizeof(s), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(err, d->d_nresp, sizeof(err), hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return hip_check(h, e, "gsim_msg_stats");
     for (int k = 0; k < 4; ++k) out4[k] = (int64_t)s[k];
+    if (err[1]) { h->err = "IWANT responses overflowed their queue (raise gsim_msg_config.max_arrivals)"; return GSIM_ERANGE; }
+    if (err[2]) {
+        h->err = "a ring slot was republished while its message could still be gossiped or promised (raise ring)";
+        return GSIM_ESTATE;
+    }
     return GSIM_OK;
+}
+
+int gsim_set_peer_behaviour(gsim_handle* h, const uint8_t* flags)
+{
+    if (!h || !flags) return GSIM_EINVAL;
+    if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
+    Deliver* d = h->dl;
+    if (!d) { h->err = "gsim_msgs_init not called"; return GSIM_ESTATE; }
+    hipError_t e = hipMemcpyAsync(d->d_behaviour, flags, (size_t)h->n, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    return hip_check(h, e, "gsim_set_peer_behaviour");
 }
 
 }  // extern "C"

@@ -21,27 +21,6 @@
 
 using namespace gsim;
 
-// Exact Go int64 division (truncation toward zero) of meshTime by a positive
-// TimeInMeshQuantum (score.go:287): an fp64 quotient estimate corrected by the
-// exact integer remainder.  Cheaper in VALU and registers than the generic
-// 64-bit division expansion; the result is identical for every input.
-__device__ __forceinline__ int64_t div_trunc_pos(int64_t n, int64_t d)
-{
-    const bool neg = n < 0;
-    const uint64_t un = neg ? (uint64_t)0 - (uint64_t)n : (uint64_t)n;
-    const uint64_t ud = (uint64_t)d;
-    uint64_t q = (uint64_t)((double)un / (double)ud);
-    // the estimate is within a few units of the true quotient; fix it exactly
-    while (q * ud > un) --q;
-    while (un - q * ud >= ud) ++q;
-    return neg ? -(int64_t)q : (int64_t)q;
-}
-
-__device__ __forceinline__ int64_t go_div(int64_t n, int64_t d)
-{
-    return d > 0 ? div_trunc_pos(n, d) : n / d;
-}
-
 // ---------------------------------------------------------------------------
 // Kernel 1:peerScore.refreshScores (score.go:504-565) fused with
 // peerScore.score (score.go:265-342).  One thread per record (record order,
@@ -60,6 +39,7 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
         const uint8_t st = a.estate[e];
         if (!(st & GSIM_ES_TRACKED)) {
             if (SCORE) a.score[e] = 0.0;
+            if (REFRESH && a.pen[e]) a.pen[e] = 0;      // AddPenalty without peerStats: no-op
             continue;
         }
         const bool conn = (st & GSIM_ES_CONNECTED) != 0;
@@ -68,6 +48,7 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
             a.estate[e] = 0;
             a.bp[e] = 0.0;
             a.expire[e] = 0;
+            a.pen[e] = 0;
             for (int32_t t = 0; t < a.T; ++t) {
                 const int64_t i = (int64_t)t * a.E + e;
                 a.first[i] = 0.0; a.meshd[i] = 0.0; a.fail[i] = 0.0; a.invalid[i] = 0.0; a.mcnt[i] = 0;
@@ -143,6 +124,12 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
             if (x < a.dtz) x = 0.0;
             if (x != bp) { bp = x; a.bp[e] = x; }
         }
+        if (REFRESH) {
+            // broken IWANT promises of the heartbeat that follows this decay
+            // (applyIwantPenalties -> AddPenalty, gossipsub.go:1620-1625)
+            const uint8_t pn = a.pen[e];
+            if (pn) { bp = bp + (double)pn; a.bp[e] = bp; a.pen[e] = 0; }
+        }
         if (SCORE) {
             if (a.topic_cap > 0 && score > a.topic_cap) score = a.topic_cap;
             const double p5 = a.p5[a.owner[e]];                           // P5 (neighbour = row owner)
@@ -198,7 +185,7 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
         const bool valid = e < a.E;
         // per-edge inputs are loaded unconditionally (not behind estate) so
         // they share one memory round trip with the first topic chunk
-        uint8_t st = 0;
+        uint8_t st = 0, pn = 0;
         int64_t expire = 0;
         double bp = 0.0, p6 = 0.0, p5 = 0.0;
         uint32_t c = 0;
@@ -206,6 +193,7 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
             st = a.estate[e];
             expire = a.expire[e];
             bp = a.bp[e];
+            if (REFRESH) pn = a.pen[e];
             if (SCORE) {
                 p6 = a.p6[e];
                 c = a.owner[e];   // the neighbour this record is about
@@ -324,10 +312,12 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
         if (!valid) continue;
         if (!tracked) {
             if (SCORE) a.score[e] = 0.0;
+            if (pn) a.pen[e] = 0;                             // AddPenalty without peerStats: no-op
         } else if (purge) {                                  // score.go:512-516
             a.estate[e] = 0;
             a.bp[e] = 0.0;
             a.expire[e] = 0;
+            if (pn) a.pen[e] = 0;
             *a.purged = 1;
             if (SCORE) a.score[e] = 0.0;
         } else {
@@ -335,6 +325,11 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
                 double x = bp * a.bp_decay;
                 if (x < a.dtz) x = 0.0;
                 if (x != bp) { bp = x; a.bp[e] = x; }
+            }
+            if (pn) {   // broken IWANT promises (applyIwantPenalties, gossipsub.go:1620-1625)
+                bp = bp + (double)pn;
+                a.bp[e] = bp;
+                a.pen[e] = 0;
             }
             if (SCORE) {
                 if (a.topic_cap > 0 && score > a.topic_cap) score = a.topic_cap;
@@ -600,7 +595,7 @@ void free_graph(gsim_handle* h)
     dfree(h->d_first); dfree(h->d_meshd); dfree(h->d_fail); dfree(h->d_invalid);
     dfree(h->d_graft); dfree(h->d_mtime); dfree(h->d_tflags); dfree(h->d_mflags);
     dfree(h->d_bp); dfree(h->d_estate); dfree(h->d_expire); dfree(h->d_p6); dfree(h->d_score);
-    dfree(h->d_backoff); dfree(h->d_rstate); dfree(h->d_dstate); dfree(h->d_mcnt);
+    dfree(h->d_backoff); dfree(h->d_rstate); dfree(h->d_dstate); dfree(h->d_mcnt); dfree(h->d_pen);
     h->bytes_allocated = 0;
     h->n = h->e = 0;
 }
@@ -624,7 +619,7 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     a.mcnt = h->d_mcnt;
     a.graft = h->d_graft; a.mtime = h->d_mtime; a.tflags = h->d_tflags;
     a.mflags = h->d_mflags; a.rstate = h->d_rstate; a.rev = h->d_rev;
-    a.bp = h->d_bp; a.estate = h->d_estate; a.expire = h->d_expire; a.p6 = h->d_p6; a.score = h->d_score;
+    a.bp = h->d_bp; a.pen = h->d_pen; a.estate = h->d_estate; a.expire = h->d_expire; a.p6 = h->d_p6; a.score = h->d_score;
     a.now = now;
     a.purged = h->d_flags;
     a.diag = h->diag;
@@ -679,6 +674,7 @@ static void launch_score_kernel(gsim_handle* h, const ScoreArgs& a)
 int launch_refresh_scores(gsim_handle* h, int64_t now)
 {
     int rc0 = deliver_flush(h);   // the last round's first deliveries precede the decay
+    if (!rc0) rc0 = deliver_promise_check(h, now);   // broken promises of this heartbeat
     if (rc0) return rc0;
     ScoreArgs a = make_score_args(h, now);
     if (h->p6_dirty) {
@@ -984,6 +980,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     rc = rc ? rc : dalloc(h, &h->d_backoff, ET);
     rc = rc ? rc : dalloc(h, &h->d_rstate, E);
     rc = rc ? rc : dalloc(h, &h->d_dstate, E);
+    rc = rc ? rc : dalloc(h, &h->d_pen, E);
     rc = rc ? rc : dalloc(h, &h->d_mcnt, ET);
     rc = rc ? rc : dalloc(h, &h->d_bp, E);
     rc = rc ? rc : dalloc(h, &h->d_estate, E);
@@ -1023,6 +1020,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     zero(h->d_tflags, (size_t)ET);
     zero(h->d_mflags, (size_t)ET);
     zero(h->d_mcnt, (size_t)ET);
+    zero(h->d_pen, (size_t)E);
     zero(h->d_backoff, sizeof(int64_t) * (size_t)ET);
     zero(h->d_bp, sizeof(double) * (size_t)E);
     zero(h->d_expire, sizeof(int64_t) * (size_t)E);

@@ -28,6 +28,7 @@ struct ScoreArgs {
     uint8_t* rstate;           // router connected bit, edge order (fill)
     const uint32_t* rev;
     double* bp;
+    uint8_t* pen;              // pending P7 penalty counts, added after the decay
     uint8_t* estate;
     int64_t* expire;
     const double* p6;
@@ -73,6 +74,27 @@ __device__ __forceinline__ double apply_incs(double x, uint32_t n, double cap)
         if (x > cap) { x = cap; break; }   // further increments keep the cap
     }
     return x;
+}
+
+// Exact Go int64 division (truncation toward zero) of meshTime by a positive
+// TimeInMeshQuantum (score.go:287): an fp64 quotient estimate corrected by the
+// exact integer remainder.  Cheaper in VALU and registers than the generic
+// 64-bit division expansion; the result is identical for every input.
+__device__ __forceinline__ int64_t div_trunc_pos(int64_t n, int64_t d)
+{
+    const bool neg = n < 0;
+    const uint64_t un = neg ? (uint64_t)0 - (uint64_t)n : (uint64_t)n;
+    const uint64_t ud = (uint64_t)d;
+    uint64_t q = (uint64_t)((double)un / (double)ud);
+    // the estimate is within a few units of the true quotient; fix it exactly
+    while (q * ud > un) --q;
+    while (un - q * ud >= ud) ++q;
+    return neg ? -(int64_t)q : (int64_t)q;
+}
+
+__device__ __forceinline__ int64_t go_div(int64_t n, int64_t d)
+{
+    return d > 0 ? div_trunc_pos(n, d) : n / d;
 }
 
 // Topic parameters are read-only for a kernel's lifetime.  Reading them
@@ -163,6 +185,7 @@ struct gsim_handle {
     int64_t* d_expire = nullptr;
     double* d_p6 = nullptr;
     double* d_score = nullptr;
+    uint8_t* d_pen = nullptr;         // pending broken-promise penalties (applyIwantPenalties), record order
     uint8_t* d_dstate = nullptr;      // delivery state per edge, derived (GSIM_DS_*)
     uint64_t score_version = 1, acc_version = 0;
 
@@ -214,4 +237,15 @@ bool extra_field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r);
 void free_deliver(gsim_handle* h);
 bool deliver_field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r);
 int deliver_flush(gsim_handle* h);                  // commit the last round's claims (if any)
+
+// What the heartbeat's emitGossip needs from the message state.
+struct GossipView {
+    const int32_t* lastput;   // [T][N] tick of the newest mcache.Put
+    uint8_t* ihave;           // [T][E] receiver edge: IHAVE(topic) from col[e] this heartbeat
+    uint8_t* gstate;          // [E] edge order: owner's snapshot score of col >= gossipThreshold
+};
+bool deliver_gossip_view(gsim_handle* h, GossipView* v);   // false before gsim_msgs_init
+int deliver_promise_check(gsim_handle* h, int64_t now);    // broken promises -> pending P7
+int deliver_heartbeat_begin(gsim_handle* h, uint64_t tick); // fresh IHAVE marks
+uint64_t gsim_get_seed(const gsim_handle* h);              // heartbeat.hip
 int deliver_read_seen(gsim_handle* h, void* dst);

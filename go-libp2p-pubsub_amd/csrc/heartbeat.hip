@@ -50,6 +50,16 @@ struct HbArgs {
     uint64_t opp_ticks;
     int64_t prune_backoff, graft_flood;
     double opp_threshold;
+    // emitGossip (gossipsub.go:1711-1775); gossip == false before gsim_msgs_init
+    bool gossip;
+    const int32_t* lastput;    // [T][N]
+    uint8_t* ihave;            // [T][E] receiver edge
+    uint8_t* gstate;           // [E] edge order: snapshot score >= gossipThreshold
+    double gossip_thr, gossip_factor;
+    int32_t dlazy, hist_gossip;
+    // live Score(p) for emitGossip (score.go:265-342)
+    const double *first, *invalid, *p5, *p6;
+    double topic_cap, w5, w6, bp_thr, w7;
 };
 
 namespace {
@@ -138,6 +148,84 @@ __device__ __forceinline__ void stats_prune(const HbArgs& a, bool tracked, bool 
     fl &= (uint8_t)~GSIM_TF_IN_MESH;
 }
 
+// peerScore.score of one record (score.go:265-342), in the score pass's
+// operation order: the live Score(p) emitGossip uses after this heartbeat's
+// Graft/Prune changed the record (gossipsub.go:1734).
+__device__ double score_of_record(const HbArgs& a, uint32_t rv, uint32_t col)
+{
+    if (!(a.estate[rv] & GSIM_ES_TRACKED)) return 0.0;
+    double score = 0.0;
+    for (int32_t t = 0; t < a.T; ++t) {
+        const ctp_t tp = const_tp(a.tp) + t;
+        if (!tp->scored) continue;
+        const int64_t i = (int64_t)t * a.E + rv;
+        const uint8_t fl = a.tflags[i];
+        const double meshd = apply_incs(a.meshd[i], a.mcnt[i], tp->mesh_message_deliveries_cap);
+        double ts = 0.0;
+        if (fl & GSIM_TF_IN_MESH) {                                   // P1
+            double p1 = 0.0;
+            if (tp->time_in_mesh_quantum_ns != 0) p1 = (double)go_div(a.mtime[i], tp->time_in_mesh_quantum_ns);
+            if (p1 > tp->time_in_mesh_cap) p1 = tp->time_in_mesh_cap;
+            ts += p1 * tp->time_in_mesh_weight;
+        }
+        ts += a.first[i] * tp->first_message_deliveries_weight;        // P2
+        if (fl & GSIM_TF_ACTIVE) {                                     // P3
+            if (meshd < tp->mesh_message_deliveries_threshold) {
+                const double deficit = tp->mesh_message_deliveries_threshold - meshd;
+                const double p3 = deficit * deficit;
+                ts += p3 * tp->mesh_message_deliveries_weight;
+            }
+        }
+        ts += a.fail[i] * tp->mesh_failure_penalty_weight;             // P3b
+        const double inval = a.invalid[i];
+        const double p4 = inval * inval;                               // P4
+        ts += p4 * tp->invalid_message_deliveries_weight;
+        score += ts * tp->topic_weight;
+    }
+    if (a.topic_cap > 0 && score > a.topic_cap) score = a.topic_cap;
+    score += a.p5[col] * a.w5;                                         // P5
+    score += a.p6[rv] * a.w6;                                          // P6
+    const double bp = a.bp[rv];
+    if (bp > a.bp_thr) {                                               // P7
+        const double excess = bp - a.bp_thr;
+        const double p7 = excess * excess;
+        score += p7 * a.w7;
+    }
+    return score;
+}
+
+// emitGossip's target choice over the list L = candidates (key P_GOSSIP)
+// followed, when fewer than Dlo, by fill instances (key P_GOSSIP_DUP) of
+// the topic peers taken in P_GOSSIP_FILL order (gossipsub.go:1739-1762):
+// target = max(Dlazy, int(GossipFactor * |L|)), all of L if that is not
+// smaller, else the target smallest keys.  A lane is selected if any of its
+// instances is.  Must be called by the whole wave.
+__device__ bool gossip_targets(const HbArgs& a, bool cand, bool tpeer, uint32_t obs, int32_t t, uint32_t col,
+                               uint32_t pos)
+{
+    const int c = __popcll(__ballot(cand));
+    bool dup = false;
+    if (c < a.Dlo) dup = select_smallest(a, tpeer, a.Dlo - c, obs, t, P_GOSSIP_FILL, col, pos);
+    const int n = c + __popcll(__ballot(dup));
+    if (n == 0) return false;
+    int target = a.dlazy;
+    const int factor = (int)(a.gossip_factor * (double)n);
+    if (factor > target) target = factor;
+    if (target >= n) return cand || dup;
+    uint64_t k1 = cand ? hb_key(a, obs, t, P_GOSSIP, col, pos) : ~0ull;
+    uint64_t k2 = dup ? hb_key(a, obs, t, P_GOSSIP_DUP, col, pos) : ~0ull;
+    bool sel = false;
+    for (int q = 0; q < target; ++q) {
+        const uint64_t mine = k1 < k2 ? k1 : k2;
+        const uint64_t mn = wave_min_u64(mine);
+        if (mine == mn) {
+            sel = true;
+            if (k1 < k2) k1 = ~0ull; else k2 = ~0ull;
+        }
+    }
+    return sel;
+}
+
 }  // namespace
 
 // One wavefront = one observer's heartbeat (gossipsub.go:1345-1557).
@@ -158,6 +246,11 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
         const double S = valid ? a.score[rv] : 0.0;
         const uint64_t subj = valid ? a.sub[col] : 0ull;
         const uint64_t subi = a.sub[obs];
+        // live score for emitGossip: the snapshot until this heartbeat's
+        // Graft/Prune touches one of the lane's records
+        double S_live = S;
+        bool dirty = false;
+        if (a.gossip && valid) a.gstate[e] = S >= a.gossip_thr ? 1 : 0;
 
         // clearBackoff every 15 ticks (gossipsub.go:1627-1646)
         if (a.tick % 15 == 0 && valid) {
@@ -207,6 +300,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
 
             auto prune = [&]() {
                 stats_prune(a, tracked, scored, thr, mcap, sf);
+                dirty |= tracked && scored;
                 fl &= (uint8_t)~GSIM_TF_MESH;
                 m = false;
                 need_bo();
@@ -216,6 +310,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             };
             auto graft = [&]() {
                 stats_graft(a, tracked, scored, sf);
+                dirty |= tracked && scored;
                 fl |= GSIM_TF_MESH;
                 m = true;
                 ctl |= GSIM_CTL_GRAFT;
@@ -313,6 +408,21 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
                 if (fl != fl0) a.mflags[i] = fl;
                 sf.store(a);
                 if (bo_dirty) a.backoff[i] = bo;
+            }
+
+            // emitGossip(topic, mesh) (gossipsub.go:1554-1556, 1711-1775):
+            // only if GetGossipIDs(topic) is non-empty, i.e. this peer put a
+            // message of the topic in the last HistoryGossip ticks
+            if (a.gossip && a.lastput[(int64_t)t * a.N + obs] >= (int64_t)a.tick - a.hist_gossip) {
+                if (__ballot(dirty)) {
+                    if (dirty) S_live = score_of_record(a, rv, col);
+                    dirty = false;
+                }
+                const bool gcand = tpeer && !m && S_live >= a.gossip_thr;
+                if (gossip_targets(a, gcand, tpeer, (uint32_t)obs, t, col, pos) && valid)
+                    a.ihave[(int64_t)t * a.E + rv] = 1;          // enqueueGossip: IHAVE in the receiver's inbox
+            }
+            if (valid) {
                 if (ctl) {
                     const int64_t r = (int64_t)t * a.E + a.rev[e];
                     a.ctl_out[r] = (uint8_t)(a.ctl_out[r] | ctl);
@@ -477,6 +587,14 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.opp_peers = h->gp.opportunistic_graft_peers; a.opp_ticks = h->gp.opportunistic_graft_ticks;
     a.prune_backoff = h->gp.prune_backoff_ns; a.graft_flood = h->gp.graft_flood_threshold_ns;
     a.opp_threshold = h->th.opportunistic_graft_threshold;
+    GossipView gv{};
+    a.gossip = deliver_gossip_view(h, &gv);
+    a.lastput = gv.lastput; a.ihave = gv.ihave; a.gstate = gv.gstate;
+    a.gossip_thr = h->th.gossip_threshold; a.gossip_factor = h->gp.gossip_factor;
+    a.dlazy = h->gp.dlazy; a.hist_gossip = h->gp.history_gossip;
+    a.first = h->d_first; a.invalid = h->d_invalid; a.p5 = h->d_p5; a.p6 = h->d_p6;
+    a.topic_cap = h->pp.topic_score_cap; a.w5 = h->pp.app_specific_weight; a.w6 = h->pp.ip_colocation_factor_weight;
+    a.bp_thr = h->pp.behaviour_penalty_threshold; a.w7 = h->pp.behaviour_penalty_weight;
     return a;
 }
 
@@ -495,6 +613,8 @@ static int check_degree(gsim_handle* h)
     return GSIM_OK;
 }
 
+uint64_t gsim_get_seed(const gsim_handle* h) { return h->x ? h->x->seed : 0; }
+
 extern "C" {
 
 int gsim_set_seed(gsim_handle* h, uint64_t seed)
@@ -512,6 +632,7 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     int rc = check_degree(h);
     if (rc) return rc;
     rc = deliver_flush(h);
+    if (!rc) rc = deliver_heartbeat_begin(h, tick);
     if (rc) return rc;
     // heartbeat output goes to the parity-0 inbox, read by control round 0
     HbArgs a = make_hb_args(h, tick, now, 1);

@@ -47,7 +47,19 @@ enum Purpose : uint32_t {
     P_GOSSIP = 6,      // emitGossip target shuffle            gossipsub.go:1758
     P_IWANT = 7,       // shuffleStrings(iwantlst)             gossipsub.go:687
     P_PROMISE = 8,     // rand.Intn in AddPromise              gossip_tracer.go:53
+    P_GOSSIP_FILL = 9, // map order of emitGossip's Dlo fill   gossipsub.go:1739-1748
+    P_GOSSIP_DUP = 10, // shuffle key of a fill duplicate      gossipsub.go:1758
 };
+
+// Key of a choice made per (observer, other peer, message slot): the other
+// peer goes into the Philox key's high word (oracle_gossip.c okey_pair).
+GSIM_HD uint64_t pair_key(uint64_t seed, uint32_t tick, uint32_t observer, uint32_t topic, uint32_t purpose,
+                          uint32_t slot, uint32_t other)
+{
+    u32x4 r = philox4x32_10(tick, observer, (topic << 8) | purpose, slot, (uint32_t)seed,
+                            (uint32_t)(seed >> 32) ^ other);
+    return ((uint64_t)r.x << 32) | slot;
+}
 
 // 64-bit selection key: 32 random bits above the item's row position, so keys
 // are unique within a row and ties cannot occur.

@@ -102,7 +102,8 @@ MSG_DTYPE = [("id", "<u8"), ("topic", "<u4"), ("origin", "<u4"), ("invalid", "u1
 UNSEEN = 0xFFFFFFFF
 
 KERNEL_CLASSES = ["refresh_score", "score", "ip_colocation", "heartbeat", "control", "publish", "send",
-                  "commit", "accept"]
+                  "commit", "accept", "gossip"]
+BEHAVE_IGNORE_IWANT = 0x01
 
 SIGNATURES = [
     ("gsim_default_gossipsub_params", None, [POINTER(CGossipSubParams)]),
@@ -146,6 +147,7 @@ SIGNATURES = [
     ("gsim_publish", c_int32, [c_void_p, c_void_p, c_int32, c_int64]),
     ("gsim_round", c_int32, [c_void_p, c_int64]),
     ("gsim_msg_stats", c_int32, [c_void_p, c_void_p]),
+    ("gsim_set_peer_behaviour", c_int32, [c_void_p, c_void_p]),
     ("gsim_profile", c_int32, [c_void_p, c_int32]),
     ("gsim_profile_read", c_int32, [c_void_p, c_void_p, c_void_p, c_int32]),
 ]

@@ -247,6 +247,11 @@ class Engine:
         """One propagation round for the whole network (gsim_round)."""
         self._check(self.lib.gsim_round(self.h, int(rnd)))
 
+    def set_peer_behaviour(self, flags: np.ndarray):
+        """Per-peer adversarial behaviour (gsim_set_peer_behaviour)."""
+        f = np.ascontiguousarray(flags, dtype=np.uint8)
+        self._check(self.lib.gsim_set_peer_behaviour(self.h, _ptr(f)))
+
     def msg_stats(self) -> list:
         out = np.zeros(4, dtype=np.int64)
         self._check(self.lib.gsim_msg_stats(self.h, _ptr(out)))

@@ -241,7 +241,7 @@ typedef struct gsim_msg_config {
     int64_t t0_ns;           /* virtual time of tick 0 */
     int64_t heartbeat_ns;    /* heartbeat interval (GossipSubParams.HeartbeatInterval) */
     int64_t max_frontier;    /* reserved (ignored): the engine keeps no per-copy lists */
-    int64_t max_arrivals;    /* reserved (ignored) */
+    int64_t max_arrivals;    /* capacity of the IWANT response queue per tick (0: max(8 N, 2^20)) */
 } gsim_msg_config;
 
 /* One published message (Topic.Publish, topic.go:217-283, at its origin). */
@@ -272,8 +272,17 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
 int gsim_round(gsim_handle* h, int64_t round);
 /* Cumulative totals since gsim_msgs_init: out4 = {msg-edge deliveries
  * (accepted arrivals, duplicates included), first deliveries, duplicates,
- * graylisted arrivals}.  Synchronizes. */
+ * graylisted arrivals}.  Synchronizes.  GSIM_ERANGE if the IWANT response
+ * queue overflowed, GSIM_ESTATE if a slot was republished while its message
+ * could still be gossiped (results are then incomplete). */
 int gsim_msg_stats(gsim_handle* h, int64_t* out4);
+
+/* Per-peer behaviour flags for adversarial configurations:
+ * GSIM_BEHAVE_IGNORE_IWANT = the peer advertises (IHAVE) but never answers
+ * IWANT (gossipsub_spam_test.go:134-286), so the requesters' promises break
+ * and P7 penalties follow (gossip_tracer.go:79-115, gossipsub.go:1620-1625). */
+#define GSIM_BEHAVE_IGNORE_IWANT 0x01u
+int gsim_set_peer_behaviour(gsim_handle* h, const uint8_t* flags);
 
 /* Aggregate census of the state (the network-wide analogue of the
  * reference's score inspection, score.go:448-500): out8 = {connected scored
@@ -340,6 +349,7 @@ typedef enum gsim_kernel_class {
     GSIM_K_SEND,               /* mesh forwarding: AcceptFrom, seen-set claims, duplicate/invalid counters */
     GSIM_K_COMMIT,             /* seen commit + first-delivery credit */
     GSIM_K_ACCEPT,             /* AcceptFrom verdicts from a new score snapshot */
+    GSIM_K_GOSSIP,             /* handleIHave/handleIWant + IWANT response delivery */
     GSIM_K__COUNT
 } gsim_kernel_class;
 /* Enable (1) or disable (0) recording; clears recorded totals. */

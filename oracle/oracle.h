@@ -72,8 +72,12 @@ typedef struct orc_msgs {
     uint32_t* seen;            /* [ring][N] */
     int32_t*  lastput;         /* [T][N] tick of the newest mcache.Put per (peer, topic) */
     int64_t   stats[4];        /* arrivals, first deliveries, duplicates, graylisted */
-    void*     priv;            /* frontier storage (oracle-owned) */
+    void*     priv;            /* frontier / gossip storage (oracle-owned) */
+    uint64_t* mid;             /* [ring] message id of the slot's current message (or NULL) */
+    const uint8_t* behaviour;  /* [N] ORC_BEHAVE_* per peer, or NULL */
 } orc_msgs;
+
+#define ORC_BEHAVE_IGNORE_IWANT 0x01   /* never answers IWANT (gossipsub_spam_test.go:134-286) */
 
 int64_t orc_round_time(const orc_msgs* m, int64_t g);
 /* Topic.Publish at the origin (pubsub.go:1196-1202 via pushMsg): slot =
@@ -90,6 +94,15 @@ void orc_publish(orc_net* s, orc_msgs* m, uint64_t id, uint32_t topic, uint32_t 
  * is handled.  A message whose slot was reused is no longer forwarded. */
 void orc_round(orc_net* s, orc_msgs* m, int64_t g);
 void orc_msgs_free_priv(orc_msgs* m);
+
+/* ---- gossip (oracle_gossip.c) -------------------------- */
+/* heartbeat (as orc_heartbeat) followed, per joined topic, by emitGossip
+ * (gossipsub.go:1554-1556, 1711-1775); IHAVE are handled in control round 0
+ * and IWANT in control round 1 of the tick by orc_round. */
+void orc_heartbeat_gossip(orc_net* s, orc_msgs* m, uint64_t tick, int64_t now, uint64_t seed);
+/* applyIwantPenalties (gossipsub.go:1620-1625) at heartbeat time now: call
+ * after orc_refresh_scores and before orc_compute_scores of the tick. */
+void orc_gossip_penalties(orc_net* s, orc_msgs* m, int64_t now);
 
 /* ---- gossipsub.go heartbeat / control handling (oracle_net.c) ----------- */
 /* One heartbeat (gossipsub.go:1345-1606) for every observer at tick `tick`

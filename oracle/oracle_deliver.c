@@ -13,27 +13,20 @@
  *     (pubsub.go:1118-1162);
  *  3. the control inbox of the round is handled.
  */
-#include "oracle.h"
+#include "oracle_internal.h"
 
 #include <stdlib.h>
 #include <string.h>
 
 #define UNSEEN 0xFFFFFFFFu
 
-typedef struct fr_ent { uint32_t peer, slot, from; } fr_ent;
-typedef struct arr_ent { uint32_t recv, slot, er; } arr_ent;
-
-typedef struct priv {
-    fr_ent* fr; int64_t nfr, capfr;     /* peers that first-saw a message this round */
-    fr_ent* fp; int64_t nfp, capfp;     /* ... in the previous round: they forward now */
-    arr_ent* ar; int64_t nar, capar;    /* copies forwarded this round */
-} priv;
-
-static priv* P(orc_msgs* m)
+priv* orc_msgs_priv(orc_msgs* m)
 {
     if (!m->priv) m->priv = calloc(1, sizeof(priv));
     return (priv*)m->priv;
 }
+
+static priv* P(orc_msgs* m) { return orc_msgs_priv(m); }
 
 void orc_msgs_free_priv(orc_msgs* m)
 {
@@ -42,6 +35,17 @@ void orc_msgs_free_priv(orc_msgs* m)
     free(p->fr);
     free(p->fp);
     free(p->ar);
+    free(p->gr);
+    free(p->ihave);
+    free(p->iw);
+    if (p->pr) for (int64_t q = 0; q < p->n_alloc; ++q) free(p->pr[q]);
+    free(p->pr);
+    free(p->npr);
+    free(p->cappr);
+    free(p->tx);
+    free(p->slot_last);
+    free(p->cand);
+    free(p->cand_ptr);
     free(p);
     m->priv = NULL;
 }
@@ -88,6 +92,15 @@ void orc_publish(orc_net* s, orc_msgs* m, uint64_t id, uint32_t topic, uint32_t 
     m->topic[slot] = topic;
     m->origin[slot] = origin;
     m->invalid[slot] = invalid;
+    if (m->mid) m->mid[slot] = id;
+    {
+        priv* pv = P(m);
+        if (!pv->slot_last) {
+            pv->slot_last = (int64_t*)malloc(sizeof(int64_t) * (size_t)m->ring);
+            for (int32_t q = 0; q < m->ring; ++q) pv->slot_last[q] = -1;
+        }
+        pv->slot_last[slot] = g;
+    }
     uint32_t* row = m->seen + (int64_t)slot * s->n;
     for (int64_t i = 0; i < s->n; ++i) row[i] = UNSEEN;
     /* the origin validated and saw its own message (markSeen) and puts it in
@@ -119,6 +132,9 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
         }
     }
     p->nfp = 0;
+    /* IWANT responses sent in the previous round arrive with them */
+    for (int64_t q = 0; q < p->ngr; ++q) ar_push(p, p->gr[q].recv, p->gr[q].slot, p->gr[q].er);
+    p->ngr = 0;
 
     /* 2. receivers handle the copies, in canonical order */
     arr_ent* ar = p->ar;
@@ -137,6 +153,8 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
         if (*cell == UNSEEN) {
             *cell = (uint32_t)g;               /* markSeen */
             m->stats[1]++;
+            orc_gossip_fulfill(m, i, slot);    /* gossipTracer: promises for it are kept */
+            if (p->slot_last) p->slot_last[slot] = g;
             if (m->invalid[slot]) {
                 /* ValidateMessage + RejectMessage(ValidationFailed), score.go:728-793 */
                 orc_mark_invalid(s, er, t);
@@ -154,8 +172,11 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
     }
     free(ar);
 
-    /* 3. control records of this round */
+    /* 3. control records of this round: GRAFT/PRUNE, then IHAVE (round 0)
+     * and IWANT (round 1) */
     orc_handle_control(s, (int32_t)(g % m->rounds), now);
+    if (g % m->rounds == 0) orc_gossip_ihave(s, m, g);
+    if (g % m->rounds == 1) orc_gossip_iwant(s, m, g);
 
     /* this round's first receivers forward in the next one */
     fr_ent* tmp = p->fp; const int64_t cap = p->capfp;

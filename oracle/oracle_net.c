@@ -9,7 +9,7 @@
  * key.  Observers are independent within a phase, so the OpenMP split over
  * observers gives identical results.
  */
-#include "oracle.h"
+#include "oracle_internal.h"
 
 #include <stdlib.h>
 #include <string.h>
@@ -19,7 +19,6 @@
 #define ES_TRACKED GSIM_ES_TRACKED
 #define ES_CONN    GSIM_ES_CONNECTED
 
-enum { P_GRAFT_DLO = 1, P_PRUNE_SHUF1 = 2, P_PRUNE_SHUF2 = 3, P_GRAFT_DOUT = 4, P_GRAFT_OPP = 5 };
 
 static const int64_t kSecond = 1000000000LL;
 /* clearBackoff adds 2*GossipSubHeartbeatInterval — the package default
@@ -27,16 +26,6 @@ static const int64_t kSecond = 1000000000LL;
 static const int64_t kBackoffSlack = 2 * 1000000000LL;
 
 typedef struct cand { uint64_t key; uint32_t e; double score; } cand;
-
-static uint64_t okey(uint64_t seed, uint64_t tick, uint32_t obs, int32_t topic, uint32_t purpose, uint32_t item,
-                     uint32_t pos)
-{
-    uint32_t ctr[4] = {(uint32_t)tick, obs, ((uint32_t)topic << 8) | purpose, item};
-    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-    uint32_t out[4];
-    orc_philox4x32_10(ctr, key, out);
-    return ((uint64_t)out[0] << 32) | pos;
-}
 
 static int cmp_key(const void* a, const void* b)
 {
@@ -235,9 +224,28 @@ static void maintain(hb* h)
     if (c != buf) free(c);
 }
 
-void orc_heartbeat(orc_net* s, uint64_t tick, int64_t now, uint64_t seed)
+void orc_heartbeat_gossip(orc_net* s, orc_msgs* m, uint64_t tick, int64_t now, uint64_t seed)
 {
     uint8_t* out = s->ctl;   /* heartbeat output = parity-0 inbox, handled in round 0 */
+    if (m) {
+        priv* p = orc_msgs_priv(m);
+        const size_t te = (size_t)s->t * (size_t)s->e;
+        if (!p->ihave || p->te_alloc != (int64_t)te) {
+            free(p->ihave);
+            p->ihave = (uint8_t*)calloc(te ? te : 1, 1);
+            p->te_alloc = (int64_t)te;
+        }
+        memset(p->ihave, 0, te);
+        p->ihave_tick = (int64_t)tick;
+        p->seed = seed;
+        orc_gossip_index(s, m, (int64_t)tick);
+        if (!p->npr) {
+            p->pr = (promise**)calloc((size_t)s->n, sizeof(promise*));
+            p->npr = (int32_t*)calloc((size_t)s->n, sizeof(int32_t));
+            p->cappr = (int32_t*)calloc((size_t)s->n, sizeof(int32_t));
+            p->n_alloc = s->n;
+        }
+    }
 #pragma omp parallel for schedule(dynamic, 64)
     for (int64_t i = 0; i < s->n; ++i) {
         hb h = {s, (uint32_t)i, s->row_ptr[i], s->row_ptr[i + 1], 0, tick, seed, now, out};
@@ -248,13 +256,20 @@ void orc_heartbeat(orc_net* s, uint64_t tick, int64_t now, uint64_t seed)
                     int64_t* bo = &s->backoff[(int64_t)t * s->e + e];
                     if (*bo != 0 && *bo + kBackoffSlack < now) *bo = 0;
                 }
-        /* maintain the mesh for topics we have joined (1385-1557) */
+        /* maintain the mesh for topics we have joined (1385-1557), each
+         * followed by emitGossip(topic, mesh) */
         for (int32_t t = 0; t < s->t; ++t) {
             if (!((s->sub[i] >> t) & 1u)) continue;
             h.t = t;
             maintain(&h);
+            if (m) orc_gossip_emit(s, m, (uint32_t)i, t, tick, seed);
         }
     }
+}
+
+void orc_heartbeat(orc_net* s, uint64_t tick, int64_t now, uint64_t seed)
+{
+    orc_heartbeat_gossip(s, NULL, tick, now, seed);
 }
 
 /* handleGraft for one (receiver, sender edge, topic), gossipsub.go:748-825. */

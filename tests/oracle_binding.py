@@ -41,6 +41,7 @@ class OrcMsgs(Structure):
         ("ring", c_int32), ("rounds", c_int32), ("t0", c_int64), ("hb", c_int64),
         ("topic", c_void_p), ("origin", c_void_p), ("invalid", c_void_p), ("seen", c_void_p),
         ("lastput", c_void_p), ("stats", c_int64 * 4), ("priv", c_void_p),
+        ("mid", c_void_p), ("behaviour", c_void_p),
     ]
 
 
@@ -103,6 +104,8 @@ def load():
             "orc_publish": (None, [P, POINTER(OrcMsgs), c_uint64, c_uint32, c_uint32, ctypes.c_uint8, c_int64]),
             "orc_round": (None, [P, POINTER(OrcMsgs), c_int64]),
             "orc_msgs_free_priv": (None, [POINTER(OrcMsgs)]),
+            "orc_heartbeat_gossip": (None, [P, POINTER(OrcMsgs), c_uint64, c_int64, c_uint64]),
+            "orc_gossip_penalties": (None, [P, POINTER(OrcMsgs), c_int64]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -189,21 +192,25 @@ class NetState:
 
 
 UNSEEN = 0xFFFFFFFF
+ORC_BEHAVE_IGNORE_IWANT = 0x01   # oracle.h: never answers IWANT
 
 
 class Msgs:
     """Oracle message ring + seen-set of a network (oracle_deliver.c)."""
 
-    def __init__(self, n, T, ring, rounds, t0, hb):
+    def __init__(self, n, T, ring, rounds, t0, hb, behaviour=None):
         self.seen = np.full((ring, n), UNSEEN, dtype=np.uint32)
         self.topic = np.zeros(ring, dtype=np.uint32)
         self.origin = np.zeros(ring, dtype=np.uint32)
         self.invalid = np.zeros(ring, dtype=np.uint8)
+        self.mid = np.zeros(ring, dtype=np.uint64)
         self.lastput = np.full((T, n), -1, dtype=np.int32)
+        self.behaviour = None if behaviour is None else np.ascontiguousarray(behaviour, dtype=np.uint8)
         m = OrcMsgs()
         m.ring, m.rounds, m.t0, m.hb = ring, rounds, t0, hb
         m.topic, m.origin, m.invalid = _p(self.topic), _p(self.origin), _p(self.invalid)
         m.seen, m.lastput = _p(self.seen), _p(self.lastput)
+        m.mid, m.behaviour = _p(self.mid), _p(self.behaviour)
         self.m = m
 
     @property
@@ -218,6 +225,14 @@ class Msgs:
 
     def round(self, st, g):
         load().orc_round(st.view(), ctypes.byref(self.m), g)
+
+    def heartbeat(self, st, tick, now, seed):
+        """orc_heartbeat_gossip: mesh maintenance + emitGossip for every peer."""
+        load().orc_heartbeat_gossip(st.view(), ctypes.byref(self.m), tick, now, seed)
+
+    def penalties(self, st, now):
+        """applyIwantPenalties at heartbeat time now (after refresh, before scoring)."""
+        load().orc_gossip_penalties(st.view(), ctypes.byref(self.m), now)
 
     def __del__(self):
         try:

@@ -219,8 +219,8 @@ def _schedule(rng, ticks, T, R, rate, inv_frac, n):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,k,T,ticks,rate,inv_frac,retained,ring", [
-    (1500, 16, 2, [1, 2, 3, 4], 6, 0.1, 0.0, 64),
-    (3000, 32, 3, [14, 15, 16], 12, 0.05, 0.03, 64),     # ring slots reused; clearBackoff tick
+    (1500, 16, 2, [1, 2, 3, 4], 6, 0.1, 0.0, 256),
+    (3000, 32, 3, [14, 15, 16], 12, 0.05, 0.03, 512),    # clearBackoff tick
 ])
 def test_rounds_bit_exact(require_gpu, n, k, T, ticks, rate, inv_frac, retained, ring):
     from fixtures import beacon_params, beacon_topic, synthetic_state
@@ -254,9 +254,10 @@ def test_rounds_bit_exact(require_gpu, n, k, T, ticks, rate, inv_frac, retained,
         eng.heartbeat(kk, now)
         v = st.view()
         lib.orc_refresh_scores(v, now)
+        msgs.penalties(st, now)
         lib.orc_ip_colocation(v)
         lib.orc_compute_scores(v)
-        lib.orc_heartbeat(v, kk, now, SEED)
+        msgs.heartbeat(st, kk, now, SEED)
         for g in range(kk * R, kk * R + R):
             for (mid, t, o, inv) in sched.get(g, []):
                 msgs.publish(st, mid, t, o, inv, g)
