@@ -195,6 +195,7 @@ def main():
     eng.synchronize()
     census0 = eng.census()
     stats0 = eng.msg_stats()
+    gossip0 = eng.gossip_stats()
 
     def barrier():
         if dist is not None:
@@ -217,6 +218,7 @@ def main():
     eng.profile(False)
     census1 = eng.census()
     stats1 = eng.msg_stats()
+    gossip1 = eng.gossip_stats()
     if dist is not None:
         import torch
         t = torch.tensor([wall], device=f"cuda:{local}", dtype=torch.float64)
@@ -277,6 +279,7 @@ def main():
             "deliveries_per_tick": {"accepted": (stats1[0] - stats0[0]) / K, "first": firsts / K,
                                     "duplicate": dups / K, "graylisted": (stats1[3] - stats0[3]) / K},
             "kernel_ms_per_tick": kms,
+            "gossip_per_tick": {k: (gossip1[k] - gossip0[k]) / K for k in gossip1},
             "census": census1,
             "roofline": dominant,
             "roofline_kernels": {"refresh_score": roof_refresh, "delivery": roof_deliv},

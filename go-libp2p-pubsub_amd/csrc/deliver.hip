@@ -73,7 +73,8 @@ struct Deliver {
     bool lazy = true;                  // every window >= 0: commits may trail a round
     // gossip
     int32_t* d_slot_last = nullptr;    // [ring] last round with a new claim or the publication
-    uint8_t* d_ihave = nullptr;        // [T][E] receiver edge: IHAVE(topic) from col[e] this heartbeat
+    uint8_t* d_gsel = nullptr;         // [T][E] sender edge order: emitGossip chose col[e] this heartbeat
+    uint32_t* d_gcount = nullptr;      // [2][ring] holders / wanting receivers per slot (direction choice)
     uint8_t* d_gstate = nullptr;       // [E] edge order: owner's snapshot score of col >= gossipThreshold
     uint64_t* d_resp = nullptr;        // IWANT responses (record edge | slot << 32), delivered in round 2
     uint32_t* d_nresp = nullptr;       // [1] responses queued; [1] overflow; [2] ring-reuse error
@@ -81,6 +82,7 @@ struct Deliver {
     uint32_t* d_prom = nullptr;        // [P][E] promise ring, edge order of the promiser: slot or none
     uint64_t* d_pcand = nullptr;       // [E] per-IWANT promise candidate (min Philox key | slot)
     uint8_t* d_behaviour = nullptr;    // [N] GSIM_BEHAVE_*
+    unsigned long long* d_gstats = nullptr;   // [4] gossip totals (gsim_gossip_stats)
     int32_t prom_ticks = 1;            // P
     std::vector<int64_t> prom_made;    // [P] tick that filled each ring index, -1 = empty
     int64_t ihave_tick = -1;           // heartbeat whose IHAVE marks are pending
@@ -523,13 +525,14 @@ struct IhArgs {
     const uint8_t* minv;
     const uint64_t* cell;
     const int32_t* slot_last;
-    const uint8_t *ihave, *gstate, *behaviour;
+    const uint8_t *gsel, *gstate, *behaviour;
     uint64_t* pcand;
     uint32_t* prom;
     int32_t P, prom_idx;
     uint64_t* resp;
     uint32_t* nresp;               // [0] count, [1] overflow
     int64_t resp_cap;
+    unsigned long long* gstats;    // [0] receivers x slots walked, [1] IWANT ids, [2] responses, [3] broken promises
     bool respond;                  // GossipRetransmission >= 1
     uint64_t seed;
 };
@@ -546,10 +549,74 @@ __device__ __forceinline__ int64_t cell_round(uint64_t c, int64_t g)
 
 constexpr int kRespStage = 256;    // per-wave LDS staging of queued responses
 
-template <int W>
-__global__ __launch_bounds__(256) void k_ihave(IhArgs a)
+// Direction choice per slot (as in direction-optimizing BFS): a message few
+// peers hold is handled from its holders (each walks its row for the peers it
+// gossiped to: "push"); one few peers still miss, from those receivers (each
+// walks its row for advertisers: "pull").  Both enumerate exactly the same
+// (receiver, advertiser, message) IWANT triples.
+__device__ __forceinline__ bool holds_in_window(uint64_t c, int64_t g, int32_t lo_round, int64_t tick_round,
+                                                bool inv, bool is_origin)
 {
-    extern __shared__ uint16_t s_act[];   // [ring] candidate slots, then per-wave response staging
+    const int64_t fr = cell_round(c, g);
+    return fr >= lo_round && fr < tick_round && (!inv || is_origin);
+}
+
+__global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount)
+{
+    extern __shared__ uint16_t s_act[];   // [ring] candidate slots, then [2][ring] u32 counters
+    __shared__ int s_n;
+    uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_act + ((a.ring + 1) & ~1));
+    for (int w = threadIdx.x; w < 2 * a.ring; w += blockDim.x) s_cnt[w] = 0;
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        int n = 0;
+        for (int m0 = 0; m0 < a.ring; m0 += 64) {
+            const int m = m0 + lane;
+            const bool act = m < a.ring && a.slot_last[m] >= a.lo_round;
+            const uint64_t b = __ballot(act);
+            if (act) s_act[n + __popcll(b & ((1ull << lane) - 1))] = (uint16_t)m;
+            n += __popcll(b);
+        }
+        if (lane == 0) s_n = n;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t p0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+    const int nact = p0 < a.N ? s_n : 0;
+    const int64_t pl = p0 + lane;
+    const bool vp = pl < a.N;
+    const uint64_t subp = vp ? a.sub[pl] : 0ull;
+    const int64_t tick_round = a.tick * a.R;
+    for (int k0 = 0; k0 < nact; k0 += kSlotBatch) {
+        uint64_t cv[kSlotBatch];
+#pragma unroll
+        for (int b = 0; b < kSlotBatch; ++b) {
+            const int k = k0 + b;
+            cv[b] = (k < nact && vp) ? a.cell[(int64_t)s_act[k] * a.N + pl] : 0ull;
+        }
+#pragma unroll
+        for (int b = 0; b < kSlotBatch; ++b) {
+            const int k = k0 + b;
+            if (k >= nact) break;
+            const uint32_t m = s_act[k];
+            const int32_t t = (int32_t)a.mtopic[m];
+            const bool hold = vp && holds_in_window(cv[b], a.g, a.lo_round, tick_round, a.minv[m] != 0,
+                                                   (uint32_t)pl == a.morigin[m]);
+            const bool want = vp && cv[b] == kUnseen64 && ((subp >> t) & 1ull);
+            const int nh = __popcll(__ballot(hold)), nw = __popcll(__ballot(want));
+            if (lane == 0 && nh) atomicAdd(&s_cnt[m], (uint32_t)nh);
+            if (lane == 0 && nw) atomicAdd(&s_cnt[a.ring + m], (uint32_t)nw);
+        }
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < 2 * a.ring; w += blockDim.x)
+        if (s_cnt[w]) atomicAdd(&gcount[w], s_cnt[w]);
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
+{
+    extern __shared__ uint16_t s_act[];   // [ring] candidate slots (bit 15: push), then response staging
     __shared__ int s_n;
     const int wid = threadIdx.x >> 6;
     uint64_t* stage = reinterpret_cast<uint64_t*>(s_act + ((a.ring + 3) & ~3)) + wid * kRespStage;
@@ -558,9 +625,11 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a)
         int n = 0;
         for (int m0 = 0; m0 < a.ring; m0 += 64) {
             const int m = m0 + lane;
-            const bool act = m < a.ring && a.slot_last[m] >= a.lo_round;   // someone put it in the window
+            const bool act = m < a.ring && a.slot_last[m] >= a.lo_round && gcount[m] != 0 && gcount[a.ring + m] != 0;
+            // cost model: a holder walk probes ~Dlazy cells, a receiver walk ~deg
+            const bool push = act && (uint64_t)gcount[m] * 4u < (uint64_t)gcount[a.ring + m] * 32u;
             const uint64_t b = __ballot(act);
-            if (act) s_act[n + __popcll(b & ((1ull << lane) - 1))] = (uint16_t)m;
+            if (act) s_act[n + __popcll(b & ((1ull << lane) - 1))] = (uint16_t)(m | (push ? 0x8000 : 0));
             n += __popcll(b);
         }
         if (lane == 0) s_n = n;
@@ -576,8 +645,10 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a)
     const uint64_t subp = vp ? a.sub[pl] : 0ull;
     const uint32_t rp0 = vp ? a.row_ptr[pl] : 0u;
     const uint32_t rp1 = vp ? a.row_ptr[pl + 1] : 0u;
-    bool asked = false;                       // this lane's receiver sent an IWANT
+    const bool ign_l = vp && (a.behaviour[pl] & GSIM_BEHAVE_IGNORE_IWANT);
+    const int64_t tick_round = a.tick * a.R;
     int nstage = 0;
+    unsigned long long n_walk = 0, n_req = 0, n_resp = 0;
     auto flush_stage = [&]() {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -595,20 +666,23 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a)
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
-            cv[b] = (k < nact && vp) ? a.cell[(int64_t)s_act[k] * a.N + pl] : 0ull;
+            cv[b] = (k < nact && vp) ? a.cell[(int64_t)(s_act[k] & 0x7FFF) * a.N + pl] : 0ull;
         }
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
             if (k >= nact) break;                            // wave-uniform
-            const uint32_t m = s_act[k];
+            const uint32_t m = s_act[k] & 0x7FFF;
+            const bool push = (s_act[k] & 0x8000) != 0;
             const int32_t t = (int32_t)a.mtopic[m];
-            // handleIHave: a joined topic and a message not seen yet (seenMessage)
-            const bool wanted = vp && cv[b] == kUnseen64 && ((subp >> t) & 1ull);
-            const uint64_t mask = __ballot(wanted);
-            if (!mask) continue;
             const uint32_t origin = a.morigin[m];
             const bool inv = a.minv[m] != 0;
+            // push: lanes are holders of m (its advertisers); pull: lanes are
+            // receivers that joined t and have not seen m (handleIHave's seenMessage)
+            const bool me = vp && (push ? holds_in_window(cv[b], a.g, a.lo_round, tick_round, inv, (uint32_t)pl == origin)
+                                        : (cv[b] == kUnseen64 && ((subp >> t) & 1ull)));
+            const uint64_t mask = __ballot(me);
+            if (!mask) continue;
             const int64_t row_m = (int64_t)m * a.N;
             const int64_t plane = (int64_t)t * a.E;
             uint64_t gm = mask & gmask;
@@ -617,26 +691,43 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a)
                 if (gm) { bs = __ffsll((long long)gm) - 1; gm &= gm - 1; }
                 const int sl = bs < 0 ? lane : bs;
                 const uint32_t beg = __shfl(rp0, sl, 64), end = __shfl(rp1, sl, 64);
+                const bool ign_s = __shfl(ign_l, sl, 64);
                 const bool v = bs >= 0 && (uint32_t)gl < end - beg;
                 const uint32_t e = beg + (uint32_t)gl;
-                const uint32_t prcv = (uint32_t)(p0 + (bs < 0 ? 0 : bs));
+                const uint32_t me_id = (uint32_t)(p0 + (bs < 0 ? 0 : bs));
+                n_walk += (gl == 0 && bs >= 0);
                 bool req = false, resp = false;
-                uint32_t i = 0, r = 0;
-                if (v && a.ihave[plane + e] && a.gstate[e]) {          // IHAVE(t) from i, score >= gossipThreshold
-                    i = a.col[e];
-                    const int64_t fr = cell_round(a.cell[row_m + i], a.g);
-                    // the IHAVE lists i's mcache gossip window: puts of ticks k-HG .. k-1
-                    req = fr >= a.lo_round && fr < (int64_t)a.tick * a.R && (!inv || i == origin);
+                uint32_t r = 0;
+                if (push) {
+                    // holder me_id walks its row: the peers it gossiped t to
+                    if (v && a.gsel[plane + e]) {
+                        const uint32_t p = a.col[e], re = a.rev[e];
+                        req = a.gstate[re] && a.cell[row_m + p] == kUnseen64;   // p's gate on i, p has not seen m
+                        if (req) {
+                            const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, p, 0, P_PROMISE, m, me_id);
+                            atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[re]), (unsigned long long)key);
+                            r = e;
+                            resp = a.respond && a.gstate[e] && !ign_s;
+                        }
+                    }
+                } else {
+                    // receiver me_id walks its row: the peers that gossiped t to it and hold m
+                    if (v) {
+                        const uint32_t re = a.rev[e];
+                        if (a.gsel[plane + re] && a.gstate[e]) {
+                            const uint32_t i = a.col[e];
+                            req = holds_in_window(a.cell[row_m + i], a.g, a.lo_round, tick_round, inv, i == origin);
+                            if (req) {
+                                const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, me_id, 0, P_PROMISE, m, i);
+                                atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[e]), (unsigned long long)key);
+                                r = re;
+                                resp = a.respond && a.gstate[re] && !(a.behaviour[i] & GSIM_BEHAVE_IGNORE_IWANT);
+                            }
+                        }
+                    }
                 }
-                if (req) {
-                    const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, prcv, 0, P_PROMISE, m, i);
-                    if (key < a.pcand[e]) a.pcand[e] = key;          // AddPromise's random pick
-                    r = a.rev[e];
-                    // handleIWant at i: score gate on p, honoured IWANT, retransmission budget
-                    resp = a.respond && a.gstate[r] && !(a.behaviour[i] & GSIM_BEHAVE_IGNORE_IWANT);
-                }
-                const uint64_t rb = __ballot(req) & gmask;
-                if (rb && lane == bs) asked = true;
+                n_req += req;
+                n_resp += resp;
                 const uint64_t sb = __ballot(resp);
                 if (sb) {
                     if (nstage + __popcll(sb) > kRespStage) flush_stage();
@@ -647,23 +738,30 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a)
         }
     }
     flush_stage();
-    // AddPromise (gossip_tracer.go:48-75): one tracked id per IWANT, unless
-    // the same (id, peer) promise is still pending
-    uint64_t am = __ballot(asked) & gmask;
-    while (__ballot(am != 0)) {
-        int bs = -1;
-        if (am) { bs = __ffsll((long long)am) - 1; am &= am - 1; }
-        const int sl = bs < 0 ? lane : bs;
-        const uint32_t beg = __shfl(rp0, sl, 64), end = __shfl(rp1, sl, 64);
-        if (bs < 0 || (uint32_t)gl >= end - beg) continue;
-        const uint32_t e = beg + (uint32_t)gl;
-        const uint64_t key = a.pcand[e];
+    n_walk = wave_sum_u64(n_walk);
+    n_req = wave_sum_u64(n_req);
+    n_resp = wave_sum_u64(n_resp);
+    if (lane == 0 && (n_walk | n_req)) {
+        atomicAdd(&a.gstats[0], n_walk);
+        atomicAdd(&a.gstats[1], n_req);
+        atomicAdd(&a.gstats[2], n_resp);
+    }
+}
+
+// AddPromise (gossip_tracer.go:48-75): the one tracked id of each IWANT,
+// unless the same (id, peer) promise is still pending.
+__global__ __launch_bounds__(256) void k_promise_insert(uint64_t* pcand, uint32_t* prom, int32_t P, int32_t idx,
+                                                        int64_t E)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride) {
+        const uint64_t key = pcand[e];
         if (key == ~0ull) continue;
-        a.pcand[e] = ~0ull;
+        pcand[e] = ~0ull;
         const uint32_t slot = (uint32_t)key;
         bool exists = false;
-        for (int q = 0; q < a.P; ++q) exists |= a.prom[(int64_t)q * a.E + e] == slot;
-        if (!exists) a.prom[(int64_t)a.prom_idx * a.E + e] = slot;
+        for (int q = 0; q < P; ++q) exists |= prom[(int64_t)q * E + e] == slot;
+        if (!exists) prom[(int64_t)idx * E + e] = slot;
     }
 }
 
@@ -786,15 +884,22 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
 // (fulfillPromise at first reception).  Record order: the penalty lands on
 // the promiser's record of the advertiser, rev[e].
 __global__ __launch_bounds__(256) void k_promise_check(uint32_t* prom_q, const uint64_t* cell, const uint32_t* owner,
-                                                       const uint32_t* rev, uint8_t* pen, int64_t E, int64_t N)
+                                                       const uint32_t* rev, uint8_t* pen, int64_t E, int64_t N,
+                                                       unsigned long long* gstats)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    unsigned long long broken = 0;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride) {
         const uint32_t slot = prom_q[e];
         if (slot == 0xFFFFFFFFu) continue;
         prom_q[e] = 0xFFFFFFFFu;
-        if (cell[(int64_t)slot * N + owner[e]] == kUnseen64) pen[rev[e]] = (uint8_t)(pen[rev[e]] + 1);
+        if (cell[(int64_t)slot * N + owner[e]] == kUnseen64) {
+            pen[rev[e]] = (uint8_t)(pen[rev[e]] + 1);
+            ++broken;
+        }
     }
+    broken = wave_sum_u64(broken);
+    if ((threadIdx.x & 63) == 0 && broken) atomicAdd(&gstats[3], broken);
 }
 
 __global__ void k_seen_view(const uint64_t* cell, uint32_t* out, int64_t n)
@@ -817,8 +922,8 @@ static void dl_free(Deliver* d)
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
-    f(d->d_slot_last); f(d->d_ihave); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_prom); f(d->d_pcand);
-    f(d->d_behaviour);
+    f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_prom); f(d->d_pcand);
+    f(d->d_behaviour); f(d->d_gstats);
     delete d;
 }
 
@@ -876,7 +981,7 @@ bool deliver_gossip_view(gsim_handle* h, GossipView* v)
     Deliver* d = h->dl;
     if (!d) return false;
     v->lastput = d->d_lastput;
-    v->ihave = d->d_ihave;
+    v->gsel = d->d_gsel;
     v->gstate = d->d_gstate;
     return true;
 }
@@ -901,7 +1006,7 @@ int deliver_promise_check(gsim_handle* h, int64_t now)
         if (!(expire < now)) continue;
         hipLaunchKernelGGL(k_promise_check, dim3(std::min<int64_t>((h->e + 255) / 256, 16384)), dim3(256), 0,
                            h->stream, d->d_prom + (size_t)q * (size_t)h->e, (const uint64_t*)d->d_cell,
-                           (const uint32_t*)h->d_owner, (const uint32_t*)h->d_rev, h->d_pen, h->e, h->n);
+                           (const uint32_t*)h->d_owner, (const uint32_t*)h->d_rev, h->d_pen, h->e, h->n, d->d_gstats);
         d->prom_made[(size_t)q] = -1;
         int rc = hip_check(h, hipGetLastError(), "k_promise_check");
         if (rc) return rc;
@@ -909,14 +1014,13 @@ int deliver_promise_check(gsim_handle* h, int64_t now)
     return GSIM_OK;
 }
 
-// The heartbeat's emitGossip writes fresh IHAVE marks.
+// The heartbeat's emitGossip rewrites the gossip choices of every joined topic.
 int deliver_heartbeat_begin(gsim_handle* h, uint64_t tick)
 {
     Deliver* d = h->dl;
     if (!d) return GSIM_OK;
-    hipError_t e = hipMemsetAsync(d->d_ihave, 0, (size_t)h->e * (size_t)std::max(1, h->t), h->stream);
     d->ihave_tick = (int64_t)tick;
-    return hip_check(h, e, "ihave reset");
+    return GSIM_OK;
 }
 
 // Control round 0: handleIHave (+ the advertisers' handleIWant) for the
@@ -935,7 +1039,7 @@ static int launch_ihave(gsim_handle* h, int64_t g)
     a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.rev = h->d_rev; a.sub = h->d_sub;
     a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv;
     a.cell = d->d_cell; a.slot_last = d->d_slot_last;
-    a.ihave = d->d_ihave; a.gstate = d->d_gstate; a.behaviour = d->d_behaviour;
+    a.gsel = d->d_gsel; a.gstate = d->d_gstate; a.behaviour = d->d_behaviour;
     a.pcand = d->d_pcand; a.prom = d->d_prom; a.P = d->prom_ticks;
     a.prom_idx = (int32_t)(tick % d->prom_ticks);
     if (d->prom_made[(size_t)a.prom_idx] >= 0) {
@@ -943,20 +1047,25 @@ static int launch_ihave(gsim_handle* h, int64_t g)
         return GSIM_ESTATE;
     }
     d->prom_made[(size_t)a.prom_idx] = tick;
-    a.resp = d->d_resp; a.nresp = d->d_nresp; a.resp_cap = d->resp_cap;
+    a.resp = d->d_resp; a.nresp = d->d_nresp; a.resp_cap = d->resp_cap; a.gstats = d->d_gstats;
     a.respond = h->gp.gossip_retransmission >= 1;
     a.seed = h->x ? gsim_get_seed(h) : 0;
     const size_t lds = (((size_t)d->cfg.ring + 3) & ~(size_t)3) * sizeof(uint16_t) + 4 * kRespStage * sizeof(uint64_t);
+    const size_t lds_c = (((size_t)d->cfg.ring + 1) & ~(size_t)1) * sizeof(uint16_t) + 2 * (size_t)d->cfg.ring * 4;
     const int grid = grid_peers(h->n);
     ProfScope ps(h, GSIM_K_GOSSIP);
     hipError_t e = hipMemsetAsync(d->d_nresp, 0, 2 * sizeof(uint32_t), h->stream);
-    if (e != hipSuccess) return hip_check(h, e, "nresp reset");
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_gcount, 0, 2 * (size_t)d->cfg.ring * 4, h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "gossip reset");
+    hipLaunchKernelGGL(k_gossip_count, dim3(grid), dim3(256), lds_c, h->stream, a, d->d_gcount);
     if (h->max_degree <= 16)
-        hipLaunchKernelGGL(k_ihave<16>, dim3(grid), dim3(256), lds, h->stream, a);
+        hipLaunchKernelGGL(k_ihave<16>, dim3(grid), dim3(256), lds, h->stream, a, (const uint32_t*)d->d_gcount);
     else if (h->max_degree <= 32)
-        hipLaunchKernelGGL(k_ihave<32>, dim3(grid), dim3(256), lds, h->stream, a);
+        hipLaunchKernelGGL(k_ihave<32>, dim3(grid), dim3(256), lds, h->stream, a, (const uint32_t*)d->d_gcount);
     else
-        hipLaunchKernelGGL(k_ihave<64>, dim3(grid), dim3(256), lds, h->stream, a);
+        hipLaunchKernelGGL(k_ihave<64>, dim3(grid), dim3(256), lds, h->stream, a, (const uint32_t*)d->d_gcount);
+    hipLaunchKernelGGL(k_promise_insert, dim3(std::min<int64_t>((h->e + 255) / 256, 16384)), dim3(256), 0, h->stream,
+                       d->d_pcand, d->d_prom, d->prom_ticks, a.prom_idx, h->e);
     d->resp_round = g + 2;
     return hip_check(h, hipGetLastError(), "k_ihave");
 }
@@ -1040,13 +1149,15 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     }
     d->resp_cap = cfg->max_arrivals > 0 ? cfg->max_arrivals : std::max<int64_t>(8 * h->n, 1 << 20);
     A((void**)&d->d_slot_last, ring * 4);
-    A((void**)&d->d_ihave, T * (size_t)h->e);
+    A((void**)&d->d_gsel, T * (size_t)h->e);
+    A((void**)&d->d_gcount, 2 * ring * 4);
     A((void**)&d->d_gstate, (size_t)h->e);
     A((void**)&d->d_resp, (size_t)d->resp_cap * 8);
     A((void**)&d->d_nresp, 4 * 4);
     A((void**)&d->d_prom, (size_t)d->prom_ticks * (size_t)h->e * 4);
     A((void**)&d->d_pcand, (size_t)h->e * 8);
     A((void**)&d->d_behaviour, N);
+    A((void**)&d->d_gstats, 4 * 8);
     if (e != hipSuccess) {
         dl_free(d);
         h->err = std::string("message ring allocation: ") + hipGetErrorString(e);
@@ -1061,12 +1172,13 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     if (e == hipSuccess) e = hipMemsetAsync(d->d_nnew, 0, 2 * words * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_stats, 0, 4 * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_slot_last, 0xFF, ring * 4, h->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(d->d_ihave, 0, T * (size_t)h->e, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_gsel, 0, T * (size_t)h->e, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_gstate, 0, (size_t)h->e, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_nresp, 0, 4 * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_prom, 0xFF, (size_t)d->prom_ticks * (size_t)h->e * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_pcand, 0xFF, (size_t)h->e * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_behaviour, 0, N, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_gstats, 0, 4 * 8, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     return hip_check(h, e, "gsim_msgs_init");
 }
@@ -1212,6 +1324,20 @@ int gsim_msg_stats(gsim_handle* h, int64_t* out4)
         h->err = "a ring slot was republished while its message could still be gossiped or promised (raise ring)";
         return GSIM_ESTATE;
     }
+    return GSIM_OK;
+}
+
+int gsim_gossip_stats(gsim_handle* h, int64_t* out4)
+{
+    if (!h || !out4) return GSIM_EINVAL;
+    if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
+    Deliver* d = h->dl;
+    if (!d) { h->err = "gsim_msgs_init not called"; return GSIM_ESTATE; }
+    unsigned long long s[4];
+    hipError_t e = hipMemcpyAsync(s, d->d_gstats, sizeof(s), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "gsim_gossip_stats");
+    for (int k = 0; k < 4; ++k) out4[k] = (int64_t)s[k];
     return GSIM_OK;
 }
 

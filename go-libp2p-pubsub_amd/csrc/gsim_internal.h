@@ -51,6 +51,8 @@ enum : uint32_t {
     DIAG_D_PLAIN_CLAIM = 64,    // plain store instead of the claim atomicMin (racy)
     DIAG_D_NO_ROWSTATE = 128,   // skip the acc/estate/tflags/rstate loads (all pass)
     DIAG_D_NO_COMMIT = 256,     // skip the P2 credit of commits
+    DIAG_H_NO_GOSSIP = 512,     // heartbeat: skip emitGossip
+    DIAG_H_NO_IHAVE_STORE = 1024,   // heartbeat: choose gossip targets but do not store the marks
 };
 
 struct ColocArgs {
@@ -241,7 +243,7 @@ int deliver_flush(gsim_handle* h);                  // commit the last round's c
 // What the heartbeat's emitGossip needs from the message state.
 struct GossipView {
     const int32_t* lastput;   // [T][N] tick of the newest mcache.Put
-    uint8_t* ihave;           // [T][E] receiver edge: IHAVE(topic) from col[e] this heartbeat
+    uint8_t* gsel;            // [T][E] sender edge order: emitGossip chose col[e] this heartbeat
     uint8_t* gstate;          // [E] edge order: owner's snapshot score of col >= gossipThreshold
 };
 bool deliver_gossip_view(gsim_handle* h, GossipView* v);   // false before gsim_msgs_init

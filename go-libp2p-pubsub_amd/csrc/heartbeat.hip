@@ -53,13 +53,14 @@ struct HbArgs {
     // emitGossip (gossipsub.go:1711-1775); gossip == false before gsim_msgs_init
     bool gossip;
     const int32_t* lastput;    // [T][N]
-    uint8_t* ihave;            // [T][E] receiver edge
+    uint8_t* gsel;             // [T][E] sender edge order: emitGossip chose col[e] this heartbeat
     uint8_t* gstate;           // [E] edge order: snapshot score >= gossipThreshold
     double gossip_thr, gossip_factor;
     int32_t dlazy, hist_gossip;
     // live Score(p) for emitGossip (score.go:265-342)
     const double *first, *invalid, *p5, *p6;
     double topic_cap, w5, w6, bp_thr, w7;
+    uint32_t diag;             // timing ablations (bit0: no emitGossip, bit1: no IHAVE store)
 };
 
 namespace {
@@ -70,14 +71,18 @@ constexpr int kFlagChunk = 8;                    // topics whose flags are loade
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
+// Minimum of a 32-bit value over the 64 lanes with DPP row shifts and row
+// broadcasts (VALU data paths, no LDS permute); every lane must be active.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
 {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t o = __shfl_xor(v, off, 64);
-        v = o < v ? o : v;
-    }
-    return v;
+    const int I = -1;   // 0xFFFFFFFF: identity of min for lanes a shift leaves empty
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x111, 0xF, 0xF, false));   // row_shr:1
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x112, 0xF, 0xF, false));   // row_shr:2
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x114, 0xF, 0xF, false));   // row_shr:4
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x118, 0xF, 0xF, false));   // row_shr:8
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x142, 0xA, 0xF, false));   // row_bcast:15
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x143, 0xC, 0xF, false));   // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 __device__ __forceinline__ uint64_t hb_key(const HbArgs& a, uint32_t obs, int32_t t, uint32_t purpose, uint32_t col,
@@ -86,20 +91,32 @@ __device__ __forceinline__ uint64_t hb_key(const HbArgs& a, uint32_t obs, int32_
     return select_key(a.seed, (uint32_t)a.tick, obs, (uint32_t)t, purpose, col, pos);
 }
 
+__device__ __forceinline__ uint32_t hb_key_hi(const HbArgs& a, uint32_t obs, int32_t t, uint32_t purpose,
+                                              uint32_t col, uint32_t pos)
+{
+    return (uint32_t)(select_key(a.seed, (uint32_t)a.tick, obs, (uint32_t)t, purpose, col, pos) >> 32);
+}
+
 // getPeers (gossipsub.go:1908-1928) restated: among candidate lanes keep the
 // `count` with the smallest Philox key (all of them if count <= 0 or fewer).
+// A key is (32 random bits, row position); the row position is the lane, so
+// each round takes the wave minimum of the random word and breaks ties by
+// the lowest lane.
 __device__ bool select_smallest(const HbArgs& a, bool cand, int count, uint32_t obs, int32_t t, uint32_t purpose,
                                 uint32_t col, uint32_t pos)
 {
-    const uint64_t m = ballot(cand);
-    const int n = __popcll(m);
+    uint64_t avail = __ballot(cand);
+    const int n = __popcll(avail);
     if (n == 0) return false;
     if (count <= 0 || n <= count) return cand;
-    uint64_t key = cand ? hb_key(a, obs, t, purpose, col, pos) : ~0ull;
+    const int lane = threadIdx.x & 63;
+    uint32_t hi = cand ? hb_key_hi(a, obs, t, purpose, col, pos) : 0xFFFFFFFFu;
     bool sel = false;
     for (int c = 0; c < count; ++c) {
-        const uint64_t mn = wave_min_u64(key);
-        if (key == mn) { sel = true; key = ~0ull; }
+        const uint32_t mn = wave_min_u32(hi);
+        const int win = __ffsll((long long)(__ballot(hi == mn) & avail)) - 1;
+        avail &= ~(1ull << win);
+        if (lane == win) { sel = true; hi = 0xFFFFFFFFu; }
     }
     return sel;
 }
@@ -212,16 +229,21 @@ __device__ bool gossip_targets(const HbArgs& a, bool cand, bool tpeer, uint32_t 
     const int factor = (int)(a.gossip_factor * (double)n);
     if (factor > target) target = factor;
     if (target >= n) return cand || dup;
-    uint64_t k1 = cand ? hb_key(a, obs, t, P_GOSSIP, col, pos) : ~0ull;
-    uint64_t k2 = dup ? hb_key(a, obs, t, P_GOSSIP_DUP, col, pos) : ~0ull;
+    // each lane holds up to two instances (candidate, fill duplicate)
+    uint32_t h1 = cand ? hb_key_hi(a, obs, t, P_GOSSIP, col, pos) : 0xFFFFFFFFu;
+    uint32_t h2 = dup ? hb_key_hi(a, obs, t, P_GOSSIP_DUP, col, pos) : 0xFFFFFFFFu;
+    uint64_t av1 = __ballot(cand), av2 = __ballot(dup);
+    const int lane = threadIdx.x & 63;
     bool sel = false;
     for (int q = 0; q < target; ++q) {
-        const uint64_t mine = k1 < k2 ? k1 : k2;
-        const uint64_t mn = wave_min_u64(mine);
-        if (mine == mn) {
-            sel = true;
-            if (k1 < k2) k1 = ~0ull; else k2 = ~0ull;
-        }
+        // a lane's next instance: its smaller key (instance 1 on a tie)
+        const bool has1 = (av1 >> lane) & 1ull, has2 = (av2 >> lane) & 1ull;
+        const bool use1 = has1 && (!has2 || h1 <= h2);
+        const uint32_t mine = use1 ? h1 : (has2 ? h2 : 0xFFFFFFFFu);
+        const uint32_t mn = wave_min_u32(mine);
+        const int win = __ffsll((long long)(__ballot(mine == mn && (has1 || has2)))) - 1;
+        if (__shfl(use1, win, 64)) av1 &= ~(1ull << win); else av2 &= ~(1ull << win);
+        if (lane == win) sel = true;
     }
     return sel;
 }
@@ -250,6 +272,8 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
         // Graft/Prune touches one of the lane's records
         double S_live = S;
         bool dirty = false;
+        // newest mcache put per topic (GetGossipIDs non-empty test), one lane per topic
+        const int32_t lp_lane = (a.gossip && lane < a.T) ? a.lastput[(int64_t)lane * a.N + obs] : -1;
         if (a.gossip && valid) a.gstate[e] = S >= a.gossip_thr ? 1 : 0;
 
         // clearBackoff every 15 ticks (gossipsub.go:1627-1646)
@@ -412,15 +436,20 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
 
             // emitGossip(topic, mesh) (gossipsub.go:1554-1556, 1711-1775):
             // only if GetGossipIDs(topic) is non-empty, i.e. this peer put a
-            // message of the topic in the last HistoryGossip ticks
-            if (a.gossip && a.lastput[(int64_t)t * a.N + obs] >= (int64_t)a.tick - a.hist_gossip) {
-                if (__ballot(dirty)) {
-                    if (dirty) S_live = score_of_record(a, rv, col);
-                    dirty = false;
+            // message of the topic in the last HistoryGossip ticks.  The
+            // choice is stored in the sender's row (enqueueGossip); every
+            // joined topic's plane is rewritten each heartbeat.
+            if (a.gossip) {
+                bool gsel = false;
+                if (!(a.diag & 1) && __shfl(lp_lane, t, 64) >= (int64_t)a.tick - a.hist_gossip) {
+                    if (__ballot(dirty)) {
+                        if (dirty) S_live = score_of_record(a, rv, col);
+                        dirty = false;
+                    }
+                    const bool gcand = tpeer && !m && S_live >= a.gossip_thr;
+                    gsel = gossip_targets(a, gcand, tpeer, (uint32_t)obs, t, col, pos);
                 }
-                const bool gcand = tpeer && !m && S_live >= a.gossip_thr;
-                if (gossip_targets(a, gcand, tpeer, (uint32_t)obs, t, col, pos) && valid)
-                    a.ihave[(int64_t)t * a.E + rv] = 1;          // enqueueGossip: IHAVE in the receiver's inbox
+                if (valid && !(a.diag & 2)) a.gsel[i] = gsel ? 1 : 0;
             }
             if (valid) {
                 if (ctl) {
@@ -589,12 +618,13 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.opp_threshold = h->th.opportunistic_graft_threshold;
     GossipView gv{};
     a.gossip = deliver_gossip_view(h, &gv);
-    a.lastput = gv.lastput; a.ihave = gv.ihave; a.gstate = gv.gstate;
+    a.lastput = gv.lastput; a.gsel = gv.gsel; a.gstate = gv.gstate;
     a.gossip_thr = h->th.gossip_threshold; a.gossip_factor = h->gp.gossip_factor;
     a.dlazy = h->gp.dlazy; a.hist_gossip = h->gp.history_gossip;
     a.first = h->d_first; a.invalid = h->d_invalid; a.p5 = h->d_p5; a.p6 = h->d_p6;
     a.topic_cap = h->pp.topic_score_cap; a.w5 = h->pp.app_specific_weight; a.w6 = h->pp.ip_colocation_factor_weight;
     a.bp_thr = h->pp.behaviour_penalty_threshold; a.w7 = h->pp.behaviour_penalty_weight;
+    a.diag = (h->diag >> 9) & 3u;    // DIAG_H_NO_GOSSIP / DIAG_H_NO_IHAVE_STORE
     return a;
 }
 
@@ -632,7 +662,7 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     int rc = check_degree(h);
     if (rc) return rc;
     rc = deliver_flush(h);
-    if (!rc) rc = deliver_heartbeat_begin(h, tick);
+    if (!rc) rc = deliver_heartbeat_begin(h, tick);   // IHAVE marks of this heartbeat are pending
     if (rc) return rc;
     // heartbeat output goes to the parity-0 inbox, read by control round 0
     HbArgs a = make_hb_args(h, tick, now, 1);

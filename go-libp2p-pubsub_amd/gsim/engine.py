@@ -252,6 +252,11 @@ class Engine:
         f = np.ascontiguousarray(flags, dtype=np.uint8)
         self._check(self.lib.gsim_set_peer_behaviour(self.h, _ptr(f)))
 
+    def gossip_stats(self) -> dict:
+        out = np.zeros(4, dtype=np.int64)
+        self._check(self.lib.gsim_gossip_stats(self.h, _ptr(out)))
+        return dict(zip(["ihave_walks", "iwant_ids", "iwant_responses", "broken_promises"], (int(x) for x in out)))
+
     def msg_stats(self) -> list:
         out = np.zeros(4, dtype=np.int64)
         self._check(self.lib.gsim_msg_stats(self.h, _ptr(out)))

@@ -283,6 +283,10 @@ int gsim_msg_stats(gsim_handle* h, int64_t* out4);
  * and P7 penalties follow (gossip_tracer.go:79-115, gossipsub.go:1620-1625). */
 #define GSIM_BEHAVE_IGNORE_IWANT 0x01u
 int gsim_set_peer_behaviour(gsim_handle* h, const uint8_t* flags);
+/* Cumulative gossip totals: out4 = {(receiver, message) pairs handleIHave
+ * examined for an unseen advertised id, IWANT ids sent, messages sent in
+ * answer to IWANT, broken promises penalised}. */
+int gsim_gossip_stats(gsim_handle* h, int64_t* out4);
 
 /* Aggregate census of the state (the network-wide analogue of the
  * reference's score inspection, score.go:448-500): out8 = {connected scored

@@ -18,8 +18,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import bench  # noqa: E402
 
-ARMS = {0: "full", 32: "no_counters", 64: "plain_claim", 128: "no_rowstate", 256: "no_commit_credit",
-        32 | 128 | 256: "cells_and_claims_only", 32 | 64 | 128 | 256: "cells_only(plain claim)"}
+ARMS = {0: "full", 512: "hb_no_emit_gossip", 1024: "hb_no_ihave_store", 32: "send_no_counters",
+        128: "send_no_rowstate"}
 
 
 def main():
@@ -45,10 +45,12 @@ def main():
                 bench.run_tick(eng, k, sched)
             prof = eng.profile_read()
             eng.profile(False)
-            times[d].append(prof["send"][0] / args.ticks)
+            times[d].append({c: ms / args.ticks for c, (ms, _) in prof.items() if ms > 0})
     eng.set_kernel_variant(1, 0)
-    out = {ARMS[d]: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v))} for d, v in times.items()}
-    print(json.dumps({"k_send_ms_per_tick": out}))
+    out = {}
+    for d, v in times.items():
+        out[ARMS[d]] = {c: round(float(np.median([x.get(c, 0.0) for x in v])), 3) for c in v[0]}
+    print(json.dumps({"kernel_ms_per_tick_median": out, "gossip_per_run": eng.gossip_stats()}))
     eng.close()
 
 

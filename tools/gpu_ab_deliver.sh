@@ -6,7 +6,7 @@ ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out/$TAG"
 mkdir -p "$OUT"
 cd "$ROOT"
-timeout -k 10 400 python -u tools/ab_deliver.py > "$OUT/ab.log" 2>&1
+timeout -k 10 400 python -u tools/ab_deliver.py > "$OUT/ab.log" 2>&1 || { tail -20 "$OUT/ab.log"; exit 1; }
 tail -1 "$OUT/ab.log"
 export TMPDIR=/tmp
 cd /tmp
