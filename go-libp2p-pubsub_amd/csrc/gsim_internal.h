@@ -53,6 +53,7 @@ enum : uint32_t {
     DIAG_D_NO_COMMIT = 256,     // skip the P2 credit of commits
     DIAG_H_NO_GOSSIP = 512,     // heartbeat: skip emitGossip
     DIAG_H_NO_IHAVE_STORE = 1024,   // heartbeat: choose gossip targets but do not store the marks
+    DIAG_H_NO_RECOMPUTE = 2048,     // heartbeat: emitGossip uses the snapshot score (no live recompute)
 };
 
 struct ColocArgs {

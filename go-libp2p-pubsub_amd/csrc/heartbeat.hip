@@ -60,7 +60,7 @@ struct HbArgs {
     // live Score(p) for emitGossip (score.go:265-342)
     const double *first, *invalid, *p5, *p6;
     double topic_cap, w5, w6, bp_thr, w7;
-    uint32_t diag;             // timing ablations (bit0: no emitGossip, bit1: no IHAVE store)
+    uint32_t diag;             // timing ablations (bit0: no emitGossip, bit1: no IHAVE store, bit2: no live recompute)
 };
 
 namespace {
@@ -168,36 +168,57 @@ __device__ __forceinline__ void stats_prune(const HbArgs& a, bool tracked, bool 
 // peerScore.score of one record (score.go:265-342), in the score pass's
 // operation order: the live Score(p) emitGossip uses after this heartbeat's
 // Graft/Prune changed the record (gossipsub.go:1734).
+constexpr int kScoreChunk = 2;   // topics whose record fields are loaded together
+
 __device__ double score_of_record(const HbArgs& a, uint32_t rv, uint32_t col)
 {
     if (!(a.estate[rv] & GSIM_ES_TRACKED)) return 0.0;
     double score = 0.0;
-    for (int32_t t = 0; t < a.T; ++t) {
-        const ctp_t tp = const_tp(a.tp) + t;
-        if (!tp->scored) continue;
-        const int64_t i = (int64_t)t * a.E + rv;
-        const uint8_t fl = a.tflags[i];
-        const double meshd = apply_incs(a.meshd[i], a.mcnt[i], tp->mesh_message_deliveries_cap);
-        double ts = 0.0;
-        if (fl & GSIM_TF_IN_MESH) {                                   // P1
-            double p1 = 0.0;
-            if (tp->time_in_mesh_quantum_ns != 0) p1 = (double)go_div(a.mtime[i], tp->time_in_mesh_quantum_ns);
-            if (p1 > tp->time_in_mesh_cap) p1 = tp->time_in_mesh_cap;
-            ts += p1 * tp->time_in_mesh_weight;
+    for (int32_t t0 = 0; t0 < a.T; t0 += kScoreChunk) {
+        // the records sit at rv in each topic plane, away from the row: load a
+        // chunk of topics before using any (one memory round trip per chunk)
+        uint8_t fl[kScoreChunk], mc[kScoreChunk];
+        double f[kScoreChunk], md[kScoreChunk], fa[kScoreChunk], iv[kScoreChunk];
+        int64_t mt[kScoreChunk];
+#pragma unroll
+        for (int j = 0; j < kScoreChunk; ++j) {
+            const int32_t t = t0 + j;
+            const bool ok = t < a.T && (const_tp(a.tp) + t)->scored;
+            const int64_t i = (int64_t)t * a.E + rv;
+            fl[j] = ok ? a.tflags[i] : 0;
+            mc[j] = ok ? a.mcnt[i] : 0;
+            f[j] = ok ? a.first[i] : 0.0;
+            md[j] = ok ? a.meshd[i] : 0.0;
+            fa[j] = ok ? a.fail[i] : 0.0;
+            iv[j] = ok ? a.invalid[i] : 0.0;
+            mt[j] = ok ? a.mtime[i] : 0;
         }
-        ts += a.first[i] * tp->first_message_deliveries_weight;        // P2
-        if (fl & GSIM_TF_ACTIVE) {                                     // P3
-            if (meshd < tp->mesh_message_deliveries_threshold) {
-                const double deficit = tp->mesh_message_deliveries_threshold - meshd;
-                const double p3 = deficit * deficit;
-                ts += p3 * tp->mesh_message_deliveries_weight;
+        for (int j = 0; j < kScoreChunk; ++j) {
+            const int32_t t = t0 + j;
+            if (t >= a.T) break;
+            const ctp_t tp = const_tp(a.tp) + t;
+            if (!tp->scored) continue;
+            const double meshd = apply_incs(md[j], mc[j], tp->mesh_message_deliveries_cap);
+            double ts = 0.0;
+            if (fl[j] & GSIM_TF_IN_MESH) {                                // P1
+                double p1 = 0.0;
+                if (tp->time_in_mesh_quantum_ns != 0) p1 = (double)go_div(mt[j], tp->time_in_mesh_quantum_ns);
+                if (p1 > tp->time_in_mesh_cap) p1 = tp->time_in_mesh_cap;
+                ts += p1 * tp->time_in_mesh_weight;
             }
+            ts += f[j] * tp->first_message_deliveries_weight;              // P2
+            if (fl[j] & GSIM_TF_ACTIVE) {                                  // P3
+                if (meshd < tp->mesh_message_deliveries_threshold) {
+                    const double deficit = tp->mesh_message_deliveries_threshold - meshd;
+                    const double p3 = deficit * deficit;
+                    ts += p3 * tp->mesh_message_deliveries_weight;
+                }
+            }
+            ts += fa[j] * tp->mesh_failure_penalty_weight;                 // P3b
+            const double p4 = iv[j] * iv[j];                               // P4
+            ts += p4 * tp->invalid_message_deliveries_weight;
+            score += ts * tp->topic_weight;
         }
-        ts += a.fail[i] * tp->mesh_failure_penalty_weight;             // P3b
-        const double inval = a.invalid[i];
-        const double p4 = inval * inval;                               // P4
-        ts += p4 * tp->invalid_message_deliveries_weight;
-        score += ts * tp->topic_weight;
     }
     if (a.topic_cap > 0 && score > a.topic_cap) score = a.topic_cap;
     score += a.p5[col] * a.w5;                                         // P5
@@ -230,6 +251,8 @@ __device__ bool gossip_targets(const HbArgs& a, bool cand, bool tpeer, uint32_t 
     if (factor > target) target = factor;
     if (target >= n) return cand || dup;
     // each lane holds up to two instances (candidate, fill duplicate)
+    // no fill duplicates (the usual case): one instance per lane
+    if (!__ballot(dup)) return select_smallest(a, cand, target, obs, t, P_GOSSIP, col, pos);
     uint32_t h1 = cand ? hb_key_hi(a, obs, t, P_GOSSIP, col, pos) : 0xFFFFFFFFu;
     uint32_t h2 = dup ? hb_key_hi(a, obs, t, P_GOSSIP_DUP, col, pos) : 0xFFFFFFFFu;
     uint64_t av1 = __ballot(cand), av2 = __ballot(dup);
@@ -241,8 +264,10 @@ __device__ bool gossip_targets(const HbArgs& a, bool cand, bool tpeer, uint32_t 
         const bool use1 = has1 && (!has2 || h1 <= h2);
         const uint32_t mine = use1 ? h1 : (has2 ? h2 : 0xFFFFFFFFu);
         const uint32_t mn = wave_min_u32(mine);
-        const int win = __ffsll((long long)(__ballot(mine == mn && (has1 || has2)))) - 1;
-        if (__shfl(use1, win, 64)) av1 &= ~(1ull << win); else av2 &= ~(1ull << win);
+        const bool at_min = mine == mn && (has1 || has2);
+        const int win = __ffsll((long long)__ballot(at_min)) - 1;
+        // which instance the winner used, from a ballot (no lane shuffle)
+        if ((__ballot(at_min && use1) >> win) & 1ull) av1 &= ~(1ull << win); else av2 &= ~(1ull << win);
         if (lane == win) sel = true;
     }
     return sel;
@@ -442,7 +467,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             if (a.gossip) {
                 bool gsel = false;
                 if (!(a.diag & 1) && __shfl(lp_lane, t, 64) >= (int64_t)a.tick - a.hist_gossip) {
-                    if (__ballot(dirty)) {
+                    if (__ballot(dirty) && !(a.diag & 4)) {
                         if (dirty) S_live = score_of_record(a, rv, col);
                         dirty = false;
                     }
@@ -624,7 +649,7 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.first = h->d_first; a.invalid = h->d_invalid; a.p5 = h->d_p5; a.p6 = h->d_p6;
     a.topic_cap = h->pp.topic_score_cap; a.w5 = h->pp.app_specific_weight; a.w6 = h->pp.ip_colocation_factor_weight;
     a.bp_thr = h->pp.behaviour_penalty_threshold; a.w7 = h->pp.behaviour_penalty_weight;
-    a.diag = (h->diag >> 9) & 3u;    // DIAG_H_NO_GOSSIP / DIAG_H_NO_IHAVE_STORE
+    a.diag = (h->diag >> 9) & 7u;    // DIAG_H_NO_GOSSIP / _NO_IHAVE_STORE / _NO_RECOMPUTE
     return a;
 }
 
