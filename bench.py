@@ -251,8 +251,13 @@ def main():
                         "frac": ref_gbs / HBM_PEAK_GBS, "traffic": load_traffic(args.config),
                         "kernel": "k_refresh_score<true,true>", "kernel_ms": ref_ms,
                         "algorithmic_bytes_per_launch": alg_refresh}
+        # PMC traffic of k_send (profiles/traffic.json, per launch) scaled to a tick
+        tr_send = load_traffic(args.config + ":send")
+        if tr_send is not None:
+            per_tick = tr_send["bytes_per_launch"] * launches["send"] / K
+            tr_send = dict(tr_send, bytes_per_tick=per_tick)
         roof_deliv = {"bound": "hbm", "achieved": deliv_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                      "frac": deliv_gbs / HBM_PEAK_GBS, "traffic": None,
+                      "frac": deliv_gbs / HBM_PEAK_GBS, "traffic": tr_send,
                       "kernel": "k_send+k_commit+k_accept (per tick)", "kernel_ms": deliv_ms,
                       "algorithmic_bytes_per_tick": alg_deliv}
         dominant = roof_refresh if ref_ms * launches["refresh_score"] / K >= deliv_ms else roof_deliv

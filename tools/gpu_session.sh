@@ -20,10 +20,14 @@ echo "== rocprofv3 kernel stats"
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline > "$OUT/prof.log" 2>&1
-echo "== pmc FETCH_SIZE"
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_refresh_score<true, true>" -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fetch.log" 2>&1
-echo "== pmc WRITE_SIZE"
-timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_refresh_score<true, true>" -d "$OUT/pmc_write" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write.log" 2>&1
+for K in refresh send; do
+  if [ "$K" = refresh ]; then RE="k_refresh_score<true, true>"; else RE="k_send"; fi
+  echo "== pmc FETCH_SIZE $K"
+  timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$RE" -d "$OUT/pmc_fetch_$K" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fetch_$K.log" 2>&1
+  echo "== pmc WRITE_SIZE $K"
+  timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$RE" -d "$OUT/pmc_write_$K" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write_$K.log" 2>&1
+done
 cd "$ROOT"
-python3 tools/pmc_traffic.py c3 "k_refresh_score<true, ?true>" "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/traffic.json" || true
+python3 tools/pmc_traffic.py c3 "k_refresh_score<true, ?true>" "$OUT/pmc_fetch_refresh" "$OUT/pmc_write_refresh" "$OUT/traffic.json" || true
+python3 tools/pmc_traffic.py c3:send "k_send" "$OUT/pmc_fetch_send" "$OUT/pmc_write_send" "$OUT/traffic.json" || true
 echo "== done"

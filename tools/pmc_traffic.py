@@ -47,6 +47,9 @@ def main():
     rec = {"bytes_per_launch": (2 * fk + wk) * 1024, "fetch_kib_raw": fk, "write_kib_raw": wk,
            "launches": [len(f), len(w)], "kernel_regex": kre,
            "correction": "read side x2 (gfx950 FETCH_SIZE under-count), write exact"}
+    if workload.endswith(":send"):
+        rec["calibration"] = ("k_send's accesses are 1-8 B gathers and atomics at random addresses; the x2 "
+                              "read correction is calibrated for 16-B/lane streaming reads only")
     data = {}
     if os.path.exists(out):
         data = json.load(open(out))
