@@ -585,6 +585,107 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
 }
 
 // ---------------------------------------------------------------------------
+// Connection churn between ticks (handleDeadPeers pubsub.go:711-759, the
+// new-peer case of processLoop pubsub.go:575-595): both endpoints of each
+// listed connection run the router's RemovePeer / AddPeer
+// (gossipsub.go:525-567) and the score tracer's (score.go:595-644).
+
+struct ChurnArgs {
+    const uint32_t* edges;     // [2*count] the observer's edge of each (pair, direction)
+    int32_t n2;
+    int32_t up;
+    int64_t retain;            // PeerScoreParams.RetainScore
+    uint8_t *estate, *rstate, *pen;
+    int64_t* expire;
+    double *first, *invalid;
+};
+
+// The observer's edge to the other end of each (pair, direction), by binary
+// search in the observer's sorted row; *bad = lowest pair that is not a
+// connection.
+__global__ __launch_bounds__(256) void k_churn_find(const uint32_t* row_ptr, const uint32_t* col, int64_t N,
+                                                    const uint32_t* pairs, int32_t n2, uint32_t* edges,
+                                                    uint32_t* bad)
+{
+    const int32_t q = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (q >= n2) return;
+    const uint32_t o = pairs[(q & ~1) + (q & 1)], p = pairs[(q & ~1) + 1 - (q & 1)];
+    uint32_t e = 0xFFFFFFFFu;
+    if (o < N && p < N) {
+        uint32_t lo = row_ptr[o], hi = row_ptr[o + 1];
+        const uint32_t end = hi;
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if (col[mid] < p) lo = mid + 1; else hi = mid;
+        }
+        if (lo < end && col[lo] == p) e = lo;
+    }
+    edges[q] = e;
+    if (e == 0xFFFFFFFFu) atomicMin(bad, (uint32_t)(q >> 1));
+}
+
+// Fresh (or dropped) score record r: an empty peerStats.
+__device__ void churn_reset_record(const HbArgs& a, const ChurnArgs& c, uint32_t r)
+{
+    a.bp[r] = 0.0;
+    c.expire[r] = 0;
+    c.pen[r] = 0;
+    for (int32_t t = 0; t < a.T; ++t) {
+        const int64_t i = (int64_t)t * a.E + r;
+        c.first[i] = 0.0; a.meshd[i] = 0.0; a.fail[i] = 0.0; c.invalid[i] = 0.0;
+        a.graft[i] = 0; a.mtime[i] = 0;
+        a.tflags[i] = 0;
+    }
+}
+
+// One thread per (connection, direction): the observer owning edge e, about
+// neighbour col[e]; the observer's record of it sits at rev[e].
+__global__ __launch_bounds__(256) void k_churn_apply(HbArgs a, ChurnArgs c)
+{
+    const int32_t q = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (q >= c.n2) return;
+    const uint32_t e = c.edges[q];
+    const uint32_t r = a.rev[e];
+    if (c.up) {
+        // AddPeer: connected; a retained record comes back as it is
+        c.rstate[e] = (uint8_t)(c.rstate[e] | GSIM_ES_CONNECTED);
+        if (!(c.estate[r] & GSIM_ES_TRACKED)) churn_reset_record(a, c, r);
+        c.estate[r] = GSIM_ES_TRACKED | GSIM_ES_CONNECTED;
+        return;
+    }
+    // router RemovePeer: out of every mesh without PRUNE, pending control dropped
+    for (int32_t t = 0; t < a.T; ++t) {
+        const int64_t i = (int64_t)t * a.E + e;
+        a.mflags[i] = (uint8_t)(a.mflags[i] & ~GSIM_TF_MESH);
+        a.ctl_in[i] = 0;
+        a.ctl_out[i] = 0;
+    }
+    c.rstate[e] = (uint8_t)(c.rstate[e] & ~GSIM_ES_CONNECTED);
+    // peerScore.RemovePeer: positive scores are dropped, the rest retained
+    if (!(c.estate[r] & GSIM_ES_TRACKED)) return;
+    if (score_of_record(a, r, a.col[e]) > 0) {
+        churn_reset_record(a, c, r);
+        c.estate[r] = 0;
+        return;
+    }
+    for (int32_t t = 0; t < a.T; ++t) {
+        const ctp_t tp = const_tp(a.tp) + t;
+        if (!tp->scored) continue;
+        const int64_t i = (int64_t)t * a.E + r;
+        c.first[i] = 0.0;
+        const uint8_t fl = a.tflags[i];
+        const double thr = tp->mesh_message_deliveries_threshold;
+        if ((fl & GSIM_TF_IN_MESH) && (fl & GSIM_TF_ACTIVE) && a.meshd[i] < thr) {
+            const double deficit = thr - a.meshd[i];
+            a.fail[i] = a.fail[i] + deficit * deficit;
+        }
+        a.tflags[i] = (uint8_t)(fl & ~GSIM_TF_IN_MESH);
+    }
+    c.estate[r] = GSIM_ES_TRACKED;
+    c.expire[r] = a.now + c.retain;
+}
+
+// ---------------------------------------------------------------------------
 // host side
 
 int alloc_extra(gsim_handle* h)
@@ -707,6 +808,70 @@ int gsim_handle_control(gsim_handle* h, int32_t round, int64_t now)
     ProfScope ps(h, GSIM_K_CONTROL);
     hipLaunchKernelGGL(k_handle_control, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_handle_control");
+}
+
+
+int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, int32_t up, int64_t now)
+{
+    if (!h) return GSIM_EINVAL;
+    if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
+    if (h->e == 0 || !h->x) { h->err = "no graph loaded"; return GSIM_ESTATE; }
+    if (count < 0 || (count > 0 && !pairs)) { h->err = "bad connection list"; return GSIM_EINVAL; }
+    if (count == 0) return GSIM_OK;
+    {
+        // a connection listed twice would be handled by two threads at once
+        std::vector<uint64_t> key((size_t)count);
+        for (int32_t q = 0; q < count; ++q) {
+            const uint32_t u = pairs[2 * q], v = pairs[2 * q + 1];
+            key[(size_t)q] = ((uint64_t)std::min(u, v) << 32) | std::max(u, v);
+        }
+        std::sort(key.begin(), key.end());
+        if (std::adjacent_find(key.begin(), key.end()) != key.end()) {
+            h->err = "a connection is listed twice";
+            return GSIM_EINVAL;
+        }
+    }
+    int rc = deliver_flush(h);              // pending first deliveries precede the removal
+    if (!rc) rc = materialize_mcnt(h);      // the P3b test reads meshMessageDeliveries
+    if (rc) return rc;
+    const int32_t n2 = 2 * count;
+    uint32_t *d_pairs = nullptr, *d_edges = nullptr, *d_bad = nullptr;
+    hipError_t e = hipMalloc((void**)&d_pairs, sizeof(uint32_t) * (size_t)n2);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_edges, sizeof(uint32_t) * (size_t)n2);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_bad, sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemcpyAsync(d_pairs, pairs, sizeof(uint32_t) * (size_t)n2, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d_bad, 0xFF, sizeof(uint32_t), h->stream);
+    uint32_t bad = 0xFFFFFFFFu;
+    const int grid = (n2 + 255) / 256;
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_churn_find, dim3(grid), dim3(256), 0, h->stream, (const uint32_t*)h->d_row_ptr,
+                           (const uint32_t*)h->d_col, h->n, (const uint32_t*)d_pairs, n2, d_edges, d_bad);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(&bad, d_bad, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess && bad == 0xFFFFFFFFu) {
+        HbArgs a = make_hb_args(h, 0, now, 0);   // ctl_in/ctl_out cover both inbox planes
+        ChurnArgs c{};
+        c.edges = d_edges; c.n2 = n2; c.up = up ? 1 : 0; c.retain = h->pp.retain_score_ns;
+        c.estate = h->d_estate; c.rstate = h->d_rstate; c.pen = h->d_pen; c.expire = h->d_expire;
+        c.first = h->d_first; c.invalid = h->d_invalid;
+        hipLaunchKernelGGL(k_churn_apply, dim3(grid), dim3(256), 0, h->stream, a, c);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    }
+    (void)hipFree(d_pairs);
+    (void)hipFree(d_edges);
+    (void)hipFree(d_bad);
+    if (e != hipSuccess) return hip_check(h, e, "gsim_set_connections");
+    if (bad != 0xFFFFFFFFu) {
+        h->err = "pair " + std::to_string(bad) + " is not a connection";
+        return GSIM_EINVAL;
+    }
+    h->p6_dirty = true;          // the tracked set (and so the IP sets) changed
+    if (!up) h->maybe_retained = true;
+    h->score_version++;          // connected / tracked bits feed the delivery state
+    return GSIM_OK;
 }
 
 }  // extern "C"

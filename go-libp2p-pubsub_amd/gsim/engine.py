@@ -252,6 +252,13 @@ class Engine:
         f = np.ascontiguousarray(flags, dtype=np.uint8)
         self._check(self.lib.gsim_set_peer_behaviour(self.h, _ptr(f)))
 
+    def set_connections(self, pairs, up: bool, now: int):
+        """Connections (a, b) going down or up between ticks, both endpoints
+        notified: the router's and the score tracer's RemovePeer / AddPeer
+        (gsim_set_connections; gossipsub.go:525-567, score.go:595-644)."""
+        p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint32).reshape(-1, 2))
+        self._check(self.lib.gsim_set_connections(self.h, _ptr(p), int(p.shape[0]), 1 if up else 0, int(now)))
+
     def gossip_stats(self) -> dict:
         out = np.zeros(4, dtype=np.int64)
         self._check(self.lib.gsim_gossip_stats(self.h, _ptr(out)))

@@ -226,6 +226,21 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now_ns);
  * of round+1. */
 int gsim_handle_control(gsim_handle* h, int32_t round, int64_t now_ns);
 
+/* Connections going down (up = 0) or up (up = 1) between two ticks, both
+ * endpoints notified (handleDeadPeers pubsub.go:711-759; the new-peer case of
+ * processLoop pubsub.go:575-595).  pairs = count (peer a, peer b) u32 pairs,
+ * each an existing CSR connection, each at most once.
+ *   down: router RemovePeer (gossipsub.go:554-567): out of every mesh without
+ *         PRUNE, pending control dropped, backoff kept; score tracer
+ *         RemovePeer (score.go:611-644): a positive live score is dropped,
+ *         otherwise retained until now + RetainScore with P2 reset and the
+ *         P3b penalty applied.
+ *   up:   router AddPeer (gossipsub.go:525-552), peerScore.AddPeer
+ *         (score.go:595-609): a retained record is reused, else a fresh one.
+ * The removed peer's live score uses P6 as last derived.  GSIM_EINVAL if a
+ * pair is not a connection or is listed twice (nothing is changed then). */
+int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, int32_t up, int64_t now_ns);
+
 /* ---- message propagation ------------------------------ */
 /* Rounds are numbered globally: round g belongs to heartbeat tick g / rounds
  * and happens at virtual time

@@ -125,6 +125,8 @@ void   orc_graft(orc_net* s, int64_t e, int32_t topic, int64_t now); /* score.go
 void   orc_prune(orc_net* s, int64_t e, int32_t topic);          /* score.go:669-691 */
 void   orc_add_peer(orc_net* s, int64_t e);                      /* score.go:595-609 */
 void   orc_remove_peer(orc_net* s, int64_t e, int64_t now);      /* score.go:611-644 */
+/* connection churn between ticks, both endpoints (oracle_net.c) */
+int32_t orc_churn(orc_net* s, const uint32_t* pairs, int32_t count, int32_t up, int64_t now);
 void   orc_set_topic_params(orc_net* s, int32_t topic, gsim_topic_score_params* tp_slot,
                             const gsim_topic_score_params* np); /* score.go:201-241 */
 void   orc_mark_first(orc_net* s, int64_t e, int32_t topic);     /* score.go:919-946 */

@@ -339,3 +339,54 @@ int64_t orc_handle_control(orc_net* s, int32_t round, int64_t now)
     }
     return handled;
 }
+
+/* ---- connection churn ---------------------------------------------------- */
+
+static int64_t find_edge(const orc_net* s, uint32_t i, uint32_t j)
+{
+    uint32_t lo = s->row_ptr[i], hi = s->row_ptr[i + 1];
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if (s->col[mid] < j) lo = mid + 1; else hi = mid;
+    }
+    return (lo < s->row_ptr[i + 1] && s->col[lo] == j) ? (int64_t)lo : -1;
+}
+
+/* Connections going down or up between two ticks, both endpoints notified
+ * (handleDeadPeers pubsub.go:711-759 / the new-peer case of processLoop
+ * pubsub.go:575-595).
+ * Down: the router's RemovePeer (gossipsub.go:554-567: out of every mesh,
+ * no PRUNE, pending control dropped, backoff kept) and the score tracer's
+ * RemovePeer (score.go:611-644: drop a positive score, else retain with P2
+ * reset and the P3b penalty).  Up: the router's AddPeer (gossipsub.go:525-552)
+ * and peerScore.AddPeer (score.go:595-609).  The live score of a removed peer
+ * uses the stored P6 (ipColocationFactor as last derived).  Returns the index
+ * of the first pair that is not a connection, or -1. */
+int32_t orc_churn(orc_net* s, const uint32_t* pairs, int32_t count, int32_t up, int64_t now)
+{
+    for (int32_t q = 0; q < count; ++q) {
+        const uint32_t a = pairs[2 * q], b = pairs[2 * q + 1];
+        if (a >= s->n || b >= s->n || find_edge(s, a, b) < 0) return q;
+    }
+    for (int32_t q = 0; q < count; ++q) {
+        for (int d = 0; d < 2; ++d) {
+            const uint32_t o = pairs[2 * q + d], p = pairs[2 * q + 1 - d];
+            const int64_t e = find_edge(s, o, p);
+            if (up) {
+                orc_add_peer(s, e);
+                continue;
+            }
+            for (int32_t t = 0; t < s->t; ++t) {
+                const int64_t i = (int64_t)t * s->e + e;
+                s->tflags[i] &= (uint8_t)~GSIM_TF_MESH;
+                if (s->ctl) {
+                    s->ctl[i] = 0;
+                    s->ctl[(int64_t)s->t * s->e + i] = 0;
+                }
+            }
+            orc_remove_peer(s, e, now);
+            s->estate[e] &= (uint8_t)~GSIM_ES_CONNECTED;
+        }
+    }
+    return -1;
+}

@@ -65,6 +65,7 @@ def load():
             "orc_prune": (None, [P, c_int64, c_int32]),
             "orc_add_peer": (None, [P, c_int64]),
             "orc_remove_peer": (None, [P, c_int64, c_int64]),
+            "orc_churn": (c_int32, [P, c_void_p, c_int32, c_int32, c_int64]),
             "orc_set_topic_params": (None, [P, c_int32, c_void_p, c_void_p]),
             "orc_mark_first": (None, [P, c_int64, c_int32]),
             "orc_mark_duplicate": (None, [P, c_int64, c_int32, c_int32, c_int64, c_int64]),
@@ -179,6 +180,12 @@ class NetState:
     def copy_fields_from(self, other):
         for f in self.TOPIC_FIELDS + self.EDGE_FIELDS:
             getattr(self, f)[...] = getattr(other, f)
+
+    def churn(self, pairs, up, now):
+        """orc_churn: connections going down / up between ticks, both endpoints."""
+        p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint32).reshape(-1, 2))
+        bad = load().orc_churn(self.view(), _p(p), int(p.shape[0]), 1 if up else 0, int(now))
+        assert bad < 0, f"pair {bad} is not a connection"
 
     def push_to_engine(self, eng):
         for f in self.TOPIC_FIELDS + self.EDGE_FIELDS:
