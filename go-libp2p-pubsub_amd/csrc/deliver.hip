@@ -111,6 +111,12 @@ struct RoundArgs {
     int32_t* slot_last;
     uint32_t* err;                 // [0] responses queued, [1] overflow, [2] ring slot reused too early
     int32_t reuse_guard;           // rounds a slot must stay unpublished after its last activity
+    // the origin's own Publish (gossipsub.go:989-1028): flood, mesh or fanout
+    const uint64_t* sub;
+    const double* score;           // snapshot, record order (flood publish filter)
+    const uint32_t* rev;
+    int32_t flood;
+    double pub_thr;
 };
 
 __device__ __forceinline__ int64_t round_time(const RoundArgs& a, int64_t g)
@@ -336,6 +342,10 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
             // (2) forward
             const uint32_t from_l = (uint32_t)c0 & kPeerMask;
             const int32_t t = (int32_t)a.mtopic[m];
+            // the origin's own Publish goes to its mesh, to its fanout when it
+            // has not joined the topic, or floods every topic peer with score
+            // >= publishThreshold (gossipsub.go:989-1028); forwarders use their mesh
+            const uint8_t o_want = ((a.sub[origin] >> t) & 1ull) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
             const ctp_t tp = tpa + t;
             const bool scored_t = tp->scored != 0;
             const int64_t window = tp->mesh_message_deliveries_window_ns;
@@ -367,8 +377,14 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
                     i2 = a.col[e2]; mf2 = a.mflags[plane + e2];
                     ds2 = rowst ? a.dstate[e2] : (uint8_t)0xFF; tf2 = rowst ? a.tflags[plane + e2] : GSIM_TF_IN_MESH;
                 }
-                const bool tg1 = v1 && (mf1 & GSIM_TF_MESH) && (ds1 & GSIM_DS_CONNECTED) && i1 != f1 && i1 != origin;
-                const bool tg2 = v2 && (mf2 & GSIM_TF_MESH) && (ds2 & GSIM_DS_CONNECTED) && i2 != f2 && i2 != origin;
+                bool sel1 = (mf1 & (j1 == origin ? o_want : GSIM_TF_MESH)) != 0;
+                bool sel2 = (mf2 & (j2 == origin ? o_want : GSIM_TF_MESH)) != 0;
+                if (a.flood) {
+                    if (v1 && j1 == origin) sel1 = ((a.sub[i1] >> t) & 1ull) && a.score[a.rev[e1]] >= a.pub_thr;
+                    if (v2 && j2 == origin) sel2 = ((a.sub[i2] >> t) & 1ull) && a.score[a.rev[e2]] >= a.pub_thr;
+                }
+                const bool tg1 = v1 && sel1 && (ds1 & GSIM_DS_CONNECTED) && i1 != f1 && i1 != origin;
+                const bool tg2 = v2 && sel2 && (ds2 & GSIM_DS_CONNECTED) && i2 != f2 && i2 != origin;
                 const bool ok1 = tg1 && (ds1 & GSIM_DS_ACCEPT), ok2 = tg2 && (ds2 & GSIM_DS_ACCEPT);
                 n_gray += (tg1 && !ok1) + (tg2 && !ok2);     // AcceptFrom: graylisted sender
                 n_acc += ok1 + ok2;
@@ -973,6 +989,9 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.slot_last = d->d_slot_last;
     a.err = d->d_nresp;
     a.reuse_guard = (std::max(h->gp.history_gossip, h->gp.history_length) + d->prom_ticks + 2) * d->cfg.rounds;
+    a.sub = h->d_sub; a.score = h->d_score; a.rev = h->d_rev;
+    a.flood = h->gp.flood_publish ? 1 : 0;
+    a.pub_thr = h->th.publish_threshold;
     return a;
 }
 
@@ -1227,7 +1246,10 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
     hipLaunchKernelGGL(k_publish, dim3((count + 255) / 256), dim3(256), 0, h->stream, a,
                        (const gsim_msg*)d->d_pub, count);
     d->next_round = round;
-    return hip_check(h, hipGetLastError(), "k_publish");
+    int rc = hip_check(h, hipGetLastError(), "k_publish");
+    // origins that have not joined the topic publish to their fanout
+    if (!rc) rc = launch_fanout_publish(h, d->d_pub, count, round, round_time_host(d, round));
+    return rc;
 }
 
 int gsim_round(gsim_handle* h, int64_t round)

@@ -500,7 +500,7 @@ __global__ __launch_bounds__(256) void k_tflags_compose(const uint8_t* rec, cons
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += stride) {
         const int64_t p = x / E, e = x - p * E;
-        out[x] = (uint8_t)((rec[p * E + rev[e]] & (GSIM_TF_IN_MESH | GSIM_TF_ACTIVE)) | (mf[x] & GSIM_TF_MESH));
+        out[x] = (uint8_t)((rec[p * E + rev[e]] & (GSIM_TF_IN_MESH | GSIM_TF_ACTIVE)) | (mf[x] & (GSIM_TF_MESH | GSIM_TF_FANOUT)));
     }
 }
 
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(256) void k_tflags_split(const uint8_t* in, uint8_t
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += stride) {
         const int64_t p = x / E, e = x - p * E;
         rec[x] = (uint8_t)(in[p * E + rev[e]] & (GSIM_TF_IN_MESH | GSIM_TF_ACTIVE));
-        mf[x] = (uint8_t)(in[x] & GSIM_TF_MESH);
+        mf[x] = (uint8_t)(in[x] & (GSIM_TF_MESH | GSIM_TF_FANOUT));
     }
 }
 

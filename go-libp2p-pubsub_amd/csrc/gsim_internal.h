@@ -212,6 +212,8 @@ int launch_refresh_scores(gsim_handle* h, int64_t now);
 int launch_compute_scores(gsim_handle* h);
 int refresh_accept(gsim_handle* h);   // recompute d_dstate if the snapshot changed
 int materialize_mcnt(gsim_handle* h); // apply pending meshd increments everywhere
+// Publish's fanout branch for a batch already on the device (heartbeat.hip)
+int launch_fanout_publish(gsim_handle* h, const gsim_msg* d_pub, int32_t count, int64_t g, int64_t now);
 
 // Delivery state byte per edge index e: what one forwarded
 // copy over e needs besides the topic planes.

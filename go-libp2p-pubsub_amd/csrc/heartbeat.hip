@@ -21,6 +21,8 @@ using namespace gsim;
 
 struct Extra {
     uint8_t* d_ctl = nullptr;   // [2][T][E] control inbox by round parity
+    int64_t* d_lastpub = nullptr;      // [N][T] gs.lastpub (ns), 0 = none
+    uint64_t* d_fantopics = nullptr;   // [N] bit t: gs.fanout[t] exists
     uint32_t max_degree = 0;
     uint64_t seed = 0x9E3779B97F4A7C15ull;
 };
@@ -61,6 +63,11 @@ struct HbArgs {
     const double *first, *invalid, *p5, *p6;
     double topic_cap, w5, w6, bp_thr, w7;
     uint32_t diag;             // timing ablations (bit0: no emitGossip, bit1: no IHAVE store, bit2: no live recompute)
+    // fanout (gossipsub.go:1011-1028, 1558-1596); router bit GSIM_TF_FANOUT in mflags
+    int64_t* lastpub;          // [N][T]
+    uint64_t* fan_topics;      // [N]
+    double pub_thr;
+    int64_t fanout_ttl;
 };
 
 namespace {
@@ -464,6 +471,11 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             // message of the topic in the last HistoryGossip ticks.  The
             // choice is stored in the sender's row (enqueueGossip); every
             // joined topic's plane is rewritten each heartbeat.
+            // emitGossip(topic, mesh) (gossipsub.go:1554-1556, 1711-1775):
+            // only if GetGossipIDs(topic) is non-empty, i.e. this peer put a
+            // message of the topic in the last HistoryGossip ticks.  The
+            // choice is stored in the sender's row (enqueueGossip); every
+            // joined topic's plane is rewritten each heartbeat.
             if (a.gossip) {
                 bool gsel = false;
                 if (!(a.diag & 1) && __shfl(lp_lane, t, 64) >= (int64_t)a.tick - a.hist_gossip) {
@@ -483,6 +495,73 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
                 }
             }
           }
+        }
+    }
+}
+
+// Fanout expiry and maintenance (gossipsub.go:1558-1596), run after
+// k_heartbeat (the reference handles fanouts after every joined topic): drop
+// the fanouts not published to for FanoutTTL; for each remaining fanout topic
+// (ascending) drop peers that left the topic or score below
+// publishThreshold, top up to D, and emitGossip excluding the fanout peers
+// with the live score after this heartbeat's Graft/Prune.  One wave per
+// observer; observers without fanout state leave after two loads.
+__global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int64_t obs = (int64_t)blockIdx.x * 4 + wid; obs < a.N; obs += (int64_t)gridDim.x * 4) {
+        const int64_t lpub = lane < a.T ? a.lastpub[obs * a.T + lane] : 0;
+        const uint64_t expired = __ballot(lpub != 0 && lpub + a.fanout_ttl < a.now);
+        const uint64_t fant0 = a.fan_topics[obs];
+        if (!expired && !fant0) continue;                       // wave-uniform
+        const uint32_t b = a.row_ptr[obs];
+        const int deg = (int)(a.row_ptr[obs + 1] - b);
+        const bool valid = lane < deg;
+        const uint32_t e = b + (uint32_t)lane;
+        if ((expired >> lane) & 1ull) a.lastpub[obs * a.T + lane] = 0;
+        for (uint64_t q = expired & fant0; q; q &= q - 1) {
+            const int64_t i = (int64_t)(__ffsll((long long)q) - 1) * a.E + e;
+            if (valid) {
+                const uint8_t fl = a.mflags[i];
+                if (fl & GSIM_TF_FANOUT) a.mflags[i] = (uint8_t)(fl & ~GSIM_TF_FANOUT);
+                if (a.gossip) a.gsel[i] = 0;                    // no more gossip for it
+            }
+        }
+        const uint64_t fant = fant0 & ~expired;
+        if (lane == 0 && fant != fant0) a.fan_topics[obs] = fant;
+        if (!fant) continue;
+        const uint32_t col = valid ? a.col[e] : 0u;
+        const uint32_t rv = valid ? a.rev[e] : 0u;
+        const bool conn = valid && (a.rstate[e] & GSIM_ES_CONNECTED);
+        const double S = valid ? a.score[rv] : 0.0;
+        const uint64_t subj = valid ? a.sub[col] : 0ull;
+        const int32_t lp_lane = (a.gossip && lane < a.T) ? a.lastput[(int64_t)lane * a.N + obs] : -1;
+        double S_live = 0.0;
+        bool have_live = false;
+        for (uint64_t q = fant; q; q &= q - 1) {
+            const int32_t t = __ffsll((long long)q) - 1;
+            const int64_t i = (int64_t)t * a.E + e;
+            const uint8_t fl = valid ? a.mflags[i] : 0;
+            const bool tpeer = conn && ((subj >> t) & 1ull);
+            bool inf = (fl & GSIM_TF_FANOUT) && tpeer && S >= a.pub_thr;
+            const int have = __popcll(ballot(inf));
+            if (have < a.D) {
+                const bool cand = tpeer && !inf && S >= a.pub_thr;
+                if (select_smallest(a, cand, a.D - have, (uint32_t)obs, t, P_FANOUT, col, (uint32_t)lane)) inf = true;
+            }
+            const uint8_t nf = inf ? (uint8_t)(fl | GSIM_TF_FANOUT) : (uint8_t)(fl & ~GSIM_TF_FANOUT);
+            if (valid && nf != fl) a.mflags[i] = nf;
+            if (!a.gossip) continue;
+            bool gsel = false;
+            if (__shfl(lp_lane, t, 64) >= (int64_t)a.tick - a.hist_gossip) {
+                if (!have_live) {                               // live Score(p), gossipsub.go:1734
+                    if (valid) S_live = score_of_record(a, rv, col);
+                    have_live = true;
+                }
+                const bool gcand = tpeer && !inf && S_live >= a.gossip_thr;
+                gsel = gossip_targets(a, gcand, tpeer, (uint32_t)obs, t, col, (uint32_t)lane);
+            }
+            if (valid) a.gsel[i] = gsel ? 1 : 0;
         }
     }
 }
@@ -656,7 +735,7 @@ __global__ __launch_bounds__(256) void k_churn_apply(HbArgs a, ChurnArgs c)
     // router RemovePeer: out of every mesh without PRUNE, pending control dropped
     for (int32_t t = 0; t < a.T; ++t) {
         const int64_t i = (int64_t)t * a.E + e;
-        a.mflags[i] = (uint8_t)(a.mflags[i] & ~GSIM_TF_MESH);
+        a.mflags[i] = (uint8_t)(a.mflags[i] & ~(GSIM_TF_MESH | GSIM_TF_FANOUT));
         a.ctl_in[i] = 0;
         a.ctl_out[i] = 0;
     }
@@ -685,6 +764,44 @@ __global__ __launch_bounds__(256) void k_churn_apply(HbArgs a, ChurnArgs c)
     c.expire[r] = a.now + c.retain;
 }
 
+// Publish's fanout branch (gossipsub.go:1011-1028), one wave per published
+// message whose origin has not joined the topic: with no fanout peers yet,
+// getPeers(topic, D, score >= publishThreshold) becomes the fanout (Philox
+// counter word 0 = the round, a.tick); then lastpub = now.  Of several
+// messages of one (origin, topic) in a batch the first does the selection
+// (the others would find the fanout non-empty).
+__global__ __launch_bounds__(256) void k_fanout_publish(HbArgs a, const gsim_msg* pub, int32_t count)
+{
+    const int lane = threadIdx.x & 63;
+    const int32_t k = (int32_t)blockIdx.x * 4 + (int32_t)(threadIdx.x >> 6);
+    if (k >= count) return;                                   // wave-uniform
+    const uint32_t o = pub[k].origin;
+    const int32_t t = (int32_t)pub[k].topic;
+    if ((a.sub[o] >> t) & 1ull) return;                       // joined: it publishes to its mesh
+    bool dup = false;
+    for (int32_t q = lane; q < k; q += 64) dup |= pub[q].origin == o && (int32_t)pub[q].topic == t;
+    if (__ballot(dup)) return;
+    const uint32_t b = a.row_ptr[o];
+    const int deg = (int)(a.row_ptr[o + 1] - b);
+    const bool valid = lane < deg;
+    const uint32_t e = b + (uint32_t)lane;
+    const int64_t i = (int64_t)t * a.E + e;
+    const uint8_t fl = valid ? a.mflags[i] : 0;
+    const bool have = ((a.fan_topics[o] >> t) & 1ull) && __ballot((fl & GSIM_TF_FANOUT) != 0) != 0;
+    if (!have) {
+        const uint32_t col = valid ? a.col[e] : 0u;
+        const bool conn = valid && (a.rstate[e] & GSIM_ES_CONNECTED);
+        const bool tpeer = conn && ((a.sub[col] >> t) & 1ull);
+        const double S = valid ? a.score[a.rev[e]] : 0.0;
+        const bool cand = tpeer && !(fl & GSIM_TF_FANOUT) && S >= a.pub_thr;
+        const bool sel = select_smallest(a, cand, a.D, o, t, P_FANOUT_NEW, col, (uint32_t)lane);
+        if (valid && sel) a.mflags[i] = (uint8_t)(fl | GSIM_TF_FANOUT);
+        const bool any = __ballot(sel) != 0;
+        if (lane == 0 && any) atomicOr(reinterpret_cast<unsigned long long*>(a.fan_topics + o), 1ull << t);
+    }
+    if (lane == 0) a.lastpub[(int64_t)o * a.T + t] = a.now;
+}
+
 // ---------------------------------------------------------------------------
 // host side
 
@@ -699,6 +816,14 @@ int alloc_extra(gsim_handle* h)
     h->bytes_allocated += bytes;
     e = hipMemsetAsync(h->x->d_ctl, 0, bytes, h->stream);
     if (e != hipSuccess) return hip_check(h, e, "memset ctl");
+    const size_t lp_bytes = sizeof(int64_t) * (size_t)h->n * (size_t)std::max(1, h->t);
+    e = hipMalloc((void**)&h->x->d_lastpub, lp_bytes);
+    if (e == hipSuccess) e = hipMalloc((void**)&h->x->d_fantopics, sizeof(uint64_t) * (size_t)h->n);
+    if (e != hipSuccess) return hip_check(h, e, "hipMalloc fanout");
+    h->bytes_allocated += lp_bytes + sizeof(uint64_t) * (size_t)h->n;
+    e = hipMemsetAsync(h->x->d_lastpub, 0, lp_bytes, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(h->x->d_fantopics, 0, sizeof(uint64_t) * (size_t)h->n, h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "memset fanout");
     std::vector<uint32_t> rp((size_t)h->n + 1);
     e = hipMemcpy(rp.data(), h->d_row_ptr, sizeof(uint32_t) * rp.size(), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_check(h, e, "row_ptr readback");
@@ -713,6 +838,8 @@ void free_extra(gsim_handle* h)
 {
     if (!h->x) return;
     if (h->x->d_ctl) (void)hipFree(h->x->d_ctl);
+    if (h->x->d_lastpub) (void)hipFree(h->x->d_lastpub);
+    if (h->x->d_fantopics) (void)hipFree(h->x->d_fantopics);
     delete h->x;
     h->x = nullptr;
 }
@@ -721,6 +848,14 @@ bool extra_field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r)
 {
     if (f == GSIM_F_CTL && h->x && h->x->d_ctl) {
         *r = {h->x->d_ctl, 2 * (size_t)h->e * (size_t)std::max(1, h->t)};
+        return true;
+    }
+    if (f == GSIM_F_LASTPUB && h->x && h->x->d_lastpub) {
+        *r = {h->x->d_lastpub, sizeof(int64_t) * (size_t)h->n * (size_t)std::max(1, h->t)};
+        return true;
+    }
+    if (f == GSIM_F_FANOUT_TOPICS && h->x && h->x->d_fantopics) {
+        *r = {h->x->d_fantopics, sizeof(uint64_t) * (size_t)h->n};
         return true;
     }
     return false;
@@ -751,6 +886,8 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.topic_cap = h->pp.topic_score_cap; a.w5 = h->pp.app_specific_weight; a.w6 = h->pp.ip_colocation_factor_weight;
     a.bp_thr = h->pp.behaviour_penalty_threshold; a.w7 = h->pp.behaviour_penalty_weight;
     a.diag = (h->diag >> 9) & 7u;    // DIAG_H_NO_GOSSIP / _NO_IHAVE_STORE / _NO_RECOMPUTE
+    a.lastpub = h->x->d_lastpub; a.fan_topics = h->x->d_fantopics;
+    a.pub_thr = h->th.publish_threshold; a.fanout_ttl = h->gp.fanout_ttl_ns;
     return a;
 }
 
@@ -770,6 +907,14 @@ static int check_degree(gsim_handle* h)
 }
 
 uint64_t gsim_get_seed(const gsim_handle* h) { return h->x ? h->x->seed : 0; }
+
+int launch_fanout_publish(gsim_handle* h, const gsim_msg* d_pub, int32_t count, int64_t g, int64_t now)
+{
+    if (h->gp.flood_publish || count <= 0 || !h->x || !h->x->d_lastpub) return GSIM_OK;
+    HbArgs a = make_hb_args(h, (uint64_t)g, now, 0);
+    hipLaunchKernelGGL(k_fanout_publish, dim3((count + 3) / 4), dim3(256), 0, h->stream, a, d_pub, count);
+    return hip_check(h, hipGetLastError(), "k_fanout_publish");
+}
 
 extern "C" {
 
@@ -794,6 +939,7 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     HbArgs a = make_hb_args(h, tick, now, 1);
     ProfScope ps(h, GSIM_K_HEARTBEAT);
     hipLaunchKernelGGL(k_heartbeat, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a);
+    hipLaunchKernelGGL(k_fanout_heartbeat, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_heartbeat");
 }
 

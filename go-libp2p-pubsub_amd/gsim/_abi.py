@@ -22,11 +22,12 @@ GSIM_ERANGE = -34
 GSIM_ESTATE = -71
 
 (F_FIRST, F_MESHD, F_FAIL, F_INVALID, F_GRAFT_TIME, F_MESH_TIME, F_TFLAGS, F_BP, F_ESTATE,
- F_EXPIRE, F_P6, F_SCORE, F_BACKOFF, F_CTL, F_SEEN, F_LASTPUT) = range(16)
+ F_EXPIRE, F_P6, F_SCORE, F_BACKOFF, F_CTL, F_SEEN, F_LASTPUT, F_LASTPUB, F_FANOUT_TOPICS) = range(18)
 
 TF_IN_MESH = 0x01
 TF_ACTIVE = 0x02
 TF_MESH = 0x04
+TF_FANOUT = 0x08
 CTL_GRAFT = 0x01
 CTL_PRUNE = 0x02
 CTL_NOPX = 0x04
@@ -80,7 +81,7 @@ class CGossipSubParams(Structure):
         ("connection_timeout_ns", c_int64), ("direct_connect_ticks", c_uint64),
         ("direct_connect_initial_delay_ns", c_int64), ("opportunistic_graft_ticks", c_uint64),
         ("opportunistic_graft_peers", c_int32), ("max_ihave_length", c_int32),
-        ("graft_flood_threshold_ns", c_int64), ("max_ihave_messages", c_int32), ("_pad0", c_int32),
+        ("graft_flood_threshold_ns", c_int64), ("max_ihave_messages", c_int32), ("flood_publish", c_int32),
         ("iwant_followup_time_ns", c_int64),
     ]
 

@@ -21,6 +21,7 @@ _FIELD_DTYPES = {
     _abi.F_GRAFT_TIME: np.int64, _abi.F_MESH_TIME: np.int64, _abi.F_TFLAGS: np.uint8, _abi.F_BP: np.float64,
     _abi.F_ESTATE: np.uint8, _abi.F_EXPIRE: np.int64, _abi.F_P6: np.float64, _abi.F_SCORE: np.float64,
     _abi.F_BACKOFF: np.int64, _abi.F_CTL: np.uint8, _abi.F_SEEN: np.uint32, _abi.F_LASTPUT: np.int32,
+    _abi.F_LASTPUB: np.int64, _abi.F_FANOUT_TOPICS: np.uint64,
 }
 TOPIC_FIELDS = {_abi.F_FIRST, _abi.F_MESHD, _abi.F_FAIL, _abi.F_INVALID, _abi.F_GRAFT_TIME,
                 _abi.F_MESH_TIME, _abi.F_TFLAGS, _abi.F_BACKOFF}
@@ -193,6 +194,10 @@ class Engine:
             return (self._msg_cfg.ring, self.net.n)
         if f == _abi.F_LASTPUT:
             return (max(1, len(self.topics)), self.net.n)
+        if f == _abi.F_LASTPUB:
+            return (self.net.n, max(1, len(self.topics)))
+        if f == _abi.F_FANOUT_TOPICS:
+            return (self.net.n,)
         return (max(1, len(self.topics)), e) if f in TOPIC_FIELDS else (e,)
 
     # -- heartbeat / control ------------------------------------------------------

@@ -184,6 +184,8 @@ class GossipSubParams:
     MaxIHaveLength: int = 5000
     MaxIHaveMessages: int = 10
     IWantFollowupTime: int = 3 * Second
+    # router option WithFloodPublish (gossipsub.go:321-334), not a GossipSubParams field
+    FloodPublish: bool = False
 
     def to_c(self) -> _abi.CGossipSubParams:
         c = _abi.CGossipSubParams()
@@ -200,6 +202,7 @@ class GossipSubParams:
         c.opportunistic_graft_ticks, c.opportunistic_graft_peers = (self.OpportunisticGraftTicks,
                                                                      self.OpportunisticGraftPeers)
         c.max_ihave_length, c.graft_flood_threshold_ns = self.MaxIHaveLength, self.GraftFloodThreshold
+        c.flood_publish = 1 if self.FloodPublish else 0
         c.max_ihave_messages, c.iwant_followup_time_ns = self.MaxIHaveMessages, self.IWantFollowupTime
         return c
 

@@ -119,7 +119,7 @@ typedef struct gsim_gossipsub_params {
     int32_t max_ihave_length;
     int64_t graft_flood_threshold_ns;
     int32_t max_ihave_messages;
-    int32_t _pad0;
+    int32_t flood_publish;   /* router option WithFloodPublish (gossipsub.go:321-334); this fork's default is 0 */
     int64_t iwant_followup_time_ns;
 } gsim_gossipsub_params;
 
@@ -321,7 +321,7 @@ typedef enum gsim_field {
     GSIM_F_INVALID,       /* f64 [T][E] invalidMessageDeliveries        score.go:61 */
     GSIM_F_GRAFT_TIME,    /* i64 [T][E] graftTime (ns)                  score.go:42 */
     GSIM_F_MESH_TIME,     /* i64 [T][E] meshTime (ns)                   score.go:46 */
-    GSIM_F_TFLAGS,        /* u8  [T][E] bit0 inMesh, bit1 meshMessageDeliveriesActive */
+    GSIM_F_TFLAGS,        /* u8  [T][E] bit0 inMesh, bit1 meshMessageDeliveriesActive, bit2 mesh, bit3 fanout */
     GSIM_F_BP,            /* f64 [E]    behaviourPenalty                score.go:34 */
     GSIM_F_ESTATE,        /* u8  [E]    bit0 tracked (peerStats exists), bit1 connected */
     GSIM_F_EXPIRE,        /* i64 [E]    retention expiry (ns)           score.go:22 */
@@ -331,12 +331,15 @@ typedef enum gsim_field {
     GSIM_F_CTL,           /* u8 [2][T][E] control inbox by round parity (receiver's edge) */
     GSIM_F_SEEN,          /* u32 [ring][N] first-seen round, 0xFFFFFFFF unseen (after msgs_init) */
     GSIM_F_LASTPUT,       /* i32 [T][N] tick of the newest mcache.Put, -1 none (after msgs_init) */
+    GSIM_F_LASTPUB,       /* i64 [N][T] gs.lastpub[topic] (ns), 0 = none  gossipsub.go:426 (peer-major) */
+    GSIM_F_FANOUT_TOPICS, /* u64 [N]    bit t: gs.fanout[topic t] exists  gossipsub.go:425 */
     GSIM_F__COUNT
 } gsim_field;
 
 #define GSIM_TF_IN_MESH   0x01u  /* topicStats.inMesh (score.go:39)               */
 #define GSIM_TF_ACTIVE    0x02u  /* topicStats.meshMessageDeliveriesActive         */
 #define GSIM_TF_MESH      0x04u  /* router membership: gs.mesh[topic][p] (gossipsub.go:424) */
+#define GSIM_TF_FANOUT    0x08u  /* router fanout: gs.fanout[topic][p] (gossipsub.go:425) */
 /* control inbox bits (GSIM_F_CTL), one byte per [parity][topic][receiver edge] */
 #define GSIM_CTL_GRAFT    0x01u  /* ControlGraft  (pb/rpc.proto) */
 #define GSIM_CTL_PRUNE    0x02u  /* ControlPrune with Backoff = PruneBackoff/1s */

@@ -42,7 +42,7 @@ void orc_refresh_scores(orc_net* s, int64_t now)
                     int64_t i = te(s, t, e);
                     s->first[i] = s->meshd[i] = s->fail[i] = s->invalid[i] = 0.0;
                     s->graft_time[i] = s->mesh_time[i] = 0;
-                    s->tflags[i] &= (uint8_t)GSIM_TF_MESH;   /* router membership is not score state */
+                    s->tflags[i] &= (uint8_t)(GSIM_TF_MESH | GSIM_TF_FANOUT);   /* router membership is not score state */
                 }
             }
             continue;
@@ -212,7 +212,7 @@ void orc_add_peer(orc_net* s, int64_t e)
             int64_t i = te(s, t, e);
             s->first[i] = s->meshd[i] = s->fail[i] = s->invalid[i] = 0.0;
             s->graft_time[i] = s->mesh_time[i] = 0;
-            s->tflags[i] &= (uint8_t)GSIM_TF_MESH;   /* router membership is not score state */
+            s->tflags[i] &= (uint8_t)(GSIM_TF_MESH | GSIM_TF_FANOUT);   /* router membership is not score state */
         }
     }
     s->estate[e] = ES_TRACKED | ES_CONN;
@@ -231,7 +231,7 @@ void orc_remove_peer(orc_net* s, int64_t e, int64_t now)
             int64_t i = te(s, t, e);
             s->first[i] = s->meshd[i] = s->fail[i] = s->invalid[i] = 0.0;
             s->graft_time[i] = s->mesh_time[i] = 0;
-            s->tflags[i] &= (uint8_t)GSIM_TF_MESH;   /* router membership is not score state */
+            s->tflags[i] &= (uint8_t)(GSIM_TF_MESH | GSIM_TF_FANOUT);   /* router membership is not score state */
         }
         return;
     }

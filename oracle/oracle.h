@@ -56,6 +56,8 @@ typedef struct orc_net {
     const gsim_thresholds*         th;
     const gsim_gossipsub_params*   gp;
     uint8_t* ctl;              /* [2][T][E] control inbox by round parity */
+    int64_t* lastpub;          /* [N][T] gs.lastpub[topic] (ns), 0 = none (peer-major) */
+    uint64_t* fan_topics;      /* [N] bit t: gs.fanout[topic t] exists */
 } orc_net;
 
 /* ---- message propagation (oracle_deliver.c) ------------------------------ */

@@ -107,6 +107,10 @@ void orc_publish(orc_net* s, orc_msgs* m, uint64_t id, uint32_t topic, uint32_t 
      * its mcache (gossipsub.go:976); its own DeliverMessage is not scored
      * (trace.go skips ReceivedFrom == self) */
     row[origin] = (uint32_t)g;
+    /* Publish: an origin that has not joined the topic sends to its fanout
+     * (gossipsub.go:1011-1028); flood publishing sends to every topic peer */
+    if (!s->gp->flood_publish && !((s->sub[origin] >> topic) & 1u) && s->lastpub && s->fan_topics)
+        orc_fanout_publish(s, origin, (int32_t)topic, g, orc_round_time(m, g), P(m)->seed);
     m->lastput[(int64_t)topic * s->n + origin] = (int32_t)(g / m->rounds);
     fr_push(P(m), origin, slot, origin);
 }
@@ -123,9 +127,19 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
         if (m->seen[(int64_t)slot * s->n + j] != (uint32_t)(g - 1)) continue;   /* slot reused */
         const int32_t t = (int32_t)m->topic[slot];
         const uint32_t origin = m->origin[slot];
+        /* the origin's own Publish: flood to every topic peer with score >=
+         * publishThreshold (gossipsub.go:989-995), or its mesh, or its fanout
+         * when it has not joined the topic (1011-1028); everyone else
+         * forwards to its mesh */
+        const int flood = j == origin && s->gp->flood_publish;
+        const uint8_t want = (j == origin && !((s->sub[j] >> t) & 1u)) ? GSIM_TF_FANOUT : GSIM_TF_MESH;
         for (uint32_t e = s->row_ptr[j]; e < s->row_ptr[j + 1]; ++e) {
             const uint32_t i = s->col[e];
-            if (!(s->tflags[(int64_t)t * s->e + e] & GSIM_TF_MESH)) continue;
+            if (flood) {
+                if (!((s->sub[i] >> t) & 1u) || s->score[e] < s->th->publish_threshold) continue;
+            } else if (!(s->tflags[(int64_t)t * s->e + e] & want)) {
+                continue;
+            }
             if (!(s->estate[e] & GSIM_ES_CONNECTED)) continue;
             if (i == from || i == origin) continue;
             ar_push(p, i, slot, s->rev[e]);

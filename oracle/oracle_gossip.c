@@ -98,9 +98,11 @@ static int topic_peer(const orc_net* s, uint32_t e, int32_t t)
     return (s->estate[e] & GSIM_ES_CONNECTED) && ((s->sub[s->col[e]] >> t) & 1u);
 }
 
-/* emitGossip(topic, exclude = mesh) for observer i, after its mesh
- * maintenance of topic t (gossipsub.go:1554-1556, 1711-1775). */
-void orc_gossip_emit(orc_net* s, orc_msgs* m, uint32_t i, int32_t t, uint64_t tick, uint64_t seed)
+/* emitGossip(topic, exclude) for observer i: exclude = its mesh after the mesh
+ * maintenance of a joined topic (gossipsub.go:1554-1556), its fanout peers for
+ * a fanout topic (1593-1595); gossipsub.go:1711-1775. */
+void orc_gossip_emit(orc_net* s, orc_msgs* m, uint32_t i, int32_t t, uint64_t tick, uint64_t seed,
+                     uint8_t exclude)
 {
     priv* p = orc_msgs_priv(m);
     uint32_t* mids = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(m->ring > 0 ? m->ring : 1));
@@ -114,7 +116,7 @@ void orc_gossip_emit(orc_net* s, orc_msgs* m, uint32_t i, int32_t t, uint64_t ti
     int n = 0;
     for (uint32_t e = b; e < en; ++e) {
         if (!topic_peer(s, e, t)) continue;
-        if (s->tflags[te(s, t, e)] & GSIM_TF_MESH) continue;               /* exclude: mesh */
+        if (s->tflags[te(s, t, e)] & exclude) continue;                    /* exclude: mesh / fanout */
         if (orc_score_edge(s, e) < s->th->gossip_threshold) continue;        /* live Score(p) */
         L[n].key = okey(seed, tick, i, t, P_GOSSIP, s->col[e], e - b);
         L[n].v = e;

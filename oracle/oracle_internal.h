@@ -17,6 +17,8 @@ enum {
     P_GOSSIP_FILL = 9,  /* emitGossip: map order of the Dlo fill loop  gossipsub.go:1739-1748 */
     P_GOSSIP_DUP = 10,  /* emitGossip: shuffle key of a fill duplicate */
     P_IHAVE_TRUNC = 11, /* emitGossip: per-peer shuffleStrings(mids)   gossipsub.go:1766-1771 */
+    P_FANOUT_NEW = 12,  /* Publish: getPeers for a new fanout          gossipsub.go:1020-1023 */
+    P_FANOUT = 13,      /* heartbeat: getPeers for the fanout top-up  gossipsub.go:1578-1585 */
 };
 
 static inline uint64_t okey(uint64_t seed, uint64_t tick, uint32_t obs, int32_t topic, uint32_t purpose,
@@ -61,7 +63,10 @@ priv* orc_msgs_priv(orc_msgs* m);
 int64_t orc_round_time(const orc_msgs* m, int64_t g);
 
 /* gossip (oracle_gossip.c) */
-void orc_gossip_emit(orc_net* s, orc_msgs* m, uint32_t i, int32_t t, uint64_t tick, uint64_t seed);
+void orc_gossip_emit(orc_net* s, orc_msgs* m, uint32_t i, int32_t t, uint64_t tick, uint64_t seed,
+                     uint8_t exclude);
+/* Publish's fanout branch (oracle_net.c) */
+void orc_fanout_publish(orc_net* s, uint32_t origin, int32_t topic, int64_t g, int64_t now, uint64_t seed);
 void orc_gossip_fulfill(orc_msgs* m, uint32_t p, uint32_t slot);
 void orc_gossip_ihave(orc_net* s, orc_msgs* m, int64_t g);
 void orc_gossip_index(const orc_net* s, orc_msgs* m, int64_t tick);

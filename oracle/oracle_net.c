@@ -224,6 +224,76 @@ static void maintain(hb* h)
     if (c != buf) free(c);
 }
 
+static inline int in_fanout(const hb* h, uint32_t e) { return (h->s->tflags[ti(h, e)] & GSIM_TF_FANOUT) != 0; }
+
+static int f_fanout(const hb* h, uint32_t e, double thr)     /* gossipsub.go:1580-1584, 1020-1023 */
+{
+    return !in_fanout(h, e) && h->s->score[e] >= thr;
+}
+
+/* Fanout expiry and maintenance for one observer, after its mesh topics
+ * (gossipsub.go:1558-1596): drop fanouts not published to for FanoutTTL;
+ * for each remaining fanout topic drop peers that left the topic or score
+ * below publishThreshold, top up to D with getPeers, then emitGossip
+ * excluding the fanout peers.  Topics in ascending order. */
+static void fanout(hb* h, orc_msgs* m)
+{
+    orc_net* s = h->s;
+    if (!s->lastpub || !s->fan_topics) return;
+    const gsim_gossipsub_params* gp = s->gp;
+    const double thr = s->th->publish_threshold;
+    for (int32_t t = 0; t < s->t; ++t) {
+        int64_t* lp = &s->lastpub[(int64_t)h->i * s->t + t];
+        if (*lp != 0 && *lp + gp->fanout_ttl_ns < h->now) {
+            h->t = t;
+            for (uint32_t e = h->b; e < h->en; ++e) s->tflags[ti(h, e)] &= (uint8_t)~GSIM_TF_FANOUT;
+            s->fan_topics[h->i] &= ~(1ull << t);
+            *lp = 0;
+        }
+    }
+    cand buf[4096];
+    const uint32_t deg = h->en - h->b;
+    cand* c = deg <= 4096 ? buf : (cand*)malloc(sizeof(cand) * deg);
+    for (int32_t t = 0; t < s->t; ++t) {
+        if (!((s->fan_topics[h->i] >> t) & 1u)) continue;
+        h->t = t;
+        int have = 0;
+        for (uint32_t e = h->b; e < h->en; ++e) {
+            if (!in_fanout(h, e)) continue;
+            if (!topic_peer(h, e) || s->score[e] < thr) s->tflags[ti(h, e)] &= (uint8_t)~GSIM_TF_FANOUT;
+            else ++have;
+        }
+        if (have < gp->d) {
+            const int n = get_peers(h, gp->d - have, f_fanout, thr, P_FANOUT, c);
+            for (int q = 0; q < n; ++q) s->tflags[ti(h, c[q].e)] |= GSIM_TF_FANOUT;
+        }
+        if (m) orc_gossip_emit(s, m, h->i, t, h->tick, h->seed, GSIM_TF_FANOUT);
+    }
+    if (c != buf) free(c);
+}
+
+/* Publish's fanout branch for an origin that has not joined the topic
+ * (gossipsub.go:1011-1028): with no fanout peers yet, pick D topic peers
+ * with score >= publishThreshold (getPeers, key counter = the round); then
+ * lastpub = now.  Scores are the snapshot. */
+void orc_fanout_publish(orc_net* s, uint32_t origin, int32_t topic, int64_t g, int64_t now, uint64_t seed)
+{
+    hb h = {s, origin, s->row_ptr[origin], s->row_ptr[origin + 1], topic, (uint64_t)g, seed, now, NULL};
+    int have = 0;
+    if ((s->fan_topics[origin] >> topic) & 1u)
+        for (uint32_t e = h.b; e < h.en; ++e) have |= in_fanout(&h, e);
+    if (!have) {
+        cand buf[4096];
+        const uint32_t deg = h.en - h.b;
+        cand* c = deg <= 4096 ? buf : (cand*)malloc(sizeof(cand) * deg);
+        const int n = get_peers(&h, s->gp->d, f_fanout, s->th->publish_threshold, P_FANOUT_NEW, c);
+        for (int q = 0; q < n; ++q) s->tflags[ti(&h, c[q].e)] |= GSIM_TF_FANOUT;
+        if (n > 0) s->fan_topics[origin] |= 1ull << topic;
+        if (c != buf) free(c);
+    }
+    s->lastpub[(int64_t)origin * s->t + topic] = now;
+}
+
 void orc_heartbeat_gossip(orc_net* s, orc_msgs* m, uint64_t tick, int64_t now, uint64_t seed)
 {
     uint8_t* out = s->ctl;   /* heartbeat output = parity-0 inbox, handled in round 0 */
@@ -262,8 +332,9 @@ void orc_heartbeat_gossip(orc_net* s, orc_msgs* m, uint64_t tick, int64_t now, u
             if (!((s->sub[i] >> t) & 1u)) continue;
             h.t = t;
             maintain(&h);
-            if (m) orc_gossip_emit(s, m, (uint32_t)i, t, tick, seed);
+            if (m) orc_gossip_emit(s, m, (uint32_t)i, t, tick, seed, GSIM_TF_MESH);
         }
+        fanout(&h, m);
     }
 }
 
@@ -378,7 +449,7 @@ int32_t orc_churn(orc_net* s, const uint32_t* pairs, int32_t count, int32_t up, 
             }
             for (int32_t t = 0; t < s->t; ++t) {
                 const int64_t i = (int64_t)t * s->e + e;
-                s->tflags[i] &= (uint8_t)~GSIM_TF_MESH;
+                s->tflags[i] &= (uint8_t)~(GSIM_TF_MESH | GSIM_TF_FANOUT);   /* out of mesh and fanout */
                 if (s->ctl) {
                     s->ctl[i] = 0;
                     s->ctl[(int64_t)s->t * s->e + i] = 0;

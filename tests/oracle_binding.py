@@ -32,7 +32,7 @@ class OrcNet(Structure):
         ("bp", c_void_p), ("estate", c_void_p), ("expire", c_void_p), ("p6", c_void_p), ("score", c_void_p),
         ("backoff", c_void_p),
         ("pp", c_void_p), ("tp", c_void_p), ("th", c_void_p), ("gp", c_void_p),
-        ("ctl", c_void_p),
+        ("ctl", c_void_p), ("lastpub", c_void_p), ("fan_topics", c_void_p),
     ]
 
 
@@ -146,6 +146,8 @@ class NetState:
             setattr(self, f, np.zeros(E, dtype=self.DTYPES[f]))
         self.estate[:] = _abi.ES_TRACKED | _abi.ES_CONNECTED
         self.ctl = np.zeros((2, self.T, E), dtype=np.uint8)
+        self.lastpub = np.zeros((net.n, self.T), dtype=np.int64)
+        self.fan_topics = np.zeros(net.n, dtype=np.uint64)
         self.rev = net.rev()
         self.p5 = np.zeros(net.n) if p5 is None else np.ascontiguousarray(p5, dtype=np.float64)
         self.ip_white = None if ip_white is None else np.ascontiguousarray(ip_white, dtype=np.uint8)
@@ -174,6 +176,7 @@ class NetState:
         v.th = ctypes.cast(ctypes.byref(self.th), c_void_p)
         v.gp = ctypes.cast(ctypes.byref(self.gp), c_void_p)
         v.ctl = _p(self.ctl)
+        v.lastpub, v.fan_topics = _p(self.lastpub), _p(self.fan_topics)
         self._view = v
         return ctypes.byref(v)
 
@@ -191,11 +194,15 @@ class NetState:
         for f in self.TOPIC_FIELDS + self.EDGE_FIELDS:
             eng.write(self.FIELD_IDS[f], getattr(self, f))
         eng.write(_abi.F_CTL, self.ctl)
+        eng.write(_abi.F_LASTPUB, self.lastpub)
+        eng.write(_abi.F_FANOUT_TOPICS, self.fan_topics)
 
     def pull_from_engine(self, eng):
         for f in self.TOPIC_FIELDS + self.EDGE_FIELDS:
             getattr(self, f)[...] = eng.read(self.FIELD_IDS[f])
         self.ctl[...] = eng.read(_abi.F_CTL)
+        self.lastpub[...] = eng.read(_abi.F_LASTPUB)
+        self.fan_topics[...] = eng.read(_abi.F_FANOUT_TOPICS)
 
 
 UNSEEN = 0xFFFFFFFF

@@ -101,3 +101,14 @@ def test_create_without_device_fails_loudly():
     from gsim.engine import GsimError
     with pytest.raises(GsimError, match="no HIP device"):
         Engine(_params(), PeerScoreThresholds())
+
+
+def test_every_field_has_a_host_dtype():
+    """Each GSIM_F_* view the header declares can be read and written from
+    the host mirror (dtype and shape known)."""
+    import re
+    from gsim import engine
+    hdr = open(os.path.join(REPO, "include", "gsim.h")).read()
+    body = hdr[hdr.index("GSIM_F_FIRST = 0"):hdr.index("GSIM_F__COUNT")]
+    n = len(re.findall(r"^\s*GSIM_F_\w+", body, re.M))
+    assert set(range(n)) <= set(engine._FIELD_DTYPES)

@@ -204,7 +204,7 @@ def _random_mesh_state(st, rng, p_mesh):
 
 
 def assert_same(cpu, gpu):
-    for f in cpu.TOPIC_FIELDS + cpu.EDGE_FIELDS + ("ctl",):
+    for f in cpu.TOPIC_FIELDS + cpu.EDGE_FIELDS + ("ctl", "lastpub", "fan_topics"):
         a, b = getattr(cpu, f), getattr(gpu, f)
         av = a.view(np.uint64) if a.dtype.itemsize == 8 else a
         bv = b.view(np.uint64) if b.dtype.itemsize == 8 else b
