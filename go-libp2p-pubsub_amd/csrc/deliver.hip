@@ -62,6 +62,8 @@ struct Deliver {
     uint32_t *d_mtopic = nullptr, *d_morigin = nullptr;
     uint8_t* d_minv = nullptr;
     uint64_t* d_cell = nullptr;        // [ring][N] seen-set cells (layout above)
+    uint64_t* d_seenbm = nullptr;      // [ring][ceil(N/64)] bit: the cell is committed (a cache of the cells)
+    int32_t* d_mpub = nullptr;         // [ring] round the slot's message was published in
     int32_t* d_lastput = nullptr;      // [T][N]
     uint32_t* d_nnew = nullptr;        // [2][ring/32] bitmask: slots with new claims (or a publication), by round parity
     unsigned long long* d_stats = nullptr;   // [4]
@@ -103,6 +105,9 @@ struct RoundArgs {
     uint32_t *mtopic, *morigin;
     uint8_t* minv;
     uint64_t* cell;
+    uint64_t* seenbm;          // [ring][nw] committed bits of the cells (read before a cell)
+    int64_t nw;                // words per slot
+    int32_t* mpub;             // [ring] publication round
     int32_t* lastput;
     uint32_t diag;                 // DIAG_D_* ablations (timing experiments only)
     const uint32_t* nnew_prev;     // bitmask: slots with new claims (or a publication) in round g-1
@@ -226,6 +231,7 @@ __global__ void k_reset_slots(RoundArgs a, const gsim_msg* pub, int32_t count)
         // several reused rows may credit one record: atomic updates here
         if (a.g > 0 && is_claim_of(c, q)) commit_claim<true>(a, row + i, c, a.g - 1, m, i);
         row[i] = kUnseen64;
+        if ((i & 63) == 0) a.seenbm[(int64_t)m * a.nw + (i >> 6)] = 0;
     }
 }
 
@@ -239,6 +245,9 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, int32_t count)
     a.morigin[slot] = p.origin;
     a.minv[slot] = p.invalid;
     a.cell[(int64_t)slot * a.N + p.origin] = ((uint64_t)(uint32_t)a.g << 32) | p.origin;
+    atomicOr(reinterpret_cast<unsigned long long*>(a.seenbm + (int64_t)slot * a.nw + (p.origin >> 6)),
+             1ull << (p.origin & 63));
+    a.mpub[slot] = (int32_t)a.g;
     int32_t* lp = a.lastput + (int64_t)p.topic * a.N + p.origin;
     const int32_t tick = (int32_t)(a.g / a.R);
     if (*lp < tick) *lp = tick;
@@ -249,8 +258,10 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, int32_t count)
 // Round g.  W = lanes per row (power of two >= the longest row); group q of
 // a wave always walks the senders j0 + q*W .. j0 + q*W + W-1, two at a time
 // (their loads interleaved: two dependent memory trips per pair of rows).
-template <int W>
-__global__ __launch_bounds__(256) void k_send(RoundArgs a)
+// B = active slots whose cells are loaded together; WPE = minimum waves per
+// SIMD the register allocation must allow (1 = unconstrained).
+template <int W, int B, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_send(RoundArgs a)
 {
     extern __shared__ uint16_t s_act[];   // [ring] active slots, then [ring/32] new-claim bits
     __shared__ int s_n;
@@ -274,10 +285,10 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
     const uint32_t rp0 = vj ? a.row_ptr[jl] : 0u;
     const uint32_t rp1 = vj ? a.row_ptr[jl + 1] : 0u;
     unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
-    for (int k0 = 0; k0 < nact; k0 += kSlotBatch) {
-        uint64_t cv[kSlotBatch];
+    for (int k0 = 0; k0 < nact; k0 += B) {
+        uint64_t cv[B];
 #pragma unroll
-        for (int b = 0; b < kSlotBatch; ++b) {
+        for (int b = 0; b < B; ++b) {
             const int k = k0 + b;
             cv[b] = (k < nact && vj) ? a.cell[(int64_t)s_act[k] * a.N + jl] : kUnseen64;
         }
@@ -286,10 +297,10 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
         // slot order (a record winning several slots continues from the value
         // stored for the earlier one)
         {
-            double fv[kSlotBatch];
-            int64_t irb[kSlotBatch];
+            double fv[B];
+            int64_t irb[B];
 #pragma unroll
-            for (int b = 0; b < kSlotBatch; ++b) {
+            for (int b = 0; b < B; ++b) {
                 irb[b] = -1;
                 fv[b] = 0.0;
                 const int k = k0 + b;
@@ -300,7 +311,15 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
                 }
             }
 #pragma unroll
-            for (int b = 0; b < kSlotBatch; ++b) {
+            for (int b = 0; b < B; ++b) {
+                // the committed bits of the wave's 64 peers form one bitmap word,
+                // which only this wave writes during the round
+                const int k = k0 + b;
+                const uint64_t cb = __ballot(k < nact && is_claim_of(cv[b], qpar));
+                if (cb && lane == 0) a.seenbm[(int64_t)s_act[k] * a.nw + (j0 >> 6)] |= cb;
+            }
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
                 const int k = k0 + b;
                 if (k >= nact || !is_claim_of(cv[b], qpar)) continue;
                 const uint32_t m = s_act[k];
@@ -325,7 +344,7 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
             }
         }
 #pragma unroll
-        for (int b = 0; b < kSlotBatch; ++b) {
+        for (int b = 0; b < B; ++b) {
             const int k = k0 + b;
             if (k >= nact) break;                        // wave-uniform
             const uint32_t m = s_act[k];
@@ -352,6 +371,12 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
             const double mcap = tp->mesh_message_deliveries_cap;
             const int64_t plane = (int64_t)t * a.E;
             const unsigned long long first_before = n_first;
+            // every receiver saw the message at or after its publication: when
+            // that is within the window, a copy to a receiver whose committed
+            // bit is set is an in-window duplicate without reading its cell
+            const bool win_all = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
+            const bool use_bm = !(a.diag & DIAG_D_NO_BITMAP);
+            const int64_t bm_m = (int64_t)m * a.nw;
             uint64_t gm = mask & gmask;
             while (__ballot(gm != 0)) {
                 int b1 = -1, b2 = -1;
@@ -395,8 +420,17 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
                 uint64_t c1 = 0, c2 = 0;
                 uint32_t n1 = 0, n2 = 0;
                 double x1 = 0.0, x2 = 0.0;
-                if (ok1) c1 = a.cell[row_m + i1];
-                if (ok2) c2 = a.cell[row_m + i2];
+                // known: committed in an earlier round, and its first-seen round
+                // is not needed (in-window for sure, or no counter to update)
+                bool k1 = false, k2 = false;
+                if (use_bm) {
+                    if (ok1) k1 = ((a.seenbm[bm_m + (i1 >> 6)] >> (i1 & 63)) & 1ull) &&
+                                  (win_all || !sc1 || inv || !(tf1 & GSIM_TF_IN_MESH));
+                    if (ok2) k2 = ((a.seenbm[bm_m + (i2 >> 6)] >> (i2 & 63)) & 1ull) &&
+                                  (win_all || !sc2 || inv || !(tf2 & GSIM_TF_IN_MESH));
+                }
+                if (ok1 && !k1) c1 = a.cell[row_m + i1];
+                if (ok2 && !k2) c2 = a.cell[row_m + i2];
                 if (sc1) { if (inv) x1 = a.invalid[plane + e1]; else if (tf1 & GSIM_TF_IN_MESH) n1 = a.mcnt[plane + e1]; }
                 if (sc2) { if (inv) x2 = a.invalid[plane + e2]; else if (tf2 & GSIM_TF_IN_MESH) n2 = a.mcnt[plane + e2]; }
 #pragma unroll
@@ -408,10 +442,13 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
                     const bool sc = u ? sc2 : sc1;
                     const uint8_t tf = u ? tf2 : tf1;
                     const uint32_t hi = (uint32_t)(c >> 32);
+                    const bool known = u ? k2 : k1;
                     // first-seen round of an earlier round, or -1 for unseen /
                     // claimed in this round
                     int64_t seen_round = -1;
-                    if (c != kUnseen64) {
+                    if (known) {
+                        seen_round = a.g - 1;    // any earlier round: only "in window" is used
+                    } else if (c != kUnseen64) {
                         if (!(hi & kClaim)) seen_round = hi;
                         else if (((hi >> 30) & 1u) != par) seen_round = a.g - 1;
                     }
@@ -440,7 +477,8 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
                     } else if (tf & GSIM_TF_IN_MESH) {
                         // markDuplicateMessageDelivery's window test; a same-round
                         // copy (first or duplicate) has validated = now
-                        const bool in_window = seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window)
+                        const bool in_window = known ? true
+                                             : seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window)
                                                                : (window >= 0);
                         if (in_window) {
                             uint32_t n = u ? n2 : n1;
@@ -503,6 +541,12 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
             cv[b] = (k < nact && vi) ? a.cell[(int64_t)s_act[k] * a.N + i] : kUnseen64;
+        }
+#pragma unroll
+        for (int b = 0; b < kSlotBatch; ++b) {
+            const int k = k0 + b;
+            const uint64_t cb = __ballot(k < nact && is_claim_of(cv[b], par));
+            if (cb && lane == 0) a.seenbm[(int64_t)s_act[k] * a.nw + (i0 >> 6)] |= cb;
         }
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
@@ -936,7 +980,7 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_lastput);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_seenbm); f(d->d_mpub); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
@@ -981,6 +1025,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.first = h->d_first; a.meshd = h->d_meshd; a.invalid = h->d_invalid; a.mcnt = h->d_mcnt;
     a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv;
     a.cell = d->d_cell; a.lastput = d->d_lastput;
+    a.seenbm = d->d_seenbm; a.nw = (h->n + 63) / 64; a.mpub = d->d_mpub;
     const size_t w = (size_t)nnew_words(d);
     a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
     a.nnew_cur = d->d_nnew + (size_t)(g & 1) * w;
@@ -1119,6 +1164,16 @@ int deliver_read_seen(gsim_handle* h, void* dst)
     return hip_check(h, e, "gsim_read_field(SEEN)");
 }
 
+template <int W>
+static void launch_send(gsim_handle* h, int grid, size_t lds, const RoundArgs& a)
+{
+    switch (h->send_variant) {
+    case 1: hipLaunchKernelGGL((k_send<W, 4, 7>), dim3(grid), dim3(256), lds, h->stream, a); return;
+    case 2: hipLaunchKernelGGL((k_send<W, 4, 1>), dim3(grid), dim3(256), lds, h->stream, a); return;
+    default: hipLaunchKernelGGL((k_send<W, 8, 1>), dim3(grid), dim3(256), lds, h->stream, a); return;
+    }
+}
+
 extern "C" {
 
 int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
@@ -1155,6 +1210,8 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_morigin, ring * 4);
     A((void**)&d->d_minv, ring);
     A((void**)&d->d_cell, ring * N * 8);
+    A((void**)&d->d_seenbm, ring * ((N + 63) / 64) * 8);
+    A((void**)&d->d_mpub, ring * 4);
     A((void**)&d->d_lastput, T * N * 4);
     A((void**)&d->d_nnew, 2 * words * 4);
     A((void**)&d->d_stats, 4 * 8);
@@ -1184,6 +1241,8 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     }
     h->dl = d;
     e = hipMemsetAsync(d->d_cell, 0xFF, ring * N * 8, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_seenbm, 0, ring * ((N + 63) / 64) * 8, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_mpub, 0, ring * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_lastput, 0xFF, T * N * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_mtopic, 0, ring * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_morigin, 0, ring * 4, h->stream);
@@ -1285,11 +1344,11 @@ int gsim_round(gsim_handle* h, int64_t round)
         ProfScope ps(h, GSIM_K_SEND);
         const int grid = grid_peers(h->n);
         if (h->max_degree <= 16)
-            hipLaunchKernelGGL(k_send<16>, dim3(grid), dim3(256), lds, h->stream, a);
+            launch_send<16>(h, grid, lds, a);
         else if (h->max_degree <= 32)
-            hipLaunchKernelGGL(k_send<32>, dim3(grid), dim3(256), lds, h->stream, a);
+            launch_send<32>(h, grid, lds, a);
         else
-            hipLaunchKernelGGL(k_send<64>, dim3(grid), dim3(256), lds, h->stream, a);
+            launch_send<64>(h, grid, lds, a);
         // the claims of round g-1 were committed by k_send; round g+1's bits
         // were last read (as "previous") by round g
         d->pending = round;

@@ -54,6 +54,7 @@ enum : uint32_t {
     DIAG_H_NO_GOSSIP = 512,     // heartbeat: skip emitGossip
     DIAG_H_NO_IHAVE_STORE = 1024,   // heartbeat: choose gossip targets but do not store the marks
     DIAG_H_NO_RECOMPUTE = 2048,     // heartbeat: emitGossip uses the snapshot score (no live recompute)
+    DIAG_D_NO_BITMAP = 4096,        // delivery: read every receiver's cell (no committed-bit shortcut; results unchanged)
 };
 
 struct ColocArgs {
@@ -152,6 +153,7 @@ struct gsim_handle {
     bool p6_dirty = true;
     bool maybe_retained = false;
     int score_variant = -1;   // refresh+score kernel variant (-1: from env)
+    int send_variant = 0;     // k_send slot batch / occupancy variant (gsim_set_kernel_variant(h, 2, v))
     uint32_t diag = 0;        // DIAG_* ablations (A/B diagnostics only)
 
     // device: parameters and scratch flags
