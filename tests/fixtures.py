@@ -32,7 +32,7 @@ def beacon_params(n_topics: int, topic_cap: float = 0.0, **over) -> PeerScorePar
     # vary the topics a little so per-topic parameters are exercised
     for t in range(n_topics):
         p.Topics[f"topic{t:02d}"] = beacon_topic(TopicWeight=0.25 + 0.05 * t,
-                                                 MeshMessageDeliveriesThreshold=100 - 3 * t)
+                                                 MeshMessageDeliveriesThreshold=max(4, 100 - 3 * t))
     return p
 
 

@@ -1,0 +1,162 @@
+"""Parity at the shapes of BASELINE.json's configurations (SURVEY.md §8 table
+C1-C5), scaled to sizes the oracle finishes in seconds.  C3 itself is the
+bench workload (bench.py); its structure (random-regular k=32, 16 topics,
+beacon params) is covered by test_delivery/test_gossip.
+
+  C1  Go mocknet-like: 100 hosts, dense (k=20), 1 topic, D=6 defaults,
+      1000 messages
+  C2  10k peers, single topic, D=8, full P1-P7 + gossip (full size)
+  C4  Sybil/eclipse: 20 % sybils behind shared IPs, sybils ignore IWANT
+      (broken promises -> P7), P6 colocation, opportunistic grafting tick
+  C5  power-law graph (Chung-Lu, exponent 2.5, mean 16, rows <= 64), 64
+      topics with Zipf subscriptions (~8 per peer), churn between ticks
+"""
+import numpy as np
+import pytest
+
+import oracle_binding as ob
+from gsim import _abi
+from gsim.params import GossipSubParams, PeerScoreThresholds, Second
+
+from test_heartbeat import tick_time
+
+
+def test_power_law_graph_shape():
+    from gsim import graphs
+    net = graphs.power_law(20000, 16, 2.5, 64, seed=4)
+    d = np.diff(net.row_ptr.astype(np.int64))
+    assert d.max() <= 64 and 12 < d.mean() < 17
+    assert d.max() >= 48, "heavy tail up to the row cap"
+    assert (net.col[net.rev()] == net.owner()).all(), "symmetric"
+    rows_sorted = all((np.diff(net.col[a:b].astype(np.int64)) > 0).all()
+                      for a, b in zip(net.row_ptr[:-1:97], net.row_ptr[1::97]))
+    assert rows_sorted
+    ob_ = net.outbound.astype(np.int64) + net.outbound[net.rev()].astype(np.int64)
+    assert (ob_ == 1).all(), "exactly one side dialed"
+
+
+def test_zipf_subscriptions():
+    from gsim import graphs
+    sub = graphs.zipf_subscriptions(50000, 64, 8, seed=1)
+    per_peer = np.array([bin(int(x)).count("1") for x in sub[:1000]])
+    assert (per_peer == 8).all()
+    cnt = [int(((sub >> np.uint64(t)) & np.uint64(1)).sum()) for t in range(64)]
+    assert cnt[0] > cnt[10] > cnt[63] > 0, "popularity falls with rank"
+
+
+def test_sybil_ips():
+    from gsim import graphs
+    ip_ptr, ip_ids, n_ips, syb = graphs.sybil_ips(12500, 0.2, 50, seed=1)
+    assert syb.sum() == 2500 and n_ips == 10000 + 50
+    _, counts = np.unique(ip_ids[syb], return_counts=True)
+    assert (counts == 50).all()
+
+
+# ---- GPU parity -------------------------------------------------------------------
+
+@pytest.mark.gpu
+def test_c1_mocknet_dense_default_params(require_gpu):
+    """C1: 100 hosts, k=20, 1 topic, D=6 and the library's default
+    GossipSubParams, 1000 messages over 20 heartbeats."""
+    from gsim.engine import random_regular
+    from tickrun import run_parity, subscribed_schedule
+    from test_delivery import delivery_params
+    rng = np.random.default_rng(101)
+    net = random_regular(100, 20, seed=5, n_topics=1)
+    params = delivery_params(1)
+    th = PeerScoreThresholds(GossipThreshold=-10, PublishThreshold=-50, GraylistThreshold=-80)
+    gp = GossipSubParams()                                    # D=6, Dlo=5, Dhi=12, Dlazy=6, ...
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    ticks = list(range(1, 21))
+    sched = subscribed_schedule(rng, ticks, net, 1, 50, 0.02)
+    n_msgs = sum(len(v) for v in sched.values())
+    assert 850 <= n_msgs <= 1150
+    msgs, _ = run_parity(net, params, th, gp, st, ticks, sched, ring=1024)
+    assert msgs.stats[1] > 0.95 * n_msgs * 99, "messages reach (nearly) every host"
+
+
+@pytest.mark.gpu
+def test_c2_10k_single_topic_full_scoring(require_gpu):
+    """C2 at full size: 10k peers, k=32, one topic, D=8, P1-P7 + gossip."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim.engine import random_regular
+    from tickrun import run_parity, subscribed_schedule
+    rng = np.random.default_rng(202)
+    net = random_regular(10_000, 32, seed=7, n_topics=1)
+    params = beacon_params(1)
+    th = PeerScoreThresholds(GossipThreshold=-20, PublishThreshold=-40, GraylistThreshold=-300)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 8 / 32)
+    st.bp[rng.random(net.e) < 0.03] = 12.0
+    ticks = list(range(1, 6))
+    sched = subscribed_schedule(rng, ticks, net, 1, 8, 0.05)
+    _, gs = run_parity(net, params, th, gp, st, ticks, sched, ring=256)
+    assert gs["iwant_ids"] > 0
+
+
+@pytest.mark.gpu
+def test_c4_sybil_colocation_broken_promises(require_gpu):
+    """C4 scaled 1/10: 10k honest + 2.5k sybils that never answer IWANT.  The
+    sybils sit behind few addresses (500 per IP), so an honest peer sees several
+    of its neighbours on one IP: P6 colocation pushes them below the publish and
+    graylist thresholds, broken promises add P7; ticks 58-61 include the
+    opportunistic-grafting heartbeat."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim import graphs
+    from gsim.engine import random_regular
+    from tickrun import run_parity, subscribed_schedule
+    rng = np.random.default_rng(404)
+    n = 12_500
+    net = random_regular(n, 32, seed=9, n_topics=1)
+    ip_ptr, ip_ids, n_ips, syb = graphs.sybil_ips(n, 0.2, 500, seed=3)
+    net = graphs.with_ips(net, ip_ptr, ip_ids, n_ips)
+    params = beacon_params(1)
+    th = PeerScoreThresholds(GossipThreshold=-100, PublishThreshold=-500, GraylistThreshold=-1000,
+                             AcceptPXThreshold=100, OpportunisticGraftThreshold=5)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2, OpportunisticGraftTicks=60)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(57), 8 / 32)
+    beh = syb.astype(np.uint8) * ob.ORC_BEHAVE_IGNORE_IWANT
+    ticks = [58, 59, 60, 61]
+    sched = subscribed_schedule(rng, ticks, net, 1, 10, 0.0)
+    seen_p6 = {}
+
+    def check(kk, st_, msgs):
+        if kk == 58:
+            seen_p6["sybil"] = st_.p6[syb[net.col]]
+            seen_p6["graylisted"] = int((st_.score[syb[net.col]] < th.GraylistThreshold).sum())
+
+    run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=beh, after_tick=check)
+    assert (seen_p6["sybil"] > 0).mean() > 0.2, "many views of a sybil carry P6"
+    assert seen_p6["graylisted"] > 0, "some sybils are graylisted"
+
+
+@pytest.mark.gpu
+def test_c5_power_law_zipf_topics_churn(require_gpu):
+    """C5 scaled: power-law graph (rows up to 64), 64 topics with Zipf
+    subscriptions (~8 per peer), connections churning between ticks,
+    publishers outside a topic using fanout."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim import graphs
+    from tickrun import restrict_to_subscriptions, run_parity, subscribed_schedule
+    rng = np.random.default_rng(505)
+    n, T = 3000, 64
+    net = graphs.power_law(n, 16, 2.5, 64, seed=11, n_topics=T)
+    net = graphs.with_subscriptions(net, graphs.zipf_subscriptions(n, T, 8, seed=12))
+    params = beacon_params(T, RetainScore=3 * Second)
+    th = PeerScoreThresholds(GossipThreshold=-20, PublishThreshold=-40, GraylistThreshold=-300)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2, FanoutTTL=3 * Second)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 0.3)
+    restrict_to_subscriptions(st, net)
+    ticks = list(range(1, 7))
+    sched = subscribed_schedule(rng, ticks, net, T, 1.0, 0.02, member_only=False)
+    src = net.owner()
+    und = np.stack([src, net.col], axis=1)
+    und = und[und[:, 0] < und[:, 1]]
+    pick = lambda k: und[rng.choice(len(und), size=len(und) // 50, replace=False)]  # noqa: E731
+    downs = {k: pick(k) for k in (2, 4)}
+    churn = {2: [(downs[2], False)], 4: [(downs[2], True), (downs[4], False)], 6: [(downs[4], True)]}
+    run_parity(net, params, th, gp, st, ticks, sched, ring=1024, churn=churn)
+    assert (np.diff(net.row_ptr.astype(np.int64)) > 32).any(), "rows longer than half a wave"
