@@ -64,6 +64,7 @@ struct Deliver {
     uint64_t* d_cell = nullptr;        // [ring][N] seen-set cells (layout above)
     uint64_t* d_seenbm = nullptr;      // [ring][ceil(N/64)] bit: the cell is committed (a cache of the cells)
     int32_t* d_mpub = nullptr;         // [ring] round the slot's message was published in
+    int64_t* d_roff = nullptr;         // [rounds] offset of each round in its heartbeat
     int32_t* d_lastput = nullptr;      // [T][N]
     uint32_t* d_nnew = nullptr;        // [2][ring/32] bitmask: slots with new claims (or a publication), by round parity
     unsigned long long* d_stats = nullptr;   // [4]
@@ -108,6 +109,7 @@ struct RoundArgs {
     uint64_t* seenbm;          // [ring][nw] committed bits of the cells (read before a cell)
     int64_t nw;                // words per slot
     int32_t* mpub;             // [ring] publication round
+    const int64_t* roff;       // [R] (r + 1) * hb / (R + 1): offset of round r in its heartbeat
     int32_t* lastput;
     uint32_t diag;                 // DIAG_D_* ablations (timing experiments only)
     const uint32_t* nnew_prev;     // bitmask: slots with new claims (or a publication) in round g-1
@@ -126,7 +128,11 @@ struct RoundArgs {
 
 __device__ __forceinline__ int64_t round_time(const RoundArgs& a, int64_t g)
 {
-    return a.t0 + (g / a.R) * a.hb + (g % a.R + 1) * a.hb / (a.R + 1);
+    // T(g) = t0 + (g / R) * hb + (g % R + 1) * hb / (R + 1): rounds fit in 31
+    // bits, and the last term is a table (32-bit division, no 64-bit one)
+    const uint32_t q = (uint32_t)g / (uint32_t)a.R;
+    const uint32_t r = (uint32_t)g - q * (uint32_t)a.R;
+    return a.t0 + (int64_t)q * a.hb + a.roff[r];
 }
 
 // lanes of group `grp` when a wave is split into groups of W lanes
@@ -343,13 +349,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     atomic_inc_capped(&a.meshd[irb[b]], (tpa + t)->mesh_message_deliveries_cap);
             }
         }
-#pragma unroll
+        // the forward body is large: walk the batch without unrolling it, the
+        // cells rotating through cv[0] (registers, static indices)
+#pragma unroll 1
         for (int b = 0; b < B; ++b) {
             const int k = k0 + b;
             if (k >= nact) break;                        // wave-uniform
             const uint32_t m = s_act[k];
             const int64_t row_m = (int64_t)m * a.N;
-            const uint64_t c0 = cv[b];
+            const uint64_t c0 = cv[0];
+#pragma unroll
+            for (int q = 0; q + 1 < B; ++q) cv[q] = cv[q + 1];
             const bool pend = is_claim_of(c0, qpar);     // first received in round g-1 (committed above)
             const uint32_t origin = a.morigin[m];
             const bool inv = a.minv[m] != 0;
@@ -980,7 +990,7 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_seenbm); f(d->d_mpub); f(d->d_lastput);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_seenbm); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
@@ -1025,7 +1035,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.first = h->d_first; a.meshd = h->d_meshd; a.invalid = h->d_invalid; a.mcnt = h->d_mcnt;
     a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv;
     a.cell = d->d_cell; a.lastput = d->d_lastput;
-    a.seenbm = d->d_seenbm; a.nw = (h->n + 63) / 64; a.mpub = d->d_mpub;
+    a.seenbm = d->d_seenbm; a.nw = (h->n + 63) / 64; a.mpub = d->d_mpub; a.roff = d->d_roff;
     const size_t w = (size_t)nnew_words(d);
     a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
     a.nnew_cur = d->d_nnew + (size_t)(g & 1) * w;
@@ -1212,6 +1222,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_cell, ring * N * 8);
     A((void**)&d->d_seenbm, ring * ((N + 63) / 64) * 8);
     A((void**)&d->d_mpub, ring * 4);
+    A((void**)&d->d_roff, (size_t)cfg->rounds * 8);
     A((void**)&d->d_lastput, T * N * 4);
     A((void**)&d->d_nnew, 2 * words * 4);
     A((void**)&d->d_stats, 4 * 8);
@@ -1243,6 +1254,12 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     e = hipMemsetAsync(d->d_cell, 0xFF, ring * N * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_seenbm, 0, ring * ((N + 63) / 64) * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_mpub, 0, ring * 4, h->stream);
+    if (e == hipSuccess) {
+        std::vector<int64_t> roff((size_t)cfg->rounds);
+        for (int32_t r = 0; r < cfg->rounds; ++r)
+            roff[(size_t)r] = (int64_t)(r + 1) * cfg->heartbeat_ns / (cfg->rounds + 1);
+        e = hipMemcpy(d->d_roff, roff.data(), roff.size() * 8, hipMemcpyHostToDevice);
+    }
     if (e == hipSuccess) e = hipMemsetAsync(d->d_lastput, 0xFF, T * N * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_mtopic, 0, ring * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_morigin, 0, ring * 4, h->stream);
