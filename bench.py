@@ -87,7 +87,7 @@ def message_schedule(n: int, T: int, ticks: range, seed: int = 2) -> dict:
 
 def build_engine(cfg, seed, device):
     import gsim
-    from fixtures import beacon_params, beacon_thresholds
+    from gsim.presets import beacon_params, beacon_thresholds
     n, k, T, D, Dlo, Dhi = cfg
     params = beacon_params(T)
     gp = gsim.GossipSubParams(D=D, Dlo=Dlo, Dhi=Dhi)
