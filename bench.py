@@ -153,6 +153,26 @@ def cpu_baseline(cfg, budget_s: float = 15.0):
                       f"OpenMP {threads} threads in the heartbeat phases, {el:.1f}s"}
 
 
+def job_totals(wall: float, deliveries: float, dist=None, device: str = "cpu"):
+    """Whole-job totals over the replica ranks: the slowest
+    rank's wall time (MAX) and the deliveries of all ranks (SUM)."""
+    if dist is None:
+        return wall, deliveries
+    import torch
+    t = torch.tensor([wall, deliveries], device=device, dtype=torch.float64)
+    w = t[:1].clone()
+    dist.all_reduce(w, op=dist.ReduceOp.MAX)
+    d = t[1:].clone()
+    dist.all_reduce(d, op=dist.ReduceOp.SUM)
+    return float(w.item()), float(d.item())
+
+
+def replica_seeds(rank: int):
+    """Every rank simulates its own network: graph/state seed and message
+    schedule seed differ per rank (weak scaling, no data-path collective)."""
+    return 1 + rank, 2 + rank
+
+
 def load_traffic(workload: str):
     path = os.path.join(REPO, "profiles", "traffic.json")
     if not os.path.exists(path):
@@ -184,9 +204,10 @@ def main():
 
     cfg = CONFIGS[args.config]
     n, k, T = cfg[0], cfg[1], cfg[2]
-    eng, net = build_engine(cfg, seed=1 + rank, device=local)
+    g_seed, s_seed = replica_seeds(rank)
+    eng, net = build_engine(cfg, seed=g_seed, device=local)
     E = net.e
-    sched = message_schedule(n, T, range(1, args.warmup + args.steps + 1), seed=2 + rank)
+    sched = message_schedule(n, T, range(1, args.warmup + args.steps + 1), seed=s_seed)
 
     kk = 0
     for _ in range(args.warmup):
@@ -219,16 +240,7 @@ def main():
     census1 = eng.census()
     stats1 = eng.msg_stats()
     gossip1 = eng.gossip_stats()
-    if dist is not None:
-        import torch
-        t = torch.tensor([wall], device=f"cuda:{local}", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
-        d = torch.tensor([stats1[0] - stats0[0]], device=f"cuda:{local}", dtype=torch.float64)
-        dist.all_reduce(d)
-        deliveries = float(d.item())
-    else:
-        deliveries = float(stats1[0] - stats0[0])
+    wall, deliveries = job_totals(wall, float(stats1[0] - stats0[0]), dist, f"cuda:{local}")
 
     if rank == 0:
         K = args.steps

@@ -18,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import bench  # noqa: E402
 
-ARMS = {0: "full", 4096: "send_no_bitmap", 512: "hb_no_emit_gossip", 2048: "hb_no_recompute"}
+ARMS = {0: "full", 32: "send_no_counters", 128: "send_no_rowstate", 64: "send_plain_claim", 4096: "send_no_bitmap", 32 | 128 | 64: "send_cells_only"}
 
 
 def main():
