@@ -97,6 +97,8 @@ def build_engine(cfg, seed, device):
     eng.set_seed(0x5EED0000 + seed)
     eng.fill_synthetic(seed=seed * 7919 + 1, now=tick_time(0), p_mesh=D / k)
     eng.msgs_init(MSG_RING, ROUNDS, tick_time(0), SECOND)
+    if os.environ.get("GSIM_SEND_VARIANT"):          # A/B of the delivery kernel variants (gsim.h)
+        eng.set_kernel_variant(2, int(os.environ["GSIM_SEND_VARIANT"]))
     return eng, net
 
 

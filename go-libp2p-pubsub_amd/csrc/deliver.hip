@@ -532,6 +532,213 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// Delivery round g, topic-major.  Block (p, t) walks the
+// frontier senders of peer range p for every active slot of topic t: the
+// slot's committed bits are staged in LDS first, so the duplicate test of a
+// copy to a receiver seen in an earlier round is an LDS read instead of a
+// random HBM access.  Requires every claim of round g-1 committed (k_commit
+// runs first), so the LDS snapshot holds every receiver seen before round g.
+// Records a block updates — meshMessageDeliveries / invalid of the receivers'
+// records about its senders (record order: the senders' rows), per topic —
+// belong to this block alone; slots of one topic are walked one after the
+// other.  Results are identical to k_send's.
+constexpr int kTmThreads = 1024;
+constexpr int kTmChunk = 2048;      // peers scanned per frontier chunk (two per thread)
+
+template <int W>
+__global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t range)
+{
+    extern __shared__ uint64_t s_bm[];                       // [nw] committed bits, then [ring] u16 slots
+    uint16_t* s_slots = reinterpret_cast<uint16_t*>(s_bm + a.nw);
+    __shared__ uint32_t s_front[kTmChunk];                   // frontier senders (peer | from in s_from)
+    __shared__ uint32_t s_from[kTmChunk];
+    __shared__ uint32_t s_beg[kTmChunk];                     // the sender's row
+    __shared__ uint16_t s_len[kTmChunk];
+    __shared__ int s_ns, s_nf, s_claimed;
+    __shared__ unsigned long long s_stats[4];
+    const int32_t t = (int32_t)blockIdx.y;
+    const int64_t lo = (int64_t)blockIdx.x * range;
+    const int64_t hi = lo + range < a.N ? lo + range : a.N;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (tid == 0) { s_ns = 0; s_stats[0] = s_stats[1] = s_stats[2] = s_stats[3] = 0; }
+    __syncthreads();
+    // active slots of topic t (new claims, or a publication, in round g-1)
+    for (int m = tid; m < a.ring; m += kTmThreads) {
+        if (((a.nnew_prev[m >> 5] >> (m & 31)) & 1u) && (int32_t)a.mtopic[m] == t) {
+            const int q = atomicAdd(&s_ns, 1);
+            s_slots[q] = (uint16_t)m;
+        }
+    }
+    __syncthreads();
+    const int ns = a.g > 0 && lo < a.N ? s_ns : 0;
+    const int grp = lane / W, gl = lane % W;
+    constexpr int G = 64 / W;                                // row groups per wave
+    const ctp_t tp = const_tp(a.tp) + t;
+    const bool scored_t = tp->scored != 0;
+    const int64_t window = tp->mesh_message_deliveries_window_ns;
+    const double mcap = tp->mesh_message_deliveries_cap;
+    const int64_t plane = (int64_t)t * a.E;
+    const uint32_t gprev = (uint32_t)(a.g - 1);
+    const uint32_t par = (uint32_t)(a.g & 1);
+    const uint32_t claim_hi = kClaim | (par << 30);
+    const bool cnt = !(a.diag & DIAG_D_NO_COUNTERS);
+    unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
+    for (int k = 0; k < ns; ++k) {
+        const uint32_t m = s_slots[k];
+        const int64_t row_m = (int64_t)m * a.N;
+        const uint32_t origin = a.morigin[m];
+        const bool inv = a.minv[m] != 0;
+        const uint8_t o_want = ((a.sub[origin] >> t) & 1ull) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
+        const bool win_all = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
+        // stage the slot's committed bits
+        for (int64_t w = tid; w < a.nw; w += kTmThreads) s_bm[w] = a.seenbm[(int64_t)m * a.nw + w];
+        if (tid == 0) s_claimed = 0;
+        const unsigned long long first_before = n_first;
+        __syncthreads();
+        // the cells and row bounds of the next chunk are loaded while the
+        // current chunk's frontier rows are walked
+        constexpr int H = kTmChunk / kTmThreads;
+        uint64_t cs[H];
+        uint32_t rb[H], re[H];
+        auto fetch = [&](int64_t c0) {
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+                const int64_t x = c0 + h * kTmThreads + tid;
+                const bool in = x < hi;
+                cs[h] = in ? a.cell[row_m + x] : kUnseen64;
+                rb[h] = in ? a.row_ptr[x] : 0u;
+                re[h] = in ? a.row_ptr[x + 1] : 0u;
+            }
+        };
+        fetch(lo);
+        for (int64_t c0 = lo; c0 < hi; c0 += kTmChunk) {
+            // frontier of the chunk: first seen (or published) in round g-1
+            if (tid == 0) s_nf = 0;
+            __syncthreads();
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+                const int64_t x = c0 + h * kTmThreads + tid;
+                const uint64_t c = cs[h];
+                const uint32_t chi = (uint32_t)(c >> 32);
+                if (x < hi && c != kUnseen64 && chi == gprev && (!inv || (uint32_t)x == origin)) {
+                    const int q = atomicAdd(&s_nf, 1);
+                    s_front[q] = (uint32_t)x;
+                    s_from[q] = (uint32_t)c & kPeerMask;
+                    s_beg[q] = rb[h];
+                    s_len[q] = (uint16_t)(re[h] - rb[h]);
+                }
+            }
+            __syncthreads();
+            if (c0 + kTmChunk < hi) fetch(c0 + kTmChunk);
+            const int nf = s_nf;
+            // each row group walks P frontier senders' rows at a time; the
+            // counters are loaded with the row state (one memory trip), the
+            // receiver's cell only when its committed bit is not decisive
+            constexpr int P = 2;
+            for (int q0 = wid * G * P; q0 < nf; q0 += (kTmThreads / 64) * G * P) {
+                uint32_t jv[P], fv[P], ev[P], iv[P], nv[P];
+                uint8_t mfv[P], dsv[P], tfv[P];
+                bool vv[P];
+                double xv[P];
+#pragma unroll
+                for (int u = 0; u < P; ++u) {
+                    const int q = q0 + grp * P + u;
+                    const bool vq = q < nf;
+                    jv[u] = vq ? s_front[q] : 0u;
+                    fv[u] = vq ? s_from[q] : 0u;
+                    const uint32_t beg = vq ? s_beg[q] : 0u, len = vq ? s_len[q] : 0u;
+                    vv[u] = vq && (uint32_t)gl < len;
+                    ev[u] = beg + (uint32_t)gl;
+                }
+#pragma unroll
+                for (int u = 0; u < P; ++u) {
+                    iv[u] = 0; mfv[u] = 0; dsv[u] = 0; tfv[u] = 0; nv[u] = 0; xv[u] = 0.0;
+                    if (vv[u]) {
+                        const uint32_t e = ev[u];
+                        iv[u] = a.col[e]; mfv[u] = a.mflags[plane + e]; dsv[u] = a.dstate[e]; tfv[u] = a.tflags[plane + e];
+                        if (inv) xv[u] = a.invalid[plane + e]; else nv[u] = a.mcnt[plane + e];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < P; ++u) {
+                    const uint32_t j = jv[u], e = ev[u], i = iv[u];
+                    const uint8_t ds = dsv[u], tf = tfv[u];
+                    bool sel = (mfv[u] & (j == origin ? o_want : GSIM_TF_MESH)) != 0;
+                    if (a.flood && vv[u] && j == origin) sel = ((a.sub[i] >> t) & 1ull) && a.score[a.rev[e]] >= a.pub_thr;
+                    const bool tg = vv[u] && sel && (ds & GSIM_DS_CONNECTED) && i != fv[u] && i != origin;
+                    const bool ok = tg && (ds & GSIM_DS_ACCEPT);
+                    n_gray += tg && !ok;                         // AcceptFrom: graylisted sender
+                    n_acc += ok;
+                    if (!ok) continue;
+                    const bool sc = scored_t && (ds & GSIM_DS_TRACKED) && cnt;
+                    const bool known = ((s_bm[i >> 6] >> (i & 63)) & 1ull) &&
+                                       (win_all || !sc || inv || !(tf & GSIM_TF_IN_MESH));
+                    const uint64_t c = known ? 0ull : a.cell[row_m + i];
+                    const uint32_t chi = (uint32_t)(c >> 32);
+                    int64_t seen_round = -1;
+                    if (known) seen_round = a.g - 1;             // any earlier round: only "in window" is used
+                    else if (c != kUnseen64) {
+                        if (!(chi & kClaim)) seen_round = chi;
+                        else if (((chi >> 30) & 1u) != par) seen_round = a.g - 1;
+                    }
+                    if (seen_round < 0 && (c == kUnseen64 || (chi & kEdgeMask) > e)) {
+                        uint32_t lo_w = j;
+                        if (sc && !inv) {
+                            lo_w |= kCreditFirst;
+                            if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo_w |= kCreditMesh;
+                        }
+                        const uint64_t cv = ((uint64_t)(claim_hi | e) << 32) | lo_w;
+                        const uint64_t prev = __hip_atomic_fetch_min(a.cell + row_m + i, cv, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT);
+                        if (prev == kUnseen64) n_first++;
+                    }
+                    if (!sc) continue;
+                    const int64_t ir = plane + e;
+                    if (inv) {
+                        a.invalid[ir] = xv[u] + 1.0;                 // markInvalidMessageDelivery
+                    } else if (tf & GSIM_TF_IN_MESH) {
+                        const bool in_window = known ? true
+                                             : seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window)
+                                                               : (window >= 0);
+                        if (in_window) {
+                            uint32_t n = nv[u];
+                            if (n == 255u) {   // spill a full count into the counter (this lane owns the record)
+                                a.meshd[ir] = apply_incs(a.meshd[ir], n, mcap);
+                                n = 0;
+                            }
+                            a.mcnt[ir] = (uint8_t)(n + 1);
+                        }
+                    }
+                }
+            }
+            __syncthreads();                                     // s_front is rewritten by the next chunk
+        }
+        // the slot stays active next round if any copy claimed a new cell
+        if (n_first != first_before) s_claimed = 1;
+        __syncthreads();
+        if (tid == 0 && s_claimed) {
+            atomicOr(&a.nnew_cur[m >> 5], 1u << (m & 31));
+            atomicMax(&a.slot_last[m], (int32_t)a.g);            // mcache activity of the slot
+        }
+        __syncthreads();                                         // s_bm is rewritten by the next slot
+    }
+    n_acc = wave_sum_u64(n_acc);
+    n_gray = wave_sum_u64(n_gray);
+    n_first = wave_sum_u64(n_first);
+    if (lane == 0 && (n_acc | n_gray)) {
+        atomicAdd(&s_stats[0], n_acc);
+        atomicAdd(&s_stats[1], n_first);
+        atomicAdd(&s_stats[3], n_gray);
+    }
+    __syncthreads();
+    if (tid == 0 && (s_stats[0] | s_stats[3])) {
+        atomicAdd(&a.stats[0], s_stats[0]);
+        atomicAdd(&a.stats[1], s_stats[1]);
+        atomicAdd(&a.stats[2], s_stats[0] - s_stats[1]);
+        atomicAdd(&a.stats[3], s_stats[3]);
+    }
+}
+
 // Commit every claim of round g (markSeen + P2 credit) before the state is
 // read or changed by anything but the next round.
 __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
@@ -1175,6 +1382,28 @@ int deliver_read_seen(gsim_handle* h, void* dst)
 }
 
 template <int W>
+static int launch_send_tm(gsim_handle* h, const RoundArgs& a, size_t lds)
+{
+    const int64_t ranges = std::max<int64_t>(1, std::min<int64_t>((h->n + 4095) / 4096,
+                                                                    std::max(1, 1024 / std::max(1, h->t))));
+    const int32_t range = (int32_t)(((h->n + ranges - 1) / ranges + 63) & ~63ll);
+    const int64_t p = (h->n + range - 1) / range;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_send_tm<W>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return hip_check(h, e, "k_send_tm LDS attribute");
+    hipLaunchKernelGGL(k_send_tm<W>, dim3((uint32_t)p, (uint32_t)std::max(1, h->t)), dim3(kTmThreads), lds, h->stream,
+                       a, range);
+    return hip_check(h, hipGetLastError(), "k_send_tm");
+}
+
+// LDS of the topic-major kernel: the slot's committed bits + the slot list
+static size_t send_tm_lds(const gsim_handle* h, const Deliver* d)
+{
+    return (size_t)((h->n + 63) / 64) * 8 + (((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7);
+}
+constexpr size_t kLdsBudget = 160 * 1024 - 24 * 1024;   // minus the static frontier buffers
+
+template <int W>
 static void launch_send(gsim_handle* h, int grid, size_t lds, const RoundArgs& a)
 {
     switch (h->send_variant) {
@@ -1354,13 +1583,29 @@ int gsim_round(gsim_handle* h, int64_t round)
     bool lazy = true;
     for (const auto& tp : h->tp)
         if (tp.scored && tp.mesh_message_deliveries_window_ns < 0) lazy = false;
+    // topic-major delivery when a slot's committed bits fit in LDS: the claims
+    // of round g-1 are committed first (k_commit), then k_send_tm
+    const size_t lds_tm = send_tm_lds(h, d);
+    const bool tm = h->send_variant == 3 && lds_tm <= kLdsBudget;
+    if (tm) {
+        rc = deliver_flush(h);
+        if (rc) return rc;
+    }
     RoundArgs a = make_round_args(h, round);
     h->mcnt_dirty = true;
     const size_t lds = (((size_t)d->cfg.ring + 1) & ~(size_t)1) * sizeof(uint16_t) + (size_t)nnew_words(d) * 4;
     {
         ProfScope ps(h, GSIM_K_SEND);
         const int grid = grid_peers(h->n);
-        if (h->max_degree <= 16)
+        if (tm) {
+            if (h->max_degree <= 16)
+                rc = launch_send_tm<16>(h, a, lds_tm);
+            else if (h->max_degree <= 32)
+                rc = launch_send_tm<32>(h, a, lds_tm);
+            else
+                rc = launch_send_tm<64>(h, a, lds_tm);
+            if (rc) return rc;
+        } else if (h->max_degree <= 16)
             launch_send<16>(h, grid, lds, a);
         else if (h->max_degree <= 32)
             launch_send<32>(h, grid, lds, a);

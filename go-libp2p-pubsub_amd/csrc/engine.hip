@@ -1141,8 +1141,8 @@ int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant)
         h->diag = (uint32_t)variant;
         return GSIM_OK;
     }
-    if (which == 2) {           // k_send: 0 = 8-slot batch, 1 = 4-slot batch at >= 7 waves/SIMD, 2 = 4-slot batch
-        if (variant < 0 || variant > 2) { h->err = "unknown k_send variant"; return GSIM_EINVAL; }
+    if (which == 2) {           // k_send: 0 = 8-slot batch, 1 = 4-slot batch at >= 7 waves/SIMD, 2 = 4-slot batch, 3 = topic-major
+        if (variant < 0 || variant > 3) { h->err = "unknown k_send variant"; return GSIM_EINVAL; }
         h->send_variant = variant;
         return GSIM_OK;
     }

@@ -153,7 +153,7 @@ struct gsim_handle {
     bool p6_dirty = true;
     bool maybe_retained = false;
     int score_variant = -1;   // refresh+score kernel variant (-1: from env)
-    int send_variant = 0;     // k_send slot batch / occupancy variant (gsim_set_kernel_variant(h, 2, v))
+    int send_variant = 3;     // delivery kernel variant (gsim_set_kernel_variant(h, 2, v)); 3 = topic-major
     uint32_t diag = 0;        // DIAG_* ablations (A/B diagnostics only)
 
     // device: parameters and scratch flags

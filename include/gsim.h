@@ -384,8 +384,10 @@ int gsim_profile_read(gsim_handle* h, double* ms, int64_t* launches, int32_t n);
  * refreshScores+score pass; variant 0 thread-per-edge, 2 wave (4-topic
  * chunks, default), 3 wave (8-topic chunks).  which = 1: diagnostic ablation
  * mask for timing experiments (results are wrong while it is non-zero).
- * which = 2: the delivery kernel; variant 0 loads 8 slots' cells per trip
- * (default), 1 loads 4 with registers capped for 7 waves per SIMD, 2 loads 4. */
+ * which = 2: the delivery kernel; variant 3 (default) is topic-major with the
+ * slots' committed bits staged in LDS (used while they fit: N <= ~1.1M peers),
+ * else peer-major k_send: 0 loads 8 slots' cells per trip, 1 loads 4 with
+ * registers capped for 7 waves per SIMD, 2 loads 4. */
 int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant);
 
 /* ---- synthetic inputs -------------------------------- */

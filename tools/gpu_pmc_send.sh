@@ -10,7 +10,7 @@ cd /tmp
 timeout -s KILL 60 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
 run() {
   local name="$1"; shift
-  timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-include-regex "k_send" -d "$OUT/$name" -o run --output-format csv \
+  timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-include-regex "${KRE:-k_send}" -d "$OUT/$name" -o run --output-format csv \
     -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "$name rc=$rc"
