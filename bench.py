@@ -272,7 +272,7 @@ def main():
             tr_send = dict(tr_send, bytes_per_tick=per_tick)
         roof_deliv = {"bound": "hbm", "achieved": deliv_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": deliv_gbs / HBM_PEAK_GBS, "traffic": tr_send,
-                      "kernel": "k_send+k_commit+k_accept (per tick)", "kernel_ms": deliv_ms,
+                      "kernel": "delivery: k_send_tm + k_commit + k_delivery_state (per tick, 10 rounds)", "kernel_ms": deliv_ms,
                       "algorithmic_bytes_per_tick": alg_deliv}
         dominant = roof_refresh if ref_ms * launches["refresh_score"] / K >= deliv_ms else roof_deliv
         out = {
