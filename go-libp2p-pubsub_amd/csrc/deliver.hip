@@ -418,6 +418,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     if (v1 && j1 == origin) sel1 = ((a.sub[i1] >> t) & 1ull) && a.score[a.rev[e1]] >= a.pub_thr;
                     if (v2 && j2 == origin) sel2 = ((a.sub[i2] >> t) & 1ull) && a.score[a.rev[e2]] >= a.pub_thr;
                 }
+                // direct peers that joined the topic always get it (gossipsub.go:991-1003)
+                if (v1 && (ds1 & GSIM_DS_DIRECT) && !sel1) sel1 = (a.sub[i1] >> t) & 1ull;
+                if (v2 && (ds2 & GSIM_DS_DIRECT) && !sel2) sel2 = (a.sub[i2] >> t) & 1ull;
                 const bool tg1 = v1 && sel1 && (ds1 & GSIM_DS_CONNECTED) && i1 != f1 && i1 != origin;
                 const bool tg2 = v2 && sel2 && (ds2 & GSIM_DS_CONNECTED) && i2 != f2 && i2 != origin;
                 const bool ok1 = tg1 && (ds1 & GSIM_DS_ACCEPT), ok2 = tg2 && (ds2 & GSIM_DS_ACCEPT);
@@ -665,6 +668,8 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
                     const uint8_t ds = dsv[u], tf = tfv[u];
                     bool sel = (mfv[u] & (j == origin ? o_want : GSIM_TF_MESH)) != 0;
                     if (a.flood && vv[u] && j == origin) sel = ((a.sub[i] >> t) & 1ull) && a.score[a.rev[e]] >= a.pub_thr;
+                    // direct peers that joined the topic always get it (gossipsub.go:991-1003)
+                    if (vv[u] && (ds & GSIM_DS_DIRECT) && !sel) sel = (a.sub[i] >> t) & 1ull;
                     const bool tg = vv[u] && sel && (ds & GSIM_DS_CONNECTED) && i != fv[u] && i != origin;
                     const bool ok = tg && (ds & GSIM_DS_ACCEPT);
                     n_gray += tg && !ok;                         // AcceptFrom: graylisted sender

@@ -529,13 +529,17 @@ __global__ __launch_bounds__(256) void k_estate_split(const uint8_t* in, uint8_t
 // bit of edge e, and of record e the AcceptFrom verdict (gossipsub.go:598-609:
 // score snapshot >= graylistThreshold) and whether it is tracked.
 __global__ __launch_bounds__(256) void k_delivery_state(const double* score, const uint8_t* estate,
-                                                        const uint8_t* rstate, uint8_t* ds, int64_t E, double gray)
+                                                        const uint8_t* rstate, const uint8_t* direct,
+                                                        const uint32_t* rev, uint8_t* ds, int64_t E, double gray)
 {
+    // AcceptFrom is the receiver's: its direct peers are accepted whatever
+    // their score (gossipsub.go:598-609); its flag for the sender sits at rev[r]
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < E; r += stride)
         ds[r] = (uint8_t)(((rstate[r] & GSIM_ES_CONNECTED) ? GSIM_DS_CONNECTED : 0) |
-                          (score[r] >= gray ? GSIM_DS_ACCEPT : 0) |
-                          ((estate[r] & GSIM_ES_TRACKED) ? GSIM_DS_TRACKED : 0));
+                          ((score[r] >= gray || direct[rev[r]]) ? GSIM_DS_ACCEPT : 0) |
+                          ((estate[r] & GSIM_ES_TRACKED) ? GSIM_DS_TRACKED : 0) |
+                          (direct[r] ? GSIM_DS_DIRECT : 0));
 }
 
 __global__ void k_fill_u8(uint8_t* p, int64_t n, uint8_t v)
@@ -590,7 +594,7 @@ int hip_check(gsim_handle* h, hipError_t e, const char* what)
 void free_graph(gsim_handle* h)
 {
     dfree(h->d_row_ptr); dfree(h->d_col); dfree(h->d_rev); dfree(h->d_owner);
-    dfree(h->d_sub); dfree(h->d_outbound);
+    dfree(h->d_sub); dfree(h->d_outbound); dfree(h->d_direct);
     dfree(h->d_ip_ptr); dfree(h->d_ip_ids); dfree(h->d_ip_white); dfree(h->d_p5);
     dfree(h->d_first); dfree(h->d_meshd); dfree(h->d_fail); dfree(h->d_invalid);
     dfree(h->d_graft); dfree(h->d_mtime); dfree(h->d_tflags); dfree(h->d_mflags);
@@ -715,7 +719,8 @@ int refresh_accept(gsim_handle* h)
 {
     if (h->acc_version == h->score_version) return GSIM_OK;
     hipLaunchKernelGGL(k_delivery_state, dim3(grid_for(h->e)), dim3(256), 0, h->stream, (const double*)h->d_score,
-                       (const uint8_t*)h->d_estate, (const uint8_t*)h->d_rstate, h->d_dstate, h->e,
+                       (const uint8_t*)h->d_estate, (const uint8_t*)h->d_rstate, (const uint8_t*)h->d_direct,
+                       (const uint32_t*)h->d_rev, h->d_dstate, h->e,
                        h->th.graylist_threshold);
     h->acc_version = h->score_version;
     return hip_check(h, hipGetLastError(), "k_delivery_state");
@@ -965,6 +970,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     rc = rc ? rc : dalloc(h, &h->d_owner, E);
     rc = rc ? rc : dalloc(h, &h->d_sub, n);
     rc = rc ? rc : dalloc(h, &h->d_outbound, E);
+    rc = rc ? rc : dalloc(h, &h->d_direct, E);
     rc = rc ? rc : dalloc(h, &h->d_ip_ptr, n + 1);
     rc = rc ? rc : dalloc(h, &h->d_ip_ids, nip);
     rc = rc ? rc : dalloc(h, &h->d_ip_white, (int64_t)n_ips);
@@ -1003,6 +1009,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     up(h->d_owner, owner.data(), sizeof(uint32_t) * (size_t)E);
     if (subs) up(h->d_sub, subs, sizeof(uint64_t) * (size_t)n); else zero(h->d_sub, sizeof(uint64_t) * (size_t)n);
     if (outbound) up(h->d_outbound, outbound, (size_t)E); else zero(h->d_outbound, (size_t)E);
+    zero(h->d_direct, (size_t)E);
     if (ip_ptr) {
         up(h->d_ip_ptr, ip_ptr, sizeof(uint32_t) * (size_t)(n + 1));
         up(h->d_ip_ids, ip_ids, sizeof(uint32_t) * (size_t)nip);
@@ -1050,6 +1057,17 @@ int gsim_set_app_score(gsim_handle* h, const double* p5)
     hipError_t e = hipMemcpyAsync(h->d_p5, p5, sizeof(double) * (size_t)h->n, hipMemcpyHostToDevice, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     return hip_check(h, e, "gsim_set_app_score");
+}
+
+int gsim_set_direct_peers(gsim_handle* h, const uint8_t* direct)
+{
+    GSIM_ENTER(h);
+    GSIM_NEED_GRAPH(h);
+    hipError_t e = direct ? hipMemcpyAsync(h->d_direct, direct, (size_t)h->e, hipMemcpyHostToDevice, h->stream)
+                          : hipMemsetAsync(h->d_direct, 0, (size_t)h->e, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    h->score_version++;          // AcceptFrom and the send sets read the flags through the delivery state
+    return hip_check(h, e, "gsim_set_direct_peers");
 }
 
 int gsim_set_ip_whitelist(gsim_handle* h, const uint8_t* white)

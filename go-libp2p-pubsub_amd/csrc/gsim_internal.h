@@ -164,6 +164,7 @@ struct gsim_handle {
     uint32_t *d_row_ptr = nullptr, *d_col = nullptr, *d_rev = nullptr, *d_owner = nullptr;
     uint64_t* d_sub = nullptr;
     uint8_t* d_outbound = nullptr;
+    uint8_t* d_direct = nullptr;       // [E] edge order: col[e] is in the observer's gs.direct set
     uint32_t *d_ip_ptr = nullptr, *d_ip_ids = nullptr;
     uint8_t* d_ip_white = nullptr;
     double* d_p5 = nullptr;
@@ -223,6 +224,7 @@ enum : uint8_t {
     GSIM_DS_CONNECTED = 0x01,   // router: the sender (row owner) is connected to col[e]
     GSIM_DS_ACCEPT = 0x02,      // record e: the receiver accepts RPCs from the sender (AcceptFrom)
     GSIM_DS_TRACKED = 0x04,     // record e: the receiver keeps peerStats for the sender
+    GSIM_DS_DIRECT = 0x08,      // router: col[e] is one of the sender's direct peers (always sent to)
 };
 
 // Brackets the launches of one kernel class with pooled HIP events on the

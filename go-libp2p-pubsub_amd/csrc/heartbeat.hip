@@ -33,6 +33,7 @@ struct HbArgs {
     const uint32_t *row_ptr, *col, *rev;
     const uint64_t* sub;
     const uint8_t* outbound;
+    const uint8_t* direct;     // [E] edge order: col[e] is in the observer's gs.direct set
     const uint8_t* estate;
     const double* score;
     const gsim_topic_score_params* tp;
@@ -297,6 +298,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
         const bool tracked = est & GSIM_ES_TRACKED;
         const bool conn = valid && (a.rstate[e] & GSIM_ES_CONNECTED);
         const bool outb = valid && a.outbound[e];
+        const bool dir = valid && a.direct[e];          // direct peers are never grafted or gossiped to
         const double S = valid ? a.score[rv] : 0.0;
         const uint64_t subj = valid ? a.sub[col] : 0ull;
         const uint64_t subi = a.sub[obs];
@@ -379,7 +381,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             int l = __popcll(ballot(m));
             if (l < a.Dlo) {
                 need_bo();
-                const bool cand = tpeer && !m && bo == 0 && S >= 0;
+                const bool cand = tpeer && !m && bo == 0 && !dir && S >= 0;
                 if (select_smallest(a, cand, a.D - l, (uint32_t)obs, t, P_GRAFT_DLO, col, pos)) graft();
             }
 
@@ -437,7 +439,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
                 const int ob = __popcll(ballot(m && outb));
                 if (ob < a.Dout) {
                     need_bo();
-                    const bool cand = tpeer && !m && bo == 0 && outb && S >= 0;
+                    const bool cand = tpeer && !m && bo == 0 && !dir && outb && S >= 0;
                     if (select_smallest(a, cand, a.Dout - ob, (uint32_t)obs, t, P_GRAFT_DOUT, col, pos)) graft();
                 }
             }
@@ -455,7 +457,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
                 const double median = __shfl(S, (int)__ffsll((long long)at) - 1, 64);
                 if (median < a.opp_threshold) {
                     need_bo();
-                    const bool cand = tpeer && !m && bo == 0 && S > median;
+                    const bool cand = tpeer && !m && bo == 0 && !dir && S > median;
                     if (select_smallest(a, cand, a.opp_peers, (uint32_t)obs, t, P_GRAFT_OPP, col, pos)) graft();
                 }
             }
@@ -483,7 +485,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
                         if (dirty) S_live = score_of_record(a, rv, col);
                         dirty = false;
                     }
-                    const bool gcand = tpeer && !m && S_live >= a.gossip_thr;
+                    const bool gcand = tpeer && !m && !dir && S_live >= a.gossip_thr;
                     gsel = gossip_targets(a, gcand, tpeer, (uint32_t)obs, t, col, pos);
                 }
                 if (valid && !(a.diag & 2)) a.gsel[i] = gsel ? 1 : 0;
@@ -533,6 +535,7 @@ __global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
         const uint32_t col = valid ? a.col[e] : 0u;
         const uint32_t rv = valid ? a.rev[e] : 0u;
         const bool conn = valid && (a.rstate[e] & GSIM_ES_CONNECTED);
+        const bool dir = valid && a.direct[e];
         const double S = valid ? a.score[rv] : 0.0;
         const uint64_t subj = valid ? a.sub[col] : 0ull;
         const int32_t lp_lane = (a.gossip && lane < a.T) ? a.lastput[(int64_t)lane * a.N + obs] : -1;
@@ -546,7 +549,7 @@ __global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
             bool inf = (fl & GSIM_TF_FANOUT) && tpeer && S >= a.pub_thr;
             const int have = __popcll(ballot(inf));
             if (have < a.D) {
-                const bool cand = tpeer && !inf && S >= a.pub_thr;
+                const bool cand = tpeer && !inf && !dir && S >= a.pub_thr;
                 if (select_smallest(a, cand, a.D - have, (uint32_t)obs, t, P_FANOUT, col, (uint32_t)lane)) inf = true;
             }
             const uint8_t nf = inf ? (uint8_t)(fl | GSIM_TF_FANOUT) : (uint8_t)(fl & ~GSIM_TF_FANOUT);
@@ -558,7 +561,7 @@ __global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
                     if (valid) S_live = score_of_record(a, rv, col);
                     have_live = true;
                 }
-                const bool gcand = tpeer && !inf && S_live >= a.gossip_thr;
+                const bool gcand = tpeer && !inf && !dir && S_live >= a.gossip_thr;
                 gsel = gossip_targets(a, gcand, tpeer, (uint32_t)obs, t, col, (uint32_t)lane);
             }
             if (valid) a.gsel[i] = gsel ? 1 : 0;
@@ -616,7 +619,10 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                     const int64_t bo0 = bo;
                     uint8_t reply = 0;
                     if ((c & GSIM_CTL_GRAFT) && !(fl & GSIM_TF_MESH)) {
-                        if (bo != 0 && a.now < bo) {
+                        if (a.direct[e]) {
+                            // no GRAFT to/from direct peers: answered with PRUNE (gossipsub.go:768-776)
+                            reply = GSIM_CTL_PRUNE;
+                        } else if (bo != 0 && a.now < bo) {
                             // GRAFT while backing off: P7 penalty (+1 more under the flood cutoff)
                             if (tracked) {
                                 double x = a.bp[rv] + 1.0;
@@ -793,7 +799,7 @@ __global__ __launch_bounds__(256) void k_fanout_publish(HbArgs a, const gsim_msg
         const bool conn = valid && (a.rstate[e] & GSIM_ES_CONNECTED);
         const bool tpeer = conn && ((a.sub[col] >> t) & 1ull);
         const double S = valid ? a.score[a.rev[e]] : 0.0;
-        const bool cand = tpeer && !(fl & GSIM_TF_FANOUT) && S >= a.pub_thr;
+        const bool cand = tpeer && !(fl & GSIM_TF_FANOUT) && !(valid && a.direct[e]) && S >= a.pub_thr;
         const bool sel = select_smallest(a, cand, a.D, o, t, P_FANOUT_NEW, col, (uint32_t)lane);
         if (valid && sel) a.mflags[i] = (uint8_t)(fl | GSIM_TF_FANOUT);
         const bool any = __ballot(sel) != 0;
@@ -866,7 +872,7 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     HbArgs a{};
     a.N = h->n; a.E = h->e; a.T = h->t;
     a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.rev = h->d_rev; a.sub = h->d_sub;
-    a.outbound = h->d_outbound; a.estate = h->d_estate; a.score = h->d_score; a.tp = h->d_tp;
+    a.outbound = h->d_outbound; a.direct = h->d_direct; a.estate = h->d_estate; a.score = h->d_score; a.tp = h->d_tp;
     a.tflags = h->d_tflags; a.mflags = h->d_mflags; a.rstate = h->d_rstate; a.backoff = h->d_backoff; a.meshd = h->d_meshd; a.fail = h->d_fail; a.bp = h->d_bp;
     a.graft = h->d_graft; a.mtime = h->d_mtime; a.mcnt = h->d_mcnt;
     const size_t TE = (size_t)h->e * (size_t)std::max(1, h->t);

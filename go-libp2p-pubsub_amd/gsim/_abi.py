@@ -151,6 +151,7 @@ SIGNATURES = [
     ("gsim_set_peer_behaviour", c_int32, [c_void_p, c_void_p]),
     ("gsim_gossip_stats", c_int32, [c_void_p, c_void_p]),
     ("gsim_set_connections", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int64]),
+    ("gsim_set_direct_peers", c_int32, [c_void_p, c_void_p]),
     ("gsim_profile", c_int32, [c_void_p, c_int32]),
     ("gsim_profile_read", c_int32, [c_void_p, c_void_p, c_void_p, c_int32]),
 ]

@@ -264,6 +264,17 @@ class Engine:
         p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint32).reshape(-1, 2))
         self._check(self.lib.gsim_set_connections(self.h, _ptr(p), int(p.shape[0]), 1 if up else 0, int(now)))
 
+    def set_direct_peers(self, flags):
+        """WithDirectPeers as per-edge flags (edge order; None clears)
+        (gsim_set_direct_peers; gossipsub.go:352-374)."""
+        if flags is None:
+            self._check(self.lib.gsim_set_direct_peers(self.h, None))
+            return
+        f = np.ascontiguousarray(flags, dtype=np.uint8)
+        if f.shape != (self.net.e,):
+            raise ValueError("direct flags: one byte per edge")
+        self._check(self.lib.gsim_set_direct_peers(self.h, _ptr(f)))
+
     def gossip_stats(self) -> dict:
         out = np.zeros(4, dtype=np.int64)
         self._check(self.lib.gsim_gossip_stats(self.h, _ptr(out)))

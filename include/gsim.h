@@ -189,6 +189,13 @@ int gsim_set_app_score(gsim_handle* h, const double* p5);
 /* IPColocationFactorWhitelist (score_params.go:91): whitelisted[ip_id] = 1 if
  * any whitelisted CIDR contains that IP (host precomputes net.IPNet.Contains). */
 int gsim_set_ip_whitelist(gsim_handle* h, const uint8_t* whitelisted);
+/* WithDirectPeers (gossipsub.go:352-374): flags[e] != 0 when col[e] is in
+ * the observer's direct set (E bytes, edge order; NULL clears).  Direct
+ * peers are never grafted or gossiped to, GRAFTs from them are answered
+ * with PRUNE (gossipsub.go:768-776), they receive every message of a topic
+ * they joined (991-1003) and AcceptFrom accepts them whatever their score
+ * (598-609).  The reconnect loop (directConnect) is not modelled. */
+int gsim_set_direct_peers(gsim_handle* h, const uint8_t* flags);
 /* SetTopicScoreParams (score.go:201-241, topic.go:44-82): validates, installs,
  * and recaps first/mesh counters when caps are lowered. */
 int gsim_set_topic_params(gsim_handle* h, int32_t topic, const gsim_topic_score_params* p);

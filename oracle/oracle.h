@@ -58,6 +58,7 @@ typedef struct orc_net {
     uint8_t* ctl;              /* [2][T][E] control inbox by round parity */
     int64_t* lastpub;          /* [N][T] gs.lastpub[topic] (ns), 0 = none (peer-major) */
     uint64_t* fan_topics;      /* [N] bit t: gs.fanout[topic t] exists */
+    const uint8_t* direct;     /* [E] col[e] is in the observer's gs.direct set (WithDirectPeers), or NULL */
 } orc_net;
 
 /* ---- message propagation (oracle_deliver.c) ------------------------------ */

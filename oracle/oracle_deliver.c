@@ -135,9 +135,11 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
         const uint8_t want = (j == origin && !((s->sub[j] >> t) & 1u)) ? GSIM_TF_FANOUT : GSIM_TF_MESH;
         for (uint32_t e = s->row_ptr[j]; e < s->row_ptr[j + 1]; ++e) {
             const uint32_t i = s->col[e];
+            /* direct peers in the topic always get it (gossipsub.go:991-1003) */
+            const int direct = s->direct && s->direct[e] && ((s->sub[i] >> t) & 1u);
             if (flood) {
-                if (!((s->sub[i] >> t) & 1u) || s->score[e] < s->th->publish_threshold) continue;
-            } else if (!(s->tflags[(int64_t)t * s->e + e] & want)) {
+                if (!direct && (!((s->sub[i] >> t) & 1u) || s->score[e] < s->th->publish_threshold)) continue;
+            } else if (!direct && !(s->tflags[(int64_t)t * s->e + e] & want)) {
                 continue;
             }
             if (!(s->estate[e] & GSIM_ES_CONNECTED)) continue;
@@ -158,7 +160,7 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
     for (int64_t q = 0; q < nar; ++q) {
         const uint32_t i = ar[q].recv, slot = ar[q].slot, er = ar[q].er;
         const int32_t t = (int32_t)m->topic[slot];
-        if (s->score[er] < gray) {             /* AcceptFrom -> AcceptNone */
+        if (s->score[er] < gray && !(s->direct && s->direct[er])) {   /* AcceptFrom -> AcceptNone; direct: AcceptAll */
             m->stats[3]++;
             continue;
         }

@@ -117,6 +117,7 @@ void orc_gossip_emit(orc_net* s, orc_msgs* m, uint32_t i, int32_t t, uint64_t ti
     for (uint32_t e = b; e < en; ++e) {
         if (!topic_peer(s, e, t)) continue;
         if (s->tflags[te(s, t, e)] & exclude) continue;                    /* exclude: mesh / fanout */
+        if (s->direct && s->direct[e]) continue;                           /* no gossip to direct peers */
         if (orc_score_edge(s, e) < s->th->gossip_threshold) continue;        /* live Score(p) */
         L[n].key = okey(seed, tick, i, t, P_GOSSIP, s->col[e], e - b);
         L[n].v = e;

@@ -51,6 +51,9 @@ static inline int topic_peer(const hb* h, uint32_t e)
     return (h->s->estate[e] & ES_CONN) && ((h->s->sub[h->s->col[e]] >> h->t) & 1u);
 }
 
+/* gs.direct (WithDirectPeers, gossipsub.go:352-374): never grafted, always sent to */
+static inline int is_direct(const hb* h, uint32_t e) { return h->s->direct && h->s->direct[e]; }
+
 static int mesh_count(const hb* h)
 {
     int c = 0;
@@ -110,18 +113,18 @@ static int get_peers(const hb* h, int count, filter_fn f, double arg, uint32_t p
 static int f_graft(const hb* h, uint32_t e, double arg)      /* gossipsub.go:1416-1422 */
 {
     (void)arg;
-    return !in_mesh(h, e) && !has_backoff(h, e) && h->s->score[e] >= 0;
+    return !in_mesh(h, e) && !has_backoff(h, e) && !is_direct(h, e) && h->s->score[e] >= 0;
 }
 
 static int f_dout(const hb* h, uint32_t e, double arg)       /* gossipsub.go:1506-1512 */
 {
     (void)arg;
-    return !in_mesh(h, e) && !has_backoff(h, e) && h->s->outbound[e] && h->s->score[e] >= 0;
+    return !in_mesh(h, e) && !has_backoff(h, e) && !is_direct(h, e) && h->s->outbound[e] && h->s->score[e] >= 0;
 }
 
 static int f_opp(const hb* h, uint32_t e, double median)     /* gossipsub.go:1540-1545 */
 {
-    return !in_mesh(h, e) && !has_backoff(h, e) && h->s->score[e] > median;
+    return !in_mesh(h, e) && !has_backoff(h, e) && !is_direct(h, e) && h->s->score[e] > median;
 }
 
 /* stable insertion sort by score descending (sort.Slice with the score
@@ -228,7 +231,7 @@ static inline int in_fanout(const hb* h, uint32_t e) { return (h->s->tflags[ti(h
 
 static int f_fanout(const hb* h, uint32_t e, double thr)     /* gossipsub.go:1580-1584, 1020-1023 */
 {
-    return !in_fanout(h, e) && h->s->score[e] >= thr;
+    return !in_fanout(h, e) && !is_direct(h, e) && h->s->score[e] >= thr;
 }
 
 /* Fanout expiry and maintenance for one observer, after its mesh topics
@@ -350,6 +353,10 @@ static void handle_graft(hb* h, uint32_t e)
     const gsim_gossipsub_params* gp = s->gp;
     if (!((s->sub[h->i] >> h->t) & 1u)) return;                /* unknown topic: ignore */
     if (in_mesh(h, e)) return;                                 /* already in mesh */
+    if (is_direct(h, e)) {                                     /* no GRAFT from direct peers: PRUNE */
+        send_ctl(h, e, GSIM_CTL_PRUNE);
+        return;
+    }
     int64_t expire = s->backoff[ti(h, e)];
     if (expire != 0 && h->now < expire) {                      /* backing off that peer */
         orc_add_penalty(s, e, 1);

@@ -32,7 +32,7 @@ class OrcNet(Structure):
         ("bp", c_void_p), ("estate", c_void_p), ("expire", c_void_p), ("p6", c_void_p), ("score", c_void_p),
         ("backoff", c_void_p),
         ("pp", c_void_p), ("tp", c_void_p), ("th", c_void_p), ("gp", c_void_p),
-        ("ctl", c_void_p), ("lastpub", c_void_p), ("fan_topics", c_void_p),
+        ("ctl", c_void_p), ("lastpub", c_void_p), ("fan_topics", c_void_p), ("direct", c_void_p),
     ]
 
 
@@ -148,6 +148,7 @@ class NetState:
         self.ctl = np.zeros((2, self.T, E), dtype=np.uint8)
         self.lastpub = np.zeros((net.n, self.T), dtype=np.int64)
         self.fan_topics = np.zeros(net.n, dtype=np.uint64)
+        self.direct = np.zeros(E, dtype=np.uint8)          # gs.direct flags (configuration, not state)
         self.rev = net.rev()
         self.p5 = np.zeros(net.n) if p5 is None else np.ascontiguousarray(p5, dtype=np.float64)
         self.ip_white = None if ip_white is None else np.ascontiguousarray(ip_white, dtype=np.uint8)
@@ -177,6 +178,7 @@ class NetState:
         v.gp = ctypes.cast(ctypes.byref(self.gp), c_void_p)
         v.ctl = _p(self.ctl)
         v.lastpub, v.fan_topics = _p(self.lastpub), _p(self.fan_topics)
+        v.direct = _p(self.direct)
         self._view = v
         return ctypes.byref(v)
 
@@ -196,6 +198,7 @@ class NetState:
         eng.write(_abi.F_CTL, self.ctl)
         eng.write(_abi.F_LASTPUB, self.lastpub)
         eng.write(_abi.F_FANOUT_TOPICS, self.fan_topics)
+        eng.set_direct_peers(self.direct)
 
     def pull_from_engine(self, eng):
         for f in self.TOPIC_FIELDS + self.EDGE_FIELDS:
