@@ -1079,14 +1079,16 @@ __device__ __forceinline__ void atomic_mcnt_inc(uint8_t* mcnt, int64_t ir, doubl
 }
 
 __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint64_t* resp, const uint32_t* nresp,
-                                                       const uint32_t* owner)
+                                                       const uint32_t* owner, int64_t resp_cap)
 {
     extern __shared__ uint32_t s_new2[];
     __shared__ unsigned long long s_stats[4];
     for (int w = threadIdx.x; w < (a.ring + 31) / 32; w += blockDim.x) s_new2[w] = 0;
     if (threadIdx.x < 4) s_stats[threadIdx.x] = 0;
     __syncthreads();
-    const uint32_t n = *nresp;
+    // responses beyond the queue's capacity were dropped (reported as an
+    // overflow by gsim_msg_stats): only the stored ones are read
+    const uint32_t n = (uint32_t)min((int64_t)*nresp, resp_cap);
     const uint32_t par = (uint32_t)(a.g & 1);
     const uint32_t claim_hi = kClaim | (par << 30);
     const ctp_t tpa = const_tp(a.tp);
@@ -1630,7 +1632,7 @@ int gsim_round(gsim_handle* h, int64_t round)
         ProfScope ps(h, GSIM_K_GOSSIP);
         const size_t lds2 = (size_t)nnew_words(d) * 4;
         hipLaunchKernelGGL(k_gossip_deliver, dim3(2048), dim3(256), lds2, h->stream, a, (const uint64_t*)d->d_resp,
-                           (const uint32_t*)d->d_nresp, (const uint32_t*)h->d_owner);
+                           (const uint32_t*)d->d_nresp, (const uint32_t*)h->d_owner, d->resp_cap);
         d->resp_round = -1;
         rc = hip_check(h, hipGetLastError(), "k_gossip_deliver");
         if (rc) return rc;

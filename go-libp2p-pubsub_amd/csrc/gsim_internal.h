@@ -55,6 +55,8 @@ enum : uint32_t {
     DIAG_H_NO_IHAVE_STORE = 1024,   // heartbeat: choose gossip targets but do not store the marks
     DIAG_H_NO_RECOMPUTE = 2048,     // heartbeat: emitGossip uses the snapshot score (no live recompute)
     DIAG_D_NO_BITMAP = 4096,        // delivery: read every receiver's cell (no committed-bit shortcut; results unchanged)
+    DIAG_H_NO_SELECT = 8192,        // heartbeat: emitGossip takes every candidate (no shuffle/selection)
+    DIAG_H_CHEAP_KEYS = 16384,      // heartbeat: selection keys from a multiply hash instead of Philox
 };
 
 struct ColocArgs {

@@ -110,21 +110,45 @@ __device__ __forceinline__ uint32_t hb_key_hi(const HbArgs& a, uint32_t obs, int
 // A key is (32 random bits, row position); the row position is the lane, so
 // each round takes the wave minimum of the random word and breaks ties by
 // the lowest lane.
+//
+// The keys are uniform, so a threshold tau = count/n of the key range already
+// selects about `count` lanes with one ballot; the few lanes too many (or too
+// few) are then removed largest-first (added smallest-first) by wave
+// reductions.  Keys below tau precede every key above it whatever the lane, so
+// the result is exactly the `count` smallest (key, lane) pairs.
 __device__ bool select_smallest(const HbArgs& a, bool cand, int count, uint32_t obs, int32_t t, uint32_t purpose,
                                 uint32_t col, uint32_t pos)
 {
-    uint64_t avail = __ballot(cand);
+    const uint64_t avail = __ballot(cand);
     const int n = __popcll(avail);
     if (n == 0) return false;
     if (count <= 0 || n <= count) return cand;
     const int lane = threadIdx.x & 63;
-    uint32_t hi = cand ? hb_key_hi(a, obs, t, purpose, col, pos) : 0xFFFFFFFFu;
-    bool sel = false;
-    for (int c = 0; c < count; ++c) {
-        const uint32_t mn = wave_min_u32(hi);
-        const int win = __ffsll((long long)(__ballot(hi == mn) & avail)) - 1;
-        avail &= ~(1ull << win);
-        if (lane == win) { sel = true; hi = 0xFFFFFFFFu; }
+    uint32_t hi = 0xFFFFFFFFu;
+    if (cand) {
+        if (a.diag & 32) hi = (col ^ (uint32_t)t * 0x85EBCA6Bu) * 0x9E3779B9u;   // timing ablation only
+        else hi = hb_key_hi(a, obs, t, purpose, col, pos);
+    }
+    // any threshold gives the same selection; it only sets how many lanes the
+    // loops below adjust (fp32: no 64-bit integer division)
+    const uint32_t tau = (uint32_t)((float)count / (float)n * 4294967040.0f);
+    bool sel = cand && hi < tau;
+    int c = __popcll(__ballot(sel));
+    while (c > count) {                 // drop the largest (key, lane) among the selected
+        const uint32_t mx = ~wave_min_u32(sel ? ~hi : 0xFFFFFFFFu);
+        const uint64_t at = __ballot(sel && hi == mx);
+        const int win = 63 - __clzll((long long)at);
+        if (lane == win) sel = false;
+        --c;
+    }
+    uint32_t rest = (cand && !sel) ? hi : 0xFFFFFFFFu;
+    uint64_t left = __ballot(cand && !sel);
+    while (c < count) {                 // add the smallest (key, lane) among the others
+        const uint32_t mn = wave_min_u32(rest);
+        const int win = __ffsll((long long)(__ballot(rest == mn) & left)) - 1;
+        left &= ~(1ull << win);
+        if (lane == win) { sel = true; rest = 0xFFFFFFFFu; }
+        ++c;
     }
     return sel;
 }
@@ -486,7 +510,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
                         dirty = false;
                     }
                     const bool gcand = tpeer && !m && !dir && S_live >= a.gossip_thr;
-                    gsel = gossip_targets(a, gcand, tpeer, (uint32_t)obs, t, col, pos);
+                    gsel = (a.diag & 16) ? gcand : gossip_targets(a, gcand, tpeer, (uint32_t)obs, t, col, pos);
                 }
                 if (valid && !(a.diag & 2)) a.gsel[i] = gsel ? 1 : 0;
             }
@@ -891,7 +915,7 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.first = h->d_first; a.invalid = h->d_invalid; a.p5 = h->d_p5; a.p6 = h->d_p6;
     a.topic_cap = h->pp.topic_score_cap; a.w5 = h->pp.app_specific_weight; a.w6 = h->pp.ip_colocation_factor_weight;
     a.bp_thr = h->pp.behaviour_penalty_threshold; a.w7 = h->pp.behaviour_penalty_weight;
-    a.diag = (h->diag >> 9) & 7u;    // DIAG_H_NO_GOSSIP / _NO_IHAVE_STORE / _NO_RECOMPUTE
+    a.diag = (h->diag >> 9) & 55u;   // DIAG_H_NO_GOSSIP / _NO_IHAVE_STORE / _NO_RECOMPUTE / _NO_SELECT / _CHEAP_KEYS
     a.lastpub = h->x->d_lastpub; a.fan_topics = h->x->d_fantopics;
     a.pub_thr = h->th.publish_threshold; a.fanout_ttl = h->gp.fanout_ttl_ns;
     return a;

@@ -171,3 +171,41 @@ def test_gossip_rounds_bit_exact(require_gpu, n, k, T, nticks, rate, ignore_frac
     assert (msgs.seen % R == 2).any()
     assert (st.bp > bp0 * 0.5 + 0.5).any()
     eng.close()
+
+
+@pytest.mark.gpu
+def test_iwant_response_queue_overflow_is_reported(require_gpu):
+    """A response queue smaller than the IWANT traffic: the overflow is
+    reported by gsim_msg_stats (GSIM_ERANGE) and nothing past the queue is
+    read or written."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim.engine import Engine, GsimError, random_regular
+    from test_delivery import _schedule
+    rng = np.random.default_rng(77)
+    n, k, T = 1200, 16, 1
+    params = beacon_params(T)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2)
+    th = PeerScoreThresholds(GossipThreshold=-20, PublishThreshold=-50, GraylistThreshold=-300)
+    net = random_regular(n, k, seed=5, n_topics=T)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 8 / k)
+    eng = Engine(params, th, gossip=gp)
+    eng.load_graph(net)
+    eng.set_seed(SEED)
+    st.push_to_engine(eng)
+    eng.msgs_init(256, R, T0, Second, max_arrivals=4)
+    ticks = list(range(1, 6))
+    sched = _schedule(rng, ticks, T, R, 10, 0.0, n)
+    for kk in ticks:
+        now = tick_time(kk)
+        eng.refresh_scores(now)
+        eng.heartbeat(kk, now)
+        for g in range(kk * R, kk * R + R):
+            if g in sched:
+                eng.publish(sched[g], g)
+            eng.round(g)
+    with pytest.raises(GsimError) as ei:
+        eng.msg_stats()
+    assert ei.value.rc == _abi.GSIM_ERANGE
+    assert eng.gossip_stats()["iwant_responses"] > 4
+    eng.close()

@@ -18,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import bench  # noqa: E402
 
-ARMS = {0: "full", 32: "send_no_counters", 128: "send_no_rowstate", 64: "send_plain_claim", 4096: "send_no_bitmap", 32 | 128 | 64: "send_cells_only"}
+ARMS = {0: "full", 8192: "hb_no_select", 16384: "hb_cheap_keys"}
 
 
 def main():
