@@ -93,6 +93,28 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// Minimum over the W-lane group `grp` (W = 32: lanes 0-31 or 32-63).  The
+// row shifts and the row_bcast:15 step read only lanes of the same 32-lane
+// half, so a group may run this while the other half of the wave is inactive.
+template <int W>
+__device__ __forceinline__ uint32_t group_min_u32(uint32_t v, int grp)
+{
+    if constexpr (W == 64) {
+        return wave_min_u32(v);
+    } else {
+        static_assert(W == 32, "groups of 32 or 64 lanes");
+        const int I = -1;
+        v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x111, 0xF, 0xF, false));   // row_shr:1
+        v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x112, 0xF, 0xF, false));   // row_shr:2
+        v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x114, 0xF, 0xF, false));   // row_shr:4
+        v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x118, 0xF, 0xF, false));   // row_shr:8
+        v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x142, 0xA, 0xF, false));   // row_bcast:15
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+        return grp ? hi : lo;
+    }
+}
+
 __device__ __forceinline__ uint64_t hb_key(const HbArgs& a, uint32_t obs, int32_t t, uint32_t purpose, uint32_t col,
                                            uint32_t pos)
 {
@@ -116,10 +138,15 @@ __device__ __forceinline__ uint32_t hb_key_hi(const HbArgs& a, uint32_t obs, int
 // few) are then removed largest-first (added smallest-first) by wave
 // reductions.  Keys below tau precede every key above it whatever the lane, so
 // the result is exactly the `count` smallest (key, lane) pairs.
+//
+// W-lane groups (W = 32: two observers per wave): every ballot is masked to
+// the caller's group `gm`, the lane index keeps breaking ties (the group's
+// lanes are in row order), and a group may run this alone.
+template <int W = 64>
 __device__ bool select_smallest(const HbArgs& a, bool cand, int count, uint32_t obs, int32_t t, uint32_t purpose,
-                                uint32_t col, uint32_t pos)
+                                uint32_t col, uint32_t pos, uint64_t gm = ~0ull, int grp = 0)
 {
-    const uint64_t avail = __ballot(cand);
+    const uint64_t avail = __ballot(cand) & gm;
     const int n = __popcll(avail);
     if (n == 0) return false;
     if (count <= 0 || n <= count) return cand;
@@ -133,18 +160,18 @@ __device__ bool select_smallest(const HbArgs& a, bool cand, int count, uint32_t 
     // loops below adjust (fp32: no 64-bit integer division)
     const uint32_t tau = (uint32_t)((float)count / (float)n * 4294967040.0f);
     bool sel = cand && hi < tau;
-    int c = __popcll(__ballot(sel));
+    int c = __popcll(__ballot(sel) & gm);
     while (c > count) {                 // drop the largest (key, lane) among the selected
-        const uint32_t mx = ~wave_min_u32(sel ? ~hi : 0xFFFFFFFFu);
-        const uint64_t at = __ballot(sel && hi == mx);
+        const uint32_t mx = ~group_min_u32<W>(sel ? ~hi : 0xFFFFFFFFu, grp);
+        const uint64_t at = __ballot(sel && hi == mx) & gm;
         const int win = 63 - __clzll((long long)at);
         if (lane == win) sel = false;
         --c;
     }
     uint32_t rest = (cand && !sel) ? hi : 0xFFFFFFFFu;
-    uint64_t left = __ballot(cand && !sel);
+    uint64_t left = __ballot(cand && !sel) & gm;
     while (c < count) {                 // add the smallest (key, lane) among the others
-        const uint32_t mn = wave_min_u32(rest);
+        const uint32_t mn = group_min_u32<W>(rest, grp);
         const int win = __ffsll((long long)(__ballot(rest == mn) & left)) - 1;
         left &= ~(1ull << win);
         if (lane == win) { sel = true; rest = 0xFFFFFFFFu; }
@@ -270,13 +297,14 @@ __device__ double score_of_record(const HbArgs& a, uint32_t rv, uint32_t col)
 // target = max(Dlazy, int(GossipFactor * |L|)), all of L if that is not
 // smaller, else the target smallest keys.  A lane is selected if any of its
 // instances is.  Must be called by the whole wave.
+template <int W = 64>
 __device__ bool gossip_targets(const HbArgs& a, bool cand, bool tpeer, uint32_t obs, int32_t t, uint32_t col,
-                               uint32_t pos)
+                               uint32_t pos, uint64_t gm = ~0ull, int grp = 0)
 {
-    const int c = __popcll(__ballot(cand));
+    const int c = __popcll(__ballot(cand) & gm);
     bool dup = false;
-    if (c < a.Dlo) dup = select_smallest(a, tpeer, a.Dlo - c, obs, t, P_GOSSIP_FILL, col, pos);
-    const int n = c + __popcll(__ballot(dup));
+    if (c < a.Dlo) dup = select_smallest<W>(a, tpeer, a.Dlo - c, obs, t, P_GOSSIP_FILL, col, pos, gm, grp);
+    const int n = c + __popcll(__ballot(dup) & gm);
     if (n == 0) return false;
     int target = a.dlazy;
     const int factor = (int)(a.gossip_factor * (double)n);
@@ -284,10 +312,10 @@ __device__ bool gossip_targets(const HbArgs& a, bool cand, bool tpeer, uint32_t 
     if (target >= n) return cand || dup;
     // each lane holds up to two instances (candidate, fill duplicate)
     // no fill duplicates (the usual case): one instance per lane
-    if (!__ballot(dup)) return select_smallest(a, cand, target, obs, t, P_GOSSIP, col, pos);
+    if (!(__ballot(dup) & gm)) return select_smallest<W>(a, cand, target, obs, t, P_GOSSIP, col, pos, gm, grp);
     uint32_t h1 = cand ? hb_key_hi(a, obs, t, P_GOSSIP, col, pos) : 0xFFFFFFFFu;
     uint32_t h2 = dup ? hb_key_hi(a, obs, t, P_GOSSIP_DUP, col, pos) : 0xFFFFFFFFu;
-    uint64_t av1 = __ballot(cand), av2 = __ballot(dup);
+    uint64_t av1 = __ballot(cand) & gm, av2 = __ballot(dup) & gm;
     const int lane = threadIdx.x & 63;
     bool sel = false;
     for (int q = 0; q < target; ++q) {
@@ -295,9 +323,9 @@ __device__ bool gossip_targets(const HbArgs& a, bool cand, bool tpeer, uint32_t 
         const bool has1 = (av1 >> lane) & 1ull, has2 = (av2 >> lane) & 1ull;
         const bool use1 = has1 && (!has2 || h1 <= h2);
         const uint32_t mine = use1 ? h1 : (has2 ? h2 : 0xFFFFFFFFu);
-        const uint32_t mn = wave_min_u32(mine);
+        const uint32_t mn = group_min_u32<W>(mine, grp);
         const bool at_min = mine == mn && (has1 || has2);
-        const int win = __ffsll((long long)__ballot(at_min)) - 1;
+        const int win = __ffsll((long long)(__ballot(at_min) & gm)) - 1;
         // which instance the winner used, from a ballot (no lane shuffle)
         if ((__ballot(at_min && use1) >> win) & 1ull) av1 &= ~(1ull << win); else av2 &= ~(1ull << win);
         if (lane == win) sel = true;
@@ -307,15 +335,26 @@ __device__ bool gossip_targets(const HbArgs& a, bool cand, bool tpeer, uint32_t 
 
 }  // namespace
 
-// One wavefront = one observer's heartbeat (gossipsub.go:1345-1557).
+// One W-lane group = one observer's heartbeat (gossipsub.go:1345-1557):
+// W = 64 one observer per wavefront, W = 32 two (rows of at most 32
+// connections; every VALU instruction then serves two observers).  Group
+// lane gl holds the observer's gl-th connection; ballots are masked to the
+// group, shuffles read the group's own lanes, and branches diverge only
+// between whole groups (group_min_u32 is group-local).
+template <int W>
 __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
 {
+    constexpr int G = 64 / W;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int64_t obs = (int64_t)blockIdx.x * 4 + wid; obs < a.N; obs += (int64_t)gridDim.x * 4) {
-        const uint32_t b = a.row_ptr[obs];
-        const int deg = (int)(a.row_ptr[obs + 1] - b);
-        const bool valid = lane < deg;
-        const uint32_t e = b + (uint32_t)lane;
+    const int grp = lane / W, gl = lane % W, base = grp * W;
+    const uint64_t gm = W == 64 ? ~0ull : (((1ull << W) - 1) << base);
+    for (int64_t o0 = ((int64_t)blockIdx.x * 4 + wid) * G; o0 < a.N; o0 += (int64_t)gridDim.x * 4 * G) {
+        const int64_t obs = o0 + grp;
+        const bool ovalid = obs < a.N;
+        const uint32_t b = ovalid ? a.row_ptr[obs] : 0u;
+        const int deg = ovalid ? (int)(a.row_ptr[obs + 1] - b) : 0;
+        const bool valid = gl < deg;
+        const uint32_t e = b + (uint32_t)gl;
         const uint32_t col = valid ? a.col[e] : 0u;
         const uint32_t rv = valid ? a.rev[e] : 0u;           // this observer's record of col
         const uint8_t est = valid ? a.estate[rv] : 0;
@@ -325,13 +364,16 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
         const bool dir = valid && a.direct[e];          // direct peers are never grafted or gossiped to
         const double S = valid ? a.score[rv] : 0.0;
         const uint64_t subj = valid ? a.sub[col] : 0ull;
-        const uint64_t subi = a.sub[obs];
+        const uint64_t subi = ovalid ? a.sub[obs] : 0ull;
         // live score for emitGossip: the snapshot until this heartbeat's
         // Graft/Prune touches one of the lane's records
         double S_live = S;
         bool dirty = false;
-        // newest mcache put per topic (GetGossipIDs non-empty test), one lane per topic
-        const int32_t lp_lane = (a.gossip && lane < a.T) ? a.lastput[(int64_t)lane * a.N + obs] : -1;
+        // newest mcache put per topic (GetGossipIDs non-empty test), one lane
+        // per topic: group lane gl holds topics gl and gl + 32 (W = 32, T > 32)
+        const int32_t lp_lane = (a.gossip && ovalid && gl < a.T) ? a.lastput[(int64_t)gl * a.N + obs] : -1;
+        const int32_t lp_lane2 = (W == 32 && a.gossip && ovalid && gl + 32 < a.T)
+                                     ? a.lastput[(int64_t)(gl + 32) * a.N + obs] : -1;
         if (a.gossip && valid) a.gstate[e] = S >= a.gossip_thr ? 1 : 0;
 
         // clearBackoff every 15 ticks (gossipsub.go:1627-1646)
@@ -378,7 +420,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             const bool tpeer = valid && conn && ((subj >> t) & 1ull);
             bool m = valid && (fl & GSIM_TF_MESH);
             uint8_t ctl = 0;
-            const uint32_t pos = (uint32_t)lane;
+            const uint32_t pos = (uint32_t)gl;
 
             auto prune = [&]() {
                 stats_prune(a, tracked, scored, thr, mcap, sf);
@@ -402,20 +444,20 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             if (m && S < 0) prune();
 
             // too few peers: graft up to D (1412-1427)
-            int l = __popcll(ballot(m));
+            int l = __popcll(ballot(m) & gm);
             if (l < a.Dlo) {
                 need_bo();
                 const bool cand = tpeer && !m && bo == 0 && !dir && S >= 0;
-                if (select_smallest(a, cand, a.D - l, (uint32_t)obs, t, P_GRAFT_DLO, col, pos)) graft();
+                if (select_smallest<W>(a, cand, a.D - l, (uint32_t)obs, t, P_GRAFT_DLO, col, pos, gm, grp)) graft();
             }
 
             // too many peers: keep Dscore best + random, Dout outbound (1429-1490)
-            l = __popcll(ballot(m));
+            l = __popcll(ballot(m) & gm);
             if (l > a.Dhi) {
-                const uint64_t mm = ballot(m);
+                const uint64_t mm = ballot(m) & gm;
                 const uint64_t k1 = m ? hb_key(a, (uint32_t)obs, t, P_PRUNE_SHUF1, col, pos) : ~0ull;
                 int rank1 = 0;
-                for (int q = 0; q < 64; ++q) {
+                for (int q = base; q < base + W; ++q) {
                     const double sq = __shfl(S, q, 64);
                     const uint64_t kq = __shfl(k1, q, 64);
                     if (((mm >> q) & 1ull) && (sq > S || (sq == S && kq < k1))) ++rank1;
@@ -426,7 +468,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
                 // every lane takes part in the shuffles (a shuffle inside a
                 // divergent branch would read inactive lanes)
                 int below = 0;
-                for (int q = 0; q < 64; ++q) {
+                for (int q = base; q < base + W; ++q) {
                     const uint64_t kq = __shfl(k2, q, 64);
                     if (kq < k2) ++below;   // non-tail lanes hold ~0 and never count
                 }
@@ -438,14 +480,14 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
                 //  in order; pass 2 rotates the first j outbound peers beyond D
                 //  to the front, pushing the last j "rest" peers out of plst[:D].
                 const bool inD = m && p < a.D;
-                const int obD = __popcll(ballot(inD && outb));
+                const int obD = __popcll(ballot(inD && outb) & gm);
                 bool keep = inD;
                 if (obD < a.Dout) {
                     const bool rest = inD && !(outb && p >= 1);
                     const bool cb = m && p >= a.D && outb;
-                    const uint64_t restmask = ballot(rest), cbmask = ballot(cb);
+                    const uint64_t restmask = ballot(rest) & gm, cbmask = ballot(cb) & gm;
                     int rb = 0, rr = 0;
-                    for (int q = 0; q < 64; ++q) {
+                    for (int q = base; q < base + W; ++q) {
                         const int pq = __shfl(p, q, 64);
                         if (((cbmask >> q) & 1ull) && pq < p) ++rb;
                         if (((restmask >> q) & 1ull) && pq > p) ++rr;
@@ -458,31 +500,33 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             }
 
             // enough outbound peers? (1492-1518)
-            l = __popcll(ballot(m));
+            l = __popcll(ballot(m) & gm);
             if (l >= a.Dlo) {
-                const int ob = __popcll(ballot(m && outb));
+                const int ob = __popcll(ballot(m && outb) & gm);
                 if (ob < a.Dout) {
                     need_bo();
                     const bool cand = tpeer && !m && bo == 0 && !dir && outb && S >= 0;
-                    if (select_smallest(a, cand, a.Dout - ob, (uint32_t)obs, t, P_GRAFT_DOUT, col, pos)) graft();
+                    if (select_smallest<W>(a, cand, a.Dout - ob, (uint32_t)obs, t, P_GRAFT_DOUT, col, pos, gm, grp))
+                        graft();
                 }
             }
 
             // opportunistic grafting (1520-1552)
-            l = __popcll(ballot(m));
+            l = __popcll(ballot(m) & gm);
             if (a.opp_ticks && a.tick % a.opp_ticks == 0 && l > 1) {
-                const uint64_t mm = ballot(m);
+                const uint64_t mm = ballot(m) & gm;
                 int rank = 0;
-                for (int q = 0; q < 64; ++q) {
+                for (int q = base; q < base + W; ++q) {
                     const double sq = __shfl(S, q, 64);
                     if (((mm >> q) & 1ull) && (sq < S || (sq == S && q < lane))) ++rank;
                 }
-                const uint64_t at = ballot(m && rank == l / 2);
+                const uint64_t at = ballot(m && rank == l / 2) & gm;
                 const double median = __shfl(S, (int)__ffsll((long long)at) - 1, 64);
                 if (median < a.opp_threshold) {
                     need_bo();
                     const bool cand = tpeer && !m && bo == 0 && !dir && S > median;
-                    if (select_smallest(a, cand, a.opp_peers, (uint32_t)obs, t, P_GRAFT_OPP, col, pos)) graft();
+                    if (select_smallest<W>(a, cand, a.opp_peers, (uint32_t)obs, t, P_GRAFT_OPP, col, pos, gm, grp))
+                        graft();
                 }
             }
 
@@ -497,20 +541,17 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             // message of the topic in the last HistoryGossip ticks.  The
             // choice is stored in the sender's row (enqueueGossip); every
             // joined topic's plane is rewritten each heartbeat.
-            // emitGossip(topic, mesh) (gossipsub.go:1554-1556, 1711-1775):
-            // only if GetGossipIDs(topic) is non-empty, i.e. this peer put a
-            // message of the topic in the last HistoryGossip ticks.  The
-            // choice is stored in the sender's row (enqueueGossip); every
-            // joined topic's plane is rewritten each heartbeat.
             if (a.gossip) {
                 bool gsel = false;
-                if (!(a.diag & 1) && __shfl(lp_lane, t, 64) >= (int64_t)a.tick - a.hist_gossip) {
-                    if (__ballot(dirty) && !(a.diag & 4)) {
+                const int32_t lpt = __shfl(t < 32 || W == 64 ? lp_lane : lp_lane2, base + (t & (W - 1)), 64);
+                if (!(a.diag & 1) && lpt >= (int64_t)a.tick - a.hist_gossip) {
+                    if ((__ballot(dirty) & gm) && !(a.diag & 4)) {
                         if (dirty) S_live = score_of_record(a, rv, col);
                         dirty = false;
                     }
                     const bool gcand = tpeer && !m && !dir && S_live >= a.gossip_thr;
-                    gsel = (a.diag & 16) ? gcand : gossip_targets(a, gcand, tpeer, (uint32_t)obs, t, col, pos);
+                    gsel = (a.diag & 16) ? gcand
+                                         : gossip_targets<W>(a, gcand, tpeer, (uint32_t)obs, t, col, pos, gm, grp);
                 }
                 if (valid && !(a.diag & 2)) a.gsel[i] = gsel ? 1 : 0;
             }
@@ -915,7 +956,7 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.first = h->d_first; a.invalid = h->d_invalid; a.p5 = h->d_p5; a.p6 = h->d_p6;
     a.topic_cap = h->pp.topic_score_cap; a.w5 = h->pp.app_specific_weight; a.w6 = h->pp.ip_colocation_factor_weight;
     a.bp_thr = h->pp.behaviour_penalty_threshold; a.w7 = h->pp.behaviour_penalty_weight;
-    a.diag = (h->diag >> 9) & 55u;   // DIAG_H_NO_GOSSIP / _NO_IHAVE_STORE / _NO_RECOMPUTE / _NO_SELECT / _CHEAP_KEYS
+    a.diag = (h->diag >> 9) & 119u;  // DIAG_H_NO_GOSSIP / _NO_IHAVE_STORE / _NO_RECOMPUTE / _NO_SELECT / _CHEAP_KEYS / _WAVE_ROWS
     a.lastpub = h->x->d_lastpub; a.fan_topics = h->x->d_fantopics;
     a.pub_thr = h->th.publish_threshold; a.fanout_ttl = h->gp.fanout_ttl_ns;
     return a;
@@ -968,7 +1009,11 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     // heartbeat output goes to the parity-0 inbox, read by control round 0
     HbArgs a = make_hb_args(h, tick, now, 1);
     ProfScope ps(h, GSIM_K_HEARTBEAT);
-    hipLaunchKernelGGL(k_heartbeat, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a);
+    // two observers per wavefront when every row fits 32 lanes
+    if (h->x->max_degree <= 32 && !(a.diag & 64))
+        hipLaunchKernelGGL(k_heartbeat<32>, dim3(grid_rows((h->n + 1) / 2)), dim3(256), 0, h->stream, a);
+    else
+        hipLaunchKernelGGL(k_heartbeat<64>, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a);
     hipLaunchKernelGGL(k_fanout_heartbeat, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_heartbeat");
 }

@@ -18,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import bench  # noqa: E402
 
-ARMS = {0: "full", 8192: "hb_no_select", 16384: "hb_cheap_keys"}
+ARMS = {0: "full", 32768: "hb_wave_rows", 512: "hb_no_gossip"}
 
 
 def main():
