@@ -46,6 +46,26 @@ CONFIGS = {
     # id: (peers, degree, topics, D, Dlo, Dhi)
     "c3": (1_000_000, 32, 16, 8, 6, 12),
     "c2": (10_000, 32, 1, 8, 6, 12),
+    "c4": (125_000, 32, 1, 8, 6, 12),
+    "c5": (2_000_000, 16, 64, 8, 6, 12),
+}
+# Structure beyond (peers, degree, topics, D) for the BASELINE configurations
+# that are not plain random-regular networks:
+#  c4  Sybil/eclipse: 100k honest + 25k sybils (20 %), one IP per 50 sybils
+#      (P6), sybils ignore IWANT (broken promises -> P7), opportunistic
+#      grafting every 10 heartbeats so the timed window holds it.
+#  c5  Chung-Lu power law (exponent 2.5, mean 16, rows <= 64), 64 topics
+#      with Zipf subscriptions (8 per peer), 1 % of connections going down
+#      per tick and coming back two ticks later, publishers are topic members,
+#      2 msg/s/topic (128 msg/s network-wide; at 4 msg/s/topic the 5000-slot
+#      ring, capped by MaxIHaveLength, is reused while messages still trickle
+#      through gossip on the sparse topic graphs).
+#      2M peers: the dense [T][E] record planes of 10M peers x 64 topics
+#      (~560 GB) do not fit one GPU's 288 GB.
+SCENARIOS = {
+    "c4": {"sybil_frac": 0.2, "per_ip": 50, "opp_ticks": 10},
+    "c5": {"power_law": (2.5, 64), "zipf_per_peer": 8, "churn_frac": 0.01, "ring": 5000,
+           "msg_rate": 2.0},
 }
 
 
@@ -63,17 +83,25 @@ def tick_time(k: int) -> int:
     return 3600 * SECOND + k * SECOND
 
 
-def message_schedule(n: int, T: int, ticks: range, seed: int = 2) -> dict:
+def message_schedule(n: int, T: int, ticks: range, seed: int = 2, sub=None, rate: float = MSG_RATE) -> dict:
     """{round: gsim_msg array}: Poisson(MSG_RATE) messages per topic per
-    heartbeat, each in a uniform round of its tick, origin uniform."""
+    heartbeat, each in a uniform round of its tick, origin uniform (among
+    the topic's members when `sub`, the subscription masks, is given)."""
     from gsim import _abi
     rng = np.random.default_rng(seed)
+    members = None
+    if sub is not None:
+        members = [np.nonzero((sub >> np.uint64(t)) & np.uint64(1))[0] for t in range(T)]
     out, mid = {}, 0
     for k in ticks:
         per_round = [[] for _ in range(ROUNDS)]
         for t in range(T):
-            for _ in range(rng.poisson(MSG_RATE)):
-                per_round[int(rng.integers(0, ROUNDS))].append((mid, t, int(rng.integers(0, n))))
+            for _ in range(rng.poisson(rate)):
+                if members is not None and len(members[t]):
+                    origin = int(members[t][rng.integers(0, len(members[t]))])
+                else:
+                    origin = int(rng.integers(0, n))
+                per_round[int(rng.integers(0, ROUNDS))].append((mid, t, origin))
                 mid += 1
         for r, lst in enumerate(per_round):
             if lst:
@@ -85,25 +113,86 @@ def message_schedule(n: int, T: int, ticks: range, seed: int = 2) -> dict:
     return out
 
 
-def build_engine(cfg, seed, device):
+def build_network(cfg, seed, scen=None):
+    """The synthetic graph of a configuration; returns
+    (network, per-peer behaviour flags or None)."""
+    import gsim
+    from gsim import _abi, graphs
+    n, k, T = cfg[0], cfg[1], cfg[2]
+    scen = scen or {}
+    beh = None
+    if "power_law" in scen:
+        ex, cap = scen["power_law"]
+        net = graphs.power_law(n, k, ex, cap, seed=seed, n_topics=T)
+        net = graphs.with_subscriptions(net, graphs.zipf_subscriptions(n, T, scen["zipf_per_peer"], seed=seed + 100))
+    else:
+        net = gsim.random_regular(n, k, seed=seed, n_topics=T)
+    if "sybil_frac" in scen:
+        ip_ptr, ip_ids, n_ips, syb = graphs.sybil_ips(n, scen["sybil_frac"], scen["per_ip"], seed=seed + 200)
+        net = graphs.with_ips(net, ip_ptr, ip_ids, n_ips)
+        beh = syb.astype(np.uint8) * np.uint8(_abi.BEHAVE_IGNORE_IWANT)
+    return net, beh
+
+
+def build_engine(cfg, seed, device, scen=None):
     import gsim
     from gsim.presets import beacon_params, beacon_thresholds
     n, k, T, D, Dlo, Dhi = cfg
+    scen = scen or {}
     params = beacon_params(T)
     gp = gsim.GossipSubParams(D=D, Dlo=Dlo, Dhi=Dhi)
+    if "opp_ticks" in scen:
+        gp.OpportunisticGraftTicks = scen["opp_ticks"]
     eng = gsim.Engine(params, beacon_thresholds(), gossip=gp, device=device)
-    net = gsim.random_regular(n, k, seed=seed, n_topics=T)
+    net, beh = build_network(cfg, seed, scen)
     eng.load_graph(net)
     eng.set_seed(0x5EED0000 + seed)
     eng.fill_synthetic(seed=seed * 7919 + 1, now=tick_time(0), p_mesh=D / k)
-    eng.msgs_init(MSG_RING, ROUNDS, tick_time(0), SECOND)
+    eng.msgs_init(scen.get("ring", MSG_RING), ROUNDS, tick_time(0), SECOND)
+    if beh is not None:
+        eng.set_peer_behaviour(beh)
     if os.environ.get("GSIM_SEND_VARIANT"):          # A/B of the delivery kernel variants (gsim.h)
         eng.set_kernel_variant(2, int(os.environ["GSIM_SEND_VARIANT"]))
     return eng, net
 
 
-def run_tick(eng, k, sched):
+def describe_graph(cfg, scen) -> str:
+    k = cfg[1]
+    if "power_law" in scen:
+        d = (f"Chung-Lu power law (exponent {scen['power_law'][0]:g}, mean {k}, rows <= {scen['power_law'][1]}), "
+             f"Zipf subscriptions ({scen['zipf_per_peer']} topics/peer)")
+    else:
+        d = f"random-regular k={k}"
+    if "sybil_frac" in scen:
+        d += (f", {scen['sybil_frac']:.0%} sybils ({scen['per_ip']} per IP) ignoring IWANT, "
+              f"opportunistic grafting every {scen['opp_ticks']} heartbeats")
+    if "churn_frac" in scen:
+        d += f", {scen['churn_frac']:.0%} of connections down per tick (back 2 ticks later)"
+    return d
+
+
+def churn_schedule(net, frac: float, ticks: range, seed: int = 4) -> dict:
+    """{tick: [(pairs, up)]}: a random `frac` of the undirected connections
+    goes down before each tick and comes back two ticks later."""
+    rng = np.random.default_rng(seed)
+    src = np.repeat(np.arange(net.n, dtype=np.uint32), np.diff(net.row_ptr.astype(np.int64)))
+    und = np.stack([src, net.col], axis=1)
+    und = und[und[:, 0] < und[:, 1]]
+    out, downs = {}, {}
+    for k in ticks:
+        ev = []
+        if k - 2 in downs:
+            ev.append((downs.pop(k - 2), True))
+        downs[k] = und[rng.choice(len(und), size=max(1, int(len(und) * frac)), replace=False)]
+        ev.append((downs[k], False))
+        out[k] = ev
+    return out
+
+
+def run_tick(eng, k, sched, churn=None):
     now = tick_time(k)
+    for (pairs, up) in (churn or {}).get(k, []):
+        eng.set_connections(pairs, up=up, now=now - SECOND // 2)
     eng.refresh_scores(now)
     eng.heartbeat(k, now)
     for g in range(k * ROUNDS, (k + 1) * ROUNDS):
@@ -113,20 +202,29 @@ def run_tick(eng, k, sched):
         eng.round(g)
 
 
-def cpu_baseline(cfg, budget_s: float = 15.0):
+def cpu_baseline(cfg, budget_s: float = 15.0, scen=None):
     """Time the C oracle (OpenMP over observers in the heartbeat phases) on a
-    bounded sample of the same workload: same degree, topics, parameters and
-    message rate, 50k peers."""
+    bounded sample of the same workload: same graph model, degree, topics,
+    parameters, adversaries, churn and message rate, 50k peers."""
     import oracle_binding as ob
     from fixtures import beacon_params, beacon_thresholds, synthetic_state
+    from tickrun import restrict_to_subscriptions
     import gsim
+    scen = scen or {}
     n, k, T, D, Dlo, Dhi = 50_000, cfg[1], cfg[2], cfg[3], cfg[4], cfg[5]
-    net = gsim.random_regular(n, k, seed=2, n_topics=T)
+    net, beh = build_network((n,) + tuple(cfg[1:]), 2, scen)
     params = beacon_params(T)
-    st = ob.NetState(net, params, thresholds=beacon_thresholds(), gossip=gsim.GossipSubParams(D=D, Dlo=Dlo, Dhi=Dhi))
+    gp = gsim.GossipSubParams(D=D, Dlo=Dlo, Dhi=Dhi)
+    if "opp_ticks" in scen:
+        gp.OpportunisticGraftTicks = scen["opp_ticks"]
+    st = ob.NetState(net, params, thresholds=beacon_thresholds(), gossip=gp)
     synthetic_state(st, np.random.default_rng(3), tick_time(0), D / k)   # gsim_fill_synthetic's distributions
-    msgs = ob.Msgs(n, T, MSG_RING, ROUNDS, tick_time(0), SECOND)
-    sched = message_schedule(n, T, range(1, 201))
+    if "zipf_per_peer" in scen:
+        restrict_to_subscriptions(st, net)
+    msgs = ob.Msgs(n, T, scen.get("ring", MSG_RING), ROUNDS, tick_time(0), SECOND, behaviour=beh)
+    rate = scen.get("msg_rate", MSG_RATE)
+    sched = message_schedule(n, T, range(1, 201), sub=net.sub if "zipf_per_peer" in scen else None, rate=rate)
+    churn = churn_schedule(net, scen["churn_frac"], range(1, 201)) if "churn_frac" in scen else {}
     lib = ob.load()
     v = st.view()
     lib.orc_ip_colocation(v)
@@ -136,6 +234,8 @@ def cpu_baseline(cfg, budget_s: float = 15.0):
     while True:
         kk = steps + 1
         now = tick_time(kk)
+        for (pairs, up) in churn.get(kk, []):
+            st.churn(pairs, up=up, now=now - SECOND // 2)
         lib.orc_refresh_scores(v, now)
         msgs.penalties(st, now)
         lib.orc_compute_scores(v)
@@ -151,7 +251,8 @@ def cpu_baseline(cfg, budget_s: float = 15.0):
     return {"value": n * steps / el, "unit": "peer-heartbeat updates/sec", "cores": threads, "kind": "port",
             "msg_edge_deliveries_per_sec": msgs.stats[0] / el,
             "sample": f"C oracle heartbeat tick (refreshScores+score, mesh maintenance, {ROUNDS} propagation "
-                      f"rounds at {MSG_RATE:g} msg/s/topic) on a {n}-peer k={k} T={T} network, {steps} ticks, "
+                      f"rounds at {rate:g} msg/s/topic) on a {n}-peer {describe_graph(cfg, scen)}, T={T} "
+                      f"network, {steps} ticks, "
                       f"OpenMP {threads} threads in the heartbeat phases, {el:.1f}s"}
 
 
@@ -205,16 +306,20 @@ def main():
         dist.init_process_group("nccl")
 
     cfg = CONFIGS[args.config]
+    scen = SCENARIOS.get(args.config, {})
     n, k, T = cfg[0], cfg[1], cfg[2]
     g_seed, s_seed = replica_seeds(rank)
-    eng, net = build_engine(cfg, seed=g_seed, device=local)
+    eng, net = build_engine(cfg, seed=g_seed, device=local, scen=scen)
     E = net.e
-    sched = message_schedule(n, T, range(1, args.warmup + args.steps + 1), seed=s_seed)
+    ticks = range(1, args.warmup + args.steps + 1)
+    rate = scen.get("msg_rate", MSG_RATE)
+    sched = message_schedule(n, T, ticks, seed=s_seed, sub=net.sub if "zipf_per_peer" in scen else None, rate=rate)
+    churn = churn_schedule(net, scen["churn_frac"], ticks, seed=s_seed + 2) if "churn_frac" in scen else None
 
     kk = 0
     for _ in range(args.warmup):
         kk += 1
-        run_tick(eng, kk, sched)
+        run_tick(eng, kk, sched, churn)
     eng.synchronize()
     census0 = eng.census()
     stats0 = eng.msg_stats()
@@ -233,7 +338,7 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         kk += 1
-        run_tick(eng, kk, sched)
+        run_tick(eng, kk, sched, churn)
     eng.synchronize()
     barrier()
     wall = time.perf_counter() - t0
@@ -246,8 +351,8 @@ def main():
 
     if rank == 0:
         K = args.steps
-        workload = (f"{args.config}: {n} peers, random-regular k={k}, {T} topics, beacon-style params, "
-                    f"{MSG_RATE:g} msg/s/topic, {ROUNDS} rounds/heartbeat")
+        workload = (f"{args.config}: {n} peers, {describe_graph(cfg, scen)}, {T} topics, beacon-style params, "
+                    f"{rate:g} msg/s/topic, {ROUNDS} rounds/heartbeat")
         value = n * world * K / wall
         kms = {c: ms / K for c, (ms, _) in prof.items()}        # per tick
         launches = {c: cnt for c, (_, cnt) in prof.items()}
@@ -287,8 +392,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (seeded random-regular graph, Philox-seeded steady-state counters and meshes, "
-                    "Poisson message publications)",
+            "data": f"synthetic (seeded {'power-law' if 'power_law' in scen else 'random-regular'} graph, "
+                    "Philox-seeded steady-state counters and meshes, Poisson message publications)",
             "config": {"workload": workload, "peers_per_gpu": n, "degree": k, "topics": T,
                        "edge_topic_records": E * T, "rounds_per_heartbeat": ROUNDS,
                        "step": "heartbeat tick: refreshScores+score, mesh maintenance, "
@@ -304,7 +409,7 @@ def main():
             "roofline_kernels": {"refresh_score": roof_refresh, "delivery": roof_deliv},
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(cfg)
+            out["cpu_baseline"] = cpu_baseline(cfg, scen=scen)
         print(json.dumps(out), flush=True)
     eng.close()
     if dist is not None:

@@ -420,9 +420,17 @@ __global__ __launch_bounds__(256) void k_fill_synthetic(ScoreArgs a, uint64_t se
     const double inv = 1.0 / 4294967296.0;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
         const int64_t r = a.rev[e];
+        // topics both endpoints joined: only there can a mesh link or
+        // deliveries exist (owner[e] = observer, owner[r] = neighbour)
+        const uint64_t shared = a.sub ? a.sub[a.owner[e]] & a.sub[a.owner[r]] : ~0ull;
         for (int32_t t = 0; t < a.T; ++t) {
             const int64_t i = (int64_t)t * a.E + e;
             const int64_t ir = (int64_t)t * a.E + r;
+            if (!((shared >> t) & 1ull)) {
+                a.tflags[ir] = 0; a.mflags[i] = 0; a.graft[ir] = 0; a.mtime[ir] = 0;
+                a.first[ir] = 0.0; a.meshd[ir] = 0.0; a.fail[ir] = 0.0; a.invalid[ir] = 0.0;
+                continue;
+            }
             const u32x4 x = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), 0x5eed, 1, k0, k1);
             const u32x4 q = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), 0x5eed, 2, k0, k1);
             const bool in_mesh = x.x * inv < p_mesh;
@@ -609,6 +617,7 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     ScoreArgs a{};
     a.E = h->e;
     a.T = h->t;
+    a.sub = h->d_sub;
     a.tp = h->d_tp;
     a.dtz = h->pp.decay_to_zero;
     a.bp_decay = h->pp.behaviour_penalty_decay;

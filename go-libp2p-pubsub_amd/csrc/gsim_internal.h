@@ -36,6 +36,7 @@ struct ScoreArgs {
     int64_t now;
     int32_t* purged;
     uint32_t diag;   // diagnostic ablations (DIAG_*), 0 in production
+    const uint64_t* sub;       // announced topics per peer (fill: records only where both endpoints joined)
 };
 
 // Diagnostic ablations of the refresh+score wave kernel, for A/B timing only

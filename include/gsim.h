@@ -406,8 +406,9 @@ int gsim_gen_random_regular(int64_t n, int32_t k, uint64_t seed,
                             uint32_t* row_ptr, uint32_t* col_idx, uint8_t* outbound);
 /* Fill every edge-topic record with seeded steady-state-like counters on the
  * device (mesh membership with probability p_mesh, graft times within the
- * last hour of now_ns); every edge tracked+connected.  For benchmarking at
- * sizes where a host upload would dominate. */
+ * last hour of now_ns); every edge tracked+connected.  Records of topics the
+ * two endpoints do not both announce stay empty.  For benchmarking at sizes
+ * where a host upload would dominate. */
 int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now_ns, double p_mesh);
 
 #ifdef __cplusplus
