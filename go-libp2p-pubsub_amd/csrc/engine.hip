@@ -34,6 +34,7 @@ using namespace gsim;
 template <bool REFRESH, bool SCORE>
 __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
 {
+    if (a.gate && *a.gate == 0) return;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
         const uint8_t st = a.estate[e];
@@ -175,6 +176,7 @@ __device__ __forceinline__ void policy_store(T* p, int64_t i, T v, bool changed,
 template <bool REFRESH, bool SCORE, int CHUNK>
 __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
 {
+    if (a.gate && *a.gate == 0) return;
     const int lane = threadIdx.x & 63;
     const int64_t nwaves = (int64_t)gridDim.x * 4;
     const int64_t ntiles = (a.E + 63) / 64;
@@ -354,6 +356,7 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
 // result is the P6 value of record rev[e].  The row scan hits L1/L2.
 __global__ __launch_bounds__(256) void k_ip_colocation(ColocArgs a)
 {
+    if (a.gate && *a.gate == 0) return;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
         const uint32_t r = a.rev[e];
@@ -639,10 +642,11 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     return a;
 }
 
-int launch_ip_colocation(gsim_handle* h)
+int launch_ip_colocation(gsim_handle* h, const int32_t* gate)
 {
     ProfScope ps(h, GSIM_K_IP_COLOCATION);
     ColocArgs c{};
+    c.gate = gate;
     c.E = h->e; c.row_ptr = h->d_row_ptr; c.col = h->d_col; c.rev = h->d_rev; c.owner = h->d_owner;
     c.ip_ptr = h->d_ip_ptr; c.ip_ids = h->d_ip_ids; c.ip_white = h->has_white ? h->d_ip_white : nullptr;
     c.estate = h->d_estate; c.p6 = h->d_p6; c.thr = h->pp.ip_colocation_factor_threshold;
@@ -697,10 +701,19 @@ int launch_refresh_scores(gsim_handle* h, int64_t now)
     if (h->maybe_retained) {
         // a purge inside refresh changes the tracked set, so P6 must be
         // re-derived between decay and scoring (score.go:514 removeIPs).
-        launch_score_kernel<true, false>(h, a);
-        int rc = launch_ip_colocation(h);
+        // The fused pass runs as usual and flags a purge on the device; only
+        // then are P6 and every score recomputed (kernels gated on the flag,
+        // no host round trip): the same results as refresh, P6 and score in
+        // three unconditional passes.
+        hipError_t e = hipMemsetAsync(h->d_flags + 1, 0, sizeof(int32_t), h->stream);
+        if (e != hipSuccess) return hip_check(h, e, "purge flag");
+        a.purged = h->d_flags + 1;
+        launch_score_kernel<true, true>(h, a);
+        int rc = launch_ip_colocation(h, h->d_flags + 1);
         if (rc) return rc;
-        launch_score_kernel<false, true>(h, a);
+        ScoreArgs b = a;
+        b.gate = h->d_flags + 1;
+        launch_score_kernel<false, true>(h, b);
     } else {
         launch_score_kernel<true, true>(h, a);
     }

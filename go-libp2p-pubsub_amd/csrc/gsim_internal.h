@@ -37,6 +37,7 @@ struct ScoreArgs {
     int32_t* purged;
     uint32_t diag;   // diagnostic ablations (DIAG_*), 0 in production
     const uint64_t* sub;       // announced topics per peer (fill: records only where both endpoints joined)
+    const int32_t* gate;       // non-null: run only if *gate != 0 (a retention purge happened)
 };
 
 // Diagnostic ablations of the refresh+score wave kernel, for A/B timing only
@@ -68,6 +69,7 @@ struct ColocArgs {
     const uint8_t* estate;
     double* p6;
     int32_t thr;
+    const int32_t* gate;       // non-null: run only if *gate != 0 (a retention purge happened)
 };
 
 // meshMessageDeliveries increments from message delivery are kept as a
@@ -214,7 +216,7 @@ struct gsim_handle {
 
 int hip_check(gsim_handle* h, hipError_t e, const char* what);
 bool field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r);
-int launch_ip_colocation(gsim_handle* h);
+int launch_ip_colocation(gsim_handle* h, const int32_t* gate = nullptr);
 int launch_refresh_scores(gsim_handle* h, int64_t now);
 int launch_compute_scores(gsim_handle* h);
 int refresh_accept(gsim_handle* h);   // recompute d_dstate if the snapshot changed
