@@ -1261,6 +1261,7 @@ int gsim_write_field(gsim_handle* h, int32_t f, const void* src, size_t bytes)
     if (!rc) rc = materialize_mcnt(h);
     if (rc) return rc;
     rc = write_field_impl(h, r, src);
+    if (!rc) rc = extra_field_written(h, f);
     if (f == GSIM_F_ESTATE) { h->p6_dirty = true; h->maybe_retained = true; h->score_version++; }
     if (f == GSIM_F_SCORE) h->score_version++;
     return rc;

@@ -247,6 +247,7 @@ struct ProfScope {
 int alloc_extra(gsim_handle* h);
 void free_extra(gsim_handle* h);
 bool extra_field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r);
+int extra_field_written(gsim_handle* h, int32_t f);
 
 // implemented in deliver.hip
 void free_deliver(gsim_handle* h);

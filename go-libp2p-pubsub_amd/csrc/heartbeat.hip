@@ -21,6 +21,7 @@ using namespace gsim;
 
 struct Extra {
     uint8_t* d_ctl = nullptr;   // [2][T][E] control inbox by round parity
+    uint64_t* d_cany = nullptr;  // [2][N] per receiver: topics that may hold control (a superset), by parity
     int64_t* d_lastpub = nullptr;      // [N][T] gs.lastpub (ns), 0 = none
     uint64_t* d_fantopics = nullptr;   // [N] bit t: gs.fanout[t] exists
     uint32_t max_degree = 0;
@@ -46,6 +47,8 @@ struct HbArgs {
     int64_t *graft, *mtime;
     uint8_t* ctl_in;    // inbox this phase reads (round parity)
     uint8_t* ctl_out;   // inbox this phase writes
+    uint64_t* cany_in;  // [N] topics with pending control per receiver (ctl_in), cleared when handled
+    uint64_t* cany_out; // [N] ... for ctl_out: a sender sets bit t when it writes receiver's entry
     uint64_t tick;
     int64_t now;
     uint64_t seed;
@@ -559,6 +562,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
                 if (ctl) {
                     const int64_t r = (int64_t)t * a.E + a.rev[e];
                     a.ctl_out[r] = (uint8_t)(a.ctl_out[r] | ctl);
+                    atomicOr(reinterpret_cast<unsigned long long*>(a.cany_out + col), 1ull << t);
                 }
             }
           }
@@ -647,13 +651,19 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
         const int deg = (int)(a.row_ptr[rcv + 1] - b);
         const bool valid = lane < deg;
         const uint32_t e = b + (uint32_t)lane;
+        // topics whose inbox planes may hold entries for this receiver: the
+        // others are not read (most receivers get no GRAFT/PRUNE in a round)
+        const uint64_t any = a.cany_in[rcv];
+        if (!any) continue;
+        if (lane == 0) a.cany_in[rcv] = 0;
         const uint64_t subr = a.sub[rcv];
         for (int32_t t0 = 0; t0 < a.T; t0 += kFlagChunk) {
+          if (!((any >> t0) & ((1ull << kFlagChunk) - 1))) continue;
           uint8_t cc[kFlagChunk];
 #pragma unroll
           for (int j = 0; j < kFlagChunk; ++j) {
               const int32_t t = t0 + j;
-              cc[j] = (t < a.T && valid) ? a.ctl_in[(int64_t)t * a.E + e] : 0;
+              cc[j] = (t < a.T && valid && ((any >> t) & 1ull)) ? a.ctl_in[(int64_t)t * a.E + e] : 0;
           }
           for (int j = 0; j < kFlagChunk; ++j) {
             const int32_t t = t0 + j;
@@ -725,6 +735,7 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                     if (reply) {
                         const int64_t r = (int64_t)t * a.E + a.rev[e];
                         a.ctl_out[r] = (uint8_t)(a.ctl_out[r] | reply);
+                        atomicOr(reinterpret_cast<unsigned long long*>(a.cany_out + a.col[e]), 1ull << t);
                     }
                 }
                 mesh += __shfl(delta, q, 64);
@@ -887,6 +898,11 @@ int alloc_extra(gsim_handle* h)
     h->bytes_allocated += bytes;
     e = hipMemsetAsync(h->x->d_ctl, 0, bytes, h->stream);
     if (e != hipSuccess) return hip_check(h, e, "memset ctl");
+    const size_t any_bytes = 2 * sizeof(uint64_t) * (size_t)h->n;
+    e = hipMalloc((void**)&h->x->d_cany, any_bytes);
+    if (e == hipSuccess) e = hipMemsetAsync(h->x->d_cany, 0, any_bytes, h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "control summary");
+    h->bytes_allocated += any_bytes;
     const size_t lp_bytes = sizeof(int64_t) * (size_t)h->n * (size_t)std::max(1, h->t);
     e = hipMalloc((void**)&h->x->d_lastpub, lp_bytes);
     if (e == hipSuccess) e = hipMalloc((void**)&h->x->d_fantopics, sizeof(uint64_t) * (size_t)h->n);
@@ -909,10 +925,20 @@ void free_extra(gsim_handle* h)
 {
     if (!h->x) return;
     if (h->x->d_ctl) (void)hipFree(h->x->d_ctl);
+    if (h->x->d_cany) (void)hipFree(h->x->d_cany);
     if (h->x->d_lastpub) (void)hipFree(h->x->d_lastpub);
     if (h->x->d_fantopics) (void)hipFree(h->x->d_fantopics);
     delete h->x;
     h->x = nullptr;
+}
+
+// The inbox was written through the ABI: any topic of any receiver may hold
+// entries, so the next control pass reads every plane once.
+int extra_field_written(gsim_handle* h, int32_t f)
+{
+    if (f != GSIM_F_CTL || !h->x || !h->x->d_cany) return GSIM_OK;
+    return hip_check(h, hipMemsetAsync(h->x->d_cany, 0xFF, 2 * sizeof(uint64_t) * (size_t)h->n, h->stream),
+                     "control summary");
 }
 
 bool extra_field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r)
@@ -943,6 +969,8 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     const size_t TE = (size_t)h->e * (size_t)std::max(1, h->t);
     a.ctl_in = h->x->d_ctl + (size_t)(parity_in & 1) * TE;
     a.ctl_out = h->x->d_ctl + (size_t)((parity_in + 1) & 1) * TE;
+    a.cany_in = h->x->d_cany + (size_t)(parity_in & 1) * (size_t)h->n;
+    a.cany_out = h->x->d_cany + (size_t)((parity_in + 1) & 1) * (size_t)h->n;
     a.tick = tick; a.now = now; a.seed = h->x->seed;
     a.D = h->gp.d; a.Dlo = h->gp.dlo; a.Dhi = h->gp.dhi; a.Dscore = h->gp.dscore; a.Dout = h->gp.dout;
     a.opp_peers = h->gp.opportunistic_graft_peers; a.opp_ticks = h->gp.opportunistic_graft_ticks;
