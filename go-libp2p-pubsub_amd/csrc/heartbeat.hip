@@ -26,6 +26,10 @@ struct Extra {
     uint64_t* d_fantopics = nullptr;   // [N] bit t: gs.fanout[t] exists
     uint32_t max_degree = 0;
     uint64_t seed = 0x9E3779B97F4A7C15ull;
+    // observers by row length for the heartbeat's lane groups: [0, n16) rows
+    // of <= 16 connections, then <= 32, then the rest (nullptr: one class)
+    uint32_t* d_rows = nullptr;
+    int64_t n16 = 0, n32 = 0, n64 = 0;
 };
 
 struct HbArgs {
@@ -96,25 +100,35 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-// Minimum over the W-lane group `grp` (W = 32: lanes 0-31 or 32-63).  The
-// row shifts and the row_bcast:15 step read only lanes of the same 32-lane
-// half, so a group may run this while the other half of the wave is inactive.
+// Minimum over the W-lane group `grp` (W = 32: lanes 0-31 or 32-63; W = 16:
+// one 16-lane DPP row).  The row shifts and the row_bcast:15 step read only
+// lanes of the same group, so a group may run this while other groups of the
+// wave are inactive.
 template <int W>
 __device__ __forceinline__ uint32_t group_min_u32(uint32_t v, int grp)
 {
     if constexpr (W == 64) {
         return wave_min_u32(v);
     } else {
-        static_assert(W == 32, "groups of 32 or 64 lanes");
+        static_assert(W == 32 || W == 16, "groups of 16, 32 or 64 lanes");
         const int I = -1;
         v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x111, 0xF, 0xF, false));   // row_shr:1
         v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x112, 0xF, 0xF, false));   // row_shr:2
         v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x114, 0xF, 0xF, false));   // row_shr:4
         v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x118, 0xF, 0xF, false));   // row_shr:8
-        v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x142, 0xA, 0xF, false));   // row_bcast:15
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-        return grp ? hi : lo;
+        if constexpr (W == 32) {
+            v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x142, 0xA, 0xF, false));   // row_bcast:15
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+            return grp ? hi : lo;
+        } else {
+            // lane 15 of each 16-lane row holds the row's minimum
+            const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+            const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+            const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+            const uint32_t r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+            return grp == 0 ? r0 : grp == 1 ? r1 : grp == 2 ? r2 : r3;
+        }
     }
 }
 
@@ -344,16 +358,19 @@ __device__ bool gossip_targets(const HbArgs& a, bool cand, bool tpeer, uint32_t 
 // lane gl holds the observer's gl-th connection; ballots are masked to the
 // group, shuffles read the group's own lanes, and branches diverge only
 // between whole groups (group_min_u32 is group-local).
+//
+// rows: the observers of one row-length class (a list), or nullptr for all N.
 template <int W>
-__global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
+__global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* rows, int64_t nrows)
 {
     constexpr int G = 64 / W;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int grp = lane / W, gl = lane % W, base = grp * W;
     const uint64_t gm = W == 64 ? ~0ull : (((1ull << W) - 1) << base);
-    for (int64_t o0 = ((int64_t)blockIdx.x * 4 + wid) * G; o0 < a.N; o0 += (int64_t)gridDim.x * 4 * G) {
-        const int64_t obs = o0 + grp;
-        const bool ovalid = obs < a.N;
+    const int64_t nobs = rows ? nrows : a.N;
+    for (int64_t o0 = ((int64_t)blockIdx.x * 4 + wid) * G; o0 < nobs; o0 += (int64_t)gridDim.x * 4 * G) {
+        const bool ovalid = o0 + grp < nobs;
+        const int64_t obs = !ovalid ? 0 : rows ? (int64_t)rows[o0 + grp] : o0 + grp;
         const uint32_t b = ovalid ? a.row_ptr[obs] : 0u;
         const int deg = ovalid ? (int)(a.row_ptr[obs + 1] - b) : 0;
         const bool valid = gl < deg;
@@ -372,11 +389,15 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
         // Graft/Prune touches one of the lane's records
         double S_live = S;
         bool dirty = false;
-        // newest mcache put per topic (GetGossipIDs non-empty test), one lane
-        // per topic: group lane gl holds topics gl and gl + 32 (W = 32, T > 32)
-        const int32_t lp_lane = (a.gossip && ovalid && gl < a.T) ? a.lastput[(int64_t)gl * a.N + obs] : -1;
-        const int32_t lp_lane2 = (W == 32 && a.gossip && ovalid && gl + 32 < a.T)
-                                     ? a.lastput[(int64_t)(gl + 32) * a.N + obs] : -1;
+        // newest mcache put per joined topic (GetGossipIDs non-empty test):
+        // group lane gl holds topics gl, gl + W, ... (T <= 64)
+        constexpr int LP = 64 / W;
+        int32_t lpv[LP];
+#pragma unroll
+        for (int k = 0; k < LP; ++k) {
+            const int32_t t = gl + W * k;
+            lpv[k] = (a.gossip && ovalid && t < a.T && ((subi >> t) & 1ull)) ? a.lastput[(int64_t)t * a.N + obs] : -1;
+        }
         if (a.gossip && valid) a.gstate[e] = S >= a.gossip_thr ? 1 : 0;
 
         // clearBackoff every 15 ticks (gossipsub.go:1627-1646)
@@ -390,7 +411,10 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
 
         for (int32_t t0 = 0; t0 < a.T; t0 += kFlagChunk) {
           // the flags of a chunk of topics are loaded together (one memory
-          // round trip per chunk instead of one per topic)
+          // round trip per chunk instead of one per topic); chunks without a
+          // joined topic are skipped (a group-uniform test, like every
+          // per-topic branch below)
+          if (!((subi >> t0) & ((1ull << kFlagChunk) - 1))) continue;
           uint8_t flc[kFlagChunk];
 #pragma unroll
           for (int j = 0; j < kFlagChunk; ++j) {
@@ -546,7 +570,11 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a)
             // joined topic's plane is rewritten each heartbeat.
             if (a.gossip) {
                 bool gsel = false;
-                const int32_t lpt = __shfl(t < 32 || W == 64 ? lp_lane : lp_lane2, base + (t & (W - 1)), 64);
+                int32_t lpsel = lpv[0];
+#pragma unroll
+                for (int k = 1; k < LP; ++k)
+                    if (t >= W * k) lpsel = lpv[k];
+                const int32_t lpt = __shfl(lpsel, base + (t & (W - 1)), 64);
                 if (!(a.diag & 1) && lpt >= (int64_t)a.tick - a.hist_gossip) {
                     if ((__ballot(dirty) & gm) && !(a.diag & 4)) {
                         if (dirty) S_live = score_of_record(a, rv, col);
@@ -915,8 +943,24 @@ int alloc_extra(gsim_handle* h)
     e = hipMemcpy(rp.data(), h->d_row_ptr, sizeof(uint32_t) * rp.size(), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_check(h, e, "row_ptr readback");
     uint32_t md = 0;
-    for (int64_t i = 0; i < h->n; ++i) md = std::max(md, rp[(size_t)i + 1] - rp[(size_t)i]);
+    std::vector<uint32_t> cls[3];
+    for (int64_t i = 0; i < h->n; ++i) {
+        const uint32_t d = rp[(size_t)i + 1] - rp[(size_t)i];
+        md = std::max(md, d);
+        cls[d <= 16 ? 0 : d <= 32 ? 1 : 2].push_back((uint32_t)i);
+    }
     h->x->max_degree = md;
+    h->x->n16 = (int64_t)cls[0].size(); h->x->n32 = (int64_t)cls[1].size(); h->x->n64 = (int64_t)cls[2].size();
+    if (md > 16) {   // more than one class may be present: keep the lists
+        std::vector<uint32_t> all;
+        all.reserve((size_t)h->n);
+        for (auto& c : cls) all.insert(all.end(), c.begin(), c.end());
+        e = hipMalloc((void**)&h->x->d_rows, sizeof(uint32_t) * all.size());
+        if (e == hipSuccess)
+            e = hipMemcpy(h->x->d_rows, all.data(), sizeof(uint32_t) * all.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_check(h, e, "row classes");
+        h->bytes_allocated += sizeof(uint32_t) * all.size();
+    }
     h->max_degree = md;
     return GSIM_OK;
 }
@@ -926,6 +970,7 @@ void free_extra(gsim_handle* h)
     if (!h->x) return;
     if (h->x->d_ctl) (void)hipFree(h->x->d_ctl);
     if (h->x->d_cany) (void)hipFree(h->x->d_cany);
+    if (h->x->d_rows) (void)hipFree(h->x->d_rows);
     if (h->x->d_lastpub) (void)hipFree(h->x->d_lastpub);
     if (h->x->d_fantopics) (void)hipFree(h->x->d_fantopics);
     delete h->x;
@@ -1037,11 +1082,27 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     // heartbeat output goes to the parity-0 inbox, read by control round 0
     HbArgs a = make_hb_args(h, tick, now, 1);
     ProfScope ps(h, GSIM_K_HEARTBEAT);
-    // two observers per wavefront when every row fits 32 lanes
-    if (h->x->max_degree <= 32 && !(a.diag & 64))
-        hipLaunchKernelGGL(k_heartbeat<32>, dim3(grid_rows((h->n + 1) / 2)), dim3(256), 0, h->stream, a);
-    else
-        hipLaunchKernelGGL(k_heartbeat<64>, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a);
+    // observers in lane groups sized to their rows: 4 per wavefront for rows
+    // of <= 16 connections, 2 for <= 32, 1 otherwise (observers are
+    // independent within a heartbeat, so the classes run one after the other)
+    const Extra* x = h->x;
+    if (a.diag & 64) {
+        hipLaunchKernelGGL(k_heartbeat<64>, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a, nullptr, h->n);
+    } else if (x->n16 == h->n) {
+        hipLaunchKernelGGL(k_heartbeat<16>, dim3(grid_rows((h->n + 3) / 4)), dim3(256), 0, h->stream, a, nullptr, h->n);
+    } else if (x->n32 == h->n) {
+        hipLaunchKernelGGL(k_heartbeat<32>, dim3(grid_rows((h->n + 1) / 2)), dim3(256), 0, h->stream, a, nullptr, h->n);
+    } else if (x->n64 == h->n) {
+        hipLaunchKernelGGL(k_heartbeat<64>, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a, nullptr, h->n);
+    } else {
+        const uint32_t* r = x->d_rows;
+        if (x->n16) hipLaunchKernelGGL(k_heartbeat<16>, dim3(grid_rows((x->n16 + 3) / 4)), dim3(256), 0, h->stream,
+                                       a, r, x->n16);
+        if (x->n32) hipLaunchKernelGGL(k_heartbeat<32>, dim3(grid_rows((x->n32 + 1) / 2)), dim3(256), 0, h->stream,
+                                       a, r + x->n16, x->n32);
+        if (x->n64) hipLaunchKernelGGL(k_heartbeat<64>, dim3(grid_rows(x->n64)), dim3(256), 0, h->stream,
+                                       a, r + x->n16 + x->n32, x->n64);
+    }
     hipLaunchKernelGGL(k_fanout_heartbeat, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_heartbeat");
 }
