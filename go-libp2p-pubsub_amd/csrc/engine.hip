@@ -60,10 +60,13 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
             continue;
         }
         const bool decay = REFRESH && conn;   // retained scores are not decayed
+        // topics the observer joined (the others hold zero records: skipping
+        // them leaves every value and the score's sum unchanged)
+        const uint64_t joined = a.skip_unjoined ? a.sub[a.col[e]] : ~0ull;
         double score = 0.0;
         for (int32_t t = 0; t < a.T; ++t) {
             const ctp_t tp = const_tp(a.tp) + t;
-            if (!tp->scored) continue;
+            if (!tp->scored || !((joined >> t) & 1ull)) continue;
             const int64_t i = (int64_t)t * a.E + e;
             double first = a.first[i], meshd = a.meshd[i], fail = a.fail[i], inval = a.invalid[i];
             uint8_t fl = a.tflags[i];
@@ -467,8 +470,9 @@ __global__ __launch_bounds__(256) void k_census(ScoreArgs a, unsigned long long*
         if (!(st & GSIM_ES_TRACKED)) continue;
         c[7] += 1;
         if (!(st & GSIM_ES_CONNECTED)) continue;
+        const uint64_t joined = a.skip_unjoined ? a.sub[a.col[e]] : ~0ull;   // records the score pass reads
         for (int32_t t = 0; t < a.T; ++t) {
-            if (!const_tp(a.tp)[t].scored) continue;
+            if (!const_tp(a.tp)[t].scored || !((joined >> t) & 1ull)) continue;
             const int64_t i = (int64_t)t * a.E + e;
             const uint8_t fl = a.tflags[i];
             c[0] += 1;
@@ -621,6 +625,8 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     a.E = h->e;
     a.T = h->t;
     a.sub = h->d_sub;
+    a.col = h->d_col;
+    a.skip_unjoined = h->unjoined_zero ? 1 : 0;
     a.tp = h->d_tp;
     a.dtz = h->pp.decay_to_zero;
     a.bp_decay = h->pp.behaviour_penalty_decay;
@@ -1065,6 +1071,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     h->p6_dirty = true;
     h->maybe_retained = false;
     h->mcnt_dirty = false;
+    h->unjoined_zero = true;     // all state zero
     int rc2 = alloc_extra(h);
     if (rc2) return rc2;
     he = hipStreamSynchronize(s);
@@ -1169,6 +1176,7 @@ int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now, double p_mes
     h->p6_dirty = true;
     h->score_version++;
     h->maybe_retained = false;
+    h->unjoined_zero = true;     // the fill leaves records of unshared topics zero
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     return hip_check(h, e, "gsim_fill_synthetic");
@@ -1261,6 +1269,7 @@ int gsim_write_field(gsim_handle* h, int32_t f, const void* src, size_t bytes)
     if (!rc) rc = materialize_mcnt(h);
     if (rc) return rc;
     rc = write_field_impl(h, r, src);
+    h->unjoined_zero = false;    // arbitrary state: no record may be skipped
     if (!rc) rc = extra_field_written(h, f);
     if (f == GSIM_F_ESTATE) { h->p6_dirty = true; h->maybe_retained = true; h->score_version++; }
     if (f == GSIM_F_SCORE) h->score_version++;

@@ -38,6 +38,8 @@ struct ScoreArgs {
     uint32_t diag;   // diagnostic ablations (DIAG_*), 0 in production
     const uint64_t* sub;       // announced topics per peer (fill: records only where both endpoints joined)
     const int32_t* gate;       // non-null: run only if *gate != 0 (a retention purge happened)
+    const uint32_t* col;       // col[r]: the observer of record r (record order)
+    int32_t skip_unjoined;     // records of topics the observer did not join are zero: skip them
 };
 
 // Diagnostic ablations of the refresh+score wave kernel, for A/B timing only
@@ -158,6 +160,12 @@ struct gsim_handle {
     bool has_white = false;
     bool p6_dirty = true;
     bool maybe_retained = false;
+    // Every record of a topic its observer did not join is zero (true after
+    // gsim_load_graph and gsim_fill_synthetic, false after any state write
+    // through the ABI).  Subscriptions are fixed and nothing on the path
+    // touches such a record (deliveries, GRAFT/PRUNE and gossip reach joined
+    // topics only), so they stay zero and the score pass may skip them.
+    bool unjoined_zero = false;
     int score_variant = -1;   // refresh+score kernel variant (-1: from env)
     int send_variant = 3;     // delivery kernel variant (gsim_set_kernel_variant(h, 2, v)); 3 = topic-major
     uint32_t diag = 0;        // DIAG_* ablations (A/B diagnostics only)

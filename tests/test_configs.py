@@ -160,3 +160,39 @@ def test_c5_power_law_zipf_topics_churn(require_gpu):
     churn = {2: [(downs[2], False)], 4: [(downs[2], True), (downs[4], False)], 6: [(downs[4], True)]}
     run_parity(net, params, th, gp, st, ticks, sched, ring=1024, churn=churn)
     assert (np.diff(net.row_ptr.astype(np.int64)) > 32).any(), "rows longer than half a wave"
+
+
+@pytest.mark.gpu
+def test_c5_from_device_fill_skips_unjoined_records(require_gpu):
+    """Start from gsim_fill_synthetic (records only where both endpoints
+    joined the topic), the state bench.py's c5 runs from: the score pass then
+    skips every record of a topic its observer did not join.  Ticks with
+    churn, fanout publishers and gossip stay bit-exact against the oracle,
+    which reads every record."""
+    from gsim import graphs
+    from gsim.engine import Engine
+    from fixtures import beacon_params
+    from tickrun import SEED, run_parity, subscribed_schedule
+    rng = np.random.default_rng(606)
+    n, T = 3000, 64
+    net = graphs.power_law(n, 16, 2.5, 64, seed=13, n_topics=T)
+    net = graphs.with_subscriptions(net, graphs.zipf_subscriptions(n, T, 8, seed=14))
+    params = beacon_params(T, RetainScore=3 * Second)
+    th = PeerScoreThresholds(GossipThreshold=-20, PublishThreshold=-40, GraylistThreshold=-300)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2, FanoutTTL=3 * Second)
+    eng = Engine(params, th, gossip=gp)
+    eng.load_graph(net)
+    eng.set_seed(SEED)
+    eng.fill_synthetic(seed=77, now=tick_time(0), p_mesh=0.5)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    st.pull_from_engine(eng)
+    joined = ((net.sub[net.owner()][None, :] >> np.arange(T, dtype=np.uint64)[:, None]) & np.uint64(1)) != 0
+    assert (st.first[~joined] == 0).all() and (st.first[joined] != 0).any()
+    ticks = list(range(1, 6))
+    sched = subscribed_schedule(rng, ticks, net, T, 1.0, 0.02, member_only=False)
+    src = net.owner()
+    und = np.stack([src, net.col], axis=1)
+    und = und[und[:, 0] < und[:, 1]]
+    down = und[rng.choice(len(und), size=len(und) // 50, replace=False)]
+    churn = {2: [(down, False)], 4: [(down, True)]}
+    run_parity(net, params, th, gp, st, ticks, sched, ring=1024, churn=churn, eng=eng)

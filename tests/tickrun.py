@@ -27,16 +27,21 @@ def restrict_to_subscriptions(st, net):
         st.tflags[t, off] = 0
 
 
-def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, churn=None, after_tick=None):
+def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, churn=None, after_tick=None,
+               eng=None):
     """Run `ticks` on a fresh engine loaded with `st`'s state and on the
     oracle; assert identical state, seen-set and totals after every tick.
-    churn: {tick: [(pairs, up), ...]} applied just before the tick."""
+    churn: {tick: [(pairs, up), ...]} applied just before the tick.
+    eng: an engine whose state `st` already mirrors (nothing is pushed)."""
     from gsim.engine import Engine
-    eng = Engine(params, th, gossip=gp)
+    pushed = eng is None
+    if eng is None:
+        eng = Engine(params, th, gossip=gp)
     try:
-        eng.load_graph(net)
-        eng.set_seed(SEED)
-        st.push_to_engine(eng)
+        if pushed:
+            eng.load_graph(net)
+            eng.set_seed(SEED)
+            st.push_to_engine(eng)
         eng.msgs_init(ring, R, T0, Second)
         msgs = ob.Msgs(net.n, st.T, ring, R, T0, Second, behaviour=behaviour)
         if behaviour is not None:
