@@ -626,7 +626,7 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     a.T = h->t;
     a.sub = h->d_sub;
     a.col = h->d_col;
-    a.skip_unjoined = h->unjoined_zero ? 1 : 0;
+    a.skip_unjoined = (h->unjoined_zero && !(h->diag & DIAG_S_NO_SKIP)) ? 1 : 0;
     a.tp = h->d_tp;
     a.dtz = h->pp.decay_to_zero;
     a.bp_decay = h->pp.behaviour_penalty_decay;

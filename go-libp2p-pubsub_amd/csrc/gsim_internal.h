@@ -61,6 +61,7 @@ enum : uint32_t {
     DIAG_D_NO_BITMAP = 4096,        // delivery: read every receiver's cell (no committed-bit shortcut; results unchanged)
     DIAG_H_NO_SELECT = 8192,        // heartbeat: emitGossip takes every candidate (no shuffle/selection)
     DIAG_H_CHEAP_KEYS = 16384,      // heartbeat: selection keys from a multiply hash instead of Philox
+    DIAG_S_NO_SKIP = 65536,         // score pass: read records of unjoined topics too (results unchanged)
     DIAG_H_WAVE_ROWS = 32768,       // heartbeat: one observer per wavefront even when rows fit 32 lanes (results unchanged)
 };
 

@@ -21,7 +21,7 @@ import bench  # noqa: E402
 
 VARIANTS = {0: "thread", 2: "wave4", 3: "wave8"}
 DIAGS = {0: "full", 1: "no_p5_gather", 2: "no_mtime_store", 4: "no_stores", 8: "no_graft_load", 16: "no_p1_div",
-         4 | 8 | 1: "loads_only(no graft,no p5)"}
+         4 | 8 | 1: "loads_only(no graft,no p5)", 65536: "no_unjoined_skip"}
 
 
 def main():
@@ -33,12 +33,13 @@ def main():
     args = ap.parse_args()
     cfg = bench.CONFIGS[args.config]
     eng, net = bench.build_engine(cfg, seed=1, device=0)
+    sched = bench.message_schedule(cfg[0], cfg[2], range(1, 4))
     k = 0
     for _ in range(3):                       # settle the meshes
         k += 1
-        bench.run_tick(eng, k)
+        bench.run_tick(eng, k, sched)
     census = eng.census()
-    arms = [(v, 0) for v in VARIANTS]
+    arms = [(v, 0) for v in VARIANTS] + [(0, 65536)]
     if args.diag:
         arms += [(2, d) for d in DIAGS if d]
     times = {a: [] for a in arms}
