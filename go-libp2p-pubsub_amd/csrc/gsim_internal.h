@@ -167,6 +167,7 @@ struct gsim_handle {
     // touches such a record (deliveries, GRAFT/PRUNE and gossip reach joined
     // topics only), so they stay zero and the score pass may skip them.
     bool unjoined_zero = false;
+    bool all_joined = false;     // every peer announced every topic (nothing to skip)
     int score_variant = -1;   // refresh+score kernel variant (-1: from env)
     int send_variant = 3;     // delivery kernel variant (gsim_set_kernel_variant(h, 2, v)); 3 = topic-major
     uint32_t diag = 0;        // DIAG_* ablations (A/B diagnostics only)
