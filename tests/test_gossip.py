@@ -112,6 +112,7 @@ def test_ignored_iwant_breaks_promise_and_penalises():
     (1200, 16, 2, 8, 8, 0.1, 256),
     (2000, 32, 3, 7, 10, 0.3, 512),
     (800, 24, 40, 7, 1, 0.2, 2048),      # T > 32 with two observers per wavefront (topics gl and gl+32)
+    (1000, 16, 20, 7, 1, 0.2, 1024),     # four observers per wavefront, T > 16 (topics gl and gl+16)
 ])
 def test_gossip_rounds_bit_exact(require_gpu, n, k, T, nticks, rate, ignore_frac, ring):
     """Heartbeats with emitGossip, IHAVE/IWANT in control rounds 0/1, the

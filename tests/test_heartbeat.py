@@ -221,6 +221,8 @@ def assert_same(cpu, gpu):
     (800, 24, 2, 0.3, [59, 60, 61]),         # opportunistic grafting tick
     (600, 16, 2, 0.85, [1, 2, 3]),           # Dhi prune on short rows (16 connections)
     (300, 64, 1, 0.3, [4, 5]),               # full-wave rows (64 connections)
+    (700, 16, 3, 0.45, [59, 60]),            # four observers per wavefront: opportunistic tick, Dhi prune
+    (900, 12, 20, 0.6, [14, 15]),            # 16-lane groups, 20 topics (lastput words of topics gl, gl+16)
 ])
 def test_heartbeat_and_control_bit_exact(require_gpu, n, k, T, p_mesh, ticks):
     rng = np.random.default_rng(n + T)
