@@ -41,6 +41,7 @@
 // touched by the lanes walking j's row, always the same lanes of the same
 // wave; firstMessageDeliveries only by the lane owning receiver i.
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "gsim_internal.h"
@@ -1391,8 +1392,14 @@ int deliver_read_seen(gsim_handle* h, void* dst)
 template <int W>
 static int launch_send_tm(gsim_handle* h, const RoundArgs& a, size_t lds)
 {
+    // blocks per topic: about 2048 blocks in all (8 per CU over the launch at one
+    // resident block per CU: smaller ranges even out the frontier work; measured
+    // 512 / 1024 / 1536 / 2048 / 3072 / 4096 blocks: 30.5 / 22.7 / 21.4 / 20.9 /
+    // 21.1 / 21.3 ms per tick at C3, profiles/r01_ab_send_tm_blocks.log), ranges of
+    // at least 4096 peers; GSIM_TM_BLOCKS overrides the total (A/B only)
+    static const int64_t total = std::getenv("GSIM_TM_BLOCKS") ? std::atoll(std::getenv("GSIM_TM_BLOCKS")) : 2048;
     const int64_t ranges = std::max<int64_t>(1, std::min<int64_t>((h->n + 4095) / 4096,
-                                                                    std::max(1, 1024 / std::max(1, h->t))));
+                                                                    std::max<int64_t>(1, total / std::max(1, h->t))));
     const int32_t range = (int32_t)(((h->n + ranges - 1) / ranges + 63) & ~63ll);
     const int64_t p = (h->n + range - 1) / range;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_send_tm<W>),
