@@ -681,9 +681,12 @@ static void launch_score_kernel(gsim_handle* h, const ScoreArgs& a)
     if (h->score_variant < 0) h->score_variant = score_variant_from_env();
     const int64_t tiles = (h->e + kTileEdges - 1) / kTileEdges;
     switch (h->score_variant) {
-    case 0:
-        hipLaunchKernelGGL((k_refresh_score<REFRESH, SCORE>), dim3(grid_for(h->e)), dim3(256), 0, h->stream, a);
+    case 0: {
+        // GSIM_REFRESH_GRID_CAP: grid-size A/B only
+        static const int cap = std::getenv("GSIM_REFRESH_GRID_CAP") ? std::atoi(std::getenv("GSIM_REFRESH_GRID_CAP")) : 16384;
+        hipLaunchKernelGGL((k_refresh_score<REFRESH, SCORE>), dim3(grid_for(h->e, 256, cap)), dim3(256), 0, h->stream, a);
         return;
+    }
     default: {
         const int grid = (int)std::min<int64_t>(std::max<int64_t>((tiles + 3) / 4, 1), 256 * 32);
         if (h->score_variant == 3)
