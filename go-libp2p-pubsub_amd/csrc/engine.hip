@@ -149,6 +149,165 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
     }
 }
 
+// ---------------------------------------------------------------------------
+// Kernel 1b: k_refresh_score with the topic loop software-pipelined.  gfx950's
+// vmcnt counts stores as well as loads, so in the loop above each topic's
+// loads wait for the previous topic's stores: two or three full memory trips
+// per topic.  Here topic t's counters are in registers while topic t+1's are
+// in flight, and t+1's graftTime (a load that depends on its flags) is issued
+// right after t's stores.  Same operations in the same order per record, so
+// the results are identical.  Variant 1 (GSIM_SCORE_KERNEL=pipe).
+struct TopicRec {
+    double first, meshd, fail, inval;
+    uint8_t fl, pc;
+};
+
+// wave-uniform (scalar parameter loads): the joined mask only predicates the loads
+__device__ __forceinline__ int32_t next_scored_topic(const ScoreArgs& a, int32_t t)
+{
+    for (++t; t < a.T; ++t)
+        if (const_tp(a.tp)[t].scored) break;
+    return t;
+}
+
+__device__ __forceinline__ void load_topic_rec(const ScoreArgs& a, int64_t i, TopicRec& v)
+{
+    v.first = a.first[i]; v.meshd = a.meshd[i]; v.fail = a.fail[i]; v.inval = a.invalid[i];
+    v.fl = a.tflags[i]; v.pc = a.mcnt[i];
+}
+
+template <bool REFRESH, bool SCORE>
+__global__ __launch_bounds__(256) void k_refresh_score_pipe(ScoreArgs a)
+{
+    if (a.gate && *a.gate == 0) return;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
+        const uint8_t st = a.estate[e];
+        if (!(st & GSIM_ES_TRACKED)) {
+            if (SCORE) a.score[e] = 0.0;
+            if (REFRESH && a.pen[e]) a.pen[e] = 0;
+            continue;
+        }
+        const bool conn = (st & GSIM_ES_CONNECTED) != 0;
+        if (REFRESH && !conn && a.now > a.expire[e]) {
+            a.estate[e] = 0;
+            a.bp[e] = 0.0;
+            a.expire[e] = 0;
+            a.pen[e] = 0;
+            for (int32_t t = 0; t < a.T; ++t) {
+                const int64_t i = (int64_t)t * a.E + e;
+                a.first[i] = 0.0; a.meshd[i] = 0.0; a.fail[i] = 0.0; a.invalid[i] = 0.0; a.mcnt[i] = 0;
+                a.graft[i] = 0; a.mtime[i] = 0; a.tflags[i] = 0;
+            }
+            *a.purged = 1;
+            if (SCORE) a.score[e] = 0.0;
+            continue;
+        }
+        const bool decay = REFRESH && conn;
+        // the time field a record in the mesh needs: graftTime when decaying, else meshTime
+        const int64_t* tfield = decay ? a.graft : a.mtime;
+        const bool need_time = decay || SCORE;
+        const uint64_t joined = a.skip_unjoined ? a.sub[a.col[e]] : ~0ull;
+        double score = 0.0;
+        const TopicRec zero = {0.0, 0.0, 0.0, 0.0, 0, 0};
+        int32_t t = next_scored_topic(a, -1);
+        TopicRec cur = zero, nxt = zero;
+        int64_t tcur = 0;
+        if (t < a.T && ((joined >> t) & 1ull)) {
+            load_topic_rec(a, (int64_t)t * a.E + e, cur);
+            if (need_time && (cur.fl & GSIM_TF_IN_MESH)) tcur = tfield[(int64_t)t * a.E + e];
+        }
+        int32_t tn = t < a.T ? next_scored_topic(a, t) : a.T;
+        if (tn < a.T && ((joined >> tn) & 1ull)) load_topic_rec(a, (int64_t)tn * a.E + e, nxt);
+        while (t < a.T) {
+            const bool on = (joined >> t) & 1ull;
+            const ctp_t tp = const_tp(a.tp) + t;
+            const int64_t i = (int64_t)t * a.E + e;
+            double first = cur.first, meshd = cur.meshd, fail = cur.fail, inval = cur.inval;
+            uint8_t fl = cur.fl;
+            int64_t mt = 0;
+            if (on && cur.pc) {
+                meshd = apply_incs(meshd, cur.pc, tp->mesh_message_deliveries_cap);
+                a.meshd[i] = meshd;
+                a.mcnt[i] = 0;
+            }
+            if (decay && on) {
+                double x;
+                x = first * tp->first_message_deliveries_decay;  if (x < a.dtz) x = 0.0;
+                if (x != first) { first = x; a.first[i] = x; }
+                x = meshd * tp->mesh_message_deliveries_decay;   if (x < a.dtz) x = 0.0;
+                if (x != meshd) { meshd = x; a.meshd[i] = x; }
+                x = fail * tp->mesh_failure_penalty_decay;       if (x < a.dtz) x = 0.0;
+                if (x != fail) { fail = x; a.fail[i] = x; }
+                x = inval * tp->invalid_message_deliveries_decay; if (x < a.dtz) x = 0.0;
+                if (x != inval) { inval = x; a.invalid[i] = x; }
+                if (fl & GSIM_TF_IN_MESH) {
+                    mt = a.now - tcur;
+                    a.mtime[i] = mt;
+                    if (mt > tp->mesh_message_deliveries_activation_ns && !(fl & GSIM_TF_ACTIVE)) {
+                        fl |= GSIM_TF_ACTIVE;
+                        a.tflags[i] = fl;
+                    }
+                } else {
+                    a.mtime[i] = 0;
+                }
+            } else if (SCORE && on && (fl & GSIM_TF_IN_MESH)) {
+                mt = tcur;
+            }
+            // stage: topic tn's time field (its flags are in), then topic tn+1's counters
+            const int32_t tnn = tn < a.T ? next_scored_topic(a, tn) : a.T;
+            int64_t tnext = 0;
+            if (tn < a.T && need_time && (nxt.fl & GSIM_TF_IN_MESH)) tnext = tfield[(int64_t)tn * a.E + e];
+            TopicRec nn = zero;
+            if (tnn < a.T && ((joined >> tnn) & 1ull)) load_topic_rec(a, (int64_t)tnn * a.E + e, nn);
+            if (SCORE && on) {
+                double ts = 0.0;
+                if (fl & GSIM_TF_IN_MESH) {                               // P1
+                    double p1 = 0.0;
+                    if (tp->time_in_mesh_quantum_ns != 0) p1 = (double)go_div(mt, tp->time_in_mesh_quantum_ns);
+                    if (p1 > tp->time_in_mesh_cap) p1 = tp->time_in_mesh_cap;
+                    ts += p1 * tp->time_in_mesh_weight;
+                }
+                ts += first * tp->first_message_deliveries_weight;         // P2
+                if (fl & GSIM_TF_ACTIVE) {                                 // P3
+                    if (meshd < tp->mesh_message_deliveries_threshold) {
+                        const double deficit = tp->mesh_message_deliveries_threshold - meshd;
+                        const double p3 = deficit * deficit;
+                        ts += p3 * tp->mesh_message_deliveries_weight;
+                    }
+                }
+                ts += fail * tp->mesh_failure_penalty_weight;              // P3b
+                const double p4 = inval * inval;                           // P4
+                ts += p4 * tp->invalid_message_deliveries_weight;
+                score += ts * tp->topic_weight;
+            }
+            t = tn; tn = tnn; cur = nxt; nxt = nn; tcur = tnext;
+        }
+        double bp = a.bp[e];
+        if (decay) {
+            double x = bp * a.bp_decay;
+            if (x < a.dtz) x = 0.0;
+            if (x != bp) { bp = x; a.bp[e] = x; }
+        }
+        if (REFRESH) {
+            const uint8_t pn = a.pen[e];
+            if (pn) { bp = bp + (double)pn; a.bp[e] = bp; a.pen[e] = 0; }
+        }
+        if (SCORE) {
+            if (a.topic_cap > 0 && score > a.topic_cap) score = a.topic_cap;
+            const double p5 = a.p5[a.owner[e]];
+            score += p5 * a.w5;
+            score += a.p6[e] * a.w6;
+            if (bp > a.bp_thr) {
+                const double excess = bp - a.bp_thr;
+                const double p7 = excess * excess;
+                score += p7 * a.w7;
+            }
+            a.score[e] = score;
+        }
+    }
+}
+
 constexpr int kTileEdges = 64;
 
 // ---------------------------------------------------------------------------
@@ -669,6 +828,7 @@ static int score_variant_from_env()
 {
     const char* s = std::getenv("GSIM_SCORE_KERNEL");
     if (!s) return 0;
+    if (!std::strcmp(s, "pipe")) return 1;
     if (!std::strcmp(s, "wave4")) return 2;
     if (!std::strcmp(s, "wave8")) return 3;
     return 0;
@@ -685,6 +845,11 @@ static void launch_score_kernel(gsim_handle* h, const ScoreArgs& a)
         // GSIM_REFRESH_GRID_CAP: grid-size A/B only
         static const int cap = std::getenv("GSIM_REFRESH_GRID_CAP") ? std::atoi(std::getenv("GSIM_REFRESH_GRID_CAP")) : 16384;
         hipLaunchKernelGGL((k_refresh_score<REFRESH, SCORE>), dim3(grid_for(h->e, 256, cap)), dim3(256), 0, h->stream, a);
+        return;
+    }
+    case 1: {
+        static const int cap = std::getenv("GSIM_REFRESH_GRID_CAP") ? std::atoi(std::getenv("GSIM_REFRESH_GRID_CAP")) : 16384;
+        hipLaunchKernelGGL((k_refresh_score_pipe<REFRESH, SCORE>), dim3(grid_for(h->e, 256, cap)), dim3(256), 0, h->stream, a);
         return;
     }
     default: {
@@ -1205,7 +1370,7 @@ int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant)
         h->send_variant = variant;
         return GSIM_OK;
     }
-    if (which != 0 || variant < 0 || variant > 3 || variant == 1) {
+    if (which != 0 || variant < 0 || variant > 3) {
         h->err = "unknown kernel variant";
         return GSIM_EINVAL;
     }

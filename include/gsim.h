@@ -388,8 +388,9 @@ int gsim_profile(gsim_handle* h, int32_t enable);
 int gsim_profile_read(gsim_handle* h, double* ms, int64_t* launches, int32_t n);
 /* Select an implementation variant of a hot-path kernel for A/B timing in
  * one process (results are identical across variants).  which = 0: the
- * refreshScores+score pass; variant 0 thread-per-edge, 2 wave (4-topic
- * chunks, default), 3 wave (8-topic chunks).  which = 1: diagnostic ablation
+ * refreshScores+score pass; variant 0 thread-per-edge (default), 1 thread-
+ * per-edge with the topic loop software-pipelined, 2 wave (4-topic chunks),
+ * 3 wave (8-topic chunks).  which = 1: diagnostic ablation
  * mask for timing experiments (results are wrong while it is non-zero).
  * which = 2: the delivery kernel; variant 3 (default) is topic-major with the
  * slots' committed bits staged in LDS (used while they fit: N <= ~1.1M peers),

@@ -41,7 +41,7 @@ def build(n, k, T, seed, frac_sybil=0.2, topic_cap=0.0):
     return net, params, st, p5, white
 
 
-@pytest.mark.parametrize("variant", [0, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("n,k,T,cap", [(600, 16, 1, 0.0), (2000, 32, 4, 0.0), (3000, 32, 3, 3.5),
                                        (1000, 20, 11, 0.0)])
 def test_refresh_and_score_bit_exact(require_gpu, n, k, T, cap, variant):

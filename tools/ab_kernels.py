@@ -19,7 +19,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import bench  # noqa: E402
 
-VARIANTS = {0: "thread", 2: "wave4", 3: "wave8"}
+VARIANTS = {0: "thread", 1: "pipe", 2: "wave4", 3: "wave8"}
 DIAGS = {0: "full", 1: "no_p5_gather", 2: "no_mtime_store", 4: "no_stores", 8: "no_graft_load", 16: "no_p1_div",
          4 | 8 | 1: "loads_only(no graft,no p5)", 65536: "no_unjoined_skip"}
 
@@ -39,7 +39,7 @@ def main():
         k += 1
         bench.run_tick(eng, k, sched)
     census = eng.census()
-    arms = [(v, 0) for v in VARIANTS] + [(0, 65536)]
+    arms = [(v, 0) for v in VARIANTS] + [(0, 65536), (1, 65536)]
     if args.diag:
         arms += [(2, d) for d in DIAGS if d]
     times = {a: [] for a in arms}
