@@ -787,6 +787,7 @@ struct ChurnArgs {
     uint8_t *estate, *rstate, *pen;
     int64_t* expire;
     double *first, *invalid;
+    int32_t skip_unjoined;     // records of topics their observer did not join are zero (engine.hip)
 };
 
 // The observer's edge to the other end of each (pair, direction), by binary
@@ -814,12 +815,13 @@ __global__ __launch_bounds__(256) void k_churn_find(const uint32_t* row_ptr, con
 }
 
 // Fresh (or dropped) score record r: an empty peerStats.
-__device__ void churn_reset_record(const HbArgs& a, const ChurnArgs& c, uint32_t r)
+__device__ void churn_reset_record(const HbArgs& a, const ChurnArgs& c, uint32_t r, uint64_t joined)
 {
     a.bp[r] = 0.0;
     c.expire[r] = 0;
     c.pen[r] = 0;
     for (int32_t t = 0; t < a.T; ++t) {
+        if (!((joined >> t) & 1ull)) continue;   // already zero
         const int64_t i = (int64_t)t * a.E + r;
         c.first[i] = 0.0; a.meshd[i] = 0.0; a.fail[i] = 0.0; c.invalid[i] = 0.0;
         a.graft[i] = 0; a.mtime[i] = 0;
@@ -835,31 +837,38 @@ __global__ __launch_bounds__(256) void k_churn_apply(HbArgs a, ChurnArgs c)
     if (q >= c.n2) return;
     const uint32_t e = c.edges[q];
     const uint32_t r = a.rev[e];
+    // the observer's (col[r]) joined topics while unjoined records are known zero:
+    // a store to them would write the value already there.  Random 1-8 B stores
+    // are the churn's bound, so the router planes below are also stored only
+    // where they change.
+    const uint64_t joined = c.skip_unjoined ? a.sub[a.col[r]] : ~0ull;
     if (c.up) {
         // AddPeer: connected; a retained record comes back as it is
         c.rstate[e] = (uint8_t)(c.rstate[e] | GSIM_ES_CONNECTED);
-        if (!(c.estate[r] & GSIM_ES_TRACKED)) churn_reset_record(a, c, r);
+        if (!(c.estate[r] & GSIM_ES_TRACKED)) churn_reset_record(a, c, r, joined);
         c.estate[r] = GSIM_ES_TRACKED | GSIM_ES_CONNECTED;
         return;
     }
     // router RemovePeer: out of every mesh without PRUNE, pending control dropped
     for (int32_t t = 0; t < a.T; ++t) {
         const int64_t i = (int64_t)t * a.E + e;
-        a.mflags[i] = (uint8_t)(a.mflags[i] & ~(GSIM_TF_MESH | GSIM_TF_FANOUT));
-        a.ctl_in[i] = 0;
-        a.ctl_out[i] = 0;
+        const uint8_t mf = a.mflags[i], ci = a.ctl_in[i], co = a.ctl_out[i];
+        const uint8_t nm = (uint8_t)(mf & ~(GSIM_TF_MESH | GSIM_TF_FANOUT));
+        if (nm != mf) a.mflags[i] = nm;
+        if (ci) a.ctl_in[i] = 0;
+        if (co) a.ctl_out[i] = 0;
     }
     c.rstate[e] = (uint8_t)(c.rstate[e] & ~GSIM_ES_CONNECTED);
     // peerScore.RemovePeer: positive scores are dropped, the rest retained
     if (!(c.estate[r] & GSIM_ES_TRACKED)) return;
     if (score_of_record(a, r, a.col[e]) > 0) {
-        churn_reset_record(a, c, r);
+        churn_reset_record(a, c, r, joined);
         c.estate[r] = 0;
         return;
     }
     for (int32_t t = 0; t < a.T; ++t) {
         const ctp_t tp = const_tp(a.tp) + t;
-        if (!tp->scored) continue;
+        if (!tp->scored || !((joined >> t) & 1ull)) continue;
         const int64_t i = (int64_t)t * a.E + r;
         c.first[i] = 0.0;
         const uint8_t fl = a.tflags[i];
@@ -1166,6 +1175,7 @@ int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, i
         c.edges = d_edges; c.n2 = n2; c.up = up ? 1 : 0; c.retain = h->pp.retain_score_ns;
         c.estate = h->d_estate; c.rstate = h->d_rstate; c.pen = h->d_pen; c.expire = h->d_expire;
         c.first = h->d_first; c.invalid = h->d_invalid;
+        c.skip_unjoined = h->unjoined_zero ? 1 : 0;
         hipLaunchKernelGGL(k_churn_apply, dim3(grid), dim3(256), 0, h->stream, a, c);
         e = hipGetLastError();
         if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
