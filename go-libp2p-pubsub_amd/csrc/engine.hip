@@ -514,8 +514,31 @@ __global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
 // Kernel 2: ipColocationFactor (score.go:344-388) as a segmented count over
 // each observer's row keyed by IP id.  Only re-run when the tracked set or the
 // IP assignment changes (AddPeer/RemovePeer/purge), not every heartbeat.
-// Thread per observer edge e (observer owner[e], neighbour col[e]); the
-// result is the P6 value of record rev[e].  The row scan hits L1/L2.
+// Two passes.  k_ip_keys: thread per edge e2, key[e2] = the neighbour's IP id
+// when it is tracked and has exactly one IP (the common case), else a sentinel
+// (untracked / no IP / several IPs).  k_ip_colocation: thread per observer
+// edge e (observer owner[e], neighbour col[e]); for each of the neighbour's
+// IPs it counts the row's tracked members on that IP by scanning the row's
+// keys (contiguous u32, L1/L2 hits) and falls back to the member's IP list only
+// for several-IP members.  The result is the P6 value of record rev[e], the
+// same count in the same order as the reference's per-IP loop.
+constexpr uint32_t kIpUntracked = 0xFFFFFFFFu, kIpMulti = 0xFFFFFFFEu, kIpNone = 0xFFFFFFFDu;
+
+__global__ __launch_bounds__(256) void k_ip_keys(ColocArgs a)
+{
+    if (a.gate && *a.gate == 0) return;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
+        uint32_t k = kIpUntracked;
+        if (a.estate[a.rev[e]] & GSIM_ES_TRACKED) {
+            const uint32_t j = a.col[e];
+            const uint32_t q0 = a.ip_ptr[j], q1 = a.ip_ptr[j + 1];
+            k = q1 == q0 ? kIpNone : q1 - q0 == 1 ? a.ip_ids[q0] : kIpMulti;
+        }
+        a.key[e] = k;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_ip_colocation(ColocArgs a)
 {
     if (a.gate && *a.gate == 0) return;
@@ -523,7 +546,7 @@ __global__ __launch_bounds__(256) void k_ip_colocation(ColocArgs a)
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
         const uint32_t r = a.rev[e];
         double res = 0.0;
-        if (a.estate[r] & GSIM_ES_TRACKED) {
+        if (a.key[e] != kIpUntracked) {
             const uint32_t i = a.owner[e];
             const uint32_t b = a.row_ptr[i], en = a.row_ptr[i + 1];
             const uint32_t j = a.col[e];
@@ -532,7 +555,9 @@ __global__ __launch_bounds__(256) void k_ip_colocation(ColocArgs a)
                 if (a.ip_white && a.ip_white[ip]) continue;
                 int32_t cnt = 0;
                 for (uint32_t e2 = b; e2 < en; ++e2) {
-                    if (!(a.estate[a.rev[e2]] & GSIM_ES_TRACKED)) continue;
+                    const uint32_t k2 = a.key[e2];
+                    if (k2 == ip) { ++cnt; continue; }
+                    if (k2 != kIpMulti) continue;
                     const uint32_t j2 = a.col[e2];
                     for (uint32_t q2 = a.ip_ptr[j2]; q2 < a.ip_ptr[j2 + 1]; ++q2)
                         if (a.ip_ids[q2] == ip) { ++cnt; break; }
@@ -772,7 +797,7 @@ void free_graph(gsim_handle* h)
     dfree(h->d_ip_ptr); dfree(h->d_ip_ids); dfree(h->d_ip_white); dfree(h->d_p5);
     dfree(h->d_first); dfree(h->d_meshd); dfree(h->d_fail); dfree(h->d_invalid);
     dfree(h->d_graft); dfree(h->d_mtime); dfree(h->d_tflags); dfree(h->d_mflags);
-    dfree(h->d_bp); dfree(h->d_estate); dfree(h->d_expire); dfree(h->d_p6); dfree(h->d_score);
+    dfree(h->d_bp); dfree(h->d_estate); dfree(h->d_expire); dfree(h->d_p6); dfree(h->d_ipkey); dfree(h->d_score);
     dfree(h->d_backoff); dfree(h->d_rstate); dfree(h->d_dstate); dfree(h->d_mcnt); dfree(h->d_pen);
     h->bytes_allocated = 0;
     h->n = h->e = 0;
@@ -816,6 +841,12 @@ int launch_ip_colocation(gsim_handle* h, const int32_t* gate)
     c.E = h->e; c.row_ptr = h->d_row_ptr; c.col = h->d_col; c.rev = h->d_rev; c.owner = h->d_owner;
     c.ip_ptr = h->d_ip_ptr; c.ip_ids = h->d_ip_ids; c.ip_white = h->has_white ? h->d_ip_white : nullptr;
     c.estate = h->d_estate; c.p6 = h->d_p6; c.thr = h->pp.ip_colocation_factor_threshold;
+    if (!h->d_ipkey) {
+        const int rc = dalloc(h, &h->d_ipkey, h->e);
+        if (rc) return rc;
+    }
+    c.key = h->d_ipkey;
+    hipLaunchKernelGGL(k_ip_keys, dim3(grid_for(h->e)), dim3(256), 0, h->stream, c);
     hipLaunchKernelGGL(k_ip_colocation, dim3(grid_for(h->e)), dim3(256), 0, h->stream, c);
     h->p6_dirty = false;
     return hip_check(h, hipGetLastError(), "k_ip_colocation");
@@ -1140,6 +1171,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     }
     if (ip_ptr) {
         if (ip_ptr[0] != 0) { h->err = "ip_ptr[0] must be 0"; return GSIM_EINVAL; }
+        if (n_ips > kIpNone) { h->err = "too many IP ids"; return GSIM_EINVAL; }   // ids stay below the P6 key sentinels
         for (int64_t i = 0; i < n; ++i)
             if (ip_ptr[i + 1] < ip_ptr[i]) { h->err = "ip_ptr not monotone"; return GSIM_EINVAL; }
         for (uint32_t q = 0; q < ip_ptr[n]; ++q)

@@ -73,6 +73,7 @@ struct ColocArgs {
     double* p6;
     int32_t thr;
     const int32_t* gate;       // non-null: run only if *gate != 0 (a retention purge happened)
+    uint32_t* key;             // [E] per-edge IP key of the row member (k_ip_keys)
 };
 
 // meshMessageDeliveries increments from message delivery are kept as a
@@ -206,6 +207,7 @@ struct gsim_handle {
     uint8_t* d_estate = nullptr;
     int64_t* d_expire = nullptr;
     double* d_p6 = nullptr;
+    uint32_t* d_ipkey = nullptr;      // [E] P6 scratch: row member's single IP id / sentinel
     double* d_score = nullptr;
     uint8_t* d_pen = nullptr;         // pending broken-promise penalties (applyIwantPenalties), record order
     uint8_t* d_dstate = nullptr;      // delivery state per edge, derived (GSIM_DS_*)

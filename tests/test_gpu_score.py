@@ -29,10 +29,24 @@ def assert_state_equal(st_cpu, st_gpu, fields):
             raise AssertionError(f"{f}: {len(bad)} mismatches, first at {idx}: cpu={a[idx]!r} gpu={b[idx]!r}")
 
 
-def build(n, k, T, seed, frac_sybil=0.2, topic_cap=0.0):
+def multi_ips(n, rng, pool):
+    """0-3 IPs per peer drawn from a small shared pool: peers with no IP, one IP
+    and several IPs (ipColocationFactor counts a peer once per IP it shares)."""
+    cnt = rng.choice([0, 1, 1, 1, 2, 3], size=n)
+    ip_ptr = np.zeros(n + 1, dtype=np.uint32)
+    ip_ptr[1:] = np.cumsum(cnt)
+    ids = [np.sort(rng.choice(pool, size=c, replace=False)) for c in cnt]
+    ip_ids = np.concatenate(ids).astype(np.uint32) if ip_ptr[-1] else np.zeros(0, np.uint32)
+    return ip_ptr, ip_ids, pool
+
+
+def build(n, k, T, seed, frac_sybil=0.2, topic_cap=0.0, multi_ip=False):
     rng = np.random.default_rng(seed)
     net = random_regular(n, k, seed=seed, n_topics=T)
-    net.ip_ptr, net.ip_ids, net.n_ips = sybil_ips(n, frac_sybil, 5, rng)
+    if multi_ip:
+        net.ip_ptr, net.ip_ids, net.n_ips = multi_ips(n, rng, pool=max(8, n // 40))
+    else:
+        net.ip_ptr, net.ip_ids, net.n_ips = sybil_ips(n, frac_sybil, 5, rng)
     params = beacon_params(T, topic_cap=topic_cap)
     p5 = np.where(rng.random(n) < 0.1, -1000.0 * rng.random(n), rng.normal(0, 5, n))
     white = (rng.random(net.n_ips) < 0.1).astype(np.uint8)
@@ -42,10 +56,11 @@ def build(n, k, T, seed, frac_sybil=0.2, topic_cap=0.0):
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3])
-@pytest.mark.parametrize("n,k,T,cap", [(600, 16, 1, 0.0), (2000, 32, 4, 0.0), (3000, 32, 3, 3.5),
-                                       (1000, 20, 11, 0.0)])
-def test_refresh_and_score_bit_exact(require_gpu, n, k, T, cap, variant):
-    net, params, st, p5, white = build(n, k, T, seed=n + T, topic_cap=cap)
+@pytest.mark.parametrize("n,k,T,cap,multi_ip", [(600, 16, 1, 0.0, False), (2000, 32, 4, 0.0, False),
+                                                (3000, 32, 3, 3.5, False), (1000, 20, 11, 0.0, False),
+                                                (1500, 24, 2, 0.0, True)])
+def test_refresh_and_score_bit_exact(require_gpu, n, k, T, cap, multi_ip, variant):
+    net, params, st, p5, white = build(n, k, T, seed=n + T, topic_cap=cap, multi_ip=multi_ip)
     eng = Engine(params, beacon_thresholds())
     eng.set_kernel_variant(0, variant)
     eng.load_graph(net)
