@@ -208,6 +208,8 @@ struct gsim_handle {
     int64_t* d_expire = nullptr;
     double* d_p6 = nullptr;
     uint32_t* d_ipkey = nullptr;      // [E] P6 scratch: row member's single IP id / sentinel
+    uint32_t* d_churn = nullptr;      // gsim_set_connections scratch: [cap] pairs, [cap] edges, [1] bad
+    int64_t churn_cap = 0;
     double* d_score = nullptr;
     uint8_t* d_pen = nullptr;         // pending broken-promise penalties (applyIwantPenalties), record order
     uint8_t* d_dstate = nullptr;      // delivery state per edge, derived (GSIM_DS_*)

@@ -1154,10 +1154,15 @@ int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, i
     if (!rc) rc = materialize_mcnt(h);      // the P3b test reads meshMessageDeliveries
     if (rc) return rc;
     const int32_t n2 = 2 * count;
-    uint32_t *d_pairs = nullptr, *d_edges = nullptr, *d_bad = nullptr;
-    hipError_t e = hipMalloc((void**)&d_pairs, sizeof(uint32_t) * (size_t)n2);
-    if (e == hipSuccess) e = hipMalloc((void**)&d_edges, sizeof(uint32_t) * (size_t)n2);
-    if (e == hipSuccess) e = hipMalloc((void**)&d_bad, sizeof(uint32_t));
+    hipError_t e = hipSuccess;
+    if (h->churn_cap < n2) {   // grow-only scratch: no allocation (and no hipFree sync) per call
+        if (h->d_churn) { (void)hipFree(h->d_churn); h->d_churn = nullptr; h->churn_cap = 0; }
+        e = hipMalloc((void**)&h->d_churn, sizeof(uint32_t) * (2 * (size_t)n2 + 1));
+        if (e == hipSuccess) h->churn_cap = n2;
+    }
+    uint32_t* d_pairs = h->d_churn;
+    uint32_t* d_edges = d_pairs + n2;
+    uint32_t* d_bad = d_edges + n2;
     if (e == hipSuccess) e = hipMemcpyAsync(d_pairs, pairs, sizeof(uint32_t) * (size_t)n2, hipMemcpyHostToDevice, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d_bad, 0xFF, sizeof(uint32_t), h->stream);
     uint32_t bad = 0xFFFFFFFFu;
@@ -1168,7 +1173,7 @@ int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, i
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpyAsync(&bad, d_bad, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);   // a bad pair fails the call before any change
     if (e == hipSuccess && bad == 0xFFFFFFFFu) {
         HbArgs a = make_hb_args(h, 0, now, 0);   // ctl_in/ctl_out cover both inbox planes
         ChurnArgs c{};
@@ -1177,12 +1182,8 @@ int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, i
         c.first = h->d_first; c.invalid = h->d_invalid;
         c.skip_unjoined = h->unjoined_zero ? 1 : 0;
         hipLaunchKernelGGL(k_churn_apply, dim3(grid), dim3(256), 0, h->stream, a, c);
-        e = hipGetLastError();
-        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        e = hipGetLastError();   // stream-ordered: the next call's copy into the scratch follows this kernel
     }
-    (void)hipFree(d_pairs);
-    (void)hipFree(d_edges);
-    (void)hipFree(d_bad);
     if (e != hipSuccess) return hip_check(h, e, "gsim_set_connections");
     if (bad != 0xFFFFFFFFu) {
         h->err = "pair " + std::to_string(bad) + " is not a connection";
