@@ -1153,6 +1153,7 @@ int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, i
     int rc = deliver_flush(h);              // pending first deliveries precede the removal
     if (!rc) rc = materialize_mcnt(h);      // the P3b test reads meshMessageDeliveries
     if (rc) return rc;
+    ProfScope ps(h, GSIM_K_CHURN);
     const int32_t n2 = 2 * count;
     hipError_t e = hipSuccess;
     if (h->churn_cap < n2) {   // grow-only scratch: no allocation (and no hipFree sync) per call

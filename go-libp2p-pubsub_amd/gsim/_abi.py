@@ -103,7 +103,7 @@ MSG_DTYPE = [("id", "<u8"), ("topic", "<u4"), ("origin", "<u4"), ("invalid", "u1
 UNSEEN = 0xFFFFFFFF
 
 KERNEL_CLASSES = ["refresh_score", "score", "ip_colocation", "heartbeat", "control", "publish", "send",
-                  "commit", "accept", "gossip"]
+                  "commit", "accept", "gossip", "churn"]
 BEHAVE_IGNORE_IWANT = 0x01
 
 SIGNATURES = [

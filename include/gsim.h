@@ -379,6 +379,7 @@ typedef enum gsim_kernel_class {
     GSIM_K_COMMIT,             /* seen commit + first-delivery credit */
     GSIM_K_ACCEPT,             /* AcceptFrom verdicts from a new score snapshot */
     GSIM_K_GOSSIP,             /* handleIHave/handleIWant + IWANT response delivery */
+    GSIM_K_CHURN,              /* AddPeer/RemovePeer of gsim_set_connections */
     GSIM_K__COUNT
 } gsim_kernel_class;
 /* Enable (1) or disable (0) recording; clears recorded totals. */
