@@ -975,10 +975,13 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                 const int sl = bs < 0 ? lane : bs;
                 const uint32_t beg = __shfl(rp0, sl, 64), end = __shfl(rp1, sl, 64);
                 const bool ign_s = __shfl(ign_l, sl, 64);
-                const bool v = bs >= 0 && (uint32_t)gl < end - beg;
-                const uint32_t e = beg + (uint32_t)gl;
                 const uint32_t me_id = (uint32_t)(p0 + (bs < 0 ? 0 : bs));
                 n_walk += (gl == 0 && bs >= 0);
+                // rows longer than the group are walked in W-edge chunks (wave-uniform trip count)
+                const uint32_t deg = bs >= 0 ? end - beg : 0u;
+                for (uint32_t off = 0; __ballot(off < deg) != 0; off += W) {
+                const bool v = off + (uint32_t)gl < deg;
+                const uint32_t e = beg + off + (uint32_t)gl;
                 bool req = false, resp = false;
                 uint32_t r = 0;
                 if (push) {
@@ -1016,6 +1019,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                     if (nstage + __popcll(sb) > kRespStage) flush_stage();
                     if (resp) stage[nstage + __popcll(sb & ((1ull << lane) - 1))] = (uint64_t)r | ((uint64_t)m << 32);
                     nstage += __popcll(sb);
+                }
                 }
             }
         }
@@ -1347,7 +1351,10 @@ static int launch_ihave(gsim_handle* h, int64_t g)
     if (e == hipSuccess) e = hipMemsetAsync(d->d_gcount, 0, 2 * (size_t)d->cfg.ring * 4, h->stream);
     if (e != hipSuccess) return hip_check(h, e, "gossip reset");
     hipLaunchKernelGGL(k_gossip_count, dim3(grid), dim3(256), lds_c, h->stream, a, d->d_gcount);
-    if (h->max_degree <= 16)
+    // lane groups sized to the rows: power-law graphs (long rows, short mean) walk
+    // their few long rows in chunks rather than idling 3/4 of a 64-lane group
+    const bool short_mean = h->e <= 24 * (int64_t)h->n;
+    if (h->max_degree <= 16 || (h->max_degree > 32 && short_mean && !std::getenv("GSIM_IHAVE_W64")))
         hipLaunchKernelGGL(k_ihave<16>, dim3(grid), dim3(256), lds, h->stream, a, (const uint32_t*)d->d_gcount);
     else if (h->max_degree <= 32)
         hipLaunchKernelGGL(k_ihave<32>, dim3(grid), dim3(256), lds, h->stream, a, (const uint32_t*)d->d_gcount);
