@@ -112,7 +112,6 @@ struct RoundArgs {
     int32_t* mpub;             // [ring] publication round
     const int64_t* roff;       // [R] (r + 1) * hb / (R + 1): offset of round r in its heartbeat
     int32_t* lastput;
-    uint32_t diag;                 // DIAG_D_* ablations (timing experiments only)
     const uint32_t* nnew_prev;     // bitmask: slots with new claims (or a publication) in round g-1
     uint32_t* nnew_cur;            // bitmask: slots with new claims in round g
     unsigned long long* stats;
@@ -200,7 +199,7 @@ __device__ __forceinline__ void commit_claim(const RoundArgs& a, uint64_t* cellp
     int32_t* lp = a.lastput + (int64_t)t * a.N + peer;
     const int32_t tick = (int32_t)(gc / a.R);
     if (ATOMIC) atomicMax(lp, tick); else if (*lp < tick) *lp = tick;
-    if (!(lo & kCreditFirst) || (a.diag & DIAG_D_NO_COMMIT)) return;
+    if (!(lo & kCreditFirst)) return;
     const ctp_t tp = const_tp(a.tp) + t;
     const int64_t ir = (int64_t)t * a.E + (hi & kEdgeMask);
     const double cap = tp->first_message_deliveries_cap;
@@ -265,10 +264,9 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, int32_t count)
 // Round g.  W = lanes per row (power of two >= the longest row); group q of
 // a wave always walks the senders j0 + q*W .. j0 + q*W + W-1, two at a time
 // (their loads interleaved: two dependent memory trips per pair of rows).
-// B = active slots whose cells are loaded together; WPE = minimum waves per
-// SIMD the register allocation must allow (1 = unconstrained).
-template <int W, int B, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_send(RoundArgs a)
+// B = active slots whose cells are loaded together.
+template <int W, int B>
+__global__ __launch_bounds__(256) void k_send(RoundArgs a)
 {
     extern __shared__ uint16_t s_act[];   // [ring] active slots, then [ring/32] new-claim bits
     __shared__ int s_n;
@@ -337,7 +335,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 int32_t* lp = a.lastput + (int64_t)t * a.N + jl;
                 const int32_t tick = (int32_t)((a.g - 1) / a.R);
                 if (*lp < tick) *lp = tick;              // mcache.Put
-                if (irb[b] < 0 || (a.diag & DIAG_D_NO_COMMIT)) continue;
+                if (irb[b] < 0) continue;
                 double x = fv[b];
 #pragma unroll
                 for (int bb = 0; bb < b; ++bb)
@@ -386,7 +384,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             // that is within the window, a copy to a receiver whose committed
             // bit is set is an in-window duplicate without reading its cell
             const bool win_all = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
-            const bool use_bm = !(a.diag & DIAG_D_NO_BITMAP);
             const int64_t bm_m = (int64_t)m * a.nw;
             uint64_t gm = mask & gmask;
             while (__ballot(gm != 0)) {
@@ -402,16 +399,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 const uint32_t e1 = beg1 + (uint32_t)gl, e2 = beg2 + (uint32_t)gl;
                 const uint32_t j1 = (uint32_t)(j0 + (b1 < 0 ? 0 : b1)), j2 = (uint32_t)(j0 + (b2 < 0 ? 0 : b2));
                 // trip 1: the edge's router and record state
-                const bool rowst = !(a.diag & DIAG_D_NO_ROWSTATE);
                 uint32_t i1 = 0, i2 = 0;
                 uint8_t mf1 = 0, mf2 = 0, ds1 = 0, ds2 = 0, tf1 = 0, tf2 = 0;
                 if (v1) {
                     i1 = a.col[e1]; mf1 = a.mflags[plane + e1];
-                    ds1 = rowst ? a.dstate[e1] : (uint8_t)0xFF; tf1 = rowst ? a.tflags[plane + e1] : GSIM_TF_IN_MESH;
+                    ds1 = a.dstate[e1]; tf1 = a.tflags[plane + e1];
                 }
                 if (v2) {
                     i2 = a.col[e2]; mf2 = a.mflags[plane + e2];
-                    ds2 = rowst ? a.dstate[e2] : (uint8_t)0xFF; tf2 = rowst ? a.tflags[plane + e2] : GSIM_TF_IN_MESH;
+                    ds2 = a.dstate[e2]; tf2 = a.tflags[plane + e2];
                 }
                 bool sel1 = (mf1 & (j1 == origin ? o_want : GSIM_TF_MESH)) != 0;
                 bool sel2 = (mf2 & (j2 == origin ? o_want : GSIM_TF_MESH)) != 0;
@@ -428,16 +424,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 n_gray += (tg1 && !ok1) + (tg2 && !ok2);     // AcceptFrom: graylisted sender
                 n_acc += ok1 + ok2;
                 // trip 2: the receiver's cell and the counter to update
-                const bool cnt = !(a.diag & DIAG_D_NO_COUNTERS);
-                const bool sc1 = ok1 && scored_t && (ds1 & GSIM_DS_TRACKED) && cnt;
-                const bool sc2 = ok2 && scored_t && (ds2 & GSIM_DS_TRACKED) && cnt;
+                const bool sc1 = ok1 && scored_t && (ds1 & GSIM_DS_TRACKED);
+                const bool sc2 = ok2 && scored_t && (ds2 & GSIM_DS_TRACKED);
                 uint64_t c1 = 0, c2 = 0;
                 uint32_t n1 = 0, n2 = 0;
                 double x1 = 0.0, x2 = 0.0;
                 // known: committed in an earlier round, and its first-seen round
                 // is not needed (in-window for sure, or no counter to update)
                 bool k1 = false, k2 = false;
-                if (use_bm) {
+                {
                     if (ok1) k1 = ((a.seenbm[bm_m + (i1 >> 6)] >> (i1 & 63)) & 1ull) &&
                                   (win_all || !sc1 || inv || !(tf1 & GSIM_TF_IN_MESH));
                     if (ok2) k2 = ((a.seenbm[bm_m + (i2 >> 6)] >> (i2 & 63)) & 1ull) &&
@@ -474,14 +469,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                             if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo |= kCreditMesh;
                         }
                         const uint64_t v = ((uint64_t)(claim_hi | e) << 32) | lo;
-                        uint64_t prev;
-                        if (a.diag & DIAG_D_PLAIN_CLAIM) {
-                            prev = c;
-                            a.cell[row_m + i] = v;
-                        } else {
-                            prev = __hip_atomic_fetch_min(a.cell + row_m + i, v, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
-                        }
+                        const uint64_t prev = __hip_atomic_fetch_min(a.cell + row_m + i, v, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT);
                         if (prev == kUnseen64) n_first++;
                     }
                     if (!sc) continue;
@@ -585,7 +574,6 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
     const uint32_t gprev = (uint32_t)(a.g - 1);
     const uint32_t par = (uint32_t)(a.g & 1);
     const uint32_t claim_hi = kClaim | (par << 30);
-    const bool cnt = !(a.diag & DIAG_D_NO_COUNTERS);
     unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
     for (int k = 0; k < ns; ++k) {
         const uint32_t m = s_slots[k];
@@ -676,7 +664,7 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
                     n_gray += tg && !ok;                         // AcceptFrom: graylisted sender
                     n_acc += ok;
                     if (!ok) continue;
-                    const bool sc = scored_t && (ds & GSIM_DS_TRACKED) && cnt;
+                    const bool sc = scored_t && (ds & GSIM_DS_TRACKED);
                     const bool known = ((s_bm[i >> 6] >> (i & 63)) & 1ull) &&
                                        (win_all || !sc || inv || !(tf & GSIM_TF_IN_MESH));
                     const uint64_t c = known ? 0ull : a.cell[row_m + i];
@@ -1259,7 +1247,6 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
     a.nnew_cur = d->d_nnew + (size_t)(g & 1) * w;
     a.stats = d->d_stats;
-    a.diag = h->diag;
     a.slot_last = d->d_slot_last;
     a.err = d->d_nresp;
     a.reuse_guard = (std::max(h->gp.history_gossip, h->gp.history_length) + d->prom_ticks + 2) * d->cfg.rounds;
@@ -1353,10 +1340,14 @@ static int launch_ihave(gsim_handle* h, int64_t g)
     hipLaunchKernelGGL(k_gossip_count, dim3(grid), dim3(256), lds_c, h->stream, a, d->d_gcount);
     // lane groups sized to the rows: power-law graphs (long rows, short mean) walk
     // their few long rows in chunks rather than idling 3/4 of a 64-lane group
-    const bool short_mean = h->e <= 24 * (int64_t)h->n;
-    if (h->max_degree <= 16 || (h->max_degree > 32 && short_mean && !std::getenv("GSIM_IHAVE_W64")))
+    int w = h->ihave_w;
+    if (w == 0) {
+        const bool short_mean = h->e <= 24 * (int64_t)h->n;
+        w = (h->max_degree <= 16 || (h->max_degree > 32 && short_mean)) ? 16 : h->max_degree <= 32 ? 32 : 64;
+    }
+    if (w == 16)
         hipLaunchKernelGGL(k_ihave<16>, dim3(grid), dim3(256), lds, h->stream, a, (const uint32_t*)d->d_gcount);
-    else if (h->max_degree <= 32)
+    else if (w == 32)
         hipLaunchKernelGGL(k_ihave<32>, dim3(grid), dim3(256), lds, h->stream, a, (const uint32_t*)d->d_gcount);
     else
         hipLaunchKernelGGL(k_ihave<64>, dim3(grid), dim3(256), lds, h->stream, a, (const uint32_t*)d->d_gcount);
@@ -1377,6 +1368,26 @@ int deliver_flush(gsim_handle* h)
                        h->stream, a);
     d->pending = -1;
     return hip_check(h, hipGetLastError(), "k_commit");
+}
+
+// The previous tick's IWANT response queue overflow and early slot reuse,
+// checked at the heartbeat (one small synchronous read per tick) so a caller
+// that never asks for gsim_msg_stats still stops before running on with
+// state that has diverged.
+int deliver_check_errors(gsim_handle* h)
+{
+    Deliver* d = h->dl;
+    if (!d) return GSIM_OK;
+    uint32_t err[4] = {0, 0, 0, 0};
+    hipError_t e = hipMemcpyAsync(err, d->d_nresp, sizeof(err), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "delivery error flags");
+    if (err[1]) { h->err = "IWANT responses overflowed their queue (raise gsim_msg_config.max_arrivals)"; return GSIM_ERANGE; }
+    if (err[2]) {
+        h->err = "a ring slot was republished while its message could still be gossiped or promised (raise ring)";
+        return GSIM_ESTATE;
+    }
+    return GSIM_OK;
 }
 
 int deliver_read_seen(gsim_handle* h, void* dst)
@@ -1403,8 +1414,8 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a, size_t lds)
     // resident block per CU: smaller ranges even out the frontier work; measured
     // 512 / 1024 / 1536 / 2048 / 3072 / 4096 blocks: 30.5 / 22.7 / 21.4 / 20.9 /
     // 21.1 / 21.3 ms per tick at C3, profiles/r01_ab_send_tm_blocks.log), ranges of
-    // at least 4096 peers; GSIM_TM_BLOCKS overrides the total (A/B only)
-    static const int64_t total = std::getenv("GSIM_TM_BLOCKS") ? std::atoll(std::getenv("GSIM_TM_BLOCKS")) : 2048;
+    // at least 4096 peers
+    constexpr int64_t total = 2048;
     const int64_t ranges = std::max<int64_t>(1, std::min<int64_t>((h->n + 4095) / 4096,
                                                                     std::max<int64_t>(1, total / std::max(1, h->t))));
     const int32_t range = (int32_t)(((h->n + ranges - 1) / ranges + 63) & ~63ll);
@@ -1427,11 +1438,7 @@ constexpr size_t kLdsBudget = 160 * 1024 - 24 * 1024;   // minus the static fron
 template <int W>
 static void launch_send(gsim_handle* h, int grid, size_t lds, const RoundArgs& a)
 {
-    switch (h->send_variant) {
-    case 1: hipLaunchKernelGGL((k_send<W, 4, 7>), dim3(grid), dim3(256), lds, h->stream, a); return;
-    case 2: hipLaunchKernelGGL((k_send<W, 4, 1>), dim3(grid), dim3(256), lds, h->stream, a); return;
-    default: hipLaunchKernelGGL((k_send<W, 8, 1>), dim3(grid), dim3(256), lds, h->stream, a); return;
-    }
+    hipLaunchKernelGGL((k_send<W, kSlotBatch>), dim3(grid), dim3(256), lds, h->stream, a);
 }
 
 extern "C" {

@@ -150,367 +150,6 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
 }
 
 // ---------------------------------------------------------------------------
-// Kernel 1b: k_refresh_score with the topic loop software-pipelined.  gfx950's
-// vmcnt counts stores as well as loads, so in the loop above each topic's
-// loads wait for the previous topic's stores: two or three full memory trips
-// per topic.  Here topic t's counters are in registers while topic t+1's are
-// in flight, and t+1's graftTime (a load that depends on its flags) is issued
-// right after t's stores.  Same operations in the same order per record, so
-// the results are identical.  Variant 1 (GSIM_SCORE_KERNEL=pipe).
-struct TopicRec {
-    double first, meshd, fail, inval;
-    uint8_t fl, pc;
-};
-
-// wave-uniform (scalar parameter loads): the joined mask only predicates the loads
-__device__ __forceinline__ int32_t next_scored_topic(const ScoreArgs& a, int32_t t)
-{
-    for (++t; t < a.T; ++t)
-        if (const_tp(a.tp)[t].scored) break;
-    return t;
-}
-
-__device__ __forceinline__ void load_topic_rec(const ScoreArgs& a, int64_t i, TopicRec& v)
-{
-    v.first = a.first[i]; v.meshd = a.meshd[i]; v.fail = a.fail[i]; v.inval = a.invalid[i];
-    v.fl = a.tflags[i]; v.pc = a.mcnt[i];
-}
-
-template <bool REFRESH, bool SCORE>
-__global__ __launch_bounds__(256) void k_refresh_score_pipe(ScoreArgs a)
-{
-    if (a.gate && *a.gate == 0) return;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
-        const uint8_t st = a.estate[e];
-        if (!(st & GSIM_ES_TRACKED)) {
-            if (SCORE) a.score[e] = 0.0;
-            if (REFRESH && a.pen[e]) a.pen[e] = 0;
-            continue;
-        }
-        const bool conn = (st & GSIM_ES_CONNECTED) != 0;
-        if (REFRESH && !conn && a.now > a.expire[e]) {
-            a.estate[e] = 0;
-            a.bp[e] = 0.0;
-            a.expire[e] = 0;
-            a.pen[e] = 0;
-            for (int32_t t = 0; t < a.T; ++t) {
-                const int64_t i = (int64_t)t * a.E + e;
-                a.first[i] = 0.0; a.meshd[i] = 0.0; a.fail[i] = 0.0; a.invalid[i] = 0.0; a.mcnt[i] = 0;
-                a.graft[i] = 0; a.mtime[i] = 0; a.tflags[i] = 0;
-            }
-            *a.purged = 1;
-            if (SCORE) a.score[e] = 0.0;
-            continue;
-        }
-        const bool decay = REFRESH && conn;
-        // the time field a record in the mesh needs: graftTime when decaying, else meshTime
-        const int64_t* tfield = decay ? a.graft : a.mtime;
-        const bool need_time = decay || SCORE;
-        const uint64_t joined = a.skip_unjoined ? a.sub[a.col[e]] : ~0ull;
-        double score = 0.0;
-        const TopicRec zero = {0.0, 0.0, 0.0, 0.0, 0, 0};
-        int32_t t = next_scored_topic(a, -1);
-        TopicRec cur = zero, nxt = zero;
-        int64_t tcur = 0;
-        if (t < a.T && ((joined >> t) & 1ull)) {
-            load_topic_rec(a, (int64_t)t * a.E + e, cur);
-            if (need_time && (cur.fl & GSIM_TF_IN_MESH)) tcur = tfield[(int64_t)t * a.E + e];
-        }
-        int32_t tn = t < a.T ? next_scored_topic(a, t) : a.T;
-        if (tn < a.T && ((joined >> tn) & 1ull)) load_topic_rec(a, (int64_t)tn * a.E + e, nxt);
-        while (t < a.T) {
-            const bool on = (joined >> t) & 1ull;
-            const ctp_t tp = const_tp(a.tp) + t;
-            const int64_t i = (int64_t)t * a.E + e;
-            double first = cur.first, meshd = cur.meshd, fail = cur.fail, inval = cur.inval;
-            uint8_t fl = cur.fl;
-            int64_t mt = 0;
-            if (on && cur.pc) {
-                meshd = apply_incs(meshd, cur.pc, tp->mesh_message_deliveries_cap);
-                a.meshd[i] = meshd;
-                a.mcnt[i] = 0;
-            }
-            if (decay && on) {
-                double x;
-                x = first * tp->first_message_deliveries_decay;  if (x < a.dtz) x = 0.0;
-                if (x != first) { first = x; a.first[i] = x; }
-                x = meshd * tp->mesh_message_deliveries_decay;   if (x < a.dtz) x = 0.0;
-                if (x != meshd) { meshd = x; a.meshd[i] = x; }
-                x = fail * tp->mesh_failure_penalty_decay;       if (x < a.dtz) x = 0.0;
-                if (x != fail) { fail = x; a.fail[i] = x; }
-                x = inval * tp->invalid_message_deliveries_decay; if (x < a.dtz) x = 0.0;
-                if (x != inval) { inval = x; a.invalid[i] = x; }
-                if (fl & GSIM_TF_IN_MESH) {
-                    mt = a.now - tcur;
-                    a.mtime[i] = mt;
-                    if (mt > tp->mesh_message_deliveries_activation_ns && !(fl & GSIM_TF_ACTIVE)) {
-                        fl |= GSIM_TF_ACTIVE;
-                        a.tflags[i] = fl;
-                    }
-                } else {
-                    a.mtime[i] = 0;
-                }
-            } else if (SCORE && on && (fl & GSIM_TF_IN_MESH)) {
-                mt = tcur;
-            }
-            // stage: topic tn's time field (its flags are in), then topic tn+1's counters
-            const int32_t tnn = tn < a.T ? next_scored_topic(a, tn) : a.T;
-            int64_t tnext = 0;
-            if (tn < a.T && need_time && (nxt.fl & GSIM_TF_IN_MESH)) tnext = tfield[(int64_t)tn * a.E + e];
-            TopicRec nn = zero;
-            if (tnn < a.T && ((joined >> tnn) & 1ull)) load_topic_rec(a, (int64_t)tnn * a.E + e, nn);
-            if (SCORE && on) {
-                double ts = 0.0;
-                if (fl & GSIM_TF_IN_MESH) {                               // P1
-                    double p1 = 0.0;
-                    if (tp->time_in_mesh_quantum_ns != 0) p1 = (double)go_div(mt, tp->time_in_mesh_quantum_ns);
-                    if (p1 > tp->time_in_mesh_cap) p1 = tp->time_in_mesh_cap;
-                    ts += p1 * tp->time_in_mesh_weight;
-                }
-                ts += first * tp->first_message_deliveries_weight;         // P2
-                if (fl & GSIM_TF_ACTIVE) {                                 // P3
-                    if (meshd < tp->mesh_message_deliveries_threshold) {
-                        const double deficit = tp->mesh_message_deliveries_threshold - meshd;
-                        const double p3 = deficit * deficit;
-                        ts += p3 * tp->mesh_message_deliveries_weight;
-                    }
-                }
-                ts += fail * tp->mesh_failure_penalty_weight;              // P3b
-                const double p4 = inval * inval;                           // P4
-                ts += p4 * tp->invalid_message_deliveries_weight;
-                score += ts * tp->topic_weight;
-            }
-            t = tn; tn = tnn; cur = nxt; nxt = nn; tcur = tnext;
-        }
-        double bp = a.bp[e];
-        if (decay) {
-            double x = bp * a.bp_decay;
-            if (x < a.dtz) x = 0.0;
-            if (x != bp) { bp = x; a.bp[e] = x; }
-        }
-        if (REFRESH) {
-            const uint8_t pn = a.pen[e];
-            if (pn) { bp = bp + (double)pn; a.bp[e] = bp; a.pen[e] = 0; }
-        }
-        if (SCORE) {
-            if (a.topic_cap > 0 && score > a.topic_cap) score = a.topic_cap;
-            const double p5 = a.p5[a.owner[e]];
-            score += p5 * a.w5;
-            score += a.p6[e] * a.w6;
-            if (bp > a.bp_thr) {
-                const double excess = bp - a.bp_thr;
-                const double p7 = excess * excess;
-                score += p7 * a.w7;
-            }
-            a.score[e] = score;
-        }
-    }
-}
-
-constexpr int kTileEdges = 64;
-
-// ---------------------------------------------------------------------------
-// Kernel 1c: wave-independent variant.  Each wavefront owns 64 consecutive
-// edges and walks the topics in ascending order in chunks of CHUNK, issuing
-// all loads of a chunk before using any, and accumulates the score in
-// registers in the reference's order (no LDS, no block barriers).  The
-// per-edge inputs of the P5-P7 tail (bp, P6, col -> P5 gather) are issued at
-// the start of the tile so they overlap the first chunk.
-// Store policy for the [T][E] planes.  A wave-instruction store with only a few
-// active lanes writes scattered 8-B pieces and the memory side pays for whole
-// sectors (measured: sparse meshTime/counter stores cost more than rewriting
-// the full lines).  So a field is rewritten densely (every lane that holds the
-// exact stored value writes it back) when more than kDenseLanes lanes of the
-// wave changed it, and sparsely otherwise.  Either way the resulting memory
-// contents are identical.
-constexpr int kDenseLanes = 8;
-
-template <typename T>
-__device__ __forceinline__ void policy_store(T* p, int64_t i, T v, bool changed, bool can_rewrite)
-{
-    const uint64_t m = __ballot(changed);
-    if (!m) return;
-    const bool dense = __popcll(m) > kDenseLanes;
-    if (changed || (dense && can_rewrite)) p[i] = v;
-}
-
-template <bool REFRESH, bool SCORE, int CHUNK>
-__global__ __launch_bounds__(256) void k_refresh_score_wave(ScoreArgs a)
-{
-    if (a.gate && *a.gate == 0) return;
-    const int lane = threadIdx.x & 63;
-    const int64_t nwaves = (int64_t)gridDim.x * 4;
-    const int64_t ntiles = (a.E + 63) / 64;
-    const ctp_t tpa = const_tp(a.tp);
-    const bool st_ok = !(a.diag & DIAG_NO_STORES);
-    for (int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); tile < ntiles; tile += nwaves) {
-        const int64_t e = tile * 64 + lane;
-        const bool valid = e < a.E;
-        // per-edge inputs are loaded unconditionally (not behind estate) so
-        // they share one memory round trip with the first topic chunk
-        uint8_t st = 0, pn = 0;
-        int64_t expire = 0;
-        double bp = 0.0, p6 = 0.0, p5 = 0.0;
-        uint32_t c = 0;
-        if (valid) {
-            st = a.estate[e];
-            expire = a.expire[e];
-            bp = a.bp[e];
-            if (REFRESH) pn = a.pen[e];
-            if (SCORE) {
-                p6 = a.p6[e];
-                c = a.owner[e];   // the neighbour this record is about
-            }
-        }
-        if (SCORE && valid && !(a.diag & DIAG_NO_P5)) p5 = a.p5[c];
-        const bool tracked = st & GSIM_ES_TRACKED;
-        const bool conn = st & GSIM_ES_CONNECTED;
-        const bool purge = REFRESH && tracked && !conn && a.now > expire;
-        const bool decay = REFRESH && tracked && conn;
-        const bool live = valid && tracked && !purge;
-        double score = 0.0;
-        for (int t0 = 0; t0 < a.T; t0 += CHUNK) {
-            double f[CHUNK], md[CHUNK], fa[CHUNK], iv[CHUNK];
-            int64_t g[CHUNK];
-            uint8_t fl[CHUNK], mc[CHUNK];
-#pragma unroll
-            for (int j = 0; j < CHUNK; ++j) {
-                const int t = t0 + j;
-                f[j] = md[j] = fa[j] = iv[j] = 0.0;
-                g[j] = 0;
-                fl[j] = 0;
-                mc[j] = 0;
-                if (t < a.T && valid && tpa[t].scored) {
-                    const int64_t i = (int64_t)t * a.E + e;
-                    f[j] = a.first[i];
-                    md[j] = a.meshd[i];
-                    fa[j] = a.fail[i];
-                    iv[j] = a.invalid[i];
-                    fl[j] = a.tflags[i];
-                    mc[j] = a.mcnt[i];
-                    if (!(a.diag & DIAG_NO_GRAFT)) g[j] = decay ? a.graft[i] : (SCORE ? a.mtime[i] : 0);
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < CHUNK; ++j) {
-                const int t = t0 + j;
-                if (t >= a.T) break;                         // wave-uniform
-                const ctp_t tp = tpa + t;
-                if (!tp->scored) continue;                   // wave-uniform
-                const int64_t i = (int64_t)t * a.E + (valid ? e : 0);
-                double first = f[j], meshd = md[j], fail = fa[j], inval = iv[j];
-                uint8_t fj = fl[j];
-                int64_t mt = g[j];
-                bool cf = false, cm = false, cfa = false, ci = false, cfl = false, wmt = false;
-                const bool cmc = mc[j] != 0 || purge;
-                int64_t mt_store = 0;
-                if (mc[j] && !purge) {   // deliveries since the last pass precede this decay
-                    meshd = apply_incs(meshd, mc[j], tp->mesh_message_deliveries_cap);
-                    cm = true;
-                }
-                if (purge) {                                 // score.go:512-516
-                    first = meshd = fail = inval = 0.0;
-                    fj = 0;
-                    cf = cm = cfa = ci = cfl = wmt = true;
-                } else if (decay) {
-                    double x;
-                    x = first * tp->first_message_deliveries_decay;  if (x < a.dtz) x = 0.0;
-                    if (x != first) { first = x; cf = true; }
-                    x = meshd * tp->mesh_message_deliveries_decay;   if (x < a.dtz) x = 0.0;
-                    if (x != meshd) { meshd = x; cm = true; }
-                    x = fail * tp->mesh_failure_penalty_decay;       if (x < a.dtz) x = 0.0;
-                    if (x != fail) { fail = x; cfa = true; }
-                    x = inval * tp->invalid_message_deliveries_decay; if (x < a.dtz) x = 0.0;
-                    if (x != inval) { inval = x; ci = true; }
-                    // meshTime is refreshed for in-mesh records (score.go:551-556);
-                    // for records outside the mesh it is unobservable (read only
-                    // under inMesh, score.go:286,486) and is stored as 0.
-                    wmt = true;
-                    if (fj & GSIM_TF_IN_MESH) {
-                        mt = a.now - g[j];
-                        mt_store = mt;
-                        if (mt > tp->mesh_message_deliveries_activation_ns && !(fj & GSIM_TF_ACTIVE)) {
-                            fj |= GSIM_TF_ACTIVE;
-                            cfl = true;
-                        }
-                    }
-                }
-                if (SCORE && live) {
-                    double ts = 0.0;
-                    if (fj & GSIM_TF_IN_MESH) {                               // P1
-                        double p1 = 0.0;
-                        if (tp->time_in_mesh_quantum_ns != 0 && !(a.diag & DIAG_NO_DIV))
-                            p1 = (double)go_div(mt, tp->time_in_mesh_quantum_ns);
-                        if (p1 > tp->time_in_mesh_cap) p1 = tp->time_in_mesh_cap;
-                        ts += p1 * tp->time_in_mesh_weight;
-                    }
-                    ts += first * tp->first_message_deliveries_weight;         // P2
-                    if (fj & GSIM_TF_ACTIVE) {                                 // P3
-                        if (meshd < tp->mesh_message_deliveries_threshold) {
-                            const double deficit = tp->mesh_message_deliveries_threshold - meshd;
-                            const double p3 = deficit * deficit;
-                            ts += p3 * tp->mesh_message_deliveries_weight;
-                        }
-                    }
-                    ts += fail * tp->mesh_failure_penalty_weight;              // P3b
-                    const double p4 = inval * inval;                           // P4
-                    ts += p4 * tp->invalid_message_deliveries_weight;
-                    score += ts * tp->topic_weight;
-                }
-                if (REFRESH && st_ok) {
-                    policy_store(a.first, i, first, valid && cf, valid);
-                    policy_store(a.meshd, i, meshd, valid && cm, valid);
-                    if (cmc && valid) a.mcnt[i] = 0;
-                    policy_store(a.fail, i, fail, valid && cfa, valid);
-                    policy_store(a.invalid, i, inval, valid && ci, valid);
-                    policy_store(a.tflags, i, fj, valid && cfl, valid);
-                    if (!(a.diag & DIAG_NO_MTIME)) policy_store(a.mtime, i, mt_store, valid && wmt, false);
-                    if (purge) a.graft[i] = 0;
-                } else if (!REFRESH && valid && mc[j]) {   // score-only pass: still settle the counts
-                    a.meshd[i] = meshd;
-                    a.mcnt[i] = 0;
-                }
-            }
-        }
-        if (!valid) continue;
-        if (!tracked) {
-            if (SCORE) a.score[e] = 0.0;
-            if (pn) a.pen[e] = 0;                             // AddPenalty without peerStats: no-op
-        } else if (purge) {                                  // score.go:512-516
-            a.estate[e] = 0;
-            a.bp[e] = 0.0;
-            a.expire[e] = 0;
-            if (pn) a.pen[e] = 0;
-            *a.purged = 1;
-            if (SCORE) a.score[e] = 0.0;
-        } else {
-            if (decay) {
-                double x = bp * a.bp_decay;
-                if (x < a.dtz) x = 0.0;
-                if (x != bp) { bp = x; a.bp[e] = x; }
-            }
-            if (pn) {   // broken IWANT promises (applyIwantPenalties, gossipsub.go:1620-1625)
-                bp = bp + (double)pn;
-                a.bp[e] = bp;
-                a.pen[e] = 0;
-            }
-            if (SCORE) {
-                if (a.topic_cap > 0 && score > a.topic_cap) score = a.topic_cap;
-                score += p5 * a.w5;                                        // P5
-                score += p6 * a.w6;                                        // P6
-                if (bp > a.bp_thr) {                                       // P7
-                    const double excess = bp - a.bp_thr;
-                    const double p7 = excess * excess;
-                    score += p7 * a.w7;
-                }
-                a.score[e] = score;
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Kernel 2: ipColocationFactor (score.go:344-388) as a segmented count over
 // each observer's row keyed by IP id.  Only re-run when the tracked set or the
 // IP assignment changes (AddPeer/RemovePeer/purge), not every heartbeat.
@@ -811,7 +450,7 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     a.sub = h->d_sub;
     a.col = h->d_col;
     // (the subscription gather costs ≈1 ms per pass at C3, where nothing is skipped)
-    a.skip_unjoined = (h->unjoined_zero && !h->all_joined && !(h->diag & DIAG_S_NO_SKIP)) ? 1 : 0;
+    a.skip_unjoined = (h->unjoined_zero && !h->all_joined) ? 1 : 0;
     a.tp = h->d_tp;
     a.dtz = h->pp.decay_to_zero;
     a.bp_decay = h->pp.behaviour_penalty_decay;
@@ -829,7 +468,6 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     a.bp = h->d_bp; a.pen = h->d_pen; a.estate = h->d_estate; a.expire = h->d_expire; a.p6 = h->d_p6; a.score = h->d_score;
     a.now = now;
     a.purged = h->d_flags;
-    a.diag = h->diag;
     return a;
 }
 
@@ -852,46 +490,11 @@ int launch_ip_colocation(gsim_handle* h, const int32_t* gate)
     return hip_check(h, hipGetLastError(), "k_ip_colocation");
 }
 
-// Kernel variant for the refresh+score pass (A/B): GSIM_SCORE_KERNEL =
-// thread | wave4 | wave8 (default thread: measured fastest on MI355X, run 7
-// in DESIGN.md §5) or gsim_set_kernel_variant().
-static int score_variant_from_env()
-{
-    const char* s = std::getenv("GSIM_SCORE_KERNEL");
-    if (!s) return 0;
-    if (!std::strcmp(s, "pipe")) return 1;
-    if (!std::strcmp(s, "wave4")) return 2;
-    if (!std::strcmp(s, "wave8")) return 3;
-    return 0;
-}
-
 template <bool REFRESH, bool SCORE>
 static void launch_score_kernel(gsim_handle* h, const ScoreArgs& a)
 {
     ProfScope ps(h, REFRESH ? GSIM_K_REFRESH_SCORE : GSIM_K_SCORE);
-    if (h->score_variant < 0) h->score_variant = score_variant_from_env();
-    const int64_t tiles = (h->e + kTileEdges - 1) / kTileEdges;
-    switch (h->score_variant) {
-    case 0: {
-        // GSIM_REFRESH_GRID_CAP: grid-size A/B only
-        static const int cap = std::getenv("GSIM_REFRESH_GRID_CAP") ? std::atoi(std::getenv("GSIM_REFRESH_GRID_CAP")) : 16384;
-        hipLaunchKernelGGL((k_refresh_score<REFRESH, SCORE>), dim3(grid_for(h->e, 256, cap)), dim3(256), 0, h->stream, a);
-        return;
-    }
-    case 1: {
-        static const int cap = std::getenv("GSIM_REFRESH_GRID_CAP") ? std::atoi(std::getenv("GSIM_REFRESH_GRID_CAP")) : 16384;
-        hipLaunchKernelGGL((k_refresh_score_pipe<REFRESH, SCORE>), dim3(grid_for(h->e, 256, cap)), dim3(256), 0, h->stream, a);
-        return;
-    }
-    default: {
-        const int grid = (int)std::min<int64_t>(std::max<int64_t>((tiles + 3) / 4, 1), 256 * 32);
-        if (h->score_variant == 3)
-            hipLaunchKernelGGL((k_refresh_score_wave<REFRESH, SCORE, 8>), dim3(grid), dim3(256), 0, h->stream, a);
-        else
-            hipLaunchKernelGGL((k_refresh_score_wave<REFRESH, SCORE, 4>), dim3(grid), dim3(256), 0, h->stream, a);
-        return;
-    }
-    }
+    hipLaunchKernelGGL((k_refresh_score<REFRESH, SCORE>), dim3(grid_for(h->e)), dim3(256), 0, h->stream, a);
 }
 
 int launch_refresh_scores(gsim_handle* h, int64_t now)
@@ -1393,21 +996,21 @@ int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now, double p_mes
 int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant)
 {
     if (!h) return GSIM_EINVAL;
-    if (which == 1) {           // diagnostic ablation mask (timing experiments only)
-        h->diag = (uint32_t)variant;
-        return GSIM_OK;
-    }
-    if (which == 2) {           // k_send: 0 = 8-slot batch, 1 = 4-slot batch at >= 7 waves/SIMD, 2 = 4-slot batch, 3 = topic-major
-        if (variant < 0 || variant > 3) { h->err = "unknown k_send variant"; return GSIM_EINVAL; }
+    if (which == 2) {           // delivery: 0 = peer-major k_send (8-slot batch), 3 = topic-major k_send_tm
+        if (variant != 0 && variant != 3) { h->err = "unknown delivery kernel variant (0 or 3)"; return GSIM_EINVAL; }
         h->send_variant = variant;
         return GSIM_OK;
     }
-    if (which != 0 || variant < 0 || variant > 3) {
-        h->err = "unknown kernel variant";
-        return GSIM_EINVAL;
+    if (which == 3) {           // k_ihave lane group: 0 = by row lengths, else 16 / 32 / 64
+        if (variant != 0 && variant != 16 && variant != 32 && variant != 64) {
+            h->err = "unknown IHAVE lane width (0, 16, 32 or 64)";
+            return GSIM_EINVAL;
+        }
+        h->ihave_w = variant;
+        return GSIM_OK;
     }
-    h->score_variant = variant;
-    return GSIM_OK;
+    h->err = "unknown kernel variant class";
+    return GSIM_EINVAL;
 }
 
 int gsim_census(gsim_handle* h, int64_t* out8)

@@ -35,34 +35,10 @@ struct ScoreArgs {
     double* score;
     int64_t now;
     int32_t* purged;
-    uint32_t diag;   // diagnostic ablations (DIAG_*), 0 in production
     const uint64_t* sub;       // announced topics per peer (fill: records only where both endpoints joined)
     const int32_t* gate;       // non-null: run only if *gate != 0 (a retention purge happened)
     const uint32_t* col;       // col[r]: the observer of record r (record order)
     int32_t skip_unjoined;     // records of topics the observer did not join are zero: skip them
-};
-
-// Diagnostic ablations of the refresh+score wave kernel, for A/B timing only
-// (results are wrong when any is set; never used by tests or the bench value).
-enum : uint32_t {
-    DIAG_NO_P5 = 1,      // skip the P5 gather
-    DIAG_NO_MTIME = 2,   // skip the meshTime store
-    DIAG_NO_STORES = 4,  // skip every record store
-    DIAG_NO_GRAFT = 8,   // skip the graftTime load
-    DIAG_NO_DIV = 16,    // skip the P1 division
-    // delivery (k_send) ablations
-    DIAG_D_NO_COUNTERS = 32,    // skip the meshMessageDeliveries / invalid read-modify-writes
-    DIAG_D_PLAIN_CLAIM = 64,    // plain store instead of the claim atomicMin (racy)
-    DIAG_D_NO_ROWSTATE = 128,   // skip the acc/estate/tflags/rstate loads (all pass)
-    DIAG_D_NO_COMMIT = 256,     // skip the P2 credit of commits
-    DIAG_H_NO_GOSSIP = 512,     // heartbeat: skip emitGossip
-    DIAG_H_NO_IHAVE_STORE = 1024,   // heartbeat: choose gossip targets but do not store the marks
-    DIAG_H_NO_RECOMPUTE = 2048,     // heartbeat: emitGossip uses the snapshot score (no live recompute)
-    DIAG_D_NO_BITMAP = 4096,        // delivery: read every receiver's cell (no committed-bit shortcut; results unchanged)
-    DIAG_H_NO_SELECT = 8192,        // heartbeat: emitGossip takes every candidate (no shuffle/selection)
-    DIAG_H_CHEAP_KEYS = 16384,      // heartbeat: selection keys from a multiply hash instead of Philox
-    DIAG_S_NO_SKIP = 65536,         // score pass: read records of unjoined topics too (results unchanged)
-    DIAG_H_WAVE_ROWS = 32768,       // heartbeat: one observer per wavefront even when rows fit 32 lanes (results unchanged)
 };
 
 struct ColocArgs {
@@ -169,9 +145,8 @@ struct gsim_handle {
     // topics only), so they stay zero and the score pass may skip them.
     bool unjoined_zero = false;
     bool all_joined = false;     // every peer announced every topic (nothing to skip)
-    int score_variant = -1;   // refresh+score kernel variant (-1: from env)
     int send_variant = 3;     // delivery kernel variant (gsim_set_kernel_variant(h, 2, v)); 3 = topic-major
-    uint32_t diag = 0;        // DIAG_* ablations (A/B diagnostics only)
+    int ihave_w = 0;          // k_ihave lane group width (gsim_set_kernel_variant(h, 3, w)); 0 = by row lengths
 
     // device: parameters and scratch flags
     gsim_topic_score_params* d_tp = nullptr;
@@ -279,3 +254,4 @@ int deliver_promise_check(gsim_handle* h, int64_t now);    // broken promises ->
 int deliver_heartbeat_begin(gsim_handle* h, uint64_t tick); // fresh IHAVE marks
 uint64_t gsim_get_seed(const gsim_handle* h);              // heartbeat.hip
 int deliver_read_seen(gsim_handle* h, void* dst);
+int deliver_check_errors(gsim_handle* h);             // queue overflow / early slot reuse of the last tick

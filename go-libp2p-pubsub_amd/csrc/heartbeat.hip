@@ -70,7 +70,6 @@ struct HbArgs {
     // live Score(p) for emitGossip (score.go:265-342)
     const double *first, *invalid, *p5, *p6;
     double topic_cap, w5, w6, bp_thr, w7;
-    uint32_t diag;             // timing ablations (bit0: no emitGossip, bit1: no IHAVE store, bit2: no live recompute)
     // fanout (gossipsub.go:1011-1028, 1558-1596); router bit GSIM_TF_FANOUT in mflags
     int64_t* lastpub;          // [N][T]
     uint64_t* fan_topics;      // [N]
@@ -169,10 +168,7 @@ __device__ bool select_smallest(const HbArgs& a, bool cand, int count, uint32_t 
     if (count <= 0 || n <= count) return cand;
     const int lane = threadIdx.x & 63;
     uint32_t hi = 0xFFFFFFFFu;
-    if (cand) {
-        if (a.diag & 32) hi = (col ^ (uint32_t)t * 0x85EBCA6Bu) * 0x9E3779B9u;   // timing ablation only
-        else hi = hb_key_hi(a, obs, t, purpose, col, pos);
-    }
+    if (cand) hi = hb_key_hi(a, obs, t, purpose, col, pos);
     // any threshold gives the same selection; it only sets how many lanes the
     // loops below adjust (fp32: no 64-bit integer division)
     const uint32_t tau = (uint32_t)((float)count / (float)n * 4294967040.0f);
@@ -575,16 +571,15 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* row
                 for (int k = 1; k < LP; ++k)
                     if (t >= W * k) lpsel = lpv[k];
                 const int32_t lpt = __shfl(lpsel, base + (t & (W - 1)), 64);
-                if (!(a.diag & 1) && lpt >= (int64_t)a.tick - a.hist_gossip) {
-                    if ((__ballot(dirty) & gm) && !(a.diag & 4)) {
+                if (lpt >= (int64_t)a.tick - a.hist_gossip) {
+                    if (__ballot(dirty) & gm) {
                         if (dirty) S_live = score_of_record(a, rv, col);
                         dirty = false;
                     }
                     const bool gcand = tpeer && !m && !dir && S_live >= a.gossip_thr;
-                    gsel = (a.diag & 16) ? gcand
-                                         : gossip_targets<W>(a, gcand, tpeer, (uint32_t)obs, t, col, pos, gm, grp);
+                    gsel = gossip_targets<W>(a, gcand, tpeer, (uint32_t)obs, t, col, pos, gm, grp);
                 }
-                if (valid && !(a.diag & 2)) a.gsel[i] = gsel ? 1 : 0;
+                if (valid) a.gsel[i] = gsel ? 1 : 0;
             }
             if (valid) {
                 if (ctl) {
@@ -1038,7 +1033,6 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.first = h->d_first; a.invalid = h->d_invalid; a.p5 = h->d_p5; a.p6 = h->d_p6;
     a.topic_cap = h->pp.topic_score_cap; a.w5 = h->pp.app_specific_weight; a.w6 = h->pp.ip_colocation_factor_weight;
     a.bp_thr = h->pp.behaviour_penalty_threshold; a.w7 = h->pp.behaviour_penalty_weight;
-    a.diag = (h->diag >> 9) & 119u;  // DIAG_H_NO_GOSSIP / _NO_IHAVE_STORE / _NO_RECOMPUTE / _NO_SELECT / _CHEAP_KEYS / _WAVE_ROWS
     a.lastpub = h->x->d_lastpub; a.fan_topics = h->x->d_fantopics;
     a.pub_thr = h->th.publish_threshold; a.fanout_ttl = h->gp.fanout_ttl_ns;
     return a;
@@ -1084,6 +1078,7 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
     if (h->e == 0 || !h->x) { h->err = "no graph loaded"; return GSIM_ESTATE; }
     int rc = check_degree(h);
+    if (!rc) rc = deliver_check_errors(h);
     if (rc) return rc;
     rc = deliver_flush(h);
     if (!rc) rc = deliver_heartbeat_begin(h, tick);   // IHAVE marks of this heartbeat are pending
@@ -1095,9 +1090,7 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     // of <= 16 connections, 2 for <= 32, 1 otherwise (observers are
     // independent within a heartbeat, so the classes run one after the other)
     const Extra* x = h->x;
-    if (a.diag & 64) {
-        hipLaunchKernelGGL(k_heartbeat<64>, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a, nullptr, h->n);
-    } else if (x->n16 == h->n) {
+    if (x->n16 == h->n) {
         hipLaunchKernelGGL(k_heartbeat<16>, dim3(grid_rows((h->n + 3) / 4)), dim3(256), 0, h->stream, a, nullptr, h->n);
     } else if (x->n32 == h->n) {
         hipLaunchKernelGGL(k_heartbeat<32>, dim3(grid_rows((h->n + 1) / 2)), dim3(256), 0, h->stream, a, nullptr, h->n);
@@ -1152,6 +1145,9 @@ int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, i
     }
     int rc = deliver_flush(h);              // pending first deliveries precede the removal
     if (!rc) rc = materialize_mcnt(h);      // the P3b test reads meshMessageDeliveries
+    // RemovePeer scores the peer live (score.go:611-644): P6 over the tracked
+    // set as it is now (an up batch since the last derivation changed it)
+    if (!rc && !up && h->p6_dirty) rc = launch_ip_colocation(h);
     if (rc) return rc;
     ProfScope ps(h, GSIM_K_CHURN);
     const int32_t n2 = 2 * count;

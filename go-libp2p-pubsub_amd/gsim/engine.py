@@ -87,6 +87,19 @@ def random_regular(n: int, k: int, seed: int = 1, n_topics: int = 1, unique_ips:
     return Network(n, row_ptr, col, ob, sub, ip_ptr, ip_ids, n_ips)
 
 
+def app_scores(fn, n: int) -> np.ndarray:
+    """AppSpecificScore(p) for every peer index (score_params.go:78), the array
+    gsim_set_app_score installs.  A callback marked ``fn.vectorized = True``
+    takes the whole index array at once; any other is called once per peer.
+    Every peer's value is evaluated: there is no size above which it is skipped."""
+    if getattr(fn, "vectorized", False):
+        out = np.asarray(fn(np.arange(n, dtype=np.int64)), dtype=np.float64)
+        if out.shape != (n,):
+            raise ValueError("a vectorized AppSpecificScore must return one value per peer")
+        return np.ascontiguousarray(out)
+    return np.fromiter((fn(p) for p in range(n)), dtype=np.float64, count=n)
+
+
 class Engine:
     """One simulated GossipSub network on one GPU."""
 
@@ -150,8 +163,7 @@ class Engine:
             _ptr(net.ip_ptr), _ptr(net.ip_ids), net.n_ips))
         self.net = net
         if self.params.AppSpecificScore is not None:
-            self.set_app_score(np.array([self.params.AppSpecificScore(p) for p in range(net.n)],
-                                        dtype=np.float64) if net.n <= 100000 else np.zeros(net.n))
+            self.set_app_score(app_scores(self.params.AppSpecificScore, net.n))
 
     def set_app_score(self, p5: np.ndarray):
         p5 = np.ascontiguousarray(p5, dtype=np.float64)
@@ -226,7 +238,8 @@ class Engine:
         c = _abi.CMsgConfig()
         c.ring, c.rounds, c.t0_ns = int(ring), int(rounds), int(t0)
         c.heartbeat_ns = int(heartbeat if heartbeat is not None else self.gossip.HeartbeatInterval)
-        # reserved fields of the ABI (the engine keeps no per-copy lists)
+        # max_frontier is reserved (the engine keeps no per-copy lists); max_arrivals
+        # sizes the IWANT response queue (0: the library default, gsim.h)
         c.max_frontier = int(max_frontier or 0)
         c.max_arrivals = int(max_arrivals or 0)
         self._check(self.lib.gsim_msgs_init(self.h, ctypes.byref(c)))

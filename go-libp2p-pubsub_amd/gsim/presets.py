@@ -4,7 +4,18 @@ TopicScoreParams / PeerScoreParams / thresholds of gossipsub_spam_test.go
 workload and the parity tests."""
 from __future__ import annotations
 
+import numpy as np
+
 from .params import Minute, PeerScoreParams, PeerScoreThresholds, Second, TopicScoreParams
+
+
+def zero_app_score(p):
+    """AppSpecificScore that is 0 for every peer (vectorized: takes a peer
+    index or an array of them, see gsim.engine.app_scores)."""
+    return np.zeros(np.shape(p)) if np.ndim(p) else 0.0
+
+
+zero_app_score.vectorized = True
 
 
 def beacon_topic(**over) -> TopicScoreParams:
@@ -23,7 +34,7 @@ def beacon_topic(**over) -> TopicScoreParams:
 
 def beacon_params(n_topics: int, topic_cap: float = 0.0, **over) -> PeerScoreParams:
     """gossipsub_spam_test.go:627-637 peer params (+P6/P7 enabled for coverage)."""
-    kw = dict(AppSpecificScore=lambda p: 0.0, AppSpecificWeight=1.0, IPColocationFactorWeight=-35.11,
+    kw = dict(AppSpecificScore=zero_app_score, AppSpecificWeight=1.0, IPColocationFactorWeight=-35.11,
               IPColocationFactorThreshold=2, BehaviourPenaltyWeight=-15.92, BehaviourPenaltyThreshold=6,
               BehaviourPenaltyDecay=0.986, DecayInterval=Second, DecayToZero=0.01, RetainScore=10 * Second,
               TopicScoreCap=topic_cap)

@@ -225,7 +225,9 @@ int gsim_set_seed(gsim_handle* h, uint64_t seed);
  * every OpportunisticGraftTicks; Graft/Prune traced into the score counters.
  * Uses the current score snapshot as the heartbeat's score cache
  * (gossipsub.go:1375-1383): call gsim_refresh_scores first.  GRAFT/PRUNE
- * records land in the receivers' control inbox for round 0. */
+ * records land in the receivers' control inbox for round 0.  Fails with the
+ * previous tick's delivery error, if any (GSIM_ERANGE: the IWANT response
+ * queue overflowed; GSIM_ESTATE: a slot was republished too early). */
 int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now_ns);
 /* Control-message round: every receiver handles the GRAFT/PRUNE records in
  * its inbox for `round` (handleGraft gossipsub.go:741-837, handlePrune
@@ -244,7 +246,8 @@ int gsim_handle_control(gsim_handle* h, int32_t round, int64_t now_ns);
  *         P3b penalty applied.
  *   up:   router AddPeer (gossipsub.go:525-552), peerScore.AddPeer
  *         (score.go:595-609): a retained record is reused, else a fresh one.
- * The removed peer's live score uses P6 as last derived.  GSIM_EINVAL if a
+ * The removed peer's live score uses P6 over the tracked set as the batch
+ * starts (re-derived if an up batch changed it).  GSIM_EINVAL if a
  * pair is not a connection or is listed twice (nothing is changed then). */
 int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, int32_t up, int64_t now_ns);
 
@@ -388,15 +391,11 @@ int gsim_profile(gsim_handle* h, int32_t enable);
  * since the last read (n entries, indexed by gsim_kernel_class) and reset. */
 int gsim_profile_read(gsim_handle* h, double* ms, int64_t* launches, int32_t n);
 /* Select an implementation variant of a hot-path kernel for A/B timing in
- * one process (results are identical across variants).  which = 0: the
- * refreshScores+score pass; variant 0 thread-per-edge (default), 1 thread-
- * per-edge with the topic loop software-pipelined, 2 wave (4-topic chunks),
- * 3 wave (8-topic chunks).  which = 1: diagnostic ablation
- * mask for timing experiments (results are wrong while it is non-zero).
- * which = 2: the delivery kernel; variant 3 (default) is topic-major with the
- * slots' committed bits staged in LDS (used while they fit: N <= ~1.1M peers),
- * else peer-major k_send: 0 loads 8 slots' cells per trip, 1 loads 4 with
- * registers capped for 7 waves per SIMD, 2 loads 4. */
+ * one process.  Results are identical across variants (the GPU tests run
+ * each).  which = 2: the delivery kernel; variant 3 (default) is topic-major
+ * with the slots' committed bits staged in LDS (used while they fit), 0 is
+ * the peer-major k_send.  which = 3: the IHAVE walk's lane group width
+ * (16, 32 or 64 lanes per row; 0 = chosen from the row lengths). */
 int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant);
 
 /* ---- synthetic inputs -------------------------------- */

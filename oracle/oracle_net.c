@@ -438,14 +438,17 @@ static int64_t find_edge(const orc_net* s, uint32_t i, uint32_t j)
  * RemovePeer (score.go:611-644: drop a positive score, else retain with P2
  * reset and the P3b penalty).  Up: the router's AddPeer (gossipsub.go:525-552)
  * and peerScore.AddPeer (score.go:595-609).  The live score of a removed peer
- * uses the stored P6 (ipColocationFactor as last derived).  Returns the index
- * of the first pair that is not a connection, or -1. */
+ * uses ipColocationFactor over the tracked set as the batch starts (Go
+ * computes it live, score.go:344-388; an earlier up batch of the same tick
+ * has changed that set), the same for every removal of the batch.  Returns
+ * the index of the first pair that is not a connection, or -1. */
 int32_t orc_churn(orc_net* s, const uint32_t* pairs, int32_t count, int32_t up, int64_t now)
 {
     for (int32_t q = 0; q < count; ++q) {
         const uint32_t a = pairs[2 * q], b = pairs[2 * q + 1];
         if (a >= s->n || b >= s->n || find_edge(s, a, b) < 0) return q;
     }
+    if (!up) orc_ip_colocation(s);
     for (int32_t q = 0; q < count; ++q) {
         for (int d = 0; d < 2; ++d) {
             const uint32_t o = pairs[2 * q + d], p = pairs[2 * q + 1 - d];

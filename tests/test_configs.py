@@ -96,6 +96,88 @@ def test_c2_10k_single_topic_full_scoring(require_gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_c3_shape_from_device_fill(require_gpu):
+    """C3's shape at 20k peers: random-regular k=32, 16 topics, the bench's
+    beacon-style params and thresholds, starting from gsim_fill_synthetic
+    (the state bench.py runs from), 5 ticks at 4 msg/s/topic with 2 % invalid
+    messages: mesh maintenance, control, gossip and promises, every array
+    bit-exact against the oracle after each tick."""
+    from fixtures import beacon_params, beacon_thresholds
+    from gsim.engine import Engine, random_regular
+    from tickrun import SEED, run_parity, subscribed_schedule
+    rng = np.random.default_rng(303)
+    n, T = 20_000, 16
+    net = random_regular(n, 32, seed=17, n_topics=T)
+    params = beacon_params(T)
+    th = beacon_thresholds()
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12)
+    eng = Engine(params, th, gossip=gp)
+    eng.load_graph(net)
+    eng.set_seed(SEED)
+    eng.fill_synthetic(seed=31, now=tick_time(0), p_mesh=8 / 32)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    st.pull_from_engine(eng)
+    ticks = list(range(1, 6))
+    sched = subscribed_schedule(rng, ticks, net, T, 4.0, 0.02)
+    msgs, gs = run_parity(net, params, th, gp, st, ticks, sched, ring=1024, eng=eng)
+    assert gs["iwant_ids"] > 0 and msgs.stats[3] >= 0
+    assert msgs.stats[0] == msgs.stats[1] + msgs.stats[2]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_c3_full_size_invariants(require_gpu):
+    """The bench workload itself (1M peers, k=32, 16 topics, beacon params,
+    4 msg/s/topic) for 3 ticks, checked through size-independent properties:
+      * right after the heartbeat every (peer, topic) mesh has <= Dhi members;
+      * every mesh link that changed between the start of a tick and the end
+        of its control rounds (GRAFT/PRUNE and their replies) ends symmetric;
+      * accepted deliveries = first + duplicate, and no error (queue overflow,
+        early slot reuse) is reported."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    cfg = bench.CONFIGS["c3"]
+    eng, net = bench.build_engine(cfg, seed=1, device=0)
+    n, T, Dhi = cfg[0], cfg[2], cfg[5]
+    rev = net.rev()
+    rp = net.row_ptr.astype(np.int64)
+    sched = bench.message_schedule(n, T, range(1, 4), seed=2)
+    try:
+        def mesh():
+            return (eng.read(_abi.F_TFLAGS) & _abi.TF_MESH) != 0
+        before = mesh()
+        for k in range(1, 4):
+            now = bench.tick_time(k)
+            eng.refresh_scores(now)
+            eng.heartbeat(k, now)
+            after_hb = mesh()
+            for t in range(T):
+                sizes = np.add.reduceat(after_hb[t].astype(np.int32), rp[:-1])
+                assert sizes.max() <= Dhi, f"tick {k} topic {t}: mesh above Dhi after the heartbeat"
+            del after_hb
+            for g in range(k * bench.ROUNDS, (k + 1) * bench.ROUNDS):
+                if g in sched:
+                    eng.publish_array(sched[g], g)
+                eng.round(g)
+                if g == k * bench.ROUNDS + 1:
+                    final = mesh()
+                    changed = before != final
+                    assert changed.any(), "the heartbeat changed some links"
+                    for t in range(T):
+                        c = np.nonzero(changed[t])[0]
+                        assert np.array_equal(final[t][c], final[t][rev[c]]), f"tick {k} topic {t}: asymmetric"
+                    del changed
+            before = mesh()
+            st = eng.msg_stats()
+            assert st[0] == st[1] + st[2] and st[1] > 0
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
 def test_c4_sybil_colocation_broken_promises(require_gpu):
     """C4 scaled 1/10: 10k honest + 2.5k sybils that never answer IWANT.  The
     sybils sit behind few addresses (500 per IP), so an honest peer sees several
@@ -160,6 +242,38 @@ def test_c5_power_law_zipf_topics_churn(require_gpu):
     churn = {2: [(downs[2], False)], 4: [(downs[2], True), (downs[4], False)], 6: [(downs[4], True)]}
     run_parity(net, params, th, gp, st, ticks, sched, ring=1024, churn=churn)
     assert (np.diff(net.row_ptr.astype(np.int64)) > 32).any(), "rows longer than half a wave"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("width", [16, 32, 64])
+def test_ihave_lane_widths_bit_exact(require_gpu, width):
+    """The IHAVE/IWANT walk (k_ihave) with 16-, 32- and 64-lane row groups on
+    one power-law graph (rows of 1-64 connections: a 16-lane group walks the
+    long rows in chunks): every width is bit-exact against the oracle, so
+    all give the same promises, IWANT ids and responses."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim import graphs
+    from gsim.engine import Engine
+    from tickrun import SEED, restrict_to_subscriptions, run_parity, subscribed_schedule
+    rng = np.random.default_rng(707)
+    n, T = 2500, 8
+    net = graphs.power_law(n, 16, 2.5, 64, seed=21, n_topics=T)
+    net = graphs.with_subscriptions(net, graphs.zipf_subscriptions(n, T, 3, seed=22))
+    params = beacon_params(T)
+    th = PeerScoreThresholds(GossipThreshold=-20, PublishThreshold=-40, GraylistThreshold=-300)
+    gp = GossipSubParams(D=6, Dlo=4, Dhi=10, Dscore=3, Dout=2)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 0.25)
+    restrict_to_subscriptions(st, net)
+    eng = Engine(params, th, gossip=gp)
+    eng.load_graph(net)
+    eng.set_seed(SEED)
+    st.push_to_engine(eng)
+    eng.set_kernel_variant(3, width)
+    ticks = list(range(1, 5))
+    sched = subscribed_schedule(rng, ticks, net, T, 3.0, 0.02)
+    _, gs = run_parity(net, params, th, gp, st, ticks, sched, ring=512, eng=eng)
+    assert gs["iwant_ids"] > 0 and (np.diff(net.row_ptr.astype(np.int64)) > 32).any()
 
 
 @pytest.mark.gpu

@@ -55,14 +55,12 @@ def build(n, k, T, seed, frac_sybil=0.2, topic_cap=0.0, multi_ip=False):
     return net, params, st, p5, white
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("n,k,T,cap,multi_ip", [(600, 16, 1, 0.0, False), (2000, 32, 4, 0.0, False),
                                                 (3000, 32, 3, 3.5, False), (1000, 20, 11, 0.0, False),
                                                 (1500, 24, 2, 0.0, True)])
-def test_refresh_and_score_bit_exact(require_gpu, n, k, T, cap, multi_ip, variant):
+def test_refresh_and_score_bit_exact(require_gpu, n, k, T, cap, multi_ip):
     net, params, st, p5, white = build(n, k, T, seed=n + T, topic_cap=cap, multi_ip=multi_ip)
     eng = Engine(params, beacon_thresholds())
-    eng.set_kernel_variant(0, variant)
     eng.load_graph(net)
     eng.set_app_score(p5)
     eng.set_ip_whitelist(white)
