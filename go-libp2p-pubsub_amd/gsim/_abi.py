@@ -106,6 +106,14 @@ KERNEL_CLASSES = ["refresh_score", "score", "ip_colocation", "heartbeat", "contr
                   "commit", "accept", "gossip", "churn"]
 BEHAVE_IGNORE_IWANT = 0x01
 
+class CShardInfo(Structure):
+    _fields_ = [("shard", c_int32), ("shards", c_int32), ("n_local", c_int64), ("e_local", c_int64),
+                ("own_lo", c_int64), ("own_hi", c_int64), ("own_e_lo", c_int64), ("own_e_hi", c_int64),
+                ("n_cross", c_int64)]
+
+
+MAX_SHARDS = 64
+
 SIGNATURES = [
     ("gsim_default_gossipsub_params", None, [POINTER(CGossipSubParams)]),
     ("gsim_validate_topic_params", c_int32, [POINTER(CTopicScoreParams), c_char_p, c_size_t]),
@@ -154,6 +162,11 @@ SIGNATURES = [
     ("gsim_set_direct_peers", c_int32, [c_void_p, c_void_p]),
     ("gsim_profile", c_int32, [c_void_p, c_int32]),
     ("gsim_profile_read", c_int32, [c_void_p, c_void_p, c_void_p, c_int32]),
+    ("gsim_shard_partition", c_int32, [c_int64, c_void_p, c_void_p, c_int32, c_void_p]),
+    ("gsim_shard_layout_info", c_int32, [c_int64, c_void_p, c_void_p, c_void_p, c_int32, c_int32,
+                                         POINTER(CShardInfo)]),
+    ("gsim_shard_layout", c_int32, [c_int64, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 ]
 
 _lib = None

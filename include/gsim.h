@@ -412,6 +412,44 @@ int gsim_gen_random_regular(int64_t n, int32_t k, uint64_t seed,
  * where a host upload would dominate. */
 int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now_ns, double p_mesh);
 
+/* ---- graph sharding across GPUs -------- */
+/* The reference simulates nothing across processes: one GossipSubRouter per
+ * host, RPCs over libp2p streams (gossipsub.go:1138-1202 sendRPC).  Here one
+ * network is split into contiguous peer ranges, one per shard (GPU); a shard
+ * holds its peers' rows in full plus a "ghost" row per remote neighbour (that
+ * neighbour's connections into the shard), so every record an owned observer
+ * keeps is local, and the per-round halo exchange carries message copies,
+ * GRAFT/PRUNE records and gossip marks between shards. */
+#define GSIM_MAX_SHARDS 64
+
+/* Contiguous peer ranges for `shards` shards balanced by the sum of (row
+ * length x joined topics): bounds[0] = 0 < bounds[1] < ... < bounds[shards]
+ * = n, interior bounds multiples of 64.  sub may be NULL (one topic each). */
+int gsim_shard_partition(int64_t n, const uint32_t* row_ptr, const uint64_t* sub, int32_t shards,
+                         int64_t* bounds);
+
+typedef struct gsim_shard_info {
+    int32_t shard, shards;
+    int64_t n_local, e_local;   /* local peers (owned + ghosts) and edges (owned rows + ghost rows) */
+    int64_t own_lo, own_hi;     /* owned peers: local ids [own_lo, own_hi) = global [bounds[s], bounds[s+1]) */
+    int64_t own_e_lo, own_e_hi; /* local edges of the owned rows */
+    int64_t n_cross;            /* owned-row edges whose column belongs to another shard */
+} gsim_shard_info;
+int gsim_shard_layout_info(int64_t n, const uint32_t* row_ptr, const uint32_t* col, const int64_t* bounds,
+                           int32_t shards, int32_t shard, gsim_shard_info* out);
+/* The local graph of one shard (sizes from gsim_shard_layout_info; any output
+ * may be NULL): gid[n_local] global id of each local peer (ascending);
+ * row_ptr_l/col_l the local CSR; gidx[e_local] the global index of each local
+ * edge; per other shard s, ghost_base[s]/ghost_count[s] the local edges of the
+ * ghost rows of s's peers, and cross_count[s] owned-row edges into s, listed
+ * in edge order one shard after the other in cross_out (n_cross entries).
+ * Two shards enumerate their common cross edges in the same order:
+ * cross_out of a into b, position q, is the edge ghost_base[a] + q of b. */
+int gsim_shard_layout(int64_t n, const uint32_t* row_ptr, const uint32_t* col, const int64_t* bounds,
+                      int32_t shards, int32_t shard, uint32_t* gid, uint32_t* row_ptr_l, uint32_t* col_l,
+                      uint64_t* gidx, int64_t* ghost_base, int64_t* ghost_count, uint32_t* cross_out,
+                      int64_t* cross_count);
+
 #ifdef __cplusplus
 }
 #endif
