@@ -58,6 +58,8 @@ constexpr uint32_t kPeerMask = 0x3FFFFFFFu;
 constexpr int kMaxRing = 8192;     // active-slot list lives in LDS (u16, sized by the ring)
 constexpr int kSlotBatch = 8;      // active slots whose cells are loaded together
 
+struct IhaveStage;
+
 struct Deliver {
     gsim_msg_config cfg{};
     uint32_t *d_mtopic = nullptr, *d_morigin = nullptr;
@@ -91,6 +93,7 @@ struct Deliver {
     std::vector<int64_t> prom_made;    // [P] tick that filled each ring index, -1 = empty
     int64_t ihave_tick = -1;           // heartbeat whose IHAVE marks are pending
     int64_t resp_round = -1;           // round in which the queued responses arrive
+    struct IhaveStage* ih = nullptr;   // a sharded group's IHAVE stage between count and walk
 };
 
 struct RoundArgs {
@@ -124,6 +127,19 @@ struct RoundArgs {
     const uint32_t* rev;
     int32_t flood;
     double pub_thr;
+    // seen-set cells exist for peers [clo, clo + CN) only (a shard's owned
+    // peers; every peer when unsharded): cell[m * CN + (i - clo)]
+    int64_t CN;
+    uint32_t clo;
+    // sharded network: a copy to a ghost receiver (outside
+    // [clo, clo + CN)) is queued for its shard: xout[dest * xcap + k] =
+    // the receiver's record there (xr[e]) | slot << 32, xcnt[dest] counts
+    int32_t sharded;
+    const uint32_t* xr;
+    const uint8_t* pshard;
+    uint64_t* xout;
+    uint32_t* xcnt;
+    int64_t xcap;
 };
 
 __device__ __forceinline__ int64_t round_time(const RoundArgs& a, int64_t g)
@@ -227,15 +243,15 @@ __global__ void k_reset_slots(RoundArgs a, const gsim_msg* pub, int32_t count)
     const int k = blockIdx.y;
     if (k >= count) return;
     const uint32_t m = (uint32_t)(pub[k].id % (uint64_t)a.ring);
-    uint64_t* row = a.cell + (int64_t)m * a.N;
+    uint64_t* row = a.cell + (int64_t)m * a.CN;
     const uint32_t q = (uint32_t)((a.g - 1) & 1);
     // the previous message may still sit in a gossip window or a promise
     if (blockIdx.x == 0 && threadIdx.x == 0 && a.slot_last[m] >= 0 && a.g - a.slot_last[m] < a.reuse_guard)
         atomicOr(&a.err[2], 1u);
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.N; i += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.CN; i += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t c = row[i];
         // several reused rows may credit one record: atomic updates here
-        if (a.g > 0 && is_claim_of(c, q)) commit_claim<true>(a, row + i, c, a.g - 1, m, i);
+        if (a.g > 0 && is_claim_of(c, q)) commit_claim<true>(a, row + i, c, a.g - 1, m, a.clo + i);
         row[i] = kUnseen64;
         if ((i & 63) == 0) a.seenbm[(int64_t)m * a.nw + (i >> 6)] = 0;
     }
@@ -248,15 +264,17 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, int32_t count)
     const gsim_msg p = pub[k];
     const uint32_t slot = (uint32_t)(p.id % (uint64_t)a.ring);
     a.mtopic[slot] = p.topic;
-    a.morigin[slot] = p.origin;
+    a.morigin[slot] = p.origin;          // local id (a shard: 0xFFFFFFFF when not a local peer)
     a.minv[slot] = p.invalid;
-    a.cell[(int64_t)slot * a.N + p.origin] = ((uint64_t)(uint32_t)a.g << 32) | p.origin;
-    atomicOr(reinterpret_cast<unsigned long long*>(a.seenbm + (int64_t)slot * a.nw + (p.origin >> 6)),
-             1ull << (p.origin & 63));
     a.mpub[slot] = (int32_t)a.g;
-    int32_t* lp = a.lastput + (int64_t)p.topic * a.N + p.origin;
-    const int32_t tick = (int32_t)(a.g / a.R);
-    if (*lp < tick) *lp = tick;
+    if (p.origin >= a.clo && (int64_t)(p.origin - a.clo) < a.CN) {   // the origin's own cell
+        const uint32_t oc = p.origin - a.clo;
+        a.cell[(int64_t)slot * a.CN + oc] = ((uint64_t)(uint32_t)a.g << 32) | p.origin;
+        atomicOr(reinterpret_cast<unsigned long long*>(a.seenbm + (int64_t)slot * a.nw + (oc >> 6)), 1ull << (oc & 63));
+        int32_t* lp = a.lastput + (int64_t)p.topic * a.N + p.origin;
+        const int32_t tick = (int32_t)(a.g / a.R);
+        if (*lp < tick) *lp = tick;
+    }
     atomicOr(&a.nnew_cur[slot >> 5], 1u << (slot & 31));   // the origin forwards in round g+1
     a.slot_last[slot] = (int32_t)a.g;
 }
@@ -295,7 +313,7 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
 #pragma unroll
         for (int b = 0; b < B; ++b) {
             const int k = k0 + b;
-            cv[b] = (k < nact && vj) ? a.cell[(int64_t)s_act[k] * a.N + jl] : kUnseen64;
+            cv[b] = (k < nact && vj) ? a.cell[(int64_t)s_act[k] * a.CN + jl] : kUnseen64;
         }
         // (1) commit this lane's claims of round g-1: the winners' records are
         // loaded for the whole batch first (one memory trip), then updated in
@@ -329,7 +347,7 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
                 if (k >= nact || !is_claim_of(cv[b], qpar)) continue;
                 const uint32_t m = s_act[k];
                 const uint64_t c0 = cv[b];
-                a.cell[(int64_t)m * a.N + jl] = ((uint64_t)gprev << 32) | ((uint32_t)c0 & kPeerMask);
+                a.cell[(int64_t)m * a.CN + jl] = ((uint64_t)gprev << 32) | ((uint32_t)c0 & kPeerMask);
                 if (a.minv[m]) continue;                 // RejectMessage: counted when sent
                 const int32_t t = (int32_t)a.mtopic[m];
                 int32_t* lp = a.lastput + (int64_t)t * a.N + jl;
@@ -355,7 +373,7 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
             const int k = k0 + b;
             if (k >= nact) break;                        // wave-uniform
             const uint32_t m = s_act[k];
-            const int64_t row_m = (int64_t)m * a.N;
+            const int64_t row_m = (int64_t)m * a.CN;
             const uint64_t c0 = cv[0];
 #pragma unroll
             for (int q = 0; q + 1 < B; ++q) cv[q] = cv[q + 1];
@@ -373,7 +391,7 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
             // the origin's own Publish goes to its mesh, to its fanout when it
             // has not joined the topic, or floods every topic peer with score
             // >= publishThreshold (gossipsub.go:989-1028); forwarders use their mesh
-            const uint8_t o_want = ((a.sub[origin] >> t) & 1ull) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
+            const uint8_t o_want = (origin < a.N && ((a.sub[origin] >> t) & 1ull)) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
             const ctp_t tp = tpa + t;
             const bool scored_t = tp->scored != 0;
             const int64_t window = tp->mesh_message_deliveries_window_ns;
@@ -538,6 +556,27 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
 constexpr int kTmThreads = 1024;
 constexpr int kTmChunk = 2048;      // peers scanned per frontier chunk (two per thread)
 
+// Queue copies to ghost receivers for their shards (all lanes of the wave
+// call this): one atomic per destination shard per wave.
+__device__ __forceinline__ void emit_remote(const RoundArgs& a, bool emit, uint32_t dest, uint64_t v)
+{
+    const int lane = threadIdx.x & 63;
+    uint64_t pend = __ballot(emit);
+    while (pend) {
+        const int lead = __ffsll((long long)pend) - 1;
+        const uint32_t d = (uint32_t)__shfl((int)dest, lead, 64);
+        const uint64_t mask = __ballot(emit && dest == d);
+        uint32_t base = 0;
+        if (lane == lead) base = atomicAdd(&a.xcnt[d], (uint32_t)__popcll(mask));
+        base = (uint32_t)__shfl((int)base, lead, 64);
+        if (emit && dest == d) {
+            const int64_t pos = (int64_t)base + __popcll(mask & ((1ull << lane) - 1));
+            if (pos < a.xcap) a.xout[(int64_t)d * a.xcap + pos] = v;
+        }
+        pend &= ~mask;
+    }
+}
+
 template <int W>
 __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t range)
 {
@@ -550,8 +589,10 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
     __shared__ int s_ns, s_nf, s_claimed;
     __shared__ unsigned long long s_stats[4];
     const int32_t t = (int32_t)blockIdx.y;
-    const int64_t lo = (int64_t)blockIdx.x * range;
-    const int64_t hi = lo + range < a.N ? lo + range : a.N;
+    // senders: the peers with cells, [clo, clo + CN)
+    const int64_t pend_ = (int64_t)a.clo + a.CN;
+    const int64_t lo = (int64_t)a.clo + (int64_t)blockIdx.x * range;
+    const int64_t hi = lo + range < pend_ ? lo + range : pend_;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     if (tid == 0) { s_ns = 0; s_stats[0] = s_stats[1] = s_stats[2] = s_stats[3] = 0; }
     __syncthreads();
@@ -563,7 +604,7 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
         }
     }
     __syncthreads();
-    const int ns = a.g > 0 && lo < a.N ? s_ns : 0;
+    const int ns = a.g > 0 && lo < pend_ ? s_ns : 0;
     const int grp = lane / W, gl = lane % W;
     constexpr int G = 64 / W;                                // row groups per wave
     const ctp_t tp = const_tp(a.tp) + t;
@@ -574,13 +615,15 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
     const uint32_t gprev = (uint32_t)(a.g - 1);
     const uint32_t par = (uint32_t)(a.g & 1);
     const uint32_t claim_hi = kClaim | (par << 30);
+    const uint32_t clo = a.clo;
+    const uint64_t cn = (uint64_t)a.CN;
     unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
     for (int k = 0; k < ns; ++k) {
         const uint32_t m = s_slots[k];
-        const int64_t row_m = (int64_t)m * a.N;
+        const int64_t row_m = (int64_t)m * a.CN;
         const uint32_t origin = a.morigin[m];
         const bool inv = a.minv[m] != 0;
-        const uint8_t o_want = ((a.sub[origin] >> t) & 1ull) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
+        const uint8_t o_want = (origin < a.N && ((a.sub[origin] >> t) & 1ull)) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
         const bool win_all = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
         // stage the slot's committed bits
         for (int64_t w = tid; w < a.nw; w += kTmThreads) s_bm[w] = a.seenbm[(int64_t)m * a.nw + w];
@@ -597,7 +640,7 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
             for (int h = 0; h < H; ++h) {
                 const int64_t x = c0 + h * kTmThreads + tid;
                 const bool in = x < hi;
-                cs[h] = in ? a.cell[row_m + x] : kUnseen64;
+                cs[h] = in ? a.cell[row_m + (x - clo)] : kUnseen64;
                 rb[h] = in ? a.row_ptr[x] : 0u;
                 re[h] = in ? a.row_ptr[x + 1] : 0u;
             }
@@ -660,14 +703,21 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
                     // direct peers that joined the topic always get it (gossipsub.go:991-1003)
                     if (vv[u] && (ds & GSIM_DS_DIRECT) && !sel) sel = (a.sub[i] >> t) & 1ull;
                     const bool tg = vv[u] && sel && (ds & GSIM_DS_CONNECTED) && i != fv[u] && i != origin;
-                    const bool ok = tg && (ds & GSIM_DS_ACCEPT);
-                    n_gray += tg && !ok;                         // AcceptFrom: graylisted sender
+                    // a ghost receiver belongs to another shard: the copy goes
+                    // there, its AcceptFrom, seen check and counters too
+                    const uint32_t ic = i - clo;
+                    const bool remote = (uint64_t)ic >= cn;
+                    if (a.sharded)                           // (every lane of the wave is here)
+                        emit_remote(a, tg && remote, remote && vv[u] ? (uint32_t)a.pshard[i] : 0u,
+                                    (tg && remote) ? ((uint64_t)a.xr[e] | ((uint64_t)m << 32)) : 0ull);
+                    const bool ok = tg && !remote && (ds & GSIM_DS_ACCEPT);
+                    n_gray += tg && !remote && !ok;              // AcceptFrom: graylisted sender
                     n_acc += ok;
                     if (!ok) continue;
                     const bool sc = scored_t && (ds & GSIM_DS_TRACKED);
-                    const bool known = ((s_bm[i >> 6] >> (i & 63)) & 1ull) &&
+                    const bool known = ((s_bm[ic >> 6] >> (ic & 63)) & 1ull) &&
                                        (win_all || !sc || inv || !(tf & GSIM_TF_IN_MESH));
-                    const uint64_t c = known ? 0ull : a.cell[row_m + i];
+                    const uint64_t c = known ? 0ull : a.cell[row_m + ic];
                     const uint32_t chi = (uint32_t)(c >> 32);
                     int64_t seen_round = -1;
                     if (known) seen_round = a.g - 1;             // any earlier round: only "in window" is used
@@ -682,7 +732,7 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
                             if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo_w |= kCreditMesh;
                         }
                         const uint64_t cv = ((uint64_t)(claim_hi | e) << 32) | lo_w;
-                        const uint64_t prev = __hip_atomic_fetch_min(a.cell + row_m + i, cv, __ATOMIC_RELAXED,
+                        const uint64_t prev = __hip_atomic_fetch_min(a.cell + row_m + ic, cv, __ATOMIC_RELAXED,
                                                                      __HIP_MEMORY_SCOPE_AGENT);
                         if (prev == kUnseen64) n_first++;
                     }
@@ -741,17 +791,17 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
     __shared__ int s_n;
     const int nact = active_slots(a.nnew_cur, a.ring, s_act, &s_n);
     const int lane = threadIdx.x & 63;
-    const int64_t i0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
-    if (i0 >= a.N || nact == 0) return;
+    const int64_t i0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;   // cell index (peer clo + i)
+    if (i0 >= a.CN || nact == 0) return;
     const int64_t i = i0 + lane;
-    const bool vi = i < a.N;
+    const bool vi = i < a.CN;
     const uint32_t par = (uint32_t)(a.g & 1);
     for (int k0 = 0; k0 < nact; k0 += kSlotBatch) {
         uint64_t cv[kSlotBatch];
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
-            cv[b] = (k < nact && vi) ? a.cell[(int64_t)s_act[k] * a.N + i] : kUnseen64;
+            cv[b] = (k < nact && vi) ? a.cell[(int64_t)s_act[k] * a.CN + i] : kUnseen64;
         }
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
@@ -765,7 +815,7 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
             if (k >= nact) break;
             if (is_claim_of(cv[b], par)) {
                 const uint32_t m = s_act[k];
-                commit_claim(a, a.cell + (int64_t)m * a.N + i, cv[b], a.g, m, i);
+                commit_claim(a, a.cell + (int64_t)m * a.CN + i, cv[b], a.g, m, a.clo + i);
             }
         }
     }
@@ -806,6 +856,17 @@ struct IhArgs {
     unsigned long long* gstats;    // [0] receivers x slots walked, [1] IWANT ids, [2] responses, [3] broken promises
     bool respond;                  // GossipRetransmission >= 1
     uint64_t seed;
+    int64_t CN;                    // cells exist for peers [clo, clo + CN) (RoundArgs)
+    uint32_t clo;
+    // sharded network: every slot is pulled (receivers walk), an advertiser's
+    // holding of active slot k is a bit of the all-gathered holder bitmaps
+    // (bit gid - bounds[s] of block hoff[s] + k * hwords[s], s its shard)
+    int32_t sharded;
+    const uint32_t* gid;
+    const uint8_t* pshard;
+    const uint64_t* hbm;
+    const int64_t* hoff;           // [K+1] word offset of each shard's block
+    const int64_t* bounds;         // [K+1] global peer ranges
 };
 
 // first-seen round of a cell at control time of round g (any claim still
@@ -852,10 +913,10 @@ __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int64_t p0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
-    const int nact = p0 < a.N ? s_n : 0;
-    const int64_t pl = p0 + lane;
-    const bool vp = pl < a.N;
+    const int64_t p0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;   // cell index (peer clo + p)
+    const int nact = p0 < a.CN ? s_n : 0;
+    const int64_t pc = p0 + lane, pl = a.clo + pc;
+    const bool vp = pc < a.CN;
     const uint64_t subp = vp ? a.sub[pl] : 0ull;
     const int64_t tick_round = a.tick * a.R;
     for (int k0 = 0; k0 < nact; k0 += kSlotBatch) {
@@ -863,7 +924,7 @@ __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
-            cv[b] = (k < nact && vp) ? a.cell[(int64_t)s_act[k] * a.N + pl] : 0ull;
+            cv[b] = (k < nact && vp) ? a.cell[(int64_t)s_act[k] * a.CN + pc] : 0ull;
         }
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
@@ -898,7 +959,8 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
             const int m = m0 + lane;
             const bool act = m < a.ring && a.slot_last[m] >= a.lo_round && gcount[m] != 0 && gcount[a.ring + m] != 0;
             // cost model: a holder walk probes ~Dlazy cells, a receiver walk ~deg
-            const bool push = act && (uint64_t)gcount[m] * 4u < (uint64_t)gcount[a.ring + m] * 32u;
+            // (a sharded network pulls: receivers walk, holders are looked up)
+            const bool push = act && !a.sharded && (uint64_t)gcount[m] * 4u < (uint64_t)gcount[a.ring + m] * 32u;
             const uint64_t b = __ballot(act);
             if (act) s_act[n + __popcll(b & ((1ull << lane) - 1))] = (uint16_t)(m | (push ? 0x8000 : 0));
             n += __popcll(b);
@@ -907,10 +969,10 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int64_t p0 = ((int64_t)blockIdx.x * 4 + wid) * 64;
-    const int nact = p0 < a.N ? s_n : 0;
-    const int64_t pl = p0 + lane;
-    const bool vp = pl < a.N;
+    const int64_t p0 = ((int64_t)blockIdx.x * 4 + wid) * 64;   // cell index (peer clo + p)
+    const int nact = p0 < a.CN ? s_n : 0;
+    const int64_t pc = p0 + lane, pl = a.clo + pc;
+    const bool vp = pc < a.CN;
     const int grp = lane / W, gl = lane % W;
     const uint64_t gmask = group_mask<W>(grp);
     const uint64_t subp = vp ? a.sub[pl] : 0ull;
@@ -937,7 +999,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
-            cv[b] = (k < nact && vp) ? a.cell[(int64_t)(s_act[k] & 0x7FFF) * a.N + pl] : 0ull;
+            cv[b] = (k < nact && vp) ? a.cell[(int64_t)(s_act[k] & 0x7FFF) * a.CN + pc] : 0ull;
         }
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
@@ -954,7 +1016,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                                         : (cv[b] == kUnseen64 && ((subp >> t) & 1ull)));
             const uint64_t mask = __ballot(me);
             if (!mask) continue;
-            const int64_t row_m = (int64_t)m * a.N;
+            const int64_t row_m = (int64_t)m * a.CN;
             const int64_t plane = (int64_t)t * a.E;
             uint64_t gm = mask & gmask;
             while (__ballot(gm != 0)) {
@@ -963,7 +1025,8 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                 const int sl = bs < 0 ? lane : bs;
                 const uint32_t beg = __shfl(rp0, sl, 64), end = __shfl(rp1, sl, 64);
                 const bool ign_s = __shfl(ign_l, sl, 64);
-                const uint32_t me_id = (uint32_t)(p0 + (bs < 0 ? 0 : bs));
+                const uint32_t me_id = (uint32_t)(a.clo + p0 + (bs < 0 ? 0 : bs));
+                const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;   // Philox keys use global ids
                 n_walk += (gl == 0 && bs >= 0);
                 // rows longer than the group are walked in W-edge chunks (wave-uniform trip count)
                 const uint32_t deg = bs >= 0 ? end - beg : 0u;
@@ -976,7 +1039,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                     // holder me_id walks its row: the peers it gossiped t to
                     if (v && a.gsel[plane + e]) {
                         const uint32_t p = a.col[e], re = a.rev[e];
-                        req = a.gstate[re] && a.cell[row_m + p] == kUnseen64;   // p's gate on i, p has not seen m
+                        req = a.gstate[re] && a.cell[row_m + (p - a.clo)] == kUnseen64;   // p's gate on i, p has not seen m
                         if (req) {
                             const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, p, 0, P_PROMISE, m, me_id);
                             atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[re]), (unsigned long long)key);
@@ -990,9 +1053,19 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                         const uint32_t re = a.rev[e];
                         if (a.gsel[plane + re] && a.gstate[e]) {
                             const uint32_t i = a.col[e];
-                            req = holds_in_window(a.cell[row_m + i], a.g, a.lo_round, tick_round, inv, i == origin);
+                            if (a.sharded) {
+                                // the advertiser's holding: its shard's bit for active slot k
+                                const uint32_t s = a.pshard[i];
+                                const uint64_t gi = (uint64_t)a.gid[i] - (uint64_t)a.bounds[s];
+                                const int64_t words = (a.bounds[s + 1] - a.bounds[s] + 63) >> 6;
+                                req = (a.hbm[a.hoff[s] + (int64_t)k * words + (int64_t)(gi >> 6)] >> (gi & 63)) & 1ull;
+                            } else {
+                                req = holds_in_window(a.cell[row_m + (i - a.clo)], a.g, a.lo_round, tick_round, inv,
+                                                      i == origin);
+                            }
                             if (req) {
-                                const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, me_id, 0, P_PROMISE, m, i);
+                                const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, me_g, 0, P_PROMISE, m,
+                                                              a.gid ? a.gid[i] : i);
                                 atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[e]), (unsigned long long)key);
                                 r = re;
                                 resp = a.respond && a.gstate[re] && !(a.behaviour[i] & GSIM_BEHAVE_IGNORE_IWANT);
@@ -1100,7 +1173,7 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
         const bool sc = tp->scored && (ds & GSIM_DS_TRACKED);
         const uint8_t tf = a.tflags[ir];
         const int64_t window = tp->mesh_message_deliveries_window_ns;
-        uint64_t* cellp = a.cell + (int64_t)m * a.N + p;
+        uint64_t* cellp = a.cell + (int64_t)m * a.CN + (p - a.clo);
         const uint64_t c = *cellp;
         const uint32_t hi = (uint32_t)(c >> 32);
         int64_t seen_round = -1;
@@ -1161,16 +1234,17 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
 // (fulfillPromise at first reception).  Record order: the penalty lands on
 // the promiser's record of the advertiser, rev[e].
 __global__ __launch_bounds__(256) void k_promise_check(uint32_t* prom_q, const uint64_t* cell, const uint32_t* owner,
-                                                       const uint32_t* rev, uint8_t* pen, int64_t E, int64_t N,
-                                                       unsigned long long* gstats)
+                                                       const uint32_t* rev, uint8_t* pen, int64_t E, int64_t CN,
+                                                       uint32_t clo, unsigned long long* gstats)
 {
+    // promises sit at the promiser's (an owned receiver's) edges only
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     unsigned long long broken = 0;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride) {
         const uint32_t slot = prom_q[e];
         if (slot == 0xFFFFFFFFu) continue;
         prom_q[e] = 0xFFFFFFFFu;
-        if (cell[(int64_t)slot * N + owner[e]] == kUnseen64) {
+        if (cell[(int64_t)slot * CN + (owner[e] - clo)] == kUnseen64) {
             pen[rev[e]] = (uint8_t)(pen[rev[e]] + 1);
             ++broken;
         }
@@ -1179,11 +1253,14 @@ __global__ __launch_bounds__(256) void k_promise_check(uint32_t* prom_q, const u
     if ((threadIdx.x & 63) == 0 && broken) atomicAdd(&gstats[3], broken);
 }
 
-__global__ void k_seen_view(const uint64_t* cell, uint32_t* out, int64_t n)
+// F_SEEN view [ring][N]: first-seen rounds of the peers with cells, unseen elsewhere
+__global__ void k_seen_view(const uint64_t* cell, uint32_t* out, int64_t n, int64_t N, int64_t CN, uint32_t clo)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += stride)
-        out[x] = (uint32_t)(cell[x] >> 32);
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += stride) {
+        const int64_t m = x / N, i = x - m * N - (int64_t)clo;
+        out[x] = (i >= 0 && i < CN) ? (uint32_t)(cell[m * CN + i] >> 32) : 0xFFFFFFFFu;
+    }
 }
 
 }  // namespace gsim
@@ -1193,6 +1270,8 @@ using namespace gsim;
 // ---------------------------------------------------------------------------
 // host side
 
+static void free_ihave_stage(Deliver* d);
+
 static void dl_free(Deliver* d)
 {
     if (!d) return;
@@ -1201,6 +1280,7 @@ static void dl_free(Deliver* d)
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
+    free_ihave_stage(d);
     delete d;
 }
 
@@ -1242,7 +1322,9 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.first = h->d_first; a.meshd = h->d_meshd; a.invalid = h->d_invalid; a.mcnt = h->d_mcnt;
     a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv;
     a.cell = d->d_cell; a.lastput = d->d_lastput;
-    a.seenbm = d->d_seenbm; a.nw = (h->n + 63) / 64; a.mpub = d->d_mpub; a.roff = d->d_roff;
+    a.CN = h->ohi() - h->olo();
+    a.clo = (uint32_t)h->olo();
+    a.seenbm = d->d_seenbm; a.nw = (a.CN + 63) / 64; a.mpub = d->d_mpub; a.roff = d->d_roff;
     const size_t w = (size_t)nnew_words(d);
     a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
     a.nnew_cur = d->d_nnew + (size_t)(g & 1) * w;
@@ -1253,6 +1335,14 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.sub = h->d_sub; a.score = h->d_score; a.rev = h->d_rev;
     a.flood = h->gp.flood_publish ? 1 : 0;
     a.pub_thr = h->th.publish_threshold;
+    if (ShardCtx* sh = h->sh) {
+        a.sharded = 1;
+        a.xr = sh->d_xr;
+        a.pshard = sh->d_pshard;
+        a.xout = sh->d_xout;
+        a.xcnt = sh->d_xcnt;
+        a.xcap = sh->xcap;
+    }
     return a;
 }
 
@@ -1286,7 +1376,8 @@ int deliver_promise_check(gsim_handle* h, int64_t now)
         if (!(expire < now)) continue;
         hipLaunchKernelGGL(k_promise_check, dim3(std::min<int64_t>((h->e + 255) / 256, 16384)), dim3(256), 0,
                            h->stream, d->d_prom + (size_t)q * (size_t)h->e, (const uint64_t*)d->d_cell,
-                           (const uint32_t*)h->d_owner, (const uint32_t*)h->d_rev, h->d_pen, h->e, h->n, d->d_gstats);
+                           (const uint32_t*)h->d_owner, (const uint32_t*)h->d_rev, h->d_pen, h->e,
+                           h->ohi() - h->olo(), (uint32_t)h->olo(), d->d_gstats);
         d->prom_made[(size_t)q] = -1;
         int rc = hip_check(h, hipGetLastError(), "k_promise_check");
         if (rc) return rc;
@@ -1304,15 +1395,27 @@ int deliver_heartbeat_begin(gsim_handle* h, uint64_t tick)
 }
 
 // Control round 0: handleIHave (+ the advertisers' handleIWant) for the
-// heartbeat's IHAVE marks.
-static int launch_ihave(gsim_handle* h, int64_t g)
+// heartbeat's IHAVE marks.  Staged so a sharded network can reduce the
+// per-slot counts and share the holders between the stages (shard.hip).
+namespace gsim {
+struct IhaveStage {
+    IhArgs a{};
+    size_t lds, lds_c;
+    int grid;
+};
+}  // namespace gsim
+
+// false: no IHAVE handling in this round
+static bool ihave_prepare(gsim_handle* h, int64_t g, IhaveStage* st, int* rc)
 {
+    *rc = GSIM_OK;
     Deliver* d = h->dl;
     const int64_t tick = g / d->cfg.rounds;
-    if (d->ihave_tick != tick) return GSIM_OK;
+    if (d->ihave_tick != tick) return false;
     d->ihave_tick = -1;
-    if (h->gp.max_ihave_messages < 1 || h->gp.max_ihave_length < 1) return GSIM_OK;
-    IhArgs a{};
+    if (h->gp.max_ihave_messages < 1 || h->gp.max_ihave_length < 1) return false;
+    IhArgs& a = st->a;
+    a = IhArgs{};
     a.N = h->n; a.E = h->e; a.T = h->t; a.ring = d->cfg.ring; a.R = d->cfg.rounds;
     a.g = g; a.tick = tick;
     a.lo_round = (int32_t)std::max<int64_t>((tick - h->gp.history_gossip) * d->cfg.rounds, 0);
@@ -1324,20 +1427,46 @@ static int launch_ihave(gsim_handle* h, int64_t g)
     a.prom_idx = (int32_t)(tick % d->prom_ticks);
     if (d->prom_made[(size_t)a.prom_idx] >= 0) {
         h->err = "IWANT promise ring index still pending (refresh_scores must run every heartbeat)";
-        return GSIM_ESTATE;
+        *rc = GSIM_ESTATE;
+        return false;
     }
     d->prom_made[(size_t)a.prom_idx] = tick;
     a.resp = d->d_resp; a.nresp = d->d_nresp; a.resp_cap = d->resp_cap; a.gstats = d->d_gstats;
     a.respond = h->gp.gossip_retransmission >= 1;
     a.seed = h->x ? gsim_get_seed(h) : 0;
-    const size_t lds = (((size_t)d->cfg.ring + 3) & ~(size_t)3) * sizeof(uint16_t) + 4 * kRespStage * sizeof(uint64_t);
-    const size_t lds_c = (((size_t)d->cfg.ring + 1) & ~(size_t)1) * sizeof(uint16_t) + 2 * (size_t)d->cfg.ring * 4;
-    const int grid = grid_peers(h->n);
-    ProfScope ps(h, GSIM_K_GOSSIP);
+    a.CN = h->ohi() - h->olo();
+    a.clo = (uint32_t)h->olo();
+    if (ShardCtx* sh = h->sh) {
+        a.sharded = 1;
+        a.gid = sh->d_gid;
+        a.pshard = sh->d_pshard;
+        a.hbm = sh->d_hbm;
+        a.hoff = sh->d_hoff;
+        a.bounds = sh->d_bounds;
+        a.slot_last = sh->d_slot_last_g;   // MAX over the shards (set by the caller)
+    }
+    st->lds = (((size_t)d->cfg.ring + 3) & ~(size_t)3) * sizeof(uint16_t) + 4 * kRespStage * sizeof(uint64_t);
+    st->lds_c = (((size_t)d->cfg.ring + 1) & ~(size_t)1) * sizeof(uint16_t) + 2 * (size_t)d->cfg.ring * 4;
+    st->grid = grid_peers(a.CN);
     hipError_t e = hipMemsetAsync(d->d_nresp, 0, 2 * sizeof(uint32_t), h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_gcount, 0, 2 * (size_t)d->cfg.ring * 4, h->stream);
-    if (e != hipSuccess) return hip_check(h, e, "gossip reset");
-    hipLaunchKernelGGL(k_gossip_count, dim3(grid), dim3(256), lds_c, h->stream, a, d->d_gcount);
+    if (e != hipSuccess) { *rc = hip_check(h, e, "gossip reset"); return false; }
+    return true;
+}
+
+// Holders and wanting receivers per slot (d_gcount), over the peers with cells.
+static int ihave_count(gsim_handle* h, IhaveStage* st)
+{
+    ProfScope ps(h, GSIM_K_GOSSIP);
+    hipLaunchKernelGGL(k_gossip_count, dim3(st->grid), dim3(256), st->lds_c, h->stream, st->a, h->dl->d_gcount);
+    return hip_check(h, hipGetLastError(), "k_gossip_count");
+}
+
+static int ihave_walk(gsim_handle* h, IhaveStage* st)
+{
+    Deliver* d = h->dl;
+    IhArgs& a = st->a;
+    ProfScope ps(h, GSIM_K_GOSSIP);
     // lane groups sized to the rows: power-law graphs (long rows, short mean) walk
     // their few long rows in chunks rather than idling 3/4 of a 64-lane group
     int w = h->ihave_w;
@@ -1346,17 +1475,26 @@ static int launch_ihave(gsim_handle* h, int64_t g)
         w = (h->max_degree <= 16 || (h->max_degree > 32 && short_mean)) ? 16 : h->max_degree <= 32 ? 32 : 64;
     }
     if (w == 16)
-        hipLaunchKernelGGL(k_ihave<16>, dim3(grid), dim3(256), lds, h->stream, a, (const uint32_t*)d->d_gcount);
+        hipLaunchKernelGGL(k_ihave<16>, dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)d->d_gcount);
     else if (w == 32)
-        hipLaunchKernelGGL(k_ihave<32>, dim3(grid), dim3(256), lds, h->stream, a, (const uint32_t*)d->d_gcount);
+        hipLaunchKernelGGL(k_ihave<32>, dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)d->d_gcount);
     else
-        hipLaunchKernelGGL(k_ihave<64>, dim3(grid), dim3(256), lds, h->stream, a, (const uint32_t*)d->d_gcount);
+        hipLaunchKernelGGL(k_ihave<64>, dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)d->d_gcount);
     hipLaunchKernelGGL(k_promise_insert, dim3(std::min<int64_t>((h->e + 255) / 256, 16384)), dim3(256), 0, h->stream,
                        d->d_pcand, d->d_prom, d->prom_ticks, a.prom_idx, h->e);
-    d->resp_round = g + 2;
+    d->resp_round = a.g + 2;
     return hip_check(h, hipGetLastError(), "k_ihave");
 }
 
+static int launch_ihave(gsim_handle* h, int64_t g)
+{
+    IhaveStage st;
+    int rc = GSIM_OK;
+    if (!ihave_prepare(h, g, &st, &rc)) return rc;
+    rc = ihave_count(h, &st);
+    if (!rc) rc = ihave_walk(h, &st);
+    return rc;
+}
 
 int deliver_flush(gsim_handle* h)
 {
@@ -1364,7 +1502,7 @@ int deliver_flush(gsim_handle* h)
     if (!d || d->pending < 0) return GSIM_OK;
     ProfScope ps(h, GSIM_K_COMMIT);
     RoundArgs a = make_round_args(h, d->pending);
-    hipLaunchKernelGGL(k_commit, dim3(grid_peers(h->n)), dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t),
+    hipLaunchKernelGGL(k_commit, dim3(grid_peers(a.CN)), dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t),
                        h->stream, a);
     d->pending = -1;
     return hip_check(h, hipGetLastError(), "k_commit");
@@ -1400,7 +1538,8 @@ int deliver_read_seen(gsim_handle* h, void* dst)
     if (!d->d_seen32) e = hipMalloc((void**)&d->d_seen32, std::max<size_t>(n * 4, 4));
     if (e != hipSuccess) return hip_check(h, e, "seen view scratch");
     hipLaunchKernelGGL(k_seen_view, dim3(std::min<int64_t>(((int64_t)n + 255) / 256, 16384)), dim3(256), 0, h->stream,
-                       (const uint64_t*)d->d_cell, d->d_seen32, (int64_t)n);
+                       (const uint64_t*)d->d_cell, d->d_seen32, (int64_t)n, h->n, h->ohi() - h->olo(),
+                       (uint32_t)h->olo());
     e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpyAsync(dst, d->d_seen32, n * 4, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
@@ -1416,10 +1555,11 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a, size_t lds)
     // 21.1 / 21.3 ms per tick at C3, profiles/r01_ab_send_tm_blocks.log), ranges of
     // at least 4096 peers
     constexpr int64_t total = 2048;
-    const int64_t ranges = std::max<int64_t>(1, std::min<int64_t>((h->n + 4095) / 4096,
+    const int64_t cn = h->ohi() - h->olo();
+    const int64_t ranges = std::max<int64_t>(1, std::min<int64_t>((cn + 4095) / 4096,
                                                                     std::max<int64_t>(1, total / std::max(1, h->t))));
-    const int32_t range = (int32_t)(((h->n + ranges - 1) / ranges + 63) & ~63ll);
-    const int64_t p = (h->n + range - 1) / range;
+    const int32_t range = (int32_t)(((cn + ranges - 1) / ranges + 63) & ~63ll);
+    const int64_t p = (cn + range - 1) / range;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_send_tm<W>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return hip_check(h, e, "k_send_tm LDS attribute");
@@ -1431,7 +1571,7 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a, size_t lds)
 // LDS of the topic-major kernel: the slot's committed bits + the slot list
 static size_t send_tm_lds(const gsim_handle* h, const Deliver* d)
 {
-    return (size_t)((h->n + 63) / 64) * 8 + (((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7);
+    return (size_t)((h->ohi() - h->olo() + 63) / 64) * 8 + (((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7);
 }
 constexpr size_t kLdsBudget = 160 * 1024 - 24 * 1024;   // minus the static frontier buffers
 
@@ -1440,6 +1580,156 @@ static void launch_send(gsim_handle* h, int grid, size_t lds, const RoundArgs& a
 {
     hipLaunchKernelGGL((k_send<W, kSlotBatch>), dim3(grid), dim3(256), lds, h->stream, a);
 }
+
+// ---- round stages (gsim_round runs them in order; a sharded group
+// exchanges copies between send and post, control records after control,
+// and the IHAVE counts / holders inside the IHAVE stage, shard.hip) --------
+
+static bool lazy_commits(const gsim_handle* h)
+{
+    // commits may trail their round only while every window is >= 0: with a
+    // negative window the first delivery's P3 credit must land before control
+    for (const auto& tp : h->tp)
+        if (tp.scored && tp.mesh_message_deliveries_window_ns < 0) return false;
+    return true;
+}
+
+int deliver_round_send(gsim_handle* h, int64_t round)
+{
+    Deliver* d = h->dl;
+    if (!d) { h->err = "gsim_msgs_init not called"; return GSIM_ESTATE; }
+    if (round < 0 || round >= 0x7FFFFFFF) { h->err = "round out of range [0, 2^31-1)"; return GSIM_ERANGE; }
+    if (d->next_round >= 0 && round != d->next_round) {
+        h->err = "rounds must be consecutive";
+        return GSIM_ESTATE;
+    }
+    if (h->max_degree > 64) {
+        h->err = "propagation kernels support rows of at most 64 connections in this build";
+        return GSIM_ERANGE;
+    }
+    int rc = 0;
+    {
+        ProfScope ps(h, GSIM_K_ACCEPT);
+        rc = refresh_accept(h);
+        if (rc) return rc;
+    }
+    // topic-major delivery when a slot's committed bits fit in LDS: the claims
+    // of round g-1 are committed first (k_commit), then k_send_tm
+    const size_t lds_tm = send_tm_lds(h, d);
+    const bool tm = h->send_variant == 3 && lds_tm <= kLdsBudget;
+    if (h->sh && !tm) {
+        h->err = "a shard's delivery needs the topic-major kernel (its owned peers' bits must fit in LDS)";
+        return GSIM_ERANGE;
+    }
+    if (tm) {
+        rc = deliver_flush(h);
+        if (rc) return rc;
+    }
+    if (h->sh) {   // the copy queues of this round
+        hipError_t e = hipMemsetAsync(h->sh->d_xcnt, 0, sizeof(uint32_t) * (size_t)h->sh->K, h->stream);
+        if (e != hipSuccess) return hip_check(h, e, "copy queue reset");
+    }
+    RoundArgs a = make_round_args(h, round);
+    h->mcnt_dirty = true;
+    const size_t lds = (((size_t)d->cfg.ring + 1) & ~(size_t)1) * sizeof(uint16_t) + (size_t)nnew_words(d) * 4;
+    {
+        ProfScope ps(h, GSIM_K_SEND);
+        const int grid = grid_peers(h->n);
+        if (tm) {
+            if (h->max_degree <= 16)
+                rc = launch_send_tm<16>(h, a, lds_tm);
+            else if (h->max_degree <= 32)
+                rc = launch_send_tm<32>(h, a, lds_tm);
+            else
+                rc = launch_send_tm<64>(h, a, lds_tm);
+            if (rc) return rc;
+        } else if (h->max_degree <= 16)
+            launch_send<16>(h, grid, lds, a);
+        else if (h->max_degree <= 32)
+            launch_send<32>(h, grid, lds, a);
+        else
+            launch_send<64>(h, grid, lds, a);
+        // the claims of round g-1 were committed by k_send; round g+1's bits
+        // were last read (as "previous") by round g
+        d->pending = round;
+        hipError_t e = hipMemsetAsync(d->d_nnew + (size_t)((round + 1) & 1) * (size_t)nnew_words(d), 0,
+                                      (size_t)nnew_words(d) * 4, h->stream);
+        if (e != hipSuccess) return hip_check(h, e, "nnew reset");
+    }
+    return hip_check(h, hipGetLastError(), "k_send");
+}
+
+// Copies arriving in round g at this handle's peers, one entry per copy:
+// the receiver's record of the sender | slot << 32 (the IWANT responses, and
+// a shard's copies from other shards).  *d_n entries, at most cap.
+int deliver_round_queue(gsim_handle* h, int64_t round, const uint64_t* q, const uint32_t* d_n, int64_t cap)
+{
+    Deliver* d = h->dl;
+    RoundArgs a = make_round_args(h, round);
+    const size_t lds2 = (size_t)nnew_words(d) * 4;
+    hipLaunchKernelGGL(k_gossip_deliver, dim3(2048), dim3(256), lds2, h->stream, a, q, d_n,
+                       (const uint32_t*)h->d_owner, cap);
+    return hip_check(h, hipGetLastError(), "k_gossip_deliver");
+}
+
+int deliver_round_post(gsim_handle* h, int64_t round)
+{
+    Deliver* d = h->dl;
+    int rc = GSIM_OK;
+    if (d->resp_round == round) {
+        // the messages handleIWant sent in control round 1 arrive with this round's copies
+        ProfScope ps(h, GSIM_K_GOSSIP);
+        rc = deliver_round_queue(h, round, d->d_resp, d->d_nresp, d->resp_cap);
+        d->resp_round = -1;
+        if (rc) return rc;
+    }
+    if (!lazy_commits(h)) rc = deliver_flush(h);
+    return rc;
+}
+
+int deliver_round_control(gsim_handle* h, int64_t round)
+{
+    Deliver* d = h->dl;
+    const int32_t r = (int32_t)(round % d->cfg.rounds);
+    // rounds >= 2 of a heartbeat have an empty control inbox: handling PRUNE
+    // replies (round 1) emits nothing
+    if (r >= 2) return GSIM_OK;
+    RoundArgs a = make_round_args(h, round);
+    return handle_control(h, r, a.now);
+}
+
+// The IHAVE stage of round g (control round 0) for a sharded group: prepare
+// and count (the caller then reduces d_gcount over the shards and fills the
+// holder bitmaps), then walk.  d_slot_last_g must hold the reduced slot_last.
+static void free_ihave_stage(Deliver* d)
+{
+    delete d->ih;
+    d->ih = nullptr;
+}
+
+int deliver_ihave_count(gsim_handle* h, int64_t g, bool* run)
+{
+    Deliver* d = h->dl;
+    delete d->ih;
+    d->ih = new IhaveStage();
+    int rc = GSIM_OK;
+    *run = g % d->cfg.rounds == 0 && ihave_prepare(h, g, d->ih, &rc);
+    if (!*run) { delete d->ih; d->ih = nullptr; return rc; }
+    return ihave_count(h, d->ih);
+}
+
+int deliver_ihave_walk(gsim_handle* h)
+{
+    Deliver* d = h->dl;
+    if (!d->ih) return GSIM_OK;
+    const int rc = ihave_walk(h, d->ih);
+    delete d->ih;
+    d->ih = nullptr;
+    return rc;
+}
+
+uint32_t* deliver_gcount(gsim_handle* h) { return h->dl ? h->dl->d_gcount : nullptr; }
+int32_t* deliver_slot_last(gsim_handle* h) { return h->dl ? h->dl->d_slot_last : nullptr; }
 
 extern "C" {
 
@@ -1467,6 +1757,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     Deliver* d = new Deliver();
     d->cfg = *cfg;
     const size_t ring = (size_t)cfg->ring, N = (size_t)h->n, T = (size_t)std::max(1, h->t);
+    const size_t CN = (size_t)(h->ohi() - h->olo());   // peers with seen-set cells (a shard's owned peers)
     const size_t words = (size_t)nnew_words(d);
     hipError_t e = hipSuccess;
     auto A = [&](void** p, size_t bytes) {
@@ -1476,8 +1767,8 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_mtopic, ring * 4);
     A((void**)&d->d_morigin, ring * 4);
     A((void**)&d->d_minv, ring);
-    A((void**)&d->d_cell, ring * N * 8);
-    A((void**)&d->d_seenbm, ring * ((N + 63) / 64) * 8);
+    A((void**)&d->d_cell, ring * CN * 8);
+    A((void**)&d->d_seenbm, ring * ((CN + 63) / 64) * 8);
     A((void**)&d->d_mpub, ring * 4);
     A((void**)&d->d_roff, (size_t)cfg->rounds * 8);
     A((void**)&d->d_lastput, T * N * 4);
@@ -1508,8 +1799,8 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
         return e == hipErrorOutOfMemory ? GSIM_ENOMEM : GSIM_EDEVICE;
     }
     h->dl = d;
-    e = hipMemsetAsync(d->d_cell, 0xFF, ring * N * 8, h->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(d->d_seenbm, 0, ring * ((N + 63) / 64) * 8, h->stream);
+    e = hipMemsetAsync(d->d_cell, 0xFF, ring * CN * 8, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_seenbm, 0, ring * ((CN + 63) / 64) * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_mpub, 0, ring * 4, h->stream);
     if (e == hipSuccess) {
         std::vector<int64_t> roff((size_t)cfg->rounds);
@@ -1573,7 +1864,7 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
     ProfScope ps(h, GSIM_K_PUBLISH);
     RoundArgs a = make_round_args(h, round);
     const int64_t per_block = 256 * 16;
-    const int gx = (int)std::min<int64_t>((h->n + per_block - 1) / per_block, 1024);
+    const int gx = (int)std::min<int64_t>((h->ohi() - h->olo() + per_block - 1) / per_block, 1024);
     hipLaunchKernelGGL(k_reset_slots, dim3(std::max(gx, 1), count), dim3(256), 0, h->stream, a,
                        (const gsim_msg*)d->d_pub, count);
     hipLaunchKernelGGL(k_publish, dim3((count + 255) / 256), dim3(256), 0, h->stream, a,
@@ -1589,91 +1880,14 @@ int gsim_round(gsim_handle* h, int64_t round)
 {
     if (!h) return GSIM_EINVAL;
     if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
-    Deliver* d = h->dl;
-    if (!d) { h->err = "gsim_msgs_init not called"; return GSIM_ESTATE; }
-    if (round < 0 || round >= 0x7FFFFFFF) { h->err = "round out of range [0, 2^31-1)"; return GSIM_ERANGE; }
-    if (d->next_round >= 0 && round != d->next_round) {
-        h->err = "rounds must be consecutive";
-        return GSIM_ESTATE;
-    }
-    if (h->max_degree > 64) {
-        h->err = "propagation kernels support rows of at most 64 connections in this build";
-        return GSIM_ERANGE;
-    }
-    int rc = 0;
-    {
-        ProfScope ps(h, GSIM_K_ACCEPT);
-        rc = refresh_accept(h);
-        if (rc) return rc;
-    }
-    // commits may trail their round only while every window is >= 0: with a
-    // negative window the first delivery's P3 credit must land before control
-    bool lazy = true;
-    for (const auto& tp : h->tp)
-        if (tp.scored && tp.mesh_message_deliveries_window_ns < 0) lazy = false;
-    // topic-major delivery when a slot's committed bits fit in LDS: the claims
-    // of round g-1 are committed first (k_commit), then k_send_tm
-    const size_t lds_tm = send_tm_lds(h, d);
-    const bool tm = h->send_variant == 3 && lds_tm <= kLdsBudget;
-    if (tm) {
-        rc = deliver_flush(h);
-        if (rc) return rc;
-    }
-    RoundArgs a = make_round_args(h, round);
-    h->mcnt_dirty = true;
-    const size_t lds = (((size_t)d->cfg.ring + 1) & ~(size_t)1) * sizeof(uint16_t) + (size_t)nnew_words(d) * 4;
-    {
-        ProfScope ps(h, GSIM_K_SEND);
-        const int grid = grid_peers(h->n);
-        if (tm) {
-            if (h->max_degree <= 16)
-                rc = launch_send_tm<16>(h, a, lds_tm);
-            else if (h->max_degree <= 32)
-                rc = launch_send_tm<32>(h, a, lds_tm);
-            else
-                rc = launch_send_tm<64>(h, a, lds_tm);
-            if (rc) return rc;
-        } else if (h->max_degree <= 16)
-            launch_send<16>(h, grid, lds, a);
-        else if (h->max_degree <= 32)
-            launch_send<32>(h, grid, lds, a);
-        else
-            launch_send<64>(h, grid, lds, a);
-        // the claims of round g-1 were committed by k_send; round g+1's bits
-        // were last read (as "previous") by round g
-        d->pending = round;
-        hipError_t e = hipMemsetAsync(d->d_nnew + (size_t)((round + 1) & 1) * (size_t)nnew_words(d), 0,
-                                      (size_t)nnew_words(d) * 4, h->stream);
-        if (e != hipSuccess) return hip_check(h, e, "nnew reset");
-    }
-    rc = hip_check(h, hipGetLastError(), "k_send");
+    if (h->sh) { h->err = "a shard's rounds run through its group (gsim_group_round)"; return GSIM_ESTATE; }
+    int rc = deliver_round_send(h, round);
+    if (!rc) rc = deliver_round_post(h, round);
+    if (!rc) rc = deliver_round_control(h, round);
     if (rc) return rc;
-    if (d->resp_round == round) {
-        // the messages handleIWant sent in control round 1 arrive with this round's copies
-        ProfScope ps(h, GSIM_K_GOSSIP);
-        const size_t lds2 = (size_t)nnew_words(d) * 4;
-        hipLaunchKernelGGL(k_gossip_deliver, dim3(2048), dim3(256), lds2, h->stream, a, (const uint64_t*)d->d_resp,
-                           (const uint32_t*)d->d_nresp, (const uint32_t*)h->d_owner, d->resp_cap);
-        d->resp_round = -1;
-        rc = hip_check(h, hipGetLastError(), "k_gossip_deliver");
-        if (rc) return rc;
-    }
-    if (!lazy) {
-        rc = deliver_flush(h);
-        if (rc) return rc;
-    }
-    const int32_t r = (int32_t)(round % d->cfg.rounds);
-    if (r < 2) {
-        // rounds >= 2 of a heartbeat have an empty control inbox: handling
-        // PRUNE replies (round 1) emits nothing
-        rc = gsim_handle_control(h, r, a.now);
-        if (rc) return rc;
-    }
-    if (r == 0) {
-        rc = launch_ihave(h, round);
-        if (rc) return rc;
-    }
-    d->next_round = round + 1;
+    if (round % h->dl->cfg.rounds == 0) rc = launch_ihave(h, round);
+    if (rc) return rc;
+    h->dl->next_round = round + 1;
     return GSIM_OK;
 }
 

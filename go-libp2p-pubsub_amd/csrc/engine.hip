@@ -37,6 +37,10 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
     if (a.gate && *a.gate == 0) return;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
+        if (a.sharded) {   // a record of a ghost observer belongs to another shard
+            const uint32_t o = a.col[e];
+            if (o < a.olo || o >= a.ohi) continue;
+        }
         const uint8_t st = a.estate[e];
         if (!(st & GSIM_ES_TRACKED)) {
             if (SCORE) a.score[e] = 0.0;
@@ -184,9 +188,10 @@ __global__ __launch_bounds__(256) void k_ip_colocation(ColocArgs a)
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
         const uint32_t r = a.rev[e];
+        const uint32_t i = a.owner[e];
+        if (a.sharded && (i < a.olo || i >= a.ohi)) continue;   // a ghost observer's row is partial
         double res = 0.0;
         if (a.key[e] != kIpUntracked) {
-            const uint32_t i = a.owner[e];
             const uint32_t b = a.row_ptr[i], en = a.row_ptr[i + 1];
             const uint32_t j = a.col[e];
             for (uint32_t q = a.ip_ptr[j]; q < a.ip_ptr[j + 1]; ++q) {
@@ -243,12 +248,15 @@ __global__ __launch_bounds__(256) void k_apply_mcnt(ScoreArgs a)
 // membership (probability D/k), activation, graft time and the four counters.
 __global__ __launch_bounds__(256) void k_fill_synthetic(ScoreArgs a, uint64_t seed, double p_mesh)
 {
-    // thread per observer edge e; its record lives at r = rev[e]
+    // thread per observer edge e of the owned rows; its record lives at r =
+    // rev[e].  The draws are keyed by the global edge index, so a sharded
+    // network gets the same state as the whole one.
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     const double inv = 1.0 / 4294967296.0;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
+    for (int64_t e = a.e_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.e_hi; e += stride) {
         const int64_t r = a.rev[e];
+        const int64_t ge = a.geid_base + (e - a.e_lo);
         // topics both endpoints joined: only there can a mesh link or
         // deliveries exist (owner[e] = observer, owner[r] = neighbour)
         const uint64_t shared = a.sub ? a.sub[a.owner[e]] & a.sub[a.owner[r]] : ~0ull;
@@ -260,8 +268,9 @@ __global__ __launch_bounds__(256) void k_fill_synthetic(ScoreArgs a, uint64_t se
                 a.first[ir] = 0.0; a.meshd[ir] = 0.0; a.fail[ir] = 0.0; a.invalid[ir] = 0.0;
                 continue;
             }
-            const u32x4 x = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), 0x5eed, 1, k0, k1);
-            const u32x4 q = philox4x32_10((uint32_t)i, (uint32_t)(i >> 32), 0x5eed, 2, k0, k1);
+            const int64_t gi = (int64_t)t * a.E_glob + ge;
+            const u32x4 x = philox4x32_10((uint32_t)gi, (uint32_t)(gi >> 32), 0x5eed, 1, k0, k1);
+            const u32x4 q = philox4x32_10((uint32_t)gi, (uint32_t)(gi >> 32), 0x5eed, 2, k0, k1);
             const bool in_mesh = x.x * inv < p_mesh;
             uint8_t fl = in_mesh ? GSIM_TF_IN_MESH : 0;
             if (in_mesh && (x.y & 15) != 0) fl |= GSIM_TF_ACTIVE;
@@ -275,7 +284,7 @@ __global__ __launch_bounds__(256) void k_fill_synthetic(ScoreArgs a, uint64_t se
             a.fail[ir] = (q.z & 7) == 0 ? (double)(q.z % 4000u) * 0.125 : 0.0;
             a.invalid[ir] = (q.w & 511) == 0 ? (double)(q.w % 64u) * 0.125 : 0.0;
         }
-        const u32x4 b = philox4x32_10((uint32_t)e, (uint32_t)(e >> 32), 0x5eed, 3, k0, k1);
+        const u32x4 b = philox4x32_10((uint32_t)ge, (uint32_t)(ge >> 32), 0x5eed, 3, k0, k1);
         a.bp[r] = (b.x & 15) == 0 ? (double)(b.y % 100u) * 0.125 : 0.0;
         a.estate[r] = GSIM_ES_TRACKED | GSIM_ES_CONNECTED;
         a.expire[r] = 0;
@@ -289,6 +298,7 @@ __global__ __launch_bounds__(256) void k_census(ScoreArgs a, unsigned long long*
     unsigned long long c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
+        if (a.sharded && (a.col[e] < a.olo || a.col[e] >= a.ohi)) continue;   // another shard's record
         const uint8_t st = a.estate[e];
         if (!(st & GSIM_ES_TRACKED)) continue;
         c[7] += 1;
@@ -306,8 +316,8 @@ __global__ __launch_bounds__(256) void k_census(ScoreArgs a, unsigned long long*
             c[5] += a.invalid[i] != 0.0;
         }
     }
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
-        if (!(a.rstate[e] & GSIM_ES_CONNECTED)) continue;   // router mesh links (edge order)
+    for (int64_t e = a.e_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.e_hi; e += stride) {
+        if (!(a.rstate[e] & GSIM_ES_CONNECTED)) continue;   // router mesh links (edge order), owned rows
         for (int32_t t = 0; t < a.T; ++t)
             c[6] += (a.mflags[(int64_t)t * a.E + e] & GSIM_TF_MESH) != 0;
     }
@@ -468,6 +478,13 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     a.bp = h->d_bp; a.pen = h->d_pen; a.estate = h->d_estate; a.expire = h->d_expire; a.p6 = h->d_p6; a.score = h->d_score;
     a.now = now;
     a.purged = h->d_flags;
+    a.sharded = h->sh ? 1 : 0;
+    a.olo = (uint32_t)h->olo();
+    a.ohi = (uint32_t)h->ohi();
+    a.e_lo = h->sh ? h->sh->own_e_lo : 0;
+    a.e_hi = h->sh ? h->sh->own_e_hi : h->e;
+    a.geid_base = h->sh ? h->sh->geid_base : 0;
+    a.E_glob = h->sh ? h->sh->E_global : h->e;
     return a;
 }
 
@@ -479,6 +496,9 @@ int launch_ip_colocation(gsim_handle* h, const int32_t* gate)
     c.E = h->e; c.row_ptr = h->d_row_ptr; c.col = h->d_col; c.rev = h->d_rev; c.owner = h->d_owner;
     c.ip_ptr = h->d_ip_ptr; c.ip_ids = h->d_ip_ids; c.ip_white = h->has_white ? h->d_ip_white : nullptr;
     c.estate = h->d_estate; c.p6 = h->d_p6; c.thr = h->pp.ip_colocation_factor_threshold;
+    c.sharded = h->sh ? 1 : 0;
+    c.olo = (uint32_t)h->olo();
+    c.ohi = (uint32_t)h->ohi();
     if (!h->d_ipkey) {
         const int rc = dalloc(h, &h->d_ipkey, h->e);
         if (rc) return rc;

@@ -39,6 +39,12 @@ struct ScoreArgs {
     const int32_t* gate;       // non-null: run only if *gate != 0 (a retention purge happened)
     const uint32_t* col;       // col[r]: the observer of record r (record order)
     int32_t skip_unjoined;     // records of topics the observer did not join are zero: skip them
+    // sharded network: only records whose observer is owned
+    // ([olo, ohi)) are this shard's; the owned rows are local edges [e_lo, e_hi),
+    // global edge index geid_base + (e - e_lo) of E_glob
+    int32_t sharded;
+    uint32_t olo, ohi;
+    int64_t e_lo, e_hi, geid_base, E_glob;
 };
 
 struct ColocArgs {
@@ -50,6 +56,8 @@ struct ColocArgs {
     int32_t thr;
     const int32_t* gate;       // non-null: run only if *gate != 0 (a retention purge happened)
     uint32_t* key;             // [E] per-edge IP key of the row member (k_ip_keys)
+    int32_t sharded;           // only owned observers ([olo, ohi)) get P6
+    uint32_t olo, ohi;
 };
 
 // meshMessageDeliveries increments from message delivery are kept as a
@@ -115,6 +123,50 @@ struct FieldRef {
 };
 
 struct Deliver;   // message ring, seen-set and round lists (deliver.hip)
+
+// A shard of a graph-sharded network (shard.hip): which local
+// peers / edges the handle owns and the device side of the halo exchange.
+// A handle without one owns every peer (sh == nullptr).
+struct ShardCtx {
+    int32_t k = 0, K = 1;
+    int64_t own_lo = 0, own_hi = 0;        // owned local peers
+    int64_t own_e_lo = 0, own_e_hi = 0;    // local edges of the owned rows
+    int64_t N_global = 0, E_global = 0;
+    int64_t geid_base = 0;                 // global edge index of own_e_lo
+    std::vector<int64_t> bounds;           // [K+1] global peer ranges
+    std::vector<int64_t> lpeer;            // [K+1] local ids of each shard's peers
+    std::vector<int64_t> gbase, gcnt;      // [K] ghost rows of shard s's peers (local edges)
+    std::vector<int64_t> xoff;             // [K+1] cross-out lists, concatenated (d_xgather)
+    uint32_t* d_gid = nullptr;             // [n] global id of each local peer
+    uint8_t* d_pshard = nullptr;           // [n] shard of each local peer
+    uint32_t* d_xr = nullptr;              // [e] owned-row cross edge: the receiver shard's record index
+    uint32_t* d_ymap = nullptr;            // [e] ghost-row edge: the owner shard's owned-row edge index
+    uint32_t* d_xgather = nullptr;         // [n_cross] cross-out lists (local edge indices)
+    int64_t* d_bounds = nullptr;           // [K+1] device copy of bounds
+    // per-round halo buffers (allocated by gsim_group_msgs_init)
+    uint64_t* d_xout = nullptr;            // [K][xcap] outbound copies: record index there | slot << 32
+    uint32_t* d_xcnt = nullptr;            // [K] outbound copy counts
+    int64_t xcap = 0;
+    uint64_t* d_xin = nullptr;             // inbound copies (every source, concatenated)
+    int64_t xin_cap = 0;
+    uint32_t* d_xin_n = nullptr;           // [1] inbound count (k_gossip_deliver's queue length)
+    uint64_t* d_cout = nullptr;            // [K][ccap] outbound control entries: edge | topic << 32 | bits << 40
+    uint32_t* d_ccnt = nullptr;            // [K]
+    int64_t ccap = 0;
+    uint64_t* d_cin = nullptr;             // inbound control entries
+    int64_t cin_cap = 0;
+    uint64_t* d_gout = nullptr;            // [n_cross] gossip marks out: topic mask of gsel
+    uint8_t* d_gsout = nullptr;            // [n_cross] gstate out
+    uint64_t* d_gin = nullptr;             // [e] gossip marks in (ghost-row positions)
+    uint8_t* d_gsin = nullptr;             // [e]
+    int32_t* d_slot_last_g = nullptr;      // [ring] slot_last, MAX over shards
+    uint32_t* d_act = nullptr;             // [ring] active IHAVE slots (same list on every shard)
+    uint64_t* d_hbm = nullptr;             // holder bits of every shard's peers per active slot
+    int64_t hbm_cap = 0;                   // words
+    int64_t* d_hoff = nullptr;             // [K] word offset of each shard's block in d_hbm
+    std::vector<int32_t> act;              // host copy of the active slots
+    uint32_t* h_counts = nullptr;          // pinned scratch for count readbacks
+};
 
 }  // namespace gsim
 
@@ -201,6 +253,11 @@ struct gsim_handle {
     // heartbeat state lives in heartbeat.hip, message propagation in deliver.hip
     struct Extra* x = nullptr;
     gsim::Deliver* dl = nullptr;
+    gsim::ShardCtx* sh = nullptr;   // graph-sharded network: this handle is one shard (shard.hip)
+
+    // owned peers / observer rows (all of them unless sharded)
+    int64_t olo() const { return sh ? sh->own_lo : 0; }
+    int64_t ohi() const { return sh ? sh->own_hi : n; }
 };
 
 int hip_check(gsim_handle* h, hipError_t e, const char* what);
@@ -255,3 +312,14 @@ int deliver_heartbeat_begin(gsim_handle* h, uint64_t tick); // fresh IHAVE marks
 uint64_t gsim_get_seed(const gsim_handle* h);              // heartbeat.hip
 int deliver_read_seen(gsim_handle* h, void* dst);
 int deliver_check_errors(gsim_handle* h);             // queue overflow / early slot reuse of the last tick
+int handle_control(gsim_handle* h, int32_t round, int64_t now);   // heartbeat.hip: k_handle_control
+// round stages (deliver.hip; gsim_round runs them in order, a sharded group
+// exchanges between them, shard.hip)
+int deliver_round_send(gsim_handle* h, int64_t round);
+int deliver_round_queue(gsim_handle* h, int64_t round, const uint64_t* q, const uint32_t* d_n, int64_t cap);
+int deliver_round_post(gsim_handle* h, int64_t round);
+int deliver_round_control(gsim_handle* h, int64_t round);
+int deliver_ihave_count(gsim_handle* h, int64_t g, bool* run);
+int deliver_ihave_walk(gsim_handle* h);
+uint32_t* deliver_gcount(gsim_handle* h);             // [2][ring] holders / wanting receivers per slot
+int32_t* deliver_slot_last(gsim_handle* h);           // [ring]

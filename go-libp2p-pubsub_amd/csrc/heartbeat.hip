@@ -75,6 +75,10 @@ struct HbArgs {
     uint64_t* fan_topics;      // [N]
     double pub_thr;
     int64_t fanout_ttl;
+    // sharded network: observers / receivers [olo, ohi) are
+    // this shard's; selection keys use global peer ids (gid, nullptr: local = global)
+    const uint32_t* gid;
+    uint32_t olo, ohi;
 };
 
 namespace {
@@ -130,6 +134,9 @@ __device__ __forceinline__ uint32_t group_min_u32(uint32_t v, int grp)
         }
     }
 }
+
+// The global id of a local peer: selection keys are those of the whole network.
+__device__ __forceinline__ uint32_t glob(const HbArgs& a, uint32_t p) { return a.gid ? a.gid[p] : p; }
 
 __device__ __forceinline__ uint64_t hb_key(const HbArgs& a, uint32_t obs, int32_t t, uint32_t purpose, uint32_t col,
                                            uint32_t pos)
@@ -355,24 +362,26 @@ __device__ bool gossip_targets(const HbArgs& a, bool cand, bool tpeer, uint32_t 
 // group, shuffles read the group's own lanes, and branches diverge only
 // between whole groups (group_min_u32 is group-local).
 //
-// rows: the observers of one row-length class (a list), or nullptr for all N.
+// rows: the observers of one row-length class (a list), or nullptr for the
+// nrows observers from obs_base on.
 template <int W>
-__global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* rows, int64_t nrows)
+__global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* rows, int64_t nrows, int64_t obs_base)
 {
     constexpr int G = 64 / W;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int grp = lane / W, gl = lane % W, base = grp * W;
     const uint64_t gm = W == 64 ? ~0ull : (((1ull << W) - 1) << base);
-    const int64_t nobs = rows ? nrows : a.N;
+    const int64_t nobs = nrows;
     for (int64_t o0 = ((int64_t)blockIdx.x * 4 + wid) * G; o0 < nobs; o0 += (int64_t)gridDim.x * 4 * G) {
         const bool ovalid = o0 + grp < nobs;
-        const int64_t obs = !ovalid ? 0 : rows ? (int64_t)rows[o0 + grp] : o0 + grp;
+        const int64_t obs = !ovalid ? 0 : rows ? (int64_t)rows[o0 + grp] : obs_base + o0 + grp;
         const uint32_t b = ovalid ? a.row_ptr[obs] : 0u;
         const int deg = ovalid ? (int)(a.row_ptr[obs + 1] - b) : 0;
         const bool valid = gl < deg;
         const uint32_t e = b + (uint32_t)gl;
         const uint32_t col = valid ? a.col[e] : 0u;
         const uint32_t rv = valid ? a.rev[e] : 0u;           // this observer's record of col
+        const uint32_t gobs = ovalid ? glob(a, (uint32_t)obs) : 0u, gcol = valid ? glob(a, col) : 0u;
         const uint8_t est = valid ? a.estate[rv] : 0;
         const bool tracked = est & GSIM_ES_TRACKED;
         const bool conn = valid && (a.rstate[e] & GSIM_ES_CONNECTED);
@@ -471,14 +480,14 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* row
             if (l < a.Dlo) {
                 need_bo();
                 const bool cand = tpeer && !m && bo == 0 && !dir && S >= 0;
-                if (select_smallest<W>(a, cand, a.D - l, (uint32_t)obs, t, P_GRAFT_DLO, col, pos, gm, grp)) graft();
+                if (select_smallest<W>(a, cand, a.D - l, gobs, t, P_GRAFT_DLO, gcol, pos, gm, grp)) graft();
             }
 
             // too many peers: keep Dscore best + random, Dout outbound (1429-1490)
             l = __popcll(ballot(m) & gm);
             if (l > a.Dhi) {
                 const uint64_t mm = ballot(m) & gm;
-                const uint64_t k1 = m ? hb_key(a, (uint32_t)obs, t, P_PRUNE_SHUF1, col, pos) : ~0ull;
+                const uint64_t k1 = m ? hb_key(a, gobs, t, P_PRUNE_SHUF1, gcol, pos) : ~0ull;
                 int rank1 = 0;
                 for (int q = base; q < base + W; ++q) {
                     const double sq = __shfl(S, q, 64);
@@ -487,7 +496,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* row
                 }
                 const int ds = a.Dscore < l ? a.Dscore : l;
                 const bool tail = m && rank1 >= ds;
-                const uint64_t k2 = tail ? hb_key(a, (uint32_t)obs, t, P_PRUNE_SHUF2, col, pos) : ~0ull;
+                const uint64_t k2 = tail ? hb_key(a, gobs, t, P_PRUNE_SHUF2, gcol, pos) : ~0ull;
                 // every lane takes part in the shuffles (a shuffle inside a
                 // divergent branch would read inactive lanes)
                 int below = 0;
@@ -529,7 +538,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* row
                 if (ob < a.Dout) {
                     need_bo();
                     const bool cand = tpeer && !m && bo == 0 && !dir && outb && S >= 0;
-                    if (select_smallest<W>(a, cand, a.Dout - ob, (uint32_t)obs, t, P_GRAFT_DOUT, col, pos, gm, grp))
+                    if (select_smallest<W>(a, cand, a.Dout - ob, gobs, t, P_GRAFT_DOUT, gcol, pos, gm, grp))
                         graft();
                 }
             }
@@ -548,7 +557,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* row
                 if (median < a.opp_threshold) {
                     need_bo();
                     const bool cand = tpeer && !m && bo == 0 && !dir && S > median;
-                    if (select_smallest<W>(a, cand, a.opp_peers, (uint32_t)obs, t, P_GRAFT_OPP, col, pos, gm, grp))
+                    if (select_smallest<W>(a, cand, a.opp_peers, gobs, t, P_GRAFT_OPP, gcol, pos, gm, grp))
                         graft();
                 }
             }
@@ -577,7 +586,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* row
                         dirty = false;
                     }
                     const bool gcand = tpeer && !m && !dir && S_live >= a.gossip_thr;
-                    gsel = gossip_targets<W>(a, gcand, tpeer, (uint32_t)obs, t, col, pos, gm, grp);
+                    gsel = gossip_targets<W>(a, gcand, tpeer, gobs, t, gcol, pos, gm, grp);
                 }
                 if (valid) a.gsel[i] = gsel ? 1 : 0;
             }
@@ -603,7 +612,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* row
 __global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
 {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int64_t obs = (int64_t)blockIdx.x * 4 + wid; obs < a.N; obs += (int64_t)gridDim.x * 4) {
+    for (int64_t obs = a.olo + (int64_t)blockIdx.x * 4 + wid; obs < a.ohi; obs += (int64_t)gridDim.x * 4) {
         const int64_t lpub = lane < a.T ? a.lastpub[obs * a.T + lane] : 0;
         const uint64_t expired = __ballot(lpub != 0 && lpub + a.fanout_ttl < a.now);
         const uint64_t fant0 = a.fan_topics[obs];
@@ -626,6 +635,7 @@ __global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
         if (!fant) continue;
         const uint32_t col = valid ? a.col[e] : 0u;
         const uint32_t rv = valid ? a.rev[e] : 0u;
+        const uint32_t gobs = glob(a, (uint32_t)obs), gcol = valid ? glob(a, col) : 0u;
         const bool conn = valid && (a.rstate[e] & GSIM_ES_CONNECTED);
         const bool dir = valid && a.direct[e];
         const double S = valid ? a.score[rv] : 0.0;
@@ -642,7 +652,7 @@ __global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
             const int have = __popcll(ballot(inf));
             if (have < a.D) {
                 const bool cand = tpeer && !inf && !dir && S >= a.pub_thr;
-                if (select_smallest(a, cand, a.D - have, (uint32_t)obs, t, P_FANOUT, col, (uint32_t)lane)) inf = true;
+                if (select_smallest(a, cand, a.D - have, gobs, t, P_FANOUT, gcol, (uint32_t)lane)) inf = true;
             }
             const uint8_t nf = inf ? (uint8_t)(fl | GSIM_TF_FANOUT) : (uint8_t)(fl & ~GSIM_TF_FANOUT);
             if (valid && nf != fl) a.mflags[i] = nf;
@@ -654,7 +664,7 @@ __global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
                     have_live = true;
                 }
                 const bool gcand = tpeer && !inf && !dir && S_live >= a.gossip_thr;
-                gsel = gossip_targets(a, gcand, tpeer, (uint32_t)obs, t, col, (uint32_t)lane);
+                gsel = gossip_targets(a, gcand, tpeer, gobs, t, gcol, (uint32_t)lane);
             }
             if (valid) a.gsel[i] = gsel ? 1 : 0;
         }
@@ -669,7 +679,7 @@ __global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
 __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
 {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int64_t rcv = (int64_t)blockIdx.x * 4 + wid; rcv < a.N; rcv += (int64_t)gridDim.x * 4) {
+    for (int64_t rcv = a.olo + (int64_t)blockIdx.x * 4 + wid; rcv < a.ohi; rcv += (int64_t)gridDim.x * 4) {
         const uint32_t b = a.row_ptr[rcv];
         const int deg = (int)(a.row_ptr[rcv + 1] - b);
         const bool valid = lane < deg;
@@ -832,6 +842,7 @@ __global__ __launch_bounds__(256) void k_churn_apply(HbArgs a, ChurnArgs c)
     if (q >= c.n2) return;
     const uint32_t e = c.edges[q];
     const uint32_t r = a.rev[e];
+    if (a.col[r] < a.olo || a.col[r] >= a.ohi) return;   // the other shard handles a ghost observer's side
     // the observer's (col[r]) joined topics while unjoined records are known zero:
     // a store to them would write the value already there.  Random 1-8 B stores
     // are the churn's bound, so the router planes below are also stored only
@@ -891,6 +902,7 @@ __global__ __launch_bounds__(256) void k_fanout_publish(HbArgs a, const gsim_msg
     if (k >= count) return;                                   // wave-uniform
     const uint32_t o = pub[k].origin;
     const int32_t t = (int32_t)pub[k].topic;
+    if (o < a.olo || o >= a.ohi) return;                      // published on another shard
     if ((a.sub[o] >> t) & 1ull) return;                       // joined: it publishes to its mesh
     bool dup = false;
     for (int32_t q = lane; q < k; q += 64) dup |= pub[q].origin == o && (int32_t)pub[q].topic == t;
@@ -908,7 +920,8 @@ __global__ __launch_bounds__(256) void k_fanout_publish(HbArgs a, const gsim_msg
         const bool tpeer = conn && ((a.sub[col] >> t) & 1ull);
         const double S = valid ? a.score[a.rev[e]] : 0.0;
         const bool cand = tpeer && !(fl & GSIM_TF_FANOUT) && !(valid && a.direct[e]) && S >= a.pub_thr;
-        const bool sel = select_smallest(a, cand, a.D, o, t, P_FANOUT_NEW, col, (uint32_t)lane);
+        const bool sel = select_smallest(a, cand, a.D, glob(a, o), t, P_FANOUT_NEW, valid ? glob(a, col) : 0u,
+                                         (uint32_t)lane);
         if (valid && sel) a.mflags[i] = (uint8_t)(fl | GSIM_TF_FANOUT);
         const bool any = __ballot(sel) != 0;
         if (lane == 0 && any) atomicOr(reinterpret_cast<unsigned long long*>(a.fan_topics + o), 1ull << t);
@@ -948,7 +961,7 @@ int alloc_extra(gsim_handle* h)
     if (e != hipSuccess) return hip_check(h, e, "row_ptr readback");
     uint32_t md = 0;
     std::vector<uint32_t> cls[3];
-    for (int64_t i = 0; i < h->n; ++i) {
+    for (int64_t i = h->olo(); i < h->ohi(); ++i) {
         const uint32_t d = rp[(size_t)i + 1] - rp[(size_t)i];
         md = std::max(md, d);
         cls[d <= 16 ? 0 : d <= 32 ? 1 : 2].push_back((uint32_t)i);
@@ -1035,6 +1048,9 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.bp_thr = h->pp.behaviour_penalty_threshold; a.w7 = h->pp.behaviour_penalty_weight;
     a.lastpub = h->x->d_lastpub; a.fan_topics = h->x->d_fantopics;
     a.pub_thr = h->th.publish_threshold; a.fanout_ttl = h->gp.fanout_ttl_ns;
+    a.gid = h->sh ? h->sh->d_gid : nullptr;
+    a.olo = (uint32_t)h->olo();
+    a.ohi = (uint32_t)h->ohi();
     return a;
 }
 
@@ -1090,24 +1106,39 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     // of <= 16 connections, 2 for <= 32, 1 otherwise (observers are
     // independent within a heartbeat, so the classes run one after the other)
     const Extra* x = h->x;
-    if (x->n16 == h->n) {
-        hipLaunchKernelGGL(k_heartbeat<16>, dim3(grid_rows((h->n + 3) / 4)), dim3(256), 0, h->stream, a, nullptr, h->n);
-    } else if (x->n32 == h->n) {
-        hipLaunchKernelGGL(k_heartbeat<32>, dim3(grid_rows((h->n + 1) / 2)), dim3(256), 0, h->stream, a, nullptr, h->n);
-    } else if (x->n64 == h->n) {
-        hipLaunchKernelGGL(k_heartbeat<64>, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a, nullptr, h->n);
+    const int64_t nown = h->ohi() - h->olo();
+    if (x->n16 == nown) {   // one class: the owned rows in order
+        hipLaunchKernelGGL(k_heartbeat<16>, dim3(grid_rows((nown + 3) / 4)), dim3(256), 0, h->stream, a, nullptr, nown,
+                           h->olo());
+    } else if (x->n32 == nown) {
+        hipLaunchKernelGGL(k_heartbeat<32>, dim3(grid_rows((nown + 1) / 2)), dim3(256), 0, h->stream, a, nullptr, nown,
+                           h->olo());
+    } else if (x->n64 == nown) {
+        hipLaunchKernelGGL(k_heartbeat<64>, dim3(grid_rows(nown)), dim3(256), 0, h->stream, a, nullptr, nown, h->olo());
     } else {
         const uint32_t* r = x->d_rows;
         if (x->n16) hipLaunchKernelGGL(k_heartbeat<16>, dim3(grid_rows((x->n16 + 3) / 4)), dim3(256), 0, h->stream,
-                                       a, r, x->n16);
+                                       a, r, x->n16, (int64_t)0);
         if (x->n32) hipLaunchKernelGGL(k_heartbeat<32>, dim3(grid_rows((x->n32 + 1) / 2)), dim3(256), 0, h->stream,
-                                       a, r + x->n16, x->n32);
+                                       a, r + x->n16, x->n32, (int64_t)0);
         if (x->n64) hipLaunchKernelGGL(k_heartbeat<64>, dim3(grid_rows(x->n64)), dim3(256), 0, h->stream,
-                                       a, r + x->n16 + x->n32, x->n64);
+                                       a, r + x->n16 + x->n32, x->n64, (int64_t)0);
     }
-    hipLaunchKernelGGL(k_fanout_heartbeat, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a);
+    hipLaunchKernelGGL(k_fanout_heartbeat, dim3(grid_rows(nown)), dim3(256), 0, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_heartbeat");
 }
+
+}  // extern "C"
+
+int handle_control(gsim_handle* h, int32_t round, int64_t now)
+{
+    HbArgs a = make_hb_args(h, 0, now, round & 1);
+    ProfScope ps(h, GSIM_K_CONTROL);
+    hipLaunchKernelGGL(k_handle_control, dim3(grid_rows(h->ohi() - h->olo())), dim3(256), 0, h->stream, a);
+    return hip_check(h, hipGetLastError(), "k_handle_control");
+}
+
+extern "C" {
 
 int gsim_handle_control(gsim_handle* h, int32_t round, int64_t now)
 {
@@ -1116,10 +1147,7 @@ int gsim_handle_control(gsim_handle* h, int32_t round, int64_t now)
     if (h->e == 0 || !h->x) { h->err = "no graph loaded"; return GSIM_ESTATE; }
     int rc = check_degree(h);
     if (rc) return rc;
-    HbArgs a = make_hb_args(h, 0, now, round & 1);
-    ProfScope ps(h, GSIM_K_CONTROL);
-    hipLaunchKernelGGL(k_handle_control, dim3(grid_rows(h->n)), dim3(256), 0, h->stream, a);
-    return hip_check(h, hipGetLastError(), "k_handle_control");
+    return handle_control(h, round, now);
 }
 
 
