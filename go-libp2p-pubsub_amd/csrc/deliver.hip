@@ -1466,6 +1466,7 @@ static int ihave_walk(gsim_handle* h, IhaveStage* st)
 {
     Deliver* d = h->dl;
     IhArgs& a = st->a;
+    if (h->sh) { a.hbm = h->sh->d_hbm; a.hoff = h->sh->d_hoff; }   // (re)allocated after the count
     ProfScope ps(h, GSIM_K_GOSSIP);
     // lane groups sized to the rows: power-law graphs (long rows, short mean) walk
     // their few long rows in chunks rather than idling 3/4 of a 64-lane group
@@ -1729,6 +1730,41 @@ int deliver_ihave_walk(gsim_handle* h)
 }
 
 uint32_t* deliver_gcount(gsim_handle* h) { return h->dl ? h->dl->d_gcount : nullptr; }
+
+void deliver_round_end(gsim_handle* h, int64_t round) { h->dl->next_round = round + 1; }
+
+// A shard's block of the IHAVE holder bitmaps: for each active slot act[k],
+// bit p of word w says whether peer clo + 64 w + p holds the message in its
+// gossip window (the rule holds_in_window applies to local advertisers).
+__global__ __launch_bounds__(256) void k_holder_bits(RoundArgs a, const uint32_t* act, int32_t n_act, int32_t lo_round,
+                                                     int64_t tick_round, uint64_t* out)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t words = (a.CN + 63) / 64;
+    const int64_t total = words * n_act;
+    for (int64_t x = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); x < total; x += (int64_t)gridDim.x * 4) {
+        const int64_t k = x / words, w = x - k * words;
+        const uint32_t m = act[k];
+        const int64_t i = w * 64 + lane;
+        const bool hold = i < a.CN && holds_in_window(a.cell[(int64_t)m * a.CN + i], a.g, lo_round, tick_round,
+                                                      a.minv[m] != 0, a.clo + (uint32_t)i == a.morigin[m]);
+        const uint64_t b = __ballot(hold);
+        if (lane == 0) out[x] = b;
+    }
+}
+
+int deliver_holder_bits(gsim_handle* h, int64_t g, const uint32_t* d_act, int32_t n_act, uint64_t* out)
+{
+    Deliver* d = h->dl;
+    RoundArgs a = make_round_args(h, g);
+    const int64_t tick = g / d->cfg.rounds;
+    const int32_t lo_round = (int32_t)std::max<int64_t>((tick - h->gp.history_gossip) * d->cfg.rounds, 0);
+    const int64_t total = ((a.CN + 63) / 64) * n_act;
+    if (total == 0) return GSIM_OK;
+    hipLaunchKernelGGL(k_holder_bits, dim3((uint32_t)std::min<int64_t>((total + 3) / 4, 65536)), dim3(256), 0,
+                       h->stream, a, d_act, n_act, lo_round, tick * d->cfg.rounds, out);
+    return hip_check(h, hipGetLastError(), "k_holder_bits");
+}
 int32_t* deliver_slot_last(gsim_handle* h) { return h->dl ? h->dl->d_slot_last : nullptr; }
 
 extern "C" {
@@ -1840,7 +1876,9 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
     }
     std::vector<uint32_t> slots((size_t)count);
     for (int32_t m = 0; m < count; ++m) {
-        if (msgs[m].topic >= (uint32_t)std::max(1, h->t) || (int64_t)msgs[m].origin >= h->n) {
+        // a shard gets every message; an origin that is not one of its peers is 0xFFFFFFFF
+        const bool foreign = h->sh && msgs[m].origin == 0xFFFFFFFFu;
+        if (msgs[m].topic >= (uint32_t)std::max(1, h->t) || ((int64_t)msgs[m].origin >= h->n && !foreign)) {
             h->err = "message topic or origin out of range";
             return GSIM_EINVAL;
         }

@@ -323,3 +323,8 @@ int deliver_ihave_count(gsim_handle* h, int64_t g, bool* run);
 int deliver_ihave_walk(gsim_handle* h);
 uint32_t* deliver_gcount(gsim_handle* h);             // [2][ring] holders / wanting receivers per slot
 int32_t* deliver_slot_last(gsim_handle* h);           // [ring]
+void deliver_round_end(gsim_handle* h, int64_t round);
+int deliver_holder_bits(gsim_handle* h, int64_t g, const uint32_t* d_act, int32_t n_act, uint64_t* out);
+// heartbeat.hip: the control inbox ([2][T][E] by round parity) and its per-receiver summary ([2][N])
+uint8_t* extra_ctl(gsim_handle* h);
+uint64_t* extra_cany(gsim_handle* h);

@@ -1003,6 +1003,9 @@ int extra_field_written(gsim_handle* h, int32_t f)
                      "control summary");
 }
 
+uint8_t* extra_ctl(gsim_handle* h) { return h->x ? h->x->d_ctl : nullptr; }
+uint64_t* extra_cany(gsim_handle* h) { return h->x ? h->x->d_cany : nullptr; }
+
 bool extra_field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r)
 {
     if (f == GSIM_F_CTL && h->x && h->x->d_ctl) {

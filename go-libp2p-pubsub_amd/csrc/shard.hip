@@ -1,0 +1,1161 @@
+// shard.hip — graph-sharded networks over several GPUs (SURVEY.md §8(e),
+// DESIGN.md §5): a group of shard handles and the halo exchange between them.
+//
+// The reference runs one router per host and moves RPCs between hosts over
+// libp2p streams (gossipsub.go:1138-1202 sendRPC).  Here one simulated network
+// is split into contiguous peer ranges (shard_plan.cpp).  Each shard is an
+// ordinary engine handle over its local graph — owned rows plus ghost rows —
+// that computes only for its owned peers, and the group moves between shards
+// exactly what a remote neighbour produced:
+//   per round      message copies to ghost receivers (k_send_tm queues them:
+//                  the receiver's record there | slot), delivered by the
+//                  receiving shard like any arriving copy;
+//   per control    GRAFT/PRUNE records written into ghost receivers' inboxes;
+//   per heartbeat  the gossip marks (emitGossip's choice per topic + the
+//                  advertiser's IWANT gate) of cross edges, into the receiving
+//                  shard's ghost rows;
+//   per IHAVE      the per-slot holder / want counts (a sum), slot activity (a
+//                  max) and the holders' bitmaps (an all-gather).
+// Two transports move the bytes: in-process (every shard in this process, one
+// HIP stream each; device-to-device copies) and RCCL (one shard per process,
+// ncclSend/ncclRecv grouped all-to-all, all-reduce, broadcasts over xGMI).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "gsim.h"
+#include "gsim_internal.h"
+#include "shard_layout.h"
+
+using namespace gsim;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// exchange kernels
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+// GRAFT/PRUNE records written into ghost receivers' inboxes (plane `ctl`,
+// summary `cany`), one thread per ghost peer with a summary bit: entries
+// (owner shard's edge | topic << 32 | bits << 40) to the ghost's shard.
+__global__ __launch_bounds__(256) void k_ctl_export(uint8_t* ctl, uint64_t* cany, const uint32_t* row_ptr,
+                                                    const uint32_t* ymap, const uint8_t* pshard, int64_t E,
+                                                    int64_t olo, int64_t ohi, int64_t n, uint64_t* out,
+                                                    uint32_t* cnt, int64_t cap)
+{
+    const int64_t nghost = olo + (n - ohi);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < nghost; x += stride) {
+        const int64_t g = x < olo ? x : ohi + (x - olo);
+        uint64_t any = cany[g];
+        if (!any) continue;
+        cany[g] = 0;
+        const uint32_t d = pshard[g];
+        for (; any; any &= any - 1) {
+            const int32_t t = __ffsll((long long)any) - 1;
+            for (uint32_t e = row_ptr[g]; e < row_ptr[g + 1]; ++e) {
+                const int64_t i = (int64_t)t * E + e;
+                const uint8_t c = ctl[i];
+                if (!c) continue;
+                ctl[i] = 0;
+                const uint32_t pos = atomicAdd(&cnt[d], 1u);
+                if ((int64_t)pos < cap)
+                    out[(int64_t)d * cap + pos] = (uint64_t)ymap[e] | ((uint64_t)t << 32) | ((uint64_t)c << 40);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ctl_import(const uint64_t* in, int64_t n_in, uint8_t* ctl, uint64_t* cany,
+                                                    const uint32_t* owner, int64_t E)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n_in; x += stride) {
+        const uint64_t v = in[x];
+        const uint32_t e = (uint32_t)v;
+        const int32_t t = (int32_t)((v >> 32) & 0xFF);
+        const uint8_t bits = (uint8_t)(v >> 40);
+        uint8_t* p = ctl + (int64_t)t * E + e;
+        *p = (uint8_t)(*p | bits);      // one entry per (receiver edge, topic)
+        atomicOr(reinterpret_cast<unsigned long long*>(cany + owner[e]), 1ull << t);
+    }
+}
+
+// emitGossip's choices of the owned rows' cross edges, one topic mask per
+// edge in cross-out order, with the advertiser's IWANT gate (gstate).
+__global__ __launch_bounds__(256) void k_gsel_export(const uint32_t* xgather, int64_t n_cross, const uint8_t* gsel,
+                                                     const uint8_t* gstate, int32_t T, int64_t E, uint64_t* out,
+                                                     uint8_t* gs_out)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n_cross; q += stride) {
+        const uint32_t e = xgather[q];
+        uint64_t m = 0;
+        for (int32_t t = 0; t < T; ++t) m |= (uint64_t)(gsel[(int64_t)t * E + e] != 0) << t;
+        out[q] = m;
+        gs_out[q] = gstate[e];
+    }
+}
+
+// ... into the ghost rows: every topic plane of every ghost-row edge.
+__global__ __launch_bounds__(256) void k_gsel_import(const uint64_t* in, const uint8_t* gs_in, uint8_t* gsel,
+                                                     uint8_t* gstate, int32_t T, int64_t E, int64_t e_lo, int64_t e_hi)
+{
+    const int64_t nghost = e_lo + (E - e_hi);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < nghost; x += stride) {
+        const int64_t e = x < e_lo ? x : e_hi + (x - e_lo);
+        const uint64_t m = in[e];
+        for (int32_t t = 0; t < T; ++t) gsel[(int64_t)t * E + e] = (uint8_t)((m >> t) & 1ull);
+        gstate[e] = gs_in[e];
+    }
+}
+
+int grid_for(int64_t n)
+{
+    int64_t g = (n + 255) / 256;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(g, 16384));
+}
+
+// ---------------------------------------------------------------------------
+// transports
+
+enum { DT_U32 = 0, DT_I32 = 1, DT_U64 = 2 };
+enum { OP_SUM = 0, OP_MAX = 1 };
+
+struct Transport {
+    virtual ~Transport() = default;
+    // send[l][d]: 64-bit values local shard l sends shard d -> recv[l][s]
+    virtual int exchange_counts(const std::vector<std::vector<uint64_t>>& send,
+                                std::vector<std::vector<uint64_t>>& recv) = 0;
+    // bytes sp[l][d] (sb[l][d] of them) from local shard l to shard d, landing
+    // at d's rp[.][l] (rb bytes)
+    virtual int alltoallv(const std::vector<std::vector<const void*>>& sp, const std::vector<std::vector<uint64_t>>& sb,
+                          const std::vector<std::vector<void*>>& rp, const std::vector<std::vector<uint64_t>>& rb) = 0;
+    // elementwise over every shard's array p[l] (count elements), in place
+    virtual int allreduce(const std::vector<void*>& p, int64_t count, int dt, int op) = 0;
+    // shard s's block (bytes[s] at byte offset off[s]) into every shard's buf
+    virtual int allgatherv(const std::vector<void*>& buf, const std::vector<uint64_t>& off,
+                           const std::vector<uint64_t>& bytes) = 0;
+    virtual int sync() = 0;
+    std::string err;
+};
+
+// Every shard in this process (possibly on one device): device-to-device
+// copies between the shards' buffers, ordered by synchronizing the streams.
+struct LocalTransport : Transport {
+    std::vector<gsim_handle*> hs;   // index = shard id
+    int sync() override
+    {
+        for (gsim_handle* h : hs) {
+            (void)hipSetDevice(h->device);
+            if (hipStreamSynchronize(h->stream) != hipSuccess) { err = "stream synchronize"; return GSIM_EDEVICE; }
+        }
+        return GSIM_OK;
+    }
+    int exchange_counts(const std::vector<std::vector<uint64_t>>& send, std::vector<std::vector<uint64_t>>& recv) override
+    {
+        const size_t K = hs.size();
+        recv.assign(K, std::vector<uint64_t>(K, 0));
+        for (size_t a = 0; a < K; ++a)
+            for (size_t b = 0; b < K; ++b) recv[b][a] = send[a][b];
+        return GSIM_OK;
+    }
+    int alltoallv(const std::vector<std::vector<const void*>>& sp, const std::vector<std::vector<uint64_t>>& sb,
+                  const std::vector<std::vector<void*>>& rp, const std::vector<std::vector<uint64_t>>& rb) override
+    {
+        int rc = sync();
+        if (rc) return rc;
+        const size_t K = hs.size();
+        for (size_t a = 0; a < K; ++a)
+            for (size_t b = 0; b < K; ++b) {
+                if (a == b || !sb[a][b]) continue;
+                if (rb[b][a] != sb[a][b]) { err = "exchange size mismatch"; return GSIM_EINVAL; }
+                (void)hipSetDevice(hs[b]->device);
+                if (hipMemcpyAsync(rp[b][a], sp[a][b], sb[a][b], hipMemcpyDefault, hs[b]->stream) != hipSuccess) {
+                    err = "device copy";
+                    return GSIM_EDEVICE;
+                }
+            }
+        return sync();
+    }
+    int allreduce(const std::vector<void*>& p, int64_t count, int dt, int op) override
+    {
+        int rc = sync();
+        if (rc) return rc;
+        const size_t es = dt == DT_U64 ? 8 : 4, K = hs.size();
+        std::vector<std::vector<uint8_t>> host(K, std::vector<uint8_t>(es * (size_t)count));
+        for (size_t s = 0; s < K; ++s) {
+            (void)hipSetDevice(hs[s]->device);
+            if (hipMemcpy(host[s].data(), p[s], es * (size_t)count, hipMemcpyDeviceToHost) != hipSuccess) {
+                err = "reduce readback";
+                return GSIM_EDEVICE;
+            }
+        }
+        std::vector<uint8_t> acc = host[0];
+        for (size_t s = 1; s < K; ++s)
+            for (int64_t i = 0; i < count; ++i) {
+                if (dt == DT_U64) {
+                    uint64_t& x = reinterpret_cast<uint64_t*>(acc.data())[i];
+                    const uint64_t y = reinterpret_cast<const uint64_t*>(host[s].data())[i];
+                    x = op == OP_SUM ? x + y : std::max(x, y);
+                } else if (dt == DT_U32) {
+                    uint32_t& x = reinterpret_cast<uint32_t*>(acc.data())[i];
+                    const uint32_t y = reinterpret_cast<const uint32_t*>(host[s].data())[i];
+                    x = op == OP_SUM ? x + y : std::max(x, y);
+                } else {
+                    int32_t& x = reinterpret_cast<int32_t*>(acc.data())[i];
+                    const int32_t y = reinterpret_cast<const int32_t*>(host[s].data())[i];
+                    x = op == OP_SUM ? x + y : std::max(x, y);
+                }
+            }
+        for (size_t s = 0; s < K; ++s) {
+            (void)hipSetDevice(hs[s]->device);
+            if (hipMemcpy(p[s], acc.data(), es * (size_t)count, hipMemcpyHostToDevice) != hipSuccess) {
+                err = "reduce upload";
+                return GSIM_EDEVICE;
+            }
+        }
+        return GSIM_OK;
+    }
+    int allgatherv(const std::vector<void*>& buf, const std::vector<uint64_t>& off,
+                   const std::vector<uint64_t>& bytes) override
+    {
+        int rc = sync();
+        if (rc) return rc;
+        const size_t K = hs.size();
+        for (size_t s = 0; s < K; ++s)
+            for (size_t d = 0; d < K; ++d) {
+                if (s == d || !bytes[s]) continue;
+                (void)hipSetDevice(hs[d]->device);
+                if (hipMemcpyAsync((uint8_t*)buf[d] + off[s], (const uint8_t*)buf[s] + off[s], bytes[s],
+                                   hipMemcpyDefault, hs[d]->stream) != hipSuccess) {
+                    err = "device copy";
+                    return GSIM_EDEVICE;
+                }
+            }
+        return sync();
+    }
+};
+
+// One shard per process, RCCL over xGMI: every collective is enqueued on the
+// shard's own stream, so the kernels before and after it stay stream-ordered.
+struct RcclTransport : Transport {
+    gsim_handle* h = nullptr;
+    int k = 0, K = 1;
+    ncclComm_t comm = nullptr;
+    uint64_t* d_cnt = nullptr;     // [K*K] count matrix
+    uint64_t* h_cnt = nullptr;     // pinned
+    ~RcclTransport() override
+    {
+        if (d_cnt) (void)hipFree(d_cnt);
+        if (h_cnt) (void)hipHostFree(h_cnt);
+        if (comm) ncclCommDestroy(comm);
+    }
+    int check(ncclResult_t r, const char* what)
+    {
+        if (r == ncclSuccess) return GSIM_OK;
+        err = std::string(what) + ": " + ncclGetErrorString(r);
+        return GSIM_EDEVICE;
+    }
+    int sync() override
+    {
+        if (hipStreamSynchronize(h->stream) != hipSuccess) { err = "stream synchronize"; return GSIM_EDEVICE; }
+        return GSIM_OK;
+    }
+    int exchange_counts(const std::vector<std::vector<uint64_t>>& send, std::vector<std::vector<uint64_t>>& recv) override
+    {
+        for (int d = 0; d < K; ++d) h_cnt[(size_t)k * K + d] = send[0][(size_t)d];
+        if (hipMemcpyAsync(d_cnt + (size_t)k * K, h_cnt + (size_t)k * K, sizeof(uint64_t) * K, hipMemcpyHostToDevice,
+                           h->stream) != hipSuccess) { err = "count upload"; return GSIM_EDEVICE; }
+        int rc = check(ncclAllGather(d_cnt + (size_t)k * K, d_cnt, (size_t)K, ncclUint64, comm, h->stream),
+                       "ncclAllGather(counts)");
+        if (rc) return rc;
+        if (hipMemcpyAsync(h_cnt, d_cnt, sizeof(uint64_t) * K * K, hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+            { err = "count readback"; return GSIM_EDEVICE; }
+        rc = sync();
+        if (rc) return rc;
+        recv.assign(1, std::vector<uint64_t>((size_t)K, 0));
+        for (int s = 0; s < K; ++s) recv[0][(size_t)s] = h_cnt[(size_t)s * K + k];
+        return GSIM_OK;
+    }
+    int alltoallv(const std::vector<std::vector<const void*>>& sp, const std::vector<std::vector<uint64_t>>& sb,
+                  const std::vector<std::vector<void*>>& rp, const std::vector<std::vector<uint64_t>>& rb) override
+    {
+        int rc = check(ncclGroupStart(), "ncclGroupStart");
+        for (int d = 0; d < K && !rc; ++d) {
+            if (d == k) continue;
+            if (sb[0][(size_t)d])
+                rc = check(ncclSend(sp[0][(size_t)d], sb[0][(size_t)d], ncclChar, d, comm, h->stream), "ncclSend");
+            if (!rc && rb[0][(size_t)d])
+                rc = check(ncclRecv(rp[0][(size_t)d], rb[0][(size_t)d], ncclChar, d, comm, h->stream), "ncclRecv");
+        }
+        const int rc2 = check(ncclGroupEnd(), "ncclGroupEnd");
+        return rc ? rc : rc2;
+    }
+    int allreduce(const std::vector<void*>& p, int64_t count, int dt, int op) override
+    {
+        const ncclDataType_t t = dt == DT_U64 ? ncclUint64 : dt == DT_U32 ? ncclUint32 : ncclInt32;
+        return check(ncclAllReduce(p[0], p[0], (size_t)count, t, op == OP_SUM ? ncclSum : ncclMax, comm, h->stream),
+                     "ncclAllReduce");
+    }
+    int allgatherv(const std::vector<void*>& buf, const std::vector<uint64_t>& off,
+                   const std::vector<uint64_t>& bytes) override
+    {
+        int rc = check(ncclGroupStart(), "ncclGroupStart");
+        for (int s = 0; s < K && !rc; ++s) {
+            if (!bytes[(size_t)s]) continue;
+            void* p = (uint8_t*)buf[0] + off[(size_t)s];
+            rc = check(ncclBroadcast(p, p, bytes[(size_t)s], ncclChar, s, comm, h->stream), "ncclBroadcast");
+        }
+        const int rc2 = check(ncclGroupEnd(), "ncclGroupEnd");
+        return rc ? rc : rc2;
+    }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// the group
+
+struct gsim_group {
+    int K = 1;
+    std::vector<gsim_handle*> hs;     // local shards
+    std::vector<int> ids;             // their shard ids
+    std::unique_ptr<Transport> tr;
+    std::string err;
+    std::vector<int64_t> bounds;
+    int64_t N = 0, E = 0;
+    std::vector<std::vector<uint32_t>> gid;   // per local shard: local -> global peer id (host)
+    std::vector<std::vector<uint64_t>> gidx;  // per local shard: local -> global edge index (host)
+    int32_t ring = 0, rounds = 0;
+    bool msgs = false;
+
+    int fail(int rc, const std::string& m)
+    {
+        err = m;
+        return rc;
+    }
+    int take(gsim_handle* h, int rc)   // adopt a shard's error message
+    {
+        if (rc) err = "shard: " + h->err;
+        return rc;
+    }
+    int take_tr(int rc)
+    {
+        if (rc) err = "exchange: " + tr->err;
+        return rc;
+    }
+};
+
+namespace {
+
+template <typename T>
+int dalloc(gsim_handle* h, T** p, size_t n)
+{
+    *p = nullptr;
+    hipError_t e = hipMalloc((void**)p, sizeof(T) * std::max<size_t>(n, 1));
+    if (e != hipSuccess) { h->err = std::string("hipMalloc: ") + hipGetErrorString(e); return GSIM_ENOMEM; }
+    h->bytes_allocated += sizeof(T) * n;
+    return GSIM_OK;
+}
+
+void free_shard_ctx(gsim_handle* h)
+{
+    ShardCtx* s = h->sh;
+    if (!s) return;
+    auto f = [](void* p) { if (p) (void)hipFree(p); };
+    f(s->d_gid); f(s->d_pshard); f(s->d_xr); f(s->d_ymap); f(s->d_xgather); f(s->d_bounds);
+    f(s->d_xout); f(s->d_xcnt); f(s->d_xin); f(s->d_xin_n); f(s->d_cout); f(s->d_ccnt); f(s->d_cin);
+    f(s->d_gout); f(s->d_gsout); f(s->d_gin); f(s->d_gsin); f(s->d_slot_last_g); f(s->d_act); f(s->d_hbm);
+    f(s->d_hoff);
+    if (s->h_counts) (void)hipHostFree(s->h_counts);
+    delete s;
+    h->sh = nullptr;
+}
+
+// grow a device buffer (contents are not kept)
+template <typename T>
+int ensure(gsim_handle* h, T** p, int64_t* cap, int64_t need)
+{
+    if (*cap >= need && *p) return GSIM_OK;
+    if (*p) { (void)hipStreamSynchronize(h->stream); (void)hipFree(*p); *p = nullptr; }
+    const int64_t c = std::max<int64_t>(need, 1) + need / 4;
+    int rc = dalloc(h, p, (size_t)c);
+    *cap = rc ? 0 : c;
+    return rc;
+}
+
+int sync_all(gsim_group* g)
+{
+    for (gsim_handle* h : g->hs) {
+        (void)hipSetDevice(h->device);
+        if (hipStreamSynchronize(h->stream) != hipSuccess) return g->fail(GSIM_EDEVICE, "stream synchronize");
+    }
+    return GSIM_OK;
+}
+
+// GRAFT/PRUNE records in ghost receivers' inboxes of plane `parity` go to
+// their shards (after the heartbeat: parity 0; after control round r: r+1).
+int exchange_control(gsim_group* g, int parity)
+{
+    const size_t L = g->hs.size();
+    const int K = g->K;
+    std::vector<std::vector<uint64_t>> scnt(L, std::vector<uint64_t>((size_t)K, 0)), rcnt;
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        (void)hipSetDevice(h->device);
+        const size_t TE = (size_t)h->e * (size_t)std::max(1, h->t);
+        uint8_t* ctl = extra_ctl(h) + (size_t)parity * TE;
+        uint64_t* cany = extra_cany(h) + (size_t)parity * (size_t)h->n;
+        if (hipMemsetAsync(s->d_ccnt, 0, sizeof(uint32_t) * K, h->stream) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "control count reset");
+        const int64_t nghost = s->own_lo + (h->n - s->own_hi);
+        hipLaunchKernelGGL(k_ctl_export, dim3(grid_for(nghost)), dim3(256), 0, h->stream, ctl, cany,
+                           (const uint32_t*)h->d_row_ptr, (const uint32_t*)s->d_ymap, (const uint8_t*)s->d_pshard,
+                           h->e, s->own_lo, s->own_hi, h->n, s->d_cout, s->d_ccnt, s->ccap);
+        if (hipMemcpyAsync(s->h_counts, s->d_ccnt, sizeof(uint32_t) * K, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+            hipStreamSynchronize(h->stream) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "control counts");
+        for (int d = 0; d < K; ++d) {
+            if ((int64_t)s->h_counts[d] > s->ccap)
+                return g->fail(GSIM_ERANGE, "control exchange queue overflow");
+            scnt[l][(size_t)d] = s->h_counts[d];
+        }
+    }
+    int rc = g->take_tr(g->tr->exchange_counts(scnt, rcnt));
+    if (rc) return rc;
+    std::vector<std::vector<const void*>> sp(L, std::vector<const void*>((size_t)K, nullptr));
+    std::vector<std::vector<void*>> rp(L, std::vector<void*>((size_t)K, nullptr));
+    std::vector<std::vector<uint64_t>> sb(L, std::vector<uint64_t>((size_t)K, 0)), rb = sb;
+    std::vector<int64_t> total(L, 0);
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        for (int q = 0; q < K; ++q) total[l] += (int64_t)rcnt[l][(size_t)q];
+        (void)hipSetDevice(h->device);
+        rc = g->take(h, ensure(h, &s->d_cin, &s->cin_cap, total[l]));
+        if (rc) return rc;
+        int64_t off = 0;
+        for (int q = 0; q < K; ++q) {
+            sp[l][(size_t)q] = s->d_cout + (int64_t)q * s->ccap;
+            sb[l][(size_t)q] = scnt[l][(size_t)q] * 8;
+            rp[l][(size_t)q] = s->d_cin + off;
+            rb[l][(size_t)q] = rcnt[l][(size_t)q] * 8;
+            off += (int64_t)rcnt[l][(size_t)q];
+        }
+    }
+    rc = g->take_tr(g->tr->alltoallv(sp, sb, rp, rb));
+    if (rc) return rc;
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        if (!total[l]) continue;
+        (void)hipSetDevice(h->device);
+        const size_t TE = (size_t)h->e * (size_t)std::max(1, h->t);
+        hipLaunchKernelGGL(k_ctl_import, dim3(grid_for(total[l])), dim3(256), 0, h->stream,
+                           (const uint64_t*)h->sh->d_cin, total[l], extra_ctl(h) + (size_t)parity * TE,
+                           extra_cany(h) + (size_t)parity * (size_t)h->n, (const uint32_t*)h->d_owner, h->e);
+        if (hipGetLastError() != hipSuccess) return g->fail(GSIM_EDEVICE, "k_ctl_import");
+    }
+    return GSIM_OK;
+}
+
+// emitGossip's marks of cross edges into the receiving shards' ghost rows
+int exchange_gossip_marks(gsim_group* g)
+{
+    const size_t L = g->hs.size();
+    const int K = g->K;
+    std::vector<std::vector<const void*>> sp(L, std::vector<const void*>((size_t)K, nullptr));
+    std::vector<std::vector<void*>> rp(L, std::vector<void*>((size_t)K, nullptr));
+    std::vector<std::vector<uint64_t>> sb(L, std::vector<uint64_t>((size_t)K, 0)), rb = sb;
+    std::vector<std::vector<const void*>> sp2 = sp;
+    std::vector<std::vector<void*>> rp2 = rp;
+    std::vector<std::vector<uint64_t>> sb2 = sb, rb2 = sb;
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        GossipView gv{};
+        if (!deliver_gossip_view(h, &gv)) return GSIM_OK;      // no message state: nothing gossips
+        (void)hipSetDevice(h->device);
+        const int64_t ncross = s->xoff[(size_t)K];
+        if (ncross)
+            hipLaunchKernelGGL(k_gsel_export, dim3(grid_for(ncross)), dim3(256), 0, h->stream,
+                               (const uint32_t*)s->d_xgather, ncross, (const uint8_t*)gv.gsel,
+                               (const uint8_t*)gv.gstate, h->t, h->e, s->d_gout, s->d_gsout);
+        for (int q = 0; q < K; ++q) {
+            const int64_t n_out = s->xoff[(size_t)q + 1] - s->xoff[(size_t)q];
+            sp[l][(size_t)q] = s->d_gout + s->xoff[(size_t)q];
+            sb[l][(size_t)q] = (uint64_t)n_out * 8;
+            sp2[l][(size_t)q] = s->d_gsout + s->xoff[(size_t)q];
+            sb2[l][(size_t)q] = (uint64_t)n_out;
+            rp[l][(size_t)q] = s->d_gin + s->gbase[(size_t)q];
+            rb[l][(size_t)q] = (uint64_t)s->gcnt[(size_t)q] * 8;
+            rp2[l][(size_t)q] = s->d_gsin + s->gbase[(size_t)q];
+            rb2[l][(size_t)q] = (uint64_t)s->gcnt[(size_t)q];
+        }
+    }
+    int rc = g->take_tr(g->tr->alltoallv(sp, sb, rp, rb));
+    if (!rc) rc = g->take_tr(g->tr->alltoallv(sp2, sb2, rp2, rb2));
+    if (rc) return rc;
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        GossipView gv{};
+        deliver_gossip_view(h, &gv);
+        (void)hipSetDevice(h->device);
+        const int64_t nghost = s->own_e_lo + (h->e - s->own_e_hi);
+        if (nghost)
+            hipLaunchKernelGGL(k_gsel_import, dim3(grid_for(nghost)), dim3(256), 0, h->stream,
+                               (const uint64_t*)s->d_gin, (const uint8_t*)s->d_gsin, gv.gsel, gv.gstate, h->t, h->e,
+                               s->own_e_lo, s->own_e_hi);
+        if (hipGetLastError() != hipSuccess) return g->fail(GSIM_EDEVICE, "k_gsel_import");
+    }
+    return GSIM_OK;
+}
+
+// the copies every shard queued for ghost receivers in round `round`
+int exchange_copies(gsim_group* g, int64_t round)
+{
+    const size_t L = g->hs.size();
+    const int K = g->K;
+    std::vector<std::vector<uint64_t>> scnt(L, std::vector<uint64_t>((size_t)K, 0)), rcnt;
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        (void)hipSetDevice(h->device);
+        if (hipMemcpyAsync(s->h_counts, s->d_xcnt, sizeof(uint32_t) * K, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+            hipStreamSynchronize(h->stream) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "copy counts");
+        for (int d = 0; d < K; ++d) {
+            if ((int64_t)s->h_counts[d] > s->xcap)
+                return g->fail(GSIM_ERANGE, "copy queue to another shard overflowed (raise gsim_msg_config.max_frontier)");
+            scnt[l][(size_t)d] = s->h_counts[d];
+        }
+    }
+    int rc = g->take_tr(g->tr->exchange_counts(scnt, rcnt));
+    if (rc) return rc;
+    std::vector<std::vector<const void*>> sp(L, std::vector<const void*>((size_t)K, nullptr));
+    std::vector<std::vector<void*>> rp(L, std::vector<void*>((size_t)K, nullptr));
+    std::vector<std::vector<uint64_t>> sb(L, std::vector<uint64_t>((size_t)K, 0)), rb = sb;
+    std::vector<int64_t> total(L, 0);
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        for (int q = 0; q < K; ++q) total[l] += (int64_t)rcnt[l][(size_t)q];
+        (void)hipSetDevice(h->device);
+        rc = g->take(h, ensure(h, &s->d_xin, &s->xin_cap, total[l]));
+        if (rc) return rc;
+        int64_t off = 0;
+        for (int q = 0; q < K; ++q) {
+            sp[l][(size_t)q] = s->d_xout + (int64_t)q * s->xcap;
+            sb[l][(size_t)q] = scnt[l][(size_t)q] * 8;
+            rp[l][(size_t)q] = s->d_xin + off;
+            rb[l][(size_t)q] = rcnt[l][(size_t)q] * 8;
+            off += (int64_t)rcnt[l][(size_t)q];
+        }
+    }
+    rc = g->take_tr(g->tr->alltoallv(sp, sb, rp, rb));
+    if (rc) return rc;
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        if (!total[l]) continue;
+        (void)hipSetDevice(h->device);
+        s->h_counts[0] = (uint32_t)total[l];
+        if (hipMemcpyAsync(s->d_xin_n, s->h_counts, sizeof(uint32_t), hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+            hipStreamSynchronize(h->stream) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "copy count upload");
+        ProfScope ps(h, GSIM_K_SEND);
+        rc = g->take(h, deliver_round_queue(h, round, s->d_xin, s->d_xin_n, s->xin_cap));
+        if (rc) return rc;
+    }
+    return GSIM_OK;
+}
+
+// The IHAVE stage of a control round 0 (gossipsub.go:630-739) over shards.
+int group_ihave(gsim_group* g, int64_t round)
+{
+    const size_t L = g->hs.size();
+    const int K = g->K;
+    // slot activity: the max over shards (the candidate-slot filter)
+    std::vector<void*> p(L);
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        (void)hipSetDevice(h->device);
+        if (hipMemcpyAsync(h->sh->d_slot_last_g, deliver_slot_last(h), sizeof(int32_t) * (size_t)g->ring,
+                           hipMemcpyDeviceToDevice, h->stream) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "slot activity copy");
+        p[l] = h->sh->d_slot_last_g;
+    }
+    int rc = g->take_tr(g->tr->allreduce(p, g->ring, DT_I32, OP_MAX));
+    if (rc) return rc;
+    bool run = false;
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        (void)hipSetDevice(h->device);
+        bool r = false;
+        rc = g->take(h, deliver_ihave_count(h, round, &r));
+        if (rc) return rc;
+        run = r;
+        p[l] = deliver_gcount(h);
+    }
+    if (!run) return GSIM_OK;
+    rc = g->take_tr(g->tr->allreduce(p, 2 * (int64_t)g->ring, DT_U32, OP_SUM));
+    if (rc) return rc;
+    // the active slots, the same list on every shard (and in k_ihave)
+    gsim_handle* h0 = g->hs[0];
+    (void)hipSetDevice(h0->device);
+    std::vector<uint32_t> cnt(2 * (size_t)g->ring);
+    std::vector<int32_t> last((size_t)g->ring);
+    if (hipMemcpyAsync(cnt.data(), deliver_gcount(h0), cnt.size() * 4, hipMemcpyDeviceToHost, h0->stream) != hipSuccess ||
+        hipMemcpyAsync(last.data(), h0->sh->d_slot_last_g, last.size() * 4, hipMemcpyDeviceToHost, h0->stream) != hipSuccess ||
+        hipStreamSynchronize(h0->stream) != hipSuccess)
+        return g->fail(GSIM_EDEVICE, "gossip counts readback");
+    const int64_t tick = round / g->rounds;
+    const int64_t lo_round = std::max<int64_t>((tick - h0->gp.history_gossip) * g->rounds, 0);
+    std::vector<uint32_t> act;
+    for (int32_t m = 0; m < g->ring; ++m)
+        if (last[(size_t)m] >= lo_round && cnt[(size_t)m] != 0 && cnt[(size_t)g->ring + m] != 0) act.push_back((uint32_t)m);
+    const int32_t n_act = (int32_t)act.size();
+    // holder bitmaps: shard s's block is n_act x ceil(peers_s / 64) words at hoff[s]
+    std::vector<int64_t> hoff((size_t)K + 1, 0);
+    for (int s = 0; s < K; ++s) hoff[(size_t)s + 1] = hoff[(size_t)s] + (int64_t)n_act * ((g->bounds[(size_t)s + 1] - g->bounds[(size_t)s] + 63) / 64);
+    std::vector<void*> buf(L);
+    std::vector<uint64_t> off((size_t)K), bytes((size_t)K);
+    for (int s = 0; s < K; ++s) { off[(size_t)s] = (uint64_t)hoff[(size_t)s] * 8; bytes[(size_t)s] = (uint64_t)(hoff[(size_t)s + 1] - hoff[(size_t)s]) * 8; }
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        (void)hipSetDevice(h->device);
+        rc = g->take(h, ensure(h, &s->d_hbm, &s->hbm_cap, std::max<int64_t>(hoff[(size_t)K], 1)));
+        if (rc) return rc;
+        if ((n_act && hipMemcpyAsync(s->d_act, act.data(), act.size() * 4, hipMemcpyHostToDevice, h->stream) != hipSuccess) ||
+            hipMemcpyAsync(s->d_hoff, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "holder table upload");
+        ProfScope ps(h, GSIM_K_GOSSIP);
+        rc = g->take(h, deliver_holder_bits(h, round, s->d_act, n_act, s->d_hbm + hoff[(size_t)s->k]));
+        if (rc) return rc;
+        buf[l] = s->d_hbm;
+    }
+    if (n_act) {
+        rc = g->take_tr(g->tr->allgatherv(buf, off, bytes));
+        if (rc) return rc;
+    }
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        (void)hipSetDevice(h->device);
+        // every shard's view of the counts and slots is the global one
+        if (hipMemcpyAsync(deliver_gcount(h), cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice, h->stream) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "gossip counts upload");
+        rc = g->take(h, deliver_ihave_walk(h));
+        if (rc) return rc;
+    }
+    return sync_all(g);   // the host-side tables above must outlive the uploads
+}
+
+// Create the group's shard handles; transport set by the caller.
+int group_create(const gsim_peer_score_params* params, const gsim_topic_score_params* topics, int32_t n_topics,
+                 const gsim_thresholds* th, const gsim_gossipsub_params* gp, int32_t shards,
+                 const std::vector<std::pair<int, int>>& local, gsim_group** out, char* err, size_t errlen)
+{
+    gsim_group* g = new gsim_group();
+    g->K = shards;
+    for (const auto& sd : local) {
+        gsim_handle* h = nullptr;
+        const int rc = gsim_create(params, topics, n_topics, th, gp, sd.second, &h, err, errlen);
+        if (rc) {
+            for (gsim_handle* x : g->hs) gsim_destroy(x);
+            delete g;
+            return rc;
+        }
+        h->sh = new ShardCtx();
+        h->sh->k = sd.first;
+        h->sh->K = shards;
+        g->hs.push_back(h);
+        g->ids.push_back(sd.first);
+    }
+    *out = g;
+    return GSIM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gsim_rccl_unique_id(void* out, size_t bytes)
+{
+    if (!out || bytes < sizeof(ncclUniqueId)) return GSIM_EINVAL;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return GSIM_EDEVICE;
+    std::memcpy(out, &id, sizeof(id));
+    return GSIM_OK;
+}
+
+int gsim_group_create(const gsim_peer_score_params* params, const gsim_topic_score_params* topics, int32_t n_topics,
+                      const gsim_thresholds* thresholds, const gsim_gossipsub_params* gossip, int32_t shards,
+                      const int32_t* devices, gsim_group** out, char* err, size_t errlen)
+{
+    if (!out || shards < 1 || shards > GSIM_MAX_SHARDS) return GSIM_EINVAL;
+    std::vector<std::pair<int, int>> local;
+    for (int s = 0; s < shards; ++s) local.push_back({s, devices ? devices[s] : 0});
+    int rc = group_create(params, topics, n_topics, thresholds, gossip, shards, local, out, err, errlen);
+    if (rc) return rc;
+    auto* t = new LocalTransport();
+    t->hs = (*out)->hs;
+    (*out)->tr.reset(t);
+    return GSIM_OK;
+}
+
+int gsim_group_create_rccl(const gsim_peer_score_params* params, const gsim_topic_score_params* topics,
+                           int32_t n_topics, const gsim_thresholds* thresholds, const gsim_gossipsub_params* gossip,
+                           int32_t shards, int32_t rank, int32_t device, const void* unique_id, gsim_group** out,
+                           char* err, size_t errlen)
+{
+    if (!out || !unique_id || shards < 1 || shards > GSIM_MAX_SHARDS || rank < 0 || rank >= shards) return GSIM_EINVAL;
+    int rc = group_create(params, topics, n_topics, thresholds, gossip, shards, {{rank, device}}, out, err, errlen);
+    if (rc) return rc;
+    auto* t = new RcclTransport();
+    t->h = (*out)->hs[0];
+    t->k = rank;
+    t->K = shards;
+    (void)hipSetDevice(device);
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof(id));
+    ncclResult_t nr = ncclCommInitRank(&t->comm, shards, id, rank);
+    if (nr != ncclSuccess || hipMalloc((void**)&t->d_cnt, sizeof(uint64_t) * shards * shards) != hipSuccess ||
+        hipHostMalloc((void**)&t->h_cnt, sizeof(uint64_t) * shards * shards, 0) != hipSuccess) {
+        if (err && errlen)
+            std::snprintf(err, errlen, "RCCL communicator: %s", nr != ncclSuccess ? ncclGetErrorString(nr) : "allocation");
+        delete t;
+        gsim_group_destroy(*out);
+        *out = nullptr;
+        return GSIM_EDEVICE;
+    }
+    (*out)->tr.reset(t);
+    return GSIM_OK;
+}
+
+int gsim_group_destroy(gsim_group* g)
+{
+    if (!g) return GSIM_OK;
+    for (gsim_handle* h : g->hs) {
+        (void)hipSetDevice(h->device);
+        (void)hipStreamSynchronize(h->stream);
+    }
+    g->tr.reset();
+    for (gsim_handle* h : g->hs) {
+        (void)hipSetDevice(h->device);
+        free_shard_ctx(h);
+        gsim_destroy(h);
+    }
+    delete g;
+    return GSIM_OK;
+}
+
+const char* gsim_group_last_error(const gsim_group* g) { return g ? g->err.c_str() : "null group"; }
+
+gsim_handle* gsim_group_shard(gsim_group* g, int32_t shard)
+{
+    if (!g) return nullptr;
+    for (size_t l = 0; l < g->hs.size(); ++l)
+        if (g->ids[l] == shard) return g->hs[l];
+    return nullptr;
+}
+
+int gsim_group_bounds(const gsim_group* g, int64_t* bounds)
+{
+    if (!g || !bounds || g->bounds.empty()) return GSIM_EINVAL;
+    std::copy(g->bounds.begin(), g->bounds.end(), bounds);
+    return GSIM_OK;
+}
+
+int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, const uint32_t* col,
+                          const uint8_t* outbound, const uint64_t* subs, const uint32_t* ip_ptr,
+                          const uint32_t* ip_ids, uint32_t n_ips, const int64_t* bounds)
+{
+    if (!g || n <= 0 || !row_ptr || !col) return GSIM_EINVAL;
+    const int K = g->K;
+    g->bounds.assign((size_t)K + 1, 0);
+    if (bounds) {
+        std::copy(bounds, bounds + K + 1, g->bounds.begin());
+    } else {
+        const int rc = gsim_shard_partition(n, row_ptr, subs, K, g->bounds.data());
+        if (rc) return g->fail(rc, "cannot partition the network into " + std::to_string(K) + " shards");
+    }
+    g->N = n;
+    g->E = row_ptr[n];
+    g->gid.assign(g->hs.size(), {});
+    g->gidx.assign(g->hs.size(), {});
+    g->msgs = false;
+    // every shard's ghost-block bases, for the copy destinations (xr)
+    std::vector<std::vector<uint64_t>> gb_send(g->hs.size(), std::vector<uint64_t>((size_t)K, 0)), gb_recv;
+    std::vector<ShardLayout> lay(g->hs.size());
+    for (size_t l = 0; l < g->hs.size(); ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardLayout& L = lay[l];
+        std::string e;
+        int rc = build_layout(n, row_ptr, col, g->bounds.data(), K, g->ids[l], &L, &e);
+        if (rc) return g->fail(rc, e);
+        ShardCtx* s = h->sh;
+        s->own_lo = L.own_lo; s->own_hi = L.own_hi; s->own_e_lo = L.own_e_lo; s->own_e_hi = L.own_e_hi;
+        s->N_global = n; s->E_global = g->E;
+        s->geid_base = L.own_e_hi > L.own_e_lo ? (int64_t)L.gidx[(size_t)L.own_e_lo] : 0;
+        s->bounds = g->bounds; s->lpeer = L.lpeer; s->gbase = L.gbase; s->gcnt = L.gcnt;
+        s->xoff.assign((size_t)K + 1, 0);
+        for (int q = 0; q < K; ++q) s->xoff[(size_t)q + 1] = s->xoff[(size_t)q] + (int64_t)L.crossout[(size_t)q].size();
+        for (int q = 0; q < K; ++q) gb_send[l][(size_t)q] = (uint64_t)L.gbase[(size_t)q];
+        // the local inputs
+        std::vector<uint8_t> ob((size_t)L.e_loc, 0);
+        if (outbound) for (int64_t x = 0; x < L.e_loc; ++x) ob[(size_t)x] = outbound[L.gidx[(size_t)x]];
+        std::vector<uint64_t> sb((size_t)L.n_loc, 0);
+        if (subs) for (int64_t x = 0; x < L.n_loc; ++x) sb[(size_t)x] = subs[L.gid[(size_t)x]];
+        std::vector<uint32_t> ipp, ipi;
+        if (ip_ptr) {
+            ipp.assign((size_t)L.n_loc + 1, 0);
+            for (int64_t x = 0; x < L.n_loc; ++x) {
+                const uint32_t gg = L.gid[(size_t)x];
+                for (uint32_t q = ip_ptr[gg]; q < ip_ptr[gg + 1]; ++q) ipi.push_back(ip_ids[q]);
+                ipp[(size_t)x + 1] = (uint32_t)ipi.size();
+            }
+        }
+        (void)hipSetDevice(h->device);
+        rc = gsim_load_graph(h, L.n_loc, L.row_ptr.data(), L.col.data(), ob.data(), subs ? sb.data() : nullptr,
+                             ip_ptr ? ipp.data() : nullptr, ip_ptr ? ipi.data() : nullptr, n_ips);
+        if (rc) return g->take(h, rc);
+        // device bookkeeping
+        std::vector<uint8_t> psh((size_t)L.n_loc);
+        for (int s2 = 0; s2 < K; ++s2)
+            for (int64_t x = L.lpeer[(size_t)s2]; x < L.lpeer[(size_t)s2 + 1]; ++x) psh[(size_t)x] = (uint8_t)s2;
+        std::vector<uint32_t> xg;
+        xg.reserve((size_t)L.n_cross);
+        for (int q = 0; q < K; ++q) xg.insert(xg.end(), L.crossout[(size_t)q].begin(), L.crossout[(size_t)q].end());
+        if ((rc = dalloc(h, &s->d_gid, (size_t)L.n_loc)) || (rc = dalloc(h, &s->d_pshard, (size_t)L.n_loc)) ||
+            (rc = dalloc(h, &s->d_xr, (size_t)L.e_loc)) || (rc = dalloc(h, &s->d_ymap, (size_t)L.e_loc)) ||
+            (rc = dalloc(h, &s->d_xgather, xg.size())) || (rc = dalloc(h, &s->d_bounds, (size_t)K + 1)) ||
+            (rc = dalloc(h, &s->d_hoff, (size_t)K + 1)))
+            return g->take(h, rc);
+        if (hipHostMalloc((void**)&s->h_counts, sizeof(uint32_t) * GSIM_MAX_SHARDS, 0) != hipSuccess)
+            return g->fail(GSIM_ENOMEM, "pinned scratch");
+        hipError_t he = hipMemcpy(s->d_gid, L.gid.data(), L.gid.size() * 4, hipMemcpyHostToDevice);
+        if (he == hipSuccess) he = hipMemcpy(s->d_pshard, psh.data(), psh.size(), hipMemcpyHostToDevice);
+        if (he == hipSuccess && !xg.empty()) he = hipMemcpy(s->d_xgather, xg.data(), xg.size() * 4, hipMemcpyHostToDevice);
+        if (he == hipSuccess) he = hipMemcpy(s->d_bounds, g->bounds.data(), g->bounds.size() * 8, hipMemcpyHostToDevice);
+        if (he == hipSuccess) he = hipMemset(s->d_ymap, 0xFF, (size_t)L.e_loc * 4);
+        if (he != hipSuccess) return g->fail(GSIM_EDEVICE, "shard tables upload");
+        g->gid[l] = L.gid;
+        g->gidx[l] = L.gidx;
+    }
+    // copy destinations: the receiving shard's ghost block for this shard + q
+    int rc = g->take_tr(g->tr->exchange_counts(gb_send, gb_recv));
+    if (rc) return rc;
+    for (size_t l = 0; l < g->hs.size(); ++l) {
+        gsim_handle* h = g->hs[l];
+        const ShardLayout& L = lay[l];
+        std::vector<uint32_t> xr((size_t)L.e_loc, kNone);
+        for (int64_t x = L.own_e_lo; x < L.own_e_hi; ++x) {
+            if (L.xq[(size_t)x] == kNone) continue;
+            const int d = shard_of_peer(g->bounds, L.gid[L.col[(size_t)x]]);
+            xr[(size_t)x] = (uint32_t)(gb_recv[l][(size_t)d] + L.xq[(size_t)x]);
+        }
+        (void)hipSetDevice(h->device);
+        if (hipMemcpy(h->sh->d_xr, xr.data(), xr.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "copy destinations upload");
+    }
+    // control destinations: a ghost-row edge's owned-row edge in the ghost's
+    // shard = that shard's cross-out list into this one (ymap, ghost blocks)
+    const int Kk = K;
+    std::vector<std::vector<const void*>> sp(g->hs.size(), std::vector<const void*>((size_t)Kk, nullptr));
+    std::vector<std::vector<void*>> rp(g->hs.size(), std::vector<void*>((size_t)Kk, nullptr));
+    std::vector<std::vector<uint64_t>> sbytes(g->hs.size(), std::vector<uint64_t>((size_t)Kk, 0)), rbytes = sbytes;
+    for (size_t l = 0; l < g->hs.size(); ++l) {
+        ShardCtx* s = g->hs[l]->sh;
+        for (int q = 0; q < Kk; ++q) {
+            sp[l][(size_t)q] = s->d_xgather + s->xoff[(size_t)q];
+            sbytes[l][(size_t)q] = (uint64_t)(s->xoff[(size_t)q + 1] - s->xoff[(size_t)q]) * 4;
+            rp[l][(size_t)q] = s->d_ymap + s->gbase[(size_t)q];
+            rbytes[l][(size_t)q] = (uint64_t)s->gcnt[(size_t)q] * 4;
+        }
+    }
+    rc = g->take_tr(g->tr->alltoallv(sp, sbytes, rp, rbytes));
+    if (rc) return rc;
+    return sync_all(g);
+}
+
+int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg)
+{
+    if (!g || !cfg) return GSIM_EINVAL;
+    for (gsim_handle* h : g->hs) {
+        (void)hipSetDevice(h->device);
+        int rc = gsim_msgs_init(h, cfg);
+        if (rc) return g->take(h, rc);
+        ShardCtx* s = h->sh;
+        const int K = g->K;
+        int64_t xmax = 0, gmax = 0;
+        for (int q = 0; q < K; ++q) {
+            xmax = std::max<int64_t>(xmax, s->xoff[(size_t)q + 1] - s->xoff[(size_t)q]);
+            gmax = std::max<int64_t>(gmax, s->gcnt[(size_t)q]);
+        }
+        // per destination: a round's copies cross each cross edge at most once per
+        // message; max_frontier overrides (entries per destination shard)
+        s->xcap = cfg->max_frontier > 0 ? cfg->max_frontier : std::max<int64_t>(8 * xmax, 1 << 16);
+        s->ccap = std::max<int64_t>(4 * gmax, 1 << 14);
+        const int64_t ncross = s->xoff[(size_t)K];
+        rc = GSIM_OK;
+        auto A = [&](auto** p, size_t n) { if (!rc) rc = dalloc(h, p, n); };
+        A(&s->d_xout, (size_t)(K * s->xcap));
+        A(&s->d_xcnt, (size_t)K);
+        A(&s->d_xin_n, 1);
+        A(&s->d_cout, (size_t)(K * s->ccap));
+        A(&s->d_ccnt, (size_t)K);
+        A(&s->d_gout, (size_t)ncross);
+        A(&s->d_gsout, (size_t)ncross);
+        A(&s->d_gin, (size_t)h->e);
+        A(&s->d_gsin, (size_t)h->e);
+        A(&s->d_slot_last_g, (size_t)cfg->ring);
+        A(&s->d_act, (size_t)cfg->ring);
+        if (rc) return g->take(h, rc);
+        if (hipMemset(s->d_gin, 0, (size_t)h->e * 8) != hipSuccess || hipMemset(s->d_gsin, 0, (size_t)h->e) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "gossip mark buffers");
+    }
+    g->ring = cfg->ring;
+    g->rounds = cfg->rounds;
+    g->msgs = true;
+    return sync_all(g);
+}
+
+#define GROUP_EACH(g, call)                                      \
+    do {                                                         \
+        for (gsim_handle* h : (g)->hs) {                         \
+            int rc_ = (call);                                    \
+            if (rc_) return (g)->take(h, rc_);                   \
+        }                                                        \
+    } while (0)
+
+int gsim_group_set_seed(gsim_group* g, uint64_t seed) { GROUP_EACH(g, gsim_set_seed(h, seed)); return GSIM_OK; }
+
+int gsim_group_fill_synthetic(gsim_group* g, uint64_t seed, int64_t now, double p_mesh)
+{
+    GROUP_EACH(g, gsim_fill_synthetic(h, seed, now, p_mesh));
+    return GSIM_OK;
+}
+
+int gsim_group_set_app_score(gsim_group* g, const double* p5)
+{
+    if (!g || !p5) return GSIM_EINVAL;
+    for (size_t l = 0; l < g->hs.size(); ++l) {
+        std::vector<double> v(g->gid[l].size());
+        for (size_t x = 0; x < v.size(); ++x) v[x] = p5[g->gid[l][x]];
+        const int rc = gsim_set_app_score(g->hs[l], v.data());
+        if (rc) return g->take(g->hs[l], rc);
+    }
+    return GSIM_OK;
+}
+
+int gsim_group_set_ip_whitelist(gsim_group* g, const uint8_t* white)
+{
+    GROUP_EACH(g, gsim_set_ip_whitelist(h, white));
+    return GSIM_OK;
+}
+
+int gsim_group_set_direct_peers(gsim_group* g, const uint8_t* flags)
+{
+    if (!g) return GSIM_EINVAL;
+    for (size_t l = 0; l < g->hs.size(); ++l) {
+        int rc;
+        if (!flags) {
+            rc = gsim_set_direct_peers(g->hs[l], nullptr);
+        } else {
+            std::vector<uint8_t> v(g->gidx[l].size());
+            for (size_t x = 0; x < v.size(); ++x) v[x] = flags[g->gidx[l][x]];
+            rc = gsim_set_direct_peers(g->hs[l], v.data());
+        }
+        if (rc) return g->take(g->hs[l], rc);
+    }
+    return GSIM_OK;
+}
+
+int gsim_group_set_peer_behaviour(gsim_group* g, const uint8_t* flags)
+{
+    if (!g || !flags) return GSIM_EINVAL;
+    for (size_t l = 0; l < g->hs.size(); ++l) {
+        std::vector<uint8_t> v(g->gid[l].size());
+        for (size_t x = 0; x < v.size(); ++x) v[x] = flags[g->gid[l][x]];
+        const int rc = gsim_set_peer_behaviour(g->hs[l], v.data());
+        if (rc) return g->take(g->hs[l], rc);
+    }
+    return GSIM_OK;
+}
+
+int gsim_group_set_topic_params(gsim_group* g, int32_t topic, const gsim_topic_score_params* p)
+{
+    GROUP_EACH(g, gsim_set_topic_params(h, topic, p));
+    return GSIM_OK;
+}
+
+int gsim_group_refresh_scores(gsim_group* g, int64_t now)
+{
+    GROUP_EACH(g, gsim_refresh_scores(h, now));
+    return GSIM_OK;
+}
+
+int gsim_group_heartbeat(gsim_group* g, uint64_t tick, int64_t now)
+{
+    if (!g) return GSIM_EINVAL;
+    GROUP_EACH(g, gsim_heartbeat(h, tick, now));
+    int rc = exchange_control(g, 0);                 // GRAFT/PRUNE for control round 0
+    if (!rc) rc = exchange_gossip_marks(g);
+    return rc;
+}
+
+int gsim_group_publish(gsim_group* g, const gsim_msg* msgs, int32_t count, int64_t round)
+{
+    if (!g || count < 0 || (count > 0 && !msgs)) return GSIM_EINVAL;
+    for (size_t l = 0; l < g->hs.size(); ++l) {
+        std::vector<gsim_msg> v(msgs, msgs + count);
+        const std::vector<uint32_t>& gid = g->gid[l];
+        for (auto& m : v) {
+            auto it = std::lower_bound(gid.begin(), gid.end(), m.origin);
+            m.origin = (it != gid.end() && *it == m.origin) ? (uint32_t)(it - gid.begin()) : kNone;
+        }
+        const int rc = gsim_publish(g->hs[l], v.data(), count, round);
+        if (rc) return g->take(g->hs[l], rc);
+    }
+    return GSIM_OK;
+}
+
+int gsim_group_round(gsim_group* g, int64_t round)
+{
+    if (!g) return GSIM_EINVAL;
+    if (!g->msgs) return g->fail(GSIM_ESTATE, "gsim_group_msgs_init not called");
+    for (gsim_handle* h : g->hs) {
+        (void)hipSetDevice(h->device);
+        const int rc = deliver_round_send(h, round);
+        if (rc) return g->take(h, rc);
+    }
+    int rc = exchange_copies(g, round);
+    if (rc) return rc;
+    for (gsim_handle* h : g->hs) {
+        (void)hipSetDevice(h->device);
+        rc = deliver_round_post(h, round);
+        if (!rc) rc = deliver_round_control(h, round);
+        if (rc) return g->take(h, rc);
+    }
+    const int64_t r = round % g->rounds;
+    if (r < 2) {
+        rc = exchange_control(g, (int)((r + 1) & 1));   // PRUNE replies for the next control round
+        if (rc) return rc;
+    }
+    if (r == 0) {
+        rc = group_ihave(g, round);
+        if (rc) return rc;
+    }
+    for (gsim_handle* h : g->hs) deliver_round_end(h, round);
+    return GSIM_OK;
+}
+
+int gsim_group_set_connections(gsim_group* g, const uint32_t* pairs, int32_t count, int32_t up, int64_t now)
+{
+    if (!g || count < 0 || (count > 0 && !pairs)) return GSIM_EINVAL;
+    for (size_t l = 0; l < g->hs.size(); ++l) {
+        const std::vector<uint32_t>& gid = g->gid[l];
+        ShardCtx* s = g->hs[l]->sh;
+        auto loc = [&](uint32_t p) -> int64_t {
+            auto it = std::lower_bound(gid.begin(), gid.end(), p);
+            return (it != gid.end() && *it == p) ? (int64_t)(it - gid.begin()) : -1;
+        };
+        std::vector<uint32_t> v;
+        for (int32_t q = 0; q < count; ++q) {
+            const int64_t a = loc(pairs[2 * q]), b = loc(pairs[2 * q + 1]);
+            const bool own_a = a >= s->own_lo && a < s->own_hi, own_b = b >= s->own_lo && b < s->own_hi;
+            if (!own_a && !own_b) continue;                  // both endpoints elsewhere
+            if (a < 0 || b < 0) return g->fail(GSIM_EINVAL, "pair " + std::to_string(q) + " is not a connection");
+            v.push_back((uint32_t)a);
+            v.push_back((uint32_t)b);
+        }
+        const int rc = gsim_set_connections(g->hs[l], v.data(), (int32_t)(v.size() / 2), up, now);
+        if (rc) return g->take(g->hs[l], rc);
+    }
+    return GSIM_OK;
+}
+
+// Totals summed over the shards (every process gets the job's totals).
+static int group_sum(gsim_group* g, int (*fn)(gsim_handle*, int64_t*), int n, int64_t* out)
+{
+    std::vector<int64_t> acc((size_t)n, 0), v((size_t)n);
+    int first_err = GSIM_OK;
+    for (gsim_handle* h : g->hs) {
+        const int rc = fn(h, v.data());
+        if (rc && !first_err) { first_err = rc; g->err = "shard: " + h->err; }
+        for (int i = 0; i < n; ++i) acc[(size_t)i] += v[(size_t)i];
+    }
+    if (dynamic_cast<RcclTransport*>(g->tr.get())) {
+        gsim_handle* h = g->hs[0];
+        int64_t* d = nullptr;
+        if (hipMalloc((void**)&d, sizeof(int64_t) * (n + 1)) != hipSuccess) return g->fail(GSIM_ENOMEM, "totals scratch");
+        acc.push_back(first_err ? 1 : 0);
+        (void)hipMemcpy(d, acc.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice);
+        int rc = g->take_tr(g->tr->allreduce({d}, n + 1, DT_U64, OP_SUM));
+        if (!rc) rc = g->take_tr(g->tr->sync());
+        (void)hipMemcpy(acc.data(), d, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost);
+        (void)hipFree(d);
+        (void)h;
+        if (rc) return rc;
+        if (acc[(size_t)n] && !first_err) { first_err = GSIM_ERANGE; g->err = "another shard reported an error"; }
+    }
+    for (int i = 0; i < n; ++i) out[i] = acc[(size_t)i];
+    return first_err;
+}
+
+int gsim_group_msg_stats(gsim_group* g, int64_t* out4)
+{
+    if (!g || !out4) return GSIM_EINVAL;
+    return group_sum(g, gsim_msg_stats, 4, out4);
+}
+
+int gsim_group_gossip_stats(gsim_group* g, int64_t* out4)
+{
+    if (!g || !out4) return GSIM_EINVAL;
+    return group_sum(g, gsim_gossip_stats, 4, out4);
+}
+
+int gsim_group_census(gsim_group* g, int64_t* out8)
+{
+    if (!g || !out8) return GSIM_EINVAL;
+    return group_sum(g, gsim_census, 8, out8);
+}
+
+int gsim_group_synchronize(gsim_group* g)
+{
+    if (!g) return GSIM_EINVAL;
+    return sync_all(g);
+}
+
+int gsim_group_profile(gsim_group* g, int32_t enable)
+{
+    GROUP_EACH(g, gsim_profile(h, enable));
+    return GSIM_OK;
+}
+
+int gsim_group_profile_read(gsim_group* g, double* ms, int64_t* launches, int32_t n)
+{
+    if (!g || n < 0) return GSIM_EINVAL;
+    std::vector<double> m((size_t)n);
+    std::vector<int64_t> c((size_t)n);
+    for (int32_t i = 0; i < n; ++i) { ms[i] = 0.0; launches[i] = 0; }
+    for (gsim_handle* h : g->hs) {
+        const int rc = gsim_profile_read(h, m.data(), c.data(), n);
+        if (rc) return g->take(h, rc);
+        for (int32_t i = 0; i < n; ++i) { ms[i] += m[(size_t)i]; launches[i] += c[(size_t)i]; }
+    }
+    return GSIM_OK;
+}
+
+}  // extern "C"

@@ -167,6 +167,38 @@ SIGNATURES = [
                                          POINTER(CShardInfo)]),
     ("gsim_shard_layout", c_int32, [c_int64, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("gsim_rccl_unique_id", c_int32, [c_void_p, c_size_t]),
+    ("gsim_group_create", c_int32,
+     [POINTER(CPeerScoreParams), POINTER(CTopicScoreParams), c_int32, POINTER(CThresholds),
+      POINTER(CGossipSubParams), c_int32, c_void_p, POINTER(c_void_p), c_char_p, c_size_t]),
+    ("gsim_group_create_rccl", c_int32,
+     [POINTER(CPeerScoreParams), POINTER(CTopicScoreParams), c_int32, POINTER(CThresholds),
+      POINTER(CGossipSubParams), c_int32, c_int32, c_int32, c_void_p, POINTER(c_void_p), c_char_p, c_size_t]),
+    ("gsim_group_destroy", c_int32, [c_void_p]),
+    ("gsim_group_last_error", c_char_p, [c_void_p]),
+    ("gsim_group_shard", c_void_p, [c_void_p, c_int32]),
+    ("gsim_group_bounds", c_int32, [c_void_p, c_void_p]),
+    ("gsim_group_load_graph", c_int32,
+     [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]),
+    ("gsim_group_set_app_score", c_int32, [c_void_p, c_void_p]),
+    ("gsim_group_set_ip_whitelist", c_int32, [c_void_p, c_void_p]),
+    ("gsim_group_set_direct_peers", c_int32, [c_void_p, c_void_p]),
+    ("gsim_group_set_peer_behaviour", c_int32, [c_void_p, c_void_p]),
+    ("gsim_group_set_topic_params", c_int32, [c_void_p, c_int32, POINTER(CTopicScoreParams)]),
+    ("gsim_group_set_seed", c_int32, [c_void_p, c_uint64]),
+    ("gsim_group_fill_synthetic", c_int32, [c_void_p, c_uint64, c_int64, c_double]),
+    ("gsim_group_msgs_init", c_int32, [c_void_p, POINTER(CMsgConfig)]),
+    ("gsim_group_refresh_scores", c_int32, [c_void_p, c_int64]),
+    ("gsim_group_heartbeat", c_int32, [c_void_p, c_uint64, c_int64]),
+    ("gsim_group_publish", c_int32, [c_void_p, c_void_p, c_int32, c_int64]),
+    ("gsim_group_round", c_int32, [c_void_p, c_int64]),
+    ("gsim_group_set_connections", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int64]),
+    ("gsim_group_msg_stats", c_int32, [c_void_p, c_void_p]),
+    ("gsim_group_gossip_stats", c_int32, [c_void_p, c_void_p]),
+    ("gsim_group_census", c_int32, [c_void_p, c_void_p]),
+    ("gsim_group_synchronize", c_int32, [c_void_p]),
+    ("gsim_group_profile", c_int32, [c_void_p, c_int32]),
+    ("gsim_group_profile_read", c_int32, [c_void_p, c_void_p, c_void_p, c_int32]),
 ]
 
 _lib = None

@@ -126,3 +126,259 @@ def plan(net: Network, shards: int, bounds: Optional[np.ndarray] = None) -> List
     """Partition `net` and build every shard's local graph."""
     b = partition(net, shards) if bounds is None else np.asarray(bounds, dtype=np.int64)
     return [ShardPlan.build(net, b, s) for s in range(len(b) - 1)]
+
+
+class ShardedEngine:
+    """One simulated network split over shards (gsim_group_*): the Engine API
+    with global peer / edge indexing.  In-process (``shards`` handles in this
+    process, device copies between them) or one shard of an RCCL job
+    (``rccl=(rank, unique_id, device)``, one process per GPU)."""
+
+    def __init__(self, params, thresholds, gossip=None, topics=None, shards: int = 2, devices=None,
+                 rccl=None):
+        """Parameters are validated like WithPeerScore (gossipsub.go:278-319)
+        by every shard's gsim_create."""
+        from .engine import Engine
+        from .params import GossipSubParams
+        self.lib = _abi.load()
+        self.params = params
+        self.thresholds = thresholds
+        self.gossip = gossip or GossipSubParams()
+        self.topics = sorted(set(topics or []) | set(params.Topics))
+        self.topic_index = {t: i for i, t in enumerate(self.topics)}
+        self.shards = shards
+        pc, tc, gc = params.to_c(), thresholds.to_c(), self.gossip.to_c()
+        self._tarr = params.topic_array(self.topics)
+        g = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(512)
+        if rccl is None:
+            dev = None if devices is None else (ctypes.c_int32 * shards)(*devices)
+            rc = self.lib.gsim_group_create(ctypes.byref(pc), self._tarr, len(self.topics), ctypes.byref(tc),
+                                            ctypes.byref(gc), shards, dev, ctypes.byref(g), buf, len(buf))
+            self.local = list(range(shards))
+        else:
+            rank, uid, device = rccl
+            ub = ctypes.create_string_buffer(bytes(uid), 128)
+            rc = self.lib.gsim_group_create_rccl(ctypes.byref(pc), self._tarr, len(self.topics), ctypes.byref(tc),
+                                                 ctypes.byref(gc), shards, rank, device, ub, ctypes.byref(g), buf,
+                                                 len(buf))
+            self.local = [rank]
+        if rc != 0:
+            raise GsimError(rc, buf.value.decode())
+        self.g = g
+        self.net: Optional[Network] = None
+        self.plans: List[ShardPlan] = []
+        self._msg_cfg = None
+        self._engine_cls = Engine
+
+    @staticmethod
+    def rccl_unique_id() -> bytes:
+        lib = _abi.load()
+        b = ctypes.create_string_buffer(128)
+        rc = lib.gsim_rccl_unique_id(b, 128)
+        if rc != 0:
+            raise GsimError(rc, "ncclGetUniqueId failed")
+        return b.raw
+
+    def close(self):
+        if getattr(self, "g", None):
+            self.lib.gsim_group_destroy(self.g)
+            self.g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int):
+        if rc != 0:
+            msg = self.lib.gsim_group_last_error(self.g)
+            msg = msg.decode() if msg else ""
+            if rc == _abi.GSIM_EINVAL:
+                raise ValueError(msg)
+            raise GsimError(rc, msg)
+
+    # -- setup ------------------------------------------------------------------------
+    def load_graph(self, net: Network, bounds: Optional[np.ndarray] = None):
+        b = None if bounds is None else np.ascontiguousarray(bounds, dtype=np.int64)
+        self._check(self.lib.gsim_group_load_graph(self.g, net.n, _ptr(net.row_ptr), _ptr(net.col), _ptr(net.outbound),
+                                                   _ptr(net.sub), _ptr(net.ip_ptr), _ptr(net.ip_ids), net.n_ips,
+                                                   _ptr(b)))
+        self.net = net
+        self.bounds = np.zeros(self.shards + 1, dtype=np.int64)
+        self._check(self.lib.gsim_group_bounds(self.g, _ptr(self.bounds)))
+        self.plans = [ShardPlan.build(net, self.bounds, s) for s in self.local]
+        if self.params.AppSpecificScore is not None:
+            from .engine import app_scores
+            self.set_app_score(app_scores(self.params.AppSpecificScore, net.n))
+
+    def set_app_score(self, p5: np.ndarray):
+        p5 = np.ascontiguousarray(p5, dtype=np.float64)
+        self._check(self.lib.gsim_group_set_app_score(self.g, _ptr(p5)))
+
+    def set_ip_whitelist(self, white: Optional[np.ndarray]):
+        w = None if white is None else np.ascontiguousarray(white, dtype=np.uint8)
+        self._check(self.lib.gsim_group_set_ip_whitelist(self.g, _ptr(w)))
+
+    def set_direct_peers(self, flags):
+        f = None if flags is None else np.ascontiguousarray(flags, dtype=np.uint8)
+        self._check(self.lib.gsim_group_set_direct_peers(self.g, _ptr(f)))
+
+    def set_peer_behaviour(self, flags: np.ndarray):
+        f = np.ascontiguousarray(flags, dtype=np.uint8)
+        self._check(self.lib.gsim_group_set_peer_behaviour(self.g, _ptr(f)))
+
+    def set_topic_score_params(self, topic: str, p):
+        c = p.to_c(True)
+        self._check(self.lib.gsim_group_set_topic_params(self.g, self.topic_index[topic], ctypes.byref(c)))
+        self.params.Topics[topic] = p
+
+    def set_seed(self, seed: int):
+        self._check(self.lib.gsim_group_set_seed(self.g, int(seed)))
+
+    def fill_synthetic(self, seed: int, now: int, p_mesh: float):
+        self._check(self.lib.gsim_group_fill_synthetic(self.g, int(seed), int(now), float(p_mesh)))
+
+    # -- hot path -------------------------------------------------------------------
+    def msgs_init(self, ring: int, rounds: int, t0: int, heartbeat: Optional[int] = None,
+                  max_frontier: Optional[int] = None, max_arrivals: Optional[int] = None):
+        c = _abi.CMsgConfig()
+        c.ring, c.rounds, c.t0_ns = int(ring), int(rounds), int(t0)
+        c.heartbeat_ns = int(heartbeat if heartbeat is not None else self.gossip.HeartbeatInterval)
+        c.max_frontier = int(max_frontier or 0)      # copies queued per destination shard per round
+        c.max_arrivals = int(max_arrivals or 0)
+        self._check(self.lib.gsim_group_msgs_init(self.g, ctypes.byref(c)))
+        self._msg_cfg = c
+
+    def refresh_scores(self, now: int):
+        self._check(self.lib.gsim_group_refresh_scores(self.g, int(now)))
+
+    def heartbeat(self, tick: int, now: int):
+        self._check(self.lib.gsim_group_heartbeat(self.g, int(tick), int(now)))
+
+    def publish(self, msgs, rnd: int):
+        arr = np.zeros(len(msgs), dtype=_abi.MSG_DTYPE)
+        for k, (mid, topic, origin, invalid) in enumerate(msgs):
+            arr[k]["id"], arr[k]["topic"], arr[k]["origin"], arr[k]["invalid"] = mid, topic, origin, invalid
+        self.publish_array(arr, rnd)
+
+    def publish_array(self, arr: np.ndarray, rnd: int):
+        a = np.ascontiguousarray(arr)
+        self._check(self.lib.gsim_group_publish(self.g, _ptr(a), len(a), int(rnd)))
+
+    def round(self, rnd: int):
+        self._check(self.lib.gsim_group_round(self.g, int(rnd)))
+
+    def set_connections(self, pairs, up: bool, now: int):
+        p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint32).reshape(-1, 2))
+        self._check(self.lib.gsim_group_set_connections(self.g, _ptr(p), int(p.shape[0]), 1 if up else 0, int(now)))
+
+    def msg_stats(self) -> list:
+        out = np.zeros(4, dtype=np.int64)
+        self._check(self.lib.gsim_group_msg_stats(self.g, _ptr(out)))
+        return [int(x) for x in out]
+
+    def gossip_stats(self) -> dict:
+        out = np.zeros(4, dtype=np.int64)
+        self._check(self.lib.gsim_group_gossip_stats(self.g, _ptr(out)))
+        return dict(zip(["ihave_walks", "iwant_ids", "iwant_responses", "broken_promises"], (int(x) for x in out)))
+
+    def census(self) -> dict:
+        out = np.zeros(8, dtype=np.int64)
+        self._check(self.lib.gsim_group_census(self.g, _ptr(out)))
+        keys = ["records", "in_mesh", "nz_first", "nz_meshd", "nz_fail", "nz_invalid", "mesh_links", "tracked_edges"]
+        return {k: int(v) for k, v in zip(keys, out)}
+
+    def synchronize(self):
+        self._check(self.lib.gsim_group_synchronize(self.g))
+
+    def profile(self, enable: bool = True):
+        self._check(self.lib.gsim_group_profile(self.g, int(bool(enable))))
+
+    def profile_read(self) -> dict:
+        n = len(_abi.KERNEL_CLASSES)
+        ms = np.zeros(n, dtype=np.float64)
+        cnt = np.zeros(n, dtype=np.int64)
+        self._check(self.lib.gsim_group_profile_read(self.g, _ptr(ms), _ptr(cnt), n))
+        return {c: (float(ms[i]), int(cnt[i])) for i, c in enumerate(_abi.KERNEL_CLASSES)}
+
+    # -- state in the whole network's view (this process's shards) --------------------
+    _PEER_LAST = {_abi.F_SEEN, _abi.F_LASTPUT}          # [..., N]
+    _PEER_FIRST = {_abi.F_LASTPUB, _abi.F_FANOUT_TOPICS}   # [N, ...]
+
+    def _shard_handle(self, s: int):
+        h = self.lib.gsim_group_shard(self.g, s)
+        if not h:
+            raise GsimError(_abi.GSIM_EINVAL, f"shard {s} is not in this process")
+        return ctypes.c_void_p(h)
+
+    def _shape(self, f: int, n: int, e: int):
+        T = max(1, len(self.topics))
+        from .engine import PARITY_TOPIC_FIELDS, TOPIC_FIELDS
+        if f in PARITY_TOPIC_FIELDS:
+            return (2, T, e)
+        if f == _abi.F_SEEN:
+            return (self._msg_cfg.ring, n)
+        if f == _abi.F_LASTPUT:
+            return (T, n)
+        if f == _abi.F_LASTPUB:
+            return (n, T)
+        if f == _abi.F_FANOUT_TOPICS:
+            return (n,)
+        return (T, e) if f in TOPIC_FIELDS else (e,)
+
+    def read_local(self, s: int, f: int) -> np.ndarray:
+        """Shard s's field in its local view."""
+        from .engine import _FIELD_DTYPES
+        p = self.plans[self.local.index(s)]
+        out = np.empty(self._shape(f, p.n_local, p.e_local), dtype=_FIELD_DTYPES[f])
+        h = self._shard_handle(s)
+        rc = self.lib.gsim_read_field(h, f, _ptr(out), out.nbytes)
+        if rc != 0:
+            raise GsimError(rc, (self.lib.gsim_last_error(h) or b"").decode())
+        return out
+
+    def read(self, f: int) -> np.ndarray:
+        """A field of the whole network, assembled from the owned parts of
+        every shard (every shard must be in this process)."""
+        from .engine import _FIELD_DTYPES
+        if len(self.local) != self.shards:
+            raise GsimError(_abi.GSIM_EINVAL, "the whole network's view needs every shard in this process")
+        out = np.zeros(self._shape(f, self.net.n, self.net.e), dtype=_FIELD_DTYPES[f])
+        for p in self.plans:
+            loc = self.read_local(p.shard, f)
+            if f in self._PEER_LAST:
+                out[..., p.bounds[p.shard]:p.bounds[p.shard + 1]] = loc[..., p.own_lo:p.own_hi]
+            elif f in self._PEER_FIRST:
+                out[p.bounds[p.shard]:p.bounds[p.shard + 1]] = loc[p.own_lo:p.own_hi]
+            else:
+                sl = p.global_edges()
+                out[..., sl] = loc[..., p.own_e_lo:p.own_e_hi]
+        return out
+
+    def write(self, f: int, arr: np.ndarray):
+        """Install a field given in the whole network's view on every local shard."""
+        from .engine import _FIELD_DTYPES
+        a = np.asarray(arr, dtype=_FIELD_DTYPES[f]).reshape(self._shape(f, self.net.n, self.net.e))
+        for p in self.plans:
+            if f in self._PEER_LAST:
+                loc = p.peer_view(a, axis=-1)
+            elif f in self._PEER_FIRST:
+                loc = p.peer_view(a, axis=0)
+            else:
+                loc = p.edge_view(a)
+            h = self._shard_handle(p.shard)
+            loc = np.ascontiguousarray(loc)
+            rc = self.lib.gsim_write_field(h, f, _ptr(loc), loc.nbytes)
+            if rc != 0:
+                raise GsimError(rc, (self.lib.gsim_last_error(h) or b"").decode())
+
+    def scores(self) -> np.ndarray:
+        return self.read(_abi.F_SCORE)

@@ -450,6 +450,59 @@ int gsim_shard_layout(int64_t n, const uint32_t* row_ptr, const uint32_t* col, c
                       uint64_t* gidx, int64_t* ghost_base, int64_t* ghost_count, uint32_t* cross_out,
                       int64_t* cross_count);
 
+/* A sharded network: a group of shards, each an engine handle over its
+ * local graph.  gsim_group_create puts every shard in this process (shard s
+ * on devices[s]; devices NULL: all on device 0), exchanging with device
+ * copies.  gsim_group_create_rccl is one shard of a multi-process job (one
+ * process per GPU): `unique_id` comes from gsim_rccl_unique_id on rank 0,
+ * shared by the caller (128 bytes), and the exchanges run over RCCL. */
+typedef struct gsim_group gsim_group;
+int gsim_rccl_unique_id(void* out, size_t bytes);
+int gsim_group_create(const gsim_peer_score_params* params, const gsim_topic_score_params* topics, int32_t n_topics,
+                      const gsim_thresholds* thresholds, const gsim_gossipsub_params* gossip, int32_t shards,
+                      const int32_t* devices, gsim_group** out, char* err, size_t errlen);
+int gsim_group_create_rccl(const gsim_peer_score_params* params, const gsim_topic_score_params* topics,
+                           int32_t n_topics, const gsim_thresholds* thresholds, const gsim_gossipsub_params* gossip,
+                           int32_t shards, int32_t rank, int32_t device, const void* unique_id, gsim_group** out,
+                           char* err, size_t errlen);
+int gsim_group_destroy(gsim_group* g);
+const char* gsim_group_last_error(const gsim_group* g);
+/* The handle of a shard hosted by this process (NULL otherwise): its state is
+ * read and written through the gsim_*_field calls in the local view (owned
+ * rows are edges [own_e_lo, own_e_hi) of gsim_shard_layout_info). */
+gsim_handle* gsim_group_shard(gsim_group* g, int32_t shard);
+int gsim_group_bounds(const gsim_group* g, int64_t* bounds);
+/* The whole network's CSR and inputs, as for gsim_load_graph (every process
+ * passes the same); bounds NULL: gsim_shard_partition. */
+int gsim_group_load_graph(gsim_group* g, int64_t n_peers, const uint32_t* row_ptr, const uint32_t* col_idx,
+                          const uint8_t* outbound, const uint64_t* subscriptions, const uint32_t* ip_ptr,
+                          const uint32_t* ip_ids, uint32_t n_ips, const int64_t* bounds);
+/* The single-handle calls over the whole network (global peer / edge
+ * indexing; the per-round halo exchange happens inside). */
+int gsim_group_set_app_score(gsim_group* g, const double* p5);
+int gsim_group_set_ip_whitelist(gsim_group* g, const uint8_t* whitelisted);
+int gsim_group_set_direct_peers(gsim_group* g, const uint8_t* flags);
+int gsim_group_set_peer_behaviour(gsim_group* g, const uint8_t* flags);
+int gsim_group_set_topic_params(gsim_group* g, int32_t topic, const gsim_topic_score_params* p);
+int gsim_group_set_seed(gsim_group* g, uint64_t seed);
+int gsim_group_fill_synthetic(gsim_group* g, uint64_t seed, int64_t now_ns, double p_mesh);
+/* max_frontier > 0 caps the copies one shard queues for another per round
+ * (default 8 x their cross edges); GSIM_ERANGE when a round exceeds it. */
+int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg);
+int gsim_group_refresh_scores(gsim_group* g, int64_t now_ns);
+int gsim_group_heartbeat(gsim_group* g, uint64_t tick, int64_t now_ns);
+int gsim_group_publish(gsim_group* g, const gsim_msg* msgs, int32_t count, int64_t round);
+int gsim_group_round(gsim_group* g, int64_t round);
+int gsim_group_set_connections(gsim_group* g, const uint32_t* pairs, int32_t count, int32_t up, int64_t now_ns);
+/* Totals of the whole job (summed over every shard, every process). */
+int gsim_group_msg_stats(gsim_group* g, int64_t* out4);
+int gsim_group_gossip_stats(gsim_group* g, int64_t* out4);
+int gsim_group_census(gsim_group* g, int64_t* out8);
+int gsim_group_synchronize(gsim_group* g);
+/* Per-kernel-class time of this process's shards (summed). */
+int gsim_group_profile(gsim_group* g, int32_t enable);
+int gsim_group_profile_read(gsim_group* g, double* ms, int64_t* launches, int32_t n);
+
 #ifdef __cplusplus
 }
 #endif

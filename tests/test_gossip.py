@@ -178,8 +178,8 @@ def test_gossip_rounds_bit_exact(require_gpu, n, k, T, nticks, rate, ignore_frac
 @pytest.mark.gpu
 def test_iwant_response_queue_overflow_is_reported(require_gpu):
     """A response queue smaller than the IWANT traffic: the overflow is
-    reported by gsim_msg_stats (GSIM_ERANGE) and nothing past the queue is
-    read or written."""
+    reported by the next heartbeat and by gsim_msg_stats (GSIM_ERANGE), and
+    nothing past the queue is read or written."""
     from fixtures import beacon_params, synthetic_state
     from gsim.engine import Engine, GsimError, random_regular
     from test_delivery import _schedule
@@ -198,14 +198,20 @@ def test_iwant_response_queue_overflow_is_reported(require_gpu):
     eng.msgs_init(256, R, T0, Second, max_arrivals=4)
     ticks = list(range(1, 6))
     sched = _schedule(rng, ticks, T, R, 10, 0.0, n)
+    stopped = None
     for kk in ticks:
         now = tick_time(kk)
         eng.refresh_scores(now)
-        eng.heartbeat(kk, now)
+        try:
+            eng.heartbeat(kk, now)
+        except GsimError as ex:          # the previous tick overflowed: stop before running on
+            stopped = (kk, ex.rc)
+            break
         for g in range(kk * R, kk * R + R):
             if g in sched:
                 eng.publish(sched[g], g)
             eng.round(g)
+    assert stopped is not None and stopped[1] == _abi.GSIM_ERANGE
     with pytest.raises(GsimError) as ei:
         eng.msg_stats()
     assert ei.value.rc == _abi.GSIM_ERANGE
