@@ -46,17 +46,19 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 // summary `cany`), one thread per ghost peer with a summary bit: entries
 // (owner shard's edge | topic << 32 | bits << 40) to the ghost's shard.
 __global__ __launch_bounds__(256) void k_ctl_export(uint8_t* ctl, uint64_t* cany, const uint32_t* row_ptr,
-                                                    const uint32_t* ymap, const uint8_t* pshard, int64_t E,
+                                                    const uint32_t* ymap, const uint8_t* pshard, int64_t E, int32_t T,
                                                     int64_t olo, int64_t ohi, int64_t n, uint64_t* out,
                                                     uint32_t* cnt, int64_t cap)
 {
+    // a summary word may be a superset (all ones after an ABI write of the inbox)
+    const uint64_t tmask = T >= 64 ? ~0ull : ((1ull << T) - 1);
     const int64_t nghost = olo + (n - ohi);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < nghost; x += stride) {
         const int64_t g = x < olo ? x : ohi + (x - olo);
-        uint64_t any = cany[g];
+        uint64_t any = cany[g] & tmask;
+        if (cany[g]) cany[g] = 0;
         if (!any) continue;
-        cany[g] = 0;
         const uint32_t d = pshard[g];
         for (; any; any &= any - 1) {
             const int32_t t = __ffsll((long long)any) - 1;
@@ -421,7 +423,7 @@ int exchange_control(gsim_group* g, int parity)
         const int64_t nghost = s->own_lo + (h->n - s->own_hi);
         hipLaunchKernelGGL(k_ctl_export, dim3(grid_for(nghost)), dim3(256), 0, h->stream, ctl, cany,
                            (const uint32_t*)h->d_row_ptr, (const uint32_t*)s->d_ymap, (const uint8_t*)s->d_pshard,
-                           h->e, s->own_lo, s->own_hi, h->n, s->d_cout, s->d_ccnt, s->ccap);
+                           h->e, std::max(1, h->t), s->own_lo, s->own_hi, h->n, s->d_cout, s->d_ccnt, s->ccap);
         if (hipMemcpyAsync(s->h_counts, s->d_ccnt, sizeof(uint32_t) * K, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
             hipStreamSynchronize(h->stream) != hipSuccess)
             return g->fail(GSIM_EDEVICE, "control counts");
