@@ -16,9 +16,11 @@ device sync; max over ranks; rank 0 prints one JSON line.  Per-kernel-class
 device time comes from HIP events recorded on the engine stream around every
 launch inside the timed region (gsim_profile).
 
-Multi-GPU: each rank simulates its own 1M-peer network on its own GPU (weak
-scaling, "replicas only" until the sharded halo-exchange path lands;
-DESIGN.md §5).
+Multi-GPU: the one network is graph-sharded over the ranks
+(contiguous peer ranges, one shard per GPU), with the halo exchange of message
+copies, GRAFT/PRUNE records, gossip marks and IHAVE holders over RCCL
+(strong scaling: the same 1M-peer network at every N).  --replicas runs one
+independent network per rank instead (weak scaling).
 """
 from __future__ import annotations
 
@@ -134,7 +136,9 @@ def build_network(cfg, seed, scen=None):
     return net, beh
 
 
-def build_engine(cfg, seed, device, scen=None):
+def build_engine(cfg, seed, device, scen=None, shard=None):
+    """The bench network on one GPU, or (shard = (rank, world, unique_id))
+    this rank's shard of it (gsim.shard.ShardedEngine over RCCL)."""
     import gsim
     from gsim.presets import beacon_params, beacon_thresholds
     n, k, T, D, Dlo, Dhi = cfg
@@ -143,7 +147,15 @@ def build_engine(cfg, seed, device, scen=None):
     gp = gsim.GossipSubParams(D=D, Dlo=Dlo, Dhi=Dhi)
     if "opp_ticks" in scen:
         gp.OpportunisticGraftTicks = scen["opp_ticks"]
-    eng = gsim.Engine(params, beacon_thresholds(), gossip=gp, device=device)
+    if shard is None:
+        eng = gsim.Engine(params, beacon_thresholds(), gossip=gp, device=device)
+    elif isinstance(shard, int):          # every shard in this process, on this device
+        from gsim.shard import ShardedEngine
+        eng = ShardedEngine(params, beacon_thresholds(), gossip=gp, shards=shard, devices=[device] * shard)
+    else:
+        from gsim.shard import ShardedEngine
+        rank, world, uid = shard
+        eng = ShardedEngine(params, beacon_thresholds(), gossip=gp, shards=world, rccl=(rank, uid, device))
     net, beh = build_network(cfg, seed, scen)
     eng.load_graph(net)
     eng.set_seed(0x5EED0000 + seed)
@@ -151,7 +163,7 @@ def build_engine(cfg, seed, device, scen=None):
     eng.msgs_init(scen.get("ring", MSG_RING), ROUNDS, tick_time(0), SECOND)
     if beh is not None:
         eng.set_peer_behaviour(beh)
-    if os.environ.get("GSIM_SEND_VARIANT"):          # A/B of the delivery kernel variants (gsim.h)
+    if os.environ.get("GSIM_SEND_VARIANT") and shard is None:   # A/B of the delivery kernel (gsim.h)
         eng.set_kernel_variant(2, int(os.environ["GSIM_SEND_VARIANT"]))
     return eng, net
 
@@ -293,6 +305,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--replicas", action="store_true",
+                    help="N > 1: one independent network per rank (weak scaling) instead of one sharded network")
+    ap.add_argument("--shards", type=int, default=1,
+                    help="N = 1: split the network into this many shards on the one GPU (exercises the halo "
+                         "exchange through the in-process transport; not the headline configuration)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -308,8 +325,21 @@ def main():
     cfg = CONFIGS[args.config]
     scen = SCENARIOS.get(args.config, {})
     n, k, T = cfg[0], cfg[1], cfg[2]
-    g_seed, s_seed = replica_seeds(rank)
-    eng, net = build_engine(cfg, seed=g_seed, device=local, scen=scen)
+    sharded = (world > 1 and not args.replicas) or args.shards > 1
+    shard = None
+    if args.shards > 1 and world == 1:
+        g_seed, s_seed = replica_seeds(0)
+        shard = args.shards
+    elif sharded:
+        # one network over every rank: same graph / schedule seeds, RCCL id from rank 0
+        g_seed, s_seed = replica_seeds(0)
+        from gsim.shard import ShardedEngine
+        box = [ShardedEngine.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        shard = (rank, world, box[0])
+    else:
+        g_seed, s_seed = replica_seeds(rank)
+    eng, net = build_engine(cfg, seed=g_seed, device=local, scen=scen, shard=shard)
     E = net.e
     ticks = range(1, args.warmup + args.steps + 1)
     rate = scen.get("msg_rate", MSG_RATE)
@@ -324,6 +354,7 @@ def main():
     census0 = eng.census()
     stats0 = eng.msg_stats()
     gossip0 = eng.gossip_stats()
+    local_stats0 = eng.local_msg_stats() if sharded else stats0
 
     def barrier():
         if dist is not None:
@@ -344,25 +375,36 @@ def main():
     wall = time.perf_counter() - t0
     prof = eng.profile_read()
     eng.profile(False)
+    local_stats1 = eng.local_msg_stats() if sharded else None
     census1 = eng.census()
     stats1 = eng.msg_stats()
     gossip1 = eng.gossip_stats()
-    wall, deliveries = job_totals(wall, float(stats1[0] - stats0[0]), dist, f"cuda:{local}")
+    if sharded:
+        # group totals are already the whole job's: only the wall time is reduced
+        wall, _ = job_totals(wall, 0.0, dist, f"cuda:{local}")
+        deliveries = float(stats1[0] - stats0[0])
+    else:
+        wall, deliveries = job_totals(wall, float(stats1[0] - stats0[0]), dist, f"cuda:{local}")
 
     if rank == 0:
         K = args.steps
         workload = (f"{args.config}: {n} peers, {describe_graph(cfg, scen)}, {T} topics, beacon-style params, "
                     f"{rate:g} msg/s/topic, {ROUNDS} rounds/heartbeat")
-        value = n * world * K / wall
+        # peer-heartbeats of the whole job: one network (sharded) or one per rank
+        value = n * (1 if sharded else world) * K / wall
         kms = {c: ms / K for c, (ms, _) in prof.items()}        # per tick
         launches = {c: cnt for c, (_, cnt) in prof.items()}
         # refresh+score: census-based compulsory bytes per launch
         alg_refresh = (refresh_bytes(census0, E) + refresh_bytes(census1, E)) // 2
+        if sharded and world > 1:   # the kernels timed are rank 0's shard: its share of the network
+            alg_refresh = alg_refresh // world
         ref_ms = prof["refresh_score"][0] / max(1, launches["refresh_score"])
         ref_gbs = alg_refresh / (ref_ms * 1e-3) / 1e9
         # delivery: SURVEY.md §8(d) bytes per first / duplicate delivery, over send+commit(+accept)
         firsts = stats1[1] - stats0[1]
         dups = stats1[2] - stats0[2]
+        if sharded:   # ... and the deliveries to its peers
+            firsts, dups = (s1 - s0 for s1, s0 in zip(local_stats1[1:3], local_stats0[1:3]))
         alg_deliv = (FIRST_BYTES * firsts + DUP_BYTES * dups) / K
         deliv_ms = kms["send"] + kms["commit"] + kms["accept"]
         deliv_gbs = alg_deliv / (deliv_ms * 1e-3) / 1e9 if deliv_ms > 0 else 0.0
@@ -389,7 +431,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": wall / K * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": f"synthetic (seeded {'power-law' if 'power_law' in scen else 'random-regular'} graph, "
@@ -398,10 +440,12 @@ def main():
                        "edge_topic_records": E * T, "rounds_per_heartbeat": ROUNDS,
                        "step": "heartbeat tick: refreshScores+score, mesh maintenance, "
                                f"{ROUNDS} propagation rounds (publish, deliver, control, forward)",
-                       "parallelism": f"replica-per-gpu x{world}"},
+                       "parallelism": (f"graph-sharded x{world} (RCCL halo exchange)" if sharded and world > 1
+                                       else f"graph-sharded x{args.shards} on one GPU (in-process exchange)"
+                                       if sharded else f"replica-per-gpu x{world}")},
             "msg_edge_deliveries_per_sec": deliveries / wall,
-            "deliveries_per_tick": {"accepted": (stats1[0] - stats0[0]) / K, "first": firsts / K,
-                                    "duplicate": dups / K, "graylisted": (stats1[3] - stats0[3]) / K},
+            "deliveries_per_tick": {"accepted": (stats1[0] - stats0[0]) / K, "first": (stats1[1] - stats0[1]) / K,
+                                    "duplicate": (stats1[2] - stats0[2]) / K, "graylisted": (stats1[3] - stats0[3]) / K},
             "kernel_ms_per_tick": kms,
             "gossip_per_tick": {k: (gossip1[k] - gossip0[k]) / K for k in gossip1},
             "census": census1,

@@ -285,6 +285,18 @@ class ShardedEngine:
         self._check(self.lib.gsim_group_msg_stats(self.g, _ptr(out)))
         return [int(x) for x in out]
 
+    def local_msg_stats(self) -> list:
+        """gsim_msg_stats of this process's shards only (deliveries to their peers)."""
+        tot = np.zeros(4, dtype=np.int64)
+        for s in self.local:
+            out = np.zeros(4, dtype=np.int64)
+            h = self._shard_handle(s)
+            rc = self.lib.gsim_msg_stats(h, _ptr(out))
+            if rc != 0:
+                raise GsimError(rc, (self.lib.gsim_last_error(h) or b"").decode())
+            tot += out
+        return [int(x) for x in tot]
+
     def gossip_stats(self) -> dict:
         out = np.zeros(4, dtype=np.int64)
         self._check(self.lib.gsim_group_gossip_stats(self.g, _ptr(out)))
