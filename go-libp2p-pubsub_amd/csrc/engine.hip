@@ -930,6 +930,38 @@ int gsim_set_direct_peers(gsim_handle* h, const uint8_t* direct)
     return hip_check(h, e, "gsim_set_direct_peers");
 }
 
+int gsim_set_ips(gsim_handle* h, const uint32_t* ip_ptr, const uint32_t* ip_ids, uint32_t n_ips)
+{
+    GSIM_ENTER(h);
+    GSIM_NEED_GRAPH(h);
+    if (!ip_ptr || ip_ptr[0] != 0) { h->err = "ip_ptr[0] must be 0"; return GSIM_EINVAL; }
+    if (n_ips > kIpNone) { h->err = "too many IP ids"; return GSIM_EINVAL; }
+    const int64_t n = h->n;
+    for (int64_t i = 0; i < n; ++i)
+        if (ip_ptr[i + 1] < ip_ptr[i]) { h->err = "ip_ptr not monotone"; return GSIM_EINVAL; }
+    const int64_t nip = ip_ptr[n];
+    if (nip > 0 && !ip_ids) { h->err = "ip_ids missing"; return GSIM_EINVAL; }
+    for (int64_t q = 0; q < nip; ++q)
+        if (ip_ids[q] >= n_ips) { h->err = "ip id out of range"; return GSIM_EINVAL; }
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "gsim_set_ips");
+    dfree(h->d_ip_ids);
+    int rc = dalloc(h, &h->d_ip_ids, nip);
+    if (!rc && n_ips != h->n_ips) {
+        dfree(h->d_ip_white);
+        rc = dalloc(h, &h->d_ip_white, (int64_t)n_ips);
+        h->has_white = false;
+        if (!rc) e = hipMemsetAsync(h->d_ip_white, 0, std::max<size_t>(n_ips, 1), h->stream);
+    }
+    if (rc) return rc;
+    h->n_ips = n_ips;
+    if (e == hipSuccess) e = hipMemcpyAsync(h->d_ip_ptr, ip_ptr, sizeof(uint32_t) * (size_t)(n + 1), hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess && nip) e = hipMemcpyAsync(h->d_ip_ids, ip_ids, sizeof(uint32_t) * (size_t)nip, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    h->p6_dirty = true;
+    return hip_check(h, e, "gsim_set_ips");
+}
+
 int gsim_set_ip_whitelist(gsim_handle* h, const uint8_t* white)
 {
     GSIM_ENTER(h);

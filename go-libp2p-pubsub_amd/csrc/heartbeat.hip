@@ -778,6 +778,43 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
     }
 }
 
+// inspectScoresExtended (score.go:472-500) for the connections e of
+// [e_lo, e_hi): the live score and its components.
+__global__ __launch_bounds__(256) void k_snapshot(HbArgs a, int64_t e_lo, int64_t e_hi, gsim_peer_score_snapshot* ps,
+                                                  gsim_topic_score_snapshot* ts)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = e_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < e_hi; e += stride) {
+        const int64_t x = e - e_lo;
+        const uint32_t col = a.col[e], rv = a.rev[e];
+        const bool tracked = (a.estate[rv] & GSIM_ES_TRACKED) != 0;
+        gsim_peer_score_snapshot p{};
+        p.observer = glob(a, a.col[rv]);
+        p.peer = glob(a, col);
+        p.tracked = tracked ? 1 : 0;
+        if (tracked) {
+            p.score = score_of_record(a, rv, col);
+            p.app_specific_score = a.p5[col];
+            p.ip_colocation_factor = a.p6[rv];
+            p.behaviour_penalty = a.bp[rv];
+        }
+        ps[x] = p;
+        for (int32_t t = 0; t < a.T; ++t) {
+            const int64_t i = (int64_t)t * a.E + rv;
+            gsim_topic_score_snapshot q{};
+            if (tracked) {
+                const uint8_t fl = a.tflags[i];
+                q.time_in_mesh_ns = (fl & GSIM_TF_IN_MESH) ? a.mtime[i] : 0;
+                q.first_message_deliveries = a.first[i];
+                q.mesh_message_deliveries =
+                    apply_incs(a.meshd[i], a.mcnt[i], const_tp(a.tp)[t].mesh_message_deliveries_cap);
+                q.invalid_message_deliveries = a.invalid[i];
+            }
+            ts[x * a.T + t] = q;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Connection churn between ticks (handleDeadPeers pubsub.go:711-759, the
 // new-peer case of processLoop pubsub.go:575-595): both endpoints of each
@@ -1153,6 +1190,44 @@ int gsim_handle_control(gsim_handle* h, int32_t round, int64_t now)
     return handle_control(h, round, now);
 }
 
+
+int gsim_read_snapshot(gsim_handle* h, int64_t obs_lo, int64_t obs_hi, gsim_peer_score_snapshot* peers,
+                       gsim_topic_score_snapshot* topics)
+{
+    if (!h) return GSIM_EINVAL;
+    if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
+    if (h->e == 0 || !h->x) { h->err = "no graph loaded"; return GSIM_ESTATE; }
+    if (obs_lo < 0 || obs_hi > h->n || obs_lo > obs_hi || (!peers && obs_hi > obs_lo)) {
+        h->err = "observer range out of bounds";
+        return GSIM_EINVAL;
+    }
+    int rc = deliver_flush(h);                    // first deliveries of the last round are credited
+    if (!rc && h->p6_dirty) rc = launch_ip_colocation(h);
+    if (rc) return rc;
+    uint32_t rp[2];
+    hipError_t e = hipMemcpy(rp, h->d_row_ptr + obs_lo, sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(rp + 1, h->d_row_ptr + obs_hi, sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_check(h, e, "row bounds");
+    const int64_t ne = (int64_t)rp[1] - rp[0], T = std::max(1, h->t);
+    if (ne == 0) return GSIM_OK;
+    gsim_peer_score_snapshot* dp = nullptr;
+    gsim_topic_score_snapshot* dt = nullptr;
+    e = hipMalloc((void**)&dp, sizeof(*dp) * (size_t)ne);
+    if (e == hipSuccess) e = hipMalloc((void**)&dt, sizeof(*dt) * (size_t)(ne * T));
+    if (e == hipSuccess) {
+        HbArgs a = make_hb_args(h, 0, 0, 0);
+        hipLaunchKernelGGL(k_snapshot, dim3((uint32_t)std::min<int64_t>((ne + 255) / 256, 16384)), dim3(256), 0,
+                           h->stream, a, (int64_t)rp[0], (int64_t)rp[1], dp, dt);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(peers, dp, sizeof(*dp) * (size_t)ne, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && topics)
+        e = hipMemcpyAsync(topics, dt, sizeof(*dt) * (size_t)(ne * T), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (dp) (void)hipFree(dp);
+    if (dt) (void)hipFree(dt);
+    return hip_check(h, e, "gsim_read_snapshot");
+}
 
 int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, int32_t up, int64_t now)
 {

@@ -102,6 +102,13 @@ MSG_DTYPE = [("id", "<u8"), ("topic", "<u4"), ("origin", "<u4"), ("invalid", "u1
 
 UNSEEN = 0xFFFFFFFF
 
+# numpy views of gsim_peer_score_snapshot (48 bytes) / gsim_topic_score_snapshot (32 bytes)
+PEER_SNAPSHOT_DTYPE = [("score", "<f8"), ("app_specific_score", "<f8"), ("ip_colocation_factor", "<f8"),
+                       ("behaviour_penalty", "<f8"), ("observer", "<u4"), ("peer", "<u4"), ("tracked", "<i4"),
+                       ("_pad", "<i4")]
+TOPIC_SNAPSHOT_DTYPE = [("time_in_mesh_ns", "<i8"), ("first_message_deliveries", "<f8"),
+                        ("mesh_message_deliveries", "<f8"), ("invalid_message_deliveries", "<f8")]
+
 KERNEL_CLASSES = ["refresh_score", "score", "ip_colocation", "heartbeat", "control", "publish", "send",
                   "commit", "accept", "gossip", "churn"]
 BEHAVE_IGNORE_IWANT = 0x01
@@ -167,6 +174,8 @@ SIGNATURES = [
                                          POINTER(CShardInfo)]),
     ("gsim_shard_layout", c_int32, [c_int64, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("gsim_read_snapshot", c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
+    ("gsim_set_ips", c_int32, [c_void_p, c_void_p, c_void_p, c_uint32]),
     ("gsim_rccl_unique_id", c_int32, [c_void_p, c_size_t]),
     ("gsim_group_create", c_int32,
      [POINTER(CPeerScoreParams), POINTER(CTopicScoreParams), c_int32, POINTER(CThresholds),

@@ -169,6 +169,24 @@ class Engine:
         p5 = np.ascontiguousarray(p5, dtype=np.float64)
         self._check(self.lib.gsim_set_app_score(self.h, _ptr(p5)))
 
+    def set_ips(self, ip_ptr: np.ndarray, ip_ids: np.ndarray, n_ips: int):
+        """refreshIPs (score.go:568-585): every peer's IP list replaced (gsim_set_ips)."""
+        p = np.ascontiguousarray(ip_ptr, dtype=np.uint32)
+        i = np.ascontiguousarray(ip_ids, dtype=np.uint32)
+        self._check(self.lib.gsim_set_ips(self.h, _ptr(p), _ptr(i), int(n_ips)))
+
+    def snapshot(self, obs_lo: int = 0, obs_hi: Optional[int] = None):
+        """ExtendedPeerScoreInspectFn's view (score.go:127-140, 472-500) of the
+        observers [obs_lo, obs_hi): one PeerScoreSnapshot per connection (edge
+        order) and its TopicScoreSnapshots [edges, T] (gsim_read_snapshot)."""
+        hi = self.net.n if obs_hi is None else obs_hi
+        ne = int(self.net.row_ptr[hi]) - int(self.net.row_ptr[obs_lo])
+        T = max(1, len(self.topics))
+        peers = np.zeros(ne, dtype=_abi.PEER_SNAPSHOT_DTYPE)
+        topics = np.zeros((ne, T), dtype=_abi.TOPIC_SNAPSHOT_DTYPE)
+        self._check(self.lib.gsim_read_snapshot(self.h, int(obs_lo), int(hi), _ptr(peers), _ptr(topics)))
+        return peers, topics
+
     def set_ip_whitelist(self, white: Optional[np.ndarray]):
         w = None if white is None else np.ascontiguousarray(white, dtype=np.uint8)
         self._check(self.lib.gsim_set_ip_whitelist(self.h, _ptr(w)))

@@ -323,6 +323,36 @@ int gsim_census(gsim_handle* h, int64_t* out8);
 /* Copy the score snapshot (E doubles, edge order) to host. */
 int gsim_read_scores(gsim_handle* h, double* out);
 
+/* WithPeerScoreInspect's ExtendedPeerScoreInspectFn (score.go:127-180),
+ * filled as inspectScoresExtended does (score.go:472-500) for every
+ * connection of the observers [obs_lo, obs_hi): peers[x] for the x-th edge of
+ * those rows (edge order), topics[x * T + t] its topic t.  Score is the live
+ * score(p) (deliveries since the last refresh included); a topic without
+ * events reads as a zero record; an untracked edge (no peerStats) has
+ * tracked = 0 and zeros. */
+typedef struct gsim_topic_score_snapshot {
+    int64_t time_in_mesh_ns;            /* meshTime while inMesh, else 0 */
+    double  first_message_deliveries;
+    double  mesh_message_deliveries;
+    double  invalid_message_deliveries;
+} gsim_topic_score_snapshot;
+typedef struct gsim_peer_score_snapshot {
+    double   score;
+    double   app_specific_score;
+    double   ip_colocation_factor;       /* the P6 value before its weight */
+    double   behaviour_penalty;
+    uint32_t observer, peer;             /* peer ids (global ids on a shard) */
+    int32_t  tracked;
+    int32_t  _pad;
+} gsim_peer_score_snapshot;
+int gsim_read_snapshot(gsim_handle* h, int64_t obs_lo, int64_t obs_hi, gsim_peer_score_snapshot* peers,
+                       gsim_topic_score_snapshot* topics);
+
+/* refreshIPs (score.go:568-585): replace every peer's IP list (CSR as for
+ * gsim_load_graph); P6 is re-derived before the next score.  The whitelist
+ * stays if n_ips is unchanged, else it is cleared. */
+int gsim_set_ips(gsim_handle* h, const uint32_t* ip_ptr, const uint32_t* ip_ids, uint32_t n_ips);
+
 /* ---- raw state access (tests, checkpoint/resume, golden fixtures) ------- */
 typedef enum gsim_field {
     GSIM_F_FIRST = 0,     /* f64 [T][E] firstMessageDeliveries          score.go:49 */
