@@ -56,6 +56,15 @@ constexpr uint32_t kCreditFirst = 0x80000000u;     // lo-word flag: winner's rec
 constexpr uint32_t kCreditMesh = 0x40000000u;      // lo-word flag: ... and P3 (negative window)
 constexpr uint32_t kPeerMask = 0x3FFFFFFFu;
 constexpr int kMaxRing = 8192;     // active-slot list lives in LDS (u16, sized by the ring)
+
+// The verdict of a message (gsim.h GSIM_VERDICT_*, stored in minv[slot]):
+// any verdict but ACCEPT stops receivers from forwarding and putting it in
+// their mcache; REJECT and SIGNATURE penalise every copy's sender (P4);
+// SIGNATURE is rejected before markSeen, so its copies never claim a cell.
+__device__ __forceinline__ bool verdict_penalises(uint8_t v)
+{
+    return v == GSIM_VERDICT_REJECT || v == GSIM_VERDICT_SIGNATURE;
+}
 constexpr int kSlotBatch = 8;      // active slots whose cells are loaded together
 
 struct IhaveStage;
@@ -265,7 +274,7 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, int32_t count)
     const uint32_t slot = (uint32_t)(p.id % (uint64_t)a.ring);
     a.mtopic[slot] = p.topic;
     a.morigin[slot] = p.origin;          // local id (a shard: 0xFFFFFFFF when not a local peer)
-    a.minv[slot] = p.invalid;
+    a.minv[slot] = p.verdict;
     a.mpub[slot] = (int32_t)a.g;
     if (p.origin >= a.clo && (int64_t)(p.origin - a.clo) < a.CN) {   // the origin's own cell
         const uint32_t oc = p.origin - a.clo;
@@ -379,8 +388,10 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
             for (int q = 0; q + 1 < B; ++q) cv[q] = cv[q + 1];
             const bool pend = is_claim_of(c0, qpar);     // first received in round g-1 (committed above)
             const uint32_t origin = a.morigin[m];
-            const bool inv = a.minv[m] != 0;
-            // receivers reject an invalid message and do not forward it; its
+            const uint8_t vd = a.minv[m];
+            const bool inv = vd != GSIM_VERDICT_ACCEPT;
+            const bool pen = verdict_penalises(vd), seeable = vd != GSIM_VERDICT_SIGNATURE;
+            // receivers do not forward a message they did not accept; its
             // origin publishes it regardless
             const bool fr = (pend || (uint32_t)(c0 >> 32) == gprev) && (!inv || (uint32_t)jl == origin);
             const uint64_t mask = __ballot(fr);
@@ -458,8 +469,8 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
                 }
                 if (ok1 && !k1) c1 = a.cell[row_m + i1];
                 if (ok2 && !k2) c2 = a.cell[row_m + i2];
-                if (sc1) { if (inv) x1 = a.invalid[plane + e1]; else if (tf1 & GSIM_TF_IN_MESH) n1 = a.mcnt[plane + e1]; }
-                if (sc2) { if (inv) x2 = a.invalid[plane + e2]; else if (tf2 & GSIM_TF_IN_MESH) n2 = a.mcnt[plane + e2]; }
+                if (sc1) { if (pen) x1 = a.invalid[plane + e1]; else if (!inv && (tf1 & GSIM_TF_IN_MESH)) n1 = a.mcnt[plane + e1]; }
+                if (sc2) { if (pen) x2 = a.invalid[plane + e2]; else if (!inv && (tf2 & GSIM_TF_IN_MESH)) n2 = a.mcnt[plane + e2]; }
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
                     const bool ok = u ? ok2 : ok1;
@@ -479,7 +490,7 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
                         if (!(hi & kClaim)) seen_round = hi;
                         else if (((hi >> 30) & 1u) != par) seen_round = a.g - 1;
                     }
-                    if (seen_round < 0 && (c == kUnseen64 || (hi & kEdgeMask) > e)) {
+                    if (seeable && seen_round < 0 && (c == kUnseen64 || (hi & kEdgeMask) > e)) {
                         // claim unless a lower edge already holds the cell
                         uint32_t lo = j;
                         if (sc && !inv) {
@@ -493,9 +504,9 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
                     }
                     if (!sc) continue;
                     const int64_t ir = plane + e;
-                    if (inv) {
+                    if (pen) {
                         a.invalid[ir] = (u ? x2 : x1) + 1.0;    // markInvalidMessageDelivery
-                    } else if (tf & GSIM_TF_IN_MESH) {
+                    } else if (!inv && (tf & GSIM_TF_IN_MESH)) {
                         // markDuplicateMessageDelivery's window test; a same-round
                         // copy (first or duplicate) has validated = now
                         const bool in_window = known ? true
@@ -622,7 +633,9 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
         const uint32_t m = s_slots[k];
         const int64_t row_m = (int64_t)m * a.CN;
         const uint32_t origin = a.morigin[m];
-        const bool inv = a.minv[m] != 0;
+        const uint8_t vd = a.minv[m];
+        const bool inv = vd != GSIM_VERDICT_ACCEPT;
+        const bool pen = verdict_penalises(vd), seeable = vd != GSIM_VERDICT_SIGNATURE;
         const uint8_t o_want = (origin < a.N && ((a.sub[origin] >> t) & 1ull)) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
         const bool win_all = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
         // stage the slot's committed bits
@@ -691,7 +704,7 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
                     if (vv[u]) {
                         const uint32_t e = ev[u];
                         iv[u] = a.col[e]; mfv[u] = a.mflags[plane + e]; dsv[u] = a.dstate[e]; tfv[u] = a.tflags[plane + e];
-                        if (inv) xv[u] = a.invalid[plane + e]; else nv[u] = a.mcnt[plane + e];
+                        if (pen) xv[u] = a.invalid[plane + e]; else if (!inv) nv[u] = a.mcnt[plane + e];
                     }
                 }
 #pragma unroll
@@ -725,7 +738,7 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
                         if (!(chi & kClaim)) seen_round = chi;
                         else if (((chi >> 30) & 1u) != par) seen_round = a.g - 1;
                     }
-                    if (seen_round < 0 && (c == kUnseen64 || (chi & kEdgeMask) > e)) {
+                    if (seeable && seen_round < 0 && (c == kUnseen64 || (chi & kEdgeMask) > e)) {
                         uint32_t lo_w = j;
                         if (sc && !inv) {
                             lo_w |= kCreditFirst;
@@ -738,9 +751,9 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
                     }
                     if (!sc) continue;
                     const int64_t ir = plane + e;
-                    if (inv) {
+                    if (pen) {
                         a.invalid[ir] = xv[u] + 1.0;                 // markInvalidMessageDelivery
-                    } else if (tf & GSIM_TF_IN_MESH) {
+                    } else if (!inv && (tf & GSIM_TF_IN_MESH)) {
                         const bool in_window = known ? true
                                              : seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window)
                                                                : (window >= 0);
@@ -1168,7 +1181,9 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
         const uint32_t p = a.col[r], i = owner[r];
         const int32_t t = (int32_t)a.mtopic[m];
         const ctp_t tp = tpa + t;
-        const bool inv = a.minv[m] != 0;
+        const uint8_t vd = a.minv[m];
+        const bool inv = vd != GSIM_VERDICT_ACCEPT;
+        const bool pen = verdict_penalises(vd);
         const int64_t ir = (int64_t)t * a.E + r;
         const bool sc = tp->scored && (ds & GSIM_DS_TRACKED);
         const uint8_t tf = a.tflags[ir];
@@ -1181,7 +1196,7 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
             if (!(hi & kClaim)) seen_round = hi;
             else if (((hi >> 30) & 1u) != par) seen_round = a.g - 1;
         }
-        if (seen_round < 0 && (c == kUnseen64 || (hi & kEdgeMask) > r)) {
+        if (vd != GSIM_VERDICT_SIGNATURE && seen_round < 0 && (c == kUnseen64 || (hi & kEdgeMask) > r)) {
             uint32_t lo = i;
             if (sc && !inv) {
                 lo |= kCreditFirst;
@@ -1195,9 +1210,9 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
             }
         }
         if (!sc) continue;
-        if (inv) {
+        if (pen) {
             atomicAdd(&a.invalid[ir], 1.0);                           // markInvalidMessageDelivery
-        } else if (tf & GSIM_TF_IN_MESH) {
+        } else if (!inv && (tf & GSIM_TF_IN_MESH)) {
             const bool in_window = seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window) : (window >= 0);
             if (in_window) atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], tp->mesh_message_deliveries_cap);
         }
@@ -1878,7 +1893,8 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
     for (int32_t m = 0; m < count; ++m) {
         // a shard gets every message; an origin that is not one of its peers is 0xFFFFFFFF
         const bool foreign = h->sh && msgs[m].origin == 0xFFFFFFFFu;
-        if (msgs[m].topic >= (uint32_t)std::max(1, h->t) || ((int64_t)msgs[m].origin >= h->n && !foreign)) {
+        if (msgs[m].topic >= (uint32_t)std::max(1, h->t) || ((int64_t)msgs[m].origin >= h->n && !foreign) ||
+            msgs[m].verdict > GSIM_VERDICT_SIGNATURE) {
             h->err = "message topic or origin out of range";
             return GSIM_EINVAL;
         }

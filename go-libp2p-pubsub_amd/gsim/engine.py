@@ -268,10 +268,11 @@ class Engine:
         return c.t0_ns + (g // c.rounds) * c.heartbeat_ns + (g % c.rounds + 1) * c.heartbeat_ns // (c.rounds + 1)
 
     def publish(self, msgs, rnd: int):
-        """Topic.Publish of each (id, topic, origin, invalid) at its origin in round `rnd`."""
+        """Topic.Publish of each (id, topic, origin, verdict) at its origin in round `rnd`
+        (verdict: _abi.VERDICT_*, the validation result at every receiver)."""
         arr = np.zeros(len(msgs), dtype=_abi.MSG_DTYPE)
-        for k, (mid, topic, origin, invalid) in enumerate(msgs):
-            arr[k]["id"], arr[k]["topic"], arr[k]["origin"], arr[k]["invalid"] = mid, topic, origin, invalid
+        for k, (mid, topic, origin, verdict) in enumerate(msgs):
+            arr[k]["id"], arr[k]["topic"], arr[k]["origin"], arr[k]["verdict"] = mid, topic, origin, verdict
         self._check(self.lib.gsim_publish(self.h, _ptr(arr), len(arr), int(rnd)))
 
     def publish_array(self, arr: np.ndarray, rnd: int):

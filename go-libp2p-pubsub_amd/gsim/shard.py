@@ -265,8 +265,8 @@ class ShardedEngine:
 
     def publish(self, msgs, rnd: int):
         arr = np.zeros(len(msgs), dtype=_abi.MSG_DTYPE)
-        for k, (mid, topic, origin, invalid) in enumerate(msgs):
-            arr[k]["id"], arr[k]["topic"], arr[k]["origin"], arr[k]["invalid"] = mid, topic, origin, invalid
+        for k, (mid, topic, origin, verdict) in enumerate(msgs):
+            arr[k]["id"], arr[k]["topic"], arr[k]["origin"], arr[k]["verdict"] = mid, topic, origin, verdict
         self.publish_array(arr, rnd)
 
     def publish_array(self, arr: np.ndarray, rnd: int):

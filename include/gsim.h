@@ -269,12 +269,26 @@ typedef struct gsim_msg_config {
     int64_t max_arrivals;    /* capacity of the IWANT response queue per tick (0: max(8 N, 2^20)) */
 } gsim_msg_config;
 
+/* The validation verdict every receiver reaches for a message (validation
+ * is instantaneous here, validation.go:282-407), with the score tracer's
+ * handling of it (score.go:693-827) and the gossip tracer's (gossip_tracer.go
+ * 148-170).  The origin publishes its message whatever the verdict. */
+#define GSIM_VERDICT_ACCEPT    0  /* DeliverMessage: P2 / P3 credit, forwarded, mcache.Put           */
+#define GSIM_VERDICT_REJECT    1  /* RejectValidationFailed: seen, P4 for the first and every later
+                                     sender, not forwarded                                          */
+#define GSIM_VERDICT_IGNORE    2  /* RejectValidationIgnored: seen, no credit and no penalty for any
+                                     copy, not forwarded                                            */
+#define GSIM_VERDICT_THROTTLE  3  /* RejectValidationThrottled: as IGNORE                           */
+#define GSIM_VERDICT_SIGNATURE 4  /* RejectInvalidSignature (before markSeen, validation.go:282-290):
+                                     every copy's sender gets P4, the message is never seen (so IWANT
+                                     asks again) and the IWANT promise is not fulfilled            */
+
 /* One published message (Topic.Publish, topic.go:217-283, at its origin). */
 typedef struct gsim_msg {
     uint64_t id;             /* message id; slot = id % ring */
     uint32_t topic;          /* dense topic index */
     uint32_t origin;         /* publishing peer (must be subscribed) */
-    uint8_t  invalid;        /* validator verdict: 1 = ValidationFailed at every receiver */
+    uint8_t  verdict;        /* GSIM_VERDICT_* at every receiver */
     uint8_t  _pad[7];
 } gsim_msg;
 

@@ -71,7 +71,7 @@ typedef struct orc_msgs {
     int64_t t0, hb;
     uint32_t* topic;           /* [ring] */
     uint32_t* origin;          /* [ring] */
-    uint8_t*  invalid;         /* [ring] validator verdict: 1 = reject */
+    uint8_t*  invalid;         /* [ring] validator verdict GSIM_VERDICT_*: 0 = accept (gsim.h) */
     uint32_t* seen;            /* [ring][N] */
     int32_t*  lastput;         /* [T][N] tick of the newest mcache.Put per (peer, topic) */
     int64_t   stats[4];        /* arrivals, first deliveries, duplicates, graylisted */

@@ -166,24 +166,36 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
         }
         m->stats[0]++;
         uint32_t* cell = &m->seen[(int64_t)slot * s->n + i];
+        const uint8_t verdict = m->invalid[slot];
+        if (verdict == GSIM_VERDICT_SIGNATURE) {
+            /* RejectInvalidSignature before markSeen (validation.go:282-290):
+             * every copy's sender is penalised, nothing is seen, no promise is
+             * fulfilled (gossip_tracer.go:148-162) */
+            m->stats[2]++;
+            orc_mark_invalid(s, er, t);
+            continue;
+        }
         if (*cell == UNSEEN) {
             *cell = (uint32_t)g;               /* markSeen */
             m->stats[1]++;
             orc_gossip_fulfill(m, i, slot);    /* gossipTracer: promises for it are kept */
             if (p->slot_last) p->slot_last[slot] = g;
-            if (m->invalid[slot]) {
+            if (verdict == GSIM_VERDICT_REJECT) {
                 /* ValidateMessage + RejectMessage(ValidationFailed), score.go:728-793 */
                 orc_mark_invalid(s, er, t);
-            } else {
+            } else if (verdict == GSIM_VERDICT_ACCEPT) {
                 /* DeliverMessage, score.go:702-726; mcache.Put; forward next round */
                 orc_mark_first(s, er, t);
                 m->lastput[(int64_t)t * s->n + i] = (int32_t)(g / m->rounds);
                 fr_push(p, i, slot, s->col[er]);
             }
+            /* RejectValidationIgnored / Throttled: deliveryIgnored / deliveryThrottled,
+             * no penalty and no credit (score.go:759-781) */
         } else {
             m->stats[2]++;                     /* DuplicateMessage, score.go:795-827 */
-            if (m->invalid[slot]) orc_mark_invalid(s, er, t);
-            else orc_mark_duplicate(s, er, t, 1, orc_round_time(m, (int64_t)*cell), now);
+            if (verdict == GSIM_VERDICT_REJECT) orc_mark_invalid(s, er, t);
+            else if (verdict == GSIM_VERDICT_ACCEPT)
+                orc_mark_duplicate(s, er, t, 1, orc_round_time(m, (int64_t)*cell), now);
         }
     }
     free(ar);
