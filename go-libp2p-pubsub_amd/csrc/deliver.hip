@@ -67,14 +67,14 @@ __device__ __forceinline__ bool verdict_penalises(uint8_t v)
 }
 constexpr int kSlotBatch = 8;      // active slots whose cells are loaded together
 
-struct IhaveStage;
-
 struct Deliver {
     gsim_msg_config cfg{};
     uint32_t *d_mtopic = nullptr, *d_morigin = nullptr;
     uint8_t* d_minv = nullptr;
     uint64_t* d_cell = nullptr;        // [ring][N] seen-set cells (layout above)
     uint64_t* d_seenbm = nullptr;      // [ring][ceil(N/64)] bit: the cell is committed (a cache of the cells)
+    uint64_t* d_fresh = nullptr;       // [ring][ceil(N/64)] bit: the peer forwards the slot's message next round
+    bool fresh_on = false;             // the topic-major delivery (and so the fresh bits) is in use
     int32_t* d_mpub = nullptr;         // [ring] round the slot's message was published in
     int64_t* d_roff = nullptr;         // [rounds] offset of each round in its heartbeat
     int32_t* d_lastput = nullptr;      // [T][N]
@@ -102,7 +102,6 @@ struct Deliver {
     std::vector<int64_t> prom_made;    // [P] tick that filled each ring index, -1 = empty
     int64_t ihave_tick = -1;           // heartbeat whose IHAVE marks are pending
     int64_t resp_round = -1;           // round in which the queued responses arrive
-    struct IhaveStage* ih = nullptr;   // a sharded group's IHAVE stage between count and walk
 };
 
 struct RoundArgs {
@@ -120,6 +119,7 @@ struct RoundArgs {
     uint8_t* minv;
     uint64_t* cell;
     uint64_t* seenbm;          // [ring][nw] committed bits of the cells (read before a cell)
+    uint64_t* fresh;           // [ring][nw] forwarders of the next round (topic-major delivery; nullptr otherwise)
     int64_t nw;                // words per slot
     int32_t* mpub;             // [ring] publication round
     const int64_t* roff;       // [R] (r + 1) * hb / (R + 1): offset of round r in its heartbeat
@@ -136,19 +136,17 @@ struct RoundArgs {
     const uint32_t* rev;
     int32_t flood;
     double pub_thr;
-    // seen-set cells exist for peers [clo, clo + CN) only (a shard's owned
-    // peers; every peer when unsharded): cell[m * CN + (i - clo)]
+    // seen-set cells: cell[m * CN + (i - clo)] for peers [clo, clo + CN)
+    // (every local peer: a shard's ghost cells hold the first-seen rounds its
+    // owners exported)
     int64_t CN;
     uint32_t clo;
-    // sharded network: a copy to a ghost receiver (outside
-    // [clo, clo + CN)) is queued for its shard: xout[dest * xcap + k] =
-    // the receiver's record there (xr[e]) | slot << 32, xcnt[dest] counts
+    // receivers: the owned peers [rlo, rhi) (every peer unless sharded); a
+    // shard pulls the copies its ghost senders forward to them, and leaves
+    // the copies its own senders forward to ghosts to the ghosts' shards
+    uint32_t rlo, rhi;
     int32_t sharded;
-    const uint32_t* xr;
-    const uint8_t* pshard;
-    uint64_t* xout;
-    uint32_t* xcnt;
-    int64_t xcap;
+    const uint8_t* pgate;          // sharded flood publish: a ghost origin's score of the receiver >= publishThreshold
 };
 
 __device__ __forceinline__ int64_t round_time(const RoundArgs& a, int64_t g)
@@ -262,7 +260,10 @@ __global__ void k_reset_slots(RoundArgs a, const gsim_msg* pub, int32_t count)
         // several reused rows may credit one record: atomic updates here
         if (a.g > 0 && is_claim_of(c, q)) commit_claim<true>(a, row + i, c, a.g - 1, m, a.clo + i);
         row[i] = kUnseen64;
-        if ((i & 63) == 0) a.seenbm[(int64_t)m * a.nw + (i >> 6)] = 0;
+        if ((i & 63) == 0) {
+            a.seenbm[(int64_t)m * a.nw + (i >> 6)] = 0;
+            if (a.fresh) a.fresh[(int64_t)m * a.nw + (i >> 6)] = 0;
+        }
     }
 }
 
@@ -280,6 +281,8 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, int32_t count)
         const uint32_t oc = p.origin - a.clo;
         a.cell[(int64_t)slot * a.CN + oc] = ((uint64_t)(uint32_t)a.g << 32) | p.origin;
         atomicOr(reinterpret_cast<unsigned long long*>(a.seenbm + (int64_t)slot * a.nw + (oc >> 6)), 1ull << (oc & 63));
+        if (a.fresh)   // the origin publishes whatever the verdict
+            atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)slot * a.nw + (oc >> 6)), 1ull << (oc & 63));
         int32_t* lp = a.lastput + (int64_t)p.topic * a.N + p.origin;
         const int32_t tick = (int32_t)(a.g / a.R);
         if (*lp < tick) *lp = tick;
@@ -567,33 +570,14 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
 constexpr int kTmThreads = 1024;
 constexpr int kTmChunk = 2048;      // peers scanned per frontier chunk (two per thread)
 
-// Queue copies to ghost receivers for their shards (all lanes of the wave
-// call this): one atomic per destination shard per wave.
-__device__ __forceinline__ void emit_remote(const RoundArgs& a, bool emit, uint32_t dest, uint64_t v)
-{
-    const int lane = threadIdx.x & 63;
-    uint64_t pend = __ballot(emit);
-    while (pend) {
-        const int lead = __ffsll((long long)pend) - 1;
-        const uint32_t d = (uint32_t)__shfl((int)dest, lead, 64);
-        const uint64_t mask = __ballot(emit && dest == d);
-        uint32_t base = 0;
-        if (lane == lead) base = atomicAdd(&a.xcnt[d], (uint32_t)__popcll(mask));
-        base = (uint32_t)__shfl((int)base, lead, 64);
-        if (emit && dest == d) {
-            const int64_t pos = (int64_t)base + __popcll(mask & ((1ull << lane) - 1));
-            if (pos < a.xcap) a.xout[(int64_t)d * a.xcap + pos] = v;
-        }
-        pend &= ~mask;
-    }
-}
-
 template <int W>
 __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t range)
 {
-    extern __shared__ uint64_t s_bm[];                       // [nw] committed bits, then [ring] u16 slots
-    uint16_t* s_slots = reinterpret_cast<uint16_t*>(s_bm + a.nw);
-    __shared__ uint32_t s_front[kTmChunk];                   // frontier senders (peer | from in s_from)
+    // [nws] committed bits of the receivers' words, then [ring] u16 slots
+    extern __shared__ uint64_t s_bm[];
+    const int64_t wlo = (int64_t)a.rlo >> 6, nws = (((int64_t)a.rhi + 63) >> 6) - wlo;
+    uint16_t* s_slots = reinterpret_cast<uint16_t*>(s_bm + nws);
+    __shared__ uint32_t s_front[kTmChunk];                   // frontier senders (their first sender in s_from)
     __shared__ uint32_t s_from[kTmChunk];
     __shared__ uint32_t s_beg[kTmChunk];                     // the sender's row
     __shared__ uint16_t s_len[kTmChunk];
@@ -623,11 +607,9 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
     const int64_t window = tp->mesh_message_deliveries_window_ns;
     const double mcap = tp->mesh_message_deliveries_cap;
     const int64_t plane = (int64_t)t * a.E;
-    const uint32_t gprev = (uint32_t)(a.g - 1);
     const uint32_t par = (uint32_t)(a.g & 1);
     const uint32_t claim_hi = kClaim | (par << 30);
     const uint32_t clo = a.clo;
-    const uint64_t cn = (uint64_t)a.CN;
     unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
     for (int k = 0; k < ns; ++k) {
         const uint32_t m = s_slots[k];
@@ -638,47 +620,43 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
         const bool pen = verdict_penalises(vd), seeable = vd != GSIM_VERDICT_SIGNATURE;
         const uint8_t o_want = (origin < a.N && ((a.sub[origin] >> t) & 1ull)) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
         const bool win_all = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
-        // stage the slot's committed bits
-        for (int64_t w = tid; w < a.nw; w += kTmThreads) s_bm[w] = a.seenbm[(int64_t)m * a.nw + w];
+        // stage the slot's committed bits (receivers' words)
+        for (int64_t w = tid; w < nws; w += kTmThreads) s_bm[w] = a.seenbm[(int64_t)m * a.nw + wlo + w];
         if (tid == 0) s_claimed = 0;
         const unsigned long long first_before = n_first;
         __syncthreads();
-        // the cells and row bounds of the next chunk are loaded while the
-        // current chunk's frontier rows are walked
-        constexpr int H = kTmChunk / kTmThreads;
-        uint64_t cs[H];
-        uint32_t rb[H], re[H];
-        auto fetch = [&](int64_t c0) {
-#pragma unroll
-            for (int h = 0; h < H; ++h) {
-                const int64_t x = c0 + h * kTmThreads + tid;
-                const bool in = x < hi;
-                cs[h] = in ? a.cell[row_m + (x - clo)] : kUnseen64;
-                rb[h] = in ? a.row_ptr[x] : 0u;
-                re[h] = in ? a.row_ptr[x + 1] : 0u;
-            }
-        };
-        fetch(lo);
+        // each chunk's frontier comes from the slot's fresh bits: the peers
+        // that first saw the message in round g-1 and forward it (an accepted
+        // copy k_commit committed, the publication, a ghost's import), cleared
+        // as they are read; only those peers' cells and rows are loaded
+        uint64_t* fresh_m = a.fresh + (int64_t)m * a.nw;
+        constexpr int kWords = kTmChunk / 64;
         for (int64_t c0 = lo; c0 < hi; c0 += kTmChunk) {
-            // frontier of the chunk: first seen (or published) in round g-1
             if (tid == 0) s_nf = 0;
             __syncthreads();
-#pragma unroll
-            for (int h = 0; h < H; ++h) {
-                const int64_t x = c0 + h * kTmThreads + tid;
-                const uint64_t c = cs[h];
-                const uint32_t chi = (uint32_t)(c >> 32);
-                if (x < hi && c != kUnseen64 && chi == gprev && (!inv || (uint32_t)x == origin)) {
-                    const int q = atomicAdd(&s_nf, 1);
-                    s_front[q] = (uint32_t)x;
-                    s_from[q] = (uint32_t)c & kPeerMask;
-                    s_beg[q] = rb[h];
-                    s_len[q] = (uint16_t)(re[h] - rb[h]);
+            if (tid < kWords) {
+                const int64_t x0 = c0 + (int64_t)tid * 64;      // ranges start on whole words
+                uint64_t w = 0;
+                if (x0 < hi) {
+                    w = fresh_m[(x0 - clo) >> 6];
+                    if (w) fresh_m[(x0 - clo) >> 6] = 0;
+                    if (hi - x0 < 64) w &= (1ull << (hi - x0)) - 1;
+                }
+                if (w) {
+                    int q = atomicAdd(&s_nf, __popcll(w));
+                    for (; w; w &= w - 1) s_front[q++] = (uint32_t)(x0 + __ffsll((long long)w) - 1);
                 }
             }
             __syncthreads();
-            if (c0 + kTmChunk < hi) fetch(c0 + kTmChunk);
             const int nf = s_nf;
+            for (int q = tid; q < nf; q += kTmThreads) {
+                const uint32_t x = s_front[q];
+                s_from[q] = (uint32_t)a.cell[row_m + (x - clo)] & kPeerMask;
+                const uint32_t rb = a.row_ptr[x];
+                s_beg[q] = rb;
+                s_len[q] = (uint16_t)(a.row_ptr[x + 1] - rb);
+            }
+            __syncthreads();
             // each row group walks P frontier senders' rows at a time; the
             // counters are loaded with the row state (one memory trip), the
             // receiver's cell only when its committed bit is not decisive
@@ -712,23 +690,24 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
                     const uint32_t j = jv[u], e = ev[u], i = iv[u];
                     const uint8_t ds = dsv[u], tf = tfv[u];
                     bool sel = (mfv[u] & (j == origin ? o_want : GSIM_TF_MESH)) != 0;
-                    if (a.flood && vv[u] && j == origin) sel = ((a.sub[i] >> t) & 1ull) && a.score[a.rev[e]] >= a.pub_thr;
+                    if (a.flood && vv[u] && j == origin)
+                        sel = ((a.sub[i] >> t) & 1ull) &&
+                              ((a.sharded && (j < a.rlo || j >= a.rhi)) ? a.pgate[e] != 0
+                                                                        : a.score[a.rev[e]] >= a.pub_thr);
                     // direct peers that joined the topic always get it (gossipsub.go:991-1003)
                     if (vv[u] && (ds & GSIM_DS_DIRECT) && !sel) sel = (a.sub[i] >> t) & 1ull;
                     const bool tg = vv[u] && sel && (ds & GSIM_DS_CONNECTED) && i != fv[u] && i != origin;
-                    // a ghost receiver belongs to another shard: the copy goes
-                    // there, its AcceptFrom, seen check and counters too
+                    // a ghost receiver's shard pulls this copy from the frontier
+                    // export (it walks this sender's ghost row there)
+                    const bool remote = i < a.rlo || i >= a.rhi;
                     const uint32_t ic = i - clo;
-                    const bool remote = (uint64_t)ic >= cn;
-                    if (a.sharded)                           // (every lane of the wave is here)
-                        emit_remote(a, tg && remote, remote && vv[u] ? (uint32_t)a.pshard[i] : 0u,
-                                    (tg && remote) ? ((uint64_t)a.xr[e] | ((uint64_t)m << 32)) : 0ull);
                     const bool ok = tg && !remote && (ds & GSIM_DS_ACCEPT);
                     n_gray += tg && !remote && !ok;              // AcceptFrom: graylisted sender
                     n_acc += ok;
                     if (!ok) continue;
                     const bool sc = scored_t && (ds & GSIM_DS_TRACKED);
-                    const bool known = ((s_bm[ic >> 6] >> (ic & 63)) & 1ull) &&
+                    const int64_t bw = ((int64_t)i >> 6) - wlo;
+                    const bool known = ((s_bm[bw] >> (i & 63)) & 1ull) &&
                                        (win_all || !sc || inv || !(tf & GSIM_TF_IN_MESH));
                     const uint64_t c = known ? 0ull : a.cell[row_m + ic];
                     const uint32_t chi = (uint32_t)(c >> 32);
@@ -804,8 +783,9 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
     __shared__ int s_n;
     const int nact = active_slots(a.nnew_cur, a.ring, s_act, &s_n);
     const int lane = threadIdx.x & 63;
-    const int64_t i0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;   // cell index (peer clo + i)
-    if (i0 >= a.CN || nact == 0) return;
+    // claims exist only at receivers' cells: the words of [rlo, rhi)
+    const int64_t i0 = (((int64_t)a.rlo - a.clo) & ~63ll) + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+    if (i0 >= (int64_t)a.rhi - a.clo || nact == 0) return;
     const int64_t i = i0 + lane;
     const bool vi = i < a.CN;
     const uint32_t par = (uint32_t)(a.g & 1);
@@ -820,7 +800,13 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
             const uint64_t cb = __ballot(k < nact && is_claim_of(cv[b], par));
-            if (cb && lane == 0) a.seenbm[(int64_t)s_act[k] * a.nw + (i0 >> 6)] |= cb;
+            if (cb && lane == 0) {
+                const uint32_t m = s_act[k];
+                a.seenbm[(int64_t)m * a.nw + (i0 >> 6)] |= cb;
+                // receivers forward what they accepted, in the next round
+                if (a.fresh && a.minv[m] == GSIM_VERDICT_ACCEPT)
+                    atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (i0 >> 6)), cb);
+            }
         }
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
@@ -871,15 +857,12 @@ struct IhArgs {
     uint64_t seed;
     int64_t CN;                    // cells exist for peers [clo, clo + CN) (RoundArgs)
     uint32_t clo;
-    // sharded network: every slot is pulled (receivers walk), an advertiser's
-    // holding of active slot k is a bit of the all-gathered holder bitmaps
-    // (bit gid - bounds[s] of block hoff[s] + k * hwords[s], s its shard)
+    // sharded network: receivers are the owned peers [rlo, rhi) and every slot
+    // is pulled (receivers walk); a ghost advertiser's holding is its ghost
+    // cell (first-seen rounds its shard exported); keys use global ids
+    uint32_t rlo, rhi;
     int32_t sharded;
     const uint32_t* gid;
-    const uint8_t* pshard;
-    const uint64_t* hbm;
-    const int64_t* hoff;           // [K+1] word offset of each shard's block
-    const int64_t* bounds;         // [K+1] global peer ranges
 };
 
 // first-seen round of a cell at control time of round g (any claim still
@@ -947,7 +930,7 @@ __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount
             const int32_t t = (int32_t)a.mtopic[m];
             const bool hold = vp && holds_in_window(cv[b], a.g, a.lo_round, tick_round, a.minv[m] != 0,
                                                    (uint32_t)pl == a.morigin[m]);
-            const bool want = vp && cv[b] == kUnseen64 && ((subp >> t) & 1ull);
+            const bool want = vp && cv[b] == kUnseen64 && ((subp >> t) & 1ull) && pl >= a.rlo && pl < a.rhi;
             const int nh = __popcll(__ballot(hold)), nw = __popcll(__ballot(want));
             if (lane == 0 && nh) atomicAdd(&s_cnt[m], (uint32_t)nh);
             if (lane == 0 && nw) atomicAdd(&s_cnt[a.ring + m], (uint32_t)nw);
@@ -1026,7 +1009,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
             // push: lanes are holders of m (its advertisers); pull: lanes are
             // receivers that joined t and have not seen m (handleIHave's seenMessage)
             const bool me = vp && (push ? holds_in_window(cv[b], a.g, a.lo_round, tick_round, inv, (uint32_t)pl == origin)
-                                        : (cv[b] == kUnseen64 && ((subp >> t) & 1ull)));
+                                        : (cv[b] == kUnseen64 && ((subp >> t) & 1ull) && pl >= a.rlo && pl < a.rhi));
             const uint64_t mask = __ballot(me);
             if (!mask) continue;
             const int64_t row_m = (int64_t)m * a.CN;
@@ -1066,16 +1049,8 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                         const uint32_t re = a.rev[e];
                         if (a.gsel[plane + re] && a.gstate[e]) {
                             const uint32_t i = a.col[e];
-                            if (a.sharded) {
-                                // the advertiser's holding: its shard's bit for active slot k
-                                const uint32_t s = a.pshard[i];
-                                const uint64_t gi = (uint64_t)a.gid[i] - (uint64_t)a.bounds[s];
-                                const int64_t words = (a.bounds[s + 1] - a.bounds[s] + 63) >> 6;
-                                req = (a.hbm[a.hoff[s] + (int64_t)k * words + (int64_t)(gi >> 6)] >> (gi & 63)) & 1ull;
-                            } else {
-                                req = holds_in_window(a.cell[row_m + (i - a.clo)], a.g, a.lo_round, tick_round, inv,
-                                                      i == origin);
-                            }
+                            req = holds_in_window(a.cell[row_m + (i - a.clo)], a.g, a.lo_round, tick_round, inv,
+                                                  i == origin);
                             if (req) {
                                 const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, me_g, 0, P_PROMISE, m,
                                                               a.gid ? a.gid[i] : i);
@@ -1285,17 +1260,14 @@ using namespace gsim;
 // ---------------------------------------------------------------------------
 // host side
 
-static void free_ihave_stage(Deliver* d);
-
 static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_seenbm); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
-    free_ihave_stage(d);
     delete d;
 }
 
@@ -1337,9 +1309,12 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.first = h->d_first; a.meshd = h->d_meshd; a.invalid = h->d_invalid; a.mcnt = h->d_mcnt;
     a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv;
     a.cell = d->d_cell; a.lastput = d->d_lastput;
-    a.CN = h->ohi() - h->olo();
-    a.clo = (uint32_t)h->olo();
+    a.CN = h->n;
+    a.clo = 0;
+    a.rlo = (uint32_t)h->olo();
+    a.rhi = (uint32_t)h->ohi();
     a.seenbm = d->d_seenbm; a.nw = (a.CN + 63) / 64; a.mpub = d->d_mpub; a.roff = d->d_roff;
+    a.fresh = d->fresh_on ? d->d_fresh : nullptr;
     const size_t w = (size_t)nnew_words(d);
     a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
     a.nnew_cur = d->d_nnew + (size_t)(g & 1) * w;
@@ -1352,11 +1327,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.pub_thr = h->th.publish_threshold;
     if (ShardCtx* sh = h->sh) {
         a.sharded = 1;
-        a.xr = sh->d_xr;
-        a.pshard = sh->d_pshard;
-        a.xout = sh->d_xout;
-        a.xcnt = sh->d_xcnt;
-        a.xcap = sh->xcap;
+        a.pgate = sh->d_pgate;
     }
     return a;
 }
@@ -1392,7 +1363,7 @@ int deliver_promise_check(gsim_handle* h, int64_t now)
         hipLaunchKernelGGL(k_promise_check, dim3(std::min<int64_t>((h->e + 255) / 256, 16384)), dim3(256), 0,
                            h->stream, d->d_prom + (size_t)q * (size_t)h->e, (const uint64_t*)d->d_cell,
                            (const uint32_t*)h->d_owner, (const uint32_t*)h->d_rev, h->d_pen, h->e,
-                           h->ohi() - h->olo(), (uint32_t)h->olo(), d->d_gstats);
+                           h->n, (uint32_t)0, d->d_gstats);
         d->prom_made[(size_t)q] = -1;
         int rc = hip_check(h, hipGetLastError(), "k_promise_check");
         if (rc) return rc;
@@ -1449,16 +1420,13 @@ static bool ihave_prepare(gsim_handle* h, int64_t g, IhaveStage* st, int* rc)
     a.resp = d->d_resp; a.nresp = d->d_nresp; a.resp_cap = d->resp_cap; a.gstats = d->d_gstats;
     a.respond = h->gp.gossip_retransmission >= 1;
     a.seed = h->x ? gsim_get_seed(h) : 0;
-    a.CN = h->ohi() - h->olo();
-    a.clo = (uint32_t)h->olo();
+    a.CN = h->n;
+    a.clo = 0;
+    a.rlo = (uint32_t)h->olo();
+    a.rhi = (uint32_t)h->ohi();
     if (ShardCtx* sh = h->sh) {
         a.sharded = 1;
         a.gid = sh->d_gid;
-        a.pshard = sh->d_pshard;
-        a.hbm = sh->d_hbm;
-        a.hoff = sh->d_hoff;
-        a.bounds = sh->d_bounds;
-        a.slot_last = sh->d_slot_last_g;   // MAX over the shards (set by the caller)
     }
     st->lds = (((size_t)d->cfg.ring + 3) & ~(size_t)3) * sizeof(uint16_t) + 4 * kRespStage * sizeof(uint64_t);
     st->lds_c = (((size_t)d->cfg.ring + 1) & ~(size_t)1) * sizeof(uint16_t) + 2 * (size_t)d->cfg.ring * 4;
@@ -1481,7 +1449,6 @@ static int ihave_walk(gsim_handle* h, IhaveStage* st)
 {
     Deliver* d = h->dl;
     IhArgs& a = st->a;
-    if (h->sh) { a.hbm = h->sh->d_hbm; a.hoff = h->sh->d_hoff; }   // (re)allocated after the count
     ProfScope ps(h, GSIM_K_GOSSIP);
     // lane groups sized to the rows: power-law graphs (long rows, short mean) walk
     // their few long rows in chunks rather than idling 3/4 of a 64-lane group
@@ -1518,8 +1485,8 @@ int deliver_flush(gsim_handle* h)
     if (!d || d->pending < 0) return GSIM_OK;
     ProfScope ps(h, GSIM_K_COMMIT);
     RoundArgs a = make_round_args(h, d->pending);
-    hipLaunchKernelGGL(k_commit, dim3(grid_peers(a.CN)), dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t),
-                       h->stream, a);
+    hipLaunchKernelGGL(k_commit, dim3(grid_peers((int64_t)a.rhi - (((int64_t)a.rlo - a.clo) & ~63ll))), dim3(256),
+                       (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     d->pending = -1;
     return hip_check(h, hipGetLastError(), "k_commit");
 }
@@ -1554,8 +1521,7 @@ int deliver_read_seen(gsim_handle* h, void* dst)
     if (!d->d_seen32) e = hipMalloc((void**)&d->d_seen32, std::max<size_t>(n * 4, 4));
     if (e != hipSuccess) return hip_check(h, e, "seen view scratch");
     hipLaunchKernelGGL(k_seen_view, dim3(std::min<int64_t>(((int64_t)n + 255) / 256, 16384)), dim3(256), 0, h->stream,
-                       (const uint64_t*)d->d_cell, d->d_seen32, (int64_t)n, h->n, h->ohi() - h->olo(),
-                       (uint32_t)h->olo());
+                       (const uint64_t*)d->d_cell, d->d_seen32, (int64_t)n, h->n, h->n, (uint32_t)0);
     e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpyAsync(dst, d->d_seen32, n * 4, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
@@ -1571,7 +1537,7 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a, size_t lds)
     // 21.1 / 21.3 ms per tick at C3, profiles/r01_ab_send_tm_blocks.log), ranges of
     // at least 4096 peers
     constexpr int64_t total = 2048;
-    const int64_t cn = h->ohi() - h->olo();
+    const int64_t cn = h->n;                 // every local peer sends (a shard's ghosts too)
     const int64_t ranges = std::max<int64_t>(1, std::min<int64_t>((cn + 4095) / 4096,
                                                                     std::max<int64_t>(1, total / std::max(1, h->t))));
     const int32_t range = (int32_t)(((cn + ranges - 1) / ranges + 63) & ~63ll);
@@ -1587,7 +1553,9 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a, size_t lds)
 // LDS of the topic-major kernel: the slot's committed bits + the slot list
 static size_t send_tm_lds(const gsim_handle* h, const Deliver* d)
 {
-    return (size_t)((h->ohi() - h->olo() + 63) / 64) * 8 + (((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7);
+    // the receivers' (owned peers') words of the committed bits, then the slot list
+    const int64_t nws = ((h->ohi() + 63) >> 6) - (h->olo() >> 6);
+    return (size_t)nws * 8 + (((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7);
 }
 constexpr size_t kLdsBudget = 160 * 1024 - 24 * 1024;   // minus the static frontier buffers
 
@@ -1610,7 +1578,10 @@ static bool lazy_commits(const gsim_handle* h)
     return true;
 }
 
-int deliver_round_send(gsim_handle* h, int64_t round)
+// Stage 1 of round g: order checks, AcceptFrom verdicts of a new score
+// snapshot, and (topic-major delivery) the commits of round g-1, which set
+// the fresh bits of round g's forwarders.
+int deliver_round_prepare(gsim_handle* h, int64_t round)
 {
     Deliver* d = h->dl;
     if (!d) { h->err = "gsim_msgs_init not called"; return GSIM_ESTATE; }
@@ -1623,35 +1594,33 @@ int deliver_round_send(gsim_handle* h, int64_t round)
         h->err = "propagation kernels support rows of at most 64 connections in this build";
         return GSIM_ERANGE;
     }
+    if (h->sh && !d->fresh_on) {
+        h->err = "a shard's delivery needs the topic-major kernel (its owned peers' bits must fit in LDS)";
+        return GSIM_ERANGE;
+    }
     int rc = 0;
     {
         ProfScope ps(h, GSIM_K_ACCEPT);
         rc = refresh_accept(h);
         if (rc) return rc;
     }
-    // topic-major delivery when a slot's committed bits fit in LDS: the claims
-    // of round g-1 are committed first (k_commit), then k_send_tm
-    const size_t lds_tm = send_tm_lds(h, d);
-    const bool tm = h->send_variant == 3 && lds_tm <= kLdsBudget;
-    if (h->sh && !tm) {
-        h->err = "a shard's delivery needs the topic-major kernel (its owned peers' bits must fit in LDS)";
-        return GSIM_ERANGE;
-    }
-    if (tm) {
-        rc = deliver_flush(h);
-        if (rc) return rc;
-    }
-    if (h->sh) {   // the copy queues of this round
-        hipError_t e = hipMemsetAsync(h->sh->d_xcnt, 0, sizeof(uint32_t) * (size_t)h->sh->K, h->stream);
-        if (e != hipSuccess) return hip_check(h, e, "copy queue reset");
-    }
+    if (d->fresh_on) rc = deliver_flush(h);
+    return rc;
+}
+
+// Stage 2: the delivery kernel of round g.
+int deliver_round_send(gsim_handle* h, int64_t round)
+{
+    Deliver* d = h->dl;
+    int rc = 0;
     RoundArgs a = make_round_args(h, round);
     h->mcnt_dirty = true;
     const size_t lds = (((size_t)d->cfg.ring + 1) & ~(size_t)1) * sizeof(uint16_t) + (size_t)nnew_words(d) * 4;
     {
         ProfScope ps(h, GSIM_K_SEND);
         const int grid = grid_peers(h->n);
-        if (tm) {
+        if (d->fresh_on) {
+            const size_t lds_tm = send_tm_lds(h, d);
             if (h->max_degree <= 16)
                 rc = launch_send_tm<16>(h, a, lds_tm);
             else if (h->max_degree <= 32)
@@ -1676,8 +1645,8 @@ int deliver_round_send(gsim_handle* h, int64_t round)
 }
 
 // Copies arriving in round g at this handle's peers, one entry per copy:
-// the receiver's record of the sender | slot << 32 (the IWANT responses, and
-// a shard's copies from other shards).  *d_n entries, at most cap.
+// the receiver's record of the sender | slot << 32 (the IWANT responses).
+// *d_n entries, at most cap.
 int deliver_round_queue(gsim_handle* h, int64_t round, const uint64_t* q, const uint32_t* d_n, int64_t cap)
 {
     Deliver* d = h->dl;
@@ -1714,72 +1683,117 @@ int deliver_round_control(gsim_handle* h, int64_t round)
     return handle_control(h, r, a.now);
 }
 
-// The IHAVE stage of round g (control round 0) for a sharded group: prepare
-// and count (the caller then reduces d_gcount over the shards and fills the
-// holder bitmaps), then walk.  d_slot_last_g must hold the reduced slot_last.
-static void free_ihave_stage(Deliver* d)
+int deliver_round_ihave(gsim_handle* h, int64_t round)
 {
-    delete d->ih;
-    d->ih = nullptr;
+    return round % h->dl->cfg.rounds == 0 ? launch_ihave(h, round) : GSIM_OK;
 }
-
-int deliver_ihave_count(gsim_handle* h, int64_t g, bool* run)
-{
-    Deliver* d = h->dl;
-    delete d->ih;
-    d->ih = new IhaveStage();
-    int rc = GSIM_OK;
-    *run = g % d->cfg.rounds == 0 && ihave_prepare(h, g, d->ih, &rc);
-    if (!*run) { delete d->ih; d->ih = nullptr; return rc; }
-    return ihave_count(h, d->ih);
-}
-
-int deliver_ihave_walk(gsim_handle* h)
-{
-    Deliver* d = h->dl;
-    if (!d->ih) return GSIM_OK;
-    const int rc = ihave_walk(h, d->ih);
-    delete d->ih;
-    d->ih = nullptr;
-    return rc;
-}
-
-uint32_t* deliver_gcount(gsim_handle* h) { return h->dl ? h->dl->d_gcount : nullptr; }
 
 void deliver_round_end(gsim_handle* h, int64_t round) { h->dl->next_round = round + 1; }
 
-// A shard's block of the IHAVE holder bitmaps: for each active slot act[k],
-// bit p of word w says whether peer clo + 64 w + p holds the message in its
-// gossip window (the rule holds_in_window applies to local advertisers).
-__global__ __launch_bounds__(256) void k_holder_bits(RoundArgs a, const uint32_t* act, int32_t n_act, int32_t lo_round,
-                                                     int64_t tick_round, uint64_t* out)
+// ---- a sharded network's frontier exchange -----------------
+// Round g's forwarders among a shard's owned peers (their fresh bits, set by
+// the commits of round g-1 and by publication), one entry each: global peer
+// id | global id of its first sender << 24 (0xFFFFFF: none) | slot << 48.
+// Every other shard imports the entries of its ghosts: the ghost's cell gets
+// the first-seen round and first sender, its fresh bit and the slot's
+// activity are set, so that shard's k_send_tm walks the ghost's row (its
+// connections into the shard) and delivers those copies itself.
+constexpr uint64_t kG24 = 0xFFFFFFull;
+
+__global__ __launch_bounds__(256) void k_frontier_export(RoundArgs a, const uint32_t* gid, uint64_t* out,
+                                                         uint32_t* cnt, int64_t cap)
 {
+    extern __shared__ uint16_t s_act[];
+    __shared__ int s_n;
+    const int nact = active_slots(a.nnew_prev, a.ring, s_act, &s_n);
     const int lane = threadIdx.x & 63;
-    const int64_t words = (a.CN + 63) / 64;
-    const int64_t total = words * n_act;
-    for (int64_t x = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); x < total; x += (int64_t)gridDim.x * 4) {
-        const int64_t k = x / words, w = x - k * words;
-        const uint32_t m = act[k];
+    const int64_t w0 = (int64_t)a.rlo >> 6, w1 = ((int64_t)a.rhi + 63) >> 6;
+    for (int64_t x = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); x < (w1 - w0) * nact; x += (int64_t)gridDim.x * 4) {
+        const int64_t k = x / (w1 - w0), w = w0 + (x - k * (w1 - w0));
+        const uint32_t m = s_act[k];
+        uint64_t bits = a.fresh[(int64_t)m * a.nw + w];
         const int64_t i = w * 64 + lane;
-        const bool hold = i < a.CN && holds_in_window(a.cell[(int64_t)m * a.CN + i], a.g, lo_round, tick_round,
-                                                      a.minv[m] != 0, a.clo + (uint32_t)i == a.morigin[m]);
-        const uint64_t b = __ballot(hold);
-        if (lane == 0) out[x] = b;
+        bits &= (w * 64 < (int64_t)a.rlo) ? ~0ull << ((int64_t)a.rlo - w * 64) : ~0ull;   // owned peers only
+        const bool me = ((bits >> lane) & 1ull) && i >= (int64_t)a.rlo && i < (int64_t)a.rhi;
+        const uint64_t mm = __ballot(me);
+        if (!mm) continue;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(cnt, (uint32_t)__popcll(mm));
+        base = (uint32_t)__shfl((int)base, 0, 64);
+        if (me) {
+            const uint32_t f = (uint32_t)a.cell[(int64_t)m * a.CN + i] & kPeerMask;
+            const uint64_t gf = f < a.N ? (uint64_t)gid[f] : kG24;
+            const int64_t pos = (int64_t)base + __popcll(mm & ((1ull << lane) - 1));
+            if (pos < cap) out[pos] = (uint64_t)gid[i] | (gf << 24) | ((uint64_t)m << 48);
+        }
     }
 }
 
-int deliver_holder_bits(gsim_handle* h, int64_t g, const uint32_t* d_act, int32_t n_act, uint64_t* out)
+__global__ __launch_bounds__(256) void k_frontier_import(RoundArgs a, const uint32_t* g2l, const uint64_t* in,
+                                                         int64_t n)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += stride) {
+        const uint64_t v = in[x];
+        const uint32_t l = g2l[v & kG24];
+        if (l == 0xFFFFFFFFu || (l >= a.rlo && l < a.rhi)) continue;      // not a ghost of this shard
+        const uint64_t gf = (v >> 24) & kG24;
+        uint32_t f = gf == kG24 ? 0xFFFFFFFFu : g2l[gf];
+        if (f == 0xFFFFFFFFu) f = kPeerMask;                                 // not a local peer
+        const uint32_t m = (uint32_t)(v >> 48);
+        a.cell[(int64_t)m * a.CN + l] = ((uint64_t)(uint32_t)(a.g - 1) << 32) | f;
+        atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (l >> 6)), 1ull << (l & 63));
+        atomicOr(const_cast<uint32_t*>(a.nnew_prev) + (m >> 5), 1u << (m & 31));
+        atomicMax(&a.slot_last[m], (int32_t)(a.g - 1));
+    }
+}
+
+int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32_t* d_cnt, int64_t cap)
 {
     Deliver* d = h->dl;
-    RoundArgs a = make_round_args(h, g);
-    const int64_t tick = g / d->cfg.rounds;
-    const int32_t lo_round = (int32_t)std::max<int64_t>((tick - h->gp.history_gossip) * d->cfg.rounds, 0);
-    const int64_t total = ((a.CN + 63) / 64) * n_act;
-    if (total == 0) return GSIM_OK;
-    hipLaunchKernelGGL(k_holder_bits, dim3((uint32_t)std::min<int64_t>((total + 3) / 4, 65536)), dim3(256), 0,
-                       h->stream, a, d_act, n_act, lo_round, tick * d->cfg.rounds, out);
-    return hip_check(h, hipGetLastError(), "k_holder_bits");
+    RoundArgs a = make_round_args(h, round);
+    hipError_t e = hipMemsetAsync(d_cnt, 0, sizeof(uint32_t), h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "frontier count");
+    if (round == 0) return GSIM_OK;
+    const int64_t words = ((h->ohi() + 63) >> 6) - (h->olo() >> 6);
+    hipLaunchKernelGGL(k_frontier_export, dim3((uint32_t)std::max<int64_t>(1, std::min<int64_t>((words + 3) / 4, 4096))),
+                       dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a, (const uint32_t*)h->sh->d_gid,
+                       out, d_cnt, cap);
+    return hip_check(h, hipGetLastError(), "k_frontier_export");
 }
+
+int deliver_frontier_import(gsim_handle* h, int64_t round, const uint64_t* in, int64_t n)
+{
+    if (n <= 0 || round == 0) return GSIM_OK;
+    RoundArgs a = make_round_args(h, round);
+    hipLaunchKernelGGL(k_frontier_import, dim3((uint32_t)std::min<int64_t>((n + 255) / 256, 16384)), dim3(256), 0,
+                       h->stream, a, (const uint32_t*)h->sh->d_g2l, in, n);
+    return hip_check(h, hipGetLastError(), "k_frontier_import");
+}
+
+// The delivery kernel changed (gsim_set_kernel_variant): the fresh bits are
+// kept only by the topic-major one.
+int deliver_variant_changed(gsim_handle* h)
+{
+    Deliver* d = h->dl;
+    if (!d) return GSIM_OK;
+    int rc = deliver_flush(h);
+    if (rc) return rc;
+    const bool on = h->send_variant == 3 && send_tm_lds(h, d) <= kLdsBudget;
+    if (on != d->fresh_on) {
+        // the topic-major kernel's next frontier would be missing its fresh bits
+        if (on && d->next_round > 0) {
+            h->err = "the delivery kernel can change to topic-major only before the first round";
+            return GSIM_ESTATE;
+        }
+        const size_t bytes = (size_t)d->cfg.ring * (size_t)((h->n + 63) / 64) * 8;
+        hipError_t e = hipMemsetAsync(d->d_fresh, 0, bytes, h->stream);
+        if (e != hipSuccess) return hip_check(h, e, "fresh bits");
+        d->fresh_on = on;
+    }
+    return GSIM_OK;
+}
+
 int32_t* deliver_slot_last(gsim_handle* h) { return h->dl ? h->dl->d_slot_last : nullptr; }
 
 extern "C" {
@@ -1808,7 +1822,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     Deliver* d = new Deliver();
     d->cfg = *cfg;
     const size_t ring = (size_t)cfg->ring, N = (size_t)h->n, T = (size_t)std::max(1, h->t);
-    const size_t CN = (size_t)(h->ohi() - h->olo());   // peers with seen-set cells (a shard's owned peers)
+    const size_t CN = N;   // every local peer has cells (a shard's ghost cells: imported first-seen rounds)
     const size_t words = (size_t)nnew_words(d);
     hipError_t e = hipSuccess;
     auto A = [&](void** p, size_t bytes) {
@@ -1820,6 +1834,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_minv, ring);
     A((void**)&d->d_cell, ring * CN * 8);
     A((void**)&d->d_seenbm, ring * ((CN + 63) / 64) * 8);
+    A((void**)&d->d_fresh, ring * ((CN + 63) / 64) * 8);
     A((void**)&d->d_mpub, ring * 4);
     A((void**)&d->d_roff, (size_t)cfg->rounds * 8);
     A((void**)&d->d_lastput, T * N * 4);
@@ -1850,8 +1865,10 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
         return e == hipErrorOutOfMemory ? GSIM_ENOMEM : GSIM_EDEVICE;
     }
     h->dl = d;
+    d->fresh_on = h->send_variant == 3 && send_tm_lds(h, d) <= kLdsBudget;
     e = hipMemsetAsync(d->d_cell, 0xFF, ring * CN * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_seenbm, 0, ring * ((CN + 63) / 64) * 8, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_fresh, 0, ring * ((CN + 63) / 64) * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_mpub, 0, ring * 4, h->stream);
     if (e == hipSuccess) {
         std::vector<int64_t> roff((size_t)cfg->rounds);
@@ -1918,7 +1935,7 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
     ProfScope ps(h, GSIM_K_PUBLISH);
     RoundArgs a = make_round_args(h, round);
     const int64_t per_block = 256 * 16;
-    const int gx = (int)std::min<int64_t>((h->ohi() - h->olo() + per_block - 1) / per_block, 1024);
+    const int gx = (int)std::min<int64_t>((h->n + per_block - 1) / per_block, 1024);
     hipLaunchKernelGGL(k_reset_slots, dim3(std::max(gx, 1), count), dim3(256), 0, h->stream, a,
                        (const gsim_msg*)d->d_pub, count);
     hipLaunchKernelGGL(k_publish, dim3((count + 255) / 256), dim3(256), 0, h->stream, a,
@@ -1935,13 +1952,13 @@ int gsim_round(gsim_handle* h, int64_t round)
     if (!h) return GSIM_EINVAL;
     if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
     if (h->sh) { h->err = "a shard's rounds run through its group (gsim_group_round)"; return GSIM_ESTATE; }
-    int rc = deliver_round_send(h, round);
+    int rc = deliver_round_prepare(h, round);
+    if (!rc) rc = deliver_round_send(h, round);
     if (!rc) rc = deliver_round_post(h, round);
     if (!rc) rc = deliver_round_control(h, round);
+    if (!rc) rc = deliver_round_ihave(h, round);
     if (rc) return rc;
-    if (round % h->dl->cfg.rounds == 0) rc = launch_ihave(h, round);
-    if (rc) return rc;
-    h->dl->next_round = round + 1;
+    deliver_round_end(h, round);
     return GSIM_OK;
 }
 

@@ -138,33 +138,32 @@ struct ShardCtx {
     std::vector<int64_t> gbase, gcnt;      // [K] ghost rows of shard s's peers (local edges)
     std::vector<int64_t> xoff;             // [K+1] cross-out lists, concatenated (d_xgather)
     uint32_t* d_gid = nullptr;             // [n] global id of each local peer
-    uint8_t* d_pshard = nullptr;           // [n] shard of each local peer
-    uint32_t* d_xr = nullptr;              // [e] owned-row cross edge: the receiver shard's record index
+    uint32_t* d_g2l = nullptr;             // [N_global] local id of a global peer (0xFFFFFFFF: not local)
     uint32_t* d_ymap = nullptr;            // [e] ghost-row edge: the owner shard's owned-row edge index
     uint32_t* d_xgather = nullptr;         // [n_cross] cross-out lists (local edge indices)
-    int64_t* d_bounds = nullptr;           // [K+1] device copy of bounds
-    // per-round halo buffers (allocated by gsim_group_msgs_init)
-    uint64_t* d_xout = nullptr;            // [K][xcap] outbound copies: record index there | slot << 32
-    uint32_t* d_xcnt = nullptr;            // [K] outbound copy counts
-    int64_t xcap = 0;
-    uint64_t* d_xin = nullptr;             // inbound copies (every source, concatenated)
-    int64_t xin_cap = 0;
-    uint32_t* d_xin_n = nullptr;           // [1] inbound count (k_gossip_deliver's queue length)
+    uint8_t* d_pgate = nullptr;            // [e] ghost-row edge: the sender's score of the receiver >= publishThreshold
+    // frontier exchange (gsim_group_msgs_init)
+    uint64_t* d_fout = nullptr;            // owned forwarders of the round (k_frontier_export)
+    uint32_t* d_fcnt = nullptr;
+    int64_t fcap = 0;
+    uint64_t* d_fin = nullptr;             // every other shard's forwarders
+    int64_t fin_cap = 0;
+    // control exchange
     uint64_t* d_cout = nullptr;            // [K][ccap] outbound control entries: edge | topic << 32 | bits << 40
     uint32_t* d_ccnt = nullptr;            // [K]
     int64_t ccap = 0;
     uint64_t* d_cin = nullptr;             // inbound control entries
     int64_t cin_cap = 0;
-    uint64_t* d_gout = nullptr;            // [n_cross] gossip marks out: topic mask of gsel
-    uint8_t* d_gsout = nullptr;            // [n_cross] gstate out
-    uint64_t* d_gin = nullptr;             // [e] gossip marks in (ghost-row positions)
+    // router state of cross edges (mesh / fanout masks, connected | direct | publish gate)
+    uint64_t *d_rmesh_out = nullptr, *d_rfan_out = nullptr;   // [n_cross]
+    uint8_t* d_rflag_out = nullptr;
+    uint64_t *d_rmesh_in = nullptr, *d_rfan_in = nullptr;     // [e] (ghost-row positions)
+    uint8_t* d_rflag_in = nullptr;
+    // gossip marks of cross edges
+    uint64_t* d_gout = nullptr;            // [n_cross] topic mask of gsel
+    uint8_t* d_gsout = nullptr;            // [n_cross] gstate
+    uint64_t* d_gin = nullptr;             // [e] (ghost-row positions)
     uint8_t* d_gsin = nullptr;             // [e]
-    int32_t* d_slot_last_g = nullptr;      // [ring] slot_last, MAX over shards
-    uint32_t* d_act = nullptr;             // [ring] active IHAVE slots (same list on every shard)
-    uint64_t* d_hbm = nullptr;             // holder bits of every shard's peers per active slot
-    int64_t hbm_cap = 0;                   // words
-    int64_t* d_hoff = nullptr;             // [K] word offset of each shard's block in d_hbm
-    std::vector<int32_t> act;              // host copy of the active slots
     uint32_t* h_counts = nullptr;          // pinned scratch for count readbacks
 };
 
@@ -315,16 +314,17 @@ int deliver_check_errors(gsim_handle* h);             // queue overflow / early 
 int handle_control(gsim_handle* h, int32_t round, int64_t now);   // heartbeat.hip: k_handle_control
 // round stages (deliver.hip; gsim_round runs them in order, a sharded group
 // exchanges between them, shard.hip)
+int deliver_round_prepare(gsim_handle* h, int64_t round);
 int deliver_round_send(gsim_handle* h, int64_t round);
 int deliver_round_queue(gsim_handle* h, int64_t round, const uint64_t* q, const uint32_t* d_n, int64_t cap);
 int deliver_round_post(gsim_handle* h, int64_t round);
 int deliver_round_control(gsim_handle* h, int64_t round);
-int deliver_ihave_count(gsim_handle* h, int64_t g, bool* run);
-int deliver_ihave_walk(gsim_handle* h);
-uint32_t* deliver_gcount(gsim_handle* h);             // [2][ring] holders / wanting receivers per slot
-int32_t* deliver_slot_last(gsim_handle* h);           // [ring]
+int deliver_round_ihave(gsim_handle* h, int64_t round);
 void deliver_round_end(gsim_handle* h, int64_t round);
-int deliver_holder_bits(gsim_handle* h, int64_t g, const uint32_t* d_act, int32_t n_act, uint64_t* out);
+int32_t* deliver_slot_last(gsim_handle* h);           // [ring]
+int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32_t* d_cnt, int64_t cap);
+int deliver_frontier_import(gsim_handle* h, int64_t round, const uint64_t* in, int64_t n);
+int deliver_variant_changed(gsim_handle* h);          // gsim_set_kernel_variant(h, 2, v)
 // heartbeat.hip: the control inbox ([2][T][E] by round parity) and its per-receiver summary ([2][N])
 uint8_t* extra_ctl(gsim_handle* h);
 uint64_t* extra_cany(gsim_handle* h);

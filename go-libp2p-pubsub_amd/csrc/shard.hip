@@ -4,21 +4,24 @@
 // The reference runs one router per host and moves RPCs between hosts over
 // libp2p streams (gossipsub.go:1138-1202 sendRPC).  Here one simulated network
 // is split into contiguous peer ranges (shard_plan.cpp).  Each shard is an
-// ordinary engine handle over its local graph — owned rows plus ghost rows —
-// that computes only for its owned peers, and the group moves between shards
-// exactly what a remote neighbour produced:
-//   per round      message copies to ghost receivers (k_send_tm queues them:
-//                  the receiver's record there | slot), delivered by the
-//                  receiving shard like any arriving copy;
-//   per control    GRAFT/PRUNE records written into ghost receivers' inboxes;
-//   per heartbeat  the gossip marks (emitGossip's choice per topic + the
-//                  advertiser's IWANT gate) of cross edges, into the receiving
-//                  shard's ghost rows;
-//   per IHAVE      the per-slot holder / want counts (a sum), slot activity (a
-//                  max) and the holders' bitmaps (an all-gather).
-// Two transports move the bytes: in-process (every shard in this process, one
-// HIP stream each; device-to-device copies) and RCCL (one shard per process,
-// ncclSend/ncclRecv grouped all-to-all, all-reduce, broadcasts over xGMI).
+// ordinary engine handle over its local graph — owned rows plus ghost rows
+// (a remote neighbour's connections into the shard) — that computes only for
+// its owned peers.  Copies are pulled, not pushed: a shard learns which
+// ghosts forward which message this round and walks their ghost rows itself,
+// so every delivery is processed by the receiver's shard with the same
+// kernel as a local one.  What moves between shards:
+//   per round      the forwarders of the round (peer, first sender, slot),
+//                  from every shard to every other (the frontier);
+//   per control    GRAFT/PRUNE records written into ghost receivers' inboxes,
+//                  and then the router state of cross edges (mesh and fanout
+//                  bits, connected, direct, publish gate) into ghost rows;
+//   per heartbeat  the gossip marks of cross edges (emitGossip's choice per
+//                  topic + the advertiser's IWANT gate), into ghost rows.
+// A ghost's cell holds the first-seen round its shard exported, which is all
+// IHAVE needs to know about a remote advertiser.  Two transports move the
+// bytes: in-process (every shard in this process, one HIP stream each;
+// device-to-device copies) and RCCL (one shard per process, ncclSend/ncclRecv
+// grouped all-to-all over xGMI).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -42,11 +45,17 @@ namespace {
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
+// local peer ranges of the shards ([lo[s], lo[s+1]) are shard s's peers)
+struct PeerRanges {
+    int64_t lo[GSIM_MAX_SHARDS + 1];
+    int32_t K;
+};
+
 // GRAFT/PRUNE records written into ghost receivers' inboxes (plane `ctl`,
 // summary `cany`), one thread per ghost peer with a summary bit: entries
 // (owner shard's edge | topic << 32 | bits << 40) to the ghost's shard.
 __global__ __launch_bounds__(256) void k_ctl_export(uint8_t* ctl, uint64_t* cany, const uint32_t* row_ptr,
-                                                    const uint32_t* ymap, const uint8_t* pshard, int64_t E, int32_t T,
+                                                    const uint32_t* ymap, PeerRanges pr, int64_t E, int32_t T,
                                                     int64_t olo, int64_t ohi, int64_t n, uint64_t* out,
                                                     uint32_t* cnt, int64_t cap)
 {
@@ -59,7 +68,8 @@ __global__ __launch_bounds__(256) void k_ctl_export(uint8_t* ctl, uint64_t* cany
         uint64_t any = cany[g] & tmask;
         if (cany[g]) cany[g] = 0;
         if (!any) continue;
-        const uint32_t d = pshard[g];
+        uint32_t d = 0;
+        while ((int32_t)d + 1 < pr.K && g >= pr.lo[d + 1]) ++d;
         for (; any; any &= any - 1) {
             const int32_t t = __ffsll((long long)any) - 1;
             for (uint32_t e = row_ptr[g]; e < row_ptr[g + 1]; ++e) {
@@ -117,6 +127,49 @@ __global__ __launch_bounds__(256) void k_gsel_import(const uint64_t* in, const u
         const uint64_t m = in[e];
         for (int32_t t = 0; t < T; ++t) gsel[(int64_t)t * E + e] = (uint8_t)((m >> t) & 1ull);
         gstate[e] = gs_in[e];
+    }
+}
+
+// The router state of the owned rows' cross edges (cross-out order): the
+// mesh and fanout bits per topic, connected | direct | publish gate.
+__global__ __launch_bounds__(256) void k_router_export(const uint32_t* xgather, int64_t n_cross, const uint8_t* mflags,
+                                                       const uint8_t* rstate, const uint8_t* direct, const double* score,
+                                                       const uint32_t* rev, double pub_thr, int32_t T, int64_t E,
+                                                       uint64_t* mesh, uint64_t* fan, uint8_t* flags)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n_cross; q += stride) {
+        const uint32_t e = xgather[q];
+        uint64_t mm = 0, fm = 0;
+        for (int32_t t = 0; t < T; ++t) {
+            const uint8_t f = mflags[(int64_t)t * E + e];
+            mm |= (uint64_t)((f & GSIM_TF_MESH) != 0) << t;
+            fm |= (uint64_t)((f & GSIM_TF_FANOUT) != 0) << t;
+        }
+        mesh[q] = mm;
+        fan[q] = fm;
+        flags[q] = (uint8_t)(((rstate[e] & GSIM_ES_CONNECTED) ? 1 : 0) | (direct[e] ? 2 : 0) |
+                             (score[rev[e]] >= pub_thr ? 4 : 0));
+    }
+}
+
+// ... into the ghost rows (the ghost's edges into this shard).
+__global__ __launch_bounds__(256) void k_router_import(const uint64_t* mesh, const uint64_t* fan, const uint8_t* flags,
+                                                       uint8_t* mflags, uint8_t* rstate, uint8_t* direct, uint8_t* pgate,
+                                                       int32_t T, int64_t E, int64_t e_lo, int64_t e_hi)
+{
+    const int64_t nghost = e_lo + (E - e_hi);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < nghost; x += stride) {
+        const int64_t e = x < e_lo ? x : e_hi + (x - e_lo);
+        const uint64_t mm = mesh[e], fm = fan[e];
+        for (int32_t t = 0; t < T; ++t)
+            mflags[(int64_t)t * E + e] = (uint8_t)((((mm >> t) & 1ull) ? GSIM_TF_MESH : 0) |
+                                                   (((fm >> t) & 1ull) ? GSIM_TF_FANOUT : 0));
+        const uint8_t f = flags[e];
+        rstate[e] = (f & 1) ? GSIM_ES_CONNECTED : 0;
+        direct[e] = (f & 2) ? 1 : 0;
+        pgate[e] = (f & 4) ? 1 : 0;
     }
 }
 
@@ -337,8 +390,10 @@ struct gsim_group {
     int64_t N = 0, E = 0;
     std::vector<std::vector<uint32_t>> gid;   // per local shard: local -> global peer id (host)
     std::vector<std::vector<uint64_t>> gidx;  // per local shard: local -> global edge index (host)
+    std::vector<uint64_t> sub;                // the peers' subscriptions (publish: fanout possible?)
     int32_t ring = 0, rounds = 0;
     bool msgs = false;
+    bool router_dirty = true;                 // ghost rows' router state must be re-imported
 
     int fail(int rc, const std::string& m)
     {
@@ -374,10 +429,10 @@ void free_shard_ctx(gsim_handle* h)
     ShardCtx* s = h->sh;
     if (!s) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(s->d_gid); f(s->d_pshard); f(s->d_xr); f(s->d_ymap); f(s->d_xgather); f(s->d_bounds);
-    f(s->d_xout); f(s->d_xcnt); f(s->d_xin); f(s->d_xin_n); f(s->d_cout); f(s->d_ccnt); f(s->d_cin);
-    f(s->d_gout); f(s->d_gsout); f(s->d_gin); f(s->d_gsin); f(s->d_slot_last_g); f(s->d_act); f(s->d_hbm);
-    f(s->d_hoff);
+    f(s->d_gid); f(s->d_g2l); f(s->d_ymap); f(s->d_xgather); f(s->d_pgate);
+    f(s->d_fout); f(s->d_fcnt); f(s->d_fin); f(s->d_cout); f(s->d_ccnt); f(s->d_cin);
+    f(s->d_rmesh_out); f(s->d_rfan_out); f(s->d_rflag_out); f(s->d_rmesh_in); f(s->d_rfan_in); f(s->d_rflag_in);
+    f(s->d_gout); f(s->d_gsout); f(s->d_gin); f(s->d_gsin);
     if (s->h_counts) (void)hipHostFree(s->h_counts);
     delete s;
     h->sh = nullptr;
@@ -404,6 +459,28 @@ int sync_all(gsim_group* g)
     return GSIM_OK;
 }
 
+// A dense exchange over the cross edges: every local shard's cross-out
+// ordered `elem`-byte records (out[l] at xoff) into the other shards' ghost
+// blocks (in[l] at gbase).
+int exchange_dense(gsim_group* g, const std::vector<const void*>& out, const std::vector<void*>& in, size_t elem)
+{
+    const size_t L = g->hs.size();
+    const int K = g->K;
+    std::vector<std::vector<const void*>> sp(L, std::vector<const void*>((size_t)K, nullptr));
+    std::vector<std::vector<void*>> rp(L, std::vector<void*>((size_t)K, nullptr));
+    std::vector<std::vector<uint64_t>> sb(L, std::vector<uint64_t>((size_t)K, 0)), rb = sb;
+    for (size_t l = 0; l < L; ++l) {
+        const ShardCtx* s = g->hs[l]->sh;
+        for (int q = 0; q < K; ++q) {
+            sp[l][(size_t)q] = (const uint8_t*)out[l] + (size_t)s->xoff[(size_t)q] * elem;
+            sb[l][(size_t)q] = (uint64_t)(s->xoff[(size_t)q + 1] - s->xoff[(size_t)q]) * elem;
+            rp[l][(size_t)q] = (uint8_t*)in[l] + (size_t)s->gbase[(size_t)q] * elem;
+            rb[l][(size_t)q] = (uint64_t)s->gcnt[(size_t)q] * elem;
+        }
+    }
+    return g->take_tr(g->tr->alltoallv(sp, sb, rp, rb));
+}
+
 // GRAFT/PRUNE records in ghost receivers' inboxes of plane `parity` go to
 // their shards (after the heartbeat: parity 0; after control round r: r+1).
 int exchange_control(gsim_group* g, int parity)
@@ -421,8 +498,11 @@ int exchange_control(gsim_group* g, int parity)
         if (hipMemsetAsync(s->d_ccnt, 0, sizeof(uint32_t) * K, h->stream) != hipSuccess)
             return g->fail(GSIM_EDEVICE, "control count reset");
         const int64_t nghost = s->own_lo + (h->n - s->own_hi);
+        PeerRanges pr{};
+        pr.K = K;
+        for (int q = 0; q <= K; ++q) pr.lo[q] = s->lpeer[(size_t)q];
         hipLaunchKernelGGL(k_ctl_export, dim3(grid_for(nghost)), dim3(256), 0, h->stream, ctl, cany,
-                           (const uint32_t*)h->d_row_ptr, (const uint32_t*)s->d_ymap, (const uint8_t*)s->d_pshard,
+                           (const uint32_t*)h->d_row_ptr, (const uint32_t*)s->d_ymap, pr,
                            h->e, std::max(1, h->t), s->own_lo, s->own_hi, h->n, s->d_cout, s->d_ccnt, s->ccap);
         if (hipMemcpyAsync(s->h_counts, s->d_ccnt, sizeof(uint32_t) * K, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
             hipStreamSynchronize(h->stream) != hipSuccess)
@@ -474,38 +554,23 @@ int exchange_control(gsim_group* g, int parity)
 int exchange_gossip_marks(gsim_group* g)
 {
     const size_t L = g->hs.size();
-    const int K = g->K;
-    std::vector<std::vector<const void*>> sp(L, std::vector<const void*>((size_t)K, nullptr));
-    std::vector<std::vector<void*>> rp(L, std::vector<void*>((size_t)K, nullptr));
-    std::vector<std::vector<uint64_t>> sb(L, std::vector<uint64_t>((size_t)K, 0)), rb = sb;
-    std::vector<std::vector<const void*>> sp2 = sp;
-    std::vector<std::vector<void*>> rp2 = rp;
-    std::vector<std::vector<uint64_t>> sb2 = sb, rb2 = sb;
+    std::vector<const void*> o1(L), o2(L);
+    std::vector<void*> i1(L), i2(L);
     for (size_t l = 0; l < L; ++l) {
         gsim_handle* h = g->hs[l];
         ShardCtx* s = h->sh;
         GossipView gv{};
         if (!deliver_gossip_view(h, &gv)) return GSIM_OK;      // no message state: nothing gossips
         (void)hipSetDevice(h->device);
-        const int64_t ncross = s->xoff[(size_t)K];
+        const int64_t ncross = s->xoff[(size_t)g->K];
         if (ncross)
             hipLaunchKernelGGL(k_gsel_export, dim3(grid_for(ncross)), dim3(256), 0, h->stream,
                                (const uint32_t*)s->d_xgather, ncross, (const uint8_t*)gv.gsel,
                                (const uint8_t*)gv.gstate, h->t, h->e, s->d_gout, s->d_gsout);
-        for (int q = 0; q < K; ++q) {
-            const int64_t n_out = s->xoff[(size_t)q + 1] - s->xoff[(size_t)q];
-            sp[l][(size_t)q] = s->d_gout + s->xoff[(size_t)q];
-            sb[l][(size_t)q] = (uint64_t)n_out * 8;
-            sp2[l][(size_t)q] = s->d_gsout + s->xoff[(size_t)q];
-            sb2[l][(size_t)q] = (uint64_t)n_out;
-            rp[l][(size_t)q] = s->d_gin + s->gbase[(size_t)q];
-            rb[l][(size_t)q] = (uint64_t)s->gcnt[(size_t)q] * 8;
-            rp2[l][(size_t)q] = s->d_gsin + s->gbase[(size_t)q];
-            rb2[l][(size_t)q] = (uint64_t)s->gcnt[(size_t)q];
-        }
+        o1[l] = s->d_gout; o2[l] = s->d_gsout; i1[l] = s->d_gin; i2[l] = s->d_gsin;
     }
-    int rc = g->take_tr(g->tr->alltoallv(sp, sb, rp, rb));
-    if (!rc) rc = g->take_tr(g->tr->alltoallv(sp2, sb2, rp2, rb2));
+    int rc = exchange_dense(g, o1, i1, 8);
+    if (!rc) rc = exchange_dense(g, o2, i2, 1);
     if (rc) return rc;
     for (size_t l = 0; l < L; ++l) {
         gsim_handle* h = g->hs[l];
@@ -523,8 +588,52 @@ int exchange_gossip_marks(gsim_group* g)
     return GSIM_OK;
 }
 
-// the copies every shard queued for ghost receivers in round `round`
-int exchange_copies(gsim_group* g, int64_t round)
+// The router state of cross edges into the ghost rows: what a ghost sender's
+// forwarding decision needs (mesh / fanout membership, connected, direct,
+// the flood-publish gate on its score of the receiver).
+int exchange_router(gsim_group* g)
+{
+    const size_t L = g->hs.size();
+    std::vector<const void*> o1(L), o2(L), o3(L);
+    std::vector<void*> i1(L), i2(L), i3(L);
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        (void)hipSetDevice(h->device);
+        const int64_t ncross = s->xoff[(size_t)g->K];
+        if (ncross)
+            hipLaunchKernelGGL(k_router_export, dim3(grid_for(ncross)), dim3(256), 0, h->stream,
+                               (const uint32_t*)s->d_xgather, ncross, (const uint8_t*)h->d_mflags,
+                               (const uint8_t*)h->d_rstate, (const uint8_t*)h->d_direct, (const double*)h->d_score,
+                               (const uint32_t*)h->d_rev, h->th.publish_threshold, h->t, h->e, s->d_rmesh_out,
+                               s->d_rfan_out, s->d_rflag_out);
+        o1[l] = s->d_rmesh_out; o2[l] = s->d_rfan_out; o3[l] = s->d_rflag_out;
+        i1[l] = s->d_rmesh_in; i2[l] = s->d_rfan_in; i3[l] = s->d_rflag_in;
+    }
+    int rc = exchange_dense(g, o1, i1, 8);
+    if (!rc) rc = exchange_dense(g, o2, i2, 8);
+    if (!rc) rc = exchange_dense(g, o3, i3, 1);
+    if (rc) return rc;
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        (void)hipSetDevice(h->device);
+        const int64_t nghost = s->own_e_lo + (h->e - s->own_e_hi);
+        if (nghost)
+            hipLaunchKernelGGL(k_router_import, dim3(grid_for(nghost)), dim3(256), 0, h->stream,
+                               (const uint64_t*)s->d_rmesh_in, (const uint64_t*)s->d_rfan_in,
+                               (const uint8_t*)s->d_rflag_in, h->d_mflags, h->d_rstate, h->d_direct, s->d_pgate,
+                               h->t, h->e, s->own_e_lo, s->own_e_hi);
+        if (hipGetLastError() != hipSuccess) return g->fail(GSIM_EDEVICE, "k_router_import");
+        h->score_version++;    // ghost rows' connected / direct bits feed the delivery state
+    }
+    g->router_dirty = false;
+    return GSIM_OK;
+}
+
+// Round `round`'s forwarders: every shard's owned ones to every other shard,
+// which imports its ghosts among them.
+int exchange_frontier(gsim_group* g, int64_t round)
 {
     const size_t L = g->hs.size();
     const int K = g->K;
@@ -533,14 +642,14 @@ int exchange_copies(gsim_group* g, int64_t round)
         gsim_handle* h = g->hs[l];
         ShardCtx* s = h->sh;
         (void)hipSetDevice(h->device);
-        if (hipMemcpyAsync(s->h_counts, s->d_xcnt, sizeof(uint32_t) * K, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+        int rc = g->take(h, deliver_frontier_export(h, round, s->d_fout, s->d_fcnt, s->fcap));
+        if (rc) return rc;
+        if (hipMemcpyAsync(s->h_counts, s->d_fcnt, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
             hipStreamSynchronize(h->stream) != hipSuccess)
-            return g->fail(GSIM_EDEVICE, "copy counts");
-        for (int d = 0; d < K; ++d) {
-            if ((int64_t)s->h_counts[d] > s->xcap)
-                return g->fail(GSIM_ERANGE, "copy queue to another shard overflowed (raise gsim_msg_config.max_frontier)");
-            scnt[l][(size_t)d] = s->h_counts[d];
-        }
+            return g->fail(GSIM_EDEVICE, "frontier count");
+        if ((int64_t)s->h_counts[0] > s->fcap)
+            return g->fail(GSIM_ERANGE, "a round's forwarders overflowed the frontier buffer (raise gsim_msg_config.max_frontier)");
+        for (int d = 0; d < K; ++d) scnt[l][(size_t)d] = d == g->ids[l] ? 0 : s->h_counts[0];
     }
     int rc = g->take_tr(g->tr->exchange_counts(scnt, rcnt));
     if (rc) return rc;
@@ -553,13 +662,13 @@ int exchange_copies(gsim_group* g, int64_t round)
         ShardCtx* s = h->sh;
         for (int q = 0; q < K; ++q) total[l] += (int64_t)rcnt[l][(size_t)q];
         (void)hipSetDevice(h->device);
-        rc = g->take(h, ensure(h, &s->d_xin, &s->xin_cap, total[l]));
+        rc = g->take(h, ensure(h, &s->d_fin, &s->fin_cap, total[l]));
         if (rc) return rc;
         int64_t off = 0;
         for (int q = 0; q < K; ++q) {
-            sp[l][(size_t)q] = s->d_xout + (int64_t)q * s->xcap;
+            sp[l][(size_t)q] = s->d_fout;
             sb[l][(size_t)q] = scnt[l][(size_t)q] * 8;
-            rp[l][(size_t)q] = s->d_xin + off;
+            rp[l][(size_t)q] = s->d_fin + off;
             rb[l][(size_t)q] = rcnt[l][(size_t)q] * 8;
             off += (int64_t)rcnt[l][(size_t)q];
         }
@@ -568,99 +677,12 @@ int exchange_copies(gsim_group* g, int64_t round)
     if (rc) return rc;
     for (size_t l = 0; l < L; ++l) {
         gsim_handle* h = g->hs[l];
-        ShardCtx* s = h->sh;
-        if (!total[l]) continue;
         (void)hipSetDevice(h->device);
-        s->h_counts[0] = (uint32_t)total[l];
-        if (hipMemcpyAsync(s->d_xin_n, s->h_counts, sizeof(uint32_t), hipMemcpyHostToDevice, h->stream) != hipSuccess ||
-            hipStreamSynchronize(h->stream) != hipSuccess)
-            return g->fail(GSIM_EDEVICE, "copy count upload");
         ProfScope ps(h, GSIM_K_SEND);
-        rc = g->take(h, deliver_round_queue(h, round, s->d_xin, s->d_xin_n, s->xin_cap));
+        rc = g->take(h, deliver_frontier_import(h, round, h->sh->d_fin, total[l]));
         if (rc) return rc;
     }
     return GSIM_OK;
-}
-
-// The IHAVE stage of a control round 0 (gossipsub.go:630-739) over shards.
-int group_ihave(gsim_group* g, int64_t round)
-{
-    const size_t L = g->hs.size();
-    const int K = g->K;
-    // slot activity: the max over shards (the candidate-slot filter)
-    std::vector<void*> p(L);
-    for (size_t l = 0; l < L; ++l) {
-        gsim_handle* h = g->hs[l];
-        (void)hipSetDevice(h->device);
-        if (hipMemcpyAsync(h->sh->d_slot_last_g, deliver_slot_last(h), sizeof(int32_t) * (size_t)g->ring,
-                           hipMemcpyDeviceToDevice, h->stream) != hipSuccess)
-            return g->fail(GSIM_EDEVICE, "slot activity copy");
-        p[l] = h->sh->d_slot_last_g;
-    }
-    int rc = g->take_tr(g->tr->allreduce(p, g->ring, DT_I32, OP_MAX));
-    if (rc) return rc;
-    bool run = false;
-    for (size_t l = 0; l < L; ++l) {
-        gsim_handle* h = g->hs[l];
-        (void)hipSetDevice(h->device);
-        bool r = false;
-        rc = g->take(h, deliver_ihave_count(h, round, &r));
-        if (rc) return rc;
-        run = r;
-        p[l] = deliver_gcount(h);
-    }
-    if (!run) return GSIM_OK;
-    rc = g->take_tr(g->tr->allreduce(p, 2 * (int64_t)g->ring, DT_U32, OP_SUM));
-    if (rc) return rc;
-    // the active slots, the same list on every shard (and in k_ihave)
-    gsim_handle* h0 = g->hs[0];
-    (void)hipSetDevice(h0->device);
-    std::vector<uint32_t> cnt(2 * (size_t)g->ring);
-    std::vector<int32_t> last((size_t)g->ring);
-    if (hipMemcpyAsync(cnt.data(), deliver_gcount(h0), cnt.size() * 4, hipMemcpyDeviceToHost, h0->stream) != hipSuccess ||
-        hipMemcpyAsync(last.data(), h0->sh->d_slot_last_g, last.size() * 4, hipMemcpyDeviceToHost, h0->stream) != hipSuccess ||
-        hipStreamSynchronize(h0->stream) != hipSuccess)
-        return g->fail(GSIM_EDEVICE, "gossip counts readback");
-    const int64_t tick = round / g->rounds;
-    const int64_t lo_round = std::max<int64_t>((tick - h0->gp.history_gossip) * g->rounds, 0);
-    std::vector<uint32_t> act;
-    for (int32_t m = 0; m < g->ring; ++m)
-        if (last[(size_t)m] >= lo_round && cnt[(size_t)m] != 0 && cnt[(size_t)g->ring + m] != 0) act.push_back((uint32_t)m);
-    const int32_t n_act = (int32_t)act.size();
-    // holder bitmaps: shard s's block is n_act x ceil(peers_s / 64) words at hoff[s]
-    std::vector<int64_t> hoff((size_t)K + 1, 0);
-    for (int s = 0; s < K; ++s) hoff[(size_t)s + 1] = hoff[(size_t)s] + (int64_t)n_act * ((g->bounds[(size_t)s + 1] - g->bounds[(size_t)s] + 63) / 64);
-    std::vector<void*> buf(L);
-    std::vector<uint64_t> off((size_t)K), bytes((size_t)K);
-    for (int s = 0; s < K; ++s) { off[(size_t)s] = (uint64_t)hoff[(size_t)s] * 8; bytes[(size_t)s] = (uint64_t)(hoff[(size_t)s + 1] - hoff[(size_t)s]) * 8; }
-    for (size_t l = 0; l < L; ++l) {
-        gsim_handle* h = g->hs[l];
-        ShardCtx* s = h->sh;
-        (void)hipSetDevice(h->device);
-        rc = g->take(h, ensure(h, &s->d_hbm, &s->hbm_cap, std::max<int64_t>(hoff[(size_t)K], 1)));
-        if (rc) return rc;
-        if ((n_act && hipMemcpyAsync(s->d_act, act.data(), act.size() * 4, hipMemcpyHostToDevice, h->stream) != hipSuccess) ||
-            hipMemcpyAsync(s->d_hoff, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice, h->stream) != hipSuccess)
-            return g->fail(GSIM_EDEVICE, "holder table upload");
-        ProfScope ps(h, GSIM_K_GOSSIP);
-        rc = g->take(h, deliver_holder_bits(h, round, s->d_act, n_act, s->d_hbm + hoff[(size_t)s->k]));
-        if (rc) return rc;
-        buf[l] = s->d_hbm;
-    }
-    if (n_act) {
-        rc = g->take_tr(g->tr->allgatherv(buf, off, bytes));
-        if (rc) return rc;
-    }
-    for (size_t l = 0; l < L; ++l) {
-        gsim_handle* h = g->hs[l];
-        (void)hipSetDevice(h->device);
-        // every shard's view of the counts and slots is the global one
-        if (hipMemcpyAsync(deliver_gcount(h), cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice, h->stream) != hipSuccess)
-            return g->fail(GSIM_EDEVICE, "gossip counts upload");
-        rc = g->take(h, deliver_ihave_walk(h));
-        if (rc) return rc;
-    }
-    return sync_all(g);   // the host-side tables above must outlive the uploads
 }
 
 // Create the group's shard handles; transport set by the caller.
@@ -779,12 +801,20 @@ int gsim_group_bounds(const gsim_group* g, int64_t* bounds)
     return GSIM_OK;
 }
 
+int gsim_group_state_written(gsim_group* g)
+{
+    if (!g) return GSIM_EINVAL;
+    g->router_dirty = true;
+    return GSIM_OK;
+}
+
 int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, const uint32_t* col,
                           const uint8_t* outbound, const uint64_t* subs, const uint32_t* ip_ptr,
                           const uint32_t* ip_ids, uint32_t n_ips, const int64_t* bounds)
 {
     if (!g || n <= 0 || !row_ptr || !col) return GSIM_EINVAL;
     const int K = g->K;
+    if (K > 1 && n >= 0xFFFFFF) return g->fail(GSIM_ERANGE, "a sharded network holds at most 2^24 - 2 peers");
     g->bounds.assign((size_t)K + 1, 0);
     if (bounds) {
         std::copy(bounds, bounds + K + 1, g->bounds.begin());
@@ -796,13 +826,12 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
     g->E = row_ptr[n];
     g->gid.assign(g->hs.size(), {});
     g->gidx.assign(g->hs.size(), {});
+    g->sub.assign(subs ? subs : nullptr, subs ? subs + n : nullptr);
     g->msgs = false;
-    // every shard's ghost-block bases, for the copy destinations (xr)
-    std::vector<std::vector<uint64_t>> gb_send(g->hs.size(), std::vector<uint64_t>((size_t)K, 0)), gb_recv;
-    std::vector<ShardLayout> lay(g->hs.size());
+    g->router_dirty = true;
     for (size_t l = 0; l < g->hs.size(); ++l) {
         gsim_handle* h = g->hs[l];
-        ShardLayout& L = lay[l];
+        ShardLayout L;
         std::string e;
         int rc = build_layout(n, row_ptr, col, g->bounds.data(), K, g->ids[l], &L, &e);
         if (rc) return g->fail(rc, e);
@@ -813,7 +842,6 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
         s->bounds = g->bounds; s->lpeer = L.lpeer; s->gbase = L.gbase; s->gcnt = L.gcnt;
         s->xoff.assign((size_t)K + 1, 0);
         for (int q = 0; q < K; ++q) s->xoff[(size_t)q + 1] = s->xoff[(size_t)q] + (int64_t)L.crossout[(size_t)q].size();
-        for (int q = 0; q < K; ++q) gb_send[l][(size_t)q] = (uint64_t)L.gbase[(size_t)q];
         // the local inputs
         std::vector<uint8_t> ob((size_t)L.e_loc, 0);
         if (outbound) for (int64_t x = 0; x < L.e_loc; ++x) ob[(size_t)x] = outbound[L.gidx[(size_t)x]];
@@ -833,60 +861,39 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
                              ip_ptr ? ipp.data() : nullptr, ip_ptr ? ipi.data() : nullptr, n_ips);
         if (rc) return g->take(h, rc);
         // device bookkeeping
-        std::vector<uint8_t> psh((size_t)L.n_loc);
-        for (int s2 = 0; s2 < K; ++s2)
-            for (int64_t x = L.lpeer[(size_t)s2]; x < L.lpeer[(size_t)s2 + 1]; ++x) psh[(size_t)x] = (uint8_t)s2;
         std::vector<uint32_t> xg;
         xg.reserve((size_t)L.n_cross);
         for (int q = 0; q < K; ++q) xg.insert(xg.end(), L.crossout[(size_t)q].begin(), L.crossout[(size_t)q].end());
-        if ((rc = dalloc(h, &s->d_gid, (size_t)L.n_loc)) || (rc = dalloc(h, &s->d_pshard, (size_t)L.n_loc)) ||
-            (rc = dalloc(h, &s->d_xr, (size_t)L.e_loc)) || (rc = dalloc(h, &s->d_ymap, (size_t)L.e_loc)) ||
-            (rc = dalloc(h, &s->d_xgather, xg.size())) || (rc = dalloc(h, &s->d_bounds, (size_t)K + 1)) ||
-            (rc = dalloc(h, &s->d_hoff, (size_t)K + 1)))
+        std::vector<uint32_t> g2l((size_t)n, kNone);
+        for (int64_t x = 0; x < L.n_loc; ++x) g2l[L.gid[(size_t)x]] = (uint32_t)x;
+        const int64_t ncross = L.n_cross;
+        if ((rc = dalloc(h, &s->d_gid, (size_t)L.n_loc)) || (rc = dalloc(h, &s->d_g2l, (size_t)n)) ||
+            (rc = dalloc(h, &s->d_ymap, (size_t)L.e_loc)) || (rc = dalloc(h, &s->d_xgather, xg.size())) ||
+            (rc = dalloc(h, &s->d_pgate, (size_t)L.e_loc)) ||
+            (rc = dalloc(h, &s->d_rmesh_out, (size_t)ncross)) || (rc = dalloc(h, &s->d_rfan_out, (size_t)ncross)) ||
+            (rc = dalloc(h, &s->d_rflag_out, (size_t)ncross)) || (rc = dalloc(h, &s->d_rmesh_in, (size_t)L.e_loc)) ||
+            (rc = dalloc(h, &s->d_rfan_in, (size_t)L.e_loc)) || (rc = dalloc(h, &s->d_rflag_in, (size_t)L.e_loc)))
             return g->take(h, rc);
-        if (hipHostMalloc((void**)&s->h_counts, sizeof(uint32_t) * GSIM_MAX_SHARDS, 0) != hipSuccess)
+        if (!s->h_counts && hipHostMalloc((void**)&s->h_counts, sizeof(uint32_t) * GSIM_MAX_SHARDS, 0) != hipSuccess)
             return g->fail(GSIM_ENOMEM, "pinned scratch");
         hipError_t he = hipMemcpy(s->d_gid, L.gid.data(), L.gid.size() * 4, hipMemcpyHostToDevice);
-        if (he == hipSuccess) he = hipMemcpy(s->d_pshard, psh.data(), psh.size(), hipMemcpyHostToDevice);
+        if (he == hipSuccess) he = hipMemcpy(s->d_g2l, g2l.data(), g2l.size() * 4, hipMemcpyHostToDevice);
         if (he == hipSuccess && !xg.empty()) he = hipMemcpy(s->d_xgather, xg.data(), xg.size() * 4, hipMemcpyHostToDevice);
-        if (he == hipSuccess) he = hipMemcpy(s->d_bounds, g->bounds.data(), g->bounds.size() * 8, hipMemcpyHostToDevice);
         if (he == hipSuccess) he = hipMemset(s->d_ymap, 0xFF, (size_t)L.e_loc * 4);
+        if (he == hipSuccess) he = hipMemset(s->d_pgate, 0, (size_t)L.e_loc);
         if (he != hipSuccess) return g->fail(GSIM_EDEVICE, "shard tables upload");
         g->gid[l] = L.gid;
         g->gidx[l] = L.gidx;
     }
-    // copy destinations: the receiving shard's ghost block for this shard + q
-    int rc = g->take_tr(g->tr->exchange_counts(gb_send, gb_recv));
-    if (rc) return rc;
-    for (size_t l = 0; l < g->hs.size(); ++l) {
-        gsim_handle* h = g->hs[l];
-        const ShardLayout& L = lay[l];
-        std::vector<uint32_t> xr((size_t)L.e_loc, kNone);
-        for (int64_t x = L.own_e_lo; x < L.own_e_hi; ++x) {
-            if (L.xq[(size_t)x] == kNone) continue;
-            const int d = shard_of_peer(g->bounds, L.gid[L.col[(size_t)x]]);
-            xr[(size_t)x] = (uint32_t)(gb_recv[l][(size_t)d] + L.xq[(size_t)x]);
-        }
-        (void)hipSetDevice(h->device);
-        if (hipMemcpy(h->sh->d_xr, xr.data(), xr.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
-            return g->fail(GSIM_EDEVICE, "copy destinations upload");
-    }
     // control destinations: a ghost-row edge's owned-row edge in the ghost's
     // shard = that shard's cross-out list into this one (ymap, ghost blocks)
-    const int Kk = K;
-    std::vector<std::vector<const void*>> sp(g->hs.size(), std::vector<const void*>((size_t)Kk, nullptr));
-    std::vector<std::vector<void*>> rp(g->hs.size(), std::vector<void*>((size_t)Kk, nullptr));
-    std::vector<std::vector<uint64_t>> sbytes(g->hs.size(), std::vector<uint64_t>((size_t)Kk, 0)), rbytes = sbytes;
+    std::vector<const void*> xo(g->hs.size());
+    std::vector<void*> ym(g->hs.size());
     for (size_t l = 0; l < g->hs.size(); ++l) {
-        ShardCtx* s = g->hs[l]->sh;
-        for (int q = 0; q < Kk; ++q) {
-            sp[l][(size_t)q] = s->d_xgather + s->xoff[(size_t)q];
-            sbytes[l][(size_t)q] = (uint64_t)(s->xoff[(size_t)q + 1] - s->xoff[(size_t)q]) * 4;
-            rp[l][(size_t)q] = s->d_ymap + s->gbase[(size_t)q];
-            rbytes[l][(size_t)q] = (uint64_t)s->gcnt[(size_t)q] * 4;
-        }
+        xo[l] = g->hs[l]->sh->d_xgather;
+        ym[l] = g->hs[l]->sh->d_ymap;
     }
-    rc = g->take_tr(g->tr->alltoallv(sp, sbytes, rp, rbytes));
+    int rc = exchange_dense(g, xo, ym, 4);
     if (rc) return rc;
     return sync_all(g);
 }
@@ -900,29 +907,26 @@ int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg)
         if (rc) return g->take(h, rc);
         ShardCtx* s = h->sh;
         const int K = g->K;
-        int64_t xmax = 0, gmax = 0;
-        for (int q = 0; q < K; ++q) {
-            xmax = std::max<int64_t>(xmax, s->xoff[(size_t)q + 1] - s->xoff[(size_t)q]);
-            gmax = std::max<int64_t>(gmax, s->gcnt[(size_t)q]);
-        }
-        // per destination: a round's copies cross each cross edge at most once per
-        // message; max_frontier overrides (entries per destination shard)
-        s->xcap = cfg->max_frontier > 0 ? cfg->max_frontier : std::max<int64_t>(8 * xmax, 1 << 16);
+        int64_t gmax = 0;
+        for (int q = 0; q < K; ++q) gmax = std::max<int64_t>(gmax, s->gcnt[(size_t)q]);
+        // a round's forwarders: each owned peer at most once per message it first
+        // saw in the round before; max_frontier overrides (entries per shard)
+        s->fcap = cfg->max_frontier > 0 ? cfg->max_frontier : std::max<int64_t>(8 * (s->own_hi - s->own_lo), 1 << 16);
         s->ccap = std::max<int64_t>(4 * gmax, 1 << 14);
         const int64_t ncross = s->xoff[(size_t)K];
         rc = GSIM_OK;
         auto A = [&](auto** p, size_t n) { if (!rc) rc = dalloc(h, p, n); };
-        A(&s->d_xout, (size_t)(K * s->xcap));
-        A(&s->d_xcnt, (size_t)K);
-        A(&s->d_xin_n, 1);
-        A(&s->d_cout, (size_t)(K * s->ccap));
-        A(&s->d_ccnt, (size_t)K);
-        A(&s->d_gout, (size_t)ncross);
-        A(&s->d_gsout, (size_t)ncross);
-        A(&s->d_gin, (size_t)h->e);
-        A(&s->d_gsin, (size_t)h->e);
-        A(&s->d_slot_last_g, (size_t)cfg->ring);
-        A(&s->d_act, (size_t)cfg->ring);
+        if (s->d_fout) { (void)hipFree(s->d_fout); s->d_fout = nullptr; }
+        A(&s->d_fout, (size_t)s->fcap);
+        if (!s->d_fcnt) A(&s->d_fcnt, 1);
+        if (!s->d_cout) {
+            A(&s->d_cout, (size_t)(K * s->ccap));
+            A(&s->d_ccnt, (size_t)K);
+            A(&s->d_gout, (size_t)ncross);
+            A(&s->d_gsout, (size_t)ncross);
+            A(&s->d_gin, (size_t)h->e);
+            A(&s->d_gsin, (size_t)h->e);
+        }
         if (rc) return g->take(h, rc);
         if (hipMemset(s->d_gin, 0, (size_t)h->e * 8) != hipSuccess || hipMemset(s->d_gsin, 0, (size_t)h->e) != hipSuccess)
             return g->fail(GSIM_EDEVICE, "gossip mark buffers");
@@ -935,6 +939,7 @@ int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg)
 
 #define GROUP_EACH(g, call)                                      \
     do {                                                         \
+        if (!(g)) return GSIM_EINVAL;                            \
         for (gsim_handle* h : (g)->hs) {                         \
             int rc_ = (call);                                    \
             if (rc_) return (g)->take(h, rc_);                   \
@@ -946,6 +951,7 @@ int gsim_group_set_seed(gsim_group* g, uint64_t seed) { GROUP_EACH(g, gsim_set_s
 int gsim_group_fill_synthetic(gsim_group* g, uint64_t seed, int64_t now, double p_mesh)
 {
     GROUP_EACH(g, gsim_fill_synthetic(h, seed, now, p_mesh));
+    g->router_dirty = true;
     return GSIM_OK;
 }
 
@@ -967,6 +973,22 @@ int gsim_group_set_ip_whitelist(gsim_group* g, const uint8_t* white)
     return GSIM_OK;
 }
 
+int gsim_group_set_ips(gsim_group* g, const uint32_t* ip_ptr, const uint32_t* ip_ids, uint32_t n_ips)
+{
+    if (!g || !ip_ptr) return GSIM_EINVAL;
+    for (size_t l = 0; l < g->hs.size(); ++l) {
+        std::vector<uint32_t> ipp(g->gid[l].size() + 1, 0), ipi;
+        for (size_t x = 0; x < g->gid[l].size(); ++x) {
+            const uint32_t gg = g->gid[l][x];
+            for (uint32_t q = ip_ptr[gg]; q < ip_ptr[gg + 1]; ++q) ipi.push_back(ip_ids[q]);
+            ipp[x + 1] = (uint32_t)ipi.size();
+        }
+        const int rc = gsim_set_ips(g->hs[l], ipp.data(), ipi.data(), n_ips);
+        if (rc) return g->take(g->hs[l], rc);
+    }
+    return GSIM_OK;
+}
+
 int gsim_group_set_direct_peers(gsim_group* g, const uint8_t* flags)
 {
     if (!g) return GSIM_EINVAL;
@@ -981,6 +1003,7 @@ int gsim_group_set_direct_peers(gsim_group* g, const uint8_t* flags)
         }
         if (rc) return g->take(g->hs[l], rc);
     }
+    g->router_dirty = true;
     return GSIM_OK;
 }
 
@@ -1005,13 +1028,14 @@ int gsim_group_set_topic_params(gsim_group* g, int32_t topic, const gsim_topic_s
 int gsim_group_refresh_scores(gsim_group* g, int64_t now)
 {
     GROUP_EACH(g, gsim_refresh_scores(h, now));
+    g->router_dirty = true;                          // the flood-publish gate reads the new snapshot
     return GSIM_OK;
 }
 
 int gsim_group_heartbeat(gsim_group* g, uint64_t tick, int64_t now)
 {
-    if (!g) return GSIM_EINVAL;
     GROUP_EACH(g, gsim_heartbeat(h, tick, now));
+    g->router_dirty = true;                          // meshes and fanouts changed
     int rc = exchange_control(g, 0);                 // GRAFT/PRUNE for control round 0
     if (!rc) rc = exchange_gossip_marks(g);
     return rc;
@@ -1030,6 +1054,9 @@ int gsim_group_publish(gsim_group* g, const gsim_msg* msgs, int32_t count, int64
         const int rc = gsim_publish(g->hs[l], v.data(), count, round);
         if (rc) return g->take(g->hs[l], rc);
     }
+    // an origin outside its topic may have chosen new fanout peers
+    for (int32_t q = 0; q < count; ++q)
+        if (g->sub.empty() || !((g->sub[msgs[q].origin] >> msgs[q].topic) & 1ull)) g->router_dirty = true;
     return GSIM_OK;
 }
 
@@ -1037,16 +1064,22 @@ int gsim_group_round(gsim_group* g, int64_t round)
 {
     if (!g) return GSIM_EINVAL;
     if (!g->msgs) return g->fail(GSIM_ESTATE, "gsim_group_msgs_init not called");
+    int rc = GSIM_OK;
+    if (g->router_dirty) {                           // the ghosts' forwarding state of this round
+        rc = exchange_router(g);
+        if (rc) return rc;
+    }
     for (gsim_handle* h : g->hs) {
         (void)hipSetDevice(h->device);
-        const int rc = deliver_round_send(h, round);
+        rc = deliver_round_prepare(h, round);        // commits of the last round: fresh forwarders
         if (rc) return g->take(h, rc);
     }
-    int rc = exchange_copies(g, round);
+    rc = exchange_frontier(g, round);                // the ghosts among them
     if (rc) return rc;
     for (gsim_handle* h : g->hs) {
         (void)hipSetDevice(h->device);
-        rc = deliver_round_post(h, round);
+        rc = deliver_round_send(h, round);
+        if (!rc) rc = deliver_round_post(h, round);
         if (!rc) rc = deliver_round_control(h, round);
         if (rc) return g->take(h, rc);
     }
@@ -1054,12 +1087,14 @@ int gsim_group_round(gsim_group* g, int64_t round)
     if (r < 2) {
         rc = exchange_control(g, (int)((r + 1) & 1));   // PRUNE replies for the next control round
         if (rc) return rc;
+        g->router_dirty = true;                         // control changed meshes
     }
-    if (r == 0) {
-        rc = group_ihave(g, round);
-        if (rc) return rc;
+    for (gsim_handle* h : g->hs) {
+        (void)hipSetDevice(h->device);
+        rc = deliver_round_ihave(h, round);             // ghost advertisers: their cells
+        if (rc) return g->take(h, rc);
+        deliver_round_end(h, round);
     }
-    for (gsim_handle* h : g->hs) deliver_round_end(h, round);
     return GSIM_OK;
 }
 
@@ -1085,6 +1120,7 @@ int gsim_group_set_connections(gsim_group* g, const uint32_t* pairs, int32_t cou
         const int rc = gsim_set_connections(g->hs[l], v.data(), (int32_t)(v.size() / 2), up, now);
         if (rc) return g->take(g->hs[l], rc);
     }
+    g->router_dirty = true;
     return GSIM_OK;
 }
 
@@ -1099,7 +1135,6 @@ static int group_sum(gsim_group* g, int (*fn)(gsim_handle*, int64_t*), int n, in
         for (int i = 0; i < n; ++i) acc[(size_t)i] += v[(size_t)i];
     }
     if (dynamic_cast<RcclTransport*>(g->tr.get())) {
-        gsim_handle* h = g->hs[0];
         int64_t* d = nullptr;
         if (hipMalloc((void**)&d, sizeof(int64_t) * (n + 1)) != hipSuccess) return g->fail(GSIM_ENOMEM, "totals scratch");
         acc.push_back(first_err ? 1 : 0);
@@ -1108,7 +1143,6 @@ static int group_sum(gsim_group* g, int (*fn)(gsim_handle*, int64_t*), int n, in
         if (!rc) rc = g->take_tr(g->tr->sync());
         (void)hipMemcpy(acc.data(), d, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost);
         (void)hipFree(d);
-        (void)h;
         if (rc) return rc;
         if (acc[(size_t)n] && !first_err) { first_err = GSIM_ERANGE; g->err = "another shard reported an error"; }
     }

@@ -204,6 +204,8 @@ SIGNATURES = [
     ("gsim_group_publish", c_int32, [c_void_p, c_void_p, c_int32, c_int64]),
     ("gsim_group_round", c_int32, [c_void_p, c_int64]),
     ("gsim_group_set_connections", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int64]),
+    ("gsim_group_set_ips", c_int32, [c_void_p, c_void_p, c_void_p, c_uint32]),
+    ("gsim_group_state_written", c_int32, [c_void_p]),
     ("gsim_group_msg_stats", c_int32, [c_void_p, c_void_p]),
     ("gsim_group_gossip_stats", c_int32, [c_void_p, c_void_p]),
     ("gsim_group_census", c_int32, [c_void_p, c_void_p]),

@@ -252,7 +252,7 @@ class ShardedEngine:
         c = _abi.CMsgConfig()
         c.ring, c.rounds, c.t0_ns = int(ring), int(rounds), int(t0)
         c.heartbeat_ns = int(heartbeat if heartbeat is not None else self.gossip.HeartbeatInterval)
-        c.max_frontier = int(max_frontier or 0)      # copies queued per destination shard per round
+        c.max_frontier = int(max_frontier or 0)      # forwarders one shard exports per round (0: default)
         c.max_arrivals = int(max_arrivals or 0)
         self._check(self.lib.gsim_group_msgs_init(self.g, ctypes.byref(c)))
         self._msg_cfg = c
@@ -279,6 +279,11 @@ class ShardedEngine:
     def set_connections(self, pairs, up: bool, now: int):
         p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint32).reshape(-1, 2))
         self._check(self.lib.gsim_group_set_connections(self.g, _ptr(p), int(p.shape[0]), 1 if up else 0, int(now)))
+
+    def set_ips(self, ip_ptr: np.ndarray, ip_ids: np.ndarray, n_ips: int):
+        pp = np.ascontiguousarray(ip_ptr, dtype=np.uint32)
+        ii = np.ascontiguousarray(ip_ids, dtype=np.uint32)
+        self._check(self.lib.gsim_group_set_ips(self.g, _ptr(pp), _ptr(ii), int(n_ips)))
 
     def msg_stats(self) -> list:
         out = np.zeros(4, dtype=np.int64)
@@ -391,6 +396,7 @@ class ShardedEngine:
             rc = self.lib.gsim_write_field(h, f, _ptr(loc), loc.nbytes)
             if rc != 0:
                 raise GsimError(rc, (self.lib.gsim_last_error(h) or b"").decode())
+        self._check(self.lib.gsim_group_state_written(self.g))
 
     def scores(self) -> np.ndarray:
         return self.read(_abi.F_SCORE)

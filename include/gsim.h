@@ -462,8 +462,12 @@ int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now_ns, double p_
  * network is split into contiguous peer ranges, one per shard (GPU); a shard
  * holds its peers' rows in full plus a "ghost" row per remote neighbour (that
  * neighbour's connections into the shard), so every record an owned observer
- * keeps is local, and the per-round halo exchange carries message copies,
- * GRAFT/PRUNE records and gossip marks between shards. */
+ * keeps is local.  Copies are pulled: each round every shard sends the
+ * others its forwarders of the round (peer, first sender, slot), and a shard
+ * walks the ghost rows of the remote forwarders itself, so each copy is
+ * delivered by the receiver's shard.  GRAFT/PRUNE records, the router state
+ * of cross edges (mesh / fanout bits, connected, direct, publish gate) and
+ * gossip marks move the same way.  At most 2^24 - 2 peers per network. */
 #define GSIM_MAX_SHARDS 64
 
 /* Contiguous peer ranges for `shards` shards balanced by the sum of (row
@@ -530,14 +534,19 @@ int gsim_group_set_peer_behaviour(gsim_group* g, const uint8_t* flags);
 int gsim_group_set_topic_params(gsim_group* g, int32_t topic, const gsim_topic_score_params* p);
 int gsim_group_set_seed(gsim_group* g, uint64_t seed);
 int gsim_group_fill_synthetic(gsim_group* g, uint64_t seed, int64_t now_ns, double p_mesh);
-/* max_frontier > 0 caps the copies one shard queues for another per round
- * (default 8 x their cross edges); GSIM_ERANGE when a round exceeds it. */
+/* max_frontier > 0 caps the forwarders one shard exports per round (default
+ * max(8 x owned peers, 65536)); GSIM_ERANGE when a round exceeds it. */
 int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg);
 int gsim_group_refresh_scores(gsim_group* g, int64_t now_ns);
 int gsim_group_heartbeat(gsim_group* g, uint64_t tick, int64_t now_ns);
 int gsim_group_publish(gsim_group* g, const gsim_msg* msgs, int32_t count, int64_t round);
 int gsim_group_round(gsim_group* g, int64_t round);
 int gsim_group_set_connections(gsim_group* g, const uint32_t* pairs, int32_t count, int32_t up, int64_t now_ns);
+int gsim_group_set_ips(gsim_group* g, const uint32_t* ip_ptr, const uint32_t* ip_ids, uint32_t n_ips);
+/* Router state (mesh / fanout flags, connection state, direct flags) was
+ * written through gsim_write_field on a shard handle: the ghost rows are
+ * refreshed from their owners before the next round. */
+int gsim_group_state_written(gsim_group* g);
 /* Totals of the whole job (summed over every shard, every process). */
 int gsim_group_msg_stats(gsim_group* g, int64_t* out4);
 int gsim_group_gossip_stats(gsim_group* g, int64_t* out4);
