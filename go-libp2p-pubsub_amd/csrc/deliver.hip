@@ -955,8 +955,9 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
             const int m = m0 + lane;
             const bool act = m < a.ring && a.slot_last[m] >= a.lo_round && gcount[m] != 0 && gcount[a.ring + m] != 0;
             // cost model: a holder walk probes ~Dlazy cells, a receiver walk ~deg
-            // (a sharded network pulls: receivers walk, holders are looked up)
-            const bool push = act && !a.sharded && (uint64_t)gcount[m] * 4u < (uint64_t)gcount[a.ring + m] * 32u;
+            // (a shard's holders include its ghosts: their ghost rows are their
+            // connections to its receivers)
+            const bool push = act && (uint64_t)gcount[m] * 4u < (uint64_t)gcount[a.ring + m] * 32u;
             const uint64_t b = __ballot(act);
             if (act) s_act[n + __popcll(b & ((1ull << lane) - 1))] = (uint16_t)(m | (push ? 0x8000 : 0));
             n += __popcll(b);
@@ -1035,9 +1036,11 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                     // holder me_id walks its row: the peers it gossiped t to
                     if (v && a.gsel[plane + e]) {
                         const uint32_t p = a.col[e], re = a.rev[e];
-                        req = a.gstate[re] && a.cell[row_m + (p - a.clo)] == kUnseen64;   // p's gate on i, p has not seen m
+                        // p's gate on i, p has not seen m (a shard: p one of its receivers)
+                        req = p >= a.rlo && p < a.rhi && a.gstate[re] && a.cell[row_m + (p - a.clo)] == kUnseen64;
                         if (req) {
-                            const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, p, 0, P_PROMISE, m, me_id);
+                            const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, a.gid ? a.gid[p] : p, 0, P_PROMISE,
+                                                          m, me_g);
                             atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[re]), (unsigned long long)key);
                             r = e;
                             resp = a.respond && a.gstate[e] && !ign_s;
@@ -1700,32 +1703,57 @@ void deliver_round_end(gsim_handle* h, int64_t round) { h->dl->next_round = roun
 // connections into the shard) and delivers those copies itself.
 constexpr uint64_t kG24 = 0xFFFFFFull;
 
-__global__ __launch_bounds__(256) void k_frontier_export(RoundArgs a, const uint32_t* gid, uint64_t* out,
-                                                         uint32_t* cnt, int64_t cap)
+// Entries go only to the shards the forwarder has connections into (xmask:
+// bit q = a cross edge into shard q), one list of `cap` entries per shard.
+// One thread per (active slot, owned word); a block counts its entries per
+// shard in LDS, reserves each shard's range with one atomic, then writes.
+__global__ __launch_bounds__(256) void k_frontier_export(RoundArgs a, const uint32_t* gid, const uint64_t* xmask,
+                                                         uint64_t* out, uint32_t* cnt, int64_t cap, int32_t K)
 {
     extern __shared__ uint16_t s_act[];
     __shared__ int s_n;
+    __shared__ uint32_t s_cnt[GSIM_MAX_SHARDS], s_base[GSIM_MAX_SHARDS];
     const int nact = active_slots(a.nnew_prev, a.ring, s_act, &s_n);
-    const int lane = threadIdx.x & 63;
-    const int64_t w0 = (int64_t)a.rlo >> 6, w1 = ((int64_t)a.rhi + 63) >> 6;
-    for (int64_t x = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); x < (w1 - w0) * nact; x += (int64_t)gridDim.x * 4) {
-        const int64_t k = x / (w1 - w0), w = w0 + (x - k * (w1 - w0));
-        const uint32_t m = s_act[k];
-        uint64_t bits = a.fresh[(int64_t)m * a.nw + w];
-        const int64_t i = w * 64 + lane;
-        bits &= (w * 64 < (int64_t)a.rlo) ? ~0ull << ((int64_t)a.rlo - w * 64) : ~0ull;   // owned peers only
-        const bool me = ((bits >> lane) & 1ull) && i >= (int64_t)a.rlo && i < (int64_t)a.rhi;
-        const uint64_t mm = __ballot(me);
-        if (!mm) continue;
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(cnt, (uint32_t)__popcll(mm));
-        base = (uint32_t)__shfl((int)base, 0, 64);
-        if (me) {
+    const int tid = threadIdx.x;
+    const int64_t w0 = (int64_t)a.rlo >> 6, nwd = (((int64_t)a.rhi + 63) >> 6) - w0;
+    const int64_t items = nwd * nact;
+    for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < items; b0 += (int64_t)gridDim.x * 256) {   // block-uniform
+        for (int q = tid; q < K; q += 256) s_cnt[q] = 0;
+        __syncthreads();
+        const int64_t x = b0 + tid;
+        uint64_t bits = 0;
+        uint32_t m = 0;
+        int64_t w = 0;
+        if (x < items) {
+            const int64_t k = x / nwd;
+            w = w0 + (x - k * nwd);
+            m = s_act[k];
+            bits = a.fresh[(int64_t)m * a.nw + w];
+            if (w * 64 < (int64_t)a.rlo) bits &= ~0ull << ((int64_t)a.rlo - w * 64);        // owned peers only
+            if (w * 64 + 64 > (int64_t)a.rhi) bits &= (1ull << ((int64_t)a.rhi - w * 64)) - 1;
+        }
+        for (uint64_t b = bits; b; b &= b - 1) {
+            const int64_t i = w * 64 + __ffsll((long long)b) - 1;
+            for (uint64_t xm = xmask[i]; xm; xm &= xm - 1) atomicAdd(&s_cnt[__ffsll((long long)xm) - 1], 1u);
+        }
+        __syncthreads();
+        for (int q = tid; q < K; q += 256) {
+            s_base[q] = s_cnt[q] ? atomicAdd(cnt + q, s_cnt[q]) : 0u;
+            s_cnt[q] = 0;
+        }
+        __syncthreads();
+        for (uint64_t b = bits; b; b &= b - 1) {
+            const int64_t i = w * 64 + __ffsll((long long)b) - 1;
             const uint32_t f = (uint32_t)a.cell[(int64_t)m * a.CN + i] & kPeerMask;
             const uint64_t gf = f < a.N ? (uint64_t)gid[f] : kG24;
-            const int64_t pos = (int64_t)base + __popcll(mm & ((1ull << lane) - 1));
-            if (pos < cap) out[pos] = (uint64_t)gid[i] | (gf << 24) | ((uint64_t)m << 48);
+            const uint64_t v = (uint64_t)gid[i] | (gf << 24) | ((uint64_t)m << 48);
+            for (uint64_t xm = xmask[i]; xm; xm &= xm - 1) {
+                const int q = __ffsll((long long)xm) - 1;
+                const int64_t pos = (int64_t)s_base[q] + atomicAdd(&s_cnt[q], 1u);
+                if (pos < cap) out[(int64_t)q * cap + pos] = v;
+            }
         }
+        __syncthreads();
     }
 }
 
@@ -1743,8 +1771,12 @@ __global__ __launch_bounds__(256) void k_frontier_import(RoundArgs a, const uint
         const uint32_t m = (uint32_t)(v >> 48);
         a.cell[(int64_t)m * a.CN + l] = ((uint64_t)(uint32_t)(a.g - 1) << 32) | f;
         atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (l >> 6)), 1ull << (l & 63));
-        atomicOr(const_cast<uint32_t*>(a.nnew_prev) + (m >> 5), 1u << (m & 31));
-        atomicMax(&a.slot_last[m], (int32_t)(a.g - 1));
+        // many entries share a slot: test before the atomic (one 0 -> 1 transition)
+        uint32_t* nw = const_cast<uint32_t*>(a.nnew_prev) + (m >> 5);
+        if (!((__hip_atomic_load(nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (m & 31)) & 1u))
+            atomicOr(nw, 1u << (m & 31));
+        if (__hip_atomic_load(&a.slot_last[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int32_t)(a.g - 1))
+            atomicMax(&a.slot_last[m], (int32_t)(a.g - 1));
     }
 }
 
@@ -1752,13 +1784,14 @@ int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32
 {
     Deliver* d = h->dl;
     RoundArgs a = make_round_args(h, round);
-    hipError_t e = hipMemsetAsync(d_cnt, 0, sizeof(uint32_t), h->stream);
+    hipError_t e = hipMemsetAsync(d_cnt, 0, sizeof(uint32_t) * (size_t)h->sh->K, h->stream);
     if (e != hipSuccess) return hip_check(h, e, "frontier count");
     if (round == 0) return GSIM_OK;
     const int64_t words = ((h->ohi() + 63) >> 6) - (h->olo() >> 6);
-    hipLaunchKernelGGL(k_frontier_export, dim3((uint32_t)std::max<int64_t>(1, std::min<int64_t>((words + 3) / 4, 4096))),
+    const int64_t items = words * (int64_t)d->cfg.ring;      // an upper bound: the active slots are on the device
+    hipLaunchKernelGGL(k_frontier_export, dim3((uint32_t)std::max<int64_t>(1, std::min<int64_t>((items + 255) / 256, 2048))),
                        dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a, (const uint32_t*)h->sh->d_gid,
-                       out, d_cnt, cap);
+                       (const uint64_t*)h->sh->d_xmask, out, d_cnt, cap, (int32_t)h->sh->K);
     return hip_check(h, hipGetLastError(), "k_frontier_export");
 }
 

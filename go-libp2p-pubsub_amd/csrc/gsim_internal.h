@@ -142,9 +142,10 @@ struct ShardCtx {
     uint32_t* d_ymap = nullptr;            // [e] ghost-row edge: the owner shard's owned-row edge index
     uint32_t* d_xgather = nullptr;         // [n_cross] cross-out lists (local edge indices)
     uint8_t* d_pgate = nullptr;            // [e] ghost-row edge: the sender's score of the receiver >= publishThreshold
+    uint64_t* d_xmask = nullptr;           // [n] owned peer: bit q = a connection into shard q's peers
     // frontier exchange (gsim_group_msgs_init)
-    uint64_t* d_fout = nullptr;            // owned forwarders of the round (k_frontier_export)
-    uint32_t* d_fcnt = nullptr;
+    uint64_t* d_fout = nullptr;            // [K][fcap] owned forwarders of the round per shard (k_frontier_export)
+    uint32_t* d_fcnt = nullptr;            // [K]
     int64_t fcap = 0;
     uint64_t* d_fin = nullptr;             // every other shard's forwarders
     int64_t fin_cap = 0;

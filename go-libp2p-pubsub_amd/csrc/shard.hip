@@ -53,35 +53,55 @@ struct PeerRanges {
 
 // GRAFT/PRUNE records written into ghost receivers' inboxes (plane `ctl`,
 // summary `cany`), one thread per ghost peer with a summary bit: entries
-// (owner shard's edge | topic << 32 | bits << 40) to the ghost's shard.
+// (owner shard's edge | topic << 32 | bits << 40) to the ghost's shard.  A
+// block counts its entries per shard in LDS and reserves each shard's range
+// with one atomic.
 __global__ __launch_bounds__(256) void k_ctl_export(uint8_t* ctl, uint64_t* cany, const uint32_t* row_ptr,
                                                     const uint32_t* ymap, PeerRanges pr, int64_t E, int32_t T,
                                                     int64_t olo, int64_t ohi, int64_t n, uint64_t* out,
                                                     uint32_t* cnt, int64_t cap)
 {
+    __shared__ uint32_t s_cnt[GSIM_MAX_SHARDS], s_base[GSIM_MAX_SHARDS];
     // a summary word may be a superset (all ones after an ABI write of the inbox)
     const uint64_t tmask = T >= 64 ? ~0ull : ((1ull << T) - 1);
     const int64_t nghost = olo + (n - ohi);
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < nghost; x += stride) {
-        const int64_t g = x < olo ? x : ohi + (x - olo);
-        uint64_t any = cany[g] & tmask;
-        if (cany[g]) cany[g] = 0;
-        if (!any) continue;
-        uint32_t d = 0;
-        while ((int32_t)d + 1 < pr.K && g >= pr.lo[d + 1]) ++d;
-        for (; any; any &= any - 1) {
-            const int32_t t = __ffsll((long long)any) - 1;
-            for (uint32_t e = row_ptr[g]; e < row_ptr[g + 1]; ++e) {
-                const int64_t i = (int64_t)t * E + e;
-                const uint8_t c = ctl[i];
-                if (!c) continue;
-                ctl[i] = 0;
-                const uint32_t pos = atomicAdd(&cnt[d], 1u);
-                if ((int64_t)pos < cap)
-                    out[(int64_t)d * cap + pos] = (uint64_t)ymap[e] | ((uint64_t)t << 32) | ((uint64_t)c << 40);
+    const int tid = threadIdx.x;
+    for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < nghost; b0 += (int64_t)gridDim.x * 256) {   // block-uniform
+        for (int q = tid; q < pr.K; q += 256) s_cnt[q] = 0;
+        __syncthreads();
+        const int64_t x = b0 + tid;
+        int64_t g = -1;
+        uint64_t any = 0;
+        uint32_t d = 0, mine = 0, off = 0;
+        if (x < nghost) {
+            g = x < olo ? x : ohi + (x - olo);
+            any = cany[g] & tmask;
+            if (cany[g]) cany[g] = 0;
+            while ((int32_t)d + 1 < pr.K && g >= pr.lo[d + 1]) ++d;
+            for (uint64_t r = any; r; r &= r - 1) {
+                const int32_t t = __ffsll((long long)r) - 1;
+                for (uint32_t e = row_ptr[g]; e < row_ptr[g + 1]; ++e) mine += ctl[(int64_t)t * E + e] != 0;
+            }
+            if (mine) off = atomicAdd(&s_cnt[d], mine);
+        }
+        __syncthreads();
+        for (int q = tid; q < pr.K; q += 256) s_base[q] = s_cnt[q] ? atomicAdd(cnt + q, s_cnt[q]) : 0u;
+        __syncthreads();
+        if (mine) {
+            int64_t pos = (int64_t)s_base[d] + off;
+            for (uint64_t r = any; r; r &= r - 1) {
+                const int32_t t = __ffsll((long long)r) - 1;
+                for (uint32_t e = row_ptr[g]; e < row_ptr[g + 1]; ++e) {
+                    const int64_t i = (int64_t)t * E + e;
+                    const uint8_t c = ctl[i];
+                    if (!c) continue;
+                    ctl[i] = 0;
+                    if (pos < cap) out[(int64_t)d * cap + pos] = (uint64_t)ymap[e] | ((uint64_t)t << 32) | ((uint64_t)c << 40);
+                    ++pos;
+                }
             }
         }
+        __syncthreads();
     }
 }
 
@@ -424,17 +444,25 @@ int dalloc(gsim_handle* h, T** p, size_t n)
     return GSIM_OK;
 }
 
-void free_shard_ctx(gsim_handle* h)
+void free_shard_bufs(ShardCtx* s)
 {
-    ShardCtx* s = h->sh;
-    if (!s) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(s->d_gid); f(s->d_g2l); f(s->d_ymap); f(s->d_xgather); f(s->d_pgate);
+    f(s->d_gid); f(s->d_g2l); f(s->d_xmask); f(s->d_ymap); f(s->d_xgather); f(s->d_pgate);
     f(s->d_fout); f(s->d_fcnt); f(s->d_fin); f(s->d_cout); f(s->d_ccnt); f(s->d_cin);
     f(s->d_rmesh_out); f(s->d_rfan_out); f(s->d_rflag_out); f(s->d_rmesh_in); f(s->d_rfan_in); f(s->d_rflag_in);
     f(s->d_gout); f(s->d_gsout); f(s->d_gin); f(s->d_gsin);
     if (s->h_counts) (void)hipHostFree(s->h_counts);
-    delete s;
+    ShardCtx fresh;
+    fresh.k = s->k;
+    fresh.K = s->K;
+    *s = fresh;
+}
+
+void free_shard_ctx(gsim_handle* h)
+{
+    if (!h->sh) return;
+    free_shard_bufs(h->sh);
+    delete h->sh;
     h->sh = nullptr;
 }
 
@@ -631,8 +659,8 @@ int exchange_router(gsim_group* g)
     return GSIM_OK;
 }
 
-// Round `round`'s forwarders: every shard's owned ones to every other shard,
-// which imports its ghosts among them.
+// Round `round`'s forwarders: every shard's owned ones to the shards they
+// have connections into, which import them into their ghosts.
 int exchange_frontier(gsim_group* g, int64_t round)
 {
     const size_t L = g->hs.size();
@@ -642,14 +670,25 @@ int exchange_frontier(gsim_group* g, int64_t round)
         gsim_handle* h = g->hs[l];
         ShardCtx* s = h->sh;
         (void)hipSetDevice(h->device);
-        int rc = g->take(h, deliver_frontier_export(h, round, s->d_fout, s->d_fcnt, s->fcap));
-        if (rc) return rc;
-        if (hipMemcpyAsync(s->h_counts, s->d_fcnt, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
-            hipStreamSynchronize(h->stream) != hipSuccess)
-            return g->fail(GSIM_EDEVICE, "frontier count");
-        if ((int64_t)s->h_counts[0] > s->fcap)
-            return g->fail(GSIM_ERANGE, "a round's forwarders overflowed the frontier buffer (raise gsim_msg_config.max_frontier)");
-        for (int d = 0; d < K; ++d) scnt[l][(size_t)d] = d == g->ids[l] ? 0 : s->h_counts[0];
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            int rc = g->take(h, deliver_frontier_export(h, round, s->d_fout, s->d_fcnt, s->fcap));
+            if (rc) return rc;
+            if (hipMemcpyAsync(s->h_counts, s->d_fcnt, sizeof(uint32_t) * K, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+                hipStreamSynchronize(h->stream) != hipSuccess)
+                return g->fail(GSIM_EDEVICE, "frontier counts");
+            int64_t need = 0;
+            for (int d = 0; d < K; ++d) need = std::max<int64_t>(need, s->h_counts[d]);
+            if (need <= s->fcap) break;
+            if (attempt) return g->fail(GSIM_ERANGE, "frontier export overflow");
+            // a busier round than any before: grow the lists and export again
+            // (the export only reads the round's state)
+            (void)hipFree(s->d_fout);
+            s->d_fout = nullptr;
+            s->fcap = need + need / 2;
+            rc = g->take(h, dalloc(h, &s->d_fout, (size_t)(s->fcap * K)));
+            if (rc) return rc;
+        }
+        for (int d = 0; d < K; ++d) scnt[l][(size_t)d] = d == g->ids[l] ? 0 : s->h_counts[d];
     }
     int rc = g->take_tr(g->tr->exchange_counts(scnt, rcnt));
     if (rc) return rc;
@@ -664,9 +703,12 @@ int exchange_frontier(gsim_group* g, int64_t round)
         (void)hipSetDevice(h->device);
         rc = g->take(h, ensure(h, &s->d_fin, &s->fin_cap, total[l]));
         if (rc) return rc;
+    }
+    for (size_t l = 0; l < L; ++l) {
+        ShardCtx* s = g->hs[l]->sh;
         int64_t off = 0;
         for (int q = 0; q < K; ++q) {
-            sp[l][(size_t)q] = s->d_fout;
+            sp[l][(size_t)q] = s->d_fout + (int64_t)q * s->fcap;
             sb[l][(size_t)q] = scnt[l][(size_t)q] * 8;
             rp[l][(size_t)q] = s->d_fin + off;
             rb[l][(size_t)q] = rcnt[l][(size_t)q] * 8;
@@ -836,6 +878,9 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
         int rc = build_layout(n, row_ptr, col, g->bounds.data(), K, g->ids[l], &L, &e);
         if (rc) return g->fail(rc, e);
         ShardCtx* s = h->sh;
+        (void)hipSetDevice(h->device);
+        (void)hipStreamSynchronize(h->stream);
+        free_shard_bufs(s);
         s->own_lo = L.own_lo; s->own_hi = L.own_hi; s->own_e_lo = L.own_e_lo; s->own_e_hi = L.own_e_hi;
         s->N_global = n; s->E_global = g->E;
         s->geid_base = L.own_e_hi > L.own_e_lo ? (int64_t)L.gidx[(size_t)L.own_e_lo] : 0;
@@ -866,8 +911,15 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
         for (int q = 0; q < K; ++q) xg.insert(xg.end(), L.crossout[(size_t)q].begin(), L.crossout[(size_t)q].end());
         std::vector<uint32_t> g2l((size_t)n, kNone);
         for (int64_t x = 0; x < L.n_loc; ++x) g2l[L.gid[(size_t)x]] = (uint32_t)x;
+        std::vector<uint64_t> xm((size_t)L.n_loc, 0);
+        for (int64_t x = L.own_lo; x < L.own_hi; ++x)
+            for (uint32_t e = L.row_ptr[(size_t)x]; e < L.row_ptr[(size_t)x + 1]; ++e) {
+                const int q = shard_of_peer(g->bounds, L.gid[L.col[e]]);
+                if (q != g->ids[l]) xm[(size_t)x] |= 1ull << q;
+            }
         const int64_t ncross = L.n_cross;
         if ((rc = dalloc(h, &s->d_gid, (size_t)L.n_loc)) || (rc = dalloc(h, &s->d_g2l, (size_t)n)) ||
+            (rc = dalloc(h, &s->d_xmask, (size_t)L.n_loc)) ||
             (rc = dalloc(h, &s->d_ymap, (size_t)L.e_loc)) || (rc = dalloc(h, &s->d_xgather, xg.size())) ||
             (rc = dalloc(h, &s->d_pgate, (size_t)L.e_loc)) ||
             (rc = dalloc(h, &s->d_rmesh_out, (size_t)ncross)) || (rc = dalloc(h, &s->d_rfan_out, (size_t)ncross)) ||
@@ -878,6 +930,7 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
             return g->fail(GSIM_ENOMEM, "pinned scratch");
         hipError_t he = hipMemcpy(s->d_gid, L.gid.data(), L.gid.size() * 4, hipMemcpyHostToDevice);
         if (he == hipSuccess) he = hipMemcpy(s->d_g2l, g2l.data(), g2l.size() * 4, hipMemcpyHostToDevice);
+        if (he == hipSuccess) he = hipMemcpy(s->d_xmask, xm.data(), xm.size() * 8, hipMemcpyHostToDevice);
         if (he == hipSuccess && !xg.empty()) he = hipMemcpy(s->d_xgather, xg.data(), xg.size() * 4, hipMemcpyHostToDevice);
         if (he == hipSuccess) he = hipMemset(s->d_ymap, 0xFF, (size_t)L.e_loc * 4);
         if (he == hipSuccess) he = hipMemset(s->d_pgate, 0, (size_t)L.e_loc);
@@ -909,16 +962,17 @@ int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg)
         const int K = g->K;
         int64_t gmax = 0;
         for (int q = 0; q < K; ++q) gmax = std::max<int64_t>(gmax, s->gcnt[(size_t)q]);
-        // a round's forwarders: each owned peer at most once per message it first
-        // saw in the round before; max_frontier overrides (entries per shard)
+        // a round's forwarders per destination shard: each owned peer once per
+        // message it first saw in the round before (grown on demand);
+        // max_frontier sets the initial size
         s->fcap = cfg->max_frontier > 0 ? cfg->max_frontier : std::max<int64_t>(8 * (s->own_hi - s->own_lo), 1 << 16);
         s->ccap = std::max<int64_t>(4 * gmax, 1 << 14);
         const int64_t ncross = s->xoff[(size_t)K];
         rc = GSIM_OK;
         auto A = [&](auto** p, size_t n) { if (!rc) rc = dalloc(h, p, n); };
         if (s->d_fout) { (void)hipFree(s->d_fout); s->d_fout = nullptr; }
-        A(&s->d_fout, (size_t)s->fcap);
-        if (!s->d_fcnt) A(&s->d_fcnt, 1);
+        A(&s->d_fout, (size_t)(s->fcap * K));
+        if (!s->d_fcnt) A(&s->d_fcnt, (size_t)K);
         if (!s->d_cout) {
             A(&s->d_cout, (size_t)(K * s->ccap));
             A(&s->d_ccnt, (size_t)K);

@@ -534,8 +534,9 @@ int gsim_group_set_peer_behaviour(gsim_group* g, const uint8_t* flags);
 int gsim_group_set_topic_params(gsim_group* g, int32_t topic, const gsim_topic_score_params* p);
 int gsim_group_set_seed(gsim_group* g, uint64_t seed);
 int gsim_group_fill_synthetic(gsim_group* g, uint64_t seed, int64_t now_ns, double p_mesh);
-/* max_frontier > 0 caps the forwarders one shard exports per round (default
- * max(8 x owned peers, 65536)); GSIM_ERANGE when a round exceeds it. */
+/* max_frontier > 0: the initial size of the per-shard forwarder lists
+ * (default max(8 x owned peers, 65536) entries; they grow when a round needs
+ * more). */
 int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg);
 int gsim_group_refresh_scores(gsim_group* g, int64_t now_ns);
 int gsim_group_heartbeat(gsim_group* g, uint64_t tick, int64_t now_ns);
