@@ -165,6 +165,8 @@ def build_engine(cfg, seed, device, scen=None, shard=None):
         eng.set_peer_behaviour(beh)
     if os.environ.get("GSIM_SEND_VARIANT") and shard is None:   # A/B of the delivery kernel (gsim.h)
         eng.set_kernel_variant(2, int(os.environ["GSIM_SEND_VARIANT"]))
+    if os.environ.get("GSIM_TM_WALK"):                           # topic-major walk: 1 per edge, 2 per row
+        eng.set_kernel_variant(4, int(os.environ["GSIM_TM_WALK"]))
     return eng, net
 
 
@@ -373,7 +375,12 @@ def main():
     eng.synchronize()
     barrier()
     wall = time.perf_counter() - t0
-    prof = eng.profile_read()
+    per_shard = None
+    if shard is not None and world == 1:          # in-process shards: each one's kernel time
+        per_shard = eng.profile_read_shards()
+        prof = {c: (sum(p[c][0] for p in per_shard), sum(p[c][1] for p in per_shard)) for c in per_shard[0]}
+    else:
+        prof = eng.profile_read()
     eng.profile(False)
     local_stats1 = eng.local_msg_stats() if sharded else None
     census1 = eng.census()
@@ -447,6 +454,9 @@ def main():
             "deliveries_per_tick": {"accepted": (stats1[0] - stats0[0]) / K, "first": (stats1[1] - stats0[1]) / K,
                                     "duplicate": (stats1[2] - stats0[2]) / K, "graylisted": (stats1[3] - stats0[3]) / K},
             "kernel_ms_per_tick": kms,
+            # in-process shards (GSIM_GROUP_SERIAL=1: each alone on the device): kernel ms per tick of each
+            "kernel_ms_per_tick_shards": (None if per_shard is None else
+                                          [round(sum(ms for ms, _ in p.values()) / K, 3) for p in per_shard]),
             "gossip_per_tick": {k: (gossip1[k] - gossip0[k]) / K for k in gossip1},
             "census": census1,
             "roofline": dominant,

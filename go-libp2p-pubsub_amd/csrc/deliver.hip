@@ -147,6 +147,9 @@ struct RoundArgs {
     uint32_t rlo, rhi;
     int32_t sharded;
     const uint8_t* pgate;          // sharded flood publish: a ghost origin's score of the receiver >= publishThreshold
+    // sharded: the edges of each row into owned peers (the copies this shard
+    // delivers), a CSR of edge indices: row x's are sedge[sptr[x] .. sptr[x+1])
+    const uint32_t *sptr, *sedge;
 };
 
 __device__ __forceinline__ int64_t round_time(const RoundArgs& a, int64_t g)
@@ -567,21 +570,29 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
 // records about its senders (record order: the senders' rows), per topic —
 // belong to this block alone; slots of one topic are walked one after the
 // other.  Results are identical to k_send's.
+//
+// The frontier of a chunk (its senders' fresh bits) is flattened into its
+// edges: a prefix sum of the senders' row lengths in LDS, one thread per
+// edge (binary search for the edge's sender), so rows of any length keep
+// every lane busy — a shard's short rows (owned rows cut to their owned
+// receivers, ghost rows) as much as power-law hubs.
 constexpr int kTmThreads = 1024;
-constexpr int kTmChunk = 2048;      // peers scanned per frontier chunk (two per thread)
+constexpr int kTmChunk = 2048;      // peers scanned per frontier chunk
 
-template <int W>
+template <int W>   // 0: one thread per edge; 16 / 32 / 64: W lanes per row
 __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t range)
 {
     // [nws] committed bits of the receivers' words, then [ring] u16 slots
     extern __shared__ uint64_t s_bm[];
     const int64_t wlo = (int64_t)a.rlo >> 6, nws = (((int64_t)a.rhi + 63) >> 6) - wlo;
     uint16_t* s_slots = reinterpret_cast<uint16_t*>(s_bm + nws);
-    __shared__ uint32_t s_front[kTmChunk];                   // frontier senders (their first sender in s_from)
-    __shared__ uint32_t s_from[kTmChunk];
-    __shared__ uint32_t s_beg[kTmChunk];                     // the sender's row
-    __shared__ uint16_t s_len[kTmChunk];
+    __shared__ uint32_t s_front[kTmChunk];                   // frontier senders
+    __shared__ uint32_t s_from[kTmChunk];                    // their first senders
+    __shared__ uint32_t s_off[kTmChunk];                     // first flattened edge of each sender
+    __shared__ uint32_t s_dlt[kTmChunk];                     // its row's first edge - s_off (mod 2^32)
+    __shared__ uint32_t s_wsum[64];                          // per-wave sums and their prefixes
     __shared__ int s_ns, s_nf, s_claimed;
+    __shared__ uint32_t s_ne;
     __shared__ unsigned long long s_stats[4];
     const int32_t t = (int32_t)blockIdx.y;
     // senders: the peers with cells, [clo, clo + CN)
@@ -600,8 +611,6 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
     }
     __syncthreads();
     const int ns = a.g > 0 && lo < pend_ ? s_ns : 0;
-    const int grp = lane / W, gl = lane % W;
-    constexpr int G = 64 / W;                                // row groups per wave
     const ctp_t tp = const_tp(a.tp) + t;
     const bool scored_t = tp->scored != 0;
     const int64_t window = tp->mesh_message_deliveries_window_ns;
@@ -630,51 +639,105 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
         // copy k_commit committed, the publication, a ghost's import), cleared
         // as they are read; only those peers' cells and rows are loaded
         uint64_t* fresh_m = a.fresh + (int64_t)m * a.nw;
-        constexpr int kWords = kTmChunk / 64;
         for (int64_t c0 = lo; c0 < hi; c0 += kTmChunk) {
-            if (tid == 0) s_nf = 0;
+            // thread tid: peers x0, x0 + 1 of the chunk (ranges start on whole
+            // words; 32 threads share a word)
+            const int64_t x0 = c0 + 2 * (int64_t)tid;
+            uint64_t word = 0;
+            uint32_t fb = 0;
+            if (x0 < hi) {
+                word = fresh_m[(x0 - clo) >> 6];
+                fb = (uint32_t)(word >> ((x0 - clo) & 63)) & (x0 + 1 < hi ? 3u : 1u);
+            }
+            uint32_t len2[2] = {0, 0}, beg2[2] = {0, 0}, from2[2] = {0, 0};
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                if ((fb >> u) & 1u) {
+                    const uint32_t x = (uint32_t)(x0 + u);
+                    from2[u] = (uint32_t)a.cell[row_m + (x - clo)] & kPeerMask;
+                    const uint32_t* rp = a.sptr ? a.sptr : a.row_ptr;
+                    beg2[u] = rp[x];
+                    len2[u] = rp[x + 1] - beg2[u];
+                }
+            }
+            // block scan of (forwarders, edges): the frontier in peer order
+            uint32_t vc = (uint32_t)__popc(fb), ve = len2[0] + len2[1];
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t yc = (uint32_t)__shfl_up((int)vc, o, 64), ye = (uint32_t)__shfl_up((int)ve, o, 64);
+                if (lane >= o) { vc += yc; ve += ye; }
+            }
+            if (lane == 63) { s_wsum[wid] = vc; s_wsum[16 + wid] = ve; }
             __syncthreads();
-            if (tid < kWords) {
-                const int64_t x0 = c0 + (int64_t)tid * 64;      // ranges start on whole words
-                uint64_t w = 0;
-                if (x0 < hi) {
-                    w = fresh_m[(x0 - clo) >> 6];
-                    if (w) fresh_m[(x0 - clo) >> 6] = 0;
-                    if (hi - x0 < 64) w &= (1ull << (hi - x0)) - 1;
+            if (tid < 64) {
+                const uint32_t c = tid < 16 ? s_wsum[tid] : 0u, e = tid < 16 ? s_wsum[16 + tid] : 0u;
+                uint32_t ic = c, ie = e;
+                for (int o = 1; o < 16; o <<= 1) {
+                    const uint32_t yc = (uint32_t)__shfl_up((int)ic, o, 64), ye = (uint32_t)__shfl_up((int)ie, o, 64);
+                    if (lane >= o) { ic += yc; ie += ye; }
                 }
-                if (w) {
-                    int q = atomicAdd(&s_nf, __popcll(w));
-                    for (; w; w &= w - 1) s_front[q++] = (uint32_t)(x0 + __ffsll((long long)w) - 1);
+                if (tid < 16) { s_wsum[32 + tid] = ic - c; s_wsum[48 + tid] = ie - e; }
+                if (tid == 15) { s_nf = (int)ic; s_ne = ie; }
+            }
+            __syncthreads();
+            {
+                uint32_t q = s_wsum[32 + wid] + vc - (uint32_t)__popc(fb);
+                uint32_t off = s_wsum[48 + wid] + ve - (len2[0] + len2[1]);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    if ((fb >> u) & 1u) {
+                        s_front[q] = (uint32_t)(x0 + u);
+                        s_from[q] = from2[u];
+                        if (W == 0) { s_off[q] = off; s_dlt[q] = beg2[u] - off; }
+                        else { s_off[q] = len2[u]; s_dlt[q] = beg2[u]; }
+                        ++q;
+                        off += len2[u];
+                    }
                 }
+                // the bits are read: clear them (one thread per nonzero word)
+                if (word && ((x0 - clo) & 63) == 0) fresh_m[(x0 - clo) >> 6] = 0;
             }
             __syncthreads();
             const int nf = s_nf;
-            for (int q = tid; q < nf; q += kTmThreads) {
-                const uint32_t x = s_front[q];
-                s_from[q] = (uint32_t)a.cell[row_m + (x - clo)] & kPeerMask;
-                const uint32_t rb = a.row_ptr[x];
-                s_beg[q] = rb;
-                s_len[q] = (uint16_t)(a.row_ptr[x + 1] - rb);
-            }
-            __syncthreads();
-            // each row group walks P frontier senders' rows at a time; the
-            // counters are loaded with the row state (one memory trip), the
-            // receiver's cell only when its committed bit is not decisive
+            const uint32_t ne = s_ne;
+            if (nf == 0) continue;                               // block-uniform
             constexpr int P = 2;
-            for (int q0 = wid * G * P; q0 < nf; q0 += (kTmThreads / 64) * G * P) {
+            constexpr int G = W ? 64 / W : 1;                    // row groups per wave
+            constexpr uint32_t kPerIt = W ? (kTmThreads / 64) * G * P : kTmThreads * P;
+            const uint32_t n_it = ((W ? (uint32_t)nf : ne) + kPerIt - 1) / kPerIt;
+            for (uint32_t it = 0; it < n_it; ++it) {
                 uint32_t jv[P], fv[P], ev[P], iv[P], nv[P];
                 uint8_t mfv[P], dsv[P], tfv[P];
                 bool vv[P];
                 double xv[P];
 #pragma unroll
                 for (int u = 0; u < P; ++u) {
-                    const int q = q0 + grp * P + u;
-                    const bool vq = q < nf;
-                    jv[u] = vq ? s_front[q] : 0u;
-                    fv[u] = vq ? s_from[q] : 0u;
-                    const uint32_t beg = vq ? s_beg[q] : 0u, len = vq ? s_len[q] : 0u;
-                    vv[u] = vq && (uint32_t)gl < len;
-                    ev[u] = beg + (uint32_t)gl;
+                    int q = 0;
+                    uint32_t fi = 0;
+                    if constexpr (W == 0) {
+                        // flat: one thread per edge; its sender is the last
+                        // whose first edge is <= fi
+                        fi = it * kPerIt + (uint32_t)(u * kTmThreads + tid);
+                        vv[u] = fi < ne;
+                        if (vv[u]) {
+                            int l = 0, r = nf;
+                            while (r - l > 1) {
+                                const int mid = (l + r) >> 1;
+                                if (s_off[mid] <= fi) l = mid; else r = mid;
+                            }
+                            q = l;
+                        }
+                    } else {
+                        // row groups: W lanes walk one sender's row (rows <= W)
+                        q = (int)(it * kPerIt) + (wid * G + lane / W) * P + u;
+                        const bool vq = q < nf;
+                        if (!vq) q = 0;
+                        vv[u] = vq && (uint32_t)(lane % W) < s_off[q];
+                        fi = (uint32_t)(lane % W);
+                    }
+                    jv[u] = vv[u] ? s_front[q] : 0u;
+                    fv[u] = vv[u] ? s_from[q] : 0u;
+                    ev[u] = fi + s_dlt[q];
+                    if (a.sedge && vv[u]) ev[u] = a.sedge[ev[u]];
                 }
 #pragma unroll
                 for (int u = 0; u < P; ++u) {
@@ -1331,6 +1394,8 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     if (ShardCtx* sh = h->sh) {
         a.sharded = 1;
         a.pgate = sh->d_pgate;
+        a.sptr = sh->d_sptr;
+        a.sedge = sh->d_sedge;
     }
     return a;
 }
@@ -1560,7 +1625,7 @@ static size_t send_tm_lds(const gsim_handle* h, const Deliver* d)
     const int64_t nws = ((h->ohi() + 63) >> 6) - (h->olo() >> 6);
     return (size_t)nws * 8 + (((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7);
 }
-constexpr size_t kLdsBudget = 160 * 1024 - 24 * 1024;   // minus the static frontier buffers
+constexpr size_t kLdsBudget = 160 * 1024 - 33 * 1024;   // minus the static frontier buffers
 
 template <int W>
 static void launch_send(gsim_handle* h, int grid, size_t lds, const RoundArgs& a)
@@ -1624,9 +1689,17 @@ int deliver_round_send(gsim_handle* h, int64_t round)
         const int grid = grid_peers(h->n);
         if (d->fresh_on) {
             const size_t lds_tm = send_tm_lds(h, d);
-            if (h->max_degree <= 16)
+            // W lanes per row while rows fill them (mean >= 3/4 of W), one
+            // thread per edge otherwise (short or skewed rows, a shard's rows)
+            const int64_t dmax = h->sh ? h->sh->send_max : h->max_degree;
+            const int64_t esend = h->sh ? h->sh->send_edges : h->e;
+            const int Wr = dmax <= 16 ? 16 : dmax <= 32 ? 32 : dmax <= 64 ? 64 : 0;
+            const bool flat = Wr == 0 || esend * 4 < (int64_t)Wr * 3 * std::max<int64_t>(1, h->n);
+            if (Wr == 0 || (h->send_variant_flat >= 0 ? h->send_variant_flat == 1 : flat))
+                rc = launch_send_tm<0>(h, a, lds_tm);
+            else if (Wr == 16)
                 rc = launch_send_tm<16>(h, a, lds_tm);
-            else if (h->max_degree <= 32)
+            else if (Wr == 32)
                 rc = launch_send_tm<32>(h, a, lds_tm);
             else
                 rc = launch_send_tm<64>(h, a, lds_tm);
@@ -1703,23 +1776,20 @@ void deliver_round_end(gsim_handle* h, int64_t round) { h->dl->next_round = roun
 // connections into the shard) and delivers those copies itself.
 constexpr uint64_t kG24 = 0xFFFFFFull;
 
-// Entries go only to the shards the forwarder has connections into (xmask:
-// bit q = a cross edge into shard q), one list of `cap` entries per shard.
-// One thread per (active slot, owned word); a block counts its entries per
-// shard in LDS, reserves each shard's range with one atomic, then writes.
-__global__ __launch_bounds__(256) void k_frontier_export(RoundArgs a, const uint32_t* gid, const uint64_t* xmask,
-                                                         uint64_t* out, uint32_t* cnt, int64_t cap, int32_t K)
+// One thread per (active slot, owned word); a block's entries are written
+// in item order (slot-major, ascending peers: the importers' cell and bitmap
+// writes coalesce) at a range reserved with one atomic.
+__global__ __launch_bounds__(256) void k_frontier_export(RoundArgs a, const uint32_t* gid, uint64_t* out, uint32_t* cnt,
+                                                         int64_t cap)
 {
     extern __shared__ uint16_t s_act[];
     __shared__ int s_n;
-    __shared__ uint32_t s_cnt[GSIM_MAX_SHARDS], s_base[GSIM_MAX_SHARDS];
+    __shared__ uint32_t s_wsum[4], s_base;
     const int nact = active_slots(a.nnew_prev, a.ring, s_act, &s_n);
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int64_t w0 = (int64_t)a.rlo >> 6, nwd = (((int64_t)a.rhi + 63) >> 6) - w0;
     const int64_t items = nwd * nact;
     for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < items; b0 += (int64_t)gridDim.x * 256) {   // block-uniform
-        for (int q = tid; q < K; q += 256) s_cnt[q] = 0;
-        __syncthreads();
         const int64_t x = b0 + tid;
         uint64_t bits = 0;
         uint32_t m = 0;
@@ -1732,51 +1802,79 @@ __global__ __launch_bounds__(256) void k_frontier_export(RoundArgs a, const uint
             if (w * 64 < (int64_t)a.rlo) bits &= ~0ull << ((int64_t)a.rlo - w * 64);        // owned peers only
             if (w * 64 + 64 > (int64_t)a.rhi) bits &= (1ull << ((int64_t)a.rhi - w * 64)) - 1;
         }
-        for (uint64_t b = bits; b; b &= b - 1) {
-            const int64_t i = w * 64 + __ffsll((long long)b) - 1;
-            for (uint64_t xm = xmask[i]; xm; xm &= xm - 1) atomicAdd(&s_cnt[__ffsll((long long)xm) - 1], 1u);
+        const uint32_t c = (uint32_t)__popcll(bits);
+        uint32_t v = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)v, o, 64);
+            if (lane >= o) v += y;
+        }
+        if (lane == 63) s_wsum[wid] = v;
+        __syncthreads();
+        if (tid == 0) {
+            const uint32_t tot = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+            s_wsum[3] = s_wsum[0] + s_wsum[1] + s_wsum[2];
+            s_wsum[2] = s_wsum[0] + s_wsum[1];
+            s_wsum[1] = s_wsum[0];
+            s_wsum[0] = 0;
+            s_base = tot ? atomicAdd(cnt, tot) : 0u;
         }
         __syncthreads();
-        for (int q = tid; q < K; q += 256) {
-            s_base[q] = s_cnt[q] ? atomicAdd(cnt + q, s_cnt[q]) : 0u;
-            s_cnt[q] = 0;
-        }
-        __syncthreads();
-        for (uint64_t b = bits; b; b &= b - 1) {
+        int64_t pos = (int64_t)s_base + s_wsum[wid] + (v - c);
+        for (uint64_t b = bits; b; b &= b - 1, ++pos) {
             const int64_t i = w * 64 + __ffsll((long long)b) - 1;
             const uint32_t f = (uint32_t)a.cell[(int64_t)m * a.CN + i] & kPeerMask;
             const uint64_t gf = f < a.N ? (uint64_t)gid[f] : kG24;
-            const uint64_t v = (uint64_t)gid[i] | (gf << 24) | ((uint64_t)m << 48);
-            for (uint64_t xm = xmask[i]; xm; xm &= xm - 1) {
-                const int q = __ffsll((long long)xm) - 1;
-                const int64_t pos = (int64_t)s_base[q] + atomicAdd(&s_cnt[q], 1u);
-                if (pos < cap) out[(int64_t)q * cap + pos] = v;
-            }
+            if (pos < cap) out[pos] = (uint64_t)gid[i] | (gf << 24) | ((uint64_t)m << 48);
         }
         __syncthreads();
     }
 }
 
+// The ghosts among the other shards' forwarders.  Entries come in runs of
+// one slot and ascending peers: a wave ORs its fresh bits per word before
+// one atomic, and tests the slot's activity bits once per run.
 __global__ __launch_bounds__(256) void k_frontier_import(RoundArgs a, const uint32_t* g2l, const uint64_t* in,
                                                          int64_t n)
 {
+    const int lane = threadIdx.x & 63;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += stride) {
-        const uint64_t v = in[x];
-        const uint32_t l = g2l[v & kG24];
-        if (l == 0xFFFFFFFFu || (l >= a.rlo && l < a.rhi)) continue;      // not a ghost of this shard
-        const uint64_t gf = (v >> 24) & kG24;
-        uint32_t f = gf == kG24 ? 0xFFFFFFFFu : g2l[gf];
-        if (f == 0xFFFFFFFFu) f = kPeerMask;                                 // not a local peer
-        const uint32_t m = (uint32_t)(v >> 48);
-        a.cell[(int64_t)m * a.CN + l] = ((uint64_t)(uint32_t)(a.g - 1) << 32) | f;
-        atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (l >> 6)), 1ull << (l & 63));
-        // many entries share a slot: test before the atomic (one 0 -> 1 transition)
-        uint32_t* nw = const_cast<uint32_t*>(a.nnew_prev) + (m >> 5);
-        if (!((__hip_atomic_load(nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (m & 31)) & 1u))
-            atomicOr(nw, 1u << (m & 31));
-        if (__hip_atomic_load(&a.slot_last[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int32_t)(a.g - 1))
-            atomicMax(&a.slot_last[m], (int32_t)(a.g - 1));
+    for (int64_t b0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); b0 < n; b0 += stride) {   // wave-uniform
+        const int64_t x = b0 + lane;
+        bool ghost = false;
+        uint32_t l = 0, m = 0;
+        if (x < n) {
+            const uint64_t v = in[x];
+            l = g2l[v & kG24];
+            ghost = l != 0xFFFFFFFFu && !(l >= a.rlo && l < a.rhi);         // a ghost of this shard
+            if (ghost) {
+                const uint64_t gf = (v >> 24) & kG24;
+                uint32_t f = gf == kG24 ? 0xFFFFFFFFu : g2l[gf];
+                if (f == 0xFFFFFFFFu) f = kPeerMask;                         // not a local peer
+                m = (uint32_t)(v >> 48);
+                a.cell[(int64_t)m * a.CN + l] = ((uint64_t)(uint32_t)(a.g - 1) << 32) | f;
+            }
+        }
+        // fresh bits: one atomic per distinct (slot, word) of the wave
+        const uint64_t key = ghost ? (uint64_t)m * (uint64_t)a.nw + (l >> 6) : ~0ull;
+        uint64_t pending = __ballot(ghost);
+        while (pending) {
+            const int leader = __ffsll((long long)pending) - 1;
+            const uint64_t k0 = (uint64_t)__shfl((long long)key, leader, 64);
+            const bool same = ghost && key == k0;
+            uint64_t bit = same ? 1ull << (l & 63) : 0ull;
+            for (int o = 32; o; o >>= 1) bit |= (uint64_t)__shfl_xor((long long)bit, o, 64);
+            if (lane == leader) {
+                atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + k0), bit);
+                // the slot's activity (one 0 -> 1 transition per round)
+                const uint32_t ms = (uint32_t)(k0 / (uint64_t)a.nw);
+                uint32_t* nw = const_cast<uint32_t*>(a.nnew_prev) + (ms >> 5);
+                if (!((__hip_atomic_load(nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (ms & 31)) & 1u))
+                    atomicOr(nw, 1u << (ms & 31));
+                if (__hip_atomic_load(&a.slot_last[ms], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int32_t)(a.g - 1))
+                    atomicMax(&a.slot_last[ms], (int32_t)(a.g - 1));
+            }
+            pending &= ~__ballot(same);
+        }
     }
 }
 
@@ -1784,14 +1882,14 @@ int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32
 {
     Deliver* d = h->dl;
     RoundArgs a = make_round_args(h, round);
-    hipError_t e = hipMemsetAsync(d_cnt, 0, sizeof(uint32_t) * (size_t)h->sh->K, h->stream);
+    hipError_t e = hipMemsetAsync(d_cnt, 0, sizeof(uint32_t), h->stream);
     if (e != hipSuccess) return hip_check(h, e, "frontier count");
     if (round == 0) return GSIM_OK;
     const int64_t words = ((h->ohi() + 63) >> 6) - (h->olo() >> 6);
     const int64_t items = words * (int64_t)d->cfg.ring;      // an upper bound: the active slots are on the device
     hipLaunchKernelGGL(k_frontier_export, dim3((uint32_t)std::max<int64_t>(1, std::min<int64_t>((items + 255) / 256, 2048))),
                        dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a, (const uint32_t*)h->sh->d_gid,
-                       (const uint64_t*)h->sh->d_xmask, out, d_cnt, cap, (int32_t)h->sh->K);
+                       out, d_cnt, cap);
     return hip_check(h, hipGetLastError(), "k_frontier_export");
 }
 

@@ -1065,6 +1065,11 @@ int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant)
         h->ihave_w = variant;
         return GSIM_OK;
     }
+    if (which == 4) {           // topic-major walk: 0 = by row lengths, 1 = one thread per edge, 2 = lanes per row
+        if (variant < 0 || variant > 2) { h->err = "unknown topic-major walk (0, 1 or 2)"; return GSIM_EINVAL; }
+        h->send_variant_flat = variant == 0 ? -1 : variant == 1 ? 1 : 0;
+        return GSIM_OK;
+    }
     h->err = "unknown kernel variant class";
     return GSIM_EINVAL;
 }

@@ -142,10 +142,13 @@ struct ShardCtx {
     uint32_t* d_ymap = nullptr;            // [e] ghost-row edge: the owner shard's owned-row edge index
     uint32_t* d_xgather = nullptr;         // [n_cross] cross-out lists (local edge indices)
     uint8_t* d_pgate = nullptr;            // [e] ghost-row edge: the sender's score of the receiver >= publishThreshold
-    uint64_t* d_xmask = nullptr;           // [n] owned peer: bit q = a connection into shard q's peers
+    int64_t send_edges = 0, send_max = 0;  // edges into owned peers, longest such run of a row
+    uint32_t* d_sptr = nullptr;            // [n+1] CSR of each row's edges into owned peers (the copies this shard delivers)
+    uint32_t* d_sedge = nullptr;           // their local edge indices, in row order
+    std::vector<uint8_t> xto;              // [K] the owned peers have connections into shard q's
     // frontier exchange (gsim_group_msgs_init)
-    uint64_t* d_fout = nullptr;            // [K][fcap] owned forwarders of the round per shard (k_frontier_export)
-    uint32_t* d_fcnt = nullptr;            // [K]
+    uint64_t* d_fout = nullptr;            // owned forwarders of the round (k_frontier_export)
+    uint32_t* d_fcnt = nullptr;
     int64_t fcap = 0;
     uint64_t* d_fin = nullptr;             // every other shard's forwarders
     int64_t fin_cap = 0;
@@ -199,6 +202,7 @@ struct gsim_handle {
     bool all_joined = false;     // every peer announced every topic (nothing to skip)
     int send_variant = 3;     // delivery kernel variant (gsim_set_kernel_variant(h, 2, v)); 3 = topic-major
     int ihave_w = 0;          // k_ihave lane group width (gsim_set_kernel_variant(h, 3, w)); 0 = by row lengths
+    int send_variant_flat = -1;   // k_send_tm walk (gsim_set_kernel_variant(h, 4, v)): -1 by row lengths, 1 per edge, 0 per row
 
     // device: parameters and scratch flags
     gsim_topic_score_params* d_tp = nullptr;

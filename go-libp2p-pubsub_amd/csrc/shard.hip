@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -414,6 +415,15 @@ struct gsim_group {
     int32_t ring = 0, rounds = 0;
     bool msgs = false;
     bool router_dirty = true;                 // ghost rows' router state must be re-imported
+    // GSIM_GROUP_SERIAL=1: each shard's work completes before the next
+    // shard's starts (in-process groups on one device: per-shard kernel
+    // times as if each shard had the device to itself)
+    bool serial = false;
+
+    void settle(gsim_handle* h)
+    {
+        if (serial) (void)hipStreamSynchronize(h->stream);
+    }
 
     int fail(int rc, const std::string& m)
     {
@@ -447,7 +457,7 @@ int dalloc(gsim_handle* h, T** p, size_t n)
 void free_shard_bufs(ShardCtx* s)
 {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(s->d_gid); f(s->d_g2l); f(s->d_xmask); f(s->d_ymap); f(s->d_xgather); f(s->d_pgate);
+    f(s->d_gid); f(s->d_g2l); f(s->d_sptr); f(s->d_sedge); f(s->d_ymap); f(s->d_xgather); f(s->d_pgate);
     f(s->d_fout); f(s->d_fcnt); f(s->d_fin); f(s->d_cout); f(s->d_ccnt); f(s->d_cin);
     f(s->d_rmesh_out); f(s->d_rfan_out); f(s->d_rflag_out); f(s->d_rmesh_in); f(s->d_rfan_in); f(s->d_rflag_in);
     f(s->d_gout); f(s->d_gsout); f(s->d_gin); f(s->d_gsin);
@@ -659,8 +669,8 @@ int exchange_router(gsim_group* g)
     return GSIM_OK;
 }
 
-// Round `round`'s forwarders: every shard's owned ones to the shards they
-// have connections into, which import them into their ghosts.
+// Round `round`'s forwarders: every shard's owned ones (one list) to every
+// shard they have connections into, which imports its ghosts among them.
 int exchange_frontier(gsim_group* g, int64_t round)
 {
     const size_t L = g->hs.size();
@@ -673,22 +683,22 @@ int exchange_frontier(gsim_group* g, int64_t round)
         for (int attempt = 0; attempt < 2; ++attempt) {
             int rc = g->take(h, deliver_frontier_export(h, round, s->d_fout, s->d_fcnt, s->fcap));
             if (rc) return rc;
-            if (hipMemcpyAsync(s->h_counts, s->d_fcnt, sizeof(uint32_t) * K, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+            if (hipMemcpyAsync(s->h_counts, s->d_fcnt, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
                 hipStreamSynchronize(h->stream) != hipSuccess)
-                return g->fail(GSIM_EDEVICE, "frontier counts");
-            int64_t need = 0;
-            for (int d = 0; d < K; ++d) need = std::max<int64_t>(need, s->h_counts[d]);
+                return g->fail(GSIM_EDEVICE, "frontier count");
+            const int64_t need = s->h_counts[0];
             if (need <= s->fcap) break;
             if (attempt) return g->fail(GSIM_ERANGE, "frontier export overflow");
-            // a busier round than any before: grow the lists and export again
+            // a busier round than any before: grow the list and export again
             // (the export only reads the round's state)
             (void)hipFree(s->d_fout);
             s->d_fout = nullptr;
             s->fcap = need + need / 2;
-            rc = g->take(h, dalloc(h, &s->d_fout, (size_t)(s->fcap * K)));
+            rc = g->take(h, dalloc(h, &s->d_fout, (size_t)s->fcap));
             if (rc) return rc;
         }
-        for (int d = 0; d < K; ++d) scnt[l][(size_t)d] = d == g->ids[l] ? 0 : s->h_counts[d];
+        for (int d = 0; d < K; ++d)
+            scnt[l][(size_t)d] = (d == g->ids[l] || !s->xto[(size_t)d]) ? 0 : s->h_counts[0];
     }
     int rc = g->take_tr(g->tr->exchange_counts(scnt, rcnt));
     if (rc) return rc;
@@ -708,7 +718,7 @@ int exchange_frontier(gsim_group* g, int64_t round)
         ShardCtx* s = g->hs[l]->sh;
         int64_t off = 0;
         for (int q = 0; q < K; ++q) {
-            sp[l][(size_t)q] = s->d_fout + (int64_t)q * s->fcap;
+            sp[l][(size_t)q] = s->d_fout;
             sb[l][(size_t)q] = scnt[l][(size_t)q] * 8;
             rp[l][(size_t)q] = s->d_fin + off;
             rb[l][(size_t)q] = rcnt[l][(size_t)q] * 8;
@@ -734,6 +744,8 @@ int group_create(const gsim_peer_score_params* params, const gsim_topic_score_pa
 {
     gsim_group* g = new gsim_group();
     g->K = shards;
+    const char* ser = std::getenv("GSIM_GROUP_SERIAL");
+    g->serial = ser && ser[0] == '1';
     for (const auto& sd : local) {
         gsim_handle* h = nullptr;
         const int rc = gsim_create(params, topics, n_topics, th, gp, sd.second, &h, err, errlen);
@@ -911,15 +923,23 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
         for (int q = 0; q < K; ++q) xg.insert(xg.end(), L.crossout[(size_t)q].begin(), L.crossout[(size_t)q].end());
         std::vector<uint32_t> g2l((size_t)n, kNone);
         for (int64_t x = 0; x < L.n_loc; ++x) g2l[L.gid[(size_t)x]] = (uint32_t)x;
-        std::vector<uint64_t> xm((size_t)L.n_loc, 0);
-        for (int64_t x = L.own_lo; x < L.own_hi; ++x)
-            for (uint32_t e = L.row_ptr[(size_t)x]; e < L.row_ptr[(size_t)x + 1]; ++e) {
-                const int q = shard_of_peer(g->bounds, L.gid[L.col[e]]);
-                if (q != g->ids[l]) xm[(size_t)x] |= 1ull << q;
-            }
+        // the edges of each row into owned peers, in row order: the copies
+        // this shard delivers (ghost rows: all of them)
+        std::vector<uint32_t> sptr((size_t)L.n_loc + 1, 0), sedge;
+        sedge.reserve((size_t)L.e_loc);
+        for (int64_t x = 0; x < L.n_loc; ++x) {
+            for (uint32_t q = L.row_ptr[(size_t)x]; q < L.row_ptr[(size_t)x + 1]; ++q)
+                if ((int64_t)L.col[q] >= L.own_lo && (int64_t)L.col[q] < L.own_hi) sedge.push_back(q);
+            sptr[(size_t)x + 1] = (uint32_t)sedge.size();
+            s->send_max = std::max<int64_t>(s->send_max, sptr[(size_t)x + 1] - sptr[(size_t)x]);
+        }
+        s->send_edges = (int64_t)sedge.size();
+        s->xto.assign((size_t)K, 0);
+        for (int q = 0; q < K; ++q) s->xto[(size_t)q] = L.crossout[(size_t)q].empty() ? 0 : 1;
         const int64_t ncross = L.n_cross;
         if ((rc = dalloc(h, &s->d_gid, (size_t)L.n_loc)) || (rc = dalloc(h, &s->d_g2l, (size_t)n)) ||
-            (rc = dalloc(h, &s->d_xmask, (size_t)L.n_loc)) ||
+            (rc = dalloc(h, &s->d_sptr, sptr.size())) ||
+            (rc = dalloc(h, &s->d_sedge, sedge.size())) ||
             (rc = dalloc(h, &s->d_ymap, (size_t)L.e_loc)) || (rc = dalloc(h, &s->d_xgather, xg.size())) ||
             (rc = dalloc(h, &s->d_pgate, (size_t)L.e_loc)) ||
             (rc = dalloc(h, &s->d_rmesh_out, (size_t)ncross)) || (rc = dalloc(h, &s->d_rfan_out, (size_t)ncross)) ||
@@ -930,7 +950,9 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
             return g->fail(GSIM_ENOMEM, "pinned scratch");
         hipError_t he = hipMemcpy(s->d_gid, L.gid.data(), L.gid.size() * 4, hipMemcpyHostToDevice);
         if (he == hipSuccess) he = hipMemcpy(s->d_g2l, g2l.data(), g2l.size() * 4, hipMemcpyHostToDevice);
-        if (he == hipSuccess) he = hipMemcpy(s->d_xmask, xm.data(), xm.size() * 8, hipMemcpyHostToDevice);
+        if (he == hipSuccess) he = hipMemcpy(s->d_sptr, sptr.data(), sptr.size() * 4, hipMemcpyHostToDevice);
+        if (he == hipSuccess && !sedge.empty())
+            he = hipMemcpy(s->d_sedge, sedge.data(), sedge.size() * 4, hipMemcpyHostToDevice);
         if (he == hipSuccess && !xg.empty()) he = hipMemcpy(s->d_xgather, xg.data(), xg.size() * 4, hipMemcpyHostToDevice);
         if (he == hipSuccess) he = hipMemset(s->d_ymap, 0xFF, (size_t)L.e_loc * 4);
         if (he == hipSuccess) he = hipMemset(s->d_pgate, 0, (size_t)L.e_loc);
@@ -971,8 +993,8 @@ int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg)
         rc = GSIM_OK;
         auto A = [&](auto** p, size_t n) { if (!rc) rc = dalloc(h, p, n); };
         if (s->d_fout) { (void)hipFree(s->d_fout); s->d_fout = nullptr; }
-        A(&s->d_fout, (size_t)(s->fcap * K));
-        if (!s->d_fcnt) A(&s->d_fcnt, (size_t)K);
+        A(&s->d_fout, (size_t)s->fcap);
+        if (!s->d_fcnt) A(&s->d_fcnt, 1);
         if (!s->d_cout) {
             A(&s->d_cout, (size_t)(K * s->ccap));
             A(&s->d_ccnt, (size_t)K);
@@ -997,6 +1019,7 @@ int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg)
         for (gsim_handle* h : (g)->hs) {                         \
             int rc_ = (call);                                    \
             if (rc_) return (g)->take(h, rc_);                   \
+            (g)->settle(h);                                      \
         }                                                        \
     } while (0)
 
@@ -1127,6 +1150,7 @@ int gsim_group_round(gsim_group* g, int64_t round)
         (void)hipSetDevice(h->device);
         rc = deliver_round_prepare(h, round);        // commits of the last round: fresh forwarders
         if (rc) return g->take(h, rc);
+        g->settle(h);
     }
     rc = exchange_frontier(g, round);                // the ghosts among them
     if (rc) return rc;
@@ -1136,6 +1160,7 @@ int gsim_group_round(gsim_group* g, int64_t round)
         if (!rc) rc = deliver_round_post(h, round);
         if (!rc) rc = deliver_round_control(h, round);
         if (rc) return g->take(h, rc);
+        g->settle(h);
     }
     const int64_t r = round % g->rounds;
     if (r < 2) {
@@ -1147,6 +1172,7 @@ int gsim_group_round(gsim_group* g, int64_t round)
         (void)hipSetDevice(h->device);
         rc = deliver_round_ihave(h, round);             // ghost advertisers: their cells
         if (rc) return g->take(h, rc);
+        g->settle(h);
         deliver_round_end(h, round);
     }
     return GSIM_OK;

@@ -240,6 +240,14 @@ class ShardedEngine:
         self._check(self.lib.gsim_group_set_topic_params(self.g, self.topic_index[topic], ctypes.byref(c)))
         self.params.Topics[topic] = p
 
+    def set_kernel_variant(self, which: int, variant: int):
+        """gsim_set_kernel_variant on every shard of this process."""
+        for s in self.local:
+            h = self._shard_handle(s)
+            rc = self.lib.gsim_set_kernel_variant(h, int(which), int(variant))
+            if rc != 0:
+                raise GsimError(rc, (self.lib.gsim_last_error(h) or b"").decode())
+
     def set_seed(self, seed: int):
         self._check(self.lib.gsim_group_set_seed(self.g, int(seed)))
 
@@ -325,6 +333,20 @@ class ShardedEngine:
         cnt = np.zeros(n, dtype=np.int64)
         self._check(self.lib.gsim_group_profile_read(self.g, _ptr(ms), _ptr(cnt), n))
         return {c: (float(ms[i]), int(cnt[i])) for i, c in enumerate(_abi.KERNEL_CLASSES)}
+
+    def profile_read_shards(self) -> list:
+        """profile_read of each shard of this process (list in shard order)."""
+        n = len(_abi.KERNEL_CLASSES)
+        res = []
+        for s in self.local:
+            ms = np.zeros(n, dtype=np.float64)
+            cnt = np.zeros(n, dtype=np.int64)
+            h = self._shard_handle(s)
+            rc = self.lib.gsim_profile_read(h, _ptr(ms), _ptr(cnt), n)
+            if rc != 0:
+                raise GsimError(rc, (self.lib.gsim_last_error(h) or b"").decode())
+            res.append({c: (float(ms[i]), int(cnt[i])) for i, c in enumerate(_abi.KERNEL_CLASSES)})
+        return res
 
     # -- state in the whole network's view (this process's shards) --------------------
     _PEER_LAST = {_abi.F_SEEN, _abi.F_LASTPUT}          # [..., N]

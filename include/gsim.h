@@ -439,7 +439,10 @@ int gsim_profile_read(gsim_handle* h, double* ms, int64_t* launches, int32_t n);
  * each).  which = 2: the delivery kernel; variant 3 (default) is topic-major
  * with the slots' committed bits staged in LDS (used while they fit), 0 is
  * the peer-major k_send.  which = 3: the IHAVE walk's lane group width
- * (16, 32 or 64 lanes per row; 0 = chosen from the row lengths). */
+ * (16, 32 or 64 lanes per row; 0 = chosen from the row lengths).  which = 4:
+ * the topic-major walk over a round's forwarders: 1 = one thread per edge
+ * (rows flattened), 2 = a lane group per row, 0 (default) = chosen from the
+ * row lengths. */
 int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant);
 
 /* ---- synthetic inputs -------------------------------- */
