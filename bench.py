@@ -216,58 +216,75 @@ def run_tick(eng, k, sched, churn=None):
         eng.round(g)
 
 
-def cpu_baseline(cfg, budget_s: float = 15.0, scen=None):
-    """Time the C oracle (OpenMP over observers in the heartbeat phases) on a
-    bounded sample of the same workload: same graph model, degree, topics,
-    parameters, adversaries, churn and message rate, 50k peers."""
+def cpu_baseline(cfg, scen=None, n: int = 10_000, ticks: int = 5, budget_s: float = 25.0):
+    """Time the C oracle on a bounded sample of the same workload (same graph
+    model, degree, topics, parameters, adversaries, churn and message rate,
+    `n` peers): one warm-up tick, then `ticks` ticks timed one by one, the
+    median reported — once on one core and once with OpenMP over the host's
+    threads in the parallel phases (refresh/score, heartbeat, control)."""
     import oracle_binding as ob
     from fixtures import beacon_params, beacon_thresholds, synthetic_state
     from tickrun import restrict_to_subscriptions
     import gsim
     scen = scen or {}
-    n, k, T, D, Dlo, Dhi = 50_000, cfg[1], cfg[2], cfg[3], cfg[4], cfg[5]
+    k, T, D, Dlo, Dhi = cfg[1], cfg[2], cfg[3], cfg[4], cfg[5]
     net, beh = build_network((n,) + tuple(cfg[1:]), 2, scen)
     params = beacon_params(T)
     gp = gsim.GossipSubParams(D=D, Dlo=Dlo, Dhi=Dhi)
     if "opp_ticks" in scen:
         gp.OpportunisticGraftTicks = scen["opp_ticks"]
-    st = ob.NetState(net, params, thresholds=beacon_thresholds(), gossip=gp)
-    synthetic_state(st, np.random.default_rng(3), tick_time(0), D / k)   # gsim_fill_synthetic's distributions
-    if "zipf_per_peer" in scen:
-        restrict_to_subscriptions(st, net)
-    msgs = ob.Msgs(n, T, scen.get("ring", MSG_RING), ROUNDS, tick_time(0), SECOND, behaviour=beh)
     rate = scen.get("msg_rate", MSG_RATE)
-    sched = message_schedule(n, T, range(1, 201), sub=net.sub if "zipf_per_peer" in scen else None, rate=rate)
-    churn = churn_schedule(net, scen["churn_frac"], range(1, 201)) if "churn_frac" in scen else {}
     lib = ob.load()
-    v = st.view()
-    lib.orc_ip_colocation(v)
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    steps = 0
-    t0 = time.perf_counter()
-    while True:
-        kk = steps + 1
-        now = tick_time(kk)
-        for (pairs, up) in churn.get(kk, []):
-            st.churn(pairs, up=up, now=now - SECOND // 2)
-        lib.orc_refresh_scores(v, now)
-        msgs.penalties(st, now)
-        lib.orc_compute_scores(v)
-        msgs.heartbeat(st, kk, now, 0x5EED0001)
-        for g in range(kk * ROUNDS, (kk + 1) * ROUNDS):
-            for m in sched.get(g, []):
-                msgs.publish(st, int(m["id"]), int(m["topic"]), int(m["origin"]), 0, g)
-            msgs.round(st, g)
-        steps += 1
-        if time.perf_counter() - t0 > budget_s or steps >= 200:
-            break
-    el = time.perf_counter() - t0
-    return {"value": n * steps / el, "unit": "peer-heartbeat updates/sec", "cores": threads, "kind": "port",
-            "msg_edge_deliveries_per_sec": msgs.stats[0] / el,
+    all_threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+
+    def leg(threads: int):
+        got = lib.orc_set_threads(threads)
+        st = ob.NetState(net, params, thresholds=beacon_thresholds(), gossip=gp)
+        synthetic_state(st, np.random.default_rng(3), tick_time(0), D / k)   # gsim_fill_synthetic's distributions
+        if "zipf_per_peer" in scen:
+            restrict_to_subscriptions(st, net)
+        msgs = ob.Msgs(n, T, scen.get("ring", MSG_RING), ROUNDS, tick_time(0), SECOND, behaviour=beh)
+        sched = message_schedule(n, T, range(1, ticks + 2), sub=net.sub if "zipf_per_peer" in scen else None,
+                                 rate=rate)
+        churn = churn_schedule(net, scen["churn_frac"], range(1, ticks + 2)) if "churn_frac" in scen else {}
+        v = st.view()
+        lib.orc_ip_colocation(v)
+        times, deliv = [], []
+        t_leg = time.perf_counter()
+        for kk in range(1, ticks + 2):
+            now = tick_time(kk)
+            d0 = msgs.stats[0]
+            t0 = time.perf_counter()
+            for (pairs, up) in churn.get(kk, []):
+                st.churn(pairs, up=up, now=now - SECOND // 2)
+            lib.orc_refresh_scores(v, now)
+            msgs.penalties(st, now)
+            lib.orc_compute_scores(v)
+            msgs.heartbeat(st, kk, now, 0x5EED0001)
+            for g in range(kk * ROUNDS, (kk + 1) * ROUNDS):
+                for m in sched.get(g, []):
+                    msgs.publish(st, int(m["id"]), int(m["topic"]), int(m["origin"]), 0, g)
+                msgs.round(st, g)
+            if kk > 1:                                  # tick 1 warms up
+                times.append(time.perf_counter() - t0)
+                deliv.append(msgs.stats[0] - d0)
+            if time.perf_counter() - t_leg > budget_s and len(times) >= 1:
+                break
+        med = float(np.median(times))
+        return {"value": n / med, "cores": got, "ticks_timed": len(times), "median_tick_s": med,
+                "msg_edge_deliveries_per_sec": float(np.median(deliv)) / med}
+
+    one = leg(1)
+    allc = leg(all_threads)
+    lib.orc_set_threads(all_threads)
+    return {"value": allc["value"], "unit": "peer-heartbeat updates/sec", "cores": allc["cores"], "kind": "port",
+            "msg_edge_deliveries_per_sec": allc["msg_edge_deliveries_per_sec"],
+            "single_core": one, "all_core": allc,
             "sample": f"C oracle heartbeat tick (refreshScores+score, mesh maintenance, {ROUNDS} propagation "
                       f"rounds at {rate:g} msg/s/topic) on a {n}-peer {describe_graph(cfg, scen)}, T={T} "
-                      f"network, {steps} ticks, "
-                      f"OpenMP {threads} threads in the heartbeat phases, {el:.1f}s"}
+                      f"network; median of {one['ticks_timed']} (1 core) / {allc['ticks_timed']} "
+                      f"({allc['cores']} OpenMP threads in the refresh, score, heartbeat and control phases; "
+                      f"propagation rounds serial) ticks after a warm-up tick"}
 
 
 def job_totals(wall: float, deliveries: float, dist=None, device: str = "cpu"):

@@ -10,6 +10,9 @@
 
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define TF_IN_MESH GSIM_TF_IN_MESH
 #define TF_ACTIVE  GSIM_TF_ACTIVE
@@ -126,6 +129,19 @@ double orc_score_edge(const orc_net* s, int64_t e)
         score += p7 * pp->behaviour_penalty_weight;
     }
     return score;
+}
+
+/* OpenMP threads of the parallel phases (the CPU baseline's single-core and
+ * all-core legs); returns the number in effect (1 without OpenMP) */
+int orc_set_threads(int n)
+{
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+    return omp_get_max_threads();
+#else
+    (void)n;
+    return 1;
+#endif
 }
 
 void orc_compute_scores(orc_net* s)

@@ -122,6 +122,7 @@ int64_t orc_handle_control(orc_net* s, int32_t round, int64_t now);
 void   orc_refresh_scores(orc_net* s, int64_t now);              /* score.go:504-565 */
 double orc_score_edge(const orc_net* s, int64_t e);              /* score.go:265-342 */
 void   orc_compute_scores(orc_net* s);                           /* score() for every edge */
+int    orc_set_threads(int n);                                   /* OpenMP threads (n <= 0: query) */
 void   orc_ip_colocation(orc_net* s);                            /* score.go:344-388 */
 void   orc_add_penalty(orc_net* s, int64_t e, int32_t count);    /* score.go:391-405 */
 void   orc_graft(orc_net* s, int64_t e, int32_t topic, int64_t now); /* score.go:649-667 */

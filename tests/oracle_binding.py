@@ -59,6 +59,7 @@ def load():
             "orc_refresh_scores": (None, [P, c_int64]),
             "orc_score_edge": (c_double, [P, c_int64]),
             "orc_compute_scores": (None, [P]),
+            "orc_set_threads": (ctypes.c_int, [ctypes.c_int]),
             "orc_ip_colocation": (None, [P]),
             "orc_add_penalty": (None, [P, c_int64, c_int32]),
             "orc_graft": (None, [P, c_int64, c_int32, c_int64]),

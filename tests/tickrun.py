@@ -80,9 +80,11 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
         eng.close()
 
 
-def subscribed_schedule(rng, ticks, net, T, rate, inv_frac, member_only=True):
+def subscribed_schedule(rng, ticks, net, T, rate, inv_frac, member_only=True, verdicts=None):
     """Poisson(rate) publications per topic per tick at uniform rounds; the
-    origin is a uniform member of the topic (or any peer)."""
+    origin is a uniform member of the topic (or any peer).  The verdict is
+    reject with probability inv_frac, or drawn from `verdicts` (probabilities
+    of accept / reject / ignore / throttle / signature) when given."""
     sched, mid = {}, 0
     members = [np.nonzero((net.sub >> np.uint64(t)) & np.uint64(1))[0] for t in range(T)]
     for k in ticks:
@@ -92,7 +94,10 @@ def subscribed_schedule(rng, ticks, net, T, rate, inv_frac, member_only=True):
             for t in range(T):
                 pool = members[t] if member_only and len(members[t]) else np.arange(net.n)
                 for _ in range(rng.poisson(rate / R)):
-                    batch.append((mid, t, int(pool[rng.integers(0, len(pool))]), int(rng.random() < inv_frac)))
+                    o = int(pool[rng.integers(0, len(pool))])
+                    v = (int(rng.choice(len(verdicts), p=verdicts)) if verdicts is not None
+                         else int(rng.random() < inv_frac))
+                    batch.append((mid, t, o, v))
                     mid += 1
             if batch:
                 sched[g] = batch
