@@ -56,7 +56,7 @@ CONFIGS = {
 #  c4  Sybil/eclipse: 100k honest + 25k sybils (20 %), one IP per 50 sybils
 #      (P6), sybils ignore IWANT (broken promises -> P7), opportunistic
 #      grafting every 10 heartbeats so the timed window holds it.
-#  c5  Chung-Lu power law (exponent 2.5, mean 16, rows <= 64), 64 topics
+#  c5  Chung-Lu power law (exponent 2.5, mean 16, rows <= 4096: hubs of a few hundred), 64 topics
 #      with Zipf subscriptions (8 per peer), 1 % of connections going down
 #      per tick and coming back two ticks later, publishers are topic members,
 #      2 msg/s/topic (128 msg/s network-wide; at 4 msg/s/topic the 5000-slot
@@ -66,7 +66,7 @@ CONFIGS = {
 #      (~560 GB) do not fit one GPU's 288 GB.
 SCENARIOS = {
     "c4": {"sybil_frac": 0.2, "per_ip": 50, "opp_ticks": 10},
-    "c5": {"power_law": (2.5, 64), "zipf_per_peer": 8, "churn_frac": 0.01, "ring": 5000,
+    "c5": {"power_law": (2.5, 4096), "zipf_per_peer": 8, "churn_frac": 0.01, "ring": 5000,
            "msg_rate": 2.0},
 }
 

@@ -1658,8 +1658,9 @@ int deliver_round_prepare(gsim_handle* h, int64_t round)
         h->err = "rounds must be consecutive";
         return GSIM_ESTATE;
     }
-    if (h->max_degree > 64) {
-        h->err = "propagation kernels support rows of at most 64 connections in this build";
+    if (h->max_degree > 64 && !d->fresh_on) {
+        // the peer-major k_send walks a row with one wavefront
+        h->err = "the peer-major delivery kernel supports rows of at most 64 connections";
         return GSIM_ERANGE;
     }
     if (h->sh && !d->fresh_on) {

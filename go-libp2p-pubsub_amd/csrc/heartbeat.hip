@@ -30,6 +30,8 @@ struct Extra {
     // of <= 16 connections, then <= 32, then the rest (nullptr: one class)
     uint32_t* d_rows = nullptr;
     int64_t n16 = 0, n32 = 0, n64 = 0;
+    // hub observers after them: rows of 65..256, then 257..1024 connections
+    int64_t nh256 = 0, nh1024 = 0;
 };
 
 struct HbArgs {
@@ -353,28 +355,232 @@ __device__ bool gossip_targets(const HbArgs& a, bool cand, bool tpeer, uint32_t 
     return sel;
 }
 
+
+
+// ---------------------------------------------------------------------------
+// The lane group that holds one observer's row.  The heartbeat body
+// (hb_observer) is written once against this interface:
+//   WaveGroup<W>  W lanes of a wavefront (rows of at most 16 / 32 / 64
+//                 connections; 4 / 2 / 1 observers per wavefront)
+//   BlockGroup<B> a whole B-thread block (hub rows of 65 .. B connections):
+//                 counts and keyed minima are block reductions through LDS,
+//                 a lane's neighbours are read from LDS instead of shuffles.
+// Position q of a group is the row position (tie breaks, Philox keys).
+
+template <int W>
+struct WaveGroup {
+    static constexpr int LP = 64 / W;     // topics per lane of the mcache-put cache
+    int lane, grp, gl, base;
+    uint64_t gm;
+    int32_t lpv[LP];
+    __device__ explicit WaveGroup(int lane_)
+        : lane(lane_), grp(lane_ / W), gl(lane_ % W), base((lane_ / W) * W),
+          gm(W == 64 ? ~0ull : (((1ull << W) - 1) << ((lane_ / W) * W)))
+    {
+    }
+    __device__ int pos() const { return gl; }
+    __device__ int span() const { return W; }
+    __device__ int count(bool p) const { return __popcll(__ballot(p) & gm); }
+    __device__ bool any(bool p) const { return (__ballot(p) & gm) != 0; }
+    __device__ bool select(const HbArgs& a, bool cand, int count, uint32_t obs, int32_t t, uint32_t purpose,
+                           uint32_t col)
+    {
+        return select_smallest<W>(a, cand, count, obs, t, purpose, col, (uint32_t)gl, gm, grp);
+    }
+    __device__ bool gossip(const HbArgs& a, bool cand, bool tpeer, uint32_t obs, int32_t t, uint32_t col)
+    {
+        return gossip_targets<W>(a, cand, tpeer, obs, t, col, (uint32_t)gl, gm, grp);
+    }
+    // a lane's value at position q of the group (every lane asks for the same q)
+    template <typename T>
+    struct View {
+        T v;
+        int base;
+        __device__ T operator[](int q) const { return __shfl(v, base + q, 64); }
+    };
+    struct BoolView {
+        uint64_t m;
+        int base;
+        __device__ bool operator[](int q) const { return (m >> (base + q)) & 1ull; }
+    };
+    template <int SLOT, typename T>
+    __device__ View<T> view(T v) const { return View<T>{v, base}; }
+    template <int SLOT>
+    __device__ BoolView view_b(bool v) const { return BoolView{__ballot(v), base}; }
+    // the value at the lowest position where p holds (p must hold somewhere)
+    __device__ double at_lowest(bool p, double v) const
+    {
+        return __shfl(v, (int)__ffsll((long long)(__ballot(p) & gm)) - 1, 64);
+    }
+    // newest mcache put of topic t by observer obs (GetGossipIDs non-empty test):
+    // group lane gl caches topics gl, gl + W, ... (T <= 64)
+    // bit q = p at position q < 64 (W = 64: the wave's ballot)
+    __device__ uint64_t topic_mask(bool p) const { return __ballot(p) & gm; }
+    __device__ void load_lastput(const HbArgs& a, int64_t obs, uint64_t subi, bool ovalid)
+    {
+#pragma unroll
+        for (int k = 0; k < LP; ++k) {
+            const int32_t t = gl + W * k;
+            lpv[k] = (a.gossip && ovalid && t < a.T && ((subi >> t) & 1ull)) ? a.lastput[(int64_t)t * a.N + obs] : -1;
+        }
+    }
+    __device__ int32_t lastput(const HbArgs&, int64_t, int32_t t) const
+    {
+        int32_t lpsel = lpv[0];
+#pragma unroll
+        for (int k = 1; k < LP; ++k)
+            if (t >= W * k) lpsel = lpv[k];
+        return __shfl(lpsel, base + (t & (W - 1)), 64);
+    }
+};
+
+template <int B>
+struct BlockGroup {
+    static constexpr int NW = B / 64;
+    struct Shared {
+        unsigned long long red[2][NW];     // reductions (alternating: one barrier each)
+        double d0[B];
+        uint64_t u0[B], u1[B];
+        int32_t i0[B];
+        uint8_t b0[B], b1[B];
+    };
+    Shared* sh;
+    int tid, lane, wid, phase;
+    __device__ BlockGroup(Shared* s) : sh(s), tid((int)threadIdx.x), lane((int)threadIdx.x & 63),
+                                       wid((int)threadIdx.x >> 6), phase(0) {}
+    __device__ int pos() const { return tid; }
+    __device__ int span() const { return B; }
+    __device__ unsigned long long reduce(unsigned long long v, int op)   // 0 sum, 1 min, 2 max
+    {
+        for (int o = 32; o; o >>= 1) {
+            const unsigned long long y = (unsigned long long)__shfl_xor((long long)v, o, 64);
+            v = op == 0 ? v + y : op == 1 ? (y < v ? y : v) : (y > v ? y : v);
+        }
+        unsigned long long* r = sh->red[phase & 1];
+        ++phase;
+        if (lane == 0) r[wid] = v;
+        __syncthreads();
+        unsigned long long acc = r[0];
+        for (int w = 1; w < NW; ++w) {
+            const unsigned long long y = r[w];
+            acc = op == 0 ? acc + y : op == 1 ? (y < acc ? y : acc) : (y > acc ? y : acc);
+        }
+        return acc;
+    }
+    __device__ int count(bool p) { return (int)reduce((unsigned long long)__popcll(__ballot(p)) * (lane == 0), 0); }
+    __device__ bool any(bool p) { return count(p) != 0; }
+    __device__ uint64_t min_u64(uint64_t v) { return reduce(v, 1); }
+    __device__ uint64_t max_u64(uint64_t v) { return reduce(v, 2); }
+    // select_smallest (above) over the block: the count smallest (key, position)
+    __device__ bool select(const HbArgs& a, bool cand, int count, uint32_t obs, int32_t t, uint32_t purpose,
+                           uint32_t col)
+    {
+        const int n = this->count(cand);
+        if (n == 0) return false;
+        if (count <= 0 || n <= count) return cand;
+        const uint32_t hi = cand ? hb_key_hi(a, obs, t, purpose, col, (uint32_t)tid) : 0xFFFFFFFFu;
+        const uint64_t key = ((uint64_t)hi << 32) | (uint32_t)tid;
+        const uint32_t tau = (uint32_t)((float)count / (float)n * 4294967040.0f);
+        bool sel = cand && hi < tau;
+        int c = this->count(sel);
+        while (c > count) {                 // drop the largest (key, position) among the selected
+            const uint64_t mx = max_u64(sel ? key : 0ull);
+            if (sel && key == mx) sel = false;
+            --c;
+        }
+        bool rest = cand && !sel;
+        while (c < count) {                 // add the smallest among the others
+            const uint64_t mn = min_u64(rest ? key : ~0ull);
+            if (rest && key == mn) { sel = true; rest = false; }
+            ++c;
+        }
+        return sel;
+    }
+    // gossip_targets (above) over the block
+    __device__ bool gossip(const HbArgs& a, bool cand, bool tpeer, uint32_t obs, int32_t t, uint32_t col)
+    {
+        const int c = count(cand);
+        bool dup = false;
+        if (c < a.Dlo) dup = select(a, tpeer, a.Dlo - c, obs, t, P_GOSSIP_FILL, col);
+        const int n = c + count(dup);
+        if (n == 0) return false;
+        int target = a.dlazy;
+        const int factor = (int)(a.gossip_factor * (double)n);
+        if (factor > target) target = factor;
+        if (target >= n) return cand || dup;
+        if (!any(dup)) return select(a, cand, target, obs, t, P_GOSSIP, col);
+        const uint32_t h1 = cand ? hb_key_hi(a, obs, t, P_GOSSIP, col, (uint32_t)tid) : 0xFFFFFFFFu;
+        const uint32_t h2 = dup ? hb_key_hi(a, obs, t, P_GOSSIP_DUP, col, (uint32_t)tid) : 0xFFFFFFFFu;
+        bool has1 = cand, has2 = dup, sel = false;
+        for (int q = 0; q < target; ++q) {
+            const bool use1 = has1 && (!has2 || h1 <= h2);
+            const uint32_t mine = use1 ? h1 : (has2 ? h2 : 0xFFFFFFFFu);
+            const uint64_t k = (has1 || has2) ? (((uint64_t)mine << 32) | (uint32_t)tid) : ~0ull;
+            const uint64_t mn = min_u64(k);
+            if ((has1 || has2) && k == mn) {
+                if (use1) has1 = false; else has2 = false;
+                sel = true;
+            }
+        }
+        return sel;
+    }
+    template <typename T>
+    struct View {
+        const T* p;
+        __device__ T operator[](int q) const { return p[q]; }
+    };
+    template <int SLOT, typename T>
+    __device__ View<T> view(T v)
+    {
+        T* buf;
+        if constexpr (sizeof(T) == 8 && (T)0.5 != (T)0) buf = reinterpret_cast<T*>(sh->d0);     // double
+        else if constexpr (sizeof(T) == 8) buf = reinterpret_cast<T*>(SLOT ? sh->u1 : sh->u0);
+        else buf = reinterpret_cast<T*>(sh->i0);
+        __syncthreads();                    // earlier readers of the buffer are done
+        buf[tid] = v;
+        __syncthreads();
+        return View<T>{buf};
+    }
+    template <int SLOT>
+    __device__ View<uint8_t> view_b(bool v)
+    {
+        uint8_t* buf = SLOT ? sh->b1 : sh->b0;
+        __syncthreads();
+        buf[tid] = v ? 1 : 0;
+        __syncthreads();
+        return View<uint8_t>{buf};
+    }
+    __device__ double at_lowest(bool p, double v)
+    {
+        const uint64_t q = min_u64(p ? (uint64_t)tid : ~0ull);
+        __syncthreads();
+        if ((uint64_t)tid == q) sh->d0[0] = v;
+        __syncthreads();
+        return sh->d0[0];
+    }
+    __device__ uint64_t topic_mask(bool p)
+    {
+        const uint64_t m = __ballot(p);
+        return reduce((wid == 0 && lane == 0) ? m : 0ull, 0);
+    }
+    __device__ void load_lastput(const HbArgs&, int64_t, uint64_t, bool) {}
+    __device__ int32_t lastput(const HbArgs& a, int64_t obs, int32_t t) const
+    {
+        return a.lastput[(int64_t)t * a.N + obs];
+    }
+};
+
 }  // namespace
 
-// One W-lane group = one observer's heartbeat (gossipsub.go:1345-1557):
-// W = 64 one observer per wavefront, W = 32 two (rows of at most 32
-// connections; every VALU instruction then serves two observers).  Group
-// lane gl holds the observer's gl-th connection; ballots are masked to the
-// group, shuffles read the group's own lanes, and branches diverge only
-// between whole groups (group_min_u32 is group-local).
-//
-// rows: the observers of one row-length class (a list), or nullptr for the
-// nrows observers from obs_base on.
-template <int W>
-__global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* rows, int64_t nrows, int64_t obs_base)
+// One observer's heartbeat (gossipsub.go:1345-1557) on its lane group:
+// position q holds the observer's q-th connection; counts, selections and
+// the neighbours' values go through the group (WaveGroup: ballots masked to
+// the group, shuffles of the group's own lanes; BlockGroup: LDS).  Branches
+// diverge only between whole groups.
+template <class Grp>
+__device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs, bool ovalid)
 {
-    constexpr int G = 64 / W;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int grp = lane / W, gl = lane % W, base = grp * W;
-    const uint64_t gm = W == 64 ? ~0ull : (((1ull << W) - 1) << base);
-    const int64_t nobs = nrows;
-    for (int64_t o0 = ((int64_t)blockIdx.x * 4 + wid) * G; o0 < nobs; o0 += (int64_t)gridDim.x * 4 * G) {
-        const bool ovalid = o0 + grp < nobs;
-        const int64_t obs = !ovalid ? 0 : rows ? (int64_t)rows[o0 + grp] : obs_base + o0 + grp;
+        const int gl = g.pos();
         const uint32_t b = ovalid ? a.row_ptr[obs] : 0u;
         const int deg = ovalid ? (int)(a.row_ptr[obs + 1] - b) : 0;
         const bool valid = gl < deg;
@@ -394,15 +600,7 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* row
         // Graft/Prune touches one of the lane's records
         double S_live = S;
         bool dirty = false;
-        // newest mcache put per joined topic (GetGossipIDs non-empty test):
-        // group lane gl holds topics gl, gl + W, ... (T <= 64)
-        constexpr int LP = 64 / W;
-        int32_t lpv[LP];
-#pragma unroll
-        for (int k = 0; k < LP; ++k) {
-            const int32_t t = gl + W * k;
-            lpv[k] = (a.gossip && ovalid && t < a.T && ((subi >> t) & 1ull)) ? a.lastput[(int64_t)t * a.N + obs] : -1;
-        }
+        g.load_lastput(a, obs, subi, ovalid);
         if (a.gossip && valid) a.gstate[e] = S >= a.gossip_thr ? 1 : 0;
 
         // clearBackoff every 15 ticks (gossipsub.go:1627-1646)
@@ -452,7 +650,6 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* row
             const bool tpeer = valid && conn && ((subj >> t) & 1ull);
             bool m = valid && (fl & GSIM_TF_MESH);
             uint8_t ctl = 0;
-            const uint32_t pos = (uint32_t)gl;
 
             auto prune = [&]() {
                 stats_prune(a, tracked, scored, thr, mcap, sf);
@@ -476,33 +673,38 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* row
             if (m && S < 0) prune();
 
             // too few peers: graft up to D (1412-1427)
-            int l = __popcll(ballot(m) & gm);
+            int l = g.count(m);
             if (l < a.Dlo) {
                 need_bo();
                 const bool cand = tpeer && !m && bo == 0 && !dir && S >= 0;
-                if (select_smallest<W>(a, cand, a.D - l, gobs, t, P_GRAFT_DLO, gcol, pos, gm, grp)) graft();
+                if (g.select(a, cand, a.D - l, gobs, t, P_GRAFT_DLO, gcol)) graft();
             }
 
             // too many peers: keep Dscore best + random, Dout outbound (1429-1490)
-            l = __popcll(ballot(m) & gm);
+            l = g.count(m);
             if (l > a.Dhi) {
-                const uint64_t mm = ballot(m) & gm;
-                const uint64_t k1 = m ? hb_key(a, gobs, t, P_PRUNE_SHUF1, gcol, pos) : ~0ull;
+                const uint64_t k1 = m ? hb_key(a, gobs, t, P_PRUNE_SHUF1, gcol, (uint32_t)gl) : ~0ull;
                 int rank1 = 0;
-                for (int q = base; q < base + W; ++q) {
-                    const double sq = __shfl(S, q, 64);
-                    const uint64_t kq = __shfl(k1, q, 64);
-                    if (((mm >> q) & 1ull) && (sq > S || (sq == S && kq < k1))) ++rank1;
+                {
+                    const auto vm = g.template view_b<0>(m);
+                    const auto vs = g.template view<0>(S);
+                    const auto vk = g.template view<0>(k1);
+                    for (int q = 0; q < g.span(); ++q) {
+                        const double sq = vs[q];
+                        const uint64_t kq = vk[q];
+                        if (vm[q] && (sq > S || (sq == S && kq < k1))) ++rank1;
+                    }
                 }
                 const int ds = a.Dscore < l ? a.Dscore : l;
                 const bool tail = m && rank1 >= ds;
-                const uint64_t k2 = tail ? hb_key(a, gobs, t, P_PRUNE_SHUF2, gcol, pos) : ~0ull;
+                const uint64_t k2 = tail ? hb_key(a, gobs, t, P_PRUNE_SHUF2, gcol, (uint32_t)gl) : ~0ull;
                 // every lane takes part in the shuffles (a shuffle inside a
                 // divergent branch would read inactive lanes)
                 int below = 0;
-                for (int q = base; q < base + W; ++q) {
-                    const uint64_t kq = __shfl(k2, q, 64);
-                    if (kq < k2) ++below;   // non-tail lanes hold ~0 and never count
+                {
+                    const auto vk2 = g.template view<1>(k2);
+                    for (int q = 0; q < g.span(); ++q)
+                        if (vk2[q] < k2) ++below;   // non-tail lanes hold ~0 and never count
                 }
                 const int p = tail ? ds + below : rank1;
                 // Keep plst[:D] after Go's Dout rotation (1457-1485), computed
@@ -512,19 +714,23 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* row
                 //  in order; pass 2 rotates the first j outbound peers beyond D
                 //  to the front, pushing the last j "rest" peers out of plst[:D].
                 const bool inD = m && p < a.D;
-                const int obD = __popcll(ballot(inD && outb) & gm);
+                const int obD = g.count(inD && outb);
                 bool keep = inD;
                 if (obD < a.Dout) {
                     const bool rest = inD && !(outb && p >= 1);
                     const bool cb = m && p >= a.D && outb;
-                    const uint64_t restmask = ballot(rest) & gm, cbmask = ballot(cb) & gm;
+                    const int nb = g.count(cb);
                     int rb = 0, rr = 0;
-                    for (int q = base; q < base + W; ++q) {
-                        const int pq = __shfl(p, q, 64);
-                        if (((cbmask >> q) & 1ull) && pq < p) ++rb;
-                        if (((restmask >> q) & 1ull) && pq > p) ++rr;
+                    {
+                        const auto vrest = g.template view_b<0>(rest);
+                        const auto vcb = g.template view_b<1>(cb);
+                        const auto vp = g.template view<0>((int32_t)p);
+                        for (int q = 0; q < g.span(); ++q) {
+                            const int pq = vp[q];
+                            if (vcb[q] && pq < p) ++rb;
+                            if (vrest[q] && pq > p) ++rr;
+                        }
                     }
-                    const int nb = __popcll(cbmask);
                     const int j = a.Dout - obD < nb ? a.Dout - obD : nb;
                     keep = (inD && !(rest && rr < j)) || (cb && rb < j);
                 }
@@ -532,33 +738,33 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* row
             }
 
             // enough outbound peers? (1492-1518)
-            l = __popcll(ballot(m) & gm);
+            l = g.count(m);
             if (l >= a.Dlo) {
-                const int ob = __popcll(ballot(m && outb) & gm);
+                const int ob = g.count(m && outb);
                 if (ob < a.Dout) {
                     need_bo();
                     const bool cand = tpeer && !m && bo == 0 && !dir && outb && S >= 0;
-                    if (select_smallest<W>(a, cand, a.Dout - ob, gobs, t, P_GRAFT_DOUT, gcol, pos, gm, grp))
-                        graft();
+                    if (g.select(a, cand, a.Dout - ob, gobs, t, P_GRAFT_DOUT, gcol)) graft();
                 }
             }
 
             // opportunistic grafting (1520-1552)
-            l = __popcll(ballot(m) & gm);
+            l = g.count(m);
             if (a.opp_ticks && a.tick % a.opp_ticks == 0 && l > 1) {
-                const uint64_t mm = ballot(m) & gm;
                 int rank = 0;
-                for (int q = base; q < base + W; ++q) {
-                    const double sq = __shfl(S, q, 64);
-                    if (((mm >> q) & 1ull) && (sq < S || (sq == S && q < lane))) ++rank;
+                {
+                    const auto vm = g.template view_b<0>(m);
+                    const auto vs = g.template view<0>(S);
+                    for (int q = 0; q < g.span(); ++q) {
+                        const double sq = vs[q];
+                        if (vm[q] && (sq < S || (sq == S && q < gl))) ++rank;
+                    }
                 }
-                const uint64_t at = ballot(m && rank == l / 2) & gm;
-                const double median = __shfl(S, (int)__ffsll((long long)at) - 1, 64);
+                const double median = g.at_lowest(m && rank == l / 2, S);
                 if (median < a.opp_threshold) {
                     need_bo();
                     const bool cand = tpeer && !m && bo == 0 && !dir && S > median;
-                    if (select_smallest<W>(a, cand, a.opp_peers, gobs, t, P_GRAFT_OPP, gcol, pos, gm, grp))
-                        graft();
+                    if (g.select(a, cand, a.opp_peers, gobs, t, P_GRAFT_OPP, gcol)) graft();
                 }
             }
 
@@ -575,18 +781,14 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* row
             // joined topic's plane is rewritten each heartbeat.
             if (a.gossip) {
                 bool gsel = false;
-                int32_t lpsel = lpv[0];
-#pragma unroll
-                for (int k = 1; k < LP; ++k)
-                    if (t >= W * k) lpsel = lpv[k];
-                const int32_t lpt = __shfl(lpsel, base + (t & (W - 1)), 64);
+                const int32_t lpt = g.lastput(a, obs, t);
                 if (lpt >= (int64_t)a.tick - a.hist_gossip) {
-                    if (__ballot(dirty) & gm) {
+                    if (g.any(dirty)) {
                         if (dirty) S_live = score_of_record(a, rv, col);
                         dirty = false;
                     }
                     const bool gcand = tpeer && !m && !dir && S_live >= a.gossip_thr;
-                    gsel = gossip_targets<W>(a, gcand, tpeer, gobs, t, gcol, pos, gm, grp);
+                    gsel = g.gossip(a, gcand, tpeer, gobs, t, gcol);
                 }
                 if (valid) a.gsel[i] = gsel ? 1 : 0;
             }
@@ -599,7 +801,32 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* row
             }
           }
         }
+}
+
+// W-lane groups: W = 64 one observer per wavefront, W = 32 two, W = 16 four
+// (rows of at most W connections; every VALU instruction serves G observers).
+// rows: the observers of one row-length class (a list), or nullptr for the
+// nrows observers from obs_base on.
+template <int W>
+__global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* rows, int64_t nrows, int64_t obs_base)
+{
+    constexpr int G = 64 / W;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    WaveGroup<W> g(lane);
+    for (int64_t o0 = ((int64_t)blockIdx.x * 4 + wid) * G; o0 < nrows; o0 += (int64_t)gridDim.x * 4 * G) {
+        const bool ovalid = o0 + g.grp < nrows;
+        const int64_t obs = !ovalid ? 0 : rows ? (int64_t)rows[o0 + g.grp] : obs_base + o0 + g.grp;
+        hb_observer(a, g, obs, ovalid);
     }
+}
+
+// Hub observers (rows of 65 .. B connections): one block per observer.
+template <int B>
+__global__ __launch_bounds__(B) void k_heartbeat_hub(HbArgs a, const uint32_t* rows, int64_t nrows)
+{
+    __shared__ typename BlockGroup<B>::Shared sh;
+    BlockGroup<B> g(&sh);
+    for (int64_t o = blockIdx.x; o < nrows; o += gridDim.x) hb_observer(a, g, (int64_t)rows[o], true);
 }
 
 // Fanout expiry and maintenance (gossipsub.go:1558-1596), run after
@@ -609,19 +836,19 @@ __global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* row
 // publishThreshold, top up to D, and emitGossip excluding the fanout peers
 // with the live score after this heartbeat's Graft/Prune.  One wave per
 // observer; observers without fanout state leave after two loads.
-__global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
+template <class Grp>
+__device__ __forceinline__ void fanout_observer(const HbArgs& a, Grp& g, int64_t obs)
 {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int64_t obs = a.olo + (int64_t)blockIdx.x * 4 + wid; obs < a.ohi; obs += (int64_t)gridDim.x * 4) {
-        const int64_t lpub = lane < a.T ? a.lastpub[obs * a.T + lane] : 0;
-        const uint64_t expired = __ballot(lpub != 0 && lpub + a.fanout_ttl < a.now);
+        const int gl = g.pos();
+        const int64_t lpub = gl < a.T ? a.lastpub[obs * a.T + gl] : 0;
+        const uint64_t expired = g.topic_mask(lpub != 0 && lpub + a.fanout_ttl < a.now);
         const uint64_t fant0 = a.fan_topics[obs];
-        if (!expired && !fant0) continue;                       // wave-uniform
+        if (!expired && !fant0) return;                         // group-uniform
         const uint32_t b = a.row_ptr[obs];
         const int deg = (int)(a.row_ptr[obs + 1] - b);
-        const bool valid = lane < deg;
-        const uint32_t e = b + (uint32_t)lane;
-        if ((expired >> lane) & 1ull) a.lastpub[obs * a.T + lane] = 0;
+        const bool valid = gl < deg;
+        const uint32_t e = b + (uint32_t)gl;
+        if (gl < 64 && ((expired >> gl) & 1ull)) a.lastpub[obs * a.T + gl] = 0;
         for (uint64_t q = expired & fant0; q; q &= q - 1) {
             const int64_t i = (int64_t)(__ffsll((long long)q) - 1) * a.E + e;
             if (valid) {
@@ -631,8 +858,8 @@ __global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
             }
         }
         const uint64_t fant = fant0 & ~expired;
-        if (lane == 0 && fant != fant0) a.fan_topics[obs] = fant;
-        if (!fant) continue;
+        if (gl == 0 && fant != fant0) a.fan_topics[obs] = fant;
+        if (!fant) return;
         const uint32_t col = valid ? a.col[e] : 0u;
         const uint32_t rv = valid ? a.rev[e] : 0u;
         const uint32_t gobs = glob(a, (uint32_t)obs), gcol = valid ? glob(a, col) : 0u;
@@ -640,7 +867,6 @@ __global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
         const bool dir = valid && a.direct[e];
         const double S = valid ? a.score[rv] : 0.0;
         const uint64_t subj = valid ? a.sub[col] : 0ull;
-        const int32_t lp_lane = (a.gossip && lane < a.T) ? a.lastput[(int64_t)lane * a.N + obs] : -1;
         double S_live = 0.0;
         bool have_live = false;
         for (uint64_t q = fant; q; q &= q - 1) {
@@ -649,26 +875,46 @@ __global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
             const uint8_t fl = valid ? a.mflags[i] : 0;
             const bool tpeer = conn && ((subj >> t) & 1ull);
             bool inf = (fl & GSIM_TF_FANOUT) && tpeer && S >= a.pub_thr;
-            const int have = __popcll(ballot(inf));
+            const int have = g.count(inf);
             if (have < a.D) {
                 const bool cand = tpeer && !inf && !dir && S >= a.pub_thr;
-                if (select_smallest(a, cand, a.D - have, gobs, t, P_FANOUT, gcol, (uint32_t)lane)) inf = true;
+                if (g.select(a, cand, a.D - have, gobs, t, P_FANOUT, gcol)) inf = true;
             }
             const uint8_t nf = inf ? (uint8_t)(fl | GSIM_TF_FANOUT) : (uint8_t)(fl & ~GSIM_TF_FANOUT);
             if (valid && nf != fl) a.mflags[i] = nf;
             if (!a.gossip) continue;
             bool gsel = false;
-            if (__shfl(lp_lane, t, 64) >= (int64_t)a.tick - a.hist_gossip) {
+            if (a.lastput[(int64_t)t * a.N + obs] >= (int64_t)a.tick - a.hist_gossip) {
                 if (!have_live) {                               // live Score(p), gossipsub.go:1734
                     if (valid) S_live = score_of_record(a, rv, col);
                     have_live = true;
                 }
                 const bool gcand = tpeer && !inf && !dir && S_live >= a.gossip_thr;
-                gsel = gossip_targets(a, gcand, tpeer, gobs, t, gcol, (uint32_t)lane);
+                gsel = g.gossip(a, gcand, tpeer, gobs, t, gcol);
             }
             if (valid) a.gsel[i] = gsel ? 1 : 0;
         }
+}
+
+// Fanout expiry and maintenance, one wave per observer of at most 64
+// connections; observers without fanout state leave after two loads.
+__global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    WaveGroup<64> g(lane);
+    for (int64_t obs = a.olo + (int64_t)blockIdx.x * 4 + wid; obs < a.ohi; obs += (int64_t)gridDim.x * 4) {
+        if (a.row_ptr[obs + 1] - a.row_ptr[obs] > 64u) continue;    // a hub: k_fanout_heartbeat_hub
+        fanout_observer(a, g, obs);
     }
+}
+
+// ... of the hub observers (rows of 65 .. B connections), one block each
+template <int B>
+__global__ __launch_bounds__(B) void k_fanout_heartbeat_hub(HbArgs a, const uint32_t* rows, int64_t nrows)
+{
+    __shared__ typename BlockGroup<B>::Shared sh;
+    BlockGroup<B> g(&sh);
+    for (int64_t o = blockIdx.x; o < nrows; o += gridDim.x) fanout_observer(a, g, (int64_t)rows[o]);
 }
 
 // HandleRPC control processing for every receiver: handleGraft
@@ -680,40 +926,44 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
 {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (int64_t rcv = a.olo + (int64_t)blockIdx.x * 4 + wid; rcv < a.ohi; rcv += (int64_t)gridDim.x * 4) {
-        const uint32_t b = a.row_ptr[rcv];
-        const int deg = (int)(a.row_ptr[rcv + 1] - b);
-        const bool valid = lane < deg;
-        const uint32_t e = b + (uint32_t)lane;
         // topics whose inbox planes may hold entries for this receiver: the
         // others are not read (most receivers get no GRAFT/PRUNE in a round)
         const uint64_t any = a.cany_in[rcv];
         if (!any) continue;
         if (lane == 0) a.cany_in[rcv] = 0;
+        const uint32_t b = a.row_ptr[rcv];
+        const int deg = (int)(a.row_ptr[rcv + 1] - b);
+        const int nch = (deg + 63) >> 6;                    // rows longer than 64: 64-edge chunks in order
         const uint64_t subr = a.sub[rcv];
         for (int32_t t0 = 0; t0 < a.T; t0 += kFlagChunk) {
           if (!((any >> t0) & ((1ull << kFlagChunk) - 1))) continue;
-          uint8_t cc[kFlagChunk];
-#pragma unroll
-          for (int j = 0; j < kFlagChunk; ++j) {
-              const int32_t t = t0 + j;
-              cc[j] = (t < a.T && valid && ((any >> t) & 1ull)) ? a.ctl_in[(int64_t)t * a.E + e] : 0;
-          }
           for (int j = 0; j < kFlagChunk; ++j) {
             const int32_t t = t0 + j;
             if (t >= a.T) break;
-            const int64_t i = (int64_t)t * a.E + e;
-            const uint8_t c = cc[j];
-            uint64_t pending = ballot(c != 0);
-            if (!pending) continue;
-            if (c) a.ctl_in[i] = 0;
-            if (!((subr >> t) & 1ull)) continue;            // unknown topic: ignored
+            if (!((any >> t) & 1ull)) continue;
+            const bool joined = (subr >> t) & 1ull;
             const ctp_t tp = const_tp(a.tp) + t;
             const bool scored = tp->scored != 0;
             const double thr = tp->mesh_message_deliveries_threshold;
             const double mcap = tp->mesh_message_deliveries_cap;
-            uint8_t fl = valid ? a.mflags[i] : 0;
-            int mesh = __popcll(ballot(valid && (fl & GSIM_TF_MESH)));
-            while (pending) {
+            // the mesh size before this round's records (the whole row)
+            int mesh = 0;
+            if (joined)
+                for (int ch = 0; ch < nch; ++ch) {
+                    const bool v = ch * 64 + lane < deg;
+                    mesh += __popcll(ballot(v && (a.mflags[(int64_t)t * a.E + b + ch * 64 + lane] & GSIM_TF_MESH)));
+                }
+            for (int ch = 0; ch < nch; ++ch) {
+              const bool valid = ch * 64 + lane < deg;
+              const uint32_t e = b + (uint32_t)(ch * 64 + lane);
+              const int64_t i = (int64_t)t * a.E + e;
+              const uint8_t c = valid ? a.ctl_in[i] : 0;
+              uint64_t pending = ballot(c != 0);
+              if (!pending) continue;
+              if (c) a.ctl_in[i] = 0;
+              if (!joined) continue;                          // unknown topic: ignored
+              uint8_t fl = valid ? a.mflags[i] : 0;
+              while (pending) {
                 const int q = __ffsll((long long)pending) - 1;
                 pending &= pending - 1;
                 int delta = 0;
@@ -772,6 +1022,7 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                     }
                 }
                 mesh += __shfl(delta, q, 64);
+              }
             }
           }
         }
@@ -932,38 +1183,63 @@ __global__ __launch_bounds__(256) void k_churn_apply(HbArgs a, ChurnArgs c)
 // counter word 0 = the round, a.tick); then lastpub = now.  Of several
 // messages of one (origin, topic) in a batch the first does the selection
 // (the others would find the fanout non-empty).
-__global__ __launch_bounds__(256) void k_fanout_publish(HbArgs a, const gsim_msg* pub, int32_t count)
+template <class Grp>
+__device__ __forceinline__ void fanout_publish_one(const HbArgs& a, Grp& g, const gsim_msg* pub, int32_t k)
 {
-    const int lane = threadIdx.x & 63;
-    const int32_t k = (int32_t)blockIdx.x * 4 + (int32_t)(threadIdx.x >> 6);
-    if (k >= count) return;                                   // wave-uniform
+    const int gl = g.pos();
     const uint32_t o = pub[k].origin;
     const int32_t t = (int32_t)pub[k].topic;
-    if (o < a.olo || o >= a.ohi) return;                      // published on another shard
-    if ((a.sub[o] >> t) & 1ull) return;                       // joined: it publishes to its mesh
     bool dup = false;
-    for (int32_t q = lane; q < k; q += 64) dup |= pub[q].origin == o && (int32_t)pub[q].topic == t;
-    if (__ballot(dup)) return;
+    for (int32_t q = gl; q < k; q += g.span()) dup |= pub[q].origin == o && (int32_t)pub[q].topic == t;
+    if (g.any(dup)) return;
     const uint32_t b = a.row_ptr[o];
     const int deg = (int)(a.row_ptr[o + 1] - b);
-    const bool valid = lane < deg;
-    const uint32_t e = b + (uint32_t)lane;
+    const bool valid = gl < deg;
+    const uint32_t e = b + (uint32_t)gl;
     const int64_t i = (int64_t)t * a.E + e;
     const uint8_t fl = valid ? a.mflags[i] : 0;
-    const bool have = ((a.fan_topics[o] >> t) & 1ull) && __ballot((fl & GSIM_TF_FANOUT) != 0) != 0;
+    const bool have = ((a.fan_topics[o] >> t) & 1ull) && g.any((fl & GSIM_TF_FANOUT) != 0);
     if (!have) {
         const uint32_t col = valid ? a.col[e] : 0u;
         const bool conn = valid && (a.rstate[e] & GSIM_ES_CONNECTED);
         const bool tpeer = conn && ((a.sub[col] >> t) & 1ull);
         const double S = valid ? a.score[a.rev[e]] : 0.0;
         const bool cand = tpeer && !(fl & GSIM_TF_FANOUT) && !(valid && a.direct[e]) && S >= a.pub_thr;
-        const bool sel = select_smallest(a, cand, a.D, glob(a, o), t, P_FANOUT_NEW, valid ? glob(a, col) : 0u,
-                                         (uint32_t)lane);
+        const bool sel = g.select(a, cand, a.D, glob(a, o), t, P_FANOUT_NEW, valid ? glob(a, col) : 0u);
         if (valid && sel) a.mflags[i] = (uint8_t)(fl | GSIM_TF_FANOUT);
-        const bool any = __ballot(sel) != 0;
-        if (lane == 0 && any) atomicOr(reinterpret_cast<unsigned long long*>(a.fan_topics + o), 1ull << t);
+        const bool any = g.any(sel);
+        if (gl == 0 && any) atomicOr(reinterpret_cast<unsigned long long*>(a.fan_topics + o), 1ull << t);
     }
-    if (lane == 0) a.lastpub[(int64_t)o * a.T + t] = a.now;
+    if (gl == 0) a.lastpub[(int64_t)o * a.T + t] = a.now;
+}
+
+__device__ __forceinline__ bool fanout_publisher(const HbArgs& a, const gsim_msg* pub, int32_t k)
+{
+    const uint32_t o = pub[k].origin;
+    if (o < a.olo || o >= a.ohi) return false;                // published on another shard
+    return !((a.sub[o] >> pub[k].topic) & 1ull);               // joined: it publishes to its mesh
+}
+
+__global__ __launch_bounds__(256) void k_fanout_publish(HbArgs a, const gsim_msg* pub, int32_t count)
+{
+    const int32_t k = (int32_t)blockIdx.x * 4 + (int32_t)(threadIdx.x >> 6);
+    if (k >= count || !fanout_publisher(a, pub, k)) return;  // wave-uniform
+    const uint32_t o = pub[k].origin;
+    if (a.row_ptr[o + 1] - a.row_ptr[o] > 64u) return;        // a hub: k_fanout_publish_hub
+    WaveGroup<64> g(threadIdx.x & 63);
+    fanout_publish_one(a, g, pub, k);
+}
+
+template <int B>
+__global__ __launch_bounds__(B) void k_fanout_publish_hub(HbArgs a, const gsim_msg* pub, int32_t count)
+{
+    __shared__ typename BlockGroup<B>::Shared sh;
+    const int32_t k = (int32_t)blockIdx.x;
+    if (k >= count || !fanout_publisher(a, pub, k)) return;  // block-uniform
+    const uint32_t o = pub[k].origin;
+    if (a.row_ptr[o + 1] - a.row_ptr[o] <= 64u) return;
+    BlockGroup<B> g(&sh);
+    fanout_publish_one(a, g, pub, k);
 }
 
 // ---------------------------------------------------------------------------
@@ -996,15 +1272,17 @@ int alloc_extra(gsim_handle* h)
     std::vector<uint32_t> rp((size_t)h->n + 1);
     e = hipMemcpy(rp.data(), h->d_row_ptr, sizeof(uint32_t) * rp.size(), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_check(h, e, "row_ptr readback");
-    uint32_t md = 0;
-    std::vector<uint32_t> cls[3];
+    uint32_t md = 0, mdall = 0;
+    std::vector<uint32_t> cls[5];
     for (int64_t i = h->olo(); i < h->ohi(); ++i) {
         const uint32_t d = rp[(size_t)i + 1] - rp[(size_t)i];
         md = std::max(md, d);
-        cls[d <= 16 ? 0 : d <= 32 ? 1 : 2].push_back((uint32_t)i);
+        cls[d <= 16 ? 0 : d <= 32 ? 1 : d <= 64 ? 2 : d <= 256 ? 3 : 4].push_back((uint32_t)i);
     }
+    for (int64_t i = 0; i < h->n; ++i) mdall = std::max(mdall, rp[(size_t)i + 1] - rp[(size_t)i]);
     h->x->max_degree = md;
     h->x->n16 = (int64_t)cls[0].size(); h->x->n32 = (int64_t)cls[1].size(); h->x->n64 = (int64_t)cls[2].size();
+    h->x->nh256 = (int64_t)cls[3].size(); h->x->nh1024 = (int64_t)cls[4].size();
     if (md > 16) {   // more than one class may be present: keep the lists
         std::vector<uint32_t> all;
         all.reserve((size_t)h->n);
@@ -1015,7 +1293,7 @@ int alloc_extra(gsim_handle* h)
         if (e != hipSuccess) return hip_check(h, e, "row classes");
         h->bytes_allocated += sizeof(uint32_t) * all.size();
     }
-    h->max_degree = md;
+    h->max_degree = mdall;   // every local row (a shard's ghost rows too)
     return GSIM_OK;
 }
 
@@ -1102,8 +1380,8 @@ static int grid_rows(int64_t n)
 
 static int check_degree(gsim_handle* h)
 {
-    if (h->x->max_degree > 64) {
-        h->err = "heartbeat kernels support rows of at most 64 connections in this build";
+    if (h->x->max_degree > 1024) {
+        h->err = "heartbeat kernels support rows of at most 1024 connections in this build";
         return GSIM_ERANGE;
     }
     return GSIM_OK;
@@ -1116,6 +1394,8 @@ int launch_fanout_publish(gsim_handle* h, const gsim_msg* d_pub, int32_t count, 
     if (h->gp.flood_publish || count <= 0 || !h->x || !h->x->d_lastpub) return GSIM_OK;
     HbArgs a = make_hb_args(h, (uint64_t)g, now, 0);
     hipLaunchKernelGGL(k_fanout_publish, dim3((count + 3) / 4), dim3(256), 0, h->stream, a, d_pub, count);
+    if (h->x->nh256 + h->x->nh1024)
+        hipLaunchKernelGGL(k_fanout_publish_hub<1024>, dim3(count), dim3(1024), 0, h->stream, a, d_pub, count);
     return hip_check(h, hipGetLastError(), "k_fanout_publish");
 }
 
@@ -1163,8 +1443,22 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
                                        a, r + x->n16, x->n32, (int64_t)0);
         if (x->n64) hipLaunchKernelGGL(k_heartbeat<64>, dim3(grid_rows(x->n64)), dim3(256), 0, h->stream,
                                        a, r + x->n16 + x->n32, x->n64, (int64_t)0);
+        // hubs: one block per observer
+        const uint32_t* rh = r + x->n16 + x->n32 + x->n64;
+        if (x->nh256)
+            hipLaunchKernelGGL(k_heartbeat_hub<256>, dim3((uint32_t)std::min<int64_t>(x->nh256, 65536)), dim3(256), 0,
+                               h->stream, a, rh, x->nh256);
+        if (x->nh1024)
+            hipLaunchKernelGGL(k_heartbeat_hub<1024>, dim3((uint32_t)std::min<int64_t>(x->nh1024, 65536)), dim3(1024),
+                               0, h->stream, a, rh + x->nh256, x->nh1024);
     }
     hipLaunchKernelGGL(k_fanout_heartbeat, dim3(grid_rows(nown)), dim3(256), 0, h->stream, a);
+    if (x->nh256)
+        hipLaunchKernelGGL(k_fanout_heartbeat_hub<256>, dim3((uint32_t)std::min<int64_t>(x->nh256, 65536)), dim3(256),
+                           0, h->stream, a, x->d_rows + x->n16 + x->n32 + x->n64, x->nh256);
+    if (x->nh1024)
+        hipLaunchKernelGGL(k_fanout_heartbeat_hub<1024>, dim3((uint32_t)std::min<int64_t>(x->nh1024, 65536)),
+                           dim3(1024), 0, h->stream, a, x->d_rows + x->n16 + x->n32 + x->n64 + x->nh256, x->nh1024);
     return hip_check(h, hipGetLastError(), "k_heartbeat");
 }
 

@@ -317,3 +317,39 @@ def test_c5_from_device_fill_skips_unjoined_records(require_gpu):
     down = und[rng.choice(len(und), size=len(und) // 50, replace=False)]
     churn = {2: [(down, False)], 4: [(down, True)]}
     run_parity(net, params, th, gp, st, ticks, sched, ring=1024, churn=churn, eng=eng)
+
+
+@pytest.mark.gpu
+def test_hub_rows_bit_exact(require_gpu):
+    """Hub observers (rows of 65-1024 connections, SURVEY §8 C5's power law
+    with its cap raised): the heartbeat, fanout maintenance and fanout
+    publication of hubs run one block per observer (BlockGroup), control
+    handling walks long rows in 64-edge chunks, delivery uses the flattened
+    topic-major walk.  Dense meshes on hub rows exercise the Dhi prune ranks,
+    opportunistic grafting every other tick the median; churn and fanout
+    publishers outside their topics included.  Bit-exact against the oracle
+    every tick."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim import graphs
+    from tickrun import restrict_to_subscriptions, run_parity, subscribed_schedule
+    rng = np.random.default_rng(909)
+    n, T = 3000, 8
+    net = graphs.power_law(n, 16, 2.5, 1024, seed=41, n_topics=T)
+    net = graphs.with_subscriptions(net, graphs.zipf_subscriptions(n, T, 3, seed=42))
+    deg = np.diff(net.row_ptr.astype(np.int64))
+    assert deg.max() > 256 and ((deg > 64) & (deg <= 256)).sum() > 10, "both hub classes present"
+    params = beacon_params(T, RetainScore=3 * Second)
+    th = PeerScoreThresholds(GossipThreshold=-20, PublishThreshold=-40, GraylistThreshold=-300,
+                             OpportunisticGraftThreshold=5)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2, FanoutTTL=3 * Second, OpportunisticGraftTicks=2)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 0.3)
+    restrict_to_subscriptions(st, net)
+    ticks = list(range(1, 7))
+    sched = subscribed_schedule(rng, ticks, net, T, 2.0, 0.02, member_only=False)
+    src = net.owner()
+    und = np.stack([src, net.col], axis=1)
+    und = und[und[:, 0] < und[:, 1]]
+    down = und[rng.choice(len(und), size=len(und) // 50, replace=False)]
+    churn = {3: [(down, False)], 5: [(down, True)]}
+    run_parity(net, params, th, gp, st, ticks, sched, ring=1024, churn=churn)
