@@ -92,7 +92,9 @@ struct Deliver {
     uint32_t* d_gcount = nullptr;      // [2][ring] holders / wanting receivers per slot (direction choice)
     uint8_t* d_gstate = nullptr;       // [E] edge order: owner's snapshot score of col >= gossipThreshold
     uint64_t* d_resp = nullptr;        // IWANT responses (record edge | slot << 32), delivered in round 2
-    uint32_t* d_nresp = nullptr;       // [1] responses queued; [1] overflow; [2] ring-reuse error
+    uint32_t* d_nresp = nullptr;       // [0] responses queued; [1] overflow; [2] ring-reuse error;
+                                       // [3] MaxIHaveLength: bit 0 IHAVE / bit 1 IWANT truncation needed, bit 2 counting
+    uint32_t* d_pair_cnt = nullptr;    // [E] IWANT ids per edge this IHAVE stage (ring > MaxIHaveLength only)
     int64_t resp_cap = 0;
     uint32_t* d_prom = nullptr;        // [P][E] promise ring, edge order of the promiser: slot or none
     uint64_t* d_pcand = nullptr;       // [E] per-IWANT promise candidate (min Philox key | slot)
@@ -580,12 +582,13 @@ constexpr int kTmThreads = 1024;
 constexpr int kTmChunk = 2048;      // peers scanned per frontier chunk
 
 template <int W>   // 0: one thread per edge; 16 / 32 / 64: W lanes per row
-__global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t range)
+__global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t range, int32_t stage)
 {
-    // [nws] committed bits of the receivers' words, then [ring] u16 slots
-    extern __shared__ uint64_t s_bm[];
+    // [nws] committed bits of the receivers' words (stage: more receivers than
+    // fit in LDS read them from HBM instead), then [ring] u16 slots
+    extern __shared__ uint64_t s_dyn[];
     const int64_t wlo = (int64_t)a.rlo >> 6, nws = (((int64_t)a.rhi + 63) >> 6) - wlo;
-    uint16_t* s_slots = reinterpret_cast<uint16_t*>(s_bm + nws);
+    uint16_t* s_slots = reinterpret_cast<uint16_t*>(s_dyn + (stage ? nws : 0));
     __shared__ uint32_t s_front[kTmChunk];                   // frontier senders
     __shared__ uint32_t s_from[kTmChunk];                    // their first senders
     __shared__ uint32_t s_off[kTmChunk];                     // first flattened edge of each sender
@@ -630,7 +633,9 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
         const uint8_t o_want = (origin < a.N && ((a.sub[origin] >> t) & 1ull)) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
         const bool win_all = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
         // stage the slot's committed bits (receivers' words)
-        for (int64_t w = tid; w < nws; w += kTmThreads) s_bm[w] = a.seenbm[(int64_t)m * a.nw + wlo + w];
+        const uint64_t* s_bm = stage ? s_dyn : a.seenbm + (int64_t)m * a.nw + wlo;
+        if (stage)
+            for (int64_t w = tid; w < nws; w += kTmThreads) s_dyn[w] = a.seenbm[(int64_t)m * a.nw + wlo + w];
         if (tid == 0) s_claimed = 0;
         const unsigned long long first_before = n_first;
         __syncthreads();
@@ -892,8 +897,9 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
 // behaviour) — the advertisers' handleIWant with it: the messages they send
 // are queued for round 2.  Invariants this relies on (checked by the oracle,
 // which implements the reference's counters in full): a receiver gets at most
-// one IHAVE RPC per advertiser per heartbeat (peerhave <= 1, iasked = 0); the
-// ring is not larger than MaxIHaveLength (no IHAVE/IWANT truncation); and a
+// one IHAVE RPC per advertiser per heartbeat (peerhave <= 1, iasked = 0); no
+// topic's gossip window and no IWANT list exceeds MaxIHaveLength ids (no
+// truncation: checked on the device when the ring is larger); and a
 // receiver asks an advertiser for a message at most once while it is in the
 // advertiser's mcache, because the answer always arrives (peertx <= 1).
 
@@ -926,6 +932,10 @@ struct IhArgs {
     uint32_t rlo, rhi;
     int32_t sharded;
     const uint32_t* gid;
+    // MaxIHaveLength (gossipsub.go:679-690, 1766-1771): the truncations are
+    // not modeled; a window that could need one is detected instead
+    int32_t max_ihave;
+    uint32_t* pair_cnt;        // [E] IWANT ids per (receiver, advertiser) edge (nullptr: ring <= MaxIHaveLength)
 };
 
 // first-seen round of a cell at control time of round g (any claim still
@@ -971,6 +981,22 @@ __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount
         if (lane == 0) s_n = n;
     }
     __syncthreads();
+    if (blockIdx.x == 0 && a.pair_cnt && s_n > a.max_ihave) {
+        // more slots in the gossip window than MaxIHaveLength: one topic's
+        // window over it would need the per-peer IHAVE truncation (err[3] bit
+        // 0); otherwise IWANT lists are counted per edge (bit 2: check them)
+        uint32_t* s_tc = reinterpret_cast<uint32_t*>(s_act + ((a.ring + 1) & ~1));   // s_cnt, not yet in use
+        for (int t = threadIdx.x; t < a.T; t += blockDim.x) s_tc[t] = 0;
+        __syncthreads();
+        for (int k = threadIdx.x; k < s_n; k += blockDim.x) atomicAdd(&s_tc[a.mtopic[s_act[k]]], 1u);
+        __syncthreads();
+        for (int t = threadIdx.x; t < a.T; t += blockDim.x)
+            if ((int32_t)s_tc[t] > a.max_ihave) atomicOr(&a.nresp[3], 1u);
+        if (threadIdx.x == 0) atomicOr(&a.nresp[3], 4u);
+        __syncthreads();
+        for (int w = threadIdx.x; w < 2 * a.ring; w += blockDim.x) s_cnt[w] = 0;
+        __syncthreads();
+    }
     const int lane = threadIdx.x & 63;
     const int64_t p0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;   // cell index (peer clo + p)
     const int nact = p0 < a.CN ? s_n : 0;
@@ -1127,6 +1153,8 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                         }
                     }
                 }
+                if (req && a.pair_cnt && (a.nresp[3] & 4u))
+                    atomicAdd(&a.pair_cnt[push ? a.rev[e] : e], 1u);   // the receiver's edge to the advertiser
                 n_req += req;
                 n_resp += resp;
                 const uint64_t sb = __ballot(resp);
@@ -1147,6 +1175,20 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
         atomicAdd(&a.gstats[0], n_walk);
         atomicAdd(&a.gstats[1], n_req);
         atomicAdd(&a.gstats[2], n_resp);
+    }
+}
+
+// A receiver asking one advertiser for more than MaxIHaveLength ids would
+// have its IWANT truncated (gossipsub.go:679-690): reported (err[3] bit 1).
+__global__ __launch_bounds__(256) void k_iwant_check(uint32_t* pair_cnt, int64_t E, int32_t max_ihave, uint32_t* err)
+{
+    if (!(err[3] & 4u)) return;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride) {
+        const uint32_t c = pair_cnt[e];
+        if (!c) continue;
+        if ((int32_t)c > max_ihave) atomicOr(&err[3], 2u);
+        pair_cnt[e] = 0;
     }
 }
 
@@ -1332,7 +1374,7 @@ static void dl_free(Deliver* d)
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
-    f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_prom); f(d->d_pcand);
+    f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_pair_cnt); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
     delete d;
 }
@@ -1496,6 +1538,8 @@ static bool ihave_prepare(gsim_handle* h, int64_t g, IhaveStage* st, int* rc)
         a.sharded = 1;
         a.gid = sh->d_gid;
     }
+    a.max_ihave = h->gp.max_ihave_length;
+    a.pair_cnt = d->d_pair_cnt;
     st->lds = (((size_t)d->cfg.ring + 3) & ~(size_t)3) * sizeof(uint16_t) + 4 * kRespStage * sizeof(uint64_t);
     st->lds_c = (((size_t)d->cfg.ring + 1) & ~(size_t)1) * sizeof(uint16_t) + 2 * (size_t)d->cfg.ring * 4;
     st->grid = grid_peers(a.CN);
@@ -1533,6 +1577,9 @@ static int ihave_walk(gsim_handle* h, IhaveStage* st)
         hipLaunchKernelGGL(k_ihave<64>, dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)d->d_gcount);
     hipLaunchKernelGGL(k_promise_insert, dim3(std::min<int64_t>((h->e + 255) / 256, 16384)), dim3(256), 0, h->stream,
                        d->d_pcand, d->d_prom, d->prom_ticks, a.prom_idx, h->e);
+    if (d->d_pair_cnt)
+        hipLaunchKernelGGL(k_iwant_check, dim3(std::min<int64_t>((h->e + 255) / 256, 16384)), dim3(256), 0, h->stream,
+                           d->d_pair_cnt, h->e, h->gp.max_ihave_length, d->d_nresp);
     d->resp_round = a.g + 2;
     return hip_check(h, hipGetLastError(), "k_ihave");
 }
@@ -1572,6 +1619,11 @@ int deliver_check_errors(gsim_handle* h)
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return hip_check(h, e, "delivery error flags");
     if (err[1]) { h->err = "IWANT responses overflowed their queue (raise gsim_msg_config.max_arrivals)"; return GSIM_ERANGE; }
+    if (err[3] & 3u) {
+        h->err = (err[3] & 1u) ? "a topic's gossip window exceeded MaxIHaveLength ids (IHAVE truncation is not modeled)"
+                               : "an IWANT list exceeded MaxIHaveLength ids (IWANT truncation is not modeled)";
+        return GSIM_ERANGE;
+    }
     if (err[2]) {
         h->err = "a ring slot was republished while its message could still be gossiped or promised (raise ring)";
         return GSIM_ESTATE;
@@ -1596,6 +1648,8 @@ int deliver_read_seen(gsim_handle* h, void* dst)
     return hip_check(h, e, "gsim_read_field(SEEN)");
 }
 
+constexpr size_t kLdsBudget = 160 * 1024 - 33 * 1024;   // minus the static frontier buffers
+
 template <int W>
 static int launch_send_tm(gsim_handle* h, const RoundArgs& a, size_t lds)
 {
@@ -1610,11 +1664,14 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a, size_t lds)
                                                                     std::max<int64_t>(1, total / std::max(1, h->t))));
     const int32_t range = (int32_t)(((cn + ranges - 1) / ranges + 63) & ~63ll);
     const int64_t p = (cn + range - 1) / range;
+    // the committed bits are staged in LDS while they fit, else read from HBM
+    const int32_t stage = (lds <= kLdsBudget && h->tm_stage != 0) ? 1 : 0;
+    if (!stage) lds = ((size_t)h->dl->cfg.ring * 2 + 7) & ~(size_t)7;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_send_tm<W>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return hip_check(h, e, "k_send_tm LDS attribute");
     hipLaunchKernelGGL(k_send_tm<W>, dim3((uint32_t)p, (uint32_t)std::max(1, h->t)), dim3(kTmThreads), lds, h->stream,
-                       a, range);
+                       a, range, stage);
     return hip_check(h, hipGetLastError(), "k_send_tm");
 }
 
@@ -1625,7 +1682,6 @@ static size_t send_tm_lds(const gsim_handle* h, const Deliver* d)
     const int64_t nws = ((h->ohi() + 63) >> 6) - (h->olo() >> 6);
     return (size_t)nws * 8 + (((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7);
 }
-constexpr size_t kLdsBudget = 160 * 1024 - 33 * 1024;   // minus the static frontier buffers
 
 template <int W>
 static void launch_send(gsim_handle* h, int grid, size_t lds, const RoundArgs& a)
@@ -1911,7 +1967,7 @@ int deliver_variant_changed(gsim_handle* h)
     if (!d) return GSIM_OK;
     int rc = deliver_flush(h);
     if (rc) return rc;
-    const bool on = h->send_variant == 3 && send_tm_lds(h, d) <= kLdsBudget;
+    const bool on = h->send_variant == 3;
     if (on != d->fresh_on) {
         // the topic-major kernel's next frontier would be missing its fresh bits
         if (on && d->next_round > 0) {
@@ -1941,12 +1997,6 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     }
     if (h->e >= (int64_t)kEdgeMask || h->n >= (int64_t)kPeerMask) {
         h->err = "too many edges or peers for the seen-set claim encoding (< 2^30 - 1)";
-        return GSIM_ERANGE;
-    }
-    if (cfg->ring > h->gp.max_ihave_length) {
-        // a gossip window could then exceed MaxIHaveLength ids: the per-peer
-        // IHAVE / IWANT truncation (gossipsub.go:679-690, 1766-1771) is not modeled
-        h->err = "ring larger than MaxIHaveLength (IHAVE/IWANT truncation is not modeled on the device)";
         return GSIM_ERANGE;
     }
     (void)hipStreamSynchronize(h->stream);
@@ -1987,6 +2037,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_gstate, (size_t)h->e);
     A((void**)&d->d_resp, (size_t)d->resp_cap * 8);
     A((void**)&d->d_nresp, 4 * 4);
+    if (cfg->ring > h->gp.max_ihave_length) A((void**)&d->d_pair_cnt, (size_t)h->e * 4);
     A((void**)&d->d_prom, (size_t)d->prom_ticks * (size_t)h->e * 4);
     A((void**)&d->d_pcand, (size_t)h->e * 8);
     A((void**)&d->d_behaviour, N);
@@ -1997,7 +2048,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
         return e == hipErrorOutOfMemory ? GSIM_ENOMEM : GSIM_EDEVICE;
     }
     h->dl = d;
-    d->fresh_on = h->send_variant == 3 && send_tm_lds(h, d) <= kLdsBudget;
+    d->fresh_on = h->send_variant == 3;
     e = hipMemsetAsync(d->d_cell, 0xFF, ring * CN * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_seenbm, 0, ring * ((CN + 63) / 64) * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_fresh, 0, ring * ((CN + 63) / 64) * 8, h->stream);
@@ -2018,6 +2069,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     if (e == hipSuccess) e = hipMemsetAsync(d->d_gsel, 0, T * (size_t)h->e, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_gstate, 0, (size_t)h->e, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_nresp, 0, 4 * 4, h->stream);
+    if (e == hipSuccess && d->d_pair_cnt) e = hipMemsetAsync(d->d_pair_cnt, 0, (size_t)h->e * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_prom, 0xFF, (size_t)d->prom_ticks * (size_t)h->e * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_pcand, 0xFF, (size_t)h->e * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_behaviour, 0, N, h->stream);
@@ -2108,6 +2160,11 @@ int gsim_msg_stats(gsim_handle* h, int64_t* out4)
     if (e != hipSuccess) return hip_check(h, e, "gsim_msg_stats");
     for (int k = 0; k < 4; ++k) out4[k] = (int64_t)s[k];
     if (err[1]) { h->err = "IWANT responses overflowed their queue (raise gsim_msg_config.max_arrivals)"; return GSIM_ERANGE; }
+    if (err[3] & 3u) {
+        h->err = (err[3] & 1u) ? "a topic's gossip window exceeded MaxIHaveLength ids (IHAVE truncation is not modeled)"
+                               : "an IWANT list exceeded MaxIHaveLength ids (IWANT truncation is not modeled)";
+        return GSIM_ERANGE;
+    }
     if (err[2]) {
         h->err = "a ring slot was republished while its message could still be gossiped or promised (raise ring)";
         return GSIM_ESTATE;

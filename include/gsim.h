@@ -442,7 +442,9 @@ int gsim_profile_read(gsim_handle* h, double* ms, int64_t* launches, int32_t n);
  * (16, 32 or 64 lanes per row; 0 = chosen from the row lengths).  which = 4:
  * the topic-major walk over a round's forwarders: 1 = one thread per edge
  * (rows flattened), 2 = a lane group per row, 0 (default) = chosen from the
- * row lengths. */
+ * row lengths.  which = 5: the topic-major kernel's committed bits: 0
+ * (default) staged in LDS while a slot's bits fit (<= ~10^6 receivers), 1
+ * always read from HBM. */
 int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant);
 
 /* ---- synthetic inputs -------------------------------- */

@@ -223,6 +223,7 @@ def _schedule(rng, ticks, T, R, rate, inv_frac, n):
     (3000, 32, 3, [14, 15, 16], 12, 0.05, 0.03, 512, 3),    # clearBackoff tick
     (1500, 24, 2, [1, 2, 3, 4], 6, 0.1, 0.02, 256, 31),     # topic-major, one thread per edge
     (1500, 24, 2, [1, 2, 3, 4], 6, 0.1, 0.02, 256, 32),     # topic-major, a lane group per row
+    (1500, 24, 2, [1, 2, 3, 4], 6, 0.1, 0.02, 256, 315),    # topic-major, committed bits read from HBM
     (1500, 32, 2, [1, 2, 3], 8, 0.1, 0.02, 256, 0),         # peer-major k_send (same results)
     (1500, 24, 2, [1, 2, 3], 8, 0.1, 0.02, 256, 0),
     (3000, 32, 3, [14, 15, 16], 12, 0.05, 0.03, 512, 0),
@@ -251,9 +252,11 @@ def test_rounds_bit_exact(require_gpu, n, k, T, ticks, rate, inv_frac, retained,
     eng.set_seed(SEED)
     st.push_to_engine(eng)
     eng.msgs_init(ring, R, T0, HB)
-    eng.set_kernel_variant(2, send_variant if send_variant < 10 else send_variant // 10)
+    eng.set_kernel_variant(2, int(str(send_variant)[0]))
     if send_variant >= 10:
-        eng.set_kernel_variant(4, send_variant % 10)
+        eng.set_kernel_variant(4, int(str(send_variant)[1]))
+    if send_variant >= 100:
+        eng.set_kernel_variant(5, 1)
     sched = _schedule(rng, ticks, T, R, rate, inv_frac, n)
     lib = ob.load()
     for kk in ticks:

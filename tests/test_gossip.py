@@ -217,3 +217,59 @@ def test_iwant_response_queue_overflow_is_reported(require_gpu):
     assert ei.value.rc == _abi.GSIM_ERANGE
     assert eng.gossip_stats()["iwant_responses"] > 4
     eng.close()
+
+
+def _gossip_window_run(max_ihave_length, ring=256, n=1200, T=8, rate=10, ticks=5):
+    """Every topic busy: several messages per topic in each gossip window."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim.engine import Engine, random_regular
+    from test_delivery import _schedule
+    rng = np.random.default_rng(4242)
+    params = beacon_params(T)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2, MaxIHaveLength=max_ihave_length)
+    th = PeerScoreThresholds(GossipThreshold=-20, PublishThreshold=-50, GraylistThreshold=-300)
+    net = random_regular(n, 16, seed=n + 3, n_topics=T)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 8 / 16)
+    sched = _schedule(rng, list(range(1, ticks + 1)), T, R, rate, 0.0, n)
+    return net, params, th, gp, st, sched
+
+
+@pytest.mark.gpu
+def test_ring_larger_than_max_ihave_length_bit_exact(require_gpu):
+    """A ring larger than MaxIHaveLength (gsim_msgs_init accepts it): the
+    gossip window holds more ids than MaxIHaveLength in all, but no topic's
+    window and no IWANT list exceeds it, so no truncation applies
+    (gossipsub.go:679-690, 1766-1771) and the device is bit-exact with the
+    oracle, which implements the truncations."""
+    from tickrun import run_parity
+    net, params, th, gp, st, sched = _gossip_window_run(max_ihave_length=60)
+    msgs, gs = run_parity(net, params, th, gp, st, list(range(1, 6)), sched, ring=256)
+    assert gs["iwant_ids"] > 0
+
+
+@pytest.mark.gpu
+def test_topic_window_over_max_ihave_length_is_reported(require_gpu):
+    """One topic's gossip window over MaxIHaveLength would need the per-peer
+    IHAVE truncation, which the device does not model: it is reported
+    (GSIM_ERANGE) instead of silently advertising too much."""
+    from gsim.engine import Engine, GsimError
+    net, params, th, gp, st, sched = _gossip_window_run(max_ihave_length=4)
+    eng = Engine(params, th, gossip=gp)
+    try:
+        eng.load_graph(net)
+        eng.set_seed(SEED)
+        st.push_to_engine(eng)
+        eng.msgs_init(256, R, T0, Second)
+        with pytest.raises(GsimError) as ei:
+            for kk in range(1, 6):
+                eng.refresh_scores(tick_time(kk))
+                eng.heartbeat(kk, tick_time(kk))
+                for g in range(kk * R, kk * R + R):
+                    if g in sched:
+                        eng.publish(sched[g], g)
+                    eng.round(g)
+            eng.msg_stats()
+        assert ei.value.rc == _abi.GSIM_ERANGE and "MaxIHaveLength" in str(ei.value)
+    finally:
+        eng.close()
