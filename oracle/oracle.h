@@ -160,6 +160,27 @@ enum {
     ORC_REJECT_VALIDATION_IGNORED, ORC_REJECT_SELF_ORIGIN
 };
 
+/* ---- event log of the network oracle (tests/test_oracle_linkage.py) ----- */
+/* With logging on, the network oracle records what each simulated router's
+ * MessageCache, seen cache and gossip tracer observe, so the KAT-pinned
+ * single-router structures below can be driven with the same events and
+ * compared with the network oracle's implicit windows, seen cells and
+ * promise lists. */
+enum {
+    ORC_EV_PUT = 1,        /* a: peer, mid, topic            mcache.Put            */
+    ORC_EV_SEEN = 2,       /* a: peer, mid, x: 1 new / 0 seen  seenMessage/markSeen */
+    ORC_EV_SERVE = 3,      /* a: advertiser, b: requester, mid, x: GetForPeer count */
+    ORC_EV_PROMISE = 4,    /* a: requester, b: advertiser, mid, x: now (AddPromise)  */
+    ORC_EV_FULFILL = 5,    /* a: peer, mid                   fulfillPromise        */
+    ORC_EV_BROKEN = 6,     /* a: peer, b: advertiser, x: count (GetBrokenPromises)  */
+    ORC_EV_PENALTIES = 7,  /* x: now: applyIwantPenalties (every peer)              */
+    ORC_EV_HEARTBEAT = 8,  /* x: tick: GetGossipIDs then Shift (every peer)         */
+    ORC_EV_GOSSIP_ID = 9,  /* a: peer, mid, topic: one id of GetGossipIDs(topic)    */
+};
+typedef struct orc_event { int32_t kind, topic; uint32_t a, b; int64_t g; uint64_t mid; int64_t x; } orc_event;
+void    orc_msgs_log(orc_msgs* m, int32_t on);
+int64_t orc_msgs_events(orc_msgs* m, orc_event* out, int64_t cap);   /* copies and clears; returns the count */
+
 /* ---- mcache.go (one router's MessageCache) ------------------------------ */
 typedef struct orc_mcache orc_mcache;
 orc_mcache* orc_mcache_new(int32_t gossip, int32_t history);            /* mcache.go:21-36 */

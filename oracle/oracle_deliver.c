@@ -28,10 +28,36 @@ priv* orc_msgs_priv(orc_msgs* m)
 
 static priv* P(orc_msgs* m) { return orc_msgs_priv(m); }
 
+void orc_msgs_log(orc_msgs* m, int32_t on) { P(m)->log_on = on; }
+
+void orc_log(orc_msgs* m, int32_t kind, uint32_t a, uint32_t b, uint32_t slot, int32_t topic, int64_t g, int64_t x)
+{
+    priv* p = P(m);
+    if (!p->log_on) return;
+    if (p->nev == p->capev) {
+        p->capev = p->capev ? 2 * p->capev : 4096;
+        p->ev = (orc_event*)realloc(p->ev, sizeof(orc_event) * (size_t)p->capev);
+    }
+    orc_event* v = &p->ev[p->nev++];
+    v->kind = kind; v->topic = topic; v->a = a; v->b = b; v->g = g;
+    v->mid = m->mid ? m->mid[slot] : slot;
+    v->x = x;
+}
+
+int64_t orc_msgs_events(orc_msgs* m, orc_event* out, int64_t cap)
+{
+    priv* p = P(m);
+    const int64_t n = p->nev;
+    if (out) memcpy(out, p->ev, sizeof(orc_event) * (size_t)(n < cap ? n : cap));
+    if (out) p->nev = 0;
+    return n;
+}
+
 void orc_msgs_free_priv(orc_msgs* m)
 {
     if (!m->priv) return;
     priv* p = (priv*)m->priv;
+    free(p->ev);
     free(p->fr);
     free(p->fp);
     free(p->ar);
@@ -107,6 +133,8 @@ void orc_publish(orc_net* s, orc_msgs* m, uint64_t id, uint32_t topic, uint32_t 
      * its mcache (gossipsub.go:976); its own DeliverMessage is not scored
      * (trace.go skips ReceivedFrom == self) */
     row[origin] = (uint32_t)g;
+    orc_log(m, ORC_EV_SEEN, origin, 0, slot, (int32_t)topic, g, 1);
+    orc_log(m, ORC_EV_PUT, origin, 0, slot, (int32_t)topic, g, 0);
     /* Publish: an origin that has not joined the topic sends to its fanout
      * (gossipsub.go:1011-1028); flood publishing sends to every topic peer */
     if (!s->gp->flood_publish && !((s->sub[origin] >> topic) & 1u) && s->lastpub && s->fan_topics)
@@ -175,6 +203,7 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
             orc_mark_invalid(s, er, t);
             continue;
         }
+        orc_log(m, ORC_EV_SEEN, i, 0, slot, t, g, *cell == UNSEEN);
         if (*cell == UNSEEN) {
             *cell = (uint32_t)g;               /* markSeen */
             m->stats[1]++;
@@ -187,6 +216,7 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
                 /* DeliverMessage, score.go:702-726; mcache.Put; forward next round */
                 orc_mark_first(s, er, t);
                 m->lastput[(int64_t)t * s->n + i] = (int32_t)(g / m->rounds);
+                orc_log(m, ORC_EV_PUT, i, 0, slot, t, g, 0);
                 fr_push(p, i, slot, s->col[er]);
             }
             /* RejectValidationIgnored / Throttled: deliveryIgnored / deliveryThrottled,

@@ -51,6 +51,8 @@ static int put_tick(const orc_net* s, const orc_msgs* m, uint32_t slot, uint32_t
 /* Slots of topic t that anyone can hold in a gossip window at heartbeat
  * `tick`: a first reception (or the publication) in ticks >= tick-HG.
  * Rebuilt once per heartbeat (an index, not a semantic filter). */
+static int gossip_ids(const orc_net* s, const orc_msgs* m, uint32_t i, int32_t t, int64_t tick, uint32_t* out);
+
 void orc_gossip_index(const orc_net* s, orc_msgs* m, int64_t tick)
 {
     priv* p = orc_msgs_priv(m);
@@ -66,6 +68,16 @@ void orc_gossip_index(const orc_net* s, orc_msgs* m, int64_t tick)
             if (p->slot_last && p->slot_last[slot] >= lo && (int32_t)m->topic[slot] == t) p->cand[n++] = (uint32_t)slot;
     }
     p->cand_ptr[s->t] = n;
+    if (p->log_on) {                     /* every router's GetGossipIDs(topic) at this heartbeat */
+        orc_log(m, ORC_EV_HEARTBEAT, 0, 0, 0, 0, 0, tick);
+        uint32_t* ids = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(m->ring + 1));
+        for (int64_t i = 0; i < s->n; ++i)
+            for (int32_t t = 0; t < s->t; ++t) {
+                const int k = gossip_ids(s, m, (uint32_t)i, t, tick, ids);
+                for (int q = 0; q < k; ++q) orc_log(m, ORC_EV_GOSSIP_ID, (uint32_t)i, 0, ids[q], t, 0, 0);
+            }
+        free(ids);
+    }
 }
 
 /* MessageCache.GetGossipIDs(topic) of peer i at heartbeat `tick` (before
@@ -178,6 +190,7 @@ static void promise_add(priv* p, uint32_t peer, uint32_t e, uint32_t slot, uint6
 void orc_gossip_fulfill(orc_msgs* m, uint32_t peer, uint32_t slot)
 {
     priv* p = orc_msgs_priv(m);
+    orc_log(m, ORC_EV_FULFILL, peer, 0, slot, 0, 0, 0);
     if (!p->npr) return;
     const uint64_t mid = m->mid ? m->mid[slot] : slot;
     int32_t w = 0;
@@ -192,6 +205,7 @@ void orc_gossip_fulfill(orc_msgs* m, uint32_t peer, uint32_t slot)
 void orc_gossip_penalties(orc_net* s, orc_msgs* m, int64_t now)
 {
     priv* p = orc_msgs_priv(m);
+    orc_log(m, ORC_EV_PENALTIES, 0, 0, 0, 0, 0, now);
     if (!p->npr) return;
     uint32_t* broken = NULL;
     int32_t capb = 0;
@@ -215,6 +229,7 @@ void orc_gossip_penalties(orc_net* s, orc_msgs* m, int64_t now)
             int32_t r = q;
             while (r < nb && broken[r] == broken[q]) ++r;
             orc_add_penalty(s, broken[q], r - q);
+            orc_log(m, ORC_EV_BROKEN, (uint32_t)peer, s->col[broken[q]], 0, 0, 0, r - q);
             q = r;
         }
     }
@@ -313,6 +328,7 @@ void orc_gossip_ihave(orc_net* s, orc_msgs* m, int64_t g)
                 if (k < best) { best = k; pick = q; }
             }
             const uint32_t ps = want[pick].v;
+            orc_log(m, ORC_EV_PROMISE, (uint32_t)pr, i, ps, 0, g, now);
             promise_add(p, (uint32_t)pr, e, ps, m->mid ? m->mid[ps] : ps, now + gp->iwant_followup_time_ns);
             for (int q = 0; q < iask; ++q) {                         /* IWANT to i */
                 if (p->niw == p->capiw) {
@@ -348,6 +364,7 @@ void orc_gossip_iwant(orc_net* s, orc_msgs* m, int64_t g)
         if (!put_tick(s, m, slot, i, &pt) || pt < tick - gp->history_length + 1 || pt > tick) continue;
         int32_t* cnt = tx_slot(p, m->mid ? m->mid[slot] : slot, ei);
         *cnt += 1;
+        orc_log(m, ORC_EV_SERVE, i, s->col[ei], slot, 0, g, *cnt);
         if (*cnt > gp->gossip_retransmission) continue;
         if (p->ngr == p->capgr) {
             p->capgr = p->capgr ? 2 * p->capgr : 1024;

@@ -57,7 +57,12 @@ typedef struct priv {
     int64_t n_alloc, te_alloc;
     int64_t* slot_last;                 /* [ring] last round with a first reception (or the publication) */
     uint32_t* cand; int32_t* cand_ptr;  /* per-topic recent slots at the current heartbeat (CSR) */
+    int32_t log_on;                     /* event log (orc_msgs_log) */
+    orc_event* ev; int64_t nev, capev;
 } priv;
+
+/* one event, when logging is on */
+void orc_log(orc_msgs* m, int32_t kind, uint32_t a, uint32_t b, uint32_t slot, int32_t topic, int64_t g, int64_t x);
 
 priv* orc_msgs_priv(orc_msgs* m);
 int64_t orc_round_time(const orc_msgs* m, int64_t g);

@@ -94,6 +94,8 @@ def load():
             "orc_gtracer_fulfill": (None, [c_void_p, c_uint64]),
             "orc_gtracer_throttle": (None, [c_void_p, c_uint32]),
             "orc_gtracer_peer_promises": (c_int32, [c_void_p]),
+            "orc_msgs_log": (None, [POINTER(OrcMsgs), c_int32]),
+            "orc_msgs_events": (c_int64, [POINTER(OrcMsgs), c_void_p, c_int64]),
             "orc_tcache_new": (c_void_p, [c_int32, c_int64]),
             "orc_tcache_free": (None, [c_void_p]),
             "orc_tcache_add": (c_int32, [c_void_p, c_uint64, c_int64]),
@@ -213,6 +215,12 @@ UNSEEN = 0xFFFFFFFF
 ORC_BEHAVE_IGNORE_IWANT = 0x01   # oracle.h: never answers IWANT
 
 
+# oracle.h ORC_EV_*: the network oracle's event log
+EV_PUT, EV_SEEN, EV_SERVE, EV_PROMISE, EV_FULFILL, EV_BROKEN, EV_PENALTIES, EV_HEARTBEAT, EV_GOSSIP_ID = range(1, 10)
+EVENT_DTYPE = np.dtype([("kind", np.int32), ("topic", np.int32), ("a", np.uint32), ("b", np.uint32),
+                        ("g", np.int64), ("mid", np.uint64), ("x", np.int64)])
+
+
 class Msgs:
     """Oracle message ring + seen-set of a network (oracle_deliver.c)."""
 
@@ -251,6 +259,19 @@ class Msgs:
     def penalties(self, st, now):
         """applyIwantPenalties at heartbeat time now (after refresh, before scoring)."""
         load().orc_gossip_penalties(st.view(), ctypes.byref(self.m), now)
+
+    def log(self, on=True):
+        """Record the events the routers' caches and tracers observe (orc_msgs_log)."""
+        load().orc_msgs_log(ctypes.byref(self.m), 1 if on else 0)
+
+    def events(self):
+        """The events recorded since the last call (and clear them)."""
+        lib = load()
+        n = lib.orc_msgs_events(ctypes.byref(self.m), None, 0)
+        out = np.zeros(n, dtype=EVENT_DTYPE)
+        if n:
+            lib.orc_msgs_events(ctypes.byref(self.m), out.ctypes.data_as(c_void_p), n)
+        return out
 
     def __del__(self):
         try:
