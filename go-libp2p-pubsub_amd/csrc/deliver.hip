@@ -74,6 +74,7 @@ struct Deliver {
     uint64_t* d_cell = nullptr;        // [ring][N] seen-set cells (layout above)
     uint64_t* d_seenbm = nullptr;      // [ring][ceil(N/64)] bit: the cell is committed (a cache of the cells)
     uint64_t* d_fresh = nullptr;       // [ring][ceil(N/64)] bit: the peer forwards the slot's message next round
+    uint64_t* d_fsum = nullptr;        // [ring][ceil(N/4096)] bit: that fresh word may be non-zero
     bool fresh_on = false;             // the topic-major delivery (and so the fresh bits) is in use
     int32_t* d_mpub = nullptr;         // [ring] round the slot's message was published in
     int64_t* d_roff = nullptr;         // [rounds] offset of each round in its heartbeat
@@ -122,7 +123,9 @@ struct RoundArgs {
     uint64_t* cell;
     uint64_t* seenbm;          // [ring][nw] committed bits of the cells (read before a cell)
     uint64_t* fresh;           // [ring][nw] forwarders of the next round (topic-major delivery; nullptr otherwise)
+    uint64_t* fsum;            // [ring][nsw] summary: bit j of word s = fresh word 64 s + j may be non-zero
     int64_t nw;                // words per slot
+    int64_t nsw;               // summary words per slot
     int32_t* mpub;             // [ring] publication round
     const int64_t* roff;       // [R] (r + 1) * hb / (R + 1): offset of round r in its heartbeat
     int32_t* lastput;
@@ -248,6 +251,16 @@ __device__ __forceinline__ bool is_claim_of(uint64_t c, uint32_t parity)
     return c != kUnseen64 && (hi & kClaim) && ((hi >> 30) & 1u) == parity;
 }
 
+// Mark fresh bits of word w of slot m (and the word in the summary).
+__device__ __forceinline__ void fresh_set(const RoundArgs& a, uint32_t m, int64_t w, uint64_t bits)
+{
+    atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + w), bits);
+    uint64_t* sp = a.fsum + (int64_t)m * a.nsw + (w >> 6);
+    const uint64_t sb = 1ull << (w & 63);
+    if (!(__hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & sb))
+        atomicOr(reinterpret_cast<unsigned long long*>(sp), sb);
+}
+
 // Reset the rows of the slots being published into; a claim still pending
 // there (its message was propagating) is committed first.
 __global__ void k_reset_slots(RoundArgs a, const gsim_msg* pub, int32_t count)
@@ -268,6 +281,7 @@ __global__ void k_reset_slots(RoundArgs a, const gsim_msg* pub, int32_t count)
         if ((i & 63) == 0) {
             a.seenbm[(int64_t)m * a.nw + (i >> 6)] = 0;
             if (a.fresh) a.fresh[(int64_t)m * a.nw + (i >> 6)] = 0;
+            if (a.fresh && (i & 4095) == 0) a.fsum[(int64_t)m * a.nsw + (i >> 12)] = 0;
         }
     }
 }
@@ -286,8 +300,7 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, int32_t count)
         const uint32_t oc = p.origin - a.clo;
         a.cell[(int64_t)slot * a.CN + oc] = ((uint64_t)(uint32_t)a.g << 32) | p.origin;
         atomicOr(reinterpret_cast<unsigned long long*>(a.seenbm + (int64_t)slot * a.nw + (oc >> 6)), 1ull << (oc & 63));
-        if (a.fresh)   // the origin publishes whatever the verdict
-            atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)slot * a.nw + (oc >> 6)), 1ull << (oc & 63));
+        if (a.fresh) fresh_set(a, slot, oc >> 6, 1ull << (oc & 63));   // the origin publishes whatever the verdict
         int32_t* lp = a.lastput + (int64_t)p.topic * a.N + p.origin;
         const int32_t tick = (int32_t)(a.g / a.R);
         if (*lp < tick) *lp = tick;
@@ -644,7 +657,13 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
         // copy k_commit committed, the publication, a ghost's import), cleared
         // as they are read; only those peers' cells and rows are loaded
         uint64_t* fresh_m = a.fresh + (int64_t)m * a.nw;
+        uint64_t* fsum_m = a.fsum + (int64_t)m * a.nsw;
         for (int64_t c0 = lo; c0 < hi; c0 += kTmChunk) {
+            // the chunk's 32 fresh words in the summary (ranges start on whole
+            // chunks): a chunk with none is skipped without touching them
+            const int64_t cw0 = (c0 - clo) >> 6;
+            const uint64_t cbits = (fsum_m[cw0 >> 6] >> (cw0 & 63)) & 0xFFFFFFFFull;
+            if (!cbits) continue;                                // block-uniform
             // thread tid: peers x0, x0 + 1 of the chunk (ranges start on whole
             // words; 32 threads share a word)
             const int64_t x0 = c0 + 2 * (int64_t)tid;
@@ -700,6 +719,8 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
                 }
                 // the bits are read: clear them (one thread per nonzero word)
                 if (word && ((x0 - clo) & 63) == 0) fresh_m[(x0 - clo) >> 6] = 0;
+                if (tid == 0)
+                    atomicAnd(reinterpret_cast<unsigned long long*>(fsum_m + (cw0 >> 6)), ~(0xFFFFFFFFull << (cw0 & 63)));
             }
             __syncthreads();
             const int nf = s_nf;
@@ -872,8 +893,12 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
                 const uint32_t m = s_act[k];
                 a.seenbm[(int64_t)m * a.nw + (i0 >> 6)] |= cb;
                 // receivers forward what they accepted, in the next round
-                if (a.fresh && a.minv[m] == GSIM_VERDICT_ACCEPT)
+                if (a.fresh && a.minv[m] == GSIM_VERDICT_ACCEPT) {
+                    // fire-and-forget atomics: the wave does not wait on them
                     atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (i0 >> 6)), cb);
+                    atomicOr(reinterpret_cast<unsigned long long*>(a.fsum + (int64_t)m * a.nsw + (i0 >> 12)),
+                             1ull << ((i0 >> 6) & 63));
+                }
             }
         }
 #pragma unroll
@@ -1372,7 +1397,7 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_pair_cnt); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
@@ -1423,6 +1448,8 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.rhi = (uint32_t)h->ohi();
     a.seenbm = d->d_seenbm; a.nw = (a.CN + 63) / 64; a.mpub = d->d_mpub; a.roff = d->d_roff;
     a.fresh = d->fresh_on ? d->d_fresh : nullptr;
+    a.fsum = d->d_fsum;
+    a.nsw = (a.nw + 63) / 64;
     const size_t w = (size_t)nnew_words(d);
     a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
     a.nnew_cur = d->d_nnew + (size_t)(g & 1) * w;
@@ -1660,9 +1687,13 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a, size_t lds)
     // at least 4096 peers
     constexpr int64_t total = 2048;
     const int64_t cn = h->n;                 // every local peer sends (a shard's ghosts too)
+    // at least 256 ranges per topic (when the peers allow): with skewed topics
+    // (Zipf subscriptions) the busy topics' blocks must still fill the chip;
+    // blocks of idle topics leave after the slot scan
     const int64_t ranges = std::max<int64_t>(1, std::min<int64_t>((cn + 4095) / 4096,
-                                                                    std::max<int64_t>(1, total / std::max(1, h->t))));
-    const int32_t range = (int32_t)(((cn + ranges - 1) / ranges + 63) & ~63ll);
+                                                                    std::max<int64_t>(h->t >= 32 ? 256 : 1,
+                                                                                      total / std::max(1, h->t))));
+    const int32_t range = (int32_t)(((cn + ranges - 1) / ranges + kTmChunk - 1) / kTmChunk * kTmChunk);
     const int64_t p = (cn + range - 1) / range;
     // the committed bits are staged in LDS while they fit, else read from HBM
     const int32_t stage = (lds <= kLdsBudget && h->tm_stage != 0) ? 1 : 0;
@@ -1921,7 +1952,7 @@ __global__ __launch_bounds__(256) void k_frontier_import(RoundArgs a, const uint
             uint64_t bit = same ? 1ull << (l & 63) : 0ull;
             for (int o = 32; o; o >>= 1) bit |= (uint64_t)__shfl_xor((long long)bit, o, 64);
             if (lane == leader) {
-                atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + k0), bit);
+                fresh_set(a, (uint32_t)(k0 / (uint64_t)a.nw), (int64_t)(k0 % (uint64_t)a.nw), bit);
                 // the slot's activity (one 0 -> 1 transition per round)
                 const uint32_t ms = (uint32_t)(k0 / (uint64_t)a.nw);
                 uint32_t* nw = const_cast<uint32_t*>(a.nnew_prev) + (ms >> 5);
@@ -1976,6 +2007,8 @@ int deliver_variant_changed(gsim_handle* h)
         }
         const size_t bytes = (size_t)d->cfg.ring * (size_t)((h->n + 63) / 64) * 8;
         hipError_t e = hipMemsetAsync(d->d_fresh, 0, bytes, h->stream);
+        if (e == hipSuccess)
+            e = hipMemsetAsync(d->d_fsum, 0, (size_t)d->cfg.ring * (size_t)(((h->n + 63) / 64 + 63) / 64) * 8, h->stream);
         if (e != hipSuccess) return hip_check(h, e, "fresh bits");
         d->fresh_on = on;
     }
@@ -2017,6 +2050,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_cell, ring * CN * 8);
     A((void**)&d->d_seenbm, ring * ((CN + 63) / 64) * 8);
     A((void**)&d->d_fresh, ring * ((CN + 63) / 64) * 8);
+    A((void**)&d->d_fsum, ring * (((CN + 63) / 64 + 63) / 64) * 8);
     A((void**)&d->d_mpub, ring * 4);
     A((void**)&d->d_roff, (size_t)cfg->rounds * 8);
     A((void**)&d->d_lastput, T * N * 4);
@@ -2052,6 +2086,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     e = hipMemsetAsync(d->d_cell, 0xFF, ring * CN * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_seenbm, 0, ring * ((CN + 63) / 64) * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_fresh, 0, ring * ((CN + 63) / 64) * 8, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_fsum, 0, ring * (((CN + 63) / 64 + 63) / 64) * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_mpub, 0, ring * 4, h->stream);
     if (e == hipSuccess) {
         std::vector<int64_t> roff((size_t)cfg->rounds);

@@ -219,7 +219,7 @@ def test_iwant_response_queue_overflow_is_reported(require_gpu):
     eng.close()
 
 
-def _gossip_window_run(max_ihave_length, ring=256, n=1200, T=8, rate=10, ticks=5):
+def _gossip_window_run(max_ihave_length, ring=1024, n=1200, T=8, rate=10, ticks=5):
     """Every topic busy: several messages per topic in each gossip window."""
     from fixtures import beacon_params, synthetic_state
     from gsim.engine import Engine, random_regular
@@ -244,7 +244,7 @@ def test_ring_larger_than_max_ihave_length_bit_exact(require_gpu):
     oracle, which implements the truncations."""
     from tickrun import run_parity
     net, params, th, gp, st, sched = _gossip_window_run(max_ihave_length=60)
-    msgs, gs = run_parity(net, params, th, gp, st, list(range(1, 6)), sched, ring=256)
+    msgs, gs = run_parity(net, params, th, gp, st, list(range(1, 6)), sched, ring=1024)
     assert gs["iwant_ids"] > 0
 
 
@@ -260,7 +260,7 @@ def test_topic_window_over_max_ihave_length_is_reported(require_gpu):
         eng.load_graph(net)
         eng.set_seed(SEED)
         st.push_to_engine(eng)
-        eng.msgs_init(256, R, T0, Second)
+        eng.msgs_init(1024, R, T0, Second)
         with pytest.raises(GsimError) as ei:
             for kk in range(1, 6):
                 eng.refresh_scores(tick_time(kk))
