@@ -75,6 +75,8 @@ struct Deliver {
     uint64_t* d_seenbm = nullptr;      // [ring][ceil(N/64)] bit: the cell is committed (a cache of the cells)
     uint64_t* d_fresh = nullptr;       // [ring][ceil(N/64)] bit: the peer forwards the slot's message next round
     uint64_t* d_fsum = nullptr;        // [ring][ceil(N/4096)] bit: that fresh word may be non-zero
+    uint64_t* d_mmask = nullptr;       // [T][N] mesh | direct positions of rows <= 64 (RoundArgs::mmask)
+    uint64_t mask_version = 0;         // h->mesh_version the masks were built for
     bool fresh_on = false;             // the topic-major delivery (and so the fresh bits) is in use
     int32_t* d_mpub = nullptr;         // [ring] round the slot's message was published in
     int64_t* d_roff = nullptr;         // [rounds] offset of each round in its heartbeat
@@ -155,6 +157,10 @@ struct RoundArgs {
     // sharded: the edges of each row into owned peers (the copies this shard
     // delivers), a CSR of edge indices: row x's are sedge[sptr[x] .. sptr[x+1])
     const uint32_t *sptr, *sedge;
+    // [T][n] rows of at most 64 connections: bit q = row position q is a mesh or
+    // direct edge (to an owned peer); a forwarder other than the origin sends
+    // on no other edge, so only these are walked
+    const uint64_t* mmask;
 };
 
 __device__ __forceinline__ int64_t round_time(const RoundArgs& a, int64_t g)
@@ -575,6 +581,43 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
     }
 }
 
+// Position of the k-th set bit (k < popcount) of m.
+__device__ __forceinline__ uint32_t kth_bit(uint64_t m, uint32_t k)
+{
+    uint32_t pos = 0;
+#pragma unroll
+    for (int w = 32; w; w >>= 1) {
+        const uint64_t lo = m & ((1ull << w) - 1);
+        const uint32_t c = (uint32_t)__popcll(lo);
+        if (k >= c) { k -= c; m >>= w; pos += (uint32_t)w; } else { m = lo; }
+    }
+    return pos;
+}
+
+// The mesh masks of rows of at most 64 connections: bit q of mmask[t][x] =
+// position q of row x carries the router's mesh bit for t, or is a direct
+// peer; only edges to the receivers [rlo, rhi) (a shard's owned peers).
+__global__ __launch_bounds__(256) void k_mesh_mask(const uint32_t* row_ptr, const uint32_t* col, const uint8_t* mflags,
+                                                   const uint8_t* direct, int64_t n, int64_t E, int32_t T,
+                                                   uint32_t rlo, uint32_t rhi, uint64_t* mmask)
+{
+    // one wave per row, lane = row position: coalesced flag planes, one ballot per topic
+    const int lane = threadIdx.x & 63;
+    for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += (int64_t)gridDim.x * 4) {
+        const uint32_t b = row_ptr[r], d = row_ptr[r + 1] - b;
+        const bool v = d <= 64 && (uint32_t)lane < d;
+        const uint32_t e = b + (uint32_t)lane;
+        const uint32_t i = v ? col[e] : 0u;
+        const bool own = v && i >= rlo && i < rhi;
+        const bool dir = own && direct && direct[e];
+        for (int32_t t = 0; t < T; ++t) {
+            const bool me = own && (dir || (mflags[(int64_t)t * E + e] & GSIM_TF_MESH));
+            const uint64_t m = __ballot(me);
+            if (lane == 0) mmask[(int64_t)t * n + r] = m;
+        }
+    }
+}
+
 // Delivery round g, topic-major.  Block (p, t) walks the
 // frontier senders of peer range p for every active slot of topic t: the
 // slot's committed bits are staged in LDS first, so the duplicate test of a
@@ -591,10 +634,11 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
 // edge (binary search for the edge's sender), so rows of any length keep
 // every lane busy — a shard's short rows (owned rows cut to their owned
 // receivers, ghost rows) as much as power-law hubs.
-constexpr int kTmThreads = 1024;
-constexpr int kTmChunk = 2048;      // peers scanned per frontier chunk
 
-template <int W>   // 0: one thread per edge; 16 / 32 / 64: W lanes per row
+// W: 0 one thread per edge; 16 / 32 / 64: W lanes per row.  kTmThreads: the
+// block (1024 with the committed bits in LDS: one block per CU anyway; 512
+// reading them from HBM: three blocks per CU).
+template <int W, int kTmThreads>
 __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t range, int32_t stage)
 {
     // [nws] committed bits of the receivers' words (stage: more receivers than
@@ -602,10 +646,14 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
     extern __shared__ uint64_t s_dyn[];
     const int64_t wlo = (int64_t)a.rlo >> 6, nws = (((int64_t)a.rhi + 63) >> 6) - wlo;
     uint16_t* s_slots = reinterpret_cast<uint16_t*>(s_dyn + (stage ? nws : 0));
+    constexpr int kTmChunk = 2 * kTmThreads;                 // peers per frontier chunk (two per thread)
+    constexpr int kWv = kTmThreads / 64;                     // waves per block
+    constexpr uint64_t kChunkWords = (1ull << (kTmChunk / 64)) - 1;
     __shared__ uint32_t s_front[kTmChunk];                   // frontier senders
     __shared__ uint32_t s_from[kTmChunk];                    // their first senders
-    __shared__ uint32_t s_off[kTmChunk];                     // first flattened edge of each sender
-    __shared__ uint32_t s_dlt[kTmChunk];                     // its row's first edge - s_off (mod 2^32)
+    __shared__ uint32_t s_off[kTmChunk];                     // first flattened edge of each sender (rows: its length)
+    __shared__ uint32_t s_beg[kTmChunk];                     // its row's first edge (sedge: first entry)
+    __shared__ uint64_t s_msk[kTmChunk];                     // its mesh mask (0: the whole row)
     __shared__ uint32_t s_wsum[64];                          // per-wave sums and their prefixes
     __shared__ int s_ns, s_nf, s_claimed;
     __shared__ uint32_t s_ne;
@@ -662,7 +710,7 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
             // the chunk's 32 fresh words in the summary (ranges start on whole
             // chunks): a chunk with none is skipped without touching them
             const int64_t cw0 = (c0 - clo) >> 6;
-            const uint64_t cbits = (fsum_m[cw0 >> 6] >> (cw0 & 63)) & 0xFFFFFFFFull;
+            const uint64_t cbits = (fsum_m[cw0 >> 6] >> (cw0 & 63)) & kChunkWords;
             if (!cbits) continue;                                // block-uniform
             // thread tid: peers x0, x0 + 1 of the chunk (ranges start on whole
             // words; 32 threads share a word)
@@ -674,14 +722,25 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
                 fb = (uint32_t)(word >> ((x0 - clo) & 63)) & (x0 + 1 < hi ? 3u : 1u);
             }
             uint32_t len2[2] = {0, 0}, beg2[2] = {0, 0}, from2[2] = {0, 0};
+            uint64_t msk2[2] = {0, 0};
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 if ((fb >> u) & 1u) {
                     const uint32_t x = (uint32_t)(x0 + u);
                     from2[u] = (uint32_t)a.cell[row_m + (x - clo)] & kPeerMask;
-                    const uint32_t* rp = a.sptr ? a.sptr : a.row_ptr;
-                    beg2[u] = rp[x];
-                    len2[u] = rp[x + 1] - beg2[u];
+                    const uint32_t rb = a.row_ptr[x], deg = a.row_ptr[x + 1] - rb;
+                    if (deg <= 64 && x != origin) {
+                        // a forwarder sends on its mesh (and direct) edges only
+                        msk2[u] = a.mmask[(int64_t)t * a.N + x];
+                        beg2[u] = rb;
+                        len2[u] = (uint32_t)__popcll(msk2[u]);
+                        if (!msk2[u]) len2[u] = 0;
+                    } else {
+                        // the origin (fanout / flood publish) and hubs: the whole row
+                        const uint32_t* rp = a.sptr ? a.sptr : a.row_ptr;
+                        beg2[u] = rp[x];
+                        len2[u] = rp[x + 1] - beg2[u];
+                    }
                 }
             }
             // block scan of (forwarders, edges): the frontier in peer order
@@ -693,14 +752,14 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
             if (lane == 63) { s_wsum[wid] = vc; s_wsum[16 + wid] = ve; }
             __syncthreads();
             if (tid < 64) {
-                const uint32_t c = tid < 16 ? s_wsum[tid] : 0u, e = tid < 16 ? s_wsum[16 + tid] : 0u;
+                const uint32_t c = tid < kWv ? s_wsum[tid] : 0u, e = tid < kWv ? s_wsum[16 + tid] : 0u;
                 uint32_t ic = c, ie = e;
-                for (int o = 1; o < 16; o <<= 1) {
+                for (int o = 1; o < kWv; o <<= 1) {
                     const uint32_t yc = (uint32_t)__shfl_up((int)ic, o, 64), ye = (uint32_t)__shfl_up((int)ie, o, 64);
                     if (lane >= o) { ic += yc; ie += ye; }
                 }
-                if (tid < 16) { s_wsum[32 + tid] = ic - c; s_wsum[48 + tid] = ie - e; }
-                if (tid == 15) { s_nf = (int)ic; s_ne = ie; }
+                if (tid < kWv) { s_wsum[32 + tid] = ic - c; s_wsum[48 + tid] = ie - e; }
+                if (tid == kWv - 1) { s_nf = (int)ic; s_ne = ie; }
             }
             __syncthreads();
             {
@@ -711,8 +770,9 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
                     if ((fb >> u) & 1u) {
                         s_front[q] = (uint32_t)(x0 + u);
                         s_from[q] = from2[u];
-                        if (W == 0) { s_off[q] = off; s_dlt[q] = beg2[u] - off; }
-                        else { s_off[q] = len2[u]; s_dlt[q] = beg2[u]; }
+                        s_off[q] = W == 0 ? off : len2[u];
+                        s_beg[q] = beg2[u];
+                        s_msk[q] = msk2[u];
                         ++q;
                         off += len2[u];
                     }
@@ -720,7 +780,7 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
                 // the bits are read: clear them (one thread per nonzero word)
                 if (word && ((x0 - clo) & 63) == 0) fresh_m[(x0 - clo) >> 6] = 0;
                 if (tid == 0)
-                    atomicAnd(reinterpret_cast<unsigned long long*>(fsum_m + (cw0 >> 6)), ~(0xFFFFFFFFull << (cw0 & 63)));
+                    atomicAnd(reinterpret_cast<unsigned long long*>(fsum_m + (cw0 >> 6)), ~(kChunkWords << (cw0 & 63)));
             }
             __syncthreads();
             const int nf = s_nf;
@@ -762,8 +822,13 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
                     }
                     jv[u] = vv[u] ? s_front[q] : 0u;
                     fv[u] = vv[u] ? s_from[q] : 0u;
-                    ev[u] = fi + s_dlt[q];
-                    if (a.sedge && vv[u]) ev[u] = a.sedge[ev[u]];
+                    // the k-th edge of the sender: k-th mesh position, or the
+                    // k-th edge of the whole row (through sedge on a shard)
+                    const uint32_t k = W == 0 ? fi - s_off[q] : fi;
+                    const uint64_t msk = s_msk[q];
+                    if (msk) ev[u] = s_beg[q] + kth_bit(msk, k);
+                    else if (a.sedge && vv[u]) ev[u] = a.sedge[s_beg[q] + k];
+                    else ev[u] = s_beg[q] + k;
                 }
 #pragma unroll
                 for (int u = 0; u < P; ++u) {
@@ -1397,7 +1462,7 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_pair_cnt); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
@@ -1449,6 +1514,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.seenbm = d->d_seenbm; a.nw = (a.CN + 63) / 64; a.mpub = d->d_mpub; a.roff = d->d_roff;
     a.fresh = d->fresh_on ? d->d_fresh : nullptr;
     a.fsum = d->d_fsum;
+    a.mmask = d->d_mmask;
     a.nsw = (a.nw + 63) / 64;
     const size_t w = (size_t)nnew_words(d);
     a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
@@ -1675,35 +1741,43 @@ int deliver_read_seen(gsim_handle* h, void* dst)
     return hip_check(h, e, "gsim_read_field(SEEN)");
 }
 
-constexpr size_t kLdsBudget = 160 * 1024 - 33 * 1024;   // minus the static frontier buffers
-
-template <int W>
-static int launch_send_tm(gsim_handle* h, const RoundArgs& a, size_t lds)
+template <int W, int TB>
+static int launch_send_tm_tb(gsim_handle* h, const RoundArgs& a, size_t lds, int32_t stage)
 {
     // blocks per topic: about 2048 blocks in all (8 per CU over the launch at one
     // resident block per CU: smaller ranges even out the frontier work; measured
     // 512 / 1024 / 1536 / 2048 / 3072 / 4096 blocks: 30.5 / 22.7 / 21.4 / 20.9 /
     // 21.1 / 21.3 ms per tick at C3, profiles/r01_ab_send_tm_blocks.log), ranges of
-    // at least 4096 peers
+    // at least 4096 peers; at least 256 ranges per topic when there are many
+    // topics (Zipf subscriptions skew them: the busy topics' blocks must still
+    // fill the chip; blocks of idle topics leave after the slot scan)
     constexpr int64_t total = 2048;
+    constexpr int64_t chunk = 2 * TB;
     const int64_t cn = h->n;                 // every local peer sends (a shard's ghosts too)
-    // at least 256 ranges per topic (when the peers allow): with skewed topics
-    // (Zipf subscriptions) the busy topics' blocks must still fill the chip;
-    // blocks of idle topics leave after the slot scan
     const int64_t ranges = std::max<int64_t>(1, std::min<int64_t>((cn + 4095) / 4096,
                                                                     std::max<int64_t>(h->t >= 32 ? 256 : 1,
                                                                                       total / std::max(1, h->t))));
-    const int32_t range = (int32_t)(((cn + ranges - 1) / ranges + kTmChunk - 1) / kTmChunk * kTmChunk);
+    const int32_t range = (int32_t)(((cn + ranges - 1) / ranges + chunk - 1) / chunk * chunk);
     const int64_t p = (cn + range - 1) / range;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_send_tm<W, TB>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return hip_check(h, e, "k_send_tm LDS attribute");
+    hipLaunchKernelGGL((k_send_tm<W, TB>), dim3((uint32_t)p, (uint32_t)std::max(1, h->t)), dim3(TB), lds, h->stream,
+                       a, range, stage);
+    return hip_check(h, hipGetLastError(), "k_send_tm");
+}
+
+constexpr size_t kLdsBudget = 160 * 1024 - 50 * 1024;   // minus the static frontier buffers
+
+template <int W>
+static int launch_send_tm(gsim_handle* h, const RoundArgs& a, size_t lds)
+{
     // the committed bits are staged in LDS while they fit, else read from HBM
     const int32_t stage = (lds <= kLdsBudget && h->tm_stage != 0) ? 1 : 0;
     if (!stage) lds = ((size_t)h->dl->cfg.ring * 2 + 7) & ~(size_t)7;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_send_tm<W>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return hip_check(h, e, "k_send_tm LDS attribute");
-    hipLaunchKernelGGL(k_send_tm<W>, dim3((uint32_t)p, (uint32_t)std::max(1, h->t)), dim3(kTmThreads), lds, h->stream,
-                       a, range, stage);
-    return hip_check(h, hipGetLastError(), "k_send_tm");
+    // 1024-thread blocks either way (512 with the bits in HBM: c5 43 against 30
+    // ms of delivery per tick)
+    return launch_send_tm_tb<W, 1024>(h, a, lds, stage);
 }
 
 // LDS of the topic-major kernel: the slot's committed bits + the slot list
@@ -1776,14 +1850,22 @@ int deliver_round_send(gsim_handle* h, int64_t round)
         ProfScope ps(h, GSIM_K_SEND);
         const int grid = grid_peers(h->n);
         if (d->fresh_on) {
+            if (d->mask_version != h->mesh_version) {
+                // the router's mesh / direct flags changed: rebuild the masks
+                hipLaunchKernelGGL(k_mesh_mask, dim3((uint32_t)std::min<int64_t>((h->n + 3) / 4, 65536)), dim3(256), 0,
+                                   h->stream, (const uint32_t*)h->d_row_ptr, (const uint32_t*)h->d_col,
+                                   (const uint8_t*)h->d_mflags, (const uint8_t*)h->d_direct, h->n, h->e,
+                                   std::max(1, h->t), (uint32_t)h->olo(), (uint32_t)h->ohi(), d->d_mmask);
+                d->mask_version = h->mesh_version;
+            }
             const size_t lds_tm = send_tm_lds(h, d);
-            // W lanes per row while rows fill them (mean >= 3/4 of W), one
-            // thread per edge otherwise (short or skewed rows, a shard's rows)
+            // one thread per edge by default: forwarders walk only their mesh
+            // edges (a handful of a row's positions), so lane groups per row
+            // would idle most lanes (C3: 21.0 against 32.9 ms per tick,
+            // profiles/r02_ab_walk_masks.log); lane groups on request
             const int64_t dmax = h->sh ? h->sh->send_max : h->max_degree;
-            const int64_t esend = h->sh ? h->sh->send_edges : h->e;
             const int Wr = dmax <= 16 ? 16 : dmax <= 32 ? 32 : dmax <= 64 ? 64 : 0;
-            const bool flat = Wr == 0 || esend * 4 < (int64_t)Wr * 3 * std::max<int64_t>(1, h->n);
-            if (Wr == 0 || (h->send_variant_flat >= 0 ? h->send_variant_flat == 1 : flat))
+            if (Wr == 0 || h->send_variant_flat != 0)
                 rc = launch_send_tm<0>(h, a, lds_tm);
             else if (Wr == 16)
                 rc = launch_send_tm<16>(h, a, lds_tm);
@@ -2051,6 +2133,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_seenbm, ring * ((CN + 63) / 64) * 8);
     A((void**)&d->d_fresh, ring * ((CN + 63) / 64) * 8);
     A((void**)&d->d_fsum, ring * (((CN + 63) / 64 + 63) / 64) * 8);
+    A((void**)&d->d_mmask, T * N * 8);
     A((void**)&d->d_mpub, ring * 4);
     A((void**)&d->d_roff, (size_t)cfg->rounds * 8);
     A((void**)&d->d_lastput, T * N * 4);

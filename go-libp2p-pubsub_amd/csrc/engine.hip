@@ -898,6 +898,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
                        (uint8_t)(GSIM_ES_TRACKED | GSIM_ES_CONNECTED));
     hipLaunchKernelGGL(k_fill_u8, dim3(grid_for(E)), dim3(256), 0, s, h->d_rstate, E, (uint8_t)GSIM_ES_CONNECTED);
     h->score_version++;
+    h->mesh_version++;
     h->has_white = false;
     h->p6_dirty = true;
     h->maybe_retained = false;
@@ -926,7 +927,8 @@ int gsim_set_direct_peers(gsim_handle* h, const uint8_t* direct)
     hipError_t e = direct ? hipMemcpyAsync(h->d_direct, direct, (size_t)h->e, hipMemcpyHostToDevice, h->stream)
                           : hipMemsetAsync(h->d_direct, 0, (size_t)h->e, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-    h->score_version++;          // AcceptFrom and the send sets read the flags through the delivery state
+    h->score_version++;
+    h->mesh_version++;          // AcceptFrom and the send sets read the flags through the delivery state
     return hip_check(h, e, "gsim_set_direct_peers");
 }
 
@@ -1038,6 +1040,7 @@ int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now, double p_mes
     hipLaunchKernelGGL(k_fill_synthetic, dim3(grid_for(h->e)), dim3(256), 0, h->stream, a, seed, p_mesh);
     h->p6_dirty = true;
     h->score_version++;
+    h->mesh_version++;
     h->maybe_retained = false;
     h->unjoined_zero = true;     // the fill leaves records of unshared topics zero
     hipError_t e = hipGetLastError();
@@ -1148,8 +1151,11 @@ int gsim_write_field(gsim_handle* h, int32_t f, const void* src, size_t bytes)
     rc = write_field_impl(h, r, src);
     h->unjoined_zero = false;    // arbitrary state: no record may be skipped
     if (!rc) rc = extra_field_written(h, f);
-    if (f == GSIM_F_ESTATE) { h->p6_dirty = true; h->maybe_retained = true; h->score_version++; }
+    if (f == GSIM_F_ESTATE) { h->p6_dirty = true; h->maybe_retained = true; h->score_version++;
+    h->mesh_version++; }
     if (f == GSIM_F_SCORE) h->score_version++;
+    h->mesh_version++;          // router flags may have changed (delivery's mesh masks)
+    h->mesh_version++;
     return rc;
 }
 

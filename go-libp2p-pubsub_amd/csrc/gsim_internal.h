@@ -246,6 +246,7 @@ struct gsim_handle {
     uint8_t* d_pen = nullptr;         // pending broken-promise penalties (applyIwantPenalties), record order
     uint8_t* d_dstate = nullptr;      // delivery state per edge, derived (GSIM_DS_*)
     uint64_t score_version = 1, acc_version = 0;
+    uint64_t mesh_version = 1;   // router mesh / direct flags changed (delivery rebuilds its mesh masks)
 
     // per-kernel-class device timing (gsim_profile); events are pooled
     struct ProfMark { int32_t cls; uint32_t a, b; };

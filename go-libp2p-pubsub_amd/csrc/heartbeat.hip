@@ -1421,6 +1421,7 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     if (rc) return rc;
     // heartbeat output goes to the parity-0 inbox, read by control round 0
     HbArgs a = make_hb_args(h, tick, now, 1);
+    h->mesh_version++;
     ProfScope ps(h, GSIM_K_HEARTBEAT);
     // observers in lane groups sized to their rows: 4 per wavefront for rows
     // of <= 16 connections, 2 for <= 32, 1 otherwise (observers are
@@ -1468,6 +1469,7 @@ int handle_control(gsim_handle* h, int32_t round, int64_t now)
 {
     HbArgs a = make_hb_args(h, 0, now, round & 1);
     ProfScope ps(h, GSIM_K_CONTROL);
+    h->mesh_version++;
     hipLaunchKernelGGL(k_handle_control, dim3(grid_rows(h->ohi() - h->olo())), dim3(256), 0, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_handle_control");
 }
@@ -1588,7 +1590,8 @@ int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, i
     }
     h->p6_dirty = true;          // the tracked set (and so the IP sets) changed
     if (!up) h->maybe_retained = true;
-    h->score_version++;          // connected / tracked bits feed the delivery state
+    h->score_version++;
+    h->mesh_version++;          // connected / tracked bits feed the delivery state
     return GSIM_OK;
 }
 

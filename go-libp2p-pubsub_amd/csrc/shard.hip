@@ -663,7 +663,8 @@ int exchange_router(gsim_group* g)
                                (const uint8_t*)s->d_rflag_in, h->d_mflags, h->d_rstate, h->d_direct, s->d_pgate,
                                h->t, h->e, s->own_e_lo, s->own_e_hi);
         if (hipGetLastError() != hipSuccess) return g->fail(GSIM_EDEVICE, "k_router_import");
-        h->score_version++;    // ghost rows' connected / direct bits feed the delivery state
+        h->score_version++;
+        h->mesh_version++;    // ghost rows' connected / direct bits feed the delivery state
     }
     g->router_dirty = false;
     return GSIM_OK;

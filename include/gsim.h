@@ -440,9 +440,9 @@ int gsim_profile_read(gsim_handle* h, double* ms, int64_t* launches, int32_t n);
  * with the slots' committed bits staged in LDS (used while they fit), 0 is
  * the peer-major k_send.  which = 3: the IHAVE walk's lane group width
  * (16, 32 or 64 lanes per row; 0 = chosen from the row lengths).  which = 4:
- * the topic-major walk over a round's forwarders: 1 = one thread per edge
- * (rows flattened), 2 = a lane group per row, 0 (default) = chosen from the
- * row lengths.  which = 5: the topic-major kernel's committed bits: 0
+ * the topic-major walk over a round's forwarders: 1 (default, also 0) = one
+ * thread per edge (the forwarders' mesh edges flattened), 2 = a lane group
+ * per row.  which = 5: the topic-major kernel's committed bits: 0
  * (default) staged in LDS while a slot's bits fit (<= ~10^6 receivers), 1
  * always read from HBM. */
 int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant);
