@@ -2,7 +2,7 @@
 """A/B timing of kernel variants (gsim_set_kernel_variant(h, which, v)) on the
 C3 workload.  Results are identical across variants; each arm runs whole ticks
 and the per-tick kernel times are compared.  Arms are interleaved.
-usage: python tools/ab_variants.py --which 2 --variants 0,1,2 [--rounds 3] [--ticks 2]
+usage: python tools/ab_variants.py --which 4 --variants 1,2 [--rounds 3] [--ticks 2]
 """
 import argparse
 import json
