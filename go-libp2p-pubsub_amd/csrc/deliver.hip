@@ -1542,6 +1542,7 @@ bool deliver_gossip_view(gsim_handle* h, GossipView* v)
     v->lastput = d->d_lastput;
     v->gsel = d->d_gsel;
     v->gstate = d->d_gstate;
+    v->mmask = d->d_mmask;
     return true;
 }
 
@@ -1851,7 +1852,10 @@ int deliver_round_send(gsim_handle* h, int64_t round)
         const int grid = grid_peers(h->n);
         if (d->fresh_on) {
             if (d->mask_version != h->mesh_version) {
-                // the router's mesh / direct flags changed: rebuild the masks
+                // the masks are kept current by the heartbeat, the control pass
+                // and a shard's router import; other writers of the router's
+                // flags (ABI writes, direct peers, the device fill) bump the
+                // version: rebuild them all
                 hipLaunchKernelGGL(k_mesh_mask, dim3((uint32_t)std::min<int64_t>((h->n + 3) / 4, 65536)), dim3(256), 0,
                                    h->stream, (const uint32_t*)h->d_row_ptr, (const uint32_t*)h->d_col,
                                    (const uint8_t*)h->d_mflags, (const uint8_t*)h->d_direct, h->n, h->e,

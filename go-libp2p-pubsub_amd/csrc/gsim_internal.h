@@ -311,6 +311,7 @@ struct GossipView {
     const int32_t* lastput;   // [T][N] tick of the newest mcache.Put
     uint8_t* gsel;            // [T][E] sender edge order: emitGossip chose col[e] this heartbeat
     uint8_t* gstate;          // [E] edge order: owner's snapshot score of col >= gossipThreshold
+    uint64_t* mmask;          // [T][N] delivery's mesh masks (rows <= 64), kept current by the router kernels
 };
 bool deliver_gossip_view(gsim_handle* h, GossipView* v);   // false before gsim_msgs_init
 int deliver_promise_check(gsim_handle* h, int64_t now);    // broken promises -> pending P7

@@ -81,6 +81,7 @@ struct HbArgs {
     // this shard's; selection keys use global peer ids (gid, nullptr: local = global)
     const uint32_t* gid;
     uint32_t olo, ohi;
+    uint64_t* mmask;           // [T][N] delivery's mesh masks (nullptr before gsim_msgs_init)
 };
 
 namespace {
@@ -416,6 +417,9 @@ struct WaveGroup {
     // group lane gl caches topics gl, gl + W, ... (T <= 64)
     // bit q = p at position q < 64 (W = 64: the wave's ballot)
     __device__ uint64_t topic_mask(bool p) const { return __ballot(p) & gm; }
+    // bit q = p at the group's row position q (the delivery's mesh masks)
+    static constexpr bool kRowMask = true;
+    __device__ uint64_t row_mask(bool p) const { return (__ballot(p) & gm) >> base; }
     __device__ void load_lastput(const HbArgs& a, int64_t obs, uint64_t subi, bool ovalid)
     {
 #pragma unroll
@@ -558,6 +562,8 @@ struct BlockGroup {
         __syncthreads();
         return sh->d0[0];
     }
+    static constexpr bool kRowMask = false;    // hub rows: delivery walks the whole row
+    __device__ uint64_t row_mask(bool) const { return 0; }
     __device__ uint64_t topic_mask(bool p)
     {
         const uint64_t m = __ballot(p);
@@ -772,6 +778,14 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
                 if (fl != fl0) a.mflags[i] = fl;
                 sf.store(a);
                 if (bo_dirty) a.backoff[i] = bo;
+            }
+            // the delivery's mesh mask of this row and topic (mesh or direct
+            // edges to this shard's peers)
+            if constexpr (Grp::kRowMask) {
+                if (a.mmask) {
+                    const uint64_t mk = g.row_mask(valid && (m || dir) && col >= a.olo && col < a.ohi);
+                    if (gl == 0 && ovalid) a.mmask[(int64_t)t * a.N + obs] = mk;
+                }
             }
 
             // emitGossip(topic, mesh) (gossipsub.go:1554-1556, 1711-1775):
@@ -1022,6 +1036,11 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                     }
                 }
                 mesh += __shfl(delta, q, 64);
+              }
+              if (nch == 1 && a.mmask) {                      // the delivery's mesh mask of the row
+                  const uint32_t cj = valid ? a.col[e] : 0u;
+                  const uint64_t mk = ballot(valid && ((fl & GSIM_TF_MESH) || a.direct[e]) && cj >= a.olo && cj < a.ohi);
+                  if (lane == 0) a.mmask[(int64_t)t * a.N + rcv] = mk;
               }
             }
           }
@@ -1358,7 +1377,7 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.opp_threshold = h->th.opportunistic_graft_threshold;
     GossipView gv{};
     a.gossip = deliver_gossip_view(h, &gv);
-    a.lastput = gv.lastput; a.gsel = gv.gsel; a.gstate = gv.gstate;
+    a.lastput = gv.lastput; a.gsel = gv.gsel; a.gstate = gv.gstate; a.mmask = a.gossip ? gv.mmask : nullptr;
     a.gossip_thr = h->th.gossip_threshold; a.gossip_factor = h->gp.gossip_factor;
     a.dlazy = h->gp.dlazy; a.hist_gossip = h->gp.history_gossip;
     a.first = h->d_first; a.invalid = h->d_invalid; a.p5 = h->d_p5; a.p6 = h->d_p6;
@@ -1421,7 +1440,6 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     if (rc) return rc;
     // heartbeat output goes to the parity-0 inbox, read by control round 0
     HbArgs a = make_hb_args(h, tick, now, 1);
-    h->mesh_version++;
     ProfScope ps(h, GSIM_K_HEARTBEAT);
     // observers in lane groups sized to their rows: 4 per wavefront for rows
     // of <= 16 connections, 2 for <= 32, 1 otherwise (observers are
@@ -1469,7 +1487,6 @@ int handle_control(gsim_handle* h, int32_t round, int64_t now)
 {
     HbArgs a = make_hb_args(h, 0, now, round & 1);
     ProfScope ps(h, GSIM_K_CONTROL);
-    h->mesh_version++;
     hipLaunchKernelGGL(k_handle_control, dim3(grid_rows(h->ohi() - h->olo())), dim3(256), 0, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_handle_control");
 }
@@ -1590,8 +1607,7 @@ int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, i
     }
     h->p6_dirty = true;          // the tracked set (and so the IP sets) changed
     if (!up) h->maybe_retained = true;
-    h->score_version++;
-    h->mesh_version++;          // connected / tracked bits feed the delivery state
+    h->score_version++;          // (churn only clears mesh bits: the masks stay a superset)          // connected / tracked bits feed the delivery state
     return GSIM_OK;
 }
 

@@ -194,6 +194,27 @@ __global__ __launch_bounds__(256) void k_router_import(const uint64_t* mesh, con
     }
 }
 
+// The delivery's mesh masks of the ghost rows (rows <= 64) from the imported
+// router state: one wave per ghost row, lane = row position.
+__global__ __launch_bounds__(256) void k_ghost_mask(const uint32_t* row_ptr, const uint64_t* mesh, const uint8_t* flags,
+                                                    int64_t olo, int64_t ohi, int64_t n, int32_t T, uint64_t* mmask)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t nghost = olo + (n - ohi);
+    for (int64_t x = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); x < nghost; x += (int64_t)gridDim.x * 4) {
+        const int64_t r = x < olo ? x : ohi + (x - olo);
+        const uint32_t b = row_ptr[r], d = row_ptr[r + 1] - b;
+        if (d > 64) continue;                                  // hub rows are walked whole
+        const bool v = (uint32_t)lane < d;
+        const uint64_t mm = v ? mesh[b + lane] : 0ull;         // a ghost row's edges all lead to owned peers
+        const bool dir = v && (flags[b + lane] & 2);
+        for (int32_t t = 0; t < T; ++t) {
+            const uint64_t mk = __ballot(v && (((mm >> t) & 1ull) || dir));
+            if (lane == 0) mmask[(int64_t)t * n + r] = mk;
+        }
+    }
+}
+
 int grid_for(int64_t n)
 {
     int64_t g = (n + 255) / 256;
@@ -663,8 +684,12 @@ int exchange_router(gsim_group* g)
                                (const uint8_t*)s->d_rflag_in, h->d_mflags, h->d_rstate, h->d_direct, s->d_pgate,
                                h->t, h->e, s->own_e_lo, s->own_e_hi);
         if (hipGetLastError() != hipSuccess) return g->fail(GSIM_EDEVICE, "k_router_import");
-        h->score_version++;
-        h->mesh_version++;    // ghost rows' connected / direct bits feed the delivery state
+        GossipView gv{};
+        if (deliver_gossip_view(h, &gv) && gv.mmask && nghost)
+            hipLaunchKernelGGL(k_ghost_mask, dim3(grid_for((nghost + 3) / 4 * 256)), dim3(256), 0, h->stream,
+                               (const uint32_t*)h->d_row_ptr, (const uint64_t*)s->d_rmesh_in,
+                               (const uint8_t*)s->d_rflag_in, s->own_lo, s->own_hi, h->n, std::max(1, h->t), gv.mmask);
+        h->score_version++;    // ghost rows' connected / direct bits feed the delivery state
     }
     g->router_dirty = false;
     return GSIM_OK;

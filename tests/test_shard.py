@@ -48,18 +48,20 @@ def test_sharded_c3_shape_bit_exact(require_gpu, shards):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
-def test_sharded_power_law_churn_fanout_sybils(require_gpu):
-    """A power-law graph (rows 1-64) over 3 shards with Zipf subscriptions,
-    publishers outside their topic (fanout), sybils sharing IPs that ignore
-    IWANT (broken promises), direct peers, retained peers and connections
-    churning between ticks."""
+@pytest.mark.parametrize("cap,verdicts", [(64, None), (1024, (0.85, 0.05, 0.04, 0.03, 0.03))])
+def test_sharded_power_law_churn_fanout_sybils(require_gpu, cap, verdicts):
+    """A power-law graph (rows 1-64, or with hub rows up to ~500) over 3
+    shards with Zipf subscriptions, publishers outside their topic (fanout),
+    sybils sharing IPs that ignore IWANT (broken promises), direct peers,
+    retained peers, connections churning between ticks (and every validation
+    verdict with the hubs)."""
     from fixtures import beacon_params, synthetic_state
     from gsim import graphs
     from gsim.shard import ShardedEngine
     from tickrun import SEED, restrict_to_subscriptions, run_parity, subscribed_schedule
     rng = np.random.default_rng(4242)
     n, T = 4000, 12
-    net = graphs.power_law(n, 16, 2.5, 64, seed=31, n_topics=T)
+    net = graphs.power_law(n, 16, 2.5, cap, seed=31, n_topics=T)
     net = graphs.with_subscriptions(net, graphs.zipf_subscriptions(n, T, 4, seed=32))
     ip_ptr, ip_ids, n_ips, syb = graphs.sybil_ips(n, 0.1, 40, seed=33)
     net = graphs.with_ips(net, ip_ptr, ip_ids, n_ips)
@@ -80,7 +82,7 @@ def test_sharded_power_law_churn_fanout_sybils(require_gpu):
     eng.set_seed(SEED)
     st.push_to_engine(eng)
     ticks = list(range(1, 7))
-    sched = subscribed_schedule(rng, ticks, net, T, 2.0, 0.03, member_only=False)
+    sched = subscribed_schedule(rng, ticks, net, T, 2.0, 0.03, member_only=False, verdicts=verdicts)
     src = net.owner()
     und = np.stack([src, net.col], axis=1)
     und = und[und[:, 0] < und[:, 1]]
