@@ -822,7 +822,8 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
 // rows: the observers of one row-length class (a list), or nullptr for the
 // nrows observers from obs_base on.
 template <int W>
-__global__ __launch_bounds__(256) void k_heartbeat(HbArgs a, const uint32_t* rows, int64_t nrows, int64_t obs_base)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))   // W = 16: keep 3 waves per SIMD
+void k_heartbeat(HbArgs a, const uint32_t* rows, int64_t nrows, int64_t obs_base)
 {
     constexpr int G = 64 / W;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
