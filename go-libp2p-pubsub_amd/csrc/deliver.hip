@@ -2005,8 +2005,8 @@ __global__ __launch_bounds__(256) void k_frontier_export(RoundArgs a, const uint
 }
 
 // The ghosts among the other shards' forwarders.  Entries come in runs of
-// one slot and ascending peers: a wave ORs its fresh bits per word before
-// one atomic, and tests the slot's activity bits once per run.
+// one slot and ascending peers: the summary and activity bits are touched
+// once per run.
 __global__ __launch_bounds__(256) void k_frontier_import(RoundArgs a, const uint32_t* g2l, const uint64_t* in,
                                                          int64_t n)
 {
@@ -2028,26 +2028,23 @@ __global__ __launch_bounds__(256) void k_frontier_import(RoundArgs a, const uint
                 a.cell[(int64_t)m * a.CN + l] = ((uint64_t)(uint32_t)(a.g - 1) << 32) | f;
             }
         }
-        // fresh bits: one atomic per distinct (slot, word) of the wave
-        const uint64_t key = ghost ? (uint64_t)m * (uint64_t)a.nw + (l >> 6) : ~0ull;
-        uint64_t pending = __ballot(ghost);
-        while (pending) {
-            const int leader = __ffsll((long long)pending) - 1;
-            const uint64_t k0 = (uint64_t)__shfl((long long)key, leader, 64);
-            const bool same = ghost && key == k0;
-            uint64_t bit = same ? 1ull << (l & 63) : 0ull;
-            for (int o = 32; o; o >>= 1) bit |= (uint64_t)__shfl_xor((long long)bit, o, 64);
-            if (lane == leader) {
-                fresh_set(a, (uint32_t)(k0 / (uint64_t)a.nw), (int64_t)(k0 % (uint64_t)a.nw), bit);
-                // the slot's activity (one 0 -> 1 transition per round)
-                const uint32_t ms = (uint32_t)(k0 / (uint64_t)a.nw);
-                uint32_t* nw = const_cast<uint32_t*>(a.nnew_prev) + (ms >> 5);
-                if (!((__hip_atomic_load(nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (ms & 31)) & 1u))
-                    atomicOr(nw, 1u << (ms & 31));
-                if (__hip_atomic_load(&a.slot_last[ms], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int32_t)(a.g - 1))
-                    atomicMax(&a.slot_last[ms], (int32_t)(a.g - 1));
-            }
-            pending &= ~__ballot(same);
+        // fresh bit (non-returning atomic: distinct words mostly); the summary
+        // bit and the slot's activity once per run of equal keys (the entries
+        // come sorted by slot and peer)
+        if (ghost)
+            atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (l >> 6)), 1ull << (l & 63));
+        const uint64_t ks = ghost ? (((uint64_t)m * (uint64_t)a.nsw + (l >> 12)) << 6) | ((l >> 6) & 63) : ~0ull;
+        const uint64_t kp = (uint64_t)__shfl_up((long long)ks, 1, 64);
+        if (ghost && (lane == 0 || kp != ks))
+            atomicOr(reinterpret_cast<unsigned long long*>(a.fsum + (ks >> 6)), 1ull << (ks & 63));
+        const uint32_t mp = (uint32_t)__shfl_up((int)(ghost ? m : 0xFFFFFFFFu), 1, 64);
+        if (ghost && (lane == 0 || mp != m)) {
+            // the slot's activity (one 0 -> 1 transition per round)
+            uint32_t* nw = const_cast<uint32_t*>(a.nnew_prev) + (m >> 5);
+            if (!((__hip_atomic_load(nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (m & 31)) & 1u))
+                atomicOr(nw, 1u << (m & 31));
+            if (__hip_atomic_load(&a.slot_last[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int32_t)(a.g - 1))
+                atomicMax(&a.slot_last[m], (int32_t)(a.g - 1));
         }
     }
 }

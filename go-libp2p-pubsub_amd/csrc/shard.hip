@@ -174,10 +174,14 @@ __global__ __launch_bounds__(256) void k_router_export(const uint32_t* xgather, 
     }
 }
 
-// ... into the ghost rows (the ghost's edges into this shard).
+// ... into the ghost rows (the ghost's edges into this shard), and the
+// delivery's mesh masks of the ghost rows of at most 64 connections (zeroed
+// before: bit (row position) per topic with the mesh bit or a direct peer).
 __global__ __launch_bounds__(256) void k_router_import(const uint64_t* mesh, const uint64_t* fan, const uint8_t* flags,
                                                        uint8_t* mflags, uint8_t* rstate, uint8_t* direct, uint8_t* pgate,
-                                                       int32_t T, int64_t E, int64_t e_lo, int64_t e_hi)
+                                                       int32_t T, int64_t E, int64_t e_lo, int64_t e_hi,
+                                                       const uint32_t* row_ptr, const uint32_t* owner, int64_t n,
+                                                       uint64_t* mmask)
 {
     const int64_t nghost = e_lo + (E - e_hi);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -191,27 +195,26 @@ __global__ __launch_bounds__(256) void k_router_import(const uint64_t* mesh, con
         rstate[e] = (f & 1) ? GSIM_ES_CONNECTED : 0;
         direct[e] = (f & 2) ? 1 : 0;
         pgate[e] = (f & 4) ? 1 : 0;
+        if (mmask) {
+            const uint32_t r = owner[e], b = row_ptr[r];
+            if (row_ptr[r + 1] - b <= 64u) {
+                const uint64_t bit = 1ull << (e - b);
+                for (uint64_t q = (f & 2) ? (T >= 64 ? ~0ull : (1ull << T) - 1) : mm; q; q &= q - 1)
+                    atomicOr(reinterpret_cast<unsigned long long*>(mmask + (int64_t)(__ffsll((long long)q) - 1) * n + r), bit);
+            }
+        }
     }
 }
 
-// The delivery's mesh masks of the ghost rows (rows <= 64) from the imported
-// router state: one wave per ghost row, lane = row position.
-__global__ __launch_bounds__(256) void k_ghost_mask(const uint32_t* row_ptr, const uint64_t* mesh, const uint8_t* flags,
-                                                    int64_t olo, int64_t ohi, int64_t n, int32_t T, uint64_t* mmask)
+// zero the ghost rows' masks of every topic
+__global__ __launch_bounds__(256) void k_ghost_mask_clear(uint64_t* mmask, int64_t olo, int64_t ohi, int64_t n,
+                                                          int32_t T)
 {
-    const int lane = threadIdx.x & 63;
     const int64_t nghost = olo + (n - ohi);
-    for (int64_t x = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); x < nghost; x += (int64_t)gridDim.x * 4) {
-        const int64_t r = x < olo ? x : ohi + (x - olo);
-        const uint32_t b = row_ptr[r], d = row_ptr[r + 1] - b;
-        if (d > 64) continue;                                  // hub rows are walked whole
-        const bool v = (uint32_t)lane < d;
-        const uint64_t mm = v ? mesh[b + lane] : 0ull;         // a ghost row's edges all lead to owned peers
-        const bool dir = v && (flags[b + lane] & 2);
-        for (int32_t t = 0; t < T; ++t) {
-            const uint64_t mk = __ballot(v && (((mm >> t) & 1ull) || dir));
-            if (lane == 0) mmask[(int64_t)t * n + r] = mk;
-        }
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < nghost * T; x += stride) {
+        const int64_t t = x / nghost, y = x - t * nghost;
+        mmask[t * n + (y < olo ? y : ohi + (y - olo))] = 0;
     }
 }
 
@@ -678,17 +681,19 @@ int exchange_router(gsim_group* g)
         ShardCtx* s = h->sh;
         (void)hipSetDevice(h->device);
         const int64_t nghost = s->own_e_lo + (h->e - s->own_e_hi);
+        GossipView gv{};
+        uint64_t* mm = deliver_gossip_view(h, &gv) ? gv.mmask : nullptr;
+        const int64_t ngr = s->own_lo + (h->n - s->own_hi);
+        if (mm && ngr)
+            hipLaunchKernelGGL(k_ghost_mask_clear, dim3(grid_for(ngr * std::max(1, h->t))), dim3(256), 0, h->stream, mm,
+                               s->own_lo, s->own_hi, h->n, std::max(1, h->t));
         if (nghost)
             hipLaunchKernelGGL(k_router_import, dim3(grid_for(nghost)), dim3(256), 0, h->stream,
                                (const uint64_t*)s->d_rmesh_in, (const uint64_t*)s->d_rfan_in,
                                (const uint8_t*)s->d_rflag_in, h->d_mflags, h->d_rstate, h->d_direct, s->d_pgate,
-                               h->t, h->e, s->own_e_lo, s->own_e_hi);
+                               h->t, h->e, s->own_e_lo, s->own_e_hi, (const uint32_t*)h->d_row_ptr,
+                               (const uint32_t*)h->d_owner, h->n, mm);
         if (hipGetLastError() != hipSuccess) return g->fail(GSIM_EDEVICE, "k_router_import");
-        GossipView gv{};
-        if (deliver_gossip_view(h, &gv) && gv.mmask && nghost)
-            hipLaunchKernelGGL(k_ghost_mask, dim3(grid_for((nghost + 3) / 4 * 256)), dim3(256), 0, h->stream,
-                               (const uint32_t*)h->d_row_ptr, (const uint64_t*)s->d_rmesh_in,
-                               (const uint8_t*)s->d_rflag_in, s->own_lo, s->own_hi, h->n, std::max(1, h->t), gv.mmask);
         h->score_version++;    // ghost rows' connected / direct bits feed the delivery state
     }
     g->router_dirty = false;
