@@ -2028,17 +2028,25 @@ __global__ __launch_bounds__(256) void k_frontier_import(RoundArgs a, const uint
                 a.cell[(int64_t)m * a.CN + l] = ((uint64_t)(uint32_t)(a.g - 1) << 32) | f;
             }
         }
-        // fresh bit (non-returning atomic: distinct words mostly); the summary
-        // bit and the slot's activity once per run of equal keys (the entries
-        // come sorted by slot and peer)
-        if (ghost)
-            atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (l >> 6)), 1ull << (l & 63));
-        const uint64_t ks = ghost ? (((uint64_t)m * (uint64_t)a.nsw + (l >> 12)) << 6) | ((l >> 6) & 63) : ~0ull;
-        const uint64_t kp = (uint64_t)__shfl_up((long long)ks, 1, 64);
-        if (ghost && (lane == 0 || kp != ks))
-            atomicOr(reinterpret_cast<unsigned long long*>(a.fsum + (ks >> 6)), 1ull << (ks & 63));
-        const uint32_t mp = (uint32_t)__shfl_up((int)(ghost ? m : 0xFFFFFFFFu), 1, 64);
-        if (ghost && (lane == 0 || mp != m)) {
+        // one atomic per run of equal (slot, word) keys: a segmented OR scan
+        // over the wave (the entries come sorted by slot and peer, so equal
+        // keys are contiguous); the run's last lane holds its bits
+        const uint64_t kw = ghost ? (uint64_t)m * (uint64_t)a.nw + (l >> 6) : ~0ull;
+        uint64_t bits = ghost ? 1ull << (l & 63) : 0ull;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t ko = (uint64_t)__shfl_up((long long)kw, o, 64);
+            const uint64_t vo = (uint64_t)__shfl_up((long long)bits, o, 64);
+            if (lane >= o && ko == kw) bits |= vo;
+        }
+        const uint64_t kn = (uint64_t)__shfl_down((long long)kw, 1, 64);
+        const bool last = ghost && (lane == 63 || kn != kw);
+        if (last) {
+            atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + kw), bits);
+            const int64_t w = (int64_t)(l >> 6);
+            atomicOr(reinterpret_cast<unsigned long long*>(a.fsum + (int64_t)m * a.nsw + (w >> 6)), 1ull << (w & 63));
+        }
+        const uint32_t mn = (uint32_t)__shfl_down((int)(ghost ? m : 0xFFFFFFFFu), 1, 64);
+        if (ghost && (lane == 63 || mn != m)) {
             // the slot's activity (one 0 -> 1 transition per round)
             uint32_t* nw = const_cast<uint32_t*>(a.nnew_prev) + (m >> 5);
             if (!((__hip_atomic_load(nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (m & 31)) & 1u))
