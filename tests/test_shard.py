@@ -90,3 +90,35 @@ def test_sharded_power_law_churn_fanout_sybils(require_gpu, cap, verdicts):
     churn = {2: [(downs[2], False)], 4: [(downs[2], True), (downs[4], False)], 6: [(downs[4], True)]}
     _, gs = run_parity(net, params, th, gp, st, ticks, sched, ring=1024, behaviour=beh, churn=churn, eng=eng)
     assert gs["broken_promises"] > 0 and gs["iwant_ids"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_rccl_single_rank_group_bit_exact(require_gpu):
+    """The RCCL transport end to end on the one GPU a test box has: a
+    one-rank communicator (gsim_group_create_rccl; counts by ncclAllGather,
+    totals by ncclAllReduce) running a gossip network bit-exact against the
+    oracle.  The exchange logic above the transport is the in-process tests'
+    (RCCL refuses two ranks on one device, so K > 1 over RCCL runs only in
+    the multi-GPU bench)."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim.engine import random_regular
+    from gsim.shard import ShardedEngine
+    from tickrun import SEED, run_parity, subscribed_schedule
+    rng = np.random.default_rng(77)
+    n, T = 3000, 4
+    net = random_regular(n, 16, seed=5, n_topics=T)
+    params = beacon_params(T)
+    th = PeerScoreThresholds(GossipThreshold=-20, PublishThreshold=-40, GraylistThreshold=-300)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2)
+    uid = ShardedEngine.rccl_unique_id()
+    eng = ShardedEngine(params, th, gossip=gp, shards=1, rccl=(0, uid, 0))
+    eng.load_graph(net)
+    eng.set_seed(SEED)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 0.5)
+    st.push_to_engine(eng)
+    ticks = list(range(1, 5))
+    sched = subscribed_schedule(rng, ticks, net, T, 4.0, 0.03)
+    msgs, gs = run_parity(net, params, th, gp, st, ticks, sched, ring=512, eng=eng)
+    assert msgs.stats[1] > n and gs["iwant_ids"] >= 0
