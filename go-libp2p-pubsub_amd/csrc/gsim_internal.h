@@ -127,6 +127,13 @@ struct Deliver;   // message ring, seen-set and round lists (deliver.hip)
 // A shard of a graph-sharded network (shard.hip): which local
 // peers / edges the handle owns and the device side of the halo exchange.
 // A handle without one owns every peer (sh == nullptr).
+// A shard's view of the peer ranges (kernel argument): local ids
+// [lo[s], lo[s+1]) are shard s's peers; self = this shard.
+struct ShardRanges {
+    int64_t lo[GSIM_MAX_SHARDS + 1];
+    int32_t K, self;
+};
+
 struct ShardCtx {
     int32_t k = 0, K = 1;
     int64_t own_lo = 0, own_hi = 0;        // owned local peers
@@ -143,6 +150,12 @@ struct ShardCtx {
     uint32_t* d_xgather = nullptr;         // [n_cross] cross-out lists (local edge indices)
     uint8_t* d_pgate = nullptr;            // [e] ghost-row edge: the sender's score of the receiver >= publishThreshold
     int64_t send_edges = 0, send_max = 0;  // edges into owned peers, longest such run of a row
+    uint32_t* d_xq = nullptr;              // [e] owned-row cross edge: its position in the cross-out list to its shard
+    uint64_t* d_rdel = nullptr;            // control-round router changes of cross edges (k_handle_control)
+    uint32_t* d_rdel_n = nullptr;
+    int64_t rdel_cap = 0;
+    uint64_t* d_rdel_in = nullptr;         // ... every other shard's
+    int64_t rdel_in_cap = 0;
     uint32_t* d_sptr = nullptr;            // [n+1] CSR of each row's edges into owned peers (the copies this shard delivers)
     uint32_t* d_sedge = nullptr;           // their local edge indices, in row order
     std::vector<uint8_t> xto;              // [K] the owned peers have connections into shard q's

@@ -82,6 +82,13 @@ struct HbArgs {
     const uint32_t* gid;
     uint32_t olo, ohi;
     uint64_t* mmask;           // [T][N] delivery's mesh masks (nullptr before gsim_msgs_init)
+    // a shard's control pass: mesh changes of cross edges for the other shards'
+    // ghost rows (src | dest << 6 | topic << 12 | flags << 20 | position << 32)
+    uint64_t* rdel;
+    uint32_t* rdel_n;
+    int64_t rdel_cap;
+    const uint32_t* xq;
+    ShardRanges sr;
 };
 
 namespace {
@@ -983,6 +990,7 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                 pending &= pending - 1;
                 int delta = 0;
                 if (lane == q) {
+                    const uint8_t fl_in = fl;
                     const uint32_t rv = a.rev[e];                // receiver's record of the sender
                     const uint8_t est = a.estate[rv];
                     const bool tracked = est & GSIM_ES_TRACKED;
@@ -1028,6 +1036,17 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                         if (bo < ex) bo = ex;
                     }
                     a.mflags[i] = fl;
+                    if (a.rdel && ((fl ^ fl_in) & GSIM_TF_MESH) && a.xq[e] != 0xFFFFFFFFu) {
+                        // a cross edge: its copy in the other shard's ghost row changes
+                        const uint32_t cj = a.col[e];
+                        uint32_t dsh = 0;
+                        while ((int32_t)dsh + 1 < a.sr.K && (int64_t)cj >= a.sr.lo[dsh + 1]) ++dsh;
+                        const uint32_t pos = atomicAdd(a.rdel_n, 1u);
+                        if ((int64_t)pos < a.rdel_cap)
+                            a.rdel[pos] = (uint64_t)a.sr.self | ((uint64_t)dsh << 6) | ((uint64_t)t << 12) |
+                                          ((uint64_t)(fl & (GSIM_TF_MESH | GSIM_TF_FANOUT)) << 20) |
+                                          ((uint64_t)a.xq[e] << 32);
+                    }
                     sf.store(a);
                     if (bo != bo0) a.backoff[i] = bo;
                     if (reply) {
@@ -1387,6 +1406,15 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.lastpub = h->x->d_lastpub; a.fan_topics = h->x->d_fantopics;
     a.pub_thr = h->th.publish_threshold; a.fanout_ttl = h->gp.fanout_ttl_ns;
     a.gid = h->sh ? h->sh->d_gid : nullptr;
+    if (ShardCtx* sh = h->sh; sh && sh->d_rdel) {
+        a.rdel = sh->d_rdel;
+        a.rdel_n = sh->d_rdel_n;
+        a.rdel_cap = sh->rdel_cap;
+        a.xq = sh->d_xq;
+        a.sr.K = sh->K;
+        a.sr.self = sh->k;
+        for (int q = 0; q <= sh->K; ++q) a.sr.lo[q] = sh->lpeer[(size_t)q];
+    }
     a.olo = (uint32_t)h->olo();
     a.ohi = (uint32_t)h->ohi();
     return a;

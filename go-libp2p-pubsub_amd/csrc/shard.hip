@@ -218,6 +218,37 @@ __global__ __launch_bounds__(256) void k_ghost_mask_clear(uint64_t* mmask, int64
     }
 }
 
+// Control-round mesh changes of other shards' cross edges, into this shard's
+// ghost rows (router flags and the delivery's mesh masks).
+struct EdgeBases {
+    int64_t b[GSIM_MAX_SHARDS];
+};
+
+__global__ __launch_bounds__(256) void k_router_delta(const uint64_t* in, int64_t n_in, int32_t self, EdgeBases gb,
+                                                      uint8_t* mflags, const uint8_t* direct, const uint32_t* row_ptr,
+                                                      const uint32_t* owner, int64_t E, int64_t n, uint64_t* mmask)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n_in; x += stride) {
+        const uint64_t v = in[x];
+        if ((int32_t)((v >> 6) & 63) != self) continue;
+        const int32_t src = (int32_t)(v & 63), t = (int32_t)((v >> 12) & 0xFF);
+        const uint8_t fl = (uint8_t)((v >> 20) & 0xFF);
+        const int64_t ge = gb.b[src] + (int64_t)(v >> 32);
+        uint8_t* p = mflags + (int64_t)t * E + ge;
+        *p = (uint8_t)((*p & ~(GSIM_TF_MESH | GSIM_TF_FANOUT)) | fl);
+        if (mmask) {
+            const uint32_t r = owner[ge], b = row_ptr[r];
+            if (row_ptr[r + 1] - b <= 64u) {
+                const uint64_t bit = 1ull << (ge - b);
+                unsigned long long* w = reinterpret_cast<unsigned long long*>(mmask + (int64_t)t * n + r);
+                if (fl & GSIM_TF_MESH) atomicOr(w, bit);
+                else if (!direct[ge]) atomicAnd(w, ~bit);
+            }
+        }
+    }
+}
+
 int grid_for(int64_t n)
 {
     int64_t g = (n + 255) / 256;
@@ -481,7 +512,7 @@ int dalloc(gsim_handle* h, T** p, size_t n)
 void free_shard_bufs(ShardCtx* s)
 {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(s->d_gid); f(s->d_g2l); f(s->d_sptr); f(s->d_sedge); f(s->d_ymap); f(s->d_xgather); f(s->d_pgate);
+    f(s->d_gid); f(s->d_g2l); f(s->d_sptr); f(s->d_sedge); f(s->d_xq); f(s->d_rdel); f(s->d_rdel_n); f(s->d_rdel_in); f(s->d_ymap); f(s->d_xgather); f(s->d_pgate);
     f(s->d_fout); f(s->d_fcnt); f(s->d_fin); f(s->d_cout); f(s->d_ccnt); f(s->d_cin);
     f(s->d_rmesh_out); f(s->d_rfan_out); f(s->d_rflag_out); f(s->d_rmesh_in); f(s->d_rfan_in); f(s->d_rflag_in);
     f(s->d_gout); f(s->d_gsout); f(s->d_gin); f(s->d_gsin);
@@ -697,6 +728,79 @@ int exchange_router(gsim_group* g)
         h->score_version++;    // ghost rows' connected / direct bits feed the delivery state
     }
     g->router_dirty = false;
+    return GSIM_OK;
+}
+
+// The mesh changes control round r made to cross edges (k_handle_control's
+// list), to the shards holding their ghost copies.  A list over its capacity
+// (seen by every process through the counts) falls back to the full router
+// exchange before the next round.
+int exchange_router_delta(gsim_group* g)
+{
+    const size_t L = g->hs.size();
+    const int K = g->K;
+    constexpr uint64_t kOver = ~0ull;
+    std::vector<std::vector<uint64_t>> scnt(L, std::vector<uint64_t>((size_t)K, 0)), rcnt;
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        (void)hipSetDevice(h->device);
+        if (hipMemcpyAsync(s->h_counts, s->d_rdel_n, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+            hipStreamSynchronize(h->stream) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "router delta count");
+        const uint64_t n = s->h_counts[0];
+        for (int d = 0; d < K; ++d)
+            scnt[l][(size_t)d] = d == g->ids[l] ? 0 : ((int64_t)n > s->rdel_cap ? kOver : n);
+    }
+    int rc = g->take_tr(g->tr->exchange_counts(scnt, rcnt));
+    if (rc) return rc;
+    bool over = false;
+    for (size_t l = 0; l < L; ++l) {
+        for (int q = 0; q < K; ++q) over |= rcnt[l][(size_t)q] == kOver || scnt[l][(size_t)q] == kOver;
+    }
+    std::vector<std::vector<const void*>> sp(L, std::vector<const void*>((size_t)K, nullptr));
+    std::vector<std::vector<void*>> rp(L, std::vector<void*>((size_t)K, nullptr));
+    std::vector<std::vector<uint64_t>> sb(L, std::vector<uint64_t>((size_t)K, 0)), rb = sb;
+    std::vector<int64_t> total(L, 0);
+    if (!over) {
+        for (size_t l = 0; l < L; ++l) {
+            gsim_handle* h = g->hs[l];
+            ShardCtx* s = h->sh;
+            for (int q = 0; q < K; ++q) total[l] += (int64_t)rcnt[l][(size_t)q];
+            (void)hipSetDevice(h->device);
+            rc = g->take(h, ensure(h, &s->d_rdel_in, &s->rdel_in_cap, total[l]));
+            if (rc) return rc;
+            int64_t off = 0;
+            for (int q = 0; q < K; ++q) {
+                sp[l][(size_t)q] = s->d_rdel;
+                sb[l][(size_t)q] = scnt[l][(size_t)q] * 8;
+                rp[l][(size_t)q] = s->d_rdel_in + off;
+                rb[l][(size_t)q] = rcnt[l][(size_t)q] * 8;
+                off += (int64_t)rcnt[l][(size_t)q];
+            }
+        }
+        rc = g->take_tr(g->tr->alltoallv(sp, sb, rp, rb));
+        if (rc) return rc;
+    }
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        (void)hipSetDevice(h->device);
+        if (!over && total[l]) {
+            EdgeBases gb{};
+            for (int q = 0; q < K; ++q) gb.b[q] = s->gbase[(size_t)q];
+            GossipView gv{};
+            uint64_t* mm = deliver_gossip_view(h, &gv) ? gv.mmask : nullptr;
+            hipLaunchKernelGGL(k_router_delta, dim3(grid_for(total[l])), dim3(256), 0, h->stream,
+                               (const uint64_t*)s->d_rdel_in, total[l], g->ids[l], gb, h->d_mflags,
+                               (const uint8_t*)h->d_direct, (const uint32_t*)h->d_row_ptr, (const uint32_t*)h->d_owner,
+                               h->e, h->n, mm);
+            if (hipGetLastError() != hipSuccess) return g->fail(GSIM_EDEVICE, "k_router_delta");
+        }
+        if (hipMemsetAsync(s->d_rdel_n, 0, sizeof(uint32_t), h->stream) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "router delta reset");
+    }
+    if (over) g->router_dirty = true;
     return GSIM_OK;
 }
 
@@ -969,7 +1073,7 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
         for (int q = 0; q < K; ++q) s->xto[(size_t)q] = L.crossout[(size_t)q].empty() ? 0 : 1;
         const int64_t ncross = L.n_cross;
         if ((rc = dalloc(h, &s->d_gid, (size_t)L.n_loc)) || (rc = dalloc(h, &s->d_g2l, (size_t)n)) ||
-            (rc = dalloc(h, &s->d_sptr, sptr.size())) ||
+            (rc = dalloc(h, &s->d_sptr, sptr.size())) || (rc = dalloc(h, &s->d_xq, (size_t)L.e_loc)) ||
             (rc = dalloc(h, &s->d_sedge, sedge.size())) ||
             (rc = dalloc(h, &s->d_ymap, (size_t)L.e_loc)) || (rc = dalloc(h, &s->d_xgather, xg.size())) ||
             (rc = dalloc(h, &s->d_pgate, (size_t)L.e_loc)) ||
@@ -982,6 +1086,7 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
         hipError_t he = hipMemcpy(s->d_gid, L.gid.data(), L.gid.size() * 4, hipMemcpyHostToDevice);
         if (he == hipSuccess) he = hipMemcpy(s->d_g2l, g2l.data(), g2l.size() * 4, hipMemcpyHostToDevice);
         if (he == hipSuccess) he = hipMemcpy(s->d_sptr, sptr.data(), sptr.size() * 4, hipMemcpyHostToDevice);
+        if (he == hipSuccess) he = hipMemcpy(s->d_xq, L.xq.data(), L.xq.size() * 4, hipMemcpyHostToDevice);
         if (he == hipSuccess && !sedge.empty())
             he = hipMemcpy(s->d_sedge, sedge.data(), sedge.size() * 4, hipMemcpyHostToDevice);
         if (he == hipSuccess && !xg.empty()) he = hipMemcpy(s->d_xgather, xg.data(), xg.size() * 4, hipMemcpyHostToDevice);
@@ -1023,6 +1128,12 @@ int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg)
         const int64_t ncross = s->xoff[(size_t)K];
         rc = GSIM_OK;
         auto A = [&](auto** p, size_t n) { if (!rc) rc = dalloc(h, p, n); };
+        if (!s->d_rdel) {
+            s->rdel_cap = std::max<int64_t>(1 << 16, (s->own_e_hi - s->own_e_lo) / 16);
+            A(&s->d_rdel, (size_t)s->rdel_cap);
+            A(&s->d_rdel_n, 1);
+            if (!rc && hipMemset(s->d_rdel_n, 0, 4) != hipSuccess) return g->fail(GSIM_EDEVICE, "router delta count");
+        }
         if (s->d_fout) { (void)hipFree(s->d_fout); s->d_fout = nullptr; }
         A(&s->d_fout, (size_t)s->fcap);
         if (!s->d_fcnt) A(&s->d_fcnt, 1);
@@ -1196,8 +1307,8 @@ int gsim_group_round(gsim_group* g, int64_t round)
     const int64_t r = round % g->rounds;
     if (r < 2) {
         rc = exchange_control(g, (int)((r + 1) & 1));   // PRUNE replies for the next control round
+        if (!rc) rc = exchange_router_delta(g);         // the meshes control changed, on cross edges
         if (rc) return rc;
-        g->router_dirty = true;                         // control changed meshes
     }
     for (gsim_handle* h : g->hs) {
         (void)hipSetDevice(h->device);
