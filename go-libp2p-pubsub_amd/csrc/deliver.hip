@@ -2014,7 +2014,7 @@ __global__ __launch_bounds__(256) void k_frontier_import(RoundArgs a, const uint
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t b0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); b0 < n; b0 += stride) {   // wave-uniform
         const int64_t x = b0 + lane;
-        bool ghost = false;
+        bool ghost = false, fwd = false;
         uint32_t l = 0, m = 0;
         if (x < n) {
             const uint64_t v = in[x];
@@ -2026,31 +2026,38 @@ __global__ __launch_bounds__(256) void k_frontier_import(RoundArgs a, const uint
                 if (f == 0xFFFFFFFFu) f = kPeerMask;                         // not a local peer
                 m = (uint32_t)(v >> 48);
                 a.cell[(int64_t)m * a.CN + l] = ((uint64_t)(uint32_t)(a.g - 1) << 32) | f;
+                // the cell is what IHAVE needs of a ghost advertiser; it forwards
+                // here only along mesh / direct edges into this shard (its mask),
+                // unless it is the origin (fanout / flood) or a hub (whole row)
+                const uint32_t rb = a.row_ptr[l];
+                fwd = a.row_ptr[l + 1] - rb > 64u || l == a.morigin[m] || a.mmask[(int64_t)a.mtopic[m] * a.N + l];
             }
         }
         // one atomic per run of equal (slot, word) keys: a segmented OR scan
         // over the wave (the entries come sorted by slot and peer, so equal
         // keys are contiguous); the run's last lane holds its bits
-        const uint64_t kw = ghost ? (uint64_t)m * (uint64_t)a.nw + (l >> 6) : ~0ull;
-        uint64_t bits = ghost ? 1ull << (l & 63) : 0ull;
+        const uint64_t kw = fwd ? (uint64_t)m * (uint64_t)a.nw + (l >> 6) : ~0ull;
+        uint64_t bits = fwd ? 1ull << (l & 63) : 0ull;
         for (int o = 1; o < 64; o <<= 1) {
             const uint64_t ko = (uint64_t)__shfl_up((long long)kw, o, 64);
             const uint64_t vo = (uint64_t)__shfl_up((long long)bits, o, 64);
             if (lane >= o && ko == kw) bits |= vo;
         }
         const uint64_t kn = (uint64_t)__shfl_down((long long)kw, 1, 64);
-        const bool last = ghost && (lane == 63 || kn != kw);
-        if (last) {
+        if (fwd && (lane == 63 || kn != kw)) {
             atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + kw), bits);
             const int64_t w = (int64_t)(l >> 6);
             atomicOr(reinterpret_cast<unsigned long long*>(a.fsum + (int64_t)m * a.nsw + (w >> 6)), 1ull << (w & 63));
         }
+        // the slot's activity: forwarding next round (nnew), mcache (slot_last)
         const uint32_t mn = (uint32_t)__shfl_down((int)(ghost ? m : 0xFFFFFFFFu), 1, 64);
-        if (ghost && (lane == 63 || mn != m)) {
-            // the slot's activity (one 0 -> 1 transition per round)
+        const uint32_t fwn = (uint32_t)__shfl_down((int)(fwd ? m : 0xFFFFFFFFu), 1, 64);
+        if (fwd && (lane == 63 || fwn != m)) {
             uint32_t* nw = const_cast<uint32_t*>(a.nnew_prev) + (m >> 5);
             if (!((__hip_atomic_load(nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (m & 31)) & 1u))
                 atomicOr(nw, 1u << (m & 31));
+        }
+        if (ghost && (lane == 63 || mn != m)) {
             if (__hip_atomic_load(&a.slot_last[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int32_t)(a.g - 1))
                 atomicMax(&a.slot_last[m], (int32_t)(a.g - 1));
         }
