@@ -167,8 +167,6 @@ def build_engine(cfg, seed, device, scen=None, shard=None):
         eng.set_kernel_variant(2, int(os.environ["GSIM_SEND_VARIANT"]))
     if os.environ.get("GSIM_TM_WALK"):                           # topic-major walk: 1 per edge, 2 per row
         eng.set_kernel_variant(4, int(os.environ["GSIM_TM_WALK"]))
-    if os.environ.get("GSIM_IMPORT_FILTER"):                     # shard import filter (variant 6)
-        eng.set_kernel_variant(6, int(os.environ["GSIM_IMPORT_FILTER"]))
     if os.environ.get("GSIM_TM_HBM"):                            # topic-major committed bits from HBM
         eng.set_kernel_variant(5, int(os.environ["GSIM_TM_HBM"]))
     return eng, net

@@ -1073,11 +1073,6 @@ int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant)
         h->send_variant_flat = variant == 0 ? -1 : variant == 1 ? 1 : 0;
         return GSIM_OK;
     }
-    if (which == 6) {           // shard frontier import: 1 = fresh bits only for ghosts with mesh edges here, 0 = all
-        if (variant < 0 || variant > 1) { h->err = "unknown import filter (0 or 1)"; return GSIM_EINVAL; }
-        h->import_filter = variant;
-        return GSIM_OK;
-    }
     if (which == 5) {           // topic-major committed bits: 0 = in LDS while they fit, 1 = read from HBM
         if (variant < 0 || variant > 1) { h->err = "unknown staging choice (0 or 1)"; return GSIM_EINVAL; }
         h->tm_stage = variant == 1 ? 0 : -1;

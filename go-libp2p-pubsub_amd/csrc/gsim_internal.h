@@ -215,7 +215,6 @@ struct gsim_handle {
     bool all_joined = false;     // every peer announced every topic (nothing to skip)
     int send_variant = 3;     // delivery kernel variant (gsim_set_kernel_variant(h, 2, v)); 3 = topic-major
     int ihave_w = 0;          // k_ihave lane group width (gsim_set_kernel_variant(h, 3, w)); 0 = by row lengths
-    int import_filter = 1;    // a shard's frontier import filters ghosts by their mesh masks (variant 6)
     int tm_stage = -1;        // k_send_tm committed bits (gsim_set_kernel_variant(h, 5, v)): -1 LDS while they fit, 0 HBM
     int send_variant_flat = -1;   // k_send_tm walk (gsim_set_kernel_variant(h, 4, v)): -1 by row lengths, 1 per edge, 0 per row
 

@@ -444,9 +444,7 @@ int gsim_profile_read(gsim_handle* h, double* ms, int64_t* launches, int32_t n);
  * thread per edge (the forwarders' mesh edges flattened), 2 = a lane group
  * per row.  which = 5: the topic-major kernel's committed bits: 0
  * (default) staged in LDS while a slot's bits fit (<= ~10^6 receivers), 1
- * always read from HBM.  which = 6: a shard's frontier import: 1 (default)
- * marks only ghosts that forward into the shard (mesh / direct edges), 0
- * marks every imported ghost. */
+ * always read from HBM. */
 int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant);
 
 /* ---- synthetic inputs -------------------------------- */
