@@ -434,17 +434,21 @@ def main():
         alg_deliv = (FIRST_BYTES * firsts + DUP_BYTES * dups) / K
         deliv_ms = kms["send"] + kms["commit"] + kms["accept"]
         deliv_gbs = alg_deliv / (deliv_ms * 1e-3) / 1e9 if deliv_ms > 0 else 0.0
+        # traffic: PMC HBM bytes (profiles/traffic.json), per launch like `achieved`
+        tr_ref = load_traffic(args.config)
         roof_refresh = {"bound": "hbm", "achieved": ref_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": ref_gbs / HBM_PEAK_GBS, "traffic": load_traffic(args.config),
+                        "frac": ref_gbs / HBM_PEAK_GBS,
+                        "traffic": tr_ref["bytes_per_launch"] if tr_ref else None, "traffic_detail": tr_ref,
                         "kernel": "k_refresh_score<true,true>", "kernel_ms": ref_ms,
                         "algorithmic_bytes_per_launch": alg_refresh}
-        # PMC traffic of k_send (profiles/traffic.json, per launch) scaled to a tick
+        # PMC traffic of k_send (per launch) scaled to a tick, the unit delivery's bytes are quoted in
         tr_send = load_traffic(args.config + ":send")
+        tr_send_tick = None
         if tr_send is not None:
-            per_tick = tr_send["bytes_per_launch"] * launches["send"] / K
-            tr_send = dict(tr_send, bytes_per_tick=per_tick)
+            tr_send_tick = tr_send["bytes_per_launch"] * launches["send"] / K
+            tr_send = dict(tr_send, bytes_per_tick=tr_send_tick, covers="k_send_tm only (k_commit not counted)")
         roof_deliv = {"bound": "hbm", "achieved": deliv_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                      "frac": deliv_gbs / HBM_PEAK_GBS, "traffic": tr_send,
+                      "frac": deliv_gbs / HBM_PEAK_GBS, "traffic": tr_send_tick, "traffic_detail": tr_send,
                       "kernel": "delivery: k_send_tm + k_commit + k_delivery_state (per tick, 10 rounds)", "kernel_ms": deliv_ms,
                       "algorithmic_bytes_per_tick": alg_deliv}
         dominant = roof_refresh if ref_ms * launches["refresh_score"] / K >= deliv_ms else roof_deliv
