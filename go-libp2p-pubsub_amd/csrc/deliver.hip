@@ -77,6 +77,9 @@ struct Deliver {
     uint64_t* d_fsum = nullptr;        // [ring][ceil(N/4096)] bit: that fresh word may be non-zero
     uint64_t* d_mmask = nullptr;       // [T][N] mesh | direct positions of rows <= 64 (RoundArgs::mmask)
     uint64_t mask_version = 0;         // h->mesh_version the masks were built for
+    uint32_t* d_tmtab = nullptr;       // k_send_tm blocks: [T+1] first block of each topic, [T] its range
+    std::vector<uint32_t> tmtab;       // host copy (the upload's source)
+    int64_t tm_cn = -1;                // peers the table was built for
     bool fresh_on = false;             // the topic-major delivery (and so the fresh bits) is in use
     int32_t* d_mpub = nullptr;         // [ring] round the slot's message was published in
     int64_t* d_roff = nullptr;         // [rounds] offset of each round in its heartbeat
@@ -161,6 +164,7 @@ struct RoundArgs {
     // direct edge (to an owned peer); a forwarder other than the origin sends
     // on no other edge, so only these are walked
     const uint64_t* mmask;
+    const uint32_t* tmtab;         // k_send_tm blocks per topic (Deliver::d_tmtab)
 };
 
 __device__ __forceinline__ int64_t round_time(const RoundArgs& a, int64_t g)
@@ -639,7 +643,7 @@ __global__ __launch_bounds__(256) void k_mesh_mask(const uint32_t* row_ptr, cons
 // block (1024 with the committed bits in LDS: one block per CU anyway; 512
 // reading them from HBM: three blocks per CU).
 template <int W, int kTmThreads>
-__global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t range, int32_t stage)
+__global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t stage)
 {
     // [nws] committed bits of the receivers' words (stage: more receivers than
     // fit in LDS read them from HBM instead), then [ring] u16 slots
@@ -658,10 +662,20 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t ran
     __shared__ int s_ns, s_nf, s_claimed;
     __shared__ uint32_t s_ne;
     __shared__ unsigned long long s_stats[4];
-    const int32_t t = (int32_t)blockIdx.y;
+    // the block's topic and peer range: topics get blocks in proportion to
+    // their subscribers (tmtab, launch_send_tm_tb)
+    int32_t t = 0;
+    {
+        int32_t r = a.T > 0 ? a.T : 1;
+        while (r - t > 1) {
+            const int32_t mid = (t + r) >> 1;
+            if (a.tmtab[mid] <= blockIdx.x) t = mid; else r = mid;
+        }
+    }
+    const int64_t range = a.tmtab[(a.T > 0 ? a.T : 1) + 1 + t];
     // senders: the peers with cells, [clo, clo + CN)
     const int64_t pend_ = (int64_t)a.clo + a.CN;
-    const int64_t lo = (int64_t)a.clo + (int64_t)blockIdx.x * range;
+    const int64_t lo = (int64_t)a.clo + (int64_t)(blockIdx.x - a.tmtab[t]) * range;
     const int64_t hi = lo + range < pend_ ? lo + range : pend_;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     if (tid == 0) { s_ns = 0; s_stats[0] = s_stats[1] = s_stats[2] = s_stats[3] = 0; }
@@ -1462,7 +1476,7 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_pair_cnt); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
@@ -1515,6 +1529,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.fresh = d->fresh_on ? d->d_fresh : nullptr;
     a.fsum = d->d_fsum;
     a.mmask = d->d_mmask;
+    a.tmtab = d->d_tmtab;
     a.nsw = (a.nw + 63) / 64;
     const size_t w = (size_t)nnew_words(d);
     a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
@@ -1755,16 +1770,39 @@ static int launch_send_tm_tb(gsim_handle* h, const RoundArgs& a, size_t lds, int
     constexpr int64_t total = 2048;
     constexpr int64_t chunk = 2 * TB;
     const int64_t cn = h->n;                 // every local peer sends (a shard's ghosts too)
+    const int T = std::max(1, h->t);
     const int64_t ranges = std::max<int64_t>(1, std::min<int64_t>((cn + 4095) / 4096,
                                                                     std::max<int64_t>(h->t >= 32 ? 256 : 1,
-                                                                                      total / std::max(1, h->t))));
-    const int32_t range = (int32_t)(((cn + ranges - 1) / ranges + chunk - 1) / chunk * chunk);
-    const int64_t p = (cn + range - 1) / range;
+                                                                                      total / T)));
+    Deliver* d = h->dl;
+    if (d->tm_cn != cn) {
+        // the same budget of ranges x T blocks, shared out by subscribers
+        // (Zipf topics: the busiest topic's blocks set the launch's length),
+        // ranges of whole chunks
+        int64_t wsum = 0;
+        for (int t = 0; t < T && !h->tm_uniform; ++t) wsum += t < (int)h->topic_subs.size() ? h->topic_subs[t] : 0;
+        const int64_t budget = ranges * T, max_blocks = (cn + chunk - 1) / chunk;
+        d->tmtab.assign((size_t)(2 * T + 1), 0);
+        uint32_t start = 0;
+        for (int t = 0; t < T; ++t) {
+            int64_t b = ranges;
+            if (wsum > 0) b = (budget * h->topic_subs[t] + wsum - 1) / wsum;
+            b = std::max<int64_t>(1, std::min(b, max_blocks));
+            const int64_t range = ((cn + b - 1) / b + chunk - 1) / chunk * chunk;
+            d->tmtab[t] = start;
+            d->tmtab[T + 1 + t] = (uint32_t)range;
+            start += (uint32_t)((cn + range - 1) / range);
+        }
+        d->tmtab[T] = start;
+        hipError_t e = hipMemcpyAsync(d->d_tmtab, d->tmtab.data(), d->tmtab.size() * 4, hipMemcpyHostToDevice,
+                                      h->stream);
+        if (e != hipSuccess) return hip_check(h, e, "k_send_tm block table");
+        d->tm_cn = cn;
+    }
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_send_tm<W, TB>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return hip_check(h, e, "k_send_tm LDS attribute");
-    hipLaunchKernelGGL((k_send_tm<W, TB>), dim3((uint32_t)p, (uint32_t)std::max(1, h->t)), dim3(TB), lds, h->stream,
-                       a, range, stage);
+    hipLaunchKernelGGL((k_send_tm<W, TB>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a, stage);
     return hip_check(h, hipGetLastError(), "k_send_tm");
 }
 
@@ -2089,6 +2127,11 @@ int deliver_frontier_import(gsim_handle* h, int64_t round, const uint64_t* in, i
 
 // The delivery kernel changed (gsim_set_kernel_variant): the fresh bits are
 // kept only by the topic-major one.
+void deliver_blocks_changed(gsim_handle* h)
+{
+    h->dl->tm_cn = -1;          // the next k_send_tm launch rebuilds its block table
+}
+
 int deliver_variant_changed(gsim_handle* h)
 {
     Deliver* d = h->dl;
@@ -2149,6 +2192,8 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_fresh, ring * ((CN + 63) / 64) * 8);
     A((void**)&d->d_fsum, ring * (((CN + 63) / 64 + 63) / 64) * 8);
     A((void**)&d->d_mmask, T * N * 8);
+    A((void**)&d->d_tmtab, (2 * 64 + 1) * 4);
+    d->tm_cn = -1;
     A((void**)&d->d_mpub, ring * 4);
     A((void**)&d->d_roff, (size_t)cfg->rounds * 8);
     A((void**)&d->d_lastput, T * N * 4);

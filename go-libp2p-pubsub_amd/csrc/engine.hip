@@ -866,6 +866,9 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
         bool all = subs != nullptr;
         for (int64_t i = 0; all && i < n; ++i) all = (subs[i] & tmask) == tmask;
         h->all_joined = all;
+        h->topic_subs.assign((size_t)std::max(1, h->t), 0);
+        for (int64_t i = 0; subs && i < n; ++i)
+            for (uint64_t b = subs[i] & tmask; b; b &= b - 1) h->topic_subs[__builtin_ctzll(b)]++;
     }
     if (outbound) up(h->d_outbound, outbound, (size_t)E); else zero(h->d_outbound, (size_t)E);
     zero(h->d_direct, (size_t)E);
@@ -1076,6 +1079,12 @@ int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant)
     if (which == 5) {           // topic-major committed bits: 0 = in LDS while they fit, 1 = read from HBM
         if (variant < 0 || variant > 1) { h->err = "unknown staging choice (0 or 1)"; return GSIM_EINVAL; }
         h->tm_stage = variant == 1 ? 0 : -1;
+        return GSIM_OK;
+    }
+    if (which == 6) {           // topic-major blocks: 0 = shared out by subscribers, 1 = the same per topic
+        if (variant < 0 || variant > 1) { h->err = "unknown block share (0 or 1)"; return GSIM_EINVAL; }
+        h->tm_uniform = variant == 1;
+        if (h->dl) deliver_blocks_changed(h);
         return GSIM_OK;
     }
     h->err = "unknown kernel variant class";

@@ -213,6 +213,8 @@ struct gsim_handle {
     // topics only), so they stay zero and the score pass may skip them.
     bool unjoined_zero = false;
     bool all_joined = false;     // every peer announced every topic (nothing to skip)
+    std::vector<int64_t> topic_subs;   // [T] local peers that joined each topic (k_send_tm's block shares)
+    bool tm_uniform = false;  // k_send_tm blocks the same for every topic (gsim_set_kernel_variant(h, 6, 1))
     int send_variant = 3;     // delivery kernel variant (gsim_set_kernel_variant(h, 2, v)); 3 = topic-major
     int ihave_w = 0;          // k_ihave lane group width (gsim_set_kernel_variant(h, 3, w)); 0 = by row lengths
     int tm_stage = -1;        // k_send_tm committed bits (gsim_set_kernel_variant(h, 5, v)): -1 LDS while they fit, 0 HBM
@@ -346,6 +348,7 @@ int32_t* deliver_slot_last(gsim_handle* h);           // [ring]
 int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32_t* d_cnt, int64_t cap);
 int deliver_frontier_import(gsim_handle* h, int64_t round, const uint64_t* in, int64_t n);
 int deliver_variant_changed(gsim_handle* h);          // gsim_set_kernel_variant(h, 2, v)
+void deliver_blocks_changed(gsim_handle* h);          // gsim_set_kernel_variant(h, 6, v)
 // heartbeat.hip: the control inbox ([2][T][E] by round parity) and its per-receiver summary ([2][N])
 uint8_t* extra_ctl(gsim_handle* h);
 uint64_t* extra_cany(gsim_handle* h);

@@ -444,7 +444,9 @@ int gsim_profile_read(gsim_handle* h, double* ms, int64_t* launches, int32_t n);
  * thread per edge (the forwarders' mesh edges flattened), 2 = a lane group
  * per row.  which = 5: the topic-major kernel's committed bits: 0
  * (default) staged in LDS while a slot's bits fit (<= ~10^6 receivers), 1
- * always read from HBM. */
+ * always read from HBM.  which = 6: the topic-major kernel's blocks: 0
+ * (default) shared out among the topics by their subscribers, 1 the same
+ * number for every topic. */
 int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant);
 
 /* ---- synthetic inputs -------------------------------- */

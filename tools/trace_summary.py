@@ -1,6 +1,6 @@
 """Summarise a rocprofv3 kernel trace (csv): per-kernel time per tick per
 shard over the timed ticks (the warmup tick's dispatches are dropped: the
-trace starts at the (shards+1)-th heartbeat dispatch)."""
+trace starts at the (shards+1)-th refresh dispatch, one per tick and shard)."""
 import collections
 import csv
 import sys
@@ -9,7 +9,7 @@ import sys
 def main(path, shards, ticks):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    hb = [i for i, r in enumerate(rows) if "k_heartbeat<" in r["Kernel_Name"]]
+    hb = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("void k_refresh_score<true")]
     rows = rows[hb[shards]:] if len(hb) > shards else rows
     agg, cnt = collections.Counter(), collections.Counter()
     for r in rows:
