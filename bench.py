@@ -165,10 +165,6 @@ def build_engine(cfg, seed, device, scen=None, shard=None):
         eng.set_peer_behaviour(beh)
     if os.environ.get("GSIM_SEND_VARIANT") and shard is None:   # A/B of the delivery kernel (gsim.h)
         eng.set_kernel_variant(2, int(os.environ["GSIM_SEND_VARIANT"]))
-    if os.environ.get("GSIM_TM_WALK"):                           # topic-major walk: 1 per edge, 2 per row
-        eng.set_kernel_variant(4, int(os.environ["GSIM_TM_WALK"]))
-    if os.environ.get("GSIM_TM_HBM"):                            # topic-major committed bits from HBM
-        eng.set_kernel_variant(5, int(os.environ["GSIM_TM_HBM"]))
     if os.environ.get("GSIM_TM_UNIFORM"):                        # topic-major blocks the same per topic
         eng.set_kernel_variant(6, int(os.environ["GSIM_TM_UNIFORM"]))
     return eng, net

@@ -622,48 +622,51 @@ __global__ __launch_bounds__(256) void k_mesh_mask(const uint32_t* row_ptr, cons
     }
 }
 
-// Delivery round g, topic-major.  Block (p, t) walks the
-// frontier senders of peer range p for every active slot of topic t: the
-// slot's committed bits are staged in LDS first, so the duplicate test of a
-// copy to a receiver seen in an earlier round is an LDS read instead of a
-// random HBM access.  Requires every claim of round g-1 committed (k_commit
-// runs first), so the LDS snapshot holds every receiver seen before round g.
+// Delivery round g, topic-major.  Block (range, topic)
+// walks the forwarders of its peer range for every active slot of topic t.
+// It takes each chunk of the range once and gathers there the forwarders of
+// all the topic's active slots (64 slots per pass), so a round with many
+// sparse slots (c5: a few forwarders per slot and chunk) walks one frontier
+// per chunk, not one per slot and chunk.  Requires every claim of round g-1
+// committed (k_commit runs first): the committed bits then hold every
+// receiver seen before round g.
+//
 // Records a block updates — meshMessageDeliveries / invalid of the receivers'
 // records about its senders (record order: the senders' rows), per topic —
-// belong to this block alone; slots of one topic are walked one after the
-// other.  Results are identical to k_send's.
+// belong to this block alone.  A sender fresh in several slots of the topic
+// would update them from several lanes at once, so its slots are taken in
+// layers (layer l: each peer's l-th slot of the pass), one after the other.
+// Results are identical to k_send's.
 //
-// The frontier of a chunk (its senders' fresh bits) is flattened into its
-// edges: a prefix sum of the senders' row lengths in LDS, one thread per
-// edge (binary search for the edge's sender), so rows of any length keep
-// every lane busy — a shard's short rows (owned rows cut to their owned
-// receivers, ghost rows) as much as power-law hubs.
+// A chunk's frontier is flattened into its edges: a prefix sum of the
+// senders' walk lengths in LDS, one thread per edge (binary search for the
+// edge's sender), so rows of any length keep every lane busy — a shard's
+// short rows (owned rows cut to their owned receivers, ghost rows) as much as
+// power-law hubs.  Forwarders walk their mesh mask (rows <= 64), the origin
+// and hubs their whole row.
+constexpr int kTsSlots = 64;
 
-// W: 0 one thread per edge; 16 / 32 / 64: W lanes per row.  kTmThreads: the
-// block (1024 with the committed bits in LDS: one block per CU anyway; 512
-// reading them from HBM: three blocks per CU).
-template <int W, int kTmThreads>
-__global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t stage)
+template <int kTmThreads>
+__global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a)
 {
-    // [nws] committed bits of the receivers' words (stage: more receivers than
-    // fit in LDS read them from HBM instead), then [ring] u16 slots
     extern __shared__ uint64_t s_dyn[];
-    const int64_t wlo = (int64_t)a.rlo >> 6, nws = (((int64_t)a.rhi + 63) >> 6) - wlo;
-    uint16_t* s_slots = reinterpret_cast<uint16_t*>(s_dyn + (stage ? nws : 0));
-    constexpr int kTmChunk = 2 * kTmThreads;                 // peers per frontier chunk (two per thread)
-    constexpr int kWv = kTmThreads / 64;                     // waves per block
+    uint16_t* s_slots = reinterpret_cast<uint16_t*>(s_dyn);  // [ring] active slots of topic t
+    constexpr int kTmChunk = 2 * kTmThreads;                 // peers per chunk (two per thread)
+    constexpr int kWv = kTmThreads / 64;
     constexpr uint64_t kChunkWords = (1ull << (kTmChunk / 64)) - 1;
     __shared__ uint32_t s_front[kTmChunk];                   // frontier senders
     __shared__ uint32_t s_from[kTmChunk];                    // their first senders
-    __shared__ uint32_t s_off[kTmChunk];                     // first flattened edge of each sender (rows: its length)
+    __shared__ uint32_t s_off[kTmChunk];                     // first flattened edge of each sender
     __shared__ uint32_t s_beg[kTmChunk];                     // its row's first edge (sedge: first entry)
     __shared__ uint64_t s_msk[kTmChunk];                     // its mesh mask (0: the whole row)
-    __shared__ uint32_t s_wsum[64];                          // per-wave sums and their prefixes
-    __shared__ int s_ns, s_nf, s_claimed;
+    __shared__ uint8_t s_sk[kTmChunk];                       // its slot (index in the pass)
+    __shared__ uint32_t s_wsum[64];
+    __shared__ uint32_t s_m[kTsSlots], s_org[kTsSlots];      // the pass's slots and their origins
+    __shared__ uint8_t s_vd[kTsSlots], s_ow[kTsSlots], s_wa[kTsSlots];
+    __shared__ int s_ns, s_nf;
     __shared__ uint32_t s_ne;
+    __shared__ unsigned long long s_clm;                     // slots of the pass with a new claim
     __shared__ unsigned long long s_stats[4];
-    // the block's topic and peer range: topics get blocks in proportion to
-    // their subscribers (tmtab, launch_send_tm_tb)
     int32_t t = 0;
     {
         int32_t r = a.T > 0 ? a.T : 1;
@@ -673,14 +676,13 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t sta
         }
     }
     const int64_t range = a.tmtab[(a.T > 0 ? a.T : 1) + 1 + t];
-    // senders: the peers with cells, [clo, clo + CN)
     const int64_t pend_ = (int64_t)a.clo + a.CN;
     const int64_t lo = (int64_t)a.clo + (int64_t)(blockIdx.x - a.tmtab[t]) * range;
     const int64_t hi = lo + range < pend_ ? lo + range : pend_;
+    const int64_t wlo = (int64_t)a.rlo >> 6;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     if (tid == 0) { s_ns = 0; s_stats[0] = s_stats[1] = s_stats[2] = s_stats[3] = 0; }
     __syncthreads();
-    // active slots of topic t (new claims, or a publication, in round g-1)
     for (int m = tid; m < a.ring; m += kTmThreads) {
         if (((a.nnew_prev[m >> 5] >> (m & 31)) & 1u) && (int32_t)a.mtopic[m] == t) {
             const int q = atomicAdd(&s_ns, 1);
@@ -698,233 +700,251 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a, int32_t sta
     const uint32_t claim_hi = kClaim | (par << 30);
     const uint32_t clo = a.clo;
     unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
-    for (int k = 0; k < ns; ++k) {
-        const uint32_t m = s_slots[k];
-        const int64_t row_m = (int64_t)m * a.CN;
-        const uint32_t origin = a.morigin[m];
-        const uint8_t vd = a.minv[m];
-        const bool inv = vd != GSIM_VERDICT_ACCEPT;
-        const bool pen = verdict_penalises(vd), seeable = vd != GSIM_VERDICT_SIGNATURE;
-        const uint8_t o_want = (origin < a.N && ((a.sub[origin] >> t) & 1ull)) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
-        const bool win_all = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
-        // stage the slot's committed bits (receivers' words)
-        const uint64_t* s_bm = stage ? s_dyn : a.seenbm + (int64_t)m * a.nw + wlo;
-        if (stage)
-            for (int64_t w = tid; w < nws; w += kTmThreads) s_dyn[w] = a.seenbm[(int64_t)m * a.nw + wlo + w];
-        if (tid == 0) s_claimed = 0;
-        const unsigned long long first_before = n_first;
+    for (int k0 = 0; k0 < ns; k0 += kTsSlots) {
+        const int nb = ns - k0 < kTsSlots ? ns - k0 : kTsSlots;
+        if (tid < nb) {
+            const uint32_t m = s_slots[k0 + tid], origin = a.morigin[m];
+            s_m[tid] = m;
+            s_org[tid] = origin;
+            s_vd[tid] = a.minv[m];
+            s_ow[tid] = (origin < a.N && ((a.sub[origin] >> t) & 1ull)) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
+            s_wa[tid] = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
+        }
+        if (tid == 0) s_clm = 0;
+        uint64_t clm = 0;
         __syncthreads();
-        // each chunk's frontier comes from the slot's fresh bits: the peers
-        // that first saw the message in round g-1 and forward it (an accepted
-        // copy k_commit committed, the publication, a ghost's import), cleared
-        // as they are read; only those peers' cells and rows are loaded
-        uint64_t* fresh_m = a.fresh + (int64_t)m * a.nw;
-        uint64_t* fsum_m = a.fsum + (int64_t)m * a.nsw;
         for (int64_t c0 = lo; c0 < hi; c0 += kTmChunk) {
-            // the chunk's 32 fresh words in the summary (ranges start on whole
-            // chunks): a chunk with none is skipped without touching them
+            // the pass's slots with fresh bits in the chunk: every wave
+            // computes the same ballot from the summary words
             const int64_t cw0 = (c0 - clo) >> 6;
-            const uint64_t cbits = (fsum_m[cw0 >> 6] >> (cw0 & 63)) & kChunkWords;
-            if (!cbits) continue;                                // block-uniform
-            // thread tid: peers x0, x0 + 1 of the chunk (ranges start on whole
-            // words; 32 threads share a word)
+            bool nzs = false;
+            if (lane < nb)
+                nzs = ((a.fsum[(int64_t)s_m[lane] * a.nsw + (cw0 >> 6)] >> (cw0 & 63)) & kChunkWords) != 0;
+            const uint64_t cm = __ballot(nzs);
+            if (!cm) continue;                                   // block-uniform
+            // thread tid: peers x0, x0 + 1; pm[u] bit k: fresh in the pass's slot k
             const int64_t x0 = c0 + 2 * (int64_t)tid;
-            uint64_t word = 0;
-            uint32_t fb = 0;
+            const int64_t wi = (x0 - clo) >> 6;
+            const int sh = (int)((x0 - clo) & 63);
+            const uint32_t vmask = x0 + 1 < hi ? 3u : 1u;
+            uint64_t pm[2] = {0, 0}, nzk = 0;
             if (x0 < hi) {
-                word = fresh_m[(x0 - clo) >> 6];
-                fb = (uint32_t)(word >> ((x0 - clo) & 63)) & (x0 + 1 < hi ? 3u : 1u);
-            }
-            uint32_t len2[2] = {0, 0}, beg2[2] = {0, 0}, from2[2] = {0, 0};
-            uint64_t msk2[2] = {0, 0};
+                uint64_t b = cm;
+                while (b) {
+                    int kk[4];
+                    uint64_t wv[4];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                if ((fb >> u) & 1u) {
-                    const uint32_t x = (uint32_t)(x0 + u);
-                    from2[u] = (uint32_t)a.cell[row_m + (x - clo)] & kPeerMask;
-                    const uint32_t rb = a.row_ptr[x], deg = a.row_ptr[x + 1] - rb;
-                    if (deg <= 64 && x != origin) {
-                        // a forwarder sends on its mesh (and direct) edges only
-                        msk2[u] = a.mmask[(int64_t)t * a.N + x];
-                        beg2[u] = rb;
-                        len2[u] = (uint32_t)__popcll(msk2[u]);
-                        if (!msk2[u]) len2[u] = 0;
-                    } else {
-                        // the origin (fanout / flood publish) and hubs: the whole row
-                        const uint32_t* rp = a.sptr ? a.sptr : a.row_ptr;
-                        beg2[u] = rp[x];
-                        len2[u] = rp[x + 1] - beg2[u];
+                    for (int q = 0; q < 4; ++q) {
+                        kk[q] = b ? __builtin_ctzll(b) : -1;
+                        if (b) b &= b - 1;
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) wv[q] = kk[q] >= 0 ? a.fresh[(int64_t)s_m[kk[q]] * a.nw + wi] : 0ull;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if (kk[q] < 0) continue;
+                        const uint32_t f = (uint32_t)(wv[q] >> sh) & vmask;
+                        if (wv[q]) nzk |= 1ull << kk[q];
+                        if (f & 1u) pm[0] |= 1ull << kk[q];
+                        if (f & 2u) pm[1] |= 1ull << kk[q];
                     }
                 }
             }
-            // block scan of (forwarders, edges): the frontier in peer order
-            uint32_t vc = (uint32_t)__popc(fb), ve = len2[0] + len2[1];
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t yc = (uint32_t)__shfl_up((int)vc, o, 64), ye = (uint32_t)__shfl_up((int)ve, o, 64);
-                if (lane >= o) { vc += yc; ve += ye; }
-            }
-            if (lane == 63) { s_wsum[wid] = vc; s_wsum[16 + wid] = ve; }
-            __syncthreads();
-            if (tid < 64) {
-                const uint32_t c = tid < kWv ? s_wsum[tid] : 0u, e = tid < kWv ? s_wsum[16 + tid] : 0u;
-                uint32_t ic = c, ie = e;
-                for (int o = 1; o < kWv; o <<= 1) {
-                    const uint32_t yc = (uint32_t)__shfl_up((int)ic, o, 64), ye = (uint32_t)__shfl_up((int)ie, o, 64);
-                    if (lane >= o) { ic += yc; ie += ye; }
-                }
-                if (tid < kWv) { s_wsum[32 + tid] = ic - c; s_wsum[48 + tid] = ie - e; }
-                if (tid == kWv - 1) { s_nf = (int)ic; s_ne = ie; }
-            }
-            __syncthreads();
-            {
-                uint32_t q = s_wsum[32 + wid] + vc - (uint32_t)__popc(fb);
-                uint32_t off = s_wsum[48 + wid] + ve - (len2[0] + len2[1]);
+            bool first_layer = true;
+            for (;;) {
+                const uint32_t fb = (pm[0] ? 1u : 0u) | (pm[1] ? 2u : 0u);
+                uint32_t len2[2] = {0, 0}, beg2[2] = {0, 0}, from2[2] = {0, 0}, k2[2] = {0, 0};
+                uint64_t msk2[2] = {0, 0};
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
                     if ((fb >> u) & 1u) {
-                        s_front[q] = (uint32_t)(x0 + u);
-                        s_from[q] = from2[u];
-                        s_off[q] = W == 0 ? off : len2[u];
-                        s_beg[q] = beg2[u];
-                        s_msk[q] = msk2[u];
-                        ++q;
-                        off += len2[u];
+                        k2[u] = (uint32_t)__builtin_ctzll(pm[u]);
+                        const uint32_t x = (uint32_t)(x0 + u), m = s_m[k2[u]];
+                        from2[u] = (uint32_t)a.cell[(int64_t)m * a.CN + (x - clo)] & kPeerMask;
+                        const uint32_t rb = a.row_ptr[x], deg = a.row_ptr[x + 1] - rb;
+                        if (deg <= 64 && x != s_org[k2[u]]) {
+                            msk2[u] = a.mmask[(int64_t)t * a.N + x];
+                            beg2[u] = rb;
+                            len2[u] = (uint32_t)__popcll(msk2[u]);
+                        } else {
+                            const uint32_t* rp = a.sptr ? a.sptr : a.row_ptr;
+                            beg2[u] = rp[x];
+                            len2[u] = rp[x + 1] - beg2[u];
+                        }
                     }
                 }
-                // the bits are read: clear them (one thread per nonzero word)
-                if (word && ((x0 - clo) & 63) == 0) fresh_m[(x0 - clo) >> 6] = 0;
-                if (tid == 0)
-                    atomicAnd(reinterpret_cast<unsigned long long*>(fsum_m + (cw0 >> 6)), ~(kChunkWords << (cw0 & 63)));
-            }
-            __syncthreads();
-            const int nf = s_nf;
-            const uint32_t ne = s_ne;
-            if (nf == 0) continue;                               // block-uniform
-            constexpr int P = 2;
-            constexpr int G = W ? 64 / W : 1;                    // row groups per wave
-            constexpr uint32_t kPerIt = W ? (kTmThreads / 64) * G * P : kTmThreads * P;
-            const uint32_t n_it = ((W ? (uint32_t)nf : ne) + kPerIt - 1) / kPerIt;
-            for (uint32_t it = 0; it < n_it; ++it) {
-                uint32_t jv[P], fv[P], ev[P], iv[P], nv[P];
-                uint8_t mfv[P], dsv[P], tfv[P];
-                bool vv[P];
-                double xv[P];
+                uint32_t vc = (uint32_t)__popc(fb), ve = len2[0] + len2[1];
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t yc = (uint32_t)__shfl_up((int)vc, o, 64), ye = (uint32_t)__shfl_up((int)ve, o, 64);
+                    if (lane >= o) { vc += yc; ve += ye; }
+                }
+                if (lane == 63) { s_wsum[wid] = vc; s_wsum[16 + wid] = ve; }
+                __syncthreads();
+                if (tid < 64) {
+                    const uint32_t c = tid < kWv ? s_wsum[tid] : 0u, e = tid < kWv ? s_wsum[16 + tid] : 0u;
+                    uint32_t ic = c, ie = e;
+                    for (int o = 1; o < kWv; o <<= 1) {
+                        const uint32_t yc = (uint32_t)__shfl_up((int)ic, o, 64), ye = (uint32_t)__shfl_up((int)ie, o, 64);
+                        if (lane >= o) { ic += yc; ie += ye; }
+                    }
+                    if (tid < kWv) { s_wsum[32 + tid] = ic - c; s_wsum[48 + tid] = ie - e; }
+                    if (tid == kWv - 1) { s_nf = (int)ic; s_ne = ie; }
+                }
+                __syncthreads();
+                {
+                    uint32_t q = s_wsum[32 + wid] + vc - (uint32_t)__popc(fb);
+                    uint32_t off = s_wsum[48 + wid] + ve - (len2[0] + len2[1]);
 #pragma unroll
-                for (int u = 0; u < P; ++u) {
-                    int q = 0;
-                    uint32_t fi = 0;
-                    if constexpr (W == 0) {
-                        // flat: one thread per edge; its sender is the last
-                        // whose first edge is <= fi
-                        fi = it * kPerIt + (uint32_t)(u * kTmThreads + tid);
-                        vv[u] = fi < ne;
-                        if (vv[u]) {
-                            int l = 0, r = nf;
-                            while (r - l > 1) {
-                                const int mid = (l + r) >> 1;
-                                if (s_off[mid] <= fi) l = mid; else r = mid;
+                    for (int u = 0; u < 2; ++u) {
+                        if ((fb >> u) & 1u) {
+                            s_front[q] = (uint32_t)(x0 + u);
+                            s_from[q] = from2[u];
+                            s_off[q] = off;
+                            s_beg[q] = beg2[u];
+                            s_msk[q] = msk2[u];
+                            s_sk[q] = (uint8_t)k2[u];
+                            ++q;
+                            off += len2[u];
+                        }
+                    }
+                    if (first_layer) {
+                        // the bits are read: clear them (one thread per word)
+                        if (((x0 - clo) & 63) == 0)
+                            for (uint64_t b = nzk; b; b &= b - 1)
+                                a.fresh[(int64_t)s_m[__builtin_ctzll(b)] * a.nw + wi] = 0;
+                        if (tid < nb && ((cm >> tid) & 1ull))
+                            atomicAnd(reinterpret_cast<unsigned long long*>(a.fsum + (int64_t)s_m[tid] * a.nsw + (cw0 >> 6)),
+                                      ~(kChunkWords << (cw0 & 63)));
+                    }
+                }
+                __syncthreads();
+                const int nf = s_nf;
+                const uint32_t ne = s_ne;
+                if (nf > 0) {
+                    constexpr int P = 2;
+                    constexpr uint32_t kPerIt = kTmThreads * P;
+                    const uint32_t n_it = (ne + kPerIt - 1) / kPerIt;
+                    for (uint32_t it = 0; it < n_it; ++it) {
+                        uint32_t jv[P], fv[P], ev[P], iv[P], nv[P], kv[P];
+                        uint8_t mfv[P], dsv[P], tfv[P];
+                        bool vv[P];
+                        double xv[P];
+#pragma unroll
+                        for (int u = 0; u < P; ++u) {
+                            const uint32_t fi = it * kPerIt + (uint32_t)(u * kTmThreads + tid);
+                            int q = 0;
+                            vv[u] = fi < ne;
+                            if (vv[u]) {
+                                int l = 0, r = nf;
+                                while (r - l > 1) {
+                                    const int mid = (l + r) >> 1;
+                                    if (s_off[mid] <= fi) l = mid; else r = mid;
+                                }
+                                q = l;
                             }
-                            q = l;
+                            jv[u] = vv[u] ? s_front[q] : 0u;
+                            fv[u] = vv[u] ? s_from[q] : 0u;
+                            kv[u] = vv[u] ? s_sk[q] : 0u;
+                            const uint32_t k = fi - s_off[q];
+                            const uint64_t msk = s_msk[q];
+                            if (msk) ev[u] = s_beg[q] + kth_bit(msk, k);
+                            else if (a.sedge && vv[u]) ev[u] = a.sedge[s_beg[q] + k];
+                            else ev[u] = s_beg[q] + k;
                         }
-                    } else {
-                        // row groups: W lanes walk one sender's row (rows <= W)
-                        q = (int)(it * kPerIt) + (wid * G + lane / W) * P + u;
-                        const bool vq = q < nf;
-                        if (!vq) q = 0;
-                        vv[u] = vq && (uint32_t)(lane % W) < s_off[q];
-                        fi = (uint32_t)(lane % W);
-                    }
-                    jv[u] = vv[u] ? s_front[q] : 0u;
-                    fv[u] = vv[u] ? s_from[q] : 0u;
-                    // the k-th edge of the sender: k-th mesh position, or the
-                    // k-th edge of the whole row (through sedge on a shard)
-                    const uint32_t k = W == 0 ? fi - s_off[q] : fi;
-                    const uint64_t msk = s_msk[q];
-                    if (msk) ev[u] = s_beg[q] + kth_bit(msk, k);
-                    else if (a.sedge && vv[u]) ev[u] = a.sedge[s_beg[q] + k];
-                    else ev[u] = s_beg[q] + k;
-                }
 #pragma unroll
-                for (int u = 0; u < P; ++u) {
-                    iv[u] = 0; mfv[u] = 0; dsv[u] = 0; tfv[u] = 0; nv[u] = 0; xv[u] = 0.0;
-                    if (vv[u]) {
-                        const uint32_t e = ev[u];
-                        iv[u] = a.col[e]; mfv[u] = a.mflags[plane + e]; dsv[u] = a.dstate[e]; tfv[u] = a.tflags[plane + e];
-                        if (pen) xv[u] = a.invalid[plane + e]; else if (!inv) nv[u] = a.mcnt[plane + e];
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < P; ++u) {
-                    const uint32_t j = jv[u], e = ev[u], i = iv[u];
-                    const uint8_t ds = dsv[u], tf = tfv[u];
-                    bool sel = (mfv[u] & (j == origin ? o_want : GSIM_TF_MESH)) != 0;
-                    if (a.flood && vv[u] && j == origin)
-                        sel = ((a.sub[i] >> t) & 1ull) &&
-                              ((a.sharded && (j < a.rlo || j >= a.rhi)) ? a.pgate[e] != 0
-                                                                        : a.score[a.rev[e]] >= a.pub_thr);
-                    // direct peers that joined the topic always get it (gossipsub.go:991-1003)
-                    if (vv[u] && (ds & GSIM_DS_DIRECT) && !sel) sel = (a.sub[i] >> t) & 1ull;
-                    const bool tg = vv[u] && sel && (ds & GSIM_DS_CONNECTED) && i != fv[u] && i != origin;
-                    // a ghost receiver's shard pulls this copy from the frontier
-                    // export (it walks this sender's ghost row there)
-                    const bool remote = i < a.rlo || i >= a.rhi;
-                    const uint32_t ic = i - clo;
-                    const bool ok = tg && !remote && (ds & GSIM_DS_ACCEPT);
-                    n_gray += tg && !remote && !ok;              // AcceptFrom: graylisted sender
-                    n_acc += ok;
-                    if (!ok) continue;
-                    const bool sc = scored_t && (ds & GSIM_DS_TRACKED);
-                    const int64_t bw = ((int64_t)i >> 6) - wlo;
-                    const bool known = ((s_bm[bw] >> (i & 63)) & 1ull) &&
-                                       (win_all || !sc || inv || !(tf & GSIM_TF_IN_MESH));
-                    const uint64_t c = known ? 0ull : a.cell[row_m + ic];
-                    const uint32_t chi = (uint32_t)(c >> 32);
-                    int64_t seen_round = -1;
-                    if (known) seen_round = a.g - 1;             // any earlier round: only "in window" is used
-                    else if (c != kUnseen64) {
-                        if (!(chi & kClaim)) seen_round = chi;
-                        else if (((chi >> 30) & 1u) != par) seen_round = a.g - 1;
-                    }
-                    if (seeable && seen_round < 0 && (c == kUnseen64 || (chi & kEdgeMask) > e)) {
-                        uint32_t lo_w = j;
-                        if (sc && !inv) {
-                            lo_w |= kCreditFirst;
-                            if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo_w |= kCreditMesh;
-                        }
-                        const uint64_t cv = ((uint64_t)(claim_hi | e) << 32) | lo_w;
-                        const uint64_t prev = __hip_atomic_fetch_min(a.cell + row_m + ic, cv, __ATOMIC_RELAXED,
-                                                                     __HIP_MEMORY_SCOPE_AGENT);
-                        if (prev == kUnseen64) n_first++;
-                    }
-                    if (!sc) continue;
-                    const int64_t ir = plane + e;
-                    if (pen) {
-                        a.invalid[ir] = xv[u] + 1.0;                 // markInvalidMessageDelivery
-                    } else if (!inv && (tf & GSIM_TF_IN_MESH)) {
-                        const bool in_window = known ? true
-                                             : seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window)
-                                                               : (window >= 0);
-                        if (in_window) {
-                            uint32_t n = nv[u];
-                            if (n == 255u) {   // spill a full count into the counter (this lane owns the record)
-                                a.meshd[ir] = apply_incs(a.meshd[ir], n, mcap);
-                                n = 0;
+                        for (int u = 0; u < P; ++u) {
+                            iv[u] = 0; mfv[u] = 0; dsv[u] = 0; tfv[u] = 0; nv[u] = 0; xv[u] = 0.0;
+                            if (vv[u]) {
+                                const uint32_t e = ev[u];
+                                const uint8_t vd = s_vd[kv[u]];
+                                iv[u] = a.col[e]; mfv[u] = a.mflags[plane + e]; dsv[u] = a.dstate[e]; tfv[u] = a.tflags[plane + e];
+                                if (verdict_penalises(vd)) xv[u] = a.invalid[plane + e];
+                                else if (vd == GSIM_VERDICT_ACCEPT) nv[u] = a.mcnt[plane + e];
                             }
-                            a.mcnt[ir] = (uint8_t)(n + 1);
+                        }
+#pragma unroll
+                        for (int u = 0; u < P; ++u) {
+                            const uint32_t j = jv[u], e = ev[u], i = iv[u], k = kv[u];
+                            const uint32_t m = s_m[k], origin = s_org[k];
+                            const uint8_t vd = s_vd[k];
+                            const bool inv = vd != GSIM_VERDICT_ACCEPT;
+                            const bool pen = verdict_penalises(vd), seeable = vd != GSIM_VERDICT_SIGNATURE;
+                            const uint8_t ds = dsv[u], tf = tfv[u];
+                            bool sel = (mfv[u] & (j == origin ? s_ow[k] : GSIM_TF_MESH)) != 0;
+                            if (a.flood && vv[u] && j == origin)
+                                sel = ((a.sub[i] >> t) & 1ull) &&
+                                      ((a.sharded && (j < a.rlo || j >= a.rhi)) ? a.pgate[e] != 0
+                                                                                : a.score[a.rev[e]] >= a.pub_thr);
+                            if (vv[u] && (ds & GSIM_DS_DIRECT) && !sel) sel = (a.sub[i] >> t) & 1ull;
+                            const bool tg = vv[u] && sel && (ds & GSIM_DS_CONNECTED) && i != fv[u] && i != origin;
+                            const bool remote = i < a.rlo || i >= a.rhi;
+                            const uint32_t ic = i - clo;
+                            const bool ok = tg && !remote && (ds & GSIM_DS_ACCEPT);
+                            n_gray += tg && !remote && !ok;
+                            n_acc += ok;
+                            if (!ok) continue;
+                            const bool sc = scored_t && (ds & GSIM_DS_TRACKED);
+                            const uint64_t* s_bm = a.seenbm + (int64_t)m * a.nw + wlo;
+                            const int64_t bw = ((int64_t)i >> 6) - wlo;
+                            const bool known = ((s_bm[bw] >> (i & 63)) & 1ull) &&
+                                               (s_wa[k] || !sc || inv || !(tf & GSIM_TF_IN_MESH));
+                            const int64_t row_m = (int64_t)m * a.CN;
+                            const uint64_t c = known ? 0ull : a.cell[row_m + ic];
+                            const uint32_t chi = (uint32_t)(c >> 32);
+                            int64_t seen_round = -1;
+                            if (known) seen_round = a.g - 1;
+                            else if (c != kUnseen64) {
+                                if (!(chi & kClaim)) seen_round = chi;
+                                else if (((chi >> 30) & 1u) != par) seen_round = a.g - 1;
+                            }
+                            if (seeable && seen_round < 0 && (c == kUnseen64 || (chi & kEdgeMask) > e)) {
+                                uint32_t lo_w = j;
+                                if (sc && !inv) {
+                                    lo_w |= kCreditFirst;
+                                    if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo_w |= kCreditMesh;
+                                }
+                                const uint64_t cv = ((uint64_t)(claim_hi | e) << 32) | lo_w;
+                                const uint64_t prev = __hip_atomic_fetch_min(a.cell + row_m + ic, cv, __ATOMIC_RELAXED,
+                                                                             __HIP_MEMORY_SCOPE_AGENT);
+                                if (prev == kUnseen64) { n_first++; clm |= 1ull << k; }
+                            }
+                            if (!sc) continue;
+                            const int64_t ir = plane + e;
+                            if (pen) {
+                                a.invalid[ir] = xv[u] + 1.0;
+                            } else if (!inv && (tf & GSIM_TF_IN_MESH)) {
+                                const bool in_window = known ? true
+                                                     : seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window)
+                                                                       : (window >= 0);
+                                if (in_window) {
+                                    uint32_t n = nv[u];
+                                    if (n == 255u) {
+                                        a.meshd[ir] = apply_incs(a.meshd[ir], n, mcap);
+                                        n = 0;
+                                    }
+                                    a.mcnt[ir] = (uint8_t)(n + 1);
+                                }
+                            }
                         }
                     }
                 }
+                // the next layer: each peer's next slot
+                first_layer = false;
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    if (pm[u]) pm[u] &= pm[u] - 1;
+                if (!__syncthreads_or((pm[0] | pm[1]) != 0)) break;   // also: s_front is rewritten next
             }
-            __syncthreads();                                     // s_front is rewritten by the next chunk
         }
-        // the slot stays active next round if any copy claimed a new cell
-        if (n_first != first_before) s_claimed = 1;
+        // slots that stay active next round: a copy claimed a new cell
+        if (clm) atomicOr(&s_clm, (unsigned long long)clm);
         __syncthreads();
-        if (tid == 0 && s_claimed) {
+        if (tid < nb && ((s_clm >> tid) & 1ull)) {
+            const uint32_t m = s_m[tid];
             atomicOr(&a.nnew_cur[m >> 5], 1u << (m & 31));
-            atomicMax(&a.slot_last[m], (int32_t)a.g);            // mcache activity of the slot
+            atomicMax(&a.slot_last[m], (int32_t)a.g);
         }
-        __syncthreads();                                         // s_bm is rewritten by the next slot
+        __syncthreads();                                         // the pass's slot table is rewritten next
     }
     n_acc = wave_sum_u64(n_acc);
     n_gray = wave_sum_u64(n_gray);
@@ -1757,8 +1777,7 @@ int deliver_read_seen(gsim_handle* h, void* dst)
     return hip_check(h, e, "gsim_read_field(SEEN)");
 }
 
-template <int W, int TB>
-static int launch_send_tm_tb(gsim_handle* h, const RoundArgs& a, size_t lds, int32_t stage)
+static int launch_send_tm(gsim_handle* h, const RoundArgs& a)
 {
     // blocks per topic: about 2048 blocks in all (8 per CU over the launch at one
     // resident block per CU: smaller ranges even out the frontier work; measured
@@ -1766,7 +1785,10 @@ static int launch_send_tm_tb(gsim_handle* h, const RoundArgs& a, size_t lds, int
     // 21.1 / 21.3 ms per tick at C3, profiles/r01_ab_send_tm_blocks.log), ranges of
     // at least 4096 peers; at least 256 ranges per topic when there are many
     // topics (Zipf subscriptions skew them: the busy topics' blocks must still
-    // fill the chip; blocks of idle topics leave after the slot scan)
+    // fill the chip; blocks of idle topics leave after the slot scan).  c5 block
+    // budgets 4096 / 8192 / 15680 (default) / 32768 / 65536: 29.7 / 25.0 / 24.7 /
+    // 28.0 / 32.9 ms of send per tick (profiles/r02_ab_send_blocks.log)
+    constexpr int TB = 1024;
     constexpr int64_t total = 2048;
     constexpr int64_t chunk = 2 * TB;
     const int64_t cn = h->n;                 // every local peer sends (a shard's ghosts too)
@@ -1781,7 +1803,7 @@ static int launch_send_tm_tb(gsim_handle* h, const RoundArgs& a, size_t lds, int
         // ranges of whole chunks
         int64_t wsum = 0;
         for (int t = 0; t < T && !h->tm_uniform; ++t) wsum += t < (int)h->topic_subs.size() ? h->topic_subs[t] : 0;
-        const int64_t budget = ranges * T, max_blocks = (cn + chunk - 1) / chunk;
+        const int64_t budget = h->tm_budget ? h->tm_budget : ranges * T, max_blocks = (cn + chunk - 1) / chunk;
         d->tmtab.assign((size_t)(2 * T + 1), 0);
         uint32_t start = 0;
         for (int t = 0; t < T; ++t) {
@@ -1799,32 +1821,10 @@ static int launch_send_tm_tb(gsim_handle* h, const RoundArgs& a, size_t lds, int
         if (e != hipSuccess) return hip_check(h, e, "k_send_tm block table");
         d->tm_cn = cn;
     }
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_send_tm<W, TB>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return hip_check(h, e, "k_send_tm LDS attribute");
-    hipLaunchKernelGGL((k_send_tm<W, TB>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a, stage);
+    // the slot list in LDS
+    const size_t lds = ((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7;
+    hipLaunchKernelGGL((k_send_tm<TB>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_send_tm");
-}
-
-constexpr size_t kLdsBudget = 160 * 1024 - 50 * 1024;   // minus the static frontier buffers
-
-template <int W>
-static int launch_send_tm(gsim_handle* h, const RoundArgs& a, size_t lds)
-{
-    // the committed bits are staged in LDS while they fit, else read from HBM
-    const int32_t stage = (lds <= kLdsBudget && h->tm_stage != 0) ? 1 : 0;
-    if (!stage) lds = ((size_t)h->dl->cfg.ring * 2 + 7) & ~(size_t)7;
-    // 1024-thread blocks either way (512 with the bits in HBM: c5 43 against 30
-    // ms of delivery per tick)
-    return launch_send_tm_tb<W, 1024>(h, a, lds, stage);
-}
-
-// LDS of the topic-major kernel: the slot's committed bits + the slot list
-static size_t send_tm_lds(const gsim_handle* h, const Deliver* d)
-{
-    // the receivers' (owned peers') words of the committed bits, then the slot list
-    const int64_t nws = ((h->ohi() + 63) >> 6) - (h->olo() >> 6);
-    return (size_t)nws * 8 + (((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7);
 }
 
 template <int W>
@@ -1900,21 +1900,11 @@ int deliver_round_send(gsim_handle* h, int64_t round)
                                    std::max(1, h->t), (uint32_t)h->olo(), (uint32_t)h->ohi(), d->d_mmask);
                 d->mask_version = h->mesh_version;
             }
-            const size_t lds_tm = send_tm_lds(h, d);
-            // one thread per edge by default: forwarders walk only their mesh
-            // edges (a handful of a row's positions), so lane groups per row
-            // would idle most lanes (C3: 21.0 against 32.9 ms per tick,
-            // profiles/r02_ab_walk_masks.log); lane groups on request
-            const int64_t dmax = h->sh ? h->sh->send_max : h->max_degree;
-            const int Wr = dmax <= 16 ? 16 : dmax <= 32 ? 32 : dmax <= 64 ? 64 : 0;
-            if (Wr == 0 || h->send_variant_flat != 0)
-                rc = launch_send_tm<0>(h, a, lds_tm);
-            else if (Wr == 16)
-                rc = launch_send_tm<16>(h, a, lds_tm);
-            else if (Wr == 32)
-                rc = launch_send_tm<32>(h, a, lds_tm);
-            else
-                rc = launch_send_tm<64>(h, a, lds_tm);
+            // one thread per edge: forwarders walk only their mesh edges (a
+            // handful of a row's positions), so lane groups per row would idle
+            // most lanes (C3: 21.0 against 32.9 ms per tick,
+            // profiles/r02_ab_walk_masks.log)
+            rc = launch_send_tm(h, a);
             if (rc) return rc;
         } else if (h->max_degree <= 16)
             launch_send<16>(h, grid, lds, a);

@@ -1071,19 +1071,11 @@ int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant)
         h->ihave_w = variant;
         return GSIM_OK;
     }
-    if (which == 4) {           // topic-major walk: 0 = by row lengths, 1 = one thread per edge, 2 = lanes per row
-        if (variant < 0 || variant > 2) { h->err = "unknown topic-major walk (0, 1 or 2)"; return GSIM_EINVAL; }
-        h->send_variant_flat = variant == 0 ? -1 : variant == 1 ? 1 : 0;
-        return GSIM_OK;
-    }
-    if (which == 5) {           // topic-major committed bits: 0 = in LDS while they fit, 1 = read from HBM
-        if (variant < 0 || variant > 1) { h->err = "unknown staging choice (0 or 1)"; return GSIM_EINVAL; }
-        h->tm_stage = variant == 1 ? 0 : -1;
-        return GSIM_OK;
-    }
-    if (which == 6) {           // topic-major blocks: 0 = shared out by subscribers, 1 = the same per topic
-        if (variant < 0 || variant > 1) { h->err = "unknown block share (0 or 1)"; return GSIM_EINVAL; }
+    if (which == 6) {           // topic-major blocks: 0 = shared out by subscribers, 1 = the same per topic,
+                                // >= 64: shared out by subscribers, this many in all
+        if (variant < 0 || (variant > 1 && variant < 64)) { h->err = "unknown block share (0, 1 or >= 64)"; return GSIM_EINVAL; }
         h->tm_uniform = variant == 1;
+        h->tm_budget = variant >= 64 ? variant : 0;
         if (h->dl) deliver_blocks_changed(h);
         return GSIM_OK;
     }

@@ -215,10 +215,9 @@ struct gsim_handle {
     bool all_joined = false;     // every peer announced every topic (nothing to skip)
     std::vector<int64_t> topic_subs;   // [T] local peers that joined each topic (k_send_tm's block shares)
     bool tm_uniform = false;  // k_send_tm blocks the same for every topic (gsim_set_kernel_variant(h, 6, 1))
+    int64_t tm_budget = 0;    // k_send_tm blocks in all (0: ranges x T, launch_send_tm_tb)
     int send_variant = 3;     // delivery kernel variant (gsim_set_kernel_variant(h, 2, v)); 3 = topic-major
     int ihave_w = 0;          // k_ihave lane group width (gsim_set_kernel_variant(h, 3, w)); 0 = by row lengths
-    int tm_stage = -1;        // k_send_tm committed bits (gsim_set_kernel_variant(h, 5, v)): -1 LDS while they fit, 0 HBM
-    int send_variant_flat = -1;   // k_send_tm walk (gsim_set_kernel_variant(h, 4, v)): -1 by row lengths, 1 per edge, 0 per row
 
     // device: parameters and scratch flags
     gsim_topic_score_params* d_tp = nullptr;

@@ -437,16 +437,11 @@ int gsim_profile_read(gsim_handle* h, double* ms, int64_t* launches, int32_t n);
 /* Select an implementation variant of a hot-path kernel for A/B timing in
  * one process.  Results are identical across variants (the GPU tests run
  * each).  which = 2: the delivery kernel; variant 3 (default) is topic-major
- * with the slots' committed bits staged in LDS (used while they fit), 0 is
- * the peer-major k_send.  which = 3: the IHAVE walk's lane group width
- * (16, 32 or 64 lanes per row; 0 = chosen from the row lengths).  which = 4:
- * the topic-major walk over a round's forwarders: 1 (default, also 0) = one
- * thread per edge (the forwarders' mesh edges flattened), 2 = a lane group
- * per row.  which = 5: the topic-major kernel's committed bits: 0
- * (default) staged in LDS while a slot's bits fit (<= ~10^6 receivers), 1
- * always read from HBM.  which = 6: the topic-major kernel's blocks: 0
- * (default) shared out among the topics by their subscribers, 1 the same
- * number for every topic. */
+ * (k_send_tm), 0 the peer-major k_send.  which = 3: the IHAVE walk's lane
+ * group width (16, 32 or 64 lanes per row; 0 = chosen from the row lengths).
+ * which = 6: the topic-major kernel's blocks: 0 (default) shared out among
+ * the topics by their subscribers, 1 the same number for every topic, >= 64
+ * shared out by subscribers, this many in all. */
 int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant);
 
 /* ---- synthetic inputs -------------------------------- */

@@ -221,9 +221,9 @@ def _schedule(rng, ticks, T, R, rate, inv_frac, n):
 @pytest.mark.parametrize("n,k,T,ticks,rate,inv_frac,retained,ring,send_variant", [
     (1500, 16, 2, [1, 2, 3, 4], 6, 0.1, 0.0, 256, 3),       # default: topic-major delivery
     (3000, 32, 3, [14, 15, 16], 12, 0.05, 0.03, 512, 3),    # clearBackoff tick
-    (1500, 24, 2, [1, 2, 3, 4], 6, 0.1, 0.02, 256, 31),     # topic-major, one thread per edge
-    (1500, 24, 2, [1, 2, 3, 4], 6, 0.1, 0.02, 256, 32),     # topic-major, a lane group per row
-    (1500, 24, 2, [1, 2, 3, 4], 6, 0.1, 0.02, 256, 315),    # topic-major, committed bits read from HBM
+    (1500, 24, 2, [1, 2, 3, 4], 6, 0.1, 0.02, 256, 3),
+    (1200, 16, 2, [1, 2], 200, 0.1, 0.02, 1024, 3),         # > 64 active slots a topic: passes, layers
+    (1200, 16, 2, [1, 2], 200, 0.1, 0.02, 1024, 36),        # the same, blocks the same per topic
     (1500, 32, 2, [1, 2, 3], 8, 0.1, 0.02, 256, 0),         # peer-major k_send (same results)
     (1500, 24, 2, [1, 2, 3], 8, 0.1, 0.02, 256, 0),
     (3000, 32, 3, [14, 15, 16], 12, 0.05, 0.03, 512, 0),
@@ -253,10 +253,8 @@ def test_rounds_bit_exact(require_gpu, n, k, T, ticks, rate, inv_frac, retained,
     st.push_to_engine(eng)
     eng.msgs_init(ring, R, T0, HB)
     eng.set_kernel_variant(2, int(str(send_variant)[0]))
-    if send_variant >= 10:
-        eng.set_kernel_variant(4, int(str(send_variant)[1]))
-    if send_variant >= 100:
-        eng.set_kernel_variant(5, 1)
+    if send_variant == 36:
+        eng.set_kernel_variant(6, 1)
     sched = _schedule(rng, ticks, T, R, rate, inv_frac, n)
     lib = ob.load()
     for kk in ticks:
@@ -279,7 +277,9 @@ def test_rounds_bit_exact(require_gpu, n, k, T, ticks, rate, inv_frac, retained,
         assert eng.msg_stats() == msgs.stats, f"tick {kk}"
         seen = eng.read(_abi.F_SEEN)
         assert np.array_equal(seen, msgs.seen), f"seen-set differs at tick {kk}: {(seen != msgs.seen).sum()} cells"
-        assert np.array_equal(eng.read(_abi.F_LASTPUT), msgs.lastput)
+        lp, want = eng.read(_abi.F_LASTPUT).ravel(), np.asarray(msgs.lastput).ravel()
+        bad = np.nonzero(lp != want)[0]
+        assert len(bad) == 0, f"lastput differs at tick {kk}: {len(bad)} entries, e.g. {[(int(b), int(lp[b]), int(want[b])) for b in bad[:4]]}"
         gpu = ob.NetState(net, params, thresholds=th, gossip=gp)
         gpu.pull_from_engine(eng)
         assert_same(st, gpu)
