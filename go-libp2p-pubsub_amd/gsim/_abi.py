@@ -227,7 +227,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("GSIM_LIB") or LIB_PATH      # GSIM_LIB: another build, for A/B runs
     if not os.path.exists(p):
         raise ImportError(f"libgsim.so not built at {p}; run `make -C go-libp2p-pubsub_amd` "
                           "(the engine has no CPU fallback)")

@@ -1,18 +1,16 @@
 #!/bin/bash
-# GPU: parity tests (-m gpu), smoke, one bench line; each step under its own limit.
-# usage: tools/gpu_check.sh <tag> [pytest-args...]
+# GPU: the full -m gpu suite, then bench lines of the given configs.
+#   CONFIGS="c3 c5" tools/gpu_check.sh TAG
 set -euo pipefail
-TAG="${1:-check}"; shift || true
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-OUT="$ROOT/gpurun_out/$TAG"
+OUT="$ROOT/gpurun_out/${1:-check}"
 mkdir -p "$OUT"
 cd "$ROOT"
-echo "== pytest -m gpu"
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread "$@" > "$OUT/pytest_gpu.log" 2>&1 || { tail -60 "$OUT/pytest_gpu.log"; exit 1; }
-tail -2 "$OUT/pytest_gpu.log"
-echo "== smoke"
-timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -30 "$OUT/smoke.log"; exit 1; }
-tail -1 "$OUT/smoke.log"
-echo "== bench"
-timeout -k 10 400 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > "$OUT/bench.log" 2>&1 || { tail -30 "$OUT/bench.log"; exit 1; }
-tail -1 "$OUT/bench.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['ms_per_step'],2), {k: round(v,2) for k, v in d['kernel_ms_per_tick'].items()})"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
+  > "$OUT/pytest_gpu.log" 2>&1 || { grep -E "^E |FAILED|passed|failed" "$OUT/pytest_gpu.log" | head -30; exit 1; }
+tail -1 "$OUT/pytest_gpu.log"
+for c in ${CONFIGS:-c3}; do
+  timeout -k 10 300 python bench.py --config "$c" --steps "${STEPS:-10}" --warmup 2 --no-cpu-baseline \
+    > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err"
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], round(d['ms_per_step'],2), round(d['roofline']['frac'],4), {k: round(v,2) for k,v in d['kernel_ms_per_tick'].items() if v > 0.05})" "$OUT/bench_$c.json" "$c"
+done
