@@ -1,5 +1,7 @@
 #!/bin/bash
-# PMC passes over k_send (one counter group per pass, separate runs).
+# GPU: k_send_tm / k_commit request mix at C3 (one counter group per run,
+# kernel-trace only): TCP->TCC read / write / atomic requests and the SQ
+# instruction and wait counts, summed per launch.
 set -uo pipefail
 TAG="${1:-pmc_send}"
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -7,24 +9,28 @@ OUT="$ROOT/gpurun_out/$TAG"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-timeout -s KILL 60 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
 run() {
-  local name="$1"; shift
-  timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-include-regex "${KRE:-k_send}" -d "$OUT/$name" -o run --output-format csv \
+  local name="$1" kre="$2"; shift 2
+  timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-include-regex "$kre" -d "$OUT/$name" -o run --output-format csv \
     -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "$name rc=$rc"
   return $rc
 }
-run sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES && \
-run tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum
+run send_tcp "k_send_tm|k_commit" TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_TCC_ATOMIC_WITH_RET_REQ_sum TCP_TCC_ATOMIC_WITHOUT_RET_REQ_sum && \
+run send_sq "k_send_tm|k_commit" SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY || exit 1
 python3 - "$OUT" <<'PY'
-import csv, glob, os, sys, collections
+import csv, collections, glob, sys
 out = sys.argv[1]
-agg = collections.defaultdict(list)
-for p in glob.glob(os.path.join(out, "*", "**", "*counter_collection.csv"), recursive=True):
-    for r in csv.DictReader(open(p)):
-        agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
-for k, v in sorted(agg.items()):
-    print(f"{k:28s} n={len(v):4d} mean={sum(v)/len(v):.4g}")
+for grp in ("send_tcp", "send_sq"):
+    f = glob.glob(f"{out}/{grp}/**/*counter_collection.csv", recursive=True)
+    if not f:
+        print(grp, "no counter file"); continue
+    tot = collections.defaultdict(float); disp = collections.defaultdict(set)
+    for r in csv.DictReader(open(f[0])):
+        k = "k_send_tm" if "k_send_tm" in r["Kernel_Name"] else "k_commit"
+        tot[(k, r["Counter_Name"])] += float(r["Counter_Value"])
+        disp[k].add(r["Dispatch_Id"])
+    for (k, c), v in sorted(tot.items()):
+        print(f"{grp} {k} {c} per launch {v / max(1, len(disp[k])):.4g}")
 PY
