@@ -49,12 +49,7 @@
 
 namespace gsim {
 
-constexpr uint64_t kUnseen64 = ~0ull;
-constexpr uint32_t kClaim = 0x80000000u;
-constexpr uint32_t kEdgeMask = 0x3FFFFFFFu;       // claim edge bits (E < 2^30 - 1)
-constexpr uint32_t kCreditFirst = 0x80000000u;     // lo-word flag: winner's record gets P2
-constexpr uint32_t kCreditMesh = 0x40000000u;      // lo-word flag: ... and P3 (negative window)
-constexpr uint32_t kPeerMask = 0x3FFFFFFFu;
+// seen-set cell encoding: kUnseen64, kClaim, ... (gsim_internal.h)
 constexpr int kMaxRing = 8192;     // active-slot list lives in LDS (u16, sized by the ring)
 
 // The verdict of a message (gsim.h GSIM_VERDICT_*, stored in minv[slot]):
@@ -71,6 +66,7 @@ struct Deliver {
     gsim_msg_config cfg{};
     uint32_t *d_mtopic = nullptr, *d_morigin = nullptr;
     uint8_t* d_minv = nullptr;
+    uint64_t* d_mid = nullptr;         // [ring] gsim_msg.id of the slot's message (wire ids)
     uint64_t* d_cell = nullptr;        // [ring][N] seen-set cells (layout above)
     uint64_t* d_seenbm = nullptr;      // [ring][ceil(N/64)] bit: the cell is committed (a cache of the cells)
     uint64_t* d_fresh = nullptr;       // [ring][ceil(N/64)] bit: the peer forwards the slot's message next round
@@ -125,6 +121,7 @@ struct RoundArgs {
     uint8_t* mcnt;             // pending meshd increments, record order
     uint32_t *mtopic, *morigin;
     uint8_t* minv;
+    uint64_t* mid;             // [ring] gsim_msg ids (wire ids)
     uint64_t* cell;
     uint64_t* seenbm;          // [ring][nw] committed bits of the cells (read before a cell)
     uint64_t* fresh;           // [ring][nw] forwarders of the next round (topic-major delivery; nullptr otherwise)
@@ -306,6 +303,7 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, int32_t count)
     a.morigin[slot] = p.origin;          // local id (a shard: 0xFFFFFFFF when not a local peer)
     a.minv[slot] = p.verdict;
     a.mpub[slot] = (int32_t)a.g;
+    if (a.mid) a.mid[slot] = p.id;
     if (p.origin >= a.clo && (int64_t)(p.origin - a.clo) < a.CN) {   // the origin's own cell
         const uint32_t oc = p.origin - a.clo;
         a.cell[(int64_t)slot * a.CN + oc] = ((uint64_t)(uint32_t)a.g << 32) | p.origin;
@@ -1496,7 +1494,7 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_pair_cnt); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
@@ -1539,7 +1537,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.dstate = h->d_dstate; a.mflags = h->d_mflags;
     a.tflags = h->d_tflags; a.tp = h->d_tp;
     a.first = h->d_first; a.meshd = h->d_meshd; a.invalid = h->d_invalid; a.mcnt = h->d_mcnt;
-    a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv;
+    a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv; a.mid = d->d_mid;
     a.cell = d->d_cell; a.lastput = d->d_lastput;
     a.CN = h->n;
     a.clo = 0;
@@ -1578,6 +1576,19 @@ bool deliver_gossip_view(gsim_handle* h, GossipView* v)
     v->gsel = d->d_gsel;
     v->gstate = d->d_gstate;
     v->mmask = d->d_mmask;
+    return true;
+}
+
+bool deliver_wire_view(gsim_handle* h, WireView* v)
+{
+    Deliver* d = h->dl;
+    if (!d) return false;
+    v->cell = d->d_cell;
+    v->mtopic = d->d_mtopic; v->morigin = d->d_morigin; v->minv = d->d_minv; v->mid = d->d_mid;
+    v->slot_last = d->d_slot_last;
+    v->gsel = d->d_gsel;
+    v->ring = d->cfg.ring; v->rounds = d->cfg.rounds;
+    v->ihave_tick = d->ihave_tick;
     return true;
 }
 
@@ -2177,6 +2188,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_mtopic, ring * 4);
     A((void**)&d->d_morigin, ring * 4);
     A((void**)&d->d_minv, ring);
+    A((void**)&d->d_mid, ring * 8);
     A((void**)&d->d_cell, ring * CN * 8);
     A((void**)&d->d_seenbm, ring * ((CN + 63) / 64) * 8);
     A((void**)&d->d_fresh, ring * ((CN + 63) / 64) * 8);

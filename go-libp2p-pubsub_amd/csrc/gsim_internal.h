@@ -184,6 +184,16 @@ struct ShardCtx {
     uint32_t* h_counts = nullptr;          // pinned scratch for count readbacks
 };
 
+// Seen-set cells [ring][N] (deliver.hip): unseen; committed (hi = first-seen
+// round, lo = first sender); or claimed in round g (hi = kClaim | parity of g
+// << 30 | claiming edge, lo = sender | credit flags).
+constexpr uint64_t kUnseen64 = ~0ull;
+constexpr uint32_t kClaim = 0x80000000u;
+constexpr uint32_t kEdgeMask = 0x3FFFFFFFu;       // claim edge bits (E < 2^30 - 1)
+constexpr uint32_t kCreditFirst = 0x80000000u;     // lo-word flag: winner's record gets P2
+constexpr uint32_t kCreditMesh = 0x40000000u;      // lo-word flag: ... and P3 (negative window)
+constexpr uint32_t kPeerMask = 0x3FFFFFFFu;
+
 }  // namespace gsim
 
 struct gsim_handle {
@@ -328,6 +338,18 @@ struct GossipView {
     uint64_t* mmask;          // [T][N] delivery's mesh masks (rows <= 64), kept current by the router kernels
 };
 bool deliver_gossip_view(gsim_handle* h, GossipView* v);   // false before gsim_msgs_init
+// What the wire encoder reads of the message state (wire.hip)
+struct WireView {
+    const uint64_t* cell;      // [ring][N]
+    const uint32_t *mtopic, *morigin;
+    const uint8_t* minv;
+    const uint64_t* mid;       // [ring] gsim_msg ids
+    const int32_t* slot_last;  // [ring] last round with a new claim or the publication
+    const uint8_t* gsel;       // [T][E] emitGossip's targets (sender edge order)
+    int32_t ring, rounds;
+    int64_t ihave_tick;        // heartbeat whose gossip is pending, -1 none
+};
+bool deliver_wire_view(gsim_handle* h, WireView* v);     // false before gsim_msgs_init
 int deliver_promise_check(gsim_handle* h, int64_t now);    // broken promises -> pending P7
 int deliver_heartbeat_begin(gsim_handle* h, uint64_t tick); // fresh IHAVE marks
 uint64_t gsim_get_seed(const gsim_handle* h);              // heartbeat.hip

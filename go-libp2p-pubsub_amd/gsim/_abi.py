@@ -123,6 +123,57 @@ class CShardInfo(Structure):
 
 MAX_SHARDS = 64
 
+
+# ---- gsim_wire.h ------------------------------------------------------------------
+class CBytes(Structure):
+    _fields_ = [("p", c_void_p), ("n", c_uint32)]
+
+
+class CWireSub(Structure):
+    _fields_ = [("subscribe", c_int32), ("topic", CBytes)]
+
+
+class CWireMsg(Structure):
+    _fields_ = [("from_", CBytes), ("data", CBytes), ("seqno", CBytes), ("topic", CBytes), ("signature", CBytes),
+                ("key", CBytes)]
+
+
+class CWireIHave(Structure):
+    _fields_ = [("topic", CBytes), ("id0", c_uint32), ("nid", c_uint32)]
+
+
+class CWireIWant(Structure):
+    _fields_ = [("id0", c_uint32), ("nid", c_uint32)]
+
+
+class CWireGraft(Structure):
+    _fields_ = [("topic", CBytes)]
+
+
+class CWirePx(Structure):
+    _fields_ = [("peer", CBytes), ("record", CBytes)]
+
+
+class CWirePrune(Structure):
+    _fields_ = [("topic", CBytes), ("px0", c_uint32), ("npx", c_uint32), ("has_backoff", c_int32),
+                ("backoff", c_uint64)]
+
+
+class CWireRpc(Structure):
+    _fields_ = [("subs", c_void_p), ("nsubs", c_uint32), ("msgs", c_void_p), ("nmsgs", c_uint32),
+                ("has_control", c_int32), ("ihave", c_void_p), ("nihave", c_uint32), ("iwant", c_void_p),
+                ("niwant", c_uint32), ("graft", c_void_p), ("ngraft", c_uint32), ("prune", c_void_p),
+                ("nprune", c_uint32), ("ids", c_void_p), ("nids", c_uint32), ("px", c_void_p), ("npx", c_uint32)]
+
+
+class CWireNames(Structure):
+    _fields_ = [("topic_names", c_void_p), ("peer_ids", c_void_p), ("peer_id_len", c_uint32),
+                ("prune_backoff_s", c_uint64)]
+
+
+# numpy view of gsim_wire_ref (24 bytes)
+WIRE_REF_DTYPE = [("from", "<u4"), ("to", "<u4"), ("len", "<u4"), ("pad", "<u4"), ("offset", "<u8")]
+
 SIGNATURES = [
     ("gsim_default_gossipsub_params", None, [POINTER(CGossipSubParams)]),
     ("gsim_validate_topic_params", c_int32, [POINTER(CTopicScoreParams), c_char_p, c_size_t]),
@@ -212,6 +263,13 @@ SIGNATURES = [
     ("gsim_group_synchronize", c_int32, [c_void_p]),
     ("gsim_group_profile", c_int32, [c_void_p, c_int32]),
     ("gsim_group_profile_read", c_int32, [c_void_p, c_void_p, c_void_p, c_int32]),
+    # gsim_wire.h
+    ("gsim_wire_size", c_uint64, [POINTER(CWireRpc)]),
+    ("gsim_wire_encode", c_int32, [POINTER(CWireRpc), c_void_p, c_uint64, POINTER(c_uint64)]),
+    ("gsim_wire_fragment", c_int32, [POINTER(CWireRpc), c_int64, c_void_p, c_uint64, POINTER(c_uint64), c_void_p,
+                                     c_int32, POINTER(c_int32)]),
+    ("gsim_wire_heartbeat", c_int32, [c_void_p, c_int64, c_uint32, c_uint32, POINTER(CWireNames), c_void_p, c_uint64,
+                                      c_void_p, c_int64, POINTER(c_int64), POINTER(c_uint64)]),
 ]
 
 _lib = None

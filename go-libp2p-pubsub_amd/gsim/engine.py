@@ -128,6 +128,7 @@ class Engine:
                 raise ValueError(buf.value.decode())
             raise GsimError(rc, buf.value.decode())
         self.h = h
+        self.device = device
         self.net: Optional[Network] = None
 
     # -- lifecycle -----------------------------------------------------------

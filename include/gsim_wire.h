@@ -1,0 +1,163 @@
+/* gsim_wire.h — the GossipSub wire format.
+ *
+ * Two halves:
+ *
+ *   1. Host encoders of the reference's protobuf messages (pb/rpc.proto:5-57,
+ *      proto2, gogo-protobuf field order) and its fragmentRPC
+ *      (gossipsub.go:1204-1318).  An RPC is described by flat tables; every
+ *      optional field is present when its pointer is non-NULL (an empty byte
+ *      string with a non-NULL pointer is encoded, as Go encodes a non-nil
+ *      empty slice).
+ *
+ *   2. gsim_wire_heartbeat: the RPCs the engine's routers send at a
+ *      heartbeat — GRAFT/PRUNE (sendGraftPrune, gossipsub.go:1672-1709) with
+ *      the IHAVE gossip piggybacked on them (emitGossip + piggybackGossip,
+ *      gossipsub.go:1711-1816), or the IHAVE gossip alone (flush,
+ *      gossipsub.go:1777-1791) — encoded on the device for a range of
+ *      senders, one RPC per (sender, receiver) edge that carries any.
+ *
+ * Orders the reference leaves to Go map iteration are fixed here: topics
+ * ascend by index in every control list; a topic's IHAVE ids follow
+ * mcache.GetGossipIDs (mcache.go:82-92: newest history window first, each
+ * window in Put order — within a round the origin's own publication first,
+ * then receipts by (first sender, message id)).
+ */
+#ifndef GSIM_WIRE_H
+#define GSIM_WIRE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "gsim.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* A byte string; absent (optional field not set) when p is NULL. */
+typedef struct gsim_bytes {
+    const uint8_t* p;
+    uint32_t n;
+} gsim_bytes;
+
+/* RPC.SubOpts (rpc.proto:8-11): subscribe < 0 = absent. */
+typedef struct gsim_wire_sub {
+    int32_t subscribe;
+    gsim_bytes topic;
+} gsim_wire_sub;
+
+/* Message (rpc.proto:16-23). */
+typedef struct gsim_wire_msg {
+    gsim_bytes from, data, seqno, topic, signature, key;
+} gsim_wire_msg;
+
+/* ControlIHave (rpc.proto:32-36): message ids ids[id0 .. id0 + nid). */
+typedef struct gsim_wire_ihave {
+    gsim_bytes topic;
+    uint32_t id0, nid;
+} gsim_wire_ihave;
+
+/* ControlIWant (rpc.proto:38-41). */
+typedef struct gsim_wire_iwant {
+    uint32_t id0, nid;
+} gsim_wire_iwant;
+
+/* ControlGraft (rpc.proto:43-45). */
+typedef struct gsim_wire_graft {
+    gsim_bytes topic;
+} gsim_wire_graft;
+
+/* PeerInfo (rpc.proto:53-56). */
+typedef struct gsim_wire_px {
+    gsim_bytes peer, record;
+} gsim_wire_px;
+
+/* ControlPrune (rpc.proto:47-51): peers px[px0 .. px0 + npx); has_backoff 0 =
+ * Backoff absent. */
+typedef struct gsim_wire_prune {
+    gsim_bytes topic;
+    uint32_t px0, npx;
+    int32_t has_backoff;
+    uint64_t backoff;
+} gsim_wire_prune;
+
+/* RPC (rpc.proto:5-14).  has_control: the ControlMessage is present (Go:
+ * Control != nil), even when all its lists are empty. */
+typedef struct gsim_wire_rpc {
+    const gsim_wire_sub* subs;
+    uint32_t nsubs;
+    const gsim_wire_msg* msgs;
+    uint32_t nmsgs;
+    int32_t has_control;
+    const gsim_wire_ihave* ihave;
+    uint32_t nihave;
+    const gsim_wire_iwant* iwant;
+    uint32_t niwant;
+    const gsim_wire_graft* graft;
+    uint32_t ngraft;
+    const gsim_wire_prune* prune;
+    uint32_t nprune;
+    const gsim_bytes* ids;       /* message-id table of ihave / iwant */
+    uint32_t nids;
+    const gsim_wire_px* px;      /* PeerInfo table of prune */
+    uint32_t npx;
+} gsim_wire_rpc;
+
+/* RPC.Size() (rpc.pb.go): encoded length in bytes. */
+uint64_t gsim_wire_size(const gsim_wire_rpc* rpc);
+
+/* RPC.Marshal(): writes gsim_wire_size(rpc) bytes to out.  GSIM_ERANGE when
+ * cap is too small (*len = the size needed). */
+int gsim_wire_encode(const gsim_wire_rpc* rpc, uint8_t* out, uint64_t cap, uint64_t* len);
+
+/* fragmentRPC(rpc, limit) (gossipsub.go:1204-1296, with fragmentMessageIds
+ * 1298-1318), its quirks kept: a fragmented IHAVE loses its topic id; a
+ * message id longer than the limit is dropped; an RPC that fits (Size() <
+ * limit) is returned whole.  The fragments are encoded back to back in out;
+ * off[k] .. off[k+1] is fragment k (off has room for max_frags + 1 entries).
+ * GSIM_EINVAL when a published message alone exceeds the limit (the
+ * reference's error), GSIM_ERANGE when out or off is too small (*nfrags and
+ * *len then hold what is needed). */
+int gsim_wire_fragment(const gsim_wire_rpc* rpc, int64_t limit, uint8_t* out, uint64_t cap, uint64_t* len,
+                       uint64_t* off, int32_t max_frags, int32_t* nfrags);
+
+/* ---- device: the heartbeat's RPCs ---------------------------------------- */
+
+/* One encoded RPC in the device output. */
+typedef struct gsim_wire_ref {
+    uint32_t from, to;      /* sender, receiver (network peer ids) */
+    uint32_t len;           /* bytes */
+    uint32_t pad;
+    uint64_t offset;        /* into the output buffer */
+} gsim_wire_ref;
+
+/* Names and ids the RPCs carry.
+ *   topic_names[t]: ControlIHave/Graft/Prune.topicID of topic t (T entries);
+ *   peer_ids / peer_id_len: optional fixed-length peer ids (N x peer_id_len
+ *     bytes); a message's id is then peer_id(origin) || seqno (the reference's
+ *     DefaultMsgIdFn, pubsub.go: from + seqno), else seqno alone;
+ *     the seqno is the gsim_msg id as 8 big-endian bytes;
+ *   prune_backoff_s: ControlPrune.Backoff (PruneBackoff / 1s, gossipsub.go:1872).
+ * PX peer lists are not emitted (the default router has doPX off). */
+typedef struct gsim_wire_names {
+    const gsim_bytes* topic_names;
+    const uint8_t* peer_ids;
+    uint32_t peer_id_len;
+    uint64_t prune_backoff_s;
+} gsim_wire_names;
+
+/* Encode, on the device, the RPCs that senders [p0, p1) sent at heartbeat
+ * `tick` (call it after gsim_heartbeat(tick) and before the tick's first
+ * round).  d_out / d_refs are device buffers of out_cap bytes / ref_cap
+ * entries; refs come in sender order, each sender's in its row order.
+ * *n_rpcs / *bytes: what was written (GSIM_ERANGE with the totals needed
+ * when a buffer is too small; nothing is written then). */
+int gsim_wire_heartbeat(gsim_handle* h, int64_t tick, uint32_t p0, uint32_t p1, const gsim_wire_names* names,
+                        uint8_t* d_out, uint64_t out_cap, gsim_wire_ref* d_refs, int64_t ref_cap,
+                        int64_t* n_rpcs, uint64_t* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSIM_WIRE_H */

@@ -180,6 +180,7 @@ enum {
 typedef struct orc_event { int32_t kind, topic; uint32_t a, b; int64_t g; uint64_t mid; int64_t x; } orc_event;
 void    orc_msgs_log(orc_msgs* m, int32_t on);
 int64_t orc_msgs_events(orc_msgs* m, orc_event* out, int64_t cap);   /* copies and clears; returns the count */
+int64_t orc_msgs_ihave_marks(orc_msgs* m, uint8_t* out, int64_t n);   /* last heartbeat's [T][E] IHAVE marks */
 
 /* ---- mcache.go (one router's MessageCache) ------------------------------ */
 typedef struct orc_mcache orc_mcache;

@@ -268,6 +268,19 @@ static int32_t* tx_slot(priv* p, uint64_t mid, uint32_t e)
 
 /* ---- control round 0: handleIHave --------------------------------------- */
 
+/* Test access: the last heartbeat's IHAVE marks, [T][E] at the receivers'
+ * edges (n = T * E bytes; zeros when gossip is off). */
+int64_t orc_msgs_ihave_marks(orc_msgs* m, uint8_t* out, int64_t n)
+{
+    priv* p = orc_msgs_priv(m);
+    if (!p->ihave) {
+        memset(out, 0, (size_t)n);
+        return 0;
+    }
+    memcpy(out, p->ihave, (size_t)n);
+    return n;
+}
+
 void orc_gossip_ihave(orc_net* s, orc_msgs* m, int64_t g)
 {
     priv* p = orc_msgs_priv(m);

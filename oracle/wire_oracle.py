@@ -1,0 +1,137 @@
+"""CPU restatement of the GossipSub wire format — TEST INFRASTRUCTURE ONLY.
+
+Only tests/ may import this; the product path (libgsim's gsim_wire_*) never
+does.  Two independent pieces check the library's encoders:
+
+* `pb()`: protobuf message classes built at run time from a descriptor that
+  restates the schema of pb/rpc.proto:5-57 (proto2; field names, numbers and
+  labels as there).  The serializer is the protobuf runtime's own — an
+  encoder written by others, not ours.  The id fields declared `string` in
+  rpc.proto are declared `bytes` here: same wire type (length-delimited), no
+  UTF-8 check (the reference's own comment: Go emits invalid UTF-8 there).
+* `fragment_rpc` / `fragment_message_ids`: fragmentRPC restated from
+  gossipsub.go:1204-1296 and fragmentMessageIds from 1298-1318, on those
+  classes (Size() = ByteSize()).
+
+Parity: the restatement is pinned by the reference's own test,
+TestFragmentRPCFunction (gossipsub_test.go:2338-2500), restated in
+tests/test_wire.py against both this module and the library.
+"""
+from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+
+_CLASSES = None
+
+
+def pb():
+    """{name: class} for RPC, RPC.SubOpts, Message, ControlMessage,
+    ControlIHave, ControlIWant, ControlGraft, ControlPrune, PeerInfo."""
+    global _CLASSES
+    if _CLASSES is not None:
+        return _CLASSES
+    F = descriptor_pb2.FieldDescriptorProto
+    fdp = descriptor_pb2.FileDescriptorProto(name="gsim_test_rpc.proto", package="gsimtest.pb", syntax="proto2")
+
+    def msg(name, fields, parent=None):
+        m = (parent.nested_type if parent is not None else fdp.message_type).add(name=name)
+        for (fname, num, label, typ, tname) in fields:
+            f = m.field.add(name=fname, number=num, label=label, type=typ)
+            if tname:
+                f.type_name = tname
+        return m
+
+    OPT, REP = F.LABEL_OPTIONAL, F.LABEL_REPEATED
+    B, S, BOOL, U64, M = F.TYPE_BYTES, F.TYPE_STRING, F.TYPE_BOOL, F.TYPE_UINT64, F.TYPE_MESSAGE
+    rpc = msg("RPC", [("subscriptions", 1, REP, M, ".gsimtest.pb.RPC.SubOpts"),
+                      ("publish", 2, REP, M, ".gsimtest.pb.Message"),
+                      ("control", 3, OPT, M, ".gsimtest.pb.ControlMessage")])
+    msg("SubOpts", [("subscribe", 1, OPT, BOOL, None), ("topicid", 2, OPT, B, None)], parent=rpc)
+    msg("Message", [("from", 1, OPT, B, None), ("data", 2, OPT, B, None), ("seqno", 3, OPT, B, None),
+                    ("topic", 4, OPT, B, None), ("signature", 5, OPT, B, None), ("key", 6, OPT, B, None)])
+    msg("ControlMessage", [("ihave", 1, REP, M, ".gsimtest.pb.ControlIHave"),
+                           ("iwant", 2, REP, M, ".gsimtest.pb.ControlIWant"),
+                           ("graft", 3, REP, M, ".gsimtest.pb.ControlGraft"),
+                           ("prune", 4, REP, M, ".gsimtest.pb.ControlPrune")])
+    msg("ControlIHave", [("topicID", 1, OPT, B, None), ("messageIDs", 2, REP, B, None)])
+    msg("ControlIWant", [("messageIDs", 1, REP, B, None)])
+    msg("ControlGraft", [("topicID", 1, OPT, B, None)])
+    msg("ControlPrune", [("topicID", 1, OPT, B, None), ("peers", 2, REP, M, ".gsimtest.pb.PeerInfo"),
+                         ("backoff", 3, OPT, U64, None)])
+    msg("PeerInfo", [("peerID", 1, OPT, B, None), ("signedPeerRecord", 2, OPT, B, None)])
+    del S
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(fdp)
+    names = ["RPC", "RPC.SubOpts", "Message", "ControlMessage", "ControlIHave", "ControlIWant", "ControlGraft",
+             "ControlPrune", "PeerInfo"]
+    _CLASSES = {n: message_factory.GetMessageClass(pool.FindMessageTypeByName("gsimtest.pb." + n)) for n in names}
+    return _CLASSES
+
+
+class FragmentError(ValueError):
+    pass
+
+
+def fragment_message_ids(msg_ids, limit):
+    """fragmentMessageIds (gossipsub.go:1298-1318)."""
+    overhead = 2                                    # protobuf overhead per array element
+    out = [[]]
+    bucket_len = 0
+    for mid in msg_ids:
+        size = len(mid) + overhead
+        if size > limit:                            # pathological: removed from the outgoing gossip
+            continue
+        bucket_len += size
+        if bucket_len > limit:
+            out.append([])
+            bucket_len = size
+        out[-1].append(mid)
+    return out
+
+
+def fragment_rpc(rpc, limit):
+    """fragmentRPC (gossipsub.go:1204-1296) on pb() RPC objects."""
+    C = pb()
+    if rpc.ByteSize() < limit:
+        return [rpc]
+    rpcs = [C["RPC"]()]
+
+    def out_rpc(size_to_add, with_ctl):            # outRPC (1218-1236)
+        cur = rpcs[-1]
+        if cur.ByteSize() + size_to_add + 1 < limit:
+            if with_ctl and not cur.HasField("control"):
+                cur.control.SetInParent()
+            return cur
+        nxt = C["RPC"]()
+        if with_ctl:
+            nxt.control.SetInParent()
+        rpcs.append(nxt)
+        return nxt
+
+    for m in rpc.publish:                          # 1238-1246
+        s = m.ByteSize()
+        if s > limit:
+            raise FragmentError(f"message with len={s} exceeds limit {limit}")
+        out_rpc(s, False).publish.add().CopyFrom(m)
+    for sub in rpc.subscriptions:                  # 1248-1251
+        out_rpc(sub.ByteSize(), False).subscriptions.add().CopyFrom(sub)
+    if not rpc.HasField("control"):                # 1253-1257
+        return rpcs
+    ctl = rpc.control
+    ctl_out = C["RPC"]()                           # 1259-1264
+    ctl_out.control.CopyFrom(ctl)
+    if ctl_out.ByteSize() < limit:
+        rpcs.append(ctl_out)
+        return rpcs
+    for g in ctl.graft:                            # 1266-1274
+        out_rpc(g.ByteSize(), True).control.graft.add().CopyFrom(g)
+    for p in ctl.prune:
+        out_rpc(p.ByteSize(), True).control.prune.add().CopyFrom(p)
+    overhead = 6                                   # 1279-1295
+    for iw in ctl.iwant:
+        for ids in fragment_message_ids(list(iw.messageIDs), limit - overhead):
+            x = C["ControlIWant"](messageIDs=ids)
+            out_rpc(x.ByteSize(), True).control.iwant.add().CopyFrom(x)
+    for ih in ctl.ihave:
+        for ids in fragment_message_ids(list(ih.messageIDs), limit - overhead):
+            x = C["ControlIHave"](messageIDs=ids)  # the topic id is not carried over
+            out_rpc(x.ByteSize(), True).control.ihave.add().CopyFrom(x)
+    return rpcs

@@ -96,6 +96,7 @@ def load():
             "orc_gtracer_peer_promises": (c_int32, [c_void_p]),
             "orc_msgs_log": (None, [POINTER(OrcMsgs), c_int32]),
             "orc_msgs_events": (c_int64, [POINTER(OrcMsgs), c_void_p, c_int64]),
+            "orc_msgs_ihave_marks": (c_int64, [POINTER(OrcMsgs), c_void_p, c_int64]),
             "orc_tcache_new": (c_void_p, [c_int32, c_int64]),
             "orc_tcache_free": (None, [c_void_p]),
             "orc_tcache_add": (c_int32, [c_void_p, c_uint64, c_int64]),
@@ -263,6 +264,12 @@ class Msgs:
     def log(self, on=True):
         """Record the events the routers' caches and tracers observe (orc_msgs_log)."""
         load().orc_msgs_log(ctypes.byref(self.m), 1 if on else 0)
+
+    def ihave_marks(self, E):
+        """The last heartbeat's IHAVE marks [T][E] (receivers' edges)."""
+        out = np.zeros((self.lastput.shape[0], E), dtype=np.uint8)
+        load().orc_msgs_ihave_marks(ctypes.byref(self.m), out.ctypes.data_as(c_void_p), out.size)
+        return out
 
     def events(self):
         """The events recorded since the last call (and clear them)."""

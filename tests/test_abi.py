@@ -14,10 +14,11 @@ from gsim.engine import Engine, random_regular
 from gsim.params import PeerScoreParams, PeerScoreThresholds, Second, TopicScoreParams
 
 HEADER = os.path.join(REPO, "include", "gsim.h")
+HEADERS = [HEADER, os.path.join(REPO, "include", "gsim_wire.h")]
 
 
 def declared_functions():
-    src = open(HEADER).read()
+    src = "".join(open(h).read() for h in HEADERS)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(gsim_[a-z0-9_]+)\s*\(", src)))
 
@@ -46,8 +47,12 @@ def test_struct_layout_matches_c(tmp_path):
     import subprocess
     structs = {"gsim_topic_score_params": _abi.CTopicScoreParams, "gsim_peer_score_params": _abi.CPeerScoreParams,
                "gsim_thresholds": _abi.CThresholds, "gsim_gossipsub_params": _abi.CGossipSubParams,
-               "gsim_msg_config": _abi.CMsgConfig, "gsim_msg": _abi.CMsg}
-    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "gsim.h"', "int main(void){"]
+               "gsim_msg_config": _abi.CMsgConfig, "gsim_msg": _abi.CMsg, "gsim_bytes": _abi.CBytes,
+               "gsim_wire_sub": _abi.CWireSub, "gsim_wire_ihave": _abi.CWireIHave, "gsim_wire_iwant": _abi.CWireIWant,
+               "gsim_wire_graft": _abi.CWireGraft, "gsim_wire_px": _abi.CWirePx, "gsim_wire_prune": _abi.CWirePrune,
+               "gsim_wire_rpc": _abi.CWireRpc, "gsim_wire_names": _abi.CWireNames}
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "gsim.h"', '#include "gsim_wire.h"',
+             "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
         for fname, _ in py._fields_:

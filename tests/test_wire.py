@@ -1,0 +1,316 @@
+"""The wire format (include/gsim_wire.h).
+
+CPU part:
+  * gsim_wire_encode is byte-identical to the protobuf runtime's serializer
+    on the schema of pb/rpc.proto:5-57 (oracle/wire_oracle.py), over random
+    RPCs with every field present, absent and empty;
+  * gsim_wire_fragment follows fragmentRPC (gossipsub.go:1204-1318): the
+    reference's own TestFragmentRPCFunction (gossipsub_test.go:2338-2500) is
+    restated against both the library and the Python restatement, and the two
+    agree fragment for fragment on random RPCs and limits.
+GPU part: gsim_wire_heartbeat, the RPCs the routers send at a heartbeat
+encoded on the device, equals the RPCs built on the CPU from the oracle's
+heartbeat (GRAFT/PRUNE inbox, emitGossip targets) and from mcache windows
+driven by the oracle's Put stream (the pinned orc_mcache, mcache.go).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+from gsim import wire
+
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import wire_oracle as wo  # noqa: E402  (test infrastructure)
+
+
+def to_pb(r: wire.RPC):
+    C = wo.pb()
+    out = C["RPC"]()
+    for s in r.subscriptions:
+        x = out.subscriptions.add()
+        if s.subscribe is not None:
+            x.subscribe = bool(s.subscribe)
+        if s.topicid is not None:
+            x.topicid = wire._b(s.topicid)
+    for m in r.publish:
+        x = out.publish.add()
+        for name, v in (("from", m.from_), ("data", m.data), ("seqno", m.seqno), ("topic", m.topic),
+                        ("signature", m.signature), ("key", m.key)):
+            if v is not None:
+                setattr(x, name, wire._b(v))
+    if r.control is not None:
+        c = out.control
+        c.SetInParent()
+        for g in r.control.ihave:
+            x = c.ihave.add()
+            if g.topicID is not None:
+                x.topicID = wire._b(g.topicID)
+            x.messageIDs.extend([wire._b(i) for i in g.messageIDs])
+        for g in r.control.iwant:
+            c.iwant.add().messageIDs.extend([wire._b(i) for i in g.messageIDs])
+        for g in r.control.graft:
+            x = c.graft.add()
+            if g.topicID is not None:
+                x.topicID = wire._b(g.topicID)
+        for p in r.control.prune:
+            x = c.prune.add()
+            if p.topicID is not None:
+                x.topicID = wire._b(p.topicID)
+            for pi in p.peers:
+                y = x.peers.add()
+                if pi.peerID is not None:
+                    y.peerID = pi.peerID
+                if pi.signedPeerRecord is not None:
+                    y.signedPeerRecord = pi.signedPeerRecord
+            if p.backoff is not None:
+                x.backoff = p.backoff
+    return out
+
+
+def rand_bytes(rng, lo=0, hi=40, absent=0.2):
+    if rng.random() < absent:
+        return None
+    return rng.bytes(int(rng.integers(lo, hi + 1)))
+
+
+def rand_rpc(rng, scale=1.0):
+    n = lambda k: int(rng.integers(0, max(1, int(k * scale)) + 1))  # noqa: E731
+    r = wire.RPC()
+    for _ in range(n(3)):
+        r.subscriptions.append(wire.SubOpts(None if rng.random() < 0.2 else bool(rng.integers(2)),
+                                            rand_bytes(rng, 0, 12)))
+    for _ in range(n(4)):
+        r.publish.append(wire.Message(*(rand_bytes(rng, 0, int(300 * scale)) for _ in range(6))))
+    if rng.random() < 0.8:
+        c = wire.ControlMessage()
+        for _ in range(n(3)):
+            c.ihave.append(wire.ControlIHave(rand_bytes(rng, 0, 10), [rng.bytes(int(rng.integers(0, 50)))
+                                                                       for _ in range(n(20))]))
+        for _ in range(n(3)):
+            c.iwant.append(wire.ControlIWant([rng.bytes(int(rng.integers(0, 50))) for _ in range(n(20))]))
+        for _ in range(n(3)):
+            c.graft.append(wire.ControlGraft(rand_bytes(rng, 0, 10)))
+        for _ in range(n(3)):
+            c.prune.append(wire.ControlPrune(rand_bytes(rng, 0, 10),
+                                             [wire.PeerInfo(rand_bytes(rng), rand_bytes(rng)) for _ in range(n(2))],
+                                             None if rng.random() < 0.3 else int(rng.integers(0, 2**40))))
+        r.control = c
+    return r
+
+
+def test_encode_matches_protobuf_runtime():
+    rng = np.random.default_rng(1)
+    for k in range(400):
+        r = rand_rpc(rng, scale=1.0 + (k % 7))
+        want = to_pb(r).SerializeToString()
+        assert wire.marshal(r) == want, k
+        assert wire.size(r) == len(want)
+
+
+def test_encode_edge_cases():
+    """Empty RPC, an empty (present) control message, empty present bytes,
+    varint lengths of several bytes."""
+    cases = [wire.RPC(), wire.RPC(control=wire.ControlMessage()),
+             wire.RPC(publish=[wire.Message(data=b"")]),
+             wire.RPC(publish=[wire.Message(data=b"x" * 70000)]),
+             wire.RPC(control=wire.ControlMessage(prune=[wire.ControlPrune(b"t", [], 2**63)]))]
+    for r in cases:
+        assert wire.marshal(r) == to_pb(r).SerializeToString()
+    assert wire.marshal(wire.RPC(control=wire.ControlMessage())) == b"\x1a\x00"
+
+
+def frags_pb(rpcs):
+    return [x.SerializeToString() for x in rpcs]
+
+
+def test_fragment_matches_restatement_random():
+    rng = np.random.default_rng(2)
+    for k in range(300):
+        r = rand_rpc(rng, scale=1.0 + (k % 9))
+        limit = int(rng.integers(64, 3000))
+        if k % 5:                                   # mostly limits every message fits under
+            limit += max([to_pb(wire.RPC(publish=[m])).publish[0].ByteSize() for m in r.publish] + [0])
+        try:
+            want = frags_pb(wo.fragment_rpc(to_pb(r), limit))
+        except wo.FragmentError:
+            with pytest.raises(wire.WireError):
+                wire.fragment_rpc(r, limit)
+            continue
+        assert wire.fragment_rpc(r, limit) == want, (k, limit)
+
+
+def _mk_msg(rng, size):
+    """mkMsg (gossipsub_test.go:2344-2349): data of size-4 random bytes."""
+    return wire.Message(data=rng.bytes(size - 4))
+
+
+@pytest.mark.parametrize("impl", ["library", "restatement"])
+def test_fragment_rpc_function(impl):
+    """TestFragmentRPCFunction (gossipsub_test.go:2338-2500), restated."""
+    C = wo.pb()
+    rng = np.random.default_rng(3)
+    limit = 1024
+    topic = b"test"
+
+    def frag(r):
+        if impl == "library":
+            return [C["RPC"].FromString(b) for b in wire.fragment_rpc(r, limit)]
+        return wo.fragment_rpc(to_pb(r), limit)
+
+    def below(results):
+        for x in results:
+            assert x.ByteSize() <= limit
+
+    r = wire.RPC(publish=[_mk_msg(rng, 10), _mk_msg(rng, 10)])
+    assert len(frag(r)) == 1, "single RPC if input is < limit"
+
+    r = wire.RPC(publish=[_mk_msg(rng, 10), _mk_msg(rng, limit * 2)])
+    with pytest.raises((wire.WireError, wo.FragmentError)):
+        frag(r)
+
+    n_messages, msg_size = 100, 200
+    r = wire.RPC(subscriptions=[wire.SubOpts(True, topic)], publish=[_mk_msg(rng, msg_size) for _ in range(n_messages)])
+    results = frag(r)
+    below(results)
+    msgs_per_rpc = limit // msg_size
+    assert len(results) == n_messages // msgs_per_rpc
+    assert sum(len(x.publish) for x in results) == n_messages
+    assert sum(len(x.subscriptions) for x in results) == 1
+
+    r.control = wire.ControlMessage(graft=[wire.ControlGraft(topic)], prune=[wire.ControlPrune(topic)],
+                                    ihave=[wire.ControlIHave(None, [b"foo"])], iwant=[wire.ControlIWant([b"bar"])])
+    results = frag(r)
+    below(results)
+    assert len(results) == n_messages // msgs_per_rpc + 1
+    assert results[-1].HasField("control")
+    assert results[-1].control.SerializeToString() == to_pb(r).control.SerializeToString(), \
+        "control unaltered when it fits in one RPC"
+
+    n_topics, id_size, per_topic = 5, 32, 100
+    ids = [[rng.bytes(id_size) for _ in range(per_topic)] for _ in range(n_topics)]
+    r.control.ihave = [wire.ControlIHave(None, x) for x in ids]
+    r.control.iwant = [wire.ControlIWant(x) for x in ids]
+    results = frag(r)
+    below(results)
+    min_ctl = to_pb(r).control.ByteSize() // limit
+    assert len(results) >= n_messages // msgs_per_rpc + min_ctl
+
+    giant = rng.bytes(limit * 2)
+    r = wire.RPC(control=wire.ControlMessage(iwant=[wire.ControlIWant([b"hello", giant])]))
+    results = frag(r)
+    assert len(results) == 1
+    assert len(results[0].control.iwant) == 1
+    assert results[0].control.iwant[0].messageIDs[0] == b"hello"
+
+
+def test_fragmented_ihave_loses_its_topic():
+    """The reference's fragmentRPC builds the split IHAVEs without TopicID
+    (gossipsub.go:1288); kept."""
+    C = wo.pb()
+    r = wire.RPC(control=wire.ControlMessage(ihave=[wire.ControlIHave(b"topic", [bytes([k]) * 40 for k in range(80)])]))
+    frs = [C["RPC"].FromString(b) for b in wire.fragment_rpc(r, 1024)]
+    assert len(frs) > 1
+    assert all(not ih.HasField("topicID") for f in frs for ih in f.control.ihave)
+    assert [i for f in frs for ih in f.control.ihave for i in ih.messageIDs] == r.control.ihave[0].messageIDs
+
+
+# ---- GPU ----------------------------------------------------------------------------
+
+
+def expected_heartbeat_rpcs(net, st, msgs, mcaches, lib, T, names, backoff, p0, p1, peer_ids=None):
+    """CPU build of the heartbeat RPCs of senders [p0, p1): GRAFT/PRUNE from
+    the oracle's inbox (parity 0, the receiver's edge), IHAVE from its
+    emitGossip marks, ids from the pinned mcaches (GetGossipIDs order)."""
+    import ctypes
+    C = wo.pb()
+    E = net.e
+    marks = msgs.ihave_marks(E)
+    rev = st.rev
+    buf = (ctypes.c_uint64 * 65536)()
+    out = []
+    for p in range(p0, p1):
+        gids = {}
+        for e in range(int(net.row_ptr[p]), int(net.row_ptr[p + 1])):
+            q = int(net.col[e])
+            re = int(rev[e])
+            r = C["RPC"]()
+            c = r.control
+            any_ = False
+            for t in range(T):
+                if marks[t, re]:
+                    if t not in gids:
+                        k = lib.orc_mcache_gossip_ids(mcaches[p], t, buf, 65536)
+                        gids[t] = [int(buf[i]) for i in range(k)]
+                    ids = []
+                    for mid in gids[t]:
+                        pre = b"" if peer_ids is None else bytes(peer_ids[int(msgs.origin[mid % msgs.seen.shape[0]])])
+                        ids.append(pre + int(mid).to_bytes(8, "big"))
+                    c.ihave.add(topicID=names[t], messageIDs=ids)
+                    any_ = True
+            for t in range(T):
+                if st.ctl[0, t, re] & 0x01:
+                    c.graft.add(topicID=names[t])
+                    any_ = True
+            for t in range(T):
+                if st.ctl[0, t, re] & 0x02:
+                    c.prune.add(topicID=names[t], backoff=backoff)
+                    any_ = True
+            if any_:
+                out.append((p, q, r.SerializeToString()))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_peer_ids", [False, True])
+def test_heartbeat_rpcs_match_oracle(require_gpu, with_peer_ids):
+    import oracle_binding as ob
+    from fixtures import beacon_params, synthetic_state
+    from gsim.engine import random_regular
+    from gsim.params import GossipSubParams, PeerScoreThresholds, Second
+    from test_heartbeat import tick_time
+    from tickrun import run_parity, subscribed_schedule
+    n, k, T = 600, 12, 3
+    rng = np.random.default_rng(91)
+    params = beacon_params(T)
+    gp = GossipSubParams(D=6, Dlo=5, Dhi=10, Dscore=3, Dout=2)
+    th = PeerScoreThresholds(GossipThreshold=-50, PublishThreshold=-100, GraylistThreshold=-300)
+    net = random_regular(n, k, seed=n + 1, n_topics=T)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 6 / k)
+    ticks = list(range(1, 7))
+    sched = subscribed_schedule(rng, ticks, net, T, 5.0, 0.0, verdicts=(0.85, 0.05, 0.05, 0.05, 0.0))
+    names = [f"topic{t:02d}".encode() for t in range(T)]
+    peer_ids = rng.integers(0, 256, size=(n, 38), dtype=np.uint8) if with_peer_ids else None
+    lib = ob.load()
+    backoff = int(gp.PruneBackoff // Second)
+    state = {"mc": None, "checked": 0}
+
+    def after_heartbeat(kk, eng, st_, msgs):
+        if state["mc"] is None:
+            msgs.log()                      # the Put stream starts now: windows are empty before tick 1
+            state["mc"] = [lib.orc_mcache_new(gp.HistoryGossip, gp.HistoryLength) for _ in range(n)]
+        mc = state["mc"]
+        ev = msgs.events()
+        for e in ev:
+            if int(e["kind"]) == ob.EV_PUT:
+                lib.orc_mcache_put(mc[int(e["a"])], int(e["mid"]), int(e["topic"]))
+        if kk >= 2:
+            p0, p1 = 37, 337
+            got = wire.heartbeat_rpcs(eng, kk, p0, p1, names, peer_ids=peer_ids, prune_backoff_s=backoff)
+            want = expected_heartbeat_rpcs(net, st_, msgs, mc, lib, T, names, backoff, p0, p1, peer_ids)
+            assert len(got) == len(want), f"tick {kk}: {len(got)} RPCs, expected {len(want)}"
+            for g_, w_ in zip(got, want):
+                assert g_ == w_, f"tick {kk}: RPC {g_[0]}->{g_[1]} differs"
+            state["checked"] += len(got)
+        for p in range(n):                  # the heartbeat ends with mcache.Shift
+            lib.orc_mcache_shift(mc[p])
+
+    try:
+        run_parity(net, params, th, gp, st, ticks, sched, ring=512, after_heartbeat=after_heartbeat)
+    finally:
+        for m in state["mc"] or []:
+            lib.orc_mcache_free(m)
+    assert state["checked"] > 200

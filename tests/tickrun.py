@@ -28,11 +28,12 @@ def restrict_to_subscriptions(st, net):
 
 
 def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, churn=None, after_tick=None,
-               eng=None):
+               eng=None, after_heartbeat=None):
     """Run `ticks` on a fresh engine loaded with `st`'s state and on the
     oracle; assert identical state, seen-set and totals after every tick.
     churn: {tick: [(pairs, up), ...]} applied just before the tick.
-    eng: an engine whose state `st` already mirrors (nothing is pushed)."""
+    eng: an engine whose state `st` already mirrors (nothing is pushed).
+    after_heartbeat(kk, eng, st, msgs): called once both heartbeats ran."""
     from gsim.engine import Engine
     pushed = eng is None
     if eng is None:
@@ -60,6 +61,8 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
             lib.orc_ip_colocation(v)
             lib.orc_compute_scores(v)
             msgs.heartbeat(st, kk, now, SEED)
+            if after_heartbeat:
+                after_heartbeat(kk, eng, st, msgs)
             for g in range(kk * R, kk * R + R):
                 for (mid, t, o, inv) in sched.get(g, []):
                     msgs.publish(st, mid, t, o, inv, g)
