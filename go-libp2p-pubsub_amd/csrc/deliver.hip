@@ -95,8 +95,9 @@ struct Deliver {
     uint8_t* d_gstate = nullptr;       // [E] edge order: owner's snapshot score of col >= gossipThreshold
     uint64_t* d_resp = nullptr;        // IWANT responses (record edge | slot << 32), delivered in round 2
     uint32_t* d_nresp = nullptr;       // [0] responses queued; [1] overflow; [2] ring-reuse error;
-                                       // [3] MaxIHaveLength: bit 0 IHAVE / bit 1 IWANT truncation needed, bit 2 counting
-    uint32_t* d_pair_cnt = nullptr;    // [E] IWANT ids per edge this IHAVE stage (ring > MaxIHaveLength only)
+                                       // [3] bit 2: the gossip window exceeds MaxIHaveLength (k_ihave_pairs)
+    uint8_t* d_peertx = nullptr;       // [ring][ptx_w] GetForPeer counts of bad-signature slots (IhArgs::peertx)
+    int32_t ptx_w = 0;                 // longest local row
     int64_t resp_cap = 0;
     uint32_t* d_prom = nullptr;        // [P][E] promise ring, edge order of the promiser: slot or none
     uint64_t* d_pcand = nullptr;       // [E] per-IWANT promise candidate (min Philox key | slot)
@@ -162,6 +163,8 @@ struct RoundArgs {
     // on no other edge, so only these are walked
     const uint64_t* mmask;
     const uint32_t* tmtab;         // k_send_tm blocks per topic (Deliver::d_tmtab)
+    uint8_t* peertx;               // [ring][ptx_w] GetForPeer counts (Deliver::d_peertx), zeroed on reuse
+    int32_t ptx_w;
 };
 
 __device__ __forceinline__ int64_t round_time(const RoundArgs& a, int64_t g)
@@ -280,6 +283,8 @@ __global__ void k_reset_slots(RoundArgs a, const gsim_msg* pub, int32_t count)
     // the previous message may still sit in a gossip window or a promise
     if (blockIdx.x == 0 && threadIdx.x == 0 && a.slot_last[m] >= 0 && a.g - a.slot_last[m] < a.reuse_guard)
         atomicOr(&a.err[2], 1u);
+    if (blockIdx.x == 0 && a.peertx)
+        for (int j = threadIdx.x; j < a.ptx_w; j += blockDim.x) a.peertx[(int64_t)m * a.ptx_w + j] = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.CN; i += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t c = row[i];
         // several reused rows may credit one record: atomic updates here
@@ -1017,13 +1022,15 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
 // handleIHave for every receiver, and — because nothing a handleIWant gate
 // reads can change between rounds 0 and 1 (score snapshot, mcache window,
 // behaviour) — the advertisers' handleIWant with it: the messages they send
-// are queued for round 2.  Invariants this relies on (checked by the oracle,
-// which implements the reference's counters in full): a receiver gets at most
-// one IHAVE RPC per advertiser per heartbeat (peerhave <= 1, iasked = 0); no
-// topic's gossip window and no IWANT list exceeds MaxIHaveLength ids (no
-// truncation: checked on the device when the ring is larger); and a
-// receiver asks an advertiser for a message at most once while it is in the
-// advertiser's mcache, because the answer always arrives (peertx <= 1).
+// are queued for round 2.  A receiver gets one IHAVE RPC per advertiser per
+// heartbeat, so handleIHave sees peerhave = 1 and iasked = 0
+// (gossipsub.go:638-648).  The MaxIHaveLength truncations (emitGossip's
+// per-peer subset, gossipsub.go:1763-1772; the IWANT cap, 679-690) can only
+// apply when the window holds more than MaxIHaveLength slots: then
+// k_ihave_pairs runs instead of k_ihave.  mcache.peertx (GetForPeer's count,
+// mcache.go:73-86) can exceed 1 only for a message its receiver never marks
+// seen — a bad signature, served by its origin alone — and is counted per
+// (slot, origin's row position) for those (Deliver::d_peertx).
 
 struct IhArgs {
     int64_t N, E;
@@ -1054,11 +1061,24 @@ struct IhArgs {
     uint32_t rlo, rhi;
     int32_t sharded;
     const uint32_t* gid;
-    // MaxIHaveLength (gossipsub.go:679-690, 1766-1771): the truncations are
-    // not modeled; a window that could need one is detected instead
-    int32_t max_ihave;
-    uint32_t* pair_cnt;        // [E] IWANT ids per (receiver, advertiser) edge (nullptr: ring <= MaxIHaveLength)
+    int32_t max_ihave;             // MaxIHaveLength
+    // GetForPeer counts of bad-signature slots: [ring][ptx_w] by the origin's row position
+    uint8_t* peertx;
+    int32_t ptx_w;
+    int32_t retrans;               // GossipRetransmission
 };
+
+// handleIWant's GetForPeer count (mcache.go:73-86) for a response to
+// (slot m, the advertiser's edge re): only a bad-signature message can be
+// asked for twice (its receivers never see it), and only its origin serves it.
+__device__ __forceinline__ bool peertx_allows(const IhArgs& a, uint32_t m, uint32_t re, uint32_t advertiser)
+{
+    if (a.minv[m] != GSIM_VERDICT_SIGNATURE || !a.peertx) return true;
+    uint8_t* c = a.peertx + (int64_t)m * a.ptx_w + (re - a.row_ptr[advertiser]);
+    const uint32_t n = (uint32_t)*c + 1u;
+    *c = (uint8_t)(n > 255u ? 255u : n);
+    return (int32_t)n <= a.retrans;
+}
 
 // first-seen round of a cell at control time of round g (any claim still
 // pending is from round g-1 or g), or -1
@@ -1103,22 +1123,9 @@ __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount
         if (lane == 0) s_n = n;
     }
     __syncthreads();
-    if (blockIdx.x == 0 && a.pair_cnt && s_n > a.max_ihave) {
-        // more slots in the gossip window than MaxIHaveLength: one topic's
-        // window over it would need the per-peer IHAVE truncation (err[3] bit
-        // 0); otherwise IWANT lists are counted per edge (bit 2: check them)
-        uint32_t* s_tc = reinterpret_cast<uint32_t*>(s_act + ((a.ring + 1) & ~1));   // s_cnt, not yet in use
-        for (int t = threadIdx.x; t < a.T; t += blockDim.x) s_tc[t] = 0;
-        __syncthreads();
-        for (int k = threadIdx.x; k < s_n; k += blockDim.x) atomicAdd(&s_tc[a.mtopic[s_act[k]]], 1u);
-        __syncthreads();
-        for (int t = threadIdx.x; t < a.T; t += blockDim.x)
-            if ((int32_t)s_tc[t] > a.max_ihave) atomicOr(&a.nresp[3], 1u);
-        if (threadIdx.x == 0) atomicOr(&a.nresp[3], 4u);
-        __syncthreads();
-        for (int w = threadIdx.x; w < 2 * a.ring; w += blockDim.x) s_cnt[w] = 0;
-        __syncthreads();
-    }
+    // more slots in the gossip window than MaxIHaveLength: a truncation may
+    // apply, k_ihave_pairs handles this stage (bit 2)
+    if (blockIdx.x == 0 && threadIdx.x == 0 && s_n > a.max_ihave) atomicOr(&a.nresp[3], 4u);
     const int lane = threadIdx.x & 63;
     const int64_t p0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;   // cell index (peer clo + p)
     const int nact = p0 < a.CN ? s_n : 0;
@@ -1157,6 +1164,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
 {
     extern __shared__ uint16_t s_act[];   // [ring] candidate slots (bit 15: push), then response staging
     __shared__ int s_n;
+    if (a.nresp[3] & 4u) return;          // a truncation may apply: k_ihave_pairs
     const int wid = threadIdx.x >> 6;
     uint64_t* stage = reinterpret_cast<uint64_t*>(s_act + ((a.ring + 3) & ~3)) + wid * kRespStage;
     if (threadIdx.x < 64) {
@@ -1254,7 +1262,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                                                           m, me_g);
                             atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[re]), (unsigned long long)key);
                             r = e;
-                            resp = a.respond && a.gstate[e] && !ign_s;
+                            resp = a.respond && a.gstate[e] && !ign_s && peertx_allows(a, m, e, me_id);
                         }
                     }
                 } else {
@@ -1270,13 +1278,12 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                                                               a.gid ? a.gid[i] : i);
                                 atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[e]), (unsigned long long)key);
                                 r = re;
-                                resp = a.respond && a.gstate[re] && !(a.behaviour[i] & GSIM_BEHAVE_IGNORE_IWANT);
+                                resp = a.respond && a.gstate[re] && !(a.behaviour[i] & GSIM_BEHAVE_IGNORE_IWANT) &&
+                                       peertx_allows(a, m, re, i);
                             }
                         }
                     }
                 }
-                if (req && a.pair_cnt && (a.nresp[3] & 4u))
-                    atomicAdd(&a.pair_cnt[push ? a.rev[e] : e], 1u);   // the receiver's edge to the advertiser
                 n_req += req;
                 n_resp += resp;
                 const uint64_t sb = __ballot(resp);
@@ -1300,17 +1307,184 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
     }
 }
 
-// A receiver asking one advertiser for more than MaxIHaveLength ids would
-// have its IWANT truncated (gossipsub.go:679-690): reported (err[3] bit 1).
-__global__ __launch_bounds__(256) void k_iwant_check(uint32_t* pair_cnt, int64_t E, int32_t max_ihave, uint32_t* err)
+// handleIHave when a MaxIHaveLength truncation may apply (the window holds
+// more than MaxIHaveLength slots: nresp[3] bit 2).  One wave per receiver,
+// walking its (receiver, advertiser) pairs in row order, as the oracle does
+// (oracle_gossip.c orc_gossip_ihave):
+//   * an advertiser whose window for topic t holds more than MaxIHaveLength
+//     ids sends this receiver a random MaxIHaveLength-subset of it
+//     (emitGossip's per-peer shuffle, gossipsub.go:1763-1772);
+//   * an IWANT of more than MaxIHaveLength ids asks for a random
+//     MaxIHaveLength of them (handleIHave, gossipsub.go:679-690), and the
+//     promise is one of those (AddPromise, gossip_tracer.go:48-64).
+// A random subset is the MaxIHaveLength smallest Philox keys; keys are unique
+// (their low word is the slot), so it is {key <= tau} for the
+// MaxIHaveLength-th smallest key tau, found by a binary search over the key
+// value (64 counting passes over the window: a path for rare, huge windows).
+constexpr int kPairTopics = 64;
+
+__global__ __launch_bounds__(256) void k_ihave_pairs(IhArgs a)
 {
-    if (!(err[3] & 4u)) return;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride) {
-        const uint32_t c = pair_cnt[e];
-        if (!c) continue;
-        if ((int32_t)c > max_ihave) atomicOr(&err[3], 2u);
-        pair_cnt[e] = 0;
+    extern __shared__ uint16_t s_act[];   // [ring] window slots, then per wave: staging, tau[64], count[64]
+    __shared__ int s_n;
+    if (!(a.nresp[3] & 4u)) return;       // k_ihave handles this stage
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint64_t* base = reinterpret_cast<uint64_t*>(s_act + ((a.ring + 3) & ~3));
+    uint64_t* stage = base + wid * kRespStage;
+    uint64_t* s_tau = base + 4 * kRespStage + wid * kPairTopics;
+    uint32_t* s_cnt = reinterpret_cast<uint32_t*>(base + 4 * kRespStage + 4 * kPairTopics) + wid * kPairTopics;
+    if (threadIdx.x < 64) {
+        int n = 0;
+        for (int m0 = 0; m0 < a.ring; m0 += 64) {
+            const int m = m0 + lane;
+            const bool act = m < a.ring && a.slot_last[m] >= a.lo_round;
+            const uint64_t b = __ballot(act);
+            if (act) s_act[n + __popcll(b & ((1ull << lane) - 1))] = (uint16_t)m;
+            n += __popcll(b);
+        }
+        if (lane == 0) s_n = n;
+    }
+    __syncthreads();
+    const int ns = s_n;
+    const uint32_t L = (uint32_t)a.max_ihave;
+    const int64_t tick_round = a.tick * a.R;
+    int nstage = 0;
+    unsigned long long n_walk = 0, n_req = 0, n_resp = 0;
+    auto flush_stage = [&]() {
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        uint32_t b0 = 0;
+        if (lane == 0 && nstage) b0 = atomicAdd(&a.nresp[0], (uint32_t)nstage);
+        b0 = __shfl(b0, 0, 64);
+        for (int q = lane; q < nstage; q += 64) {
+            if ((int64_t)b0 + q < a.resp_cap) a.resp[b0 + q] = stage[q];
+            else atomicOr(&a.nresp[1], 1u);
+        }
+        nstage = 0;
+    };
+    auto lds_sync = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // the L-th smallest key over the window slots k with sel(k, &key)
+    auto kth_key = [&](auto sel) -> uint64_t {
+        uint64_t lo = 0, hi = ~0ull;
+        while (lo < hi) {
+            const uint64_t mid = lo + ((hi - lo) >> 1);
+            uint32_t c = 0;
+            for (int k0 = 0; k0 < ns; k0 += 64) {
+                const int k = k0 + lane;
+                uint64_t key = 0;
+                c += (uint32_t)__popcll(__ballot(k < ns && sel(k, key) && key <= mid));
+            }
+            if (c >= L) hi = mid; else lo = mid + 1;
+        }
+        return lo;
+    };
+    for (int64_t pc = (int64_t)blockIdx.x * 4 + wid; pc < a.CN; pc += (int64_t)gridDim.x * 4) {
+        const uint32_t p = a.clo + (uint32_t)pc;
+        if (p < a.rlo || p >= a.rhi) continue;                    // receivers: owned peers
+        const uint64_t subp = a.sub[p];
+        const uint32_t beg = a.row_ptr[p], end = a.row_ptr[p + 1];
+        const uint32_t p_g = a.gid ? a.gid[p] : p;
+        for (uint32_t e = beg; e < end; ++e) {
+            if (!a.gstate[e]) continue;                           // IHAVE from a peer below gossipThreshold
+            const uint32_t re = a.rev[e], i = a.col[e];
+            // topics i gossiped to p that p joined (gs.mesh[topic] exists)
+            const bool tb = lane < a.T && ((subp >> lane) & 1ull) && a.gsel[(int64_t)lane * a.E + re];
+            const uint64_t tmask = __ballot(tb);
+            if (!tmask) continue;
+            n_walk += (lane == 0);
+            const uint32_t i_g = a.gid ? a.gid[i] : i;
+            const int64_t ic = (int64_t)i - a.clo;
+            const uint32_t origin_ign = a.behaviour[i] & GSIM_BEHAVE_IGNORE_IWANT;
+            auto holds = [&](uint32_t m) {
+                return holds_in_window(a.cell[(int64_t)m * a.CN + ic], a.g, a.lo_round, tick_round, a.minv[m] != 0,
+                                       i == a.morigin[m]);
+            };
+            // GetGossipIDs(topic) of i: ids per topic
+            s_cnt[lane] = 0;
+            lds_sync();
+            for (int k0 = 0; k0 < ns; k0 += 64) {
+                const int k = k0 + lane;
+                if (k < ns) {
+                    const uint32_t m = s_act[k];
+                    const int t = (int)a.mtopic[m];
+                    if (((tmask >> t) & 1ull) && holds(m)) atomicAdd(&s_cnt[t], 1u);
+                }
+            }
+            lds_sync();
+            const uint64_t omask = __ballot(s_cnt[lane] > L) & tmask;
+            for (uint64_t om = omask; om; om &= om - 1) {
+                const int t = __ffsll((long long)om) - 1;
+                const uint64_t tau = kth_key([&](int k, uint64_t& key) {
+                    const uint32_t m = s_act[k];
+                    if ((int)a.mtopic[m] != t || !holds(m)) return false;
+                    key = pair_key(a.seed, (uint32_t)a.tick, i_g, (uint32_t)t, P_IHAVE_TRUNC, m, p_g);
+                    return true;
+                });
+                if (lane == 0) s_tau[t] = tau;
+            }
+            lds_sync();
+            // the ids i advertised to p and p has not seen
+            auto wanted = [&](uint32_t m) {
+                const int t = (int)a.mtopic[m];
+                if (!((tmask >> t) & 1ull) || a.cell[(int64_t)m * a.CN + pc] != kUnseen64 || !holds(m)) return false;
+                return s_cnt[t] <= L ||
+                       pair_key(a.seed, (uint32_t)a.tick, i_g, (uint32_t)t, P_IHAVE_TRUNC, m, p_g) <= s_tau[t];
+            };
+            uint32_t nw = 0;
+            for (int k0 = 0; k0 < ns; k0 += 64) {
+                const int k = k0 + lane;
+                nw += (uint32_t)__popcll(__ballot(k < ns && wanted(s_act[k])));
+            }
+            if (nw == 0) continue;
+            uint64_t tau_w = ~0ull;
+            if (nw > L)
+                tau_w = kth_key([&](int k, uint64_t& key) {
+                    const uint32_t m = s_act[k];
+                    if (!wanted(m)) return false;
+                    key = pair_key(a.seed, (uint32_t)a.tick, p_g, 0, P_IWANT, m, i_g);
+                    return true;
+                });
+            uint64_t pmin = ~0ull;
+            for (int k0 = 0; k0 < ns; k0 += 64) {
+                const int k = k0 + lane;
+                const uint32_t m = k < ns ? s_act[k] : 0u;
+                const bool ask = k < ns && wanted(m) &&
+                                 (nw <= L || pair_key(a.seed, (uint32_t)a.tick, p_g, 0, P_IWANT, m, i_g) <= tau_w);
+                bool resp = false;
+                if (ask) {
+                    const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, p_g, 0, P_PROMISE, m, i_g);
+                    pmin = key < pmin ? key : pmin;
+                    // handleIWant at i: its gate on p, IWANT-ignoring behaviour, GetForPeer's count
+                    resp = a.respond && a.gstate[re] && !origin_ign && peertx_allows(a, m, re, i);
+                }
+                n_req += ask;
+                n_resp += resp;
+                const uint64_t sb = __ballot(resp);
+                if (sb) {
+                    if (nstage + __popcll(sb) > kRespStage) flush_stage();
+                    if (resp) stage[nstage + __popcll(sb & ((1ull << lane) - 1))] = (uint64_t)re | ((uint64_t)m << 32);
+                    nstage += __popcll(sb);
+                }
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                const uint64_t x = __shfl_xor(pmin, o, 64);
+                pmin = x < pmin ? x : pmin;
+            }
+            if (lane == 0) atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[e]), (unsigned long long)pmin);
+        }
+    }
+    flush_stage();
+    n_walk = wave_sum_u64(n_walk);
+    n_req = wave_sum_u64(n_req);
+    n_resp = wave_sum_u64(n_resp);
+    if (lane == 0 && (n_walk | n_req)) {
+        atomicAdd(&a.gstats[0], n_walk);
+        atomicAdd(&a.gstats[1], n_req);
+        atomicAdd(&a.gstats[2], n_resp);
     }
 }
 
@@ -1496,7 +1670,7 @@ static void dl_free(Deliver* d)
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
-    f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_pair_cnt); f(d->d_prom); f(d->d_pcand);
+    f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_peertx); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
     delete d;
 }
@@ -1548,6 +1722,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.fsum = d->d_fsum;
     a.mmask = d->d_mmask;
     a.tmtab = d->d_tmtab;
+    a.peertx = d->d_peertx; a.ptx_w = d->ptx_w;
     a.nsw = (a.nw + 63) / 64;
     const size_t w = (size_t)nnew_words(d);
     a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
@@ -1679,11 +1854,13 @@ static bool ihave_prepare(gsim_handle* h, int64_t g, IhaveStage* st, int* rc)
         a.gid = sh->d_gid;
     }
     a.max_ihave = h->gp.max_ihave_length;
-    a.pair_cnt = d->d_pair_cnt;
+    a.peertx = d->d_peertx; a.ptx_w = d->ptx_w;
+    a.retrans = h->gp.gossip_retransmission;
     st->lds = (((size_t)d->cfg.ring + 3) & ~(size_t)3) * sizeof(uint16_t) + 4 * kRespStage * sizeof(uint64_t);
     st->lds_c = (((size_t)d->cfg.ring + 1) & ~(size_t)1) * sizeof(uint16_t) + 2 * (size_t)d->cfg.ring * 4;
     st->grid = grid_peers(a.CN);
     hipError_t e = hipMemsetAsync(d->d_nresp, 0, 2 * sizeof(uint32_t), h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_nresp + 3, 0, sizeof(uint32_t), h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_gcount, 0, 2 * (size_t)d->cfg.ring * 4, h->stream);
     if (e != hipSuccess) { *rc = hip_check(h, e, "gossip reset"); return false; }
     return true;
@@ -1715,11 +1892,16 @@ static int ihave_walk(gsim_handle* h, IhaveStage* st)
         hipLaunchKernelGGL(k_ihave<32>, dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)d->d_gcount);
     else
         hipLaunchKernelGGL(k_ihave<64>, dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)d->d_gcount);
+    if (d->cfg.ring > h->gp.max_ihave_length) {
+        // the window may hold more than MaxIHaveLength slots: k_gossip_count
+        // decided on the device which of the two walks runs
+        const size_t lds = (((size_t)d->cfg.ring + 3) & ~(size_t)3) * sizeof(uint16_t) +
+                           4 * (kRespStage + kPairTopics) * sizeof(uint64_t) + 4 * kPairTopics * sizeof(uint32_t);
+        const int grid = (int)std::min<int64_t>((a.CN + 3) / 4, 4096);
+        hipLaunchKernelGGL(k_ihave_pairs, dim3(grid), dim3(256), lds, h->stream, a);
+    }
     hipLaunchKernelGGL(k_promise_insert, dim3(std::min<int64_t>((h->e + 255) / 256, 16384)), dim3(256), 0, h->stream,
                        d->d_pcand, d->d_prom, d->prom_ticks, a.prom_idx, h->e);
-    if (d->d_pair_cnt)
-        hipLaunchKernelGGL(k_iwant_check, dim3(std::min<int64_t>((h->e + 255) / 256, 16384)), dim3(256), 0, h->stream,
-                           d->d_pair_cnt, h->e, h->gp.max_ihave_length, d->d_nresp);
     d->resp_round = a.g + 2;
     return hip_check(h, hipGetLastError(), "k_ihave");
 }
@@ -1759,11 +1941,6 @@ int deliver_check_errors(gsim_handle* h)
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return hip_check(h, e, "delivery error flags");
     if (err[1]) { h->err = "IWANT responses overflowed their queue (raise gsim_msg_config.max_arrivals)"; return GSIM_ERANGE; }
-    if (err[3] & 3u) {
-        h->err = (err[3] & 1u) ? "a topic's gossip window exceeded MaxIHaveLength ids (IHAVE truncation is not modeled)"
-                               : "an IWANT list exceeded MaxIHaveLength ids (IWANT truncation is not modeled)";
-        return GSIM_ERANGE;
-    }
     if (err[2]) {
         h->err = "a ring slot was republished while its message could still be gossiped or promised (raise ring)";
         return GSIM_ESTATE;
@@ -2216,7 +2393,8 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_gstate, (size_t)h->e);
     A((void**)&d->d_resp, (size_t)d->resp_cap * 8);
     A((void**)&d->d_nresp, 4 * 4);
-    if (cfg->ring > h->gp.max_ihave_length) A((void**)&d->d_pair_cnt, (size_t)h->e * 4);
+    d->ptx_w = (int32_t)std::max<uint32_t>(h->max_degree, 1u);
+    A((void**)&d->d_peertx, ring * (size_t)d->ptx_w);
     A((void**)&d->d_prom, (size_t)d->prom_ticks * (size_t)h->e * 4);
     A((void**)&d->d_pcand, (size_t)h->e * 8);
     A((void**)&d->d_behaviour, N);
@@ -2249,7 +2427,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     if (e == hipSuccess) e = hipMemsetAsync(d->d_gsel, 0, T * (size_t)h->e, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_gstate, 0, (size_t)h->e, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_nresp, 0, 4 * 4, h->stream);
-    if (e == hipSuccess && d->d_pair_cnt) e = hipMemsetAsync(d->d_pair_cnt, 0, (size_t)h->e * 4, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_peertx, 0, ring * (size_t)d->ptx_w, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_prom, 0xFF, (size_t)d->prom_ticks * (size_t)h->e * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_pcand, 0xFF, (size_t)h->e * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_behaviour, 0, N, h->stream);
@@ -2340,11 +2518,6 @@ int gsim_msg_stats(gsim_handle* h, int64_t* out4)
     if (e != hipSuccess) return hip_check(h, e, "gsim_msg_stats");
     for (int k = 0; k < 4; ++k) out4[k] = (int64_t)s[k];
     if (err[1]) { h->err = "IWANT responses overflowed their queue (raise gsim_msg_config.max_arrivals)"; return GSIM_ERANGE; }
-    if (err[3] & 3u) {
-        h->err = (err[3] & 1u) ? "a topic's gossip window exceeded MaxIHaveLength ids (IHAVE truncation is not modeled)"
-                               : "an IWANT list exceeded MaxIHaveLength ids (IWANT truncation is not modeled)";
-        return GSIM_ERANGE;
-    }
     if (err[2]) {
         h->err = "a ring slot was republished while its message could still be gossiped or promised (raise ring)";
         return GSIM_ESTATE;

@@ -803,7 +803,7 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
             if (a.gossip) {
                 bool gsel = false;
                 const int32_t lpt = g.lastput(a, obs, t);
-                if (lpt >= (int64_t)a.tick - a.hist_gossip) {
+                if (lpt >= 0 && lpt >= (int64_t)a.tick - a.hist_gossip) {   // -1: no put yet
                     if (g.any(dirty)) {
                         if (dirty) S_live = score_of_record(a, rv, col);
                         dirty = false;
@@ -906,7 +906,8 @@ __device__ __forceinline__ void fanout_observer(const HbArgs& a, Grp& g, int64_t
             if (valid && nf != fl) a.mflags[i] = nf;
             if (!a.gossip) continue;
             bool gsel = false;
-            if (a.lastput[(int64_t)t * a.N + obs] >= (int64_t)a.tick - a.hist_gossip) {
+            const int32_t lpt = a.lastput[(int64_t)t * a.N + obs];
+            if (lpt >= 0 && lpt >= (int64_t)a.tick - a.hist_gossip) {
                 if (!have_live) {                               // live Score(p), gossipsub.go:1734
                     if (valid) S_live = score_of_record(a, rv, col);
                     have_live = true;

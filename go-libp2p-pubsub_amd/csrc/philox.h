@@ -49,6 +49,7 @@ enum Purpose : uint32_t {
     P_PROMISE = 8,     // rand.Intn in AddPromise              gossip_tracer.go:53
     P_GOSSIP_FILL = 9, // map order of emitGossip's Dlo fill   gossipsub.go:1739-1748
     P_GOSSIP_DUP = 10, // shuffle key of a fill duplicate      gossipsub.go:1758
+    P_IHAVE_TRUNC = 11,// emitGossip's per-peer shuffleStrings  gossipsub.go:1766-1771
     P_FANOUT_NEW = 12, // Publish: getPeers for a new fanout   gossipsub.go:1020-1023 (counter word 0 = round)
     P_FANOUT = 13,     // heartbeat fanout top-up             gossipsub.go:1578-1585
 };

@@ -249,27 +249,71 @@ def test_ring_larger_than_max_ihave_length_bit_exact(require_gpu):
 
 
 @pytest.mark.gpu
-def test_topic_window_over_max_ihave_length_is_reported(require_gpu):
-    """One topic's gossip window over MaxIHaveLength would need the per-peer
-    IHAVE truncation, which the device does not model: it is reported
-    (GSIM_ERANGE) instead of silently advertising too much."""
-    from gsim.engine import Engine, GsimError
-    net, params, th, gp, st, sched = _gossip_window_run(max_ihave_length=4)
-    eng = Engine(params, th, gossip=gp)
-    try:
-        eng.load_graph(net)
-        eng.set_seed(SEED)
-        st.push_to_engine(eng)
-        eng.msgs_init(1024, R, T0, Second)
-        with pytest.raises(GsimError) as ei:
-            for kk in range(1, 6):
-                eng.refresh_scores(tick_time(kk))
-                eng.heartbeat(kk, tick_time(kk))
-                for g in range(kk * R, kk * R + R):
-                    if g in sched:
-                        eng.publish(sched[g], g)
-                    eng.round(g)
-            eng.msg_stats()
-        assert ei.value.rc == _abi.GSIM_ERANGE and "MaxIHaveLength" in str(ei.value)
-    finally:
-        eng.close()
+@pytest.mark.parametrize("max_ihave_length", [4, 25])
+def test_max_ihave_length_truncations_bit_exact(require_gpu, max_ihave_length):
+    """Gossip windows over MaxIHaveLength: an advertiser sends each target a
+    random MaxIHaveLength-subset of a topic's window (emitGossip,
+    gossipsub.go:1763-1772) and a receiver asks for at most MaxIHaveLength
+    ids (handleIHave, gossipsub.go:679-690), with the promise among them.
+    k_ihave_pairs against the oracle's truncations, bit-exact per tick."""
+    from tickrun import run_parity
+    net, params, th, gp, st, sched = _gossip_window_run(max_ihave_length=max_ihave_length)
+    msgs, gs = run_parity(net, params, th, gp, st, list(range(1, 6)), sched, ring=1024)
+    assert gs["iwant_ids"] > 0 and gs["iwant_responses"] > 0
+
+
+def _retransmission_case(retransmission):
+    from fixtures import beacon_params, synthetic_state
+    from gsim.engine import random_regular
+    from tickrun import subscribed_schedule
+    rng = np.random.default_rng(3131 + retransmission)
+    n, k, T = 800, 16, 2
+    params = beacon_params(T)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2, GossipRetransmission=retransmission)
+    th = PeerScoreThresholds(GossipThreshold=-20000, PublishThreshold=-50000, GraylistThreshold=-80000)
+    net = random_regular(n, k, seed=n + 9, n_topics=T)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 8 / k)
+    ticks = list(range(1, 8))
+    sched = subscribed_schedule(rng, ticks, net, T, 4.0, 0.0, verdicts=(0.5, 0.0, 0.0, 0.0, 0.5))
+    return net, params, th, gp, st, ticks, sched
+
+
+@pytest.mark.parametrize("retransmission", [1, 2])
+def test_retransmission_case_refuses_serves_in_the_oracle(retransmission):
+    """The GPU case below is sensitive: in the oracle some (message, peer)
+    pairs are asked for more than GossipRetransmission times, and refused."""
+    net, params, th, gp, st, ticks, sched = _retransmission_case(retransmission)
+    msgs = ob.Msgs(net.n, st.T, 512, R, T0, Second)
+    msgs.log()
+    lib = ob.load()
+    refused = 0
+    for kk in ticks:
+        now = tick_time(kk)
+        v = st.view()
+        lib.orc_refresh_scores(v, now)
+        msgs.penalties(st, now)
+        lib.orc_ip_colocation(v)
+        lib.orc_compute_scores(v)
+        msgs.heartbeat(st, kk, now, SEED)
+        for g in range(kk * R, kk * R + R):
+            for (mid, t, o, inv) in sched.get(g, []):
+                msgs.publish(st, mid, t, o, inv, g)
+            msgs.round(st, g)
+        ev = msgs.events()
+        refused += int(((ev["kind"] == ob.EV_SERVE) & (ev["x"] > retransmission)).sum())
+    assert refused > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("retransmission", [1, 2])
+def test_gossip_retransmission_limits_bad_signature_serves(require_gpu, retransmission):
+    """mcache.GetForPeer's count (mcache.go:73-86, handleIWant
+    gossipsub.go:712-715): a message with a bad signature is never marked
+    seen by its receivers, so they keep asking its origin; answers beyond
+    GossipRetransmission per (message, peer) are refused.  Bit-exact with the
+    oracle's peertx table."""
+    from tickrun import run_parity
+    net, params, th, gp, st, ticks, sched = _retransmission_case(retransmission)
+    msgs, gs = run_parity(net, params, th, gp, st, ticks, sched, ring=512)
+    assert gs["iwant_responses"] > 0

@@ -122,3 +122,32 @@ def test_rccl_single_rank_group_bit_exact(require_gpu):
     sched = subscribed_schedule(rng, ticks, net, T, 4.0, 0.03)
     msgs, gs = run_parity(net, params, th, gp, st, ticks, sched, ring=512, eng=eng)
     assert msgs.stats[1] > n and gs["iwant_ids"] >= 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_sharded_gossip_truncation_and_retransmission(require_gpu):
+    """3 shards with MaxIHaveLength below the topics' gossip windows (the
+    per-peer IHAVE subsets and the IWANT cap, k_ihave_pairs on ghost
+    advertisers) and bad-signature messages served at most
+    GossipRetransmission times per (message, peer)."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim.engine import random_regular
+    from gsim.shard import ShardedEngine
+    from tickrun import SEED, run_parity, subscribed_schedule
+    rng = np.random.default_rng(515)
+    n, T = 2400, 6
+    net = random_regular(n, 16, seed=41, n_topics=T)
+    params = beacon_params(T)
+    th = PeerScoreThresholds(GossipThreshold=-20000, PublishThreshold=-50000, GraylistThreshold=-80000)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2, MaxIHaveLength=6, GossipRetransmission=1)
+    eng = ShardedEngine(params, th, gossip=gp, shards=3)
+    eng.load_graph(net)
+    eng.set_seed(SEED)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 0.5)
+    st.push_to_engine(eng)
+    ticks = list(range(1, 6))
+    sched = subscribed_schedule(rng, ticks, net, T, 8.0, 0.0, verdicts=(0.7, 0.05, 0.05, 0.0, 0.2))
+    _, gs = run_parity(net, params, th, gp, st, ticks, sched, ring=1024, eng=eng)
+    assert gs["iwant_ids"] > 0 and gs["iwant_responses"] > 0
