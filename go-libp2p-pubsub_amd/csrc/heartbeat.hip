@@ -32,6 +32,12 @@ struct Extra {
     int64_t n16 = 0, n32 = 0, n64 = 0;
     // hub observers after them: rows of 65..256, then 257..1024 connections
     int64_t nh256 = 0, nh1024 = 0;
+    // peer exchange (gsim_gossipsub_params.do_px): topics with PX PRUNEs per
+    // observer, connection attempts per edge, the GRAFT RPCs that turned PX off
+    uint64_t* d_pxo = nullptr;
+    uint8_t* d_pxm = nullptr;
+    uint8_t* d_nopx = nullptr;
+    uint32_t* d_pxc = nullptr;         // [1 + 2E] connections made: count, then (dialer edge, peer edge)
 };
 
 struct HbArgs {
@@ -89,6 +95,12 @@ struct HbArgs {
     int64_t rdel_cap;
     const uint32_t* xq;
     ShardRanges sr;
+    // peer exchange (makePrune doPX, gossipsub.go:1866-1906; pxConnect 893-939)
+    int32_t do_px, prune_peers;
+    double accept_px;
+    uint64_t* pxo;             // [N] topics in which the observer sent a PRUNE with PX
+    uint8_t* pxm;              // [E] the row's owner tries to connect to col[e]
+    uint8_t* nopx;             // [E] a GRAFT of this sender turned PX off for its RPC
 };
 
 namespace {
@@ -614,6 +626,7 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
         double S_live = S;
         bool dirty = false;
         g.load_lastput(a, obs, subi, ovalid);
+        uint64_t pxt = 0;                               // topics with a PRUNE carrying PX
         if (a.gossip && valid) a.gstate[e] = S >= a.gossip_thr ? 1 : 0;
 
         // clearBackoff every 15 ticks (gossipsub.go:1627-1646)
@@ -747,7 +760,10 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
                     const int j = a.Dout - obD < nb ? a.Dout - obD : nb;
                     keep = (inD && !(rest && rr < j)) || (cb && rb < j);
                 }
-                if (m && !keep) prune();
+                if (m && !keep) {
+                    prune();
+                    if (a.do_px) ctl |= GSIM_CTL_PX;     // makePrune(p, topic, doPX && !noPX[p]) (1690)
+                }
             }
 
             // enough outbound peers? (1492-1518)
@@ -820,8 +836,11 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
                     atomicOr(reinterpret_cast<unsigned long long*>(a.cany_out + col), 1ull << t);
                 }
             }
+            if (a.do_px && g.any((ctl & GSIM_CTL_PX) != 0)) pxt |= 1ull << t;
           }
         }
+        // sendGraftPrune follows every topic: k_px_emit picks the PX peers
+        if (a.do_px && pxt && gl == 0 && ovalid) a.pxo[obs] = pxt;
 }
 
 // W-lane groups: W = 64 one observer per wavefront, W = 32 two, W = 16 four
@@ -958,6 +977,8 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
         const int deg = (int)(a.row_ptr[rcv + 1] - b);
         const int nch = (deg + 63) >> 6;                    // rows longer than 64: 64-edge chunks in order
         const uint64_t subr = a.sub[rcv];
+        uint64_t pxo = 0;          // topics with a PRUNE reply carrying PX (mesh full, gossipsub.go:812-818)
+        bool nopx_set = false;     // this lane marked a sender whose RPC turned PX off
         for (int32_t t0 = 0; t0 < a.T; t0 += kFlagChunk) {
           if (!((any >> t0) & ((1ull << kFlagChunk) - 1))) continue;
           for (int j = 0; j < kFlagChunk; ++j) {
@@ -984,12 +1005,15 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
               uint64_t pending = ballot(c != 0);
               if (!pending) continue;
               if (c) a.ctl_in[i] = 0;
-              if (!joined) continue;                          // unknown topic: ignored
+              if (!joined) {                                  // unknown topic: ignored, no PX (753-759)
+                  if (a.do_px && (c & GSIM_CTL_GRAFT)) { a.nopx[e] = 1; nopx_set = true; }
+                  continue;
+              }
               uint8_t fl = valid ? a.mflags[i] : 0;
               while (pending) {
                 const int q = __ffsll((long long)pending) - 1;
                 pending &= pending - 1;
-                int delta = 0;
+                int delta = 0, pxr = 0;
                 if (lane == q) {
                     const uint8_t fl_in = fl;
                     const uint32_t rv = a.rev[e];                // receiver's record of the sender
@@ -1001,6 +1025,7 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                     const int64_t bo0 = bo;
                     uint8_t reply = 0;
                     if ((c & GSIM_CTL_GRAFT) && !(fl & GSIM_TF_MESH)) {
+                        bool off = true;                     // doPX = false for the RPC
                         if (a.direct[e]) {
                             // no GRAFT to/from direct peers: answered with PRUNE (gossipsub.go:768-776)
                             reply = GSIM_CTL_PRUNE;
@@ -1019,14 +1044,18 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                             const int64_t ex = a.now + a.prune_backoff;
                             if (bo < ex) bo = ex;
                         } else if (mesh >= a.Dhi && !a.outbound[e]) {
-                            reply = GSIM_CTL_PRUNE;
+                            reply = (uint8_t)(GSIM_CTL_PRUNE | (a.do_px ? GSIM_CTL_PX : 0));
+                            pxr = a.do_px;
+                            off = false;
                             const int64_t ex = a.now + a.prune_backoff;
                             if (bo < ex) bo = ex;
                         } else {
                             stats_graft(a, tracked, scored, sf);
                             fl |= GSIM_TF_MESH;
                             delta += 1;
+                            off = false;
                         }
+                        if (a.do_px && off) { a.nopx[e] = 1; nopx_set = true; }
                     }
                     if (c & GSIM_CTL_PRUNE) {
                         if (fl & GSIM_TF_MESH) delta -= 1;
@@ -1057,6 +1086,7 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                     }
                 }
                 mesh += __shfl(delta, q, 64);
+                if (__shfl(pxr, q, 64)) pxo |= 1ull << t;
               }
               if (nch == 1 && a.mmask) {                      // the delivery's mesh mask of the row
                   const uint32_t cj = valid ? a.col[e] : 0u;
@@ -1066,7 +1096,162 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
             }
           }
         }
+        if (a.do_px && (pxo || ballot(nopx_set))) {
+            // a sender whose RPC turned PX off gets its PRUNE replies without PX
+            // (doPX is per handleGraft call, gossipsub.go:744-834); the marks are reset
+            for (int ch = 0; ch < nch; ++ch) {
+                const bool valid = ch * 64 + lane < deg;
+                const uint32_t e = b + (uint32_t)(ch * 64 + lane);
+                if (!valid || !a.nopx[e]) continue;
+                a.nopx[e] = 0;
+                const uint32_t re = a.rev[e];
+                for (uint64_t q = pxo; q; q &= q - 1) {
+                    const int64_t r = (int64_t)(__ffsll((long long)q) - 1) * a.E + re;
+                    a.ctl_out[r] = (uint8_t)(a.ctl_out[r] & ~GSIM_CTL_PX);
+                }
+            }
+            if (lane == 0 && pxo) a.pxo[rcv] = pxo;
+        }
     }
+}
+
+// makePrune's peer exchange and the pruned peer's handlePrune / pxConnect
+// (gossipsub.go:1866-1906, 860-869, 893-939) for the PRUNEs an observer just
+// sent with PX (GSIM_CTL_PX in ctl_out; pxo[obs] lists their topics): the
+// PX list is getPeers(topic, PrunePeers, xp != p && Score(xp) >= 0), the
+// PrunePeers smallest Philox keys (the pruned peer's row position in the
+// topic word: every PRUNE its own shuffle).  live: Score is the observer's
+// live score (the heartbeat's sendGraftPrune, after every topic); else the
+// snapshot (the control round's GRAFT replies).  The pruned
+// peer ignores PX from a peer it scores below acceptPXThreshold; every listed
+// peer with a known address (an edge of its row) is a connection attempt
+// (pxm), resolved between ticks by gsim_px_connect.  One wave per observer;
+// rows of at most 1024 connections (keys and scores staged in LDS).
+constexpr int kPxRow = 1024;
+
+// LDS written by some lanes of a wave, read by others
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(256) void k_px_emit(HbArgs a, int live, uint32_t key_tick, uint32_t purpose)
+{
+    __shared__ double s_sc[4][kPxRow];
+    __shared__ uint64_t s_key[4][kPxRow];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double* sc = s_sc[wid];
+    uint64_t* key = s_key[wid];
+    for (int64_t obs = a.olo + (int64_t)blockIdx.x * 4 + wid; obs < a.ohi; obs += (int64_t)gridDim.x * 4) {
+        const uint64_t mask = a.pxo[obs];
+        if (!mask) continue;
+        if (lane == 0) a.pxo[obs] = 0;
+        const uint32_t b = a.row_ptr[obs];
+        const int deg = (int)(a.row_ptr[obs + 1] - b);
+        const uint32_t gobs = glob(a, (uint32_t)obs);
+        for (int q = lane; q < deg; q += 64) {
+            const uint32_t e = b + (uint32_t)q, x = a.col[e], rv = a.rev[e];
+            sc[q] = live ? score_of_record(a, rv, x) : a.score[rv];
+        }
+        wave_lds_sync();
+        for (uint64_t tm = mask; tm; tm &= tm - 1) {
+            const int32_t t = __ffsll((long long)tm) - 1;
+            for (int p0 = 0; p0 < deg; p0 += 64) {
+                const uint32_t ep_l = b + (uint32_t)(p0 + lane);
+                const bool pr = p0 + lane < deg && (a.ctl_out[(int64_t)t * a.E + a.rev[ep_l]] & GSIM_CTL_PX);
+                for (uint64_t pm = __ballot(pr); pm; pm &= pm - 1) {
+                    const int pos = p0 + __ffsll((long long)pm) - 1;
+                    const uint32_t ep = b + (uint32_t)pos, p = a.col[ep];
+                    if (a.score[ep] < a.accept_px) continue;       // p's snapshot score of obs (record order)
+                    const uint32_t kt = (uint32_t)t + 64u * (uint32_t)(pos + 1);
+                    uint32_t n = 0;
+                    for (int q0 = 0; q0 < deg; q0 += 64) {
+                        const int q = q0 + lane;
+                        bool c = false;
+                        if (q < deg && q != pos) {
+                            const uint32_t e = b + (uint32_t)q, x = a.col[e];
+                            c = (a.rstate[e] & GSIM_ES_CONNECTED) && ((a.sub[x] >> t) & 1ull) && sc[q] >= 0.0;
+                            key[q] = c ? select_key(a.seed, key_tick, gobs, kt, purpose, glob(a, x), (uint32_t)q) : ~0ull;
+                        } else if (q < deg) {
+                            key[q] = ~0ull;
+                        }
+                        n += (uint32_t)__popcll(__ballot(c));
+                    }
+                    wave_lds_sync();
+                    uint64_t tau = ~0ull - 1;                      // every candidate (keys of others are ~0)
+                    if ((int32_t)n > a.prune_peers) {
+                        uint64_t lo = 0, hi = ~0ull - 1;
+                        while (lo < hi) {
+                            const uint64_t mid = lo + ((hi - lo) >> 1);
+                            uint32_t c = 0;
+                            for (int q0 = 0; q0 < deg; q0 += 64) {
+                                const int q = q0 + lane;
+                                c += (uint32_t)__popcll(__ballot(q < deg && key[q] <= mid));
+                            }
+                            if ((int32_t)c >= a.prune_peers) hi = mid; else lo = mid + 1;
+                        }
+                        tau = lo;
+                    }
+                    const uint32_t pb = a.row_ptr[p], pe = a.row_ptr[p + 1];
+                    for (int q0 = 0; q0 < deg; q0 += 64) {
+                        const int q = q0 + lane;
+                        if (q >= deg || key[q] > tau) continue;
+                        const uint32_t x = a.col[b + (uint32_t)q];
+                        uint32_t lo = pb, hi = pe;                 // p's row is sorted: its edge to x
+                        while (lo < hi) {
+                            const uint32_t mid = lo + ((hi - lo) >> 1);
+                            if (a.col[mid] < x) lo = mid + 1; else hi = mid;
+                        }
+                        // pxConnect skips peers it is connected to
+                        if (lo < pe && a.col[lo] == x && !(a.rstate[lo] & GSIM_ES_CONNECTED)) a.pxm[lo] = 1;
+                    }
+                    wave_lds_sync();
+                }
+            }
+        }
+    }
+}
+
+// Connection attempts to connections (the connector, gossipsub.go:941-973):
+// each marked pair once (from its lower end), dialled by the peer that asked
+// (the lower id when both did); pairs already connected are skipped.  Out:
+// pxc[0] = count, then per connection (dialer's edge, peer's edge).
+__global__ __launch_bounds__(256) void k_px_collect(const uint32_t* owner, const uint32_t* col, const uint32_t* rev,
+                                                    const uint8_t* rstate, uint8_t* pxm, int64_t E, uint32_t* pxc)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride) {
+        const uint32_t u = owner[e], v = col[e], r = rev[e];
+        if (u > v) continue;
+        const uint8_t x = pxm[e], y = pxm[r];
+        if (!(x | y)) continue;
+        pxm[e] = 0;
+        pxm[r] = 0;
+        if (rstate[e] & GSIM_ES_CONNECTED) continue;
+        const uint32_t k = atomicAdd(pxc, 1u);
+        pxc[1 + 2 * k] = x ? (uint32_t)e : r;
+        pxc[2 + 2 * k] = x ? r : (uint32_t)e;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_px_pairs(const uint32_t* pxc, uint32_t n, const uint32_t* owner,
+                                                  const uint32_t* col, uint32_t* out)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t ed = pxc[1 + 2 * k];
+    out[2 * k] = owner[ed];
+    out[2 * k + 1] = col[ed];
+}
+
+__global__ __launch_bounds__(256) void k_px_outbound(const uint32_t* pxc, uint32_t n, uint8_t* outbound)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    outbound[pxc[1 + 2 * k]] = 1;          // gs.outbound: the dialer's side (gossipsub.go:532-551)
+    outbound[pxc[2 + 2 * k]] = 0;
 }
 
 // inspectScoresExtended (score.go:472-500) for the connections e of
@@ -1334,6 +1519,18 @@ int alloc_extra(gsim_handle* h)
         h->bytes_allocated += sizeof(uint32_t) * all.size();
     }
     h->max_degree = mdall;   // every local row (a shard's ghost rows too)
+    if (h->gp.do_px && !h->sh) {
+        const size_t pb = sizeof(uint64_t) * (size_t)h->n + 2 * (size_t)h->e + sizeof(uint32_t) * (1 + 2 * (size_t)h->e);
+        e = hipMalloc((void**)&h->x->d_pxo, sizeof(uint64_t) * (size_t)h->n);
+        if (e == hipSuccess) e = hipMalloc((void**)&h->x->d_pxm, (size_t)h->e);
+        if (e == hipSuccess) e = hipMalloc((void**)&h->x->d_nopx, (size_t)h->e);
+        if (e == hipSuccess) e = hipMalloc((void**)&h->x->d_pxc, sizeof(uint32_t) * (1 + 2 * (size_t)h->e));
+        if (e == hipSuccess) e = hipMemsetAsync(h->x->d_pxo, 0, sizeof(uint64_t) * (size_t)h->n, h->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(h->x->d_pxm, 0, (size_t)h->e, h->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(h->x->d_nopx, 0, (size_t)h->e, h->stream);
+        if (e != hipSuccess) return hip_check(h, e, "peer exchange state");
+        h->bytes_allocated += pb;
+    }
     return GSIM_OK;
 }
 
@@ -1345,6 +1542,10 @@ void free_extra(gsim_handle* h)
     if (h->x->d_rows) (void)hipFree(h->x->d_rows);
     if (h->x->d_lastpub) (void)hipFree(h->x->d_lastpub);
     if (h->x->d_fantopics) (void)hipFree(h->x->d_fantopics);
+    if (h->x->d_pxo) (void)hipFree(h->x->d_pxo);
+    if (h->x->d_pxm) (void)hipFree(h->x->d_pxm);
+    if (h->x->d_nopx) (void)hipFree(h->x->d_nopx);
+    if (h->x->d_pxc) (void)hipFree(h->x->d_pxc);
     delete h->x;
     h->x = nullptr;
 }
@@ -1418,6 +1619,10 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     }
     a.olo = (uint32_t)h->olo();
     a.ohi = (uint32_t)h->ohi();
+    a.do_px = h->x->d_pxo ? 1 : 0;
+    a.prune_peers = h->gp.prune_peers;
+    a.accept_px = h->th.accept_px_threshold;
+    a.pxo = h->x->d_pxo; a.pxm = h->x->d_pxm; a.nopx = h->x->d_nopx;
     return a;
 }
 
@@ -1508,6 +1713,8 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     if (x->nh1024)
         hipLaunchKernelGGL(k_fanout_heartbeat_hub<1024>, dim3((uint32_t)std::min<int64_t>(x->nh1024, 65536)),
                            dim3(1024), 0, h->stream, a, x->d_rows + x->n16 + x->n32 + x->n64 + x->nh256, x->nh1024);
+    if (a.do_px)   // sendGraftPrune's makePrune with PX, live scores after every topic
+        hipLaunchKernelGGL(k_px_emit, dim3(grid_rows(nown)), dim3(256), 0, h->stream, a, 1, (uint32_t)tick, (uint32_t)P_PX);
     return hip_check(h, hipGetLastError(), "k_heartbeat");
 }
 
@@ -1518,6 +1725,9 @@ int handle_control(gsim_handle* h, int32_t round, int64_t now)
     HbArgs a = make_hb_args(h, 0, now, round & 1);
     ProfScope ps(h, GSIM_K_CONTROL);
     hipLaunchKernelGGL(k_handle_control, dim3(grid_rows(h->ohi() - h->olo())), dim3(256), 0, h->stream, a);
+    if (a.do_px)   // handleGraft's PRUNE replies with PX (snapshot scores)
+        hipLaunchKernelGGL(k_px_emit, dim3(grid_rows(h->ohi() - h->olo())), dim3(256), 0, h->stream, a, 0,
+                           (uint32_t)((uint64_t)now ^ ((uint64_t)now >> 32)), (uint32_t)P_PX_GRAFT);
     return hip_check(h, hipGetLastError(), "k_handle_control");
 }
 
@@ -1572,6 +1782,30 @@ int gsim_read_snapshot(gsim_handle* h, int64_t obs_lo, int64_t obs_hi, gsim_peer
     return hip_check(h, e, "gsim_read_snapshot");
 }
 
+}  // extern "C"
+
+// AddPeer / RemovePeer at both ends of connections given as device edges:
+// edges[2q + d] = the edge of direction d of connection q (n2 = 2 * count).
+static int apply_connections(gsim_handle* h, const uint32_t* d_edges, int32_t n2, int32_t up, int64_t now)
+{
+    const int grid = (n2 + 255) / 256;
+    HbArgs a = make_hb_args(h, 0, now, 0);   // ctl_in/ctl_out cover both inbox planes
+    ChurnArgs c{};
+    c.edges = d_edges; c.n2 = n2; c.up = up ? 1 : 0; c.retain = h->pp.retain_score_ns;
+    c.estate = h->d_estate; c.rstate = h->d_rstate; c.pen = h->d_pen; c.expire = h->d_expire;
+    c.first = h->d_first; c.invalid = h->d_invalid;
+    c.skip_unjoined = h->unjoined_zero ? 1 : 0;
+    hipLaunchKernelGGL(k_churn_apply, dim3(grid), dim3(256), 0, h->stream, a, c);
+    const hipError_t e = hipGetLastError();   // stream-ordered: the next call's copy into the scratch follows this kernel
+    if (e != hipSuccess) return hip_check(h, e, "k_churn_apply");
+    h->p6_dirty = true;          // the tracked set (and so the IP sets) changed
+    if (!up) h->maybe_retained = true;
+    h->score_version++;          // connected / tracked bits feed the delivery state (churn only clears mesh bits: the masks stay a superset)
+    return GSIM_OK;
+}
+
+extern "C" {
+
 int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, int32_t up, int64_t now)
 {
     if (!h) return GSIM_EINVAL;
@@ -1620,25 +1854,60 @@ int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, i
     }
     if (e == hipSuccess) e = hipMemcpyAsync(&bad, d_bad, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);   // a bad pair fails the call before any change
-    if (e == hipSuccess && bad == 0xFFFFFFFFu) {
-        HbArgs a = make_hb_args(h, 0, now, 0);   // ctl_in/ctl_out cover both inbox planes
-        ChurnArgs c{};
-        c.edges = d_edges; c.n2 = n2; c.up = up ? 1 : 0; c.retain = h->pp.retain_score_ns;
-        c.estate = h->d_estate; c.rstate = h->d_rstate; c.pen = h->d_pen; c.expire = h->d_expire;
-        c.first = h->d_first; c.invalid = h->d_invalid;
-        c.skip_unjoined = h->unjoined_zero ? 1 : 0;
-        hipLaunchKernelGGL(k_churn_apply, dim3(grid), dim3(256), 0, h->stream, a, c);
-        e = hipGetLastError();   // stream-ordered: the next call's copy into the scratch follows this kernel
-    }
     if (e != hipSuccess) return hip_check(h, e, "gsim_set_connections");
     if (bad != 0xFFFFFFFFu) {
         h->err = "pair " + std::to_string(bad) + " is not a connection";
         return GSIM_EINVAL;
     }
-    h->p6_dirty = true;          // the tracked set (and so the IP sets) changed
-    if (!up) h->maybe_retained = true;
-    h->score_version++;          // (churn only clears mesh bits: the masks stay a superset)          // connected / tracked bits feed the delivery state
-    return GSIM_OK;
+    return apply_connections(h, d_edges, n2, up, now);
+}
+
+int gsim_px_connect(gsim_handle* h, int64_t now, uint32_t* pairs, int64_t cap, int64_t* n_connected)
+{
+    if (!h || !n_connected) return GSIM_EINVAL;
+    if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
+    *n_connected = 0;
+    if (h->e == 0 || !h->x) { h->err = "no graph loaded"; return GSIM_ESTATE; }
+    if (!h->x->d_pxm) return GSIM_OK;                     // WithPeerExchange is off
+    uint32_t* pxc = h->x->d_pxc;
+    hipError_t e = hipMemsetAsync(pxc, 0, sizeof(uint32_t), h->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_px_collect, dim3((uint32_t)std::min<int64_t>((h->e + 255) / 256, 16384)), dim3(256), 0,
+                           h->stream, (const uint32_t*)h->d_owner, (const uint32_t*)h->d_col,
+                           (const uint32_t*)h->d_rev, (const uint8_t*)h->d_rstate, h->x->d_pxm, h->e, pxc);
+        e = hipGetLastError();
+    }
+    uint32_t n = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&n, pxc, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "gsim_px_connect");
+    *n_connected = n;
+    if (n == 0) return GSIM_OK;
+    if (pairs && cap > 0) {
+        // (dialer, peer) of every connection, sorted (4n <= 2E: after the edge list)
+        hipLaunchKernelGGL(k_px_pairs, dim3((n + 255) / 256), dim3(256), 0, h->stream, (const uint32_t*)pxc, n,
+                           (const uint32_t*)h->d_owner, (const uint32_t*)h->d_col, pxc + 1 + 2 * (size_t)n);
+        std::vector<uint32_t> pv(2 * (size_t)n);
+        e = hipGetLastError();
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(pv.data(), pxc + 1 + 2 * (size_t)n, sizeof(uint32_t) * pv.size(), hipMemcpyDeviceToHost,
+                               h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) return hip_check(h, e, "gsim_px_connect pairs");
+        std::vector<std::pair<uint32_t, uint32_t>> pr((size_t)n);
+        for (size_t q = 0; q < n; ++q) pr[q] = {pv[2 * q], pv[2 * q + 1]};
+        std::sort(pr.begin(), pr.end());
+        for (size_t q = 0; q < n && (int64_t)q < cap; ++q) { pairs[2 * q] = pr[q].first; pairs[2 * q + 1] = pr[q].second; }
+    }
+    int rc = deliver_flush(h);                    // as gsim_set_connections
+    if (!rc) rc = materialize_mcnt(h);
+    if (rc) return rc;
+    ProfScope ps(h, GSIM_K_CHURN);
+    hipLaunchKernelGGL(k_px_outbound, dim3((n + 255) / 256), dim3(256), 0, h->stream, (const uint32_t*)pxc, n,
+                       h->d_outbound);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_check(h, e, "k_px_outbound");
+    return apply_connections(h, pxc + 1, (int32_t)(2 * n), 1, now);
 }
 
 }  // extern "C"

@@ -52,6 +52,8 @@ enum Purpose : uint32_t {
     P_IHAVE_TRUNC = 11,// emitGossip's per-peer shuffleStrings  gossipsub.go:1766-1771
     P_FANOUT_NEW = 12, // Publish: getPeers for a new fanout   gossipsub.go:1020-1023 (counter word 0 = round)
     P_FANOUT = 13,     // heartbeat fanout top-up             gossipsub.go:1578-1585
+    P_PX = 14,         // makePrune's getPeers (heartbeat)    gossipsub.go:1879-1882
+    P_PX_GRAFT = 15,   // makePrune's getPeers (GRAFT reply)  gossipsub.go:831-834
 };
 
 // Key of a choice made per (observer, other peer, message slot): the other

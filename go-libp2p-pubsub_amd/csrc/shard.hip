@@ -877,6 +877,11 @@ int group_create(const gsim_peer_score_params* params, const gsim_topic_score_pa
                  const gsim_thresholds* th, const gsim_gossipsub_params* gp, int32_t shards,
                  const std::vector<std::pair<int, int>>& local, gsim_group** out, char* err, size_t errlen)
 {
+    if (gp && gp->do_px) {
+        // pxConnect resolves a pruned peer's whole row, which a shard holds only for its own peers
+        if (err && errlen) std::snprintf(err, errlen, "peer exchange (do_px) is not supported on a sharded group");
+        return GSIM_EINVAL;
+    }
     gsim_group* g = new gsim_group();
     g->K = shards;
     const char* ser = std::getenv("GSIM_GROUP_SERIAL");

@@ -30,7 +30,7 @@ TF_MESH = 0x04
 TF_FANOUT = 0x08
 CTL_GRAFT = 0x01
 CTL_PRUNE = 0x02
-CTL_NOPX = 0x04
+CTL_PX = 0x04
 CTL_IHAVE = 0x08
 ES_TRACKED = 0x01
 ES_CONNECTED = 0x02
@@ -82,7 +82,7 @@ class CGossipSubParams(Structure):
         ("direct_connect_initial_delay_ns", c_int64), ("opportunistic_graft_ticks", c_uint64),
         ("opportunistic_graft_peers", c_int32), ("max_ihave_length", c_int32),
         ("graft_flood_threshold_ns", c_int64), ("max_ihave_messages", c_int32), ("flood_publish", c_int32),
-        ("iwant_followup_time_ns", c_int64),
+        ("iwant_followup_time_ns", c_int64), ("do_px", c_int32), ("_pad_px", c_int32),
     ]
 
 
@@ -219,6 +219,7 @@ SIGNATURES = [
     ("gsim_set_peer_behaviour", c_int32, [c_void_p, c_void_p]),
     ("gsim_gossip_stats", c_int32, [c_void_p, c_void_p]),
     ("gsim_set_connections", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int64]),
+    ("gsim_px_connect", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p]),
     ("gsim_set_direct_peers", c_int32, [c_void_p, c_void_p]),
     ("gsim_profile", c_int32, [c_void_p, c_int32]),
     ("gsim_profile_read", c_int32, [c_void_p, c_void_p, c_void_p, c_int32]),

@@ -297,6 +297,16 @@ class Engine:
         p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint32).reshape(-1, 2))
         self._check(self.lib.gsim_set_connections(self.h, _ptr(p), int(p.shape[0]), 1 if up else 0, int(now)))
 
+    def px_connect(self, now: int) -> np.ndarray:
+        """The connector for the attempts peer exchange queued this tick
+        (gsim_px_connect; pxConnect gossipsub.go:893-973): returns the
+        (dialer, peer) pairs that became connections, sorted."""
+        n = ctypes.c_int64(0)
+        cap = max(1, self.net.e // 2)
+        out = np.zeros((cap, 2), dtype=np.uint32)
+        self._check(self.lib.gsim_px_connect(self.h, int(now), _ptr(out), int(cap), ctypes.byref(n)))
+        return out[:min(n.value, cap)].copy()
+
     def set_direct_peers(self, flags):
         """WithDirectPeers as per-edge flags (edge order; None clears)
         (gsim_set_direct_peers; gossipsub.go:352-374)."""

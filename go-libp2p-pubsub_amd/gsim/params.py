@@ -186,6 +186,8 @@ class GossipSubParams:
     IWantFollowupTime: int = 3 * Second
     # router option WithFloodPublish (gossipsub.go:321-334), not a GossipSubParams field
     FloodPublish: bool = False
+    # router option WithPeerExchange (gossipsub.go:340-350): PRUNEs carry PX
+    PeerExchange: bool = False
 
     def to_c(self) -> _abi.CGossipSubParams:
         c = _abi.CGossipSubParams()
@@ -203,6 +205,7 @@ class GossipSubParams:
                                                                      self.OpportunisticGraftPeers)
         c.max_ihave_length, c.graft_flood_threshold_ns = self.MaxIHaveLength, self.GraftFloodThreshold
         c.flood_publish = 1 if self.FloodPublish else 0
+        c.do_px = 1 if self.PeerExchange else 0
         c.max_ihave_messages, c.iwant_followup_time_ns = self.MaxIHaveMessages, self.IWantFollowupTime
         return c
 

@@ -121,6 +121,8 @@ typedef struct gsim_gossipsub_params {
     int32_t max_ihave_messages;
     int32_t flood_publish;   /* router option WithFloodPublish (gossipsub.go:321-334); this fork's default is 0 */
     int64_t iwant_followup_time_ns;
+    int32_t do_px;           /* router option WithPeerExchange (gossipsub.go:340-350): PRUNEs carry PX; default 0 */
+    int32_t _pad_px;
 } gsim_gossipsub_params;
 
 /* ---- host-side parameter API (no device needed) ------------------------ */
@@ -250,6 +252,20 @@ int gsim_handle_control(gsim_handle* h, int32_t round, int64_t now_ns);
  * starts (re-derived if an up batch changed it).  GSIM_EINVAL if a
  * pair is not a connection or is listed twice (nothing is changed then). */
 int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, int32_t up, int64_t now_ns);
+
+/* Peer exchange (WithPeerExchange: gsim_gossipsub_params.do_px).  PRUNEs
+ * carry PX (makePrune, gossipsub.go:1866-1906: the heartbeat's Dhi prunes and
+ * handleGraft's mesh-full replies); the pruned peer's handlePrune accepts it
+ * from peers it scores at least acceptPXThreshold and pxConnect queues a
+ * connection attempt to every listed peer it is not connected to
+ * (gossipsub.go:860-869, 893-939).  This call is the connector
+ * (gossipsub.go:941-973), run between ticks: every attempt whose peers know
+ * each other's address (an edge of the loaded graph) and are not connected
+ * becomes a connection, dialled by the peer that asked (outbound on its side;
+ * the lower id when both asked), with AddPeer at both ends as in
+ * gsim_set_connections.  pairs (optional, cap entries): the (dialer, peer)
+ * pairs connected, sorted.  Single engines only. */
+int gsim_px_connect(gsim_handle* h, int64_t now_ns, uint32_t* pairs, int64_t cap, int64_t* n_connected);
 
 /* ---- message propagation ------------------------------ */
 /* Rounds are numbered globally: round g belongs to heartbeat tick g / rounds
@@ -397,7 +413,7 @@ typedef enum gsim_field {
 /* control inbox bits (GSIM_F_CTL), one byte per [parity][topic][receiver edge] */
 #define GSIM_CTL_GRAFT    0x01u  /* ControlGraft  (pb/rpc.proto) */
 #define GSIM_CTL_PRUNE    0x02u  /* ControlPrune with Backoff = PruneBackoff/1s */
-#define GSIM_CTL_NOPX     0x04u  /* prune sent without peer exchange (noPX) */
+#define GSIM_CTL_PX       0x04u  /* the PRUNE carries peer exchange (makePrune doPX, gossipsub.go:1878-1903) */
 #define GSIM_CTL_IHAVE    0x08u  /* ControlIHave for this topic */
 #define GSIM_ES_TRACKED   0x01u
 #define GSIM_ES_CONNECTED 0x02u

@@ -59,6 +59,8 @@ typedef struct orc_net {
     int64_t* lastpub;          /* [N][T] gs.lastpub[topic] (ns), 0 = none (peer-major) */
     uint64_t* fan_topics;      /* [N] bit t: gs.fanout[topic t] exists */
     const uint8_t* direct;     /* [E] col[e] is in the observer's gs.direct set (WithDirectPeers), or NULL */
+    uint8_t* px;               /* [E] peer exchange (WithPeerExchange): 1 = the row's owner tries to
+                                  connect to col[e] (pxConnect), or NULL */
 } orc_net;
 
 /* ---- message propagation (oracle_deliver.c) ------------------------------ */
@@ -131,6 +133,13 @@ void   orc_add_peer(orc_net* s, int64_t e);                      /* score.go:595
 void   orc_remove_peer(orc_net* s, int64_t e, int64_t now);      /* score.go:611-644 */
 /* connection churn between ticks, both endpoints (oracle_net.c) */
 int32_t orc_churn(orc_net* s, const uint32_t* pairs, int32_t count, int32_t up, int64_t now);
+/* The connector (gossipsub.go:941-973) for the attempts pxConnect queued
+ * (893-939): every marked pair that is a known address (a CSR edge) and not
+ * connected becomes a connection, dialled by the peer that asked (the lower
+ * id when both did: outbound on its side), with AddPeer at both ends.  The
+ * connections made go to pairs (dialer, peer), at most cap; returns their
+ * number.  Clears the marks. */
+int64_t orc_px_connect(orc_net* s, int64_t now, uint32_t* pairs, int64_t cap);
 void   orc_set_topic_params(orc_net* s, int32_t topic, gsim_topic_score_params* tp_slot,
                             const gsim_topic_score_params* np); /* score.go:201-241 */
 void   orc_mark_first(orc_net* s, int64_t e, int32_t topic);     /* score.go:919-946 */

@@ -19,6 +19,8 @@ enum {
     P_IHAVE_TRUNC = 11, /* emitGossip: per-peer shuffleStrings(mids)   gossipsub.go:1766-1771 */
     P_FANOUT_NEW = 12,  /* Publish: getPeers for a new fanout          gossipsub.go:1020-1023 */
     P_FANOUT = 13,      /* heartbeat: getPeers for the fanout top-up  gossipsub.go:1578-1585 */
+    P_PX = 14,          /* makePrune: getPeers for PX (heartbeat)      gossipsub.go:1879-1882 */
+    P_PX_GRAFT = 15,    /* makePrune: getPeers for PX (GRAFT reply)    gossipsub.go:831-834 */
 };
 
 static inline uint64_t okey(uint64_t seed, uint64_t tick, uint32_t obs, int32_t topic, uint32_t purpose,

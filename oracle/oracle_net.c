@@ -91,6 +91,51 @@ static void graft_peer(hb* h, uint32_t e)
     send_ctl(h, e, GSIM_CTL_GRAFT);
 }
 
+/* Peer exchange of one PRUNE (observer h->i to col[ep], topic h->t):
+ * makePrune's getPeers(topic, PrunePeers, xp != p && Score(xp) >= 0)
+ * (gossipsub.go:1866-1906) and the pruned peer's handlePrune / pxConnect
+ * (860-869, 893-939).  live: Score is the observer's live score (the
+ * heartbeat's sendGraftPrune); else its snapshot (handleGraft's replies, the
+ * control rounds' declared divergence).  The keys put the pruned peer's row
+ * position into the topic word: each PRUNE's list is its own shuffle.  The
+ * receiver ignores PX from a peer it scores below acceptPXThreshold (its
+ * snapshot); every listed peer it is not connected to is a connection
+ * attempt, marked at its edge to that peer when the address is known (a CSR
+ * edge).  Attempts are resolved between ticks (orc_px_connect). */
+static int64_t find_edge(const orc_net* s, uint32_t i, uint32_t j);
+
+static void px_emit(hb* h, uint32_t ep, int live, uint32_t purpose, uint64_t key_tick)
+{
+    orc_net* s = h->s;
+    if (!s->px) return;
+    const uint32_t p = s->col[ep];
+    if (s->score[s->rev[ep]] < s->th->accept_px_threshold) return;
+    const uint32_t deg = h->en - h->b;
+    cand buf[1024];
+    cand* c = deg <= 1024 ? buf : (cand*)malloc(sizeof(cand) * deg);
+    int n = 0;
+    const int32_t kt = h->t + 64 * (int32_t)(ep - h->b + 1);
+    for (uint32_t e = h->b; e < h->en; ++e) {
+        if (e == ep || !topic_peer(h, e)) continue;
+        const double sc = live ? orc_score_edge(s, e) : s->score[e];
+        if (sc < 0) continue;
+        c[n].key = okey(h->seed, key_tick, h->i, kt, purpose, s->col[e], e - h->b);
+        c[n].e = e;
+        c[n].score = sc;
+        ++n;
+    }
+    qsort(c, (size_t)n, sizeof(cand), cmp_key);
+    if (n > s->gp->prune_peers) n = s->gp->prune_peers;
+    for (int q = 0; q < n; ++q) {
+        const int64_t ex = find_edge(s, p, s->col[c[q].e]);
+        if (ex < 0) continue;                                  /* no known address */
+        if (s->estate[ex] & ES_CONN) continue;                 /* pxConnect: already connected */
+#pragma omp atomic write
+        s->px[ex] = 1;
+    }
+    if (c != buf) free(c);
+}
+
 typedef int (*filter_fn)(const hb* h, uint32_t e, double arg);
 
 /* getPeers, gossipsub.go:1908-1928: filter the topic peers, shuffle (= order
@@ -196,7 +241,12 @@ static void maintain(hb* h)
                 if (s->outbound[c[q].e]) { ROTATE(q); --ineed; }
             #undef ROTATE
         }
-        for (int q = gp->d; q < n; ++q) prune_peer(h, c[q].e);
+        for (int q = gp->d; q < n; ++q) {
+            prune_peer(h, c[q].e);
+            /* sendGraftPrune: makePrune(p, topic, doPX && !noPX[p]); noPX marks the
+             * negative-score prunes only (1404-1410, 1690) */
+            if (gp->do_px) send_ctl(h, c[q].e, GSIM_CTL_PX);
+        }
     }
 
     /* do we have enough outbound peers? (1492-1518) */
@@ -297,8 +347,13 @@ void orc_fanout_publish(orc_net* s, uint32_t origin, int32_t topic, int64_t g, i
     s->lastpub[(int64_t)origin * s->t + topic] = now;
 }
 
+/* The network's Philox seed as the last heartbeat received it: the control
+ * rounds' PX choices (GRAFT replies) use it too. */
+static uint64_t g_px_seed;
+
 void orc_heartbeat_gossip(orc_net* s, orc_msgs* m, uint64_t tick, int64_t now, uint64_t seed)
 {
+    g_px_seed = seed;
     uint8_t* out = s->ctl;   /* heartbeat output = parity-0 inbox, handled in round 0 */
     if (m) {
         priv* p = orc_msgs_priv(m);
@@ -337,6 +392,13 @@ void orc_heartbeat_gossip(orc_net* s, orc_msgs* m, uint64_t tick, int64_t now, u
             maintain(&h);
             if (m) orc_gossip_emit(s, m, (uint32_t)i, t, tick, seed, GSIM_TF_MESH);
         }
+        /* sendGraftPrune (1672-1707) after every topic: PX with the live scores */
+        if (s->gp->do_px)
+            for (int32_t t = 0; t < s->t; ++t) {
+                h.t = t;
+                for (uint32_t e = h.b; e < h.en; ++e)
+                    if (out[(int64_t)t * s->e + s->rev[e]] & GSIM_CTL_PX) px_emit(&h, e, 1, P_PX, tick);
+            }
         fanout(&h, m);
     }
 }
@@ -346,16 +408,18 @@ void orc_heartbeat(orc_net* s, uint64_t tick, int64_t now, uint64_t seed)
     orc_heartbeat_gossip(s, NULL, tick, now, seed);
 }
 
-/* handleGraft for one (receiver, sender edge, topic), gossipsub.go:748-825. */
-static void handle_graft(hb* h, uint32_t e)
+/* handleGraft for one (receiver, sender edge, topic), gossipsub.go:748-825.
+ * Returns 1 when the GRAFT turns off PX for the whole RPC (doPX = false:
+ * unknown topic, direct peer, backoff, negative score). */
+static int handle_graft(hb* h, uint32_t e)
 {
     orc_net* s = h->s;
     const gsim_gossipsub_params* gp = s->gp;
-    if (!((s->sub[h->i] >> h->t) & 1u)) return;                /* unknown topic: ignore */
-    if (in_mesh(h, e)) return;                                 /* already in mesh */
+    if (!((s->sub[h->i] >> h->t) & 1u)) return 1;             /* unknown topic: ignore, no PX */
+    if (in_mesh(h, e)) return 0;                               /* already in mesh */
     if (is_direct(h, e)) {                                     /* no GRAFT from direct peers: PRUNE */
         send_ctl(h, e, GSIM_CTL_PRUNE);
-        return;
+        return 1;
     }
     int64_t expire = s->backoff[ti(h, e)];
     if (expire != 0 && h->now < expire) {                      /* backing off that peer */
@@ -364,20 +428,21 @@ static void handle_graft(hb* h, uint32_t e)
         if (h->now < flood_cutoff) orc_add_penalty(s, e, 1);
         do_add_backoff(h, e, gp->prune_backoff_ns);
         send_ctl(h, e, GSIM_CTL_PRUNE);
-        return;
+        return 1;
     }
     if (s->score[e] < 0) {                                     /* negative score */
         send_ctl(h, e, GSIM_CTL_PRUNE);
         do_add_backoff(h, e, gp->prune_backoff_ns);
-        return;
+        return 1;
     }
-    if (mesh_count(h) >= gp->dhi && !s->outbound[e]) {         /* mesh full, inbound */
-        send_ctl(h, e, GSIM_CTL_PRUNE);
+    if (mesh_count(h) >= gp->dhi && !s->outbound[e]) {         /* mesh full, inbound: PRUNE with PX */
+        send_ctl(h, e, (uint8_t)(GSIM_CTL_PRUNE | (gp->do_px ? GSIM_CTL_PX : 0)));
         do_add_backoff(h, e, gp->prune_backoff_ns);
-        return;
+        return 0;
     }
     orc_graft(s, e, h->t, h->now);                             /* tracer.Graft + mesh add */
     s->tflags[ti(h, e)] |= TF_MESH;
+    return 0;
 }
 
 /* handlePrune for one (receiver, sender edge, topic), gossipsub.go:842-870. */
@@ -396,13 +461,15 @@ static void handle_prune(hb* h, uint32_t e)
 
 int64_t orc_handle_control(orc_net* s, int32_t round, int64_t now)
 {
+    const uint64_t seed = g_px_seed;
     const int64_t TE = (int64_t)s->t * s->e;
     uint8_t* in = s->ctl + (int64_t)(round & 1) * TE;
     uint8_t* out = s->ctl + (int64_t)((round + 1) & 1) * TE;
     int64_t handled = 0;
 #pragma omp parallel for schedule(dynamic, 64) reduction(+ : handled)
     for (int64_t j = 0; j < s->n; ++j) {
-        hb h = {s, (uint32_t)j, s->row_ptr[j], s->row_ptr[j + 1], 0, 0, 0, now, out};
+        hb h = {s, (uint32_t)j, s->row_ptr[j], s->row_ptr[j + 1], 0, 0, s->gp->do_px ? seed : 0, now, out};
+        uint8_t* nopx = s->gp->do_px ? (uint8_t*)calloc((size_t)(h.en - h.b) + 1, 1) : NULL;
         for (int32_t t = 0; t < s->t; ++t) {
             h.t = t;
             for (uint32_t e = h.b; e < h.en; ++e) {     /* senders in row order */
@@ -410,9 +477,27 @@ int64_t orc_handle_control(orc_net* s, int32_t round, int64_t now)
                 if (!c) continue;
                 in[(int64_t)t * s->e + e] = 0;
                 ++handled;
-                if (c & GSIM_CTL_GRAFT) handle_graft(&h, e);
+                if (c & GSIM_CTL_GRAFT) {
+                    const int off = handle_graft(&h, e);
+                    if (nopx && off) nopx[e - h.b] = 1;
+                }
                 if (c & GSIM_CTL_PRUNE) handle_prune(&h, e);
             }
+        }
+        if (nopx) {
+            /* the replies of one RPC carry PX only if no GRAFT of it turned doPX off
+             * (gossipsub.go:744-834) */
+            const uint64_t kt = (uint64_t)now ^ ((uint64_t)now >> 32);
+            for (int32_t t = 0; t < s->t; ++t) {
+                h.t = t;
+                for (uint32_t e = h.b; e < h.en; ++e) {
+                    uint8_t* r = &out[(int64_t)t * s->e + s->rev[e]];
+                    if (!(*r & GSIM_CTL_PX)) continue;
+                    if (nopx[e - h.b]) *r &= (uint8_t)~GSIM_CTL_PX;
+                    else px_emit(&h, e, 0, P_PX_GRAFT, kt);
+                }
+            }
+            free(nopx);
         }
     }
     return handled;
@@ -470,4 +555,35 @@ int32_t orc_churn(orc_net* s, const uint32_t* pairs, int32_t count, int32_t up, 
         }
     }
     return -1;
+}
+
+int64_t orc_px_connect(orc_net* s, int64_t now, uint32_t* pairs, int64_t cap)
+{
+    if (!s->px) return 0;
+    uint32_t* conn = NULL;
+    int64_t n = 0, capc = 0;
+    for (int64_t u = 0; u < s->n; ++u)
+        for (uint32_t e = s->row_ptr[u]; e < s->row_ptr[u + 1]; ++e) {
+            const uint32_t v = s->col[e], r = s->rev[e];
+            if ((uint32_t)u > v || !(s->px[e] | s->px[r])) continue;      /* each pair once, from its lower end */
+            const int a = s->px[e] != 0;
+            s->px[e] = s->px[r] = 0;
+            if (s->estate[e] & ES_CONN) continue;                        /* connector: already connected */
+            if (n == capc) {
+                capc = capc ? 2 * capc : 256;
+                conn = (uint32_t*)realloc(conn, sizeof(uint32_t) * 2 * (size_t)capc);
+            }
+            conn[2 * n] = a ? (uint32_t)u : v;                           /* the dialer */
+            conn[2 * n + 1] = a ? v : (uint32_t)u;
+            ++n;
+        }
+    for (int64_t q = 0; q < n; ++q) {
+        const int64_t ed = find_edge(s, conn[2 * q], conn[2 * q + 1]);
+        ((uint8_t*)s->outbound)[ed] = 1;                                  /* gs.outbound (gossipsub.go:532-551) */
+        ((uint8_t*)s->outbound)[s->rev[ed]] = 0;
+        if (q < cap && pairs) { pairs[2 * q] = conn[2 * q]; pairs[2 * q + 1] = conn[2 * q + 1]; }
+    }
+    if (n) orc_churn(s, conn, (int32_t)n, 1, now);
+    free(conn);
+    return n;
 }

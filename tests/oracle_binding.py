@@ -33,6 +33,7 @@ class OrcNet(Structure):
         ("backoff", c_void_p),
         ("pp", c_void_p), ("tp", c_void_p), ("th", c_void_p), ("gp", c_void_p),
         ("ctl", c_void_p), ("lastpub", c_void_p), ("fan_topics", c_void_p), ("direct", c_void_p),
+        ("px", c_void_p),
     ]
 
 
@@ -111,6 +112,7 @@ def load():
             "orc_msgs_free_priv": (None, [POINTER(OrcMsgs)]),
             "orc_heartbeat_gossip": (None, [P, POINTER(OrcMsgs), c_uint64, c_int64, c_uint64]),
             "orc_gossip_penalties": (None, [P, POINTER(OrcMsgs), c_int64]),
+            "orc_px_connect": (c_int64, [P, c_int64, c_void_p, c_int64]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -153,6 +155,8 @@ class NetState:
         self.lastpub = np.zeros((net.n, self.T), dtype=np.int64)
         self.fan_topics = np.zeros(net.n, dtype=np.uint64)
         self.direct = np.zeros(E, dtype=np.uint8)          # gs.direct flags (configuration, not state)
+        # peer exchange attempts (WithPeerExchange), when on
+        self.px = np.zeros(E, dtype=np.uint8) if (gossip is not None and gossip.PeerExchange) else None
         self.rev = net.rev()
         self.p5 = np.zeros(net.n) if p5 is None else np.ascontiguousarray(p5, dtype=np.float64)
         self.ip_white = None if ip_white is None else np.ascontiguousarray(ip_white, dtype=np.uint8)
@@ -183,6 +187,7 @@ class NetState:
         v.ctl = _p(self.ctl)
         v.lastpub, v.fan_topics = _p(self.lastpub), _p(self.fan_topics)
         v.direct = _p(self.direct)
+        v.px = _p(self.px)
         self._view = v
         return ctypes.byref(v)
 
@@ -195,6 +200,16 @@ class NetState:
         p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint32).reshape(-1, 2))
         bad = load().orc_churn(self.view(), _p(p), int(p.shape[0]), 1 if up else 0, int(now))
         assert bad < 0, f"pair {bad} is not a connection"
+
+    def px_connect(self, now):
+        """orc_px_connect: the connector for this tick's PX attempts; returns
+        the (dialer, peer) pairs connected, sorted (outbound flags updated in
+        the network's array)."""
+        cap = max(1, self.net.e // 2)
+        out = np.zeros((cap, 2), dtype=np.uint32)
+        n = load().orc_px_connect(self.view(), int(now), _p(out), cap)
+        out = out[:n]
+        return out[np.lexsort((out[:, 1], out[:, 0]))] if n else out
 
     def push_to_engine(self, eng):
         for f in self.TOPIC_FIELDS + self.EDGE_FIELDS:

@@ -28,12 +28,15 @@ def restrict_to_subscriptions(st, net):
 
 
 def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, churn=None, after_tick=None,
-               eng=None, after_heartbeat=None):
+               eng=None, after_heartbeat=None, px_log=None):
     """Run `ticks` on a fresh engine loaded with `st`'s state and on the
     oracle; assert identical state, seen-set and totals after every tick.
     churn: {tick: [(pairs, up), ...]} applied just before the tick.
     eng: an engine whose state `st` already mirrors (nothing is pushed).
-    after_heartbeat(kk, eng, st, msgs): called once both heartbeats ran."""
+    after_heartbeat(kk, eng, st, msgs): called once both heartbeats ran.
+    With peer exchange on (gp.PeerExchange) the connector runs after every
+    tick on both sides and the connections made must agree (appended to
+    px_log when given)."""
     from gsim.engine import Engine
     pushed = eng is None
     if eng is None:
@@ -76,6 +79,12 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
             gpu = ob.NetState(net, params, thresholds=th, gossip=gp)
             gpu.pull_from_engine(eng)
             assert_same(st, gpu)
+            if gp.PeerExchange:
+                t_px = now + Second // 2
+                got, want = eng.px_connect(t_px), st.px_connect(t_px)
+                assert np.array_equal(got, want), f"PX connections differ after tick {kk}: {len(got)} vs {len(want)}"
+                if px_log is not None:
+                    px_log.append(len(want))
             if after_tick:
                 after_tick(kk, st, msgs)
         return msgs, eng.gossip_stats()
