@@ -165,6 +165,7 @@ struct RoundArgs {
     const uint32_t* tmtab;         // k_send_tm blocks per topic (Deliver::d_tmtab)
     uint8_t* peertx;               // [ring][ptx_w] GetForPeer counts (Deliver::d_peertx), zeroed on reuse
     int32_t ptx_w;
+    TraceRef tr;                   // gsim_trace_config
 };
 
 __device__ __forceinline__ int64_t round_time(const RoundArgs& a, int64_t g)
@@ -320,6 +321,8 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, int32_t count)
     }
     atomicOr(&a.nnew_cur[slot >> 5], 1u << (slot & 31));   // the origin forwards in round g+1
     a.slot_last[slot] = (int32_t)a.g;
+    if (a.tr.on(p.origin))                                  // PublishMessage (trace.go:70-91)
+        a.tr.push(round_time(a, a.g), p.id, p.origin, p.origin, (int32_t)p.topic, GSIM_TRACE_PUBLISH_MESSAGE, 0);
 }
 
 // Round g.  W = lanes per row (power of two >= the longest row); group q of
@@ -515,6 +518,9 @@ __global__ __launch_bounds__(256) void k_send(RoundArgs a)
                     const uint8_t tf = u ? tf2 : tf1;
                     const uint32_t hi = (uint32_t)(c >> 32);
                     const bool known = u ? k2 : k1;
+                    if (a.tr.on(i))
+                        a.tr.push(round_time(a, a.g), ((uint64_t)a.g << 32) | m, i, j, t,
+                                  seeable ? kTraceCopy : (uint8_t)GSIM_TRACE_REJECT_MESSAGE, a.minv[m]);
                     // first-seen round of an earlier round, or -1 for unseen /
                     // claimed in this round
                     int64_t seen_round = -1;
@@ -886,6 +892,9 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a)
                             n_gray += tg && !remote && !ok;
                             n_acc += ok;
                             if (!ok) continue;
+                            if (a.tr.on(i))
+                                a.tr.push(round_time(a, a.g), ((uint64_t)a.g << 32) | m, i, j, t,
+                                          seeable ? kTraceCopy : (uint8_t)GSIM_TRACE_REJECT_MESSAGE, vd);
                             const bool sc = scored_t && (ds & GSIM_DS_TRACKED);
                             const uint64_t* s_bm = a.seenbm + (int64_t)m * a.nw + wlo;
                             const int64_t bw = ((int64_t)i >> 6) - wlo;
@@ -1561,6 +1570,9 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
         const int32_t t = (int32_t)a.mtopic[m];
         const ctp_t tp = tpa + t;
         const uint8_t vd = a.minv[m];
+        if (a.tr.on(p))
+            a.tr.push(round_time(a, a.g), ((uint64_t)a.g << 32) | m, p, i, t,
+                      vd != GSIM_VERDICT_SIGNATURE ? kTraceCopy : (uint8_t)GSIM_TRACE_REJECT_MESSAGE, vd);
         const bool inv = vd != GSIM_VERDICT_ACCEPT;
         const bool pen = verdict_penalises(vd);
         const int64_t ir = (int64_t)t * a.E + r;
@@ -1723,6 +1735,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.mmask = d->d_mmask;
     a.tmtab = d->d_tmtab;
     a.peertx = d->d_peertx; a.ptx_w = d->ptx_w;
+    a.tr = h->trace;
     a.nsw = (a.nw + 63) / 64;
     const size_t w = (size_t)nnew_words(d);
     a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
@@ -1946,6 +1959,15 @@ int deliver_check_errors(gsim_handle* h)
         return GSIM_ESTATE;
     }
     return GSIM_OK;
+}
+
+bool deliver_trace_view(gsim_handle* h, TraceView* v)
+{
+    Deliver* d = h->dl;
+    if (!d) return false;
+    v->cell = d->d_cell; v->mtopic = d->d_mtopic; v->minv = d->d_minv; v->mid = d->d_mid;
+    v->ring = d->cfg.ring; v->rounds = d->cfg.rounds;
+    return true;
 }
 
 int deliver_read_seen(gsim_handle* h, void* dst)

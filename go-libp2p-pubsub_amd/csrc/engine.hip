@@ -750,6 +750,7 @@ int gsim_destroy(gsim_handle* h)
     free_graph(h);
     free_extra(h);
     free_deliver(h);
+    trace_release(h);
     dfree(h->d_tp);
     dfree(h->d_flags);
     for (auto& ev : h->ev)
@@ -810,6 +811,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     free_graph(h);
     free_extra(h);
     free_deliver(h);
+    trace_release(h);
     h->n = n;
     h->e = E;
     h->n_ips = n_ips;

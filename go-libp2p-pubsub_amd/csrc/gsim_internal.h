@@ -194,6 +194,29 @@ constexpr uint32_t kCreditFirst = 0x80000000u;     // lo-word flag: winner's rec
 constexpr uint32_t kCreditMesh = 0x40000000u;      // lo-word flag: ... and P3 (negative window)
 constexpr uint32_t kPeerMask = 0x3FFFFFFFu;
 
+// Trace capture (gsim_trace_config, include/gsim.h): the events of the
+// routers [lo, hi) are appended to a device buffer.  A message copy is
+// recorded unclassified (kTraceCopy, msg_id = round << 32 | slot) and resolved
+// into DELIVER / REJECT / DUPLICATE against the seen-set cell when read.
+constexpr uint8_t kTraceCopy = 0xFF;
+struct TraceRef {
+    gsim_trace_event* ev = nullptr;
+    uint32_t* n = nullptr;
+    int64_t cap = 0;
+    uint32_t lo = 0, hi = 0;
+    __device__ __forceinline__ bool on(uint32_t p) const { return ev != nullptr && p >= lo && p < hi; }
+    __device__ __forceinline__ void push(int64_t ts, uint64_t mid, uint32_t peer, uint32_t other, int32_t topic,
+                                         uint8_t type, uint8_t reason) const
+    {
+        const uint32_t k = atomicAdd(n, 1u);
+        if ((int64_t)k >= cap) return;                 // counted: gsim_trace_read reports the overflow
+        gsim_trace_event x;
+        x.timestamp_ns = ts; x.msg_id = mid; x.peer = peer; x.other = other; x.topic = topic;
+        x.type = type; x.reason = reason; x._pad = 0;
+        ev[k] = x;
+    }
+};
+
 }  // namespace gsim
 
 struct gsim_handle {
@@ -284,6 +307,7 @@ struct gsim_handle {
     struct Extra* x = nullptr;
     gsim::Deliver* dl = nullptr;
     gsim::ShardCtx* sh = nullptr;   // graph-sharded network: this handle is one shard (shard.hip)
+    gsim::TraceRef trace;           // gsim_trace_config (trace.hip)
 
     // owned peers / observer rows (all of them unless sharded)
     int64_t olo() const { return sh ? sh->own_lo : 0; }
@@ -356,6 +380,16 @@ uint64_t gsim_get_seed(const gsim_handle* h);              // heartbeat.hip
 int deliver_read_seen(gsim_handle* h, void* dst);
 int deliver_check_errors(gsim_handle* h);             // queue overflow / early slot reuse of the last tick
 int handle_control(gsim_handle* h, int32_t round, int64_t now);   // heartbeat.hip: k_handle_control
+// trace.hip: resolve the recorded message copies (seen-set cells, slot tables)
+struct TraceView {
+    const uint64_t* cell;
+    const uint32_t* mtopic;
+    const uint8_t* minv;
+    const uint64_t* mid;
+    int32_t ring, rounds;
+};
+bool deliver_trace_view(gsim_handle* h, TraceView* v);
+void trace_release(gsim_handle* h);   // trace.hip
 // round stages (deliver.hip; gsim_round runs them in order, a sharded group
 // exchanges between them, shard.hip)
 int deliver_round_prepare(gsim_handle* h, int64_t round);

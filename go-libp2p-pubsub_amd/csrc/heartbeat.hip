@@ -101,6 +101,7 @@ struct HbArgs {
     uint64_t* pxo;             // [N] topics in which the observer sent a PRUNE with PX
     uint8_t* pxm;              // [E] the row's owner tries to connect to col[e]
     uint8_t* nopx;             // [E] a GRAFT of this sender turned PX off for its RPC
+    TraceRef tr;               // gsim_trace_config: tracer.Graft / Prune / AddPeer / RemovePeer
 };
 
 namespace {
@@ -678,6 +679,7 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
             uint8_t ctl = 0;
 
             auto prune = [&]() {
+                if (a.tr.on((uint32_t)obs)) a.tr.push(a.now, 0, (uint32_t)obs, col, t, GSIM_TRACE_PRUNE, 0);
                 stats_prune(a, tracked, scored, thr, mcap, sf);
                 dirty |= tracked && scored;
                 fl &= (uint8_t)~GSIM_TF_MESH;
@@ -688,6 +690,7 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
                 ctl |= GSIM_CTL_PRUNE;
             };
             auto graft = [&]() {
+                if (a.tr.on((uint32_t)obs)) a.tr.push(a.now, 0, (uint32_t)obs, col, t, GSIM_TRACE_GRAFT, 0);
                 stats_graft(a, tracked, scored, sf);
                 dirty |= tracked && scored;
                 fl |= GSIM_TF_MESH;
@@ -1050,6 +1053,7 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                             const int64_t ex = a.now + a.prune_backoff;
                             if (bo < ex) bo = ex;
                         } else {
+                            if (a.tr.on((uint32_t)rcv)) a.tr.push(a.now, 0, (uint32_t)rcv, a.col[e], t, GSIM_TRACE_GRAFT, 0);
                             stats_graft(a, tracked, scored, sf);
                             fl |= GSIM_TF_MESH;
                             delta += 1;
@@ -1058,6 +1062,8 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                         if (a.do_px && off) { a.nopx[e] = 1; nopx_set = true; }
                     }
                     if (c & GSIM_CTL_PRUNE) {
+                        // handlePrune: tracer.Prune whether or not the sender was in the mesh (gossipsub.go:849-851)
+                        if (a.tr.on((uint32_t)rcv)) a.tr.push(a.now, 0, (uint32_t)rcv, a.col[e], t, GSIM_TRACE_PRUNE, 0);
                         if (fl & GSIM_TF_MESH) delta -= 1;
                         stats_prune(a, tracked, scored, thr, mcap, sf);
                         fl &= (uint8_t)~GSIM_TF_MESH;
@@ -1356,6 +1362,8 @@ __global__ __launch_bounds__(256) void k_churn_apply(HbArgs a, ChurnArgs c)
     const uint32_t e = c.edges[q];
     const uint32_t r = a.rev[e];
     if (a.col[r] < a.olo || a.col[r] >= a.ohi) return;   // the other shard handles a ghost observer's side
+    if (a.tr.on(a.col[r]))                                 // tracer.AddPeer / RemovePeer (trace.go:196-248)
+        a.tr.push(a.now, 0, a.col[r], a.col[e], -1, c.up ? GSIM_TRACE_ADD_PEER : GSIM_TRACE_REMOVE_PEER, 0);
     // the observer's (col[r]) joined topics while unjoined records are known zero:
     // a store to them would write the value already there.  Random 1-8 B stores
     // are the churn's bound, so the router planes below are also stored only
@@ -1623,6 +1631,7 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.prune_peers = h->gp.prune_peers;
     a.accept_px = h->th.accept_px_threshold;
     a.pxo = h->x->d_pxo; a.pxm = h->x->d_pxm; a.nopx = h->x->d_nopx;
+    a.tr = h->trace;
     return a;
 }
 

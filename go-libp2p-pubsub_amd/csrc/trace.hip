@@ -1,0 +1,149 @@
+// Trace export (include/gsim.h gsim_trace_config / gsim_trace_read;
+// SURVEY.md §8(f) row 2): the events pubsubTracer hands to a TraceEvent sink
+// (trace.go:70-530, pb/trace.proto) for a range of routers.
+//
+// The kernels append events as they happen (gsim_internal.h TraceRef): the
+// origin's publication (k_publish), every message copy that passes AcceptFrom
+// (k_send_tm / k_send / k_gossip_deliver), the router's mesh additions and
+// removals (the heartbeat's graftPeer / prunePeer, handleGraft,
+// handlePrune) and connection churn (k_churn_apply).  Whether a copy was the
+// first reception is decided only when every copy of its round has claimed
+// (the lowest receiving edge wins), so a copy is recorded unclassified and
+// k_trace_resolve settles it at read time from the receiver's seen-set cell
+// (first-seen round + first sender): the first reception of an accepted
+// message is DELIVER_MESSAGE, of a rejected / ignored / throttled one
+// REJECT_MESSAGE with the verdict as its reason (pushMsg -> validate,
+// pubsub.go:1118-1162, validation.go:282-345), any other copy
+// DUPLICATE_MESSAGE.  Bad-signature copies are rejected before markSeen and
+// recorded as REJECT_MESSAGE directly.
+#include <algorithm>
+#include <tuple>
+#include <vector>
+
+#include "gsim_internal.h"
+
+namespace gsim {
+namespace {
+
+__global__ __launch_bounds__(256) void k_trace_resolve(gsim_trace_event* ev, int64_t n, TraceView v, int64_t CN,
+                                                       uint32_t clo)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+        gsim_trace_event x = ev[k];
+        if (x.type != kTraceCopy) continue;
+        const uint32_t m = (uint32_t)x.msg_id;
+        const int64_t g = (int64_t)(x.msg_id >> 32);
+        const uint64_t c = v.cell[(int64_t)m * CN + (x.peer - clo)];
+        // every claim is committed before a read (gsim_trace_read flushes)
+        const int64_t fr = c == kUnseen64 ? -1 : (int64_t)(c >> 32);
+        const uint32_t from = (uint32_t)c & kPeerMask;
+        const uint8_t vd = v.minv[m];
+        if (fr == g && from == x.other) {
+            x.type = vd == GSIM_VERDICT_ACCEPT ? GSIM_TRACE_DELIVER_MESSAGE : GSIM_TRACE_REJECT_MESSAGE;
+            x.reason = vd == GSIM_VERDICT_ACCEPT ? 0 : vd;
+        } else {
+            x.type = GSIM_TRACE_DUPLICATE_MESSAGE;
+            x.reason = 0;
+        }
+        x.msg_id = v.mid[m];
+        ev[k] = x;
+    }
+}
+
+// bad-signature copies carry round << 32 | slot too: only the id changes
+__global__ __launch_bounds__(256) void k_trace_sig_ids(gsim_trace_event* ev, int64_t n, const uint64_t* mid)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+        gsim_trace_event x = ev[k];
+        if (x.type != GSIM_TRACE_REJECT_MESSAGE || x.reason != GSIM_VERDICT_SIGNATURE) continue;
+        ev[k].msg_id = mid[(uint32_t)x.msg_id];
+    }
+}
+
+void trace_free(gsim_handle* h)
+{
+    if (h->trace.ev) (void)hipFree(h->trace.ev);
+    if (h->trace.n) (void)hipFree(h->trace.n);
+    h->trace = TraceRef{};
+}
+
+}  // namespace
+}  // namespace gsim
+
+using namespace gsim;
+
+extern "C" {
+
+int gsim_trace_config(gsim_handle* h, uint32_t peer_lo, uint32_t peer_hi, int64_t cap)
+{
+    if (!h) return GSIM_EINVAL;
+    if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
+    if (h->sh) { h->err = "tracing runs on a single engine, not a shard"; return GSIM_ESTATE; }
+    if (cap < 0 || peer_lo > peer_hi || (int64_t)peer_hi > h->n) return GSIM_EINVAL;
+    (void)hipStreamSynchronize(h->stream);
+    trace_free(h);
+    if (cap == 0) return GSIM_OK;
+    TraceRef t;
+    hipError_t e = hipMalloc((void**)&t.ev, sizeof(gsim_trace_event) * (size_t)cap);
+    if (e == hipSuccess) e = hipMalloc((void**)&t.n, sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(t.n, 0, sizeof(uint32_t), h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) {
+        if (t.ev) (void)hipFree(t.ev);
+        if (t.n) (void)hipFree(t.n);
+        return hip_check(h, e, "gsim_trace_config");
+    }
+    t.cap = std::min<int64_t>(cap, 0xFFFFFFFFll);
+    t.lo = peer_lo;
+    t.hi = peer_hi;
+    h->trace = t;
+    return GSIM_OK;
+}
+
+int gsim_trace_read(gsim_handle* h, gsim_trace_event* out, int64_t cap, int64_t* n)
+{
+    if (!h || !n) return GSIM_EINVAL;
+    if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
+    *n = 0;
+    if (!h->trace.ev) { h->err = "tracing is off (gsim_trace_config)"; return GSIM_ESTATE; }
+    int rc = deliver_flush(h);                     // the last round's claims decide its first receptions
+    if (rc) return rc;
+    uint32_t cnt = 0;
+    hipError_t e = hipMemcpyAsync(&cnt, h->trace.n, sizeof(cnt), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "trace count");
+    if ((int64_t)cnt > h->trace.cap) {
+        h->err = "the trace buffer overflowed (raise the gsim_trace_config capacity)";
+        return GSIM_ERANGE;
+    }
+    *n = cnt;
+    if (!out) return GSIM_OK;                      // a query: nothing consumed
+    if ((int64_t)cnt > cap) { h->err = "output buffer too small for the traced events"; return GSIM_ERANGE; }
+    if (cnt) {
+        TraceView v{};
+        const bool have = deliver_trace_view(h, &v);
+        const int grid = (int)std::min<int64_t>(((int64_t)cnt + 255) / 256, 4096);
+        if (have) {
+            hipLaunchKernelGGL(k_trace_resolve, dim3(grid), dim3(256), 0, h->stream, h->trace.ev, (int64_t)cnt, v,
+                               h->n, 0u);
+            hipLaunchKernelGGL(k_trace_sig_ids, dim3(grid), dim3(256), 0, h->stream, h->trace.ev, (int64_t)cnt, v.mid);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(out, h->trace.ev, sizeof(gsim_trace_event) * cnt, hipMemcpyDeviceToHost, h->stream);
+    }
+    if (e == hipSuccess) e = hipMemsetAsync(h->trace.n, 0, sizeof(uint32_t), h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "gsim_trace_read");
+    std::sort(out, out + cnt, [](const gsim_trace_event& a, const gsim_trace_event& b) {
+        return std::tie(a.timestamp_ns, a.peer, a.type, a.other, a.topic, a.msg_id) <
+               std::tie(b.timestamp_ns, b.peer, b.type, b.other, b.topic, b.msg_id);
+    });
+    return GSIM_OK;
+}
+
+}  // extern "C"
+
+void trace_release(gsim_handle* h) { gsim::trace_free(h); }

@@ -86,6 +86,11 @@ class CGossipSubParams(Structure):
     ]
 
 
+# gsim_trace_event (include/gsim.h): TraceEvent.Type values
+TRACE_PUBLISH_MESSAGE, TRACE_REJECT_MESSAGE, TRACE_DUPLICATE_MESSAGE, TRACE_DELIVER_MESSAGE = 0, 1, 2, 3
+TRACE_ADD_PEER, TRACE_REMOVE_PEER, TRACE_GRAFT, TRACE_PRUNE = 4, 5, 11, 12
+
+
 # (name, restype, argtypes) for every symbol include/gsim.h declares.
 class CMsgConfig(Structure):
     _fields_ = [("ring", c_int32), ("rounds", c_int32), ("t0_ns", c_int64), ("heartbeat_ns", c_int64),
@@ -220,6 +225,8 @@ SIGNATURES = [
     ("gsim_gossip_stats", c_int32, [c_void_p, c_void_p]),
     ("gsim_set_connections", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int64]),
     ("gsim_px_connect", c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_void_p]),
+    ("gsim_trace_config", c_int32, [c_void_p, c_uint32, c_uint32, c_int64]),
+    ("gsim_trace_read", c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     ("gsim_set_direct_peers", c_int32, [c_void_p, c_void_p]),
     ("gsim_profile", c_int32, [c_void_p, c_int32]),
     ("gsim_profile_read", c_int32, [c_void_p, c_void_p, c_void_p, c_int32]),
@@ -267,6 +274,8 @@ SIGNATURES = [
     # gsim_wire.h
     ("gsim_wire_size", c_uint64, [POINTER(CWireRpc)]),
     ("gsim_wire_encode", c_int32, [POINTER(CWireRpc), c_void_p, c_uint64, POINTER(c_uint64)]),
+    ("gsim_trace_encode", c_int32, [c_void_p, c_int64, POINTER(CWireNames), ctypes.c_char_p, c_void_p, c_uint64,
+                                    POINTER(c_uint64)]),
     ("gsim_wire_fragment", c_int32, [POINTER(CWireRpc), c_int64, c_void_p, c_uint64, POINTER(c_uint64), c_void_p,
                                      c_int32, POINTER(c_int32)]),
     ("gsim_wire_heartbeat", c_int32, [c_void_p, c_int64, c_uint32, c_uint32, POINTER(CWireNames), c_void_p, c_uint64,

@@ -307,6 +307,24 @@ class Engine:
         self._check(self.lib.gsim_px_connect(self.h, int(now), _ptr(out), int(cap), ctypes.byref(n)))
         return out[:min(n.value, cap)].copy()
 
+    # gsim_trace_event
+    TRACE_DTYPE = np.dtype([("timestamp", np.int64), ("msg_id", np.uint64), ("peer", np.uint32),
+                            ("other", np.uint32), ("topic", np.int32), ("type", np.uint8), ("reason", np.uint8),
+                            ("_pad", np.uint16)])
+
+    def trace_config(self, peer_lo: int, peer_hi: int, cap: int = 1 << 20):
+        """Trace the routers [peer_lo, peer_hi) (gsim_trace_config; cap 0 stops)."""
+        self._check(self.lib.gsim_trace_config(self.h, int(peer_lo), int(peer_hi), int(cap)))
+
+    def trace_read(self) -> np.ndarray:
+        """The traced events since the last read, sorted (gsim_trace_read):
+        the pubsubTracer events of trace.go:70-530 as TRACE_DTYPE records."""
+        n = ctypes.c_int64(0)
+        self._check(self.lib.gsim_trace_read(self.h, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, dtype=self.TRACE_DTYPE)
+        self._check(self.lib.gsim_trace_read(self.h, _ptr(out) if n.value else None, n.value, ctypes.byref(n)))
+        return out[:n.value]
+
     def set_direct_peers(self, flags):
         """WithDirectPeers as per-edge flags (edge order; None clears)
         (gsim_set_direct_peers; gossipsub.go:352-374)."""

@@ -242,3 +242,35 @@ def heartbeat_rpcs(engine, tick: int, p0: int, p1: int, topic_names, peer_ids: O
     raw = out.cpu().numpy().tobytes()
     rv = np.frombuffer(refs.cpu().numpy().tobytes()[:n.value * 24], dtype=_abi.WIRE_REF_DTYPE)
     return [(int(r["from"]), int(r["to"]), raw[int(r["offset"]):int(r["offset"]) + int(r["len"])]) for r in rv]
+
+
+def trace_batch(records: np.ndarray, topic_names, peer_ids: Optional[np.ndarray] = None,
+                proto: bytes = b"/meshsub/1.1.0") -> bytes:
+    """TraceEventBatch bytes (pb/trace.proto) of engine trace records
+    (Engine.trace_read; gsim_trace_encode)."""
+    lib = _abi.load()
+    recs = np.ascontiguousarray(records)
+    names = [_b(x) for x in topic_names]
+    tn = (_abi.CBytes * max(1, len(names)))()
+    keep = []
+    for k, x in enumerate(names):
+        buf = ctypes.create_string_buffer(x, max(1, len(x)))
+        keep.append(buf)
+        tn[k] = _abi.CBytes(ctypes.addressof(buf), len(x))
+    nm = _abi.CWireNames()
+    nm.topic_names = ctypes.addressof(tn)
+    if peer_ids is not None:
+        pid = np.ascontiguousarray(peer_ids, dtype=np.uint8)
+        keep.append(pid)
+        nm.peer_ids = pid.ctypes.data
+        nm.peer_id_len = pid.shape[1]
+    n = ctypes.c_uint64()
+    ptr = recs.ctypes.data_as(ctypes.c_void_p) if len(recs) else None
+    rc = lib.gsim_trace_encode(ptr, len(recs), ctypes.byref(nm), proto, None, 0, ctypes.byref(n))
+    if rc not in (0, _abi.GSIM_ERANGE):
+        raise WireError(rc, "gsim_trace_encode")
+    out = ctypes.create_string_buffer(max(1, n.value))
+    rc = lib.gsim_trace_encode(ptr, len(recs), ctypes.byref(nm), proto, out, n.value, ctypes.byref(n))
+    if rc != 0:
+        raise WireError(rc, "gsim_trace_encode")
+    return out.raw[:n.value]

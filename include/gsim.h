@@ -350,6 +350,52 @@ int gsim_gossip_stats(gsim_handle* h, int64_t* out4);
  * invalidMessageDeliveries, router mesh links, tracked edges}. */
 int gsim_census(gsim_handle* h, int64_t* out8);
 
+/* ---- trace export (pb/trace.proto, trace.go) ------ */
+/* The events the routers [peer_lo, peer_hi) hand their tracer
+ * (pubsubTracer, trace.go:70-530), one record each, in the order of
+ * pb/trace.proto's TraceEvent.Type:
+ *   PUBLISH_MESSAGE   the origin publishes (trace.go:70-91)
+ *   REJECT_MESSAGE    first reception of a message that failed validation
+ *                     (reason = the verdict), or every copy with a bad
+ *                     signature (105-134)
+ *   DUPLICATE_MESSAGE a copy of a message already seen (136-164)
+ *   DELIVER_MESSAGE   first reception of an accepted message (166-194)
+ *   ADD_PEER / REMOVE_PEER   connections made or lost (196-248)
+ *   GRAFT / PRUNE     the router adds / drops a mesh link: heartbeat,
+ *                     handleGraft, handlePrune (468-520)
+ * RPC-level events (RECV_RPC, SEND_RPC, DROP_RPC) and JOIN/LEAVE are not
+ * produced: the engine models no RPC framing and no subscription changes.
+ * Copies dropped by AcceptFrom produce no event, as in pushMsg. */
+#define GSIM_TRACE_PUBLISH_MESSAGE   0
+#define GSIM_TRACE_REJECT_MESSAGE    1
+#define GSIM_TRACE_DUPLICATE_MESSAGE 2
+#define GSIM_TRACE_DELIVER_MESSAGE   3
+#define GSIM_TRACE_ADD_PEER          4
+#define GSIM_TRACE_REMOVE_PEER       5
+#define GSIM_TRACE_GRAFT             11
+#define GSIM_TRACE_PRUNE             12
+
+typedef struct gsim_trace_event {
+    int64_t  timestamp_ns;    /* TraceEvent.timestamp */
+    uint64_t msg_id;          /* gsim_msg.id of message events */
+    uint32_t peer;            /* TraceEvent.peerID: the router */
+    uint32_t other;           /* receivedFrom (message events); the peer (ADD/REMOVE_PEER, GRAFT, PRUNE) */
+    int32_t  topic;           /* message events, GRAFT, PRUNE; -1 otherwise */
+    uint8_t  type;            /* GSIM_TRACE_* */
+    uint8_t  reason;          /* REJECT_MESSAGE: GSIM_VERDICT_* */
+    uint16_t _pad;
+} gsim_trace_event;
+
+/* Start tracing the routers [peer_lo, peer_hi) into a device buffer of cap
+ * events (0: stop and free it). */
+int gsim_trace_config(gsim_handle* h, uint32_t peer_lo, uint32_t peer_hi, int64_t cap);
+
+/* The events traced since the last call, sorted by (timestamp, peer, type,
+ * other, topic, msg_id); *n is their number (GSIM_ERANGE, nothing lost from
+ * the buffer, when it exceeds cap; GSIM_ERANGE when the device buffer
+ * overflowed). */
+int gsim_trace_read(gsim_handle* h, gsim_trace_event* out, int64_t cap, int64_t* n);
+
 /* Copy the score snapshot (E doubles, edge order) to host. */
 int gsim_read_scores(gsim_handle* h, double* out);
 

@@ -156,6 +156,18 @@ int gsim_wire_heartbeat(gsim_handle* h, int64_t tick, uint32_t p0, uint32_t p1, 
                         uint8_t* d_out, uint64_t out_cap, gsim_wire_ref* d_refs, int64_t ref_cap,
                         int64_t* n_rpcs, uint64_t* bytes);
 
+/* TraceEventBatch (pb/trace.proto:148-150) of n trace records from
+ * gsim_trace_read (include/gsim.h): one TraceEvent {type, peerID, timestamp,
+ * and the event's message} per record, fields in number order as gogo's
+ * Marshal writes them (trace.pb.go).  Peer ids come from names->peer_ids (4
+ * big-endian bytes of the peer index when peer_id_len is 0), topics from
+ * names->topic_names; a messageID is the gsim id as 8 big-endian bytes;
+ * AddPeer.proto is `proto` (e.g. "/meshsub/1.1.0"); RejectMessage.reason is
+ * the reference's string for the verdict (tracer.go:31-38).  *len: the
+ * bytes written (GSIM_ERANGE with *len = the size needed when cap is short). */
+int gsim_trace_encode(const gsim_trace_event* ev, int64_t n, const gsim_wire_names* names, const char* proto,
+                      uint8_t* out, uint64_t cap, uint64_t* len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -177,7 +177,8 @@ enum {
  * promise lists. */
 enum {
     ORC_EV_PUT = 1,        /* a: peer, mid, topic            mcache.Put            */
-    ORC_EV_SEEN = 2,       /* a: peer, mid, x: 1 new / 0 seen  seenMessage/markSeen */
+    ORC_EV_SEEN = 2,       /* a: peer, b: sender (0xFFFFFFFF: its own publication), mid,
+                              x: 1 new / 0 seen  seenMessage/markSeen */
     ORC_EV_SERVE = 3,      /* a: advertiser, b: requester, mid, x: GetForPeer count */
     ORC_EV_PROMISE = 4,    /* a: requester, b: advertiser, mid, x: now (AddPromise)  */
     ORC_EV_FULFILL = 5,    /* a: peer, mid                   fulfillPromise        */
@@ -185,6 +186,13 @@ enum {
     ORC_EV_PENALTIES = 7,  /* x: now: applyIwantPenalties (every peer)              */
     ORC_EV_HEARTBEAT = 8,  /* x: tick: GetGossipIDs then Shift (every peer)         */
     ORC_EV_GOSSIP_ID = 9,  /* a: peer, mid, topic: one id of GetGossipIDs(topic)    */
+    /* the tracer's view (trace export, include/gsim.h gsim_trace_event) */
+    ORC_EV_REJECT_SIG = 10,  /* a: peer, b: sender, mid, topic: a bad-signature copy  */
+    ORC_EV_PUBLISH = 11,     /* a: origin, mid, topic                                */
+    ORC_EV_GRAFT = 12,       /* a: router, b: peer, topic, x: now  tracer.Graft      */
+    ORC_EV_PRUNE = 13,       /* a: router, b: peer, topic, x: now  tracer.Prune      */
+    ORC_EV_ADD_PEER = 14,    /* a: router, b: peer, x: now                           */
+    ORC_EV_REMOVE_PEER = 15, /* a: router, b: peer, x: now                           */
 };
 typedef struct orc_event { int32_t kind, topic; uint32_t a, b; int64_t g; uint64_t mid; int64_t x; } orc_event;
 void    orc_msgs_log(orc_msgs* m, int32_t on);

@@ -28,7 +28,20 @@ priv* orc_msgs_priv(orc_msgs* m)
 
 static priv* P(orc_msgs* m) { return orc_msgs_priv(m); }
 
-void orc_msgs_log(orc_msgs* m, int32_t on) { P(m)->log_on = on; }
+static orc_msgs* g_net_log;
+
+void orc_msgs_log(orc_msgs* m, int32_t on)
+{
+    P(m)->log_on = on;
+    g_net_log = on ? m : (g_net_log == m ? NULL : g_net_log);
+}
+
+void orc_log_net(int32_t kind, uint32_t a, uint32_t b, int32_t topic, int64_t now)
+{
+    if (!g_net_log) return;
+#pragma omp critical(orc_log)
+    orc_log(g_net_log, kind, a, b, 0, topic, 0, now);
+}
 
 void orc_log(orc_msgs* m, int32_t kind, uint32_t a, uint32_t b, uint32_t slot, int32_t topic, int64_t g, int64_t x)
 {
@@ -55,6 +68,7 @@ int64_t orc_msgs_events(orc_msgs* m, orc_event* out, int64_t cap)
 
 void orc_msgs_free_priv(orc_msgs* m)
 {
+    if (g_net_log == m) g_net_log = NULL;
     if (!m->priv) return;
     priv* p = (priv*)m->priv;
     free(p->ev);
@@ -133,8 +147,9 @@ void orc_publish(orc_net* s, orc_msgs* m, uint64_t id, uint32_t topic, uint32_t 
      * its mcache (gossipsub.go:976); its own DeliverMessage is not scored
      * (trace.go skips ReceivedFrom == self) */
     row[origin] = (uint32_t)g;
-    orc_log(m, ORC_EV_SEEN, origin, 0, slot, (int32_t)topic, g, 1);
+    orc_log(m, ORC_EV_SEEN, origin, 0xFFFFFFFFu, slot, (int32_t)topic, g, 1);
     orc_log(m, ORC_EV_PUT, origin, 0, slot, (int32_t)topic, g, 0);
+    orc_log(m, ORC_EV_PUBLISH, origin, origin, slot, (int32_t)topic, g, 0);
     /* Publish: an origin that has not joined the topic sends to its fanout
      * (gossipsub.go:1011-1028); flood publishing sends to every topic peer */
     if (!s->gp->flood_publish && !((s->sub[origin] >> topic) & 1u) && s->lastpub && s->fan_topics)
@@ -201,9 +216,10 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
              * fulfilled (gossip_tracer.go:148-162) */
             m->stats[2]++;
             orc_mark_invalid(s, er, t);
+            orc_log(m, ORC_EV_REJECT_SIG, i, s->col[er], slot, t, g, 0);
             continue;
         }
-        orc_log(m, ORC_EV_SEEN, i, 0, slot, t, g, *cell == UNSEEN);
+        orc_log(m, ORC_EV_SEEN, i, s->col[er], slot, t, g, *cell == UNSEEN);
         if (*cell == UNSEEN) {
             *cell = (uint32_t)g;               /* markSeen */
             m->stats[1]++;

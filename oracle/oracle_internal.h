@@ -65,6 +65,9 @@ typedef struct priv {
 
 /* one event, when logging is on */
 void orc_log(orc_msgs* m, int32_t kind, uint32_t a, uint32_t b, uint32_t slot, int32_t topic, int64_t g, int64_t x);
+/* router-level events (GRAFT/PRUNE/ADD/REMOVE) go to the message log that
+ * last turned logging on (orc_msgs_log); safe inside the OpenMP phases */
+void orc_log_net(int32_t kind, uint32_t a, uint32_t b, int32_t topic, int64_t now);
 
 priv* orc_msgs_priv(orc_msgs* m);
 int64_t orc_round_time(const orc_msgs* m, int64_t g);

@@ -77,6 +77,7 @@ static void send_ctl(hb* h, uint32_t e, uint8_t bits)
 /* heartbeat prunePeer closure, gossipsub.go:1387-1393 */
 static void prune_peer(hb* h, uint32_t e)
 {
+    orc_log_net(ORC_EV_PRUNE, h->i, h->s->col[e], h->t, h->now);
     orc_prune(h->s, e, h->t);
     h->s->tflags[ti(h, e)] &= (uint8_t)~TF_MESH;
     do_add_backoff(h, e, h->s->gp->prune_backoff_ns);
@@ -86,6 +87,7 @@ static void prune_peer(hb* h, uint32_t e)
 /* heartbeat graftPeer closure, gossipsub.go:1395-1401 */
 static void graft_peer(hb* h, uint32_t e)
 {
+    orc_log_net(ORC_EV_GRAFT, h->i, h->s->col[e], h->t, h->now);
     orc_graft(h->s, e, h->t, h->now);
     h->s->tflags[ti(h, e)] |= TF_MESH;
     send_ctl(h, e, GSIM_CTL_GRAFT);
@@ -440,6 +442,7 @@ static int handle_graft(hb* h, uint32_t e)
         do_add_backoff(h, e, gp->prune_backoff_ns);
         return 0;
     }
+    orc_log_net(ORC_EV_GRAFT, h->i, s->col[e], h->t, h->now);
     orc_graft(s, e, h->t, h->now);                             /* tracer.Graft + mesh add */
     s->tflags[ti(h, e)] |= TF_MESH;
     return 0;
@@ -450,6 +453,7 @@ static void handle_prune(hb* h, uint32_t e)
 {
     orc_net* s = h->s;
     if (!((s->sub[h->i] >> h->t) & 1u)) return;
+    orc_log_net(ORC_EV_PRUNE, h->i, s->col[e], h->t, h->now);  /* tracer.Prune (gossipsub.go:849) */
     orc_prune(s, e, h->t);
     s->tflags[ti(h, e)] &= (uint8_t)~TF_MESH;
     /* makePrune sends Backoff = PruneBackoff / time.Second (whole seconds);
@@ -538,6 +542,7 @@ int32_t orc_churn(orc_net* s, const uint32_t* pairs, int32_t count, int32_t up, 
         for (int d = 0; d < 2; ++d) {
             const uint32_t o = pairs[2 * q + d], p = pairs[2 * q + 1 - d];
             const int64_t e = find_edge(s, o, p);
+            orc_log_net(up ? ORC_EV_ADD_PEER : ORC_EV_REMOVE_PEER, o, p, -1, now);
             if (up) {
                 orc_add_peer(s, e);
                 continue;

@@ -66,6 +66,63 @@ def pb():
     return _CLASSES
 
 
+_TRACE = None
+
+
+def trace_pb():
+    """{name: class} for TraceEvent and TraceEventBatch, from a descriptor
+    restating pb/trace.proto:5-150 for the events the engine produces
+    (PublishMessage, RejectMessage, DuplicateMessage, DeliverMessage,
+    AddPeer, RemovePeer, Graft, Prune; field names, numbers, types as
+    there).  Serialized by the protobuf runtime."""
+    global _TRACE
+    if _TRACE is not None:
+        return _TRACE
+    F = descriptor_pb2.FieldDescriptorProto
+    fdp = descriptor_pb2.FileDescriptorProto(name="gsim_test_trace.proto", package="gsimtest.tr", syntax="proto2")
+    OPT, REP = F.LABEL_OPTIONAL, F.LABEL_REPEATED
+    B, S, I64, E, M = F.TYPE_BYTES, F.TYPE_STRING, F.TYPE_INT64, F.TYPE_ENUM, F.TYPE_MESSAGE
+    ev = fdp.message_type.add(name="TraceEvent")
+    ty = ev.enum_type.add(name="Type")
+    for k, name in enumerate(["PUBLISH_MESSAGE", "REJECT_MESSAGE", "DUPLICATE_MESSAGE", "DELIVER_MESSAGE", "ADD_PEER",
+                              "REMOVE_PEER", "RECV_RPC", "SEND_RPC", "DROP_RPC", "JOIN", "LEAVE", "GRAFT", "PRUNE"]):
+        ty.value.add(name=name, number=k)
+    T = ".gsimtest.tr.TraceEvent."
+    for (fname, num, label, typ, tname) in [("type", 1, OPT, E, T + "Type"), ("peerID", 2, OPT, B, None),
+                                            ("timestamp", 3, OPT, I64, None),
+                                            ("publishMessage", 4, OPT, M, T + "PublishMessage"),
+                                            ("rejectMessage", 5, OPT, M, T + "RejectMessage"),
+                                            ("duplicateMessage", 6, OPT, M, T + "DuplicateMessage"),
+                                            ("deliverMessage", 7, OPT, M, T + "DeliverMessage"),
+                                            ("addPeer", 8, OPT, M, T + "AddPeer"),
+                                            ("removePeer", 9, OPT, M, T + "RemovePeer"),
+                                            ("graft", 15, OPT, M, T + "Graft"), ("prune", 16, OPT, M, T + "Prune")]:
+        f = ev.field.add(name=fname, number=num, label=label, type=typ)
+        if tname:
+            f.type_name = tname
+
+    def sub(name, fields):
+        m = ev.nested_type.add(name=name)
+        for (fname, num, typ) in fields:
+            m.field.add(name=fname, number=num, label=OPT, type=typ)
+
+    sub("PublishMessage", [("messageID", 1, B), ("topic", 2, S)])
+    sub("RejectMessage", [("messageID", 1, B), ("receivedFrom", 2, B), ("reason", 3, S), ("topic", 4, S)])
+    sub("DuplicateMessage", [("messageID", 1, B), ("receivedFrom", 2, B), ("topic", 3, S)])
+    sub("DeliverMessage", [("messageID", 1, B), ("topic", 2, S), ("receivedFrom", 3, B)])
+    sub("AddPeer", [("peerID", 1, B), ("proto", 2, S)])
+    sub("RemovePeer", [("peerID", 1, B)])
+    sub("Graft", [("peerID", 1, B), ("topic", 2, S)])
+    sub("Prune", [("peerID", 1, B), ("topic", 2, S)])
+    b = fdp.message_type.add(name="TraceEventBatch")
+    b.field.add(name="batch", number=1, label=REP, type=M, type_name=".gsimtest.tr.TraceEvent")
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(fdp)
+    _TRACE = {n: message_factory.GetMessageClass(pool.FindMessageTypeByName("gsimtest.tr." + n))
+              for n in ["TraceEvent", "TraceEventBatch"]}
+    return _TRACE
+
+
 class FragmentError(ValueError):
     pass
 

@@ -1,0 +1,180 @@
+"""Trace export: the pubsubTracer events
+(trace.go:70-530) of a range of routers, and their TraceEventBatch encoding
+(pb/trace.proto).
+
+CPU part:
+  * gsim_trace_encode is byte-identical to the protobuf runtime's serializer
+    on a restatement of pb/trace.proto (oracle/wire_oracle.py trace_pb) for
+    every event type the engine produces;
+  * the oracle's event log, read as a trace, keeps the tracer's rules: one
+    DELIVER or REJECT per (router, message) at its first reception, later
+    copies DUPLICATE, a PUBLISH at the origin.
+GPU part: the engine's trace of routers [lo, hi) equals the oracle's log
+event for event (time, router, type, peer, topic, message, reason) after
+every tick of a network with gossip, every validation verdict, mesh churn
+and connection churn."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_binding as ob
+from conftest import REPO
+from gsim import _abi, wire
+from gsim.engine import Engine
+from gsim.params import GossipSubParams, PeerScoreThresholds, Second
+
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import wire_oracle as wo  # noqa: E402  (test infrastructure)
+
+from test_delivery import R, T0  # noqa: E402
+from test_heartbeat import SEED, tick_time  # noqa: E402
+
+REASONS = {1: "validation failed", 2: "validation ignored", 3: "validation throttled", 4: "invalid signature"}
+
+
+def _pid(p, peer_ids):
+    return bytes(peer_ids[p]) if peer_ids is not None else int(p).to_bytes(4, "big")
+
+
+def _expected_batch(recs, names, peer_ids, proto=b"/meshsub/1.1.0"):
+    C = wo.trace_pb()
+    batch = C["TraceEventBatch"]()
+    for r in recs:
+        e = batch.batch.add()
+        typ = int(r["type"])
+        e.type = typ
+        e.peerID = _pid(int(r["peer"]), peer_ids)
+        e.timestamp = int(r["timestamp"])
+        mid = int(r["msg_id"]).to_bytes(8, "big")
+        other = _pid(int(r["other"]), peer_ids)
+        topic = names[int(r["topic"])].decode() if int(r["topic"]) >= 0 else None
+        if typ == _abi.TRACE_PUBLISH_MESSAGE:
+            e.publishMessage.messageID, e.publishMessage.topic = mid, topic
+        elif typ == _abi.TRACE_REJECT_MESSAGE:
+            x = e.rejectMessage
+            x.messageID, x.receivedFrom, x.reason, x.topic = mid, other, REASONS[int(r["reason"])], topic
+        elif typ == _abi.TRACE_DUPLICATE_MESSAGE:
+            x = e.duplicateMessage
+            x.messageID, x.receivedFrom, x.topic = mid, other, topic
+        elif typ == _abi.TRACE_DELIVER_MESSAGE:
+            x = e.deliverMessage
+            x.messageID, x.topic, x.receivedFrom = mid, topic, other
+        elif typ == _abi.TRACE_ADD_PEER:
+            e.addPeer.peerID, e.addPeer.proto = other, proto.decode()
+        elif typ == _abi.TRACE_REMOVE_PEER:
+            e.removePeer.peerID = other
+        elif typ == _abi.TRACE_GRAFT:
+            e.graft.peerID, e.graft.topic = other, topic
+        elif typ == _abi.TRACE_PRUNE:
+            e.prune.peerID, e.prune.topic = other, topic
+    return batch.SerializeToString()
+
+
+def _random_records(rng, n, T, N):
+    types = [0, 1, 2, 3, 4, 5, 11, 12]
+    recs = np.zeros(n, dtype=Engine.TRACE_DTYPE)
+    for k in range(n):
+        typ = types[rng.integers(0, len(types))]
+        recs[k]["type"] = typ
+        recs[k]["timestamp"] = int(rng.integers(-5, 1 << 62))
+        recs[k]["peer"] = rng.integers(0, N)
+        recs[k]["other"] = rng.integers(0, N)
+        recs[k]["msg_id"] = int(rng.integers(0, 1 << 63))
+        recs[k]["topic"] = -1 if typ in (4, 5) else rng.integers(0, T)
+        recs[k]["reason"] = rng.integers(1, 5) if typ == 1 else 0
+    return recs
+
+
+@pytest.mark.parametrize("with_ids", [False, True])
+def test_trace_encode_matches_protobuf_runtime(with_ids):
+    rng = np.random.default_rng(17 + with_ids)
+    T, N = 5, 300
+    names = [f"/eth2/topic/{t:03d}".encode() for t in range(T)]
+    peer_ids = rng.integers(0, 256, size=(N, 38), dtype=np.uint8) if with_ids else None
+    for n in (0, 1, 7, 200):
+        recs = _random_records(rng, n, T, N)
+        got = wire.trace_batch(recs, names, peer_ids=peer_ids)
+        assert got == _expected_batch(recs, names, peer_ids)
+
+
+def test_oracle_log_follows_tracer_rules():
+    """Read as a trace: a router's first reception of a message is one
+    DELIVER (accepted) or REJECT (with the verdict as reason), every later
+    copy a DUPLICATE; bad-signature copies are REJECT each; the origin
+    publishes."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim.engine import random_regular
+    from tickrun import oracle_trace, subscribed_schedule
+    rng = np.random.default_rng(23)
+    n, k, T = 500, 16, 2
+    params = beacon_params(T)
+    th = PeerScoreThresholds(GossipThreshold=-2000, PublishThreshold=-4000, GraylistThreshold=-8000)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2)
+    net = random_regular(n, k, seed=31, n_topics=T)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 8 / k)
+    ticks = list(range(1, 5))
+    sched = subscribed_schedule(rng, ticks, net, T, 4.0, 0.0, verdicts=(0.6, 0.1, 0.1, 0.1, 0.1))
+    msgs = ob.Msgs(n, T, 256, R, T0, Second)
+    msgs.log()
+    lib = ob.load()
+    seen_first = {}
+    counts = np.zeros(13, dtype=np.int64)
+    for kk in ticks:
+        now = tick_time(kk)
+        v = st.view()
+        lib.orc_refresh_scores(v, now)
+        msgs.penalties(st, now)
+        lib.orc_ip_colocation(v)
+        lib.orc_compute_scores(v)
+        msgs.heartbeat(st, kk, now, SEED)
+        for g in range(kk * R, kk * R + R):
+            for (mid, t, o, inv) in sched.get(g, []):
+                msgs.publish(st, mid, t, o, inv, g)
+            msgs.round(st, g)
+        tr = oracle_trace(msgs.events(), msgs, 0, n)
+        counts += np.bincount(tr["type"], minlength=13)
+        dups = []
+        for r in tr:
+            typ, key = int(r["type"]), (int(r["peer"]), int(r["msg_id"]))
+            if typ in (_abi.TRACE_DELIVER_MESSAGE, _abi.TRACE_PUBLISH_MESSAGE) or \
+                    (typ == _abi.TRACE_REJECT_MESSAGE and int(r["reason"]) != 4):
+                assert key not in seen_first, "one first reception per router and message"
+                seen_first[key] = int(r["timestamp"])
+            elif typ == _abi.TRACE_DUPLICATE_MESSAGE:
+                dups.append((key, int(r["timestamp"])))
+        for key, ts in dups:                            # same-round copies share the timestamp
+            assert key in seen_first and seen_first[key] <= ts, "a duplicate follows the first reception"
+    for typ in (_abi.TRACE_PUBLISH_MESSAGE, _abi.TRACE_REJECT_MESSAGE, _abi.TRACE_DUPLICATE_MESSAGE,
+                _abi.TRACE_DELIVER_MESSAGE, _abi.TRACE_GRAFT, _abi.TRACE_PRUNE):
+        assert counts[typ] > 0, f"event type {typ} occurs"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lo,hi", [(0, 1000), (137, 400)])
+def test_trace_bit_exact(require_gpu, lo, hi):
+    from fixtures import beacon_params, synthetic_state
+    from gsim.engine import random_regular
+    from tickrun import run_parity, subscribed_schedule
+    rng = np.random.default_rng(99 + lo)
+    n, k, T = 1000, 16, 3
+    params = beacon_params(T)
+    th = PeerScoreThresholds(GossipThreshold=-200, PublishThreshold=-400, GraylistThreshold=-800)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2)
+    net = random_regular(n, k, seed=77, n_topics=T)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 0.6)          # meshes over Dhi: heartbeat prunes
+    ticks = list(range(1, 6))
+    sched = subscribed_schedule(rng, ticks, net, T, 4.0, 0.0, verdicts=(0.7, 0.08, 0.08, 0.07, 0.07))
+    src = net.owner()
+    und = np.stack([src, net.col], axis=1)
+    und = und[und[:, 0] < und[:, 1]]
+    down = und[rng.choice(len(und), size=len(und) // 30, replace=False)]
+    churn = {2: [(down, False)], 4: [(down, True)]}
+    log = []
+    run_parity(net, params, th, gp, st, ticks, sched, ring=512, churn=churn, trace=(lo, hi), trace_log=log)
+    total = np.sum(log, axis=0)
+    for typ in (0, 1, 2, 3, 4, 5, 11, 12):
+        assert total[typ] > 0, f"event type {typ} traced"

@@ -27,8 +27,41 @@ def restrict_to_subscriptions(st, net):
         st.tflags[t, off] = 0
 
 
+def oracle_trace(ev, msgs, lo, hi):
+    """The oracle's event log as the engine's trace records (gsim_trace_event)
+    of the routers [lo, hi), sorted as gsim_trace_read sorts them."""
+    from gsim.engine import Engine
+    out = []
+    ring = msgs.seen.shape[0]
+    for e in ev:
+        kind, a, b = int(e["kind"]), int(e["a"]), int(e["b"])
+        if not (lo <= a < hi):
+            continue
+        mid, topic = int(e["mid"]), int(e["topic"])
+        if kind == ob.EV_PUBLISH:
+            out.append((msgs.round_time(int(e["g"])), mid, a, a, topic, _abi.TRACE_PUBLISH_MESSAGE, 0))
+        elif kind == ob.EV_SEEN and b != 0xFFFFFFFF:
+            ts = msgs.round_time(int(e["g"]))
+            if int(e["x"]):
+                vd = int(msgs.invalid[mid % ring])
+                typ = _abi.TRACE_DELIVER_MESSAGE if vd == 0 else _abi.TRACE_REJECT_MESSAGE
+                out.append((ts, mid, a, b, topic, typ, vd))
+            else:
+                out.append((ts, mid, a, b, topic, _abi.TRACE_DUPLICATE_MESSAGE, 0))
+        elif kind == ob.EV_REJECT_SIG:
+            out.append((msgs.round_time(int(e["g"])), mid, a, b, topic, _abi.TRACE_REJECT_MESSAGE, 4))
+        elif kind in (ob.EV_GRAFT, ob.EV_PRUNE, ob.EV_ADD_PEER, ob.EV_REMOVE_PEER):
+            typ = {ob.EV_GRAFT: _abi.TRACE_GRAFT, ob.EV_PRUNE: _abi.TRACE_PRUNE, ob.EV_ADD_PEER: _abi.TRACE_ADD_PEER,
+                   ob.EV_REMOVE_PEER: _abi.TRACE_REMOVE_PEER}[kind]
+            out.append((int(e["x"]), 0, a, b, topic, typ, 0))
+    arr = np.zeros(len(out), dtype=Engine.TRACE_DTYPE)
+    for q, (ts, mid, a, b, topic, typ, rs) in enumerate(out):
+        arr[q] = (ts, mid, a, b, topic, typ, rs, 0)
+    return arr[np.lexsort((arr["msg_id"], arr["topic"], arr["other"], arr["type"], arr["peer"], arr["timestamp"]))]
+
+
 def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, churn=None, after_tick=None,
-               eng=None, after_heartbeat=None, px_log=None):
+               eng=None, after_heartbeat=None, px_log=None, trace=None, trace_log=None):
     """Run `ticks` on a fresh engine loaded with `st`'s state and on the
     oracle; assert identical state, seen-set and totals after every tick.
     churn: {tick: [(pairs, up), ...]} applied just before the tick.
@@ -36,7 +69,9 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
     after_heartbeat(kk, eng, st, msgs): called once both heartbeats ran.
     With peer exchange on (gp.PeerExchange) the connector runs after every
     tick on both sides and the connections made must agree (appended to
-    px_log when given)."""
+    px_log when given).  trace=(lo, hi): the engine traces routers [lo, hi)
+    and its events must equal the oracle's event log per tick (the event
+    counts appended to trace_log)."""
     from gsim.engine import Engine
     pushed = eng is None
     if eng is None:
@@ -48,6 +83,9 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
             st.push_to_engine(eng)
         eng.msgs_init(ring, R, T0, Second)
         msgs = ob.Msgs(net.n, st.T, ring, R, T0, Second, behaviour=behaviour)
+        if trace is not None:
+            eng.trace_config(trace[0], trace[1], 1 << 22)
+            msgs.log()
         if behaviour is not None:
             eng.set_peer_behaviour(behaviour)
         lib = ob.load()
@@ -79,6 +117,14 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
             gpu = ob.NetState(net, params, thresholds=th, gossip=gp)
             gpu.pull_from_engine(eng)
             assert_same(st, gpu)
+            if trace is not None:
+                got, want = eng.trace_read(), oracle_trace(msgs.events(), msgs, trace[0], trace[1])
+                assert len(got) == len(want), f"trace length differs at tick {kk}: {len(got)} vs {len(want)}"
+                for f in ("timestamp", "msg_id", "peer", "other", "topic", "type", "reason"):
+                    bad = np.nonzero(got[f] != want[f])[0]
+                    assert len(bad) == 0, f"trace field {f} differs at tick {kk}: first at {bad[:1]}"
+                if trace_log is not None:
+                    trace_log.append(np.bincount(want["type"], minlength=13))
             if gp.PeerExchange:
                 t_px = now + Second // 2
                 got, want = eng.px_connect(t_px), st.px_connect(t_px)
