@@ -28,19 +28,32 @@ priv* orc_msgs_priv(orc_msgs* m)
 
 static priv* P(orc_msgs* m) { return orc_msgs_priv(m); }
 
-static orc_msgs* g_net_log;
+/* Router-level events (GRAFT/PRUNE/ADD/REMOVE) have no message log at hand
+ * in oracle_net.c: they go to one buffer the oracle owns, on while any
+ * message log is, and are handed out with the next orc_msgs_events. */
+static int g_net_on;
+static orc_event* g_net_ev;
+static int64_t g_net_n, g_net_cap;
 
 void orc_msgs_log(orc_msgs* m, int32_t on)
 {
     P(m)->log_on = on;
-    g_net_log = on ? m : (g_net_log == m ? NULL : g_net_log);
+    g_net_on = on;
+    g_net_n = 0;
 }
 
 void orc_log_net(int32_t kind, uint32_t a, uint32_t b, int32_t topic, int64_t now)
 {
-    if (!g_net_log) return;
+    if (!g_net_on) return;
 #pragma omp critical(orc_log)
-    orc_log(g_net_log, kind, a, b, 0, topic, 0, now);
+    {
+        if (g_net_n == g_net_cap) {
+            g_net_cap = g_net_cap ? 2 * g_net_cap : 4096;
+            g_net_ev = (orc_event*)realloc(g_net_ev, sizeof(orc_event) * (size_t)g_net_cap);
+        }
+        orc_event* v = &g_net_ev[g_net_n++];
+        v->kind = kind; v->topic = topic; v->a = a; v->b = b; v->g = 0; v->mid = 0; v->x = now;
+    }
 }
 
 void orc_log(orc_msgs* m, int32_t kind, uint32_t a, uint32_t b, uint32_t slot, int32_t topic, int64_t g, int64_t x)
@@ -60,15 +73,19 @@ void orc_log(orc_msgs* m, int32_t kind, uint32_t a, uint32_t b, uint32_t slot, i
 int64_t orc_msgs_events(orc_msgs* m, orc_event* out, int64_t cap)
 {
     priv* p = P(m);
-    const int64_t n = p->nev;
-    if (out) memcpy(out, p->ev, sizeof(orc_event) * (size_t)(n < cap ? n : cap));
-    if (out) p->nev = 0;
-    return n;
+    const int64_t n = p->nev, nn = p->log_on ? g_net_n : 0;
+    if (out) {
+        memcpy(out, p->ev, sizeof(orc_event) * (size_t)(n < cap ? n : cap));
+        if (cap > n) memcpy(out + n, g_net_ev, sizeof(orc_event) * (size_t)(nn < cap - n ? nn : cap - n));
+        p->nev = 0;
+        if (p->log_on) g_net_n = 0;
+    }
+    return n + nn;
 }
 
 void orc_msgs_free_priv(orc_msgs* m)
 {
-    if (g_net_log == m) g_net_log = NULL;
+    if (m->priv && ((priv*)m->priv)->log_on) g_net_on = 0;
     if (!m->priv) return;
     priv* p = (priv*)m->priv;
     free(p->ev);
