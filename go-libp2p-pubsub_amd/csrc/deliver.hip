@@ -654,9 +654,17 @@ __global__ __launch_bounds__(256) void k_mesh_mask(const uint32_t* row_ptr, cons
 // power-law hubs.  Forwarders walk their mesh mask (rows <= 64), the origin
 // and hubs their whole row.
 constexpr int kTsSlots = 64;
+#ifndef GSIM_TM_P
+#define GSIM_TM_P 2          // flattened edges per thread per iteration (loads interleaved)
+#endif
+#ifndef GSIM_TM_MINB
+#define GSIM_TM_MINB 1       // resident blocks per CU the register budget is fitted to
+#endif
+constexpr uint32_t kTmWin = 8192;   // flattened edges whose senders are tabled in LDS at once
+constexpr int kTmTabMin = 256;      // forwarders in a chunk from which the table pays for its fill
 
 template <int kTmThreads>
-__global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a)
+__global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs a)
 {
     extern __shared__ uint64_t s_dyn[];
     uint16_t* s_slots = reinterpret_cast<uint16_t*>(s_dyn);  // [ring] active slots of topic t
@@ -669,6 +677,7 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a)
     __shared__ uint32_t s_beg[kTmChunk];                     // its row's first edge (sedge: first entry)
     __shared__ uint64_t s_msk[kTmChunk];                     // its mesh mask (0: the whole row)
     __shared__ uint8_t s_sk[kTmChunk];                       // its slot (index in the pass)
+    __shared__ uint16_t s_own[kTmWin];                       // sender (index above) of each flattened edge of a window
     __shared__ uint32_t s_wsum[64];
     __shared__ uint32_t s_m[kTsSlots], s_org[kTsSlots];      // the pass's slots and their origins
     __shared__ uint8_t s_vd[kTsSlots], s_ow[kTsSlots], s_wa[kTsSlots];
@@ -830,20 +839,35 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a)
                 const int nf = s_nf;
                 const uint32_t ne = s_ne;
                 if (nf > 0) {
-                    constexpr int P = 2;
+                    constexpr int P = GSIM_TM_P;
                     constexpr uint32_t kPerIt = kTmThreads * P;
-                    const uint32_t n_it = (ne + kPerIt - 1) / kPerIt;
-                    for (uint32_t it = 0; it < n_it; ++it) {
+                    static_assert(kTmWin % kPerIt == 0, "whole iterations per window");
+                  // dense chunks table each flattened edge's sender in LDS (written by
+                  // the senders); sparse ones search the offsets per edge
+                  const bool tab = nf >= kTmTabMin;
+                  for (uint32_t w0 = 0; w0 < ne; w0 += tab ? kTmWin : ne) {
+                    const uint32_t w1 = (!tab || ne - w0 < kTmWin) ? ne : w0 + kTmWin;
+                    if (tab) {
+                        for (int q = tid; q < nf; q += kTmThreads) {
+                            const uint32_t o0 = s_off[q], o1 = q + 1 < nf ? s_off[q + 1] : ne;
+                            const uint32_t lo_f = o0 > w0 ? o0 : w0, hi_f = o1 < w1 ? o1 : w1;
+                            for (uint32_t f = lo_f; f < hi_f; ++f) s_own[f - w0] = (uint16_t)q;
+                        }
+                        __syncthreads();
+                    }
+                    for (uint32_t it0 = w0; it0 < w1; it0 += kPerIt) {
                         uint32_t jv[P], fv[P], ev[P], iv[P], nv[P], kv[P];
                         uint8_t mfv[P], dsv[P], tfv[P];
-                        bool vv[P];
+                        bool vv[P], mk[P];
                         double xv[P];
 #pragma unroll
                         for (int u = 0; u < P; ++u) {
-                            const uint32_t fi = it * kPerIt + (uint32_t)(u * kTmThreads + tid);
+                            const uint32_t fi = it0 + (uint32_t)(u * kTmThreads + tid);
+                            vv[u] = fi < w1;
                             int q = 0;
-                            vv[u] = fi < ne;
-                            if (vv[u]) {
+                            if (vv[u] && tab) {
+                                q = (int)s_own[fi - w0];
+                            } else if (vv[u]) {
                                 int l = 0, r = nf;
                                 while (r - l > 1) {
                                     const int mid = (l + r) >> 1;
@@ -856,6 +880,7 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a)
                             kv[u] = vv[u] ? s_sk[q] : 0u;
                             const uint32_t k = fi - s_off[q];
                             const uint64_t msk = s_msk[q];
+                            mk[u] = msk != 0;
                             if (msk) ev[u] = s_beg[q] + kth_bit(msk, k);
                             else if (a.sedge && vv[u]) ev[u] = a.sedge[s_beg[q] + k];
                             else ev[u] = s_beg[q] + k;
@@ -866,7 +891,10 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a)
                             if (vv[u]) {
                                 const uint32_t e = ev[u];
                                 const uint8_t vd = s_vd[kv[u]];
-                                iv[u] = a.col[e]; mfv[u] = a.mflags[plane + e]; dsv[u] = a.dstate[e]; tfv[u] = a.tflags[plane + e];
+                                // a masked row's positions are its mesh (or direct) edges: the
+                                // router flags are read only for direct ones (below)
+                                iv[u] = a.col[e]; dsv[u] = a.dstate[e]; tfv[u] = a.tflags[plane + e];
+                                if (!mk[u]) mfv[u] = a.mflags[plane + e];
                                 if (verdict_penalises(vd)) xv[u] = a.invalid[plane + e];
                                 else if (vd == GSIM_VERDICT_ACCEPT) nv[u] = a.mcnt[plane + e];
                             }
@@ -879,7 +907,9 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a)
                             const bool inv = vd != GSIM_VERDICT_ACCEPT;
                             const bool pen = verdict_penalises(vd), seeable = vd != GSIM_VERDICT_SIGNATURE;
                             const uint8_t ds = dsv[u], tf = tfv[u];
-                            bool sel = (mfv[u] & (j == origin ? s_ow[k] : GSIM_TF_MESH)) != 0;
+                            bool sel;
+                            if (mk[u]) sel = !(ds & GSIM_DS_DIRECT) || (a.mflags[plane + e] & GSIM_TF_MESH);
+                            else sel = (mfv[u] & (j == origin ? s_ow[k] : GSIM_TF_MESH)) != 0;
                             if (a.flood && vv[u] && j == origin)
                                 sel = ((a.sub[i] >> t) & 1ull) &&
                                       ((a.sharded && (j < a.rlo || j >= a.rhi)) ? a.pgate[e] != 0
@@ -939,6 +969,8 @@ __global__ __launch_bounds__(kTmThreads) void k_send_tm(RoundArgs a)
                             }
                         }
                     }
+                    if (tab) __syncthreads();                    // s_own is rewritten by the next window
+                  }
                 }
                 // the next layer: each peer's next slot
                 first_layer = false;
