@@ -324,6 +324,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--msg-rate", type=float, default=None, help="messages per second per topic (config default)")
+    ap.add_argument("--ring", type=int, default=None, help="message ring slots (config default)")
     ap.add_argument("--replicas", action="store_true",
                     help="N > 1: one independent network per rank (weak scaling) instead of one sharded network")
     ap.add_argument("--shards", type=int, default=1,
@@ -342,7 +344,11 @@ def main():
         dist.init_process_group("nccl")
 
     cfg = CONFIGS[args.config]
-    scen = SCENARIOS.get(args.config, {})
+    scen = dict(SCENARIOS.get(args.config, {}))
+    if args.msg_rate is not None:
+        scen["msg_rate"] = args.msg_rate
+    if args.ring is not None:
+        scen["ring"] = args.ring
     n, k, T = cfg[0], cfg[1], cfg[2]
     sharded = (world > 1 and not args.replicas) or args.shards > 1
     shard = None
