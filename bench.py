@@ -59,15 +59,15 @@ CONFIGS = {
 #  c5  Chung-Lu power law (exponent 2.5, mean 16, rows <= 4096: hubs of a few hundred), 64 topics
 #      with Zipf subscriptions (8 per peer), 1 % of connections going down
 #      per tick and coming back two ticks later, publishers are topic members,
-#      2 msg/s/topic (128 msg/s network-wide; at 4 msg/s/topic the 5000-slot
-#      ring, capped by MaxIHaveLength, is reused while messages still trickle
-#      through gossip on the sparse topic graphs).
+#      4 msg/s/topic (256 msg/s network-wide) over an 8192-slot ring, peer
+#      exchange on (PRUNEs carry PX; the connector runs between ticks and
+#      reconnects churned-down addresses).
 #      2M peers: the dense [T][E] record planes of 10M peers x 64 topics
 #      (~560 GB) do not fit one GPU's 288 GB.
 SCENARIOS = {
     "c4": {"sybil_frac": 0.2, "per_ip": 50, "opp_ticks": 10},
-    "c5": {"power_law": (2.5, 4096), "zipf_per_peer": 8, "churn_frac": 0.01, "ring": 5000,
-           "msg_rate": 2.0},
+    "c5": {"power_law": (2.5, 4096), "zipf_per_peer": 8, "churn_frac": 0.01, "ring": 8192,
+           "msg_rate": 4.0, "px": True},
 }
 
 
@@ -144,7 +144,7 @@ def build_engine(cfg, seed, device, scen=None, shard=None):
     n, k, T, D, Dlo, Dhi = cfg
     scen = scen or {}
     params = beacon_params(T)
-    gp = gsim.GossipSubParams(D=D, Dlo=Dlo, Dhi=Dhi)
+    gp = gsim.GossipSubParams(D=D, Dlo=Dlo, Dhi=Dhi, PeerExchange=bool(scen.get("px")) and shard is None)
     if "opp_ticks" in scen:
         gp.OpportunisticGraftTicks = scen["opp_ticks"]
     if shard is None:
@@ -182,6 +182,8 @@ def describe_graph(cfg, scen) -> str:
               f"opportunistic grafting every {scen['opp_ticks']} heartbeats")
     if "churn_frac" in scen:
         d += f", {scen['churn_frac']:.0%} of connections down per tick (back 2 ticks later)"
+    if scen.get("px"):
+        d += ", peer exchange"
     return d
 
 
@@ -203,7 +205,7 @@ def churn_schedule(net, frac: float, ticks: range, seed: int = 4) -> dict:
     return out
 
 
-def run_tick(eng, k, sched, churn=None):
+def run_tick(eng, k, sched, churn=None, px=False):
     now = tick_time(k)
     for (pairs, up) in (churn or {}).get(k, []):
         eng.set_connections(pairs, up=up, now=now - SECOND // 2)
@@ -214,6 +216,8 @@ def run_tick(eng, k, sched, churn=None):
         if m is not None:
             eng.publish_array(m, g)
         eng.round(g)
+    if px:                                     # the connector for this tick's PX attempts
+        eng.px_connect(now + SECOND // 2)
 
 
 def cpu_baseline(cfg, scen=None, n: int = 10_000, ticks: int = 5, budget_s: float = 25.0):
@@ -230,7 +234,7 @@ def cpu_baseline(cfg, scen=None, n: int = 10_000, ticks: int = 5, budget_s: floa
     k, T, D, Dlo, Dhi = cfg[1], cfg[2], cfg[3], cfg[4], cfg[5]
     net, beh = build_network((n,) + tuple(cfg[1:]), 2, scen)
     params = beacon_params(T)
-    gp = gsim.GossipSubParams(D=D, Dlo=Dlo, Dhi=Dhi)
+    gp = gsim.GossipSubParams(D=D, Dlo=Dlo, Dhi=Dhi, PeerExchange=bool(scen.get("px")))
     if "opp_ticks" in scen:
         gp.OpportunisticGraftTicks = scen["opp_ticks"]
     rate = scen.get("msg_rate", MSG_RATE)
@@ -265,6 +269,8 @@ def cpu_baseline(cfg, scen=None, n: int = 10_000, ticks: int = 5, budget_s: floa
                 for m in sched.get(g, []):
                     msgs.publish(st, int(m["id"]), int(m["topic"]), int(m["origin"]), 0, g)
                 msgs.round(st, g)
+            if gp.PeerExchange:
+                st.px_connect(now + SECOND // 2)
             if kk > 1:                                  # tick 1 warms up
                 times.append(time.perf_counter() - t0)
                 deliv.append(msgs.stats[0] - d0)
@@ -374,7 +380,7 @@ def main():
     kk = 0
     for _ in range(args.warmup):
         kk += 1
-        run_tick(eng, kk, sched, churn)
+        run_tick(eng, kk, sched, churn, px=bool(scen.get("px")) and shard is None)
     eng.synchronize()
     census0 = eng.census()
     stats0 = eng.msg_stats()
@@ -394,7 +400,7 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         kk += 1
-        run_tick(eng, kk, sched, churn)
+        run_tick(eng, kk, sched, churn, px=bool(scen.get("px")) and shard is None)
     eng.synchronize()
     barrier()
     wall = time.perf_counter() - t0
