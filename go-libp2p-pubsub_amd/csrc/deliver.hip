@@ -658,7 +658,10 @@ constexpr int kTsSlots = 64;
 #define GSIM_TM_P 2          // flattened edges per thread per iteration (loads interleaved)
 #endif
 #ifndef GSIM_TM_MINB
-#define GSIM_TM_MINB 1       // resident blocks per CU the register budget is fitted to
+#define GSIM_TM_MINB 1       // waves per SIMD the register budget is fitted to
+#endif
+#ifndef GSIM_TM_TB
+#define GSIM_TM_TB 1024      // threads per k_send_tm block
 #endif
 constexpr uint32_t kTmWin = 8192;   // flattened edges whose senders are tabled in LDS at once
 constexpr int kTmTabMin = 256;      // forwarders in a chunk from which the table pays for its fill
@@ -2030,8 +2033,8 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a)
     // fill the chip; blocks of idle topics leave after the slot scan).  c5 block
     // budgets 4096 / 8192 / 15680 (default) / 32768 / 65536: 29.7 / 25.0 / 24.7 /
     // 28.0 / 32.9 ms of send per tick (profiles/r02_ab_send_blocks.log)
-    constexpr int TB = 1024;
-    constexpr int64_t total = 2048;
+    constexpr int TB = GSIM_TM_TB;
+    constexpr int64_t total = 2048 * (1024 / TB);
     constexpr int64_t chunk = 2 * TB;
     const int64_t cn = h->n;                 // every local peer sends (a shard's ghosts too)
     const int T = std::max(1, h->t);
