@@ -38,6 +38,7 @@ struct Extra {
     uint8_t* d_pxm = nullptr;
     uint8_t* d_nopx = nullptr;
     uint32_t* d_pxc = nullptr;         // [1 + 2E] connections made: count, then (dialer edge, peer edge)
+    double* d_pxs = nullptr;           // [E] live scores of PX observers (HbArgs::pxs)
 };
 
 struct HbArgs {
@@ -101,6 +102,7 @@ struct HbArgs {
     uint64_t* pxo;             // [N] topics in which the observer sent a PRUNE with PX
     uint8_t* pxm;              // [E] the row's owner tries to connect to col[e]
     uint8_t* nopx;             // [E] a GRAFT of this sender turned PX off for its RPC
+    double* pxs;               // [E] the observer's live score of col[e] after its heartbeat (PX observers)
     TraceRef tr;               // gsim_trace_config: tracer.Graft / Prune / AddPeer / RemovePeer
 };
 
@@ -843,7 +845,16 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
           }
         }
         // sendGraftPrune follows every topic: k_px_emit picks the PX peers
-        if (a.do_px && pxt && gl == 0 && ovalid) a.pxo[obs] = pxt;
+        if (a.do_px && pxt) {
+            // the live scores makePrune's PX filter reads (k_px_emit): lanes this
+            // heartbeat's Graft/Prune touched since their last re-score
+            if (g.any(dirty)) {
+                if (dirty) S_live = score_of_record(a, rv, col);
+                dirty = false;
+            }
+            if (valid) a.pxs[e] = S_live;
+            if (gl == 0 && ovalid) a.pxo[obs] = pxt;
+        }
 }
 
 // W-lane groups: W = 64 one observer per wavefront, W = 32 two, W = 16 four
@@ -1135,6 +1146,24 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
 // rows of at most 1024 connections (keys and scores staged in LDS).
 constexpr int kPxRow = 1024;
 
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v)
+{
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t y = (uint64_t)__shfl_xor((long long)v, o, 64);
+        v = y > v ? y : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
+{
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t y = (uint64_t)__shfl_xor((long long)v, o, 64);
+        v = y < v ? y : v;
+    }
+    return v;
+}
+
 // LDS written by some lanes of a wave, read by others
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -1159,7 +1188,8 @@ __global__ __launch_bounds__(256) void k_px_emit(HbArgs a, int live, uint32_t ke
         const uint32_t gobs = glob(a, (uint32_t)obs);
         for (int q = lane; q < deg; q += 64) {
             const uint32_t e = b + (uint32_t)q, x = a.col[e], rv = a.rev[e];
-            sc[q] = live ? score_of_record(a, rv, x) : a.score[rv];
+            sc[q] = live ? a.pxs[e] : a.score[rv];
+            (void)x;
         }
         wave_lds_sync();
         for (uint64_t tm = mask; tm; tm &= tm - 1) {
@@ -1186,24 +1216,42 @@ __global__ __launch_bounds__(256) void k_px_emit(HbArgs a, int live, uint32_t ke
                         n += (uint32_t)__popcll(__ballot(c));
                     }
                     wave_lds_sync();
-                    uint64_t tau = ~0ull - 1;                      // every candidate (keys of others are ~0)
+                    // the PrunePeers smallest keys are those below tau: start from the
+                    // quantile estimate of the (uniform) high words, then move tau past
+                    // one key at a time (as select_smallest)
+                    uint64_t tau = ~0ull;                          // exclusive; every candidate (others are ~0)
                     if ((int32_t)n > a.prune_peers) {
-                        uint64_t lo = 0, hi = ~0ull - 1;
-                        while (lo < hi) {
-                            const uint64_t mid = lo + ((hi - lo) >> 1);
-                            uint32_t c = 0;
+                        tau = (uint64_t)((double)a.prune_peers / (double)n * 4294967296.0) << 32;
+                        int32_t c = 0;
+                        for (int q0 = 0; q0 < deg; q0 += 64) {
+                            const int q = q0 + lane;
+                            c += (int32_t)__popcll(__ballot(q < deg && key[q] < tau));
+                        }
+                        while (c > a.prune_peers) {                // drop the largest key below tau
+                            uint64_t mx = 0;
                             for (int q0 = 0; q0 < deg; q0 += 64) {
                                 const int q = q0 + lane;
-                                c += (uint32_t)__popcll(__ballot(q < deg && key[q] <= mid));
+                                if (q < deg && key[q] < tau && key[q] >= mx) mx = key[q];
                             }
-                            if ((int32_t)c >= a.prune_peers) hi = mid; else lo = mid + 1;
+                            mx = wave_max_u64(mx);
+                            tau = mx;
+                            --c;
                         }
-                        tau = lo;
+                        while (c < a.prune_peers) {                // add the smallest key at or above tau
+                            uint64_t mn = ~0ull;
+                            for (int q0 = 0; q0 < deg; q0 += 64) {
+                                const int q = q0 + lane;
+                                if (q < deg && key[q] >= tau && key[q] < mn) mn = key[q];
+                            }
+                            mn = wave_min_u64(mn);
+                            tau = mn + 1;
+                            ++c;
+                        }
                     }
                     const uint32_t pb = a.row_ptr[p], pe = a.row_ptr[p + 1];
                     for (int q0 = 0; q0 < deg; q0 += 64) {
                         const int q = q0 + lane;
-                        if (q >= deg || key[q] > tau) continue;
+                        if (q >= deg || key[q] >= tau) continue;
                         const uint32_t x = a.col[b + (uint32_t)q];
                         uint32_t lo = pb, hi = pe;                 // p's row is sorted: its edge to x
                         while (lo < hi) {
@@ -1528,11 +1576,13 @@ int alloc_extra(gsim_handle* h)
     }
     h->max_degree = mdall;   // every local row (a shard's ghost rows too)
     if (h->gp.do_px && !h->sh) {
-        const size_t pb = sizeof(uint64_t) * (size_t)h->n + 2 * (size_t)h->e + sizeof(uint32_t) * (1 + 2 * (size_t)h->e);
+        const size_t pb = sizeof(uint64_t) * (size_t)h->n + 2 * (size_t)h->e + sizeof(uint32_t) * (1 + 2 * (size_t)h->e) +
+                          sizeof(double) * (size_t)h->e;
         e = hipMalloc((void**)&h->x->d_pxo, sizeof(uint64_t) * (size_t)h->n);
         if (e == hipSuccess) e = hipMalloc((void**)&h->x->d_pxm, (size_t)h->e);
         if (e == hipSuccess) e = hipMalloc((void**)&h->x->d_nopx, (size_t)h->e);
         if (e == hipSuccess) e = hipMalloc((void**)&h->x->d_pxc, sizeof(uint32_t) * (1 + 2 * (size_t)h->e));
+        if (e == hipSuccess) e = hipMalloc((void**)&h->x->d_pxs, sizeof(double) * (size_t)h->e);
         if (e == hipSuccess) e = hipMemsetAsync(h->x->d_pxo, 0, sizeof(uint64_t) * (size_t)h->n, h->stream);
         if (e == hipSuccess) e = hipMemsetAsync(h->x->d_pxm, 0, (size_t)h->e, h->stream);
         if (e == hipSuccess) e = hipMemsetAsync(h->x->d_nopx, 0, (size_t)h->e, h->stream);
@@ -1554,6 +1604,7 @@ void free_extra(gsim_handle* h)
     if (h->x->d_pxm) (void)hipFree(h->x->d_pxm);
     if (h->x->d_nopx) (void)hipFree(h->x->d_nopx);
     if (h->x->d_pxc) (void)hipFree(h->x->d_pxc);
+    if (h->x->d_pxs) (void)hipFree(h->x->d_pxs);
     delete h->x;
     h->x = nullptr;
 }
@@ -1630,7 +1681,7 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.do_px = h->x->d_pxo ? 1 : 0;
     a.prune_peers = h->gp.prune_peers;
     a.accept_px = h->th.accept_px_threshold;
-    a.pxo = h->x->d_pxo; a.pxm = h->x->d_pxm; a.nopx = h->x->d_nopx;
+    a.pxo = h->x->d_pxo; a.pxm = h->x->d_pxm; a.nopx = h->x->d_nopx; a.pxs = h->x->d_pxs;
     a.tr = h->trace;
     return a;
 }
