@@ -128,3 +128,15 @@ def test_px_bit_exact(require_gpu, T, accept):
     log = []
     run_parity(net, params, th, gp, st, ticks, sched, ring=512, churn=churn, px_log=log)
     assert sum(log) > 0, "PX made connections"
+
+
+def test_sharded_group_refuses_peer_exchange():
+    """pxConnect resolves a pruned peer's whole row, which a shard holds only
+    for its own peers: a group with PX is refused before any device work."""
+    from fixtures import beacon_params
+    from gsim.engine import GsimError
+    from gsim.shard import ShardedEngine
+    gp = GossipSubParams(D=6, Dlo=5, Dhi=10, PeerExchange=True)
+    with pytest.raises((GsimError, ValueError, RuntimeError)) as ei:
+        ShardedEngine(beacon_params(2), PeerScoreThresholds(), gossip=gp, shards=2)
+    assert "peer exchange" in str(ei.value)

@@ -178,3 +178,24 @@ def test_trace_bit_exact(require_gpu, lo, hi):
     total = np.sum(log, axis=0)
     for typ in (0, 1, 2, 3, 4, 5, 11, 12):
         assert total[typ] > 0, f"event type {typ} traced"
+
+
+def test_trace_encode_rejects_unknown_types_and_short_buffers():
+    import ctypes
+    names = [b"t0"]
+    recs = np.zeros(1, dtype=Engine.TRACE_DTYPE)
+    recs[0]["type"] = 6                    # RECV_RPC: not produced by the engine
+    with pytest.raises(wire.WireError):
+        wire.trace_batch(recs, names)
+    recs[0]["type"] = _abi.TRACE_REMOVE_PEER
+    lib = _abi.load()
+    nm = _abi.CWireNames()
+    tn = (_abi.CBytes * 1)()
+    buf = ctypes.create_string_buffer(b"t0", 2)
+    tn[0] = _abi.CBytes(ctypes.addressof(buf), 2)
+    nm.topic_names = ctypes.addressof(tn)
+    n = ctypes.c_uint64()
+    out = ctypes.create_string_buffer(4)
+    rc = lib.gsim_trace_encode(recs.ctypes.data_as(ctypes.c_void_p), 1, ctypes.byref(nm), b"p", out, 4,
+                               ctypes.byref(n))
+    assert rc == _abi.GSIM_ERANGE and n.value == len(wire.trace_batch(recs, names))
