@@ -1561,10 +1561,20 @@ int alloc_extra(gsim_handle* h)
         cls[d <= 16 ? 0 : d <= 32 ? 1 : d <= 64 ? 2 : d <= 256 ? 3 : 4].push_back((uint32_t)i);
     }
     for (int64_t i = 0; i < h->n; ++i) mdall = std::max(mdall, rp[(size_t)i + 1] - rp[(size_t)i]);
+    if (!h->all_joined) {
+        // lane groups pack 2-4 observers per wavefront, which runs the union of
+        // their joined topics: observers with the same subscriptions side by side
+        // (order within a heartbeat is free: observers are independent)
+        std::vector<uint64_t> sub((size_t)h->n);
+        e = hipMemcpy(sub.data(), h->d_sub, sizeof(uint64_t) * sub.size(), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return hip_check(h, e, "subscription readback");
+        for (int c = 0; c < 2; ++c)
+            std::stable_sort(cls[c].begin(), cls[c].end(), [&](uint32_t x, uint32_t y) { return sub[x] < sub[y]; });
+    }
     h->x->max_degree = md;
     h->x->n16 = (int64_t)cls[0].size(); h->x->n32 = (int64_t)cls[1].size(); h->x->n64 = (int64_t)cls[2].size();
     h->x->nh256 = (int64_t)cls[3].size(); h->x->nh1024 = (int64_t)cls[4].size();
-    if (md > 16) {   // more than one class may be present: keep the lists
+    if (md > 16 || !h->all_joined) {   // several classes, or an order by subscriptions: keep the lists
         std::vector<uint32_t> all;
         all.reserve((size_t)h->n);
         for (auto& c : cls) all.insert(all.end(), c.begin(), c.end());
@@ -1741,13 +1751,13 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     // independent within a heartbeat, so the classes run one after the other)
     const Extra* x = h->x;
     const int64_t nown = h->ohi() - h->olo();
-    if (x->n16 == nown) {   // one class: the owned rows in order
+    if (x->n16 == nown && !x->d_rows) {   // one class: the owned rows in order
         hipLaunchKernelGGL(k_heartbeat<16>, dim3(grid_rows((nown + 3) / 4)), dim3(256), 0, h->stream, a, nullptr, nown,
                            h->olo());
-    } else if (x->n32 == nown) {
+    } else if (x->n32 == nown && !x->d_rows) {
         hipLaunchKernelGGL(k_heartbeat<32>, dim3(grid_rows((nown + 1) / 2)), dim3(256), 0, h->stream, a, nullptr, nown,
                            h->olo());
-    } else if (x->n64 == nown) {
+    } else if (x->n64 == nown && !x->d_rows) {
         hipLaunchKernelGGL(k_heartbeat<64>, dim3(grid_rows(nown)), dim3(256), 0, h->stream, a, nullptr, nown, h->olo());
     } else {
         const uint32_t* r = x->d_rows;
