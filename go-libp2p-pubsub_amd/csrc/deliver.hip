@@ -62,10 +62,28 @@ __device__ __forceinline__ bool verdict_penalises(uint8_t v)
 }
 constexpr int kSlotBatch = 8;      // active slots whose cells are loaded together
 
+// Validation latency (gsim_msg.vdelay).  A cell first
+// claimed in round g of a slot with latency L > 0 is committed with
+// hi = g + L, the round its validation completes; a copy arriving before
+// that is a pending duplicate (deliveryUnknown, score.go:806-809), queued by
+// its completion round and credited or penalised at the start of that round
+// (k_vq_apply: score.go:719-725, 784-789), when the winner's
+// markFirstMessageDelivery lands too; k_vcomplete at the end of round g + L
+// sets the fresh bits (forwarding in round g + L + 1) and the mcache puts.
+constexpr int kVqPlanes = GSIM_MAX_VDELAY + 1;   // queues by completion round mod kVqPlanes
+constexpr uint32_t kVqFirst = 1, kVqDup = 2, kVqInv = 3;
+static_assert((kVqPlanes & (kVqPlanes - 1)) == 0, "power-of-two planes");
+
 struct Deliver {
     gsim_msg_config cfg{};
     uint32_t *d_mtopic = nullptr, *d_morigin = nullptr;
     uint8_t* d_minv = nullptr;
+    uint8_t* d_mlat = nullptr;         // [ring] validation latency of the slot's message (gsim_msg.vdelay)
+    uint64_t* d_vq = nullptr;          // [kVqPlanes][vq_cap] copies pending validation, by completion round
+    uint32_t* d_vqn = nullptr;         // [kVqPlanes] entries per plane; [kVqPlanes] overflow flag
+    uint32_t* d_hist = nullptr;        // [kVqPlanes][ring/32] slots with new claims, by round
+    int64_t vq_cap = 0;
+    bool lat_on = false;               // a message with vdelay > 0 was published
     uint64_t* d_mid = nullptr;         // [ring] gsim_msg.id of the slot's message (wire ids)
     uint64_t* d_cell = nullptr;        // [ring][N] seen-set cells (layout above)
     uint64_t* d_seenbm = nullptr;      // [ring][ceil(N/64)] bit: the cell is committed (a cache of the cells)
@@ -123,6 +141,11 @@ struct RoundArgs {
     uint32_t *mtopic, *morigin;
     uint8_t* minv;
     uint64_t* mid;             // [ring] gsim_msg ids (wire ids)
+    const uint8_t* mlat;       // [ring] validation latency (nullptr: none published, every latency 0)
+    uint8_t* mlat_w;           // the same array, written by k_publish
+    uint64_t* vq;              // [kVqPlanes][vq_cap] pending copies (Deliver::d_vq)
+    uint32_t* vqn;
+    int64_t vq_cap;
     uint64_t* cell;
     uint64_t* seenbm;          // [ring][nw] committed bits of the cells (read before a cell)
     uint64_t* fresh;           // [ring][nw] forwarders of the next round (topic-major delivery; nullptr otherwise)
@@ -208,6 +231,17 @@ __device__ __forceinline__ void atomic_inc_capped(double* p, double cap)
     }
 }
 
+// Queue a copy whose receiver completes validation in round c: record edge
+// e of topic t (score records sit at the sender's edge index), and what the
+// completion does with it (kVqFirst / kVqDup / kVqInv).
+__device__ __forceinline__ void vq_push(const RoundArgs& a, int64_t c, uint32_t e, int32_t t, uint32_t kind)
+{
+    const int pl = (int)(c & (kVqPlanes - 1));
+    const uint32_t k = atomicAdd(&a.vqn[pl], 1u);
+    if ((int64_t)k >= a.vq_cap) { atomicOr(&a.vqn[kVqPlanes], 1u); return; }
+    a.vq[(int64_t)pl * a.vq_cap + k] = (uint64_t)e | ((uint64_t)(uint32_t)t << 32) | ((uint64_t)kind << 40);
+}
+
 // Ordered list of the active slots (bit set in nnew), built by wave 0 into
 // LDS; every thread of the block must call it.
 __device__ __forceinline__ int active_slots(const uint32_t* nnew, int ring, uint16_t* s_act, int* s_n)
@@ -235,9 +269,16 @@ __device__ __forceinline__ void commit_claim(const RoundArgs& a, uint64_t* cellp
                                              uint32_t m, int64_t peer)
 {
     const uint32_t hi = (uint32_t)(c >> 32), lo = (uint32_t)c;
-    *cellp = ((uint64_t)(uint32_t)gc << 32) | (lo & kPeerMask);
-    if (a.minv[m]) return;                                // RejectMessage: counted when sent
+    const uint32_t L = a.mlat ? a.mlat[m] : 0u;
+    *cellp = ((uint64_t)(uint32_t)(gc + L) << 32) | (lo & kPeerMask);
     const int32_t t = (int32_t)a.mtopic[m];
+    if (L) {
+        // validation completes in round gc + L: the winner's DeliverMessage
+        // credit lands there (k_vq_apply), the put and forwarding after it
+        if (a.minv[m] == GSIM_VERDICT_ACCEPT && const_tp(a.tp)[t].scored) vq_push(a, gc + L, hi & kEdgeMask, t, kVqFirst);
+        return;
+    }
+    if (a.minv[m]) return;                                // RejectMessage: counted when sent
     int32_t* lp = a.lastput + (int64_t)t * a.N + peer;
     const int32_t tick = (int32_t)(gc / a.R);
     if (ATOMIC) atomicMax(lp, tick); else if (*lp < tick) *lp = tick;
@@ -308,6 +349,7 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, int32_t count)
     a.mtopic[slot] = p.topic;
     a.morigin[slot] = p.origin;          // local id (a shard: 0xFFFFFFFF when not a local peer)
     a.minv[slot] = p.verdict;
+    a.mlat_w[slot] = p.vdelay;
     a.mpub[slot] = (int32_t)a.g;
     if (a.mid) a.mid[slot] = p.id;
     if (p.origin >= a.clo && (int64_t)(p.origin - a.clo) < a.CN) {   // the origin's own cell
@@ -683,7 +725,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
     __shared__ uint16_t s_own[kTmWin];                       // sender (index above) of each flattened edge of a window
     __shared__ uint32_t s_wsum[64];
     __shared__ uint32_t s_m[kTsSlots], s_org[kTsSlots];      // the pass's slots and their origins
-    __shared__ uint8_t s_vd[kTsSlots], s_ow[kTsSlots], s_wa[kTsSlots];
+    __shared__ uint8_t s_vd[kTsSlots], s_ow[kTsSlots], s_wa[kTsSlots], s_lat[kTsSlots];
     __shared__ int s_ns, s_nf;
     __shared__ uint32_t s_ne;
     __shared__ unsigned long long s_clm;                     // slots of the pass with a new claim
@@ -730,6 +772,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
             s_vd[tid] = a.minv[m];
             s_ow[tid] = (origin < a.N && ((a.sub[origin] >> t) & 1ull)) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
             s_wa[tid] = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
+            s_lat[tid] = a.mlat ? a.mlat[m] : 0;
         }
         if (tid == 0) s_clm = 0;
         uint64_t clm = 0;
@@ -929,18 +972,26 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                                 a.tr.push(round_time(a, a.g), ((uint64_t)a.g << 32) | m, i, j, t,
                                           seeable ? kTraceCopy : (uint8_t)GSIM_TRACE_REJECT_MESSAGE, vd);
                             const bool sc = scored_t && (ds & GSIM_DS_TRACKED);
+                            const uint32_t L = s_lat[k];
                             const uint64_t* s_bm = a.seenbm + (int64_t)m * a.nw + wlo;
                             const int64_t bw = ((int64_t)i >> 6) - wlo;
+                            // a committed cell need not be read when the copy cannot be
+                            // credited; with a validation latency the credit is decided at
+                            // completion (mesh and record then), so only an unscored topic
+                            // or an ignored / throttled message skips it
                             const bool known = ((s_bm[bw] >> (i & 63)) & 1ull) &&
-                                               (s_wa[k] || !sc || inv || !(tf & GSIM_TF_IN_MESH));
+                                               (L ? (!scored_t || (inv && !pen))
+                                                  : (s_wa[k] || !sc || inv || !(tf & GSIM_TF_IN_MESH)));
                             const int64_t row_m = (int64_t)m * a.CN;
                             const uint64_t c = known ? 0ull : a.cell[row_m + ic];
                             const uint32_t chi = (uint32_t)(c >> 32);
+                            // the round validation completed (or completes) in; -1: unclaimed
+                            // or claimed in this round
                             int64_t seen_round = -1;
                             if (known) seen_round = a.g - 1;
                             else if (c != kUnseen64) {
                                 if (!(chi & kClaim)) seen_round = chi;
-                                else if (((chi >> 30) & 1u) != par) seen_round = a.g - 1;
+                                else if (((chi >> 30) & 1u) != par) seen_round = a.g - 1 + L;
                             }
                             if (seeable && seen_round < 0 && (c == kUnseen64 || (chi & kEdgeMask) > e)) {
                                 uint32_t lo_w = j;
@@ -952,6 +1003,12 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                                 const uint64_t prev = __hip_atomic_fetch_min(a.cell + row_m + ic, cv, __ATOMIC_RELAXED,
                                                                              __HIP_MEMORY_SCOPE_AGENT);
                                 if (prev == kUnseen64) { n_first++; clm |= 1ull << k; }
+                            }
+                            if (L && seeable && (seen_round < 0 || seen_round > a.g)) {
+                                // the receiver is still validating: drec.peers (score.go:806-809)
+                                if (scored_t && (pen || !inv))
+                                    vq_push(a, seen_round < 0 ? a.g + L : seen_round, e, t, pen ? kVqInv : kVqDup);
+                                continue;
                             }
                             if (!sc) continue;
                             const int64_t ir = plane + e;
@@ -1039,7 +1096,7 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
                 const uint32_t m = s_act[k];
                 a.seenbm[(int64_t)m * a.nw + (i0 >> 6)] |= cb;
                 // receivers forward what they accepted, in the next round
-                if (a.fresh && a.minv[m] == GSIM_VERDICT_ACCEPT) {
+                if (a.fresh && a.minv[m] == GSIM_VERDICT_ACCEPT && !(a.mlat && a.mlat[m])) {
                     // fire-and-forget atomics: the wave does not wait on them
                     atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (i0 >> 6)), cb);
                     atomicOr(reinterpret_cast<unsigned long long*>(a.fsum + (int64_t)m * a.nsw + (i0 >> 12)),
@@ -1085,6 +1142,7 @@ struct IhArgs {
     const uint64_t* sub;
     const uint32_t *mtopic, *morigin;
     const uint8_t* minv;
+    const uint8_t* mlat;           // validation latencies (RoundArgs::mlat)
     const uint64_t* cell;
     const int32_t* slot_last;
     const uint8_t *gsel, *gstate, *behaviour;
@@ -1124,14 +1182,15 @@ __device__ __forceinline__ bool peertx_allows(const IhArgs& a, uint32_t m, uint3
     return (int32_t)n <= a.retrans;
 }
 
-// first-seen round of a cell at control time of round g (any claim still
-// pending is from round g-1 or g), or -1
-__device__ __forceinline__ int64_t cell_round(uint64_t c, int64_t g)
+// round a cell's message was (or will be) validated and put in the mcache,
+// at control time of round g (any claim still pending is from round g-1 or
+// g and completes L rounds later), or -1
+__device__ __forceinline__ int64_t cell_round(uint64_t c, int64_t g, uint32_t L = 0)
 {
     if (c == kUnseen64) return -1;
     const uint32_t hi = (uint32_t)(c >> 32);
     if (!(hi & kClaim)) return hi;
-    return (((hi >> 30) & 1u) == (uint32_t)(g & 1)) ? g : g - 1;
+    return ((((hi >> 30) & 1u) == (uint32_t)(g & 1)) ? g : g - 1) + L;
 }
 
 constexpr int kRespStage = 256;    // per-wave LDS staging of queued responses
@@ -1142,9 +1201,9 @@ constexpr int kRespStage = 256;    // per-wave LDS staging of queued responses
 // walks its row for advertisers: "pull").  Both enumerate exactly the same
 // (receiver, advertiser, message) IWANT triples.
 __device__ __forceinline__ bool holds_in_window(uint64_t c, int64_t g, int32_t lo_round, int64_t tick_round,
-                                                bool inv, bool is_origin)
+                                                bool inv, bool is_origin, uint32_t L)
 {
-    const int64_t fr = cell_round(c, g);
+    const int64_t fr = cell_round(c, g, L);
     return fr >= lo_round && fr < tick_round && (!inv || is_origin);
 }
 
@@ -1191,7 +1250,7 @@ __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount
             const uint32_t m = s_act[k];
             const int32_t t = (int32_t)a.mtopic[m];
             const bool hold = vp && holds_in_window(cv[b], a.g, a.lo_round, tick_round, a.minv[m] != 0,
-                                                   (uint32_t)pl == a.morigin[m]);
+                                                   (uint32_t)pl == a.morigin[m], a.mlat ? a.mlat[m] : 0u);
             const bool want = vp && cv[b] == kUnseen64 && ((subp >> t) & 1ull) && pl >= a.rlo && pl < a.rhi;
             const int nh = __popcll(__ballot(hold)), nw = __popcll(__ballot(want));
             if (lane == 0 && nh) atomicAdd(&s_cnt[m], (uint32_t)nh);
@@ -1272,7 +1331,8 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
             const bool inv = a.minv[m] != 0;
             // push: lanes are holders of m (its advertisers); pull: lanes are
             // receivers that joined t and have not seen m (handleIHave's seenMessage)
-            const bool me = vp && (push ? holds_in_window(cv[b], a.g, a.lo_round, tick_round, inv, (uint32_t)pl == origin)
+            const bool me = vp && (push ? holds_in_window(cv[b], a.g, a.lo_round, tick_round, inv, (uint32_t)pl == origin,
+                                                          a.mlat ? a.mlat[m] : 0u)
                                         : (cv[b] == kUnseen64 && ((subp >> t) & 1ull) && pl >= a.rlo && pl < a.rhi));
             const uint64_t mask = __ballot(me);
             if (!mask) continue;
@@ -1316,7 +1376,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                         if (a.gsel[plane + re] && a.gstate[e]) {
                             const uint32_t i = a.col[e];
                             req = holds_in_window(a.cell[row_m + (i - a.clo)], a.g, a.lo_round, tick_round, inv,
-                                                  i == origin);
+                                                  i == origin, a.mlat ? a.mlat[m] : 0u);
                             if (req) {
                                 const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, me_g, 0, P_PROMISE, m,
                                                               a.gid ? a.gid[i] : i);
@@ -1445,7 +1505,7 @@ __global__ __launch_bounds__(256) void k_ihave_pairs(IhArgs a)
             const uint32_t origin_ign = a.behaviour[i] & GSIM_BEHAVE_IGNORE_IWANT;
             auto holds = [&](uint32_t m) {
                 return holds_in_window(a.cell[(int64_t)m * a.CN + ic], a.g, a.lo_round, tick_round, a.minv[m] != 0,
-                                       i == a.morigin[m]);
+                                       i == a.morigin[m], a.mlat ? a.mlat[m] : 0u);
             };
             // GetGossipIDs(topic) of i: ids per topic
             s_cnt[lane] = 0;
@@ -1617,10 +1677,11 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
         uint64_t* cellp = a.cell + (int64_t)m * a.CN + (p - a.clo);
         const uint64_t c = *cellp;
         const uint32_t hi = (uint32_t)(c >> 32);
-        int64_t seen_round = -1;
+        const uint32_t L = a.mlat ? a.mlat[m] : 0u;
+        int64_t seen_round = -1;               // completion round (k_send_tm)
         if (c != kUnseen64) {
             if (!(hi & kClaim)) seen_round = hi;
-            else if (((hi >> 30) & 1u) != par) seen_round = a.g - 1;
+            else if (((hi >> 30) & 1u) != par) seen_round = a.g - 1 + L;
         }
         if (vd != GSIM_VERDICT_SIGNATURE && seen_round < 0 && (c == kUnseen64 || (hi & kEdgeMask) > r)) {
             uint32_t lo = i;
@@ -1634,6 +1695,10 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
                 n_first++;
                 atomicOr(&s_new2[m >> 5], 1u << (m & 31));
             }
+        }
+        if (L && vd != GSIM_VERDICT_SIGNATURE && (seen_round < 0 || seen_round > a.g)) {
+            if (tp->scored && (pen || !inv)) vq_push(a, seen_round < 0 ? a.g + L : seen_round, r, t, pen ? kVqInv : kVqDup);
+            continue;
         }
         if (!sc) continue;
         if (pen) {
@@ -1694,6 +1759,84 @@ __global__ __launch_bounds__(256) void k_promise_check(uint32_t* prom_q, const u
     if ((threadIdx.x & 63) == 0 && broken) atomicAdd(&gstats[3], broken);
 }
 
+// Start of round g: the validations completing now credit or penalise the
+// copies queued for them (vq_push): the winner's markFirstMessageDelivery
+// (its P2 from k_commit's kVqFirst, its P3 from its copy's kVqDup, as for
+// the pending peers), the pending peers' markDuplicateMessageDelivery with validated zero (P3 if
+// the record is in the mesh now, no window), RejectMessage's
+// markInvalidMessageDelivery — each only if the record still exists
+// (score.go:702-793, 901-981).  Every update is a capped +1 (or +1), so the
+// queue order does not matter.
+__global__ __launch_bounds__(256) void k_vq_apply(RoundArgs a, int pl)
+{
+    const uint32_t n = (uint32_t)min((int64_t)a.vqn[pl], a.vq_cap);
+    const uint64_t* q = a.vq + (int64_t)pl * a.vq_cap;
+    const ctp_t tpa = const_tp(a.tp);
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) {
+        const uint64_t v = q[x];
+        const uint32_t e = (uint32_t)v, kind = (uint32_t)(v >> 40);
+        const int32_t t = (int32_t)((v >> 32) & 0xFFu);
+        if (!(a.dstate[e] & GSIM_DS_TRACKED)) continue;
+        const int64_t ir = (int64_t)t * a.E + e;
+        if (kind == kVqInv) { atomicAdd(&a.invalid[ir], 1.0); continue; }
+        const ctp_t tp = tpa + t;
+        // the winner's own copy was queued as kVqDup too: its kVqFirst adds
+        // only markFirstMessageDelivery's P2 part
+        if (kind == kVqFirst) atomic_inc_capped(&a.first[ir], tp->first_message_deliveries_cap);
+        else if (a.tflags[ir] & GSIM_TF_IN_MESH) atomic_inc_capped(&a.meshd[ir], tp->mesh_message_deliveries_cap);
+    }
+}
+
+// End of round g: the cells whose validation completed in round g (claimed
+// in round g - L of a slot with latency L, committed with hi = g) put the
+// message in their mcache and, if accepted, forward it in round g + 1.
+// hist: the slots with new claims of each round (Deliver::d_hist).
+__global__ __launch_bounds__(256) void k_vcomplete(RoundArgs a, const uint32_t* hist, int32_t words)
+{
+    extern __shared__ uint16_t s_act[];
+    __shared__ int s_n;
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        int n = 0;
+        for (int m0 = 0; m0 < a.ring; m0 += 64) {
+            const int m = m0 + lane;
+            const uint32_t L = m < a.ring ? a.mlat[m] : 0u;
+            const bool act = L && a.g >= (int64_t)L &&
+                             ((hist[(int64_t)((a.g - L) & (kVqPlanes - 1)) * words + (m >> 5)] >> (m & 31)) & 1u);
+            const uint64_t b = __ballot(act);
+            if (act) s_act[n + __popcll(b & ((1ull << lane) - 1))] = (uint16_t)m;
+            n += __popcll(b);
+        }
+        if (lane == 0) s_n = n;
+    }
+    __syncthreads();
+    const int nact = s_n;
+    const int lane = threadIdx.x & 63;
+    const int64_t i0 = (((int64_t)a.rlo - a.clo) & ~63ll) + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+    if (i0 >= (int64_t)a.rhi - a.clo || nact == 0) return;
+    const int64_t i = i0 + lane;
+    const bool vi = i < a.CN;
+    const int32_t tick = (int32_t)(a.g / a.R);
+    for (int k = 0; k < nact; ++k) {
+        const uint32_t m = s_act[k];
+        const uint64_t c = vi ? a.cell[(int64_t)m * a.CN + i] : kUnseen64;
+        const bool done = c != kUnseen64 && !((uint32_t)(c >> 32) & kClaim) && (int64_t)(c >> 32) == a.g;
+        const uint64_t b = __ballot(done);
+        if (!b) continue;
+        const bool acc = a.minv[m] == GSIM_VERDICT_ACCEPT;
+        if (done && acc) atomicMax(a.lastput + (int64_t)a.mtopic[m] * a.N + a.clo + i, tick);   // mcache.Put
+        if (lane == 0) {
+            atomicMax(&a.slot_last[m], (int32_t)a.g);
+            if (acc) {
+                atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (i0 >> 6)), b);
+                atomicOr(reinterpret_cast<unsigned long long*>(a.fsum + (int64_t)m * a.nsw + (i0 >> 12)),
+                         1ull << ((i0 >> 6) & 63));
+                atomicOr(&a.nnew_cur[m >> 5], 1u << (m & 31));   // round g + 1 walks the slot
+            }
+        }
+    }
+}
+
 // F_SEEN view [ring][N]: first-seen rounds of the peers with cells, unseen elsewhere
 __global__ void k_seen_view(const uint64_t* cell, uint32_t* out, int64_t n, int64_t N, int64_t CN, uint32_t clo)
 {
@@ -1719,6 +1862,7 @@ static void dl_free(Deliver* d)
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_peertx); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
+    f(d->d_mlat); f(d->d_vq); f(d->d_vqn); f(d->d_hist);
     delete d;
 }
 
@@ -1759,6 +1903,9 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.tflags = h->d_tflags; a.tp = h->d_tp;
     a.first = h->d_first; a.meshd = h->d_meshd; a.invalid = h->d_invalid; a.mcnt = h->d_mcnt;
     a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv; a.mid = d->d_mid;
+    a.mlat = d->lat_on ? d->d_mlat : nullptr;
+    a.mlat_w = d->d_mlat;
+    a.vq = d->d_vq; a.vqn = d->d_vqn; a.vq_cap = d->vq_cap;
     a.cell = d->d_cell; a.lastput = d->d_lastput;
     a.CN = h->n;
     a.clo = 0;
@@ -1880,6 +2027,7 @@ static bool ihave_prepare(gsim_handle* h, int64_t g, IhaveStage* st, int* rc)
     a.lo_round = (int32_t)std::max<int64_t>((tick - h->gp.history_gossip) * d->cfg.rounds, 0);
     a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.rev = h->d_rev; a.sub = h->d_sub;
     a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv;
+    a.mlat = d->lat_on ? d->d_mlat : nullptr;
     a.cell = d->d_cell; a.slot_last = d->d_slot_last;
     a.gsel = d->d_gsel; a.gstate = d->d_gstate; a.behaviour = d->d_behaviour;
     a.pcand = d->d_pcand; a.prom = d->d_prom; a.P = d->prom_ticks;
@@ -1980,10 +2128,23 @@ int deliver_flush(gsim_handle* h)
 // checked at the heartbeat (one small synchronous read per tick) so a caller
 // that never asks for gsim_msg_stats still stops before running on with
 // state that has diverged.
+static int vq_check(gsim_handle* h)
+{
+    Deliver* d = h->dl;
+    if (!d->lat_on) return GSIM_OK;
+    uint32_t ov = 0;
+    hipError_t e = hipMemcpyAsync(&ov, d->d_vqn + kVqPlanes, sizeof(ov), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "validation queue flag");
+    if (ov) { h->err = "copies pending validation overflowed their queue (raise gsim_msg_config.max_arrivals)"; return GSIM_ERANGE; }
+    return GSIM_OK;
+}
+
 int deliver_check_errors(gsim_handle* h)
 {
     Deliver* d = h->dl;
     if (!d) return GSIM_OK;
+    if (int rc = vq_check(h)) return rc;
     uint32_t err[4] = {0, 0, 0, 0};
     hipError_t e = hipMemcpyAsync(err, d->d_nresp, sizeof(err), hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
@@ -2002,7 +2163,16 @@ bool deliver_trace_view(gsim_handle* h, TraceView* v)
     if (!d) return false;
     v->cell = d->d_cell; v->mtopic = d->d_mtopic; v->minv = d->d_minv; v->mid = d->d_mid;
     v->ring = d->cfg.ring; v->rounds = d->cfg.rounds;
+    v->mlat = d->lat_on ? d->d_mlat : nullptr;
+    v->t0 = d->cfg.t0_ns; v->hb = d->cfg.heartbeat_ns; v->roff = d->d_roff;
     return true;
+}
+
+int64_t deliver_last_round_time(gsim_handle* h)
+{
+    const Deliver* d = h->dl;
+    if (!d || d->next_round <= 0) return INT64_MAX;
+    return round_time_host(d, d->next_round - 1);
 }
 
 int deliver_read_seen(gsim_handle* h, void* dst)
@@ -2119,7 +2289,35 @@ int deliver_round_prepare(gsim_handle* h, int64_t round)
         if (rc) return rc;
     }
     if (d->fresh_on) rc = deliver_flush(h);
+    if (!rc && d->lat_on) {
+        // validations completing now (the flush above queued round g-1's
+        // winners with latency 1)
+        ProfScope ps(h, GSIM_K_COMMIT);
+        RoundArgs a = make_round_args(h, round);
+        const int pl = (int)(round & (kVqPlanes - 1));
+        hipLaunchKernelGGL(k_vq_apply, dim3(1024), dim3(256), 0, h->stream, a, pl);
+        hipError_t e = hipMemsetAsync(d->d_vqn + pl, 0, sizeof(uint32_t), h->stream);
+        if (e == hipSuccess) e = hipGetLastError();
+        rc = hip_check(h, e, "k_vq_apply");
+    }
     return rc;
+}
+
+// End of round g (validation latencies): the round's claims are recorded for
+// their completion round, and the cells completing now put and forward.
+int deliver_round_validate(gsim_handle* h, int64_t round)
+{
+    Deliver* d = h->dl;
+    if (!d->lat_on) return GSIM_OK;
+    ProfScope ps(h, GSIM_K_COMMIT);
+    RoundArgs a = make_round_args(h, round);
+    const int w = nnew_words(d);
+    hipError_t e = hipMemcpyAsync(d->d_hist + (size_t)(round & (kVqPlanes - 1)) * (size_t)w, a.nnew_cur,
+                                  (size_t)w * 4, hipMemcpyDeviceToDevice, h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "validation history");
+    hipLaunchKernelGGL(k_vcomplete, dim3(grid_peers((int64_t)a.rhi - (((int64_t)a.rlo - a.clo) & ~63ll))), dim3(256),
+                       (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a, (const uint32_t*)d->d_hist, w);
+    return hip_check(h, hipGetLastError(), "k_vcomplete");
 }
 
 // Stage 2: the delivery kernel of round g.
@@ -2422,6 +2620,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_mtopic, ring * 4);
     A((void**)&d->d_morigin, ring * 4);
     A((void**)&d->d_minv, ring);
+    A((void**)&d->d_mlat, ring);
     A((void**)&d->d_mid, ring * 8);
     A((void**)&d->d_cell, ring * CN * 8);
     A((void**)&d->d_seenbm, ring * ((CN + 63) / 64) * 8);
@@ -2478,6 +2677,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     if (e == hipSuccess) e = hipMemsetAsync(d->d_mtopic, 0, ring * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_morigin, 0, ring * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_minv, 0, ring, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_mlat, 0, ring, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_nnew, 0, 2 * words * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_stats, 0, 4 * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_slot_last, 0xFF, ring * 4, h->stream);
@@ -2515,6 +2715,11 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
             return GSIM_EINVAL;
         }
         slots[(size_t)m] = (uint32_t)(msgs[m].id % (uint64_t)d->cfg.ring);
+        if (msgs[m].vdelay > GSIM_MAX_VDELAY) { h->err = "vdelay above GSIM_MAX_VDELAY"; return GSIM_EINVAL; }
+        if (msgs[m].vdelay && (h->sh || !d->fresh_on)) {
+            h->err = "a validation latency (vdelay) needs the topic-major delivery of a single engine";
+            return GSIM_ERANGE;
+        }
     }
     std::sort(slots.begin(), slots.end());
     if (std::adjacent_find(slots.begin(), slots.end()) != slots.end()) {
@@ -2528,6 +2733,20 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
         e = hipMalloc((void**)&d->d_pub, sizeof(gsim_msg) * (size_t)cap);
         if (e != hipSuccess) { d->pub_cap = 0; return hip_check(h, e, "hipMalloc publish"); }
         d->pub_cap = cap;
+    }
+    if (!d->lat_on && std::any_of(msgs, msgs + count, [](const gsim_msg& x) { return x.vdelay != 0; })) {
+        // first message with a validation latency: the pending-copy queues
+        // (each plane holds the copies of at most GSIM_MAX_VDELAY rounds;
+        // gsim_msg_config.max_arrivals raises it)
+        const int w = nnew_words(d);
+        d->vq_cap = std::max<int64_t>(std::max<int64_t>(4 * h->e, 1 << 16), d->cfg.max_arrivals);
+        e = hipMalloc((void**)&d->d_vq, sizeof(uint64_t) * (size_t)kVqPlanes * (size_t)d->vq_cap);
+        if (e == hipSuccess) e = hipMalloc((void**)&d->d_vqn, sizeof(uint32_t) * (kVqPlanes + 1));
+        if (e == hipSuccess) e = hipMalloc((void**)&d->d_hist, sizeof(uint32_t) * (size_t)kVqPlanes * (size_t)w);
+        if (e == hipSuccess) e = hipMemsetAsync(d->d_vqn, 0, sizeof(uint32_t) * (kVqPlanes + 1), h->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(d->d_hist, 0, sizeof(uint32_t) * (size_t)kVqPlanes * (size_t)w, h->stream);
+        if (e != hipSuccess) return hip_check(h, e, "validation queues");
+        d->lat_on = true;
     }
     e = hipMemcpyAsync(d->d_pub, msgs, sizeof(gsim_msg) * (size_t)count, hipMemcpyHostToDevice, h->stream);
     if (e != hipSuccess) return hip_check(h, e, "publish upload");
@@ -2556,6 +2775,7 @@ int gsim_round(gsim_handle* h, int64_t round)
     if (!rc) rc = deliver_round_post(h, round);
     if (!rc) rc = deliver_round_control(h, round);
     if (!rc) rc = deliver_round_ihave(h, round);
+    if (!rc) rc = deliver_round_validate(h, round);
     if (rc) return rc;
     deliver_round_end(h, round);
     return GSIM_OK;
@@ -2575,6 +2795,7 @@ int gsim_msg_stats(gsim_handle* h, int64_t* out4)
     if (e != hipSuccess) return hip_check(h, e, "gsim_msg_stats");
     for (int k = 0; k < 4; ++k) out4[k] = (int64_t)s[k];
     if (err[1]) { h->err = "IWANT responses overflowed their queue (raise gsim_msg_config.max_arrivals)"; return GSIM_ERANGE; }
+    if (int rc = vq_check(h)) return rc;
     if (err[2]) {
         h->err = "a ring slot was republished while its message could still be gossiped or promised (raise ring)";
         return GSIM_ESTATE;

@@ -387,8 +387,12 @@ struct TraceView {
     const uint8_t* minv;
     const uint64_t* mid;
     int32_t ring, rounds;
+    const uint8_t* mlat;        // validation latencies (nullptr: all 0)
+    int64_t t0, hb;             // round times (RoundArgs)
+    const int64_t* roff;
 };
 bool deliver_trace_view(gsim_handle* h, TraceView* v);
+int64_t deliver_last_round_time(gsim_handle* h);   // time of the last round run (INT64_MAX: none yet)
 void trace_release(gsim_handle* h);   // trace.hip
 // round stages (deliver.hip; gsim_round runs them in order, a sharded group
 // exchanges between them, shard.hip)

@@ -39,9 +39,16 @@ __global__ __launch_bounds__(256) void k_trace_resolve(gsim_trace_event* ev, int
         const int64_t fr = c == kUnseen64 ? -1 : (int64_t)(c >> 32);
         const uint32_t from = (uint32_t)c & kPeerMask;
         const uint8_t vd = v.minv[m];
-        if (fr == g && from == x.other) {
+        // a validation latency L: seen in round fr - L, verdict traced when
+        // validation completes in round fr (validation.go:334-341)
+        const int64_t L = v.mlat ? v.mlat[m] : 0;
+        if (fr >= 0 && fr - L == g && from == x.other) {
             x.type = vd == GSIM_VERDICT_ACCEPT ? GSIM_TRACE_DELIVER_MESSAGE : GSIM_TRACE_REJECT_MESSAGE;
             x.reason = vd == GSIM_VERDICT_ACCEPT ? 0 : vd;
+            if (L) {
+                const int64_t q = fr / v.rounds;
+                x.timestamp_ns = v.t0 + q * v.hb + v.roff[fr - q * v.rounds];
+            }
         } else {
             x.type = GSIM_TRACE_DUPLICATE_MESSAGE;
             x.reason = 0;
@@ -134,9 +141,21 @@ int gsim_trace_read(gsim_handle* h, gsim_trace_event* out, int64_t cap, int64_t*
         if (e == hipSuccess)
             e = hipMemcpyAsync(out, h->trace.ev, sizeof(gsim_trace_event) * cnt, hipMemcpyDeviceToHost, h->stream);
     }
-    if (e == hipSuccess) e = hipMemsetAsync(h->trace.n, 0, sizeof(uint32_t), h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return hip_check(h, e, "gsim_trace_read");
+    // a first reception whose validation completes after the last round run
+    // (gsim_msg.vdelay) is traced when it completes: its resolved event stays
+    // in the buffer for a later read
+    const int64_t tlast = deliver_last_round_time(h);
+    gsim_trace_event* mid = std::stable_partition(out, out + cnt,
+                                                  [tlast](const gsim_trace_event& x) { return x.timestamp_ns <= tlast; });
+    const uint32_t keep = (uint32_t)(out + cnt - mid);
+    if (keep) e = hipMemcpyAsync(h->trace.ev, mid, sizeof(gsim_trace_event) * keep, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h->trace.n, &keep, sizeof(uint32_t), hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "gsim_trace_read");
+    cnt -= keep;
+    *n = cnt;
     std::sort(out, out + cnt, [](const gsim_trace_event& a, const gsim_trace_event& b) {
         return std::tie(a.timestamp_ns, a.peer, a.type, a.other, a.topic, a.msg_id) <
                std::tie(b.timestamp_ns, b.peer, b.type, b.other, b.topic, b.msg_id);

@@ -99,11 +99,13 @@ class CMsgConfig(Structure):
 
 class CMsg(Structure):
     _fields_ = [("id", c_uint64), ("topic", c_uint32), ("origin", c_uint32), ("verdict", ctypes.c_uint8),
-                ("_pad", ctypes.c_uint8 * 7)]
+                ("vdelay", ctypes.c_uint8), ("_pad", ctypes.c_uint8 * 6)]
 
 
 # numpy view of gsim_msg (24 bytes)
-MSG_DTYPE = [("id", "<u8"), ("topic", "<u4"), ("origin", "<u4"), ("verdict", "u1"), ("_pad", "u1", (7,))]
+MSG_DTYPE = [("id", "<u8"), ("topic", "<u4"), ("origin", "<u4"), ("verdict", "u1"), ("vdelay", "u1"),
+             ("_pad", "u1", (6,))]
+MAX_VDELAY = 7          # gsim.h GSIM_MAX_VDELAY
 # gsim.h GSIM_VERDICT_*: the validation verdict of a message at every receiver
 VERDICT_ACCEPT, VERDICT_REJECT, VERDICT_IGNORE, VERDICT_THROTTLE, VERDICT_SIGNATURE = 0, 1, 2, 3, 4
 

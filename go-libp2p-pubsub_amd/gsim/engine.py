@@ -269,11 +269,14 @@ class Engine:
         return c.t0_ns + (g // c.rounds) * c.heartbeat_ns + (g % c.rounds + 1) * c.heartbeat_ns // (c.rounds + 1)
 
     def publish(self, msgs, rnd: int):
-        """Topic.Publish of each (id, topic, origin, verdict) at its origin in round `rnd`
-        (verdict: _abi.VERDICT_*, the validation result at every receiver)."""
+        """Topic.Publish of each (id, topic, origin, verdict[, vdelay]) at its origin in
+        round `rnd` (verdict: _abi.VERDICT_*, the validation result at every receiver;
+        vdelay: the validation latency at every receiver in rounds, gsim_msg.vdelay)."""
         arr = np.zeros(len(msgs), dtype=_abi.MSG_DTYPE)
-        for k, (mid, topic, origin, verdict) in enumerate(msgs):
+        for k, msg in enumerate(msgs):
+            mid, topic, origin, verdict = msg[:4]
             arr[k]["id"], arr[k]["topic"], arr[k]["origin"], arr[k]["verdict"] = mid, topic, origin, verdict
+            arr[k]["vdelay"] = msg[4] if len(msg) > 4 else 0
         self._check(self.lib.gsim_publish(self.h, _ptr(arr), len(arr), int(rnd)))
 
     def publish_array(self, arr: np.ndarray, rnd: int):

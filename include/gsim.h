@@ -305,8 +305,16 @@ typedef struct gsim_msg {
     uint32_t topic;          /* dense topic index */
     uint32_t origin;         /* publishing peer (must be subscribed) */
     uint8_t  verdict;        /* GSIM_VERDICT_* at every receiver */
-    uint8_t  _pad[7];
+    uint8_t  vdelay;         /* validation latency at every receiver, in rounds (0..GSIM_MAX_VDELAY):
+                                async validation (validation.go:246-407) — a receiver that first sees
+                                the message in round g marks it seen then, and its Deliver/Reject
+                                verdict, mcache.Put and forwarding happen at round g + vdelay; copies
+                                arriving meanwhile are pending duplicates (score.go:719-725, 806-809).
+                                Needs the topic-major delivery on a single engine (not a shard). */
+    uint8_t  _pad[6];
 } gsim_msg;
+
+#define GSIM_MAX_VDELAY 7
 
 /* Allocate the message ring and seen-set (after load_graph). */
 int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg);

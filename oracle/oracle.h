@@ -90,6 +90,16 @@ int64_t orc_round_time(const orc_msgs* m, int64_t g);
  * round g+1. */
 void orc_publish(orc_net* s, orc_msgs* m, uint64_t id, uint32_t topic, uint32_t origin, uint8_t invalid,
                  int64_t g);
+/* orc_publish with a validation latency of `vdelay` rounds at every receiver
+ * (async validation, validation.go:246-407): a receiver that first sees the
+ * message in round g marks it seen and fulfils its promises then, but its
+ * Deliver/RejectMessage (score.go:702-793), mcache.Put and forwarding happen
+ * at the start of round c = g + vdelay (forwarding in round c + 1); copies
+ * arriving in rounds [g, c) are pending duplicates, credited (or penalised)
+ * at c with validated zero (score.go:719-725, 807-811); later copies are
+ * duplicates validated at round c.  seen[] holds c. */
+void orc_publish_v(orc_net* s, orc_msgs* m, uint64_t id, uint32_t topic, uint32_t origin, uint8_t invalid,
+                   uint8_t vdelay, int64_t g);
 /* One propagation round g: every peer that first saw (or published) a
  * message in round g-1 forwards it to its current mesh peers except the
  * sender and the origin (Publish, gossipsub.go:975-1045); receivers process

@@ -101,6 +101,8 @@ void orc_msgs_free_priv(orc_msgs* m)
     free(p->cappr);
     free(p->tx);
     free(p->slot_last);
+    free(p->vd);
+    free(p->pq);
     free(p->cand);
     free(p->cand_ptr);
     free(p);
@@ -127,6 +129,16 @@ static void ar_push(priv* p, uint32_t recv, uint32_t slot, uint32_t er)
     p->nar++;
 }
 
+static void pq_push(priv* p, int64_t c, uint32_t recv, uint32_t slot, uint32_t er, int32_t first)
+{
+    if (p->npq == p->cappq) {
+        p->cappq = p->cappq ? 2 * p->cappq : 1024;
+        p->pq = (pend_ent*)realloc(p->pq, sizeof(pend_ent) * (size_t)p->cappq);
+    }
+    pend_ent* x = &p->pq[p->npq++];
+    x->c = c; x->recv = recv; x->slot = slot; x->er = er; x->first = first;
+}
+
 static int cmp_arr(const void* a, const void* b)
 {
     const arr_ent* x = (const arr_ent*)a;
@@ -145,7 +157,18 @@ int64_t orc_round_time(const orc_msgs* m, int64_t g)
 void orc_publish(orc_net* s, orc_msgs* m, uint64_t id, uint32_t topic, uint32_t origin, uint8_t invalid,
                  int64_t g)
 {
+    orc_publish_v(s, m, id, topic, origin, invalid, 0, g);
+}
+
+void orc_publish_v(orc_net* s, orc_msgs* m, uint64_t id, uint32_t topic, uint32_t origin, uint8_t invalid,
+                   uint8_t vdelay, int64_t g)
+{
     const uint32_t slot = (uint32_t)(id % (uint64_t)m->ring);
+    {
+        priv* pv = P(m);
+        if (!pv->vd) pv->vd = (uint8_t*)calloc((size_t)m->ring, 1);
+        pv->vd[slot] = vdelay;
+    }
     m->topic[slot] = topic;
     m->origin[slot] = origin;
     m->invalid[slot] = invalid;
@@ -175,11 +198,45 @@ void orc_publish(orc_net* s, orc_msgs* m, uint64_t id, uint32_t topic, uint32_t 
     fr_push(P(m), origin, slot, origin);
 }
 
+/* Validations completing at the start of round g (orc_publish_v): the first
+ * copy's DeliverMessage (markFirstMessageDelivery, then every pending peer's
+ * markDuplicateMessageDelivery with validated zero, score.go:702-726) or
+ * RejectMessage (score.go:728-793: markInvalidMessageDelivery for the first
+ * and every pending peer; ignored / throttled: nothing), mcache.Put and
+ * forwarding in round g + 1 (validation.go:334-341, pubsub.go:1159-1161). */
+static void complete_validations(orc_net* s, orc_msgs* m, int64_t g, int64_t now)
+{
+    priv* p = P(m);
+    int64_t keep = 0;
+    for (int64_t q = 0; q < p->npq; ++q) {
+        const pend_ent x = p->pq[q];
+        if (x.c != g) { p->pq[keep++] = x; continue; }
+        const int32_t t = (int32_t)m->topic[x.slot];
+        const uint8_t verdict = m->invalid[x.slot];
+        if (verdict == GSIM_VERDICT_REJECT) orc_mark_invalid(s, x.er, t);
+        else if (verdict == GSIM_VERDICT_ACCEPT) {
+            if (x.first) orc_mark_first(s, x.er, t);
+            else orc_mark_duplicate(s, x.er, t, 0, 0, now);
+        }
+        if (!x.first) continue;
+        if (p->slot_last && p->slot_last[x.slot] < g) p->slot_last[x.slot] = g;
+        orc_log(m, ORC_EV_SEEN, x.recv, s->col[x.er], x.slot, t, g, 1);
+        if (verdict == GSIM_VERDICT_ACCEPT) {
+            m->lastput[(int64_t)t * s->n + x.recv] = (int32_t)(g / m->rounds);
+            orc_log(m, ORC_EV_PUT, x.recv, 0, x.slot, t, g, 0);
+            fr_push(p, x.recv, x.slot, s->col[x.er]);
+        }
+    }
+    p->npq = keep;
+}
+
 void orc_round(orc_net* s, orc_msgs* m, int64_t g)
 {
     priv* p = P(m);
     const int64_t now = orc_round_time(m, g);
     const double gray = s->th->graylist_threshold;
+
+    if (p->npq) complete_validations(s, m, g, now);
 
     /* 1. last round's first receivers (and publishers) forward to their mesh */
     for (int64_t q = 0; q < p->nfp; ++q) {
@@ -236,8 +293,22 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
             orc_log(m, ORC_EV_REJECT_SIG, i, s->col[er], slot, t, g, 0);
             continue;
         }
-        orc_log(m, ORC_EV_SEEN, i, s->col[er], slot, t, g, *cell == UNSEEN);
-        if (*cell == UNSEEN) {
+        const uint8_t vdelay = p->vd ? p->vd[slot] : 0;
+        if (!vdelay || *cell != UNSEEN) orc_log(m, ORC_EV_SEEN, i, s->col[er], slot, t, g, *cell == UNSEEN);
+        if (*cell == UNSEEN && vdelay) {
+            /* markSeen + ValidateMessage (promises fulfilled); the verdict
+             * lands vdelay rounds later (complete_validations) */
+            *cell = (uint32_t)(g + vdelay);
+            m->stats[1]++;
+            orc_gossip_fulfill(m, i, slot);
+            if (p->slot_last) p->slot_last[slot] = g;
+            pq_push(p, g + vdelay, i, slot, er, 1);
+        } else if (*cell != UNSEEN && (int64_t)*cell > g) {
+            /* DuplicateMessage while the first copy validates
+             * (deliveryUnknown: drec.peers, score.go:806-809) */
+            m->stats[2]++;
+            if (verdict == GSIM_VERDICT_REJECT || verdict == GSIM_VERDICT_ACCEPT) pq_push(p, *cell, i, slot, er, 0);
+        } else if (*cell == UNSEEN) {
             *cell = (uint32_t)g;               /* markSeen */
             m->stats[1]++;
             orc_gossip_fulfill(m, i, slot);    /* gossipTracer: promises for it are kept */

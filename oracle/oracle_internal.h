@@ -35,6 +35,9 @@ static inline uint64_t okey(uint64_t seed, uint64_t tick, uint32_t obs, int32_t 
 
 typedef struct fr_ent { uint32_t peer, slot, from; } fr_ent;
 typedef struct arr_ent { uint32_t recv, slot, er; } arr_ent;
+/* a copy whose receiver is still validating the message: credited or
+ * penalised when validation completes in round c (orc_publish_v) */
+typedef struct pend_ent { int64_t c; uint32_t recv, slot, er; int32_t first; } pend_ent;
 
 /* one outstanding IWANT promise of a receiver (gossip_tracer.go:21-27) */
 typedef struct promise { uint32_t e; uint32_t slot; uint64_t mid; int64_t expire; } promise;
@@ -59,6 +62,8 @@ typedef struct priv {
     int64_t n_alloc, te_alloc;
     int64_t* slot_last;                 /* [ring] last round with a first reception (or the publication) */
     uint32_t* cand; int32_t* cand_ptr;  /* per-topic recent slots at the current heartbeat (CSR) */
+    uint8_t* vd;                        /* [ring] validation latency of the slot's message, rounds */
+    pend_ent* pq; int64_t npq, cappq;   /* copies pending validation */
     int32_t log_on;                     /* event log (orc_msgs_log) */
     orc_event* ev; int64_t nev, capev;
 } priv;

@@ -108,6 +108,8 @@ def load():
             "orc_handle_control": (c_int64, [P, c_int32, c_int64]),
             "orc_round_time": (c_int64, [POINTER(OrcMsgs), c_int64]),
             "orc_publish": (None, [P, POINTER(OrcMsgs), c_uint64, c_uint32, c_uint32, ctypes.c_uint8, c_int64]),
+            "orc_publish_v": (None, [P, POINTER(OrcMsgs), c_uint64, c_uint32, c_uint32, ctypes.c_uint8, ctypes.c_uint8,
+                                     c_int64]),
             "orc_round": (None, [P, POINTER(OrcMsgs), c_int64]),
             "orc_msgs_free_priv": (None, [POINTER(OrcMsgs)]),
             "orc_heartbeat_gossip": (None, [P, POINTER(OrcMsgs), c_uint64, c_int64, c_uint64]),
@@ -263,8 +265,9 @@ class Msgs:
     def round_time(self, g):
         return load().orc_round_time(ctypes.byref(self.m), g)
 
-    def publish(self, st, mid, topic, origin, invalid, g):
-        load().orc_publish(st.view(), ctypes.byref(self.m), mid, topic, origin, invalid, g)
+    def publish(self, st, mid, topic, origin, invalid, g, vdelay=0):
+        """orc_publish_v: vdelay = validation latency in rounds at every receiver."""
+        load().orc_publish_v(st.view(), ctypes.byref(self.m), mid, topic, origin, invalid, vdelay, g)
 
     def round(self, st, g):
         load().orc_round(st.view(), ctypes.byref(self.m), g)

@@ -1,0 +1,125 @@
+"""Validation latency and near-first crediting:
+async validation windows (validation.go:246-407) with pending-duplicate
+crediting (score.go:719-725, 806-811).
+
+A message carries a validation latency of L rounds (gsim_msg.vdelay) at every
+receiver.  A receiver that first sees it in round g marks it seen and fulfils
+its IWANT promises then (ValidateMessage, gossip_tracer.go:163-168); its
+verdict lands at the start of round g + L: DeliverMessage's
+markFirstMessageDelivery for the first sender, markDuplicateMessageDelivery
+with validated zero — so no window check — for every peer whose copy arrived
+meanwhile (drec.peers), or RejectMessage's penalty for all of them; the
+mcache.Put and forwarding follow (forwarded in round g + L + 1).  Copies
+arriving from round g + L on are duplicates validated at round g + L.
+
+CPU part: properties of the oracle's restatement against its own L = 0 run on
+a fixed mesh (no heartbeat): every first reception is L rounds later per hop,
+and the set of credited copies — hence every counter — is the same for a
+window that credits every duplicate and for one that credits only same-round
+copies.  GPU part: the engine bit-exact against the oracle through ticks with
+gossip, every verdict, churn and the trace, for latencies 0-3 mixed."""
+import numpy as np
+import pytest
+
+import oracle_binding as ob
+from gsim import _abi
+from gsim.engine import Engine, random_regular
+from gsim.params import GossipSubParams, PeerScoreThresholds, Second
+from gsim.presets import beacon_params, beacon_topic
+from test_delivery import R, T0
+from test_heartbeat import tick_time
+
+TH = PeerScoreThresholds(GossipThreshold=-2000, PublishThreshold=-4000, GraylistThreshold=-8000)
+GP = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2)
+
+
+def _params(T, window):
+    p = beacon_params(T)
+    for t in range(T):
+        p.Topics[f"topic{t:02d}"] = beacon_topic(MeshMessageDeliveriesWindow=window)
+    return p
+
+
+def _oracle_run(L, verdict, window, seed=5):
+    """One message from peer 0 on a fixed mesh, rounds only (no heartbeat, so
+    no mesh change): the oracle's seen rounds and score counters."""
+    from fixtures import synthetic_state
+    net = random_regular(400, 10, seed=seed, n_topics=1)
+    params = _params(1, window)
+    st = ob.NetState(net, params, thresholds=TH, gossip=GP)
+    synthetic_state(st, np.random.default_rng(seed), tick_time(0), 0.7)
+    st.first[:] = 0.0
+    st.meshd[:] = 0.0
+    st.invalid[:] = 0.0
+    msgs = ob.Msgs(net.n, 1, 64, R, T0, Second)
+    g0 = 3 * R + 2
+    msgs.publish(st, 0, 0, 0, verdict, g0, vdelay=L)
+    for g in range(g0, g0 + 12 * (L + 1) + 2):
+        msgs.round(st, g)
+    return msgs.seen[0].astype(np.int64), st.first.copy(), st.meshd.copy(), st.invalid.copy(), g0
+
+
+@pytest.mark.parametrize("L", [1, 3])
+@pytest.mark.parametrize("window", [3600 * Second, 1])
+def test_oracle_latency_delays_each_hop(L, window):
+    s0, f0, m0, i0, g0 = _oracle_run(0, _abi.VERDICT_ACCEPT, window)
+    sL, fL, mL, iL, _ = _oracle_run(L, _abi.VERDICT_ACCEPT, window)
+    reached = s0 != _abi.UNSEEN
+    assert reached.sum() > 300
+    assert np.array_equal(reached, sL != _abi.UNSEEN)
+    # hop h: seen at g0 + h without latency, validated at g0 + h (L + 1) with it
+    assert np.array_equal(sL[reached] - g0, (s0[reached] - g0) * (L + 1))
+    # the same first senders and the same credited copies
+    assert np.array_equal(f0, fL) and f0.sum() > 300
+    assert np.array_equal(m0, mL) and m0.sum() > 0
+    assert not i0.any() and not iL.any()
+
+
+def test_oracle_latency_reject_and_ignore():
+    """A rejected message penalises its first copy and every copy that arrived
+    while it was validated; an ignored one changes nothing."""
+    for verdict in (_abi.VERDICT_REJECT, _abi.VERDICT_IGNORE):
+        s0, f0, m0, i0, _ = _oracle_run(0, verdict, 3600 * Second)
+        sL, fL, mL, iL, g0 = _oracle_run(2, verdict, 3600 * Second)
+        assert np.array_equal(i0, iL)
+        assert not fL.any() and not mL.any()
+        assert (iL.sum() > 0) == (verdict == _abi.VERDICT_REJECT)
+        # not forwarded: only the origin's mesh sees it, L rounds later validated
+        recv = (s0 != _abi.UNSEEN) & (s0 != g0)
+        assert recv.sum() > 0 and np.array_equal(sL != _abi.UNSEEN, s0 != _abi.UNSEEN)
+        assert np.array_equal(sL[recv], s0[recv] + 2) and sL[0] == g0
+
+
+@pytest.mark.gpu
+def test_publish_rejects_bad_vdelay(require_gpu):
+    eng = Engine(beacon_params(1), TH, gossip=GP)
+    try:
+        eng.load_graph(random_regular(200, 8, seed=3, n_topics=1))
+        eng.msgs_init(64, R, T0, Second)
+        with pytest.raises(Exception, match="vdelay"):
+            eng.publish([(1, 0, 0, 0, _abi.MAX_VDELAY + 1)], 0)
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("window,trace", [(5 * 60 * Second, None), (100_000_000, (0, 700))])
+def test_validation_latency_bit_exact(require_gpu, window, trace):
+    from fixtures import synthetic_state
+    from tickrun import run_parity, subscribed_schedule
+    rng = np.random.default_rng(41)
+    n, k, T = 1500, 16, 3
+    params = _params(T, window)
+    net = random_regular(n, k, seed=43, n_topics=T)
+    st = ob.NetState(net, params, thresholds=TH, gossip=GP)
+    synthetic_state(st, rng, tick_time(0), 0.6)
+    ticks = list(range(1, 6))
+    sched = subscribed_schedule(rng, ticks, net, T, 4.0, 0.0, verdicts=(0.7, 0.1, 0.1, 0.05, 0.05),
+                                vdelays=(0, 1, 2, 3))
+    src = net.owner()
+    und = np.stack([src, net.col], axis=1)
+    und = und[und[:, 0] < und[:, 1]]
+    down = und[rng.choice(len(und), size=len(und) // 40, replace=False)]
+    churn = {3: [(down, False)], 5: [(down, True)]}
+    msgs, gstats = run_parity(net, params, TH, GP, st, ticks, sched, ring=512, churn=churn, trace=trace)
+    assert msgs.stats[1] > 0 and gstats["iwant_ids"] > 0, "first deliveries and IWANTs happened"

@@ -105,8 +105,9 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
             if after_heartbeat:
                 after_heartbeat(kk, eng, st, msgs)
             for g in range(kk * R, kk * R + R):
-                for (mid, t, o, inv) in sched.get(g, []):
-                    msgs.publish(st, mid, t, o, inv, g)
+                for msg in sched.get(g, []):
+                    mid, t, o, inv = msg[:4]
+                    msgs.publish(st, mid, t, o, inv, g, vdelay=msg[4] if len(msg) > 4 else 0)
                 if g in sched:
                     eng.publish(sched[g], g)
                 msgs.round(st, g)
@@ -138,11 +139,13 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
         eng.close()
 
 
-def subscribed_schedule(rng, ticks, net, T, rate, inv_frac, member_only=True, verdicts=None):
+def subscribed_schedule(rng, ticks, net, T, rate, inv_frac, member_only=True, verdicts=None, vdelays=None):
     """Poisson(rate) publications per topic per tick at uniform rounds; the
     origin is a uniform member of the topic (or any peer).  The verdict is
     reject with probability inv_frac, or drawn from `verdicts` (probabilities
-    of accept / reject / ignore / throttle / signature) when given."""
+    of accept / reject / ignore / throttle / signature) when given.  vdelays:
+    validation latencies (rounds) drawn uniformly per message, as a fifth
+    tuple element (gsim_msg.vdelay)."""
     sched, mid = {}, 0
     members = [np.nonzero((net.sub >> np.uint64(t)) & np.uint64(1))[0] for t in range(T)]
     for k in ticks:
@@ -155,7 +158,10 @@ def subscribed_schedule(rng, ticks, net, T, rate, inv_frac, member_only=True, ve
                     o = int(pool[rng.integers(0, len(pool))])
                     v = (int(rng.choice(len(verdicts), p=verdicts)) if verdicts is not None
                          else int(rng.random() < inv_frac))
-                    batch.append((mid, t, o, v))
+                    if vdelays is not None:
+                        batch.append((mid, t, o, v, int(vdelays[rng.integers(0, len(vdelays))])))
+                    else:
+                        batch.append((mid, t, o, v))
                     mid += 1
             if batch:
                 sched[g] = batch
