@@ -123,3 +123,83 @@ def test_validation_latency_bit_exact(require_gpu, window, trace):
     churn = {3: [(down, False)], 5: [(down, True)]}
     msgs, gstats = run_parity(net, params, TH, GP, st, ticks, sched, ring=512, churn=churn, trace=trace)
     assert msgs.stats[1] > 0 and gstats["iwant_ids"] > 0, "first deliveries and IWANTs happened"
+
+
+# RejectMessage reasons of each verdict (tracer.go:28-38, oracle.h ORC_REJECT_*)
+_REASON = {_abi.VERDICT_REJECT: 8, _abi.VERDICT_IGNORE: 9, _abi.VERDICT_THROTTLE: 7}
+
+
+@pytest.mark.parametrize("L", [0, 2])
+def test_latency_follows_the_pinned_score_tracer(L):
+    """The network oracle's crediting equals the KAT-pinned per-observer score
+    tracer (oracle.c's delivery records, score_test.go) driven by the same
+    copies in Go's call order: ValidateMessage at the first reception,
+    DuplicateMessage at every later copy, Deliver/RejectMessage when the
+    validation completes — for every receiver, with a window (150 ms) that
+    credits some later duplicates and not others."""
+    from fixtures import synthetic_state
+    net = random_regular(300, 10, seed=9, n_topics=1)
+    params = _params(1, 150_000_000)
+    lib = ob.load()
+
+    def state():
+        st = ob.NetState(net, params, thresholds=TH, gossip=GP)
+        synthetic_state(st, np.random.default_rng(9), tick_time(0), 0.7)
+        for f in (st.first, st.meshd, st.invalid):
+            f[:] = 0.0
+        return st
+
+    st, replay = state(), state()
+    assert np.array_equal(st.tflags, replay.tflags)
+    msgs = ob.Msgs(net.n, 1, 64, R, T0, Second)
+    msgs.log()
+    g0 = 2 * R + 3
+    pubs = {g0: (0, 5, _abi.VERDICT_ACCEPT), g0 + 1: (1, 77, _abi.VERDICT_REJECT),
+            g0 + 2: (2, 150, _abi.VERDICT_ACCEPT), g0 + 4: (3, 201, _abi.VERDICT_IGNORE),
+            g0 + 5: (4, 260, _abi.VERDICT_THROTTLE), g0 + 6: (5, 33, _abi.VERDICT_ACCEPT)}
+    verdict = {mid: v for (mid, _, v) in pubs.values()}
+    for g in range(g0, g0 + 40):
+        if g in pubs:
+            mid, origin, v = pubs[g]
+            msgs.publish(st, mid, 0, origin, v, g, vdelay=L)
+        msgs.round(st, g)
+    ev = msgs.events()
+    seen = ev[(ev["kind"] == ob.EV_SEEN) & (ev["b"] != 0xFFFFFFFF)]
+    assert len(seen) > 1000
+
+    def edge(a, b):
+        lo, hi = int(net.row_ptr[a]), int(net.row_ptr[a + 1])
+        return lo + int(np.nonzero(net.col[lo:hi] == b)[0][0])
+
+    # (round, phase, receiver, ...): completions open a round (phase 0; with
+    # no latency right after the first reception, 1.5), then first
+    # receptions (1), then duplicates (2)
+    acts = []
+    for e in seen:
+        a, b, g, mid = int(e["a"]), int(e["b"]), int(e["g"]), int(e["mid"])
+        if int(e["x"]):
+            acts.append((g - L, 1, a, b, mid, "validate"))
+            acts.append((g, 0 if L else 1.5, a, b, mid, "complete"))
+        else:
+            acts.append((g, 2, a, b, mid, "duplicate"))
+    acts.sort(key=lambda x: (x[0], x[1], x[2], x[4], x[3]))
+    v = replay.view()
+    drecs = {}
+    try:
+        for (g, _, a, b, mid, what) in acts:
+            d = drecs.setdefault(a, lib.orc_drecs_new(int(params.SeenMsgTTL)))
+            now = msgs.round_time(g)
+            if what == "validate":
+                lib.orc_validate_message(v, d, mid, now)
+            elif what == "duplicate":
+                lib.orc_duplicate_message(v, d, edge(a, b), mid, 0, now)
+            elif verdict[mid] == _abi.VERDICT_ACCEPT:
+                lib.orc_deliver_message(v, d, edge(a, b), mid, 0, now)
+            else:
+                lib.orc_reject_message(v, d, edge(a, b), mid, 0, _REASON[verdict[mid]], now)
+    finally:
+        for d in drecs.values():
+            lib.orc_drecs_free(d)
+    for f in ("first", "meshd", "invalid"):
+        assert np.array_equal(getattr(st, f), getattr(replay, f)), f
+    assert st.first.sum() > 0 and st.meshd.sum() > 0 and st.invalid.sum() > 0
