@@ -264,21 +264,27 @@ __device__ __forceinline__ int active_slots(const uint32_t* nnew, int ring, uint
 
 // Commit one claimed cell of round gc (markSeen + the winner's P2/P3 credit,
 // markFirstMessageDelivery score.go:919-946; mcache.Put for lastput).
-template <bool ATOMIC = false>
+template <bool ATOMIC = false, bool LAT = false>
 __device__ __forceinline__ void commit_claim(const RoundArgs& a, uint64_t* cellp, uint64_t c, int64_t gc,
                                              uint32_t m, int64_t peer)
 {
     const uint32_t hi = (uint32_t)(c >> 32), lo = (uint32_t)c;
-    const uint32_t L = a.mlat ? a.mlat[m] : 0u;
-    *cellp = ((uint64_t)(uint32_t)(gc + L) << 32) | (lo & kPeerMask);
-    const int32_t t = (int32_t)a.mtopic[m];
-    if (L) {
-        // validation completes in round gc + L: the winner's DeliverMessage
-        // credit lands there (k_vq_apply), the put and forwarding after it
-        if (a.minv[m] == GSIM_VERDICT_ACCEPT && const_tp(a.tp)[t].scored) vq_push(a, gc + L, hi & kEdgeMask, t, kVqFirst);
-        return;
+    if constexpr (LAT) {
+        const uint32_t L = a.mlat[m];
+        *cellp = ((uint64_t)(uint32_t)(gc + L) << 32) | (lo & kPeerMask);
+        if (L) {
+            // validation completes in round gc + L: the winner's DeliverMessage
+            // credit lands there (k_vq_apply), the put and forwarding after it
+            const int32_t t = (int32_t)a.mtopic[m];
+            if (a.minv[m] == GSIM_VERDICT_ACCEPT && const_tp(a.tp)[t].scored)
+                vq_push(a, gc + L, hi & kEdgeMask, t, kVqFirst);
+            return;
+        }
+    } else {
+        *cellp = ((uint64_t)(uint32_t)gc << 32) | (lo & kPeerMask);
     }
     if (a.minv[m]) return;                                // RejectMessage: counted when sent
+    const int32_t t = (int32_t)a.mtopic[m];
     int32_t* lp = a.lastput + (int64_t)t * a.N + peer;
     const int32_t tick = (int32_t)(gc / a.R);
     if (ATOMIC) atomicMax(lp, tick); else if (*lp < tick) *lp = tick;
@@ -330,7 +336,10 @@ __global__ void k_reset_slots(RoundArgs a, const gsim_msg* pub, int32_t count)
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.CN; i += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t c = row[i];
         // several reused rows may credit one record: atomic updates here
-        if (a.g > 0 && is_claim_of(c, q)) commit_claim<true>(a, row + i, c, a.g - 1, m, a.clo + i);
+        if (a.g > 0 && is_claim_of(c, q)) {
+            if (a.mlat) commit_claim<true, true>(a, row + i, c, a.g - 1, m, a.clo + i);
+            else commit_claim<true>(a, row + i, c, a.g - 1, m, a.clo + i);
+        }
         row[i] = kUnseen64;
         if ((i & 63) == 0) {
             a.seenbm[(int64_t)m * a.nw + (i >> 6)] = 0;
@@ -708,7 +717,7 @@ constexpr int kTsSlots = 64;
 constexpr uint32_t kTmWin = 8192;   // flattened edges whose senders are tabled in LDS at once
 constexpr int kTmTabMin = 256;      // forwarders in a chunk from which the table pays for its fill
 
-template <int kTmThreads>
+template <int kTmThreads, bool LAT>
 __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs a)
 {
     extern __shared__ uint64_t s_dyn[];
@@ -772,7 +781,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
             s_vd[tid] = a.minv[m];
             s_ow[tid] = (origin < a.N && ((a.sub[origin] >> t) & 1ull)) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
             s_wa[tid] = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
-            s_lat[tid] = a.mlat ? a.mlat[m] : 0;
+            if (LAT) s_lat[tid] = a.mlat[m];
         }
         if (tid == 0) s_clm = 0;
         uint64_t clm = 0;
@@ -972,7 +981,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                                 a.tr.push(round_time(a, a.g), ((uint64_t)a.g << 32) | m, i, j, t,
                                           seeable ? kTraceCopy : (uint8_t)GSIM_TRACE_REJECT_MESSAGE, vd);
                             const bool sc = scored_t && (ds & GSIM_DS_TRACKED);
-                            const uint32_t L = s_lat[k];
+                            const uint32_t L = LAT ? s_lat[k] : 0u;
                             const uint64_t* s_bm = a.seenbm + (int64_t)m * a.nw + wlo;
                             const int64_t bw = ((int64_t)i >> 6) - wlo;
                             // a committed cell need not be read when the copy cannot be
@@ -1069,6 +1078,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
 
 // Commit every claim of round g (markSeen + P2 credit) before the state is
 // read or changed by anything but the next round.
+template <bool LAT>
 __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
 {
     extern __shared__ uint16_t s_act[];
@@ -1096,7 +1106,7 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
                 const uint32_t m = s_act[k];
                 a.seenbm[(int64_t)m * a.nw + (i0 >> 6)] |= cb;
                 // receivers forward what they accepted, in the next round
-                if (a.fresh && a.minv[m] == GSIM_VERDICT_ACCEPT && !(a.mlat && a.mlat[m])) {
+                if (a.fresh && a.minv[m] == GSIM_VERDICT_ACCEPT && (!LAT || !a.mlat[m])) {
                     // fire-and-forget atomics: the wave does not wait on them
                     atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (i0 >> 6)), cb);
                     atomicOr(reinterpret_cast<unsigned long long*>(a.fsum + (int64_t)m * a.nsw + (i0 >> 12)),
@@ -1110,7 +1120,7 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
             if (k >= nact) break;
             if (is_claim_of(cv[b], par)) {
                 const uint32_t m = s_act[k];
-                commit_claim(a, a.cell + (int64_t)m * a.CN + i, cv[b], a.g, m, a.clo + i);
+                commit_claim<false, LAT>(a, a.cell + (int64_t)m * a.CN + i, cv[b], a.g, m, a.clo + i);
             }
         }
     }
@@ -1207,6 +1217,7 @@ __device__ __forceinline__ bool holds_in_window(uint64_t c, int64_t g, int32_t l
     return fr >= lo_round && fr < tick_round && (!inv || is_origin);
 }
 
+template <bool LAT>
 __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount)
 {
     extern __shared__ uint16_t s_act[];   // [ring] candidate slots, then [2][ring] u32 counters
@@ -1250,7 +1261,7 @@ __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount
             const uint32_t m = s_act[k];
             const int32_t t = (int32_t)a.mtopic[m];
             const bool hold = vp && holds_in_window(cv[b], a.g, a.lo_round, tick_round, a.minv[m] != 0,
-                                                   (uint32_t)pl == a.morigin[m], a.mlat ? a.mlat[m] : 0u);
+                                                   (uint32_t)pl == a.morigin[m], LAT ? a.mlat[m] : 0u);
             const bool want = vp && cv[b] == kUnseen64 && ((subp >> t) & 1ull) && pl >= a.rlo && pl < a.rhi;
             const int nh = __popcll(__ballot(hold)), nw = __popcll(__ballot(want));
             if (lane == 0 && nh) atomicAdd(&s_cnt[m], (uint32_t)nh);
@@ -1262,7 +1273,7 @@ __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount
         if (s_cnt[w]) atomicAdd(&gcount[w], s_cnt[w]);
 }
 
-template <int W>
+template <int W, bool LAT>
 __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
 {
     extern __shared__ uint16_t s_act[];   // [ring] candidate slots (bit 15: push), then response staging
@@ -1332,7 +1343,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
             // push: lanes are holders of m (its advertisers); pull: lanes are
             // receivers that joined t and have not seen m (handleIHave's seenMessage)
             const bool me = vp && (push ? holds_in_window(cv[b], a.g, a.lo_round, tick_round, inv, (uint32_t)pl == origin,
-                                                          a.mlat ? a.mlat[m] : 0u)
+                                                          LAT ? a.mlat[m] : 0u)
                                         : (cv[b] == kUnseen64 && ((subp >> t) & 1ull) && pl >= a.rlo && pl < a.rhi));
             const uint64_t mask = __ballot(me);
             if (!mask) continue;
@@ -1376,7 +1387,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                         if (a.gsel[plane + re] && a.gstate[e]) {
                             const uint32_t i = a.col[e];
                             req = holds_in_window(a.cell[row_m + (i - a.clo)], a.g, a.lo_round, tick_round, inv,
-                                                  i == origin, a.mlat ? a.mlat[m] : 0u);
+                                                  i == origin, LAT ? a.mlat[m] : 0u);
                             if (req) {
                                 const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, me_g, 0, P_PROMISE, m,
                                                               a.gid ? a.gid[i] : i);
@@ -1427,6 +1438,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
 // value (64 counting passes over the window: a path for rare, huge windows).
 constexpr int kPairTopics = 64;
 
+template <bool LAT>
 __global__ __launch_bounds__(256) void k_ihave_pairs(IhArgs a)
 {
     extern __shared__ uint16_t s_act[];   // [ring] window slots, then per wave: staging, tau[64], count[64]
@@ -1505,7 +1517,7 @@ __global__ __launch_bounds__(256) void k_ihave_pairs(IhArgs a)
             const uint32_t origin_ign = a.behaviour[i] & GSIM_BEHAVE_IGNORE_IWANT;
             auto holds = [&](uint32_t m) {
                 return holds_in_window(a.cell[(int64_t)m * a.CN + ic], a.g, a.lo_round, tick_round, a.minv[m] != 0,
-                                       i == a.morigin[m], a.mlat ? a.mlat[m] : 0u);
+                                       i == a.morigin[m], LAT ? a.mlat[m] : 0u);
             };
             // GetGossipIDs(topic) of i: ids per topic
             s_cnt[lane] = 0;
@@ -2066,8 +2078,20 @@ static bool ihave_prepare(gsim_handle* h, int64_t g, IhaveStage* st, int* rc)
 static int ihave_count(gsim_handle* h, IhaveStage* st)
 {
     ProfScope ps(h, GSIM_K_GOSSIP);
-    hipLaunchKernelGGL(k_gossip_count, dim3(st->grid), dim3(256), st->lds_c, h->stream, st->a, h->dl->d_gcount);
+    if (st->a.mlat)
+        hipLaunchKernelGGL(k_gossip_count<true>, dim3(st->grid), dim3(256), st->lds_c, h->stream, st->a, h->dl->d_gcount);
+    else
+        hipLaunchKernelGGL(k_gossip_count<false>, dim3(st->grid), dim3(256), st->lds_c, h->stream, st->a, h->dl->d_gcount);
     return hip_check(h, hipGetLastError(), "k_gossip_count");
+}
+
+template <int W>
+static void launch_ihave_w(gsim_handle* h, IhaveStage* st, const IhArgs& a)
+{
+    if (a.mlat)
+        hipLaunchKernelGGL((k_ihave<W, true>), dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)h->dl->d_gcount);
+    else
+        hipLaunchKernelGGL((k_ihave<W, false>), dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)h->dl->d_gcount);
 }
 
 static int ihave_walk(gsim_handle* h, IhaveStage* st)
@@ -2083,18 +2107,19 @@ static int ihave_walk(gsim_handle* h, IhaveStage* st)
         w = (h->max_degree <= 16 || (h->max_degree > 32 && short_mean)) ? 16 : h->max_degree <= 32 ? 32 : 64;
     }
     if (w == 16)
-        hipLaunchKernelGGL(k_ihave<16>, dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)d->d_gcount);
+        launch_ihave_w<16>(h, st, a);
     else if (w == 32)
-        hipLaunchKernelGGL(k_ihave<32>, dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)d->d_gcount);
+        launch_ihave_w<32>(h, st, a);
     else
-        hipLaunchKernelGGL(k_ihave<64>, dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)d->d_gcount);
+        launch_ihave_w<64>(h, st, a);
     if (d->cfg.ring > h->gp.max_ihave_length) {
         // the window may hold more than MaxIHaveLength slots: k_gossip_count
         // decided on the device which of the two walks runs
         const size_t lds = (((size_t)d->cfg.ring + 3) & ~(size_t)3) * sizeof(uint16_t) +
                            4 * (kRespStage + kPairTopics) * sizeof(uint64_t) + 4 * kPairTopics * sizeof(uint32_t);
         const int grid = (int)std::min<int64_t>((a.CN + 3) / 4, 4096);
-        hipLaunchKernelGGL(k_ihave_pairs, dim3(grid), dim3(256), lds, h->stream, a);
+        if (a.mlat) hipLaunchKernelGGL(k_ihave_pairs<true>, dim3(grid), dim3(256), lds, h->stream, a);
+        else hipLaunchKernelGGL(k_ihave_pairs<false>, dim3(grid), dim3(256), lds, h->stream, a);
     }
     hipLaunchKernelGGL(k_promise_insert, dim3(std::min<int64_t>((h->e + 255) / 256, 16384)), dim3(256), 0, h->stream,
                        d->d_pcand, d->d_prom, d->prom_ticks, a.prom_idx, h->e);
@@ -2118,8 +2143,11 @@ int deliver_flush(gsim_handle* h)
     if (!d || d->pending < 0) return GSIM_OK;
     ProfScope ps(h, GSIM_K_COMMIT);
     RoundArgs a = make_round_args(h, d->pending);
-    hipLaunchKernelGGL(k_commit, dim3(grid_peers((int64_t)a.rhi - (((int64_t)a.rlo - a.clo) & ~63ll))), dim3(256),
-                       (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
+    const dim3 grid(grid_peers((int64_t)a.rhi - (((int64_t)a.rlo - a.clo) & ~63ll)));
+    if (a.mlat)
+        hipLaunchKernelGGL(k_commit<true>, grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
+    else
+        hipLaunchKernelGGL(k_commit<false>, grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     d->pending = -1;
     return hip_check(h, hipGetLastError(), "k_commit");
 }
@@ -2238,7 +2266,10 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a)
     }
     // the slot list in LDS
     const size_t lds = ((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7;
-    hipLaunchKernelGGL((k_send_tm<TB>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+    if (a.mlat)
+        hipLaunchKernelGGL((k_send_tm<TB, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+    else
+        hipLaunchKernelGGL((k_send_tm<TB, false>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_send_tm");
 }
 
