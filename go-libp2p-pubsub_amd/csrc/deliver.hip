@@ -1309,6 +1309,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
     const uint32_t rp0 = vp ? a.row_ptr[pl] : 0u;
     const uint32_t rp1 = vp ? a.row_ptr[pl + 1] : 0u;
     const bool ign_l = vp && (a.behaviour[pl] & GSIM_BEHAVE_IGNORE_IWANT);
+    const uint64_t long_lanes = W < 64 ? __ballot(rp1 - rp0 > 4u * (uint32_t)W) : 0ull;
     const int64_t tick_round = a.tick * a.R;
     int nstage = 0;
     unsigned long long n_walk = 0, n_req = 0, n_resp = 0;
@@ -1349,21 +1350,12 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
             if (!mask) continue;
             const int64_t row_m = (int64_t)m * a.CN;
             const int64_t plane = (int64_t)t * a.E;
-            uint64_t gm = mask & gmask;
-            while (__ballot(gm != 0)) {
-                int bs = -1;
-                if (gm) { bs = __ffsll((long long)gm) - 1; gm &= gm - 1; }
-                const int sl = bs < 0 ? lane : bs;
-                const uint32_t beg = __shfl(rp0, sl, 64), end = __shfl(rp1, sl, 64);
-                const bool ign_s = __shfl(ign_l, sl, 64);
-                const uint32_t me_id = (uint32_t)(a.clo + p0 + (bs < 0 ? 0 : bs));
-                const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;   // Philox keys use global ids
-                n_walk += (gl == 0 && bs >= 0);
-                // rows longer than the group are walked in W-edge chunks (wave-uniform trip count)
-                const uint32_t deg = bs >= 0 ? end - beg : 0u;
-                for (uint32_t off = 0; __ballot(off < deg) != 0; off += W) {
-                const bool v = off + (uint32_t)gl < deg;
-                const uint32_t e = beg + off + (uint32_t)gl;
+            // one chunk of a row walk: lane gl of a group of `gw` lanes takes
+            // edge beg + off + gl of peer me_id's row
+            auto chunk = [&](uint32_t off, uint32_t gl_, uint32_t beg, uint32_t deg, uint32_t me_id, uint32_t me_g,
+                             bool ign_s) {
+                const bool v = off + gl_ < deg;
+                const uint32_t e = beg + off + gl_;
                 bool req = false, resp = false;
                 uint32_t r = 0;
                 if (push) {
@@ -1407,7 +1399,33 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                     if (resp) stage[nstage + __popcll(sb & ((1ull << lane) - 1))] = (uint64_t)r | ((uint64_t)m << 32);
                     nstage += __popcll(sb);
                 }
-                }
+            };
+            // rows longer than 4 groups' width are walked by the whole wave
+            // afterwards, so one hub does not hold its wave's other groups
+            // through its chunks
+            const uint64_t longm = mask & long_lanes;
+            uint64_t gm = mask & ~longm & gmask;
+            while (__ballot(gm != 0)) {
+                int bs = -1;
+                if (gm) { bs = __ffsll((long long)gm) - 1; gm &= gm - 1; }
+                const int sl = bs < 0 ? lane : bs;
+                const uint32_t beg = __shfl(rp0, sl, 64), end = __shfl(rp1, sl, 64);
+                const bool ign_s = __shfl(ign_l, sl, 64);
+                const uint32_t me_id = (uint32_t)(a.clo + p0 + (bs < 0 ? 0 : bs));
+                const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;   // Philox keys use global ids
+                n_walk += (gl == 0 && bs >= 0);
+                // rows longer than the group are walked in W-edge chunks (wave-uniform trip count)
+                const uint32_t deg = bs >= 0 ? end - beg : 0u;
+                for (uint32_t off = 0; __ballot(off < deg) != 0; off += W) chunk(off, (uint32_t)gl, beg, deg, me_id, me_g, ign_s);
+            }
+            for (uint64_t lm = longm; lm; lm &= lm - 1) {
+                const int bs = __builtin_ctzll(lm);
+                const uint32_t beg = __shfl(rp0, bs, 64), end = __shfl(rp1, bs, 64);
+                const bool ign_s = __shfl(ign_l, bs, 64);
+                const uint32_t me_id = (uint32_t)(a.clo + p0 + bs);
+                const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
+                n_walk += (lane == 0);
+                for (uint32_t off = 0; off < end - beg; off += 64) chunk(off, (uint32_t)lane, beg, end - beg, me_id, me_g, ign_s);
             }
         }
     }
