@@ -160,7 +160,7 @@ def build_engine(cfg, seed, device, scen=None, shard=None):
     eng.load_graph(net)
     eng.set_seed(0x5EED0000 + seed)
     eng.fill_synthetic(seed=seed * 7919 + 1, now=tick_time(0), p_mesh=D / k)
-    eng.msgs_init(scen.get("ring", MSG_RING), ROUNDS, tick_time(0), SECOND)
+    eng.msgs_init(scen.get("ring", MSG_RING), ROUNDS, tick_time(0), SECOND, max_arrivals=scen.get("max_arrivals"))
     if beh is not None:
         eng.set_peer_behaviour(beh)
     if os.environ.get("GSIM_SEND_VARIANT") and shard is None:   # A/B of the delivery kernel (gsim.h)
@@ -332,6 +332,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--msg-rate", type=float, default=None, help="messages per second per topic (config default)")
     ap.add_argument("--ring", type=int, default=None, help="message ring slots (config default)")
+    ap.add_argument("--vdelay", type=int, default=0,
+                    help="validation latency of every message in rounds (gsim_msg.vdelay; single engine)")
     ap.add_argument("--replicas", action="store_true",
                     help="N > 1: one independent network per rank (weak scaling) instead of one sharded network")
     ap.add_argument("--shards", type=int, default=1,
@@ -355,6 +357,9 @@ def main():
         scen["msg_rate"] = args.msg_rate
     if args.ring is not None:
         scen["ring"] = args.ring
+    if args.vdelay:
+        # slower propagation leaves more peers wanting at IHAVE time
+        scen["max_arrivals"] = 64 * cfg[0]
     n, k, T = cfg[0], cfg[1], cfg[2]
     sharded = (world > 1 and not args.replicas) or args.shards > 1
     shard = None
@@ -376,6 +381,9 @@ def main():
     rate = scen.get("msg_rate", MSG_RATE)
     sched = message_schedule(n, T, ticks, seed=s_seed, sub=net.sub if "zipf_per_peer" in scen else None, rate=rate)
     churn = churn_schedule(net, scen["churn_frac"], ticks, seed=s_seed + 2) if "churn_frac" in scen else None
+    if args.vdelay:
+        for arr in sched.values():
+            arr["vdelay"] = args.vdelay
 
     kk = 0
     for _ in range(args.warmup):
@@ -482,7 +490,8 @@ def main():
                                f"{ROUNDS} propagation rounds (publish, deliver, control, forward)",
                        "parallelism": (f"graph-sharded x{world} (RCCL halo exchange)" if sharded and world > 1
                                        else f"graph-sharded x{args.shards} on one GPU (in-process exchange)"
-                                       if sharded else f"replica-per-gpu x{world}")},
+                                       if sharded else f"replica-per-gpu x{world}"),
+                       **({"validation_latency_rounds": args.vdelay} if args.vdelay else {})},
             "msg_edge_deliveries_per_sec": deliveries / wall,
             "deliveries_per_tick": {"accepted": (stats1[0] - stats0[0]) / K, "first": (stats1[1] - stats0[1]) / K,
                                     "duplicate": (stats1[2] - stats0[2]) / K, "graylisted": (stats1[3] - stats0[3]) / K},

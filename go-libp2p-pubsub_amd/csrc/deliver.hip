@@ -242,6 +242,33 @@ __device__ __forceinline__ void vq_push(const RoundArgs& a, int64_t c, uint32_t 
     a.vq[(int64_t)pl * a.vq_cap + k] = (uint64_t)e | ((uint64_t)(uint32_t)t << 32) | ((uint64_t)kind << 40);
 }
 
+// vq_push for a whole wave from convergent code: lane entries with pl >= 0
+// go to plane pl, one queue atomic per distinct plane in the wave.
+__device__ __forceinline__ void vq_push_wave(const RoundArgs& a, int pl, uint64_t v)
+{
+    const int lane = threadIdx.x & 63;
+    uint64_t pending = __ballot(pl >= 0);
+    while (pending) {
+        const int leader = __builtin_ctzll(pending);
+        const int lpl = __shfl(pl, leader, 64);
+        const uint64_t grp = __ballot(pl == lpl) & pending;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&a.vqn[lpl], (uint32_t)__popcll(grp));
+        base = (uint32_t)__shfl((int)base, leader, 64);
+        if (pl == lpl) {
+            const uint32_t k = base + (uint32_t)__popcll(grp & ((1ull << lane) - 1));
+            if ((int64_t)k < a.vq_cap) a.vq[(int64_t)lpl * a.vq_cap + k] = v;
+            else atomicOr(&a.vqn[kVqPlanes], 1u);
+        }
+        pending &= ~grp;
+    }
+}
+
+__device__ __forceinline__ uint64_t vq_entry(uint32_t e, int32_t t, uint32_t kind)
+{
+    return (uint64_t)e | ((uint64_t)(uint32_t)t << 32) | ((uint64_t)kind << 40);
+}
+
 // Ordered list of the active slots (bit set in nnew), built by wave 0 into
 // LDS; every thread of the block must call it.
 __device__ __forceinline__ int active_slots(const uint32_t* nnew, int ring, uint16_t* s_act, int* s_n)
@@ -266,7 +293,7 @@ __device__ __forceinline__ int active_slots(const uint32_t* nnew, int ring, uint
 // markFirstMessageDelivery score.go:919-946; mcache.Put for lastput).
 template <bool ATOMIC = false, bool LAT = false>
 __device__ __forceinline__ void commit_claim(const RoundArgs& a, uint64_t* cellp, uint64_t c, int64_t gc,
-                                             uint32_t m, int64_t peer)
+                                             uint32_t m, int64_t peer, int* qpl = nullptr, uint64_t* qv = nullptr)
 {
     const uint32_t hi = (uint32_t)(c >> 32), lo = (uint32_t)c;
     if constexpr (LAT) {
@@ -276,8 +303,14 @@ __device__ __forceinline__ void commit_claim(const RoundArgs& a, uint64_t* cellp
             // validation completes in round gc + L: the winner's DeliverMessage
             // credit lands there (k_vq_apply), the put and forwarding after it
             const int32_t t = (int32_t)a.mtopic[m];
-            if (a.minv[m] == GSIM_VERDICT_ACCEPT && const_tp(a.tp)[t].scored)
-                vq_push(a, gc + L, hi & kEdgeMask, t, kVqFirst);
+            if (a.minv[m] == GSIM_VERDICT_ACCEPT && const_tp(a.tp)[t].scored) {
+                if (qpl) {                                  // k_commit pushes per wave
+                    *qpl = (int)((gc + L) & (kVqPlanes - 1));
+                    *qv = vq_entry(hi & kEdgeMask, t, kVqFirst);
+                } else {
+                    vq_push(a, gc + L, hi & kEdgeMask, t, kVqFirst);
+                }
+            }
             return;
         }
     } else {
@@ -954,6 +987,10 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                                 else if (vd == GSIM_VERDICT_ACCEPT) nv[u] = a.mcnt[plane + e];
                             }
                         }
+                        int qpl[P];              // validation latency: queue plane of the copy (-1: none)
+                        uint64_t qv[P];
+#pragma unroll
+                        for (int u = 0; u < P; ++u) { qpl[u] = -1; qv[u] = 0; }
 #pragma unroll
                         for (int u = 0; u < P; ++u) {
                             const uint32_t j = jv[u], e = ev[u], i = iv[u], k = kv[u];
@@ -1015,8 +1052,10 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             }
                             if (L && seeable && (seen_round < 0 || seen_round > a.g)) {
                                 // the receiver is still validating: drec.peers (score.go:806-809)
-                                if (scored_t && (pen || !inv))
-                                    vq_push(a, seen_round < 0 ? a.g + L : seen_round, e, t, pen ? kVqInv : kVqDup);
+                                if (scored_t && (pen || !inv)) {
+                                    qpl[u] = (int)((seen_round < 0 ? a.g + L : seen_round) & (kVqPlanes - 1));
+                                    qv[u] = vq_entry(e, t, pen ? kVqInv : kVqDup);
+                                }
                                 continue;
                             }
                             if (!sc) continue;
@@ -1036,6 +1075,10 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                                     a.mcnt[ir] = (uint8_t)(n + 1);
                                 }
                             }
+                        }
+                        if constexpr (LAT) {
+#pragma unroll
+                            for (int u = 0; u < P; ++u) vq_push_wave(a, qpl[u], qv[u]);
                         }
                     }
                     if (tab) __syncthreads();                    // s_own is rewritten by the next window
@@ -1118,10 +1161,13 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
             if (k >= nact) break;
+            int qpl = -1;
+            uint64_t qv = 0;
             if (is_claim_of(cv[b], par)) {
                 const uint32_t m = s_act[k];
-                commit_claim<false, LAT>(a, a.cell + (int64_t)m * a.CN + i, cv[b], a.g, m, a.clo + i);
+                commit_claim<false, LAT>(a, a.cell + (int64_t)m * a.CN + i, cv[b], a.g, m, a.clo + i, &qpl, &qv);
             }
+            if constexpr (LAT) vq_push_wave(a, qpl, qv);
         }
     }
 }
