@@ -1773,7 +1773,10 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
             }
         }
         if (L && vd != GSIM_VERDICT_SIGNATURE && (seen_round < 0 || seen_round > a.g)) {
-            if (tp->scored && (pen || !inv)) vq_push(a, seen_round < 0 ? a.g + L : seen_round, r, t, pen ? kVqInv : kVqDup);
+            // the lanes here push together (ballots over the active lanes)
+            const bool q = tp->scored && (pen || !inv);
+            vq_push_wave(a, q ? (int)((seen_round < 0 ? a.g + L : seen_round) & (kVqPlanes - 1)) : -1,
+                         vq_entry(r, t, pen ? kVqInv : kVqDup));
             continue;
         }
         if (!sc) continue;
