@@ -94,7 +94,6 @@ struct Deliver {
     uint32_t* d_tmtab = nullptr;       // k_send_tm blocks: [T+1] first block of each topic, [T] its range
     std::vector<uint32_t> tmtab;       // host copy (the upload's source)
     int64_t tm_cn = -1;                // peers the table was built for
-    bool fresh_on = false;             // the topic-major delivery (and so the fresh bits) is in use
     int32_t* d_mpub = nullptr;         // [ring] round the slot's message was published in
     int64_t* d_roff = nullptr;         // [rounds] offset of each round in its heartbeat
     int32_t* d_lastput = nullptr;      // [T][N]
@@ -407,275 +406,6 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, int32_t count)
     a.slot_last[slot] = (int32_t)a.g;
     if (a.tr.on(p.origin))                                  // PublishMessage (trace.go:70-91)
         a.tr.push(round_time(a, a.g), p.id, p.origin, p.origin, (int32_t)p.topic, GSIM_TRACE_PUBLISH_MESSAGE, 0);
-}
-
-// Round g.  W = lanes per row (power of two >= the longest row); group q of
-// a wave always walks the senders j0 + q*W .. j0 + q*W + W-1, two at a time
-// (their loads interleaved: two dependent memory trips per pair of rows).
-// B = active slots whose cells are loaded together.
-template <int W, int B>
-__global__ __launch_bounds__(256) void k_send(RoundArgs a)
-{
-    extern __shared__ uint16_t s_act[];   // [ring] active slots, then [ring/32] new-claim bits
-    __shared__ int s_n;
-    __shared__ unsigned long long s_stats[4];
-    uint32_t* s_new = reinterpret_cast<uint32_t*>(s_act + ((a.ring + 1) & ~1));
-    for (int w = threadIdx.x; w < (a.ring + 31) / 32; w += blockDim.x) s_new[w] = 0;
-    if (threadIdx.x < 4) s_stats[threadIdx.x] = 0;
-    const int nact0 = a.g > 0 ? active_slots(a.nnew_prev, a.ring, s_act, &s_n) : 0;   // round 0 has no predecessor
-    const int lane = threadIdx.x & 63;
-    const int64_t j0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
-    const int nact = j0 < a.N ? nact0 : 0;               // no early return: the block meets below
-    const int64_t jl = j0 + lane;
-    const bool vj = jl < a.N;
-    const int grp = lane / W, gl = lane % W;
-    const uint64_t gmask = group_mask<W>(grp);
-    const ctp_t tpa = const_tp(a.tp);
-    const uint32_t gprev = (uint32_t)(a.g - 1);
-    const uint32_t par = (uint32_t)(a.g & 1), qpar = par ^ 1u;
-    const uint32_t claim_hi = kClaim | (par << 30);
-    // row bounds of the wave's senders, shuffled to the group that walks a row
-    const uint32_t rp0 = vj ? a.row_ptr[jl] : 0u;
-    const uint32_t rp1 = vj ? a.row_ptr[jl + 1] : 0u;
-    unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
-    for (int k0 = 0; k0 < nact; k0 += B) {
-        uint64_t cv[B];
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-            const int k = k0 + b;
-            cv[b] = (k < nact && vj) ? a.cell[(int64_t)s_act[k] * a.CN + jl] : kUnseen64;
-        }
-        // (1) commit this lane's claims of round g-1: the winners' records are
-        // loaded for the whole batch first (one memory trip), then updated in
-        // slot order (a record winning several slots continues from the value
-        // stored for the earlier one)
-        {
-            double fv[B];
-            int64_t irb[B];
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                irb[b] = -1;
-                fv[b] = 0.0;
-                const int k = k0 + b;
-                if (k < nact && is_claim_of(cv[b], qpar) && ((uint32_t)cv[b] & kCreditFirst) &&
-                    !a.minv[s_act[k]]) {
-                    irb[b] = (int64_t)a.mtopic[s_act[k]] * a.E + ((uint32_t)(cv[b] >> 32) & kEdgeMask);
-                    fv[b] = a.first[irb[b]];
-                }
-            }
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                // the committed bits of the wave's 64 peers form one bitmap word,
-                // which only this wave writes during the round
-                const int k = k0 + b;
-                const uint64_t cb = __ballot(k < nact && is_claim_of(cv[b], qpar));
-                if (cb && lane == 0) a.seenbm[(int64_t)s_act[k] * a.nw + (j0 >> 6)] |= cb;
-            }
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                const int k = k0 + b;
-                if (k >= nact || !is_claim_of(cv[b], qpar)) continue;
-                const uint32_t m = s_act[k];
-                const uint64_t c0 = cv[b];
-                a.cell[(int64_t)m * a.CN + jl] = ((uint64_t)gprev << 32) | ((uint32_t)c0 & kPeerMask);
-                if (a.minv[m]) continue;                 // RejectMessage: counted when sent
-                const int32_t t = (int32_t)a.mtopic[m];
-                int32_t* lp = a.lastput + (int64_t)t * a.N + jl;
-                const int32_t tick = (int32_t)((a.g - 1) / a.R);
-                if (*lp < tick) *lp = tick;              // mcache.Put
-                if (irb[b] < 0) continue;
-                double x = fv[b];
-#pragma unroll
-                for (int bb = 0; bb < b; ++bb)
-                    if (irb[bb] == irb[b]) x = fv[bb];
-                const double cap = (tpa + t)->first_message_deliveries_cap;
-                x = (x + 1.0 > cap) ? cap : x + 1.0;
-                fv[b] = x;
-                a.first[irb[b]] = x;                     // markFirstMessageDelivery P2
-                if ((uint32_t)c0 & kCreditMesh)
-                    atomic_inc_capped(&a.meshd[irb[b]], (tpa + t)->mesh_message_deliveries_cap);
-            }
-        }
-        // the forward body is large: walk the batch without unrolling it, the
-        // cells rotating through cv[0] (registers, static indices)
-#pragma unroll 1
-        for (int b = 0; b < B; ++b) {
-            const int k = k0 + b;
-            if (k >= nact) break;                        // wave-uniform
-            const uint32_t m = s_act[k];
-            const int64_t row_m = (int64_t)m * a.CN;
-            const uint64_t c0 = cv[0];
-#pragma unroll
-            for (int q = 0; q + 1 < B; ++q) cv[q] = cv[q + 1];
-            const bool pend = is_claim_of(c0, qpar);     // first received in round g-1 (committed above)
-            const uint32_t origin = a.morigin[m];
-            const uint8_t vd = a.minv[m];
-            const bool inv = vd != GSIM_VERDICT_ACCEPT;
-            const bool pen = verdict_penalises(vd), seeable = vd != GSIM_VERDICT_SIGNATURE;
-            // receivers do not forward a message they did not accept; its
-            // origin publishes it regardless
-            const bool fr = (pend || (uint32_t)(c0 >> 32) == gprev) && (!inv || (uint32_t)jl == origin);
-            const uint64_t mask = __ballot(fr);
-            if (!mask) continue;
-            // (2) forward
-            const uint32_t from_l = (uint32_t)c0 & kPeerMask;
-            const int32_t t = (int32_t)a.mtopic[m];
-            // the origin's own Publish goes to its mesh, to its fanout when it
-            // has not joined the topic, or floods every topic peer with score
-            // >= publishThreshold (gossipsub.go:989-1028); forwarders use their mesh
-            const uint8_t o_want = (origin < a.N && ((a.sub[origin] >> t) & 1ull)) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
-            const ctp_t tp = tpa + t;
-            const bool scored_t = tp->scored != 0;
-            const int64_t window = tp->mesh_message_deliveries_window_ns;
-            const double mcap = tp->mesh_message_deliveries_cap;
-            const int64_t plane = (int64_t)t * a.E;
-            const unsigned long long first_before = n_first;
-            // every receiver saw the message at or after its publication: when
-            // that is within the window, a copy to a receiver whose committed
-            // bit is set is an in-window duplicate without reading its cell
-            const bool win_all = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
-            const int64_t bm_m = (int64_t)m * a.nw;
-            uint64_t gm = mask & gmask;
-            while (__ballot(gm != 0)) {
-                int b1 = -1, b2 = -1;
-                if (gm) { b1 = __ffsll((long long)gm) - 1; gm &= gm - 1; }
-                if (gm) { b2 = __ffsll((long long)gm) - 1; gm &= gm - 1; }
-                const int s1 = b1 < 0 ? lane : b1, s2 = b2 < 0 ? lane : b2;
-                const uint32_t f1 = __shfl(from_l, s1, 64), f2 = __shfl(from_l, s2, 64);
-                const uint32_t beg1 = __shfl(rp0, s1, 64), end1 = __shfl(rp1, s1, 64);
-                const uint32_t beg2 = __shfl(rp0, s2, 64), end2 = __shfl(rp1, s2, 64);
-                const bool v1 = b1 >= 0 && (uint32_t)gl < end1 - beg1;
-                const bool v2 = b2 >= 0 && (uint32_t)gl < end2 - beg2;
-                const uint32_t e1 = beg1 + (uint32_t)gl, e2 = beg2 + (uint32_t)gl;
-                const uint32_t j1 = (uint32_t)(j0 + (b1 < 0 ? 0 : b1)), j2 = (uint32_t)(j0 + (b2 < 0 ? 0 : b2));
-                // trip 1: the edge's router and record state
-                uint32_t i1 = 0, i2 = 0;
-                uint8_t mf1 = 0, mf2 = 0, ds1 = 0, ds2 = 0, tf1 = 0, tf2 = 0;
-                if (v1) {
-                    i1 = a.col[e1]; mf1 = a.mflags[plane + e1];
-                    ds1 = a.dstate[e1]; tf1 = a.tflags[plane + e1];
-                }
-                if (v2) {
-                    i2 = a.col[e2]; mf2 = a.mflags[plane + e2];
-                    ds2 = a.dstate[e2]; tf2 = a.tflags[plane + e2];
-                }
-                bool sel1 = (mf1 & (j1 == origin ? o_want : GSIM_TF_MESH)) != 0;
-                bool sel2 = (mf2 & (j2 == origin ? o_want : GSIM_TF_MESH)) != 0;
-                if (a.flood) {
-                    if (v1 && j1 == origin) sel1 = ((a.sub[i1] >> t) & 1ull) && a.score[a.rev[e1]] >= a.pub_thr;
-                    if (v2 && j2 == origin) sel2 = ((a.sub[i2] >> t) & 1ull) && a.score[a.rev[e2]] >= a.pub_thr;
-                }
-                // direct peers that joined the topic always get it (gossipsub.go:991-1003)
-                if (v1 && (ds1 & GSIM_DS_DIRECT) && !sel1) sel1 = (a.sub[i1] >> t) & 1ull;
-                if (v2 && (ds2 & GSIM_DS_DIRECT) && !sel2) sel2 = (a.sub[i2] >> t) & 1ull;
-                const bool tg1 = v1 && sel1 && (ds1 & GSIM_DS_CONNECTED) && i1 != f1 && i1 != origin;
-                const bool tg2 = v2 && sel2 && (ds2 & GSIM_DS_CONNECTED) && i2 != f2 && i2 != origin;
-                const bool ok1 = tg1 && (ds1 & GSIM_DS_ACCEPT), ok2 = tg2 && (ds2 & GSIM_DS_ACCEPT);
-                n_gray += (tg1 && !ok1) + (tg2 && !ok2);     // AcceptFrom: graylisted sender
-                n_acc += ok1 + ok2;
-                // trip 2: the receiver's cell and the counter to update
-                const bool sc1 = ok1 && scored_t && (ds1 & GSIM_DS_TRACKED);
-                const bool sc2 = ok2 && scored_t && (ds2 & GSIM_DS_TRACKED);
-                uint64_t c1 = 0, c2 = 0;
-                uint32_t n1 = 0, n2 = 0;
-                double x1 = 0.0, x2 = 0.0;
-                // known: committed in an earlier round, and its first-seen round
-                // is not needed (in-window for sure, or no counter to update)
-                bool k1 = false, k2 = false;
-                {
-                    if (ok1) k1 = ((a.seenbm[bm_m + (i1 >> 6)] >> (i1 & 63)) & 1ull) &&
-                                  (win_all || !sc1 || inv || !(tf1 & GSIM_TF_IN_MESH));
-                    if (ok2) k2 = ((a.seenbm[bm_m + (i2 >> 6)] >> (i2 & 63)) & 1ull) &&
-                                  (win_all || !sc2 || inv || !(tf2 & GSIM_TF_IN_MESH));
-                }
-                if (ok1 && !k1) c1 = a.cell[row_m + i1];
-                if (ok2 && !k2) c2 = a.cell[row_m + i2];
-                if (sc1) { if (pen) x1 = a.invalid[plane + e1]; else if (!inv && (tf1 & GSIM_TF_IN_MESH)) n1 = a.mcnt[plane + e1]; }
-                if (sc2) { if (pen) x2 = a.invalid[plane + e2]; else if (!inv && (tf2 & GSIM_TF_IN_MESH)) n2 = a.mcnt[plane + e2]; }
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const bool ok = u ? ok2 : ok1;
-                    if (!ok) continue;
-                    const uint64_t c = u ? c2 : c1;
-                    const uint32_t e = u ? e2 : e1, i = u ? i2 : i1, j = u ? j2 : j1;
-                    const bool sc = u ? sc2 : sc1;
-                    const uint8_t tf = u ? tf2 : tf1;
-                    const uint32_t hi = (uint32_t)(c >> 32);
-                    const bool known = u ? k2 : k1;
-                    if (a.tr.on(i))
-                        a.tr.push(round_time(a, a.g), ((uint64_t)a.g << 32) | m, i, j, t,
-                                  seeable ? kTraceCopy : (uint8_t)GSIM_TRACE_REJECT_MESSAGE, a.minv[m]);
-                    // first-seen round of an earlier round, or -1 for unseen /
-                    // claimed in this round
-                    int64_t seen_round = -1;
-                    if (known) {
-                        seen_round = a.g - 1;    // any earlier round: only "in window" is used
-                    } else if (c != kUnseen64) {
-                        if (!(hi & kClaim)) seen_round = hi;
-                        else if (((hi >> 30) & 1u) != par) seen_round = a.g - 1;
-                    }
-                    if (seeable && seen_round < 0 && (c == kUnseen64 || (hi & kEdgeMask) > e)) {
-                        // claim unless a lower edge already holds the cell
-                        uint32_t lo = j;
-                        if (sc && !inv) {
-                            lo |= kCreditFirst;
-                            if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo |= kCreditMesh;
-                        }
-                        const uint64_t v = ((uint64_t)(claim_hi | e) << 32) | lo;
-                        const uint64_t prev = __hip_atomic_fetch_min(a.cell + row_m + i, v, __ATOMIC_RELAXED,
-                                                                     __HIP_MEMORY_SCOPE_AGENT);
-                        if (prev == kUnseen64) n_first++;
-                    }
-                    if (!sc) continue;
-                    const int64_t ir = plane + e;
-                    if (pen) {
-                        a.invalid[ir] = (u ? x2 : x1) + 1.0;    // markInvalidMessageDelivery
-                    } else if (!inv && (tf & GSIM_TF_IN_MESH)) {
-                        // markDuplicateMessageDelivery's window test; a same-round
-                        // copy (first or duplicate) has validated = now
-                        const bool in_window = known ? true
-                                             : seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window)
-                                                               : (window >= 0);
-                        if (in_window) {
-                            uint32_t n = u ? n2 : n1;
-                            if (n == 255u) {   // spill a full count into the counter (this lane owns the record)
-                                a.meshd[ir] = apply_incs(a.meshd[ir], n, mcap);
-                                n = 0;
-                            }
-                            a.mcnt[ir] = (uint8_t)(n + 1);
-                        }
-                    }
-                }
-            }
-            // the slot stays active next round if any copy claimed a new cell
-            if (__ballot(n_first != first_before) && lane == 0) atomicOr(&s_new[m >> 5], 1u << (m & 31));
-        }
-    }
-    n_acc = wave_sum_u64(n_acc);
-    n_gray = wave_sum_u64(n_gray);
-    n_first = wave_sum_u64(n_first);
-    if (lane == 0 && (n_acc | n_gray)) {
-        atomicAdd(&s_stats[0], n_acc);
-        atomicAdd(&s_stats[1], n_first);
-        atomicAdd(&s_stats[3], n_gray);
-    }
-    __syncthreads();
-    for (int w = threadIdx.x; w < (a.ring + 31) / 32; w += blockDim.x) {
-        uint32_t bits = s_new[w];
-        if (!bits) continue;
-        atomicOr(&a.nnew_cur[w], bits);
-        while (bits) {                                   // mcache activity of the slot
-            const int q = __ffs(bits) - 1;
-            bits &= bits - 1;
-            atomicMax(&a.slot_last[w * 32 + q], (int32_t)a.g);
-        }
-    }
-    if (threadIdx.x == 0 && (s_stats[0] | s_stats[3])) {
-        atomicAdd(&a.stats[0], s_stats[0]);
-        atomicAdd(&a.stats[1], s_stats[1]);
-        atomicAdd(&a.stats[2], s_stats[0] - s_stats[1]);
-        atomicAdd(&a.stats[3], s_stats[3]);
-    }
 }
 
 // Position of the k-th set bit (k < popcount) of m.
@@ -1991,7 +1721,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.rlo = (uint32_t)h->olo();
     a.rhi = (uint32_t)h->ohi();
     a.seenbm = d->d_seenbm; a.nw = (a.CN + 63) / 64; a.mpub = d->d_mpub; a.roff = d->d_roff;
-    a.fresh = d->fresh_on ? d->d_fresh : nullptr;
+    a.fresh = d->d_fresh;
     a.fsum = d->d_fsum;
     a.mmask = d->d_mmask;
     a.tmtab = d->d_tmtab;
@@ -2340,12 +2070,6 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a)
     return hip_check(h, hipGetLastError(), "k_send_tm");
 }
 
-template <int W>
-static void launch_send(gsim_handle* h, int grid, size_t lds, const RoundArgs& a)
-{
-    hipLaunchKernelGGL((k_send<W, kSlotBatch>), dim3(grid), dim3(256), lds, h->stream, a);
-}
-
 // ---- round stages (gsim_round runs them in order; a sharded group
 // exchanges copies between send and post, control records after control,
 // and the IHAVE counts / holders inside the IHAVE stage, shard.hip) --------
@@ -2371,22 +2095,13 @@ int deliver_round_prepare(gsim_handle* h, int64_t round)
         h->err = "rounds must be consecutive";
         return GSIM_ESTATE;
     }
-    if (h->max_degree > 64 && !d->fresh_on) {
-        // the peer-major k_send walks a row with one wavefront
-        h->err = "the peer-major delivery kernel supports rows of at most 64 connections";
-        return GSIM_ERANGE;
-    }
-    if (h->sh && !d->fresh_on) {
-        h->err = "a shard's delivery needs the topic-major kernel (its owned peers' bits must fit in LDS)";
-        return GSIM_ERANGE;
-    }
     int rc = 0;
     {
         ProfScope ps(h, GSIM_K_ACCEPT);
         rc = refresh_accept(h);
         if (rc) return rc;
     }
-    if (d->fresh_on) rc = deliver_flush(h);
+    rc = deliver_flush(h);
     if (!rc && d->lat_on) {
         // validations completing now (the flush above queued round g-1's
         // winners with latency 1)
@@ -2425,35 +2140,26 @@ int deliver_round_send(gsim_handle* h, int64_t round)
     int rc = 0;
     RoundArgs a = make_round_args(h, round);
     h->mcnt_dirty = true;
-    const size_t lds = (((size_t)d->cfg.ring + 1) & ~(size_t)1) * sizeof(uint16_t) + (size_t)nnew_words(d) * 4;
     {
         ProfScope ps(h, GSIM_K_SEND);
-        const int grid = grid_peers(h->n);
-        if (d->fresh_on) {
-            if (d->mask_version != h->mesh_version) {
-                // the masks are kept current by the heartbeat, the control pass
-                // and a shard's router import; other writers of the router's
-                // flags (ABI writes, direct peers, the device fill) bump the
-                // version: rebuild them all
-                hipLaunchKernelGGL(k_mesh_mask, dim3((uint32_t)std::min<int64_t>((h->n + 3) / 4, 65536)), dim3(256), 0,
-                                   h->stream, (const uint32_t*)h->d_row_ptr, (const uint32_t*)h->d_col,
-                                   (const uint8_t*)h->d_mflags, (const uint8_t*)h->d_direct, h->n, h->e,
-                                   std::max(1, h->t), (uint32_t)h->olo(), (uint32_t)h->ohi(), d->d_mmask);
-                d->mask_version = h->mesh_version;
-            }
-            // one thread per edge: forwarders walk only their mesh edges (a
-            // handful of a row's positions), so lane groups per row would idle
-            // most lanes (C3: 21.0 against 32.9 ms per tick,
-            // profiles/r02_ab_walk_masks.log)
-            rc = launch_send_tm(h, a);
-            if (rc) return rc;
-        } else if (h->max_degree <= 16)
-            launch_send<16>(h, grid, lds, a);
-        else if (h->max_degree <= 32)
-            launch_send<32>(h, grid, lds, a);
-        else
-            launch_send<64>(h, grid, lds, a);
-        // the claims of round g-1 were committed by k_send; round g+1's bits
+        if (d->mask_version != h->mesh_version) {
+            // the masks are kept current by the heartbeat, the control pass
+            // and a shard's router import; other writers of the router's
+            // flags (ABI writes, direct peers, the device fill) bump the
+            // version: rebuild them all
+            hipLaunchKernelGGL(k_mesh_mask, dim3((uint32_t)std::min<int64_t>((h->n + 3) / 4, 65536)), dim3(256), 0,
+                               h->stream, (const uint32_t*)h->d_row_ptr, (const uint32_t*)h->d_col,
+                               (const uint8_t*)h->d_mflags, (const uint8_t*)h->d_direct, h->n, h->e,
+                               std::max(1, h->t), (uint32_t)h->olo(), (uint32_t)h->ohi(), d->d_mmask);
+            d->mask_version = h->mesh_version;
+        }
+        // one thread per edge: forwarders walk only their mesh edges (a
+        // handful of a row's positions), so lane groups per row would idle
+        // most lanes (C3: 21.0 against 32.9 ms per tick,
+        // profiles/r02_ab_walk_masks.log)
+        rc = launch_send_tm(h, a);
+        if (rc) return rc;
+        // the claims of round g-1 were committed before k_send_tm; round g+1's bits
         // were last read (as "previous") by round g
         d->pending = round;
         hipError_t e = hipMemsetAsync(d->d_nnew + (size_t)((round + 1) & 1) * (size_t)nnew_words(d), 0,
@@ -2663,29 +2369,6 @@ void deliver_blocks_changed(gsim_handle* h)
     h->dl->tm_cn = -1;          // the next k_send_tm launch rebuilds its block table
 }
 
-int deliver_variant_changed(gsim_handle* h)
-{
-    Deliver* d = h->dl;
-    if (!d) return GSIM_OK;
-    int rc = deliver_flush(h);
-    if (rc) return rc;
-    const bool on = h->send_variant == 3;
-    if (on != d->fresh_on) {
-        // the topic-major kernel's next frontier would be missing its fresh bits
-        if (on && d->next_round > 0) {
-            h->err = "the delivery kernel can change to topic-major only before the first round";
-            return GSIM_ESTATE;
-        }
-        const size_t bytes = (size_t)d->cfg.ring * (size_t)((h->n + 63) / 64) * 8;
-        hipError_t e = hipMemsetAsync(d->d_fresh, 0, bytes, h->stream);
-        if (e == hipSuccess)
-            e = hipMemsetAsync(d->d_fsum, 0, (size_t)d->cfg.ring * (size_t)(((h->n + 63) / 64 + 63) / 64) * 8, h->stream);
-        if (e != hipSuccess) return hip_check(h, e, "fresh bits");
-        d->fresh_on = on;
-    }
-    return GSIM_OK;
-}
-
 int32_t* deliver_slot_last(gsim_handle* h) { return h->dl ? h->dl->d_slot_last : nullptr; }
 
 extern "C" {
@@ -2759,7 +2442,6 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
         return e == hipErrorOutOfMemory ? GSIM_ENOMEM : GSIM_EDEVICE;
     }
     h->dl = d;
-    d->fresh_on = h->send_variant == 3;
     e = hipMemsetAsync(d->d_cell, 0xFF, ring * CN * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_seenbm, 0, ring * ((CN + 63) / 64) * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_fresh, 0, ring * ((CN + 63) / 64) * 8, h->stream);
@@ -2814,8 +2496,8 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
         }
         slots[(size_t)m] = (uint32_t)(msgs[m].id % (uint64_t)d->cfg.ring);
         if (msgs[m].vdelay > GSIM_MAX_VDELAY) { h->err = "vdelay above GSIM_MAX_VDELAY"; return GSIM_EINVAL; }
-        if (msgs[m].vdelay && (h->sh || !d->fresh_on)) {
-            h->err = "a validation latency (vdelay) needs the topic-major delivery of a single engine";
+        if (msgs[m].vdelay && h->sh) {
+            h->err = "a validation latency (vdelay) needs a single engine (not a shard)";
             return GSIM_ERANGE;
         }
     }

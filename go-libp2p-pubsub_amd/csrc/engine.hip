@@ -1056,14 +1056,9 @@ int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now, double p_mes
 int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant)
 {
     if (!h) return GSIM_EINVAL;
-    if (which == 2) {           // delivery: 0 = peer-major k_send (8-slot batch), 3 = topic-major k_send_tm
-        if (variant != 0 && variant != 3) { h->err = "unknown delivery kernel variant (0 or 3)"; return GSIM_EINVAL; }
-        if (h->sh && variant != 3) { h->err = "a shard delivers with the topic-major kernel"; return GSIM_EINVAL; }
-        const int old = h->send_variant;
-        h->send_variant = variant;
-        const int rc = deliver_variant_changed(h);
-        if (rc) h->send_variant = old;
-        return rc;
+    if (which == 2) {           // delivery: 3 = topic-major k_send_tm (the only kernel; the peer-major one is gone)
+        if (variant != 3) { h->err = "unknown delivery kernel variant (3: topic-major)"; return GSIM_EINVAL; }
+        return GSIM_OK;
     }
     if (which == 3) {           // k_ihave lane group: 0 = by row lengths, else 16 / 32 / 64
         if (variant != 0 && variant != 16 && variant != 32 && variant != 64) {

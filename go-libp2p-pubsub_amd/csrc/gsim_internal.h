@@ -249,7 +249,6 @@ struct gsim_handle {
     std::vector<int64_t> topic_subs;   // [T] local peers that joined each topic (k_send_tm's block shares)
     bool tm_uniform = false;  // k_send_tm blocks the same for every topic (gsim_set_kernel_variant(h, 6, 1))
     int64_t tm_budget = 0;    // k_send_tm blocks in all (0: ranges x T, launch_send_tm_tb)
-    int send_variant = 3;     // delivery kernel variant (gsim_set_kernel_variant(h, 2, v)); 3 = topic-major
     int ihave_w = 0;          // k_ihave lane group width (gsim_set_kernel_variant(h, 3, w)); 0 = by row lengths
 
     // device: parameters and scratch flags
@@ -406,7 +405,6 @@ void deliver_round_end(gsim_handle* h, int64_t round);
 int32_t* deliver_slot_last(gsim_handle* h);           // [ring]
 int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32_t* d_cnt, int64_t cap);
 int deliver_frontier_import(gsim_handle* h, int64_t round, const uint64_t* in, int64_t n);
-int deliver_variant_changed(gsim_handle* h);          // gsim_set_kernel_variant(h, 2, v)
 void deliver_blocks_changed(gsim_handle* h);          // gsim_set_kernel_variant(h, 6, v)
 // heartbeat.hip: the control inbox ([2][T][E] by round parity) and its per-receiver summary ([2][N])
 uint8_t* extra_ctl(gsim_handle* h);

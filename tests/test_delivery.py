@@ -224,9 +224,6 @@ def _schedule(rng, ticks, T, R, rate, inv_frac, n):
     (1500, 24, 2, [1, 2, 3, 4], 6, 0.1, 0.02, 256, 3),
     (1200, 16, 2, [1, 2], 200, 0.1, 0.02, 1024, 3),         # > 64 active slots a topic: passes, layers
     (1200, 16, 2, [1, 2], 200, 0.1, 0.02, 1024, 36),        # the same, blocks the same per topic
-    (1500, 32, 2, [1, 2, 3], 8, 0.1, 0.02, 256, 0),         # peer-major k_send (same results)
-    (1500, 24, 2, [1, 2, 3], 8, 0.1, 0.02, 256, 0),
-    (3000, 32, 3, [14, 15, 16], 12, 0.05, 0.03, 512, 0),
 ])
 def test_rounds_bit_exact(require_gpu, n, k, T, ticks, rate, inv_frac, retained, ring, send_variant):
     from fixtures import beacon_params, beacon_topic, synthetic_state
