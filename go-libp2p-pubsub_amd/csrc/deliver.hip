@@ -132,6 +132,8 @@ struct RoundArgs {
     int64_t t0, hb, g, now;
     const uint32_t *row_ptr, *col;
     const uint8_t* dstate;     // GSIM_DS_* per edge index (router connected; record accept/tracked)
+    const uint64_t* smask;     // topic slots of each row owner (nullptr: dense; gsim_internal.h)
+    const uint32_t* owner;     // row owner of each edge index
     const uint8_t* mflags;     // router mesh bits, edge order
     const uint8_t* tflags;     // score bits, record order
     const gsim_topic_score_params* tp;
@@ -322,7 +324,8 @@ __device__ __forceinline__ void commit_claim(const RoundArgs& a, uint64_t* cellp
     if (ATOMIC) atomicMax(lp, tick); else if (*lp < tick) *lp = tick;
     if (!(lo & kCreditFirst)) return;
     const ctp_t tp = const_tp(a.tp) + t;
-    const int64_t ir = (int64_t)t * a.E + (hi & kEdgeMask);
+    // the winner's record sits at its edge, in the sender's row (its topic slot)
+    const int64_t ir = slot_idx(smask_of(a.smask, lo & kPeerMask), t, a.E, hi & kEdgeMask);
     const double cap = tp->first_message_deliveries_cap;
     if (ATOMIC) {
         atomic_inc_capped(&a.first[ir], cap);
@@ -425,8 +428,8 @@ __device__ __forceinline__ uint32_t kth_bit(uint64_t m, uint32_t k)
 // position q of row x carries the router's mesh bit for t, or is a direct
 // peer; only edges to the receivers [rlo, rhi) (a shard's owned peers).
 __global__ __launch_bounds__(256) void k_mesh_mask(const uint32_t* row_ptr, const uint32_t* col, const uint8_t* mflags,
-                                                   const uint8_t* direct, int64_t n, int64_t E, int32_t T,
-                                                   uint32_t rlo, uint32_t rhi, uint64_t* mmask)
+                                                   const uint8_t* direct, const uint64_t* smask, int64_t n, int64_t E,
+                                                   int32_t T, uint32_t rlo, uint32_t rhi, uint64_t* mmask)
 {
     // one wave per row, lane = row position: coalesced flag planes, one ballot per topic
     const int lane = threadIdx.x & 63;
@@ -437,8 +440,9 @@ __global__ __launch_bounds__(256) void k_mesh_mask(const uint32_t* row_ptr, cons
         const uint32_t i = v ? col[e] : 0u;
         const bool own = v && i >= rlo && i < rhi;
         const bool dir = own && direct && direct[e];
+        const uint64_t m = smask_of(smask, (uint32_t)r);
         for (int32_t t = 0; t < T; ++t) {
-            const bool me = own && (dir || (mflags[(int64_t)t * E + e] & GSIM_TF_MESH));
+            const bool me = own && (dir || (slot_has(m, t) && (mflags[slot_idx(m, t, E, e)] & GSIM_TF_MESH)));
             const uint64_t m = __ballot(me);
             if (lane == 0) mmask[(int64_t)t * n + r] = m;
         }
@@ -494,6 +498,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
     __shared__ uint32_t s_beg[kTmChunk];                     // its row's first edge (sedge: first entry)
     __shared__ uint64_t s_msk[kTmChunk];                     // its mesh mask (0: the whole row)
     __shared__ uint8_t s_sk[kTmChunk];                       // its slot (index in the pass)
+    __shared__ uint8_t s_pl[kTmChunk];                       // its row's topic slot of t (plane, gsim_internal.h)
     __shared__ uint16_t s_own[kTmWin];                       // sender (index above) of each flattened edge of a window
     __shared__ uint32_t s_wsum[64];
     __shared__ uint32_t s_m[kTsSlots], s_org[kTsSlots];      // the pass's slots and their origins
@@ -530,7 +535,6 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
     const bool scored_t = tp->scored != 0;
     const int64_t window = tp->mesh_message_deliveries_window_ns;
     const double mcap = tp->mesh_message_deliveries_cap;
-    const int64_t plane = (int64_t)t * a.E;
     const uint32_t par = (uint32_t)(a.g & 1);
     const uint32_t claim_hi = kClaim | (par << 30);
     const uint32_t clo = a.clo;
@@ -589,7 +593,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
             bool first_layer = true;
             for (;;) {
                 const uint32_t fb = (pm[0] ? 1u : 0u) | (pm[1] ? 2u : 0u);
-                uint32_t len2[2] = {0, 0}, beg2[2] = {0, 0}, from2[2] = {0, 0}, k2[2] = {0, 0};
+                uint32_t len2[2] = {0, 0}, beg2[2] = {0, 0}, from2[2] = {0, 0}, k2[2] = {0, 0}, pl2[2] = {0, 0};
                 uint64_t msk2[2] = {0, 0};
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
@@ -597,8 +601,13 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                         k2[u] = (uint32_t)__builtin_ctzll(pm[u]);
                         const uint32_t x = (uint32_t)(x0 + u), m = s_m[k2[u]];
                         from2[u] = (uint32_t)a.cell[(int64_t)m * a.CN + (x - clo)] & kPeerMask;
+                        const uint64_t xm = smask_of(a.smask, x);
+                        pl2[u] = (uint32_t)__popcll(xm & ((1ull << t) - 1ull));
                         const uint32_t rb = a.row_ptr[x], deg = a.row_ptr[x + 1] - rb;
-                        if (deg <= 64 && x != s_org[k2[u]]) {
+                        if (!slot_has(xm, t)) {
+                            // no state for t in x's row (cannot happen: a forwarder holds its
+                            // topic, an origin gets the slot at publication): nothing is sent
+                        } else if (deg <= 64 && x != s_org[k2[u]]) {
                             msk2[u] = a.mmask[(int64_t)t * a.N + x];
                             beg2[u] = rb;
                             len2[u] = (uint32_t)__popcll(msk2[u]);
@@ -639,6 +648,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             s_beg[q] = beg2[u];
                             s_msk[q] = msk2[u];
                             s_sk[q] = (uint8_t)k2[u];
+                            s_pl[q] = (uint8_t)pl2[u];
                             ++q;
                             off += len2[u];
                         }
@@ -675,6 +685,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                     }
                     for (uint32_t it0 = w0; it0 < w1; it0 += kPerIt) {
                         uint32_t jv[P], fv[P], ev[P], iv[P], nv[P], kv[P];
+                        int64_t pv[P];           // the sender's plane of topic t
                         uint8_t mfv[P], dsv[P], tfv[P];
                         bool vv[P], mk[P];
                         double xv[P];
@@ -696,6 +707,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             jv[u] = vv[u] ? s_front[q] : 0u;
                             fv[u] = vv[u] ? s_from[q] : 0u;
                             kv[u] = vv[u] ? s_sk[q] : 0u;
+                            pv[u] = vv[u] ? (int64_t)s_pl[q] * a.E : 0;
                             const uint32_t k = fi - s_off[q];
                             const uint64_t msk = s_msk[q];
                             mk[u] = msk != 0;
@@ -711,10 +723,11 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                                 const uint8_t vd = s_vd[kv[u]];
                                 // a masked row's positions are its mesh (or direct) edges: the
                                 // router flags are read only for direct ones (below)
-                                iv[u] = a.col[e]; dsv[u] = a.dstate[e]; tfv[u] = a.tflags[plane + e];
-                                if (!mk[u]) mfv[u] = a.mflags[plane + e];
-                                if (verdict_penalises(vd)) xv[u] = a.invalid[plane + e];
-                                else if (vd == GSIM_VERDICT_ACCEPT) nv[u] = a.mcnt[plane + e];
+                                const int64_t pe = pv[u] + e;
+                                iv[u] = a.col[e]; dsv[u] = a.dstate[e]; tfv[u] = a.tflags[pe];
+                                if (!mk[u]) mfv[u] = a.mflags[pe];
+                                if (verdict_penalises(vd)) xv[u] = a.invalid[pe];
+                                else if (vd == GSIM_VERDICT_ACCEPT) nv[u] = a.mcnt[pe];
                             }
                         }
                         int qpl[P];              // validation latency: queue plane of the copy (-1: none)
@@ -730,7 +743,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             const bool pen = verdict_penalises(vd), seeable = vd != GSIM_VERDICT_SIGNATURE;
                             const uint8_t ds = dsv[u], tf = tfv[u];
                             bool sel;
-                            if (mk[u]) sel = !(ds & GSIM_DS_DIRECT) || (a.mflags[plane + e] & GSIM_TF_MESH);
+                            if (mk[u]) sel = !(ds & GSIM_DS_DIRECT) || (a.mflags[pv[u] + e] & GSIM_TF_MESH);
                             else sel = (mfv[u] & (j == origin ? s_ow[k] : GSIM_TF_MESH)) != 0;
                             if (a.flood && vv[u] && j == origin)
                                 sel = ((a.sub[i] >> t) & 1ull) &&
@@ -789,7 +802,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                                 continue;
                             }
                             if (!sc) continue;
-                            const int64_t ir = plane + e;
+                            const int64_t ir = pv[u] + e;
                             if (pen) {
                                 a.invalid[ir] = xv[u] + 1.0;
                             } else if (!inv && (tf & GSIM_TF_IN_MESH)) {
@@ -926,6 +939,7 @@ struct IhArgs {
     int32_t lo_round;              // first round of the gossip window
     const uint32_t *row_ptr, *col, *rev;
     const uint64_t* sub;
+    const uint64_t* smask;         // topic slots (gsel planes: the advertiser's row)
     const uint32_t *mtopic, *morigin;
     const uint8_t* minv;
     const uint8_t* mlat;           // validation latencies (RoundArgs::mlat)
@@ -1125,18 +1139,17 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
             const uint64_t mask = __ballot(me);
             if (!mask) continue;
             const int64_t row_m = (int64_t)m * a.CN;
-            const int64_t plane = (int64_t)t * a.E;
             // one chunk of a row walk: lane gl of a group of `gw` lanes takes
-            // edge beg + off + gl of peer me_id's row
+            // edge beg + off + gl of peer me_id's row (me_pl: its plane of t)
             auto chunk = [&](uint32_t off, uint32_t gl_, uint32_t beg, uint32_t deg, uint32_t me_id, uint32_t me_g,
-                             bool ign_s) {
+                             bool ign_s, int64_t me_pl) {
                 const bool v = off + gl_ < deg;
                 const uint32_t e = beg + off + gl_;
                 bool req = false, resp = false;
                 uint32_t r = 0;
                 if (push) {
                     // holder me_id walks its row: the peers it gossiped t to
-                    if (v && a.gsel[plane + e]) {
+                    if (v && me_pl >= 0 && a.gsel[me_pl + e]) {
                         const uint32_t p = a.col[e], re = a.rev[e];
                         // p's gate on i, p has not seen m (a shard: p one of its receivers)
                         req = p >= a.rlo && p < a.rhi && a.gstate[re] && a.cell[row_m + (p - a.clo)] == kUnseen64;
@@ -1152,8 +1165,9 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                     // receiver me_id walks its row: the peers that gossiped t to it and hold m
                     if (v) {
                         const uint32_t re = a.rev[e];
-                        if (a.gsel[plane + re] && a.gstate[e]) {
-                            const uint32_t i = a.col[e];
+                        const uint32_t i = a.col[e];
+                        const uint64_t mi = smask_of(a.smask, i);        // i's emitGossip choices: its row
+                        if (slot_has(mi, t) && a.gsel[slot_idx(mi, t, a.E, re)] && a.gstate[e]) {
                             req = holds_in_window(a.cell[row_m + (i - a.clo)], a.g, a.lo_round, tick_round, inv,
                                                   i == origin, LAT ? a.mlat[m] : 0u);
                             if (req) {
@@ -1189,10 +1203,13 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                 const bool ign_s = __shfl(ign_l, sl, 64);
                 const uint32_t me_id = (uint32_t)(a.clo + p0 + (bs < 0 ? 0 : bs));
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;   // Philox keys use global ids
+                const uint64_t me_m = smask_of(a.smask, me_id);
+                const int64_t me_pl = slot_has(me_m, t) ? slot_idx(me_m, t, a.E, 0) : -1;
                 n_walk += (gl == 0 && bs >= 0);
                 // rows longer than the group are walked in W-edge chunks (wave-uniform trip count)
                 const uint32_t deg = bs >= 0 ? end - beg : 0u;
-                for (uint32_t off = 0; __ballot(off < deg) != 0; off += W) chunk(off, (uint32_t)gl, beg, deg, me_id, me_g, ign_s);
+                for (uint32_t off = 0; __ballot(off < deg) != 0; off += W)
+                    chunk(off, (uint32_t)gl, beg, deg, me_id, me_g, ign_s, me_pl);
             }
             for (uint64_t lm = longm; lm; lm &= lm - 1) {
                 const int bs = __builtin_ctzll(lm);
@@ -1200,8 +1217,11 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                 const bool ign_s = __shfl(ign_l, bs, 64);
                 const uint32_t me_id = (uint32_t)(a.clo + p0 + bs);
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
+                const uint64_t me_m = smask_of(a.smask, me_id);
+                const int64_t me_pl = slot_has(me_m, t) ? slot_idx(me_m, t, a.E, 0) : -1;
                 n_walk += (lane == 0);
-                for (uint32_t off = 0; off < end - beg; off += 64) chunk(off, (uint32_t)lane, beg, end - beg, me_id, me_g, ign_s);
+                for (uint32_t off = 0; off < end - beg; off += 64)
+                    chunk(off, (uint32_t)lane, beg, end - beg, me_id, me_g, ign_s, me_pl);
             }
         }
     }
@@ -1301,8 +1321,10 @@ __global__ __launch_bounds__(256) void k_ihave_pairs(IhArgs a)
         for (uint32_t e = beg; e < end; ++e) {
             if (!a.gstate[e]) continue;                           // IHAVE from a peer below gossipThreshold
             const uint32_t re = a.rev[e], i = a.col[e];
-            // topics i gossiped to p that p joined (gs.mesh[topic] exists)
-            const bool tb = lane < a.T && ((subp >> lane) & 1ull) && a.gsel[(int64_t)lane * a.E + re];
+            // topics i gossiped to p that p joined (gs.mesh[topic] exists); i's choices sit in its row
+            const uint64_t mi = smask_of(a.smask, i);
+            const bool tb = lane < a.T && ((subp >> lane) & 1ull) && slot_has(mi, lane) &&
+                            a.gsel[slot_idx(mi, lane, a.E, re)];
             const uint64_t tmask = __ballot(tb);
             if (!tmask) continue;
             n_walk += (lane == 0);
@@ -1476,8 +1498,9 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
                       vd != GSIM_VERDICT_SIGNATURE ? kTraceCopy : (uint8_t)GSIM_TRACE_REJECT_MESSAGE, vd);
         const bool inv = vd != GSIM_VERDICT_ACCEPT;
         const bool pen = verdict_penalises(vd);
-        const int64_t ir = (int64_t)t * a.E + r;
-        const bool sc = tp->scored && (ds & GSIM_DS_TRACKED);
+        const uint64_t mi = smask_of(a.smask, i);               // the record sits in the sender's row
+        const int64_t ir = slot_idx(mi, t, a.E, r);
+        const bool sc = tp->scored && (ds & GSIM_DS_TRACKED) && slot_has(mi, t);
         const uint8_t tf = a.tflags[ir];
         const int64_t window = tp->mesh_message_deliveries_window_ns;
         uint64_t* cellp = a.cell + (int64_t)m * a.CN + (p - a.clo);
@@ -1586,7 +1609,9 @@ __global__ __launch_bounds__(256) void k_vq_apply(RoundArgs a, int pl)
         const uint32_t e = (uint32_t)v, kind = (uint32_t)(v >> 40);
         const int32_t t = (int32_t)((v >> 32) & 0xFFu);
         if (!(a.dstate[e] & GSIM_DS_TRACKED)) continue;
-        const int64_t ir = (int64_t)t * a.E + e;
+        const uint64_t mj = smask_of(a.smask, a.owner[e]);     // the sender's row
+        if (!slot_has(mj, t)) continue;
+        const int64_t ir = slot_idx(mj, t, a.E, e);
         if (kind == kVqInv) { atomicAdd(&a.invalid[ir], 1.0); continue; }
         const ctp_t tp = tpa + t;
         // the winner's own copy was queued as kVqDup too: its kVqFirst adds
@@ -1709,6 +1734,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.now = a.t0 + (g / a.R) * a.hb + (g % a.R + 1) * a.hb / (a.R + 1);
     a.row_ptr = h->d_row_ptr; a.col = h->d_col;
     a.dstate = h->d_dstate; a.mflags = h->d_mflags;
+    a.smask = h->d_smask; a.owner = h->d_owner;
     a.tflags = h->d_tflags; a.tp = h->d_tp;
     a.first = h->d_first; a.meshd = h->d_meshd; a.invalid = h->d_invalid; a.mcnt = h->d_mcnt;
     a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv; a.mid = d->d_mid;
@@ -1834,7 +1860,7 @@ static bool ihave_prepare(gsim_handle* h, int64_t g, IhaveStage* st, int* rc)
     a.N = h->n; a.E = h->e; a.T = h->t; a.ring = d->cfg.ring; a.R = d->cfg.rounds;
     a.g = g; a.tick = tick;
     a.lo_round = (int32_t)std::max<int64_t>((tick - h->gp.history_gossip) * d->cfg.rounds, 0);
-    a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.rev = h->d_rev; a.sub = h->d_sub;
+    a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.rev = h->d_rev; a.sub = h->d_sub; a.smask = h->d_smask;
     a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv;
     a.mlat = d->lat_on ? d->d_mlat : nullptr;
     a.cell = d->d_cell; a.slot_last = d->d_slot_last;
@@ -2149,7 +2175,8 @@ int deliver_round_send(gsim_handle* h, int64_t round)
             // version: rebuild them all
             hipLaunchKernelGGL(k_mesh_mask, dim3((uint32_t)std::min<int64_t>((h->n + 3) / 4, 65536)), dim3(256), 0,
                                h->stream, (const uint32_t*)h->d_row_ptr, (const uint32_t*)h->d_col,
-                               (const uint8_t*)h->d_mflags, (const uint8_t*)h->d_direct, h->n, h->e,
+                               (const uint8_t*)h->d_mflags, (const uint8_t*)h->d_direct,
+                               (const uint64_t*)h->d_smask, h->n, h->e,
                                std::max(1, h->t), (uint32_t)h->olo(), (uint32_t)h->ohi(), d->d_mmask);
             d->mask_version = h->mesh_version;
         }
@@ -2371,6 +2398,20 @@ void deliver_blocks_changed(gsim_handle* h)
 
 int32_t* deliver_slot_last(gsim_handle* h) { return h->dl ? h->dl->d_slot_last : nullptr; }
 
+uint8_t** deliver_gsel_slot(gsim_handle* h)
+{
+    static uint8_t* none = nullptr;
+    return h->dl ? &h->dl->d_gsel : &none;
+}
+
+// The topic slot masks grew (ensure_slots): the arrays were re-laid out; the
+// delivery's mesh masks are rebuilt from the moved router flags.
+int slots_changed(gsim_handle* h)
+{
+    if (h->dl) h->dl->mask_version = 0;
+    return GSIM_OK;
+}
+
 extern "C" {
 
 int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
@@ -2425,7 +2466,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     }
     d->resp_cap = cfg->max_arrivals > 0 ? cfg->max_arrivals : std::max<int64_t>(8 * h->n, 1 << 20);
     A((void**)&d->d_slot_last, ring * 4);
-    A((void**)&d->d_gsel, T * (size_t)h->e);
+    A((void**)&d->d_gsel, (size_t)std::max(1, h->S) * (size_t)h->e);
     A((void**)&d->d_gcount, 2 * ring * 4);
     A((void**)&d->d_gstate, (size_t)h->e);
     A((void**)&d->d_resp, (size_t)d->resp_cap * 8);
@@ -2461,7 +2502,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     if (e == hipSuccess) e = hipMemsetAsync(d->d_nnew, 0, 2 * words * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_stats, 0, 4 * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_slot_last, 0xFF, ring * 4, h->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(d->d_gsel, 0, T * (size_t)h->e, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_gsel, 0, (size_t)std::max(1, h->S) * (size_t)h->e, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_gstate, 0, (size_t)h->e, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_nresp, 0, 4 * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_peertx, 0, ring * (size_t)d->ptx_w, h->stream);
@@ -2505,6 +2546,21 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
     if (std::adjacent_find(slots.begin(), slots.end()) != slots.end()) {
         h->err = "two messages of one publish batch share a ring slot";
         return GSIM_EINVAL;
+    }
+    if (!h->smask.empty()) {
+        // an origin outside its topic publishes to its fanout: that state
+        // lives in its topic slots
+        std::vector<uint64_t> need;
+        for (int32_t m = 0; m < count; ++m) {
+            const uint32_t o = msgs[m].origin;
+            if ((int64_t)o >= h->n || ((h->smask[o] >> msgs[m].topic) & 1ull)) continue;
+            if (need.empty()) need.assign((size_t)h->n, 0);
+            need[o] |= 1ull << msgs[m].topic;
+        }
+        if (!need.empty()) {
+            const int rc = ensure_slots(h, need.data());
+            if (rc) return rc;
+        }
     }
     hipError_t e = hipSuccess;
     if (count > d->pub_cap) {

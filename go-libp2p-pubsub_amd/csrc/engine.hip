@@ -54,8 +54,10 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
             a.bp[e] = 0.0;
             a.expire[e] = 0;
             a.pen[e] = 0;
+            const uint64_t mj = smask_of(a.smask, a.owner[e]);
             for (int32_t t = 0; t < a.T; ++t) {
-                const int64_t i = (int64_t)t * a.E + e;
+                if (!slot_has(mj, t)) continue;
+                const int64_t i = slot_idx(mj, t, a.E, e);
                 a.first[i] = 0.0; a.meshd[i] = 0.0; a.fail[i] = 0.0; a.invalid[i] = 0.0; a.mcnt[i] = 0;
                 a.graft[i] = 0; a.mtime[i] = 0; a.tflags[i] = 0;
             }
@@ -66,12 +68,14 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
         const bool decay = REFRESH && conn;   // retained scores are not decayed
         // topics the observer joined (the others hold zero records: skipping
         // them leaves every value and the score's sum unchanged)
-        const uint64_t joined = a.skip_unjoined ? a.sub[a.col[e]] : ~0ull;
+        // ... and the topics the neighbour (the row owner) holds a slot for
+        const uint64_t mj = smask_of(a.smask, a.owner[e]);
+        const uint64_t joined = (a.skip_unjoined ? a.sub[a.col[e]] : ~0ull) & mj;
         double score = 0.0;
         for (int32_t t = 0; t < a.T; ++t) {
             const ctp_t tp = const_tp(a.tp) + t;
             if (!tp->scored || !((joined >> t) & 1ull)) continue;
-            const int64_t i = (int64_t)t * a.E + e;
+            const int64_t i = slot_idx(mj, t, a.E, e);
             double first = a.first[i], meshd = a.meshd[i], fail = a.fail[i], inval = a.invalid[i];
             uint8_t fl = a.tflags[i];
             int64_t mt = 0;
@@ -216,15 +220,19 @@ __global__ __launch_bounds__(256) void k_ip_colocation(ColocArgs a)
     }
 }
 
-// SetTopicScoreParams recap (score.go:224-238).
-__global__ __launch_bounds__(256) void k_recap(int64_t E, const uint8_t* estate, double* first, double* meshd,
+// SetTopicScoreParams recap (score.go:224-238) of topic t.
+__global__ __launch_bounds__(256) void k_recap(int64_t E, const uint8_t* estate, const uint32_t* owner,
+                                               const uint64_t* smask, int32_t t, double* first, double* meshd,
                                                double first_cap, double mesh_cap, int do_first, int do_mesh)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride) {
         if (!(estate[e] & GSIM_ES_TRACKED)) continue;
-        if (do_first && first[e] > first_cap) first[e] = first_cap;
-        if (do_mesh && meshd[e] > mesh_cap) meshd[e] = mesh_cap;
+        const uint64_t m = smask_of(smask, owner[e]);
+        if (!slot_has(m, t)) continue;
+        const int64_t i = slot_idx(m, t, E, e);
+        if (do_first && first[i] > first_cap) first[i] = first_cap;
+        if (do_mesh && meshd[i] > mesh_cap) meshd[i] = mesh_cap;
     }
 }
 
@@ -233,11 +241,13 @@ __global__ __launch_bounds__(256) void k_recap(int64_t E, const uint8_t* estate,
 __global__ __launch_bounds__(256) void k_apply_mcnt(ScoreArgs a)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const int64_t total = a.E * (int64_t)a.T;
+    const int64_t total = a.E * (int64_t)a.S;
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += stride) {
         const uint8_t n = a.mcnt[x];
         if (!n) continue;
-        const int32_t t = (int32_t)(x / a.E);
+        const int32_t p = (int32_t)(x / a.E);
+        const int32_t t = a.smask ? slot_topic(a.smask[a.owner[x - (int64_t)p * a.E]], p) : p;
+        if (t < 0) continue;
         a.meshd[x] = apply_incs(a.meshd[x], n, const_tp(a.tp)[t].mesh_message_deliveries_cap);
         a.mcnt[x] = 0;
     }
@@ -260,12 +270,18 @@ __global__ __launch_bounds__(256) void k_fill_synthetic(ScoreArgs a, uint64_t se
         // topics both endpoints joined: only there can a mesh link or
         // deliveries exist (owner[e] = observer, owner[r] = neighbour)
         const uint64_t shared = a.sub ? a.sub[a.owner[e]] & a.sub[a.owner[r]] : ~0ull;
+        // topic slots: the router state of edge e is the observer's (owner[e]),
+        // the record r the neighbour's row's (owner[r])
+        const uint64_t mi = smask_of(a.smask, a.owner[e]), mj = smask_of(a.smask, a.owner[r]);
         for (int32_t t = 0; t < a.T; ++t) {
-            const int64_t i = (int64_t)t * a.E + e;
-            const int64_t ir = (int64_t)t * a.E + r;
+            const int64_t i = slot_idx(mi, t, a.E, e);
+            const int64_t ir = slot_idx(mj, t, a.E, r);
             if (!((shared >> t) & 1ull)) {
-                a.tflags[ir] = 0; a.mflags[i] = 0; a.graft[ir] = 0; a.mtime[ir] = 0;
-                a.first[ir] = 0.0; a.meshd[ir] = 0.0; a.fail[ir] = 0.0; a.invalid[ir] = 0.0;
+                if (slot_has(mj, t)) {
+                    a.tflags[ir] = 0; a.graft[ir] = 0; a.mtime[ir] = 0;
+                    a.first[ir] = 0.0; a.meshd[ir] = 0.0; a.fail[ir] = 0.0; a.invalid[ir] = 0.0;
+                }
+                if (slot_has(mi, t)) a.mflags[i] = 0;
                 continue;
             }
             const int64_t gi = (int64_t)t * a.E_glob + ge;
@@ -303,10 +319,11 @@ __global__ __launch_bounds__(256) void k_census(ScoreArgs a, unsigned long long*
         if (!(st & GSIM_ES_TRACKED)) continue;
         c[7] += 1;
         if (!(st & GSIM_ES_CONNECTED)) continue;
-        const uint64_t joined = a.skip_unjoined ? a.sub[a.col[e]] : ~0ull;   // records the score pass reads
+        const uint64_t mj = smask_of(a.smask, a.owner[e]);
+        const uint64_t joined = (a.skip_unjoined ? a.sub[a.col[e]] : ~0ull) & mj;   // records the score pass reads
         for (int32_t t = 0; t < a.T; ++t) {
             if (!const_tp(a.tp)[t].scored || !((joined >> t) & 1ull)) continue;
-            const int64_t i = (int64_t)t * a.E + e;
+            const int64_t i = slot_idx(mj, t, a.E, e);
             const uint8_t fl = a.tflags[i];
             c[0] += 1;
             c[1] += (fl & GSIM_TF_IN_MESH) != 0;
@@ -318,8 +335,9 @@ __global__ __launch_bounds__(256) void k_census(ScoreArgs a, unsigned long long*
     }
     for (int64_t e = a.e_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.e_hi; e += stride) {
         if (!(a.rstate[e] & GSIM_ES_CONNECTED)) continue;   // router mesh links (edge order), owned rows
+        const uint64_t mi = smask_of(a.smask, a.owner[e]);
         for (int32_t t = 0; t < a.T; ++t)
-            c[6] += (a.mflags[(int64_t)t * a.E + e] & GSIM_TF_MESH) != 0;
+            if (slot_has(mi, t)) c[6] += (a.mflags[slot_idx(mi, t, a.E, e)] & GSIM_TF_MESH) != 0;
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -342,24 +360,121 @@ __global__ __launch_bounds__(256) void k_gather_rev(const T* __restrict__ in, T*
     }
 }
 
+// The ABI's dense view [npar][T][E] (edge order) of a topic-slot array
+// [npar][S][E]: view index e of topic t is device index
+// x = rev[e] (record order; rev == nullptr: edge order), in the plane of t's
+// slot of x's row owner.  Entries outside the masks read as zero.
+template <typename T>
+__global__ __launch_bounds__(256) void k_view_read(const T* __restrict__ dev, T* __restrict__ view,
+                                                   const uint32_t* rev, const uint32_t* owner, const uint64_t* smask,
+                                                   int64_t E, int32_t nT, int32_t S, int64_t total)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t TE = (int64_t)nT * E;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += stride) {
+        const int64_t par = v / TE, rem = v - par * TE;
+        const int32_t t = (int32_t)(rem / E);
+        const int64_t e = rem - (int64_t)t * E;
+        const int64_t x = rev ? (int64_t)rev[e] : e;
+        const uint64_t m = smask_of(smask, owner[x]);
+        view[v] = slot_has(m, t) ? dev[par * (int64_t)S * E + slot_idx(m, t, E, x)] : (T)0;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_view_write(const T* __restrict__ view, T* __restrict__ dev,
+                                                    const uint32_t* rev, const uint32_t* owner, const uint64_t* smask,
+                                                    int64_t E, int32_t nT, int32_t S, int64_t total)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t TE = (int64_t)nT * E;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += stride) {
+        const int64_t par = v / TE, rem = v - par * TE;
+        const int32_t t = (int32_t)(rem / E);
+        const int64_t e = rem - (int64_t)t * E;
+        const int64_t x = rev ? (int64_t)rev[e] : e;
+        const uint64_t m = smask_of(smask, owner[x]);
+        if (slot_has(m, t)) dev[par * (int64_t)S * E + slot_idx(m, t, E, x)] = view[v];
+    }
+}
+
+// The slots a written view needs: bit t for both endpoints of every edge
+// with a non-zero entry (a mesh link, control or record of a topic implies
+// both ends hold it; a record lives in one endpoint's row, the router state
+// in the other's, and replies go back the other way).
+template <typename T>
+__global__ __launch_bounds__(256) void k_view_need(const T* __restrict__ view, const uint32_t* rev,
+                                                   const uint32_t* owner, int64_t E, int32_t nT, int64_t total,
+                                                   unsigned long long* need)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t TE = (int64_t)nT * E;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += stride) {
+        const T val = view[v];
+        if (val == (T)0) continue;
+        const int64_t par = v / TE, rem = v - par * TE;
+        const int32_t t = (int32_t)(rem / E);
+        const int64_t e = rem - (int64_t)t * E;
+        const unsigned long long bit = 1ull << t;
+        atomicOr(&need[owner[e]], bit);
+        atomicOr(&need[owner[rev[e]]], bit);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_tflags_compose(const uint8_t* rec, const uint8_t* mf, uint8_t* out,
-                                                        const uint32_t* rev, int64_t E, int64_t total)
+                                                        const uint32_t* rev, const uint32_t* owner,
+                                                        const uint64_t* smask, int64_t E, int64_t total)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += stride) {
-        const int64_t p = x / E, e = x - p * E;
-        out[x] = (uint8_t)((rec[p * E + rev[e]] & (GSIM_TF_IN_MESH | GSIM_TF_ACTIVE)) | (mf[x] & (GSIM_TF_MESH | GSIM_TF_FANOUT)));
+        const int32_t t = (int32_t)(x / E);
+        const int64_t e = x - (int64_t)t * E, r = rev[e];
+        const uint64_t mr = smask_of(smask, owner[r]), me = smask_of(smask, owner[e]);
+        const uint8_t a = slot_has(mr, t) ? rec[slot_idx(mr, t, E, r)] : 0;
+        const uint8_t b = slot_has(me, t) ? mf[slot_idx(me, t, E, e)] : 0;
+        out[x] = (uint8_t)((a & (GSIM_TF_IN_MESH | GSIM_TF_ACTIVE)) | (b & (GSIM_TF_MESH | GSIM_TF_FANOUT)));
     }
 }
 
 __global__ __launch_bounds__(256) void k_tflags_split(const uint8_t* in, uint8_t* rec, uint8_t* mf,
-                                                      const uint32_t* rev, int64_t E, int64_t total)
+                                                      const uint32_t* rev, const uint32_t* owner,
+                                                      const uint64_t* smask, int64_t E, int64_t total)
+{
+    // thread per (t, x): x both the record index (score bits of view entry
+    // rev[x]) and the edge index (router bits of view entry x)
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < total; v += stride) {
+        const int32_t t = (int32_t)(v / E);
+        const int64_t x = v - (int64_t)t * E;
+        const uint64_t m = smask_of(smask, owner[x]);
+        if (!slot_has(m, t)) continue;
+        const int64_t i = slot_idx(m, t, E, x);
+        rec[i] = (uint8_t)(in[(int64_t)t * E + rev[x]] & (GSIM_TF_IN_MESH | GSIM_TF_ACTIVE));
+        mf[i] = (uint8_t)(in[v] & (GSIM_TF_MESH | GSIM_TF_FANOUT));
+    }
+}
+
+// Re-layout of a topic-slot array [npar][S0][E] -> [npar][S1][E] when slot
+// masks grow (ensure_slots): old mask m0, new m1 of each row owner.
+template <typename T>
+__global__ __launch_bounds__(256) void k_slot_relayout(const T* __restrict__ src, T* __restrict__ dst,
+                                                       const uint32_t* owner, const uint64_t* m0s, const uint64_t* m1s,
+                                                       int64_t E, int32_t S0, int32_t S1, int32_t npar)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += stride) {
-        const int64_t p = x / E, e = x - p * E;
-        rec[x] = (uint8_t)(in[p * E + rev[e]] & (GSIM_TF_IN_MESH | GSIM_TF_ACTIVE));
-        mf[x] = (uint8_t)(in[x] & (GSIM_TF_MESH | GSIM_TF_FANOUT));
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < E; x += stride) {
+        const uint32_t o = owner[x];
+        const uint64_t m0 = smask_of(m0s, o), m1 = smask_of(m1s, o);
+        for (int32_t par = 0; par < npar; ++par) {
+            const T* s0 = src + (int64_t)par * S0 * E;
+            T* s1 = dst + (int64_t)par * S1 * E;
+            int32_t p1 = 0;
+            for (uint64_t b = m1; b; b &= b - 1, ++p1) {
+                const int32_t t = __builtin_ctzll(b);
+                s1[(int64_t)p1 * E + x] = slot_has(m0, t) ? s0[slot_idx(m0, t, E, x)] : (T)0;
+            }
+            for (; p1 < S1; ++p1) s1[(int64_t)p1 * E + x] = (T)0;
+        }
     }
 }
 
@@ -448,6 +563,9 @@ void free_graph(gsim_handle* h)
     dfree(h->d_graft); dfree(h->d_mtime); dfree(h->d_tflags); dfree(h->d_mflags);
     dfree(h->d_bp); dfree(h->d_estate); dfree(h->d_expire); dfree(h->d_p6); dfree(h->d_ipkey); dfree(h->d_churn); h->churn_cap = 0; dfree(h->d_score);
     dfree(h->d_backoff); dfree(h->d_rstate); dfree(h->d_dstate); dfree(h->d_mcnt); dfree(h->d_pen);
+    dfree(h->d_smask);
+    h->smask.clear();
+    h->S = 0;
     h->bytes_allocated = 0;
     h->n = h->e = 0;
 }
@@ -459,6 +577,8 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     a.T = h->t;
     a.sub = h->d_sub;
     a.col = h->d_col;
+    a.smask = h->d_smask;
+    a.S = h->S;
     // (the subscription gather costs ≈1 ms per pass at C3, where nothing is skipped)
     a.skip_unjoined = (h->unjoined_zero && !h->all_joined) ? 1 : 0;
     a.tp = h->d_tp;
@@ -581,9 +701,76 @@ int materialize_mcnt(gsim_handle* h)
 {
     if (!h->mcnt_dirty) return GSIM_OK;
     ScoreArgs a = make_score_args(h, 0);
-    hipLaunchKernelGGL(k_apply_mcnt, dim3(grid_for(h->e * (int64_t)std::max(1, h->t))), dim3(256), 0, h->stream, a);
+    hipLaunchKernelGGL(k_apply_mcnt, dim3(grid_for(h->e * (int64_t)std::max(1, h->S))), dim3(256), 0, h->stream, a);
     h->mcnt_dirty = false;
     return hip_check(h, hipGetLastError(), "k_apply_mcnt");
+}
+
+// Grow the topic slot masks to cover need[]: every topic
+// array is re-laid out into S' planes (one array at a time, so the extra
+// memory is one array).  Called for the topics an ABI write, a publication
+// by a peer outside its topic (fanout) or a Join brings; a dense handle has
+// every slot already.
+template <typename T>
+static int relayout_one(gsim_handle* h, T** p, int32_t npar, const uint64_t* m0, const uint64_t* m1, int32_t S0,
+                        int32_t S1)
+{
+    if (!*p) return GSIM_OK;
+    T* q = nullptr;
+    hipError_t e = hipMalloc((void**)&q, sizeof(T) * (size_t)npar * (size_t)S1 * (size_t)std::max<int64_t>(h->e, 1));
+    if (e != hipSuccess) return hip_check(h, e, "slot re-layout");
+    hipLaunchKernelGGL(k_slot_relayout<T>, dim3(grid_for(h->e)), dim3(256), 0, h->stream, (const T*)*p, q,
+                       (const uint32_t*)h->d_owner, m0, m1, h->e, S0, S1, npar);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) { (void)hipFree(q); return hip_check(h, e, "k_slot_relayout"); }
+    (void)hipFree(*p);
+    *p = q;
+    h->bytes_allocated += sizeof(T) * (size_t)npar * (size_t)(S1 - S0) * (size_t)h->e;
+    return GSIM_OK;
+}
+
+int ensure_slots(gsim_handle* h, const uint64_t* need)
+{
+    if (!h->d_smask || h->smask.empty()) return GSIM_OK;     // dense: every topic has its plane
+    const uint64_t tmask = h->t >= 64 ? ~0ull : ((1ull << h->t) - 1);
+    std::vector<uint64_t> m1(h->smask);
+    bool grown = false;
+    int32_t S1 = h->S;
+    for (size_t i = 0; i < m1.size(); ++i) {
+        const uint64_t x = m1[i] | (need[i] & tmask);
+        if (x != m1[i]) { m1[i] = x; grown = true; }
+        S1 = std::max(S1, __builtin_popcountll(x));
+    }
+    if (!grown) return GSIM_OK;
+    int rc = deliver_flush(h);
+    if (!rc) rc = materialize_mcnt(h);
+    if (rc) return rc;
+    uint64_t* d1 = nullptr;
+    hipError_t e = hipMalloc((void**)&d1, sizeof(uint64_t) * m1.size());
+    if (e == hipSuccess) e = hipMemcpyAsync(d1, m1.data(), sizeof(uint64_t) * m1.size(), hipMemcpyHostToDevice, h->stream);
+    if (e != hipSuccess) { if (d1) (void)hipFree(d1); return hip_check(h, e, "slot masks"); }
+    const uint64_t* d0 = h->d_smask;
+    const int32_t S0 = h->S;
+    rc = relayout_one(h, &h->d_first, 1, d0, d1, S0, S1);
+    if (!rc) rc = relayout_one(h, &h->d_meshd, 1, d0, d1, S0, S1);
+    if (!rc) rc = relayout_one(h, &h->d_fail, 1, d0, d1, S0, S1);
+    if (!rc) rc = relayout_one(h, &h->d_invalid, 1, d0, d1, S0, S1);
+    if (!rc) rc = relayout_one(h, &h->d_graft, 1, d0, d1, S0, S1);
+    if (!rc) rc = relayout_one(h, &h->d_mtime, 1, d0, d1, S0, S1);
+    if (!rc) rc = relayout_one(h, &h->d_tflags, 1, d0, d1, S0, S1);
+    if (!rc) rc = relayout_one(h, &h->d_mcnt, 1, d0, d1, S0, S1);
+    if (!rc) rc = relayout_one(h, &h->d_mflags, 1, d0, d1, S0, S1);
+    if (!rc) rc = relayout_one(h, &h->d_backoff, 1, d0, d1, S0, S1);
+    if (!rc) rc = relayout_one(h, extra_ctl_slot(h), 2, d0, d1, S0, S1);
+    if (!rc) rc = relayout_one(h, deliver_gsel_slot(h), 1, d0, d1, S0, S1);
+    if (rc) { (void)hipFree(d1); return rc; }
+    (void)hipFree(h->d_smask);
+    h->d_smask = d1;
+    h->smask.swap(m1);
+    h->S = S1;
+    h->mesh_version++;
+    return slots_changed(h);
 }
 
 // ---------------------------------------------------------------------------
@@ -602,17 +789,28 @@ static int read_field_impl(gsim_handle* h, const FieldRef& r, void* dst)
     e = hipMalloc(&tmp, std::max<size_t>(r.bytes, 8));
     if (e != hipSuccess) return hip_check(h, e, "gsim_read_field scratch");
     const int64_t E = h->e;
-    const int64_t total = r.kind == FK_RECORD ? (int64_t)(r.bytes / (size_t)r.elem) : (int64_t)r.bytes;
+    const int32_t T = std::max(1, h->t);
+    const int64_t total = (int64_t)(r.bytes / (size_t)r.elem);
     const int g = grid_for(total);
+    const uint32_t* rev = r.kind == FK_TRECORD ? h->d_rev : nullptr;
     if (r.kind == FK_RECORD && r.elem == 8)
         hipLaunchKernelGGL(k_gather_rev<uint64_t>, dim3(g), dim3(256), 0, h->stream, (const uint64_t*)r.ptr,
                            (uint64_t*)tmp, (const uint32_t*)h->d_rev, E, total);
     else if (r.kind == FK_RECORD || r.kind == FK_ESTATE)
         hipLaunchKernelGGL(k_gather_rev<uint8_t>, dim3(g), dim3(256), 0, h->stream, (const uint8_t*)r.ptr,
                            (uint8_t*)tmp, (const uint32_t*)h->d_rev, E, total);
+    else if ((r.kind == FK_TRECORD || r.kind == FK_TEDGE) && r.elem == 8)
+        hipLaunchKernelGGL(k_view_read<uint64_t>, dim3(g), dim3(256), 0, h->stream, (const uint64_t*)r.ptr,
+                           (uint64_t*)tmp, rev, (const uint32_t*)h->d_owner, (const uint64_t*)h->d_smask, E, T, h->S,
+                           total);
+    else if (r.kind == FK_TRECORD || r.kind == FK_TEDGE)
+        hipLaunchKernelGGL(k_view_read<uint8_t>, dim3(g), dim3(256), 0, h->stream, (const uint8_t*)r.ptr,
+                           (uint8_t*)tmp, rev, (const uint32_t*)h->d_owner, (const uint64_t*)h->d_smask, E, T, h->S,
+                           total);
     else
         hipLaunchKernelGGL(k_tflags_compose, dim3(g), dim3(256), 0, h->stream, (const uint8_t*)h->d_tflags,
-                           (const uint8_t*)h->d_mflags, (uint8_t*)tmp, (const uint32_t*)h->d_rev, E, total);
+                           (const uint8_t*)h->d_mflags, (uint8_t*)tmp, (const uint32_t*)h->d_rev,
+                           (const uint32_t*)h->d_owner, (const uint64_t*)h->d_smask, E, total);
     e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpyAsync(dst, tmp, r.bytes, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
@@ -620,22 +818,60 @@ static int read_field_impl(gsim_handle* h, const FieldRef& r, void* dst)
     return hip_check(h, e, "gsim_read_field");
 }
 
+// The slots a topic-array view written through the ABI needs (its non-zero
+// entries), then grow the masks to cover them (ensure_slots).
+static int view_slots(gsim_handle* h, const FieldRef& r, const void* dview)
+{
+    if (!h->d_smask) return GSIM_OK;                      // dense: every topic has its plane
+    const int64_t E = h->e;
+    const int32_t T = std::max(1, h->t);
+    const int64_t total = (int64_t)(r.bytes / (size_t)r.elem);
+    unsigned long long* need = nullptr;
+    hipError_t e = hipMalloc((void**)&need, sizeof(uint64_t) * (size_t)std::max<int64_t>(h->n, 1));
+    if (e == hipSuccess) e = hipMemsetAsync(need, 0, sizeof(uint64_t) * (size_t)h->n, h->stream);
+    const uint32_t* rev = h->d_rev;
+    const int g = grid_for(total);
+    if (e == hipSuccess) {
+        if (r.elem == 8)
+            hipLaunchKernelGGL(k_view_need<uint64_t>, dim3(g), dim3(256), 0, h->stream, (const uint64_t*)dview, rev,
+                               (const uint32_t*)h->d_owner, E, T, total, need);
+        else
+            hipLaunchKernelGGL(k_view_need<uint8_t>, dim3(g), dim3(256), 0, h->stream, (const uint8_t*)dview, rev,
+                               (const uint32_t*)h->d_owner, E, T, total, need);
+        e = hipGetLastError();
+    }
+    std::vector<uint64_t> host((size_t)h->n);
+    if (e == hipSuccess) e = hipMemcpyAsync(host.data(), need, sizeof(uint64_t) * (size_t)h->n, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (need) (void)hipFree(need);
+    if (e != hipSuccess) return hip_check(h, e, "slot needs");
+    return ensure_slots(h, host.data());
+}
+
 // Install a field given in the ABI's edge-order view.
-static int write_field_impl(gsim_handle* h, const FieldRef& r, const void* src)
+static int write_field_impl(gsim_handle* h, int32_t f, const FieldRef& r0, const void* src)
 {
     hipError_t e = hipSuccess;
-    if (r.kind == FK_RAW) {
-        e = hipMemcpyAsync(r.ptr, src, r.bytes, hipMemcpyHostToDevice, h->stream);
+    if (r0.kind == FK_RAW) {
+        e = hipMemcpyAsync(r0.ptr, src, r0.bytes, hipMemcpyHostToDevice, h->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
         return hip_check(h, e, "gsim_write_field");
     }
     void* tmp = nullptr;
-    e = hipMalloc(&tmp, std::max<size_t>(r.bytes, 8));
+    e = hipMalloc(&tmp, std::max<size_t>(r0.bytes, 8));
     if (e != hipSuccess) return hip_check(h, e, "gsim_write_field scratch");
-    e = hipMemcpyAsync(tmp, src, r.bytes, hipMemcpyHostToDevice, h->stream);
+    e = hipMemcpyAsync(tmp, src, r0.bytes, hipMemcpyHostToDevice, h->stream);
+    FieldRef r = r0;
+    if (e == hipSuccess && (r.kind == FK_TRECORD || r.kind == FK_TEDGE || r.kind == FK_TFLAGS)) {
+        const int rc = view_slots(h, r, tmp);
+        if (rc) { (void)hipFree(tmp); return rc; }
+        field_ref(h, f, &r);      // the arrays may have moved (re-laid out for new slots)
+    }
     const int64_t E = h->e;
-    const int64_t total = r.kind == FK_RECORD ? (int64_t)(r.bytes / (size_t)r.elem) : (int64_t)r.bytes;
+    const int32_t T = std::max(1, h->t);
+    const int64_t total = (int64_t)(r.bytes / (size_t)r.elem);
     const int g = grid_for(total);
+    const uint32_t* rev = r.kind == FK_TRECORD ? h->d_rev : nullptr;
     if (e == hipSuccess) {
         if (r.kind == FK_RECORD && r.elem == 8)
             hipLaunchKernelGGL(k_gather_rev<uint64_t>, dim3(g), dim3(256), 0, h->stream, (const uint64_t*)tmp,
@@ -646,9 +882,18 @@ static int write_field_impl(gsim_handle* h, const FieldRef& r, const void* src)
         else if (r.kind == FK_ESTATE)
             hipLaunchKernelGGL(k_estate_split, dim3(g), dim3(256), 0, h->stream, (const uint8_t*)tmp,
                                h->d_estate, h->d_rstate, (const uint32_t*)h->d_rev, E);
+        else if ((r.kind == FK_TRECORD || r.kind == FK_TEDGE) && r.elem == 8)
+            hipLaunchKernelGGL(k_view_write<uint64_t>, dim3(g), dim3(256), 0, h->stream, (const uint64_t*)tmp,
+                               (uint64_t*)r.ptr, rev, (const uint32_t*)h->d_owner, (const uint64_t*)h->d_smask, E, T,
+                               h->S, total);
+        else if (r.kind == FK_TRECORD || r.kind == FK_TEDGE)
+            hipLaunchKernelGGL(k_view_write<uint8_t>, dim3(g), dim3(256), 0, h->stream, (const uint8_t*)tmp,
+                               (uint8_t*)r.ptr, rev, (const uint32_t*)h->d_owner, (const uint64_t*)h->d_smask, E, T,
+                               h->S, total);
         else
-            hipLaunchKernelGGL(k_tflags_split, dim3(g), dim3(256), 0, h->stream, (const uint8_t*)tmp, h->d_tflags,
-                               h->d_mflags, (const uint32_t*)h->d_rev, E, total);
+            hipLaunchKernelGGL(k_tflags_split, dim3(grid_for((int64_t)T * E)), dim3(256), 0, h->stream,
+                               (const uint8_t*)tmp, h->d_tflags, h->d_mflags, (const uint32_t*)h->d_rev,
+                               (const uint32_t*)h->d_owner, (const uint64_t*)h->d_smask, E, (int64_t)T * E);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
@@ -815,7 +1060,24 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     h->n = n;
     h->e = E;
     h->n_ips = n_ips;
-    const int64_t ET = E * (int64_t)std::max(1, h->t);
+    // topic slots: the announced topics of every peer; all of
+    // them when every peer joined every topic (or none announced any: a
+    // caller without subscriptions gets the dense layout)
+    const uint64_t tmask_all = h->t >= 64 ? ~0ull : ((1ull << h->t) - 1);
+    bool dense_slots = !subs;
+    if (subs) {
+        bool all = true;
+        for (int64_t i = 0; all && i < n; ++i) all = (subs[i] & tmask_all) == tmask_all;
+        dense_slots = all;
+    }
+    h->S = std::max(1, h->t);
+    if (!dense_slots) {
+        h->smask.assign(subs, subs + n);
+        int32_t S = 1;
+        for (int64_t i = 0; i < n; ++i) S = std::max(S, __builtin_popcountll(h->smask[(size_t)i]));
+        h->S = S;
+    }
+    const int64_t ET = E * (int64_t)h->S;
     const int64_t nip = ip_ptr ? ip_ptr[n] : 0;
     int rc = GSIM_OK;
     rc = rc ? rc : dalloc(h, &h->d_row_ptr, n + 1);
@@ -847,6 +1109,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     rc = rc ? rc : dalloc(h, &h->d_expire, E);
     rc = rc ? rc : dalloc(h, &h->d_p6, E);
     rc = rc ? rc : dalloc(h, &h->d_score, E);
+    if (!dense_slots) rc = rc ? rc : dalloc(h, &h->d_smask, n);
     if (rc) { std::string m = h->err; free_graph(h); h->err = m; return rc; }
 
     hipStream_t s = h->stream;
@@ -862,6 +1125,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     up(h->d_rev, rev.data(), sizeof(uint32_t) * (size_t)E);
     up(h->d_owner, owner.data(), sizeof(uint32_t) * (size_t)E);
     if (subs) up(h->d_sub, subs, sizeof(uint64_t) * (size_t)n); else zero(h->d_sub, sizeof(uint64_t) * (size_t)n);
+    if (!dense_slots) up(h->d_smask, h->smask.data(), sizeof(uint64_t) * (size_t)n);
     {
         // every peer joined every topic: the score pass has nothing to skip
         const uint64_t tmask = h->t >= 64 ? ~0ull : ((1ull << h->t) - 1);
@@ -1002,10 +1266,9 @@ int gsim_set_topic_params(gsim_handle* h, int32_t t, const gsim_topic_score_para
         const int df = p->first_message_deliveries_cap < old.first_message_deliveries_cap;
         const int dm = p->mesh_message_deliveries_cap < old.mesh_message_deliveries_cap;
         if (df || dm) {
-            const int64_t off = (int64_t)t * h->e;
             hipLaunchKernelGGL(k_recap, dim3(grid_for(h->e)), dim3(256), 0, h->stream, h->e, h->d_estate,
-                               h->d_first + off, h->d_meshd + off, p->first_message_deliveries_cap,
-                               p->mesh_message_deliveries_cap, df, dm);
+                               (const uint32_t*)h->d_owner, (const uint64_t*)h->d_smask, t, h->d_first,
+                               h->d_meshd, p->first_message_deliveries_cap, p->mesh_message_deliveries_cap, df, dm);
             e = hipGetLastError();
         }
     }
@@ -1145,8 +1408,10 @@ int gsim_write_field(gsim_handle* h, int32_t f, const void* src, size_t bytes)
     if (r.kind == FK_SEEN) { h->err = "the seen-set is read-only"; return GSIM_EINVAL; }
     int rc = deliver_flush(h);
     if (!rc) rc = materialize_mcnt(h);
+    // fanout state lives in the publisher's topic slots
+    if (!rc && f == GSIM_F_FANOUT_TOPICS) rc = ensure_slots(h, (const uint64_t*)src);
     if (rc) return rc;
-    rc = write_field_impl(h, r, src);
+    rc = write_field_impl(h, f, r, src);
     h->unjoined_zero = false;    // arbitrary state: no record may be skipped
     if (!rc) rc = extra_field_written(h, f);
     if (f == GSIM_F_ESTATE) { h->p6_dirty = true; h->maybe_retained = true; h->score_version++;
@@ -1245,19 +1510,19 @@ bool field_ref(gsim_handle* h, int32_t f, FieldRef* r)
 {
     const size_t E = (size_t)h->e, ET = E * (size_t)std::max(1, h->t);
     switch (f) {
-    case GSIM_F_FIRST:      *r = {h->d_first, ET * 8, FK_RECORD, 8}; return true;
-    case GSIM_F_MESHD:      *r = {h->d_meshd, ET * 8, FK_RECORD, 8}; return true;
-    case GSIM_F_FAIL:       *r = {h->d_fail, ET * 8, FK_RECORD, 8}; return true;
-    case GSIM_F_INVALID:    *r = {h->d_invalid, ET * 8, FK_RECORD, 8}; return true;
-    case GSIM_F_GRAFT_TIME: *r = {h->d_graft, ET * 8, FK_RECORD, 8}; return true;
-    case GSIM_F_MESH_TIME:  *r = {h->d_mtime, ET * 8, FK_RECORD, 8}; return true;
+    case GSIM_F_FIRST:      *r = {h->d_first, ET * 8, FK_TRECORD, 8}; return true;
+    case GSIM_F_MESHD:      *r = {h->d_meshd, ET * 8, FK_TRECORD, 8}; return true;
+    case GSIM_F_FAIL:       *r = {h->d_fail, ET * 8, FK_TRECORD, 8}; return true;
+    case GSIM_F_INVALID:    *r = {h->d_invalid, ET * 8, FK_TRECORD, 8}; return true;
+    case GSIM_F_GRAFT_TIME: *r = {h->d_graft, ET * 8, FK_TRECORD, 8}; return true;
+    case GSIM_F_MESH_TIME:  *r = {h->d_mtime, ET * 8, FK_TRECORD, 8}; return true;
     case GSIM_F_TFLAGS:     *r = {h->d_tflags, ET, FK_TFLAGS, 1}; return true;
     case GSIM_F_BP:         *r = {h->d_bp, E * 8, FK_RECORD, 8}; return true;
     case GSIM_F_ESTATE:     *r = {h->d_estate, E, FK_ESTATE, 1}; return true;
     case GSIM_F_EXPIRE:     *r = {h->d_expire, E * 8, FK_RECORD, 8}; return true;
     case GSIM_F_P6:         *r = {h->d_p6, E * 8, FK_RECORD, 8}; return true;
     case GSIM_F_SCORE:      *r = {h->d_score, E * 8, FK_RECORD, 8}; return true;
-    case GSIM_F_BACKOFF:    *r = {h->d_backoff, ET * 8}; return true;
+    case GSIM_F_BACKOFF:    *r = {h->d_backoff, ET * 8, FK_TEDGE, 8}; return true;
     default: return extra_field_ref(h, f, r) || deliver_field_ref(h, f, r);
     }
 }

@@ -38,6 +38,8 @@ struct ScoreArgs {
     const uint64_t* sub;       // announced topics per peer (fill: records only where both endpoints joined)
     const int32_t* gate;       // non-null: run only if *gate != 0 (a retention purge happened)
     const uint32_t* col;       // col[r]: the observer of record r (record order)
+    const uint64_t* smask;     // topic slots of each row owner (nullptr: dense, slot = topic)
+    int32_t S;                 // planes per topic array
     int32_t skip_unjoined;     // records of topics the observer did not join are zero: skip them
     // sharded network: only records whose observer is owned
     // ([olo, ohi)) are this shard's; the owned rows are local edges [e_lo, e_hi),
@@ -95,6 +97,31 @@ __device__ __forceinline__ int64_t go_div(int64_t n, int64_t d)
     return d > 0 ? div_trunc_pos(n, d) : n / d;
 }
 
+// Topic slots.  Every per-(topic, edge index) array — score
+// records in record order, router state in edge order — holds S planes, not
+// T: the plane of topic t at index x is the rank of t in the slot mask of x's
+// row owner (owner[x]: the neighbour for a record, the observer for router
+// state).  A row owner's mask covers every topic it ever joined or published
+// to, and a record (i about j, t) can only be non-zero if j has t (j
+// forwarded, was grafted for or sent control on t), so nothing outside the
+// masks is ever stored.  All-joined networks keep S = T and smask == nullptr:
+// the plane of t is t, as a dense [T][E] layout.
+__device__ __forceinline__ uint64_t smask_of(const uint64_t* smask, uint32_t owner)
+{
+    return smask ? smask[owner] : ~0ull;
+}
+__device__ __forceinline__ bool slot_has(uint64_t m, int32_t t) { return (m >> t) & 1ull; }
+__device__ __forceinline__ int64_t slot_idx(uint64_t m, int32_t t, int64_t E, int64_t x)
+{
+    return (int64_t)__popcll(m & ((1ull << t) - 1ull)) * E + x;
+}
+// topic of the p-th plane of a row owner with mask m (p < popcount(m))
+__device__ __forceinline__ int32_t slot_topic(uint64_t m, int32_t p)
+{
+    for (int32_t k = 0; k < p; ++k) m &= m - 1;
+    return m ? __builtin_ctzll(m) : -1;
+}
+
 // Topic parameters are read-only for a kernel's lifetime.  Reading them
 // through the constant address space (4) lets the compiler use scalar
 // s_load (scalar cache, lgkmcnt) instead of vector loads that it must order
@@ -109,7 +136,9 @@ __device__ __forceinline__ ctp_t const_tp(const gsim_topic_score_params* p)
 // How a field's ABI (edge-order) view maps onto device memory.
 enum FieldKind : int {
     FK_RAW = 0,      // same layout
-    FK_RECORD,       // record order: view[p][e] = dev[p][rev[e]]
+    FK_RECORD,       // per edge, record order: view[e] = dev[rev[e]]
+    FK_TRECORD,      // topic slots, record order: view[t][e] = dev[slot][rev[e]]
+    FK_TEDGE,        // topic slots, edge order: view[par][t][e] = dev[par][slot][e]
     FK_TFLAGS,       // view = score bits (record order) | router mesh bit (edge order)
     FK_ESTATE,       // record order + router connected mirror (edge order)
     FK_SEEN,         // first-seen rounds: the high words of the 64-bit seen-set cells (read-only)
@@ -117,9 +146,10 @@ enum FieldKind : int {
 
 struct FieldRef {
     void* ptr;
-    size_t bytes;
+    size_t bytes;      // of the ABI view
     int kind = FK_RAW;
-    int elem = 1;      // element size in bytes (FK_RECORD)
+    int elem = 1;      // element size in bytes
+    int npar = 1;      // FK_TEDGE: [npar] sets of topic planes
 };
 
 struct Deliver;   // message ring, seen-set and round lists (deliver.hip)
@@ -233,6 +263,11 @@ struct gsim_handle {
     int32_t t = 0;
 
     int64_t n = 0, e = 0;
+    // topic slots (smask_of above): S planes per topic array; d_smask is null
+    // while every peer holds every topic (S = T)
+    int32_t S = 0;
+    std::vector<uint64_t> smask;   // host copy of the slot masks (empty: dense)
+    uint64_t* d_smask = nullptr;
     uint32_t n_ips = 0;
     uint32_t max_degree = 0;   // longest CSR row (set when the graph is loaded)
     size_t bytes_allocated = 0;
@@ -320,6 +355,11 @@ int launch_refresh_scores(gsim_handle* h, int64_t now);
 int launch_compute_scores(gsim_handle* h);
 int refresh_accept(gsim_handle* h);   // recompute d_dstate if the snapshot changed
 int materialize_mcnt(gsim_handle* h); // apply pending meshd increments everywhere
+// grow the topic slot masks to cover need[N] (a host array; the topic arrays are re-laid out)
+int ensure_slots(gsim_handle* h, const uint64_t* need);
+uint8_t** extra_ctl_slot(gsim_handle* h);        // heartbeat.hip: the [2][S][E] control inbox
+uint8_t** deliver_gsel_slot(gsim_handle* h);     // deliver.hip: the [S][E] emitGossip choices
+int slots_changed(gsim_handle* h);               // deliver.hip: member spaces follow the masks
 // Publish's fanout branch for a batch already on the device (heartbeat.hip)
 int launch_fanout_publish(gsim_handle* h, const gsim_msg* d_pub, int32_t count, int64_t g, int64_t now);
 

@@ -46,6 +46,7 @@ struct HbArgs {
     int32_t T;
     const uint32_t *row_ptr, *col, *rev;
     const uint64_t* sub;
+    const uint64_t* smask;     // topic slots of each row owner (nullptr: dense; gsim_internal.h)
     const uint8_t* outbound;
     const uint8_t* direct;     // [E] edge order: col[e] is in the observer's gs.direct set
     const uint8_t* estate;
@@ -229,24 +230,30 @@ __device__ bool select_smallest(const HbArgs& a, bool cand, int count, uint32_t 
 // use: Graft/Prune are rare, and the record lives at rev[e] (record order,
 // DESIGN.md §2), away from the observer's row.
 struct ScoreFlags {
-    int64_t ir;          // record index t*E + rev[e]
+    int64_t ir;          // record index: topic t's slot of the neighbour's row, at rev[e]
+    bool ok = false;     // the neighbour holds a slot for t (else the record is absent: zero)
     uint8_t v = 0, v0 = 0;
     bool have = false;
+    __device__ void at(uint64_t mj, int32_t t, int64_t E, uint32_t rv)
+    {
+        ok = slot_has(mj, t);
+        ir = slot_idx(mj, t, E, rv);
+    }
     __device__ uint8_t& get(const HbArgs& a)
     {
-        if (!have) { v = v0 = a.tflags[ir]; have = true; }
+        if (!have) { v = v0 = ok ? a.tflags[ir] : 0; have = true; }
         return v;
     }
     __device__ void store(const HbArgs& a) const
     {
-        if (have && v != v0) a.tflags[ir] = v;
+        if (ok && have && v != v0) a.tflags[ir] = v;
     }
 };
 
 // peerScore.Graft / Prune on one edge-topic record (score.go:649-691)
 __device__ __forceinline__ void stats_graft(const HbArgs& a, bool tracked, bool scored, ScoreFlags& sf)
 {
-    if (!tracked || !scored) return;
+    if (!tracked || !scored || !sf.ok) return;
     uint8_t& fl = sf.get(a);
     fl = (uint8_t)((fl | GSIM_TF_IN_MESH) & ~GSIM_TF_ACTIVE);
     a.graft[sf.ir] = a.now;
@@ -256,7 +263,7 @@ __device__ __forceinline__ void stats_graft(const HbArgs& a, bool tracked, bool 
 __device__ __forceinline__ void stats_prune(const HbArgs& a, bool tracked, bool scored, double thr, double mcap,
                                             ScoreFlags& sf)
 {
-    if (!tracked || !scored) return;
+    if (!tracked || !scored || !sf.ok) return;
     uint8_t& fl = sf.get(a);
     if (fl & GSIM_TF_ACTIVE) {
         // pending delivery increments are part of the counter's value
@@ -277,6 +284,7 @@ constexpr int kScoreChunk = 2;   // topics whose record fields are loaded togeth
 __device__ double score_of_record(const HbArgs& a, uint32_t rv, uint32_t col)
 {
     if (!(a.estate[rv] & GSIM_ES_TRACKED)) return 0.0;
+    const uint64_t mj = smask_of(a.smask, col);      // the records sit in col's row
     double score = 0.0;
     for (int32_t t0 = 0; t0 < a.T; t0 += kScoreChunk) {
         // the records sit at rv in each topic plane, away from the row: load a
@@ -287,8 +295,8 @@ __device__ double score_of_record(const HbArgs& a, uint32_t rv, uint32_t col)
 #pragma unroll
         for (int j = 0; j < kScoreChunk; ++j) {
             const int32_t t = t0 + j;
-            const bool ok = t < a.T && (const_tp(a.tp) + t)->scored;
-            const int64_t i = (int64_t)t * a.E + rv;
+            const bool ok = t < a.T && (const_tp(a.tp) + t)->scored && slot_has(mj, t);
+            const int64_t i = slot_idx(mj, t, a.E, rv);
             fl[j] = ok ? a.tflags[i] : 0;
             mc[j] = ok ? a.mcnt[i] : 0;
             f[j] = ok ? a.first[i] : 0.0;
@@ -301,7 +309,7 @@ __device__ double score_of_record(const HbArgs& a, uint32_t rv, uint32_t col)
             const int32_t t = t0 + j;
             if (t >= a.T) break;
             const ctp_t tp = const_tp(a.tp) + t;
-            if (!tp->scored) continue;
+            if (!tp->scored || !slot_has(mj, t)) continue;
             const double meshd = apply_incs(md[j], mc[j], tp->mesh_message_deliveries_cap);
             double ts = 0.0;
             if (fl[j] & GSIM_TF_IN_MESH) {                                // P1
@@ -624,6 +632,10 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
         const double S = valid ? a.score[rv] : 0.0;
         const uint64_t subj = valid ? a.sub[col] : 0ull;
         const uint64_t subi = ovalid ? a.sub[obs] : 0ull;
+        // topic slots: router state is the observer's row (mi), its records of
+        // the neighbours sit in their rows (mj, per lane)
+        const uint64_t mi = ovalid ? smask_of(a.smask, (uint32_t)obs) : 0ull;
+        const uint64_t mj = valid ? smask_of(a.smask, col) : 0ull;
         // live score for emitGossip: the snapshot until this heartbeat's
         // Graft/Prune touches one of the lane's records
         double S_live = S;
@@ -635,7 +647,8 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
         // clearBackoff every 15 ticks (gossipsub.go:1627-1646)
         if (a.tick % 15 == 0 && valid) {
             for (int32_t t = 0; t < a.T; ++t) {
-                const int64_t i = (int64_t)t * a.E + e;
+                if (!slot_has(mi, t)) continue;
+                const int64_t i = slot_idx(mi, t, a.E, e);
                 const int64_t bo = a.backoff[i];
                 if (bo != 0 && bo + kBackoffSlack < a.now) a.backoff[i] = 0;
             }
@@ -651,7 +664,7 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
 #pragma unroll
           for (int j = 0; j < kFlagChunk; ++j) {
               const int32_t t = t0 + j;
-              flc[j] = (t < a.T && valid && ((subi >> t) & 1ull)) ? a.mflags[(int64_t)t * a.E + e] : 0;
+              flc[j] = (t < a.T && valid && ((subi >> t) & 1ull)) ? a.mflags[slot_idx(mi, t, a.E, e)] : 0;
           }
           for (int j = 0; j < kFlagChunk; ++j) {
             const int32_t t = t0 + j;
@@ -661,9 +674,9 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
             const bool scored = tp->scored != 0;
             const double thr = tp->mesh_message_deliveries_threshold;
             const double mcap = tp->mesh_message_deliveries_cap;
-            const int64_t i = (int64_t)t * a.E + e;
+            const int64_t i = slot_idx(mi, t, a.E, e);
             ScoreFlags sf;
-            sf.ir = (int64_t)t * a.E + rv;
+            sf.at(mj, t, a.E, rv);
             uint8_t fl = flc[j];
             const uint8_t fl0 = fl;
             // backoff is only consulted when a graft selection or a prune
@@ -835,8 +848,8 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
                 if (valid) a.gsel[i] = gsel ? 1 : 0;
             }
             if (valid) {
-                if (ctl) {
-                    const int64_t r = (int64_t)t * a.E + a.rev[e];
+                if (ctl && slot_has(mj, t)) {
+                    const int64_t r = slot_idx(mj, t, a.E, a.rev[e]);   // the receiver's row
                     a.ctl_out[r] = (uint8_t)(a.ctl_out[r] | ctl);
                     atomicOr(reinterpret_cast<unsigned long long*>(a.cany_out + col), 1ull << t);
                 }
@@ -904,8 +917,9 @@ __device__ __forceinline__ void fanout_observer(const HbArgs& a, Grp& g, int64_t
         const bool valid = gl < deg;
         const uint32_t e = b + (uint32_t)gl;
         if (gl < 64 && ((expired >> gl) & 1ull)) a.lastpub[obs * a.T + gl] = 0;
-        for (uint64_t q = expired & fant0; q; q &= q - 1) {
-            const int64_t i = (int64_t)(__ffsll((long long)q) - 1) * a.E + e;
+        const uint64_t mi = smask_of(a.smask, (uint32_t)obs);   // fanout topics hold slots (gsim_publish)
+        for (uint64_t q = expired & fant0 & mi; q; q &= q - 1) {
+            const int64_t i = slot_idx(mi, __ffsll((long long)q) - 1, a.E, e);
             if (valid) {
                 const uint8_t fl = a.mflags[i];
                 if (fl & GSIM_TF_FANOUT) a.mflags[i] = (uint8_t)(fl & ~GSIM_TF_FANOUT);
@@ -924,9 +938,9 @@ __device__ __forceinline__ void fanout_observer(const HbArgs& a, Grp& g, int64_t
         const uint64_t subj = valid ? a.sub[col] : 0ull;
         double S_live = 0.0;
         bool have_live = false;
-        for (uint64_t q = fant; q; q &= q - 1) {
+        for (uint64_t q = fant & mi; q; q &= q - 1) {
             const int32_t t = __ffsll((long long)q) - 1;
-            const int64_t i = (int64_t)t * a.E + e;
+            const int64_t i = slot_idx(mi, t, a.E, e);
             const uint8_t fl = valid ? a.mflags[i] : 0;
             const bool tpeer = conn && ((subj >> t) & 1ull);
             bool inf = (fl & GSIM_TF_FANOUT) && tpeer && S >= a.pub_thr;
@@ -991,6 +1005,7 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
         const int deg = (int)(a.row_ptr[rcv + 1] - b);
         const int nch = (deg + 63) >> 6;                    // rows longer than 64: 64-edge chunks in order
         const uint64_t subr = a.sub[rcv];
+        const uint64_t mr = smask_of(a.smask, (uint32_t)rcv);   // the inbox and router state: rcv's row
         uint64_t pxo = 0;          // topics with a PRUNE reply carrying PX (mesh full, gossipsub.go:812-818)
         bool nopx_set = false;     // this lane marked a sender whose RPC turned PX off
         for (int32_t t0 = 0; t0 < a.T; t0 += kFlagChunk) {
@@ -998,7 +1013,7 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
           for (int j = 0; j < kFlagChunk; ++j) {
             const int32_t t = t0 + j;
             if (t >= a.T) break;
-            if (!((any >> t) & 1ull)) continue;
+            if (!((any >> t) & 1ull) || !slot_has(mr, t)) continue;
             const bool joined = (subr >> t) & 1ull;
             const ctp_t tp = const_tp(a.tp) + t;
             const bool scored = tp->scored != 0;
@@ -1009,12 +1024,12 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
             if (joined)
                 for (int ch = 0; ch < nch; ++ch) {
                     const bool v = ch * 64 + lane < deg;
-                    mesh += __popcll(ballot(v && (a.mflags[(int64_t)t * a.E + b + ch * 64 + lane] & GSIM_TF_MESH)));
+                    mesh += __popcll(ballot(v && (a.mflags[slot_idx(mr, t, a.E, b + ch * 64 + lane)] & GSIM_TF_MESH)));
                 }
             for (int ch = 0; ch < nch; ++ch) {
               const bool valid = ch * 64 + lane < deg;
               const uint32_t e = b + (uint32_t)(ch * 64 + lane);
-              const int64_t i = (int64_t)t * a.E + e;
+              const int64_t i = slot_idx(mr, t, a.E, e);
               const uint8_t c = valid ? a.ctl_in[i] : 0;
               uint64_t pending = ballot(c != 0);
               if (!pending) continue;
@@ -1033,8 +1048,9 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                     const uint32_t rv = a.rev[e];                // receiver's record of the sender
                     const uint8_t est = a.estate[rv];
                     const bool tracked = est & GSIM_ES_TRACKED;
+                    const uint64_t mj = smask_of(a.smask, a.col[e]);   // the sender's row
                     ScoreFlags sf;
-                    sf.ir = (int64_t)t * a.E + rv;
+                    sf.at(mj, t, a.E, rv);
                     int64_t bo = a.backoff[i];
                     const int64_t bo0 = bo;
                     uint8_t reply = 0;
@@ -1096,8 +1112,8 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                     }
                     sf.store(a);
                     if (bo != bo0) a.backoff[i] = bo;
-                    if (reply) {
-                        const int64_t r = (int64_t)t * a.E + a.rev[e];
+                    if (reply && slot_has(mj, t)) {
+                        const int64_t r = slot_idx(mj, t, a.E, rv);
                         a.ctl_out[r] = (uint8_t)(a.ctl_out[r] | reply);
                         atomicOr(reinterpret_cast<unsigned long long*>(a.cany_out + a.col[e]), 1ull << t);
                     }
@@ -1122,8 +1138,9 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                 if (!valid || !a.nopx[e]) continue;
                 a.nopx[e] = 0;
                 const uint32_t re = a.rev[e];
-                for (uint64_t q = pxo; q; q &= q - 1) {
-                    const int64_t r = (int64_t)(__ffsll((long long)q) - 1) * a.E + re;
+                const uint64_t mj = smask_of(a.smask, a.col[e]);
+                for (uint64_t q = pxo & mj; q; q &= q - 1) {
+                    const int64_t r = slot_idx(mj, __ffsll((long long)q) - 1, a.E, re);
                     a.ctl_out[r] = (uint8_t)(a.ctl_out[r] & ~GSIM_CTL_PX);
                 }
             }
@@ -1196,7 +1213,8 @@ __global__ __launch_bounds__(256) void k_px_emit(HbArgs a, int live, uint32_t ke
             const int32_t t = __ffsll((long long)tm) - 1;
             for (int p0 = 0; p0 < deg; p0 += 64) {
                 const uint32_t ep_l = b + (uint32_t)(p0 + lane);
-                const bool pr = p0 + lane < deg && (a.ctl_out[(int64_t)t * a.E + a.rev[ep_l]] & GSIM_CTL_PX);
+                const uint64_t mp = p0 + lane < deg ? smask_of(a.smask, a.col[ep_l]) : 0ull;
+                const bool pr = slot_has(mp, t) && (a.ctl_out[slot_idx(mp, t, a.E, a.rev[ep_l])] & GSIM_CTL_PX);
                 for (uint64_t pm = __ballot(pr); pm; pm &= pm - 1) {
                     const int pos = p0 + __ffsll((long long)pm) - 1;
                     const uint32_t ep = b + (uint32_t)pos, p = a.col[ep];
@@ -1329,10 +1347,11 @@ __global__ __launch_bounds__(256) void k_snapshot(HbArgs a, int64_t e_lo, int64_
             p.behaviour_penalty = a.bp[rv];
         }
         ps[x] = p;
+        const uint64_t mj = smask_of(a.smask, col);
         for (int32_t t = 0; t < a.T; ++t) {
-            const int64_t i = (int64_t)t * a.E + rv;
+            const int64_t i = slot_idx(mj, t, a.E, rv);
             gsim_topic_score_snapshot q{};
-            if (tracked) {
+            if (tracked && slot_has(mj, t)) {
                 const uint8_t fl = a.tflags[i];
                 q.time_in_mesh_ns = (fl & GSIM_TF_IN_MESH) ? a.mtime[i] : 0;
                 q.first_message_deliveries = a.first[i];
@@ -1387,14 +1406,15 @@ __global__ __launch_bounds__(256) void k_churn_find(const uint32_t* row_ptr, con
 }
 
 // Fresh (or dropped) score record r: an empty peerStats.
-__device__ void churn_reset_record(const HbArgs& a, const ChurnArgs& c, uint32_t r, uint64_t joined)
+// joined: topics whose records may be non-zero (within the row owner's slots mj)
+__device__ void churn_reset_record(const HbArgs& a, const ChurnArgs& c, uint32_t r, uint64_t joined, uint64_t mj)
 {
     a.bp[r] = 0.0;
     c.expire[r] = 0;
     c.pen[r] = 0;
     for (int32_t t = 0; t < a.T; ++t) {
         if (!((joined >> t) & 1ull)) continue;   // already zero
-        const int64_t i = (int64_t)t * a.E + r;
+        const int64_t i = slot_idx(mj, t, a.E, r);
         c.first[i] = 0.0; a.meshd[i] = 0.0; a.fail[i] = 0.0; c.invalid[i] = 0.0;
         a.graft[i] = 0; a.mtime[i] = 0;
         a.tflags[i] = 0;
@@ -1416,17 +1436,21 @@ __global__ __launch_bounds__(256) void k_churn_apply(HbArgs a, ChurnArgs c)
     // a store to them would write the value already there.  Random 1-8 B stores
     // are the churn's bound, so the router planes below are also stored only
     // where they change.
-    const uint64_t joined = c.skip_unjoined ? a.sub[a.col[r]] : ~0ull;
+    // topic slots: the records r sit in the neighbour's row (mj), the router
+    // state e in the observer's (mi)
+    const uint64_t mj = smask_of(a.smask, a.col[e]), mi = smask_of(a.smask, a.col[r]);
+    const uint64_t joined = (c.skip_unjoined ? a.sub[a.col[r]] : ~0ull) & mj;
     if (c.up) {
         // AddPeer: connected; a retained record comes back as it is
         c.rstate[e] = (uint8_t)(c.rstate[e] | GSIM_ES_CONNECTED);
-        if (!(c.estate[r] & GSIM_ES_TRACKED)) churn_reset_record(a, c, r, joined);
+        if (!(c.estate[r] & GSIM_ES_TRACKED)) churn_reset_record(a, c, r, joined, mj);
         c.estate[r] = GSIM_ES_TRACKED | GSIM_ES_CONNECTED;
         return;
     }
     // router RemovePeer: out of every mesh without PRUNE, pending control dropped
     for (int32_t t = 0; t < a.T; ++t) {
-        const int64_t i = (int64_t)t * a.E + e;
+        if (!slot_has(mi, t)) continue;
+        const int64_t i = slot_idx(mi, t, a.E, e);
         const uint8_t mf = a.mflags[i], ci = a.ctl_in[i], co = a.ctl_out[i];
         const uint8_t nm = (uint8_t)(mf & ~(GSIM_TF_MESH | GSIM_TF_FANOUT));
         if (nm != mf) a.mflags[i] = nm;
@@ -1437,14 +1461,14 @@ __global__ __launch_bounds__(256) void k_churn_apply(HbArgs a, ChurnArgs c)
     // peerScore.RemovePeer: positive scores are dropped, the rest retained
     if (!(c.estate[r] & GSIM_ES_TRACKED)) return;
     if (score_of_record(a, r, a.col[e]) > 0) {
-        churn_reset_record(a, c, r, joined);
+        churn_reset_record(a, c, r, joined, mj);
         c.estate[r] = 0;
         return;
     }
     for (int32_t t = 0; t < a.T; ++t) {
         const ctp_t tp = const_tp(a.tp) + t;
         if (!tp->scored || !((joined >> t) & 1ull)) continue;
-        const int64_t i = (int64_t)t * a.E + r;
+        const int64_t i = slot_idx(mj, t, a.E, r);
         c.first[i] = 0.0;
         const uint8_t fl = a.tflags[i];
         const double thr = tp->mesh_message_deliveries_threshold;
@@ -1477,7 +1501,9 @@ __device__ __forceinline__ void fanout_publish_one(const HbArgs& a, Grp& g, cons
     const int deg = (int)(a.row_ptr[o + 1] - b);
     const bool valid = gl < deg;
     const uint32_t e = b + (uint32_t)gl;
-    const int64_t i = (int64_t)t * a.E + e;
+    const uint64_t mo = smask_of(a.smask, o);      // gsim_publish gave the origin a slot for t
+    if (!slot_has(mo, t)) return;                  // group-uniform
+    const int64_t i = slot_idx(mo, t, a.E, e);
     const uint8_t fl = valid ? a.mflags[i] : 0;
     const bool have = ((a.fan_topics[o] >> t) & 1ull) && g.any((fl & GSIM_TF_FANOUT) != 0);
     if (!have) {
@@ -1531,7 +1557,7 @@ int alloc_extra(gsim_handle* h)
     free_extra(h);
     h->x = new Extra();
     if (h->e == 0) return GSIM_OK;
-    const size_t bytes = 2 * (size_t)h->e * (size_t)std::max(1, h->t);
+    const size_t bytes = 2 * (size_t)h->e * (size_t)std::max(1, h->S);
     hipError_t e = hipMalloc((void**)&h->x->d_ctl, bytes);
     if (e != hipSuccess) return hip_check(h, e, "hipMalloc ctl");
     h->bytes_allocated += bytes;
@@ -1629,12 +1655,17 @@ int extra_field_written(gsim_handle* h, int32_t f)
 }
 
 uint8_t* extra_ctl(gsim_handle* h) { return h->x ? h->x->d_ctl : nullptr; }
+uint8_t** extra_ctl_slot(gsim_handle* h)
+{
+    static uint8_t* none = nullptr;
+    return h->x ? &h->x->d_ctl : &none;
+}
 uint64_t* extra_cany(gsim_handle* h) { return h->x ? h->x->d_cany : nullptr; }
 
 bool extra_field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r)
 {
     if (f == GSIM_F_CTL && h->x && h->x->d_ctl) {
-        *r = {h->x->d_ctl, 2 * (size_t)h->e * (size_t)std::max(1, h->t)};
+        *r = {h->x->d_ctl, 2 * (size_t)h->e * (size_t)std::max(1, h->t), FK_TEDGE, 1, 2};
         return true;
     }
     if (f == GSIM_F_LASTPUB && h->x && h->x->d_lastpub) {
@@ -1652,11 +1683,11 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
 {
     HbArgs a{};
     a.N = h->n; a.E = h->e; a.T = h->t;
-    a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.rev = h->d_rev; a.sub = h->d_sub;
+    a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.rev = h->d_rev; a.sub = h->d_sub; a.smask = h->d_smask;
     a.outbound = h->d_outbound; a.direct = h->d_direct; a.estate = h->d_estate; a.score = h->d_score; a.tp = h->d_tp;
     a.tflags = h->d_tflags; a.mflags = h->d_mflags; a.rstate = h->d_rstate; a.backoff = h->d_backoff; a.meshd = h->d_meshd; a.fail = h->d_fail; a.bp = h->d_bp;
     a.graft = h->d_graft; a.mtime = h->d_mtime; a.mcnt = h->d_mcnt;
-    const size_t TE = (size_t)h->e * (size_t)std::max(1, h->t);
+    const size_t TE = (size_t)h->e * (size_t)std::max(1, h->S);
     a.ctl_in = h->x->d_ctl + (size_t)(parity_in & 1) * TE;
     a.ctl_out = h->x->d_ctl + (size_t)((parity_in + 1) & 1) * TE;
     a.cany_in = h->x->d_cany + (size_t)(parity_in & 1) * (size_t)h->n;

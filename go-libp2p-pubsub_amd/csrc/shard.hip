@@ -58,7 +58,8 @@ struct PeerRanges {
 // block counts its entries per shard in LDS and reserves each shard's range
 // with one atomic.
 __global__ __launch_bounds__(256) void k_ctl_export(uint8_t* ctl, uint64_t* cany, const uint32_t* row_ptr,
-                                                    const uint32_t* ymap, PeerRanges pr, int64_t E, int32_t T,
+                                                    const uint32_t* ymap, const uint64_t* smask, PeerRanges pr,
+                                                    int64_t E, int32_t T,
                                                     int64_t olo, int64_t ohi, int64_t n, uint64_t* out,
                                                     uint32_t* cnt, int64_t cap)
 {
@@ -76,12 +77,13 @@ __global__ __launch_bounds__(256) void k_ctl_export(uint8_t* ctl, uint64_t* cany
         uint32_t d = 0, mine = 0, off = 0;
         if (x < nghost) {
             g = x < olo ? x : ohi + (x - olo);
-            any = cany[g] & tmask;
+            any = cany[g] & tmask & smask_of(smask, (uint32_t)g);
             if (cany[g]) cany[g] = 0;
             while ((int32_t)d + 1 < pr.K && g >= pr.lo[d + 1]) ++d;
             for (uint64_t r = any; r; r &= r - 1) {
                 const int32_t t = __ffsll((long long)r) - 1;
-                for (uint32_t e = row_ptr[g]; e < row_ptr[g + 1]; ++e) mine += ctl[(int64_t)t * E + e] != 0;
+                const int64_t pl = slot_idx(smask_of(smask, (uint32_t)g), t, E, 0);
+                for (uint32_t e = row_ptr[g]; e < row_ptr[g + 1]; ++e) mine += ctl[pl + e] != 0;
             }
             if (mine) off = atomicAdd(&s_cnt[d], mine);
         }
@@ -92,8 +94,9 @@ __global__ __launch_bounds__(256) void k_ctl_export(uint8_t* ctl, uint64_t* cany
             int64_t pos = (int64_t)s_base[d] + off;
             for (uint64_t r = any; r; r &= r - 1) {
                 const int32_t t = __ffsll((long long)r) - 1;
+                const int64_t pl = slot_idx(smask_of(smask, (uint32_t)g), t, E, 0);
                 for (uint32_t e = row_ptr[g]; e < row_ptr[g + 1]; ++e) {
-                    const int64_t i = (int64_t)t * E + e;
+                    const int64_t i = pl + e;
                     const uint8_t c = ctl[i];
                     if (!c) continue;
                     ctl[i] = 0;
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(256) void k_ctl_export(uint8_t* ctl, uint64_t* cany
 }
 
 __global__ __launch_bounds__(256) void k_ctl_import(const uint64_t* in, int64_t n_in, uint8_t* ctl, uint64_t* cany,
-                                                    const uint32_t* owner, int64_t E)
+                                                    const uint32_t* owner, const uint64_t* smask, int64_t E)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n_in; x += stride) {
@@ -115,7 +118,9 @@ __global__ __launch_bounds__(256) void k_ctl_import(const uint64_t* in, int64_t 
         const uint32_t e = (uint32_t)v;
         const int32_t t = (int32_t)((v >> 32) & 0xFF);
         const uint8_t bits = (uint8_t)(v >> 40);
-        uint8_t* p = ctl + (int64_t)t * E + e;
+        const uint64_t m = smask_of(smask, owner[e]);
+        if (!slot_has(m, t)) continue;
+        uint8_t* p = ctl + slot_idx(m, t, E, e);
         *p = (uint8_t)(*p | bits);      // one entry per (receiver edge, topic)
         atomicOr(reinterpret_cast<unsigned long long*>(cany + owner[e]), 1ull << t);
     }
@@ -124,14 +129,16 @@ __global__ __launch_bounds__(256) void k_ctl_import(const uint64_t* in, int64_t 
 // emitGossip's choices of the owned rows' cross edges, one topic mask per
 // edge in cross-out order, with the advertiser's IWANT gate (gstate).
 __global__ __launch_bounds__(256) void k_gsel_export(const uint32_t* xgather, int64_t n_cross, const uint8_t* gsel,
-                                                     const uint8_t* gstate, int32_t T, int64_t E, uint64_t* out,
-                                                     uint8_t* gs_out)
+                                                     const uint8_t* gstate, const uint32_t* owner, const uint64_t* smask,
+                                                     int32_t T, int64_t E, uint64_t* out, uint8_t* gs_out)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n_cross; q += stride) {
         const uint32_t e = xgather[q];
         uint64_t m = 0;
-        for (int32_t t = 0; t < T; ++t) m |= (uint64_t)(gsel[(int64_t)t * E + e] != 0) << t;
+        const uint64_t sm = smask_of(smask, owner[e]);
+        for (int32_t t = 0; t < T; ++t)
+            if (slot_has(sm, t)) m |= (uint64_t)(gsel[slot_idx(sm, t, E, e)] != 0) << t;
         out[q] = m;
         gs_out[q] = gstate[e];
     }
@@ -139,14 +146,17 @@ __global__ __launch_bounds__(256) void k_gsel_export(const uint32_t* xgather, in
 
 // ... into the ghost rows: every topic plane of every ghost-row edge.
 __global__ __launch_bounds__(256) void k_gsel_import(const uint64_t* in, const uint8_t* gs_in, uint8_t* gsel,
-                                                     uint8_t* gstate, int32_t T, int64_t E, int64_t e_lo, int64_t e_hi)
+                                                     uint8_t* gstate, const uint32_t* owner, const uint64_t* smask,
+                                                     int32_t T, int64_t E, int64_t e_lo, int64_t e_hi)
 {
     const int64_t nghost = e_lo + (E - e_hi);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < nghost; x += stride) {
         const int64_t e = x < e_lo ? x : e_hi + (x - e_lo);
         const uint64_t m = in[e];
-        for (int32_t t = 0; t < T; ++t) gsel[(int64_t)t * E + e] = (uint8_t)((m >> t) & 1ull);
+        const uint64_t sm = smask_of(smask, owner[e]);
+        for (int32_t t = 0; t < T; ++t)
+            if (slot_has(sm, t)) gsel[slot_idx(sm, t, E, e)] = (uint8_t)((m >> t) & 1ull);
         gstate[e] = gs_in[e];
     }
 }
@@ -155,15 +165,18 @@ __global__ __launch_bounds__(256) void k_gsel_import(const uint64_t* in, const u
 // mesh and fanout bits per topic, connected | direct | publish gate.
 __global__ __launch_bounds__(256) void k_router_export(const uint32_t* xgather, int64_t n_cross, const uint8_t* mflags,
                                                        const uint8_t* rstate, const uint8_t* direct, const double* score,
-                                                       const uint32_t* rev, double pub_thr, int32_t T, int64_t E,
+                                                       const uint32_t* rev, const uint32_t* owner, const uint64_t* smask,
+                                                       double pub_thr, int32_t T, int64_t E,
                                                        uint64_t* mesh, uint64_t* fan, uint8_t* flags)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n_cross; q += stride) {
         const uint32_t e = xgather[q];
         uint64_t mm = 0, fm = 0;
+        const uint64_t sm = smask_of(smask, owner[e]);
         for (int32_t t = 0; t < T; ++t) {
-            const uint8_t f = mflags[(int64_t)t * E + e];
+            if (!slot_has(sm, t)) continue;
+            const uint8_t f = mflags[slot_idx(sm, t, E, e)];
             mm |= (uint64_t)((f & GSIM_TF_MESH) != 0) << t;
             fm |= (uint64_t)((f & GSIM_TF_FANOUT) != 0) << t;
         }
@@ -181,16 +194,18 @@ __global__ __launch_bounds__(256) void k_router_import(const uint64_t* mesh, con
                                                        uint8_t* mflags, uint8_t* rstate, uint8_t* direct, uint8_t* pgate,
                                                        int32_t T, int64_t E, int64_t e_lo, int64_t e_hi,
                                                        const uint32_t* row_ptr, const uint32_t* owner, int64_t n,
-                                                       uint64_t* mmask)
+                                                       uint64_t* mmask, const uint64_t* smask)
 {
     const int64_t nghost = e_lo + (E - e_hi);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < nghost; x += stride) {
         const int64_t e = x < e_lo ? x : e_hi + (x - e_lo);
         const uint64_t mm = mesh[e], fm = fan[e];
+        const uint64_t sm = smask_of(smask, owner[e]);
         for (int32_t t = 0; t < T; ++t)
-            mflags[(int64_t)t * E + e] = (uint8_t)((((mm >> t) & 1ull) ? GSIM_TF_MESH : 0) |
-                                                   (((fm >> t) & 1ull) ? GSIM_TF_FANOUT : 0));
+            if (slot_has(sm, t))
+                mflags[slot_idx(sm, t, E, e)] = (uint8_t)((((mm >> t) & 1ull) ? GSIM_TF_MESH : 0) |
+                                                          (((fm >> t) & 1ull) ? GSIM_TF_FANOUT : 0));
         const uint8_t f = flags[e];
         rstate[e] = (f & 1) ? GSIM_ES_CONNECTED : 0;
         direct[e] = (f & 2) ? 1 : 0;
@@ -226,7 +241,8 @@ struct EdgeBases {
 
 __global__ __launch_bounds__(256) void k_router_delta(const uint64_t* in, int64_t n_in, int32_t self, EdgeBases gb,
                                                       uint8_t* mflags, const uint8_t* direct, const uint32_t* row_ptr,
-                                                      const uint32_t* owner, int64_t E, int64_t n, uint64_t* mmask)
+                                                      const uint32_t* owner, const uint64_t* smask, int64_t E, int64_t n,
+                                                      uint64_t* mmask)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n_in; x += stride) {
@@ -235,7 +251,9 @@ __global__ __launch_bounds__(256) void k_router_delta(const uint64_t* in, int64_
         const int32_t src = (int32_t)(v & 63), t = (int32_t)((v >> 12) & 0xFF);
         const uint8_t fl = (uint8_t)((v >> 20) & 0xFF);
         const int64_t ge = gb.b[src] + (int64_t)(v >> 32);
-        uint8_t* p = mflags + (int64_t)t * E + ge;
+        const uint64_t sm = smask_of(smask, owner[ge]);
+        if (!slot_has(sm, t)) continue;
+        uint8_t* p = mflags + slot_idx(sm, t, E, ge);
         *p = (uint8_t)((*p & ~(GSIM_TF_MESH | GSIM_TF_FANOUT)) | fl);
         if (mmask) {
             const uint32_t r = owner[ge], b = row_ptr[r];
@@ -585,7 +603,7 @@ int exchange_control(gsim_group* g, int parity)
         gsim_handle* h = g->hs[l];
         ShardCtx* s = h->sh;
         (void)hipSetDevice(h->device);
-        const size_t TE = (size_t)h->e * (size_t)std::max(1, h->t);
+        const size_t TE = (size_t)h->e * (size_t)std::max(1, h->S);
         uint8_t* ctl = extra_ctl(h) + (size_t)parity * TE;
         uint64_t* cany = extra_cany(h) + (size_t)parity * (size_t)h->n;
         if (hipMemsetAsync(s->d_ccnt, 0, sizeof(uint32_t) * K, h->stream) != hipSuccess)
@@ -595,7 +613,7 @@ int exchange_control(gsim_group* g, int parity)
         pr.K = K;
         for (int q = 0; q <= K; ++q) pr.lo[q] = s->lpeer[(size_t)q];
         hipLaunchKernelGGL(k_ctl_export, dim3(grid_for(nghost)), dim3(256), 0, h->stream, ctl, cany,
-                           (const uint32_t*)h->d_row_ptr, (const uint32_t*)s->d_ymap, pr,
+                           (const uint32_t*)h->d_row_ptr, (const uint32_t*)s->d_ymap, (const uint64_t*)h->d_smask, pr,
                            h->e, std::max(1, h->t), s->own_lo, s->own_hi, h->n, s->d_cout, s->d_ccnt, s->ccap);
         if (hipMemcpyAsync(s->h_counts, s->d_ccnt, sizeof(uint32_t) * K, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
             hipStreamSynchronize(h->stream) != hipSuccess)
@@ -634,10 +652,11 @@ int exchange_control(gsim_group* g, int parity)
         gsim_handle* h = g->hs[l];
         if (!total[l]) continue;
         (void)hipSetDevice(h->device);
-        const size_t TE = (size_t)h->e * (size_t)std::max(1, h->t);
+        const size_t TE = (size_t)h->e * (size_t)std::max(1, h->S);
         hipLaunchKernelGGL(k_ctl_import, dim3(grid_for(total[l])), dim3(256), 0, h->stream,
                            (const uint64_t*)h->sh->d_cin, total[l], extra_ctl(h) + (size_t)parity * TE,
-                           extra_cany(h) + (size_t)parity * (size_t)h->n, (const uint32_t*)h->d_owner, h->e);
+                           extra_cany(h) + (size_t)parity * (size_t)h->n, (const uint32_t*)h->d_owner,
+                           (const uint64_t*)h->d_smask, h->e);
         if (hipGetLastError() != hipSuccess) return g->fail(GSIM_EDEVICE, "k_ctl_import");
     }
     return GSIM_OK;
@@ -659,7 +678,8 @@ int exchange_gossip_marks(gsim_group* g)
         if (ncross)
             hipLaunchKernelGGL(k_gsel_export, dim3(grid_for(ncross)), dim3(256), 0, h->stream,
                                (const uint32_t*)s->d_xgather, ncross, (const uint8_t*)gv.gsel,
-                               (const uint8_t*)gv.gstate, h->t, h->e, s->d_gout, s->d_gsout);
+                               (const uint8_t*)gv.gstate, (const uint32_t*)h->d_owner, (const uint64_t*)h->d_smask,
+                               h->t, h->e, s->d_gout, s->d_gsout);
         o1[l] = s->d_gout; o2[l] = s->d_gsout; i1[l] = s->d_gin; i2[l] = s->d_gsin;
     }
     int rc = exchange_dense(g, o1, i1, 8);
@@ -674,7 +694,8 @@ int exchange_gossip_marks(gsim_group* g)
         const int64_t nghost = s->own_e_lo + (h->e - s->own_e_hi);
         if (nghost)
             hipLaunchKernelGGL(k_gsel_import, dim3(grid_for(nghost)), dim3(256), 0, h->stream,
-                               (const uint64_t*)s->d_gin, (const uint8_t*)s->d_gsin, gv.gsel, gv.gstate, h->t, h->e,
+                               (const uint64_t*)s->d_gin, (const uint8_t*)s->d_gsin, gv.gsel, gv.gstate,
+                               (const uint32_t*)h->d_owner, (const uint64_t*)h->d_smask, h->t, h->e,
                                s->own_e_lo, s->own_e_hi);
         if (hipGetLastError() != hipSuccess) return g->fail(GSIM_EDEVICE, "k_gsel_import");
     }
@@ -698,7 +719,8 @@ int exchange_router(gsim_group* g)
             hipLaunchKernelGGL(k_router_export, dim3(grid_for(ncross)), dim3(256), 0, h->stream,
                                (const uint32_t*)s->d_xgather, ncross, (const uint8_t*)h->d_mflags,
                                (const uint8_t*)h->d_rstate, (const uint8_t*)h->d_direct, (const double*)h->d_score,
-                               (const uint32_t*)h->d_rev, h->th.publish_threshold, h->t, h->e, s->d_rmesh_out,
+                               (const uint32_t*)h->d_rev, (const uint32_t*)h->d_owner, (const uint64_t*)h->d_smask,
+                               h->th.publish_threshold, h->t, h->e, s->d_rmesh_out,
                                s->d_rfan_out, s->d_rflag_out);
         o1[l] = s->d_rmesh_out; o2[l] = s->d_rfan_out; o3[l] = s->d_rflag_out;
         i1[l] = s->d_rmesh_in; i2[l] = s->d_rfan_in; i3[l] = s->d_rflag_in;
@@ -723,7 +745,7 @@ int exchange_router(gsim_group* g)
                                (const uint64_t*)s->d_rmesh_in, (const uint64_t*)s->d_rfan_in,
                                (const uint8_t*)s->d_rflag_in, h->d_mflags, h->d_rstate, h->d_direct, s->d_pgate,
                                h->t, h->e, s->own_e_lo, s->own_e_hi, (const uint32_t*)h->d_row_ptr,
-                               (const uint32_t*)h->d_owner, h->n, mm);
+                               (const uint32_t*)h->d_owner, h->n, mm, (const uint64_t*)h->d_smask);
         if (hipGetLastError() != hipSuccess) return g->fail(GSIM_EDEVICE, "k_router_import");
         h->score_version++;    // ghost rows' connected / direct bits feed the delivery state
     }
@@ -794,7 +816,7 @@ int exchange_router_delta(gsim_group* g)
             hipLaunchKernelGGL(k_router_delta, dim3(grid_for(total[l])), dim3(256), 0, h->stream,
                                (const uint64_t*)s->d_rdel_in, total[l], g->ids[l], gb, h->d_mflags,
                                (const uint8_t*)h->d_direct, (const uint32_t*)h->d_row_ptr, (const uint32_t*)h->d_owner,
-                               h->e, h->n, mm);
+                               (const uint64_t*)h->d_smask, h->e, h->n, mm);
             if (hipGetLastError() != hipSuccess) return g->fail(GSIM_EDEVICE, "k_router_delta");
         }
         if (hipMemsetAsync(s->d_rdel_n, 0, sizeof(uint32_t), h->stream) != hipSuccess)

@@ -40,6 +40,7 @@ struct WireArgs {
     const uint32_t *row_ptr, *col, *rev, *owner;
     const uint8_t* ctl;           // parity-0 inbox [T][E] (receivers' edges)
     const uint8_t* gsel;          // [T][E] (senders' edges)
+    const uint64_t* smask;        // topic slots of both arrays (gsim_internal.h; nullptr: dense)
     const uint64_t* cell;
     int64_t N, E;
     int32_t T, R;
@@ -97,6 +98,17 @@ __device__ __forceinline__ int64_t window_put(const WireArgs& a, uint32_t m, uin
     return fr;
 }
 
+// the slot-layout entries (gsim_internal.h): gsel of edge e in its sender
+// p's row, the inbox entry re in the receiver q's row
+__device__ __forceinline__ bool gsel_at(const WireArgs& a, int32_t t, int64_t e, uint64_t mp)
+{
+    return a.gsel && slot_has(mp, t) && a.gsel[slot_idx(mp, t, a.E, e)] != 0;
+}
+__device__ __forceinline__ uint8_t ctl_at(const WireArgs& a, int32_t t, int64_t re, uint64_t mq)
+{
+    return slot_has(mq, t) ? a.ctl[slot_idx(mq, t, a.E, re)] : 0;
+}
+
 __global__ void k_wire_ids_count(WireArgs a)
 {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -106,8 +118,8 @@ __global__ void k_wire_ids_count(WireArgs a)
     const int32_t t = (int32_t)(k % a.T);
     uint64_t cnt = 0;
     bool any = false;
-    if (a.gsel)
-        for (uint32_t e = a.row_ptr[p]; e < a.row_ptr[p + 1] && !any; ++e) any = a.gsel[(int64_t)t * a.E + e] != 0;
+    const uint64_t mp = smask_of(a.smask, p);
+    for (uint32_t e = a.row_ptr[p]; e < a.row_ptr[p + 1] && !any; ++e) any = gsel_at(a, t, e, mp);
     if (any) {
         for (int32_t q = a.cand_ptr[t]; q < a.cand_ptr[t + 1]; ++q) cnt += window_put(a, a.cand[q], p) >= 0;
         if (!cnt) atomicOr(&a.err[0], 1u);                   // emitGossip has nothing to send
@@ -136,11 +148,12 @@ __device__ uint64_t control_body(const WireArgs& a, int64_t e, uint32_t p, bool*
 {
     const int64_t re = a.rev[e];
     const int64_t base = (int64_t)(p - a.p0) * a.T;
+    const uint64_t mp = smask_of(a.smask, p), mq = smask_of(a.smask, a.col[e]);
     uint64_t s = 0;
     bool x = false;
     for (int32_t t = 0; t < a.T; ++t) {
-        const uint8_t c = a.ctl[(int64_t)t * a.E + re];
-        if (a.gsel && a.gsel[(int64_t)t * a.E + e]) { s += ld(ihave_body(a, t, (uint32_t)a.n_pt[base + t])); x = true; }
+        const uint8_t c = ctl_at(a, t, re, mq);
+        if (gsel_at(a, t, e, mp)) { s += ld(ihave_body(a, t, (uint32_t)a.n_pt[base + t])); x = true; }
         if (c & GSIM_CTL_GRAFT) { s += ld(name_field(a, t)); x = true; }
         if (c & GSIM_CTL_PRUNE) { s += ld(prune_body(a, t)); x = true; }
     }
@@ -243,11 +256,12 @@ __global__ void k_wire_write(WireArgs a)
     const uint64_t body = control_body(a, e, p, &any);
     const int64_t re = a.rev[e];
     const int64_t base = (int64_t)(p - a.p0) * a.T;
+    const uint64_t mp = smask_of(a.smask, p), mq = smask_of(a.smask, a.col[e]);
     ByteOut w{a.out + a.roff[e - a.e0]};
     w.byte(0x1a);                                          // RPC.control = 3
     w.varint(body);
     for (int32_t t = 0; t < a.T; ++t) {                    // ControlMessage.ihave = 1
-        if (!a.gsel || !a.gsel[(int64_t)t * a.E + e]) continue;
+        if (!gsel_at(a, t, e, mp)) continue;
         const uint32_t n = (uint32_t)a.n_pt[base + t];
         w.byte(0x0a);
         w.varint(ihave_body(a, t, n));
@@ -256,13 +270,13 @@ __global__ void k_wire_write(WireArgs a)
         for (uint32_t q = 0; q < n; ++q) write_id(a, w, ids[q]);
     }
     for (int32_t t = 0; t < a.T; ++t) {                    // ControlMessage.graft = 3
-        if (!(a.ctl[(int64_t)t * a.E + re] & GSIM_CTL_GRAFT)) continue;
+        if (!(ctl_at(a, t, re, mq) & GSIM_CTL_GRAFT)) continue;
         w.byte(0x1a);
         w.varint(name_field(a, t));
         write_name(a, w, 0x0a, t);                         // ControlGraft.topicID = 1
     }
     for (int32_t t = 0; t < a.T; ++t) {                    // ControlMessage.prune = 4
-        if (!(a.ctl[(int64_t)t * a.E + re] & GSIM_CTL_PRUNE)) continue;
+        if (!(ctl_at(a, t, re, mq) & GSIM_CTL_PRUNE)) continue;
         w.byte(0x22);
         w.varint(prune_body(a, t));
         write_name(a, w, 0x0a, t);                         // ControlPrune.topicID = 1
@@ -406,6 +420,7 @@ extern "C" int gsim_wire_heartbeat(gsim_handle* h, int64_t tick, uint32_t p0, ui
     a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.rev = h->d_rev; a.owner = h->d_owner;
     a.ctl = extra_ctl(h);            // parity 0: the heartbeat's output
     a.gsel = v.gsel;
+    a.smask = h->d_smask;
     a.cell = v.cell;
     a.N = h->n; a.E = h->e; a.T = T; a.R = v.rounds;
     a.mtopic = v.mtopic; a.morigin = v.morigin; a.minv = v.minv; a.mid = v.mid;
