@@ -49,24 +49,26 @@ CONFIGS = {
     "c3": (1_000_000, 32, 16, 8, 6, 12),
     "c2": (10_000, 32, 1, 8, 6, 12),
     "c4": (125_000, 32, 1, 8, 6, 12),
-    "c5": (2_000_000, 16, 64, 8, 6, 12),
+    "c5": (10_000_000, 16, 64, 8, 6, 12),
 }
 # Structure beyond (peers, degree, topics, D) for the BASELINE configurations
 # that are not plain random-regular networks:
 #  c4  Sybil/eclipse: 100k honest + 25k sybils (20 %), one IP per 50 sybils
 #      (P6), sybils ignore IWANT (broken promises -> P7), opportunistic
 #      grafting every 10 heartbeats so the timed window holds it.
-#  c5  Chung-Lu power law (exponent 2.5, mean 16, rows <= 4096: hubs of a few hundred), 64 topics
-#      with Zipf subscriptions (8 per peer), 1 % of connections going down
-#      per tick and coming back two ticks later, publishers are topic members,
-#      4 msg/s/topic (256 msg/s network-wide) over an 8192-slot ring, peer
+#  c5  10M peers, plain Chung-Lu power law (exponent 2.5, mean 16, i0 = 1:
+#      hubs up to the 4096-connection cap), 64 topics with Zipf subscriptions
+#      (8 per peer), 1 % of connections going down per tick and coming back
+#      two ticks later, publishers are topic members, 4 msg/s/topic (256 msg/s
+#      network-wide) over per-topic sub-rings of 96 slots (ring 6144), peer
 #      exchange on (PRUNEs carry PX; the connector runs between ticks and
-#      reconnects churned-down addresses).
-#      2M peers: the dense [T][E] record planes of 10M peers x 64 topics
-#      (~560 GB) do not fit one GPU's 288 GB.
+#      reconnects churned-down addresses).  Topic-slot planes and
+#      member-compacted seen-set cells keep it in one GPU's
+#      HBM (the dense layouts would need ~560 GB of planes and ~500 GB of
+#      cells).
 SCENARIOS = {
     "c4": {"sybil_frac": 0.2, "per_ip": 50, "opp_ticks": 10},
-    "c5": {"power_law": (2.5, 4096), "zipf_per_peer": 8, "churn_frac": 0.01, "ring": 8192,
+    "c5": {"power_law": (2.5, 4096), "i0": 1.0, "zipf_per_peer": 8, "churn_frac": 0.01, "topic_slots": 96,
            "msg_rate": 4.0, "px": True},
 }
 
@@ -125,7 +127,8 @@ def build_network(cfg, seed, scen=None):
     beh = None
     if "power_law" in scen:
         ex, cap = scen["power_law"]
-        net = graphs.power_law(n, k, ex, cap, seed=seed, n_topics=T)
+        gen = graphs.power_law_native if n > 200_000 else graphs.power_law   # numpy: minutes at 10M
+        net = gen(n, k, ex, cap, seed=seed, n_topics=T, i0=scen.get("i0"))
         net = graphs.with_subscriptions(net, graphs.zipf_subscriptions(n, T, scen["zipf_per_peer"], seed=seed + 100))
     else:
         net = gsim.random_regular(n, k, seed=seed, n_topics=T)
@@ -160,7 +163,9 @@ def build_engine(cfg, seed, device, scen=None, shard=None):
     eng.load_graph(net)
     eng.set_seed(0x5EED0000 + seed)
     eng.fill_synthetic(seed=seed * 7919 + 1, now=tick_time(0), p_mesh=D / k)
-    eng.msgs_init(scen.get("ring", MSG_RING), ROUNDS, tick_time(0), SECOND, max_arrivals=scen.get("max_arrivals"))
+    ts = scen.get("topic_slots", 0)
+    eng.msgs_init(T * ts if ts else scen.get("ring", MSG_RING), ROUNDS, tick_time(0), SECOND,
+                  max_arrivals=scen.get("max_arrivals"), topic_slots=ts)
     if beh is not None:
         eng.set_peer_behaviour(beh)
     if os.environ.get("GSIM_SEND_VARIANT") and shard is None:   # A/B of the delivery kernel (gsim.h)
@@ -173,7 +178,8 @@ def build_engine(cfg, seed, device, scen=None, shard=None):
 def describe_graph(cfg, scen) -> str:
     k = cfg[1]
     if "power_law" in scen:
-        d = (f"Chung-Lu power law (exponent {scen['power_law'][0]:g}, mean {k}, rows <= {scen['power_law'][1]}), "
+        d = (f"Chung-Lu power law (exponent {scen['power_law'][0]:g}, mean {k}, rows <= {scen['power_law'][1]}"
+             f"{', i0 = %g' % scen['i0'] if 'i0' in scen else ''}), "
              f"Zipf subscriptions ({scen['zipf_per_peer']} topics/peer)")
     else:
         d = f"random-regular k={k}"
@@ -184,6 +190,8 @@ def describe_graph(cfg, scen) -> str:
         d += f", {scen['churn_frac']:.0%} of connections down per tick (back 2 ticks later)"
     if scen.get("px"):
         d += ", peer exchange"
+    if scen.get("topic_slots"):
+        d += f", per-topic sub-rings of {scen['topic_slots']} slots (member-compacted seen-set)"
     return d
 
 
@@ -247,7 +255,9 @@ def cpu_baseline(cfg, scen=None, n: int = 10_000, ticks: int = 5, budget_s: floa
         synthetic_state(st, np.random.default_rng(3), tick_time(0), D / k)   # gsim_fill_synthetic's distributions
         if "zipf_per_peer" in scen:
             restrict_to_subscriptions(st, net)
-        msgs = ob.Msgs(n, T, scen.get("ring", MSG_RING), ROUNDS, tick_time(0), SECOND, behaviour=beh)
+        ts = scen.get("topic_slots", 0)
+        msgs = ob.Msgs(n, T, T * ts if ts else scen.get("ring", MSG_RING), ROUNDS, tick_time(0), SECOND,
+                       behaviour=beh, topic_slots=ts)
         sched = message_schedule(n, T, range(1, ticks + 2), sub=net.sub if "zipf_per_peer" in scen else None,
                                  rate=rate)
         churn = churn_schedule(net, scen["churn_frac"], range(1, ticks + 2)) if "churn_frac" in scen else {}
@@ -377,6 +387,13 @@ def main():
         g_seed, s_seed = replica_seeds(rank)
     eng, net = build_engine(cfg, seed=g_seed, device=local, scen=scen, shard=shard)
     E = net.e
+    hbm_used = None
+    try:                                         # device memory in use once the state is resident
+        import torch
+        free_b, total_b = torch.cuda.mem_get_info(local)
+        hbm_used = (total_b - free_b) / 1e9
+    except Exception:
+        pass
     ticks = range(1, args.warmup + args.steps + 1)
     rate = scen.get("msg_rate", MSG_RATE)
     sched = message_schedule(n, T, ticks, seed=s_seed, sub=net.sub if "zipf_per_peer" in scen else None, rate=rate)
@@ -486,6 +503,8 @@ def main():
                     "Philox-seeded steady-state counters and meshes, Poisson message publications)",
             "config": {"workload": workload, "peers_per_gpu": n, "degree": k, "topics": T,
                        "edge_topic_records": E * T, "rounds_per_heartbeat": ROUNDS,
+                       "max_degree": int(np.diff(net.row_ptr.astype(np.int64)).max()),
+                       "hbm_used_gb": hbm_used,
                        "step": "heartbeat tick: refreshScores+score, mesh maintenance, "
                                f"{ROUNDS} propagation rounds (publish, deliver, control, forward)",
                        "parallelism": (f"graph-sharded x{world} (RCCL halo exchange)" if sharded and world > 1

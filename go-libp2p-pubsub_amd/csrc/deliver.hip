@@ -85,7 +85,16 @@ struct Deliver {
     int64_t vq_cap = 0;
     bool lat_on = false;               // a message with vdelay > 0 was published
     uint64_t* d_mid = nullptr;         // [ring] gsim_msg.id of the slot's message (wire ids)
-    uint64_t* d_cell = nullptr;        // [ring][N] seen-set cells (layout above)
+    uint64_t* d_cell = nullptr;        // seen-set cells (layout above; gsim_internal.h Cells)
+    size_t n_cells = 0;
+    uint64_t* d_cbase = nullptr;       // [ring] first cell of each slot
+    std::vector<uint64_t> cbase;       // host copy
+    uint64_t* d_mbits = nullptr;       // [T][nw] members of each topic (peers with its slot, §2)
+    uint32_t* d_mpre = nullptr;        // [T][nw] members before each word
+    uint64_t sparse = 0;               // topics with member-compacted cells (Cells::sparse)
+    int64_t cell_nw = 0;               // words per topic of the member bitmaps
+    std::vector<int64_t> tcount;       // [T] messages published per topic (sub-ring slot choice)
+    uint32_t* d_pslot = nullptr;       // [pub_cap] ring slots of a publish batch
     uint64_t* d_seenbm = nullptr;      // [ring][ceil(N/64)] bit: the cell is committed (a cache of the cells)
     uint64_t* d_fresh = nullptr;       // [ring][ceil(N/64)] bit: the peer forwards the slot's message next round
     uint64_t* d_fsum = nullptr;        // [ring][ceil(N/4096)] bit: that fresh word may be non-zero
@@ -147,7 +156,7 @@ struct RoundArgs {
     uint64_t* vq;              // [kVqPlanes][vq_cap] pending copies (Deliver::d_vq)
     uint32_t* vqn;
     int64_t vq_cap;
-    uint64_t* cell;
+    Cells cs;                  // the seen-set cells (gsim_internal.h)
     uint64_t* seenbm;          // [ring][nw] committed bits of the cells (read before a cell)
     uint64_t* fresh;           // [ring][nw] forwarders of the next round (topic-major delivery; nullptr otherwise)
     uint64_t* fsum;            // [ring][nsw] summary: bit j of word s = fresh word 64 s + j may be non-zero
@@ -168,11 +177,9 @@ struct RoundArgs {
     const uint32_t* rev;
     int32_t flood;
     double pub_thr;
-    // seen-set cells: cell[m * CN + (i - clo)] for peers [clo, clo + CN)
-    // (every local peer: a shard's ghost cells hold the first-seen rounds its
-    // owners exported)
+    // every local peer may hold cells (a shard's ghost cells hold the
+    // first-seen rounds their owners exported)
     int64_t CN;
-    uint32_t clo;
     // receivers: the owned peers [rlo, rhi) (every peer unless sharded); a
     // shard pulls the copies its ghost senders forward to them, and leaves
     // the copies its own senders forward to ghosts to the ghosts' shards
@@ -338,6 +345,19 @@ __device__ __forceinline__ void commit_claim(const RoundArgs& a, uint64_t* cellp
     if (lo & kCreditMesh) atomic_inc_capped(&a.meshd[ir], tp->mesh_message_deliveries_cap);
 }
 
+// Cell index of lane `lane` of the 64-peer word w in slot m (gsim_internal.h
+// Cells): every lane of a wave asks for the same (m, w), so the slot's base
+// and the topic's member word are wave-uniform loads; -1: no cell.
+__device__ __forceinline__ int64_t word_cell(const Cells& c, const uint32_t* mtopic, uint32_t m, int64_t w, int lane)
+{
+    uint64_t bits;
+    int64_t pre;
+    c.word((int32_t)mtopic[m], w, bits, pre);
+    const uint64_t bit = 1ull << lane;
+    if (!(bits & bit)) return -1;
+    return (int64_t)c.cbase[m] + pre + __popcll(bits & (bit - 1));
+}
+
 __device__ __forceinline__ bool is_claim_of(uint64_t c, uint32_t parity)
 {
     const uint32_t hi = (uint32_t)(c >> 32);
@@ -356,12 +376,13 @@ __device__ __forceinline__ void fresh_set(const RoundArgs& a, uint32_t m, int64_
 
 // Reset the rows of the slots being published into; a claim still pending
 // there (its message was propagating) is committed first.
-__global__ void k_reset_slots(RoundArgs a, const gsim_msg* pub, int32_t count)
+__global__ void k_reset_slots(RoundArgs a, const uint32_t* pslot, int32_t count)
 {
     const int k = blockIdx.y;
     if (k >= count) return;
-    const uint32_t m = (uint32_t)(pub[k].id % (uint64_t)a.ring);
-    uint64_t* row = a.cell + (int64_t)m * a.CN;
+    const uint32_t m = pslot[k];
+    const int32_t t = (int32_t)a.mtopic[m];             // the slot's previous message (a sub-ring: its topic)
+    const int64_t base = (int64_t)a.cs.cbase[m];
     const uint32_t q = (uint32_t)((a.g - 1) & 1);
     // the previous message may still sit in a gossip window or a promise
     if (blockIdx.x == 0 && threadIdx.x == 0 && a.slot_last[m] >= 0 && a.g - a.slot_last[m] < a.reuse_guard)
@@ -369,13 +390,17 @@ __global__ void k_reset_slots(RoundArgs a, const gsim_msg* pub, int32_t count)
     if (blockIdx.x == 0 && a.peertx)
         for (int j = threadIdx.x; j < a.ptx_w; j += blockDim.x) a.peertx[(int64_t)m * a.ptx_w + j] = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.CN; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t c = row[i];
-        // several reused rows may credit one record: atomic updates here
-        if (a.g > 0 && is_claim_of(c, q)) {
-            if (a.mlat) commit_claim<true, true>(a, row + i, c, a.g - 1, m, a.clo + i);
-            else commit_claim<true>(a, row + i, c, a.g - 1, m, a.clo + i);
+        const int64_t ci = a.cs.at(base, t, (uint32_t)i);
+        if (ci >= 0) {
+            uint64_t* cp = a.cs.cell + ci;
+            const uint64_t c = *cp;
+            // several reused rows may credit one record: atomic updates here
+            if (a.g > 0 && is_claim_of(c, q)) {
+                if (a.mlat) commit_claim<true, true>(a, cp, c, a.g - 1, m, i);
+                else commit_claim<true>(a, cp, c, a.g - 1, m, i);
+            }
+            *cp = kUnseen64;
         }
-        row[i] = kUnseen64;
         if ((i & 63) == 0) {
             a.seenbm[(int64_t)m * a.nw + (i >> 6)] = 0;
             if (a.fresh) a.fresh[(int64_t)m * a.nw + (i >> 6)] = 0;
@@ -384,21 +409,22 @@ __global__ void k_reset_slots(RoundArgs a, const gsim_msg* pub, int32_t count)
     }
 }
 
-__global__ void k_publish(RoundArgs a, const gsim_msg* pub, int32_t count)
+__global__ void k_publish(RoundArgs a, const gsim_msg* pub, const uint32_t* pslot, int32_t count)
 {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= count) return;
     const gsim_msg p = pub[k];
-    const uint32_t slot = (uint32_t)(p.id % (uint64_t)a.ring);
+    const uint32_t slot = pslot[k];
     a.mtopic[slot] = p.topic;
     a.morigin[slot] = p.origin;          // local id (a shard: 0xFFFFFFFF when not a local peer)
     a.minv[slot] = p.verdict;
     a.mlat_w[slot] = p.vdelay;
     a.mpub[slot] = (int32_t)a.g;
     if (a.mid) a.mid[slot] = p.id;
-    if (p.origin >= a.clo && (int64_t)(p.origin - a.clo) < a.CN) {   // the origin's own cell
-        const uint32_t oc = p.origin - a.clo;
-        a.cell[(int64_t)slot * a.CN + oc] = ((uint64_t)(uint32_t)a.g << 32) | p.origin;
+    const int64_t oci = (int64_t)p.origin < a.CN ? a.cs.idx(slot, (int32_t)p.topic, p.origin) : -1;
+    if (oci >= 0) {                                        // the origin's own cell (it holds the topic, §2)
+        const uint32_t oc = p.origin;
+        a.cs.cell[oci] = ((uint64_t)(uint32_t)a.g << 32) | p.origin;
         atomicOr(reinterpret_cast<unsigned long long*>(a.seenbm + (int64_t)slot * a.nw + (oc >> 6)), 1ull << (oc & 63));
         if (a.fresh) fresh_set(a, slot, oc >> 6, 1ull << (oc & 63));   // the origin publishes whatever the verdict
         int32_t* lp = a.lastput + (int64_t)p.topic * a.N + p.origin;
@@ -502,6 +528,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
     __shared__ uint16_t s_own[kTmWin];                       // sender (index above) of each flattened edge of a window
     __shared__ uint32_t s_wsum[64];
     __shared__ uint32_t s_m[kTsSlots], s_org[kTsSlots];      // the pass's slots and their origins
+    __shared__ uint64_t s_cb[kTsSlots];                      // ... and their first cells (Cells::cbase)
     __shared__ uint8_t s_vd[kTsSlots], s_ow[kTsSlots], s_wa[kTsSlots], s_lat[kTsSlots];
     __shared__ int s_ns, s_nf;
     __shared__ uint32_t s_ne;
@@ -516,8 +543,8 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
         }
     }
     const int64_t range = a.tmtab[(a.T > 0 ? a.T : 1) + 1 + t];
-    const int64_t pend_ = (int64_t)a.clo + a.CN;
-    const int64_t lo = (int64_t)a.clo + (int64_t)(blockIdx.x - a.tmtab[t]) * range;
+    const int64_t pend_ = a.CN;
+    const int64_t lo = (int64_t)(blockIdx.x - a.tmtab[t]) * range;
     const int64_t hi = lo + range < pend_ ? lo + range : pend_;
     const int64_t wlo = (int64_t)a.rlo >> 6;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -537,13 +564,13 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
     const double mcap = tp->mesh_message_deliveries_cap;
     const uint32_t par = (uint32_t)(a.g & 1);
     const uint32_t claim_hi = kClaim | (par << 30);
-    const uint32_t clo = a.clo;
     unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
     for (int k0 = 0; k0 < ns; k0 += kTsSlots) {
         const int nb = ns - k0 < kTsSlots ? ns - k0 : kTsSlots;
         if (tid < nb) {
             const uint32_t m = s_slots[k0 + tid], origin = a.morigin[m];
             s_m[tid] = m;
+            s_cb[tid] = a.cs.cbase[m];
             s_org[tid] = origin;
             s_vd[tid] = a.minv[m];
             s_ow[tid] = (origin < a.N && ((a.sub[origin] >> t) & 1ull)) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
@@ -556,7 +583,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
         for (int64_t c0 = lo; c0 < hi; c0 += kTmChunk) {
             // the pass's slots with fresh bits in the chunk: every wave
             // computes the same ballot from the summary words
-            const int64_t cw0 = (c0 - clo) >> 6;
+            const int64_t cw0 = c0 >> 6;
             bool nzs = false;
             if (lane < nb)
                 nzs = ((a.fsum[(int64_t)s_m[lane] * a.nsw + (cw0 >> 6)] >> (cw0 & 63)) & kChunkWords) != 0;
@@ -564,8 +591,8 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
             if (!cm) continue;                                   // block-uniform
             // thread tid: peers x0, x0 + 1; pm[u] bit k: fresh in the pass's slot k
             const int64_t x0 = c0 + 2 * (int64_t)tid;
-            const int64_t wi = (x0 - clo) >> 6;
-            const int sh = (int)((x0 - clo) & 63);
+            const int64_t wi = x0 >> 6;
+            const int sh = (int)(x0 & 63);
             const uint32_t vmask = x0 + 1 < hi ? 3u : 1u;
             uint64_t pm[2] = {0, 0}, nzk = 0;
             if (x0 < hi) {
@@ -600,7 +627,9 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                     if ((fb >> u) & 1u) {
                         k2[u] = (uint32_t)__builtin_ctzll(pm[u]);
                         const uint32_t x = (uint32_t)(x0 + u), m = s_m[k2[u]];
-                        from2[u] = (uint32_t)a.cell[(int64_t)m * a.CN + (x - clo)] & kPeerMask;
+                        const int64_t xc = a.cs.at((int64_t)s_cb[k2[u]], t, x);   // a forwarder's cell (committed)
+                        from2[u] = xc >= 0 ? (uint32_t)a.cs.cell[xc] & kPeerMask : kPeerMask;
+                        (void)m;
                         const uint64_t xm = smask_of(a.smask, x);
                         pl2[u] = (uint32_t)__popcll(xm & ((1ull << t) - 1ull));
                         const uint32_t rb = a.row_ptr[x], deg = a.row_ptr[x + 1] - rb;
@@ -655,7 +684,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                     }
                     if (first_layer) {
                         // the bits are read: clear them (one thread per word)
-                        if (((x0 - clo) & 63) == 0)
+                        if ((x0 & 63) == 0)
                             for (uint64_t b = nzk; b; b &= b - 1)
                                 a.fresh[(int64_t)s_m[__builtin_ctzll(b)] * a.nw + wi] = 0;
                         if (tid < nb && ((cm >> tid) & 1ull))
@@ -752,7 +781,6 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             if (vv[u] && (ds & GSIM_DS_DIRECT) && !sel) sel = (a.sub[i] >> t) & 1ull;
                             const bool tg = vv[u] && sel && (ds & GSIM_DS_CONNECTED) && i != fv[u] && i != origin;
                             const bool remote = i < a.rlo || i >= a.rhi;
-                            const uint32_t ic = i - clo;
                             const bool ok = tg && !remote && (ds & GSIM_DS_ACCEPT);
                             n_gray += tg && !remote && !ok;
                             n_acc += ok;
@@ -771,8 +799,11 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             const bool known = ((s_bm[bw] >> (i & 63)) & 1ull) &&
                                                (L ? (!scored_t || (inv && !pen))
                                                   : (s_wa[k] || !sc || inv || !(tf & GSIM_TF_IN_MESH)));
-                            const int64_t row_m = (int64_t)m * a.CN;
-                            const uint64_t c = known ? 0ull : a.cell[row_m + ic];
+                            // the receiver's cell (a member of t: mesh, direct, fanout and flood
+                            // targets all hold the topic, §2); -1 cannot happen
+                            const int64_t ci = known ? 0 : a.cs.at((int64_t)s_cb[k], t, i);
+                            if (ci < 0) continue;
+                            const uint64_t c = known ? 0ull : a.cs.cell[ci];
                             const uint32_t chi = (uint32_t)(c >> 32);
                             // the round validation completed (or completes) in; -1: unclaimed
                             // or claimed in this round
@@ -789,7 +820,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                                     if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo_w |= kCreditMesh;
                                 }
                                 const uint64_t cv = ((uint64_t)(claim_hi | e) << 32) | lo_w;
-                                const uint64_t prev = __hip_atomic_fetch_min(a.cell + row_m + ic, cv, __ATOMIC_RELAXED,
+                                const uint64_t prev = __hip_atomic_fetch_min(a.cs.cell + ci, cv, __ATOMIC_RELAXED,
                                                                              __HIP_MEMORY_SCOPE_AGENT);
                                 if (prev == kUnseen64) { n_first++; clm |= 1ull << k; }
                             }
@@ -872,18 +903,21 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
     const int nact = active_slots(a.nnew_cur, a.ring, s_act, &s_n);
     const int lane = threadIdx.x & 63;
     // claims exist only at receivers' cells: the words of [rlo, rhi)
-    const int64_t i0 = (((int64_t)a.rlo - a.clo) & ~63ll) + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
-    if (i0 >= (int64_t)a.rhi - a.clo || nact == 0) return;
+    const int64_t i0 = ((int64_t)a.rlo & ~63ll) + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+    if (i0 >= (int64_t)a.rhi || nact == 0) return;
     const int64_t i = i0 + lane;
     const bool vi = i < a.CN;
     const uint32_t par = (uint32_t)(a.g & 1);
     for (int k0 = 0; k0 < nact; k0 += kSlotBatch) {
         uint64_t cv[kSlotBatch];
+        int64_t ci[kSlotBatch];
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
-            cv[b] = (k < nact && vi) ? a.cell[(int64_t)s_act[k] * a.CN + i] : kUnseen64;
+            ci[b] = (k < nact && vi) ? word_cell(a.cs, a.mtopic, s_act[k], i0 >> 6, lane) : -1;
         }
+#pragma unroll
+        for (int b = 0; b < kSlotBatch; ++b) cv[b] = ci[b] >= 0 ? a.cs.cell[ci[b]] : kUnseen64;
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
@@ -908,7 +942,7 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
             uint64_t qv = 0;
             if (is_claim_of(cv[b], par)) {
                 const uint32_t m = s_act[k];
-                commit_claim<false, LAT>(a, a.cell + (int64_t)m * a.CN + i, cv[b], a.g, m, a.clo + i, &qpl, &qv);
+                commit_claim<false, LAT>(a, a.cs.cell + ci[b], cv[b], a.g, m, i, &qpl, &qv);
             }
             if constexpr (LAT) vq_push_wave(a, qpl, qv);
         }
@@ -943,7 +977,7 @@ struct IhArgs {
     const uint32_t *mtopic, *morigin;
     const uint8_t* minv;
     const uint8_t* mlat;           // validation latencies (RoundArgs::mlat)
-    const uint64_t* cell;
+    Cells cs;                      // the seen-set (gsim_internal.h)
     const int32_t* slot_last;
     const uint8_t *gsel, *gstate, *behaviour;
     uint64_t* pcand;
@@ -955,8 +989,7 @@ struct IhArgs {
     unsigned long long* gstats;    // [0] receivers x slots walked, [1] IWANT ids, [2] responses, [3] broken promises
     bool respond;                  // GossipRetransmission >= 1
     uint64_t seed;
-    int64_t CN;                    // cells exist for peers [clo, clo + CN) (RoundArgs)
-    uint32_t clo;
+    int64_t CN;                    // local peers (RoundArgs)
     // sharded network: receivers are the owned peers [rlo, rhi) and every slot
     // is pulled (receivers walk); a ghost advertiser's holding is its ghost
     // cell (first-seen rounds its shard exported); keys use global ids
@@ -1031,9 +1064,9 @@ __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount
     // apply, k_ihave_pairs handles this stage (bit 2)
     if (blockIdx.x == 0 && threadIdx.x == 0 && s_n > a.max_ihave) atomicOr(&a.nresp[3], 4u);
     const int lane = threadIdx.x & 63;
-    const int64_t p0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;   // cell index (peer clo + p)
+    const int64_t p0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;   // peers p0 .. p0 + 63
     const int nact = p0 < a.CN ? s_n : 0;
-    const int64_t pc = p0 + lane, pl = a.clo + pc;
+    const int64_t pc = p0 + lane, pl = pc;
     const bool vp = pc < a.CN;
     const uint64_t subp = vp ? a.sub[pl] : 0ull;
     const int64_t tick_round = a.tick * a.R;
@@ -1042,7 +1075,9 @@ __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
-            cv[b] = (k < nact && vp) ? a.cell[(int64_t)s_act[k] * a.CN + pc] : 0ull;
+            // a peer without a cell (not a member of the slot's topic) has not seen it
+            const int64_t ci = (k < nact && vp) ? word_cell(a.cs, a.mtopic, s_act[k], p0 >> 6, lane) : -1;
+            cv[b] = ci >= 0 ? a.cs.cell[ci] : kUnseen64;
         }
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
@@ -1089,9 +1124,9 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int64_t p0 = ((int64_t)blockIdx.x * 4 + wid) * 64;   // cell index (peer clo + p)
+    const int64_t p0 = ((int64_t)blockIdx.x * 4 + wid) * 64;   // peers p0 .. p0 + 63
     const int nact = p0 < a.CN ? s_n : 0;
-    const int64_t pc = p0 + lane, pl = a.clo + pc;
+    const int64_t pc = p0 + lane, pl = pc;
     const bool vp = pc < a.CN;
     const int grp = lane / W, gl = lane % W;
     const uint64_t gmask = group_mask<W>(grp);
@@ -1120,7 +1155,8 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
-            cv[b] = (k < nact && vp) ? a.cell[(int64_t)(s_act[k] & 0x7FFF) * a.CN + pc] : 0ull;
+            const int64_t ci = (k < nact && vp) ? word_cell(a.cs, a.mtopic, s_act[k] & 0x7FFF, p0 >> 6, lane) : -1;
+            cv[b] = ci >= 0 ? a.cs.cell[ci] : kUnseen64;   // no cell: not a member, nothing held or wanted
         }
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
@@ -1138,7 +1174,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                                         : (cv[b] == kUnseen64 && ((subp >> t) & 1ull) && pl >= a.rlo && pl < a.rhi));
             const uint64_t mask = __ballot(me);
             if (!mask) continue;
-            const int64_t row_m = (int64_t)m * a.CN;
+            const int64_t cb_m = (int64_t)a.cs.cbase[m];
             // one chunk of a row walk: lane gl of a group of `gw` lanes takes
             // edge beg + off + gl of peer me_id's row (me_pl: its plane of t)
             auto chunk = [&](uint32_t off, uint32_t gl_, uint32_t beg, uint32_t deg, uint32_t me_id, uint32_t me_g,
@@ -1152,7 +1188,8 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                     if (v && me_pl >= 0 && a.gsel[me_pl + e]) {
                         const uint32_t p = a.col[e], re = a.rev[e];
                         // p's gate on i, p has not seen m (a shard: p one of its receivers)
-                        req = p >= a.rlo && p < a.rhi && a.gstate[re] && a.cell[row_m + (p - a.clo)] == kUnseen64;
+                        const int64_t pci = a.cs.at(cb_m, t, p);
+                        req = p >= a.rlo && p < a.rhi && a.gstate[re] && pci >= 0 && a.cs.cell[pci] == kUnseen64;
                         if (req) {
                             const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, a.gid ? a.gid[p] : p, 0, P_PROMISE,
                                                           m, me_g);
@@ -1168,7 +1205,8 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                         const uint32_t i = a.col[e];
                         const uint64_t mi = smask_of(a.smask, i);        // i's emitGossip choices: its row
                         if (slot_has(mi, t) && a.gsel[slot_idx(mi, t, a.E, re)] && a.gstate[e]) {
-                            req = holds_in_window(a.cell[row_m + (i - a.clo)], a.g, a.lo_round, tick_round, inv,
+                            const int64_t ici = a.cs.at(cb_m, t, i);
+                            req = holds_in_window(ici >= 0 ? a.cs.cell[ici] : kUnseen64, a.g, a.lo_round, tick_round, inv,
                                                   i == origin, LAT ? a.mlat[m] : 0u);
                             if (req) {
                                 const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, me_g, 0, P_PROMISE, m,
@@ -1201,7 +1239,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                 const int sl = bs < 0 ? lane : bs;
                 const uint32_t beg = __shfl(rp0, sl, 64), end = __shfl(rp1, sl, 64);
                 const bool ign_s = __shfl(ign_l, sl, 64);
-                const uint32_t me_id = (uint32_t)(a.clo + p0 + (bs < 0 ? 0 : bs));
+                const uint32_t me_id = (uint32_t)(p0 + (bs < 0 ? 0 : bs));
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;   // Philox keys use global ids
                 const uint64_t me_m = smask_of(a.smask, me_id);
                 const int64_t me_pl = slot_has(me_m, t) ? slot_idx(me_m, t, a.E, 0) : -1;
@@ -1215,7 +1253,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                 const int bs = __builtin_ctzll(lm);
                 const uint32_t beg = __shfl(rp0, bs, 64), end = __shfl(rp1, bs, 64);
                 const bool ign_s = __shfl(ign_l, bs, 64);
-                const uint32_t me_id = (uint32_t)(a.clo + p0 + bs);
+                const uint32_t me_id = (uint32_t)(p0 + bs);
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
                 const uint64_t me_m = smask_of(a.smask, me_id);
                 const int64_t me_pl = slot_has(me_m, t) ? slot_idx(me_m, t, a.E, 0) : -1;
@@ -1313,7 +1351,7 @@ __global__ __launch_bounds__(256) void k_ihave_pairs(IhArgs a)
         return lo;
     };
     for (int64_t pc = (int64_t)blockIdx.x * 4 + wid; pc < a.CN; pc += (int64_t)gridDim.x * 4) {
-        const uint32_t p = a.clo + (uint32_t)pc;
+        const uint32_t p = (uint32_t)pc;
         if (p < a.rlo || p >= a.rhi) continue;                    // receivers: owned peers
         const uint64_t subp = a.sub[p];
         const uint32_t beg = a.row_ptr[p], end = a.row_ptr[p + 1];
@@ -1329,10 +1367,9 @@ __global__ __launch_bounds__(256) void k_ihave_pairs(IhArgs a)
             if (!tmask) continue;
             n_walk += (lane == 0);
             const uint32_t i_g = a.gid ? a.gid[i] : i;
-            const int64_t ic = (int64_t)i - a.clo;
             const uint32_t origin_ign = a.behaviour[i] & GSIM_BEHAVE_IGNORE_IWANT;
             auto holds = [&](uint32_t m) {
-                return holds_in_window(a.cell[(int64_t)m * a.CN + ic], a.g, a.lo_round, tick_round, a.minv[m] != 0,
+                return holds_in_window(a.cs.get(m, (int32_t)a.mtopic[m], i), a.g, a.lo_round, tick_round, a.minv[m] != 0,
                                        i == a.morigin[m], LAT ? a.mlat[m] : 0u);
             };
             // GetGossipIDs(topic) of i: ids per topic
@@ -1362,7 +1399,7 @@ __global__ __launch_bounds__(256) void k_ihave_pairs(IhArgs a)
             // the ids i advertised to p and p has not seen
             auto wanted = [&](uint32_t m) {
                 const int t = (int)a.mtopic[m];
-                if (!((tmask >> t) & 1ull) || a.cell[(int64_t)m * a.CN + pc] != kUnseen64 || !holds(m)) return false;
+                if (!((tmask >> t) & 1ull) || a.cs.get(m, t, p) != kUnseen64 || !holds(m)) return false;
                 return s_cnt[t] <= L ||
                        pair_key(a.seed, (uint32_t)a.tick, i_g, (uint32_t)t, P_IHAVE_TRUNC, m, p_g) <= s_tau[t];
             };
@@ -1503,7 +1540,9 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
         const bool sc = tp->scored && (ds & GSIM_DS_TRACKED) && slot_has(mi, t);
         const uint8_t tf = a.tflags[ir];
         const int64_t window = tp->mesh_message_deliveries_window_ns;
-        uint64_t* cellp = a.cell + (int64_t)m * a.CN + (p - a.clo);
+        const int64_t pci = a.cs.idx(m, t, p);      // p wanted it: a member of t
+        if (pci < 0) continue;
+        uint64_t* cellp = a.cs.cell + pci;
         const uint64_t c = *cellp;
         const uint32_t hi = (uint32_t)(c >> 32);
         const uint32_t L = a.mlat ? a.mlat[m] : 0u;
@@ -1571,9 +1610,9 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
 // heartbeat; a promise is broken unless its receiver has seen the message
 // (fulfillPromise at first reception).  Record order: the penalty lands on
 // the promiser's record of the advertiser, rev[e].
-__global__ __launch_bounds__(256) void k_promise_check(uint32_t* prom_q, const uint64_t* cell, const uint32_t* owner,
-                                                       const uint32_t* rev, uint8_t* pen, int64_t E, int64_t CN,
-                                                       uint32_t clo, unsigned long long* gstats)
+__global__ __launch_bounds__(256) void k_promise_check(uint32_t* prom_q, Cells cs, const uint32_t* mtopic,
+                                                       const uint32_t* owner, const uint32_t* rev, uint8_t* pen,
+                                                       int64_t E, unsigned long long* gstats)
 {
     // promises sit at the promiser's (an owned receiver's) edges only
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -1582,7 +1621,7 @@ __global__ __launch_bounds__(256) void k_promise_check(uint32_t* prom_q, const u
         const uint32_t slot = prom_q[e];
         if (slot == 0xFFFFFFFFu) continue;
         prom_q[e] = 0xFFFFFFFFu;
-        if (cell[(int64_t)slot * CN + (owner[e] - clo)] == kUnseen64) {
+        if (cs.get(slot, (int32_t)mtopic[slot], owner[e]) == kUnseen64) {
             pen[rev[e]] = (uint8_t)(pen[rev[e]] + 1);
             ++broken;
         }
@@ -1646,19 +1685,20 @@ __global__ __launch_bounds__(256) void k_vcomplete(RoundArgs a, const uint32_t* 
     __syncthreads();
     const int nact = s_n;
     const int lane = threadIdx.x & 63;
-    const int64_t i0 = (((int64_t)a.rlo - a.clo) & ~63ll) + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
-    if (i0 >= (int64_t)a.rhi - a.clo || nact == 0) return;
+    const int64_t i0 = ((int64_t)a.rlo & ~63ll) + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+    if (i0 >= (int64_t)a.rhi || nact == 0) return;
     const int64_t i = i0 + lane;
     const bool vi = i < a.CN;
     const int32_t tick = (int32_t)(a.g / a.R);
     for (int k = 0; k < nact; ++k) {
         const uint32_t m = s_act[k];
-        const uint64_t c = vi ? a.cell[(int64_t)m * a.CN + i] : kUnseen64;
+        const int64_t ci = vi ? word_cell(a.cs, a.mtopic, m, i0 >> 6, lane) : -1;
+        const uint64_t c = ci >= 0 ? a.cs.cell[ci] : kUnseen64;
         const bool done = c != kUnseen64 && !((uint32_t)(c >> 32) & kClaim) && (int64_t)(c >> 32) == a.g;
         const uint64_t b = __ballot(done);
         if (!b) continue;
         const bool acc = a.minv[m] == GSIM_VERDICT_ACCEPT;
-        if (done && acc) atomicMax(a.lastput + (int64_t)a.mtopic[m] * a.N + a.clo + i, tick);   // mcache.Put
+        if (done && acc) atomicMax(a.lastput + (int64_t)a.mtopic[m] * a.N + i, tick);   // mcache.Put
         if (lane == 0) {
             atomicMax(&a.slot_last[m], (int32_t)a.g);
             if (acc) {
@@ -1672,12 +1712,12 @@ __global__ __launch_bounds__(256) void k_vcomplete(RoundArgs a, const uint32_t* 
 }
 
 // F_SEEN view [ring][N]: first-seen rounds of the peers with cells, unseen elsewhere
-__global__ void k_seen_view(const uint64_t* cell, uint32_t* out, int64_t n, int64_t N, int64_t CN, uint32_t clo)
+__global__ void k_seen_view(Cells cs, const uint32_t* mtopic, uint32_t* out, int64_t n, int64_t N)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += stride) {
-        const int64_t m = x / N, i = x - m * N - (int64_t)clo;
-        out[x] = (i >= 0 && i < CN) ? (uint32_t)(cell[m * CN + i] >> 32) : 0xFFFFFFFFu;
+        const int64_t m = x / N, i = x - m * N;
+        out[x] = (uint32_t)(cs.get((uint32_t)m, (int32_t)mtopic[m], (uint32_t)i) >> 32);
     }
 }
 
@@ -1697,6 +1737,7 @@ static void dl_free(Deliver* d)
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_peertx); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
     f(d->d_mlat); f(d->d_vq); f(d->d_vqn); f(d->d_hist);
+    f(d->d_cbase); f(d->d_mbits); f(d->d_mpre); f(d->d_pslot);
     delete d;
 }
 
@@ -1725,6 +1766,18 @@ static int grid_peers(int64_t n)
 }
 
 
+static Cells deliver_cells(const Deliver* d)
+{
+    Cells c;
+    c.cell = d->d_cell;
+    c.cbase = d->d_cbase;
+    c.mbits = d->d_mbits;
+    c.mpre = d->d_mpre;
+    c.nw = d->cell_nw;
+    c.sparse = d->sparse;
+    return c;
+}
+
 static RoundArgs make_round_args(gsim_handle* h, int64_t g)
 {
     Deliver* d = h->dl;
@@ -1741,9 +1794,8 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.mlat = d->lat_on ? d->d_mlat : nullptr;
     a.mlat_w = d->d_mlat;
     a.vq = d->d_vq; a.vqn = d->d_vqn; a.vq_cap = d->vq_cap;
-    a.cell = d->d_cell; a.lastput = d->d_lastput;
+    a.cs = deliver_cells(d); a.lastput = d->d_lastput;
     a.CN = h->n;
-    a.clo = 0;
     a.rlo = (uint32_t)h->olo();
     a.rhi = (uint32_t)h->ohi();
     a.seenbm = d->d_seenbm; a.nw = (a.CN + 63) / 64; a.mpub = d->d_mpub; a.roff = d->d_roff;
@@ -1788,7 +1840,7 @@ bool deliver_wire_view(gsim_handle* h, WireView* v)
 {
     Deliver* d = h->dl;
     if (!d) return false;
-    v->cell = d->d_cell;
+    v->cells = deliver_cells(d);
     v->mtopic = d->d_mtopic; v->morigin = d->d_morigin; v->minv = d->d_minv; v->mid = d->d_mid;
     v->slot_last = d->d_slot_last;
     v->gsel = d->d_gsel;
@@ -1816,9 +1868,9 @@ int deliver_promise_check(gsim_handle* h, int64_t now)
         const int64_t expire = round_time_host(d, made * d->cfg.rounds) + h->gp.iwant_followup_time_ns;
         if (!(expire < now)) continue;
         hipLaunchKernelGGL(k_promise_check, dim3(std::min<int64_t>((h->e + 255) / 256, 16384)), dim3(256), 0,
-                           h->stream, d->d_prom + (size_t)q * (size_t)h->e, (const uint64_t*)d->d_cell,
-                           (const uint32_t*)h->d_owner, (const uint32_t*)h->d_rev, h->d_pen, h->e,
-                           h->n, (uint32_t)0, d->d_gstats);
+                           h->stream, d->d_prom + (size_t)q * (size_t)h->e, deliver_cells(d),
+                           (const uint32_t*)d->d_mtopic, (const uint32_t*)h->d_owner, (const uint32_t*)h->d_rev,
+                           h->d_pen, h->e, d->d_gstats);
         d->prom_made[(size_t)q] = -1;
         int rc = hip_check(h, hipGetLastError(), "k_promise_check");
         if (rc) return rc;
@@ -1863,7 +1915,7 @@ static bool ihave_prepare(gsim_handle* h, int64_t g, IhaveStage* st, int* rc)
     a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.rev = h->d_rev; a.sub = h->d_sub; a.smask = h->d_smask;
     a.mtopic = d->d_mtopic; a.morigin = d->d_morigin; a.minv = d->d_minv;
     a.mlat = d->lat_on ? d->d_mlat : nullptr;
-    a.cell = d->d_cell; a.slot_last = d->d_slot_last;
+    a.cs = deliver_cells(d); a.slot_last = d->d_slot_last;
     a.gsel = d->d_gsel; a.gstate = d->d_gstate; a.behaviour = d->d_behaviour;
     a.pcand = d->d_pcand; a.prom = d->d_prom; a.P = d->prom_ticks;
     a.prom_idx = (int32_t)(tick % d->prom_ticks);
@@ -1877,7 +1929,6 @@ static bool ihave_prepare(gsim_handle* h, int64_t g, IhaveStage* st, int* rc)
     a.respond = h->gp.gossip_retransmission >= 1;
     a.seed = h->x ? gsim_get_seed(h) : 0;
     a.CN = h->n;
-    a.clo = 0;
     a.rlo = (uint32_t)h->olo();
     a.rhi = (uint32_t)h->ohi();
     if (ShardCtx* sh = h->sh) {
@@ -1966,7 +2017,7 @@ int deliver_flush(gsim_handle* h)
     if (!d || d->pending < 0) return GSIM_OK;
     ProfScope ps(h, GSIM_K_COMMIT);
     RoundArgs a = make_round_args(h, d->pending);
-    const dim3 grid(grid_peers((int64_t)a.rhi - (((int64_t)a.rlo - a.clo) & ~63ll)));
+    const dim3 grid(grid_peers((int64_t)a.rhi - ((int64_t)a.rlo & ~63ll)));
     if (a.mlat)
         hipLaunchKernelGGL(k_commit<true>, grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     else
@@ -2012,7 +2063,7 @@ bool deliver_trace_view(gsim_handle* h, TraceView* v)
 {
     Deliver* d = h->dl;
     if (!d) return false;
-    v->cell = d->d_cell; v->mtopic = d->d_mtopic; v->minv = d->d_minv; v->mid = d->d_mid;
+    v->cells = deliver_cells(d); v->mtopic = d->d_mtopic; v->minv = d->d_minv; v->mid = d->d_mid;
     v->ring = d->cfg.ring; v->rounds = d->cfg.rounds;
     v->mlat = d->lat_on ? d->d_mlat : nullptr;
     v->t0 = d->cfg.t0_ns; v->hb = d->cfg.heartbeat_ns; v->roff = d->d_roff;
@@ -2036,7 +2087,7 @@ int deliver_read_seen(gsim_handle* h, void* dst)
     if (!d->d_seen32) e = hipMalloc((void**)&d->d_seen32, std::max<size_t>(n * 4, 4));
     if (e != hipSuccess) return hip_check(h, e, "seen view scratch");
     hipLaunchKernelGGL(k_seen_view, dim3(std::min<int64_t>(((int64_t)n + 255) / 256, 16384)), dim3(256), 0, h->stream,
-                       (const uint64_t*)d->d_cell, d->d_seen32, (int64_t)n, h->n, h->n, (uint32_t)0);
+                       deliver_cells(d), (const uint32_t*)d->d_mtopic, d->d_seen32, (int64_t)n, h->n);
     e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpyAsync(dst, d->d_seen32, n * 4, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
@@ -2154,7 +2205,7 @@ int deliver_round_validate(gsim_handle* h, int64_t round)
     hipError_t e = hipMemcpyAsync(d->d_hist + (size_t)(round & (kVqPlanes - 1)) * (size_t)w, a.nnew_cur,
                                   (size_t)w * 4, hipMemcpyDeviceToDevice, h->stream);
     if (e != hipSuccess) return hip_check(h, e, "validation history");
-    hipLaunchKernelGGL(k_vcomplete, dim3(grid_peers((int64_t)a.rhi - (((int64_t)a.rlo - a.clo) & ~63ll))), dim3(256),
+    hipLaunchKernelGGL(k_vcomplete, dim3(grid_peers((int64_t)a.rhi - ((int64_t)a.rlo & ~63ll))), dim3(256),
                        (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a, (const uint32_t*)d->d_hist, w);
     return hip_check(h, hipGetLastError(), "k_vcomplete");
 }
@@ -2298,7 +2349,7 @@ __global__ __launch_bounds__(256) void k_frontier_export(RoundArgs a, const uint
         int64_t pos = (int64_t)s_base + s_wsum[wid] + (v - c);
         for (uint64_t b = bits; b; b &= b - 1, ++pos) {
             const int64_t i = w * 64 + __ffsll((long long)b) - 1;
-            const uint32_t f = (uint32_t)a.cell[(int64_t)m * a.CN + i] & kPeerMask;
+            const uint32_t f = (uint32_t)a.cs.get(m, (int32_t)a.mtopic[m], (uint32_t)i) & kPeerMask;
             const uint64_t gf = f < a.N ? (uint64_t)gid[f] : kG24;
             if (pos < cap) out[pos] = (uint64_t)gid[i] | (gf << 24) | ((uint64_t)m << 48);
         }
@@ -2327,7 +2378,8 @@ __global__ __launch_bounds__(256) void k_frontier_import(RoundArgs a, const uint
                 uint32_t f = gf == kG24 ? 0xFFFFFFFFu : g2l[gf];
                 if (f == 0xFFFFFFFFu) f = kPeerMask;                         // not a local peer
                 m = (uint32_t)(v >> 48);
-                a.cell[(int64_t)m * a.CN + l] = ((uint64_t)(uint32_t)(a.g - 1) << 32) | f;
+                const int64_t ci = a.cs.idx(m, (int32_t)a.mtopic[m], l);    // a forwarder holds the topic
+                if (ci >= 0) a.cs.cell[ci] = ((uint64_t)(uint32_t)(a.g - 1) << 32) | f;
                 // (filtering out ghosts without mesh edges into this shard, by
                 // their masks, cost more in the import than it saved in the
                 // walk: K = 8 serial shards 31.8 against 20.2 ms per tick)
@@ -2398,6 +2450,96 @@ void deliver_blocks_changed(gsim_handle* h)
 
 int32_t* deliver_slot_last(gsim_handle* h) { return h->dl ? h->dl->d_slot_last : nullptr; }
 
+// The seen-set layout (gsim_internal.h Cells) for the current slot masks:
+// each slot's first cell, the member bitmaps of the topics only some peers
+// hold (sub-rings only: a shared ring's slot may carry any topic), and the
+// number of cells.
+struct CellLayout {
+    std::vector<uint64_t> cbase, mbits;
+    std::vector<uint32_t> mpre;
+    uint64_t sparse = 0;
+    size_t cells = 0;
+};
+
+static CellLayout cell_layout(const gsim_handle* h, const gsim_msg_config& cfg)
+{
+    CellLayout L;
+    const int64_t N = h->n, ring = cfg.ring, R = cfg.topic_slots;
+    const int32_t T = std::max(1, h->t);
+    const int64_t nw = (N + 63) / 64;
+    L.cbase.assign((size_t)ring, 0);
+    if (R <= 0) {
+        for (int64_t m = 0; m < ring; ++m) L.cbase[(size_t)m] = (uint64_t)(m * N);
+        L.cells = (size_t)(ring * N);
+        return L;
+    }
+    std::vector<int64_t> M((size_t)T, N);
+    if (!h->smask.empty()) {
+        std::fill(M.begin(), M.end(), 0);
+        for (int64_t p = 0; p < N; ++p)
+            for (uint64_t b = h->smask[(size_t)p]; b; b &= b - 1) M[(size_t)__builtin_ctzll(b)]++;
+        for (int32_t t = 0; t < T; ++t)
+            if (M[(size_t)t] < N) L.sparse |= 1ull << t;
+    }
+    uint64_t off = 0;
+    for (int32_t t = 0; t < T; ++t)
+        for (int64_t k = 0; k < R; ++k) {
+            L.cbase[(size_t)(t * R + k)] = off;
+            off += (uint64_t)M[(size_t)t];
+        }
+    L.cells = (size_t)off;
+    if (L.sparse) {
+        L.mbits.assign((size_t)T * (size_t)nw, 0);
+        L.mpre.assign((size_t)T * (size_t)nw, 0);
+        for (int64_t p = 0; p < N; ++p)
+            for (uint64_t b = h->smask[(size_t)p] & L.sparse; b; b &= b - 1)
+                L.mbits[(size_t)__builtin_ctzll(b) * (size_t)nw + (size_t)(p >> 6)] |= 1ull << (p & 63);
+        for (int32_t t = 0; t < T; ++t) {
+            uint32_t acc = 0;
+            for (int64_t w = 0; w < nw; ++w) {
+                L.mpre[(size_t)t * (size_t)nw + (size_t)w] = acc;
+                acc += (uint32_t)__builtin_popcountll(L.mbits[(size_t)t * (size_t)nw + (size_t)w]);
+            }
+        }
+    }
+    return L;
+}
+
+// Install a layout: bases, member tables (cells allocated by the caller).
+static hipError_t install_layout(gsim_handle* h, Deliver* d, const CellLayout& L)
+{
+    hipError_t e = hipSuccess;
+    auto fr = [](void* p) { if (p) (void)hipFree(p); };
+    fr(d->d_cbase); fr(d->d_mbits); fr(d->d_mpre);
+    d->d_cbase = nullptr; d->d_mbits = nullptr; d->d_mpre = nullptr;
+    e = hipMalloc((void**)&d->d_cbase, std::max<size_t>(L.cbase.size() * 8, 8));
+    if (e == hipSuccess) e = hipMemcpy(d->d_cbase, L.cbase.data(), L.cbase.size() * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess && L.sparse) {
+        e = hipMalloc((void**)&d->d_mbits, L.mbits.size() * 8);
+        if (e == hipSuccess) e = hipMalloc((void**)&d->d_mpre, L.mpre.size() * 4);
+        if (e == hipSuccess) e = hipMemcpy(d->d_mbits, L.mbits.data(), L.mbits.size() * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(d->d_mpre, L.mpre.data(), L.mpre.size() * 4, hipMemcpyHostToDevice);
+    }
+    d->cbase = L.cbase;
+    d->sparse = L.sparse;
+    d->cell_nw = (h->n + 63) / 64;
+    d->n_cells = L.cells;
+    return e;
+}
+
+// Copy every cell of the old layout that the new one keeps (members of both),
+// the new members' cells unseen.
+__global__ void k_cell_relayout(Cells o, Cells n, const uint32_t* mtopic, int64_t ring, int64_t N)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < ring * N; x += stride) {
+        const uint32_t m = (uint32_t)(x / N), p = (uint32_t)(x - (int64_t)m * N);
+        const int32_t t = (int32_t)mtopic[m];
+        const int64_t ni = n.idx(m, t, p);
+        if (ni >= 0) n.cell[ni] = o.get(m, t, p);
+    }
+}
+
 uint8_t** deliver_gsel_slot(gsim_handle* h)
 {
     static uint8_t* none = nullptr;
@@ -2405,11 +2547,43 @@ uint8_t** deliver_gsel_slot(gsim_handle* h)
 }
 
 // The topic slot masks grew (ensure_slots): the arrays were re-laid out; the
-// delivery's mesh masks are rebuilt from the moved router flags.
+// delivery's mesh masks are rebuilt from the moved router flags, and the
+// seen-set's member spaces follow the masks (new members get unseen cells).
 int slots_changed(gsim_handle* h)
 {
-    if (h->dl) h->dl->mask_version = 0;
-    return GSIM_OK;
+    Deliver* d = h->dl;
+    if (!d) return GSIM_OK;
+    d->mask_version = 0;
+    if (d->cfg.topic_slots <= 0) return GSIM_OK;
+    CellLayout L = cell_layout(h, d->cfg);
+    if (L.cells == d->n_cells && L.sparse == d->sparse && L.mbits.empty() == (d->d_mbits == nullptr)) {
+        // same sizes: unchanged memberships keep every cell (a member set can
+        // only grow, so equal counts mean equal sets)
+        return GSIM_OK;
+    }
+    const Cells old = deliver_cells(d);
+    uint64_t* old_cbase = d->d_cbase;
+    uint64_t* old_mbits = d->d_mbits;
+    uint32_t* old_mpre = d->d_mpre;
+    uint64_t* cell1 = nullptr;
+    hipError_t e = hipMalloc((void**)&cell1, std::max<size_t>(L.cells * 8, 8));
+    if (e != hipSuccess) return hip_check(h, e, "seen-set re-layout");
+    d->d_cbase = nullptr; d->d_mbits = nullptr; d->d_mpre = nullptr;   // kept in `old` until copied
+    e = install_layout(h, d, L);
+    if (e == hipSuccess) {
+        d->d_cell = cell1;
+        const Cells nw = deliver_cells(d);
+        const int64_t n = (int64_t)d->cfg.ring * h->n;
+        hipLaunchKernelGGL(k_cell_relayout, dim3((uint32_t)std::min<int64_t>((n + 255) / 256, 65536)), dim3(256), 0,
+                           h->stream, old, nw, (const uint32_t*)d->d_mtopic, (int64_t)d->cfg.ring, h->n);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    }
+    (void)hipFree(old.cell);
+    if (old_cbase) (void)hipFree(old_cbase);
+    if (old_mbits) (void)hipFree(old_mbits);
+    if (old_mpre) (void)hipFree(old_mpre);
+    return hip_check(h, e, "k_cell_relayout");
 }
 
 extern "C" {
@@ -2427,10 +2601,16 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
         h->err = "too many edges or peers for the seen-set claim encoding (< 2^30 - 1)";
         return GSIM_ERANGE;
     }
+    if (cfg->topic_slots < 0 || (cfg->topic_slots > 0 && (int64_t)cfg->ring != cfg->topic_slots * std::max(1, h->t))) {
+        h->err = "topic_slots: every topic owns topic_slots ring slots, so ring must be n_topics * topic_slots";
+        return GSIM_EINVAL;
+    }
     (void)hipStreamSynchronize(h->stream);
     free_deliver(h);
     Deliver* d = new Deliver();
     d->cfg = *cfg;
+    const CellLayout layout = cell_layout(h, *cfg);
+    d->tcount.assign((size_t)std::max(1, h->t), 0);
     const size_t ring = (size_t)cfg->ring, N = (size_t)h->n, T = (size_t)std::max(1, h->t);
     const size_t CN = N;   // every local peer has cells (a shard's ghost cells: imported first-seen rounds)
     const size_t words = (size_t)nnew_words(d);
@@ -2444,7 +2624,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_minv, ring);
     A((void**)&d->d_mlat, ring);
     A((void**)&d->d_mid, ring * 8);
-    A((void**)&d->d_cell, ring * CN * 8);
+    A((void**)&d->d_cell, layout.cells * 8);
     A((void**)&d->d_seenbm, ring * ((CN + 63) / 64) * 8);
     A((void**)&d->d_fresh, ring * ((CN + 63) / 64) * 8);
     A((void**)&d->d_fsum, ring * (((CN + 63) / 64 + 63) / 64) * 8);
@@ -2483,7 +2663,8 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
         return e == hipErrorOutOfMemory ? GSIM_ENOMEM : GSIM_EDEVICE;
     }
     h->dl = d;
-    e = hipMemsetAsync(d->d_cell, 0xFF, ring * CN * 8, h->stream);
+    e = install_layout(h, d, layout);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_cell, 0xFF, layout.cells * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_seenbm, 0, ring * ((CN + 63) / 64) * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_fresh, 0, ring * ((CN + 63) / 64) * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_fsum, 0, ring * (((CN + 63) / 64 + 63) / 64) * 8, h->stream);
@@ -2495,7 +2676,13 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
         e = hipMemcpy(d->d_roff, roff.data(), roff.size() * 8, hipMemcpyHostToDevice);
     }
     if (e == hipSuccess) e = hipMemsetAsync(d->d_lastput, 0xFF, T * N * 4, h->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(d->d_mtopic, 0, ring * 4, h->stream);
+    if (e == hipSuccess) {
+        // a sub-ring slot carries its topic from the start (the cells' member space)
+        std::vector<uint32_t> mt(ring, 0);
+        if (cfg->topic_slots > 0)
+            for (size_t m = 0; m < ring; ++m) mt[m] = (uint32_t)(m / (size_t)cfg->topic_slots);
+        e = hipMemcpy(d->d_mtopic, mt.data(), ring * 4, hipMemcpyHostToDevice);
+    }
     if (e == hipSuccess) e = hipMemsetAsync(d->d_morigin, 0, ring * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_minv, 0, ring, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_mlat, 0, ring, h->stream);
@@ -2535,15 +2722,24 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
             h->err = "message topic or origin out of range";
             return GSIM_EINVAL;
         }
-        slots[(size_t)m] = (uint32_t)(msgs[m].id % (uint64_t)d->cfg.ring);
+        if (d->cfg.topic_slots > 0) {
+            // a sub-ring: the topic's next slot, in publication order
+            const int64_t R = d->cfg.topic_slots, t = msgs[m].topic;
+            int64_t k = d->tcount[(size_t)t];
+            for (int32_t q = 0; q < m; ++q) k += msgs[q].topic == msgs[m].topic;
+            slots[(size_t)m] = (uint32_t)(t * R + k % R);
+        } else {
+            slots[(size_t)m] = (uint32_t)(msgs[m].id % (uint64_t)d->cfg.ring);
+        }
         if (msgs[m].vdelay > GSIM_MAX_VDELAY) { h->err = "vdelay above GSIM_MAX_VDELAY"; return GSIM_EINVAL; }
         if (msgs[m].vdelay && h->sh) {
             h->err = "a validation latency (vdelay) needs a single engine (not a shard)";
             return GSIM_ERANGE;
         }
     }
-    std::sort(slots.begin(), slots.end());
-    if (std::adjacent_find(slots.begin(), slots.end()) != slots.end()) {
+    std::vector<uint32_t> sorted(slots);
+    std::sort(sorted.begin(), sorted.end());
+    if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end()) {
         h->err = "two messages of one publish batch share a ring slot";
         return GSIM_EINVAL;
     }
@@ -2564,9 +2760,12 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
     }
     hipError_t e = hipSuccess;
     if (count > d->pub_cap) {
-        if (d->d_pub) { (void)hipStreamSynchronize(h->stream); (void)hipFree(d->d_pub); d->d_pub = nullptr; }
+        (void)hipStreamSynchronize(h->stream);
+        if (d->d_pub) { (void)hipFree(d->d_pub); d->d_pub = nullptr; }
+        if (d->d_pslot) { (void)hipFree(d->d_pslot); d->d_pslot = nullptr; }
         const int32_t cap = std::max(count, 256);
         e = hipMalloc((void**)&d->d_pub, sizeof(gsim_msg) * (size_t)cap);
+        if (e == hipSuccess) e = hipMalloc((void**)&d->d_pslot, sizeof(uint32_t) * (size_t)cap);
         if (e != hipSuccess) { d->pub_cap = 0; return hip_check(h, e, "hipMalloc publish"); }
         d->pub_cap = cap;
     }
@@ -2585,15 +2784,18 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
         d->lat_on = true;
     }
     e = hipMemcpyAsync(d->d_pub, msgs, sizeof(gsim_msg) * (size_t)count, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(d->d_pslot, slots.data(), sizeof(uint32_t) * (size_t)count, hipMemcpyHostToDevice, h->stream);
     if (e != hipSuccess) return hip_check(h, e, "publish upload");
+    for (int32_t m = 0; m < count && d->cfg.topic_slots > 0; ++m) d->tcount[msgs[m].topic]++;
     ProfScope ps(h, GSIM_K_PUBLISH);
     RoundArgs a = make_round_args(h, round);
     const int64_t per_block = 256 * 16;
     const int gx = (int)std::min<int64_t>((h->n + per_block - 1) / per_block, 1024);
     hipLaunchKernelGGL(k_reset_slots, dim3(std::max(gx, 1), count), dim3(256), 0, h->stream, a,
-                       (const gsim_msg*)d->d_pub, count);
+                       (const uint32_t*)d->d_pslot, count);
     hipLaunchKernelGGL(k_publish, dim3((count + 255) / 256), dim3(256), 0, h->stream, a,
-                       (const gsim_msg*)d->d_pub, count);
+                       (const gsim_msg*)d->d_pub, (const uint32_t*)d->d_pslot, count);
     d->next_round = round;
     int rc = hip_check(h, hipGetLastError(), "k_publish");
     // origins that have not joined the topic publish to their fanout

@@ -6,6 +6,7 @@
 // paired, then self-loops and multi-edges are repaired by random double-edge
 // swaps until the graph is simple.
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -97,6 +98,123 @@ extern "C" int gsim_gen_random_regular(int64_t n, int32_t k, uint64_t seed, uint
             col[b + q] = tmp[(size_t)q].first;
             if (outbound) outbound[b + q] = tmp[(size_t)q].second;
         }
+    }
+    return GSIM_OK;
+}
+
+// Chung-Lu power law: expected degree of peer i
+// proportional to (i + i0)^(-1/(exponent-1)), scaled to `mean`, capped at
+// max_degree.  m = round(sum w / 2) endpoint pairs are drawn by inverse CDF;
+// self loops and repeated pairs are dropped; pairs are then accepted in
+// drawing order while both ends are below the cap (the model of
+// gsim.graphs.power_law, with its own seeded stream: the same distribution,
+// not the same graph).  Outbound: the first endpoint drawn dials.
+// Two calls: with col == nullptr only *n_edges (the directed edge count) is
+// computed; then row_ptr (n+1), col and outbound (*n_edges each) are filled.
+extern "C" int gsim_gen_power_law(int64_t n, double mean, double exponent, int32_t max_degree, double i0,
+                                  uint64_t seed, uint32_t* row_ptr, uint32_t* col, uint8_t* outbound,
+                                  int64_t* n_edges)
+{
+    if (n <= 1 || mean <= 0 || exponent <= 2.0 || max_degree <= 0 || i0 < 1.0 || !n_edges) return GSIM_EINVAL;
+    if (n >= (int64_t)UINT32_MAX) return GSIM_ERANGE;
+    // Vose alias table over the capped weights: O(1) per endpoint drawn
+    std::vector<double> w((size_t)n);
+    double sum = 0;
+    const double ex = -1.0 / (exponent - 1.0);
+    for (int64_t i = 0; i < n; ++i) sum += std::pow((double)i + i0, ex);
+    const double scale = mean * (double)n / sum;
+    double acc = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        w[(size_t)i] = std::min(std::pow((double)i + i0, ex) * scale, (double)max_degree);
+        acc += w[(size_t)i];
+    }
+    const int64_t m = (int64_t)std::llround(acc / 2.0);
+    std::vector<double> prob((size_t)n);
+    std::vector<uint32_t> alias((size_t)n);
+    {
+        std::vector<uint32_t> small, large;
+        for (int64_t i = 0; i < n; ++i) {
+            prob[(size_t)i] = w[(size_t)i] * (double)n / acc;
+            (prob[(size_t)i] < 1.0 ? small : large).push_back((uint32_t)i);
+        }
+        while (!small.empty() && !large.empty()) {
+            const uint32_t s0 = small.back(), l0 = large.back();
+            small.pop_back();
+            alias[s0] = l0;
+            prob[l0] = (prob[l0] + prob[s0]) - 1.0;
+            if (prob[l0] < 1.0) { large.pop_back(); small.push_back(l0); }
+        }
+        for (uint32_t x : large) prob[x] = 1.0;
+        for (uint32_t x : small) prob[x] = 1.0;
+    }
+    w.clear();
+    w.shrink_to_fit();
+    SplitMix64 rng{seed};
+    auto draw = [&]() -> uint32_t {
+        const uint64_t r = rng.next();
+        const uint32_t i = (uint32_t)((r >> 32) * (uint64_t)n >> 32);
+        const double u = (double)(r & 0xFFFFFFFFull) * (1.0 / 4294967296.0);
+        return u < prob[i] ? i : alias[i];
+    };
+    struct Pair { uint64_t key; uint32_t idx; uint8_t lo_first; };
+    std::vector<Pair> pairs;
+    pairs.reserve((size_t)m);
+    for (int64_t q = 0; q < m; ++q) {
+        const uint32_t u = draw(), v = draw();
+        if (u == v) continue;
+        pairs.push_back(Pair{ekey(u, v), (uint32_t)pairs.size(), (uint8_t)(u < v ? 1 : 0)});
+    }
+    prob.clear();
+    prob.shrink_to_fit();
+    alias.clear();
+    alias.shrink_to_fit();
+    // first occurrence of every pair, then back in drawing order
+    std::sort(pairs.begin(), pairs.end(), [](const Pair& x, const Pair& y) {
+        return x.key != y.key ? x.key < y.key : x.idx < y.idx;
+    });
+    size_t nu = 0;
+    for (size_t q = 0; q < pairs.size(); ++q)
+        if (q == 0 || pairs[q].key != pairs[q - 1].key) pairs[nu++] = pairs[q];
+    pairs.resize(nu);
+    std::sort(pairs.begin(), pairs.end(), [](const Pair& x, const Pair& y) { return x.idx < y.idx; });
+    std::vector<uint8_t> keep(pairs.size(), 1);
+    std::vector<uint32_t> deg((size_t)n, 0);
+    int64_t E = 0;
+    for (size_t q = 0; q < pairs.size(); ++q) {
+        const uint32_t a = (uint32_t)(pairs[q].key >> 32), b = (uint32_t)pairs[q].key;
+        if (deg[a] >= (uint32_t)max_degree || deg[b] >= (uint32_t)max_degree) { keep[q] = 0; continue; }
+        ++deg[a];
+        ++deg[b];
+        E += 2;
+    }
+    *n_edges = E;
+    if (E >= (int64_t)UINT32_MAX) return GSIM_ERANGE;
+    if (!col) return GSIM_OK;
+    if (!row_ptr) return GSIM_EINVAL;
+    row_ptr[0] = 0;
+    for (int64_t i = 0; i < n; ++i) row_ptr[i + 1] = row_ptr[i] + deg[(size_t)i];
+    std::vector<uint32_t> fill(row_ptr, row_ptr + n);
+    for (size_t q = 0; q < pairs.size(); ++q) {
+        if (!keep[q]) continue;
+        const uint32_t a = (uint32_t)(pairs[q].key >> 32), b = (uint32_t)pairs[q].key;
+        const uint32_t ea = fill[a]++, eb = fill[b]++;
+        col[ea] = b;
+        col[eb] = a;
+        if (outbound) {
+            outbound[ea] = pairs[q].lo_first;           // the lower id dialled
+            outbound[eb] = (uint8_t)(1 - pairs[q].lo_first);
+        }
+    }
+    // sorted rows (outbound follows its edge)
+    std::vector<uint64_t> tmp;
+    for (int64_t i = 0; i < n; ++i) {
+        const uint32_t b0 = row_ptr[i], b1 = row_ptr[i + 1];
+        if (b1 - b0 < 2) continue;
+        if (!outbound) { std::sort(col + b0, col + b1); continue; }
+        tmp.resize(b1 - b0);
+        for (uint32_t e = b0; e < b1; ++e) tmp[e - b0] = ((uint64_t)col[e] << 8) | outbound[e];
+        std::sort(tmp.begin(), tmp.end());
+        for (uint32_t e = b0; e < b1; ++e) { col[e] = (uint32_t)(tmp[e - b0] >> 8); outbound[e] = (uint8_t)tmp[e - b0]; }
     }
     return GSIM_OK;
 }

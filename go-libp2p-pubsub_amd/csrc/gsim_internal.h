@@ -224,6 +224,53 @@ constexpr uint32_t kCreditFirst = 0x80000000u;     // lo-word flag: winner's rec
 constexpr uint32_t kCreditMesh = 0x40000000u;      // lo-word flag: ... and P3 (negative window)
 constexpr uint32_t kPeerMask = 0x3FFFFFFFu;
 
+// The seen-set (a21): one 64-bit cell (encoding above) per
+// (ring slot, peer that can see the slot's message).  A ring shared by every
+// topic (slot = id % ring) and a topic every peer holds: a cell per peer,
+// cbase[m] + p.  Per-topic sub-rings (gsim_msg_config.topic_slots) of a topic
+// only some peers hold — its members, the peers with a slot for it (§2) —
+// keep one cell per member, in peer order: cbase[m] + the member's index,
+// found from a word of the topic's member bitmap and the members before it.
+struct Cells {
+    uint64_t* cell = nullptr;
+    const uint64_t* cbase = nullptr;   // [ring] first cell of each slot
+    const uint64_t* mbits = nullptr;   // [T][nw] member bits of each topic (sparse topics)
+    const uint32_t* mpre = nullptr;    // [T][nw] members in the topic's earlier words
+    int64_t nw = 0;                    // words per topic, ceil(N / 64)
+    uint64_t sparse = 0;               // topics whose slots hold member-compacted cells
+    // word w of topic t: its member bits and the cell offset of its first member
+    __device__ __forceinline__ void word(int32_t t, int64_t w, uint64_t& bits, int64_t& pre) const
+    {
+        if ((sparse >> t) & 1ull) {
+            const int64_t i = (int64_t)t * nw + w;
+            bits = mbits[i];
+            pre = mpre[i];
+        } else {
+            bits = ~0ull;
+            pre = w * 64;
+        }
+    }
+    // cell index of peer p in slot m (topic t) whose cells start at base; -1: p has none
+    __device__ __forceinline__ int64_t at(int64_t base, int32_t t, uint32_t p) const
+    {
+        uint64_t b;
+        int64_t pre;
+        word(t, (int64_t)(p >> 6), b, pre);
+        const uint64_t bit = 1ull << (p & 63);
+        if (!(b & bit)) return -1;
+        return base + pre + __popcll(b & (bit - 1));
+    }
+    __device__ __forceinline__ int64_t idx(uint32_t m, int32_t t, uint32_t p) const
+    {
+        return at((int64_t)cbase[m], t, p);
+    }
+    __device__ __forceinline__ uint64_t get(uint32_t m, int32_t t, uint32_t p) const
+    {
+        const int64_t i = idx(m, t, p);
+        return i < 0 ? kUnseen64 : cell[i];
+    }
+};
+
 // Trace capture (gsim_trace_config, include/gsim.h): the events of the
 // routers [lo, hi) are appended to a device buffer.  A message copy is
 // recorded unclassified (kTraceCopy, msg_id = round << 32 | slot) and resolved
@@ -403,7 +450,7 @@ struct GossipView {
 bool deliver_gossip_view(gsim_handle* h, GossipView* v);   // false before gsim_msgs_init
 // What the wire encoder reads of the message state (wire.hip)
 struct WireView {
-    const uint64_t* cell;      // [ring][N]
+    gsim::Cells cells;         // the seen-set
     const uint32_t *mtopic, *morigin;
     const uint8_t* minv;
     const uint64_t* mid;       // [ring] gsim_msg ids
@@ -421,7 +468,7 @@ int deliver_check_errors(gsim_handle* h);             // queue overflow / early 
 int handle_control(gsim_handle* h, int32_t round, int64_t now);   // heartbeat.hip: k_handle_control
 // trace.hip: resolve the recorded message copies (seen-set cells, slot tables)
 struct TraceView {
-    const uint64_t* cell;
+    gsim::Cells cells;
     const uint32_t* mtopic;
     const uint8_t* minv;
     const uint64_t* mid;

@@ -30,8 +30,9 @@ struct Extra {
     // of <= 16 connections, then <= 32, then the rest (nullptr: one class)
     uint32_t* d_rows = nullptr;
     int64_t n16 = 0, n32 = 0, n64 = 0;
-    // hub observers after them: rows of 65..256, then 257..1024 connections
-    int64_t nh256 = 0, nh1024 = 0;
+    // hub observers after them: rows of 65..256, 257..1024, then 1025..4096
+    // connections (a block of 1024 threads holding 4 row positions each)
+    int64_t nh256 = 0, nh1024 = 0, nh4096 = 0;
     // peer exchange (gsim_gossipsub_params.do_px): topics with PX PRUNEs per
     // observer, connection attempts per edge, the GRAFT RPCs that turned PX off
     uint64_t* d_pxo = nullptr;
@@ -391,15 +392,19 @@ __device__ bool gossip_targets(const HbArgs& a, bool cand, bool tpeer, uint32_t 
 // ---------------------------------------------------------------------------
 // The lane group that holds one observer's row.  The heartbeat body
 // (hb_observer) is written once against this interface:
-//   WaveGroup<W>  W lanes of a wavefront (rows of at most 16 / 32 / 64
-//                 connections; 4 / 2 / 1 observers per wavefront)
-//   BlockGroup<B> a whole B-thread block (hub rows of 65 .. B connections):
-//                 counts and keyed minima are block reductions through LDS,
-//                 a lane's neighbours are read from LDS instead of shuffles.
-// Position q of a group is the row position (tie breaks, Philox keys).
+//   WaveGroup<W>     W lanes of a wavefront (rows of at most 16 / 32 / 64
+//                    connections; 4 / 2 / 1 observers per wavefront)
+//   BlockGroup<B, V> a whole B-thread block holding V row positions per
+//                    thread (hub rows of 65 .. B·V connections): counts and
+//                    keyed minima are block reductions through LDS, a
+//                    position's neighbours are read from LDS, not shuffles.
+// Position q of a group is the row position (tie breaks, Philox keys); a
+// thread holds positions pos(0) .. pos(V-1), and every per-position value
+// crosses the interface as an array of V.
 
 template <int W>
 struct WaveGroup {
+    static constexpr int V = 1;
     static constexpr int LP = 64 / W;     // topics per lane of the mcache-put cache
     int lane, grp, gl, base;
     uint64_t gm;
@@ -409,18 +414,19 @@ struct WaveGroup {
           gm(W == 64 ? ~0ull : (((1ull << W) - 1) << ((lane_ / W) * W)))
     {
     }
-    __device__ int pos() const { return gl; }
+    __device__ int pos(int = 0) const { return gl; }
     __device__ int span() const { return W; }
-    __device__ int count(bool p) const { return __popcll(__ballot(p) & gm); }
-    __device__ bool any(bool p) const { return (__ballot(p) & gm) != 0; }
-    __device__ bool select(const HbArgs& a, bool cand, int count, uint32_t obs, int32_t t, uint32_t purpose,
-                           uint32_t col)
+    __device__ int count(const bool* p) const { return __popcll(__ballot(p[0]) & gm); }
+    __device__ bool any(const bool* p) const { return (__ballot(p[0]) & gm) != 0; }
+    __device__ void select(const HbArgs& a, const bool* cand, int count, uint32_t obs, int32_t t, uint32_t purpose,
+                           const uint32_t* col, bool* out)
     {
-        return select_smallest<W>(a, cand, count, obs, t, purpose, col, (uint32_t)gl, gm, grp);
+        out[0] = select_smallest<W>(a, cand[0], count, obs, t, purpose, col[0], (uint32_t)gl, gm, grp);
     }
-    __device__ bool gossip(const HbArgs& a, bool cand, bool tpeer, uint32_t obs, int32_t t, uint32_t col)
+    __device__ void gossip(const HbArgs& a, const bool* cand, const bool* tpeer, uint32_t obs, int32_t t,
+                           const uint32_t* col, bool* out)
     {
-        return gossip_targets<W>(a, cand, tpeer, obs, t, col, (uint32_t)gl, gm, grp);
+        out[0] = gossip_targets<W>(a, cand[0], tpeer[0], obs, t, col[0], (uint32_t)gl, gm, grp);
     }
     // a lane's value at position q of the group (every lane asks for the same q)
     template <typename T>
@@ -435,13 +441,13 @@ struct WaveGroup {
         __device__ bool operator[](int q) const { return (m >> (base + q)) & 1ull; }
     };
     template <int SLOT, typename T>
-    __device__ View<T> view(T v) const { return View<T>{v, base}; }
+    __device__ View<T> view(const T* v) const { return View<T>{v[0], base}; }
     template <int SLOT>
-    __device__ BoolView view_b(bool v) const { return BoolView{__ballot(v), base}; }
+    __device__ BoolView view_b(const bool* v) const { return BoolView{__ballot(v[0]), base}; }
     // the value at the lowest position where p holds (p must hold somewhere)
-    __device__ double at_lowest(bool p, double v) const
+    __device__ double at_lowest(const bool* p, const double* v) const
     {
-        return __shfl(v, (int)__ffsll((long long)(__ballot(p) & gm)) - 1, 64);
+        return __shfl(v[0], (int)__ffsll((long long)(__ballot(p[0]) & gm)) - 1, 64);
     }
     // newest mcache put of topic t by observer obs (GetGossipIDs non-empty test):
     // group lane gl caches topics gl, gl + W, ... (T <= 64)
@@ -449,7 +455,7 @@ struct WaveGroup {
     __device__ uint64_t topic_mask(bool p) const { return __ballot(p) & gm; }
     // bit q = p at the group's row position q (the delivery's mesh masks)
     static constexpr bool kRowMask = true;
-    __device__ uint64_t row_mask(bool p) const { return (__ballot(p) & gm) >> base; }
+    __device__ uint64_t row_mask(const bool* p) const { return (__ballot(p[0]) & gm) >> base; }
     __device__ void load_lastput(const HbArgs& a, int64_t obs, uint64_t subi, bool ovalid)
     {
 #pragma unroll
@@ -468,22 +474,24 @@ struct WaveGroup {
     }
 };
 
-template <int B>
+template <int B, int VV = 1>
 struct BlockGroup {
+    static constexpr int V = VV;
     static constexpr int NW = B / 64;
+    static constexpr int P = B * V;       // positions
     struct Shared {
         unsigned long long red[2][NW];     // reductions (alternating: one barrier each)
-        double d0[B];
-        uint64_t u0[B], u1[B];
-        int32_t i0[B];
-        uint8_t b0[B], b1[B];
+        double d0[P];
+        uint64_t u0[P], u1[P];
+        int32_t i0[P];
+        uint8_t b0[P], b1[P];
     };
     Shared* sh;
     int tid, lane, wid, phase;
     __device__ BlockGroup(Shared* s) : sh(s), tid((int)threadIdx.x), lane((int)threadIdx.x & 63),
                                        wid((int)threadIdx.x >> 6), phase(0) {}
-    __device__ int pos() const { return tid; }
-    __device__ int span() const { return B; }
+    __device__ int pos(int v = 0) const { return v * B + tid; }
+    __device__ int span() const { return P; }
     __device__ unsigned long long reduce(unsigned long long v, int op)   // 0 sum, 1 min, 2 max
     {
         for (int o = 32; o; o >>= 1) {
@@ -501,62 +509,107 @@ struct BlockGroup {
         }
         return acc;
     }
-    __device__ int count(bool p) { return (int)reduce((unsigned long long)__popcll(__ballot(p)) * (lane == 0), 0); }
-    __device__ bool any(bool p) { return count(p) != 0; }
+    __device__ int count(const bool* p)
+    {
+        unsigned long long c = 0;
+#pragma unroll
+        for (int v = 0; v < V; ++v) c += (unsigned long long)__popcll(__ballot(p[v]));
+        return (int)reduce(c * (lane == 0), 0);
+    }
+    __device__ bool any(const bool* p) { return count(p) != 0; }
     __device__ uint64_t min_u64(uint64_t v) { return reduce(v, 1); }
     __device__ uint64_t max_u64(uint64_t v) { return reduce(v, 2); }
     // select_smallest (above) over the block: the count smallest (key, position)
-    __device__ bool select(const HbArgs& a, bool cand, int count, uint32_t obs, int32_t t, uint32_t purpose,
-                           uint32_t col)
+    __device__ void select(const HbArgs& a, const bool* cand, int count, uint32_t obs, int32_t t, uint32_t purpose,
+                           const uint32_t* col, bool* sel)
     {
         const int n = this->count(cand);
-        if (n == 0) return false;
-        if (count <= 0 || n <= count) return cand;
-        const uint32_t hi = cand ? hb_key_hi(a, obs, t, purpose, col, (uint32_t)tid) : 0xFFFFFFFFu;
-        const uint64_t key = ((uint64_t)hi << 32) | (uint32_t)tid;
+#pragma unroll
+        for (int v = 0; v < V; ++v) sel[v] = false;
+        if (n == 0) return;
+        if (count <= 0 || n <= count) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) sel[v] = cand[v];
+            return;
+        }
         const uint32_t tau = (uint32_t)((float)count / (float)n * 4294967040.0f);
-        bool sel = cand && hi < tau;
+        uint64_t key[V];
+        bool rest[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const uint32_t hi = cand[v] ? hb_key_hi(a, obs, t, purpose, col[v], (uint32_t)pos(v)) : 0xFFFFFFFFu;
+            key[v] = ((uint64_t)hi << 32) | (uint32_t)pos(v);
+            sel[v] = cand[v] && hi < tau;
+        }
         int c = this->count(sel);
         while (c > count) {                 // drop the largest (key, position) among the selected
-            const uint64_t mx = max_u64(sel ? key : 0ull);
-            if (sel && key == mx) sel = false;
+            uint64_t mine = 0;
+#pragma unroll
+            for (int v = 0; v < V; ++v) if (sel[v] && key[v] > mine) mine = key[v];
+            const uint64_t mx = max_u64(mine);
+#pragma unroll
+            for (int v = 0; v < V; ++v) if (sel[v] && key[v] == mx) sel[v] = false;
             --c;
         }
-        bool rest = cand && !sel;
+#pragma unroll
+        for (int v = 0; v < V; ++v) rest[v] = cand[v] && !sel[v];
         while (c < count) {                 // add the smallest among the others
-            const uint64_t mn = min_u64(rest ? key : ~0ull);
-            if (rest && key == mn) { sel = true; rest = false; }
+            uint64_t mine = ~0ull;
+#pragma unroll
+            for (int v = 0; v < V; ++v) if (rest[v] && key[v] < mine) mine = key[v];
+            const uint64_t mn = min_u64(mine);
+#pragma unroll
+            for (int v = 0; v < V; ++v) if (rest[v] && key[v] == mn) { sel[v] = true; rest[v] = false; }
             ++c;
         }
-        return sel;
     }
     // gossip_targets (above) over the block
-    __device__ bool gossip(const HbArgs& a, bool cand, bool tpeer, uint32_t obs, int32_t t, uint32_t col)
+    __device__ void gossip(const HbArgs& a, const bool* cand, const bool* tpeer, uint32_t obs, int32_t t,
+                           const uint32_t* col, bool* sel)
     {
         const int c = count(cand);
-        bool dup = false;
-        if (c < a.Dlo) dup = select(a, tpeer, a.Dlo - c, obs, t, P_GOSSIP_FILL, col);
+        bool dup[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) { dup[v] = false; sel[v] = false; }
+        if (c < a.Dlo) select(a, tpeer, a.Dlo - c, obs, t, P_GOSSIP_FILL, col, dup);
         const int n = c + count(dup);
-        if (n == 0) return false;
+        if (n == 0) return;
         int target = a.dlazy;
         const int factor = (int)(a.gossip_factor * (double)n);
         if (factor > target) target = factor;
-        if (target >= n) return cand || dup;
-        if (!any(dup)) return select(a, cand, target, obs, t, P_GOSSIP, col);
-        const uint32_t h1 = cand ? hb_key_hi(a, obs, t, P_GOSSIP, col, (uint32_t)tid) : 0xFFFFFFFFu;
-        const uint32_t h2 = dup ? hb_key_hi(a, obs, t, P_GOSSIP_DUP, col, (uint32_t)tid) : 0xFFFFFFFFu;
-        bool has1 = cand, has2 = dup, sel = false;
-        for (int q = 0; q < target; ++q) {
-            const bool use1 = has1 && (!has2 || h1 <= h2);
-            const uint32_t mine = use1 ? h1 : (has2 ? h2 : 0xFFFFFFFFu);
-            const uint64_t k = (has1 || has2) ? (((uint64_t)mine << 32) | (uint32_t)tid) : ~0ull;
-            const uint64_t mn = min_u64(k);
-            if ((has1 || has2) && k == mn) {
-                if (use1) has1 = false; else has2 = false;
-                sel = true;
-            }
+        if (target >= n) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) sel[v] = cand[v] || dup[v];
+            return;
         }
-        return sel;
+        if (!any(dup)) { select(a, cand, target, obs, t, P_GOSSIP, col, sel); return; }
+        uint32_t h1[V], h2[V];
+        bool has1[V], has2[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            h1[v] = cand[v] ? hb_key_hi(a, obs, t, P_GOSSIP, col[v], (uint32_t)pos(v)) : 0xFFFFFFFFu;
+            h2[v] = dup[v] ? hb_key_hi(a, obs, t, P_GOSSIP_DUP, col[v], (uint32_t)pos(v)) : 0xFFFFFFFFu;
+            has1[v] = cand[v];
+            has2[v] = dup[v];
+        }
+        for (int q = 0; q < target; ++q) {
+            uint64_t k[V], mine = ~0ull;
+            bool use1[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                use1[v] = has1[v] && (!has2[v] || h1[v] <= h2[v]);
+                const uint32_t hv = use1[v] ? h1[v] : (has2[v] ? h2[v] : 0xFFFFFFFFu);
+                k[v] = (has1[v] || has2[v]) ? (((uint64_t)hv << 32) | (uint32_t)pos(v)) : ~0ull;
+                if (k[v] < mine) mine = k[v];
+            }
+            const uint64_t mn = min_u64(mine);
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                if ((has1[v] || has2[v]) && k[v] == mn) {
+                    if (use1[v]) has1[v] = false; else has2[v] = false;
+                    sel[v] = true;
+                }
+        }
     }
     template <typename T>
     struct View {
@@ -564,36 +617,42 @@ struct BlockGroup {
         __device__ T operator[](int q) const { return p[q]; }
     };
     template <int SLOT, typename T>
-    __device__ View<T> view(T v)
+    __device__ View<T> view(const T* v)
     {
         T* buf;
         if constexpr (sizeof(T) == 8 && (T)0.5 != (T)0) buf = reinterpret_cast<T*>(sh->d0);     // double
         else if constexpr (sizeof(T) == 8) buf = reinterpret_cast<T*>(SLOT ? sh->u1 : sh->u0);
         else buf = reinterpret_cast<T*>(sh->i0);
         __syncthreads();                    // earlier readers of the buffer are done
-        buf[tid] = v;
+#pragma unroll
+        for (int x = 0; x < V; ++x) buf[pos(x)] = v[x];
         __syncthreads();
         return View<T>{buf};
     }
     template <int SLOT>
-    __device__ View<uint8_t> view_b(bool v)
+    __device__ View<uint8_t> view_b(const bool* v)
     {
         uint8_t* buf = SLOT ? sh->b1 : sh->b0;
         __syncthreads();
-        buf[tid] = v ? 1 : 0;
+#pragma unroll
+        for (int x = 0; x < V; ++x) buf[pos(x)] = v[x] ? 1 : 0;
         __syncthreads();
         return View<uint8_t>{buf};
     }
-    __device__ double at_lowest(bool p, double v)
+    __device__ double at_lowest(const bool* p, const double* v)
     {
-        const uint64_t q = min_u64(p ? (uint64_t)tid : ~0ull);
+        uint64_t mine = ~0ull;
+#pragma unroll
+        for (int x = V - 1; x >= 0; --x) if (p[x]) mine = (uint64_t)pos(x);
+        const uint64_t q = min_u64(mine);
         __syncthreads();
-        if ((uint64_t)tid == q) sh->d0[0] = v;
+#pragma unroll
+        for (int x = 0; x < V; ++x) if ((uint64_t)pos(x) == q) sh->d0[0] = v[x];
         __syncthreads();
         return sh->d0[0];
     }
     static constexpr bool kRowMask = false;    // hub rows: delivery walks the whole row
-    __device__ uint64_t row_mask(bool) const { return 0; }
+    __device__ uint64_t row_mask(const bool*) const { return 0; }
     __device__ uint64_t topic_mask(bool p)
     {
         const uint64_t m = __ballot(p);
@@ -616,41 +675,65 @@ struct BlockGroup {
 template <class Grp>
 __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs, bool ovalid)
 {
-        const int gl = g.pos();
+        constexpr int V = Grp::V;
         const uint32_t b = ovalid ? a.row_ptr[obs] : 0u;
         const int deg = ovalid ? (int)(a.row_ptr[obs + 1] - b) : 0;
-        const bool valid = gl < deg;
-        const uint32_t e = b + (uint32_t)gl;
-        const uint32_t col = valid ? a.col[e] : 0u;
-        const uint32_t rv = valid ? a.rev[e] : 0u;           // this observer's record of col
-        const uint32_t gobs = ovalid ? glob(a, (uint32_t)obs) : 0u, gcol = valid ? glob(a, col) : 0u;
-        const uint8_t est = valid ? a.estate[rv] : 0;
-        const bool tracked = est & GSIM_ES_TRACKED;
-        const bool conn = valid && (a.rstate[e] & GSIM_ES_CONNECTED);
-        const bool outb = valid && a.outbound[e];
-        const bool dir = valid && a.direct[e];          // direct peers are never grafted or gossiped to
-        const double S = valid ? a.score[rv] : 0.0;
-        const uint64_t subj = valid ? a.sub[col] : 0ull;
+        const uint32_t gobs = ovalid ? glob(a, (uint32_t)obs) : 0u;
         const uint64_t subi = ovalid ? a.sub[obs] : 0ull;
         // topic slots: router state is the observer's row (mi), its records of
-        // the neighbours sit in their rows (mj, per lane)
+        // the neighbours sit in their rows (mj, per position)
         const uint64_t mi = ovalid ? smask_of(a.smask, (uint32_t)obs) : 0ull;
-        const uint64_t mj = valid ? smask_of(a.smask, col) : 0ull;
-        // live score for emitGossip: the snapshot until this heartbeat's
-        // Graft/Prune touches one of the lane's records
-        double S_live = S;
-        bool dirty = false;
+        // per position v of this thread: row position g.pos(v)
+        int gl[V];
+        bool valid[V], tracked[V], conn[V], outb[V], dir[V], dirty[V];
+        uint32_t e[V], col[V], rv[V], gcol[V];
+        double S[V], S_live[V];
+        uint64_t subj[V], mj[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            gl[v] = g.pos(v);
+            valid[v] = gl[v] < deg;
+            e[v] = b + (uint32_t)gl[v];
+            col[v] = valid[v] ? a.col[e[v]] : 0u;
+            rv[v] = valid[v] ? a.rev[e[v]] : 0u;           // this observer's record of col
+            gcol[v] = valid[v] ? glob(a, col[v]) : 0u;
+            const uint8_t est = valid[v] ? a.estate[rv[v]] : 0;
+            tracked[v] = est & GSIM_ES_TRACKED;
+            conn[v] = valid[v] && (a.rstate[e[v]] & GSIM_ES_CONNECTED);
+            outb[v] = valid[v] && a.outbound[e[v]];
+            dir[v] = valid[v] && a.direct[e[v]];          // direct peers are never grafted or gossiped to
+            S[v] = valid[v] ? a.score[rv[v]] : 0.0;
+            subj[v] = valid[v] ? a.sub[col[v]] : 0ull;
+            mj[v] = valid[v] ? smask_of(a.smask, col[v]) : 0ull;
+            // live score for emitGossip: the snapshot until this heartbeat's
+            // Graft/Prune touches one of the position's records
+            S_live[v] = S[v];
+            dirty[v] = false;
+            if (a.gossip && valid[v]) a.gstate[e[v]] = S[v] >= a.gossip_thr ? 1 : 0;
+        }
         g.load_lastput(a, obs, subi, ovalid);
         uint64_t pxt = 0;                               // topics with a PRUNE carrying PX
-        if (a.gossip && valid) a.gstate[e] = S >= a.gossip_thr ? 1 : 0;
+        auto rescore = [&]() {                          // live scores of the dirty positions
+            if (g.any(dirty)) {
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    if (dirty[v]) S_live[v] = score_of_record(a, rv[v], col[v]);
+                    dirty[v] = false;
+                }
+            }
+        };
 
         // clearBackoff every 15 ticks (gossipsub.go:1627-1646)
-        if (a.tick % 15 == 0 && valid) {
-            for (int32_t t = 0; t < a.T; ++t) {
-                if (!slot_has(mi, t)) continue;
-                const int64_t i = slot_idx(mi, t, a.E, e);
-                const int64_t bo = a.backoff[i];
-                if (bo != 0 && bo + kBackoffSlack < a.now) a.backoff[i] = 0;
+        if (a.tick % 15 == 0) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                if (!valid[v]) continue;
+                for (int32_t t = 0; t < a.T; ++t) {
+                    if (!slot_has(mi, t)) continue;
+                    const int64_t i = slot_idx(mi, t, a.E, e[v]);
+                    const int64_t bo = a.backoff[i];
+                    if (bo != 0 && bo + kBackoffSlack < a.now) a.backoff[i] = 0;
+                }
             }
         }
 
@@ -660,11 +743,13 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
           // joined topic are skipped (a group-uniform test, like every
           // per-topic branch below)
           if (!((subi >> t0) & ((1ull << kFlagChunk) - 1))) continue;
-          uint8_t flc[kFlagChunk];
+          uint8_t flc[kFlagChunk][V];
 #pragma unroll
           for (int j = 0; j < kFlagChunk; ++j) {
               const int32_t t = t0 + j;
-              flc[j] = (t < a.T && valid && ((subi >> t) & 1ull)) ? a.mflags[slot_idx(mi, t, a.E, e)] : 0;
+#pragma unroll
+              for (int v = 0; v < V; ++v)
+                  flc[j][v] = (t < a.T && valid[v] && ((subi >> t) & 1ull)) ? a.mflags[slot_idx(mi, t, a.E, e[v])] : 0;
           }
           for (int j = 0; j < kFlagChunk; ++j) {
             const int32_t t = t0 + j;
@@ -674,61 +759,81 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
             const bool scored = tp->scored != 0;
             const double thr = tp->mesh_message_deliveries_threshold;
             const double mcap = tp->mesh_message_deliveries_cap;
-            const int64_t i = slot_idx(mi, t, a.E, e);
-            ScoreFlags sf;
-            sf.at(mj, t, a.E, rv);
-            uint8_t fl = flc[j];
-            const uint8_t fl0 = fl;
+            int64_t i[V];
+            ScoreFlags sf[V];
+            uint8_t fl[V], fl0[V], ctl[V];
             // backoff is only consulted when a graft selection or a prune
             // happens, so it is loaded lazily (steady-state ticks read none)
-            int64_t bo = 0;
-            bool have_bo = false, bo_dirty = false;
-            auto need_bo = [&]() {
-                if (!have_bo) {
-                    bo = valid ? a.backoff[i] : 0;
-                    have_bo = true;
+            int64_t bo[V];
+            bool have_bo[V], bo_dirty[V], tpeer[V], m[V], cand[V], sel[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                i[v] = slot_idx(mi, t, a.E, e[v]);
+                sf[v].at(mj[v], t, a.E, rv[v]);
+                fl[v] = flc[j][v];
+                fl0[v] = fl[v];
+                bo[v] = 0;
+                have_bo[v] = bo_dirty[v] = false;
+                tpeer[v] = valid[v] && conn[v] && ((subj[v] >> t) & 1ull);
+                m[v] = valid[v] && (fl[v] & GSIM_TF_MESH);
+                ctl[v] = 0;
+            }
+            auto need_bo = [&](int v) {
+                if (!have_bo[v]) {
+                    bo[v] = valid[v] ? a.backoff[i[v]] : 0;
+                    have_bo[v] = true;
                 }
             };
-            const bool tpeer = valid && conn && ((subj >> t) & 1ull);
-            bool m = valid && (fl & GSIM_TF_MESH);
-            uint8_t ctl = 0;
-
-            auto prune = [&]() {
-                if (a.tr.on((uint32_t)obs)) a.tr.push(a.now, 0, (uint32_t)obs, col, t, GSIM_TRACE_PRUNE, 0);
-                stats_prune(a, tracked, scored, thr, mcap, sf);
-                dirty |= tracked && scored;
-                fl &= (uint8_t)~GSIM_TF_MESH;
-                m = false;
-                need_bo();
+            auto prune = [&](int v) {
+                if (a.tr.on((uint32_t)obs)) a.tr.push(a.now, 0, (uint32_t)obs, col[v], t, GSIM_TRACE_PRUNE, 0);
+                stats_prune(a, tracked[v], scored, thr, mcap, sf[v]);
+                dirty[v] |= tracked[v] && scored;
+                fl[v] &= (uint8_t)~GSIM_TF_MESH;
+                m[v] = false;
+                need_bo(v);
                 const int64_t ex = a.now + a.prune_backoff;
-                if (bo < ex) { bo = ex; bo_dirty = true; }
-                ctl |= GSIM_CTL_PRUNE;
+                if (bo[v] < ex) { bo[v] = ex; bo_dirty[v] = true; }
+                ctl[v] |= GSIM_CTL_PRUNE;
             };
-            auto graft = [&]() {
-                if (a.tr.on((uint32_t)obs)) a.tr.push(a.now, 0, (uint32_t)obs, col, t, GSIM_TRACE_GRAFT, 0);
-                stats_graft(a, tracked, scored, sf);
-                dirty |= tracked && scored;
-                fl |= GSIM_TF_MESH;
-                m = true;
-                ctl |= GSIM_CTL_GRAFT;
+            auto graft = [&](int v) {
+                if (a.tr.on((uint32_t)obs)) a.tr.push(a.now, 0, (uint32_t)obs, col[v], t, GSIM_TRACE_GRAFT, 0);
+                stats_graft(a, tracked[v], scored, sf[v]);
+                dirty[v] |= tracked[v] && scored;
+                fl[v] |= GSIM_TF_MESH;
+                m[v] = true;
+                ctl[v] |= GSIM_CTL_GRAFT;
             };
 
             // drop all peers with negative score (1403-1410)
-            if (m && S < 0) prune();
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                if (m[v] && S[v] < 0) prune(v);
 
             // too few peers: graft up to D (1412-1427)
             int l = g.count(m);
             if (l < a.Dlo) {
-                need_bo();
-                const bool cand = tpeer && !m && bo == 0 && !dir && S >= 0;
-                if (g.select(a, cand, a.D - l, gobs, t, P_GRAFT_DLO, gcol)) graft();
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    need_bo(v);
+                    cand[v] = tpeer[v] && !m[v] && bo[v] == 0 && !dir[v] && S[v] >= 0;
+                }
+                g.select(a, cand, a.D - l, gobs, t, P_GRAFT_DLO, gcol, sel);
+#pragma unroll
+                for (int v = 0; v < V; ++v)
+                    if (sel[v]) graft(v);
             }
 
             // too many peers: keep Dscore best + random, Dout outbound (1429-1490)
             l = g.count(m);
             if (l > a.Dhi) {
-                const uint64_t k1 = m ? hb_key(a, gobs, t, P_PRUNE_SHUF1, gcol, (uint32_t)gl) : ~0ull;
-                int rank1 = 0;
+                uint64_t k1[V], k2[V];
+                int rank1[V], below[V], p[V];
+                bool tail[V];
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    k1[v] = m[v] ? hb_key(a, gobs, t, P_PRUNE_SHUF1, gcol[v], (uint32_t)gl[v]) : ~0ull;
+                    rank1[v] = 0;
+                }
                 {
                     const auto vm = g.template view_b<0>(m);
                     const auto vs = g.template view<0>(S);
@@ -736,96 +841,152 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
                     for (int q = 0; q < g.span(); ++q) {
                         const double sq = vs[q];
                         const uint64_t kq = vk[q];
-                        if (vm[q] && (sq > S || (sq == S && kq < k1))) ++rank1;
+                        const bool mq = vm[q];
+#pragma unroll
+                        for (int v = 0; v < V; ++v)
+                            if (mq && (sq > S[v] || (sq == S[v] && kq < k1[v]))) ++rank1[v];
                     }
                 }
                 const int ds = a.Dscore < l ? a.Dscore : l;
-                const bool tail = m && rank1 >= ds;
-                const uint64_t k2 = tail ? hb_key(a, gobs, t, P_PRUNE_SHUF2, gcol, (uint32_t)gl) : ~0ull;
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    tail[v] = m[v] && rank1[v] >= ds;
+                    k2[v] = tail[v] ? hb_key(a, gobs, t, P_PRUNE_SHUF2, gcol[v], (uint32_t)gl[v]) : ~0ull;
+                    below[v] = 0;
+                }
                 // every lane takes part in the shuffles (a shuffle inside a
                 // divergent branch would read inactive lanes)
-                int below = 0;
                 {
                     const auto vk2 = g.template view<1>(k2);
-                    for (int q = 0; q < g.span(); ++q)
-                        if (vk2[q] < k2) ++below;   // non-tail lanes hold ~0 and never count
+                    for (int q = 0; q < g.span(); ++q) {
+                        const uint64_t kq = vk2[q];
+#pragma unroll
+                        for (int v = 0; v < V; ++v)
+                            if (kq < k2[v]) ++below[v];   // non-tail positions hold ~0 and never count
+                    }
                 }
-                const int p = tail ? ds + below : rank1;
                 // Keep plst[:D] after Go's Dout rotation (1457-1485), computed
-                // data-parallel from each lane's position p in plst:
+                // data-parallel from each position's place p in plst:
                 //  pass 1 moves every outbound peer at positions 1..D-1 to the
                 //  front, leaving the other first-D peers ("rest") behind them
                 //  in order; pass 2 rotates the first j outbound peers beyond D
                 //  to the front, pushing the last j "rest" peers out of plst[:D].
-                const bool inD = m && p < a.D;
-                const int obD = g.count(inD && outb);
-                bool keep = inD;
+                bool inD[V], keep[V], obc[V];
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    p[v] = tail[v] ? ds + below[v] : rank1[v];
+                    inD[v] = m[v] && p[v] < a.D;
+                    keep[v] = inD[v];
+                    obc[v] = inD[v] && outb[v];
+                }
+                const int obD = g.count(obc);
                 if (obD < a.Dout) {
-                    const bool rest = inD && !(outb && p >= 1);
-                    const bool cb = m && p >= a.D && outb;
+                    bool rest[V], cb[V];
+                    int rb[V], rr[V];
+#pragma unroll
+                    for (int v = 0; v < V; ++v) {
+                        rest[v] = inD[v] && !(outb[v] && p[v] >= 1);
+                        cb[v] = m[v] && p[v] >= a.D && outb[v];
+                        rb[v] = rr[v] = 0;
+                    }
                     const int nb = g.count(cb);
-                    int rb = 0, rr = 0;
                     {
                         const auto vrest = g.template view_b<0>(rest);
                         const auto vcb = g.template view_b<1>(cb);
-                        const auto vp = g.template view<0>((int32_t)p);
+                        const auto vp = g.template view<0>(p);
                         for (int q = 0; q < g.span(); ++q) {
                             const int pq = vp[q];
-                            if (vcb[q] && pq < p) ++rb;
-                            if (vrest[q] && pq > p) ++rr;
+                            const bool cq = vcb[q], rq = vrest[q];
+#pragma unroll
+                            for (int v = 0; v < V; ++v) {
+                                if (cq && pq < p[v]) ++rb[v];
+                                if (rq && pq > p[v]) ++rr[v];
+                            }
                         }
                     }
-                    const int j = a.Dout - obD < nb ? a.Dout - obD : nb;
-                    keep = (inD && !(rest && rr < j)) || (cb && rb < j);
+                    const int jj = a.Dout - obD < nb ? a.Dout - obD : nb;
+#pragma unroll
+                    for (int v = 0; v < V; ++v) keep[v] = (inD[v] && !(rest[v] && rr[v] < jj)) || (cb[v] && rb[v] < jj);
                 }
-                if (m && !keep) {
-                    prune();
-                    if (a.do_px) ctl |= GSIM_CTL_PX;     // makePrune(p, topic, doPX && !noPX[p]) (1690)
-                }
+#pragma unroll
+                for (int v = 0; v < V; ++v)
+                    if (m[v] && !keep[v]) {
+                        prune(v);
+                        if (a.do_px) ctl[v] |= GSIM_CTL_PX;     // makePrune(p, topic, doPX && !noPX[p]) (1690)
+                    }
             }
 
             // enough outbound peers? (1492-1518)
             l = g.count(m);
             if (l >= a.Dlo) {
-                const int ob = g.count(m && outb);
+                bool mo[V];
+#pragma unroll
+                for (int v = 0; v < V; ++v) mo[v] = m[v] && outb[v];
+                const int ob = g.count(mo);
                 if (ob < a.Dout) {
-                    need_bo();
-                    const bool cand = tpeer && !m && bo == 0 && !dir && outb && S >= 0;
-                    if (g.select(a, cand, a.Dout - ob, gobs, t, P_GRAFT_DOUT, gcol)) graft();
+#pragma unroll
+                    for (int v = 0; v < V; ++v) {
+                        need_bo(v);
+                        cand[v] = tpeer[v] && !m[v] && bo[v] == 0 && !dir[v] && outb[v] && S[v] >= 0;
+                    }
+                    g.select(a, cand, a.Dout - ob, gobs, t, P_GRAFT_DOUT, gcol, sel);
+#pragma unroll
+                    for (int v = 0; v < V; ++v)
+                        if (sel[v]) graft(v);
                 }
             }
 
             // opportunistic grafting (1520-1552)
             l = g.count(m);
             if (a.opp_ticks && a.tick % a.opp_ticks == 0 && l > 1) {
-                int rank = 0;
+                int rank[V];
+#pragma unroll
+                for (int v = 0; v < V; ++v) rank[v] = 0;
                 {
                     const auto vm = g.template view_b<0>(m);
                     const auto vs = g.template view<0>(S);
                     for (int q = 0; q < g.span(); ++q) {
                         const double sq = vs[q];
-                        if (vm[q] && (sq < S || (sq == S && q < gl))) ++rank;
+                        const bool mq = vm[q];
+#pragma unroll
+                        for (int v = 0; v < V; ++v)
+                            if (mq && (sq < S[v] || (sq == S[v] && q < gl[v]))) ++rank[v];
                     }
                 }
-                const double median = g.at_lowest(m && rank == l / 2, S);
+                bool atm[V];
+#pragma unroll
+                for (int v = 0; v < V; ++v) atm[v] = m[v] && rank[v] == l / 2;
+                const double median = g.at_lowest(atm, S);
                 if (median < a.opp_threshold) {
-                    need_bo();
-                    const bool cand = tpeer && !m && bo == 0 && !dir && S > median;
-                    if (g.select(a, cand, a.opp_peers, gobs, t, P_GRAFT_OPP, gcol)) graft();
+#pragma unroll
+                    for (int v = 0; v < V; ++v) {
+                        need_bo(v);
+                        cand[v] = tpeer[v] && !m[v] && bo[v] == 0 && !dir[v] && S[v] > median;
+                    }
+                    g.select(a, cand, a.opp_peers, gobs, t, P_GRAFT_OPP, gcol, sel);
+#pragma unroll
+                    for (int v = 0; v < V; ++v)
+                        if (sel[v]) graft(v);
                 }
             }
 
-            if (valid) {
-                if (fl != fl0) a.mflags[i] = fl;
-                sf.store(a);
-                if (bo_dirty) a.backoff[i] = bo;
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                if (!valid[v]) continue;
+                if (fl[v] != fl0[v]) a.mflags[i[v]] = fl[v];
+                sf[v].store(a);
+                if (bo_dirty[v]) a.backoff[i[v]] = bo[v];
             }
             // the delivery's mesh mask of this row and topic (mesh or direct
             // edges to this shard's peers)
             if constexpr (Grp::kRowMask) {
                 if (a.mmask) {
-                    const uint64_t mk = g.row_mask(valid && (m || dir) && col >= a.olo && col < a.ohi);
-                    if (gl == 0 && ovalid) a.mmask[(int64_t)t * a.N + obs] = mk;
+                    bool mm[V];
+#pragma unroll
+                    for (int v = 0; v < V; ++v)
+                        mm[v] = valid[v] && (m[v] || dir[v]) && col[v] >= a.olo && col[v] < a.ohi;
+                    const uint64_t mk = g.row_mask(mm);
+                    if (gl[0] == 0 && ovalid) a.mmask[(int64_t)t * a.N + obs] = mk;
                 }
             }
 
@@ -835,38 +996,43 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
             // choice is stored in the sender's row (enqueueGossip); every
             // joined topic's plane is rewritten each heartbeat.
             if (a.gossip) {
-                bool gsel = false;
+                bool gs[V];
+#pragma unroll
+                for (int v = 0; v < V; ++v) gs[v] = false;
                 const int32_t lpt = g.lastput(a, obs, t);
                 if (lpt >= 0 && lpt >= (int64_t)a.tick - a.hist_gossip) {   // -1: no put yet
-                    if (g.any(dirty)) {
-                        if (dirty) S_live = score_of_record(a, rv, col);
-                        dirty = false;
-                    }
-                    const bool gcand = tpeer && !m && !dir && S_live >= a.gossip_thr;
-                    gsel = g.gossip(a, gcand, tpeer, gobs, t, gcol);
+                    rescore();
+#pragma unroll
+                    for (int v = 0; v < V; ++v)
+                        cand[v] = tpeer[v] && !m[v] && !dir[v] && S_live[v] >= a.gossip_thr;
+                    g.gossip(a, cand, tpeer, gobs, t, gcol, gs);
                 }
-                if (valid) a.gsel[i] = gsel ? 1 : 0;
+#pragma unroll
+                for (int v = 0; v < V; ++v)
+                    if (valid[v]) a.gsel[i[v]] = gs[v] ? 1 : 0;
             }
-            if (valid) {
-                if (ctl && slot_has(mj, t)) {
-                    const int64_t r = slot_idx(mj, t, a.E, a.rev[e]);   // the receiver's row
-                    a.ctl_out[r] = (uint8_t)(a.ctl_out[r] | ctl);
-                    atomicOr(reinterpret_cast<unsigned long long*>(a.cany_out + col), 1ull << t);
+            bool pxc[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                if (valid[v] && ctl[v] && slot_has(mj[v], t)) {
+                    const int64_t r = slot_idx(mj[v], t, a.E, rv[v]);   // the receiver's row
+                    a.ctl_out[r] = (uint8_t)(a.ctl_out[r] | ctl[v]);
+                    atomicOr(reinterpret_cast<unsigned long long*>(a.cany_out + col[v]), 1ull << t);
                 }
+                pxc[v] = (ctl[v] & GSIM_CTL_PX) != 0;
             }
-            if (a.do_px && g.any((ctl & GSIM_CTL_PX) != 0)) pxt |= 1ull << t;
+            if (a.do_px && g.any(pxc)) pxt |= 1ull << t;
           }
         }
         // sendGraftPrune follows every topic: k_px_emit picks the PX peers
         if (a.do_px && pxt) {
-            // the live scores makePrune's PX filter reads (k_px_emit): lanes this
-            // heartbeat's Graft/Prune touched since their last re-score
-            if (g.any(dirty)) {
-                if (dirty) S_live = score_of_record(a, rv, col);
-                dirty = false;
-            }
-            if (valid) a.pxs[e] = S_live;
-            if (gl == 0 && ovalid) a.pxo[obs] = pxt;
+            // the live scores makePrune's PX filter reads (k_px_emit): positions
+            // this heartbeat's Graft/Prune touched since their last re-score
+            rescore();
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                if (valid[v]) a.pxs[e[v]] = S_live[v];
+            if (gl[0] == 0 && ovalid) a.pxo[obs] = pxt;
         }
 }
 
@@ -889,11 +1055,11 @@ void k_heartbeat(HbArgs a, const uint32_t* rows, int64_t nrows, int64_t obs_base
 }
 
 // Hub observers (rows of 65 .. B connections): one block per observer.
-template <int B>
+template <int B, int V>
 __global__ __launch_bounds__(B) void k_heartbeat_hub(HbArgs a, const uint32_t* rows, int64_t nrows)
 {
-    __shared__ typename BlockGroup<B>::Shared sh;
-    BlockGroup<B> g(&sh);
+    __shared__ typename BlockGroup<B, V>::Shared sh;
+    BlockGroup<B, V> g(&sh);
     for (int64_t o = blockIdx.x; o < nrows; o += gridDim.x) hb_observer(a, g, (int64_t)rows[o], true);
 }
 
@@ -907,62 +1073,97 @@ __global__ __launch_bounds__(B) void k_heartbeat_hub(HbArgs a, const uint32_t* r
 template <class Grp>
 __device__ __forceinline__ void fanout_observer(const HbArgs& a, Grp& g, int64_t obs)
 {
-        const int gl = g.pos();
-        const int64_t lpub = gl < a.T ? a.lastpub[obs * a.T + gl] : 0;
+        constexpr int V = Grp::V;
+        const int gl0 = g.pos(0);
+        const int64_t lpub = gl0 < a.T ? a.lastpub[obs * a.T + gl0] : 0;   // position 0 < 64 covers the topics
         const uint64_t expired = g.topic_mask(lpub != 0 && lpub + a.fanout_ttl < a.now);
         const uint64_t fant0 = a.fan_topics[obs];
         if (!expired && !fant0) return;                         // group-uniform
         const uint32_t b = a.row_ptr[obs];
         const int deg = (int)(a.row_ptr[obs + 1] - b);
-        const bool valid = gl < deg;
-        const uint32_t e = b + (uint32_t)gl;
-        if (gl < 64 && ((expired >> gl) & 1ull)) a.lastpub[obs * a.T + gl] = 0;
+        bool valid[V];
+        uint32_t e[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            valid[v] = g.pos(v) < deg;
+            e[v] = b + (uint32_t)g.pos(v);
+        }
+        if (gl0 < 64 && ((expired >> gl0) & 1ull)) a.lastpub[obs * a.T + gl0] = 0;
         const uint64_t mi = smask_of(a.smask, (uint32_t)obs);   // fanout topics hold slots (gsim_publish)
         for (uint64_t q = expired & fant0 & mi; q; q &= q - 1) {
-            const int64_t i = slot_idx(mi, __ffsll((long long)q) - 1, a.E, e);
-            if (valid) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                if (!valid[v]) continue;
+                const int64_t i = slot_idx(mi, __ffsll((long long)q) - 1, a.E, e[v]);
                 const uint8_t fl = a.mflags[i];
                 if (fl & GSIM_TF_FANOUT) a.mflags[i] = (uint8_t)(fl & ~GSIM_TF_FANOUT);
                 if (a.gossip) a.gsel[i] = 0;                    // no more gossip for it
             }
         }
         const uint64_t fant = fant0 & ~expired;
-        if (gl == 0 && fant != fant0) a.fan_topics[obs] = fant;
+        if (gl0 == 0 && fant != fant0) a.fan_topics[obs] = fant;
         if (!fant) return;
-        const uint32_t col = valid ? a.col[e] : 0u;
-        const uint32_t rv = valid ? a.rev[e] : 0u;
-        const uint32_t gobs = glob(a, (uint32_t)obs), gcol = valid ? glob(a, col) : 0u;
-        const bool conn = valid && (a.rstate[e] & GSIM_ES_CONNECTED);
-        const bool dir = valid && a.direct[e];
-        const double S = valid ? a.score[rv] : 0.0;
-        const uint64_t subj = valid ? a.sub[col] : 0ull;
-        double S_live = 0.0;
+        const uint32_t gobs = glob(a, (uint32_t)obs);
+        uint32_t col[V], rv[V], gcol[V];
+        bool conn[V], dir[V];
+        double S[V], S_live[V];
+        uint64_t subj[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            col[v] = valid[v] ? a.col[e[v]] : 0u;
+            rv[v] = valid[v] ? a.rev[e[v]] : 0u;
+            gcol[v] = valid[v] ? glob(a, col[v]) : 0u;
+            conn[v] = valid[v] && (a.rstate[e[v]] & GSIM_ES_CONNECTED);
+            dir[v] = valid[v] && a.direct[e[v]];
+            S[v] = valid[v] ? a.score[rv[v]] : 0.0;
+            subj[v] = valid[v] ? a.sub[col[v]] : 0ull;
+            S_live[v] = 0.0;
+        }
         bool have_live = false;
         for (uint64_t q = fant & mi; q; q &= q - 1) {
             const int32_t t = __ffsll((long long)q) - 1;
-            const int64_t i = slot_idx(mi, t, a.E, e);
-            const uint8_t fl = valid ? a.mflags[i] : 0;
-            const bool tpeer = conn && ((subj >> t) & 1ull);
-            bool inf = (fl & GSIM_TF_FANOUT) && tpeer && S >= a.pub_thr;
+            int64_t i[V];
+            uint8_t fl[V];
+            bool tpeer[V], inf[V], cand[V], sel[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                i[v] = slot_idx(mi, t, a.E, e[v]);
+                fl[v] = valid[v] ? a.mflags[i[v]] : 0;
+                tpeer[v] = conn[v] && ((subj[v] >> t) & 1ull);
+                inf[v] = (fl[v] & GSIM_TF_FANOUT) && tpeer[v] && S[v] >= a.pub_thr;
+            }
             const int have = g.count(inf);
             if (have < a.D) {
-                const bool cand = tpeer && !inf && !dir && S >= a.pub_thr;
-                if (g.select(a, cand, a.D - have, gobs, t, P_FANOUT, gcol)) inf = true;
+#pragma unroll
+                for (int v = 0; v < V; ++v) cand[v] = tpeer[v] && !inf[v] && !dir[v] && S[v] >= a.pub_thr;
+                g.select(a, cand, a.D - have, gobs, t, P_FANOUT, gcol, sel);
+#pragma unroll
+                for (int v = 0; v < V; ++v) if (sel[v]) inf[v] = true;
             }
-            const uint8_t nf = inf ? (uint8_t)(fl | GSIM_TF_FANOUT) : (uint8_t)(fl & ~GSIM_TF_FANOUT);
-            if (valid && nf != fl) a.mflags[i] = nf;
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                const uint8_t nf = inf[v] ? (uint8_t)(fl[v] | GSIM_TF_FANOUT) : (uint8_t)(fl[v] & ~GSIM_TF_FANOUT);
+                if (valid[v] && nf != fl[v]) a.mflags[i[v]] = nf;
+            }
             if (!a.gossip) continue;
-            bool gsel = false;
+            bool gs[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) gs[v] = false;
             const int32_t lpt = a.lastput[(int64_t)t * a.N + obs];
             if (lpt >= 0 && lpt >= (int64_t)a.tick - a.hist_gossip) {
                 if (!have_live) {                               // live Score(p), gossipsub.go:1734
-                    if (valid) S_live = score_of_record(a, rv, col);
+#pragma unroll
+                    for (int v = 0; v < V; ++v)
+                        if (valid[v]) S_live[v] = score_of_record(a, rv[v], col[v]);
                     have_live = true;
                 }
-                const bool gcand = tpeer && !inf && !dir && S_live >= a.gossip_thr;
-                gsel = g.gossip(a, gcand, tpeer, gobs, t, gcol);
+#pragma unroll
+                for (int v = 0; v < V; ++v) cand[v] = tpeer[v] && !inf[v] && !dir[v] && S_live[v] >= a.gossip_thr;
+                g.gossip(a, cand, tpeer, gobs, t, gcol, gs);
             }
-            if (valid) a.gsel[i] = gsel ? 1 : 0;
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                if (valid[v]) a.gsel[i[v]] = gs[v] ? 1 : 0;
         }
 }
 
@@ -979,11 +1180,11 @@ __global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
 }
 
 // ... of the hub observers (rows of 65 .. B connections), one block each
-template <int B>
+template <int B, int V>
 __global__ __launch_bounds__(B) void k_fanout_heartbeat_hub(HbArgs a, const uint32_t* rows, int64_t nrows)
 {
-    __shared__ typename BlockGroup<B>::Shared sh;
-    BlockGroup<B> g(&sh);
+    __shared__ typename BlockGroup<B, V>::Shared sh;
+    BlockGroup<B, V> g(&sh);
     for (int64_t o = blockIdx.x; o < nrows; o += gridDim.x) fanout_observer(a, g, (int64_t)rows[o]);
 }
 
@@ -1189,19 +1390,27 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ __launch_bounds__(256) void k_px_emit(HbArgs a, int live, uint32_t key_tick, uint32_t purpose)
+// ROW: the longest row staged (WV waves per block, ROW scores and keys each):
+// <kPxRow, 4> walks the owned observers with rows of at most kPxRow,
+// <4 kPxRow, 1> the hub list `rows` (rows of kPxRow+1 .. 4 kPxRow).
+template <int ROW, int WV>
+__global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a, int live, uint32_t key_tick, uint32_t purpose,
+                                                     const uint32_t* rows, int64_t nrows)
 {
-    __shared__ double s_sc[4][kPxRow];
-    __shared__ uint64_t s_key[4][kPxRow];
+    __shared__ double s_sc[WV][ROW];
+    __shared__ uint64_t s_key[WV][ROW];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double* sc = s_sc[wid];
     uint64_t* key = s_key[wid];
-    for (int64_t obs = a.olo + (int64_t)blockIdx.x * 4 + wid; obs < a.ohi; obs += (int64_t)gridDim.x * 4) {
+    const int64_t nobs = rows ? nrows : a.ohi - a.olo;
+    for (int64_t x = (int64_t)blockIdx.x * WV + wid; x < nobs; x += (int64_t)gridDim.x * WV) {
+        const int64_t obs = rows ? (int64_t)rows[x] : a.olo + x;
+        const uint32_t b = a.row_ptr[obs];
+        const int deg = (int)(a.row_ptr[obs + 1] - b);
+        if (deg > ROW) continue;                                 // a longer hub: the <4 kPxRow, 1> instance
         const uint64_t mask = a.pxo[obs];
         if (!mask) continue;
         if (lane == 0) a.pxo[obs] = 0;
-        const uint32_t b = a.row_ptr[obs];
-        const int deg = (int)(a.row_ptr[obs + 1] - b);
         const uint32_t gobs = glob(a, (uint32_t)obs);
         for (int q = lane; q < deg; q += 64) {
             const uint32_t e = b + (uint32_t)q, x = a.col[e], rv = a.rev[e];
@@ -1491,33 +1700,52 @@ __global__ __launch_bounds__(256) void k_churn_apply(HbArgs a, ChurnArgs c)
 template <class Grp>
 __device__ __forceinline__ void fanout_publish_one(const HbArgs& a, Grp& g, const gsim_msg* pub, int32_t k)
 {
-    const int gl = g.pos();
+    constexpr int V = Grp::V;
+    const int gl0 = g.pos(0);
     const uint32_t o = pub[k].origin;
     const int32_t t = (int32_t)pub[k].topic;
-    bool dup = false;
-    for (int32_t q = gl; q < k; q += g.span()) dup |= pub[q].origin == o && (int32_t)pub[q].topic == t;
+    bool dup[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) dup[v] = false;
+    for (int32_t q = gl0; q < k; q += g.span() / V) dup[0] |= pub[q].origin == o && (int32_t)pub[q].topic == t;
     if (g.any(dup)) return;
     const uint32_t b = a.row_ptr[o];
     const int deg = (int)(a.row_ptr[o + 1] - b);
-    const bool valid = gl < deg;
-    const uint32_t e = b + (uint32_t)gl;
     const uint64_t mo = smask_of(a.smask, o);      // gsim_publish gave the origin a slot for t
     if (!slot_has(mo, t)) return;                  // group-uniform
-    const int64_t i = slot_idx(mo, t, a.E, e);
-    const uint8_t fl = valid ? a.mflags[i] : 0;
-    const bool have = ((a.fan_topics[o] >> t) & 1ull) && g.any((fl & GSIM_TF_FANOUT) != 0);
-    if (!have) {
-        const uint32_t col = valid ? a.col[e] : 0u;
-        const bool conn = valid && (a.rstate[e] & GSIM_ES_CONNECTED);
-        const bool tpeer = conn && ((a.sub[col] >> t) & 1ull);
-        const double S = valid ? a.score[a.rev[e]] : 0.0;
-        const bool cand = tpeer && !(fl & GSIM_TF_FANOUT) && !(valid && a.direct[e]) && S >= a.pub_thr;
-        const bool sel = g.select(a, cand, a.D, glob(a, o), t, P_FANOUT_NEW, valid ? glob(a, col) : 0u);
-        if (valid && sel) a.mflags[i] = (uint8_t)(fl | GSIM_TF_FANOUT);
-        const bool any = g.any(sel);
-        if (gl == 0 && any) atomicOr(reinterpret_cast<unsigned long long*>(a.fan_topics + o), 1ull << t);
+    bool valid[V], isf[V];
+    uint32_t e[V];
+    int64_t i[V];
+    uint8_t fl[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        valid[v] = g.pos(v) < deg;
+        e[v] = b + (uint32_t)g.pos(v);
+        i[v] = slot_idx(mo, t, a.E, e[v]);
+        fl[v] = valid[v] ? a.mflags[i[v]] : 0;
+        isf[v] = (fl[v] & GSIM_TF_FANOUT) != 0;
     }
-    if (gl == 0) a.lastpub[(int64_t)o * a.T + t] = a.now;
+    const bool have = ((a.fan_topics[o] >> t) & 1ull) && g.any(isf);
+    if (!have) {
+        uint32_t gcol[V];
+        bool cand[V], sel[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const uint32_t col = valid[v] ? a.col[e[v]] : 0u;
+            const bool conn = valid[v] && (a.rstate[e[v]] & GSIM_ES_CONNECTED);
+            const bool tpeer = conn && ((a.sub[col] >> t) & 1ull);
+            const double S = valid[v] ? a.score[a.rev[e[v]]] : 0.0;
+            cand[v] = tpeer && !isf[v] && !(valid[v] && a.direct[e[v]]) && S >= a.pub_thr;
+            gcol[v] = valid[v] ? glob(a, col) : 0u;
+        }
+        g.select(a, cand, a.D, glob(a, o), t, P_FANOUT_NEW, gcol, sel);
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+            if (valid[v] && sel[v]) a.mflags[i[v]] = (uint8_t)(fl[v] | GSIM_TF_FANOUT);
+        const bool any = g.any(sel);
+        if (gl0 == 0 && any) atomicOr(reinterpret_cast<unsigned long long*>(a.fan_topics + o), 1ull << t);
+    }
+    if (gl0 == 0) a.lastpub[(int64_t)o * a.T + t] = a.now;
 }
 
 __device__ __forceinline__ bool fanout_publisher(const HbArgs& a, const gsim_msg* pub, int32_t k)
@@ -1537,15 +1765,16 @@ __global__ __launch_bounds__(256) void k_fanout_publish(HbArgs a, const gsim_msg
     fanout_publish_one(a, g, pub, k);
 }
 
-template <int B>
-__global__ __launch_bounds__(B) void k_fanout_publish_hub(HbArgs a, const gsim_msg* pub, int32_t count)
+// origins with rows of lo+1 .. B·V connections
+template <int B, int V>
+__global__ __launch_bounds__(B) void k_fanout_publish_hub(HbArgs a, const gsim_msg* pub, int32_t count, uint32_t lo)
 {
-    __shared__ typename BlockGroup<B>::Shared sh;
+    __shared__ typename BlockGroup<B, V>::Shared sh;
     const int32_t k = (int32_t)blockIdx.x;
     if (k >= count || !fanout_publisher(a, pub, k)) return;  // block-uniform
-    const uint32_t o = pub[k].origin;
-    if (a.row_ptr[o + 1] - a.row_ptr[o] <= 64u) return;
-    BlockGroup<B> g(&sh);
+    const uint32_t o = pub[k].origin, d = a.row_ptr[o + 1] - a.row_ptr[o];
+    if (d <= lo || d > (uint32_t)(B * V)) return;
+    BlockGroup<B, V> g(&sh);
     fanout_publish_one(a, g, pub, k);
 }
 
@@ -1580,11 +1809,11 @@ int alloc_extra(gsim_handle* h)
     e = hipMemcpy(rp.data(), h->d_row_ptr, sizeof(uint32_t) * rp.size(), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_check(h, e, "row_ptr readback");
     uint32_t md = 0, mdall = 0;
-    std::vector<uint32_t> cls[5];
+    std::vector<uint32_t> cls[6];
     for (int64_t i = h->olo(); i < h->ohi(); ++i) {
         const uint32_t d = rp[(size_t)i + 1] - rp[(size_t)i];
         md = std::max(md, d);
-        cls[d <= 16 ? 0 : d <= 32 ? 1 : d <= 64 ? 2 : d <= 256 ? 3 : 4].push_back((uint32_t)i);
+        cls[d <= 16 ? 0 : d <= 32 ? 1 : d <= 64 ? 2 : d <= 256 ? 3 : d <= 1024 ? 4 : 5].push_back((uint32_t)i);
     }
     for (int64_t i = 0; i < h->n; ++i) mdall = std::max(mdall, rp[(size_t)i + 1] - rp[(size_t)i]);
     if (!h->all_joined) {
@@ -1599,7 +1828,7 @@ int alloc_extra(gsim_handle* h)
     }
     h->x->max_degree = md;
     h->x->n16 = (int64_t)cls[0].size(); h->x->n32 = (int64_t)cls[1].size(); h->x->n64 = (int64_t)cls[2].size();
-    h->x->nh256 = (int64_t)cls[3].size(); h->x->nh1024 = (int64_t)cls[4].size();
+    h->x->nh256 = (int64_t)cls[3].size(); h->x->nh1024 = (int64_t)cls[4].size(); h->x->nh4096 = (int64_t)cls[5].size();
     if (md > 16 || !h->all_joined) {   // several classes, or an order by subscriptions: keep the lists
         std::vector<uint32_t> all;
         all.reserve((size_t)h->n);
@@ -1735,8 +1964,8 @@ static int grid_rows(int64_t n)
 
 static int check_degree(gsim_handle* h)
 {
-    if (h->x->max_degree > 1024) {
-        h->err = "heartbeat kernels support rows of at most 1024 connections in this build";
+    if (h->x->max_degree > 4096) {
+        h->err = "heartbeat kernels support rows of at most 4096 connections in this build";
         return GSIM_ERANGE;
     }
     return GSIM_OK;
@@ -1750,7 +1979,10 @@ int launch_fanout_publish(gsim_handle* h, const gsim_msg* d_pub, int32_t count, 
     HbArgs a = make_hb_args(h, (uint64_t)g, now, 0);
     hipLaunchKernelGGL(k_fanout_publish, dim3((count + 3) / 4), dim3(256), 0, h->stream, a, d_pub, count);
     if (h->x->nh256 + h->x->nh1024)
-        hipLaunchKernelGGL(k_fanout_publish_hub<1024>, dim3(count), dim3(1024), 0, h->stream, a, d_pub, count);
+        hipLaunchKernelGGL((k_fanout_publish_hub<1024, 1>), dim3(count), dim3(1024), 0, h->stream, a, d_pub, count, 64u);
+    if (h->x->nh4096)
+        hipLaunchKernelGGL((k_fanout_publish_hub<1024, 4>), dim3(count), dim3(1024), 0, h->stream, a, d_pub, count,
+                           1024u);
     return hip_check(h, hipGetLastError(), "k_fanout_publish");
 }
 
@@ -1801,21 +2033,34 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
         // hubs: one block per observer
         const uint32_t* rh = r + x->n16 + x->n32 + x->n64;
         if (x->nh256)
-            hipLaunchKernelGGL(k_heartbeat_hub<256>, dim3((uint32_t)std::min<int64_t>(x->nh256, 65536)), dim3(256), 0,
-                               h->stream, a, rh, x->nh256);
+            hipLaunchKernelGGL((k_heartbeat_hub<256, 1>), dim3((uint32_t)std::min<int64_t>(x->nh256, 65536)), dim3(256),
+                               0, h->stream, a, rh, x->nh256);
         if (x->nh1024)
-            hipLaunchKernelGGL(k_heartbeat_hub<1024>, dim3((uint32_t)std::min<int64_t>(x->nh1024, 65536)), dim3(1024),
-                               0, h->stream, a, rh + x->nh256, x->nh1024);
+            hipLaunchKernelGGL((k_heartbeat_hub<1024, 1>), dim3((uint32_t)std::min<int64_t>(x->nh1024, 65536)),
+                               dim3(1024), 0, h->stream, a, rh + x->nh256, x->nh1024);
+        if (x->nh4096)   // 4 row positions per thread
+            hipLaunchKernelGGL((k_heartbeat_hub<1024, 4>), dim3((uint32_t)std::min<int64_t>(x->nh4096, 65536)),
+                               dim3(1024), 0, h->stream, a, rh + x->nh256 + x->nh1024, x->nh4096);
     }
     hipLaunchKernelGGL(k_fanout_heartbeat, dim3(grid_rows(nown)), dim3(256), 0, h->stream, a);
+    const uint32_t* rh = x->d_rows + x->n16 + x->n32 + x->n64;
     if (x->nh256)
-        hipLaunchKernelGGL(k_fanout_heartbeat_hub<256>, dim3((uint32_t)std::min<int64_t>(x->nh256, 65536)), dim3(256),
-                           0, h->stream, a, x->d_rows + x->n16 + x->n32 + x->n64, x->nh256);
+        hipLaunchKernelGGL((k_fanout_heartbeat_hub<256, 1>), dim3((uint32_t)std::min<int64_t>(x->nh256, 65536)),
+                           dim3(256), 0, h->stream, a, rh, x->nh256);
     if (x->nh1024)
-        hipLaunchKernelGGL(k_fanout_heartbeat_hub<1024>, dim3((uint32_t)std::min<int64_t>(x->nh1024, 65536)),
-                           dim3(1024), 0, h->stream, a, x->d_rows + x->n16 + x->n32 + x->n64 + x->nh256, x->nh1024);
-    if (a.do_px)   // sendGraftPrune's makePrune with PX, live scores after every topic
-        hipLaunchKernelGGL(k_px_emit, dim3(grid_rows(nown)), dim3(256), 0, h->stream, a, 1, (uint32_t)tick, (uint32_t)P_PX);
+        hipLaunchKernelGGL((k_fanout_heartbeat_hub<1024, 1>), dim3((uint32_t)std::min<int64_t>(x->nh1024, 65536)),
+                           dim3(1024), 0, h->stream, a, rh + x->nh256, x->nh1024);
+    if (x->nh4096)
+        hipLaunchKernelGGL((k_fanout_heartbeat_hub<1024, 4>), dim3((uint32_t)std::min<int64_t>(x->nh4096, 65536)),
+                           dim3(1024), 0, h->stream, a, rh + x->nh256 + x->nh1024, x->nh4096);
+    if (a.do_px) {  // sendGraftPrune's makePrune with PX, live scores after every topic
+        hipLaunchKernelGGL((k_px_emit<kPxRow, 4>), dim3(grid_rows(nown)), dim3(256), 0, h->stream, a, 1, (uint32_t)tick,
+                           (uint32_t)P_PX, (const uint32_t*)nullptr, (int64_t)0);
+        if (x->nh4096)
+            hipLaunchKernelGGL((k_px_emit<4 * kPxRow, 1>), dim3((uint32_t)std::min<int64_t>(x->nh4096, 65536)), dim3(64),
+                               0, h->stream, a, 1, (uint32_t)tick, (uint32_t)P_PX,
+                               (const uint32_t*)(rh + x->nh256 + x->nh1024), x->nh4096);
+    }
     return hip_check(h, hipGetLastError(), "k_heartbeat");
 }
 
@@ -1826,9 +2071,17 @@ int handle_control(gsim_handle* h, int32_t round, int64_t now)
     HbArgs a = make_hb_args(h, 0, now, round & 1);
     ProfScope ps(h, GSIM_K_CONTROL);
     hipLaunchKernelGGL(k_handle_control, dim3(grid_rows(h->ohi() - h->olo())), dim3(256), 0, h->stream, a);
-    if (a.do_px)   // handleGraft's PRUNE replies with PX (snapshot scores)
-        hipLaunchKernelGGL(k_px_emit, dim3(grid_rows(h->ohi() - h->olo())), dim3(256), 0, h->stream, a, 0,
-                           (uint32_t)((uint64_t)now ^ ((uint64_t)now >> 32)), (uint32_t)P_PX_GRAFT);
+    if (a.do_px) {  // handleGraft's PRUNE replies with PX (snapshot scores)
+        const uint32_t kt = (uint32_t)((uint64_t)now ^ ((uint64_t)now >> 32));
+        hipLaunchKernelGGL((k_px_emit<kPxRow, 4>), dim3(grid_rows(h->ohi() - h->olo())), dim3(256), 0, h->stream, a, 0,
+                           kt, (uint32_t)P_PX_GRAFT, (const uint32_t*)nullptr, (int64_t)0);
+        const Extra* x = h->x;
+        if (x->nh4096)
+            hipLaunchKernelGGL((k_px_emit<4 * kPxRow, 1>), dim3((uint32_t)std::min<int64_t>(x->nh4096, 65536)), dim3(64),
+                               0, h->stream, a, 0, kt, (uint32_t)P_PX_GRAFT,
+                               (const uint32_t*)(x->d_rows + x->n16 + x->n32 + x->n64 + x->nh256 + x->nh1024),
+                               x->nh4096);
+    }
     return hip_check(h, hipGetLastError(), "k_handle_control");
 }
 

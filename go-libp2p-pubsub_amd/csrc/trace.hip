@@ -34,7 +34,8 @@ __global__ __launch_bounds__(256) void k_trace_resolve(gsim_trace_event* ev, int
         if (x.type != kTraceCopy) continue;
         const uint32_t m = (uint32_t)x.msg_id;
         const int64_t g = (int64_t)(x.msg_id >> 32);
-        const uint64_t c = v.cell[(int64_t)m * CN + (x.peer - clo)];
+        const uint64_t c = v.cells.get(m, (int32_t)v.mtopic[m], x.peer);
+        (void)CN; (void)clo;
         // every claim is committed before a read (gsim_trace_read flushes)
         const int64_t fr = c == kUnseen64 ? -1 : (int64_t)(c >> 32);
         const uint32_t from = (uint32_t)c & kPeerMask;

@@ -41,7 +41,7 @@ struct WireArgs {
     const uint8_t* ctl;           // parity-0 inbox [T][E] (receivers' edges)
     const uint8_t* gsel;          // [T][E] (senders' edges)
     const uint64_t* smask;        // topic slots of both arrays (gsim_internal.h; nullptr: dense)
-    const uint64_t* cell;
+    Cells cells;                  // the seen-set (gsim_internal.h)
     int64_t N, E;
     int32_t T, R;
     const uint32_t *mtopic, *morigin;
@@ -92,7 +92,7 @@ __device__ __forceinline__ int64_t seen_round(uint64_t c, int64_t g)
 // accepted first delivery, or of its own publication); its round, else -1
 __device__ __forceinline__ int64_t window_put(const WireArgs& a, uint32_t m, uint32_t p)
 {
-    const int64_t fr = seen_round(a.cell[(int64_t)m * a.N + p], a.g);
+    const int64_t fr = seen_round(a.cells.get(m, (int32_t)a.mtopic[m], p), a.g);
     if (fr < a.lo_round || fr >= a.g) return -1;
     if (a.minv[m] != GSIM_VERDICT_ACCEPT && a.morigin[m] != p) return -1;
     return fr;
@@ -421,7 +421,7 @@ extern "C" int gsim_wire_heartbeat(gsim_handle* h, int64_t tick, uint32_t p0, ui
     a.ctl = extra_ctl(h);            // parity 0: the heartbeat's output
     a.gsel = v.gsel;
     a.smask = h->d_smask;
-    a.cell = v.cell;
+    a.cells = v.cells;
     a.N = h->n; a.E = h->e; a.T = T; a.R = v.rounds;
     a.mtopic = v.mtopic; a.morigin = v.morigin; a.minv = v.minv; a.mid = v.mid;
     a.cand = d_cand; a.cand_ptr = d_cand_ptr;

@@ -94,7 +94,7 @@ TRACE_ADD_PEER, TRACE_REMOVE_PEER, TRACE_GRAFT, TRACE_PRUNE = 4, 5, 11, 12
 # (name, restype, argtypes) for every symbol include/gsim.h declares.
 class CMsgConfig(Structure):
     _fields_ = [("ring", c_int32), ("rounds", c_int32), ("t0_ns", c_int64), ("heartbeat_ns", c_int64),
-                ("max_frontier", c_int64), ("max_arrivals", c_int64)]
+                ("max_frontier", c_int64), ("max_arrivals", c_int64), ("topic_slots", c_int64)]
 
 
 class CMsg(Structure):
@@ -214,6 +214,8 @@ SIGNATURES = [
     ("gsim_synchronize", c_int32, [c_void_p]),
     ("gsim_set_kernel_variant", c_int32, [c_void_p, c_int32, c_int32]),
     ("gsim_gen_random_regular", c_int32, [c_int64, c_int32, c_uint64, c_void_p, c_void_p, c_void_p]),
+    ("gsim_gen_power_law", c_int32, [c_int64, c_double, c_double, c_int32, c_double, c_uint64, c_void_p, c_void_p,
+                                     c_void_p, c_void_p]),
     ("gsim_fill_synthetic", c_int32, [c_void_p, c_uint64, c_int64, c_double]),
     ("gsim_set_seed", c_int32, [c_void_p, c_uint64]),
     ("gsim_census", c_int32, [c_void_p, c_void_p]),

@@ -252,8 +252,11 @@ class Engine:
 
     # -- message propagation ------------------------------------------------------
     def msgs_init(self, ring: int, rounds: int, t0: int, heartbeat: Optional[int] = None,
-                  max_frontier: Optional[int] = None, max_arrivals: Optional[int] = None):
-        """Allocate the message ring / seen-set (gsim_msgs_init)."""
+                  max_frontier: Optional[int] = None, max_arrivals: Optional[int] = None,
+                  topic_slots: int = 0):
+        """Allocate the message ring / seen-set (gsim_msgs_init).  topic_slots > 0:
+        per-topic sub-rings (a message takes its topic's next slot in publication
+        order) with member-compacted seen-set cells."""
         c = _abi.CMsgConfig()
         c.ring, c.rounds, c.t0_ns = int(ring), int(rounds), int(t0)
         c.heartbeat_ns = int(heartbeat if heartbeat is not None else self.gossip.HeartbeatInterval)
@@ -261,6 +264,9 @@ class Engine:
         # sizes the IWANT response queue (0: the library default, gsim.h)
         c.max_frontier = int(max_frontier or 0)
         c.max_arrivals = int(max_arrivals or 0)
+        # > 0: per-topic sub-rings of this many slots (ring = n_topics * topic_slots),
+        # seen-set cells only for each topic's members (gsim.h gsim_msg_config)
+        c.topic_slots = int(topic_slots or 0)
         self._check(self.lib.gsim_msgs_init(self.h, ctypes.byref(c)))
         self._msg_cfg = c
 

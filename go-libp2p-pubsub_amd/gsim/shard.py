@@ -256,12 +256,16 @@ class ShardedEngine:
 
     # -- hot path -------------------------------------------------------------------
     def msgs_init(self, ring: int, rounds: int, t0: int, heartbeat: Optional[int] = None,
-                  max_frontier: Optional[int] = None, max_arrivals: Optional[int] = None):
+                  max_frontier: Optional[int] = None, max_arrivals: Optional[int] = None,
+                  topic_slots: int = 0):
         c = _abi.CMsgConfig()
         c.ring, c.rounds, c.t0_ns = int(ring), int(rounds), int(t0)
         c.heartbeat_ns = int(heartbeat if heartbeat is not None else self.gossip.HeartbeatInterval)
         c.max_frontier = int(max_frontier or 0)      # forwarders one shard exports per round (0: default)
         c.max_arrivals = int(max_arrivals or 0)
+        # > 0: per-topic sub-rings of this many slots (ring = n_topics * topic_slots),
+        # seen-set cells only for each topic's members (gsim.h gsim_msg_config)
+        c.topic_slots = int(topic_slots or 0)
         self._check(self.lib.gsim_group_msgs_init(self.g, ctypes.byref(c)))
         self._msg_cfg = c
 

@@ -283,6 +283,13 @@ typedef struct gsim_msg_config {
     int64_t heartbeat_ns;    /* heartbeat interval (GossipSubParams.HeartbeatInterval) */
     int64_t max_frontier;    /* reserved (ignored): the engine keeps no per-copy lists */
     int64_t max_arrivals;    /* capacity of the IWANT response queue per tick (0: max(8 N, 2^20)) */
+    int64_t topic_slots;     /* 0: one ring shared by every topic, a message's slot is id % ring, and
+                                every slot keeps a seen-set cell per peer.  > 0: per-topic sub-rings
+                                (ring = n_topics * topic_slots): topic t owns slots [t * topic_slots,
+                                (t + 1) * topic_slots) and its messages take them in publication
+                                order; each slot keeps cells only for the peers holding topic t (its
+                                slot mask), so the seen-set scales with the topics'
+                                members, not with the network (timecache, pubsub.go:987-995) */
 } gsim_msg_config;
 
 /* The validation verdict every receiver reaches for a message (validation
@@ -521,6 +528,14 @@ int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant);
  * (n*k, may be NULL) gets a Bernoulli(0.5) initiator per undirected edge. */
 int gsim_gen_random_regular(int64_t n, int32_t k, uint64_t seed,
                             uint32_t* row_ptr, uint32_t* col_idx, uint8_t* outbound);
+/* Chung-Lu power law (C5 inputs): expected degree of peer i proportional to
+ * (i + i0)^(-1/(exponent-1)) scaled to `mean`, capped at max_degree; pairs
+ * drawn by inverse CDF, self loops and repeats dropped, then accepted in
+ * drawing order while both ends are below the cap.  Call with col_idx NULL
+ * for the directed edge count (*n_edges), then with row_ptr (n+1), col_idx
+ * and outbound (may be NULL) sized to it; rows come out sorted. */
+int gsim_gen_power_law(int64_t n, double mean, double exponent, int32_t max_degree, double i0, uint64_t seed,
+                       uint32_t* row_ptr, uint32_t* col_idx, uint8_t* outbound, int64_t* n_edges);
 /* Fill every edge-topic record with seeded steady-state-like counters on the
  * device (mesh membership with probability p_mesh, graft times within the
  * last hour of now_ns); every edge tracked+connected.  Records of topics the

@@ -80,6 +80,10 @@ typedef struct orc_msgs {
     void*     priv;            /* frontier / gossip storage (oracle-owned) */
     uint64_t* mid;             /* [ring] message id of the slot's current message (or NULL) */
     const uint8_t* behaviour;  /* [N] ORC_BEHAVE_* per peer, or NULL */
+    int32_t topic_slots;       /* 0: slot = id % ring; > 0: per-topic sub-rings, topic t's messages take
+                                  slots t * topic_slots + (its earlier messages mod topic_slots), as
+                                  gsim_msg_config.topic_slots (the engine's seen-set layout, not the
+                                  reference's: its timecache is keyed by message id) */
 } orc_msgs;
 
 #define ORC_BEHAVE_IGNORE_IWANT 0x01   /* never answers IWANT (gossipsub_spam_test.go:134-286) */

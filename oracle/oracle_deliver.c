@@ -102,6 +102,7 @@ void orc_msgs_free_priv(orc_msgs* m)
     free(p->tx);
     free(p->slot_last);
     free(p->vd);
+    free(p->tcount);
     free(p->pq);
     free(p->cand);
     free(p->cand_ptr);
@@ -163,7 +164,12 @@ void orc_publish(orc_net* s, orc_msgs* m, uint64_t id, uint32_t topic, uint32_t 
 void orc_publish_v(orc_net* s, orc_msgs* m, uint64_t id, uint32_t topic, uint32_t origin, uint8_t invalid,
                    uint8_t vdelay, int64_t g)
 {
-    const uint32_t slot = (uint32_t)(id % (uint64_t)m->ring);
+    uint32_t slot = (uint32_t)(id % (uint64_t)m->ring);
+    if (m->topic_slots > 0) {
+        priv* pv = P(m);
+        if (!pv->tcount) pv->tcount = (int64_t*)calloc(64, sizeof(int64_t));
+        slot = (uint32_t)((int64_t)topic * m->topic_slots + pv->tcount[topic]++ % m->topic_slots);
+    }
     {
         priv* pv = P(m);
         if (!pv->vd) pv->vd = (uint8_t*)calloc((size_t)m->ring, 1);

@@ -63,6 +63,7 @@ typedef struct priv {
     int64_t* slot_last;                 /* [ring] last round with a first reception (or the publication) */
     uint32_t* cand; int32_t* cand_ptr;  /* per-topic recent slots at the current heartbeat (CSR) */
     uint8_t* vd;                        /* [ring] validation latency of the slot's message, rounds */
+    int64_t* tcount;                    /* [64] messages published per topic (orc_msgs.topic_slots) */
     pend_ent* pq; int64_t npq, cappq;   /* copies pending validation */
     int32_t log_on;                     /* event log (orc_msgs_log) */
     orc_event* ev; int64_t nev, capev;

@@ -42,7 +42,7 @@ class OrcMsgs(Structure):
         ("ring", c_int32), ("rounds", c_int32), ("t0", c_int64), ("hb", c_int64),
         ("topic", c_void_p), ("origin", c_void_p), ("invalid", c_void_p), ("seen", c_void_p),
         ("lastput", c_void_p), ("stats", c_int64 * 4), ("priv", c_void_p),
-        ("mid", c_void_p), ("behaviour", c_void_p),
+        ("mid", c_void_p), ("behaviour", c_void_p), ("topic_slots", c_int32),
     ]
 
 
@@ -243,7 +243,7 @@ EVENT_DTYPE = np.dtype([("kind", np.int32), ("topic", np.int32), ("a", np.uint32
 class Msgs:
     """Oracle message ring + seen-set of a network (oracle_deliver.c)."""
 
-    def __init__(self, n, T, ring, rounds, t0, hb, behaviour=None):
+    def __init__(self, n, T, ring, rounds, t0, hb, behaviour=None, topic_slots=0):
         self.seen = np.full((ring, n), UNSEEN, dtype=np.uint32)
         self.topic = np.zeros(ring, dtype=np.uint32)
         self.origin = np.zeros(ring, dtype=np.uint32)
@@ -256,6 +256,9 @@ class Msgs:
         m.topic, m.origin, m.invalid = _p(self.topic), _p(self.origin), _p(self.invalid)
         m.seen, m.lastput = _p(self.seen), _p(self.lastput)
         m.mid, m.behaviour = _p(self.mid), _p(self.behaviour)
+        m.topic_slots = int(topic_slots)     # per-topic sub-rings (gsim_msg_config.topic_slots)
+        if topic_slots:
+            self.topic[:] = np.arange(ring, dtype=np.uint32) // np.uint32(topic_slots)
         self.m = m
 
     @property

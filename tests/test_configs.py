@@ -222,10 +222,13 @@ def test_c4_sybil_colocation_broken_promises(require_gpu):
 
 
 @pytest.mark.gpu
-def test_c5_power_law_zipf_topics_churn(require_gpu):
+@pytest.mark.parametrize("topic_slots", [0, 16])
+def test_c5_power_law_zipf_topics_churn(require_gpu, topic_slots):
     """C5 scaled: power-law graph (rows up to 64), 64 topics with Zipf
     subscriptions (~8 per peer), connections churning between ticks,
-    publishers outside a topic using fanout."""
+    publishers outside a topic using fanout (their topic slots and, with
+    per-topic sub-rings, the topics' member-compacted seen-set cells grow at
+    publication).  topic_slots: 0 = one shared ring, 16 = sub-rings."""
     from fixtures import beacon_params, synthetic_state
     from gsim import graphs
     from tickrun import restrict_to_subscriptions, run_parity, subscribed_schedule
@@ -247,7 +250,7 @@ def test_c5_power_law_zipf_topics_churn(require_gpu):
     pick = lambda k: und[rng.choice(len(und), size=len(und) // 50, replace=False)]  # noqa: E731
     downs = {k: pick(k) for k in (2, 4)}
     churn = {2: [(downs[2], False)], 4: [(downs[2], True), (downs[4], False)], 6: [(downs[4], True)]}
-    run_parity(net, params, th, gp, st, ticks, sched, ring=1024, churn=churn)
+    run_parity(net, params, th, gp, st, ticks, sched, ring=1024, churn=churn, topic_slots=topic_slots)
     assert (np.diff(net.row_ptr.astype(np.int64)) > 32).any(), "rows longer than half a wave"
 
 
@@ -320,7 +323,8 @@ def test_c5_from_device_fill_skips_unjoined_records(require_gpu):
 
 
 @pytest.mark.gpu
-def test_hub_rows_bit_exact(require_gpu):
+@pytest.mark.parametrize("topic_slots", [0, 32])
+def test_hub_rows_bit_exact(require_gpu, topic_slots):
     """Hub observers (rows of 65-1024 connections, SURVEY §8 C5's power law
     with its cap raised): the heartbeat, fanout maintenance and fanout
     publication of hubs run one block per observer (BlockGroup), control
@@ -352,4 +356,45 @@ def test_hub_rows_bit_exact(require_gpu):
     und = und[und[:, 0] < und[:, 1]]
     down = und[rng.choice(len(und), size=len(und) // 50, replace=False)]
     churn = {3: [(down, False)], 5: [(down, True)]}
-    run_parity(net, params, th, gp, st, ticks, sched, ring=1024, churn=churn)
+    run_parity(net, params, th, gp, st, ticks, sched, ring=1024, churn=churn, topic_slots=topic_slots)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("topic_slots", [0, 24])
+def test_c5_combined_wide_hubs_zipf_churn_px_verdicts(require_gpu, topic_slots):
+    """C5's whole shape on one engine: a plain Chung-Lu
+    power law (exponent 2.5, i0 = 1) whose hubs exceed 1024 connections (up
+    to the 4096 cap: heartbeat, fanout and PX on 4 row positions per thread),
+    64 topics with Zipf subscriptions, dense meshes on the hubs (Dhi prune
+    ranks over thousands of positions), churn, peer exchange with the
+    connector, every validation verdict, fanout publishers outside their
+    topics, and (topic_slots) per-topic sub-rings with member-compacted
+    seen-set cells.  Bit-exact against the oracle every tick."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim import graphs
+    from tickrun import restrict_to_subscriptions, run_parity, subscribed_schedule
+    rng = np.random.default_rng(3131)
+    n, T = 20000, 64
+    net = graphs.power_law(n, 16, 2.5, 4096, seed=31, n_topics=T, i0=1)
+    net = graphs.with_subscriptions(net, graphs.zipf_subscriptions(n, T, 8, seed=32))
+    deg = np.diff(net.row_ptr.astype(np.int64))
+    assert (deg > 1024).sum() >= 3 and deg.max() <= 4096, "hub rows above 1024 connections"
+    params = beacon_params(T, RetainScore=3 * Second)
+    th = PeerScoreThresholds(GossipThreshold=-20, PublishThreshold=-40, GraylistThreshold=-300,
+                             AcceptPXThreshold=0.0, OpportunisticGraftThreshold=5)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2, FanoutTTL=3 * Second, OpportunisticGraftTicks=3,
+                         PeerExchange=True)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 0.3)
+    restrict_to_subscriptions(st, net)
+    ticks = list(range(1, 6))
+    sched = subscribed_schedule(rng, ticks, net, T, 0.6, 0.0, member_only=False,
+                                verdicts=[0.9, 0.04, 0.03, 0.02, 0.01])
+    src = net.owner()
+    und = np.stack([src, net.col], axis=1)
+    und = und[und[:, 0] < und[:, 1]]
+    down = und[rng.choice(len(und), size=len(und) // 100, replace=False)]
+    churn = {2: [(down, False)], 4: [(down, True)]}
+    log = []
+    run_parity(net, params, th, gp, st, ticks, sched, ring=2048, churn=churn, px_log=log, topic_slots=topic_slots)
+    assert sum(log) > 0, "PX made connections"

@@ -132,3 +132,23 @@ def test_network_oracle_matches_pinned_structures():
     assert seen[ob.EV_HEARTBEAT] == 10 and seen[ob.EV_GOSSIP_ID] > 0
     assert seen[ob.EV_SERVE] > 0 and seen[ob.EV_PROMISE] > 0 and seen[ob.EV_BROKEN] > 0
     assert seen[ob.EV_SEEN] > seen[ob.EV_PUT] > 0
+
+
+def test_topic_subrings_assign_slots_in_publication_order():
+    """gsim_msg_config.topic_slots: topic t's messages take slots
+    t * topic_slots + (earlier messages of t mod topic_slots), whatever their
+    ids; the seen-set rows of a slot start unseen except at the origin."""
+    from fixtures import beacon_params
+    from gsim.engine import random_regular
+    n, T, R_t = 200, 3, 4
+    net = random_regular(n, 8, seed=3, n_topics=T)
+    st = ob.NetState(net, beacon_params(T), gossip=GossipSubParams(D=4, Dlo=3, Dhi=6))
+    msgs = ob.Msgs(n, T, T * R_t, R, T0, Second, topic_slots=R_t)
+    order = [(101, 1, 5), (7, 1, 9), (55, 0, 11), (3, 2, 13), (8, 1, 17), (9, 1, 19), (10, 1, 21)]
+    for g, (mid, t, o) in enumerate(order):
+        msgs.publish(st, mid, t, o, 0, g)
+    # topic 1 took 1*4+0, +1, +2, +3, then wrapped to 1*4+0
+    assert list(msgs.mid[4:8]) == [10, 7, 8, 9]
+    assert msgs.mid[0] == 55 and msgs.mid[8] == 3
+    assert list(msgs.topic) == [0] * 4 + [1] * 4 + [2] * 4
+    assert msgs.seen[4, 21] == 6 and (msgs.seen[4] != ob.UNSEEN).sum() == 1

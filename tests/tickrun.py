@@ -61,7 +61,7 @@ def oracle_trace(ev, msgs, lo, hi):
 
 
 def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, churn=None, after_tick=None,
-               eng=None, after_heartbeat=None, px_log=None, trace=None, trace_log=None):
+               eng=None, after_heartbeat=None, px_log=None, trace=None, trace_log=None, topic_slots=0):
     """Run `ticks` on a fresh engine loaded with `st`'s state and on the
     oracle; assert identical state, seen-set and totals after every tick.
     churn: {tick: [(pairs, up), ...]} applied just before the tick.
@@ -71,7 +71,9 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
     tick on both sides and the connections made must agree (appended to
     px_log when given).  trace=(lo, hi): the engine traces routers [lo, hi)
     and its events must equal the oracle's event log per tick (the event
-    counts appended to trace_log)."""
+    counts appended to trace_log).  topic_slots > 0: per-topic sub-rings of
+    that many slots (ring = T * topic_slots) with member-compacted seen-set
+    cells (gsim_msg_config.topic_slots), on both sides."""
     from gsim.engine import Engine
     pushed = eng is None
     if eng is None:
@@ -81,8 +83,10 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
             eng.load_graph(net)
             eng.set_seed(SEED)
             st.push_to_engine(eng)
-        eng.msgs_init(ring, R, T0, Second)
-        msgs = ob.Msgs(net.n, st.T, ring, R, T0, Second, behaviour=behaviour)
+        if topic_slots:
+            ring = st.T * topic_slots
+        eng.msgs_init(ring, R, T0, Second, topic_slots=topic_slots)
+        msgs = ob.Msgs(net.n, st.T, ring, R, T0, Second, behaviour=behaviour, topic_slots=topic_slots)
         if trace is not None:
             eng.trace_config(trace[0], trace[1], 1 << 22)
             msgs.log()
