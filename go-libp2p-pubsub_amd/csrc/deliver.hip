@@ -93,6 +93,7 @@ struct Deliver {
     uint32_t* d_mpre = nullptr;        // [T][nw] members before each word
     uint64_t sparse = 0;               // topics with member-compacted cells (Cells::sparse)
     int64_t cell_nw = 0;               // words per topic of the member bitmaps
+    int64_t n_peers = 0;               // peers the cells were laid out for
     std::vector<int64_t> tcount;       // [T] messages published per topic (sub-ring slot choice)
     uint32_t* d_pslot = nullptr;       // [pub_cap] ring slots of a publish batch
     uint64_t* d_seenbm = nullptr;      // [ring][ceil(N/64)] bit: the cell is committed (a cache of the cells)
@@ -299,7 +300,7 @@ __device__ __forceinline__ int active_slots(const uint32_t* nnew, int ring, uint
 
 // Commit one claimed cell of round gc (markSeen + the winner's P2/P3 credit,
 // markFirstMessageDelivery score.go:919-946; mcache.Put for lastput).
-template <bool ATOMIC = false, bool LAT = false>
+template <bool ATOMIC = false, bool LAT = false, bool SP = true>
 __device__ __forceinline__ void commit_claim(const RoundArgs& a, uint64_t* cellp, uint64_t c, int64_t gc,
                                              uint32_t m, int64_t peer, int* qpl = nullptr, uint64_t* qv = nullptr)
 {
@@ -332,7 +333,8 @@ __device__ __forceinline__ void commit_claim(const RoundArgs& a, uint64_t* cellp
     if (!(lo & kCreditFirst)) return;
     const ctp_t tp = const_tp(a.tp) + t;
     // the winner's record sits at its edge, in the sender's row (its topic slot)
-    const int64_t ir = slot_idx(smask_of(a.smask, lo & kPeerMask), t, a.E, hi & kEdgeMask);
+    const int64_t ir = SP ? slot_idx(smask_of(a.smask, lo & kPeerMask), t, a.E, hi & kEdgeMask)
+                          : (int64_t)t * a.E + (hi & kEdgeMask);
     const double cap = tp->first_message_deliveries_cap;
     if (ATOMIC) {
         atomic_inc_capped(&a.first[ir], cap);
@@ -348,8 +350,11 @@ __device__ __forceinline__ void commit_claim(const RoundArgs& a, uint64_t* cellp
 // Cell index of lane `lane` of the 64-peer word w in slot m (gsim_internal.h
 // Cells): every lane of a wave asks for the same (m, w), so the slot's base
 // and the topic's member word are wave-uniform loads; -1: no cell.
+// SP = false: the dense layout (no sparse topic), m * n + p without a read.
+template <bool SP>
 __device__ __forceinline__ int64_t word_cell(const Cells& c, const uint32_t* mtopic, uint32_t m, int64_t w, int lane)
 {
+    if (!SP || !c.sparse) return (int64_t)m * c.n + w * 64 + lane;
     uint64_t bits;
     int64_t pre;
     c.word((int32_t)mtopic[m], w, bits, pre);
@@ -510,7 +515,9 @@ constexpr int kTsSlots = 64;
 constexpr uint32_t kTmWin = 8192;   // flattened edges whose senders are tabled in LDS at once
 constexpr int kTmTabMin = 256;      // forwarders in a chunk from which the table pays for its fill
 
-template <int kTmThreads, bool LAT>
+// SP: topic slots or member-compacted cells are in use (gsim_internal.h); the
+// dense instance indexes plane t and cell m * N + p with no table reads.
+template <int kTmThreads, bool LAT, bool SP>
 __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs a)
 {
     extern __shared__ uint64_t s_dyn[];
@@ -627,10 +634,10 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                     if ((fb >> u) & 1u) {
                         k2[u] = (uint32_t)__builtin_ctzll(pm[u]);
                         const uint32_t x = (uint32_t)(x0 + u), m = s_m[k2[u]];
-                        const int64_t xc = a.cs.at((int64_t)s_cb[k2[u]], t, x);   // a forwarder's cell (committed)
+                        // a forwarder's cell (committed)
+                        const int64_t xc = SP ? a.cs.at((int64_t)s_cb[k2[u]], t, x) : (int64_t)m * a.cs.n + x;
                         from2[u] = xc >= 0 ? (uint32_t)a.cs.cell[xc] & kPeerMask : kPeerMask;
-                        (void)m;
-                        const uint64_t xm = smask_of(a.smask, x);
+                        const uint64_t xm = SP ? smask_of(a.smask, x) : ~0ull;
                         pl2[u] = (uint32_t)__popcll(xm & ((1ull << t) - 1ull));
                         const uint32_t rb = a.row_ptr[x], deg = a.row_ptr[x + 1] - rb;
                         if (!slot_has(xm, t)) {
@@ -736,7 +743,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             jv[u] = vv[u] ? s_front[q] : 0u;
                             fv[u] = vv[u] ? s_from[q] : 0u;
                             kv[u] = vv[u] ? s_sk[q] : 0u;
-                            pv[u] = vv[u] ? (int64_t)s_pl[q] * a.E : 0;
+                            pv[u] = !vv[u] ? 0 : (SP && a.smask) ? (int64_t)s_pl[q] * a.E : (int64_t)t * a.E;
                             const uint32_t k = fi - s_off[q];
                             const uint64_t msk = s_msk[q];
                             mk[u] = msk != 0;
@@ -801,8 +808,8 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                                                   : (s_wa[k] || !sc || inv || !(tf & GSIM_TF_IN_MESH)));
                             // the receiver's cell (a member of t: mesh, direct, fanout and flood
                             // targets all hold the topic, §2); -1 cannot happen
-                            const int64_t ci = known ? 0 : a.cs.at((int64_t)s_cb[k], t, i);
-                            if (ci < 0) continue;
+                            const int64_t ci = known ? 0 : SP ? a.cs.at((int64_t)s_cb[k], t, i) : (int64_t)m * a.cs.n + i;
+                            if (SP && ci < 0) continue;
                             const uint64_t c = known ? 0ull : a.cs.cell[ci];
                             const uint32_t chi = (uint32_t)(c >> 32);
                             // the round validation completed (or completes) in; -1: unclaimed
@@ -895,7 +902,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
 
 // Commit every claim of round g (markSeen + P2 credit) before the state is
 // read or changed by anything but the next round.
-template <bool LAT>
+template <bool LAT, bool SP>
 __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
 {
     extern __shared__ uint16_t s_act[];
@@ -910,14 +917,14 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
     const uint32_t par = (uint32_t)(a.g & 1);
     for (int k0 = 0; k0 < nact; k0 += kSlotBatch) {
         uint64_t cv[kSlotBatch];
-        int64_t ci[kSlotBatch];
+        int64_t ci[SP ? kSlotBatch : 1];   // the dense layout recomputes m * N + i
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
-            ci[b] = (k < nact && vi) ? word_cell(a.cs, a.mtopic, s_act[k], i0 >> 6, lane) : -1;
+            const int64_t c = (k < nact && vi) ? word_cell<SP>(a.cs, a.mtopic, s_act[k], i0 >> 6, lane) : -1;
+            if constexpr (SP) ci[b] = c;
+            cv[b] = c >= 0 ? a.cs.cell[c] : kUnseen64;
         }
-#pragma unroll
-        for (int b = 0; b < kSlotBatch; ++b) cv[b] = ci[b] >= 0 ? a.cs.cell[ci[b]] : kUnseen64;
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
@@ -942,7 +949,8 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
             uint64_t qv = 0;
             if (is_claim_of(cv[b], par)) {
                 const uint32_t m = s_act[k];
-                commit_claim<false, LAT>(a, a.cs.cell + ci[b], cv[b], a.g, m, i, &qpl, &qv);
+                uint64_t* cp = a.cs.cell + (SP ? ci[b] : (int64_t)m * a.cs.n + i);
+                commit_claim<false, LAT, SP>(a, cp, cv[b], a.g, m, i, &qpl, &qv);
             }
             if constexpr (LAT) vq_push_wave(a, qpl, qv);
         }
@@ -1040,7 +1048,7 @@ __device__ __forceinline__ bool holds_in_window(uint64_t c, int64_t g, int32_t l
     return fr >= lo_round && fr < tick_round && (!inv || is_origin);
 }
 
-template <bool LAT>
+template <bool LAT, bool SP>
 __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount)
 {
     extern __shared__ uint16_t s_act[];   // [ring] candidate slots, then [2][ring] u32 counters
@@ -1076,7 +1084,7 @@ __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
             // a peer without a cell (not a member of the slot's topic) has not seen it
-            const int64_t ci = (k < nact && vp) ? word_cell(a.cs, a.mtopic, s_act[k], p0 >> 6, lane) : -1;
+            const int64_t ci = (k < nact && vp) ? word_cell<SP>(a.cs, a.mtopic, s_act[k], p0 >> 6, lane) : -1;
             cv[b] = ci >= 0 ? a.cs.cell[ci] : kUnseen64;
         }
 #pragma unroll
@@ -1098,7 +1106,7 @@ __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount
         if (s_cnt[w]) atomicAdd(&gcount[w], s_cnt[w]);
 }
 
-template <int W, bool LAT>
+template <int W, bool LAT, bool SP>
 __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
 {
     extern __shared__ uint16_t s_act[];   // [ring] candidate slots (bit 15: push), then response staging
@@ -1155,7 +1163,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
-            const int64_t ci = (k < nact && vp) ? word_cell(a.cs, a.mtopic, s_act[k] & 0x7FFF, p0 >> 6, lane) : -1;
+            const int64_t ci = (k < nact && vp) ? word_cell<SP>(a.cs, a.mtopic, s_act[k] & 0x7FFF, p0 >> 6, lane) : -1;
             cv[b] = ci >= 0 ? a.cs.cell[ci] : kUnseen64;   // no cell: not a member, nothing held or wanted
         }
 #pragma unroll
@@ -1692,7 +1700,7 @@ __global__ __launch_bounds__(256) void k_vcomplete(RoundArgs a, const uint32_t* 
     const int32_t tick = (int32_t)(a.g / a.R);
     for (int k = 0; k < nact; ++k) {
         const uint32_t m = s_act[k];
-        const int64_t ci = vi ? word_cell(a.cs, a.mtopic, m, i0 >> 6, lane) : -1;
+        const int64_t ci = vi ? word_cell<true>(a.cs, a.mtopic, m, i0 >> 6, lane) : -1;
         const uint64_t c = ci >= 0 ? a.cs.cell[ci] : kUnseen64;
         const bool done = c != kUnseen64 && !((uint32_t)(c >> 32) & kClaim) && (int64_t)(c >> 32) == a.g;
         const uint64_t b = __ballot(done);
@@ -1766,6 +1774,13 @@ static int grid_peers(int64_t n)
 }
 
 
+// Topic slots or member-compacted cells in use: the kernels' table-reading
+// instances (SP = true); a dense layout runs the ones that index directly.
+static bool sparse_layout(const gsim_handle* h)
+{
+    return h->d_smask != nullptr || (h->dl && h->dl->sparse != 0);
+}
+
 static Cells deliver_cells(const Deliver* d)
 {
     Cells c;
@@ -1774,6 +1789,7 @@ static Cells deliver_cells(const Deliver* d)
     c.mbits = d->d_mbits;
     c.mpre = d->d_mpre;
     c.nw = d->cell_nw;
+    c.n = d->cell_nw ? d->n_peers : 0;
     c.sparse = d->sparse;
     return c;
 }
@@ -1953,9 +1969,11 @@ static int ihave_count(gsim_handle* h, IhaveStage* st)
 {
     ProfScope ps(h, GSIM_K_GOSSIP);
     if (st->a.mlat)
-        hipLaunchKernelGGL(k_gossip_count<true>, dim3(st->grid), dim3(256), st->lds_c, h->stream, st->a, h->dl->d_gcount);
+        hipLaunchKernelGGL((k_gossip_count<true, true>), dim3(st->grid), dim3(256), st->lds_c, h->stream, st->a, h->dl->d_gcount);
+    else if (sparse_layout(h))
+        hipLaunchKernelGGL((k_gossip_count<false, true>), dim3(st->grid), dim3(256), st->lds_c, h->stream, st->a, h->dl->d_gcount);
     else
-        hipLaunchKernelGGL(k_gossip_count<false>, dim3(st->grid), dim3(256), st->lds_c, h->stream, st->a, h->dl->d_gcount);
+        hipLaunchKernelGGL((k_gossip_count<false, false>), dim3(st->grid), dim3(256), st->lds_c, h->stream, st->a, h->dl->d_gcount);
     return hip_check(h, hipGetLastError(), "k_gossip_count");
 }
 
@@ -1963,9 +1981,11 @@ template <int W>
 static void launch_ihave_w(gsim_handle* h, IhaveStage* st, const IhArgs& a)
 {
     if (a.mlat)
-        hipLaunchKernelGGL((k_ihave<W, true>), dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)h->dl->d_gcount);
+        hipLaunchKernelGGL((k_ihave<W, true, true>), dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)h->dl->d_gcount);
+    else if (sparse_layout(h))
+        hipLaunchKernelGGL((k_ihave<W, false, true>), dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)h->dl->d_gcount);
     else
-        hipLaunchKernelGGL((k_ihave<W, false>), dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)h->dl->d_gcount);
+        hipLaunchKernelGGL((k_ihave<W, false, false>), dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)h->dl->d_gcount);
 }
 
 static int ihave_walk(gsim_handle* h, IhaveStage* st)
@@ -2019,9 +2039,11 @@ int deliver_flush(gsim_handle* h)
     RoundArgs a = make_round_args(h, d->pending);
     const dim3 grid(grid_peers((int64_t)a.rhi - ((int64_t)a.rlo & ~63ll)));
     if (a.mlat)
-        hipLaunchKernelGGL(k_commit<true>, grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
+        hipLaunchKernelGGL((k_commit<true, true>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
+    else if (sparse_layout(h))
+        hipLaunchKernelGGL((k_commit<false, true>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     else
-        hipLaunchKernelGGL(k_commit<false>, grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
+        hipLaunchKernelGGL((k_commit<false, false>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     d->pending = -1;
     return hip_check(h, hipGetLastError(), "k_commit");
 }
@@ -2141,9 +2163,11 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a)
     // the slot list in LDS
     const size_t lds = ((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7;
     if (a.mlat)
-        hipLaunchKernelGGL((k_send_tm<TB, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<TB, true, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+    else if (sparse_layout(h))
+        hipLaunchKernelGGL((k_send_tm<TB, false, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
     else
-        hipLaunchKernelGGL((k_send_tm<TB, false>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<TB, false, false>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_send_tm");
 }
 
@@ -2523,6 +2547,7 @@ static hipError_t install_layout(gsim_handle* h, Deliver* d, const CellLayout& L
     d->cbase = L.cbase;
     d->sparse = L.sparse;
     d->cell_nw = (h->n + 63) / 64;
+    d->n_peers = h->n;
     d->n_cells = L.cells;
     return e;
 }

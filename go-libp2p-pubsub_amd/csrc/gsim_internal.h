@@ -237,7 +237,9 @@ struct Cells {
     const uint64_t* mbits = nullptr;   // [T][nw] member bits of each topic (sparse topics)
     const uint32_t* mpre = nullptr;    // [T][nw] members in the topic's earlier words
     int64_t nw = 0;                    // words per topic, ceil(N / 64)
+    int64_t n = 0;                     // peers
     uint64_t sparse = 0;               // topics whose slots hold member-compacted cells
+    // (no sparse topic: every slot holds a cell per peer at m * n + p, no table read)
     // word w of topic t: its member bits and the cell offset of its first member
     __device__ __forceinline__ void word(int32_t t, int64_t w, uint64_t& bits, int64_t& pre) const
     {
@@ -253,6 +255,7 @@ struct Cells {
     // cell index of peer p in slot m (topic t) whose cells start at base; -1: p has none
     __device__ __forceinline__ int64_t at(int64_t base, int32_t t, uint32_t p) const
     {
+        if (!((sparse >> t) & 1ull)) return base + p;
         uint64_t b;
         int64_t pre;
         word(t, (int64_t)(p >> 6), b, pre);
@@ -262,6 +265,7 @@ struct Cells {
     }
     __device__ __forceinline__ int64_t idx(uint32_t m, int32_t t, uint32_t p) const
     {
+        if (!sparse) return (int64_t)m * n + p;
         return at((int64_t)cbase[m], t, p);
     }
     __device__ __forceinline__ uint64_t get(uint32_t m, int32_t t, uint32_t p) const

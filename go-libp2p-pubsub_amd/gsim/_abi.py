@@ -308,7 +308,10 @@ def load(path: str | None = None) -> ctypes.CDLL:
     except Exception:  # pragma: no cover - torch is present in this image
         pass
     lib = ctypes.CDLL(p)
+    older = p != LIB_PATH                                    # an A/B build may predate newer entry points
     for name, res, args in SIGNATURES:
+        if older and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
