@@ -103,6 +103,10 @@ struct Deliver {
     uint64_t mask_version = 0;         // h->mesh_version the masks were built for
     uint32_t* d_tmtab = nullptr;       // k_send_tm blocks: [T+1] first block of each topic, [T] its range
     std::vector<uint32_t> tmtab;       // host copy (the upload's source)
+    uint32_t* d_tmmap = nullptr;       // [tm_grid] logical k_send_tm block of each launched block (XCD placement)
+    std::vector<uint32_t> tmmap;       // host copy
+    int64_t tmmap_cap = 0;
+    uint32_t tm_grid = 0;              // blocks launched
     int64_t tm_cn = -1;                // peers the table was built for
     int32_t* d_mpub = nullptr;         // [ring] round the slot's message was published in
     int64_t* d_roff = nullptr;         // [rounds] offset of each round in its heartbeat
@@ -195,6 +199,7 @@ struct RoundArgs {
     // on no other edge, so only these are walked
     const uint64_t* mmask;
     const uint32_t* tmtab;         // k_send_tm blocks per topic (Deliver::d_tmtab)
+    const uint32_t* tmmap;         // launched block -> logical block (nullptr: the same; ~0: idle)
     uint8_t* peertx;               // [ring][ptx_w] GetForPeer counts (Deliver::d_peertx), zeroed on reuse
     int32_t ptx_w;
     TraceRef tr;                   // gsim_trace_config
@@ -541,17 +546,23 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
     __shared__ uint32_t s_ne;
     __shared__ unsigned long long s_clm;                     // slots of the pass with a new claim
     __shared__ unsigned long long s_stats[4];
+    // XCD placement (launch_send_tm): the hardware deals blocks out to the 8
+    // XCDs round-robin, so launched block b runs on XCD b % 8; the map gives
+    // every block of a topic the same XCD, and the topic's slot bitmaps and
+    // cells stay in that XCD's L2
+    const uint32_t lb = a.tmmap ? a.tmmap[blockIdx.x] : blockIdx.x;
+    if (lb == 0xFFFFFFFFu) return;                               // padding of a shorter XCD list
     int32_t t = 0;
     {
         int32_t r = a.T > 0 ? a.T : 1;
         while (r - t > 1) {
             const int32_t mid = (t + r) >> 1;
-            if (a.tmtab[mid] <= blockIdx.x) t = mid; else r = mid;
+            if (a.tmtab[mid] <= lb) t = mid; else r = mid;
         }
     }
     const int64_t range = a.tmtab[(a.T > 0 ? a.T : 1) + 1 + t];
     const int64_t pend_ = a.CN;
-    const int64_t lo = (int64_t)(blockIdx.x - a.tmtab[t]) * range;
+    const int64_t lo = (int64_t)(lb - a.tmtab[t]) * range;
     const int64_t hi = lo + range < pend_ ? lo + range : pend_;
     const int64_t wlo = (int64_t)a.rlo >> 6;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1740,7 +1751,7 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_tmmap); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_peertx); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
@@ -1819,6 +1830,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.fsum = d->d_fsum;
     a.mmask = d->d_mmask;
     a.tmtab = d->d_tmtab;
+    a.tmmap = nullptr;
     a.peertx = d->d_peertx; a.ptx_w = d->ptx_w;
     a.tr = h->trace;
     a.nsw = (a.nw + 63) / 64;
@@ -2116,7 +2128,7 @@ int deliver_read_seen(gsim_handle* h, void* dst)
     return hip_check(h, e, "gsim_read_field(SEEN)");
 }
 
-static int launch_send_tm(gsim_handle* h, const RoundArgs& a)
+static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
 {
     // blocks per topic: about 2048 blocks in all (8 per CU over the launch at one
     // resident block per CU: smaller ranges even out the frontier work; measured
@@ -2158,16 +2170,53 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a)
         hipError_t e = hipMemcpyAsync(d->d_tmtab, d->tmtab.data(), d->tmtab.size() * 4, hipMemcpyHostToDevice,
                                       h->stream);
         if (e != hipSuccess) return hip_check(h, e, "k_send_tm block table");
+        // XCD placement: topics to the 8 XCDs, largest block count first onto
+        // the least loaded; launched block 8 j + x runs the j-th block of XCD
+        // x's list (the lists padded with idle blocks to the longest)
+        d->tm_grid = start;
+        if (h->tm_xcd && T > 1) {
+            constexpr int kXcd = 8;           // MI355X: 8 XCDs, each with its own L2
+            std::vector<int> order((size_t)T);
+            for (int t = 0; t < T; ++t) order[(size_t)t] = t;
+            auto nb = [&](int t) { return d->tmtab[(size_t)t + 1] - d->tmtab[(size_t)t]; };
+            std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return nb(x) > nb(y); });
+            std::vector<std::vector<uint32_t>> lists(kXcd);
+            std::vector<uint64_t> load(kXcd, 0);
+            for (int t : order) {
+                const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+                for (uint32_t b = d->tmtab[(size_t)t]; b < d->tmtab[(size_t)t + 1]; ++b) lists[(size_t)x].push_back(b);
+                load[(size_t)x] += nb(t);
+            }
+            size_t longest = 0;
+            for (const auto& l : lists) longest = std::max(longest, l.size());
+            std::vector<uint32_t>& map = d->tmmap;
+            map.assign(longest * kXcd, 0xFFFFFFFFu);
+            for (int x = 0; x < kXcd; ++x)
+                for (size_t j = 0; j < lists[(size_t)x].size(); ++j) map[j * kXcd + (size_t)x] = lists[(size_t)x][j];
+            if ((int64_t)map.size() > d->tmmap_cap) {
+                if (d->d_tmmap) (void)hipFree(d->d_tmmap);
+                d->d_tmmap = nullptr;
+                d->tmmap_cap = 0;
+                e = hipMalloc((void**)&d->d_tmmap, map.size() * 4);
+                if (e != hipSuccess) return hip_check(h, e, "k_send_tm block map");
+                d->tmmap_cap = (int64_t)map.size();
+            }
+            e = hipMemcpyAsync(d->d_tmmap, map.data(), map.size() * 4, hipMemcpyHostToDevice, h->stream);
+            if (e != hipSuccess) return hip_check(h, e, "k_send_tm block map");
+            d->tm_grid = (uint32_t)map.size();
+        }
         d->tm_cn = cn;
     }
+    RoundArgs a = a0;
+    a.tmmap = h->tm_xcd && T > 1 ? d->d_tmmap : nullptr;
     // the slot list in LDS
     const size_t lds = ((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7;
     if (a.mlat)
-        hipLaunchKernelGGL((k_send_tm<TB, true, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<TB, true, true>), dim3(d->tm_grid), dim3(TB), lds, h->stream, a);
     else if (sparse_layout(h))
-        hipLaunchKernelGGL((k_send_tm<TB, false, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<TB, false, true>), dim3(d->tm_grid), dim3(TB), lds, h->stream, a);
     else
-        hipLaunchKernelGGL((k_send_tm<TB, false, false>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<TB, false, false>), dim3(d->tm_grid), dim3(TB), lds, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_send_tm");
 }
 

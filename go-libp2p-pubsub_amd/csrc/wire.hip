@@ -67,7 +67,9 @@ struct WireArgs {
     uint32_t* rcnt;               // [edges + 1]
     uint8_t* out;
     gsim_wire_ref* refs;
-    uint32_t* err;                // [0] an IHAVE target without ids
+    int32_t max_ihave;            // MaxIHaveLength
+    uint32_t* err;                // [0] bit 0: an IHAVE target without ids; bit 1: a window longer than
+                                  // MaxIHaveLength; bit 2: a PRUNE carrying peer exchange
 };
 
 __device__ __forceinline__ uint32_t vlen(uint64_t v)
@@ -123,6 +125,9 @@ __global__ void k_wire_ids_count(WireArgs a)
     if (any) {
         for (int32_t q = a.cand_ptr[t]; q < a.cand_ptr[t + 1]; ++q) cnt += window_put(a, a.cand[q], p) >= 0;
         if (!cnt) atomicOr(&a.err[0], 1u);                   // emitGossip has nothing to send
+        // emitGossip would send each target its own random MaxIHaveLength-subset
+        // (gossipsub.go:1763-1772), which is not encoded here
+        if (cnt > (uint64_t)a.max_ihave) atomicOr(&a.err[0], 2u);
     }
     a.n_pt[k] = cnt;
 }
@@ -156,6 +161,8 @@ __device__ uint64_t control_body(const WireArgs& a, int64_t e, uint32_t p, bool*
         if (gsel_at(a, t, e, mp)) { s += ld(ihave_body(a, t, (uint32_t)a.n_pt[base + t])); x = true; }
         if (c & GSIM_CTL_GRAFT) { s += ld(name_field(a, t)); x = true; }
         if (c & GSIM_CTL_PRUNE) { s += ld(prune_body(a, t)); x = true; }
+        // makePrune's PX peer list (gossipsub.go:1878-1903) is not kept per PRUNE
+        if ((c & GSIM_CTL_PRUNE) && (c & GSIM_CTL_PX)) atomicOr(&a.err[0], 4u);
     }
     *any = x;
     return s;
@@ -430,6 +437,7 @@ extern "C" int gsim_wire_heartbeat(gsim_handle* h, int64_t tick, uint32_t p0, ui
     a.names = d_names; a.name_off = d_name_off;
     a.peer_ids = d_pid; a.pid_len = names->peer_id_len;
     a.backoff = names->prune_backoff_s;
+    a.max_ihave = h->gp.max_ihave_length;
     a.out = d_out; a.refs = d_refs;
     if (!a.ctl) return finish(GSIM_ESTATE);
 
@@ -450,8 +458,16 @@ extern "C" int gsim_wire_heartbeat(gsim_handle* h, int64_t tick, uint32_t p0, ui
     if (he == hipSuccess) he = hipMemcpyAsync(&err, a.err, 4, hipMemcpyDeviceToHost, h->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(h->stream);
     if (he != hipSuccess) return finish(hip_check(h, he, "wire totals"));
-    if (err) {
+    if (err & 1u) {
         h->err = "an IHAVE target without message ids in the gossip window";
+        return finish(GSIM_ESTATE);
+    }
+    if (err & 2u) {
+        h->err = "a gossip window holds more than MaxIHaveLength ids: emitGossip's per-target subsets are not encoded";
+        return finish(GSIM_ESTATE);
+    }
+    if (err & 4u) {
+        h->err = "a PRUNE carries peer exchange: its PX peer list is not encoded";
         return finish(GSIM_ESTATE);
     }
     *n_rpcs = tot_rpcs;

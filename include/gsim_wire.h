@@ -138,7 +138,10 @@ typedef struct gsim_wire_ref {
  *     DefaultMsgIdFn, pubsub.go: from + seqno), else seqno alone;
  *     the seqno is the gsim_msg id as 8 big-endian bytes;
  *   prune_backoff_s: ControlPrune.Backoff (PruneBackoff / 1s, gossipsub.go:1872).
- * PX peer lists are not emitted (the default router has doPX off). */
+ * Not encoded, refused instead: a PRUNE that carries peer exchange (doPX,
+ * makePrune gossipsub.go:1878-1903: its PX list is not kept per PRUNE) ->
+ * GSIM_ESTATE; a gossip window of more than MaxIHaveLength ids (emitGossip's
+ * per-target random subsets, 1763-1772) -> GSIM_ESTATE. */
 typedef struct gsim_wire_names {
     const gsim_bytes* topic_names;
     const uint8_t* peer_ids;

@@ -314,3 +314,47 @@ def test_heartbeat_rpcs_match_oracle(require_gpu, with_peer_ids):
         for m in state["mc"] or []:
             lib.orc_mcache_free(m)
     assert state["checked"] > 200
+
+
+@pytest.mark.gpu
+def test_heartbeat_rpcs_refuse_what_they_cannot_encode(require_gpu):
+    """Two heartbeat outputs the device encoder does not hold per RPC are
+    refused rather than encoded wrongly: emitGossip's per-target random
+    MaxIHaveLength-subsets (gossipsub.go:1763-1772: a window longer than
+    MaxIHaveLength) and makePrune's PX peer lists (1878-1903)."""
+    import oracle_binding as ob
+    from fixtures import beacon_params, synthetic_state
+    from gsim.engine import random_regular
+    from gsim.params import GossipSubParams, PeerScoreThresholds, Second
+    from test_heartbeat import tick_time
+    from tickrun import run_parity, subscribed_schedule
+    n, k, T = 400, 16, 2
+    names = [f"t{t}".encode() for t in range(T)]
+    th = PeerScoreThresholds(GossipThreshold=-50, PublishThreshold=-100, GraylistThreshold=-300)
+    params = beacon_params(T)
+    for case in ("window", "px"):
+        rng = np.random.default_rng(7)
+        if case == "window":
+            gp = GossipSubParams(D=6, Dlo=5, Dhi=10, Dscore=3, Dout=2, MaxIHaveLength=2)
+            rate, p_mesh = 8.0, 6 / k
+        else:
+            gp = GossipSubParams(D=6, Dlo=5, Dhi=10, Dscore=3, Dout=2, PeerExchange=True)
+            rate, p_mesh = 2.0, 14 / k          # meshes above Dhi: the heartbeat prunes with PX
+        net = random_regular(n, k, seed=33, n_topics=T)
+        st = ob.NetState(net, params, thresholds=th, gossip=gp)
+        synthetic_state(st, rng, tick_time(0), p_mesh)
+        ticks = [1, 2, 3]
+        sched = subscribed_schedule(rng, ticks, net, T, rate, 0.0)
+        seen = {"refused": 0}
+
+        def after_heartbeat(kk, eng, st_, msgs):
+            if kk < 2:
+                return
+            with pytest.raises(wire.WireError) as ex:
+                wire.heartbeat_rpcs(eng, kk, 0, n, names, prune_backoff_s=int(gp.PruneBackoff // Second))
+            msg = str(ex.value)
+            assert ("MaxIHaveLength" in msg) if case == "window" else ("peer exchange" in msg), msg
+            seen["refused"] += 1
+
+        run_parity(net, params, th, gp, st, ticks, sched, ring=256, after_heartbeat=after_heartbeat)
+        assert seen["refused"] == 2, case
