@@ -345,10 +345,14 @@ def test_heartbeat_rpcs_refuse_what_they_cannot_encode(require_gpu):
         synthetic_state(st, rng, tick_time(0), p_mesh)
         ticks = [1, 2, 3]
         sched = subscribed_schedule(rng, ticks, net, T, rate, 0.0)
-        seen = {"refused": 0}
+        seen = {"refused": 0, "encoded": 0}
 
         def after_heartbeat(kk, eng, st_, msgs):
-            if kk < 2:
+            # the oracle's inbox says which PRUNEs carry PX (GSIM_CTL_PX, parity 0)
+            refuse = kk >= 2 if case == "window" else bool(((st_.ctl[0] & 0x04) != 0).any())
+            if not refuse:
+                wire.heartbeat_rpcs(eng, kk, 0, n, names, prune_backoff_s=int(gp.PruneBackoff // Second))
+                seen["encoded"] += 1
                 return
             with pytest.raises(wire.WireError) as ex:
                 wire.heartbeat_rpcs(eng, kk, 0, n, names, prune_backoff_s=int(gp.PruneBackoff // Second))
@@ -357,4 +361,4 @@ def test_heartbeat_rpcs_refuse_what_they_cannot_encode(require_gpu):
             seen["refused"] += 1
 
         run_parity(net, params, th, gp, st, ticks, sched, ring=256, after_heartbeat=after_heartbeat)
-        assert seen["refused"] == 2, case
+        assert seen["refused"] >= 1 and seen["encoded"] >= 1, (case, seen)
