@@ -96,6 +96,11 @@ struct Deliver {
     int64_t n_peers = 0;               // peers the cells were laid out for
     std::vector<int64_t> tcount;       // [T] messages published per topic (sub-ring slot choice)
     uint32_t* d_pslot = nullptr;       // [pub_cap] ring slots of a publish batch
+    // claim list (member-compacted cells): the cells a round claimed, so the
+    // commit touches those alone instead of every (active slot, peer word)
+    uint64_t* d_clist = nullptr;       // [clist_cap] receiver | slot << 32
+    uint32_t* d_clist_n = nullptr;     // [0] entries, [1] overflow (the commit then scans every word)
+    int64_t clist_cap = 0;
     uint64_t* d_seenbm = nullptr;      // [ring][ceil(N/64)] bit: the cell is committed (a cache of the cells)
     uint64_t* d_fresh = nullptr;       // [ring][ceil(N/64)] bit: the peer forwards the slot's message next round
     uint64_t* d_fsum = nullptr;        // [ring][ceil(N/4096)] bit: that fresh word may be non-zero
@@ -103,10 +108,6 @@ struct Deliver {
     uint64_t mask_version = 0;         // h->mesh_version the masks were built for
     uint32_t* d_tmtab = nullptr;       // k_send_tm blocks: [T+1] first block of each topic, [T] its range
     std::vector<uint32_t> tmtab;       // host copy (the upload's source)
-    uint32_t* d_tmmap = nullptr;       // [tm_grid] logical k_send_tm block of each launched block (XCD placement)
-    std::vector<uint32_t> tmmap;       // host copy
-    int64_t tmmap_cap = 0;
-    uint32_t tm_grid = 0;              // blocks launched
     int64_t tm_cn = -1;                // peers the table was built for
     int32_t* d_mpub = nullptr;         // [ring] round the slot's message was published in
     int64_t* d_roff = nullptr;         // [rounds] offset of each round in its heartbeat
@@ -199,10 +200,14 @@ struct RoundArgs {
     // on no other edge, so only these are walked
     const uint64_t* mmask;
     const uint32_t* tmtab;         // k_send_tm blocks per topic (Deliver::d_tmtab)
-    const uint32_t* tmmap;         // launched block -> logical block (nullptr: the same; ~0: idle)
     uint8_t* peertx;               // [ring][ptx_w] GetForPeer counts (Deliver::d_peertx), zeroed on reuse
     int32_t ptx_w;
     TraceRef tr;                   // gsim_trace_config
+    uint64_t* clist;               // claim list (Deliver::d_clist; nullptr: commits scan the words)
+    uint32_t* clist_n;
+    int64_t clist_cap;
+    int64_t ncells;                // cells of the seen-set (the last slot's end)
+    int32_t topic_slots;           // sub-rings: slots [t R, t R + R) carry topic t (0: one shared ring)
 };
 
 __device__ __forceinline__ int64_t round_time(const RoundArgs& a, int64_t g)
@@ -281,6 +286,23 @@ __device__ __forceinline__ void vq_push_wave(const RoundArgs& a, int pl, uint64_
 __device__ __forceinline__ uint64_t vq_entry(uint32_t e, int32_t t, uint32_t kind)
 {
     return (uint64_t)e | ((uint64_t)(uint32_t)t << 32) | ((uint64_t)kind << 40);
+}
+
+// Append the lanes' new claims (receiver | slot << 32) to the claim list,
+// one atomic per wave; every lane of the wave calls it.
+__device__ __forceinline__ void clist_push_wave(const RoundArgs& a, bool on, uint64_t v)
+{
+    const uint64_t b = __ballot(on);
+    if (!b) return;
+    const int lane = threadIdx.x & 63, leader = __builtin_ctzll(b);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(a.clist_n, (uint32_t)__popcll(b));
+    base = (uint32_t)__shfl((int)base, leader, 64);
+    if (on) {
+        const uint32_t k = base + (uint32_t)__popcll(b & ((1ull << lane) - 1));
+        if ((int64_t)k < a.clist_cap) a.clist[k] = v;
+        else atomicOr(&a.clist_n[1], 1u);
+    }
 }
 
 // Ordered list of the active slots (bit set in nnew), built by wave 0 into
@@ -384,39 +406,29 @@ __device__ __forceinline__ void fresh_set(const RoundArgs& a, uint32_t m, int64_
         atomicOr(reinterpret_cast<unsigned long long*>(sp), sb);
 }
 
-// Reset the rows of the slots being published into; a claim still pending
-// there (its message was propagating) is committed first.
+// Reset the cells and bitmaps of the slots being published into.  Every
+// claim is committed before (gsim_publish flushes the last round), so the
+// slot's cells — one contiguous range per slot — are simply made unseen.
 __global__ void k_reset_slots(RoundArgs a, const uint32_t* pslot, int32_t count)
 {
     const int k = blockIdx.y;
     if (k >= count) return;
     const uint32_t m = pslot[k];
-    const int32_t t = (int32_t)a.mtopic[m];             // the slot's previous message (a sub-ring: its topic)
-    const int64_t base = (int64_t)a.cs.cbase[m];
-    const uint32_t q = (uint32_t)((a.g - 1) & 1);
     // the previous message may still sit in a gossip window or a promise
     if (blockIdx.x == 0 && threadIdx.x == 0 && a.slot_last[m] >= 0 && a.g - a.slot_last[m] < a.reuse_guard)
         atomicOr(&a.err[2], 1u);
     if (blockIdx.x == 0 && a.peertx)
         for (int j = threadIdx.x; j < a.ptx_w; j += blockDim.x) a.peertx[(int64_t)m * a.ptx_w + j] = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.CN; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t ci = a.cs.at(base, t, (uint32_t)i);
-        if (ci >= 0) {
-            uint64_t* cp = a.cs.cell + ci;
-            const uint64_t c = *cp;
-            // several reused rows may credit one record: atomic updates here
-            if (a.g > 0 && is_claim_of(c, q)) {
-                if (a.mlat) commit_claim<true, true>(a, cp, c, a.g - 1, m, i);
-                else commit_claim<true>(a, cp, c, a.g - 1, m, i);
-            }
-            *cp = kUnseen64;
-        }
-        if ((i & 63) == 0) {
-            a.seenbm[(int64_t)m * a.nw + (i >> 6)] = 0;
-            if (a.fresh) a.fresh[(int64_t)m * a.nw + (i >> 6)] = 0;
-            if (a.fresh && (i & 4095) == 0) a.fsum[(int64_t)m * a.nsw + (i >> 12)] = 0;
-        }
+    const int64_t base = (int64_t)a.cs.cbase[m];
+    const int64_t end = (int64_t)m + 1 < a.ring ? (int64_t)a.cs.cbase[m + 1] : a.ncells;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t j = base + tid; j < end; j += stride) a.cs.cell[j] = kUnseen64;
+    for (int64_t w = tid; w < a.nw; w += stride) {
+        a.seenbm[(int64_t)m * a.nw + w] = 0;
+        if (a.fresh) a.fresh[(int64_t)m * a.nw + w] = 0;
     }
+    if (a.fresh)
+        for (int64_t w = tid; w < a.nsw; w += stride) a.fsum[(int64_t)m * a.nsw + w] = 0;
 }
 
 __global__ void k_publish(RoundArgs a, const gsim_msg* pub, const uint32_t* pslot, int32_t count)
@@ -546,12 +558,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
     __shared__ uint32_t s_ne;
     __shared__ unsigned long long s_clm;                     // slots of the pass with a new claim
     __shared__ unsigned long long s_stats[4];
-    // XCD placement (launch_send_tm): the hardware deals blocks out to the 8
-    // XCDs round-robin, so launched block b runs on XCD b % 8; the map gives
-    // every block of a topic the same XCD, and the topic's slot bitmaps and
-    // cells stay in that XCD's L2
-    const uint32_t lb = a.tmmap ? a.tmmap[blockIdx.x] : blockIdx.x;
-    if (lb == 0xFFFFFFFFu) return;                               // padding of a shorter XCD list
+    const uint32_t lb = blockIdx.x;
     int32_t t = 0;
     {
         int32_t r = a.T > 0 ? a.T : 1;
@@ -568,7 +575,10 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     if (tid == 0) { s_ns = 0; s_stats[0] = s_stats[1] = s_stats[2] = s_stats[3] = 0; }
     __syncthreads();
-    for (int m = tid; m < a.ring; m += kTmThreads) {
+    // a sub-ring (gsim_msg_config.topic_slots) holds topic t's slots alone
+    const int m_lo = a.topic_slots > 0 ? t * a.topic_slots : 0;
+    const int m_hi = a.topic_slots > 0 ? m_lo + a.topic_slots : a.ring;
+    for (int m = m_lo + tid; m < m_hi; m += kTmThreads) {
         if (((a.nnew_prev[m >> 5] >> (m & 31)) & 1u) && (int32_t)a.mtopic[m] == t) {
             const int q = atomicAdd(&s_ns, 1);
             s_slots[q] = (uint16_t)m;
@@ -779,8 +789,9 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                         }
                         int qpl[P];              // validation latency: queue plane of the copy (-1: none)
                         uint64_t qv[P];
+                        bool clw[P];             // the copy claimed an unseen cell (claim list)
 #pragma unroll
-                        for (int u = 0; u < P; ++u) { qpl[u] = -1; qv[u] = 0; }
+                        for (int u = 0; u < P; ++u) { qpl[u] = -1; qv[u] = 0; clw[u] = false; }
 #pragma unroll
                         for (int u = 0; u < P; ++u) {
                             const uint32_t j = jv[u], e = ev[u], i = iv[u], k = kv[u];
@@ -840,7 +851,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                                 const uint64_t cv = ((uint64_t)(claim_hi | e) << 32) | lo_w;
                                 const uint64_t prev = __hip_atomic_fetch_min(a.cs.cell + ci, cv, __ATOMIC_RELAXED,
                                                                              __HIP_MEMORY_SCOPE_AGENT);
-                                if (prev == kUnseen64) { n_first++; clm |= 1ull << k; }
+                                if (prev == kUnseen64) { n_first++; clm |= 1ull << k; clw[u] = true; }
                             }
                             if (L && seeable && (seen_round < 0 || seen_round > a.g)) {
                                 // the receiver is still validating: drec.peers (score.go:806-809)
@@ -871,6 +882,13 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                         if constexpr (LAT) {
 #pragma unroll
                             for (int u = 0; u < P; ++u) vq_push_wave(a, qpl[u], qv[u]);
+                        }
+                        if constexpr (SP && !LAT) {
+                            if (a.clist) {
+#pragma unroll
+                                for (int u = 0; u < P; ++u)
+                                    clist_push_wave(a, clw[u], (uint64_t)iv[u] | ((uint64_t)s_m[kv[u]] << 32));
+                            }
                         }
                     }
                     if (tab) __syncthreads();                    // s_own is rewritten by the next window
@@ -918,6 +936,7 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
 {
     extern __shared__ uint16_t s_act[];
     __shared__ int s_n;
+    if (a.clist && !a.clist_n[1]) return;                // the claim list covers the round (k_commit_list)
     const int nact = active_slots(a.nnew_cur, a.ring, s_act, &s_n);
     const int lane = threadIdx.x & 63;
     // claims exist only at receivers' cells: the words of [rlo, rhi)
@@ -968,6 +987,33 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
     }
 }
 
+// The same commits from the claim list (member-compacted cells: a round's
+// claims are few next to its active slots x peers): one thread per claimed
+// cell; several claims may share a bitmap word, a lastput or a winner's
+// record, so those updates are atomic.  An overflowed list leaves the round
+// to k_commit's word scan.
+template <bool SP>
+__global__ __launch_bounds__(256) void k_commit_list(RoundArgs a)
+{
+    if (a.clist_n[1]) return;
+    const int64_t n = (int64_t)a.clist_n[0];
+    const uint32_t par = (uint32_t)(a.g & 1);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+        const uint64_t v = a.clist[k];
+        const uint32_t i = (uint32_t)v, m = (uint32_t)(v >> 32);
+        const int64_t ci = SP ? a.cs.idx(m, (int32_t)a.mtopic[m], i) : (int64_t)m * a.cs.n + i;
+        if (ci < 0) continue;
+        uint64_t* cp = a.cs.cell + ci;
+        const uint64_t c = *cp;
+        if (!is_claim_of(c, par)) continue;
+        const int64_t w = (int64_t)(i >> 6);
+        const uint64_t bit = 1ull << (i & 63);
+        atomicOr(reinterpret_cast<unsigned long long*>(a.seenbm + (int64_t)m * a.nw + w), bit);
+        if (a.fresh && a.minv[m] == GSIM_VERDICT_ACCEPT) fresh_set(a, m, w, bit);
+        commit_claim<true, false, SP>(a, cp, c, a.g, m, i);
+    }
+}
 
 // ---------------------------------------------------------------------------
 // Gossip.  Heartbeat k's emitGossip marked ihave[t][e] in
@@ -1581,6 +1627,11 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
             if (prev == kUnseen64) {
                 n_first++;
                 atomicOr(&s_new2[m >> 5], 1u << (m & 31));
+                if (a.clist) {
+                    const uint32_t q = atomicAdd(a.clist_n, 1u);
+                    if ((int64_t)q < a.clist_cap) a.clist[q] = (uint64_t)p | ((uint64_t)m << 32);
+                    else atomicOr(&a.clist_n[1], 1u);
+                }
             }
         }
         if (L && vd != GSIM_VERDICT_SIGNATURE && (seen_round < 0 || seen_round > a.g)) {
@@ -1751,7 +1802,7 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_tmmap); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_clist); f(d->d_clist_n); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_peertx); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
@@ -1792,6 +1843,13 @@ static bool sparse_layout(const gsim_handle* h)
     return h->d_smask != nullptr || (h->dl && h->dl->sparse != 0);
 }
 
+// Commits from the claim list: member-compacted cells (sub-rings of topics
+// only some peers hold) and no validation latency
+static bool list_commit(const gsim_handle* h)
+{
+    return h->dl && h->dl->d_clist && h->dl->sparse != 0 && !h->dl->lat_on;
+}
+
 static Cells deliver_cells(const Deliver* d)
 {
     Cells c;
@@ -1830,10 +1888,16 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.fsum = d->d_fsum;
     a.mmask = d->d_mmask;
     a.tmtab = d->d_tmtab;
-    a.tmmap = nullptr;
     a.peertx = d->d_peertx; a.ptx_w = d->ptx_w;
     a.tr = h->trace;
     a.nsw = (a.nw + 63) / 64;
+    a.ncells = (int64_t)d->n_cells;
+    a.topic_slots = d->cfg.topic_slots > 0 ? (int32_t)d->cfg.topic_slots : 0;
+    if (list_commit(h)) {
+        a.clist = d->d_clist;
+        a.clist_n = d->d_clist_n;
+        a.clist_cap = d->clist_cap;
+    }
     const size_t w = (size_t)nnew_words(d);
     a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
     a.nnew_cur = d->d_nnew + (size_t)(g & 1) * w;
@@ -2050,6 +2114,8 @@ int deliver_flush(gsim_handle* h)
     ProfScope ps(h, GSIM_K_COMMIT);
     RoundArgs a = make_round_args(h, d->pending);
     const dim3 grid(grid_peers((int64_t)a.rhi - ((int64_t)a.rlo & ~63ll)));
+    if (a.clist)
+        hipLaunchKernelGGL(k_commit_list<true>, dim3(2048), dim3(256), 0, h->stream, a);
     if (a.mlat)
         hipLaunchKernelGGL((k_commit<true, true>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     else if (sparse_layout(h))
@@ -2057,7 +2123,9 @@ int deliver_flush(gsim_handle* h)
     else
         hipLaunchKernelGGL((k_commit<false, false>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     d->pending = -1;
-    return hip_check(h, hipGetLastError(), "k_commit");
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && a.clist) e = hipMemsetAsync(d->d_clist_n, 0, 2 * sizeof(uint32_t), h->stream);
+    return hip_check(h, e, "k_commit");
 }
 
 // The previous tick's IWANT response queue overflow and early slot reuse,
@@ -2160,7 +2228,11 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
         for (int t = 0; t < T; ++t) {
             int64_t b = ranges;
             if (wsum > 0) b = (budget * h->topic_subs[t] + wsum - 1) / wsum;
-            b = std::max<int64_t>(1, std::min(b, max_blocks));
+            // ranges of at most kMaxRange peers: a quiet topic's block still scans
+            // its range chunk by chunk, and one block over all N peers would
+            // set the launch's length
+            constexpr int64_t kMaxRange = 64 * chunk;
+            b = std::max<int64_t>(std::max<int64_t>(1, (cn + kMaxRange - 1) / kMaxRange), std::min(b, max_blocks));
             const int64_t range = ((cn + b - 1) / b + chunk - 1) / chunk * chunk;
             d->tmtab[t] = start;
             d->tmtab[T + 1 + t] = (uint32_t)range;
@@ -2170,53 +2242,17 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
         hipError_t e = hipMemcpyAsync(d->d_tmtab, d->tmtab.data(), d->tmtab.size() * 4, hipMemcpyHostToDevice,
                                       h->stream);
         if (e != hipSuccess) return hip_check(h, e, "k_send_tm block table");
-        // XCD placement: topics to the 8 XCDs, largest block count first onto
-        // the least loaded; launched block 8 j + x runs the j-th block of XCD
-        // x's list (the lists padded with idle blocks to the longest)
-        d->tm_grid = start;
-        if (h->tm_xcd && T > 1) {
-            constexpr int kXcd = 8;           // MI355X: 8 XCDs, each with its own L2
-            std::vector<int> order((size_t)T);
-            for (int t = 0; t < T; ++t) order[(size_t)t] = t;
-            auto nb = [&](int t) { return d->tmtab[(size_t)t + 1] - d->tmtab[(size_t)t]; };
-            std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return nb(x) > nb(y); });
-            std::vector<std::vector<uint32_t>> lists(kXcd);
-            std::vector<uint64_t> load(kXcd, 0);
-            for (int t : order) {
-                const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-                for (uint32_t b = d->tmtab[(size_t)t]; b < d->tmtab[(size_t)t + 1]; ++b) lists[(size_t)x].push_back(b);
-                load[(size_t)x] += nb(t);
-            }
-            size_t longest = 0;
-            for (const auto& l : lists) longest = std::max(longest, l.size());
-            std::vector<uint32_t>& map = d->tmmap;
-            map.assign(longest * kXcd, 0xFFFFFFFFu);
-            for (int x = 0; x < kXcd; ++x)
-                for (size_t j = 0; j < lists[(size_t)x].size(); ++j) map[j * kXcd + (size_t)x] = lists[(size_t)x][j];
-            if ((int64_t)map.size() > d->tmmap_cap) {
-                if (d->d_tmmap) (void)hipFree(d->d_tmmap);
-                d->d_tmmap = nullptr;
-                d->tmmap_cap = 0;
-                e = hipMalloc((void**)&d->d_tmmap, map.size() * 4);
-                if (e != hipSuccess) return hip_check(h, e, "k_send_tm block map");
-                d->tmmap_cap = (int64_t)map.size();
-            }
-            e = hipMemcpyAsync(d->d_tmmap, map.data(), map.size() * 4, hipMemcpyHostToDevice, h->stream);
-            if (e != hipSuccess) return hip_check(h, e, "k_send_tm block map");
-            d->tm_grid = (uint32_t)map.size();
-        }
         d->tm_cn = cn;
     }
-    RoundArgs a = a0;
-    a.tmmap = h->tm_xcd && T > 1 ? d->d_tmmap : nullptr;
+    const RoundArgs& a = a0;
     // the slot list in LDS
     const size_t lds = ((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7;
     if (a.mlat)
-        hipLaunchKernelGGL((k_send_tm<TB, true, true>), dim3(d->tm_grid), dim3(TB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<TB, true, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
     else if (sparse_layout(h))
-        hipLaunchKernelGGL((k_send_tm<TB, false, true>), dim3(d->tm_grid), dim3(TB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<TB, false, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
     else
-        hipLaunchKernelGGL((k_send_tm<TB, false, false>), dim3(d->tm_grid), dim3(TB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<TB, false, false>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_send_tm");
 }
 
@@ -2705,6 +2741,14 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_mmask, T * N * 8);
     A((void**)&d->d_tmtab, (2 * 64 + 1) * 4);
     d->tm_cn = -1;
+    if (cfg->topic_slots > 0) {
+        // claim list for member-compacted cells (list_commit): a round's first
+        // deliveries; more overflow into k_commit's word scan
+        d->clist_cap = std::max<int64_t>(2 * (int64_t)N, 1 << 20);
+        A((void**)&d->d_clist, (size_t)d->clist_cap * 8);
+        A((void**)&d->d_clist_n, 2 * 4);
+        if (e == hipSuccess) e = hipMemsetAsync(d->d_clist_n, 0, 2 * 4, h->stream);
+    }
     A((void**)&d->d_mpub, ring * 4);
     A((void**)&d->d_roff, (size_t)cfg->rounds * 8);
     A((void**)&d->d_lastput, T * N * 4);
@@ -2856,6 +2900,11 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
         if (e == hipSuccess) e = hipMemsetAsync(d->d_hist, 0, sizeof(uint32_t) * (size_t)kVqPlanes * (size_t)w, h->stream);
         if (e != hipSuccess) return hip_check(h, e, "validation queues");
         d->lat_on = true;
+    }
+    {
+        // the last round's claims are committed before slots are reset (k_reset_slots)
+        const int rcf = deliver_flush(h);
+        if (rcf) return rcf;
     }
     e = hipMemcpyAsync(d->d_pub, msgs, sizeof(gsim_msg) * (size_t)count, hipMemcpyHostToDevice, h->stream);
     if (e == hipSuccess)

@@ -1339,12 +1339,6 @@ int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant)
         if (h->dl) deliver_blocks_changed(h);
         return GSIM_OK;
     }
-    if (which == 7) {           // k_send_tm block placement: 1 = each topic's blocks on one XCD, 0 = launch order
-        if (variant != 0 && variant != 1) { h->err = "unknown block placement (0 or 1)"; return GSIM_EINVAL; }
-        h->tm_xcd = variant;
-        if (h->dl) deliver_blocks_changed(h);
-        return GSIM_OK;
-    }
     h->err = "unknown kernel variant class";
     return GSIM_EINVAL;
 }

@@ -335,7 +335,6 @@ struct gsim_handle {
     std::vector<int64_t> topic_subs;   // [T] local peers that joined each topic (k_send_tm's block shares)
     bool tm_uniform = false;  // k_send_tm blocks the same for every topic (gsim_set_kernel_variant(h, 6, 1))
     int64_t tm_budget = 0;    // k_send_tm blocks in all (0: ranges x T, launch_send_tm_tb)
-    int tm_xcd = 1;           // k_send_tm blocks of a topic placed on one XCD (gsim_set_kernel_variant(h, 7, v))
     int ihave_w = 0;          // k_ihave lane group width (gsim_set_kernel_variant(h, 3, w)); 0 = by row lengths
 
     // device: parameters and scratch flags
