@@ -61,6 +61,9 @@ __device__ __forceinline__ bool verdict_penalises(uint8_t v)
     return v == GSIM_VERDICT_REJECT || v == GSIM_VERDICT_SIGNATURE;
 }
 constexpr int kSlotBatch = 8;      // active slots whose cells are loaded together
+constexpr int kClSub = 64;
+constexpr int kHubMesh = 16;       // mesh | direct edges listed per (hub, topic); more: the whole row is walked
+constexpr uint32_t kHubList = 0x80000000u;   // k_send_tm s_beg flag: an offset into the hub lists         // claim sub-lists (block % kClSub): spreads the append atomics
 
 // Validation latency (gsim_msg.vdelay).  A cell first
 // claimed in round g of a slot with latency L > 0 is committed with
@@ -92,19 +95,34 @@ struct Deliver {
     uint64_t* d_mbits = nullptr;       // [T][nw] members of each topic (peers with its slot, §2)
     uint32_t* d_mpre = nullptr;        // [T][nw] members before each word
     uint64_t sparse = 0;               // topics with member-compacted cells (Cells::sparse)
+    // member-major gossip (sub-rings with member-compacted cells): each topic's
+    // members in peer order, so the IHAVE passes walk a topic's members, not N
+    uint32_t* d_mlist = nullptr;       // members of the sparse topics, concatenated
+    int64_t* d_mloff = nullptr;        // [T] first entry of each topic (-1: every peer, member j = peer j)
+    int64_t* d_mcount = nullptr;       // [T] members of each topic
+    uint32_t* d_mmtab = nullptr;       // [T+1] first 256-member block of each topic (k_ihave<MM>)
+    uint32_t* d_mctab = nullptr;       // [T+1] first 1024-member block of each topic (k_gossip_count_mm)
+    std::vector<uint32_t> mmtab, mctab;
     int64_t cell_nw = 0;               // words per topic of the member bitmaps
     int64_t n_peers = 0;               // peers the cells were laid out for
     std::vector<int64_t> tcount;       // [T] messages published per topic (sub-ring slot choice)
     uint32_t* d_pslot = nullptr;       // [pub_cap] ring slots of a publish batch
     // claim list (member-compacted cells): the cells a round claimed, so the
     // commit touches those alone instead of every (active slot, peer word)
-    uint64_t* d_clist = nullptr;       // [clist_cap] receiver | slot << 32
-    uint32_t* d_clist_n = nullptr;     // [0] entries, [1] overflow (the commit then scans every word)
-    int64_t clist_cap = 0;
+    uint64_t* d_clist = nullptr;       // [kClSub][clist_cap] receiver | slot << 32, in sub-lists
+    uint32_t* d_clist_n = nullptr;     // [kClSub] entries, [kClSub] overflow (the commit then scans every word)
+    int64_t clist_cap = 0;             // per sub-list
     uint64_t* d_seenbm = nullptr;      // [ring][ceil(N/64)] bit: the cell is committed (a cache of the cells)
     uint64_t* d_fresh = nullptr;       // [ring][ceil(N/64)] bit: the peer forwards the slot's message next round
     uint64_t* d_fsum = nullptr;        // [ring][ceil(N/4096)] bit: that fresh word may be non-zero
     uint64_t* d_mmask = nullptr;       // [T][N] mesh | direct positions of rows <= 64 (RoundArgs::mmask)
+    // hub rows (> 64 connections): per (hub, topic) the row edges that are mesh
+    // or direct, so a forwarding hub walks those few edges, not its whole row
+    uint32_t* d_hidx = nullptr;        // [N] hub index of each row (~0: a row of at most 64)
+    uint32_t* d_hrow = nullptr;        // [nhub] the hubs' rows
+    uint32_t* d_hlist = nullptr;       // [nhub][T][1 + kHubMesh] count (~0: more) then the edges
+    int64_t nhub = 0;
+    int64_t hub_round = -1;            // round the lists were last built for (-1: stale)
     uint64_t mask_version = 0;         // h->mesh_version the masks were built for
     uint32_t* d_tmtab = nullptr;       // k_send_tm blocks: [T+1] first block of each topic, [T] its range
     std::vector<uint32_t> tmtab;       // host copy (the upload's source)
@@ -199,6 +217,7 @@ struct RoundArgs {
     // direct edge (to an owned peer); a forwarder other than the origin sends
     // on no other edge, so only these are walked
     const uint64_t* mmask;
+    const uint32_t *hidx, *hlist;  // hub rows' mesh edge lists (Deliver::d_hlist; nullptr: none)
     const uint32_t* tmtab;         // k_send_tm blocks per topic (Deliver::d_tmtab)
     uint8_t* peertx;               // [ring][ptx_w] GetForPeer counts (Deliver::d_peertx), zeroed on reuse
     int32_t ptx_w;
@@ -288,20 +307,21 @@ __device__ __forceinline__ uint64_t vq_entry(uint32_t e, int32_t t, uint32_t kin
     return (uint64_t)e | ((uint64_t)(uint32_t)t << 32) | ((uint64_t)kind << 40);
 }
 
-// Append the lanes' new claims (receiver | slot << 32) to the claim list,
-// one atomic per wave; every lane of the wave calls it.
+// Append the lanes' new claims (receiver | slot << 32) to the block's claim
+// sub-list, one atomic per wave; every lane of the wave calls it.
 __device__ __forceinline__ void clist_push_wave(const RoundArgs& a, bool on, uint64_t v)
 {
     const uint64_t b = __ballot(on);
     if (!b) return;
     const int lane = threadIdx.x & 63, leader = __builtin_ctzll(b);
+    const uint32_t q = blockIdx.x % kClSub;
     uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(a.clist_n, (uint32_t)__popcll(b));
+    if (lane == leader) base = atomicAdd(&a.clist_n[q], (uint32_t)__popcll(b));
     base = (uint32_t)__shfl((int)base, leader, 64);
     if (on) {
         const uint32_t k = base + (uint32_t)__popcll(b & ((1ull << lane) - 1));
-        if ((int64_t)k < a.clist_cap) a.clist[k] = v;
-        else atomicOr(&a.clist_n[1], 1u);
+        if ((int64_t)k < a.clist_cap) a.clist[(int64_t)q * a.clist_cap + k] = v;
+        else atomicOr(&a.clist_n[kClSub], 1u);
     }
 }
 
@@ -497,6 +517,61 @@ __global__ __launch_bounds__(256) void k_mesh_mask(const uint32_t* row_ptr, cons
     }
 }
 
+// The mesh lists of hub rows: per (hub, topic) the row edges to the receivers
+// [rlo, rhi) that carry the router's mesh bit or are direct peers, in row
+// order, one wave per hub (ballots over 64-position chunks).  More than
+// kHubMesh such edges: count ~0, the hub walks its whole row for t.
+__global__ __launch_bounds__(256) void k_hub_mesh(const uint32_t* row_ptr, const uint32_t* col, const uint8_t* mflags,
+                                                  const uint8_t* direct, const uint64_t* smask, const uint32_t* hrow,
+                                                  int64_t nhub, int64_t E, int32_t T, uint32_t rlo, uint32_t rhi,
+                                                  uint32_t* hlist)
+{
+    const int lane = threadIdx.x & 63;
+    for (int64_t hx = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); hx < nhub; hx += (int64_t)gridDim.x * 4) {
+        const uint32_t x = hrow[hx];
+        const uint32_t b = row_ptr[x], d = row_ptr[x + 1] - b;
+        const uint64_t m = smask_of(smask, x);
+        for (int32_t t = 0; t < T; ++t) {
+            uint32_t* L = hlist + ((int64_t)hx * T + t) * (1 + kHubMesh);
+            if (!slot_has(m, t)) {
+                if (lane == 0) L[0] = 0;
+                continue;
+            }
+            uint32_t cnt = 0;
+            for (uint32_t off = 0; off < d; off += 64) {
+                const uint32_t e = b + off + (uint32_t)lane;
+                bool me = false;
+                if (off + (uint32_t)lane < d) {
+                    const uint32_t i = col[e];
+                    if (i >= rlo && i < rhi)
+                        me = (direct && direct[e]) || (mflags[slot_idx(m, t, E, e)] & GSIM_TF_MESH);
+                }
+                const uint64_t bal = __ballot(me);
+                if (me) {
+                    const uint32_t pos = cnt + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+                    if (pos < (uint32_t)kHubMesh) L[1 + pos] = e;
+                }
+                cnt += (uint32_t)__popcll(bal);
+            }
+            if (lane == 0) L[0] = cnt <= (uint32_t)kHubMesh ? cnt : 0xFFFFFFFFu;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_hub_index(const uint32_t* row_ptr, int64_t n, uint32_t* hidx, uint32_t* hrow,
+                                                   uint32_t* count)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += stride) {
+        uint32_t k = 0xFFFFFFFFu;
+        if (row_ptr[x + 1] - row_ptr[x] > 64u) {
+            k = atomicAdd(count, 1u);
+            if (hrow) hrow[k] = (uint32_t)x;
+        }
+        if (hidx) hidx[x] = k;
+    }
+}
+
 // Delivery round g, topic-major.  Block (range, topic)
 // walks the forwarders of its peer range for every active slot of topic t.
 // It takes each chunk of the range once and gathers there the forwarders of
@@ -550,6 +625,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
     __shared__ uint8_t s_sk[kTmChunk];                       // its slot (index in the pass)
     __shared__ uint8_t s_pl[kTmChunk];                       // its row's topic slot of t (plane, gsim_internal.h)
     __shared__ uint16_t s_own[kTmWin];                       // sender (index above) of each flattened edge of a window
+    __shared__ uint64_t s_cl[SP && !LAT ? kTmThreads * GSIM_TM_P : 1];   // claim-list entries of the iteration's copies
     __shared__ uint32_t s_wsum[64];
     __shared__ uint32_t s_m[kTsSlots], s_org[kTsSlots];      // the pass's slots and their origins
     __shared__ uint64_t s_cb[kTsSlots];                      // ... and their first cells (Cells::cbase)
@@ -668,6 +744,12 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             msk2[u] = a.mmask[(int64_t)t * a.N + x];
                             beg2[u] = rb;
                             len2[u] = (uint32_t)__popcll(msk2[u]);
+                        } else if (a.hlist && x != s_org[k2[u]] &&
+                                   a.hlist[((int64_t)a.hidx[x] * a.T + t) * (1 + kHubMesh)] != 0xFFFFFFFFu) {
+                            // a hub: its listed mesh | direct edges
+                            const uint32_t lo_ = (uint32_t)(((int64_t)a.hidx[x] * a.T + t) * (1 + kHubMesh));
+                            beg2[u] = kHubList | (lo_ + 1u);
+                            len2[u] = a.hlist[lo_];
                         } else {
                             const uint32_t* rp = a.sptr ? a.sptr : a.row_ptr;
                             beg2[u] = rp[x];
@@ -767,9 +849,11 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             pv[u] = !vv[u] ? 0 : (SP && a.smask) ? (int64_t)s_pl[q] * a.E : (int64_t)t * a.E;
                             const uint32_t k = fi - s_off[q];
                             const uint64_t msk = s_msk[q];
-                            mk[u] = msk != 0;
-                            if (msk) ev[u] = s_beg[q] + kth_bit(msk, k);
-                            else if (a.sedge && vv[u]) ev[u] = a.sedge[s_beg[q] + k];
+                            const uint32_t bq = s_beg[q];
+                            mk[u] = msk != 0 || (bq & kHubList);
+                            if (msk) ev[u] = bq + kth_bit(msk, k);
+                            else if (bq & kHubList) ev[u] = vv[u] ? a.hlist[(bq & ~kHubList) + k] : 0u;
+                            else if (a.sedge && vv[u]) ev[u] = a.sedge[bq + k];
                             else ev[u] = s_beg[q] + k;
                         }
 #pragma unroll
@@ -789,9 +873,9 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                         }
                         int qpl[P];              // validation latency: queue plane of the copy (-1: none)
                         uint64_t qv[P];
-                        bool clw[P];             // the copy claimed an unseen cell (claim list)
+                        uint32_t clw = 0;        // bit u: copy u claimed an unseen cell (its entry in s_cl)
 #pragma unroll
-                        for (int u = 0; u < P; ++u) { qpl[u] = -1; qv[u] = 0; clw[u] = false; }
+                        for (int u = 0; u < P; ++u) { qpl[u] = -1; qv[u] = 0; }
 #pragma unroll
                         for (int u = 0; u < P; ++u) {
                             const uint32_t j = jv[u], e = ev[u], i = iv[u], k = kv[u];
@@ -851,7 +935,14 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                                 const uint64_t cv = ((uint64_t)(claim_hi | e) << 32) | lo_w;
                                 const uint64_t prev = __hip_atomic_fetch_min(a.cs.cell + ci, cv, __ATOMIC_RELAXED,
                                                                              __HIP_MEMORY_SCOPE_AGENT);
-                                if (prev == kUnseen64) { n_first++; clm |= 1ull << k; clw[u] = true; }
+                                if (prev == kUnseen64) {
+                                    n_first++;
+                                    clm |= 1ull << k;
+                                    if constexpr (SP && !LAT) {
+                                        clw |= 1u << u;
+                                        s_cl[u * kTmThreads + tid] = (uint64_t)i | ((uint64_t)m << 32);
+                                    }
+                                }
                             }
                             if (L && seeable && (seen_round < 0 || seen_round > a.g)) {
                                 // the receiver is still validating: drec.peers (score.go:806-809)
@@ -887,7 +978,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             if (a.clist) {
 #pragma unroll
                                 for (int u = 0; u < P; ++u)
-                                    clist_push_wave(a, clw[u], (uint64_t)iv[u] | ((uint64_t)s_m[kv[u]] << 32));
+                                    clist_push_wave(a, (clw >> u) & 1u, s_cl[u * kTmThreads + tid]);
                             }
                         }
                     }
@@ -936,7 +1027,7 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
 {
     extern __shared__ uint16_t s_act[];
     __shared__ int s_n;
-    if (a.clist && !a.clist_n[1]) return;                // the claim list covers the round (k_commit_list)
+    if (a.clist && !a.clist_n[kClSub]) return;           // the claim list covers the round (k_commit_list)
     const int nact = active_slots(a.nnew_cur, a.ring, s_act, &s_n);
     const int lane = threadIdx.x & 63;
     // claims exist only at receivers' cells: the words of [rlo, rhi)
@@ -995,12 +1086,13 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
 template <bool SP>
 __global__ __launch_bounds__(256) void k_commit_list(RoundArgs a)
 {
-    if (a.clist_n[1]) return;
-    const int64_t n = (int64_t)a.clist_n[0];
+    if (a.clist_n[kClSub]) return;
+    const uint32_t q = blockIdx.y;                       // sub-list
+    const int64_t n = (int64_t)a.clist_n[q];
     const uint32_t par = (uint32_t)(a.g & 1);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
-        const uint64_t v = a.clist[k];
+        const uint64_t v = a.clist[(int64_t)q * a.clist_cap + k];
         const uint32_t i = (uint32_t)v, m = (uint32_t)(v >> 32);
         const int64_t ci = SP ? a.cs.idx(m, (int32_t)a.mtopic[m], i) : (int64_t)m * a.cs.n + i;
         if (ci < 0) continue;
@@ -1066,7 +1158,29 @@ struct IhArgs {
     uint8_t* peertx;
     int32_t ptx_w;
     int32_t retrans;               // GossipRetransmission
+    // member-major walk (Deliver::d_mlist): blocks of a topic's members
+    const uint32_t* mlist;
+    const int64_t *mloff, *mcount;
+    const uint32_t* mmtab;
+    int32_t topic_slots;
 };
+
+// Member-major blocks: block b of a launch over topics' member ranges (table
+// tab[T+1] of first blocks) -> its topic.
+__device__ __forceinline__ int32_t block_topic(const uint32_t* tab, int32_t T, uint32_t b)
+{
+    int32_t t = 0, r = T > 0 ? T : 1;
+    while (r - t > 1) {
+        const int32_t mid = (t + r) >> 1;
+        if (tab[mid] <= b) t = mid; else r = mid;
+    }
+    return t;
+}
+__device__ __forceinline__ uint32_t member_peer(const IhArgs& a, int32_t t, int64_t j)
+{
+    const int64_t off = a.mloff[t];
+    return off < 0 ? (uint32_t)j : a.mlist[off + j];
+}
 
 // handleIWant's GetForPeer count (mcache.go:73-86) for a response to
 // (slot m, the advertiser's edge re): only a bad-signature message can be
@@ -1163,7 +1277,67 @@ __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount
         if (s_cnt[w]) atomicAdd(&gcount[w], s_cnt[w]);
 }
 
-template <int W, bool LAT, bool SP>
+// k_gossip_count over the members of each topic (sub-rings with
+// member-compacted cells): block b takes 1024 members of its topic, whose
+// cells in each of the topic's slots are consecutive; only the topic's own
+// sub-ring is scanned.  Counts are the same as k_gossip_count's: a peer
+// without a cell neither holds nor wants.
+template <bool LAT>
+__global__ __launch_bounds__(256) void k_gossip_count_mm(IhArgs a, const uint32_t* mctab, uint32_t* gcount)
+{
+    extern __shared__ uint32_t s_c[];     // [2][R] holders, wanting receivers per slot of the sub-ring
+    __shared__ uint16_t s_slot[kMaxRing / 8];
+    __shared__ int s_n;
+    const int32_t t = block_topic(mctab, a.T, blockIdx.x);
+    const int32_t R = a.topic_slots, m_lo = t * R;
+    for (int w = threadIdx.x; w < 2 * R; w += blockDim.x) s_c[w] = 0;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (threadIdx.x < 64) {
+        int n = 0;
+        for (int k0 = 0; k0 < R; k0 += 64) {
+            const int k = k0 + lane;
+            const bool act = k < R && a.slot_last[m_lo + k] >= a.lo_round;
+            const uint64_t b = __ballot(act);
+            if (act) s_slot[n + __popcll(b & ((1ull << lane) - 1))] = (uint16_t)k;
+            n += __popcll(b);
+        }
+        if (lane == 0) s_n = n;
+    }
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        // the window's slots of every topic (k_ihave_pairs decision, as k_gossip_count)
+        int tot = 0;
+        for (int m0 = 0; m0 < a.ring; m0 += 64)
+            tot += __popcll(__ballot(m0 + lane < a.ring && a.slot_last[m0 + lane] >= a.lo_round));
+        if (lane == 0 && tot > a.max_ihave) atomicOr(&a.nresp[3], 4u);
+    }
+    const int ns = s_n;
+    const int64_t M = a.mcount[t];
+    const int64_t tick_round = a.tick * a.R;
+    for (int64_t j0 = (int64_t)(blockIdx.x - mctab[t]) * 1024 + wid * 64; j0 < M && ns; j0 += 256) {
+        if (j0 >= (int64_t)(blockIdx.x - mctab[t] + 1) * 1024) break;
+        const int64_t j = j0 + lane;
+        const bool vp = j < M;
+        const uint32_t p = vp ? member_peer(a, t, j) : 0u;
+        const bool subp = vp && ((a.sub[p] >> t) & 1ull) && p >= a.rlo && p < a.rhi;
+        for (int q = 0; q < ns; ++q) {
+            const int k = s_slot[q];
+            const uint32_t m = (uint32_t)(m_lo + k);
+            const uint64_t c = vp ? a.cs.cell[(int64_t)a.cs.cbase[m] + j] : kUnseen64;
+            const bool hold = vp && holds_in_window(c, a.g, a.lo_round, tick_round, a.minv[m] != 0, p == a.morigin[m],
+                                                    LAT ? a.mlat[m] : 0u);
+            const bool want = subp && c == kUnseen64;
+            const int nh = __popcll(__ballot(hold)), nw = __popcll(__ballot(want));
+            if (lane == 0 && nh) atomicAdd(&s_c[k], (uint32_t)nh);
+            if (lane == 0 && nw) atomicAdd(&s_c[R + k], (uint32_t)nw);
+        }
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < 2 * R; w += blockDim.x)
+        if (s_c[w]) atomicAdd(&gcount[(w < R ? 0 : a.ring - R) + m_lo + w], s_c[w]);
+}
+
+template <int W, bool LAT, bool SP, bool MM = false>
 __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
 {
     extern __shared__ uint16_t s_act[];   // [ring] candidate slots (bit 15: push), then response staging
@@ -1171,12 +1345,17 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
     if (a.nresp[3] & 4u) return;          // a truncation may apply: k_ihave_pairs
     const int wid = threadIdx.x >> 6;
     uint64_t* stage = reinterpret_cast<uint64_t*>(s_act + ((a.ring + 3) & ~3)) + wid * kRespStage;
+    // MM: the block's topic and its 256 members [jb, jb + 256) (member-major
+    // walk of a sub-ring: only the topic's slots, cells at cbase[m] + member)
+    const int32_t tb = MM ? block_topic(a.mmtab, a.T, blockIdx.x) : 0;
+    const int64_t jb = MM ? (int64_t)(blockIdx.x - a.mmtab[tb]) * 256 : 0;
+    const int m_lo = MM ? tb * a.topic_slots : 0, m_hi = MM ? m_lo + a.topic_slots : a.ring;
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         int n = 0;
-        for (int m0 = 0; m0 < a.ring; m0 += 64) {
+        for (int m0 = m_lo; m0 < m_hi; m0 += 64) {
             const int m = m0 + lane;
-            const bool act = m < a.ring && a.slot_last[m] >= a.lo_round && gcount[m] != 0 && gcount[a.ring + m] != 0;
+            const bool act = m < m_hi && a.slot_last[m] >= a.lo_round && gcount[m] != 0 && gcount[a.ring + m] != 0;
             // cost model: a holder walk probes ~Dlazy cells, a receiver walk ~deg
             // (a shard's holders include its ghosts: their ghost rows are their
             // connections to its receivers)
@@ -1189,10 +1368,11 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int64_t p0 = ((int64_t)blockIdx.x * 4 + wid) * 64;   // peers p0 .. p0 + 63
-    const int nact = p0 < a.CN ? s_n : 0;
-    const int64_t pc = p0 + lane, pl = pc;
-    const bool vp = pc < a.CN;
+    const int64_t p0 = MM ? 0 : ((int64_t)blockIdx.x * 4 + wid) * 64;   // peers p0 .. p0 + 63
+    const int64_t jw = jb + wid * 64;                                  // MM: members jw .. jw + 63
+    const int nact = (MM ? jw < a.mcount[tb] : p0 < a.CN) ? s_n : 0;
+    const bool vp = MM ? jw + lane < a.mcount[tb] : p0 + lane < a.CN;
+    const int64_t pl = MM ? (vp ? (int64_t)member_peer(a, tb, jw + lane) : 0) : p0 + lane;
     const int grp = lane / W, gl = lane % W;
     const uint64_t gmask = group_mask<W>(grp);
     const uint64_t subp = vp ? a.sub[pl] : 0ull;
@@ -1220,7 +1400,10 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
             const int k = k0 + b;
-            const int64_t ci = (k < nact && vp) ? word_cell<SP>(a.cs, a.mtopic, s_act[k] & 0x7FFF, p0 >> 6, lane) : -1;
+            const int64_t ci = (k < nact && vp)
+                                   ? (MM ? (int64_t)a.cs.cbase[s_act[k] & 0x7FFF] + jw + lane
+                                         : word_cell<SP>(a.cs, a.mtopic, s_act[k] & 0x7FFF, p0 >> 6, lane))
+                                   : -1;
             cv[b] = ci >= 0 ? a.cs.cell[ci] : kUnseen64;   // no cell: not a member, nothing held or wanted
         }
 #pragma unroll
@@ -1304,7 +1487,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                 const int sl = bs < 0 ? lane : bs;
                 const uint32_t beg = __shfl(rp0, sl, 64), end = __shfl(rp1, sl, 64);
                 const bool ign_s = __shfl(ign_l, sl, 64);
-                const uint32_t me_id = (uint32_t)(p0 + (bs < 0 ? 0 : bs));
+                const uint32_t me_id = MM ? (uint32_t)__shfl((int)pl, sl, 64) : (uint32_t)(p0 + (bs < 0 ? 0 : bs));
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;   // Philox keys use global ids
                 const uint64_t me_m = smask_of(a.smask, me_id);
                 const int64_t me_pl = slot_has(me_m, t) ? slot_idx(me_m, t, a.E, 0) : -1;
@@ -1318,7 +1501,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
                 const int bs = __builtin_ctzll(lm);
                 const uint32_t beg = __shfl(rp0, bs, 64), end = __shfl(rp1, bs, 64);
                 const bool ign_s = __shfl(ign_l, bs, 64);
-                const uint32_t me_id = (uint32_t)(p0 + bs);
+                const uint32_t me_id = MM ? (uint32_t)__shfl((int)pl, bs, 64) : (uint32_t)(p0 + bs);
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
                 const uint64_t me_m = smask_of(a.smask, me_id);
                 const int64_t me_pl = slot_has(me_m, t) ? slot_idx(me_m, t, a.E, 0) : -1;
@@ -1628,9 +1811,10 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
                 n_first++;
                 atomicOr(&s_new2[m >> 5], 1u << (m & 31));
                 if (a.clist) {
-                    const uint32_t q = atomicAdd(a.clist_n, 1u);
-                    if ((int64_t)q < a.clist_cap) a.clist[q] = (uint64_t)p | ((uint64_t)m << 32);
-                    else atomicOr(&a.clist_n[1], 1u);
+                    const uint32_t sq = blockIdx.x % kClSub;
+                    const uint32_t q = atomicAdd(&a.clist_n[sq], 1u);
+                    if ((int64_t)q < a.clist_cap) a.clist[(int64_t)sq * a.clist_cap + q] = (uint64_t)p | ((uint64_t)m << 32);
+                    else atomicOr(&a.clist_n[kClSub], 1u);
                 }
             }
         }
@@ -1802,7 +1986,7 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_clist); f(d->d_clist_n); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_clist); f(d->d_clist_n); f(d->d_hidx); f(d->d_hrow); f(d->d_hlist); f(d->d_mlist); f(d->d_mloff); f(d->d_mcount); f(d->d_mmtab); f(d->d_mctab); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_peertx); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
@@ -1841,6 +2025,12 @@ static int grid_peers(int64_t n)
 static bool sparse_layout(const gsim_handle* h)
 {
     return h->d_smask != nullptr || (h->dl && h->dl->sparse != 0);
+}
+
+// Member-major IHAVE passes: member lists of a sub-ring layout, single engine
+static bool mm_gossip(const gsim_handle* h)
+{
+    return h->dl && h->dl->d_mmtab && h->dl->sparse != 0 && !h->sh;
 }
 
 // Commits from the claim list: member-compacted cells (sub-rings of topics
@@ -1887,6 +2077,8 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.fresh = d->d_fresh;
     a.fsum = d->d_fsum;
     a.mmask = d->d_mmask;
+    a.hidx = d->d_hlist ? d->d_hidx : nullptr;
+    a.hlist = d->d_hlist;
     a.tmtab = d->d_tmtab;
     a.peertx = d->d_peertx; a.ptx_w = d->ptx_w;
     a.tr = h->trace;
@@ -2030,6 +2222,10 @@ static bool ihave_prepare(gsim_handle* h, int64_t g, IhaveStage* st, int* rc)
     a.max_ihave = h->gp.max_ihave_length;
     a.peertx = d->d_peertx; a.ptx_w = d->ptx_w;
     a.retrans = h->gp.gossip_retransmission;
+    if (mm_gossip(h)) {
+        a.mlist = d->d_mlist; a.mloff = d->d_mloff; a.mcount = d->d_mcount; a.mmtab = d->d_mmtab;
+        a.topic_slots = (int32_t)d->cfg.topic_slots;
+    }
     st->lds = (((size_t)d->cfg.ring + 3) & ~(size_t)3) * sizeof(uint16_t) + 4 * kRespStage * sizeof(uint64_t);
     st->lds_c = (((size_t)d->cfg.ring + 1) & ~(size_t)1) * sizeof(uint16_t) + 2 * (size_t)d->cfg.ring * 4;
     st->grid = grid_peers(a.CN);
@@ -2044,7 +2240,17 @@ static bool ihave_prepare(gsim_handle* h, int64_t g, IhaveStage* st, int* rc)
 static int ihave_count(gsim_handle* h, IhaveStage* st)
 {
     ProfScope ps(h, GSIM_K_GOSSIP);
-    if (st->a.mlat)
+    Deliver* d = h->dl;
+    if (st->a.mmtab) {
+        const uint32_t grid = d->mctab.back();
+        const size_t lds = 2 * (size_t)d->cfg.topic_slots * 4;
+        if (grid && st->a.mlat)
+            hipLaunchKernelGGL(k_gossip_count_mm<true>, dim3(grid), dim3(256), lds, h->stream, st->a,
+                               (const uint32_t*)d->d_mctab, d->d_gcount);
+        else if (grid)
+            hipLaunchKernelGGL(k_gossip_count_mm<false>, dim3(grid), dim3(256), lds, h->stream, st->a,
+                               (const uint32_t*)d->d_mctab, d->d_gcount);
+    } else if (st->a.mlat)
         hipLaunchKernelGGL((k_gossip_count<true, true>), dim3(st->grid), dim3(256), st->lds_c, h->stream, st->a, h->dl->d_gcount);
     else if (sparse_layout(h))
         hipLaunchKernelGGL((k_gossip_count<false, true>), dim3(st->grid), dim3(256), st->lds_c, h->stream, st->a, h->dl->d_gcount);
@@ -2056,7 +2262,14 @@ static int ihave_count(gsim_handle* h, IhaveStage* st)
 template <int W>
 static void launch_ihave_w(gsim_handle* h, IhaveStage* st, const IhArgs& a)
 {
-    if (a.mlat)
+    if (a.mmtab) {
+        const uint32_t grid = h->dl->mmtab.back();
+        if (!grid) return;
+        if (a.mlat)
+            hipLaunchKernelGGL((k_ihave<W, true, true, true>), dim3(grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)h->dl->d_gcount);
+        else
+            hipLaunchKernelGGL((k_ihave<W, false, true, true>), dim3(grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)h->dl->d_gcount);
+    } else if (a.mlat)
         hipLaunchKernelGGL((k_ihave<W, true, true>), dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)h->dl->d_gcount);
     else if (sparse_layout(h))
         hipLaunchKernelGGL((k_ihave<W, false, true>), dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)h->dl->d_gcount);
@@ -2115,7 +2328,7 @@ int deliver_flush(gsim_handle* h)
     RoundArgs a = make_round_args(h, d->pending);
     const dim3 grid(grid_peers((int64_t)a.rhi - ((int64_t)a.rlo & ~63ll)));
     if (a.clist)
-        hipLaunchKernelGGL(k_commit_list<true>, dim3(2048), dim3(256), 0, h->stream, a);
+        hipLaunchKernelGGL(k_commit_list<true>, dim3(64, kClSub), dim3(256), 0, h->stream, a);
     if (a.mlat)
         hipLaunchKernelGGL((k_commit<true, true>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     else if (sparse_layout(h))
@@ -2124,7 +2337,7 @@ int deliver_flush(gsim_handle* h)
         hipLaunchKernelGGL((k_commit<false, false>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     d->pending = -1;
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess && a.clist) e = hipMemsetAsync(d->d_clist_n, 0, 2 * sizeof(uint32_t), h->stream);
+    if (e == hipSuccess && a.clist) e = hipMemsetAsync(d->d_clist_n, 0, (kClSub + 1) * sizeof(uint32_t), h->stream);
     return hip_check(h, e, "k_commit");
 }
 
@@ -2339,6 +2552,17 @@ int deliver_round_send(gsim_handle* h, int64_t round)
                                (const uint64_t*)h->d_smask, h->n, h->e,
                                std::max(1, h->t), (uint32_t)h->olo(), (uint32_t)h->ohi(), d->d_mmask);
             d->mask_version = h->mesh_version;
+            d->hub_round = -1;
+        }
+        // hub lists: after the heartbeat (round 0 of a tick) and the control
+        // rounds (0, 1) and any rebuild of the masks
+        if (d->d_hlist && (d->hub_round < 0 || round % d->cfg.rounds < 3)) {
+            hipLaunchKernelGGL(k_hub_mesh, dim3((uint32_t)std::min<int64_t>((d->nhub + 3) / 4, 65536)), dim3(256), 0,
+                               h->stream, (const uint32_t*)h->d_row_ptr, (const uint32_t*)h->d_col,
+                               (const uint8_t*)h->d_mflags, (const uint8_t*)h->d_direct,
+                               (const uint64_t*)h->d_smask, (const uint32_t*)d->d_hrow, d->nhub, h->e,
+                               std::max(1, h->t), (uint32_t)h->olo(), (uint32_t)h->ohi(), d->d_hlist);
+            d->hub_round = round;
         }
         // one thread per edge: forwarders walk only their mesh edges (a
         // handful of a row's positions), so lane groups per row would idle
@@ -2568,7 +2792,12 @@ struct CellLayout {
     std::vector<uint32_t> mpre;
     uint64_t sparse = 0;
     size_t cells = 0;
+    // member-major gossip (sub-rings of at most kMmMaxSlots slots): members per
+    // topic in peer order (sparse topics), offsets, counts
+    std::vector<uint32_t> mlist;
+    std::vector<int64_t> mloff, mcount;
 };
+constexpr int64_t kMmMaxSlots = kMaxRing / 8;   // k_gossip_count_mm's slot list
 
 static CellLayout cell_layout(const gsim_handle* h, const gsim_msg_config& cfg)
 {
@@ -2610,6 +2839,18 @@ static CellLayout cell_layout(const gsim_handle* h, const gsim_msg_config& cfg)
                 acc += (uint32_t)__builtin_popcountll(L.mbits[(size_t)t * (size_t)nw + (size_t)w]);
             }
         }
+        if (R <= kMmMaxSlots) {
+            L.mloff.assign((size_t)T, -1);
+            L.mcount.assign(M.begin(), M.end());
+            int64_t off = 0;
+            for (int32_t t = 0; t < T; ++t)
+                if ((L.sparse >> t) & 1ull) { L.mloff[(size_t)t] = off; off += M[(size_t)t]; }
+            L.mlist.assign((size_t)off, 0);
+            std::vector<int64_t> fill(L.mloff);
+            for (int64_t p = 0; p < N; ++p)
+                for (uint64_t b = h->smask[(size_t)p] & L.sparse; b; b &= b - 1)
+                    L.mlist[(size_t)fill[(size_t)__builtin_ctzll(b)]++] = (uint32_t)p;
+        }
     }
     return L;
 }
@@ -2620,7 +2861,9 @@ static hipError_t install_layout(gsim_handle* h, Deliver* d, const CellLayout& L
     hipError_t e = hipSuccess;
     auto fr = [](void* p) { if (p) (void)hipFree(p); };
     fr(d->d_cbase); fr(d->d_mbits); fr(d->d_mpre);
+    fr(d->d_mlist); fr(d->d_mloff); fr(d->d_mcount); fr(d->d_mmtab); fr(d->d_mctab);
     d->d_cbase = nullptr; d->d_mbits = nullptr; d->d_mpre = nullptr;
+    d->d_mlist = nullptr; d->d_mloff = nullptr; d->d_mcount = nullptr; d->d_mmtab = nullptr; d->d_mctab = nullptr;
     e = hipMalloc((void**)&d->d_cbase, std::max<size_t>(L.cbase.size() * 8, 8));
     if (e == hipSuccess) e = hipMemcpy(d->d_cbase, L.cbase.data(), L.cbase.size() * 8, hipMemcpyHostToDevice);
     if (e == hipSuccess && L.sparse) {
@@ -2628,6 +2871,26 @@ static hipError_t install_layout(gsim_handle* h, Deliver* d, const CellLayout& L
         if (e == hipSuccess) e = hipMalloc((void**)&d->d_mpre, L.mpre.size() * 4);
         if (e == hipSuccess) e = hipMemcpy(d->d_mbits, L.mbits.data(), L.mbits.size() * 8, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(d->d_mpre, L.mpre.data(), L.mpre.size() * 4, hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess && !L.mloff.empty()) {
+        const size_t T = L.mloff.size();
+        d->mmtab.assign(T + 1, 0);
+        d->mctab.assign(T + 1, 0);
+        for (size_t t = 0; t < T; ++t) {
+            d->mmtab[t + 1] = d->mmtab[t] + (uint32_t)((L.mcount[t] + 255) / 256);
+            d->mctab[t + 1] = d->mctab[t] + (uint32_t)((L.mcount[t] + 1023) / 1024);
+        }
+        e = hipMalloc((void**)&d->d_mlist, std::max<size_t>(L.mlist.size() * 4, 4));
+        if (e == hipSuccess) e = hipMalloc((void**)&d->d_mloff, T * 8);
+        if (e == hipSuccess) e = hipMalloc((void**)&d->d_mcount, T * 8);
+        if (e == hipSuccess) e = hipMalloc((void**)&d->d_mmtab, (T + 1) * 4);
+        if (e == hipSuccess) e = hipMalloc((void**)&d->d_mctab, (T + 1) * 4);
+        if (e == hipSuccess && !L.mlist.empty())
+            e = hipMemcpy(d->d_mlist, L.mlist.data(), L.mlist.size() * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(d->d_mloff, L.mloff.data(), T * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(d->d_mcount, L.mcount.data(), T * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(d->d_mmtab, d->mmtab.data(), (T + 1) * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(d->d_mctab, d->mctab.data(), (T + 1) * 4, hipMemcpyHostToDevice);
     }
     d->cbase = L.cbase;
     d->sparse = L.sparse;
@@ -2744,10 +3007,37 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     if (cfg->topic_slots > 0) {
         // claim list for member-compacted cells (list_commit): a round's first
         // deliveries; more overflow into k_commit's word scan
-        d->clist_cap = std::max<int64_t>(2 * (int64_t)N, 1 << 20);
-        A((void**)&d->d_clist, (size_t)d->clist_cap * 8);
-        A((void**)&d->d_clist_n, 2 * 4);
-        if (e == hipSuccess) e = hipMemsetAsync(d->d_clist_n, 0, 2 * 4, h->stream);
+        d->clist_cap = std::max<int64_t>(2 * (int64_t)N, 1 << 20) / kClSub;
+        A((void**)&d->d_clist, (size_t)d->clist_cap * kClSub * 8);
+        A((void**)&d->d_clist_n, (kClSub + 1) * 4);
+        if (e == hipSuccess) e = hipMemsetAsync(d->d_clist_n, 0, (kClSub + 1) * 4, h->stream);
+    }
+    if (h->max_degree > 64 && e == hipSuccess) {
+        // hub rows and their mesh lists (k_hub_mesh)
+        uint32_t* cnt = nullptr;
+        uint32_t nh = 0;
+        e = hipMalloc((void**)&cnt, 4);
+        if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, 4, h->stream);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_hub_index, dim3(1024), dim3(256), 0, h->stream, (const uint32_t*)h->d_row_ptr, h->n,
+                               (uint32_t*)nullptr, (uint32_t*)nullptr, cnt);
+            e = hipMemcpyAsync(&nh, cnt, 4, hipMemcpyDeviceToHost, h->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        }
+        const int64_t words = (int64_t)nh * (int64_t)T * (1 + kHubMesh);
+        if (e == hipSuccess && nh && words < (int64_t)kHubList) {
+            d->nhub = nh;
+            A((void**)&d->d_hidx, N * 4);
+            A((void**)&d->d_hrow, (size_t)nh * 4);
+            A((void**)&d->d_hlist, (size_t)words * 4);
+            if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, 4, h->stream);
+            if (e == hipSuccess)
+                hipLaunchKernelGGL(k_hub_index, dim3(1024), dim3(256), 0, h->stream, (const uint32_t*)h->d_row_ptr, h->n,
+                                   d->d_hidx, d->d_hrow, cnt);
+            if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        }
+        if (cnt) (void)hipFree(cnt);
+        d->hub_round = -1;
     }
     A((void**)&d->d_mpub, ring * 4);
     A((void**)&d->d_roff, (size_t)cfg->rounds * 8);
