@@ -227,7 +227,62 @@ struct RoundArgs {
     int64_t clist_cap;
     int64_t ncells;                // cells of the seen-set (the last slot's end)
     int32_t topic_slots;           // sub-rings: slots [t R, t R + R) carry topic t (0: one shared ring)
+    GaterRef gt;                   // peer gater (gater.hip; gt.act == nullptr: off)
 };
+
+// The peer gater's AcceptFrom (peer_gater.go:320-363) at receiver i for a
+// copy from sender j, record r (i's record of j: its stats group gq[r]),
+// slot m: true = AcceptAll.  rand.Float64() is a Philox uniform keyed by
+// (round, receiver, slot | P_GATER, sender) (oracle_gater.c).  AcceptControl
+// drops the message and runs ThrottlePeer (gossip_tracer.go:182-200): i's
+// promises from j are forgotten.  Direct peers are accepted
+// (gossipsub.go:599-602).
+__device__ __forceinline__ bool gater_accept(const RoundArgs& a, uint32_t i, uint32_t r, uint32_t m, uint32_t j)
+{
+    const GaterRef& g = a.gt;
+    if (!g.act[i]) return true;
+    const uint32_t ei = a.rev[r];                          // i's edge to j
+    if (g.direct && g.direct[ei]) return true;
+    const uint32_t q = g.gq[r];
+    const double del = g.del[q];
+    const double total = del + g.dw * g.dup[q] + g.iw * g.ign[q] + g.rw * g.rej[q];
+    if (total == 0) return true;
+    const double thr = (1 + del) / (1 + total);
+    const u32x4 x = philox4x32_10((uint32_t)a.g, i, (m << 8) | P_GATER, j, (uint32_t)g.seed, (uint32_t)(g.seed >> 32));
+    const uint64_t r53 = ((uint64_t)x.x << 21) | (x.y >> 11);
+    if ((double)r53 * (1.0 / 9007199254740992.0) < thr) return true;
+    for (int32_t q2 = 0; q2 < g.P; ++q2) g.prom[(int64_t)q2 * a.E + ei] = 0xFFFFFFFFu;
+    atomicAdd(g.n_thr, 1ull);
+    return false;
+}
+
+// a copy the receiver handled: DuplicateMessage, or the bad signature's
+// RejectMessage (peer_gater.go:393-432); the claim winner is converted at commit
+__device__ __forceinline__ void gater_copy(const RoundArgs& a, uint32_t r, bool sig)
+{
+    const uint32_t q = a.gt.gq[r];
+    atomicAdd(sig ? &a.gt.a_rej[q] : &a.gt.a_dup[q], 1u);
+}
+
+// the first delivery of record r at receiver i: ValidateMessage and the
+// verdict's Deliver/RejectMessage instead of a duplicate
+__device__ __forceinline__ void gater_first(const RoundArgs& a, uint32_t r, uint32_t i, int32_t t, uint8_t verdict)
+{
+    const GaterRef& g = a.gt;
+    const uint32_t q = g.gq[r];
+    atomicSub(&g.a_dup[q], 1u);
+    atomicAdd(&g.a_val[i], 1u);
+    if (verdict == GSIM_VERDICT_ACCEPT) {
+        atomicAdd(&g.a_del[q], g.tw[t]);
+    } else if (verdict == GSIM_VERDICT_REJECT) {
+        atomicAdd(&g.a_rej[q], 1u);
+    } else if (verdict == GSIM_VERDICT_IGNORE) {
+        atomicAdd(&g.a_ign[q], 1u);
+    } else if (verdict == GSIM_VERDICT_THROTTLE) {
+        atomicAdd(&g.a_thr[i], 1u);
+        g.a_last[i] = 1;
+    }
+}
 
 __device__ __forceinline__ int64_t round_time(const RoundArgs& a, int64_t g)
 {
@@ -372,6 +427,7 @@ __device__ __forceinline__ void commit_claim(const RoundArgs& a, uint64_t* cellp
     } else {
         *cellp = ((uint64_t)(uint32_t)gc << 32) | (lo & kPeerMask);
     }
+    if (a.gt.act) gater_first(a, hi & kEdgeMask, (uint32_t)peer, (int32_t)a.mtopic[m], a.minv[m]);
     if (a.minv[m]) return;                                // RejectMessage: counted when sent
     const int32_t t = (int32_t)a.mtopic[m];
     int32_t* lp = a.lastput + (int64_t)t * a.N + peer;
@@ -609,7 +665,7 @@ constexpr int kTmTabMin = 256;      // forwarders in a chunk from which the tabl
 
 // SP: topic slots or member-compacted cells are in use (gsim_internal.h); the
 // dense instance indexes plane t and cell m * N + p with no table reads.
-template <int kTmThreads, bool LAT, bool SP>
+template <int kTmThreads, bool LAT, bool SP, bool GT = false>
 __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs a)
 {
     extern __shared__ uint64_t s_dyn[];
@@ -896,8 +952,12 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             const bool remote = i < a.rlo || i >= a.rhi;
                             const bool ok = tg && !remote && (ds & GSIM_DS_ACCEPT);
                             n_gray += tg && !remote && !ok;
-                            n_acc += ok;
                             if (!ok) continue;
+                            if constexpr (GT) {                  // the peer gater (gater_accept)
+                                if (!gater_accept(a, i, e, m, j)) continue;
+                                gater_copy(a, e, !seeable);
+                            }
+                            n_acc++;
                             if (a.tr.on(i))
                                 a.tr.push(round_time(a, a.g), ((uint64_t)a.g << 32) | m, i, j, t,
                                           seeable ? kTraceCopy : (uint8_t)GSIM_TRACE_REJECT_MESSAGE, vd);
@@ -1773,8 +1833,12 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
         const uint32_t r = (uint32_t)ent, m = (uint32_t)(ent >> 32);
         const uint8_t ds = a.dstate[r];
         if (!(ds & GSIM_DS_ACCEPT)) { n_gray++; continue; }        // AcceptFrom
-        n_acc++;
         const uint32_t p = a.col[r], i = owner[r];
+        if (a.gt.act) {                                            // the peer gater (gater_accept)
+            if (!gater_accept(a, p, r, m, i)) continue;
+            gater_copy(a, r, a.minv[m] == GSIM_VERDICT_SIGNATURE);
+        }
+        n_acc++;
         const int32_t t = (int32_t)a.mtopic[m];
         const ctp_t tp = tpa + t;
         const uint8_t vd = a.minv[m];
@@ -2027,6 +2091,8 @@ static bool sparse_layout(const gsim_handle* h)
     return h->d_smask != nullptr || (h->dl && h->dl->sparse != 0);
 }
 
+bool deliver_latency_on(gsim_handle* h) { return h->dl && h->dl->lat_on; }
+
 // Member-major IHAVE passes: member lists of a sub-ring layout, single engine
 static bool mm_gossip(const gsim_handle* h)
 {
@@ -2084,6 +2150,8 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.tr = h->trace;
     a.nsw = (a.nw + 63) / 64;
     a.ncells = (int64_t)d->n_cells;
+    a.gt = gater_ref(h);
+    if (a.gt.act) { a.gt.prom = d->d_prom; a.gt.P = d->prom_ticks; }
     a.topic_slots = d->cfg.topic_slots > 0 ? (int32_t)d->cfg.topic_slots : 0;
     if (list_commit(h)) {
         a.clist = d->d_clist;
@@ -2335,10 +2403,12 @@ int deliver_flush(gsim_handle* h)
         hipLaunchKernelGGL((k_commit<false, true>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     else
         hipLaunchKernelGGL((k_commit<false, false>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
+    const int64_t committed = d->pending;
     d->pending = -1;
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && a.clist) e = hipMemsetAsync(d->d_clist_n, 0, (kClSub + 1) * sizeof(uint32_t), h->stream);
-    return hip_check(h, e, "k_commit");
+    const int rc = hip_check(h, e, "k_commit");
+    return rc ? rc : gater_fold(h, committed, a.now);    // the round's gater events, claims resolved
 }
 
 // The previous tick's IWANT response queue overflow and early slot reuse,
@@ -2462,6 +2532,10 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
     const size_t lds = ((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7;
     if (a.mlat)
         hipLaunchKernelGGL((k_send_tm<TB, true, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+    else if (a.gt.act && sparse_layout(h))
+        hipLaunchKernelGGL((k_send_tm<TB, false, true, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+    else if (a.gt.act)
+        hipLaunchKernelGGL((k_send_tm<TB, false, false, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
     else if (sparse_layout(h))
         hipLaunchKernelGGL((k_send_tm<TB, false, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
     else
@@ -2568,8 +2642,10 @@ int deliver_round_send(gsim_handle* h, int64_t round)
         // handful of a row's positions), so lane groups per row would idle
         // most lanes (C3: 21.0 against 32.9 ms per tick,
         // profiles/r02_ab_walk_masks.log)
-        rc = launch_send_tm(h, a);
+        rc = gater_round_begin(h, a.now);   // the gate's state before the round's copies
+        if (!rc) rc = launch_send_tm(h, a);
         if (rc) return rc;
+        gater_round_sent(h, round);
         // the claims of round g-1 were committed before k_send_tm; round g+1's bits
         // were last read (as "previous") by round g
         d->pending = round;
@@ -3140,6 +3216,10 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
             slots[(size_t)m] = (uint32_t)(msgs[m].id % (uint64_t)d->cfg.ring);
         }
         if (msgs[m].vdelay > GSIM_MAX_VDELAY) { h->err = "vdelay above GSIM_MAX_VDELAY"; return GSIM_EINVAL; }
+        if (msgs[m].vdelay && h->gt) {
+            h->err = "a validation latency (vdelay) cannot be combined with the peer gater";
+            return GSIM_ESTATE;
+        }
         if (msgs[m].vdelay && h->sh) {
             h->err = "a validation latency (vdelay) needs a single engine (not a shard)";
             return GSIM_ERANGE;

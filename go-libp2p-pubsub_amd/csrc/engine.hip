@@ -640,6 +640,7 @@ static void launch_score_kernel(gsim_handle* h, const ScoreArgs& a)
 int launch_refresh_scores(gsim_handle* h, int64_t now)
 {
     int rc0 = deliver_flush(h);   // the last round's first deliveries precede the decay
+    if (!rc0) rc0 = gater_decay(h, now);              // the peer gater's decayStats
     if (!rc0) rc0 = deliver_promise_check(h, now);   // broken promises of this heartbeat
     if (rc0) return rc0;
     ScoreArgs a = make_score_args(h, now);
@@ -994,6 +995,7 @@ int gsim_destroy(gsim_handle* h)
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     free_graph(h);
     free_extra(h);
+    free_gater(h);
     free_deliver(h);
     trace_release(h);
     dfree(h->d_tp);
@@ -1055,6 +1057,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     (void)hipStreamSynchronize(h->stream);
     free_graph(h);
     free_extra(h);
+    free_gater(h);
     free_deliver(h);
     trace_release(h);
     h->n = n;

@@ -298,6 +298,26 @@ struct TraceRef {
     }
 };
 
+struct Gater;   // the peer gater's state (gater.hip)
+
+// The peer gater's device state as the delivery kernels see it (gater.hip;
+// act == nullptr: the gater is off).
+struct GaterRef {
+    const uint8_t* act = nullptr;        // [N] the receiver's gate may throttle this round
+    const uint32_t* gq = nullptr;        // [E] record order: the receiver's IP group of the sender (edge order)
+    const double *del = nullptr, *dup = nullptr, *ign = nullptr, *rej = nullptr;
+    unsigned long long* a_del = nullptr; // the round's events
+    uint32_t *a_dup = nullptr, *a_ign = nullptr, *a_rej = nullptr, *a_val = nullptr, *a_thr = nullptr;
+    uint8_t* a_last = nullptr;
+    const unsigned long long* tw = nullptr;   // [T] delivery weights (2^-16 units)
+    double dw = 0, iw = 0, rw = 0;
+    uint64_t seed = 0;
+    unsigned long long* n_thr = nullptr;
+    const uint8_t* direct = nullptr;     // [E] edge order: gs.direct (AcceptFrom: AcceptAll)
+    uint32_t* prom = nullptr;            // [P][E] IWANT promises (ThrottlePeer forgets the peer's)
+    int32_t P = 0;
+};
+
 }  // namespace gsim
 
 struct gsim_handle {
@@ -392,6 +412,7 @@ struct gsim_handle {
     struct Extra* x = nullptr;
     gsim::Deliver* dl = nullptr;
     gsim::ShardCtx* sh = nullptr;   // graph-sharded network: this handle is one shard (shard.hip)
+    struct gsim::Gater* gt = nullptr;   // peer gater (gater.hip), nullptr: off
     gsim::TraceRef trace;           // gsim_trace_config (trace.hip)
 
     // owned peers / observer rows (all of them unless sharded)
@@ -497,6 +518,15 @@ int32_t* deliver_slot_last(gsim_handle* h);           // [ring]
 int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32_t* d_cnt, int64_t cap);
 int deliver_frontier_import(gsim_handle* h, int64_t round, const uint64_t* in, int64_t n);
 void deliver_blocks_changed(gsim_handle* h);          // gsim_set_kernel_variant(h, 6, v)
+// gater.hip: the peer gater (gsim_set_peer_gater)
+gsim::GaterRef gater_ref(gsim_handle* h);
+int gater_round_begin(gsim_handle* h, int64_t now);        // AcceptFrom preamble of the round
+void gater_round_sent(gsim_handle* h, int64_t round);      // the round's events await its commit
+int gater_fold(gsim_handle* h, int64_t round, int64_t now); // after the commit of `round`
+int gater_decay(gsim_handle* h, int64_t now);               // decayStats (at the refresh)
+int gater_connections(gsim_handle* h, const uint32_t* d_edges, int32_t n2, int32_t up, int64_t now);
+void free_gater(gsim_handle* h);
+bool deliver_latency_on(gsim_handle* h);                    // deliver.hip: a vdelay > 0 message was published
 // heartbeat.hip: the control inbox ([2][T][E] by round parity) and its per-receiver summary ([2][N])
 uint8_t* extra_ctl(gsim_handle* h);
 uint64_t* extra_cany(gsim_handle* h);

@@ -2152,6 +2152,8 @@ static int apply_connections(gsim_handle* h, const uint32_t* d_edges, int32_t n2
     hipLaunchKernelGGL(k_churn_apply, dim3(grid), dim3(256), 0, h->stream, a, c);
     const hipError_t e = hipGetLastError();   // stream-ordered: the next call's copy into the scratch follows this kernel
     if (e != hipSuccess) return hip_check(h, e, "k_churn_apply");
+    const int rcg = gater_connections(h, d_edges, n2, up, now);   // the peer gater's AddPeer / RemovePeer
+    if (rcg) return rcg;
     h->p6_dirty = true;          // the tracked set (and so the IP sets) changed
     if (!up) h->maybe_retained = true;
     h->score_version++;          // connected / tracked bits feed the delivery state (churn only clears mesh bits: the masks stay a superset)

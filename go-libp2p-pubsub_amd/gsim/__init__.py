@@ -7,14 +7,15 @@ drives libgsim.so's HIP kernels through the C ABI in include/gsim.h.
 """
 from . import _abi
 from .engine import Engine, GsimError, Network, random_regular
-from .params import (DefaultDecayInterval, DefaultDecayToZero, DefaultGossipSubParams, GossipSubParams, Hour,
-                     Microsecond, Millisecond, Minute, Nanosecond, PeerScoreParams, PeerScoreThresholds,
-                     ScoreParameterDecay, ScoreParameterDecayWithBase, Second, TimeCacheDuration,
-                     TopicScoreParams)
+from .params import (DefaultDecayInterval, DefaultDecayToZero, DefaultGossipSubParams, DefaultPeerGaterParams,
+                     GossipSubParams, Hour, Microsecond, Millisecond, Minute, Nanosecond, NewPeerGaterParams,
+                     PeerGaterParams, PeerScoreParams, PeerScoreThresholds, ScoreParameterDecay,
+                     ScoreParameterDecayWithBase, Second, TimeCacheDuration, TopicScoreParams)
 
 __all__ = [
     "Engine", "GsimError", "Network", "random_regular", "PeerScoreParams", "TopicScoreParams",
     "PeerScoreThresholds", "GossipSubParams", "DefaultGossipSubParams", "ScoreParameterDecay",
     "ScoreParameterDecayWithBase", "Nanosecond", "Microsecond", "Millisecond", "Second", "Minute", "Hour",
-    "DefaultDecayInterval", "DefaultDecayToZero", "TimeCacheDuration", "_abi",
+    "DefaultDecayInterval", "DefaultDecayToZero", "TimeCacheDuration", "PeerGaterParams", "NewPeerGaterParams",
+    "DefaultPeerGaterParams", "_abi",
 ]

@@ -86,6 +86,15 @@ class CGossipSubParams(Structure):
     ]
 
 
+class CPeerGaterParams(Structure):
+    _fields_ = [
+        ("threshold", c_double), ("global_decay", c_double), ("source_decay", c_double),
+        ("decay_interval_ns", c_int64), ("decay_to_zero", c_double), ("retain_stats_ns", c_int64),
+        ("quiet_ns", c_int64), ("duplicate_weight", c_double), ("ignore_weight", c_double),
+        ("reject_weight", c_double),
+    ]
+
+
 # gsim_trace_event (include/gsim.h): TraceEvent.Type values
 TRACE_PUBLISH_MESSAGE, TRACE_REJECT_MESSAGE, TRACE_DUPLICATE_MESSAGE, TRACE_DELIVER_MESSAGE = 0, 1, 2, 3
 TRACE_ADD_PEER, TRACE_REMOVE_PEER, TRACE_GRAFT, TRACE_PRUNE = 4, 5, 11, 12
@@ -241,6 +250,11 @@ SIGNATURES = [
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gsim_read_snapshot", c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
     ("gsim_set_ips", c_int32, [c_void_p, c_void_p, c_void_p, c_uint32]),
+    ("gsim_validate_peer_gater_params", c_int32, [POINTER(CPeerGaterParams), c_char_p, c_size_t]),
+    ("gsim_default_peer_gater_params", c_int32, [c_double, c_double, c_double, POINTER(CPeerGaterParams)]),
+    ("gsim_set_peer_gater", c_int32, [c_void_p, POINTER(CPeerGaterParams), c_void_p]),
+    ("gsim_gater_throttled", c_int32, [c_void_p, POINTER(c_int64)]),
+    ("gsim_gater_read", c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gsim_rccl_unique_id", c_int32, [c_void_p, c_size_t]),
     ("gsim_group_create", c_int32,
      [POINTER(CPeerScoreParams), POINTER(CTopicScoreParams), c_int32, POINTER(CThresholds),

@@ -306,6 +306,38 @@ class Engine:
         p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint32).reshape(-1, 2))
         self._check(self.lib.gsim_set_connections(self.h, _ptr(p), int(p.shape[0]), 1 if up else 0, int(now)))
 
+    def set_peer_gater(self, params, topic_weights=None):
+        """WithPeerGater (peer_gater.go:161-186) on every router (gsim_set_peer_gater):
+        params is a gsim.PeerGaterParams; its TopicDeliveryWeights (topic index ->
+        weight) unless topic_weights ([T]) is given."""
+        c = params.to_c()
+        T = max(1, len(self.topics))
+        w = np.zeros(T, dtype=np.float64)
+        for t, x in (params.TopicDeliveryWeights or {}).items():
+            w[int(t)] = float(x)
+        if topic_weights is not None:
+            w = np.ascontiguousarray(topic_weights, dtype=np.float64)
+        self._check(self.lib.gsim_set_peer_gater(self.h, ctypes.byref(c), _ptr(w)))
+
+    def gater_throttled(self) -> int:
+        """Message copies the peer gater dropped (AcceptControl) so far."""
+        n = ctypes.c_int64(0)
+        self._check(self.lib.gsim_gater_throttled(self.h, ctypes.byref(n)))
+        return n.value
+
+    def gater_read(self) -> dict:
+        """The peer gater's state (gsim_gater_read): validate / throttle / last per
+        router, and per connection (edge order) the IP group's counters
+        [deliver, duplicate, ignore, reject], connected and expire at the group's
+        representative position."""
+        N, E = self.net.n, self.net.e
+        out = {"validate": np.zeros(N), "throttle": np.zeros(N), "last": np.zeros(N, dtype=np.int64),
+               "counters": np.zeros((4, E)), "connected": np.zeros(E, dtype=np.int32),
+               "expire": np.zeros(E, dtype=np.int64)}
+        self._check(self.lib.gsim_gater_read(self.h, _ptr(out["validate"]), _ptr(out["throttle"]), _ptr(out["last"]),
+                                             _ptr(out["counters"]), _ptr(out["connected"]), _ptr(out["expire"])))
+        return out
+
     def px_connect(self, now: int) -> np.ndarray:
         """The connector for the attempts peer exchange queued this tick
         (gsim_px_connect; pxConnect gossipsub.go:893-973): returns the

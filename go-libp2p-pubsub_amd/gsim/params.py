@@ -236,3 +236,52 @@ def ScoreParameterDecay(decay: int) -> float:
 def ScoreParameterDecayWithBase(decay: int, base: int, decayToZero: float) -> float:
     """score_params.go:411-417."""
     return _abi.load().gsim_score_parameter_decay_with_base(int(decay), int(base), float(decayToZero))
+
+
+@dataclass
+class PeerGaterParams:
+    """PeerGaterParams, peer_gater.go:31-55 (durations in ns).  TopicDeliveryWeights
+    maps a topic index to its weight (0 / absent: 1.0; multiples of 2**-16)."""
+    Threshold: float
+    GlobalDecay: float
+    SourceDecay: float
+    DecayInterval: int = Second
+    DecayToZero: float = 0.01
+    RetainStats: int = 6 * Hour
+    Quiet: int = Minute
+    DuplicateWeight: float = 0.125
+    IgnoreWeight: float = 1.0
+    RejectWeight: float = 16.0
+    TopicDeliveryWeights: Dict[int, float] = field(default_factory=dict)
+
+    def to_c(self) -> _abi.CPeerGaterParams:
+        c = _abi.CPeerGaterParams()
+        c.threshold, c.global_decay, c.source_decay = self.Threshold, self.GlobalDecay, self.SourceDecay
+        c.decay_interval_ns, c.decay_to_zero = int(self.DecayInterval), self.DecayToZero
+        c.retain_stats_ns, c.quiet_ns = int(self.RetainStats), int(self.Quiet)
+        c.duplicate_weight, c.ignore_weight, c.reject_weight = (self.DuplicateWeight, self.IgnoreWeight,
+                                                                self.RejectWeight)
+        return c
+
+    def validate(self) -> None:
+        """PeerGaterParams.validate (peer_gater.go:57-90)."""
+        buf = ctypes.create_string_buffer(256)
+        c = self.to_c()
+        if _abi.load().gsim_validate_peer_gater_params(ctypes.byref(c), buf, len(buf)) != 0:
+            raise ValueError(buf.value.decode())
+
+
+def NewPeerGaterParams(threshold: float, globalDecay: float, sourceDecay: float) -> PeerGaterParams:
+    """NewPeerGaterParams (peer_gater.go:99-111), defaults from the engine library."""
+    c = _abi.CPeerGaterParams()
+    _abi.load().gsim_default_peer_gater_params(threshold, globalDecay, sourceDecay, ctypes.byref(c))
+    return PeerGaterParams(Threshold=c.threshold, GlobalDecay=c.global_decay, SourceDecay=c.source_decay,
+                           DecayInterval=c.decay_interval_ns, DecayToZero=c.decay_to_zero,
+                           RetainStats=c.retain_stats_ns, Quiet=c.quiet_ns, DuplicateWeight=c.duplicate_weight,
+                           IgnoreWeight=c.ignore_weight, RejectWeight=c.reject_weight)
+
+
+def DefaultPeerGaterParams() -> PeerGaterParams:
+    """DefaultPeerGaterParams (peer_gater.go:113-116): Threshold 0.33, GlobalDecay
+    ScoreParameterDecay(2m), SourceDecay ScoreParameterDecay(1h)."""
+    return NewPeerGaterParams(0.33, ScoreParameterDecay(2 * Minute), ScoreParameterDecay(Hour))

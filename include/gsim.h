@@ -276,6 +276,56 @@ int gsim_px_connect(gsim_handle* h, int64_t now_ns, uint32_t* pairs, int64_t cap
  * restricted to messages that can still arrive.  Publishing into a slot ends
  * the propagation of its previous message; SeenMsgTTL and the ring must
  * outlast a message's propagation (they do for every reference configuration). */
+/* ---- peer gater (peer_gater.go) ------------------------------------------
+ * WithPeerGater(params) (peer_gater.go:161-186): every router's AcceptFrom
+ * adds the random-early-drop gate of peer_gater.go:320-363 behind the
+ * graylist (gossipsub.go:598-609): once the router's validation throttles
+ * (a message with GSIM_VERDICT_THROTTLE) and throttle/validate reaches
+ * Threshold within Quiet of the last throttle, a message from a peer is
+ * accepted with probability (1 + deliver) / (1 + weighted total) of its
+ * IP's counters, else dropped (AcceptControl; the receiver's IWANT promises
+ * from that peer are forgotten, gossip_tracer.go:182-200).  Field for field
+ * PeerGaterParams (peer_gater.go:31-55); durations in ns.  Restatement
+ * (DESIGN.md §3.9 step 7): the gate is drawn per message copy (Philox), a
+ * round's tracer events are added to the counters at the end of the round,
+ * TopicDeliveryWeights in 2^-16 units, decayStats at every score refresh
+ * (DecayInterval must equal the heartbeat interval); single engine, no
+ * validation latency. */
+typedef struct gsim_peer_gater_params {
+    double threshold;          /* Threshold: throttle / validate ratio that turns the gate on */
+    double global_decay;       /* GlobalDecay (validate, throttle) */
+    double source_decay;       /* SourceDecay (per-IP counters) */
+    int64_t decay_interval_ns; /* DecayInterval */
+    double decay_to_zero;      /* DecayToZero */
+    int64_t retain_stats_ns;   /* RetainStats: an IP's stats after its last peer left */
+    int64_t quiet_ns;          /* Quiet: the gate turns off this long after the last throttle */
+    double duplicate_weight;   /* DuplicateWeight */
+    double ignore_weight;      /* IgnoreWeight */
+    double reject_weight;      /* RejectWeight */
+} gsim_peer_gater_params;
+
+/* PeerGaterParams.validate (peer_gater.go:57-90), the reference's messages. */
+int gsim_validate_peer_gater_params(const gsim_peer_gater_params* p, char* err, size_t errlen);
+/* NewPeerGaterParams(threshold, globalDecay, sourceDecay) defaults (peer_gater.go:99-111). */
+int gsim_default_peer_gater_params(double threshold, double global_decay, double source_decay,
+                                   gsim_peer_gater_params* out);
+/* Turn the gater on for every router (after gsim_msgs_init).  topic_weights:
+ * TopicDeliveryWeights per topic index ([T], 0 = 1.0; multiples of 2^-16),
+ * or NULL.  GSIM_EINVAL: invalid params or weights; GSIM_ESTATE: a shard,
+ * a message with validation latency published, or DecayInterval not the
+ * heartbeat interval. */
+int gsim_set_peer_gater(gsim_handle* h, const gsim_peer_gater_params* p, const double* topic_weights);
+/* Message copies dropped by the gate (AcceptControl) so far. */
+int gsim_gater_throttled(gsim_handle* h, int64_t* out);
+/* The gater state (host buffers, each may be NULL): per router validate,
+ * throttle [N] and lastThrottle [N] (INT64_MIN: never); per connection
+ * e (edge order) the counters deliver, duplicate, ignore, reject [4][E],
+ * connected [E] and expire [E] of its IP group, held at the group's
+ * representative edge (the row's lowest position of that IP; other
+ * positions read 0). */
+int gsim_gater_read(gsim_handle* h, double* validate, double* throttle, int64_t* last, double* counters4,
+                    int32_t* connected, int64_t* expire);
+
 typedef struct gsim_msg_config {
     int32_t ring;            /* message slots (live-message window), 1..8192 */
     int32_t rounds;          /* propagation rounds per heartbeat, >= 2 */

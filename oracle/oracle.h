@@ -61,6 +61,7 @@ typedef struct orc_net {
     const uint8_t* direct;     /* [E] col[e] is in the observer's gs.direct set (WithDirectPeers), or NULL */
     uint8_t* px;               /* [E] peer exchange (WithPeerExchange): 1 = the row's owner tries to
                                   connect to col[e] (pxConnect), or NULL */
+    struct orc_gater* gater;   /* peer gater (oracle_gater.c, orc_gater_new), or NULL */
 } orc_net;
 
 /* ---- message propagation (oracle_deliver.c) ------------------------------ */
@@ -207,6 +208,7 @@ enum {
     ORC_EV_PRUNE = 13,       /* a: router, b: peer, topic, x: now  tracer.Prune      */
     ORC_EV_ADD_PEER = 14,    /* a: router, b: peer, x: now                           */
     ORC_EV_REMOVE_PEER = 15, /* a: router, b: peer, x: now                           */
+    ORC_EV_THROTTLE = 16,    /* a: receiver, b: sender, x: now: AcceptControl -> ThrottlePeer */
 };
 typedef struct orc_event { int32_t kind, topic; uint32_t a, b; int64_t g; uint64_t mid; int64_t x; } orc_event;
 void    orc_msgs_log(orc_msgs* m, int32_t on);
@@ -246,6 +248,25 @@ void orc_tcache_free(orc_tcache* c);
 int  orc_tcache_add(orc_tcache* c, uint64_t id, int64_t now);  /* first_seen_cache.go:47-56 / last_seen_cache.go:38-45 */
 int  orc_tcache_has(orc_tcache* c, uint64_t id, int64_t now);  /* first_seen_cache.go:37-45 / last_seen_cache.go:47-58 */
 void orc_tcache_sweep(orc_tcache* c, int64_t now);             /* timecache/util.go:26-35 */
+
+/* ---- peer gater (oracle_gater.c, peer_gater.go) ------------------------- */
+typedef struct orc_gater orc_gater;
+enum { ORC_GATE_VALIDATE = 0, ORC_GATE_DELIVER, ORC_GATE_DUPLICATE, ORC_GATE_IGNORE, ORC_GATE_REJECT,
+       ORC_GATE_THROTTLE };
+int orc_gater_validate(const gsim_peer_gater_params* p);                /* peer_gater.go:57-90 */
+uint64_t orc_gater_weight_fp(double w);
+orc_gater* orc_gater_new(orc_net* s, const gsim_peer_gater_params* p, const double* topic_w);   /* sets s->gater */
+void orc_gater_free(orc_gater* g);
+void orc_gater_round_begin(orc_net* s, int64_t now);                    /* AcceptFrom preamble :327-343 */
+double orc_gater_uniform(uint64_t seed, int64_t g, uint32_t recv, uint32_t slot, uint32_t sender);
+int orc_gater_accept(orc_net* s, uint64_t seed, int64_t g, uint32_t i, uint32_t er, uint32_t slot);   /* :320-363 */
+void orc_gater_event(orc_net* s, uint32_t i, uint32_t er, int32_t topic, int32_t kind);   /* :386-432 */
+void orc_gater_round_end(orc_net* s, int64_t now);
+void orc_gater_decay(orc_net* s, int64_t now);                          /* decayStats :207-241 */
+void orc_gater_connection(orc_net* s, int64_t e, int32_t up, int64_t now);   /* AddPeer/RemovePeer :366-384 */
+int64_t orc_gater_throttled(const orc_gater* g);
+void orc_gater_read(const orc_gater* g, double* val, double* thr, int64_t* last, double* counters4, int32_t* con,
+                    int64_t* exp);
 
 /* ---- Philox4x32-10 (the canonical selection stream) ----- */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

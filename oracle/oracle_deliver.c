@@ -243,6 +243,7 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
     const double gray = s->th->graylist_threshold;
 
     if (p->npq) complete_validations(s, m, g, now);
+    orc_gater_round_begin(s, now);
 
     /* 1. last round's first receivers (and publishers) forward to their mesh */
     for (int64_t q = 0; q < p->nfp; ++q) {
@@ -287,10 +288,24 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
             m->stats[3]++;
             continue;
         }
+        if (s->gater && !(s->direct && s->direct[er]) && !orc_gater_accept(s, p->seed, g, i, er, slot)) {
+            /* the peer gater's AcceptControl: the message is dropped and the
+             * receiver forgets its promises from the sender (ThrottlePeer,
+             * gossip_tracer.go:182-200) */
+            if (p->npr) {
+                int32_t w = 0;
+                for (int32_t q2 = 0; q2 < p->npr[i]; ++q2)
+                    if (p->pr[i][q2].e != er) p->pr[i][w++] = p->pr[i][q2];
+                p->npr[i] = w;
+            }
+            orc_log(m, ORC_EV_THROTTLE, i, s->col[er], slot, t, g, now);
+            continue;
+        }
         m->stats[0]++;
         uint32_t* cell = &m->seen[(int64_t)slot * s->n + i];
         const uint8_t verdict = m->invalid[slot];
         if (verdict == GSIM_VERDICT_SIGNATURE) {
+            orc_gater_event(s, i, er, t, ORC_GATE_REJECT);      /* RejectInvalidSignature */
             /* RejectInvalidSignature before markSeen (validation.go:282-290):
              * every copy's sender is penalised, nothing is seen, no promise is
              * fulfilled (gossip_tracer.go:148-162) */
@@ -301,6 +316,12 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
         }
         const uint8_t vdelay = p->vd ? p->vd[slot] : 0;
         if (!vdelay || *cell != UNSEEN) orc_log(m, ORC_EV_SEEN, i, s->col[er], slot, t, g, *cell == UNSEEN);
+        if (s->gater) {
+            /* first delivery: ValidateMessage, then the verdict's tracer call */
+            static const int32_t kind[4] = {ORC_GATE_DELIVER, ORC_GATE_REJECT, ORC_GATE_IGNORE, ORC_GATE_THROTTLE};
+            if (*cell == UNSEEN) orc_gater_event(s, i, er, t, ORC_GATE_VALIDATE);
+            orc_gater_event(s, i, er, t, *cell == UNSEEN ? kind[verdict] : ORC_GATE_DUPLICATE);
+        }
         if (*cell == UNSEEN && vdelay) {
             /* markSeen + ValidateMessage (promises fulfilled); the verdict
              * lands vdelay rounds later (complete_validations) */
@@ -339,6 +360,7 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
         }
     }
     free(ar);
+    orc_gater_round_end(s, now);
 
     /* 3. control records of this round: GRAFT/PRUNE, then IHAVE (round 0)
      * and IWANT (round 1) */

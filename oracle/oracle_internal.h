@@ -21,6 +21,7 @@ enum {
     P_FANOUT = 13,      /* heartbeat: getPeers for the fanout top-up  gossipsub.go:1578-1585 */
     P_PX = 14,          /* makePrune: getPeers for PX (heartbeat)      gossipsub.go:1879-1882 */
     P_PX_GRAFT = 15,    /* makePrune: getPeers for PX (GRAFT reply)    gossipsub.go:831-834 */
+    P_GATER = 16,       /* peer gater: rand.Float64() of AcceptFrom    peer_gater.go:357 */
 };
 
 static inline uint64_t okey(uint64_t seed, uint64_t tick, uint32_t obs, int32_t topic, uint32_t purpose,

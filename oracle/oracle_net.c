@@ -543,6 +543,7 @@ int32_t orc_churn(orc_net* s, const uint32_t* pairs, int32_t count, int32_t up, 
             const uint32_t o = pairs[2 * q + d], p = pairs[2 * q + 1 - d];
             const int64_t e = find_edge(s, o, p);
             orc_log_net(up ? ORC_EV_ADD_PEER : ORC_EV_REMOVE_PEER, o, p, -1, now);
+            orc_gater_connection(s, e, up, now);
             if (up) {
                 orc_add_peer(s, e);
                 continue;

@@ -33,7 +33,7 @@ class OrcNet(Structure):
         ("backoff", c_void_p),
         ("pp", c_void_p), ("tp", c_void_p), ("th", c_void_p), ("gp", c_void_p),
         ("ctl", c_void_p), ("lastpub", c_void_p), ("fan_topics", c_void_p), ("direct", c_void_p),
-        ("px", c_void_p),
+        ("px", c_void_p), ("gater", c_void_p),
     ]
 
 
@@ -115,6 +115,18 @@ def load():
             "orc_heartbeat_gossip": (None, [P, POINTER(OrcMsgs), c_uint64, c_int64, c_uint64]),
             "orc_gossip_penalties": (None, [P, POINTER(OrcMsgs), c_int64]),
             "orc_px_connect": (c_int64, [P, c_int64, c_void_p, c_int64]),
+            "orc_gater_validate": (c_int32, [POINTER(_abi.CPeerGaterParams)]),
+            "orc_gater_new": (c_void_p, [P, POINTER(_abi.CPeerGaterParams), c_void_p]),
+            "orc_gater_free": (None, [c_void_p]),
+            "orc_gater_round_begin": (None, [P, c_int64]),
+            "orc_gater_accept": (c_int32, [P, c_uint64, c_int64, c_uint32, c_uint32, c_uint32]),
+            "orc_gater_event": (None, [P, c_uint32, c_uint32, c_int32, c_int32]),
+            "orc_gater_round_end": (None, [P, c_int64]),
+            "orc_gater_decay": (None, [P, c_int64]),
+            "orc_gater_connection": (None, [P, c_int64, c_int32, c_int64]),
+            "orc_gater_throttled": (c_int64, [c_void_p]),
+            "orc_gater_read": (None, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+            "orc_gater_uniform": (ctypes.c_double, [c_uint64, c_int64, c_uint32, c_uint32, c_uint32]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -166,6 +178,7 @@ class NetState:
         self.tp = params.topic_array(self.topics)
         self.th = (thresholds or PeerScoreThresholds()).to_c()
         self.gp = (gossip or GossipSubParams()).to_c()
+        self.gater = None            # orc_gater* (enable_gater)
         self._view = None
 
     def view(self):
@@ -190,8 +203,40 @@ class NetState:
         v.lastpub, v.fan_topics = _p(self.lastpub), _p(self.fan_topics)
         v.direct = _p(self.direct)
         v.px = _p(self.px)
+        v.gater = self.gater
         self._view = v
         return ctypes.byref(v)
+
+    # ---- peer gater (oracle_gater.c) ----
+    GATE_VALIDATE, GATE_DELIVER, GATE_DUPLICATE, GATE_IGNORE, GATE_REJECT, GATE_THROTTLE = range(6)
+
+    def enable_gater(self, params, topic_weights=None):
+        """orc_gater_new: WithPeerGater on every router of the oracle network."""
+        c = params.to_c()
+        T = max(1, len(self.topics))
+        w = np.zeros(T, dtype=np.float64)
+        for t, x in (params.TopicDeliveryWeights or {}).items():
+            w[int(t)] = float(x)
+        if topic_weights is not None:
+            w = np.ascontiguousarray(topic_weights, dtype=np.float64)
+        self._gater_w = w
+        self.gater = None
+        self.gater = load().orc_gater_new(self.view(), ctypes.byref(c), _p(w))
+
+    def gater_decay(self, now):
+        load().orc_gater_decay(self.view(), int(now))
+
+    def gater_read(self) -> dict:
+        N, E = self.net.n, self.net.e
+        out = {"validate": np.zeros(N), "throttle": np.zeros(N), "last": np.zeros(N, dtype=np.int64),
+               "counters": np.zeros((4, E)), "connected": np.zeros(E, dtype=np.int32),
+               "expire": np.zeros(E, dtype=np.int64)}
+        load().orc_gater_read(self.gater, _p(out["validate"]), _p(out["throttle"]), _p(out["last"]),
+                              _p(out["counters"]), _p(out["connected"]), _p(out["expire"]))
+        return out
+
+    def gater_throttled(self) -> int:
+        return int(load().orc_gater_throttled(self.gater))
 
     def copy_fields_from(self, other):
         for f in self.TOPIC_FIELDS + self.EDGE_FIELDS:

@@ -61,7 +61,8 @@ def oracle_trace(ev, msgs, lo, hi):
 
 
 def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, churn=None, after_tick=None,
-               eng=None, after_heartbeat=None, px_log=None, trace=None, trace_log=None, topic_slots=0):
+               eng=None, after_heartbeat=None, px_log=None, trace=None, trace_log=None, topic_slots=0, gater=None,
+               gater_log=None):
     """Run `ticks` on a fresh engine loaded with `st`'s state and on the
     oracle; assert identical state, seen-set and totals after every tick.
     churn: {tick: [(pairs, up), ...]} applied just before the tick.
@@ -73,7 +74,10 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
     and its events must equal the oracle's event log per tick (the event
     counts appended to trace_log).  topic_slots > 0: per-topic sub-rings of
     that many slots (ring = T * topic_slots) with member-compacted seen-set
-    cells (gsim_msg_config.topic_slots), on both sides."""
+    cells (gsim_msg_config.topic_slots), on both sides.  gater: a
+    gsim.PeerGaterParams turned on at both sides (WithPeerGater); its state
+    and the copies it dropped must agree after every tick (the per-tick drop
+    counts appended to gater_log)."""
     from gsim.engine import Engine
     pushed = eng is None
     if eng is None:
@@ -92,6 +96,9 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
             msgs.log()
         if behaviour is not None:
             eng.set_peer_behaviour(behaviour)
+        if gater is not None:
+            eng.set_peer_gater(gater)
+            st.enable_gater(gater)
         lib = ob.load()
         for kk in ticks:
             now = tick_time(kk)
@@ -102,6 +109,8 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
             eng.heartbeat(kk, now)
             v = st.view()
             lib.orc_refresh_scores(v, now)
+            if gater is not None:
+                st.gater_decay(now)
             msgs.penalties(st, now)
             lib.orc_ip_colocation(v)
             lib.orc_compute_scores(v)
@@ -130,6 +139,17 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
                     assert len(bad) == 0, f"trace field {f} differs at tick {kk}: first at {bad[:1]}"
                 if trace_log is not None:
                     trace_log.append(np.bincount(want["type"], minlength=13))
+            if gater is not None:
+                got, want = eng.gater_read(), st.gater_read()
+                for f in want:
+                    a_, b_ = got[f], want[f]
+                    if a_.dtype.itemsize == 8:
+                        a_, b_ = a_.view(np.uint64), b_.view(np.uint64)
+                    bad = np.argwhere(a_ != b_)
+                    assert len(bad) == 0, f"gater {f} differs at tick {kk}: first at {bad[:1].tolist()}"
+                assert eng.gater_throttled() == st.gater_throttled(), f"gater drops differ at tick {kk}"
+                if gater_log is not None:
+                    gater_log.append(st.gater_throttled())
             if gp.PeerExchange:
                 t_px = now + Second // 2
                 got, want = eng.px_connect(t_px), st.px_connect(t_px)
