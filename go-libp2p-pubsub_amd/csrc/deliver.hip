@@ -228,6 +228,7 @@ struct RoundArgs {
     int64_t ncells;                // cells of the seen-set (the last slot's end)
     int32_t topic_slots;           // sub-rings: slots [t R, t R + R) carry topic t (0: one shared ring)
     GaterRef gt;                   // peer gater (gater.hip; gt.act == nullptr: off)
+    int32_t subdyn;                // a Leave happened: a receiver drops copies of topics it left
 };
 
 // The peer gater's AcceptFrom (peer_gater.go:320-363) at receiver i for a
@@ -402,7 +403,7 @@ __device__ __forceinline__ int active_slots(const uint32_t* nnew, int ring, uint
 
 // Commit one claimed cell of round gc (markSeen + the winner's P2/P3 credit,
 // markFirstMessageDelivery score.go:919-946; mcache.Put for lastput).
-template <bool ATOMIC = false, bool LAT = false, bool SP = true>
+template <bool ATOMIC = false, bool LAT = false, bool SP = true, bool GT = false>
 __device__ __forceinline__ void commit_claim(const RoundArgs& a, uint64_t* cellp, uint64_t c, int64_t gc,
                                              uint32_t m, int64_t peer, int* qpl = nullptr, uint64_t* qv = nullptr)
 {
@@ -427,7 +428,7 @@ __device__ __forceinline__ void commit_claim(const RoundArgs& a, uint64_t* cellp
     } else {
         *cellp = ((uint64_t)(uint32_t)gc << 32) | (lo & kPeerMask);
     }
-    if (a.gt.act) gater_first(a, hi & kEdgeMask, (uint32_t)peer, (int32_t)a.mtopic[m], a.minv[m]);
+    if constexpr (GT) gater_first(a, hi & kEdgeMask, (uint32_t)peer, (int32_t)a.mtopic[m], a.minv[m]);
     if (a.minv[m]) return;                                // RejectMessage: counted when sent
     const int32_t t = (int32_t)a.mtopic[m];
     int32_t* lp = a.lastput + (int64_t)t * a.N + peer;
@@ -955,8 +956,10 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             if (!ok) continue;
                             if constexpr (GT) {                  // the peer gater (gater_accept)
                                 if (!gater_accept(a, i, e, m, j)) continue;
-                                gater_copy(a, e, !seeable);
                             }
+                            // a topic the receiver left: skipped (pubsub.go:1094-1098)
+                            if (a.subdyn && !((a.sub[i] >> t) & 1ull)) continue;
+                            if constexpr (GT) gater_copy(a, e, !seeable);
                             n_acc++;
                             if (a.tr.on(i))
                                 a.tr.push(round_time(a, a.g), ((uint64_t)a.g << 32) | m, i, j, t,
@@ -1082,7 +1085,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
 
 // Commit every claim of round g (markSeen + P2 credit) before the state is
 // read or changed by anything but the next round.
-template <bool LAT, bool SP>
+template <bool LAT, bool SP, bool GT = false>
 __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
 {
     extern __shared__ uint16_t s_act[];
@@ -1131,7 +1134,7 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
             if (is_claim_of(cv[b], par)) {
                 const uint32_t m = s_act[k];
                 uint64_t* cp = a.cs.cell + (SP ? ci[b] : (int64_t)m * a.cs.n + i);
-                commit_claim<false, LAT, SP>(a, cp, cv[b], a.g, m, i, &qpl, &qv);
+                commit_claim<false, LAT, SP, GT>(a, cp, cv[b], a.g, m, i, &qpl, &qv);
             }
             if constexpr (LAT) vq_push_wave(a, qpl, qv);
         }
@@ -1163,7 +1166,8 @@ __global__ __launch_bounds__(256) void k_commit_list(RoundArgs a)
         const uint64_t bit = 1ull << (i & 63);
         atomicOr(reinterpret_cast<unsigned long long*>(a.seenbm + (int64_t)m * a.nw + w), bit);
         if (a.fresh && a.minv[m] == GSIM_VERDICT_ACCEPT) fresh_set(a, m, w, bit);
-        commit_claim<true, false, SP>(a, cp, c, a.g, m, i);
+        if (a.gt.act) commit_claim<true, false, SP, true>(a, cp, c, a.g, m, i);
+        else commit_claim<true, false, SP>(a, cp, c, a.g, m, i);
     }
 }
 
@@ -1834,10 +1838,9 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
         const uint8_t ds = a.dstate[r];
         if (!(ds & GSIM_DS_ACCEPT)) { n_gray++; continue; }        // AcceptFrom
         const uint32_t p = a.col[r], i = owner[r];
-        if (a.gt.act) {                                            // the peer gater (gater_accept)
-            if (!gater_accept(a, p, r, m, i)) continue;
-            gater_copy(a, r, a.minv[m] == GSIM_VERDICT_SIGNATURE);
-        }
+        if (a.gt.act && !gater_accept(a, p, r, m, i)) continue;   // the peer gater (gater_accept)
+        if (a.subdyn && !((a.sub[p] >> (int32_t)a.mtopic[m]) & 1ull)) continue;   // a topic p left
+        if (a.gt.act) gater_copy(a, r, a.minv[m] == GSIM_VERDICT_SIGNATURE);
         n_acc++;
         const int32_t t = (int32_t)a.mtopic[m];
         const ctp_t tp = tpa + t;
@@ -2151,6 +2154,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.nsw = (a.nw + 63) / 64;
     a.ncells = (int64_t)d->n_cells;
     a.gt = gater_ref(h);
+    a.subdyn = h->sub_dynamic ? 1 : 0;
     if (a.gt.act) { a.gt.prom = d->d_prom; a.gt.P = d->prom_ticks; }
     a.topic_slots = d->cfg.topic_slots > 0 ? (int32_t)d->cfg.topic_slots : 0;
     if (list_commit(h)) {
@@ -2399,6 +2403,10 @@ int deliver_flush(gsim_handle* h)
         hipLaunchKernelGGL(k_commit_list<true>, dim3(64, kClSub), dim3(256), 0, h->stream, a);
     if (a.mlat)
         hipLaunchKernelGGL((k_commit<true, true>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
+    else if (a.gt.act && sparse_layout(h))
+        hipLaunchKernelGGL((k_commit<false, true, true>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
+    else if (a.gt.act)
+        hipLaunchKernelGGL((k_commit<false, false, true>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     else if (sparse_layout(h))
         hipLaunchKernelGGL((k_commit<false, true>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     else

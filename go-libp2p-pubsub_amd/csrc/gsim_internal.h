@@ -352,6 +352,7 @@ struct gsim_handle {
     // topics only), so they stay zero and the score pass may skip them.
     bool unjoined_zero = false;
     bool all_joined = false;     // every peer announced every topic (nothing to skip)
+    bool sub_dynamic = false;    // a Leave happened: receivers check the copy's topic (gsim_set_subscriptions)
     std::vector<int64_t> topic_subs;   // [T] local peers that joined each topic (k_send_tm's block shares)
     bool tm_uniform = false;  // k_send_tm blocks the same for every topic (gsim_set_kernel_variant(h, 6, 1))
     int64_t tm_budget = 0;    // k_send_tm blocks in all (0: ranges x T, launch_send_tm_tb)

@@ -70,6 +70,7 @@ struct HbArgs {
     int32_t D, Dlo, Dhi, Dscore, Dout, opp_peers;
     uint64_t opp_ticks;
     int64_t prune_backoff, graft_flood;
+    int64_t unsub_backoff;     // UnsubscribeBackoff (Leave's PRUNE, GSIM_CTL_UNSUB)
     double opp_threshold;
     // emitGossip (gossipsub.go:1711-1775); gossip == false before gsim_msgs_init
     bool gossip;
@@ -1295,7 +1296,8 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
                         if (fl & GSIM_TF_MESH) delta -= 1;
                         stats_prune(a, tracked, scored, thr, mcap, sf);
                         fl &= (uint8_t)~GSIM_TF_MESH;
-                        const int64_t secs = a.prune_backoff / kSecond;
+                        // the PRUNE's Backoff: PruneBackoff/1s, or UnsubscribeBackoff/1s for Leave's
+                        const int64_t secs = ((c & GSIM_CTL_UNSUB) ? a.unsub_backoff : a.prune_backoff) / kSecond;
                         const int64_t ex = a.now + (secs > 0 ? secs * kSecond : a.prune_backoff);
                         if (bo < ex) bo = ex;
                     }
@@ -1593,6 +1595,109 @@ struct ChurnArgs {
 // The observer's edge to the other end of each (pair, direction), by binary
 // search in the observer's sorted row; *bad = lowest pair that is not a
 // connection.
+// Join / Leave (gossipsub.go:1047-1124) of the (peer, topic) pairs in order:
+// one thread, because each change is seen by the later ones (the topic peers
+// of a Join include the peers that joined before it), as in the oracle's
+// orc_set_subscriptions.  Rare and between ticks.
+__device__ __forceinline__ bool sub_topic_peer(const HbArgs& a, uint64_t* sub, uint32_t e, int32_t t)
+{
+    return (a.rstate[e] & GSIM_ES_CONNECTED) && ((sub[a.col[e]] >> t) & 1ull);
+}
+
+__global__ void k_subscribe(HbArgs a, uint64_t* sub, const uint32_t* pairs, int32_t count, int32_t join)
+{
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    for (int32_t q = 0; q < count; ++q) {
+        const uint32_t p = pairs[2 * q];
+        const int32_t t = (int32_t)pairs[2 * q + 1];
+        const uint64_t bit = 1ull << t;
+        const uint32_t b = a.row_ptr[p], en = a.row_ptr[p + 1];
+        const uint64_t mi = smask_of(a.smask, p);           // p's router state (its slots: gsim_set_subscriptions grew them)
+        const uint32_t gp_ = glob(a, p);
+        auto mf = [&](uint32_t e) -> uint8_t& { return a.mflags[slot_idx(mi, t, a.E, e)]; };
+        auto bo = [&](uint32_t e) -> int64_t& { return a.backoff[slot_idx(mi, t, a.E, e)]; };
+        auto send = [&](uint32_t e, uint8_t bits) {
+            const uint32_t c = a.col[e];
+            const uint64_t mq = smask_of(a.smask, c);
+            if (!slot_has(mq, t)) return;
+            const int64_t r = slot_idx(mq, t, a.E, a.rev[e]);   // the receiver's inbox entry
+            a.ctl_out[r] = (uint8_t)(a.ctl_out[r] | bits);
+            atomicOr(reinterpret_cast<unsigned long long*>(a.cany_out + c), bit);
+        };
+        const ctp_t tp = const_tp(a.tp) + t;
+        if (join) {
+            if (sub[p] & bit) continue;                      // gs.mesh[topic] exists
+            sub[p] |= bit;                                   // the announcement
+            if (a.tr.on(p)) a.tr.push(a.now, 0, p, p, t, GSIM_TRACE_JOIN, 0);
+            // getPeers: the `count` candidates with the smallest keys, in key order
+            auto pick = [&](int count, bool more) {
+                uint64_t last = 0;
+                bool first_pick = true;
+                for (int k = 0; k < count; ++k) {
+                    uint64_t best = ~0ull;
+                    uint32_t be = 0xFFFFFFFFu;
+                    for (uint32_t e = b; e < en; ++e) {
+                        if (!sub_topic_peer(a, sub, e, t)) continue;
+                        if (a.direct[e] || bo(e) != 0 || a.score[a.rev[e]] < 0.0) continue;
+                        if (more && (mf(e) & GSIM_TF_FANOUT)) continue;
+                        const uint64_t key = hb_key(a, gp_, t, P_JOIN, glob(a, a.col[e]), e - b);
+                        if ((!first_pick && key <= last) || key >= best) continue;
+                        best = key;
+                        be = e;
+                    }
+                    if (be == 0xFFFFFFFFu) break;
+                    last = best;
+                    first_pick = false;
+                    mf(be) |= more ? GSIM_TF_FANOUT : GSIM_TF_MESH;
+                }
+            };
+            if ((a.fan_topics[p] >> t) & 1ull) {
+                int have = 0;
+                for (uint32_t e = b; e < en; ++e) {
+                    if (!(mf(e) & GSIM_TF_FANOUT)) continue;
+                    if (a.score[a.rev[e]] < 0.0 || bo(e) != 0) mf(e) &= (uint8_t)~GSIM_TF_FANOUT;
+                    else ++have;
+                }
+                if (have < a.D) pick(a.D - have, true);
+                for (uint32_t e = b; e < en; ++e)
+                    if (mf(e) & GSIM_TF_FANOUT) mf(e) = (uint8_t)((mf(e) & ~GSIM_TF_FANOUT) | GSIM_TF_MESH);
+                a.fan_topics[p] &= ~bit;                     // delete(gs.fanout, topic), delete(gs.lastpub, topic)
+                a.lastpub[(int64_t)p * a.T + t] = 0;
+            } else {
+                pick(a.D, false);
+            }
+            for (uint32_t e = b; e < en; ++e) {
+                if (!(mf(e) & GSIM_TF_MESH)) continue;
+                if (a.tr.on(p)) a.tr.push(a.now, 0, p, a.col[e], t, GSIM_TRACE_GRAFT, 0);   // tracer.Graft
+                const uint32_t rv = a.rev[e];
+                ScoreFlags sf;
+                sf.at(smask_of(a.smask, a.col[e]), t, a.E, rv);
+                stats_graft(a, (a.estate[rv] & GSIM_ES_TRACKED) != 0, tp->scored != 0, sf);
+                sf.store(a);
+                send(e, GSIM_CTL_GRAFT);
+            }
+        } else {
+            if (!(sub[p] & bit)) continue;                   // no mesh for the topic
+            sub[p] &= ~bit;
+            if (a.tr.on(p)) a.tr.push(a.now, 0, p, p, t, GSIM_TRACE_LEAVE, 0);
+            for (uint32_t e = b; e < en; ++e) {
+                if (!(mf(e) & GSIM_TF_MESH)) continue;
+                if (a.tr.on(p)) a.tr.push(a.now, 0, p, a.col[e], t, GSIM_TRACE_PRUNE, 0);   // tracer.Prune
+                const uint32_t rv = a.rev[e];
+                ScoreFlags sf;
+                sf.at(smask_of(a.smask, a.col[e]), t, a.E, rv);
+                stats_prune(a, (a.estate[rv] & GSIM_ES_TRACKED) != 0, tp->scored != 0,
+                            tp->mesh_message_deliveries_threshold, tp->mesh_message_deliveries_cap, sf);
+                sf.store(a);
+                mf(e) &= (uint8_t)~GSIM_TF_MESH;
+                send(e, GSIM_CTL_PRUNE | GSIM_CTL_UNSUB);
+                const int64_t ex = a.now + a.unsub_backoff;   // addBackoff(p, topic, isUnsubscribe)
+                if (bo(e) < ex) bo(e) = ex;
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_churn_find(const uint32_t* row_ptr, const uint32_t* col, int64_t N,
                                                     const uint32_t* pairs, int32_t n2, uint32_t* edges,
                                                     uint32_t* bad)
@@ -1925,6 +2030,7 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.D = h->gp.d; a.Dlo = h->gp.dlo; a.Dhi = h->gp.dhi; a.Dscore = h->gp.dscore; a.Dout = h->gp.dout;
     a.opp_peers = h->gp.opportunistic_graft_peers; a.opp_ticks = h->gp.opportunistic_graft_ticks;
     a.prune_backoff = h->gp.prune_backoff_ns; a.graft_flood = h->gp.graft_flood_threshold_ns;
+    a.unsub_backoff = h->gp.unsubscribe_backoff_ns;
     a.opp_threshold = h->th.opportunistic_graft_threshold;
     GossipView gv{};
     a.gossip = deliver_gossip_view(h, &gv);
@@ -2216,6 +2322,58 @@ int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, i
         return GSIM_EINVAL;
     }
     return apply_connections(h, d_edges, n2, up, now);
+}
+
+int gsim_set_subscriptions(gsim_handle* h, const uint32_t* pairs, int32_t count, int32_t join, uint64_t tick,
+                           int64_t now)
+{
+    if (!h) return GSIM_EINVAL;
+    if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
+    if (h->e == 0 || !h->x) { h->err = "no graph loaded"; return GSIM_ESTATE; }
+    if (h->sh) { h->err = "subscription changes run on a single engine, not a shard"; return GSIM_ESTATE; }
+    if (count < 0 || (count > 0 && !pairs)) { h->err = "bad subscription list"; return GSIM_EINVAL; }
+    if (count == 0) return GSIM_OK;
+    const int32_t T = std::max(1, h->t);
+    std::vector<uint64_t> need;
+    for (int32_t q = 0; q < count; ++q) {
+        if ((int64_t)pairs[2 * q] >= h->n || (int32_t)pairs[2 * q + 1] >= T) {
+            h->err = "subscription pair out of range";
+            return GSIM_EINVAL;
+        }
+        // a joining peer's router state for the topic lives in its topic slot
+        if (join && !h->smask.empty() && !((h->smask[pairs[2 * q]] >> pairs[2 * q + 1]) & 1ull)) {
+            if (need.empty()) need.assign((size_t)h->n, 0);
+            need[pairs[2 * q]] |= 1ull << pairs[2 * q + 1];
+        }
+    }
+    int rc = deliver_flush(h);
+    if (!rc) rc = materialize_mcnt(h);       // stats_prune reads meshMessageDeliveries
+    if (!rc && !need.empty()) rc = ensure_slots(h, need.data());
+    if (rc) return rc;
+    ProfScope ps(h, GSIM_K_CHURN);
+    if (h->churn_cap < 2 * count) {
+        if (h->d_churn) { (void)hipFree(h->d_churn); h->d_churn = nullptr; h->churn_cap = 0; }
+        const hipError_t e = hipMalloc((void**)&h->d_churn, sizeof(uint32_t) * (4 * (size_t)count + 1));
+        if (e != hipSuccess) return hip_check(h, e, "gsim_set_subscriptions");
+        h->churn_cap = 2 * count;
+    }
+    hipError_t e = hipMemcpyAsync(h->d_churn, pairs, sizeof(uint32_t) * 2 * (size_t)count, hipMemcpyHostToDevice,
+                                  h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "gsim_set_subscriptions");
+    HbArgs a = make_hb_args(h, tick, now, 1);   // ctl_out: the heartbeat's inbox (control round 0)
+    hipLaunchKernelGGL(k_subscribe, dim3(1), dim3(64), 0, h->stream, a, h->d_sub, (const uint32_t*)h->d_churn, count,
+                       join ? 1 : 0);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "k_subscribe");
+    h->mesh_version++;            // router mesh / fanout bits changed: delivery masks rebuild
+    h->score_version++;
+    if (!join) {
+        h->unjoined_zero = false; // a peer that left keeps records of the topic
+        h->all_joined = false;
+        h->sub_dynamic = true;    // receivers may hold copies of topics they left
+    }
+    return GSIM_OK;
 }
 
 int gsim_px_connect(gsim_handle* h, int64_t now, uint32_t* pairs, int64_t cap, int64_t* n_connected)

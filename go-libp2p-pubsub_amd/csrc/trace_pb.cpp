@@ -52,6 +52,8 @@ struct Enc {
         case GSIM_TRACE_DELIVER_MESSAGE: *field = 7; return mid + ld(topic_len(e.topic)) + pid;
         case GSIM_TRACE_ADD_PEER: *field = 8; return pid + ld(proto_len);
         case GSIM_TRACE_REMOVE_PEER: *field = 9; return pid;
+        case GSIM_TRACE_JOIN: *field = 13; return ld(topic_len(e.topic));
+        case GSIM_TRACE_LEAVE: *field = 14; return ld(topic_len(e.topic));
         case GSIM_TRACE_GRAFT: *field = 15; return pid + ld(topic_len(e.topic));
         case GSIM_TRACE_PRUNE: *field = 16; return pid + ld(topic_len(e.topic));
         default: *field = 0; return 0;
@@ -169,6 +171,12 @@ extern "C" int gsim_trace_encode(const gsim_trace_event* ev, int64_t n, const gs
             break;
         case GSIM_TRACE_REMOVE_PEER:                         // peerID
             put_peer(w, c, 1, e.other);
+            break;
+        case GSIM_TRACE_JOIN:                                // topic = 1
+            put_topic(w, c, 1, e.topic);
+            break;
+        case GSIM_TRACE_LEAVE:                               // topic = 2 (pb/trace.proto:92-94)
+            put_topic(w, c, 2, e.topic);
             break;
         default:                                             // GRAFT / PRUNE: peerID, topic
             put_peer(w, c, 1, e.other);

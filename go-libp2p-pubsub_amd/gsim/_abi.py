@@ -31,6 +31,7 @@ TF_FANOUT = 0x08
 CTL_GRAFT = 0x01
 CTL_PRUNE = 0x02
 CTL_PX = 0x04
+CTL_UNSUB = 0x10
 CTL_IHAVE = 0x08
 ES_TRACKED = 0x01
 ES_CONNECTED = 0x02
@@ -98,6 +99,7 @@ class CPeerGaterParams(Structure):
 # gsim_trace_event (include/gsim.h): TraceEvent.Type values
 TRACE_PUBLISH_MESSAGE, TRACE_REJECT_MESSAGE, TRACE_DUPLICATE_MESSAGE, TRACE_DELIVER_MESSAGE = 0, 1, 2, 3
 TRACE_ADD_PEER, TRACE_REMOVE_PEER, TRACE_GRAFT, TRACE_PRUNE = 4, 5, 11, 12
+TRACE_JOIN, TRACE_LEAVE = 9, 10
 
 
 # (name, restype, argtypes) for every symbol include/gsim.h declares.
@@ -250,6 +252,7 @@ SIGNATURES = [
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gsim_read_snapshot", c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
     ("gsim_set_ips", c_int32, [c_void_p, c_void_p, c_void_p, c_uint32]),
+    ("gsim_set_subscriptions", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_uint64, c_int64]),
     ("gsim_validate_peer_gater_params", c_int32, [POINTER(CPeerGaterParams), c_char_p, c_size_t]),
     ("gsim_default_peer_gater_params", c_int32, [c_double, c_double, c_double, POINTER(CPeerGaterParams)]),
     ("gsim_set_peer_gater", c_int32, [c_void_p, POINTER(CPeerGaterParams), c_void_p]),

@@ -306,6 +306,14 @@ class Engine:
         p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint32).reshape(-1, 2))
         self._check(self.lib.gsim_set_connections(self.h, _ptr(p), int(p.shape[0]), 1 if up else 0, int(now)))
 
+    def set_subscriptions(self, pairs, join: bool, tick: int, now: int):
+        """Join (join=True) or Leave the (peer, topic) pairs between ticks
+        (gsim_set_subscriptions; gossipsub.go:1047-1124, pubsub.go:1051-1079),
+        before the refresh of `tick`."""
+        p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint32).reshape(-1, 2))
+        self._check(self.lib.gsim_set_subscriptions(self.h, _ptr(p), int(p.shape[0]), 1 if join else 0, int(tick),
+                                                    int(now)))
+
     def set_peer_gater(self, params, topic_weights=None):
         """WithPeerGater (peer_gater.go:161-186) on every router (gsim_set_peer_gater):
         params is a gsim.PeerGaterParams; its TopicDeliveryWeights (topic index ->

@@ -276,6 +276,23 @@ int gsim_px_connect(gsim_handle* h, int64_t now_ns, uint32_t* pairs, int64_t cap
  * restricted to messages that can still arrive.  Publishing into a slot ends
  * the propagation of its previous message; SeenMsgTTL and the ring must
  * outlast a message's propagation (they do for every reference configuration). */
+/* Subscription changes between ticks (Topic.Subscribe / Cancel through
+ * pubsub.go:1051-1079 announcements and the router's Join / Leave,
+ * gossipsub.go:1047-1124), for (peer, topic) pairs.  join = 1: Join(topic):
+ * the peer announces the topic; its fanout peers (score >= 0, no backoff)
+ * become the mesh, topped up to D with getPeers (not direct, no backoff,
+ * score >= 0), or D such peers without a fanout; tracer.Graft and a GRAFT to
+ * each.  join = 0: Leave(topic): the announcement is withdrawn; every mesh
+ * peer gets tracer.Prune, a PRUNE whose backoff is UnsubscribeBackoff and an
+ * UnsubscribeBackoff of its own.  A change that is already in effect is a
+ * no-op.  Scores are the snapshot; getPeers keys use `tick` (call before that
+ * tick's refresh, as gsim_set_connections); the GRAFT/PRUNE are handled with
+ * the heartbeat's in control round 0.  Peers that withdrew a topic drop its
+ * messages (pubsub.go:1094-1098).  Leave's PRUNEs carry no peer exchange.
+ * JOIN / LEAVE / GRAFT / PRUNE trace events.  Single engine. */
+int gsim_set_subscriptions(gsim_handle* h, const uint32_t* pairs, int32_t count, int32_t join, uint64_t tick,
+                           int64_t now_ns);
+
 /* ---- peer gater (peer_gater.go) ------------------------------------------
  * WithPeerGater(params) (peer_gater.go:161-186): every router's AcceptFrom
  * adds the random-early-drop gate of peer_gater.go:320-363 behind the
@@ -437,6 +454,8 @@ int gsim_census(gsim_handle* h, int64_t* out8);
 #define GSIM_TRACE_DELIVER_MESSAGE   3
 #define GSIM_TRACE_ADD_PEER          4
 #define GSIM_TRACE_REMOVE_PEER       5
+#define GSIM_TRACE_JOIN              9
+#define GSIM_TRACE_LEAVE             10
 #define GSIM_TRACE_GRAFT             11
 #define GSIM_TRACE_PRUNE             12
 
@@ -526,6 +545,8 @@ typedef enum gsim_field {
 #define GSIM_CTL_PRUNE    0x02u  /* ControlPrune with Backoff = PruneBackoff/1s */
 #define GSIM_CTL_PX       0x04u  /* the PRUNE carries peer exchange (makePrune doPX, gossipsub.go:1878-1903) */
 #define GSIM_CTL_IHAVE    0x08u  /* ControlIHave for this topic */
+#define GSIM_CTL_UNSUB    0x10u  /* the PRUNE is Leave's (makePrune isUnsubscribe, gossipsub.go:1104-1124):
+                                    Backoff = UnsubscribeBackoff/1s */
 #define GSIM_ES_TRACKED   0x01u
 #define GSIM_ES_CONNECTED 0x02u
 

@@ -155,6 +155,10 @@ int32_t orc_churn(orc_net* s, const uint32_t* pairs, int32_t count, int32_t up, 
  * connections made go to pairs (dialer, peer), at most cap; returns their
  * number.  Clears the marks. */
 int64_t orc_px_connect(orc_net* s, int64_t now, uint32_t* pairs, int64_t cap);
+/* Join / Leave of (peer, topic) pairs between ticks (gossipsub.go:1047-1124,
+ * gsim_set_subscriptions). */
+void orc_set_subscriptions(orc_net* s, const uint32_t* pairs, int32_t count, int32_t join, uint64_t tick, int64_t now,
+                           uint64_t seed);
 void   orc_set_topic_params(orc_net* s, int32_t topic, gsim_topic_score_params* tp_slot,
                             const gsim_topic_score_params* np); /* score.go:201-241 */
 void   orc_mark_first(orc_net* s, int64_t e, int32_t topic);     /* score.go:919-946 */
@@ -209,6 +213,8 @@ enum {
     ORC_EV_ADD_PEER = 14,    /* a: router, b: peer, x: now                           */
     ORC_EV_REMOVE_PEER = 15, /* a: router, b: peer, x: now                           */
     ORC_EV_THROTTLE = 16,    /* a: receiver, b: sender, x: now: AcceptControl -> ThrottlePeer */
+    ORC_EV_JOIN = 17,        /* a: router, topic, x: now    tracer.Join              */
+    ORC_EV_LEAVE = 18,       /* a: router, topic, x: now    tracer.Leave             */
 };
 typedef struct orc_event { int32_t kind, topic; uint32_t a, b; int64_t g; uint64_t mid; int64_t x; } orc_event;
 void    orc_msgs_log(orc_msgs* m, int32_t on);

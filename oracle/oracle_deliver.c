@@ -301,6 +301,9 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
             orc_log(m, ORC_EV_THROTTLE, i, s->col[er], slot, t, g, now);
             continue;
         }
+        /* a topic the receiver no longer subscribes to: the message is skipped
+         * (pubsub.go:1094-1098; only after a Leave, orc_set_subscriptions) */
+        if (!((s->sub[i] >> t) & 1u)) continue;
         m->stats[0]++;
         uint32_t* cell = &m->seen[(int64_t)slot * s->n + i];
         const uint8_t verdict = m->invalid[slot];

@@ -22,6 +22,7 @@ enum {
     P_PX = 14,          /* makePrune: getPeers for PX (heartbeat)      gossipsub.go:1879-1882 */
     P_PX_GRAFT = 15,    /* makePrune: getPeers for PX (GRAFT reply)    gossipsub.go:831-834 */
     P_GATER = 16,       /* peer gater: rand.Float64() of AcceptFrom    peer_gater.go:357 */
+    P_JOIN = 17,        /* Join: getPeers for the new mesh             gossipsub.go:1068-1092 */
 };
 
 static inline uint64_t okey(uint64_t seed, uint64_t tick, uint32_t obs, int32_t topic, uint32_t purpose,

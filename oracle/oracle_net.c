@@ -40,6 +40,7 @@ typedef struct hb {
     uint64_t tick, seed;
     int64_t now;
     uint8_t* out;            /* inbox buffer the replies/heartbeat messages go to */
+    int unsub;               /* the PRUNE being handled is Leave's (GSIM_CTL_UNSUB) */
 } hb;
 
 static inline int64_t ti(const hb* h, uint32_t e) { return (int64_t)h->t * h->s->e + e; }
@@ -333,7 +334,7 @@ static void fanout(hb* h, orc_msgs* m)
  * lastpub = now.  Scores are the snapshot. */
 void orc_fanout_publish(orc_net* s, uint32_t origin, int32_t topic, int64_t g, int64_t now, uint64_t seed)
 {
-    hb h = {s, origin, s->row_ptr[origin], s->row_ptr[origin + 1], topic, (uint64_t)g, seed, now, NULL};
+    hb h = {s, origin, s->row_ptr[origin], s->row_ptr[origin + 1], topic, (uint64_t)g, seed, now, NULL, 0};
     int have = 0;
     if ((s->fan_topics[origin] >> topic) & 1u)
         for (uint32_t e = h.b; e < h.en; ++e) have |= in_fanout(&h, e);
@@ -378,7 +379,7 @@ void orc_heartbeat_gossip(orc_net* s, orc_msgs* m, uint64_t tick, int64_t now, u
     }
 #pragma omp parallel for schedule(dynamic, 64)
     for (int64_t i = 0; i < s->n; ++i) {
-        hb h = {s, (uint32_t)i, s->row_ptr[i], s->row_ptr[i + 1], 0, tick, seed, now, out};
+        hb h = {s, (uint32_t)i, s->row_ptr[i], s->row_ptr[i + 1], 0, tick, seed, now, out, 0};
         /* clearBackoff every 15 ticks (gossipsub.go:1627-1646) */
         if (tick % 15 == 0)
             for (int32_t t = 0; t < s->t; ++t)
@@ -456,9 +457,10 @@ static void handle_prune(hb* h, uint32_t e)
     orc_log_net(ORC_EV_PRUNE, h->i, s->col[e], h->t, h->now);  /* tracer.Prune (gossipsub.go:849) */
     orc_prune(s, e, h->t);
     s->tflags[ti(h, e)] &= (uint8_t)~TF_MESH;
-    /* makePrune sends Backoff = PruneBackoff / time.Second (whole seconds);
+    /* makePrune sends Backoff = PruneBackoff / time.Second (whole seconds),
+     * UnsubscribeBackoff for Leave's PRUNE (isUnsubscribe, gossipsub.go:1870-1872);
      * handlePrune obeys it when > 0, else uses its own PruneBackoff. */
-    int64_t secs = s->gp->prune_backoff_ns / kSecond;
+    int64_t secs = (h->unsub ? s->gp->unsubscribe_backoff_ns : s->gp->prune_backoff_ns) / kSecond;
     if (secs > 0) do_add_backoff(h, e, secs * kSecond);
     else do_add_backoff(h, e, s->gp->prune_backoff_ns);
 }
@@ -472,7 +474,7 @@ int64_t orc_handle_control(orc_net* s, int32_t round, int64_t now)
     int64_t handled = 0;
 #pragma omp parallel for schedule(dynamic, 64) reduction(+ : handled)
     for (int64_t j = 0; j < s->n; ++j) {
-        hb h = {s, (uint32_t)j, s->row_ptr[j], s->row_ptr[j + 1], 0, 0, s->gp->do_px ? seed : 0, now, out};
+        hb h = {s, (uint32_t)j, s->row_ptr[j], s->row_ptr[j + 1], 0, 0, s->gp->do_px ? seed : 0, now, out, 0};
         uint8_t* nopx = s->gp->do_px ? (uint8_t*)calloc((size_t)(h.en - h.b) + 1, 1) : NULL;
         for (int32_t t = 0; t < s->t; ++t) {
             h.t = t;
@@ -485,7 +487,11 @@ int64_t orc_handle_control(orc_net* s, int32_t round, int64_t now)
                     const int off = handle_graft(&h, e);
                     if (nopx && off) nopx[e - h.b] = 1;
                 }
-                if (c & GSIM_CTL_PRUNE) handle_prune(&h, e);
+                if (c & GSIM_CTL_PRUNE) {
+                    h.unsub = (c & GSIM_CTL_UNSUB) != 0;
+                    handle_prune(&h, e);
+                    h.unsub = 0;
+                }
             }
         }
         if (nopx) {
@@ -592,4 +598,77 @@ int64_t orc_px_connect(orc_net* s, int64_t now, uint32_t* pairs, int64_t cap)
     if (n) orc_churn(s, conn, (int32_t)n, 1, now);
     free(conn);
     return n;
+}
+
+/* ---- Join / Leave (gossipsub.go:1047-1124) ------------------------------- */
+
+static int f_join(const hb* h, uint32_t e, double arg)        /* gossipsub.go:1084-1090 */
+{
+    (void)arg;
+    return !is_direct(h, e) && !has_backoff(h, e) && h->s->score[e] >= 0;
+}
+
+static int f_join_more(const hb* h, uint32_t e, double arg)   /* gossipsub.go:1070-1077 */
+{
+    return !in_fanout(h, e) && f_join(h, e, arg);
+}
+
+void orc_set_subscriptions(orc_net* s, const uint32_t* pairs, int32_t count, int32_t join, uint64_t tick, int64_t now,
+                           uint64_t seed)
+{
+    uint64_t* sub = (uint64_t*)s->sub;
+    const gsim_gossipsub_params* gp = s->gp;
+    for (int32_t q = 0; q < count; ++q) {
+        const uint32_t p = pairs[2 * q];
+        const int32_t t = (int32_t)pairs[2 * q + 1];
+        const uint64_t bit = 1ull << t;
+        hb h = {s, p, s->row_ptr[p], s->row_ptr[p + 1], t, tick, seed, now, s->ctl, 0};
+        if (join) {
+            if (sub[p] & bit) continue;                          /* gs.mesh[topic] exists */
+            sub[p] |= bit;                                       /* the announcement */
+            orc_log_net(ORC_EV_JOIN, p, p, t, now);
+            cand buf[4096];
+            const uint32_t deg = h.en - h.b;
+            cand* c = deg <= 4096 ? buf : (cand*)malloc(sizeof(cand) * deg);
+            if (s->fan_topics && ((s->fan_topics[p] >> t) & 1u)) {
+                int have = 0;
+                for (uint32_t e = h.b; e < h.en; ++e) {
+                    if (!in_fanout(&h, e)) continue;
+                    if (s->score[e] < 0 || has_backoff(&h, e)) s->tflags[ti(&h, e)] &= (uint8_t)~GSIM_TF_FANOUT;
+                    else ++have;
+                }
+                if (have < gp->d) {
+                    const int n = get_peers(&h, gp->d - have, f_join_more, 0, P_JOIN, c);
+                    for (int k = 0; k < n; ++k) s->tflags[ti(&h, c[k].e)] |= GSIM_TF_FANOUT;
+                }
+                for (uint32_t e = h.b; e < h.en; ++e)
+                    if (in_fanout(&h, e))
+                        s->tflags[ti(&h, e)] = (uint8_t)((s->tflags[ti(&h, e)] & ~GSIM_TF_FANOUT) | TF_MESH);
+                s->fan_topics[p] &= ~bit;                        /* delete(gs.fanout, topic), lastpub */
+                if (s->lastpub) s->lastpub[(int64_t)p * s->t + t] = 0;
+            } else {
+                const int n = get_peers(&h, gp->d, f_join, 0, P_JOIN, c);
+                for (int k = 0; k < n; ++k) s->tflags[ti(&h, c[k].e)] |= TF_MESH;
+            }
+            if (c != buf) free(c);
+            for (uint32_t e = h.b; e < h.en; ++e) {
+                if (!in_mesh(&h, e)) continue;
+                orc_log_net(ORC_EV_GRAFT, p, s->col[e], t, now);   /* tracer.Graft + sendGraft */
+                orc_graft(s, e, t, now);
+                send_ctl(&h, e, GSIM_CTL_GRAFT);
+            }
+        } else {
+            if (!(sub[p] & bit)) continue;                       /* no mesh for the topic */
+            sub[p] &= ~bit;
+            orc_log_net(ORC_EV_LEAVE, p, p, t, now);
+            for (uint32_t e = h.b; e < h.en; ++e) {
+                if (!in_mesh(&h, e)) continue;
+                orc_log_net(ORC_EV_PRUNE, p, s->col[e], t, now);   /* tracer.Prune, sendPrune, addBackoff */
+                orc_prune(s, e, t);
+                s->tflags[ti(&h, e)] &= (uint8_t)~TF_MESH;
+                send_ctl(&h, e, GSIM_CTL_PRUNE | GSIM_CTL_UNSUB);
+                do_add_backoff(&h, e, gp->unsubscribe_backoff_ns);
+            }
+        }
+    }
 }

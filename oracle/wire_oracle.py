@@ -73,7 +73,7 @@ def trace_pb():
     """{name: class} for TraceEvent and TraceEventBatch, from a descriptor
     restating pb/trace.proto:5-150 for the events the engine produces
     (PublishMessage, RejectMessage, DuplicateMessage, DeliverMessage,
-    AddPeer, RemovePeer, Graft, Prune; field names, numbers, types as
+    AddPeer, RemovePeer, Join, Leave, Graft, Prune; field names, numbers, types as
     there).  Serialized by the protobuf runtime."""
     global _TRACE
     if _TRACE is not None:
@@ -96,6 +96,7 @@ def trace_pb():
                                             ("deliverMessage", 7, OPT, M, T + "DeliverMessage"),
                                             ("addPeer", 8, OPT, M, T + "AddPeer"),
                                             ("removePeer", 9, OPT, M, T + "RemovePeer"),
+                                            ("join", 13, OPT, M, T + "Join"), ("leave", 14, OPT, M, T + "Leave"),
                                             ("graft", 15, OPT, M, T + "Graft"), ("prune", 16, OPT, M, T + "Prune")]:
         f = ev.field.add(name=fname, number=num, label=label, type=typ)
         if tname:
@@ -112,6 +113,8 @@ def trace_pb():
     sub("DeliverMessage", [("messageID", 1, B), ("topic", 2, S), ("receivedFrom", 3, B)])
     sub("AddPeer", [("peerID", 1, B), ("proto", 2, S)])
     sub("RemovePeer", [("peerID", 1, B)])
+    sub("Join", [("topic", 1, S)])
+    sub("Leave", [("topic", 2, S)])             # pb/trace.proto:92-94: Leave.topic is field 2
     sub("Graft", [("peerID", 1, B), ("topic", 2, S)])
     sub("Prune", [("peerID", 1, B), ("topic", 2, S)])
     b = fdp.message_type.add(name="TraceEventBatch")

@@ -115,6 +115,7 @@ def load():
             "orc_heartbeat_gossip": (None, [P, POINTER(OrcMsgs), c_uint64, c_int64, c_uint64]),
             "orc_gossip_penalties": (None, [P, POINTER(OrcMsgs), c_int64]),
             "orc_px_connect": (c_int64, [P, c_int64, c_void_p, c_int64]),
+"orc_set_subscriptions": (None, [P, c_void_p, c_int32, c_int32, c_uint64, c_int64, c_uint64]),
             "orc_gater_validate": (c_int32, [POINTER(_abi.CPeerGaterParams)]),
             "orc_gater_new": (c_void_p, [P, POINTER(_abi.CPeerGaterParams), c_void_p]),
             "orc_gater_free": (None, [c_void_p]),
@@ -248,6 +249,12 @@ class NetState:
         bad = load().orc_churn(self.view(), _p(p), int(p.shape[0]), 1 if up else 0, int(now))
         assert bad < 0, f"pair {bad} is not a connection"
 
+    def set_subscriptions(self, pairs, join, tick, now, seed):
+        """orc_set_subscriptions: Join / Leave of (peer, topic) pairs between ticks."""
+        p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint32).reshape(-1, 2))
+        load().orc_set_subscriptions(self.view(), _p(p), int(p.shape[0]), 1 if join else 0, int(tick), int(now),
+                                     int(seed))
+
     def px_connect(self, now):
         """orc_px_connect: the connector for this tick's PX attempts; returns
         the (dialer, peer) pairs connected, sorted (outbound flags updated in
@@ -281,6 +288,7 @@ ORC_BEHAVE_IGNORE_IWANT = 0x01   # oracle.h: never answers IWANT
 # oracle.h ORC_EV_*: the network oracle's event log
 EV_PUT, EV_SEEN, EV_SERVE, EV_PROMISE, EV_FULFILL, EV_BROKEN, EV_PENALTIES, EV_HEARTBEAT, EV_GOSSIP_ID = range(1, 10)
 EV_REJECT_SIG, EV_PUBLISH, EV_GRAFT, EV_PRUNE, EV_ADD_PEER, EV_REMOVE_PEER = range(10, 16)
+EV_THROTTLE, EV_JOIN, EV_LEAVE = range(16, 19)
 EVENT_DTYPE = np.dtype([("kind", np.int32), ("topic", np.int32), ("a", np.uint32), ("b", np.uint32),
                         ("g", np.int64), ("mid", np.uint64), ("x", np.int64)])
 

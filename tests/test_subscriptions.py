@@ -1,0 +1,145 @@
+"""Dynamic subscriptions: Join / Leave (gossipsub.go:1047-1124) with the
+subscription announcements other routers see (pubsub.go:1051-1079)
+(SURVEY.md §8(f) row 4).
+
+CPU part: the oracle's Join / Leave against the reference's rules — the
+fanout becomes the mesh (negative scores and backoffs dropped, topped up to D
+with getPeers), tracer.Graft + GRAFT to each, fanout and lastpub deleted; a
+Join without a fanout takes getPeers(D); Leave prunes every mesh peer with an
+UnsubscribeBackoff at both ends; a router drops messages of a topic it left.
+
+GPU part: the engine bit-exact against the oracle over ticks with Joins and
+Leaves mixed with fanout publishers, gossip and the trace (JOIN / LEAVE /
+GRAFT / PRUNE events), on a dense layout and on sub-rings with topic slots
+(a Join may grow a peer's slot mask)."""
+import numpy as np
+import pytest
+
+import oracle_binding as ob
+from gsim import _abi
+from gsim.params import GossipSubParams, PeerScoreThresholds, Second
+from test_delivery import R, T0, delivery_params
+from test_fanout import fanout_net, row, tick, unsubscribe
+from test_heartbeat import SEED, tick_time
+
+
+def test_join_turns_the_fanout_into_the_mesh():
+    net, st = fanout_net(ttl=60 * Second)
+    msgs = ob.Msgs(net.n, 2, 64, R, T0, Second)
+    for kk in range(1, 3):
+        tick(st, msgs, kk)
+    o = 7                                             # not joined to topic 1: publishes to a fanout
+    b, en = row(net, o)
+    tick(st, msgs, 3, sched={3 * R: [(1, 1, o, 0)]})
+    fan = b + np.nonzero(st.tflags[1, b:en] & _abi.TF_FANOUT)[0]
+    assert len(fan) == 6 and st.fan_topics[o] == 2
+    st.score[fan[0]] = -5.0                           # dropped: negative score
+    st.backoff[1, fan[1]] = tick_time(4)              # dropped: a backoff entry
+    now = tick_time(4) - Second // 2
+    st.set_subscriptions([(o, 1)], True, 4, now, SEED)
+    assert (net.sub[o] >> np.uint64(1)) & np.uint64(1)
+    mesh = b + np.nonzero(st.tflags[1, b:en] & _abi.TF_MESH)[0]
+    assert not (st.tflags[1, b:en] & _abi.TF_FANOUT).any()
+    assert st.fan_topics[o] == 0 and st.lastpub[o, 1] == 0
+    assert set(fan[2:]) <= set(mesh), "the remaining fanout peers are kept"
+    assert fan[0] not in mesh and fan[1] not in mesh
+    assert len(mesh) == 6, "topped up to D"
+    for e in mesh:
+        assert st.ctl[0, 1, st.rev[e]] & _abi.CTL_GRAFT, "a GRAFT to every mesh peer"
+        assert st.tflags[1, e] & _abi.TF_IN_MESH, "tracer.Graft"
+    st.set_subscriptions([(o, 1)], True, 4, now, SEED)        # already joined: no-op
+    assert (b + np.nonzero(st.tflags[1, b:en] & _abi.TF_MESH)[0] == mesh).all()
+
+
+def test_join_without_fanout_takes_d_peers():
+    net, st = fanout_net()
+    o = 3
+    b, en = row(net, o)
+    st.set_subscriptions([(o, 1)], True, 1, tick_time(1), SEED)
+    mesh = np.nonzero(st.tflags[1, b:en] & _abi.TF_MESH)[0]
+    assert len(mesh) == 6
+    assert all((net.sub[net.col[b + q]] >> np.uint64(1)) & np.uint64(1) for q in mesh), "topic peers only"
+
+
+def test_leave_prunes_with_the_unsubscribe_backoff():
+    net, st = fanout_net()
+    gp = GossipSubParams(D=6, Dlo=5, Dhi=12)
+    msgs = ob.Msgs(net.n, 2, 64, R, T0, Second)
+    for kk in range(1, 3):
+        tick(st, msgs, kk)
+    o = 150
+    b, en = row(net, o)
+    mesh = b + np.nonzero(st.tflags[0, b:en] & _abi.TF_MESH)[0]
+    assert len(mesh) >= gp.Dlo
+    now = tick_time(3) - Second // 2
+    st.set_subscriptions([(o, 0)], False, 3, now, SEED)
+    assert not (net.sub[o] & np.uint64(1))
+    assert not (st.tflags[0, b:en] & _abi.TF_MESH).any()
+    for e in mesh:
+        c = st.ctl[0, 0, st.rev[e]]
+        assert (c & _abi.CTL_PRUNE) and (c & _abi.CTL_UNSUB)
+        assert st.backoff[0, e] == now + gp.UnsubscribeBackoff
+        assert not (st.tflags[0, e] & _abi.TF_IN_MESH), "tracer.Prune"
+    # the pruned peers obey the PRUNE's backoff (UnsubscribeBackoff / 1s)
+    ob.load().orc_handle_control(st.view(), 0, now)
+    for e in mesh:
+        re = st.rev[e]
+        assert not (st.tflags[0, re] & _abi.TF_MESH)
+        assert st.backoff[0, re] == now + gp.UnsubscribeBackoff
+
+
+def test_a_router_drops_messages_of_a_topic_it_left():
+    net, st = fanout_net()
+    msgs = ob.Msgs(net.n, 2, 64, R, T0, Second)
+    for kk in range(1, 3):
+        tick(st, msgs, kk)
+    o = 200
+    st.set_subscriptions([(o, 0)], False, 3, tick_time(3) - Second // 2, SEED)
+    tick(st, msgs, 3, sched={3 * R + 1: [(5, 0, 201, 0)]})
+    assert msgs.seen[5, o] == ob.UNSEEN, "the copies to the peer that left were skipped"
+    subscribed = (net.sub & np.uint64(1)).astype(bool)
+    assert (msgs.seen[5, subscribed] != ob.UNSEEN).all()
+
+
+# ---- GPU parity -------------------------------------------------------------------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("topic_slots", [0, 32])
+def test_join_leave_bit_exact(require_gpu, topic_slots):
+    """Joins (with and without a fanout) and Leaves between ticks, fanout
+    publishers, gossip, churn and the trace: every state array, the seen-set,
+    the totals and the JOIN / LEAVE / GRAFT / PRUNE events bit-exact."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim.engine import random_regular
+    from tickrun import restrict_to_subscriptions, run_parity, subscribed_schedule
+    n, k, T = 900, 16, 3
+    rng = np.random.default_rng(515 + topic_slots)
+    params = beacon_params(T)
+    gp = GossipSubParams(D=6, Dlo=5, Dhi=10, Dscore=3, Dout=2, FanoutTTL=30 * Second)
+    th = PeerScoreThresholds(GossipThreshold=-50, PublishThreshold=-100, GraylistThreshold=-400)
+    net = random_regular(n, k, seed=91, n_topics=T)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 6 / k)
+    for t in range(1, T):
+        unsubscribe(net, st, np.nonzero(rng.random(n) < 0.3)[0], t)
+    restrict_to_subscriptions(st, net)
+    ticks = list(range(1, 8))
+    # publishers are any peers: non-members build fanouts that later Joins turn into meshes
+    sched = subscribed_schedule(rng, ticks, net, T, 6.0, 0.05, member_only=False)
+
+    def members(t, want):
+        return np.nonzero(((net.sub >> np.uint64(t)) & np.uint64(1)).astype(bool) == want)[0]
+
+    subs = {}
+    for kk, join in ((3, True), (4, False), (5, True), (6, False)):
+        ev = []
+        for t in range(T):
+            pool = members(t, not join)
+            for p in rng.choice(pool, size=min(12, len(pool)), replace=False):
+                ev.append((int(p), t))
+        subs[kk] = [(np.array(ev, dtype=np.uint32), join)]
+    log = []
+    run_parity(net, params, th, gp, st, ticks, sched, ring=256, subs=subs, trace=(0, n), trace_log=log,
+               topic_slots=topic_slots)
+    total = np.sum(log, axis=0)
+    assert total[_abi.TRACE_JOIN] > 0 and total[_abi.TRACE_LEAVE] > 0

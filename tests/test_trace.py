@@ -69,11 +69,15 @@ def _expected_batch(recs, names, peer_ids, proto=b"/meshsub/1.1.0"):
             e.graft.peerID, e.graft.topic = other, topic
         elif typ == _abi.TRACE_PRUNE:
             e.prune.peerID, e.prune.topic = other, topic
+        elif typ == _abi.TRACE_JOIN:
+            e.join.topic = topic
+        elif typ == _abi.TRACE_LEAVE:
+            e.leave.topic = topic
     return batch.SerializeToString()
 
 
 def _random_records(rng, n, T, N):
-    types = [0, 1, 2, 3, 4, 5, 11, 12]
+    types = [0, 1, 2, 3, 4, 5, 9, 10, 11, 12]
     recs = np.zeros(n, dtype=Engine.TRACE_DTYPE)
     for k in range(n):
         typ = types[rng.integers(0, len(types))]

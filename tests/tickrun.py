@@ -50,9 +50,10 @@ def oracle_trace(ev, msgs, lo, hi):
                 out.append((ts, mid, a, b, topic, _abi.TRACE_DUPLICATE_MESSAGE, 0))
         elif kind == ob.EV_REJECT_SIG:
             out.append((msgs.round_time(int(e["g"])), mid, a, b, topic, _abi.TRACE_REJECT_MESSAGE, 4))
-        elif kind in (ob.EV_GRAFT, ob.EV_PRUNE, ob.EV_ADD_PEER, ob.EV_REMOVE_PEER):
+        elif kind in (ob.EV_GRAFT, ob.EV_PRUNE, ob.EV_ADD_PEER, ob.EV_REMOVE_PEER, ob.EV_JOIN, ob.EV_LEAVE):
             typ = {ob.EV_GRAFT: _abi.TRACE_GRAFT, ob.EV_PRUNE: _abi.TRACE_PRUNE, ob.EV_ADD_PEER: _abi.TRACE_ADD_PEER,
-                   ob.EV_REMOVE_PEER: _abi.TRACE_REMOVE_PEER}[kind]
+                   ob.EV_REMOVE_PEER: _abi.TRACE_REMOVE_PEER, ob.EV_JOIN: _abi.TRACE_JOIN,
+                   ob.EV_LEAVE: _abi.TRACE_LEAVE}[kind]
             out.append((int(e["x"]), 0, a, b, topic, typ, 0))
     arr = np.zeros(len(out), dtype=Engine.TRACE_DTYPE)
     for q, (ts, mid, a, b, topic, typ, rs) in enumerate(out):
@@ -62,7 +63,7 @@ def oracle_trace(ev, msgs, lo, hi):
 
 def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, churn=None, after_tick=None,
                eng=None, after_heartbeat=None, px_log=None, trace=None, trace_log=None, topic_slots=0, gater=None,
-               gater_log=None):
+               gater_log=None, subs=None):
     """Run `ticks` on a fresh engine loaded with `st`'s state and on the
     oracle; assert identical state, seen-set and totals after every tick.
     churn: {tick: [(pairs, up), ...]} applied just before the tick.
@@ -77,7 +78,8 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
     cells (gsim_msg_config.topic_slots), on both sides.  gater: a
     gsim.PeerGaterParams turned on at both sides (WithPeerGater); its state
     and the copies it dropped must agree after every tick (the per-tick drop
-    counts appended to gater_log)."""
+    counts appended to gater_log).  subs: {tick: [(pairs, join), ...]} Join /
+    Leave of (peer, topic) pairs applied just before the tick, after churn."""
     from gsim.engine import Engine
     pushed = eng is None
     if eng is None:
@@ -105,6 +107,9 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
             for (pairs, up) in (churn or {}).get(kk, []):
                 st.churn(pairs, up=up, now=now - Second // 2)
                 eng.set_connections(pairs, up=up, now=now - Second // 2)
+            for (pairs, join) in (subs or {}).get(kk, []):
+                st.set_subscriptions(pairs, join, kk, now - Second // 2, SEED)
+                eng.set_subscriptions(pairs, join, kk, now - Second // 2)
             eng.refresh_scores(now)
             eng.heartbeat(kk, now)
             v = st.view()
