@@ -1680,6 +1680,10 @@ __global__ void k_subscribe(HbArgs a, uint64_t* sub, const uint32_t* pairs, int3
             if (!(sub[p] & bit)) continue;                   // no mesh for the topic
             sub[p] &= ~bit;
             if (a.tr.on(p)) a.tr.push(a.now, 0, p, p, t, GSIM_TRACE_LEAVE, 0);
+            // emitGossip no longer runs for the topic (unless as a fanout): its
+            // last IHAVE targets must not be advertised to again
+            if (a.gsel)
+                for (uint32_t e = b; e < en; ++e) a.gsel[slot_idx(mi, t, a.E, e)] = 0;
             for (uint32_t e = b; e < en; ++e) {
                 if (!(mf(e) & GSIM_TF_MESH)) continue;
                 if (a.tr.on(p)) a.tr.push(a.now, 0, p, a.col[e], t, GSIM_TRACE_PRUNE, 0);   // tracer.Prune

@@ -130,7 +130,7 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
                     eng.publish(sched[g], g)
                 msgs.round(st, g)
                 eng.round(g)
-            assert eng.msg_stats() == msgs.stats, f"totals differ at tick {kk}"
+            assert eng.msg_stats() == msgs.stats, f"totals differ at tick {kk}: {eng.msg_stats()} vs {msgs.stats}"
             assert np.array_equal(eng.read(_abi.F_SEEN), msgs.seen), f"seen-set differs at tick {kk}"
             assert np.array_equal(eng.read(_abi.F_LASTPUT), msgs.lastput), f"mcache puts differ at tick {kk}"
             gpu = ob.NetState(net, params, thresholds=th, gossip=gp)
@@ -141,7 +141,8 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
                 assert len(got) == len(want), f"trace length differs at tick {kk}: {len(got)} vs {len(want)}"
                 for f in ("timestamp", "msg_id", "peer", "other", "topic", "type", "reason"):
                     bad = np.nonzero(got[f] != want[f])[0]
-                    assert len(bad) == 0, f"trace field {f} differs at tick {kk}: first at {bad[:1]}"
+                    assert len(bad) == 0, (f"trace field {f} differs at tick {kk}: first at {bad[:1]}: "
+                                           f"{got[max(0, bad[0] - 2):bad[0] + 3]} vs {want[max(0, bad[0] - 2):bad[0] + 3]}")
                 if trace_log is not None:
                     trace_log.append(np.bincount(want["type"], minlength=13))
             if gater is not None:
