@@ -104,7 +104,7 @@ def test_a_router_drops_messages_of_a_topic_it_left():
 # ---- GPU parity -------------------------------------------------------------------
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("topic_slots", [0, 32])
+@pytest.mark.parametrize("topic_slots", [0, 80])
 def test_join_leave_bit_exact(require_gpu, topic_slots):
     """Joins (with and without a fanout) and Leaves between ticks, fanout
     publishers, gossip, churn and the trace: every state array, the seen-set,

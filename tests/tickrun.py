@@ -43,7 +43,9 @@ def oracle_trace(ev, msgs, lo, hi):
         elif kind == ob.EV_SEEN and b != 0xFFFFFFFF:
             ts = msgs.round_time(int(e["g"]))
             if int(e["x"]):
-                vd = int(msgs.invalid[mid % ring])
+                # the slot holding the message (sub-rings: not id % ring)
+                slots = np.nonzero(msgs.mid == np.uint64(mid))[0]
+                vd = int(msgs.invalid[slots[0] if len(slots) else mid % ring])
                 typ = _abi.TRACE_DELIVER_MESSAGE if vd == 0 else _abi.TRACE_REJECT_MESSAGE
                 out.append((ts, mid, a, b, topic, typ, vd))
             else:
