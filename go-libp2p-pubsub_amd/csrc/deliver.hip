@@ -913,6 +913,12 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             else if (a.sedge && vv[u]) ev[u] = a.sedge[bq + k];
                             else ev[u] = s_beg[q] + k;
                         }
+#ifdef GSIM_DIAG_NO_RX
+                        // diagnostic build (timing only, wrong results): the frontier walk
+                        // alone, no receiver-side access
+                        if (vv[0] && ev[0] == 0xFFFFFFFFu) n_acc++;
+                        continue;
+#endif
 #pragma unroll
                         for (int u = 0; u < P; ++u) {
                             iv[u] = 0; mfv[u] = 0; dsv[u] = 0; tfv[u] = 0; nv[u] = 0; xv[u] = 0.0;
@@ -972,9 +978,16 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             // credited; with a validation latency the credit is decided at
                             // completion (mesh and record then), so only an unscored topic
                             // or an ignored / throttled message skips it
+#ifdef GSIM_DIAG_NO_SEEN
+                            // diagnostic build (timing only, wrong results): every receiver is
+                            // an earlier-round duplicate, no seen-set access
+                            const bool known = true;
+                            (void)s_bm; (void)bw;
+#else
                             const bool known = ((s_bm[bw] >> (i & 63)) & 1ull) &&
                                                (L ? (!scored_t || (inv && !pen))
                                                   : (s_wa[k] || !sc || inv || !(tf & GSIM_TF_IN_MESH)));
+#endif
                             // the receiver's cell (a member of t: mesh, direct, fanout and flood
                             // targets all hold the topic, §2); -1 cannot happen
                             const int64_t ci = known ? 0 : SP ? a.cs.at((int64_t)s_cb[k], t, i) : (int64_t)m * a.cs.n + i;
