@@ -228,7 +228,8 @@ def run_tick(eng, k, sched, churn=None, px=False):
         eng.px_connect(now + SECOND // 2)
 
 
-def cpu_baseline(cfg, scen=None, n: int = 10_000, ticks: int = 5, budget_s: float = 25.0):
+def cpu_baseline(cfg, scen=None, n: int = 10_000, ticks: int = 5, budget_s: float = 25.0, warmup: int = 1,
+                 legs=("single", "all")):
     """Time the C oracle on a bounded sample of the same workload (same graph
     model, degree, topics, parameters, adversaries, churn and message rate,
     `n` peers): one warm-up tick, then `ticks` ticks timed one by one, the
@@ -265,7 +266,7 @@ def cpu_baseline(cfg, scen=None, n: int = 10_000, ticks: int = 5, budget_s: floa
         lib.orc_ip_colocation(v)
         times, deliv = [], []
         t_leg = time.perf_counter()
-        for kk in range(1, ticks + 2):
+        for kk in range(1, ticks + 1 + warmup):
             now = tick_time(kk)
             d0 = msgs.stats[0]
             t0 = time.perf_counter()
@@ -281,7 +282,7 @@ def cpu_baseline(cfg, scen=None, n: int = 10_000, ticks: int = 5, budget_s: floa
                 msgs.round(st, g)
             if gp.PeerExchange:
                 st.px_connect(now + SECOND // 2)
-            if kk > 1:                                  # tick 1 warms up
+            if kk > warmup:                             # the first `warmup` ticks warm up
                 times.append(time.perf_counter() - t0)
                 deliv.append(msgs.stats[0] - d0)
             if time.perf_counter() - t_leg > budget_s and len(times) >= 1:
@@ -290,17 +291,18 @@ def cpu_baseline(cfg, scen=None, n: int = 10_000, ticks: int = 5, budget_s: floa
         return {"value": n / med, "cores": got, "ticks_timed": len(times), "median_tick_s": med,
                 "msg_edge_deliveries_per_sec": float(np.median(deliv)) / med}
 
-    one = leg(1)
-    allc = leg(all_threads)
+    one = leg(1) if "single" in legs else None
+    allc = leg(all_threads) if "all" in legs else one
     lib.orc_set_threads(all_threads)
+    n1 = one["ticks_timed"] if one else 0
     return {"value": allc["value"], "unit": "peer-heartbeat updates/sec", "cores": allc["cores"], "kind": "port",
             "msg_edge_deliveries_per_sec": allc["msg_edge_deliveries_per_sec"],
             "single_core": one, "all_core": allc,
             "sample": f"C oracle heartbeat tick (refreshScores+score, mesh maintenance, {ROUNDS} propagation "
                       f"rounds at {rate:g} msg/s/topic) on a {n}-peer {describe_graph(cfg, scen)}, T={T} "
-                      f"network; median of {one['ticks_timed']} (1 core) / {allc['ticks_timed']} "
-                      f"({allc['cores']} OpenMP threads in the refresh, score, heartbeat and control phases; "
-                      f"propagation rounds serial) ticks after a warm-up tick"}
+                      f"network; median of {n1} (1 core) / {allc['ticks_timed']} "
+                      f"({allc['cores']} OpenMP threads: refresh, score, heartbeat, control and the "
+                      f"receivers of each propagation round) ticks after {warmup} warm-up tick(s)"}
 
 
 def job_totals(wall: float, deliveries: float, dist=None, device: str = "cpu"):
@@ -340,6 +342,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-full", action="store_true",
+                    help="time only the C oracle on the config's full network (no GPU): one tick per leg "
+                         "(DESIGN.md §7); prints one JSON line")
     ap.add_argument("--msg-rate", type=float, default=None, help="messages per second per topic (config default)")
     ap.add_argument("--ring", type=int, default=None, help="message ring slots (config default)")
     ap.add_argument("--vdelay", type=int, default=0,
@@ -350,6 +355,14 @@ def main():
                     help="N = 1: split the network into this many shards on the one GPU (exercises the halo "
                          "exchange through the in-process transport; not the headline configuration)")
     args = ap.parse_args()
+    if args.cpu_full:
+        cfg = CONFIGS[args.config]
+        scen = dict(SCENARIOS.get(args.config, {}))
+        legs = tuple(os.environ.get("GSIM_CPU_LEGS", "all,single").split(","))
+        out = cpu_baseline(cfg, scen, n=cfg[0], ticks=1, budget_s=0.0, warmup=0, legs=legs)
+        out["config"] = args.config
+        print(json.dumps(out), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -17,6 +17,9 @@
 
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define UNSEEN 0xFFFFFFFFu
 
@@ -236,6 +239,108 @@ static void complete_validations(orc_net* s, orc_msgs* m, int64_t g, int64_t now
     p->npq = keep;
 }
 
+typedef struct frbuf { fr_ent* v; int64_t n, cap; } frbuf;
+
+static void frb_push(frbuf* b, uint32_t peer, uint32_t slot, uint32_t from)
+{
+    if (b->n == b->cap) {
+        b->cap = b->cap ? 2 * b->cap : 1024;
+        b->v = (fr_ent*)realloc(b->v, sizeof(fr_ent) * (size_t)b->cap);
+    }
+    b->v[b->n].peer = peer; b->v[b->n].slot = slot; b->v[b->n].from = from;
+    b->n++;
+}
+
+/* One copy at receiver i (step 2 of orc_round): AcceptFrom (graylist, the
+ * peer gater), the subscription, pushMsg's seen check and the score
+ * tracer's Deliver / Duplicate / RejectMessage. */
+static void handle_copy(orc_net* s, orc_msgs* m, priv* p, int64_t g, int64_t now, double gray, arr_ent x, frbuf* fb,
+                        int64_t* stats)
+{
+    const uint32_t i = x.recv, slot = x.slot, er = x.er;
+    const int32_t t = (int32_t)m->topic[slot];
+    if (s->score[er] < gray && !(s->direct && s->direct[er])) {   /* AcceptFrom -> AcceptNone; direct: AcceptAll */
+        stats[3]++;
+        return;
+    }
+    if (s->gater && !(s->direct && s->direct[er]) && !orc_gater_accept(s, p->seed, g, i, er, slot)) {
+        /* the peer gater's AcceptControl: the message is dropped and the
+         * receiver forgets its promises from the sender (ThrottlePeer,
+         * gossip_tracer.go:182-200) */
+        if (p->npr) {
+            int32_t w = 0;
+            for (int32_t q2 = 0; q2 < p->npr[i]; ++q2)
+                if (p->pr[i][q2].e != er) p->pr[i][w++] = p->pr[i][q2];
+            p->npr[i] = w;
+        }
+        orc_log(m, ORC_EV_THROTTLE, i, s->col[er], slot, t, g, now);
+        return;
+    }
+    /* a topic the receiver no longer subscribes to: the message is skipped
+     * (pubsub.go:1094-1098; only after a Leave, orc_set_subscriptions) */
+    if (!((s->sub[i] >> t) & 1u)) return;
+    stats[0]++;
+    uint32_t* cell = &m->seen[(int64_t)slot * s->n + i];
+    const uint8_t verdict = m->invalid[slot];
+    if (verdict == GSIM_VERDICT_SIGNATURE) {
+        orc_gater_event(s, i, er, t, ORC_GATE_REJECT);      /* RejectInvalidSignature */
+        /* RejectInvalidSignature before markSeen (validation.go:282-290):
+         * every copy's sender is penalised, nothing is seen, no promise is
+         * fulfilled (gossip_tracer.go:148-162) */
+        stats[2]++;
+        orc_mark_invalid(s, er, t);
+        orc_log(m, ORC_EV_REJECT_SIG, i, s->col[er], slot, t, g, 0);
+        return;
+    }
+    const uint8_t vdelay = p->vd ? p->vd[slot] : 0;
+    if (!vdelay || *cell != UNSEEN) orc_log(m, ORC_EV_SEEN, i, s->col[er], slot, t, g, *cell == UNSEEN);
+    if (s->gater) {
+        /* first delivery: ValidateMessage, then the verdict's tracer call */
+        static const int32_t kind[4] = {ORC_GATE_DELIVER, ORC_GATE_REJECT, ORC_GATE_IGNORE, ORC_GATE_THROTTLE};
+        if (*cell == UNSEEN) orc_gater_event(s, i, er, t, ORC_GATE_VALIDATE);
+        orc_gater_event(s, i, er, t, *cell == UNSEEN ? kind[verdict] : ORC_GATE_DUPLICATE);
+    }
+    if (*cell == UNSEEN && vdelay) {
+        /* markSeen + ValidateMessage (promises fulfilled); the verdict
+         * lands vdelay rounds later (complete_validations) */
+        *cell = (uint32_t)(g + vdelay);
+        stats[1]++;
+        orc_gossip_fulfill(m, i, slot);
+        if (p->slot_last) p->slot_last[slot] = g;
+        pq_push(p, g + vdelay, i, slot, er, 1);
+    } else if (*cell != UNSEEN && (int64_t)*cell > g) {
+        /* DuplicateMessage while the first copy validates
+         * (deliveryUnknown: drec.peers, score.go:806-809) */
+        stats[2]++;
+        if (verdict == GSIM_VERDICT_REJECT || verdict == GSIM_VERDICT_ACCEPT) pq_push(p, *cell, i, slot, er, 0);
+    } else if (*cell == UNSEEN) {
+        *cell = (uint32_t)g;               /* markSeen */
+        stats[1]++;
+        orc_gossip_fulfill(m, i, slot);    /* gossipTracer: promises for it are kept */
+        if (p->slot_last) {
+#pragma omp atomic write
+            p->slot_last[slot] = g;
+        }
+        if (verdict == GSIM_VERDICT_REJECT) {
+            /* ValidateMessage + RejectMessage(ValidationFailed), score.go:728-793 */
+            orc_mark_invalid(s, er, t);
+        } else if (verdict == GSIM_VERDICT_ACCEPT) {
+            /* DeliverMessage, score.go:702-726; mcache.Put; forward next round */
+            orc_mark_first(s, er, t);
+            m->lastput[(int64_t)t * s->n + i] = (int32_t)(g / m->rounds);
+            orc_log(m, ORC_EV_PUT, i, 0, slot, t, g, 0);
+            frb_push(fb, i, slot, s->col[er]);
+        }
+        /* RejectValidationIgnored / Throttled: deliveryIgnored / deliveryThrottled,
+         * no penalty and no credit (score.go:759-781) */
+    } else {
+        stats[2]++;                        /* DuplicateMessage, score.go:795-827 */
+        if (verdict == GSIM_VERDICT_REJECT) orc_mark_invalid(s, er, t);
+        else if (verdict == GSIM_VERDICT_ACCEPT)
+            orc_mark_duplicate(s, er, t, 1, orc_round_time(m, (int64_t)*cell), now);
+    }
+}
+
 void orc_round(orc_net* s, orc_msgs* m, int64_t g)
 {
     priv* p = P(m);
@@ -276,93 +381,61 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
     for (int64_t q = 0; q < p->ngr; ++q) ar_push(p, p->gr[q].recv, p->gr[q].slot, p->gr[q].er);
     p->ngr = 0;
 
-    /* 2. receivers handle the copies, in canonical order */
+    /* 2. receivers handle the copies, in canonical order: by receiver
+     * (counting sort, stable), then by (slot, receiver edge) within one */
     arr_ent* ar = p->ar;
     const int64_t nar = p->nar;
     p->ar = NULL; p->nar = 0; p->capar = 0;
-    qsort(ar, (size_t)nar, sizeof(arr_ent), cmp_arr);
-    for (int64_t q = 0; q < nar; ++q) {
-        const uint32_t i = ar[q].recv, slot = ar[q].slot, er = ar[q].er;
-        const int32_t t = (int32_t)m->topic[slot];
-        if (s->score[er] < gray && !(s->direct && s->direct[er])) {   /* AcceptFrom -> AcceptNone; direct: AcceptAll */
-            m->stats[3]++;
-            continue;
-        }
-        if (s->gater && !(s->direct && s->direct[er]) && !orc_gater_accept(s, p->seed, g, i, er, slot)) {
-            /* the peer gater's AcceptControl: the message is dropped and the
-             * receiver forgets its promises from the sender (ThrottlePeer,
-             * gossip_tracer.go:182-200) */
-            if (p->npr) {
-                int32_t w = 0;
-                for (int32_t q2 = 0; q2 < p->npr[i]; ++q2)
-                    if (p->pr[i][q2].e != er) p->pr[i][w++] = p->pr[i][q2];
-                p->npr[i] = w;
-            }
-            orc_log(m, ORC_EV_THROTTLE, i, s->col[er], slot, t, g, now);
-            continue;
-        }
-        /* a topic the receiver no longer subscribes to: the message is skipped
-         * (pubsub.go:1094-1098; only after a Leave, orc_set_subscriptions) */
-        if (!((s->sub[i] >> t) & 1u)) continue;
-        m->stats[0]++;
-        uint32_t* cell = &m->seen[(int64_t)slot * s->n + i];
-        const uint8_t verdict = m->invalid[slot];
-        if (verdict == GSIM_VERDICT_SIGNATURE) {
-            orc_gater_event(s, i, er, t, ORC_GATE_REJECT);      /* RejectInvalidSignature */
-            /* RejectInvalidSignature before markSeen (validation.go:282-290):
-             * every copy's sender is penalised, nothing is seen, no promise is
-             * fulfilled (gossip_tracer.go:148-162) */
-            m->stats[2]++;
-            orc_mark_invalid(s, er, t);
-            orc_log(m, ORC_EV_REJECT_SIG, i, s->col[er], slot, t, g, 0);
-            continue;
-        }
-        const uint8_t vdelay = p->vd ? p->vd[slot] : 0;
-        if (!vdelay || *cell != UNSEEN) orc_log(m, ORC_EV_SEEN, i, s->col[er], slot, t, g, *cell == UNSEEN);
-        if (s->gater) {
-            /* first delivery: ValidateMessage, then the verdict's tracer call */
-            static const int32_t kind[4] = {ORC_GATE_DELIVER, ORC_GATE_REJECT, ORC_GATE_IGNORE, ORC_GATE_THROTTLE};
-            if (*cell == UNSEEN) orc_gater_event(s, i, er, t, ORC_GATE_VALIDATE);
-            orc_gater_event(s, i, er, t, *cell == UNSEEN ? kind[verdict] : ORC_GATE_DUPLICATE);
-        }
-        if (*cell == UNSEEN && vdelay) {
-            /* markSeen + ValidateMessage (promises fulfilled); the verdict
-             * lands vdelay rounds later (complete_validations) */
-            *cell = (uint32_t)(g + vdelay);
-            m->stats[1]++;
-            orc_gossip_fulfill(m, i, slot);
-            if (p->slot_last) p->slot_last[slot] = g;
-            pq_push(p, g + vdelay, i, slot, er, 1);
-        } else if (*cell != UNSEEN && (int64_t)*cell > g) {
-            /* DuplicateMessage while the first copy validates
-             * (deliveryUnknown: drec.peers, score.go:806-809) */
-            m->stats[2]++;
-            if (verdict == GSIM_VERDICT_REJECT || verdict == GSIM_VERDICT_ACCEPT) pq_push(p, *cell, i, slot, er, 0);
-        } else if (*cell == UNSEEN) {
-            *cell = (uint32_t)g;               /* markSeen */
-            m->stats[1]++;
-            orc_gossip_fulfill(m, i, slot);    /* gossipTracer: promises for it are kept */
-            if (p->slot_last) p->slot_last[slot] = g;
-            if (verdict == GSIM_VERDICT_REJECT) {
-                /* ValidateMessage + RejectMessage(ValidationFailed), score.go:728-793 */
-                orc_mark_invalid(s, er, t);
-            } else if (verdict == GSIM_VERDICT_ACCEPT) {
-                /* DeliverMessage, score.go:702-726; mcache.Put; forward next round */
-                orc_mark_first(s, er, t);
-                m->lastput[(int64_t)t * s->n + i] = (int32_t)(g / m->rounds);
-                orc_log(m, ORC_EV_PUT, i, 0, slot, t, g, 0);
-                fr_push(p, i, slot, s->col[er]);
-            }
-            /* RejectValidationIgnored / Throttled: deliveryIgnored / deliveryThrottled,
-             * no penalty and no credit (score.go:759-781) */
-        } else {
-            m->stats[2]++;                     /* DuplicateMessage, score.go:795-827 */
-            if (verdict == GSIM_VERDICT_REJECT) orc_mark_invalid(s, er, t);
-            else if (verdict == GSIM_VERDICT_ACCEPT)
-                orc_mark_duplicate(s, er, t, 1, orc_round_time(m, (int64_t)*cell), now);
-        }
+    arr_ent* sorted = (arr_ent*)malloc(sizeof(arr_ent) * (size_t)(nar > 0 ? nar : 1));
+    int64_t* start = (int64_t*)calloc((size_t)s->n + 1, sizeof(int64_t));
+    for (int64_t q = 0; q < nar; ++q) start[ar[q].recv + 1]++;
+    for (int64_t i = 0; i < s->n; ++i) start[i + 1] += start[i];
+    {
+        int64_t* fill = (int64_t*)malloc(sizeof(int64_t) * (size_t)(s->n > 0 ? s->n : 1));
+        memcpy(fill, start, sizeof(int64_t) * (size_t)s->n);
+        for (int64_t q = 0; q < nar; ++q) sorted[fill[ar[q].recv]++] = ar[q];
+        free(fill);
     }
     free(ar);
+    /* receivers are independent (each copy touches its receiver's records,
+     * cell, mcache and promises), so they run in parallel unless the event
+     * log or validation latency needs one global order */
+    int serial = p->log_on != 0;
+    if (p->vd)
+        for (int32_t q = 0; q < m->ring && !serial; ++q) serial = p->vd[q] != 0;
+    int nth = 1;
+#ifdef _OPENMP
+    nth = serial ? 1 : omp_get_max_threads();
+#endif
+    frbuf* fb = (frbuf*)calloc((size_t)nth, sizeof(frbuf));
+    int64_t stats[4] = {0, 0, 0, 0};
+#pragma omp parallel num_threads(nth) reduction(+ : stats[:4])
+    {
+        int tid = 0;
+#ifdef _OPENMP
+        tid = omp_get_thread_num();
+#endif
+#pragma omp for schedule(dynamic, 256)
+        for (int64_t i = 0; i < s->n; ++i) {
+            arr_ent* seg = sorted + start[i];
+            const int64_t len = start[i + 1] - start[i];
+            for (int64_t a = 1; a < len; ++a) {          /* by (slot, er): a handful of copies */
+                arr_ent x = seg[a];
+                int64_t b = a - 1;
+                while (b >= 0 && cmp_arr(&seg[b], &x) > 0) { seg[b + 1] = seg[b]; --b; }
+                seg[b + 1] = x;
+            }
+            for (int64_t q = 0; q < len; ++q) handle_copy(s, m, p, g, now, gray, seg[q], &fb[tid], stats);
+        }
+    }
+    for (int k = 0; k < 4; ++k) m->stats[k] += stats[k];
+    for (int t = 0; t < nth; ++t) {
+        for (int64_t q = 0; q < fb[t].n; ++q) fr_push(p, fb[t].v[q].peer, fb[t].v[q].slot, fb[t].v[q].from);
+        free(fb[t].v);
+    }
+    free(fb);
+    free(start);
+    free(sorted);
     orc_gater_round_end(s, now);
 
     /* 3. control records of this round: GRAFT/PRUNE, then IHAVE (round 0)

@@ -162,6 +162,7 @@ int orc_gater_accept(orc_net* s, uint64_t seed, int64_t g_round, uint32_t i, uin
     if (total == 0) return 1;
     const double threshold = (1 + g->del[r]) / (1 + total);
     if (orc_gater_uniform(seed, g_round, i, slot, s->col[er]) < threshold) return 1;
+#pragma omp atomic
     g->throttled++;
     return 0;
 }
