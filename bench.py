@@ -472,6 +472,8 @@ def main():
         alg_refresh = (refresh_bytes(census0, E) + refresh_bytes(census1, E)) // 2
         if sharded and world > 1:   # the kernels timed are rank 0's shard: its share of the network
             alg_refresh = alg_refresh // world
+        elif per_shard is not None:  # in-process shards: ref_ms below is the average launch of ONE shard
+            alg_refresh = alg_refresh // args.shards
         ref_ms = prof["refresh_score"][0] / max(1, launches["refresh_score"])
         ref_gbs = alg_refresh / (ref_ms * 1e-3) / 1e9
         # delivery: SURVEY.md §8(d) bytes per first / duplicate delivery, over send+commit(+accept)
@@ -483,14 +485,15 @@ def main():
         deliv_ms = kms["send"] + kms["commit"] + kms["accept"]
         deliv_gbs = alg_deliv / (deliv_ms * 1e-3) / 1e9 if deliv_ms > 0 else 0.0
         # traffic: PMC HBM bytes (profiles/traffic.json), per launch like `achieved`
-        tr_ref = load_traffic(args.config)
+        # (measured on the default kernels: a --vdelay run uses other instances, so none is attached)
+        tr_ref = None if args.vdelay else load_traffic(args.config)
         roof_refresh = {"bound": "hbm", "achieved": ref_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": ref_gbs / HBM_PEAK_GBS,
                         "traffic": tr_ref["bytes_per_launch"] if tr_ref else None, "traffic_detail": tr_ref,
                         "kernel": "k_refresh_score<true,true>", "kernel_ms": ref_ms,
                         "algorithmic_bytes_per_launch": alg_refresh}
         # PMC traffic of k_send (per launch) scaled to a tick, the unit delivery's bytes are quoted in
-        tr_send = load_traffic(args.config + ":send")
+        tr_send = None if args.vdelay else load_traffic(args.config + ":send")
         tr_send_tick = None
         if tr_send is not None:
             tr_send_tick = tr_send["bytes_per_launch"] * launches["send"] / K
@@ -536,7 +539,8 @@ def main():
             "roofline": dominant,
             "roofline_kernels": {"refresh_score": roof_refresh, "delivery": roof_deliv},
         }
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and not args.vdelay:
+            # (the oracle baseline publishes without latency: not the same workload as a --vdelay line)
             out["cpu_baseline"] = cpu_baseline(cfg, scen=scen)
         print(json.dumps(out), flush=True)
     eng.close()

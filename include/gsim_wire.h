@@ -164,7 +164,11 @@ int gsim_wire_heartbeat(gsim_handle* h, int64_t tick, uint32_t p0, uint32_t p1, 
  * and the event's message} per record, fields in number order as gogo's
  * Marshal writes them (trace.pb.go).  Peer ids come from names->peer_ids (4
  * big-endian bytes of the peer index when peer_id_len is 0), topics from
- * names->topic_names; a messageID is the gsim id as 8 big-endian bytes;
+ * names->topic_names; a messageID is the gsim id as 8 big-endian bytes —
+ * the seqno alone, even when peer_ids is given (trace records carry no
+ * origin), so with peer ids these messageIDs are NOT the ids
+ * gsim_wire_heartbeat's IHAVEs carry (peer_id(origin) || seqno): join the
+ * two on the trailing 8 bytes;
  * AddPeer.proto is `proto` (e.g. "/meshsub/1.1.0"); RejectMessage.reason is
  * the reference's string for the verdict (tracer.go:31-38).  *len: the
  * bytes written (GSIM_ERANGE with *len = the size needed when cap is short). */
