@@ -213,6 +213,15 @@ struct RoundArgs {
     // sharded: the edges of each row into owned peers (the copies this shard
     // delivers), a CSR of edge indices: row x's are sedge[sptr[x] .. sptr[x+1])
     const uint32_t *sptr, *sedge;
+    // sharded, copy push: a copy to a ghost receiver goes to
+    // sub-list (its shard pshard[i], block % kXSub) as xre[e] | slot << 32
+    int32_t push, xK;
+    int64_t slo, shi;              // k_send_tm's senders: [slo, shi) (slo a multiple of its chunk)
+    const uint32_t* xre;
+    const uint8_t* pshard;
+    uint64_t* xsub;
+    uint32_t* xcnt;
+    int64_t xsub_cap;
     // [T][n] rows of at most 64 connections: bit q = row position q is a mesh or
     // direct edge (to an owned peer); a forwarder other than the origin sends
     // on no other edge, so only these are walked
@@ -383,6 +392,33 @@ __device__ __forceinline__ void clist_push_wave(const RoundArgs& a, bool on, uin
 
 // Ordered list of the active slots (bit set in nnew), built by wave 0 into
 // LDS; every thread of the block must call it.
+// A copy to a ghost receiver (k_send_tm<PUSH>): entry v = receiver-shard edge
+// | slot << 32 | shard << 48 appended to sub-list (shard, wave % kXSub); one
+// atomic per (wave, destination).  Wave-uniform call.
+__device__ __forceinline__ void xcopy_push_wave(const RoundArgs& a, bool on, uint64_t v)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t dst = (uint32_t)(v >> 48);
+    uint64_t act = __ballot(on);
+    while (act) {
+        const int leader = __builtin_ctzll(act);
+        const uint32_t dl = (uint32_t)__shfl((int)dst, leader, 64);
+        const bool mine = on && dst == dl;
+        const uint64_t grp = __ballot(mine);
+        // sub-list by wave: the block's waves spread over the counters (each on its own line)
+        const int64_t sl = (int64_t)dl * kXSub + (int64_t)((blockIdx.x * 16u + (threadIdx.x >> 6)) % kXSub);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&a.xcnt[sl * kXStride], (uint32_t)__popcll(grp));
+        base = (uint32_t)__shfl((int)base, leader, 64);
+        if (mine) {
+            const uint32_t q = base + (uint32_t)__popcll(grp & ((1ull << lane) - 1ull));
+            if ((int64_t)q < a.xsub_cap) a.xsub[sl * a.xsub_cap + q] = v & 0xFFFFFFFFFFFFull;
+            else atomicOr(&a.xcnt[(int64_t)a.xK * kXSub * kXStride], 1u);   // overflow: the round fails
+        }
+        act &= ~grp;
+    }
+}
+
 __device__ __forceinline__ int active_slots(const uint32_t* nnew, int ring, uint16_t* s_act, int* s_n)
 {
     if (threadIdx.x < 64) {
@@ -525,7 +561,8 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, const uint32_t* pslo
         const uint32_t oc = p.origin;
         a.cs.cell[oci] = ((uint64_t)(uint32_t)a.g << 32) | p.origin;
         atomicOr(reinterpret_cast<unsigned long long*>(a.seenbm + (int64_t)slot * a.nw + (oc >> 6)), 1ull << (oc & 63));
-        if (a.fresh) fresh_set(a, slot, oc >> 6, 1ull << (oc & 63));   // the origin publishes whatever the verdict
+        // the origin publishes whatever the verdict (push: a ghost origin's own shard sends)
+        if (a.fresh && (!a.push || (oc >= a.rlo && oc < a.rhi))) fresh_set(a, slot, oc >> 6, 1ull << (oc & 63));
         int32_t* lp = a.lastput + (int64_t)p.topic * a.N + p.origin;
         const int32_t tick = (int32_t)(a.g / a.R);
         if (*lp < tick) *lp = tick;
@@ -666,7 +703,7 @@ constexpr int kTmTabMin = 256;      // forwarders in a chunk from which the tabl
 
 // SP: topic slots or member-compacted cells are in use (gsim_internal.h); the
 // dense instance indexes plane t and cell m * N + p with no table reads.
-template <int kTmThreads, bool LAT, bool SP, bool GT = false>
+template <int kTmThreads, bool LAT, bool SP, bool GT = false, bool PUSH = false>
 __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs a)
 {
     extern __shared__ uint64_t s_dyn[];
@@ -682,7 +719,8 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
     __shared__ uint8_t s_sk[kTmChunk];                       // its slot (index in the pass)
     __shared__ uint8_t s_pl[kTmChunk];                       // its row's topic slot of t (plane, gsim_internal.h)
     __shared__ uint16_t s_own[kTmWin];                       // sender (index above) of each flattened edge of a window
-    __shared__ uint64_t s_cl[SP && !LAT ? kTmThreads * GSIM_TM_P : 1];   // claim-list entries of the iteration's copies
+    // claim-list entries of the iteration's copies, or (PUSH) copies to ghost receivers
+    __shared__ uint64_t s_cl[(SP && !LAT) || PUSH ? kTmThreads * GSIM_TM_P : 1];
     __shared__ uint32_t s_wsum[64];
     __shared__ uint32_t s_m[kTsSlots], s_org[kTsSlots];      // the pass's slots and their origins
     __shared__ uint64_t s_cb[kTsSlots];                      // ... and their first cells (Cells::cbase)
@@ -701,8 +739,8 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
         }
     }
     const int64_t range = a.tmtab[(a.T > 0 ? a.T : 1) + 1 + t];
-    const int64_t pend_ = a.CN;
-    const int64_t lo = (int64_t)(lb - a.tmtab[t]) * range;
+    const int64_t pend_ = a.shi;
+    const int64_t lo = a.slo + (int64_t)(lb - a.tmtab[t]) * range;
     const int64_t hi = lo + range < pend_ ? lo + range : pend_;
     const int64_t wlo = (int64_t)a.rlo >> 6;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -937,6 +975,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                         int qpl[P];              // validation latency: queue plane of the copy (-1: none)
                         uint64_t qv[P];
                         uint32_t clw = 0;        // bit u: copy u claimed an unseen cell (its entry in s_cl)
+                        uint32_t xw = 0;         // bit u: copy u goes to a ghost receiver's shard (PUSH, s_cl)
 #pragma unroll
                         for (int u = 0; u < P; ++u) { qpl[u] = -1; qv[u] = 0; }
 #pragma unroll
@@ -957,6 +996,15 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             if (vv[u] && (ds & GSIM_DS_DIRECT) && !sel) sel = (a.sub[i] >> t) & 1ull;
                             const bool tg = vv[u] && sel && (ds & GSIM_DS_CONNECTED) && i != fv[u] && i != origin;
                             const bool remote = i < a.rlo || i >= a.rhi;
+                            if constexpr (PUSH) {
+                                // the receiver's shard delivers it (its AcceptFrom, records, cell)
+                                if (tg && remote) {
+                                    xw |= 1u << u;
+                                    s_cl[u * kTmThreads + tid] = (uint64_t)a.xre[e] | ((uint64_t)m << 32) |
+                                                                 ((uint64_t)a.pshard[i] << 48);
+                                    continue;
+                                }
+                            }
                             const bool ok = tg && !remote && (ds & GSIM_DS_ACCEPT);
                             n_gray += tg && !remote && !ok;
                             if (!ok) continue;
@@ -1056,6 +1104,10 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                                 for (int u = 0; u < P; ++u)
                                     clist_push_wave(a, (clw >> u) & 1u, s_cl[u * kTmThreads + tid]);
                             }
+                        }
+                        if constexpr (PUSH) {
+#pragma unroll
+                            for (int u = 0; u < P; ++u) xcopy_push_wave(a, (xw >> u) & 1u, s_cl[u * kTmThreads + tid]);
                         }
                     }
                     if (tab) __syncthreads();                    // s_own is rewritten by the next window
@@ -2185,11 +2237,23 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.sub = h->d_sub; a.score = h->d_score; a.rev = h->d_rev;
     a.flood = h->gp.flood_publish ? 1 : 0;
     a.pub_thr = h->th.publish_threshold;
+    a.slo = 0;
+    a.shi = a.CN;
     if (ShardCtx* sh = h->sh) {
         a.sharded = 1;
         a.pgate = sh->d_pgate;
-        a.sptr = sh->d_sptr;
-        a.sedge = sh->d_sedge;
+        if (sh->push) {
+            // owned senders walk their whole rows; ghosts never send here
+            a.push = 1;
+            a.xK = sh->K;
+            a.xre = sh->d_xre; a.pshard = sh->d_pshard;
+            a.xsub = sh->d_xsub; a.xcnt = sh->d_xcnt; a.xsub_cap = sh->xsub_cap;
+            a.slo = (sh->own_lo / (2 * GSIM_TM_TB)) * (2 * GSIM_TM_TB);
+            a.shi = sh->own_hi;
+        } else {
+            a.sptr = sh->d_sptr;
+            a.sedge = sh->d_sedge;
+        }
     }
     return a;
 }
@@ -2514,9 +2578,12 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
     constexpr int TB = GSIM_TM_TB;
     constexpr int64_t total = 2048 * (1024 / TB);
     constexpr int64_t chunk = 2 * TB;
-    const int64_t cn = h->n;                 // every local peer sends (a shard's ghosts too)
+    // every local peer sends (pull: a shard's ghosts too), or the owned range (push)
+    const int64_t cn = a0.shi - a0.slo;
     const int T = std::max(1, h->t);
-    const int64_t ranges = std::max<int64_t>(1, std::min<int64_t>((cn + 4095) / 4096,
+    // (push: a shard's owned range alone, ranges down to one chunk)
+    const int64_t min_range = a0.push ? chunk : 4096;
+    const int64_t ranges = std::max<int64_t>(1, std::min<int64_t>((cn + min_range - 1) / min_range,
                                                                     std::max<int64_t>(h->t >= 32 ? 256 : 1,
                                                                                       total / T)));
     Deliver* d = h->dl;
@@ -2551,7 +2618,11 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
     const RoundArgs& a = a0;
     // the slot list in LDS
     const size_t lds = ((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7;
-    if (a.mlat)
+    if (a.push && sparse_layout(h))
+        hipLaunchKernelGGL((k_send_tm<TB, false, true, false, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+    else if (a.push)
+        hipLaunchKernelGGL((k_send_tm<TB, false, false, false, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+    else if (a.mlat)
         hipLaunchKernelGGL((k_send_tm<TB, true, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
     else if (a.gt.act && sparse_layout(h))
         hipLaunchKernelGGL((k_send_tm<TB, false, true, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
@@ -2634,6 +2705,8 @@ int deliver_round_send(gsim_handle* h, int64_t round)
     int rc = 0;
     RoundArgs a = make_round_args(h, round);
     h->mcnt_dirty = true;
+    // the receivers a forwarder's walk covers: every peer (push), else the owned ones
+    const uint32_t mlo = a.push ? 0u : (uint32_t)h->olo(), mhi = a.push ? (uint32_t)h->n : (uint32_t)h->ohi();
     {
         ProfScope ps(h, GSIM_K_SEND);
         if (d->mask_version != h->mesh_version) {
@@ -2645,7 +2718,7 @@ int deliver_round_send(gsim_handle* h, int64_t round)
                                h->stream, (const uint32_t*)h->d_row_ptr, (const uint32_t*)h->d_col,
                                (const uint8_t*)h->d_mflags, (const uint8_t*)h->d_direct,
                                (const uint64_t*)h->d_smask, h->n, h->e,
-                               std::max(1, h->t), (uint32_t)h->olo(), (uint32_t)h->ohi(), d->d_mmask);
+                               std::max(1, h->t), mlo, mhi, d->d_mmask);
             d->mask_version = h->mesh_version;
             d->hub_round = -1;
         }
@@ -2656,7 +2729,7 @@ int deliver_round_send(gsim_handle* h, int64_t round)
                                h->stream, (const uint32_t*)h->d_row_ptr, (const uint32_t*)h->d_col,
                                (const uint8_t*)h->d_mflags, (const uint8_t*)h->d_direct,
                                (const uint64_t*)h->d_smask, (const uint32_t*)d->d_hrow, d->nhub, h->e,
-                               std::max(1, h->t), (uint32_t)h->olo(), (uint32_t)h->ohi(), d->d_hlist);
+                               std::max(1, h->t), mlo, mhi, d->d_hlist);
             d->hub_round = round;
         }
         // one thread per edge: forwarders walk only their mesh edges (a
@@ -2804,7 +2877,9 @@ __global__ __launch_bounds__(256) void k_frontier_import(RoundArgs a, const uint
             l = g2l[v & kG24];
             ghost = l != 0xFFFFFFFFu && !(l >= a.rlo && l < a.rhi);         // a ghost of this shard
             if (ghost) {
-                const uint64_t gf = (v >> 24) & kG24;
+                // (push: only the round is read, by IHAVE; pull: the first
+                // sender too, by the ghost's walk)
+                const uint64_t gf = a.push ? kG24 : (v >> 24) & kG24;
                 uint32_t f = gf == kG24 ? 0xFFFFFFFFu : g2l[gf];
                 if (f == 0xFFFFFFFFu) f = kPeerMask;                         // not a local peer
                 m = (uint32_t)(v >> 48);
@@ -2813,7 +2888,8 @@ __global__ __launch_bounds__(256) void k_frontier_import(RoundArgs a, const uint
                 // (filtering out ghosts without mesh edges into this shard, by
                 // their masks, cost more in the import than it saved in the
                 // walk: K = 8 serial shards 31.8 against 20.2 ms per tick)
-                fwd = true;
+                // push: the cell alone (IHAVE holders); the ghost's own shard sends
+                fwd = !a.push;
             }
         }
         // one atomic per run of equal (slot, word) keys: a segmented OR scan

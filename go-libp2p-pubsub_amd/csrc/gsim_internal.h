@@ -212,7 +212,24 @@ struct ShardCtx {
     uint64_t* d_gin = nullptr;             // [e] (ghost-row positions)
     uint8_t* d_gsin = nullptr;             // [e]
     uint32_t* h_counts = nullptr;          // pinned scratch for count readbacks
+    // copy push: a round's copies from owned senders to ghost
+    // receivers go to the receivers' shards as (receiver-shard edge | slot << 32)
+    bool push = true;
+    std::vector<int64_t> rbase;            // [K] first local edge of this shard's ghost block at shard d
+    uint32_t* d_xre = nullptr;             // [e] owned-row cross edge: the edge's index at the receiver's shard
+    uint8_t* d_pshard = nullptr;           // [n] shard of each local peer
+    uint64_t* d_xsub = nullptr;            // [K][kXSub][xsub_cap] sub-lists of outbound copies
+    uint32_t* d_xcnt = nullptr;            // [K * kXSub + 1] their counts, then an overflow flag (stride kXStride)
+    int64_t xsub_cap = 0;
+    uint64_t* d_xsend = nullptr;           // [K][xsend_cap] each destination's copies, contiguous
+    int64_t xsend_cap = 0;
+    uint64_t* d_xrecv = nullptr;           // copies from every other shard
+    int64_t xrecv_cap = 0;
+    uint32_t* d_xn = nullptr;              // [1] copies received
+    uint32_t* h_xcnt = nullptr;            // pinned: count readback ([K * kXSub + 1] strided), then the received count
 };
+constexpr int kXSub = 32;                  // outbound sub-lists per destination (append contention)
+constexpr int kXStride = 32;               // u32s between two sub-list counters (one cache line each)
 
 // Seen-set cells [ring][N] (deliver.hip): unseen; committed (hi = first-seen
 // round, lo = first sender); or claimed in round g (hi = kClaim | parity of g

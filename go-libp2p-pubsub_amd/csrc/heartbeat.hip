@@ -92,6 +92,7 @@ struct HbArgs {
     const uint32_t* gid;
     uint32_t olo, ohi;
     uint64_t* mmask;           // [T][N] delivery's mesh masks (nullptr before gsim_msgs_init)
+    uint32_t mlo, mhi;         // ... of edges to [mlo, mhi): a shard's owned peers (pull) or all (push)
     // a shard's control pass: mesh changes of cross edges for the other shards'
     // ghost rows (src | dest << 6 | topic << 12 | flags << 20 | position << 32)
     uint64_t* rdel;
@@ -985,7 +986,7 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
                     bool mm[V];
 #pragma unroll
                     for (int v = 0; v < V; ++v)
-                        mm[v] = valid[v] && (m[v] || dir[v]) && col[v] >= a.olo && col[v] < a.ohi;
+                        mm[v] = valid[v] && (m[v] || dir[v]) && col[v] >= a.mlo && col[v] < a.mhi;
                     const uint64_t mk = g.row_mask(mm);
                     if (gl[0] == 0 && ovalid) a.mmask[(int64_t)t * a.N + obs] = mk;
                 }
@@ -1326,7 +1327,7 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
               }
               if (nch == 1 && a.mmask) {                      // the delivery's mesh mask of the row
                   const uint32_t cj = valid ? a.col[e] : 0u;
-                  const uint64_t mk = ballot(valid && ((fl & GSIM_TF_MESH) || a.direct[e]) && cj >= a.olo && cj < a.ohi);
+                  const uint64_t mk = ballot(valid && ((fl & GSIM_TF_MESH) || a.direct[e]) && cj >= a.mlo && cj < a.mhi);
                   if (lane == 0) a.mmask[(int64_t)t * a.N + rcv] = mk;
               }
             }
@@ -2058,6 +2059,9 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     }
     a.olo = (uint32_t)h->olo();
     a.ohi = (uint32_t)h->ohi();
+    const bool push = h->sh && h->sh->push;
+    a.mlo = push ? 0u : a.olo;
+    a.mhi = push ? (uint32_t)h->n : a.ohi;
     a.do_px = h->x->d_pxo ? 1 : 0;
     a.prune_peers = h->gp.prune_peers;
     a.accept_px = h->th.accept_px_threshold;

@@ -6,12 +6,14 @@
 // is split into contiguous peer ranges (shard_plan.cpp).  Each shard is an
 // ordinary engine handle over its local graph — owned rows plus ghost rows
 // (a remote neighbour's connections into the shard) — that computes only for
-// its owned peers.  Copies are pulled, not pushed: a shard learns which
-// ghosts forward which message this round and walks their ghost rows itself,
-// so every delivery is processed by the receiver's shard with the same
-// kernel as a local one.  What moves between shards:
-//   per round      the forwarders of the round (peer, first sender, slot),
-//                  from every shard to every other (the frontier);
+// its owned peers.  Copies are pushed: a shard walks its own forwarders'
+// whole rows and sends each copy to a ghost receiver to the receiver's shard
+// as (the edge's index there, slot), which applies it (AcceptFrom, claim,
+// records) before its commit (GSIM_SHARD_PULL=1: round 2's pull, where the
+// receiver's shard walks the ghost forwarders' rows itself).  What moves:
+//   per round      the copies to other shards' peers (push), and the
+//                  forwarders of the round (peer, first sender, slot), from
+//                  every shard to every other (the frontier: ghost cells);
 //   per control    GRAFT/PRUNE records written into ghost receivers' inboxes,
 //                  and then the router state of cross edges (mesh and fanout
 //                  bits, connected, direct, publish gate) into ghost rows;
@@ -267,6 +269,33 @@ __global__ __launch_bounds__(256) void k_router_delta(const uint64_t* in, int64_
     }
 }
 
+// Copy push: an owned-row cross edge's index at the
+// receiver's shard = that shard's ghost block of this shard's peers (rb) +
+// the edge's position in the cross-out list to it.
+__global__ __launch_bounds__(256) void k_xre_build(const uint32_t* xq, const uint32_t* col, const uint8_t* pshard,
+                                                   EdgeBases rb, uint32_t* xre, int64_t E)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += stride)
+        xre[e] = xq[e] == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)(rb.b[pshard[col[e]]] + (int64_t)xq[e]);
+}
+
+// A round's outbound copies: each destination's kXSub sub-lists (k_send_tm
+// appends) into one contiguous list, in sub-list order.  Blocks (destination,
+// sub-list) x gridDim.y slices.
+__global__ __launch_bounds__(256) void k_xcompact(const uint64_t* xsub, const uint32_t* xcnt, int64_t sub_cap,
+                                                  uint64_t* xsend, int64_t send_cap)
+{
+    const int32_t b = (int32_t)blockIdx.x, d = b / kXSub, q = b % kXSub;
+    int64_t off = 0;
+    for (int32_t k = 0; k < q; ++k) off += std::min<int64_t>(xcnt[(d * kXSub + k) * kXStride], sub_cap);
+    const int64_t n = std::min<int64_t>(xcnt[b * kXStride], sub_cap);
+    const uint64_t* src = xsub + (int64_t)b * sub_cap;
+    uint64_t* dst = xsend + (int64_t)d * send_cap + off;
+    const int64_t stride = (int64_t)gridDim.y * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.y * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+}
+
 int grid_for(int64_t n)
 {
     int64_t g = (n + 255) / 256;
@@ -469,6 +498,131 @@ struct RcclTransport : Transport {
     }
 };
 
+// One shard per process, exchanges through the caller's host collectives
+// (gsim_host_transport): every device buffer is staged through pinned host
+// memory.  Same call sequence as RcclTransport, so it runs the one-shard-
+// per-process path of the group on any number of ranks per GPU.
+struct HostTransport : Transport {
+    gsim_handle* h = nullptr;
+    int k = 0, K = 1;
+    gsim_host_transport cb{};
+    uint8_t* hs_ = nullptr;          // pinned staging: send | recv
+    size_t hcap = 0;
+    ~HostTransport() override
+    {
+        if (hs_) (void)hipHostFree(hs_);
+    }
+    int stage(size_t need)
+    {
+        if (need <= hcap) return GSIM_OK;
+        if (hs_) (void)hipHostFree(hs_);
+        hs_ = nullptr;
+        hcap = 0;
+        const size_t c = std::max<size_t>(need + need / 2, 1 << 16);
+        if (hipHostMalloc((void**)&hs_, c, 0) != hipSuccess) { err = "pinned staging"; return GSIM_ENOMEM; }
+        hcap = c;
+        return GSIM_OK;
+    }
+    int sync() override
+    {
+        if (hipStreamSynchronize(h->stream) != hipSuccess) { err = "stream synchronize"; return GSIM_EDEVICE; }
+        return GSIM_OK;
+    }
+    // host-to-host all-to-all of byte blocks (the rank's own block skipped)
+    int a2a(const uint8_t* send, const std::vector<uint64_t>& sb, uint8_t* recv, const std::vector<uint64_t>& rb)
+    {
+        std::vector<uint64_t> sd((size_t)K, 0), rd((size_t)K, 0);
+        for (int q = 1; q < K; ++q) { sd[(size_t)q] = sd[(size_t)q - 1] + sb[(size_t)q - 1]; rd[(size_t)q] = rd[(size_t)q - 1] + rb[(size_t)q - 1]; }
+        if (cb.alltoallv(cb.ctx, send, sb.data(), sd.data(), recv, rb.data(), rd.data()) != 0) {
+            err = "host alltoallv callback";
+            return GSIM_EDEVICE;
+        }
+        return GSIM_OK;
+    }
+    int exchange_counts(const std::vector<std::vector<uint64_t>>& send, std::vector<std::vector<uint64_t>>& recv) override
+    {
+        // blocks are packed in rank order without this rank's own
+        std::vector<uint64_t> out, in((size_t)K, 0), b((size_t)K, 8);
+        for (int d = 0; d < K; ++d)
+            if (d != k) out.push_back(send[0][(size_t)d]);
+        out.push_back(0);
+        b[(size_t)k] = 0;
+        int rc = a2a(reinterpret_cast<const uint8_t*>(out.data()), b, reinterpret_cast<uint8_t*>(in.data()), b);
+        if (rc) return rc;
+        // the packed blocks skip this rank: unpack in rank order
+        recv.assign(1, std::vector<uint64_t>((size_t)K, 0));
+        size_t x = 0;
+        for (int s = 0; s < K; ++s) {
+            if (s == k) { recv[0][(size_t)s] = send[0][(size_t)s]; continue; }
+            recv[0][(size_t)s] = in[x++];
+        }
+        return GSIM_OK;
+    }
+    int alltoallv(const std::vector<std::vector<const void*>>& sp, const std::vector<std::vector<uint64_t>>& sb,
+                  const std::vector<std::vector<void*>>& rp, const std::vector<std::vector<uint64_t>>& rb) override
+    {
+        std::vector<uint64_t> s8((size_t)K, 0), r8((size_t)K, 0);
+        size_t st = 0, rt = 0;
+        for (int q = 0; q < K; ++q) {
+            if (q == k) continue;
+            s8[(size_t)q] = sb[0][(size_t)q];
+            r8[(size_t)q] = rb[0][(size_t)q];
+            st += s8[(size_t)q];
+            rt += r8[(size_t)q];
+        }
+        int rc = stage(st + rt);
+        if (rc) return rc;
+        uint8_t* sh = hs_;
+        uint8_t* rh = hs_ + st;
+        size_t off = 0;
+        for (int q = 0; q < K; ++q) {
+            if (!s8[(size_t)q]) continue;
+            if (hipMemcpyAsync(sh + off, sp[0][(size_t)q], s8[(size_t)q], hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+                { err = "staging download"; return GSIM_EDEVICE; }
+            off += s8[(size_t)q];
+        }
+        if ((rc = sync())) return rc;
+        if ((rc = a2a(sh, s8, rh, r8))) return rc;
+        off = 0;
+        for (int q = 0; q < K; ++q) {
+            if (!r8[(size_t)q]) continue;
+            if (hipMemcpyAsync(rp[0][(size_t)q], rh + off, r8[(size_t)q], hipMemcpyHostToDevice, h->stream) != hipSuccess)
+                { err = "staging upload"; return GSIM_EDEVICE; }
+            off += r8[(size_t)q];
+        }
+        return sync();            // the staging buffer is reused by the next exchange
+    }
+    int allreduce(const std::vector<void*>& p, int64_t count, int dt, int op) override
+    {
+        const size_t bytes = (size_t)count * (dt == DT_U64 ? 8 : 4);
+        int rc = stage(bytes);
+        if (rc) return rc;
+        if (hipMemcpyAsync(hs_, p[0], bytes, hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+            { err = "staging download"; return GSIM_EDEVICE; }
+        if ((rc = sync())) return rc;
+        if (cb.allreduce(cb.ctx, hs_, count, dt, op) != 0) { err = "host allreduce callback"; return GSIM_EDEVICE; }
+        if (hipMemcpyAsync(p[0], hs_, bytes, hipMemcpyHostToDevice, h->stream) != hipSuccess)
+            { err = "staging upload"; return GSIM_EDEVICE; }
+        return sync();
+    }
+    int allgatherv(const std::vector<void*>& buf, const std::vector<uint64_t>& off,
+                   const std::vector<uint64_t>& bytes) override
+    {
+        // this rank's block to every other rank, theirs into their offsets
+        std::vector<std::vector<const void*>> sp(1, std::vector<const void*>((size_t)K, nullptr));
+        std::vector<std::vector<void*>> rp(1, std::vector<void*>((size_t)K, nullptr));
+        std::vector<std::vector<uint64_t>> sb(1, std::vector<uint64_t>((size_t)K, 0)), rb = sb;
+        for (int q = 0; q < K; ++q) {
+            if (q == k) continue;
+            sp[0][(size_t)q] = (const uint8_t*)buf[0] + off[(size_t)k];
+            sb[0][(size_t)q] = bytes[(size_t)k];
+            rp[0][(size_t)q] = (uint8_t*)buf[0] + off[(size_t)q];
+            rb[0][(size_t)q] = bytes[(size_t)q];
+        }
+        return alltoallv(sp, sb, rp, rb);
+    }
+};
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -534,10 +688,13 @@ void free_shard_bufs(ShardCtx* s)
     f(s->d_fout); f(s->d_fcnt); f(s->d_fin); f(s->d_cout); f(s->d_ccnt); f(s->d_cin);
     f(s->d_rmesh_out); f(s->d_rfan_out); f(s->d_rflag_out); f(s->d_rmesh_in); f(s->d_rfan_in); f(s->d_rflag_in);
     f(s->d_gout); f(s->d_gsout); f(s->d_gin); f(s->d_gsin);
+    f(s->d_xre); f(s->d_pshard); f(s->d_xsub); f(s->d_xcnt); f(s->d_xsend); f(s->d_xrecv); f(s->d_xn);
     if (s->h_counts) (void)hipHostFree(s->h_counts);
+    if (s->h_xcnt) (void)hipHostFree(s->h_xcnt);
     ShardCtx fresh;
     fresh.k = s->k;
     fresh.K = s->K;
+    fresh.push = s->push;
     *s = fresh;
 }
 
@@ -894,6 +1051,81 @@ int exchange_frontier(gsim_group* g, int64_t round)
     return GSIM_OK;
 }
 
+// Copy push: round `round`'s copies from owned senders to
+// ghost receivers, appended by k_send_tm<PUSH>, go to the receivers' shards,
+// whose k_gossip_deliver applies them (AcceptFrom, the claim of the cell,
+// the records) with the round's local copies, before the commit.
+int exchange_copies(gsim_group* g, int64_t round)
+{
+    const size_t L = g->hs.size();
+    const int K = g->K;
+    const int nc = K * kXSub;
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        (void)hipSetDevice(h->device);
+        ProfScope ps(h, GSIM_K_SEND);
+        hipLaunchKernelGGL(k_xcompact, dim3((uint32_t)nc, 16), dim3(256), 0, h->stream, (const uint64_t*)s->d_xsub,
+                           (const uint32_t*)s->d_xcnt, s->xsub_cap, s->d_xsend, s->xsend_cap);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(s->h_xcnt, s->d_xcnt, sizeof(uint32_t) * (size_t)(nc + 1) * kXStride,
+                               hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess)
+            e = hipMemsetAsync(s->d_xcnt, 0, sizeof(uint32_t) * (size_t)(nc + 1) * kXStride, h->stream);
+        if (e != hipSuccess) return g->fail(GSIM_EDEVICE, "copy list compaction");
+    }
+    int rc = sync_all(g);
+    if (rc) return rc;
+    std::vector<std::vector<uint64_t>> scnt(L, std::vector<uint64_t>((size_t)K, 0)), rcnt;
+    for (size_t l = 0; l < L; ++l) {
+        const ShardCtx* s = g->hs[l]->sh;
+        if (s->h_xcnt[(size_t)nc * kXStride])
+            return g->fail(GSIM_ERANGE, "cross-shard copy list overflow (a round's copies over a sub-list's capacity)");
+        for (int d = 0; d < K; ++d)
+            for (int q = 0; q < kXSub; ++q) scnt[l][(size_t)d] += s->h_xcnt[(size_t)(d * kXSub + q) * kXStride];
+    }
+    rc = g->take_tr(g->tr->exchange_counts(scnt, rcnt));
+    if (rc) return rc;
+    std::vector<std::vector<const void*>> sp(L, std::vector<const void*>((size_t)K, nullptr));
+    std::vector<std::vector<void*>> rp(L, std::vector<void*>((size_t)K, nullptr));
+    std::vector<std::vector<uint64_t>> sb(L, std::vector<uint64_t>((size_t)K, 0)), rb = sb;
+    std::vector<int64_t> total(L, 0);
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        for (int q = 0; q < K; ++q) total[l] += (int64_t)rcnt[l][(size_t)q];
+        (void)hipSetDevice(h->device);
+        rc = g->take(h, ensure(h, &s->d_xrecv, &s->xrecv_cap, total[l]));
+        if (rc) return rc;
+        int64_t off = 0;
+        for (int q = 0; q < K; ++q) {
+            sp[l][(size_t)q] = s->d_xsend + (size_t)q * (size_t)s->xsend_cap;
+            sb[l][(size_t)q] = scnt[l][(size_t)q] * 8;
+            rp[l][(size_t)q] = s->d_xrecv + off;
+            rb[l][(size_t)q] = rcnt[l][(size_t)q] * 8;
+            off += (int64_t)rcnt[l][(size_t)q];
+        }
+    }
+    rc = g->take_tr(g->tr->alltoallv(sp, sb, rp, rb));
+    if (rc) return rc;
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        if (total[l] <= 0) continue;
+        (void)hipSetDevice(h->device);
+        ProfScope ps(h, GSIM_K_SEND);
+        uint32_t* hn = s->h_xcnt + (size_t)(nc + 1) * kXStride;
+        *hn = (uint32_t)total[l];
+        if (hipMemcpyAsync(s->d_xn, hn, sizeof(uint32_t), hipMemcpyHostToDevice, h->stream) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "received copy count");
+        rc = g->take(h, deliver_round_queue(h, round, s->d_xrecv, s->d_xn, total[l]));
+        if (rc) return rc;
+        g->settle(h);
+    }
+    return GSIM_OK;
+}
+
 // Create the group's shard handles; transport set by the caller.
 int group_create(const gsim_peer_score_params* params, const gsim_topic_score_params* topics, int32_t n_topics,
                  const gsim_thresholds* th, const gsim_gossipsub_params* gp, int32_t shards,
@@ -919,6 +1151,10 @@ int group_create(const gsim_peer_score_params* params, const gsim_topic_score_pa
         h->sh = new ShardCtx();
         h->sh->k = sd.first;
         h->sh->K = shards;
+        // GSIM_SHARD_PULL=1: the pull exchange (ghost forwarders walked by the
+        // receivers' shards; A/B and parity reference for the push)
+        const char* pl = std::getenv("GSIM_SHARD_PULL");
+        h->sh->push = !(pl && pl[0] == '1');
         g->hs.push_back(h);
         g->ids.push_back(sd.first);
     }
@@ -979,6 +1215,25 @@ int gsim_group_create_rccl(const gsim_peer_score_params* params, const gsim_topi
         *out = nullptr;
         return GSIM_EDEVICE;
     }
+    (*out)->tr.reset(t);
+    return GSIM_OK;
+}
+
+int gsim_group_create_host(const gsim_peer_score_params* params, const gsim_topic_score_params* topics,
+                           int32_t n_topics, const gsim_thresholds* thresholds, const gsim_gossipsub_params* gossip,
+                           int32_t shards, int32_t rank, int32_t device, const gsim_host_transport* transport,
+                           gsim_group** out, char* err, size_t errlen)
+{
+    if (!out || !transport || !transport->alltoallv || !transport->allreduce || shards < 1 ||
+        shards > GSIM_MAX_SHARDS || rank < 0 || rank >= shards)
+        return GSIM_EINVAL;
+    int rc = group_create(params, topics, n_topics, thresholds, gossip, shards, {{rank, device}}, out, err, errlen);
+    if (rc) return rc;
+    auto* t = new HostTransport();
+    t->h = (*out)->hs[0];
+    t->k = rank;
+    t->K = shards;
+    t->cb = *transport;
     (*out)->tr.reset(t);
     return GSIM_OK;
 }
@@ -1120,6 +1375,15 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
         if (he == hipSuccess) he = hipMemset(s->d_ymap, 0xFF, (size_t)L.e_loc * 4);
         if (he == hipSuccess) he = hipMemset(s->d_pgate, 0, (size_t)L.e_loc);
         if (he != hipSuccess) return g->fail(GSIM_EDEVICE, "shard tables upload");
+        // copy push: each local peer's shard; the cross edges' indices at the
+        // receivers' shards follow once every shard's ghost blocks are known
+        std::vector<uint8_t> psh((size_t)L.n_loc, 0);
+        for (int q = 0; q < K; ++q)
+            for (int64_t x = L.lpeer[(size_t)q]; x < L.lpeer[(size_t)q + 1]; ++x) psh[(size_t)x] = (uint8_t)q;
+        if ((rc = dalloc(h, &s->d_pshard, psh.size())) || (rc = dalloc(h, &s->d_xre, (size_t)L.e_loc)))
+            return g->take(h, rc);
+        if (hipMemcpy(s->d_pshard, psh.data(), psh.size(), hipMemcpyHostToDevice) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "shard tables upload");
         g->gid[l] = L.gid;
         g->gidx[l] = L.gidx;
     }
@@ -1133,6 +1397,27 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
     }
     int rc = exchange_dense(g, xo, ym, 4);
     if (rc) return rc;
+    // copy push: shard d's ghost block of this shard's peers starts at its
+    // local edge gbase_d[this] (one count exchange)
+    {
+        const size_t Ls = g->hs.size();
+        std::vector<std::vector<uint64_t>> sc(Ls, std::vector<uint64_t>((size_t)K, 0)), rcv;
+        for (size_t l = 0; l < Ls; ++l)
+            for (int q = 0; q < K; ++q) sc[l][(size_t)q] = (uint64_t)g->hs[l]->sh->gbase[(size_t)q];
+        rc = g->take_tr(g->tr->exchange_counts(sc, rcv));
+        if (rc) return rc;
+        for (size_t l = 0; l < Ls; ++l) {
+            gsim_handle* h = g->hs[l];
+            ShardCtx* s = h->sh;
+            s->rbase.assign((size_t)K, 0);
+            EdgeBases rb{};
+            for (int q = 0; q < K; ++q) rb.b[q] = s->rbase[(size_t)q] = (int64_t)rcv[l][(size_t)q];
+            (void)hipSetDevice(h->device);
+            hipLaunchKernelGGL(k_xre_build, dim3(grid_for(h->e)), dim3(256), 0, h->stream, (const uint32_t*)s->d_xq,
+                               (const uint32_t*)h->d_col, (const uint8_t*)s->d_pshard, rb, s->d_xre, h->e);
+            if (hipGetLastError() != hipSuccess) return g->fail(GSIM_EDEVICE, "k_xre_build");
+        }
+    }
     return sync_all(g);
 }
 
@@ -1171,6 +1456,24 @@ int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg)
             A(&s->d_gsout, (size_t)ncross);
             A(&s->d_gin, (size_t)h->e);
             A(&s->d_gsin, (size_t)h->e);
+        }
+        if (!rc && s->push && !s->d_xsub) {
+            // a round's copies to each other shard: sub-lists of half the cross
+            // edges into it each (32 x 1/2 = 16 copies per cross edge in all,
+            // several times a C3 round's; an overflow fails the round)
+            int64_t xmax = 0;
+            for (int q = 0; q < K; ++q) xmax = std::max<int64_t>(xmax, s->xoff[(size_t)q + 1] - s->xoff[(size_t)q]);
+            s->xsub_cap = std::max<int64_t>(xmax / 2, 1 << 12);
+            s->xsend_cap = kXSub * s->xsub_cap;
+            const size_t nct = (size_t)(K * kXSub + 2) * kXStride;
+            A(&s->d_xsub, (size_t)(K * s->xsend_cap));
+            A(&s->d_xsend, (size_t)(K * s->xsend_cap));
+            A(&s->d_xcnt, nct);
+            A(&s->d_xn, 1);
+            if (!rc && hipHostMalloc((void**)&s->h_xcnt, sizeof(uint32_t) * nct, 0) != hipSuccess)
+                return g->fail(GSIM_ENOMEM, "pinned scratch");
+            if (!rc && hipMemset(s->d_xcnt, 0, sizeof(uint32_t) * nct) != hipSuccess)
+                return g->fail(GSIM_EDEVICE, "copy list counts");
         }
         if (rc) return g->take(h, rc);
         if (hipMemset(s->d_gin, 0, (size_t)h->e * 8) != hipSuccess || hipMemset(s->d_gsin, 0, (size_t)h->e) != hipSuccess)
@@ -1326,7 +1629,16 @@ int gsim_group_round(gsim_group* g, int64_t round)
     for (gsim_handle* h : g->hs) {
         (void)hipSetDevice(h->device);
         rc = deliver_round_send(h, round);
-        if (!rc) rc = deliver_round_post(h, round);
+        if (rc) return g->take(h, rc);
+        g->settle(h);
+    }
+    if (g->hs.empty() || g->hs[0]->sh->push) {
+        rc = exchange_copies(g, round);              // copies to other shards' peers
+        if (rc) return rc;
+    }
+    for (gsim_handle* h : g->hs) {
+        (void)hipSetDevice(h->device);
+        rc = deliver_round_post(h, round);
         if (!rc) rc = deliver_round_control(h, round);
         if (rc) return g->take(h, rc);
         g->settle(h);
@@ -1383,7 +1695,7 @@ static int group_sum(gsim_group* g, int (*fn)(gsim_handle*, int64_t*), int n, in
         if (rc && !first_err) { first_err = rc; g->err = "shard: " + h->err; }
         for (int i = 0; i < n; ++i) acc[(size_t)i] += v[(size_t)i];
     }
-    if (dynamic_cast<RcclTransport*>(g->tr.get())) {
+    if (g->hs.size() < (size_t)g->K) {                  // one shard per process: sum over the ranks
         int64_t* d = nullptr;
         if (hipMalloc((void**)&d, sizeof(int64_t) * (n + 1)) != hipSuccess) return g->fail(GSIM_ENOMEM, "totals scratch");
         acc.push_back(first_err ? 1 : 0);

@@ -133,6 +133,16 @@ KERNEL_CLASSES = ["refresh_score", "score", "ip_colocation", "heartbeat", "contr
                   "commit", "accept", "gossip", "churn"]
 BEHAVE_IGNORE_IWANT = 0x01
 
+# gsim_host_transport callbacks (include/gsim.h)
+HOST_A2A = ctypes.CFUNCTYPE(c_int32, c_void_p, POINTER(c_uint8), POINTER(c_uint64), POINTER(c_uint64),
+                            POINTER(c_uint8), POINTER(c_uint64), POINTER(c_uint64))
+HOST_ALLREDUCE = ctypes.CFUNCTYPE(c_int32, c_void_p, c_void_p, c_int64, c_int32, c_int32)
+
+
+class CHostTransport(Structure):
+    _fields_ = [("ctx", c_void_p), ("alltoallv", HOST_A2A), ("allreduce", HOST_ALLREDUCE)]
+
+
 class CShardInfo(Structure):
     _fields_ = [("shard", c_int32), ("shards", c_int32), ("n_local", c_int64), ("e_local", c_int64),
                 ("own_lo", c_int64), ("own_hi", c_int64), ("own_e_lo", c_int64), ("own_e_hi", c_int64),
@@ -265,6 +275,10 @@ SIGNATURES = [
     ("gsim_group_create_rccl", c_int32,
      [POINTER(CPeerScoreParams), POINTER(CTopicScoreParams), c_int32, POINTER(CThresholds),
       POINTER(CGossipSubParams), c_int32, c_int32, c_int32, c_void_p, POINTER(c_void_p), c_char_p, c_size_t]),
+    ("gsim_group_create_host", c_int32,
+     [POINTER(CPeerScoreParams), POINTER(CTopicScoreParams), c_int32, POINTER(CThresholds),
+      POINTER(CGossipSubParams), c_int32, c_int32, c_int32, POINTER(CHostTransport), POINTER(c_void_p), c_char_p,
+      c_size_t]),
     ("gsim_group_destroy", c_int32, [c_void_p]),
     ("gsim_group_last_error", c_char_p, [c_void_p]),
     ("gsim_group_shard", c_void_p, [c_void_p, c_int32]),

@@ -128,6 +128,57 @@ def plan(net: Network, shards: int, bounds: Optional[np.ndarray] = None) -> List
     return [ShardPlan.build(net, b, s) for s in range(len(b) - 1)]
 
 
+class HostCollectives:
+    """gsim_host_transport over a torch.distributed process group (gloo on
+    host tensors): the exchanges of a one-shard-per-process group staged
+    through host memory (gsim_group_create_host).  Keep the object alive as
+    long as the group."""
+
+    _DT = {0: np.uint32, 1: np.int32, 2: np.uint64}
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self._a2a = _abi.HOST_A2A(self._alltoallv)
+        self._ar = _abi.HOST_ALLREDUCE(self._allreduce)
+        self.c = _abi.CHostTransport(None, self._a2a, self._ar)
+        self.error = None
+
+    def _alltoallv(self, ctx, send, sbytes, sdisp, recv, rbytes, rdisp):
+        import torch
+        try:
+            K = self.world
+            sb = [int(sbytes[i]) for i in range(K)]
+            rb = [int(rbytes[i]) for i in range(K)]
+            st, rt = sum(sb), sum(rb)
+            s_np = np.ctypeslib.as_array(send, shape=(st,)).copy() if st else np.zeros(0, np.uint8)
+            r_t = torch.empty(rt, dtype=torch.uint8)
+            self.dist.all_to_all_single(r_t, torch.from_numpy(s_np), rb, sb, group=self.group)
+            if rt:
+                ctypes.memmove(recv, r_t.numpy().ctypes.data, rt)
+            return 0
+        except Exception as ex:                 # reported by the group call's error
+            self.error = ex
+            return 1
+
+    def _allreduce(self, ctx, buf, count, dtype, op):
+        import torch
+        try:
+            dt = self._DT[int(dtype)]
+            a = np.ctypeslib.as_array(ctypes.cast(buf, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dt))),
+                                      shape=(int(count),))
+            t = torch.from_numpy(a.astype(np.int64))
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM if op == 0 else self.dist.ReduceOp.MAX,
+                                 group=self.group)
+            a[...] = t.numpy().astype(dt)
+            return 0
+        except Exception as ex:
+            self.error = ex
+            return 1
+
+
 class ShardedEngine:
     """One simulated network split over shards (gsim_group_*): the Engine API
     with global peer / edge indexing.  In-process (``shards`` handles in this
@@ -135,7 +186,7 @@ class ShardedEngine:
     (``rccl=(rank, unique_id, device)``, one process per GPU)."""
 
     def __init__(self, params, thresholds, gossip=None, topics=None, shards: int = 2, devices=None,
-                 rccl=None):
+                 rccl=None, host=None):
         """Parameters are validated like WithPeerScore (gossipsub.go:278-319)
         by every shard's gsim_create."""
         from .engine import Engine
@@ -151,7 +202,14 @@ class ShardedEngine:
         self._tarr = params.topic_array(self.topics)
         g = ctypes.c_void_p()
         buf = ctypes.create_string_buffer(512)
-        if rccl is None:
+        if host is not None:
+            rank, coll, device = host          # (rank, HostCollectives, device)
+            self._coll = coll
+            rc = self.lib.gsim_group_create_host(ctypes.byref(pc), self._tarr, len(self.topics), ctypes.byref(tc),
+                                                 ctypes.byref(gc), shards, rank, device, ctypes.byref(coll.c),
+                                                 ctypes.byref(g), buf, len(buf))
+            self.local = [rank]
+        elif rccl is None:
             dev = None if devices is None else (ctypes.c_int32 * shards)(*devices)
             rc = self.lib.gsim_group_create(ctypes.byref(pc), self._tarr, len(self.topics), ctypes.byref(tc),
                                             ctypes.byref(gc), shards, dev, ctypes.byref(g), buf, len(buf))
@@ -388,13 +446,15 @@ class ShardedEngine:
             raise GsimError(rc, (self.lib.gsim_last_error(h) or b"").decode())
         return out
 
-    def read(self, f: int) -> np.ndarray:
+    def read(self, f: int, into: Optional[np.ndarray] = None) -> np.ndarray:
         """A field of the whole network, assembled from the owned parts of
-        every shard (every shard must be in this process)."""
+        every shard (every shard must be in this process).  into: an array
+        of the whole network's shape whose parts owned by this process's
+        shards are overwritten (any subset of the shards; returned)."""
         from .engine import _FIELD_DTYPES
-        if len(self.local) != self.shards:
+        if into is None and len(self.local) != self.shards:
             raise GsimError(_abi.GSIM_EINVAL, "the whole network's view needs every shard in this process")
-        out = np.zeros(self._shape(f, self.net.n, self.net.e), dtype=_FIELD_DTYPES[f])
+        out = np.zeros(self._shape(f, self.net.n, self.net.e), dtype=_FIELD_DTYPES[f]) if into is None else into
         for p in self.plans:
             loc = self.read_local(p.shard, f)
             if f in self._PEER_LAST:

@@ -671,6 +671,26 @@ int gsim_group_create_rccl(const gsim_peer_score_params* params, const gsim_topi
                            int32_t n_topics, const gsim_thresholds* thresholds, const gsim_gossipsub_params* gossip,
                            int32_t shards, int32_t rank, int32_t device, const void* unique_id, gsim_group** out,
                            char* err, size_t errlen);
+/* One shard of a multi-process job whose exchanges go through the caller's
+ * own collectives over host memory (device -> pinned host -> callback ->
+ * device): the one-shard-per-process code path of gsim_group_create_rccl
+ * without RCCL (tests on one GPU with gloo; hosts without xGMI).  Callbacks
+ * return 0 on success and are called by every rank in the same order.
+ *   alltoallv: send[sdisp[d] .. + sbytes[d]) to rank d; recv[rdisp[s] .. +
+ *              rbytes[s]) from rank s (sizes agreed beforehand; the rank's own
+ *              entries are 0);
+ *   allreduce: elementwise over `count` values of every rank, in place;
+ *              dtype 0 = u32, 1 = i32, 2 = u64; op 0 = sum, 1 = max. */
+typedef struct gsim_host_transport {
+    void* ctx;
+    int (*alltoallv)(void* ctx, const uint8_t* send, const uint64_t* sbytes, const uint64_t* sdisp, uint8_t* recv,
+                     const uint64_t* rbytes, const uint64_t* rdisp);
+    int (*allreduce)(void* ctx, void* buf, int64_t count, int32_t dtype, int32_t op);
+} gsim_host_transport;
+int gsim_group_create_host(const gsim_peer_score_params* params, const gsim_topic_score_params* topics,
+                           int32_t n_topics, const gsim_thresholds* thresholds, const gsim_gossipsub_params* gossip,
+                           int32_t shards, int32_t rank, int32_t device, const gsim_host_transport* transport,
+                           gsim_group** out, char* err, size_t errlen);
 int gsim_group_destroy(gsim_group* g);
 const char* gsim_group_last_error(const gsim_group* g);
 /* The handle of a shard hosted by this process (NULL otherwise): its state is

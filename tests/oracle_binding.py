@@ -273,12 +273,16 @@ class NetState:
         eng.write(_abi.F_FANOUT_TOPICS, self.fan_topics)
         eng.set_direct_peers(self.direct)
 
-    def pull_from_engine(self, eng):
+    def pull_from_engine(self, eng, base=None):
+        """The engine's state; base: a NetState whose values stand for the
+        parts no shard of this process owns (a one-shard-per-process group)."""
+        def rd(fid, name):
+            return eng.read(fid) if base is None else eng.read(fid, into=getattr(base, name).copy())
         for f in self.TOPIC_FIELDS + self.EDGE_FIELDS:
-            getattr(self, f)[...] = eng.read(self.FIELD_IDS[f])
-        self.ctl[...] = eng.read(_abi.F_CTL)
-        self.lastpub[...] = eng.read(_abi.F_LASTPUB)
-        self.fan_topics[...] = eng.read(_abi.F_FANOUT_TOPICS)
+            getattr(self, f)[...] = rd(self.FIELD_IDS[f], f)
+        self.ctl[...] = rd(_abi.F_CTL, "ctl")
+        self.lastpub[...] = rd(_abi.F_LASTPUB, "lastpub")
+        self.fan_topics[...] = rd(_abi.F_FANOUT_TOPICS, "fan_topics")
 
 
 UNSEEN = 0xFFFFFFFF

@@ -120,18 +120,25 @@ def _rank_main(rank, world, port, q):
         gid = p.gid.astype(np.int64)
         loc = Network(p.n_local, p.row_ptr, p.col, np.zeros(p.e_local, np.uint8), np.zeros(p.n_local, np.uint64))
         own = loc.owner()
-        # 1. message copies over every cross edge: (cross-out index q, sender gid, receiver gid)
+        # 1. copy push (shard.hip exchange_copies): each shard learns where its
+        # ghost block starts at every other shard (gsim_group_load_graph's count
+        # exchange), then sends a copy over every cross edge as the edge's index
+        # at the receiver's shard (xre = rbase[d] + cross-out position), with
+        # (sender gid, receiver gid) to check it against
+        rbase = _exchange(dist, torch, [np.array([p.ghost_base[d] if d != rank else 0]) for d in range(world)],
+                          world)
         sends = []
         for d in range(world):
             xo = p.cross_out[d] if d != rank else np.zeros(0, np.uint32)
-            sends.append(np.stack([np.arange(len(xo)), gid[own[xo]], gid[p.col[xo]]], 1).ravel())
+            xre = (int(rbase[d][0]) if d != rank else 0) + np.arange(len(xo))
+            sends.append(np.stack([xre, gid[own[xo]], gid[p.col[xo]]], 1).ravel())
         got = _exchange(dist, torch, sends, world)
         n_copies = 0
         for s in range(world):
             if s == rank:
                 continue
             e = got[s].reshape(-1, 3)
-            r = p.ghost_base[s] + e[:, 0]                  # the receiver's record of the sender
+            r = e[:, 0]                                    # the receiver's record of the sender
             assert (gid[own[r]] == e[:, 1]).all() and (gid[p.col[r]] == e[:, 2]).all()
             assert ((p.col[r] >= p.own_lo) & (p.col[r] < p.own_hi)).all(), "lands on an owned receiver"
             n_copies += len(e)

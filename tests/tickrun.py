@@ -65,7 +65,7 @@ def oracle_trace(ev, msgs, lo, hi):
 
 def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, churn=None, after_tick=None,
                eng=None, after_heartbeat=None, px_log=None, trace=None, trace_log=None, topic_slots=0, gater=None,
-               gater_log=None, subs=None):
+               gater_log=None, subs=None, local_only=False):
     """Run `ticks` on a fresh engine loaded with `st`'s state and on the
     oracle; assert identical state, seen-set and totals after every tick.
     churn: {tick: [(pairs, up), ...]} applied just before the tick.
@@ -81,7 +81,9 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
     gsim.PeerGaterParams turned on at both sides (WithPeerGater); its state
     and the copies it dropped must agree after every tick (the per-tick drop
     counts appended to gater_log).  subs: {tick: [(pairs, join), ...]} Join /
-    Leave of (peer, topic) pairs applied just before the tick, after churn."""
+    Leave of (peer, topic) pairs applied just before the tick, after churn.
+    local_only: `eng` holds only some shards of the network (one shard per
+    process): the parts they own are compared, the totals in full."""
     from gsim.engine import Engine
     pushed = eng is None
     if eng is None:
@@ -133,10 +135,12 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
                 msgs.round(st, g)
                 eng.round(g)
             assert eng.msg_stats() == msgs.stats, f"totals differ at tick {kk}: {eng.msg_stats()} vs {msgs.stats}"
-            assert np.array_equal(eng.read(_abi.F_SEEN), msgs.seen), f"seen-set differs at tick {kk}"
-            assert np.array_equal(eng.read(_abi.F_LASTPUT), msgs.lastput), f"mcache puts differ at tick {kk}"
+            seen = eng.read(_abi.F_SEEN, into=msgs.seen.copy()) if local_only else eng.read(_abi.F_SEEN)
+            lput = eng.read(_abi.F_LASTPUT, into=msgs.lastput.copy()) if local_only else eng.read(_abi.F_LASTPUT)
+            assert np.array_equal(seen, msgs.seen), f"seen-set differs at tick {kk}"
+            assert np.array_equal(lput, msgs.lastput), f"mcache puts differ at tick {kk}"
             gpu = ob.NetState(net, params, thresholds=th, gossip=gp)
-            gpu.pull_from_engine(eng)
+            gpu.pull_from_engine(eng, base=st if local_only else None)
             assert_same(st, gpu)
             if trace is not None:
                 got, want = eng.trace_read(), oracle_trace(msgs.events(), msgs, trace[0], trace[1])
