@@ -1851,37 +1851,35 @@ __global__ __launch_bounds__(256) void k_promise_insert(uint64_t* pcand, uint32_
     }
 }
 
-// Round 2: the messages queued by handleIWant arrive.  Same tracer rules as
-// k_send's copies; a record can receive several responses in one launch, so
-// counters are updated atomically.
+// One pending meshMessageDeliveries increment of record ir: a byte add on
+// the containing word; the add that makes kMcntSpill pending moves them to
+// meshd.  Increments are x -> min(x + 1, cap) one after the other until the
+// next refresh applies the rest, so how they are grouped into spills does not
+// change the result; fewer than 256 - kMcntSpill copies of one record arrive
+// in one launch, so the byte never carries into its neighbour.
+constexpr uint32_t kMcntSpill = 128;
 __device__ __forceinline__ void atomic_mcnt_inc(uint8_t* mcnt, int64_t ir, double* meshd, double cap)
 {
     uint32_t* w = reinterpret_cast<uint32_t*>(mcnt + (ir & ~(int64_t)3));
     const int sh = (int)(ir & 3) * 8;
-    uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t old = atomicAdd(w, 1u << sh);
+    if (((old >> sh) & 0xFFu) != kMcntSpill - 1u) return;
+    atomicSub(w, kMcntSpill << sh);
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(meshd);
+    unsigned long long o = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {
-        const uint32_t byte = (old >> sh) & 0xFFu;
-        const uint32_t nb = byte == 255u ? 1u : byte + 1u;
-        const uint32_t nw = (old & ~(0xFFu << sh)) | (nb << sh);
-        const uint32_t prev = atomicCAS(w, old, nw);
-        if (prev == old) {
-            if (byte == 255u) {                      // spill the full count
-                unsigned long long* q = reinterpret_cast<unsigned long long*>(meshd);
-                unsigned long long o = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                for (;;) {
-                    const double x = apply_incs(__longlong_as_double((long long)o), 255u, cap);
-                    const unsigned long long nx = (unsigned long long)__double_as_longlong(x);
-                    const unsigned long long pv = atomicCAS(q, o, nx);
-                    if (pv == o) break;
-                    o = pv;
-                }
-            }
-            return;
-        }
-        old = prev;
+        const double x = apply_incs(__longlong_as_double((long long)o), kMcntSpill, cap);
+        const unsigned long long nx = (unsigned long long)__double_as_longlong(x);
+        const unsigned long long pv = atomicCAS(q, o, nx);
+        if (pv == o) break;
+        o = pv;
     }
 }
 
+// Copies that arrive as a list of (record, slot): round 2's messages queued by
+// handleIWant, and a shard's copies pushed by other shards (shard.hip).  Same
+// rules and tracer events as k_send_tm's copies; a record can receive several
+// copies in one launch, so counters are updated atomically.
 __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint64_t* resp, const uint32_t* nresp,
                                                        const uint32_t* owner, int64_t resp_cap)
 {

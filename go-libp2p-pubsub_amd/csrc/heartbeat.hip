@@ -2048,7 +2048,8 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.lastpub = h->x->d_lastpub; a.fan_topics = h->x->d_fantopics;
     a.pub_thr = h->th.publish_threshold; a.fanout_ttl = h->gp.fanout_ttl_ns;
     a.gid = h->sh ? h->sh->d_gid : nullptr;
-    if (ShardCtx* sh = h->sh; sh && sh->d_rdel) {
+    // (push: no shard reads a ghost row's router state)
+    if (ShardCtx* sh = h->sh; sh && sh->d_rdel && !sh->push) {
         a.rdel = sh->d_rdel;
         a.rdel_n = sh->d_rdel_n;
         a.rdel_cap = sh->rdel_cap;

@@ -1614,7 +1614,10 @@ int gsim_group_round(gsim_group* g, int64_t round)
     if (!g) return GSIM_EINVAL;
     if (!g->msgs) return g->fail(GSIM_ESTATE, "gsim_group_msgs_init not called");
     int rc = GSIM_OK;
-    if (g->router_dirty) {                           // the ghosts' forwarding state of this round
+    const bool push = g->hs.empty() || g->hs[0]->sh->push;
+    // pull: the ghosts' forwarding state of this round (push: the senders'
+    // shards decide, nothing reads a ghost row's router state)
+    if (g->router_dirty && !push) {
         rc = exchange_router(g);
         if (rc) return rc;
     }
@@ -1632,7 +1635,7 @@ int gsim_group_round(gsim_group* g, int64_t round)
         if (rc) return g->take(h, rc);
         g->settle(h);
     }
-    if (g->hs.empty() || g->hs[0]->sh->push) {
+    if (push) {
         rc = exchange_copies(g, round);              // copies to other shards' peers
         if (rc) return rc;
     }
@@ -1646,7 +1649,7 @@ int gsim_group_round(gsim_group* g, int64_t round)
     const int64_t r = round % g->rounds;
     if (r < 2) {
         rc = exchange_control(g, (int)((r + 1) & 1));   // PRUNE replies for the next control round
-        if (!rc) rc = exchange_router_delta(g);         // the meshes control changed, on cross edges
+        if (!rc && !push) rc = exchange_router_delta(g);   // the meshes control changed, on cross edges
         if (rc) return rc;
     }
     for (gsim_handle* h : g->hs) {

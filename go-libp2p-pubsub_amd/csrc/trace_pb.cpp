@@ -186,3 +186,247 @@ extern "C" int gsim_trace_encode(const gsim_trace_event* ev, int64_t n, const gs
     }
     return GSIM_OK;
 }
+
+// ---- SendRPC / RecvRPC / DropRPC (trace.go:250-324) ----------------------
+// The RPCMeta of an encoded RPC as traceRPCMeta builds it (trace.go:326-414):
+// messages -> MessageMeta{messageID = from || seqno (DefaultMsgIdFn),
+// topic}; subscriptions -> SubMeta{subscribe, topic}; control (present
+// whenever the RPC has one) -> ControlMeta{ihave{topic, messageIDs},
+// iwant{messageIDs}, graft{topic}, prune{topic, peers = PeerInfo.peerID}}.
+// Optional fields are copied when present in the RPC, as the Go pointers
+// are; repeated bytes elements always (an absent peerID is an empty one).
+namespace {
+
+struct Rd {
+    const uint8_t* p;
+    const uint8_t* e;
+    bool ok = true;
+    bool more() const { return ok && p < e; }
+    uint64_t varint()
+    {
+        uint64_t v = 0;
+        for (int s = 0; s < 64 && p < e; s += 7) {
+            const uint8_t b = *p++;
+            v |= (uint64_t)(b & 0x7F) << s;
+            if (!(b & 0x80)) return v;
+        }
+        ok = false;
+        return 0;
+    }
+    // the next field: number, wire type; length-delimited payload in (q, n)
+    bool field(int* f, int* wt, const uint8_t** q, uint64_t* n, uint64_t* v)
+    {
+        const uint64_t k = varint();
+        if (!ok) return false;
+        *f = (int)(k >> 3);
+        *wt = (int)(k & 7);
+        *q = nullptr; *n = 0; *v = 0;
+        switch (*wt) {
+        case 0: *v = varint(); break;
+        case 1: if (e - p < 8) ok = false; else p += 8; break;
+        case 5: if (e - p < 4) ok = false; else p += 4; break;
+        case 2: {
+            const uint64_t L = varint();
+            if (!ok || (uint64_t)(e - p) < L) { ok = false; break; }
+            *q = p; *n = L; p += L;
+            break;
+        }
+        default: ok = false;
+        }
+        return ok;
+    }
+};
+
+struct Pw {
+    std::string s;
+    void varint(uint64_t v)
+    {
+        while (v >= 0x80) { s.push_back((char)(v | 0x80)); v >>= 7; }
+        s.push_back((char)v);
+    }
+    void tag(int f, int wt) { varint((uint64_t)((f << 3) | wt)); }
+    void bytes(int f, const void* q, uint64_t n)
+    {
+        tag(f, 2);
+        varint(n);
+        s.append((const char*)q, (size_t)n);
+    }
+    void sub(int f, const std::string& body) { bytes(f, body.data(), body.size()); }
+    void u64(int f, uint64_t v) { tag(f, 0); varint(v); }
+};
+
+// copy the length-delimited fields `from` -> `to` of a message (optional
+// ones present / repeated ones in order), everything else dropped
+bool remap(const uint8_t* q, uint64_t n, const int* from, const int* to, int k, Pw* w)
+{
+    Rd r{q, q + n};
+    int f, wt;
+    const uint8_t* b;
+    uint64_t L, v;
+    // fields in ascending output order: one pass per output field
+    for (int x = 0; x < k; ++x) {
+        r = Rd{q, q + n};
+        while (r.more()) {
+            if (!r.field(&f, &wt, &b, &L, &v)) return false;
+            if (f == from[x] && wt == 2) w->bytes(to[x], b, L);
+        }
+    }
+    return r.ok;
+}
+
+bool rpc_meta(const uint8_t* q, uint64_t n, Pw* meta)
+{
+    Rd r{q, q + n};
+    int f, wt;
+    const uint8_t* b;
+    uint64_t L, v;
+    // messages (RPC.publish = 2) -> RPCMeta.messages = 1
+    while (r.more()) {
+        if (!r.field(&f, &wt, &b, &L, &v)) return false;
+        if (f != 2 || wt != 2) continue;
+        Rd m{b, b + L};
+        std::string from, seqno;
+        const uint8_t* tp = nullptr;
+        uint64_t tn = 0;
+        bool has_topic = false;
+        int mf, mwt;
+        const uint8_t* mb;
+        uint64_t ml, mv;
+        while (m.more()) {
+            if (!m.field(&mf, &mwt, &mb, &ml, &mv)) return false;
+            if (mwt != 2) continue;
+            if (mf == 1) from.assign((const char*)mb, ml);
+            else if (mf == 3) seqno.assign((const char*)mb, ml);
+            else if (mf == 4) { tp = mb; tn = ml; has_topic = true; }
+        }
+        Pw mm;
+        const std::string id = from + seqno;
+        mm.bytes(1, id.data(), id.size());
+        if (has_topic) mm.bytes(2, tp, tn);
+        meta->sub(1, mm.s);
+    }
+    if (!r.ok) return false;
+    // subscriptions (1) -> subscription = 2: SubOpts{subscribe = 1, topicid = 2}
+    r = Rd{q, q + n};
+    while (r.more()) {
+        if (!r.field(&f, &wt, &b, &L, &v)) return false;
+        if (f != 1 || wt != 2) continue;
+        Rd m{b, b + L};
+        Pw sm;
+        bool has_sub = false, subv = false, has_topic = false;
+        const uint8_t* tp = nullptr;
+        uint64_t tn = 0;
+        int mf, mwt;
+        const uint8_t* mb;
+        uint64_t ml, mv;
+        while (m.more()) {
+            if (!m.field(&mf, &mwt, &mb, &ml, &mv)) return false;
+            if (mf == 1 && mwt == 0) { has_sub = true; subv = mv != 0; }
+            else if (mf == 2 && mwt == 2) { has_topic = true; tp = mb; tn = ml; }
+        }
+        if (has_sub) sm.u64(1, subv ? 1 : 0);
+        if (has_topic) sm.bytes(2, tp, tn);
+        meta->sub(2, sm.s);
+    }
+    if (!r.ok) return false;
+    // control (3) -> control = 3 (the last one, as proto2 merges; one in practice)
+    r = Rd{q, q + n};
+    bool has_ctl = false;
+    Pw cm;
+    while (r.more()) {
+        if (!r.field(&f, &wt, &b, &L, &v)) return false;
+        if (f != 3 || wt != 2) continue;
+        has_ctl = true;
+        cm.s.clear();
+        static const int ih_from[] = {1, 2}, ih_to[] = {1, 2};     // ControlIHave{topicID, messageIDs}
+        static const int iw_from[] = {1}, iw_to[] = {1};            // ControlIWant{messageIDs}
+        static const int gr_from[] = {1}, gr_to[] = {1};            // ControlGraft{topicID}
+        for (int kind = 1; kind <= 4; ++kind) {
+            Rd c{b, b + L};
+            int cf, cwt;
+            const uint8_t* cb;
+            uint64_t cl, cv;
+            while (c.more()) {
+                if (!c.field(&cf, &cwt, &cb, &cl, &cv)) return false;
+                if (cf != kind || cwt != 2) continue;
+                Pw x;
+                bool ok = true;
+                if (kind == 1) ok = remap(cb, cl, ih_from, ih_to, 2, &x);
+                else if (kind == 2) ok = remap(cb, cl, iw_from, iw_to, 1, &x);
+                else if (kind == 3) ok = remap(cb, cl, gr_from, gr_to, 1, &x);
+                else {
+                    // ControlPrune{topicID = 1, peers = 2 (PeerInfo{peerID = 1})}
+                    ok = remap(cb, cl, gr_from, gr_to, 1, &x);
+                    Rd pr{cb, cb + cl};
+                    int pf, pwt;
+                    const uint8_t* pb;
+                    uint64_t pl, pv;
+                    while (ok && pr.more()) {
+                        if (!pr.field(&pf, &pwt, &pb, &pl, &pv)) return false;
+                        if (pf != 2 || pwt != 2) continue;
+                        Rd pi{pb, pb + pl};
+                        const uint8_t* id = nullptr;
+                        uint64_t idn = 0;
+                        int qf, qwt;
+                        const uint8_t* qb;
+                        uint64_t ql, qv;
+                        while (pi.more()) {
+                            if (!pi.field(&qf, &qwt, &qb, &ql, &qv)) return false;
+                            if (qf == 1 && qwt == 2) { id = qb; idn = ql; }
+                        }
+                        x.bytes(2, id, idn);
+                    }
+                }
+                if (!ok) return false;
+                cm.sub(kind, x.s);
+            }
+            if (!c.ok) return false;
+        }
+    }
+    if (!r.ok) return false;
+    if (has_ctl) meta->sub(3, cm.s);
+    return true;
+}
+
+}  // namespace
+
+extern "C" int gsim_trace_rpc_encode(const uint8_t* rpcs, const gsim_wire_ref* refs, int64_t n,
+                                     const gsim_wire_names* names, int64_t timestamp_ns, int32_t which, uint8_t* out,
+                                     uint64_t cap, uint64_t* len)
+{
+    if (!len || n < 0 || (n > 0 && (!rpcs || !refs || !names)) || (which & ~7) || !which) return GSIM_EINVAL;
+    if (names && names->peer_id_len && !names->peer_ids) return GSIM_EINVAL;
+    auto pid = [&](uint32_t p) -> std::string {
+        if (names->peer_id_len)
+            return std::string((const char*)names->peer_ids + (size_t)p * names->peer_id_len, names->peer_id_len);
+        const char b[4] = {(char)(p >> 24), (char)(p >> 16), (char)(p >> 8), (char)p};
+        return std::string(b, 4);
+    };
+    Pw batch;
+    for (int64_t k = 0; k < n; ++k) {
+        const gsim_wire_ref& r = refs[k];
+        Pw meta;
+        if (!rpc_meta(rpcs + r.offset, r.len, &meta)) return GSIM_EINVAL;
+        // SEND_RPC = 7 (sendRPC = 11), RECV_RPC = 6 (recvRPC = 10), DROP_RPC = 8 (dropRPC = 12)
+        static const int kType[3] = {7, 6, 8}, kField[3] = {11, 10, 12};
+        for (int q = 0; q < 3; ++q) {
+            if (!((which >> q) & 1)) continue;
+            const bool recv = q == 1;
+            Pw body;
+            const std::string other = pid(recv ? r.from : r.to);   // receivedFrom / sendTo
+            body.bytes(1, other.data(), other.size());
+            body.sub(2, meta.s);
+            Pw ev;
+            ev.u64(1, (uint64_t)kType[q]);
+            const std::string me = pid(recv ? r.to : r.from);
+            ev.bytes(2, me.data(), me.size());
+            ev.u64(3, (uint64_t)timestamp_ns);
+            ev.sub(kField[q], body.s);
+            batch.sub(1, ev.s);
+        }
+    }
+    *len = batch.s.size();
+    if (batch.s.size() > cap || (!batch.s.empty() && !out)) return GSIM_ERANGE;
+    if (!batch.s.empty()) std::memcpy(out, batch.s.data(), batch.s.size());
+    return GSIM_OK;
+}

@@ -313,6 +313,8 @@ SIGNATURES = [
                                     POINTER(c_uint64)]),
     ("gsim_wire_fragment", c_int32, [POINTER(CWireRpc), c_int64, c_void_p, c_uint64, POINTER(c_uint64), c_void_p,
                                      c_int32, POINTER(c_int32)]),
+    ("gsim_trace_rpc_encode", c_int32, [c_void_p, c_void_p, c_int64, POINTER(CWireNames), c_int64, c_int32, c_void_p,
+                                        c_uint64, POINTER(c_uint64)]),
     ("gsim_wire_heartbeat", c_int32, [c_void_p, c_int64, c_uint32, c_uint32, POINTER(CWireNames), c_void_p, c_uint64,
                                       c_void_p, c_int64, POINTER(c_int64), POINTER(c_uint64)]),
 ]

@@ -274,3 +274,43 @@ def trace_batch(records: np.ndarray, topic_names, peer_ids: Optional[np.ndarray]
     if rc != 0:
         raise WireError(rc, "gsim_trace_encode")
     return out.raw[:n.value]
+
+
+def trace_rpc_batch(rpcs, topic_names=(), peer_ids: Optional[np.ndarray] = None, timestamp: int = 0,
+                    which: int = 3) -> bytes:
+    """TraceEventBatch of the SendRPC (which bit 0) / RecvRPC (bit 1) /
+    DropRPC (bit 2) events of encoded RPCs [(from, to, bytes)], e.g.
+    heartbeat_rpcs' output (gsim_trace_rpc_encode)."""
+    lib = _abi.load()
+    raw = b"".join(r[2] for r in rpcs)
+    refs = np.zeros(len(rpcs), dtype=_abi.WIRE_REF_DTYPE)
+    off = 0
+    for k, (frm, to, b) in enumerate(rpcs):
+        refs[k]["from"], refs[k]["to"], refs[k]["len"], refs[k]["offset"] = frm, to, len(b), off
+        off += len(b)
+    names = [_b(x) for x in topic_names]
+    tn = (_abi.CBytes * max(1, len(names)))()
+    keep = []
+    for k, x in enumerate(names):
+        buf = ctypes.create_string_buffer(x, max(1, len(x)))
+        keep.append(buf)
+        tn[k] = _abi.CBytes(ctypes.addressof(buf), len(x))
+    nm = _abi.CWireNames()
+    nm.topic_names = ctypes.addressof(tn)
+    if peer_ids is not None:
+        pid = np.ascontiguousarray(peer_ids, dtype=np.uint8)
+        keep.append(pid)
+        nm.peer_ids = pid.ctypes.data
+        nm.peer_id_len = pid.shape[1]
+    rb = ctypes.create_string_buffer(raw, max(1, len(raw)))
+    n = ctypes.c_uint64()
+    rp = refs.ctypes.data if len(refs) else None
+    rc = lib.gsim_trace_rpc_encode(rb, rp, len(refs), ctypes.byref(nm), timestamp, which, None, 0, ctypes.byref(n))
+    if rc not in (0, _abi.GSIM_ERANGE):
+        raise WireError(rc, "gsim_trace_rpc_encode")
+    out = ctypes.create_string_buffer(max(1, n.value))
+    rc = lib.gsim_trace_rpc_encode(rb, rp, len(refs), ctypes.byref(nm), timestamp, which, out, n.value,
+                                   ctypes.byref(n))
+    if rc != 0:
+        raise WireError(rc, "gsim_trace_rpc_encode")
+    return out.raw[:n.value]

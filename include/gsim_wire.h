@@ -175,6 +175,21 @@ int gsim_wire_heartbeat(gsim_handle* h, int64_t tick, uint32_t p0, uint32_t p1, 
 int gsim_trace_encode(const gsim_trace_event* ev, int64_t n, const gsim_wire_names* names, const char* proto,
                       uint8_t* out, uint64_t cap, uint64_t* len);
 
+/* The RPC-level trace events (pubsubTracer.SendRPC / RecvRPC / DropRPC,
+ * trace.go:250-324) of n encoded RPCs — e.g. gsim_wire_heartbeat's output
+ * copied to host, with its refs (from, to, offset, len into rpcs).  Per RPC,
+ * in ref order, one TraceEvent per bit of `which`: bit 0 SEND_RPC at the
+ * sender (sendTo = receiver), bit 1 RECV_RPC at the receiver (receivedFrom =
+ * sender), bit 2 DROP_RPC at the sender (the caller decides which RPCs a full
+ * queue dropped: the engine models no outbound queue), each with the RPC's
+ * RPCMeta as traceRPCMeta builds it (trace.go:326-414: message ids from ||
+ * seqno, topics, subscriptions, IHAVE / IWANT ids, GRAFT / PRUNE topics and
+ * PX peer ids) and timestamp_ns.  Peer ids as gsim_trace_encode.  Written as
+ * a TraceEventBatch; *len the bytes (GSIM_ERANGE with *len = the size needed
+ * when cap is short; GSIM_EINVAL for a malformed RPC). */
+int gsim_trace_rpc_encode(const uint8_t* rpcs, const gsim_wire_ref* refs, int64_t n, const gsim_wire_names* names,
+                          int64_t timestamp_ns, int32_t which, uint8_t* out, uint64_t cap, uint64_t* len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -73,8 +73,9 @@ def trace_pb():
     """{name: class} for TraceEvent and TraceEventBatch, from a descriptor
     restating pb/trace.proto:5-150 for the events the engine produces
     (PublishMessage, RejectMessage, DuplicateMessage, DeliverMessage,
-    AddPeer, RemovePeer, Join, Leave, Graft, Prune; field names, numbers, types as
-    there).  Serialized by the protobuf runtime."""
+    AddPeer, RemovePeer, RecvRPC, SendRPC, DropRPC with their RPCMeta, Join,
+    Leave, Graft, Prune; field names, numbers, types as there).  Serialized by
+    the protobuf runtime."""
     global _TRACE
     if _TRACE is not None:
         return _TRACE
@@ -96,6 +97,9 @@ def trace_pb():
                                             ("deliverMessage", 7, OPT, M, T + "DeliverMessage"),
                                             ("addPeer", 8, OPT, M, T + "AddPeer"),
                                             ("removePeer", 9, OPT, M, T + "RemovePeer"),
+                                            ("recvRPC", 10, OPT, M, T + "RecvRPC"),
+                                            ("sendRPC", 11, OPT, M, T + "SendRPC"),
+                                            ("dropRPC", 12, OPT, M, T + "DropRPC"),
                                             ("join", 13, OPT, M, T + "Join"), ("leave", 14, OPT, M, T + "Leave"),
                                             ("graft", 15, OPT, M, T + "Graft"), ("prune", 16, OPT, M, T + "Prune")]:
         f = ev.field.add(name=fname, number=num, label=label, type=typ)
@@ -104,8 +108,27 @@ def trace_pb():
 
     def sub(name, fields):
         m = ev.nested_type.add(name=name)
-        for (fname, num, typ) in fields:
-            m.field.add(name=fname, number=num, label=OPT, type=typ)
+        for fd in fields:
+            fname, num, typ = fd[:3]
+            f = m.field.add(name=fname, number=num, label=fd[3] if len(fd) > 3 else OPT, type=typ)
+            if len(fd) > 4:
+                f.type_name = T + fd[4]
+
+    BOOL = F.TYPE_BOOL
+    # RPCMeta and its parts (pb/trace.proto:107-146); RecvRPC / SendRPC / DropRPC (76-89)
+    sub("MessageMeta", [("messageID", 1, B), ("topic", 2, S)])
+    sub("SubMeta", [("subscribe", 1, BOOL), ("topic", 2, S)])
+    sub("ControlIHaveMeta", [("topic", 1, S), ("messageIDs", 2, B, REP)])
+    sub("ControlIWantMeta", [("messageIDs", 1, B, REP)])
+    sub("ControlGraftMeta", [("topic", 1, S)])
+    sub("ControlPruneMeta", [("topic", 1, S), ("peers", 2, B, REP)])
+    sub("ControlMeta", [("ihave", 1, M, REP, "ControlIHaveMeta"), ("iwant", 2, M, REP, "ControlIWantMeta"),
+                        ("graft", 3, M, REP, "ControlGraftMeta"), ("prune", 4, M, REP, "ControlPruneMeta")])
+    sub("RPCMeta", [("messages", 1, M, REP, "MessageMeta"), ("subscription", 2, M, REP, "SubMeta"),
+                    ("control", 3, M, OPT, "ControlMeta")])
+    sub("RecvRPC", [("receivedFrom", 1, B), ("meta", 2, M, OPT, "RPCMeta")])
+    sub("SendRPC", [("sendTo", 1, B), ("meta", 2, M, OPT, "RPCMeta")])
+    sub("DropRPC", [("sendTo", 1, B), ("meta", 2, M, OPT, "RPCMeta")])
 
     sub("PublishMessage", [("messageID", 1, B), ("topic", 2, S)])
     sub("RejectMessage", [("messageID", 1, B), ("receivedFrom", 2, B), ("reason", 3, S), ("topic", 4, S)])
@@ -195,3 +218,70 @@ def fragment_rpc(rpc, limit):
             x = C["ControlIHave"](messageIDs=ids)  # the topic id is not carried over
             out_rpc(x.ByteSize(), True).control.ihave.add().CopyFrom(x)
     return rpcs
+
+
+def trace_rpc_meta(rpc, meta):
+    """traceRPCMeta (trace.go:326-414) restated: fill the TraceEvent.RPCMeta
+    `meta` from a decoded RPC (pb() classes).  Message ids are
+    DefaultMsgIdFn's from || seqno (pubsub.go); optional fields are copied when
+    present (Go copies the pointers); the control meta exists whenever the RPC
+    has a control message; a PRUNE's peers are its PeerInfo ids (an absent id
+    is an empty one)."""
+    for m in rpc.publish:
+        mm = meta.messages.add()
+        mm.messageID = getattr(m, "from") + m.seqno
+        if m.HasField("topic"):
+            mm.topic = m.topic.decode("utf-8", "surrogateescape")
+    for sub in rpc.subscriptions:
+        sm = meta.subscription.add()
+        if sub.HasField("subscribe"):
+            sm.subscribe = sub.subscribe
+        if sub.HasField("topicid"):
+            sm.topic = sub.topicid.decode("utf-8", "surrogateescape")
+    if rpc.HasField("control"):
+        c = meta.control
+        c.SetInParent()
+        for ih in rpc.control.ihave:
+            x = c.ihave.add()
+            if ih.HasField("topicID"):
+                x.topic = ih.topicID.decode("utf-8", "surrogateescape")
+            x.messageIDs.extend(ih.messageIDs)
+        for iw in rpc.control.iwant:
+            c.iwant.add().messageIDs.extend(iw.messageIDs)
+        for g in rpc.control.graft:
+            x = c.graft.add()
+            if g.HasField("topicID"):
+                x.topic = g.topicID.decode("utf-8", "surrogateescape")
+        for p in rpc.control.prune:
+            x = c.prune.add()
+            if p.HasField("topicID"):
+                x.topic = p.topicID.decode("utf-8", "surrogateescape")
+            x.peers.extend([pi.peerID for pi in p.peers])
+
+
+def trace_rpc_events(rpcs, peer_id, timestamp, which):
+    """The TraceEventBatch pubsubTracer's SendRPC / RecvRPC / DropRPC
+    (trace.go:250-324) would write for encoded RPCs [(from, to, bytes)]: per
+    RPC, SEND_RPC at the sender (bit 0 of which), RECV_RPC at the receiver
+    (bit 1), DROP_RPC at the sender (bit 2)."""
+    P, T = pb(), trace_pb()
+    batch = T["TraceEventBatch"]()
+    for (frm, to, raw) in rpcs:
+        rpc = P["RPC"]()
+        rpc.ParseFromString(raw)
+        for bit, (typ, field, me, other) in enumerate([(7, "sendRPC", frm, to), (6, "recvRPC", to, frm),
+                                                       (8, "dropRPC", frm, to)]):
+            if not (which >> bit) & 1:
+                continue
+            ev = batch.batch.add()
+            ev.type = typ
+            ev.peerID = peer_id(me)
+            ev.timestamp = timestamp
+            body = getattr(ev, field)
+            if field == "recvRPC":
+                body.receivedFrom = peer_id(other)
+            else:
+                body.sendTo = peer_id(other)
+            trace_rpc_meta(rpc, body.meta)
+            body.meta.SetInParent()
+    return batch.SerializeToString()

@@ -184,6 +184,79 @@ def test_trace_bit_exact(require_gpu, lo, hi):
         assert total[typ] > 0, f"event type {typ} traced"
 
 
+def _random_rpc(rng, P):
+    """An RPC with every part traceRPCMeta reads, optional fields present or
+    absent at random (pb() classes)."""
+    rpc = P["RPC"]()
+    for _ in range(rng.integers(0, 3)):
+        s = rpc.subscriptions.add()
+        if rng.random() < 0.7:
+            s.subscribe = bool(rng.integers(0, 2))
+        if rng.random() < 0.8:
+            s.topicid = f"t{rng.integers(0, 9)}".encode()
+    for _ in range(rng.integers(0, 3)):
+        m = rpc.publish.add()
+        setattr(m, "from", bytes(rng.integers(0, 256, size=6, dtype=np.uint8)))
+        m.seqno = int(rng.integers(0, 2**63)).to_bytes(8, "big")
+        m.data = b"x" * int(rng.integers(0, 5))
+        if rng.random() < 0.8:
+            m.topic = f"topic-{rng.integers(0, 5)}".encode()
+    if rng.random() < 0.85:
+        c = rpc.control
+        c.SetInParent()
+        for _ in range(rng.integers(0, 3)):
+            ih = c.ihave.add()
+            if rng.random() < 0.8:
+                ih.topicID = b"ih" + bytes([97 + int(rng.integers(0, 5))])
+            ih.messageIDs.extend(bytes(rng.integers(0, 256, size=10, dtype=np.uint8))
+                                 for _ in range(rng.integers(0, 4)))
+        for _ in range(rng.integers(0, 2)):
+            c.iwant.add().messageIDs.extend(bytes(rng.integers(0, 256, size=7, dtype=np.uint8))
+                                            for _ in range(rng.integers(0, 3)))
+        for _ in range(rng.integers(0, 3)):
+            g = c.graft.add()
+            if rng.random() < 0.8:
+                g.topicID = b"gr"
+        for _ in range(rng.integers(0, 3)):
+            pr = c.prune.add()
+            if rng.random() < 0.8:
+                pr.topicID = b"pr"
+            pr.backoff = int(rng.integers(0, 100))
+            for _ in range(rng.integers(0, 3)):
+                pi = pr.peers.add()
+                if rng.random() < 0.8:
+                    pi.peerID = bytes(rng.integers(0, 256, size=5, dtype=np.uint8))
+                if rng.random() < 0.3:
+                    pi.signedPeerRecord = b"rec"
+    return rpc
+
+
+@pytest.mark.parametrize("with_ids,which", [(False, 3), (True, 7), (True, 1)])
+def test_rpc_trace_events_match_trace_rpc_meta(with_ids, which):
+    """gsim_trace_rpc_encode against traceRPCMeta restated on the protobuf
+    runtime (oracle/wire_oracle.py): SendRPC / RecvRPC / DropRPC events of
+    RPCs with subscriptions, published messages, IHAVE / IWANT / GRAFT / PRUNE
+    (with and without PX peers and optional fields), and empty control."""
+    rng = np.random.default_rng(31 + which)
+    P = wo.pb()
+    N = 50
+    peer_ids = rng.integers(0, 256, size=(N, 38), dtype=np.uint8) if with_ids else None
+    rpcs = []
+    for _ in range(60):
+        a, b = (int(x) for x in rng.integers(0, N, size=2))
+        rpcs.append((a, b, _random_rpc(rng, P).SerializeToString()))
+    pid = (lambda p: bytes(peer_ids[p])) if with_ids else (lambda p: int(p).to_bytes(4, "big"))
+    ts = 1_700_000_000_123_456_789
+    got = wire.trace_rpc_batch(rpcs, peer_ids=peer_ids, timestamp=ts, which=which)
+    assert got == wo.trace_rpc_events(rpcs, pid, ts, which)
+    T = wo.trace_pb()
+    batch = T["TraceEventBatch"]()
+    batch.ParseFromString(got)
+    assert len(batch.batch) == len(rpcs) * bin(which).count("1")
+    with pytest.raises(wire.WireError):
+        wire.trace_rpc_batch([(0, 1, b"\x0a\x05ab")], which=1)        # truncated field
+
+
 def test_trace_encode_rejects_unknown_types_and_short_buffers():
     import ctypes
     names = [b"t0"]

@@ -305,6 +305,10 @@ def test_heartbeat_rpcs_match_oracle(require_gpu, with_peer_ids):
             for g_, w_ in zip(got, want):
                 assert g_ == w_, f"tick {kk}: RPC {g_[0]}->{g_[1]} differs"
             state["checked"] += len(got)
+            # their SendRPC / RecvRPC trace events (trace.go:250-324, traceRPCMeta 326-414)
+            pid = (lambda p: bytes(peer_ids[p])) if peer_ids is not None else (lambda p: int(p).to_bytes(4, "big"))
+            assert wire.trace_rpc_batch(got, names, peer_ids=peer_ids, timestamp=tick_time(kk), which=3) == \
+                wo.trace_rpc_events(want, pid, tick_time(kk), 3), f"tick {kk}: RPC trace events differ"
         for p in range(n):                  # the heartbeat ends with mcache.Shift
             lib.orc_mcache_shift(mc[p])
 
