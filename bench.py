@@ -343,7 +343,8 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-full", action="store_true",
-                    help="time only the C oracle on the config's full network (no GPU): one tick per leg "
+                    help="time only the C oracle on the config's full network (no GPU): one tick per leg after "
+                         "GSIM_CPU_WARMUP (1) warm-up ticks; GSIM_CPU_LEGS=all,single "
                          "(DESIGN.md §7); prints one JSON line")
     ap.add_argument("--msg-rate", type=float, default=None, help="messages per second per topic (config default)")
     ap.add_argument("--ring", type=int, default=None, help="message ring slots (config default)")
@@ -359,7 +360,8 @@ def main():
         cfg = CONFIGS[args.config]
         scen = dict(SCENARIOS.get(args.config, {}))
         legs = tuple(os.environ.get("GSIM_CPU_LEGS", "all,single").split(","))
-        out = cpu_baseline(cfg, scen, n=cfg[0], ticks=1, budget_s=0.0, warmup=0, legs=legs)
+        out = cpu_baseline(cfg, scen, n=cfg[0], ticks=1, budget_s=0.0,
+                           warmup=int(os.environ.get("GSIM_CPU_WARMUP", "1")), legs=legs)
         out["config"] = args.config
         print(json.dumps(out), flush=True)
         return

@@ -591,11 +591,12 @@ __device__ __forceinline__ uint32_t kth_bit(uint64_t m, uint32_t k)
 // peer; only edges to the receivers [rlo, rhi) (a shard's owned peers).
 __global__ __launch_bounds__(256) void k_mesh_mask(const uint32_t* row_ptr, const uint32_t* col, const uint8_t* mflags,
                                                    const uint8_t* direct, const uint64_t* smask, int64_t n, int64_t E,
-                                                   int32_t T, uint32_t rlo, uint32_t rhi, uint64_t* mmask)
+                                                   int32_t T, uint32_t rlo, uint32_t rhi, uint64_t* mmask,
+                                                   int64_t row_lo, int64_t row_hi)
 {
-    // one wave per row, lane = row position: coalesced flag planes, one ballot per topic
+    // one wave per row of [row_lo, row_hi), lane = row position: coalesced flag planes, one ballot per topic
     const int lane = threadIdx.x & 63;
-    for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += (int64_t)gridDim.x * 4) {
+    for (int64_t r = row_lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < row_hi; r += (int64_t)gridDim.x * 4) {
         const uint32_t b = row_ptr[r], d = row_ptr[r + 1] - b;
         const bool v = d <= 64 && (uint32_t)lane < d;
         const uint32_t e = b + (uint32_t)lane;
@@ -698,6 +699,7 @@ constexpr int kTsSlots = 64;
 #ifndef GSIM_TM_TB
 #define GSIM_TM_TB 1024      // threads per k_send_tm block
 #endif
+constexpr int kPushTB = 512;         // ... of a shard's push walk (its owned range: twice the blocks)
 constexpr uint32_t kTmWin = 8192;   // flattened edges whose senders are tabled in LDS at once
 constexpr int kTmTabMin = 256;      // forwarders in a chunk from which the table pays for its fill
 
@@ -1918,12 +1920,24 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
         const bool sc = tp->scored && (ds & GSIM_DS_TRACKED) && slot_has(mi, t);
         const uint8_t tf = a.tflags[ir];
         const int64_t window = tp->mesh_message_deliveries_window_ns;
+        const uint32_t L = a.mlat ? a.mlat[m] : 0u;
+        // committed before this round and the cell's round cannot matter (as
+        // k_send_tm's known copies): a duplicate, credited without the cell
+        if (!L && ((a.seenbm[(int64_t)m * a.nw + (p >> 6)] >> (p & 63)) & 1ull)) {
+            const bool wa = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
+            if (wa || !sc || inv || !(tf & GSIM_TF_IN_MESH)) {
+                if (!sc) continue;
+                if (pen) atomicAdd(&a.invalid[ir], 1.0);
+                else if (!inv && (tf & GSIM_TF_IN_MESH))         // wa: within the window
+                    atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], tp->mesh_message_deliveries_cap);
+                continue;
+            }
+        }
         const int64_t pci = a.cs.idx(m, t, p);      // p wanted it: a member of t
         if (pci < 0) continue;
         uint64_t* cellp = a.cs.cell + pci;
         const uint64_t c = *cellp;
         const uint32_t hi = (uint32_t)(c >> 32);
-        const uint32_t L = a.mlat ? a.mlat[m] : 0u;
         int64_t seen_round = -1;               // completion round (k_send_tm)
         if (c != kUnseen64) {
             if (!(hi & kClaim)) seen_round = hi;
@@ -2246,7 +2260,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
             a.xK = sh->K;
             a.xre = sh->d_xre; a.pshard = sh->d_pshard;
             a.xsub = sh->d_xsub; a.xcnt = sh->d_xcnt; a.xsub_cap = sh->xsub_cap;
-            a.slo = (sh->own_lo / (2 * GSIM_TM_TB)) * (2 * GSIM_TM_TB);
+            a.slo = (sh->own_lo / (2 * kPushTB)) * (2 * kPushTB);   // whole chunks of the push walk
             a.shi = sh->own_hi;
         } else {
             a.sptr = sh->d_sptr;
@@ -2574,8 +2588,9 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
     // budgets 4096 / 8192 / 15680 (default) / 32768 / 65536: 29.7 / 25.0 / 24.7 /
     // 28.0 / 32.9 ms of send per tick (profiles/r02_ab_send_blocks.log)
     constexpr int TB = GSIM_TM_TB;
-    constexpr int64_t total = 2048 * (1024 / TB);
-    constexpr int64_t chunk = 2 * TB;
+    const int TBv = a0.push ? kPushTB : TB;
+    const int64_t total = 2048 * (1024 / TBv);
+    const int64_t chunk = 2 * TBv;
     // every local peer sends (pull: a shard's ghosts too), or the owned range (push)
     const int64_t cn = a0.shi - a0.slo;
     const int T = std::max(1, h->t);
@@ -2600,7 +2615,7 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
             // ranges of at most kMaxRange peers: a quiet topic's block still scans
             // its range chunk by chunk, and one block over all N peers would
             // set the launch's length
-            constexpr int64_t kMaxRange = 64 * chunk;
+            const int64_t kMaxRange = 64 * chunk;
             b = std::max<int64_t>(std::max<int64_t>(1, (cn + kMaxRange - 1) / kMaxRange), std::min(b, max_blocks));
             const int64_t range = ((cn + b - 1) / b + chunk - 1) / chunk * chunk;
             d->tmtab[t] = start;
@@ -2617,9 +2632,11 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
     // the slot list in LDS
     const size_t lds = ((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7;
     if (a.push && sparse_layout(h))
-        hipLaunchKernelGGL((k_send_tm<TB, false, true, false, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<kPushTB, false, true, false, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
+                           h->stream, a);
     else if (a.push)
-        hipLaunchKernelGGL((k_send_tm<TB, false, false, false, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<kPushTB, false, false, false, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
+                           h->stream, a);
     else if (a.mlat)
         hipLaunchKernelGGL((k_send_tm<TB, true, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
     else if (a.gt.act && sparse_layout(h))
@@ -2716,7 +2733,8 @@ int deliver_round_send(gsim_handle* h, int64_t round)
                                h->stream, (const uint32_t*)h->d_row_ptr, (const uint32_t*)h->d_col,
                                (const uint8_t*)h->d_mflags, (const uint8_t*)h->d_direct,
                                (const uint64_t*)h->d_smask, h->n, h->e,
-                               std::max(1, h->t), mlo, mhi, d->d_mmask);
+                               std::max(1, h->t), mlo, mhi, d->d_mmask,
+                               a.push ? h->olo() : (int64_t)0, a.push ? h->ohi() : h->n);   // push: owned senders only
             d->mask_version = h->mesh_version;
             d->hub_round = -1;
         }

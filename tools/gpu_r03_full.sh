@@ -17,6 +17,6 @@ echo "default bench wall: $((SECONDS - t0)) s"
 python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('c3', round(d['ms_per_step'],2), 'frac', round(d['roofline']['frac'],4), 'cpu', d['cpu_baseline']['value'])" "$OUT/bench_default.json"
 export TMPDIR=/tmp
 ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c3" -o s -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_c3.log" 2>&1 ) || { tail -20 "$OUT/prof_c3.log"; exit 1; }
-python3 "$ROOT/tools/trace_summary.py" "$OUT/prof_c3/s_kernel_trace.csv" 1 5 > "$OUT/prof_c3_summary.txt"; head -12 "$OUT/prof_c3_summary.txt"
+python3 "$ROOT/tools/trace_summary.py" "$OUT/prof_c3/s_kernel_trace.csv" 1 6 > "$OUT/prof_c3_summary.txt"; head -12 "$OUT/prof_c3_summary.txt"
 timeout -k 10 500 python -u bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/bench_c5.json" 2> "$OUT/bench_c5.err" || { tail -20 "$OUT/bench_c5.err"; exit 1; }
 python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('c5', round(d['ms_per_step'],2), {k: round(v,1) for k,v in d['kernel_ms_per_tick'].items() if v > 1})" "$OUT/bench_c5.json"
