@@ -504,6 +504,17 @@ def main():
                       "frac": deliv_gbs / HBM_PEAK_GBS, "traffic": tr_send_tick, "traffic_detail": tr_send,
                       "kernel": "delivery: k_send_tm + k_commit + k_delivery_state (per tick, 10 rounds)", "kernel_ms": deliv_ms,
                       "algorithmic_bytes_per_tick": alg_deliv}
+        # the delivery walk's actual bound: TCC requests per second (PMC, per launch of k_send_tm)
+        # against the random-access probe's ceiling
+        rq = None if args.vdelay or sharded else load_traffic(args.config + ":send_req")
+        if rq is not None and launches.get("send"):
+            send_launch_ms = kms["send"] * K / launches["send"]
+            ach = rq["requests_per_launch"] / (send_launch_ms * 1e-3)
+            roof_deliv["request_rate"] = {"bound": "tcc_requests", "achieved": ach, "peak": rq["ceiling_req_per_s"],
+                                          "unit": "requests/s", "frac": ach / rq["ceiling_req_per_s"],
+                                          "requests_per_launch": rq["requests_per_launch"],
+                                          "kernel": rq["kernel"], "kernel_ms_per_launch": send_launch_ms,
+                                          "source": rq["source"], "ceiling_source": rq["ceiling_source"]}
         dominant = roof_refresh if ref_ms * launches["refresh_score"] / K >= deliv_ms else roof_deliv
         out = {
             "metric": "peer-heartbeat updates/sec + msg-edge deliveries/sec, 1M-peer gossipsub sim",
