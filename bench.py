@@ -420,7 +420,7 @@ def main():
     kk = 0
     for _ in range(args.warmup):
         kk += 1
-        run_tick(eng, kk, sched, churn, px=bool(scen.get("px")) and shard is None)
+        run_tick(eng, kk, sched, churn, px=bool(scen.get("px")))
     eng.synchronize()
     census0 = eng.census()
     stats0 = eng.msg_stats()
@@ -440,7 +440,7 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         kk += 1
-        run_tick(eng, kk, sched, churn, px=bool(scen.get("px")) and shard is None)
+        run_tick(eng, kk, sched, churn, px=bool(scen.get("px")))
     eng.synchronize()
     barrier()
     wall = time.perf_counter() - t0

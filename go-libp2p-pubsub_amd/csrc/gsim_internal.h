@@ -227,6 +227,12 @@ struct ShardCtx {
     int64_t xrecv_cap = 0;
     uint32_t* d_xn = nullptr;              // [1] copies received
     uint32_t* h_xcnt = nullptr;            // pinned: count readback ([K * kXSub + 1] strided), then the received count
+    // peer exchange to ghosts (k_px_emit's remote path, gsim_group_px_connect)
+    uint64_t* d_pxout = nullptr;           // [K][pxcap] PX list entries per destination shard
+    uint32_t* d_pxcnt = nullptr;           // [K + 1] their counts, overflow
+    int64_t pxcap = 0;
+    uint64_t* d_pxin = nullptr;            // entries from the other shards / the job's attempts / its connections
+    int64_t pxin_cap = 0;
 };
 constexpr int kXSub = 32;                  // outbound sub-lists per destination (append contention)
 constexpr int kXStride = 32;               // u32s between two sub-list counters (one cache line each)
@@ -509,6 +515,12 @@ uint64_t gsim_get_seed(const gsim_handle* h);              // heartbeat.hip
 int deliver_read_seen(gsim_handle* h, void* dst);
 int deliver_check_errors(gsim_handle* h);             // queue overflow / early slot reuse of the last tick
 int handle_control(gsim_handle* h, int32_t round, int64_t now);   // heartbeat.hip: k_handle_control
+// heartbeat.hip, a shard's peer exchange (gsim_group_px_connect): remote PX lists in,
+// its connection attempts out (global asker | peer << 32), gs.outbound of the connections
+bool px_enabled(const gsim_handle* h);
+int px_import(gsim_handle* h, const uint64_t* d_in, int64_t n);
+int px_asks(gsim_handle* h, uint64_t* d_out, uint32_t* d_cnt, int64_t cap);
+int px_mark_outbound(gsim_handle* h, const uint64_t* d_pairs, int64_t n);
 // trace.hip: resolve the recorded message copies (seen-set cells, slot tables)
 struct TraceView {
     gsim::Cells cells;

@@ -104,6 +104,15 @@ struct HbArgs {
     int32_t do_px, prune_peers;
     double accept_px;
     uint64_t* pxo;             // [N] topics in which the observer sent a PRUNE with PX
+    // sharded: a PRUNE with PX to a ghost goes to the ghost's shard, one entry per
+    // listed peer (the cross edge's index there | topic << 32 | listed peer's
+    // global id << 38) in per-destination lists [K][pxcap] (pxcnt[K]: overflow)
+    uint64_t* pxout;
+    uint32_t* pxcnt;
+    int64_t pxcap;
+    int32_t pxK;
+    const uint32_t* xre;       // ShardCtx::d_xre
+    const uint8_t* pshard;
     uint8_t* pxm;              // [E] the row's owner tries to connect to col[e]
     uint8_t* nopx;             // [E] a GRAFT of this sender turned PX off for its RPC
     double* pxs;               // [E] the observer's live score of col[e] after its heartbeat (PX observers)
@@ -1430,7 +1439,9 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a, int live, uint32_
                 for (uint64_t pm = __ballot(pr); pm; pm &= pm - 1) {
                     const int pos = p0 + __ffsll((long long)pm) - 1;
                     const uint32_t ep = b + (uint32_t)pos, p = a.col[ep];
-                    if (a.score[ep] < a.accept_px) continue;       // p's snapshot score of obs (record order)
+                    // a ghost p: its shard holds its score of obs and its row (below)
+                    const bool remote = a.pxout && (p < a.olo || p >= a.ohi);
+                    if (!remote && a.score[ep] < a.accept_px) continue;   // p's snapshot score of obs (record order)
                     const uint32_t kt = (uint32_t)t + 64u * (uint32_t)(pos + 1);
                     uint32_t n = 0;
                     for (int q0 = 0; q0 < deg; q0 += 64) {
@@ -1477,6 +1488,26 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a, int live, uint32_
                             tau = mn + 1;
                             ++c;
                         }
+                    }
+                    if (remote) {
+                        // the PX list to p's shard, which makes handlePrune's checks (k_px_import)
+                        const uint32_t d = a.pshard[p];
+                        const uint64_t hdr = (uint64_t)a.xre[ep] | ((uint64_t)t << 32);
+                        for (int q0 = 0; q0 < deg; q0 += 64) {
+                            const int q = q0 + lane;
+                            const bool in = q < deg && key[q] < tau;
+                            const uint64_t bm = __ballot(in);
+                            uint32_t base = 0;
+                            if (lane == 0 && bm) base = atomicAdd(&a.pxcnt[d], (uint32_t)__popcll(bm));
+                            base = (uint32_t)__shfl((int)base, 0, 64);
+                            if (!in) continue;
+                            const uint32_t k = base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+                            const uint64_t gx = glob(a, a.col[b + (uint32_t)q]);
+                            if ((int64_t)k < a.pxcap) a.pxout[(int64_t)d * a.pxcap + k] = hdr | (gx << 38);
+                            else atomicOr(&a.pxcnt[a.pxK], 1u);
+                        }
+                        wave_lds_sync();
+                        continue;
                     }
                     const uint32_t pb = a.row_ptr[p], pe = a.row_ptr[p + 1];
                     for (int q0 = 0; q0 < deg; q0 += 64) {
@@ -1536,6 +1567,102 @@ __global__ __launch_bounds__(256) void k_px_outbound(const uint32_t* pxc, uint32
     if (k >= n) return;
     outbound[pxc[1 + 2 * k]] = 1;          // gs.outbound: the dialer's side (gossipsub.go:532-551)
     outbound[pxc[2 + 2 * k]] = 0;
+}
+
+// A shard's end of a remote pruner's PX lists (entries of k_px_emit's remote
+// path): handlePrune's acceptPXThreshold on the pruned peer's snapshot score
+// of the pruner (its record at the cross edge's index r here), then
+// pxConnect's attempt to every listed peer with a known address (an edge of
+// the pruned peer's row) it is not connected to.
+__global__ __launch_bounds__(256) void k_px_import(const uint64_t* in, int64_t n, const double* score,
+                                                   const uint32_t* col, const uint32_t* row_ptr, const uint8_t* rstate,
+                                                   const uint32_t* g2l, double accept_px, uint8_t* pxm)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+        const uint64_t v = in[k];
+        const uint32_t r = (uint32_t)v;
+        if (score[r] < accept_px) continue;
+        const uint32_t p = col[r], x = g2l[(uint32_t)(v >> 38)];
+        if (x == 0xFFFFFFFFu) continue;                      // not a neighbour of p
+        uint32_t lo = row_ptr[p], hi = row_ptr[p + 1];
+        const uint32_t pe = hi;
+        while (lo < hi) {
+            const uint32_t mid = lo + ((hi - lo) >> 1);
+            if (col[mid] < x) lo = mid + 1; else hi = mid;
+        }
+        if (lo < pe && col[lo] == x && !(rstate[lo] & GSIM_ES_CONNECTED)) pxm[lo] = 1;
+    }
+}
+
+// A shard's connection attempts: every marked owned-row edge (p asked for x),
+// as global (asker | peer << 32); the marks are cleared.
+__global__ __launch_bounds__(256) void k_px_asks(const uint32_t* owner, const uint32_t* col, const uint8_t* rstate,
+                                                 const uint32_t* gid, uint8_t* pxm, int64_t e_lo, int64_t e_hi,
+                                                 uint64_t* out, uint32_t* cnt, int64_t cap)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = e_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < e_hi; e += stride) {
+        if (!pxm[e]) continue;
+        pxm[e] = 0;
+        if (rstate[e] & GSIM_ES_CONNECTED) continue;
+        const uint32_t k = atomicAdd(cnt, 1u);
+        if ((int64_t)k < cap) out[k] = (uint64_t)gid[owner[e]] | ((uint64_t)gid[col[e]] << 32);
+    }
+}
+
+// The connector's (dialer | peer << 32) global pairs: gs.outbound on this
+// shard's owned ends (the dialer's side outbound, the peer's not).
+__global__ __launch_bounds__(256) void k_px_outbound_pairs(const uint64_t* pairs, int64_t n, const uint32_t* g2l,
+                                                           const uint32_t* row_ptr, const uint32_t* col, uint32_t olo,
+                                                           uint32_t ohi, uint8_t* outbound)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < 2 * n; k += stride) {
+        const uint64_t v = pairs[k >> 1];
+        const bool dial = !(k & 1);
+        const uint32_t a_ = g2l[dial ? (uint32_t)v : (uint32_t)(v >> 32)], b_ = g2l[dial ? (uint32_t)(v >> 32) : (uint32_t)v];
+        if (a_ == 0xFFFFFFFFu || b_ == 0xFFFFFFFFu || a_ < olo || a_ >= ohi) continue;
+        uint32_t lo = row_ptr[a_], hi = row_ptr[a_ + 1];
+        const uint32_t pe = hi;
+        while (lo < hi) {
+            const uint32_t mid = lo + ((hi - lo) >> 1);
+            if (col[mid] < b_) lo = mid + 1; else hi = mid;
+        }
+        if (lo < pe && col[lo] == b_) outbound[lo] = dial ? 1 : 0;
+    }
+}
+
+bool px_enabled(const gsim_handle* h) { return h->x && h->x->d_pxo; }
+
+int px_import(gsim_handle* h, const uint64_t* d_in, int64_t n)
+{
+    if (n <= 0 || !h->x || !h->x->d_pxm) return GSIM_OK;
+    hipLaunchKernelGGL(k_px_import, dim3((uint32_t)std::min<int64_t>((n + 255) / 256, 16384)), dim3(256), 0, h->stream,
+                       d_in, n, (const double*)h->d_score, (const uint32_t*)h->d_col, (const uint32_t*)h->d_row_ptr,
+                       (const uint8_t*)h->d_rstate, (const uint32_t*)h->sh->d_g2l, h->th.accept_px_threshold,
+                       h->x->d_pxm);
+    return hip_check(h, hipGetLastError(), "k_px_import");
+}
+
+int px_asks(gsim_handle* h, uint64_t* d_out, uint32_t* d_cnt, int64_t cap)
+{
+    hipError_t e = hipMemsetAsync(d_cnt, 0, sizeof(uint32_t), h->stream);
+    if (e != hipSuccess || !h->x || !h->x->d_pxm) return hip_check(h, e, "px asks");
+    const int64_t lo = h->sh->own_e_lo, hi = h->sh->own_e_hi;
+    hipLaunchKernelGGL(k_px_asks, dim3((uint32_t)std::min<int64_t>((hi - lo + 255) / 256 + 1, 16384)), dim3(256), 0,
+                       h->stream, (const uint32_t*)h->d_owner, (const uint32_t*)h->d_col, (const uint8_t*)h->d_rstate,
+                       (const uint32_t*)h->sh->d_gid, h->x->d_pxm, lo, hi, d_out, d_cnt, cap);
+    return hip_check(h, hipGetLastError(), "k_px_asks");
+}
+
+int px_mark_outbound(gsim_handle* h, const uint64_t* d_pairs, int64_t n)
+{
+    if (n <= 0) return GSIM_OK;
+    hipLaunchKernelGGL(k_px_outbound_pairs, dim3((uint32_t)std::min<int64_t>((2 * n + 255) / 256, 16384)), dim3(256),
+                       0, h->stream, d_pairs, n, (const uint32_t*)h->sh->d_g2l, (const uint32_t*)h->d_row_ptr,
+                       (const uint32_t*)h->d_col, (uint32_t)h->olo(), (uint32_t)h->ohi(), h->d_outbound);
+    return hip_check(h, hipGetLastError(), "k_px_outbound_pairs");
 }
 
 // inspectScoresExtended (score.go:472-500) for the connections e of
@@ -1950,7 +2077,7 @@ int alloc_extra(gsim_handle* h)
         h->bytes_allocated += sizeof(uint32_t) * all.size();
     }
     h->max_degree = mdall;   // every local row (a shard's ghost rows too)
-    if (h->gp.do_px && !h->sh) {
+    if (h->gp.do_px) {
         const size_t pb = sizeof(uint64_t) * (size_t)h->n + 2 * (size_t)h->e + sizeof(uint32_t) * (1 + 2 * (size_t)h->e) +
                           sizeof(double) * (size_t)h->e;
         e = hipMalloc((void**)&h->x->d_pxo, sizeof(uint64_t) * (size_t)h->n);
@@ -2067,6 +2194,10 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.prune_peers = h->gp.prune_peers;
     a.accept_px = h->th.accept_px_threshold;
     a.pxo = h->x->d_pxo; a.pxm = h->x->d_pxm; a.nopx = h->x->d_nopx; a.pxs = h->x->d_pxs;
+    if (ShardCtx* sh = h->sh; sh && sh->d_pxout && a.do_px) {
+        a.pxout = sh->d_pxout; a.pxcnt = sh->d_pxcnt; a.pxcap = sh->pxcap; a.pxK = sh->K;
+        a.xre = sh->d_xre; a.pshard = sh->d_pshard;
+    }
     a.tr = h->trace;
     return a;
 }

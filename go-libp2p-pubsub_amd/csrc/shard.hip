@@ -689,6 +689,7 @@ void free_shard_bufs(ShardCtx* s)
     f(s->d_rmesh_out); f(s->d_rfan_out); f(s->d_rflag_out); f(s->d_rmesh_in); f(s->d_rfan_in); f(s->d_rflag_in);
     f(s->d_gout); f(s->d_gsout); f(s->d_gin); f(s->d_gsin);
     f(s->d_xre); f(s->d_pshard); f(s->d_xsub); f(s->d_xcnt); f(s->d_xsend); f(s->d_xrecv); f(s->d_xn);
+    f(s->d_pxout); f(s->d_pxcnt); f(s->d_pxin);
     if (s->h_counts) (void)hipHostFree(s->h_counts);
     if (s->h_xcnt) (void)hipHostFree(s->h_xcnt);
     ShardCtx fresh;
@@ -1131,11 +1132,6 @@ int group_create(const gsim_peer_score_params* params, const gsim_topic_score_pa
                  const gsim_thresholds* th, const gsim_gossipsub_params* gp, int32_t shards,
                  const std::vector<std::pair<int, int>>& local, gsim_group** out, char* err, size_t errlen)
 {
-    if (gp && gp->do_px) {
-        // pxConnect resolves a pruned peer's whole row, which a shard holds only for its own peers
-        if (err && errlen) std::snprintf(err, errlen, "peer exchange (do_px) is not supported on a sharded group");
-        return GSIM_EINVAL;
-    }
     gsim_group* g = new gsim_group();
     g->K = shards;
     const char* ser = std::getenv("GSIM_GROUP_SERIAL");
@@ -1418,6 +1414,21 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
             if (hipGetLastError() != hipSuccess) return g->fail(GSIM_EDEVICE, "k_xre_build");
         }
     }
+    // peer exchange: PX lists to ghosts (k_px_emit's remote path), per destination
+    for (gsim_handle* h : g->hs) {
+        ShardCtx* s = h->sh;
+        if (!px_enabled(h)) continue;
+        (void)hipSetDevice(h->device);
+        // a tick's PX lists to one shard: PrunePeers entries per cross edge into it
+        // (an overflow fails gsim_group_px_connect)
+        int64_t xmax = 0;
+        for (int q = 0; q < K; ++q) xmax = std::max<int64_t>(xmax, s->xoff[(size_t)q + 1] - s->xoff[(size_t)q]);
+        s->pxcap = std::max<int64_t>(1 << 16, (int64_t)std::max(1, h->gp.prune_peers) * xmax);
+        if ((rc = dalloc(h, &s->d_pxout, (size_t)(K * s->pxcap))) || (rc = dalloc(h, &s->d_pxcnt, (size_t)K + 1)))
+            return g->take(h, rc);
+        if (hipMemset(s->d_pxcnt, 0, sizeof(uint32_t) * ((size_t)K + 1)) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "PX list counts");
+    }
     return sync_all(g);
 }
 
@@ -1686,6 +1697,159 @@ int gsim_group_set_connections(gsim_group* g, const uint32_t* pairs, int32_t cou
     }
     g->router_dirty = true;
     return GSIM_OK;
+}
+
+// The connector (gossipsub.go:941-973) over the shards, run between ticks by
+// every rank: (1) the PX lists PRUNEs carried to other shards' peers are
+// delivered and checked there (handlePrune's acceptPXThreshold, a known
+// address, not connected: k_px_import); (2) every shard's attempts (asker,
+// peer) go to every rank, which resolves each pair once as gsim_px_connect
+// does — the asker dials, the lower id when both asked; (3) gs.outbound is set
+// on the owned ends and the connections are made with AddPeer at both ends
+// (gsim_group_set_connections).
+int gsim_group_px_connect(gsim_group* g, int64_t now, uint32_t* pairs, int64_t cap, int64_t* n_connected)
+{
+    if (!g || !n_connected) return GSIM_EINVAL;
+    *n_connected = 0;
+    const size_t L = g->hs.size();
+    const int K = g->K;
+    if (L == 0 || !px_enabled(g->hs[0])) return GSIM_OK;      // WithPeerExchange is off
+    // (1) PX lists to the pruned peers' shards
+    std::vector<std::vector<uint64_t>> scnt(L, std::vector<uint64_t>((size_t)K, 0)), rcnt;
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        (void)hipSetDevice(h->device);
+        if (hipMemcpyAsync(s->h_counts, s->d_pxcnt, sizeof(uint32_t) * ((size_t)K + 1), hipMemcpyDeviceToHost,
+                           h->stream) != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "PX list counts");
+        if (s->h_counts[K]) return g->fail(GSIM_ERANGE, "PX list overflow");
+        for (int d = 0; d < K; ++d) scnt[l][(size_t)d] = d == g->ids[l] ? 0 : s->h_counts[d];
+    }
+    int rc = g->take_tr(g->tr->exchange_counts(scnt, rcnt));
+    if (rc) return rc;
+    std::vector<std::vector<const void*>> sp(L, std::vector<const void*>((size_t)K, nullptr));
+    std::vector<std::vector<void*>> rp(L, std::vector<void*>((size_t)K, nullptr));
+    std::vector<std::vector<uint64_t>> sb(L, std::vector<uint64_t>((size_t)K, 0)), rb = sb;
+    std::vector<int64_t> total(L, 0);
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        for (int q = 0; q < K; ++q) total[l] += (int64_t)rcnt[l][(size_t)q];
+        (void)hipSetDevice(h->device);
+        rc = g->take(h, ensure(h, &s->d_pxin, &s->pxin_cap, std::max<int64_t>(total[l], 1)));
+        if (rc) return rc;
+        int64_t off = 0;
+        for (int q = 0; q < K; ++q) {
+            sp[l][(size_t)q] = s->d_pxout + (size_t)q * (size_t)s->pxcap;
+            sb[l][(size_t)q] = scnt[l][(size_t)q] * 8;
+            rp[l][(size_t)q] = s->d_pxin + off;
+            rb[l][(size_t)q] = rcnt[l][(size_t)q] * 8;
+            off += (int64_t)rcnt[l][(size_t)q];
+        }
+    }
+    rc = g->take_tr(g->tr->alltoallv(sp, sb, rp, rb));
+    if (rc) return rc;
+    // (2) every shard's attempts, to every rank
+    std::vector<std::vector<uint64_t>> acnt(L, std::vector<uint64_t>((size_t)K, 0));
+    std::vector<std::vector<uint64_t>> own(L);
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        (void)hipSetDevice(h->device);
+        rc = g->take(h, px_import(h, s->d_pxin, total[l]));
+        if (!rc) rc = g->take(h, px_asks(h, s->d_pxout, s->d_pxcnt, (int64_t)K * s->pxcap));
+        if (rc) return rc;
+        if (hipMemcpyAsync(s->h_counts, s->d_pxcnt, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+            hipStreamSynchronize(h->stream) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "PX attempts count");
+        const int64_t na = s->h_counts[0];
+        if (na > (int64_t)K * s->pxcap) return g->fail(GSIM_ERANGE, "PX attempts overflow");
+        own[l].resize((size_t)na);
+        if (na && hipMemcpy(own[l].data(), s->d_pxout, sizeof(uint64_t) * (size_t)na, hipMemcpyDeviceToHost) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "PX attempts readback");
+        if (hipMemset(s->d_pxcnt, 0, sizeof(uint32_t) * ((size_t)K + 1)) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "PX list counts");
+        for (int d = 0; d < K; ++d) acnt[l][(size_t)d] = d == g->ids[l] ? 0 : (uint64_t)na;
+    }
+    rc = g->take_tr(g->tr->exchange_counts(acnt, rcnt));
+    if (rc) return rc;
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        total[l] = 0;
+        for (int q = 0; q < K; ++q) total[l] += (int64_t)rcnt[l][(size_t)q];
+        (void)hipSetDevice(h->device);
+        rc = g->take(h, ensure(h, &s->d_pxin, &s->pxin_cap, std::max<int64_t>(total[l], 1)));
+        if (rc) return rc;
+        int64_t off = 0;
+        for (int q = 0; q < K; ++q) {
+            sp[l][(size_t)q] = s->d_pxout;
+            sb[l][(size_t)q] = acnt[l][(size_t)q] * 8;
+            rp[l][(size_t)q] = s->d_pxin + off;
+            rb[l][(size_t)q] = rcnt[l][(size_t)q] * 8;
+            off += (int64_t)rcnt[l][(size_t)q];
+        }
+    }
+    rc = g->take_tr(g->tr->alltoallv(sp, sb, rp, rb));
+    if (rc) return rc;
+    // every attempt of the job (this process's shards' own, the others' received)
+    std::vector<uint64_t> asks;
+    for (size_t l = 0; l < L; ++l) asks.insert(asks.end(), own[l].begin(), own[l].end());
+    if (L < (size_t)K) {        // one shard per process: the other ranks' lists (in-process: all are local)
+        gsim_handle* h = g->hs[0];
+        std::vector<uint64_t> in((size_t)total[0]);
+        (void)hipSetDevice(h->device);
+        if (total[0] && hipMemcpy(in.data(), h->sh->d_pxin, sizeof(uint64_t) * in.size(), hipMemcpyDeviceToHost) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "PX attempts readback");
+        asks.insert(asks.end(), in.begin(), in.end());
+    }
+    // resolve: per unordered pair, the asker dials (the lower id when both asked)
+    std::vector<std::pair<uint64_t, uint32_t>> keyed;     // (lo | hi << 32, bit 1: lo asked, bit 2: hi asked)
+    keyed.reserve(asks.size());
+    for (uint64_t v : asks) {
+        const uint32_t a_ = (uint32_t)v, b_ = (uint32_t)(v >> 32);
+        const uint32_t lo = std::min(a_, b_), hi = std::max(a_, b_);
+        keyed.push_back({(uint64_t)lo | ((uint64_t)hi << 32), a_ == lo ? 1u : 2u});
+    }
+    std::sort(keyed.begin(), keyed.end());
+    std::vector<std::pair<uint32_t, uint32_t>> made;
+    for (size_t q = 0; q < keyed.size();) {
+        uint32_t who = 0;
+        size_t r = q;
+        while (r < keyed.size() && keyed[r].first == keyed[q].first) who |= keyed[r++].second;
+        const uint32_t lo = (uint32_t)keyed[q].first, hi = (uint32_t)(keyed[q].first >> 32);
+        made.push_back((who & 1u) ? std::make_pair(lo, hi) : std::make_pair(hi, lo));
+        q = r;
+    }
+    std::sort(made.begin(), made.end());
+    *n_connected = (int64_t)made.size();
+    if (pairs)
+        for (size_t q = 0; q < made.size() && (int64_t)q < cap; ++q) {
+            pairs[2 * q] = made[q].first;
+            pairs[2 * q + 1] = made[q].second;
+        }
+    if (made.empty()) return GSIM_OK;
+    // (3) gs.outbound on the owned ends, then the connections
+    std::vector<uint64_t> pv(made.size());
+    std::vector<uint32_t> flat(2 * made.size());
+    for (size_t q = 0; q < made.size(); ++q) {
+        pv[q] = (uint64_t)made[q].first | ((uint64_t)made[q].second << 32);
+        flat[2 * q] = made[q].first;
+        flat[2 * q + 1] = made[q].second;
+    }
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        (void)hipSetDevice(h->device);
+        rc = g->take(h, ensure(h, &s->d_pxin, &s->pxin_cap, (int64_t)pv.size()));
+        if (rc) return rc;
+        if (hipMemcpy(s->d_pxin, pv.data(), sizeof(uint64_t) * pv.size(), hipMemcpyHostToDevice) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "PX connections upload");
+        rc = g->take(h, px_mark_outbound(h, s->d_pxin, (int64_t)pv.size()));
+        if (rc) return rc;
+    }
+    return gsim_group_set_connections(g, flat.data(), (int32_t)made.size(), 1, now);
 }
 
 // Totals summed over the shards (every process gets the job's totals).

@@ -355,6 +355,15 @@ class ShardedEngine:
         ii = np.ascontiguousarray(ip_ids, dtype=np.uint32)
         self._check(self.lib.gsim_group_set_ips(self.g, _ptr(pp), _ptr(ii), int(n_ips)))
 
+    def px_connect(self, now: int) -> np.ndarray:
+        """The connector over the shards (gsim_group_px_connect; every rank
+        calls it): the (dialer, peer) pairs that became connections, sorted."""
+        n = ctypes.c_int64(0)
+        cap = max(1, self.net.e // 2)
+        out = np.zeros((cap, 2), dtype=np.uint32)
+        self._check(self.lib.gsim_group_px_connect(self.g, int(now), _ptr(out), int(cap), ctypes.byref(n)))
+        return out[:min(n.value, cap)].copy()
+
     def msg_stats(self) -> list:
         out = np.zeros(4, dtype=np.int64)
         self._check(self.lib.gsim_group_msg_stats(self.g, _ptr(out)))

@@ -721,6 +721,13 @@ int gsim_group_heartbeat(gsim_group* g, uint64_t tick, int64_t now_ns);
 int gsim_group_publish(gsim_group* g, const gsim_msg* msgs, int32_t count, int64_t round);
 int gsim_group_round(gsim_group* g, int64_t round);
 int gsim_group_set_connections(gsim_group* g, const uint32_t* pairs, int32_t count, int32_t up, int64_t now_ns);
+/* gsim_px_connect over the shards (every rank calls it between ticks): PX
+ * lists PRUNEs carried to other shards' peers are checked there
+ * (acceptPXThreshold on the pruned peer's score, a known address, not
+ * connected), every attempt is resolved once (the asker dials, the lower id
+ * when both asked) and connected at both ends; pairs: the (dialer, peer)
+ * global ids, sorted.  The same connections as one engine's gsim_px_connect. */
+int gsim_group_px_connect(gsim_group* g, int64_t now_ns, uint32_t* pairs, int64_t cap, int64_t* n_connected);
 int gsim_group_set_ips(gsim_group* g, const uint32_t* ip_ptr, const uint32_t* ip_ids, uint32_t n_ips);
 /* Router state (mesh / fanout flags, connection state, direct flags) was
  * written through gsim_write_field on a shard handle: the ghost rows are

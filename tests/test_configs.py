@@ -360,9 +360,10 @@ def test_hub_rows_bit_exact(require_gpu, topic_slots):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("topic_slots", [0, 24])
-def test_c5_combined_wide_hubs_zipf_churn_px_verdicts(require_gpu, topic_slots):
-    """C5's whole shape on one engine: a plain Chung-Lu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("topic_slots,shards", [(0, 0), (24, 0), (0, 3)])
+def test_c5_combined_wide_hubs_zipf_churn_px_verdicts(require_gpu, topic_slots, shards):
+    """C5's whole shape on one engine and on 3 shards: a plain Chung-Lu
     power law (exponent 2.5, i0 = 1) whose hubs exceed 1024 connections (up
     to the 4096 cap: heartbeat, fanout and PX on 4 row positions per thread),
     64 topics with Zipf subscriptions, dense meshes on the hubs (Dhi prune
@@ -396,5 +397,14 @@ def test_c5_combined_wide_hubs_zipf_churn_px_verdicts(require_gpu, topic_slots):
     down = und[rng.choice(len(und), size=len(und) // 100, replace=False)]
     churn = {2: [(down, False)], 4: [(down, True)]}
     log = []
-    run_parity(net, params, th, gp, st, ticks, sched, ring=2048, churn=churn, px_log=log, topic_slots=topic_slots)
+    eng = None
+    if shards:
+        from gsim.shard import ShardedEngine
+        from tickrun import SEED
+        eng = ShardedEngine(params, th, gossip=gp, shards=shards)
+        eng.load_graph(net)
+        eng.set_seed(SEED)
+        st.push_to_engine(eng)
+    run_parity(net, params, th, gp, st, ticks, sched, ring=2048, churn=churn, px_log=log, topic_slots=topic_slots,
+               eng=eng)
     assert sum(log) > 0, "PX made connections"

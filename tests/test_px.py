@@ -130,13 +130,25 @@ def test_px_bit_exact(require_gpu, T, accept):
     assert sum(log) > 0, "PX made connections"
 
 
-def test_sharded_group_refuses_peer_exchange():
-    """pxConnect resolves a pruned peer's whole row, which a shard holds only
-    for its own peers: a group with PX is refused before any device work."""
-    from fixtures import beacon_params
-    from gsim.engine import GsimError
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards", [2, 3])
+def test_px_sharded_bit_exact(require_gpu, shards):
+    """Peer exchange on a graph-sharded network: PRUNEs with PX to a peer of
+    another shard carry their lists there (handlePrune's acceptPXThreshold and
+    pxConnect's known-address check run at the pruned peer's shard), and the
+    connector resolves every shard's attempts once (gsim_group_px_connect):
+    state, seen-set and the connections made bit-exact against the oracle."""
     from gsim.shard import ShardedEngine
-    gp = GossipSubParams(D=6, Dlo=5, Dhi=10, PeerExchange=True)
-    with pytest.raises((GsimError, ValueError, RuntimeError)) as ei:
-        ShardedEngine(beacon_params(2), PeerScoreThresholds(), gossip=gp, shards=2)
-    assert "peer exchange" in str(ei.value)
+    from tickrun import SEED, run_parity, subscribed_schedule
+    net, params, th, gp, st, down = _px_network(n=900, k=24, T=3, accept=1.0, seed=41 + shards)
+    rng = np.random.default_rng(50 + shards)
+    eng = ShardedEngine(params, th, gossip=gp, shards=shards)
+    eng.load_graph(net)
+    eng.set_seed(SEED)
+    st.push_to_engine(eng)
+    ticks = list(range(1, 6))
+    sched = subscribed_schedule(rng, ticks, net, 3, 3.0, 0.02)
+    churn = {1: [(down, False)]}
+    log = []
+    run_parity(net, params, th, gp, st, ticks, sched, ring=512, churn=churn, px_log=log, eng=eng)
+    assert sum(log) > 0, "PX made connections"
