@@ -147,7 +147,7 @@ def build_engine(cfg, seed, device, scen=None, shard=None):
     n, k, T, D, Dlo, Dhi = cfg
     scen = scen or {}
     params = beacon_params(T)
-    gp = gsim.GossipSubParams(D=D, Dlo=Dlo, Dhi=Dhi, PeerExchange=bool(scen.get("px")) and shard is None)
+    gp = gsim.GossipSubParams(D=D, Dlo=Dlo, Dhi=Dhi, PeerExchange=bool(scen.get("px")))
     if "opp_ticks" in scen:
         gp.OpportunisticGraftTicks = scen["opp_ticks"]
     if shard is None:
