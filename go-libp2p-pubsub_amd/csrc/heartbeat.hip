@@ -1753,9 +1753,12 @@ __global__ void k_subscribe(HbArgs a, uint64_t* sub, const uint32_t* pairs, int3
             atomicOr(reinterpret_cast<unsigned long long*>(a.cany_out + c), bit);
         };
         const ctp_t tp = const_tp(a.tp) + t;
+        // a shard: a ghost's announcement only (its own shard runs its router)
+        const bool own = p >= a.olo && p < a.ohi;
         if (join) {
             if (sub[p] & bit) continue;                      // gs.mesh[topic] exists
             sub[p] |= bit;                                   // the announcement
+            if (!own) continue;
             if (a.tr.on(p)) a.tr.push(a.now, 0, p, p, t, GSIM_TRACE_JOIN, 0);
             // getPeers: the `count` candidates with the smallest keys, in key order
             auto pick = [&](int count, bool more) {
@@ -1807,6 +1810,7 @@ __global__ void k_subscribe(HbArgs a, uint64_t* sub, const uint32_t* pairs, int3
         } else {
             if (!(sub[p] & bit)) continue;                   // no mesh for the topic
             sub[p] &= ~bit;
+            if (!own) continue;
             if (a.tr.on(p)) a.tr.push(a.now, 0, p, p, t, GSIM_TRACE_LEAVE, 0);
             // emitGossip no longer runs for the topic (unless as a fanout): its
             // last IHAVE targets must not be advertised to again
@@ -2470,7 +2474,6 @@ int gsim_set_subscriptions(gsim_handle* h, const uint32_t* pairs, int32_t count,
     if (!h) return GSIM_EINVAL;
     if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
     if (h->e == 0 || !h->x) { h->err = "no graph loaded"; return GSIM_ESTATE; }
-    if (h->sh) { h->err = "subscription changes run on a single engine, not a shard"; return GSIM_ESTATE; }
     if (count < 0 || (count > 0 && !pairs)) { h->err = "bad subscription list"; return GSIM_EINVAL; }
     if (count == 0) return GSIM_OK;
     const int32_t T = std::max(1, h->t);

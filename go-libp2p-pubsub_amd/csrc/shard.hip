@@ -1852,6 +1852,39 @@ int gsim_group_px_connect(gsim_group* g, int64_t now, uint32_t* pairs, int64_t c
     return gsim_group_set_connections(g, flat.data(), (int32_t)made.size(), 1, now);
 }
 
+// Join / Leave over the shards (gsim_set_subscriptions per shard, every
+// rank with the same list): each shard runs the batch in order over its local
+// peers — the owned ones' routers (Join's getPeers and GRAFTs, Leave's PRUNEs),
+// the ghosts' announcements — so a later pair sees the earlier ones as on one
+// engine; GRAFT/PRUNE to other shards' peers sit in the ghosts' inboxes of
+// control round 0 and leave with the heartbeat's control exchange.
+int gsim_group_set_subscriptions(gsim_group* g, const uint32_t* pairs, int32_t count, int32_t join, uint64_t tick,
+                                 int64_t now)
+{
+    if (!g || count < 0 || (count > 0 && !pairs)) return GSIM_EINVAL;
+    for (int32_t q = 0; q < count; ++q)
+        if ((int64_t)pairs[2 * q] >= g->N) return g->fail(GSIM_EINVAL, "subscription pair out of range");
+    for (size_t l = 0; l < g->hs.size(); ++l) {
+        const std::vector<uint32_t>& gid = g->gid[l];
+        std::vector<uint32_t> v;
+        for (int32_t q = 0; q < count; ++q) {
+            auto it = std::lower_bound(gid.begin(), gid.end(), pairs[2 * q]);
+            if (it == gid.end() || *it != pairs[2 * q]) continue;          // not a peer of this shard
+            v.push_back((uint32_t)(it - gid.begin()));
+            v.push_back(pairs[2 * q + 1]);
+        }
+        (void)hipSetDevice(g->hs[l]->device);
+        const int rc = gsim_set_subscriptions(g->hs[l], v.data(), (int32_t)(v.size() / 2), join, tick, now);
+        if (rc) return g->take(g->hs[l], rc);
+    }
+    for (int32_t q = 0; q < count && !g->sub.empty(); ++q) {
+        const uint64_t bit = 1ull << pairs[2 * q + 1];
+        if (join) g->sub[pairs[2 * q]] |= bit; else g->sub[pairs[2 * q]] &= ~bit;
+    }
+    g->router_dirty = true;
+    return GSIM_OK;
+}
+
 // Totals summed over the shards (every process gets the job's totals).
 static int group_sum(gsim_group* g, int (*fn)(gsim_handle*, int64_t*), int n, int64_t* out)
 {

@@ -280,6 +280,7 @@ SIGNATURES = [
       POINTER(CGossipSubParams), c_int32, c_int32, c_int32, POINTER(CHostTransport), POINTER(c_void_p), c_char_p,
       c_size_t]),
     ("gsim_group_px_connect", c_int32, [c_void_p, c_int64, c_void_p, c_int64, POINTER(c_int64)]),
+    ("gsim_group_set_subscriptions", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_uint64, c_int64]),
     ("gsim_group_destroy", c_int32, [c_void_p]),
     ("gsim_group_last_error", c_char_p, [c_void_p]),
     ("gsim_group_shard", c_void_p, [c_void_p, c_int32]),

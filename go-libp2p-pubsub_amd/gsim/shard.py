@@ -355,6 +355,13 @@ class ShardedEngine:
         ii = np.ascontiguousarray(ip_ids, dtype=np.uint32)
         self._check(self.lib.gsim_group_set_ips(self.g, _ptr(pp), _ptr(ii), int(n_ips)))
 
+    def set_subscriptions(self, pairs, join: bool, tick: int, now: int):
+        """Join / Leave of (peer, topic) pairs between ticks, over the shards
+        (gsim_group_set_subscriptions; every rank passes the same pairs)."""
+        p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint32).reshape(-1, 2))
+        self._check(self.lib.gsim_group_set_subscriptions(self.g, _ptr(p), int(p.shape[0]), 1 if join else 0,
+                                                          int(tick), int(now)))
+
     def px_connect(self, now: int) -> np.ndarray:
         """The connector over the shards (gsim_group_px_connect; every rank
         calls it): the (dialer, peer) pairs that became connections, sorted."""

@@ -728,6 +728,10 @@ int gsim_group_set_connections(gsim_group* g, const uint32_t* pairs, int32_t cou
  * when both asked) and connected at both ends; pairs: the (dialer, peer)
  * global ids, sorted.  The same connections as one engine's gsim_px_connect. */
 int gsim_group_px_connect(gsim_group* g, int64_t now_ns, uint32_t* pairs, int64_t cap, int64_t* n_connected);
+/* gsim_set_subscriptions over the shards (global peer ids; every rank passes
+ * the same list): the same Joins / Leaves as one engine. */
+int gsim_group_set_subscriptions(gsim_group* g, const uint32_t* pairs, int32_t count, int32_t join, uint64_t tick,
+                                 int64_t now_ns);
 int gsim_group_set_ips(gsim_group* g, const uint32_t* ip_ptr, const uint32_t* ip_ids, uint32_t n_ips);
 /* Router state (mesh / fanout flags, connection state, direct flags) was
  * written through gsim_write_field on a shard handle: the ghost rows are

@@ -104,11 +104,13 @@ def test_a_router_drops_messages_of_a_topic_it_left():
 # ---- GPU parity -------------------------------------------------------------------
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("topic_slots", [0, 80])
-def test_join_leave_bit_exact(require_gpu, topic_slots):
+@pytest.mark.parametrize("topic_slots,shards", [(0, 0), (80, 0), (0, 3)])
+def test_join_leave_bit_exact(require_gpu, topic_slots, shards):
     """Joins (with and without a fanout) and Leaves between ticks, fanout
     publishers, gossip, churn and the trace: every state array, the seen-set,
-    the totals and the JOIN / LEAVE / GRAFT / PRUNE events bit-exact."""
+    the totals and the JOIN / LEAVE / GRAFT / PRUNE events bit-exact — on one
+    engine and on 3 shards (GRAFT / PRUNE to other shards' peers leave with
+    the heartbeat's control exchange)."""
     from fixtures import beacon_params, synthetic_state
     from gsim.engine import random_regular
     from tickrun import restrict_to_subscriptions, run_parity, subscribed_schedule
@@ -139,7 +141,16 @@ def test_join_leave_bit_exact(require_gpu, topic_slots):
                 ev.append((int(p), t))
         subs[kk] = [(np.array(ev, dtype=np.uint32), join)]
     log = []
-    run_parity(net, params, th, gp, st, ticks, sched, ring=256, subs=subs, trace=(0, n), trace_log=log,
-               topic_slots=topic_slots)
-    total = np.sum(log, axis=0)
-    assert total[_abi.TRACE_JOIN] > 0 and total[_abi.TRACE_LEAVE] > 0
+    eng = None
+    if shards:
+        from gsim.shard import ShardedEngine
+        from tickrun import SEED as TSEED
+        eng = ShardedEngine(params, th, gossip=gp, shards=shards)
+        eng.load_graph(net)
+        eng.set_seed(TSEED)
+        st.push_to_engine(eng)
+    run_parity(net, params, th, gp, st, ticks, sched, ring=256, subs=subs, trace=None if shards else (0, n),
+               trace_log=log, topic_slots=topic_slots, eng=eng)
+    if not shards:
+        total = np.sum(log, axis=0)
+        assert total[_abi.TRACE_JOIN] > 0 and total[_abi.TRACE_LEAVE] > 0
