@@ -349,7 +349,7 @@ def main():
     ap.add_argument("--msg-rate", type=float, default=None, help="messages per second per topic (config default)")
     ap.add_argument("--ring", type=int, default=None, help="message ring slots (config default)")
     ap.add_argument("--vdelay", type=int, default=0,
-                    help="validation latency of every message in rounds (gsim_msg.vdelay; single engine)")
+                    help="validation latency of every message in rounds (gsim_msg.vdelay)")
     ap.add_argument("--replicas", action="store_true",
                     help="N > 1: one independent network per rank (weak scaling) instead of one sharded network")
     ap.add_argument("--shards", type=int, default=1,

@@ -2631,7 +2631,10 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
     const RoundArgs& a = a0;
     // the slot list in LDS
     const size_t lds = ((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7;
-    if (a.push && sparse_layout(h))
+    if (a.push && a.mlat)
+        hipLaunchKernelGGL((k_send_tm<kPushTB, true, true, false, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
+                           h->stream, a);
+    else if (a.push && sparse_layout(h))
         hipLaunchKernelGGL((k_send_tm<kPushTB, false, true, false, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
                            h->stream, a);
     else if (a.push)
@@ -2868,8 +2871,11 @@ __global__ __launch_bounds__(256) void k_frontier_export(RoundArgs a, const uint
         int64_t pos = (int64_t)s_base + s_wsum[wid] + (v - c);
         for (uint64_t b = bits; b; b &= b - 1, ++pos) {
             const int64_t i = w * 64 + __ffsll((long long)b) - 1;
-            const uint32_t f = (uint32_t)a.cs.get(m, (int32_t)a.mtopic[m], (uint32_t)i) & kPeerMask;
-            const uint64_t gf = f < a.N ? (uint64_t)gid[f] : kG24;
+            const uint64_t c = a.cs.get(m, (int32_t)a.mtopic[m], (uint32_t)i);
+            const uint32_t f = (uint32_t)c & kPeerMask;
+            // push: the cell's first-seen (or validation-completion) round in
+            // place of the first sender, which no other shard reads
+            const uint64_t gf = a.push ? ((c >> 32) & kG24) : f < a.N ? (uint64_t)gid[f] : kG24;
             if (pos < cap) out[pos] = (uint64_t)gid[i] | (gf << 24) | ((uint64_t)m << 48);
         }
         __syncthreads();
@@ -2893,14 +2899,15 @@ __global__ __launch_bounds__(256) void k_frontier_import(RoundArgs a, const uint
             l = g2l[v & kG24];
             ghost = l != 0xFFFFFFFFu && !(l >= a.rlo && l < a.rhi);         // a ghost of this shard
             if (ghost) {
-                // (push: only the round is read, by IHAVE; pull: the first
-                // sender too, by the ghost's walk)
+                // (push: only the round is read, by IHAVE, and comes with the
+                // entry; pull: the first sender too, by the ghost's walk)
                 const uint64_t gf = a.push ? kG24 : (v >> 24) & kG24;
                 uint32_t f = gf == kG24 ? 0xFFFFFFFFu : g2l[gf];
                 if (f == 0xFFFFFFFFu) f = kPeerMask;                         // not a local peer
+                const uint32_t fr = a.push ? (uint32_t)((v >> 24) & kG24) : (uint32_t)(a.g - 1);
                 m = (uint32_t)(v >> 48);
                 const int64_t ci = a.cs.idx(m, (int32_t)a.mtopic[m], l);    // a forwarder holds the topic
-                if (ci >= 0) a.cs.cell[ci] = ((uint64_t)(uint32_t)(a.g - 1) << 32) | f;
+                if (ci >= 0) a.cs.cell[ci] = ((uint64_t)fr << 32) | f;
                 // (filtering out ghosts without mesh edges into this shard, by
                 // their masks, cost more in the import than it saved in the
                 // walk: K = 8 serial shards 31.8 against 20.2 ms per tick)
@@ -3333,8 +3340,8 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
             h->err = "a validation latency (vdelay) cannot be combined with the peer gater";
             return GSIM_ESTATE;
         }
-        if (msgs[m].vdelay && h->sh) {
-            h->err = "a validation latency (vdelay) needs a single engine (not a shard)";
+        if (msgs[m].vdelay && h->sh && !h->sh->push) {
+            h->err = "a validation latency (vdelay) on shards needs the copy push (GSIM_SHARD_PULL unset)";
             return GSIM_ERANGE;
         }
     }

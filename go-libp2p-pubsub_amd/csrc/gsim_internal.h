@@ -543,6 +543,7 @@ int deliver_round_queue(gsim_handle* h, int64_t round, const uint64_t* q, const 
 int deliver_round_post(gsim_handle* h, int64_t round);
 int deliver_round_control(gsim_handle* h, int64_t round);
 int deliver_round_ihave(gsim_handle* h, int64_t round);
+int deliver_round_validate(gsim_handle* h, int64_t round);
 void deliver_round_end(gsim_handle* h, int64_t round);
 int32_t* deliver_slot_last(gsim_handle* h);           // [ring]
 int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32_t* d_cnt, int64_t cap);

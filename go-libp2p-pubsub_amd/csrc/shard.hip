@@ -1666,6 +1666,7 @@ int gsim_group_round(gsim_group* g, int64_t round)
     for (gsim_handle* h : g->hs) {
         (void)hipSetDevice(h->device);
         rc = deliver_round_ihave(h, round);             // ghost advertisers: their cells
+        if (!rc) rc = deliver_round_validate(h, round);  // validations completing (gsim_msg.vdelay)
         if (rc) return g->take(h, rc);
         g->settle(h);
         deliver_round_end(h, round);

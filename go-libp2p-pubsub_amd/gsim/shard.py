@@ -334,9 +334,12 @@ class ShardedEngine:
         self._check(self.lib.gsim_group_heartbeat(self.g, int(tick), int(now)))
 
     def publish(self, msgs, rnd: int):
+        """As Engine.publish: (id, topic, origin, verdict[, vdelay]) with global origins."""
         arr = np.zeros(len(msgs), dtype=_abi.MSG_DTYPE)
-        for k, (mid, topic, origin, verdict) in enumerate(msgs):
+        for k, msg in enumerate(msgs):
+            mid, topic, origin, verdict = msg[:4]
             arr[k]["id"], arr[k]["topic"], arr[k]["origin"], arr[k]["verdict"] = mid, topic, origin, verdict
+            arr[k]["vdelay"] = msg[4] if len(msg) > 4 else 0
         self.publish_array(arr, rnd)
 
     def publish_array(self, arr: np.ndarray, rnd: int):

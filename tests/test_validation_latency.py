@@ -125,6 +125,40 @@ def test_validation_latency_bit_exact(require_gpu, window, trace):
     assert msgs.stats[1] > 0 and gstats["iwant_ids"] > 0, "first deliveries and IWANTs happened"
 
 
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("shards", [2, 3])
+def test_validation_latency_sharded_bit_exact(require_gpu, shards):
+    """Validation latency on a graph-sharded network (copy push): pending
+    duplicates of copies pushed from other shards queue at the receiver's
+    shard, completions forward from the owner's shard, and the ghosts'
+    holder rounds carry the completion round — bit-exact against the oracle
+    with every verdict, gossip and churn."""
+    from fixtures import synthetic_state
+    from gsim.shard import ShardedEngine
+    from tickrun import SEED, run_parity, subscribed_schedule
+    rng = np.random.default_rng(43 + shards)
+    n, k, T = 1500, 16, 3
+    params = _params(T, 5 * 60 * Second)
+    net = random_regular(n, k, seed=47, n_topics=T)
+    st = ob.NetState(net, params, thresholds=TH, gossip=GP)
+    synthetic_state(st, rng, tick_time(0), 0.6)
+    eng = ShardedEngine(params, TH, gossip=GP, shards=shards)
+    eng.load_graph(net)
+    eng.set_seed(SEED)
+    st.push_to_engine(eng)
+    ticks = list(range(1, 6))
+    sched = subscribed_schedule(rng, ticks, net, T, 4.0, 0.0, verdicts=(0.7, 0.1, 0.1, 0.05, 0.05),
+                                vdelays=(0, 1, 2, 3))
+    src = net.owner()
+    und = np.stack([src, net.col], axis=1)
+    und = und[und[:, 0] < und[:, 1]]
+    down = und[rng.choice(len(und), size=len(und) // 40, replace=False)]
+    churn = {3: [(down, False)], 5: [(down, True)]}
+    msgs, gstats = run_parity(net, params, TH, GP, st, ticks, sched, ring=512, churn=churn, eng=eng)
+    assert msgs.stats[1] > 0 and gstats["iwant_ids"] > 0, "first deliveries and IWANTs happened"
+
+
 # RejectMessage reasons of each verdict (tracer.go:28-38, oracle.h ORC_REJECT_*)
 _REASON = {_abi.VERDICT_REJECT: 8, _abi.VERDICT_IGNORE: 9, _abi.VERDICT_THROTTLE: 7}
 
