@@ -75,6 +75,12 @@ constexpr uint32_t kHubList = 0x80000000u;   // k_send_tm s_beg flag: an offset 
 // sets the fresh bits (forwarding in round g + L + 1) and the mcache puts.
 constexpr int kVqPlanes = GSIM_MAX_VDELAY + 1;   // queues by completion round mod kVqPlanes
 constexpr uint32_t kVqFirst = 1, kVqDup = 2, kVqInv = 3;
+// each plane's queue is kVqSub sub-lists (vq_cap / kVqSub entries) whose
+// counters sit kVqStride u32s apart (own cache lines: append contention)
+constexpr int kVqSub = 16, kVqStride = 32;
+__host__ __device__ constexpr int64_t vq_ctr(int pl, int sub) { return ((int64_t)pl * kVqSub + sub) * kVqStride; }
+constexpr int64_t kVqOver = (int64_t)kVqPlanes * kVqSub * kVqStride;   // overflow flag
+constexpr int64_t kVqnWords = kVqOver + kVqStride;
 static_assert((kVqPlanes & (kVqPlanes - 1)) == 0, "power-of-two planes");
 
 struct Deliver {
@@ -83,7 +89,8 @@ struct Deliver {
     uint8_t* d_minv = nullptr;
     uint8_t* d_mlat = nullptr;         // [ring] validation latency of the slot's message (gsim_msg.vdelay)
     uint64_t* d_vq = nullptr;          // [kVqPlanes][vq_cap] copies pending validation, by completion round
-    uint32_t* d_vqn = nullptr;         // [kVqPlanes] entries per plane; [kVqPlanes] overflow flag
+    uint8_t* d_vpc = nullptr;          // dense layout: [2][kVqPlanes][T * E] pending duplicate / invalid counts per record
+    uint32_t* d_vqn = nullptr;         // sub-list counters (vq_ctr), then the overflow flag (kVqOver)
     uint32_t* d_hist = nullptr;        // [kVqPlanes][ring/32] slots with new claims, by round
     int64_t vq_cap = 0;
     bool lat_on = false;               // a message with vdelay > 0 was published
@@ -178,6 +185,8 @@ struct RoundArgs {
     const uint8_t* mlat;       // [ring] validation latency (nullptr: none published, every latency 0)
     uint8_t* mlat_w;           // the same array, written by k_publish
     uint64_t* vq;              // [kVqPlanes][vq_cap] pending copies (Deliver::d_vq)
+    uint8_t* vpc;              // Deliver::d_vpc (nullptr: every pending copy is a queue entry)
+    int64_t vpe;               // records per plane of vpc (T * E)
     uint32_t* vqn;
     int64_t vq_cap;
     Cells cs;                  // the seen-set cells (gsim_internal.h)
@@ -340,9 +349,11 @@ __device__ __forceinline__ void atomic_inc_capped(double* p, double cap)
 __device__ __forceinline__ void vq_push(const RoundArgs& a, int64_t c, uint32_t e, int32_t t, uint32_t kind)
 {
     const int pl = (int)(c & (kVqPlanes - 1));
-    const uint32_t k = atomicAdd(&a.vqn[pl], 1u);
-    if ((int64_t)k >= a.vq_cap) { atomicOr(&a.vqn[kVqPlanes], 1u); return; }
-    a.vq[(int64_t)pl * a.vq_cap + k] = (uint64_t)e | ((uint64_t)(uint32_t)t << 32) | ((uint64_t)kind << 40);
+    const int sub = (int)((blockIdx.x + (threadIdx.x >> 6)) % kVqSub);
+    const int64_t scap = a.vq_cap / kVqSub;
+    const uint32_t k = atomicAdd(&a.vqn[vq_ctr(pl, sub)], 1u);
+    if ((int64_t)k >= scap) { atomicOr(&a.vqn[kVqOver], 1u); return; }
+    a.vq[(int64_t)pl * a.vq_cap + sub * scap + k] = (uint64_t)e | ((uint64_t)(uint32_t)t << 32) | ((uint64_t)kind << 40);
 }
 
 // vq_push for a whole wave from convergent code: lane entries with pl >= 0
@@ -350,18 +361,20 @@ __device__ __forceinline__ void vq_push(const RoundArgs& a, int64_t c, uint32_t 
 __device__ __forceinline__ void vq_push_wave(const RoundArgs& a, int pl, uint64_t v)
 {
     const int lane = threadIdx.x & 63;
+    const int sub = (int)((blockIdx.x * 16u + (threadIdx.x >> 6)) % kVqSub);
+    const int64_t scap = a.vq_cap / kVqSub;
     uint64_t pending = __ballot(pl >= 0);
     while (pending) {
         const int leader = __builtin_ctzll(pending);
         const int lpl = __shfl(pl, leader, 64);
         const uint64_t grp = __ballot(pl == lpl) & pending;
         uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&a.vqn[lpl], (uint32_t)__popcll(grp));
+        if (lane == leader) base = atomicAdd(&a.vqn[vq_ctr(lpl, sub)], (uint32_t)__popcll(grp));
         base = (uint32_t)__shfl((int)base, leader, 64);
         if (pl == lpl) {
             const uint32_t k = base + (uint32_t)__popcll(grp & ((1ull << lane) - 1));
-            if ((int64_t)k < a.vq_cap) a.vq[(int64_t)lpl * a.vq_cap + k] = v;
-            else atomicOr(&a.vqn[kVqPlanes], 1u);
+            if ((int64_t)k < scap) a.vq[(int64_t)lpl * a.vq_cap + sub * scap + k] = v;
+            else atomicOr(&a.vqn[kVqOver], 1u);
         }
         pending &= ~grp;
     }
@@ -1073,8 +1086,19 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             if (L && seeable && (seen_round < 0 || seen_round > a.g)) {
                                 // the receiver is still validating: drec.peers (score.go:806-809)
                                 if (scored_t && (pen || !inv)) {
-                                    qpl[u] = (int)((seen_round < 0 ? a.g + L : seen_round) & (kVqPlanes - 1));
-                                    qv[u] = vq_entry(e, t, pen ? kVqInv : kVqDup);
+                                    const int pl = (int)((seen_round < 0 ? a.g + L : seen_round) & (kVqPlanes - 1));
+                                    // dense layout: a count on the record (this block's alone,
+                                    // as mcnt), else / when full a queue entry
+                                    bool counted = false;
+                                    if (a.vpc) {
+                                        uint8_t* cp = a.vpc + ((int64_t)(pen ? kVqPlanes : 0) + pl) * a.vpe + pv[u] + e;
+                                        const uint8_t x = *cp;
+                                        if (x < 255u) { *cp = (uint8_t)(x + 1u); counted = true; }
+                                    }
+                                    if (!counted) {
+                                        qpl[u] = pl;
+                                        qv[u] = vq_entry(e, t, pen ? kVqInv : kVqDup);
+                                    }
                                 }
                                 continue;
                             }
@@ -2038,10 +2062,12 @@ __global__ __launch_bounds__(256) void k_promise_check(uint32_t* prom_q, Cells c
 // queue order does not matter.
 __global__ __launch_bounds__(256) void k_vq_apply(RoundArgs a, int pl)
 {
-    const uint32_t n = (uint32_t)min((int64_t)a.vqn[pl], a.vq_cap);
-    const uint64_t* q = a.vq + (int64_t)pl * a.vq_cap;
+    const int64_t scap = a.vq_cap / kVqSub;
+    const int sub = (int)blockIdx.y;                       // one sub-list per grid row
+    const uint64_t* q = a.vq + (int64_t)pl * a.vq_cap + sub * scap;
+    const int64_t n = min((int64_t)a.vqn[vq_ctr(pl, sub)], scap);
     const ctp_t tpa = const_tp(a.tp);
-    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t v = q[x];
         const uint32_t e = (uint32_t)v, kind = (uint32_t)(v >> 40);
         const int32_t t = (int32_t)((v >> 32) & 0xFFu);
@@ -2055,6 +2081,41 @@ __global__ __launch_bounds__(256) void k_vq_apply(RoundArgs a, int pl)
         // only markFirstMessageDelivery's P2 part
         if (kind == kVqFirst) atomic_inc_capped(&a.first[ir], tp->first_message_deliveries_cap);
         else if (a.tflags[ir] & GSIM_TF_IN_MESH) atomic_inc_capped(&a.meshd[ir], tp->mesh_message_deliveries_cap);
+    }
+}
+
+// The counted pending copies of completion plane pl (dense layout, Deliver::
+// d_vpc): per record, its invalid deliveries (markInvalidMessageDelivery, one
+// +1 each) and, if in the mesh now, its duplicates (meshMessageDeliveries +1
+// capped each) — the same +1 steps k_vq_apply makes for queue entries; the
+// counts are cleared.  One thread per 8 records.
+__global__ __launch_bounds__(256) void k_vq_counts(RoundArgs a, int pl)
+{
+    uint64_t* dw = reinterpret_cast<uint64_t*>(a.vpc + (int64_t)pl * a.vpe);
+    uint64_t* iw = reinterpret_cast<uint64_t*>(a.vpc + (int64_t)(kVqPlanes + pl) * a.vpe);
+    const int64_t nw = a.vpe >> 3;
+    const ctp_t tpa = const_tp(a.tp);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
+        const uint64_t dv = dw[w], iv = iw[w];
+        if (!(dv | iv)) continue;
+        dw[w] = 0;
+        iw[w] = 0;
+        for (int b = 0; b < 8; ++b) {
+            const uint32_t nd = (uint32_t)(dv >> (8 * b)) & 0xFFu, ni = (uint32_t)(iv >> (8 * b)) & 0xFFu;
+            if (!(nd | ni)) continue;
+            const int64_t ir = w * 8 + b;
+            const int32_t t = (int32_t)(ir / a.E);
+            const int64_t e = ir - (int64_t)t * a.E;
+            if (!(a.dstate[e] & GSIM_DS_TRACKED)) continue;
+            if (ni) {
+                double x = a.invalid[ir];
+                for (uint32_t k = 0; k < ni; ++k) x = x + 1.0;
+                a.invalid[ir] = x;
+            }
+            if (nd && (a.tflags[ir] & GSIM_TF_IN_MESH))
+                a.meshd[ir] = apply_incs(a.meshd[ir], nd, (tpa + t)->mesh_message_deliveries_cap);
+        }
     }
 }
 
@@ -2096,14 +2157,22 @@ __global__ __launch_bounds__(256) void k_vcomplete(RoundArgs a, const uint32_t* 
         const uint64_t b = __ballot(done);
         if (!b) continue;
         const bool acc = a.minv[m] == GSIM_VERDICT_ACCEPT;
-        if (done && acc) atomicMax(a.lastput + (int64_t)a.mtopic[m] * a.N + i, tick);   // mcache.Put
+        if (done && acc) {                                // mcache.Put (this thread's peer alone)
+            int32_t* lp = a.lastput + (int64_t)a.mtopic[m] * a.N + i;
+            if (*lp < tick) *lp = tick;
+        }
         if (lane == 0) {
-            atomicMax(&a.slot_last[m], (int32_t)a.g);
+            // slot-wide flags: every wave with a completion would hit the same
+            // word; an atomic only while it still lacks the value
+            if (__hip_atomic_load(&a.slot_last[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int32_t)a.g)
+                atomicMax(&a.slot_last[m], (int32_t)a.g);
             if (acc) {
                 atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (i0 >> 6)), b);
                 atomicOr(reinterpret_cast<unsigned long long*>(a.fsum + (int64_t)m * a.nsw + (i0 >> 12)),
                          1ull << ((i0 >> 6) & 63));
-                atomicOr(&a.nnew_cur[m >> 5], 1u << (m & 31));   // round g + 1 walks the slot
+                uint32_t* nn = a.nnew_cur + (m >> 5);
+                if (!((__hip_atomic_load(nn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (m & 31)) & 1u))
+                    atomicOr(nn, 1u << (m & 31));        // round g + 1 walks the slot
             }
         }
     }
@@ -2134,7 +2203,7 @@ static void dl_free(Deliver* d)
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_peertx); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
-    f(d->d_mlat); f(d->d_vq); f(d->d_vqn); f(d->d_hist);
+    f(d->d_mlat); f(d->d_vq); f(d->d_vqn); f(d->d_hist); f(d->d_vpc);
     f(d->d_cbase); f(d->d_mbits); f(d->d_mpre); f(d->d_pslot);
     delete d;
 }
@@ -2215,6 +2284,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.mlat = d->lat_on ? d->d_mlat : nullptr;
     a.mlat_w = d->d_mlat;
     a.vq = d->d_vq; a.vqn = d->d_vqn; a.vq_cap = d->vq_cap;
+    a.vpc = d->d_vpc; a.vpe = d->d_vpc ? (((int64_t)std::max(1, h->t) * h->e + 7) & ~(int64_t)7) : 0;
     a.cs = deliver_cells(d); a.lastput = d->d_lastput;
     a.CN = h->n;
     a.rlo = (uint32_t)h->olo();
@@ -2517,7 +2587,7 @@ static int vq_check(gsim_handle* h)
     Deliver* d = h->dl;
     if (!d->lat_on) return GSIM_OK;
     uint32_t ov = 0;
-    hipError_t e = hipMemcpyAsync(&ov, d->d_vqn + kVqPlanes, sizeof(ov), hipMemcpyDeviceToHost, h->stream);
+    hipError_t e = hipMemcpyAsync(&ov, d->d_vqn + kVqOver, sizeof(ov), hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return hip_check(h, e, "validation queue flag");
     if (ov) { h->err = "copies pending validation overflowed their queue (raise gsim_msg_config.max_arrivals)"; return GSIM_ERANGE; }
@@ -2691,8 +2761,11 @@ int deliver_round_prepare(gsim_handle* h, int64_t round)
         ProfScope ps(h, GSIM_K_COMMIT);
         RoundArgs a = make_round_args(h, round);
         const int pl = (int)(round & (kVqPlanes - 1));
-        hipLaunchKernelGGL(k_vq_apply, dim3(1024), dim3(256), 0, h->stream, a, pl);
-        hipError_t e = hipMemsetAsync(d->d_vqn + pl, 0, sizeof(uint32_t), h->stream);
+        hipLaunchKernelGGL(k_vq_apply, dim3(128, kVqSub), dim3(256), 0, h->stream, a, pl);
+        if (d->d_vpc)
+            hipLaunchKernelGGL(k_vq_counts, dim3((uint32_t)std::min<int64_t>((a.vpe / 8 + 255) / 256, 16384)), dim3(256),
+                               0, h->stream, a, pl);
+        hipError_t e = hipMemsetAsync(d->d_vqn + vq_ctr(pl, 0), 0, sizeof(uint32_t) * kVqSub * kVqStride, h->stream);
         if (e == hipSuccess) e = hipGetLastError();
         rc = hip_check(h, e, "k_vq_apply");
     }
@@ -3382,11 +3455,20 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
         // (each plane holds the copies of at most GSIM_MAX_VDELAY rounds;
         // gsim_msg_config.max_arrivals raises it)
         const int w = nnew_words(d);
-        d->vq_cap = std::max<int64_t>(std::max<int64_t>(4 * h->e, 1 << 16), d->cfg.max_arrivals);
+        // dense layout (every peer holds every topic's records, no slot relayout):
+        // the copies k_send_tm makes pending are counted per record, the queue
+        // keeps the winners' P2, the IWANT responses and counts that overflow
+        const bool counts = h->smask.empty() && !h->sh;
+        const size_t vpe = ((size_t)std::max(1, h->t) * (size_t)h->e + 7) & ~(size_t)7;
+        d->vq_cap = counts ? std::max<int64_t>(std::max<int64_t>(4 * h->n, 1 << 16), d->cfg.max_arrivals)
+                           : std::max<int64_t>(std::max<int64_t>(4 * h->e, 1 << 16), d->cfg.max_arrivals);
+        d->vq_cap = (d->vq_cap / kVqSub + 1) * kVqSub * 2;     // sub-lists of twice the average share
         e = hipMalloc((void**)&d->d_vq, sizeof(uint64_t) * (size_t)kVqPlanes * (size_t)d->vq_cap);
-        if (e == hipSuccess) e = hipMalloc((void**)&d->d_vqn, sizeof(uint32_t) * (kVqPlanes + 1));
+        if (e == hipSuccess && counts) e = hipMalloc((void**)&d->d_vpc, 2 * (size_t)kVqPlanes * vpe);
+        if (e == hipSuccess && counts) e = hipMemsetAsync(d->d_vpc, 0, 2 * (size_t)kVqPlanes * vpe, h->stream);
+        if (e == hipSuccess) e = hipMalloc((void**)&d->d_vqn, sizeof(uint32_t) * (size_t)kVqnWords);
         if (e == hipSuccess) e = hipMalloc((void**)&d->d_hist, sizeof(uint32_t) * (size_t)kVqPlanes * (size_t)w);
-        if (e == hipSuccess) e = hipMemsetAsync(d->d_vqn, 0, sizeof(uint32_t) * (kVqPlanes + 1), h->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(d->d_vqn, 0, sizeof(uint32_t) * (size_t)kVqnWords, h->stream);
         if (e == hipSuccess) e = hipMemsetAsync(d->d_hist, 0, sizeof(uint32_t) * (size_t)kVqPlanes * (size_t)w, h->stream);
         if (e != hipSuccess) return hip_check(h, e, "validation queues");
         d->lat_on = true;
