@@ -62,6 +62,7 @@ __device__ __forceinline__ bool verdict_penalises(uint8_t v)
 }
 constexpr int kSlotBatch = 8;      // active slots whose cells are loaded together
 constexpr int kClSub = 64;
+constexpr int kClStride = 32;       // u32s between two claim sub-list counters (own cache lines)
 constexpr int kHubMesh = 16;       // mesh | direct edges listed per (hub, topic); more: the whole row is walked
 constexpr uint32_t kHubList = 0x80000000u;   // k_send_tm s_beg flag: an offset into the hub lists         // claim sub-lists (block % kClSub): spreads the append atomics
 
@@ -117,7 +118,8 @@ struct Deliver {
     // claim list (member-compacted cells): the cells a round claimed, so the
     // commit touches those alone instead of every (active slot, peer word)
     uint64_t* d_clist = nullptr;       // [kClSub][clist_cap] receiver | slot << 32, in sub-lists
-    uint32_t* d_clist_n = nullptr;     // [kClSub] entries, [kClSub] overflow (the commit then scans every word)
+    uint32_t* d_clist_n = nullptr;     // [kClSub] entries, [kClSub] overflow (the commit then scans every word);
+                                       // counter q at q * kClStride (one cache line each)
     int64_t clist_cap = 0;             // per sub-list
     uint64_t* d_seenbm = nullptr;      // [ring][ceil(N/64)] bit: the cell is committed (a cache of the cells)
     uint64_t* d_fresh = nullptr;       // [ring][ceil(N/64)] bit: the peer forwards the slot's message next round
@@ -394,12 +396,12 @@ __device__ __forceinline__ void clist_push_wave(const RoundArgs& a, bool on, uin
     const int lane = threadIdx.x & 63, leader = __builtin_ctzll(b);
     const uint32_t q = blockIdx.x % kClSub;
     uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(&a.clist_n[q], (uint32_t)__popcll(b));
+    if (lane == leader) base = atomicAdd(&a.clist_n[q * kClStride], (uint32_t)__popcll(b));
     base = (uint32_t)__shfl((int)base, leader, 64);
     if (on) {
         const uint32_t k = base + (uint32_t)__popcll(b & ((1ull << lane) - 1));
         if ((int64_t)k < a.clist_cap) a.clist[(int64_t)q * a.clist_cap + k] = v;
-        else atomicOr(&a.clist_n[kClSub], 1u);
+        else atomicOr(&a.clist_n[kClSub * kClStride], 1u);
     }
 }
 
@@ -1181,7 +1183,7 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
 {
     extern __shared__ uint16_t s_act[];
     __shared__ int s_n;
-    if (a.clist && !a.clist_n[kClSub]) return;           // the claim list covers the round (k_commit_list)
+    if (a.clist && !a.clist_n[kClSub * kClStride]) return;   // the claim list covers the round (k_commit_list)
     const int nact = active_slots(a.nnew_cur, a.ring, s_act, &s_n);
     const int lane = threadIdx.x & 63;
     // claims exist only at receivers' cells: the words of [rlo, rhi)
@@ -1240,9 +1242,9 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
 template <bool SP>
 __global__ __launch_bounds__(256) void k_commit_list(RoundArgs a)
 {
-    if (a.clist_n[kClSub]) return;
+    if (a.clist_n[kClSub * kClStride]) return;
     const uint32_t q = blockIdx.y;                       // sub-list
-    const int64_t n = (int64_t)a.clist_n[q];
+    const int64_t n = (int64_t)a.clist_n[q * kClStride];
     const uint32_t par = (uint32_t)(a.g & 1);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
@@ -1980,9 +1982,9 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
                 atomicOr(&s_new2[m >> 5], 1u << (m & 31));
                 if (a.clist) {
                     const uint32_t sq = blockIdx.x % kClSub;
-                    const uint32_t q = atomicAdd(&a.clist_n[sq], 1u);
+                    const uint32_t q = atomicAdd(&a.clist_n[sq * kClStride], 1u);
                     if ((int64_t)q < a.clist_cap) a.clist[(int64_t)sq * a.clist_cap + q] = (uint64_t)p | ((uint64_t)m << 32);
-                    else atomicOr(&a.clist_n[kClSub], 1u);
+                    else atomicOr(&a.clist_n[kClSub * kClStride], 1u);
                 }
             }
         }
@@ -2573,7 +2575,7 @@ int deliver_flush(gsim_handle* h)
     const int64_t committed = d->pending;
     d->pending = -1;
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess && a.clist) e = hipMemsetAsync(d->d_clist_n, 0, (kClSub + 1) * sizeof(uint32_t), h->stream);
+    if (e == hipSuccess && a.clist) e = hipMemsetAsync(d->d_clist_n, 0, (kClSub + 1) * kClStride * sizeof(uint32_t), h->stream);
     const int rc = hip_check(h, e, "k_commit");
     return rc ? rc : gater_fold(h, committed, a.now);    // the round's gater events, claims resolved
 }
@@ -3278,8 +3280,8 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
         // deliveries; more overflow into k_commit's word scan
         d->clist_cap = std::max<int64_t>(2 * (int64_t)N, 1 << 20) / kClSub;
         A((void**)&d->d_clist, (size_t)d->clist_cap * kClSub * 8);
-        A((void**)&d->d_clist_n, (kClSub + 1) * 4);
-        if (e == hipSuccess) e = hipMemsetAsync(d->d_clist_n, 0, (kClSub + 1) * 4, h->stream);
+        A((void**)&d->d_clist_n, (kClSub + 1) * kClStride * 4);
+        if (e == hipSuccess) e = hipMemsetAsync(d->d_clist_n, 0, (kClSub + 1) * kClStride * 4, h->stream);
     }
     if (h->max_degree > 64 && e == hipSuccess) {
         // hub rows and their mesh lists (k_hub_mesh)
