@@ -3014,19 +3014,23 @@ __global__ __launch_bounds__(256) void k_frontier_import(RoundArgs a, const uint
             if (!((__hip_atomic_load(nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (m & 31)) & 1u))
                 atomicOr(nw, 1u << (m & 31));
         }
-        if (ghost && (lane == 63 || mn != m)) {
-            if (__hip_atomic_load(&a.slot_last[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int32_t)(a.g - 1))
-                atomicMax(&a.slot_last[m], (int32_t)(a.g - 1));
+        // (push: the entries of a tick carry their own rounds; pull: all g - 1)
+        if (ghost && (a.push || lane == 63 || mn != m)) {
+            const int32_t fr = a.push ? (int32_t)(uint32_t)((in[x] >> 24) & kG24) : (int32_t)(a.g - 1);
+            if (__hip_atomic_load(&a.slot_last[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < fr)
+                atomicMax(&a.slot_last[m], fr);
         }
     }
 }
 
-int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32_t* d_cnt, int64_t cap)
+int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32_t* d_cnt, int64_t cap, bool append)
 {
     Deliver* d = h->dl;
     RoundArgs a = make_round_args(h, round);
-    hipError_t e = hipMemsetAsync(d_cnt, 0, sizeof(uint32_t), h->stream);
-    if (e != hipSuccess) return hip_check(h, e, "frontier count");
+    if (!append) {
+        hipError_t e = hipMemsetAsync(d_cnt, 0, sizeof(uint32_t), h->stream);
+        if (e != hipSuccess) return hip_check(h, e, "frontier count");
+    }
     if (round == 0) return GSIM_OK;
     const int64_t words = ((h->ohi() + 63) >> 6) - (h->olo() >> 6);
     const int64_t items = words * (int64_t)d->cfg.ring;      // an upper bound: the active slots are on the device

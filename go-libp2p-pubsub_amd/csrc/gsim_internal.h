@@ -193,6 +193,7 @@ struct ShardCtx {
     uint64_t* d_fout = nullptr;            // owned forwarders of the round (k_frontier_export)
     uint32_t* d_fcnt = nullptr;
     int64_t fcap = 0;
+    int64_t fpend = 0;                     // push: entries accumulated since the last flush (one per tick)
     uint64_t* d_fin = nullptr;             // every other shard's forwarders
     int64_t fin_cap = 0;
     // control exchange
@@ -546,7 +547,8 @@ int deliver_round_ihave(gsim_handle* h, int64_t round);
 int deliver_round_validate(gsim_handle* h, int64_t round);
 void deliver_round_end(gsim_handle* h, int64_t round);
 int32_t* deliver_slot_last(gsim_handle* h);           // [ring]
-int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32_t* d_cnt, int64_t cap);
+int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32_t* d_cnt, int64_t cap,
+                            bool append = false);
 int deliver_frontier_import(gsim_handle* h, int64_t round, const uint64_t* in, int64_t n);
 void deliver_blocks_changed(gsim_handle* h);          // gsim_set_kernel_variant(h, 6, v)
 // gater.hip: the peer gater (gsim_set_peer_gater)

@@ -986,17 +986,22 @@ int exchange_router_delta(gsim_group* g)
 
 // Round `round`'s forwarders: every shard's owned ones (one list) to every
 // shard they have connections into, which imports its ghosts among them.
-int exchange_frontier(gsim_group* g, int64_t round)
+// Push: only IHAVE reads a ghost's holder round, and the entries carry it, so
+// the rounds' exports accumulate and go out once per tick (flush: the round
+// whose IHAVE follows), one exchange instead of one per round.
+int exchange_frontier(gsim_group* g, int64_t round, bool flush)
 {
     const size_t L = g->hs.size();
     const int K = g->K;
+    const bool push = L > 0 && g->hs[0]->sh->push;
     std::vector<std::vector<uint64_t>> scnt(L, std::vector<uint64_t>((size_t)K, 0)), rcnt;
     for (size_t l = 0; l < L; ++l) {
         gsim_handle* h = g->hs[l];
         ShardCtx* s = h->sh;
         (void)hipSetDevice(h->device);
+        const int64_t prev = push ? s->fpend : 0;
         for (int attempt = 0; attempt < 2; ++attempt) {
-            int rc = g->take(h, deliver_frontier_export(h, round, s->d_fout, s->d_fcnt, s->fcap));
+            int rc = g->take(h, deliver_frontier_export(h, round, s->d_fout, s->d_fcnt, s->fcap, push));
             if (rc) return rc;
             if (hipMemcpyAsync(s->h_counts, s->d_fcnt, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
                 hipStreamSynchronize(h->stream) != hipSuccess)
@@ -1004,17 +1009,27 @@ int exchange_frontier(gsim_group* g, int64_t round)
             const int64_t need = s->h_counts[0];
             if (need <= s->fcap) break;
             if (attempt) return g->fail(GSIM_ERANGE, "frontier export overflow");
-            // a busier round than any before: grow the list and export again
-            // (the export only reads the round's state)
-            (void)hipFree(s->d_fout);
+            // a busier round (or tick) than any before: grow the list, keep the
+            // entries accumulated before this round and export it again (the
+            // export only reads the round's state)
+            uint64_t* old = s->d_fout;
             s->d_fout = nullptr;
-            s->fcap = need + need / 2;
-            rc = g->take(h, dalloc(h, &s->d_fout, (size_t)s->fcap));
+            const int64_t cap = need + need / 2;
+            rc = g->take(h, dalloc(h, &s->d_fout, (size_t)cap));
             if (rc) return rc;
+            if (prev && hipMemcpy(s->d_fout, old, sizeof(uint64_t) * (size_t)prev, hipMemcpyDeviceToDevice) != hipSuccess)
+                return g->fail(GSIM_EDEVICE, "frontier list grow");
+            (void)hipFree(old);
+            s->fcap = cap;
+            const uint32_t pv = (uint32_t)prev;
+            if (hipMemcpy(s->d_fcnt, &pv, sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess)
+                return g->fail(GSIM_EDEVICE, "frontier count");
         }
+        s->fpend = s->h_counts[0];
         for (int d = 0; d < K; ++d)
-            scnt[l][(size_t)d] = (d == g->ids[l] || !s->xto[(size_t)d]) ? 0 : s->h_counts[0];
+            scnt[l][(size_t)d] = (d == g->ids[l] || !s->xto[(size_t)d]) ? 0 : (uint64_t)s->fpend;
     }
+    if (push && !flush) return GSIM_OK;
     int rc = g->take_tr(g->tr->exchange_counts(scnt, rcnt));
     if (rc) return rc;
     std::vector<std::vector<const void*>> sp(L, std::vector<const void*>((size_t)K, nullptr));
@@ -1048,6 +1063,11 @@ int exchange_frontier(gsim_group* g, int64_t round)
         ProfScope ps(h, GSIM_K_SEND);
         rc = g->take(h, deliver_frontier_import(h, round, h->sh->d_fin, total[l]));
         if (rc) return rc;
+        if (push) {                                   // the next tick accumulates afresh
+            if (hipMemsetAsync(h->sh->d_fcnt, 0, sizeof(uint32_t), h->stream) != hipSuccess)
+                return g->fail(GSIM_EDEVICE, "frontier count");
+            h->sh->fpend = 0;
+        }
     }
     return GSIM_OK;
 }
@@ -1460,6 +1480,8 @@ int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg)
         if (s->d_fout) { (void)hipFree(s->d_fout); s->d_fout = nullptr; }
         A(&s->d_fout, (size_t)s->fcap);
         if (!s->d_fcnt) A(&s->d_fcnt, 1);
+        if (!rc && hipMemset(s->d_fcnt, 0, sizeof(uint32_t)) != hipSuccess) return g->fail(GSIM_EDEVICE, "frontier count");
+        s->fpend = 0;
         if (!s->d_cout) {
             A(&s->d_cout, (size_t)(K * s->ccap));
             A(&s->d_ccnt, (size_t)K);
@@ -1638,7 +1660,7 @@ int gsim_group_round(gsim_group* g, int64_t round)
         if (rc) return g->take(h, rc);
         g->settle(h);
     }
-    rc = exchange_frontier(g, round);                // the ghosts among them
+    rc = exchange_frontier(g, round, round % g->rounds == 0);   // the ghosts among them (push: once per tick)
     if (rc) return rc;
     for (gsim_handle* h : g->hs) {
         (void)hipSetDevice(h->device);
