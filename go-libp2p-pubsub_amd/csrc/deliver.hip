@@ -1928,7 +1928,11 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
         const uint32_t r = (uint32_t)ent, m = (uint32_t)(ent >> 32);
         const uint8_t ds = a.dstate[r];
         if (!(ds & GSIM_DS_ACCEPT)) { n_gray++; continue; }        // AcceptFrom
-        const uint32_t p = a.col[r], i = owner[r];
+        const uint32_t p = a.col[r];
+        // the sender (row owner) is read only where it matters: topic slots,
+        // the gater, the trace, a claim (most copies are plain duplicates)
+        const bool need_i = a.smask || a.gt.act || a.tr.on(p);
+        uint32_t i = need_i ? owner[r] : 0xFFFFFFFFu;
         if (a.gt.act && !gater_accept(a, p, r, m, i)) continue;   // the peer gater (gater_accept)
         if (a.subdyn && !((a.sub[p] >> (int32_t)a.mtopic[m]) & 1ull)) continue;   // a topic p left
         if (a.gt.act) gater_copy(a, r, a.minv[m] == GSIM_VERDICT_SIGNATURE);
@@ -1970,6 +1974,7 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
             else if (((hi >> 30) & 1u) != par) seen_round = a.g - 1 + L;
         }
         if (vd != GSIM_VERDICT_SIGNATURE && seen_round < 0 && (c == kUnseen64 || (hi & kEdgeMask) > r)) {
+            if (!need_i) i = owner[r];
             uint32_t lo = i;
             if (sc && !inv) {
                 lo |= kCreditFirst;
