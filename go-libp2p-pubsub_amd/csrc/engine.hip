@@ -97,16 +97,21 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
                 if (x != inval) { inval = x; a.invalid[i] = x; }
                 if (fl & GSIM_TF_IN_MESH) {
                     mt = a.now - a.graft[i];
-                    a.mtime[i] = mt;
+                    // lazy meshTime: derived from graftTime and
+                    // this refresh's clock where it is read (lazy_mtime)
+                    if (!a.mt_lazy || mt < 0) a.mtime[i] = mt;
                     if (mt > tp->mesh_message_deliveries_activation_ns && !(fl & GSIM_TF_ACTIVE)) {
                         fl |= GSIM_TF_ACTIVE;
                         a.tflags[i] = fl;
                     }
-                } else {
-                    a.mtime[i] = 0;   // unobservable outside the mesh
+                } else if (!a.mt_lazy) {
+                    // 0 outside the mesh, unobservable there; in
+                    // lazy mode every exit from the mesh stored the 0 itself
+                    a.mtime[i] = 0;
                 }
             } else if (SCORE && (fl & GSIM_TF_IN_MESH)) {
-                mt = a.mtime[i];
+                const int64_t g = conn && a.mt_lazy ? a.graft[i] : INT64_MAX;
+                mt = g <= a.mt_R ? a.mt_R - g : a.mtime[i];
             }
             if (SCORE) {
                 double ts = 0.0;
@@ -250,6 +255,30 @@ __global__ __launch_bounds__(256) void k_apply_mcnt(ScoreArgs a)
         if (t < 0) continue;
         a.meshd[x] = apply_incs(a.meshd[x], n, const_tp(a.tp)[t].mesh_message_deliveries_cap);
         a.mcnt[x] = 0;
+    }
+}
+
+// Store every lazy meshTime (lazy_mtime): the records the refresh pass
+// rewrites (tracked, connected, owned, scored topics) get R - graftTime in the
+// mesh and 0 outside it, the others keep what they hold.
+__global__ __launch_bounds__(256) void k_mtime_materialize(ScoreArgs a)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
+        if (a.sharded) {
+            const uint32_t o = a.col[e];
+            if (o < a.olo || o >= a.ohi) continue;
+        }
+        const uint8_t st = a.estate[e];
+        if ((st & (GSIM_ES_TRACKED | GSIM_ES_CONNECTED)) != (GSIM_ES_TRACKED | GSIM_ES_CONNECTED)) continue;
+        const uint64_t mj = smask_of(a.smask, a.owner[e]);
+        for (int32_t t = 0; t < a.T; ++t) {
+            if (!const_tp(a.tp)[t].scored || !slot_has(mj, t)) continue;
+            const int64_t i = slot_idx(mj, t, a.E, e);
+            const int64_t old = a.mtime[i];
+            const int64_t v = (a.tflags[i] & GSIM_TF_IN_MESH) ? lazy_mtime(1, a.mt_R, a.graft[i], old) : 0;
+            if (v != old) a.mtime[i] = v;
+        }
     }
 }
 
@@ -597,6 +626,8 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     a.mflags = h->d_mflags; a.rstate = h->d_rstate; a.rev = h->d_rev;
     a.bp = h->d_bp; a.pen = h->d_pen; a.estate = h->d_estate; a.expire = h->d_expire; a.p6 = h->d_p6; a.score = h->d_score;
     a.now = now;
+    a.mt_lazy = h->mt_lazy ? 1 : 0;
+    a.mt_R = h->mt_R;
     a.purged = h->d_flags;
     a.sharded = h->sh ? 1 : 0;
     a.olo = (uint32_t)h->olo();
@@ -663,10 +694,14 @@ int launch_refresh_scores(gsim_handle* h, int64_t now)
         if (rc) return rc;
         ScoreArgs b = a;
         b.gate = h->d_flags + 1;
+        b.mt_lazy = 1;       // meshTime as the pass above left it
+        b.mt_R = now;
         launch_score_kernel<false, true>(h, b);
     } else {
         launch_score_kernel<true, true>(h, a);
     }
+    h->mt_lazy = true;
+    h->mt_R = now;
     h->mcnt_dirty = false;   // the score pass settled every pending count
     h->score_version++;
     return hip_check(h, hipGetLastError(), "k_refresh_score");
@@ -705,6 +740,16 @@ int materialize_mcnt(gsim_handle* h)
     hipLaunchKernelGGL(k_apply_mcnt, dim3(grid_for(h->e * (int64_t)std::max(1, h->S))), dim3(256), 0, h->stream, a);
     h->mcnt_dirty = false;
     return hip_check(h, hipGetLastError(), "k_apply_mcnt");
+}
+
+int materialize_mtime(gsim_handle* h, bool leave)
+{
+    if (!h->mt_lazy) return GSIM_OK;
+    ScoreArgs a = make_score_args(h, 0);
+    hipLaunchKernelGGL(k_mtime_materialize, dim3(grid_for(h->e)), dim3(256), 0, h->stream, a);
+    // (a read may stay lazy: the stored values are the derived ones)
+    if (leave) h->mt_lazy = false;
+    return hip_check(h, hipGetLastError(), "k_mtime_materialize");
 }
 
 // Grow the topic slot masks to cover need[]: every topic
@@ -1175,6 +1220,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     h->p6_dirty = true;
     h->maybe_retained = false;
     h->mcnt_dirty = false;
+    h->mt_lazy = false;
     h->unjoined_zero = true;     // all state zero
     int rc2 = alloc_extra(h);
     if (rc2) return rc2;
@@ -1260,6 +1306,7 @@ int gsim_set_topic_params(gsim_handle* h, int32_t t, const gsim_topic_score_para
     if (h->validate && p->scored && gsim_validate_topic_params(p, buf, sizeof buf)) { h->err = buf; return GSIM_EINVAL; }
     int rcf = deliver_flush(h);
     if (!rcf) rcf = materialize_mcnt(h);   // pending increments saw the old cap
+    if (!rcf) rcf = materialize_mtime(h, true);   // the records the refresh rewrites may change
     if (rcf) return rcf;
     const gsim_topic_score_params old = h->tp[t];
     h->tp[t] = *p;
@@ -1309,6 +1356,7 @@ int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now, double p_mes
     if (rcf) return rcf;
     ScoreArgs a = make_score_args(h, now);
     hipLaunchKernelGGL(k_fill_synthetic, dim3(grid_for(h->e)), dim3(256), 0, h->stream, a, seed, p_mesh);
+    h->mt_lazy = false;          // the fill stores meshTime
     h->p6_dirty = true;
     h->score_version++;
     h->mesh_version++;
@@ -1397,6 +1445,7 @@ int gsim_read_field(gsim_handle* h, int32_t f, void* dst, size_t bytes)
     if (r.kind == FK_SEEN) return deliver_read_seen(h, dst);
     int rc = deliver_flush(h);
     if (!rc) rc = materialize_mcnt(h);
+    if (!rc && f == GSIM_F_MESH_TIME) rc = materialize_mtime(h, false);
     if (rc) return rc;
     return read_field_impl(h, r, dst);
 }
@@ -1411,6 +1460,7 @@ int gsim_write_field(gsim_handle* h, int32_t f, const void* src, size_t bytes)
     if (r.kind == FK_SEEN) { h->err = "the seen-set is read-only"; return GSIM_EINVAL; }
     int rc = deliver_flush(h);
     if (!rc) rc = materialize_mcnt(h);
+    if (!rc) rc = materialize_mtime(h, true);   // arbitrary state: meshTime is stored again
     // fanout state lives in the publisher's topic slots
     if (!rc && f == GSIM_F_FANOUT_TOPICS) rc = ensure_slots(h, (const uint64_t*)src);
     if (rc) return rc;

@@ -34,6 +34,8 @@ struct ScoreArgs {
     const double* p6;
     double* score;
     int64_t now;
+    int32_t mt_lazy;           // lazy meshTime (lazy_mtime): in-mesh records were not stored at the last refresh
+    int64_t mt_R;              // ... whose time this is
     int32_t* purged;
     const uint64_t* sub;       // announced topics per peer (fill: records only where both endpoints joined)
     const int32_t* gate;       // non-null: run only if *gate != 0 (a retention purge happened)
@@ -95,6 +97,18 @@ __device__ __forceinline__ int64_t div_trunc_pos(int64_t n, int64_t d)
 __device__ __forceinline__ int64_t go_div(int64_t n, int64_t d)
 {
     return d > 0 ? div_trunc_pos(n, d) : n / d;
+}
+
+// meshTime of an in-mesh record of a connected, tracked peer in a scored
+// topic — the records refreshScores rewrites (score.go:550-556) — once the
+// engine stopped storing it (lazy meshTime): the last refresh
+// at R left R - graftTime there, and a Graft since then (graftTime >= R)
+// stored 0 itself.  Stored values stay authoritative until the first refresh
+// (lazy = 0) and for a graft time after R (Graft's 0, or a refresh that met a
+// graft time in the future and stored its negative meshTime).
+__device__ __forceinline__ int64_t lazy_mtime(int32_t lazy, int64_t R, int64_t graft, int64_t stored)
+{
+    return lazy && graft <= R ? R - graft : stored;
 }
 
 // Topic slots.  Every per-(topic, edge index) array — score
@@ -405,6 +419,8 @@ struct gsim_handle {
     uint8_t* d_mcnt = nullptr;        // pending meshd increments (apply_incs)
     bool mcnt_dirty = false;
     int64_t *d_graft = nullptr, *d_mtime = nullptr;
+    bool mt_lazy = false;             // lazy meshTime since the refresh at mt_R (lazy_mtime)
+    int64_t mt_R = 0;
     uint8_t* d_tflags = nullptr;      // GSIM_TF_IN_MESH | GSIM_TF_ACTIVE
     // device: router state [T][E] / [E], edge (observer) order
     uint8_t* d_mflags = nullptr;      // GSIM_TF_MESH: gs.mesh[topic] membership
@@ -452,6 +468,10 @@ int launch_refresh_scores(gsim_handle* h, int64_t now);
 int launch_compute_scores(gsim_handle* h);
 int refresh_accept(gsim_handle* h);   // recompute d_dstate if the snapshot changed
 int materialize_mcnt(gsim_handle* h); // apply pending meshd increments everywhere
+// store every lazy meshTime (lazy_mtime) — before meshTime is read out — and
+// with leave, end lazy mode: before state is written through the ABI, topic
+// parameters change or the clock runs backwards
+int materialize_mtime(gsim_handle* h, bool leave);
 // grow the topic slot masks to cover need[N] (a host array; the topic arrays are re-laid out)
 int ensure_slots(gsim_handle* h, const uint64_t* need);
 uint8_t** extra_ctl_slot(gsim_handle* h);        // heartbeat.hip: the [2][S][E] control inbox

@@ -60,6 +60,8 @@ struct HbArgs {
     double *meshd, *fail, *bp;
     const uint8_t* mcnt;
     int64_t *graft, *mtime;
+    int32_t mt_lazy;    // lazy meshTime since the refresh at mt_R (lazy_mtime)
+    int64_t mt_R;
     uint8_t* ctl_in;    // inbox this phase reads (round parity)
     uint8_t* ctl_out;   // inbox this phase writes
     uint64_t* cany_in;  // [N] topics with pending control per receiver (ctl_in), cleared when handled
@@ -285,6 +287,7 @@ __device__ __forceinline__ void stats_prune(const HbArgs& a, bool tracked, bool 
             a.fail[sf.ir] = a.fail[sf.ir] + deficit * deficit;
         }
     }
+    if (fl & GSIM_TF_IN_MESH) a.mtime[sf.ir] = 0;   // meshTime outside the mesh is 0
     fl &= (uint8_t)~GSIM_TF_IN_MESH;
 }
 
@@ -295,7 +298,10 @@ constexpr int kScoreChunk = 2;   // topics whose record fields are loaded togeth
 
 __device__ double score_of_record(const HbArgs& a, uint32_t rv, uint32_t col)
 {
-    if (!(a.estate[rv] & GSIM_ES_TRACKED)) return 0.0;
+    const uint8_t st = a.estate[rv];
+    if (!(st & GSIM_ES_TRACKED)) return 0.0;
+    // lazy meshTime (lazy_mtime): the graft times are loaded instead
+    const int64_t* mts = a.mt_lazy ? a.graft : a.mtime;
     const uint64_t mj = smask_of(a.smask, col);      // the records sit in col's row
     double score = 0.0;
     for (int32_t t0 = 0; t0 < a.T; t0 += kScoreChunk) {
@@ -315,7 +321,7 @@ __device__ double score_of_record(const HbArgs& a, uint32_t rv, uint32_t col)
             md[j] = ok ? a.meshd[i] : 0.0;
             fa[j] = ok ? a.fail[i] : 0.0;
             iv[j] = ok ? a.invalid[i] : 0.0;
-            mt[j] = ok ? a.mtime[i] : 0;
+            mt[j] = ok ? mts[i] : 0;
         }
         for (int j = 0; j < kScoreChunk; ++j) {
             const int32_t t = t0 + j;
@@ -325,6 +331,9 @@ __device__ double score_of_record(const HbArgs& a, uint32_t rv, uint32_t col)
             const double meshd = apply_incs(md[j], mc[j], tp->mesh_message_deliveries_cap);
             double ts = 0.0;
             if (fl[j] & GSIM_TF_IN_MESH) {                                // P1
+                if (a.mt_lazy)
+                    mt[j] = (st & GSIM_ES_CONNECTED) && mt[j] <= a.mt_R ? a.mt_R - mt[j]
+                                                                       : a.mtime[slot_idx(mj, t, a.E, rv)];
                 double p1 = 0.0;
                 if (tp->time_in_mesh_quantum_ns != 0) p1 = (double)go_div(mt[j], tp->time_in_mesh_quantum_ns);
                 if (p1 > tp->time_in_mesh_cap) p1 = tp->time_in_mesh_cap;
@@ -1052,7 +1061,7 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
 // rows: the observers of one row-length class (a list), or nullptr for the
 // nrows observers from obs_base on.
 template <int W>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))   // W = 16: keep 3 waves per SIMD
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W == 16 ? 3 : 4)))   // W = 16: 3 waves per SIMD, else 4
 void k_heartbeat(HbArgs a, const uint32_t* rows, int64_t nrows, int64_t obs_base)
 {
     constexpr int G = 64 / W;
@@ -1692,7 +1701,9 @@ __global__ __launch_bounds__(256) void k_snapshot(HbArgs a, int64_t e_lo, int64_
             gsim_topic_score_snapshot q{};
             if (tracked && slot_has(mj, t)) {
                 const uint8_t fl = a.tflags[i];
-                q.time_in_mesh_ns = (fl & GSIM_TF_IN_MESH) ? a.mtime[i] : 0;
+                q.time_in_mesh_ns = !(fl & GSIM_TF_IN_MESH) ? 0
+                                    : lazy_mtime(a.mt_lazy && (a.estate[rv] & GSIM_ES_CONNECTED), a.mt_R, a.graft[i],
+                                                 a.mtime[i]);
                 q.first_message_deliveries = a.first[i];
                 q.mesh_message_deliveries =
                     apply_incs(a.meshd[i], a.mcnt[i], const_tp(a.tp)[t].mesh_message_deliveries_cap);
@@ -1926,6 +1937,7 @@ __global__ __launch_bounds__(256) void k_churn_apply(HbArgs a, ChurnArgs c)
             const double deficit = thr - a.meshd[i];
             a.fail[i] = a.fail[i] + deficit * deficit;
         }
+        if (fl & GSIM_TF_IN_MESH) a.mtime[i] = 0;   // meshTime outside the mesh is 0
         a.tflags[i] = (uint8_t)(fl & ~GSIM_TF_IN_MESH);
     }
     c.estate[r] = GSIM_ES_TRACKED;
@@ -2157,6 +2169,11 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.outbound = h->d_outbound; a.direct = h->d_direct; a.estate = h->d_estate; a.score = h->d_score; a.tp = h->d_tp;
     a.tflags = h->d_tflags; a.mflags = h->d_mflags; a.rstate = h->d_rstate; a.backoff = h->d_backoff; a.meshd = h->d_meshd; a.fail = h->d_fail; a.bp = h->d_bp;
     a.graft = h->d_graft; a.mtime = h->d_mtime; a.mcnt = h->d_mcnt;
+    // a Graft before the last refresh's time would read as older than it is
+    // (lazy_mtime): a clock that runs backwards stores meshTime again
+    if (h->mt_lazy && now < h->mt_R) (void)materialize_mtime(h, true);
+    a.mt_lazy = h->mt_lazy ? 1 : 0;
+    a.mt_R = h->mt_R;
     const size_t TE = (size_t)h->e * (size_t)std::max(1, h->S);
     a.ctl_in = h->x->d_ctl + (size_t)(parity_in & 1) * TE;
     a.ctl_out = h->x->d_ctl + (size_t)((parity_in + 1) & 1) * TE;
@@ -2372,7 +2389,7 @@ int gsim_read_snapshot(gsim_handle* h, int64_t obs_lo, int64_t obs_hi, gsim_peer
     e = hipMalloc((void**)&dp, sizeof(*dp) * (size_t)ne);
     if (e == hipSuccess) e = hipMalloc((void**)&dt, sizeof(*dt) * (size_t)(ne * T));
     if (e == hipSuccess) {
-        HbArgs a = make_hb_args(h, 0, 0, 0);
+        HbArgs a = make_hb_args(h, 0, h->mt_R, 0);   // (no clock read; the last refresh's keeps meshTime lazy)
         hipLaunchKernelGGL(k_snapshot, dim3((uint32_t)std::min<int64_t>((ne + 255) / 256, 16384)), dim3(256), 0,
                            h->stream, a, (int64_t)rp[0], (int64_t)rp[1], dp, dt);
         e = hipGetLastError();

@@ -215,6 +215,8 @@ void orc_prune(orc_net* s, int64_t e, int32_t topic)
         double deficit = thr - s->meshd[i];
         s->fail[i] += deficit * deficit;
     }
+    /* meshTime outside the mesh is never read; normalized to 0 */
+    if (s->tflags[i] & TF_IN_MESH) s->mesh_time[i] = 0;
     s->tflags[i] &= (uint8_t)~TF_IN_MESH;
 }
 
@@ -260,6 +262,7 @@ void orc_remove_peer(orc_net* s, int64_t e, int64_t now)
             double deficit = thr - s->meshd[i];
             s->fail[i] += deficit * deficit;
         }
+        if (s->tflags[i] & TF_IN_MESH) s->mesh_time[i] = 0;   /* as in orc_prune */
         s->tflags[i] &= (uint8_t)~TF_IN_MESH;
     }
     s->estate[e] = ES_TRACKED;                      /* connected = false */

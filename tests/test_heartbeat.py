@@ -253,6 +253,63 @@ def test_heartbeat_and_control_bit_exact(require_gpu, n, k, T, p_mesh, ticks):
     eng.close()
 
 
+@pytest.mark.gpu
+def test_lazy_mesh_time_unread_ticks(require_gpu):
+    """Lazy meshTime (DESIGN.md §3.8): the refresh no longer stores meshTime;
+    scores, PRUNE freezes, churn and the read-out derive it from graftTime and
+    the last refresh's clock.  Several ticks with churn and no read in between,
+    then a heartbeat whose clock runs backwards, must leave every array (the
+    scores included) bit-exact against the oracle, which stores it."""
+    n, k, T = 1000, 24, 2
+    rng = np.random.default_rng(77)
+    params = beacon_params(T)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2, OpportunisticGraftTicks=60)
+    th = PeerScoreThresholds(GossipThreshold=-100, PublishThreshold=-200, GraylistThreshold=-300,
+                             OpportunisticGraftThreshold=3.0)
+    net = random_regular(n, k, seed=n, n_topics=T)
+    p5 = np.where(rng.random(n) < 0.08, -50.0, np.round(rng.normal(0, 3, n)))
+    st = ob.NetState(net, params, thresholds=th, gossip=gp, p5=p5)
+    randomize_state(st, rng, tick_time(0), retained_frac=0.0)
+    _random_mesh_state(st, rng, 0.55)
+    eng = Engine(params, th, gossip=gp)
+    eng.load_graph(net)
+    eng.set_app_score(p5)
+    eng.set_seed(SEED)
+    st.push_to_engine(eng)
+    src = net.owner()
+    und = np.nonzero(src < net.col)[0]
+    down = np.stack([src[und], net.col[und]], 1)[rng.random(len(und)) < 0.03].astype(np.uint32)
+    lib = ob.load()
+    try:
+        for kk in range(58, 64):
+            now = tick_time(kk)
+            if kk == 60:
+                eng.set_connections(down, up=False, now=now - HB // 2)
+                st.churn(down, up=False, now=now - HB // 2)
+            if kk == 62:
+                eng.set_connections(down, up=True, now=now - HB // 2)
+                st.churn(down, up=True, now=now - HB // 2)
+            eng.refresh_scores(now)
+            eng.heartbeat(kk, now)
+            eng.handle_control(0, now + HB // 11)
+            eng.handle_control(1, now + 2 * HB // 11)
+            run_tick_oracle(st, kk)
+        # the clock runs backwards: a heartbeat before the last refresh's time
+        back = tick_time(63) - 3 * HB
+        eng.heartbeat(64, back)
+        eng.handle_control(0, back + HB // 11)
+        lib.orc_heartbeat(st.view(), 64, back, SEED)
+        lib.orc_handle_control(st.view(), 0, back + HB // 11)
+        eng.compute_scores()
+        lib.orc_compute_scores(st.view())
+        gpu = ob.NetState(net, params, thresholds=th, gossip=gp, p5=p5)
+        gpu.pull_from_engine(eng)
+        assert_same(st, gpu)
+        assert ((st.tflags & _abi.TF_IN_MESH) != 0).any() and (st.mesh_time > 0).any()
+    finally:
+        eng.close()
+
+
 def _go_dout_keep(plst, outbound, D, Dout):
     """gossipsub.go:1457-1488 verbatim: returns plst[:D] after the rotation."""
     plst = list(plst)
