@@ -240,6 +240,20 @@ __device__ bool select_smallest(const HbArgs& a, bool cand, int count, uint32_t 
     return sel;
 }
 
+// The kernel arguments re-read per topic: every pointer of HbArgs hoisted out
+// of the topic loop would otherwise stay live in SGPRs across it, and the
+// excess spills to VGPR lanes (v_readlane per use).  The opaque pointer keeps
+// the scalar loads (constant address space, K$ hits) inside the loop.
+// Only for kernels whose first parameter is the HbArgs (k_heartbeat,
+// k_heartbeat_hub): it is read at the start of the kernarg segment.
+__device__ __forceinline__ const HbArgs& hb_launder(const HbArgs&)
+{
+    using CP = const __attribute__((address_space(4))) HbArgs*;
+    CP p = (CP)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const HbArgs*)p;
+}
+
 // The score bits of one (observer, neighbour, topic) record, loaded on first
 // use: Graft/Prune are rare, and the record lives at rev[e] (record order,
 // DESIGN.md §2), away from the observer's row.
@@ -296,8 +310,9 @@ __device__ __forceinline__ void stats_prune(const HbArgs& a, bool tracked, bool 
 // Graft/Prune changed the record (gossipsub.go:1734).
 constexpr int kScoreChunk = 2;   // topics whose record fields are loaded together
 
-__device__ double score_of_record(const HbArgs& a, uint32_t rv, uint32_t col)
+__device__ double score_of_record(const HbArgs& a_, uint32_t rv, uint32_t col)
 {
+    const HbArgs& a = hb_launder(a_);
     const uint8_t st = a.estate[rv];
     if (!(st & GSIM_ES_TRACKED)) return 0.0;
     // lazy meshTime (lazy_mtime): the graft times are loaded instead
@@ -693,8 +708,9 @@ struct BlockGroup {
 // the group, shuffles of the group's own lanes; BlockGroup: LDS).  Branches
 // diverge only between whole groups.
 template <class Grp>
-__device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs, bool ovalid)
+__device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t obs, bool ovalid)
 {
+        const HbArgs& a = a_;
         constexpr int V = Grp::V;
         const uint32_t b = ovalid ? a.row_ptr[obs] : 0u;
         const int deg = ovalid ? (int)(a.row_ptr[obs + 1] - b) : 0;
@@ -775,6 +791,7 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
             const int32_t t = t0 + j;
             if (t >= a.T) break;
             if (!((subi >> t) & 1ull)) continue;           // not joined
+            const HbArgs& a = hb_launder(a_);
             const ctp_t tp = const_tp(a.tp) + t;
             const bool scored = tp->scored != 0;
             const double thr = tp->mesh_message_deliveries_threshold;
@@ -997,6 +1014,8 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
                 sf[v].store(a);
                 if (bo_dirty[v]) a.backoff[i[v]] = bo[v];
             }
+          {
+            const HbArgs& a = hb_launder(a_);   // (the mesh maintenance's pointers are dead here)
             // the delivery's mesh mask of this row and topic (mesh or direct
             // edges to this shard's peers)
             if constexpr (Grp::kRowMask) {
@@ -1042,6 +1061,7 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a, Grp& g, int64_t obs
                 pxc[v] = (ctl[v] & GSIM_CTL_PX) != 0;
             }
             if (a.do_px && g.any(pxc)) pxt |= 1ull << t;
+          }
           }
         }
         // sendGraftPrune follows every topic: k_px_emit picks the PX peers
