@@ -721,8 +721,9 @@ constexpr int kTmTabMin = 256;      // forwarders in a chunk from which the tabl
 // SP: topic slots or member-compacted cells are in use (gsim_internal.h); the
 // dense instance indexes plane t and cell m * N + p with no table reads.
 template <int kTmThreads, bool LAT, bool SP, bool GT = false, bool PUSH = false>
-__global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs a)
+__global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs a_)
 {
+    const RoundArgs& a = a_;
     extern __shared__ uint64_t s_dyn[];
     uint16_t* s_slots = reinterpret_cast<uint16_t*>(s_dyn);  // [ring] active slots of topic t
     constexpr int kTmChunk = 2 * kTmThreads;                 // peers per chunk (two per thread)
@@ -835,6 +836,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
             }
             bool first_layer = true;
             for (;;) {
+                const RoundArgs& a = kernarg0(a_);   // (re-read per layer: SGPR pressure)
                 const uint32_t fb = (pm[0] ? 1u : 0u) | (pm[1] ? 2u : 0u);
                 uint32_t len2[2] = {0, 0}, beg2[2] = {0, 0}, from2[2] = {0, 0}, k2[2] = {0, 0}, pl2[2] = {0, 0};
                 uint64_t msk2[2] = {0, 0};
@@ -935,6 +937,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                         __syncthreads();
                     }
                     for (uint32_t it0 = w0; it0 < w1; it0 += kPerIt) {
+                        const RoundArgs& a = kernarg0(a_);   // (re-read per iteration: SGPR pressure)
                         uint32_t jv[P], fv[P], ev[P], iv[P], nv[P], kv[P];
                         int64_t pv[P];           // the sender's plane of topic t
                         uint8_t mfv[P], dsv[P], tfv[P];
@@ -1495,8 +1498,9 @@ __global__ __launch_bounds__(256) void k_gossip_count_mm(IhArgs a, const uint32_
 }
 
 template <int W, bool LAT, bool SP, bool MM = false>
-__global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
+__global__ __launch_bounds__(256) void k_ihave(IhArgs a_, const uint32_t* gcount)
 {
+    const IhArgs& a = a_;
     extern __shared__ uint16_t s_act[];   // [ring] candidate slots (bit 15: push), then response staging
     __shared__ int s_n;
     if (a.nresp[3] & 4u) return;          // a truncation may apply: k_ihave_pairs
@@ -1565,6 +1569,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a, const uint32_t* gcount)
         }
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
+            const IhArgs& a = kernarg0(a_);   // (re-read per slot: SGPR pressure)
             const int k = k0 + b;
             if (k >= nact) break;                            // wave-uniform
             const uint32_t m = s_act[k] & 0x7FFF;
@@ -1908,9 +1913,10 @@ __device__ __forceinline__ void atomic_mcnt_inc(uint8_t* mcnt, int64_t ir, doubl
 // handleIWant, and a shard's copies pushed by other shards (shard.hip).  Same
 // rules and tracer events as k_send_tm's copies; a record can receive several
 // copies in one launch, so counters are updated atomically.
-__global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint64_t* resp, const uint32_t* nresp,
+__global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a_, const uint64_t* resp, const uint32_t* nresp,
                                                        const uint32_t* owner, int64_t resp_cap)
 {
+    const RoundArgs& a = a_;
     extern __shared__ uint32_t s_new2[];
     __shared__ unsigned long long s_stats[4];
     for (int w = threadIdx.x; w < (a.ring + 31) / 32; w += blockDim.x) s_new2[w] = 0;
@@ -1924,6 +1930,7 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a, const uint6
     const ctp_t tpa = const_tp(a.tp);
     unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
     for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) {
+        const RoundArgs& a = kernarg0(a_);   // (re-read per copy: SGPR pressure)
         const uint64_t ent = resp[x];
         const uint32_t r = (uint32_t)ent, m = (uint32_t)(ent >> 32);
         const uint8_t ds = a.dstate[r];

@@ -99,6 +99,20 @@ __device__ __forceinline__ int64_t go_div(int64_t n, int64_t d)
     return d > 0 ? div_trunc_pos(n, d) : n / d;
 }
 
+// A kernel's first argument re-read from the kernarg segment behind an opaque
+// pointer: loads of its fields stay where they are used (scalar loads, K$
+// hits) instead of being hoisted out of the loops, where dozens of live
+// pointers overflow the SGPRs and spill to VGPR lanes (a v_readlane per use).
+// Only valid in a kernel whose FIRST parameter is the A passed.
+template <class A>
+__device__ __forceinline__ const A& kernarg0(const A&)
+{
+    using CP = const __attribute__((address_space(4))) A*;
+    CP p = (CP)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const A*)p;
+}
+
 // meshTime of an in-mesh record of a connected, tracked peer in a scored
 // topic — the records refreshScores rewrites (score.go:550-556) — once the
 // engine stopped storing it (lazy meshTime): the last refresh

@@ -1233,8 +1233,9 @@ __global__ __launch_bounds__(B) void k_fanout_heartbeat_hub(HbArgs a, const uint
 // The control records of one (receiver, topic) are usually few, so they are
 // walked with a wave-uniform loop over the set bits of a ballot; the mesh size
 // is carried in a scalar.
-__global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
+__global__ __launch_bounds__(256) void k_handle_control(HbArgs a_)
 {
+    const HbArgs& a = a_;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (int64_t rcv = a.olo + (int64_t)blockIdx.x * 4 + wid; rcv < a.ohi; rcv += (int64_t)gridDim.x * 4) {
         // topics whose inbox planes may hold entries for this receiver: the
@@ -1255,6 +1256,7 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a)
             const int32_t t = t0 + j;
             if (t >= a.T) break;
             if (!((any >> t) & 1ull) || !slot_has(mr, t)) continue;
+            const HbArgs& a = hb_launder(a_);   // (re-read per topic: SGPR pressure)
             const bool joined = (subr >> t) & 1ull;
             const ctp_t tp = const_tp(a.tp) + t;
             const bool scored = tp->scored != 0;
