@@ -515,6 +515,18 @@ def main():
                                           "requests_per_launch": rq["requests_per_launch"],
                                           "kernel": rq["kernel"], "kernel_ms_per_launch": send_launch_ms,
                                           "source": rq["source"], "ceiling_source": rq["ceiling_source"]}
+        # the heartbeat's bound: VALU issue (PMC SQ_INSTS_VALU per launch of k_heartbeat<32>) over
+        # the heartbeat class's time per tick (it also holds k_fanout_heartbeat: a slight under-estimate)
+        hv = None if args.vdelay or sharded else load_traffic(args.config + ":hb_valu")
+        roof_hb = None
+        if hv is not None and kms.get("heartbeat"):
+            ach = hv["valu_insts_per_launch"] / (kms["heartbeat"] * 1e-3)
+            roof_hb = {"bound": "valu_issue", "achieved": ach, "peak": hv["peak_wave_insts_per_s"],
+                       "unit": "wave-instructions/s", "frac": ach / hv["peak_wave_insts_per_s"],
+                       "valu_insts_per_launch": hv["valu_insts_per_launch"],
+                       "valu_insts_per_peer_topic": hv["valu_insts_per_launch"] / (n * T),
+                       "kernel": hv["kernel"] + " (+ k_fanout_heartbeat in kernel_ms)", "kernel_ms": kms["heartbeat"],
+                       "source": hv["source"], "peak_source": hv["peak_source"]}
         dominant = roof_refresh if ref_ms * launches["refresh_score"] / K >= deliv_ms else roof_deliv
         out = {
             "metric": "peer-heartbeat updates/sec + msg-edge deliveries/sec, 1M-peer gossipsub sim",
@@ -550,7 +562,8 @@ def main():
             "gossip_per_tick": {k: (gossip1[k] - gossip0[k]) / K for k in gossip1},
             "census": census1,
             "roofline": dominant,
-            "roofline_kernels": {"refresh_score": roof_refresh, "delivery": roof_deliv},
+            "roofline_kernels": {"refresh_score": roof_refresh, "delivery": roof_deliv,
+                                 **({"heartbeat": roof_hb} if roof_hb else {})},
         }
         if not args.no_cpu_baseline and world == 1 and not args.vdelay:
             # (the oracle baseline publishes without latency: not the same workload as a --vdelay line)
