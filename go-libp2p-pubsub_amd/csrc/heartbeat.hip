@@ -1209,13 +1209,14 @@ __device__ __forceinline__ void fanout_observer(const HbArgs& a, Grp& g, int64_t
 
 // Fanout expiry and maintenance, one wave per observer of at most 64
 // connections; observers without fanout state leave after two loads.
-__global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a)
+__global__ __launch_bounds__(256) void k_fanout_heartbeat(HbArgs a_)
 {
+    const HbArgs& a = a_;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     WaveGroup<64> g(lane);
     for (int64_t obs = a.olo + (int64_t)blockIdx.x * 4 + wid; obs < a.ohi; obs += (int64_t)gridDim.x * 4) {
         if (a.row_ptr[obs + 1] - a.row_ptr[obs] > 64u) continue;    // a hub: k_fanout_heartbeat_hub
-        fanout_observer(a, g, obs);
+        fanout_observer(hb_launder(a_), g, obs);   // (re-read per observer: SGPR pressure)
     }
 }
 
@@ -1437,9 +1438,10 @@ __device__ __forceinline__ void wave_lds_sync()
 // <kPxRow, 4> walks the owned observers with rows of at most kPxRow,
 // <4 kPxRow, 1> the hub list `rows` (rows of kPxRow+1 .. 4 kPxRow).
 template <int ROW, int WV>
-__global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a, int live, uint32_t key_tick, uint32_t purpose,
+__global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32_t key_tick, uint32_t purpose,
                                                      const uint32_t* rows, int64_t nrows)
 {
+    const HbArgs& a = a_;
     __shared__ double s_sc[WV][ROW];
     __shared__ uint64_t s_key[WV][ROW];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1462,6 +1464,7 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a, int live, uint32_
         }
         wave_lds_sync();
         for (uint64_t tm = mask; tm; tm &= tm - 1) {
+            const HbArgs& a = hb_launder(a_);   // (re-read per topic: SGPR pressure)
             const int32_t t = __ffsll((long long)tm) - 1;
             for (int p0 = 0; p0 < deg; p0 += 64) {
                 const uint32_t ep_l = b + (uint32_t)(p0 + lane);
