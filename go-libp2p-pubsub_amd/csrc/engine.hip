@@ -32,11 +32,13 @@ using namespace gsim;
 // reference's, compiled with -ffp-contract=off: results are bit-identical to
 // the CPU oracle.
 template <bool REFRESH, bool SCORE>
-__global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a)
+__global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a_)
 {
-    if (a.gate && *a.gate == 0) return;
+    const ScoreArgs& a0 = a_;
+    if (a0.gate && *a0.gate == 0) return;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a0.E; e += stride) {
+        const ScoreArgs& a = kernarg0(a_);   // (re-read per record: SGPR pressure)
         if (a.sharded) {   // a record of a ghost observer belongs to another shard
             const uint32_t o = a.col[e];
             if (o < a.olo || o >= a.ohi) continue;
