@@ -37,6 +37,7 @@ sys.path.insert(0, os.path.join(REPO, "go-libp2p-pubsub_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 SECOND = 1_000_000_000
+SALU_PEAK = 256 * 2.4e9       # scalar instructions/s: one scalar unit per CU
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 ROUNDS = 10                    # propagation rounds per heartbeat
 MSG_RATE = 4.0                 # messages / s / topic
@@ -76,11 +77,12 @@ SCENARIOS = {
 def refresh_bytes(census: dict, n_edges: int) -> int:
     """Compulsory HBM bytes of one refreshScores+score pass on this state
     (DESIGN.md §4.1): every connected scored record reads its 4 counters and
-    flags (33 B); in-mesh records also read graftTime and write meshTime
-    (16 B); every non-zero counter changes under decay and is written (8 B);
-    per edge: estate 1, bp r+w 16, P5 gather 8, col 4, P6 8, score write 8."""
+    flags (33 B); in-mesh records also read graftTime (8 B) -- with lazy
+    meshTime the pass no longer stores meshTime; every
+    non-zero counter changes under decay and is written (8 B); per edge:
+    estate 1, bp r+w 16, P5 gather 8, col 4, P6 8, score write 8."""
     nz = census["nz_first"] + census["nz_meshd"] + census["nz_fail"] + census["nz_invalid"]
-    return 33 * census["records"] + 16 * census["in_mesh"] + 8 * nz + 45 * n_edges
+    return 33 * census["records"] + 8 * census["in_mesh"] + 8 * nz + 45 * n_edges
 
 
 def tick_time(k: int) -> int:
@@ -499,7 +501,7 @@ def main():
         tr_send_tick = None
         if tr_send is not None:
             tr_send_tick = tr_send["bytes_per_launch"] * launches["send"] / K
-            tr_send = dict(tr_send, bytes_per_tick=tr_send_tick, covers="k_send_tm only (k_commit not counted)")
+            tr_send = dict(tr_send, bytes_per_tick=tr_send_tick, covers="k_send_tm + k_commit")
         roof_deliv = {"bound": "hbm", "achieved": deliv_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": deliv_gbs / HBM_PEAK_GBS, "traffic": tr_send_tick, "traffic_detail": tr_send,
                       "kernel": "delivery: k_send_tm + k_commit + k_delivery_state (per tick, 10 rounds)", "kernel_ms": deliv_ms,
@@ -510,9 +512,14 @@ def main():
         if rq is not None and launches.get("send"):
             send_launch_ms = kms["send"] * K / launches["send"]
             ach = rq["requests_per_launch"] / (send_launch_ms * 1e-3)
+            copies_per_launch = (firsts + dups) / launches["send"] if launches["send"] else 0
             roof_deliv["request_rate"] = {"bound": "tcc_requests", "achieved": ach, "peak": rq["ceiling_req_per_s"],
                                           "unit": "requests/s", "frac": ach / rq["ceiling_req_per_s"],
                                           "requests_per_launch": rq["requests_per_launch"],
+                                          "requests_per_copy": rq["requests_per_launch"] / max(1, copies_per_launch),
+                                          "l2_hit_rate": rq.get("hit_rate"),
+                                          "l2_misses_per_copy": (rq["tcc_miss"] / max(1, copies_per_launch)
+                                                                 if "tcc_miss" in rq else None),
                                           "kernel": rq["kernel"], "kernel_ms_per_launch": send_launch_ms,
                                           "source": rq["source"], "ceiling_source": rq["ceiling_source"]}
         # the heartbeat's bound: VALU issue (PMC SQ_INSTS_VALU per launch of k_heartbeat<32>) over
@@ -527,6 +534,14 @@ def main():
                        "valu_insts_per_peer_topic": hv["valu_insts_per_launch"] / (n * T),
                        "kernel": hv["kernel"] + " (+ k_fanout_heartbeat in kernel_ms)", "kernel_ms": kms["heartbeat"],
                        "source": hv["source"], "peak_source": hv["peak_source"]}
+            if hv.get("salu_insts_per_launch"):
+                # the scalar unit: one SALU instruction per cycle per CU (shared by its 4 SIMDs)
+                s_ach = hv["salu_insts_per_launch"] / (kms["heartbeat"] * 1e-3)
+                s_peak = SALU_PEAK
+                roof_hb["salu_issue"] = {"bound": "salu_issue", "achieved": s_ach, "peak": s_peak,
+                                         "unit": "instructions/s", "frac": s_ach / s_peak,
+                                         "salu_insts_per_launch": hv["salu_insts_per_launch"],
+                                         "peak_source": "256 CUs x 2.4 GHz, one scalar issue per CU per cycle"}
         dominant = roof_refresh if ref_ms * launches["refresh_score"] / K >= deliv_ms else roof_deliv
         out = {
             "metric": "peer-heartbeat updates/sec + msg-edge deliveries/sec, 1M-peer gossipsub sim",

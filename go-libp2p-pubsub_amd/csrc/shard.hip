@@ -642,6 +642,7 @@ struct gsim_group {
     int32_t ring = 0, rounds = 0;
     bool msgs = false;
     bool router_dirty = true;                 // ghost rows' router state must be re-imported
+    uint32_t xseq = 0;                        // exchanges so far (the tag's sequence part, tagged_counts)
     // GSIM_GROUP_SERIAL=1: each shard's work completes before the next
     // shard's starts (in-process groups on one device: per-shard kernel
     // times as if each shard had the device to itself)
@@ -728,9 +729,56 @@ int sync_all(gsim_group* g)
     return GSIM_OK;
 }
 
+// Exchange kinds, the high part of a count's tag (tagged_counts).
+enum { XK_DENSE = 1, XK_CONTROL, XK_RDELTA, XK_FRONTIER, XK_COPIES, XK_GBASE, XK_PX, XK_PXA };
+constexpr int kCountBits = 48;
+constexpr uint64_t kCountMask = (1ull << kCountBits) - 1;
+
+// The count exchange in front of every payload exchange, with a symmetry
+// check.  Each 64-bit count carries a 16-bit tag in its top bits: the
+// exchange kind and the group's running exchange number.  Every process runs
+// the same sequence of exchanges, so a shard that receives another kind or
+// number -- its peer's control flow went another way -- or a count other
+// than the one it expects (`expect`, when the receiving side knows its size
+// itself, as the dense exchanges do) returns GSIM_ESTATE before any payload
+// moves.  Without the check such a mismatch reaches the payload collective:
+// gloo aborts on the size ("38576 vs 0") and RCCL's ncclRecv
+// waits forever.
+int tagged_counts(gsim_group* g, int kind, const std::vector<std::vector<uint64_t>>& scnt,
+                  std::vector<std::vector<uint64_t>>& rcnt, const std::vector<std::vector<uint64_t>>* expect = nullptr)
+{
+    const uint64_t tag = ((uint64_t)(kind & 0xF) << 12 | (g->xseq & 0xFFF)) << kCountBits;
+    ++g->xseq;
+    std::vector<std::vector<uint64_t>> t = scnt;
+    for (auto& row : t)
+        for (uint64_t& c : row) {
+            if (c > kCountMask) return g->fail(GSIM_ERANGE, "exchange count over 2^48");
+            c |= tag;
+        }
+    int rc = g->take_tr(g->tr->exchange_counts(t, rcnt));
+    if (rc) return rc;
+    for (size_t l = 0; l < rcnt.size(); ++l)
+        for (size_t q = 0; q < rcnt[l].size(); ++q) {
+            const uint64_t got = rcnt[l][q];
+            if ((got & ~kCountMask) != tag)
+                return g->fail(GSIM_ESTATE, "exchange sequence mismatch: shard " + std::to_string(q) + " sent kind " +
+                                                std::to_string((got >> (kCountBits + 12)) & 0xF) + " #" +
+                                                std::to_string((got >> kCountBits) & 0xFFF) + ", shard " +
+                                                std::to_string(g->ids[l]) + " expects kind " + std::to_string(kind) +
+                                                " #" + std::to_string((tag >> kCountBits) & 0xFFF));
+            rcnt[l][q] = got & kCountMask;
+            if (expect && (int)q != g->ids[l] && rcnt[l][q] != (*expect)[l][q])
+                return g->fail(GSIM_ESTATE, "exchange size mismatch: shard " + std::to_string(q) + " sends " +
+                                                std::to_string(rcnt[l][q]) + " B, shard " + std::to_string(g->ids[l]) +
+                                                " expects " + std::to_string((*expect)[l][q]) + " B");
+        }
+    return GSIM_OK;
+}
+
 // A dense exchange over the cross edges: every local shard's cross-out
 // ordered `elem`-byte records (out[l] at xoff) into the other shards' ghost
-// blocks (in[l] at gbase).
+// blocks (in[l] at gbase).  Both sides know the sizes from the layout; the
+// tagged count exchange checks that they agree before the payload moves.
 int exchange_dense(gsim_group* g, const std::vector<const void*>& out, const std::vector<void*>& in, size_t elem)
 {
     const size_t L = g->hs.size();
@@ -746,7 +794,11 @@ int exchange_dense(gsim_group* g, const std::vector<const void*>& out, const std
             rp[l][(size_t)q] = (uint8_t*)in[l] + (size_t)s->gbase[(size_t)q] * elem;
             rb[l][(size_t)q] = (uint64_t)s->gcnt[(size_t)q] * elem;
         }
+        sb[l][(size_t)g->ids[l]] = rb[l][(size_t)g->ids[l]] = 0;
     }
+    std::vector<std::vector<uint64_t>> rcnt;
+    int rc = tagged_counts(g, XK_DENSE, sb, rcnt, &rb);
+    if (rc) return rc;
     return g->take_tr(g->tr->alltoallv(sp, sb, rp, rb));
 }
 
@@ -782,7 +834,7 @@ int exchange_control(gsim_group* g, int parity)
             scnt[l][(size_t)d] = s->h_counts[d];
         }
     }
-    int rc = g->take_tr(g->tr->exchange_counts(scnt, rcnt));
+    int rc = tagged_counts(g, XK_CONTROL, scnt, rcnt);
     if (rc) return rc;
     std::vector<std::vector<const void*>> sp(L, std::vector<const void*>((size_t)K, nullptr));
     std::vector<std::vector<void*>> rp(L, std::vector<void*>((size_t)K, nullptr));
@@ -919,7 +971,7 @@ int exchange_router_delta(gsim_group* g)
 {
     const size_t L = g->hs.size();
     const int K = g->K;
-    constexpr uint64_t kOver = ~0ull;
+    constexpr uint64_t kOver = kCountMask;
     std::vector<std::vector<uint64_t>> scnt(L, std::vector<uint64_t>((size_t)K, 0)), rcnt;
     for (size_t l = 0; l < L; ++l) {
         gsim_handle* h = g->hs[l];
@@ -932,7 +984,7 @@ int exchange_router_delta(gsim_group* g)
         for (int d = 0; d < K; ++d)
             scnt[l][(size_t)d] = d == g->ids[l] ? 0 : ((int64_t)n > s->rdel_cap ? kOver : n);
     }
-    int rc = g->take_tr(g->tr->exchange_counts(scnt, rcnt));
+    int rc = tagged_counts(g, XK_RDELTA, scnt, rcnt);
     if (rc) return rc;
     bool over = false;
     for (size_t l = 0; l < L; ++l) {
@@ -1030,7 +1082,7 @@ int exchange_frontier(gsim_group* g, int64_t round, bool flush)
             scnt[l][(size_t)d] = (d == g->ids[l] || !s->xto[(size_t)d]) ? 0 : (uint64_t)s->fpend;
     }
     if (push && !flush) return GSIM_OK;
-    int rc = g->take_tr(g->tr->exchange_counts(scnt, rcnt));
+    int rc = tagged_counts(g, XK_FRONTIER, scnt, rcnt);
     if (rc) return rc;
     std::vector<std::vector<const void*>> sp(L, std::vector<const void*>((size_t)K, nullptr));
     std::vector<std::vector<void*>> rp(L, std::vector<void*>((size_t)K, nullptr));
@@ -1106,7 +1158,7 @@ int exchange_copies(gsim_group* g, int64_t round)
         for (int d = 0; d < K; ++d)
             for (int q = 0; q < kXSub; ++q) scnt[l][(size_t)d] += s->h_xcnt[(size_t)(d * kXSub + q) * kXStride];
     }
-    rc = g->take_tr(g->tr->exchange_counts(scnt, rcnt));
+    rc = tagged_counts(g, XK_COPIES, scnt, rcnt);
     if (rc) return rc;
     std::vector<std::vector<const void*>> sp(L, std::vector<const void*>((size_t)K, nullptr));
     std::vector<std::vector<void*>> rp(L, std::vector<void*>((size_t)K, nullptr));
@@ -1420,7 +1472,7 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
         std::vector<std::vector<uint64_t>> sc(Ls, std::vector<uint64_t>((size_t)K, 0)), rcv;
         for (size_t l = 0; l < Ls; ++l)
             for (int q = 0; q < K; ++q) sc[l][(size_t)q] = (uint64_t)g->hs[l]->sh->gbase[(size_t)q];
-        rc = g->take_tr(g->tr->exchange_counts(sc, rcv));
+        rc = tagged_counts(g, XK_GBASE, sc, rcv);
         if (rc) return rc;
         for (size_t l = 0; l < Ls; ++l) {
             gsim_handle* h = g->hs[l];
@@ -1749,7 +1801,7 @@ int gsim_group_px_connect(gsim_group* g, int64_t now, uint32_t* pairs, int64_t c
         if (s->h_counts[K]) return g->fail(GSIM_ERANGE, "PX list overflow");
         for (int d = 0; d < K; ++d) scnt[l][(size_t)d] = d == g->ids[l] ? 0 : s->h_counts[d];
     }
-    int rc = g->take_tr(g->tr->exchange_counts(scnt, rcnt));
+    int rc = tagged_counts(g, XK_PX, scnt, rcnt);
     if (rc) return rc;
     std::vector<std::vector<const void*>> sp(L, std::vector<const void*>((size_t)K, nullptr));
     std::vector<std::vector<void*>> rp(L, std::vector<void*>((size_t)K, nullptr));
@@ -1795,7 +1847,7 @@ int gsim_group_px_connect(gsim_group* g, int64_t now, uint32_t* pairs, int64_t c
             return g->fail(GSIM_EDEVICE, "PX list counts");
         for (int d = 0; d < K; ++d) acnt[l][(size_t)d] = d == g->ids[l] ? 0 : (uint64_t)na;
     }
-    rc = g->take_tr(g->tr->exchange_counts(acnt, rcnt));
+    rc = tagged_counts(g, XK_PXA, acnt, rcnt);
     if (rc) return rc;
     for (size_t l = 0; l < L; ++l) {
         gsim_handle* h = g->hs[l];

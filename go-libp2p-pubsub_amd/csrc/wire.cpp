@@ -235,9 +235,352 @@ std::vector<std::vector<uint32_t>> fragment_ids(const gsim_wire_rpc& r, const st
     return out;
 }
 
+// ---- decoding (rpc.pb.go's generated Unmarshal, restated) ------------------
+
+// A reader over one message's bytes, with the generated code's checks:
+// varints of at most 64 bits, lengths inside the buffer.
+struct Rd {
+    const uint8_t* p;
+    const uint8_t* e;
+    bool ok = true;
+    bool more() const { return ok && p < e; }
+    uint64_t varint()
+    {
+        uint64_t v = 0;
+        for (int s = 0; s < 64; s += 7) {
+            if (p >= e) { ok = false; return 0; }            // io.ErrUnexpectedEOF
+            const uint8_t b = *p++;
+            v |= (uint64_t)(b & 0x7F) << s;
+            if (!(b & 0x80)) return v;
+        }
+        ok = false;                                          // ErrIntOverflow
+        return 0;
+    }
+    // a length-delimited body
+    bool body(const uint8_t** q, uint64_t* n)
+    {
+        const uint64_t L = varint();
+        if (!ok || L > (uint64_t)(e - p)) { ok = false; return false; }   // ErrInvalidLength / EOF
+        *q = p;
+        *n = L;
+        p += L;
+        return true;
+    }
+    // skip<Msg>: an unknown field's value (groups nest; an end-group at depth 0 is an error)
+    bool skip(int wt)
+    {
+        int depth = 0;
+        for (;;) {
+            switch (wt) {
+            case 0: varint(); break;
+            case 1: if (e - p < 8) ok = false; else p += 8; break;
+            case 5: if (e - p < 4) ok = false; else p += 4; break;
+            case 2: { const uint8_t* q; uint64_t n; body(&q, &n); break; }
+            case 3: ++depth; break;
+            case 4: if (depth == 0) ok = false; else --depth; break;   // ErrUnexpectedEndOfGroup
+            default: ok = false;                                       // illegal wireType
+            }
+            if (!ok || depth == 0) return ok;
+            const uint64_t k = varint();                     // the group's next field
+            if (!ok) return false;
+            wt = (int)(k & 7);
+            if ((k >> 3) == 0) { ok = false; return false; }
+        }
+    }
+    // the next field's number and wire type (tag checks of the generated code)
+    bool tag(uint32_t* f, int* wt)
+    {
+        const uint64_t k = varint();
+        if (!ok) return false;
+        *wt = (int)(k & 7);
+        if ((k >> 3) == 0 || (k >> 3) > 0x1FFFFFFFu || *wt == 4) { ok = false; return false; }   // illegal tag
+        *f = (uint32_t)(k >> 3);
+        return true;
+    }
+};
+
+// Two passes over the same bytes: counting (t == nullptr) then filling.
+struct Dec {
+    gsim_wire_tables* t;
+    uint32_t nsubs = 0, nmsgs = 0, nihave = 0, niwant = 0, ngraft = 0, nprune = 0, nids = 0, npx = 0;
+    bool has_control = false;
+
+    static gsim_bytes view(const uint8_t* q, uint64_t n) { return gsim_bytes{q, (uint32_t)n}; }
+
+    // a bytes / string field: present, last occurrence wins
+    static bool bytes_field(Rd& r, int wt, gsim_bytes* out)
+    {
+        if (wt != 2) return false;                           // "wrong wireType"
+        const uint8_t* q;
+        uint64_t n;
+        if (!r.body(&q, &n) || n > 0xFFFFFFFFull) return false;
+        if (out) *out = view(q, n);
+        return true;
+    }
+
+    bool sub(const uint8_t* q, uint64_t n)                   // RPC.SubOpts
+    {
+        gsim_wire_sub x{-1, {nullptr, 0}};
+        Rd r{q, q + n};
+        uint32_t f;
+        int wt;
+        while (r.more()) {
+            if (!r.tag(&f, &wt)) return false;
+            if (f == 1) {
+                if (wt != 0) return false;
+                const uint64_t v = r.varint();
+                x.subscribe = v != 0 ? 1 : 0;
+            } else if (f == 2) {
+                if (!bytes_field(r, wt, &x.topic)) return false;
+            } else if (!r.skip(wt)) {
+                return false;
+            }
+        }
+        if (!r.ok) return false;
+        if (t) t->subs[nsubs] = x;
+        ++nsubs;
+        return true;
+    }
+
+    bool msg(const uint8_t* q, uint64_t n)                   // Message
+    {
+        gsim_wire_msg x{};
+        Rd r{q, q + n};
+        uint32_t f;
+        int wt;
+        while (r.more()) {
+            if (!r.tag(&f, &wt)) return false;
+            gsim_bytes* dst = f == 1 ? &x.from : f == 2 ? &x.data : f == 3 ? &x.seqno : f == 4 ? &x.topic
+                            : f == 5 ? &x.signature : f == 6 ? &x.key : nullptr;
+            if (dst) {
+                if (!bytes_field(r, wt, dst)) return false;
+            } else if (!r.skip(wt)) {
+                return false;
+            }
+        }
+        if (!r.ok) return false;
+        if (t) t->msgs[nmsgs] = x;
+        ++nmsgs;
+        return true;
+    }
+
+    // ControlIHave (id field 2, topic 1) / ControlIWant (id field 1, no topic)
+    bool gossip(const uint8_t* q, uint64_t n, bool ihave)
+    {
+        const uint32_t id_field = ihave ? 2 : 1;
+        gsim_bytes topic{nullptr, 0};
+        const uint32_t id0 = nids;
+        Rd r{q, q + n};
+        uint32_t f;
+        int wt;
+        while (r.more()) {
+            if (!r.tag(&f, &wt)) return false;
+            if (f == id_field) {
+                gsim_bytes b;
+                if (!bytes_field(r, wt, &b)) return false;
+                if (t) t->ids[nids] = b;
+                ++nids;
+            } else if (ihave && f == 1) {
+                if (!bytes_field(r, wt, &topic)) return false;
+            } else if (!r.skip(wt)) {
+                return false;
+            }
+        }
+        if (!r.ok) return false;
+        if (ihave) {
+            if (t) t->ihave[nihave] = gsim_wire_ihave{topic, id0, nids - id0};
+            ++nihave;
+        } else {
+            if (t) t->iwant[niwant] = gsim_wire_iwant{id0, nids - id0};
+            ++niwant;
+        }
+        return true;
+    }
+
+    bool graft(const uint8_t* q, uint64_t n)                 // ControlGraft
+    {
+        gsim_wire_graft x{{nullptr, 0}};
+        Rd r{q, q + n};
+        uint32_t f;
+        int wt;
+        while (r.more()) {
+            if (!r.tag(&f, &wt)) return false;
+            if (f == 1) {
+                if (!bytes_field(r, wt, &x.topic)) return false;
+            } else if (!r.skip(wt)) {
+                return false;
+            }
+        }
+        if (!r.ok) return false;
+        if (t) t->graft[ngraft] = x;
+        ++ngraft;
+        return true;
+    }
+
+    bool peer(const uint8_t* q, uint64_t n)                  // PeerInfo
+    {
+        gsim_wire_px x{};
+        Rd r{q, q + n};
+        uint32_t f;
+        int wt;
+        while (r.more()) {
+            if (!r.tag(&f, &wt)) return false;
+            gsim_bytes* dst = f == 1 ? &x.peer : f == 2 ? &x.record : nullptr;
+            if (dst) {
+                if (!bytes_field(r, wt, dst)) return false;
+            } else if (!r.skip(wt)) {
+                return false;
+            }
+        }
+        if (!r.ok) return false;
+        if (t) t->px[npx] = x;
+        ++npx;
+        return true;
+    }
+
+    bool prune(const uint8_t* q, uint64_t n)                 // ControlPrune
+    {
+        gsim_wire_prune x{{nullptr, 0}, npx, 0, 0, 0};
+        Rd r{q, q + n};
+        uint32_t f;
+        int wt;
+        while (r.more()) {
+            if (!r.tag(&f, &wt)) return false;
+            if (f == 1) {
+                if (!bytes_field(r, wt, &x.topic)) return false;
+            } else if (f == 2) {
+                const uint8_t* b;
+                uint64_t bn;
+                if (wt != 2 || !r.body(&b, &bn) || !peer(b, bn)) return false;
+            } else if (f == 3) {
+                if (wt != 0) return false;
+                x.backoff = r.varint();
+                x.has_backoff = 1;
+            } else if (!r.skip(wt)) {
+                return false;
+            }
+        }
+        if (!r.ok) return false;
+        x.npx = npx - x.px0;
+        if (t) t->prune[nprune] = x;
+        ++nprune;
+        return true;
+    }
+
+    bool control(const uint8_t* q, uint64_t n)               // ControlMessage (merged)
+    {
+        has_control = true;
+        Rd r{q, q + n};
+        uint32_t f;
+        int wt;
+        while (r.more()) {
+            if (!r.tag(&f, &wt)) return false;
+            if (f >= 1 && f <= 4) {
+                const uint8_t* b;
+                uint64_t bn;
+                if (wt != 2 || !r.body(&b, &bn)) return false;
+                const bool ok = f == 1 ? gossip(b, bn, true) : f == 2 ? gossip(b, bn, false)
+                              : f == 3 ? graft(b, bn) : prune(b, bn);
+                if (!ok) return false;
+            } else if (!r.skip(wt)) {
+                return false;
+            }
+        }
+        return r.ok;
+    }
+
+    bool rpc(const uint8_t* q, uint64_t n)                   // RPC
+    {
+        Rd r{q, q + n};
+        uint32_t f;
+        int wt;
+        while (r.more()) {
+            if (!r.tag(&f, &wt)) return false;
+            if (f >= 1 && f <= 3) {
+                const uint8_t* b;
+                uint64_t bn;
+                if (wt != 2 || !r.body(&b, &bn)) return false;
+                const bool ok = f == 1 ? sub(b, bn) : f == 2 ? msg(b, bn) : control(b, bn);
+                if (!ok) return false;
+            } else if (!r.skip(wt)) {
+                return false;
+            }
+        }
+        return r.ok;
+    }
+};
+
 }  // namespace
 
 extern "C" {
+
+int gsim_wire_decode(const uint8_t* in, uint64_t len, gsim_wire_tables* t, gsim_wire_rpc* rpc)
+{
+    if (!rpc || !t || (len && !in)) return GSIM_EINVAL;
+    *rpc = gsim_wire_rpc{};
+    Dec count{nullptr};
+    if (!count.rpc(in, len)) return GSIM_EINVAL;
+    rpc->nsubs = count.nsubs;
+    rpc->nmsgs = count.nmsgs;
+    rpc->nihave = count.nihave;
+    rpc->niwant = count.niwant;
+    rpc->ngraft = count.ngraft;
+    rpc->nprune = count.nprune;
+    rpc->nids = count.nids;
+    rpc->npx = count.npx;
+    rpc->has_control = count.has_control ? 1 : 0;
+    if (count.nsubs > t->subs_cap || count.nmsgs > t->msgs_cap || count.nihave > t->ihave_cap ||
+        count.niwant > t->iwant_cap || count.ngraft > t->graft_cap || count.nprune > t->prune_cap ||
+        count.nids > t->ids_cap || count.npx > t->px_cap)
+        return GSIM_ERANGE;
+    if ((count.nsubs && !t->subs) || (count.nmsgs && !t->msgs) || (count.nihave && !t->ihave) ||
+        (count.niwant && !t->iwant) || (count.ngraft && !t->graft) || (count.nprune && !t->prune) ||
+        (count.nids && !t->ids) || (count.npx && !t->px))
+        return GSIM_EINVAL;
+    Dec fill{t};
+    fill.rpc(in, len);
+    rpc->subs = t->subs;
+    rpc->msgs = t->msgs;
+    rpc->ihave = t->ihave;
+    rpc->iwant = t->iwant;
+    rpc->graft = t->graft;
+    rpc->prune = t->prune;
+    rpc->ids = t->ids;
+    rpc->px = t->px;
+    return GSIM_OK;
+}
+
+int gsim_wire_frames(const uint8_t* in, uint64_t len, uint64_t max_size, uint64_t* off, uint64_t* lens, int32_t cap,
+                     int32_t* n, uint64_t* consumed)
+{
+    if (!n || !consumed || cap < 0 || (cap && (!off || !lens)) || (len && !in)) return GSIM_EINVAL;
+    *n = 0;
+    *consumed = 0;
+    uint64_t pos = 0;
+    while (pos < len) {
+        // msgio's uvarint length prefix
+        uint64_t L = 0, q = pos;
+        int s = 0;
+        bool done = false;
+        while (q < len) {
+            const uint8_t b = in[q++];
+            if (s >= 64 || (s == 63 && b > 1)) return GSIM_EINVAL;   // binary.ErrOverflow
+            L |= (uint64_t)(b & 0x7F) << s;
+            s += 7;
+            if (!(b & 0x80)) { done = true; break; }
+        }
+        if (!done) break;                                    // the prefix is still arriving
+        if (L > max_size) return GSIM_ERANGE;                // msgio.ErrMsgTooLarge
+        if (len - q < L) break;                              // the body is still arriving
+        if (*n >= cap) return GSIM_ERANGE;
+        off[*n] = q;
+        lens[*n] = L;
+        ++*n;
+        pos = q + L;
+        *consumed = pos;
+    }
+    return GSIM_OK;
+}
 
 uint64_t gsim_wire_size(const gsim_wire_rpc* rpc)
 {

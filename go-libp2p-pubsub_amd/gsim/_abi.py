@@ -194,6 +194,13 @@ class CWireRpc(Structure):
                 ("nprune", c_uint32), ("ids", c_void_p), ("nids", c_uint32), ("px", c_void_p), ("npx", c_uint32)]
 
 
+class CWireTables(Structure):
+    _fields_ = [("subs", c_void_p), ("msgs", c_void_p), ("ihave", c_void_p), ("iwant", c_void_p), ("graft", c_void_p),
+                ("prune", c_void_p), ("ids", c_void_p), ("px", c_void_p),
+                ("subs_cap", c_uint32), ("msgs_cap", c_uint32), ("ihave_cap", c_uint32), ("iwant_cap", c_uint32),
+                ("graft_cap", c_uint32), ("prune_cap", c_uint32), ("ids_cap", c_uint32), ("px_cap", c_uint32)]
+
+
 class CWireNames(Structure):
     _fields_ = [("topic_names", c_void_p), ("peer_ids", c_void_p), ("peer_id_len", c_uint32),
                 ("prune_backoff_s", c_uint64)]
@@ -310,6 +317,9 @@ SIGNATURES = [
     ("gsim_group_profile_read", c_int32, [c_void_p, c_void_p, c_void_p, c_int32]),
     # gsim_wire.h
     ("gsim_wire_size", c_uint64, [POINTER(CWireRpc)]),
+    ("gsim_wire_decode", c_int32, [c_void_p, c_uint64, POINTER(CWireTables), POINTER(CWireRpc)]),
+    ("gsim_wire_frames", c_int32, [c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_int32, POINTER(c_int32),
+                                   POINTER(c_uint64)]),
     ("gsim_wire_encode", c_int32, [POINTER(CWireRpc), c_void_p, c_uint64, POINTER(c_uint64)]),
     ("gsim_trace_encode", c_int32, [c_void_p, c_int64, POINTER(CWireNames), ctypes.c_char_p, c_void_p, c_uint64,
                                     POINTER(c_uint64)]),

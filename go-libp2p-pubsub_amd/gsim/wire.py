@@ -200,6 +200,98 @@ def fragment_rpc(rpc: RPC, limit: int) -> List[bytes]:
     return [raw[off[k]:off[k + 1]] for k in range(nf.value)]
 
 
+def _bytes_at(b: _abi.CBytes) -> Optional[bytes]:
+    return None if not b.p else ctypes.string_at(b.p, b.n)
+
+
+def unmarshal(data: bytes) -> RPC:
+    """RPC.Unmarshal (gsim_wire_decode): the RPC encoded in `data`.  Raises
+    WireError (GSIM_EINVAL) for a malformed RPC ("bogus rpc", comm.go:82)."""
+    lib = _abi.load()
+    buf = ctypes.create_string_buffer(bytes(data), max(1, len(data)))
+    t = _abi.CWireTables()
+    r = _abi.CWireRpc()
+    rc = lib.gsim_wire_decode(buf, len(data), ctypes.byref(t), ctypes.byref(r))
+    if rc == _abi.GSIM_ERANGE:                       # the counts needed: size the tables
+        keep = []
+
+        def arr(ct, n, name):
+            a = (ct * max(1, n))()
+            keep.append(a)
+            setattr(t, name, ctypes.addressof(a))
+            setattr(t, name + "_cap", n)
+            return a
+        subs = arr(_abi.CWireSub, r.nsubs, "subs")
+        msgs = arr(_abi.CWireMsg, r.nmsgs, "msgs")
+        ihave = arr(_abi.CWireIHave, r.nihave, "ihave")
+        iwant = arr(_abi.CWireIWant, r.niwant, "iwant")
+        graft = arr(_abi.CWireGraft, r.ngraft, "graft")
+        prune = arr(_abi.CWirePrune, r.nprune, "prune")
+        ids = arr(_abi.CBytes, r.nids, "ids")
+        pxs = arr(_abi.CWirePx, r.npx, "px")
+        rc = lib.gsim_wire_decode(buf, len(data), ctypes.byref(t), ctypes.byref(r))
+    else:
+        subs = msgs = ihave = iwant = graft = prune = ids = pxs = []
+    if rc != 0:
+        raise WireError(rc, "bogus rpc")
+    out = RPC()
+    for k in range(r.nsubs):
+        out.subscriptions.append(SubOpts(None if subs[k].subscribe < 0 else bool(subs[k].subscribe),
+                                         _bytes_at(subs[k].topic)))
+    for k in range(r.nmsgs):
+        m = msgs[k]
+        out.publish.append(Message(*(_bytes_at(getattr(m, f)) for f in ("from_", "data", "seqno", "topic",
+                                                                          "signature", "key"))))
+    if r.has_control:
+        c = ControlMessage()
+        for k in range(r.nihave):
+            g = ihave[k]
+            c.ihave.append(ControlIHave(_bytes_at(g.topic), [_bytes_at(ids[g.id0 + q]) for q in range(g.nid)]))
+        for k in range(r.niwant):
+            g = iwant[k]
+            c.iwant.append(ControlIWant([_bytes_at(ids[g.id0 + q]) for q in range(g.nid)]))
+        for k in range(r.ngraft):
+            c.graft.append(ControlGraft(_bytes_at(graft[k].topic)))
+        for k in range(r.nprune):
+            p = prune[k]
+            c.prune.append(ControlPrune(_bytes_at(p.topic),
+                                        [PeerInfo(_bytes_at(pxs[p.px0 + q].peer), _bytes_at(pxs[p.px0 + q].record))
+                                         for q in range(p.npx)],
+                                        p.backoff if p.has_backoff else None))
+        out.control = c
+    return out
+
+
+def delimited(rpcs) -> bytes:
+    """The varint-delimited stream of encoded RPCs (the sender's msgio varint
+    writer, comm.go)."""
+    out = bytearray()
+    for b in rpcs:
+        n = len(b)
+        while n >= 0x80:
+            out.append((n & 0x7F) | 0x80)
+            n >>= 7
+        out.append(n)
+        out += b
+    return bytes(out)
+
+
+def frames(stream: bytes, max_size: int = 1 << 20):
+    """gsim_wire_frames: the whole frames of a varint-delimited stream
+    (msgio.NewVarintReaderSize(s, maxMessageSize), comm.go:64) and the bytes
+    they use; raises WireError (GSIM_ERANGE) for a frame over max_size."""
+    lib = _abi.load()
+    buf = ctypes.create_string_buffer(bytes(stream), max(1, len(stream)))
+    cap = max(1, len(stream))
+    off = (ctypes.c_uint64 * cap)()
+    ln = (ctypes.c_uint64 * cap)()
+    n, used = ctypes.c_int32(), ctypes.c_uint64()
+    rc = lib.gsim_wire_frames(buf, len(stream), max_size, off, ln, cap, ctypes.byref(n), ctypes.byref(used))
+    if rc != 0:
+        raise WireError(rc, "message too large" if rc == _abi.GSIM_ERANGE else "bad length prefix")
+    return [bytes(stream[off[k]:off[k] + ln[k]]) for k in range(n.value)], used.value
+
+
 def heartbeat_rpcs(engine, tick: int, p0: int, p1: int, topic_names, peer_ids: Optional[np.ndarray] = None,
                    prune_backoff_s: Optional[int] = None):
     """The RPCs senders [p0, p1) sent at heartbeat `tick` (after

@@ -121,6 +121,48 @@ int gsim_wire_encode(const gsim_wire_rpc* rpc, uint8_t* out, uint64_t cap, uint6
 int gsim_wire_fragment(const gsim_wire_rpc* rpc, int64_t limit, uint8_t* out, uint64_t cap, uint64_t* len,
                        uint64_t* off, int32_t max_frags, int32_t* nfrags);
 
+/* ---- decoding: RPC.Unmarshal and the delimited stream --------------------- */
+
+/* Caller-owned tables gsim_wire_decode fills (no allocation crosses the
+ * boundary).  Each pointer has room for its *_cap entries. */
+typedef struct gsim_wire_tables {
+    gsim_wire_sub* subs;
+    gsim_wire_msg* msgs;
+    gsim_wire_ihave* ihave;
+    gsim_wire_iwant* iwant;
+    gsim_wire_graft* graft;
+    gsim_wire_prune* prune;
+    gsim_bytes* ids;
+    gsim_wire_px* px;
+    uint32_t subs_cap, msgs_cap, ihave_cap, iwant_cap, graft_cap, prune_cap, ids_cap, px_cap;
+} gsim_wire_tables;
+
+/* RPC.Unmarshal (rpc.pb.go, gogo-protobuf; called by handleNewStream,
+ * comm.go:66-82): decodes one RPC of len bytes into *rpc, whose tables point
+ * into t and whose byte strings point into `in` (zero copy: keep `in` alive).
+ * Semantics of the generated code: a repeated field appends per occurrence;
+ * an optional scalar or bytes field takes its last occurrence; the optional
+ * ControlMessage merges every occurrence (its lists concatenate in order);
+ * unknown fields (any wire type, groups included) are skipped, not kept
+ * (gogo keeps them in XXX_unrecognized, which nothing on the path reads).
+ * GSIM_EINVAL for a malformed RPC (truncated field, varint overflow, a known
+ * field with the wrong wire type, field number 0, a stray end-group:
+ * "bogus rpc" in the reference) with *rpc zeroed; GSIM_ERANGE when a table
+ * is too small, with rpc's counts set to the entries needed and its table
+ * pointers NULL. */
+int gsim_wire_decode(const uint8_t* in, uint64_t len, gsim_wire_tables* t, gsim_wire_rpc* rpc);
+
+/* The varint-delimited stream of RPCs (msgio.NewVarintReaderSize(s,
+ * maxMessageSize), comm.go:64-82; the sender's msgio varint writer): splits
+ * in[0 .. len) into frames, frame k being the body in[off[k] .. off[k] +
+ * lens[k]).  Stops at a trailing incomplete frame (*consumed = the bytes of
+ * the whole frames; the rest waits for more input).  GSIM_ERANGE when a
+ * frame's length exceeds max_size (msgio.ErrMsgTooLarge: the reference resets
+ * the stream) or when more than cap frames are complete (*n = the frames
+ * found so far, all returned); GSIM_EINVAL for a length varint over 64 bits. */
+int gsim_wire_frames(const uint8_t* in, uint64_t len, uint64_t max_size, uint64_t* off, uint64_t* lens, int32_t cap,
+                     int32_t* n, uint64_t* consumed);
+
 /* ---- device: the heartbeat's RPCs ---------------------------------------- */
 
 /* One encoded RPC in the device output. */

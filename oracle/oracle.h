@@ -90,6 +90,10 @@ typedef struct orc_msgs {
 #define ORC_BEHAVE_IGNORE_IWANT 0x01   /* never answers IWANT (gossipsub_spam_test.go:134-286) */
 
 int64_t orc_round_time(const orc_msgs* m, int64_t g);
+/* sizeof(orc_net), sizeof(orc_msgs): the ctypes mirrors (tests/oracle_binding.py)
+ * check their own size against these when the library loads, so a field added
+ * on one side only fails loudly instead of reading past the caller's struct. */
+int64_t orc_layout_size(int32_t which);
 /* Topic.Publish at the origin (pubsub.go:1196-1202 via pushMsg): slot =
  * id % ring is reset, the origin marks it seen at round g and forwards it in
  * round g+1. */

@@ -152,6 +152,11 @@ static int cmp_arr(const void* a, const void* b)
     return x->er < y->er ? -1 : x->er > y->er;
 }
 
+int64_t orc_layout_size(int32_t which)
+{
+    return which == 0 ? (int64_t)sizeof(orc_net) : which == 1 ? (int64_t)sizeof(orc_msgs) : -1;
+}
+
 int64_t orc_round_time(const orc_msgs* m, int64_t g)
 {
     const int64_t r = g % m->rounds, k = g / m->rounds;

@@ -224,7 +224,7 @@ void orc_gossip_penalties(orc_net* s, orc_msgs* m, int64_t now)
             }
         }
         p->npr[peer] = w;
-        qsort(broken, (size_t)nb, sizeof(uint32_t), cmp_u32);
+        if (nb) qsort(broken, (size_t)nb, sizeof(uint32_t), cmp_u32);
         for (int32_t q = 0; q < nb;) {               /* AddPenalty(p, count) once per peer */
             int32_t r = q;
             while (r < nb && broken[r] == broken[q]) ++r;

@@ -14,7 +14,8 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
-ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+# GSIM_ORACLE_LIB: another build of the same sources (tools/asan_oracle.py: ASan/UBSan)
+ORACLE_LIB = os.environ.get("GSIM_ORACLE_LIB") or os.path.join(ORACLE_DIR, "liboracle.so")
 
 import sys  # noqa: E402
 
@@ -55,6 +56,15 @@ def load():
         if not os.path.exists(ORACLE_LIB):
             subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
         lib = ctypes.CDLL(ORACLE_LIB)
+        # the ctypes mirrors must match the C structs field for field: a field
+        # added to orc_net on one side only made orc_round read past the struct
+        # (round 3's segfault under test_churn_ticks_bit_exact)
+        lib.orc_layout_size.restype = c_int64
+        lib.orc_layout_size.argtypes = [c_int32]
+        for which, st in ((0, OrcNet), (1, OrcMsgs)):
+            got = lib.orc_layout_size(which)
+            if got != ctypes.sizeof(st):
+                raise RuntimeError(f"{st.__name__}: ctypes size {ctypes.sizeof(st)} != C size {got} ({ORACLE_LIB})")
         P = POINTER(OrcNet)
         sig = {
             "orc_refresh_scores": (None, [P, c_int64]),

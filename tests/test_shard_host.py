@@ -61,16 +61,89 @@ def _rank_main(rank, world, port, q):
         q.put((rank, None, None, traceback.format_exc() + str(ex)))
 
 
-@pytest.mark.gpu
-@pytest.mark.timeout(600)
-def test_two_processes_one_shard_each_bit_exact(require_gpu):
+def _diverge_main(rank, world, port, q):
+    """The ranks' control flow diverges on purpose: rank 0 runs a heartbeat
+    (its control exchange), rank 1 a tick's first round (its frontier
+    exchange).  Both count exchanges are K x 8 B, so the transport itself
+    sees nothing wrong; the tags must (gsim error ESTATE on both ranks,
+    before any payload: no gloo abort, no hang)."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        from datetime import timedelta
+
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=60))
+        import oracle_binding as ob
+        from fixtures import beacon_params, synthetic_state
+        from gsim import _abi
+        from gsim.engine import GsimError, random_regular
+        from gsim.params import GossipSubParams, PeerScoreThresholds, Second
+        from gsim.shard import HostCollectives, ShardedEngine
+        from test_delivery import R, T0
+        from test_heartbeat import tick_time
+        from tickrun import SEED
+        n, T = 600, 2
+        net = random_regular(n, 12, seed=3, n_topics=T)
+        params = beacon_params(T)
+        th = PeerScoreThresholds(GossipThreshold=-20, PublishThreshold=-40, GraylistThreshold=-300)
+        gp = GossipSubParams(D=6, Dlo=5, Dhi=10)
+        st = ob.NetState(net, params, thresholds=th, gossip=gp)
+        synthetic_state(st, np.random.default_rng(5), tick_time(0), 0.5)
+        eng = ShardedEngine(params, th, gossip=gp, shards=world, host=(rank, HostCollectives(), 0))
+        eng.load_graph(net)
+        eng.set_seed(SEED)
+        st.push_to_engine(eng)
+        eng.msgs_init(64, R, T0, Second)
+        eng.refresh_scores(tick_time(1))
+        err, rc = None, None
+        try:
+            if rank == 0:
+                eng.heartbeat(1, tick_time(1))
+            else:
+                eng.round(1 * R)
+        except GsimError as ex:
+            err, rc = str(ex), ex.rc
+        assert err is not None and "exchange sequence mismatch" in err and rc == _abi.GSIM_ESTATE, err
+        q.put((rank, err, None, None))
+        dist.destroy_process_group()
+    except Exception as ex:  # reported to the parent
+        q.put((rank, None, None, traceback.format_exc() + str(ex)))
+
+
+def _spawn(target, world=2):
     import torch.multiprocessing as mp
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    return q, [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_diverged_exchange_sequence_is_an_error_not_an_abort(require_gpu):
+    q, procs = _spawn(_diverge_main)
+    for pr in procs:
+        pr.start()
+    res = []
+    try:
+        for _ in procs:
+            r = q.get(timeout=240)
+            assert r[3] is None, f"rank {r[0]}: {r[3]}"
+            res.append(r)
+    finally:
+        for pr in procs:
+            pr.join(timeout=30)
+            if pr.is_alive():
+                pr.kill()
+    assert sorted(r[0] for r in res) == [0, 1]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_two_processes_one_shard_each_bit_exact(require_gpu):
+    q, procs = _spawn(_rank_main)
     for pr in procs:
         pr.start()
     import queue

@@ -217,6 +217,159 @@ def test_fragmented_ihave_loses_its_topic():
     assert [i for f in frs for ih in f.control.ihave for i in ih.messageIDs] == r.control.ihave[0].messageIDs
 
 
+# ---- decoding (gsim_wire_decode / gsim_wire_frames) ----------------------------------
+
+def from_pb(x) -> wire.RPC:
+    """A protobuf-runtime RPC as the library's dataclasses."""
+    def opt(m, f):
+        return getattr(m, f) if m.HasField(f) else None
+    r = wire.RPC()
+    for s in x.subscriptions:
+        r.subscriptions.append(wire.SubOpts(opt(s, "subscribe"), opt(s, "topicid")))
+    for m in x.publish:
+        r.publish.append(wire.Message(*(opt(m, f) for f in ("from", "data", "seqno", "topic", "signature", "key"))))
+    if x.HasField("control"):
+        c = wire.ControlMessage()
+        for g in x.control.ihave:
+            c.ihave.append(wire.ControlIHave(opt(g, "topicID"), list(g.messageIDs)))
+        for g in x.control.iwant:
+            c.iwant.append(wire.ControlIWant(list(g.messageIDs)))
+        for g in x.control.graft:
+            c.graft.append(wire.ControlGraft(opt(g, "topicID")))
+        for p in x.control.prune:
+            c.prune.append(wire.ControlPrune(opt(p, "topicID"),
+                                             [wire.PeerInfo(opt(i, "peerID"), opt(i, "signedPeerRecord")) for i in p.peers],
+                                             opt(p, "backoff")))
+        r.control = c
+    return r
+
+
+def test_decode_round_trips_protobuf_runtime():
+    """Random RPCs serialized by the protobuf runtime decode to the same
+    fields as the runtime's own parse, and re-encode to the same bytes."""
+    rng = np.random.default_rng(11)
+    for k in range(400):
+        r = rand_rpc(rng, scale=1.0 + (k % 7))
+        data = to_pb(r).SerializeToString()
+        got = wire.unmarshal(data)
+        assert got == from_pb(wo.pb()["RPC"].FromString(data)), k
+        assert got == r, k
+        assert wire.marshal(got) == data, k
+
+
+def test_decode_merges_as_proto2():
+    """Concatenated encodings are one message (proto2 merge, what gogo's
+    generated Unmarshal does): repeated fields append, the control message
+    merges its lists, optional scalars take the last value.  The protobuf
+    runtime's MergeFromString is the reference."""
+    C = wo.pb()
+    rng = np.random.default_rng(12)
+    for k in range(200):
+        parts = [to_pb(rand_rpc(rng, scale=1.0 + (k % 3))).SerializeToString() for _ in range(int(rng.integers(2, 5)))]
+        want = C["RPC"]()
+        for b in parts:
+            want.MergeFromString(b)
+        got = wire.unmarshal(b"".join(parts))
+        assert got == from_pb(want), k
+        assert wire.marshal(got) == want.SerializeToString(), k
+
+
+def test_decode_skips_unknown_fields():
+    """Fields the schema does not know (every wire type, nested groups)
+    are skipped at every level, as gogo's skipRpc does."""
+    C = wo.pb()
+    rng = np.random.default_rng(13)
+    unknown = [b"\x78\x05",                          # field 15, varint
+               b"\x81\x01" + bytes(8),                # field 16, fixed64
+               b"\x8d\x01" + bytes(4),                # field 17, fixed32
+               b"\x92\x01\x03abc",                   # field 18, bytes
+               b"\x9b\x01\x08\x01\xa3\x01\xa4\x01\x9c\x01"]   # field 19, a group holding a group
+    for k in range(100):
+        r = rand_rpc(rng)
+        data = to_pb(r).SerializeToString()
+        junk = b"".join(unknown[int(q)] for q in rng.integers(0, len(unknown), size=3))
+        got = wire.unmarshal(junk + data + junk)
+        assert got == r, k
+        want = C["RPC"]()
+        want.MergeFromString(junk + data + junk)
+        want.DiscardUnknownFields()
+        assert wire.marshal(got) == want.SerializeToString()
+    # inside the nested messages too: a PRUNE's PeerInfo with an unknown field
+    pi = b"\x0a\x02id" + unknown[3] + b"\x12\x01r"
+    prune = b"\x0a\x01t" + b"\x12" + bytes([len(pi)]) + pi + b"\x18\x3c"
+    ctl = b"\x22" + bytes([len(prune)]) + prune
+    got = wire.unmarshal(b"\x1a" + bytes([len(ctl)]) + ctl)
+    assert got.control.prune == [wire.ControlPrune(b"t", [wire.PeerInfo(b"id", b"r")], 60)]
+
+
+def test_decode_rejects_malformed():
+    """What gogo's Unmarshal errors on (a "bogus rpc", comm.go:82)."""
+    good = wire.marshal(wire.RPC(subscriptions=[wire.SubOpts(True, b"t")],
+                                 publish=[wire.Message(data=b"hello", seqno=bytes(8))],
+                                 control=wire.ControlMessage(graft=[wire.ControlGraft(b"t")])))
+    for cut in range(1, len(good)):          # truncated inside a field
+        try:
+            wire.unmarshal(good[:cut])
+        except wire.WireError:
+            continue
+        # a cut at a field boundary of the top level is a valid shorter RPC
+        assert wire.marshal(wire.unmarshal(good[:cut])) == good[:cut]
+    bad = [b"\x0a\x05\x08",                       # length past the end
+           b"\x08\x01",                            # RPC.subscriptions with a varint wire type
+           b"\x0a\x02\x0a\x00",                    # SubOpts.subscribe with a bytes wire type
+           b"\x1a\x03\x22\x01\x18",                 # ControlPrune.backoff cut
+           b"\x00\x00",                            # field number 0
+           b"\x0c",                                 # end group with none open
+           b"\x78" + b"\xff" * 10 + b"\x01",        # varint over 64 bits
+           b"\x7e\x00"]                             # wire type 6
+    for b in bad:
+        with pytest.raises(wire.WireError):
+            wire.unmarshal(b)
+    assert wire.unmarshal(b"") == wire.RPC()
+    assert wire.unmarshal(b"\x1a\x00") == wire.RPC(control=wire.ControlMessage())
+
+
+def test_decode_fragments_of_fragment_rpc_function():
+    """The fragments TestFragmentRPCFunction's RPCs split into
+    (gossipsub_test.go:2338-2500) decode to the original's contents, in
+    order: messages, subscriptions, grafts, prunes, iwant and ihave ids."""
+    rng = np.random.default_rng(14)
+    topic = b"test"
+    ids = [[rng.bytes(32) for _ in range(100)] for _ in range(5)]
+    r = wire.RPC(subscriptions=[wire.SubOpts(True, topic)], publish=[_mk_msg(rng, 200) for _ in range(100)],
+                 control=wire.ControlMessage(graft=[wire.ControlGraft(topic)], prune=[wire.ControlPrune(topic)],
+                                             ihave=[wire.ControlIHave(None, x) for x in ids],
+                                             iwant=[wire.ControlIWant(x) for x in ids]))
+    frs = [wire.unmarshal(b) for b in wire.fragment_rpc(r, 1024)]
+    assert [m for f in frs for m in f.publish] == r.publish
+    assert [x for f in frs for x in f.subscriptions] == r.subscriptions
+    ctl = [f.control for f in frs if f.control is not None]
+    assert [g for c in ctl for g in c.graft] == r.control.graft
+    assert [p for c in ctl for p in c.prune] == r.control.prune
+    assert [i for c in ctl for g in c.iwant for i in g.messageIDs] == [i for x in ids for i in x]
+    assert [i for c in ctl for g in c.ihave for i in g.messageIDs] == [i for x in ids for i in x]
+
+
+def test_frames_split_a_delimited_stream():
+    """msgio's varint-delimited reader (comm.go:64-82): whole frames, a
+    partial one left for later, frames over maxMessageSize refused."""
+    rng = np.random.default_rng(15)
+    rpcs = [to_pb(rand_rpc(rng, scale=1 + k % 5)).SerializeToString() for k in range(30)] + [b"", b"x" * 300]
+    stream = wire.delimited(rpcs)
+    got, used = wire.frames(stream)
+    assert got == rpcs and used == len(stream)
+    assert [wire.unmarshal(b) for b in got[:30]] == [wire.unmarshal(b) for b in rpcs[:30]]
+    for cut in (1, len(stream) // 3, len(stream) - 1):
+        part, used = wire.frames(stream[:cut])
+        assert part == rpcs[:len(part)] and stream[:used] == wire.delimited(part)
+        rest, _ = wire.frames(stream[used:])
+        assert part + rest == rpcs
+    with pytest.raises(wire.WireError):
+        wire.frames(wire.delimited([b"y" * 2000]), max_size=1024)
+    ok, _ = wire.frames(wire.delimited([b"y" * 1024]), max_size=1024)
+    assert ok == [b"y" * 1024]
+
+
 # ---- GPU ----------------------------------------------------------------------------
 
 
