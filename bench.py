@@ -583,6 +583,18 @@ def main():
         if not args.no_cpu_baseline and world == 1 and not args.vdelay:
             # (the oracle baseline publishes without latency: not the same workload as a --vdelay line)
             out["cpu_baseline"] = cpu_baseline(cfg, scen=scen)
+            # the same oracle on the whole network, timed on a GPU box's host cores by
+            # `bench.py --cpu-full` (minutes per tick: not re-run here)
+            full = os.path.join(REPO, "profiles", f"r04_cpu_full_{args.config}_box16.json")
+            if os.path.exists(full):
+                try:
+                    fd = json.loads(open(full).read().strip().splitlines()[-1])
+                    out["cpu_baseline"]["full_network"] = {
+                        "value": fd["value"], "cores": fd["cores"], "median_tick_s": fd["all_core"]["median_tick_s"],
+                        "msg_edge_deliveries_per_sec": fd["msg_edge_deliveries_per_sec"],
+                        "gpu_over_cpu": value / fd["value"], "source": os.path.relpath(full, REPO)}
+                except (OSError, ValueError, KeyError):
+                    pass
         print(json.dumps(out), flush=True)
     eng.close()
     if dist is not None:
