@@ -585,7 +585,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(cfg, scen=scen)
             # the same oracle on the whole network, timed on a GPU box's host cores by
             # `bench.py --cpu-full` (minutes per tick: not re-run here)
-            full = os.path.join(REPO, "profiles", f"r04_cpu_full_{args.config}_box16.json")
+            full = os.path.join(REPO, "profiles", f"cpu_full_{args.config}_box16.json")
             if os.path.exists(full):
                 try:
                     fd = json.loads(open(full).read().strip().splitlines()[-1])

@@ -103,13 +103,24 @@ __device__ __forceinline__ int64_t go_div(int64_t n, int64_t d)
 // pointer: loads of its fields stay where they are used (scalar loads, K$
 // hits) instead of being hoisted out of the loops, where dozens of live
 // pointers overflow the SGPRs and spill to VGPR lanes (a v_readlane per use).
-// Only valid in a kernel whose FIRST parameter is the A passed.
+// Only valid in a kernel whose FIRST parameter is the A passed, unmodified:
+// a helper reached from another kernel, or handed a modified copy, would read
+// the wrong memory silently.  Debug builds (GSIM_DEBUG_KERNARG, `make debug`)
+// trap when the re-read struct's leading 16 bytes differ from the argument's.
 template <class A>
-__device__ __forceinline__ const A& kernarg0(const A&)
+__device__ __forceinline__ const A& kernarg0(const A& arg)
 {
     using CP = const __attribute__((address_space(4))) A*;
     CP p = (CP)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(p));
+#ifdef GSIM_DEBUG_KERNARG
+    static_assert(sizeof(A) >= 16, "kernarg0 check reads 16 bytes");
+    const uint64_t* x = (const uint64_t*)&arg;
+    const __attribute__((address_space(4))) uint64_t* y = (const __attribute__((address_space(4))) uint64_t*)p;
+    if (x[0] != y[0] || x[1] != y[1]) __builtin_trap();
+#else
+    (void)arg;
+#endif
     return *(const A*)p;
 }
 

@@ -246,12 +246,9 @@ __device__ bool select_smallest(const HbArgs& a, bool cand, int count, uint32_t 
 // the scalar loads (constant address space, K$ hits) inside the loop.
 // Only for kernels whose first parameter is the HbArgs (k_heartbeat,
 // k_heartbeat_hub): it is read at the start of the kernarg segment.
-__device__ __forceinline__ const HbArgs& hb_launder(const HbArgs&)
+__device__ __forceinline__ const HbArgs& hb_launder(const HbArgs& a)
 {
-    using CP = const __attribute__((address_space(4))) HbArgs*;
-    CP p = (CP)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(p));
-    return *(const HbArgs*)p;
+    return kernarg0(a);        // (the same re-read; debug builds check its argument)
 }
 
 // The score bits of one (observer, neighbour, topic) record, loaded on first
@@ -1805,7 +1802,9 @@ __global__ void k_subscribe(HbArgs a, uint64_t* sub, const uint32_t* pairs, int3
                     uint32_t be = 0xFFFFFFFFu;
                     for (uint32_t e = b; e < en; ++e) {
                         if (!sub_topic_peer(a, sub, e, t)) continue;
-                        if (a.direct[e] || bo(e) != 0 || a.score[a.rev[e]] < 0.0) continue;
+                        // the live Score(p) (gossipsub.go:1076, 1091): deliveries since the
+                        // last refresh count, as for emitGossip's candidates
+                        if (a.direct[e] || bo(e) != 0 || score_of_record(a, a.rev[e], a.col[e]) < 0.0) continue;
                         if (more && (mf(e) & GSIM_TF_FANOUT)) continue;
                         const uint64_t key = hb_key(a, gp_, t, P_JOIN, glob(a, a.col[e]), e - b);
                         if ((!first_pick && key <= last) || key >= best) continue;
@@ -1822,7 +1821,8 @@ __global__ void k_subscribe(HbArgs a, uint64_t* sub, const uint32_t* pairs, int3
                 int have = 0;
                 for (uint32_t e = b; e < en; ++e) {
                     if (!(mf(e) & GSIM_TF_FANOUT)) continue;
-                    if (a.score[a.rev[e]] < 0.0 || bo(e) != 0) mf(e) &= (uint8_t)~GSIM_TF_FANOUT;
+                    if (score_of_record(a, a.rev[e], a.col[e]) < 0.0 || bo(e) != 0)   // live Score (1063)
+                        mf(e) &= (uint8_t)~GSIM_TF_FANOUT;
                     else ++have;
                 }
                 if (have < a.D) pick(a.D - have, true);

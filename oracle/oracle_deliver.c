@@ -47,6 +47,11 @@ void orc_msgs_log(orc_msgs* m, int32_t on)
 
 void orc_log_net(int32_t kind, uint32_t a, uint32_t b, int32_t topic, int64_t now)
 {
+    orc_log_net_x(kind, a, b, topic, 0, 0, now);
+}
+
+void orc_log_net_x(int32_t kind, uint32_t a, uint32_t b, int32_t topic, uint64_t mid, int64_t g, int64_t x)
+{
     if (!g_net_on) return;
 #pragma omp critical(orc_log)
     {
@@ -55,7 +60,7 @@ void orc_log_net(int32_t kind, uint32_t a, uint32_t b, int32_t topic, int64_t no
             g_net_ev = (orc_event*)realloc(g_net_ev, sizeof(orc_event) * (size_t)g_net_cap);
         }
         orc_event* v = &g_net_ev[g_net_n++];
-        v->kind = kind; v->topic = topic; v->a = a; v->b = b; v->g = 0; v->mid = 0; v->x = now;
+        v->kind = kind; v->topic = topic; v->a = a; v->b = b; v->g = g; v->mid = mid; v->x = x;
     }
 }
 

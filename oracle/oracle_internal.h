@@ -23,6 +23,7 @@ enum {
     P_PX_GRAFT = 15,    /* makePrune: getPeers for PX (GRAFT reply)    gossipsub.go:831-834 */
     P_GATER = 16,       /* peer gater: rand.Float64() of AcceptFrom    peer_gater.go:357 */
     P_JOIN = 17,        /* Join: getPeers for the new mesh             gossipsub.go:1068-1092 */
+    P_PX_LEAVE = 18,    /* makePrune: getPeers for PX (Leave's PRUNEs)  gossipsub.go:1118, 1866-1906 */
 };
 
 static inline uint64_t okey(uint64_t seed, uint64_t tick, uint32_t obs, int32_t topic, uint32_t purpose,
@@ -76,6 +77,7 @@ void orc_log(orc_msgs* m, int32_t kind, uint32_t a, uint32_t b, uint32_t slot, i
 /* router-level events (GRAFT/PRUNE/ADD/REMOVE) go to the message log that
  * last turned logging on (orc_msgs_log); safe inside the OpenMP phases */
 void orc_log_net(int32_t kind, uint32_t a, uint32_t b, int32_t topic, int64_t now);
+void orc_log_net_x(int32_t kind, uint32_t a, uint32_t b, int32_t topic, uint64_t mid, int64_t g, int64_t x);
 
 priv* orc_msgs_priv(orc_msgs* m);
 int64_t orc_round_time(const orc_msgs* m, int64_t g);

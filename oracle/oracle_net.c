@@ -98,24 +98,23 @@ static void graft_peer(hb* h, uint32_t e)
  * makePrune's getPeers(topic, PrunePeers, xp != p && Score(xp) >= 0)
  * (gossipsub.go:1866-1906) and the pruned peer's handlePrune / pxConnect
  * (860-869, 893-939).  live: Score is the observer's live score (the
- * heartbeat's sendGraftPrune); else its snapshot (handleGraft's replies, the
- * control rounds' declared divergence).  The keys put the pruned peer's row
- * position into the topic word: each PRUNE's list is its own shuffle.  The
+ * heartbeat's sendGraftPrune, Leave's sendPrune); else its snapshot
+ * (handleGraft's replies, the control rounds' declared divergence).  The keys
+ * put the pruned peer's row position into the topic word: each PRUNE's list
+ * is its own shuffle.  The list is what the PRUNE carries, whatever the
+ * receiver then does with it (ORC_EV_PX_PEER events, in list order).  The
  * receiver ignores PX from a peer it scores below acceptPXThreshold (its
  * snapshot); every listed peer it is not connected to is a connection
  * attempt, marked at its edge to that peer when the address is known (a CSR
- * edge).  Attempts are resolved between ticks (orc_px_connect). */
+ * edge).  Attempts are resolved between ticks (orc_px_connect).  pend: Leave's
+ * PRUNEs -- the receiver handles them with the tick's control (its snapshot
+ * after the next refresh), so the list waits in the pending table
+ * (px_pending) until orc_px_connect. */
 static int64_t find_edge(const orc_net* s, uint32_t i, uint32_t j);
 
-static void px_emit(hb* h, uint32_t ep, int live, uint32_t purpose, uint64_t key_tick)
+static int px_list(hb* h, uint32_t ep, int live, uint32_t purpose, uint64_t key_tick, cand* c)
 {
     orc_net* s = h->s;
-    if (!s->px) return;
-    const uint32_t p = s->col[ep];
-    if (s->score[s->rev[ep]] < s->th->accept_px_threshold) return;
-    const uint32_t deg = h->en - h->b;
-    cand buf[1024];
-    cand* c = deg <= 1024 ? buf : (cand*)malloc(sizeof(cand) * deg);
     int n = 0;
     const int32_t kt = h->t + 64 * (int32_t)(ep - h->b + 1);
     for (uint32_t e = h->b; e < h->en; ++e) {
@@ -129,14 +128,64 @@ static void px_emit(hb* h, uint32_t ep, int live, uint32_t purpose, uint64_t key
     }
     qsort(c, (size_t)n, sizeof(cand), cmp_key);
     if (n > s->gp->prune_peers) n = s->gp->prune_peers;
+    for (int q = 0; q < n; ++q)
+        orc_log_net_x(ORC_EV_PX_PEER, h->i, s->col[c[q].e], h->t, s->col[ep], q, h->now);
+    return n;
+}
+
+/* the pruned peer's handlePrune PX part: acceptPXThreshold, then pxConnect */
+static void px_accept(orc_net* s, uint32_t ep, const uint32_t* listed, int n)
+{
+    if (s->score[s->rev[ep]] < s->th->accept_px_threshold) return;
+    const uint32_t p = s->col[ep];
     for (int q = 0; q < n; ++q) {
-        const int64_t ex = find_edge(s, p, s->col[c[q].e]);
+        const int64_t ex = find_edge(s, p, listed[q]);
         if (ex < 0) continue;                                  /* no known address */
         if (s->estate[ex] & ES_CONN) continue;                 /* pxConnect: already connected */
 #pragma omp atomic write
         s->px[ex] = 1;
     }
+}
+
+/* Leave's PX lists until orc_px_connect: (pruner's edge, listed peer) per
+ * entry, one table per network (keyed by its px array) */
+typedef struct px_pend { const uint8_t* key; uint64_t* ent; int64_t n, cap; } px_pend;
+static px_pend g_pxp[8];
+
+static px_pend* px_pending(const orc_net* s)
+{
+    for (int k = 0; k < 8; ++k)
+        if (g_pxp[k].key == s->px) return &g_pxp[k];
+    for (int k = 0; k < 8; ++k)
+        if (!g_pxp[k].key) { g_pxp[k].key = s->px; return &g_pxp[k]; }
+    g_pxp[0].n = 0;                                            /* (8 live networks at most) */
+    g_pxp[0].key = s->px;
+    return &g_pxp[0];
+}
+
+static void px_emit(hb* h, uint32_t ep, int live, uint32_t purpose, uint64_t key_tick, int pend)
+{
+    orc_net* s = h->s;
+    if (!s->px) return;
+    const uint32_t deg = h->en - h->b;
+    cand buf[1024];
+    cand* c = deg <= 1024 ? buf : (cand*)malloc(sizeof(cand) * deg);
+    const int n = px_list(h, ep, live, purpose, key_tick, c);
+    uint32_t listed[256];
+    for (int q = 0; q < n && q < 256; ++q) listed[q] = s->col[c[q].e];
     if (c != buf) free(c);
+    if (!pend) {
+        px_accept(s, ep, listed, n < 256 ? n : 256);
+        return;
+    }
+    px_pend* pp = px_pending(s);
+    for (int q = 0; q < n && q < 256; ++q) {
+        if (pp->n == pp->cap) {
+            pp->cap = pp->cap ? 2 * pp->cap : 256;
+            pp->ent = (uint64_t*)realloc(pp->ent, sizeof(uint64_t) * (size_t)pp->cap);
+        }
+        pp->ent[pp->n++] = (uint64_t)ep | ((uint64_t)listed[q] << 32);
+    }
 }
 
 typedef int (*filter_fn)(const hb* h, uint32_t e, double arg);
@@ -400,7 +449,7 @@ void orc_heartbeat_gossip(orc_net* s, orc_msgs* m, uint64_t tick, int64_t now, u
             for (int32_t t = 0; t < s->t; ++t) {
                 h.t = t;
                 for (uint32_t e = h.b; e < h.en; ++e)
-                    if (out[(int64_t)t * s->e + s->rev[e]] & GSIM_CTL_PX) px_emit(&h, e, 1, P_PX, tick);
+                    if (out[(int64_t)t * s->e + s->rev[e]] & GSIM_CTL_PX) px_emit(&h, e, 1, P_PX, tick, 0);
             }
         fanout(&h, m);
     }
@@ -504,7 +553,7 @@ int64_t orc_handle_control(orc_net* s, int32_t round, int64_t now)
                     uint8_t* r = &out[(int64_t)t * s->e + s->rev[e]];
                     if (!(*r & GSIM_CTL_PX)) continue;
                     if (nopx[e - h.b]) *r &= (uint8_t)~GSIM_CTL_PX;
-                    else px_emit(&h, e, 0, P_PX_GRAFT, kt);
+                    else px_emit(&h, e, 0, P_PX_GRAFT, kt, 0);
                 }
             }
             free(nopx);
@@ -572,6 +621,17 @@ int32_t orc_churn(orc_net* s, const uint32_t* pairs, int32_t count, int32_t up, 
 int64_t orc_px_connect(orc_net* s, int64_t now, uint32_t* pairs, int64_t cap)
 {
     if (!s->px) return 0;
+    {   /* Leave's PRUNEs: their receivers' PX handling, with this tick's snapshot */
+        px_pend* pp = px_pending(s);
+        for (int64_t q = 0; q < pp->n;) {
+            const uint32_t ep = (uint32_t)pp->ent[q];
+            uint32_t listed[256];
+            int n = 0;
+            while (q < pp->n && (uint32_t)pp->ent[q] == ep && n < 256) listed[n++] = (uint32_t)(pp->ent[q++] >> 32);
+            px_accept(s, ep, listed, n);
+        }
+        pp->n = 0;
+    }
     uint32_t* conn = NULL;
     int64_t n = 0, capc = 0;
     for (int64_t u = 0; u < s->n; ++u)
@@ -605,7 +665,7 @@ int64_t orc_px_connect(orc_net* s, int64_t now, uint32_t* pairs, int64_t cap)
 static int f_join(const hb* h, uint32_t e, double arg)        /* gossipsub.go:1084-1090 */
 {
     (void)arg;
-    return !is_direct(h, e) && !has_backoff(h, e) && h->s->score[e] >= 0;
+    return !is_direct(h, e) && !has_backoff(h, e) && orc_score_edge(h->s, e) >= 0;   /* the live Score (1091) */
 }
 
 static int f_join_more(const hb* h, uint32_t e, double arg)   /* gossipsub.go:1070-1077 */
@@ -634,7 +694,8 @@ void orc_set_subscriptions(orc_net* s, const uint32_t* pairs, int32_t count, int
                 int have = 0;
                 for (uint32_t e = h.b; e < h.en; ++e) {
                     if (!in_fanout(&h, e)) continue;
-                    if (s->score[e] < 0 || has_backoff(&h, e)) s->tflags[ti(&h, e)] &= (uint8_t)~GSIM_TF_FANOUT;
+                    if (orc_score_edge(s, e) < 0 || has_backoff(&h, e))                 /* live Score (1063) */
+                        s->tflags[ti(&h, e)] &= (uint8_t)~GSIM_TF_FANOUT;
                     else ++have;
                 }
                 if (have < gp->d) {
@@ -666,8 +727,11 @@ void orc_set_subscriptions(orc_net* s, const uint32_t* pairs, int32_t count, int
                 orc_log_net(ORC_EV_PRUNE, p, s->col[e], t, now);   /* tracer.Prune, sendPrune, addBackoff */
                 orc_prune(s, e, t);
                 s->tflags[ti(&h, e)] &= (uint8_t)~TF_MESH;
-                send_ctl(&h, e, GSIM_CTL_PRUNE | GSIM_CTL_UNSUB);
+                send_ctl(&h, e, GSIM_CTL_PRUNE | GSIM_CTL_UNSUB | (gp->do_px ? GSIM_CTL_PX : 0));
                 do_add_backoff(&h, e, gp->unsubscribe_backoff_ns);
+                /* sendPrune(p, topic, true) -> makePrune(p, topic, gs.doPX, true): the list with
+                 * the live scores after the Prunes so far (gossipsub.go:1118, 1132-1133) */
+                if (gp->do_px) px_emit(&h, e, 1, P_PX_LEAVE, tick, 1);
             }
         }
     }

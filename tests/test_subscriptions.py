@@ -33,7 +33,8 @@ def test_join_turns_the_fanout_into_the_mesh():
     tick(st, msgs, 3, sched={3 * R: [(1, 1, o, 0)]})
     fan = b + np.nonzero(st.tflags[1, b:en] & _abi.TF_FANOUT)[0]
     assert len(fan) == 6 and st.fan_topics[o] == 2
-    st.score[fan[0]] = -5.0                           # dropped: negative score
+    st.invalid[1, fan[0]] = 3.0                       # dropped: negative (live) score, P4
+    assert ob.load().orc_score_edge(st.view(), int(fan[0])) < 0
     st.backoff[1, fan[1]] = tick_time(4)              # dropped: a backoff entry
     now = tick_time(4) - Second // 2
     st.set_subscriptions([(o, 1)], True, 4, now, SEED)
@@ -49,6 +50,31 @@ def test_join_turns_the_fanout_into_the_mesh():
         assert st.tflags[1, e] & _abi.TF_IN_MESH, "tracer.Graft"
     st.set_subscriptions([(o, 1)], True, 4, now, SEED)        # already joined: no-op
     assert (b + np.nonzero(st.tflags[1, b:en] & _abi.TF_MESH)[0] == mesh).all()
+
+
+def test_join_filters_on_the_live_score():
+    """Join's fanout filter and getPeers call the live gs.score.Score(p)
+    (gossipsub.go:1063, 1076, 1091), not the snapshot of the last refresh: a
+    candidate whose invalid deliveries since that refresh made its score
+    negative is not grafted, although its snapshot score is still >= 0."""
+    lib = ob.load()
+    net, st = fanout_net()
+    msgs = ob.Msgs(net.n, 2, 64, R, T0, Second)
+    for kk in range(1, 3):
+        tick(st, msgs, kk)
+    o = 3
+    b, en = row(net, o)
+    cands = [e for e in range(b, en) if (net.sub[net.col[e]] >> np.uint64(1)) & np.uint64(1)]
+    assert len(cands) > 6
+    bad = cands[:len(cands) - 6]                  # leave exactly D good candidates
+    v = st.view()
+    for e in bad:
+        st.invalid[1, e] = 3.0                    # RejectMessage deliveries since the refresh (P4)
+        assert st.score[e] >= 0 and lib.orc_score_edge(v, e) < 0
+    st.set_subscriptions([(o, 1)], True, 3, tick_time(3) - Second // 2, SEED)
+    mesh = set(b + np.nonzero(st.tflags[1, b:en] & _abi.TF_MESH)[0])
+    assert not (mesh & set(bad)), "a negative live score is filtered out"
+    assert mesh == set(cands) - set(bad)
 
 
 def test_join_without_fanout_takes_d_peers():
