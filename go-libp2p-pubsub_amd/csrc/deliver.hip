@@ -1016,6 +1016,12 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             if (vv[u] && (ds & GSIM_DS_DIRECT) && !sel) sel = (a.sub[i] >> t) & 1ull;
                             const bool tg = vv[u] && sel && (ds & GSIM_DS_CONNECTED) && i != fv[u] && i != origin;
                             const bool remote = i < a.rlo || i >= a.rhi;
+                            if (tg && a.tr.ev) {         // the copy's RPC: SendRPC / RecvRPC (trace.go:250-297)
+                                const int64_t ts = round_time(a, a.g);
+                                const uint64_t tm = ((uint64_t)a.g << 32) | m;
+                                if (a.tr.on(j)) a.tr.push(ts, tm, j, i, t, GSIM_TRACE_SEND_RPC, 0);
+                                if (a.tr.on(i)) a.tr.push(ts, tm, i, j, t, GSIM_TRACE_RECV_RPC, 0);
+                            }
                             if constexpr (PUSH) {
                                 // the receiver's shard delivers it (its AcceptFrom, records, cell)
                                 if (tg && remote) {
@@ -1933,6 +1939,14 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a_, const uint
         const RoundArgs& a = kernarg0(a_);   // (re-read per copy: SGPR pressure)
         const uint64_t ent = resp[x];
         const uint32_t r = (uint32_t)ent, m = (uint32_t)(ent >> 32);
+        if (a.tr.ev) {
+            // the IWANT answer's RPC (a single engine: every entry is one), sent by
+            // handleIWant in the round before it arrives (trace.go:250-297)
+            const uint32_t rp = a.col[r], rs = owner[r];
+            const int32_t rt = (int32_t)a.mtopic[m];
+            if (a.tr.on(rs)) a.tr.push(round_time(a, a.g - 1), ((uint64_t)a.g << 32) | m, rs, rp, rt, GSIM_TRACE_SEND_RPC, 1);
+            if (a.tr.on(rp)) a.tr.push(round_time(a, a.g), ((uint64_t)a.g << 32) | m, rp, rs, rt, GSIM_TRACE_RECV_RPC, 1);
+        }
         const uint8_t ds = a.dstate[r];
         if (!(ds & GSIM_DS_ACCEPT)) { n_gray++; continue; }        // AcceptFrom
         const uint32_t p = a.col[r];

@@ -555,6 +555,17 @@ struct WireView {
     int64_t ihave_tick;        // heartbeat whose gossip is pending, -1 none
 };
 bool deliver_wire_view(gsim_handle* h, WireView* v);     // false before gsim_msgs_init
+// What the wire encoder needs of peer exchange (heartbeat.hip): the PX
+// observers' live scores, the selection seed, Leave's kept PX lists; false
+// when WithPeerExchange is off
+struct WirePx {
+    const double* pxs;
+    uint64_t seed;
+    const uint64_t* pxl;
+    const uint32_t* pxl_tick;
+    uint32_t n_pxl;
+};
+bool deliver_wire_px(gsim_handle* h, WirePx* w);
 int deliver_promise_check(gsim_handle* h, int64_t now);    // broken promises -> pending P7
 int deliver_heartbeat_begin(gsim_handle* h, uint64_t tick); // fresh IHAVE marks
 uint64_t gsim_get_seed(const gsim_handle* h);              // heartbeat.hip
@@ -565,6 +576,7 @@ int handle_control(gsim_handle* h, int32_t round, int64_t now);   // heartbeat.h
 // its connection attempts out (global asker | peer << 32), gs.outbound of the connections
 bool px_enabled(const gsim_handle* h);
 int px_import(gsim_handle* h, const uint64_t* d_in, int64_t n);
+int px_leave_import(gsim_handle* h, const uint32_t* g2l);
 int px_asks(gsim_handle* h, uint64_t* d_out, uint32_t* d_cnt, int64_t cap);
 int px_mark_outbound(gsim_handle* h, const uint64_t* d_pairs, int64_t n);
 // trace.hip: resolve the recorded message copies (seen-set cells, slot tables)

@@ -40,6 +40,14 @@ struct Extra {
     uint8_t* d_nopx = nullptr;
     uint32_t* d_pxc = nullptr;         // [1 + 2E] connections made: count, then (dialer edge, peer edge)
     double* d_pxs = nullptr;           // [E] live scores of PX observers (HbArgs::pxs)
+    // Leave's PRUNEs with PX (makePrune(p, topic, doPX, true), gossipsub.go:1118): their
+    // lists, one entry per listed peer (the pruner's edge | topic << 32 | listed peer's
+    // global id << 38) and the Leave's tick, until the connector (gsim_px_connect)
+    // hands them to the pruned peers and the wire encoder has read them
+    uint64_t* d_pxl = nullptr;
+    uint32_t* d_pxl_tick = nullptr;
+    uint32_t* d_pxl_n = nullptr;       // [2] entries, overflow
+    int64_t pxl_cap = 0;
 };
 
 struct HbArgs {
@@ -118,6 +126,10 @@ struct HbArgs {
     uint8_t* pxm;              // [E] the row's owner tries to connect to col[e]
     uint8_t* nopx;             // [E] a GRAFT of this sender turned PX off for its RPC
     double* pxs;               // [E] the observer's live score of col[e] after its heartbeat (PX observers)
+    uint64_t* pxl;             // Leave's PX lists (Extra::d_pxl), their ticks, count
+    uint32_t* pxl_tick;
+    uint32_t* pxl_n;
+    int64_t pxl_cap;
     TraceRef tr;               // gsim_trace_config: tracer.Graft / Prune / AddPeer / RemovePeer
 };
 
@@ -1466,7 +1478,9 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
             for (int p0 = 0; p0 < deg; p0 += 64) {
                 const uint32_t ep_l = b + (uint32_t)(p0 + lane);
                 const uint64_t mp = p0 + lane < deg ? smask_of(a.smask, a.col[ep_l]) : 0ull;
-                const bool pr = slot_has(mp, t) && (a.ctl_out[slot_idx(mp, t, a.E, a.rev[ep_l])] & GSIM_CTL_PX);
+                // (a Leave's PRUNE in the same inbox, GSIM_CTL_UNSUB, was listed at the Leave)
+                const bool pr = slot_has(mp, t) &&
+                                (a.ctl_out[slot_idx(mp, t, a.E, a.rev[ep_l])] & (GSIM_CTL_PX | GSIM_CTL_UNSUB)) == GSIM_CTL_PX;
                 for (uint64_t pm = __ballot(pr); pm; pm &= pm - 1) {
                     const int pos = p0 + __ffsll((long long)pm) - 1;
                     const uint32_t ep = b + (uint32_t)pos, p = a.col[ep];
@@ -1614,7 +1628,7 @@ __global__ __launch_bounds__(256) void k_px_import(const uint64_t* in, int64_t n
         const uint64_t v = in[k];
         const uint32_t r = (uint32_t)v;
         if (score[r] < accept_px) continue;
-        const uint32_t p = col[r], x = g2l[(uint32_t)(v >> 38)];
+        const uint32_t p = col[r], x = g2l ? g2l[(uint32_t)(v >> 38)] : (uint32_t)(v >> 38);
         if (x == 0xFFFFFFFFu) continue;                      // not a neighbour of p
         uint32_t lo = row_ptr[p], hi = row_ptr[p + 1];
         const uint32_t pe = hi;
@@ -1674,6 +1688,39 @@ int px_import(gsim_handle* h, const uint64_t* d_in, int64_t n)
                        (const uint8_t*)h->d_rstate, (const uint32_t*)h->sh->d_g2l, h->th.accept_px_threshold,
                        h->x->d_pxm);
     return hip_check(h, hipGetLastError(), "k_px_import");
+}
+
+// Leave's PX lists (Extra::d_pxl) to their pruned peers (local to this
+// handle): handlePrune's acceptPXThreshold on the snapshot, pxConnect's
+// attempts (k_px_import); the lists are consumed.  g2l: a shard's global ->
+// local ids (nullptr: a single engine).
+int px_leave_import(gsim_handle* h, const uint32_t* g2l)
+{
+    if (!h->x || !h->x->d_pxl_n) return GSIM_OK;
+    uint32_t n[2] = {0, 0};
+    hipError_t e = hipMemcpyAsync(n, h->x->d_pxl_n, sizeof(n), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "Leave PX count");
+    if (n[1]) { h->err = "Leave PX list overflow"; return GSIM_ERANGE; }
+    if (!n[0]) return GSIM_OK;
+    hipLaunchKernelGGL(k_px_import, dim3((uint32_t)std::min<int64_t>((n[0] + 255) / 256, 16384)), dim3(256), 0,
+                       h->stream, (const uint64_t*)h->x->d_pxl, (int64_t)n[0], (const double*)h->d_score,
+                       (const uint32_t*)h->d_col, (const uint32_t*)h->d_row_ptr, (const uint8_t*)h->d_rstate, g2l,
+                       h->th.accept_px_threshold, h->x->d_pxm);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemsetAsync(h->x->d_pxl_n, 0, sizeof(n), h->stream);
+    return hip_check(h, e, "k_px_import (Leave)");
+}
+
+bool deliver_wire_px(gsim_handle* h, WirePx* w)
+{
+    if (!h->x || !h->x->d_pxo) return false;
+    uint32_t n[2] = {0, 0};
+    if (hipMemcpyAsync(n, h->x->d_pxl_n, sizeof(n), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+        hipStreamSynchronize(h->stream) != hipSuccess)
+        n[0] = 0;
+    *w = WirePx{h->x->d_pxs, h->x->seed, h->x->d_pxl, h->x->d_pxl_tick, n[0]};
+    return true;
 }
 
 int px_asks(gsim_handle* h, uint64_t* d_out, uint32_t* d_cnt, int64_t cap)
@@ -1765,6 +1812,62 @@ __device__ __forceinline__ bool sub_topic_peer(const HbArgs& a, uint64_t* sub, u
     return (a.rstate[e] & GSIM_ES_CONNECTED) && ((sub[a.col[e]] >> t) & 1ull);
 }
 
+// Leave's sendPrune(p, topic, true) -> makePrune(p, topic, gs.doPX, true)
+// (gossipsub.go:1118, 1132-1133, 1866-1906): the PX list of the PRUNE at row
+// edge ep, getPeers(topic, PrunePeers, xp != p && Score(xp) >= 0) with the
+// live scores after the Leave's Prunes so far (sc[], the observer's row in
+// pxs), the PrunePeers smallest keys in key order.  Kept for the connector
+// (the pruned peer's handlePrune runs with the tick's control: its snapshot
+// after the next refresh) and the wire encoder; a pruned peer of another
+// shard gets its list through the group's PX exchange, as k_px_emit's.
+__device__ void px_leave_list(const HbArgs& a, const uint64_t* sub, uint32_t obs, uint32_t b, uint32_t en, uint32_t ep,
+                              int32_t t)
+{
+    const double* sc = a.pxs;
+    const uint32_t gobs = glob(a, obs);
+    const uint32_t kt = (uint32_t)t + 64u * (ep - b + 1u);
+    const uint32_t p = a.col[ep];
+    const bool remote = a.pxout && (p < a.olo || p >= a.ohi);
+    uint64_t last = 0;
+    for (int k = 0; k < a.prune_peers; ++k) {
+        uint64_t best = ~0ull;
+        uint32_t bx = 0xFFFFFFFFu;
+        for (uint32_t e = b; e < en; ++e) {
+            if (e == ep || !sub_topic_peer(a, const_cast<uint64_t*>(sub), e, t) || sc[e] < 0.0) continue;
+            const uint64_t key = select_key(a.seed, (uint32_t)a.tick, gobs, kt, P_PX_LEAVE, glob(a, a.col[e]), e - b);
+            if ((k > 0 && key <= last) || key >= best) continue;
+            best = key;
+            bx = e;
+        }
+        if (bx == 0xFFFFFFFFu) break;
+        last = best;
+        const uint64_t gx = glob(a, a.col[bx]);
+        if (remote) {
+            const uint32_t d = a.pshard[p];
+            const uint32_t q = atomicAdd(&a.pxcnt[d], 1u);
+            if ((int64_t)q < a.pxcap) a.pxout[(int64_t)d * a.pxcap + q] = (uint64_t)a.xre[ep] | ((uint64_t)t << 32) | (gx << 38);
+            else atomicOr(&a.pxcnt[a.pxK], 1u);
+        } else {
+            const uint32_t q = a.pxl_n[0]++;
+            if ((int64_t)q < a.pxl_cap) {
+                a.pxl[q] = (uint64_t)ep | ((uint64_t)t << 32) | (gx << 38);
+                a.pxl_tick[q] = (uint32_t)a.tick;
+            } else {
+                a.pxl_n[1] = 1;
+            }
+        }
+    }
+}
+
+// Σ row lengths of the pairs' peers (Leave's PX list entries need at most
+// PrunePeers per connection of a leaving peer)
+__global__ void k_pair_degrees(const uint32_t* row_ptr, const uint32_t* pairs, int32_t count, unsigned long long* out)
+{
+    unsigned long long s = 0;
+    for (int32_t q = threadIdx.x; q < count; q += blockDim.x) s += row_ptr[pairs[2 * q] + 1] - row_ptr[pairs[2 * q]];
+    atomicAdd(out, s);
+}
+
 __global__ void k_subscribe(HbArgs a, uint64_t* sub, const uint32_t* pairs, int32_t count, int32_t join)
 {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
@@ -1852,6 +1955,8 @@ __global__ void k_subscribe(HbArgs a, uint64_t* sub, const uint32_t* pairs, int3
             // last IHAVE targets must not be advertised to again
             if (a.gsel)
                 for (uint32_t e = b; e < en; ++e) a.gsel[slot_idx(mi, t, a.E, e)] = 0;
+            if (a.do_px)     // the live scores makePrune's PX filter reads (updated per Prune below)
+                for (uint32_t e = b; e < en; ++e) a.pxs[e] = score_of_record(a, a.rev[e], a.col[e]);
             for (uint32_t e = b; e < en; ++e) {
                 if (!(mf(e) & GSIM_TF_MESH)) continue;
                 if (a.tr.on(p)) a.tr.push(a.now, 0, p, a.col[e], t, GSIM_TRACE_PRUNE, 0);   // tracer.Prune
@@ -1862,9 +1967,13 @@ __global__ void k_subscribe(HbArgs a, uint64_t* sub, const uint32_t* pairs, int3
                             tp->mesh_message_deliveries_threshold, tp->mesh_message_deliveries_cap, sf);
                 sf.store(a);
                 mf(e) &= (uint8_t)~GSIM_TF_MESH;
-                send(e, GSIM_CTL_PRUNE | GSIM_CTL_UNSUB);
+                send(e, (uint8_t)(GSIM_CTL_PRUNE | GSIM_CTL_UNSUB | (a.do_px ? GSIM_CTL_PX : 0)));
                 const int64_t ex = a.now + a.unsub_backoff;   // addBackoff(p, topic, isUnsubscribe)
                 if (bo(e) < ex) bo(e) = ex;
+                if (a.do_px) {
+                    a.pxs[e] = score_of_record(a, rv, a.col[e]);   // tracer.Prune changed this record
+                    px_leave_list(a, sub, p, b, en, e, t);
+                }
             }
         }
     }
@@ -2126,6 +2235,8 @@ int alloc_extra(gsim_handle* h)
         if (e == hipSuccess) e = hipMalloc((void**)&h->x->d_nopx, (size_t)h->e);
         if (e == hipSuccess) e = hipMalloc((void**)&h->x->d_pxc, sizeof(uint32_t) * (1 + 2 * (size_t)h->e));
         if (e == hipSuccess) e = hipMalloc((void**)&h->x->d_pxs, sizeof(double) * (size_t)h->e);
+        if (e == hipSuccess) e = hipMalloc((void**)&h->x->d_pxl_n, 2 * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMemsetAsync(h->x->d_pxl_n, 0, 2 * sizeof(uint32_t), h->stream);
         if (e == hipSuccess) e = hipMemsetAsync(h->x->d_pxo, 0, sizeof(uint64_t) * (size_t)h->n, h->stream);
         if (e == hipSuccess) e = hipMemsetAsync(h->x->d_pxm, 0, (size_t)h->e, h->stream);
         if (e == hipSuccess) e = hipMemsetAsync(h->x->d_nopx, 0, (size_t)h->e, h->stream);
@@ -2148,6 +2259,9 @@ void free_extra(gsim_handle* h)
     if (h->x->d_nopx) (void)hipFree(h->x->d_nopx);
     if (h->x->d_pxc) (void)hipFree(h->x->d_pxc);
     if (h->x->d_pxs) (void)hipFree(h->x->d_pxs);
+    if (h->x->d_pxl) (void)hipFree(h->x->d_pxl);
+    if (h->x->d_pxl_tick) (void)hipFree(h->x->d_pxl_tick);
+    if (h->x->d_pxl_n) (void)hipFree(h->x->d_pxl_n);
     delete h->x;
     h->x = nullptr;
 }
@@ -2240,6 +2354,7 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.prune_peers = h->gp.prune_peers;
     a.accept_px = h->th.accept_px_threshold;
     a.pxo = h->x->d_pxo; a.pxm = h->x->d_pxm; a.nopx = h->x->d_nopx; a.pxs = h->x->d_pxs;
+    a.pxl = h->x->d_pxl; a.pxl_tick = h->x->d_pxl_tick; a.pxl_n = h->x->d_pxl_n; a.pxl_cap = h->x->pxl_cap;
     if (ShardCtx* sh = h->sh; sh && sh->d_pxout && a.do_px) {
         a.pxout = sh->d_pxout; a.pxcnt = sh->d_pxcnt; a.pxcap = sh->pxcap; a.pxK = sh->K;
         a.xre = sh->d_xre; a.pshard = sh->d_pshard;
@@ -2545,6 +2660,46 @@ int gsim_set_subscriptions(gsim_handle* h, const uint32_t* pairs, int32_t count,
     hipError_t e = hipMemcpyAsync(h->d_churn, pairs, sizeof(uint32_t) * 2 * (size_t)count, hipMemcpyHostToDevice,
                                   h->stream);
     if (e != hipSuccess) return hip_check(h, e, "gsim_set_subscriptions");
+    if (!join && h->x->d_pxo) {
+        // room for Leave's PX lists: PrunePeers entries per connection of a leaving peer
+        unsigned long long* d_sum = reinterpret_cast<unsigned long long*>(h->d_churn + 2 * (size_t)count);
+        e = hipMemsetAsync(d_sum, 0, sizeof(unsigned long long), h->stream);
+        if (e == hipSuccess)
+            hipLaunchKernelGGL(k_pair_degrees, dim3(1), dim3(256), 0, h->stream, (const uint32_t*)h->d_row_ptr,
+                               (const uint32_t*)h->d_churn, count, d_sum);
+        unsigned long long sum = 0;
+        uint32_t cur[2] = {0, 0};
+        if (e == hipSuccess) e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(&sum, d_sum, sizeof(sum), hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(cur, h->x->d_pxl_n, sizeof(cur), hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) return hip_check(h, e, "Leave PX room");
+        const int64_t need = (int64_t)cur[0] + (int64_t)sum * std::max(0, h->gp.prune_peers);
+        if (need > h->x->pxl_cap) {
+            const int64_t cap = need + need / 2 + 1024;
+            uint64_t* nl = nullptr;
+            uint32_t* nt = nullptr;
+            e = hipMalloc((void**)&nl, sizeof(uint64_t) * (size_t)cap);
+            if (e == hipSuccess) e = hipMalloc((void**)&nt, sizeof(uint32_t) * (size_t)cap);
+            if (e == hipSuccess && cur[0] && h->x->d_pxl) {
+                e = hipMemcpyAsync(nl, h->x->d_pxl, sizeof(uint64_t) * cur[0], hipMemcpyDeviceToDevice, h->stream);
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(nt, h->x->d_pxl_tick, sizeof(uint32_t) * cur[0], hipMemcpyDeviceToDevice, h->stream);
+                if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+            }
+            if (e != hipSuccess) {
+                if (nl) (void)hipFree(nl);
+                if (nt) (void)hipFree(nt);
+                return hip_check(h, e, "Leave PX lists");
+            }
+            if (h->x->d_pxl) (void)hipFree(h->x->d_pxl);
+            if (h->x->d_pxl_tick) (void)hipFree(h->x->d_pxl_tick);
+            h->x->d_pxl = nl;
+            h->x->d_pxl_tick = nt;
+            h->bytes_allocated += 12 * (size_t)(cap - h->x->pxl_cap);
+            h->x->pxl_cap = cap;
+        }
+    }
     HbArgs a = make_hb_args(h, tick, now, 1);   // ctl_out: the heartbeat's inbox (control round 0)
     hipLaunchKernelGGL(k_subscribe, dim3(1), dim3(64), 0, h->stream, a, h->d_sub, (const uint32_t*)h->d_churn, count,
                        join ? 1 : 0);
@@ -2568,6 +2723,8 @@ int gsim_px_connect(gsim_handle* h, int64_t now, uint32_t* pairs, int64_t cap, i
     *n_connected = 0;
     if (h->e == 0 || !h->x) { h->err = "no graph loaded"; return GSIM_ESTATE; }
     if (!h->x->d_pxm) return GSIM_OK;                     // WithPeerExchange is off
+    int rc0 = px_leave_import(h, nullptr);                 // Leave's PRUNEs: the pruned peers' PX handling
+    if (rc0) return rc0;
     uint32_t* pxc = h->x->d_pxc;
     hipError_t e = hipMemsetAsync(pxc, 0, sizeof(uint32_t), h->stream);
     if (e == hipSuccess) {

@@ -56,6 +56,7 @@ enum Purpose : uint32_t {
     P_PX_GRAFT = 15,   // makePrune's getPeers (GRAFT reply)  gossipsub.go:831-834
     P_GATER = 16,      // the peer gater's rand.Float64()      peer_gater.go:357
     P_JOIN = 17,       // Join's getPeers                     gossipsub.go:1068-1092
+    P_PX_LEAVE = 18,   // makePrune's getPeers (Leave's PRUNE) gossipsub.go:1118, 1866-1906
 };
 
 // Key of a choice made per (observer, other peer, message slot): the other

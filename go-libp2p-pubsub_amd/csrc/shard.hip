@@ -1833,6 +1833,7 @@ int gsim_group_px_connect(gsim_group* g, int64_t now, uint32_t* pairs, int64_t c
         ShardCtx* s = h->sh;
         (void)hipSetDevice(h->device);
         rc = g->take(h, px_import(h, s->d_pxin, total[l]));
+        if (!rc) rc = g->take(h, px_leave_import(h, (const uint32_t*)s->d_g2l));   // Leave's, to owned peers
         if (!rc) rc = g->take(h, px_asks(h, s->d_pxout, s->d_pxcnt, (int64_t)K * s->pxcap));
         if (rc) return rc;
         if (hipMemcpyAsync(s->h_counts, s->d_pxcnt, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||

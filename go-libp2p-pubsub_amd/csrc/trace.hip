@@ -31,6 +31,10 @@ __global__ __launch_bounds__(256) void k_trace_resolve(gsim_trace_event* ev, int
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
         gsim_trace_event x = ev[k];
+        if (x.type == GSIM_TRACE_SEND_RPC || x.type == GSIM_TRACE_RECV_RPC) {   // round << 32 | slot: the id
+            ev[k].msg_id = v.mid[(uint32_t)x.msg_id];
+            continue;
+        }
         if (x.type != kTraceCopy) continue;
         const uint32_t m = (uint32_t)x.msg_id;
         const int64_t g = (int64_t)(x.msg_id >> 32);
@@ -158,8 +162,9 @@ int gsim_trace_read(gsim_handle* h, gsim_trace_event* out, int64_t cap, int64_t*
     cnt -= keep;
     *n = cnt;
     std::sort(out, out + cnt, [](const gsim_trace_event& a, const gsim_trace_event& b) {
-        return std::tie(a.timestamp_ns, a.peer, a.type, a.other, a.topic, a.msg_id) <
-               std::tie(b.timestamp_ns, b.peer, b.type, b.other, b.topic, b.msg_id);
+        // (reason before topic: one IWANT answer's messages stay together, gsim_trace_encode)
+        return std::tie(a.timestamp_ns, a.peer, a.type, a.other, a.reason, a.topic, a.msg_id) <
+               std::tie(b.timestamp_ns, b.peer, b.type, b.other, b.reason, b.topic, b.msg_id);
     });
     return GSIM_OK;
 }

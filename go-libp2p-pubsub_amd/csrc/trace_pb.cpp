@@ -66,7 +66,41 @@ struct Enc {
         const uint64_t b = body(e, &f);
         return 1 + vlen(e.type) + ld(pid_len()) + 1 + vlen((uint64_t)e.timestamp_ns) + (f >= 16 ? 2 : 1) + vlen(b) + b;
     }
+
+    // A message RPC (RECV_RPC / SEND_RPC) of the records [k0, k1): RPCMeta of
+    // its messages, MessageMeta{messageID, topic} each (trace.go:326-345)
+    uint64_t mmeta(const gsim_trace_event& e) const { return ld(8) + ld(topic_len(e.topic)); }
+    uint64_t meta(const gsim_trace_event* ev, int64_t k0, int64_t k1) const
+    {
+        uint64_t s = 0;
+        for (int64_t k = k0; k < k1; ++k) s += ld(mmeta(ev[k]));
+        return s;
+    }
+    uint64_t rpc_body(const gsim_trace_event* ev, int64_t k0, int64_t k1) const
+    {
+        return ld(pid_len()) + ld(meta(ev, k0, k1));             // receivedFrom / sendTo, meta
+    }
+    uint64_t rpc_event(const gsim_trace_event* ev, int64_t k0, int64_t k1) const
+    {
+        const gsim_trace_event& e = ev[k0];
+        const uint64_t b = rpc_body(ev, k0, k1);
+        return 1 + vlen(e.type) + ld(pid_len()) + 1 + vlen((uint64_t)e.timestamp_ns) + 1 + vlen(b) + b;
+    }
 };
+
+bool is_rpc(const gsim_trace_event& e) { return e.type == GSIM_TRACE_RECV_RPC || e.type == GSIM_TRACE_SEND_RPC; }
+
+// the records one TraceEvent covers: [k, end) -- an IWANT answer's messages
+// (reason 1) to one peer in one round are one RPC, everything else one record
+int64_t unit_end(const gsim_trace_event* ev, int64_t n, int64_t k)
+{
+    int64_t q = k + 1;
+    if (is_rpc(ev[k]) && ev[k].reason == 1)
+        while (q < n && ev[q].type == ev[k].type && ev[q].reason == 1 && ev[q].timestamp_ns == ev[k].timestamp_ns &&
+               ev[q].peer == ev[k].peer && ev[q].other == ev[k].other)
+            ++q;
+    return q;
+}
 
 struct W {
     uint8_t* p;
@@ -120,17 +154,45 @@ extern "C" int gsim_trace_encode(const gsim_trace_event* ev, int64_t n, const gs
     if (names && names->peer_id_len && !names->peer_ids) return GSIM_EINVAL;
     Enc c{names, proto ? proto : "", proto ? std::strlen(proto) : 0};
     uint64_t total = 0;
-    for (int64_t k = 0; k < n; ++k) {
+    for (int64_t k = 0; k < n;) {
+        const int64_t k1 = unit_end(ev, n, k);
         int f = 0;
         (void)c.body(ev[k], &f);
-        if (!f) return GSIM_EINVAL;
-        total += ld(c.event(ev[k]));                        // TraceEventBatch.batch = 1
+        if (!f && !is_rpc(ev[k])) return GSIM_EINVAL;
+        for (int64_t q = k; q < k1; ++q)
+            if (ev[q].topic < 0 && is_rpc(ev[q])) return GSIM_EINVAL;
+        total += ld(is_rpc(ev[k]) ? c.rpc_event(ev, k, k1) : c.event(ev[k]));   // TraceEventBatch.batch = 1
+        k = k1;
     }
     *len = total;
     if (total > cap || (total && !out)) return GSIM_ERANGE;
     W w{out};
-    for (int64_t k = 0; k < n; ++k) {
+    for (int64_t k = 0; k < n;) {
+        const int64_t k1 = unit_end(ev, n, k);
         const gsim_trace_event& e = ev[k];
+        if (is_rpc(e)) {
+            w.tag(1, 2);
+            w.varint(c.rpc_event(ev, k, k1));
+            w.tag(1, 0);                                     // type
+            w.varint(e.type);
+            put_peer(w, c, 2, e.peer);                       // peerID
+            w.tag(3, 0);                                     // timestamp
+            w.varint((uint64_t)e.timestamp_ns);
+            w.tag(e.type == GSIM_TRACE_RECV_RPC ? 10 : 11, 2);   // recvRPC = 10 / sendRPC = 11
+            w.varint(c.rpc_body(ev, k, k1));
+            put_peer(w, c, 1, e.other);                      // receivedFrom / sendTo
+            w.tag(2, 2);                                     // meta
+            w.varint(c.meta(ev, k, k1));
+            for (int64_t q = k; q < k1; ++q) {               // RPCMeta.messages = 1
+                w.tag(1, 2);
+                w.varint(c.mmeta(ev[q]));
+                put_mid(w, 1, ev[q].msg_id);
+                put_topic(w, c, 2, ev[q].topic);
+            }
+            k = k1;
+            continue;
+        }
+        k = k1;
         w.tag(1, 2);
         w.varint(c.event(e));
         w.tag(1, 0);                                         // type
@@ -430,3 +492,34 @@ extern "C" int gsim_trace_rpc_encode(const uint8_t* rpcs, const gsim_wire_ref* r
     if (!batch.s.empty()) std::memcpy(out, batch.s.data(), batch.s.size());
     return GSIM_OK;
 }
+
+// PBTracer's file (tracer.go:130-179): protoio.NewDelimitedWriter writes each
+// TraceEvent as its uvarint length then its bytes.  A TraceEventBatch holds the
+// same events as field 1 entries (tag 0x0a, length, bytes): dropping each tag
+// gives the delimited stream.
+extern "C" int gsim_trace_delimited(const uint8_t* batch, uint64_t len, uint8_t* out, uint64_t cap, uint64_t* n)
+{
+    if (!n || (len && !batch)) return GSIM_EINVAL;
+    Rd r{batch, batch + len};
+    uint64_t total = 0;
+    int f, wt;
+    const uint8_t* q;
+    uint64_t L, v;
+    while (r.more()) {
+        if (!r.field(&f, &wt, &q, &L, &v) || f != 1 || wt != 2) return GSIM_EINVAL;
+        total += vlen(L) + L;
+    }
+    if (!r.ok) return GSIM_EINVAL;
+    *n = total;
+    if (total > cap || (total && !out)) return GSIM_ERANGE;
+    W w{out};
+    r = Rd{batch, batch + len};
+    while (r.more()) {
+        r.field(&f, &wt, &q, &L, &v);
+        w.varint(L);
+        if (L) std::memcpy(w.p, q, L);
+        w.p += L;
+    }
+    return GSIM_OK;
+}
+

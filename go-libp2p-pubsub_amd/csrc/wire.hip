@@ -32,6 +32,7 @@
 
 #include "gsim_internal.h"
 #include "gsim_wire.h"
+#include "philox.h"
 
 namespace gsim {
 namespace {
@@ -69,8 +70,23 @@ struct WireArgs {
     gsim_wire_ref* refs;
     int32_t max_ihave;            // MaxIHaveLength
     uint32_t* err;                // [0] bit 0: an IHAVE target without ids; bit 1: a window longer than
-                                  // MaxIHaveLength; bit 2: a PRUNE carrying peer exchange
+                                  // MaxIHaveLength
+    // makePrune's PX lists (gossipsub.go:1866-1906): a heartbeat PRUNE's is recomputed from the
+    // live scores its k_px_emit read (pxs) and the same Philox keys; a Leave PRUNE's
+    // (GSIM_CTL_UNSUB) was kept at the Leave (pxl entries of this tick)
+    const uint8_t* rstate;
+    const uint64_t* sub;
+    const double* pxs;
+    uint64_t seed;
+    int64_t tick;
+    int32_t prune_peers;
+    const uint64_t* pxl;
+    const uint32_t* pxl_tick;
+    uint32_t n_pxl;
+    uint64_t unsub_backoff;       // UnsubscribeBackoff / 1s: a Leave PRUNE's Backoff
 };
+
+constexpr int kWirePxMax = 64;    // PrunePeers the encoder lists (more: refused)
 
 __device__ __forceinline__ uint32_t vlen(uint64_t v)
 {
@@ -143,9 +159,50 @@ __device__ __forceinline__ uint64_t ihave_body(const WireArgs& a, int32_t t, uin
     return name_field(a, t) + (uint64_t)n * ld(a.pid_len + 8);
 }
 
-__device__ __forceinline__ uint64_t prune_body(const WireArgs& a, int32_t t)
+// The PX list of the PRUNE p -> col[e] in topic t (ctl: its inbox bits), in
+// list order; returns its length.
+__device__ uint32_t px_list(const WireArgs& a, int64_t e, uint32_t p, int32_t t, uint8_t ctl, uint32_t* out)
 {
-    return name_field(a, t) + 1 + vlen(a.backoff);
+    if (!(ctl & GSIM_CTL_PX)) return 0;
+    uint32_t n = 0;
+    if (ctl & GSIM_CTL_UNSUB) {                              // Leave's: kept at the Leave
+        for (uint32_t q = 0; q < a.n_pxl && n < kWirePxMax; ++q) {
+            const uint64_t v = a.pxl[q];
+            if ((uint32_t)v == (uint32_t)e && (int32_t)((v >> 32) & 63u) == t && a.pxl_tick[q] == (uint32_t)a.tick)
+                out[n++] = (uint32_t)(v >> 38);
+        }
+        return n;
+    }
+    // the heartbeat's: getPeers(topic, PrunePeers, xp != p && Score(xp) >= 0) on the live
+    // scores after the heartbeat, the PrunePeers smallest keys (k_px_emit)
+    const uint32_t b = a.row_ptr[p], en = a.row_ptr[p + 1];
+    const uint32_t kt = (uint32_t)t + 64u * ((uint32_t)(e - b) + 1u);
+    uint64_t last = 0;
+    for (int k = 0; k < a.prune_peers && k < kWirePxMax; ++k) {
+        uint64_t best = ~0ull;
+        uint32_t bx = 0xFFFFFFFFu;
+        for (uint32_t q = b; q < en; ++q) {
+            if ((int64_t)q == e) continue;
+            const uint32_t x = a.col[q];
+            if (!(a.rstate[q] & GSIM_ES_CONNECTED) || !((a.sub[x] >> t) & 1ull) || a.pxs[q] < 0.0) continue;
+            const uint64_t key = select_key(a.seed, (uint32_t)a.tick, p, kt, P_PX, x, q - b);
+            if ((k > 0 && key <= last) || key >= best) continue;
+            best = key;
+            bx = x;
+        }
+        if (bx == 0xFFFFFFFFu) break;
+        last = best;
+        out[n++] = bx;
+    }
+    return n;
+}
+
+__device__ __forceinline__ uint32_t pid_bytes(const WireArgs& a) { return a.pid_len ? a.pid_len : 4u; }
+
+__device__ __forceinline__ uint64_t prune_body(const WireArgs& a, int32_t t, uint8_t ctl, uint32_t npx)
+{
+    const uint64_t bo = (ctl & GSIM_CTL_UNSUB) ? a.unsub_backoff : a.backoff;
+    return name_field(a, t) + (uint64_t)npx * ld(ld(pid_bytes(a))) + 1 + vlen(bo);
 }
 
 // ControlMessage body of edge e (p -> col[e]); 0 and *any = false: no RPC
@@ -160,9 +217,12 @@ __device__ uint64_t control_body(const WireArgs& a, int64_t e, uint32_t p, bool*
         const uint8_t c = ctl_at(a, t, re, mq);
         if (gsel_at(a, t, e, mp)) { s += ld(ihave_body(a, t, (uint32_t)a.n_pt[base + t])); x = true; }
         if (c & GSIM_CTL_GRAFT) { s += ld(name_field(a, t)); x = true; }
-        if (c & GSIM_CTL_PRUNE) { s += ld(prune_body(a, t)); x = true; }
-        // makePrune's PX peer list (gossipsub.go:1878-1903) is not kept per PRUNE
-        if ((c & GSIM_CTL_PRUNE) && (c & GSIM_CTL_PX)) atomicOr(&a.err[0], 4u);
+        if (c & GSIM_CTL_PRUNE) {
+            uint32_t px[kWirePxMax];
+            const uint32_t npx = px_list(a, e, p, t, c, px);
+            s += ld(prune_body(a, t, c, npx));
+            x = true;
+        }
     }
     *any = x;
     return s;
@@ -283,12 +343,27 @@ __global__ void k_wire_write(WireArgs a)
         write_name(a, w, 0x0a, t);                         // ControlGraft.topicID = 1
     }
     for (int32_t t = 0; t < a.T; ++t) {                    // ControlMessage.prune = 4
-        if (!(ctl_at(a, t, re, mq) & GSIM_CTL_PRUNE)) continue;
+        const uint8_t c = ctl_at(a, t, re, mq);
+        if (!(c & GSIM_CTL_PRUNE)) continue;
+        uint32_t px[kWirePxMax];
+        const uint32_t npx = px_list(a, e, p, t, c, px);
         w.byte(0x22);
-        w.varint(prune_body(a, t));
+        w.varint(prune_body(a, t, c, npx));
         write_name(a, w, 0x0a, t);                         // ControlPrune.topicID = 1
+        for (uint32_t q = 0; q < npx; ++q) {               // ControlPrune.peers = 2: PeerInfo{peerID = 1}
+            const uint32_t L = pid_bytes(a);
+            w.byte(0x12);
+            w.varint(ld(L));
+            w.byte(0x0a);
+            w.varint(L);
+            if (a.pid_len) {
+                w.raw(a.peer_ids + (int64_t)px[q] * a.pid_len, a.pid_len);
+            } else {
+                for (int sh = 24; sh >= 0; sh -= 8) w.byte((uint8_t)(px[q] >> sh));
+            }
+        }
         w.byte(0x18);                                      // ControlPrune.backoff = 3
-        w.varint(a.backoff);
+        w.varint((c & GSIM_CTL_UNSUB) ? a.unsub_backoff : a.backoff);
     }
     gsim_wire_ref r;
     r.from = p;
@@ -439,6 +514,16 @@ extern "C" int gsim_wire_heartbeat(gsim_handle* h, int64_t tick, uint32_t p0, ui
     a.backoff = names->prune_backoff_s;
     a.max_ihave = h->gp.max_ihave_length;
     a.out = d_out; a.refs = d_refs;
+    a.unsub_backoff = (uint64_t)(h->gp.unsubscribe_backoff_ns / 1000000000);
+    WirePx wp{};
+    if (deliver_wire_px(h, &wp)) {                  // WithPeerExchange: the lists' inputs
+        if (h->gp.prune_peers > kWirePxMax) {
+            h->err = "PrunePeers above " + std::to_string(kWirePxMax) + ": PX lists are not encoded";
+            return finish(GSIM_ERANGE);
+        }
+        a.rstate = h->d_rstate; a.sub = h->d_sub; a.pxs = wp.pxs; a.seed = wp.seed; a.tick = tick;
+        a.prune_peers = h->gp.prune_peers; a.pxl = wp.pxl; a.pxl_tick = wp.pxl_tick; a.n_pxl = wp.n_pxl;
+    }
     if (!a.ctl) return finish(GSIM_ESTATE);
 
     constexpr int B = 256;
@@ -466,10 +551,7 @@ extern "C" int gsim_wire_heartbeat(gsim_handle* h, int64_t tick, uint32_t p0, ui
         h->err = "a gossip window holds more than MaxIHaveLength ids: emitGossip's per-target subsets are not encoded";
         return finish(GSIM_ESTATE);
     }
-    if (err & 4u) {
-        h->err = "a PRUNE carries peer exchange: its PX peer list is not encoded";
-        return finish(GSIM_ESTATE);
-    }
+
     *n_rpcs = tot_rpcs;
     *bytes = tot_bytes;
     if (tot_bytes > out_cap || (int64_t)tot_rpcs > ref_cap) {

@@ -100,6 +100,7 @@ class CPeerGaterParams(Structure):
 TRACE_PUBLISH_MESSAGE, TRACE_REJECT_MESSAGE, TRACE_DUPLICATE_MESSAGE, TRACE_DELIVER_MESSAGE = 0, 1, 2, 3
 TRACE_ADD_PEER, TRACE_REMOVE_PEER, TRACE_GRAFT, TRACE_PRUNE = 4, 5, 11, 12
 TRACE_JOIN, TRACE_LEAVE = 9, 10
+TRACE_RECV_RPC, TRACE_SEND_RPC = 6, 7          # reason 0: a forwarded message, 1: an IWANT answer
 
 
 # (name, restype, argtypes) for every symbol include/gsim.h declares.
@@ -317,6 +318,7 @@ SIGNATURES = [
     ("gsim_group_profile_read", c_int32, [c_void_p, c_void_p, c_void_p, c_int32]),
     # gsim_wire.h
     ("gsim_wire_size", c_uint64, [POINTER(CWireRpc)]),
+    ("gsim_trace_delimited", c_int32, [c_void_p, c_uint64, c_void_p, c_uint64, POINTER(c_uint64)]),
     ("gsim_wire_decode", c_int32, [c_void_p, c_uint64, POINTER(CWireTables), POINTER(CWireRpc)]),
     ("gsim_wire_frames", c_int32, [c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_int32, POINTER(c_int32),
                                    POINTER(c_uint64)]),

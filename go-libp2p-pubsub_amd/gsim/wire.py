@@ -406,3 +406,21 @@ def trace_rpc_batch(rpcs, topic_names=(), peer_ids: Optional[np.ndarray] = None,
     if rc != 0:
         raise WireError(rc, "gsim_trace_rpc_encode")
     return out.raw[:n.value]
+
+
+def pb_tracer_stream(batch: bytes) -> bytes:
+    """PBTracer's trace file (tracer.go:130-179) of a TraceEventBatch
+    (trace_batch / trace_rpc_batch output): each TraceEvent varint-delimited
+    (gsim_trace_delimited)."""
+    lib = _abi.load()
+    src = ctypes.create_string_buffer(bytes(batch), max(1, len(batch)))
+    n = ctypes.c_uint64()
+    rc = lib.gsim_trace_delimited(src, len(batch), None, 0, ctypes.byref(n))
+    if rc not in (0, _abi.GSIM_ERANGE):
+        raise WireError(rc, "not a TraceEventBatch")
+    out = ctypes.create_string_buffer(max(1, n.value))
+    rc = lib.gsim_trace_delimited(src, len(batch), out, n.value, ctypes.byref(n))
+    if rc != 0:
+        raise WireError(rc, "gsim_trace_delimited")
+    return out.raw[:n.value]
+

@@ -443,17 +443,32 @@ int gsim_census(gsim_handle* h, int64_t* out8);
  *   DUPLICATE_MESSAGE a copy of a message already seen (136-164)
  *   DELIVER_MESSAGE   first reception of an accepted message (166-194)
  *   ADD_PEER / REMOVE_PEER   connections made or lost (196-248)
+ *   RECV_RPC / SEND_RPC  the message RPCs (trace.go:250-297): every copy a
+ *                     router forwards is its own RPC (Publish -> sendRPC per
+ *                     peer, gossipsub.go:1032-1044, 1195-1200), SEND_RPC at
+ *                     the sender (other = the receiver) and RECV_RPC at the
+ *                     receiver (other = the sender; handleIncomingRPC,
+ *                     pubsub.go:1039, before AcceptFrom), reason 0; an
+ *                     advertiser's IWANT answers to one requester in a round
+ *                     are one RPC (handleIWant, gossipsub.go:700-739): reason
+ *                     1, sent the round before they arrive, one record per
+ *                     message (gsim_trace_encode joins them).  The
+ *                     heartbeat's control / IHAVE RPCs are traced from their
+ *                     encoding (gsim_trace_rpc_encode, include/gsim_wire.h)
+ *   JOIN / LEAVE      gsim_set_subscriptions (1047-1124)
  *   GRAFT / PRUNE     the router adds / drops a mesh link: heartbeat,
  *                     handleGraft, handlePrune (468-520)
- * RPC-level events (RECV_RPC, SEND_RPC, DROP_RPC) and JOIN/LEAVE are not
- * produced: the engine models no RPC framing and no subscription changes.
- * Copies dropped by AcceptFrom produce no event, as in pushMsg. */
+ * Not produced: DROP_RPC (no outbound queue is modelled) and the IWANT
+ * requests' RPCs.  Copies dropped by AcceptFrom produce no message event, as
+ * in pushMsg. */
 #define GSIM_TRACE_PUBLISH_MESSAGE   0
 #define GSIM_TRACE_REJECT_MESSAGE    1
 #define GSIM_TRACE_DUPLICATE_MESSAGE 2
 #define GSIM_TRACE_DELIVER_MESSAGE   3
 #define GSIM_TRACE_ADD_PEER          4
 #define GSIM_TRACE_REMOVE_PEER       5
+#define GSIM_TRACE_RECV_RPC          6   /* a message RPC received: reason 0 a forwarded message, 1 an IWANT answer */
+#define GSIM_TRACE_SEND_RPC          7   /* a message RPC sent (same reasons)                                     */
 #define GSIM_TRACE_JOIN              9
 #define GSIM_TRACE_LEAVE             10
 #define GSIM_TRACE_GRAFT             11
@@ -475,7 +490,7 @@ typedef struct gsim_trace_event {
 int gsim_trace_config(gsim_handle* h, uint32_t peer_lo, uint32_t peer_hi, int64_t cap);
 
 /* The events traced since the last call, sorted by (timestamp, peer, type,
- * other, topic, msg_id); *n is their number (GSIM_ERANGE, nothing lost from
+ * other, reason, topic, msg_id); *n is their number (GSIM_ERANGE, nothing lost from
  * the buffer, when it exceeds cap; GSIM_ERANGE when the device buffer
  * overflowed). */
 int gsim_trace_read(gsim_handle* h, gsim_trace_event* out, int64_t cap, int64_t* n);

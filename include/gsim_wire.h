@@ -232,6 +232,13 @@ int gsim_trace_encode(const gsim_trace_event* ev, int64_t n, const gsim_wire_nam
 int gsim_trace_rpc_encode(const uint8_t* rpcs, const gsim_wire_ref* refs, int64_t n, const gsim_wire_names* names,
                           int64_t timestamp_ns, int32_t which, uint8_t* out, uint64_t cap, uint64_t* len);
 
+/* PBTracer's output (tracer.go:130-179): the events of a TraceEventBatch
+ * (gsim_trace_encode / gsim_trace_rpc_encode output, len bytes) as the
+ * varint-delimited TraceEvent stream protoio's DelimitedWriter writes to the
+ * trace file.  *n: the bytes (GSIM_ERANGE with *n = the size needed when cap
+ * is short; GSIM_EINVAL for bytes that are not a TraceEventBatch). */
+int gsim_trace_delimited(const uint8_t* batch, uint64_t len, uint8_t* out, uint64_t cap, uint64_t* n);
+
 #ifdef __cplusplus
 }
 #endif

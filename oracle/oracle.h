@@ -221,6 +221,8 @@ enum {
     ORC_EV_LEAVE = 18,       /* a: router, topic, x: now    tracer.Leave             */
     ORC_EV_PX_PEER = 19,     /* a: pruner, b: a peer of the PRUNE's PX list, topic,
                                 mid: the pruned peer, g: its rank in the list (makePrune) */
+    ORC_EV_RPC_MSG = 20,     /* a: sender, b: receiver, mid, topic, g: the round it arrives in,
+                                x: 0 a forwarded copy (sent in g), 1 an IWANT answer (sent in g - 1) */
 };
 typedef struct orc_event { int32_t kind, topic; uint32_t a, b; int64_t g; uint64_t mid; int64_t x; } orc_event;
 void    orc_msgs_log(orc_msgs* m, int32_t on);

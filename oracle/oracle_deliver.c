@@ -383,12 +383,17 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
             }
             if (!(s->estate[e] & GSIM_ES_CONNECTED)) continue;
             if (i == from || i == origin) continue;
+            orc_log(m, ORC_EV_RPC_MSG, j, i, slot, t, g, 0);     /* the copy's RPC (sendRPC, gossipsub.go:1195-1200) */
             ar_push(p, i, slot, s->rev[e]);
         }
     }
     p->nfp = 0;
     /* IWANT responses sent in the previous round arrive with them */
-    for (int64_t q = 0; q < p->ngr; ++q) ar_push(p, p->gr[q].recv, p->gr[q].slot, p->gr[q].er);
+    for (int64_t q = 0; q < p->ngr; ++q) {
+        orc_log(m, ORC_EV_RPC_MSG, s->col[p->gr[q].er], p->gr[q].recv, p->gr[q].slot, (int32_t)m->topic[p->gr[q].slot],
+                g, 1);
+        ar_push(p, p->gr[q].recv, p->gr[q].slot, p->gr[q].er);
+    }
     p->ngr = 0;
 
     /* 2. receivers handle the copies, in canonical order: by receiver

@@ -449,7 +449,9 @@ void orc_heartbeat_gossip(orc_net* s, orc_msgs* m, uint64_t tick, int64_t now, u
             for (int32_t t = 0; t < s->t; ++t) {
                 h.t = t;
                 for (uint32_t e = h.b; e < h.en; ++e)
-                    if (out[(int64_t)t * s->e + s->rev[e]] & GSIM_CTL_PX) px_emit(&h, e, 1, P_PX, tick, 0);
+                    /* (a Leave's PRUNE in the same inbox was listed at the Leave) */
+                    if ((out[(int64_t)t * s->e + s->rev[e]] & (GSIM_CTL_PX | GSIM_CTL_UNSUB)) == GSIM_CTL_PX)
+                        px_emit(&h, e, 1, P_PX, tick, 0);
             }
         fanout(&h, m);
     }

@@ -114,6 +114,48 @@ def test_leave_prunes_with_the_unsubscribe_backoff():
         assert st.backoff[0, re] == now + gp.UnsubscribeBackoff
 
 
+def test_leave_prunes_carry_peer_exchange():
+    """With WithPeerExchange, Leave's sendPrune(p, topic, true) builds its
+    PRUNE with makePrune(p, topic, gs.doPX, true) (gossipsub.go:1118,
+    1132-1133): a PX list of up to PrunePeers topic peers other than p with a
+    live score >= 0 (1866-1906).  The pruned peers take it up with the tick's
+    control: at the connector, each one that scores the leaver >=
+    acceptPXThreshold asks for every listed peer it knows and is not
+    connected to."""
+    from gsim.engine import random_regular
+    net = random_regular(300, 12, seed=11, n_topics=2)
+    gp = GossipSubParams(D=6, Dlo=5, Dhi=12, PeerExchange=True, PrunePeers=4)
+    from test_fanout import TH
+    st = ob.NetState(net, delivery_params(2), thresholds=TH, gossip=gp)
+    msgs = ob.Msgs(net.n, 2, 64, R, T0, Second)
+    for kk in range(1, 3):
+        tick(st, msgs, kk)
+    o = 150
+    b, en = row(net, o)
+    mesh = b + np.nonzero(st.tflags[0, b:en] & _abi.TF_MESH)[0]
+    assert len(mesh) >= gp.Dlo
+    msgs.log()
+    now = tick_time(3) - Second // 2
+    st.set_subscriptions([(o, 0)], False, 3, now, SEED)
+    ev = msgs.events()
+    px = ev[ev["kind"] == ob.EV_PX_PEER]
+    lib = ob.load()
+    for e in mesh:
+        c = st.ctl[0, 0, st.rev[e]]
+        assert (c & _abi.CTL_PRUNE) and (c & _abi.CTL_UNSUB) and (c & _abi.CTL_PX)
+        lst = px[px["mid"] == net.col[e]]
+        assert len(lst) == gp.PrunePeers and list(lst["g"]) == list(range(gp.PrunePeers))
+        assert all(lst["a"] == o) and all(lst["topic"] == 0)
+        assert net.col[e] not in lst["b"], "xp != p"
+        for y in lst["b"]:
+            ey = b + int(np.searchsorted(net.col[b:en], y))
+            assert net.col[ey] == y and (net.sub[y] & np.uint64(1))
+            assert lib.orc_score_edge(st.view(), ey) >= 0
+    # the connector: a listed peer whose address the pruned peer knows is one it
+    # is connected to here (no churn): no connection attempt comes of the lists
+    assert len(st.px_connect(tick_time(3) + Second // 2)) == 0
+
+
 def test_a_router_drops_messages_of_a_topic_it_left():
     net, st = fanout_net()
     msgs = ob.Msgs(net.n, 2, 64, R, T0, Second)
@@ -130,8 +172,9 @@ def test_a_router_drops_messages_of_a_topic_it_left():
 # ---- GPU parity -------------------------------------------------------------------
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("topic_slots,shards", [(0, 0), (80, 0), (0, 3)])
-def test_join_leave_bit_exact(require_gpu, topic_slots, shards):
+@pytest.mark.parametrize("topic_slots,shards,px", [(0, 0, False), (80, 0, False), (0, 3, False), (0, 0, True),
+                                                   (0, 3, True)])
+def test_join_leave_bit_exact(require_gpu, topic_slots, shards, px):
     """Joins (with and without a fanout) and Leaves between ticks, fanout
     publishers, gossip, churn and the trace: every state array, the seen-set,
     the totals and the JOIN / LEAVE / GRAFT / PRUNE events bit-exact — on one
@@ -143,7 +186,7 @@ def test_join_leave_bit_exact(require_gpu, topic_slots, shards):
     n, k, T = 900, 16, 3
     rng = np.random.default_rng(515 + topic_slots)
     params = beacon_params(T)
-    gp = GossipSubParams(D=6, Dlo=5, Dhi=10, Dscore=3, Dout=2, FanoutTTL=30 * Second)
+    gp = GossipSubParams(D=6, Dlo=5, Dhi=10, Dscore=3, Dout=2, FanoutTTL=30 * Second, PeerExchange=px)
     th = PeerScoreThresholds(GossipThreshold=-50, PublishThreshold=-100, GraylistThreshold=-400)
     net = random_regular(n, k, seed=91, n_topics=T)
     st = ob.NetState(net, params, thresholds=th, gossip=gp)

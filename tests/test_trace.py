@@ -38,10 +38,27 @@ def _pid(p, peer_ids):
     return bytes(peer_ids[p]) if peer_ids is not None else int(p).to_bytes(4, "big")
 
 
+def _rpc_units(recs):
+    """The TraceEvents of the records: an IWANT answer's messages (RPC
+    records of reason 1 with the same time, router, type and peer, adjacent
+    in gsim_trace_read's order) are one RPC, every other record one event."""
+    out, k = [], 0
+    while k < len(recs):
+        q = k + 1
+        r = recs[k]
+        if int(r["type"]) in (_abi.TRACE_RECV_RPC, _abi.TRACE_SEND_RPC) and int(r["reason"]) == 1:
+            while q < len(recs) and all(recs[q][f] == r[f] for f in ("type", "reason", "timestamp", "peer", "other")):
+                q += 1
+        out.append(recs[k:q])
+        k = q
+    return out
+
+
 def _expected_batch(recs, names, peer_ids, proto=b"/meshsub/1.1.0"):
     C = wo.trace_pb()
     batch = C["TraceEventBatch"]()
-    for r in recs:
+    for unit in _rpc_units(recs):
+        r = unit[0]
         e = batch.batch.add()
         typ = int(r["type"])
         e.type = typ
@@ -50,6 +67,18 @@ def _expected_batch(recs, names, peer_ids, proto=b"/meshsub/1.1.0"):
         mid = int(r["msg_id"]).to_bytes(8, "big")
         other = _pid(int(r["other"]), peer_ids)
         topic = names[int(r["topic"])].decode() if int(r["topic"]) >= 0 else None
+        if typ in (_abi.TRACE_RECV_RPC, _abi.TRACE_SEND_RPC):
+            # RecvRPC{receivedFrom, meta} / SendRPC{sendTo, meta}, RPCMeta.messages (trace.go:250-345)
+            x = e.recvRPC if typ == _abi.TRACE_RECV_RPC else e.sendRPC
+            if typ == _abi.TRACE_RECV_RPC:
+                x.receivedFrom = other
+            else:
+                x.sendTo = other
+            for y in unit:
+                mm = x.meta.messages.add()
+                mm.messageID = int(y["msg_id"]).to_bytes(8, "big")
+                mm.topic = names[int(y["topic"])].decode()
+            continue
         if typ == _abi.TRACE_PUBLISH_MESSAGE:
             e.publishMessage.messageID, e.publishMessage.topic = mid, topic
         elif typ == _abi.TRACE_REJECT_MESSAGE:
@@ -77,7 +106,7 @@ def _expected_batch(recs, names, peer_ids, proto=b"/meshsub/1.1.0"):
 
 
 def _random_records(rng, n, T, N):
-    types = [0, 1, 2, 3, 4, 5, 9, 10, 11, 12]
+    types = [0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 11, 12]
     recs = np.zeros(n, dtype=Engine.TRACE_DTYPE)
     for k in range(n):
         typ = types[rng.integers(0, len(types))]
@@ -87,8 +116,30 @@ def _random_records(rng, n, T, N):
         recs[k]["other"] = rng.integers(0, N)
         recs[k]["msg_id"] = int(rng.integers(0, 1 << 63))
         recs[k]["topic"] = -1 if typ in (4, 5) else rng.integers(0, T)
-        recs[k]["reason"] = rng.integers(1, 5) if typ == 1 else 0
+        recs[k]["reason"] = rng.integers(1, 5) if typ == 1 else rng.integers(0, 2) if typ in (6, 7) else 0
+        if typ in (6, 7) and recs[k]["reason"] == 1 and k > 0 and rng.random() < 0.6:
+            # another message of the same IWANT answer
+            for f in ("type", "timestamp", "peer", "other", "reason"):
+                recs[k][f] = recs[k - 1][f] if recs[k - 1]["type"] == typ else recs[k][f]
     return recs
+
+
+def test_pb_tracer_stream():
+    """PBTracer's file (tracer.go:130-179, protoio's DelimitedWriter): every
+    TraceEvent of the batch, varint-delimited, in order."""
+    C = wo.trace_pb()
+    rng = np.random.default_rng(29)
+    names = [f"t{t}".encode() for t in range(3)]
+    recs = _random_records(rng, 150, 3, 200)
+    batch = wire.trace_batch(recs, names)
+    frames, used = wire.frames(wire.pb_tracer_stream(batch))
+    want = C["TraceEventBatch"].FromString(batch).batch
+    assert used == len(wire.pb_tracer_stream(batch)) and len(frames) == len(want) > 0
+    for f, w in zip(frames, want):
+        assert C["TraceEvent"].FromString(f) == w
+    assert wire.pb_tracer_stream(b"") == b""
+    with pytest.raises(wire.WireError):
+        wire.pb_tracer_stream(b"\x08\x01")
 
 
 @pytest.mark.parametrize("with_ids", [False, True])
@@ -180,7 +231,7 @@ def test_trace_bit_exact(require_gpu, lo, hi):
     log = []
     run_parity(net, params, th, gp, st, ticks, sched, ring=512, churn=churn, trace=(lo, hi), trace_log=log)
     total = np.sum(log, axis=0)
-    for typ in (0, 1, 2, 3, 4, 5, 11, 12):
+    for typ in (0, 1, 2, 3, 4, 5, 6, 7, 11, 12):
         assert total[typ] > 0, f"event type {typ} traced"
 
 
@@ -261,9 +312,14 @@ def test_trace_encode_rejects_unknown_types_and_short_buffers():
     import ctypes
     names = [b"t0"]
     recs = np.zeros(1, dtype=Engine.TRACE_DTYPE)
-    recs[0]["type"] = 6                    # RECV_RPC: not produced by the engine
+    recs[0]["type"] = 8                    # DROP_RPC: not produced by the engine
     with pytest.raises(wire.WireError):
         wire.trace_batch(recs, names)
+    recs[0]["type"] = 6                    # RECV_RPC without a topic: malformed
+    recs[0]["topic"] = -1
+    with pytest.raises(wire.WireError):
+        wire.trace_batch(recs, names)
+    recs[0]["topic"] = 0
     recs[0]["type"] = _abi.TRACE_REMOVE_PEER
     lib = _abi.load()
     nm = _abi.CWireNames()

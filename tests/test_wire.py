@@ -20,7 +20,7 @@ import numpy as np
 import pytest
 
 from conftest import REPO
-from gsim import wire
+from gsim import _abi, wire
 
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 import wire_oracle as wo  # noqa: E402  (test infrastructure)
@@ -373,10 +373,14 @@ def test_frames_split_a_delimited_stream():
 # ---- GPU ----------------------------------------------------------------------------
 
 
-def expected_heartbeat_rpcs(net, st, msgs, mcaches, lib, T, names, backoff, p0, p1, peer_ids=None):
+def expected_heartbeat_rpcs(net, st, msgs, mcaches, lib, T, names, backoff, p0, p1, peer_ids=None, px=None,
+                            unsub_backoff=None):
     """CPU build of the heartbeat RPCs of senders [p0, p1): GRAFT/PRUNE from
     the oracle's inbox (parity 0, the receiver's edge), IHAVE from its
-    emitGossip marks, ids from the pinned mcaches (GetGossipIDs order)."""
+    emitGossip marks, ids from the pinned mcaches (GetGossipIDs order).
+    px: {(pruner, pruned, topic): [listed peers]} -- the PX lists the oracle's
+    makePrune chose (ORC_EV_PX_PEER); a Leave's PRUNE (CTL_UNSUB) carries
+    unsub_backoff."""
     import ctypes
     C = wo.pb()
     E = net.e
@@ -408,8 +412,13 @@ def expected_heartbeat_rpcs(net, st, msgs, mcaches, lib, T, names, backoff, p0, 
                     c.graft.add(topicID=names[t])
                     any_ = True
             for t in range(T):
-                if st.ctl[0, t, re] & 0x02:
-                    c.prune.add(topicID=names[t], backoff=backoff)
+                ct = int(st.ctl[0, t, re])
+                if ct & 0x02:
+                    x = c.prune.add(topicID=names[t])
+                    if ct & _abi.CTL_PX:
+                        for y in (px or {}).get((p, q, t), []):
+                            x.peers.add(peerID=bytes(peer_ids[y]) if peer_ids is not None else int(y).to_bytes(4, "big"))
+                    x.backoff = unsub_backoff if (ct & _abi.CTL_UNSUB) else backoff
                     any_ = True
             if any_:
                 out.append((p, q, r.SerializeToString()))
@@ -417,8 +426,11 @@ def expected_heartbeat_rpcs(net, st, msgs, mcaches, lib, T, names, backoff, p0, 
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("with_peer_ids", [False, True])
-def test_heartbeat_rpcs_match_oracle(require_gpu, with_peer_ids):
+@pytest.mark.parametrize("with_peer_ids,px", [(False, False), (True, False), (False, True), (True, True)])
+def test_heartbeat_rpcs_match_oracle(require_gpu, with_peer_ids, px):
+    """px: WithPeerExchange, meshes above Dhi (the heartbeat prunes with PX)
+    and Leaves (their PRUNEs carry PX too, UnsubscribeBackoff): every PRUNE's
+    PeerInfo list equals the oracle's makePrune choice."""
     import oracle_binding as ob
     from fixtures import beacon_params, synthetic_state
     from gsim.engine import random_regular
@@ -428,18 +440,23 @@ def test_heartbeat_rpcs_match_oracle(require_gpu, with_peer_ids):
     n, k, T = 600, 12, 3
     rng = np.random.default_rng(91)
     params = beacon_params(T)
-    gp = GossipSubParams(D=6, Dlo=5, Dhi=10, Dscore=3, Dout=2)
+    gp = GossipSubParams(D=6, Dlo=5, Dhi=10, Dscore=3, Dout=2, PeerExchange=px)
     th = PeerScoreThresholds(GossipThreshold=-50, PublishThreshold=-100, GraylistThreshold=-300)
     net = random_regular(n, k, seed=n + 1, n_topics=T)
     st = ob.NetState(net, params, thresholds=th, gossip=gp)
-    synthetic_state(st, rng, tick_time(0), 6 / k)
+    synthetic_state(st, rng, tick_time(0), (11 if px else 6) / k)
     ticks = list(range(1, 7))
     sched = subscribed_schedule(rng, ticks, net, T, 5.0, 0.0, verdicts=(0.85, 0.05, 0.05, 0.05, 0.0))
+    subs = None
+    if px:                                  # Leaves at ticks 3 and 5 (PRUNE | UNSUB | PX)
+        subs = {kk: [(np.array([(int(p), int(rng.integers(0, T))) for p in rng.choice(n, 25, replace=False)],
+                               dtype=np.uint32), False)] for kk in (3, 5)}
     names = [f"topic{t:02d}".encode() for t in range(T)]
     peer_ids = rng.integers(0, 256, size=(n, 38), dtype=np.uint8) if with_peer_ids else None
     lib = ob.load()
     backoff = int(gp.PruneBackoff // Second)
-    state = {"mc": None, "checked": 0}
+    unsub_backoff = int(gp.UnsubscribeBackoff // Second)
+    state = {"mc": None, "checked": 0, "px": 0, "px_leave": 0}
 
     def after_heartbeat(kk, eng, st_, msgs):
         if state["mc"] is None:
@@ -447,13 +464,24 @@ def test_heartbeat_rpcs_match_oracle(require_gpu, with_peer_ids):
             state["mc"] = [lib.orc_mcache_new(gp.HistoryGossip, gp.HistoryLength) for _ in range(n)]
         mc = state["mc"]
         ev = msgs.events()
+        lists = {}
         for e in ev:
             if int(e["kind"]) == ob.EV_PUT:
                 lib.orc_mcache_put(mc[int(e["a"])], int(e["mid"]), int(e["topic"]))
+            # this tick's makePrune lists: the heartbeat's and the Leaves' before it (not the
+            # last tick's GRAFT replies)
+            if int(e["kind"]) == ob.EV_PX_PEER and int(e["x"]) in (tick_time(kk), tick_time(kk) - Second // 2):
+                lists.setdefault((int(e["a"]), int(e["mid"]), int(e["topic"])), []).append((int(e["g"]), int(e["b"])))
+        px_lists = {key: [y for _, y in sorted(v)] for key, v in lists.items()}
         if kk >= 2:
             p0, p1 = 37, 337
             got = wire.heartbeat_rpcs(eng, kk, p0, p1, names, peer_ids=peer_ids, prune_backoff_s=backoff)
-            want = expected_heartbeat_rpcs(net, st_, msgs, mc, lib, T, names, backoff, p0, p1, peer_ids)
+            want = expected_heartbeat_rpcs(net, st_, msgs, mc, lib, T, names, backoff, p0, p1, peer_ids, px=px_lists,
+                                           unsub_backoff=unsub_backoff)
+            for (_, _, b_) in want:
+                r_ = wo.pb()["RPC"].FromString(b_)
+                state["px"] += sum(len(x.peers) > 0 for x in r_.control.prune)
+                state["px_leave"] += sum(len(x.peers) > 0 and x.backoff == unsub_backoff for x in r_.control.prune)
             assert len(got) == len(want), f"tick {kk}: {len(got)} RPCs, expected {len(want)}"
             for g_, w_ in zip(got, want):
                 assert g_ == w_, f"tick {kk}: RPC {g_[0]}->{g_[1]} differs"
@@ -466,19 +494,22 @@ def test_heartbeat_rpcs_match_oracle(require_gpu, with_peer_ids):
             lib.orc_mcache_shift(mc[p])
 
     try:
-        run_parity(net, params, th, gp, st, ticks, sched, ring=512, after_heartbeat=after_heartbeat)
+        run_parity(net, params, th, gp, st, ticks, sched, ring=512, after_heartbeat=after_heartbeat, subs=subs)
     finally:
         for m in state["mc"] or []:
             lib.orc_mcache_free(m)
     assert state["checked"] > 200
+    if px:
+        assert state["px"] > 20 and state["px_leave"] > 0, state
 
 
 @pytest.mark.gpu
 def test_heartbeat_rpcs_refuse_what_they_cannot_encode(require_gpu):
-    """Two heartbeat outputs the device encoder does not hold per RPC are
+    """A heartbeat output the device encoder does not hold per RPC is
     refused rather than encoded wrongly: emitGossip's per-target random
     MaxIHaveLength-subsets (gossipsub.go:1763-1772: a window longer than
-    MaxIHaveLength) and makePrune's PX peer lists (1878-1903)."""
+    MaxIHaveLength).  (makePrune's PX lists are encoded:
+    test_heartbeat_rpcs_match_oracle[px].)"""
     import oracle_binding as ob
     from fixtures import beacon_params, synthetic_state
     from gsim.engine import random_regular
@@ -489,7 +520,7 @@ def test_heartbeat_rpcs_refuse_what_they_cannot_encode(require_gpu):
     names = [f"t{t}".encode() for t in range(T)]
     th = PeerScoreThresholds(GossipThreshold=-50, PublishThreshold=-100, GraylistThreshold=-300)
     params = beacon_params(T)
-    for case in ("window", "px"):
+    for case in ("window",):
         rng = np.random.default_rng(7)
         if case == "window":
             gp = GossipSubParams(D=6, Dlo=5, Dhi=10, Dscore=3, Dout=2, MaxIHaveLength=2)

@@ -35,9 +35,18 @@ def oracle_trace(ev, msgs, lo, hi):
     ring = msgs.seen.shape[0]
     for e in ev:
         kind, a, b = int(e["kind"]), int(e["a"]), int(e["b"])
+        mid, topic = int(e["mid"]), int(e["topic"])
+        if kind == ob.EV_RPC_MSG:
+            # a message RPC: SEND_RPC at the sender, RECV_RPC at the receiver; an IWANT
+            # answer (x = 1) is sent the round before it arrives
+            g, x = int(e["g"]), int(e["x"])
+            if lo <= a < hi:
+                out.append((msgs.round_time(g - x), mid, a, b, topic, _abi.TRACE_SEND_RPC, x))
+            if lo <= b < hi:
+                out.append((msgs.round_time(g), mid, b, a, topic, _abi.TRACE_RECV_RPC, x))
+            continue
         if not (lo <= a < hi):
             continue
-        mid, topic = int(e["mid"]), int(e["topic"])
         if kind == ob.EV_PUBLISH:
             out.append((msgs.round_time(int(e["g"])), mid, a, a, topic, _abi.TRACE_PUBLISH_MESSAGE, 0))
         elif kind == ob.EV_SEEN and b != 0xFFFFFFFF:
@@ -60,7 +69,8 @@ def oracle_trace(ev, msgs, lo, hi):
     arr = np.zeros(len(out), dtype=Engine.TRACE_DTYPE)
     for q, (ts, mid, a, b, topic, typ, rs) in enumerate(out):
         arr[q] = (ts, mid, a, b, topic, typ, rs, 0)
-    return arr[np.lexsort((arr["msg_id"], arr["topic"], arr["other"], arr["type"], arr["peer"], arr["timestamp"]))]
+    return arr[np.lexsort((arr["msg_id"], arr["topic"], arr["reason"], arr["other"], arr["type"], arr["peer"],
+                           arr["timestamp"]))]
 
 
 def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, churn=None, after_tick=None,
