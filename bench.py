@@ -138,6 +138,9 @@ def build_network(cfg, seed, scen=None):
         ip_ptr, ip_ids, n_ips, syb = graphs.sybil_ips(n, scen["sybil_frac"], scen["per_ip"], seed=seed + 200)
         net = graphs.with_ips(net, ip_ptr, ip_ids, n_ips)
         beh = syb.astype(np.uint8) * np.uint8(_abi.BEHAVE_IGNORE_IWANT)
+    else:
+        # honest peers get a unique IP id (P6 is derived, and is 0)
+        net = graphs.with_ips(net, np.arange(n + 1, dtype=np.uint32), np.arange(n, dtype=np.uint32), n)
     return net, beh
 
 
@@ -185,6 +188,8 @@ def describe_graph(cfg, scen) -> str:
              f"Zipf subscriptions ({scen['zipf_per_peer']} topics/peer)")
     else:
         d = f"random-regular k={k}"
+    if "sybil_frac" not in scen:
+        d += ", one IP per peer"
     if "sybil_frac" in scen:
         d += (f", {scen['sybil_frac']:.0%} sybils ({scen['per_ip']} per IP) ignoring IWANT, "
               f"opportunistic grafting every {scen['opp_ticks']} heartbeats")

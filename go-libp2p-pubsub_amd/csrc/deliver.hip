@@ -258,6 +258,8 @@ struct RoundArgs {
 // drops the message and runs ThrottlePeer (gossip_tracer.go:182-200): i's
 // promises from j are forgotten.  Direct peers are accepted
 // (gossipsub.go:599-602).
+constexpr uint32_t kGaterRpcSlot = 0xFFFFFFu;   // the draw key of an IWANT answer (oracle ORC_GATER_RPC_SLOT)
+
 __device__ __forceinline__ bool gater_accept(const RoundArgs& a, uint32_t i, uint32_t r, uint32_t m, uint32_t j)
 {
     const GaterRef& g = a.gt;
@@ -714,6 +716,18 @@ constexpr int kTsSlots = 64;
 #ifndef GSIM_TM_TB
 #define GSIM_TM_TB 1024      // threads per k_send_tm block
 #endif
+// GSIM_TM_NT (A/B builds): the forwarders' row fields and the receivers' cells
+// are loaded non-temporal, so the L2 keeps the slots' committed bitmaps
+#ifdef GSIM_TM_NT
+#define TM_LD(x) __builtin_nontemporal_load(&(x))
+#else
+#define TM_LD(x) (x)
+#endif
+#if defined(GSIM_TM_NT) && GSIM_TM_NT > 1
+#define TM_LDC(x) __builtin_nontemporal_load(&(x))
+#else
+#define TM_LDC(x) (x)
+#endif
 constexpr int kPushTB = GSIM_TM_TB;  // ... of a shard's push walk (512: 21 against 18.5 ms per shard at K = 8)
 constexpr uint32_t kTmWin = 8192;   // flattened edges whose senders are tabled in LDS at once
 constexpr int kTmTabMin = 256;      // forwarders in a chunk from which the table pays for its fill
@@ -986,10 +1000,10 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                                 // a masked row's positions are its mesh (or direct) edges: the
                                 // router flags are read only for direct ones (below)
                                 const int64_t pe = pv[u] + e;
-                                iv[u] = a.col[e]; dsv[u] = a.dstate[e]; tfv[u] = a.tflags[pe];
-                                if (!mk[u]) mfv[u] = a.mflags[pe];
-                                if (verdict_penalises(vd)) xv[u] = a.invalid[pe];
-                                else if (vd == GSIM_VERDICT_ACCEPT) nv[u] = a.mcnt[pe];
+                                iv[u] = TM_LD(a.col[e]); dsv[u] = TM_LD(a.dstate[e]); tfv[u] = TM_LD(a.tflags[pe]);
+                                if (!mk[u]) mfv[u] = TM_LD(a.mflags[pe]);
+                                if (verdict_penalises(vd)) xv[u] = TM_LD(a.invalid[pe]);
+                                else if (vd == GSIM_VERDICT_ACCEPT) nv[u] = TM_LD(a.mcnt[pe]);
                             }
                         }
                         int qpl[P];              // validation latency: queue plane of the copy (-1: none)
@@ -1066,7 +1080,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             // targets all hold the topic, §2); -1 cannot happen
                             const int64_t ci = known ? 0 : SP ? a.cs.at((int64_t)s_cb[k], t, i) : (int64_t)m * a.cs.n + i;
                             if (SP && ci < 0) continue;
-                            const uint64_t c = known ? 0ull : a.cs.cell[ci];
+                            const uint64_t c = known ? 0ull : TM_LDC(a.cs.cell[ci]);
                             const uint32_t chi = (uint32_t)(c >> 32);
                             // the round validation completed (or completes) in; -1: unclaimed
                             // or claimed in this round
@@ -1954,7 +1968,10 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a_, const uint
         // the gater, the trace, a claim (most copies are plain duplicates)
         const bool need_i = a.smask || a.gt.act || a.tr.on(p);
         uint32_t i = need_i ? owner[r] : 0xFFFFFFFFu;
-        if (a.gt.act && !gater_accept(a, p, r, m, i)) continue;   // the peer gater (gater_accept)
+        // the peer gater (gater_accept): one draw per IWANT answer RPC -- (round,
+        // receiver, sender), the slot left out (AcceptFrom runs per RPC, pubsub.go);
+        // a shard's pushed copies are forwarded messages, one RPC each
+        if (a.gt.act && !gater_accept(a, p, r, a.sharded ? m : kGaterRpcSlot, i)) continue;
         if (a.subdyn && !((a.sub[p] >> (int32_t)a.mtopic[m]) & 1ull)) continue;   // a topic p left
         if (a.gt.act) gater_copy(a, r, a.minv[m] == GSIM_VERDICT_SIGNATURE);
         n_acc++;

@@ -64,6 +64,7 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a_)
                 a.graft[i] = 0; a.mtime[i] = 0; a.tflags[i] = 0;
             }
             *a.purged = 1;
+            if (a.p6row) a.p6row[a.col[e]] = 1;        // the observer's tracked set shrank
             if (SCORE) a.score[e] = 0.0;
             continue;
         }
@@ -168,62 +169,148 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a_)
 // Kernel 2: ipColocationFactor (score.go:344-388) as a segmented count over
 // each observer's row keyed by IP id.  Only re-run when the tracked set or the
 // IP assignment changes (AddPeer/RemovePeer/purge), not every heartbeat.
-// Two passes.  k_ip_keys: thread per edge e2, key[e2] = the neighbour's IP id
-// when it is tracked and has exactly one IP (the common case), else a sentinel
-// (untracked / no IP / several IPs).  k_ip_colocation: thread per observer
-// edge e (observer owner[e], neighbour col[e]); for each of the neighbour's
-// IPs it counts the row's tracked members on that IP by scanning the row's
-// keys (contiguous u32, L1/L2 hits) and falls back to the member's IP list only
-// for several-IP members.  The result is the P6 value of record rev[e], the
-// same count in the same order as the reference's per-IP loop.
+// One observer row per lane group (the heartbeat's row classes: W = 16 / 32
+// / 64 lanes for rows of at most W connections), lane l = the row's l-th
+// connection.  Each lane forms its member's IP key: the neighbour's IP id when
+// the neighbour is tracked and has exactly one IP (the common case), else a
+// sentinel (untracked / no IP / several IPs).  A member's count for its IP is
+// the number of equal keys in the group, W shuffles in registers.  A row with a
+// several-IP member counts per IP of the neighbour over the row from memory,
+// walking a member's IP list only when it has several.  The counts and the
+// order of the sum are the reference's per-IP loop (score.go:344-388); the
+// result is the P6 value of record rev[e].  Hub rows (more than 64
+// connections): k_ip_colocation_hub.
 constexpr uint32_t kIpUntracked = 0xFFFFFFFFu, kIpMulti = 0xFFFFFFFEu, kIpNone = 0xFFFFFFFDu;
 
-__global__ __launch_bounds__(256) void k_ip_keys(ColocArgs a)
+__device__ __forceinline__ uint32_t ip_key(const ColocArgs& a, uint32_t e)
+{
+    if (!(a.estate[a.rev[e]] & GSIM_ES_TRACKED)) return kIpUntracked;
+    const uint32_t j = a.col[e];
+    const uint32_t q0 = a.ip_ptr[j], q1 = a.ip_ptr[j + 1];
+    return q1 == q0 ? kIpNone : q1 - q0 == 1 ? a.ip_ids[q0] : kIpMulti;
+}
+
+// several-IP rows: the per-IP count of member e's neighbour over the row [b, en)
+__device__ double p6_scan(const ColocArgs& a, uint32_t b, uint32_t en, uint32_t e)
+{
+    double res = 0.0;
+    const uint32_t j = a.col[e];
+    for (uint32_t q = a.ip_ptr[j]; q < a.ip_ptr[j + 1]; ++q) {
+        const uint32_t ip = a.ip_ids[q];
+        if (a.ip_white && a.ip_white[ip]) continue;
+        int32_t cnt = 0;
+        for (uint32_t e2 = b; e2 < en; ++e2) {
+            if (!(a.estate[a.rev[e2]] & GSIM_ES_TRACKED)) continue;
+            const uint32_t j2 = a.col[e2];
+            for (uint32_t q2 = a.ip_ptr[j2]; q2 < a.ip_ptr[j2 + 1]; ++q2)
+                if (a.ip_ids[q2] == ip) { ++cnt; break; }
+        }
+        if (cnt > a.thr) {
+            const double surplus = (double)(cnt - a.thr);
+            res += surplus * surplus;
+        }
+    }
+    return res;
+}
+
+__device__ __forceinline__ double p6_of(const ColocArgs& a, uint32_t k, int32_t cnt)
+{
+    if (k >= kIpNone || (a.ip_white && a.ip_white[k]) || cnt <= a.thr) return 0.0;   // no IP, untracked, whitelisted
+    const double surplus = (double)(cnt - a.thr);
+    return surplus * surplus;
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void k_ip_coloc_rows(ColocArgs a, const uint32_t* rows, int64_t nrows, int64_t base)
 {
     if (a.gate && *a.gate == 0) return;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
-        uint32_t k = kIpUntracked;
-        if (a.estate[a.rev[e]] & GSIM_ES_TRACKED) {
-            const uint32_t j = a.col[e];
-            const uint32_t q0 = a.ip_ptr[j], q1 = a.ip_ptr[j + 1];
-            k = q1 == q0 ? kIpNone : q1 - q0 == 1 ? a.ip_ids[q0] : kIpMulti;
+    constexpr int G = 64 / W;
+    const int lane = threadIdx.x & 63, gl = lane % W;
+    const int64_t ngroups = (nrows + G - 1) / G * G;
+    for (int64_t x = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / W; x < ngroups; x += (int64_t)gridDim.x * blockDim.x / W) {
+        bool row_ok = x < nrows;
+        const uint32_t i = row_ok ? (rows ? rows[x] : (uint32_t)(base + x)) : 0u;
+        if (row_ok && a.rowflag) {                                // only rows whose tracked set changed
+            row_ok = a.rowflag[i] != 0;
+            if (row_ok && gl == 0) a.rowflag[i] = 0;
         }
-        a.key[e] = k;
+        const uint32_t b = row_ok ? a.row_ptr[i] : 0u, deg = row_ok ? a.row_ptr[i + 1] - b : 0u;
+        const bool on = (uint32_t)gl < deg;
+        const uint32_t e = b + (uint32_t)gl;
+        const uint32_t k = on ? ip_key(a, e) : kIpUntracked;
+        const uint64_t gm = W == 64 ? ~0ull : (((1ull << W) - 1ull) << (lane - gl));
+        const bool multi = (__ballot(k == kIpMulti) & gm) != 0;
+        int32_t cnt = 0;
+#pragma unroll 16
+        for (int q = 0; q < W; ++q) {
+            const uint32_t kq = (uint32_t)__shfl((int)k, q, W);
+            cnt += (q < (int)deg && kq == k) ? 1 : 0;
+        }
+        if (!on) continue;
+        a.p6[a.rev[e]] = multi ? (k == kIpUntracked ? 0.0 : p6_scan(a, b, b + deg, e)) : p6_of(a, k, cnt);
     }
 }
 
-__global__ __launch_bounds__(256) void k_ip_colocation(ColocArgs a)
+// Hub rows (more than hub_min connections, the heartbeat's hub classes):
+// one block per row.  The row's keys are staged in LDS; when every tracked
+// member has at most one IP they are sorted (bitonic) and each member's count
+// is an equal range of its IP, O(deg log deg) instead of O(deg^2) (a
+// 4096-connection row: 1.7e7 key loads); a row with a several-IP member
+// counts per IP from memory (p6_scan).
+constexpr int kHubP6Max = 4096;
+
+__global__ __launch_bounds__(256) void k_ip_colocation_hub(ColocArgs a, const uint32_t* rows, int64_t nrows)
 {
     if (a.gate && *a.gate == 0) return;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.E; e += stride) {
-        const uint32_t r = a.rev[e];
-        const uint32_t i = a.owner[e];
-        if (a.sharded && (i < a.olo || i >= a.ohi)) continue;   // a ghost observer's row is partial
-        double res = 0.0;
-        if (a.key[e] != kIpUntracked) {
-            const uint32_t b = a.row_ptr[i], en = a.row_ptr[i + 1];
-            const uint32_t j = a.col[e];
-            for (uint32_t q = a.ip_ptr[j]; q < a.ip_ptr[j + 1]; ++q) {
-                const uint32_t ip = a.ip_ids[q];
-                if (a.ip_white && a.ip_white[ip]) continue;
-                int32_t cnt = 0;
-                for (uint32_t e2 = b; e2 < en; ++e2) {
-                    const uint32_t k2 = a.key[e2];
-                    if (k2 == ip) { ++cnt; continue; }
-                    if (k2 != kIpMulti) continue;
-                    const uint32_t j2 = a.col[e2];
-                    for (uint32_t q2 = a.ip_ptr[j2]; q2 < a.ip_ptr[j2 + 1]; ++q2)
-                        if (a.ip_ids[q2] == ip) { ++cnt; break; }
-                }
-                if (cnt > a.thr) {
-                    const double surplus = (double)(cnt - a.thr);
-                    res += surplus * surplus;
-                }
-            }
+    __shared__ uint32_t s_key[kHubP6Max];
+    __shared__ uint32_t s_srt[kHubP6Max];
+    for (int64_t x = blockIdx.x; x < nrows; x += gridDim.x) {
+        const uint32_t i = rows[x];
+        const uint32_t b = a.row_ptr[i], deg = a.row_ptr[i + 1] - b;
+        if (deg > (uint32_t)kHubP6Max || deg <= a.hub_min) continue;   // (cannot happen: rows <= 4096, hubs > 64)
+        if (a.sharded && (i < a.olo || i >= a.ohi)) continue;
+        if (a.rowflag && !a.rowflag[i]) continue;               // only rows whose tracked set changed
+        __syncthreads();                                          // (every thread has read the flag)
+        if (a.rowflag && threadIdx.x == 0) a.rowflag[i] = 0;
+        bool multi = false;
+        for (uint32_t q = threadIdx.x; q < deg; q += blockDim.x) {
+            const uint32_t k = ip_key(a, b + q);
+            s_key[q] = k;
+            multi |= k == kIpMulti;
         }
-        a.p6[r] = res;
+        uint32_t n2 = 1;
+        while (n2 < deg) n2 <<= 1;
+        if (!__syncthreads_or(multi)) {
+            for (uint32_t q = threadIdx.x; q < n2; q += blockDim.x) s_srt[q] = q < deg ? s_key[q] : 0xFFFFFFFFu;
+            __syncthreads();
+            for (uint32_t k = 2; k <= n2; k <<= 1)               // bitonic sort, ascending
+                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                    for (uint32_t q = threadIdx.x; q < n2; q += blockDim.x) {
+                        const uint32_t p = q ^ j;
+                        if (p > q) {
+                            const uint32_t u = s_srt[q], v = s_srt[p];
+                            if (((q & k) == 0) ? (u > v) : (u < v)) { s_srt[q] = v; s_srt[p] = u; }
+                        }
+                    }
+                    __syncthreads();
+                }
+            for (uint32_t q = threadIdx.x; q < deg; q += blockDim.x) {
+                const uint32_t k = s_key[q];
+                int32_t cnt = 0;
+                if (k < kIpNone) {
+                    uint32_t lo = 0, hi = n2;
+                    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (s_srt[m] < k) lo = m + 1; else hi = m; }
+                    uint32_t lo2 = lo, hi2 = n2;
+                    while (lo2 < hi2) { const uint32_t m = (lo2 + hi2) >> 1; if (s_srt[m] <= k) lo2 = m + 1; else hi2 = m; }
+                    cnt = (int32_t)(lo2 - lo);
+                }
+                a.p6[a.rev[b + q]] = p6_of(a, k, cnt);
+            }
+        } else {
+            for (uint32_t q = threadIdx.x; q < deg; q += blockDim.x)
+                a.p6[a.rev[b + q]] = s_key[q] == kIpUntracked ? 0.0 : p6_scan(a, b, b + deg, b + q);
+        }
+        __syncthreads();                                          // LDS is rewritten by the next row
     }
 }
 
@@ -592,7 +679,7 @@ void free_graph(gsim_handle* h)
     dfree(h->d_ip_ptr); dfree(h->d_ip_ids); dfree(h->d_ip_white); dfree(h->d_p5);
     dfree(h->d_first); dfree(h->d_meshd); dfree(h->d_fail); dfree(h->d_invalid);
     dfree(h->d_graft); dfree(h->d_mtime); dfree(h->d_tflags); dfree(h->d_mflags);
-    dfree(h->d_bp); dfree(h->d_estate); dfree(h->d_expire); dfree(h->d_p6); dfree(h->d_ipkey); dfree(h->d_churn); h->churn_cap = 0; dfree(h->d_score);
+    dfree(h->d_bp); dfree(h->d_estate); dfree(h->d_expire); dfree(h->d_p6); dfree(h->d_p6row); dfree(h->d_churn); h->churn_cap = 0; dfree(h->d_score);
     dfree(h->d_backoff); dfree(h->d_rstate); dfree(h->d_dstate); dfree(h->d_mcnt); dfree(h->d_pen);
     dfree(h->d_smask);
     h->smask.clear();
@@ -631,6 +718,7 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     a.mt_lazy = h->mt_lazy ? 1 : 0;
     a.mt_R = h->mt_R;
     a.purged = h->d_flags;
+    a.p6row = h->d_p6row;
     a.sharded = h->sh ? 1 : 0;
     a.olo = (uint32_t)h->olo();
     a.ohi = (uint32_t)h->ohi();
@@ -652,15 +740,38 @@ int launch_ip_colocation(gsim_handle* h, const int32_t* gate)
     c.sharded = h->sh ? 1 : 0;
     c.olo = (uint32_t)h->olo();
     c.ohi = (uint32_t)h->ohi();
-    if (!h->d_ipkey) {
-        const int rc = dalloc(h, &h->d_ipkey, h->e);
-        if (rc) return rc;
+    c.hub_min = 64u;
+    // churn / purges changed some rows' tracked sets: those rows alone
+    c.rowflag = h->p6_rows_only ? h->d_p6row : nullptr;
+    // the heartbeat's row classes: owned observers by row length
+    RowClasses rc{};
+    row_classes(h, &rc);
+    auto grid = [](int64_t groups, int per_block) {
+        return dim3((uint32_t)std::max<int64_t>(1, std::min<int64_t>((groups + per_block - 1) / per_block, 65536)));
+    };
+    if (!rc.rows) {                          // one class: the owned rows [olo, ohi) in order
+        const int64_t n = h->ohi() - h->olo();
+        if (rc.n16 == n) hipLaunchKernelGGL(k_ip_coloc_rows<16>, grid(n, 16), dim3(256), 0, h->stream, c, nullptr, n, h->olo());
+        else if (rc.n32 == n) hipLaunchKernelGGL(k_ip_coloc_rows<32>, grid(n, 8), dim3(256), 0, h->stream, c, nullptr, n, h->olo());
+        else hipLaunchKernelGGL(k_ip_coloc_rows<64>, grid(n, 4), dim3(256), 0, h->stream, c, nullptr, n, h->olo());
+    } else {
+        if (rc.n16) hipLaunchKernelGGL(k_ip_coloc_rows<16>, grid(rc.n16, 16), dim3(256), 0, h->stream, c, rc.rows, rc.n16,
+                                       (int64_t)0);
+        if (rc.n32) hipLaunchKernelGGL(k_ip_coloc_rows<32>, grid(rc.n32, 8), dim3(256), 0, h->stream, c, rc.rows + rc.n16,
+                                       rc.n32, (int64_t)0);
+        if (rc.n64) hipLaunchKernelGGL(k_ip_coloc_rows<64>, grid(rc.n64, 4), dim3(256), 0, h->stream, c,
+                                       rc.rows + rc.n16 + rc.n32, rc.n64, (int64_t)0);
+        const int64_t nhub = rc.nhub;
+        if (nhub)
+            hipLaunchKernelGGL(k_ip_colocation_hub, dim3((uint32_t)std::min<int64_t>(nhub, 65536)), dim3(256), 0,
+                               h->stream, c, rc.rows + rc.n16 + rc.n32 + rc.n64, nhub);
     }
-    c.key = h->d_ipkey;
-    hipLaunchKernelGGL(k_ip_keys, dim3(grid_for(h->e)), dim3(256), 0, h->stream, c);
-    hipLaunchKernelGGL(k_ip_colocation, dim3(grid_for(h->e)), dim3(256), 0, h->stream, c);
+    hipError_t e = hipGetLastError();
+    // a full pass re-derived every row: no row stays flagged
+    if (e == hipSuccess && !c.rowflag) e = hipMemsetAsync(h->d_p6row, 0, (size_t)h->n, h->stream);
     h->p6_dirty = false;
-    return hip_check(h, hipGetLastError(), "k_ip_colocation");
+    h->p6_rows_only = true;      // until a change of more than the tracked sets
+    return hip_check(h, e, "k_ip_colocation");
 }
 
 template <bool REFRESH, bool SCORE>
@@ -1141,6 +1252,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     rc = rc ? rc : dalloc(h, &h->d_ip_ids, nip);
     rc = rc ? rc : dalloc(h, &h->d_ip_white, (int64_t)n_ips);
     rc = rc ? rc : dalloc(h, &h->d_p5, n);
+    rc = rc ? rc : dalloc(h, &h->d_p6row, n);
     rc = rc ? rc : dalloc(h, &h->d_first, ET);
     rc = rc ? rc : dalloc(h, &h->d_meshd, ET);
     rc = rc ? rc : dalloc(h, &h->d_fail, ET);
@@ -1216,10 +1328,11 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     hipLaunchKernelGGL(k_fill_u8, dim3(grid_for(E)), dim3(256), 0, s, h->d_estate, E,
                        (uint8_t)(GSIM_ES_TRACKED | GSIM_ES_CONNECTED));
     hipLaunchKernelGGL(k_fill_u8, dim3(grid_for(E)), dim3(256), 0, s, h->d_rstate, E, (uint8_t)GSIM_ES_CONNECTED);
+    hipLaunchKernelGGL(k_fill_u8, dim3(grid_for(n)), dim3(256), 0, s, h->d_p6row, n, (uint8_t)0);
     h->score_version++;
     h->mesh_version++;
     h->has_white = false;
-    h->p6_dirty = true;
+    h->p6_dirty = true; h->p6_rows_only = false;
     h->maybe_retained = false;
     h->mcnt_dirty = false;
     h->mt_lazy = false;
@@ -1258,6 +1371,11 @@ int gsim_set_ips(gsim_handle* h, const uint32_t* ip_ptr, const uint32_t* ip_ids,
     GSIM_NEED_GRAPH(h);
     if (!ip_ptr || ip_ptr[0] != 0) { h->err = "ip_ptr[0] must be 0"; return GSIM_EINVAL; }
     if (n_ips > kIpNone) { h->err = "too many IP ids"; return GSIM_EINVAL; }
+    if (h->gt) {
+        // the peer gater's per-IP groups are built by gsim_set_peer_gater from the IPs then
+        h->err = "gsim_set_ips with the peer gater on: set the IPs before gsim_set_peer_gater";
+        return GSIM_ESTATE;
+    }
     const int64_t n = h->n;
     for (int64_t i = 0; i < n; ++i)
         if (ip_ptr[i + 1] < ip_ptr[i]) { h->err = "ip_ptr not monotone"; return GSIM_EINVAL; }
@@ -1280,7 +1398,7 @@ int gsim_set_ips(gsim_handle* h, const uint32_t* ip_ptr, const uint32_t* ip_ids,
     if (e == hipSuccess) e = hipMemcpyAsync(h->d_ip_ptr, ip_ptr, sizeof(uint32_t) * (size_t)(n + 1), hipMemcpyHostToDevice, h->stream);
     if (e == hipSuccess && nip) e = hipMemcpyAsync(h->d_ip_ids, ip_ids, sizeof(uint32_t) * (size_t)nip, hipMemcpyHostToDevice, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-    h->p6_dirty = true;
+    h->p6_dirty = true; h->p6_rows_only = false;
     return hip_check(h, e, "gsim_set_ips");
 }
 
@@ -1295,7 +1413,7 @@ int gsim_set_ip_whitelist(gsim_handle* h, const uint8_t* white)
     } else {
         h->has_white = false;
     }
-    h->p6_dirty = true;
+    h->p6_dirty = true; h->p6_rows_only = false;
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     return hip_check(h, e, "gsim_set_ip_whitelist");
 }
@@ -1359,7 +1477,7 @@ int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now, double p_mes
     ScoreArgs a = make_score_args(h, now);
     hipLaunchKernelGGL(k_fill_synthetic, dim3(grid_for(h->e)), dim3(256), 0, h->stream, a, seed, p_mesh);
     h->mt_lazy = false;          // the fill stores meshTime
-    h->p6_dirty = true;
+    h->p6_dirty = true; h->p6_rows_only = false;
     h->score_version++;
     h->mesh_version++;
     h->maybe_retained = false;
@@ -1469,7 +1587,7 @@ int gsim_write_field(gsim_handle* h, int32_t f, const void* src, size_t bytes)
     rc = write_field_impl(h, f, r, src);
     h->unjoined_zero = false;    // arbitrary state: no record may be skipped
     if (!rc) rc = extra_field_written(h, f);
-    if (f == GSIM_F_ESTATE) { h->p6_dirty = true; h->maybe_retained = true; h->score_version++;
+    if (f == GSIM_F_ESTATE) { h->p6_dirty = true; h->p6_rows_only = false; h->maybe_retained = true; h->score_version++;
     h->mesh_version++; }
     if (f == GSIM_F_SCORE) h->score_version++;
     h->mesh_version++;          // router flags may have changed (delivery's mesh masks)

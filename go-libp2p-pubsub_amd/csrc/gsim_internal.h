@@ -49,6 +49,7 @@ struct ScoreArgs {
     int32_t sharded;
     uint32_t olo, ohi;
     int64_t e_lo, e_hi, geid_base, E_glob;
+    uint8_t* p6row;            // [N] a purge marks its observer's row for the next P6 pass
 };
 
 struct ColocArgs {
@@ -59,9 +60,10 @@ struct ColocArgs {
     double* p6;
     int32_t thr;
     const int32_t* gate;       // non-null: run only if *gate != 0 (a retention purge happened)
-    uint32_t* key;             // [E] per-edge IP key of the row member (k_ip_keys)
     int32_t sharded;           // only owned observers ([olo, ohi)) get P6
     uint32_t olo, ohi;
+    uint32_t hub_min;          // rows longer than this are the hub kernel's (k_ip_colocation_hub)
+    uint8_t* rowflag;          // non-null: only rows flagged here are re-derived (and their flags cleared)
 };
 
 // meshMessageDeliveries increments from message delivery are kept as a
@@ -407,6 +409,9 @@ struct gsim_handle {
     size_t bytes_allocated = 0;
     bool has_white = false;
     bool p6_dirty = true;
+    // only the rows flagged in d_p6row changed (churn, retention purges): the
+    // P6 pass re-derives those; false: every row (graph, IPs, whitelist, writes)
+    bool p6_rows_only = false;
     bool maybe_retained = false;
     // Every record of a topic its observer did not join is zero (true after
     // gsim_load_graph and gsim_fill_synthetic, false after any state write
@@ -457,7 +462,7 @@ struct gsim_handle {
     uint8_t* d_estate = nullptr;
     int64_t* d_expire = nullptr;
     double* d_p6 = nullptr;
-    uint32_t* d_ipkey = nullptr;      // [E] P6 scratch: row member's single IP id / sentinel
+    uint8_t* d_p6row = nullptr;       // [N] the observer's tracked set changed since its last P6
     uint32_t* d_churn = nullptr;      // gsim_set_connections scratch: [cap] pairs, [cap] edges, [1] bad
     int64_t churn_cap = 0;
     double* d_score = nullptr;
@@ -576,6 +581,15 @@ int handle_control(gsim_handle* h, int32_t round, int64_t now);   // heartbeat.h
 // its connection attempts out (global asker | peer << 32), gs.outbound of the connections
 bool px_enabled(const gsim_handle* h);
 int px_import(gsim_handle* h, const uint64_t* d_in, int64_t n);
+// The heartbeat's row classes (heartbeat.hip): the owned observers by row
+// length, rows[0, n16) of at most 16 connections, then <= 32, <= 64, then the
+// hub rows (nhub, more than 64).  rows == nullptr: one class holds every owned
+// observer, in order from olo.
+struct RowClasses {
+    const uint32_t* rows;
+    int64_t n16, n32, n64, nhub;
+};
+void row_classes(gsim_handle* h, RowClasses* rc);
 int px_leave_import(gsim_handle* h, const uint32_t* g2l);
 int px_asks(gsim_handle* h, uint64_t* d_out, uint32_t* d_cnt, int64_t cap);
 int px_mark_outbound(gsim_handle* h, const uint64_t* d_pairs, int64_t n);

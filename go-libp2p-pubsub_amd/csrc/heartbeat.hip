@@ -1680,6 +1680,13 @@ __global__ __launch_bounds__(256) void k_px_outbound_pairs(const uint64_t* pairs
 
 bool px_enabled(const gsim_handle* h) { return h->x && h->x->d_pxo; }
 
+void row_classes(gsim_handle* h, RowClasses* rc)
+{
+    const Extra* x = h->x;
+    if (!x) { *rc = RowClasses{nullptr, 0, 0, h->ohi() - h->olo(), 0}; return; }
+    *rc = RowClasses{x->d_rows, x->n16, x->n32, x->n64, x->nh256 + x->nh1024 + x->nh4096};
+}
+
 int px_import(gsim_handle* h, const uint64_t* d_in, int64_t n)
 {
     if (n <= 0 || !h->x || !h->x->d_pxm) return GSIM_OK;
@@ -1798,6 +1805,7 @@ struct ChurnArgs {
     int64_t* expire;
     double *first, *invalid;
     int32_t skip_unjoined;     // records of topics their observer did not join are zero (engine.hip)
+    uint8_t* p6row;            // [N] rows whose P6 must be re-derived (engine.hip launch_ip_colocation)
 };
 
 // The observer's edge to the other end of each (pair, direction), by binary
@@ -2025,6 +2033,7 @@ __global__ __launch_bounds__(256) void k_churn_apply(HbArgs a, ChurnArgs c)
     const uint32_t e = c.edges[q];
     const uint32_t r = a.rev[e];
     if (a.col[r] < a.olo || a.col[r] >= a.ohi) return;   // the other shard handles a ghost observer's side
+    if (c.p6row) c.p6row[a.col[r]] = 1;                   // the observer's tracked set may change: P6 of its row
     if (a.tr.on(a.col[r]))                                 // tracer.AddPeer / RemovePeer (trace.go:196-248)
         a.tr.push(a.now, 0, a.col[r], a.col[e], -1, c.up ? GSIM_TRACE_ADD_PEER : GSIM_TRACE_REMOVE_PEER, 0);
     // the observer's (col[r]) joined topics while unjoined records are known zero:
@@ -2556,6 +2565,7 @@ static int apply_connections(gsim_handle* h, const uint32_t* d_edges, int32_t n2
     c.estate = h->d_estate; c.rstate = h->d_rstate; c.pen = h->d_pen; c.expire = h->d_expire;
     c.first = h->d_first; c.invalid = h->d_invalid;
     c.skip_unjoined = h->unjoined_zero ? 1 : 0;
+    c.p6row = h->d_p6row;
     hipLaunchKernelGGL(k_churn_apply, dim3(grid), dim3(256), 0, h->stream, a, c);
     const hipError_t e = hipGetLastError();   // stream-ordered: the next call's copy into the scratch follows this kernel
     if (e != hipSuccess) return hip_check(h, e, "k_churn_apply");

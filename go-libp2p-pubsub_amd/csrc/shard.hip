@@ -1938,8 +1938,12 @@ int gsim_group_set_subscriptions(gsim_group* g, const uint32_t* pairs, int32_t c
                                  int64_t now)
 {
     if (!g || count < 0 || (count > 0 && !pairs)) return GSIM_EINVAL;
+    // every pair checked on every process before any shard applies the batch: a
+    // rank that held no peer of a bad pair would otherwise go on alone
+    const int32_t T = g->hs.empty() ? 64 : std::max(1, g->hs[0]->t);
     for (int32_t q = 0; q < count; ++q)
-        if ((int64_t)pairs[2 * q] >= g->N) return g->fail(GSIM_EINVAL, "subscription pair out of range");
+        if ((int64_t)pairs[2 * q] >= g->N || pairs[2 * q + 1] >= (uint32_t)T || pairs[2 * q + 1] >= 64u)
+            return g->fail(GSIM_EINVAL, "subscription pair " + std::to_string(q) + " out of range");
     for (size_t l = 0; l < g->hs.size(); ++l) {
         const std::vector<uint32_t>& gid = g->gid[l];
         std::vector<uint32_t> v;

@@ -525,7 +525,8 @@ int gsim_read_snapshot(gsim_handle* h, int64_t obs_lo, int64_t obs_hi, gsim_peer
 
 /* refreshIPs (score.go:568-585): replace every peer's IP list (CSR as for
  * gsim_load_graph); P6 is re-derived before the next score.  The whitelist
- * stays if n_ips is unchanged, else it is cleared. */
+ * stays if n_ips is unchanged, else it is cleared.  GSIM_ESTATE once the peer
+ * gater is on (its per-IP groups are fixed by gsim_set_peer_gater). */
 int gsim_set_ips(gsim_handle* h, const uint32_t* ip_ptr, const uint32_t* ip_ids, uint32_t n_ips);
 
 /* ---- raw state access (tests, checkpoint/resume, golden fixtures) ------- */

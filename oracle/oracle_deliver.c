@@ -128,13 +128,13 @@ static void fr_push(priv* p, uint32_t peer, uint32_t slot, uint32_t from)
     p->nfr++;
 }
 
-static void ar_push(priv* p, uint32_t recv, uint32_t slot, uint32_t er)
+static void ar_push(priv* p, uint32_t recv, uint32_t slot, uint32_t er, uint32_t resp)
 {
     if (p->nar == p->capar) {
         p->capar = p->capar ? 2 * p->capar : 4096;
         p->ar = (arr_ent*)realloc(p->ar, sizeof(arr_ent) * (size_t)p->capar);
     }
-    p->ar[p->nar].recv = recv; p->ar[p->nar].slot = slot; p->ar[p->nar].er = er;
+    p->ar[p->nar].recv = recv; p->ar[p->nar].slot = slot; p->ar[p->nar].er = er; p->ar[p->nar].resp = resp;
     p->nar++;
 }
 
@@ -273,7 +273,8 @@ static void handle_copy(orc_net* s, orc_msgs* m, priv* p, int64_t g, int64_t now
         stats[3]++;
         return;
     }
-    if (s->gater && !(s->direct && s->direct[er]) && !orc_gater_accept(s, p->seed, g, i, er, slot)) {
+    if (s->gater && !(s->direct && s->direct[er]) &&
+        !orc_gater_accept(s, p->seed, g, i, er, x.resp ? ORC_GATER_RPC_SLOT : slot)) {
         /* the peer gater's AcceptControl: the message is dropped and the
          * receiver forgets its promises from the sender (ThrottlePeer,
          * gossip_tracer.go:182-200) */
@@ -384,7 +385,7 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
             if (!(s->estate[e] & GSIM_ES_CONNECTED)) continue;
             if (i == from || i == origin) continue;
             orc_log(m, ORC_EV_RPC_MSG, j, i, slot, t, g, 0);     /* the copy's RPC (sendRPC, gossipsub.go:1195-1200) */
-            ar_push(p, i, slot, s->rev[e]);
+            ar_push(p, i, slot, s->rev[e], 0);
         }
     }
     p->nfp = 0;
@@ -392,7 +393,7 @@ void orc_round(orc_net* s, orc_msgs* m, int64_t g)
     for (int64_t q = 0; q < p->ngr; ++q) {
         orc_log(m, ORC_EV_RPC_MSG, s->col[p->gr[q].er], p->gr[q].recv, p->gr[q].slot, (int32_t)m->topic[p->gr[q].slot],
                 g, 1);
-        ar_push(p, p->gr[q].recv, p->gr[q].slot, p->gr[q].er);
+        ar_push(p, p->gr[q].recv, p->gr[q].slot, p->gr[q].er, 1);
     }
     p->ngr = 0;
 

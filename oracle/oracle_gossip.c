@@ -386,6 +386,7 @@ void orc_gossip_iwant(orc_net* s, orc_msgs* m, int64_t g)
         p->gr[p->ngr].recv = s->col[ei];
         p->gr[p->ngr].slot = slot;
         p->gr[p->ngr].er = er;
+        p->gr[p->ngr].resp = 1;
         p->ngr++;
     }
     p->niw = 0;

@@ -37,7 +37,11 @@ static inline uint64_t okey(uint64_t seed, uint64_t tick, uint32_t obs, int32_t 
 }
 
 typedef struct fr_ent { uint32_t peer, slot, from; } fr_ent;
-typedef struct arr_ent { uint32_t recv, slot, er; } arr_ent;
+/* a copy at its receiver; resp: an IWANT answer (one RPC per sender and round) */
+typedef struct arr_ent { uint32_t recv, slot, er, resp; } arr_ent;
+/* the peer gater's draw key of an IWANT answer: one draw per (round, receiver,
+ * sender) covers the whole answer RPC (AcceptFrom per RPC, pubsub.go) */
+#define ORC_GATER_RPC_SLOT 0xFFFFFFu
 /* a copy whose receiver is still validating the message: credited or
  * penalised when validation completes in round c (orc_publish_v) */
 typedef struct pend_ent { int64_t c; uint32_t recv, slot, er; int32_t first; } pend_ent;

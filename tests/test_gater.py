@@ -189,3 +189,27 @@ def test_gater_network_bit_exact(require_gpu, weights):
     log = []
     run_parity(net, params, th, gp, st, ticks, sched, ring=512, churn=churn, gater=gater, gater_log=log)
     assert log[-1] > 100, f"the gate should have dropped copies: {log}"
+
+
+@pytest.mark.gpu
+def test_gater_refuses_new_ips(require_gpu):
+    """The gater's per-IP groups are built from the IPs at gsim_set_peer_gater
+    (peer_gater.go getPeerIP at AddPeer): replacing the IPs afterwards is
+    refused (GSIM_ESTATE) rather than leaving the groups stale."""
+    from fixtures import beacon_params
+    from gsim import _abi
+    from gsim.engine import Engine, GsimError, random_regular
+    n = 200
+    net = random_regular(n, 8, seed=3, n_topics=1)
+    ip_ptr = np.arange(n + 1, dtype=np.uint32)
+    ip_ids = (np.arange(n) // 4).astype(np.uint32)
+    eng = Engine(beacon_params(1))
+    try:
+        eng.load_graph(net)
+        eng.set_ips(ip_ptr, ip_ids, n // 4)                 # before the gater: fine
+        eng.set_peer_gater(NewPeerGaterParams(0.05, 0.9, 0.99))
+        with pytest.raises(GsimError) as ex:
+            eng.set_ips(ip_ptr, np.arange(n, dtype=np.uint32), n)
+        assert ex.value.rc == _abi.GSIM_ESTATE
+    finally:
+        eng.close()

@@ -40,9 +40,15 @@ def multi_ips(n, rng, pool):
     return ip_ptr, ip_ids, pool
 
 
-def build(n, k, T, seed, frac_sybil=0.2, topic_cap=0.0, multi_ip=False):
+def build(n, k, T, seed, frac_sybil=0.2, topic_cap=0.0, multi_ip=False, hub_cap=0):
     rng = np.random.default_rng(seed)
-    net = random_regular(n, k, seed=seed, n_topics=T)
+    if hub_cap:
+        # power law with hub rows above 64 connections (k_ip_colocation_hub) up to hub_cap
+        from gsim import graphs
+        net = graphs.power_law(n, k, 2.1, hub_cap, seed=seed, n_topics=T, i0=1.0)
+        assert int(np.diff(net.row_ptr.astype(np.int64)).max()) > 256
+    else:
+        net = random_regular(n, k, seed=seed, n_topics=T)
     if multi_ip:
         net.ip_ptr, net.ip_ids, net.n_ips = multi_ips(n, rng, pool=max(8, n // 40))
     else:
@@ -55,11 +61,16 @@ def build(n, k, T, seed, frac_sybil=0.2, topic_cap=0.0, multi_ip=False):
     return net, params, st, p5, white
 
 
-@pytest.mark.parametrize("n,k,T,cap,multi_ip", [(600, 16, 1, 0.0, False), (2000, 32, 4, 0.0, False),
-                                                (3000, 32, 3, 3.5, False), (1000, 20, 11, 0.0, False),
-                                                (1500, 24, 2, 0.0, True)])
-def test_refresh_and_score_bit_exact(require_gpu, n, k, T, cap, multi_ip):
-    net, params, st, p5, white = build(n, k, T, seed=n + T, topic_cap=cap, multi_ip=multi_ip)
+@pytest.mark.parametrize("n,k,T,cap,multi_ip,hub_cap", [(600, 16, 1, 0.0, False, 0), (2000, 32, 4, 0.0, False, 0),
+                                                        (3000, 32, 3, 3.5, False, 0), (1000, 20, 11, 0.0, False, 0),
+                                                        (1500, 24, 2, 0.0, True, 0), (6000, 12, 2, 0.0, False, 2000),
+                                                        (6000, 12, 2, 0.0, True, 2000)])
+def test_refresh_and_score_bit_exact(require_gpu, n, k, T, cap, multi_ip, hub_cap):
+    """hub_cap: a power law whose hub rows (65-2000 connections) take the
+    sorted-key P6 path (k_ip_colocation_hub), sybil IPs shared by dozens of a
+    hub's members, or several IPs per peer (the hub's per-IP scan)."""
+    net, params, st, p5, white = build(n, k, T, seed=n + T, topic_cap=cap, multi_ip=multi_ip, hub_cap=hub_cap,
+                                       frac_sybil=0.4 if hub_cap else 0.2)
     eng = Engine(params, beacon_thresholds())
     eng.load_graph(net)
     eng.set_app_score(p5)
