@@ -203,10 +203,12 @@ def test_gater_refuses_new_ips(require_gpu):
     net = random_regular(n, 8, seed=3, n_topics=1)
     ip_ptr = np.arange(n + 1, dtype=np.uint32)
     ip_ids = (np.arange(n) // 4).astype(np.uint32)
-    eng = Engine(beacon_params(1))
+    from fixtures import beacon_thresholds
+    eng = Engine(beacon_params(1), beacon_thresholds())
     try:
         eng.load_graph(net)
         eng.set_ips(ip_ptr, ip_ids, n // 4)                 # before the gater: fine
+        eng.msgs_init(64, 10, 0, 10**9)
         eng.set_peer_gater(NewPeerGaterParams(0.05, 0.9, 0.99))
         with pytest.raises(GsimError) as ex:
             eng.set_ips(ip_ptr, np.arange(n, dtype=np.uint32), n)
