@@ -33,6 +33,7 @@ struct Extra {
     // hub observers after them: rows of 65..256, 257..1024, then 1025..4096
     // connections (a block of 1024 threads holding 4 row positions each)
     int64_t nh256 = 0, nh1024 = 0, nh4096 = 0;
+    int64_t nh2048 = 0;                 // the first rows of the 1025-4096 class, of at most 2048 connections
     // peer exchange (gsim_gossipsub_params.do_px): topics with PX PRUNEs per
     // observer, connection attempts per edge, the GRAFT RPCs that turned PX off
     uint64_t* d_pxo = nullptr;
@@ -1446,32 +1447,50 @@ __device__ __forceinline__ void wave_lds_sync()
 // ROW: the longest row staged (WV waves per block, ROW scores and keys each):
 // <kPxRow, 4> walks the owned observers with rows of at most kPxRow,
 // <4 kPxRow, 1> the hub list `rows` (rows of kPxRow+1 .. 4 kPxRow).
-template <int ROW, int WV>
+template <int ROW, int WV, bool SPLIT = false>
 __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32_t key_tick, uint32_t purpose,
                                                      const uint32_t* rows, int64_t nrows)
 {
     const HbArgs& a = a_;
-    __shared__ double s_sc[WV][ROW];
-    __shared__ uint64_t s_key[WV][ROW];
+    // SPLIT (hub rows): the block's waves share one observer and take its PRUNEs in
+    // turn; a wave's keys are then the Philox words alone (the low word is the
+    // row position, the index) with a candidate bitmap, to fit WV rows in LDS
+    using KeyT = typename std::conditional<SPLIT, uint32_t, uint64_t>::type;
+    __shared__ double s_sc[SPLIT ? 1 : WV][ROW];
+    __shared__ KeyT s_key[WV][ROW];
+    __shared__ uint64_t s_ok[SPLIT ? WV : 1][SPLIT ? ROW / 64 : 1];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    double* sc = s_sc[wid];
-    uint64_t* key = s_key[wid];
+    double* sc = s_sc[SPLIT ? 0 : wid];
+    KeyT* key = s_key[wid];
+    uint64_t* ok = s_ok[SPLIT ? wid : 0];
+    auto kget = [&](int q) -> uint64_t {
+        if constexpr (SPLIT) return ((ok[q >> 6] >> (q & 63)) & 1ull) ? (((uint64_t)key[q] << 32) | (uint32_t)q) : ~0ull;
+        else return key[q];
+    };
     const int64_t nobs = rows ? nrows : a.ohi - a.olo;
-    for (int64_t x = (int64_t)blockIdx.x * WV + wid; x < nobs; x += (int64_t)gridDim.x * WV) {
+    constexpr int OPB = SPLIT ? 1 : WV;                          // observers per block
+    const int slot = SPLIT ? 0 : wid;
+    for (int64_t x = (int64_t)blockIdx.x * OPB + slot; x < nobs; x += (int64_t)gridDim.x * OPB) {
         const int64_t obs = rows ? (int64_t)rows[x] : a.olo + x;
         const uint32_t b = a.row_ptr[obs];
         const int deg = (int)(a.row_ptr[obs + 1] - b);
-        if (deg > ROW) continue;                                 // a longer hub: the <4 kPxRow, 1> instance
+        if (deg > ROW) continue;                                 // a longer hub: the hub instances
         const uint64_t mask = a.pxo[obs];
         if (!mask) continue;
-        if (lane == 0) a.pxo[obs] = 0;
         const uint32_t gobs = glob(a, (uint32_t)obs);
-        for (int q = lane; q < deg; q += 64) {
-            const uint32_t e = b + (uint32_t)q, x = a.col[e], rv = a.rev[e];
-            sc[q] = live ? a.pxs[e] : a.score[rv];
-            (void)x;
+        if constexpr (SPLIT) {
+            for (int q = threadIdx.x; q < deg; q += 64 * WV) sc[q] = live ? a.pxs[b + (uint32_t)q] : a.score[a.rev[b + (uint32_t)q]];
+            __syncthreads();                                     // (every wave has read the mask too)
+            if (threadIdx.x == 0) a.pxo[obs] = 0;
+        } else {
+            if (lane == 0) a.pxo[obs] = 0;
+            for (int q = lane; q < deg; q += 64) {
+                const uint32_t e = b + (uint32_t)q, rv = a.rev[e];
+                sc[q] = live ? a.pxs[e] : a.score[rv];
+            }
+            wave_lds_sync();
         }
-        wave_lds_sync();
+        int turn = 0;                                            // SPLIT: the PRUNEs dealt to the waves in turn
         for (uint64_t tm = mask; tm; tm &= tm - 1) {
             const HbArgs& a = hb_launder(a_);   // (re-read per topic: SGPR pressure)
             const int32_t t = __ffsll((long long)tm) - 1;
@@ -1482,6 +1501,9 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
                 const bool pr = slot_has(mp, t) &&
                                 (a.ctl_out[slot_idx(mp, t, a.E, a.rev[ep_l])] & (GSIM_CTL_PX | GSIM_CTL_UNSUB)) == GSIM_CTL_PX;
                 for (uint64_t pm = __ballot(pr); pm; pm &= pm - 1) {
+                    if constexpr (SPLIT) {
+                        if ((turn++ % WV) != wid) continue;
+                    }
                     const int pos = p0 + __ffsll((long long)pm) - 1;
                     const uint32_t ep = b + (uint32_t)pos, p = a.col[ep];
                     // a ghost p: its shard holds its score of obs and its row (below)
@@ -1495,11 +1517,17 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
                         if (q < deg && q != pos) {
                             const uint32_t e = b + (uint32_t)q, x = a.col[e];
                             c = (a.rstate[e] & GSIM_ES_CONNECTED) && ((a.sub[x] >> t) & 1ull) && sc[q] >= 0.0;
-                            key[q] = c ? select_key(a.seed, key_tick, gobs, kt, purpose, glob(a, x), (uint32_t)q) : ~0ull;
+                            const uint64_t kv = c ? select_key(a.seed, key_tick, gobs, kt, purpose, glob(a, x), (uint32_t)q) : ~0ull;
+                            if constexpr (SPLIT) key[q] = (uint32_t)(kv >> 32);
+                            else key[q] = kv;
                         } else if (q < deg) {
-                            key[q] = ~0ull;
+                            if constexpr (!SPLIT) key[q] = ~0ull;
                         }
-                        n += (uint32_t)__popcll(__ballot(c));
+                        const uint64_t cb = __ballot(c);
+                        if constexpr (SPLIT) {
+                            if (lane == 0) ok[q0 >> 6] = cb;
+                        }
+                        n += (uint32_t)__popcll(cb);
                     }
                     wave_lds_sync();
                     // the PrunePeers smallest keys are those below tau: start from the
@@ -1511,13 +1539,13 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
                         int32_t c = 0;
                         for (int q0 = 0; q0 < deg; q0 += 64) {
                             const int q = q0 + lane;
-                            c += (int32_t)__popcll(__ballot(q < deg && key[q] < tau));
+                            c += (int32_t)__popcll(__ballot(q < deg && kget(q) < tau));
                         }
                         while (c > a.prune_peers) {                // drop the largest key below tau
                             uint64_t mx = 0;
                             for (int q0 = 0; q0 < deg; q0 += 64) {
                                 const int q = q0 + lane;
-                                if (q < deg && key[q] < tau && key[q] >= mx) mx = key[q];
+                                if (q < deg && kget(q) < tau && kget(q) >= mx) mx = kget(q);
                             }
                             mx = wave_max_u64(mx);
                             tau = mx;
@@ -1527,7 +1555,7 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
                             uint64_t mn = ~0ull;
                             for (int q0 = 0; q0 < deg; q0 += 64) {
                                 const int q = q0 + lane;
-                                if (q < deg && key[q] >= tau && key[q] < mn) mn = key[q];
+                                if (q < deg && kget(q) >= tau && kget(q) < mn) mn = kget(q);
                             }
                             mn = wave_min_u64(mn);
                             tau = mn + 1;
@@ -1540,7 +1568,7 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
                         const uint64_t hdr = (uint64_t)a.xre[ep] | ((uint64_t)t << 32);
                         for (int q0 = 0; q0 < deg; q0 += 64) {
                             const int q = q0 + lane;
-                            const bool in = q < deg && key[q] < tau;
+                            const bool in = q < deg && kget(q) < tau;
                             const uint64_t bm = __ballot(in);
                             uint32_t base = 0;
                             if (lane == 0 && bm) base = atomicAdd(&a.pxcnt[d], (uint32_t)__popcll(bm));
@@ -1557,7 +1585,7 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
                     const uint32_t pb = a.row_ptr[p], pe = a.row_ptr[p + 1];
                     for (int q0 = 0; q0 < deg; q0 += 64) {
                         const int q = q0 + lane;
-                        if (q >= deg || key[q] >= tau) continue;
+                        if (q >= deg || kget(q) >= tau) continue;
                         const uint32_t x = a.col[b + (uint32_t)q];
                         uint32_t lo = pb, hi = pe;                 // p's row is sorted: its edge to x
                         while (lo < hi) {
@@ -1571,7 +1599,30 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
                 }
             }
         }
+        if constexpr (SPLIT) __syncthreads();                    // sc is rewritten by the next observer
     }
+}
+
+// makePrune's PX lists of every observer that sent PX PRUNEs: rows of at most
+// 256 connections a wave each (4 observers per block), hub rows (257-1024,
+// 1025-4096) a block of 4 waves each sharing the observer's scores and taking
+// its PRUNEs in turn (a hub's GRAFT replies are many: one wave made c5's hub
+// pass 20 ms per tick).
+constexpr int kPxSmall = 256;
+static void launch_px_emit(gsim_handle* h, const HbArgs& a, int live, uint32_t key_tick, uint32_t purpose)
+{
+    const Extra* x = h->x;
+    const int64_t nown = h->ohi() - h->olo();
+    hipLaunchKernelGGL((k_px_emit<kPxSmall, 4>), dim3((uint32_t)std::min<int64_t>(std::max<int64_t>((nown + 3) / 4, 1), 65536)),
+                       dim3(256), 0, h->stream, a, live, key_tick, purpose, (const uint32_t*)nullptr, (int64_t)0);
+    if (!x->d_rows) return;                      // one class of rows <= 16: no hub
+    const uint32_t* rh = x->d_rows + x->n16 + x->n32 + x->n64 + x->nh256;
+    if (x->nh1024)
+        hipLaunchKernelGGL((k_px_emit<kPxRow, 4, true>), dim3((uint32_t)std::min<int64_t>(x->nh1024, 65536)), dim3(256),
+                           0, h->stream, a, live, key_tick, purpose, rh, x->nh1024);
+    if (x->nh4096)
+        hipLaunchKernelGGL((k_px_emit<4 * kPxRow, 4, true>), dim3((uint32_t)std::min<int64_t>(x->nh4096, 65536)),
+                           dim3(256), 0, h->stream, a, live, key_tick, purpose, rh + x->nh1024, x->nh4096);
 }
 
 // Connection attempts to connections (the connector, gossipsub.go:941-973):
@@ -2222,6 +2273,13 @@ int alloc_extra(gsim_handle* h)
         for (int c = 0; c < 2; ++c)
             std::stable_sort(cls[c].begin(), cls[c].end(), [&](uint32_t x, uint32_t y) { return sub[x] < sub[y]; });
     }
+    // the 1025-4096 class by row length: its first nh2048 rows take 2 positions
+    // per thread (k_heartbeat_hub<1024, 2>: 4 spill registers)
+    std::stable_sort(cls[5].begin(), cls[5].end(), [&](uint32_t x, uint32_t y) {
+        return rp[(size_t)x + 1] - rp[(size_t)x] < rp[(size_t)y + 1] - rp[(size_t)y];
+    });
+    h->x->nh2048 = (int64_t)std::count_if(cls[5].begin(), cls[5].end(),
+                                          [&](uint32_t x) { return rp[(size_t)x + 1] - rp[(size_t)x] <= 2048u; });
     h->x->max_degree = md;
     h->x->n16 = (int64_t)cls[0].size(); h->x->n32 = (int64_t)cls[1].size(); h->x->n64 = (int64_t)cls[2].size();
     h->x->nh256 = (int64_t)cls[3].size(); h->x->nh1024 = (int64_t)cls[4].size(); h->x->nh4096 = (int64_t)cls[5].size();
@@ -2454,9 +2512,12 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
         if (x->nh1024)
             hipLaunchKernelGGL((k_heartbeat_hub<1024, 1>), dim3((uint32_t)std::min<int64_t>(x->nh1024, 65536)),
                                dim3(1024), 0, h->stream, a, rh + x->nh256, x->nh1024);
-        if (x->nh4096)   // 4 row positions per thread
-            hipLaunchKernelGGL((k_heartbeat_hub<1024, 4>), dim3((uint32_t)std::min<int64_t>(x->nh4096, 65536)),
-                               dim3(1024), 0, h->stream, a, rh + x->nh256 + x->nh1024, x->nh4096);
+        if (x->nh2048)   // 2 row positions per thread
+            hipLaunchKernelGGL((k_heartbeat_hub<1024, 2>), dim3((uint32_t)std::min<int64_t>(x->nh2048, 65536)),
+                               dim3(1024), 0, h->stream, a, rh + x->nh256 + x->nh1024, x->nh2048);
+        if (x->nh4096 > x->nh2048)   // 4 row positions per thread
+            hipLaunchKernelGGL((k_heartbeat_hub<1024, 4>), dim3((uint32_t)std::min<int64_t>(x->nh4096 - x->nh2048, 65536)),
+                               dim3(1024), 0, h->stream, a, rh + x->nh256 + x->nh1024 + x->nh2048, x->nh4096 - x->nh2048);
     }
     hipLaunchKernelGGL(k_fanout_heartbeat, dim3(grid_rows(nown)), dim3(256), 0, h->stream, a);
     const uint32_t* rh = x->d_rows + x->n16 + x->n32 + x->n64;
@@ -2469,14 +2530,8 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     if (x->nh4096)
         hipLaunchKernelGGL((k_fanout_heartbeat_hub<1024, 4>), dim3((uint32_t)std::min<int64_t>(x->nh4096, 65536)),
                            dim3(1024), 0, h->stream, a, rh + x->nh256 + x->nh1024, x->nh4096);
-    if (a.do_px) {  // sendGraftPrune's makePrune with PX, live scores after every topic
-        hipLaunchKernelGGL((k_px_emit<kPxRow, 4>), dim3(grid_rows(nown)), dim3(256), 0, h->stream, a, 1, (uint32_t)tick,
-                           (uint32_t)P_PX, (const uint32_t*)nullptr, (int64_t)0);
-        if (x->nh4096)
-            hipLaunchKernelGGL((k_px_emit<4 * kPxRow, 1>), dim3((uint32_t)std::min<int64_t>(x->nh4096, 65536)), dim3(64),
-                               0, h->stream, a, 1, (uint32_t)tick, (uint32_t)P_PX,
-                               (const uint32_t*)(rh + x->nh256 + x->nh1024), x->nh4096);
-    }
+    if (a.do_px)    // sendGraftPrune's makePrune with PX, live scores after every topic
+        launch_px_emit(h, a, 1, (uint32_t)tick, (uint32_t)P_PX);
     return hip_check(h, hipGetLastError(), "k_heartbeat");
 }
 
@@ -2489,14 +2544,7 @@ int handle_control(gsim_handle* h, int32_t round, int64_t now)
     hipLaunchKernelGGL(k_handle_control, dim3(grid_rows(h->ohi() - h->olo())), dim3(256), 0, h->stream, a);
     if (a.do_px) {  // handleGraft's PRUNE replies with PX (snapshot scores)
         const uint32_t kt = (uint32_t)((uint64_t)now ^ ((uint64_t)now >> 32));
-        hipLaunchKernelGGL((k_px_emit<kPxRow, 4>), dim3(grid_rows(h->ohi() - h->olo())), dim3(256), 0, h->stream, a, 0,
-                           kt, (uint32_t)P_PX_GRAFT, (const uint32_t*)nullptr, (int64_t)0);
-        const Extra* x = h->x;
-        if (x->nh4096)
-            hipLaunchKernelGGL((k_px_emit<4 * kPxRow, 1>), dim3((uint32_t)std::min<int64_t>(x->nh4096, 65536)), dim3(64),
-                               0, h->stream, a, 0, kt, (uint32_t)P_PX_GRAFT,
-                               (const uint32_t*)(x->d_rows + x->n16 + x->n32 + x->n64 + x->nh256 + x->nh1024),
-                               x->nh4096);
+        launch_px_emit(h, a, 0, kt, (uint32_t)P_PX_GRAFT);
     }
     return hip_check(h, hipGetLastError(), "k_handle_control");
 }

@@ -365,7 +365,8 @@ def test_hub_rows_bit_exact(require_gpu, topic_slots):
 def test_c5_combined_wide_hubs_zipf_churn_px_verdicts(require_gpu, topic_slots, shards):
     """C5's whole shape on one engine and on 3 shards: a plain Chung-Lu
     power law (exponent 2.5, i0 = 1) whose hubs exceed 1024 connections (up
-    to the 4096 cap: heartbeat, fanout and PX on 4 row positions per thread),
+    to the 4096 cap: the heartbeat on 2 row positions per thread up to 2048 connections and 4
+    beyond, PX on a block of 4 waves per hub observer),
     64 topics with Zipf subscriptions, dense meshes on the hubs (Dhi prune
     ranks over thousands of positions), churn, peer exchange with the
     connector, every validation verdict, fanout publishers outside their
