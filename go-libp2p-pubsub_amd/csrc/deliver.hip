@@ -1594,6 +1594,7 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a_, const uint32_t* gcount
             if (k >= nact) break;                            // wave-uniform
             const uint32_t m = s_act[k] & 0x7FFF;
             const bool push = (s_act[k] & 0x8000) != 0;
+            if (MM && !push) continue;                       // pulled below, one row walk for many slots
             const int32_t t = (int32_t)a.mtopic[m];
             const uint32_t origin = a.morigin[m];
             const bool inv = a.minv[m] != 0;
@@ -1690,6 +1691,90 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a_, const uint32_t* gcount
                 n_walk += (lane == 0);
                 for (uint32_t off = 0; off < end - beg; off += 64)
                     chunk(off, (uint32_t)lane, beg, end - beg, me_id, me_g, ign_s, me_pl);
+            }
+        }
+    }
+    if constexpr (MM) {
+        // pull slots of the block's topic, up to 64 at a time: a receiver walks
+        // its row once for all the slots it wants (not once per slot), and an
+        // edge whose advertiser gossiped tb to it asks for each wanted slot
+        // the advertiser holds (the same (receiver, advertiser, message)
+        // triples as a walk per slot)
+        const bool rcv = vp && ((subp >> tb) & 1ull) && pl >= a.rlo && pl < a.rhi;
+        for (int k0 = 0; k0 < nact; k0 += 64) {
+            const int kn = nact - k0 < 64 ? nact - k0 : 64;
+            uint64_t wm = 0;
+            for (int q = 0; q < kn; ++q) {
+                const uint16_t sa = s_act[k0 + q];
+                if (sa & 0x8000) continue;                   // pushed above (wave-uniform)
+                const uint64_t c = rcv ? a.cs.cell[(int64_t)a.cs.cbase[sa & 0x7FFF] + jw + lane] : 0ull;
+                if (rcv && c == kUnseen64) wm |= 1ull << q;
+            }
+            const uint64_t mask = __ballot(wm != 0);
+            if (!mask) continue;
+            const int32_t t = tb;
+            auto pchunk = [&](uint32_t off, uint32_t gl_, uint32_t beg, uint32_t deg, uint32_t me_g, uint64_t wmw) {
+                const bool v = off + gl_ < deg;
+                const uint32_t e = beg + off + gl_;
+                uint32_t re = 0, i = 0;
+                bool gs = false;
+                if (v) {
+                    re = a.rev[e];
+                    i = a.col[e];
+                    const uint64_t mi = smask_of(a.smask, i);        // i's emitGossip choices: its row
+                    gs = slot_has(mi, t) && a.gsel[slot_idx(mi, t, a.E, re)] && a.gstate[e];
+                }
+                const uint64_t mine = gs ? wmw : 0ull;
+                uint64_t uw = mine;                                  // the slots some lane asks about
+                for (int o = 32; o; o >>= 1) uw |= (uint64_t)__shfl_xor((long long)uw, o, 64);
+                const uint32_t ig = gs ? (a.gid ? a.gid[i] : i) : 0u;
+                for (; uw; uw &= uw - 1) {
+                    const int q = __builtin_ctzll(uw);
+                    const uint32_t m = s_act[k0 + q] & 0x7FFF;
+                    bool req = false, resp = false;
+                    if ((mine >> q) & 1ull) {
+                        const int64_t ici = a.cs.at((int64_t)a.cs.cbase[m], t, i);
+                        req = holds_in_window(ici >= 0 ? a.cs.cell[ici] : kUnseen64, a.g, a.lo_round, tick_round,
+                                              a.minv[m] != 0, i == a.morigin[m], LAT ? a.mlat[m] : 0u);
+                        if (req) {
+                            const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, me_g, 0, P_PROMISE, m, ig);
+                            atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[e]), (unsigned long long)key);
+                            resp = a.respond && a.gstate[re] && !(a.behaviour[i] & GSIM_BEHAVE_IGNORE_IWANT) &&
+                                   peertx_allows(a, m, re, i);
+                        }
+                    }
+                    n_req += req;
+                    n_resp += resp;
+                    const uint64_t sb = __ballot(resp);
+                    if (sb) {
+                        if (nstage + __popcll(sb) > kRespStage) flush_stage();
+                        if (resp) stage[nstage + __popcll(sb & ((1ull << lane) - 1))] = (uint64_t)re | ((uint64_t)m << 32);
+                        nstage += __popcll(sb);
+                    }
+                }
+            };
+            const uint64_t longm = mask & long_lanes;
+            uint64_t gm = mask & ~longm & gmask;
+            while (__ballot(gm != 0)) {
+                int bs = -1;
+                if (gm) { bs = __ffsll((long long)gm) - 1; gm &= gm - 1; }
+                const int sl = bs < 0 ? lane : bs;
+                const uint32_t beg = __shfl(rp0, sl, 64), end = __shfl(rp1, sl, 64);
+                const uint32_t me_id = (uint32_t)__shfl((int)pl, sl, 64);
+                const uint64_t wmw = bs < 0 ? 0ull : (uint64_t)__shfl((long long)wm, sl, 64);
+                const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
+                n_walk += (gl == 0 && bs >= 0);
+                const uint32_t deg = bs >= 0 ? end - beg : 0u;
+                for (uint32_t off = 0; __ballot(off < deg) != 0; off += W) pchunk(off, (uint32_t)gl, beg, deg, me_g, wmw);
+            }
+            for (uint64_t lm = longm; lm; lm &= lm - 1) {
+                const int bs = __builtin_ctzll(lm);
+                const uint32_t beg = __shfl(rp0, bs, 64), end = __shfl(rp1, bs, 64);
+                const uint32_t me_id = (uint32_t)__shfl((int)pl, bs, 64);
+                const uint64_t wmw = (uint64_t)__shfl((long long)wm, bs, 64);
+                const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
+                n_walk += (lane == 0);
+                for (uint32_t off = 0; off < end - beg; off += 64) pchunk(off, (uint32_t)lane, beg, end - beg, me_g, wmw);
             }
         }
     }
