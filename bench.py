@@ -359,6 +359,9 @@ def main():
                     help="validation latency of every message in rounds (gsim_msg.vdelay)")
     ap.add_argument("--replicas", action="store_true",
                     help="N > 1: one independent network per rank (weak scaling) instead of one sharded network")
+    ap.add_argument("--peers", type=int, default=None,
+                    help="peers of the config's network (its default otherwise): a reduced shape, e.g. c5 split "
+                         "into 8 shards on one GPU, whose ghost rows would not fit its HBM at 10M peers")
     ap.add_argument("--shards", type=int, default=1,
                     help="N = 1: split the network into this many shards on the one GPU (exercises the halo "
                          "exchange through the in-process transport; not the headline configuration)")
@@ -384,6 +387,8 @@ def main():
         dist.init_process_group("nccl")
 
     cfg = CONFIGS[args.config]
+    if args.peers:
+        cfg = (args.peers,) + tuple(cfg[1:])
     scen = dict(SCENARIOS.get(args.config, {}))
     if args.msg_rate is not None:
         scen["msg_rate"] = args.msg_rate
@@ -471,7 +476,8 @@ def main():
 
     if rank == 0:
         K = args.steps
-        workload = (f"{args.config}: {n} peers, {describe_graph(cfg, scen)}, {T} topics, beacon-style params, "
+        workload = (f"{args.config}: {n} peers{' (reduced: --peers)' if args.peers else ''}, "
+                    f"{describe_graph(cfg, scen)}, {T} topics, beacon-style params, "
                     f"{rate:g} msg/s/topic, {ROUNDS} rounds/heartbeat")
         # peer-heartbeats of the whole job: one network (sharded) or one per rank
         value = n * (1 if sharded else world) * K / wall

@@ -224,15 +224,14 @@ struct RoundArgs {
     // sharded: the edges of each row into owned peers (the copies this shard
     // delivers), a CSR of edge indices: row x's are sedge[sptr[x] .. sptr[x+1])
     const uint32_t *sptr, *sedge;
-    // sharded, copy push: a copy to a ghost receiver goes to
-    // sub-list (its shard pshard[i], block % kXSub) as xre[e] | slot << 32
-    int32_t push, xK;
+    // sharded, copy push: a copy of slot m on cross edge e sets
+    // bit xwq[e] of row m of xbits ([ring][xbw] words: per destination shard a
+    // word-aligned segment, bit = the edge's position in the cross-out list)
+    int32_t push;
     int64_t slo, shi;              // k_send_tm's senders: [slo, shi) (slo a multiple of its chunk)
-    const uint32_t* xre;
-    const uint8_t* pshard;
-    uint64_t* xsub;
-    uint32_t* xcnt;
-    int64_t xsub_cap;
+    const uint32_t* xwq;
+    uint64_t* xbits;
+    int64_t xbw;
     // [T][n] rows of at most 64 connections: bit q = row position q is a mesh or
     // direct edge (to an owned peer); a forwarder other than the origin sends
     // on no other edge, so only these are walked
@@ -396,7 +395,8 @@ __device__ __forceinline__ void clist_push_wave(const RoundArgs& a, bool on, uin
     const uint64_t b = __ballot(on);
     if (!b) return;
     const int lane = threadIdx.x & 63, leader = __builtin_ctzll(b);
-    const uint32_t q = blockIdx.x % kClSub;
+    // sub-list by wave: a popular topic's few blocks spread over all of them
+    const uint32_t q = (blockIdx.x * 16u + (threadIdx.x >> 6)) % kClSub;
     uint32_t base = 0;
     if (lane == leader) base = atomicAdd(&a.clist_n[q * kClStride], (uint32_t)__popcll(b));
     base = (uint32_t)__shfl((int)base, leader, 64);
@@ -409,33 +409,6 @@ __device__ __forceinline__ void clist_push_wave(const RoundArgs& a, bool on, uin
 
 // Ordered list of the active slots (bit set in nnew), built by wave 0 into
 // LDS; every thread of the block must call it.
-// A copy to a ghost receiver (k_send_tm<PUSH>): entry v = receiver-shard edge
-// | slot << 32 | shard << 48 appended to sub-list (shard, wave % kXSub); one
-// atomic per (wave, destination).  Wave-uniform call.
-__device__ __forceinline__ void xcopy_push_wave(const RoundArgs& a, bool on, uint64_t v)
-{
-    const int lane = threadIdx.x & 63;
-    const uint32_t dst = (uint32_t)(v >> 48);
-    uint64_t act = __ballot(on);
-    while (act) {
-        const int leader = __builtin_ctzll(act);
-        const uint32_t dl = (uint32_t)__shfl((int)dst, leader, 64);
-        const bool mine = on && dst == dl;
-        const uint64_t grp = __ballot(mine);
-        // sub-list by wave: the block's waves spread over the counters (each on its own line)
-        const int64_t sl = (int64_t)dl * kXSub + (int64_t)((blockIdx.x * 16u + (threadIdx.x >> 6)) % kXSub);
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&a.xcnt[sl * kXStride], (uint32_t)__popcll(grp));
-        base = (uint32_t)__shfl((int)base, leader, 64);
-        if (mine) {
-            const uint32_t q = base + (uint32_t)__popcll(grp & ((1ull << lane) - 1ull));
-            if ((int64_t)q < a.xsub_cap) a.xsub[sl * a.xsub_cap + q] = v & 0xFFFFFFFFFFFFull;
-            else atomicOr(&a.xcnt[(int64_t)a.xK * kXSub * kXStride], 1u);   // overflow: the round fails
-        }
-        act &= ~grp;
-    }
-}
-
 __device__ __forceinline__ int active_slots(const uint32_t* nnew, int ring, uint16_t* s_act, int* s_n)
 {
     if (threadIdx.x < 64) {
@@ -751,8 +724,8 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
     __shared__ uint8_t s_sk[kTmChunk];                       // its slot (index in the pass)
     __shared__ uint8_t s_pl[kTmChunk];                       // its row's topic slot of t (plane, gsim_internal.h)
     __shared__ uint16_t s_own[kTmWin];                       // sender (index above) of each flattened edge of a window
-    // claim-list entries of the iteration's copies, or (PUSH) copies to ghost receivers
-    __shared__ uint64_t s_cl[(SP && !LAT) || PUSH ? kTmThreads * GSIM_TM_P : 1];
+    // claim-list entries of the iteration's copies
+    __shared__ uint64_t s_cl[(SP && !LAT) ? kTmThreads * GSIM_TM_P : 1];
     __shared__ uint32_t s_wsum[64];
     __shared__ uint32_t s_m[kTsSlots], s_org[kTsSlots];      // the pass's slots and their origins
     __shared__ uint64_t s_cb[kTsSlots];                      // ... and their first cells (Cells::cbase)
@@ -1009,7 +982,6 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                         int qpl[P];              // validation latency: queue plane of the copy (-1: none)
                         uint64_t qv[P];
                         uint32_t clw = 0;        // bit u: copy u claimed an unseen cell (its entry in s_cl)
-                        uint32_t xw = 0;         // bit u: copy u goes to a ghost receiver's shard (PUSH, s_cl)
 #pragma unroll
                         for (int u = 0; u < P; ++u) { qpl[u] = -1; qv[u] = 0; }
 #pragma unroll
@@ -1039,9 +1011,9 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             if constexpr (PUSH) {
                                 // the receiver's shard delivers it (its AcceptFrom, records, cell)
                                 if (tg && remote) {
-                                    xw |= 1u << u;
-                                    s_cl[u * kTmThreads + tid] = (uint64_t)a.xre[e] | ((uint64_t)m << 32) |
-                                                                 ((uint64_t)a.pshard[i] << 48);
+                                    const uint32_t xb = a.xwq[e];
+                                    atomicOr(reinterpret_cast<unsigned long long*>(a.xbits + (int64_t)m * a.xbw + (xb >> 6)),
+                                             1ull << (xb & 63u));
                                     continue;
                                 }
                             }
@@ -1155,10 +1127,6 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                                 for (int u = 0; u < P; ++u)
                                     clist_push_wave(a, (clw >> u) & 1u, s_cl[u * kTmThreads + tid]);
                             }
-                        }
-                        if constexpr (PUSH) {
-#pragma unroll
-                            for (int u = 0; u < P; ++u) xcopy_push_wave(a, (xw >> u) & 1u, s_cl[u * kTmThreads + tid]);
                         }
                     }
                     if (tab) __syncthreads();                    // s_own is rewritten by the next window
@@ -2014,10 +1982,104 @@ __device__ __forceinline__ void atomic_mcnt_inc(uint8_t* mcnt, int64_t ir, doubl
     }
 }
 
+// One copy of slot m on record r (the receiver col[r]'s record of the sender,
+// the row owner): AcceptFrom, the peer gater, the claim of the receiver's
+// cell (the lowest edge wins), the record's counters -- k_send_tm's rules for
+// a copy that arrives listed (k_gossip_deliver) or as a bit (k_xbits_deliver).
+// A record can receive several copies in one launch: counters are atomic.
+__device__ __forceinline__ void listed_copy(const RoundArgs& a, uint32_t r, uint32_t m, const uint32_t* owner,
+                                            uint32_t par, uint32_t claim_hi, ctp_t tpa, unsigned long long& n_acc,
+                                            unsigned long long& n_gray, unsigned long long& n_first, uint32_t* s_new2)
+{
+    const uint8_t ds = a.dstate[r];
+    if (!(ds & GSIM_DS_ACCEPT)) { n_gray++; return; }        // AcceptFrom
+    const uint32_t p = a.col[r];
+    // the sender (row owner) is read only where it matters: topic slots,
+    // the gater, the trace, a claim (most copies are plain duplicates)
+    const bool need_i = a.smask || a.gt.act || a.tr.on(p);
+    uint32_t i = need_i ? owner[r] : 0xFFFFFFFFu;
+    // the peer gater (gater_accept): one draw per IWANT answer RPC -- (round,
+    // receiver, sender), the slot left out (AcceptFrom runs per RPC, pubsub.go);
+    // a shard's pushed copies are forwarded messages, one RPC each
+    if (a.gt.act && !gater_accept(a, p, r, a.sharded ? m : kGaterRpcSlot, i)) return;
+    if (a.subdyn && !((a.sub[p] >> (int32_t)a.mtopic[m]) & 1ull)) return;   // a topic p left
+    if (a.gt.act) gater_copy(a, r, a.minv[m] == GSIM_VERDICT_SIGNATURE);
+    n_acc++;
+    const int32_t t = (int32_t)a.mtopic[m];
+    const ctp_t tp = tpa + t;
+    const uint8_t vd = a.minv[m];
+    if (a.tr.on(p))
+        a.tr.push(round_time(a, a.g), ((uint64_t)a.g << 32) | m, p, i, t,
+                  vd != GSIM_VERDICT_SIGNATURE ? kTraceCopy : (uint8_t)GSIM_TRACE_REJECT_MESSAGE, vd);
+    const bool inv = vd != GSIM_VERDICT_ACCEPT;
+    const bool pen = verdict_penalises(vd);
+    const uint64_t mi = smask_of(a.smask, i);               // the record sits in the sender's row
+    const int64_t ir = slot_idx(mi, t, a.E, r);
+    const bool sc = tp->scored && (ds & GSIM_DS_TRACKED) && slot_has(mi, t);
+    const uint8_t tf = a.tflags[ir];
+    const int64_t window = tp->mesh_message_deliveries_window_ns;
+    const uint32_t L = a.mlat ? a.mlat[m] : 0u;
+    // committed before this round and the cell's round cannot matter (as
+    // k_send_tm's known copies): a duplicate, credited without the cell
+    if (!L && ((a.seenbm[(int64_t)m * a.nw + (p >> 6)] >> (p & 63)) & 1ull)) {
+        const bool wa = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
+        if (wa || !sc || inv || !(tf & GSIM_TF_IN_MESH)) {
+            if (!sc) return;
+            if (pen) atomicAdd(&a.invalid[ir], 1.0);
+            else if (!inv && (tf & GSIM_TF_IN_MESH))         // wa: within the window
+                atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], tp->mesh_message_deliveries_cap);
+            return;
+        }
+    }
+    const int64_t pci = a.cs.idx(m, t, p);      // p wanted it: a member of t
+    if (pci < 0) return;
+    uint64_t* cellp = a.cs.cell + pci;
+    const uint64_t c = *cellp;
+    const uint32_t hi = (uint32_t)(c >> 32);
+    int64_t seen_round = -1;               // completion round (k_send_tm)
+    if (c != kUnseen64) {
+        if (!(hi & kClaim)) seen_round = hi;
+        else if (((hi >> 30) & 1u) != par) seen_round = a.g - 1 + L;
+    }
+    if (vd != GSIM_VERDICT_SIGNATURE && seen_round < 0 && (c == kUnseen64 || (hi & kEdgeMask) > r)) {
+        if (!need_i) i = owner[r];
+        uint32_t lo = i;
+        if (sc && !inv) {
+            lo |= kCreditFirst;
+            if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo |= kCreditMesh;
+        }
+        const uint64_t v = ((uint64_t)(claim_hi | r) << 32) | lo;
+        const uint64_t prev = __hip_atomic_fetch_min(cellp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == kUnseen64) {
+            n_first++;
+            atomicOr(&s_new2[m >> 5], 1u << (m & 31));
+            if (a.clist) {
+                const uint32_t sq = blockIdx.x % kClSub;
+                const uint32_t q = atomicAdd(&a.clist_n[sq * kClStride], 1u);
+                if ((int64_t)q < a.clist_cap) a.clist[(int64_t)sq * a.clist_cap + q] = (uint64_t)p | ((uint64_t)m << 32);
+                else atomicOr(&a.clist_n[kClSub * kClStride], 1u);
+            }
+        }
+    }
+    if (L && vd != GSIM_VERDICT_SIGNATURE && (seen_round < 0 || seen_round > a.g)) {
+        // the lanes here push together (ballots over the active lanes)
+        const bool q = tp->scored && (pen || !inv);
+        vq_push_wave(a, q ? (int)((seen_round < 0 ? a.g + L : seen_round) & (kVqPlanes - 1)) : -1,
+                     vq_entry(r, t, pen ? kVqInv : kVqDup));
+        return;
+    }
+    if (!sc) return;
+    if (pen) {
+        atomicAdd(&a.invalid[ir], 1.0);                           // markInvalidMessageDelivery
+    } else if (!inv && (tf & GSIM_TF_IN_MESH)) {
+        const bool in_window = seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window) : (window >= 0);
+        if (in_window) atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], tp->mesh_message_deliveries_cap);
+    }
+}
+
 // Copies that arrive as a list of (record, slot): round 2's messages queued by
-// handleIWant, and a shard's copies pushed by other shards (shard.hip).  Same
-// rules and tracer events as k_send_tm's copies; a record can receive several
-// copies in one launch, so counters are updated atomically.
+// handleIWant (a shard's copies pushed by other shards arrive as bits:
+// k_xbits_deliver).  Same rules and tracer events as k_send_tm's copies.
 __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a_, const uint64_t* resp, const uint32_t* nresp,
                                                        const uint32_t* owner, int64_t resp_cap)
 {
@@ -2046,90 +2108,7 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a_, const uint
             if (a.tr.on(rs)) a.tr.push(round_time(a, a.g - 1), ((uint64_t)a.g << 32) | m, rs, rp, rt, GSIM_TRACE_SEND_RPC, 1);
             if (a.tr.on(rp)) a.tr.push(round_time(a, a.g), ((uint64_t)a.g << 32) | m, rp, rs, rt, GSIM_TRACE_RECV_RPC, 1);
         }
-        const uint8_t ds = a.dstate[r];
-        if (!(ds & GSIM_DS_ACCEPT)) { n_gray++; continue; }        // AcceptFrom
-        const uint32_t p = a.col[r];
-        // the sender (row owner) is read only where it matters: topic slots,
-        // the gater, the trace, a claim (most copies are plain duplicates)
-        const bool need_i = a.smask || a.gt.act || a.tr.on(p);
-        uint32_t i = need_i ? owner[r] : 0xFFFFFFFFu;
-        // the peer gater (gater_accept): one draw per IWANT answer RPC -- (round,
-        // receiver, sender), the slot left out (AcceptFrom runs per RPC, pubsub.go);
-        // a shard's pushed copies are forwarded messages, one RPC each
-        if (a.gt.act && !gater_accept(a, p, r, a.sharded ? m : kGaterRpcSlot, i)) continue;
-        if (a.subdyn && !((a.sub[p] >> (int32_t)a.mtopic[m]) & 1ull)) continue;   // a topic p left
-        if (a.gt.act) gater_copy(a, r, a.minv[m] == GSIM_VERDICT_SIGNATURE);
-        n_acc++;
-        const int32_t t = (int32_t)a.mtopic[m];
-        const ctp_t tp = tpa + t;
-        const uint8_t vd = a.minv[m];
-        if (a.tr.on(p))
-            a.tr.push(round_time(a, a.g), ((uint64_t)a.g << 32) | m, p, i, t,
-                      vd != GSIM_VERDICT_SIGNATURE ? kTraceCopy : (uint8_t)GSIM_TRACE_REJECT_MESSAGE, vd);
-        const bool inv = vd != GSIM_VERDICT_ACCEPT;
-        const bool pen = verdict_penalises(vd);
-        const uint64_t mi = smask_of(a.smask, i);               // the record sits in the sender's row
-        const int64_t ir = slot_idx(mi, t, a.E, r);
-        const bool sc = tp->scored && (ds & GSIM_DS_TRACKED) && slot_has(mi, t);
-        const uint8_t tf = a.tflags[ir];
-        const int64_t window = tp->mesh_message_deliveries_window_ns;
-        const uint32_t L = a.mlat ? a.mlat[m] : 0u;
-        // committed before this round and the cell's round cannot matter (as
-        // k_send_tm's known copies): a duplicate, credited without the cell
-        if (!L && ((a.seenbm[(int64_t)m * a.nw + (p >> 6)] >> (p & 63)) & 1ull)) {
-            const bool wa = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
-            if (wa || !sc || inv || !(tf & GSIM_TF_IN_MESH)) {
-                if (!sc) continue;
-                if (pen) atomicAdd(&a.invalid[ir], 1.0);
-                else if (!inv && (tf & GSIM_TF_IN_MESH))         // wa: within the window
-                    atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], tp->mesh_message_deliveries_cap);
-                continue;
-            }
-        }
-        const int64_t pci = a.cs.idx(m, t, p);      // p wanted it: a member of t
-        if (pci < 0) continue;
-        uint64_t* cellp = a.cs.cell + pci;
-        const uint64_t c = *cellp;
-        const uint32_t hi = (uint32_t)(c >> 32);
-        int64_t seen_round = -1;               // completion round (k_send_tm)
-        if (c != kUnseen64) {
-            if (!(hi & kClaim)) seen_round = hi;
-            else if (((hi >> 30) & 1u) != par) seen_round = a.g - 1 + L;
-        }
-        if (vd != GSIM_VERDICT_SIGNATURE && seen_round < 0 && (c == kUnseen64 || (hi & kEdgeMask) > r)) {
-            if (!need_i) i = owner[r];
-            uint32_t lo = i;
-            if (sc && !inv) {
-                lo |= kCreditFirst;
-                if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo |= kCreditMesh;
-            }
-            const uint64_t v = ((uint64_t)(claim_hi | r) << 32) | lo;
-            const uint64_t prev = __hip_atomic_fetch_min(cellp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (prev == kUnseen64) {
-                n_first++;
-                atomicOr(&s_new2[m >> 5], 1u << (m & 31));
-                if (a.clist) {
-                    const uint32_t sq = blockIdx.x % kClSub;
-                    const uint32_t q = atomicAdd(&a.clist_n[sq * kClStride], 1u);
-                    if ((int64_t)q < a.clist_cap) a.clist[(int64_t)sq * a.clist_cap + q] = (uint64_t)p | ((uint64_t)m << 32);
-                    else atomicOr(&a.clist_n[kClSub * kClStride], 1u);
-                }
-            }
-        }
-        if (L && vd != GSIM_VERDICT_SIGNATURE && (seen_round < 0 || seen_round > a.g)) {
-            // the lanes here push together (ballots over the active lanes)
-            const bool q = tp->scored && (pen || !inv);
-            vq_push_wave(a, q ? (int)((seen_round < 0 ? a.g + L : seen_round) & (kVqPlanes - 1)) : -1,
-                         vq_entry(r, t, pen ? kVqInv : kVqDup));
-            continue;
-        }
-        if (!sc) continue;
-        if (pen) {
-            atomicAdd(&a.invalid[ir], 1.0);                           // markInvalidMessageDelivery
-        } else if (!inv && (tf & GSIM_TF_IN_MESH)) {
-            const bool in_window = seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window) : (window >= 0);
-            if (in_window) atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], tp->mesh_message_deliveries_cap);
-        }
+        listed_copy(a, r, m, owner, par, claim_hi, tpa, n_acc, n_gray, n_first, s_new2);
     }
     n_acc = wave_sum_u64(n_acc);
     n_gray = wave_sum_u64(n_gray);
@@ -2457,9 +2436,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
         if (sh->push) {
             // owned senders walk their whole rows; ghosts never send here
             a.push = 1;
-            a.xK = sh->K;
-            a.xre = sh->d_xre; a.pshard = sh->d_pshard;
-            a.xsub = sh->d_xsub; a.xcnt = sh->d_xcnt; a.xsub_cap = sh->xsub_cap;
+            a.xwq = sh->d_xwq; a.xbits = sh->d_xbits; a.xbw = sh->xbw;
             a.slo = (sh->own_lo / (2 * kPushTB)) * (2 * kPushTB);   // whole chunks of the push walk
             a.shi = sh->own_hi;
         } else {
@@ -2920,6 +2897,8 @@ int deliver_round_validate(gsim_handle* h, int64_t round)
 }
 
 // Stage 2: the delivery kernel of round g.
+static int xbits_gather(gsim_handle* h, int64_t round);   // (below: the copy bits)
+
 int deliver_round_send(gsim_handle* h, int64_t round)
 {
     Deliver* d = h->dl;
@@ -2962,6 +2941,10 @@ int deliver_round_send(gsim_handle* h, int64_t round)
         if (!rc) rc = launch_send_tm(h, a);
         if (rc) return rc;
         gater_round_sent(h, round);
+        if (h->sh && h->sh->push) {                    // the copies to ghost receivers, per destination
+            rc = xbits_gather(h, round);
+            if (rc) return rc;
+        }
         // the claims of round g-1 were committed before k_send_tm; round g+1's bits
         // were last read (as "previous") by round g
         d->pending = round;
@@ -2983,6 +2966,144 @@ int deliver_round_queue(gsim_handle* h, int64_t round, const uint64_t* q, const 
     hipLaunchKernelGGL(k_gossip_deliver, dim3(2048), dim3(256), lds2, h->stream, a, q, d_n,
                        (const uint32_t*)h->d_owner, cap);
     return hip_check(h, hipGetLastError(), "k_gossip_deliver");
+}
+
+// ---- copy push as bitmaps -------------------------------
+// A round's copies to ghost receivers are bits of xbits ([ring][xbw] words,
+// k_send_tm<PUSH>).  The gather lists each destination's segment of every
+// active slot (the slots k_send_tm walked: nnew_prev), slot ids first, and
+// clears it:  out[d] = [m_0 .. m_{n-1}] [n x xw_d words]; cnt[0] = n.
+__global__ __launch_bounds__(256) void k_xbits_gather(const uint32_t* nnew, int32_t ring, uint64_t* xbits, int64_t xbw,
+                                                      const int64_t* xwo, uint64_t* out, int64_t out_cap, uint32_t* cnt)
+{
+    extern __shared__ uint16_t s_act[];
+    __shared__ int s_n;
+    const int n = active_slots(nnew, ring, s_act, &s_n);
+    const int d = (int)blockIdx.y;
+    const int64_t w0 = xwo[d], xw = xwo[d + 1] - w0;
+    uint64_t* o = out + (int64_t)d * out_cap;
+    if (blockIdx.x == 0) {
+        for (int k = threadIdx.x; k < n && xw > 0; k += blockDim.x) o[k] = s_act[k];
+        if (d == 0 && threadIdx.x == 0) *cnt = (uint32_t)n;
+    }
+    const int64_t tot = (int64_t)n * xw;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < tot; x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = x / xw, w = x - k * xw;
+        uint64_t* src = xbits + (int64_t)s_act[k] * xbw + w0 + w;
+        const uint64_t v = *src;
+        o[n + x] = v;
+        if (v) *src = 0;
+    }
+}
+
+// The bits from every other shard: per source q, n slots of xw words, a bit
+// at position b of slot m's words is a copy of m on record gbase + b (the
+// ghost block of q's peers, in q's cross-out order).  A wave takes 64 words
+// of one slot and applies their copies in record order (the set bits listed
+// in LDS), so neighbouring lanes touch neighbouring records.
+constexpr int kXbList = 1024;                // per-wave LDS list of a task's copies
+
+__global__ __launch_bounds__(256) void k_xbits_deliver(RoundArgs a_, const uint64_t* in, const XSrc* src, int32_t K,
+                                                       int64_t ntask, const uint32_t* owner)
+{
+    const RoundArgs& a = a_;
+    extern __shared__ uint32_t s_new2[];
+    __shared__ uint32_t s_list[4][kXbList];
+    __shared__ unsigned long long s_stats[4];
+    for (int w = threadIdx.x; w < (a.ring + 31) / 32; w += blockDim.x) s_new2[w] = 0;
+    if (threadIdx.x < 4) s_stats[threadIdx.x] = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t par = (uint32_t)(a.g & 1);
+    const uint32_t claim_hi = kClaim | (par << 30);
+    const ctp_t tpa = const_tp(a.tp);
+    unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
+    uint32_t* lst = s_list[wid];
+    for (int64_t tk = (int64_t)blockIdx.x * 4 + wid; tk < ntask; tk += (int64_t)gridDim.x * 4) {   // wave-uniform
+        const RoundArgs& a = kernarg0(a_);
+        int q = 0;
+        while (q + 1 < K && src[q + 1].toff <= tk) ++q;
+        const XSrc sq = src[q];
+        const int64_t cpw = ((int64_t)sq.xw + 63) / 64;
+        const int64_t rel = tk - sq.toff, k = rel / cpw, c0 = (rel - k * cpw) * 64;
+        const uint32_t m = (uint32_t)in[sq.in_off + k];
+        const int64_t w = c0 + lane;
+        const uint64_t bits = w < sq.xw ? in[sq.in_off + sq.n + k * sq.xw + w] : 0ull;
+        const uint32_t cnt = (uint32_t)__popcll(bits);
+        uint32_t pre = cnt;                                   // inclusive scan over the wave
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)pre, o, 64);
+            if (lane >= o) pre += y;
+        }
+        const uint32_t total = (uint32_t)__shfl((int)pre, 63, 64);
+        if (!total) continue;
+        const int64_t rb = sq.gbase + w * 64;
+        if (total <= (uint32_t)kXbList) {
+            uint32_t pos = pre - cnt;
+            for (uint64_t b = bits; b; b &= b - 1) lst[pos++] = (uint32_t)(w * 64) + (uint32_t)__builtin_ctzll(b);
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+                if (j0 + lane < total)
+                    listed_copy(a, (uint32_t)(sq.gbase + lst[j0 + lane]), m, owner, par, claim_hi, tpa, n_acc, n_gray,
+                                n_first, s_new2);
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // lst is rewritten by the next task
+        } else {
+            for (uint64_t b = bits; b; b &= b - 1)
+                listed_copy(a, (uint32_t)(rb + __builtin_ctzll(b)), m, owner, par, claim_hi, tpa, n_acc, n_gray, n_first,
+                            s_new2);
+        }
+    }
+    n_acc = wave_sum_u64(n_acc);
+    n_gray = wave_sum_u64(n_gray);
+    n_first = wave_sum_u64(n_first);
+    if (lane == 0 && (n_acc | n_gray)) {
+        atomicAdd(&s_stats[0], n_acc);
+        atomicAdd(&s_stats[1], n_first);
+        atomicAdd(&s_stats[3], n_gray);
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < (a.ring + 31) / 32; w += blockDim.x) {
+        uint32_t bits = s_new2[w];
+        if (!bits) continue;
+        atomicOr(&a.nnew_cur[w], bits);
+        while (bits) {
+            const int q = __ffs(bits) - 1;
+            bits &= bits - 1;
+            atomicMax(&a.slot_last[w * 32 + q], (int32_t)a.g);
+        }
+    }
+    if (threadIdx.x == 0 && (s_stats[0] | s_stats[3])) {
+        atomicAdd(&a.stats[0], s_stats[0]);
+        atomicAdd(&a.stats[1], s_stats[1]);
+        atomicAdd(&a.stats[2], s_stats[0] - s_stats[1]);
+        atomicAdd(&a.stats[3], s_stats[3]);
+    }
+}
+
+// right after round g's k_send_tm, while its slots (nnew of g-1) are still set
+static int xbits_gather(gsim_handle* h, int64_t round)
+{
+    Deliver* d = h->dl;
+    ShardCtx* sh = h->sh;
+    hipLaunchKernelGGL(k_xbits_gather, dim3(64, (uint32_t)sh->K), dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t),
+                       h->stream, (const uint32_t*)(d->d_nnew + (size_t)((round + 1) & 1) * (size_t)nnew_words(d)),
+                       d->cfg.ring, sh->d_xbits, sh->xbw, (const int64_t*)sh->d_xwo, sh->d_xsend, sh->xsend_cap, sh->d_xn);
+    return hip_check(h, hipGetLastError(), "k_xbits_gather");
+}
+
+int deliver_xbits_apply(gsim_handle* h, int64_t round, const uint64_t* in, const XSrc* d_src, int K, int64_t ntask)
+{
+    if (ntask <= 0) return GSIM_OK;
+    Deliver* d = h->dl;
+    RoundArgs a = make_round_args(h, round);
+    const size_t lds2 = (size_t)nnew_words(d) * 4;
+    const uint32_t grid = (uint32_t)std::min<int64_t>((ntask + 3) / 4, 8192);
+    hipLaunchKernelGGL(k_xbits_deliver, dim3(grid), dim3(256), lds2, h->stream, a, in, d_src, (int32_t)K,
+                       ntask, (const uint32_t*)h->d_owner);
+    return hip_check(h, hipGetLastError(), "k_xbits_deliver");
 }
 
 int deliver_round_post(gsim_handle* h, int64_t round)
@@ -3409,8 +3530,9 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     d->tm_cn = -1;
     if (cfg->topic_slots > 0) {
         // claim list for member-compacted cells (list_commit): a round's first
-        // deliveries; more overflow into k_commit's word scan
-        d->clist_cap = std::max<int64_t>(2 * (int64_t)N, 1 << 20) / kClSub;
+        // deliveries; more overflow into k_commit's word scan (c5's busiest
+        // rounds overflowed 2 N: the scan ran in most rounds, 30 ms per tick)
+        d->clist_cap = std::max<int64_t>(4 * (int64_t)N, 1 << 20) / kClSub;
         A((void**)&d->d_clist, (size_t)d->clist_cap * kClSub * 8);
         A((void**)&d->d_clist_n, (kClSub + 1) * kClStride * 4);
         if (e == hipSuccess) e = hipMemsetAsync(d->d_clist_n, 0, (kClSub + 1) * kClStride * 4, h->stream);

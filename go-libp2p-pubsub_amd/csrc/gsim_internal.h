@@ -205,6 +205,16 @@ struct ShardRanges {
     int32_t K, self;
 };
 
+// One source shard's part of a round's received copy bits (k_xbits_deliver):
+// its n active slots' ids at in_off, then n x xw words; bit b of slot k is a
+// copy on record gbase + b (the ghost block of the source's peers).
+struct XSrc {
+    int64_t in_off;    // first entry of the source's part (slot ids, then words)
+    int64_t gbase;     // first record of its ghost block
+    int64_t toff;      // first wave task (64 words of one slot each)
+    int32_t n, xw;     // slots, words per slot
+};
+
 struct ShardCtx {
     int32_t k = 0, K = 1;
     int64_t own_lo = 0, own_hi = 0;        // owned local peers
@@ -255,20 +265,26 @@ struct ShardCtx {
     uint8_t* d_gsin = nullptr;             // [e]
     uint32_t* h_counts = nullptr;          // pinned scratch for count readbacks
     // copy push: a round's copies from owned senders to ghost
-    // receivers go to the receivers' shards as (receiver-shard edge | slot << 32)
+    // receivers go to the receivers' shards as bits, per (destination, slot)
+    // one bit per cross edge into the destination, in its cross-out order
     bool push = true;
     std::vector<int64_t> rbase;            // [K] first local edge of this shard's ghost block at shard d
-    uint32_t* d_xre = nullptr;             // [e] owned-row cross edge: the edge's index at the receiver's shard
+    uint32_t* d_xre = nullptr;             // [e] owned-row cross edge: the edge's index at the receiver's shard (PX)
     uint8_t* d_pshard = nullptr;           // [n] shard of each local peer
-    uint64_t* d_xsub = nullptr;            // [K][kXSub][xsub_cap] sub-lists of outbound copies
-    uint32_t* d_xcnt = nullptr;            // [K * kXSub + 1] their counts, then an overflow flag (stride kXStride)
-    int64_t xsub_cap = 0;
-    uint64_t* d_xsend = nullptr;           // [K][xsend_cap] each destination's copies, contiguous
+    std::vector<int64_t> xwo;              // [K+1] word offset of each destination's segment in a slot's row
+    int64_t* d_xwo = nullptr;              // ... on the device
+    int64_t xbw = 0;                       // words per slot row (xwo[K])
+    uint32_t* d_xwq = nullptr;             // [e] owned-row cross edge: its bit in a slot's row (64 xwo[d] + position)
+    uint64_t* d_xbits = nullptr;           // [ring][xbw] the round's copies to ghost receivers (k_send_tm<PUSH>)
+    int32_t xring = 0;                     // slots d_xbits holds
+    uint64_t* d_xsend = nullptr;           // [K][xsend_cap] per destination: the active slots, then their segments
     int64_t xsend_cap = 0;
-    uint64_t* d_xrecv = nullptr;           // copies from every other shard
+    uint64_t* d_xrecv = nullptr;           // the same from every other shard
     int64_t xrecv_cap = 0;
-    uint32_t* d_xn = nullptr;              // [1] copies received
-    uint32_t* h_xcnt = nullptr;            // pinned: count readback ([K * kXSub + 1] strided), then the received count
+    uint32_t* d_xn = nullptr;              // [1] active slots of the round (k_xbits_gather)
+    uint32_t* h_xcnt = nullptr;            // pinned: its readback
+    XSrc* d_xsrc = nullptr;                // [K] the received parts (k_xbits_deliver)
+    XSrc* h_xsrc = nullptr;                // pinned staging of it
     // peer exchange to ghosts (k_px_emit's remote path, gsim_group_px_connect)
     uint64_t* d_pxout = nullptr;           // [K][pxcap] PX list entries per destination shard
     uint32_t* d_pxcnt = nullptr;           // [K + 1] their counts, overflow
@@ -276,8 +292,6 @@ struct ShardCtx {
     uint64_t* d_pxin = nullptr;            // entries from the other shards / the job's attempts / its connections
     int64_t pxin_cap = 0;
 };
-constexpr int kXSub = 32;                  // outbound sub-lists per destination (append contention)
-constexpr int kXStride = 32;               // u32s between two sub-list counters (one cache line each)
 
 // Seen-set cells [ring][N] (deliver.hip): unseen; committed (hi = first-seen
 // round, lo = first sender); or claimed in round g (hi = kClaim | parity of g
@@ -620,6 +634,7 @@ void deliver_round_end(gsim_handle* h, int64_t round);
 int32_t* deliver_slot_last(gsim_handle* h);           // [ring]
 int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32_t* d_cnt, int64_t cap,
                             bool append = false);
+int deliver_xbits_apply(gsim_handle* h, int64_t round, const uint64_t* in, const gsim::XSrc* d_src, int K, int64_t ntask);
 int deliver_frontier_import(gsim_handle* h, int64_t round, const uint64_t* in, int64_t n);
 void deliver_blocks_changed(gsim_handle* h);          // gsim_set_kernel_variant(h, 6, v)
 // gater.hip: the peer gater (gsim_set_peer_gater)

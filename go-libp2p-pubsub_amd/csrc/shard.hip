@@ -280,22 +280,6 @@ __global__ __launch_bounds__(256) void k_xre_build(const uint32_t* xq, const uin
         xre[e] = xq[e] == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)(rb.b[pshard[col[e]]] + (int64_t)xq[e]);
 }
 
-// A round's outbound copies: each destination's kXSub sub-lists (k_send_tm
-// appends) into one contiguous list, in sub-list order.  Blocks (destination,
-// sub-list) x gridDim.y slices.
-__global__ __launch_bounds__(256) void k_xcompact(const uint64_t* xsub, const uint32_t* xcnt, int64_t sub_cap,
-                                                  uint64_t* xsend, int64_t send_cap)
-{
-    const int32_t b = (int32_t)blockIdx.x, d = b / kXSub, q = b % kXSub;
-    int64_t off = 0;
-    for (int32_t k = 0; k < q; ++k) off += std::min<int64_t>(xcnt[(d * kXSub + k) * kXStride], sub_cap);
-    const int64_t n = std::min<int64_t>(xcnt[b * kXStride], sub_cap);
-    const uint64_t* src = xsub + (int64_t)b * sub_cap;
-    uint64_t* dst = xsend + (int64_t)d * send_cap + off;
-    const int64_t stride = (int64_t)gridDim.y * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.y * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[i];
-}
-
 int grid_for(int64_t n)
 {
     int64_t g = (n + 255) / 256;
@@ -689,7 +673,9 @@ void free_shard_bufs(ShardCtx* s)
     f(s->d_fout); f(s->d_fcnt); f(s->d_fin); f(s->d_cout); f(s->d_ccnt); f(s->d_cin);
     f(s->d_rmesh_out); f(s->d_rfan_out); f(s->d_rflag_out); f(s->d_rmesh_in); f(s->d_rfan_in); f(s->d_rflag_in);
     f(s->d_gout); f(s->d_gsout); f(s->d_gin); f(s->d_gsin);
-    f(s->d_xre); f(s->d_pshard); f(s->d_xsub); f(s->d_xcnt); f(s->d_xsend); f(s->d_xrecv); f(s->d_xn);
+    f(s->d_xre); f(s->d_pshard); f(s->d_xwo); f(s->d_xwq); f(s->d_xbits); f(s->d_xsend); f(s->d_xrecv); f(s->d_xn);
+    f(s->d_xsrc);
+    if (s->h_xsrc) (void)hipHostFree(s->h_xsrc);
     f(s->d_pxout); f(s->d_pxcnt); f(s->d_pxin);
     if (s->h_counts) (void)hipHostFree(s->h_counts);
     if (s->h_xcnt) (void)hipHostFree(s->h_xcnt);
@@ -1125,45 +1111,39 @@ int exchange_frontier(gsim_group* g, int64_t round, bool flush)
 }
 
 // Copy push: round `round`'s copies from owned senders to
-// ghost receivers, appended by k_send_tm<PUSH>, go to the receivers' shards,
-// whose k_gossip_deliver applies them (AcceptFrom, the claim of the cell,
-// the records) with the round's local copies, before the commit.
+// ghost receivers, bits of (slot, cross edge) set by k_send_tm<PUSH> and
+// gathered per destination (the round's active slots, then their segments:
+// k_xbits_gather, right after the send), go to the receivers' shards, whose
+// k_xbits_deliver applies them (AcceptFrom, the claim of the cell, the
+// records) with the round's local copies, before the commit.
 int exchange_copies(gsim_group* g, int64_t round)
 {
     const size_t L = g->hs.size();
     const int K = g->K;
-    const int nc = K * kXSub;
     for (size_t l = 0; l < L; ++l) {
         gsim_handle* h = g->hs[l];
         ShardCtx* s = h->sh;
         (void)hipSetDevice(h->device);
-        ProfScope ps(h, GSIM_K_SEND);
-        hipLaunchKernelGGL(k_xcompact, dim3((uint32_t)nc, 16), dim3(256), 0, h->stream, (const uint64_t*)s->d_xsub,
-                           (const uint32_t*)s->d_xcnt, s->xsub_cap, s->d_xsend, s->xsend_cap);
-        hipError_t e = hipGetLastError();
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(s->h_xcnt, s->d_xcnt, sizeof(uint32_t) * (size_t)(nc + 1) * kXStride,
-                               hipMemcpyDeviceToHost, h->stream);
-        if (e == hipSuccess)
-            e = hipMemsetAsync(s->d_xcnt, 0, sizeof(uint32_t) * (size_t)(nc + 1) * kXStride, h->stream);
-        if (e != hipSuccess) return g->fail(GSIM_EDEVICE, "copy list compaction");
+        if (hipMemcpyAsync(s->h_xcnt, s->d_xn, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "copy bits: slot count");
     }
     int rc = sync_all(g);
     if (rc) return rc;
     std::vector<std::vector<uint64_t>> scnt(L, std::vector<uint64_t>((size_t)K, 0)), rcnt;
     for (size_t l = 0; l < L; ++l) {
         const ShardCtx* s = g->hs[l]->sh;
-        if (s->h_xcnt[(size_t)nc * kXStride])
-            return g->fail(GSIM_ERANGE, "cross-shard copy list overflow (a round's copies over a sub-list's capacity)");
-        for (int d = 0; d < K; ++d)
-            for (int q = 0; q < kXSub; ++q) scnt[l][(size_t)d] += s->h_xcnt[(size_t)(d * kXSub + q) * kXStride];
+        const uint64_t n = s->h_xcnt[0];
+        for (int d = 0; d < K; ++d) {
+            const int64_t xw = s->xwo[(size_t)d + 1] - s->xwo[(size_t)d];
+            scnt[l][(size_t)d] = (d == g->ids[l] || xw == 0) ? 0 : n * (uint64_t)(1 + xw);
+        }
     }
     rc = tagged_counts(g, XK_COPIES, scnt, rcnt);
     if (rc) return rc;
     std::vector<std::vector<const void*>> sp(L, std::vector<const void*>((size_t)K, nullptr));
     std::vector<std::vector<void*>> rp(L, std::vector<void*>((size_t)K, nullptr));
     std::vector<std::vector<uint64_t>> sb(L, std::vector<uint64_t>((size_t)K, 0)), rb = sb;
-    std::vector<int64_t> total(L, 0);
+    std::vector<int64_t> total(L, 0), ntask(L, 0);
     for (size_t l = 0; l < L; ++l) {
         gsim_handle* h = g->hs[l];
         ShardCtx* s = h->sh;
@@ -1177,7 +1157,23 @@ int exchange_copies(gsim_group* g, int64_t round)
             sb[l][(size_t)q] = scnt[l][(size_t)q] * 8;
             rp[l][(size_t)q] = s->d_xrecv + off;
             rb[l][(size_t)q] = rcnt[l][(size_t)q] * 8;
-            off += (int64_t)rcnt[l][(size_t)q];
+            // source q's part: its slots' ids, then xw words each (xw from the
+            // ghost block of its peers, which is its cross-out list into here)
+            const int64_t xw = (s->gcnt[(size_t)q] + 63) / 64;
+            const int64_t c = (int64_t)rcnt[l][(size_t)q];
+            XSrc& x = s->h_xsrc[q];
+            x.in_off = off;
+            x.gbase = s->gbase[(size_t)q];
+            x.xw = (int32_t)xw;
+            x.n = 0;
+            if (c) {
+                if (xw == 0 || c % (1 + xw)) return g->fail(GSIM_ESTATE, "copy bits from shard " + std::to_string(q) +
+                                                                        " do not match its ghost block");
+                x.n = (int32_t)(c / (1 + xw));
+            }
+            x.toff = ntask[l];
+            ntask[l] += (int64_t)x.n * ((xw + 63) / 64);
+            off += c;
         }
     }
     rc = g->take_tr(g->tr->alltoallv(sp, sb, rp, rb));
@@ -1185,14 +1181,12 @@ int exchange_copies(gsim_group* g, int64_t round)
     for (size_t l = 0; l < L; ++l) {
         gsim_handle* h = g->hs[l];
         ShardCtx* s = h->sh;
-        if (total[l] <= 0) continue;
+        if (ntask[l] <= 0) continue;
         (void)hipSetDevice(h->device);
         ProfScope ps(h, GSIM_K_SEND);
-        uint32_t* hn = s->h_xcnt + (size_t)(nc + 1) * kXStride;
-        *hn = (uint32_t)total[l];
-        if (hipMemcpyAsync(s->d_xn, hn, sizeof(uint32_t), hipMemcpyHostToDevice, h->stream) != hipSuccess)
-            return g->fail(GSIM_EDEVICE, "received copy count");
-        rc = g->take(h, deliver_round_queue(h, round, s->d_xrecv, s->d_xn, total[l]));
+        if (hipMemcpyAsync(s->d_xsrc, s->h_xsrc, sizeof(XSrc) * (size_t)K, hipMemcpyHostToDevice, h->stream) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "copy bits: source table");
+        rc = g->take(h, deliver_xbits_apply(h, round, s->d_xrecv, s->d_xsrc, K, ntask[l]));
         if (rc) return rc;
         g->settle(h);
     }
@@ -1452,6 +1446,24 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
             return g->take(h, rc);
         if (hipMemcpy(s->d_pshard, psh.data(), psh.size(), hipMemcpyHostToDevice) != hipSuccess)
             return g->fail(GSIM_EDEVICE, "shard tables upload");
+        // copy bits: per destination a word-aligned segment of a slot's row, a
+        // cross edge's bit at its position in the cross-out list
+        s->xwo.assign((size_t)K + 1, 0);
+        for (int q = 0; q < K; ++q)
+            s->xwo[(size_t)q + 1] = s->xwo[(size_t)q] + ((int64_t)L.crossout[(size_t)q].size() + 63) / 64;
+        s->xbw = s->xwo[(size_t)K];
+        if (s->xbw * 64 >= (int64_t)0xFFFFFFFFll) return g->fail(GSIM_ERANGE, "too many cross edges for the copy bits");
+        {
+            std::vector<uint32_t> xwq((size_t)L.e_loc, 0xFFFFFFFFu);
+            for (int q = 0; q < K; ++q)
+                for (size_t x = 0; x < L.crossout[(size_t)q].size(); ++x)
+                    xwq[L.crossout[(size_t)q][x]] = (uint32_t)(s->xwo[(size_t)q] * 64 + (int64_t)x);
+            if ((rc = dalloc(h, &s->d_xwq, xwq.size())) || (rc = dalloc(h, &s->d_xwo, s->xwo.size())))
+                return g->take(h, rc);
+            if (hipMemcpy(s->d_xwq, xwq.data(), xwq.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(s->d_xwo, s->xwo.data(), s->xwo.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+                return g->fail(GSIM_EDEVICE, "shard tables upload");
+        }
         g->gid[l] = L.gid;
         g->gidx[l] = L.gidx;
     }
@@ -1542,23 +1554,25 @@ int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg)
             A(&s->d_gin, (size_t)h->e);
             A(&s->d_gsin, (size_t)h->e);
         }
-        if (!rc && s->push && !s->d_xsub) {
-            // a round's copies to each other shard: sub-lists of half the cross
-            // edges into it each (32 x 1/2 = 16 copies per cross edge in all,
-            // several times a C3 round's; an overflow fails the round)
-            int64_t xmax = 0;
-            for (int q = 0; q < K; ++q) xmax = std::max<int64_t>(xmax, s->xoff[(size_t)q + 1] - s->xoff[(size_t)q]);
-            s->xsub_cap = std::max<int64_t>(xmax / 2, 1 << 12);
-            s->xsend_cap = kXSub * s->xsub_cap;
-            const size_t nct = (size_t)(K * kXSub + 2) * kXStride;
-            A(&s->d_xsub, (size_t)(K * s->xsend_cap));
+        if (!rc && s->push && s->xring != cfg->ring) {
+            // a round's copies to ghost receivers: a bit per (slot, cross edge);
+            // per destination the active slots' ids and segments go out
+            if (s->d_xbits) { (void)hipFree(s->d_xbits); s->d_xbits = nullptr; }
+            if (s->d_xsend) { (void)hipFree(s->d_xsend); s->d_xsend = nullptr; }
+            int64_t xwmax = 0;
+            for (int q = 0; q < K; ++q) xwmax = std::max<int64_t>(xwmax, s->xwo[(size_t)q + 1] - s->xwo[(size_t)q]);
+            s->xsend_cap = (int64_t)cfg->ring * (1 + xwmax);
+            A(&s->d_xbits, (size_t)((int64_t)cfg->ring * s->xbw));
             A(&s->d_xsend, (size_t)(K * s->xsend_cap));
-            A(&s->d_xcnt, nct);
-            A(&s->d_xn, 1);
-            if (!rc && hipHostMalloc((void**)&s->h_xcnt, sizeof(uint32_t) * nct, 0) != hipSuccess)
+            if (!s->d_xn) A(&s->d_xn, 1);
+            if (!s->d_xsrc) A(&s->d_xsrc, (size_t)K);
+            if (!rc && !s->h_xcnt && hipHostMalloc((void**)&s->h_xcnt, sizeof(uint32_t) * 2, 0) != hipSuccess)
                 return g->fail(GSIM_ENOMEM, "pinned scratch");
-            if (!rc && hipMemset(s->d_xcnt, 0, sizeof(uint32_t) * nct) != hipSuccess)
-                return g->fail(GSIM_EDEVICE, "copy list counts");
+            if (!rc && !s->h_xsrc && hipHostMalloc((void**)&s->h_xsrc, sizeof(XSrc) * (size_t)K, 0) != hipSuccess)
+                return g->fail(GSIM_ENOMEM, "pinned scratch");
+            if (!rc && hipMemset(s->d_xbits, 0, sizeof(uint64_t) * (size_t)((int64_t)cfg->ring * s->xbw)) != hipSuccess)
+                return g->fail(GSIM_EDEVICE, "copy bits");
+            if (!rc) s->xring = cfg->ring;
         }
         if (rc) return g->take(h, rc);
         if (hipMemset(s->d_gin, 0, (size_t)h->e * 8) != hipSuccess || hipMemset(s->d_gsin, 0, (size_t)h->e) != hipSuccess)

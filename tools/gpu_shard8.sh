@@ -12,7 +12,7 @@ OUT="$ROOT/gpurun_out/$TAG"
 mkdir -p "$OUT"
 cd "$ROOT"
 export GSIM_GROUP_SERIAL=1
-timeout -k 10 500 python -u bench.py --steps "${STEPS:-5}" --warmup 2 --no-cpu-baseline --shards "$S" \
+timeout -k 10 500 python -u bench.py --steps "${STEPS:-5}" --warmup 2 --no-cpu-baseline --shards "$S" ${BENCH_ARGS:-} \
   > "$OUT/bench_s$S.json" 2> "$OUT/bench_s$S.err" || { echo "bench rc=$?"; tail -20 "$OUT/bench_s$S.err"; exit 1; }
 python3 - "$OUT/bench_s$S.json" <<'PY'
 import json, sys
@@ -26,6 +26,6 @@ PY
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o s \
-  -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --shards "$S" > "$OUT/prof.json" 2> "$OUT/prof.err" \
+  -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --shards "$S" ${BENCH_ARGS:-} > "$OUT/prof.json" 2> "$OUT/prof.err" \
   || { echo "prof rc=$?"; tail -20 "$OUT/prof.err"; exit 1; }
 python3 "$ROOT/tools/trace_summary.py" "$OUT/prof/s_kernel_trace.csv" "$S" > "$OUT/prof_summary.txt"; head -30 "$OUT/prof_summary.txt"
