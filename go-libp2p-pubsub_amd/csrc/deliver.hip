@@ -3272,6 +3272,141 @@ __global__ __launch_bounds__(256) void k_frontier_import(RoundArgs a, const uint
     }
 }
 
+// Push: a ghost's cell is read by IHAVE only, against the
+// gossip window's tick-aligned bounds, so the holders go out once per tick as
+// bits.  Each round ORs its forwarders (fresh bits of the round's slots) into
+// the bitmap of the tick of their first-seen round (a publication's origin
+// belongs to the round's own tick, every other forwarder to the round
+// before's), over global words of the owned range.
+__global__ __launch_bounds__(256) void k_holder_accum(RoundArgs a, uint64_t* hb, uint32_t* hs, int64_t how, int64_t gw0,
+                                                      int64_t glo, int64_t ghi)
+{
+    extern __shared__ uint16_t s_act[];
+    __shared__ int s_n;
+    const int nact = active_slots(a.nnew_prev, a.ring, s_act, &s_n);
+    const int64_t items = (int64_t)nact * how;
+    const int64_t hw = (int64_t)((a.ring + 31) / 32);
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < items; x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = x / how, w = x - k * how;
+        const uint32_t m = s_act[k];
+        const int64_t gp0 = (gw0 + w) * 64;                // global peer of bit 0
+        const int64_t lb = (int64_t)a.rlo + (gp0 - glo);    // its local bit (glo: a multiple of 64)
+        const uint64_t* f = a.fresh + (int64_t)m * a.nw;
+        uint64_t bits = 0;
+        if (lb >= 0) {
+            const int64_t lw = lb >> 6;
+            const int sh = (int)(lb & 63);
+            bits = f[lw] >> sh;
+            if (sh && lw + 1 < a.nw) bits |= f[lw + 1] << (64 - sh);
+        }
+        if (gp0 + 64 > ghi) bits &= ghi - gp0 >= 64 ? ~0ull : ((1ull << (ghi - gp0)) - 1ull);   // owned peers only
+        if (!bits) continue;
+        uint64_t mp[2] = {0, 0};
+        const int32_t t = (int32_t)a.mtopic[m];
+        for (uint64_t b = bits; b; b &= b - 1) {
+            const int q = __builtin_ctzll(b);
+            const uint64_t c = a.cs.get(m, t, (uint32_t)(lb + q));
+            const int64_t fr = (int64_t)((c >> 32) & kG24);
+            mp[(fr / a.R) & 1] |= 1ull << q;
+        }
+        for (int p = 0; p < 2; ++p) {
+            if (!mp[p]) continue;
+            hb[((int64_t)p * a.ring + m) * how + w] |= mp[p];
+            atomicOr(&hs[p * hw + (m >> 5)], 1u << (m & 31));
+        }
+    }
+}
+
+// The tick's holder bits (parity p): the slots touched, then their words,
+// cleared as they are read; *cnt = the slots.
+__global__ __launch_bounds__(256) void k_holder_gather(uint64_t* hb, const uint32_t* hs, int32_t ring, int64_t how,
+                                                       uint64_t* out, uint32_t* cnt)
+{
+    extern __shared__ uint16_t s_act[];
+    __shared__ int s_n;
+    const int n = active_slots(hs, ring, s_act, &s_n);
+    if (blockIdx.x == 0) {
+        for (int k = threadIdx.x; k < n; k += blockDim.x) out[k] = s_act[k];
+        if (threadIdx.x == 0) *cnt = (uint32_t)n;
+    }
+    const int64_t tot = (int64_t)n * how;
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < tot; x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = x / how, w = x - k * how;
+        uint64_t* src = hb + (int64_t)s_act[k] * how + w;
+        const uint64_t v = *src;
+        out[n + x] = v;
+        if (v) *src = 0;
+    }
+}
+
+// Every other shard's holders of tick k: each set bit that is a ghost here
+// gets its cell (first-seen round fr, the tick's first; no local sender) and
+// the slot's activity.  A wave takes 64 words of one (source, slot).
+__global__ __launch_bounds__(256) void k_holder_import(RoundArgs a, const uint32_t* g2l, const uint64_t* in,
+                                                       const HSrc* src, int32_t K, int64_t ntask, int64_t fr)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int64_t tk = (int64_t)blockIdx.x * 4 + wid; tk < ntask; tk += (int64_t)gridDim.x * 4) {   // wave-uniform
+        int q = 0;
+        while (q + 1 < K && src[q + 1].toff <= tk) ++q;
+        const HSrc sq = src[q];
+        const int64_t cpw = ((int64_t)sq.nw + 63) / 64;
+        const int64_t rel = tk - sq.toff, k = rel / cpw, w = (rel - k * cpw) * 64 + lane;
+        const uint32_t m = (uint32_t)in[sq.in_off + k];
+        const int32_t t = (int32_t)a.mtopic[m];
+        const uint64_t bits = w < sq.nw ? in[sq.in_off + sq.n + k * sq.nw + w] : 0ull;
+        for (uint64_t b = bits; b; b &= b - 1) {
+            const uint32_t l = g2l[sq.pbase + w * 64 + __builtin_ctzll(b)];
+            if (l == 0xFFFFFFFFu || (l >= a.rlo && l < a.rhi)) continue;      // not a ghost of this shard
+            const int64_t ci = a.cs.idx(m, t, l);                              // a forwarder holds the topic
+            if (ci >= 0) a.cs.cell[ci] = ((uint64_t)fr << 32) | kPeerMask;
+        }
+        if (__ballot(bits != 0) && lane == 0 &&
+            __hip_atomic_load(&a.slot_last[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int32_t)fr)
+            atomicMax(&a.slot_last[m], (int32_t)fr);
+    }
+}
+
+int deliver_holder_accum(gsim_handle* h, int64_t round)
+{
+    if (round == 0) return GSIM_OK;
+    Deliver* d = h->dl;
+    ShardCtx* sh = h->sh;
+    RoundArgs a = make_round_args(h, round);
+    const int64_t gw0 = sh->bounds[(size_t)sh->k] >> 6;
+    const int64_t items = sh->how * (int64_t)d->cfg.ring;   // an upper bound: the active slots are on the device
+    hipLaunchKernelGGL(k_holder_accum, dim3((uint32_t)std::max<int64_t>(1, std::min<int64_t>((items + 255) / 256, 2048))),
+                       dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a, sh->d_hbits, sh->d_hslots,
+                       sh->how, gw0, (int64_t)sh->bounds[(size_t)sh->k], (int64_t)sh->bounds[(size_t)sh->k + 1]);
+    return hip_check(h, hipGetLastError(), "k_holder_accum");
+}
+
+int deliver_holder_gather(gsim_handle* h, int parity)
+{
+    Deliver* d = h->dl;
+    ShardCtx* sh = h->sh;
+    const int64_t hw = (d->cfg.ring + 31) / 32;
+    hipLaunchKernelGGL(k_holder_gather, dim3(256), dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream,
+                       sh->d_hbits + (size_t)parity * (size_t)d->cfg.ring * (size_t)sh->how,
+                       (const uint32_t*)(sh->d_hslots + (size_t)parity * (size_t)hw), d->cfg.ring, sh->how, sh->d_hsend,
+                       sh->d_hn);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess)
+        e = hipMemsetAsync(sh->d_hslots + (size_t)parity * (size_t)hw, 0, (size_t)hw * 4, h->stream);
+    return hip_check(h, e, "k_holder_gather");
+}
+
+int deliver_holder_import(gsim_handle* h, int64_t round, const uint64_t* in, const HSrc* d_src, int K, int64_t ntask,
+                          int64_t fr)
+{
+    if (ntask <= 0) return GSIM_OK;
+    RoundArgs a = make_round_args(h, round);
+    const uint32_t grid = (uint32_t)std::min<int64_t>((ntask + 3) / 4, 8192);
+    hipLaunchKernelGGL(k_holder_import, dim3(grid), dim3(256), 0, h->stream, a, (const uint32_t*)h->sh->d_g2l, in, d_src,
+                       (int32_t)K, ntask, fr);
+    return hip_check(h, hipGetLastError(), "k_holder_import");
+}
+
 int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32_t* d_cnt, int64_t cap, bool append)
 {
     Deliver* d = h->dl;

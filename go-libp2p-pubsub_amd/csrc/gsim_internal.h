@@ -205,6 +205,14 @@ struct ShardRanges {
     int32_t K, self;
 };
 
+// One source shard's part of a tick's received holder bits (k_holder_import):
+// n slots' ids at in_off, then n x nw words over its owned peers; bit b of
+// word w of a slot is global peer pbase + 64 w + b.
+struct HSrc {
+    int64_t in_off, pbase, toff;
+    int32_t n, nw;
+};
+
 // One source shard's part of a round's received copy bits (k_xbits_deliver):
 // its n active slots' ids at in_off, then n x xw words; bit b of slot k is a
 // copy on record gbase + b (the ghost block of the source's peers).
@@ -247,6 +255,17 @@ struct ShardCtx {
     int64_t fpend = 0;                     // push: entries accumulated since the last flush (one per tick)
     uint64_t* d_fin = nullptr;             // every other shard's forwarders
     int64_t fin_cap = 0;
+    // push: the holders of a tick as bits (a ghost's cell is read by IHAVE
+    // only, at tick granularity): [2][ring][how] by the tick's parity, over
+    // the owned peers' global words; the slots touched [2][ring/32]
+    uint64_t* d_hbits = nullptr;
+    uint32_t* d_hslots = nullptr;
+    int64_t how = 0;                       // owned global words
+    int32_t hring = 0;
+    uint64_t* d_hsend = nullptr;           // [ring * (1 + how)] the tick's slots, then their words
+    uint32_t* d_hn = nullptr;              // [1] its slots
+    HSrc* d_hsrc = nullptr;                // [K] the received parts
+    HSrc* h_hsrc = nullptr;                // pinned staging of it
     // control exchange
     uint64_t* d_cout = nullptr;            // [K][ccap] outbound control entries: edge | topic << 32 | bits << 40
     uint32_t* d_ccnt = nullptr;            // [K]
@@ -635,6 +654,10 @@ int32_t* deliver_slot_last(gsim_handle* h);           // [ring]
 int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32_t* d_cnt, int64_t cap,
                             bool append = false);
 int deliver_xbits_apply(gsim_handle* h, int64_t round, const uint64_t* in, const gsim::XSrc* d_src, int K, int64_t ntask);
+int deliver_holder_accum(gsim_handle* h, int64_t round);
+int deliver_holder_gather(gsim_handle* h, int parity);
+int deliver_holder_import(gsim_handle* h, int64_t round, const uint64_t* in, const gsim::HSrc* d_src, int K,
+                          int64_t ntask, int64_t fr);
 int deliver_frontier_import(gsim_handle* h, int64_t round, const uint64_t* in, int64_t n);
 void deliver_blocks_changed(gsim_handle* h);          // gsim_set_kernel_variant(h, 6, v)
 // gater.hip: the peer gater (gsim_set_peer_gater)

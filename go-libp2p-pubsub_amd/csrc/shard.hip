@@ -674,8 +674,9 @@ void free_shard_bufs(ShardCtx* s)
     f(s->d_rmesh_out); f(s->d_rfan_out); f(s->d_rflag_out); f(s->d_rmesh_in); f(s->d_rfan_in); f(s->d_rflag_in);
     f(s->d_gout); f(s->d_gsout); f(s->d_gin); f(s->d_gsin);
     f(s->d_xre); f(s->d_pshard); f(s->d_xwo); f(s->d_xwq); f(s->d_xbits); f(s->d_xsend); f(s->d_xrecv); f(s->d_xn);
-    f(s->d_xsrc);
+    f(s->d_xsrc); f(s->d_hbits); f(s->d_hslots); f(s->d_hsend); f(s->d_hn); f(s->d_hsrc);
     if (s->h_xsrc) (void)hipHostFree(s->h_xsrc);
+    if (s->h_hsrc) (void)hipHostFree(s->h_hsrc);
     f(s->d_pxout); f(s->d_pxcnt); f(s->d_pxin);
     if (s->h_counts) (void)hipHostFree(s->h_counts);
     if (s->h_xcnt) (void)hipHostFree(s->h_xcnt);
@@ -1027,11 +1028,103 @@ int exchange_router_delta(gsim_group* g)
 // Push: only IHAVE reads a ghost's holder round, and the entries carry it, so
 // the rounds' exports accumulate and go out once per tick (flush: the round
 // whose IHAVE follows), one exchange instead of one per round.
+// Push: the tick's holders as bits (deliver_holder_*): every round ORs its
+// forwarders into the bits of their first-seen tick; the flush (the first
+// round of tick k+1, before its IHAVE) sends tick k's to every shard the
+// owned peers have connections into, whose ghosts among them get cells with
+// first-seen round kR.  No host synchronisation but the flush's count.
+static int exchange_holders(gsim_group* g, int64_t round, bool flush)
+{
+    const size_t L = g->hs.size();
+    const int K = g->K;
+    for (gsim_handle* h : g->hs) {
+        (void)hipSetDevice(h->device);
+        ProfScope ps(h, GSIM_K_SEND);
+        int rc = g->take(h, deliver_holder_accum(h, round));
+        if (rc) return rc;
+    }
+    const int64_t R = g->rounds;
+    if (!flush || round < R) return GSIM_OK;
+    const int64_t tk = round / R - 1;                      // the tick whose holders go out
+    for (gsim_handle* h : g->hs) {
+        ShardCtx* s = h->sh;
+        (void)hipSetDevice(h->device);
+        ProfScope ps(h, GSIM_K_SEND);
+        int rc = g->take(h, deliver_holder_gather(h, (int)(tk & 1)));
+        if (!rc && hipMemcpyAsync(s->h_counts, s->d_hn, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+            rc = g->fail(GSIM_EDEVICE, "holder bits: slot count");
+        if (rc) return rc;
+    }
+    int rc = sync_all(g);
+    if (rc) return rc;
+    std::vector<std::vector<uint64_t>> scnt(L, std::vector<uint64_t>((size_t)K, 0)), rcnt;
+    for (size_t l = 0; l < L; ++l) {
+        const ShardCtx* s = g->hs[l]->sh;
+        const uint64_t n = s->h_counts[0];
+        for (int d = 0; d < K; ++d)
+            scnt[l][(size_t)d] = (d == g->ids[l] || !s->xto[(size_t)d] || !n) ? 0 : n * (uint64_t)(1 + s->how);
+    }
+    rc = tagged_counts(g, XK_FRONTIER, scnt, rcnt);
+    if (rc) return rc;
+    std::vector<std::vector<const void*>> sp(L, std::vector<const void*>((size_t)K, nullptr));
+    std::vector<std::vector<void*>> rp(L, std::vector<void*>((size_t)K, nullptr));
+    std::vector<std::vector<uint64_t>> sb(L, std::vector<uint64_t>((size_t)K, 0)), rb = sb;
+    std::vector<int64_t> ntask(L, 0);
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        int64_t total = 0;
+        for (int q = 0; q < K; ++q) total += (int64_t)rcnt[l][(size_t)q];
+        (void)hipSetDevice(h->device);
+        rc = g->take(h, ensure(h, &s->d_fin, &s->fin_cap, total));
+        if (rc) return rc;
+        int64_t off = 0;
+        for (int q = 0; q < K; ++q) {
+            sp[l][(size_t)q] = s->d_hsend;
+            sb[l][(size_t)q] = scnt[l][(size_t)q] * 8;
+            rp[l][(size_t)q] = s->d_fin + off;
+            rb[l][(size_t)q] = rcnt[l][(size_t)q] * 8;
+            // source q's part: its touched slots, then its owned global words each
+            const int64_t glo = g->bounds[(size_t)q], ghi = g->bounds[(size_t)q + 1];
+            const int64_t nw = ghi > glo ? ((ghi + 63) >> 6) - (glo >> 6) : 0;
+            const int64_t c = (int64_t)rcnt[l][(size_t)q];
+            HSrc& x = s->h_hsrc[q];
+            x.in_off = off;
+            x.pbase = (glo >> 6) * 64;
+            x.nw = (int32_t)nw;
+            x.n = 0;
+            if (c) {
+                if (nw == 0 || c % (1 + nw))
+                    return g->fail(GSIM_ESTATE, "holder bits from shard " + std::to_string(q) + " do not match its range");
+                x.n = (int32_t)(c / (1 + nw));
+            }
+            x.toff = ntask[l];
+            ntask[l] += (int64_t)x.n * ((nw + 63) / 64);
+            off += c;
+        }
+    }
+    rc = g->take_tr(g->tr->alltoallv(sp, sb, rp, rb));
+    if (rc) return rc;
+    for (size_t l = 0; l < L; ++l) {
+        gsim_handle* h = g->hs[l];
+        ShardCtx* s = h->sh;
+        if (ntask[l] <= 0) continue;
+        (void)hipSetDevice(h->device);
+        ProfScope ps(h, GSIM_K_SEND);
+        if (hipMemcpyAsync(s->d_hsrc, s->h_hsrc, sizeof(HSrc) * (size_t)K, hipMemcpyHostToDevice, h->stream) != hipSuccess)
+            return g->fail(GSIM_EDEVICE, "holder bits: source table");
+        rc = g->take(h, deliver_holder_import(h, round, s->d_fin, s->d_hsrc, K, ntask[l], tk * R));
+        if (rc) return rc;
+    }
+    return GSIM_OK;
+}
+
 int exchange_frontier(gsim_group* g, int64_t round, bool flush)
 {
     const size_t L = g->hs.size();
     const int K = g->K;
     const bool push = L > 0 && g->hs[0]->sh->push;
+    if (push) return exchange_holders(g, round, flush);
     std::vector<std::vector<uint64_t>> scnt(L, std::vector<uint64_t>((size_t)K, 0)), rcnt;
     for (size_t l = 0; l < L; ++l) {
         gsim_handle* h = g->hs[l];
@@ -1553,6 +1646,30 @@ int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg)
             A(&s->d_gsout, (size_t)ncross);
             A(&s->d_gin, (size_t)h->e);
             A(&s->d_gsin, (size_t)h->e);
+        }
+        if (!rc && s->push && s->hring != cfg->ring) {
+            // a tick's holders as bits over the owned peers' global words
+            for (auto* p : {(void*)s->d_hbits, (void*)s->d_hsend}) if (p) (void)hipFree(p);
+            s->d_hbits = nullptr; s->d_hsend = nullptr;
+            const int64_t glo = s->bounds[(size_t)s->k], ghi = s->bounds[(size_t)s->k + 1];
+            s->how = ghi > glo ? ((ghi + 63) >> 6) - (glo >> 6) : 0;
+            const size_t hw = (size_t)(cfg->ring + 31) / 32;
+            A(&s->d_hbits, (size_t)(2 * (int64_t)cfg->ring * s->how));
+            A(&s->d_hsend, (size_t)((int64_t)cfg->ring * (1 + s->how)));
+            if (!s->d_hslots) A(&s->d_hslots, 2 * hw);
+            if (!s->d_hn) A(&s->d_hn, 1);
+            if (!s->d_hsrc) A(&s->d_hsrc, (size_t)K);
+            if (!rc && !s->h_hsrc && hipHostMalloc((void**)&s->h_hsrc, sizeof(HSrc) * (size_t)K, 0) != hipSuccess)
+                return g->fail(GSIM_ENOMEM, "pinned scratch");
+            if (!rc && (hipMemset(s->d_hbits, 0, sizeof(uint64_t) * (size_t)(2 * (int64_t)cfg->ring * s->how)) != hipSuccess ||
+                        hipMemset(s->d_hslots, 0, sizeof(uint32_t) * 2 * hw) != hipSuccess))
+                return g->fail(GSIM_EDEVICE, "holder bits");
+            if (!rc) s->hring = cfg->ring;
+        } else if (!rc && s->push) {   // a new message configuration: no holders pending
+            const size_t hw = (size_t)(cfg->ring + 31) / 32;
+            if (hipMemset(s->d_hbits, 0, sizeof(uint64_t) * (size_t)(2 * (int64_t)cfg->ring * s->how)) != hipSuccess ||
+                hipMemset(s->d_hslots, 0, sizeof(uint32_t) * 2 * hw) != hipSuccess)
+                return g->fail(GSIM_EDEVICE, "holder bits");
         }
         if (!rc && s->push && s->xring != cfg->ring) {
             // a round's copies to ghost receivers: a bit per (slot, cross edge);
