@@ -395,8 +395,7 @@ __device__ __forceinline__ void clist_push_wave(const RoundArgs& a, bool on, uin
     const uint64_t b = __ballot(on);
     if (!b) return;
     const int lane = threadIdx.x & 63, leader = __builtin_ctzll(b);
-    // sub-list by wave: a popular topic's few blocks spread over all of them
-    const uint32_t q = (blockIdx.x * 16u + (threadIdx.x >> 6)) % kClSub;
+    const uint32_t q = blockIdx.x % kClSub;
     uint32_t base = 0;
     if (lane == leader) base = atomicAdd(&a.clist_n[q * kClStride], (uint32_t)__popcll(b));
     base = (uint32_t)__shfl((int)base, leader, 64);
@@ -3283,9 +3282,11 @@ __global__ __launch_bounds__(256) void k_holder_accum(RoundArgs a, uint64_t* hb,
 {
     extern __shared__ uint16_t s_act[];
     __shared__ int s_n;
+    const int64_t hw = (int64_t)((a.ring + 31) / 32);
+    uint32_t* s_hs = reinterpret_cast<uint32_t*>(s_act + ((a.ring + 1) & ~1));   // [2][hw] the slots touched
+    for (int64_t w = threadIdx.x; w < 2 * hw; w += blockDim.x) s_hs[w] = 0;
     const int nact = active_slots(a.nnew_prev, a.ring, s_act, &s_n);
     const int64_t items = (int64_t)nact * how;
-    const int64_t hw = (int64_t)((a.ring + 31) / 32);
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < items; x += (int64_t)gridDim.x * blockDim.x) {
         const int64_t k = x / how, w = x - k * how;
         const uint32_t m = s_act[k];
@@ -3301,20 +3302,31 @@ __global__ __launch_bounds__(256) void k_holder_accum(RoundArgs a, uint64_t* hb,
         }
         if (gp0 + 64 > ghi) bits &= ghi - gp0 >= 64 ? ~0ull : ((1ull << (ghi - gp0)) - 1ull);   // owned peers only
         if (!bits) continue;
+        // forwarders of round g first saw the message in round g-1, or in g (a
+        // publication's origin): only the first round of a tick tells them apart
+        // (with validation latencies the cells say: a completion round)
         uint64_t mp[2] = {0, 0};
-        const int32_t t = (int32_t)a.mtopic[m];
-        for (uint64_t b = bits; b; b &= b - 1) {
-            const int q = __builtin_ctzll(b);
-            const uint64_t c = a.cs.get(m, t, (uint32_t)(lb + q));
-            const int64_t fr = (int64_t)((c >> 32) & kG24);
-            mp[(fr / a.R) & 1] |= 1ull << q;
+        const int pg = (int)((a.g / a.R) & 1);
+        if (a.g % a.R != 0 && !a.mlat) {
+            mp[pg] = bits;
+        } else {
+            const int32_t t = (int32_t)a.mtopic[m];
+            for (uint64_t b = bits; b; b &= b - 1) {
+                const int q = __builtin_ctzll(b);
+                const uint64_t c = a.cs.get(m, t, (uint32_t)(lb + q));
+                const int64_t fr = (int64_t)((c >> 32) & kG24);
+                mp[(fr / a.R) & 1] |= 1ull << q;
+            }
         }
         for (int p = 0; p < 2; ++p) {
             if (!mp[p]) continue;
             hb[((int64_t)p * a.ring + m) * how + w] |= mp[p];
-            atomicOr(&hs[p * hw + (m >> 5)], 1u << (m & 31));
+            atomicOr(&s_hs[p * hw + (m >> 5)], 1u << (m & 31));   // (one global atomic per block and word, below)
         }
     }
+    __syncthreads();
+    for (int64_t w = threadIdx.x; w < 2 * hw; w += blockDim.x)
+        if (s_hs[w]) atomicOr(&hs[w], s_hs[w]);
 }
 
 // The tick's holder bits (parity p): the slots touched, then their words,
@@ -3375,8 +3387,9 @@ int deliver_holder_accum(gsim_handle* h, int64_t round)
     RoundArgs a = make_round_args(h, round);
     const int64_t gw0 = sh->bounds[(size_t)sh->k] >> 6;
     const int64_t items = sh->how * (int64_t)d->cfg.ring;   // an upper bound: the active slots are on the device
-    hipLaunchKernelGGL(k_holder_accum, dim3((uint32_t)std::max<int64_t>(1, std::min<int64_t>((items + 255) / 256, 2048))),
-                       dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a, sh->d_hbits, sh->d_hslots,
+    const size_t lds = (size_t)((d->cfg.ring + 1) & ~1) * sizeof(uint16_t) + 2 * (size_t)((d->cfg.ring + 31) / 32) * 4;
+    hipLaunchKernelGGL(k_holder_accum, dim3((uint32_t)std::max<int64_t>(1, std::min<int64_t>((items + 255) / 256, 1024))),
+                       dim3(256), lds, h->stream, a, sh->d_hbits, sh->d_hslots,
                        sh->how, gw0, (int64_t)sh->bounds[(size_t)sh->k], (int64_t)sh->bounds[(size_t)sh->k + 1]);
     return hip_check(h, hipGetLastError(), "k_holder_accum");
 }
@@ -3665,9 +3678,10 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     d->tm_cn = -1;
     if (cfg->topic_slots > 0) {
         // claim list for member-compacted cells (list_commit): a round's first
-        // deliveries; more overflow into k_commit's word scan (c5's busiest
-        // rounds overflowed 2 N: the scan ran in most rounds, 30 ms per tick)
-        d->clist_cap = std::max<int64_t>(4 * (int64_t)N, 1 << 20) / kClSub;
+        // deliveries; more overflow into k_commit's word scan, which is the
+        // cheaper commit for such a busy round (c5 with 4 N lists spread over
+        // waves: commit 73 -> 141 ms per tick)
+        d->clist_cap = std::max<int64_t>(2 * (int64_t)N, 1 << 20) / kClSub;
         A((void**)&d->d_clist, (size_t)d->clist_cap * kClSub * 8);
         A((void**)&d->d_clist_n, (kClSub + 1) * kClStride * 4);
         if (e == hipSuccess) e = hipMemsetAsync(d->d_clist_n, 0, (kClSub + 1) * kClStride * 4, h->stream);

@@ -1459,10 +1459,12 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
     __shared__ double s_sc[SPLIT ? 1 : WV][ROW];
     __shared__ KeyT s_key[WV][ROW];
     __shared__ uint64_t s_ok[SPLIT ? WV : 1][SPLIT ? ROW / 64 : 1];
+    __shared__ uint64_t s_cb[SPLIT ? 1 : WV][ROW / 64];          // the topic's candidates (makePrune's filter)
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double* sc = s_sc[SPLIT ? 0 : wid];
     KeyT* key = s_key[wid];
     uint64_t* ok = s_ok[SPLIT ? wid : 0];
+    uint64_t* cb = s_cb[SPLIT ? 0 : wid];
     auto kget = [&](int q) -> uint64_t {
         if constexpr (SPLIT) return ((ok[q >> 6] >> (q & 63)) & 1ull) ? (((uint64_t)key[q] << 32) | (uint32_t)q) : ~0ull;
         else return key[q];
@@ -1494,6 +1496,22 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
         for (uint64_t tm = mask; tm; tm &= tm - 1) {
             const HbArgs& a = hb_launder(a_);   // (re-read per topic: SGPR pressure)
             const int32_t t = __ffsll((long long)tm) - 1;
+            // the candidates of every PRUNE of topic t but its own peer: connected
+            // peers in t scored >= 0 (a bit per row position, once per topic)
+            if constexpr (SPLIT) __syncthreads();                // the last topic's PRUNEs are done with cb
+            else wave_lds_sync();
+            for (int q0 = SPLIT ? wid * 64 : 0; q0 < deg; q0 += SPLIT ? 64 * WV : 64) {
+                const int q = q0 + lane;
+                bool c = false;
+                if (q < deg) {
+                    const uint32_t e = b + (uint32_t)q;
+                    c = (a.rstate[e] & GSIM_ES_CONNECTED) && ((a.sub[a.col[e]] >> t) & 1ull) && sc[q] >= 0.0;
+                }
+                const uint64_t bm = __ballot(c);
+                if (lane == 0) cb[q0 >> 6] = bm;
+            }
+            if constexpr (SPLIT) __syncthreads();
+            else wave_lds_sync();
             for (int p0 = 0; p0 < deg; p0 += 64) {
                 const uint32_t ep_l = b + (uint32_t)(p0 + lane);
                 const uint64_t mp = p0 + lane < deg ? smask_of(a.smask, a.col[ep_l]) : 0ull;
@@ -1515,9 +1533,10 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
                         const int q = q0 + lane;
                         bool c = false;
                         if (q < deg && q != pos) {
-                            const uint32_t e = b + (uint32_t)q, x = a.col[e];
-                            c = (a.rstate[e] & GSIM_ES_CONNECTED) && ((a.sub[x] >> t) & 1ull) && sc[q] >= 0.0;
-                            const uint64_t kv = c ? select_key(a.seed, key_tick, gobs, kt, purpose, glob(a, x), (uint32_t)q) : ~0ull;
+                            c = (cb[q >> 6] >> (q & 63)) & 1ull;
+                            const uint64_t kv = c ? select_key(a.seed, key_tick, gobs, kt, purpose, glob(a, a.col[b + (uint32_t)q]),
+                                                               (uint32_t)q)
+                                                  : ~0ull;
                             if constexpr (SPLIT) key[q] = (uint32_t)(kv >> 32);
                             else key[q] = kv;
                         } else if (q < deg) {
