@@ -963,19 +963,39 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                         if (vv[0] && ev[0] == 0xFFFFFFFFu) n_acc++;
                         continue;
 #endif
+                        uint32_t xq[PUSH ? P : 1];   // PUSH: the copy's bit (a cross edge), ~0: an owned receiver
 #pragma unroll
                         for (int u = 0; u < P; ++u) {
                             iv[u] = 0; mfv[u] = 0; dsv[u] = 0; tfv[u] = 0; nv[u] = 0; xv[u] = 0.0;
+                            if constexpr (PUSH) xq[u] = ~0u;
                             if (vv[u]) {
                                 const uint32_t e = ev[u];
                                 const uint8_t vd = s_vd[kv[u]];
                                 // a masked row's positions are its mesh (or direct) edges: the
                                 // router flags are read only for direct ones (below)
                                 const int64_t pe = pv[u] + e;
-                                iv[u] = TM_LD(a.col[e]); dsv[u] = TM_LD(a.dstate[e]); tfv[u] = TM_LD(a.tflags[pe]);
+                                iv[u] = TM_LD(a.col[e]); dsv[u] = TM_LD(a.dstate[e]);
                                 if (!mk[u]) mfv[u] = TM_LD(a.mflags[pe]);
-                                if (verdict_penalises(vd)) xv[u] = TM_LD(a.invalid[pe]);
-                                else if (vd == GSIM_VERDICT_ACCEPT) nv[u] = TM_LD(a.mcnt[pe]);
+                                if constexpr (PUSH) {
+                                    xq[u] = a.xwq[e];
+                                } else {
+                                    tfv[u] = TM_LD(a.tflags[pe]);
+                                    if (verdict_penalises(vd)) xv[u] = TM_LD(a.invalid[pe]);
+                                    else if (vd == GSIM_VERDICT_ACCEPT) nv[u] = TM_LD(a.mcnt[pe]);
+                                }
+                            }
+                        }
+                        if constexpr (PUSH) {
+                            // the records of owned receivers only: a ghost's shard holds its own
+#pragma unroll
+                            for (int u = 0; u < P; ++u) {
+                                if (vv[u] && xq[u] == ~0u) {
+                                    const uint8_t vd = s_vd[kv[u]];
+                                    const int64_t pe = pv[u] + ev[u];
+                                    tfv[u] = TM_LD(a.tflags[pe]);
+                                    if (verdict_penalises(vd)) xv[u] = TM_LD(a.invalid[pe]);
+                                    else if (vd == GSIM_VERDICT_ACCEPT) nv[u] = TM_LD(a.mcnt[pe]);
+                                }
                             }
                         }
                         int qpl[P];              // validation latency: queue plane of the copy (-1: none)
@@ -1010,7 +1030,7 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                             if constexpr (PUSH) {
                                 // the receiver's shard delivers it (its AcceptFrom, records, cell)
                                 if (tg && remote) {
-                                    const uint32_t xb = a.xwq[e];
+                                    const uint32_t xb = xq[u];
                                     atomicOr(reinterpret_cast<unsigned long long*>(a.xbits + (int64_t)m * a.xbw + (xb >> 6)),
                                              1ull << (xb & 63u));
                                     continue;
@@ -3363,17 +3383,22 @@ __global__ __launch_bounds__(256) void k_holder_import(RoundArgs a, const uint32
         while (q + 1 < K && src[q + 1].toff <= tk) ++q;
         const HSrc sq = src[q];
         const int64_t cpw = ((int64_t)sq.nw + 63) / 64;
-        const int64_t rel = tk - sq.toff, k = rel / cpw, w = (rel - k * cpw) * 64 + lane;
+        const int64_t rel = tk - sq.toff, k = rel / cpw, w0 = (rel - k * cpw) * 64;
         const uint32_t m = (uint32_t)in[sq.in_off + k];
         const int32_t t = (int32_t)a.mtopic[m];
-        const uint64_t bits = w < sq.nw ? in[sq.in_off + sq.n + k * sq.nw + w] : 0ull;
-        for (uint64_t b = bits; b; b &= b - 1) {
-            const uint32_t l = g2l[sq.pbase + w * 64 + __builtin_ctzll(b)];
+        const uint64_t mine = w0 + lane < sq.nw ? in[sq.in_off + sq.n + k * sq.nw + w0 + lane] : 0ull;
+        // word by word, lane b taking bit b: the peers' g2l entries and cells
+        // are consecutive (most holders' words are dense)
+        for (uint64_t wm = __ballot(mine != 0); wm; wm &= wm - 1) {
+            const int j = __builtin_ctzll(wm);
+            const uint64_t bits = (uint64_t)__shfl((long long)mine, j, 64);
+            if (!((bits >> lane) & 1ull)) continue;
+            const uint32_t l = g2l[sq.pbase + (w0 + j) * 64 + lane];
             if (l == 0xFFFFFFFFu || (l >= a.rlo && l < a.rhi)) continue;      // not a ghost of this shard
             const int64_t ci = a.cs.idx(m, t, l);                              // a forwarder holds the topic
             if (ci >= 0) a.cs.cell[ci] = ((uint64_t)fr << 32) | kPeerMask;
         }
-        if (__ballot(bits != 0) && lane == 0 &&
+        if (__ballot(mine != 0) && lane == 0 &&
             __hip_atomic_load(&a.slot_last[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int32_t)fr)
             atomicMax(&a.slot_last[m], (int32_t)fr);
     }

@@ -34,6 +34,7 @@ struct Extra {
     // connections (a block of 1024 threads holding 4 row positions each)
     int64_t nh256 = 0, nh1024 = 0, nh4096 = 0;
     int64_t nh2048 = 0;                 // the first rows of the 1025-4096 class, of at most 2048 connections
+    int64_t nh128 = 0, nh512 = 0;       // ... of the 65-256 class of at most 128, of the 257-1024 class of at most 512
     // peer exchange (gsim_gossipsub_params.do_px): topics with PX PRUNEs per
     // observer, connection attempts per edge, the GRAFT RPCs that turned PX off
     uint64_t* d_pxo = nullptr;
@@ -2292,13 +2293,19 @@ int alloc_extra(gsim_handle* h)
         for (int c = 0; c < 2; ++c)
             std::stable_sort(cls[c].begin(), cls[c].end(), [&](uint32_t x, uint32_t y) { return sub[x] < sub[y]; });
     }
-    // the 1025-4096 class by row length: its first nh2048 rows take 2 positions
-    // per thread (k_heartbeat_hub<1024, 2>: 4 spill registers)
-    std::stable_sort(cls[5].begin(), cls[5].end(), [&](uint32_t x, uint32_t y) {
-        return rp[(size_t)x + 1] - rp[(size_t)x] < rp[(size_t)y + 1] - rp[(size_t)y];
-    });
-    h->x->nh2048 = (int64_t)std::count_if(cls[5].begin(), cls[5].end(),
-                                          [&](uint32_t x) { return rp[(size_t)x + 1] - rp[(size_t)x] <= 2048u; });
+    // the hub classes by row length: the shorter half of a class's range runs
+    // on a block of half the threads (a 1024-thread block idles most of its
+    // lanes on a row of 300), and the 1025-4096 class's first nh2048 rows take
+    // 2 positions per thread (k_heartbeat_hub<1024, 2>: 4 spill registers)
+    auto by_len = [&](std::vector<uint32_t>& c, uint32_t lim) {
+        std::stable_sort(c.begin(), c.end(), [&](uint32_t x, uint32_t y) {
+            return rp[(size_t)x + 1] - rp[(size_t)x] < rp[(size_t)y + 1] - rp[(size_t)y];
+        });
+        return (int64_t)std::count_if(c.begin(), c.end(), [&](uint32_t x) { return rp[(size_t)x + 1] - rp[(size_t)x] <= lim; });
+    };
+    h->x->nh128 = by_len(cls[3], 128);
+    h->x->nh512 = by_len(cls[4], 512);
+    h->x->nh2048 = by_len(cls[5], 2048);
     h->x->max_degree = md;
     h->x->n16 = (int64_t)cls[0].size(); h->x->n32 = (int64_t)cls[1].size(); h->x->n64 = (int64_t)cls[2].size();
     h->x->nh256 = (int64_t)cls[3].size(); h->x->nh1024 = (int64_t)cls[4].size(); h->x->nh4096 = (int64_t)cls[5].size();
@@ -2525,12 +2532,18 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
                                        a, r + x->n16 + x->n32, x->n64, (int64_t)0);
         // hubs: one block per observer
         const uint32_t* rh = r + x->n16 + x->n32 + x->n64;
-        if (x->nh256)
-            hipLaunchKernelGGL((k_heartbeat_hub<256, 1>), dim3((uint32_t)std::min<int64_t>(x->nh256, 65536)), dim3(256),
-                               0, h->stream, a, rh, x->nh256);
-        if (x->nh1024)
-            hipLaunchKernelGGL((k_heartbeat_hub<1024, 1>), dim3((uint32_t)std::min<int64_t>(x->nh1024, 65536)),
-                               dim3(1024), 0, h->stream, a, rh + x->nh256, x->nh1024);
+        if (x->nh128)
+            hipLaunchKernelGGL((k_heartbeat_hub<128, 1>), dim3((uint32_t)std::min<int64_t>(x->nh128, 65536)), dim3(128),
+                               0, h->stream, a, rh, x->nh128);
+        if (x->nh256 > x->nh128)
+            hipLaunchKernelGGL((k_heartbeat_hub<256, 1>), dim3((uint32_t)std::min<int64_t>(x->nh256 - x->nh128, 65536)),
+                               dim3(256), 0, h->stream, a, rh + x->nh128, x->nh256 - x->nh128);
+        if (x->nh512)
+            hipLaunchKernelGGL((k_heartbeat_hub<512, 1>), dim3((uint32_t)std::min<int64_t>(x->nh512, 65536)),
+                               dim3(512), 0, h->stream, a, rh + x->nh256, x->nh512);
+        if (x->nh1024 > x->nh512)
+            hipLaunchKernelGGL((k_heartbeat_hub<1024, 1>), dim3((uint32_t)std::min<int64_t>(x->nh1024 - x->nh512, 65536)),
+                               dim3(1024), 0, h->stream, a, rh + x->nh256 + x->nh512, x->nh1024 - x->nh512);
         if (x->nh2048)   // 2 row positions per thread
             hipLaunchKernelGGL((k_heartbeat_hub<1024, 2>), dim3((uint32_t)std::min<int64_t>(x->nh2048, 65536)),
                                dim3(1024), 0, h->stream, a, rh + x->nh256 + x->nh1024, x->nh2048);
