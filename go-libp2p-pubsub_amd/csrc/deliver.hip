@@ -1563,7 +1563,8 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a_, const uint32_t* gcount
         }
         nstage = 0;
     };
-    for (int k0 = 0; k0 < nact; k0 += kSlotBatch) {
+    // MM: the member-major phases below walk a row once for many slots
+    for (int k0 = 0; !MM && k0 < nact; k0 += kSlotBatch) {
         uint64_t cv[kSlotBatch];
 #pragma unroll
         for (int b = 0; b < kSlotBatch; ++b) {
@@ -1581,7 +1582,6 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a_, const uint32_t* gcount
             if (k >= nact) break;                            // wave-uniform
             const uint32_t m = s_act[k] & 0x7FFF;
             const bool push = (s_act[k] & 0x8000) != 0;
-            if (MM && !push) continue;                       // pulled below, one row walk for many slots
             const int32_t t = (int32_t)a.mtopic[m];
             const uint32_t origin = a.morigin[m];
             const bool inv = a.minv[m] != 0;
@@ -1682,6 +1682,95 @@ __global__ __launch_bounds__(256) void k_ihave(IhArgs a_, const uint32_t* gcount
         }
     }
     if constexpr (MM) {
+        // push slots of the block's topic, up to 64 at a time: a holder walks its
+        // row once for all the slots it holds, and each peer it gossiped tb to
+        // (and that is one of this shard's receivers, whose gate passes) is
+        // asked about each of them (the same triples as a walk per slot)
+        for (int k0 = 0; k0 < nact; k0 += 64) {
+            const int kn = nact - k0 < 64 ? nact - k0 : 64;
+            uint64_t hm = 0;
+            for (int q = 0; q < kn; ++q) {
+                const uint16_t sa = s_act[k0 + q];
+                if (!(sa & 0x8000)) continue;                // pulled below (wave-uniform)
+                const uint32_t m = sa & 0x7FFF;
+                const uint64_t c = vp ? a.cs.cell[(int64_t)a.cs.cbase[m] + jw + lane] : kUnseen64;
+                if (vp && holds_in_window(c, a.g, a.lo_round, tick_round, a.minv[m] != 0, (uint32_t)pl == a.morigin[m],
+                                          LAT ? a.mlat[m] : 0u))
+                    hm |= 1ull << q;
+            }
+            const uint64_t mask = __ballot(hm != 0);
+            if (!mask) continue;
+            const int32_t t = tb;
+            auto hchunk = [&](uint32_t off, uint32_t gl_, uint32_t beg, uint32_t deg, uint32_t me_id, uint32_t me_g,
+                              bool ign_s, int64_t me_pl, uint64_t hmw) {
+                const bool v = off + gl_ < deg;
+                const uint32_t e = beg + off + gl_;
+                uint32_t p = 0, re = 0;
+                bool gs = false;
+                if (v && me_pl >= 0 && a.gsel[me_pl + e]) {        // holder me_id gossiped tb to p
+                    p = a.col[e];
+                    re = a.rev[e];
+                    gs = p >= a.rlo && p < a.rhi && a.gstate[re];  // p's gate on me_id
+                }
+                const uint64_t mine = gs ? hmw : 0ull;
+                uint64_t uw = mine;
+                for (int o = 32; o; o >>= 1) uw |= (uint64_t)__shfl_xor((long long)uw, o, 64);
+                const uint32_t pg = gs ? (a.gid ? a.gid[p] : p) : 0u;
+                for (; uw; uw &= uw - 1) {
+                    const int q = __builtin_ctzll(uw);
+                    const uint32_t m = s_act[k0 + q] & 0x7FFF;
+                    bool req = false, resp = false;
+                    if ((mine >> q) & 1ull) {
+                        const int64_t pci = a.cs.at((int64_t)a.cs.cbase[m], t, p);
+                        req = pci >= 0 && a.cs.cell[pci] == kUnseen64;   // p has not seen m
+                        if (req) {
+                            const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, pg, 0, P_PROMISE, m, me_g);
+                            atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[re]), (unsigned long long)key);
+                            resp = a.respond && a.gstate[e] && !ign_s && peertx_allows(a, m, e, me_id);
+                        }
+                    }
+                    n_req += req;
+                    n_resp += resp;
+                    const uint64_t sb = __ballot(resp);
+                    if (sb) {
+                        if (nstage + __popcll(sb) > kRespStage) flush_stage();
+                        if (resp) stage[nstage + __popcll(sb & ((1ull << lane) - 1))] = (uint64_t)e | ((uint64_t)m << 32);
+                        nstage += __popcll(sb);
+                    }
+                }
+            };
+            const uint64_t longm = mask & long_lanes;
+            uint64_t gm = mask & ~longm & gmask;
+            while (__ballot(gm != 0)) {
+                int bs = -1;
+                if (gm) { bs = __ffsll((long long)gm) - 1; gm &= gm - 1; }
+                const int sl = bs < 0 ? lane : bs;
+                const uint32_t beg = __shfl(rp0, sl, 64), end = __shfl(rp1, sl, 64);
+                const bool ign_s = __shfl(ign_l, sl, 64);
+                const uint32_t me_id = (uint32_t)__shfl((int)pl, sl, 64);
+                const uint64_t hmw = bs < 0 ? 0ull : (uint64_t)__shfl((long long)hm, sl, 64);
+                const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
+                const uint64_t me_m = smask_of(a.smask, me_id);
+                const int64_t me_pl = slot_has(me_m, t) ? slot_idx(me_m, t, a.E, 0) : -1;
+                n_walk += (gl == 0 && bs >= 0);
+                const uint32_t deg = bs >= 0 ? end - beg : 0u;
+                for (uint32_t off = 0; __ballot(off < deg) != 0; off += W)
+                    hchunk(off, (uint32_t)gl, beg, deg, me_id, me_g, ign_s, me_pl, hmw);
+            }
+            for (uint64_t lm = longm; lm; lm &= lm - 1) {
+                const int bs = __builtin_ctzll(lm);
+                const uint32_t beg = __shfl(rp0, bs, 64), end = __shfl(rp1, bs, 64);
+                const bool ign_s = __shfl(ign_l, bs, 64);
+                const uint32_t me_id = (uint32_t)__shfl((int)pl, bs, 64);
+                const uint64_t hmw = (uint64_t)__shfl((long long)hm, bs, 64);
+                const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
+                const uint64_t me_m = smask_of(a.smask, me_id);
+                const int64_t me_pl = slot_has(me_m, t) ? slot_idx(me_m, t, a.E, 0) : -1;
+                n_walk += (lane == 0);
+                for (uint32_t off = 0; off < end - beg; off += 64)
+                    hchunk(off, (uint32_t)lane, beg, end - beg, me_id, me_g, ign_s, me_pl, hmw);
+            }
+        }
         // pull slots of the block's topic, up to 64 at a time: a receiver walks
         // its row once for all the slots it wants (not once per slot), and an
         // edge whose advertiser gossiped tb to it asks for each wanted slot
