@@ -2185,109 +2185,6 @@ __device__ __forceinline__ void listed_copy(const RoundArgs& a, uint32_t r, uint
     }
 }
 
-// One copy of slot m on record r whose counters no other thread of the launch
-// touches (k_xbits_deliver: a record is one bit position of one source, and
-// one lane takes all of its slots): listed_copy with the record's state
-// passed in and plain read-modify-writes of its counters (as k_send_tm).
-__device__ __forceinline__ void owned_mcnt_inc(const RoundArgs& a, int64_t ir, double cap)
-{
-    uint32_t n = a.mcnt[ir];
-    if (n == 255u) {
-        a.meshd[ir] = apply_incs(a.meshd[ir], n, cap);
-        n = 0;
-    }
-    a.mcnt[ir] = (uint8_t)(n + 1);
-}
-
-__device__ __forceinline__ void owned_copy(const RoundArgs& a, uint32_t r, uint32_t m, uint8_t ds, uint32_t p,
-                                           const uint32_t* owner, uint32_t par, uint32_t claim_hi, ctp_t tpa,
-                                           unsigned long long& n_acc, unsigned long long& n_gray,
-                                           unsigned long long& n_first, uint32_t* s_new2)
-{
-    if (!(ds & GSIM_DS_ACCEPT)) { n_gray++; return; }        // AcceptFrom
-    // the sender (row owner) is read only where it matters: topic slots,
-    // the gater, the trace, a claim (most copies are plain duplicates)
-    const bool need_i = a.smask || a.gt.act || a.tr.on(p);
-    uint32_t i = need_i ? owner[r] : 0xFFFFFFFFu;
-    // the peer gater (gater_accept): one draw per IWANT answer RPC -- (round,
-    // receiver, sender), the slot left out (AcceptFrom runs per RPC, pubsub.go);
-    // a shard's pushed copies are forwarded messages, one RPC each
-    if (a.gt.act && !gater_accept(a, p, r, a.sharded ? m : kGaterRpcSlot, i)) return;
-    if (a.subdyn && !((a.sub[p] >> (int32_t)a.mtopic[m]) & 1ull)) return;   // a topic p left
-    if (a.gt.act) gater_copy(a, r, a.minv[m] == GSIM_VERDICT_SIGNATURE);
-    n_acc++;
-    const int32_t t = (int32_t)a.mtopic[m];
-    const ctp_t tp = tpa + t;
-    const uint8_t vd = a.minv[m];
-    if (a.tr.on(p))
-        a.tr.push(round_time(a, a.g), ((uint64_t)a.g << 32) | m, p, i, t,
-                  vd != GSIM_VERDICT_SIGNATURE ? kTraceCopy : (uint8_t)GSIM_TRACE_REJECT_MESSAGE, vd);
-    const bool inv = vd != GSIM_VERDICT_ACCEPT;
-    const bool pen = verdict_penalises(vd);
-    const uint64_t mi = smask_of(a.smask, i);               // the record sits in the sender's row
-    const int64_t ir = slot_idx(mi, t, a.E, r);
-    const bool sc = tp->scored && (ds & GSIM_DS_TRACKED) && slot_has(mi, t);
-    const uint8_t tf = a.tflags[ir];
-    const int64_t window = tp->mesh_message_deliveries_window_ns;
-    const uint32_t L = a.mlat ? a.mlat[m] : 0u;
-    // committed before this round and the cell's round cannot matter (as
-    // k_send_tm's known copies): a duplicate, credited without the cell
-    if (!L && ((a.seenbm[(int64_t)m * a.nw + (p >> 6)] >> (p & 63)) & 1ull)) {
-        const bool wa = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
-        if (wa || !sc || inv || !(tf & GSIM_TF_IN_MESH)) {
-            if (!sc) return;
-            if (pen) a.invalid[ir] += 1.0;
-            else if (!inv && (tf & GSIM_TF_IN_MESH))         // wa: within the window
-                owned_mcnt_inc(a, ir, tp->mesh_message_deliveries_cap);
-            return;
-        }
-    }
-    const int64_t pci = a.cs.idx(m, t, p);      // p wanted it: a member of t
-    if (pci < 0) return;
-    uint64_t* cellp = a.cs.cell + pci;
-    const uint64_t c = *cellp;
-    const uint32_t hi = (uint32_t)(c >> 32);
-    int64_t seen_round = -1;               // completion round (k_send_tm)
-    if (c != kUnseen64) {
-        if (!(hi & kClaim)) seen_round = hi;
-        else if (((hi >> 30) & 1u) != par) seen_round = a.g - 1 + L;
-    }
-    if (vd != GSIM_VERDICT_SIGNATURE && seen_round < 0 && (c == kUnseen64 || (hi & kEdgeMask) > r)) {
-        if (!need_i) i = owner[r];
-        uint32_t lo = i;
-        if (sc && !inv) {
-            lo |= kCreditFirst;
-            if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo |= kCreditMesh;
-        }
-        const uint64_t v = ((uint64_t)(claim_hi | r) << 32) | lo;
-        const uint64_t prev = __hip_atomic_fetch_min(cellp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == kUnseen64) {
-            n_first++;
-            atomicOr(&s_new2[m >> 5], 1u << (m & 31));
-            if (a.clist) {
-                const uint32_t sq = blockIdx.x % kClSub;
-                const uint32_t q = atomicAdd(&a.clist_n[sq * kClStride], 1u);
-                if ((int64_t)q < a.clist_cap) a.clist[(int64_t)sq * a.clist_cap + q] = (uint64_t)p | ((uint64_t)m << 32);
-                else atomicOr(&a.clist_n[kClSub * kClStride], 1u);
-            }
-        }
-    }
-    if (L && vd != GSIM_VERDICT_SIGNATURE && (seen_round < 0 || seen_round > a.g)) {
-        // the lanes here push together (ballots over the active lanes)
-        const bool q = tp->scored && (pen || !inv);
-        vq_push_wave(a, q ? (int)((seen_round < 0 ? a.g + L : seen_round) & (kVqPlanes - 1)) : -1,
-                     vq_entry(r, t, pen ? kVqInv : kVqDup));
-        return;
-    }
-    if (!sc) return;
-    if (pen) {
-        a.invalid[ir] += 1.0;                           // markInvalidMessageDelivery
-    } else if (!inv && (tf & GSIM_TF_IN_MESH)) {
-        const bool in_window = seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window) : (window >= 0);
-        if (in_window) owned_mcnt_inc(a, ir, tp->mesh_message_deliveries_cap);
-    }
-}
-
 // Copies that arrive as a list of (record, slot): round 2's messages queued by
 // handleIWant (a shard's copies pushed by other shards arrive as bits:
 // k_xbits_deliver).  Same rules and tracer events as k_send_tm's copies.
@@ -3182,9 +3079,8 @@ int deliver_round_queue(gsim_handle* h, int64_t round, const uint64_t* q, const 
 // ---- copy push as bitmaps -------------------------------
 // A round's copies to ghost receivers are bits of xbits ([ring][xbw] words,
 // k_send_tm<PUSH>).  The gather lists each destination's segment of every
-// active slot (the slots k_send_tm walked: nnew_prev), slot ids first, then
-// word-major (word w of every slot together), and clears it:
-// out[d] = [m_0 .. m_{n-1}] [xw_d x n words]; cnt[0] = n.
+// active slot (the slots k_send_tm walked: nnew_prev), slot ids first, and
+// clears it:  out[d] = [m_0 .. m_{n-1}] [n x xw_d words]; cnt[0] = n.
 __global__ __launch_bounds__(256) void k_xbits_gather(const uint32_t* nnew, int32_t ring, uint64_t* xbits, int64_t xbw,
                                                       const int64_t* xwo, uint64_t* out, int64_t out_cap, uint32_t* cnt)
 {
@@ -3200,7 +3096,7 @@ __global__ __launch_bounds__(256) void k_xbits_gather(const uint32_t* nnew, int3
     }
     const int64_t tot = (int64_t)n * xw;
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < tot; x += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t w = x / n, k = x - w * n;
+        const int64_t k = x / xw, w = x - k * xw;
         uint64_t* src = xbits + (int64_t)s_act[k] * xbw + w0 + w;
         const uint64_t v = *src;
         o[n + x] = v;
@@ -3208,17 +3104,19 @@ __global__ __launch_bounds__(256) void k_xbits_gather(const uint32_t* nnew, int3
     }
 }
 
-// The bits from every other shard: per source q, n slots, xw words each (word
-// w of every slot together); bit b of word w is the record gbase + 64 w + b
-// (the ghost block of q's peers, in q's cross-out order).  A wave takes
-// kXbWords words of a source; lane b owns record 64 w + b of each word, loads its state
-// once and applies every slot's copy to it in slot order: neighbouring lanes
-// touch neighbouring records, and the records' counters need no atomics.
+// The bits from every other shard: per source q, n slots of xw words, a bit
+// at position b of slot m's words is a copy of m on record gbase + b (the
+// ghost block of q's peers, in q's cross-out order).  A wave takes 64 words
+// of one slot and applies their copies in record order (the set bits listed
+// in LDS), so neighbouring lanes touch neighbouring records.
+constexpr int kXbList = 1024;                // per-wave LDS list of a task's copies
+
 __global__ __launch_bounds__(256) void k_xbits_deliver(RoundArgs a_, const uint64_t* in, const XSrc* src, int32_t K,
                                                        int64_t ntask, const uint32_t* owner)
 {
     const RoundArgs& a = a_;
     extern __shared__ uint32_t s_new2[];
+    __shared__ uint32_t s_list[4][kXbList];
     __shared__ unsigned long long s_stats[4];
     for (int w = threadIdx.x; w < (a.ring + 31) / 32; w += blockDim.x) s_new2[w] = 0;
     if (threadIdx.x < 4) s_stats[threadIdx.x] = 0;
@@ -3228,33 +3126,42 @@ __global__ __launch_bounds__(256) void k_xbits_deliver(RoundArgs a_, const uint6
     const uint32_t claim_hi = kClaim | (par << 30);
     const ctp_t tpa = const_tp(a.tp);
     unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
+    uint32_t* lst = s_list[wid];
     for (int64_t tk = (int64_t)blockIdx.x * 4 + wid; tk < ntask; tk += (int64_t)gridDim.x * 4) {   // wave-uniform
         const RoundArgs& a = kernarg0(a_);
         int q = 0;
         while (q + 1 < K && src[q + 1].toff <= tk) ++q;
         const XSrc sq = src[q];
-        const int64_t c0 = (tk - sq.toff) * kXbWords;
-        const uint64_t* ids = in + sq.in_off;
-        const uint64_t* wb = ids + sq.n;
-        for (int64_t w = c0; w < c0 + kXbWords && w < sq.xw; ++w) {
-            for (int k0 = 0; k0 < sq.n; k0 += 64) {
-                const uint64_t sw = k0 + lane < sq.n ? wb[w * sq.n + k0 + lane] : 0ull;
-                uint64_t nz = __ballot(sw != 0);
-                if (!nz) continue;
-                uint64_t any = sw;                                      // the records with a copy
-                for (int o = 32; o; o >>= 1) any |= (uint64_t)__shfl_xor((long long)any, o, 64);
-                const uint32_t r = (uint32_t)(sq.gbase + w * 64 + lane);
-                const bool mine = (any >> lane) & 1ull;
-                const uint8_t ds = mine ? a.dstate[r] : (uint8_t)0;
-                const uint32_t p = mine ? a.col[r] : 0u;
-                for (; nz; nz &= nz - 1) {
-                    const int kk = __builtin_ctzll(nz);
-                    const uint64_t bits = (uint64_t)__shfl((long long)sw, kk, 64);
-                    const uint32_t m = (uint32_t)ids[k0 + kk];
-                    if ((bits >> lane) & 1ull)
-                        owned_copy(a, r, m, ds, p, owner, par, claim_hi, tpa, n_acc, n_gray, n_first, s_new2);
-                }
+        const int64_t cpw = ((int64_t)sq.xw + 63) / 64;
+        const int64_t rel = tk - sq.toff, k = rel / cpw, c0 = (rel - k * cpw) * 64;
+        const uint32_t m = (uint32_t)in[sq.in_off + k];
+        const int64_t w = c0 + lane;
+        const uint64_t bits = w < sq.xw ? in[sq.in_off + sq.n + k * sq.xw + w] : 0ull;
+        const uint32_t cnt = (uint32_t)__popcll(bits);
+        uint32_t pre = cnt;                                   // inclusive scan over the wave
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)pre, o, 64);
+            if (lane >= o) pre += y;
+        }
+        const uint32_t total = (uint32_t)__shfl((int)pre, 63, 64);
+        if (!total) continue;
+        const int64_t rb = sq.gbase + w * 64;
+        if (total <= (uint32_t)kXbList) {
+            uint32_t pos = pre - cnt;
+            for (uint64_t b = bits; b; b &= b - 1) lst[pos++] = (uint32_t)(w * 64) + (uint32_t)__builtin_ctzll(b);
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+                if (j0 + lane < total)
+                    listed_copy(a, (uint32_t)(sq.gbase + lst[j0 + lane]), m, owner, par, claim_hi, tpa, n_acc, n_gray,
+                                n_first, s_new2);
             }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // lst is rewritten by the next task
+        } else {
+            for (uint64_t b = bits; b; b &= b - 1)
+                listed_copy(a, (uint32_t)(rb + __builtin_ctzll(b)), m, owner, par, claim_hi, tpa, n_acc, n_gray, n_first,
+                            s_new2);
         }
     }
     n_acc = wave_sum_u64(n_acc);

@@ -214,14 +214,12 @@ struct HSrc {
 };
 
 // One source shard's part of a round's received copy bits (k_xbits_deliver):
-// its n active slots' ids at in_off, then xw x n words (word-major); bit b of
-// word w of slot k is a copy on record gbase + 64 w + b (the ghost block of
-// the source's peers).
-constexpr int kXbWords = 8;                // words of a source per k_xbits_deliver wave
+// its n active slots' ids at in_off, then n x xw words; bit b of slot k is a
+// copy on record gbase + b (the ghost block of the source's peers).
 struct XSrc {
     int64_t in_off;    // first entry of the source's part (slot ids, then words)
     int64_t gbase;     // first record of its ghost block
-    int64_t toff;      // first wave task (kXbWords words, every slot of them)
+    int64_t toff;      // first wave task (64 words of one slot each)
     int32_t n, xw;     // slots, words per slot
 };
 

@@ -1265,7 +1265,7 @@ int exchange_copies(gsim_group* g, int64_t round)
                 x.n = (int32_t)(c / (1 + xw));
             }
             x.toff = ntask[l];
-            ntask[l] += x.n ? (xw + kXbWords - 1) / kXbWords : 0;   // a wave per kXbWords words (every slot of them)
+            ntask[l] += (int64_t)x.n * ((xw + 63) / 64);
             off += c;
         }
     }
