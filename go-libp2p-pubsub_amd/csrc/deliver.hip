@@ -136,6 +136,7 @@ struct Deliver {
     uint32_t* d_tmtab = nullptr;       // k_send_tm blocks: [T+1] first block of each topic, [T] its range
     std::vector<uint32_t> tmtab;       // host copy (the upload's source)
     int64_t tm_cn = -1;                // peers the table was built for
+    int32_t tm_tb = 0;                 // k_send_tm block size d_tmtab was laid out for
     int32_t* d_mpub = nullptr;         // [ring] round the slot's message was published in
     int64_t* d_roff = nullptr;         // [rounds] offset of each round in its heartbeat
     int32_t* d_lastput = nullptr;      // [T][N]
@@ -701,6 +702,10 @@ constexpr int kTsSlots = 64;
 #define TM_LDC(x) (x)
 #endif
 constexpr int kPushTB = GSIM_TM_TB;  // ... of a shard's push walk (512: 21 against 18.5 ms per shard at K = 8)
+// ... with member-compacted cells (sparse frontiers: many topics, each block's
+// chunks hold few forwarders): c5 send 184 / 151 / 158 ms per tick at 1024 / 512 /
+// 256 threads (gpurun_out/r04n); dense C3 is fastest at 1024 (§4.2)
+constexpr int kSparseTB = 512;
 constexpr uint32_t kTmWin = 8192;   // flattened edges whose senders are tabled in LDS at once
 constexpr int kTmTabMin = 256;      // forwarders in a chunk from which the table pays for its fill
 
@@ -1196,50 +1201,54 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
     if (a.clist && !a.clist_n[kClSub * kClStride]) return;   // the claim list covers the round (k_commit_list)
     const int nact = active_slots(a.nnew_cur, a.ring, s_act, &s_n);
     const int lane = threadIdx.x & 63;
-    // claims exist only at receivers' cells: the words of [rlo, rhi)
-    const int64_t i0 = ((int64_t)a.rlo & ~63ll) + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
-    if (i0 >= (int64_t)a.rhi || nact == 0) return;
-    const int64_t i = i0 + lane;
-    const bool vi = i < a.CN;
-    const uint32_t par = (uint32_t)(a.g & 1);
-    for (int k0 = 0; k0 < nact; k0 += kSlotBatch) {
-        uint64_t cv[kSlotBatch];
-        int64_t ci[SP ? kSlotBatch : 1];   // the dense layout recomputes m * N + i
+    // claims exist only at receivers' cells: the words of [rlo, rhi), a wave per
+    // word, grid-stride (a launch that exits early stays cheap: c5's 39k blocks
+    // cost 1 ms per round doing nothing)
+    for (int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);; wv += (int64_t)gridDim.x * 4) {
+        const int64_t i0 = ((int64_t)a.rlo & ~63ll) + wv * 64;
+        if (i0 >= (int64_t)a.rhi || nact == 0) return;
+        const int64_t i = i0 + lane;
+        const bool vi = i < a.CN;
+        const uint32_t par = (uint32_t)(a.g & 1);
+        for (int k0 = 0; k0 < nact; k0 += kSlotBatch) {
+            uint64_t cv[kSlotBatch];
+            int64_t ci[SP ? kSlotBatch : 1];   // the dense layout recomputes m * N + i
 #pragma unroll
-        for (int b = 0; b < kSlotBatch; ++b) {
-            const int k = k0 + b;
-            const int64_t c = (k < nact && vi) ? word_cell<SP>(a.cs, a.mtopic, s_act[k], i0 >> 6, lane) : -1;
-            if constexpr (SP) ci[b] = c;
-            cv[b] = c >= 0 ? a.cs.cell[c] : kUnseen64;
-        }
+            for (int b = 0; b < kSlotBatch; ++b) {
+                const int k = k0 + b;
+                const int64_t c = (k < nact && vi) ? word_cell<SP>(a.cs, a.mtopic, s_act[k], i0 >> 6, lane) : -1;
+                if constexpr (SP) ci[b] = c;
+                cv[b] = c >= 0 ? a.cs.cell[c] : kUnseen64;
+            }
 #pragma unroll
-        for (int b = 0; b < kSlotBatch; ++b) {
-            const int k = k0 + b;
-            const uint64_t cb = __ballot(k < nact && is_claim_of(cv[b], par));
-            if (cb && lane == 0) {
-                const uint32_t m = s_act[k];
-                a.seenbm[(int64_t)m * a.nw + (i0 >> 6)] |= cb;
-                // receivers forward what they accepted, in the next round
-                if (a.fresh && a.minv[m] == GSIM_VERDICT_ACCEPT && (!LAT || !a.mlat[m])) {
-                    // fire-and-forget atomics: the wave does not wait on them
-                    atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (i0 >> 6)), cb);
-                    atomicOr(reinterpret_cast<unsigned long long*>(a.fsum + (int64_t)m * a.nsw + (i0 >> 12)),
-                             1ull << ((i0 >> 6) & 63));
+            for (int b = 0; b < kSlotBatch; ++b) {
+                const int k = k0 + b;
+                const uint64_t cb = __ballot(k < nact && is_claim_of(cv[b], par));
+                if (cb && lane == 0) {
+                    const uint32_t m = s_act[k];
+                    a.seenbm[(int64_t)m * a.nw + (i0 >> 6)] |= cb;
+                    // receivers forward what they accepted, in the next round
+                    if (a.fresh && a.minv[m] == GSIM_VERDICT_ACCEPT && (!LAT || !a.mlat[m])) {
+                        // fire-and-forget atomics: the wave does not wait on them
+                        atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (i0 >> 6)), cb);
+                        atomicOr(reinterpret_cast<unsigned long long*>(a.fsum + (int64_t)m * a.nsw + (i0 >> 12)),
+                                 1ull << ((i0 >> 6) & 63));
+                    }
                 }
             }
-        }
 #pragma unroll
-        for (int b = 0; b < kSlotBatch; ++b) {
-            const int k = k0 + b;
-            if (k >= nact) break;
-            int qpl = -1;
-            uint64_t qv = 0;
-            if (is_claim_of(cv[b], par)) {
-                const uint32_t m = s_act[k];
-                uint64_t* cp = a.cs.cell + (SP ? ci[b] : (int64_t)m * a.cs.n + i);
-                commit_claim<false, LAT, SP, GT>(a, cp, cv[b], a.g, m, i, &qpl, &qv);
+            for (int b = 0; b < kSlotBatch; ++b) {
+                const int k = k0 + b;
+                if (k >= nact) break;
+                int qpl = -1;
+                uint64_t qv = 0;
+                if (is_claim_of(cv[b], par)) {
+                    const uint32_t m = s_act[k];
+                    uint64_t* cp = a.cs.cell + (SP ? ci[b] : (int64_t)m * a.cs.n + i);
+                    commit_claim<false, LAT, SP, GT>(a, cp, cv[b], a.g, m, i, &qpl, &qv);
+                }
+                if constexpr (LAT) vq_push_wave(a, qpl, qv);
             }
-            if constexpr (LAT) vq_push_wave(a, qpl, qv);
         }
     }
 }
@@ -2772,7 +2781,7 @@ int deliver_flush(gsim_handle* h)
     if (!d || d->pending < 0) return GSIM_OK;
     ProfScope ps(h, GSIM_K_COMMIT);
     RoundArgs a = make_round_args(h, d->pending);
-    const dim3 grid(grid_peers((int64_t)a.rhi - ((int64_t)a.rlo & ~63ll)));
+    const dim3 grid(std::min(grid_peers((int64_t)a.rhi - ((int64_t)a.rlo & ~63ll)), 8192));
     if (a.clist)
         hipLaunchKernelGGL(k_commit_list<true>, dim3(64, kClSub), dim3(256), 0, h->stream, a);
     if (a.mlat)
@@ -2873,7 +2882,8 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
     // budgets 4096 / 8192 / 15680 (default) / 32768 / 65536: 29.7 / 25.0 / 24.7 /
     // 28.0 / 32.9 ms of send per tick (profiles/r02_ab_send_blocks.log)
     constexpr int TB = GSIM_TM_TB;
-    const int TBv = a0.push ? kPushTB : TB;
+    const bool sp = sparse_layout(h);
+    const int TBv = a0.push ? kPushTB : sp ? kSparseTB : TB;
     const int64_t total = 2048 * (1024 / TBv);
     const int64_t chunk = 2 * TBv;
     // every local peer sends (pull: a shard's ghosts too), or the owned range (push)
@@ -2885,7 +2895,7 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
                                                                     std::max<int64_t>(h->t >= 32 ? 256 : 1,
                                                                                       total / T)));
     Deliver* d = h->dl;
-    if (d->tm_cn != cn) {
+    if (d->tm_cn != cn || d->tm_tb != TBv) {
         // the same budget of ranges x T blocks, shared out by subscribers
         // (Zipf topics: the busiest topic's blocks set the launch's length),
         // ranges of whole chunks
@@ -2912,6 +2922,7 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
                                       h->stream);
         if (e != hipSuccess) return hip_check(h, e, "k_send_tm block table");
         d->tm_cn = cn;
+        d->tm_tb = TBv;
     }
     const RoundArgs& a = a0;
     // the slot list in LDS
@@ -2919,20 +2930,22 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
     if (a.push && a.mlat)
         hipLaunchKernelGGL((k_send_tm<kPushTB, true, true, false, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
                            h->stream, a);
-    else if (a.push && sparse_layout(h))
+    else if (a.push && sp)
         hipLaunchKernelGGL((k_send_tm<kPushTB, false, true, false, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
                            h->stream, a);
     else if (a.push)
         hipLaunchKernelGGL((k_send_tm<kPushTB, false, false, false, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
                            h->stream, a);
+    else if (a.mlat && sp)
+        hipLaunchKernelGGL((k_send_tm<kSparseTB, true, true>), dim3(d->tmtab[T]), dim3(kSparseTB), lds, h->stream, a);
     else if (a.mlat)
         hipLaunchKernelGGL((k_send_tm<TB, true, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
-    else if (a.gt.act && sparse_layout(h))
-        hipLaunchKernelGGL((k_send_tm<TB, false, true, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+    else if (a.gt.act && sp)
+        hipLaunchKernelGGL((k_send_tm<kSparseTB, false, true, true>), dim3(d->tmtab[T]), dim3(kSparseTB), lds, h->stream, a);
     else if (a.gt.act)
         hipLaunchKernelGGL((k_send_tm<TB, false, false, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
-    else if (sparse_layout(h))
-        hipLaunchKernelGGL((k_send_tm<TB, false, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+    else if (sp)
+        hipLaunchKernelGGL((k_send_tm<kSparseTB, false, true>), dim3(d->tmtab[T]), dim3(kSparseTB), lds, h->stream, a);
     else
         hipLaunchKernelGGL((k_send_tm<TB, false, false>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_send_tm");
