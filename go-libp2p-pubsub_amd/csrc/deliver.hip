@@ -114,6 +114,12 @@ struct Deliver {
     int64_t cell_nw = 0;               // words per topic of the member bitmaps
     int64_t n_peers = 0;               // peers the cells were laid out for
     std::vector<int64_t> tcount;       // [T] messages published per topic (sub-ring slot choice)
+    // publications per topic of the last kPubTicks ticks (ring by tick), for the
+    // bound on a record's pending meshd increments (RoundArgs::mcnt_fast)
+    std::vector<int32_t> pubw;         // [kPubTicks][T]
+    std::vector<int64_t> pubw_tick;    // [kPubTicks] the tick each row counts
+    int32_t pub_bound = 0;             // max over topics of the window's publications
+    int64_t applied_tick = 0;          // tick of the last application of the pending increments
     uint32_t* d_pslot = nullptr;       // [pub_cap] ring slots of a publish batch
     // claim list (member-compacted cells): the cells a round claimed, so the
     // commit touches those alone instead of every (active slot, peer word)
@@ -247,6 +253,11 @@ struct RoundArgs {
     int64_t clist_cap;
     int64_t ncells;                // cells of the seen-set (the last slot's end)
     int32_t topic_slots;           // sub-rings: slots [t R, t R + R) carry topic t (0: one shared ring)
+    // no record can collect 256 - 56 pending increments before the next refresh
+    // (a record gets at most 1 + GossipRetransmission copies of a message, and
+    // only of a message published in the last kPubTicks ticks): listed copies
+    // add theirs without a returned value, no spill (atomic_mcnt_inc)
+    int32_t mcnt_fast;
     GaterRef gt;                   // peer gater (gater.hip; gt.act == nullptr: off)
     int32_t subdyn;                // a Leave happened: a receiver drops copies of topics it left
 };
@@ -2081,10 +2092,15 @@ __global__ __launch_bounds__(256) void k_promise_insert(uint64_t* pcand, uint32_
 // change the result; fewer than 256 - kMcntSpill copies of one record arrive
 // in one launch, so the byte never carries into its neighbour.
 constexpr uint32_t kMcntSpill = 128;
-__device__ __forceinline__ void atomic_mcnt_inc(uint8_t* mcnt, int64_t ir, double* meshd, double cap)
+constexpr int kPubTicks = 16;      // publication window of the mcnt_fast bound (>= HistoryLength + 3)
+__device__ __forceinline__ void atomic_mcnt_inc(uint8_t* mcnt, int64_t ir, double* meshd, double cap, bool fast = false)
 {
     uint32_t* w = reinterpret_cast<uint32_t*>(mcnt + (ir & ~(int64_t)3));
     const int sh = (int)(ir & 3) * 8;
+    if (fast) {                      // bounded pending increments: no spill to watch for
+        __hip_atomic_fetch_add(w, 1u << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     const uint32_t old = atomicAdd(w, 1u << sh);
     if (((old >> sh) & 0xFFu) != kMcntSpill - 1u) return;
     atomicSub(w, kMcntSpill << sh);
@@ -2144,7 +2160,7 @@ __device__ __forceinline__ void listed_copy(const RoundArgs& a, uint32_t r, uint
             if (!sc) return;
             if (pen) atomicAdd(&a.invalid[ir], 1.0);
             else if (!inv && (tf & GSIM_TF_IN_MESH))         // wa: within the window
-                atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], tp->mesh_message_deliveries_cap);
+                atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], tp->mesh_message_deliveries_cap, a.mcnt_fast);
             return;
         }
     }
@@ -2190,7 +2206,7 @@ __device__ __forceinline__ void listed_copy(const RoundArgs& a, uint32_t r, uint
         atomicAdd(&a.invalid[ir], 1.0);                           // markInvalidMessageDelivery
     } else if (!inv && (tf & GSIM_TF_IN_MESH)) {
         const bool in_window = seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window) : (window >= 0);
-        if (in_window) atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], tp->mesh_message_deliveries_cap);
+        if (in_window) atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], tp->mesh_message_deliveries_cap, a.mcnt_fast);
     }
 }
 
@@ -2542,6 +2558,8 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.slot_last = d->d_slot_last;
     a.err = d->d_nresp;
     a.reuse_guard = (std::max(h->gp.history_gossip, h->gp.history_length) + d->prom_ticks + 2) * d->cfg.rounds;
+    a.mcnt_fast = !a.mlat && d->pub_bound > 0 && d->pub_bound < INT32_MAX &&
+                  (int64_t)d->pub_bound * (1 + std::max(0, h->gp.gossip_retransmission)) <= 200;
     a.sub = h->d_sub; a.score = h->d_score; a.rev = h->d_rev;
     a.flood = h->gp.flood_publish ? 1 : 0;
     a.pub_thr = h->th.publish_threshold;
@@ -3227,6 +3245,13 @@ int deliver_xbits_apply(gsim_handle* h, int64_t round, const uint64_t* in, const
     return hip_check(h, hipGetLastError(), "k_xbits_deliver");
 }
 
+// the pending meshd increments were applied (refresh, materialize_mcnt)
+void deliver_mcnt_applied(gsim_handle* h)
+{
+    Deliver* d = h->dl;
+    if (d && d->next_round >= 0) d->applied_tick = d->next_round / std::max(1, d->cfg.rounds);
+}
+
 int deliver_round_post(gsim_handle* h, int64_t round)
 {
     Deliver* d = h->dl;
@@ -3783,6 +3808,10 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     d->cfg = *cfg;
     const CellLayout layout = cell_layout(h, *cfg);
     d->tcount.assign((size_t)std::max(1, h->t), 0);
+    d->pubw.assign((size_t)kPubTicks * (size_t)std::max(1, h->t), 0);
+    d->pubw_tick.assign((size_t)kPubTicks, -1);
+    d->pub_bound = 0;
+    d->applied_tick = 0;
     const size_t ring = (size_t)cfg->ring, N = (size_t)h->n, T = (size_t)std::max(1, h->t);
     const size_t CN = N;   // every local peer has cells (a shard's ghost cells: imported first-seen rounds)
     const size_t words = (size_t)nnew_words(d);
@@ -4015,6 +4044,34 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
         e = hipMemcpyAsync(d->d_pslot, slots.data(), sizeof(uint32_t) * (size_t)count, hipMemcpyHostToDevice, h->stream);
     if (e != hipSuccess) return hip_check(h, e, "publish upload");
     for (int32_t m = 0; m < count && d->cfg.topic_slots > 0; ++m) d->tcount[msgs[m].topic]++;
+    {
+        // the publication window (RoundArgs::mcnt_fast)
+        const int64_t tick = round / std::max(1, d->cfg.rounds);
+        const size_t T = (size_t)std::max(1, h->t), row = (size_t)(tick % kPubTicks);
+        if (d->pubw_tick[row] != tick) {
+            std::fill(d->pubw.begin() + (int64_t)(row * T), d->pubw.begin() + (int64_t)((row + 1) * T), 0);
+            d->pubw_tick[row] = tick;
+        }
+        for (int32_t m = 0; m < count; ++m) d->pubw[row * T + msgs[m].topic]++;
+        // a copy of a message comes at most HistoryLength + 2 ticks after its
+        // publication (forwarded, or an IWANT answer from an mcache): the
+        // pending increments since the last application are copies of messages
+        // published after applied_tick - W
+        const int64_t W = (int64_t)h->gp.history_length + 3;
+        const int64_t from = std::min(tick, d->applied_tick) - W;
+        int32_t mx = 0;
+        if (tick - from > kPubTicks) {
+            mx = INT32_MAX;                                  // beyond the window's memory: no bound
+        } else {
+            for (size_t t = 0; t < T; ++t) {
+                int32_t sum = 0;
+                for (size_t r = 0; r < (size_t)kPubTicks; ++r)
+                    if (d->pubw_tick[r] > from) sum += d->pubw[r * T + t];
+                mx = std::max(mx, sum);
+            }
+        }
+        d->pub_bound = mx;
+    }
     ProfScope ps(h, GSIM_K_PUBLISH);
     RoundArgs a = make_round_args(h, round);
     const int64_t per_block = 256 * 16;

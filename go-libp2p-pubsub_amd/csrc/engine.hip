@@ -778,7 +778,11 @@ template <bool REFRESH, bool SCORE>
 static void launch_score_kernel(gsim_handle* h, const ScoreArgs& a)
 {
     ProfScope ps(h, REFRESH ? GSIM_K_REFRESH_SCORE : GSIM_K_SCORE);
-    hipLaunchKernelGGL((k_refresh_score<REFRESH, SCORE>), dim3(grid_for(h->e)), dim3(256), 0, h->stream, a);
+#ifndef GSIM_REFRESH_GRID
+#define GSIM_REFRESH_GRID 16384
+#endif
+    hipLaunchKernelGGL((k_refresh_score<REFRESH, SCORE>), dim3(grid_for(h->e, 256, GSIM_REFRESH_GRID)), dim3(256), 0,
+                       h->stream, a);
 }
 
 int launch_refresh_scores(gsim_handle* h, int64_t now)
@@ -816,6 +820,7 @@ int launch_refresh_scores(gsim_handle* h, int64_t now)
     h->mt_lazy = true;
     h->mt_R = now;
     h->mcnt_dirty = false;   // the score pass settled every pending count
+    deliver_mcnt_applied(h);
     h->score_version++;
     return hip_check(h, hipGetLastError(), "k_refresh_score");
 }
@@ -852,6 +857,7 @@ int materialize_mcnt(gsim_handle* h)
     ScoreArgs a = make_score_args(h, 0);
     hipLaunchKernelGGL(k_apply_mcnt, dim3(grid_for(h->e * (int64_t)std::max(1, h->S))), dim3(256), 0, h->stream, a);
     h->mcnt_dirty = false;
+    deliver_mcnt_applied(h);
     return hip_check(h, hipGetLastError(), "k_apply_mcnt");
 }
 

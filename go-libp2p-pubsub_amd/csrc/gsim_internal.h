@@ -655,6 +655,7 @@ int deliver_frontier_export(gsim_handle* h, int64_t round, uint64_t* out, uint32
                             bool append = false);
 int deliver_xbits_apply(gsim_handle* h, int64_t round, const uint64_t* in, const gsim::XSrc* d_src, int K, int64_t ntask);
 int deliver_holder_accum(gsim_handle* h, int64_t round);
+void deliver_mcnt_applied(gsim_handle* h);
 int deliver_holder_gather(gsim_handle* h, int parity);
 int deliver_holder_import(gsim_handle* h, int64_t round, const uint64_t* in, const gsim::HSrc* d_src, int K,
                           int64_t ntask, int64_t fr);

@@ -1092,7 +1092,10 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
 // rows: the observers of one row-length class (a list), or nullptr for the
 // nrows observers from obs_base on.
 template <int W>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W == 16 ? 3 : 4)))   // W = 16: 3 waves per SIMD, else 4
+#ifndef GSIM_HB_WPE
+#define GSIM_HB_WPE 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W == 16 ? 3 : GSIM_HB_WPE)))   // W = 16: 3 waves per SIMD, else 4
 void k_heartbeat(HbArgs a, const uint32_t* rows, int64_t nrows, int64_t obs_base)
 {
     constexpr int G = 64 / W;
