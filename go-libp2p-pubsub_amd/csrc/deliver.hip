@@ -1261,6 +1261,7 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
                 if constexpr (LAT) vq_push_wave(a, qpl, qv);
             }
         }
+        if constexpr (!SP) return;                        // dense: a launch covers every word
     }
 }
 
@@ -2799,7 +2800,10 @@ int deliver_flush(gsim_handle* h)
     if (!d || d->pending < 0) return GSIM_OK;
     ProfScope ps(h, GSIM_K_COMMIT);
     RoundArgs a = make_round_args(h, d->pending);
-    const dim3 grid(std::min(grid_peers((int64_t)a.rhi - ((int64_t)a.rlo & ~63ll)), 8192));
+    // member-compacted cells: a capped grid (the scan usually exits at once: the
+    // claim list covers the round); dense: a wave per word
+    const int gp = grid_peers((int64_t)a.rhi - ((int64_t)a.rlo & ~63ll));
+    const dim3 grid(sparse_layout(h) ? std::min(gp, 8192) : gp);
     if (a.clist)
         hipLaunchKernelGGL(k_commit_list<true>, dim3(64, kClSub), dim3(256), 0, h->stream, a);
     if (a.mlat)

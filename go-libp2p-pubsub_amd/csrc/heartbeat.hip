@@ -1094,12 +1094,13 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
 template <int W>
 // waves per SIMD the register budget is fitted to: 5 for W = 32 / 64 (C3's
 // k_heartbeat<32>: 96 VGPRs with 10 spilled, 7.91 -> 6.81 ms per tick against 4
-// waves at 106, gpurun_out/r04pab), 3 for W = 16
+// waves at 106, 7.13 at 6; gpurun_out/r04pab, r04q), 4 for W = 16 (c5's
+// heartbeat 116.8 -> 114.1 ms per tick against 3, r04qc5)
 #ifndef GSIM_HB_WPE
 #define GSIM_HB_WPE 5
 #endif
 #ifndef GSIM_HB_WPE16
-#define GSIM_HB_WPE16 3
+#define GSIM_HB_WPE16 4
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W == 16 ? GSIM_HB_WPE16 : GSIM_HB_WPE)))
 void k_heartbeat(HbArgs a, const uint32_t* rows, int64_t nrows, int64_t obs_base)
