@@ -1596,11 +1596,13 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
         ShardCtx* s = h->sh;
         if (!px_enabled(h)) continue;
         (void)hipSetDevice(h->device);
-        // a tick's PX lists to one shard: PrunePeers entries per cross edge into it
-        // (an overflow fails gsim_group_px_connect)
+        // a tick's PX lists to one shard: PrunePeers entries per cross edge into it,
+        // four PX PRUNEs per cross edge and tick (the heartbeat's and the two
+        // control rounds' GRAFT replies, of several topics: c5's hubs overflowed
+        // one; an overflow fails gsim_group_px_connect)
         int64_t xmax = 0;
         for (int q = 0; q < K; ++q) xmax = std::max<int64_t>(xmax, s->xoff[(size_t)q + 1] - s->xoff[(size_t)q]);
-        s->pxcap = std::max<int64_t>(1 << 16, (int64_t)std::max(1, h->gp.prune_peers) * xmax);
+        s->pxcap = std::max<int64_t>(1 << 16, 4 * (int64_t)std::max(1, h->gp.prune_peers) * xmax);
         if ((rc = dalloc(h, &s->d_pxout, (size_t)(K * s->pxcap))) || (rc = dalloc(h, &s->d_pxcnt, (size_t)K + 1)))
             return g->take(h, rc);
         if (hipMemset(s->d_pxcnt, 0, sizeof(uint32_t) * ((size_t)K + 1)) != hipSuccess)
