@@ -2485,10 +2485,12 @@ static bool sparse_layout(const gsim_handle* h)
 
 bool deliver_latency_on(gsim_handle* h) { return h->dl && h->dl->lat_on; }
 
-// Member-major IHAVE passes: member lists of a sub-ring layout, single engine
+// Member-major IHAVE passes: member lists of a sub-ring layout (a shard's
+// members include its ghosts: their ghost rows hold their gossip marks into
+// the shard, their cells the holdings their shards exported)
 static bool mm_gossip(const gsim_handle* h)
 {
-    return h->dl && h->dl->d_mmtab && h->dl->sparse != 0 && !h->sh;
+    return h->dl && h->dl->d_mmtab && h->dl->sparse != 0;
 }
 
 // Commits from the claim list: member-compacted cells (sub-rings of topics
