@@ -124,12 +124,17 @@ int gsim_shard_partition(int64_t n, const uint32_t* row_ptr, const uint64_t* sub
 {
     if (n <= 0 || !row_ptr || !bounds || shards < 1 || shards > GSIM_MAX_SHARDS) return GSIM_EINVAL;
     if (n < 64 * (int64_t)shards) return GSIM_ERANGE;    // ranges are whole 64-peer words
-    // weight of a peer: its records (row length x joined topics) + 1
+    // weight of a peer, per joined topic: its records (row length), a lane
+    // group's worth of heartbeat per observer (16 positions), and for a hub
+    // row the block-wide selections and PX lists that grow with its length
+    // (d^2 / 512: c5's Chung-Lu hubs, all in the lowest ids, made shard 0 the
+    // slowest at K = 8 under the records alone)
     std::vector<double> cum((size_t)n + 1, 0.0);
     for (int64_t i = 0; i < n; ++i) {
         const double d = (double)(row_ptr[i + 1] - row_ptr[i]);
         const double s = sub ? (double)__builtin_popcountll(sub[i]) : 1.0;
-        cum[(size_t)i + 1] = cum[(size_t)i] + d * std::max(1.0, s) + 1.0;
+        const double hub = d > 64.0 ? d * d / 512.0 : 0.0;
+        cum[(size_t)i + 1] = cum[(size_t)i] + std::max(1.0, s) * (d + 16.0 + hub) + 1.0;
     }
     bounds[0] = 0;
     for (int32_t s = 1; s < shards; ++s) {

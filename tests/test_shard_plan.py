@@ -14,9 +14,12 @@ from gsim.engine import Network, random_regular
 
 
 def _weights(net):
-    d = np.diff(net.row_ptr.astype(np.int64))
-    s = np.array([bin(int(x)).count("1") for x in net.sub], dtype=np.int64)
-    return d * np.maximum(s, 1) + 1
+    """gsim_shard_partition's peer weight (shard_plan.cpp): per joined topic the
+    row length, 16 for the observer's lane group, d^2 / 512 for a hub row."""
+    d = np.diff(net.row_ptr.astype(np.int64)).astype(np.float64)
+    s = np.array([bin(int(x)).count("1") for x in net.sub], dtype=np.float64)
+    hub = np.where(d > 64, d * d / 512.0, 0.0)
+    return np.maximum(s, 1) * (d + 16.0 + hub) + 1.0
 
 
 @pytest.mark.parametrize("K", [1, 2, 3, 4, 8])
