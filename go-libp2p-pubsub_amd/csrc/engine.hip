@@ -729,9 +729,33 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     return a;
 }
 
+// Whether an IP id is listed by two different peers (ip_ptr CSR over n peers).
+static bool ips_shared(int64_t n, const uint32_t* ip_ptr, const uint32_t* ip_ids, uint32_t n_ips)
+{
+    if (!ip_ptr || !ip_ids || n_ips == 0) return false;
+    std::vector<int64_t> owner((size_t)n_ips, -1);
+    for (int64_t i = 0; i < n; ++i)
+        for (uint32_t q = ip_ptr[i]; q < ip_ptr[i + 1]; ++q) {
+            int64_t& o = owner[ip_ids[q]];
+            if (o >= 0 && o != i) return true;
+            o = i;
+        }
+    return false;
+}
+
 int launch_ip_colocation(gsim_handle* h, const int32_t* gate)
 {
     ProfScope ps(h, GSIM_K_IP_COLOCATION);
+    if (!h->ip_shared && h->pp.ip_colocation_factor_threshold >= 1) {
+        // every IP is one peer's: peersInIP - threshold <= 0 for every record
+        // (score.go:426-446), P6 = 0 -- as the scan computes, without it (c5
+        // with one IP per peer: 11 ms per tick)
+        hipError_t e = hipMemsetAsync(h->d_p6, 0, sizeof(double) * (size_t)h->e, h->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(h->d_p6row, 0, (size_t)h->n, h->stream);
+        h->p6_dirty = false;
+        h->p6_rows_only = false;
+        return hip_check(h, e, "P6 (no shared IP)");
+    }
     ColocArgs c{};
     c.gate = gate;
     c.E = h->e; c.row_ptr = h->d_row_ptr; c.col = h->d_col; c.rev = h->d_rev; c.owner = h->d_owner;
@@ -1309,6 +1333,7 @@ int gsim_load_graph(gsim_handle* h, int64_t n, const uint32_t* row_ptr, const ui
     }
     if (outbound) up(h->d_outbound, outbound, (size_t)E); else zero(h->d_outbound, (size_t)E);
     zero(h->d_direct, (size_t)E);
+    h->ip_shared = ips_shared(n, ip_ptr, ip_ids, n_ips);
     if (ip_ptr) {
         up(h->d_ip_ptr, ip_ptr, sizeof(uint32_t) * (size_t)(n + 1));
         up(h->d_ip_ids, ip_ids, sizeof(uint32_t) * (size_t)nip);
@@ -1408,6 +1433,7 @@ int gsim_set_ips(gsim_handle* h, const uint32_t* ip_ptr, const uint32_t* ip_ids,
     if (e == hipSuccess && nip) e = hipMemcpyAsync(h->d_ip_ids, ip_ids, sizeof(uint32_t) * (size_t)nip, hipMemcpyHostToDevice, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     h->p6_dirty = true; h->p6_rows_only = false;
+    h->ip_shared = ips_shared(n, ip_ptr, ip_ids, n_ips);
     return hip_check(h, e, "gsim_set_ips");
 }
 

@@ -445,6 +445,9 @@ struct gsim_handle {
     // only the rows flagged in d_p6row changed (churn, retention purges): the
     // P6 pass re-derives those; false: every row (graph, IPs, whitelist, writes)
     bool p6_rows_only = false;
+    // some IP is held by two local peers (gsim_set_ips / load): otherwise every
+    // peersInIP is 1 and P6 is 0 everywhere (launch_ip_colocation)
+    bool ip_shared = false;
     bool maybe_retained = false;
     // Every record of a topic its observer did not join is zero (true after
     // gsim_load_graph and gsim_fill_synthetic, false after any state write
