@@ -1076,18 +1076,32 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
 #ifdef GSIM_DIAG_NO_SEEN
                             // diagnostic build (timing only, wrong results): every receiver is
                             // an earlier-round duplicate, no seen-set access
-                            const bool known = true;
+                            const bool sbit = true;
                             (void)s_bm; (void)bw;
 #else
-                            const bool known = ((s_bm[bw] >> (i & 63)) & 1ull) &&
-                                               (L ? (!scored_t || (inv && !pen))
-                                                  : (s_wa[k] || !sc || inv || !(tf & GSIM_TF_IN_MESH)));
+                            const bool sbit = (s_bm[bw] >> (i & 63)) & 1ull;   // committed before this round
 #endif
+                            const bool known = sbit && (L ? (!scored_t || (inv && !pen))
+                                                          : (s_wa[k] || !sc || inv || !(tf & GSIM_TF_IN_MESH)));
                             // the receiver's cell (a member of t: mesh, direct, fanout and flood
                             // targets all hold the topic, §2); -1 cannot happen
                             const int64_t ci = known ? 0 : SP ? a.cs.at((int64_t)s_cb[k], t, i) : (int64_t)m * a.cs.n + i;
                             if (SP && ci < 0) continue;
-                            const uint64_t c = known ? 0ull : TM_LDC(a.cs.cell[ci]);
+                            uint32_t lo_w = j;
+                            if (sc && !inv) {
+                                lo_w |= kCreditFirst;
+                                if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo_w |= kCreditMesh;
+                            }
+                            const uint64_t cv = ((uint64_t)(claim_hi | e) << 32) | lo_w;
+                            // a receiver that had not seen m before this round (no claims of
+                            // round g-1 remain without a latency): the claim is the cell's only
+                            // access -- atomicMin keeps a lower edge's claim of this round and
+                            // returns what the cell held (a load, then the claim, otherwise)
+                            const bool fold = !LAT && !sbit && seeable;
+                            const uint64_t c = known ? 0ull
+                                             : fold ? __hip_atomic_fetch_min(a.cs.cell + ci, cv, __ATOMIC_RELAXED,
+                                                                             __HIP_MEMORY_SCOPE_AGENT)
+                                                    : TM_LDC(a.cs.cell[ci]);
                             const uint32_t chi = (uint32_t)(c >> 32);
                             // the round validation completed (or completes) in; -1: unclaimed
                             // or claimed in this round
@@ -1097,15 +1111,10 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
                                 if (!(chi & kClaim)) seen_round = chi;
                                 else if (((chi >> 30) & 1u) != par) seen_round = a.g - 1 + L;
                             }
-                            if (seeable && seen_round < 0 && (c == kUnseen64 || (chi & kEdgeMask) > e)) {
-                                uint32_t lo_w = j;
-                                if (sc && !inv) {
-                                    lo_w |= kCreditFirst;
-                                    if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo_w |= kCreditMesh;
-                                }
-                                const uint64_t cv = ((uint64_t)(claim_hi | e) << 32) | lo_w;
-                                const uint64_t prev = __hip_atomic_fetch_min(a.cs.cell + ci, cv, __ATOMIC_RELAXED,
-                                                                             __HIP_MEMORY_SCOPE_AGENT);
+                            if (fold || (seeable && seen_round < 0 && (c == kUnseen64 || (chi & kEdgeMask) > e))) {
+                                const uint64_t prev = fold ? c
+                                                           : __hip_atomic_fetch_min(a.cs.cell + ci, cv, __ATOMIC_RELAXED,
+                                                                                    __HIP_MEMORY_SCOPE_AGENT);
                                 if (prev == kUnseen64) {
                                     n_first++;
                                     clm |= 1ull << k;
