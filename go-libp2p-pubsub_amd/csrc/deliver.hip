@@ -1213,7 +1213,10 @@ __global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs 
 
 // Commit every claim of round g (markSeen + P2 credit) before the state is
 // read or changed by anything but the next round.
-template <bool LAT, bool SP, bool GT = false>
+// SPLIT (a shard's few words: a wave per word leaves the CUs idle): the slot
+// batches dealt over gridDim.y, a claim's record credit and lastput atomic
+// (two slots of one sender can credit the same record)
+template <bool LAT, bool SP, bool GT = false, bool SPLIT = false>
 __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
 {
     extern __shared__ uint16_t s_act[];
@@ -1230,7 +1233,8 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
         const int64_t i = i0 + lane;
         const bool vi = i < a.CN;
         const uint32_t par = (uint32_t)(a.g & 1);
-        for (int k0 = 0; k0 < nact; k0 += kSlotBatch) {
+        for (int k0 = SPLIT ? (int)blockIdx.y * kSlotBatch : 0; k0 < nact;
+             k0 += (SPLIT ? (int)gridDim.y : 1) * kSlotBatch) {
             uint64_t cv[kSlotBatch];
             int64_t ci[SP ? kSlotBatch : 1];   // the dense layout recomputes m * N + i
 #pragma unroll
@@ -1265,7 +1269,7 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
                 if (is_claim_of(cv[b], par)) {
                     const uint32_t m = s_act[k];
                     uint64_t* cp = a.cs.cell + (SP ? ci[b] : (int64_t)m * a.cs.n + i);
-                    commit_claim<false, LAT, SP, GT>(a, cp, cv[b], a.g, m, i, &qpl, &qv);
+                    commit_claim<SPLIT, LAT, SP, GT>(a, cp, cv[b], a.g, m, i, &qpl, &qv);
                 }
                 if constexpr (LAT) vq_push_wave(a, qpl, qv);
             }
@@ -2815,6 +2819,8 @@ int deliver_flush(gsim_handle* h)
     // claim list covers the round); dense: a wave per word
     const int gp = grid_peers((int64_t)a.rhi - ((int64_t)a.rlo & ~63ll));
     const dim3 grid(sparse_layout(h) ? std::min(gp, 8192) : gp);
+    // a shard's few words (< 2^14, dense, no latency or gater): 4 slot groups
+    const bool split = gp < 4096 && h->sh && !a.mlat && !a.gt.act && !sparse_layout(h);
     if (a.clist)
         hipLaunchKernelGGL(k_commit_list<true>, dim3(64, kClSub), dim3(256), 0, h->stream, a);
     if (a.mlat)
@@ -2825,6 +2831,9 @@ int deliver_flush(gsim_handle* h)
         hipLaunchKernelGGL((k_commit<false, false, true>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     else if (sparse_layout(h))
         hipLaunchKernelGGL((k_commit<false, true>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
+    else if (split)
+        hipLaunchKernelGGL((k_commit<false, false, false, true>), dim3(gp, 4), dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t),
+                           h->stream, a);
     else
         hipLaunchKernelGGL((k_commit<false, false>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     const int64_t committed = d->pending;
