@@ -139,7 +139,10 @@ namespace {
 
 constexpr int64_t kSecond = 1000000000LL;
 constexpr int64_t kBackoffSlack = 2 * kSecond;   // 2*GossipSubHeartbeatInterval (gossipsub.go:1638)
-constexpr int kFlagChunk = 8;                    // topics whose flags are loaded together
+#ifndef GSIM_FLAG_CHUNK
+#define GSIM_FLAG_CHUNK 8
+#endif
+constexpr int kFlagChunk = GSIM_FLAG_CHUNK;      // topics whose flags are loaded together
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
