@@ -697,8 +697,18 @@ constexpr int kTsSlots = 64;
 #ifndef GSIM_TM_MINB
 #define GSIM_TM_MINB 1       // waves per SIMD the register budget is fitted to
 #endif
+// threads per dense k_send_tm block, and its waves per SIMD: 512 threads at 6
+// waves (80 VGPRs, 11 spilled; 3 blocks per CU) against 1024 at 4 (1 block): C3
+// send 15.25 -> 13.56 ms per tick, 256 at 6: 15.68 (gpurun_out/r04ab2, one box).
+// The walk waits on its dependent trips; more resident waves hide more of them.
 #ifndef GSIM_TM_TB
-#define GSIM_TM_TB 1024      // threads per k_send_tm block
+#define GSIM_TM_TB 512
+#endif
+#ifndef GSIM_TM_MINB_DENSE
+#define GSIM_TM_MINB_DENSE 6
+#endif
+#ifndef GSIM_TM_MINB_SPARSE
+#define GSIM_TM_MINB_SPARSE 1
 #endif
 // GSIM_TM_NT (A/B builds): the forwarders' row fields and the receivers' cells
 // are loaded non-temporal, so the L2 keeps the slots' committed bitmaps
@@ -712,7 +722,7 @@ constexpr int kTsSlots = 64;
 #else
 #define TM_LDC(x) (x)
 #endif
-constexpr int kPushTB = GSIM_TM_TB;  // ... of a shard's push walk (512: 21 against 18.5 ms per shard at K = 8)
+constexpr int kPushTB = 1024;        // ... of a shard's push walk (512: 21 against 18.5 ms per shard at K = 8)
 // ... with member-compacted cells (sparse frontiers: many topics, each block's
 // chunks hold few forwarders): c5 send 184 / 151 / 158 ms per tick at 1024 / 512 /
 // 256 threads (gpurun_out/r04n); dense C3 is fastest at 1024 (§4.2)
@@ -723,7 +733,11 @@ constexpr int kTmTabMin = 256;      // forwarders in a chunk from which the tabl
 // SP: topic slots or member-compacted cells are in use (gsim_internal.h); the
 // dense instance indexes plane t and cell m * N + p with no table reads.
 template <int kTmThreads, bool LAT, bool SP, bool GT = false, bool PUSH = false>
-__global__ __launch_bounds__(kTmThreads, GSIM_TM_MINB) void k_send_tm(RoundArgs a_)
+__global__ __launch_bounds__(kTmThreads, PUSH ? GSIM_TM_MINB
+                                        : (!SP && kTmThreads == GSIM_TM_TB) ? GSIM_TM_MINB_DENSE
+                                        : (SP && !LAT && kTmThreads == kSparseTB) ? GSIM_TM_MINB_SPARSE
+                                                                                   : GSIM_TM_MINB)
+void k_send_tm(RoundArgs a_)
 {
     const RoundArgs& a = a_;
     extern __shared__ uint64_t s_dyn[];
