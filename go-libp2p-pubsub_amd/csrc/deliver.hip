@@ -722,7 +722,13 @@ constexpr int kTsSlots = 64;
 #else
 #define TM_LDC(x) (x)
 #endif
-constexpr int kPushTB = 1024;        // ... of a shard's push walk (512: 21 against 18.5 ms per shard at K = 8)
+#ifndef GSIM_TM_PUSH_TB
+#define GSIM_TM_PUSH_TB 1024
+#endif
+#ifndef GSIM_TM_MINB_PUSH
+#define GSIM_TM_MINB_PUSH GSIM_TM_MINB
+#endif
+constexpr int kPushTB = GSIM_TM_PUSH_TB;  // ... of a shard's push walk (512 at 1 wave: 21 against 18.5 ms per shard at K = 8)
 // ... with member-compacted cells (sparse frontiers: many topics, each block's
 // chunks hold few forwarders): c5 send 184 / 151 / 158 ms per tick at 1024 / 512 /
 // 256 threads (gpurun_out/r04n); dense C3 is fastest at 1024 (§4.2)
@@ -733,7 +739,7 @@ constexpr int kTmTabMin = 256;      // forwarders in a chunk from which the tabl
 // SP: topic slots or member-compacted cells are in use (gsim_internal.h); the
 // dense instance indexes plane t and cell m * N + p with no table reads.
 template <int kTmThreads, bool LAT, bool SP, bool GT = false, bool PUSH = false>
-__global__ __launch_bounds__(kTmThreads, PUSH ? GSIM_TM_MINB
+__global__ __launch_bounds__(kTmThreads, PUSH ? GSIM_TM_MINB_PUSH
                                         : (!SP && kTmThreads == GSIM_TM_TB) ? GSIM_TM_MINB_DENSE
                                         : (SP && !LAT && kTmThreads == kSparseTB) ? GSIM_TM_MINB_SPARSE
                                                                                    : GSIM_TM_MINB)
@@ -3180,7 +3186,10 @@ __global__ __launch_bounds__(256) void k_xbits_gather(const uint32_t* nnew, int3
 // in LDS), so neighbouring lanes touch neighbouring records.
 constexpr int kXbList = 1024;                // per-wave LDS list of a task's copies
 
-__global__ __launch_bounds__(256) void k_xbits_deliver(RoundArgs a_, const uint64_t* in, const XSrc* src, int32_t K,
+#ifndef GSIM_XB_WPE
+#define GSIM_XB_WPE 1
+#endif
+__global__ __launch_bounds__(256, GSIM_XB_WPE) void k_xbits_deliver(RoundArgs a_, const uint64_t* in, const XSrc* src, int32_t K,
                                                        int64_t ntask, const uint32_t* owner)
 {
     const RoundArgs& a = a_;
