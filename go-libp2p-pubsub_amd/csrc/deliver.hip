@@ -1558,8 +1558,11 @@ __global__ __launch_bounds__(256) void k_gossip_count_mm(IhArgs a, const uint32_
         if (s_c[w]) atomicAdd(&gcount[(w < R ? 0 : a.ring - R) + m_lo + w], s_c[w]);
 }
 
+#ifndef GSIM_IH_WPE
+#define GSIM_IH_WPE 1
+#endif
 template <int W, bool LAT, bool SP, bool MM = false>
-__global__ __launch_bounds__(256) void k_ihave(IhArgs a_, const uint32_t* gcount)
+__global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, const uint32_t* gcount)
 {
     const IhArgs& a = a_;
     extern __shared__ uint16_t s_act[];   // [ring] candidate slots (bit 15: push), then response staging
