@@ -60,7 +60,10 @@ __device__ __forceinline__ bool verdict_penalises(uint8_t v)
 {
     return v == GSIM_VERDICT_REJECT || v == GSIM_VERDICT_SIGNATURE;
 }
-constexpr int kSlotBatch = 8;      // active slots whose cells are loaded together
+#ifndef GSIM_SLOT_BATCH
+#define GSIM_SLOT_BATCH 8
+#endif
+constexpr int kSlotBatch = GSIM_SLOT_BATCH;      // active slots whose cells are loaded together
 constexpr int kClSub = 64;
 constexpr int kClStride = 32;       // u32s between two claim sub-list counters (own cache lines)
 constexpr int kHubMesh = 16;       // mesh | direct edges listed per (hub, topic); more: the whole row is walked
