@@ -493,6 +493,7 @@ struct WaveGroup {
     __device__ View<T> view(const T* v) const { return View<T>{v[0], base}; }
     template <int SLOT>
     __device__ BoolView view_b(const bool* v) const { return BoolView{__ballot(v[0]), base}; }
+    static constexpr bool kList = false;  // rank loops over every position (shuffles: the whole group)
     // the value at the lowest position where p holds (p must hold somewhere)
     __device__ double at_lowest(const bool* p, const double* v) const
     {
@@ -533,6 +534,8 @@ struct BlockGroup {
         double d0[P];
         uint64_t u0[P], u1[P];
         int32_t i0[P];
+        int32_t l0[P];                     // each(): positions where a predicate holds
+        int ln;
         uint8_t b0[P], b1[P];
     };
     Shared* sh;
@@ -687,6 +690,23 @@ struct BlockGroup {
         for (int x = 0; x < V; ++x) buf[pos(x)] = v[x] ? 1 : 0;
         __syncthreads();
         return View<uint8_t>{buf};
+    }
+    // f(q) for the positions q where p holds, in no particular order: a hub's
+    // rank loops count over its mesh, not its whole row (c5's hubs: rows of
+    // thousands, meshes of tens)
+    static constexpr bool kList = true;
+    template <class F>
+    __device__ void each(const bool* p, F f)
+    {
+        __syncthreads();                    // earlier readers of the list are done
+        if (tid == 0) sh->ln = 0;
+        __syncthreads();
+#pragma unroll
+        for (int x = 0; x < V; ++x)
+            if (p[x]) sh->l0[atomicAdd(&sh->ln, 1)] = pos(x);
+        __syncthreads();
+        const int n = sh->ln;
+        for (int j = 0; j < n; ++j) f(sh->l0[j]);
     }
     __device__ double at_lowest(const bool* p, const double* v)
     {
@@ -889,13 +909,24 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
                     const auto vm = g.template view_b<0>(m);
                     const auto vs = g.template view<0>(S);
                     const auto vk = g.template view<0>(k1);
-                    for (int q = 0; q < g.span(); ++q) {
-                        const double sq = vs[q];
-                        const uint64_t kq = vk[q];
-                        const bool mq = vm[q];
+                    if constexpr (Grp::kList) {
+                        g.each(m, [&](int q) {   // mesh positions: the only ones that count
+                            const double sq = vs[q];
+                            const uint64_t kq = vk[q];
+                            const bool mq = vm[q];
 #pragma unroll
-                        for (int v = 0; v < V; ++v)
-                            if (mq && (sq > S[v] || (sq == S[v] && kq < k1[v]))) ++rank1[v];
+                            for (int v = 0; v < V; ++v)
+                                if (mq && (sq > S[v] || (sq == S[v] && kq < k1[v]))) ++rank1[v];
+                        });
+                    } else {
+                        for (int q = 0; q < g.span(); ++q) {
+                            const double sq = vs[q];
+                            const uint64_t kq = vk[q];
+                            const bool mq = vm[q];
+#pragma unroll
+                            for (int v = 0; v < V; ++v)
+                                if (mq && (sq > S[v] || (sq == S[v] && kq < k1[v]))) ++rank1[v];
+                        }
                     }
                 }
                 const int ds = a.Dscore < l ? a.Dscore : l;
@@ -909,11 +940,20 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
                 // divergent branch would read inactive lanes)
                 {
                     const auto vk2 = g.template view<1>(k2);
-                    for (int q = 0; q < g.span(); ++q) {
-                        const uint64_t kq = vk2[q];
+                    if constexpr (Grp::kList) {
+                        g.each(m, [&](int q) {   // mesh positions: the only ones that count
+                            const uint64_t kq = vk2[q];
 #pragma unroll
-                        for (int v = 0; v < V; ++v)
-                            if (kq < k2[v]) ++below[v];   // non-tail positions hold ~0 and never count
+                            for (int v = 0; v < V; ++v)
+                                if (kq < k2[v]) ++below[v];   // non-tail positions hold ~0 and never count
+                        });
+                    } else {
+                        for (int q = 0; q < g.span(); ++q) {
+                            const uint64_t kq = vk2[q];
+#pragma unroll
+                            for (int v = 0; v < V; ++v)
+                                if (kq < k2[v]) ++below[v];   // non-tail positions hold ~0 and never count
+                        }
                     }
                 }
                 // Keep plst[:D] after Go's Dout rotation (1457-1485), computed
@@ -945,13 +985,25 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
                         const auto vrest = g.template view_b<0>(rest);
                         const auto vcb = g.template view_b<1>(cb);
                         const auto vp = g.template view<0>(p);
-                        for (int q = 0; q < g.span(); ++q) {
-                            const int pq = vp[q];
-                            const bool cq = vcb[q], rq = vrest[q];
+                        if constexpr (Grp::kList) {
+                            g.each(m, [&](int q) {   // mesh positions: the only ones that count
+                                const int pq = vp[q];
+                                const bool cq = vcb[q], rq = vrest[q];
 #pragma unroll
-                            for (int v = 0; v < V; ++v) {
-                                if (cq && pq < p[v]) ++rb[v];
-                                if (rq && pq > p[v]) ++rr[v];
+                                for (int v = 0; v < V; ++v) {
+                                    if (cq && pq < p[v]) ++rb[v];
+                                    if (rq && pq > p[v]) ++rr[v];
+                                }
+                            });
+                        } else {
+                            for (int q = 0; q < g.span(); ++q) {
+                                const int pq = vp[q];
+                                const bool cq = vcb[q], rq = vrest[q];
+#pragma unroll
+                                for (int v = 0; v < V; ++v) {
+                                    if (cq && pq < p[v]) ++rb[v];
+                                    if (rq && pq > p[v]) ++rr[v];
+                                }
                             }
                         }
                     }
@@ -996,12 +1048,22 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
                 {
                     const auto vm = g.template view_b<0>(m);
                     const auto vs = g.template view<0>(S);
-                    for (int q = 0; q < g.span(); ++q) {
-                        const double sq = vs[q];
-                        const bool mq = vm[q];
+                    if constexpr (Grp::kList) {
+                        g.each(m, [&](int q) {   // mesh positions: the only ones that count
+                            const double sq = vs[q];
+                            const bool mq = vm[q];
 #pragma unroll
-                        for (int v = 0; v < V; ++v)
-                            if (mq && (sq < S[v] || (sq == S[v] && q < gl[v]))) ++rank[v];
+                            for (int v = 0; v < V; ++v)
+                                if (mq && (sq < S[v] || (sq == S[v] && q < gl[v]))) ++rank[v];
+                        });
+                    } else {
+                        for (int q = 0; q < g.span(); ++q) {
+                            const double sq = vs[q];
+                            const bool mq = vm[q];
+#pragma unroll
+                            for (int v = 0; v < V; ++v)
+                                if (mq && (sq < S[v] || (sq == S[v] && q < gl[v]))) ++rank[v];
+                        }
                     }
                 }
                 bool atm[V];
