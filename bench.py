@@ -220,19 +220,32 @@ def churn_schedule(net, frac: float, ticks: range, seed: int = 4) -> dict:
     return out
 
 
+CALLTIME = None      # --calltime: wall ms per engine call (each one synchronised; diagnostic only)
+
+
+def _timed(name, f, *a, **kw):
+    if CALLTIME is None:
+        return f(*a, **kw)
+    t0 = time.perf_counter()
+    r = f(*a, **kw)
+    CALLTIME["_eng"].synchronize()
+    CALLTIME[name] = CALLTIME.get(name, 0.0) + (time.perf_counter() - t0) * 1e3
+    return r
+
+
 def run_tick(eng, k, sched, churn=None, px=False):
     now = tick_time(k)
     for (pairs, up) in (churn or {}).get(k, []):
-        eng.set_connections(pairs, up=up, now=now - SECOND // 2)
-    eng.refresh_scores(now)
-    eng.heartbeat(k, now)
+        _timed("set_connections", eng.set_connections, pairs, up=up, now=now - SECOND // 2)
+    _timed("refresh_scores", eng.refresh_scores, now)
+    _timed("heartbeat", eng.heartbeat, k, now)
     for g in range(k * ROUNDS, (k + 1) * ROUNDS):
         m = sched.get(g)
         if m is not None:
-            eng.publish_array(m, g)
-        eng.round(g)
+            _timed("publish", eng.publish_array, m, g)
+        _timed("round", eng.round, g)
     if px:                                     # the connector for this tick's PX attempts
-        eng.px_connect(now + SECOND // 2)
+        _timed("px_connect", eng.px_connect, now + SECOND // 2)
 
 
 def cpu_baseline(cfg, scen=None, n: int = 10_000, ticks: int = 5, budget_s: float = 25.0, warmup: int = 1,
@@ -359,6 +372,8 @@ def main():
                     help="validation latency of every message in rounds (gsim_msg.vdelay)")
     ap.add_argument("--replicas", action="store_true",
                     help="N > 1: one independent network per rank (weak scaling) instead of one sharded network")
+    ap.add_argument("--calltime", action="store_true",
+                    help="diagnostic: print the wall ms per tick of each engine call (synchronised) to stderr")
     ap.add_argument("--peers", type=int, default=None,
                     help="peers of the config's network (its default otherwise): a reduced shape, e.g. c5 split "
                          "into 8 shards on one GPU, whose ghost rows would not fit its HBM at 10M peers")
@@ -449,6 +464,9 @@ def main():
     barrier()
     eng.profile(True)
     eng.synchronize()
+    global CALLTIME
+    if args.calltime:
+        CALLTIME = {"_eng": eng}
     t0 = time.perf_counter()
     for s in range(args.steps):
         kk += 1
@@ -456,6 +474,10 @@ def main():
     eng.synchronize()
     barrier()
     wall = time.perf_counter() - t0
+    if CALLTIME is not None:
+        print(json.dumps({"calltime_ms_per_tick": {c: v / args.steps for c, v in CALLTIME.items() if c != "_eng"}}),
+              file=sys.stderr)
+        CALLTIME = None
     per_shard = None
     if shard is not None and world == 1:          # in-process shards: each one's kernel time
         per_shard = eng.profile_read_shards()

@@ -679,7 +679,7 @@ void free_graph(gsim_handle* h)
     dfree(h->d_ip_ptr); dfree(h->d_ip_ids); dfree(h->d_ip_white); dfree(h->d_p5);
     dfree(h->d_first); dfree(h->d_meshd); dfree(h->d_fail); dfree(h->d_invalid);
     dfree(h->d_graft); dfree(h->d_mtime); dfree(h->d_tflags); dfree(h->d_mflags);
-    dfree(h->d_bp); dfree(h->d_estate); dfree(h->d_expire); dfree(h->d_p6); dfree(h->d_p6row); dfree(h->d_churn); h->churn_cap = 0; dfree(h->d_score);
+    dfree(h->d_bp); dfree(h->d_estate); dfree(h->d_expire); dfree(h->d_p6); dfree(h->d_p6row); dfree(h->d_churn); h->churn_cap = 0; dfree(h->d_churn_mark); dfree(h->d_score);
     dfree(h->d_backoff); dfree(h->d_rstate); dfree(h->d_dstate); dfree(h->d_mcnt); dfree(h->d_pen);
     dfree(h->d_smask);
     h->smask.clear();

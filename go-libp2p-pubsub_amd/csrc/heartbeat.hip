@@ -2135,7 +2135,7 @@ __global__ void k_subscribe(HbArgs a, uint64_t* sub, const uint32_t* pairs, int3
 
 __global__ __launch_bounds__(256) void k_churn_find(const uint32_t* row_ptr, const uint32_t* col, int64_t N,
                                                     const uint32_t* pairs, int32_t n2, uint32_t* edges,
-                                                    uint32_t* bad)
+                                                    uint32_t* bad, uint32_t* mark)
 {
     const int32_t q = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (q >= n2) return;
@@ -2151,7 +2151,25 @@ __global__ __launch_bounds__(256) void k_churn_find(const uint32_t* row_ptr, con
         if (lo < end && col[lo] == p) e = lo;
     }
     edges[q] = e;
-    if (e == 0xFFFFFFFFu) atomicMin(bad, (uint32_t)(q >> 1));
+    if (e == 0xFFFFFFFFu) {
+        atomicMin(bad, (uint32_t)(q >> 1));
+    } else if (o < p) {
+        // the connection's lower-to-higher edge, marked once per listing: a
+        // second listing (in either order) finds the mark set
+        const uint32_t bit = 1u << (e & 31);
+        if (atomicOr(mark + (e >> 5), bit) & bit) atomicMin(bad + 1, (uint32_t)(q >> 1));
+    }
+}
+
+// Clears the marks k_churn_find set (the bitmap is zero between calls).
+__global__ __launch_bounds__(256) void k_churn_unmark(const uint32_t* pairs, const uint32_t* edges, int32_t n2,
+                                                      uint32_t* mark)
+{
+    const int32_t q = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (q >= n2) return;
+    const uint32_t o = pairs[(q & ~1) + (q & 1)], p = pairs[(q & ~1) + 1 - (q & 1)];
+    const uint32_t e = edges[q];
+    if (e != 0xFFFFFFFFu && o < p) atomicAnd(mark + (e >> 5), ~(1u << (e & 31)));
 }
 
 // Fresh (or dropped) score record r: an empty peerStats.
@@ -2741,18 +2759,49 @@ int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, i
     if (h->e == 0 || !h->x) { h->err = "no graph loaded"; return GSIM_ESTATE; }
     if (count < 0 || (count > 0 && !pairs)) { h->err = "bad connection list"; return GSIM_EINVAL; }
     if (count == 0) return GSIM_OK;
-    {
-        // a connection listed twice would be handled by two threads at once
-        std::vector<uint64_t> key((size_t)count);
-        for (int32_t q = 0; q < count; ++q) {
-            const uint32_t u = pairs[2 * q], v = pairs[2 * q + 1];
-            key[(size_t)q] = ((uint64_t)std::min(u, v) << 32) | std::max(u, v);
-        }
-        std::sort(key.begin(), key.end());
-        if (std::adjacent_find(key.begin(), key.end()) != key.end()) {
-            h->err = "a connection is listed twice";
-            return GSIM_EINVAL;
-        }
+    // the pairs' edges, found (and checked) before anything changes: a pair
+    // that is not a connection, or a connection listed twice (it would be
+    // handled by two threads at once), fails the call
+    const int32_t n2 = 2 * count;
+    hipError_t e = hipSuccess;
+    if (h->churn_cap < n2) {   // grow-only scratch: no allocation (and no hipFree sync) per call
+        if (h->d_churn) { (void)hipFree(h->d_churn); h->d_churn = nullptr; h->churn_cap = 0; }
+        e = hipMalloc((void**)&h->d_churn, sizeof(uint32_t) * (2 * (size_t)n2 + 2));
+        if (e == hipSuccess) h->churn_cap = n2;
+    }
+    if (e == hipSuccess && !h->d_churn_mark) {
+        const size_t words = ((size_t)h->e + 31) / 32;
+        e = hipMalloc((void**)&h->d_churn_mark, sizeof(uint32_t) * words);
+        if (e == hipSuccess) e = hipMemsetAsync(h->d_churn_mark, 0, sizeof(uint32_t) * words, h->stream);
+    }
+    uint32_t* d_pairs = h->d_churn;
+    uint32_t* d_edges = d_pairs + n2;
+    uint32_t* d_bad = d_edges + n2;
+    if (e == hipSuccess) e = hipMemcpyAsync(d_pairs, pairs, sizeof(uint32_t) * (size_t)n2, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d_bad, 0xFF, 2 * sizeof(uint32_t), h->stream);
+    uint32_t bad[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+    const int grid = (n2 + 255) / 256;
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_churn_find, dim3(grid), dim3(256), 0, h->stream, (const uint32_t*)h->d_row_ptr,
+                           (const uint32_t*)h->d_col, h->n, (const uint32_t*)d_pairs, n2, d_edges, d_bad,
+                           h->d_churn_mark);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_churn_unmark, dim3(grid), dim3(256), 0, h->stream, (const uint32_t*)d_pairs,
+                           (const uint32_t*)d_edges, n2, h->d_churn_mark);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(bad, d_bad, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);   // a bad list fails the call before any change
+    if (e != hipSuccess) return hip_check(h, e, "gsim_set_connections");
+    if (bad[0] != 0xFFFFFFFFu) {
+        h->err = "pair " + std::to_string(bad[0]) + " is not a connection";
+        return GSIM_EINVAL;
+    }
+    if (bad[1] != 0xFFFFFFFFu) {
+        h->err = "pair " + std::to_string(bad[1]) + ": the connection is listed twice";
+        return GSIM_EINVAL;
     }
     int rc = deliver_flush(h);              // pending first deliveries precede the removal
     if (!rc) rc = materialize_mcnt(h);      // the P3b test reads meshMessageDeliveries
@@ -2761,32 +2810,6 @@ int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, i
     if (!rc && !up && h->p6_dirty) rc = launch_ip_colocation(h);
     if (rc) return rc;
     ProfScope ps(h, GSIM_K_CHURN);
-    const int32_t n2 = 2 * count;
-    hipError_t e = hipSuccess;
-    if (h->churn_cap < n2) {   // grow-only scratch: no allocation (and no hipFree sync) per call
-        if (h->d_churn) { (void)hipFree(h->d_churn); h->d_churn = nullptr; h->churn_cap = 0; }
-        e = hipMalloc((void**)&h->d_churn, sizeof(uint32_t) * (2 * (size_t)n2 + 1));
-        if (e == hipSuccess) h->churn_cap = n2;
-    }
-    uint32_t* d_pairs = h->d_churn;
-    uint32_t* d_edges = d_pairs + n2;
-    uint32_t* d_bad = d_edges + n2;
-    if (e == hipSuccess) e = hipMemcpyAsync(d_pairs, pairs, sizeof(uint32_t) * (size_t)n2, hipMemcpyHostToDevice, h->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(d_bad, 0xFF, sizeof(uint32_t), h->stream);
-    uint32_t bad = 0xFFFFFFFFu;
-    const int grid = (n2 + 255) / 256;
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_churn_find, dim3(grid), dim3(256), 0, h->stream, (const uint32_t*)h->d_row_ptr,
-                           (const uint32_t*)h->d_col, h->n, (const uint32_t*)d_pairs, n2, d_edges, d_bad);
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess) e = hipMemcpyAsync(&bad, d_bad, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);   // a bad pair fails the call before any change
-    if (e != hipSuccess) return hip_check(h, e, "gsim_set_connections");
-    if (bad != 0xFFFFFFFFu) {
-        h->err = "pair " + std::to_string(bad) + " is not a connection";
-        return GSIM_EINVAL;
-    }
     return apply_connections(h, d_edges, n2, up, now);
 }
 

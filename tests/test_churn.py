@@ -202,3 +202,39 @@ def test_churn_ticks_bit_exact(require_gpu, n, k, T, nticks, rate, churn_frac):
         assert_same(st, gpu)
     assert n_retained > 0, "some removals were retained"
     eng.close()
+
+
+@pytest.mark.gpu
+def test_set_connections_rejects_bad_lists(require_gpu):
+    """gsim_set_connections fails, changing nothing, on a pair that is not a
+    connection or a connection listed twice (in either order: the checks run
+    on the device, the listed connections marked in an edge bitmap that is
+    cleared again); a good list afterwards applies as the oracle does."""
+    from gsim.engine import Engine
+    from test_heartbeat import assert_same
+    net, st = churn_net()
+    params = delivery_params(1)
+    params.RetainScore = RETAIN
+    eng = Engine(params, PeerScoreThresholds(GraylistThreshold=-100), gossip=GossipSubParams(D=6, Dlo=5, Dhi=12))
+    eng.load_graph(net)
+    st.push_to_engine(eng)
+    a = 3
+    b, c = (int(x) for x in net.col[net.row_ptr[a]:net.row_ptr[a] + 2])
+    non = next(j for j in range(net.n) if j != a and j not in set(net.col[net.row_ptr[a]:net.row_ptr[a + 1]].tolist()))
+    now = tick_time(2)
+    for bad, what in (([(a, b), (a, c), (b, a)], "listed twice"), ([(a, c), (a, c)], "listed twice"),
+                      ([(a, b), (a, non)], "not a connection"), ([(a, a)], "not a connection")):
+        with pytest.raises(ValueError, match=what):
+            eng.set_connections(bad, up=False, now=now)
+        gpu = ob.NetState(net, params, thresholds=PeerScoreThresholds(GraylistThreshold=-100),
+                          gossip=GossipSubParams(D=6, Dlo=5, Dhi=12))
+        gpu.pull_from_engine(eng)
+        assert_same(st, gpu)
+    good = [(a, b), (c, a)]
+    eng.set_connections(good, up=False, now=now)
+    st.churn(good, up=False, now=now)
+    gpu = ob.NetState(net, params, thresholds=PeerScoreThresholds(GraylistThreshold=-100),
+                      gossip=GossipSubParams(D=6, Dlo=5, Dhi=12))
+    gpu.pull_from_engine(eng)
+    assert_same(st, gpu)
+    eng.close()
