@@ -1564,6 +1564,10 @@ __global__ __launch_bounds__(256) void k_gossip_count_mm(IhArgs a, const uint32_
 #ifndef GSIM_IH_WPE
 #define GSIM_IH_WPE 1
 #endif
+#ifndef GSIM_IH_BATCH
+#define GSIM_IH_BATCH 4
+#endif
+constexpr int kIhBatch = GSIM_IH_BATCH;   // MM walks: slots whose cells one lane loads at once
 template <int W, bool LAT, bool SP, bool MM = false>
 __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, const uint32_t* gcount)
 {
@@ -1776,13 +1780,27 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 uint64_t uw = mine;
                 for (int o = 32; o; o >>= 1) uw |= (uint64_t)__shfl_xor((long long)uw, o, 64);
                 const uint32_t pg = gs ? (a.gid ? a.gid[p] : p) : 0u;
-                for (; uw; uw &= uw - 1) {
-                    const int q = __builtin_ctzll(uw);
+                const int64_t poff = gs ? a.cs.at(0, t, p) : -1;    // p's cell in every slot of tb
+                while (uw) {
+                  // kIhBatch slots' cells in flight at once (nothing here writes a cell)
+                  int qb[kIhBatch];
+                  bool ask[kIhBatch];
+                  uint64_t cvb[kIhBatch];
+#pragma unroll
+                  for (int b = 0; b < kIhBatch; ++b) {
+                      qb[b] = uw ? __builtin_ctzll(uw) : -1;
+                      if (uw) uw &= uw - 1;
+                      ask[b] = qb[b] >= 0 && ((mine >> qb[b]) & 1ull) && poff >= 0;
+                      cvb[b] = ask[b] ? a.cs.cell[(int64_t)a.cs.cbase[s_act[k0 + qb[b]] & 0x7FFF] + poff] : 0ull;
+                  }
+#pragma unroll
+                  for (int b = 0; b < kIhBatch; ++b) {
+                    const int q = qb[b];
+                    if (q < 0) break;                                // wave-uniform
                     const uint32_t m = s_act[k0 + q] & 0x7FFF;
                     bool req = false, resp = false;
-                    if ((mine >> q) & 1ull) {
-                        const int64_t pci = a.cs.at((int64_t)a.cs.cbase[m], t, p);
-                        req = pci >= 0 && a.cs.cell[pci] == kUnseen64;   // p has not seen m
+                    if (ask[b]) {
+                        req = cvb[b] == kUnseen64;                   // p has not seen m
                         if (req) {
                             const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, pg, 0, P_PROMISE, m, me_g);
                             atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[re]), (unsigned long long)key);
@@ -1797,6 +1815,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                         if (resp) stage[nstage + __popcll(sb & ((1ull << lane) - 1))] = (uint64_t)e | ((uint64_t)m << 32);
                         nstage += __popcll(sb);
                     }
+                  }
                 }
             };
             const uint64_t longm = mask & long_lanes;
@@ -1864,13 +1883,26 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 uint64_t uw = mine;                                  // the slots some lane asks about
                 for (int o = 32; o; o >>= 1) uw |= (uint64_t)__shfl_xor((long long)uw, o, 64);
                 const uint32_t ig = gs ? (a.gid ? a.gid[i] : i) : 0u;
-                for (; uw; uw &= uw - 1) {
-                    const int q = __builtin_ctzll(uw);
+                const int64_t ioff = gs ? a.cs.at(0, t, i) : -1;    // i's cell in every slot of tb
+                while (uw) {
+                  // kIhBatch slots' cells in flight at once (nothing here writes a cell)
+                  int qb[kIhBatch];
+                  uint64_t cvb[kIhBatch];
+#pragma unroll
+                  for (int b = 0; b < kIhBatch; ++b) {
+                      qb[b] = uw ? __builtin_ctzll(uw) : -1;
+                      if (uw) uw &= uw - 1;
+                      const bool ask = qb[b] >= 0 && ((mine >> qb[b]) & 1ull) && ioff >= 0;
+                      cvb[b] = ask ? a.cs.cell[(int64_t)a.cs.cbase[s_act[k0 + qb[b]] & 0x7FFF] + ioff] : kUnseen64;
+                  }
+#pragma unroll
+                  for (int b = 0; b < kIhBatch; ++b) {
+                    const int q = qb[b];
+                    if (q < 0) break;                                // wave-uniform
                     const uint32_t m = s_act[k0 + q] & 0x7FFF;
                     bool req = false, resp = false;
                     if ((mine >> q) & 1ull) {
-                        const int64_t ici = a.cs.at((int64_t)a.cs.cbase[m], t, i);
-                        req = holds_in_window(ici >= 0 ? a.cs.cell[ici] : kUnseen64, a.g, a.lo_round, tick_round,
+                        req = holds_in_window(cvb[b], a.g, a.lo_round, tick_round,
                                               a.minv[m] != 0, i == a.morigin[m], LAT ? a.mlat[m] : 0u);
                         if (req) {
                             const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, me_g, 0, P_PROMISE, m, ig);
@@ -1887,6 +1919,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                         if (resp) stage[nstage + __popcll(sb & ((1ull << lane) - 1))] = (uint64_t)re | ((uint64_t)m << 32);
                         nstage += __popcll(sb);
                     }
+                  }
                 }
             };
             const uint64_t longm = mask & long_lanes;

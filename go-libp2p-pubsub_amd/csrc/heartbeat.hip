@@ -1484,8 +1484,8 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a_)
 // (gossipsub.go:1866-1906, 860-869, 893-939) for the PRUNEs an observer just
 // sent with PX (GSIM_CTL_PX in ctl_out; pxo[obs] lists their topics): the
 // PX list is getPeers(topic, PrunePeers, xp != p && Score(xp) >= 0), the
-// PrunePeers smallest Philox keys (the pruned peer's row position in the
-// topic word: every PRUNE its own shuffle).  live: Score is the observer's
+// PrunePeers smallest keys (px_key: the topic's draw per candidate, px_base,
+// mixed with the pruned peer's row position: every PRUNE its own shuffle).  live: Score is the observer's
 // live score (the heartbeat's sendGraftPrune, after every topic); else the
 // snapshot (the control round's GRAFT replies).  The pruned
 // peer ignores PX from a peer it scores below acceptPXThreshold; every listed
@@ -1536,11 +1536,13 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
     __shared__ KeyT s_key[WV][ROW];
     __shared__ uint64_t s_ok[SPLIT ? WV : 1][SPLIT ? ROW / 64 : 1];
     __shared__ uint64_t s_cb[SPLIT ? 1 : WV][ROW / 64];          // the topic's candidates (makePrune's filter)
+    __shared__ uint32_t s_pb[SPLIT ? 1 : WV][ROW];               // ... and their draws (px_base)
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double* sc = s_sc[SPLIT ? 0 : wid];
     KeyT* key = s_key[wid];
     uint64_t* ok = s_ok[SPLIT ? wid : 0];
     uint64_t* cb = s_cb[SPLIT ? 0 : wid];
+    uint32_t* pb = s_pb[SPLIT ? 0 : wid];
     auto kget = [&](int q) -> uint64_t {
         if constexpr (SPLIT) return ((ok[q >> 6] >> (q & 63)) & 1ull) ? (((uint64_t)key[q] << 32) | (uint32_t)q) : ~0ull;
         else return key[q];
@@ -1582,6 +1584,7 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
                 if (q < deg) {
                     const uint32_t e = b + (uint32_t)q;
                     c = (a.rstate[e] & GSIM_ES_CONNECTED) && ((a.sub[a.col[e]] >> t) & 1ull) && sc[q] >= 0.0;
+                    if (c) pb[q] = px_base(a.seed, key_tick, gobs, (uint32_t)t, purpose, glob(a, a.col[e]));
                 }
                 const uint64_t bm = __ballot(c);
                 if (lane == 0) cb[q0 >> 6] = bm;
@@ -1603,16 +1606,13 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
                     // a ghost p: its shard holds its score of obs and its row (below)
                     const bool remote = a.pxout && (p < a.olo || p >= a.ohi);
                     if (!remote && a.score[ep] < a.accept_px) continue;   // p's snapshot score of obs (record order)
-                    const uint32_t kt = (uint32_t)t + 64u * (uint32_t)(pos + 1);
                     uint32_t n = 0;
                     for (int q0 = 0; q0 < deg; q0 += 64) {
                         const int q = q0 + lane;
                         bool c = false;
                         if (q < deg && q != pos) {
                             c = (cb[q >> 6] >> (q & 63)) & 1ull;
-                            const uint64_t kv = c ? select_key(a.seed, key_tick, gobs, kt, purpose, glob(a, a.col[b + (uint32_t)q]),
-                                                               (uint32_t)q)
-                                                  : ~0ull;
+                            const uint64_t kv = c ? px_key(pb[q], (uint32_t)pos, (uint32_t)q) : ~0ull;
                             if constexpr (SPLIT) key[q] = (uint32_t)(kv >> 32);
                             else key[q] = kv;
                         } else if (q < deg) {
@@ -1979,7 +1979,6 @@ __device__ void px_leave_list(const HbArgs& a, const uint64_t* sub, uint32_t obs
 {
     const double* sc = a.pxs;
     const uint32_t gobs = glob(a, obs);
-    const uint32_t kt = (uint32_t)t + 64u * (ep - b + 1u);
     const uint32_t p = a.col[ep];
     const bool remote = a.pxout && (p < a.olo || p >= a.ohi);
     uint64_t last = 0;
@@ -1988,7 +1987,8 @@ __device__ void px_leave_list(const HbArgs& a, const uint64_t* sub, uint32_t obs
         uint32_t bx = 0xFFFFFFFFu;
         for (uint32_t e = b; e < en; ++e) {
             if (e == ep || !sub_topic_peer(a, const_cast<uint64_t*>(sub), e, t) || sc[e] < 0.0) continue;
-            const uint64_t key = select_key(a.seed, (uint32_t)a.tick, gobs, kt, P_PX_LEAVE, glob(a, a.col[e]), e - b);
+            const uint64_t key = px_key(px_base(a.seed, (uint32_t)a.tick, gobs, (uint32_t)t, P_PX_LEAVE, glob(a, a.col[e])),
+                                        ep - b, e - b);
             if ((k > 0 && key <= last) || key >= best) continue;
             best = key;
             bx = e;

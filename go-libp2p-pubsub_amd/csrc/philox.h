@@ -79,4 +79,26 @@ GSIM_HD uint64_t select_key(uint64_t seed, uint32_t tick, uint32_t observer, uin
     return ((uint64_t)r.x << 32) | pos;
 }
 
+// PX keys (makePrune's getPeers, gossipsub.go:1879-1882): one Philox draw per
+// (observer, topic, candidate) and pass, shared by every PRUNE of the topic,
+// mixed (murmur3's 32-bit finaliser) with the pruned peer's row position so
+// that each PRUNE's list is its own shuffle.  A hub answering hundreds of
+// GRAFTs per tick draws each candidate once instead of once per PRUNE.
+GSIM_HD uint32_t px_base(uint64_t seed, uint32_t tick, uint32_t observer, uint32_t topic, uint32_t purpose,
+                         uint32_t item)
+{
+    return philox4x32_10(tick, observer, (topic << 8) | purpose, item, (uint32_t)seed, (uint32_t)(seed >> 32)).x;
+}
+
+GSIM_HD uint64_t px_key(uint32_t base, uint32_t pruned_pos, uint32_t pos)
+{
+    uint32_t h = base ^ ((pruned_pos + 1u) * 0x9E3779B9u);
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return ((uint64_t)h << 32) | pos;
+}
+
 }  // namespace gsim

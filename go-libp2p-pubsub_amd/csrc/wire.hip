@@ -176,7 +176,6 @@ __device__ uint32_t px_list(const WireArgs& a, int64_t e, uint32_t p, int32_t t,
     // the heartbeat's: getPeers(topic, PrunePeers, xp != p && Score(xp) >= 0) on the live
     // scores after the heartbeat, the PrunePeers smallest keys (k_px_emit)
     const uint32_t b = a.row_ptr[p], en = a.row_ptr[p + 1];
-    const uint32_t kt = (uint32_t)t + 64u * ((uint32_t)(e - b) + 1u);
     uint64_t last = 0;
     for (int k = 0; k < a.prune_peers && k < kWirePxMax; ++k) {
         uint64_t best = ~0ull;
@@ -185,7 +184,7 @@ __device__ uint32_t px_list(const WireArgs& a, int64_t e, uint32_t p, int32_t t,
             if ((int64_t)q == e) continue;
             const uint32_t x = a.col[q];
             if (!(a.rstate[q] & GSIM_ES_CONNECTED) || !((a.sub[x] >> t) & 1ull) || a.pxs[q] < 0.0) continue;
-            const uint64_t key = select_key(a.seed, (uint32_t)a.tick, p, kt, P_PX, x, q - b);
+            const uint64_t key = px_key(px_base(a.seed, (uint32_t)a.tick, p, (uint32_t)t, P_PX, x), (uint32_t)(e - b), q - b);
             if ((k > 0 && key <= last) || key >= best) continue;
             best = key;
             bx = x;

@@ -36,6 +36,29 @@ static inline uint64_t okey(uint64_t seed, uint64_t tick, uint32_t obs, int32_t 
     return ((uint64_t)out[0] << 32) | pos;
 }
 
+/* PX keys (csrc/philox.h px_base / px_key): one draw per (observer, topic,
+ * candidate) and pass, mixed with the pruned peer's row position per PRUNE */
+static inline uint32_t opx_base(uint64_t seed, uint64_t tick, uint32_t obs, int32_t topic, uint32_t purpose,
+                                uint32_t item)
+{
+    uint32_t ctr[4] = {(uint32_t)tick, obs, ((uint32_t)topic << 8) | purpose, item};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t out[4];
+    orc_philox4x32_10(ctr, key, out);
+    return out[0];
+}
+
+static inline uint64_t opx_key(uint32_t base, uint32_t pruned_pos, uint32_t pos)
+{
+    uint32_t h = base ^ ((pruned_pos + 1u) * 0x9E3779B9u);
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return ((uint64_t)h << 32) | pos;
+}
+
 typedef struct fr_ent { uint32_t peer, slot, from; } fr_ent;
 /* a copy at its receiver; resp: an IWANT answer (one RPC per sender and round) */
 typedef struct arr_ent { uint32_t recv, slot, er, resp; } arr_ent;

@@ -100,8 +100,8 @@ static void graft_peer(hb* h, uint32_t e)
  * (860-869, 893-939).  live: Score is the observer's live score (the
  * heartbeat's sendGraftPrune, Leave's sendPrune); else its snapshot
  * (handleGraft's replies, the control rounds' declared divergence).  The keys
- * put the pruned peer's row position into the topic word: each PRUNE's list
- * is its own shuffle.  The list is what the PRUNE carries, whatever the
+ * (opx_key) mix the topic's draw per candidate with the pruned peer's row
+ * position: each PRUNE's list is its own shuffle.  The list is what the PRUNE carries, whatever the
  * receiver then does with it (ORC_EV_PX_PEER events, in list order).  The
  * receiver ignores PX from a peer it scores below acceptPXThreshold (its
  * snapshot); every listed peer it is not connected to is a connection
@@ -116,12 +116,11 @@ static int px_list(hb* h, uint32_t ep, int live, uint32_t purpose, uint64_t key_
 {
     orc_net* s = h->s;
     int n = 0;
-    const int32_t kt = h->t + 64 * (int32_t)(ep - h->b + 1);
     for (uint32_t e = h->b; e < h->en; ++e) {
         if (e == ep || !topic_peer(h, e)) continue;
         const double sc = live ? orc_score_edge(s, e) : s->score[e];
         if (sc < 0) continue;
-        c[n].key = okey(h->seed, key_tick, h->i, kt, purpose, s->col[e], e - h->b);
+        c[n].key = opx_key(opx_base(h->seed, key_tick, h->i, h->t, purpose, s->col[e]), ep - h->b, e - h->b);
         c[n].e = e;
         c[n].score = sc;
         ++n;
