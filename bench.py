@@ -245,7 +245,7 @@ def run_tick(eng, k, sched, churn=None, px=False):
             _timed("publish", eng.publish_array, m, g)
         _timed("round", eng.round, g)
     if px:                                     # the connector for this tick's PX attempts
-        _timed("px_connect", eng.px_connect, now + SECOND // 2)
+        _timed("px_connect", eng.px_connect, now + SECOND // 2, want_pairs=False)
 
 
 def cpu_baseline(cfg, scen=None, n: int = 10_000, ticks: int = 5, budget_s: float = 25.0, warmup: int = 1,

@@ -1493,6 +1493,7 @@ __global__ __launch_bounds__(256) void k_handle_control(HbArgs a_)
 // (pxm), resolved between ticks by gsim_px_connect.  One wave per observer;
 // rows of at most 1024 connections (keys and scores staged in LDS).
 constexpr int kPxRow = 1024;
+constexpr int kPxList = 64;     // keys a PRUNE lists below its bound (one per lane)
 
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v)
 {
@@ -1500,6 +1501,12 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v)
         const uint64_t y = (uint64_t)__shfl_xor((long long)v, o, 64);
         v = y > v ? y : v;
     }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
+{
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
     return v;
 }
 
@@ -1528,25 +1535,17 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
                                                      const uint32_t* rows, int64_t nrows)
 {
     const HbArgs& a = a_;
-    // SPLIT (hub rows): the block's waves share one observer and take its PRUNEs in
-    // turn; a wave's keys are then the Philox words alone (the low word is the
-    // row position, the index) with a candidate bitmap, to fit WV rows in LDS
-    using KeyT = typename std::conditional<SPLIT, uint32_t, uint64_t>::type;
+    // SPLIT (hub rows): the block's waves share one observer (its scores, each
+    // topic's candidates and draws) and take its PRUNEs in turn
     __shared__ double s_sc[SPLIT ? 1 : WV][ROW];
-    __shared__ KeyT s_key[WV][ROW];
-    __shared__ uint64_t s_ok[SPLIT ? WV : 1][SPLIT ? ROW / 64 : 1];
     __shared__ uint64_t s_cb[SPLIT ? 1 : WV][ROW / 64];          // the topic's candidates (makePrune's filter)
     __shared__ uint32_t s_pb[SPLIT ? 1 : WV][ROW];               // ... and their draws (px_base)
+    __shared__ uint64_t s_lst[WV][kPxList];                      // a PRUNE's smallest keys
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double* sc = s_sc[SPLIT ? 0 : wid];
-    KeyT* key = s_key[wid];
-    uint64_t* ok = s_ok[SPLIT ? wid : 0];
     uint64_t* cb = s_cb[SPLIT ? 0 : wid];
     uint32_t* pb = s_pb[SPLIT ? 0 : wid];
-    auto kget = [&](int q) -> uint64_t {
-        if constexpr (SPLIT) return ((ok[q >> 6] >> (q & 63)) & 1ull) ? (((uint64_t)key[q] << 32) | (uint32_t)q) : ~0ull;
-        else return key[q];
-    };
+    uint64_t* lst = s_lst[wid];
     const int64_t nobs = rows ? nrows : a.ohi - a.olo;
     constexpr int OPB = SPLIT ? 1 : WV;                          // observers per block
     const int slot = SPLIT ? 0 : wid;
@@ -1606,30 +1605,45 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
                     // a ghost p: its shard holds its score of obs and its row (below)
                     const bool remote = a.pxout && (p < a.olo || p >= a.ohi);
                     if (!remote && a.score[ep] < a.accept_px) continue;   // p's snapshot score of obs (record order)
+                    // the PRUNE's candidates (every candidate of t but p) and their keys
+                    auto kget = [&](int q) -> uint64_t {
+                        return (q != pos && ((cb[q >> 6] >> (q & 63)) & 1ull)) ? px_key(pb[q], (uint32_t)pos, (uint32_t)q)
+                                                                                 : ~0ull;
+                    };
                     uint32_t n = 0;
+                    for (int w = lane; w < (deg + 63) / 64; w += 64) n += (uint32_t)__popcll(cb[w]);
+                    n = (uint32_t)wave_sum_u32(n) - (uint32_t)((cb[pos >> 6] >> (pos & 63)) & 1ull);
+                    // the keys below a bound that holds ~PrunePeers + 24 of the (uniform)
+                    // high words, listed in row order in one pass; the PrunePeers smallest
+                    // are then ranked within the list (if it holds them and fits)
+                    const uint64_t tau_hi = (int32_t)n <= kPxList || (double)(a.prune_peers + 24) >= (double)n
+                                                ? ~0ull
+                                                : (uint64_t)((double)(a.prune_peers + 24) / (double)n * 4294967296.0) << 32;
+                    uint32_t nl = 0;
                     for (int q0 = 0; q0 < deg; q0 += 64) {
                         const int q = q0 + lane;
-                        bool c = false;
-                        if (q < deg && q != pos) {
-                            c = (cb[q >> 6] >> (q & 63)) & 1ull;
-                            const uint64_t kv = c ? px_key(pb[q], (uint32_t)pos, (uint32_t)q) : ~0ull;
-                            if constexpr (SPLIT) key[q] = (uint32_t)(kv >> 32);
-                            else key[q] = kv;
-                        } else if (q < deg) {
-                            if constexpr (!SPLIT) key[q] = ~0ull;
-                        }
-                        const uint64_t cb = __ballot(c);
-                        if constexpr (SPLIT) {
-                            if (lane == 0) ok[q0 >> 6] = cb;
-                        }
-                        n += (uint32_t)__popcll(cb);
+                        const uint64_t kv = q < deg ? kget(q) : ~0ull;
+                        const bool in = kv != ~0ull && kv < tau_hi;
+                        const uint64_t bm = __ballot(in);
+                        const uint32_t at = nl + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+                        if (in && at < (uint32_t)kPxList) lst[at] = kv;
+                        nl += (uint32_t)__popcll(bm);
                     }
                     wave_lds_sync();
-                    // the PrunePeers smallest keys are those below tau: start from the
-                    // quantile estimate of the (uniform) high words, then move tau past
-                    // one key at a time (as select_smallest)
-                    uint64_t tau = ~0ull;                          // exclusive; every candidate (others are ~0)
-                    if ((int32_t)n > a.prune_peers) {
+                    const bool listed = nl <= (uint32_t)kPxList && ((int32_t)nl >= a.prune_peers || tau_hi == ~0ull);
+                    // exclusive bound: the PrunePeers smallest keys are those below tau
+                    uint64_t tau = ~0ull;
+                    if (listed) {
+                        if ((int32_t)nl > a.prune_peers) {
+                            const uint64_t kv = lane < (int)nl ? lst[lane] : ~0ull;
+                            uint32_t rank = 0;
+                            for (uint32_t j = 0; j < nl; ++j) rank += lst[j] < kv;
+                            const uint64_t hit = __ballot(lane < (int)nl && (int32_t)rank == a.prune_peers);
+                            tau = (uint64_t)__shfl((long long)kv, __builtin_ctzll(hit), 64);
+                        }
+                    } else if ((int32_t)n > a.prune_peers) {
+                        // the list missed: start from the quantile estimate, then move tau
+                        // past one key at a time (as select_smallest)
                         tau = (uint64_t)((double)a.prune_peers / (double)n * 4294967296.0) << 32;
                         int32_t c = 0;
                         for (int q0 = 0; q0 < deg; q0 += 64) {
@@ -1640,7 +1654,8 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
                             uint64_t mx = 0;
                             for (int q0 = 0; q0 < deg; q0 += 64) {
                                 const int q = q0 + lane;
-                                if (q < deg && kget(q) < tau && kget(q) >= mx) mx = kget(q);
+                                const uint64_t kv = q < deg ? kget(q) : ~0ull;
+                                if (kv < tau && kv >= mx) mx = kv;
                             }
                             mx = wave_max_u64(mx);
                             tau = mx;
@@ -1650,47 +1665,52 @@ __global__ __launch_bounds__(64 * WV) void k_px_emit(HbArgs a_, int live, uint32
                             uint64_t mn = ~0ull;
                             for (int q0 = 0; q0 < deg; q0 += 64) {
                                 const int q = q0 + lane;
-                                if (q < deg && kget(q) >= tau && kget(q) < mn) mn = kget(q);
+                                const uint64_t kv = q < deg ? kget(q) : ~0ull;
+                                if (kv >= tau && kv < mn) mn = kv;
                             }
                             mn = wave_min_u64(mn);
                             tau = mn + 1;
                             ++c;
                         }
                     }
-                    if (remote) {
-                        // the PX list to p's shard, which makes handlePrune's checks (k_px_import)
-                        const uint32_t d = a.pshard[p];
-                        const uint64_t hdr = (uint64_t)a.xre[ep] | ((uint64_t)t << 32);
-                        for (int q0 = 0; q0 < deg; q0 += 64) {
-                            const int q = q0 + lane;
-                            const bool in = q < deg && kget(q) < tau;
-                            const uint64_t bm = __ballot(in);
+                    // the list's entries in row order: from the ranked list, else a pass
+                    // over the row (lane-strided: entry j of chunk j / 64)
+                    const int span = listed ? (int)nl : deg;
+                    const uint32_t d = remote ? a.pshard[p] : 0u;
+                    const uint64_t hdr = remote ? ((uint64_t)a.xre[ep] | ((uint64_t)t << 32)) : 0ull;
+                    const uint32_t rb = a.row_ptr[p], re = a.row_ptr[p + 1];
+                    for (int j0 = 0; j0 < span; j0 += 64) {
+                        const int j = j0 + lane;
+                        int q = -1;
+                        if (listed) {
+                            if (j < span && lst[j] < tau) q = (int)(uint32_t)lst[j];
+                        } else if (j < span && kget(j) < tau) {
+                            q = j;
+                        }
+                        if (remote) {
+                            // the PX list to p's shard, which makes handlePrune's checks (k_px_import)
+                            const uint64_t bm = __ballot(q >= 0);
                             uint32_t base = 0;
                             if (lane == 0 && bm) base = atomicAdd(&a.pxcnt[d], (uint32_t)__popcll(bm));
                             base = (uint32_t)__shfl((int)base, 0, 64);
-                            if (!in) continue;
+                            if (q < 0) continue;
                             const uint32_t k = base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
                             const uint64_t gx = glob(a, a.col[b + (uint32_t)q]);
                             if ((int64_t)k < a.pxcap) a.pxout[(int64_t)d * a.pxcap + k] = hdr | (gx << 38);
                             else atomicOr(&a.pxcnt[a.pxK], 1u);
+                            continue;
                         }
-                        wave_lds_sync();
-                        continue;
-                    }
-                    const uint32_t pb = a.row_ptr[p], pe = a.row_ptr[p + 1];
-                    for (int q0 = 0; q0 < deg; q0 += 64) {
-                        const int q = q0 + lane;
-                        if (q >= deg || kget(q) >= tau) continue;
+                        if (q < 0) continue;
                         const uint32_t x = a.col[b + (uint32_t)q];
-                        uint32_t lo = pb, hi = pe;                 // p's row is sorted: its edge to x
+                        uint32_t lo = rb, hi = re;                 // p's row is sorted: its edge to x
                         while (lo < hi) {
                             const uint32_t mid = lo + ((hi - lo) >> 1);
                             if (a.col[mid] < x) lo = mid + 1; else hi = mid;
                         }
                         // pxConnect skips peers it is connected to
-                        if (lo < pe && a.col[lo] == x && !(a.rstate[lo] & GSIM_ES_CONNECTED)) a.pxm[lo] = 1;
+                        if (lo < re && a.col[lo] == x && !(a.rstate[lo] & GSIM_ES_CONNECTED)) a.pxm[lo] = 1;
                     }
-                    wave_lds_sync();
+                    wave_lds_sync();                               // lst is rewritten by the next PRUNE
                 }
             }
         }

@@ -346,11 +346,15 @@ class Engine:
                                              _ptr(out["counters"]), _ptr(out["connected"]), _ptr(out["expire"])))
         return out
 
-    def px_connect(self, now: int) -> np.ndarray:
+    def px_connect(self, now: int, want_pairs: bool = True):
         """The connector for the attempts peer exchange queued this tick
         (gsim_px_connect; pxConnect gossipsub.go:893-973): returns the
-        (dialer, peer) pairs that became connections, sorted."""
+        (dialer, peer) pairs that became connections, sorted (want_pairs
+        False: only their number, nothing read back or sorted)."""
         n = ctypes.c_int64(0)
+        if not want_pairs:
+            self._check(self.lib.gsim_px_connect(self.h, int(now), None, 0, ctypes.byref(n)))
+            return n.value
         cap = max(1, self.net.e // 2)
         out = np.zeros((cap, 2), dtype=np.uint32)
         self._check(self.lib.gsim_px_connect(self.h, int(now), _ptr(out), int(cap), ctypes.byref(n)))

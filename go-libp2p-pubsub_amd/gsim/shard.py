@@ -365,10 +365,14 @@ class ShardedEngine:
         self._check(self.lib.gsim_group_set_subscriptions(self.g, _ptr(p), int(p.shape[0]), 1 if join else 0,
                                                           int(tick), int(now)))
 
-    def px_connect(self, now: int) -> np.ndarray:
+    def px_connect(self, now: int, want_pairs: bool = True):
         """The connector over the shards (gsim_group_px_connect; every rank
-        calls it): the (dialer, peer) pairs that became connections, sorted."""
+        calls it): the (dialer, peer) pairs that became connections, sorted
+        (want_pairs False: only their number)."""
         n = ctypes.c_int64(0)
+        if not want_pairs:
+            self._check(self.lib.gsim_group_px_connect(self.g, int(now), None, 0, ctypes.byref(n)))
+            return n.value
         cap = max(1, self.net.e // 2)
         out = np.zeros((cap, 2), dtype=np.uint32)
         self._check(self.lib.gsim_group_px_connect(self.g, int(now), _ptr(out), int(cap), ctypes.byref(n)))
