@@ -1561,8 +1561,10 @@ __global__ __launch_bounds__(256) void k_gossip_count_mm(IhArgs a, const uint32_
         if (s_c[w]) atomicAdd(&gcount[(w < R ? 0 : a.ring - R) + m_lo + w], s_c[w]);
 }
 
+// waves per SIMD the member-major IHAVE walk is fitted to: 5 (96 VGPRs, 25
+// spilled) against 4 (112): c5 gossip 96.4 -> 92.0 ms per tick (gpurun_out/r04ab_occ)
 #ifndef GSIM_IH_WPE
-#define GSIM_IH_WPE 1
+#define GSIM_IH_WPE 5
 #endif
 #ifndef GSIM_IH_BATCH
 #define GSIM_IH_BATCH 4
