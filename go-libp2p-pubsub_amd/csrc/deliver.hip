@@ -112,6 +112,8 @@ struct Deliver {
     int64_t* d_mloff = nullptr;        // [T] first entry of each topic (-1: every peer, member j = peer j)
     int64_t* d_mcount = nullptr;       // [T] members of each topic
     uint32_t* d_mmtab = nullptr;       // [T+1] first 256-member block of each topic (k_ihave<MM>)
+    uint32_t* d_hubw = nullptr;        // [hubw_cap] k_ihave<MM>'s waves with hub rows, then [1] their count
+    int64_t hubw_cap = 0;
     uint32_t* d_mctab = nullptr;       // [T+1] first 1024-member block of each topic (k_gossip_count_mm)
     std::vector<uint32_t> mmtab, mctab;
     int64_t cell_nw = 0;               // words per topic of the member bitmaps
@@ -1387,6 +1389,9 @@ struct IhArgs {
     const int64_t *mloff, *mcount;
     const uint32_t* mmtab;
     int32_t topic_slots;
+    // MM hub rows (k_ihave LP 1 / 2): the listed waves (block * 4 + wave) and their count
+    uint32_t* hubw;
+    uint32_t* hubn;
 };
 
 // Member-major blocks: block b of a launch over topics' member ranges (table
@@ -1570,7 +1575,18 @@ __global__ __launch_bounds__(256) void k_gossip_count_mm(IhArgs a, const uint32_
 #define GSIM_IH_BATCH 4
 #endif
 constexpr int kIhBatch = GSIM_IH_BATCH;   // MM walks: slots whose cells one lane loads at once
-template <int W, bool LAT, bool SP, bool MM = false>
+// MM hub rows (members are in peer-id order, and a power law's largest rows
+// cluster at the low ids: a topic's first waves would walk dozens of hubs each,
+// serially): LP 1 walks every row of at most kIhHub connections and lists the
+// waves holding longer ones (IhArgs::hubw, with their slice count: one per
+// 256 connections of the wave's longest row); LP 2 walks only those rows, a
+// block of one wave per (listed wave, slice) -- slice s of ns taking the
+// 64-edge chunks s, s + ns, ... of each row (blocks past ns exit at once)
+// (128: 38.3 + 63.6 ms at c5 -- many more listed waves -- against 256: 39.4 + 11.0
+// with 16 slices each, gpurun_out/r04c5h, r04c5i)
+constexpr uint32_t kIhHub = 256;
+constexpr int kIhSlices = 16;
+template <int W, bool LAT, bool SP, bool MM = false, int LP = 0>
 __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, const uint32_t* gcount)
 {
     const IhArgs& a = a_;
@@ -1579,10 +1595,17 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
     if (a.nresp[3] & 4u) return;          // a truncation may apply: k_ihave_pairs
     const int wid = threadIdx.x >> 6;
     uint64_t* stage = reinterpret_cast<uint64_t*>(s_act + ((a.ring + 3) & ~3)) + wid * kRespStage;
+    // LP 2: the listed wave (its block and wave) and the slice
+    const uint32_t hw = LP == 2 ? a.hubw[blockIdx.x / kIhSlices] : 0u;
+    const uint32_t bx = LP == 2 ? (hw & 0x07FFFFFFu) >> 2 : blockIdx.x;
+    const int wsel = LP == 2 ? (int)(hw & 3u) : wid;
+    const uint32_t slice = LP == 2 ? blockIdx.x % kIhSlices : 0u;
+    const uint32_t nsl = LP == 2 ? (hw >> 27) + 1u : 1u;          // the wave's slice count
+    if (LP == 2 && slice >= nsl) return;
     // MM: the block's topic and its 256 members [jb, jb + 256) (member-major
     // walk of a sub-ring: only the topic's slots, cells at cbase[m] + member)
-    const int32_t tb = MM ? block_topic(a.mmtab, a.T, blockIdx.x) : 0;
-    const int64_t jb = MM ? (int64_t)(blockIdx.x - a.mmtab[tb]) * 256 : 0;
+    const int32_t tb = MM ? block_topic(a.mmtab, a.T, bx) : 0;
+    const int64_t jb = MM ? (int64_t)(bx - a.mmtab[tb]) * 256 : 0;
     const int m_lo = MM ? tb * a.topic_slots : 0, m_hi = MM ? m_lo + a.topic_slots : a.ring;
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
@@ -1603,7 +1626,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int64_t p0 = MM ? 0 : ((int64_t)blockIdx.x * 4 + wid) * 64;   // peers p0 .. p0 + 63
-    const int64_t jw = jb + wid * 64;                                  // MM: members jw .. jw + 63
+    const int64_t jw = jb + wsel * 64;                                 // MM: members jw .. jw + 63
     const int nact = (MM ? jw < a.mcount[tb] : p0 < a.CN) ? s_n : 0;
     const bool vp = MM ? jw + lane < a.mcount[tb] : p0 + lane < a.CN;
     const int64_t pl = MM ? (vp ? (int64_t)member_peer(a, tb, jw + lane) : 0) : p0 + lane;
@@ -1614,6 +1637,12 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
     const uint32_t rp1 = vp ? a.row_ptr[pl + 1] : 0u;
     const bool ign_l = vp && (a.behaviour[pl] & GSIM_BEHAVE_IGNORE_IWANT);
     const uint64_t long_lanes = W < 64 ? __ballot(rp1 - rp0 > 4u * (uint32_t)W) : 0ull;
+    // LP 1: rows left to LP 2; LP 2: its only rows
+    const uint64_t hub_lanes = LP ? __ballot(rp1 - rp0 > kIhHub) : 0ull;
+    bool had_hub = false;
+    uint32_t hub_max = LP == 1 && rp1 - rp0 > kIhHub ? rp1 - rp0 : 0u;
+    if constexpr (LP == 1)
+        for (int o = 32; o; o >>= 1) hub_max = max(hub_max, (uint32_t)__shfl_xor((int)hub_max, o, 64));
     const int64_t tick_round = a.tick * a.R;
     int nstage = 0;
     unsigned long long n_walk = 0, n_req = 0, n_resp = 0;
@@ -1820,8 +1849,10 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                   }
                 }
             };
-            const uint64_t longm = mask & long_lanes;
-            uint64_t gm = mask & ~longm & gmask;
+            had_hub = had_hub || (mask & hub_lanes) != 0;
+            const uint64_t longm = LP == 2 ? (mask & hub_lanes) : LP == 1 ? (mask & long_lanes & ~hub_lanes)
+                                                                           : (mask & long_lanes);
+            uint64_t gm = LP == 2 ? 0ull : (mask & ~long_lanes & gmask);
             while (__ballot(gm != 0)) {
                 int bs = -1;
                 if (gm) { bs = __ffsll((long long)gm) - 1; gm &= gm - 1; }
@@ -1847,8 +1878,8 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
                 const uint64_t me_m = smask_of(a.smask, me_id);
                 const int64_t me_pl = slot_has(me_m, t) ? slot_idx(me_m, t, a.E, 0) : -1;
-                n_walk += (lane == 0);
-                for (uint32_t off = 0; off < end - beg; off += 64)
+                n_walk += (lane == 0 && slice == 0);
+                for (uint32_t off = slice * 64; off < end - beg; off += 64 * nsl)
                     hchunk(off, (uint32_t)lane, beg, end - beg, me_id, me_g, ign_s, me_pl, hmw);
             }
         }
@@ -1924,8 +1955,10 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                   }
                 }
             };
-            const uint64_t longm = mask & long_lanes;
-            uint64_t gm = mask & ~longm & gmask;
+            had_hub = had_hub || (mask & hub_lanes) != 0;
+            const uint64_t longm = LP == 2 ? (mask & hub_lanes) : LP == 1 ? (mask & long_lanes & ~hub_lanes)
+                                                                           : (mask & long_lanes);
+            uint64_t gm = LP == 2 ? 0ull : (mask & ~long_lanes & gmask);
             while (__ballot(gm != 0)) {
                 int bs = -1;
                 if (gm) { bs = __ffsll((long long)gm) - 1; gm &= gm - 1; }
@@ -1944,8 +1977,18 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 const uint32_t me_id = (uint32_t)__shfl((int)pl, bs, 64);
                 const uint64_t wmw = (uint64_t)__shfl((long long)wm, bs, 64);
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
-                n_walk += (lane == 0);
-                for (uint32_t off = 0; off < end - beg; off += 64) pchunk(off, (uint32_t)lane, beg, end - beg, me_g, wmw);
+                n_walk += (lane == 0 && slice == 0);
+                for (uint32_t off = slice * 64; off < end - beg; off += 64 * nsl)
+                    pchunk(off, (uint32_t)lane, beg, end - beg, me_g, wmw);
+            }
+        }
+        if constexpr (LP == 1) {
+            if (had_hub && lane == 0) {
+                // every slice (one per 256 connections of the longest row made fewer,
+                // longer blocks: 25.3 against 11.0 ms, gpurun_out/r04c5j)
+                const uint32_t ns = (uint32_t)kIhSlices;
+                (void)hub_max;
+                a.hubw[atomicAdd(a.hubn, 1u)] = (blockIdx.x * 4u + (uint32_t)wid) | ((ns - 1u) << 27);
             }
         }
     }
@@ -2516,7 +2559,7 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_clist); f(d->d_clist_n); f(d->d_hidx); f(d->d_hrow); f(d->d_hlist); f(d->d_mlist); f(d->d_mloff); f(d->d_mcount); f(d->d_mmtab); f(d->d_mctab); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_clist); f(d->d_clist_n); f(d->d_hidx); f(d->d_hrow); f(d->d_hlist); f(d->d_mlist); f(d->d_mloff); f(d->d_mcount); f(d->d_mmtab); f(d->d_hubw); f(d->d_mctab); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_peertx); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
@@ -2775,6 +2818,16 @@ static bool ihave_prepare(gsim_handle* h, int64_t g, IhaveStage* st, int* rc)
     if (mm_gossip(h)) {
         a.mlist = d->d_mlist; a.mloff = d->d_mloff; a.mcount = d->d_mcount; a.mmtab = d->d_mmtab;
         a.topic_slots = (int32_t)d->cfg.topic_slots;
+        // the hub-row list: at most every wave of the launch (grow-only)
+        const int64_t need = 4 * (int64_t)(d->mmtab.empty() ? 0 : d->mmtab.back());
+        if (need > d->hubw_cap) {
+            if (d->d_hubw) { (void)hipFree(d->d_hubw); d->d_hubw = nullptr; d->hubw_cap = 0; }
+            if (hipMalloc((void**)&d->d_hubw, sizeof(uint32_t) * (size_t)(need + 1)) == hipSuccess) d->hubw_cap = need;
+        }
+        if (d->d_hubw && need > 0) {
+            a.hubw = d->d_hubw;
+            a.hubn = d->d_hubw + d->hubw_cap;
+        }
     }
     st->lds = (((size_t)d->cfg.ring + 3) & ~(size_t)3) * sizeof(uint16_t) + 4 * kRespStage * sizeof(uint64_t);
     st->lds_c = (((size_t)d->cfg.ring + 1) & ~(size_t)1) * sizeof(uint16_t) + 2 * (size_t)d->cfg.ring * 4;
@@ -2815,10 +2868,31 @@ static void launch_ihave_w(gsim_handle* h, IhaveStage* st, const IhArgs& a)
     if (a.mmtab) {
         const uint32_t grid = h->dl->mmtab.back();
         if (!grid) return;
+        const uint32_t* gc = h->dl->d_gcount;
+        if (a.hubw && W < 64) {
+            // rows of at most kIhHub connections, listing the waves with longer ones;
+            // then those rows, kIhSlices blocks of one wave per listed wave
+            uint32_t n = 0;
+            hipError_t e = hipMemsetAsync(a.hubn, 0, sizeof(uint32_t), h->stream);
+            if (e != hipSuccess) return;
+            if (a.mlat)
+                hipLaunchKernelGGL((k_ihave<W, true, true, true, 1>), dim3(grid), dim3(256), st->lds, h->stream, a, gc);
+            else
+                hipLaunchKernelGGL((k_ihave<W, false, true, true, 1>), dim3(grid), dim3(256), st->lds, h->stream, a, gc);
+            e = hipMemcpyAsync(&n, a.hubn, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+            if (e != hipSuccess || n == 0) return;
+            const uint32_t g2 = n * (uint32_t)kIhSlices;
+            if (a.mlat)
+                hipLaunchKernelGGL((k_ihave<W, true, true, true, 2>), dim3(g2), dim3(64), st->lds, h->stream, a, gc);
+            else
+                hipLaunchKernelGGL((k_ihave<W, false, true, true, 2>), dim3(g2), dim3(64), st->lds, h->stream, a, gc);
+            return;
+        }
         if (a.mlat)
-            hipLaunchKernelGGL((k_ihave<W, true, true, true>), dim3(grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)h->dl->d_gcount);
+            hipLaunchKernelGGL((k_ihave<W, true, true, true>), dim3(grid), dim3(256), st->lds, h->stream, a, gc);
         else
-            hipLaunchKernelGGL((k_ihave<W, false, true, true>), dim3(grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)h->dl->d_gcount);
+            hipLaunchKernelGGL((k_ihave<W, false, true, true>), dim3(grid), dim3(256), st->lds, h->stream, a, gc);
     } else if (a.mlat)
         hipLaunchKernelGGL((k_ihave<W, true, true>), dim3(st->grid), dim3(256), st->lds, h->stream, a, (const uint32_t*)h->dl->d_gcount);
     else if (sparse_layout(h))
