@@ -39,6 +39,9 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 SECOND = 1_000_000_000
 SALU_PEAK = 256 * 2.4e9       # scalar instructions/s: one scalar unit per CU
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# random 8-B load probes (tools/probe_random.hip, profiles/r01_probe_random_access.jsonl)
+PROBE_MISS_PER_S = 54.1e9      # 2 GB table: every load an L2 miss
+PROBE_L2_REQ_PER_S = 251.2e9   # 4 MB table: L2-resident
 ROUNDS = 10                    # propagation rounds per heartbeat
 MSG_RATE = 4.0                 # messages / s / topic
 MSG_RING = 1024                # live-message window: >= 16 heartbeats of publications, so no slot
@@ -539,22 +542,30 @@ def main():
                       "frac": deliv_gbs / HBM_PEAK_GBS, "traffic": tr_send_tick, "traffic_detail": tr_send,
                       "kernel": "delivery: k_send_tm + k_commit + k_delivery_state (per tick, 10 rounds)", "kernel_ms": deliv_ms,
                       "algorithmic_bytes_per_tick": alg_deliv}
-        # the delivery walk's actual bound: TCC requests per second (PMC, per launch of k_send_tm)
-        # against the random-access probe's ceiling
+        # the delivery walk against the random-access probes (profiles/r01_probe_random_access.jsonl):
+        # its L2 misses against random 8-B loads over a 2 GB table (every one a miss, 54 G/s), and
+        # all its TCC requests against the same loads over an L2-resident 4 MB table (251 G/s) --
+        # two ceilings a request stream cannot pass, so neither fraction can exceed 1
         rq = None if args.vdelay or sharded else load_traffic(args.config + ":send_req")
         if rq is not None and launches.get("send"):
             send_launch_ms = kms["send"] * K / launches["send"]
-            ach = rq["requests_per_launch"] / (send_launch_ms * 1e-3)
             copies_per_launch = (firsts + dups) / launches["send"] if launches["send"] else 0
-            roof_deliv["request_rate"] = {"bound": "tcc_requests", "achieved": ach, "peak": rq["ceiling_req_per_s"],
-                                          "unit": "requests/s", "frac": ach / rq["ceiling_req_per_s"],
-                                          "requests_per_launch": rq["requests_per_launch"],
-                                          "requests_per_copy": rq["requests_per_launch"] / max(1, copies_per_launch),
-                                          "l2_hit_rate": rq.get("hit_rate"),
-                                          "l2_misses_per_copy": (rq["tcc_miss"] / max(1, copies_per_launch)
-                                                                 if "tcc_miss" in rq else None),
-                                          "kernel": rq["kernel"], "kernel_ms_per_launch": send_launch_ms,
-                                          "source": rq["source"], "ceiling_source": rq["ceiling_source"]}
+            req_s = rq["requests_per_launch"] / (send_launch_ms * 1e-3)
+            miss_s = rq["tcc_miss"] / (send_launch_ms * 1e-3)
+            roof_deliv["request_bounds"] = {
+                "kernel": rq["kernel"], "kernel_ms_per_launch": send_launch_ms, "source": rq["source"],
+                "copies_per_launch": copies_per_launch,
+                "l2_misses": {"bound": "random_miss_rate", "achieved": miss_s, "peak": PROBE_MISS_PER_S,
+                              "unit": "requests/s", "frac": miss_s / PROBE_MISS_PER_S,
+                              "per_launch": rq["tcc_miss"], "per_copy": rq["tcc_miss"] / max(1, copies_per_launch),
+                              "peak_source": "random 8-B loads, 2 GB table (L2 misses): 54.1 G/s"},
+                "tcc_requests": {"bound": "l2_request_rate", "achieved": req_s, "peak": PROBE_L2_REQ_PER_S,
+                                 "unit": "requests/s", "frac": req_s / PROBE_L2_REQ_PER_S,
+                                 "per_launch": rq["requests_per_launch"],
+                                 "per_copy": rq["requests_per_launch"] / max(1, copies_per_launch),
+                                 "l2_hit_rate": rq.get("hit_rate"),
+                                 "peak_source": "random 8-B loads, L2-resident 4 MB table: 251 G/s"},
+                "probe": "profiles/r01_probe_random_access.jsonl"}
         # the heartbeat's bound: VALU issue (PMC SQ_INSTS_VALU per launch of k_heartbeat<32>) over
         # the heartbeat class's time per tick (it also holds k_fanout_heartbeat: a slight under-estimate)
         hv = None if args.vdelay or sharded else load_traffic(args.config + ":hb_valu")
@@ -607,6 +618,12 @@ def main():
             # in-process shards (GSIM_GROUP_SERIAL=1: each alone on the device): kernel ms per tick of each
             "kernel_ms_per_tick_shards": (None if per_shard is None else
                                           [round(sum(ms for ms, _ in p.values()) / K, 3) for p in per_shard]),
+            # strong scaling is set by the slowest shard (each alone on the device, in-process
+            # exchange): per-tick kernel ms of the max and mean shard
+            "shard_kernel_ms_per_tick": (None if per_shard is None else {
+                "max": max(sum(ms for ms, _ in p.values()) for p in per_shard) / K,
+                "mean": sum(sum(ms for ms, _ in p.values()) for p in per_shard) / len(per_shard) / K,
+                "summed": sum(sum(ms for ms, _ in p.values()) for p in per_shard) / K}),
             "gossip_per_tick": {k: (gossip1[k] - gossip0[k]) / K for k in gossip1},
             "census": census1,
             "roofline": dominant,

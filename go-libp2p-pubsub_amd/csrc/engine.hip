@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256) void k_ip_colocation_hub(ColocArgs a, const ui
     for (int64_t x = blockIdx.x; x < nrows; x += gridDim.x) {
         const uint32_t i = rows[x];
         const uint32_t b = a.row_ptr[i], deg = a.row_ptr[i + 1] - b;
-        if (deg > (uint32_t)kHubP6Max || deg <= a.hub_min) continue;   // (cannot happen: rows <= 4096, hubs > 64)
+        if (deg > (uint32_t)kHubP6Max || deg <= a.hub_min) continue;   // (cannot happen: launch_ip_colocation refuses longer rows)
         if (a.sharded && (i < a.olo || i >= a.ohi)) continue;
         if (a.rowflag && !a.rowflag[i]) continue;               // only rows whose tracked set changed
         __syncthreads();                                          // (every thread has read the flag)
@@ -755,6 +755,11 @@ int launch_ip_colocation(gsim_handle* h, const int32_t* gate)
         h->p6_dirty = false;
         h->p6_rows_only = false;
         return hip_check(h, e, "P6 (no shared IP)");
+    }
+    if (h->max_degree > (uint32_t)kHubP6Max) {
+        // k_ip_colocation_hub stages a row's keys in LDS (kHubP6Max of them)
+        h->err = "P6 (IP colocation) supports rows of at most 4096 connections in this build";
+        return GSIM_ERANGE;
     }
     ColocArgs c{};
     c.gate = gate;

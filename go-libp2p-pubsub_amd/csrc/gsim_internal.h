@@ -500,7 +500,7 @@ struct gsim_handle {
     double* d_p6 = nullptr;
     uint8_t* d_p6row = nullptr;       // [N] the observer's tracked set changed since its last P6
     uint32_t* d_churn = nullptr;      // gsim_set_connections scratch: [cap] pairs, [cap] edges, [2] bad / twice
-    int64_t churn_cap = 0;
+    int64_t churn_cap = 0;            // u32 words allocated at d_churn
     uint32_t* d_churn_mark = nullptr; // [E/32] connections listed in the current call (zero between calls)
     double* d_score = nullptr;
     uint8_t* d_pen = nullptr;         // pending broken-promise penalties (applyIwantPenalties), record order

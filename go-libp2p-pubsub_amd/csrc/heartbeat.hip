@@ -2784,10 +2784,11 @@ int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, i
     // handled by two threads at once), fails the call
     const int32_t n2 = 2 * count;
     hipError_t e = hipSuccess;
-    if (h->churn_cap < n2) {   // grow-only scratch: no allocation (and no hipFree sync) per call
+    const int64_t need = 2 * (int64_t)n2 + 2;   // pairs, edges, bad[2]
+    if (h->churn_cap < need) {   // grow-only scratch: no allocation (and no hipFree sync) per call
         if (h->d_churn) { (void)hipFree(h->d_churn); h->d_churn = nullptr; h->churn_cap = 0; }
-        e = hipMalloc((void**)&h->d_churn, sizeof(uint32_t) * (2 * (size_t)n2 + 2));
-        if (e == hipSuccess) h->churn_cap = n2;
+        e = hipMalloc((void**)&h->d_churn, sizeof(uint32_t) * (size_t)need);
+        if (e == hipSuccess) h->churn_cap = need;
     }
     if (e == hipSuccess && !h->d_churn_mark) {
         const size_t words = ((size_t)h->e + 31) / 32;
@@ -2859,11 +2860,12 @@ int gsim_set_subscriptions(gsim_handle* h, const uint32_t* pairs, int32_t count,
     if (!rc && !need.empty()) rc = ensure_slots(h, need.data());
     if (rc) return rc;
     ProfScope ps(h, GSIM_K_CHURN);
-    if (h->churn_cap < 2 * count) {
+    const int64_t words = 2 * (int64_t)count + 2;   // pairs, then one u64 (Leave's PX room)
+    if (h->churn_cap < words) {
         if (h->d_churn) { (void)hipFree(h->d_churn); h->d_churn = nullptr; h->churn_cap = 0; }
-        const hipError_t e = hipMalloc((void**)&h->d_churn, sizeof(uint32_t) * (4 * (size_t)count + 1));
+        const hipError_t e = hipMalloc((void**)&h->d_churn, sizeof(uint32_t) * (size_t)words);
         if (e != hipSuccess) return hip_check(h, e, "gsim_set_subscriptions");
-        h->churn_cap = 2 * count;
+        h->churn_cap = words;
     }
     hipError_t e = hipMemcpyAsync(h->d_churn, pairs, sizeof(uint32_t) * 2 * (size_t)count, hipMemcpyHostToDevice,
                                   h->stream);

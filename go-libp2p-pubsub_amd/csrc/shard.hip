@@ -623,6 +623,7 @@ struct gsim_group {
     std::vector<std::vector<uint32_t>> gid;   // per local shard: local -> global peer id (host)
     std::vector<std::vector<uint64_t>> gidx;  // per local shard: local -> global edge index (host)
     std::vector<uint64_t> sub;                // the peers' subscriptions (publish: fanout possible?)
+    std::vector<uint32_t> row_ptr;            // the global CSR rows (group readback: a range's global edges)
     int32_t ring = 0, rounds = 0;
     bool msgs = false;
     bool router_dirty = true;                 // ghost rows' router state must be re-imported
@@ -1453,6 +1454,7 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
     g->gid.assign(g->hs.size(), {});
     g->gidx.assign(g->hs.size(), {});
     g->sub.assign(subs ? subs : nullptr, subs ? subs + n : nullptr);
+    g->row_ptr.assign(row_ptr, row_ptr + n + 1);
     g->msgs = false;
     g->router_dirty = true;
     for (size_t l = 0; l < g->hs.size(); ++l) {
@@ -2164,6 +2166,102 @@ int gsim_group_profile_read(gsim_group* g, double* ms, int64_t* launches, int32_
         const int rc = gsim_profile_read(h, m.data(), c.data(), n);
         if (rc) return g->take(h, rc);
         for (int32_t i = 0; i < n; ++i) { ms[i] += m[(size_t)i]; launches[i] += c[(size_t)i]; }
+    }
+    return GSIM_OK;
+}
+
+
+// ---- group readback: the whole network's view of this process's shards ----
+// (WithPeerScoreInspect over a sharded network, score.go:152-180, 448-500)
+
+// element size of a field (include/gsim.h gsim_field) and where its peer or
+// edge axis is: 0 edge-major [..., E], 1 peer-last [..., N], 2 peer-first [N, ...]
+static int field_kind(int32_t f, size_t* es)
+{
+    switch (f) {
+    case GSIM_F_TFLAGS: case GSIM_F_ESTATE: case GSIM_F_CTL: *es = 1; return 0;
+    case GSIM_F_SEEN: case GSIM_F_LASTPUT: *es = 4; return 1;
+    case GSIM_F_LASTPUB: case GSIM_F_FANOUT_TOPICS: *es = 8; return 2;
+    default: *es = 8; return 0;
+    }
+}
+
+int gsim_group_field_bytes(gsim_group* g, int32_t field, size_t* out)
+{
+    if (!g || !out || g->hs.empty() || g->bounds.empty()) return GSIM_EINVAL;
+    gsim_handle* h = g->hs[0];
+    size_t lb = 0;
+    int rc = gsim_field_bytes(h, field, &lb);
+    if (rc) return g->take(h, rc);
+    size_t es = 0;
+    const int kind = field_kind(field, &es);
+    const size_t per = kind == 0 ? (size_t)h->e * es : (size_t)h->n * es;   // one lead row (or one peer's)
+    if (!per) return g->fail(GSIM_ESTATE, "no graph loaded");
+    *out = kind == 0 ? lb / per * (size_t)g->E * es : lb / per * (size_t)g->N * es;
+    return GSIM_OK;
+}
+
+int gsim_group_read_field(gsim_group* g, int32_t field, void* dst, size_t bytes)
+{
+    if (!g || !dst) return GSIM_EINVAL;
+    size_t want = 0;
+    int rc = gsim_group_field_bytes(g, field, &want);
+    if (rc) return rc;
+    if (bytes != want) return g->fail(GSIM_EINVAL, "destination is not the whole network's field size");
+    size_t es = 0;
+    const int kind = field_kind(field, &es);
+    uint8_t* out = static_cast<uint8_t*>(dst);
+    std::vector<uint8_t> loc;
+    for (size_t l = 0; l < g->hs.size(); ++l) {
+        gsim_handle* h = g->hs[l];
+        const ShardCtx* sc = h->sh;
+        const int k = g->ids[l];
+        size_t lb = 0;
+        if ((rc = gsim_field_bytes(h, field, &lb))) return g->take(h, rc);
+        loc.resize(lb);
+        if ((rc = gsim_read_field(h, field, loc.data(), lb))) return g->take(h, rc);
+        const int64_t g0 = g->bounds[(size_t)k], np = sc->own_hi - sc->own_lo;
+        if (kind == 0) {                         // owned rows: one contiguous run of edges
+            const size_t rows = lb / ((size_t)h->e * es), ne = (size_t)(sc->own_e_hi - sc->own_e_lo) * es;
+            for (size_t q = 0; q < rows; ++q)
+                std::memcpy(out + (q * (size_t)g->E + (size_t)sc->geid_base) * es,
+                            loc.data() + (q * (size_t)h->e + (size_t)sc->own_e_lo) * es, ne);
+        } else if (kind == 1) {
+            const size_t rows = lb / ((size_t)h->n * es);
+            for (size_t q = 0; q < rows; ++q)
+                std::memcpy(out + (q * (size_t)g->N + (size_t)g0) * es,
+                            loc.data() + (q * (size_t)h->n + (size_t)sc->own_lo) * es, (size_t)np * es);
+        } else {
+            const size_t rowb = lb / (size_t)h->n;
+            std::memcpy(out + (size_t)g0 * rowb, loc.data() + (size_t)sc->own_lo * rowb, (size_t)np * rowb);
+        }
+    }
+    return GSIM_OK;
+}
+
+int gsim_group_read_scores(gsim_group* g, double* out)
+{
+    if (!g || !out) return GSIM_EINVAL;
+    return gsim_group_read_field(g, GSIM_F_SCORE, out, sizeof(double) * (size_t)g->E);
+}
+
+int gsim_group_read_snapshot(gsim_group* g, int64_t obs_lo, int64_t obs_hi, gsim_peer_score_snapshot* peers,
+                             gsim_topic_score_snapshot* topics)
+{
+    if (!g || g->row_ptr.empty()) return GSIM_EINVAL;
+    if (obs_lo < 0 || obs_hi > g->N || obs_lo > obs_hi || (!peers && obs_hi > obs_lo))
+        return g->fail(GSIM_EINVAL, "observer range out of bounds");
+    const int64_t e0 = g->row_ptr[(size_t)obs_lo];
+    for (size_t l = 0; l < g->hs.size(); ++l) {
+        gsim_handle* h = g->hs[l];
+        const ShardCtx* sc = h->sh;
+        const int k = g->ids[l];
+        const int64_t lo = std::max(obs_lo, g->bounds[(size_t)k]), hi = std::min(obs_hi, g->bounds[(size_t)k + 1]);
+        if (lo >= hi) continue;
+        const int64_t off = (int64_t)g->row_ptr[(size_t)lo] - e0, T = std::max(1, h->t);
+        const int64_t llo = sc->own_lo + (lo - g->bounds[(size_t)k]), lhi = llo + (hi - lo);
+        const int rc = gsim_read_snapshot(h, llo, lhi, peers + off, topics ? topics + off * T : nullptr);
+        if (rc) return g->take(h, rc);
     }
     return GSIM_OK;
 }

@@ -283,18 +283,20 @@ struct Rd {
             if (!ok || depth == 0) return ok;
             const uint64_t k = varint();                     // the group's next field
             if (!ok) return false;
-            wt = (int)(k & 7);
-            if ((k >> 3) == 0) { ok = false; return false; }
+            wt = (int)(k & 7);                               // (skipRpc takes any field number here)
         }
     }
-    // the next field's number and wire type (tag checks of the generated code)
+    // the next field's number and wire type (tag checks of the generated code,
+    // rpc.pb.go:1345-1352: fieldNum := int32(wire >> 3), so a number above
+    // 2^31 is illegal and one of 2^32 + f is field f)
     bool tag(uint32_t* f, int* wt)
     {
         const uint64_t k = varint();
         if (!ok) return false;
         *wt = (int)(k & 7);
-        if ((k >> 3) == 0 || (k >> 3) > 0x1FFFFFFFu || *wt == 4) { ok = false; return false; }   // illegal tag
-        *f = (uint32_t)(k >> 3);
+        const int32_t fn = (int32_t)(uint32_t)(k >> 3);
+        if (*wt == 4 || fn <= 0) { ok = false; return false; }   // end group for non-group / illegal tag
+        *f = (uint32_t)fn;
         return true;
     }
 };

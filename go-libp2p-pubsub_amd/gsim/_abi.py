@@ -316,6 +316,10 @@ SIGNATURES = [
     ("gsim_group_synchronize", c_int32, [c_void_p]),
     ("gsim_group_profile", c_int32, [c_void_p, c_int32]),
     ("gsim_group_profile_read", c_int32, [c_void_p, c_void_p, c_void_p, c_int32]),
+    ("gsim_group_field_bytes", c_int32, [c_void_p, c_int32, POINTER(c_size_t)]),
+    ("gsim_group_read_field", c_int32, [c_void_p, c_int32, c_void_p, c_size_t]),
+    ("gsim_group_read_scores", c_int32, [c_void_p, c_void_p]),
+    ("gsim_group_read_snapshot", c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
     # gsim_wire.h
     ("gsim_wire_size", c_uint64, [POINTER(CWireRpc)]),
     ("gsim_trace_delimited", c_int32, [c_void_p, c_uint64, c_void_p, c_uint64, POINTER(c_uint64)]),

@@ -471,23 +471,28 @@ class ShardedEngine:
 
     def read(self, f: int, into: Optional[np.ndarray] = None) -> np.ndarray:
         """A field of the whole network, assembled from the owned parts of
-        every shard (every shard must be in this process).  into: an array
-        of the whole network's shape whose parts owned by this process's
-        shards are overwritten (any subset of the shards; returned)."""
+        every shard by gsim_group_read_field (every shard must be in this
+        process).  into: an array of the whole network's shape whose parts
+        owned by this process's shards are overwritten (any subset of the
+        shards; returned)."""
         from .engine import _FIELD_DTYPES
         if into is None and len(self.local) != self.shards:
             raise GsimError(_abi.GSIM_EINVAL, "the whole network's view needs every shard in this process")
         out = np.zeros(self._shape(f, self.net.n, self.net.e), dtype=_FIELD_DTYPES[f]) if into is None else into
-        for p in self.plans:
-            loc = self.read_local(p.shard, f)
-            if f in self._PEER_LAST:
-                out[..., p.bounds[p.shard]:p.bounds[p.shard + 1]] = loc[..., p.own_lo:p.own_hi]
-            elif f in self._PEER_FIRST:
-                out[p.bounds[p.shard]:p.bounds[p.shard + 1]] = loc[p.own_lo:p.own_hi]
-            else:
-                sl = p.global_edges()
-                out[..., sl] = loc[..., p.own_e_lo:p.own_e_hi]
+        assert out.flags.c_contiguous and out.dtype == _FIELD_DTYPES[f]
+        self._check(self.lib.gsim_group_read_field(self.g, int(f), _ptr(out), out.nbytes))
         return out
+
+    def snapshot(self, obs_lo: int = 0, obs_hi: Optional[int] = None):
+        """Engine.snapshot over the whole network (gsim_group_read_snapshot):
+        the global observers [obs_lo, obs_hi) of this process's shards."""
+        hi = self.net.n if obs_hi is None else obs_hi
+        ne = int(self.net.row_ptr[hi]) - int(self.net.row_ptr[obs_lo])
+        T = max(1, len(self.topics))
+        peers = np.zeros(ne, dtype=_abi.PEER_SNAPSHOT_DTYPE)
+        topics = np.zeros((ne, T), dtype=_abi.TOPIC_SNAPSHOT_DTYPE)
+        self._check(self.lib.gsim_group_read_snapshot(self.g, int(obs_lo), int(hi), _ptr(peers), _ptr(topics)))
+        return peers, topics
 
     def write(self, f: int, arr: np.ndarray):
         """Install a field given in the whole network's view on every local shard."""
@@ -508,4 +513,6 @@ class ShardedEngine:
         self._check(self.lib.gsim_group_state_written(self.g))
 
     def scores(self) -> np.ndarray:
-        return self.read(_abi.F_SCORE)
+        out = np.zeros(self.net.e, dtype=np.float64)
+        self._check(self.lib.gsim_group_read_scores(self.g, _ptr(out)))
+        return out

@@ -758,6 +758,23 @@ int gsim_group_msg_stats(gsim_group* g, int64_t* out4);
 int gsim_group_gossip_stats(gsim_group* g, int64_t* out4);
 int gsim_group_census(gsim_group* g, int64_t* out8);
 int gsim_group_synchronize(gsim_group* g);
+/* WithPeerScoreInspect over a sharded network (score.go:152-180, 448-500):
+ * the whole network's view, filled from the rows this process's shards own
+ * (every shard with gsim_group_create; one rank's range with the RCCL / host
+ * transports, the rest of dst left as it was).
+ * gsim_group_field_bytes: the size of a field for the whole network (N peers,
+ *   E edges; gsim_field_bytes's shapes).
+ * gsim_group_read_field: gsim_read_field in global peer / edge order.
+ * gsim_group_read_scores: the score snapshot, E doubles in global edge order.
+ * gsim_group_read_snapshot: gsim_read_snapshot for the global observers
+ *   [obs_lo, obs_hi): peers[x] for the x-th edge of those rows (global edge
+ *   order from row_ptr[obs_lo]), topics[x * T + t]; observer and peer are
+ *   global ids. */
+int gsim_group_field_bytes(gsim_group* g, int32_t field, size_t* out);
+int gsim_group_read_field(gsim_group* g, int32_t field, void* dst, size_t bytes);
+int gsim_group_read_scores(gsim_group* g, double* out);
+int gsim_group_read_snapshot(gsim_group* g, int64_t obs_lo, int64_t obs_hi, gsim_peer_score_snapshot* peers,
+                             gsim_topic_score_snapshot* topics);
 /* Per-kernel-class time of this process's shards (summed). */
 int gsim_group_profile(gsim_group* g, int32_t enable);
 int gsim_group_profile_read(gsim_group* g, double* ms, int64_t* launches, int32_t n);

@@ -62,6 +62,8 @@ typedef struct orc_net {
     uint8_t* px;               /* [E] peer exchange (WithPeerExchange): 1 = the row's owner tries to
                                   connect to col[e] (pxConnect), or NULL */
     struct orc_gater* gater;   /* peer gater (oracle_gater.c, orc_gater_new), or NULL */
+    struct orc_px_pend* px_pend;   /* Leave's pending PX lists (orc_px_pend_new), owned by the caller
+                                      with the network; NULL: Leave's PRUNEs carry no lists */
 } orc_net;
 
 /* ---- message propagation (oracle_deliver.c) ------------------------------ */
@@ -159,6 +161,9 @@ int32_t orc_churn(orc_net* s, const uint32_t* pairs, int32_t count, int32_t up, 
  * connections made go to pairs (dialer, peer), at most cap; returns their
  * number.  Clears the marks. */
 int64_t orc_px_connect(orc_net* s, int64_t now, uint32_t* pairs, int64_t cap);
+/* Leave's PX lists wait here until orc_px_connect: one table per network */
+struct orc_px_pend* orc_px_pend_new(void);
+void orc_px_pend_free(struct orc_px_pend* p);
 /* Join / Leave of (peer, topic) pairs between ticks (gossipsub.go:1047-1124,
  * gsim_set_subscriptions). */
 void orc_set_subscriptions(orc_net* s, const uint32_t* pairs, int32_t count, int32_t join, uint64_t tick, int64_t now,

@@ -147,19 +147,16 @@ static void px_accept(orc_net* s, uint32_t ep, const uint32_t* listed, int n)
 }
 
 /* Leave's PX lists until orc_px_connect: (pruner's edge, listed peer) per
- * entry, one table per network (keyed by its px array) */
-typedef struct px_pend { const uint8_t* key; uint64_t* ent; int64_t n, cap; } px_pend;
-static px_pend g_pxp[8];
+ * entry, in the network's own table (orc_net.px_pend) */
+typedef struct orc_px_pend { uint64_t* ent; int64_t n, cap; } px_pend;
 
-static px_pend* px_pending(const orc_net* s)
+struct orc_px_pend* orc_px_pend_new(void) { return (px_pend*)calloc(1, sizeof(px_pend)); }
+
+void orc_px_pend_free(struct orc_px_pend* p)
 {
-    for (int k = 0; k < 8; ++k)
-        if (g_pxp[k].key == s->px) return &g_pxp[k];
-    for (int k = 0; k < 8; ++k)
-        if (!g_pxp[k].key) { g_pxp[k].key = s->px; return &g_pxp[k]; }
-    g_pxp[0].n = 0;                                            /* (8 live networks at most) */
-    g_pxp[0].key = s->px;
-    return &g_pxp[0];
+    if (!p) return;
+    free(p->ent);
+    free(p);
 }
 
 static void px_emit(hb* h, uint32_t ep, int live, uint32_t purpose, uint64_t key_tick, int pend)
@@ -177,7 +174,8 @@ static void px_emit(hb* h, uint32_t ep, int live, uint32_t purpose, uint64_t key
         px_accept(s, ep, listed, n < 256 ? n : 256);
         return;
     }
-    px_pend* pp = px_pending(s);
+    px_pend* pp = s->px_pend;
+    if (!pp) return;
     for (int q = 0; q < n && q < 256; ++q) {
         if (pp->n == pp->cap) {
             pp->cap = pp->cap ? 2 * pp->cap : 256;
@@ -622,10 +620,11 @@ int32_t orc_churn(orc_net* s, const uint32_t* pairs, int32_t count, int32_t up, 
 int64_t orc_px_connect(orc_net* s, int64_t now, uint32_t* pairs, int64_t cap)
 {
     if (!s->px) return 0;
-    {   /* Leave's PRUNEs: their receivers' PX handling, with this tick's snapshot */
-        px_pend* pp = px_pending(s);
+    if (s->px_pend) {   /* Leave's PRUNEs: their receivers' PX handling, with this tick's snapshot */
+        px_pend* pp = s->px_pend;
         for (int64_t q = 0; q < pp->n;) {
             const uint32_t ep = (uint32_t)pp->ent[q];
+            if ((int64_t)ep >= s->e) { ++q; continue; }          /* (a list of another graph: cannot happen) */
             uint32_t listed[256];
             int n = 0;
             while (q < pp->n && (uint32_t)pp->ent[q] == ep && n < 256) listed[n++] = (uint32_t)(pp->ent[q++] >> 32);

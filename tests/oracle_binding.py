@@ -34,7 +34,7 @@ class OrcNet(Structure):
         ("backoff", c_void_p),
         ("pp", c_void_p), ("tp", c_void_p), ("th", c_void_p), ("gp", c_void_p),
         ("ctl", c_void_p), ("lastpub", c_void_p), ("fan_topics", c_void_p), ("direct", c_void_p),
-        ("px", c_void_p), ("gater", c_void_p),
+        ("px", c_void_p), ("gater", c_void_p), ("px_pend", c_void_p),
     ]
 
 
@@ -129,6 +129,8 @@ def load():
             "orc_gater_validate": (c_int32, [POINTER(_abi.CPeerGaterParams)]),
             "orc_gater_new": (c_void_p, [P, POINTER(_abi.CPeerGaterParams), c_void_p]),
             "orc_gater_free": (None, [c_void_p]),
+            "orc_px_pend_new": (c_void_p, []),
+            "orc_px_pend_free": (None, [c_void_p]),
             "orc_gater_round_begin": (None, [P, c_int64]),
             "orc_gater_accept": (c_int32, [P, c_uint64, c_int64, c_uint32, c_uint32, c_uint32]),
             "orc_gater_event": (None, [P, c_uint32, c_uint32, c_int32, c_int32]),
@@ -182,6 +184,8 @@ class NetState:
         self.direct = np.zeros(E, dtype=np.uint8)          # gs.direct flags (configuration, not state)
         # peer exchange attempts (WithPeerExchange), when on
         self.px = np.zeros(E, dtype=np.uint8) if (gossip is not None and gossip.PeerExchange) else None
+        # Leave's pending PX lists (oracle_net.c), owned with this network
+        self._px_pend = load().orc_px_pend_new() if self.px is not None else None
         self.rev = net.rev()
         self.p5 = np.zeros(net.n) if p5 is None else np.ascontiguousarray(p5, dtype=np.float64)
         self.ip_white = None if ip_white is None else np.ascontiguousarray(ip_white, dtype=np.uint8)
@@ -191,6 +195,14 @@ class NetState:
         self.gp = (gossip or GossipSubParams()).to_c()
         self.gater = None            # orc_gater* (enable_gater)
         self._view = None
+
+    def __del__(self):
+        try:
+            if self._px_pend:
+                load().orc_px_pend_free(self._px_pend)
+                self._px_pend = None
+        except Exception:
+            pass
 
     def view(self):
         n = self.net
@@ -215,6 +227,7 @@ class NetState:
         v.direct = _p(self.direct)
         v.px = _p(self.px)
         v.gater = self.gater
+        v.px_pend = self._px_pend
         self._view = v
         return ctypes.byref(v)
 

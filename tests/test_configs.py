@@ -361,7 +361,7 @@ def test_hub_rows_bit_exact(require_gpu, topic_slots):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("topic_slots,shards", [(0, 0), (24, 0), (0, 3), (24, 3)])
+@pytest.mark.parametrize("topic_slots,shards", [(0, 0), (24, 0), (0, 3), (24, 3), (0, 8), (24, 8)])
 def test_c5_combined_wide_hubs_zipf_churn_px_verdicts(require_gpu, topic_slots, shards):
     """C5's whole shape on one engine and on 3 shards: a plain Chung-Lu
     power law (exponent 2.5, i0 = 1) whose hubs exceed 1024 connections (up

@@ -229,3 +229,31 @@ def test_gpu_kat_reset_topic_params(require_gpu):
     eng.compute_scores()
     assert eng.scores()[0] == -100000
     eng.close()
+
+
+def test_ip_colocation_refuses_rows_over_4096(require_gpu):
+    """P6's hub kernel stages a row's IP keys in LDS (4096 of them): a row
+    of more connections with shared IPs fails the call with GSIM_ERANGE
+    instead of leaving that row's P6 stale; with one IP per peer P6 is 0
+    everywhere (no scan) and the row is accepted."""
+    from gsim.engine import GsimError, Network
+    n = 5002                                        # peer 0: a row of 5001 connections
+    leaves = np.arange(1, n, dtype=np.uint32)
+    row_ptr = np.zeros(n + 1, dtype=np.uint32)
+    row_ptr[1:] = n - 1 + np.arange(0, n, dtype=np.uint32)
+    col = np.concatenate([leaves, np.zeros(n - 1, dtype=np.uint32)])
+    ob_ = np.concatenate([np.ones(n - 1, np.uint8), np.zeros(n - 1, np.uint8)])
+    sub = np.ones(n, dtype=np.uint64)
+    params = beacon_params(1)
+    for shared in (False, True):
+        ids = (np.arange(n) // 10 if shared else np.arange(n)).astype(np.uint32)
+        net = Network(n, row_ptr, col, ob_, sub, np.arange(n + 1, dtype=np.uint32), ids, int(ids.max()) + 1)
+        with Engine(params, beacon_thresholds(), device=0) as eng:
+            eng.load_graph(net)
+            if not shared:
+                eng.compute_ip_colocation()
+                assert not eng.read(_abi.F_P6).any()
+                continue
+            with pytest.raises(GsimError) as ex:
+                eng.compute_ip_colocation()
+            assert ex.value.rc == _abi.GSIM_ERANGE

@@ -19,9 +19,10 @@ def test_snapshot_layout_matches_header():
     assert np.dtype(_abi.TOPIC_SNAPSHOT_DTYPE).itemsize == 32
 
 
-def _setup(n=1500, k=16, T=3, seed=12):
+def _setup(n=1500, k=16, T=3, seed=12, shards=0):
     from fixtures import beacon_params, sybil_ips, synthetic_state
     from gsim.engine import Engine, random_regular
+    from gsim.shard import ShardedEngine
     rng = np.random.default_rng(seed)
     net = random_regular(n, k, seed=seed, n_topics=T)
     net.ip_ptr, net.ip_ids, net.n_ips = sybil_ips(n, 0.2, 4, rng)
@@ -32,7 +33,7 @@ def _setup(n=1500, k=16, T=3, seed=12):
     st = ob.NetState(net, params, thresholds=th, gossip=gp, p5=p5)
     synthetic_state(st, rng, tick_time(0), 8 / k)
     st.estate[rng.random(net.e) < 0.03] = 0                   # some untracked edges
-    eng = Engine(params, th, gossip=gp)
+    eng = ShardedEngine(params, th, gossip=gp, shards=shards) if shards else Engine(params, th, gossip=gp)
     eng.load_graph(net)
     eng.set_app_score(p5)
     eng.set_seed(SEED)
@@ -63,12 +64,14 @@ def _check_snapshot(eng, st, net, p5, lo, hi):
 
 
 @pytest.mark.gpu
-def test_snapshot_after_refresh_and_live_after_deliveries(require_gpu):
+@pytest.mark.parametrize("shards", [0, 3])
+def test_snapshot_after_refresh_and_live_after_deliveries(require_gpu, shards):
     """Right after a refresh the snapshot's scores are the score snapshot;
     after a tick of deliveries they are the live score (the oracle's counters
     already hold every delivery), meshMessageDeliveries pending increments
-    included."""
-    rng, net, params, th, gp, p5, st, eng = _setup()
+    included.  On 3 shards through the group readback (gsim_group_read_snapshot,
+    gsim_group_read_scores): observer ranges that cross shard bounds."""
+    rng, net, params, th, gp, p5, st, eng = _setup(shards=shards)
     lib = ob.load()
     now = tick_time(1)
     eng.refresh_scores(now)
@@ -78,6 +81,10 @@ def test_snapshot_after_refresh_and_live_after_deliveries(require_gpu):
     lib.orc_compute_scores(v)
     _check_snapshot(eng, st, net, p5, 0, net.n)
     _check_snapshot(eng, st, net, p5, 100, 117)
+    if shards:
+        b = eng.bounds
+        _check_snapshot(eng, st, net, p5, int(b[1]) - 7, int(b[2]) + 5)   # across two bounds
+        assert np.array_equal(eng.scores().view(np.uint64), st.score.view(np.uint64))
     # a tick of propagation: deliveries change counters after the snapshot
     from test_delivery import _schedule
     msgs = ob.Msgs(net.n, st.T, 256, R, T0, Second)

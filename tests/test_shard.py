@@ -17,7 +17,7 @@ from test_heartbeat import tick_time
 
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("shards", [2, 4])
+@pytest.mark.parametrize("shards", [2, 4, 8])
 def test_sharded_c3_shape_bit_exact(require_gpu, shards):
     """C3's shape (random-regular k=32, 16 topics, beacon-style params and
     thresholds) at 20k peers from the device fill, 5 ticks at 4 msg/s/topic

@@ -329,6 +329,38 @@ def test_decode_rejects_malformed():
     assert wire.unmarshal(b"\x1a\x00") == wire.RPC(control=wire.ControlMessage())
 
 
+def _varint(v):
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        if v:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def test_decode_field_numbers_as_generated_code():
+    """Tag handling of gogo's generated Unmarshal (pb/rpc.pb.go:1345-1352):
+    fieldNum := int32(wire >> 3), rejected only when <= 0, so a large number
+    is an unknown field, one of 2^31 or more is illegal, and 2^32 + f wraps
+    to field f; skipRpc (rpc.pb.go:2566-2641) takes any field number inside
+    a group, field 0 included."""
+    sub = wire.marshal(wire.RPC(subscriptions=[wire.SubOpts(True, b"t")]))   # field 1, bytes
+    want = wire.unmarshal(sub)
+    body = sub[2:]
+    for fn in (0x20000000, 0x7FFFFFFF):               # unknown, above the old 29-bit cap
+        assert wire.unmarshal(_varint(fn << 3) + b"\x05" + sub) == want, fn
+    for fn in (0x80000000, 0xFFFFFFFF):               # int32 <= 0: illegal tag
+        with pytest.raises(wire.WireError):
+            wire.unmarshal(_varint(fn << 3) + b"\x05" + sub)
+    wrapped = _varint(((1 << 32) + 1) << 3 | 2) + bytes([len(body)]) + body   # field 2^32 + 1 = subscriptions
+    assert wire.unmarshal(wrapped) == want
+    group0 = b"\x9b\x01" + b"\x00\x05" + b"\x9c\x01"   # field 19 group holding field 0
+    assert wire.unmarshal(group0 + sub) == want
+
+
 def test_decode_fragments_of_fragment_rpc_function():
     """The fragments TestFragmentRPCFunction's RPCs split into
     (gossipsub_test.go:2338-2500) decode to the original's contents, in
