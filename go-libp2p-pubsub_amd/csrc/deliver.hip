@@ -1066,7 +1066,8 @@ void k_send_tm(RoundArgs a_)
                                 const int64_t ts = round_time(a, a.g);
                                 const uint64_t tm = ((uint64_t)a.g << 32) | m;
                                 if (a.tr.on(j)) a.tr.push(ts, tm, j, i, t, GSIM_TRACE_SEND_RPC, 0);
-                                if (a.tr.on(i)) a.tr.push(ts, tm, i, j, t, GSIM_TRACE_RECV_RPC, 0);
+                                // (a pushed copy's RecvRPC: only the sender's shard knows of it)
+                                if (a.tr.on_any(i)) a.tr.push(ts, tm, i, j, t, GSIM_TRACE_RECV_RPC, 0);
                             }
                             if constexpr (PUSH) {
                                 // the receiver's shard delivers it (its AcceptFrom, records, cell)
@@ -1392,7 +1393,28 @@ struct IhArgs {
     // MM hub rows (k_ihave LP 1 / 2): the listed waves (block * 4 + wave) and their count
     uint32_t* hubw;
     uint32_t* hubn;
+    // trace: the IWANT requests' RPCs (round times as RoundArgs)
+    TraceRef tr;
+    int64_t t0, hb;
+    const int64_t* roff;
 };
+
+// The IWANT of receiver p to advertiser i (handleIHave's reply, HandleRPC ->
+// sendRPC, gossipsub.go:611-627, 1195-1200) asks for message slot m: one
+// record per id of the RPC (reason 2; gsim_trace_encode joins a request's ids
+// into one ControlMeta.iwant), SendRPC at p in control round g and RecvRPC at i
+// in round g + 1, where handleIWant runs.
+__device__ __forceinline__ void trace_iwant(const IhArgs& a, uint32_t p, uint32_t i, uint32_t m)
+{
+    auto rt = [&](int64_t g) {
+        const uint32_t q = (uint32_t)g / (uint32_t)a.R;
+        return a.t0 + (int64_t)q * a.hb + a.roff[(uint32_t)g - q * (uint32_t)a.R];
+    };
+    const uint64_t tm = ((uint64_t)a.g << 32) | m;
+    const int32_t t = (int32_t)a.mtopic[m];
+    if (a.tr.on(p)) a.tr.push(rt(a.g), tm, p, i, t, GSIM_TRACE_SEND_RPC, 2);
+    if (a.tr.on_any(i)) a.tr.push(rt(a.g + 1), tm, i, p, t, GSIM_TRACE_RECV_RPC, 2);
+}
 
 // Member-major blocks: block b of a launch over topics' member ranges (table
 // tab[T+1] of first blocks) -> its topic.
@@ -1704,6 +1726,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                         const int64_t pci = a.cs.at(cb_m, t, p);
                         req = p >= a.rlo && p < a.rhi && a.gstate[re] && pci >= 0 && a.cs.cell[pci] == kUnseen64;
                         if (req) {
+                            if (a.tr.ev) trace_iwant(a, p, me_id, m);
                             const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, a.gid ? a.gid[p] : p, 0, P_PROMISE,
                                                           m, me_g);
                             atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[re]), (unsigned long long)key);
@@ -1722,6 +1745,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                             req = holds_in_window(ici >= 0 ? a.cs.cell[ici] : kUnseen64, a.g, a.lo_round, tick_round, inv,
                                                   i == origin, LAT ? a.mlat[m] : 0u);
                             if (req) {
+                                if (a.tr.ev) trace_iwant(a, me_id, i, m);
                                 const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, me_g, 0, P_PROMISE, m,
                                                               a.gid ? a.gid[i] : i);
                                 atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[e]), (unsigned long long)key);
@@ -1833,6 +1857,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                     if (ask[b]) {
                         req = cvb[b] == kUnseen64;                   // p has not seen m
                         if (req) {
+                            if (a.tr.ev) trace_iwant(a, p, me_id, m);
                             const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, pg, 0, P_PROMISE, m, me_g);
                             atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[re]), (unsigned long long)key);
                             resp = a.respond && a.gstate[e] && !ign_s && peertx_allows(a, m, e, me_id);
@@ -1901,7 +1926,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
             const uint64_t mask = __ballot(wm != 0);
             if (!mask) continue;
             const int32_t t = tb;
-            auto pchunk = [&](uint32_t off, uint32_t gl_, uint32_t beg, uint32_t deg, uint32_t me_g, uint64_t wmw) {
+            auto pchunk = [&](uint32_t off, uint32_t gl_, uint32_t beg, uint32_t deg, uint32_t me_id, uint32_t me_g, uint64_t wmw) {
                 const bool v = off + gl_ < deg;
                 const uint32_t e = beg + off + gl_;
                 uint32_t re = 0, i = 0;
@@ -1938,6 +1963,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                         req = holds_in_window(cvb[b], a.g, a.lo_round, tick_round,
                                               a.minv[m] != 0, i == a.morigin[m], LAT ? a.mlat[m] : 0u);
                         if (req) {
+                            if (a.tr.ev) trace_iwant(a, me_id, i, m);
                             const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, me_g, 0, P_PROMISE, m, ig);
                             atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[e]), (unsigned long long)key);
                             resp = a.respond && a.gstate[re] && !(a.behaviour[i] & GSIM_BEHAVE_IGNORE_IWANT) &&
@@ -1969,7 +1995,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
                 n_walk += (gl == 0 && bs >= 0);
                 const uint32_t deg = bs >= 0 ? end - beg : 0u;
-                for (uint32_t off = 0; __ballot(off < deg) != 0; off += W) pchunk(off, (uint32_t)gl, beg, deg, me_g, wmw);
+                for (uint32_t off = 0; __ballot(off < deg) != 0; off += W) pchunk(off, (uint32_t)gl, beg, deg, me_id, me_g, wmw);
             }
             for (uint64_t lm = longm; lm; lm &= lm - 1) {
                 const int bs = __builtin_ctzll(lm);
@@ -1979,7 +2005,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
                 n_walk += (lane == 0 && slice == 0);
                 for (uint32_t off = slice * 64; off < end - beg; off += 64 * nsl)
-                    pchunk(off, (uint32_t)lane, beg, end - beg, me_g, wmw);
+                    pchunk(off, (uint32_t)lane, beg, end - beg, me_id, me_g, wmw);
             }
         }
         if constexpr (LP == 1) {
@@ -2154,6 +2180,7 @@ __global__ __launch_bounds__(256) void k_ihave_pairs(IhArgs a)
                                  (nw <= L || pair_key(a.seed, (uint32_t)a.tick, p_g, 0, P_IWANT, m, i_g) <= tau_w);
                 bool resp = false;
                 if (ask) {
+                    if (a.tr.ev) trace_iwant(a, p, i, m);
                     const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, p_g, 0, P_PROMISE, m, i_g);
                     pmin = key < pmin ? key : pmin;
                     // handleIWant at i: its gate on p, IWANT-ignoring behaviour, GetForPeer's count
@@ -2356,7 +2383,8 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a_, const uint
             // handleIWant in the round before it arrives (trace.go:250-297)
             const uint32_t rp = a.col[r], rs = owner[r];
             const int32_t rt = (int32_t)a.mtopic[m];
-            if (a.tr.on(rs)) a.tr.push(round_time(a, a.g - 1), ((uint64_t)a.g << 32) | m, rs, rp, rt, GSIM_TRACE_SEND_RPC, 1);
+            // (a ghost advertiser's answers are known only at the requester's shard)
+            if (a.tr.on_any(rs)) a.tr.push(round_time(a, a.g - 1), ((uint64_t)a.g << 32) | m, rs, rp, rt, GSIM_TRACE_SEND_RPC, 1);
             if (a.tr.on(rp)) a.tr.push(round_time(a, a.g), ((uint64_t)a.g << 32) | m, rp, rs, rt, GSIM_TRACE_RECV_RPC, 1);
         }
         listed_copy(a, r, m, owner, par, claim_hi, tpa, n_acc, n_gray, n_first, s_new2);
@@ -2813,6 +2841,8 @@ static bool ihave_prepare(gsim_handle* h, int64_t g, IhaveStage* st, int* rc)
         a.gid = sh->d_gid;
     }
     a.max_ihave = h->gp.max_ihave_length;
+    a.tr = h->trace;
+    a.t0 = d->cfg.t0_ns; a.hb = d->cfg.heartbeat_ns; a.roff = d->d_roff;
     a.peertx = d->d_peertx; a.ptx_w = d->ptx_w;
     a.retrans = h->gp.gossip_retransmission;
     if (mm_gossip(h)) {

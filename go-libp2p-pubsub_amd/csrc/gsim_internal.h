@@ -382,8 +382,13 @@ struct TraceRef {
     gsim_trace_event* ev = nullptr;
     uint32_t* n = nullptr;
     int64_t cap = 0;
-    uint32_t lo = 0, hi = 0;
+    uint32_t lo = 0, hi = 0;          // traced routers this engine owns (a shard: local ids)
+    uint32_t xlo = 0, xhi = 0;        // ... and its ghosts in the traced range (a shard; else = lo, hi)
     __device__ __forceinline__ bool on(uint32_t p) const { return ev != nullptr && p >= lo && p < hi; }
+    // a traced router that may be another shard's ghost here: events only
+    // this shard knows of (the RecvRPC of a copy it pushes, the SendRPC of an
+    // IWANT answer or the RecvRPC of an IWANT request whose other end is a ghost)
+    __device__ __forceinline__ bool on_any(uint32_t p) const { return ev != nullptr && p >= xlo && p < xhi; }
     __device__ __forceinline__ void push(int64_t ts, uint64_t mid, uint32_t peer, uint32_t other, int32_t topic,
                                          uint8_t type, uint8_t reason) const
     {
@@ -530,6 +535,7 @@ struct gsim_handle {
 
 int hip_check(gsim_handle* h, hipError_t e, const char* what);
 bool field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r);
+int trace_config_local(gsim_handle* h, uint32_t peer_lo, uint32_t peer_hi, uint32_t xlo, uint32_t xhi, int64_t cap);
 int launch_ip_colocation(gsim_handle* h, const int32_t* gate = nullptr);
 int launch_refresh_scores(gsim_handle* h, int64_t now);
 int launch_compute_scores(gsim_handle* h);

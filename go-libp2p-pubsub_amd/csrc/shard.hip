@@ -28,6 +28,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <tuple>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -2263,6 +2264,66 @@ int gsim_group_read_snapshot(gsim_group* g, int64_t obs_lo, int64_t obs_hi, gsim
         const int rc = gsim_read_snapshot(h, llo, lhi, peers + off, topics ? topics + off * T : nullptr);
         if (rc) return g->take(h, rc);
     }
+    return GSIM_OK;
+}
+
+// ---- group trace (trace.go:70-530 over a sharded network) ----
+// Each shard traces the routers of [peer_lo, peer_hi) it owns, plus the
+// events only it knows of at the range's ghosts (TraceRef::on_any: the
+// RecvRPC of a copy it pushes to another shard, the SendRPC of an IWANT
+// answer from a ghost advertiser, the RecvRPC of an IWANT request to one);
+// gsim_group_trace_read merges the shards' events in global ids.
+int gsim_group_trace_config(gsim_group* g, uint32_t peer_lo, uint32_t peer_hi, int64_t cap)
+{
+    if (!g || cap < 0 || peer_lo > peer_hi || (int64_t)peer_hi > g->N) return GSIM_EINVAL;
+    for (size_t l = 0; l < g->hs.size(); ++l) {
+        gsim_handle* h = g->hs[l];
+        const ShardCtx* sc = h->sh;
+        if (cap > 0 && !sc->push)
+            return g->fail(GSIM_ESTATE, "tracing needs the copy push exchange (GSIM_SHARD_PULL is set)");
+        // local ids are in global order: a global range is one local range
+        const std::vector<uint32_t>& gid = g->gid[l];
+        const uint32_t xlo = (uint32_t)(std::lower_bound(gid.begin(), gid.end(), peer_lo) - gid.begin());
+        const uint32_t xhi = (uint32_t)(std::lower_bound(gid.begin(), gid.end(), peer_hi) - gid.begin());
+        const uint32_t lo = std::max<uint32_t>(xlo, (uint32_t)sc->own_lo);
+        const uint32_t hi = std::max(lo, std::min<uint32_t>(xhi, (uint32_t)sc->own_hi));
+        const int rc = trace_config_local(h, lo, hi, xlo, xhi, cap);
+        if (rc) return g->take(h, rc);
+    }
+    return GSIM_OK;
+}
+
+int gsim_group_trace_read(gsim_group* g, gsim_trace_event* out, int64_t cap, int64_t* n)
+{
+    if (!g || !n) return GSIM_EINVAL;
+    *n = 0;
+    std::vector<int64_t> cnt(g->hs.size(), 0);
+    int64_t total = 0;
+    for (size_t l = 0; l < g->hs.size(); ++l) {            // the counts first: nothing consumed
+        const int rc = gsim_trace_read(g->hs[l], nullptr, 0, &cnt[l]);
+        if (rc) return g->take(g->hs[l], rc);
+        total += cnt[l];
+    }
+    *n = total;
+    if (!out) return GSIM_OK;
+    if (total > cap) return g->fail(GSIM_ERANGE, "output buffer too small for the traced events");
+    int64_t off = 0;
+    for (size_t l = 0; l < g->hs.size(); ++l) {
+        int64_t got = 0;
+        const int rc = gsim_trace_read(g->hs[l], out + off, cnt[l], &got);
+        if (rc) return g->take(g->hs[l], rc);
+        const std::vector<uint32_t>& gid = g->gid[l];
+        for (int64_t q = off; q < off + got; ++q) {          // local -> global ids
+            out[q].peer = gid[out[q].peer];
+            out[q].other = gid[out[q].other];
+        }
+        off += got;
+    }
+    *n = off;
+    std::sort(out, out + off, [](const gsim_trace_event& a, const gsim_trace_event& b) {
+        return std::tie(a.timestamp_ns, a.peer, a.type, a.other, a.reason, a.topic, a.msg_id) <
+               std::tie(b.timestamp_ns, b.peer, b.type, b.other, b.reason, b.topic, b.msg_id);
+    });
     return GSIM_OK;
 }
 

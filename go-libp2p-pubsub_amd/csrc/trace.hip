@@ -91,9 +91,18 @@ extern "C" {
 int gsim_trace_config(gsim_handle* h, uint32_t peer_lo, uint32_t peer_hi, int64_t cap)
 {
     if (!h) return GSIM_EINVAL;
+    if (h->sh) { h->err = "a shard traces through gsim_group_trace_config (global ids)"; return GSIM_ESTATE; }
+    return trace_config_local(h, peer_lo, peer_hi, peer_lo, peer_hi, cap);
+}
+
+}  // extern "C"
+
+// Trace the local routers [lo, hi) (owned) and accept events of [xlo, xhi)
+// (owned and ghosts) where only this engine knows of them (TraceRef::on_any).
+int trace_config_local(gsim_handle* h, uint32_t peer_lo, uint32_t peer_hi, uint32_t xlo, uint32_t xhi, int64_t cap)
+{
     if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
-    if (h->sh) { h->err = "tracing runs on a single engine, not a shard"; return GSIM_ESTATE; }
-    if (cap < 0 || peer_lo > peer_hi || (int64_t)peer_hi > h->n) return GSIM_EINVAL;
+    if (cap < 0 || peer_lo > peer_hi || (int64_t)peer_hi > h->n || xlo > xhi || (int64_t)xhi > h->n) return GSIM_EINVAL;
     (void)hipStreamSynchronize(h->stream);
     trace_free(h);
     if (cap == 0) return GSIM_OK;
@@ -110,9 +119,13 @@ int gsim_trace_config(gsim_handle* h, uint32_t peer_lo, uint32_t peer_hi, int64_
     t.cap = std::min<int64_t>(cap, 0xFFFFFFFFll);
     t.lo = peer_lo;
     t.hi = peer_hi;
+    t.xlo = xlo;
+    t.xhi = xhi;
     h->trace = t;
     return GSIM_OK;
 }
+
+extern "C" {
 
 int gsim_trace_read(gsim_handle* h, gsim_trace_event* out, int64_t cap, int64_t* n)
 {

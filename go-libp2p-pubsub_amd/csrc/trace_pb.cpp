@@ -68,10 +68,15 @@ struct Enc {
     }
 
     // A message RPC (RECV_RPC / SEND_RPC) of the records [k0, k1): RPCMeta of
-    // its messages, MessageMeta{messageID, topic} each (trace.go:326-345)
+    // its messages, MessageMeta{messageID, topic} each (trace.go:326-345);
+    // an IWANT request (reason 2): RPCMeta.control = ControlMeta{iwant =
+    // [ControlIWantMeta{messageIDs}]} (trace.go:362-414), one IWANT per RPC
+    // (handleIHave, gossipsub.go:692-697)
     uint64_t mmeta(const gsim_trace_event& e) const { return ld(8) + ld(topic_len(e.topic)); }
+    static uint64_t iwmeta(int64_t k0, int64_t k1) { return (uint64_t)(k1 - k0) * ld(8); }
     uint64_t meta(const gsim_trace_event* ev, int64_t k0, int64_t k1) const
     {
+        if (ev[k0].reason == 2) return ld(ld(iwmeta(k0, k1)));      // control { iwant { ids } }
         uint64_t s = 0;
         for (int64_t k = k0; k < k1; ++k) s += ld(mmeta(ev[k]));
         return s;
@@ -91,12 +96,14 @@ struct Enc {
 bool is_rpc(const gsim_trace_event& e) { return e.type == GSIM_TRACE_RECV_RPC || e.type == GSIM_TRACE_SEND_RPC; }
 
 // the records one TraceEvent covers: [k, end) -- an IWANT answer's messages
-// (reason 1) to one peer in one round are one RPC, everything else one record
+// (reason 1) or an IWANT request's ids (reason 2) to one peer in one round
+// are one RPC, everything else one record
 int64_t unit_end(const gsim_trace_event* ev, int64_t n, int64_t k)
 {
     int64_t q = k + 1;
-    if (is_rpc(ev[k]) && ev[k].reason == 1)
-        while (q < n && ev[q].type == ev[k].type && ev[q].reason == 1 && ev[q].timestamp_ns == ev[k].timestamp_ns &&
+    if (is_rpc(ev[k]) && (ev[k].reason == 1 || ev[k].reason == 2))
+        while (q < n && ev[q].type == ev[k].type && ev[q].reason == ev[k].reason &&
+               ev[q].timestamp_ns == ev[k].timestamp_ns &&
                ev[q].peer == ev[k].peer && ev[q].other == ev[k].other)
             ++q;
     return q;
@@ -183,6 +190,16 @@ extern "C" int gsim_trace_encode(const gsim_trace_event* ev, int64_t n, const gs
             put_peer(w, c, 1, e.other);                      // receivedFrom / sendTo
             w.tag(2, 2);                                     // meta
             w.varint(c.meta(ev, k, k1));
+            if (e.reason == 2) {                             // RPCMeta.control = 3 { iwant = 2 { messageIDs = 1 } }
+                const uint64_t iw = Enc::iwmeta(k, k1);
+                w.tag(3, 2);
+                w.varint(ld(iw));
+                w.tag(2, 2);
+                w.varint(iw);
+                for (int64_t q = k; q < k1; ++q) put_mid(w, 1, ev[q].msg_id);
+                k = k1;
+                continue;
+            }
             for (int64_t q = k; q < k1; ++q) {               // RPCMeta.messages = 1
                 w.tag(1, 2);
                 w.varint(c.mmeta(ev[q]));

@@ -320,6 +320,8 @@ SIGNATURES = [
     ("gsim_group_read_field", c_int32, [c_void_p, c_int32, c_void_p, c_size_t]),
     ("gsim_group_read_scores", c_int32, [c_void_p, c_void_p]),
     ("gsim_group_read_snapshot", c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
+    ("gsim_group_trace_config", c_int32, [c_void_p, c_uint32, c_uint32, c_int64]),
+    ("gsim_group_trace_read", c_int32, [c_void_p, c_void_p, c_int64, POINTER(c_int64)]),
     # gsim_wire.h
     ("gsim_wire_size", c_uint64, [POINTER(CWireRpc)]),
     ("gsim_trace_delimited", c_int32, [c_void_p, c_uint64, c_void_p, c_uint64, POINTER(c_uint64)]),

@@ -378,6 +378,21 @@ class ShardedEngine:
         self._check(self.lib.gsim_group_px_connect(self.g, int(now), _ptr(out), int(cap), ctypes.byref(n)))
         return out[:min(n.value, cap)].copy()
 
+    def trace_config(self, peer_lo: int, peer_hi: int, cap: int = 1 << 20):
+        """Trace the routers [peer_lo, peer_hi) (global ids) over the shards
+        (gsim_group_trace_config; cap 0 stops)."""
+        self._check(self.lib.gsim_group_trace_config(self.g, int(peer_lo), int(peer_hi), int(cap)))
+
+    def trace_read(self) -> np.ndarray:
+        """Engine.trace_read over the shards of this process, in global ids
+        (gsim_group_trace_read)."""
+        from .engine import Engine
+        n = ctypes.c_int64(0)
+        self._check(self.lib.gsim_group_trace_read(self.g, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, dtype=Engine.TRACE_DTYPE)
+        self._check(self.lib.gsim_group_trace_read(self.g, _ptr(out) if n.value else None, n.value, ctypes.byref(n)))
+        return out[:n.value]
+
     def msg_stats(self) -> list:
         out = np.zeros(4, dtype=np.int64)
         self._check(self.lib.gsim_group_msg_stats(self.g, _ptr(out)))

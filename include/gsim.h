@@ -452,15 +452,20 @@ int gsim_census(gsim_handle* h, int64_t* out8);
  *                     advertiser's IWANT answers to one requester in a round
  *                     are one RPC (handleIWant, gossipsub.go:700-739): reason
  *                     1, sent the round before they arrive, one record per
- *                     message (gsim_trace_encode joins them).  The
+ *                     message (gsim_trace_encode joins them); reason 2:
+ *                     handleIHave's IWANT request (HandleRPC -> sendRPC,
+ *                     gossipsub.go:611-627), SEND_RPC at the requester in
+ *                     control round 0 and RECV_RPC at the advertiser in round
+ *                     1, one record per requested id (encoded as one
+ *                     ControlMeta.iwant; ids in (topic, id) order).  The
  *                     heartbeat's control / IHAVE RPCs are traced from their
  *                     encoding (gsim_trace_rpc_encode, include/gsim_wire.h)
  *   JOIN / LEAVE      gsim_set_subscriptions (1047-1124)
  *   GRAFT / PRUNE     the router adds / drops a mesh link: heartbeat,
  *                     handleGraft, handlePrune (468-520)
- * Not produced: DROP_RPC (no outbound queue is modelled) and the IWANT
- * requests' RPCs.  Copies dropped by AcceptFrom produce no message event, as
- * in pushMsg. */
+ * Not produced: DROP_RPC (no outbound queue is modelled, so no RPC is
+ * dropped: doDropRPC needs a full queue, gossipsub.go:1185-1200).  Copies
+ * dropped by AcceptFrom produce no message event, as in pushMsg. */
 #define GSIM_TRACE_PUBLISH_MESSAGE   0
 #define GSIM_TRACE_REJECT_MESSAGE    1
 #define GSIM_TRACE_DUPLICATE_MESSAGE 2
@@ -486,7 +491,7 @@ typedef struct gsim_trace_event {
 } gsim_trace_event;
 
 /* Start tracing the routers [peer_lo, peer_hi) into a device buffer of cap
- * events (0: stop and free it). */
+ * events (0: stop and free it).  A shard of a group: gsim_group_trace_config. */
 int gsim_trace_config(gsim_handle* h, uint32_t peer_lo, uint32_t peer_hi, int64_t cap);
 
 /* The events traced since the last call, sorted by (timestamp, peer, type,
@@ -775,6 +780,12 @@ int gsim_group_read_field(gsim_group* g, int32_t field, void* dst, size_t bytes)
 int gsim_group_read_scores(gsim_group* g, double* out);
 int gsim_group_read_snapshot(gsim_group* g, int64_t obs_lo, int64_t obs_hi, gsim_peer_score_snapshot* peers,
                              gsim_topic_score_snapshot* topics);
+/* gsim_trace_config / gsim_trace_read over a sharded network: the routers
+ * [peer_lo, peer_hi) (global ids) that this process's shards own, every
+ * event in global ids, sorted as gsim_trace_read sorts.  Needs the copy push
+ * exchange (the default). */
+int gsim_group_trace_config(gsim_group* g, uint32_t peer_lo, uint32_t peer_hi, int64_t cap);
+int gsim_group_trace_read(gsim_group* g, gsim_trace_event* out, int64_t cap, int64_t* n);
 /* Per-kernel-class time of this process's shards (summed). */
 int gsim_group_profile(gsim_group* g, int32_t enable);
 int gsim_group_profile_read(gsim_group* g, double* ms, int64_t* launches, int32_t n);

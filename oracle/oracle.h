@@ -228,6 +228,8 @@ enum {
                                 mid: the pruned peer, g: its rank in the list (makePrune) */
     ORC_EV_RPC_MSG = 20,     /* a: sender, b: receiver, mid, topic, g: the round it arrives in,
                                 x: 0 a forwarded copy (sent in g), 1 an IWANT answer (sent in g - 1) */
+    ORC_EV_RPC_IWANT = 21,   /* a: requester, b: advertiser, mid, topic, g: the round the IWANT is sent
+                                in (handleIHave's reply, gossipsub.go:611-627); it arrives in g + 1 */
 };
 typedef struct orc_event { int32_t kind, topic; uint32_t a, b; int64_t g; uint64_t mid; int64_t x; } orc_event;
 void    orc_msgs_log(orc_msgs* m, int32_t on);

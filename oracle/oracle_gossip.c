@@ -344,6 +344,7 @@ void orc_gossip_ihave(orc_net* s, orc_msgs* m, int64_t g)
             orc_log(m, ORC_EV_PROMISE, (uint32_t)pr, i, ps, 0, g, now);
             promise_add(p, (uint32_t)pr, e, ps, m->mid ? m->mid[ps] : ps, now + gp->iwant_followup_time_ns);
             for (int q = 0; q < iask; ++q) {                         /* IWANT to i */
+                orc_log(m, ORC_EV_RPC_IWANT, (uint32_t)pr, i, want[q].v, (int32_t)m->topic[want[q].v], g, 0);
                 if (p->niw == p->capiw) {
                     p->capiw = p->capiw ? 2 * p->capiw : 1024;
                     p->iw = (iwant_ent*)realloc(p->iw, sizeof(iwant_ent) * (size_t)p->capiw);

@@ -315,7 +315,7 @@ ORC_BEHAVE_IGNORE_IWANT = 0x01   # oracle.h: never answers IWANT
 # oracle.h ORC_EV_*: the network oracle's event log
 EV_PUT, EV_SEEN, EV_SERVE, EV_PROMISE, EV_FULFILL, EV_BROKEN, EV_PENALTIES, EV_HEARTBEAT, EV_GOSSIP_ID = range(1, 10)
 EV_REJECT_SIG, EV_PUBLISH, EV_GRAFT, EV_PRUNE, EV_ADD_PEER, EV_REMOVE_PEER = range(10, 16)
-EV_THROTTLE, EV_JOIN, EV_LEAVE, EV_PX_PEER, EV_RPC_MSG = range(16, 21)
+EV_THROTTLE, EV_JOIN, EV_LEAVE, EV_PX_PEER, EV_RPC_MSG, EV_RPC_IWANT = range(16, 22)
 EVENT_DTYPE = np.dtype([("kind", np.int32), ("topic", np.int32), ("a", np.uint32), ("b", np.uint32),
                         ("g", np.int64), ("mid", np.uint64), ("x", np.int64)])
 

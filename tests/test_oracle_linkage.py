@@ -65,7 +65,7 @@ def test_network_oracle_matches_pinned_structures():
     tc = [lib.orc_tcache_new(0, 120 * Second) for _ in range(n)]
     gt = [lib.orc_gtracer_new(gp.IWantFollowupTime) for _ in range(n)]
     kinds = ev["kind"]
-    seen = {k: 0 for k in range(1, 21)}
+    seen = {k: 0 for k in range(1, 22)}
     buf = (ctypes.c_uint64 * 256)()
     peers = (ctypes.c_uint32 * 256)()
     counts = (ctypes.c_int32 * 256)()

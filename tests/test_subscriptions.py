@@ -218,8 +218,7 @@ def test_join_leave_bit_exact(require_gpu, topic_slots, shards, px):
         eng.load_graph(net)
         eng.set_seed(TSEED)
         st.push_to_engine(eng)
-    run_parity(net, params, th, gp, st, ticks, sched, ring=256, subs=subs, trace=None if shards else (0, n),
+    run_parity(net, params, th, gp, st, ticks, sched, ring=256, subs=subs, trace=(0, n),
                trace_log=log, topic_slots=topic_slots, eng=eng)
-    if not shards:
-        total = np.sum(log, axis=0)
-        assert total[_abi.TRACE_JOIN] > 0 and total[_abi.TRACE_LEAVE] > 0
+    total = np.sum([x[0] for x in log], axis=0)
+    assert total[_abi.TRACE_JOIN] > 0 and total[_abi.TRACE_LEAVE] > 0

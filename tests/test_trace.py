@@ -46,7 +46,7 @@ def _rpc_units(recs):
     while k < len(recs):
         q = k + 1
         r = recs[k]
-        if int(r["type"]) in (_abi.TRACE_RECV_RPC, _abi.TRACE_SEND_RPC) and int(r["reason"]) == 1:
+        if int(r["type"]) in (_abi.TRACE_RECV_RPC, _abi.TRACE_SEND_RPC) and int(r["reason"]) in (1, 2):
             while q < len(recs) and all(recs[q][f] == r[f] for f in ("type", "reason", "timestamp", "peer", "other")):
                 q += 1
         out.append(recs[k:q])
@@ -74,6 +74,10 @@ def _expected_batch(recs, names, peer_ids, proto=b"/meshsub/1.1.0"):
                 x.receivedFrom = other
             else:
                 x.sendTo = other
+            if int(r["reason"]) == 2:
+                # an IWANT request: RPCMeta.control.iwant = [ControlIWantMeta{messageIDs}]
+                x.meta.control.iwant.add().messageIDs.extend(int(y["msg_id"]).to_bytes(8, "big") for y in unit)
+                continue
             for y in unit:
                 mm = x.meta.messages.add()
                 mm.messageID = int(y["msg_id"]).to_bytes(8, "big")
@@ -116,11 +120,13 @@ def _random_records(rng, n, T, N):
         recs[k]["other"] = rng.integers(0, N)
         recs[k]["msg_id"] = int(rng.integers(0, 1 << 63))
         recs[k]["topic"] = -1 if typ in (4, 5) else rng.integers(0, T)
-        recs[k]["reason"] = rng.integers(1, 5) if typ == 1 else rng.integers(0, 2) if typ in (6, 7) else 0
-        if typ in (6, 7) and recs[k]["reason"] == 1 and k > 0 and rng.random() < 0.6:
-            # another message of the same IWANT answer
-            for f in ("type", "timestamp", "peer", "other", "reason"):
+        recs[k]["reason"] = rng.integers(1, 5) if typ == 1 else rng.integers(0, 3) if typ in (6, 7) else 0
+        if typ in (6, 7) and recs[k]["reason"] in (1, 2) and k > 0 and rng.random() < 0.6:
+            # another message of the same IWANT answer / another id of the same IWANT request
+            for f in ("type", "timestamp", "peer", "other"):
                 recs[k][f] = recs[k - 1][f] if recs[k - 1]["type"] == typ else recs[k][f]
+            if recs[k - 1]["type"] == typ and recs[k - 1]["reason"] in (1, 2):
+                recs[k]["reason"] = recs[k - 1]["reason"]
     return recs
 
 
@@ -208,8 +214,11 @@ def test_oracle_log_follows_tracer_rules():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lo,hi", [(0, 1000), (137, 400)])
-def test_trace_bit_exact(require_gpu, lo, hi):
+@pytest.mark.parametrize("lo,hi,shards", [(0, 1000, 0), (137, 400, 0), (0, 1000, 3), (137, 400, 2)])
+def test_trace_bit_exact(require_gpu, lo, hi, shards):
+    """Every event type the engine produces, IWANT requests (reason 2) and
+    answers (reason 1) included, equals the oracle's log; on 2 / 3 shards
+    through gsim_group_trace_* (a range that starts and ends inside shards)."""
     from fixtures import beacon_params, synthetic_state
     from gsim.engine import random_regular
     from tickrun import run_parity, subscribed_schedule
@@ -229,10 +238,19 @@ def test_trace_bit_exact(require_gpu, lo, hi):
     down = und[rng.choice(len(und), size=len(und) // 30, replace=False)]
     churn = {2: [(down, False)], 4: [(down, True)]}
     log = []
-    run_parity(net, params, th, gp, st, ticks, sched, ring=512, churn=churn, trace=(lo, hi), trace_log=log)
-    total = np.sum(log, axis=0)
+    eng = None
+    if shards:
+        from gsim.shard import ShardedEngine
+        eng = ShardedEngine(params, th, gossip=gp, shards=shards)
+        eng.load_graph(net)
+        eng.set_seed(SEED)
+        st.push_to_engine(eng)
+    run_parity(net, params, th, gp, st, ticks, sched, ring=512, churn=churn, trace=(lo, hi), trace_log=log, eng=eng)
+    total = np.sum([x[0] for x in log], axis=0)
     for typ in (0, 1, 2, 3, 4, 5, 6, 7, 11, 12):
         assert total[typ] > 0, f"event type {typ} traced"
+    reasons = np.sum([x[1] for x in log], axis=0)
+    assert reasons[1] > 0 and reasons[2] > 0, "IWANT answers and requests traced"
 
 
 def _random_rpc(rng, P):

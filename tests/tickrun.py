@@ -45,6 +45,14 @@ def oracle_trace(ev, msgs, lo, hi):
             if lo <= b < hi:
                 out.append((msgs.round_time(g), mid, b, a, topic, _abi.TRACE_RECV_RPC, x))
             continue
+        if kind == ob.EV_RPC_IWANT:
+            # handleIHave's IWANT (reason 2): sent in control round g, handled in g + 1
+            g = int(e["g"])
+            if lo <= a < hi:
+                out.append((msgs.round_time(g), mid, a, b, topic, _abi.TRACE_SEND_RPC, 2))
+            if lo <= b < hi:
+                out.append((msgs.round_time(g + 1), mid, b, a, topic, _abi.TRACE_RECV_RPC, 2))
+            continue
         if not (lo <= a < hi):
             continue
         if kind == ob.EV_PUBLISH:
@@ -160,7 +168,9 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
                     assert len(bad) == 0, (f"trace field {f} differs at tick {kk}: first at {bad[:1]}: "
                                            f"{got[max(0, bad[0] - 2):bad[0] + 3]} vs {want[max(0, bad[0] - 2):bad[0] + 3]}")
                 if trace_log is not None:
-                    trace_log.append(np.bincount(want["type"], minlength=13))
+                    rpc = (want["type"] == _abi.TRACE_SEND_RPC) | (want["type"] == _abi.TRACE_RECV_RPC)
+                    trace_log.append((np.bincount(want["type"], minlength=13),
+                                      np.bincount(want["reason"][rpc], minlength=3)))
             if gater is not None:
                 got, want = eng.gater_read(), st.gater_read()
                 for f in want:
