@@ -287,7 +287,9 @@ __device__ __forceinline__ bool gater_accept(const RoundArgs& a, uint32_t i, uin
     const double total = del + g.dw * g.dup[q] + g.iw * g.ign[q] + g.rw * g.rej[q];
     if (total == 0) return true;
     const double thr = (1 + del) / (1 + total);
-    const u32x4 x = philox4x32_10((uint32_t)a.g, i, (m << 8) | P_GATER, j, (uint32_t)g.seed, (uint32_t)(g.seed >> 32));
+    // (a shard: the draw keys on global ids, as the single engine's)
+    const uint32_t ig = g.gid ? g.gid[i] : i, jg = g.gid ? g.gid[j] : j;
+    const u32x4 x = philox4x32_10((uint32_t)a.g, ig, (m << 8) | P_GATER, jg, (uint32_t)g.seed, (uint32_t)(g.seed >> 32));
     const uint64_t r53 = ((uint64_t)x.x << 21) | (x.y >> 11);
     if ((double)r53 * (1.0 / 9007199254740992.0) < thr) return true;
     for (int32_t q2 = 0; q2 < g.P; ++q2) g.prom[(int64_t)q2 * a.E + ei] = 0xFFFFFFFFu;
@@ -2267,7 +2269,8 @@ __device__ __forceinline__ void atomic_mcnt_inc(uint8_t* mcnt, int64_t ir, doubl
 // A record can receive several copies in one launch: counters are atomic.
 __device__ __forceinline__ void listed_copy(const RoundArgs& a, uint32_t r, uint32_t m, const uint32_t* owner,
                                             uint32_t par, uint32_t claim_hi, ctp_t tpa, unsigned long long& n_acc,
-                                            unsigned long long& n_gray, unsigned long long& n_first, uint32_t* s_new2)
+                                            unsigned long long& n_gray, unsigned long long& n_first, uint32_t* s_new2,
+                                            bool iwant_rpc)
 {
     const uint8_t ds = a.dstate[r];
     if (!(ds & GSIM_DS_ACCEPT)) { n_gray++; return; }        // AcceptFrom
@@ -2279,7 +2282,7 @@ __device__ __forceinline__ void listed_copy(const RoundArgs& a, uint32_t r, uint
     // the peer gater (gater_accept): one draw per IWANT answer RPC -- (round,
     // receiver, sender), the slot left out (AcceptFrom runs per RPC, pubsub.go);
     // a shard's pushed copies are forwarded messages, one RPC each
-    if (a.gt.act && !gater_accept(a, p, r, a.sharded ? m : kGaterRpcSlot, i)) return;
+    if (a.gt.act && !gater_accept(a, p, r, iwant_rpc ? kGaterRpcSlot : m, i)) return;
     if (a.subdyn && !((a.sub[p] >> (int32_t)a.mtopic[m]) & 1ull)) return;   // a topic p left
     if (a.gt.act) gater_copy(a, r, a.minv[m] == GSIM_VERDICT_SIGNATURE);
     n_acc++;
@@ -2387,7 +2390,7 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a_, const uint
             if (a.tr.on_any(rs)) a.tr.push(round_time(a, a.g - 1), ((uint64_t)a.g << 32) | m, rs, rp, rt, GSIM_TRACE_SEND_RPC, 1);
             if (a.tr.on(rp)) a.tr.push(round_time(a, a.g), ((uint64_t)a.g << 32) | m, rp, rs, rt, GSIM_TRACE_RECV_RPC, 1);
         }
-        listed_copy(a, r, m, owner, par, claim_hi, tpa, n_acc, n_gray, n_first, s_new2);
+        listed_copy(a, r, m, owner, par, claim_hi, tpa, n_acc, n_gray, n_first, s_new2, true);
     }
     n_acc = wave_sum_u64(n_acc);
     n_gray = wave_sum_u64(n_gray);
@@ -3137,6 +3140,12 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
     if (a.push && a.mlat)
         hipLaunchKernelGGL((k_send_tm<kPushTB, true, true, false, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
                            h->stream, a);
+    else if (a.push && a.gt.act && sp)
+        hipLaunchKernelGGL((k_send_tm<kPushTB, false, true, true, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
+                           h->stream, a);
+    else if (a.push && a.gt.act)
+        hipLaunchKernelGGL((k_send_tm<kPushTB, false, false, true, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
+                           h->stream, a);
     else if (a.push && sp)
         hipLaunchKernelGGL((k_send_tm<kPushTB, false, true, false, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
                            h->stream, a);
@@ -3377,14 +3386,14 @@ __global__ __launch_bounds__(256, GSIM_XB_WPE) void k_xbits_deliver(RoundArgs a_
             for (uint32_t j0 = 0; j0 < total; j0 += 64) {
                 if (j0 + lane < total)
                     listed_copy(a, (uint32_t)(sq.gbase + lst[j0 + lane]), m, owner, par, claim_hi, tpa, n_acc, n_gray,
-                                n_first, s_new2);
+                                n_first, s_new2, false);
             }
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // lst is rewritten by the next task
         } else {
             for (uint64_t b = bits; b; b &= b - 1)
                 listed_copy(a, (uint32_t)(rb + __builtin_ctzll(b)), m, owner, par, claim_hi, tpa, n_acc, n_gray, n_first,
-                            s_new2);
+                            s_new2, false);
         }
     }
     n_acc = wave_sum_u64(n_acc);

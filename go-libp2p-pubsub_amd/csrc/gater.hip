@@ -201,6 +201,7 @@ GaterRef gater_ref(gsim_handle* h)
     r.seed = gsim_get_seed(h);
     r.n_thr = g->n_thr;
     r.direct = h->d_direct;
+    r.gid = h->sh ? h->sh->d_gid : nullptr;
     return r;
 }
 
@@ -304,7 +305,6 @@ int gsim_set_peer_gater(gsim_handle* h, const gsim_peer_gater_params* p, const d
     char buf[160];
     if (gsim_validate_peer_gater_params(p, buf, sizeof buf) != GSIM_OK) { h->err = buf; return GSIM_EINVAL; }
     if (h->e == 0 || !h->dl) { h->err = "gsim_set_peer_gater needs a loaded graph and gsim_msgs_init"; return GSIM_ESTATE; }
-    if (h->sh) { h->err = "the peer gater runs on a single engine, not a shard"; return GSIM_ESTATE; }
     if (p->decay_interval_ns != h->gp.heartbeat_interval_ns) {
         h->err = "the peer gater's DecayInterval must equal the heartbeat interval (decayStats runs at every refresh)";
         return GSIM_ESTATE;

@@ -419,6 +419,7 @@ struct GaterRef {
     const uint8_t* direct = nullptr;     // [E] edge order: gs.direct (AcceptFrom: AcceptAll)
     uint32_t* prom = nullptr;            // [P][E] IWANT promises (ThrottlePeer forgets the peer's)
     int32_t P = 0;
+    const uint32_t* gid = nullptr;       // a shard: global id of each local peer (the draw's key)
 };
 
 }  // namespace gsim

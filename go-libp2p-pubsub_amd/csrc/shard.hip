@@ -2327,4 +2327,53 @@ int gsim_group_trace_read(gsim_group* g, gsim_trace_event* out, int64_t cap, int
     return GSIM_OK;
 }
 
+// ---- the peer gater over a sharded network (peer_gater.go) ----
+// Every router's gate lives with its row, on the shard that owns it: the
+// copies it receives are gated there -- in place for a copy from an owned
+// sender, at the receiving shard's bit apply for a pushed one -- with the
+// draw keyed on global ids, so the drops are the single engine's.
+int gsim_group_set_peer_gater(gsim_group* g, const gsim_peer_gater_params* p, const double* topic_weights)
+{
+    if (!g || !p) return GSIM_EINVAL;
+    for (gsim_handle* h : g->hs) {
+        (void)hipSetDevice(h->device);
+        const int rc = gsim_set_peer_gater(h, p, topic_weights);
+        if (rc) return g->take(h, rc);
+    }
+    return GSIM_OK;
+}
+
+int gsim_group_gater_throttled(gsim_group* g, int64_t* out)
+{
+    if (!g || !out) return GSIM_EINVAL;
+    return group_sum(g, gsim_gater_throttled, 1, out);
+}
+
+int gsim_group_gater_read(gsim_group* g, double* validate, double* throttle, int64_t* last, double* counters4,
+                          int32_t* connected, int64_t* expire)
+{
+    if (!g) return GSIM_EINVAL;
+    for (size_t l = 0; l < g->hs.size(); ++l) {
+        gsim_handle* h = g->hs[l];
+        const ShardCtx* sc = h->sh;
+        const int k = g->ids[l];
+        const size_t n = (size_t)h->n, e = (size_t)h->e;
+        std::vector<double> v(n), t(n), c4(4 * e);
+        std::vector<int64_t> la(n), ex(e);
+        std::vector<int32_t> co(e);
+        const int rc = gsim_gater_read(h, v.data(), t.data(), la.data(), c4.data(), co.data(), ex.data());
+        if (rc) return g->take(h, rc);
+        const size_t g0 = (size_t)g->bounds[(size_t)k], np = (size_t)(sc->own_hi - sc->own_lo);
+        const size_t ge = (size_t)sc->geid_base, ne = (size_t)(sc->own_e_hi - sc->own_e_lo), le = (size_t)sc->own_e_lo;
+        if (validate) std::memcpy(validate + g0, v.data() + sc->own_lo, np * 8);
+        if (throttle) std::memcpy(throttle + g0, t.data() + sc->own_lo, np * 8);
+        if (last) std::memcpy(last + g0, la.data() + sc->own_lo, np * 8);
+        if (counters4)
+            for (size_t q = 0; q < 4; ++q) std::memcpy(counters4 + q * (size_t)g->E + ge, c4.data() + q * e + le, ne * 8);
+        if (connected) std::memcpy(connected + ge, co.data() + le, ne * 4);
+        if (expire) std::memcpy(expire + ge, ex.data() + le, ne * 8);
+    }
+    return GSIM_OK;
+}
+
 }  // extern "C"

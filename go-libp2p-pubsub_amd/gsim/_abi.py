@@ -321,6 +321,9 @@ SIGNATURES = [
     ("gsim_group_read_scores", c_int32, [c_void_p, c_void_p]),
     ("gsim_group_read_snapshot", c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
     ("gsim_group_trace_config", c_int32, [c_void_p, c_uint32, c_uint32, c_int64]),
+    ("gsim_group_set_peer_gater", c_int32, [c_void_p, POINTER(CPeerGaterParams), c_void_p]),
+    ("gsim_group_gater_throttled", c_int32, [c_void_p, POINTER(c_int64)]),
+    ("gsim_group_gater_read", c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("gsim_group_trace_read", c_int32, [c_void_p, c_void_p, c_int64, POINTER(c_int64)]),
     # gsim_wire.h
     ("gsim_wire_size", c_uint64, [POINTER(CWireRpc)]),

@@ -378,6 +378,34 @@ class ShardedEngine:
         self._check(self.lib.gsim_group_px_connect(self.g, int(now), _ptr(out), int(cap), ctypes.byref(n)))
         return out[:min(n.value, cap)].copy()
 
+    def set_peer_gater(self, params, topic_weights=None):
+        """Engine.set_peer_gater on every shard (gsim_group_set_peer_gater)."""
+        c = params.to_c()
+        T = max(1, len(self.topics))
+        w = np.zeros(T, dtype=np.float64)
+        for t, x in (params.TopicDeliveryWeights or {}).items():
+            w[int(t)] = float(x)
+        if topic_weights is not None:
+            w = np.ascontiguousarray(topic_weights, dtype=np.float64)
+        self._check(self.lib.gsim_group_set_peer_gater(self.g, ctypes.byref(c), _ptr(w)))
+
+    def gater_throttled(self) -> int:
+        """Copies the peer gaters of the whole job dropped so far."""
+        n = ctypes.c_int64(0)
+        self._check(self.lib.gsim_group_gater_throttled(self.g, ctypes.byref(n)))
+        return n.value
+
+    def gater_read(self) -> dict:
+        """Engine.gater_read in the whole network's view (gsim_group_gater_read)."""
+        N, E = self.net.n, self.net.e
+        out = {"validate": np.zeros(N), "throttle": np.zeros(N), "last": np.zeros(N, dtype=np.int64),
+               "counters": np.zeros((4, E)), "connected": np.zeros(E, dtype=np.int32),
+               "expire": np.zeros(E, dtype=np.int64)}
+        self._check(self.lib.gsim_group_gater_read(self.g, _ptr(out["validate"]), _ptr(out["throttle"]),
+                                                   _ptr(out["last"]), _ptr(out["counters"]), _ptr(out["connected"]),
+                                                   _ptr(out["expire"])))
+        return out
+
     def trace_config(self, peer_lo: int, peer_hi: int, cap: int = 1 << 20):
         """Trace the routers [peer_lo, peer_hi) (global ids) over the shards
         (gsim_group_trace_config; cap 0 stops)."""

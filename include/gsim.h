@@ -780,6 +780,14 @@ int gsim_group_read_field(gsim_group* g, int32_t field, void* dst, size_t bytes)
 int gsim_group_read_scores(gsim_group* g, double* out);
 int gsim_group_read_snapshot(gsim_group* g, int64_t obs_lo, int64_t obs_hi, gsim_peer_score_snapshot* peers,
                              gsim_topic_score_snapshot* topics);
+/* WithPeerGater over a sharded network (peer_gater.go:161-186): every
+ * shard's routers; gsim_group_gater_throttled sums the drops over the job,
+ * gsim_group_gater_read is gsim_gater_read in global peer / edge order (the
+ * parts this process's shards own). */
+int gsim_group_set_peer_gater(gsim_group* g, const gsim_peer_gater_params* p, const double* topic_weights);
+int gsim_group_gater_throttled(gsim_group* g, int64_t* out);
+int gsim_group_gater_read(gsim_group* g, double* validate, double* throttle, int64_t* last, double* counters4,
+                          int32_t* connected, int64_t* expire);
 /* gsim_trace_config / gsim_trace_read over a sharded network: the routers
  * [peer_lo, peer_hi) (global ids) that this process's shards own, every
  * event in global ids, sorted as gsim_trace_read sorts.  Needs the copy push

@@ -156,12 +156,13 @@ def test_gater_drop_rate_follows_goodput():
 # ---- GPU -------------------------------------------------------------------------------
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("weights", [None, {0: 0.5, 2: 2.25}])
-def test_gater_network_bit_exact(require_gpu, weights):
+@pytest.mark.parametrize("weights,shards", [(None, 0), ({0: 0.5, 2: 2.25}, 0), (None, 2), ({0: 0.5, 2: 2.25}, 3)])
+def test_gater_network_bit_exact(require_gpu, weights, shards):
     """A network whose validations often throttle (so every router's gate
     turns on), sybils sharing IPs (shared stats), churn and gossip: the
     engine's gater state, its drops and everything the gated deliveries touch
-    equal the oracle's after every tick."""
+    equal the oracle's after every tick.  On 2 / 3 shards too: each router's
+    gate on its shard, pushed copies gated at the receiving shard."""
     from fixtures import beacon_params, sybil_ips, synthetic_state
     from gsim.engine import random_regular
     from gsim.params import GossipSubParams, PeerScoreThresholds
@@ -187,7 +188,15 @@ def test_gater_network_bit_exact(require_gpu, weights):
     if weights:
         gater.TopicDeliveryWeights = weights
     log = []
-    run_parity(net, params, th, gp, st, ticks, sched, ring=512, churn=churn, gater=gater, gater_log=log)
+    eng = None
+    if shards:
+        from gsim.shard import ShardedEngine
+        from tickrun import SEED
+        eng = ShardedEngine(params, th, gossip=gp, shards=shards)
+        eng.load_graph(net)
+        eng.set_seed(SEED)
+        st.push_to_engine(eng)
+    run_parity(net, params, th, gp, st, ticks, sched, ring=512, churn=churn, gater=gater, gater_log=log, eng=eng)
     assert log[-1] > 100, f"the gate should have dropped copies: {log}"
 
 
