@@ -141,7 +141,7 @@ def build_network(cfg, seed, scen=None):
         ip_ptr, ip_ids, n_ips, syb = graphs.sybil_ips(n, scen["sybil_frac"], scen["per_ip"], seed=seed + 200)
         net = graphs.with_ips(net, ip_ptr, ip_ids, n_ips)
         beh = syb.astype(np.uint8) * np.uint8(_abi.BEHAVE_IGNORE_IWANT)
-    else:
+    elif not os.environ.get("GSIM_BENCH_NO_IPS"):   # (diagnostic A/B: the network without IP lists)
         # honest peers get a unique IP id (P6 is derived, and is 0)
         net = graphs.with_ips(net, np.arange(n + 1, dtype=np.uint32), np.arange(n, dtype=np.uint32), n)
     return net, beh
@@ -180,6 +180,8 @@ def build_engine(cfg, seed, device, scen=None, shard=None):
         eng.set_kernel_variant(2, int(os.environ["GSIM_SEND_VARIANT"]))
     if os.environ.get("GSIM_TM_UNIFORM"):                        # topic-major blocks the same per topic
         eng.set_kernel_variant(6, int(os.environ["GSIM_TM_UNIFORM"]))
+    if os.environ.get("GSIM_TM_XCD"):                            # k_send_tm from XCD work queues (A/B)
+        eng.set_kernel_variant(7, int(os.environ["GSIM_TM_XCD"]))
     return eng, net
 
 

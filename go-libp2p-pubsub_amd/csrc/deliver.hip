@@ -148,6 +148,9 @@ struct Deliver {
     std::vector<uint32_t> tmtab;       // host copy (the upload's source)
     int64_t tm_cn = -1;                // peers the table was built for
     int32_t tm_tb = 0;                 // k_send_tm block size d_tmtab was laid out for
+    uint32_t* d_xq = nullptr;          // k_send_tm XCD work queues (xq_next), built with d_tmtab
+    int64_t xq_cap = 0;                // u32s allocated at d_xq
+    bool xq_ok = false;                // d_xq holds the queues of the current table
     int32_t* d_mpub = nullptr;         // [ring] round the slot's message was published in
     int64_t* d_roff = nullptr;         // [rounds] offset of each round in its heartbeat
     int32_t* d_lastput = nullptr;      // [T][N]
@@ -250,6 +253,7 @@ struct RoundArgs {
     const uint64_t* mmask;
     const uint32_t *hidx, *hlist;  // hub rows' mesh edge lists (Deliver::d_hlist; nullptr: none)
     const uint32_t* tmtab;         // k_send_tm blocks per topic (Deliver::d_tmtab)
+    uint32_t* xq;                  // k_send_tm XCD work queues (xq_next; nullptr: one block per item)
     uint8_t* peertx;               // [ring][ptx_w] GetForPeer counts (Deliver::d_peertx), zeroed on reuse
     int32_t ptx_w;
     TraceRef tr;                   // gsim_trace_config
@@ -743,6 +747,48 @@ constexpr int kSparseTB = 512;
 constexpr uint32_t kTmWin = 8192;   // flattened edges whose senders are tabled in LDS at once
 constexpr int kTmTabMin = 256;      // forwarders in a chunk from which the table pays for its fill
 
+// The wave's remote copies as bits (copy push): lane l sets
+// bits v of xbits word k (~0: none).  Neighbouring lanes carry neighbouring
+// senders' copies, whose bits share words: an OR-scan over runs of equal
+// words, and the run's last lane issues one atomicOr for all of them (a lane
+// may also take in bits of an earlier run of the same word: OR is idempotent).
+// Every lane of the wave calls it.
+__device__ __forceinline__ void xbits_or_wave(uint64_t* xbits, uint64_t k, uint64_t v)
+{
+    const int lane = threadIdx.x & 63;
+    if (!__ballot(k != ~0ull)) return;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t ko = (uint64_t)__shfl_up((long long)k, o, 64);
+        const uint64_t vo = (uint64_t)__shfl_up((long long)v, o, 64);
+        if (lane >= o && ko == k) v |= vo;
+    }
+    const uint64_t kn = (uint64_t)__shfl_down((long long)k, 1, 64);
+    if (k != ~0ull && (lane == 63 || kn != k))
+        atomicOr(reinterpret_cast<unsigned long long*>(xbits + k), (unsigned long long)v);
+}
+
+// XCD work queues for k_send_tm (gsim_set_kernel_variant(h, 7, 1)): the
+// items (block indices of the launch-order table) of topic t sit in the queue
+// of XCD t % 8, and a persistent block -- dealt to XCD blockIdx.x % 8 -- takes
+// its own XCD's items first, then steals from the others, so a topic's slot
+// bitmaps stay in one or two XCDs' L2 while no XCD idles.  Layout (u32):
+// [8 x kXqStride] counters (own cache lines), [9] queue offsets, items.
+constexpr int kXqStride = 32;
+__device__ __forceinline__ uint32_t xq_next(uint32_t* xq)
+{
+    const uint32_t* off = xq + 8 * kXqStride;
+    const int x0 = (int)(blockIdx.x & 7u);
+    for (int q = 0; q < 8; ++q) {
+        const int x = (x0 + q) & 7;
+        const uint32_t n = off[x + 1] - off[x];
+        uint32_t* c = xq + x * kXqStride;
+        if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= n) continue;
+        const uint32_t k = atomicAdd(c, 1u);
+        if (k < n) return xq[8 * kXqStride + 9 + off[x] + k];
+    }
+    return 0xFFFFFFFFu;
+}
+
 // SP: topic slots or member-compacted cells are in use (gsim_internal.h); the
 // dense instance indexes plane t and cell m * N + p with no table reads.
 template <int kTmThreads, bool LAT, bool SP, bool GT = false, bool PUSH = false>
@@ -776,7 +822,22 @@ void k_send_tm(RoundArgs a_)
     __shared__ uint32_t s_ne;
     __shared__ unsigned long long s_clm;                     // slots of the pass with a new claim
     __shared__ unsigned long long s_stats[4];
-    const uint32_t lb = blockIdx.x;
+    __shared__ uint32_t s_item;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (tid == 0) { s_stats[0] = s_stats[1] = s_stats[2] = s_stats[3] = 0; }
+    unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
+    // one (topic, peer range) item per block, or (a.xq) persistent blocks
+    // taking items from their XCD's queue (xq_next)
+    for (uint32_t it = 0;; ++it) {
+    uint32_t lb = blockIdx.x;
+    if (a.xq) {
+        if (tid == 0) s_item = xq_next(a.xq);
+        __syncthreads();
+        lb = s_item;
+        if (lb == 0xFFFFFFFFu) break;                        // block-uniform
+    } else if (it) {
+        break;
+    }
     int32_t t = 0;
     {
         int32_t r = a.T > 0 ? a.T : 1;
@@ -790,8 +851,7 @@ void k_send_tm(RoundArgs a_)
     const int64_t lo = a.slo + (int64_t)(lb - a.tmtab[t]) * range;
     const int64_t hi = lo + range < pend_ ? lo + range : pend_;
     const int64_t wlo = (int64_t)a.rlo >> 6;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    if (tid == 0) { s_ns = 0; s_stats[0] = s_stats[1] = s_stats[2] = s_stats[3] = 0; }
+    if (tid == 0) s_ns = 0;
     __syncthreads();
     // a sub-ring (gsim_msg_config.topic_slots) holds topic t's slots alone
     const int m_lo = a.topic_slots > 0 ? t * a.topic_slots : 0;
@@ -810,7 +870,6 @@ void k_send_tm(RoundArgs a_)
     const double mcap = tp->mesh_message_deliveries_cap;
     const uint32_t par = (uint32_t)(a.g & 1);
     const uint32_t claim_hi = kClaim | (par << 30);
-    unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
     for (int k0 = 0; k0 < ns; k0 += kTsSlots) {
         const int nb = ns - k0 < kTsSlots ? ns - k0 : kTsSlots;
         if (tid < nb) {
@@ -1007,10 +1066,12 @@ void k_send_tm(RoundArgs a_)
                         continue;
 #endif
                         uint32_t xq[PUSH ? P : 1];   // PUSH: the copy's bit (a cross edge), ~0: an owned receiver
+                        uint64_t xbk[PUSH ? P : 1];  // ... a remote copy's xbits word (~0: none) and bit
+                        uint64_t xbv[PUSH ? P : 1];
 #pragma unroll
                         for (int u = 0; u < P; ++u) {
                             iv[u] = 0; mfv[u] = 0; dsv[u] = 0; tfv[u] = 0; nv[u] = 0; xv[u] = 0.0;
-                            if constexpr (PUSH) xq[u] = ~0u;
+                            if constexpr (PUSH) { xq[u] = ~0u; xbk[u] = ~0ull; xbv[u] = 0; }
                             if (vv[u]) {
                                 const uint32_t e = ev[u];
                                 const uint8_t vd = s_vd[kv[u]];
@@ -1072,11 +1133,12 @@ void k_send_tm(RoundArgs a_)
                                 if (a.tr.on_any(i)) a.tr.push(ts, tm, i, j, t, GSIM_TRACE_RECV_RPC, 0);
                             }
                             if constexpr (PUSH) {
-                                // the receiver's shard delivers it (its AcceptFrom, records, cell)
+                                // the receiver's shard delivers it (its AcceptFrom, records, cell):
+                                // its bit, set below for the whole wave (xbits_or_wave)
                                 if (tg && remote) {
                                     const uint32_t xb = xq[u];
-                                    atomicOr(reinterpret_cast<unsigned long long*>(a.xbits + (int64_t)m * a.xbw + (xb >> 6)),
-                                             1ull << (xb & 63u));
+                                    xbk[u] = (uint64_t)((int64_t)m * a.xbw + (xb >> 6));
+                                    xbv[u] = 1ull << (xb & 63u);
                                     continue;
                                 }
                             }
@@ -1189,6 +1251,10 @@ void k_send_tm(RoundArgs a_)
                                 }
                             }
                         }
+                        if constexpr (PUSH) {
+#pragma unroll
+                            for (int u = 0; u < P; ++u) xbits_or_wave(a.xbits, xbk[u], xbv[u]);
+                        }
                         if constexpr (LAT) {
 #pragma unroll
                             for (int u = 0; u < P; ++u) vq_push_wave(a, qpl[u], qv[u]);
@@ -1222,6 +1288,7 @@ void k_send_tm(RoundArgs a_)
         }
         __syncthreads();                                         // the pass's slot table is rewritten next
     }
+    }   // items
     n_acc = wave_sum_u64(n_acc);
     n_gray = wave_sum_u64(n_gray);
     n_first = wave_sum_u64(n_first);
@@ -2590,7 +2657,7 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_clist); f(d->d_clist_n); f(d->d_hidx); f(d->d_hrow); f(d->d_hlist); f(d->d_mlist); f(d->d_mloff); f(d->d_mcount); f(d->d_mmtab); f(d->d_hubw); f(d->d_mctab); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_xq); f(d->d_clist); f(d->d_clist_n); f(d->d_hidx); f(d->d_hrow); f(d->d_hlist); f(d->d_mlist); f(d->d_mloff); f(d->d_mcount); f(d->d_mmtab); f(d->d_hubw); f(d->d_mctab); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_peertx); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
@@ -3133,37 +3200,71 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
         if (e != hipSuccess) return hip_check(h, e, "k_send_tm block table");
         d->tm_cn = cn;
         d->tm_tb = TBv;
+        d->xq_ok = false;
     }
-    const RoundArgs& a = a0;
+    RoundArgs a = a0;
     // the slot list in LDS
     const size_t lds = ((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7;
+    dim3 grid(d->tmtab[T]);
+    if (h->tm_xcd) {
+        // XCD work queues (xq_next): topic t's items on XCD t % 8
+        const int64_t items = d->tmtab[T], need = 8 * kXqStride + 9 + items;
+        if (!d->xq_ok) {
+            if (need > d->xq_cap) {
+                if (d->d_xq) { (void)hipStreamSynchronize(h->stream); (void)hipFree(d->d_xq); d->d_xq = nullptr; d->xq_cap = 0; }
+                hipError_t e = hipMalloc((void**)&d->d_xq, sizeof(uint32_t) * (size_t)need);
+                if (e != hipSuccess) return hip_check(h, e, "k_send_tm XCD queues");
+                d->xq_cap = need;
+            }
+            std::vector<uint32_t> q((size_t)need, 0);
+            uint32_t* off = q.data() + 8 * kXqStride;
+            uint32_t* it = off + 9;
+            uint32_t k = 0;
+            for (int x = 0; x < 8; ++x) {
+                off[x] = k;
+                for (int t = x; t < T; t += 8)
+                    for (uint32_t b = d->tmtab[t]; b < d->tmtab[t + 1]; ++b) it[k++] = b;
+            }
+            off[8] = k;
+            hipError_t e = hipMemcpyAsync(d->d_xq, q.data(), sizeof(uint32_t) * (size_t)need, hipMemcpyHostToDevice, h->stream);
+            if (e != hipSuccess) return hip_check(h, e, "k_send_tm XCD queues");
+            d->xq_ok = true;
+        } else {
+            hipError_t e = hipMemsetAsync(d->d_xq, 0, sizeof(uint32_t) * 8 * kXqStride, h->stream);
+            if (e != hipSuccess) return hip_check(h, e, "k_send_tm XCD queues");
+        }
+        a.xq = d->d_xq;
+        // persistent: the blocks that fit the chip at once (a multiple of 8)
+        const int64_t res = (int64_t)h->n_cu * std::max(1, h->tm_resident);
+        grid = dim3((uint32_t)std::max<int64_t>(8, std::min<int64_t>(items + 7, res) / 8 * 8));
+    }
     if (a.push && a.mlat)
-        hipLaunchKernelGGL((k_send_tm<kPushTB, true, true, false, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
+        hipLaunchKernelGGL((k_send_tm<kPushTB, true, true, false, true>), grid, dim3(kPushTB), lds,
                            h->stream, a);
     else if (a.push && a.gt.act && sp)
-        hipLaunchKernelGGL((k_send_tm<kPushTB, false, true, true, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
+        hipLaunchKernelGGL((k_send_tm<kPushTB, false, true, true, true>), grid, dim3(kPushTB), lds,
                            h->stream, a);
     else if (a.push && a.gt.act)
-        hipLaunchKernelGGL((k_send_tm<kPushTB, false, false, true, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
+        hipLaunchKernelGGL((k_send_tm<kPushTB, false, false, true, true>), grid, dim3(kPushTB), lds,
                            h->stream, a);
     else if (a.push && sp)
-        hipLaunchKernelGGL((k_send_tm<kPushTB, false, true, false, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
+        hipLaunchKernelGGL((k_send_tm<kPushTB, false, true, false, true>), grid, dim3(kPushTB), lds,
                            h->stream, a);
     else if (a.push)
-        hipLaunchKernelGGL((k_send_tm<kPushTB, false, false, false, true>), dim3(d->tmtab[T]), dim3(kPushTB), lds,
+        hipLaunchKernelGGL((k_send_tm<kPushTB, false, false, false, true>), grid, dim3(kPushTB), lds,
                            h->stream, a);
     else if (a.mlat && sp)
-        hipLaunchKernelGGL((k_send_tm<kSparseTB, true, true>), dim3(d->tmtab[T]), dim3(kSparseTB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<kSparseTB, true, true>), grid, dim3(kSparseTB), lds, h->stream, a);
     else if (a.mlat)
-        hipLaunchKernelGGL((k_send_tm<TB, true, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<TB, true, true>), grid, dim3(TB), lds, h->stream, a);
     else if (a.gt.act && sp)
-        hipLaunchKernelGGL((k_send_tm<kSparseTB, false, true, true>), dim3(d->tmtab[T]), dim3(kSparseTB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<kSparseTB, false, true, true>), grid, dim3(kSparseTB), lds, h->stream, a);
     else if (a.gt.act)
-        hipLaunchKernelGGL((k_send_tm<TB, false, false, true>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<TB, false, false, true>), grid, dim3(TB), lds, h->stream, a);
     else if (sp)
-        hipLaunchKernelGGL((k_send_tm<kSparseTB, false, true>), dim3(d->tmtab[T]), dim3(kSparseTB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<kSparseTB, false, true>), grid, dim3(kSparseTB), lds, h->stream, a);
     else
-        hipLaunchKernelGGL((k_send_tm<TB, false, false>), dim3(d->tmtab[T]), dim3(TB), lds, h->stream, a);
+        hipLaunchKernelGGL((k_send_tm<TB, false, false>), grid, dim3(TB), lds, h->stream, a);
     return hip_check(h, hipGetLastError(), "k_send_tm");
 }
 
@@ -3343,8 +3444,86 @@ constexpr int kXbList = 1024;                // per-wave LDS list of a task's co
 #ifndef GSIM_XB_WPE
 #define GSIM_XB_WPE 1
 #endif
+
+// listed_copy for kXbP copies of slot m per lane at once (records rr[], ~0u:
+// none), the common configuration only -- dense cells, no claim list, topic
+// slots, gater, trace, Leave or validation latency (xbits_fast) -- with the
+// same rules and results; each stage's loads for all the copies are issued
+// before any is used, so the copies' dependent trips overlap.
+constexpr int kXbP = 2;
+__device__ __forceinline__ void listed_copies_fast(const RoundArgs& a, const uint32_t* rr, uint32_t m, int32_t t,
+                                                   const uint32_t* owner, uint32_t claim_hi, uint32_t par, ctp_t tp,
+                                                   unsigned long long& n_acc, unsigned long long& n_gray,
+                                                   unsigned long long& n_first, uint32_t* s_new2)
+{
+    const uint8_t vd = a.minv[m];
+    const bool inv = vd != GSIM_VERDICT_ACCEPT, pen = verdict_penalises(vd);
+    const int64_t window = tp->mesh_message_deliveries_window_ns;
+    const double mcap = tp->mesh_message_deliveries_cap;
+    bool on[kXbP], sc[kXbP], known[kXbP];
+    uint8_t ds[kXbP], tf[kXbP];
+    uint32_t p[kXbP];
+    uint64_t sw[kXbP], c[kXbP];
+#pragma unroll
+    for (int u = 0; u < kXbP; ++u) {                     // stage 1: the record's edge state
+        on[u] = rr[u] != ~0u;
+        ds[u] = on[u] ? a.dstate[rr[u]] : 0;
+        p[u] = on[u] ? a.col[rr[u]] : 0u;
+        tf[u] = on[u] ? a.tflags[(int64_t)t * a.E + rr[u]] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kXbP; ++u) {                     // AcceptFrom; stage 2: the committed bit
+        if (on[u] && !(ds[u] & GSIM_DS_ACCEPT)) { n_gray++; on[u] = false; }
+        n_acc += on[u];
+        sc[u] = on[u] && tp->scored && (ds[u] & GSIM_DS_TRACKED);
+        sw[u] = on[u] ? a.seenbm[(int64_t)m * a.nw + (p[u] >> 6)] : 0ull;
+    }
+    const bool wa = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
+#pragma unroll
+    for (int u = 0; u < kXbP; ++u) {                     // stage 3: the cells that matter
+        const bool sb = (sw[u] >> (p[u] & 63)) & 1ull;
+        known[u] = on[u] && sb && (wa || !sc[u] || inv || !(tf[u] & GSIM_TF_IN_MESH));
+        c[u] = (on[u] && !known[u]) ? a.cs.cell[(int64_t)m * a.cs.n + p[u]] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < kXbP; ++u) {
+        if (!on[u]) continue;
+        const uint32_t r = rr[u];
+        const int64_t ir = (int64_t)t * a.E + r;
+        int64_t seen_round = -1;
+        if (!known[u]) {
+            const uint32_t hi = (uint32_t)(c[u] >> 32);
+            if (c[u] != kUnseen64) {
+                if (!(hi & kClaim)) seen_round = hi;
+                else if (((hi >> 30) & 1u) != par) seen_round = a.g - 1;
+            }
+            if (vd != GSIM_VERDICT_SIGNATURE && seen_round < 0 && (c[u] == kUnseen64 || (hi & kEdgeMask) > r)) {
+                uint32_t lo = owner[r];
+                if (sc[u] && !inv) {
+                    lo |= kCreditFirst;
+                    if (window < 0 && (tf[u] & GSIM_TF_IN_MESH)) lo |= kCreditMesh;
+                }
+                const uint64_t v = ((uint64_t)(claim_hi | r) << 32) | lo;
+                const uint64_t prev = __hip_atomic_fetch_min(a.cs.cell + (int64_t)m * a.cs.n + p[u], v, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+                if (prev == kUnseen64) {
+                    n_first++;
+                    atomicOr(&s_new2[m >> 5], 1u << (m & 31));
+                }
+            }
+        }
+        if (!sc[u]) continue;
+        if (pen) {
+            atomicAdd(&a.invalid[ir], 1.0);                           // markInvalidMessageDelivery
+        } else if (!inv && (tf[u] & GSIM_TF_IN_MESH)) {
+            const bool in_window = known[u] ? true
+                                 : seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window) : (window >= 0);
+            if (in_window) atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], mcap, a.mcnt_fast);
+        }
+    }
+}
 __global__ __launch_bounds__(256, GSIM_XB_WPE) void k_xbits_deliver(RoundArgs a_, const uint64_t* in, const XSrc* src, int32_t K,
-                                                       int64_t ntask, const uint32_t* owner)
+                                                       int64_t ntask, const uint32_t* owner, int32_t xbits_fast_on)
 {
     const RoundArgs& a = a_;
     extern __shared__ uint32_t s_new2[];
@@ -3359,6 +3538,9 @@ __global__ __launch_bounds__(256, GSIM_XB_WPE) void k_xbits_deliver(RoundArgs a_
     const ctp_t tpa = const_tp(a.tp);
     unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
     uint32_t* lst = s_list[wid];
+    // the common configuration: listed_copies_fast (kXbP copies per lane in flight)
+    const bool fast = !a.smask && !a.cs.sparse && !a.clist && !a.gt.act && !a.tr.ev && !a.subdyn && !a.mlat &&
+                      xbits_fast_on;
     for (int64_t tk = (int64_t)blockIdx.x * 4 + wid; tk < ntask; tk += (int64_t)gridDim.x * 4) {   // wave-uniform
         const RoundArgs& a = kernarg0(a_);
         int q = 0;
@@ -3383,10 +3565,23 @@ __global__ __launch_bounds__(256, GSIM_XB_WPE) void k_xbits_deliver(RoundArgs a_
             for (uint64_t b = bits; b; b &= b - 1) lst[pos++] = (uint32_t)(w * 64) + (uint32_t)__builtin_ctzll(b);
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            for (uint32_t j0 = 0; j0 < total; j0 += 64) {
-                if (j0 + lane < total)
-                    listed_copy(a, (uint32_t)(sq.gbase + lst[j0 + lane]), m, owner, par, claim_hi, tpa, n_acc, n_gray,
-                                n_first, s_new2, false);
+            if (fast) {
+                const int32_t t = (int32_t)a.mtopic[m];
+                for (uint32_t j0 = 0; j0 < total; j0 += 64 * kXbP) {
+                    uint32_t rr[kXbP];
+#pragma unroll
+                    for (int u = 0; u < kXbP; ++u) {
+                        const uint32_t j = j0 + (uint32_t)(u * 64 + lane);
+                        rr[u] = j < total ? (uint32_t)(sq.gbase + lst[j]) : ~0u;
+                    }
+                    listed_copies_fast(a, rr, m, t, owner, claim_hi, par, tpa + t, n_acc, n_gray, n_first, s_new2);
+                }
+            } else {
+                for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+                    if (j0 + lane < total)
+                        listed_copy(a, (uint32_t)(sq.gbase + lst[j0 + lane]), m, owner, par, claim_hi, tpa, n_acc, n_gray,
+                                    n_first, s_new2, false);
+                }
             }
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // lst is rewritten by the next task
@@ -3442,7 +3637,7 @@ int deliver_xbits_apply(gsim_handle* h, int64_t round, const uint64_t* in, const
     const size_t lds2 = (size_t)nnew_words(d) * 4;
     const uint32_t grid = (uint32_t)std::min<int64_t>((ntask + 3) / 4, 8192);
     hipLaunchKernelGGL(k_xbits_deliver, dim3(grid), dim3(256), lds2, h->stream, a, in, d_src, (int32_t)K,
-                       ntask, (const uint32_t*)h->d_owner);
+                       ntask, (const uint32_t*)h->d_owner, (int32_t)(h->xb_generic ? 0 : 1));
     return hip_check(h, hipGetLastError(), "k_xbits_deliver");
 }
 
