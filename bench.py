@@ -180,8 +180,6 @@ def build_engine(cfg, seed, device, scen=None, shard=None):
         eng.set_kernel_variant(2, int(os.environ["GSIM_SEND_VARIANT"]))
     if os.environ.get("GSIM_TM_UNIFORM"):                        # topic-major blocks the same per topic
         eng.set_kernel_variant(6, int(os.environ["GSIM_TM_UNIFORM"]))
-    if os.environ.get("GSIM_TM_XCD"):                            # k_send_tm from XCD work queues (A/B)
-        eng.set_kernel_variant(7, int(os.environ["GSIM_TM_XCD"]))
     return eng, net
 
 

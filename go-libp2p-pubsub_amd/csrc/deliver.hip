@@ -148,9 +148,6 @@ struct Deliver {
     std::vector<uint32_t> tmtab;       // host copy (the upload's source)
     int64_t tm_cn = -1;                // peers the table was built for
     int32_t tm_tb = 0;                 // k_send_tm block size d_tmtab was laid out for
-    uint32_t* d_xq = nullptr;          // k_send_tm XCD work queues (xq_next), built with d_tmtab
-    int64_t xq_cap = 0;                // u32s allocated at d_xq
-    bool xq_ok = false;                // d_xq holds the queues of the current table
     int32_t* d_mpub = nullptr;         // [ring] round the slot's message was published in
     int64_t* d_roff = nullptr;         // [rounds] offset of each round in its heartbeat
     int32_t* d_lastput = nullptr;      // [T][N]
@@ -253,7 +250,6 @@ struct RoundArgs {
     const uint64_t* mmask;
     const uint32_t *hidx, *hlist;  // hub rows' mesh edge lists (Deliver::d_hlist; nullptr: none)
     const uint32_t* tmtab;         // k_send_tm blocks per topic (Deliver::d_tmtab)
-    uint32_t* xq;                  // k_send_tm XCD work queues (xq_next; nullptr: one block per item)
     uint8_t* peertx;               // [ring][ptx_w] GetForPeer counts (Deliver::d_peertx), zeroed on reuse
     int32_t ptx_w;
     TraceRef tr;                   // gsim_trace_config
@@ -767,28 +763,6 @@ __device__ __forceinline__ void xbits_or_wave(uint64_t* xbits, uint64_t k, uint6
         atomicOr(reinterpret_cast<unsigned long long*>(xbits + k), (unsigned long long)v);
 }
 
-// XCD work queues for k_send_tm (gsim_set_kernel_variant(h, 7, 1)): the
-// items (block indices of the launch-order table) of topic t sit in the queue
-// of XCD t % 8, and a persistent block -- dealt to XCD blockIdx.x % 8 -- takes
-// its own XCD's items first, then steals from the others, so a topic's slot
-// bitmaps stay in one or two XCDs' L2 while no XCD idles.  Layout (u32):
-// [8 x kXqStride] counters (own cache lines), [9] queue offsets, items.
-constexpr int kXqStride = 32;
-__device__ __forceinline__ uint32_t xq_next(uint32_t* xq)
-{
-    const uint32_t* off = xq + 8 * kXqStride;
-    const int x0 = (int)(blockIdx.x & 7u);
-    for (int q = 0; q < 8; ++q) {
-        const int x = (x0 + q) & 7;
-        const uint32_t n = off[x + 1] - off[x];
-        uint32_t* c = xq + x * kXqStride;
-        if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= n) continue;
-        const uint32_t k = atomicAdd(c, 1u);
-        if (k < n) return xq[8 * kXqStride + 9 + off[x] + k];
-    }
-    return 0xFFFFFFFFu;
-}
-
 // SP: topic slots or member-compacted cells are in use (gsim_internal.h); the
 // dense instance indexes plane t and cell m * N + p with no table reads.
 template <int kTmThreads, bool LAT, bool SP, bool GT = false, bool PUSH = false>
@@ -822,22 +796,11 @@ void k_send_tm(RoundArgs a_)
     __shared__ uint32_t s_ne;
     __shared__ unsigned long long s_clm;                     // slots of the pass with a new claim
     __shared__ unsigned long long s_stats[4];
-    __shared__ uint32_t s_item;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     if (tid == 0) { s_stats[0] = s_stats[1] = s_stats[2] = s_stats[3] = 0; }
     unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
-    // one (topic, peer range) item per block, or (a.xq) persistent blocks
-    // taking items from their XCD's queue (xq_next)
-    for (uint32_t it = 0;; ++it) {
-    uint32_t lb = blockIdx.x;
-    if (a.xq) {
-        if (tid == 0) s_item = xq_next(a.xq);
-        __syncthreads();
-        lb = s_item;
-        if (lb == 0xFFFFFFFFu) break;                        // block-uniform
-    } else if (it) {
-        break;
-    }
+    // one (topic, peer range) item per block
+    const uint32_t lb = blockIdx.x;
     int32_t t = 0;
     {
         int32_t r = a.T > 0 ? a.T : 1;
@@ -1288,7 +1251,6 @@ void k_send_tm(RoundArgs a_)
         }
         __syncthreads();                                         // the pass's slot table is rewritten next
     }
-    }   // items
     n_acc = wave_sum_u64(n_acc);
     n_gray = wave_sum_u64(n_gray);
     n_first = wave_sum_u64(n_first);
@@ -2657,7 +2619,7 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_xq); f(d->d_clist); f(d->d_clist_n); f(d->d_hidx); f(d->d_hrow); f(d->d_hlist); f(d->d_mlist); f(d->d_mloff); f(d->d_mcount); f(d->d_mmtab); f(d->d_hubw); f(d->d_mctab); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_clist); f(d->d_clist_n); f(d->d_hidx); f(d->d_hrow); f(d->d_hlist); f(d->d_mlist); f(d->d_mloff); f(d->d_mcount); f(d->d_mmtab); f(d->d_hubw); f(d->d_mctab); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_peertx); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
@@ -3200,44 +3162,11 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
         if (e != hipSuccess) return hip_check(h, e, "k_send_tm block table");
         d->tm_cn = cn;
         d->tm_tb = TBv;
-        d->xq_ok = false;
     }
-    RoundArgs a = a0;
+    const RoundArgs& a = a0;
     // the slot list in LDS
     const size_t lds = ((size_t)d->cfg.ring * 2 + 7) & ~(size_t)7;
-    dim3 grid(d->tmtab[T]);
-    if (h->tm_xcd) {
-        // XCD work queues (xq_next): topic t's items on XCD t % 8
-        const int64_t items = d->tmtab[T], need = 8 * kXqStride + 9 + items;
-        if (!d->xq_ok) {
-            if (need > d->xq_cap) {
-                if (d->d_xq) { (void)hipStreamSynchronize(h->stream); (void)hipFree(d->d_xq); d->d_xq = nullptr; d->xq_cap = 0; }
-                hipError_t e = hipMalloc((void**)&d->d_xq, sizeof(uint32_t) * (size_t)need);
-                if (e != hipSuccess) return hip_check(h, e, "k_send_tm XCD queues");
-                d->xq_cap = need;
-            }
-            std::vector<uint32_t> q((size_t)need, 0);
-            uint32_t* off = q.data() + 8 * kXqStride;
-            uint32_t* it = off + 9;
-            uint32_t k = 0;
-            for (int x = 0; x < 8; ++x) {
-                off[x] = k;
-                for (int t = x; t < T; t += 8)
-                    for (uint32_t b = d->tmtab[t]; b < d->tmtab[t + 1]; ++b) it[k++] = b;
-            }
-            off[8] = k;
-            hipError_t e = hipMemcpyAsync(d->d_xq, q.data(), sizeof(uint32_t) * (size_t)need, hipMemcpyHostToDevice, h->stream);
-            if (e != hipSuccess) return hip_check(h, e, "k_send_tm XCD queues");
-            d->xq_ok = true;
-        } else {
-            hipError_t e = hipMemsetAsync(d->d_xq, 0, sizeof(uint32_t) * 8 * kXqStride, h->stream);
-            if (e != hipSuccess) return hip_check(h, e, "k_send_tm XCD queues");
-        }
-        a.xq = d->d_xq;
-        // persistent: the blocks that fit the chip at once (a multiple of 8)
-        const int64_t res = (int64_t)h->n_cu * std::max(1, h->tm_resident);
-        grid = dim3((uint32_t)std::max<int64_t>(8, std::min<int64_t>(items + 7, res) / 8 * 8));
-    }
+    const dim3 grid(d->tmtab[T]);
     if (a.push && a.mlat)
         hipLaunchKernelGGL((k_send_tm<kPushTB, true, true, false, true>), grid, dim3(kPushTB), lds,
                            h->stream, a);

@@ -1157,10 +1157,6 @@ static int create_impl(const gsim_peer_score_params* params, const gsim_topic_sc
         return fail(GSIM_EDEVICE, "hipStreamCreate failed");
     }
     for (auto& ev : h->ev) (void)hipEventCreate(&ev);
-    {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) h->n_cu = cus;
-    }
     if (dalloc(h, &h->d_tp, std::max(1, n_topics)) || dalloc(h, &h->d_flags, 16)) {
         std::string m = h->err;
         gsim_destroy(h);
@@ -1549,14 +1545,6 @@ int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant)
     if (which == 8) {           // k_xbits_deliver: 0 = batched copies where the configuration allows, 1 = one at a time
         if (variant < 0 || variant > 1) { h->err = "unknown bit-apply variant (0 or 1)"; return GSIM_EINVAL; }
         h->xb_generic = variant == 1;
-        return GSIM_OK;
-    }
-    if (which == 7) {           // k_send_tm placement: 0 = one block per (topic, range) item, launch order;
-                                // 1 = persistent blocks from XCD work queues (topic t on XCD t % 8, stealing),
-                                // v >= 2: the same with v - 1 resident blocks per CU
-        if (variant < 0 || variant > 16) { h->err = "unknown delivery placement (0, 1, or 2..16)"; return GSIM_EINVAL; }
-        h->tm_xcd = variant >= 1;
-        if (variant >= 2) h->tm_resident = variant - 1;
         return GSIM_OK;
     }
     if (which == 6) {           // topic-major blocks: 0 = shared out by subscribers, 1 = the same per topic,

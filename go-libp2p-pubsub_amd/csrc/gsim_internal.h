@@ -467,10 +467,7 @@ struct gsim_handle {
     bool tm_uniform = false;  // k_send_tm blocks the same for every topic (gsim_set_kernel_variant(h, 6, 1))
     int64_t tm_budget = 0;    // k_send_tm blocks in all (0: ranges x T, launch_send_tm_tb)
     int ihave_w = 0;          // k_ihave lane group width (gsim_set_kernel_variant(h, 3, w)); 0 = by row lengths
-    bool tm_xcd = false;      // k_send_tm from XCD work queues (gsim_set_kernel_variant(h, 7, 1))
     bool xb_generic = false;  // k_xbits_deliver: listed_copy only, never the batched path (variant 8, 1)
-    int tm_resident = 3;      // ... resident blocks per CU of its persistent grid (variant 7, v >= 2: v - 1)
-    int n_cu = 256;           // compute units of the device
 
     // device: parameters and scratch flags
     gsim_topic_score_params* d_tp = nullptr;

@@ -785,12 +785,21 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
             rv[v] = valid[v] ? a.rev[e[v]] : 0u;           // this observer's record of col
             gcol[v] = valid[v] ? glob(a, col[v]) : 0u;
             // tracked (peerStats exists) matters only to a Graft / Prune: loaded then
+            // (GSIM_HB_EAGER_TRACKED, A/B builds: with the position's other fields)
             tracked[v] = have_trk[v] = false;
+#ifdef GSIM_HB_EAGER_TRACKED
+            tracked[v] = valid[v] && (a.estate[rv[v]] & GSIM_ES_TRACKED);
+            have_trk[v] = true;
+#endif
             conn[v] = valid[v] && (a.rstate[e[v]] & GSIM_ES_CONNECTED);
             outb[v] = valid[v] && a.outbound[e[v]];
             dir[v] = valid[v] && a.direct[e[v]];          // direct peers are never grafted or gossiped to
             S[v] = valid[v] ? a.score[rv[v]] : 0.0;
+#ifdef GSIM_HB_GATHER_SUB
+            subj[v] = valid[v] ? a.sub[col[v]] : 0ull;              // (A/B builds: always gathered)
+#else
             subj[v] = !valid[v] ? 0ull : a.sub_all ? ~0ull : a.sub[col[v]];
+#endif
             mj[v] = valid[v] ? smask_of(a.smask, col[v]) : 0ull;
             // live score for emitGossip: the snapshot until this heartbeat's
             // Graft/Prune touches one of the position's records; B bounds how far
@@ -828,6 +837,10 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
             for (int v = 0; v < V; ++v) {
                 amb[v] = false;
                 if (!need || !dirty[v]) { out[v] = S_live[v] >= a.gossip_thr; continue; }
+#ifdef GSIM_HB_EXACT_GOSSIP
+                amb[v] = true;                                // (A/B builds: every dirty position re-scored)
+                continue;
+#endif
                 const double eps = 0x1p-30 * (1.0 + fabs(S_live[v]) + B[v] + fabs(a.gossip_thr));
                 if (S_live[v] - B[v] - eps >= a.gossip_thr) out[v] = true;
                 else if (S_live[v] + B[v] + eps < a.gossip_thr) out[v] = false;

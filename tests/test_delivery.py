@@ -224,8 +224,7 @@ def _schedule(rng, ticks, T, R, rate, inv_frac, n):
     (1500, 24, 2, [1, 2, 3, 4], 6, 0.1, 0.02, 256, 3),
     (1200, 16, 2, [1, 2], 200, 0.1, 0.02, 1024, 3),         # > 64 active slots a topic: passes, layers
     (1200, 16, 2, [1, 2], 200, 0.1, 0.02, 1024, 36),        # the same, blocks the same per topic
-    (3000, 32, 10, [1, 2, 3], 12, 0.05, 0.02, 512, 37),     # XCD work queues (persistent blocks, 10 topics)
-    (1200, 16, 2, [1, 2], 200, 0.1, 0.02, 1024, 372),       # ... one block per CU, > 64 slots a topic
+    (3000, 32, 10, [1, 2, 3], 12, 0.05, 0.02, 512, 3),      # 10 topics
 ])
 def test_rounds_bit_exact(require_gpu, n, k, T, ticks, rate, inv_frac, retained, ring, send_variant):
     from fixtures import beacon_params, beacon_topic, synthetic_state
@@ -254,8 +253,6 @@ def test_rounds_bit_exact(require_gpu, n, k, T, ticks, rate, inv_frac, retained,
     eng.set_kernel_variant(2, int(str(send_variant)[0]))
     if send_variant == 36:
         eng.set_kernel_variant(6, 1)
-    if str(send_variant).startswith("37"):
-        eng.set_kernel_variant(7, 1 if send_variant == 37 else 2)
     sched = _schedule(rng, ticks, T, R, rate, inv_frac, n)
     lib = ob.load()
     for kk in ticks:
