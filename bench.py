@@ -180,6 +180,10 @@ def build_engine(cfg, seed, device, scen=None, shard=None):
         eng.set_kernel_variant(2, int(os.environ["GSIM_SEND_VARIANT"]))
     if os.environ.get("GSIM_TM_UNIFORM"):                        # topic-major blocks the same per topic
         eng.set_kernel_variant(6, int(os.environ["GSIM_TM_UNIFORM"]))
+    if os.environ.get("GSIM_FLIST_OFF"):                         # sparse rounds by the fresh-bit scan (A/B)
+        eng.set_kernel_variant(9, 1)
+    if os.environ.get("GSIM_XB_GENERIC"):                        # the bit apply one copy at a time (A/B)
+        eng.set_kernel_variant(8, 1)
     return eng, net
 
 

@@ -132,6 +132,13 @@ struct Deliver {
     uint32_t* d_clist_n = nullptr;     // [kClSub] entries, [kClSub] overflow (the commit then scans every word);
                                        // counter q at q * kClStride (one cache line each)
     int64_t clist_cap = 0;             // per sub-list
+    // forwarder lists (list-driven send, k_send_list): the commit of round g-1
+    // and the publications of round g-1 list round g's forwarders, so a sparse
+    // round walks them instead of scanning every slot's fresh bits
+    uint64_t* d_flist = nullptr;       // [2][flist_cap] by the send round's parity: peer | slot << 32 | origin << 63
+    uint32_t* d_fst = nullptr;         // [kFstBad + p]: the list of parity p is incomplete; [p * kFstStride]: entries
+    int64_t flist_cap = 0;
+    int64_t flist_round = -1;          // the send round whose forwarders only the list holds (no fresh bits)
     uint64_t* d_seenbm = nullptr;      // [ring][ceil(N/64)] bit: the cell is committed (a cache of the cells)
     uint64_t* d_fresh = nullptr;       // [ring][ceil(N/64)] bit: the peer forwards the slot's message next round
     uint64_t* d_fsum = nullptr;        // [ring][ceil(N/4096)] bit: that fresh word may be non-zero
@@ -263,6 +270,13 @@ struct RoundArgs {
     // only of a message published in the last kPubTicks ticks): listed copies
     // add theirs without a returned value, no spill (atomic_mcnt_inc)
     int32_t mcnt_fast;
+    // forwarder lists (Deliver::d_flist; nullptr: the fresh bits alone); flist_commit:
+    // the commit lists its forwarders instead of setting fresh bits
+    uint64_t* flist;
+    uint32_t* fst;
+    int64_t flist_cap;
+    int32_t flist_commit;
+    int32_t flist_send;            // k_send_tm: the list drives this round unless incomplete
     GaterRef gt;                   // peer gater (gater.hip; gt.act == nullptr: off)
     int32_t subdyn;                // a Leave happened: a receiver drops copies of topics it left
 };
@@ -425,6 +439,29 @@ __device__ __forceinline__ void clist_push_wave(const RoundArgs& a, bool on, uin
     }
 }
 
+// Forwarder list state (Deliver::d_fst): entries of parity p at p * kFstStride
+// (own cache lines), the incomplete flag of parity p at kFstBad + p
+constexpr int kFstStride = 32;
+constexpr int kFstBad = 2 * kFstStride;
+constexpr uint64_t kFlOrigin = 1ull << 63;
+
+// Append the lanes' forwarders (on) of send round g to its list; every lane
+// of the wave calls it.
+__device__ __forceinline__ void flist_push_wave(const RoundArgs& a, int64_t g, bool on, uint64_t v)
+{
+    const uint64_t b = __ballot(on);
+    if (!b) return;
+    const int lane = threadIdx.x & 63, leader = __builtin_ctzll(b), p = (int)(g & 1);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&a.fst[p * kFstStride], (uint32_t)__popcll(b));
+    base = (uint32_t)__shfl((int)base, leader, 64);
+    if (on) {
+        const uint32_t k = base + (uint32_t)__popcll(b & ((1ull << lane) - 1));
+        if ((int64_t)k < a.flist_cap) a.flist[(int64_t)p * a.flist_cap + k] = v;
+        else a.fst[kFstBad + p] = 1;
+    }
+}
+
 // Ordered list of the active slots (bit set in nnew), built by wave 0 into
 // LDS; every thread of the block must call it.
 __device__ __forceinline__ int active_slots(const uint32_t* nnew, int ring, uint16_t* s_act, int* s_n)
@@ -570,7 +607,15 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, const uint32_t* pslo
         a.cs.cell[oci] = ((uint64_t)(uint32_t)a.g << 32) | p.origin;
         atomicOr(reinterpret_cast<unsigned long long*>(a.seenbm + (int64_t)slot * a.nw + (oc >> 6)), 1ull << (oc & 63));
         // the origin publishes whatever the verdict (push: a ghost origin's own shard sends)
-        if (a.fresh && (!a.push || (oc >= a.rlo && oc < a.rhi))) fresh_set(a, slot, oc >> 6, 1ull << (oc & 63));
+        if (a.fresh && (!a.push || (oc >= a.rlo && oc < a.rhi))) {
+            fresh_set(a, slot, oc >> 6, 1ull << (oc & 63));
+            if (a.flist) {                                 // ... and in round g+1's forwarder list
+                const int pp = (int)((a.g + 1) & 1);
+                const uint32_t q = atomicAdd(&a.fst[pp * kFstStride], 1u);
+                if ((int64_t)q < a.flist_cap) a.flist[(int64_t)pp * a.flist_cap + q] = (uint64_t)oc | ((uint64_t)slot << 32) | kFlOrigin;
+                else a.fst[kFstBad + pp] = 1;
+            }
+        }
         int32_t* lp = a.lastput + (int64_t)p.topic * a.N + p.origin;
         const int32_t tick = (int32_t)(a.g / a.R);
         if (*lp < tick) *lp = tick;
@@ -773,6 +818,7 @@ __global__ __launch_bounds__(kTmThreads, PUSH ? GSIM_TM_MINB_PUSH
 void k_send_tm(RoundArgs a_)
 {
     const RoundArgs& a = a_;
+    if (a.flist_send && !a.fst[kFstBad + (int)(a.g & 1)]) return;   // k_send_list walks this round's list
     extern __shared__ uint64_t s_dyn[];
     uint16_t* s_slots = reinterpret_cast<uint16_t*>(s_dyn);  // [ring] active slots of topic t
     constexpr int kTmChunk = 2 * kTmThreads;                 // peers per chunk (two per thread)
@@ -1279,6 +1325,8 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
     extern __shared__ uint16_t s_act[];
     __shared__ int s_n;
     if (a.clist && !a.clist_n[kClSub * kClStride]) return;   // the claim list covers the round (k_commit_list)
+    // this scan sets the fresh bits: round g+1's forwarder list is incomplete
+    if (a.flist && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.fst[kFstBad + (int)((a.g + 1) & 1)] = 1;
     const int nact = active_slots(a.nnew_cur, a.ring, s_act, &s_n);
     const int lane = threadIdx.x & 63;
     // claims exist only at receivers' cells: the words of [rlo, rhi), a wave per
@@ -1348,20 +1396,30 @@ __global__ __launch_bounds__(256) void k_commit_list(RoundArgs a)
     const int64_t n = (int64_t)a.clist_n[q * kClStride];
     const uint32_t par = (uint32_t)(a.g & 1);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
-        const uint64_t v = a.clist[(int64_t)q * a.clist_cap + k];
-        const uint32_t i = (uint32_t)v, m = (uint32_t)(v >> 32);
-        const int64_t ci = SP ? a.cs.idx(m, (int32_t)a.mtopic[m], i) : (int64_t)m * a.cs.n + i;
-        if (ci < 0) continue;
-        uint64_t* cp = a.cs.cell + ci;
-        const uint64_t c = *cp;
-        if (!is_claim_of(c, par)) continue;
-        const int64_t w = (int64_t)(i >> 6);
-        const uint64_t bit = 1ull << (i & 63);
-        atomicOr(reinterpret_cast<unsigned long long*>(a.seenbm + (int64_t)m * a.nw + w), bit);
-        if (a.fresh && a.minv[m] == GSIM_VERDICT_ACCEPT) fresh_set(a, m, w, bit);
-        if (a.gt.act) commit_claim<true, false, SP, true>(a, cp, c, a.g, m, i);
-        else commit_claim<true, false, SP>(a, cp, c, a.g, m, i);
+    // (grid-stride with a wave-uniform trip count: flist_push_wave is called by every lane)
+    for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x; k0 < n; k0 += stride) {
+        const int64_t k = k0 + threadIdx.x;
+        bool fw = false;
+        uint64_t fv = 0;
+        if (k < n) {
+            const uint64_t v = a.clist[(int64_t)q * a.clist_cap + k];
+            const uint32_t i = (uint32_t)v, m = (uint32_t)(v >> 32);
+            const int64_t ci = SP ? a.cs.idx(m, (int32_t)a.mtopic[m], i) : (int64_t)m * a.cs.n + i;
+            uint64_t* cp = ci >= 0 ? a.cs.cell + ci : nullptr;
+            const uint64_t c = cp ? *cp : kUnseen64;
+            if (cp && is_claim_of(c, par)) {
+                const int64_t w = (int64_t)(i >> 6);
+                const uint64_t bit = 1ull << (i & 63);
+                atomicOr(reinterpret_cast<unsigned long long*>(a.seenbm + (int64_t)m * a.nw + w), bit);
+                if (a.fresh && a.minv[m] == GSIM_VERDICT_ACCEPT) {
+                    if (a.flist_commit) { fw = true; fv = (uint64_t)i | ((uint64_t)m << 32); }   // round g+1's list
+                    else fresh_set(a, m, w, bit);
+                }
+                if (a.gt.act) commit_claim<true, false, SP, true>(a, cp, c, a.g, m, i);
+                else commit_claim<true, false, SP>(a, cp, c, a.g, m, i);
+            }
+        }
+        if (a.flist_commit) flist_push_wave(a, a.g + 1, fw, fv);
     }
 }
 
@@ -2387,6 +2445,252 @@ __device__ __forceinline__ void listed_copy(const RoundArgs& a, uint32_t r, uint
     }
 }
 
+// The list-driven send (member-compacted cells): round
+// g's forwarders come as a list (Deliver::d_flist: the commit of round g-1's
+// claims and round g-1's publications), so a round with a sparse frontier
+// costs its forwarders' edges, not a scan of every active slot's fresh bits
+// in 1024-peer chunks with block-wide scans per slot layer (c5: DESIGN §4.2).
+// A block takes 256 entries, lays their walks out (a block scan of the walk
+// lengths) and runs one thread per edge, kLsP edges per thread in flight.
+// Each copy follows k_send_tm's rules (AcceptFrom, the claim of the receiver's
+// cell -- the lowest edge wins --, the score tracer); the entries of one
+// sender (its slots of a topic) may sit in different blocks, so its records
+// take atomic updates (atomic_mcnt_inc, the exact +1 steps in any order, as
+// listed_copy's).  Configurations with validation latency, the peer gater,
+// the trace or shards keep the scan (flist_allowed).
+constexpr int kLsP = 2;
+constexpr int kLsB = 256;
+__global__ __launch_bounds__(kLsB) void k_send_list(RoundArgs a_)
+{
+    const RoundArgs& a = a_;
+    extern __shared__ uint32_t s_new2[];                     // [ring/32] slots with a new claim
+    __shared__ uint32_t s_off[kLsB + 1];                     // first flattened edge of each entry
+    __shared__ uint32_t s_x[kLsB], s_m[kLsB], s_from[kLsB], s_beg[kLsB], s_pl[kLsB];
+    __shared__ uint64_t s_msk[kLsB];
+    __shared__ uint64_t s_cl[kLsB * kLsP];
+    __shared__ uint32_t s_wsum[kLsB / 64];
+    __shared__ unsigned long long s_stats[4];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int par = (int)(a.g & 1);
+    if (a.fst[kFstBad + par]) return;                        // incomplete: k_send_tm scans the fresh bits
+    const int64_t n = min((int64_t)a.fst[par * kFstStride], a.flist_cap);
+    const uint64_t* fl = a.flist + (int64_t)par * a.flist_cap;
+    for (int w = tid; w < (a.ring + 31) / 32; w += kLsB) s_new2[w] = 0;
+    if (tid < 4) s_stats[tid] = 0;
+    __syncthreads();
+    const uint32_t claim_hi = kClaim | ((uint32_t)par << 30);
+    unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
+    for (int64_t c0 = (int64_t)blockIdx.x * kLsB; c0 < n; c0 += (int64_t)gridDim.x * kLsB) {   // block-uniform
+        const RoundArgs& a = kernarg0(a_);
+        uint32_t len = 0, x = 0, m = 0, from = kPeerMask, beg = 0, pl = 0;
+        uint64_t msk = 0;
+        if (c0 + tid < n) {
+            const uint64_t v = fl[c0 + tid];
+            x = (uint32_t)v;
+            m = (uint32_t)(v >> 32) & 0x7FFFFFFFu;
+            const int32_t t = (int32_t)a.mtopic[m];
+            const uint32_t origin = a.morigin[m];
+            if (v & kFlOrigin)        // the origin's fresh bit (k_publish) is taken here
+                atomicAnd(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (x >> 6)), ~(1ull << (x & 63)));
+            const int64_t xc = a.cs.at((int64_t)a.cs.cbase[m], t, x);
+            from = xc >= 0 ? (uint32_t)a.cs.cell[xc] & kPeerMask : kPeerMask;
+            const uint64_t xm = smask_of(a.smask, x);
+            pl = (uint32_t)__popcll(xm & ((1ull << t) - 1ull));
+            const uint32_t rb = a.row_ptr[x], deg = a.row_ptr[x + 1] - rb;
+            if (!slot_has(xm, t) || a.g == 0) {
+                // no state for t in x's row: nothing is sent (cannot happen)
+            } else if (deg <= 64 && x != origin) {
+                msk = a.mmask[(int64_t)t * a.N + x];
+                beg = rb;
+                len = (uint32_t)__popcll(msk);
+            } else if (a.hlist && x != origin && a.hlist[((int64_t)a.hidx[x] * a.T + t) * (1 + kHubMesh)] != 0xFFFFFFFFu) {
+                const uint32_t lo_ = (uint32_t)(((int64_t)a.hidx[x] * a.T + t) * (1 + kHubMesh));
+                beg = kHubList | (lo_ + 1u);
+                len = a.hlist[lo_];
+            } else {
+                beg = rb;
+                len = deg;
+            }
+        }
+        // exclusive scan of the walk lengths
+        uint32_t inc = len;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) s_wsum[wid] = inc;
+        __syncthreads();
+        uint32_t wbase = 0, total = 0;
+        for (int q = 0; q < kLsB / 64; ++q) {
+            if (q < wid) wbase += s_wsum[q];
+            total += s_wsum[q];
+        }
+        s_off[tid] = wbase + inc - len;
+        if (tid == 0) s_off[kLsB] = total;
+        s_x[tid] = x; s_m[tid] = m; s_from[tid] = from; s_beg[tid] = beg; s_msk[tid] = msk; s_pl[tid] = pl;
+        __syncthreads();
+        for (uint32_t f0 = 0; f0 < total; f0 += kLsB * kLsP) {
+            const RoundArgs& a = kernarg0(a_);   // (re-read per iteration: SGPR pressure)
+            uint32_t jv[kLsP], ev[kLsP], iv[kLsP], qv[kLsP];
+            int64_t pv[kLsP];
+            uint8_t mfv[kLsP], dsv[kLsP], tfv[kLsP];
+            bool vv[kLsP], mk[kLsP];
+#pragma unroll
+            for (int u = 0; u < kLsP; ++u) {
+                const uint32_t fi = f0 + (uint32_t)(u * kLsB + tid);
+                vv[u] = fi < total;
+                int l = 0, r = kLsB;
+                while (r - l > 1) {                              // the entry whose walk holds edge fi
+                    const int mid = (l + r) >> 1;
+                    if (s_off[mid] <= fi) l = mid; else r = mid;
+                }
+                qv[u] = (uint32_t)l;
+                const uint32_t k = fi - s_off[l];
+                const uint64_t mq = s_msk[l];
+                const uint32_t bq = s_beg[l];
+                jv[u] = s_x[l];
+                mk[u] = mq != 0 || (bq & kHubList);
+                const int32_t t = (int32_t)a.mtopic[s_m[l]];
+                pv[u] = (a.smask ? (int64_t)s_pl[l] : (int64_t)t) * a.E;
+                if (!vv[u]) ev[u] = 0;
+                else if (mq) ev[u] = bq + kth_bit(mq, k);
+                else if (bq & kHubList) ev[u] = a.hlist[(bq & ~kHubList) + k];
+                else ev[u] = bq + k;
+            }
+#pragma unroll
+            for (int u = 0; u < kLsP; ++u) {
+                iv[u] = 0; mfv[u] = 0; dsv[u] = 0; tfv[u] = 0;
+                if (vv[u]) {
+                    const uint32_t e = ev[u];
+                    const int64_t pe = pv[u] + e;
+                    iv[u] = a.col[e]; dsv[u] = a.dstate[e];
+                    if (!mk[u]) mfv[u] = a.mflags[pe];
+                    tfv[u] = a.tflags[pe];
+                }
+            }
+            uint32_t clw = 0;
+#pragma unroll
+            for (int u = 0; u < kLsP; ++u) {
+                if (!vv[u]) continue;
+                const uint32_t j = jv[u], e = ev[u], i = iv[u], q = qv[u];
+                const uint32_t m = s_m[q];
+                const int32_t t = (int32_t)a.mtopic[m];
+                const uint32_t origin = a.morigin[m];
+                const ctp_t tp = const_tp(a.tp) + t;
+                const uint8_t vd = a.minv[m];
+                const bool inv = vd != GSIM_VERDICT_ACCEPT;
+                const bool pen = verdict_penalises(vd), seeable = vd != GSIM_VERDICT_SIGNATURE;
+                const uint8_t ds = dsv[u], tf = tfv[u];
+                bool sel;
+                if (mk[u]) {
+                    sel = !(ds & GSIM_DS_DIRECT) || (a.mflags[pv[u] + e] & GSIM_TF_MESH);
+                } else {
+                    const uint8_t ow = (origin < a.N && ((a.sub[origin] >> t) & 1ull)) ? GSIM_TF_MESH : GSIM_TF_FANOUT;
+                    sel = (mfv[u] & (j == origin ? ow : GSIM_TF_MESH)) != 0;
+                }
+                if (a.flood && j == origin) sel = ((a.sub[i] >> t) & 1ull) && a.score[a.rev[e]] >= a.pub_thr;
+                if ((ds & GSIM_DS_DIRECT) && !sel) sel = (a.sub[i] >> t) & 1ull;
+                const bool tg = sel && (ds & GSIM_DS_CONNECTED) && i != s_from[q] && i != origin;
+                const bool ok = tg && (ds & GSIM_DS_ACCEPT);
+                n_gray += tg && !ok;
+                if (!ok) continue;
+                if (a.subdyn && !((a.sub[i] >> t) & 1ull)) continue;   // a topic the receiver left
+                n_acc++;
+                const int64_t window = tp->mesh_message_deliveries_window_ns;
+                const bool sc = tp->scored && (ds & GSIM_DS_TRACKED);
+                const bool sbit = (a.seenbm[(int64_t)m * a.nw + (i >> 6)] >> (i & 63)) & 1ull;
+                const bool wa = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
+                const bool known = sbit && (wa || !sc || inv || !(tf & GSIM_TF_IN_MESH));
+                const int64_t ci = known ? 0 : a.cs.at((int64_t)a.cs.cbase[m], t, i);
+                if (ci < 0) continue;
+                uint32_t lo_w = j;
+                if (sc && !inv) {
+                    lo_w |= kCreditFirst;
+                    if (window < 0 && (tf & GSIM_TF_IN_MESH)) lo_w |= kCreditMesh;
+                }
+                const uint64_t cv = ((uint64_t)(claim_hi | e) << 32) | lo_w;
+                const bool fold = !sbit && seeable;
+                const uint64_t c = known ? 0ull
+                                 : fold ? __hip_atomic_fetch_min(a.cs.cell + ci, cv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                        : a.cs.cell[ci];
+                const uint32_t chi = (uint32_t)(c >> 32);
+                int64_t seen_round = -1;
+                if (known) seen_round = a.g - 1;
+                else if (c != kUnseen64) {
+                    if (!(chi & kClaim)) seen_round = chi;
+                    else if (((chi >> 30) & 1u) != (uint32_t)par) seen_round = a.g - 1;
+                }
+                if (fold || (seeable && seen_round < 0 && (c == kUnseen64 || (chi & kEdgeMask) > e))) {
+                    const uint64_t prev = fold ? c
+                                               : __hip_atomic_fetch_min(a.cs.cell + ci, cv, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_AGENT);
+                    if (prev == kUnseen64) {
+                        n_first++;
+                        atomicOr(&s_new2[m >> 5], 1u << (m & 31));
+                        clw |= 1u << u;
+                        s_cl[u * kLsB + tid] = (uint64_t)i | ((uint64_t)m << 32);
+                    }
+                }
+                if (!sc) continue;
+                const int64_t ir = pv[u] + e;
+                if (pen) {
+                    atomicAdd(&a.invalid[ir], 1.0);                   // markInvalidMessageDelivery
+                } else if (!inv && (tf & GSIM_TF_IN_MESH)) {
+                    const bool in_window = known ? true
+                                         : seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window)
+                                                           : (window >= 0);
+                    if (in_window)
+                        atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], tp->mesh_message_deliveries_cap, a.mcnt_fast);
+                }
+            }
+            if (a.clist) {
+#pragma unroll
+                for (int u = 0; u < kLsP; ++u) clist_push_wave(a, (clw >> u) & 1u, s_cl[u * kLsB + tid]);
+            }
+        }
+        __syncthreads();                                     // the entry tables are rewritten next
+    }
+    n_acc = wave_sum_u64(n_acc);
+    n_gray = wave_sum_u64(n_gray);
+    n_first = wave_sum_u64(n_first);
+    if (lane == 0 && (n_acc | n_gray)) {
+        atomicAdd(&s_stats[0], n_acc);
+        atomicAdd(&s_stats[1], n_first);
+        atomicAdd(&s_stats[3], n_gray);
+    }
+    __syncthreads();
+    for (int w = tid; w < (a.ring + 31) / 32; w += kLsB) {
+        uint32_t bits = s_new2[w];
+        if (!bits) continue;
+        atomicOr(&a.nnew_cur[w], bits);
+        while (bits) {
+            const int q = __ffs(bits) - 1;
+            bits &= bits - 1;
+            atomicMax(&a.slot_last[w * 32 + q], (int32_t)a.g);
+        }
+    }
+    if (tid == 0 && (s_stats[0] | s_stats[3])) {
+        atomicAdd(&a.stats[0], s_stats[0]);
+        atomicAdd(&a.stats[1], s_stats[1]);
+        atomicAdd(&a.stats[2], s_stats[0] - s_stats[1]);
+        atomicAdd(&a.stats[3], s_stats[3]);
+    }
+}
+
+// A list the send round will not walk (the configuration changed since its
+// commit): its forwarders as fresh bits for k_send_tm.
+__global__ __launch_bounds__(256) void k_flist_fresh(RoundArgs a)
+{
+    const int par = (int)(a.g & 1);
+    const int64_t n = min((int64_t)a.fst[par * kFstStride], a.flist_cap);
+    const uint64_t* fl = a.flist + (int64_t)par * a.flist_cap;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t v = fl[k];
+        const uint32_t x = (uint32_t)v, m = (uint32_t)(v >> 32) & 0x7FFFFFFFu;
+        fresh_set(a, m, (int64_t)(x >> 6), 1ull << (x & 63));
+    }
+}
+
 // Copies that arrive as a list of (record, slot): round 2's messages queued by
 // handleIWant (a shard's copies pushed by other shards arrive as bits:
 // k_xbits_deliver).  Same rules and tracer events as k_send_tm's copies.
@@ -2619,7 +2923,7 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_clist); f(d->d_clist_n); f(d->d_hidx); f(d->d_hrow); f(d->d_hlist); f(d->d_mlist); f(d->d_mloff); f(d->d_mcount); f(d->d_mmtab); f(d->d_hubw); f(d->d_mctab); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_flist); f(d->d_fst); f(d->d_clist); f(d->d_clist_n); f(d->d_hidx); f(d->d_hrow); f(d->d_hlist); f(d->d_mlist); f(d->d_mloff); f(d->d_mcount); f(d->d_mmtab); f(d->d_hubw); f(d->d_mctab); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_peertx); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
@@ -2677,6 +2981,14 @@ static bool list_commit(const gsim_handle* h)
     return h->dl && h->dl->d_clist && h->dl->sparse != 0 && !h->dl->lat_on;
 }
 
+// The list-driven send (k_send_list) runs for this configuration: claim-list
+// commits, and nothing k_send_list leaves to k_send_tm (the peer gater, the
+// trace, shards, validation latency)
+static bool flist_allowed(const gsim_handle* h)
+{
+    return list_commit(h) && h->dl->d_flist && !h->gt && !h->trace.ev && !h->sh && !h->flist_off;
+}
+
 static Cells deliver_cells(const Deliver* d)
 {
     Cells c;
@@ -2730,6 +3042,11 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
         a.clist = d->d_clist;
         a.clist_n = d->d_clist_n;
         a.clist_cap = d->clist_cap;
+    }
+    if (flist_allowed(h)) {
+        a.flist = d->d_flist;
+        a.fst = d->d_fst;
+        a.flist_cap = d->flist_cap;
     }
     const size_t w = (size_t)nnew_words(d);
     a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
@@ -3012,6 +3329,8 @@ int deliver_flush(gsim_handle* h)
     if (!d || d->pending < 0) return GSIM_OK;
     ProfScope ps(h, GSIM_K_COMMIT);
     RoundArgs a = make_round_args(h, d->pending);
+    a.flist_commit = a.flist != nullptr;       // round g+1's forwarders go to its list, not the fresh bits
+    d->flist_round = a.flist ? d->pending + 1 : -1;
     // member-compacted cells: a capped grid (the scan usually exits at once: the
     // claim list covers the round); dense: a wave per word
     const int gp = grid_peers((int64_t)a.rhi - ((int64_t)a.rlo & ~63ll));
@@ -3197,6 +3516,39 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
     return hip_check(h, hipGetLastError(), "k_send_tm");
 }
 
+// Round g's send: the forwarder list (k_send_list) when the commit of round
+// g-1 left it complete, else the scan of the fresh bits (k_send_tm, which
+// exits at once when the list covers the round: the device decides, the
+// list may have overflowed)
+static int launch_send(gsim_handle* h, RoundArgs& a, int64_t round)
+{
+    Deliver* d = h->dl;
+    const bool listed = d->flist_round == round;
+    const bool walk = listed && flist_allowed(h);
+    d->flist_round = -1;
+    if (listed && !walk && d->d_flist) {
+        // the configuration changed since the commit: the list as fresh bits
+        RoundArgs b = a;
+        b.flist = d->d_flist; b.fst = d->d_fst; b.flist_cap = d->flist_cap;
+        hipLaunchKernelGGL(k_flist_fresh, dim3(1024), dim3(256), 0, h->stream, b);
+    }
+    a.flist_send = walk ? 1 : 0;
+    int rc = launch_send_tm(h, a);
+    if (!rc && walk) {
+        const size_t lds = (size_t)nnew_words(d) * 4;
+        hipLaunchKernelGGL(k_send_list, dim3(2048), dim3(kLsB), lds, h->stream, a);
+        rc = hip_check(h, hipGetLastError(), "k_send_list");
+    }
+    if (!rc && d->d_fst) {
+        // this round's list is consumed: its parity is refilled by the next commit
+        const int p = (int)(round & 1);
+        hipError_t e = hipMemsetAsync(d->d_fst + p * kFstStride, 0, 4, h->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(d->d_fst + kFstBad + p, 0, 4, h->stream);
+        rc = hip_check(h, e, "forwarder list reset");
+    }
+    return rc;
+}
+
 // ---- round stages (gsim_round runs them in order; a sharded group
 // exchanges copies between send and post, control records after control,
 // and the IHAVE counts / holders inside the IHAVE stage, shard.hip) --------
@@ -3305,7 +3657,7 @@ int deliver_round_send(gsim_handle* h, int64_t round)
         // most lanes (C3: 21.0 against 32.9 ms per tick,
         // profiles/r02_ab_walk_masks.log)
         rc = gater_round_begin(h, a.now);   // the gate's state before the round's copies
-        if (!rc) rc = launch_send_tm(h, a);
+        if (!rc) rc = launch_send(h, a, round);
         if (rc) return rc;
         gater_round_sent(h, round);
         if (h->sh && h->sh->push) {                    // the copies to ghost receivers, per destination
@@ -4166,6 +4518,13 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
         A((void**)&d->d_clist, (size_t)d->clist_cap * kClSub * 8);
         A((void**)&d->d_clist_n, (kClSub + 1) * kClStride * 4);
         if (e == hipSuccess) e = hipMemsetAsync(d->d_clist_n, 0, (kClSub + 1) * kClStride * 4, h->stream);
+        // forwarder lists: a round's committed claims (the claim list's capacity:
+        // more overflow into the scan) and its publications
+        d->flist_cap = d->clist_cap * kClSub + (1 << 16);
+        A((void**)&d->d_flist, (size_t)d->flist_cap * 2 * 8);
+        A((void**)&d->d_fst, (kFstBad + kFstStride) * 4);
+        if (e == hipSuccess) e = hipMemsetAsync(d->d_fst, 0, (kFstBad + kFstStride) * 4, h->stream);
+        d->flist_round = -1;
     }
     if (h->max_degree > 64 && e == hipSuccess) {
         // hub rows and their mesh lists (k_hub_mesh)

@@ -1542,6 +1542,11 @@ int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant)
         h->ihave_w = variant;
         return GSIM_OK;
     }
+    if (which == 9) {           // sparse rounds: 0 = the list-driven send where the configuration allows, 1 = the scan
+        if (variant < 0 || variant > 1) { h->err = "unknown send driver (0 or 1)"; return GSIM_EINVAL; }
+        h->flist_off = variant == 1;
+        return GSIM_OK;
+    }
     if (which == 8) {           // k_xbits_deliver: 0 = batched copies where the configuration allows, 1 = one at a time
         if (variant < 0 || variant > 1) { h->err = "unknown bit-apply variant (0 or 1)"; return GSIM_EINVAL; }
         h->xb_generic = variant == 1;

@@ -468,6 +468,7 @@ struct gsim_handle {
     int64_t tm_budget = 0;    // k_send_tm blocks in all (0: ranges x T, launch_send_tm_tb)
     int ihave_w = 0;          // k_ihave lane group width (gsim_set_kernel_variant(h, 3, w)); 0 = by row lengths
     bool xb_generic = false;  // k_xbits_deliver: listed_copy only, never the batched path (variant 8, 1)
+    bool flist_off = false;   // never the list-driven send k_send_list (gsim_set_kernel_variant(h, 9, 1))
 
     // device: parameters and scratch flags
     gsim_topic_score_params* d_tp = nullptr;

@@ -57,7 +57,6 @@ struct HbArgs {
     int32_t T;
     const uint32_t *row_ptr, *col, *rev;
     const uint64_t* sub;
-    int32_t sub_all;           // every peer announced every topic (gsim_handle::sub_all): no sub[col] gather
     const uint64_t* smask;     // topic slots of each row owner (nullptr: dense; gsim_internal.h)
     const uint8_t* outbound;
     const uint8_t* direct;     // [E] edge order: col[e] is in the observer's gs.direct set
@@ -318,22 +317,6 @@ __device__ __forceinline__ void stats_prune(const HbArgs& a, bool tracked, bool 
     }
     if (fl & GSIM_TF_IN_MESH) a.mtime[sf.ir] = 0;   // meshTime outside the mesh is 0
     fl &= (uint8_t)~GSIM_TF_IN_MESH;
-}
-
-// How far one Graft or Prune of topic t can move the score of a record
-// (score.go:265-342 with 649-691): they change only the topic's P1 (meshTime
-// reset or left: |p1| <= TimeInMeshCap, a non-negative meshTime in lazy
-// mode), P3 (the activation cleared: a deficit <= threshold, meshd >= 0) and
-// P3b (a Prune adds at most threshold^2 to meshFailurePenalty); the topic
-// score cap is 1-Lipschitz, P2, P4-P7 do not move.
-__device__ __forceinline__ double bound_graft_prune(ctp_t tp)
-{
-    if (!tp->scored) return 0.0;
-    const double cap1 = tp->time_in_mesh_quantum_ns != 0 ? fabs(tp->time_in_mesh_cap) : 0.0;
-    const double th3 = tp->mesh_message_deliveries_threshold > 0 ? tp->mesh_message_deliveries_threshold : 0.0;
-    return fabs(tp->topic_weight) * (cap1 * fabs(tp->time_in_mesh_weight) +
-                                     th3 * th3 * (fabs(tp->mesh_message_deliveries_weight) +
-                                                  fabs(tp->mesh_failure_penalty_weight)));
 }
 
 // peerScore.score of one record (score.go:265-342), in the score pass's
@@ -772,9 +755,9 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
         const uint64_t mi = ovalid ? smask_of(a.smask, (uint32_t)obs) : 0ull;
         // per position v of this thread: row position g.pos(v)
         int gl[V];
-        bool valid[V], tracked[V], have_trk[V], conn[V], outb[V], dir[V], dirty[V];
+        bool valid[V], tracked[V], conn[V], outb[V], dir[V], dirty[V];
         uint32_t e[V], col[V], rv[V], gcol[V];
-        double S[V], S_live[V], B[V];
+        double S[V], S_live[V];
         uint64_t subj[V], mj[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) {
@@ -784,38 +767,20 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
             col[v] = valid[v] ? a.col[e[v]] : 0u;
             rv[v] = valid[v] ? a.rev[e[v]] : 0u;           // this observer's record of col
             gcol[v] = valid[v] ? glob(a, col[v]) : 0u;
-            // tracked (peerStats exists) matters only to a Graft / Prune: loaded then
-            // (GSIM_HB_EAGER_TRACKED, A/B builds: with the position's other fields)
-            tracked[v] = have_trk[v] = false;
-#ifdef GSIM_HB_EAGER_TRACKED
-            tracked[v] = valid[v] && (a.estate[rv[v]] & GSIM_ES_TRACKED);
-            have_trk[v] = true;
-#endif
+            const uint8_t est = valid[v] ? a.estate[rv[v]] : 0;
+            tracked[v] = est & GSIM_ES_TRACKED;
             conn[v] = valid[v] && (a.rstate[e[v]] & GSIM_ES_CONNECTED);
             outb[v] = valid[v] && a.outbound[e[v]];
             dir[v] = valid[v] && a.direct[e[v]];          // direct peers are never grafted or gossiped to
             S[v] = valid[v] ? a.score[rv[v]] : 0.0;
-#ifdef GSIM_HB_GATHER_SUB
-            subj[v] = valid[v] ? a.sub[col[v]] : 0ull;              // (A/B builds: always gathered)
-#else
-            subj[v] = !valid[v] ? 0ull : a.sub_all ? ~0ull : a.sub[col[v]];
-#endif
+            subj[v] = valid[v] ? a.sub[col[v]] : 0ull;
             mj[v] = valid[v] ? smask_of(a.smask, col[v]) : 0ull;
             // live score for emitGossip: the snapshot until this heartbeat's
-            // Graft/Prune touches one of the position's records; B bounds how far
-            // those changes can have moved it since the last exact value
+            // Graft/Prune touches one of the position's records
             S_live[v] = S[v];
-            B[v] = 0.0;
             dirty[v] = false;
             if (a.gossip && valid[v]) a.gstate[e[v]] = S[v] >= a.gossip_thr ? 1 : 0;
         }
-        auto trk = [&](int v) {
-            if (!have_trk[v]) {
-                tracked[v] = valid[v] && (a.estate[rv[v]] & GSIM_ES_TRACKED);
-                have_trk[v] = true;
-            }
-            return tracked[v];
-        };
         g.load_lastput(a, obs, subi, ovalid);
         uint64_t pxt = 0;                               // topics with a PRUNE carrying PX
         auto rescore = [&]() {                          // live scores of the dirty positions
@@ -824,36 +789,6 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
                 for (int v = 0; v < V; ++v) {
                     if (dirty[v]) S_live[v] = score_of_record(a, rv[v], col[v]);
                     dirty[v] = false;
-                    B[v] = 0.0;
-                }
-            }
-        };
-        // S_live >= gossipThreshold: decided from S_live +- B when the interval
-        // lies on one side of the threshold (Graft / Prune move a record's
-        // score by at most B, bound_graft_prune), else from the exact live score
-        auto live_ge = [&](bool need, bool* out) {
-            bool amb[V];
-#pragma unroll
-            for (int v = 0; v < V; ++v) {
-                amb[v] = false;
-                if (!need || !dirty[v]) { out[v] = S_live[v] >= a.gossip_thr; continue; }
-#ifdef GSIM_HB_EXACT_GOSSIP
-                amb[v] = true;                                // (A/B builds: every dirty position re-scored)
-                continue;
-#endif
-                const double eps = 0x1p-30 * (1.0 + fabs(S_live[v]) + B[v] + fabs(a.gossip_thr));
-                if (S_live[v] - B[v] - eps >= a.gossip_thr) out[v] = true;
-                else if (S_live[v] + B[v] + eps < a.gossip_thr) out[v] = false;
-                else amb[v] = true;
-            }
-            if (g.any(amb)) {
-#pragma unroll
-                for (int v = 0; v < V; ++v) {
-                    if (!amb[v]) continue;
-                    S_live[v] = score_of_record(a, rv[v], col[v]);
-                    dirty[v] = false;
-                    B[v] = 0.0;
-                    out[v] = S_live[v] >= a.gossip_thr;
                 }
             }
         };
@@ -895,9 +830,6 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
             const bool scored = tp->scored != 0;
             const double thr = tp->mesh_message_deliveries_threshold;
             const double mcap = tp->mesh_message_deliveries_cap;
-            // how far one Graft / Prune of this topic can move a record's score
-            // (infinite: the exact re-score decides)
-            const double bt = a.mt_lazy ? bound_graft_prune(tp) : INFINITY;
             int64_t i[V];
             ScoreFlags sf[V];
             uint8_t fl[V], fl0[V], ctl[V];
@@ -925,8 +857,8 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
             };
             auto prune = [&](int v) {
                 if (a.tr.on((uint32_t)obs)) a.tr.push(a.now, 0, (uint32_t)obs, col[v], t, GSIM_TRACE_PRUNE, 0);
-                stats_prune(a, trk(v), scored, thr, mcap, sf[v]);
-                if (tracked[v] && scored && sf[v].ok) { dirty[v] = true; B[v] += bt; }
+                stats_prune(a, tracked[v], scored, thr, mcap, sf[v]);
+                dirty[v] |= tracked[v] && scored;
                 fl[v] &= (uint8_t)~GSIM_TF_MESH;
                 m[v] = false;
                 need_bo(v);
@@ -936,8 +868,8 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
             };
             auto graft = [&](int v) {
                 if (a.tr.on((uint32_t)obs)) a.tr.push(a.now, 0, (uint32_t)obs, col[v], t, GSIM_TRACE_GRAFT, 0);
-                stats_graft(a, trk(v), scored, sf[v]);
-                if (tracked[v] && scored && sf[v].ok) { dirty[v] = true; B[v] += bt; }
+                stats_graft(a, tracked[v], scored, sf[v]);
+                dirty[v] |= tracked[v] && scored;
                 fl[v] |= GSIM_TF_MESH;
                 m[v] = true;
                 ctl[v] |= GSIM_CTL_GRAFT;
@@ -1184,14 +1116,10 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
                 for (int v = 0; v < V; ++v) gs[v] = false;
                 const int32_t lpt = g.lastput(a, obs, t);
                 if (lpt >= 0 && lpt >= (int64_t)a.tick - a.hist_gossip) {   // -1: no put yet
-                    bool ge[V];
-                    bool need = false;
-#pragma unroll
-                    for (int v = 0; v < V; ++v) need |= tpeer[v] && !m[v] && !dir[v];
-                    live_ge(need, ge);
+                    rescore();
 #pragma unroll
                     for (int v = 0; v < V; ++v)
-                        cand[v] = tpeer[v] && !m[v] && !dir[v] && ge[v];
+                        cand[v] = tpeer[v] && !m[v] && !dir[v] && S_live[v] >= a.gossip_thr;
                     g.gossip(a, cand, tpeer, gobs, t, gcol, gs);
                 }
 #pragma unroll
@@ -2583,7 +2511,6 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     HbArgs a{};
     a.N = h->n; a.E = h->e; a.T = h->t;
     a.row_ptr = h->d_row_ptr; a.col = h->d_col; a.rev = h->d_rev; a.sub = h->d_sub; a.smask = h->d_smask;
-    a.sub_all = h->all_joined ? 1 : 0;
     a.outbound = h->d_outbound; a.direct = h->d_direct; a.estate = h->d_estate; a.score = h->d_score; a.tp = h->d_tp;
     a.tflags = h->d_tflags; a.mflags = h->d_mflags; a.rstate = h->d_rstate; a.backoff = h->d_backoff; a.meshd = h->d_meshd; a.fail = h->d_fail; a.bp = h->d_bp;
     a.graft = h->d_graft; a.mtime = h->d_mtime; a.mcnt = h->d_mcnt;
