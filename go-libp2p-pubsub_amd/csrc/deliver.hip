@@ -64,6 +64,13 @@ __device__ __forceinline__ bool verdict_penalises(uint8_t v)
 #define GSIM_SLOT_BATCH 8
 #endif
 constexpr int kSlotBatch = GSIM_SLOT_BATCH;      // active slots whose cells are loaded together
+#ifndef GSIM_SPLIT_BATCH
+#define GSIM_SPLIT_BATCH 2
+#endif
+#ifndef GSIM_SPLIT_GROUPS
+#define GSIM_SPLIT_GROUPS 16
+#endif
+constexpr int kSplitBatch = GSIM_SPLIT_BATCH;    // ... per wave of a shard's split commit (k_commit<SPLIT>)
 constexpr int kClSub = 64;
 constexpr int kClStride = 32;       // u32s between two claim sub-list counters (own cache lines)
 constexpr int kHubMesh = 16;       // mesh | direct edges listed per (hub, topic); more: the whole row is walked
@@ -1338,19 +1345,21 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
         const int64_t i = i0 + lane;
         const bool vi = i < a.CN;
         const uint32_t par = (uint32_t)(a.g & 1);
-        for (int k0 = SPLIT ? (int)blockIdx.y * kSlotBatch : 0; k0 < nact;
-             k0 += (SPLIT ? (int)gridDim.y : 1) * kSlotBatch) {
-            uint64_t cv[kSlotBatch];
-            int64_t ci[SP ? kSlotBatch : 1];   // the dense layout recomputes m * N + i
+        // (SPLIT: batches of kSplitBatch slots dealt over gridDim.y -- parallel
+        // waves instead of cells in flight per wave)
+        constexpr int kB = SPLIT ? kSplitBatch : kSlotBatch;
+        for (int k0 = SPLIT ? (int)blockIdx.y * kB : 0; k0 < nact; k0 += (SPLIT ? (int)gridDim.y : 1) * kB) {
+            uint64_t cv[kB];
+            int64_t ci[SP ? kB : 1];           // the dense layout recomputes m * N + i
 #pragma unroll
-            for (int b = 0; b < kSlotBatch; ++b) {
+            for (int b = 0; b < kB; ++b) {
                 const int k = k0 + b;
                 const int64_t c = (k < nact && vi) ? word_cell<SP>(a.cs, a.mtopic, s_act[k], i0 >> 6, lane) : -1;
                 if constexpr (SP) ci[b] = c;
                 cv[b] = c >= 0 ? a.cs.cell[c] : kUnseen64;
             }
 #pragma unroll
-            for (int b = 0; b < kSlotBatch; ++b) {
+            for (int b = 0; b < kB; ++b) {
                 const int k = k0 + b;
                 const uint64_t cb = __ballot(k < nact && is_claim_of(cv[b], par));
                 if (cb && lane == 0) {
@@ -1366,7 +1375,7 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
                 }
             }
 #pragma unroll
-            for (int b = 0; b < kSlotBatch; ++b) {
+            for (int b = 0; b < kB; ++b) {
                 const int k = k0 + b;
                 if (k >= nact) break;
                 int qpl = -1;
@@ -3348,7 +3357,8 @@ int deliver_flush(gsim_handle* h)
     else if (sparse_layout(h))
         hipLaunchKernelGGL((k_commit<false, true>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     else if (split)
-        hipLaunchKernelGGL((k_commit<false, false, false, true>), dim3(gp, 4), dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t),
+        hipLaunchKernelGGL((k_commit<false, false, false, true>), dim3(gp, GSIM_SPLIT_GROUPS), dim3(256),
+                           (size_t)d->cfg.ring * sizeof(uint16_t),
                            h->stream, a);
     else
         hipLaunchKernelGGL((k_commit<false, false>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
