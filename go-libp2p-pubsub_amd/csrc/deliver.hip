@@ -65,10 +65,10 @@ __device__ __forceinline__ bool verdict_penalises(uint8_t v)
 #endif
 constexpr int kSlotBatch = GSIM_SLOT_BATCH;      // active slots whose cells are loaded together
 #ifndef GSIM_SPLIT_BATCH
-#define GSIM_SPLIT_BATCH 2
+#define GSIM_SPLIT_BATCH 8
 #endif
 #ifndef GSIM_SPLIT_GROUPS
-#define GSIM_SPLIT_GROUPS 16
+#define GSIM_SPLIT_GROUPS 4
 #endif
 constexpr int kSplitBatch = GSIM_SPLIT_BATCH;    // ... per wave of a shard's split commit (k_commit<SPLIT>)
 constexpr int kClSub = 64;
@@ -443,6 +443,23 @@ __device__ __forceinline__ void clist_push_wave(const RoundArgs& a, bool on, uin
         const uint32_t k = base + (uint32_t)__popcll(b & ((1ull << lane) - 1));
         if ((int64_t)k < a.clist_cap) a.clist[(int64_t)q * a.clist_cap + k] = v;
         else atomicOr(&a.clist_n[kClSub * kClStride], 1u);
+    }
+}
+
+// Slots of word w (bits) got a new claim in round g: their activity bit and
+// last-active round.  Every block of a launch reports the slots it touched,
+// and same-address atomics serialise (thousands of blocks on ~40 slots), so a
+// value already there -- a load returns it or an older one, both only grow
+// within the round -- is not written again.
+__device__ __forceinline__ void slots_claimed(const RoundArgs& a, int w, uint32_t bits)
+{
+    const uint32_t have = __hip_atomic_load(&a.nnew_cur[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((have & bits) != bits) atomicOr(&a.nnew_cur[w], bits);
+    while (bits) {
+        const int q = __ffs(bits) - 1;
+        bits &= bits - 1;
+        int32_t* sl = &a.slot_last[w * 32 + q];
+        if (__hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int32_t)a.g) atomicMax(sl, (int32_t)a.g);
     }
 }
 
@@ -1299,8 +1316,7 @@ void k_send_tm(RoundArgs a_)
         __syncthreads();
         if (tid < nb && ((s_clm >> tid) & 1ull)) {
             const uint32_t m = s_m[tid];
-            atomicOr(&a.nnew_cur[m >> 5], 1u << (m & 31));
-            atomicMax(&a.slot_last[m], (int32_t)a.g);
+            slots_claimed(a, (int)(m >> 5), 1u << (m & 31));
         }
         __syncthreads();                                         // the pass's slot table is rewritten next
     }
@@ -2671,12 +2687,7 @@ __global__ __launch_bounds__(kLsB) void k_send_list(RoundArgs a_)
     for (int w = tid; w < (a.ring + 31) / 32; w += kLsB) {
         uint32_t bits = s_new2[w];
         if (!bits) continue;
-        atomicOr(&a.nnew_cur[w], bits);
-        while (bits) {
-            const int q = __ffs(bits) - 1;
-            bits &= bits - 1;
-            atomicMax(&a.slot_last[w * 32 + q], (int32_t)a.g);
-        }
+        slots_claimed(a, w, bits);
     }
     if (tid == 0 && (s_stats[0] | s_stats[3])) {
         atomicAdd(&a.stats[0], s_stats[0]);
@@ -2746,12 +2757,7 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a_, const uint
     for (int w = threadIdx.x; w < (a.ring + 31) / 32; w += blockDim.x) {
         uint32_t bits = s_new2[w];
         if (!bits) continue;
-        atomicOr(&a.nnew_cur[w], bits);
-        while (bits) {
-            const int q = __ffs(bits) - 1;
-            bits &= bits - 1;
-            atomicMax(&a.slot_last[w * 32 + q], (int32_t)a.g);
-        }
+        slots_claimed(a, w, bits);
     }
     if (threadIdx.x == 0 && (s_stats[0] | s_stats[3])) {
         atomicAdd(&a.stats[0], s_stats[0]);
@@ -3894,12 +3900,7 @@ __global__ __launch_bounds__(256, GSIM_XB_WPE) void k_xbits_deliver(RoundArgs a_
     for (int w = threadIdx.x; w < (a.ring + 31) / 32; w += blockDim.x) {
         uint32_t bits = s_new2[w];
         if (!bits) continue;
-        atomicOr(&a.nnew_cur[w], bits);
-        while (bits) {
-            const int q = __ffs(bits) - 1;
-            bits &= bits - 1;
-            atomicMax(&a.slot_last[w * 32 + q], (int32_t)a.g);
-        }
+        slots_claimed(a, w, bits);
     }
     if (threadIdx.x == 0 && (s_stats[0] | s_stats[3])) {
         atomicAdd(&a.stats[0], s_stats[0]);
@@ -3926,7 +3927,9 @@ int deliver_xbits_apply(gsim_handle* h, int64_t round, const uint64_t* in, const
     Deliver* d = h->dl;
     RoundArgs a = make_round_args(h, round);
     const size_t lds2 = (size_t)nnew_words(d) * 4;
-    const uint32_t grid = (uint32_t)std::min<int64_t>((ntask + 3) / 4, 8192);
+    // (blocks that fill the chip several times over: each block's end-of-run
+    // slot and total updates contend on a few addresses)
+    const uint32_t grid = (uint32_t)std::min<int64_t>((ntask + 3) / 4, 2048);
     hipLaunchKernelGGL(k_xbits_deliver, dim3(grid), dim3(256), lds2, h->stream, a, in, d_src, (int32_t)K,
                        ntask, (const uint32_t*)h->d_owner, (int32_t)(h->xb_generic ? 0 : 1));
     return hip_check(h, hipGetLastError(), "k_xbits_deliver");
