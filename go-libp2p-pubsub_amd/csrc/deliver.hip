@@ -166,7 +166,7 @@ struct Deliver {
     int64_t* d_roff = nullptr;         // [rounds] offset of each round in its heartbeat
     int32_t* d_lastput = nullptr;      // [T][N]
     uint32_t* d_nnew = nullptr;        // [2][ring/32] bitmask: slots with new claims (or a publication), by round parity
-    unsigned long long* d_stats = nullptr;   // [4]
+    unsigned long long* d_stats = nullptr;   // [kStatLanes][kStatStride]: 4 totals per lane (stats_add)
     uint32_t* d_seen32 = nullptr;      // scratch for the F_SEEN view
     gsim_msg* d_pub = nullptr;
     int32_t pub_cap = 0;
@@ -286,7 +286,30 @@ struct RoundArgs {
     int32_t flist_send;            // k_send_tm: the list drives this round unless incomplete
     GaterRef gt;                   // peer gater (gater.hip; gt.act == nullptr: off)
     int32_t subdyn;                // a Leave happened: a receiver drops copies of topics it left
+    uint32_t* inv_live;            // the invalid-plane flag the next refresh reads (inv_mark)
 };
+
+// The delivery totals: a block adds its 4 counts to one of kStatLanes
+// cache-line-padded copies (by block index), so the thousands of blocks of a
+// launch do not queue on 4 addresses; gsim_msg_stats sums the lanes.
+constexpr int kStatLanes = 64, kStatStride = 16;
+__device__ __forceinline__ void stats_add(const RoundArgs& a, unsigned long long acc, unsigned long long first,
+                                          unsigned long long gray)
+{
+    unsigned long long* s = a.stats + (size_t)(blockIdx.x & (kStatLanes - 1)) * kStatStride;
+    atomicAdd(&s[0], acc);
+    atomicAdd(&s[1], first);
+    atomicAdd(&s[2], acc - first);
+    atomicAdd(&s[3], gray);
+}
+
+// A copy raised an invalidMessageDeliveries counter: the next refresh must
+// read that plane (engine.hip k_refresh_score skips it while the flag is 0)
+__device__ __forceinline__ void inv_mark(const RoundArgs& a)
+{
+    if (a.inv_live && !__hip_atomic_load(a.inv_live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        __hip_atomic_store(a.inv_live, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // The peer gater's AcceptFrom (peer_gater.go:320-363) at receiver i for a
 // copy from sender j, record r (i's record of j: its stats group gq[r]),
@@ -1270,6 +1293,7 @@ void k_send_tm(RoundArgs a_)
                             const int64_t ir = pv[u] + e;
                             if (pen) {
                                 a.invalid[ir] = xv[u] + 1.0;
+                                inv_mark(a);
                             } else if (!inv && (tf & GSIM_TF_IN_MESH)) {
                                 const bool in_window = known ? true
                                                      : seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window)
@@ -1330,10 +1354,7 @@ void k_send_tm(RoundArgs a_)
     }
     __syncthreads();
     if (tid == 0 && (s_stats[0] | s_stats[3])) {
-        atomicAdd(&a.stats[0], s_stats[0]);
-        atomicAdd(&a.stats[1], s_stats[1]);
-        atomicAdd(&a.stats[2], s_stats[0] - s_stats[1]);
-        atomicAdd(&a.stats[3], s_stats[3]);
+        stats_add(a, s_stats[0], s_stats[1], s_stats[3]);
     }
 }
 
@@ -2418,7 +2439,7 @@ __device__ __forceinline__ void listed_copy(const RoundArgs& a, uint32_t r, uint
         const bool wa = window >= 0 && a.now - round_time(a, a.mpub[m]) <= window;
         if (wa || !sc || inv || !(tf & GSIM_TF_IN_MESH)) {
             if (!sc) return;
-            if (pen) atomicAdd(&a.invalid[ir], 1.0);
+            if (pen) { atomicAdd(&a.invalid[ir], 1.0); inv_mark(a); }
             else if (!inv && (tf & GSIM_TF_IN_MESH))         // wa: within the window
                 atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], tp->mesh_message_deliveries_cap, a.mcnt_fast);
             return;
@@ -2464,6 +2485,7 @@ __device__ __forceinline__ void listed_copy(const RoundArgs& a, uint32_t r, uint
     if (!sc) return;
     if (pen) {
         atomicAdd(&a.invalid[ir], 1.0);                           // markInvalidMessageDelivery
+        inv_mark(a);
     } else if (!inv && (tf & GSIM_TF_IN_MESH)) {
         const bool in_window = seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window) : (window >= 0);
         if (in_window) atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], tp->mesh_message_deliveries_cap, a.mcnt_fast);
@@ -2660,6 +2682,7 @@ __global__ __launch_bounds__(kLsB) void k_send_list(RoundArgs a_)
                 const int64_t ir = pv[u] + e;
                 if (pen) {
                     atomicAdd(&a.invalid[ir], 1.0);                   // markInvalidMessageDelivery
+                    inv_mark(a);
                 } else if (!inv && (tf & GSIM_TF_IN_MESH)) {
                     const bool in_window = known ? true
                                          : seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window)
@@ -2690,10 +2713,7 @@ __global__ __launch_bounds__(kLsB) void k_send_list(RoundArgs a_)
         slots_claimed(a, w, bits);
     }
     if (tid == 0 && (s_stats[0] | s_stats[3])) {
-        atomicAdd(&a.stats[0], s_stats[0]);
-        atomicAdd(&a.stats[1], s_stats[1]);
-        atomicAdd(&a.stats[2], s_stats[0] - s_stats[1]);
-        atomicAdd(&a.stats[3], s_stats[3]);
+        stats_add(a, s_stats[0], s_stats[1], s_stats[3]);
     }
 }
 
@@ -2760,10 +2780,7 @@ __global__ __launch_bounds__(256) void k_gossip_deliver(RoundArgs a_, const uint
         slots_claimed(a, w, bits);
     }
     if (threadIdx.x == 0 && (s_stats[0] | s_stats[3])) {
-        atomicAdd(&a.stats[0], s_stats[0]);
-        atomicAdd(&a.stats[1], s_stats[1]);
-        atomicAdd(&a.stats[2], s_stats[0] - s_stats[1]);
-        atomicAdd(&a.stats[3], s_stats[3]);
+        stats_add(a, s_stats[0], s_stats[1], s_stats[3]);
     }
 }
 
@@ -2814,7 +2831,7 @@ __global__ __launch_bounds__(256) void k_vq_apply(RoundArgs a, int pl)
         const uint64_t mj = smask_of(a.smask, a.owner[e]);     // the sender's row
         if (!slot_has(mj, t)) continue;
         const int64_t ir = slot_idx(mj, t, a.E, e);
-        if (kind == kVqInv) { atomicAdd(&a.invalid[ir], 1.0); continue; }
+        if (kind == kVqInv) { atomicAdd(&a.invalid[ir], 1.0); inv_mark(a); continue; }
         const ctp_t tp = tpa + t;
         // the winner's own copy was queued as kVqDup too: its kVqFirst adds
         // only markFirstMessageDelivery's P2 part
@@ -2851,6 +2868,7 @@ __global__ __launch_bounds__(256) void k_vq_counts(RoundArgs a, int pl)
                 double x = a.invalid[ir];
                 for (uint32_t k = 0; k < ni; ++k) x = x + 1.0;
                 a.invalid[ir] = x;
+                inv_mark(a);
             }
             if (nd && (a.tflags[ir] & GSIM_TF_IN_MESH))
                 a.meshd[ir] = apply_incs(a.meshd[ir], nd, (tpa + t)->mesh_message_deliveries_cap);
@@ -3067,6 +3085,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
     a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
     a.nnew_cur = d->d_nnew + (size_t)(g & 1) * w;
     a.stats = d->d_stats;
+    a.inv_live = h->d_inv_live ? h->d_inv_live + (h->inv_par & 1) : nullptr;
     a.slot_last = d->d_slot_last;
     a.err = d->d_nresp;
     a.reuse_guard = (std::max(h->gp.history_gossip, h->gp.history_length) + d->prom_ticks + 2) * d->cfg.rounds;
@@ -3812,6 +3831,7 @@ __device__ __forceinline__ void listed_copies_fast(const RoundArgs& a, const uin
         if (!sc[u]) continue;
         if (pen) {
             atomicAdd(&a.invalid[ir], 1.0);                           // markInvalidMessageDelivery
+            inv_mark(a);
         } else if (!inv && (tf[u] & GSIM_TF_IN_MESH)) {
             const bool in_window = known[u] ? true
                                  : seen_round >= 0 ? (a.now - round_time(a, seen_round) <= window) : (window >= 0);
@@ -3903,10 +3923,7 @@ __global__ __launch_bounds__(256, GSIM_XB_WPE) void k_xbits_deliver(RoundArgs a_
         slots_claimed(a, w, bits);
     }
     if (threadIdx.x == 0 && (s_stats[0] | s_stats[3])) {
-        atomicAdd(&a.stats[0], s_stats[0]);
-        atomicAdd(&a.stats[1], s_stats[1]);
-        atomicAdd(&a.stats[2], s_stats[0] - s_stats[1]);
-        atomicAdd(&a.stats[3], s_stats[3]);
+        stats_add(a, s_stats[0], s_stats[1], s_stats[3]);
     }
 }
 
@@ -4570,7 +4587,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     A((void**)&d->d_roff, (size_t)cfg->rounds * 8);
     A((void**)&d->d_lastput, T * N * 4);
     A((void**)&d->d_nnew, 2 * words * 4);
-    A((void**)&d->d_stats, 4 * 8);
+    A((void**)&d->d_stats, kStatLanes * kStatStride * 8);
     // promises live from round 0 of tick k until the first heartbeat after
     // round_time(kR) + IWantFollowupTime; one spare ring index
     {
@@ -4622,7 +4639,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     if (e == hipSuccess) e = hipMemsetAsync(d->d_minv, 0, ring, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_mlat, 0, ring, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_nnew, 0, 2 * words * 4, h->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(d->d_stats, 0, 4 * 8, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d->d_stats, 0, kStatLanes * kStatStride * 8, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_slot_last, 0xFF, ring * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_gsel, 0, (size_t)std::max(1, h->S) * (size_t)h->e, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_gstate, 0, (size_t)h->e, h->stream);
@@ -4806,13 +4823,17 @@ int gsim_msg_stats(gsim_handle* h, int64_t* out4)
     if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
     Deliver* d = h->dl;
     if (!d) { h->err = "gsim_msgs_init not called"; return GSIM_ESTATE; }
-    unsigned long long s[4];
+    unsigned long long sl[kStatLanes * kStatStride];
     uint32_t err[4] = {0, 0, 0, 0};
-    hipError_t e = hipMemcpyAsync(s, d->d_stats, sizeof(s), hipMemcpyDeviceToHost, h->stream);
+    hipError_t e = hipMemcpyAsync(sl, d->d_stats, sizeof(sl), hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(err, d->d_nresp, sizeof(err), hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return hip_check(h, e, "gsim_msg_stats");
-    for (int k = 0; k < 4; ++k) out4[k] = (int64_t)s[k];
+    for (int k = 0; k < 4; ++k) {
+        unsigned long long v = 0;
+        for (int l = 0; l < kStatLanes; ++l) v += sl[l * kStatStride + k];
+        out4[k] = (int64_t)v;
+    }
     if (err[1]) { h->err = "IWANT responses overflowed their queue (raise gsim_msg_config.max_arrivals)"; return GSIM_ERANGE; }
     if (int rc = vq_check(h)) return rc;
     if (err[2]) {

@@ -36,6 +36,10 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a_)
 {
     const ScoreArgs& a0 = a_;
     if (a0.gate && *a0.gate == 0) return;
+    // every invalidMessageDeliveries counter is zero while the flag is clear:
+    // those planes are not read (C3: 4 GB per pass), a zero is what they hold
+    const bool inv_on = !a0.inv_live || *a0.inv_live != 0;
+    bool inv_left = false;           // a record still holds a non-zero counter after this pass
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a0.E; e += stride) {
         const ScoreArgs& a = kernarg0(a_);   // (re-read per record: SGPR pressure)
@@ -79,7 +83,7 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a_)
             const ctp_t tp = const_tp(a.tp) + t;
             if (!tp->scored || !((joined >> t) & 1ull)) continue;
             const int64_t i = slot_idx(mj, t, a.E, e);
-            double first = a.first[i], meshd = a.meshd[i], fail = a.fail[i], inval = a.invalid[i];
+            double first = a.first[i], meshd = a.meshd[i], fail = a.fail[i], inval = inv_on ? a.invalid[i] : 0.0;
             uint8_t fl = a.tflags[i];
             int64_t mt = 0;
             const uint8_t pc = a.mcnt[i];
@@ -116,6 +120,7 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a_)
                 const int64_t g = conn && a.mt_lazy ? a.graft[i] : INT64_MAX;
                 mt = g <= a.mt_R ? a.mt_R - g : a.mtime[i];
             }
+            if (REFRESH && inval != 0.0) inv_left = true;
             if (SCORE) {
                 double ts = 0.0;
                 if (fl & GSIM_TF_IN_MESH) {                               // P1
@@ -163,6 +168,7 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a_)
             a.score[e] = score;
         }
     }
+    if (REFRESH && a0.inv_next && __ballot(inv_left) && (threadIdx.x & 63) == 0) *a0.inv_next = 1u;
 }
 
 // ---------------------------------------------------------------------------
@@ -688,6 +694,13 @@ void free_graph(gsim_handle* h)
     h->n = h->e = 0;
 }
 
+// any counter may be non-zero (state written through the ABI, a fill, new
+// parameters): the next refresh reads the invalid planes and settles the flag
+static hipError_t inv_mark_all(gsim_handle* h)
+{
+    return hipMemsetAsync(h->d_inv_live, 1, 2 * sizeof(uint32_t), h->stream);
+}
+
 static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
 {
     ScoreArgs a{};
@@ -726,6 +739,8 @@ static ScoreArgs make_score_args(gsim_handle* h, int64_t now)
     a.e_hi = h->sh ? h->sh->own_e_hi : h->e;
     a.geid_base = h->sh ? h->sh->geid_base : 0;
     a.E_glob = h->sh ? h->sh->E_global : h->e;
+    a.inv_live = h->d_inv_live + (h->inv_par & 1);
+    a.inv_next = h->d_inv_live + ((h->inv_par + 1) & 1);
     return a;
 }
 
@@ -836,18 +851,24 @@ int launch_refresh_scores(gsim_handle* h, int64_t now)
         // no host round trip): the same results as refresh, P6 and score in
         // three unconditional passes.
         hipError_t e = hipMemsetAsync(h->d_flags + 1, 0, sizeof(int32_t), h->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(a.inv_next, 0, sizeof(uint32_t), h->stream);
         if (e != hipSuccess) return hip_check(h, e, "purge flag");
         a.purged = h->d_flags + 1;
         launch_score_kernel<true, true>(h, a);
+        h->inv_par ^= 1;
         int rc = launch_ip_colocation(h, h->d_flags + 1);
         if (rc) return rc;
         ScoreArgs b = a;
+        b.inv_live = a.inv_next;     // the flag of the decayed state
         b.gate = h->d_flags + 1;
         b.mt_lazy = 1;       // meshTime as the pass above left it
         b.mt_R = now;
         launch_score_kernel<false, true>(h, b);
     } else {
+        hipError_t e = hipMemsetAsync(a.inv_next, 0, sizeof(uint32_t), h->stream);
+        if (e != hipSuccess) return hip_check(h, e, "invalid-plane flag");
         launch_score_kernel<true, true>(h, a);
+        h->inv_par ^= 1;
     }
     h->mt_lazy = true;
     h->mt_R = now;
@@ -1165,6 +1186,8 @@ static int create_impl(const gsim_peer_score_params* params, const gsim_topic_sc
     if (n_topics > 0)
         (void)hipMemcpy(h->d_tp, topics, sizeof(gsim_topic_score_params) * (size_t)n_topics, hipMemcpyHostToDevice);
     (void)hipMemset(h->d_flags, 0, 16 * sizeof(int32_t));
+    h->d_inv_live = reinterpret_cast<uint32_t*>(h->d_flags + 8);
+    (void)hipMemset(h->d_inv_live, 1, 2 * sizeof(uint32_t));
     *out = h;
     return GSIM_OK;
 }
@@ -1471,6 +1494,7 @@ int gsim_set_topic_params(gsim_handle* h, int32_t t, const gsim_topic_score_para
     const gsim_topic_score_params old = h->tp[t];
     h->tp[t] = *p;
     hipError_t e = hipMemcpyAsync(h->d_tp + t, p, sizeof(*p), hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = inv_mark_all(h);   // a topic now scored: its records are read again
     if (e != hipSuccess) return hip_check(h, e, "gsim_set_topic_params");
     if (old.scored && h->e > 0) {
         const int df = p->first_message_deliveries_cap < old.first_message_deliveries_cap;
@@ -1516,6 +1540,7 @@ int gsim_fill_synthetic(gsim_handle* h, uint64_t seed, int64_t now, double p_mes
     if (rcf) return rcf;
     ScoreArgs a = make_score_args(h, now);
     hipLaunchKernelGGL(k_fill_synthetic, dim3(grid_for(h->e)), dim3(256), 0, h->stream, a, seed, p_mesh);
+    (void)inv_mark_all(h);
     h->mt_lazy = false;          // the fill stores meshTime
     h->p6_dirty = true; h->p6_rows_only = false;
     h->score_version++;
@@ -1636,6 +1661,7 @@ int gsim_write_field(gsim_handle* h, int32_t f, const void* src, size_t bytes)
     if (rc) return rc;
     rc = write_field_impl(h, f, r, src);
     h->unjoined_zero = false;    // arbitrary state: no record may be skipped
+    if (!rc) rc = hip_check(h, inv_mark_all(h), "gsim_write_field");
     if (!rc) rc = extra_field_written(h, f);
     if (f == GSIM_F_ESTATE) { h->p6_dirty = true; h->p6_rows_only = false; h->maybe_retained = true; h->score_version++;
     h->mesh_version++; }

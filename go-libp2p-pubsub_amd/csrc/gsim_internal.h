@@ -50,6 +50,11 @@ struct ScoreArgs {
     uint32_t olo, ohi;
     int64_t e_lo, e_hi, geid_base, E_glob;
     uint8_t* p6row;            // [N] a purge marks its observer's row for the next P6 pass
+    // invalidMessageDeliveries is zero in every record while *inv_live is 0
+    // (Handle::d_inv_live): the pass reads no invalid plane then, and a
+    // refresh sets *inv_next when a record still holds a non-zero value
+    const uint32_t* inv_live;
+    uint32_t* inv_next;
 };
 
 struct ColocArgs {
@@ -473,6 +478,13 @@ struct gsim_handle {
     // device: parameters and scratch flags
     gsim_topic_score_params* d_tp = nullptr;
     int32_t* d_flags = nullptr;
+    // [2] invalidMessageDeliveries flags: d_inv_live[inv_par] != 0 unless every
+    // record's counter is zero.  Written by the copies that raise a counter
+    // (deliver.hip inv_mark) and set by any state write through the ABI; a
+    // refresh reads it, writes the exact flag of the decayed state into the
+    // other word and flips inv_par (engine.hip launch_refresh_scores)
+    uint32_t* d_inv_live = nullptr;
+    int inv_par = 0;
 
     // device: graph
     uint32_t *d_row_ptr = nullptr, *d_col = nullptr, *d_rev = nullptr, *d_owner = nullptr;
