@@ -77,6 +77,21 @@ SCENARIOS = {
 }
 
 
+def _diag_phases(eng):
+    """k_send_tm's phase clocks in a -DGSIM_DIAG_PHASE build (gsim_diag_send_phases, not part of
+    gsim.h): resets them now and returns a reader of [all, scans + layouts, walks, waves]."""
+    import ctypes
+    fn = eng.lib.gsim_diag_send_phases
+    fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
+    out = (ctypes.c_uint64 * 4)()
+    fn(eng.h, out)
+
+    def read():
+        fn(eng.h, out)
+        return list(out)
+    return read
+
+
 def refresh_bytes(census: dict, n_edges: int) -> int:
     """Compulsory HBM bytes of one refreshScores+score pass on this state
     (DESIGN.md §4.1): every connected scored record reads its 4 counters and
@@ -474,6 +489,7 @@ def main():
     global CALLTIME
     if args.calltime:
         CALLTIME = {"_eng": eng}
+    diag = _diag_phases(eng) if os.environ.get("GSIM_DIAG_PHASE") else None   # diagnostic builds only
     t0 = time.perf_counter()
     for s in range(args.steps):
         kk += 1
@@ -481,6 +497,8 @@ def main():
     eng.synchronize()
     barrier()
     wall = time.perf_counter() - t0
+    if diag:
+        print(json.dumps({"send_phase_clocks_per_tick": [v / args.steps for v in diag()]}), file=sys.stderr)
     if CALLTIME is not None:
         print(json.dumps({"calltime_ms_per_tick": {c: v / args.steps for c, v in CALLTIME.items() if c != "_eng"}}),
               file=sys.stderr)

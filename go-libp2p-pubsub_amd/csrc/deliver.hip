@@ -821,16 +821,20 @@ constexpr int kTsSlots = 64;
 #else
 #define TM_LDC(x) (x)
 #endif
+// a shard's push walk: 512-thread blocks fitted to 4 waves per SIMD (two blocks
+// per CU), serial K = 8 C3 mean shard 11.66 / 11.67 -> 11.49 / 11.52 ms against
+// 1024 threads at 4 waves (512 at 6 waves: 11.73 / 11.75; round 3: 512 at one
+// wave 21 against 18.5 ms), gpurun_out/r05h_ab
 #ifndef GSIM_TM_PUSH_TB
-#define GSIM_TM_PUSH_TB 1024
+#define GSIM_TM_PUSH_TB 512
 #endif
 #ifndef GSIM_TM_MINB_PUSH
-#define GSIM_TM_MINB_PUSH GSIM_TM_MINB
+#define GSIM_TM_MINB_PUSH 4
 #endif
-constexpr int kPushTB = GSIM_TM_PUSH_TB;  // ... of a shard's push walk (512 at 1 wave: 21 against 18.5 ms per shard at K = 8)
+constexpr int kPushTB = GSIM_TM_PUSH_TB;
 // ... with member-compacted cells (sparse frontiers: many topics, each block's
 // chunks hold few forwarders): c5 send 184 / 151 / 158 ms per tick at 1024 / 512 /
-// 256 threads (gpurun_out/r04n); dense C3 is fastest at 1024 (§4.2)
+// 256 threads (gpurun_out/r04n); dense C3: GSIM_TM_TB (§4.2)
 constexpr int kSparseTB = 512;
 constexpr uint32_t kTmWin = 8192;   // flattened edges whose senders are tabled in LDS at once
 constexpr int kTmTabMin = 256;      // forwarders in a chunk from which the table pays for its fill
@@ -854,6 +858,18 @@ __device__ __forceinline__ void xbits_or_wave(uint64_t* xbits, uint64_t k, uint6
     if (k != ~0ull && (lane == 63 || kn != k))
         atomicOr(reinterpret_cast<unsigned long long*>(xbits + k), (unsigned long long)v);
 }
+
+// Diagnostic build (-DGSIM_DIAG_PHASE, timing only): shader clocks per wave in
+// k_send_tm's phases -- [0] all, [1] chunk scans and layer layouts, [2] edge
+// walks, [3] waves -- summed over a launch (gsim_diag_send_phases)
+#ifdef GSIM_DIAG_PHASE
+__device__ unsigned long long g_tm_diag[4];
+#define TM_CLK(v) const unsigned long long v = (unsigned long long)clock64()
+#define TM_ACC(d, a, b) d += (b) - (a)
+#else
+#define TM_CLK(v)
+#define TM_ACC(d, a, b)
+#endif
 
 // SP: topic slots or member-compacted cells are in use (gsim_internal.h); the
 // dense instance indexes plane t and cell m * N + p with no table reads.
@@ -892,6 +908,10 @@ void k_send_tm(RoundArgs a_)
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     if (tid == 0) { s_stats[0] = s_stats[1] = s_stats[2] = s_stats[3] = 0; }
     unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
+#ifdef GSIM_DIAG_PHASE
+    TM_CLK(c_start);
+    unsigned long long d_scan = 0, d_walk = 0;
+#endif
     // one (topic, peer range) item per block
     const uint32_t lb = blockIdx.x;
     int32_t t = 0;
@@ -942,6 +962,7 @@ void k_send_tm(RoundArgs a_)
         uint64_t clm = 0;
         __syncthreads();
         for (int64_t c0 = lo; c0 < hi; c0 += kTmChunk) {
+            TM_CLK(c_chunk);
             // the pass's slots with fresh bits in the chunk: every wave
             // computes the same ballot from the summary words
             const int64_t cw0 = c0 >> 6;
@@ -979,8 +1000,13 @@ void k_send_tm(RoundArgs a_)
                 }
             }
             bool first_layer = true;
+#ifdef GSIM_DIAG_PHASE
+            TM_CLK(c_l0);
+            TM_ACC(d_scan, c_chunk, c_l0);
+#endif
             for (;;) {
                 const RoundArgs& a = kernarg0(a_);   // (re-read per layer: SGPR pressure)
+                TM_CLK(c_layer);
                 const uint32_t fb = (pm[0] ? 1u : 0u) | (pm[1] ? 2u : 0u);
                 uint32_t len2[2] = {0, 0}, beg2[2] = {0, 0}, from2[2] = {0, 0}, k2[2] = {0, 0}, pl2[2] = {0, 0};
                 uint64_t msk2[2] = {0, 0};
@@ -1063,6 +1089,10 @@ void k_send_tm(RoundArgs a_)
                 __syncthreads();
                 const int nf = s_nf;
                 const uint32_t ne = s_ne;
+#ifdef GSIM_DIAG_PHASE
+                TM_CLK(c_walk);
+                TM_ACC(d_scan, c_layer, c_walk);
+#endif
                 if (nf > 0) {
                     constexpr int P = GSIM_TM_P;
                     constexpr uint32_t kPerIt = kTmThreads * P;
@@ -1327,6 +1357,12 @@ void k_send_tm(RoundArgs a_)
                     if (tab) __syncthreads();                    // s_own is rewritten by the next window
                   }
                 }
+#ifdef GSIM_DIAG_PHASE
+                {
+                    TM_CLK(c_wend);
+                    TM_ACC(d_walk, c_walk, c_wend);
+                }
+#endif
                 // the next layer: each peer's next slot
                 first_layer = false;
 #pragma unroll
@@ -1356,6 +1392,15 @@ void k_send_tm(RoundArgs a_)
     if (tid == 0 && (s_stats[0] | s_stats[3])) {
         stats_add(a, s_stats[0], s_stats[1], s_stats[3]);
     }
+#ifdef GSIM_DIAG_PHASE
+    TM_CLK(c_end);
+    if (lane == 0) {
+        atomicAdd(&g_tm_diag[0], c_end - c_start);
+        atomicAdd(&g_tm_diag[1], d_scan);
+        atomicAdd(&g_tm_diag[2], d_walk);
+        atomicAdd(&g_tm_diag[3], 1ull);
+    }
+#endif
 }
 
 // Commit every claim of round g (markSeen + P2 credit) before the state is
@@ -3482,8 +3527,10 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
     // every local peer sends (pull: a shard's ghosts too), or the owned range (push)
     const int64_t cn = a0.shi - a0.slo;
     const int T = std::max(1, h->t);
-    // (push: a shard's owned range alone, ranges down to one chunk)
-    const int64_t min_range = a0.push ? chunk : 4096;
+    // ranges down to one chunk: a small network (c2: 10k peers, one topic) still
+    // spreads its frontier over several CUs (4096-peer ranges gave it 3 blocks:
+    // 122 us of send per round); large ones are capped by the budget below
+    const int64_t min_range = chunk;
     const int64_t ranges = std::max<int64_t>(1, std::min<int64_t>((cn + min_range - 1) / min_range,
                                                                     std::max<int64_t>(h->t >= 32 ? 256 : 1,
                                                                                       total / T)));
@@ -3757,8 +3804,11 @@ __global__ __launch_bounds__(256) void k_xbits_gather(const uint32_t* nnew, int3
 // in LDS), so neighbouring lanes touch neighbouring records.
 constexpr int kXbList = 1024;                // per-wave LDS list of a task's copies
 
+// waves per SIMD the bit apply is fitted to: 6 (80 VGPRs, no spill) against 5
+// (94): mean shard 11.66 / 11.67 -> 11.56 / 11.61 ms (gpurun_out/r05h_ab); two
+// copies per lane in flight (kXbP) against four: 11.82 / 11.76
 #ifndef GSIM_XB_WPE
-#define GSIM_XB_WPE 1
+#define GSIM_XB_WPE 6
 #endif
 
 // listed_copy for kXbP copies of slot m per lane at once (records rr[], ~0u:
@@ -3766,7 +3816,10 @@ constexpr int kXbList = 1024;                // per-wave LDS list of a task's co
 // slots, gater, trace, Leave or validation latency (xbits_fast) -- with the
 // same rules and results; each stage's loads for all the copies are issued
 // before any is used, so the copies' dependent trips overlap.
-constexpr int kXbP = 2;
+#ifndef GSIM_XB_P
+#define GSIM_XB_P 2
+#endif
+constexpr int kXbP = GSIM_XB_P;
 __device__ __forceinline__ void listed_copies_fast(const RoundArgs& a, const uint32_t* rr, uint32_t m, int32_t t,
                                                    const uint32_t* owner, uint32_t claim_hi, uint32_t par, ctp_t tp,
                                                    unsigned long long& n_acc, unsigned long long& n_gray,
@@ -4869,3 +4922,20 @@ int gsim_set_peer_behaviour(gsim_handle* h, const uint8_t* flags)
 }
 
 }  // extern "C"
+
+// Diagnostic build only (GSIM_DIAG_PHASE): k_send_tm's phase clocks since the
+// last call (all zero in a normal build), then reset.
+extern "C" int gsim_diag_send_phases(gsim_handle* h, uint64_t* out4)
+{
+    if (!h || !out4) return GSIM_EINVAL;
+    for (int k = 0; k < 4; ++k) out4[k] = 0;
+#ifdef GSIM_DIAG_PHASE
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return GSIM_EDEVICE;
+    unsigned long long v[4] = {0, 0, 0, 0};
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_tm_diag), sizeof(v)) != hipSuccess) return GSIM_EDEVICE;
+    for (int k = 0; k < 4; ++k) out4[k] = v[k];
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_tm_diag), z, sizeof(z)) != hipSuccess) return GSIM_EDEVICE;
+#endif
+    return GSIM_OK;
+}
