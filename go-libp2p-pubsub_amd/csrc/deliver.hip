@@ -1470,7 +1470,7 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
                 if constexpr (LAT) vq_push_wave(a, qpl, qv);
             }
         }
-        if constexpr (!SP) return;                        // dense: a launch covers every word
+        if constexpr (!SP && !SPLIT) return;              // dense: a launch covers every word
     }
 }
 
@@ -3427,7 +3427,10 @@ int deliver_flush(gsim_handle* h)
     else if (sparse_layout(h))
         hipLaunchKernelGGL((k_commit<false, true>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     else if (split)
-        hipLaunchKernelGGL((k_commit<false, false, false, true>), dim3(gp, GSIM_SPLIT_GROUPS), dim3(256),
+#ifndef GSIM_SPLIT_WPW
+#define GSIM_SPLIT_WPW 1      // words per wave of the split commit (grid-stride)
+#endif
+        hipLaunchKernelGGL((k_commit<false, false, false, true>), dim3(std::max(1, gp / GSIM_SPLIT_WPW), GSIM_SPLIT_GROUPS), dim3(256),
                            (size_t)d->cfg.ring * sizeof(uint16_t),
                            h->stream, a);
     else
@@ -3530,7 +3533,10 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
     // ranges down to one chunk: a small network (c2: 10k peers, one topic) still
     // spreads its frontier over several CUs (4096-peer ranges gave it 3 blocks:
     // 122 us of send per round); large ones are capped by the budget below
-    const int64_t min_range = chunk;
+#ifndef GSIM_PUSH_RANGE_CHUNKS
+#define GSIM_PUSH_RANGE_CHUNKS 1
+#endif
+    const int64_t min_range = a0.push ? chunk * GSIM_PUSH_RANGE_CHUNKS : chunk;
     const int64_t ranges = std::max<int64_t>(1, std::min<int64_t>((cn + min_range - 1) / min_range,
                                                                     std::max<int64_t>(h->t >= 32 ? 256 : 1,
                                                                                       total / T)));
@@ -4597,7 +4603,10 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
         // deliveries; more overflow into k_commit's word scan, which is the
         // cheaper commit for such a busy round (c5 with 4 N lists spread over
         // waves: commit 73 -> 141 ms per tick)
-        d->clist_cap = std::max<int64_t>(2 * (int64_t)N, 1 << 20) / kClSub;
+#ifndef GSIM_CLIST_MULT
+#define GSIM_CLIST_MULT 2
+#endif
+        d->clist_cap = std::max<int64_t>(GSIM_CLIST_MULT * (int64_t)N, 1 << 20) / kClSub;
         A((void**)&d->d_clist, (size_t)d->clist_cap * kClSub * 8);
         A((void**)&d->d_clist_n, (kClSub + 1) * kClStride * 4);
         if (e == hipSuccess) e = hipMemsetAsync(d->d_clist_n, 0, (kClSub + 1) * kClStride * 4, h->stream);
