@@ -4600,11 +4600,12 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     d->tm_cn = -1;
     if (cfg->topic_slots > 0) {
         // claim list for member-compacted cells (list_commit): a round's first
-        // deliveries; more overflow into k_commit's word scan, which is the
-        // cheaper commit for such a busy round (c5 with 4 N lists spread over
-        // waves: commit 73 -> 141 ms per tick)
+        // deliveries, 4 N entries; more overflow into k_commit's word scan (and
+        // the round's send into the fresh-bit scan).  c5 at 10M, ticks 2-5: 2 N
+        // overflowed in the busy rounds, 346.7 ms per tick (send 75.1, commit
+        // 63.7); 4 N 293.0 (50.7, 34.2); 8 N the same (gpurun_out/r05l)
 #ifndef GSIM_CLIST_MULT
-#define GSIM_CLIST_MULT 2
+#define GSIM_CLIST_MULT 4
 #endif
         d->clist_cap = std::max<int64_t>(GSIM_CLIST_MULT * (int64_t)N, 1 << 20) / kClSub;
         A((void**)&d->d_clist, (size_t)d->clist_cap * kClSub * 8);

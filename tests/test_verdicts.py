@@ -182,3 +182,49 @@ def test_mixed_verdicts_bit_exact(require_gpu, n, k, T):
     assert kinds == set(V.values()), "every verdict appears"
     msgs, _ = run_parity(net, params, th, gp, st, ticks, sched, ring=512)
     assert msgs.stats[1] > n
+
+
+@pytest.mark.gpu
+def test_invalid_planes_skipped_while_zero_bit_exact(require_gpu):
+    """The refresh reads no invalidMessageDeliveries plane while every counter
+    is zero (engine.hip k_refresh_score, Handle::d_inv_live).  Rejected
+    messages raise counters (ticks 1-2), a fast decay takes every one back to
+    zero (ticks 3-8, the flag clears), counters written through the ABI and
+    new rejections bring them back (ticks 9-11): every record bit-exact per
+    tick on both sides of each transition."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim.engine import random_regular
+    from tickrun import run_parity, subscribed_schedule
+    n, k, T = 1500, 16, 2
+    rng = np.random.default_rng(77)
+    params = beacon_params(T)
+    for tp in params.Topics.values():
+        tp.InvalidMessageDeliveriesDecay = 0.2          # 1.0 -> below DecayToZero (0.01) in 3 ticks
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2)
+    th = PeerScoreThresholds(GossipThreshold=-50, PublishThreshold=-100, GraylistThreshold=-300)
+    net = random_regular(n, k, seed=91, n_topics=T)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 8 / k)
+    st.invalid[...] = 0.0
+    sched = {}
+    for ticks, inv in (([1, 2], 0.3), (list(range(3, 11)), 0.0), ([11], 0.3)):
+        sched.update(subscribed_schedule(rng, ticks, net, T, 6.0, inv))
+    mid = 0
+    for g in sorted(sched):                              # ids unique across the three parts
+        sched[g] = [(mid + q,) + m[1:] for q, m in enumerate(sched[g])]
+        mid += len(sched[g])
+    seen_zero = []
+
+    def after_heartbeat(kk, eng, st_, msgs):
+        if kk == 8:
+            seen_zero.append(eng.census()["nz_invalid"])
+        if kk == 9:
+            recs = rng.choice(net.e, 40, replace=False)
+            st_.invalid[0, recs] = 2.5
+            st_.invalid[T - 1, recs[:10]] = 0.75
+            eng.write(_abi.F_INVALID, st_.invalid)
+
+    msgs, _ = run_parity(net, params, th, gp, st, list(range(1, 12)), sched, ring=512,
+                         after_heartbeat=after_heartbeat)
+    assert seen_zero == [0], "every invalid counter back at zero before the ABI write"
+    assert (st.invalid != 0).any(), "counters non-zero again at the end"
