@@ -529,6 +529,27 @@ __device__ __forceinline__ int active_slots(const uint32_t* nnew, int ring, uint
     return *s_n;
 }
 
+// The active slots of topics t with t % ngrp == grp (the split commit's share:
+// slots of different topics never credit the same record or lastput word).
+__device__ __forceinline__ int active_slots_topics(const uint32_t* nnew, int ring, const uint32_t* mtopic, int grp,
+                                                   int ngrp, uint16_t* s_act, int* s_n)
+{
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        int n = 0;
+        for (int m0 = 0; m0 < ring; m0 += 64) {
+            const int m = m0 + lane;
+            const bool act = m < ring && ((nnew[m >> 5] >> (m & 31)) & 1u) && (int)(mtopic[m] % (uint32_t)ngrp) == grp;
+            const uint64_t b = __ballot(act);
+            if (act) s_act[n + __popcll(b & ((1ull << lane) - 1))] = (uint16_t)m;
+            n += __popcll(b);
+        }
+        if (lane == 0) *s_n = n;
+    }
+    __syncthreads();
+    return *s_n;
+}
+
 // Commit one claimed cell of round gc (markSeen + the winner's P2/P3 credit,
 // markFirstMessageDelivery score.go:919-946; mcache.Put for lastput).
 template <bool ATOMIC = false, bool LAT = false, bool SP = true, bool GT = false>
@@ -809,18 +830,8 @@ constexpr int kTsSlots = 64;
 #ifndef GSIM_TM_MINB_SPARSE
 #define GSIM_TM_MINB_SPARSE 1
 #endif
-// GSIM_TM_NT (A/B builds): the forwarders' row fields and the receivers' cells
-// are loaded non-temporal, so the L2 keeps the slots' committed bitmaps
-#ifdef GSIM_TM_NT
-#define TM_LD(x) __builtin_nontemporal_load(&(x))
-#else
-#define TM_LD(x) (x)
-#endif
-#if defined(GSIM_TM_NT) && GSIM_TM_NT > 1
-#define TM_LDC(x) __builtin_nontemporal_load(&(x))
-#else
-#define TM_LDC(x) (x)
-#endif
+// (non-temporal loads of the row fields and cells, to keep the committed
+// bitmaps in L2, were measured slower in round 4 and removed)
 // a shard's push walk: 512-thread blocks fitted to 4 waves per SIMD (two blocks
 // per CU), serial K = 8 C3 mean shard 11.66 / 11.67 -> 11.49 / 11.52 ms against
 // 1024 threads at 4 waves (512 at 6 waves: 11.73 / 11.75; round 3: 512 at one
@@ -1145,12 +1156,6 @@ void k_send_tm(RoundArgs a_)
                             else if (a.sedge && vv[u]) ev[u] = a.sedge[bq + k];
                             else ev[u] = s_beg[q] + k;
                         }
-#ifdef GSIM_DIAG_NO_RX
-                        // diagnostic build (timing only, wrong results): the frontier walk
-                        // alone, no receiver-side access
-                        if (vv[0] && ev[0] == 0xFFFFFFFFu) n_acc++;
-                        continue;
-#endif
                         uint32_t xq[PUSH ? P : 1];   // PUSH: the copy's bit (a cross edge), ~0: an owned receiver
                         uint64_t xbk[PUSH ? P : 1];  // ... a remote copy's xbits word (~0: none) and bit
                         uint64_t xbv[PUSH ? P : 1];
@@ -1164,14 +1169,14 @@ void k_send_tm(RoundArgs a_)
                                 // a masked row's positions are its mesh (or direct) edges: the
                                 // router flags are read only for direct ones (below)
                                 const int64_t pe = pv[u] + e;
-                                iv[u] = TM_LD(a.col[e]); dsv[u] = TM_LD(a.dstate[e]);
-                                if (!mk[u]) mfv[u] = TM_LD(a.mflags[pe]);
+                                iv[u] = a.col[e]; dsv[u] = a.dstate[e];
+                                if (!mk[u]) mfv[u] = a.mflags[pe];
                                 if constexpr (PUSH) {
                                     xq[u] = a.xwq[e];
                                 } else {
-                                    tfv[u] = TM_LD(a.tflags[pe]);
-                                    if (verdict_penalises(vd)) xv[u] = TM_LD(a.invalid[pe]);
-                                    else if (vd == GSIM_VERDICT_ACCEPT) nv[u] = TM_LD(a.mcnt[pe]);
+                                    tfv[u] = a.tflags[pe];
+                                    if (verdict_penalises(vd)) xv[u] = a.invalid[pe];
+                                    else if (vd == GSIM_VERDICT_ACCEPT) nv[u] = a.mcnt[pe];
                                 }
                             }
                         }
@@ -1182,9 +1187,9 @@ void k_send_tm(RoundArgs a_)
                                 if (vv[u] && xq[u] == ~0u) {
                                     const uint8_t vd = s_vd[kv[u]];
                                     const int64_t pe = pv[u] + ev[u];
-                                    tfv[u] = TM_LD(a.tflags[pe]);
-                                    if (verdict_penalises(vd)) xv[u] = TM_LD(a.invalid[pe]);
-                                    else if (vd == GSIM_VERDICT_ACCEPT) nv[u] = TM_LD(a.mcnt[pe]);
+                                    tfv[u] = a.tflags[pe];
+                                    if (verdict_penalises(vd)) xv[u] = a.invalid[pe];
+                                    else if (vd == GSIM_VERDICT_ACCEPT) nv[u] = a.mcnt[pe];
                                 }
                             }
                         }
@@ -1249,14 +1254,7 @@ void k_send_tm(RoundArgs a_)
                             // credited; with a validation latency the credit is decided at
                             // completion (mesh and record then), so only an unscored topic
                             // or an ignored / throttled message skips it
-#ifdef GSIM_DIAG_NO_SEEN
-                            // diagnostic build (timing only, wrong results): every receiver is
-                            // an earlier-round duplicate, no seen-set access
-                            const bool sbit = true;
-                            (void)s_bm; (void)bw;
-#else
                             const bool sbit = (s_bm[bw] >> (i & 63)) & 1ull;   // committed before this round
-#endif
                             const bool known = sbit && (L ? (!scored_t || (inv && !pen))
                                                           : (s_wa[k] || !sc || inv || !(tf & GSIM_TF_IN_MESH)));
                             // the receiver's cell (a member of t: mesh, direct, fanout and flood
@@ -1277,7 +1275,7 @@ void k_send_tm(RoundArgs a_)
                             const uint64_t c = known ? 0ull
                                              : fold ? __hip_atomic_fetch_min(a.cs.cell + ci, cv, __ATOMIC_RELAXED,
                                                                              __HIP_MEMORY_SCOPE_AGENT)
-                                                    : TM_LDC(a.cs.cell[ci]);
+                                                    : a.cs.cell[ci];
                             const uint32_t chi = (uint32_t)(c >> 32);
                             // the round validation completed (or completes) in; -1: unclaimed
                             // or claimed in this round
@@ -1405,9 +1403,9 @@ void k_send_tm(RoundArgs a_)
 
 // Commit every claim of round g (markSeen + P2 credit) before the state is
 // read or changed by anything but the next round.
-// SPLIT (a shard's few words: a wave per word leaves the CUs idle): the slot
-// batches dealt over gridDim.y, a claim's record credit and lastput atomic
-// (two slots of one sender can credit the same record)
+// SPLIT (a shard's few words: a wave per word leaves the CUs idle): the slots
+// shared over gridDim.y groups by topic, so the record credits and lastput
+// stay plain stores (two slots of one topic can credit the same record)
 template <bool LAT, bool SP, bool GT = false, bool SPLIT = false>
 __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
 {
@@ -1416,7 +1414,13 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
     if (a.clist && !a.clist_n[kClSub * kClStride]) return;   // the claim list covers the round (k_commit_list)
     // this scan sets the fresh bits: round g+1's forwarder list is incomplete
     if (a.flist && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.fst[kFstBad + (int)((a.g + 1) & 1)] = 1;
-    const int nact = active_slots(a.nnew_cur, a.ring, s_act, &s_n);
+    // SPLIT: group y takes the slots of topics t = y mod gridDim.y, whose
+    // credits no other group can touch -- plain stores (serial K = 8 C3 mean
+    // shard 11.53 / 11.55 against 11.61 / 11.63 ms with the slot batches dealt
+    // over the groups and atomic credits, gpurun_out/r05p_ab)
+    const int nact = SPLIT ? active_slots_topics(a.nnew_cur, a.ring, a.mtopic, (int)blockIdx.y, (int)gridDim.y,
+                                                       s_act, &s_n)
+                                 : active_slots(a.nnew_cur, a.ring, s_act, &s_n);
     const int lane = threadIdx.x & 63;
     // claims exist only at receivers' cells: the words of [rlo, rhi), a wave per
     // word, grid-stride (a launch that exits early stays cheap: c5's 39k blocks
@@ -1427,10 +1431,10 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
         const int64_t i = i0 + lane;
         const bool vi = i < a.CN;
         const uint32_t par = (uint32_t)(a.g & 1);
-        // (SPLIT: batches of kSplitBatch slots dealt over gridDim.y -- parallel
-        // waves instead of cells in flight per wave)
+        // (SPLIT: the group's slots in batches of kSplitBatch -- parallel waves
+        // over the groups instead of cells in flight per wave)
         constexpr int kB = SPLIT ? kSplitBatch : kSlotBatch;
-        for (int k0 = SPLIT ? (int)blockIdx.y * kB : 0; k0 < nact; k0 += (SPLIT ? (int)gridDim.y : 1) * kB) {
+        for (int k0 = 0; k0 < nact; k0 += kB) {
             uint64_t cv[kB];
             int64_t ci[SP ? kB : 1];           // the dense layout recomputes m * N + i
 #pragma unroll
@@ -1465,7 +1469,7 @@ __global__ __launch_bounds__(256) void k_commit(RoundArgs a)
                 if (is_claim_of(cv[b], par)) {
                     const uint32_t m = s_act[k];
                     uint64_t* cp = a.cs.cell + (SP ? ci[b] : (int64_t)m * a.cs.n + i);
-                    commit_claim<SPLIT, LAT, SP, GT>(a, cp, cv[b], a.g, m, i, &qpl, &qv);
+                    commit_claim<false, LAT, SP, GT>(a, cp, cv[b], a.g, m, i, &qpl, &qv);
                 }
                 if constexpr (LAT) vq_push_wave(a, qpl, qv);
             }
@@ -1504,7 +1508,8 @@ __global__ __launch_bounds__(256) void k_commit_list(RoundArgs a)
                 atomicOr(reinterpret_cast<unsigned long long*>(a.seenbm + (int64_t)m * a.nw + w), bit);
                 if (a.fresh && a.minv[m] == GSIM_VERDICT_ACCEPT) {
                     if (a.flist_commit) { fw = true; fv = (uint64_t)i | ((uint64_t)m << 32); }   // round g+1's list
-                    else fresh_set(a, m, w, bit);
+                    // (a shard's holder accumulation reads the fresh bits before the send)
+                    if (!a.flist_commit || a.sharded) fresh_set(a, m, w, bit);
                 }
                 if (a.gt.act) commit_claim<true, false, SP, true>(a, cp, c, a.g, m, i);
                 else commit_claim<true, false, SP>(a, cp, c, a.g, m, i);
@@ -2582,7 +2587,9 @@ __global__ __launch_bounds__(kLsB) void k_send_list(RoundArgs a_)
             m = (uint32_t)(v >> 32) & 0x7FFFFFFFu;
             const int32_t t = (int32_t)a.mtopic[m];
             const uint32_t origin = a.morigin[m];
-            if (v & kFlOrigin)        // the origin's fresh bit (k_publish) is taken here
+            // the origin's fresh bit (k_publish) is taken here; on shards every
+            // entry's (the commit also set them, for the holder accumulation)
+            if ((v & kFlOrigin) || a.sharded)
                 atomicAnd(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (x >> 6)), ~(1ull << (x & 63)));
             const int64_t xc = a.cs.at((int64_t)a.cs.cbase[m], t, x);
             from = xc >= 0 ? (uint32_t)a.cs.cell[xc] & kPeerMask : kPeerMask;
@@ -2623,10 +2630,11 @@ __global__ __launch_bounds__(kLsB) void k_send_list(RoundArgs a_)
         __syncthreads();
         for (uint32_t f0 = 0; f0 < total; f0 += kLsB * kLsP) {
             const RoundArgs& a = kernarg0(a_);   // (re-read per iteration: SGPR pressure)
-            uint32_t jv[kLsP], ev[kLsP], iv[kLsP], qv[kLsP];
+            uint32_t jv[kLsP], ev[kLsP], iv[kLsP], qv[kLsP], xq[kLsP];
             int64_t pv[kLsP];
             uint8_t mfv[kLsP], dsv[kLsP], tfv[kLsP];
-            bool vv[kLsP], mk[kLsP];
+            bool vv[kLsP], mk[kLsP], rem[kLsP];
+            uint64_t xbk[kLsP], xbv[kLsP];     // push: a remote copy's xbits word (~0: none) and bit
 #pragma unroll
             for (int u = 0; u < kLsP; ++u) {
                 const uint32_t fi = f0 + (uint32_t)(u * kLsB + tid);
@@ -2651,13 +2659,18 @@ __global__ __launch_bounds__(kLsB) void k_send_list(RoundArgs a_)
             }
 #pragma unroll
             for (int u = 0; u < kLsP; ++u) {
-                iv[u] = 0; mfv[u] = 0; dsv[u] = 0; tfv[u] = 0;
+                iv[u] = 0; mfv[u] = 0; dsv[u] = 0; tfv[u] = 0; xq[u] = 0; rem[u] = false;
+                xbk[u] = ~0ull; xbv[u] = 0;
                 if (vv[u]) {
                     const uint32_t e = ev[u];
                     const int64_t pe = pv[u] + e;
                     iv[u] = a.col[e]; dsv[u] = a.dstate[e];
                     if (!mk[u]) mfv[u] = a.mflags[pe];
-                    tfv[u] = a.tflags[pe];
+                    // a shard's push: a ghost receiver's records
+                    // live on its own shard; the copy is a bit of its cross edge
+                    rem[u] = a.push && (iv[u] < a.rlo || iv[u] >= a.rhi);
+                    if (rem[u]) xq[u] = a.xwq[e];
+                    else tfv[u] = a.tflags[pe];
                 }
             }
             uint32_t clw = 0;
@@ -2683,6 +2696,11 @@ __global__ __launch_bounds__(kLsB) void k_send_list(RoundArgs a_)
                 if (a.flood && j == origin) sel = ((a.sub[i] >> t) & 1ull) && a.score[a.rev[e]] >= a.pub_thr;
                 if ((ds & GSIM_DS_DIRECT) && !sel) sel = (a.sub[i] >> t) & 1ull;
                 const bool tg = sel && (ds & GSIM_DS_CONNECTED) && i != s_from[q] && i != origin;
+                if (tg && rem[u]) {                  // the receiver's shard delivers it (k_xbits_deliver)
+                    xbk[u] = (uint64_t)((int64_t)m * a.xbw + (xq[u] >> 6));
+                    xbv[u] = 1ull << (xq[u] & 63u);
+                    continue;
+                }
                 const bool ok = tg && (ds & GSIM_DS_ACCEPT);
                 n_gray += tg && !ok;
                 if (!ok) continue;
@@ -2735,6 +2753,10 @@ __global__ __launch_bounds__(kLsB) void k_send_list(RoundArgs a_)
                     if (in_window)
                         atomic_mcnt_inc(a.mcnt, ir, &a.meshd[ir], tp->mesh_message_deliveries_cap, a.mcnt_fast);
                 }
+            }
+            if (a.push) {
+#pragma unroll
+                for (int u = 0; u < kLsP; ++u) xbits_or_wave(a.xbits, xbk[u], xbv[u]);
             }
             if (a.clist) {
 #pragma unroll
@@ -3061,10 +3083,10 @@ static bool list_commit(const gsim_handle* h)
 
 // The list-driven send (k_send_list) runs for this configuration: claim-list
 // commits, and nothing k_send_list leaves to k_send_tm (the peer gater, the
-// trace, shards, validation latency)
+// trace, the shards' pull exchange, validation latency)
 static bool flist_allowed(const gsim_handle* h)
 {
-    return list_commit(h) && h->dl->d_flist && !h->gt && !h->trace.ev && !h->sh && !h->flist_off;
+    return list_commit(h) && h->dl->d_flist && !h->gt && !h->trace.ev && (!h->sh || h->sh->push) && !h->flist_off;
 }
 
 static Cells deliver_cells(const Deliver* d)
@@ -3427,10 +3449,8 @@ int deliver_flush(gsim_handle* h)
     else if (sparse_layout(h))
         hipLaunchKernelGGL((k_commit<false, true>), grid, dim3(256), (size_t)d->cfg.ring * sizeof(uint16_t), h->stream, a);
     else if (split)
-#ifndef GSIM_SPLIT_WPW
-#define GSIM_SPLIT_WPW 1      // words per wave of the split commit (grid-stride)
-#endif
-        hipLaunchKernelGGL((k_commit<false, false, false, true>), dim3(std::max(1, gp / GSIM_SPLIT_WPW), GSIM_SPLIT_GROUPS), dim3(256),
+        // (a wave per word: 4 words per wave were slower, profiles/r05_shards8_ab_ranges_split.txt)
+        hipLaunchKernelGGL((k_commit<false, false, false, true>), dim3(gp, GSIM_SPLIT_GROUPS), dim3(256),
                            (size_t)d->cfg.ring * sizeof(uint16_t),
                            h->stream, a);
     else
@@ -3533,10 +3553,9 @@ static int launch_send_tm(gsim_handle* h, const RoundArgs& a0)
     // ranges down to one chunk: a small network (c2: 10k peers, one topic) still
     // spreads its frontier over several CUs (4096-peer ranges gave it 3 blocks:
     // 122 us of send per round); large ones are capped by the budget below
-#ifndef GSIM_PUSH_RANGE_CHUNKS
-#define GSIM_PUSH_RANGE_CHUNKS 1
-#endif
-    const int64_t min_range = a0.push ? chunk * GSIM_PUSH_RANGE_CHUNKS : chunk;
+    // (a shard's push walk too: ranges of 2 / 4 chunks were slower,
+    // profiles/r05_shards8_ab_ranges_split.txt)
+    const int64_t min_range = chunk;
     const int64_t ranges = std::max<int64_t>(1, std::min<int64_t>((cn + min_range - 1) / min_range,
                                                                     std::max<int64_t>(h->t >= 32 ? 256 : 1,
                                                                                       total / T)));

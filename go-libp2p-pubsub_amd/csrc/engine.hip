@@ -822,11 +822,12 @@ template <bool REFRESH, bool SCORE>
 static void launch_score_kernel(gsim_handle* h, const ScoreArgs& a)
 {
     ProfScope ps(h, REFRESH ? GSIM_K_REFRESH_SCORE : GSIM_K_SCORE);
-// blocks of the fused refresh (grid-stride over the records): 65536 (about one
-// record per thread at C3) 8.04 ms against 8.26 at 16384 and 8.48 at 4096
-// (gpurun_out/r04pab)
+// blocks of the fused refresh (grid-stride over the records): up to 131072, one
+// record per thread at C3 (125000 blocks): 6.99 / 7.04 ms against 7.16 / 7.15 at
+// 65536 and 7.25 / 7.24 at 32768 (gpurun_out/r05p_c3); round 4: 65536 8.04 ms
+// against 8.26 at 16384 and 8.48 at 4096 (gpurun_out/r04pab)
 #ifndef GSIM_REFRESH_GRID
-#define GSIM_REFRESH_GRID 65536
+#define GSIM_REFRESH_GRID 131072
 #endif
     hipLaunchKernelGGL((k_refresh_score<REFRESH, SCORE>), dim3(grid_for(h->e, 256, GSIM_REFRESH_GRID)), dim3(256), 0,
                        h->stream, a);

@@ -74,17 +74,9 @@ GSIM_HD uint64_t pair_key(uint64_t seed, uint32_t tick, uint32_t observer, uint3
 GSIM_HD uint64_t select_key(uint64_t seed, uint32_t tick, uint32_t observer, uint32_t topic,
                             uint32_t purpose, uint32_t item, uint32_t pos)
 {
-#ifdef GSIM_DIAG_CHEAP_KEY
-    // diagnostic build (timing only, wrong results): a multiply-xor hash for the
-    // selection keys, to price the Philox rounds
-    uint32_t h = tick * 0x9E3779B9u ^ observer * 0x85EBCA6Bu ^ ((topic << 8) | purpose) * 0xC2B2AE35u ^ item ^ (uint32_t)seed;
-    h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15;
-    return ((uint64_t)h << 32) | pos;
-#else
     u32x4 r = philox4x32_10(tick, observer, (topic << 8) | purpose, item, (uint32_t)seed,
                             (uint32_t)(seed >> 32));
     return ((uint64_t)r.x << 32) | pos;
-#endif
 }
 
 // PX keys (makePrune's getPeers, gossipsub.go:1879-1882): one Philox draw per
