@@ -4474,12 +4474,12 @@ static hipError_t install_layout(gsim_handle* h, Deliver* d, const CellLayout& L
     d->d_cbase = nullptr; d->d_mbits = nullptr; d->d_mpre = nullptr;
     d->d_mlist = nullptr; d->d_mloff = nullptr; d->d_mcount = nullptr; d->d_mmtab = nullptr; d->d_mctab = nullptr;
     e = hipMalloc((void**)&d->d_cbase, std::max<size_t>(L.cbase.size() * 8, 8));
-    if (e == hipSuccess) e = hipMemcpy(d->d_cbase, L.cbase.data(), L.cbase.size() * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = stream_copy(h, d->d_cbase, L.cbase.data(), L.cbase.size() * 8, hipMemcpyHostToDevice);
     if (e == hipSuccess && L.sparse) {
         e = hipMalloc((void**)&d->d_mbits, L.mbits.size() * 8);
         if (e == hipSuccess) e = hipMalloc((void**)&d->d_mpre, L.mpre.size() * 4);
-        if (e == hipSuccess) e = hipMemcpy(d->d_mbits, L.mbits.data(), L.mbits.size() * 8, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(d->d_mpre, L.mpre.data(), L.mpre.size() * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = stream_copy(h, d->d_mbits, L.mbits.data(), L.mbits.size() * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = stream_copy(h, d->d_mpre, L.mpre.data(), L.mpre.size() * 4, hipMemcpyHostToDevice);
     }
     if (e == hipSuccess && !L.mloff.empty()) {
         const size_t T = L.mloff.size();
@@ -4495,11 +4495,11 @@ static hipError_t install_layout(gsim_handle* h, Deliver* d, const CellLayout& L
         if (e == hipSuccess) e = hipMalloc((void**)&d->d_mmtab, (T + 1) * 4);
         if (e == hipSuccess) e = hipMalloc((void**)&d->d_mctab, (T + 1) * 4);
         if (e == hipSuccess && !L.mlist.empty())
-            e = hipMemcpy(d->d_mlist, L.mlist.data(), L.mlist.size() * 4, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(d->d_mloff, L.mloff.data(), T * 8, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(d->d_mcount, L.mcount.data(), T * 8, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(d->d_mmtab, d->mmtab.data(), (T + 1) * 4, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(d->d_mctab, d->mctab.data(), (T + 1) * 4, hipMemcpyHostToDevice);
+            e = stream_copy(h, d->d_mlist, L.mlist.data(), L.mlist.size() * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = stream_copy(h, d->d_mloff, L.mloff.data(), T * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = stream_copy(h, d->d_mcount, L.mcount.data(), T * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = stream_copy(h, d->d_mmtab, d->mmtab.data(), (T + 1) * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = stream_copy(h, d->d_mctab, d->mctab.data(), (T + 1) * 4, hipMemcpyHostToDevice);
     }
     d->cbase = L.cbase;
     d->sparse = L.sparse;
@@ -4707,7 +4707,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
         std::vector<int64_t> roff((size_t)cfg->rounds);
         for (int32_t r = 0; r < cfg->rounds; ++r)
             roff[(size_t)r] = (int64_t)(r + 1) * cfg->heartbeat_ns / (cfg->rounds + 1);
-        e = hipMemcpy(d->d_roff, roff.data(), roff.size() * 8, hipMemcpyHostToDevice);
+        e = stream_copy(h, d->d_roff, roff.data(), roff.size() * 8, hipMemcpyHostToDevice);
     }
     if (e == hipSuccess) e = hipMemsetAsync(d->d_lastput, 0xFF, T * N * 4, h->stream);
     if (e == hipSuccess) {
@@ -4715,7 +4715,7 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
         std::vector<uint32_t> mt(ring, 0);
         if (cfg->topic_slots > 0)
             for (size_t m = 0; m < ring; ++m) mt[m] = (uint32_t)(m / (size_t)cfg->topic_slots);
-        e = hipMemcpy(d->d_mtopic, mt.data(), ring * 4, hipMemcpyHostToDevice);
+        e = stream_copy(h, d->d_mtopic, mt.data(), ring * 4, hipMemcpyHostToDevice);
     }
     if (e == hipSuccess) e = hipMemsetAsync(d->d_morigin, 0, ring * 4, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(d->d_minv, 0, ring, h->stream);

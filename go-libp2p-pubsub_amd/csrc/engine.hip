@@ -1184,11 +1184,11 @@ static int create_impl(const gsim_peer_score_params* params, const gsim_topic_sc
         gsim_destroy(h);
         return fail(GSIM_ENOMEM, m);
     }
-    if (n_topics > 0)
-        (void)hipMemcpy(h->d_tp, topics, sizeof(gsim_topic_score_params) * (size_t)n_topics, hipMemcpyHostToDevice);
-    (void)hipMemset(h->d_flags, 0, 16 * sizeof(int32_t));
+    (void)stream_fill(h, h->d_flags, 0, 16 * sizeof(int32_t));
     h->d_inv_live = reinterpret_cast<uint32_t*>(h->d_flags + 8);
-    (void)hipMemset(h->d_inv_live, 1, 2 * sizeof(uint32_t));
+    (void)stream_fill(h, h->d_inv_live, 1, 2 * sizeof(uint32_t));
+    if (n_topics > 0)
+        (void)stream_copy(h, h->d_tp, topics, sizeof(gsim_topic_score_params) * (size_t)n_topics, hipMemcpyHostToDevice);
     *out = h;
     return GSIM_OK;
 }

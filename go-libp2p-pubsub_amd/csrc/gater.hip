@@ -344,10 +344,10 @@ int gsim_set_peer_gater(gsim_handle* h, const gsim_peer_gater_params* p, const d
     A((void**)&g->tw, (size_t)T * 8); A((void**)&g->n_thr, 8);
     if (e == hipSuccess) e = hipMemcpyAsync(g->tw, tw.data(), (size_t)T * 8, hipMemcpyHostToDevice, h->stream);
     if (e != hipSuccess) { free_gater(h); return hip_check(h, e, "gsim_set_peer_gater"); }
-    {
-        std::vector<int64_t> never(N, kNever);
-        e = hipMemcpy(g->last, never.data(), N * 8, hipMemcpyHostToDevice);
-    }
+    // on the handle's stream, after the zero fill above (a blocking copy on the
+    // null stream could land first and be zeroed: lastThrottle 0, not never)
+    std::vector<int64_t> never(N, kNever);
+    e = hipMemcpyAsync(g->last, never.data(), N * 8, hipMemcpyHostToDevice, h->stream);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_gater_groups, dim3(grid_of(h->e)), dim3(256), 0, h->stream, (const uint32_t*)h->d_row_ptr,
                            (const uint32_t*)h->d_col, (const uint32_t*)h->d_owner, (const uint32_t*)h->d_ip_ptr,

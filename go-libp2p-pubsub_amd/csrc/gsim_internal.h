@@ -549,6 +549,18 @@ struct gsim_handle {
 };
 
 int hip_check(gsim_handle* h, hipError_t e, const char* what);
+// The handle's stream is non-blocking: nothing orders it with the null
+// stream's hipMemcpy / hipMemset.  Copies and fills go through the stream
+// (a copy waits for it: the host buffer may be released on return).
+inline hipError_t stream_copy(gsim_handle* h, void* dst, const void* src, size_t bytes, hipMemcpyKind kind)
+{
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, h->stream);
+    return e == hipSuccess ? hipStreamSynchronize(h->stream) : e;
+}
+inline hipError_t stream_fill(gsim_handle* h, void* dst, int value, size_t bytes)
+{
+    return hipMemsetAsync(dst, value, bytes, h->stream);
+}
 bool field_ref(gsim_handle* h, int32_t f, gsim::FieldRef* r);
 int trace_config_local(gsim_handle* h, uint32_t peer_lo, uint32_t peer_hi, uint32_t xlo, uint32_t xhi, int64_t cap);
 int launch_ip_colocation(gsim_handle* h, const int32_t* gate = nullptr);

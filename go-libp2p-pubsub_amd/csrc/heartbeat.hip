@@ -2385,8 +2385,12 @@ int alloc_extra(gsim_handle* h)
     e = hipMemsetAsync(h->x->d_lastpub, 0, lp_bytes, h->stream);
     if (e == hipSuccess) e = hipMemsetAsync(h->x->d_fantopics, 0, sizeof(uint64_t) * (size_t)h->n, h->stream);
     if (e != hipSuccess) return hip_check(h, e, "memset fanout");
+    // the graph's uploads were queued on the handle's (non-blocking) stream: they
+    // must land before the blocking reads below
+    e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_check(h, e, "graph upload");
     std::vector<uint32_t> rp((size_t)h->n + 1);
-    e = hipMemcpy(rp.data(), h->d_row_ptr, sizeof(uint32_t) * rp.size(), hipMemcpyDeviceToHost);
+    e = stream_copy(h, rp.data(), h->d_row_ptr, sizeof(uint32_t) * rp.size(), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_check(h, e, "row_ptr readback");
     uint32_t md = 0, mdall = 0;
     std::vector<uint32_t> cls[6];
@@ -2401,7 +2405,7 @@ int alloc_extra(gsim_handle* h)
         // their joined topics: observers with the same subscriptions side by side
         // (order within a heartbeat is free: observers are independent)
         std::vector<uint64_t> sub((size_t)h->n);
-        e = hipMemcpy(sub.data(), h->d_sub, sizeof(uint64_t) * sub.size(), hipMemcpyDeviceToHost);
+        e = stream_copy(h, sub.data(), h->d_sub, sizeof(uint64_t) * sub.size(), hipMemcpyDeviceToHost);
         if (e != hipSuccess) return hip_check(h, e, "subscription readback");
         for (int c = 0; c < 2; ++c)
             std::stable_sort(cls[c].begin(), cls[c].end(), [&](uint32_t x, uint32_t y) { return sub[x] < sub[y]; });
@@ -2428,7 +2432,7 @@ int alloc_extra(gsim_handle* h)
         for (auto& c : cls) all.insert(all.end(), c.begin(), c.end());
         e = hipMalloc((void**)&h->x->d_rows, sizeof(uint32_t) * all.size());
         if (e == hipSuccess)
-            e = hipMemcpy(h->x->d_rows, all.data(), sizeof(uint32_t) * all.size(), hipMemcpyHostToDevice);
+            e = stream_copy(h, h->x->d_rows, all.data(), sizeof(uint32_t) * all.size(), hipMemcpyHostToDevice);
         if (e != hipSuccess) return hip_check(h, e, "row classes");
         h->bytes_allocated += sizeof(uint32_t) * all.size();
     }
@@ -2721,8 +2725,8 @@ int gsim_read_snapshot(gsim_handle* h, int64_t obs_lo, int64_t obs_hi, gsim_peer
     if (!rc && h->p6_dirty) rc = launch_ip_colocation(h);
     if (rc) return rc;
     uint32_t rp[2];
-    hipError_t e = hipMemcpy(rp, h->d_row_ptr + obs_lo, sizeof(uint32_t), hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(rp + 1, h->d_row_ptr + obs_hi, sizeof(uint32_t), hipMemcpyDeviceToHost);
+    hipError_t e = stream_copy(h, rp, h->d_row_ptr + obs_lo, sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = stream_copy(h, rp + 1, h->d_row_ptr + obs_hi, sizeof(uint32_t), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_check(h, e, "row bounds");
     const int64_t ne = (int64_t)rp[1] - rp[0], T = std::max(1, h->t);
     if (ne == 0) return GSIM_OK;

@@ -1150,12 +1150,12 @@ int exchange_frontier(gsim_group* g, int64_t round, bool flush)
             const int64_t cap = need + need / 2;
             rc = g->take(h, dalloc(h, &s->d_fout, (size_t)cap));
             if (rc) return rc;
-            if (prev && hipMemcpy(s->d_fout, old, sizeof(uint64_t) * (size_t)prev, hipMemcpyDeviceToDevice) != hipSuccess)
+            if (prev && stream_copy(h, s->d_fout, old, sizeof(uint64_t) * (size_t)prev, hipMemcpyDeviceToDevice) != hipSuccess)
                 return g->fail(GSIM_EDEVICE, "frontier list grow");
             (void)hipFree(old);
             s->fcap = cap;
             const uint32_t pv = (uint32_t)prev;
-            if (hipMemcpy(s->d_fcnt, &pv, sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess)
+            if (stream_copy(h, s->d_fcnt, &pv, sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess)
                 return g->fail(GSIM_EDEVICE, "frontier count");
         }
         s->fpend = s->h_counts[0];
@@ -1523,15 +1523,15 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
             return g->take(h, rc);
         if (!s->h_counts && hipHostMalloc((void**)&s->h_counts, sizeof(uint32_t) * GSIM_MAX_SHARDS, 0) != hipSuccess)
             return g->fail(GSIM_ENOMEM, "pinned scratch");
-        hipError_t he = hipMemcpy(s->d_gid, L.gid.data(), L.gid.size() * 4, hipMemcpyHostToDevice);
-        if (he == hipSuccess) he = hipMemcpy(s->d_g2l, g2l.data(), g2l.size() * 4, hipMemcpyHostToDevice);
-        if (he == hipSuccess) he = hipMemcpy(s->d_sptr, sptr.data(), sptr.size() * 4, hipMemcpyHostToDevice);
-        if (he == hipSuccess) he = hipMemcpy(s->d_xq, L.xq.data(), L.xq.size() * 4, hipMemcpyHostToDevice);
+        hipError_t he = stream_copy(h, s->d_gid, L.gid.data(), L.gid.size() * 4, hipMemcpyHostToDevice);
+        if (he == hipSuccess) he = stream_copy(h, s->d_g2l, g2l.data(), g2l.size() * 4, hipMemcpyHostToDevice);
+        if (he == hipSuccess) he = stream_copy(h, s->d_sptr, sptr.data(), sptr.size() * 4, hipMemcpyHostToDevice);
+        if (he == hipSuccess) he = stream_copy(h, s->d_xq, L.xq.data(), L.xq.size() * 4, hipMemcpyHostToDevice);
         if (he == hipSuccess && !sedge.empty())
-            he = hipMemcpy(s->d_sedge, sedge.data(), sedge.size() * 4, hipMemcpyHostToDevice);
-        if (he == hipSuccess && !xg.empty()) he = hipMemcpy(s->d_xgather, xg.data(), xg.size() * 4, hipMemcpyHostToDevice);
-        if (he == hipSuccess) he = hipMemset(s->d_ymap, 0xFF, (size_t)L.e_loc * 4);
-        if (he == hipSuccess) he = hipMemset(s->d_pgate, 0, (size_t)L.e_loc);
+            he = stream_copy(h, s->d_sedge, sedge.data(), sedge.size() * 4, hipMemcpyHostToDevice);
+        if (he == hipSuccess && !xg.empty()) he = stream_copy(h, s->d_xgather, xg.data(), xg.size() * 4, hipMemcpyHostToDevice);
+        if (he == hipSuccess) he = stream_fill(h, s->d_ymap, 0xFF, (size_t)L.e_loc * 4);
+        if (he == hipSuccess) he = stream_fill(h, s->d_pgate, 0, (size_t)L.e_loc);
         if (he != hipSuccess) return g->fail(GSIM_EDEVICE, "shard tables upload");
         // copy push: each local peer's shard; the cross edges' indices at the
         // receivers' shards follow once every shard's ghost blocks are known
@@ -1540,7 +1540,7 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
             for (int64_t x = L.lpeer[(size_t)q]; x < L.lpeer[(size_t)q + 1]; ++x) psh[(size_t)x] = (uint8_t)q;
         if ((rc = dalloc(h, &s->d_pshard, psh.size())) || (rc = dalloc(h, &s->d_xre, (size_t)L.e_loc)))
             return g->take(h, rc);
-        if (hipMemcpy(s->d_pshard, psh.data(), psh.size(), hipMemcpyHostToDevice) != hipSuccess)
+        if (stream_copy(h, s->d_pshard, psh.data(), psh.size(), hipMemcpyHostToDevice) != hipSuccess)
             return g->fail(GSIM_EDEVICE, "shard tables upload");
         // copy bits: per destination a word-aligned segment of a slot's row, a
         // cross edge's bit at its position in the cross-out list
@@ -1556,8 +1556,8 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
                     xwq[L.crossout[(size_t)q][x]] = (uint32_t)(s->xwo[(size_t)q] * 64 + (int64_t)x);
             if ((rc = dalloc(h, &s->d_xwq, xwq.size())) || (rc = dalloc(h, &s->d_xwo, s->xwo.size())))
                 return g->take(h, rc);
-            if (hipMemcpy(s->d_xwq, xwq.data(), xwq.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-                hipMemcpy(s->d_xwo, s->xwo.data(), s->xwo.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+            if (stream_copy(h, s->d_xwq, xwq.data(), xwq.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+                stream_copy(h, s->d_xwo, s->xwo.data(), s->xwo.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
                 return g->fail(GSIM_EDEVICE, "shard tables upload");
         }
         g->gid[l] = L.gid;
@@ -1608,7 +1608,7 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
         s->pxcap = std::max<int64_t>(1 << 16, 4 * (int64_t)std::max(1, h->gp.prune_peers) * xmax);
         if ((rc = dalloc(h, &s->d_pxout, (size_t)(K * s->pxcap))) || (rc = dalloc(h, &s->d_pxcnt, (size_t)K + 1)))
             return g->take(h, rc);
-        if (hipMemset(s->d_pxcnt, 0, sizeof(uint32_t) * ((size_t)K + 1)) != hipSuccess)
+        if (stream_fill(h, s->d_pxcnt, 0, sizeof(uint32_t) * ((size_t)K + 1)) != hipSuccess)
             return g->fail(GSIM_EDEVICE, "PX list counts");
     }
     return sync_all(g);
@@ -1637,12 +1637,12 @@ int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg)
             s->rdel_cap = std::max<int64_t>(1 << 16, (s->own_e_hi - s->own_e_lo) / 16);
             A(&s->d_rdel, (size_t)s->rdel_cap);
             A(&s->d_rdel_n, 1);
-            if (!rc && hipMemset(s->d_rdel_n, 0, 4) != hipSuccess) return g->fail(GSIM_EDEVICE, "router delta count");
+            if (!rc && stream_fill(h, s->d_rdel_n, 0, 4) != hipSuccess) return g->fail(GSIM_EDEVICE, "router delta count");
         }
         if (s->d_fout) { (void)hipFree(s->d_fout); s->d_fout = nullptr; }
         A(&s->d_fout, (size_t)s->fcap);
         if (!s->d_fcnt) A(&s->d_fcnt, 1);
-        if (!rc && hipMemset(s->d_fcnt, 0, sizeof(uint32_t)) != hipSuccess) return g->fail(GSIM_EDEVICE, "frontier count");
+        if (!rc && stream_fill(h, s->d_fcnt, 0, sizeof(uint32_t)) != hipSuccess) return g->fail(GSIM_EDEVICE, "frontier count");
         s->fpend = 0;
         if (!s->d_cout) {
             A(&s->d_cout, (size_t)(K * s->ccap));
@@ -1666,14 +1666,14 @@ int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg)
             if (!s->d_hsrc) A(&s->d_hsrc, (size_t)K);
             if (!rc && !s->h_hsrc && hipHostMalloc((void**)&s->h_hsrc, sizeof(HSrc) * (size_t)K, 0) != hipSuccess)
                 return g->fail(GSIM_ENOMEM, "pinned scratch");
-            if (!rc && (hipMemset(s->d_hbits, 0, sizeof(uint64_t) * (size_t)(2 * (int64_t)cfg->ring * s->how)) != hipSuccess ||
-                        hipMemset(s->d_hslots, 0, sizeof(uint32_t) * 2 * hw) != hipSuccess))
+            if (!rc && (stream_fill(h, s->d_hbits, 0, sizeof(uint64_t) * (size_t)(2 * (int64_t)cfg->ring * s->how)) != hipSuccess ||
+                        stream_fill(h, s->d_hslots, 0, sizeof(uint32_t) * 2 * hw) != hipSuccess))
                 return g->fail(GSIM_EDEVICE, "holder bits");
             if (!rc) s->hring = cfg->ring;
         } else if (!rc && s->push) {   // a new message configuration: no holders pending
             const size_t hw = (size_t)(cfg->ring + 31) / 32;
-            if (hipMemset(s->d_hbits, 0, sizeof(uint64_t) * (size_t)(2 * (int64_t)cfg->ring * s->how)) != hipSuccess ||
-                hipMemset(s->d_hslots, 0, sizeof(uint32_t) * 2 * hw) != hipSuccess)
+            if (stream_fill(h, s->d_hbits, 0, sizeof(uint64_t) * (size_t)(2 * (int64_t)cfg->ring * s->how)) != hipSuccess ||
+                stream_fill(h, s->d_hslots, 0, sizeof(uint32_t) * 2 * hw) != hipSuccess)
                 return g->fail(GSIM_EDEVICE, "holder bits");
         }
         if (!rc && s->push && s->xring != cfg->ring) {
@@ -1692,12 +1692,12 @@ int gsim_group_msgs_init(gsim_group* g, const gsim_msg_config* cfg)
                 return g->fail(GSIM_ENOMEM, "pinned scratch");
             if (!rc && !s->h_xsrc && hipHostMalloc((void**)&s->h_xsrc, sizeof(XSrc) * (size_t)K, 0) != hipSuccess)
                 return g->fail(GSIM_ENOMEM, "pinned scratch");
-            if (!rc && hipMemset(s->d_xbits, 0, sizeof(uint64_t) * (size_t)((int64_t)cfg->ring * s->xbw)) != hipSuccess)
+            if (!rc && stream_fill(h, s->d_xbits, 0, sizeof(uint64_t) * (size_t)((int64_t)cfg->ring * s->xbw)) != hipSuccess)
                 return g->fail(GSIM_EDEVICE, "copy bits");
             if (!rc) s->xring = cfg->ring;
         }
         if (rc) return g->take(h, rc);
-        if (hipMemset(s->d_gin, 0, (size_t)h->e * 8) != hipSuccess || hipMemset(s->d_gsin, 0, (size_t)h->e) != hipSuccess)
+        if (stream_fill(h, s->d_gin, 0, (size_t)h->e * 8) != hipSuccess || stream_fill(h, s->d_gsin, 0, (size_t)h->e) != hipSuccess)
             return g->fail(GSIM_EDEVICE, "gossip mark buffers");
     }
     g->ring = cfg->ring;
@@ -1978,9 +1978,9 @@ int gsim_group_px_connect(gsim_group* g, int64_t now, uint32_t* pairs, int64_t c
         const int64_t na = s->h_counts[0];
         if (na > (int64_t)K * s->pxcap) return g->fail(GSIM_ERANGE, "PX attempts overflow");
         own[l].resize((size_t)na);
-        if (na && hipMemcpy(own[l].data(), s->d_pxout, sizeof(uint64_t) * (size_t)na, hipMemcpyDeviceToHost) != hipSuccess)
+        if (na && stream_copy(h, own[l].data(), s->d_pxout, sizeof(uint64_t) * (size_t)na, hipMemcpyDeviceToHost) != hipSuccess)
             return g->fail(GSIM_EDEVICE, "PX attempts readback");
-        if (hipMemset(s->d_pxcnt, 0, sizeof(uint32_t) * ((size_t)K + 1)) != hipSuccess)
+        if (stream_fill(h, s->d_pxcnt, 0, sizeof(uint32_t) * ((size_t)K + 1)) != hipSuccess)
             return g->fail(GSIM_EDEVICE, "PX list counts");
         for (int d = 0; d < K; ++d) acnt[l][(size_t)d] = d == g->ids[l] ? 0 : (uint64_t)na;
     }
@@ -2012,7 +2012,7 @@ int gsim_group_px_connect(gsim_group* g, int64_t now, uint32_t* pairs, int64_t c
         gsim_handle* h = g->hs[0];
         std::vector<uint64_t> in((size_t)total[0]);
         (void)hipSetDevice(h->device);
-        if (total[0] && hipMemcpy(in.data(), h->sh->d_pxin, sizeof(uint64_t) * in.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        if (total[0] && stream_copy(h, in.data(), h->sh->d_pxin, sizeof(uint64_t) * in.size(), hipMemcpyDeviceToHost) != hipSuccess)
             return g->fail(GSIM_EDEVICE, "PX attempts readback");
         asks.insert(asks.end(), in.begin(), in.end());
     }
@@ -2056,7 +2056,7 @@ int gsim_group_px_connect(gsim_group* g, int64_t now, uint32_t* pairs, int64_t c
         (void)hipSetDevice(h->device);
         rc = g->take(h, ensure(h, &s->d_pxin, &s->pxin_cap, (int64_t)pv.size()));
         if (rc) return rc;
-        if (hipMemcpy(s->d_pxin, pv.data(), sizeof(uint64_t) * pv.size(), hipMemcpyHostToDevice) != hipSuccess)
+        if (stream_copy(h, s->d_pxin, pv.data(), sizeof(uint64_t) * pv.size(), hipMemcpyHostToDevice) != hipSuccess)
             return g->fail(GSIM_EDEVICE, "PX connections upload");
         rc = g->take(h, px_mark_outbound(h, s->d_pxin, (int64_t)pv.size()));
         if (rc) return rc;
@@ -2115,10 +2115,10 @@ static int group_sum(gsim_group* g, int (*fn)(gsim_handle*, int64_t*), int n, in
         int64_t* d = nullptr;
         if (hipMalloc((void**)&d, sizeof(int64_t) * (n + 1)) != hipSuccess) return g->fail(GSIM_ENOMEM, "totals scratch");
         acc.push_back(first_err ? 1 : 0);
-        (void)hipMemcpy(d, acc.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice);
+        (void)stream_copy(g->hs[0], d, acc.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice);
         int rc = g->take_tr(g->tr->allreduce({d}, n + 1, DT_U64, OP_SUM));
         if (!rc) rc = g->take_tr(g->tr->sync());
-        (void)hipMemcpy(acc.data(), d, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost);
+        (void)stream_copy(g->hs[0], acc.data(), d, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost);
         (void)hipFree(d);
         if (rc) return rc;
         if (acc[(size_t)n] && !first_err) { first_err = GSIM_ERANGE; g->err = "another shard reported an error"; }
