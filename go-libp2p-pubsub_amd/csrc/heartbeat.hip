@@ -767,23 +767,13 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
             col[v] = valid[v] ? a.col[e[v]] : 0u;
             rv[v] = valid[v] ? a.rev[e[v]] : 0u;           // this observer's record of col
             gcol[v] = valid[v] ? glob(a, col[v]) : 0u;
-#ifdef GSIM_DIAG_HB_NOGATHER
-            // diagnostic build (timing only, wrong results): no gathers at rev[e] / col[e]
-            const uint8_t est = valid[v] ? (uint8_t)(GSIM_ES_TRACKED | GSIM_ES_CONNECTED) : 0;
-#else
             const uint8_t est = valid[v] ? a.estate[rv[v]] : 0;
-#endif
             tracked[v] = est & GSIM_ES_TRACKED;
             conn[v] = valid[v] && (a.rstate[e[v]] & GSIM_ES_CONNECTED);
             outb[v] = valid[v] && a.outbound[e[v]];
             dir[v] = valid[v] && a.direct[e[v]];          // direct peers are never grafted or gossiped to
-#ifdef GSIM_DIAG_HB_NOGATHER
-            S[v] = valid[v] ? (double)(int)(e[v] & 7u) - 1.0 : 0.0;
-            subj[v] = valid[v] ? ~0ull : 0ull;
-#else
             S[v] = valid[v] ? a.score[rv[v]] : 0.0;
             subj[v] = valid[v] ? a.sub[col[v]] : 0ull;
-#endif
             mj[v] = valid[v] ? smask_of(a.smask, col[v]) : 0ull;
             // live score for emitGossip: the snapshot until this heartbeat's
             // Graft/Prune touches one of the position's records
