@@ -3438,7 +3438,9 @@ int deliver_flush(gsim_handle* h)
     const dim3 grid(sparse_layout(h) ? std::min(gp, 8192) : gp);
     // a shard's few words (< 2^14, dense, no latency or gater): 4 slot groups
     // (the single engine's 15.6 k words at C3 keep a wave per word: split over 4 / 8
-    // topic groups its commit took 5.43 / 6.03 against 4.47 ms per tick, gpurun_out/r05t_c3)
+    // topic groups its commit took 5.43 / 6.03 against 4.47 ms per tick, gpurun_out/r05t_c3;
+    // a slot batch's lastput / credit loads issued before its stores: 5.32,
+    // gpurun_out/r05u_c3 -- not the claims' serial read-modify-writes, then)
     const bool split = gp < 4096 && h->sh && !a.mlat && !a.gt.act && !sparse_layout(h);
     if (a.clist)
         hipLaunchKernelGGL(k_commit_list<true>, dim3(64, kClSub), dim3(256), 0, h->stream, a);
