@@ -848,7 +848,13 @@ constexpr int kPushTB = GSIM_TM_PUSH_TB;
 // 256 threads (gpurun_out/r04n); dense C3: GSIM_TM_TB (§4.2)
 constexpr int kSparseTB = 512;
 constexpr uint32_t kTmWin = 8192;   // flattened edges whose senders are tabled in LDS at once
-constexpr int kTmTabMin = 256;      // forwarders in a chunk from which the table pays for its fill
+// forwarders in a chunk from which the sender table pays for its fill: every chunk
+// since the 1024-peer chunks of round 4 (C3 holds ~165 forwarders a layer): send
+// 14.27 / 14.28 against 14.39 / 14.40 ms per tick at 256 (gpurun_out/r05v_c3)
+#ifndef GSIM_TM_TAB_MIN
+#define GSIM_TM_TAB_MIN 0
+#endif
+constexpr int kTmTabMin = GSIM_TM_TAB_MIN;
 
 // The wave's remote copies as bits (copy push): lane l sets
 // bits v of xbits word k (~0: none).  Neighbouring lanes carry neighbouring
