@@ -199,6 +199,8 @@ def build_engine(cfg, seed, device, scen=None, shard=None):
         eng.set_kernel_variant(9, 1)
     if os.environ.get("GSIM_XB_GENERIC"):                        # the bit apply one copy at a time (A/B)
         eng.set_kernel_variant(8, 1)
+    if os.environ.get("GSIM_IHAVE_W"):                           # the IHAVE walk's lane group (A/B)
+        eng.set_kernel_variant(3, int(os.environ["GSIM_IHAVE_W"]))
     return eng, net
 
 
