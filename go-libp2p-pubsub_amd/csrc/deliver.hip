@@ -850,7 +850,7 @@ constexpr int kSparseTB = 512;
 constexpr uint32_t kTmWin = 8192;   // flattened edges whose senders are tabled in LDS at once
 // forwarders in a chunk from which the sender table pays for its fill: every chunk
 // since the 1024-peer chunks of round 4 (C3 holds ~165 forwarders a layer): send
-// 14.27 / 14.28 against 14.39 / 14.40 ms per tick at 256 (gpurun_out/r05v_c3)
+// 14.27 / 14.28 against 14.39 / 14.40 ms per tick at 256 (profiles/r05_ab_summary.txt)
 #ifndef GSIM_TM_TAB_MIN
 #define GSIM_TM_TAB_MIN 0
 #endif
