@@ -4310,15 +4310,29 @@ __global__ __launch_bounds__(256) void k_holder_import(RoundArgs a, const uint32
         const int32_t t = (int32_t)a.mtopic[m];
         const uint64_t mine = w0 + lane < sq.nw ? in[sq.in_off + sq.n + k * sq.nw + w0 + lane] : 0ull;
         // word by word, lane b taking bit b: the peers' g2l entries and cells
-        // are consecutive (most holders' words are dense)
-        for (uint64_t wm = __ballot(mine != 0); wm; wm &= wm - 1) {
-            const int j = __builtin_ctzll(wm);
-            const uint64_t bits = (uint64_t)__shfl((long long)mine, j, 64);
-            if (!((bits >> lane) & 1ull)) continue;
-            const uint32_t l = g2l[sq.pbase + (w0 + j) * 64 + lane];
-            if (l == 0xFFFFFFFFu || (l >= a.rlo && l < a.rhi)) continue;      // not a ghost of this shard
-            const int64_t ci = a.cs.idx(m, t, l);                              // a forwarder holds the topic
-            if (ci >= 0) a.cs.cell[ci] = ((uint64_t)fr << 32) | kPeerMask;
+        // are consecutive (most holders' words are dense); kHiP words at a time,
+        // their g2l loads issued before any cell store (one trip, not kHiP)
+        constexpr int kHiP = 4;
+        for (uint64_t wm = __ballot(mine != 0); wm;) {
+            int jv[kHiP];
+            uint32_t lv[kHiP];
+#pragma unroll
+            for (int u = 0; u < kHiP; ++u) {                                // wave-uniform
+                jv[u] = wm ? __builtin_ctzll(wm) : -1;
+                if (wm) wm &= wm - 1;
+            }
+#pragma unroll
+            for (int u = 0; u < kHiP; ++u) {
+                const uint64_t bits = jv[u] >= 0 ? (uint64_t)__shfl((long long)mine, jv[u], 64) : 0ull;
+                lv[u] = ((bits >> lane) & 1ull) ? g2l[sq.pbase + (w0 + jv[u]) * 64 + lane] : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (int u = 0; u < kHiP; ++u) {
+                const uint32_t l = lv[u];
+                if (l == 0xFFFFFFFFu || (l >= a.rlo && l < a.rhi)) continue;  // not a ghost of this shard
+                const int64_t ci = a.cs.idx(m, t, l);                          // a forwarder holds the topic
+                if (ci >= 0) a.cs.cell[ci] = ((uint64_t)fr << 32) | kPeerMask;
+            }
         }
         if (__ballot(mine != 0) && lane == 0 &&
             __hip_atomic_load(&a.slot_last[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int32_t)fr)

@@ -242,6 +242,7 @@ struct ShardCtx {
     uint32_t* d_g2l = nullptr;             // [N_global] local id of a global peer (0xFFFFFFFF: not local)
     uint32_t* d_ymap = nullptr;            // [e] ghost-row edge: the owner shard's owned-row edge index
     uint32_t* d_xgather = nullptr;         // [n_cross] cross-out lists (local edge indices)
+    uint32_t* d_xpos = nullptr;            // [e] its inverse: an owned-row cross edge's index in them (~0: none)
     uint8_t* d_pgate = nullptr;            // [e] ghost-row edge: the sender's score of the receiver >= publishThreshold
     int64_t send_edges = 0, send_max = 0;  // edges into owned peers, longest such run of a row
     uint32_t* d_xq = nullptr;              // [e] owned-row cross edge: its position in the cross-out list to its shard

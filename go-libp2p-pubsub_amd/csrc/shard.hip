@@ -147,6 +147,30 @@ __global__ __launch_bounds__(256) void k_gsel_export(const uint32_t* xgather, in
     }
 }
 
+// The same in edge order: each owned-row edge reads its topic planes where
+// they lie (neighbouring lanes, neighbouring bytes) and a cross edge stores its
+// mask at its cross-out index (xpos).  In cross-out order every plane read was
+// a random byte gather: 16 lines per cross edge at C3 (0.33 ms per shard and
+// tick at K = 8; with the holder import below, the mean shard 11.95 -> 11.86 ms,
+// gpurun_out/r05x_s8).
+__global__ __launch_bounds__(256) void k_gsel_export_e(const uint32_t* xpos, int64_t e_lo, int64_t e_hi,
+                                                       const uint8_t* gsel, const uint8_t* gstate, const uint32_t* owner,
+                                                       const uint64_t* smask, int32_t T, int64_t E, uint64_t* out,
+                                                       uint8_t* gs_out)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = e_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < e_hi; e += stride) {
+        const uint32_t q = xpos[e];
+        if (q == 0xFFFFFFFFu) continue;
+        uint64_t m = 0;
+        const uint64_t sm = smask_of(smask, owner[e]);
+        for (int32_t t = 0; t < T; ++t)
+            if (slot_has(sm, t)) m |= (uint64_t)(gsel[slot_idx(sm, t, E, e)] != 0) << t;
+        out[q] = m;
+        gs_out[q] = gstate[e];
+    }
+}
+
 // ... into the ghost rows: every topic plane of every ghost-row edge.
 __global__ __launch_bounds__(256) void k_gsel_import(const uint64_t* in, const uint8_t* gs_in, uint8_t* gsel,
                                                      uint8_t* gstate, const uint32_t* owner, const uint64_t* smask,
@@ -671,7 +695,7 @@ int dalloc(gsim_handle* h, T** p, size_t n)
 void free_shard_bufs(ShardCtx* s)
 {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(s->d_gid); f(s->d_g2l); f(s->d_sptr); f(s->d_sedge); f(s->d_xq); f(s->d_rdel); f(s->d_rdel_n); f(s->d_rdel_in); f(s->d_ymap); f(s->d_xgather); f(s->d_pgate);
+    f(s->d_gid); f(s->d_g2l); f(s->d_sptr); f(s->d_sedge); f(s->d_xq); f(s->d_rdel); f(s->d_rdel_n); f(s->d_rdel_in); f(s->d_ymap); f(s->d_xgather); f(s->d_xpos); f(s->d_pgate);
     f(s->d_fout); f(s->d_fcnt); f(s->d_fin); f(s->d_cout); f(s->d_ccnt); f(s->d_cin);
     f(s->d_rmesh_out); f(s->d_rfan_out); f(s->d_rflag_out); f(s->d_rmesh_in); f(s->d_rfan_in); f(s->d_rflag_in);
     f(s->d_gout); f(s->d_gsout); f(s->d_gin); f(s->d_gsin);
@@ -874,7 +898,15 @@ int exchange_gossip_marks(gsim_group* g)
         if (!deliver_gossip_view(h, &gv)) return GSIM_OK;      // no message state: nothing gossips
         (void)hipSetDevice(h->device);
         const int64_t ncross = s->xoff[(size_t)g->K];
-        if (ncross)
+#ifndef GSIM_GSEL_EDGE_ORDER
+#define GSIM_GSEL_EDGE_ORDER 1
+#endif
+        if (ncross && GSIM_GSEL_EDGE_ORDER)
+            hipLaunchKernelGGL(k_gsel_export_e, dim3(grid_for(s->own_e_hi - s->own_e_lo)), dim3(256), 0, h->stream,
+                               (const uint32_t*)s->d_xpos, s->own_e_lo, s->own_e_hi, (const uint8_t*)gv.gsel,
+                               (const uint8_t*)gv.gstate, (const uint32_t*)h->d_owner, (const uint64_t*)h->d_smask,
+                               h->t, h->e, s->d_gout, s->d_gsout);
+        else if (ncross)
             hipLaunchKernelGGL(k_gsel_export, dim3(grid_for(ncross)), dim3(256), 0, h->stream,
                                (const uint32_t*)s->d_xgather, ncross, (const uint8_t*)gv.gsel,
                                (const uint8_t*)gv.gstate, (const uint32_t*)h->d_owner, (const uint64_t*)h->d_smask,
@@ -1496,6 +1528,8 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
         std::vector<uint32_t> xg;
         xg.reserve((size_t)L.n_cross);
         for (int q = 0; q < K; ++q) xg.insert(xg.end(), L.crossout[(size_t)q].begin(), L.crossout[(size_t)q].end());
+        std::vector<uint32_t> xpos((size_t)L.e_loc, 0xFFFFFFFFu);
+        for (size_t q = 0; q < xg.size(); ++q) xpos[xg[q]] = (uint32_t)q;
         std::vector<uint32_t> g2l((size_t)n, kNone);
         for (int64_t x = 0; x < L.n_loc; ++x) g2l[L.gid[(size_t)x]] = (uint32_t)x;
         // the edges of each row into owned peers, in row order: the copies
@@ -1516,6 +1550,7 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
             (rc = dalloc(h, &s->d_sptr, sptr.size())) || (rc = dalloc(h, &s->d_xq, (size_t)L.e_loc)) ||
             (rc = dalloc(h, &s->d_sedge, sedge.size())) ||
             (rc = dalloc(h, &s->d_ymap, (size_t)L.e_loc)) || (rc = dalloc(h, &s->d_xgather, xg.size())) ||
+            (rc = dalloc(h, &s->d_xpos, (size_t)L.e_loc)) ||
             (rc = dalloc(h, &s->d_pgate, (size_t)L.e_loc)) ||
             (rc = dalloc(h, &s->d_rmesh_out, (size_t)ncross)) || (rc = dalloc(h, &s->d_rfan_out, (size_t)ncross)) ||
             (rc = dalloc(h, &s->d_rflag_out, (size_t)ncross)) || (rc = dalloc(h, &s->d_rmesh_in, (size_t)L.e_loc)) ||
@@ -1530,6 +1565,7 @@ int gsim_group_load_graph(gsim_group* g, int64_t n, const uint32_t* row_ptr, con
         if (he == hipSuccess && !sedge.empty())
             he = stream_copy(h, s->d_sedge, sedge.data(), sedge.size() * 4, hipMemcpyHostToDevice);
         if (he == hipSuccess && !xg.empty()) he = stream_copy(h, s->d_xgather, xg.data(), xg.size() * 4, hipMemcpyHostToDevice);
+        if (he == hipSuccess) he = stream_copy(h, s->d_xpos, xpos.data(), xpos.size() * 4, hipMemcpyHostToDevice);
         if (he == hipSuccess) he = stream_fill(h, s->d_ymap, 0xFF, (size_t)L.e_loc * 4);
         if (he == hipSuccess) he = stream_fill(h, s->d_pgate, 0, (size_t)L.e_loc);
         if (he != hipSuccess) return g->fail(GSIM_EDEVICE, "shard tables upload");
