@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void k_gsel_export(const uint32_t* xgather, in
 // they lie (neighbouring lanes, neighbouring bytes) and a cross edge stores its
 // mask at its cross-out index (xpos).  In cross-out order every plane read was
 // a random byte gather: 16 lines per cross edge at C3 (0.33 ms per shard and
-// tick at K = 8; with the holder import below, the mean shard 11.95 -> 11.86 ms,
+// tick at K = 8; with k_holder_import's batched loads, the mean shard 11.95 -> 11.86 ms,
 // gpurun_out/r05x_s8).
 __global__ __launch_bounds__(256) void k_gsel_export_e(const uint32_t* xpos, int64_t e_lo, int64_t e_hi,
                                                        const uint8_t* gsel, const uint8_t* gstate, const uint32_t* owner,
