@@ -66,7 +66,8 @@ __device__ __forceinline__ bool verdict_penalises(uint8_t v)
 constexpr int kSlotBatch = GSIM_SLOT_BATCH;      // active slots whose cells are loaded together
 // a shard's split commit: 4 topic groups, 4-slot batches per wave (serial K = 8
 // C3 mean shard 11.80 / 11.78 ms against 11.91 / 11.87 with 8-slot batches; 8
-// groups 12.12 / 12.16, 2 groups 11.80 / 11.77; profiles/r05_ab_summary.txt)
+// groups 12.12 / 12.16, 2 groups 11.80 / 11.77; 2-slot batches 11.91 / 11.89, 1-slot
+// 12.08 / 12.02 against 11.83 / 11.84; profiles/r05_ab_summary.txt)
 #ifndef GSIM_SPLIT_BATCH
 #define GSIM_SPLIT_BATCH 4
 #endif
