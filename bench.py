@@ -272,6 +272,31 @@ def run_tick(eng, k, sched, churn=None, px=False):
         _timed("px_connect", eng.px_connect, now + SECOND // 2, want_pairs=False)
 
 
+def run_ticks(eng, k0, n, sched, churn=None, px=False):
+    """Ticks k0+1 .. k0+n through gsim_step: one call for all of
+    them when nothing happens between ticks, else one call per tick with the
+    churn before and the PX connector after it.  --calltime, sharded groups
+    and GSIM_BENCH_PHASES=1 use the per-phase calls (run_tick)."""
+    if CALLTIME is not None or not hasattr(eng, "step") or os.environ.get("GSIM_BENCH_PHASES"):
+        for kk in range(k0 + 1, k0 + n + 1):
+            run_tick(eng, kk, sched, churn, px=px)
+        return
+
+    def part(a, b):
+        return {g: sched[g] for g in range(a * ROUNDS, b * ROUNDS) if g in sched}
+
+    if not churn and not px:
+        eng.step(k0 + 1, n, part(k0 + 1, k0 + n + 1))
+        return
+    for kk in range(k0 + 1, k0 + n + 1):
+        now = tick_time(kk)
+        for (pairs, up) in (churn or {}).get(kk, []):
+            eng.set_connections(pairs, up=up, now=now - SECOND // 2)
+        eng.step(kk, 1, part(kk, kk + 1))
+        if px:
+            eng.px_connect(now + SECOND // 2, want_pairs=False)
+
+
 def cpu_baseline(cfg, scen=None, n: int = 10_000, ticks: int = 5, budget_s: float = 25.0, warmup: int = 1,
                  legs=("single", "all")):
     """Time the C oracle on a bounded sample of the same workload (same graph
@@ -469,9 +494,8 @@ def main():
             arr["vdelay"] = args.vdelay
 
     kk = 0
-    for _ in range(args.warmup):
-        kk += 1
-        run_tick(eng, kk, sched, churn, px=bool(scen.get("px")))
+    run_ticks(eng, kk, args.warmup, sched, churn, px=bool(scen.get("px")))
+    kk += args.warmup
     eng.synchronize()
     census0 = eng.census()
     stats0 = eng.msg_stats()
@@ -493,9 +517,8 @@ def main():
         CALLTIME = {"_eng": eng}
     diag = _diag_phases(eng) if os.environ.get("GSIM_DIAG_PHASE") else None   # diagnostic builds only
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        kk += 1
-        run_tick(eng, kk, sched, churn, px=bool(scen.get("px")))
+    run_ticks(eng, kk, args.steps, sched, churn, px=bool(scen.get("px")))
+    kk += args.steps
     eng.synchronize()
     barrier()
     wall = time.perf_counter() - t0

@@ -137,6 +137,9 @@ struct Deliver {
     int32_t pub_bound = 0;             // max over topics of the window's publications
     int64_t applied_tick = 0;          // tick of the last application of the pending increments
     uint32_t* d_pslot = nullptr;       // [pub_cap] ring slots of a publish batch
+    gsim_msg* d_sched = nullptr;       // [sched_cap] gsim_step's publications, uploaded once per call
+    uint32_t* d_sslot = nullptr;       // [sched_cap] ... and their ring slots
+    int64_t sched_cap = 0;
     // claim list (member-compacted cells): the cells a round claimed, so the
     // commit touches those alone instead of every (active slot, peer word)
     uint64_t* d_clist = nullptr;       // [kClSub][clist_cap] receiver | slot << 32, in sub-lists
@@ -490,14 +493,27 @@ __device__ __forceinline__ void slots_claimed(const RoundArgs& a, int w, uint32_
     }
 }
 
+// Mark fresh bits of word w of slot m (and the word in the summary).
+__device__ __forceinline__ void fresh_set(const RoundArgs& a, uint32_t m, int64_t w, uint64_t bits)
+{
+    atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + w), bits);
+    uint64_t* sp = a.fsum + (int64_t)m * a.nsw + (w >> 6);
+    const uint64_t sb = 1ull << (w & 63);
+    if (!(__hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & sb))
+        atomicOr(reinterpret_cast<unsigned long long*>(sp), sb);
+}
+
 // Forwarder list state (Deliver::d_fst): entries of parity p at p * kFstStride
 // (own cache lines), the incomplete flag of parity p at kFstBad + p
 constexpr int kFstStride = 32;
 constexpr int kFstBad = 2 * kFstStride;
 constexpr uint64_t kFlOrigin = 1ull << 63;
 
-// Append the lanes' forwarders (on) of send round g to its list; every lane
-// of the wave calls it.
+// Append the lanes' forwarders (on, peer | slot << 32) of send round g to its
+// list; every lane of the wave calls it.  An entry that does not fit marks
+// the list incomplete and becomes a fresh bit; the send then converts the
+// entries that fit (k_flist_fresh) and scans the bits (k_send_tm), so no
+// forwarder is lost however the lists are sized (gsim_msg_config.max_frontier).
 __device__ __forceinline__ void flist_push_wave(const RoundArgs& a, int64_t g, bool on, uint64_t v)
 {
     const uint64_t b = __ballot(on);
@@ -508,8 +524,13 @@ __device__ __forceinline__ void flist_push_wave(const RoundArgs& a, int64_t g, b
     base = (uint32_t)__shfl((int)base, leader, 64);
     if (on) {
         const uint32_t k = base + (uint32_t)__popcll(b & ((1ull << lane) - 1));
-        if ((int64_t)k < a.flist_cap) a.flist[(int64_t)p * a.flist_cap + k] = v;
-        else a.fst[kFstBad + p] = 1;
+        if ((int64_t)k < a.flist_cap) {
+            a.flist[(int64_t)p * a.flist_cap + k] = v;
+        } else {
+            a.fst[kFstBad + p] = 1;
+            const uint32_t x = (uint32_t)v, m = (uint32_t)(v >> 32) & 0x7FFFFFFFu;
+            fresh_set(a, m, (int64_t)(x >> 6), 1ull << (x & 63));
+        }
     }
 }
 
@@ -626,15 +647,6 @@ __device__ __forceinline__ bool is_claim_of(uint64_t c, uint32_t parity)
     return c != kUnseen64 && (hi & kClaim) && ((hi >> 30) & 1u) == parity;
 }
 
-// Mark fresh bits of word w of slot m (and the word in the summary).
-__device__ __forceinline__ void fresh_set(const RoundArgs& a, uint32_t m, int64_t w, uint64_t bits)
-{
-    atomicOr(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + w), bits);
-    uint64_t* sp = a.fsum + (int64_t)m * a.nsw + (w >> 6);
-    const uint64_t sb = 1ull << (w & 63);
-    if (!(__hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & sb))
-        atomicOr(reinterpret_cast<unsigned long long*>(sp), sb);
-}
 
 // Reset the cells and bitmaps of the slots being published into.  Every
 // claim is committed before (gsim_publish flushes the last round), so the
@@ -1282,10 +1294,24 @@ void k_send_tm(RoundArgs a_)
                             // access -- atomicMin keeps a lower edge's claim of this round and
                             // returns what the cell held (a load, then the claim, otherwise)
                             const bool fold = !LAT && !sbit && seeable;
+#if defined(GSIM_DIAG_CLAIM)
+                            // timing diagnostic (wrong first-delivery totals; 2: racy winners)
+                            uint64_t c;
+                            if (known) c = 0ull;
+                            else if (fold) {
+#if GSIM_DIAG_CLAIM == 1
+                                __hip_atomic_fetch_min(a.cs.cell + ci, cv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+                                a.cs.cell[ci] = cv;
+#endif
+                                c = kUnseen64;
+                            } else c = a.cs.cell[ci];
+#else
                             const uint64_t c = known ? 0ull
                                              : fold ? __hip_atomic_fetch_min(a.cs.cell + ci, cv, __ATOMIC_RELAXED,
                                                                              __HIP_MEMORY_SCOPE_AGENT)
                                                     : a.cs.cell[ci];
+#endif
                             const uint32_t chi = (uint32_t)(c >> 32);
                             // the round validation completed (or completes) in; -1: unclaimed
                             // or claimed in this round
@@ -2563,8 +2589,10 @@ __device__ __forceinline__ void listed_copy(const RoundArgs& a, uint32_t r, uint
 // cell -- the lowest edge wins --, the score tracer); the entries of one
 // sender (its slots of a topic) may sit in different blocks, so its records
 // take atomic updates (atomic_mcnt_inc, the exact +1 steps in any order, as
-// listed_copy's).  Configurations with validation latency, the peer gater,
-// the trace or shards keep the scan (flist_allowed).
+// listed_copy's).  Configurations with validation latency, the peer gater or
+// the trace keep the scan, and so do shards on the pull exchange; shards with
+// the copy push walk the list too (a ghost receiver's copy sets its bit, as in
+// k_send_tm<PUSH>) -- flist_allowed.
 constexpr int kLsP = 2;
 constexpr int kLsB = 256;
 __global__ __launch_bounds__(kLsB) void k_send_list(RoundArgs a_)
@@ -2795,10 +2823,12 @@ __global__ __launch_bounds__(kLsB) void k_send_list(RoundArgs a_)
 }
 
 // A list the send round will not walk (the configuration changed since its
-// commit): its forwarders as fresh bits for k_send_tm.
-__global__ __launch_bounds__(256) void k_flist_fresh(RoundArgs a)
+// commit; only_bad: the list is incomplete -- an entry did not fit, the device
+// decides): its forwarders as fresh bits for k_send_tm.
+__global__ __launch_bounds__(256) void k_flist_fresh(RoundArgs a, int only_bad)
 {
     const int par = (int)(a.g & 1);
+    if (only_bad && !a.fst[kFstBad + par]) return;       // complete: k_send_list walks it
     const int64_t n = min((int64_t)a.fst[par * kFstStride], a.flist_cap);
     const uint64_t* fl = a.flist + (int64_t)par * a.flist_cap;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
@@ -3038,7 +3068,7 @@ static void dl_free(Deliver* d)
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_peertx); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
     f(d->d_mlat); f(d->d_vq); f(d->d_vqn); f(d->d_hist); f(d->d_vpc);
-    f(d->d_cbase); f(d->d_mbits); f(d->d_mpre); f(d->d_pslot);
+    f(d->d_cbase); f(d->d_mbits); f(d->d_mpre); f(d->d_pslot); f(d->d_sched); f(d->d_sslot);
     delete d;
 }
 
@@ -3651,8 +3681,10 @@ static int launch_send(gsim_handle* h, RoundArgs& a, int64_t round)
         // the configuration changed since the commit: the list as fresh bits
         RoundArgs b = a;
         b.flist = d->d_flist; b.fst = d->d_fst; b.flist_cap = d->flist_cap;
-        hipLaunchKernelGGL(k_flist_fresh, dim3(1024), dim3(256), 0, h->stream, b);
+        hipLaunchKernelGGL(k_flist_fresh, dim3(1024), dim3(256), 0, h->stream, b, 0);
     }
+    if (walk)   // an overflowed list (device flag): its entries as fresh bits for the scan
+        hipLaunchKernelGGL(k_flist_fresh, dim3(1024), dim3(256), 0, h->stream, a, 1);
     a.flist_send = walk ? 1 : 0;
     int rc = launch_send_tm(h, a);
     if (!rc && walk) {
@@ -4654,13 +4686,17 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
 #ifndef GSIM_CLIST_MULT
 #define GSIM_CLIST_MULT 4
 #endif
-        d->clist_cap = std::max<int64_t>(GSIM_CLIST_MULT * (int64_t)N, 1 << 20) / kClSub;
+        // (gsim_msg_config.max_frontier > 0: that many claim-list entries and half
+        // as many per forwarder list, a memory bound; overflow stays exact)
+        d->clist_cap = cfg->max_frontier > 0 ? std::max<int64_t>(cfg->max_frontier / kClSub, 1)
+                                             : std::max<int64_t>(GSIM_CLIST_MULT * (int64_t)N, 1 << 20) / kClSub;
         A((void**)&d->d_clist, (size_t)d->clist_cap * kClSub * 8);
         A((void**)&d->d_clist_n, (kClSub + 1) * kClStride * 4);
         if (e == hipSuccess) e = hipMemsetAsync(d->d_clist_n, 0, (kClSub + 1) * kClStride * 4, h->stream);
         // forwarder lists: a round's committed claims (the claim list's capacity:
         // more overflow into the scan) and its publications
-        d->flist_cap = d->clist_cap * kClSub + (1 << 16);
+        d->flist_cap = cfg->max_frontier > 0 ? std::max<int64_t>(cfg->max_frontier / 2, 64)
+                                             : d->clist_cap * kClSub + (1 << 16);
         A((void**)&d->d_flist, (size_t)d->flist_cap * 2 * 8);
         A((void**)&d->d_fst, (kFstBad + kFstStride) * 4);
         if (e == hipSuccess) e = hipMemsetAsync(d->d_fst, 0, (kFstBad + kFstStride) * 4, h->stream);
@@ -4763,10 +4799,34 @@ int gsim_msgs_init(gsim_handle* h, const gsim_msg_config* cfg)
     return hip_check(h, e, "gsim_msgs_init");
 }
 
-int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t round)
+}  // extern "C"
+
+// The ring slot of each message of a publish batch: its topic's next slot of
+// a sub-ring (tcount: the topic's publications so far, advanced here), else
+// id % ring.
+static void batch_slots(const Deliver* d, std::vector<int64_t>& tcount, const gsim_msg* msgs, int32_t count,
+                        uint32_t* slots)
 {
-    if (!h) return GSIM_EINVAL;
-    if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
+    for (int32_t m = 0; m < count; ++m) {
+        if (d->cfg.topic_slots > 0) {
+            const int64_t R = d->cfg.topic_slots, t = msgs[m].topic;
+            if ((size_t)t >= tcount.size()) { slots[m] = 0; continue; }   // (refused by the caller's checks)
+            int64_t k = tcount[(size_t)t];
+            for (int32_t q = 0; q < m; ++q) k += msgs[q].topic == msgs[m].topic;
+            slots[m] = (uint32_t)(t * R + k % R);
+        } else {
+            slots[m] = (uint32_t)(msgs[m].id % (uint64_t)d->cfg.ring);
+        }
+    }
+    for (int32_t m = 0; m < count && d->cfg.topic_slots > 0; ++m)
+        if ((size_t)msgs[m].topic < tcount.size()) tcount[msgs[m].topic]++;
+}
+
+// gsim_publish; d_src / d_slots: the batch already on the device (gsim_step's
+// schedule) -- no upload
+static int publish_impl(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t round, const gsim_msg* d_src,
+                        const uint32_t* d_slots)
+{
     Deliver* d = h->dl;
     if (!d) { h->err = "gsim_msgs_init not called"; return GSIM_ESTATE; }
     if (count < 0 || (count > 0 && !msgs) || round < 0) return GSIM_EINVAL;
@@ -4776,6 +4836,10 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
         return GSIM_ESTATE;
     }
     std::vector<uint32_t> slots((size_t)count);
+    {
+        std::vector<int64_t> tc(d->tcount);         // (advanced below, once the batch is accepted)
+        batch_slots(d, tc, msgs, count, slots.data());
+    }
     for (int32_t m = 0; m < count; ++m) {
         // a shard gets every message; an origin that is not one of its peers is 0xFFFFFFFF
         const bool foreign = h->sh && msgs[m].origin == 0xFFFFFFFFu;
@@ -4783,15 +4847,6 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
             msgs[m].verdict > GSIM_VERDICT_SIGNATURE) {
             h->err = "message topic or origin out of range";
             return GSIM_EINVAL;
-        }
-        if (d->cfg.topic_slots > 0) {
-            // a sub-ring: the topic's next slot, in publication order
-            const int64_t R = d->cfg.topic_slots, t = msgs[m].topic;
-            int64_t k = d->tcount[(size_t)t];
-            for (int32_t q = 0; q < m; ++q) k += msgs[q].topic == msgs[m].topic;
-            slots[(size_t)m] = (uint32_t)(t * R + k % R);
-        } else {
-            slots[(size_t)m] = (uint32_t)(msgs[m].id % (uint64_t)d->cfg.ring);
         }
         if (msgs[m].vdelay > GSIM_MAX_VDELAY) { h->err = "vdelay above GSIM_MAX_VDELAY"; return GSIM_EINVAL; }
         if (msgs[m].vdelay && h->gt) {
@@ -4825,7 +4880,7 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
         }
     }
     hipError_t e = hipSuccess;
-    if (count > d->pub_cap) {
+    if (!d_src && count > d->pub_cap) {
         (void)hipStreamSynchronize(h->stream);
         if (d->d_pub) { (void)hipFree(d->d_pub); d->d_pub = nullptr; }
         if (d->d_pslot) { (void)hipFree(d->d_pslot); d->d_pslot = nullptr; }
@@ -4863,11 +4918,19 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
         const int rcf = deliver_flush(h);
         if (rcf) return rcf;
     }
-    e = hipMemcpyAsync(d->d_pub, msgs, sizeof(gsim_msg) * (size_t)count, hipMemcpyHostToDevice, h->stream);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(d->d_pslot, slots.data(), sizeof(uint32_t) * (size_t)count, hipMemcpyHostToDevice, h->stream);
-    if (e != hipSuccess) return hip_check(h, e, "publish upload");
-    for (int32_t m = 0; m < count && d->cfg.topic_slots > 0; ++m) d->tcount[msgs[m].topic]++;
+    if (!d_src) {
+        e = hipMemcpyAsync(d->d_pub, msgs, sizeof(gsim_msg) * (size_t)count, hipMemcpyHostToDevice, h->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(d->d_pslot, slots.data(), sizeof(uint32_t) * (size_t)count, hipMemcpyHostToDevice,
+                               h->stream);
+        if (e != hipSuccess) return hip_check(h, e, "publish upload");
+        d_src = d->d_pub;
+        d_slots = d->d_pslot;
+    }
+    {
+        std::vector<int64_t>& tc = d->tcount;
+        batch_slots(d, tc, msgs, count, slots.data());   // (advances the topics' counts)
+    }
     {
         // the publication window (RoundArgs::mcnt_fast)
         const int64_t tick = round / std::max(1, d->cfg.rounds);
@@ -4900,15 +4963,22 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
     RoundArgs a = make_round_args(h, round);
     const int64_t per_block = 256 * 16;
     const int gx = (int)std::min<int64_t>((h->n + per_block - 1) / per_block, 1024);
-    hipLaunchKernelGGL(k_reset_slots, dim3(std::max(gx, 1), count), dim3(256), 0, h->stream, a,
-                       (const uint32_t*)d->d_pslot, count);
-    hipLaunchKernelGGL(k_publish, dim3((count + 255) / 256), dim3(256), 0, h->stream, a,
-                       (const gsim_msg*)d->d_pub, (const uint32_t*)d->d_pslot, count);
+    hipLaunchKernelGGL(k_reset_slots, dim3(std::max(gx, 1), count), dim3(256), 0, h->stream, a, d_slots, count);
+    hipLaunchKernelGGL(k_publish, dim3((count + 255) / 256), dim3(256), 0, h->stream, a, d_src, d_slots, count);
     d->next_round = round;
     int rc = hip_check(h, hipGetLastError(), "k_publish");
     // origins that have not joined the topic publish to their fanout
-    if (!rc) rc = launch_fanout_publish(h, d->d_pub, count, round, round_time_host(d, round));
+    if (!rc) rc = launch_fanout_publish(h, d_src, count, round, round_time_host(d, round));
     return rc;
+}
+
+extern "C" {
+
+int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t round)
+{
+    if (!h) return GSIM_EINVAL;
+    if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
+    return publish_impl(h, msgs, count, round, nullptr, nullptr);
 }
 
 int gsim_round(gsim_handle* h, int64_t round)
@@ -4925,6 +4995,72 @@ int gsim_round(gsim_handle* h, int64_t round)
     if (rc) return rc;
     deliver_round_end(h, round);
     return GSIM_OK;
+}
+
+int gsim_step(gsim_handle* h, uint64_t tick, int32_t n_ticks, const gsim_msg* msgs, const int64_t* round_off)
+{
+    if (!h || n_ticks < 0) return GSIM_EINVAL;
+    if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
+    if (h->sh) { h->err = "a shard's ticks run through its group"; return GSIM_ESTATE; }
+    Deliver* d = h->dl;
+    if (!d) { h->err = "gsim_msgs_init not called"; return GSIM_ESTATE; }
+    if (n_ticks == 0) return GSIM_OK;
+    const int R = d->cfg.rounds;
+    const int64_t nr = (int64_t)n_ticks * R;
+    if ((msgs == nullptr) != (round_off == nullptr)) return GSIM_EINVAL;
+    int64_t nmsg = 0;
+    if (round_off) {
+        if (round_off[0] != 0) return GSIM_EINVAL;
+        for (int64_t q = 0; q < nr; ++q)
+            if (round_off[q + 1] < round_off[q] || round_off[q + 1] - round_off[q] > INT32_MAX) return GSIM_EINVAL;
+        nmsg = round_off[nr];
+    }
+    int rc = deliver_check_errors(h);                // what the last call left
+    if (rc) return rc;
+    if (nmsg > 0) {
+        // the schedule's ring slots as the publications will take them (the
+        // topics' sub-ring counts advance batch by batch), then one upload
+        std::vector<uint32_t> slots((size_t)nmsg);
+        std::vector<int64_t> tc(d->tcount);
+        for (int64_t q = 0; q < nr; ++q)
+            batch_slots(d, tc, msgs + round_off[q], (int32_t)(round_off[q + 1] - round_off[q]),
+                        slots.data() + round_off[q]);
+        hipError_t e = hipSuccess;
+        if (nmsg > d->sched_cap) {
+            e = hipStreamSynchronize(h->stream);
+            if (d->d_sched) { (void)hipFree(d->d_sched); d->d_sched = nullptr; }
+            if (d->d_sslot) { (void)hipFree(d->d_sslot); d->d_sslot = nullptr; }
+            d->sched_cap = 0;
+            const int64_t cap = std::max<int64_t>(nmsg, 4096);
+            if (e == hipSuccess) e = hipMalloc((void**)&d->d_sched, sizeof(gsim_msg) * (size_t)cap);
+            if (e == hipSuccess) e = hipMalloc((void**)&d->d_sslot, sizeof(uint32_t) * (size_t)cap);
+            if (e != hipSuccess) return hip_check(h, e, "gsim_step schedule");
+            d->sched_cap = cap;
+        }
+        // (no kernel reads the buffers any more: every call ends synchronised)
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(d->d_sched, msgs, sizeof(gsim_msg) * (size_t)nmsg, hipMemcpyHostToDevice, h->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(d->d_sslot, slots.data(), sizeof(uint32_t) * (size_t)nmsg, hipMemcpyHostToDevice,
+                               h->stream);
+        if (e != hipSuccess) return hip_check(h, e, "gsim_step schedule upload");
+    }
+    h->in_step = true;
+    for (int32_t k = 0; k < n_ticks && !rc; ++k) {
+        const uint64_t tk = tick + (uint64_t)k;
+        const int64_t now = d->cfg.t0_ns + (int64_t)tk * d->cfg.heartbeat_ns;
+        rc = gsim_refresh_scores(h, now);
+        if (!rc) rc = gsim_heartbeat(h, tk, now);
+        for (int r = 0; r < R && !rc; ++r) {
+            const int64_t q = (int64_t)k * R + r, g = (int64_t)tk * R + r;
+            const int64_t o0 = round_off ? round_off[q] : 0, cnt = round_off ? round_off[q + 1] - o0 : 0;
+            if (cnt > 0) rc = publish_impl(h, msgs + o0, (int32_t)cnt, g, d->d_sched + o0, d->d_sslot + o0);
+            if (!rc) rc = gsim_round(h, g);
+        }
+    }
+    h->in_step = false;
+    if (!rc) rc = deliver_check_errors(h);         // one synchronisation per call
+    return rc;
 }
 
 int gsim_msg_stats(gsim_handle* h, int64_t* out4)

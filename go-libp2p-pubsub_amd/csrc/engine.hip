@@ -262,59 +262,89 @@ __global__ __launch_bounds__(256) void k_ip_coloc_rows(ColocArgs a, const uint32
 // member has at most one IP they are sorted (bitonic) and each member's count
 // is an equal range of its IP, O(deg log deg) instead of O(deg^2) (a
 // 4096-connection row: 1.7e7 key loads); a row with a several-IP member
-// counts per IP from memory (p6_scan).
+// counts per IP from memory (p6_scan).  Rows longer than kHubP6Max (the
+// reference's ipColocationFactor has no degree bound, score.go:344-388) are
+// counted in tiles: per chunk of kHubP6Max members (their keys and counts in
+// LDS), every kHubP6Max-key tile of the row is sorted in turn and each member
+// adds its key's range in the tile -- the same counts, tiles^2 sorts.
 constexpr int kHubP6Max = 4096;
+
+__device__ __forceinline__ void bitonic_sort_lds(uint32_t* s, uint32_t n2)
+{
+    for (uint32_t k = 2; k <= n2; k <<= 1)               // bitonic sort, ascending
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t q = threadIdx.x; q < n2; q += blockDim.x) {
+                const uint32_t p = q ^ j;
+                if (p > q) {
+                    const uint32_t u = s[q], v = s[p];
+                    if (((q & k) == 0) ? (u > v) : (u < v)) { s[q] = v; s[p] = u; }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+// occurrences of key k in the sorted s[0, n2)
+__device__ __forceinline__ int32_t sorted_count(const uint32_t* s, uint32_t n2, uint32_t k)
+{
+    uint32_t lo = 0, hi = n2;
+    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (s[m] < k) lo = m + 1; else hi = m; }
+    uint32_t lo2 = lo, hi2 = n2;
+    while (lo2 < hi2) { const uint32_t m = (lo2 + hi2) >> 1; if (s[m] <= k) lo2 = m + 1; else hi2 = m; }
+    return (int32_t)(lo2 - lo);
+}
 
 __global__ __launch_bounds__(256) void k_ip_colocation_hub(ColocArgs a, const uint32_t* rows, int64_t nrows)
 {
     if (a.gate && *a.gate == 0) return;
-    __shared__ uint32_t s_key[kHubP6Max];
-    __shared__ uint32_t s_srt[kHubP6Max];
+    __shared__ uint32_t s_key[kHubP6Max];    // the members' keys (a chunk of them on a longer row)
+    __shared__ uint32_t s_srt[kHubP6Max];    // a sorted key tile
+    __shared__ int32_t s_cnt[kHubP6Max];     // the members' counts over the tiles so far
     for (int64_t x = blockIdx.x; x < nrows; x += gridDim.x) {
         const uint32_t i = rows[x];
         const uint32_t b = a.row_ptr[i], deg = a.row_ptr[i + 1] - b;
-        if (deg > (uint32_t)kHubP6Max || deg <= a.hub_min) continue;   // (cannot happen: launch_ip_colocation refuses longer rows)
+        if (deg <= a.hub_min) continue;
         if (a.sharded && (i < a.olo || i >= a.ohi)) continue;
         if (a.rowflag && !a.rowflag[i]) continue;               // only rows whose tracked set changed
         __syncthreads();                                          // (every thread has read the flag)
         if (a.rowflag && threadIdx.x == 0) a.rowflag[i] = 0;
+        const bool one_tile = deg <= (uint32_t)kHubP6Max;
         bool multi = false;
         for (uint32_t q = threadIdx.x; q < deg; q += blockDim.x) {
             const uint32_t k = ip_key(a, b + q);
-            s_key[q] = k;
+            if (one_tile) s_key[q] = k;
             multi |= k == kIpMulti;
         }
-        uint32_t n2 = 1;
-        while (n2 < deg) n2 <<= 1;
         if (!__syncthreads_or(multi)) {
-            for (uint32_t q = threadIdx.x; q < n2; q += blockDim.x) s_srt[q] = q < deg ? s_key[q] : 0xFFFFFFFFu;
-            __syncthreads();
-            for (uint32_t k = 2; k <= n2; k <<= 1)               // bitonic sort, ascending
-                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                    for (uint32_t q = threadIdx.x; q < n2; q += blockDim.x) {
-                        const uint32_t p = q ^ j;
-                        if (p > q) {
-                            const uint32_t u = s_srt[q], v = s_srt[p];
-                            if (((q & k) == 0) ? (u > v) : (u < v)) { s_srt[q] = v; s_srt[p] = u; }
-                        }
-                    }
+            for (uint32_t mc = 0; mc < deg; mc += kHubP6Max) {    // member chunks
+                const uint32_t nm = deg - mc < (uint32_t)kHubP6Max ? deg - mc : (uint32_t)kHubP6Max;
+                for (uint32_t q = threadIdx.x; q < nm; q += blockDim.x) {
+                    if (!one_tile) s_key[q] = ip_key(a, b + mc + q);
+                    s_cnt[q] = 0;
+                }
+                for (uint32_t tc = 0; tc < deg; tc += kHubP6Max) {  // key tiles
+                    const uint32_t nk = deg - tc < (uint32_t)kHubP6Max ? deg - tc : (uint32_t)kHubP6Max;
+                    uint32_t n2 = 1;
+                    while (n2 < nk) n2 <<= 1;
+                    __syncthreads();                              // (s_srt of the last tile is read)
+                    for (uint32_t q = threadIdx.x; q < n2; q += blockDim.x)
+                        s_srt[q] = q >= nk ? 0xFFFFFFFFu : one_tile ? s_key[q] : ip_key(a, b + tc + q);
                     __syncthreads();
+                    bitonic_sort_lds(s_srt, n2);
+                    for (uint32_t q = threadIdx.x; q < nm; q += blockDim.x) {
+                        const uint32_t k = s_key[q];
+                        if (k < kIpNone) s_cnt[q] += sorted_count(s_srt, n2, k);
+                    }
                 }
-            for (uint32_t q = threadIdx.x; q < deg; q += blockDim.x) {
-                const uint32_t k = s_key[q];
-                int32_t cnt = 0;
-                if (k < kIpNone) {
-                    uint32_t lo = 0, hi = n2;
-                    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (s_srt[m] < k) lo = m + 1; else hi = m; }
-                    uint32_t lo2 = lo, hi2 = n2;
-                    while (lo2 < hi2) { const uint32_t m = (lo2 + hi2) >> 1; if (s_srt[m] <= k) lo2 = m + 1; else hi2 = m; }
-                    cnt = (int32_t)(lo2 - lo);
-                }
-                a.p6[a.rev[b + q]] = p6_of(a, k, cnt);
+                for (uint32_t q = threadIdx.x; q < nm; q += blockDim.x)
+                    a.p6[a.rev[b + mc + q]] = p6_of(a, s_key[q], s_cnt[q]);
+                __syncthreads();                                  // s_key is rewritten by the next chunk
             }
         } else {
-            for (uint32_t q = threadIdx.x; q < deg; q += blockDim.x)
-                a.p6[a.rev[b + q]] = s_key[q] == kIpUntracked ? 0.0 : p6_scan(a, b, b + deg, b + q);
+            for (uint32_t q = threadIdx.x; q < deg; q += blockDim.x) {
+                const uint32_t k = one_tile ? s_key[q] : ip_key(a, b + q);
+                a.p6[a.rev[b + q]] = k == kIpUntracked ? 0.0 : p6_scan(a, b, b + deg, b + q);
+            }
         }
         __syncthreads();                                          // LDS is rewritten by the next row
     }
@@ -770,11 +800,6 @@ int launch_ip_colocation(gsim_handle* h, const int32_t* gate)
         h->p6_dirty = false;
         h->p6_rows_only = false;
         return hip_check(h, e, "P6 (no shared IP)");
-    }
-    if (h->max_degree > (uint32_t)kHubP6Max) {
-        // k_ip_colocation_hub stages a row's keys in LDS (kHubP6Max of them)
-        h->err = "P6 (IP colocation) supports rows of at most 4096 connections in this build";
-        return GSIM_ERANGE;
     }
     ColocArgs c{};
     c.gate = gate;

@@ -390,6 +390,10 @@ struct TraceRef {
     int64_t cap = 0;
     uint32_t lo = 0, hi = 0;          // traced routers this engine owns (a shard: local ids)
     uint32_t xlo = 0, xhi = 0;        // ... and its ghosts in the traced range (a shard; else = lo, hi)
+    // host bookkeeping: events [0, resolved) of the buffer were resolved by an
+    // earlier gsim_trace_read and kept for a later one (their ids are wire ids:
+    // resolving them again would index the slot arrays with a message id)
+    uint32_t resolved = 0;
     __device__ __forceinline__ bool on(uint32_t p) const { return ev != nullptr && p >= lo && p < hi; }
     // a traced router that may be another shard's ghost here: events only
     // this shard knows of (the RecvRPC of a copy it pushes, the SendRPC of an
@@ -475,6 +479,7 @@ struct gsim_handle {
     int ihave_w = 0;          // k_ihave lane group width (gsim_set_kernel_variant(h, 3, w)); 0 = by row lengths
     bool xb_generic = false;  // k_xbits_deliver: listed_copy only, never the batched path (variant 8, 1)
     bool flist_off = false;   // never the list-driven send k_send_list (gsim_set_kernel_variant(h, 9, 1))
+    bool in_step = false;     // inside gsim_step: the error flags are read once per call, not per heartbeat
 
     // device: parameters and scratch flags
     gsim_topic_score_params* d_tp = nullptr;

@@ -2618,7 +2618,7 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
     if (h->e == 0 || !h->x) { h->err = "no graph loaded"; return GSIM_ESTATE; }
     int rc = check_degree(h);
-    if (!rc) rc = deliver_check_errors(h);
+    if (!rc && !h->in_step) rc = deliver_check_errors(h);   // (gsim_step reads them once per call)
     if (rc) return rc;
     rc = deliver_flush(h);
     if (!rc) rc = deliver_heartbeat_begin(h, tick);   // IHAVE marks of this heartbeat are pending

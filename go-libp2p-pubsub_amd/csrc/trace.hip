@@ -25,11 +25,11 @@
 namespace gsim {
 namespace {
 
-__global__ __launch_bounds__(256) void k_trace_resolve(gsim_trace_event* ev, int64_t n, TraceView v, int64_t CN,
-                                                       uint32_t clo)
+// events [k0, n): those before k0 were resolved by an earlier read (TraceRef::resolved)
+__global__ __launch_bounds__(256) void k_trace_resolve(gsim_trace_event* ev, int64_t k0, int64_t n, TraceView v)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+    for (int64_t k = k0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
         gsim_trace_event x = ev[k];
         if (x.type == GSIM_TRACE_SEND_RPC || x.type == GSIM_TRACE_RECV_RPC) {   // round << 32 | slot: the id
             ev[k].msg_id = v.mid[(uint32_t)x.msg_id];
@@ -39,7 +39,6 @@ __global__ __launch_bounds__(256) void k_trace_resolve(gsim_trace_event* ev, int
         const uint32_t m = (uint32_t)x.msg_id;
         const int64_t g = (int64_t)(x.msg_id >> 32);
         const uint64_t c = v.cells.get(m, (int32_t)v.mtopic[m], x.peer);
-        (void)CN; (void)clo;
         // every claim is committed before a read (gsim_trace_read flushes)
         const int64_t fr = c == kUnseen64 ? -1 : (int64_t)(c >> 32);
         const uint32_t from = (uint32_t)c & kPeerMask;
@@ -64,10 +63,10 @@ __global__ __launch_bounds__(256) void k_trace_resolve(gsim_trace_event* ev, int
 }
 
 // bad-signature copies carry round << 32 | slot too: only the id changes
-__global__ __launch_bounds__(256) void k_trace_sig_ids(gsim_trace_event* ev, int64_t n, const uint64_t* mid)
+__global__ __launch_bounds__(256) void k_trace_sig_ids(gsim_trace_event* ev, int64_t k0, int64_t n, const uint64_t* mid)
 {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+    for (int64_t k = k0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
         gsim_trace_event x = ev[k];
         if (x.type != GSIM_TRACE_REJECT_MESSAGE || x.reason != GSIM_VERDICT_SIGNATURE) continue;
         ev[k].msg_id = mid[(uint32_t)x.msg_id];
@@ -149,11 +148,13 @@ int gsim_trace_read(gsim_handle* h, gsim_trace_event* out, int64_t cap, int64_t*
     if (cnt) {
         TraceView v{};
         const bool have = deliver_trace_view(h, &v);
-        const int grid = (int)std::min<int64_t>(((int64_t)cnt + 255) / 256, 4096);
-        if (have) {
-            hipLaunchKernelGGL(k_trace_resolve, dim3(grid), dim3(256), 0, h->stream, h->trace.ev, (int64_t)cnt, v,
-                               h->n, 0u);
-            hipLaunchKernelGGL(k_trace_sig_ids, dim3(grid), dim3(256), 0, h->stream, h->trace.ev, (int64_t)cnt, v.mid);
+        // the events an earlier read kept are resolved already
+        const int64_t k0 = std::min<int64_t>(h->trace.resolved, cnt);
+        const int grid = (int)std::min<int64_t>(((int64_t)cnt - k0 + 255) / 256, 4096);
+        if (have && grid > 0) {
+            hipLaunchKernelGGL(k_trace_resolve, dim3(grid), dim3(256), 0, h->stream, h->trace.ev, k0, (int64_t)cnt, v);
+            hipLaunchKernelGGL(k_trace_sig_ids, dim3(grid), dim3(256), 0, h->stream, h->trace.ev, k0, (int64_t)cnt,
+                               v.mid);
             e = hipGetLastError();
         }
         if (e == hipSuccess)
@@ -172,6 +173,7 @@ int gsim_trace_read(gsim_handle* h, gsim_trace_event* out, int64_t cap, int64_t*
     if (e == hipSuccess) e = hipMemcpyAsync(h->trace.n, &keep, sizeof(uint32_t), hipMemcpyHostToDevice, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return hip_check(h, e, "gsim_trace_read");
+    h->trace.resolved = keep;                      // the kept events lead the buffer, resolved
     cnt -= keep;
     *n = cnt;
     std::sort(out, out + cnt, [](const gsim_trace_event& a, const gsim_trace_event& b) {

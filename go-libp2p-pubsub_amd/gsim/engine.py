@@ -260,7 +260,8 @@ class Engine:
         c = _abi.CMsgConfig()
         c.ring, c.rounds, c.t0_ns = int(ring), int(rounds), int(t0)
         c.heartbeat_ns = int(heartbeat if heartbeat is not None else self.gossip.HeartbeatInterval)
-        # max_frontier is reserved (the engine keeps no per-copy lists); max_arrivals
+        # max_frontier bounds the claim / forwarder lists of member-compacted layouts
+        # (0: the default; overflow falls back to the word scans); max_arrivals
         # sizes the IWANT response queue (0: the library default, gsim.h)
         c.max_frontier = int(max_frontier or 0)
         c.max_arrivals = int(max_arrivals or 0)
@@ -293,6 +294,34 @@ class Engine:
     def round(self, rnd: int):
         """One propagation round for the whole network (gsim_round)."""
         self._check(self.lib.gsim_round(self.h, int(rnd)))
+
+    def step(self, tick: int, n_ticks: int = 1, sched: Optional[dict] = None):
+        """n_ticks whole heartbeat ticks in one call (gsim_step): refresh,
+        heartbeat and the rounds of each tick, with sched[g] (an array of
+        dtype _abi.MSG_DTYPE or a list of (id, topic, origin, verdict[, vdelay])
+        tuples) published in round g.  The heartbeat timer loop,
+        gossipsub.go:1320-1343."""
+        R = self._msg_cfg.rounds
+        g0 = int(tick) * R
+        parts, off = [], [0]
+        for q in range(int(n_ticks) * R):
+            m = (sched or {}).get(g0 + q)
+            if m is not None and len(m):
+                if not isinstance(m, np.ndarray):
+                    arr = np.zeros(len(m), dtype=_abi.MSG_DTYPE)
+                    for k, msg in enumerate(m):
+                        arr[k]["id"], arr[k]["topic"], arr[k]["origin"], arr[k]["verdict"] = msg[:4]
+                        if len(msg) > 4:
+                            arr[k]["vdelay"] = msg[4]
+                    m = arr
+                parts.append(np.ascontiguousarray(m))
+            off.append(off[-1] + (len(parts[-1]) if m is not None and len(m) else 0))
+        if off[-1]:
+            msgs = np.ascontiguousarray(np.concatenate(parts))
+            offs = np.asarray(off, dtype=np.int64)
+            self._check(self.lib.gsim_step(self.h, int(tick), int(n_ticks), _ptr(msgs), _ptr(offs)))
+        else:
+            self._check(self.lib.gsim_step(self.h, int(tick), int(n_ticks), None, None))
 
     def set_peer_behaviour(self, flags: np.ndarray):
         """Per-peer adversarial behaviour (gsim_set_peer_behaviour)."""

@@ -348,7 +348,12 @@ typedef struct gsim_msg_config {
     int32_t rounds;          /* propagation rounds per heartbeat, >= 2 */
     int64_t t0_ns;           /* virtual time of tick 0 */
     int64_t heartbeat_ns;    /* heartbeat interval (GossipSubParams.HeartbeatInterval) */
-    int64_t max_frontier;    /* reserved (ignored): the engine keeps no per-copy lists */
+    int64_t max_frontier;    /* 0: default.  > 0: a memory bound on the round lists of member-compacted
+                                layouts (topic_slots > 0): the claim list holds this many entries
+                                (default max(4 N, 2^20)), each forwarder list half as many; a round
+                                that overflows either is completed by the word scans (k_commit,
+                                k_send_tm) -- the same results, slower.  A sharded group also sizes
+                                its frontier export with it (gsim_group_msgs_init) */
     int64_t max_arrivals;    /* capacity of the IWANT response queue per tick (0: max(8 N, 2^20)) */
     int64_t topic_slots;     /* 0: one ring shared by every topic, a message's slot is id % ring, and
                                 every slot keeps a seen-set cell per peer.  > 0: per-topic sub-rings
@@ -407,6 +412,19 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
  *     of several same-round copies the lowest connection is the first;
  *  3. control inbox of round g % rounds (rounds 0 and 1 of a heartbeat). */
 int gsim_round(gsim_handle* h, int64_t round);
+/* n_ticks whole heartbeat ticks in one call (SURVEY.md §8(b) gsim_step; the
+ * heartbeat timer loop, gossipsub.go:1320-1343): for tick k = tick ..
+ * tick + n_ticks - 1 at now = t0 + k * heartbeat (gsim_msg_config):
+ * gsim_refresh_scores, gsim_heartbeat, then the rounds g = k * rounds ..
+ * k * rounds + rounds - 1, each with its publications (gsim_publish) and
+ * gsim_round.  msgs / round_off: the publications of the call's rounds,
+ * msgs[round_off[q] .. round_off[q + 1]) in round q of the call
+ * (n_ticks * rounds + 1 offsets, round_off[0] = 0; both NULL: none), uploaded
+ * once.  The same results as the calls it stands for; the error flags the
+ * heartbeat checks (response-queue overflow, early slot reuse) are read once
+ * per call, at its end (a tick after a failing one ran on flagged state).
+ * Single engines only (a sharded group steps through gsim_group_*). */
+int gsim_step(gsim_handle* h, uint64_t tick, int32_t n_ticks, const gsim_msg* msgs, const int64_t* round_off);
 /* Cumulative totals since gsim_msgs_init: out4 = {msg-edge deliveries
  * (accepted arrivals, duplicates included), first deliveries, duplicates,
  * graylisted arrivals}.  Synchronizes.  GSIM_ERANGE if the IWANT response
@@ -457,7 +475,13 @@ int gsim_census(gsim_handle* h, int64_t* out8);
  *                     gossipsub.go:611-627), SEND_RPC at the requester in
  *                     control round 0 and RECV_RPC at the advertiser in round
  *                     1, one record per requested id (encoded as one
- *                     ControlMeta.iwant; ids in (topic, id) order).  The
+ *                     ControlMeta.iwant; ids in (topic, id) order).
+ *                     Modelled difference: the reference's HandleRPC sends the
+ *                     IWANT request, the IWANT answers and the PRUNEs of one
+ *                     incoming RPC as ONE sendRPC (gossipsub.go:617-627); here
+ *                     the request (control round 0) and the answers (round 1)
+ *                     happen in different rounds, so they are separate RPCs
+ *                     (no reference fixture pins this: parity unpinned).  The
  *                     heartbeat's control / IHAVE RPCs are traced from their
  *                     encoding (gsim_trace_rpc_encode, include/gsim_wire.h)
  *   JOIN / LEAVE      gsim_set_subscriptions (1047-1124)

@@ -409,3 +409,40 @@ def test_c5_combined_wide_hubs_zipf_churn_px_verdicts(require_gpu, topic_slots, 
     run_parity(net, params, th, gp, st, ticks, sched, ring=2048, churn=churn, px_log=log, topic_slots=topic_slots,
                eng=eng)
     assert sum(log) > 0, "PX made connections"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_frontier", [256, 4096])
+def test_list_overflow_fallbacks_bit_exact(require_gpu, max_frontier):
+    """The round lists of member-compacted layouts sized far below a round's
+    first deliveries (gsim_msg_config.max_frontier): the claim list overflows
+    (the commit falls back to k_commit's word scan), the forwarder list
+    overflows (its entries that fit become fresh bits, k_flist_fresh, and the
+    send scans them, k_send_tm), and quiet rounds still fit both.  c5's shape
+    (power law with hubs, Zipf topics on sub-rings, churn, every verdict);
+    bit-exact against the oracle every tick (the c5 line ran on these
+    fallbacks before its lists were sized to 4 N)."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim import graphs
+    from tickrun import restrict_to_subscriptions, run_parity, subscribed_schedule
+    rng = np.random.default_rng(5150)
+    n, T = 6000, 16
+    net = graphs.power_law(n, 16, 2.5, 1024, seed=51, n_topics=T, i0=1)
+    net = graphs.with_subscriptions(net, graphs.zipf_subscriptions(n, T, 4, seed=52))
+    params = beacon_params(T, RetainScore=3 * Second)
+    th = PeerScoreThresholds(GossipThreshold=-20, PublishThreshold=-40, GraylistThreshold=-300,
+                             OpportunisticGraftThreshold=5)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2, FanoutTTL=3 * Second, OpportunisticGraftTicks=3)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 0.3)
+    restrict_to_subscriptions(st, net)
+    ticks = list(range(1, 5))
+    sched = subscribed_schedule(rng, ticks, net, T, 1.0, 0.0, member_only=False,
+                                verdicts=[0.9, 0.04, 0.03, 0.02, 0.01])
+    src = net.owner()
+    und = np.stack([src, net.col], axis=1)
+    und = und[und[:, 0] < und[:, 1]]
+    down = und[rng.choice(len(und), size=len(und) // 100, replace=False)]
+    churn = {2: [(down, False)], 3: [(down, True)]}
+    run_parity(net, params, th, gp, st, ticks, sched, ring=T * 24, churn=churn, topic_slots=24,
+               max_frontier=max_frontier)

@@ -231,29 +231,59 @@ def test_gpu_kat_reset_topic_params(require_gpu):
     eng.close()
 
 
-def test_ip_colocation_refuses_rows_over_4096(require_gpu):
-    """P6's hub kernel stages a row's IP keys in LDS (4096 of them): a row
-    of more connections with shared IPs fails the call with GSIM_ERANGE
-    instead of leaving that row's P6 stale; with one IP per peer P6 is 0
-    everywhere (no scan) and the row is accepted."""
-    from gsim.engine import GsimError, Network
-    n = 5002                                        # peer 0: a row of 5001 connections
-    leaves = np.arange(1, n, dtype=np.uint32)
-    row_ptr = np.zeros(n + 1, dtype=np.uint32)
-    row_ptr[1:] = n - 1 + np.arange(0, n, dtype=np.uint32)
-    col = np.concatenate([leaves, np.zeros(n - 1, dtype=np.uint32)])
-    ob_ = np.concatenate([np.ones(n - 1, np.uint8), np.zeros(n - 1, np.uint8)])
-    sub = np.ones(n, dtype=np.uint64)
-    params = beacon_params(1)
-    for shared in (False, True):
-        ids = (np.arange(n) // 10 if shared else np.arange(n)).astype(np.uint32)
-        net = Network(n, row_ptr, col, ob_, sub, np.arange(n + 1, dtype=np.uint32), ids, int(ids.max()) + 1)
-        with Engine(params, beacon_thresholds(), device=0) as eng:
-            eng.load_graph(net)
-            if not shared:
-                eng.compute_ip_colocation()
-                assert not eng.read(_abi.F_P6).any()
-                continue
-            with pytest.raises(GsimError) as ex:
-                eng.compute_ip_colocation()
-            assert ex.value.rc == _abi.GSIM_ERANGE
+@pytest.mark.parametrize("multi_ip", [False, True])
+def test_ip_colocation_rows_over_4096_bit_exact(require_gpu, multi_ip):
+    """A row of 6001 connections (peer 0 connected to every other peer, the
+    leaves also on a random 8-regular graph): ipColocationFactor has no
+    degree bound (score.go:344-388).  P6's hub kernel counts a row longer
+    than its 4096-key LDS tile in tiles (members in chunks, every key tile
+    sorted in turn); with several IPs per peer it scans per IP from memory.
+    Sybil IPs shared by 10 peers, random tracked sets and whitelists; P6 and
+    the scores equal the oracle's over three refreshes."""
+    from gsim.engine import Network
+    from gsim.graphs import _csr_from_pairs
+    rng = np.random.default_rng(4097)
+    n = 6002
+    leaves = np.arange(1, n, dtype=np.int64)
+    ring = rng.permutation(leaves)
+    u = [np.zeros(n - 1, np.int64)]
+    v = [leaves]
+    for s_ in range(1, 5):                          # 4 shifts of a random cycle: 8-regular among the leaves
+        u.append(ring)
+        v.append(np.roll(ring, s_))
+    u, v = np.concatenate(u), np.concatenate(v)
+    row_ptr, col, outbound = _csr_from_pairs(n, u, v)
+    assert int(np.diff(row_ptr.astype(np.int64)).max()) == n - 1
+    T = 2
+    sub = np.full(n, (1 << T) - 1, dtype=np.uint64)
+    if multi_ip:
+        ip_ptr, ip_ids, n_ips = multi_ips(n, rng, pool=n // 40)
+    else:
+        ip_ids = (np.arange(n) // 10).astype(np.uint32)
+        ip_ptr, n_ips = np.arange(n + 1, dtype=np.uint32), int(ip_ids.max()) + 1
+    net = Network(n, row_ptr, col, outbound, sub, ip_ptr, ip_ids, n_ips)
+    params = beacon_params(T)
+    p5 = rng.normal(0, 5, n)
+    white = (rng.random(n_ips) < 0.1).astype(np.uint8)
+    st = ob.NetState(net, params, thresholds=beacon_thresholds(), p5=p5, ip_white=white)
+    randomize_state(st, rng, NOW)
+    eng = Engine(params, beacon_thresholds())
+    eng.load_graph(net)
+    eng.set_app_score(p5)
+    eng.set_ip_whitelist(white)
+    st.push_to_engine(eng)
+    lib = ob.load()
+    v_ = st.view()
+    for step in range(3):
+        now = NOW + step * Second
+        eng.refresh_scores(now)
+        lib.orc_refresh_scores(v_, now)
+        lib.orc_ip_colocation(v_)
+        lib.orc_compute_scores(v_)
+        gpu = ob.NetState(net, params, thresholds=beacon_thresholds(), p5=p5, ip_white=white)
+        gpu.pull_from_engine(eng)
+        assert_state_equal(st, gpu, ["estate", "p6", "score"])
+        assert np.array_equal(bits(eng.scores()), bits(st.score))
+    hub = st.p6[np.asarray(net.rev)[row_ptr[0]:row_ptr[1]]]
+    assert (hub > 0).sum() > 100, "the hub's shared IPs are counted"
+    eng.close()

@@ -253,6 +253,41 @@ def test_trace_bit_exact(require_gpu, lo, hi, shards):
     assert reasons[1] > 0 and reasons[2] > 0, "IWANT answers and requests traced"
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards", [0, 2])
+def test_trace_read_every_round_bit_exact(require_gpu, shards):
+    """The trace read after every round: an IWANT request of control round 0
+    is stamped at round 1, so a read right after round 0 keeps it, already
+    resolved, for the next read; that read must not resolve it again (its id
+    is a wire id by then).  The tick's reads together equal the oracle's log,
+    on one engine and on 2 shards."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim.engine import random_regular
+    from tickrun import run_parity, subscribed_schedule
+    rng = np.random.default_rng(404)
+    n, k, T = 600, 16, 2
+    params = beacon_params(T)
+    th = PeerScoreThresholds(GossipThreshold=-200, PublishThreshold=-400, GraylistThreshold=-800)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2)
+    net = random_regular(n, k, seed=78, n_topics=T)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 0.6)
+    ticks = list(range(1, 4))
+    sched = subscribed_schedule(rng, ticks, net, T, 4.0, 0.0, verdicts=(0.8, 0.05, 0.05, 0.05, 0.05))
+    log = []
+    eng = None
+    if shards:
+        from gsim.shard import ShardedEngine
+        eng = ShardedEngine(params, th, gossip=gp, shards=shards)
+        eng.load_graph(net)
+        eng.set_seed(SEED)
+        st.push_to_engine(eng)
+    run_parity(net, params, th, gp, st, ticks, sched, ring=256, trace=(0, n), trace_log=log, eng=eng,
+               trace_every_round=True)
+    reasons = np.sum([x[1] for x in log], axis=0)
+    assert reasons[2] > 0, "IWANT requests traced (the events kept across reads)"
+
+
 def _random_rpc(rng, P):
     """An RPC with every part traceRPCMeta reads, optional fields present or
     absent at random (pb() classes)."""

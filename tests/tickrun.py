@@ -83,7 +83,8 @@ def oracle_trace(ev, msgs, lo, hi):
 
 def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, churn=None, after_tick=None,
                eng=None, after_heartbeat=None, px_log=None, trace=None, trace_log=None, topic_slots=0, gater=None,
-               gater_log=None, subs=None, local_only=False):
+               gater_log=None, subs=None, local_only=False, trace_every_round=False,
+               max_frontier=0, step=False):
     """Run `ticks` on a fresh engine loaded with `st`'s state and on the
     oracle; assert identical state, seen-set and totals after every tick.
     churn: {tick: [(pairs, up), ...]} applied just before the tick.
@@ -101,7 +102,14 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
     counts appended to gater_log).  subs: {tick: [(pairs, join), ...]} Join /
     Leave of (peer, topic) pairs applied just before the tick, after churn.
     local_only: `eng` holds only some shards of the network (one shard per
-    process): the parts they own are compared, the totals in full."""
+    process): the parts they own are compared, the totals in full.
+    step: the engine runs each tick with one gsim_step call (refresh,
+    heartbeat and the rounds with their publications) instead of the
+    per-phase calls.  max_frontier: gsim_msg_config.max_frontier (the claim / forwarder list
+    bound of member-compacted layouts: small values force their overflow
+    fallbacks).  trace_every_round: the engine's trace is read after every round (events
+    stamped after the last round run stay for a later read, resolved once)
+    and the tick's reads together must equal the oracle's log."""
     from gsim.engine import Engine
     pushed = eng is None
     if eng is None:
@@ -113,7 +121,7 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
             st.push_to_engine(eng)
         if topic_slots:
             ring = st.T * topic_slots
-        eng.msgs_init(ring, R, T0, Second, topic_slots=topic_slots)
+        eng.msgs_init(ring, R, T0, Second, topic_slots=topic_slots, max_frontier=max_frontier)
         msgs = ob.Msgs(net.n, st.T, ring, R, T0, Second, behaviour=behaviour, topic_slots=topic_slots)
         if trace is not None:
             eng.trace_config(trace[0], trace[1], 1 << 22)
@@ -126,14 +134,18 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
         lib = ob.load()
         for kk in ticks:
             now = tick_time(kk)
+            parts = []
             for (pairs, up) in (churn or {}).get(kk, []):
                 st.churn(pairs, up=up, now=now - Second // 2)
                 eng.set_connections(pairs, up=up, now=now - Second // 2)
             for (pairs, join) in (subs or {}).get(kk, []):
                 st.set_subscriptions(pairs, join, kk, now - Second // 2, SEED)
                 eng.set_subscriptions(pairs, join, kk, now - Second // 2)
-            eng.refresh_scores(now)
-            eng.heartbeat(kk, now)
+            if step:
+                eng.step(kk, 1, {g: sched[g] for g in range(kk * R, kk * R + R) if g in sched})
+            else:
+                eng.refresh_scores(now)
+                eng.heartbeat(kk, now)
             v = st.view()
             lib.orc_refresh_scores(v, now)
             if gater is not None:
@@ -148,10 +160,13 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
                 for msg in sched.get(g, []):
                     mid, t, o, inv = msg[:4]
                     msgs.publish(st, mid, t, o, inv, g, vdelay=msg[4] if len(msg) > 4 else 0)
-                if g in sched:
+                if g in sched and not step:
                     eng.publish(sched[g], g)
                 msgs.round(st, g)
-                eng.round(g)
+                if not step:
+                    eng.round(g)
+                if trace is not None and trace_every_round:
+                    parts.append(eng.trace_read())
             assert eng.msg_stats() == msgs.stats, f"totals differ at tick {kk}: {eng.msg_stats()} vs {msgs.stats}"
             seen = eng.read(_abi.F_SEEN, into=msgs.seen.copy()) if local_only else eng.read(_abi.F_SEEN)
             lput = eng.read(_abi.F_LASTPUT, into=msgs.lastput.copy()) if local_only else eng.read(_abi.F_LASTPUT)
@@ -162,6 +177,10 @@ def run_parity(net, params, th, gp, st, ticks, sched, ring=256, behaviour=None, 
             assert_same(st, gpu)
             if trace is not None:
                 got, want = eng.trace_read(), oracle_trace(msgs.events(), msgs, trace[0], trace[1])
+                if parts:
+                    got = np.concatenate(parts + [got])
+                    got = got[np.lexsort((got["msg_id"], got["topic"], got["reason"], got["other"], got["type"],
+                                          got["peer"], got["timestamp"]))]
                 assert len(got) == len(want), f"trace length differs at tick {kk}: {len(got)} vs {len(want)}"
                 for f in ("timestamp", "msg_id", "peer", "other", "topic", "type", "reason"):
                     bad = np.nonzero(got[f] != want[f])[0]
