@@ -92,6 +92,22 @@ def _diag_phases(eng):
     return read
 
 
+def _diag_hb(eng):
+    """The heartbeat's counters in a -DGSIM_DIAG_HB build (gsim_diag_hb_counts, not part of
+    gsim.h): resets them now and returns a reader of [re-scored positions, Grafts, Prunes,
+    backoff loads]."""
+    import ctypes
+    fn = eng.lib.gsim_diag_hb_counts
+    fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
+    out = (ctypes.c_uint64 * 4)()
+    fn(eng.h, out)
+
+    def read():
+        fn(eng.h, out)
+        return list(out)
+    return read
+
+
 def refresh_bytes(census: dict, n_edges: int) -> int:
     """Compulsory HBM bytes of one refreshScores+score pass on this state
     (DESIGN.md §4.1): every connected scored record reads its 4 counters and
@@ -516,6 +532,7 @@ def main():
     if args.calltime:
         CALLTIME = {"_eng": eng}
     diag = _diag_phases(eng) if os.environ.get("GSIM_DIAG_PHASE") else None   # diagnostic builds only
+    hb_diag = _diag_hb(eng) if os.environ.get("GSIM_DIAG_HB") else None
     t0 = time.perf_counter()
     run_ticks(eng, kk, args.steps, sched, churn, px=bool(scen.get("px")))
     kk += args.steps
@@ -524,6 +541,10 @@ def main():
     wall = time.perf_counter() - t0
     if diag:
         print(json.dumps({"send_phase_clocks_per_tick": [v / args.steps for v in diag()]}), file=sys.stderr)
+    if hb_diag:
+        print(json.dumps({"heartbeat_counts_per_tick": dict(zip(["rescored", "grafts", "prunes", "backoff_loads"],
+                                                                 [v / args.steps for v in hb_diag()]))}),
+              file=sys.stderr)
     if CALLTIME is not None:
         print(json.dumps({"calltime_ms_per_tick": {c: v / args.steps for c, v in CALLTIME.items() if c != "_eng"}}),
               file=sys.stderr)

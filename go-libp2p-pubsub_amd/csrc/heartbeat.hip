@@ -57,6 +57,12 @@ struct HbArgs {
     int32_t T;
     const uint32_t *row_ptr, *col, *rev;
     const uint64_t* sub;
+    // every peer announced every topic (and no Join / Leave since): a
+    // neighbour's subscriptions are the full mask, not a gather of sub[col]
+    int32_t sub_all;
+    // the refresh's invalidMessageDeliveries flag (engine.hip, inv_mark): 0 =
+    // every record's counter is zero, so score_of_record loads no invalid plane
+    const uint32_t* inv_live;
     const uint64_t* smask;     // topic slots of each row owner (nullptr: dense; gsim_internal.h)
     const uint8_t* outbound;
     const uint8_t* direct;     // [E] edge order: col[e] is in the observer's gs.direct set
@@ -323,6 +329,12 @@ __device__ __forceinline__ void stats_prune(const HbArgs& a, bool tracked, bool 
 // operation order: the live Score(p) emitGossip uses after this heartbeat's
 // Graft/Prune changed the record (gossipsub.go:1734).
 constexpr int kScoreChunk = 2;   // topics whose record fields are loaded together
+// Diagnostic build (-DGSIM_DIAG_HB, counts only, results unchanged): [0]
+// score_of_record calls, [1] Graft, [2] Prune, [3] backoff loads, summed over
+// launches (gsim_diag_hb_counts)
+#ifdef GSIM_DIAG_HB
+__device__ unsigned long long g_hb_diag[4];
+#endif
 
 __device__ double score_of_record(const HbArgs& a_, uint32_t rv, uint32_t col)
 {
@@ -332,6 +344,10 @@ __device__ double score_of_record(const HbArgs& a_, uint32_t rv, uint32_t col)
     // lazy meshTime (lazy_mtime): the graft times are loaded instead
     const int64_t* mts = a.mt_lazy ? a.graft : a.mtime;
     const uint64_t mj = smask_of(a.smask, col);      // the records sit in col's row
+    const bool inv_zero = a.inv_live && !*a.inv_live;   // no record holds an invalid delivery
+#ifdef GSIM_DIAG_HB
+    atomicAdd(&g_hb_diag[0], 1ull);
+#endif
     double score = 0.0;
     for (int32_t t0 = 0; t0 < a.T; t0 += kScoreChunk) {
         // the records sit at rv in each topic plane, away from the row: load a
@@ -349,7 +365,7 @@ __device__ double score_of_record(const HbArgs& a_, uint32_t rv, uint32_t col)
             f[j] = ok ? a.first[i] : 0.0;
             md[j] = ok ? a.meshd[i] : 0.0;
             fa[j] = ok ? a.fail[i] : 0.0;
-            iv[j] = ok ? a.invalid[i] : 0.0;
+            iv[j] = ok && !inv_zero ? a.invalid[i] : 0.0;
             mt[j] = ok ? mts[i] : 0;
         }
         for (int j = 0; j < kScoreChunk; ++j) {
@@ -773,7 +789,7 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
             outb[v] = valid[v] && a.outbound[e[v]];
             dir[v] = valid[v] && a.direct[e[v]];          // direct peers are never grafted or gossiped to
             S[v] = valid[v] ? a.score[rv[v]] : 0.0;
-            subj[v] = valid[v] ? a.sub[col[v]] : 0ull;
+            subj[v] = !valid[v] ? 0ull : a.sub_all ? ~0ull : a.sub[col[v]];
             mj[v] = valid[v] ? smask_of(a.smask, col[v]) : 0ull;
             // live score for emitGossip: the snapshot until this heartbeat's
             // Graft/Prune touches one of the position's records
@@ -851,11 +867,17 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
             }
             auto need_bo = [&](int v) {
                 if (!have_bo[v]) {
+#ifdef GSIM_DIAG_HB
+                    if (valid[v]) atomicAdd(&g_hb_diag[3], 1ull);
+#endif
                     bo[v] = valid[v] ? a.backoff[i[v]] : 0;
                     have_bo[v] = true;
                 }
             };
             auto prune = [&](int v) {
+#ifdef GSIM_DIAG_HB
+                atomicAdd(&g_hb_diag[2], 1ull);
+#endif
                 if (a.tr.on((uint32_t)obs)) a.tr.push(a.now, 0, (uint32_t)obs, col[v], t, GSIM_TRACE_PRUNE, 0);
                 stats_prune(a, tracked[v], scored, thr, mcap, sf[v]);
                 dirty[v] |= tracked[v] && scored;
@@ -867,6 +889,9 @@ __device__ __forceinline__ void hb_observer(const HbArgs& a_, Grp& g, int64_t ob
                 ctl[v] |= GSIM_CTL_PRUNE;
             };
             auto graft = [&](int v) {
+#ifdef GSIM_DIAG_HB
+                atomicAdd(&g_hb_diag[1], 1ull);
+#endif
                 if (a.tr.on((uint32_t)obs)) a.tr.push(a.now, 0, (uint32_t)obs, col[v], t, GSIM_TRACE_GRAFT, 0);
                 stats_graft(a, tracked[v], scored, sf[v]);
                 dirty[v] |= tracked[v] && scored;
@@ -1242,7 +1267,7 @@ __device__ __forceinline__ void fanout_observer(const HbArgs& a, Grp& g, int64_t
             conn[v] = valid[v] && (a.rstate[e[v]] & GSIM_ES_CONNECTED);
             dir[v] = valid[v] && a.direct[e[v]];
             S[v] = valid[v] ? a.score[rv[v]] : 0.0;
-            subj[v] = valid[v] ? a.sub[col[v]] : 0ull;
+            subj[v] = !valid[v] ? 0ull : a.sub_all ? ~0ull : a.sub[col[v]];
             S_live[v] = 0.0;
         }
         bool have_live = false;
@@ -2540,6 +2565,12 @@ static HbArgs make_hb_args(gsim_handle* h, uint64_t tick, int64_t now, int parit
     a.gossip_thr = h->th.gossip_threshold; a.gossip_factor = h->gp.gossip_factor;
     a.dlazy = h->gp.dlazy; a.hist_gossip = h->gp.history_gossip;
     a.first = h->d_first; a.invalid = h->d_invalid; a.p5 = h->d_p5; a.p6 = h->d_p6;
+#ifndef GSIM_HB_SUB_GATHER
+    a.sub_all = h->all_joined && !h->sub_dynamic ? 1 : 0;
+#endif
+#ifndef GSIM_HB_INV_GATHER
+    a.inv_live = h->d_inv_live ? h->d_inv_live + (h->inv_par & 1) : nullptr;
+#endif
     a.topic_cap = h->pp.topic_score_cap; a.w5 = h->pp.app_specific_weight; a.w6 = h->pp.ip_colocation_factor_weight;
     a.bp_thr = h->pp.behaviour_penalty_threshold; a.w7 = h->pp.behaviour_penalty_weight;
     a.lastpub = h->x->d_lastpub; a.fan_topics = h->x->d_fantopics;
@@ -2981,3 +3012,16 @@ int gsim_px_connect(gsim_handle* h, int64_t now, uint32_t* pairs, int64_t cap, i
 }
 
 }  // extern "C"
+
+#ifdef GSIM_DIAG_HB
+// the diagnostic counters (not part of gsim.h): read, then reset
+extern "C" int gsim_diag_hb_counts(gsim_handle* h, uint64_t* out4)
+{
+    if (!h || !out4) return GSIM_EINVAL;
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return GSIM_EDEVICE;
+    unsigned long long z[4] = {0, 0, 0, 0};
+    if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_hb_diag), sizeof(z)) != hipSuccess) return GSIM_EDEVICE;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_hb_diag), z, sizeof(z)) != hipSuccess) return GSIM_EDEVICE;
+    return GSIM_OK;
+}
+#endif
