@@ -64,7 +64,10 @@ CONFIGS = {
 #      hubs up to the 4096-connection cap), 64 topics with Zipf subscriptions
 #      (8 per peer), 1 % of connections going down per tick and coming back
 #      two ticks later, publishers are topic members, 4 msg/s/topic (256 msg/s
-#      network-wide) over per-topic sub-rings of 96 slots (ring 6144), peer
+#      network-wide) over per-topic sub-rings of 128 slots (ring 8192, the
+#      engine's maximum: ~32 ticks of publications per topic, so a slot is
+#      reused only after its message has left every window -- 96 slots refused
+#      runs past ~24 ticks), peer
 #      exchange on (PRUNEs carry PX; the connector runs between ticks and
 #      reconnects churned-down addresses).  Topic-slot planes and
 #      member-compacted seen-set cells keep it in one GPU's
@@ -72,18 +75,19 @@ CONFIGS = {
 #      cells).
 SCENARIOS = {
     "c4": {"sybil_frac": 0.2, "per_ip": 50, "opp_ticks": 10},
-    "c5": {"power_law": (2.5, 4096), "i0": 1.0, "zipf_per_peer": 8, "churn_frac": 0.01, "topic_slots": 96,
+    "c5": {"power_law": (2.5, 4096), "i0": 1.0, "zipf_per_peer": 8, "churn_frac": 0.01, "topic_slots": 128,
            "msg_rate": 4.0, "px": True},
 }
 
 
 def _diag_phases(eng):
     """k_send_tm's phase clocks in a -DGSIM_DIAG_PHASE build (gsim_diag_send_phases, not part of
-    gsim.h): resets them now and returns a reader of [all, scans + layouts, walks, waves]."""
+    gsim.h): resets them now and returns a reader of [all, scans + layouts, walks, waves, clocks
+    of the later layers, chunk-layers, chunks, forwarders of the later layers]."""
     import ctypes
     fn = eng.lib.gsim_diag_send_phases
     fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
-    out = (ctypes.c_uint64 * 4)()
+    out = (ctypes.c_uint64 * 8)()
     fn(eng.h, out)
 
     def read():

@@ -894,9 +894,11 @@ __device__ __forceinline__ void xbits_or_wave(uint64_t* xbits, uint64_t k, uint6
 
 // Diagnostic build (-DGSIM_DIAG_PHASE, timing only): shader clocks per wave in
 // k_send_tm's phases -- [0] all, [1] chunk scans and layer layouts, [2] edge
-// walks, [3] waves -- summed over a launch (gsim_diag_send_phases)
+// walks, [3] waves, [4] layout + walk clocks of the layers after a chunk's
+// first, [5] chunk-layers, [6] chunks with a frontier, [7] forwarders of the
+// later layers (per block, summed by wave 0) -- over a launch (gsim_diag_send_phases)
 #ifdef GSIM_DIAG_PHASE
-__device__ unsigned long long g_tm_diag[4];
+__device__ unsigned long long g_tm_diag[8];
 #define TM_CLK(v) const unsigned long long v = (unsigned long long)clock64()
 #define TM_ACC(d, a, b) d += (b) - (a)
 #else
@@ -943,7 +945,7 @@ void k_send_tm(RoundArgs a_)
     unsigned long long n_acc = 0, n_gray = 0, n_first = 0;
 #ifdef GSIM_DIAG_PHASE
     TM_CLK(c_start);
-    unsigned long long d_scan = 0, d_walk = 0;
+    unsigned long long d_scan = 0, d_walk = 0, d_late = 0, n_layers = 0, n_chunks = 0, n_latef = 0;
 #endif
     // one (topic, peer range) item per block
     const uint32_t lb = blockIdx.x;
@@ -1125,6 +1127,10 @@ void k_send_tm(RoundArgs a_)
 #ifdef GSIM_DIAG_PHASE
                 TM_CLK(c_walk);
                 TM_ACC(d_scan, c_layer, c_walk);
+                if (!first_layer) TM_ACC(d_late, c_layer, c_walk);
+                n_layers++;
+                if (first_layer) n_chunks++;
+                else n_latef += (unsigned long long)s_nf;
 #endif
                 if (nf > 0) {
                     constexpr int P = GSIM_TM_P;
@@ -1395,6 +1401,7 @@ void k_send_tm(RoundArgs a_)
                 {
                     TM_CLK(c_wend);
                     TM_ACC(d_walk, c_walk, c_wend);
+                    if (!first_layer) TM_ACC(d_late, c_walk, c_wend);
                 }
 #endif
                 // the next layer: each peer's next slot
@@ -1433,6 +1440,12 @@ void k_send_tm(RoundArgs a_)
         atomicAdd(&g_tm_diag[1], d_scan);
         atomicAdd(&g_tm_diag[2], d_walk);
         atomicAdd(&g_tm_diag[3], 1ull);
+        atomicAdd(&g_tm_diag[4], d_late);
+        if (tid == 0) {
+            atomicAdd(&g_tm_diag[5], n_layers);
+            atomicAdd(&g_tm_diag[6], n_chunks);
+            atomicAdd(&g_tm_diag[7], n_latef);
+        }
     }
 #endif
 }
@@ -5118,16 +5131,16 @@ int gsim_set_peer_behaviour(gsim_handle* h, const uint8_t* flags)
 
 // Diagnostic build only (GSIM_DIAG_PHASE): k_send_tm's phase clocks since the
 // last call (all zero in a normal build), then reset.
-extern "C" int gsim_diag_send_phases(gsim_handle* h, uint64_t* out4)
+extern "C" int gsim_diag_send_phases(gsim_handle* h, uint64_t* out8)
 {
-    if (!h || !out4) return GSIM_EINVAL;
-    for (int k = 0; k < 4; ++k) out4[k] = 0;
+    if (!h || !out8) return GSIM_EINVAL;
+    for (int k = 0; k < 8; ++k) out8[k] = 0;
 #ifdef GSIM_DIAG_PHASE
     if (hipStreamSynchronize(h->stream) != hipSuccess) return GSIM_EDEVICE;
-    unsigned long long v[4] = {0, 0, 0, 0};
+    unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_tm_diag), sizeof(v)) != hipSuccess) return GSIM_EDEVICE;
-    for (int k = 0; k < 4; ++k) out4[k] = v[k];
-    const unsigned long long z[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 8; ++k) out8[k] = v[k];
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_tm_diag), z, sizeof(z)) != hipSuccess) return GSIM_EDEVICE;
 #endif
     return GSIM_OK;

@@ -284,6 +284,6 @@ def test_ip_colocation_rows_over_4096_bit_exact(require_gpu, multi_ip):
         gpu.pull_from_engine(eng)
         assert_state_equal(st, gpu, ["estate", "p6", "score"])
         assert np.array_equal(bits(eng.scores()), bits(st.score))
-    hub = st.p6[np.asarray(net.rev)[row_ptr[0]:row_ptr[1]]]
+    hub = st.p6[row_ptr[0]:row_ptr[1]]          # (NetState fields are in edge order)
     assert (hub > 0).sum() > 100, "the hub's shared IPs are counted"
     eng.close()

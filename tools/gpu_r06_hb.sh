@@ -14,6 +14,9 @@ L=go-libp2p-pubsub_amd
 GSIM_LIB="$ROOT/$L/libgsim_hbdiag.so" GSIM_DIAG_HB=1 timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 \
   --no-cpu-baseline > "$OUT/diag.json" 2> "$OUT/diag.err" || { echo "diag rc=$?"; tail -5 "$OUT/diag.err"; exit 1; }
 grep heartbeat_counts "$OUT/diag.err"
+GSIM_LIB="$ROOT/$L/libgsim_phase.so" GSIM_DIAG_PHASE=1 timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 \
+  --no-cpu-baseline > "$OUT/phase.json" 2> "$OUT/phase.err" || { echo "phase rc=$?"; tail -5 "$OUT/phase.err"; exit 1; }
+grep send_phase "$OUT/phase.err"
 for r in 1 2; do
   for arm in hbbase hbsub head; do
     lib="$ROOT/$L/libgsim_$arm.so"; [ "$arm" = head ] && lib="$ROOT/$L/libgsim.so"
