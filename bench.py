@@ -96,6 +96,32 @@ def _diag_phases(eng):
     return read
 
 
+def host_syncs(eng) -> int:
+    """The library's host synchronisations so far in this process (gsim_host_sync_count)."""
+    import ctypes
+    v = ctypes.c_uint64(0)
+    eng.lib.gsim_host_sync_count(ctypes.byref(v))
+    return int(v.value)
+
+
+def box_info() -> dict:
+    """The box a line was measured on (the same code measured 16 % apart on two
+    boxes): host name and the GPU's current clocks from rocm-smi, best effort."""
+    import socket
+    import subprocess
+    out = {"host": socket.gethostname()}
+    try:
+        r = subprocess.run(["rocm-smi", "--showclocks", "--json"], capture_output=True, text=True, timeout=15)
+        card = next(iter(json.loads(r.stdout).values()))
+        for k, v in card.items():
+            kl = k.lower()
+            if "sclk" in kl or "mclk" in kl or "fclk" in kl:
+                out[k] = v
+    except Exception:                      # noqa: BLE001  (no rocm-smi, no JSON: the host name only)
+        pass
+    return out
+
+
 def _diag_hb(eng):
     """The heartbeat's counters in a -DGSIM_DIAG_HB build (gsim_diag_hb_counts, not part of
     gsim.h): resets them now and returns a reader of [re-scored positions, Grafts, Prunes,
@@ -537,9 +563,11 @@ def main():
         CALLTIME = {"_eng": eng}
     diag = _diag_phases(eng) if os.environ.get("GSIM_DIAG_PHASE") else None   # diagnostic builds only
     hb_diag = _diag_hb(eng) if os.environ.get("GSIM_DIAG_HB") else None
+    syncs0 = host_syncs(eng)
     t0 = time.perf_counter()
     run_ticks(eng, kk, args.steps, sched, churn, px=bool(scen.get("px")))
     kk += args.steps
+    syncs1 = host_syncs(eng)
     eng.synchronize()
     barrier()
     wall = time.perf_counter() - t0
@@ -697,6 +725,10 @@ def main():
                 "mean": sum(sum(ms for ms, _ in p.values()) for p in per_shard) / len(per_shard) / K,
                 "summed": sum(sum(ms for ms, _ in p.values()) for p in per_shard) / K}),
             "gossip_per_tick": {k: (gossip1[k] - gossip0[k]) / K for k in gossip1},
+            "box": box_info(),
+            # host round trips inside the timed ticks (stream synchronisations and blocking
+            # copies the library made, per tick)
+            "host_syncs_per_tick": (syncs1 - syncs0) / K,
             "census": census1,
             "roofline": dominant,
             "roofline_kernels": {"refresh_score": roof_refresh, "delivery": roof_deliv,

@@ -21,6 +21,15 @@
 
 using namespace gsim;
 
+std::atomic<unsigned long long> gsim::g_host_syncs{0};
+
+extern "C" int gsim_host_sync_count(uint64_t* out)
+{
+    if (!out) return GSIM_EINVAL;
+    *out = g_host_syncs.load(std::memory_order_relaxed);
+    return GSIM_OK;
+}
+
 // ---------------------------------------------------------------------------
 // Kernel 1:peerScore.refreshScores (score.go:504-565) fused with
 // peerScore.score (score.go:265-342).  One thread per record (record order,
@@ -31,6 +40,9 @@ using namespace gsim;
 // Topic parameters are wave-uniform (scalar loads).  Operation order is the
 // reference's, compiled with -ffp-contract=off: results are bit-identical to
 // the CPU oracle.
+#ifndef GSIM_REFRESH_GRAFT_EAGER
+#define GSIM_REFRESH_GRAFT_EAGER 0
+#endif
 template <bool REFRESH, bool SCORE>
 __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a_)
 {
@@ -85,6 +97,11 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a_)
             const int64_t i = slot_idx(mj, t, a.E, e);
             double first = a.first[i], meshd = a.meshd[i], fail = a.fail[i], inval = inv_on ? a.invalid[i] : 0.0;
             uint8_t fl = a.tflags[i];
+#if GSIM_REFRESH_GRAFT_EAGER
+            // graftTime with the counters (one memory trip per topic; 8 B more per
+            // record outside the mesh)
+            const int64_t gr = decay ? a.graft[i] : 0;
+#endif
             int64_t mt = 0;
             const uint8_t pc = a.mcnt[i];
             if (pc) {   // deliveries since the last pass precede this decay
@@ -103,7 +120,11 @@ __global__ __launch_bounds__(256) void k_refresh_score(ScoreArgs a_)
                 x = inval * tp->invalid_message_deliveries_decay; if (x < a.dtz) x = 0.0;
                 if (x != inval) { inval = x; a.invalid[i] = x; }
                 if (fl & GSIM_TF_IN_MESH) {
+#if GSIM_REFRESH_GRAFT_EAGER
+                    mt = a.now - gr;
+#else
                     mt = a.now - a.graft[i];
+#endif
                     // lazy meshTime: derived from graftTime and
                     // this refresh's clock where it is read (lazy_mtime)
                     if (!a.mt_lazy || mt < 0) a.mtime[i] = mt;

@@ -8,6 +8,26 @@
 
 #include "gsim.h"
 
+// Every host synchronisation the library makes is counted (gsim_host_sync_count,
+// include/gsim.h): stream synchronisations and blocking copies.  The per-tick
+// count is the host round trips a caller's tick pays (bench.py reports it).
+#include <atomic>
+namespace gsim {
+extern std::atomic<unsigned long long> g_host_syncs;
+inline hipError_t counted_stream_sync(hipStream_t s)
+{
+    g_host_syncs.fetch_add(1, std::memory_order_relaxed);
+    return (hipStreamSynchronize)(s);
+}
+inline hipError_t counted_memcpy(void* dst, const void* src, size_t n, hipMemcpyKind k)
+{
+    g_host_syncs.fetch_add(1, std::memory_order_relaxed);
+    return (hipMemcpy)(dst, src, n, k);
+}
+}  // namespace gsim
+#define hipStreamSynchronize(s) ::gsim::counted_stream_sync(s)
+#define hipMemcpy(d, s, n, k) ::gsim::counted_memcpy(d, s, n, k)
+
 namespace gsim {
 
 constexpr int GSIM_MAX_TOPICS = 64;   // subscriptions are a u64 bitmask

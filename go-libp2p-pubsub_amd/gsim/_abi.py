@@ -254,6 +254,7 @@ SIGNATURES = [
     ("gsim_publish", c_int32, [c_void_p, c_void_p, c_int32, c_int64]),
     ("gsim_round", c_int32, [c_void_p, c_int64]),
     ("gsim_step", c_int32, [c_void_p, c_uint64, c_int32, c_void_p, c_void_p]),
+    ("gsim_host_sync_count", c_int32, [c_void_p]),
     ("gsim_msg_stats", c_int32, [c_void_p, c_void_p]),
     ("gsim_set_peer_behaviour", c_int32, [c_void_p, c_void_p]),
     ("gsim_gossip_stats", c_int32, [c_void_p, c_void_p]),

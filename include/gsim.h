@@ -412,6 +412,10 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
  *     of several same-round copies the lowest connection is the first;
  *  3. control inbox of round g % rounds (rounds 0 and 1 of a heartbeat). */
 int gsim_round(gsim_handle* h, int64_t round);
+/* Host synchronisations the library has made in this process (stream
+ * synchronisations and blocking copies, every handle and group together):
+ * read it around a tick to count the host round trips the tick paid. */
+int gsim_host_sync_count(uint64_t* out);
 /* n_ticks whole heartbeat ticks in one call (SURVEY.md §8(b) gsim_step; the
  * heartbeat timer loop, gossipsub.go:1320-1343): for tick k = tick ..
  * tick + n_ticks - 1 at now = t0 + k * heartbeat (gsim_msg_config):
