@@ -106,19 +106,24 @@ def host_syncs(eng) -> int:
 
 def box_info() -> dict:
     """The box a line was measured on (the same code measured 16 % apart on two
-    boxes): host name and the GPU's current clocks from rocm-smi, best effort."""
+    boxes): host name and the GPU's current clock levels read from sysfs (pp_dpm_*: the level
+    marked '*'), best effort.  No child process: under rocprofv3 every process the bench starts
+    would initialise the GPU, and a launcher script's exec is refused on this pool."""
+    import glob
     import socket
-    import subprocess
     out = {"host": socket.gethostname()}
-    try:
-        r = subprocess.run(["rocm-smi", "--showclocks", "--json"], capture_output=True, text=True, timeout=15)
-        card = next(iter(json.loads(r.stdout).values()))
-        for k, v in card.items():
-            kl = k.lower()
-            if "sclk" in kl or "mclk" in kl or "fclk" in kl:
-                out[k] = v
-    except Exception:                      # noqa: BLE001  (no rocm-smi, no JSON: the host name only)
-        pass
+    for clk in ("sclk", "mclk", "fclk"):           # one entry per DRM card the box shows
+        vals = []
+        for dev in sorted(glob.glob("/sys/class/drm/card*/device")):
+            try:
+                with open(f"{dev}/pp_dpm_{clk}") as f:
+                    cur = [ln.split(":", 1)[1].strip(" *\n") for ln in f if ln.rstrip().endswith("*")]
+                if cur:
+                    vals.append(cur[0])
+            except OSError:
+                pass
+        if vals:
+            out[clk] = vals
     return out
 
 

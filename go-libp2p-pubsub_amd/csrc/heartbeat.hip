@@ -19,6 +19,8 @@
 
 using namespace gsim;
 
+constexpr int kGiantRow = 8192;   // longest row the heartbeat takes (k_heartbeat_hub_g)
+
 struct Extra {
     uint8_t* d_ctl = nullptr;   // [2][T][E] control inbox by round parity
     uint64_t* d_cany = nullptr;  // [2][N] per receiver: topics that may hold control (a superset), by parity
@@ -35,6 +37,13 @@ struct Extra {
     int64_t nh256 = 0, nh1024 = 0, nh4096 = 0;
     int64_t nh2048 = 0;                 // the first rows of the 1025-4096 class, of at most 2048 connections
     int64_t nh128 = 0, nh512 = 0;       // ... of the 65-256 class of at most 128, of the 257-1024 class of at most 512
+    // rows of 4097..8192 connections (the reference's heartbeat has no degree
+    // bound, gossipsub.go:1386-1557): a block of 1024 threads holding 8 row
+    // positions each, whose group state lives in global scratch (d_gscratch:
+    // one BlockGroup<1024, 8>::Shared per block, 278 KB -- more than the LDS)
+    int64_t nh8192 = 0;
+    void* d_gscratch = nullptr;
+    int64_t gscratch_blocks = 0;
     // peer exchange (gsim_gossipsub_params.do_px): topics with PX PRUNEs per
     // observer, connection attempts per edge, the GRAFT RPCs that turned PX off
     uint64_t* d_pxo = nullptr;
@@ -1214,6 +1223,17 @@ __global__ __launch_bounds__(B) void k_heartbeat_hub(HbArgs a, const uint32_t* r
     for (int64_t o = blockIdx.x; o < nrows; o += gridDim.x) hb_observer(a, g, (int64_t)rows[o], true);
 }
 
+// ... rows of 4097..8192 connections: the same code over a group whose state
+// is in global scratch (one slice per block; every view and reduction is a
+// plain pointer access, ordered by the block's barriers)
+template <int B, int V>
+__global__ __launch_bounds__(B) void k_heartbeat_hub_g(HbArgs a, const uint32_t* rows, int64_t nrows, void* scratch)
+{
+    using S = typename BlockGroup<B, V>::Shared;
+    BlockGroup<B, V> g(reinterpret_cast<S*>(scratch) + blockIdx.x);
+    for (int64_t o = blockIdx.x; o < nrows; o += gridDim.x) hb_observer(a, g, (int64_t)rows[o], true);
+}
+
 // Fanout expiry and maintenance (gossipsub.go:1558-1596), run after
 // k_heartbeat (the reference handles fanouts after every joined topic): drop
 // the fanouts not published to for FanoutTTL; for each remaining fanout topic
@@ -1337,6 +1357,14 @@ __global__ __launch_bounds__(B) void k_fanout_heartbeat_hub(HbArgs a, const uint
 {
     __shared__ typename BlockGroup<B, V>::Shared sh;
     BlockGroup<B, V> g(&sh);
+    for (int64_t o = blockIdx.x; o < nrows; o += gridDim.x) fanout_observer(a, g, (int64_t)rows[o]);
+}
+
+template <int B, int V>
+__global__ __launch_bounds__(B) void k_fanout_heartbeat_hub_g(HbArgs a, const uint32_t* rows, int64_t nrows, void* scratch)
+{
+    using S = typename BlockGroup<B, V>::Shared;
+    BlockGroup<B, V> g(reinterpret_cast<S*>(scratch) + blockIdx.x);
     for (int64_t o = blockIdx.x; o < nrows; o += gridDim.x) fanout_observer(a, g, (int64_t)rows[o]);
 }
 
@@ -1763,6 +1791,9 @@ static void launch_px_emit(gsim_handle* h, const HbArgs& a, int live, uint32_t k
     if (x->nh4096)
         hipLaunchKernelGGL((k_px_emit<4 * kPxRow, 4, true>), dim3((uint32_t)std::min<int64_t>(x->nh4096, 65536)),
                            dim3(256), 0, h->stream, a, live, key_tick, purpose, rh + x->nh1024, x->nh4096);
+    if (x->nh8192)   // (scores, candidate bits and draws of 8192 positions: 97 KB of LDS)
+        hipLaunchKernelGGL((k_px_emit<kGiantRow, 4, true>), dim3((uint32_t)std::min<int64_t>(x->nh8192, 65536)),
+                           dim3(256), 0, h->stream, a, live, key_tick, purpose, rh + x->nh1024 + x->nh4096, x->nh8192);
 }
 
 // Connection attempts to connections (the connector, gossipsub.go:941-973):
@@ -1875,7 +1906,7 @@ void row_classes(gsim_handle* h, RowClasses* rc)
 {
     const Extra* x = h->x;
     if (!x) { *rc = RowClasses{nullptr, 0, 0, h->ohi() - h->olo(), 0}; return; }
-    *rc = RowClasses{x->d_rows, x->n16, x->n32, x->n64, x->nh256 + x->nh1024 + x->nh4096};
+    *rc = RowClasses{x->d_rows, x->n16, x->n32, x->n64, x->nh256 + x->nh1024 + x->nh4096 + x->nh8192};
 }
 
 int px_import(gsim_handle* h, const uint64_t* d_in, int64_t n)
@@ -2383,6 +2414,22 @@ __global__ __launch_bounds__(B) void k_fanout_publish_hub(HbArgs a, const gsim_m
     fanout_publish_one(a, g, pub, k);
 }
 
+// ... origins with rows of lo+1 .. B*V connections, group state in global
+// scratch: the grid strides over the batch (one scratch slice per block)
+template <int B, int V>
+__global__ __launch_bounds__(B) void k_fanout_publish_hub_g(HbArgs a, const gsim_msg* pub, int32_t count, uint32_t lo,
+                                                            void* scratch)
+{
+    using S = typename BlockGroup<B, V>::Shared;
+    BlockGroup<B, V> g(reinterpret_cast<S*>(scratch) + blockIdx.x);
+    for (int32_t k = (int32_t)blockIdx.x; k < count; k += (int32_t)gridDim.x) {
+        if (!fanout_publisher(a, pub, k)) continue;      // block-uniform
+        const uint32_t o = pub[k].origin, d = a.row_ptr[o + 1] - a.row_ptr[o];
+        if (d <= lo || d > (uint32_t)(B * V)) continue;
+        fanout_publish_one(a, g, pub, k);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // host side
 
@@ -2418,11 +2465,11 @@ int alloc_extra(gsim_handle* h)
     e = stream_copy(h, rp.data(), h->d_row_ptr, sizeof(uint32_t) * rp.size(), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_check(h, e, "row_ptr readback");
     uint32_t md = 0, mdall = 0;
-    std::vector<uint32_t> cls[6];
+    std::vector<uint32_t> cls[7];
     for (int64_t i = h->olo(); i < h->ohi(); ++i) {
         const uint32_t d = rp[(size_t)i + 1] - rp[(size_t)i];
         md = std::max(md, d);
-        cls[d <= 16 ? 0 : d <= 32 ? 1 : d <= 64 ? 2 : d <= 256 ? 3 : d <= 1024 ? 4 : 5].push_back((uint32_t)i);
+        cls[d <= 16 ? 0 : d <= 32 ? 1 : d <= 64 ? 2 : d <= 256 ? 3 : d <= 1024 ? 4 : d <= 4096 ? 5 : 6].push_back((uint32_t)i);
     }
     for (int64_t i = 0; i < h->n; ++i) mdall = std::max(mdall, rp[(size_t)i + 1] - rp[(size_t)i]);
     if (!h->all_joined) {
@@ -2451,6 +2498,15 @@ int alloc_extra(gsim_handle* h)
     h->x->max_degree = md;
     h->x->n16 = (int64_t)cls[0].size(); h->x->n32 = (int64_t)cls[1].size(); h->x->n64 = (int64_t)cls[2].size();
     h->x->nh256 = (int64_t)cls[3].size(); h->x->nh1024 = (int64_t)cls[4].size(); h->x->nh4096 = (int64_t)cls[5].size();
+    h->x->nh8192 = (int64_t)cls[6].size();
+    if (h->x->nh8192 > 0 && md <= kGiantRow) {
+        // the giant rows' group state: one slice per block of their launches
+        h->x->gscratch_blocks = std::min<int64_t>(h->x->nh8192, 64);
+        const size_t gb = sizeof(typename BlockGroup<1024, kGiantRow / 1024>::Shared) * (size_t)h->x->gscratch_blocks;
+        e = hipMalloc(&h->x->d_gscratch, gb);
+        if (e != hipSuccess) return hip_check(h, e, "giant-row scratch");
+        h->bytes_allocated += gb;
+    }
     if (md > 16 || !h->all_joined) {   // several classes, or an order by subscriptions: keep the lists
         std::vector<uint32_t> all;
         all.reserve((size_t)h->n);
@@ -2487,6 +2543,7 @@ void free_extra(gsim_handle* h)
     if (h->x->d_ctl) (void)hipFree(h->x->d_ctl);
     if (h->x->d_cany) (void)hipFree(h->x->d_cany);
     if (h->x->d_rows) (void)hipFree(h->x->d_rows);
+    if (h->x->d_gscratch) (void)hipFree(h->x->d_gscratch);
     if (h->x->d_lastpub) (void)hipFree(h->x->d_lastpub);
     if (h->x->d_fantopics) (void)hipFree(h->x->d_fantopics);
     if (h->x->d_pxo) (void)hipFree(h->x->d_pxo);
@@ -2612,8 +2669,8 @@ static int grid_rows(int64_t n)
 
 static int check_degree(gsim_handle* h)
 {
-    if (h->x->max_degree > 4096) {
-        h->err = "heartbeat kernels support rows of at most 4096 connections in this build";
+    if (h->x->max_degree > (uint32_t)kGiantRow) {
+        h->err = "heartbeat kernels support rows of at most 8192 connections in this build";
         return GSIM_ERANGE;
     }
     return GSIM_OK;
@@ -2631,6 +2688,10 @@ int launch_fanout_publish(gsim_handle* h, const gsim_msg* d_pub, int32_t count, 
     if (h->x->nh4096)
         hipLaunchKernelGGL((k_fanout_publish_hub<1024, 4>), dim3(count), dim3(1024), 0, h->stream, a, d_pub, count,
                            1024u);
+    if (h->x->nh8192)
+        hipLaunchKernelGGL((k_fanout_publish_hub_g<1024, kGiantRow / 1024>),
+                           dim3((uint32_t)std::min<int64_t>(count, h->x->gscratch_blocks)), dim3(1024), 0, h->stream, a,
+                           d_pub, count, 4096u, h->x->d_gscratch);
     return hip_check(h, hipGetLastError(), "k_fanout_publish");
 }
 
@@ -2698,6 +2759,9 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
         if (x->nh4096 > x->nh2048)   // 4 row positions per thread
             hipLaunchKernelGGL((k_heartbeat_hub<1024, 4>), dim3((uint32_t)std::min<int64_t>(x->nh4096 - x->nh2048, 65536)),
                                dim3(1024), 0, h->stream, a, rh + x->nh256 + x->nh1024 + x->nh2048, x->nh4096 - x->nh2048);
+        if (x->nh8192)   // 8 row positions per thread, group state in global scratch
+            hipLaunchKernelGGL((k_heartbeat_hub_g<1024, kGiantRow / 1024>), dim3((uint32_t)x->gscratch_blocks), dim3(1024),
+                               0, h->stream, a, rh + x->nh256 + x->nh1024 + x->nh4096, x->nh8192, x->d_gscratch);
     }
     hipLaunchKernelGGL(k_fanout_heartbeat, dim3(grid_rows(nown)), dim3(256), 0, h->stream, a);
     const uint32_t* rh = x->d_rows + x->n16 + x->n32 + x->n64;
@@ -2710,6 +2774,9 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
     if (x->nh4096)
         hipLaunchKernelGGL((k_fanout_heartbeat_hub<1024, 4>), dim3((uint32_t)std::min<int64_t>(x->nh4096, 65536)),
                            dim3(1024), 0, h->stream, a, rh + x->nh256 + x->nh1024, x->nh4096);
+    if (x->nh8192)
+        hipLaunchKernelGGL((k_fanout_heartbeat_hub_g<1024, kGiantRow / 1024>), dim3((uint32_t)x->gscratch_blocks),
+                           dim3(1024), 0, h->stream, a, rh + x->nh256 + x->nh1024 + x->nh4096, x->nh8192, x->d_gscratch);
     if (a.do_px)    // sendGraftPrune's makePrune with PX, live scores after every topic
         launch_px_emit(h, a, 1, (uint32_t)tick, (uint32_t)P_PX);
     return hip_check(h, hipGetLastError(), "k_heartbeat");

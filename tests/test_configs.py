@@ -446,3 +446,65 @@ def test_list_overflow_fallbacks_bit_exact(require_gpu, max_frontier):
     churn = {2: [(down, False)], 3: [(down, True)]}
     run_parity(net, params, th, gp, st, ticks, sched, ring=T * 24, churn=churn, topic_slots=24,
                max_frontier=max_frontier)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_rows_over_4096_bit_exact(require_gpu):
+    """Hub rows of 6000 and 5000 connections (the reference's heartbeat and
+    ipColocationFactor have no degree bound, gossipsub.go:1386-1557,
+    score.go:344-388): their heartbeat runs on a block of 1024 threads with 8
+    row positions each and the group state in global scratch
+    (k_heartbeat_hub_g), fanout maintenance and publication likewise, PX lists
+    on the 8192-position k_px_emit, P6 in 4096-key tiles.  A power law with
+    two such hubs, dense hub meshes (Dhi prunes over thousands of positions),
+    opportunistic grafting, churn, PX, sybil IPs on the hubs, fanout
+    publishers and every verdict; bit-exact against the oracle every tick."""
+    from fixtures import beacon_params, synthetic_state
+    from gsim import graphs
+    from gsim.engine import Network
+    from tickrun import restrict_to_subscriptions, run_parity, subscribed_schedule
+    rng = np.random.default_rng(8192)
+    n, T = 8000, 6
+    base = graphs.power_law(n, 12, 2.5, 1024, seed=81, n_topics=T, i0=1)
+    src = base.owner()
+    u = [src[src < base.col].astype(np.int64)]
+    v = [base.col[src < base.col].astype(np.int64)]
+    for hub, deg in ((0, 6000), (1, 5000)):
+        others = rng.choice(np.arange(2, n), size=deg, replace=False)
+        u.append(np.full(deg, hub, np.int64))
+        v.append(others.astype(np.int64))
+    u, v = np.concatenate(u), np.concatenate(v)
+    a_, b_ = np.minimum(u, v), np.maximum(u, v)
+    key = np.unique(a_ * n + b_)
+    a_, b_ = key // n, key % n
+    flip = rng.random(len(a_)) < 0.5                    # who dialled
+    row_ptr, col, outbound = graphs._csr_from_pairs(n, np.where(flip, b_, a_), np.where(flip, a_, b_))
+    deg = np.diff(row_ptr.astype(np.int64))
+    assert deg[0] >= 6000 and deg[1] >= 5000 and deg.max() <= 8192
+    ip_ids = np.arange(n, dtype=np.uint32)
+    ip_ids[2:2000] = 2 + (np.arange(1998) // 25)          # sybil IPs shared by 25 peers each
+    net = Network(n, row_ptr, col, outbound, np.full(n, (1 << T) - 1, dtype=np.uint64),
+                  np.arange(n + 1, dtype=np.uint32), ip_ids, int(ip_ids.max()) + 1)
+    net = graphs.with_subscriptions(net, graphs.zipf_subscriptions(n, T, 3, seed=82))
+    sub = net.sub.copy()
+    sub[:2] = (1 << T) - 1                                # the hubs hold every topic
+    net = graphs.with_subscriptions(net, sub)
+    params = beacon_params(T, RetainScore=3 * Second)
+    th = PeerScoreThresholds(GossipThreshold=-20, PublishThreshold=-40, GraylistThreshold=-300,
+                             AcceptPXThreshold=0.0, OpportunisticGraftThreshold=5)
+    gp = GossipSubParams(D=8, Dlo=6, Dhi=12, Dscore=4, Dout=2, FanoutTTL=3 * Second, OpportunisticGraftTicks=2,
+                         PeerExchange=True)
+    st = ob.NetState(net, params, thresholds=th, gossip=gp)
+    synthetic_state(st, rng, tick_time(0), 0.3)           # hub meshes far over Dhi: prunes over thousands
+    restrict_to_subscriptions(st, net)
+    ticks = list(range(1, 5))
+    sched = subscribed_schedule(rng, ticks, net, T, 1.5, 0.0, member_only=False,
+                                verdicts=[0.85, 0.05, 0.04, 0.03, 0.03])
+    s2 = net.owner()
+    und = np.stack([s2, net.col], axis=1)
+    und = und[und[:, 0] < und[:, 1]]
+    down = und[rng.choice(len(und), size=len(und) // 80, replace=False)]
+    churn = {2: [(down, False)], 4: [(down, True)]}
+    log = []
+    run_parity(net, params, th, gp, st, ticks, sched, ring=1024, churn=churn, px_log=log)
