@@ -29,9 +29,12 @@ def main(path, shards, ticks=None):
         agg[name] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         cnt[name] += 1
     tot = sum(agg.values()) / (1e6 * kept)
+    span = (max(int(r["End_Timestamp"]) for r in rows) - int(rows[0]["Start_Timestamp"])) / (1e6 * kept)
     print(f"{kept} ticks, {shards} shard(s): {tot:.3f} ms per tick all shards, {tot / shards:.3f} ms per tick per shard")
+    print(f"  device span {span:.3f} ms per tick (first dispatch to last end; the gaps: {span - tot / shards:.3f} ms"
+          f" with one shard), {len(rows) / kept:.1f} dispatches per tick")
     print(f"  {'kernel':44s} {'all shards':>10s} {'per shard':>10s}  dispatches")
-    for n, v in agg.most_common(20):
+    for n, v in agg.most_common(int(__import__('os').environ.get('TOPK', '20'))):
         ms = v / (1e6 * kept)
         print(f"  {n[-44:]:44s} {ms:10.3f} {ms / shards:10.3f}  {cnt[n]:6d}")
 
