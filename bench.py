@@ -143,6 +143,25 @@ def _diag_hb(eng):
     return read
 
 
+def _diag_ih(eng):
+    """The member-major IHAVE walk's counters in a -DGSIM_DIAG_IH build (gsim_diag_ih_counts,
+    not part of gsim.h), per LP (1: rows of <= 256 connections, 2: the hub rows): push row
+    walks, push edges, gossip targets among them, pull row walks, pull edges, gossiping
+    advertisers among them, push and pull wave clocks.  Resets them now; returns a reader."""
+    import ctypes
+    fn = eng.lib.gsim_diag_ih_counts
+    fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
+    out = (ctypes.c_uint64 * 16)()
+    fn(eng.h, out)
+
+    def read():
+        fn(eng.h, out)
+        names = ("push_walks", "push_edges", "push_targets", "pull_walks", "pull_edges", "pull_advertisers",
+                 "push_clocks", "pull_clocks")
+        return {f"lp{lp}": {k: int(out[8 * (lp - 1) + q]) for q, k in enumerate(names)} for lp in (1, 2)}
+    return read
+
+
 def refresh_bytes(census: dict, n_edges: int) -> int:
     """Compulsory HBM bytes of one refreshScores+score pass on this state
     (DESIGN.md §4.1): every connected scored record reads its 4 counters and
@@ -568,6 +587,7 @@ def main():
         CALLTIME = {"_eng": eng}
     diag = _diag_phases(eng) if os.environ.get("GSIM_DIAG_PHASE") else None   # diagnostic builds only
     hb_diag = _diag_hb(eng) if os.environ.get("GSIM_DIAG_HB") else None
+    ih_diag = _diag_ih(eng) if os.environ.get("GSIM_DIAG_IH") else None
     syncs0 = host_syncs(eng)
     t0 = time.perf_counter()
     run_ticks(eng, kk, args.steps, sched, churn, px=bool(scen.get("px")))
@@ -582,6 +602,9 @@ def main():
         print(json.dumps({"heartbeat_counts_per_tick": dict(zip(["rescored", "grafts", "prunes", "backoff_loads"],
                                                                  [v / args.steps for v in hb_diag()]))}),
               file=sys.stderr)
+    if ih_diag:
+        print(json.dumps({"ihave_counts_per_tick": {lp: {k: v / args.steps for k, v in d.items()}
+                                                    for lp, d in ih_diag().items()}}), file=sys.stderr)
     if CALLTIME is not None:
         print(json.dumps({"calltime_ms_per_tick": {c: v / args.steps for c, v in CALLTIME.items() if c != "_eng"}}),
               file=sys.stderr)

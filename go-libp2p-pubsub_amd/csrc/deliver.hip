@@ -49,6 +49,18 @@
 
 namespace gsim {
 
+// The member-major IHAVE walk reads a member's held / unseen window slots as two
+// 128-bit masks (k_gossip_count_mm writes them) instead of one cell per slot, on
+// sub-rings of at most kIhMaskSlots slots (0: the cells, for A/B builds)
+#ifndef GSIM_IH_MASK
+#define GSIM_IH_MASK 1
+#endif
+constexpr int kIhMaskSlots = 128;
+__device__ __forceinline__ bool bit128(uint64_t w0, uint64_t w1, int k)
+{
+    return ((k < 64 ? w0 >> k : w1 >> (k - 64)) & 1ull) != 0;
+}
+
 // seen-set cell encoding: kUnseen64, kClaim, ... (gsim_internal.h)
 constexpr int kMaxRing = 8192;     // active-slot list lives in LDS (u16, sized by the ring)
 
@@ -127,6 +139,10 @@ struct Deliver {
     int64_t hubw_cap = 0;
     uint32_t* d_mctab = nullptr;       // [T+1] first 1024-member block of each topic (k_gossip_count_mm)
     std::vector<uint32_t> mmtab, mctab;
+    // member-major gossip on sub-rings of at most 128 slots: per member of each topic, the
+    // window slots it holds and the ones it has not seen, by sub-ring index (k_gossip_count_mm)
+    uint64_t* d_ihm = nullptr;         // [members][4]: held words 0-1, unseen words 2-3
+    int64_t* d_mmb = nullptr;          // [T] first member of each topic in d_ihm
     int64_t cell_nw = 0;               // words per topic of the member bitmaps
     int64_t n_peers = 0;               // peers the cells were laid out for
     std::vector<int64_t> tcount;       // [T] messages published per topic (sub-ring slot choice)
@@ -1624,6 +1640,10 @@ struct IhArgs {
     const int64_t *mloff, *mcount;
     const uint32_t* mmtab;
     int32_t topic_slots;
+    // MM on sub-rings of at most 128 slots (Deliver::d_ihm): per member, the window slots
+    // held and unseen, written by k_gossip_count_mm, read by k_ihave instead of the cells
+    uint64_t* ihm;
+    const int64_t* mmb;
     // MM hub rows (k_ihave LP 1 / 2): the listed waves (block * 4 + wave) and their count
     uint32_t* hubw;
     uint32_t* hubn;
@@ -1805,6 +1825,7 @@ __global__ __launch_bounds__(256) void k_gossip_count_mm(IhArgs a, const uint32_
         const bool vp = j < M;
         const uint32_t p = vp ? member_peer(a, t, j) : 0u;
         const bool subp = vp && ((a.sub[p] >> t) & 1ull) && p >= a.rlo && p < a.rhi;
+        uint64_t hw0 = 0, hw1 = 0, uw0 = 0, uw1 = 0;       // the member's held / unseen window slots
         for (int q = 0; q < ns; ++q) {
             const int k = s_slot[q];
             const uint32_t m = (uint32_t)(m_lo + k);
@@ -1812,9 +1833,16 @@ __global__ __launch_bounds__(256) void k_gossip_count_mm(IhArgs a, const uint32_
             const bool hold = vp && holds_in_window(c, a.g, a.lo_round, tick_round, a.minv[m] != 0, p == a.morigin[m],
                                                     LAT ? a.mlat[m] : 0u);
             const bool want = subp && c == kUnseen64;
+            const uint64_t kb = 1ull << (k & 63);
+            if (hold) { if (k < 64) hw0 |= kb; else hw1 |= kb; }
+            if (c == kUnseen64) { if (k < 64) uw0 |= kb; else uw1 |= kb; }
             const int nh = __popcll(__ballot(hold)), nw = __popcll(__ballot(want));
             if (lane == 0 && nh) atomicAdd(&s_c[k], (uint32_t)nh);
             if (lane == 0 && nw) atomicAdd(&s_c[R + k], (uint32_t)nw);
+        }
+        if (a.ihm && vp) {
+            uint64_t* o = a.ihm + (a.mmb[t] + j) * 4;
+            o[0] = hw0; o[1] = hw1; o[2] = uw0; o[3] = uw1;
         }
     }
     __syncthreads();
@@ -1842,6 +1870,16 @@ constexpr int kIhBatch = GSIM_IH_BATCH;   // MM walks: slots whose cells one lan
 // with 16 slices each, gpurun_out/r04c5h, r04c5i)
 constexpr uint32_t kIhHub = 256;
 constexpr int kIhSlices = 16;
+#ifdef GSIM_DIAG_IH
+// diagnostic build (counts and wave clocks only, results unchanged), per LP (1, 2):
+// [0] push row walks, [1] push edges, [2] their gossip targets, [3] pull row walks,
+// [4] pull edges, [5] their gossiping advertisers, [6] push clocks, [7] pull clocks
+// (per wave), read by gsim_diag_ih_counts
+__device__ unsigned long long g_ih_diag[16];
+#define IH_D(...) __VA_ARGS__
+#else
+#define IH_D(...)
+#endif
 template <int W, bool LAT, bool SP, bool MM = false, int LP = 0>
 __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, const uint32_t* gcount)
 {
@@ -2034,7 +2072,16 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
             }
         }
     }
+    IH_D(unsigned long long d_pw = 0, d_pe = 0, d_ph = 0, d_qw = 0, d_qe = 0, d_qh = 0, d_pc = 0, d_qc = 0;)
     if constexpr (MM) {
+        IH_D(const unsigned long long c_p0 = clock64();)
+        // the member's held / unseen window slots (k_gossip_count_mm), else its cells below
+        const bool msk = a.ihm != nullptr;
+        uint64_t ih0 = 0, ih1 = 0, iu0 = 0, iu1 = 0;
+        if (msk && vp) {
+            const uint64_t* o = a.ihm + (a.mmb[tb] + jw + lane) * 4;
+            ih0 = o[0]; ih1 = o[1]; iu0 = o[2]; iu1 = o[3];
+        }
         // push slots of the block's topic, up to 64 at a time: a holder walks its
         // row once for all the slots it holds, and each peer it gossiped tb to
         // (and that is one of this shard's receivers, whose gate passes) is
@@ -2046,6 +2093,10 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 const uint16_t sa = s_act[k0 + q];
                 if (!(sa & 0x8000)) continue;                // pulled below (wave-uniform)
                 const uint32_t m = sa & 0x7FFF;
+                if (msk) {
+                    if (vp && bit128(ih0, ih1, (int)m - m_lo)) hm |= 1ull << q;
+                    continue;
+                }
                 const uint64_t c = vp ? a.cs.cell[(int64_t)a.cs.cbase[m] + jw + lane] : kUnseen64;
                 if (vp && holds_in_window(c, a.g, a.lo_round, tick_round, a.minv[m] != 0, (uint32_t)pl == a.morigin[m],
                                           LAT ? a.mlat[m] : 0u))
@@ -2064,12 +2115,19 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                     p = a.col[e];
                     re = a.rev[e];
                     gs = p >= a.rlo && p < a.rhi && a.gstate[re];  // p's gate on me_id
+                    IH_D(d_ph++;)
                 }
+                IH_D(d_pe += v;)
                 const uint64_t mine = gs ? hmw : 0ull;
                 uint64_t uw = mine;
                 for (int o = 32; o; o >>= 1) uw |= (uint64_t)__shfl_xor((long long)uw, o, 64);
                 const uint32_t pg = gs ? (a.gid ? a.gid[p] : p) : 0u;
                 const int64_t poff = gs ? a.cs.at(0, t, p) : -1;    // p's cell in every slot of tb
+                uint64_t pu0 = 0, pu1 = 0;                          // ... or its unseen window slots
+                if (msk && poff >= 0) {
+                    const uint64_t* o = a.ihm + (a.mmb[t] + poff) * 4 + 2;
+                    pu0 = o[0]; pu1 = o[1];
+                }
                 while (uw) {
                   // kIhBatch slots' cells in flight at once (nothing here writes a cell)
                   int qb[kIhBatch];
@@ -2080,7 +2138,10 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                       qb[b] = uw ? __builtin_ctzll(uw) : -1;
                       if (uw) uw &= uw - 1;
                       ask[b] = qb[b] >= 0 && ((mine >> qb[b]) & 1ull) && poff >= 0;
-                      cvb[b] = ask[b] ? a.cs.cell[(int64_t)a.cs.cbase[s_act[k0 + qb[b]] & 0x7FFF] + poff] : 0ull;
+                      const uint32_t mb = ask[b] ? s_act[k0 + qb[b]] & 0x7FFF : 0u;
+                      cvb[b] = !ask[b] ? 0ull
+                             : msk ? (bit128(pu0, pu1, (int)mb - m_lo) ? kUnseen64 : 0ull)
+                                   : a.cs.cell[(int64_t)a.cs.cbase[mb] + poff];
                   }
 #pragma unroll
                   for (int b = 0; b < kIhBatch; ++b) {
@@ -2124,6 +2185,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 const uint64_t me_m = smask_of(a.smask, me_id);
                 const int64_t me_pl = slot_has(me_m, t) ? slot_idx(me_m, t, a.E, 0) : -1;
                 n_walk += (gl == 0 && bs >= 0);
+                IH_D(d_pw += (gl == 0 && bs >= 0);)
                 const uint32_t deg = bs >= 0 ? end - beg : 0u;
                 for (uint32_t off = 0; __ballot(off < deg) != 0; off += W)
                     hchunk(off, (uint32_t)gl, beg, deg, me_id, me_g, ign_s, me_pl, hmw);
@@ -2138,6 +2200,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 const uint64_t me_m = smask_of(a.smask, me_id);
                 const int64_t me_pl = slot_has(me_m, t) ? slot_idx(me_m, t, a.E, 0) : -1;
                 n_walk += (lane == 0 && slice == 0);
+                IH_D(d_pw += (lane == 0 && slice == 0);)
                 for (uint32_t off = slice * 64; off < end - beg; off += 64 * nsl)
                     hchunk(off, (uint32_t)lane, beg, end - beg, me_id, me_g, ign_s, me_pl, hmw);
             }
@@ -2147,6 +2210,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
         // edge whose advertiser gossiped tb to it asks for each wanted slot
         // the advertiser holds (the same (receiver, advertiser, message)
         // triples as a walk per slot)
+        IH_D(const unsigned long long c_p1 = clock64(); d_pc += c_p1 - c_p0;)
         const bool rcv = vp && ((subp >> tb) & 1ull) && pl >= a.rlo && pl < a.rhi;
         for (int k0 = 0; k0 < nact; k0 += 64) {
             const int kn = nact - k0 < 64 ? nact - k0 : 64;
@@ -2154,6 +2218,10 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
             for (int q = 0; q < kn; ++q) {
                 const uint16_t sa = s_act[k0 + q];
                 if (sa & 0x8000) continue;                   // pushed above (wave-uniform)
+                if (msk) {
+                    if (rcv && bit128(iu0, iu1, (int)(sa & 0x7FFF) - m_lo)) wm |= 1ull << q;
+                    continue;
+                }
                 const uint64_t c = rcv ? a.cs.cell[(int64_t)a.cs.cbase[sa & 0x7FFF] + jw + lane] : 0ull;
                 if (rcv && c == kUnseen64) wm |= 1ull << q;
             }
@@ -2171,11 +2239,17 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                     const uint64_t mi = smask_of(a.smask, i);        // i's emitGossip choices: its row
                     gs = slot_has(mi, t) && a.gsel[slot_idx(mi, t, a.E, re)] && a.gstate[e];
                 }
+                IH_D(d_qe += v; d_qh += gs;)
                 const uint64_t mine = gs ? wmw : 0ull;
                 uint64_t uw = mine;                                  // the slots some lane asks about
                 for (int o = 32; o; o >>= 1) uw |= (uint64_t)__shfl_xor((long long)uw, o, 64);
                 const uint32_t ig = gs ? (a.gid ? a.gid[i] : i) : 0u;
                 const int64_t ioff = gs ? a.cs.at(0, t, i) : -1;    // i's cell in every slot of tb
+                uint64_t ah0 = 0, ah1 = 0;                          // ... or its held window slots
+                if (msk && ioff >= 0) {
+                    const uint64_t* o = a.ihm + (a.mmb[t] + ioff) * 4;
+                    ah0 = o[0]; ah1 = o[1];
+                }
                 while (uw) {
                   // kIhBatch slots' cells in flight at once (nothing here writes a cell)
                   int qb[kIhBatch];
@@ -2185,7 +2259,10 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                       qb[b] = uw ? __builtin_ctzll(uw) : -1;
                       if (uw) uw &= uw - 1;
                       const bool ask = qb[b] >= 0 && ((mine >> qb[b]) & 1ull) && ioff >= 0;
-                      cvb[b] = ask ? a.cs.cell[(int64_t)a.cs.cbase[s_act[k0 + qb[b]] & 0x7FFF] + ioff] : kUnseen64;
+                      const uint32_t mb = ask ? s_act[k0 + qb[b]] & 0x7FFF : 0u;
+                      // a held slot: its cell (msk: the mask stands in, read as held below)
+                      cvb[b] = !ask ? kUnseen64 : msk ? (bit128(ah0, ah1, (int)mb - m_lo) ? 1ull : kUnseen64)
+                                                      : a.cs.cell[(int64_t)a.cs.cbase[mb] + ioff];
                   }
 #pragma unroll
                   for (int b = 0; b < kIhBatch; ++b) {
@@ -2194,8 +2271,9 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                     const uint32_t m = s_act[k0 + q] & 0x7FFF;
                     bool req = false, resp = false;
                     if ((mine >> q) & 1ull) {
-                        req = holds_in_window(cvb[b], a.g, a.lo_round, tick_round,
-                                              a.minv[m] != 0, i == a.morigin[m], LAT ? a.mlat[m] : 0u);
+                        req = msk ? cvb[b] != kUnseen64
+                                  : holds_in_window(cvb[b], a.g, a.lo_round, tick_round,
+                                                    a.minv[m] != 0, i == a.morigin[m], LAT ? a.mlat[m] : 0u);
                         if (req) {
                             if (a.tr.ev) trace_iwant(a, me_id, i, m);
                             const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, me_g, 0, P_PROMISE, m, ig);
@@ -2228,6 +2306,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 const uint64_t wmw = bs < 0 ? 0ull : (uint64_t)__shfl((long long)wm, sl, 64);
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
                 n_walk += (gl == 0 && bs >= 0);
+                IH_D(d_qw += (gl == 0 && bs >= 0);)
                 const uint32_t deg = bs >= 0 ? end - beg : 0u;
                 for (uint32_t off = 0; __ballot(off < deg) != 0; off += W) pchunk(off, (uint32_t)gl, beg, deg, me_id, me_g, wmw);
             }
@@ -2238,10 +2317,12 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 const uint64_t wmw = (uint64_t)__shfl((long long)wm, bs, 64);
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
                 n_walk += (lane == 0 && slice == 0);
+                IH_D(d_qw += (lane == 0 && slice == 0);)
                 for (uint32_t off = slice * 64; off < end - beg; off += 64 * nsl)
                     pchunk(off, (uint32_t)lane, beg, end - beg, me_id, me_g, wmw);
             }
         }
+        IH_D(d_qc += clock64() - c_p1;)
         if constexpr (LP == 1) {
             if (had_hub && lane == 0) {
                 // every slice (one per 256 connections of the longest row made fewer,
@@ -2253,6 +2334,18 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
         }
     }
     flush_stage();
+#ifdef GSIM_DIAG_IH
+    if (MM && LP) {
+        unsigned long long* dg = g_ih_diag + (LP == 2 ? 8 : 0);
+        const unsigned long long v6[6] = {wave_sum_u64(d_pw), wave_sum_u64(d_pe), wave_sum_u64(d_ph),
+                                          wave_sum_u64(d_qw), wave_sum_u64(d_qe), wave_sum_u64(d_qh)};
+        if (lane == 0) {
+            for (int q = 0; q < 6; ++q) if (v6[q]) atomicAdd(&dg[q], v6[q]);
+            atomicAdd(&dg[6], d_pc);
+            atomicAdd(&dg[7], d_qc);
+        }
+    }
+#endif
     n_walk = wave_sum_u64(n_walk);
     n_req = wave_sum_u64(n_req);
     n_resp = wave_sum_u64(n_resp);
@@ -3076,7 +3169,7 @@ static void dl_free(Deliver* d)
 {
     if (!d) return;
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_flist); f(d->d_fst); f(d->d_clist); f(d->d_clist_n); f(d->d_hidx); f(d->d_hrow); f(d->d_hlist); f(d->d_mlist); f(d->d_mloff); f(d->d_mcount); f(d->d_mmtab); f(d->d_hubw); f(d->d_mctab); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
+    f(d->d_mtopic); f(d->d_morigin); f(d->d_minv); f(d->d_mid); f(d->d_cell); f(d->d_seenbm); f(d->d_fresh); f(d->d_fsum); f(d->d_mmask); f(d->d_tmtab); f(d->d_flist); f(d->d_fst); f(d->d_clist); f(d->d_clist_n); f(d->d_hidx); f(d->d_hrow); f(d->d_hlist); f(d->d_mlist); f(d->d_mloff); f(d->d_mcount); f(d->d_mmtab); f(d->d_hubw); f(d->d_mctab); f(d->d_ihm); f(d->d_mmb); f(d->d_mpub); f(d->d_roff); f(d->d_lastput);
     f(d->d_nnew); f(d->d_stats); f(d->d_seen32); f(d->d_pub);
     f(d->d_slot_last); f(d->d_gsel); f(d->d_gcount); f(d->d_gstate); f(d->d_resp); f(d->d_nresp); f(d->d_peertx); f(d->d_prom); f(d->d_pcand);
     f(d->d_behaviour); f(d->d_gstats);
@@ -3351,6 +3444,7 @@ static bool ihave_prepare(gsim_handle* h, int64_t g, IhaveStage* st, int* rc)
     if (mm_gossip(h)) {
         a.mlist = d->d_mlist; a.mloff = d->d_mloff; a.mcount = d->d_mcount; a.mmtab = d->d_mmtab;
         a.topic_slots = (int32_t)d->cfg.topic_slots;
+        a.ihm = d->d_ihm; a.mmb = d->d_mmb;
         // the hub-row list: at most every wave of the launch (grow-only)
         const int64_t need = 4 * (int64_t)(d->mmtab.empty() ? 0 : d->mmtab.back());
         if (need > d->hubw_cap) {
@@ -4543,9 +4637,10 @@ static hipError_t install_layout(gsim_handle* h, Deliver* d, const CellLayout& L
     hipError_t e = hipSuccess;
     auto fr = [](void* p) { if (p) (void)hipFree(p); };
     fr(d->d_cbase); fr(d->d_mbits); fr(d->d_mpre);
-    fr(d->d_mlist); fr(d->d_mloff); fr(d->d_mcount); fr(d->d_mmtab); fr(d->d_mctab);
+    fr(d->d_mlist); fr(d->d_mloff); fr(d->d_mcount); fr(d->d_mmtab); fr(d->d_mctab); fr(d->d_ihm); fr(d->d_mmb);
     d->d_cbase = nullptr; d->d_mbits = nullptr; d->d_mpre = nullptr;
     d->d_mlist = nullptr; d->d_mloff = nullptr; d->d_mcount = nullptr; d->d_mmtab = nullptr; d->d_mctab = nullptr;
+    d->d_ihm = nullptr; d->d_mmb = nullptr;
     e = hipMalloc((void**)&d->d_cbase, std::max<size_t>(L.cbase.size() * 8, 8));
     if (e == hipSuccess) e = stream_copy(h, d->d_cbase, L.cbase.data(), L.cbase.size() * 8, hipMemcpyHostToDevice);
     if (e == hipSuccess && L.sparse) {
@@ -4573,6 +4668,14 @@ static hipError_t install_layout(gsim_handle* h, Deliver* d, const CellLayout& L
         if (e == hipSuccess) e = stream_copy(h, d->d_mcount, L.mcount.data(), T * 8, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = stream_copy(h, d->d_mmtab, d->mmtab.data(), (T + 1) * 4, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = stream_copy(h, d->d_mctab, d->mctab.data(), (T + 1) * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess && GSIM_IH_MASK && d->cfg.topic_slots > 0 && d->cfg.topic_slots <= kIhMaskSlots) {
+            std::vector<int64_t> mmb(T, 0);
+            int64_t tot = 0;
+            for (size_t t = 0; t < T; ++t) { mmb[t] = tot; tot += L.mcount[t]; }
+            e = hipMalloc((void**)&d->d_ihm, std::max<size_t>((size_t)tot * 32, 32));
+            if (e == hipSuccess) e = hipMalloc((void**)&d->d_mmb, T * 8);
+            if (e == hipSuccess) e = stream_copy(h, d->d_mmb, mmb.data(), T * 8, hipMemcpyHostToDevice);
+        }
     }
     d->cbase = L.cbase;
     d->sparse = L.sparse;
@@ -4993,6 +5096,19 @@ int gsim_publish(gsim_handle* h, const gsim_msg* msgs, int32_t count, int64_t ro
     if (hipSetDevice(h->device) != hipSuccess) return GSIM_EDEVICE;
     return publish_impl(h, msgs, count, round, nullptr, nullptr);
 }
+
+#ifdef GSIM_DIAG_IH
+// the IHAVE walk's diagnostic counters (not part of gsim.h): read, then reset
+extern "C" int gsim_diag_ih_counts(gsim_handle* h, uint64_t* out16)
+{
+    if (!h || !out16) return GSIM_EINVAL;
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return GSIM_EDEVICE;
+    unsigned long long z[16] = {};
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_ih_diag), sizeof(z)) != hipSuccess) return GSIM_EDEVICE;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_ih_diag), z, sizeof(z)) != hipSuccess) return GSIM_EDEVICE;
+    return GSIM_OK;
+}
+#endif
 
 int gsim_round(gsim_handle* h, int64_t round)
 {
