@@ -1850,10 +1850,12 @@ __global__ __launch_bounds__(256) void k_gossip_count_mm(IhArgs a, const uint32_
         if (s_c[w]) atomicAdd(&gcount[(w < R ? 0 : a.ring - R) + m_lo + w], s_c[w]);
 }
 
-// waves per SIMD the member-major IHAVE walk is fitted to: 5 (96 VGPRs, 25
-// spilled) against 4 (112): c5 gossip 96.4 -> 92.0 ms per tick (gpurun_out/r04ab_occ)
+// waves per SIMD the member-major IHAVE walk is fitted to: round 4 measured 5
+// (96 VGPRs, 25 spilled) against 4 (112): c5 gossip 96.4 -> 92.0 ms per tick; with
+// the window masks (round 6) 4 is faster again (with the hub threshold and slices
+// below: 86.3 -> 66.9 ms, profiles/r06_ihave_mask_ab.txt)
 #ifndef GSIM_IH_WPE
-#define GSIM_IH_WPE 5
+#define GSIM_IH_WPE 4
 #endif
 #ifndef GSIM_IH_BATCH
 #define GSIM_IH_BATCH 4
@@ -1867,9 +1869,16 @@ constexpr int kIhBatch = GSIM_IH_BATCH;   // MM walks: slots whose cells one lan
 // block of one wave per (listed wave, slice) -- slice s of ns taking the
 // 64-edge chunks s, s + ns, ... of each row (blocks past ns exit at once)
 // (128: 38.3 + 63.6 ms at c5 -- many more listed waves -- against 256: 39.4 + 11.0
-// with 16 slices each, gpurun_out/r04c5h, r04c5i)
-constexpr uint32_t kIhHub = 256;
-constexpr int kIhSlices = 16;
+// with 16 slices each, gpurun_out/r04c5h, r04c5i); round 6, once a target's ask is
+// one mask load: 1024 and 8 slices (256 / 16: 86.3 ms, 512 / 8: 67.9, 1024 / 8: 66.9)
+#ifndef GSIM_IH_HUB
+#define GSIM_IH_HUB 1024
+#endif
+#ifndef GSIM_IH_SLICES
+#define GSIM_IH_SLICES 8
+#endif
+constexpr uint32_t kIhHub = GSIM_IH_HUB;
+constexpr int kIhSlices = GSIM_IH_SLICES;
 #ifdef GSIM_DIAG_IH
 // diagnostic build (counts and wave clocks only, results unchanged), per LP (1, 2):
 // [0] push row walks, [1] push edges, [2] their gossip targets, [3] pull row walks,
