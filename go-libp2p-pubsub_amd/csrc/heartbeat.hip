@@ -32,6 +32,7 @@ struct Extra {
     // of <= 16 connections, then <= 32, then the rest (nullptr: one class)
     uint32_t* d_rows = nullptr;
     int64_t n16 = 0, n32 = 0, n64 = 0;
+    int64_t n8 = 0;            // the first n8 rows of [0, n16) hold at most 8 connections (k_heartbeat<8>)
     // hub observers after them: rows of 65..256, 257..1024, then 1025..4096
     // connections (a block of 1024 threads holding 4 row positions each)
     int64_t nh256 = 0, nh1024 = 0, nh4096 = 0;
@@ -176,7 +177,9 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
 }
 
 // Minimum over the W-lane group `grp` (W = 32: lanes 0-31 or 32-63; W = 16:
-// one 16-lane DPP row).  The row shifts and the row_bcast:15 step read only
+// one 16-lane DPP row; W = 8: half a row -- after the row shifts by 1, 2 and 4,
+// lane 7 and lane 15 of a row hold its halves' minima, each read only through
+// lanes of its own half).  The row shifts and the row_bcast:15 step read only
 // lanes of the same group, so a group may run this while other groups of the
 // wave are inactive.
 template <int W>
@@ -185,11 +188,20 @@ __device__ __forceinline__ uint32_t group_min_u32(uint32_t v, int grp)
     if constexpr (W == 64) {
         return wave_min_u32(v);
     } else {
-        static_assert(W == 32 || W == 16, "groups of 16, 32 or 64 lanes");
+        static_assert(W == 32 || W == 16 || W == 8, "groups of 8, 16, 32 or 64 lanes");
         const int I = -1;
         v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x111, 0xF, 0xF, false));   // row_shr:1
         v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x112, 0xF, 0xF, false));   // row_shr:2
         v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x114, 0xF, 0xF, false));   // row_shr:4
+        if constexpr (W == 8) {
+            uint32_t r = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)v, 8 * q + 7);
+                if (grp == q) r = x;
+            }
+            return r;
+        }
         v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x118, 0xF, 0xF, false));   // row_shr:8
         if constexpr (W == 32) {
             v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(I, (int)v, 0x142, 0xA, 0xF, false));   // row_bcast:15
@@ -1201,7 +1213,10 @@ template <int W>
 #ifndef GSIM_HB_WPE16
 #define GSIM_HB_WPE16 4
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W == 16 ? GSIM_HB_WPE16 : GSIM_HB_WPE)))
+#ifndef GSIM_HB_W8
+#define GSIM_HB_W8 1       // rows of <= 8 connections in 8-lane groups (0: in the 16-lane class)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W <= 16 ? GSIM_HB_WPE16 : GSIM_HB_WPE)))
 void k_heartbeat(HbArgs a, const uint32_t* rows, int64_t nrows, int64_t obs_base)
 {
     constexpr int G = 64 / W;
@@ -2482,6 +2497,13 @@ int alloc_extra(gsim_handle* h)
         for (int c = 0; c < 2; ++c)
             std::stable_sort(cls[c].begin(), cls[c].end(), [&](uint32_t x, uint32_t y) { return sub[x] < sub[y]; });
     }
+    // rows of at most 8 connections first in their class, 8 observers per wavefront
+    // (a power law's many short rows idle half of a 16-lane group)
+    int64_t n8 = 0;
+    if (GSIM_HB_W8) {
+        n8 = std::stable_partition(cls[0].begin(), cls[0].end(),
+                                   [&](uint32_t x) { return rp[(size_t)x + 1] - rp[(size_t)x] <= 8; }) - cls[0].begin();
+    }
     // the hub classes by row length: the shorter half of a class's range runs
     // on a block of half the threads (a 1024-thread block idles most of its
     // lanes on a row of 300), and the 1025-4096 class's first nh2048 rows take
@@ -2496,6 +2518,7 @@ int alloc_extra(gsim_handle* h)
     h->x->nh512 = by_len(cls[4], 512);
     h->x->nh2048 = by_len(cls[5], 2048);
     h->x->max_degree = md;
+    h->x->n8 = n8;
     h->x->n16 = (int64_t)cls[0].size(); h->x->n32 = (int64_t)cls[1].size(); h->x->n64 = (int64_t)cls[2].size();
     h->x->nh256 = (int64_t)cls[3].size(); h->x->nh1024 = (int64_t)cls[4].size(); h->x->nh4096 = (int64_t)cls[5].size();
     h->x->nh8192 = (int64_t)cls[6].size();
@@ -2507,7 +2530,7 @@ int alloc_extra(gsim_handle* h)
         if (e != hipSuccess) return hip_check(h, e, "giant-row scratch");
         h->bytes_allocated += gb;
     }
-    if (md > 16 || !h->all_joined) {   // several classes, or an order by subscriptions: keep the lists
+    if (md > 16 || !h->all_joined || n8 > 0) {   // several classes, or an order by subscriptions: keep the lists
         std::vector<uint32_t> all;
         all.reserve((size_t)h->n);
         for (auto& c : cls) all.insert(all.end(), c.begin(), c.end());
@@ -2733,8 +2756,11 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
         hipLaunchKernelGGL(k_heartbeat<64>, dim3(grid_rows(nown)), dim3(256), 0, h->stream, a, nullptr, nown, h->olo());
     } else {
         const uint32_t* r = x->d_rows;
-        if (x->n16) hipLaunchKernelGGL(k_heartbeat<16>, dim3(grid_rows((x->n16 + 3) / 4)), dim3(256), 0, h->stream,
-                                       a, r, x->n16, (int64_t)0);
+        if (x->n8) hipLaunchKernelGGL(k_heartbeat<8>, dim3(grid_rows((x->n8 + 7) / 8)), dim3(256), 0, h->stream,
+                                      a, r, x->n8, (int64_t)0);
+        if (x->n16 > x->n8)
+            hipLaunchKernelGGL(k_heartbeat<16>, dim3(grid_rows((x->n16 - x->n8 + 3) / 4)), dim3(256), 0, h->stream,
+                               a, r + x->n8, x->n16 - x->n8, (int64_t)0);
         if (x->n32) hipLaunchKernelGGL(k_heartbeat<32>, dim3(grid_rows((x->n32 + 1) / 2)), dim3(256), 0, h->stream,
                                        a, r + x->n16, x->n32, (int64_t)0);
         if (x->n64) hipLaunchKernelGGL(k_heartbeat<64>, dim3(grid_rows(x->n64)), dim3(256), 0, h->stream,
