@@ -3549,7 +3549,9 @@ static int ihave_walk(gsim_handle* h, IhaveStage* st)
         const bool short_mean = h->e <= 24 * (int64_t)h->n;
         w = (h->max_degree <= 16 || (h->max_degree > 32 && short_mean)) ? 16 : h->max_degree <= 32 ? 32 : 64;
     }
-    if (w == 16)
+    if (w == 8)
+        launch_ihave_w<8>(h, st, a);
+    else if (w == 16)
         launch_ihave_w<16>(h, st, a);
     else if (w == 32)
         launch_ihave_w<32>(h, st, a);

@@ -1606,9 +1606,9 @@ int gsim_set_kernel_variant(gsim_handle* h, int32_t which, int32_t variant)
         if (variant != 3) { h->err = "unknown delivery kernel variant (3: topic-major)"; return GSIM_EINVAL; }
         return GSIM_OK;
     }
-    if (which == 3) {           // k_ihave lane group: 0 = by row lengths, else 16 / 32 / 64
-        if (variant != 0 && variant != 16 && variant != 32 && variant != 64) {
-            h->err = "unknown IHAVE lane width (0, 16, 32 or 64)";
+    if (which == 3) {           // k_ihave lane group: 0 = by row lengths, else 8 / 16 / 32 / 64
+        if (variant != 0 && variant != 8 && variant != 16 && variant != 32 && variant != 64) {
+            h->err = "unknown IHAVE lane width (0, 8, 16, 32 or 64)";
             return GSIM_EINVAL;
         }
         h->ihave_w = variant;

@@ -635,7 +635,7 @@ int gsim_profile_read(gsim_handle* h, double* ms, int64_t* launches, int32_t n);
  * one process.  Results are identical across variants (the GPU tests run
  * each).  which = 2: the delivery kernel; 3 (topic-major k_send_tm) is the
  * only one.  which = 3: the IHAVE walk's lane
- * group width (16, 32 or 64 lanes per row; 0 = chosen from the row lengths).
+ * group width (8, 16, 32 or 64 lanes per row; 0 = chosen from the row lengths).
  * which = 6: the topic-major kernel's blocks: 0 (default) shared out among
  * the topics by their subscribers, 1 the same number for every topic, >= 64
  * shared out by subscribers, this many in all. */

@@ -255,12 +255,14 @@ def test_c5_power_law_zipf_topics_churn(require_gpu, topic_slots):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("width", [16, 32, 64])
-def test_ihave_lane_widths_bit_exact(require_gpu, width):
-    """The IHAVE/IWANT walk (k_ihave) with 16-, 32- and 64-lane row groups on
-    one power-law graph (rows of 1-64 connections: a 16-lane group walks the
+@pytest.mark.parametrize("topic_slots", [0, 64])
+@pytest.mark.parametrize("width", [8, 16, 32, 64])
+def test_ihave_lane_widths_bit_exact(require_gpu, width, topic_slots):
+    """The IHAVE/IWANT walk (k_ihave) with 8-, 16-, 32- and 64-lane row groups on
+    one power-law graph (rows of 1-64 connections: a narrow group walks the
     long rows in chunks): every width is bit-exact against the oracle, so
-    all give the same promises, IWANT ids and responses."""
+    all give the same promises, IWANT ids and responses.  topic_slots 64:
+    sub-rings, the member-major walk with the window masks."""
     from fixtures import beacon_params, synthetic_state
     from gsim import graphs
     from gsim.engine import Engine
@@ -282,7 +284,7 @@ def test_ihave_lane_widths_bit_exact(require_gpu, width):
     eng.set_kernel_variant(3, width)
     ticks = list(range(1, 5))
     sched = subscribed_schedule(rng, ticks, net, T, 3.0, 0.02)
-    _, gs = run_parity(net, params, th, gp, st, ticks, sched, ring=512, eng=eng)
+    _, gs = run_parity(net, params, th, gp, st, ticks, sched, ring=512, eng=eng, topic_slots=topic_slots)
     assert gs["iwant_ids"] > 0 and (np.diff(net.row_ptr.astype(np.int64)) > 32).any()
 
 

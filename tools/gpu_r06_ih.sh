@@ -20,8 +20,9 @@ if [ -z "${NO_DIAG:-}" ]; then
   run_c5 "$ROOT/$L/libgsim_ihdiag.so" diag GSIM_DIAG_IH=1 || exit 1
   grep ihave_counts "$OUT/diag.err"
 fi
-for arm in ${ARMS:-}; do
-  lib="$ROOT/$L/libgsim_$arm.so"; [ "$arm" = head ] && lib="$ROOT/$L/libgsim.so"
-  run_c5 "$lib" "c5_$arm" || exit 1
+for arm in ${ARMS:-}; do          # an arm: a build name, or build:VAR=value (an environment setting)
+  b="${arm%%:*}"; ev=""; [ "$b" != "$arm" ] && ev="${arm#*:}"
+  lib="$ROOT/$L/libgsim_$b.so"; [ "$b" = head ] && lib="$ROOT/$L/libgsim.so"
+  run_c5 "$lib" "c5_${arm//[:=]/_}" "$ev" || exit 1
 done
 echo "== done"
