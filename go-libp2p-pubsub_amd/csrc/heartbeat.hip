@@ -20,6 +20,24 @@
 using namespace gsim;
 
 constexpr int kGiantRow = 8192;   // longest row the heartbeat takes (k_heartbeat_hub_g)
+// row positions per thread of the heartbeat's hub classes (below)
+#ifndef GSIM_HB_HUBV
+#define GSIM_HB_HUBV 2
+#endif
+// classes: rows of 65-128, -256, -512, -1024, -2048, -4096 connections; threads x
+// positions per thread cover the class's longest row.  Scheme 1: blocks as wide as
+// the row (2 and 4 positions from 1025); 2: two positions per thread up to 1024
+// connections; 3: four from 129 to 1024 (≈95 VGPRs per position: 380-410, one wave
+// per SIMD, no scratch; 512 x 4 and 512 x 8 would spill 157 / 1373, so the 1025-4096
+// classes keep 1024 threads)
+#define GSIM_HUB_SCHEME_(s1, s2, s3) (GSIM_HB_HUBV == 1 ? (s1) : GSIM_HB_HUBV == 2 ? (s2) : (s3))
+constexpr int kHubB[6] = {GSIM_HUB_SCHEME_(128, 64, 64), GSIM_HUB_SCHEME_(256, 128, 64), GSIM_HUB_SCHEME_(512, 256, 128),
+                          GSIM_HUB_SCHEME_(1024, 512, 256), 1024, 1024};
+constexpr int kHubVv[6] = {GSIM_HUB_SCHEME_(1, 2, 2), GSIM_HUB_SCHEME_(1, 2, 4), GSIM_HUB_SCHEME_(1, 2, 4),
+                           GSIM_HUB_SCHEME_(1, 2, 4), 2, 4};
+static_assert(kHubB[0] * kHubVv[0] == 128 && kHubB[1] * kHubVv[1] == 256 && kHubB[2] * kHubVv[2] == 512 &&
+              kHubB[3] * kHubVv[3] == 1024 && kHubB[4] * kHubVv[4] == 2048 && kHubB[5] * kHubVv[5] == 4096,
+              "a hub class's block covers its longest row");
 
 struct Extra {
     uint8_t* d_ctl = nullptr;   // [2][T][E] control inbox by round parity
@@ -2767,24 +2785,17 @@ int gsim_heartbeat(gsim_handle* h, uint64_t tick, int64_t now)
                                        a, r + x->n16 + x->n32, x->n64, (int64_t)0);
         // hubs: one block per observer
         const uint32_t* rh = r + x->n16 + x->n32 + x->n64;
-        if (x->nh128)
-            hipLaunchKernelGGL((k_heartbeat_hub<128, 1>), dim3((uint32_t)std::min<int64_t>(x->nh128, 65536)), dim3(128),
-                               0, h->stream, a, rh, x->nh128);
-        if (x->nh256 > x->nh128)
-            hipLaunchKernelGGL((k_heartbeat_hub<256, 1>), dim3((uint32_t)std::min<int64_t>(x->nh256 - x->nh128, 65536)),
-                               dim3(256), 0, h->stream, a, rh + x->nh128, x->nh256 - x->nh128);
-        if (x->nh512)
-            hipLaunchKernelGGL((k_heartbeat_hub<512, 1>), dim3((uint32_t)std::min<int64_t>(x->nh512, 65536)),
-                               dim3(512), 0, h->stream, a, rh + x->nh256, x->nh512);
-        if (x->nh1024 > x->nh512)
-            hipLaunchKernelGGL((k_heartbeat_hub<1024, 1>), dim3((uint32_t)std::min<int64_t>(x->nh1024 - x->nh512, 65536)),
-                               dim3(1024), 0, h->stream, a, rh + x->nh256 + x->nh512, x->nh1024 - x->nh512);
-        if (x->nh2048)   // 2 row positions per thread
-            hipLaunchKernelGGL((k_heartbeat_hub<1024, 2>), dim3((uint32_t)std::min<int64_t>(x->nh2048, 65536)),
-                               dim3(1024), 0, h->stream, a, rh + x->nh256 + x->nh1024, x->nh2048);
-        if (x->nh4096 > x->nh2048)   // 4 row positions per thread
-            hipLaunchKernelGGL((k_heartbeat_hub<1024, 4>), dim3((uint32_t)std::min<int64_t>(x->nh4096 - x->nh2048, 65536)),
-                               dim3(1024), 0, h->stream, a, rh + x->nh256 + x->nh1024 + x->nh2048, x->nh4096 - x->nh2048);
+        // one block per class row: (threads, row positions per thread) by class (kHub*)
+        auto hub = [&](auto kern, int bt, int64_t off, int64_t n) {
+            if (n > 0)
+                hipLaunchKernelGGL(kern, dim3((uint32_t)std::min<int64_t>(n, 65536)), dim3(bt), 0, h->stream, a, rh + off, n);
+        };
+        hub(k_heartbeat_hub<kHubB[0], kHubVv[0]>, kHubB[0], 0, x->nh128);
+        hub(k_heartbeat_hub<kHubB[1], kHubVv[1]>, kHubB[1], x->nh128, x->nh256 - x->nh128);
+        hub(k_heartbeat_hub<kHubB[2], kHubVv[2]>, kHubB[2], x->nh256, x->nh512);
+        hub(k_heartbeat_hub<kHubB[3], kHubVv[3]>, kHubB[3], x->nh256 + x->nh512, x->nh1024 - x->nh512);
+        hub(k_heartbeat_hub<kHubB[4], kHubVv[4]>, kHubB[4], x->nh256 + x->nh1024, x->nh2048);
+        hub(k_heartbeat_hub<kHubB[5], kHubVv[5]>, kHubB[5], x->nh256 + x->nh1024 + x->nh2048, x->nh4096 - x->nh2048);
         if (x->nh8192)   // 8 row positions per thread, group state in global scratch
             hipLaunchKernelGGL((k_heartbeat_hub_g<1024, kGiantRow / 1024>), dim3((uint32_t)x->gscratch_blocks), dim3(1024),
                                0, h->stream, a, rh + x->nh256 + x->nh1024 + x->nh4096, x->nh8192, x->d_gscratch);
