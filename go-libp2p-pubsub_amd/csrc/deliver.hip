@@ -2094,28 +2094,63 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
         // push slots of the block's topic, up to 64 at a time: a holder walks its
         // row once for all the slots it holds, and each peer it gossiped tb to
         // (and that is one of this shard's receivers, whose gate passes) is
-        // asked about each of them (the same triples as a walk per slot)
-        for (int k0 = 0; k0 < nact; k0 += 64) {
-            const int kn = nact - k0 < 64 ? nact - k0 : 64;
-            uint64_t hm = 0;
-            for (int q = 0; q < kn; ++q) {
-                const uint16_t sa = s_act[k0 + q];
-                if (!(sa & 0x8000)) continue;                // pulled below (wave-uniform)
-                const uint32_t m = sa & 0x7FFF;
-                if (msk) {
-                    if (vp && bit128(ih0, ih1, (int)m - m_lo)) hm |= 1ull << q;
-                    continue;
-                }
-                const uint64_t c = vp ? a.cs.cell[(int64_t)a.cs.cbase[m] + jw + lane] : kUnseen64;
-                if (vp && holds_in_window(c, a.g, a.lo_round, tick_round, a.minv[m] != 0, (uint32_t)pl == a.morigin[m],
-                                          LAT ? a.mlat[m] : 0u))
-                    hm |= 1ull << q;
+        // asked about each of them (the same triples as a walk per slot).
+        // With the window masks (msk) one pass takes every push slot, by
+        // sub-ring index: a target's asks are (held & push) & its unseen slots,
+        // one AND, and only the asked slots are visited.
+        uint64_t pk0 = 0, pk1 = 0;                          // msk: the push slots by sub-ring index
+        if (msk) {
+            for (int q = lane; q < nact; q += 64) {
+                const uint16_t sa = s_act[q];
+                if (!(sa & 0x8000)) continue;
+                const int k = (int)(sa & 0x7FFF) - m_lo;
+                if (k < 64) pk0 |= 1ull << k; else pk1 |= 1ull << (k - 64);
             }
-            const uint64_t mask = __ballot(hm != 0);
+            for (int o = 32; o; o >>= 1) {
+                pk0 |= (uint64_t)__shfl_xor((long long)pk0, o, 64);
+                pk1 |= (uint64_t)__shfl_xor((long long)pk1, o, 64);
+            }
+        }
+        for (int k0 = 0; k0 < nact; k0 += msk ? nact : 64) {
+            const int kn = nact - k0 < 64 ? nact - k0 : 64;
+            uint64_t hm = 0, hm1 = 0;                        // msk: words 0 / 1 by sub-ring index
+            if (msk) {
+                if (vp) { hm = ih0 & pk0; hm1 = ih1 & pk1; }
+            } else {
+                for (int q = 0; q < kn; ++q) {
+                    const uint16_t sa = s_act[k0 + q];
+                    if (!(sa & 0x8000)) continue;                // pulled below (wave-uniform)
+                    const uint32_t m = sa & 0x7FFF;
+                    const uint64_t c = vp ? a.cs.cell[(int64_t)a.cs.cbase[m] + jw + lane] : kUnseen64;
+                    if (vp && holds_in_window(c, a.g, a.lo_round, tick_round, a.minv[m] != 0, (uint32_t)pl == a.morigin[m],
+                                              LAT ? a.mlat[m] : 0u))
+                        hm |= 1ull << q;
+                }
+            }
+            const uint64_t mask = __ballot((hm | hm1) != 0);
             if (!mask) continue;
             const int32_t t = tb;
+            // one IWANT id: p (global pg) asks holder me_id over edge e for slot m
+            auto ask_one = [&](bool req, uint32_t m, uint32_t p, uint32_t pg, uint32_t re, uint32_t e, uint32_t me_id,
+                               uint32_t me_g, bool ign_s) {
+                bool resp = false;
+                if (req) {
+                    if (a.tr.ev) trace_iwant(a, p, me_id, m);
+                    const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, pg, 0, P_PROMISE, m, me_g);
+                    atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[re]), (unsigned long long)key);
+                    resp = a.respond && a.gstate[e] && !ign_s && peertx_allows(a, m, e, me_id);
+                }
+                n_req += req;
+                n_resp += resp;
+                const uint64_t sb = __ballot(resp);
+                if (sb) {
+                    if (nstage + __popcll(sb) > kRespStage) flush_stage();
+                    if (resp) stage[nstage + __popcll(sb & ((1ull << lane) - 1))] = (uint64_t)e | ((uint64_t)m << 32);
+                    nstage += __popcll(sb);
+                }
+            };
             auto hchunk = [&](uint32_t off, uint32_t gl_, uint32_t beg, uint32_t deg, uint32_t me_id, uint32_t me_g,
-                              bool ign_s, int64_t me_pl, uint64_t hmw) {
+                              bool ign_s, int64_t me_pl, uint64_t hmw, uint64_t hmw1) {
                 const bool v = off + gl_ < deg;
                 const uint32_t e = beg + off + gl_;
                 uint32_t p = 0, re = 0;
@@ -2127,16 +2162,27 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                     IH_D(d_ph++;)
                 }
                 IH_D(d_pe += v;)
+                const uint32_t pg = gs ? (a.gid ? a.gid[p] : p) : 0u;
+                const int64_t poff = gs ? a.cs.at(0, t, p) : -1;    // p's cell in every slot of tb
+                if (msk) {
+                    // the slots p is asked for: held by me_id, pushed, unseen by p
+                    uint64_t r0 = 0, r1 = 0;
+                    if (poff >= 0) {
+                        const uint64_t* o = a.ihm + (a.mmb[t] + poff) * 4 + 2;
+                        r0 = hmw & o[0];
+                        r1 = hmw1 & o[1];
+                    }
+                    while (__ballot((r0 | r1) != 0)) {
+                        int k = -1;
+                        if (r0) { k = __builtin_ctzll(r0); r0 &= r0 - 1; }
+                        else if (r1) { k = 64 + __builtin_ctzll(r1); r1 &= r1 - 1; }
+                        ask_one(k >= 0, (uint32_t)(m_lo + (k < 0 ? 0 : k)), p, pg, re, e, me_id, me_g, ign_s);
+                    }
+                    return;
+                }
                 const uint64_t mine = gs ? hmw : 0ull;
                 uint64_t uw = mine;
                 for (int o = 32; o; o >>= 1) uw |= (uint64_t)__shfl_xor((long long)uw, o, 64);
-                const uint32_t pg = gs ? (a.gid ? a.gid[p] : p) : 0u;
-                const int64_t poff = gs ? a.cs.at(0, t, p) : -1;    // p's cell in every slot of tb
-                uint64_t pu0 = 0, pu1 = 0;                          // ... or its unseen window slots
-                if (msk && poff >= 0) {
-                    const uint64_t* o = a.ihm + (a.mmb[t] + poff) * 4 + 2;
-                    pu0 = o[0]; pu1 = o[1];
-                }
                 while (uw) {
                   // kIhBatch slots' cells in flight at once (nothing here writes a cell)
                   int qb[kIhBatch];
@@ -2147,34 +2193,13 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                       qb[b] = uw ? __builtin_ctzll(uw) : -1;
                       if (uw) uw &= uw - 1;
                       ask[b] = qb[b] >= 0 && ((mine >> qb[b]) & 1ull) && poff >= 0;
-                      const uint32_t mb = ask[b] ? s_act[k0 + qb[b]] & 0x7FFF : 0u;
-                      cvb[b] = !ask[b] ? 0ull
-                             : msk ? (bit128(pu0, pu1, (int)mb - m_lo) ? kUnseen64 : 0ull)
-                                   : a.cs.cell[(int64_t)a.cs.cbase[mb] + poff];
+                      cvb[b] = ask[b] ? a.cs.cell[(int64_t)a.cs.cbase[s_act[k0 + qb[b]] & 0x7FFF] + poff] : 0ull;
                   }
 #pragma unroll
                   for (int b = 0; b < kIhBatch; ++b) {
                     const int q = qb[b];
                     if (q < 0) break;                                // wave-uniform
-                    const uint32_t m = s_act[k0 + q] & 0x7FFF;
-                    bool req = false, resp = false;
-                    if (ask[b]) {
-                        req = cvb[b] == kUnseen64;                   // p has not seen m
-                        if (req) {
-                            if (a.tr.ev) trace_iwant(a, p, me_id, m);
-                            const uint64_t key = pair_key(a.seed, (uint32_t)a.tick, pg, 0, P_PROMISE, m, me_g);
-                            atomicMin(reinterpret_cast<unsigned long long*>(&a.pcand[re]), (unsigned long long)key);
-                            resp = a.respond && a.gstate[e] && !ign_s && peertx_allows(a, m, e, me_id);
-                        }
-                    }
-                    n_req += req;
-                    n_resp += resp;
-                    const uint64_t sb = __ballot(resp);
-                    if (sb) {
-                        if (nstage + __popcll(sb) > kRespStage) flush_stage();
-                        if (resp) stage[nstage + __popcll(sb & ((1ull << lane) - 1))] = (uint64_t)e | ((uint64_t)m << 32);
-                        nstage += __popcll(sb);
-                    }
+                    ask_one(ask[b] && cvb[b] == kUnseen64, s_act[k0 + q] & 0x7FFF, p, pg, re, e, me_id, me_g, ign_s);
                   }
                 }
             };
@@ -2190,6 +2215,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 const bool ign_s = __shfl(ign_l, sl, 64);
                 const uint32_t me_id = (uint32_t)__shfl((int)pl, sl, 64);
                 const uint64_t hmw = bs < 0 ? 0ull : (uint64_t)__shfl((long long)hm, sl, 64);
+                const uint64_t hmw1 = bs < 0 ? 0ull : (uint64_t)__shfl((long long)hm1, sl, 64);
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
                 const uint64_t me_m = smask_of(a.smask, me_id);
                 const int64_t me_pl = slot_has(me_m, t) ? slot_idx(me_m, t, a.E, 0) : -1;
@@ -2197,7 +2223,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 IH_D(d_pw += (gl == 0 && bs >= 0);)
                 const uint32_t deg = bs >= 0 ? end - beg : 0u;
                 for (uint32_t off = 0; __ballot(off < deg) != 0; off += W)
-                    hchunk(off, (uint32_t)gl, beg, deg, me_id, me_g, ign_s, me_pl, hmw);
+                    hchunk(off, (uint32_t)gl, beg, deg, me_id, me_g, ign_s, me_pl, hmw, hmw1);
             }
             for (uint64_t lm = longm; lm; lm &= lm - 1) {
                 const int bs = __builtin_ctzll(lm);
@@ -2205,13 +2231,14 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 const bool ign_s = __shfl(ign_l, bs, 64);
                 const uint32_t me_id = (uint32_t)__shfl((int)pl, bs, 64);
                 const uint64_t hmw = (uint64_t)__shfl((long long)hm, bs, 64);
+                const uint64_t hmw1 = (uint64_t)__shfl((long long)hm1, bs, 64);
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
                 const uint64_t me_m = smask_of(a.smask, me_id);
                 const int64_t me_pl = slot_has(me_m, t) ? slot_idx(me_m, t, a.E, 0) : -1;
                 n_walk += (lane == 0 && slice == 0);
                 IH_D(d_pw += (lane == 0 && slice == 0);)
                 for (uint32_t off = slice * 64; off < end - beg; off += 64 * nsl)
-                    hchunk(off, (uint32_t)lane, beg, end - beg, me_id, me_g, ign_s, me_pl, hmw);
+                    hchunk(off, (uint32_t)lane, beg, end - beg, me_id, me_g, ign_s, me_pl, hmw, hmw1);
             }
         }
         // pull slots of the block's topic, up to 64 at a time: a receiver walks
