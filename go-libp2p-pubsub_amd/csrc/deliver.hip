@@ -1787,6 +1787,10 @@ __global__ __launch_bounds__(256) void k_gossip_count(IhArgs a, uint32_t* gcount
 // cells in each of the topic's slots are consecutive; only the topic's own
 // sub-ring is scanned.  Counts are the same as k_gossip_count's: a peer
 // without a cell neither holds nor wants.
+#ifndef GSIM_COUNT_BATCH
+#define GSIM_COUNT_BATCH 4
+#endif
+constexpr int kCountBatch = GSIM_COUNT_BATCH;    // window slots whose cells one lane loads at once
 template <bool LAT>
 __global__ __launch_bounds__(256) void k_gossip_count_mm(IhArgs a, const uint32_t* mctab, uint32_t* gcount)
 {
@@ -1826,10 +1830,18 @@ __global__ __launch_bounds__(256) void k_gossip_count_mm(IhArgs a, const uint32_
         const uint32_t p = vp ? member_peer(a, t, j) : 0u;
         const bool subp = vp && ((a.sub[p] >> t) & 1ull) && p >= a.rlo && p < a.rhi;
         uint64_t hw0 = 0, hw1 = 0, uw0 = 0, uw1 = 0;       // the member's held / unseen window slots
-        for (int q = 0; q < ns; ++q) {
+        for (int q0 = 0; q0 < ns; q0 += kCountBatch) {
+          uint64_t cb[kCountBatch];                         // the batch's cells in flight together
+#pragma unroll
+          for (int b = 0; b < kCountBatch; ++b)
+              cb[b] = (vp && q0 + b < ns) ? a.cs.cell[(int64_t)a.cs.cbase[m_lo + s_slot[q0 + b]] + j] : kUnseen64;
+#pragma unroll
+          for (int b = 0; b < kCountBatch; ++b) {
+            const int q = q0 + b;
+            if (q >= ns) break;                                // block-uniform
             const int k = s_slot[q];
             const uint32_t m = (uint32_t)(m_lo + k);
-            const uint64_t c = vp ? a.cs.cell[(int64_t)a.cs.cbase[m] + j] : kUnseen64;
+            const uint64_t c = cb[b];
             const bool hold = vp && holds_in_window(c, a.g, a.lo_round, tick_round, a.minv[m] != 0, p == a.morigin[m],
                                                     LAT ? a.mlat[m] : 0u);
             const bool want = subp && c == kUnseen64;
@@ -1839,6 +1851,7 @@ __global__ __launch_bounds__(256) void k_gossip_count_mm(IhArgs a, const uint32_
             const int nh = __popcll(__ballot(hold)), nw = __popcll(__ballot(want));
             if (lane == 0 && nh) atomicAdd(&s_c[k], (uint32_t)nh);
             if (lane == 0 && nw) atomicAdd(&s_c[R + k], (uint32_t)nw);
+          }
         }
         if (a.ihm && vp) {
             uint64_t* o = a.ihm + (a.mmb[t] + j) * 4;
