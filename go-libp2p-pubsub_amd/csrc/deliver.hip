@@ -769,6 +769,7 @@ __global__ __launch_bounds__(256) void k_mesh_mask(const uint32_t* row_ptr, cons
 // [rlo, rhi) that carry the router's mesh bit or are direct peers, in row
 // order, one wave per hub (ballots over 64-position chunks).  More than
 // kHubMesh such edges: count ~0, the hub walks its whole row for t.
+constexpr int kHubBatch = 4;     // k_hub_mesh: topics whose flags a lane loads at once
 __global__ __launch_bounds__(256) void k_hub_mesh(const uint32_t* row_ptr, const uint32_t* col, const uint8_t* mflags,
                                                   const uint8_t* direct, const uint64_t* smask, const uint32_t* hrow,
                                                   int64_t nhub, int64_t E, int32_t T, uint32_t rlo, uint32_t rhi,
@@ -779,30 +780,45 @@ __global__ __launch_bounds__(256) void k_hub_mesh(const uint32_t* row_ptr, const
         const uint32_t x = hrow[hx];
         const uint32_t b = row_ptr[x], d = row_ptr[x + 1] - b;
         const uint64_t m = smask_of(smask, x);
-        for (int32_t t = 0; t < T; ++t) {
-            uint32_t* L = hlist + ((int64_t)hx * T + t) * (1 + kHubMesh);
-            if (!slot_has(m, t)) {
-                if (lane == 0) L[0] = 0;
-                continue;
-            }
-            uint32_t cnt = 0;
-            for (uint32_t off = 0; off < d; off += 64) {
-                const uint32_t e = b + off + (uint32_t)lane;
-                bool me = false;
-                if (off + (uint32_t)lane < d) {
-                    const uint32_t i = col[e];
-                    if (i >= rlo && i < rhi)
-                        me = (direct && direct[e]) || (mflags[slot_idx(m, t, E, e)] & GSIM_TF_MESH);
+        uint32_t* const L0 = hlist + (int64_t)hx * T * (1 + kHubMesh);
+        for (int32_t t = lane; t < T; t += 64)
+            if (!slot_has(m, t)) L0[(int64_t)t * (1 + kHubMesh)] = 0;
+        // the row is walked once for every topic the hub holds: a chunk's ends
+        // and direct flags are loaded once, its topics' flags kHubBatch at a time;
+        // lane t keeps topic t's count
+        uint32_t cnt = 0;
+        for (uint32_t off = 0; off < d; off += 64) {
+            const uint32_t e = b + off + (uint32_t)lane;
+            const bool v = off + (uint32_t)lane < d;
+            const uint32_t i = v ? col[e] : 0u;
+            const bool own = v && i >= rlo && i < rhi;
+            const bool dr = own && direct && direct[e];
+            for (uint64_t mm = m; mm;) {
+                int tb[kHubBatch];
+                uint8_t fb[kHubBatch];
+#pragma unroll
+                for (int q = 0; q < kHubBatch; ++q) {
+                    tb[q] = mm ? __builtin_ctzll(mm) : -1;
+                    if (mm) mm &= mm - 1;
+                    fb[q] = (tb[q] >= 0 && own && !dr) ? mflags[slot_idx(m, tb[q], E, e)] : (uint8_t)0;
                 }
-                const uint64_t bal = __ballot(me);
-                if (me) {
-                    const uint32_t pos = cnt + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
-                    if (pos < (uint32_t)kHubMesh) L[1 + pos] = e;
+#pragma unroll
+                for (int q = 0; q < kHubBatch; ++q) {
+                    const int t = tb[q];
+                    if (t < 0) break;                                    // wave-uniform
+                    const bool me = dr || (fb[q] & GSIM_TF_MESH);
+                    const uint64_t bal = __ballot(me);
+                    const uint32_t base = (uint32_t)__shfl((int)cnt, t, 64);
+                    if (me) {
+                        const uint32_t pos = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+                        if (pos < (uint32_t)kHubMesh) L0[(int64_t)t * (1 + kHubMesh) + 1 + pos] = e;
+                    }
+                    if (lane == t) cnt += (uint32_t)__popcll(bal);
                 }
-                cnt += (uint32_t)__popcll(bal);
             }
-            if (lane == 0) L[0] = cnt <= (uint32_t)kHubMesh ? cnt : 0xFFFFFFFFu;
         }
+        if (lane < T && slot_has(m, lane))
+            L0[(int64_t)lane * (1 + kHubMesh)] = cnt <= (uint32_t)kHubMesh ? cnt : 0xFFFFFFFFu;
     }
 }
 
