@@ -102,7 +102,7 @@ struct HbArgs {
     uint8_t* tflags;    // score bits (inMesh, active), record order [T][E]
     int64_t* backoff;
     double *meshd, *fail, *bp;
-    const uint8_t* mcnt;
+    uint8_t* mcnt;             // pending meshd increments (k_churn_apply applies the ones it reads)
     int64_t *graft, *mtime;
     int32_t mt_lazy;    // lazy meshTime since the refresh at mt_R (lazy_mtime)
     int64_t mt_R;
@@ -1231,6 +1231,9 @@ template <int W>
 #ifndef GSIM_HB_WPE16
 #define GSIM_HB_WPE16 4
 #endif
+#ifndef GSIM_CHURN_MCNT
+#define GSIM_CHURN_MCNT 1  // churn applies the pending meshd increments of the records it touches
+#endif
 #ifndef GSIM_HB_W8
 #define GSIM_HB_W8 1       // rows of <= 8 connections in 8-lane groups (0: in the 16-lane class)
 #endif
@@ -2294,6 +2297,7 @@ __device__ void churn_reset_record(const HbArgs& a, const ChurnArgs& c, uint32_t
         c.first[i] = 0.0; a.meshd[i] = 0.0; a.fail[i] = 0.0; c.invalid[i] = 0.0;
         a.graft[i] = 0; a.mtime[i] = 0;
         a.tflags[i] = 0;
+        if (GSIM_CHURN_MCNT) a.mcnt[i] = 0;       // pending deliveries of the dropped record
     }
 }
 
@@ -2349,8 +2353,19 @@ __global__ __launch_bounds__(256) void k_churn_apply(HbArgs a, ChurnArgs c)
         c.first[i] = 0.0;
         const uint8_t fl = a.tflags[i];
         const double thr = tp->mesh_message_deliveries_threshold;
-        if ((fl & GSIM_TF_IN_MESH) && (fl & GSIM_TF_ACTIVE) && a.meshd[i] < thr) {
-            const double deficit = thr - a.meshd[i];
+        double md = a.meshd[i];
+        if (GSIM_CHURN_MCNT) {
+            // the record's pending deliveries are part of the counter (RemovePeer's P3b
+            // reads it): applied here, not by a pass over every record first
+            const uint8_t pc = a.mcnt[i];
+            if (pc) {
+                md = apply_incs(md, pc, tp->mesh_message_deliveries_cap);
+                a.meshd[i] = md;
+                a.mcnt[i] = 0;
+            }
+        }
+        if ((fl & GSIM_TF_IN_MESH) && (fl & GSIM_TF_ACTIVE) && md < thr) {
+            const double deficit = thr - md;
             a.fail[i] = a.fail[i] + deficit * deficit;
         }
         if (fl & GSIM_TF_IN_MESH) a.mtime[i] = 0;   // meshTime outside the mesh is 0
@@ -2964,7 +2979,9 @@ int gsim_set_connections(gsim_handle* h, const uint32_t* pairs, int32_t count, i
         return GSIM_EINVAL;
     }
     int rc = deliver_flush(h);              // pending first deliveries precede the removal
-    if (!rc) rc = materialize_mcnt(h);      // the P3b test reads meshMessageDeliveries
+    // the P3b test reads meshMessageDeliveries: k_churn_apply applies the pending
+    // increments of the records it removes (GSIM_CHURN_MCNT), else a pass over all
+    if (!rc && !GSIM_CHURN_MCNT) rc = materialize_mcnt(h);
     // RemovePeer scores the peer live (score.go:611-644): P6 over the tracked
     // set as it is now (an up batch since the last derivation changed it)
     if (!rc && !up && h->p6_dirty) rc = launch_ip_colocation(h);
@@ -3105,7 +3122,7 @@ int gsim_px_connect(gsim_handle* h, int64_t now, uint32_t* pairs, int64_t cap, i
         for (size_t q = 0; q < n && (int64_t)q < cap; ++q) { pairs[2 * q] = pr[q].first; pairs[2 * q + 1] = pr[q].second; }
     }
     int rc = deliver_flush(h);                    // as gsim_set_connections
-    if (!rc) rc = materialize_mcnt(h);
+    if (!rc && !GSIM_CHURN_MCNT) rc = materialize_mcnt(h);
     if (rc) return rc;
     ProfScope ps(h, GSIM_K_CHURN);
     hipLaunchKernelGGL(k_px_outbound, dim3((n + 255) / 256), dim3(256), 0, h->stream, (const uint32_t*)pxc, n,
