@@ -291,6 +291,7 @@ struct RoundArgs {
     int32_t ptx_w;
     TraceRef tr;                   // gsim_trace_config
     uint64_t* clist;               // claim list (Deliver::d_clist; nullptr: commits scan the words)
+    int32_t cl_j;                  // entries carry the cell's member offset (cl_pack), else peer | slot << 32
     uint32_t* clist_n;
     int64_t clist_cap;
     int64_t ncells;                // cells of the seen-set (the last slot's end)
@@ -476,6 +477,17 @@ __device__ __forceinline__ uint64_t vq_entry(uint32_t e, int32_t t, uint32_t kin
 
 // Append the lanes' new claims (receiver | slot << 32) to the block's claim
 // sub-list, one atomic per wave; every lane of the wave calls it.
+// A claim-list entry.  Packed (RoundArgs::cl_j, peers < 2^24): peer i (24 bits), slot m
+// (13), the claimed cell's offset in the slot (27): the commit finds the cell from
+// cbase[m] alone, not through the member tables (one random trip less per claim).
+#ifndef GSIM_CL_PACK
+#define GSIM_CL_PACK 1
+#endif
+constexpr uint32_t kClPeerMax = 1u << 24;
+__device__ __forceinline__ uint64_t cl_entry(const RoundArgs& a, uint32_t i, uint32_t m, int64_t ci, int64_t cb)
+{
+    return a.cl_j ? (uint64_t)i | ((uint64_t)m << 24) | ((uint64_t)(ci - cb) << 37) : (uint64_t)i | ((uint64_t)m << 32);
+}
 __device__ __forceinline__ void clist_push_wave(const RoundArgs& a, bool on, uint64_t v)
 {
     const uint64_t b = __ballot(on);
@@ -1368,7 +1380,7 @@ void k_send_tm(RoundArgs a_)
                                     clm |= 1ull << k;
                                     if constexpr (SP && !LAT) {
                                         clw |= 1u << u;
-                                        s_cl[u * kTmThreads + tid] = (uint64_t)i | ((uint64_t)m << 32);
+                                        s_cl[u * kTmThreads + tid] = cl_entry(a, i, m, ci, (int64_t)s_cb[k]);
                                     }
                                 }
                             }
@@ -1579,8 +1591,10 @@ __global__ __launch_bounds__(256) void k_commit_list(RoundArgs a)
         uint64_t fv = 0;
         if (k < n) {
             const uint64_t v = a.clist[(int64_t)q * a.clist_cap + k];
-            const uint32_t i = (uint32_t)v, m = (uint32_t)(v >> 32);
-            const int64_t ci = SP ? a.cs.idx(m, (int32_t)a.mtopic[m], i) : (int64_t)m * a.cs.n + i;
+            const uint32_t i = a.cl_j ? (uint32_t)(v & (kClPeerMax - 1)) : (uint32_t)v;
+            const uint32_t m = a.cl_j ? (uint32_t)((v >> 24) & 0x1FFFu) : (uint32_t)(v >> 32);
+            const int64_t ci = a.cl_j ? (int64_t)a.cs.cbase[m] + (int64_t)(v >> 37)
+                             : SP ? a.cs.idx(m, (int32_t)a.mtopic[m], i) : (int64_t)m * a.cs.n + i;
             uint64_t* cp = ci >= 0 ? a.cs.cell + ci : nullptr;
             const uint64_t c = cp ? *cp : kUnseen64;
             if (cp && is_claim_of(c, par)) {
@@ -2727,7 +2741,8 @@ __device__ __forceinline__ void listed_copy(const RoundArgs& a, uint32_t r, uint
             if (a.clist) {
                 const uint32_t sq = blockIdx.x % kClSub;
                 const uint32_t q = atomicAdd(&a.clist_n[sq * kClStride], 1u);
-                if ((int64_t)q < a.clist_cap) a.clist[(int64_t)sq * a.clist_cap + q] = (uint64_t)p | ((uint64_t)m << 32);
+                if ((int64_t)q < a.clist_cap)
+                    a.clist[(int64_t)sq * a.clist_cap + q] = cl_entry(a, p, m, cellp - a.cs.cell, (int64_t)a.cs.cbase[m]);
                 else atomicOr(&a.clist_n[kClSub * kClStride], 1u);
             }
         }
@@ -2947,7 +2962,7 @@ __global__ __launch_bounds__(kLsB) void k_send_list(RoundArgs a_)
                         n_first++;
                         atomicOr(&s_new2[m >> 5], 1u << (m & 31));
                         clw |= 1u << u;
-                        s_cl[u * kLsB + tid] = (uint64_t)i | ((uint64_t)m << 32);
+                        s_cl[u * kLsB + tid] = cl_entry(a, i, m, ci, (int64_t)a.cs.cbase[m]);
                     }
                 }
                 if (!sc) continue;
@@ -3353,6 +3368,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
         a.clist = d->d_clist;
         a.clist_n = d->d_clist_n;
         a.clist_cap = d->clist_cap;
+        a.cl_j = GSIM_CL_PACK && h->n < (int64_t)kClPeerMax && d->cfg.ring <= kMaxRing ? 1 : 0;
     }
     if (flist_allowed(h)) {
         a.flist = d->d_flist;
