@@ -292,6 +292,7 @@ struct RoundArgs {
     TraceRef tr;                   // gsim_trace_config
     uint64_t* clist;               // claim list (Deliver::d_clist; nullptr: commits scan the words)
     int32_t cl_j;                  // entries carry the cell's member offset (cl_pack), else peer | slot << 32
+    int32_t fl_from;               // forwarder entries carry the first sender (fl_entry), else peer | slot << 32
     uint32_t* clist_n;
     int64_t clist_cap;
     int64_t ncells;                // cells of the seen-set (the last slot's end)
@@ -536,6 +537,30 @@ __device__ __forceinline__ void fresh_set(const RoundArgs& a, uint32_t m, int64_
 constexpr int kFstStride = 32;
 constexpr int kFstBad = 2 * kFstStride;
 constexpr uint64_t kFlOrigin = 1ull << 63;
+// A forwarder entry.  Packed (RoundArgs::fl_from, peers < 2^24 - 1): forwarder x (24
+// bits), slot m (13), its first sender (24; kFlNone: none), origin flag (bit 63): the
+// send reads the sender from the entry, not from the forwarder's committed cell
+// (the member tables, then the cell: two random trips per forwarder).
+#ifndef GSIM_FL_PACK
+#define GSIM_FL_PACK 1
+#endif
+constexpr uint32_t kFlNone = (1u << 24) - 1u;
+__device__ __forceinline__ uint64_t fl_entry(const RoundArgs& a, uint32_t x, uint32_t m, uint32_t from)
+{
+    if (!a.fl_from) return (uint64_t)x | ((uint64_t)m << 32);
+    const uint32_t f = from < kFlNone ? from : kFlNone;
+    return (uint64_t)x | ((uint64_t)m << 24) | ((uint64_t)f << 37);
+}
+__device__ __forceinline__ uint32_t fl_x(const RoundArgs& a, uint64_t v) { return a.fl_from ? (uint32_t)(v & kFlNone) : (uint32_t)v; }
+__device__ __forceinline__ uint32_t fl_m(const RoundArgs& a, uint64_t v)
+{
+    return a.fl_from ? (uint32_t)((v >> 24) & 0x1FFFu) : (uint32_t)(v >> 32) & 0x7FFFFFFFu;
+}
+__device__ __forceinline__ uint32_t fl_from_of(uint64_t v)
+{
+    const uint32_t f = (uint32_t)((v >> 37) & kFlNone);
+    return f == kFlNone ? kPeerMask : f;
+}
 
 // Append the lanes' forwarders (on, peer | slot << 32) of send round g to its
 // list; every lane of the wave calls it.  An entry that does not fit marks
@@ -556,7 +581,7 @@ __device__ __forceinline__ void flist_push_wave(const RoundArgs& a, int64_t g, b
             a.flist[(int64_t)p * a.flist_cap + k] = v;
         } else {
             a.fst[kFstBad + p] = 1;
-            const uint32_t x = (uint32_t)v, m = (uint32_t)(v >> 32) & 0x7FFFFFFFu;
+            const uint32_t x = fl_x(a, v), m = fl_m(a, v);
             fresh_set(a, m, (int64_t)(x >> 6), 1ull << (x & 63));
         }
     }
@@ -724,7 +749,7 @@ __global__ void k_publish(RoundArgs a, const gsim_msg* pub, const uint32_t* pslo
             if (a.flist) {                                 // ... and in round g+1's forwarder list
                 const int pp = (int)((a.g + 1) & 1);
                 const uint32_t q = atomicAdd(&a.fst[pp * kFstStride], 1u);
-                if ((int64_t)q < a.flist_cap) a.flist[(int64_t)pp * a.flist_cap + q] = (uint64_t)oc | ((uint64_t)slot << 32) | kFlOrigin;
+                if ((int64_t)q < a.flist_cap) a.flist[(int64_t)pp * a.flist_cap + q] = fl_entry(a, oc, slot, oc) | kFlOrigin;
                 else a.fst[kFstBad + pp] = 1;
             }
         }
@@ -1602,7 +1627,7 @@ __global__ __launch_bounds__(256) void k_commit_list(RoundArgs a)
                 const uint64_t bit = 1ull << (i & 63);
                 atomicOr(reinterpret_cast<unsigned long long*>(a.seenbm + (int64_t)m * a.nw + w), bit);
                 if (a.fresh && a.minv[m] == GSIM_VERDICT_ACCEPT) {
-                    if (a.flist_commit) { fw = true; fv = (uint64_t)i | ((uint64_t)m << 32); }   // round g+1's list
+                    if (a.flist_commit) { fw = true; fv = fl_entry(a, i, m, (uint32_t)c & kPeerMask); }   // round g+1's list
                     // (a shard's holder accumulation reads the fresh bits before the send)
                     if (!a.flist_commit || a.sharded) fresh_set(a, m, w, bit);
                 }
@@ -2807,16 +2832,20 @@ __global__ __launch_bounds__(kLsB) void k_send_list(RoundArgs a_)
         uint64_t msk = 0;
         if (c0 + tid < n) {
             const uint64_t v = fl[c0 + tid];
-            x = (uint32_t)v;
-            m = (uint32_t)(v >> 32) & 0x7FFFFFFFu;
+            x = fl_x(a, v);
+            m = fl_m(a, v);
             const int32_t t = (int32_t)a.mtopic[m];
             const uint32_t origin = a.morigin[m];
             // the origin's fresh bit (k_publish) is taken here; on shards every
             // entry's (the commit also set them, for the holder accumulation)
             if ((v & kFlOrigin) || a.sharded)
                 atomicAnd(reinterpret_cast<unsigned long long*>(a.fresh + (int64_t)m * a.nw + (x >> 6)), ~(1ull << (x & 63)));
-            const int64_t xc = a.cs.at((int64_t)a.cs.cbase[m], t, x);
-            from = xc >= 0 ? (uint32_t)a.cs.cell[xc] & kPeerMask : kPeerMask;
+            if (a.fl_from) {
+                from = fl_from_of(v);
+            } else {
+                const int64_t xc = a.cs.at((int64_t)a.cs.cbase[m], t, x);
+                from = xc >= 0 ? (uint32_t)a.cs.cell[xc] & kPeerMask : kPeerMask;
+            }
             const uint64_t xm = smask_of(a.smask, x);
             pl = (uint32_t)__popcll(xm & ((1ull << t) - 1ull));
             const uint32_t rb = a.row_ptr[x], deg = a.row_ptr[x + 1] - rb;
@@ -3019,7 +3048,7 @@ __global__ __launch_bounds__(256) void k_flist_fresh(RoundArgs a, int only_bad)
     const uint64_t* fl = a.flist + (int64_t)par * a.flist_cap;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t v = fl[k];
-        const uint32_t x = (uint32_t)v, m = (uint32_t)(v >> 32) & 0x7FFFFFFFu;
+        const uint32_t x = fl_x(a, v), m = fl_m(a, v);
         fresh_set(a, m, (int64_t)(x >> 6), 1ull << (x & 63));
     }
 }
@@ -3374,6 +3403,7 @@ static RoundArgs make_round_args(gsim_handle* h, int64_t g)
         a.flist = d->d_flist;
         a.fst = d->d_fst;
         a.flist_cap = d->flist_cap;
+        a.fl_from = GSIM_FL_PACK && h->n < (int64_t)kFlNone && d->cfg.ring <= kMaxRing ? 1 : 0;
     }
     const size_t w = (size_t)nnew_words(d);
     a.nnew_prev = d->d_nnew + (size_t)((g + 1) & 1) * w;
