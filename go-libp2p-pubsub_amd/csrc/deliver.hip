@@ -2166,6 +2166,12 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
         // With the window masks (msk) one pass takes every push slot, by
         // sub-ring index: a target's asks are (held & push) & its unseen slots,
         // one AND, and only the asked slots are visited.
+        // each lane's member's plane of tb (its gossip choices), shuffled to the walking group
+        int64_t own_pl = -1;
+        if (vp) {
+            const uint64_t om = smask_of(a.smask, (uint32_t)pl);
+            own_pl = slot_has(om, tb) ? slot_idx(om, tb, a.E, 0) : -1;
+        }
         uint64_t pk0 = 0, pk1 = 0;                          // msk: the push slots by sub-ring index
         if (msk) {
             for (int q = lane; q < nact; q += 64) {
@@ -2285,8 +2291,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 const uint64_t hmw = bs < 0 ? 0ull : (uint64_t)__shfl((long long)hm, sl, 64);
                 const uint64_t hmw1 = bs < 0 ? 0ull : (uint64_t)__shfl((long long)hm1, sl, 64);
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
-                const uint64_t me_m = smask_of(a.smask, me_id);
-                const int64_t me_pl = slot_has(me_m, t) ? slot_idx(me_m, t, a.E, 0) : -1;
+                const int64_t me_pl = (int64_t)__shfl((long long)own_pl, sl, 64);
                 n_walk += (gl == 0 && bs >= 0);
                 IH_D(d_pw += (gl == 0 && bs >= 0);)
                 const uint32_t deg = bs >= 0 ? end - beg : 0u;
@@ -2301,8 +2306,7 @@ __global__ __launch_bounds__(256, MM ? GSIM_IH_WPE : 1) void k_ihave(IhArgs a_, 
                 const uint64_t hmw = (uint64_t)__shfl((long long)hm, bs, 64);
                 const uint64_t hmw1 = (uint64_t)__shfl((long long)hm1, bs, 64);
                 const uint32_t me_g = a.gid ? a.gid[me_id] : me_id;
-                const uint64_t me_m = smask_of(a.smask, me_id);
-                const int64_t me_pl = slot_has(me_m, t) ? slot_idx(me_m, t, a.E, 0) : -1;
+                const int64_t me_pl = (int64_t)__shfl((long long)own_pl, bs, 64);
                 n_walk += (lane == 0 && slice == 0);
                 IH_D(d_pw += (lane == 0 && slice == 0);)
                 for (uint32_t off = slice * 64; off < end - beg; off += 64 * nsl)
